@@ -1,0 +1,490 @@
+// CPU reference backend of the H.264 stripe encoder. It is (1) the `use_cpu`
+// execution path of the pixelflux-compatible capture module and (2) the golden
+// model for the HIP pipeline: every stage below has a kernel counterpart in
+// csrc/kernels/h264_kernels.hip that must produce bit-identical buffers.
+#include "h264_frame.h"
+#include "color.h"
+#include <string.h>
+#include <algorithm>
+
+namespace sk {
+namespace h264 {
+
+CpuH264Encoder::CpuH264Encoder(const EncoderConfig& c) : cfg(c) {
+    g.init(cfg);
+    ctl_.init(cfg, g);
+    size_t ny = (size_t)g.stride_y * g.plane_h_y, nc = (size_t)g.stride_c * g.plane_h_c;
+    for (int p = 0; p < 3; p++) {
+        size_t n = p ? nc : ny;
+        src[p].assign(n, 0);
+        prev[p].assign(n, 0);
+        ref[p].assign(n, 0);
+        rec[p].assign(n, 0);
+    }
+    mb_dirty.assign(g.num_mbs(), 1);
+    stripe_dirty.assign(g.num_slices, 1);
+    mbs.assign(g.num_mbs(), MbInfo());
+    coefs.assign((size_t)g.num_mbs() * kCoefPerMb, 0);
+    me.assign(g.num_mbs(), MeResult());
+    mvfield.assign((size_t)g.num_mbs() * 2, 0);
+    tasks.assign(g.num_slices, SliceTask());
+    if (cfg.fullframe) {
+        param_sets.resize(1);
+        build_parameter_sets(g.W, g.H, cfg.full_range, cfg.fps, param_sets[0]);
+    } else {
+        param_sets.resize(g.num_slices);
+        for (int s = 0; s < g.num_slices; s++)
+            build_parameter_sets(g.W, g.slice_pix_h(s), cfg.full_range, cfg.fps, param_sets[s]);
+    }
+}
+
+void CpuH264Encoder::load_frame(const uint8_t* bgrx, int stride) {
+    const int W = g.W, H = g.H;
+    for (int qy = 0; qy < g.plane_h_c; qy++) {
+        int y0 = std::min(2 * qy, H - 1), y1 = std::min(2 * qy + 1, H - 1);
+        const uint8_t* r0 = bgrx + (size_t)y0 * stride;
+        const uint8_t* r1 = bgrx + (size_t)y1 * stride;
+        for (int qx = 0; qx < g.stride_c; qx++) {
+            int x0 = std::min(2 * qx, W - 1), x1 = std::min(2 * qx + 1, W - 1);
+            uint8_t y[4], cb, cr;
+            bgrx_quad_to_yuv(r0 + 4 * x0, r0 + 4 * x1, r1 + 4 * x0, r1 + 4 * x1, cfg.full_range, y,
+                             &cb, &cr);
+            size_t oy = (size_t)(2 * qy) * g.stride_y + 2 * qx;
+            src[0][oy] = y[0];
+            src[0][oy + 1] = y[1];
+            src[0][oy + g.stride_y] = y[2];
+            src[0][oy + g.stride_y + 1] = y[3];
+            src[1][(size_t)qy * g.stride_c + qx] = cb;
+            src[2][(size_t)qy * g.stride_c + qx] = cr;
+        }
+    }
+    std::fill(stripe_dirty.begin(), stripe_dirty.end(), 0);
+    for (int mby = 0; mby < g.mb_h; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            bool d = first_frame;
+            for (int y = 0; y < 16 && !d; y++) {
+                size_t o = (size_t)(mby * 16 + y) * g.stride_y + mbx * 16;
+                d = memcmp(&src[0][o], &prev[0][o], 16) != 0;
+            }
+            for (int p = 1; p < 3 && !d; p++)
+                for (int y = 0; y < 8 && !d; y++) {
+                    size_t o = (size_t)(mby * 8 + y) * g.stride_c + mbx * 8;
+                    d = memcmp(&src[p][o], &prev[p][o], 8) != 0;
+                }
+            mb_dirty[mby * g.mb_w + mbx] = d;
+            if (d) stripe_dirty[mby / g.rows_per_slice] = 1;
+        }
+}
+
+int CpuH264Encoder::sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t) const {
+    int y_lo = t.pic_row0 * 16, y_hi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    int x_hi = g.stride_y - 1;
+    int sad = 0;
+    for (int y = 0; y < 16; y++) {
+        int sy = sk_clip(mby * 16 + y + dy, y_lo, y_hi);
+        const uint8_t* s = &src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16];
+        const uint8_t* r = &ref[0][(size_t)sy * g.stride_y];
+        for (int x = 0; x < 16; x++) {
+            int sx = sk_clip(mbx * 16 + x + dx, 0, x_hi);
+            sad += sk_abs((int)s[x] - (int)r[sx]);
+        }
+    }
+    return sad;
+}
+
+void CpuH264Encoder::motion_search(int s) {
+    const SliceTask& t = tasks[s];
+    const int lam = lambda_for_qp(t.qp);
+    const int R = cfg.me_range;
+    auto cost_of = [&](int mbx, int mby, int dx, int dy, int* sad_out) {
+        int sad = sad_at(mbx, mby, dx, dy, t);
+        *sad_out = sad;
+        return sad + lam * (sk_se_bits(4 * dx) + sk_se_bits(4 * dy));
+    };
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            int idx = mby * g.mb_w + mbx;
+            int cx[6], cy[6], n = 0;
+            cx[n] = 0; cy[n] = 0; n++;
+            auto add = [&](int ox, int oy) {
+                int j = oy * g.mb_w + ox;
+                cx[n] = sk_clip(mvfield[2 * j], -R, R);
+                cy[n] = sk_clip(mvfield[2 * j + 1], -R, R);
+                n++;
+            };
+            add(mbx, mby);
+            if (mbx > 0) add(mbx - 1, mby);
+            if (mbx + 1 < g.mb_w) add(mbx + 1, mby);
+            if (mby - 1 >= t.pic_row0) add(mbx, mby - 1);
+            if (mby + 1 < t.pic_row0 + t.pic_rows) add(mbx, mby + 1);
+            int bx = 0, by = 0, bsad = 0;
+            int bcost = cost_of(mbx, mby, 0, 0, &bsad);
+            for (int i = 1; i < n; i++) {
+                int sd;
+                int c = cost_of(mbx, mby, cx[i], cy[i], &sd);
+                if (c < bcost) { bcost = c; bx = cx[i]; by = cy[i]; bsad = sd; }
+            }
+            const int ddx[4] = {0, -1, 1, 0}, ddy[4] = {-1, 0, 0, 1};
+            for (int it = 0; it < cfg.me_iters; it++) {
+                int nb = -1, ncost = bcost, nsad = 0;
+                for (int k = 0; k < 4; k++) {
+                    int x = bx + ddx[k], y = by + ddy[k];
+                    if (x < -R || x > R || y < -R || y > R) continue;
+                    int sd;
+                    int c = cost_of(mbx, mby, x, y, &sd);
+                    if (c < ncost) { ncost = c; nb = k; nsad = sd; }
+                }
+                if (nb < 0) break;
+                bx += ddx[nb]; by += ddy[nb]; bcost = ncost; bsad = nsad;
+            }
+            int sum = 0;
+            for (int y = 0; y < 16; y++)
+                for (int x = 0; x < 16; x++) sum += src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x];
+            int mean = (sum + 128) >> 8, dev = 0;
+            for (int y = 0; y < 16; y++)
+                for (int x = 0; x < 16; x++)
+                    dev += sk_abs((int)src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x] - mean);
+            me[idx].mvx = (int16_t)bx;
+            me[idx].mvy = (int16_t)by;
+            me[idx].sad = bsad;
+            me[idx].intra_est = dev;
+        }
+}
+
+void CpuH264Encoder::decide_scenecut(int s) {
+    SliceTask& t = tasks[s];
+    t.final_action = t.action;
+    if (t.action != ACT_P || !t.allow_scenecut) return;
+    long long inter = 0, intra = 0;
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            inter += me[mby * g.mb_w + mbx].sad;
+            intra += me[mby * g.mb_w + mbx].intra_est;
+        }
+    if (inter > intra) t.final_action = ACT_I;
+}
+
+void CpuH264Encoder::mc_luma(int mbx, int mby, int mvx, int mvy, const SliceTask& t,
+                             uint8_t* pred) const {
+    int y_lo = t.pic_row0 * 16, y_hi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    int dx = mvx >> 2, dy = mvy >> 2;  // integer-pel vectors only
+    for (int y = 0; y < 16; y++) {
+        int sy = sk_clip(mby * 16 + y + dy, y_lo, y_hi);
+        for (int x = 0; x < 16; x++) {
+            int sx = sk_clip(mbx * 16 + x + dx, 0, g.stride_y - 1);
+            pred[y * 16 + x] = ref[0][(size_t)sy * g.stride_y + sx];
+        }
+    }
+}
+
+void CpuH264Encoder::mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTask& t,
+                               uint8_t* pu, uint8_t* pv) const {
+    int h = t.pic_rows * 8;
+    int y0 = t.pic_row0 * 8;
+    for (int c = 0; c < 2; c++) {
+        const uint8_t* base = &ref[1 + c][(size_t)y0 * g.stride_c];
+        uint8_t* o = c ? pv : pu;
+        for (int y = 0; y < 8; y++)
+            for (int x = 0; x < 8; x++)
+                o[y * 8 + x] = (uint8_t)chroma_mc_sample(base, g.stride_c, g.stride_c, h, mbx * 8 + x,
+                                                         mby * 8 - y0 + y, mvx, mvy);
+    }
+}
+
+void CpuH264Encoder::code_slice_inter(int s) {
+    const SliceTask& t = tasks[s];
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            int idx = mby * g.mb_w + mbx;
+            MbInfo& mb = mbs[idx];
+            memset(&mb, 0, sizeof(mb));
+            int mvx = 4 * me[idx].mvx, mvy = 4 * me[idx].mvy;
+            auto nbr = [&](int ox, int oy, bool ok) {
+                MvNb n;
+                n.avail = ok;
+                n.inter = ok;
+                n.mvx = ok ? 4 * me[oy * g.mb_w + ox].mvx : 0;
+                n.mvy = ok ? 4 * me[oy * g.mb_w + ox].mvy : 0;
+                return n;
+            };
+            bool top = mby > t.first_row;
+            MvNb A = nbr(mbx - 1, mby, mbx > 0);
+            MvNb B = nbr(mbx, mby - 1, top);
+            MvNb C = nbr(mbx + 1, mby - 1, top && mbx + 1 < g.mb_w);
+            if (!C.avail) C = nbr(mbx - 1, mby - 1, top && mbx > 0);
+            int pmx, pmy, smx, smy;
+            mv_pred16x16(A, B, C, &pmx, &pmy);
+            mv_pskip(A, B, C, &smx, &smy);
+
+            uint8_t sy[256], su[64], sv[64], py[256], pu[64], pv[64];
+            for (int y = 0; y < 16; y++)
+                memcpy(sy + y * 16, &src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16], 16);
+            for (int y = 0; y < 8; y++) {
+                memcpy(su + y * 8, &src[1][(size_t)(mby * 8 + y) * g.stride_c + mbx * 8], 8);
+                memcpy(sv + y * 8, &src[2][(size_t)(mby * 8 + y) * g.stride_c + mbx * 8], 8);
+            }
+            mc_luma(mbx, mby, mvx, mvy, t, py);
+            mc_chroma(mbx, mby, mvx, mvy, t, pu, pv);
+            MbTransform tr;
+            residual_transform(sy, py, su, pu, sv, pv, tr);
+            int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
+            mb.type = MB_P_16x16;
+            int qp = quant_mb_with_budget(tr, t.qp, false, mb, coef);
+            mb.mvx = (int16_t)mvx;
+            mb.mvy = (int16_t)mvy;
+            if (mb.cbp == 0 && mvx == smx && mvy == smy) {
+                mb.type = MB_P_SKIP;
+            } else {
+                mb.mvdx = (int16_t)(mvx - pmx);
+                mb.mvdy = (int16_t)(mvy - pmy);
+            }
+            uint8_t ry[256], ru[64], rv[64];
+            recon_luma(coef, qp, false, mb.cbp & 15, py, ry);
+            recon_chroma(coef, qp, (mb.cbp >> 4) & 3, pu, pv, ru, rv);
+            for (int y = 0; y < 16; y++)
+                memcpy(&rec[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16], ry + y * 16, 16);
+            for (int y = 0; y < 8; y++) {
+                memcpy(&rec[1][(size_t)(mby * 8 + y) * g.stride_c + mbx * 8], ru + y * 8, 8);
+                memcpy(&rec[2][(size_t)(mby * 8 + y) * g.stride_c + mbx * 8], rv + y * 8, 8);
+            }
+        }
+}
+
+void CpuH264Encoder::code_slice_intra(int s) {
+    const SliceTask& t = tasks[s];
+    const int sy_ = g.stride_y, sc = g.stride_c;
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            int idx = mby * g.mb_w + mbx;
+            MbInfo& mb = mbs[idx];
+            memset(&mb, 0, sizeof(mb));
+            me[idx].mvx = me[idx].mvy = 0;
+            bool aT = mby > t.first_row, aL = mbx > 0;
+            uint8_t top[16] = {0}, left[16] = {0}, ctop[2][8] = {{0}}, cleft[2][8] = {{0}};
+            int tl = 0, ctl[2] = {0, 0};
+            if (aT)
+                for (int i = 0; i < 16; i++) top[i] = rec[0][(size_t)(mby * 16 - 1) * sy_ + mbx * 16 + i];
+            if (aL)
+                for (int i = 0; i < 16; i++) left[i] = rec[0][(size_t)(mby * 16 + i) * sy_ + mbx * 16 - 1];
+            if (aT && aL) tl = rec[0][(size_t)(mby * 16 - 1) * sy_ + mbx * 16 - 1];
+            for (int c = 0; c < 2; c++) {
+                const std::vector<uint8_t>& P = rec[1 + c];
+                if (aT)
+                    for (int i = 0; i < 8; i++) ctop[c][i] = P[(size_t)(mby * 8 - 1) * sc + mbx * 8 + i];
+                if (aL)
+                    for (int i = 0; i < 8; i++) cleft[c][i] = P[(size_t)(mby * 8 + i) * sc + mbx * 8 - 1];
+                if (aT && aL) ctl[c] = P[(size_t)(mby * 8 - 1) * sc + mbx * 8 - 1];
+            }
+            uint8_t sy[256], su[64], sv[64];
+            for (int y = 0; y < 16; y++)
+                memcpy(sy + y * 16, &src[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16], 16);
+            for (int y = 0; y < 8; y++) {
+                memcpy(su + y * 8, &src[1][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
+                memcpy(sv + y * 8, &src[2][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
+            }
+            // luma mode decision (SAD), evaluation order DC, V, H, Plane
+            int dc = i16_dc(top, left, aT, aL);
+            int pa = 0, pb = 0, pc = 0;
+            if (aT && aL) i16_plane_params(top, left, tl, &pa, &pb, &pc);
+            const int order[4] = {2, 0, 1, 3};
+            int best_mode = 2, best_sad = 0x7fffffff;
+            for (int oi = 0; oi < 4; oi++) {
+                int m = order[oi];
+                if ((m == 0 && !aT) || (m == 1 && !aL) || (m == 3 && !(aT && aL))) continue;
+                int sad = 0;
+                for (int y = 0; y < 16; y++)
+                    for (int x = 0; x < 16; x++)
+                        sad += sk_abs((int)sy[y * 16 + x] -
+                                      i16_pred_pixel(m, x, y, top, left, tl, aT, aL, dc, pa, pb, pc));
+                if (sad < best_sad) { best_sad = sad; best_mode = m; }
+            }
+            uint8_t py[256];
+            for (int y = 0; y < 16; y++)
+                for (int x = 0; x < 16; x++)
+                    py[y * 16 + x] = (uint8_t)i16_pred_pixel(best_mode, x, y, top, left, tl, aT, aL, dc, pa, pb, pc);
+            // chroma mode decision, order DC, H, V, Plane
+            uint8_t pcb[4][2][64];
+            int best_cm = 0, best_csad = 0x7fffffff;
+            for (int m = 0; m < 4; m++) {
+                if ((m == 1 && !aL) || (m == 2 && !aT) || (m == 3 && !(aT && aL))) continue;
+                int sad = 0;
+                for (int c = 0; c < 2; c++) {
+                    int qa = 0, qb = 0, qc = 0;
+                    if (m == 3) chroma_plane_params(ctop[c], cleft[c], ctl[c], &qa, &qb, &qc);
+                    const uint8_t* sp = c ? sv : su;
+                    for (int y = 0; y < 8; y++)
+                        for (int x = 0; x < 8; x++) {
+                            int v;
+                            if (m == 0) v = chroma_dc_block(x >> 2, y >> 2, ctop[c], cleft[c], aT, aL);
+                            else if (m == 1) v = cleft[c][y];
+                            else if (m == 2) v = ctop[c][x];
+                            else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
+                            pcb[m][c][y * 8 + x] = (uint8_t)v;
+                            sad += sk_abs((int)sp[y * 8 + x] - v);
+                        }
+                }
+                if (sad < best_csad) { best_csad = sad; best_cm = m; }
+            }
+            MbTransform tr;
+            residual_transform(sy, py, su, pcb[best_cm][0], sv, pcb[best_cm][1], tr);
+            int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
+            mb.type = MB_I16x16;
+            mb.i16_mode = (uint8_t)best_mode;
+            mb.chroma_mode = (uint8_t)best_cm;
+            int qp = quant_mb_with_budget(tr, t.qp, true, mb, coef);
+            uint8_t ry[256], ru[64], rv[64];
+            recon_luma(coef, qp, true, mb.cbp & 15, py, ry);
+            recon_chroma(coef, qp, (mb.cbp >> 4) & 3, pcb[best_cm][0], pcb[best_cm][1], ru, rv);
+            for (int y = 0; y < 16; y++)
+                memcpy(&rec[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16], ry + y * 16, 16);
+            for (int y = 0; y < 8; y++) {
+                memcpy(&rec[1][(size_t)(mby * 8 + y) * sc + mbx * 8], ru + y * 8, 8);
+                memcpy(&rec[2][(size_t)(mby * 8 + y) * sc + mbx * 8], rv + y * 8, 8);
+            }
+        }
+}
+
+void CpuH264Encoder::code_slice_skipall(int s) {
+    const SliceTask& t = tasks[s];
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            int idx = mby * g.mb_w + mbx;
+            memset(&mbs[idx], 0, sizeof(MbInfo));
+            me[idx].mvx = me[idx].mvy = 0;
+        }
+    int y0 = t.first_row * 16, y1 = (t.first_row + t.num_rows) * 16;
+    memcpy(&rec[0][(size_t)y0 * g.stride_y], &ref[0][(size_t)y0 * g.stride_y], (size_t)(y1 - y0) * g.stride_y);
+    for (int p = 1; p < 3; p++)
+        memcpy(&rec[p][(size_t)(y0 / 2) * g.stride_c], &ref[p][(size_t)(y0 / 2) * g.stride_c],
+               (size_t)(y1 - y0) / 2 * g.stride_c);
+}
+
+void CpuH264Encoder::mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb) const {
+    nb.left = mbx > 0 ? &mbs[mby * g.mb_w + mbx - 1] : nullptr;
+    nb.top = mby > first_row ? &mbs[(mby - 1) * g.mb_w + mbx] : nullptr;
+}
+
+std::vector<uint8_t> CpuH264Encoder::write_slice(int s) {
+    const SliceTask& t = tasks[s];
+    const int nmb = t.num_rows * g.mb_w;
+    std::vector<uint8_t> buf((size_t)nmb * (kMaxMbBits / 8 + 16) + 64, 0);
+    BitWriter w(buf.data());
+    SliceHeaderParams h;
+    bool intra = t.final_action == ACT_I;
+    h.first_mb = cfg.fullframe ? t.first_row * g.mb_w : 0;
+    h.slice_type = intra ? 2 : 0;
+    h.idr = intra && t.idr_on_intra;
+    h.frame_num = h.idr ? 0 : t.frame_num;
+    h.idr_pic_id = t.idr_pic_id;
+    h.slice_qp = t.qp;
+    write_slice_header(w, h);
+    if (t.final_action == ACT_SKIPALL) {
+        put_ue(w, (uint32_t)nmb);
+    } else {
+        int skip_run = 0, qp_prev = t.qp;
+        for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+            for (int mbx = 0; mbx < g.mb_w; mbx++) {
+                int idx = mby * g.mb_w + mbx;
+                const MbInfo& mb = mbs[idx];
+                if (mb.type == MB_P_SKIP) { skip_run++; continue; }
+                if (!intra) { put_ue(w, (uint32_t)skip_run); skip_run = 0; }
+                int dq = 0;
+                if (mb_has_qp_delta(mb)) { dq = mb.qp - qp_prev; qp_prev = mb.qp; }
+                write_mb_header(w, mb, !intra, dq);
+                MbNeighbours nb;
+                mb_neighbours(mbx, mby, t.first_row, nb);
+                write_mb_residual(w, mb, nb, &coefs[(size_t)idx * kCoefPerMb]);
+            }
+        if (skip_run > 0) put_ue(w, (uint32_t)skip_run);
+    }
+    w.put1(1);
+    while (w.pos & 7) w.put1(0);
+    buf.resize(w.pos / 8);
+    return buf;
+}
+
+void CpuH264Encoder::package(uint16_t frame_id, std::vector<std::vector<uint8_t>>& rbsp,
+                             std::vector<EncodedPacket>& out) {
+    if (cfg.fullframe) {
+        bool idr = ctl_.picture_is_idr(tasks.data());
+        EncodedPacket pk;
+        pk.y = 0; pk.w = g.W; pk.h = g.H; pk.key = idr;
+        pk.data.resize(10);
+        write_stripe_header(pk.data.data(), idr, frame_id, 0, g.W, g.H);
+        if (idr) pk.data.insert(pk.data.end(), param_sets[0].begin(), param_sets[0].end());
+        for (int s = 0; s < g.num_slices; s++) {
+            const SliceTask& t = tasks[s];
+            int hdr = (t.final_action == ACT_I && idr) ? 0x65 : 0x41;
+            append_nal(pk.data, hdr, rbsp[s].data(), rbsp[s].size());
+        }
+        out.push_back(std::move(pk));
+        return;
+    }
+    for (int s = 0; s < g.num_slices; s++) {
+        const SliceTask& t = tasks[s];
+        if (t.final_action == ACT_NONE) continue;
+        bool idr = t.final_action == ACT_I;
+        EncodedPacket pk;
+        pk.y = g.slice_pix_y(s); pk.w = g.W; pk.h = g.slice_pix_h(s); pk.key = idr;
+        pk.data.resize(10);
+        write_stripe_header(pk.data.data(), idr, frame_id, pk.y, pk.w, pk.h);
+        if (idr) pk.data.insert(pk.data.end(), param_sets[s].begin(), param_sets[s].end());
+        append_nal(pk.data, idr ? 0x65 : 0x41, rbsp[s].data(), rbsp[s].size());
+        out.push_back(std::move(pk));
+    }
+}
+
+void CpuH264Encoder::finish_frame() {
+    for (int s = 0; s < g.num_slices; s++) {
+        const SliceTask& t = tasks[s];
+        if (t.final_action == ACT_NONE || t.final_action == ACT_SKIPALL) {
+            if (t.final_action == ACT_SKIPALL)
+                for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+                    for (int mbx = 0; mbx < g.mb_w; mbx++) {
+                        int j = mby * g.mb_w + mbx;
+                        mvfield[2 * j] = mvfield[2 * j + 1] = 0;
+                    }
+            continue;
+        }
+        int y0 = t.first_row * 16, y1 = (t.first_row + t.num_rows) * 16;
+        memcpy(&ref[0][(size_t)y0 * g.stride_y], &rec[0][(size_t)y0 * g.stride_y], (size_t)(y1 - y0) * g.stride_y);
+        for (int p = 1; p < 3; p++)
+            memcpy(&ref[p][(size_t)(y0 / 2) * g.stride_c], &rec[p][(size_t)(y0 / 2) * g.stride_c],
+                   (size_t)(y1 - y0) / 2 * g.stride_c);
+        for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+            for (int mbx = 0; mbx < g.mb_w; mbx++) {
+                int j = mby * g.mb_w + mbx;
+                mvfield[2 * j] = me[j].mvx;
+                mvfield[2 * j + 1] = me[j].mvy;
+            }
+    }
+    for (int p = 0; p < 3; p++) prev[p].swap(src[p]);
+    ctl_.commit(tasks.data());
+    first_frame = false;
+}
+
+void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
+                            std::vector<EncodedPacket>& out) {
+    load_frame(bgrx, stride);
+    ctl_.plan(stripe_dirty.data(), tasks.data());
+    for (int s = 0; s < g.num_slices; s++)
+        if (tasks[s].action == ACT_P) {
+            motion_search(s);
+            decide_scenecut(s);
+        }
+    std::vector<std::vector<uint8_t>> rbsp(g.num_slices);
+    for (int s = 0; s < g.num_slices; s++) {
+        switch (tasks[s].final_action) {
+            case ACT_P: code_slice_inter(s); break;
+            case ACT_I: code_slice_intra(s); break;
+            case ACT_SKIPALL: code_slice_skipall(s); break;
+            default: continue;
+        }
+        rbsp[s] = write_slice(s);
+    }
+    package(frame_id, rbsp, out);
+    finish_frame();
+}
+
+}  // namespace h264
+}  // namespace sk

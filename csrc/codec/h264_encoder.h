@@ -1,0 +1,135 @@
+// Session-level H.264 encoder interface: configuration, geometry, per-stripe
+// control state (damage / paint-over / keyframe decisions) and the frame plan
+// handed to an execution backend (CPU reference or the HIP pipeline).
+//
+// Stripe semantics mirror the pixelflux contract used by the reference server
+// (selkies.py:2919-2964 CaptureSettings; client demux selkies-core.js:2925-3032):
+//  * striped mode: every stripe is an independent H.264 stream (own SPS/PPS,
+//    own IDR) emitted as a 0x04 packet [type|key|frame_id|y|w|h] + Annex-B;
+//    undamaged stripes emit nothing.
+//  * full-frame mode (encoder "x264enc"): one picture whose slices are the
+//    stripes, emitted as a single 0x04 packet with y = 0.
+#pragma once
+#include <stdint.h>
+#include <vector>
+#include <string>
+#include "h264_core.h"
+
+namespace sk {
+namespace h264 {
+
+struct EncoderConfig {
+    int width = 1920;
+    int height = 1080;
+    int stripe_height = 64;      // pixels, multiple of 16
+    int fullframe = 0;
+    int full_range = 0;          // h264_fullcolor
+    int qp = 25;                 // h264_crf mapped to a constant QP
+    int paint_qp = 18;           // h264_paintover_crf
+    int use_paint_over = 1;
+    int paint_over_trigger = 15;
+    int paint_over_burst = 5;
+    int streaming_mode = 0;
+    int damage_threshold = 10;
+    int damage_duration = 20;
+    int me_range = 64;           // max |mv| in integer pixels
+    int me_iters = 24;           // diamond refinement iterations
+    int scenecut = 1;
+    float fps = 60.f;
+};
+
+struct Geometry {
+    int W = 0, H = 0, mb_w = 0, mb_h = 0, rows_per_slice = 0, num_slices = 0;
+    int stride_y = 0, stride_c = 0, plane_h_y = 0, plane_h_c = 0;
+    int fullframe = 0, stripe_height = 0;
+    void init(const EncoderConfig& c) {
+        W = c.width;
+        H = c.height;
+        fullframe = c.fullframe;
+        stripe_height = c.stripe_height;
+        mb_w = (W + 15) / 16;
+        mb_h = (H + 15) / 16;
+        rows_per_slice = c.stripe_height / 16;
+        if (rows_per_slice < 1) rows_per_slice = 1;
+        num_slices = (mb_h + rows_per_slice - 1) / rows_per_slice;
+        stride_y = mb_w * 16;
+        stride_c = mb_w * 8;
+        plane_h_y = mb_h * 16;
+        plane_h_c = mb_h * 8;
+    }
+    int slice_first_row(int s) const { return s * rows_per_slice; }
+    int slice_rows(int s) const {
+        int r = mb_h - s * rows_per_slice;
+        return r < rows_per_slice ? r : rows_per_slice;
+    }
+    int slice_pix_y(int s) const { return s * rows_per_slice * 16; }
+    int slice_pix_h(int s) const {
+        int y0 = slice_pix_y(s);
+        int y1 = y0 + slice_rows(s) * 16;
+        if (y1 > H) y1 = H;
+        return y1 - y0;
+    }
+    int num_mbs() const { return mb_w * mb_h; }
+};
+
+// Per-slice work item for one frame (POD, copied to device memory as is).
+enum SliceAction : int32_t { ACT_NONE = 0, ACT_P = 1, ACT_I = 2, ACT_SKIPALL = 3 };
+struct SliceTask {
+    int32_t action;        // SliceAction requested by the controller
+    int32_t qp;
+    int32_t first_row;     // MB rows of the slice
+    int32_t num_rows;
+    int32_t pic_row0;      // first MB row of the picture this slice belongs to
+    int32_t pic_rows;      // MB rows of that picture (MC clamp bounds)
+    int32_t frame_num;     // frame_num if coded as P (or non-IDR I)
+    int32_t idr_pic_id;    // idr_pic_id if coded as IDR
+    int32_t allow_scenecut;
+    int32_t idr_on_intra;  // striped mode: an I decision makes the stripe an IDR
+    int32_t final_action;  // written by the backend (scene-cut may turn P into I)
+    int32_t pad;
+};
+static_assert(sizeof(SliceTask) == 48, "SliceTask layout");
+
+struct StripeState {
+    int frame_num = 0;     // next frame_num
+    int idr_pic_id = 0;
+    bool need_idr = true;
+    int static_frames = 0;
+    int dirty_streak = 0;
+    int hot_left = 0;
+    int paint_left = 0;
+    bool painted = true;   // nothing to paint before the first change
+};
+
+// Decides, per stripe, what to encode this frame.
+class Controller {
+   public:
+    void init(const EncoderConfig& cfg, const Geometry& g);
+    void request_keyframe();
+    // dirty[s] = stripe s changed since last frame. Fills tasks[num_slices].
+    void plan(const uint8_t* dirty, SliceTask* tasks);
+    // After the backend ran: update frame_num / idr state from final actions.
+    void commit(const SliceTask* tasks);
+    bool picture_is_idr(const SliceTask* tasks) const;
+    const std::vector<StripeState>& stripes() const { return st_; }
+
+   private:
+    EncoderConfig cfg_;
+    Geometry g_;
+    std::vector<StripeState> st_;
+    StripeState pic_;  // full-frame mode picture state
+};
+
+// ---- bitstream packaging (host) -------------------------------------------
+int choose_level_idc(int mb_w, int mb_h, float fps);
+// SPS + PPS NAL units (Annex-B, with start codes) for a picture of w x h pixels.
+void build_parameter_sets(int width, int height, int full_range, float fps,
+                          std::vector<uint8_t>& out);
+// Appends start code + NAL header + EP-escaped payload.
+void append_nal(std::vector<uint8_t>& out, int nal_header_byte, const uint8_t* rbsp, size_t n);
+size_t emulation_prevent(const uint8_t* in, size_t n, uint8_t* out);
+// 10-byte 0x04 stripe header (selkies-core.js:2925-2938)
+void write_stripe_header(uint8_t* p, int key, uint16_t frame_id, int y, int w, int h);
+
+}  // namespace h264
+}  // namespace sk

@@ -1,0 +1,67 @@
+// Frame-level state shared by the CPU reference backend and the HIP backend:
+// plane geometry, per-MB buffers and the stage functions of the CPU path.
+#pragma once
+#include <vector>
+#include <stdint.h>
+#include "h264_encoder.h"
+#include "h264_mb.h"
+
+namespace sk {
+namespace h264 {
+
+// Output of one encoded frame: packets already carry the 10-byte 0x04 header.
+struct EncodedPacket {
+    int y = 0, w = 0, h = 0, key = 0;
+    std::vector<uint8_t> data;
+};
+
+// Motion-search result per macroblock (SAD only: ME cost = SAD + lambda*mvbits).
+struct MeResult {
+    int16_t mvx, mvy;        // integer-pel motion vector
+    int32_t sad;             // SAD of the chosen vector
+    int32_t intra_est;       // sum |Y - mean| of the source MB (scene-cut estimate)
+};
+
+class CpuH264Encoder {
+   public:
+    explicit CpuH264Encoder(const EncoderConfig& cfg);
+    void request_keyframe() { ctl_.request_keyframe(); }
+    // Full pipeline for one captured frame.
+    void encode(const uint8_t* bgrx, int stride_bytes, uint16_t frame_id,
+                std::vector<EncodedPacket>& out);
+
+    // ---- stages (public for tests) ----
+    void load_frame(const uint8_t* bgrx, int stride_bytes);  // K1 + K3
+    void motion_search(int s);                              // K4 for slice s
+    void decide_scenecut(int s);
+    void code_slice_inter(int s);
+    void code_slice_intra(int s);
+    void code_slice_skipall(int s);
+    std::vector<uint8_t> write_slice(int s);                 // entropy + header -> RBSP
+    void package(uint16_t frame_id, std::vector<std::vector<uint8_t>>& rbsp,
+                 std::vector<EncodedPacket>& out);
+    void finish_frame();
+
+    EncoderConfig cfg;
+    Geometry g;
+    Controller ctl_;
+    std::vector<uint8_t> src[3], prev[3], ref[3], rec[3];
+    std::vector<uint8_t> mb_dirty, stripe_dirty;
+    std::vector<MbInfo> mbs;
+    std::vector<int16_t> coefs;
+    std::vector<MeResult> me;
+    std::vector<int16_t> mvfield;  // previous integer mv per MB (x, y)
+    std::vector<SliceTask> tasks;
+    std::vector<std::vector<uint8_t>> param_sets;  // per stripe (striped) or [0] (full frame)
+    bool first_frame = true;
+
+   private:
+    void mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb) const;
+    void mc_luma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pred) const;
+    void mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pu,
+                   uint8_t* pv) const;
+    int sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t) const;
+};
+
+}  // namespace h264
+}  // namespace sk

@@ -1,0 +1,228 @@
+// Macroblock-level residual coding (transform, quant, decimation, QP
+// escalation, reconstruction) shared by the CPU reference and, block by block,
+// mirrored by the GPU kernels (see csrc/kernels/h264_kernels.hip).
+#pragma once
+#include "h264_syntax.h"
+
+namespace sk {
+namespace h264 {
+
+// Forward-transformed residual of one macroblock, kept so that QP escalation can
+// requantise without recomputing prediction/transform.
+struct MbTransform {
+    int wl[16][16];      // luma, blkIdx order, raster coefficients
+    int wc[2][4][16];    // chroma [comp][blk]
+};
+
+SK_HD void residual_transform(const uint8_t* src_y, const uint8_t* pred_y, const uint8_t* src_u,
+                              const uint8_t* pred_u, const uint8_t* src_v, const uint8_t* pred_v,
+                              MbTransform& t) {
+    for (int blk = 0; blk < 16; blk++) {
+        int x0 = H264_BLK_X[blk] * 4, y0 = H264_BLK_Y[blk] * 4;
+        int r[16];
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++)
+                r[y * 4 + x] = (int)src_y[(y0 + y) * 16 + x0 + x] - (int)pred_y[(y0 + y) * 16 + x0 + x];
+        fdct4x4(r, t.wl[blk]);
+    }
+    for (int c = 0; c < 2; c++) {
+        const uint8_t* s = c ? src_v : src_u;
+        const uint8_t* p = c ? pred_v : pred_u;
+        for (int b = 0; b < 4; b++) {
+            int x0 = (b & 1) * 4, y0 = (b >> 1) * 4;
+            int r[16];
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++)
+                    r[y * 4 + x] = (int)s[(y0 + y) * 8 + x0 + x] - (int)p[(y0 + y) * 8 + x0 + x];
+            fdct4x4(r, t.wc[c][b]);
+        }
+    }
+}
+
+SK_HD int i16_dc_fwd_round(int v) { return v >= 0 ? (v + 1) >> 1 : -((-v + 1) >> 1); }
+
+// Quantise luma. intra16: Intra16x16 (DC separated), else inter 4x4 with decimation.
+// Fills coef (kCoefLuma.., kCoefLumaDC..) and returns cbp luma bits (0..15).
+SK_HD int quant_luma(const MbTransform& t, int qp, bool intra16, int16_t* coef, uint8_t* nnz) {
+    int qbits = 15 + qp / 6;
+    int f = quant_f(qbits, intra16);
+    const int* mf = H264_QUANT_MF[qp % 6];
+    if (intra16) {
+        int dc[16], hd[16];
+        for (int blk = 0; blk < 16; blk++) dc[H264_BLK_Y[blk] * 4 + H264_BLK_X[blk]] = t.wl[blk][0];
+        hadamard4x4(dc, hd);
+        for (int k = 0; k < 16; k++)
+            coef[kCoefLumaDC + k] =
+                (int16_t)quant_coef(i16_dc_fwd_round(hd[H264_ZIGZAG4x4[k]]), mf[0], 2 * f, qbits + 1);
+        bool any = false;
+        for (int blk = 0; blk < 16; blk++) {
+            int16_t* c = coef + kCoefLuma + blk * 16;
+            c[0] = 0;
+            for (int k = 1; k < 16; k++) {
+                int pos = H264_ZIGZAG4x4[k];
+                c[k] = (int16_t)quant_coef(t.wl[blk][pos], mf[H264_POS_CLASS[pos]], f, qbits);
+                any |= c[k] != 0;
+            }
+        }
+        for (int blk = 0; blk < 16; blk++)
+            nnz[blk] = any ? (uint8_t)count_nonzero(coef + kCoefLuma + blk * 16 + 1, 15) : 0;
+        return any ? 15 : 0;
+    }
+    int cbp = 0;
+    int mb_score = 0;
+    for (int b8 = 0; b8 < 4; b8++) {
+        int score8 = 0;
+        for (int i = 0; i < 4; i++) {
+            int blk = b8 * 4 + i;
+            int16_t* c = coef + kCoefLuma + blk * 16;
+            for (int k = 0; k < 16; k++) {
+                int pos = H264_ZIGZAG4x4[k];
+                c[k] = (int16_t)quant_coef(t.wl[blk][pos], mf[H264_POS_CLASS[pos]], f, qbits);
+            }
+            score8 += decimate_score(c, 16);
+        }
+        mb_score += score8;
+        if (score8 >= 4) cbp |= 1 << b8;
+    }
+    if (mb_score < 6) cbp = 0;
+    for (int blk = 0; blk < 16; blk++) {
+        int16_t* c = coef + kCoefLuma + blk * 16;
+        if (!(cbp & (1 << (blk >> 2)))) {
+            for (int k = 0; k < 16; k++) c[k] = 0;
+            nnz[blk] = 0;
+        } else {
+            nnz[blk] = (uint8_t)count_nonzero(c, 16);
+        }
+    }
+    // an 8x8 whose four blocks quantised to zero is not coded
+    for (int b8 = 0; b8 < 4; b8++) {
+        if (!(cbp & (1 << b8))) continue;
+        int n = nnz[b8 * 4] + nnz[b8 * 4 + 1] + nnz[b8 * 4 + 2] + nnz[b8 * 4 + 3];
+        if (n == 0) cbp &= ~(1 << b8);
+    }
+    return cbp;
+}
+
+// Quantise chroma; returns cbp chroma (0, 1, 2).
+SK_HD int quant_chroma(const MbTransform& t, int qp, bool intra, int16_t* coef, uint8_t* nnz) {
+    int qpc = chroma_qp(qp);
+    int qbits = 15 + qpc / 6;
+    int f = quant_f(qbits, intra);
+    const int* mf = H264_QUANT_MF[qpc % 6];
+    bool any_dc = false, any_ac = false;
+    for (int c = 0; c < 2; c++) {
+        int d0 = t.wc[c][0][0], d1 = t.wc[c][1][0], d2 = t.wc[c][2][0], d3 = t.wc[c][3][0];
+        int f2[4] = {d0 + d1 + d2 + d3, d0 - d1 + d2 - d3, d0 + d1 - d2 - d3, d0 - d1 - d2 + d3};
+        for (int i = 0; i < 4; i++) {
+            int l = quant_coef(f2[i], mf[0], 2 * f, qbits + 1);
+            coef[kCoefChromaDC + c * 4 + i] = (int16_t)l;
+            any_dc |= l != 0;
+        }
+        int score = 0;
+        bool comp_ac = false;
+        for (int b = 0; b < 4; b++) {
+            int16_t* cc = coef + kCoefChromaAC + (c * 4 + b) * 16;
+            cc[0] = 0;
+            for (int k = 1; k < 16; k++) {
+                int pos = H264_ZIGZAG4x4[k];
+                cc[k] = (int16_t)quant_coef(t.wc[c][b][pos], mf[H264_POS_CLASS[pos]], f, qbits);
+                comp_ac |= cc[k] != 0;
+            }
+            if (!intra) score += decimate_score(cc + 1, 15);
+        }
+        if (!intra && comp_ac && score < 7) {
+            for (int b = 0; b < 4; b++)
+                for (int k = 0; k < 16; k++) coef[kCoefChromaAC + (c * 4 + b) * 16 + k] = 0;
+            comp_ac = false;
+        }
+        any_ac |= comp_ac;
+    }
+    int cbp_c = any_ac ? 2 : (any_dc ? 1 : 0);
+    for (int b = 0; b < 8; b++)
+        nnz[16 + b] = cbp_c == 2 ? (uint8_t)count_nonzero(coef + kCoefChromaAC + b * 16 + 1, 15) : 0;
+    return cbp_c;
+}
+
+// Reconstruct the luma of a macroblock (16x16 raster) from its levels.
+SK_HD void recon_luma(const int16_t* coef, int qp, bool intra16, int cbp_l, const uint8_t* pred,
+                      uint8_t* rec) {
+    int dcy[16];
+    if (intra16) {
+        int c[16];
+        for (int k = 0; k < 16; k++) c[H264_ZIGZAG4x4[k]] = coef[kCoefLumaDC + k];
+        i16_dc_dequant(c, dcy, qp);
+    }
+    for (int blk = 0; blk < 16; blk++) {
+        int bx = H264_BLK_X[blk], by = H264_BLK_Y[blk];
+        int d[16];
+        for (int i = 0; i < 16; i++) d[i] = 0;
+        const int16_t* c = coef + kCoefLuma + blk * 16;
+        bool coded = intra16 ? (cbp_l != 0) : ((cbp_l >> (blk >> 2)) & 1);
+        if (coded)
+            for (int k = intra16 ? 1 : 0; k < 16; k++) {
+                int pos = H264_ZIGZAG4x4[k];
+                d[pos] = dequant_coef(c[k], qp, pos);
+            }
+        if (intra16) d[0] = dcy[by * 4 + bx];
+        int r[16];
+        idct4x4(d, r);
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++) {
+                int o = (by * 4 + y) * 16 + bx * 4 + x;
+                rec[o] = (uint8_t)sk_clip255(pred[o] + r[y * 4 + x]);
+            }
+    }
+}
+
+SK_HD void recon_chroma(const int16_t* coef, int qp, int cbp_c, const uint8_t* pred_u,
+                        const uint8_t* pred_v, uint8_t* rec_u, uint8_t* rec_v) {
+    int qpc = chroma_qp(qp);
+    for (int c = 0; c < 2; c++) {
+        int lv[4], dcc[4];
+        for (int i = 0; i < 4; i++) lv[i] = cbp_c ? coef[kCoefChromaDC + c * 4 + i] : 0;
+        chroma_dc_dequant(lv, dcc, qpc);
+        const uint8_t* p = c ? pred_v : pred_u;
+        uint8_t* o = c ? rec_v : rec_u;
+        for (int b = 0; b < 4; b++) {
+            int d[16];
+            for (int i = 0; i < 16; i++) d[i] = 0;
+            if (cbp_c == 2) {
+                const int16_t* cc = coef + kCoefChromaAC + (c * 4 + b) * 16;
+                for (int k = 1; k < 16; k++) {
+                    int pos = H264_ZIGZAG4x4[k];
+                    d[pos] = dequant_coef(cc[k], qpc, pos);
+                }
+            }
+            d[0] = dcc[b];
+            int r[16];
+            idct4x4(d, r);
+            int x0 = (b & 1) * 4, y0 = (b >> 1) * 4;
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++) {
+                    int idx = (y0 + y) * 8 + x0 + x;
+                    o[idx] = (uint8_t)sk_clip255(p[idx] + r[y * 4 + x]);
+                }
+        }
+    }
+}
+
+// Quantise with QP escalation so a macroblock never exceeds the A.3.1 bit limit.
+// Returns the final QP; fills mb.cbp / nnz and coef.
+SK_HD int quant_mb_with_budget(const MbTransform& t, int slice_qp, bool intra16, MbInfo& mb,
+                               int16_t* coef) {
+    int qp = slice_qp;
+    int qp_cap = sk_min(51, slice_qp + 24);
+    for (;;) {
+        int cbp_l = quant_luma(t, qp, intra16, coef, mb.nnz);
+        int cbp_c = quant_chroma(t, qp, intra16, coef, mb.nnz);
+        mb.cbp = (uint8_t)(cbp_l | (cbp_c << 4));
+        mb.qp = (uint8_t)qp;
+        if (qp + 6 > qp_cap) break;
+        if (mb_bits_bound(mb, coef) <= kMbBitBudget) break;
+        qp += 6;
+    }
+    return qp;
+}
+
+}  // namespace h264
+}  // namespace sk

@@ -1,0 +1,153 @@
+// H.264 syntax writers (7.3): macroblock_layer for CAVLC Constrained Baseline,
+// slice header, neighbour-dependent nC derivation. SK_HD so the GPU entropy
+// kernel and the CPU reference share one definition of the bitstream.
+#pragma once
+#include "h264_core.h"
+
+namespace sk {
+namespace h264 {
+
+constexpr int kLog2MaxFrameNum = 16;
+
+struct SliceHeaderParams {
+    int first_mb;
+    int slice_type;   // 0 = P, 2 = I
+    int idr;          // nal_unit_type 5
+    int frame_num;
+    int idr_pic_id;
+    int slice_qp;
+};
+
+template <class W>
+SK_HD void write_slice_header(W& w, const SliceHeaderParams& h) {
+    put_ue(w, (uint32_t)h.first_mb);
+    put_ue(w, (uint32_t)h.slice_type);
+    put_ue(w, 0);  // pic_parameter_set_id
+    w.put((uint32_t)h.frame_num & ((1u << kLog2MaxFrameNum) - 1), kLog2MaxFrameNum);
+    if (h.idr) put_ue(w, (uint32_t)h.idr_pic_id);
+    // pic_order_cnt_type == 2: no POC syntax
+    if (h.slice_type == 0) {
+        w.put(0, 1);  // num_ref_idx_active_override_flag
+        w.put(0, 1);  // ref_pic_list_modification_flag_l0
+    }
+    // dec_ref_pic_marking() (nal_ref_idc != 0)
+    if (h.idr) {
+        w.put(0, 1);  // no_output_of_prior_pics_flag
+        w.put(0, 1);  // long_term_reference_flag
+    } else {
+        w.put(0, 1);  // adaptive_ref_pic_marking_mode_flag
+    }
+    put_se(w, h.slice_qp - 26);
+    put_ue(w, 1);     // disable_deblocking_filter_idc = 1 (filter off)
+}
+
+// Neighbour context of one macroblock for nC prediction.
+struct MbNeighbours {
+    const MbInfo* left;  // nullptr when unavailable (outside slice/picture)
+    const MbInfo* top;
+};
+
+// nC of luma block `blk` (luma4x4BlkIdx) of macroblock `cur`.
+SK_HD int luma_nc(const MbInfo& cur, MbNeighbours nb, int blk) {
+    int bx = H264_BLK_X[blk], by = H264_BLK_Y[blk];
+    bool aA, aB;
+    int nA = 0, nB = 0;
+    if (bx > 0) { aA = true; nA = cur.nnz[H264_BLK_FROM_XY[by * 4 + bx - 1]]; }
+    else { aA = nb.left != nullptr; if (aA) nA = nb.left->nnz[H264_BLK_FROM_XY[by * 4 + 3]]; }
+    if (by > 0) { aB = true; nB = cur.nnz[H264_BLK_FROM_XY[(by - 1) * 4 + bx]]; }
+    else { aB = nb.top != nullptr; if (aB) nB = nb.top->nnz[H264_BLK_FROM_XY[12 + bx]]; }
+    return nc_from(aA, nA, aB, nB);
+}
+
+// nC of chroma AC block b (0..3, raster in 2x2) of component comp (0 Cb, 1 Cr).
+SK_HD int chroma_nc(const MbInfo& cur, MbNeighbours nb, int comp, int b) {
+    int bx = b & 1, by = b >> 1;
+    int base = 16 + comp * 4;
+    bool aA, aB;
+    int nA = 0, nB = 0;
+    if (bx > 0) { aA = true; nA = cur.nnz[base + by * 2]; }
+    else { aA = nb.left != nullptr; if (aA) nA = nb.left->nnz[base + by * 2 + 1]; }
+    if (by > 0) { aB = true; nB = cur.nnz[base + bx]; }
+    else { aB = nb.top != nullptr; if (aB) nB = nb.top->nnz[base + 2 + bx]; }
+    return nc_from(aA, nA, aB, nB);
+}
+
+// macroblock_layer() header part (everything before residual()).
+// qp_delta is only written when the syntax carries it.
+template <class W>
+SK_HD void write_mb_header(W& w, const MbInfo& mb, bool p_slice, int qp_delta) {
+    int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
+    if (mb.type == MB_I16x16) {
+        put_ue(w, (uint32_t)((p_slice ? 5 : 0) + i16_mb_type(mb.i16_mode, cbp_l, cbp_c)));
+        put_ue(w, mb.chroma_mode);
+        put_se(w, qp_delta);
+    } else {  // P_L0_16x16
+        put_ue(w, 0);
+        put_se(w, mb.mvdx);
+        put_se(w, mb.mvdy);
+        put_ue(w, H264_CBP_TO_CODE_INTER[cbp_l | (cbp_c << 4)]);
+        if (mb.cbp) put_se(w, qp_delta);
+    }
+}
+
+SK_HD bool mb_has_qp_delta(const MbInfo& mb) {
+    return mb.type == MB_I16x16 || (mb.type == MB_P_16x16 && mb.cbp != 0);
+}
+
+// residual() for one macroblock; `coef` points at the MB's kCoefPerMb levels.
+template <class W>
+SK_HD void write_mb_residual(W& w, const MbInfo& mb, MbNeighbours nb, const int16_t* coef) {
+    int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
+    if (mb.type == MB_I16x16) {
+        cavlc_block(w, coef + kCoefLumaDC, 16, luma_nc(mb, nb, 0));
+        if (cbp_l) {
+            for (int blk = 0; blk < 16; blk++)
+                cavlc_block(w, coef + kCoefLuma + blk * 16 + 1, 15, luma_nc(mb, nb, blk));
+        }
+    } else {
+        for (int b8 = 0; b8 < 4; b8++) {
+            if (!(cbp_l & (1 << b8))) continue;
+            for (int i = 0; i < 4; i++) {
+                int blk = b8 * 4 + i;
+                cavlc_block(w, coef + kCoefLuma + blk * 16, 16, luma_nc(mb, nb, blk));
+            }
+        }
+    }
+    if (cbp_c) {
+        cavlc_block(w, coef + kCoefChromaDC + 0, 4, -1);
+        cavlc_block(w, coef + kCoefChromaDC + 4, 4, -1);
+    }
+    if (cbp_c == 2) {
+        for (int comp = 0; comp < 2; comp++)
+            for (int b = 0; b < 4; b++)
+                cavlc_block(w, coef + kCoefChromaAC + (comp * 4 + b) * 16 + 1, 15,
+                            chroma_nc(mb, nb, comp, b));
+    }
+}
+
+// Conservative (nC-independent) size bound of a coded macroblock in bits.
+SK_HD int mb_bits_bound(const MbInfo& mb, const int16_t* coef) {
+    int bits = 96;  // mb_type, pred modes, mvd, cbp, qp_delta, skip_run: generous
+    int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
+    if (mb.type == MB_I16x16) {
+        bits += cavlc_block_bits_bound(coef + kCoefLumaDC, 16);
+        if (cbp_l)
+            for (int blk = 0; blk < 16; blk++)
+                bits += cavlc_block_bits_bound(coef + kCoefLuma + blk * 16 + 1, 15);
+    } else {
+        for (int blk = 0; blk < 16; blk++)
+            if (cbp_l & (1 << (blk >> 2))) bits += cavlc_block_bits_bound(coef + kCoefLuma + blk * 16, 16);
+    }
+    if (cbp_c) {
+        BitCounter bc;
+        cavlc_block(bc, coef + kCoefChromaDC, 4, -1);
+        cavlc_block(bc, coef + kCoefChromaDC + 4, 4, -1);
+        bits += bc.n;
+    }
+    if (cbp_c == 2)
+        for (int b = 0; b < 8; b++) bits += cavlc_block_bits_bound(coef + kCoefChromaAC + b * 16 + 1, 15);
+    return bits;
+}
+
+}  // namespace h264
+}  // namespace sk

@@ -1,0 +1,23 @@
+// Backend interface behind the C ABI.
+#pragma once
+#include <string>
+#include <vector>
+#include "../codec/h264_frame.h"
+
+namespace sk {
+
+class EncoderBackend {
+   public:
+    virtual ~EncoderBackend() = default;
+    virtual void request_keyframe() = 0;
+    virtual int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) = 0;
+    virtual int64_t debug_buffer(const char* name, void* dst, int64_t cap) = 0;
+    virtual int stage_times(float* dst, int n) { (void)dst; (void)n; return 0; }
+    std::vector<h264::EncodedPacket> packets_;
+};
+
+EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c);
+EncoderBackend* create_hip_backend(const h264::EncoderConfig& c, int device);
+void set_last_error(const std::string& e);
+
+}  // namespace sk

@@ -1,0 +1,149 @@
+// C ABI implementation: encoder factory (CPU reference / HIP backend), packet
+// access and debug hooks used by the Python layer and the tests.
+#include "sk_api.h"
+#include "encoder_iface.h"
+#include <hip/hip_runtime_api.h>
+#include <string.h>
+#include <string>
+#include <mutex>
+
+namespace sk {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& e) { g_last_error = e; }
+
+namespace {
+
+class CpuBackend : public EncoderBackend {
+   public:
+    explicit CpuBackend(const h264::EncoderConfig& c) : enc_(c) {}
+    void request_keyframe() override { enc_.request_keyframe(); }
+    int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        packets_.clear();
+        enc_.encode(bgrx, stride, frame_id, packets_);
+        return (int)packets_.size();
+    }
+    int64_t debug_buffer(const char* name, void* dst, int64_t cap) override {
+        const void* p = nullptr;
+        int64_t n = 0;
+        std::string s(name);
+        auto plane = [&](const std::vector<uint8_t>& v) { p = v.data(); n = (int64_t)v.size(); };
+        if (s == "src_y") plane(enc_.prev[0]);  // after finish_frame the source lives in prev
+        else if (s == "src_u") plane(enc_.prev[1]);
+        else if (s == "src_v") plane(enc_.prev[2]);
+        else if (s == "ref_y") plane(enc_.ref[0]);
+        else if (s == "ref_u") plane(enc_.ref[1]);
+        else if (s == "ref_v") plane(enc_.ref[2]);
+        else if (s == "mbs") { p = enc_.mbs.data(); n = (int64_t)(enc_.mbs.size() * sizeof(h264::MbInfo)); }
+        else if (s == "coefs") { p = enc_.coefs.data(); n = (int64_t)(enc_.coefs.size() * 2); }
+        else if (s == "me") { p = enc_.me.data(); n = (int64_t)(enc_.me.size() * sizeof(h264::MeResult)); }
+        else if (s == "tasks") { p = enc_.tasks.data(); n = (int64_t)(enc_.tasks.size() * sizeof(h264::SliceTask)); }
+        else if (s == "mb_dirty") plane(enc_.mb_dirty);
+        else return -1;
+        if (dst && cap >= n) memcpy(dst, p, (size_t)n);
+        return n;
+    }
+
+   private:
+    h264::CpuH264Encoder enc_;
+};
+
+}  // namespace
+
+EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c) { return new CpuBackend(c); }
+
+h264::EncoderConfig to_config(const sk_h264_config* c) {
+    h264::EncoderConfig e;
+    e.width = c->width;
+    e.height = c->height;
+    e.stripe_height = c->stripe_height > 0 ? c->stripe_height : 64;
+    e.fullframe = c->fullframe;
+    e.full_range = c->full_range;
+    e.qp = c->qp;
+    e.paint_qp = c->paint_qp;
+    e.use_paint_over = c->use_paint_over;
+    e.paint_over_trigger = c->paint_over_trigger;
+    e.paint_over_burst = c->paint_over_burst;
+    e.streaming_mode = c->streaming_mode;
+    e.damage_threshold = c->damage_threshold;
+    e.damage_duration = c->damage_duration;
+    e.me_range = c->me_range > 0 ? c->me_range : 64;
+    e.me_iters = c->me_iters > 0 ? c->me_iters : 24;
+    e.scenecut = c->scenecut;
+    e.fps = c->fps > 0 ? c->fps : 60.f;
+    return e;
+}
+
+}  // namespace sk
+
+using namespace sk;
+
+extern "C" {
+
+const char* sk_version(void) { return "selkies-mi355x native 0.1 (gfx950)"; }
+
+int sk_hip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* sk_last_error(void) { return g_last_error.c_str(); }
+
+void* sk_h264_create(const sk_h264_config* c) {
+    if (!c || c->width < 16 || c->height < 16 || (c->width & 1) || (c->height & 1)) {
+        set_last_error("invalid encoder geometry (width/height must be even and >= 16)");
+        return nullptr;
+    }
+    if (c->stripe_height > 0 && (c->stripe_height % 16) != 0) {
+        set_last_error("stripe_height must be a multiple of 16");
+        return nullptr;
+    }
+    if (c->qp < 0 || c->qp > 51 || c->paint_qp < 0 || c->paint_qp > 51) {
+        set_last_error("qp out of range");
+        return nullptr;
+    }
+    h264::EncoderConfig e = to_config(c);
+    try {
+        if (c->backend == 1) return create_hip_backend(e, c->device);
+        return create_cpu_backend(e);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return nullptr;
+    }
+}
+
+void sk_h264_destroy(void* enc) { delete static_cast<EncoderBackend*>(enc); }
+void sk_h264_request_keyframe(void* enc) { static_cast<EncoderBackend*>(enc)->request_keyframe(); }
+
+int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->encode(bgrx, stride, (uint16_t)frame_id);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
+int sk_h264_get_packet(void* enc, int32_t i, sk_packet* out) {
+    auto* e = static_cast<EncoderBackend*>(enc);
+    if (i < 0 || i >= (int)e->packets_.size()) return -1;
+    const h264::EncodedPacket& p = e->packets_[i];
+    out->data = p.data.data();
+    out->size = (int32_t)p.data.size();
+    out->y = p.y;
+    out->w = p.w;
+    out->h = p.h;
+    out->key = p.key;
+    return 0;
+}
+
+int64_t sk_h264_debug_buffer(void* enc, const char* name, void* dst, int64_t cap) {
+    return static_cast<EncoderBackend*>(enc)->debug_buffer(name, dst, cap);
+}
+
+int sk_h264_stage_times(void* enc, float* dst, int32_t n) {
+    return static_cast<EncoderBackend*>(enc)->stage_times(dst, n);
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+"""Builds the native library (C++ runtime + gfx950 HIP kernels) in-tree.
+
+`python -m selkies_gstreamer_amd.ops.build` compiles every ``csrc/**/*.cpp`` and
+``csrc/**/*.hip`` with ``hipcc --offload-arch=gfx950`` into
+``selkies_gstreamer_amd/_lib/libselkies_native.so`` (incremental by mtime).
+The .so travels with the repository snapshot to the GPU box (gpurun).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "native"
+LIBDIR = ROOT / "selkies_gstreamer_amd" / "_lib"
+LIB = LIBDIR / "libselkies_native.so"
+ARCH = os.environ.get("SK_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+CXXFLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+    "-Wno-unused-variable", "-Wno-unused-but-set-variable", "-Wno-unused-lambda-capture",
+    f"-I{CSRC}", f"-I{CSRC / 'codec'}", f"-I{CSRC / 'runtime'}",
+]
+
+
+def _sources():
+    return sorted([p for p in CSRC.rglob("*") if p.suffix in (".cpp", ".hip")])
+
+
+def _headers_mtime() -> float:
+    return max((p.stat().st_mtime for p in CSRC.rglob("*.h")), default=0.0)
+
+
+def _compile(src: Path, hdr_mtime: float, verbose: bool) -> Path:
+    obj = BUILD / (str(src.relative_to(CSRC)).replace("/", "__") + ".o")
+    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr_mtime):
+        return obj
+    cmd = [HIPCC, *CXXFLAGS, "-c", str(src), "-o", str(obj)]
+    if src.suffix == ".hip":
+        cmd[1:1] = ["-x", "hip"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+    if r.stderr.strip() and verbose:
+        print(r.stderr, file=sys.stderr)
+    return obj
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    hdr = _headers_mtime()
+    srcs = _sources()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
+    newest = max(o.stat().st_mtime for o in objs)
+    if not LIB.exists() or LIB.stat().st_mtime < newest:
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(LIB), *map(str, objs),
+               "-lpthread", "-ldl"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

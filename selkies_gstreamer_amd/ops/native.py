@@ -1,0 +1,164 @@
+"""ctypes binding of ``libselkies_native.so`` (C ABI in csrc/runtime/sk_api.h).
+
+The library is built in-tree by ``selkies_gstreamer_amd.ops.build`` (also called
+from ``__graft_entry__.build()``). On a GPU box the HIP backend is mandatory for
+GPU-marked paths: `require_gpu()` raises instead of silently falling back.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parents[1] / "_lib" / "libselkies_native.so"
+_lib = None
+_lock = threading.Lock()
+
+
+class SkH264Config(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("stripe_height", ctypes.c_int32),
+        ("fullframe", ctypes.c_int32), ("full_range", ctypes.c_int32),
+        ("qp", ctypes.c_int32), ("paint_qp", ctypes.c_int32), ("use_paint_over", ctypes.c_int32),
+        ("paint_over_trigger", ctypes.c_int32), ("paint_over_burst", ctypes.c_int32),
+        ("streaming_mode", ctypes.c_int32), ("damage_threshold", ctypes.c_int32),
+        ("damage_duration", ctypes.c_int32), ("me_range", ctypes.c_int32), ("me_iters", ctypes.c_int32),
+        ("scenecut", ctypes.c_int32), ("fps", ctypes.c_float), ("device", ctypes.c_int32),
+        ("backend", ctypes.c_int32),
+    ]
+
+
+class SkPacket(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8)), ("size", ctypes.c_int32), ("y", ctypes.c_int32),
+                ("w", ctypes.c_int32), ("h", ctypes.c_int32), ("key", ctypes.c_int32)]
+
+
+def lib():
+    """Loads (building first if needed and possible) the native library."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists() and os.environ.get("SK_NO_AUTOBUILD") != "1":
+            from .build import build
+            build()
+        L = ctypes.CDLL(str(LIB_PATH))
+        L.sk_version.restype = ctypes.c_char_p
+        L.sk_last_error.restype = ctypes.c_char_p
+        L.sk_hip_device_count.restype = ctypes.c_int
+        L.sk_h264_create.restype = ctypes.c_void_p
+        L.sk_h264_create.argtypes = [ctypes.POINTER(SkH264Config)]
+        L.sk_h264_destroy.argtypes = [ctypes.c_void_p]
+        L.sk_h264_request_keyframe.argtypes = [ctypes.c_void_p]
+        L.sk_h264_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        L.sk_h264_encode.restype = ctypes.c_int
+        L.sk_h264_get_packet.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(SkPacket)]
+        L.sk_h264_debug_buffer.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64]
+        L.sk_h264_debug_buffer.restype = ctypes.c_int64
+        L.sk_h264_stage_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int32]
+        L.sk_h264_stage_times.restype = ctypes.c_int
+        _lib = L
+        return L
+
+
+def hip_device_count() -> int:
+    return int(lib().sk_hip_device_count())
+
+
+def require_gpu():
+    if hip_device_count() < 1:
+        raise RuntimeError("no HIP device visible to libselkies_native (gfx950 backend required)")
+
+
+@dataclass
+class Packet:
+    data: bytes
+    y: int
+    w: int
+    h: int
+    key: bool
+
+
+MB_INFO_DTYPE = np.dtype([
+    ("mvx", "<i2"), ("mvy", "<i2"), ("mvdx", "<i2"), ("mvdy", "<i2"), ("type", "u1"), ("i16_mode", "u1"),
+    ("chroma_mode", "u1"), ("cbp", "u1"), ("qp", "u1"), ("nnz", "u1", (24,)), ("pad", "u1", (3,)),
+])
+ME_DTYPE = np.dtype([("mvx", "<i2"), ("mvy", "<i2"), ("sad", "<i4"), ("intra_est", "<i4")])
+TASK_DTYPE = np.dtype([(n, "<i4") for n in (
+    "action", "qp", "first_row", "num_rows", "pic_row0", "pic_rows", "frame_num", "idr_pic_id",
+    "allow_scenecut", "idr_on_intra", "final_action", "pad")])
+
+
+class H264Encoder:
+    """Stripe H.264 encoder session (CPU reference backend or HIP backend)."""
+
+    def __init__(self, width: int, height: int, *, stripe_height: int = 64, fullframe: bool = False,
+                 full_range: bool = False, qp: int = 25, paint_qp: int = 18, use_paint_over: bool = True,
+                 paint_over_trigger: int = 15, paint_over_burst: int = 5, streaming_mode: bool = False,
+                 damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
+                 me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
+                 backend: str = "cpu"):
+        L = lib()
+        if backend not in ("cpu", "hip"):
+            raise ValueError("backend must be 'cpu' or 'hip'")
+        if backend == "hip":
+            require_gpu()
+        self.cfg = SkH264Config(width, height, stripe_height, int(fullframe), int(full_range), qp, paint_qp,
+                                int(use_paint_over), paint_over_trigger, paint_over_burst, int(streaming_mode),
+                                damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
+                                device, 1 if backend == "hip" else 0)
+        self.width, self.height = width, height
+        self.backend = backend
+        self._h = L.sk_h264_create(ctypes.byref(self.cfg))
+        if not self._h:
+            raise RuntimeError(f"sk_h264_create failed: {L.sk_last_error().decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sk_h264_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def request_keyframe(self):
+        lib().sk_h264_request_keyframe(self._h)
+
+    def encode(self, bgrx: np.ndarray, frame_id: int = 0) -> list[Packet]:
+        """bgrx: uint8 array (H, W, 4) or (H, stride) rows. Returns 0x04 stripe packets."""
+        if bgrx.dtype != np.uint8:
+            raise TypeError("bgrx must be uint8")
+        if not bgrx.flags["C_CONTIGUOUS"]:
+            bgrx = np.ascontiguousarray(bgrx)
+        stride = bgrx.strides[0]
+        L = lib()
+        n = L.sk_h264_encode(self._h, bgrx.ctypes.data, stride, frame_id & 0xFFFF)
+        if n < 0:
+            raise RuntimeError(f"encode failed: {L.sk_last_error().decode()}")
+        out = []
+        pk = SkPacket()
+        for i in range(n):
+            L.sk_h264_get_packet(self._h, i, ctypes.byref(pk))
+            out.append(Packet(ctypes.string_at(pk.data, pk.size), pk.y, pk.w, pk.h, bool(pk.key)))
+        return out
+
+    def debug_buffer(self, name: str, dtype=np.uint8) -> np.ndarray:
+        L = lib()
+        n = L.sk_h264_debug_buffer(self._h, name.encode(), None, 0)
+        if n < 0:
+            raise KeyError(name)
+        buf = np.empty(n, dtype=np.uint8)
+        L.sk_h264_debug_buffer(self._h, name.encode(), buf.ctypes.data, n)
+        return buf.view(dtype)
+
+    def stage_times(self, n: int = 16) -> list[float]:
+        arr = (ctypes.c_float * n)()
+        k = lib().sk_h264_stage_times(self._h, arr, n)
+        return list(arr[:k])
