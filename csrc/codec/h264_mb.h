@@ -70,6 +70,7 @@ SK_HD int quant_luma(const MbTransform& t, int qp, bool intra16, int16_t* coef, 
     }
     int cbp = 0;
     int mb_score = 0;
+    for (int k = 0; k < 16; k++) coef[kCoefLumaDC + k] = 0;
     for (int b8 = 0; b8 < 4; b8++) {
         int score8 = 0;
         for (int i = 0; i < 4; i++) {

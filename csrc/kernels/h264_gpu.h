@@ -1,0 +1,56 @@
+// Device-side buffers and launch interface of the HIP H.264 pipeline.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "../codec/h264_encoder.h"
+#include "../codec/h264_frame.h"
+
+namespace sk {
+namespace h264 {
+namespace gpu {
+
+constexpr int kMbSlotBytes = 1024;     // per-MB CAVLC bit buffer (A.3.1 caps a MB at 400 B)
+constexpr int kSliceHdrMax = 64;       // SPS+PPS+stripe header prefix room per slot
+
+struct Planes {
+    uint8_t* y;
+    uint8_t* u;
+    uint8_t* v;
+};
+
+// Everything a kernel needs, passed by value (pointers are device memory).
+struct FrameArgs {
+    int W, H, mb_w, mb_h, stride_y, stride_c, num_slices, rows_per_slice, fullframe;
+    int full_range, me_range, me_iters;
+    const uint8_t* bgrx;   // device copy of the captured frame
+    int bgrx_stride;
+    Planes src, prev, ref, rec;
+    uint8_t* mb_dirty;     // [num_mbs]
+    int* stripe_dirty;     // [num_slices]
+    SliceTask* tasks;      // [num_slices]
+    long long* slice_sums; // [num_slices][2] inter SAD, intra estimate
+    MeResult* me;          // [num_mbs]
+    int16_t* mvfield;      // [num_mbs][2]
+    MbInfo* mbs;           // [num_mbs]
+    int16_t* coefs;        // [num_mbs][kCoefPerMb]
+    uint32_t* mb_bits;     // [num_mbs][kMbSlotBytes/4]
+    int* mb_nbits;         // [num_mbs]
+    uint32_t* rbsp;        // [num_slices][rbsp_slot_words]
+    int rbsp_slot_words;
+    uint8_t* out;          // packet slots (host-mapped or device)
+    int out_slot_bytes;
+    int* out_size;         // [num_slices] bytes written in each slot
+    const uint8_t* param_sets;  // [num_slices or 1][kParamSetMax]
+    const int* param_set_len;
+    int param_set_stride;
+    uint8_t* host_out;     // host-mapped compacted packet buffer (k_gather)
+    const int* frame_params;  // device: [0] = frame_id
+    int first_frame;
+};
+
+void launch_convert_damage(const FrameArgs& a, hipStream_t s);
+void launch_encode(const FrameArgs& a, hipStream_t s);   // everything after planning
+void launch_commit(const FrameArgs& a, hipStream_t s);
+
+}  // namespace gpu
+}  // namespace h264
+}  // namespace sk

@@ -1,0 +1,1146 @@
+// gfx950 (CDNA4) kernels of the H.264 stripe encoder.
+//
+// Mapping (one 64-lane wavefront per macroblock):
+//   luma   lane l -> 4x4 block b = l>>2 (luma4x4BlkIdx), row r = l&3, 4 pixels per lane
+//   chroma lane l -> comp = (l>>4)&1, block = (l>>2)&3, row = l&3 (lanes 32..63 mirror 0..31)
+// The 4x4 integer transforms run in-lane horizontally and across the 4 lanes of a
+// quad vertically with DPP quad-permutes (no LDS round trip).
+//
+// Stages (all bit-exact with the CPU reference csrc/codec/h264_cpu.cpp):
+//   k_convert_damage  K1+K3  BGRx -> NV12-planar YUV 4:2:0 + per-MB damage bits
+//   k_motion_search   K4     candidate + diamond integer search, v_sad_u8
+//   k_decide                 per-slice scene-cut decision
+//   k_code_inter      K6     MC, transform, quant/decimation, QP escalation, recon
+//   k_code_intra      K5+K6  Intra16x16 wavefront (one wave per MB row, lag 2)
+//   k_cavlc           K8     per-MB CAVLC: lanes code residual blocks in parallel,
+//                            bit offsets by wave prefix-sum, LDS atomicOr packing
+//   k_assemble        K9     slice header, MB bit concatenation, emulation
+//                            prevention as a 3-state chunk scan, packet framing
+//   k_commit                 reference / MV-field update
+#include "h264_gpu.h"
+#include "../codec/color.h"
+#include "../codec/h264_mb.h"
+
+namespace sk {
+namespace h264 {
+namespace gpu {
+
+// ---------------------------------------------------------------------------
+// wave helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// inclusive prefix sum across the wave
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+
+template <int K>
+__device__ __forceinline__ int quad_bcast(int v) {
+    return __builtin_amdgcn_mov_dpp(v, K * 0x55, 0xF, 0xF, false);
+}
+
+// XCD-aware bijective block remap (8 XCDs, round-robin dispatch): consecutive
+// logical blocks land on the same XCD so neighbouring macroblocks share L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+    int q = nwg / 8, r = nwg % 8;
+    int xcd = orig % 8;
+    int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + orig / 8;
+}
+
+// Forward core transform of one 4x4 block: each lane of the quad holds row r.
+__device__ __forceinline__ void fwd4_quad(const int* x, int r, int* w) {
+    int t[4];
+    {
+        int s03 = x[0] + x[3], d03 = x[0] - x[3], s12 = x[1] + x[2], d12 = x[1] - x[2];
+        t[0] = s03 + s12;
+        t[1] = 2 * d03 + d12;
+        t[2] = s03 - s12;
+        t[3] = d03 - 2 * d12;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int a = quad_bcast<0>(t[j]), b = quad_bcast<1>(t[j]), c = quad_bcast<2>(t[j]),
+            d = quad_bcast<3>(t[j]);
+        int s03 = a + d, d03 = a - d, s12 = b + c, d12 = b - c;
+        int o0 = s03 + s12, o1 = 2 * d03 + d12, o2 = s03 - s12, o3 = d03 - 2 * d12;
+        w[j] = r == 0 ? o0 : (r == 1 ? o1 : (r == 2 ? o2 : o3));
+    }
+}
+
+// Inverse transform (8.5.12.2): rows in-lane, columns across the quad.
+__device__ __forceinline__ void inv4_quad(const int* d, int r, int* res) {
+    int f[4];
+    {
+        int e0 = d[0] + d[2], e1 = d[0] - d[2], e2 = (d[1] >> 1) - d[3], e3 = d[1] + (d[3] >> 1);
+        f[0] = e0 + e3;
+        f[1] = e1 + e2;
+        f[2] = e1 - e2;
+        f[3] = e0 - e3;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int f0 = quad_bcast<0>(f[j]), f1 = quad_bcast<1>(f[j]), f2 = quad_bcast<2>(f[j]),
+            f3 = quad_bcast<3>(f[j]);
+        int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
+        int o0 = g0 + g3, o1 = g1 + g2, o2 = g1 - g2, o3 = g0 - g3;
+        int o = r == 0 ? o0 : (r == 1 ? o1 : (r == 2 ? o2 : o3));
+        res[j] = (o + 32) >> 6;
+    }
+}
+
+// Big-endian-in-word bit writer on a shared/global u32 buffer (atomicOr, so
+// several lanes may write disjoint bit ranges concurrently).
+struct AtomicBitWriter {
+    uint32_t* buf;
+    uint32_t pos;
+    __device__ void put(uint32_t code, int len) {
+        if (len <= 0) return;
+        if (len < 32) code &= (1u << len) - 1u;
+        uint32_t wi = pos >> 5, sh = pos & 31;
+        if (sh + len <= 32) {
+            atomicOr(&buf[wi], code << (32 - sh - len));
+        } else {
+            atomicOr(&buf[wi], code >> (sh + len - 32));
+            atomicOr(&buf[wi + 1], code << (64 - sh - len));
+        }
+        pos += len;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// K1 + K3: colour conversion and damage detection.
+// Block = 256 threads = 32 x 8 chroma quads = 64 x 16 pixels (4 macroblocks).
+__global__ __launch_bounds__(256) void k_convert_damage(FrameArgs a) {
+    __shared__ int dirty[4];
+    int t = threadIdx.x;
+    if (t < 4) dirty[t] = 0;
+    __syncthreads();
+    int qc = t & 31, qr = t >> 5;
+    int qx = blockIdx.x * 32 + qc, qy = blockIdx.y * 8 + qr;
+    bool diff = false;
+    if (qx < a.stride_c) {
+        int x0 = min(2 * qx, a.W - 1), x1 = min(2 * qx + 1, a.W - 1);
+        int y0 = min(2 * qy, a.H - 1), y1 = min(2 * qy + 1, a.H - 1);
+        const uint8_t* r0 = a.bgrx + (size_t)y0 * a.bgrx_stride;
+        const uint8_t* r1 = a.bgrx + (size_t)y1 * a.bgrx_stride;
+        uint32_t p00, p01, p10, p11;
+        if (x1 == x0 + 1) {
+            uint2 v0 = *reinterpret_cast<const uint2*>(r0 + 4 * x0);
+            uint2 v1 = *reinterpret_cast<const uint2*>(r1 + 4 * x0);
+            p00 = v0.x; p01 = v0.y; p10 = v1.x; p11 = v1.y;
+        } else {
+            p00 = *reinterpret_cast<const uint32_t*>(r0 + 4 * x0);
+            p01 = *reinterpret_cast<const uint32_t*>(r0 + 4 * x1);
+            p10 = *reinterpret_cast<const uint32_t*>(r1 + 4 * x0);
+            p11 = *reinterpret_cast<const uint32_t*>(r1 + 4 * x1);
+        }
+        uint8_t y[4], cb, cr;
+        bgrx_quad_to_yuv((const uint8_t*)&p00, (const uint8_t*)&p01, (const uint8_t*)&p10,
+                         (const uint8_t*)&p11, a.full_range, y, &cb, &cr);
+        size_t oy = (size_t)(2 * qy) * a.stride_y + 2 * qx;
+        uint16_t ya = (uint16_t)(y[0] | (y[1] << 8)), yb = (uint16_t)(y[2] | (y[3] << 8));
+        uint16_t pa = *reinterpret_cast<const uint16_t*>(a.prev.y + oy);
+        uint16_t pb = *reinterpret_cast<const uint16_t*>(a.prev.y + oy + a.stride_y);
+        size_t oc = (size_t)qy * a.stride_c + qx;
+        diff = (pa != ya) | (pb != yb) | (a.prev.u[oc] != cb) | (a.prev.v[oc] != cr);
+        *reinterpret_cast<uint16_t*>(a.src.y + oy) = ya;
+        *reinterpret_cast<uint16_t*>(a.src.y + oy + a.stride_y) = yb;
+        a.src.u[oc] = cb;
+        a.src.v[oc] = cr;
+    }
+    if (diff || a.first_frame) dirty[qc >> 3] = 1;
+    __syncthreads();
+    if (t < 4) {
+        int mbx = blockIdx.x * 4 + t, mby = blockIdx.y;
+        if (mbx < a.mb_w) {
+            a.mb_dirty[mby * a.mb_w + mbx] = (uint8_t)dirty[t];
+            if (dirty[t]) atomicOr(&a.stripe_dirty[mby / a.rows_per_slice], 1);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4: integer motion search (one wave per MB).
+__device__ __forceinline__ uint32_t load_ref4(const uint8_t* row, int x, int stride) {
+    if (x >= 0 && x + 3 <= stride - 1) {
+        int xa = x & ~3, sh = x & 3;
+        uint32_t w0 = *reinterpret_cast<const uint32_t*>(row + xa);
+        if (sh == 0) return w0;
+        uint32_t w1 = *reinterpret_cast<const uint32_t*>(row + xa + 4);
+        return __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) v |= (uint32_t)row[sk_clip(x + i, 0, stride - 1)] << (8 * i);
+    return v;
+}
+
+__device__ __forceinline__ int me_sad(const FrameArgs& a, const uint8_t* refy, uint32_t sw, int mbx,
+                                      int mby, int dx, int dy, int ylo, int yhi) {
+    int l = lane_id();
+    int row = l >> 2, col4 = (l & 3) * 4;
+    int sy = sk_clip(mby * 16 + row + dy, ylo, yhi);
+    uint32_t rw = load_ref4(refy + (size_t)sy * a.stride_y, mbx * 16 + col4 + dx, a.stride_y);
+    return wave_sum((int)__builtin_amdgcn_sad_u8(sw, rw, 0u));
+}
+
+__global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
+    int nmb = a.mb_w * a.mb_h;
+    int idx = xcd_remap(blockIdx.x, gridDim.x);
+    if (idx >= nmb) return;
+    int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    int s = mby / a.rows_per_slice;
+    const SliceTask t = a.tasks[s];
+    if (t.action != ACT_P) return;
+    int l = lane_id();
+    int row = l >> 2, col4 = (l & 3) * 4;
+    uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + row) * a.stride_y +
+                                                     mbx * 16 + col4);
+    int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    const int lam = lambda_for_qp(t.qp);
+    const int R = a.me_range;
+    // candidates (same order as the CPU reference)
+    int cx[6], cy[6], n = 0;
+    cx[0] = 0; cy[0] = 0; n = 1;
+    auto add = [&](int ox, int oy) {
+        int j = oy * a.mb_w + ox;
+        cx[n] = sk_clip(a.mvfield[2 * j], -R, R);
+        cy[n] = sk_clip(a.mvfield[2 * j + 1], -R, R);
+        n++;
+    };
+    add(mbx, mby);
+    if (mbx > 0) add(mbx - 1, mby);
+    if (mbx + 1 < a.mb_w) add(mbx + 1, mby);
+    if (mby - 1 >= t.pic_row0) add(mbx, mby - 1);
+    if (mby + 1 < t.pic_row0 + t.pic_rows) add(mbx, mby + 1);
+    int bx = 0, by = 0;
+    int bsad = me_sad(a, a.ref.y, sw, mbx, mby, 0, 0, ylo, yhi);
+    int bcost = bsad + lam * (sk_se_bits(0) + sk_se_bits(0));
+    for (int i = 1; i < n; i++) {
+        int sd = me_sad(a, a.ref.y, sw, mbx, mby, cx[i], cy[i], ylo, yhi);
+        int c = sd + lam * (sk_se_bits(4 * cx[i]) + sk_se_bits(4 * cy[i]));
+        if (c < bcost) { bcost = c; bx = cx[i]; by = cy[i]; bsad = sd; }
+    }
+    const int ddx[4] = {0, -1, 1, 0}, ddy[4] = {-1, 0, 0, 1};
+    for (int it = 0; it < a.me_iters; it++) {
+        int nb = -1, ncost = bcost, nsad = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            int x = bx + ddx[k], y = by + ddy[k];
+            if (x < -R || x > R || y < -R || y > R) continue;
+            int sd = me_sad(a, a.ref.y, sw, mbx, mby, x, y, ylo, yhi);
+            int c = sd + lam * (sk_se_bits(4 * x) + sk_se_bits(4 * y));
+            if (c < ncost) { ncost = c; nb = k; nsad = sd; }
+        }
+        if (nb < 0) break;
+        bx += ddx[nb]; by += ddy[nb]; bcost = ncost; bsad = nsad;
+    }
+    // scene-cut intra estimate: sum |Y - mean|
+    int psum = (int)(sw & 255) + (int)((sw >> 8) & 255) + (int)((sw >> 16) & 255) + (int)(sw >> 24);
+    int mean = (wave_sum(psum) + 128) >> 8;
+    int dev = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) dev += sk_abs((int)((sw >> (8 * i)) & 255) - mean);
+    dev = wave_sum(dev);
+    if (l == 0) {
+        MeResult r;
+        r.mvx = (int16_t)bx;
+        r.mvy = (int16_t)by;
+        r.sad = bsad;
+        r.intra_est = dev;
+        a.me[idx] = r;
+        atomicAdd((unsigned long long*)&a.slice_sums[2 * s], (unsigned long long)bsad);
+        atomicAdd((unsigned long long*)&a.slice_sums[2 * s + 1], (unsigned long long)dev);
+    }
+}
+
+__global__ void k_decide(FrameArgs a) {
+    int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.num_slices) return;
+    SliceTask& t = a.tasks[s];
+    int fin = t.action;
+    if (t.action == ACT_P && t.allow_scenecut && a.slice_sums[2 * s] > a.slice_sums[2 * s + 1])
+        fin = ACT_I;
+    t.final_action = fin;
+}
+
+// ---------------------------------------------------------------------------
+// Macroblock residual coding shared by the inter and intra kernels.
+struct MbScratch {                 // per-wave LDS
+    int16_t coef[kCoefPerMb];      // levels, layout identical to global coefs
+    int dcy[16];                   // I16: raw DC (raster) then dequantised DC
+    int dcc[8];                    // chroma raw DC then dequantised DC
+    int blk_stat[32];              // per-lane scratch
+    int misc[8];
+};
+
+// Per-lane quantisation of this lane's luma row and chroma row into LDS, then the
+// same analysis as quant_luma / quant_chroma of the CPU path. Returns cbp.
+__device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16, MbScratch& S,
+                              int* bound_out) {
+    const int l = lane_id();
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    // ---- luma ----
+    {
+        int qbits = 15 + qp / 6;
+        int f = quant_f(qbits, intra16);
+        const int* mf = H264_QUANT_MF[qp % 6];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            int pos = r * 4 + j;
+            int lv = quant_coef(wl[j], mf[H264_POS_CLASS[pos]], f, qbits);
+            if (intra16 && pos == 0) lv = 0;
+            S.coef[kCoefLuma + b * 16 + H264_INV_ZIGZAG4x4[pos]] = (int16_t)lv;
+        }
+        if (intra16 && r == 0) S.dcy[H264_BLK_Y[b] * 4 + H264_BLK_X[b]] = wl[0];
+        if (!intra16 && l < 16) S.coef[kCoefLumaDC + l] = 0;
+    }
+    // ---- chroma ----
+    int qpc = chroma_qp(qp);
+    {
+        int qbits = 15 + qpc / 6;
+        int f = quant_f(qbits, intra16);
+        const int* mf = H264_QUANT_MF[qpc % 6];
+        if (l < 32) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                int pos = r * 4 + j;
+                int lv = pos == 0 ? 0 : quant_coef(wc[j], mf[H264_POS_CLASS[pos]], f, qbits);
+                S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + H264_INV_ZIGZAG4x4[pos]] = (int16_t)lv;
+            }
+            if (r == 0) S.dcc[comp * 4 + cb] = wc[0];
+        }
+    }
+    wave_sync();
+    // I16 luma DC: Hadamard + quant (lanes 0..15 = raster positions)
+    if (intra16 && l < 16) {
+        int qbits = 15 + qp / 6;
+        int f = quant_f(qbits, true);
+        int mf0 = H264_QUANT_MF[qp % 6][0];
+        int row = l >> 2, col = l & 3;
+        const int H4[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
+        int acc = 0;
+        for (int p = 0; p < 4; p++)
+            for (int q = 0; q < 4; q++) acc += H4[row][p] * S.dcy[p * 4 + q] * H4[q][col];
+        S.coef[kCoefLumaDC + H264_INV_ZIGZAG4x4[l]] =
+            (int16_t)quant_coef(i16_dc_fwd_round(acc), mf0, 2 * f, qbits + 1);
+    }
+    // chroma DC 2x2 Hadamard + quant (lanes 0..7 = comp*4 + i)
+    if (l < 8) {
+        int c = l >> 2, i = l & 3;
+        int qbits = 15 + qpc / 6;
+        int f = quant_f(qbits, intra16);
+        int mf0 = H264_QUANT_MF[qpc % 6][0];
+        int d0 = S.dcc[c * 4 + 0], d1 = S.dcc[c * 4 + 1], d2 = S.dcc[c * 4 + 2], d3 = S.dcc[c * 4 + 3];
+        int v = i == 0 ? d0 + d1 + d2 + d3 : (i == 1 ? d0 - d1 + d2 - d3 : (i == 2 ? d0 + d1 - d2 - d3 : d0 - d1 - d2 + d3));
+        S.coef[kCoefChromaDC + c * 4 + i] = (int16_t)quant_coef(v, mf0, 2 * f, qbits + 1);
+    }
+    wave_sync();
+    // ---- analysis: lanes 0..15 luma blocks, 16..23 chroma AC blocks ----
+    int score = 0, nz = 0, anyc = 0;
+    if (l < 16) {
+        const int16_t* c = S.coef + kCoefLuma + l * 16;
+        if (intra16) {
+            nz = count_nonzero(c + 1, 15);
+        } else {
+            score = decimate_score(c, 16);
+            nz = count_nonzero(c, 16);
+        }
+    } else if (l < 24) {
+        const int16_t* c = S.coef + kCoefChromaAC + (l - 16) * 16;
+        nz = count_nonzero(c + 1, 15);
+        if (!intra16) score = decimate_score(c + 1, 15);
+    }
+    int cbp_l;
+    if (intra16) {
+        unsigned long long m = __ballot(l < 16 && nz > 0);
+        cbp_l = m ? 15 : 0;
+    } else {
+        // 8x8 scores: sum of 4 consecutive lanes 0..15
+        int s4 = score + __shfl_down(score, 1) + __shfl_down(score, 2) + __shfl_down(score, 3);
+        int sc8[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) sc8[k] = __shfl(s4, 4 * k);
+        int mb_score = sc8[0] + sc8[1] + sc8[2] + sc8[3];
+        cbp_l = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (sc8[k] >= 4) cbp_l |= 1 << k;
+        if (mb_score < 6) cbp_l = 0;
+    }
+    // chroma: per component decimation (inter), cbp chroma
+    int chroma_score[2], comp_ac[2];
+    {
+        int sc = (l >= 16 && l < 24) ? score : 0;
+        int ac = (l >= 16 && l < 24 && nz > 0) ? 1 : 0;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            int v = (l >= 16 + 4 * c && l < 20 + 4 * c) ? sc : 0;
+            int w = (l >= 16 + 4 * c && l < 20 + 4 * c) ? ac : 0;
+            chroma_score[c] = wave_sum(v);
+            comp_ac[c] = wave_sum(w) > 0;
+        }
+    }
+    bool zero_comp[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        zero_comp[c] = !intra16 && comp_ac[c] && chroma_score[c] < 7;
+        if (zero_comp[c]) comp_ac[c] = 0;
+    }
+    bool any_dc = __ballot(l < 8 && S.coef[kCoefChromaDC + (l & 7)] != 0) != 0ull;
+    int cbp_c = (comp_ac[0] || comp_ac[1]) ? 2 : (any_dc ? 1 : 0);
+    // zero out decimated blocks
+    if (l < 16 && !intra16 && !(cbp_l & (1 << (l >> 2)))) {
+        for (int k = 0; k < 16; k++) S.coef[kCoefLuma + l * 16 + k] = 0;
+        nz = 0;
+    }
+    if (l >= 16 && l < 24 && zero_comp[(l - 16) >> 2]) {
+        for (int k = 0; k < 16; k++) S.coef[kCoefChromaAC + (l - 16) * 16 + k] = 0;
+        nz = 0;
+    }
+    wave_sync();
+    // size bound (same terms as mb_bits_bound)
+    int bnd = 0;
+    if (l < 16) {
+        if (intra16) { if (cbp_l) bnd = cavlc_block_bits_bound(S.coef + kCoefLuma + l * 16 + 1, 15); }
+        else if (cbp_l & (1 << (l >> 2))) bnd = cavlc_block_bits_bound(S.coef + kCoefLuma + l * 16, 16);
+    } else if (l < 24) {
+        if (cbp_c == 2) bnd = cavlc_block_bits_bound(S.coef + kCoefChromaAC + (l - 16) * 16 + 1, 15);
+    } else if (l == 24) {
+        if (intra16) bnd = cavlc_block_bits_bound(S.coef + kCoefLumaDC, 16);
+    } else if (l == 25 || l == 26) {
+        if (cbp_c) {
+            BitCounter bc;
+            cavlc_block(bc, S.coef + kCoefChromaDC + (l - 25) * 4, 4, -1);
+            bnd = bc.n;
+        }
+    }
+    *bound_out = 96 + wave_sum(bnd);
+    return cbp_l | (cbp_c << 4);
+}
+
+// Reconstruct this lane's luma row (4 px) and chroma row (lanes < 32).
+__device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, const int* pred_l,
+                               const int* pred_c, int* rec_l, int* rec_c) {
+    const int l = lane_id();
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    int cbp_l = cbp & 15, cbp_c = (cbp >> 4) & 3;
+    int qpc = chroma_qp(qp);
+    // DC dequant: lanes 0..15 luma (I16), lanes 16..17 chroma components
+    if (intra16 && l < 16) {
+        int row = l >> 2, col = l & 3;
+        const int H4[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
+        int acc = 0;
+        for (int p = 0; p < 4; p++)
+            for (int q = 0; q < 4; q++)
+                acc += H4[row][p] * S.coef[kCoefLumaDC + H264_INV_ZIGZAG4x4[p * 4 + q]] * H4[q][col];
+        int ls = 16 * H264_DEQUANT_V[qp % 6][0];
+        int q6 = qp / 6;
+        int v = qp >= 36 ? (acc * ls) << (q6 - 6) : (acc * ls + (1 << (5 - q6))) >> (6 - q6);
+        S.blk_stat[l] = v;  // raster position l
+    }
+    if (l >= 16 && l < 18) {
+        int c = l - 16;
+        int lv[4], dd[4];
+        for (int i = 0; i < 4; i++) lv[i] = cbp_c ? S.coef[kCoefChromaDC + c * 4 + i] : 0;
+        chroma_dc_dequant(lv, dd, qpc);
+        for (int i = 0; i < 4; i++) S.blk_stat[16 + c * 4 + i] = dd[i];
+    }
+    wave_sync();
+    // luma
+    {
+        int d[4];
+        bool coded = intra16 ? (cbp_l != 0) : ((cbp_l >> (b >> 2)) & 1);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            int pos = r * 4 + j;
+            int lv = S.coef[kCoefLuma + b * 16 + H264_INV_ZIGZAG4x4[pos]];
+            d[j] = coded ? dequant_coef(lv, qp, pos) : 0;
+        }
+        if (intra16 && r == 0) d[0] = S.blk_stat[H264_BLK_Y[b] * 4 + H264_BLK_X[b]];
+        int res[4];
+        inv4_quad(d, r, res);
+#pragma unroll
+        for (int j = 0; j < 4; j++) rec_l[j] = sk_clip255(pred_l[j] + res[j]);
+    }
+    // chroma (all lanes execute for the DPP quads; lanes >= 32 duplicate)
+    {
+        int d[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            int pos = r * 4 + j;
+            int lv = S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + H264_INV_ZIGZAG4x4[pos]];
+            d[j] = (cbp_c == 2 && pos != 0) ? dequant_coef(lv, qpc, pos) : 0;
+        }
+        if (r == 0) d[0] = S.blk_stat[16 + comp * 4 + cb];
+        int res[4];
+        inv4_quad(d, r, res);
+#pragma unroll
+        for (int j = 0; j < 4; j++) rec_c[j] = sk_clip255(pred_c[j] + res[j]);
+    }
+}
+
+// Transform + quant (with QP escalation) + recon for one MB. Inputs per lane:
+// src/pred of its luma row (4 px) and chroma row. Writes coefs + MbInfo fields.
+__device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, const int* pred_c,
+                       int slice_qp, bool intra16, MbScratch& S, MbInfo& mb, int* rec_l, int* rec_c,
+                       int16_t* gcoef) {
+    const int l = lane_id();
+    const int r = l & 3;
+    int x[4], wl[4], wc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) x[j] = src_l[j] - pred_l[j];
+    fwd4_quad(x, r, wl);
+#pragma unroll
+    for (int j = 0; j < 4; j++) x[j] = src_c[j] - pred_c[j];
+    fwd4_quad(x, r, wc);
+    int qp = slice_qp;
+    int cap = sk_min(51, slice_qp + 24);
+    int cbp = 0;
+    for (;;) {
+        int bound;
+        cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound);
+        if (qp + 6 > cap || bound <= kMbBitBudget) break;
+        qp += 6;
+        wave_sync();
+    }
+    mb.cbp = (uint8_t)cbp;
+    mb.qp = (uint8_t)qp;
+    recon_mb_lanes(qp, intra16, cbp, S, pred_l, pred_c, rec_l, rec_c);
+    // copy levels to global (816 B = 204 words)
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(S.coef);
+    uint32_t* g32 = reinterpret_cast<uint32_t*>(gcoef);
+    for (int i = l; i < kCoefPerMb / 2; i += 64) g32[i] = s32[i];
+    return qp;
+}
+
+// ---------------------------------------------------------------------------
+// K6 inter: one wave per MB of a P slice (SKIPALL slices just record skips).
+__global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
+    __shared__ MbScratch S;
+    __shared__ uint8_t nnz[24];
+    int nmb = a.mb_w * a.mb_h;
+    int idx = xcd_remap(blockIdx.x, gridDim.x);
+    if (idx >= nmb) return;
+    int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    int s = mby / a.rows_per_slice;
+    const SliceTask t = a.tasks[s];
+    int l = lane_id();
+    if (t.final_action == ACT_SKIPALL) {
+        if (l == 0) {
+            MbInfo z;
+            memset(&z, 0, sizeof(z));
+            a.mbs[idx] = z;
+            a.me[idx].mvx = 0;
+            a.me[idx].mvy = 0;
+        }
+        return;
+    }
+    if (t.final_action != ACT_P) return;
+    // MV prediction from the final motion field (all MBs of a P slice are inter)
+    auto nbr = [&](int ox, int oy, bool ok) {
+        MvNb n;
+        n.avail = ok;
+        n.inter = ok;
+        n.mvx = ok ? 4 * a.me[oy * a.mb_w + ox].mvx : 0;
+        n.mvy = ok ? 4 * a.me[oy * a.mb_w + ox].mvy : 0;
+        return n;
+    };
+    bool top = mby > t.first_row;
+    MvNb A = nbr(mbx - 1, mby, mbx > 0);
+    MvNb B = nbr(mbx, mby - 1, top);
+    MvNb C = nbr(mbx + 1, mby - 1, top && mbx + 1 < a.mb_w);
+    if (!C.avail) C = nbr(mbx - 1, mby - 1, top && mbx > 0);
+    int pmx, pmy, smx, smy;
+    mv_pred16x16(A, B, C, &pmx, &pmy);
+    mv_pskip(A, B, C, &smx, &smy);
+    int mvx = 4 * a.me[idx].mvx, mvy = 4 * a.me[idx].mvy;
+
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    // luma source + integer MC prediction
+    int px = mbx * 16 + H264_BLK_X[b] * 4, py = mby * 16 + H264_BLK_Y[b] * 4 + r;
+    uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
+    int sy = sk_clip(py + (mvy >> 2), ylo, yhi);
+    uint32_t pw = load_ref4(a.ref.y + (size_t)sy * a.stride_y, px + (mvx >> 2), a.stride_y);
+    int src_l[4], pred_l[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        src_l[j] = (sw >> (8 * j)) & 255;
+        pred_l[j] = (pw >> (8 * j)) & 255;
+    }
+    // chroma source + bilinear MC prediction
+    const uint8_t* cs = comp ? a.src.v : a.src.u;
+    const uint8_t* crf = comp ? a.ref.v : a.ref.u;
+    int cx0 = mbx * 8 + (cb & 1) * 4, cy0 = mby * 8 + (cb >> 1) * 4 + r;
+    uint32_t csw = *reinterpret_cast<const uint32_t*>(cs + (size_t)cy0 * a.stride_c + cx0);
+    int src_c[4], pred_c[4];
+    const uint8_t* cbase = crf + (size_t)(t.pic_row0 * 8) * a.stride_c;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        src_c[j] = (csw >> (8 * j)) & 255;
+        pred_c[j] = chroma_mc_sample(cbase, a.stride_c, a.stride_c, t.pic_rows * 8, cx0 + j,
+                                     cy0 - t.pic_row0 * 8, mvx, mvy);
+    }
+    MbInfo mb;
+    memset(&mb, 0, sizeof(mb));
+    mb.type = MB_P_16x16;
+    int rec_l[4], rec_c[4];
+    code_mb(src_l, pred_l, src_c, pred_c, t.qp, false, S, mb, rec_l, rec_c,
+            a.coefs + (size_t)idx * kCoefPerMb);
+    // recon
+    uint32_t rw = (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) |
+                  ((uint32_t)rec_l[3] << 24);
+    *reinterpret_cast<uint32_t*>(a.rec.y + (size_t)py * a.stride_y + px) = rw;
+    if (l < 32) {
+        uint8_t* cr = comp ? a.rec.v : a.rec.u;
+        uint32_t cw = (uint32_t)rec_c[0] | ((uint32_t)rec_c[1] << 8) | ((uint32_t)rec_c[2] << 16) |
+                      ((uint32_t)rec_c[3] << 24);
+        *reinterpret_cast<uint32_t*>(cr + (size_t)cy0 * a.stride_c + cx0) = cw;
+    }
+    // nnz was written by quant_mb_lanes into a per-lane register path; recompute from LDS
+    int nz = 0;
+    int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
+    if (l < 16) nz = (cbp_l & (1 << (l >> 2))) ? count_nonzero(S.coef + kCoefLuma + l * 16, 16) : 0;
+    else if (l < 24) nz = cbp_c == 2 ? count_nonzero(S.coef + kCoefChromaAC + (l - 16) * 16 + 1, 15) : 0;
+    if (l < 24) nnz[l] = (uint8_t)nz;
+    wave_sync();
+    if (l == 0) {
+        mb.mvx = (int16_t)mvx;
+        mb.mvy = (int16_t)mvy;
+        if (mb.cbp == 0 && mvx == smx && mvy == smy) {
+            mb.type = MB_P_SKIP;
+        } else {
+            mb.mvdx = (int16_t)(mvx - pmx);
+            mb.mvdy = (int16_t)(mvy - pmy);
+        }
+        for (int i = 0; i < 24; i++) mb.nnz[i] = nnz[i];
+        a.mbs[idx] = mb;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K5+K6 intra: one workgroup per I slice, wave w codes MB row w, MB x at step
+// t = x + 2w (wavefront); neighbour edges travel through LDS rings.
+constexpr int kMaxRows = 16;
+struct IntraEdges {
+    uint8_t bot_y[kMaxRows][4][16];      // bottom luma row of MB (row, x mod 4)
+    uint8_t bot_c[kMaxRows][4][2][8];
+    uint8_t right_y[kMaxRows][16];       // right luma column of the previous MB in the row
+    uint8_t right_c[kMaxRows][2][8];
+};
+
+__global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
+    __shared__ MbScratch Sw[kMaxRows];
+    __shared__ IntraEdges E;
+    __shared__ uint8_t nnz_sh[kMaxRows][24];
+    int s = blockIdx.x;
+    const SliceTask t = a.tasks[s];
+    if (t.final_action != ACT_I) return;
+    int w = threadIdx.x >> 6;
+    int l = lane_id();
+    int rows = t.num_rows;
+    int steps = a.mb_w + 2 * (rows - 1);
+    MbScratch& S = Sw[w];
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    for (int step = 0; step < steps; step++) {
+        int mbx = step - 2 * w;
+        bool active = w < rows && mbx >= 0 && mbx < a.mb_w;
+        if (active) {
+            int mby = t.first_row + w;
+            int idx = mby * a.mb_w + mbx;
+            bool aT = w > 0, aL = mbx > 0;
+            const uint8_t* top = aT ? E.bot_y[w - 1][mbx & 3] : nullptr;
+            const uint8_t* left = aL ? E.right_y[w] : nullptr;
+            int tl = (aT && aL) ? E.bot_y[w - 1][(mbx - 1) & 3][15] : 0;
+            uint8_t zero16[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) zero16[i] = 0;
+            const uint8_t* topp = aT ? top : zero16;
+            const uint8_t* leftp = aL ? left : zero16;
+            // luma source
+            int px = mbx * 16 + H264_BLK_X[b] * 4, py = mby * 16 + H264_BLK_Y[b] * 4 + r;
+            int lx = H264_BLK_X[b] * 4, ly = H264_BLK_Y[b] * 4 + r;
+            uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
+            int src_l[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) src_l[j] = (sw >> (8 * j)) & 255;
+            int dc = i16_dc(topp, leftp, aT, aL);
+            int pa = 0, pb = 0, pc = 0;
+            if (aT && aL) i16_plane_params(topp, leftp, tl, &pa, &pb, &pc);
+            const int order[4] = {2, 0, 1, 3};
+            int best_mode = 2, best_sad = 0x7fffffff;
+            for (int oi = 0; oi < 4; oi++) {
+                int m = order[oi];
+                if ((m == 0 && !aT) || (m == 1 && !aL) || (m == 3 && !(aT && aL))) continue;
+                int sad = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    sad += sk_abs(src_l[j] - i16_pred_pixel(m, lx + j, ly, topp, leftp, tl, aT, aL, dc, pa, pb, pc));
+                sad = wave_sum(sad);
+                if (sad < best_sad) { best_sad = sad; best_mode = m; }
+            }
+            int pred_l[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                pred_l[j] = i16_pred_pixel(best_mode, lx + j, ly, topp, leftp, tl, aT, aL, dc, pa, pb, pc);
+            // chroma
+            const uint8_t* ctop = aT ? E.bot_c[w - 1][mbx & 3][comp] : zero16;
+            const uint8_t* cleft = aL ? E.right_c[w][comp] : zero16;
+            int ctl = (aT && aL) ? E.bot_c[w - 1][(mbx - 1) & 3][comp][7] : 0;
+            const uint8_t* cs = comp ? a.src.v : a.src.u;
+            int cx0 = mbx * 8 + (cb & 1) * 4, cy0 = mby * 8 + (cb >> 1) * 4 + r;
+            int clx = (cb & 1) * 4, cly = (cb >> 1) * 4 + r;
+            uint32_t csw = *reinterpret_cast<const uint32_t*>(cs + (size_t)cy0 * a.stride_c + cx0);
+            int src_c[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) src_c[j] = (csw >> (8 * j)) & 255;
+            int qa = 0, qb = 0, qc = 0;
+            if (aT && aL) chroma_plane_params(ctop, cleft, ctl, &qa, &qb, &qc);
+            int best_cm = 0, best_csad = 0x7fffffff;
+            for (int m = 0; m < 4; m++) {
+                if ((m == 1 && !aL) || (m == 2 && !aT) || (m == 3 && !(aT && aL))) continue;
+                int sad = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    int x = clx + j, y = cly, v;
+                    if (m == 0) v = chroma_dc_block(x >> 2, y >> 2, ctop, cleft, aT, aL);
+                    else if (m == 1) v = cleft[y];
+                    else if (m == 2) v = ctop[x];
+                    else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
+                    sad += sk_abs(src_c[j] - v);
+                }
+                sad = wave_sum(l < 32 ? sad : 0);
+                if (sad < best_csad) { best_csad = sad; best_cm = m; }
+            }
+            int pred_c[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                int x = clx + j, y = cly, v;
+                if (best_cm == 0) v = chroma_dc_block(x >> 2, y >> 2, ctop, cleft, aT, aL);
+                else if (best_cm == 1) v = cleft[y];
+                else if (best_cm == 2) v = ctop[x];
+                else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
+                pred_c[j] = v;
+            }
+            MbInfo mb;
+            memset(&mb, 0, sizeof(mb));
+            mb.type = MB_I16x16;
+            mb.i16_mode = (uint8_t)best_mode;
+            mb.chroma_mode = (uint8_t)best_cm;
+            int rec_l[4], rec_c[4];
+            code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c,
+                    a.coefs + (size_t)idx * kCoefPerMb);
+            uint32_t rw = (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) |
+                          ((uint32_t)rec_l[3] << 24);
+            *reinterpret_cast<uint32_t*>(a.rec.y + (size_t)py * a.stride_y + px) = rw;
+            if (l < 32) {
+                uint8_t* crp = comp ? a.rec.v : a.rec.u;
+                uint32_t cw = (uint32_t)rec_c[0] | ((uint32_t)rec_c[1] << 8) | ((uint32_t)rec_c[2] << 16) |
+                              ((uint32_t)rec_c[3] << 24);
+                *reinterpret_cast<uint32_t*>(crp + (size_t)cy0 * a.stride_c + cx0) = cw;
+            }
+            // nnz
+            int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
+            int nz = 0;
+            if (l < 16) nz = cbp_l ? count_nonzero(S.coef + kCoefLuma + l * 16 + 1, 15) : 0;
+            else if (l < 24) nz = cbp_c == 2 ? count_nonzero(S.coef + kCoefChromaAC + (l - 16) * 16 + 1, 15) : 0;
+            if (l < 24) nnz_sh[w][l] = (uint8_t)nz;
+            wave_sync();
+            // edges for the neighbours (written after every lane has read the old ones)
+            if (ly == 15)
+                for (int j = 0; j < 4; j++) E.bot_y[w][mbx & 3][lx + j] = (uint8_t)rec_l[j];
+            if (lx + 3 == 15) E.right_y[w][ly] = (uint8_t)rec_l[3];
+            if (l < 32) {
+                if (cly == 7)
+                    for (int j = 0; j < 4; j++) E.bot_c[w][mbx & 3][comp][clx + j] = (uint8_t)rec_c[j];
+                if (clx + 3 == 7) E.right_c[w][comp][cly] = (uint8_t)rec_c[3];
+            }
+            if (l == 0) {
+                for (int i = 0; i < 24; i++) mb.nnz[i] = nnz_sh[w][i];
+                a.mbs[idx] = mb;
+                a.me[idx].mvx = 0;
+                a.me[idx].mvy = 0;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K8: CAVLC, one wave per coded MB.
+__global__ __launch_bounds__(64) void k_cavlc(FrameArgs a) {
+    __shared__ uint32_t bits[kMbSlotBytes / 4];
+    __shared__ int16_t coef[kCoefPerMb];
+    int nmb = a.mb_w * a.mb_h;
+    int idx = xcd_remap(blockIdx.x, gridDim.x);
+    if (idx >= nmb) return;
+    int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    int s = mby / a.rows_per_slice;
+    const SliceTask t = a.tasks[s];
+    if (t.final_action != ACT_P && t.final_action != ACT_I) return;
+    int l = lane_id();
+    const MbInfo mb = a.mbs[idx];
+    if (mb.type == MB_P_SKIP) {
+        if (l == 0) a.mb_nbits[idx] = 0;
+        return;
+    }
+    bool p_slice = t.final_action == ACT_P;
+    int first = t.first_row * a.mb_w;
+    // mb_skip_run: skipped MBs since the previous coded MB of the slice
+    int run = 0;
+    if (p_slice) {
+        int j = idx - 1;
+        while (j >= first) {
+            int base = j - 63;
+            int m = base + l;
+            bool coded = m >= first && a.mbs[m].type != MB_P_SKIP;
+            unsigned long long msk = __ballot(coded);
+            if (msk) {
+                int hi = 63 - __clzll(msk);
+                run += j - (base + hi);
+                break;
+            }
+            run += j - sk_max(base, first) + 1;
+            j = base - 1;
+        }
+    }
+    // QP predictor: QP of the previous MB that carried mb_qp_delta
+    int qp_prev = t.qp;
+    {
+        int j = idx - 1;
+        while (j >= first) {
+            int base = j - 63;
+            int m = base + l;
+            bool has = m >= first && mb_has_qp_delta(a.mbs[m]);
+            unsigned long long msk = __ballot(has);
+            if (msk) {
+                int hi = 63 - __clzll(msk);
+                qp_prev = a.mbs[base + hi].qp;
+                break;
+            }
+            j = base - 1;
+        }
+    }
+    for (int i = l; i < kMbSlotBytes / 4; i += 64) bits[i] = 0;
+    const int16_t* gc = a.coefs + (size_t)idx * kCoefPerMb;
+    for (int i = l; i < kCoefPerMb / 2; i += 64)
+        reinterpret_cast<uint32_t*>(coef)[i] = reinterpret_cast<const uint32_t*>(gc)[i];
+    wave_sync();
+    MbNeighbours nb;
+    nb.left = mbx > 0 ? &a.mbs[idx - 1] : nullptr;
+    nb.top = mby > t.first_row ? &a.mbs[idx - a.mb_w] : nullptr;
+    int hdr_bits = 0;
+    if (l == 0) {
+        AtomicBitWriter w{bits, 0};
+        if (p_slice) put_ue(w, (uint32_t)run);
+        int dq = mb_has_qp_delta(mb) ? (int)mb.qp - qp_prev : 0;
+        write_mb_header(w, mb, p_slice, dq);
+        hdr_bits = (int)w.pos;
+    }
+    hdr_bits = __shfl(hdr_bits, 0);
+    // residual block list (bitstream order)
+    int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
+    bool i16 = mb.type == MB_I16x16;
+    const int16_t* bc = nullptr;
+    int maxn = 0, nc = 0;
+    bool act = false;
+    if (l == 0) {
+        if (i16) { act = true; bc = coef + kCoefLumaDC; maxn = 16; nc = luma_nc(mb, nb, 0); }
+    } else if (l <= 16) {
+        int blk = l - 1;
+        if (i16) {
+            if (cbp_l) { act = true; bc = coef + kCoefLuma + blk * 16 + 1; maxn = 15; }
+        } else if (cbp_l & (1 << (blk >> 2))) {
+            act = true; bc = coef + kCoefLuma + blk * 16; maxn = 16;
+        }
+        if (act) nc = luma_nc(mb, nb, blk);
+    } else if (l <= 18) {
+        if (cbp_c) { act = true; bc = coef + kCoefChromaDC + (l - 17) * 4; maxn = 4; nc = -1; }
+    } else if (l <= 26) {
+        if (cbp_c == 2) {
+            int k = l - 19, c = k >> 2, bb = k & 3;
+            act = true; bc = coef + kCoefChromaAC + (c * 4 + bb) * 16 + 1; maxn = 15;
+            nc = chroma_nc(mb, nb, c, bb);
+        }
+    }
+    int nbits = 0;
+    if (act) {
+        BitCounter cnt;
+        cavlc_block(cnt, bc, maxn, nc);
+        nbits = cnt.n;
+    }
+    int incl = wave_incl_scan(nbits);
+    int off = hdr_bits + incl - nbits;
+    if (act) {
+        AtomicBitWriter w{bits, (uint32_t)off};
+        cavlc_block(w, bc, maxn, nc);
+    }
+    int total = hdr_bits + __shfl(incl, 63);
+    wave_sync();
+    int nwords = (total + 31) >> 5;
+    uint32_t* dst = a.mb_bits + (size_t)idx * (kMbSlotBytes / 4);
+    for (int i = l; i < nwords; i += 64) dst[i] = bits[i];
+    if (l == 0) a.mb_nbits[idx] = total;
+}
+
+// ---------------------------------------------------------------------------
+// K9: slice assembly (one 256-thread workgroup per coded slice).
+__global__ __launch_bounds__(256) void k_assemble(FrameArgs a) {
+    __shared__ uint32_t hdr[32];
+    __shared__ int scan[256];
+    __shared__ int chunk_state[256][3];   // state_out for each state_in
+    __shared__ int chunk_ins[256][3];     // insertions for each state_in
+    __shared__ int chunk_in[256], chunk_off[256];
+    __shared__ int sh_misc[8];
+    int s = blockIdx.x;
+    SliceTask& task = a.tasks[s];
+    int fin = task.final_action;
+    int tid = threadIdx.x;
+    if (fin == ACT_NONE) {
+        if (tid == 0) a.out_size[s] = 0;
+        return;
+    }
+    const int nmb = task.num_rows * a.mb_w;
+    const int first = task.first_row * a.mb_w;
+    uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    bool intra = fin == ACT_I;
+    bool idr = intra && task.idr_on_intra;
+    if (tid < 32) hdr[tid] = 0;
+    __syncthreads();
+    if (tid == 0) {
+        AtomicBitWriter w{hdr, 0};
+        SliceHeaderParams h;
+        h.first_mb = a.fullframe ? first : 0;
+        h.slice_type = intra ? 2 : 0;
+        h.idr = idr;
+        h.frame_num = idr ? 0 : task.frame_num;
+        h.idr_pic_id = task.idr_pic_id;
+        h.slice_qp = task.qp;
+        write_slice_header(w, h);
+        if (fin == ACT_SKIPALL) put_ue(w, (uint32_t)nmb);
+        sh_misc[0] = (int)w.pos;
+    }
+    // per-thread MB ranges
+    int per = (nmb + 255) / 256;
+    int m0 = sk_min(nmb, tid * per), m1 = sk_min(nmb, m0 + per);
+    int local = 0, last_coded = -1;
+    if (fin != ACT_SKIPALL)
+        for (int m = m0; m < m1; m++) {
+            int nb = a.mb_nbits[first + m];
+            local += nb;
+            if (nb > 0) last_coded = m;
+        }
+    scan[tid] = local;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+        int v = tid >= o ? scan[tid - o] : 0;
+        __syncthreads();
+        scan[tid] += v;
+        __syncthreads();
+    }
+    int hb = sh_misc[0];
+    int excl = scan[tid] - local;
+    // last coded MB (for the trailing mb_skip_run)
+    if (tid == 0) sh_misc[1] = -1;
+    __syncthreads();
+    if (last_coded >= 0) atomicMax(&sh_misc[1], last_coded);
+    // header words
+    if (tid < 32 && tid * 32 < hb) atomicOr(&rbsp[tid], hdr[tid]);
+    // MB bit copies
+    uint32_t pos = (uint32_t)(hb + excl);
+    if (fin != ACT_SKIPALL)
+        for (int m = m0; m < m1; m++) {
+            int nb = a.mb_nbits[first + m];
+            const uint32_t* src = a.mb_bits + (size_t)(first + m) * (kMbSlotBytes / 4);
+            int nw = (nb + 31) >> 5;
+            for (int k = 0; k < nw; k++) {
+                uint32_t v = src[k];
+                uint32_t p = pos + 32u * k;
+                uint32_t wi = p >> 5, sh = p & 31;
+                atomicOr(&rbsp[wi], v >> sh);
+                if (sh) atomicOr(&rbsp[wi + 1], v << (32 - sh));
+            }
+            pos += nb;
+        }
+    __syncthreads();
+    int total_bits = hb + scan[255];
+    if (tid == 0) {
+        AtomicBitWriter w{rbsp, (uint32_t)total_bits};
+        if (fin == ACT_P) {
+            int trailing = nmb - 1 - sh_misc[1];
+            if (trailing > 0) put_ue(w, (uint32_t)trailing);
+        }
+        w.put(1, 1);  // rbsp_stop_one_bit
+        int nbytes = (int)((w.pos + 7) >> 3);
+        sh_misc[2] = nbytes;
+    }
+    __threadfence();
+    __syncthreads();
+    const int n = sh_misc[2];
+    // ---- emulation prevention: each thread a word-aligned chunk, 3-state
+    // transfer functions composed in order, then a replay that writes bytes.
+    int C = (((n + 255) / 256) + 3) & ~3;
+    int c0 = sk_min(n, tid * C), c1 = sk_min(n, c0 + C);
+    for (int st = 0; st < 3; st++) {
+        int zeros = st, ins = 0;
+        for (int j = c0; j < c1; j += 4) {
+            uint32_t wd = __hip_atomic_load(&rbsp[j >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int lim = sk_min(4, c1 - j);
+            for (int q = 0; q < lim; q++) {
+                int bt = (int)((wd >> (24 - 8 * q)) & 255u);
+                if (zeros >= 2 && bt <= 3) { ins++; zeros = 0; }
+                zeros = bt == 0 ? sk_min(zeros + 1, 2) : 0;
+            }
+        }
+        chunk_state[tid][st] = zeros;
+        chunk_ins[tid][st] = ins;
+    }
+    __syncthreads();
+    // packet prefix
+    uint8_t* slot = a.out + (size_t)s * a.out_slot_bytes;
+    if (tid == 0) {
+        int p = 0;
+        if (!a.fullframe) {
+            int y = task.first_row * 16;
+            int h = sk_min(a.H, (task.first_row + task.num_rows) * 16) - y;
+            int fid = a.frame_params[0];
+            slot[0] = 0x04;
+            slot[1] = idr ? 1 : 0;
+            slot[2] = (uint8_t)(fid >> 8);
+            slot[3] = (uint8_t)fid;
+            slot[4] = (uint8_t)(y >> 8); slot[5] = (uint8_t)y;
+            slot[6] = (uint8_t)(a.W >> 8); slot[7] = (uint8_t)a.W;
+            slot[8] = (uint8_t)(h >> 8); slot[9] = (uint8_t)h;
+            p = 10;
+            if (idr) {
+                int len = a.param_set_len[s];
+                const uint8_t* ps = a.param_sets + (size_t)s * a.param_set_stride;
+                for (int i = 0; i < len; i++) slot[p + i] = ps[i];
+                p += len;
+            }
+        }
+        slot[p++] = 0; slot[p++] = 0; slot[p++] = 0; slot[p++] = 1;
+        slot[p++] = idr ? 0x65 : 0x41;
+        int st = 0, off = p;
+        for (int k = 0; k < 256; k++) {
+            chunk_in[k] = st;
+            chunk_off[k] = off;
+            int ck0 = sk_min(n, k * C), ck1 = sk_min(n, ck0 + C);
+            off += (ck1 - ck0) + chunk_ins[k][st];
+            st = chunk_state[k][st];
+        }
+        sh_misc[3] = off;
+    }
+    __syncthreads();
+    {
+        int zeros = chunk_in[tid], o = chunk_off[tid];
+        for (int j = c0; j < c1; j += 4) {
+            uint32_t wd = __hip_atomic_load(&rbsp[j >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int lim = sk_min(4, c1 - j);
+            for (int q = 0; q < lim; q++) {
+                int bt = (int)((wd >> (24 - 8 * q)) & 255u);
+                if (zeros >= 2 && bt <= 3) { slot[o++] = 3; zeros = 0; }
+                slot[o++] = (uint8_t)bt;
+                zeros = bt == 0 ? sk_min(zeros + 1, 2) : 0;
+            }
+        }
+    }
+    if (tid == 0) a.out_size[s] = sh_misc[3];
+}
+
+// Packs the per-slice packet slots into one host-visible buffer (64-byte aligned
+// offsets, 16-byte stores): the host reads results after a single sync.
+__global__ __launch_bounds__(256) void k_gather(FrameArgs a) {
+    int s = blockIdx.x;
+    int size = a.out_size[s];
+    if (size <= 0) return;
+    long off = 0;
+    for (int k = 0; k < s; k++) off += ((long)a.out_size[k] + 63) & ~63L;
+    const uint4* src = reinterpret_cast<const uint4*>(a.out + (size_t)s * a.out_slot_bytes);
+    uint4* dst = reinterpret_cast<uint4*>(a.host_out + off);
+    int n16 = (size + 15) >> 4;
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_commit(FrameArgs a) {
+    int nmb = a.mb_w * a.mb_h;
+    int idx = blockIdx.x;
+    if (idx >= nmb) return;
+    int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    int s = mby / a.rows_per_slice;
+    int fin = a.tasks[s].final_action;
+    int l = lane_id();
+    if (fin == ACT_NONE) return;
+    if (fin == ACT_SKIPALL) {
+        if (l == 0) { a.mvfield[2 * idx] = 0; a.mvfield[2 * idx + 1] = 0; }
+        return;
+    }
+    // luma 16 rows x 16 bytes: lanes 0..63 copy one u32 each
+    {
+        int row = l >> 2, c4 = (l & 3) * 4;
+        size_t o = (size_t)(mby * 16 + row) * a.stride_y + mbx * 16 + c4;
+        *reinterpret_cast<uint32_t*>(a.ref.y + o) = *reinterpret_cast<const uint32_t*>(a.rec.y + o);
+    }
+    if (l < 32) {
+        int comp = l >> 4, row = (l >> 1) & 7, c4 = (l & 1) * 4;
+        size_t o = (size_t)(mby * 8 + row) * a.stride_c + mbx * 8 + c4;
+        uint8_t* dst = comp ? a.ref.v : a.ref.u;
+        const uint8_t* src = comp ? a.rec.v : a.rec.u;
+        *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(src + o);
+    }
+    if (l == 0) {
+        a.mvfield[2 * idx] = a.me[idx].mvx;
+        a.mvfield[2 * idx + 1] = a.me[idx].mvy;
+    }
+}
+
+// ---------------------------------------------------------------------------
+void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
+    dim3 grid((a.mb_w + 3) / 4, a.mb_h);
+    hipLaunchKernelGGL(k_convert_damage, grid, dim3(256), 0, s, a);
+}
+
+void launch_encode(const FrameArgs& a, hipStream_t s) {
+    int nmb = a.mb_w * a.mb_h;
+    hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_decide, dim3((a.num_slices + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_code_inter, dim3(nmb), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_code_intra, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
+    hipLaunchKernelGGL(k_cavlc, dim3(nmb), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_assemble, dim3(a.num_slices), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gather, dim3(a.num_slices), dim3(256), 0, s, a);
+}
+
+void launch_commit(const FrameArgs& a, hipStream_t s) {
+    int nmb = a.mb_w * a.mb_h;
+    hipLaunchKernelGGL(k_commit, dim3(nmb), dim3(64), 0, s, a);
+}
+
+}  // namespace gpu
+}  // namespace h264
+}  // namespace sk
