@@ -6,6 +6,7 @@
 #include <string.h>
 #include <string>
 #include <mutex>
+#include <stdlib.h>
 
 namespace sk {
 
@@ -89,6 +90,19 @@ int sk_hip_device_count(void) {
 }
 
 const char* sk_last_error(void) { return g_last_error.c_str(); }
+
+void* sk_host_alloc(int64_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault) != hipSuccess) {
+        p = aligned_alloc(4096, ((size_t)bytes + 4095) & ~(size_t)4095);  // no GPU: plain memory
+    }
+    return p;
+}
+
+void sk_host_free(void* p) {
+    if (!p) return;
+    if (hipHostFree(p) != hipSuccess) free(p);
+}
 
 void* sk_h264_create(const sk_h264_config* c) {
     if (!c || c->width < 16 || c->height < 16 || (c->width & 1) || (c->height & 1)) {

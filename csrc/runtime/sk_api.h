@@ -39,6 +39,10 @@ int sk_h264_stage_times(void* enc, float* dst, int32_t n);
 
 const char* sk_last_error(void);
 
+// Page-locked host memory (capture buffers / frame pools): DMA-able by HIP.
+void* sk_host_alloc(int64_t bytes);
+void sk_host_free(void* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,9 @@ def lib():
         L.sk_h264_debug_buffer.restype = ctypes.c_int64
         L.sk_h264_stage_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int32]
         L.sk_h264_stage_times.restype = ctypes.c_int
+        L.sk_host_alloc.restype = ctypes.c_void_p
+        L.sk_host_alloc.argtypes = [ctypes.c_int64]
+        L.sk_host_free.argtypes = [ctypes.c_void_p]
         _lib = L
         return L
 
@@ -72,6 +75,32 @@ def hip_device_count() -> int:
 def require_gpu():
     if hip_device_count() < 1:
         raise RuntimeError("no HIP device visible to libselkies_native (gfx950 backend required)")
+
+
+class PinnedBuffer:
+    """Page-locked host buffer exposed as a numpy array (frees on close/GC)."""
+
+    def __init__(self, shape, dtype=np.uint8):
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+        n = int(np.prod(self.shape)) * self.dtype.itemsize
+        self._ptr = lib().sk_host_alloc(n)
+        if not self._ptr:
+            raise MemoryError("sk_host_alloc failed")
+        buf = (ctypes.c_uint8 * n).from_address(self._ptr)
+        self.array = np.frombuffer(buf, dtype=self.dtype).reshape(self.shape)
+
+    def close(self):
+        if self._ptr:
+            self.array = None
+            lib().sk_host_free(self._ptr)
+            self._ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 @dataclass
