@@ -148,9 +148,17 @@ SK_HD int quant_coef(int w, int mf, int f, int qbits) {
 }
 SK_HD int quant_f(int qbits, bool intra) { return intra ? (1 << qbits) / 3 : (1 << qbits) / 6; }
 
+// Position class of raster index r: 0 = (even,even), 1 = (odd,odd), 2 = mixed.
+SK_HD int pos_class(int r) {
+    int i = r >> 2, j = r & 3;
+    return ((i | j) & 1) == 0 ? 0 : (((i & j) & 1) ? 1 : 2);
+}
+SK_HD int sel3(int c, int a0, int a1, int a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
+
 // Dequantise a non-DC coefficient at raster position `r` (flat scaling lists).
 SK_HD int dequant_coef(int l, int qp, int r) {
-    return (l * H264_DEQUANT_V[qp % 6][H264_POS_CLASS[r]]) << (qp / 6);
+    const int32_t* v = H264_DEQUANT_V[qp % 6];
+    return (l * sel3(pos_class(r), v[0], v[1], v[2])) << (qp / 6);
 }
 
 // Intra16x16 DC: inverse Hadamard of the 4x4 DC level matrix and scaling (8.5.10).
@@ -199,7 +207,7 @@ SK_HD int decimate_score(const int16_t* c, int n) {
         int run = 0;
         idx--;
         while (idx >= 0 && c[idx] == 0) { idx--; run++; }
-        score += H264_DECIMATE_RUN[run];
+        score += run == 0 ? 3 : (run <= 2 ? 2 : (run <= 5 ? 1 : 0));
     }
     return score;
 }
@@ -207,88 +215,85 @@ SK_HD int decimate_score(const int16_t* c, int n) {
 // ---------------------------------------------------------------------------
 // CAVLC residual block coder (9.2). `c` holds `maxNum` levels in scan order.
 // vlc selection: nC >= 0 -> luma/chroma-AC tables, nC == -1 -> chroma DC.
-// Returns the TotalCoeff of the block.
+// Streaming formulation (no per-coefficient arrays) so the GPU build keeps
+// everything in registers. Returns the TotalCoeff of the block.
 template <class W>
-SK_HD int cavlc_block(W& w, const int16_t* c, int maxNum, int nC) {
-    int levels[16];
-    int runs[16];
-    int total = 0;
-    int last = maxNum - 1;
-    while (last >= 0 && c[last] == 0) last--;
-    int total_zeros = 0;
-    for (int i = last; i >= 0;) {
-        levels[total] = c[i];
-        int run = 0;
-        i--;
-        while (i >= 0 && c[i] == 0) { run++; i--; }
-        runs[total] = run;
+SK_HD int cavlc_block(W& w, const int16_t* c, int maxNum, int nC, const CavlcTables& T) {
+    // pass 1: TotalCoeff, TrailingOnes, position of the last non-zero
+    int total = 0, t1 = 0, last = -1;
+    bool in_t1 = true;
+    for (int i = maxNum - 1; i >= 0; i--) {
+        int v = c[i];
+        if (v == 0) continue;
+        if (last < 0) last = i;
         total++;
+        if (in_t1 && t1 < 3 && (v == 1 || v == -1)) t1++;
+        else in_t1 = false;
     }
-    if (total > 0) total_zeros = (last + 1) - total;
-    int t1 = 0;
-    while (t1 < total && t1 < 3 && (levels[t1] == 1 || levels[t1] == -1)) t1++;
-
-    // coeff_token
     int tok = total * 4 + t1;
     if (nC == -1) {
-        w.put(H264_CDC_COEFF_TOKEN_CODE[tok], H264_CDC_COEFF_TOKEN_LEN[tok]);
+        w.put(T.cdc_code[tok], T.cdc_len[tok]);
     } else {
         int vlc = nC < 2 ? 0 : (nC < 4 ? 1 : (nC < 8 ? 2 : 3));
-        w.put(H264_COEFF_TOKEN_CODE[vlc][tok], H264_COEFF_TOKEN_LEN[vlc][tok]);
+        w.put(T.ct_code[vlc][tok], T.ct_len[vlc][tok]);
     }
     if (total == 0) return 0;
-
-    for (int i = 0; i < t1; i++) w.put(levels[i] < 0 ? 1 : 0, 1);
-
+    const int total_zeros = (last + 1) - total;
+    // pass 2: trailing-one signs and levels, highest frequency first
+    int k = 0;
     int suffix_len = (total > 10 && t1 < 3) ? 1 : 0;
-    for (int i = t1; i < total; i++) {
-        int lv = levels[i];
-        int lc = lv > 0 ? 2 * lv - 2 : -2 * lv - 1;
-        if (i == t1 && t1 < 3) lc -= 2;
-        if (suffix_len == 0) {
-            if (lc < 14) {
-                w.put(1, lc + 1);
-            } else if (lc < 30) {
-                w.put(1, 15);  // prefix 14
-                w.put(lc - 14, 4);
-            } else {
-                w.put(1, 16);  // prefix 15
-                w.put(lc - 30, 12);
-            }
+    for (int i = last; i >= 0; i--) {
+        int lv = c[i];
+        if (lv == 0) continue;
+        if (k < t1) {
+            w.put(lv < 0 ? 1 : 0, 1);
         } else {
-            if (lc < (15 << suffix_len)) {
-                w.put(1, (lc >> suffix_len) + 1);
-                w.put(lc & ((1 << suffix_len) - 1), suffix_len);
+            int lc = lv > 0 ? 2 * lv - 2 : -2 * lv - 1;
+            if (k == t1 && t1 < 3) lc -= 2;
+            if (suffix_len == 0) {
+                if (lc < 14) {
+                    w.put(1, lc + 1);
+                } else if (lc < 30) {
+                    w.put(1, 15);  // level_prefix 14
+                    w.put(lc - 14, 4);
+                } else {
+                    w.put(1, 16);  // level_prefix 15
+                    w.put(lc - 30, 12);
+                }
             } else {
-                w.put(1, 16);
-                w.put(lc - (15 << suffix_len), 12);
+                if (lc < (15 << suffix_len)) {
+                    w.put(1, (lc >> suffix_len) + 1);
+                    w.put(lc & ((1 << suffix_len) - 1), suffix_len);
+                } else {
+                    w.put(1, 16);
+                    w.put(lc - (15 << suffix_len), 12);
+                }
             }
+            if (suffix_len == 0) suffix_len = 1;
+            if (sk_abs(lv) > (3 << (suffix_len - 1)) && suffix_len < 6) suffix_len++;
         }
-        if (suffix_len == 0) suffix_len = 1;
-        if (sk_abs(lv) > (3 << (suffix_len - 1)) && suffix_len < 6) suffix_len++;
+        k++;
     }
-
     if (total < maxNum) {
-        if (maxNum == 4) {
-            w.put(H264_CDC_TOTAL_ZEROS_CODE[total - 1][total_zeros],
-                  H264_CDC_TOTAL_ZEROS_LEN[total - 1][total_zeros]);
-        } else {
-            w.put(H264_TOTAL_ZEROS_CODE[total - 1][total_zeros],
-                  H264_TOTAL_ZEROS_LEN[total - 1][total_zeros]);
-        }
+        if (maxNum == 4) w.put(T.cdc_tz_code[total - 1][total_zeros], T.cdc_tz_len[total - 1][total_zeros]);
+        else w.put(T.tz_code[total - 1][total_zeros], T.tz_len[total - 1][total_zeros]);
     }
+    // pass 3: run_before of each coefficient but the lowest-frequency one
     int zeros_left = total_zeros;
-    for (int i = 0; i < total - 1 && zeros_left > 0; i++) {
-        int rb = runs[i];
+    k = 0;
+    for (int i = last; i >= 0 && zeros_left > 0 && k < total - 1;) {
+        int run = 0;
+        int j = i - 1;
+        while (j >= 0 && c[j] == 0) { run++; j--; }
         int tbl = sk_min(zeros_left, 7) - 1;
-        w.put(H264_RUN_BEFORE_CODE[tbl][rb], H264_RUN_BEFORE_LEN[tbl][rb]);
-        zeros_left -= rb;
+        w.put(T.rb_code[tbl][run], T.rb_len[tbl][run]);
+        zeros_left -= run;
+        k++;
+        i = j;
     }
     return total;
 }
 
-// Upper bound of a luma/chroma-AC block's CAVLC bits that is independent of nC
-// (uses the longest coeff_token over the four tables).
 SK_HD void cavlc_token_stats(const int16_t* c, int maxNum, int* total, int* t1) {
     int n = 0, t = 0;
     bool in_t1 = true;
@@ -301,13 +306,23 @@ SK_HD void cavlc_token_stats(const int16_t* c, int maxNum, int* total, int* t1) 
     *total = n;
     *t1 = t;
 }
-SK_HD int cavlc_block_bits_bound(const int16_t* c, int maxNum) {
+SK_HD int cavlc_block_bits_bound(const int16_t* c, int maxNum, const CavlcTables& T) {
     BitCounter bc;
-    cavlc_block(bc, c, maxNum, 0);
+    cavlc_block(bc, c, maxNum, 0, T);
     int total, t1;
     cavlc_token_stats(c, maxNum, &total, &t1);
     int tok = total * 4 + t1;
-    return bc.n - H264_COEFF_TOKEN_LEN[0][tok] + H264_COEFF_TOKEN_MAXLEN[tok];
+    return bc.n - T.ct_len[0][tok] + T.ct_maxlen[tok];
+}
+
+// Host-side table instance (the GPU kernels keep theirs in LDS).
+inline const CavlcTables& host_cavlc_tables() {
+    static CavlcTables t = [] {
+        CavlcTables x;
+        cavlc_tables_copy_range(x, 0, 1);
+        return x;
+    }();
+    return t;
 }
 
 SK_HD int count_nonzero(const int16_t* c, int n) {

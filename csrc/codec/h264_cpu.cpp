@@ -229,7 +229,7 @@ void CpuH264Encoder::code_slice_inter(int s) {
             residual_transform(sy, py, su, pu, sv, pv, tr);
             int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
             mb.type = MB_P_16x16;
-            int qp = quant_mb_with_budget(tr, t.qp, false, mb, coef);
+            int qp = quant_mb_with_budget(tr, t.qp, false, mb, coef, host_cavlc_tables());
             mb.mvx = (int16_t)mvx;
             mb.mvy = (int16_t)mvy;
             if (mb.cbp == 0 && mvx == smx && mvy == smy) {
@@ -331,7 +331,7 @@ void CpuH264Encoder::code_slice_intra(int s) {
             mb.type = MB_I16x16;
             mb.i16_mode = (uint8_t)best_mode;
             mb.chroma_mode = (uint8_t)best_cm;
-            int qp = quant_mb_with_budget(tr, t.qp, true, mb, coef);
+            int qp = quant_mb_with_budget(tr, t.qp, true, mb, coef, host_cavlc_tables());
             uint8_t ry[256], ru[64], rv[64];
             recon_luma(coef, qp, true, mb.cbp & 15, py, ry);
             recon_chroma(coef, qp, (mb.cbp >> 4) & 3, pcb[best_cm][0], pcb[best_cm][1], ru, rv);
@@ -393,7 +393,7 @@ std::vector<uint8_t> CpuH264Encoder::write_slice(int s) {
                 write_mb_header(w, mb, !intra, dq);
                 MbNeighbours nb;
                 mb_neighbours(mbx, mby, t.first_row, nb);
-                write_mb_residual(w, mb, nb, &coefs[(size_t)idx * kCoefPerMb]);
+                write_mb_residual(w, mb, nb, &coefs[(size_t)idx * kCoefPerMb], host_cavlc_tables());
             }
         if (skip_run > 0) put_ue(w, (uint32_t)skip_run);
     }

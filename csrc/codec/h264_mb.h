@@ -18,7 +18,7 @@ SK_HD void residual_transform(const uint8_t* src_y, const uint8_t* pred_y, const
                               const uint8_t* pred_u, const uint8_t* src_v, const uint8_t* pred_v,
                               MbTransform& t) {
     for (int blk = 0; blk < 16; blk++) {
-        int x0 = H264_BLK_X[blk] * 4, y0 = H264_BLK_Y[blk] * 4;
+        int x0 = blk_x(blk) * 4, y0 = blk_y(blk) * 4;
         int r[16];
         for (int y = 0; y < 4; y++)
             for (int x = 0; x < 4; x++)
@@ -49,18 +49,18 @@ SK_HD int quant_luma(const MbTransform& t, int qp, bool intra16, int16_t* coef, 
     const int* mf = H264_QUANT_MF[qp % 6];
     if (intra16) {
         int dc[16], hd[16];
-        for (int blk = 0; blk < 16; blk++) dc[H264_BLK_Y[blk] * 4 + H264_BLK_X[blk]] = t.wl[blk][0];
+        for (int blk = 0; blk < 16; blk++) dc[blk_y(blk) * 4 + blk_x(blk)] = t.wl[blk][0];
         hadamard4x4(dc, hd);
         for (int k = 0; k < 16; k++)
             coef[kCoefLumaDC + k] =
-                (int16_t)quant_coef(i16_dc_fwd_round(hd[H264_ZIGZAG4x4[k]]), mf[0], 2 * f, qbits + 1);
+                (int16_t)quant_coef(i16_dc_fwd_round(hd[zigzag4x4(k)]), mf[0], 2 * f, qbits + 1);
         bool any = false;
         for (int blk = 0; blk < 16; blk++) {
             int16_t* c = coef + kCoefLuma + blk * 16;
             c[0] = 0;
             for (int k = 1; k < 16; k++) {
-                int pos = H264_ZIGZAG4x4[k];
-                c[k] = (int16_t)quant_coef(t.wl[blk][pos], mf[H264_POS_CLASS[pos]], f, qbits);
+                int pos = zigzag4x4(k);
+                c[k] = (int16_t)quant_coef(t.wl[blk][pos], sel3(pos_class(pos), mf[0], mf[1], mf[2]), f, qbits);
                 any |= c[k] != 0;
             }
         }
@@ -77,8 +77,8 @@ SK_HD int quant_luma(const MbTransform& t, int qp, bool intra16, int16_t* coef, 
             int blk = b8 * 4 + i;
             int16_t* c = coef + kCoefLuma + blk * 16;
             for (int k = 0; k < 16; k++) {
-                int pos = H264_ZIGZAG4x4[k];
-                c[k] = (int16_t)quant_coef(t.wl[blk][pos], mf[H264_POS_CLASS[pos]], f, qbits);
+                int pos = zigzag4x4(k);
+                c[k] = (int16_t)quant_coef(t.wl[blk][pos], sel3(pos_class(pos), mf[0], mf[1], mf[2]), f, qbits);
             }
             score8 += decimate_score(c, 16);
         }
@@ -125,8 +125,8 @@ SK_HD int quant_chroma(const MbTransform& t, int qp, bool intra, int16_t* coef, 
             int16_t* cc = coef + kCoefChromaAC + (c * 4 + b) * 16;
             cc[0] = 0;
             for (int k = 1; k < 16; k++) {
-                int pos = H264_ZIGZAG4x4[k];
-                cc[k] = (int16_t)quant_coef(t.wc[c][b][pos], mf[H264_POS_CLASS[pos]], f, qbits);
+                int pos = zigzag4x4(k);
+                cc[k] = (int16_t)quant_coef(t.wc[c][b][pos], sel3(pos_class(pos), mf[0], mf[1], mf[2]), f, qbits);
                 comp_ac |= cc[k] != 0;
             }
             if (!intra) score += decimate_score(cc + 1, 15);
@@ -150,18 +150,18 @@ SK_HD void recon_luma(const int16_t* coef, int qp, bool intra16, int cbp_l, cons
     int dcy[16];
     if (intra16) {
         int c[16];
-        for (int k = 0; k < 16; k++) c[H264_ZIGZAG4x4[k]] = coef[kCoefLumaDC + k];
+        for (int k = 0; k < 16; k++) c[zigzag4x4(k)] = coef[kCoefLumaDC + k];
         i16_dc_dequant(c, dcy, qp);
     }
     for (int blk = 0; blk < 16; blk++) {
-        int bx = H264_BLK_X[blk], by = H264_BLK_Y[blk];
+        int bx = blk_x(blk), by = blk_y(blk);
         int d[16];
         for (int i = 0; i < 16; i++) d[i] = 0;
         const int16_t* c = coef + kCoefLuma + blk * 16;
         bool coded = intra16 ? (cbp_l != 0) : ((cbp_l >> (blk >> 2)) & 1);
         if (coded)
             for (int k = intra16 ? 1 : 0; k < 16; k++) {
-                int pos = H264_ZIGZAG4x4[k];
+                int pos = zigzag4x4(k);
                 d[pos] = dequant_coef(c[k], qp, pos);
             }
         if (intra16) d[0] = dcy[by * 4 + bx];
@@ -190,7 +190,7 @@ SK_HD void recon_chroma(const int16_t* coef, int qp, int cbp_c, const uint8_t* p
             if (cbp_c == 2) {
                 const int16_t* cc = coef + kCoefChromaAC + (c * 4 + b) * 16;
                 for (int k = 1; k < 16; k++) {
-                    int pos = H264_ZIGZAG4x4[k];
+                    int pos = zigzag4x4(k);
                     d[pos] = dequant_coef(cc[k], qpc, pos);
                 }
             }
@@ -210,7 +210,7 @@ SK_HD void recon_chroma(const int16_t* coef, int qp, int cbp_c, const uint8_t* p
 // Quantise with QP escalation so a macroblock never exceeds the A.3.1 bit limit.
 // Returns the final QP; fills mb.cbp / nnz and coef.
 SK_HD int quant_mb_with_budget(const MbTransform& t, int slice_qp, bool intra16, MbInfo& mb,
-                               int16_t* coef) {
+                               int16_t* coef, const CavlcTables& T) {
     int qp = slice_qp;
     int qp_cap = sk_min(51, slice_qp + 24);
     for (;;) {
@@ -219,7 +219,7 @@ SK_HD int quant_mb_with_budget(const MbTransform& t, int slice_qp, bool intra16,
         mb.cbp = (uint8_t)(cbp_l | (cbp_c << 4));
         mb.qp = (uint8_t)qp;
         if (qp + 6 > qp_cap) break;
-        if (mb_bits_bound(mb, coef) <= kMbBitBudget) break;
+        if (mb_bits_bound(mb, coef, T) <= kMbBitBudget) break;
         qp += 6;
     }
     return qp;

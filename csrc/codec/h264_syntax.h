@@ -49,13 +49,13 @@ struct MbNeighbours {
 
 // nC of luma block `blk` (luma4x4BlkIdx) of macroblock `cur`.
 SK_HD int luma_nc(const MbInfo& cur, MbNeighbours nb, int blk) {
-    int bx = H264_BLK_X[blk], by = H264_BLK_Y[blk];
+    int bx = blk_x(blk), by = blk_y(blk);
     bool aA, aB;
     int nA = 0, nB = 0;
-    if (bx > 0) { aA = true; nA = cur.nnz[H264_BLK_FROM_XY[by * 4 + bx - 1]]; }
-    else { aA = nb.left != nullptr; if (aA) nA = nb.left->nnz[H264_BLK_FROM_XY[by * 4 + 3]]; }
-    if (by > 0) { aB = true; nB = cur.nnz[H264_BLK_FROM_XY[(by - 1) * 4 + bx]]; }
-    else { aB = nb.top != nullptr; if (aB) nB = nb.top->nnz[H264_BLK_FROM_XY[12 + bx]]; }
+    if (bx > 0) { aA = true; nA = cur.nnz[blk_from_xy(bx - 1, by)]; }
+    else { aA = nb.left != nullptr; if (aA) nA = nb.left->nnz[blk_from_xy(3, by)]; }
+    if (by > 0) { aB = true; nB = cur.nnz[blk_from_xy(bx, by - 1)]; }
+    else { aB = nb.top != nullptr; if (aB) nB = nb.top->nnz[blk_from_xy(bx, 3)]; }
     return nc_from(aA, nA, aB, nB);
 }
 
@@ -96,56 +96,57 @@ SK_HD bool mb_has_qp_delta(const MbInfo& mb) {
 
 // residual() for one macroblock; `coef` points at the MB's kCoefPerMb levels.
 template <class W>
-SK_HD void write_mb_residual(W& w, const MbInfo& mb, MbNeighbours nb, const int16_t* coef) {
+SK_HD void write_mb_residual(W& w, const MbInfo& mb, MbNeighbours nb, const int16_t* coef,
+                             const CavlcTables& T) {
     int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
     if (mb.type == MB_I16x16) {
-        cavlc_block(w, coef + kCoefLumaDC, 16, luma_nc(mb, nb, 0));
+        cavlc_block(w, coef + kCoefLumaDC, 16, luma_nc(mb, nb, 0), T);
         if (cbp_l) {
             for (int blk = 0; blk < 16; blk++)
-                cavlc_block(w, coef + kCoefLuma + blk * 16 + 1, 15, luma_nc(mb, nb, blk));
+                cavlc_block(w, coef + kCoefLuma + blk * 16 + 1, 15, luma_nc(mb, nb, blk), T);
         }
     } else {
         for (int b8 = 0; b8 < 4; b8++) {
             if (!(cbp_l & (1 << b8))) continue;
             for (int i = 0; i < 4; i++) {
                 int blk = b8 * 4 + i;
-                cavlc_block(w, coef + kCoefLuma + blk * 16, 16, luma_nc(mb, nb, blk));
+                cavlc_block(w, coef + kCoefLuma + blk * 16, 16, luma_nc(mb, nb, blk), T);
             }
         }
     }
     if (cbp_c) {
-        cavlc_block(w, coef + kCoefChromaDC + 0, 4, -1);
-        cavlc_block(w, coef + kCoefChromaDC + 4, 4, -1);
+        cavlc_block(w, coef + kCoefChromaDC + 0, 4, -1, T);
+        cavlc_block(w, coef + kCoefChromaDC + 4, 4, -1, T);
     }
     if (cbp_c == 2) {
         for (int comp = 0; comp < 2; comp++)
             for (int b = 0; b < 4; b++)
                 cavlc_block(w, coef + kCoefChromaAC + (comp * 4 + b) * 16 + 1, 15,
-                            chroma_nc(mb, nb, comp, b));
+                            chroma_nc(mb, nb, comp, b), T);
     }
 }
 
 // Conservative (nC-independent) size bound of a coded macroblock in bits.
-SK_HD int mb_bits_bound(const MbInfo& mb, const int16_t* coef) {
+SK_HD int mb_bits_bound(const MbInfo& mb, const int16_t* coef, const CavlcTables& T) {
     int bits = 96;  // mb_type, pred modes, mvd, cbp, qp_delta, skip_run: generous
     int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
     if (mb.type == MB_I16x16) {
-        bits += cavlc_block_bits_bound(coef + kCoefLumaDC, 16);
+        bits += cavlc_block_bits_bound(coef + kCoefLumaDC, 16, T);
         if (cbp_l)
             for (int blk = 0; blk < 16; blk++)
-                bits += cavlc_block_bits_bound(coef + kCoefLuma + blk * 16 + 1, 15);
+                bits += cavlc_block_bits_bound(coef + kCoefLuma + blk * 16 + 1, 15, T);
     } else {
         for (int blk = 0; blk < 16; blk++)
-            if (cbp_l & (1 << (blk >> 2))) bits += cavlc_block_bits_bound(coef + kCoefLuma + blk * 16, 16);
+            if (cbp_l & (1 << (blk >> 2))) bits += cavlc_block_bits_bound(coef + kCoefLuma + blk * 16, 16, T);
     }
     if (cbp_c) {
         BitCounter bc;
-        cavlc_block(bc, coef + kCoefChromaDC, 4, -1);
-        cavlc_block(bc, coef + kCoefChromaDC + 4, 4, -1);
+        cavlc_block(bc, coef + kCoefChromaDC, 4, -1, T);
+        cavlc_block(bc, coef + kCoefChromaDC + 4, 4, -1, T);
         bits += bc.n;
     }
     if (cbp_c == 2)
-        for (int b = 0; b < 8; b++) bits += cavlc_block_bits_bound(coef + kCoefChromaAC + b * 16 + 1, 15);
+        for (int b = 0; b < 8; b++) bits += cavlc_block_bits_bound(coef + kCoefChromaAC + b * 16 + 1, 15, T);
     return bits;
 }
 

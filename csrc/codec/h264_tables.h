@@ -47,6 +47,12 @@ SK_TABLE uint8_t H264_COEFF_TOKEN_MAXLEN[68] = {
     13, 13, 11, 9, 13, 13, 13, 10, 14, 14, 13, 11, 14, 14, 14, 13, 15, 15, 14, 14, 15, 15,
     15, 14, 16, 15, 15, 15, 16, 16, 16, 15, 16, 16, 16, 16, 16, 16, 16, 16};
 
+// Longest coeff_token (any nC table, any TrailingOnes) per TotalCoeff, and longest
+// total_zeros code per TotalCoeff (derived from the tables above; used only for
+// conservative size bounds).
+SK_TABLE uint8_t H264_CT_MAX_TC[17] = {6, 6, 8, 9, 10, 11, 13, 13, 13, 14, 14, 15, 15, 16, 16, 16, 16};
+SK_TABLE uint8_t H264_TZ_MAX_TC[16] = {0, 9, 6, 6, 5, 5, 6, 6, 6, 6, 5, 4, 4, 3, 2, 1};
+
 // ---- total_zeros (Tables 9-7, 9-8), index [TotalCoeff-1][total_zeros] -------
 SK_TABLE uint8_t H264_TOTAL_ZEROS_LEN[15][16] = {
     {1, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 9},
@@ -117,6 +123,14 @@ SK_TABLE uint8_t H264_BLK_Y[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 
 // (y*4 + x) -> luma4x4BlkIdx
 SK_TABLE uint8_t H264_BLK_FROM_XY[16] = {0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15};
 
+// Arithmetic forms of the small per-position tables above (no memory access on
+// the GPU; lane-dependent table indices would otherwise become vector loads).
+SK_HD int zigzag4x4(int k) { return (int)((0xfeb7adc963258410ULL >> (4 * k)) & 15); }
+SK_HD int inv_zigzag4x4(int r) { return (int)((0xfea9db83c7426510ULL >> (4 * r)) & 15); }
+SK_HD int blk_x(int b) { return (b & 1) | (((b >> 2) & 1) << 1); }
+SK_HD int blk_y(int b) { return ((b >> 1) & 1) | (((b >> 3) & 1) << 1); }
+SK_HD int blk_from_xy(int x, int y) { return (x & 1) | ((y & 1) << 1) | ((x >> 1) << 2) | ((y >> 1) << 3); }
+
 // ---- quantisation ------------------------------------------------------------
 // Forward quant multipliers MF[qp%6][class]; class 0: (even,even) positions,
 // 1: (odd,odd), 2: mixed.
@@ -144,3 +158,38 @@ SK_TABLE uint8_t H264_CBP_TO_CODE_INTER[48] = {
     0,  2,  3,  7,  4,  8,  17, 13, 5,  18, 9,  14, 10, 15, 16, 11,
     1,  32, 33, 36, 34, 37, 44, 40, 35, 45, 38, 41, 39, 42, 43, 19,
     6,  24, 25, 20, 26, 21, 46, 28, 27, 47, 22, 29, 23, 30, 31, 12};
+
+// ---- VLC tables as one POD block: copied into LDS by the GPU kernels so that
+// per-lane (divergent) lookups are LDS reads, not dependent global loads.
+struct CavlcTables {
+    uint8_t ct_len[4][68], ct_code[4][68];
+    uint8_t cdc_len[20], cdc_code[20];
+    uint8_t tz_len[15][16], tz_code[15][16];
+    uint8_t cdc_tz_len[3][4], cdc_tz_code[3][4];
+    uint8_t rb_len[7][16], rb_code[7][16];
+    uint8_t ct_maxlen[68];
+    uint8_t ct_max_tc[17], tz_max_tc[16];
+    uint8_t pad[11];
+};
+
+SK_HD void cavlc_tables_copy_range(CavlcTables& t, int begin, int step) {
+    uint8_t* d = reinterpret_cast<uint8_t*>(&t);
+    for (int i = begin; i < (int)sizeof(CavlcTables); i += step) {
+        uint8_t v = 0;
+        int k = i;
+#define SK_CP(arr)                                                   \
+    if (k >= 0 && k < (int)sizeof(arr)) v = (&arr[0][0])[k];         \
+    k -= (int)sizeof(arr);
+#define SK_CP1(arr)                                                  \
+    if (k >= 0 && k < (int)sizeof(arr)) v = arr[k];                  \
+    k -= (int)sizeof(arr);
+        SK_CP(H264_COEFF_TOKEN_LEN) SK_CP(H264_COEFF_TOKEN_CODE) SK_CP1(H264_CDC_COEFF_TOKEN_LEN)
+        SK_CP1(H264_CDC_COEFF_TOKEN_CODE) SK_CP(H264_TOTAL_ZEROS_LEN) SK_CP(H264_TOTAL_ZEROS_CODE)
+        SK_CP(H264_CDC_TOTAL_ZEROS_LEN) SK_CP(H264_CDC_TOTAL_ZEROS_CODE) SK_CP(H264_RUN_BEFORE_LEN)
+        SK_CP(H264_RUN_BEFORE_CODE) SK_CP1(H264_COEFF_TOKEN_MAXLEN)
+        SK_CP1(H264_CT_MAX_TC) SK_CP1(H264_TZ_MAX_TC)
+#undef SK_CP
+#undef SK_CP1
+        d[i] = v;
+    }
+}

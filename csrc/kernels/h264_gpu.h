@@ -45,6 +45,7 @@ struct FrameArgs {
     uint8_t* host_out;     // host-mapped compacted packet buffer (k_gather)
     const int* frame_params;  // device: [0] = frame_id
     int first_frame;
+    unsigned long long* dbg;  // optional s_memtime stamps (SK_STAMPS=1), else nullptr
 };
 
 void launch_convert_damage(const FrameArgs& a, hipStream_t s);

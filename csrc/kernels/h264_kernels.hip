@@ -35,9 +35,24 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Full-wave sum with DPP (quad swaps + row rotations) and 4 readlanes; every
+// lane must be active. Result is wave-uniform.
 __device__ __forceinline__ int wave_sum(int v) {
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+           __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+}
+
+__device__ __forceinline__ int wave_incl_scan_max(int v) {
+    int l = threadIdx.x & 63;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o);
+        if (l >= o) v = max(v, t);
+    }
     return v;
 }
 
@@ -106,6 +121,22 @@ __device__ __forceinline__ void inv4_quad(const int* d, int r, int* res) {
         res[j] = (o + 32) >> 6;
     }
 }
+
+// Diagnostic stamp: wave 0 of block 0 records s_memtime at numbered points.
+#ifdef SK_STAMPS
+__device__ __forceinline__ void stamp(unsigned long long* dbg, int step, int point) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    if (dbg && blockIdx.x == 0 && threadIdx.x == 0 && step < 64) dbg[step * 16 + point] = t;
+}
+#define STAMP(step, pt) stamp(a.dbg, step, pt)
+#define STAMP_S(dbg, step, pt) stamp(dbg, step, pt)
+#else
+#define STAMP(step, pt)
+#define STAMP_S(dbg, step, pt)
+#endif
 
 // Big-endian-in-word bit writer on a shared/global u32 buffer (atomicOr, so
 // several lanes may write disjoint bit ranges concurrently).
@@ -281,6 +312,10 @@ __global__ void k_decide(FrameArgs a) {
     if (t.action == ACT_P && t.allow_scenecut && a.slice_sums[2 * s] > a.slice_sums[2 * s + 1])
         fin = ACT_I;
     t.final_action = fin;
+    // self-cleaning accumulators for the next frame
+    a.slice_sums[2 * s] = 0;
+    a.slice_sums[2 * s + 1] = 0;
+    a.stripe_dirty[s] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -291,28 +326,98 @@ struct MbScratch {                 // per-wave LDS
     int dcc[8];                    // chroma raw DC then dequantised DC
     int blk_stat[32];              // per-lane scratch
     int misc[8];
+    uint8_t nnz[24];               // TotalCoeff per block (luma blkIdx, Cb, Cr)
+    uint8_t pad[8];
+    int cdcp[8];                   // chroma DC predictions [comp][block]
 };
 
+// In-place 4x4 Hadamard H*X*H of a raster int[16] in LDS: rows by lanes 0..3,
+// then columns by lanes 0..3 (3 LDS round trips instead of 16 serial reads).
+__device__ __forceinline__ void lds_hadamard4x4(int* x) {
+    const int l = lane_id();
+    if (l < 4) {
+        int a = x[l * 4 + 0], b = x[l * 4 + 1], c = x[l * 4 + 2], d = x[l * 4 + 3];
+        int s01 = a + b, d01 = a - b, s23 = c + d, d23 = c - d;
+        x[l * 4 + 0] = s01 + s23;
+        x[l * 4 + 1] = s01 - s23;
+        x[l * 4 + 2] = d01 - d23;
+        x[l * 4 + 3] = d01 + d23;
+    }
+    wave_sync();
+    if (l < 4) {
+        int a = x[l], b = x[4 + l], c = x[8 + l], d = x[12 + l];
+        int s01 = a + b, d01 = a - b, s23 = c + d, d23 = c - d;
+        x[l] = s01 + s23;
+        x[4 + l] = s01 - s23;
+        x[8 + l] = d01 - d23;
+        x[12 + l] = d01 + d23;
+    }
+    wave_sync();
+}
+
+// Upper bound of the CAVLC bits of one non-zero level of magnitude a, over every
+// suffixLength the block can reach (<= sl_max, 9.2.2.1). With per-TotalCoeff
+// maxima for coeff_token / total_zeros and a 3n+8 bound on run_before this
+// dominates the exact nC-free bound, so bound <= budget implies exact <= budget.
+__device__ __forceinline__ int level_bits_bound(int a, int sl_max) {
+    int lc = 2 * a - 1;
+    int best = lc < 14 ? lc + 1 : (lc < 30 ? 19 : 28);
+#pragma unroll
+    for (int sl = 1; sl <= 6; sl++) {
+        int bsl = lc < (15 << sl) ? (lc >> sl) + 1 + sl : 28;
+        if (sl <= sl_max) best = sk_max(best, bsl);
+    }
+    return best;
+}
+__device__ __forceinline__ int suffix_len_cap(int maxabs) {
+    return sk_min(6, 1 + (maxabs > 3) + (maxabs > 6) + (maxabs > 12) + (maxabs > 24) + (maxabs > 48));
+}
+__device__ __forceinline__ int quad_max(int v) {
+    v = sk_max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
+    v = sk_max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
+    return v;
+}
+
+// Sum across the 4 lanes of a quad (DPP), result in every lane of the quad.
+__device__ __forceinline__ int quad_sum(int v) {
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+    return v;
+}
+
 // Per-lane quantisation of this lane's luma row and chroma row into LDS, then the
-// same analysis as quant_luma / quant_chroma of the CPU path. Returns cbp.
+// same analysis as quant_luma / quant_chroma of the CPU path. Returns cbp and
+// writes per-block TotalCoeff into S.nnz. The MB size check first uses a
+// lane-parallel conservative bound and only runs the exact (nC-free) CAVLC bound
+// of mb_bits_bound when that one exceeds the budget: same decisions as the CPU.
 __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16, MbScratch& S,
-                              int* bound_out) {
+                              int* bound_out, const CavlcTables& T, unsigned long long* dbg = nullptr,
+                              int step = 0) {
     const int l = lane_id();
     const int b = l >> 2, r = l & 3;
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    const uint32_t izz_row = r == 0 ? 0x06050100u : (r == 1 ? 0x0C070402u : (r == 2 ? 0x0D0B0803u : 0x0F0E0A09u));
+    int ln_l = 0, lc_l = 0;   // luma: non-zero count and bound bits of this lane's row
+    int ln_c = 0, lc_c = 0;   // chroma AC row
+    int lvl[4], lvc[4];       // this lane's quantised levels (|.|) for the bound
+    int lastl = -1, lastc = -1;  // highest scan position holding a non-zero level
     // ---- luma ----
     {
         int qbits = 15 + qp / 6;
         int f = quant_f(qbits, intra16);
         const int* mf = H264_QUANT_MF[qp % 6];
+        int m0 = mf[0], m1 = mf[1], m2 = mf[2];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             int pos = r * 4 + j;
-            int lv = quant_coef(wl[j], mf[H264_POS_CLASS[pos]], f, qbits);
+            int lv = quant_coef(wl[j], sel3(pos_class(pos), m0, m1, m2), f, qbits);
             if (intra16 && pos == 0) lv = 0;
-            S.coef[kCoefLuma + b * 16 + H264_INV_ZIGZAG4x4[pos]] = (int16_t)lv;
+            S.coef[kCoefLuma + b * 16 + ((izz_row >> (8 * j)) & 255)] = (int16_t)lv;
+            lvl[j] = sk_abs(lv);
+            ln_l += lv != 0;
+            if (lv) lastl = sk_max(lastl, (int)((izz_row >> (8 * j)) & 255));
         }
-        if (intra16 && r == 0) S.dcy[H264_BLK_Y[b] * 4 + H264_BLK_X[b]] = wl[0];
+        if (intra16 && r == 0) S.dcy[blk_y(b) * 4 + blk_x(b)] = wl[0];
         if (!intra16 && l < 16) S.coef[kCoefLumaDC + l] = 0;
     }
     // ---- chroma ----
@@ -321,31 +426,48 @@ __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16
         int qbits = 15 + qpc / 6;
         int f = quant_f(qbits, intra16);
         const int* mf = H264_QUANT_MF[qpc % 6];
-        if (l < 32) {
+        int m0 = mf[0], m1 = mf[1], m2 = mf[2];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                int pos = r * 4 + j;
-                int lv = pos == 0 ? 0 : quant_coef(wc[j], mf[H264_POS_CLASS[pos]], f, qbits);
-                S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + H264_INV_ZIGZAG4x4[pos]] = (int16_t)lv;
-            }
-            if (r == 0) S.dcc[comp * 4 + cb] = wc[0];
+        for (int j = 0; j < 4; j++) {
+            int pos = r * 4 + j;
+            int lv = pos == 0 ? 0 : quant_coef(wc[j], sel3(pos_class(pos), m0, m1, m2), f, qbits);
+            if (l < 32) S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + ((izz_row >> (8 * j)) & 255)] = (int16_t)lv;
+            lvc[j] = sk_abs(lv);
+            ln_c += lv != 0;
+            if (lv) lastc = sk_max(lastc, (int)((izz_row >> (8 * j)) & 255));
         }
+        if (l < 32 && r == 0) S.dcc[comp * 4 + cb] = wc[0];
     }
+    STAMP_S(dbg, step, 9);
+    {
+        int sl_l = suffix_len_cap(quad_max(sk_max(sk_max(lvl[0], lvl[1]), sk_max(lvl[2], lvl[3]))));
+        int sl_c = suffix_len_cap(quad_max(sk_max(sk_max(lvc[0], lvc[1]), sk_max(lvc[2], lvc[3]))));
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (lvl[j]) lc_l += level_bits_bound(lvl[j], sl_l);
+            if (lvc[j]) lc_c += level_bits_bound(lvc[j], sl_c);
+        }
+        lastl = quad_max(lastl);
+        lastc = quad_max(lastc);
+    }
+    int bn_l = quad_sum(ln_l), bc_l = quad_sum(lc_l);   // per luma block
+    int bn_c = quad_sum(ln_c), bc_c = quad_sum(lc_c);   // per chroma block (lanes < 32)
     wave_sync();
     // I16 luma DC: Hadamard + quant (lanes 0..15 = raster positions)
-    if (intra16 && l < 16) {
-        int qbits = 15 + qp / 6;
-        int f = quant_f(qbits, true);
-        int mf0 = H264_QUANT_MF[qp % 6][0];
-        int row = l >> 2, col = l & 3;
-        const int H4[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
-        int acc = 0;
-        for (int p = 0; p < 4; p++)
-            for (int q = 0; q < 4; q++) acc += H4[row][p] * S.dcy[p * 4 + q] * H4[q][col];
-        S.coef[kCoefLumaDC + H264_INV_ZIGZAG4x4[l]] =
-            (int16_t)quant_coef(i16_dc_fwd_round(acc), mf0, 2 * f, qbits + 1);
+    int dc_crude = 0, dc_nz = 0;
+    if (intra16) {
+        lds_hadamard4x4(S.dcy);
+        if (l < 16) {
+            int qbits = 15 + qp / 6;
+            int f = quant_f(qbits, true);
+            int mf0 = H264_QUANT_MF[qp % 6][0];
+            int lv = quant_coef(i16_dc_fwd_round(S.dcy[l]), mf0, 2 * f, qbits + 1);
+            S.coef[kCoefLumaDC + inv_zigzag4x4(l)] = (int16_t)lv;
+            if (lv) { dc_nz = 1; dc_crude = level_bits_bound(sk_abs(lv), 6) + 3; }
+        }
     }
     // chroma DC 2x2 Hadamard + quant (lanes 0..7 = comp*4 + i)
+    int cdc_crude = 0, cdc_nz = 0;
     if (l < 8) {
         int c = l >> 2, i = l & 3;
         int qbits = 15 + qpc / 6;
@@ -353,30 +475,19 @@ __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16
         int mf0 = H264_QUANT_MF[qpc % 6][0];
         int d0 = S.dcc[c * 4 + 0], d1 = S.dcc[c * 4 + 1], d2 = S.dcc[c * 4 + 2], d3 = S.dcc[c * 4 + 3];
         int v = i == 0 ? d0 + d1 + d2 + d3 : (i == 1 ? d0 - d1 + d2 - d3 : (i == 2 ? d0 + d1 - d2 - d3 : d0 - d1 - d2 + d3));
-        S.coef[kCoefChromaDC + c * 4 + i] = (int16_t)quant_coef(v, mf0, 2 * f, qbits + 1);
+        int lv = quant_coef(v, mf0, 2 * f, qbits + 1);
+        S.coef[kCoefChromaDC + c * 4 + i] = (int16_t)lv;
+        if (lv) { cdc_nz = 1; cdc_crude = level_bits_bound(sk_abs(lv), 6) + 3; }
     }
     wave_sync();
-    // ---- analysis: lanes 0..15 luma blocks, 16..23 chroma AC blocks ----
-    int score = 0, nz = 0, anyc = 0;
-    if (l < 16) {
-        const int16_t* c = S.coef + kCoefLuma + l * 16;
-        if (intra16) {
-            nz = count_nonzero(c + 1, 15);
-        } else {
-            score = decimate_score(c, 16);
-            nz = count_nonzero(c, 16);
-        }
-    } else if (l < 24) {
-        const int16_t* c = S.coef + kCoefChromaAC + (l - 16) * 16;
-        nz = count_nonzero(c + 1, 15);
-        if (!intra16) score = decimate_score(c + 1, 15);
-    }
+    STAMP_S(dbg, step, 10);
+    // ---- cbp analysis ----
     int cbp_l;
     if (intra16) {
-        unsigned long long m = __ballot(l < 16 && nz > 0);
-        cbp_l = m ? 15 : 0;
+        cbp_l = __ballot(bn_l > 0) ? 15 : 0;
     } else {
-        // 8x8 scores: sum of 4 consecutive lanes 0..15
+        // decimation scores (sequential per block, lanes 0..15)
+        int score = l < 16 ? decimate_score(S.coef + kCoefLuma + l * 16, 16) : 0;
         int s4 = score + __shfl_down(score, 1) + __shfl_down(score, 2) + __shfl_down(score, 3);
         int sc8[4];
 #pragma unroll
@@ -388,17 +499,15 @@ __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16
             if (sc8[k] >= 4) cbp_l |= 1 << k;
         if (mb_score < 6) cbp_l = 0;
     }
-    // chroma: per component decimation (inter), cbp chroma
-    int chroma_score[2], comp_ac[2];
+    // chroma: per component decimation (inter), cbp chroma; block b of lanes 4b..4b+3
+    int comp_ac[2], chroma_score[2];
     {
-        int sc = (l >= 16 && l < 24) ? score : 0;
-        int ac = (l >= 16 && l < 24 && nz > 0) ? 1 : 0;
+        int cscore = 0;
+        if (!intra16 && l < 8) cscore = decimate_score(S.coef + kCoefChromaAC + l * 16 + 1, 15);
 #pragma unroll
         for (int c = 0; c < 2; c++) {
-            int v = (l >= 16 + 4 * c && l < 20 + 4 * c) ? sc : 0;
-            int w = (l >= 16 + 4 * c && l < 20 + 4 * c) ? ac : 0;
-            chroma_score[c] = wave_sum(v);
-            comp_ac[c] = wave_sum(w) > 0;
+            comp_ac[c] = __ballot(l >= 16 * c && l < 16 * c + 16 && bn_c > 0) != 0ull;
+            chroma_score[c] = wave_sum((l >= 4 * c && l < 4 * c + 4) ? cscore : 0);
         }
     }
     bool zero_comp[2];
@@ -407,31 +516,72 @@ __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16
         zero_comp[c] = !intra16 && comp_ac[c] && chroma_score[c] < 7;
         if (zero_comp[c]) comp_ac[c] = 0;
     }
-    bool any_dc = __ballot(l < 8 && S.coef[kCoefChromaDC + (l & 7)] != 0) != 0ull;
+    bool any_dc = __ballot(cdc_nz != 0) != 0ull;
     int cbp_c = (comp_ac[0] || comp_ac[1]) ? 2 : (any_dc ? 1 : 0);
-    // zero out decimated blocks
-    if (l < 16 && !intra16 && !(cbp_l & (1 << (l >> 2)))) {
-        for (int k = 0; k < 16; k++) S.coef[kCoefLuma + l * 16 + k] = 0;
-        nz = 0;
+    // zero decimated blocks (LDS) and their counts
+    bool luma_coded = intra16 ? (cbp_l != 0) : ((cbp_l >> (b >> 2)) & 1);
+    if (!intra16 && !luma_coded) {
+        if (r == 0) {
+            for (int k = 0; k < 16; k++) S.coef[kCoefLuma + b * 16 + k] = 0;
+        }
+        bn_l = 0;
+        bc_l = 0;
     }
-    if (l >= 16 && l < 24 && zero_comp[(l - 16) >> 2]) {
-        for (int k = 0; k < 16; k++) S.coef[kCoefChromaAC + (l - 16) * 16 + k] = 0;
-        nz = 0;
+    if (l < 32 && zero_comp[comp]) {
+        if (r == 0)
+            for (int k = 0; k < 16; k++) S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + k] = 0;
+        bn_c = 0;
+        bc_c = 0;
     }
+    // TotalCoeff per block for nC (written by the quad leader)
+    if (r == 0) S.nnz[b] = luma_coded ? (uint8_t)bn_l : 0;
+    if (l < 32 && r == 0) S.nnz[16 + comp * 4 + cb] = cbp_c == 2 ? (uint8_t)bn_c : 0;
+    STAMP_S(dbg, step, 11);
+    // ---- size check: conservative bound first ----
+    // block bound: longest coeff_token for n, exact total_zeros code, run_before
+    // <= 2/3 bits per coefficient while zerosLeft <= 2/6 (+8 beyond), level bounds
+    auto block_bound = [&](int n, int last, int maxn, int lvbits) {
+        if (n == 0) return 6;
+        int tz = (maxn == 16 ? last + 1 : last) - n;  // AC blocks (15) start at scan index 1
+        int b = T.ct_max_tc[n] + lvbits;
+        if (n < maxn) b += T.tz_len[n - 1][tz];
+        if (n > 1 && tz > 0) b += tz <= 2 ? 2 * (n - 1) : (tz <= 6 ? 3 * (n - 1) : 3 * (n - 1) + 8);
+        return b;
+    };
+    const int lmax = intra16 ? 15 : 16;
+    int crude = 0;
+    if (r == 0) {
+        if (luma_coded) crude += block_bound(bn_l, lastl, lmax, bc_l);
+        if (l < 32 && cbp_c == 2) crude += block_bound(bn_c, lastc, 15, bc_c);
+    }
+    int dc_sum_n = wave_sum(dc_nz), dc_sum_c = wave_sum(dc_crude);
+    int cdc_sum_c = wave_sum(cdc_crude), cdc_sum_n0 = wave_sum(l < 4 ? cdc_nz : 0),
+        cdc_sum_n1 = wave_sum(l >= 4 && l < 8 ? cdc_nz : 0);
+    int total_crude = 96 + wave_sum(crude);
+    if (intra16)
+        total_crude += dc_sum_n > 0 ? T.ct_max_tc[dc_sum_n] + (dc_sum_n < 16 ? T.tz_max_tc[dc_sum_n] : 0) + 8 + dc_sum_c : 6;
+    // chroma DC: coeff_token <= 8, total_zeros <= 3, run_before <= 2 per coefficient
+    if (cbp_c) total_crude += (cdc_sum_n0 > 0 ? 11 : 2) + (cdc_sum_n1 > 0 ? 11 : 2) + cdc_sum_c;
     wave_sync();
-    // size bound (same terms as mb_bits_bound)
+    STAMP_S(dbg, step, 12);
+    if (dbg && blockIdx.x == 0 && threadIdx.x == 0 && step < 64) dbg[step * 16 + 14] = total_crude;
+    if (total_crude <= kMbBitBudget) {
+        *bound_out = total_crude;
+        return cbp_l | (cbp_c << 4);
+    }
+    // ---- exact bound (same terms as mb_bits_bound) ----
     int bnd = 0;
     if (l < 16) {
-        if (intra16) { if (cbp_l) bnd = cavlc_block_bits_bound(S.coef + kCoefLuma + l * 16 + 1, 15); }
-        else if (cbp_l & (1 << (l >> 2))) bnd = cavlc_block_bits_bound(S.coef + kCoefLuma + l * 16, 16);
+        if (intra16) { if (cbp_l) bnd = cavlc_block_bits_bound(S.coef + kCoefLuma + l * 16 + 1, 15, T); }
+        else if (cbp_l & (1 << (l >> 2))) bnd = cavlc_block_bits_bound(S.coef + kCoefLuma + l * 16, 16, T);
     } else if (l < 24) {
-        if (cbp_c == 2) bnd = cavlc_block_bits_bound(S.coef + kCoefChromaAC + (l - 16) * 16 + 1, 15);
+        if (cbp_c == 2) bnd = cavlc_block_bits_bound(S.coef + kCoefChromaAC + (l - 16) * 16 + 1, 15, T);
     } else if (l == 24) {
-        if (intra16) bnd = cavlc_block_bits_bound(S.coef + kCoefLumaDC, 16);
+        if (intra16) bnd = cavlc_block_bits_bound(S.coef + kCoefLumaDC, 16, T);
     } else if (l == 25 || l == 26) {
         if (cbp_c) {
             BitCounter bc;
-            cavlc_block(bc, S.coef + kCoefChromaDC + (l - 25) * 4, 4, -1);
+            cavlc_block(bc, S.coef + kCoefChromaDC + (l - 25) * 4, 4, -1, T);
             bnd = bc.n;
         }
     }
@@ -447,18 +597,17 @@ __device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, cons
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
     int cbp_l = cbp & 15, cbp_c = (cbp >> 4) & 3;
     int qpc = chroma_qp(qp);
-    // DC dequant: lanes 0..15 luma (I16), lanes 16..17 chroma components
-    if (intra16 && l < 16) {
-        int row = l >> 2, col = l & 3;
-        const int H4[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
-        int acc = 0;
-        for (int p = 0; p < 4; p++)
-            for (int q = 0; q < 4; q++)
-                acc += H4[row][p] * S.coef[kCoefLumaDC + H264_INV_ZIGZAG4x4[p * 4 + q]] * H4[q][col];
-        int ls = 16 * H264_DEQUANT_V[qp % 6][0];
-        int q6 = qp / 6;
-        int v = qp >= 36 ? (acc * ls) << (q6 - 6) : (acc * ls + (1 << (5 - q6))) >> (6 - q6);
-        S.blk_stat[l] = v;  // raster position l
+    // DC dequant: luma (I16) via the LDS Hadamard, lanes 16..17 chroma components
+    if (intra16) {
+        if (l < 16) S.blk_stat[l] = S.coef[kCoefLumaDC + inv_zigzag4x4(l)];
+        wave_sync();
+        lds_hadamard4x4(S.blk_stat);
+        if (l < 16) {
+            int ls = 16 * H264_DEQUANT_V[qp % 6][0];
+            int q6 = qp / 6;
+            int acc = S.blk_stat[l];
+            S.blk_stat[l] = qp >= 36 ? (acc * ls) << (q6 - 6) : (acc * ls + (1 << (5 - q6))) >> (6 - q6);
+        }
     }
     if (l >= 16 && l < 18) {
         int c = l - 16;
@@ -475,10 +624,10 @@ __device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, cons
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             int pos = r * 4 + j;
-            int lv = S.coef[kCoefLuma + b * 16 + H264_INV_ZIGZAG4x4[pos]];
+            int lv = S.coef[kCoefLuma + b * 16 + inv_zigzag4x4(pos)];
             d[j] = coded ? dequant_coef(lv, qp, pos) : 0;
         }
-        if (intra16 && r == 0) d[0] = S.blk_stat[H264_BLK_Y[b] * 4 + H264_BLK_X[b]];
+        if (intra16 && r == 0) d[0] = S.blk_stat[blk_y(b) * 4 + blk_x(b)];
         int res[4];
         inv4_quad(d, r, res);
 #pragma unroll
@@ -490,7 +639,7 @@ __device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, cons
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             int pos = r * 4 + j;
-            int lv = S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + H264_INV_ZIGZAG4x4[pos]];
+            int lv = S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + inv_zigzag4x4(pos)];
             d[j] = (cbp_c == 2 && pos != 0) ? dequant_coef(lv, qpc, pos) : 0;
         }
         if (r == 0) d[0] = S.blk_stat[16 + comp * 4 + cb];
@@ -505,7 +654,8 @@ __device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, cons
 // src/pred of its luma row (4 px) and chroma row. Writes coefs + MbInfo fields.
 __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, const int* pred_c,
                        int slice_qp, bool intra16, MbScratch& S, MbInfo& mb, int* rec_l, int* rec_c,
-                       int16_t* gcoef) {
+                       int16_t* gcoef, const CavlcTables& T, unsigned long long* dbg = nullptr,
+                       int step = 0) {
     const int l = lane_id();
     const int r = l & 3;
     int x[4], wl[4], wc[4];
@@ -518,16 +668,20 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
     int qp = slice_qp;
     int cap = sk_min(51, slice_qp + 24);
     int cbp = 0;
+    STAMP_S(dbg, step, 3);
     for (;;) {
         int bound;
-        cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound);
+        cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound, T, dbg, step);
+        if (dbg && blockIdx.x == 0 && threadIdx.x == 0 && step < 64) dbg[step * 16 + 15] = (dbg[step * 16 + 15] & 0xffff) + 1 + ((unsigned long long)bound << 32);
         if (qp + 6 > cap || bound <= kMbBitBudget) break;
         qp += 6;
         wave_sync();
     }
+    STAMP_S(dbg, step, 4);
     mb.cbp = (uint8_t)cbp;
     mb.qp = (uint8_t)qp;
     recon_mb_lanes(qp, intra16, cbp, S, pred_l, pred_c, rec_l, rec_c);
+    STAMP_S(dbg, step, 5);
     // copy levels to global (816 B = 204 words)
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(S.coef);
     uint32_t* g32 = reinterpret_cast<uint32_t*>(gcoef);
@@ -539,7 +693,6 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
 // K6 inter: one wave per MB of a P slice (SKIPALL slices just record skips).
 __global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
     __shared__ MbScratch S;
-    __shared__ uint8_t nnz[24];
     int nmb = a.mb_w * a.mb_h;
     int idx = xcd_remap(blockIdx.x, gridDim.x);
     if (idx >= nmb) return;
@@ -558,6 +711,9 @@ __global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
         return;
     }
     if (t.final_action != ACT_P) return;
+    __shared__ CavlcTables T;
+    cavlc_tables_copy_range(T, l, 64);
+    __syncthreads();
     // MV prediction from the final motion field (all MBs of a P slice are inter)
     auto nbr = [&](int ox, int oy, bool ok) {
         MvNb n;
@@ -581,7 +737,7 @@ __global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
     int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
     // luma source + integer MC prediction
-    int px = mbx * 16 + H264_BLK_X[b] * 4, py = mby * 16 + H264_BLK_Y[b] * 4 + r;
+    int px = mbx * 16 + blk_x(b) * 4, py = mby * 16 + blk_y(b) * 4 + r;
     uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
     int sy = sk_clip(py + (mvy >> 2), ylo, yhi);
     uint32_t pw = load_ref4(a.ref.y + (size_t)sy * a.stride_y, px + (mvx >> 2), a.stride_y);
@@ -609,7 +765,7 @@ __global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
     mb.type = MB_P_16x16;
     int rec_l[4], rec_c[4];
     code_mb(src_l, pred_l, src_c, pred_c, t.qp, false, S, mb, rec_l, rec_c,
-            a.coefs + (size_t)idx * kCoefPerMb);
+            a.coefs + (size_t)idx * kCoefPerMb, T);
     // recon
     uint32_t rw = (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) |
                   ((uint32_t)rec_l[3] << 24);
@@ -620,13 +776,6 @@ __global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
                       ((uint32_t)rec_c[3] << 24);
         *reinterpret_cast<uint32_t*>(cr + (size_t)cy0 * a.stride_c + cx0) = cw;
     }
-    // nnz was written by quant_mb_lanes into a per-lane register path; recompute from LDS
-    int nz = 0;
-    int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
-    if (l < 16) nz = (cbp_l & (1 << (l >> 2))) ? count_nonzero(S.coef + kCoefLuma + l * 16, 16) : 0;
-    else if (l < 24) nz = cbp_c == 2 ? count_nonzero(S.coef + kCoefChromaAC + (l - 16) * 16 + 1, 15) : 0;
-    if (l < 24) nnz[l] = (uint8_t)nz;
-    wave_sync();
     if (l == 0) {
         mb.mvx = (int16_t)mvx;
         mb.mvy = (int16_t)mvy;
@@ -636,7 +785,7 @@ __global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
             mb.mvdx = (int16_t)(mvx - pmx);
             mb.mvdy = (int16_t)(mvy - pmy);
         }
-        for (int i = 0; i < 24; i++) mb.nnz[i] = nnz[i];
+        for (int i = 0; i < 24; i++) mb.nnz[i] = S.nnz[i];
         a.mbs[idx] = mb;
     }
 }
@@ -652,10 +801,15 @@ struct IntraEdges {
     uint8_t right_c[kMaxRows][2][8];
 };
 
-__global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
-    __shared__ MbScratch Sw[kMaxRows];
+template <int MAXROWS>
+__global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
+    __shared__ MbScratch Sw[MAXROWS];
     __shared__ IntraEdges E;
-    __shared__ uint8_t nnz_sh[kMaxRows][24];
+    __shared__ uint8_t zero16[16];
+    __shared__ CavlcTables T;
+    if (threadIdx.x < 16) zero16[threadIdx.x] = 0;
+    cavlc_tables_copy_range(T, threadIdx.x, blockDim.x);
+    __syncthreads();
     int s = blockIdx.x;
     const SliceTask t = a.tasks[s];
     if (t.final_action != ACT_I) return;
@@ -670,20 +824,18 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
         int mbx = step - 2 * w;
         bool active = w < rows && mbx >= 0 && mbx < a.mb_w;
         if (active) {
+            STAMP(step, 0);
             int mby = t.first_row + w;
             int idx = mby * a.mb_w + mbx;
             bool aT = w > 0, aL = mbx > 0;
             const uint8_t* top = aT ? E.bot_y[w - 1][mbx & 3] : nullptr;
             const uint8_t* left = aL ? E.right_y[w] : nullptr;
             int tl = (aT && aL) ? E.bot_y[w - 1][(mbx - 1) & 3][15] : 0;
-            uint8_t zero16[16];
-#pragma unroll
-            for (int i = 0; i < 16; i++) zero16[i] = 0;
             const uint8_t* topp = aT ? top : zero16;
             const uint8_t* leftp = aL ? left : zero16;
             // luma source
-            int px = mbx * 16 + H264_BLK_X[b] * 4, py = mby * 16 + H264_BLK_Y[b] * 4 + r;
-            int lx = H264_BLK_X[b] * 4, ly = H264_BLK_Y[b] * 4 + r;
+            int px = mbx * 16 + blk_x(b) * 4, py = mby * 16 + blk_y(b) * 4 + r;
+            int lx = blk_x(b) * 4, ly = blk_y(b) * 4 + r;
             uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
             int src_l[4];
 #pragma unroll
@@ -703,6 +855,7 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
                 sad = wave_sum(sad);
                 if (sad < best_sad) { best_sad = sad; best_mode = m; }
             }
+            STAMP(step, 1);
             int pred_l[4];
 #pragma unroll
             for (int j = 0; j < 4; j++)
@@ -720,6 +873,13 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
             for (int j = 0; j < 4; j++) src_c[j] = (csw >> (8 * j)) & 255;
             int qa = 0, qb = 0, qc = 0;
             if (aT && aL) chroma_plane_params(ctop, cleft, ctl, &qa, &qb, &qc);
+            if (l < 8) {
+                const uint8_t* t8 = aT ? E.bot_c[w - 1][mbx & 3][l >> 2] : zero16;
+                const uint8_t* l8 = aL ? E.right_c[w][l >> 2] : zero16;
+                S.cdcp[l] = chroma_dc_block(l & 1, (l >> 1) & 1, t8, l8, aT, aL);
+            }
+            wave_sync();
+            const int cdc_mine = S.cdcp[comp * 4 + cb];
             int best_cm = 0, best_csad = 0x7fffffff;
             for (int m = 0; m < 4; m++) {
                 if ((m == 1 && !aL) || (m == 2 && !aT) || (m == 3 && !(aT && aL))) continue;
@@ -727,7 +887,7 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     int x = clx + j, y = cly, v;
-                    if (m == 0) v = chroma_dc_block(x >> 2, y >> 2, ctop, cleft, aT, aL);
+                    if (m == 0) v = cdc_mine;
                     else if (m == 1) v = cleft[y];
                     else if (m == 2) v = ctop[x];
                     else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
@@ -740,12 +900,13 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 int x = clx + j, y = cly, v;
-                if (best_cm == 0) v = chroma_dc_block(x >> 2, y >> 2, ctop, cleft, aT, aL);
+                if (best_cm == 0) v = cdc_mine;
                 else if (best_cm == 1) v = cleft[y];
                 else if (best_cm == 2) v = ctop[x];
                 else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
                 pred_c[j] = v;
             }
+            STAMP(step, 2);
             MbInfo mb;
             memset(&mb, 0, sizeof(mb));
             mb.type = MB_I16x16;
@@ -753,7 +914,8 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
             mb.chroma_mode = (uint8_t)best_cm;
             int rec_l[4], rec_c[4];
             code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c,
-                    a.coefs + (size_t)idx * kCoefPerMb);
+                    a.coefs + (size_t)idx * kCoefPerMb, T, a.dbg, step);
+            STAMP(step, 6);
             uint32_t rw = (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) |
                           ((uint32_t)rec_l[3] << 24);
             *reinterpret_cast<uint32_t*>(a.rec.y + (size_t)py * a.stride_y + px) = rw;
@@ -763,12 +925,6 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
                               ((uint32_t)rec_c[3] << 24);
                 *reinterpret_cast<uint32_t*>(crp + (size_t)cy0 * a.stride_c + cx0) = cw;
             }
-            // nnz
-            int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
-            int nz = 0;
-            if (l < 16) nz = cbp_l ? count_nonzero(S.coef + kCoefLuma + l * 16 + 1, 15) : 0;
-            else if (l < 24) nz = cbp_c == 2 ? count_nonzero(S.coef + kCoefChromaAC + (l - 16) * 16 + 1, 15) : 0;
-            if (l < 24) nnz_sh[w][l] = (uint8_t)nz;
             wave_sync();
             // edges for the neighbours (written after every lane has read the old ones)
             if (ly == 15)
@@ -780,13 +936,15 @@ __global__ __launch_bounds__(1024) void k_code_intra(FrameArgs a) {
                 if (clx + 3 == 7) E.right_c[w][comp][cly] = (uint8_t)rec_c[3];
             }
             if (l == 0) {
-                for (int i = 0; i < 24; i++) mb.nnz[i] = nnz_sh[w][i];
+                for (int i = 0; i < 24; i++) mb.nnz[i] = S.nnz[i];
                 a.mbs[idx] = mb;
                 a.me[idx].mvx = 0;
                 a.me[idx].mvy = 0;
             }
+            STAMP(step, 7);
         }
         __syncthreads();
+        if (w == 0) STAMP(step, 8);
     }
 }
 
@@ -808,6 +966,9 @@ __global__ __launch_bounds__(64) void k_cavlc(FrameArgs a) {
         if (l == 0) a.mb_nbits[idx] = 0;
         return;
     }
+    __shared__ CavlcTables T;
+    cavlc_tables_copy_range(T, l, 64);
+    __syncthreads();
     bool p_slice = t.final_action == ACT_P;
     int first = t.first_row * a.mb_w;
     // mb_skip_run: skipped MBs since the previous coded MB of the slice
@@ -890,14 +1051,14 @@ __global__ __launch_bounds__(64) void k_cavlc(FrameArgs a) {
     int nbits = 0;
     if (act) {
         BitCounter cnt;
-        cavlc_block(cnt, bc, maxn, nc);
+        cavlc_block(cnt, bc, maxn, nc, T);
         nbits = cnt.n;
     }
     int incl = wave_incl_scan(nbits);
     int off = hdr_bits + incl - nbits;
     if (act) {
         AtomicBitWriter w{bits, (uint32_t)off};
-        cavlc_block(w, bc, maxn, nc);
+        cavlc_block(w, bc, maxn, nc, T);
     }
     int total = hdr_bits + __shfl(incl, 63);
     wave_sync();
@@ -912,9 +1073,6 @@ __global__ __launch_bounds__(64) void k_cavlc(FrameArgs a) {
 __global__ __launch_bounds__(256) void k_assemble(FrameArgs a) {
     __shared__ uint32_t hdr[32];
     __shared__ int scan[256];
-    __shared__ int chunk_state[256][3];   // state_out for each state_in
-    __shared__ int chunk_ins[256][3];     // insertions for each state_in
-    __shared__ int chunk_in[256], chunk_off[256];
     __shared__ int sh_misc[8];
     int s = blockIdx.x;
     SliceTask& task = a.tasks[s];
@@ -1001,26 +1159,7 @@ __global__ __launch_bounds__(256) void k_assemble(FrameArgs a) {
     __threadfence();
     __syncthreads();
     const int n = sh_misc[2];
-    // ---- emulation prevention: each thread a word-aligned chunk, 3-state
-    // transfer functions composed in order, then a replay that writes bytes.
-    int C = (((n + 255) / 256) + 3) & ~3;
-    int c0 = sk_min(n, tid * C), c1 = sk_min(n, c0 + C);
-    for (int st = 0; st < 3; st++) {
-        int zeros = st, ins = 0;
-        for (int j = c0; j < c1; j += 4) {
-            uint32_t wd = __hip_atomic_load(&rbsp[j >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int lim = sk_min(4, c1 - j);
-            for (int q = 0; q < lim; q++) {
-                int bt = (int)((wd >> (24 - 8 * q)) & 255u);
-                if (zeros >= 2 && bt <= 3) { ins++; zeros = 0; }
-                zeros = bt == 0 ? sk_min(zeros + 1, 2) : 0;
-            }
-        }
-        chunk_state[tid][st] = zeros;
-        chunk_ins[tid][st] = ins;
-    }
-    __syncthreads();
-    // packet prefix
+    // ---- packet prefix (stripe header, SPS/PPS on IDR, start code, NAL header)
     uint8_t* slot = a.out + (size_t)s * a.out_slot_bytes;
     if (tid == 0) {
         int p = 0;
@@ -1045,30 +1184,80 @@ __global__ __launch_bounds__(256) void k_assemble(FrameArgs a) {
         }
         slot[p++] = 0; slot[p++] = 0; slot[p++] = 0; slot[p++] = 1;
         slot[p++] = idr ? 0x65 : 0x41;
-        int st = 0, off = p;
-        for (int k = 0; k < 256; k++) {
-            chunk_in[k] = st;
-            chunk_off[k] = off;
-            int ck0 = sk_min(n, k * C), ck1 = sk_min(n, ck0 + C);
-            off += (ck1 - ck0) + chunk_ins[k][st];
-            st = chunk_state[k][st];
-        }
-        sh_misc[3] = off;
+        sh_misc[4] = p;
     }
     __syncthreads();
-    {
-        int zeros = chunk_in[tid], o = chunk_off[tid];
-        for (int j = c0; j < c1; j += 4) {
-            uint32_t wd = __hip_atomic_load(&rbsp[j >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int lim = sk_min(4, c1 - j);
-            for (int q = 0; q < lim; q++) {
-                int bt = (int)((wd >> (24 - 8 * q)) & 255u);
-                if (zeros >= 2 && bt <= 3) { slot[o++] = 3; zeros = 0; }
-                slot[o++] = (uint8_t)bt;
-                zeros = bt == 0 ? sk_min(zeros + 1, 2) : 0;
+    // ---- emulation prevention (7.4.1): 0x03 goes before byte i iff b_i <= 3 and
+    // the run z(i) of zero bytes right before i is even and >= 2. z comes from a
+    // prefix-max of non-zero positions, output offsets from a prefix-sum of the
+    // insertions; 4 KiB tiles, 16 bytes per thread, wave scans + LDS combine.
+    const int wv = tid >> 6, ln = tid & 63;
+    int carry_nz = -1;               // last non-zero byte index before the tile (NAL header at -1)
+    int out_off = sh_misc[4];
+    for (int base = 0, it = 0; base < n; base += 4096, it++) {
+        int i0 = base + tid * 16;
+        uint32_t wd[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            wd[q] = (i0 + 4 * q < n) ? __hip_atomic_load(&rbsp[(i0 >> 2) + q], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0u;
+        int lastnz = -1;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            int bt = (int)((wd[q >> 2] >> (24 - 8 * (q & 3))) & 255u);
+            if (i0 + q < n && bt != 0) lastnz = i0 + q;
+        }
+        int incl = wave_incl_scan_max(lastnz);
+        int excl = __shfl_up(incl, 1);
+        if (ln == 0) excl = -1;
+        int* wmax = scan;              // reuse LDS: [it&1][4] maxima, [it&1][4] sums
+        int par = (it & 1) * 8;
+        if (ln == 63) wmax[par + wv] = incl;
+        __syncthreads();
+        int prev = carry_nz;
+        for (int k = 0; k < wv; k++) prev = max(prev, wmax[par + k]);
+        prev = max(prev, excl);
+        int ins = 0;
+        uint32_t insmask = 0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            int i = i0 + q;
+            int bt = (int)((wd[q >> 2] >> (24 - 8 * (q & 3))) & 255u);
+            if (i < n) {
+                int z = i - 1 - prev;
+                if (bt <= 3 && z >= 2 && !(z & 1)) { ins++; insmask |= 1u << q; }
+                if (bt != 0) prev = i;
             }
         }
+        int sincl = wave_incl_scan(ins);
+        if (ln == 63) wmax[par + 4 + wv] = sincl;
+        __syncthreads();
+        int before = sincl - ins;
+        for (int k = 0; k < wv; k++) before += wmax[par + 4 + k];
+        int o = out_off + (i0 - base) + before;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            int i = i0 + q;
+            if (i < n) {
+                if (insmask & (1u << q)) slot[o++] = 3;
+                slot[o++] = (uint8_t)((wd[q >> 2] >> (24 - 8 * (q & 3))) & 255u);
+            }
+        }
+        // self-clean the RBSP words for the next frame
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i0 + 4 * q < n) rbsp[(i0 >> 2) + q] = 0u;
+        int tile_ins = 0, tile_max = carry_nz;
+        for (int k = 0; k < 4; k++) {
+            tile_ins += wmax[par + 4 + k];
+            tile_max = max(tile_max, wmax[par + k]);
+        }
+        carry_nz = tile_max;
+        out_off += sk_min(4096, n - base) + tile_ins;
     }
+    if (tid == 0) sh_misc[3] = out_off;
+    __syncthreads();
     if (tid == 0) a.out_size[s] = sh_misc[3];
 }
 
@@ -1130,7 +1319,10 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3((a.num_slices + 63) / 64), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3(nmb), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_code_intra, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
+    if (a.rows_per_slice <= 4)
+        hipLaunchKernelGGL(k_code_intra<4>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_code_intra<kMaxRows>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
     hipLaunchKernelGGL(k_cavlc, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_assemble, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gather, dim3(a.num_slices), dim3(256), 0, s, a);

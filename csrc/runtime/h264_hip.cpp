@@ -60,7 +60,6 @@ class HipBackend : public EncoderBackend {
         set_parity_args(stride);
         HIPCHECK(hipEventRecord(ev_[0], stream_));
         HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, stream_));
-        HIPCHECK(hipMemsetAsync(args_.stripe_dirty, 0, sizeof(int) * g_.num_slices, stream_));
         gpu::launch_convert_damage(args_, stream_);
         HIPCHECK(hipMemcpyAsync(h_dirty_, args_.stripe_dirty, sizeof(int) * g_.num_slices,
                                 hipMemcpyDeviceToHost, stream_));
@@ -116,6 +115,7 @@ class HipBackend : public EncoderBackend {
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
         else if (s == "me") { p = args_.me; n = (int64_t)g_.num_mbs() * sizeof(MeResult); }
         else if (s == "mb_dirty") { p = args_.mb_dirty; n = g_.num_mbs(); }
+        else if (s == "stamps") { if (!args_.dbg) return -1; p = args_.dbg; n = 64 * 16 * 8; }
         else if (s == "tasks") {
             n = (int64_t)g_.num_slices * sizeof(SliceTask);
             if (dst && cap >= n) memcpy(dst, h_tasks_, (size_t)n);
@@ -212,6 +212,7 @@ class HipBackend : public EncoderBackend {
         a.param_sets = dps;
         a.param_set_len = dlen;
         d_frame_params_ = dmalloc<int>(4);
+        if (getenv("SK_STAMPS")) a.dbg = dmalloc<unsigned long long>(64 * 16);
         a.frame_params = d_frame_params_;
         h_dirty_ = hmalloc<int>(ns);
         h_tasks_ = hmalloc<SliceTask>(ns);
@@ -235,8 +236,7 @@ class HipBackend : public EncoderBackend {
 
     void enqueue_encode() {
         const int ns = g_.num_slices;
-        HIPCHECK(hipMemsetAsync(args_.slice_sums, 0, sizeof(long long) * 2 * ns, stream_));
-        HIPCHECK(hipMemsetAsync(args_.rbsp, 0, (size_t)ns * args_.rbsp_slot_words * 4, stream_));
+        (void)ns;  // slice_sums, stripe_dirty and rbsp are self-cleaning (k_decide / k_assemble)
         gpu::launch_encode(args_, stream_);
         gpu::launch_commit(args_, stream_);
     }

@@ -25,7 +25,7 @@ CXXFLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
     "-Wno-unused-variable", "-Wno-unused-but-set-variable", "-Wno-unused-lambda-capture",
     f"-I{CSRC}", f"-I{CSRC / 'codec'}", f"-I{CSRC / 'runtime'}",
-]
+] + (["-DSK_STAMPS"] if os.environ.get("SK_STAMPS_BUILD") else [])
 
 
 def _sources():
