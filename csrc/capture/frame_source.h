@@ -1,0 +1,28 @@
+// Frame sources for the capture thread: an X11 MIT-SHM grabber (libX11/libXext
+// loaded with dlopen at run time, so the library has no X link dependency) and
+// a synthetic desktop renderer for headless hosts.
+#pragma once
+#include <stdint.h>
+#include <memory>
+#include <string>
+
+namespace sk {
+
+class FrameSource {
+   public:
+    virtual ~FrameSource() = default;
+    // Captures one frame; returns a pointer to BGRx pixels (valid until the next
+    // grab) and the row stride in bytes, or nullptr on failure.
+    virtual const uint8_t* grab(int* stride) = 0;
+    virtual const char* name() const = 0;
+};
+
+// X11 region grabber (XShmGetImage of the root window at x,y,w,h). Returns
+// nullptr if no display/extension is available.
+std::unique_ptr<FrameSource> make_x11_source(const char* display, int x, int y, int w, int h,
+                                             bool capture_cursor, std::string* err);
+
+// Synthetic desktop (moving windows, scrolling text, a video-like region).
+std::unique_ptr<FrameSource> make_synthetic_source(int w, int h, int kind, uint32_t seed);
+
+}  // namespace sk

@@ -1,0 +1,202 @@
+// X11 MIT-SHM region grabber. libX11 / libXext / libXfixes are resolved with
+// dlopen at run time: the library loads on hosts without X, and the reference's
+// XShm + XFixes capture path (ximagesrc / pixelflux) is used
+// when an X server (Xvfb or Xorg) is reachable. The SHM segment is page-locked
+// for HIP (hipHostRegister) so the H2D upload DMAs straight out of it.
+#include "frame_source.h"
+#include <X11/Xlib.h>
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+#include <string.h>
+#include <sys/ipc.h>
+#include <sys/shm.h>
+#include <vector>
+
+namespace sk {
+namespace {
+
+struct XShmSegmentInfo_ {
+    unsigned long shmseg;
+    int shmid;
+    char* shmaddr;
+    int readOnly;
+};
+struct XFixesCursorImage_ {
+    short x, y;
+    unsigned short width, height, xhot, yhot;
+    unsigned long cursor_serial;
+    unsigned long* pixels;
+    Atom atom;
+    const char* name;
+};
+
+struct XApi {
+    void* x11 = nullptr;
+    void* xext = nullptr;
+    void* xfixes = nullptr;
+    Display* (*OpenDisplay)(const char*) = nullptr;
+    int (*CloseDisplay)(Display*) = nullptr;
+    Window (*DefRootWindow)(Display*) = nullptr;
+    int (*DefScreen)(Display*) = nullptr;
+    Visual* (*DefVisual)(Display*, int) = nullptr;
+    int (*DefDepth)(Display*, int) = nullptr;
+    int (*Sync)(Display*, Bool) = nullptr;
+    int (*Free)(void*) = nullptr;
+    Bool (*ShmQueryExtension)(Display*) = nullptr;
+    XImage* (*ShmCreateImage)(Display*, Visual*, unsigned int, int, char*, XShmSegmentInfo_*,
+                              unsigned int, unsigned int) = nullptr;
+    Bool (*ShmAttach)(Display*, XShmSegmentInfo_*) = nullptr;
+    Bool (*ShmDetach)(Display*, XShmSegmentInfo_*) = nullptr;
+    Bool (*ShmGetImage)(Display*, Drawable, XImage*, int, int, unsigned long) = nullptr;
+    XFixesCursorImage_* (*FixesGetCursorImage)(Display*) = nullptr;
+
+    bool load(std::string* err) {
+        x11 = dlopen("libX11.so.6", RTLD_NOW | RTLD_LOCAL);
+        xext = dlopen("libXext.so.6", RTLD_NOW | RTLD_LOCAL);
+        xfixes = dlopen("libXfixes.so.3", RTLD_NOW | RTLD_LOCAL);
+        if (!x11 || !xext) {
+            if (err) *err = "libX11/libXext not found";
+            return false;
+        }
+#define SYM(lib, dst, name)                                    \
+    dst = reinterpret_cast<decltype(dst)>(dlsym(lib, name));   \
+    if (!dst) { if (err) *err = std::string("missing ") + name; return false; }
+        SYM(x11, OpenDisplay, "XOpenDisplay");
+        SYM(x11, CloseDisplay, "XCloseDisplay");
+        SYM(x11, DefRootWindow, "XDefaultRootWindow");
+        SYM(x11, DefScreen, "XDefaultScreen");
+        SYM(x11, DefVisual, "XDefaultVisual");
+        SYM(x11, DefDepth, "XDefaultDepth");
+        SYM(x11, Sync, "XSync");
+        SYM(x11, Free, "XFree");
+        SYM(xext, ShmQueryExtension, "XShmQueryExtension");
+        SYM(xext, ShmCreateImage, "XShmCreateImage");
+        SYM(xext, ShmAttach, "XShmAttach");
+        SYM(xext, ShmDetach, "XShmDetach");
+        SYM(xext, ShmGetImage, "XShmGetImage");
+#undef SYM
+        if (xfixes)
+            FixesGetCursorImage =
+                reinterpret_cast<decltype(FixesGetCursorImage)>(dlsym(xfixes, "XFixesGetCursorImage"));
+        return true;
+    }
+};
+
+class X11Source : public FrameSource {
+   public:
+    X11Source(int x, int y, int w, int h, bool cursor) : x_(x), y_(y), w_(w), h_(h), cursor_(cursor) {}
+    ~X11Source() override {
+        if (dpy_) {
+            if (attached_) api_.ShmDetach(dpy_, &shm_);
+            if (img_) {
+                img_->data = nullptr;
+                api_.Free(img_);
+            }
+            api_.CloseDisplay(dpy_);
+        }
+        if (shm_.shmaddr && shm_.shmaddr != (char*)-1) {
+            if (registered_) hipHostUnregister(shm_.shmaddr);
+            shmdt(shm_.shmaddr);
+        }
+    }
+    bool open(const char* display, std::string* err) {
+        if (!api_.load(err)) return false;
+        dpy_ = api_.OpenDisplay(display);
+        if (!dpy_) {
+            if (err) *err = "cannot open X display";
+            return false;
+        }
+        if (!api_.ShmQueryExtension(dpy_)) {
+            if (err) *err = "MIT-SHM extension unavailable";
+            return false;
+        }
+        int scr = api_.DefScreen(dpy_);
+        if (api_.DefDepth(dpy_, scr) < 24) {
+            if (err) *err = "X screen depth < 24 not supported";
+            return false;
+        }
+        memset(&shm_, 0, sizeof(shm_));
+        img_ = api_.ShmCreateImage(dpy_, api_.DefVisual(dpy_, scr), 24, ZPixmap, nullptr, &shm_,
+                                   (unsigned)w_, (unsigned)h_);
+        if (!img_ || img_->bits_per_pixel != 32) {
+            if (err) *err = "XShmCreateImage failed (need 32 bpp)";
+            return false;
+        }
+        size_t bytes = (size_t)img_->bytes_per_line * img_->height;
+        shm_.shmid = shmget(IPC_PRIVATE, bytes, IPC_CREAT | 0600);
+        if (shm_.shmid < 0) {
+            if (err) *err = "shmget failed";
+            return false;
+        }
+        shm_.shmaddr = (char*)shmat(shm_.shmid, nullptr, 0);
+        shmctl(shm_.shmid, IPC_RMID, nullptr);
+        if (shm_.shmaddr == (char*)-1) {
+            if (err) *err = "shmat failed";
+            return false;
+        }
+        img_->data = shm_.shmaddr;
+        shm_.readOnly = False;
+        if (!api_.ShmAttach(dpy_, &shm_)) {
+            if (err) *err = "XShmAttach failed";
+            return false;
+        }
+        attached_ = true;
+        api_.Sync(dpy_, False);
+        registered_ = hipHostRegister(shm_.shmaddr, bytes, hipHostRegisterDefault) == hipSuccess;
+        root_ = api_.DefRootWindow(dpy_);
+        return true;
+    }
+    const uint8_t* grab(int* stride) override {
+        if (!api_.ShmGetImage(dpy_, root_, img_, x_, y_, AllPlanes)) return nullptr;
+        if (cursor_ && api_.FixesGetCursorImage) composite_cursor();
+        *stride = img_->bytes_per_line;
+        return (const uint8_t*)img_->data;
+    }
+    const char* name() const override { return "x11-shm"; }
+
+   private:
+    // K13: server-side cursor composite (small, CPU; alpha in ARGB32 longs)
+    void composite_cursor() {
+        XFixesCursorImage_* ci = api_.FixesGetCursorImage(dpy_);
+        if (!ci) return;
+        int cx = ci->x - ci->xhot - x_, cy = ci->y - ci->yhot - y_;
+        uint8_t* base = (uint8_t*)img_->data;
+        for (int j = 0; j < ci->height; j++) {
+            int py = cy + j;
+            if (py < 0 || py >= h_) continue;
+            for (int i = 0; i < ci->width; i++) {
+                int px = cx + i;
+                if (px < 0 || px >= w_) continue;
+                uint32_t argb = (uint32_t)ci->pixels[j * ci->width + i];
+                uint32_t a = argb >> 24;
+                if (!a) continue;
+                uint8_t* d = base + (size_t)py * img_->bytes_per_line + 4 * px;
+                for (int c = 0; c < 3; c++) {
+                    uint32_t s = (argb >> (8 * c)) & 255;  // premultiplied B, G, R
+                    d[c] = (uint8_t)(s + (d[c] * (255 - a) + 127) / 255);
+                }
+            }
+        }
+        api_.Free(ci);
+    }
+
+    XApi api_;
+    Display* dpy_ = nullptr;
+    XImage* img_ = nullptr;
+    XShmSegmentInfo_ shm_{};
+    Window root_ = 0;
+    int x_, y_, w_, h_;
+    bool cursor_;
+    bool attached_ = false, registered_ = false;
+};
+
+}  // namespace
+
+std::unique_ptr<FrameSource> make_x11_source(const char* display, int x, int y, int w, int h,
+                                             bool capture_cursor, std::string* err) {
+    std::unique_ptr<X11Source> s(new X11Source(x, y, w, h, capture_cursor));
+    if (!s->open(display, err)) return nullptr;
+    return s;
+}
+
+}  // namespace sk

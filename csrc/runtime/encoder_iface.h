@@ -3,6 +3,7 @@
 #include <string>
 #include <vector>
 #include "../codec/h264_frame.h"
+#include "../codec/jpeg_encoder.h"
 
 namespace sk {
 
@@ -18,6 +19,8 @@ class EncoderBackend {
 
 EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c);
 EncoderBackend* create_hip_backend(const h264::EncoderConfig& c, int device);
+EncoderBackend* create_cpu_jpeg_backend(const jpeg::JpegConfig& c);
+EncoderBackend* create_hip_jpeg_backend(const jpeg::JpegConfig& c, int device);
 void set_last_error(const std::string& e);
 
 }  // namespace sk

@@ -49,7 +49,24 @@ class CpuBackend : public EncoderBackend {
     h264::CpuH264Encoder enc_;
 };
 
+class CpuJpegBackend : public EncoderBackend {
+   public:
+    explicit CpuJpegBackend(const jpeg::JpegConfig& c) : enc_(c) {}
+    void request_keyframe() override { enc_.request_keyframe(); }
+    int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        packets_.clear();
+        enc_.encode(bgrx, stride, frame_id, packets_);
+        return (int)packets_.size();
+    }
+    int64_t debug_buffer(const char*, void*, int64_t) override { return -1; }
+
+   private:
+    jpeg::CpuJpegEncoder enc_;
+};
+
 }  // namespace
+
+EncoderBackend* create_cpu_jpeg_backend(const jpeg::JpegConfig& c) { return new CpuJpegBackend(c); }
 
 EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c) { return new CpuBackend(c); }
 
@@ -121,6 +138,28 @@ void* sk_h264_create(const sk_h264_config* c) {
     try {
         if (c->backend == 1) return create_hip_backend(e, c->device);
         return create_cpu_backend(e);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return nullptr;
+    }
+}
+
+void* sk_jpeg_create(const sk_jpeg_config* c) {
+    if (!c || c->width < 16 || c->height < 16 || (c->stripe_height % 16) != 0 || c->stripe_height <= 0) {
+        set_last_error("invalid JPEG encoder geometry");
+        return nullptr;
+    }
+    jpeg::JpegConfig j;
+    j.width = c->width;
+    j.height = c->height;
+    j.stripe_height = c->stripe_height;
+    j.quality = c->quality;
+    j.paint_quality = c->paint_quality;
+    j.use_paint_over = c->use_paint_over;
+    j.paint_over_trigger = c->paint_over_trigger;
+    try {
+        if (c->backend == 1) return create_hip_jpeg_backend(j, c->device);
+        return create_cpu_jpeg_backend(j);
     } catch (const std::exception& ex) {
         set_last_error(ex.what());
         return nullptr;

@@ -39,6 +39,56 @@ int sk_h264_stage_times(void* enc, float* dst, int32_t n);
 
 const char* sk_last_error(void);
 
+typedef struct sk_jpeg_config {
+    int32_t width, height, stripe_height;
+    int32_t quality, paint_quality, use_paint_over, paint_over_trigger;
+    int32_t device;
+    int32_t backend;  // 0 = CPU reference, 1 = HIP
+} sk_jpeg_config;
+
+// JPEG stripe encoder; shares sk_h264_encode / get_packet / destroy (generic encoder handle).
+void* sk_jpeg_create(const sk_jpeg_config* cfg);
+
+// ---- capture session (pixelflux-compatible ScreenCapture) ----
+typedef struct sk_capture_settings {
+    // pixelflux CaptureSettings fields (selkies.py:2925-2962)
+    int32_t capture_width, capture_height, capture_x, capture_y;
+    double target_fps;
+    int32_t capture_cursor, debug_logging, output_mode;
+    int32_t jpeg_quality, paint_over_jpeg_quality, use_paint_over_quality;
+    int32_t paint_over_trigger_frames, damage_block_threshold, damage_block_duration;
+    int32_t h264_crf, h264_paintover_crf, h264_paintover_burst_frames;
+    int32_t h264_fullcolor, h264_streaming_mode, h264_fullframe;
+    int32_t use_cpu, vaapi_render_node_index;
+    const char* watermark_path;
+    int32_t watermark_location_enum;
+    // extensions
+    int32_t device;          // HIP device ordinal
+    int32_t stripe_height;   // 0 -> 64
+    int32_t source;          // -1 auto (X11 if reachable), 0 X11 only, 1/2/3 synthetic motion/desktop/noise
+    const char* display;     // X display name (nullptr -> $DISPLAY)
+} sk_capture_settings;
+
+typedef struct sk_stripe_result {
+    int32_t type;            // 0 = JPEG stripe, 1 = H.264 stripe/frame
+    int32_t stripe_y_start;
+    int32_t stripe_height;
+    int32_t size;
+    uint8_t* data;
+    int32_t frame_id;
+} sk_stripe_result;
+
+typedef void (*sk_stripe_cb)(sk_stripe_result*, void*);
+
+void* sk_capture_create(void);
+void sk_capture_destroy(void* c);
+// Starts the capture thread; cb runs on that thread once per stripe packet.
+int sk_capture_start(void* c, const sk_capture_settings* s, sk_stripe_cb cb, void* user);
+void sk_capture_stop(void* c);
+void sk_capture_request_keyframe(void* c);
+// frames, mean encode ms, bytes, packets, source (1 = X11, 0 = synthetic), last encode ms
+void sk_capture_stats(void* c, double* out, int n);
+
 // Page-locked host memory (capture buffers / frame pools): DMA-able by HIP.
 void* sk_host_alloc(int64_t bytes);
 void sk_host_free(void* p);

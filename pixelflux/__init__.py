@@ -1,0 +1,108 @@
+"""pixelflux-compatible screen capture API backed by the MI355X encoder.
+
+The reference server drives an external ``pixelflux`` module (selkies.py:64-75,
+2846-2964): it fills a ``CaptureSettings`` structure, wraps a Python function in
+``StripeCallback`` and calls ``ScreenCapture().start_capture(settings, cb)``; the
+callback receives a ``StripeEncodeResult`` pointer per encoded stripe
+(``.data[:.size]``, ``.frame_id``, ``.stripe_y_start``). This module keeps that
+contract so the server code and existing integrations work unchanged, while the
+capture/encode loop itself runs in ``libselkies_native.so`` (csrc/runtime/capture.cpp):
+X11 MIT-SHM grab -> HIP colour convert / damage / H.264 or JPEG stripe encode on
+gfx950 -> callback from the native thread.
+
+Extensions over the reference: ``device`` (HIP ordinal), ``stripe_height``,
+``source`` (-1 auto, 0 X11 only, 1/2/3 synthetic motion/desktop/noise) and
+``display``. Without an X server the synthetic desktop keeps the pipeline
+testable.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+from selkies_gstreamer_amd.ops import native as _native
+
+CaptureSettings = _native.SkCaptureSettings
+StripeEncodeResult = _native.SkStripeResult
+StripeCallback = _native.SK_STRIPE_CB
+
+OUTPUT_MODE_JPEG = 0
+OUTPUT_MODE_H264 = 1
+
+
+def default_settings(width: int = 1920, height: int = 1080, **kw) -> CaptureSettings:
+    """CaptureSettings with the server defaults (selkies.py:2925-2962)."""
+    s = CaptureSettings()
+    s.capture_width, s.capture_height = width, height
+    s.capture_x = s.capture_y = 0
+    s.target_fps = 60.0
+    s.capture_cursor = 0
+    s.output_mode = OUTPUT_MODE_H264
+    s.jpeg_quality, s.paint_over_jpeg_quality, s.use_paint_over_quality = 40, 90, 1
+    s.paint_over_trigger_frames, s.damage_block_threshold, s.damage_block_duration = 15, 10, 20
+    s.h264_crf, s.h264_paintover_crf, s.h264_paintover_burst_frames = 25, 18, 5
+    s.h264_fullcolor = s.h264_streaming_mode = s.h264_fullframe = 0
+    s.use_cpu = 0
+    s.vaapi_render_node_index = -1
+    s.watermark_path = None
+    s.watermark_location_enum = -1
+    s.device = 0
+    s.stripe_height = 64
+    s.source = -1
+    s.display = None
+    for k, v in kw.items():
+        if isinstance(v, str):
+            v = v.encode()
+        setattr(s, k, v)
+    return s
+
+
+class ScreenCapture:
+    """One capture + encode session (one per display / per GPU)."""
+
+    def __init__(self):
+        self._lib = _native.lib()
+        self._h = self._lib.sk_capture_create()
+        self._cb = None
+        self._settings = None
+        self._lock = threading.Lock()
+
+    def start_capture(self, settings: CaptureSettings, callback) -> None:
+        if not isinstance(callback, StripeCallback):
+            callback = StripeCallback(callback)
+        with self._lock:
+            self._cb = callback  # keep the thunk alive while the native thread runs
+            self._settings = settings
+            rc = self._lib.sk_capture_start(self._h, ctypes.byref(settings), callback, None)
+            if rc != 0:
+                self._cb = None
+                raise RuntimeError(f"start_capture failed: {self._lib.sk_last_error().decode()}")
+
+    def stop_capture(self) -> None:
+        with self._lock:
+            if self._h:
+                self._lib.sk_capture_stop(self._h)
+            self._cb = None
+
+    def request_keyframe(self) -> None:
+        if self._h:
+            self._lib.sk_capture_request_keyframe(self._h)
+
+    def stats(self) -> dict:
+        arr = (ctypes.c_double * 6)()
+        self._lib.sk_capture_stats(self._h, arr, 6)
+        return {"frames": int(arr[0]), "encode_ms_mean": arr[1], "bytes": int(arr[2]),
+                "packets": int(arr[3]), "source": {1.0: "x11", 0.0: "synthetic"}.get(arr[4], "none"),
+                "encode_ms_last": arr[5]}
+
+    def close(self) -> None:
+        self.stop_capture()
+        if self._h:
+            self._lib.sk_capture_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

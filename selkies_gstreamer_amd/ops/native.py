@@ -32,6 +32,42 @@ class SkH264Config(ctypes.Structure):
     ]
 
 
+class SkJpegConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "width", "height", "stripe_height", "quality", "paint_quality", "use_paint_over",
+        "paint_over_trigger", "device", "backend")]
+
+
+class SkCaptureSettings(ctypes.Structure):
+    """Mirror of ``sk_capture_settings`` (pixelflux CaptureSettings + extensions)."""
+    _fields_ = [
+        ("capture_width", ctypes.c_int32), ("capture_height", ctypes.c_int32),
+        ("capture_x", ctypes.c_int32), ("capture_y", ctypes.c_int32),
+        ("target_fps", ctypes.c_double),
+        ("capture_cursor", ctypes.c_int32), ("debug_logging", ctypes.c_int32), ("output_mode", ctypes.c_int32),
+        ("jpeg_quality", ctypes.c_int32), ("paint_over_jpeg_quality", ctypes.c_int32),
+        ("use_paint_over_quality", ctypes.c_int32),
+        ("paint_over_trigger_frames", ctypes.c_int32), ("damage_block_threshold", ctypes.c_int32),
+        ("damage_block_duration", ctypes.c_int32),
+        ("h264_crf", ctypes.c_int32), ("h264_paintover_crf", ctypes.c_int32),
+        ("h264_paintover_burst_frames", ctypes.c_int32),
+        ("h264_fullcolor", ctypes.c_int32), ("h264_streaming_mode", ctypes.c_int32),
+        ("h264_fullframe", ctypes.c_int32),
+        ("use_cpu", ctypes.c_int32), ("vaapi_render_node_index", ctypes.c_int32),
+        ("watermark_path", ctypes.c_char_p), ("watermark_location_enum", ctypes.c_int32),
+        ("device", ctypes.c_int32), ("stripe_height", ctypes.c_int32), ("source", ctypes.c_int32),
+        ("display", ctypes.c_char_p),
+    ]
+
+
+class SkStripeResult(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("stripe_y_start", ctypes.c_int32), ("stripe_height", ctypes.c_int32),
+                ("size", ctypes.c_int32), ("data", ctypes.POINTER(ctypes.c_ubyte)), ("frame_id", ctypes.c_int32)]
+
+
+SK_STRIPE_CB = ctypes.CFUNCTYPE(None, ctypes.POINTER(SkStripeResult), ctypes.c_void_p)
+
+
 class SkPacket(ctypes.Structure):
     _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8)), ("size", ctypes.c_int32), ("y", ctypes.c_int32),
                 ("w", ctypes.c_int32), ("h", ctypes.c_int32), ("key", ctypes.c_int32)]
@@ -64,6 +100,16 @@ def lib():
         L.sk_host_alloc.restype = ctypes.c_void_p
         L.sk_host_alloc.argtypes = [ctypes.c_int64]
         L.sk_host_free.argtypes = [ctypes.c_void_p]
+        L.sk_jpeg_create.restype = ctypes.c_void_p
+        L.sk_jpeg_create.argtypes = [ctypes.POINTER(SkJpegConfig)]
+        L.sk_capture_create.restype = ctypes.c_void_p
+        L.sk_capture_destroy.argtypes = [ctypes.c_void_p]
+        L.sk_capture_start.argtypes = [ctypes.c_void_p, ctypes.POINTER(SkCaptureSettings), SK_STRIPE_CB,
+                                       ctypes.c_void_p]
+        L.sk_capture_start.restype = ctypes.c_int
+        L.sk_capture_stop.argtypes = [ctypes.c_void_p]
+        L.sk_capture_request_keyframe.argtypes = [ctypes.c_void_p]
+        L.sk_capture_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         _lib = L
         return L
 
@@ -191,3 +237,25 @@ class H264Encoder:
         arr = (ctypes.c_float * n)()
         k = lib().sk_h264_stage_times(self._h, arr, n)
         return list(arr[:k])
+
+
+class JpegEncoder(H264Encoder):
+    """JPEG stripe encoder session; packets are [frame_id u16][y u16][JPEG]."""
+
+    def __init__(self, width: int, height: int, *, stripe_height: int = 64, quality: int = 40,
+                 paint_quality: int = 90, use_paint_over: bool = True, paint_over_trigger: int = 15,
+                 device: int = 0, backend: str = "cpu"):
+        L = lib()
+        if backend not in ("cpu", "hip"):
+            raise ValueError("backend must be 'cpu' or 'hip'")
+        if backend == "hip":
+            require_gpu()
+        if stripe_height % 16:
+            raise ValueError("JPEG stripe_height must be a multiple of 16")
+        self.cfg = SkJpegConfig(width, height, stripe_height, quality, paint_quality, int(use_paint_over),
+                                paint_over_trigger, device, 1 if backend == "hip" else 0)
+        self.width, self.height = width, height
+        self.backend = backend
+        self._h = L.sk_jpeg_create(ctypes.byref(self.cfg))
+        if not self._h:
+            raise RuntimeError(f"sk_jpeg_create failed: {L.sk_last_error().decode()}")
