@@ -89,6 +89,18 @@ void sk_capture_request_keyframe(void* c);
 // frames, mean encode ms, bytes, packets, source (1 = X11, 0 = synthetic), last encode ms
 void sk_capture_stats(void* c, double* out, int n);
 
+// ---- X11 input injection (XTest) and cursor watching (XFixes) ----
+// cursor_only=1 opens a connection that only watches cursor changes.
+void* sk_x11_input_open(const char* display, int cursor_only);
+void sk_x11_input_close(void* h);
+int sk_x11_key(void* h, uint32_t keysym, int down, int shift_held);
+int sk_x11_motion(void* h, int x, int y);
+int sk_x11_motion_rel(void* h, int dx, int dy);
+int sk_x11_button(void* h, int button, int down);
+void sk_x11_screen_size(void* h, int* w, int* hh);
+int sk_x11_cursor_wait(void* h, int timeout_ms);
+int sk_x11_cursor_image(void* h, uint64_t* serial, int* w, int* hh, int* xhot, int* yhot, uint32_t* argb, int cap);
+
 // Page-locked host memory (capture buffers / frame pools): DMA-able by HIP.
 void* sk_host_alloc(int64_t bytes);
 void sk_host_free(void* p);

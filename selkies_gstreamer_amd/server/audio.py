@@ -1,0 +1,187 @@
+"""Audio in/out helpers: pcmflux pipeline wrapper and the microphone sink.
+
+Microphone path (reference selkies.py:1642-1840): the browser sends ``0x02`` +
+s16le mono 24 kHz PCM; the server makes sure a PulseAudio virtual source
+``SelkiesVirtualMic`` (master ``input.monitor``) exists and plays the PCM into
+sink ``input`` through a simple playback stream, keeping at most 2 s buffered
+and dropping the older half on overflow. The reference uses pulsectl + pasimple;
+here ``pactl`` creates the virtual source and libpulse-simple (ctypes) plays.
+Everything degrades to a logged no-op when PulseAudio is absent.
+"""
+from __future__ import annotations
+
+import asyncio
+import ctypes
+import ctypes.util
+import logging
+import shutil
+from typing import Optional
+
+from . import protocol
+
+log = logging.getLogger("audio")
+
+VIRTUAL_SOURCE = "SelkiesVirtualMic"
+MASTER_MONITOR = "input.monitor"
+
+
+class _Spec(ctypes.Structure):
+    _fields_ = [("format", ctypes.c_int), ("rate", ctypes.c_uint32), ("channels", ctypes.c_uint8)]
+
+
+class MicSink:
+    def __init__(self):
+        self.stream = None
+        self.pa = None
+        self.ready = False
+        self.failed = False
+        self.buffer = bytearray()
+        self._warned = False
+
+    def _load(self) -> bool:
+        path = ctypes.util.find_library("pulse-simple")
+        if not path:
+            return False
+        try:
+            self.pa = ctypes.CDLL(path)
+        except OSError:
+            return False
+        self.pa.pa_simple_new.restype = ctypes.c_void_p
+        self.pa.pa_simple_new.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p,
+                                          ctypes.c_char_p, ctypes.POINTER(_Spec), ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_int)]
+        self.pa.pa_simple_write.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.POINTER(ctypes.c_int)]
+        self.pa.pa_simple_free.argtypes = [ctypes.c_void_p]
+        return True
+
+    async def setup(self) -> bool:
+        if self.ready or self.failed:
+            return self.ready
+        pactl = shutil.which("pactl")
+        if not pactl or not self._load():
+            self.failed = True
+            log.warning("microphone forwarding unavailable (needs pactl and libpulse-simple)")
+            return False
+        p = await asyncio.create_subprocess_exec(pactl, "list", "short", "sources", stdout=asyncio.subprocess.PIPE,
+                                                 stderr=asyncio.subprocess.DEVNULL)
+        out, _ = await p.communicate()
+        if VIRTUAL_SOURCE not in out.decode(errors="replace"):
+            p = await asyncio.create_subprocess_exec(pactl, "load-module", "module-virtual-source",
+                                                     f"source_name={VIRTUAL_SOURCE}", f"master={MASTER_MONITOR}",
+                                                     stdout=asyncio.subprocess.DEVNULL,
+                                                     stderr=asyncio.subprocess.DEVNULL)
+            if await p.wait() != 0:
+                self.failed = True
+                log.error("could not load module-virtual-source")
+                return False
+        err = ctypes.c_int(0)
+        spec = _Spec(3, protocol.MIC_SAMPLE_RATE, 1)  # s16le mono 24 kHz
+        self.stream = self.pa.pa_simple_new(None, b"SelkiesClientMic", 1, b"input", b"MicStream",
+                                            ctypes.byref(spec), None, None, ctypes.byref(err))
+        if not self.stream:
+            self.failed = True
+            log.error("pa_simple_new playback failed (%d)", err.value)
+            return False
+        self.ready = True
+        return True
+
+    def push(self, pcm: bytes) -> int:
+        """Buffers and plays one chunk; returns bytes written."""
+        if not self.ready or not pcm:
+            return 0
+        self.buffer += pcm
+        if len(self.buffer) > protocol.MIC_BUFFER_MAX:
+            del self.buffer[: len(self.buffer) // 2]
+            log.warning("microphone buffer overflow; dropped old audio")
+        n = len(pcm)
+        chunk = bytes(self.buffer[:n])
+        del self.buffer[:n]
+        err = ctypes.c_int(0)
+        if self.pa.pa_simple_write(self.stream, chunk, len(chunk), ctypes.byref(err)) < 0:
+            log.error("microphone write failed (%d)", err.value)
+            self.close()
+            return 0
+        return len(chunk)
+
+    def close(self):
+        if self.stream and self.pa:
+            self.pa.pa_simple_free(self.stream)
+        self.stream = None
+        self.ready = False
+        self.buffer.clear()
+
+
+class AudioPipeline:
+    """pcmflux capture -> asyncio queue -> broadcast (0x01 0x00 + opus)."""
+
+    def __init__(self, broadcast, device_name: str, channels: int = 2, debug: bool = False):
+        self.broadcast = broadcast
+        self.device_name = device_name
+        self.channels = channels
+        self.debug = debug
+        self.capture = None
+        self.queue: Optional[asyncio.Queue] = None
+        self.task: Optional[asyncio.Task] = None
+        self.loop = None
+        self._cb = None
+
+    @property
+    def running(self) -> bool:
+        return self.capture is not None
+
+    async def start(self, bitrate: int) -> bool:
+        if self.running:
+            return True
+        try:
+            import pcmflux
+        except ImportError:
+            return False
+        if not pcmflux.available():
+            log.warning("audio capture unavailable (libpulse-simple/libopus missing)")
+            return False
+        self.loop = asyncio.get_running_loop()
+        self.queue = asyncio.Queue(maxsize=500)
+        s = pcmflux.AudioCaptureSettings()
+        s.device_name = self.device_name.encode() if self.device_name else None
+        s.sample_rate, s.channels, s.opus_bitrate, s.frame_duration_ms = 48000, self.channels, int(bitrate), 20
+        s.use_vbr, s.use_silence_gate, s.debug_logging = True, False, self.debug
+        q, loop = self.queue, self.loop
+
+        def on_chunk(res_ptr, user):
+            r = res_ptr.contents
+            if r.size > 0:
+                data = bytes(ctypes.cast(r.data, ctypes.POINTER(ctypes.c_ubyte * r.size)).contents)
+                loop.call_soon_threadsafe(_put, q, data)
+
+        self._cb = pcmflux.AudioChunkCallback(on_chunk)
+        cap = pcmflux.AudioCapture()
+        try:
+            await self.loop.run_in_executor(None, cap.start_capture, s, self._cb)
+        except RuntimeError as e:
+            log.error("audio start failed: %s", e)
+            return False
+        self.capture = cap
+        self.task = asyncio.create_task(self._sender())
+        return True
+
+    async def _sender(self):
+        while True:
+            data = await self.queue.get()
+            await self.broadcast(protocol.AUDIO_PREFIX + data)
+
+    async def stop(self):
+        if self.task:
+            self.task.cancel()
+            self.task = None
+        if self.capture:
+            cap, self.capture = self.capture, None
+            await asyncio.get_running_loop().run_in_executor(None, cap.stop_capture)
+        self.queue = None
+
+
+def _put(q: asyncio.Queue, item):
+    try:
+        q.put_nowait(item)
+    except asyncio.QueueFull:
+        pass

@@ -1,0 +1,799 @@
+"""Data websocket server: sessions, displays, capture lifecycle, fan-out, backpressure.
+
+Behavior parity with the reference ``DataStreamingServer`` (selkies.py:803-2964,
+SURVEY C04/C05/C07/C08/C09/C10/C11): same wire protocol (see :mod:`.protocol`),
+same display registry (``primary`` + one secondary), same settings sanitization,
+same reconnect debounce and ``KILL`` on takeover, same stats cadence.
+
+MI355X-first differences:
+
+* video comes from the native capture session (pixelflux-compatible API over
+  libselkies_native): HIP colour conversion, damage, motion search and CAVLC on
+  the GPU; each display may be pinned to its own HIP device (``gpu_id`` + display
+  index, see :mod:`selkies_gstreamer_amd.parallel.placement`);
+* transport is aiohttp: one ordered outbound queue + writer task per client, so
+  a slow viewer never blocks the event loop or other viewers, and static client
+  files / ``/health`` / ``/metrics`` are served from the same port;
+* frame backpressure really gates sending (for every display) and asks the
+  encoder for a keyframe when it lifts, because skipped P-stripes are not
+  decodable (the reference only gates secondary displays).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import os
+import time
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Any, Callable, Optional
+
+from aiohttp import WSMsgType, web
+
+from . import protocol
+from .audio import AudioPipeline, MicSink
+from .display import XrandrDisplay, compute_layout, set_cursor_size, set_dpi
+from .settings import Settings
+from .stats import BandwidthMeter, StatsPublisher
+
+log = logging.getLogger("data_websocket")
+
+VIDEO_QUEUE_SIZE = 120
+RECONNECT_DEBOUNCE_S = 0.5
+CURSOR_SIZE = 32
+VIDEO_KEYS = ("encoder", "framerate", "h264_crf", "h264_fullcolor", "h264_streaming_mode", "jpeg_quality",
+              "paint_over_jpeg_quality", "use_cpu", "h264_paintover_crf", "h264_paintover_burst_frames",
+              "use_paint_over_quality")
+
+
+class Client:
+    """One websocket connection with its own ordered outbound queue."""
+
+    def __init__(self, ws: web.WebSocketResponse, remote: str, meter: BandwidthMeter):
+        self.ws = ws
+        self.remote = remote
+        self.meter = meter
+        self.out: asyncio.Queue = asyncio.Queue()
+        self.writer = asyncio.create_task(self._write())
+        self.display_id: Optional[str] = None
+        self.closed = False
+
+    async def _write(self):
+        try:
+            while True:
+                msg = await self.out.get()
+                if msg is None:
+                    break
+                if isinstance(msg, (bytes, bytearray)):
+                    await self.ws.send_bytes(msg)
+                else:
+                    await self.ws.send_str(msg)
+                self.meter.add(len(msg))
+        except (ConnectionError, RuntimeError, asyncio.CancelledError):
+            pass
+        finally:
+            self.closed = True
+
+    def send(self, msg) -> bool:
+        if self.closed or self.ws.closed:
+            return False
+        self.out.put_nowait(msg)
+        return True
+
+    async def send_now(self, msg) -> bool:
+        return self.send(msg)
+
+    async def close(self, code: int = 1000, reason: str = ""):
+        self.out.put_nowait(None)
+        try:
+            await asyncio.wait_for(self.writer, 2.0)
+        except (asyncio.TimeoutError, asyncio.CancelledError):
+            self.writer.cancel()
+        if not self.ws.closed:
+            await self.ws.close(code=code, message=reason.encode())
+
+
+@dataclass
+class DisplayState:
+    client: Client
+    width: int = 0
+    height: int = 0
+    position: str = "right"
+    video_active: bool = True
+    flow: protocol.DisplayFlow = field(default_factory=protocol.DisplayFlow)
+    params: dict = field(default_factory=dict)
+    bp_task: Optional[asyncio.Task] = None
+    scaling_dpi: Optional[Any] = None
+    audio_bitrate: Optional[Any] = None
+
+
+class Capture:
+    """One display's capture session + queue + sender task."""
+
+    def __init__(self, display_id: str, module, queue: asyncio.Queue, sender: asyncio.Task):
+        self.display_id, self.module, self.queue, self.sender = display_id, module, queue, sender
+        self.callback = None
+
+
+class DataStreamingServer:
+    def __init__(self, settings: Settings, *, upload_dir: Optional[str] = None, input_factory=None,
+                 capture_factory: Optional[Callable[[], Any]] = None, display_manager=None,
+                 capture_source: str = "auto", gpu_id: int = 0, num_gpus: int = 1, clock=time.monotonic,
+                 web_root: Optional[str] = None, metrics=None):
+        self.settings = settings
+        self.clock = clock
+        self.mode = "websockets"
+        self.clients: set[Client] = set()
+        self.displays: "OrderedDict[str, DisplayState]" = OrderedDict()
+        self.layouts: dict = {}
+        self.captures: dict[str, Capture] = {}
+        self.meter = BandwidthMeter(clock)
+        self.recent: "OrderedDict[str, float]" = OrderedDict()
+        self.reconfigure_lock = asyncio.Lock()
+        self._reconfiguring = False
+        self._reconfigure_pending = False
+        self.settings_received = asyncio.Event()
+        self.capture_cursor = False
+        self.last_cursor: Optional[dict] = None
+        self.upload_dir = upload_dir
+        if upload_dir:
+            try:
+                os.makedirs(upload_dir, exist_ok=True)
+            except OSError as e:
+                log.error("upload dir %s unusable: %s", upload_dir, e)
+                self.upload_dir = None
+        self.input_factory = input_factory
+        self.input = None
+        if capture_factory is None:
+            import pixelflux
+            capture_factory = pixelflux.ScreenCapture
+        self.capture_factory = capture_factory
+        self.display_manager = display_manager or XrandrDisplay()
+        self.capture_source = capture_source
+        self.gpu_id, self.num_gpus = gpu_id, max(1, num_gpus)
+        self.web_root = web_root
+        self.metrics = metrics
+        self.audio = AudioPipeline(self._broadcast_audio, settings.audio_device_name,
+                                   debug=settings.debug[0])
+        self.audio_bitrate = int(settings.initial("audio_bitrate"))
+        self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self.runner: Optional[web.AppRunner] = None
+        self.encoder = settings.encoder
+        self.framerate = settings.initial("framerate")
+
+    # ================================================================ app / routes
+    def make_app(self) -> web.Application:
+        app = web.Application(client_max_size=64 * 1024 * 1024)
+        app.router.add_get("/health", self._health)
+        if self.metrics is not None:
+            app.router.add_get("/metrics", self.metrics.handler)
+        app.router.add_get("/{tail:.*}", self._root)
+        return app
+
+    async def _health(self, request):
+        return web.Response(text="OK\n")
+
+    async def _root(self, request: web.Request):
+        if request.headers.get("Upgrade", "").lower() == "websocket":
+            return await self.ws_handler(request)
+        if self.web_root:
+            rel = request.match_info.get("tail", "") or "index.html"
+            path = os.path.realpath(os.path.join(self.web_root, rel))
+            root = os.path.realpath(self.web_root)
+            if path.startswith(root + os.sep) or path == root:
+                if os.path.isdir(path):
+                    path = os.path.join(path, "index.html")
+                if os.path.isfile(path):
+                    return web.FileResponse(path)
+        raise web.HTTPNotFound()
+
+    async def start(self, host: str = "0.0.0.0", port: Optional[int] = None):
+        self.loop = asyncio.get_running_loop()
+        self.runner = web.AppRunner(self.make_app())
+        await self.runner.setup()
+        site = web.TCPSite(self.runner, host, port if port is not None else self.settings.port)
+        await site.start()
+        self.port = site._server.sockets[0].getsockname()[1]
+        if self.input_factory is not None:
+            self.input = await self.input_factory(self)
+        log.info("data websocket server on %s:%d", host, self.port)
+        return self.port
+
+    async def stop(self):
+        for c in list(self.clients):
+            await c.close(1001, "server shutdown")
+        async with self.reconfigure_lock:
+            await self.shutdown_pipelines()
+        if self.input is not None:
+            await self.input.close()
+        if self.runner:
+            await self.runner.cleanup()
+
+    # ================================================================ broadcast helpers
+    def broadcast(self, clients, msg):
+        for c in list(clients):
+            c.send(msg)
+
+    def primary_viewers(self) -> set:
+        secondary = {d.client for did, d in self.displays.items() if did != "primary"}
+        return self.clients - secondary
+
+    async def _broadcast_audio(self, data: bytes):
+        self.broadcast(self.primary_viewers(), data)
+
+    def send_cursor(self, msg: dict):
+        """Thread-safe: cursor watcher thread -> all clients."""
+        self.last_cursor = msg
+        if self.loop is not None:
+            self.loop.call_soon_threadsafe(self.broadcast, self.clients, "cursor," + json.dumps(msg))
+
+    async def send_clipboard(self, data: bytes, mime: str = "text/plain"):
+        if mime != "text/plain" and not (self.input and self.input.enable_binary_clipboard):
+            return
+        for m in protocol.clipboard_messages(data, mime):
+            self.broadcast(self.clients, m)
+            await asyncio.sleep(0)
+
+    # ================================================================ websocket handler
+    async def ws_handler(self, request: web.Request):
+        ip = request.remote or "?"
+        now = self.clock()
+        last = self.recent.get(ip)
+        ws = web.WebSocketResponse(max_msg_size=64 * 1024 * 1024, heartbeat=None)
+        await ws.prepare(request)
+        if last is not None and (now - last) < RECONNECT_DEBOUNCE_S:
+            log.warning("client %s reconnecting too quickly; rejected", ip)
+            await ws.close(code=4029, message=b"Rate limited: reconnecting too quickly")
+            return ws
+        self.recent[ip] = now
+        if len(self.recent) > 1000:
+            self.recent.popitem(last=False)
+        client = Client(ws, ip, self.meter)
+        self.clients.add(client)
+        self.settings_received = asyncio.Event() if not self.displays else self.settings_received
+        initial_done = False
+        uploads = _UploadState(self.upload_dir)
+        mic = MicSink()
+        stats = StatsPublisher(client.send_now, self.meter, self._primary_rtt, gpu_id=self.gpu_id)
+        client.send(f"MODE {self.mode}")
+        if self.last_cursor:
+            client.send("cursor," + json.dumps(self.last_cursor))
+        client.send(json.dumps(self.settings.client_payload()))
+        stats.start()
+        try:
+            async for msg in ws:
+                if msg.type == WSMsgType.BINARY:
+                    await self._on_binary(msg.data, uploads, mic)
+                elif msg.type == WSMsgType.TEXT:
+                    initial_done = await self._on_text(client, msg.data, uploads, initial_done)
+                    if client.closed or ws.closed:
+                        break
+                elif msg.type in (WSMsgType.ERROR, WSMsgType.CLOSE):
+                    break
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # keep the server alive whatever one client does
+            log.error("error in data websocket handler for %s: %s", ip, e, exc_info=True)
+        finally:
+            await stats.cancel()
+            uploads.abort()
+            mic.close()
+            await self._disconnect(client)
+        return ws
+
+    async def _disconnect(self, client: Client):
+        self.clients.discard(client)
+        gone = [did for did, d in self.displays.items() if d.client is client]
+        for did in gone:
+            await self._stop_bp(did)
+            del self.displays[did]
+        if gone:
+            await self.reconfigure_displays()
+        await client.close()
+        if not self.clients:
+            self.capture_cursor = False
+            async with self.reconfigure_lock:
+                await self.shutdown_pipelines()
+
+    async def shutdown_pipelines(self):
+        for did in list(self.captures):
+            await self._stop_capture(did)
+        await self.audio.stop()
+
+    # ---------------------------------------------------------------- binary
+    async def _on_binary(self, data: bytes, uploads: "_UploadState", mic: MicSink):
+        if not data:
+            return
+        kind, payload = data[0], data[1:]
+        if kind == 0x01:
+            uploads.write(payload)
+        elif kind == 0x02:
+            if not self.settings.microphone_enabled[0]:
+                return
+            if await mic.setup():
+                mic.push(payload)
+
+    # ---------------------------------------------------------------- text
+    async def _on_text(self, client: Client, m: str, uploads: "_UploadState", initial_done: bool) -> bool:
+        s = self.settings
+        if m.startswith("FILE_UPLOAD_START:"):
+            if "upload" not in s.file_transfers:
+                log.warning("upload refused: uploads disabled")
+            else:
+                uploads.start(m)
+        elif m.startswith("FILE_UPLOAD_END:"):
+            uploads.finish()
+        elif m.startswith("FILE_UPLOAD_ERROR:"):
+            log.error("client upload error: %s", m)
+            uploads.abort()
+        elif m.startswith("SETTINGS,"):
+            initial_done = await self._on_settings(client, m[len("SETTINGS,"):], initial_done)
+        elif m.startswith("CLIENT_FRAME_ACK"):
+            did = client.display_id
+            if did and did in self.displays:
+                try:
+                    self.displays[did].flow.on_ack(protocol.parse_frame_ack(m), self.clock())
+                except ValueError:
+                    log.warning("malformed ACK: %s", m)
+        elif m == "START_VIDEO":
+            await self._start_video(client)
+        elif m == "STOP_VIDEO":
+            did = client.display_id
+            if did and did in self.displays:
+                self.displays[did].video_active = False
+                await self._stop_capture(did)
+                client.send("VIDEO_STOPPED")
+        elif m == "START_AUDIO":
+            async with self.reconfigure_lock:
+                if s.audio_enabled[0]:
+                    await self.audio.start(self.audio_bitrate)
+                self.broadcast(self.clients, "AUDIO_STARTED")
+        elif m == "STOP_AUDIO":
+            async with self.reconfigure_lock:
+                await self.audio.stop()
+                self.broadcast(self.clients, "AUDIO_STOPPED")
+        elif m.startswith("r,"):
+            await self._on_resize(m)
+        elif m.startswith("SET_NATIVE_CURSOR_RENDERING,"):
+            want = m.split(",", 1)[1].strip().lower() in ("1", "true")
+            if want != self.capture_cursor:
+                self.capture_cursor = want
+                if self.captures:
+                    await self.reconfigure_displays()
+        elif m.startswith("s,"):
+            try:
+                dpi = int(m.split(",")[1])
+            except (ValueError, IndexError):
+                log.error("malformed DPI message %s", m)
+            else:
+                await set_dpi(dpi)
+                await set_cursor_size(max(1, round(dpi / 96.0 * CURSOR_SIZE)))
+        elif m.startswith("cmd,"):
+            if not s.command_enabled[0]:
+                log.warning("cmd refused: commands disabled")
+            else:
+                cmd = m[len("cmd,"):]
+                if cmd:
+                    try:
+                        p = await asyncio.create_subprocess_shell(cmd, stdout=asyncio.subprocess.DEVNULL,
+                                                                  stderr=asyncio.subprocess.DEVNULL,
+                                                                  cwd=os.path.expanduser("~"))
+                        log.info("launched '%s' (pid %d)", cmd, p.pid)
+                    except OSError as e:
+                        log.error("cmd failed: %s", e)
+        elif self.input is not None:
+            await self.input.on_message(m, client.display_id or "primary")
+        return initial_done
+
+    # ---------------------------------------------------------------- SETTINGS
+    async def _on_settings(self, client: Client, payload: str, initial_done: bool) -> bool:
+        try:
+            parsed = protocol.parse_settings_payload(payload)
+        except (ValueError, TypeError) as e:
+            log.error("bad SETTINGS payload: %s", e)
+            return initial_done
+        did = parsed.get("displayId") or "primary"
+        if did != "primary" and not self.settings.second_screen[0]:
+            client.send("KILL Second screens are disabled on this server.")
+            await client.close(1008, "Second screens disabled")
+            return initial_done
+        client.display_id = did
+        existing = self.displays.get(did)
+        if existing is not None and existing.client is not client and not existing.client.closed:
+            reason = f"a new {did} client connected connection killed"
+            existing.client.send(f"KILL {reason}")
+            await existing.client.close(1000, "Superseded by new client")
+        if did != "primary":
+            for other, st in list(self.displays.items()):
+                if other != "primary" and other != did and st.client is not client:
+                    await self._stop_capture(other)
+                    st.video_active = False
+                    st.client.send("VIDEO_STOPPED")
+        if did not in self.displays:
+            self.displays[did] = DisplayState(client=client, params=self._initial_params())
+        else:
+            st = self.displays[did]
+            st.client = client
+            st.video_active = True
+            st.flow.reset(self.clock())
+        await self.apply_client_settings(did, parsed, not initial_done)
+        if not initial_done:
+            initial_done = True
+            if did == "primary" and self.settings.audio_enabled[0] and not self.audio.running:
+                async with self.reconfigure_lock:
+                    await self.audio.start(self.audio_bitrate)
+        return initial_done
+
+    def _initial_params(self) -> dict:
+        s = self.settings
+        return {"encoder": s.encoder, "framerate": s.initial("framerate"), "h264_crf": s.initial("h264_crf"),
+                "h264_fullcolor": s.initial("h264_fullcolor"),
+                "h264_streaming_mode": s.initial("h264_streaming_mode"),
+                "jpeg_quality": s.initial("jpeg_quality"),
+                "paint_over_jpeg_quality": s.initial("paint_over_jpeg_quality"), "use_cpu": s.initial("use_cpu"),
+                "h264_paintover_crf": s.initial("h264_paintover_crf"),
+                "h264_paintover_burst_frames": s.initial("h264_paintover_burst_frames"),
+                "use_paint_over_quality": s.initial("use_paint_over_quality")}
+
+    async def apply_client_settings(self, did: str, parsed: dict, initial: bool):
+        st = self.displays.get(did)
+        if st is None:
+            return
+        s = self.settings
+        restart_audio = False
+        async with self.reconfigure_lock:
+            old = dict(st.params)
+            old_w, old_h, old_pos = st.width, st.height, st.position
+            new_pos = parsed.get("displayPosition") or "right"
+            tw = th = None
+            if s.is_manual_resolution_mode[0] and s.is_manual_resolution_mode[1]:
+                tw, th = int(s.manual_width), int(s.manual_height)
+            elif s.sanitize("is_manual_resolution_mode", parsed.get("is_manual_resolution_mode")):
+                tw = s.sanitize("manual_width", parsed.get("manual_width"))
+                th = s.sanitize("manual_height", parsed.get("manual_height"))
+            elif initial:
+                tw, th = parsed.get("initialClientWidth"), parsed.get("initialClientHeight")
+            if not isinstance(tw, int) or tw <= 0:
+                tw = old_w if old_w > 0 else 1024
+            if not isinstance(th, int) or th <= 0:
+                th = old_h if old_h > 0 else 768
+            tw, th = protocol.even_dims(tw, th)
+            dims_changed = (tw, th) != (old_w, old_h) or new_pos != old_pos
+            st.width, st.height, st.position = tw, th, new_pos
+            for k in VIDEO_KEYS:
+                st.params[k] = s.sanitize(k, parsed.get(k))
+            bitrate = s.sanitize("audio_bitrate", parsed.get("audio_bitrate"))
+            if bitrate is not None and int(bitrate) != self.audio_bitrate:
+                self.audio_bitrate = int(bitrate)
+                restart_audio = self.audio.running
+            if self.input is not None:
+                await self.input.update_binary_clipboard_setting(
+                    bool(s.sanitize("enable_binary_clipboard", parsed.get("enable_binary_clipboard"))))
+            dpi = s.sanitize("scaling_dpi", parsed.get("scaling_dpi"))
+            if dpi is not None and dpi != st.scaling_dpi:
+                if st.scaling_dpi is not None or initial:
+                    await set_dpi(int(dpi))
+                st.scaling_dpi = dpi
+            video_changed = any(st.params.get(k) != old.get(k) for k in VIDEO_KEYS)
+        if restart_audio:
+            await self.audio.stop()
+            await self.audio.start(self.audio_bitrate)
+        if initial or dims_changed:
+            await self.reconfigure_displays()
+        elif video_changed:
+            if did in self.layouts:
+                l = self.layouts[did]
+                await self._stop_capture(did)
+                await self._start_capture(did, l["w"], l["h"], l["x"], l["y"])
+            else:
+                await self.reconfigure_displays()
+        if initial:
+            self.settings_received.set()
+
+    # ---------------------------------------------------------------- resize / video
+    async def _on_resize(self, m: str):
+        parts = m.split(",")
+        if len(parts) != 3:
+            log.warning("malformed resize: %s", m)
+            return
+        _, res, did = parts
+        st = self.displays.get(did)
+        if st is None:
+            return
+        if self.settings.is_manual_resolution_mode[0] and self.settings.is_manual_resolution_mode[1]:
+            log.warning("resize ignored: manual resolution mode")
+            return
+        try:
+            w, h = protocol.even_dims(*protocol.parse_resolution(res))
+        except ValueError:
+            log.error("invalid resolution %s", res)
+            return
+        if w <= 0 or h <= 0 or (w, h) == (st.width, st.height):
+            return
+        st.width, st.height = w, h
+        await self.reconfigure_displays()
+
+    async def _start_video(self, client: Client):
+        did = client.display_id
+        if did and did in self.displays:
+            st = self.displays[did]
+            st.video_active = True
+            if did in self.layouts:
+                l = self.layouts[did]
+                await self._start_capture(did, l["w"], l["h"], l["x"], l["y"])
+            else:
+                await self.reconfigure_displays()
+            client.send("VIDEO_STARTED")
+        else:
+            await self.reconfigure_displays()
+
+    async def reconfigure_displays(self):
+        """Lays out all displays and (re)starts their captures.
+
+        Requests arriving while a reconfiguration runs are coalesced into one
+        more pass (the reference drops them, which can leave a just-connected
+        secondary display without a stream).
+        """
+        if self._reconfiguring:
+            self._reconfigure_pending = True
+            return
+        self._reconfiguring = True
+        try:
+            async with self.reconfigure_lock:
+                while True:
+                    self._reconfigure_pending = False
+                    await self._reconfigure_once()
+                    if not self._reconfigure_pending:
+                        break
+        finally:
+            self._reconfiguring = False
+
+    async def _reconfigure_once(self):
+        for did in list(self.captures):
+            await self._stop_capture(did)
+        if not self.displays:
+            await self.display_manager.clear()
+            return
+        layouts, tw, th = compute_layout({k: {"width": v.width, "height": v.height, "position": v.position}
+                                          for k, v in self.displays.items()})
+        if not tw or not th:
+            log.error("display layout is empty; not starting capture")
+            return
+        self.layouts = layouts
+        if getattr(self.display_manager, "available", False):
+            ok = await self.display_manager.apply(layouts, tw, th)
+            if not ok:
+                log.warning("xrandr layout failed; capturing the current screen")
+        for did, l in layouts.items():
+            st = self.displays.get(did)
+            if st and st.video_active:
+                await self._start_capture(did, l["w"], l["h"], l["x"], l["y"])
+        p = self.displays.get("primary")
+        if p and p.width and p.height:
+            self.broadcast(self.clients, protocol.stream_resolution_message(p.width, p.height))
+        self.broadcast(self.clients, protocol.display_config_message(list(self.displays)))
+
+    # ---------------------------------------------------------------- capture
+    def capture_settings(self, did: str, w: int, h: int, x: int, y: int):
+        import pixelflux
+        st = self.displays[did]
+        p = st.params
+        enc = p.get("encoder") or self.settings.encoder
+        cs = pixelflux.default_settings(w, h)
+        cs.capture_x, cs.capture_y = x, y
+        cs.target_fps = float(p.get("framerate") or 60)
+        cs.capture_cursor = int(self.capture_cursor)
+        cs.debug_logging = int(self.settings.debug[0])
+        if enc == "jpeg":
+            cs.output_mode = 0
+            cs.jpeg_quality = int(p["jpeg_quality"])
+            cs.paint_over_jpeg_quality = int(p["paint_over_jpeg_quality"])
+            cs.stripe_height = 64
+        else:
+            cs.output_mode = 1
+            cs.h264_crf = int(p["h264_crf"])
+            cs.h264_paintover_crf = int(p["h264_paintover_crf"])
+            cs.h264_paintover_burst_frames = int(p["h264_paintover_burst_frames"])
+            cs.h264_fullcolor = int(bool(p["h264_fullcolor"]))
+            cs.h264_streaming_mode = int(bool(p["h264_streaming_mode"]))
+            cs.h264_fullframe = int(enc == "x264enc")
+        cs.use_paint_over_quality = int(bool(p["use_paint_over_quality"]))
+        cs.paint_over_trigger_frames, cs.damage_block_threshold, cs.damage_block_duration = 15, 10, 20
+        cs.use_cpu = int(bool(p["use_cpu"]))
+        index = list(self.displays).index(did)
+        cs.device = (self.gpu_id + index) % self.num_gpus
+        cs.source = {"auto": -1, "x11": 0, "synthetic": 2, "motion": 1, "noise": 3}.get(self.capture_source, -1)
+        wm = self.settings.watermark_path
+        if wm and os.path.exists(wm):
+            cs.watermark_path = wm.encode()
+            cs.watermark_location_enum = int(self.settings.watermark_location)
+        return cs, enc
+
+    async def _start_capture(self, did: str, w: int, h: int, x: int, y: int):
+        if did in self.captures:
+            return
+        try:
+            cs, enc = self.capture_settings(did, w, h, x, y)
+        except KeyError:
+            return
+        loop = asyncio.get_running_loop()
+        queue: asyncio.Queue = asyncio.Queue(maxsize=VIDEO_QUEUE_SIZE)
+        jpeg = enc == "jpeg"
+
+        def on_stripe(res_ptr, user):
+            r = res_ptr.contents
+            if r.size <= 0:
+                return
+            data = bytes(r.data[:r.size])
+            item = (protocol.JPEG_PREFIX + data if jpeg else data, r.frame_id & 0xFFFF)
+            loop.call_soon_threadsafe(_put_drop, queue, item)
+
+        import pixelflux
+        cb = pixelflux.StripeCallback(on_stripe)
+        module = self.capture_factory()
+        sender = asyncio.create_task(self._video_sender(did, queue))
+        try:
+            await loop.run_in_executor(None, module.start_capture, cs, cb)
+        except Exception as e:
+            sender.cancel()
+            log.error("capture start failed for %s: %s", did, e)
+            return
+        cap = Capture(did, module, queue, sender)
+        cap.callback = cb
+        self.captures[did] = cap
+        st = self.displays.get(did)
+        if st is not None:
+            st.flow.reset(self.clock())
+            await self._start_bp(did)
+        if self.metrics is not None:
+            self.metrics.capture_started(did, module)
+
+    async def _stop_capture(self, did: str):
+        await self._stop_bp(did)
+        cap = self.captures.pop(did, None)
+        if cap is None:
+            return
+        try:
+            await asyncio.get_running_loop().run_in_executor(None, cap.module.stop_capture)
+        except Exception as e:
+            log.error("stop_capture failed for %s: %s", did, e)
+        cap.sender.cancel()
+        try:
+            await cap.sender
+        except (asyncio.CancelledError, Exception):
+            pass
+        if self.metrics is not None:
+            self.metrics.capture_stopped(did)
+
+    async def _video_sender(self, did: str, queue: asyncio.Queue):
+        was_enabled = True
+        while True:
+            data, fid = await queue.get()
+            st = self.displays.get(did)
+            if st is None:
+                continue
+            if not st.flow.enabled:
+                was_enabled = False
+                continue
+            if not was_enabled:
+                # frames were skipped while backpressured: resynchronise decoders
+                was_enabled = True
+                cap = self.captures.get(did)
+                if cap is not None and hasattr(cap.module, "request_keyframe"):
+                    cap.module.request_keyframe()
+            st.flow.on_sent(fid, self.clock())
+            viewers = self.primary_viewers() if did == "primary" else {st.client}
+            self.broadcast(viewers, data)
+
+    # ---------------------------------------------------------------- backpressure
+    async def _start_bp(self, did: str):
+        await self._stop_bp(did)
+        st = self.displays.get(did)
+        if st is not None:
+            st.bp_task = asyncio.create_task(self._bp_loop(did))
+
+    async def _stop_bp(self, did: str):
+        st = self.displays.get(did)
+        if st is None or st.bp_task is None:
+            return
+        t, st.bp_task = st.bp_task, None
+        t.cancel()
+        try:
+            await t
+        except (asyncio.CancelledError, Exception):
+            pass
+        st.flow.reset(self.clock())
+        msg = f"PIPELINE_RESETTING {did}"
+        if did == "primary":
+            self.broadcast(self.clients, msg)
+        else:
+            st.client.send(msg)
+
+    async def _bp_loop(self, did: str):
+        await self.settings_received.wait()
+        while True:
+            await asyncio.sleep(protocol.CHECK_INTERVAL_S)
+            st = self.displays.get(did)
+            if st is None:
+                return
+            before = st.flow.enabled
+            after = st.flow.evaluate(self.clock(), did in self.captures, float(st.params.get("framerate") or 60))
+            if before != after:
+                log.warning("backpressure %s for '%s' (sent %d, acked %d, rtt %.1f ms)",
+                            "lifted" if after else "engaged", did, st.flow.last_sent, st.flow.acknowledged,
+                            st.flow.smoothed_rtt_ms)
+
+    def _primary_rtt(self) -> float:
+        p = self.displays.get("primary")
+        return p.flow.smoothed_rtt_ms if p else 0.0
+
+    def set_client_fps(self, fps: int, did: str = "primary"):
+        st = self.displays.get(did)
+        if st is not None:
+            st.flow.client_fps = float(fps)
+
+
+def _put_drop(q: asyncio.Queue, item):
+    try:
+        q.put_nowait(item)
+    except asyncio.QueueFull:
+        pass
+
+
+class _UploadState:
+    """Per-connection upload (``FILE_UPLOAD_START`` / 0x01 chunks / END / ERROR)."""
+
+    def __init__(self, root: Optional[str]):
+        self.root = root
+        self.path: Optional[str] = None
+        self.fh = None
+        self.expected = 0
+        self.written = 0
+
+    def start(self, msg: str):
+        if not self.root:
+            log.error("upload refused: no upload directory")
+            return
+        try:
+            rel, size = protocol.parse_upload_start(msg)
+        except ValueError:
+            log.error("malformed %s", msg[:200])
+            return
+        target = protocol.sanitize_upload_path(self.root, rel)
+        if target is None:
+            log.error("upload path rejected: %r", rel)
+            return
+        self.finish()
+        try:
+            os.makedirs(os.path.dirname(target), exist_ok=True)
+            self.fh = open(target, "wb")
+        except OSError as e:
+            log.error("cannot open %s: %s", target, e)
+            return
+        self.path, self.expected, self.written = target, size, 0
+
+    def write(self, data: bytes):
+        if self.fh is None:
+            return
+        try:
+            self.fh.write(data)
+            self.written += len(data)
+        except OSError as e:
+            log.error("upload write failed: %s", e)
+            self.abort()
+
+    def finish(self):
+        if self.fh is not None:
+            self.fh.close()
+            log.info("upload finished: %s (%d bytes)", self.path, self.written)
+        self.fh, self.path = None, None
+
+    def abort(self):
+        if self.fh is not None:
+            self.fh.close()
+            try:
+                os.remove(self.path)
+            except OSError:
+                pass
+        self.fh, self.path = None, None

@@ -1,0 +1,221 @@
+"""End-to-end data-websocket sessions against a live server (aiohttp client).
+
+The server runs with the synthetic capture source and the CPU reference
+encoders (``--use-cpu true``) so the full path — SETTINGS -> display layout ->
+native capture session -> stripe packets -> websocket -> decode — runs on CPU.
+The GPU twin of this test lives in test_server_gpu.py.
+"""
+import asyncio
+import json
+import os
+
+import aiohttp
+import numpy as np
+import pytest
+
+from selkies_gstreamer_amd.server.data_server import DataStreamingServer
+from selkies_gstreamer_amd.server.input import InputHandler, RecordingInjector
+from selkies_gstreamer_amd.server.settings import Settings
+from tests.h264_util import StripeDecoder
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 60))
+
+
+async def _server(tmp_path, argv=(), with_input=False):
+    s = Settings(["--port", "0", "--use-cpu", "true", "--audio-enabled", "false", *argv], env={})
+    rec = RecordingInjector()
+
+    async def factory(server):
+        return InputHandler(rec)
+    srv = DataStreamingServer(s, upload_dir=str(tmp_path / "up"), capture_source="synthetic",
+                              input_factory=factory if with_input else None)
+    port = await srv.start("127.0.0.1", 0)
+    return srv, port, rec
+
+
+async def _recv_until(ws, pred, timeout=10.0):
+    """Reads messages until pred(msg) is true; returns (match, all_messages)."""
+    seen = []
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while True:
+        msg = await asyncio.wait_for(ws.receive(), max(0.01, end - loop.time()))
+        if msg.type in (aiohttp.WSMsgType.CLOSE, aiohttp.WSMsgType.CLOSED, aiohttp.WSMsgType.ERROR):
+            raise ConnectionError(f"closed: {msg}")
+        seen.append(msg.data)
+        if pred(msg.data):
+            return msg.data, seen
+
+
+def _settings(w=256, h=128, **kw):
+    d = {"initialClientWidth": w, "initialClientHeight": h, "framerate": 30, "encoder": "x264enc-striped"}
+    d.update(kw)
+    return "SETTINGS," + json.dumps(d)
+
+
+def test_session_h264_striped(tmp_path):
+    async def main():
+        srv, port, _ = await _server(tmp_path)
+        async with aiohttp.ClientSession() as sess:
+            async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket") as ws:
+                first = await ws.receive()
+                assert first.data == "MODE websockets"
+                ss, _ = await _recv_until(ws, lambda m: isinstance(m, str) and "server_settings" in m)
+                assert json.loads(ss)["settings"]["encoder"]["value"] == "x264enc"
+                await ws.send_str(_settings())
+                res, seen = await _recv_until(ws, lambda m: isinstance(m, str) and "stream_resolution" in m)
+                assert json.loads(res) == {"type": "stream_resolution", "width": 256, "height": 128}
+                dec = StripeDecoder(256, 128)
+                pending = [m for m in seen if isinstance(m, bytes)]
+                n = 0
+                while n < 8:
+                    if pending:
+                        data = pending.pop(0)
+                    else:
+                        data = (await asyncio.wait_for(ws.receive(), 10)).data
+                    if isinstance(data, bytes):
+                        assert data[0] == 0x04
+                        dec.feed(data)
+                        fid = int.from_bytes(data[2:4], "big")
+                        await ws.send_str(f"CLIENT_FRAME_ACK {fid}")
+                        n += 1
+                assert srv.displays["primary"].flow.acknowledged >= 0
+                assert dec.Y.std() > 1.0  # decoded real content
+                # resize -> new resolution broadcast
+                await ws.send_str("r,320x160,primary")
+                res, _ = await _recv_until(ws, lambda m: isinstance(m, str) and "stream_resolution" in m)
+                assert json.loads(res)["width"] == 320
+                # stop / start video
+                await ws.send_str("STOP_VIDEO")
+                await _recv_until(ws, lambda m: m == "VIDEO_STOPPED")
+                assert "primary" not in srv.captures
+                await ws.send_str("START_VIDEO")
+                await _recv_until(ws, lambda m: m == "VIDEO_STARTED")
+                assert "primary" in srv.captures
+        await asyncio.sleep(0.2)
+        assert not srv.captures and not srv.displays
+        await srv.stop()
+    run(main())
+
+
+def test_session_jpeg_and_fullframe(tmp_path):
+    async def main():
+        srv, port, _ = await _server(tmp_path)
+        async with aiohttp.ClientSession() as sess:
+            async with sess.ws_connect(f"http://127.0.0.1:{port}/") as ws:
+                await ws.send_str(_settings(192, 128, encoder="jpeg", jpeg_quality=60))
+                data, _ = await _recv_until(ws, lambda m: isinstance(m, bytes))
+                assert data[:2] == b"\x03\x00" and data[6:8] == b"\xff\xd8"
+                # switch encoder to full-frame H.264 (video params change -> capture restart)
+                await ws.send_str(_settings(192, 128, encoder="x264enc"))
+                data, _ = await _recv_until(ws, lambda m: isinstance(m, bytes) and m[0] == 0x04)
+                assert int.from_bytes(data[4:6], "big") == 0  # full frame: y = 0
+        await srv.stop()
+    run(main())
+
+
+def test_takeover_kill_and_debounce(tmp_path):
+    async def main():
+        srv, port, _ = await _server(tmp_path)
+        async with aiohttp.ClientSession() as sess:
+            ws1 = await sess.ws_connect(f"http://127.0.0.1:{port}/")
+            await ws1.send_str(_settings())
+            await _recv_until(ws1, lambda m: isinstance(m, str) and "stream_resolution" in m)
+            # immediate reconnect from the same IP -> rate limited
+            ws_fast = await sess.ws_connect(f"http://127.0.0.1:{port}/")
+            m = await ws_fast.receive()
+            assert m.type == aiohttp.WSMsgType.CLOSE and ws_fast.close_code == 4029
+            await asyncio.sleep(0.6)
+            ws2 = await sess.ws_connect(f"http://127.0.0.1:{port}/")
+            await ws2.send_str(_settings())
+            kill, _ = await _recv_until(ws1, lambda m: isinstance(m, str) and m.startswith("KILL"))
+            assert "primary" in kill
+            await _recv_until(ws2, lambda m: isinstance(m, bytes))
+            await ws2.close()
+            await ws1.close()
+        await srv.stop()
+    run(main())
+
+
+def test_second_screen_layout(tmp_path):
+    async def main():
+        srv, port, _ = await _server(tmp_path)
+        async with aiohttp.ClientSession() as sess:
+            p = await sess.ws_connect(f"http://127.0.0.1:{port}/")
+            await p.send_str(_settings(256, 128))
+            await _recv_until(p, lambda m: isinstance(m, bytes))
+            await asyncio.sleep(0.6)
+            d2 = await sess.ws_connect(f"http://127.0.0.1:{port}/")
+            await d2.send_str(_settings(128, 64, displayId="display2", displayPosition="down"))
+            cfg, _ = await _recv_until(p, lambda m: isinstance(m, str) and m.startswith("DISPLAY_CONFIG_UPDATE")
+                                       and "display2" in m)
+            assert json.loads(cfg.split(",", 1)[1])["displays"] == ["primary", "display2"]
+            assert srv.layouts["display2"] == {"x": 0, "y": 128, "w": 128, "h": 64}
+            data, _ = await _recv_until(d2, lambda m: isinstance(m, bytes))
+            assert int.from_bytes(data[6:8], "big") == 128  # display2's own stream width
+            await d2.close()
+            await p.close()
+        await srv.stop()
+    run(main())
+
+
+def test_second_screen_refused_when_disabled(tmp_path):
+    async def main():
+        srv, port, _ = await _server(tmp_path, ["--second-screen", "false"])
+        async with aiohttp.ClientSession() as sess:
+            ws = await sess.ws_connect(f"http://127.0.0.1:{port}/")
+            await ws.send_str(_settings(displayId="display2"))
+            kill, _ = await _recv_until(ws, lambda m: isinstance(m, str) and m.startswith("KILL"))
+            assert "disabled" in kill
+            await ws.close()
+        await srv.stop()
+    run(main())
+
+
+def test_upload_and_commands(tmp_path):
+    async def main():
+        srv, port, rec = await _server(tmp_path, ["--command-enabled", "false"], with_input=True)
+        async with aiohttp.ClientSession() as sess:
+            ws = await sess.ws_connect(f"http://127.0.0.1:{port}/")
+            await ws.send_str("FILE_UPLOAD_START:docs/a.txt:6")
+            await ws.send_bytes(b"\x01abc")
+            await ws.send_bytes(b"\x01def")
+            await ws.send_str("FILE_UPLOAD_END:docs/a.txt")
+            await ws.send_str("FILE_UPLOAD_START:../escape.txt:1")
+            await ws.send_bytes(b"\x01x")
+            await ws.send_str("FILE_UPLOAD_END:../escape.txt")
+            await ws.send_str("FILE_UPLOAD_START:b.bin:10")
+            await ws.send_bytes(b"\x01partial")
+            await ws.send_str("FILE_UPLOAD_ERROR:b.bin:cancelled")
+            await ws.send_str("cmd,touch " + str(tmp_path / "should_not_exist"))
+            await ws.send_str("kd,97")
+            await ws.send_str("ku,97")
+            await asyncio.sleep(0.3)
+            await ws.close()
+        assert (tmp_path / "up" / "docs" / "a.txt").read_bytes() == b"abcdef"
+        assert not (tmp_path / "escape.txt").exists() and not (tmp_path / "up" / "b.bin").exists()
+        assert not (tmp_path / "should_not_exist").exists()
+        assert rec.events == [("key", 97, True), ("key", 97, False)]
+        await srv.stop()
+    run(main())
+
+
+def test_static_and_health(tmp_path):
+    async def main():
+        web = tmp_path / "web"
+        web.mkdir()
+        (web / "index.html").write_text("<html>ok</html>")
+        s = Settings(["--port", "0"], env={})
+        srv = DataStreamingServer(s, capture_source="synthetic", web_root=str(web))
+        port = await srv.start("127.0.0.1", 0)
+        async with aiohttp.ClientSession() as sess:
+            async with sess.get(f"http://127.0.0.1:{port}/") as r:
+                assert r.status == 200 and "ok" in await r.text()
+            async with sess.get(f"http://127.0.0.1:{port}/health") as r:
+                assert r.status == 200
+            async with sess.get(f"http://127.0.0.1:{port}/../../etc/passwd") as r:
+                assert r.status == 404
+        await srv.stop()
+    run(main())
