@@ -128,20 +128,7 @@ void CpuJpegEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         bool dirty = first;
         for (int y = y0; y < y0 + h && !dirty; y++)
             dirty = memcmp(bgrx + (size_t)y * stride, &prev[(size_t)y * L.W * 4], (size_t)L.W * 4) != 0;
-        JpegStripeState& S = st[s];
-        int which = -1;
-        if (dirty || S.need_send) {
-            S.static_frames = 0;
-            S.painted = false;
-            S.need_send = false;
-            which = 0;
-        } else {
-            S.static_frames++;
-            if (cfg.use_paint_over && !S.painted && S.static_frames >= cfg.paint_over_trigger) {
-                S.painted = true;
-                which = 1;
-            }
-        }
+        const int which = jpeg_plan_stripe(st[s], dirty, cfg);
         if (which < 0) continue;
         h264::EncodedPacket pk;
         pk.y = y0;

@@ -26,6 +26,24 @@ struct JpegStripeState {
     bool need_send = true;
 };
 
+// Per-stripe send decision shared by both backends: -1 skip, 0 send at
+// `quality` (damaged / keyframe request), 1 send once at `paint_quality` after
+// `paint_over_trigger` static frames.
+inline int jpeg_plan_stripe(JpegStripeState& S, bool dirty, const JpegConfig& cfg) {
+    if (dirty || S.need_send) {
+        S.static_frames = 0;
+        S.painted = false;
+        S.need_send = false;
+        return 0;
+    }
+    S.static_frames++;
+    if (cfg.use_paint_over && !S.painted && S.static_frames >= cfg.paint_over_trigger) {
+        S.painted = true;
+        return 1;
+    }
+    return -1;
+}
+
 // Geometry + header cache shared by both backends.
 struct JpegLayout {
     int W = 0, H = 0, stripe_h = 0, num_stripes = 0, mcu_w = 0;
