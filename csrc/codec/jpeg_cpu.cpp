@@ -78,7 +78,7 @@ CpuJpegEncoder::CpuJpegEncoder(const JpegConfig& c) : cfg(c) {
 }
 
 void CpuJpegEncoder::request_keyframe() {
-    for (auto& s : st) s.need_send = true;
+    for (auto& s : st) s.need_send = 1;
 }
 
 void CpuJpegEncoder::encode_stripe(const uint8_t* bgrx, int stride, int s, const JpegTables& t,
@@ -128,7 +128,7 @@ void CpuJpegEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         bool dirty = first;
         for (int y = y0; y < y0 + h && !dirty; y++)
             dirty = memcmp(bgrx + (size_t)y * stride, &prev[(size_t)y * L.W * 4], (size_t)L.W * 4) != 0;
-        const int which = jpeg_plan_stripe(st[s], dirty, cfg);
+        const int which = jpeg_plan_stripe(st[s], dirty, cfg.use_paint_over, cfg.paint_over_trigger);
         if (which < 0) continue;
         h264::EncodedPacket pk;
         pk.y = y0;

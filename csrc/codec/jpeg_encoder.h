@@ -22,23 +22,24 @@ struct JpegConfig {
 
 struct JpegStripeState {
     int static_frames = 0;
-    bool painted = true;
-    bool need_send = true;
+    int painted = 1;
+    int need_send = 1;
 };
 
 // Per-stripe send decision shared by both backends: -1 skip, 0 send at
 // `quality` (damaged / keyframe request), 1 send once at `paint_quality` after
 // `paint_over_trigger` static frames.
-inline int jpeg_plan_stripe(JpegStripeState& S, bool dirty, const JpegConfig& cfg) {
+// Runs on the host (CPU backend) and on the device (k_decide) alike.
+SK_HD int jpeg_plan_stripe(JpegStripeState& S, bool dirty, int use_paint_over, int paint_over_trigger) {
     if (dirty || S.need_send) {
         S.static_frames = 0;
-        S.painted = false;
-        S.need_send = false;
+        S.painted = 0;
+        S.need_send = 0;
         return 0;
     }
     S.static_frames++;
-    if (cfg.use_paint_over && !S.painted && S.static_frames >= cfg.paint_over_trigger) {
-        S.painted = true;
+    if (use_paint_over && !S.painted && S.static_frames >= paint_over_trigger) {
+        S.painted = 1;
         return 1;
     }
     return -1;

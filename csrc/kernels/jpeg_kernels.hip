@@ -2,6 +2,8 @@
 //
 //   k_damage  per-stripe BGRx compare against the previous frame (all 4 bytes,
 //             like the CPU memcmp; 16-byte loads, one ballot + atomicOr per wave)
+//             the last workgroup to finish runs the per-stripe send / paint-over
+//             plan (same function as the CPU backend): one host sync per frame
 //   k_blocks  one 64-lane wave per 8x8 block: BGRx -> Y / 2x2-averaged Cb,Cr,
 //             separable integer FDCT through LDS (lane = coefficient), exact
 //             rounding quantisation (32-bit division), zig-zag permute via LDS,
@@ -12,10 +14,12 @@
 //             clears the stripe's bit buffer
 //   k_write   one wave per block again: every lane builds its own symbol string
 //             (ZRLs + code + amplitude, DC on lane 0, EOB on lane 63), a wave
-//             prefix sum places it, atomicOr writes it into a big-endian buffer
-//   k_stuff   one workgroup per stripe: 1-bit padding, 0xFF -> 0xFF 0x00 byte
-//             stuffing as a tile-wise prefix count, EOI, then a 16-byte copy of
-//             the finished entropy segment into host-mapped memory
+//             prefix sum places it, ds_or assembles the block in LDS and the wave
+//             stores whole words (global atomics only on the two edge words)
+//   k_ffcount / k_stuff  4 KiB tiles: per-tile 0xFF counts, then every tile
+//             workgroup stuffs (0xFF -> 0xFF 0x00, 1-bit padding, EOI on the last
+//             tile) into LDS and streams it to host-mapped memory with 16-byte
+//             stores
 //
 // Bit-exact with the CPU reference (jpeg_cpu.cpp); the host prepends the
 // JFIF header (it only depends on quality and stripe height).
@@ -98,7 +102,37 @@ __device__ __forceinline__ void load_tables(const JpegTables* src, JpegTables* d
 }
 
 // ---------------------------------------------------------------------------
+// Stripe send plan (same function as the CPU backend); run by the last
+// workgroup of k_damage once every dirty flag of the frame is visible.
+__device__ void decide_stripes(const JpegArgs& a) {
+    __shared__ int key;
+    if (threadIdx.x == 0) {
+        const int seq = *a.key_seq;
+        key = seq != a.ctl[1];
+        a.ctl[1] = seq;
+    }
+    __syncthreads();
+    const int first = a.ctl[0];
+    for (int s = threadIdx.x; s < a.num_stripes; s += blockDim.x) {
+        JpegStripeState S = a.state[s];
+        if (key) S.need_send = 1;
+        const int dirty = __hip_atomic_load(&a.stripe_dirty[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int act = jpeg_plan_stripe(S, first || dirty, a.use_paint_over, a.paint_over_trigger);
+        a.state[s] = S;
+        a.action[s] = act;
+        a.host_action[s] = act;
+        if (act < 0) a.host_size[s] = 0;
+        a.stripe_dirty[s] = 0;  // self-cleaning for the next frame
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a.ctl[0] = 0;
+        a.ctl[2] = 0;  // reset the workgroup-completion counter
+    }
+}
+
 __global__ __launch_bounds__(256) void k_damage(JpegArgs a) {
+    __shared__ int last;
     const int s = blockIdx.y;
     const int y0 = s * a.stripe_h;
     int h = a.H - y0;
@@ -120,7 +154,25 @@ __global__ __launch_bounds__(256) void k_damage(JpegArgs a) {
             for (int i = threadIdx.x; i < a.W; i += blockDim.x) diff |= c[i] != p[i];
         }
     }
-    if (__ballot(diff) && lane_id() == 0) atomicOr(&a.stripe_dirty[s], 1);
+    // One plain store per workgroup (same-address atomics from every wave
+    // serialise in L2, ~35 ns each). Completion is counted hierarchically:
+    // per stripe (gridDim.x workgroups), then per frame (num_stripes).
+    if (__syncthreads_or(diff) && threadIdx.x == 0) a.stripe_dirty[s] = 1;
+    if (threadIdx.x == 0) {
+        __threadfence();
+        int fin = 0;
+        if (atomicAdd(&a.ctl[32 * (s + 1)], 1) == (int)gridDim.x - 1) {  // one 128 B line per stripe
+            a.ctl[32 * (s + 1)] = 0;
+            __threadfence();
+            fin = atomicAdd(&a.ctl[2], 1) == (int)gridDim.y - 1;
+        }
+        last = fin;
+    }
+    __syncthreads();
+    if (last) {
+        __threadfence();
+        decide_stripes(a);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -144,9 +196,10 @@ __global__ __launch_bounds__(256) void k_blocks(JpegArgs a) {
     const int w = tid >> 6, l = lane_id();
     const int nblk = stripe_mcu_rows(a, s) * a.mcu_w * 6;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
-    const int blk = wg * 4 + w;
-    if (blk >= nblk) return;  // whole wave leaves; no block barrier follows
-    const int mcu = blk / 6, b = blk - mcu * 6;
+    const int mcu = wg * 4 + w;  // one MCU (6 blocks) per wave: tables loaded once per 24 blocks
+    if (mcu * 6 >= nblk) return;  // whole wave leaves; no block barrier follows
+    for (int b = 0; b < 6; b++) {
+    const int blk = mcu * 6 + b;
     const int my = mcu / a.mcu_w, mx = mcu - my * a.mcu_w;
     const int y0 = s * a.stripe_h;
     const int yy = l >> 3, xx = l & 7;
@@ -216,6 +269,7 @@ __global__ __launch_bounds__(256) void k_blocks(JpegArgs a) {
         a.ac_bits[gblk] = total;
         a.dc[gblk] = (int16_t)zz;
     }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -280,6 +334,7 @@ __device__ __forceinline__ void put_bits(uint32_t* buf, int pos, unsigned long l
 
 __global__ __launch_bounds__(256) void k_write(JpegArgs a) {
     __shared__ JpegTables sT;
+    __shared__ uint32_t sBits[4][kBlockWords];
     const int s = blockIdx.y;
     const int act = a.action[s];
     if (act < 0) return;
@@ -288,12 +343,15 @@ __global__ __launch_bounds__(256) void k_write(JpegArgs a) {
     const int w = threadIdx.x >> 6, l = lane_id();
     const int nblk = stripe_mcu_rows(a, s) * a.mcu_w * 6;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
-    const int blk = wg * 4 + w;
-    if (blk >= nblk) return;
-    const int b = blk % 6;
+    const int mcu = wg * 4 + w;
+    if (mcu * 6 >= nblk) return;
+    for (int b = 0; b < 6; b++) {
+    const int blk = mcu * 6 + b;
     const int c = b < 4 ? 0 : 1;
     const size_t gblk = (size_t)s * a.blocks_per_stripe + blk;
     const int zz = a.coef[gblk * 64 + l];
+    wave_sync();  // previous block's LDS words have been stored
+    if (l < kBlockWords) sBits[w][l] = 0u;
     const unsigned long long mask = __ballot(l > 0 && zz != 0);
     unsigned long long acc = 0;
     int n = 0;
@@ -326,72 +384,139 @@ __global__ __launch_bounds__(256) void k_write(JpegArgs a) {
         acc = (acc << sT.ac_len[c][0]) | sT.ac_code[c][0];
         n += sT.ac_len[c][0];
     }
-    const int pos = a.blk_off[gblk] + wave_incl_scan(n) - n;
-    put_bits(a.bits + (size_t)s * a.bits_slot_words, pos, acc, n);
+    const int off = a.blk_off[gblk];
+    const int bit0 = off & 31;
+    const int incl = wave_incl_scan(n);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    wave_sync();
+    put_bits(sBits[w], bit0 + incl - n, acc, n);  // ds_or_b32 into the wave's LDS block buffer
+    wave_sync();
+    const int nwords = (bit0 + total + 31) >> 5;
+    if (l < nwords) {
+        uint32_t* dst = a.bits + (size_t)s * a.bits_slot_words + (off >> 5);
+        const uint32_t v = sBits[w][l];
+        if (l == 0 || l == nwords - 1) {
+            if (v) atomicOr(&dst[l], v);  // edge words are shared with the neighbour blocks
+        } else {
+            dst[l] = v;
+        }
+    }
+    }
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_stuff(JpegArgs a) {
-    __shared__ int wave_tot[17];
-    const int s = blockIdx.x, tid = threadIdx.x;
-    if (a.action[s] < 0) {
-        if (tid == 0) a.host_size[s] = 0;
-        return;
-    }
+// Byte i of a stripe's entropy segment with the final partial byte padded by 1s.
+__device__ __forceinline__ uint8_t seg_byte(uint32_t word, int j, int i, int n, int rem) {
+    uint8_t v = (uint8_t)(word >> (24 - 8 * j));
+    if (i == n - 1 && rem) v |= (uint8_t)((1u << (8 - rem)) - 1u);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_ffcount(JpegArgs a) {
+    __shared__ int red[4];
+    const int s = blockIdx.y, t = blockIdx.x;
+    if (a.action[s] < 0) return;
     const int nbits = a.stripe_bits[s];
     const int n = (nbits + 7) >> 3, rem = nbits & 7;
+    const int t0 = t * kTileBytes;
+    if (t0 >= n) return;
     const uint32_t* buf = a.bits + (size_t)s * a.bits_slot_words;
-    uint8_t* out = a.stage + (size_t)s * a.out_slot;
-    int carry = 0;
-    for (int t0 = 0; t0 < n; t0 += 4096) {
-        const int i0 = t0 + tid * 4;
-        uint32_t word = i0 < n ? buf[i0 >> 2] : 0u;  // i0 is 4-aligned: one word holds the 4 bytes
-        uint8_t by[4];
-        int cnt = 0;
+    const int i0 = t0 + threadIdx.x * 16;
+    int cnt = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            int i = i0 + j;
-            uint8_t v = (uint8_t)(word >> (24 - 8 * j));
-            if (i == n - 1 && rem) v |= (uint8_t)((1u << (8 - rem)) - 1u);
-            by[j] = v;
-            cnt += (i < n && v == 0xFF);
-        }
-        int tile_total;
-        int ex = block_excl_scan<16>(cnt, wave_tot, &tile_total);
-        int o = i0 + carry + ex;
+    for (int q = 0; q < 4; q++) {
+        const int iq = i0 + 4 * q;
+        if (iq >= n) break;
+        const uint32_t word = buf[iq >> 2];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (i0 + j < n) {
-                out[o++] = by[j];
-                if (by[j] == 0xFF) out[o++] = 0x00;
-            }
-        }
-        carry += tile_total;
+        for (int j = 0; j < 4; j++) cnt += (iq + j < n) && seg_byte(word, j, iq + j, n, rem) == 0xFF;
     }
-    const int size = n + carry + 2;
-    if (tid == 0) {
-        out[n + carry] = 0xFF;
-        out[n + carry + 1] = 0xD9;
-    }
-    __threadfence();
+    cnt = wave_sum(cnt);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = cnt;
     __syncthreads();
-    const uint4* src = reinterpret_cast<const uint4*>(out);
-    uint4* dst = reinterpret_cast<uint4*>(a.host_out + (size_t)s * a.out_slot);
-    for (int v = tid; v < (size + 15) / 16; v += 1024) dst[v] = src[v];
-    if (tid == 0) a.host_size[s] = size;
+    if (threadIdx.x == 0) a.tile_ff[s * a.max_tiles + t] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void k_stuff(JpegArgs a) {
+    __shared__ int wave_tot[5];
+    __shared__ int sh_prefix;
+    __shared__ uint8_t sOut[2 * kTileBytes + 16];
+    const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x;
+    if (a.action[s] < 0) return;
+    const int nbits = a.stripe_bits[s];
+    const int n = (nbits + 7) >> 3, rem = nbits & 7;
+    const int t0 = t * kTileBytes;
+    if (t0 >= n) return;
+    if (tid < 64) {  // 0xFF count of all earlier tiles of this stripe
+        int p = 0;
+        for (int k = tid; k < t; k += 64) p += a.tile_ff[s * a.max_tiles + k];
+        p = wave_sum(p);
+        if (tid == 0) sh_prefix = p;
+    }
+    const uint32_t* buf = a.bits + (size_t)s * a.bits_slot_words;
+    const int i0 = t0 + tid * 16;
+    uint8_t by[16];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int iq = i0 + 4 * q;
+        const uint32_t word = iq < n ? buf[iq >> 2] : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            by[4 * q + j] = seg_byte(word, j, iq + j, n, rem);
+            cnt += (iq + j < n) && by[4 * q + j] == 0xFF;
+        }
+    }
+    int tile_ff;
+    const int ex = block_excl_scan<4>(cnt, wave_tot, &tile_ff);
+    int o = tid * 16 + ex;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        if (i0 + k < n) {
+            sOut[o++] = by[k];
+            if (by[k] == 0xFF) sOut[o++] = 0x00;
+        }
+    }
+    const int in_len = min(n - t0, kTileBytes);
+    const bool last = t0 + kTileBytes >= n;
+    int len = in_len + tile_ff;
+    if (last && tid == 0) {
+        sOut[len] = 0xFF;
+        sOut[len + 1] = 0xD9;
+    }
+    __syncthreads();
+    if (last) len += 2;
+    const int g0 = t0 + sh_prefix;  // output position inside the stripe slot
+    uint8_t* dst = a.host_out + (size_t)s * a.out_slot;
+    const int head = min(len, (16 - (g0 & 15)) & 15);
+    if (tid < head) dst[g0 + tid] = sOut[tid];
+    const int nvec = (len - head) >> 4;
+    for (int v = tid; v < nvec; v += 256) {
+        const uint8_t* p = sOut + head + 16 * v;
+        uint4 x;
+        x.x = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
+        x.y = p[4] | (p[5] << 8) | (p[6] << 16) | ((uint32_t)p[7] << 24);
+        x.z = p[8] | (p[9] << 8) | (p[10] << 16) | ((uint32_t)p[11] << 24);
+        x.w = p[12] | (p[13] << 8) | (p[14] << 16) | ((uint32_t)p[15] << 24);
+        *reinterpret_cast<uint4*>(dst + g0 + head + 16 * v) = x;
+    }
+    const int tail0 = head + 16 * nvec;
+    if (tid < len - tail0) dst[g0 + tail0 + tid] = sOut[tail0 + tid];
+    if (last && tid == 0) a.host_size[s] = n + sh_prefix + tile_ff + 2;
 }
 
 // ---------------------------------------------------------------------------
 void launch_damage(const JpegArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_damage, dim3(16, a.num_stripes), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_damage, dim3((a.stripe_h + 1) / 2, a.num_stripes), dim3(256), 0, st, a);  // 2 rows/WG
 }
 
 void launch_encode(const JpegArgs& a, hipStream_t st) {
-    const int wgs = (a.blocks_per_stripe + 3) / 4;
+    const int wgs = (a.blocks_per_stripe + 23) / 24;  // 4 waves x 1 MCU
     hipLaunchKernelGGL(k_blocks, dim3(wgs, a.num_stripes), dim3(256), 0, st, a);
     hipLaunchKernelGGL(k_scan, dim3(a.num_stripes), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(k_write, dim3(wgs, a.num_stripes), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_stuff, dim3(a.num_stripes), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(k_ffcount, dim3(a.max_tiles, a.num_stripes), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_stuff, dim3(a.max_tiles, a.num_stripes), dim3(256), 0, st, a);
 }
 
 }  // namespace gpu

@@ -121,7 +121,8 @@ class HipBackend : public EncoderBackend {
             if (dst && cap >= n) memcpy(dst, h_tasks_, (size_t)n);
             return n;
         } else return -1;
-        if (dst && cap >= n) HIPCHECK(hipMemcpy(dst, p, (size_t)n, hipMemcpyDeviceToHost));
+        if (dst && cap >= n) HIPCHECK(hipMemcpyAsync(dst, p, (size_t)n, hipMemcpyDeviceToHost, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
         return n;
     }
 
@@ -130,7 +131,7 @@ class HipBackend : public EncoderBackend {
     T* dmalloc(size_t count, bool zero = true) {
         void* p = nullptr;
         HIPCHECK(hipMalloc(&p, count * sizeof(T)));
-        if (zero) HIPCHECK(hipMemset(p, 0, count * sizeof(T)));
+        if (zero) HIPCHECK(hipMemsetAsync(p, 0, count * sizeof(T), stream_));
         dev_allocs_.push_back(p);
         return (T*)p;
     }
@@ -206,9 +207,11 @@ class HipBackend : public EncoderBackend {
             lens[s] = (int)v.size();
         }
         uint8_t* dps = dmalloc<uint8_t>(flat.size());
-        HIPCHECK(hipMemcpy(dps, flat.data(), flat.size(), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpyAsync(dps, flat.data(), flat.size(), hipMemcpyHostToDevice, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
         int* dlen = dmalloc<int>(ns);
-        HIPCHECK(hipMemcpy(dlen, lens.data(), sizeof(int) * ns, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpyAsync(dlen, lens.data(), sizeof(int) * ns, hipMemcpyHostToDevice, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
         a.param_sets = dps;
         a.param_set_len = dlen;
         d_frame_params_ = dmalloc<int>(4);
@@ -249,7 +252,7 @@ class HipBackend : public EncoderBackend {
         hipGraphExec_t& gx = graph_exec_[parity_];
         if (!gx) {
             hipGraph_t graph;
-            HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+            HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
             enqueue_encode();
             HIPCHECK(hipStreamEndCapture(stream_, &graph));
             HIPCHECK(hipGraphInstantiate(&gx, graph, nullptr, nullptr, 0));

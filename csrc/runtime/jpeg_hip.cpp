@@ -1,9 +1,9 @@
 // HIP backend of the JPEG stripe encoder. Frame flow:
-//   H2D(BGRx into the ping-pong frame buffer) -> k_damage -> D2H(dirty bits)
-//   -> host stripe plan (shared jpeg_plan_stripe) -> H2D(actions)
-//   -> [k_blocks, k_scan, k_write, k_stuff] (one hipGraph per frame-buffer parity)
-//   -> sync -> packets = [frame_id][y] + cached JFIF header + entropy segment
-//      read straight out of host-mapped memory.
+//   H2D(BGRx into the ping-pong frame buffer)
+//   -> [k_damage(+plan), k_blocks, k_scan, k_write, k_ffcount, k_stuff]
+//      (one hipGraph per frame-buffer parity; stripe plan state lives on the GPU)
+//   -> one sync -> packets = [frame_id][y] + cached JFIF header + entropy
+//      segment read straight out of host-mapped memory.
 #include "encoder_iface.h"
 #include "../kernels/jpeg_gpu.h"
 #include <hip/hip_runtime.h>
@@ -52,7 +52,8 @@ class HipJpegBackend : public EncoderBackend {
     }
 
     void request_keyframe() override {
-        for (auto& s : st_) s.need_send = true;
+        // consumed by k_damage's plan step on the next frame (host-mapped counter)
+        __atomic_add_fetch(h_key_seq_, 1, __ATOMIC_SEQ_CST);
     }
 
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
@@ -70,44 +71,37 @@ class HipJpegBackend : public EncoderBackend {
             for (auto& g : graph_)
                 if (g) { hipGraphExecDestroy(g); g = nullptr; }
         }
+        if (first_) {
+            const int ctl[3] = {1, *h_key_seq_, 0};
+            HIPCHECK(hipMemcpyAsync(a_.ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice, stream_));
+            HIPCHECK(hipStreamSynchronize(stream_));  // `ctl` is a stack array
+            first_ = false;
+        }
         a_.cur = frame_[parity_];
         a_.prev = frame_[parity_ ^ 1];
         HIPCHECK(hipMemcpyAsync(frame_[parity_], bgrx, bytes, hipMemcpyHostToDevice, stream_));
-        HIPCHECK(hipMemsetAsync(a_.stripe_dirty, 0, sizeof(int) * L_.num_stripes, stream_));
         gpu::launch_damage(a_, stream_);
-        HIPCHECK(hipMemcpyAsync(h_dirty_, a_.stripe_dirty, sizeof(int) * L_.num_stripes, hipMemcpyDeviceToHost,
-                                stream_));
+        run_graph();
         HIPCHECK(hipStreamSynchronize(stream_));
-        int any = 0;
         for (int s = 0; s < L_.num_stripes; s++) {
-            h_action_[s] = jpeg_plan_stripe(st_[s], first_ || h_dirty_[s] != 0, cfg_);
-            any |= h_action_[s] >= 0;
-        }
-        first_ = false;
-        if (any) {
-            HIPCHECK(hipMemcpyAsync(d_action_, h_action_, sizeof(int) * L_.num_stripes, hipMemcpyHostToDevice,
-                                    stream_));
-            run_graph();
-            HIPCHECK(hipStreamSynchronize(stream_));
-            for (int s = 0; s < L_.num_stripes; s++) {
-                if (h_action_[s] < 0) continue;
-                const int n = h_size_[s];
-                if (n <= 0 || n > a_.out_slot) throw std::runtime_error("JPEG stripe size out of range");
-                const std::vector<uint8_t>& hdr = hdr_[h_action_[s]][s == L_.num_stripes - 1 ? 1 : 0];
-                h264::EncodedPacket pk;
-                pk.y = L_.stripe_y(s);
-                pk.w = L_.W;
-                pk.h = L_.stripe_pix_h(s);
-                pk.key = 1;
-                pk.data.reserve(4 + hdr.size() + (size_t)n);
-                const uint8_t pre[4] = {(uint8_t)(frame_id >> 8), (uint8_t)frame_id, (uint8_t)(pk.y >> 8),
-                                        (uint8_t)pk.y};
-                pk.data.insert(pk.data.end(), pre, pre + 4);
-                pk.data.insert(pk.data.end(), hdr.begin(), hdr.end());
-                const uint8_t* seg = h_out_ + (size_t)s * a_.out_slot;
-                pk.data.insert(pk.data.end(), seg, seg + n);
-                packets_.push_back(std::move(pk));
-            }
+            const int act = h_action_[s];
+            if (act < 0) continue;
+            const int n = h_size_[s];
+            if (n <= 0 || n > a_.out_slot) throw std::runtime_error("JPEG stripe size out of range");
+            const std::vector<uint8_t>& hdr = hdr_[act][s == L_.num_stripes - 1 ? 1 : 0];
+            h264::EncodedPacket pk;
+            pk.y = L_.stripe_y(s);
+            pk.w = L_.W;
+            pk.h = L_.stripe_pix_h(s);
+            pk.key = 1;
+            pk.data.reserve(4 + hdr.size() + (size_t)n);
+            const uint8_t pre[4] = {(uint8_t)(frame_id >> 8), (uint8_t)frame_id, (uint8_t)(pk.y >> 8),
+                                    (uint8_t)pk.y};
+            pk.data.insert(pk.data.end(), pre, pre + 4);
+            pk.data.insert(pk.data.end(), hdr.begin(), hdr.end());
+            const uint8_t* seg = h_out_ + (size_t)s * a_.out_slot;
+            pk.data.insert(pk.data.end(), seg, seg + n);
+            packets_.push_back(std::move(pk));
         }
         parity_ ^= 1;
         return (int)packets_.size();
@@ -124,8 +118,10 @@ class HipJpegBackend : public EncoderBackend {
         else if (s == "dc") { p = a_.dc; n = nb * 2; }
         else if (s == "blk_off") { p = a_.blk_off; n = nb * 4; }
         else if (s == "stripe_bits") { p = a_.stripe_bits; n = L_.num_stripes * 4; }
+        else if (s == "state") { p = a_.state; n = L_.num_stripes * (int64_t)sizeof(JpegStripeState); }
         else return -1;
-        if (dst && cap >= n) HIPCHECK(hipMemcpy(dst, p, (size_t)n, hipMemcpyDeviceToHost));
+        if (dst && cap >= n) HIPCHECK(hipMemcpyAsync(dst, p, (size_t)n, hipMemcpyDeviceToHost, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
         return n;
     }
 
@@ -134,7 +130,7 @@ class HipJpegBackend : public EncoderBackend {
     T* dmalloc(size_t count) {
         void* p = nullptr;
         HIPCHECK(hipMalloc(&p, count * sizeof(T)));
-        HIPCHECK(hipMemset(p, 0, count * sizeof(T)));
+        HIPCHECK(hipMemsetAsync(p, 0, count * sizeof(T), stream_));
         dev_.push_back(p);
         return (T*)p;
     }
@@ -160,10 +156,16 @@ class HipJpegBackend : public EncoderBackend {
         a_.blocks_per_stripe = bps;
         a_.stride = -1;
         a_.stripe_dirty = dmalloc<int>(ns);
-        d_action_ = dmalloc<int>(ns);
-        a_.action = d_action_;
+        a_.action = dmalloc<int>(ns);
+        a_.state = dmalloc<JpegStripeState>(ns);
+        HIPCHECK(hipMemcpyAsync(a_.state, st_.data(), sizeof(JpegStripeState) * ns, hipMemcpyHostToDevice, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
+        a_.ctl = dmalloc<int>(32 * ((size_t)ns + 1));
+        a_.use_paint_over = cfg_.use_paint_over;
+        a_.paint_over_trigger = cfg_.paint_over_trigger;
         JpegTables* dt = dmalloc<JpegTables>(2);
-        HIPCHECK(hipMemcpy(dt, tab_, sizeof(tab_), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpyAsync(dt, tab_, sizeof(tab_), hipMemcpyHostToDevice, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
         a_.tabs = dt;
         a_.coef = dmalloc<int16_t>(nb * 64);
         a_.dc = dmalloc<int16_t>(nb);
@@ -175,23 +177,30 @@ class HipJpegBackend : public EncoderBackend {
         a_.bits_slot_words = (int)(slot_bytes / 4);
         a_.bits = dmalloc<uint32_t>((size_t)ns * a_.bits_slot_words);
         a_.out_slot = (int)slot_bytes;
-        a_.stage = dmalloc<uint8_t>((size_t)ns * slot_bytes);
+        a_.max_tiles = (int)(((size_t)bps * 208 + gpu::kTileBytes - 1) / gpu::kTileBytes);
+        a_.tile_ff = dmalloc<int>((size_t)ns * a_.max_tiles);
         h_out_ = hmalloc<uint8_t>((size_t)ns * slot_bytes, hipHostMallocMapped);
         h_size_ = hmalloc<int>(ns, hipHostMallocMapped);
+        h_action_ = hmalloc<int>(ns, hipHostMallocMapped);
+        h_key_seq_ = hmalloc<int>(1, hipHostMallocMapped);
+        a_.host_out = dev_ptr(h_out_);
+        a_.host_size = dev_ptr(h_size_);
+        a_.host_action = dev_ptr(h_action_);
+        a_.key_seq = dev_ptr(h_key_seq_);
+    }
+
+    template <class T>
+    T* dev_ptr(T* host) {
         void* dp = nullptr;
-        HIPCHECK(hipHostGetDevicePointer(&dp, h_out_, 0));
-        a_.host_out = (uint8_t*)dp;
-        HIPCHECK(hipHostGetDevicePointer(&dp, h_size_, 0));
-        a_.host_size = (int*)dp;
-        h_dirty_ = hmalloc<int>(ns, hipHostMallocDefault);
-        h_action_ = hmalloc<int>(ns, hipHostMallocDefault);
+        HIPCHECK(hipHostGetDevicePointer(&dp, host, 0));
+        return (T*)dp;
     }
 
     void run_graph() {
         hipGraphExec_t& g = graph_[parity_];
         if (!g) {
             hipGraph_t graph;
-            HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+            HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
             gpu::launch_encode(a_, stream_);
             HIPCHECK(hipStreamEndCapture(stream_, &graph));
             HIPCHECK(hipGraphInstantiate(&g, graph, nullptr, nullptr, 0));
@@ -212,9 +221,8 @@ class HipJpegBackend : public EncoderBackend {
     size_t frame_cap_ = 0;
     int parity_ = 0;
     bool first_ = true;
-    int* d_action_ = nullptr;
-    int* h_dirty_ = nullptr;
     int* h_action_ = nullptr;
+    int* h_key_seq_ = nullptr;
     int* h_size_ = nullptr;
     uint8_t* h_out_ = nullptr;
     std::vector<void*> dev_, host_;

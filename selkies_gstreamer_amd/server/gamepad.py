@@ -112,8 +112,8 @@ def _axis_value(v: float, trigger: bool, hat: bool, js: bool) -> int:
     if hat:
         h = int(max(-1, min(1, round(v))))
         return h * AXIS_MAX if js else h
-    if trigger:  # 0..1
-        return int(AXIS_MIN + v * (AXIS_MAX - AXIS_MIN))
+    if trigger:  # 0..1: full axis range on the joystick API, 0..255 on evdev (xpad's ABS_Z/ABS_RZ)
+        return int(AXIS_MIN + v * (AXIS_MAX - AXIS_MIN)) if js else int(round(max(0.0, min(1.0, v)) * 255))
     return int(AXIS_MIN + (v + 1.0) / 2.0 * (AXIS_MAX - AXIS_MIN))  # -1..1
 
 
