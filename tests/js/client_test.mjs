@@ -1,0 +1,64 @@
+// Unit tests of the browser client's pure modules (run by tests/test_web_client.py).
+import assertModule from 'assert';
+const assert = assertModule.strict;
+// node < 16 has no btoa/atob (browsers do)
+if (typeof globalThis.btoa === 'undefined') {
+  globalThis.btoa = (s) => Buffer.from(s, 'binary').toString('base64');
+  globalThis.atob = (b) => Buffer.from(b, 'base64').toString('binary');
+}
+import { keysymFor, charToKeysym } from '../../selkies_gstreamer_amd/web/lib/keysyms.js';
+import {
+  parseFrame, parseText, toStreamCoords, mouseMessage, buttonBit, downsampleToS16Mono, utf8ToB64, b64ToUtf8, evenDown,
+} from '../../selkies_gstreamer_amd/web/lib/protocol.js';
+
+// keysyms
+assert.equal(keysymFor({ key: 'a', code: 'KeyA' }), 0x61);
+assert.equal(keysymFor({ key: 'A', code: 'KeyA' }), 0x41);
+assert.equal(keysymFor({ key: 'Enter', code: 'Enter' }), 0xff0d);
+assert.equal(keysymFor({ key: 'Enter', code: 'NumpadEnter' }), 0xff8d);
+assert.equal(keysymFor({ key: 'Shift', code: 'ShiftRight' }), 0xffe2);
+assert.equal(keysymFor({ key: 'Control', code: 'ControlLeft' }), 0xffe3);
+assert.equal(keysymFor({ key: 'F12', code: 'F12' }), 0xffc9);
+assert.equal(keysymFor({ key: '€', code: 'KeyE' }), 0x010020ac);
+assert.equal(keysymFor({ key: 'é', code: 'Digit2' }), 0xe9);
+assert.equal(keysymFor({ key: 'Dead', code: 'BracketLeft' }), null);
+assert.equal(keysymFor({ key: '1', code: 'Numpad1', getModifierState: () => true }), 0xffb1);
+assert.equal(keysymFor({ key: 'End', code: 'Numpad1', getModifierState: () => false }), 0xff9c);
+assert.equal(charToKeysym('😀'), (0x01000000 | 0x1f600) >>> 0);
+
+// binary frames
+const h264 = new Uint8Array([0x04, 1, 0x12, 0x34, 0, 64, 7, 128, 0, 64, 0, 0, 0, 1, 0x67]);
+const f = parseFrame(h264.buffer);
+assert.deepEqual([f.type, f.key, f.frameId, f.y, f.width, f.height, f.payload.length], ['h264', true, 0x1234, 64, 1920, 64, 5]);
+const jpeg = parseFrame(new Uint8Array([0x03, 0, 0, 7, 0, 128, 0xff, 0xd8]));
+assert.deepEqual([jpeg.type, jpeg.frameId, jpeg.y, jpeg.payload[0]], ['jpeg', 7, 128, 0xff]);
+assert.equal(parseFrame(new Uint8Array([0x01, 0, 9, 9])).payload.length, 2);
+assert.equal(parseFrame(new Uint8Array([0x09, 0])), null);
+
+// text messages
+assert.deepEqual(parseText('MODE websockets'), { kind: 'mode', mode: 'websockets' });
+assert.equal(parseText('KILL a new primary client connected connection killed').kind, 'kill');
+assert.deepEqual(parseText('PIPELINE_RESETTING display2'), { kind: 'reset', display: 'display2' });
+assert.deepEqual(parseText('DISPLAY_CONFIG_UPDATE,{"type":"display_config_update","displays":["primary"]}').data.displays, ['primary']);
+assert.equal(parseText('cursor,{"curdata":"","handle":3}').data.handle, 3);
+assert.deepEqual(parseText('clipboard_binary,image/png,AAEC'), { kind: 'clipboard', mime: 'image/png', b64: 'AAEC' });
+assert.equal(b64ToUtf8(parseText('clipboard,' + utf8ToB64('héllo')).b64), 'héllo');
+assert.deepEqual(parseText('clipboard_start,text/plain,5'), { kind: 'clipboard_start', mime: 'text/plain', size: 5 });
+assert.equal(parseText('{"type":"stream_resolution","width":2,"height":4}').data.width, 2);
+
+// pointer
+assert.deepEqual(toStreamCoords(50, 50, 100, 100, 200, 200), [100, 100]);
+assert.deepEqual(toStreamCoords(0, 25, 200, 100, 100, 100), [0, 25]);     // left of the letterboxed image
+assert.deepEqual(toStreamCoords(150, 50, 200, 100, 100, 100), [99, 50]);  // clamp
+assert.equal(mouseMessage(false, 10.4, 20.6, 1), 'm,10,21,1,0');
+assert.equal(mouseMessage(true, -3, 4, 0, 2), 'm2,-3,4,0,2');
+assert.deepEqual([0, 1, 2, 3, 4, 5].map(buttonBit), [1, 2, 4, 8, 16, 0]);
+assert.equal(evenDown(1921.5), 1920);
+
+// microphone downsampling 48k -> 24k s16 mono
+const a = new Float32Array(480).fill(0.5), b = new Float32Array(480).fill(-0.5);
+const pcm = downsampleToS16Mono([a, a], 48000);
+assert.equal(pcm.length, 240);
+assert.equal(pcm[0], Math.trunc(0.5 * 0x7fff));
+assert.equal(downsampleToS16Mono([a, b], 48000)[10], 0);
+console.log('client tests ok');
