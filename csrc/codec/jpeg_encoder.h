@@ -24,6 +24,7 @@ struct JpegStripeState {
     int static_frames = 0;
     int painted = 1;
     int need_send = 1;
+    int key_seq = 0;   // last keyframe-request sequence applied (GPU backend)
 };
 
 // Per-stripe send decision shared by both backends: -1 skip, 0 send at

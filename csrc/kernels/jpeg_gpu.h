@@ -20,12 +20,18 @@ struct JpegArgs {
     const uint8_t* cur;           // BGRx frame (device), `stride` bytes per row
     const uint8_t* prev;          // previous frame (device) for damage
     int stride;
-    int* stripe_dirty;            // [num_stripes] (k_decide clears it for the next frame)
+    // Frame-parity double buffers (the host swaps them per hipGraph): k_damage
+    // writes dirty_in, every k_blocks workgroup evaluates the stripe plan from
+    // state_in (deterministic, no cross-workgroup sync), workgroup 0 of each
+    // stripe publishes state_out / action / host_action and clears dirty_out.
+    int* dirty_in;
+    int* dirty_out;
+    const JpegStripeState* state_in;
+    JpegStripeState* state_out;
     int* action;                  // [num_stripes] -1 skip, 0 quality, 1 paint quality (device)
     int* host_action;             // host-mapped copy of `action` for packet assembly
-    JpegStripeState* state;       // [num_stripes] damage / paint-over state (device resident)
-    int* ctl;                     // [0] first frame, [1] keyframe seq seen, [2] stripe counter, [32*(s+1)] WG counters (one cache line each)
-    const volatile int* key_seq;  // host-mapped keyframe-request counter
+    const volatile int* key_seq;  // host-mapped keyframe-request counter (read once per frame)
+    int* key_now;                 // device copy of key_seq for this frame
     int use_paint_over, paint_over_trigger;
     const JpegTables* tabs;       // [2]
     int16_t* coef;                // [num_stripes * blocks_per_stripe * 64] zig-zag levels
@@ -43,10 +49,8 @@ struct JpegArgs {
     int out_slot;
 };
 
-// damage(+decide) is launched directly after the upload; blocks -> scan ->
-// write -> ffcount -> stuff are captured in a graph.
-void launch_damage(const JpegArgs& a, hipStream_t s);
-void launch_encode(const JpegArgs& a, hipStream_t s);
+// damage -> blocks(+plan) -> scan -> write -> ffcount -> stuff (one graph per parity)
+void launch_frame(const JpegArgs& a, hipStream_t s);
 
 }  // namespace gpu
 }  // namespace jpeg

@@ -1,10 +1,11 @@
 // gfx950 kernels of the JPEG stripe encoder (pixelflux output_mode 0).
 //
 //   k_damage  per-stripe BGRx compare against the previous frame (all 4 bytes,
-//             like the CPU memcmp; 16-byte loads, one ballot + atomicOr per wave)
-//             the last workgroup to finish runs the per-stripe send / paint-over
-//             plan (same function as the CPU backend): one host sync per frame
-//   k_blocks  one 64-lane wave per 8x8 block: BGRx -> Y / 2x2-averaged Cb,Cr,
+//             like the CPU memcmp; 16-byte loads, one plain store per workgroup)
+//   k_blocks  evaluates the per-stripe send / paint-over plan (same function as
+//             the CPU backend) in every workgroup, so a frame needs no
+//             cross-workgroup sync and a single host sync;
+//             then one 64-lane wave per 8x8 block: BGRx -> Y / 2x2-averaged Cb,Cr,
 //             separable integer FDCT through LDS (lane = coefficient), exact
 //             rounding quantisation (32-bit division), zig-zag permute via LDS,
 //             AC Huffman bit count with a ballot of non-zero lanes (run length =
@@ -102,38 +103,9 @@ __device__ __forceinline__ void load_tables(const JpegTables* src, JpegTables* d
 }
 
 // ---------------------------------------------------------------------------
-// Stripe send plan (same function as the CPU backend); run by the last
-// workgroup of k_damage once every dirty flag of the frame is visible.
-__device__ void decide_stripes(const JpegArgs& a) {
-    __shared__ int key;
-    if (threadIdx.x == 0) {
-        const int seq = *a.key_seq;
-        key = seq != a.ctl[1];
-        a.ctl[1] = seq;
-    }
-    __syncthreads();
-    const int first = a.ctl[0];
-    for (int s = threadIdx.x; s < a.num_stripes; s += blockDim.x) {
-        JpegStripeState S = a.state[s];
-        if (key) S.need_send = 1;
-        const int dirty = __hip_atomic_load(&a.stripe_dirty[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int act = jpeg_plan_stripe(S, first || dirty, a.use_paint_over, a.paint_over_trigger);
-        a.state[s] = S;
-        a.action[s] = act;
-        a.host_action[s] = act;
-        if (act < 0) a.host_size[s] = 0;
-        a.stripe_dirty[s] = 0;  // self-cleaning for the next frame
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        a.ctl[0] = 0;
-        a.ctl[2] = 0;  // reset the workgroup-completion counter
-    }
-}
-
 __global__ __launch_bounds__(256) void k_damage(JpegArgs a) {
-    __shared__ int last;
     const int s = blockIdx.y;
+    if (s == 0 && blockIdx.x == 0 && threadIdx.x == 0) *a.key_now = *a.key_seq;  // one PCIe read per frame
     const int y0 = s * a.stripe_h;
     int h = a.H - y0;
     h = h < a.stripe_h ? h : a.stripe_h;
@@ -154,25 +126,28 @@ __global__ __launch_bounds__(256) void k_damage(JpegArgs a) {
             for (int i = threadIdx.x; i < a.W; i += blockDim.x) diff |= c[i] != p[i];
         }
     }
-    // One plain store per workgroup (same-address atomics from every wave
-    // serialise in L2, ~35 ns each). Completion is counted hierarchically:
-    // per stripe (gridDim.x workgroups), then per frame (num_stripes).
-    if (__syncthreads_or(diff) && threadIdx.x == 0) a.stripe_dirty[s] = 1;
-    if (threadIdx.x == 0) {
-        __threadfence();
-        int fin = 0;
-        if (atomicAdd(&a.ctl[32 * (s + 1)], 1) == (int)gridDim.x - 1) {  // one 128 B line per stripe
-            a.ctl[32 * (s + 1)] = 0;
-            __threadfence();
-            fin = atomicAdd(&a.ctl[2], 1) == (int)gridDim.y - 1;
-        }
-        last = fin;
+    // one plain store per workgroup; visibility to k_blocks comes from the kernel boundary
+    if (__syncthreads_or(diff) && threadIdx.x == 0) a.dirty_in[s] = 1;
+}
+
+// Stripe plan for this frame, evaluated identically by every workgroup of the
+// stripe (same inputs); workgroup 0 publishes the result.
+__device__ __forceinline__ int plan_stripe(const JpegArgs& a, int s, bool publish) {
+    JpegStripeState S = a.state_in[s];
+    const int key = *a.key_now;
+    if (S.key_seq != key) {
+        S.need_send = 1;
+        S.key_seq = key;
     }
-    __syncthreads();
-    if (last) {
-        __threadfence();
-        decide_stripes(a);
+    const int act = jpeg_plan_stripe(S, a.dirty_in[s] != 0, a.use_paint_over, a.paint_over_trigger);
+    if (publish) {
+        a.state_out[s] = S;
+        a.action[s] = act;
+        a.host_action[s] = act;
+        if (act < 0) a.host_size[s] = 0;
+        a.dirty_out[s] = 0;  // next frame's k_damage target
     }
+    return act;
 }
 
 // ---------------------------------------------------------------------------
@@ -184,7 +159,7 @@ __global__ __launch_bounds__(256) void k_blocks(JpegArgs a) {
     __shared__ int sTmp[4][64];
     __shared__ int sZz[4][64];
     const int s = blockIdx.y;
-    const int act = a.action[s];
+    const int act = plan_stripe(a, s, blockIdx.x == 0 && threadIdx.x == 0);
     if (act < 0) return;
     const int tid = threadIdx.x;
     if (tid < 64) {
@@ -506,12 +481,9 @@ __global__ __launch_bounds__(256) void k_stuff(JpegArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-void launch_damage(const JpegArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_damage, dim3((a.stripe_h + 1) / 2, a.num_stripes), dim3(256), 0, st, a);  // 2 rows/WG
-}
-
-void launch_encode(const JpegArgs& a, hipStream_t st) {
+void launch_frame(const JpegArgs& a, hipStream_t st) {
     const int wgs = (a.blocks_per_stripe + 23) / 24;  // 4 waves x 1 MCU
+    hipLaunchKernelGGL(k_damage, dim3(a.stripe_h, a.num_stripes), dim3(256), 0, st, a);  // 1 row / WG
     hipLaunchKernelGGL(k_blocks, dim3(wgs, a.num_stripes), dim3(256), 0, st, a);
     hipLaunchKernelGGL(k_scan, dim3(a.num_stripes), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(k_write, dim3(wgs, a.num_stripes), dim3(256), 0, st, a);

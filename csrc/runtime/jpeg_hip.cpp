@@ -1,7 +1,8 @@
 // HIP backend of the JPEG stripe encoder. Frame flow:
 //   H2D(BGRx into the ping-pong frame buffer)
-//   -> [k_damage(+plan), k_blocks, k_scan, k_write, k_ffcount, k_stuff]
-//      (one hipGraph per frame-buffer parity; stripe plan state lives on the GPU)
+//   -> [k_damage, k_blocks(+stripe plan), k_scan, k_write, k_ffcount, k_stuff]
+//      (one hipGraph per frame-buffer parity; stripe plan state lives on the GPU,
+//      double-buffered by parity)
 //   -> one sync -> packets = [frame_id][y] + cached JFIF header + entropy
 //      segment read straight out of host-mapped memory.
 #include "encoder_iface.h"
@@ -52,7 +53,7 @@ class HipJpegBackend : public EncoderBackend {
     }
 
     void request_keyframe() override {
-        // consumed by k_damage's plan step on the next frame (host-mapped counter)
+        // consumed by the next frame's stripe plan (host-mapped counter)
         __atomic_add_fetch(h_key_seq_, 1, __ATOMIC_SEQ_CST);
     }
 
@@ -71,16 +72,21 @@ class HipJpegBackend : public EncoderBackend {
             for (auto& g : graph_)
                 if (g) { hipGraphExecDestroy(g); g = nullptr; }
         }
-        if (first_) {
-            const int ctl[3] = {1, *h_key_seq_, 0};
-            HIPCHECK(hipMemcpyAsync(a_.ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice, stream_));
-            HIPCHECK(hipStreamSynchronize(stream_));  // `ctl` is a stack array
+        if (first_) {  // (re)start: every stripe is sent on the first frame
+            for (auto* st : state_)
+                HIPCHECK(hipMemcpyAsync(st, st_.data(), sizeof(JpegStripeState) * st_.size(), hipMemcpyHostToDevice,
+                                        stream_));
+            for (auto* d : dirty_) HIPCHECK(hipMemsetAsync(d, 0, sizeof(int) * L_.num_stripes, stream_));
+            HIPCHECK(hipStreamSynchronize(stream_));
             first_ = false;
         }
         a_.cur = frame_[parity_];
         a_.prev = frame_[parity_ ^ 1];
+        a_.state_in = state_[parity_];
+        a_.state_out = state_[parity_ ^ 1];
+        a_.dirty_in = dirty_[parity_];
+        a_.dirty_out = dirty_[parity_ ^ 1];
         HIPCHECK(hipMemcpyAsync(frame_[parity_], bgrx, bytes, hipMemcpyHostToDevice, stream_));
-        gpu::launch_damage(a_, stream_);
         run_graph();
         HIPCHECK(hipStreamSynchronize(stream_));
         for (int s = 0; s < L_.num_stripes; s++) {
@@ -118,7 +124,7 @@ class HipJpegBackend : public EncoderBackend {
         else if (s == "dc") { p = a_.dc; n = nb * 2; }
         else if (s == "blk_off") { p = a_.blk_off; n = nb * 4; }
         else if (s == "stripe_bits") { p = a_.stripe_bits; n = L_.num_stripes * 4; }
-        else if (s == "state") { p = a_.state; n = L_.num_stripes * (int64_t)sizeof(JpegStripeState); }
+        else if (s == "state") { p = state_[parity_]; n = L_.num_stripes * (int64_t)sizeof(JpegStripeState); }
         else return -1;
         if (dst && cap >= n) HIPCHECK(hipMemcpyAsync(dst, p, (size_t)n, hipMemcpyDeviceToHost, stream_));
         HIPCHECK(hipStreamSynchronize(stream_));
@@ -155,12 +161,12 @@ class HipJpegBackend : public EncoderBackend {
         a_.mcu_w = L_.mcu_w;
         a_.blocks_per_stripe = bps;
         a_.stride = -1;
-        a_.stripe_dirty = dmalloc<int>(ns);
+        for (int i = 0; i < 2; i++) {
+            dirty_[i] = dmalloc<int>(ns);
+            state_[i] = dmalloc<JpegStripeState>(ns);
+        }
         a_.action = dmalloc<int>(ns);
-        a_.state = dmalloc<JpegStripeState>(ns);
-        HIPCHECK(hipMemcpyAsync(a_.state, st_.data(), sizeof(JpegStripeState) * ns, hipMemcpyHostToDevice, stream_));
-        HIPCHECK(hipStreamSynchronize(stream_));
-        a_.ctl = dmalloc<int>(32 * ((size_t)ns + 1));
+        a_.key_now = dmalloc<int>(1);
         a_.use_paint_over = cfg_.use_paint_over;
         a_.paint_over_trigger = cfg_.paint_over_trigger;
         JpegTables* dt = dmalloc<JpegTables>(2);
@@ -201,7 +207,7 @@ class HipJpegBackend : public EncoderBackend {
         if (!g) {
             hipGraph_t graph;
             HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
-            gpu::launch_encode(a_, stream_);
+            gpu::launch_frame(a_, stream_);
             HIPCHECK(hipStreamEndCapture(stream_, &graph));
             HIPCHECK(hipGraphInstantiate(&g, graph, nullptr, nullptr, 0));
             hipGraphDestroy(graph);
@@ -223,6 +229,8 @@ class HipJpegBackend : public EncoderBackend {
     bool first_ = true;
     int* h_action_ = nullptr;
     int* h_key_seq_ = nullptr;
+    int* dirty_[2] = {nullptr, nullptr};
+    JpegStripeState* state_[2] = {nullptr, nullptr};
     int* h_size_ = nullptr;
     uint8_t* h_out_ = nullptr;
     std::vector<void*> dev_, host_;
