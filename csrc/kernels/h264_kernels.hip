@@ -234,7 +234,25 @@ __device__ __forceinline__ int me_sad(const FrameArgs& a, const uint8_t* refy, u
     return wave_sum((int)__builtin_amdgcn_sad_u8(sw, rw, 0u));
 }
 
+// Reference window cached in LDS for the diamond refinement: +-kWin pixels
+// around the best predictor, 32 rows x 36 bytes (the extra word serves the
+// aligned-pair read of the last unaligned column). Window bytes are produced
+// by load_ref4, so every SAD is identical to the global-memory path.
+constexpr int kWin = 8;
+constexpr int kWinWords = 10;  // words per LDS row (40 B)
+
+__device__ __forceinline__ int win_sad(const uint32_t* win, uint32_t sw, int ox, int oy) {
+    const int l = lane_id();
+    const int row = l >> 2, col4 = (l & 3) * 4;
+    const int bc = col4 + ox + kWin;              // byte column inside the window row
+    const uint32_t* w = win + (row + oy + kWin) * kWinWords + (bc >> 2);
+    const int sh = bc & 3;
+    const uint32_t rw = sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+    return wave_sum((int)__builtin_amdgcn_sad_u8(sw, rw, 0u));
+}
+
 __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
+    __shared__ uint32_t win[32 * kWinWords];
     int nmb = a.mb_w * a.mb_h;
     int idx = xcd_remap(blockIdx.x, gridDim.x);
     if (idx >= nmb) return;
@@ -271,6 +289,17 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
         int c = sd + lam * (sk_se_bits(4 * cx[i]) + sk_se_bits(4 * cy[i]));
         if (c < bcost) { bcost = c; bx = cx[i]; by = cy[i]; bsad = sd; }
     }
+    // fill the LDS window around the best predictor: lane -> (row l>>1, 5 words)
+    const int cx0 = bx, cy0 = by;
+    {
+        const int r = l >> 1, h = l & 1;
+        const int y = sk_clip(mby * 16 + cy0 - kWin + r, ylo, yhi);
+        const uint8_t* rowp = a.ref.y + (size_t)y * a.stride_y;
+        const int x0 = mbx * 16 + cx0 - kWin + 16 * h;
+#pragma unroll
+        for (int k = 0; k < 5; k++) win[r * kWinWords + 4 * h + k] = load_ref4(rowp, x0 + 4 * k, a.stride_y);
+    }
+    wave_sync();
     const int ddx[4] = {0, -1, 1, 0}, ddy[4] = {-1, 0, 0, 1};
     for (int it = 0; it < a.me_iters; it++) {
         int nb = -1, ncost = bcost, nsad = 0;
@@ -278,7 +307,10 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
         for (int k = 0; k < 4; k++) {
             int x = bx + ddx[k], y = by + ddy[k];
             if (x < -R || x > R || y < -R || y > R) continue;
-            int sd = me_sad(a, a.ref.y, sw, mbx, mby, x, y, ylo, yhi);
+            const int ox = x - cx0, oy = y - cy0;
+            int sd = (ox >= -kWin && ox <= kWin && oy >= -kWin && oy <= kWin)
+                         ? win_sad(win, sw, ox, oy)
+                         : me_sad(a, a.ref.y, sw, mbx, mby, x, y, ylo, yhi);
             int c = sd + lam * (sk_se_bits(4 * x) + sk_se_bits(4 * y));
             if (c < ncost) { ncost = c; nb = k; nsad = sd; }
         }
@@ -298,24 +330,40 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
         r.mvy = (int16_t)by;
         r.sad = bsad;
         r.intra_est = dev;
-        a.me[idx] = r;
-        atomicAdd((unsigned long long*)&a.slice_sums[2 * s], (unsigned long long)bsad);
-        atomicAdd((unsigned long long*)&a.slice_sums[2 * s + 1], (unsigned long long)dev);
+        a.me[idx] = r;  // per-slice sums are reduced in k_decide (no same-line atomics)
     }
 }
 
-__global__ void k_decide(FrameArgs a) {
-    int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.num_slices) return;
+// One workgroup per slice: scene-cut decision from the per-MB ME results.
+__global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
+    __shared__ long long red[2][4];
+    const int s = blockIdx.x;
     SliceTask& t = a.tasks[s];
-    int fin = t.action;
-    if (t.action == ACT_P && t.allow_scenecut && a.slice_sums[2 * s] > a.slice_sums[2 * s + 1])
-        fin = ACT_I;
-    t.final_action = fin;
-    // self-cleaning accumulators for the next frame
-    a.slice_sums[2 * s] = 0;
-    a.slice_sums[2 * s + 1] = 0;
-    a.stripe_dirty[s] = 0;
+    const bool p = t.action == ACT_P && t.allow_scenecut;
+    long long sad = 0, dev = 0;
+    if (p) {
+        const int first = t.first_row * a.mb_w, nmb = t.num_rows * a.mb_w;
+        for (int i = threadIdx.x; i < nmb; i += 256) {
+            const MeResult r = a.me[first + i];
+            sad += r.sad;
+            dev += r.intra_est;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sad += __shfl_down(sad, o);
+        dev += __shfl_down(dev, o);
+    }
+    if (lane_id() == 0) {
+        red[0][threadIdx.x >> 6] = sad;
+        red[1][threadIdx.x >> 6] = dev;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const long long ts = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        const long long td = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        t.final_action = (p && ts > td) ? ACT_I : t.action;
+        a.stripe_dirty[s] = 0;  // self-cleaning for the next frame
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1317,7 +1365,7 @@ void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
 void launch_encode(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_decide, dim3((a.num_slices + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3(nmb), dim3(64), 0, s, a);
     if (a.rows_per_slice <= 4)
         hipLaunchKernelGGL(k_code_intra<4>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
