@@ -120,18 +120,11 @@ def main():
     run_all(args.warmup, args.steps, True)
     gather_bytes = 0
     if args.gather and dist is not None:
-        # single-server topology: every rank's packets are gathered to rank 0 over xGMI
-        blob = b"".join(p.data for s in out_packets for step in s for p in step)
-        t = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda() if blob else torch.zeros(1, dtype=torch.uint8, device="cuda")
-        n = torch.tensor([t.numel()], device="cuda")
-        sizes = [torch.zeros_like(n) for _ in range(world)]
-        dist.all_gather(sizes, n)
-        mx = int(max(x.item() for x in sizes))
-        buf = torch.zeros(mx, dtype=torch.uint8, device="cuda")
-        buf[: t.numel()] = t
-        bufs = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(bufs, buf)
-        gather_bytes = int(sum(x.item() for x in sizes))
+        # single-server topology: every rank's packets are gathered to rank 0 over xGMI in one step
+        from selkies_gstreamer_amd.parallel.fanout import gather_packets
+        mine = [(i, p.data) for i, s in enumerate(out_packets) for step in s for p in step]
+        got = gather_packets(mine)
+        gather_bytes = sum(len(d) for _, _, d in got) if got is not None else 0
     if dist is not None:
         torch.cuda.synchronize()
         dist.barrier()

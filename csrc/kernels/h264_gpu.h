@@ -27,22 +27,25 @@ struct FrameArgs {
     uint8_t* mb_dirty;     // [num_mbs]
     int* stripe_dirty;     // [num_slices]
     SliceTask* tasks;      // [num_slices]
-    long long* slice_sums; // [num_slices][2] inter SAD, intra estimate
     MeResult* me;          // [num_mbs]
     int16_t* mvfield;      // [num_mbs][2]
     MbInfo* mbs;           // [num_mbs]
     int16_t* coefs;        // [num_mbs][kCoefPerMb]
     uint32_t* mb_bits;     // [num_mbs][kMbSlotBytes/4]
     int* mb_nbits;         // [num_mbs]
-    uint32_t* rbsp;        // [num_slices][rbsp_slot_words]
+    uint32_t* rbsp;        // [num_slices][rbsp_slot_words] (self-cleaning)
     int rbsp_slot_words;
-    uint8_t* out;          // packet slots (host-mapped or device)
-    int out_slot_bytes;
-    int* out_size;         // [num_slices] bytes written in each slot
+    int* mb_off;           // [num_mbs] bit offset of each MB inside its slice RBSP
+    int* slice_info;       // [num_slices][4]: RBSP bytes, packet prefix bytes
+    int* tile_nz;          // [num_slices][max_tiles] last non-zero RBSP byte per EP tile
+    int* tile_ins;         // [num_slices][max_tiles] emulation-prevention insertions per tile
+    int max_tiles;
+    int out_slot_bytes;    // bytes per slice slot in host_out
     const uint8_t* param_sets;  // [num_slices or 1][kParamSetMax]
     const int* param_set_len;
     int param_set_stride;
-    uint8_t* host_out;     // host-mapped compacted packet buffer (k_gather)
+    uint8_t* host_out;     // host-mapped packet slots [num_slices][out_slot_bytes]
+    int* host_size;        // host-mapped [num_slices] bytes in each slot
     const int* frame_params;  // device: [0] = frame_id
     int first_frame;
     unsigned long long* dbg;  // optional s_memtime stamps (SK_STAMPS=1), else nullptr

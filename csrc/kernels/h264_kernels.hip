@@ -14,8 +14,9 @@
 //   k_code_intra      K5+K6  Intra16x16 wavefront (one wave per MB row, lag 2)
 //   k_cavlc           K8     per-MB CAVLC: lanes code residual blocks in parallel,
 //                            bit offsets by wave prefix-sum, LDS atomicOr packing
-//   k_assemble        K9     slice header, MB bit concatenation, emulation
-//                            prevention as a 3-state chunk scan, packet framing
+//   k_slice_scan, k_mb_concat, k_ep_*   K9  slice header + MB offsets, MB bit
+//                            concatenation, tile-parallel emulation prevention
+//                            straight into host-mapped packet slots
 //   k_commit                 reference / MV-field update
 #include "h264_gpu.h"
 #include "../codec/color.h"
@@ -65,6 +66,26 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
         if (l >= o) v += t;
     }
     return v;
+}
+
+// Exclusive block-wide scan for blockDim = 64 * NW; the block total goes to *total.
+template <int NW>
+__device__ __forceinline__ int block_excl_scan(int v, int* wave_tot, int* total) {
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const int inc = wave_incl_scan(v);
+    if (l == 63) wave_tot[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        const int t = l < NW ? wave_tot[l] : 0;
+        const int ti = wave_incl_scan(t);
+        if (l < NW) wave_tot[l] = ti - t;
+        if (l == NW - 1) wave_tot[NW] = ti;
+    }
+    __syncthreads();
+    const int r = wave_tot[w] + inc - v;
+    *total = wave_tot[NW];
+    __syncthreads();
+    return r;
 }
 
 template <int K>
@@ -1118,24 +1139,46 @@ __global__ __launch_bounds__(64) void k_cavlc(FrameArgs a) {
 
 // ---------------------------------------------------------------------------
 // K9: slice assembly (one 256-thread workgroup per coded slice).
-__global__ __launch_bounds__(256) void k_assemble(FrameArgs a) {
+// ---------------------------------------------------------------------------
+// K9: slice assembly, tile-parallel.
+//   k_slice_scan  one workgroup per slice: slice header, exclusive scan of the MB
+//                 bit counts -> per-MB bit offsets, trailing mb_skip_run + stop
+//                 bit, packet prefix (stripe header, SPS/PPS on IDR, start code,
+//                 NAL header) written straight into the host-mapped slot
+//   k_mb_concat   one wave per MB: shifts its CAVLC words into the slice RBSP
+//                 (plain stores; atomicOr only on the two edge words it shares)
+//   k_ep_nz / k_ep_count / k_ep_write   4 KiB tiles of every slice in parallel:
+//                 emulation prevention (7.4.1) — a 0x03 goes before byte i iff
+//                 b_i <= 3 and the zero run z(i) right before i is even and >= 2,
+//                 which only depends on the input bytes; a tile needs the last
+//                 non-zero byte before it (prefix max of k_ep_nz) and the number
+//                 of insertions before it (prefix sum of k_ep_count). k_ep_write
+//                 stages its output in LDS, streams it to host memory with 16-byte
+//                 stores and self-cleans the RBSP words it consumed.
+constexpr int kTile = 4096;
+
+__global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
     __shared__ uint32_t hdr[32];
-    __shared__ int scan[256];
-    __shared__ int sh_misc[8];
-    int s = blockIdx.x;
-    SliceTask& task = a.tasks[s];
-    int fin = task.final_action;
-    int tid = threadIdx.x;
+    __shared__ int wave_tot[5];
+    __shared__ int sh_misc[4];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const SliceTask task = a.tasks[s];
+    const int fin = task.final_action;
+    int* info = a.slice_info + 4 * s;
     if (fin == ACT_NONE) {
-        if (tid == 0) a.out_size[s] = 0;
+        if (tid == 0) {
+            info[0] = 0;
+            a.host_size[s] = 0;
+        }
         return;
     }
     const int nmb = task.num_rows * a.mb_w;
     const int first = task.first_row * a.mb_w;
     uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
-    bool intra = fin == ACT_I;
-    bool idr = intra && task.idr_on_intra;
+    const bool intra = fin == ACT_I;
+    const bool idr = intra && task.idr_on_intra;
     if (tid < 32) hdr[tid] = 0;
+    if (tid == 0) sh_misc[1] = -1;
     __syncthreads();
     if (tid == 0) {
         AtomicBitWriter w{hdr, 0};
@@ -1150,81 +1193,48 @@ __global__ __launch_bounds__(256) void k_assemble(FrameArgs a) {
         if (fin == ACT_SKIPALL) put_ue(w, (uint32_t)nmb);
         sh_misc[0] = (int)w.pos;
     }
-    // per-thread MB ranges
-    int per = (nmb + 255) / 256;
-    int m0 = sk_min(nmb, tid * per), m1 = sk_min(nmb, m0 + per);
+    const int per = (nmb + 255) / 256;
+    const int m0 = sk_min(nmb, tid * per), m1 = sk_min(nmb, m0 + per);
     int local = 0, last_coded = -1;
     if (fin != ACT_SKIPALL)
         for (int m = m0; m < m1; m++) {
-            int nb = a.mb_nbits[first + m];
+            const int nb = a.mb_nbits[first + m];
             local += nb;
             if (nb > 0) last_coded = m;
         }
-    scan[tid] = local;
-    __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
-        int v = tid >= o ? scan[tid - o] : 0;
-        __syncthreads();
-        scan[tid] += v;
-        __syncthreads();
-    }
-    int hb = sh_misc[0];
-    int excl = scan[tid] - local;
-    // last coded MB (for the trailing mb_skip_run)
-    if (tid == 0) sh_misc[1] = -1;
-    __syncthreads();
     if (last_coded >= 0) atomicMax(&sh_misc[1], last_coded);
-    // header words
-    if (tid < 32 && tid * 32 < hb) atomicOr(&rbsp[tid], hdr[tid]);
-    // MB bit copies
-    uint32_t pos = (uint32_t)(hb + excl);
-    if (fin != ACT_SKIPALL)
+    int total;
+    const int excl = block_excl_scan<4>(local, wave_tot, &total);
+    const int hb = sh_misc[0];
+    if (fin != ACT_SKIPALL) {
+        int off = hb + excl;
         for (int m = m0; m < m1; m++) {
-            int nb = a.mb_nbits[first + m];
-            const uint32_t* src = a.mb_bits + (size_t)(first + m) * (kMbSlotBytes / 4);
-            int nw = (nb + 31) >> 5;
-            for (int k = 0; k < nw; k++) {
-                uint32_t v = src[k];
-                uint32_t p = pos + 32u * k;
-                uint32_t wi = p >> 5, sh = p & 31;
-                atomicOr(&rbsp[wi], v >> sh);
-                if (sh) atomicOr(&rbsp[wi + 1], v << (32 - sh));
-            }
-            pos += nb;
+            a.mb_off[first + m] = off;
+            off += a.mb_nbits[first + m];
         }
-    __syncthreads();
-    int total_bits = hb + scan[255];
+    }
+    if (tid < 32 && tid * 32 < hb) atomicOr(&rbsp[tid], hdr[tid]);  // last header word is shared with MB 0
     if (tid == 0) {
-        AtomicBitWriter w{rbsp, (uint32_t)total_bits};
+        AtomicBitWriter w{rbsp, (uint32_t)(hb + total)};
         if (fin == ACT_P) {
-            int trailing = nmb - 1 - sh_misc[1];
+            const int trailing = nmb - 1 - sh_misc[1];
             if (trailing > 0) put_ue(w, (uint32_t)trailing);
         }
         w.put(1, 1);  // rbsp_stop_one_bit
-        int nbytes = (int)((w.pos + 7) >> 3);
-        sh_misc[2] = nbytes;
-    }
-    __threadfence();
-    __syncthreads();
-    const int n = sh_misc[2];
-    // ---- packet prefix (stripe header, SPS/PPS on IDR, start code, NAL header)
-    uint8_t* slot = a.out + (size_t)s * a.out_slot_bytes;
-    if (tid == 0) {
+        info[0] = (int)((w.pos + 7) >> 3);
+        // packet prefix, written directly into the host-mapped slot
+        uint8_t* slot = a.host_out + (size_t)s * a.out_slot_bytes;
         int p = 0;
         if (!a.fullframe) {
-            int y = task.first_row * 16;
-            int h = sk_min(a.H, (task.first_row + task.num_rows) * 16) - y;
-            int fid = a.frame_params[0];
-            slot[0] = 0x04;
-            slot[1] = idr ? 1 : 0;
-            slot[2] = (uint8_t)(fid >> 8);
-            slot[3] = (uint8_t)fid;
-            slot[4] = (uint8_t)(y >> 8); slot[5] = (uint8_t)y;
-            slot[6] = (uint8_t)(a.W >> 8); slot[7] = (uint8_t)a.W;
-            slot[8] = (uint8_t)(h >> 8); slot[9] = (uint8_t)h;
+            const int y = task.first_row * 16;
+            const int h = sk_min(a.H, (task.first_row + task.num_rows) * 16) - y;
+            const int fid = a.frame_params[0];
+            uint8_t pre[10] = {0x04, (uint8_t)(idr ? 1 : 0), (uint8_t)(fid >> 8), (uint8_t)fid, (uint8_t)(y >> 8),
+                               (uint8_t)y, (uint8_t)(a.W >> 8), (uint8_t)a.W, (uint8_t)(h >> 8), (uint8_t)h};
+            for (int i = 0; i < 10; i++) slot[i] = pre[i];
             p = 10;
             if (idr) {
-                int len = a.param_set_len[s];
+                const int len = a.param_set_len[s];
                 const uint8_t* ps = a.param_sets + (size_t)s * a.param_set_stride;
                 for (int i = 0; i < len; i++) slot[p + i] = ps[i];
                 p += len;
@@ -1232,95 +1242,196 @@ __global__ __launch_bounds__(256) void k_assemble(FrameArgs a) {
         }
         slot[p++] = 0; slot[p++] = 0; slot[p++] = 0; slot[p++] = 1;
         slot[p++] = idr ? 0x65 : 0x41;
-        sh_misc[4] = p;
+        info[1] = p;
     }
-    __syncthreads();
-    // ---- emulation prevention (7.4.1): 0x03 goes before byte i iff b_i <= 3 and
-    // the run z(i) of zero bytes right before i is even and >= 2. z comes from a
-    // prefix-max of non-zero positions, output offsets from a prefix-sum of the
-    // insertions; 4 KiB tiles, 16 bytes per thread, wave scans + LDS combine.
-    const int wv = tid >> 6, ln = tid & 63;
-    int carry_nz = -1;               // last non-zero byte index before the tile (NAL header at -1)
-    int out_off = sh_misc[4];
-    for (int base = 0, it = 0; base < n; base += 4096, it++) {
-        int i0 = base + tid * 16;
-        uint32_t wd[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            wd[q] = (i0 + 4 * q < n) ? __hip_atomic_load(&rbsp[(i0 >> 2) + q], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                     : 0u;
-        int lastnz = -1;
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            int bt = (int)((wd[q >> 2] >> (24 - 8 * (q & 3))) & 255u);
-            if (i0 + q < n && bt != 0) lastnz = i0 + q;
-        }
-        int incl = wave_incl_scan_max(lastnz);
-        int excl = __shfl_up(incl, 1);
-        if (ln == 0) excl = -1;
-        int* wmax = scan;              // reuse LDS: [it&1][4] maxima, [it&1][4] sums
-        int par = (it & 1) * 8;
-        if (ln == 63) wmax[par + wv] = incl;
-        __syncthreads();
-        int prev = carry_nz;
-        for (int k = 0; k < wv; k++) prev = max(prev, wmax[par + k]);
-        prev = max(prev, excl);
-        int ins = 0;
-        uint32_t insmask = 0;
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            int i = i0 + q;
-            int bt = (int)((wd[q >> 2] >> (24 - 8 * (q & 3))) & 255u);
-            if (i < n) {
-                int z = i - 1 - prev;
-                if (bt <= 3 && z >= 2 && !(z & 1)) { ins++; insmask |= 1u << q; }
-                if (bt != 0) prev = i;
-            }
-        }
-        int sincl = wave_incl_scan(ins);
-        if (ln == 63) wmax[par + 4 + wv] = sincl;
-        __syncthreads();
-        int before = sincl - ins;
-        for (int k = 0; k < wv; k++) before += wmax[par + 4 + k];
-        int o = out_off + (i0 - base) + before;
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            int i = i0 + q;
-            if (i < n) {
-                if (insmask & (1u << q)) slot[o++] = 3;
-                slot[o++] = (uint8_t)((wd[q >> 2] >> (24 - 8 * (q & 3))) & 255u);
-            }
-        }
-        // self-clean the RBSP words for the next frame
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (i0 + 4 * q < n) rbsp[(i0 >> 2) + q] = 0u;
-        int tile_ins = 0, tile_max = carry_nz;
-        for (int k = 0; k < 4; k++) {
-            tile_ins += wmax[par + 4 + k];
-            tile_max = max(tile_max, wmax[par + k]);
-        }
-        carry_nz = tile_max;
-        out_off += sk_min(4096, n - base) + tile_ins;
-    }
-    if (tid == 0) sh_misc[3] = out_off;
-    __syncthreads();
-    if (tid == 0) a.out_size[s] = sh_misc[3];
 }
 
-// Packs the per-slice packet slots into one host-visible buffer (64-byte aligned
-// offsets, 16-byte stores): the host reads results after a single sync.
-__global__ __launch_bounds__(256) void k_gather(FrameArgs a) {
-    int s = blockIdx.x;
-    int size = a.out_size[s];
-    if (size <= 0) return;
-    long off = 0;
-    for (int k = 0; k < s; k++) off += ((long)a.out_size[k] + 63) & ~63L;
-    const uint4* src = reinterpret_cast<const uint4*>(a.out + (size_t)s * a.out_slot_bytes);
-    uint4* dst = reinterpret_cast<uint4*>(a.host_out + off);
-    int n16 = (size + 15) >> 4;
-    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+__global__ __launch_bounds__(256) void k_mb_concat(FrameArgs a) {
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const int mb = blockIdx.x * 4 + w;
+    if (mb >= a.mb_w * a.mb_h) return;
+    const int s = (mb / a.mb_w) / a.rows_per_slice;
+    const int fin = a.tasks[s].final_action;
+    if (fin == ACT_NONE || fin == ACT_SKIPALL) return;
+    const int nb = a.mb_nbits[mb];
+    if (nb <= 0) return;
+    const int p = a.mb_off[mb];
+    const int w0 = p >> 5, w1 = (p + nb - 1) >> 5, sh = p & 31;
+    const int nw = (nb + 31) >> 5;
+    const uint32_t lastmask = (nb & 31) ? ~0u << (32 - (nb & 31)) : ~0u;
+    const uint32_t* src = a.mb_bits + (size_t)mb * (kMbSlotBytes / 4);
+    uint32_t* dst = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    for (int j = w0 + l; j <= w1; j += 64) {
+        const int k = j - w0;
+        uint32_t lo = k < nw ? src[k] : 0u;
+        if (k == nw - 1) lo &= lastmask;
+        uint32_t v;
+        if (sh == 0) {
+            v = lo;
+        } else {
+            uint32_t hi = 0u;
+            if (k >= 1) {
+                hi = src[k - 1];
+                if (k - 1 == nw - 1) hi &= lastmask;
+            }
+            v = (lo >> sh) | (k >= 1 ? hi << (32 - sh) : 0u);
+        }
+        if (j == w0 || j == w1) {
+            if (v) atomicOr(&dst[j], v);
+        } else {
+            dst[j] = v;
+        }
+    }
+}
+
+__device__ __forceinline__ uint8_t rbsp_byte(uint32_t word, int q) { return (uint8_t)(word >> (24 - 8 * q)); }
+
+__global__ __launch_bounds__(256) void k_ep_nz(FrameArgs a) {
+    __shared__ int red[4];
+    const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x;
+    if (a.tasks[s].final_action == ACT_NONE) return;
+    const int n = a.slice_info[4 * s];
+    const int t0 = t * kTile;
+    if (t0 >= n) return;
+    const uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    const int i0 = t0 + tid * 16;
+    int lastnz = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int iq = i0 + 4 * q;
+        const uint32_t wd = iq < n ? rbsp[iq >> 2] : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (iq + j < n && rbsp_byte(wd, j)) lastnz = iq + j;
+    }
+    for (int o = 32; o > 0; o >>= 1) lastnz = max(lastnz, __shfl_down(lastnz, o));
+    if (lane_id() == 0) red[tid >> 6] = lastnz;
+    __syncthreads();
+    if (tid == 0) a.tile_nz[s * a.max_tiles + t] = max(max(red[0], red[1]), max(red[2], red[3]));
+}
+
+// Per-thread EP decisions for 16 bytes starting at i0; `carry` = last non-zero
+// byte index before the tile. Returns the insertion count; bytes and insertion
+// mask through the out parameters.
+__device__ __forceinline__ int ep_thread(const uint32_t* rbsp, int n, int t0, int carry, int* scan_lds,
+                                         uint8_t* by, uint32_t* insmask) {
+    const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
+    const int i0 = t0 + tid * 16;
+    int lastnz = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int iq = i0 + 4 * q;
+        const uint32_t wd = iq < n ? rbsp[iq >> 2] : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            by[4 * q + j] = rbsp_byte(wd, j);
+            if (iq + j < n && by[4 * q + j]) lastnz = iq + j;
+        }
+    }
+    const int incl = wave_incl_scan_max(lastnz);
+    int ex = __shfl_up(incl, 1);
+    if (ln == 0) ex = -1;
+    if (ln == 63) scan_lds[wv] = incl;
+    __syncthreads();
+    int prev = carry;
+    for (int k = 0; k < wv; k++) prev = max(prev, scan_lds[k]);
+    prev = max(prev, ex);
+    int ins = 0;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int i = i0 + q;
+        if (i < n) {
+            const int z = i - 1 - prev;
+            if (by[q] <= 3 && z >= 2 && !(z & 1)) {
+                ins++;
+                mask |= 1u << q;
+            }
+            if (by[q]) prev = i;
+        }
+    }
+    *insmask = mask;
+    return ins;
+}
+
+__device__ __forceinline__ int tile_carry(const FrameArgs& a, int s, int t) {
+    int c = -1;  // the NAL header byte before the RBSP is non-zero
+    for (int k = 0; k < t; k++) c = max(c, a.tile_nz[s * a.max_tiles + k]);
+    return c;
+}
+
+__global__ __launch_bounds__(256) void k_ep_count(FrameArgs a) {
+    __shared__ int scan_lds[4];
+    __shared__ int red[4];
+    const int s = blockIdx.y, t = blockIdx.x;
+    if (a.tasks[s].final_action == ACT_NONE) return;
+    const int n = a.slice_info[4 * s];
+    const int t0 = t * kTile;
+    if (t0 >= n) return;
+    const uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    uint8_t by[16];
+    uint32_t mask;
+    int ins = ep_thread(rbsp, n, t0, tile_carry(a, s, t), scan_lds, by, &mask);
+    for (int o = 32; o > 0; o >>= 1) ins += __shfl_down(ins, o);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = ins;
+    __syncthreads();
+    if (threadIdx.x == 0) a.tile_ins[s * a.max_tiles + t] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
+    __shared__ int scan_lds[4];
+    __shared__ int wave_tot[5];
+    __shared__ int sh_before;
+    __shared__ uint8_t sOut[kTile + kTile / 2 + 16];
+    const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x;
+    if (a.tasks[s].final_action == ACT_NONE) return;
+    const int n = a.slice_info[4 * s];
+    const int t0 = t * kTile;
+    if (t0 >= n) return;
+    if (tid < 64) {
+        int b = 0;
+        for (int k = tid; k < t; k += 64) b += a.tile_ins[s * a.max_tiles + k];
+        b = wave_sum(b);
+        if (tid == 0) sh_before = b;
+    }
+    uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    uint8_t by[16];
+    uint32_t mask;
+    const int ins = ep_thread(rbsp, n, t0, tile_carry(a, s, t), scan_lds, by, &mask);
+    int tile_ins;
+    const int ex = block_excl_scan<4>(ins, wave_tot, &tile_ins);
+    const int i0 = t0 + tid * 16;
+    int o = tid * 16 + ex;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        if (i0 + q < n) {
+            if (mask & (1u << q)) sOut[o++] = 3;
+            sOut[o++] = by[q];
+        }
+    }
+    // self-clean the RBSP words of this tile for the next frame
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (i0 + 4 * q < n) rbsp[(i0 >> 2) + q] = 0u;
+    __syncthreads();
+    const int len = sk_min(n - t0, kTile) + tile_ins;
+    const int g0 = a.slice_info[4 * s + 1] + t0 + sh_before;
+    uint8_t* dst = a.host_out + (size_t)s * a.out_slot_bytes;
+    const int head = sk_min(len, (16 - (g0 & 15)) & 15);
+    if (tid < head) dst[g0 + tid] = sOut[tid];
+    const int nvec = (len - head) >> 4;
+    for (int v = tid; v < nvec; v += 256) {
+        const uint8_t* q = sOut + head + 16 * v;
+        uint4 x;
+        x.x = q[0] | (q[1] << 8) | (q[2] << 16) | ((uint32_t)q[3] << 24);
+        x.y = q[4] | (q[5] << 8) | (q[6] << 16) | ((uint32_t)q[7] << 24);
+        x.z = q[8] | (q[9] << 8) | (q[10] << 16) | ((uint32_t)q[11] << 24);
+        x.w = q[12] | (q[13] << 8) | (q[14] << 16) | ((uint32_t)q[15] << 24);
+        *reinterpret_cast<uint4*>(dst + g0 + head + 16 * v) = x;
+    }
+    const int tail0 = head + 16 * nvec;
+    if (tid < len - tail0) dst[g0 + tail0 + tid] = sOut[tail0 + tid];
+    if (t0 + kTile >= n && tid == 0) a.host_size[s] = g0 + len;
 }
 
 // ---------------------------------------------------------------------------
@@ -1372,8 +1483,12 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
     else
         hipLaunchKernelGGL(k_code_intra<kMaxRows>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
     hipLaunchKernelGGL(k_cavlc, dim3(nmb), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_assemble, dim3(a.num_slices), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_gather, dim3(a.num_slices), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_slice_scan, dim3(a.num_slices), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_mb_concat, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
+    const dim3 tiles(a.max_tiles, a.num_slices);
+    hipLaunchKernelGGL(k_ep_nz, tiles, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_ep_count, tiles, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_ep_write, tiles, dim3(256), 0, s, a);
 }
 
 void launch_commit(const FrameArgs& a, hipStream_t s) {

@@ -74,8 +74,6 @@ class HipBackend : public EncoderBackend {
         run_encode_graph();
         HIPCHECK(hipMemcpyAsync(h_tasks_, args_.tasks, sizeof(SliceTask) * g_.num_slices,
                                 hipMemcpyDeviceToHost, stream_));
-        HIPCHECK(hipMemcpyAsync(h_out_size_, args_.out_size, sizeof(int) * g_.num_slices,
-                                hipMemcpyDeviceToHost, stream_));
         HIPCHECK(hipEventRecord(ev_[2], stream_));
         HIPCHECK(hipStreamSynchronize(stream_));
         build_packets(frame_id);
@@ -168,7 +166,6 @@ class HipBackend : public EncoderBackend {
         a.mb_dirty = dmalloc<uint8_t>(nmb);
         a.stripe_dirty = dmalloc<int>(ns);
         a.tasks = dmalloc<SliceTask>(ns);
-        a.slice_sums = dmalloc<long long>(2 * ns);
         a.me = dmalloc<MeResult>(nmb);
         a.mvfield = dmalloc<int16_t>(2 * nmb);
         a.mbs = dmalloc<MbInfo>(nmb);
@@ -178,15 +175,21 @@ class HipBackend : public EncoderBackend {
         int max_slice_mbs = g_.rows_per_slice * g_.mb_w;
         a.rbsp_slot_words = (max_slice_mbs * gpu::kMbSlotBytes + 1024) / 4;
         a.rbsp = dmalloc<uint32_t>((size_t)ns * a.rbsp_slot_words);
+        a.mb_off = dmalloc<int>(nmb);
+        a.slice_info = dmalloc<int>(4 * (size_t)ns);
+        a.max_tiles = (a.rbsp_slot_words * 4 + 4095) / 4096;
+        a.tile_nz = dmalloc<int>((size_t)ns * a.max_tiles);
+        a.tile_ins = dmalloc<int>((size_t)ns * a.max_tiles);
         // worst case: header + SPS/PPS + 3/2 emulation-prevention growth, 64-byte multiple
         size_t slot = ((size_t)a.rbsp_slot_words * 4 * 3 / 2 + 1024 + 63) & ~(size_t)63;
         a.out_slot_bytes = (int)slot;
-        a.out = dmalloc<uint8_t>(slot * ns, false);
-        a.out_size = dmalloc<int>(ns);
         host_out_ = hmalloc<uint8_t>(slot * ns);
+        h_out_size_ = hmalloc<int>(ns);
         void* dptr = nullptr;
         HIPCHECK(hipHostGetDevicePointer(&dptr, host_out_, 0));
         a.host_out = (uint8_t*)dptr;
+        HIPCHECK(hipHostGetDevicePointer(&dptr, h_out_size_, 0));
+        a.host_size = (int*)dptr;
         // parameter sets
         std::vector<std::vector<uint8_t>> ps;
         if (cfg_.fullframe) {
@@ -219,7 +222,6 @@ class HipBackend : public EncoderBackend {
         a.frame_params = d_frame_params_;
         h_dirty_ = hmalloc<int>(ns);
         h_tasks_ = hmalloc<SliceTask>(ns);
-        h_out_size_ = hmalloc<int>(ns);
         h_frame_params_ = hmalloc<int>(4);
         dirty8_.assign(ns, 0);
     }
@@ -239,7 +241,7 @@ class HipBackend : public EncoderBackend {
 
     void enqueue_encode() {
         const int ns = g_.num_slices;
-        (void)ns;  // slice_sums, stripe_dirty and rbsp are self-cleaning (k_decide / k_assemble)
+        (void)ns;  // stripe_dirty and rbsp are self-cleaning (k_decide / k_ep_write)
         gpu::launch_encode(args_, stream_);
         gpu::launch_commit(args_, stream_);
     }
@@ -263,12 +265,8 @@ class HipBackend : public EncoderBackend {
 
     void build_packets(uint16_t frame_id) {
         const int ns = g_.num_slices;
-        long off = 0;
         std::vector<long> offs(ns);
-        for (int s = 0; s < ns; s++) {
-            offs[s] = off;
-            off += ((long)h_out_size_[s] + 63) & ~63L;
-        }
+        for (int s = 0; s < ns; s++) offs[s] = (long)s * args_.out_slot_bytes;
         if (cfg_.fullframe) {
             bool idr = ctl_.picture_is_idr(h_tasks_);
             EncodedPacket pk;

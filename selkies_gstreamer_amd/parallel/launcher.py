@@ -1,0 +1,162 @@
+"""Node launcher: many desktop sessions on one multi-GPU MI355X node.
+
+Starts one ``selkies`` server process per session (its own X display, port and
+GPU chosen by :class:`SessionPlacer`), watches them (process exit and the
+``/health`` endpoint) and restarts failed sessions with exponential back-off —
+the failure-detection / recovery role the reference delegates to supervisord
+(addons/example/supervisord.conf).
+
+    python -m selkies_gstreamer_amd.parallel.launcher --sessions 16 --gpus 8 \
+        --base-port 8082 --display-base 20 [-- extra selkies flags]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+import sys
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+from .placement import SessionPlacer, session_weight
+
+log = logging.getLogger("launcher")
+
+
+@dataclass
+class SessionSpec:
+    name: str
+    display: str
+    port: int
+    gpu: int
+    extra: list = field(default_factory=list)
+
+    def command(self, python: str = sys.executable) -> list[str]:
+        return [python, "-m", "selkies_gstreamer_amd", "--port", str(self.port), "--gpu-id", str(self.gpu),
+                *self.extra]
+
+    def env(self, base: Optional[dict] = None) -> dict:
+        e = dict(os.environ if base is None else base)
+        e["DISPLAY"] = self.display
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        return e
+
+
+def plan_sessions(n: int, gpus: int, base_port: int, display_base: int, width: int = 1920, height: int = 1080,
+                  fps: float = 60.0, extra: Optional[list] = None, capacity: float = 48.0) -> list[SessionSpec]:
+    placer = SessionPlacer(gpus, capacity)
+    out = []
+    for i in range(n):
+        gpu = placer.acquire(f"s{i}", session_weight(width, height, fps))
+        if gpu is None:
+            raise RuntimeError(f"node is full after {i} sessions (capacity {capacity} x 1080p60 per GPU)")
+        out.append(SessionSpec(f"s{i}", f":{display_base + i}", base_port + i, gpu, list(extra or [])))
+    return out
+
+
+class Supervisor:
+    def __init__(self, specs: list[SessionSpec], health_interval: float = 5.0, max_backoff: float = 60.0,
+                 check_health: bool = True):
+        self.specs = specs
+        self.procs: dict = {}
+        self.restarts: dict = {s.name: 0 for s in specs}
+        self.health_interval, self.max_backoff = health_interval, max_backoff
+        self.check_health = check_health
+        self.stopping = False
+
+    async def _spawn(self, spec: SessionSpec):
+        p = await asyncio.create_subprocess_exec(*spec.command(), env=spec.env())
+        self.procs[spec.name] = p
+        log.info("session %s: pid %d, display %s, port %d, gpu %d", spec.name, p.pid, spec.display, spec.port,
+                 spec.gpu)
+        return p
+
+    async def _healthy(self, spec: SessionSpec) -> bool:
+        import aiohttp
+        try:
+            async with aiohttp.ClientSession() as s:
+                async with s.get(f"http://127.0.0.1:{spec.port}/health",
+                                 timeout=aiohttp.ClientTimeout(total=3)) as r:
+                    return r.status == 200
+        except Exception:
+            return False
+
+    async def _watch(self, spec: SessionSpec):
+        backoff = 1.0
+        while not self.stopping:
+            p = await self._spawn(spec)
+            started = time.monotonic()
+            unhealthy = 0
+            while p.returncode is None and not self.stopping:
+                try:
+                    await asyncio.wait_for(p.wait(), self.health_interval)
+                except asyncio.TimeoutError:
+                    if self.check_health and time.monotonic() - started > 3 * self.health_interval:
+                        unhealthy = 0 if await self._healthy(spec) else unhealthy + 1
+                        if unhealthy >= 3:
+                            log.error("session %s failed health checks; restarting", spec.name)
+                            p.terminate()
+                            await p.wait()
+            if self.stopping:
+                break
+            self.restarts[spec.name] += 1
+            if time.monotonic() - started > 60:
+                backoff = 1.0
+            log.warning("session %s exited (%s); restart #%d in %.0fs", spec.name, p.returncode,
+                        self.restarts[spec.name], backoff)
+            await asyncio.sleep(backoff)
+            backoff = min(self.max_backoff, backoff * 2)
+
+    async def run(self):
+        await asyncio.gather(*(self._watch(s) for s in self.specs))
+
+    async def stop(self):
+        self.stopping = True
+        for p in self.procs.values():
+            if p.returncode is None:
+                p.send_signal(signal.SIGTERM)
+        for p in self.procs.values():
+            try:
+                await asyncio.wait_for(p.wait(), 10)
+            except asyncio.TimeoutError:
+                p.kill()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Run many selkies sessions across the GPUs of one node")
+    ap.add_argument("--sessions", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--base-port", type=int, default=8082)
+    ap.add_argument("--display-base", type=int, default=20)
+    ap.add_argument("--capacity", type=float, default=48.0, help="1080p60 sessions per GPU")
+    ap.add_argument("--dry-run", action="store_true", help="print the plan and exit")
+    args, extra = ap.parse_known_args(argv)
+    if extra and extra[0] == "--":
+        extra = extra[1:]
+    logging.basicConfig(level=logging.INFO)
+    specs = plan_sessions(args.sessions, args.gpus, args.base_port, args.display_base, extra=extra,
+                          capacity=args.capacity)
+    if args.dry_run:
+        for s in specs:
+            print(f"{s.name} DISPLAY={s.display} {' '.join(s.command())}")
+        return 0
+    sup = Supervisor(specs)
+
+    async def run():
+        loop = asyncio.get_running_loop()
+        stop = asyncio.Event()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(sig, stop.set)
+        task = asyncio.create_task(sup.run())
+        await stop.wait()
+        await sup.stop()
+        task.cancel()
+    asyncio.run(run())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
