@@ -14,6 +14,8 @@
 #include <string.h>
 #include <string>
 #include <thread>
+#include <algorithm>
+#include <vector>
 
 
 namespace sk {
@@ -93,6 +95,18 @@ class CaptureSession {
 
     void request_keyframe() { key_req_ = true; }
 
+    // Premultiplied BGRA watermark, composited onto every captured frame before
+    // encoding. location: 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right,
+    // 4 centre, 5 bouncing (moves 2 px per frame), 6 tiled; < 0 disables.
+    // (pixelflux's own enum is not part of the reference tree; this mapping is ours.)
+    void set_watermark(const uint8_t* bgra, int w, int h, int location) {
+        std::lock_guard<std::mutex> g(mu_);
+        wm_.assign(bgra, bgra + (size_t)w * h * 4);
+        wm_w_ = w;
+        wm_h_ = h;
+        wm_loc_ = location;
+    }
+
     void stats(double* out, int n) {
         std::lock_guard<std::mutex> g(mu_);
         double v[6] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
@@ -112,6 +126,7 @@ class CaptureSession {
             if (key_req_.exchange(false)) enc_->request_keyframe();
             int stride = 0;
             const uint8_t* px = src_->grab(&stride);
+            if (px && wm_loc_ >= 0 && !wm_.empty()) composite_watermark(const_cast<uint8_t*>(px), stride, frame_id);
             if (px) {
                 auto t0 = clk::now();
                 int n = -1;
@@ -152,6 +167,47 @@ class CaptureSession {
         }
     }
 
+    void composite_watermark(uint8_t* px, int stride, unsigned t) {
+        std::lock_guard<std::mutex> g(mu_);
+        const int W = s_.capture_width, H = s_.capture_height, w = wm_w_, h = wm_h_;
+        auto blit = [&](int x0, int y0) {
+            for (int j = 0; j < h; j++) {
+                const int y = y0 + j;
+                if (y < 0 || y >= H) continue;
+                for (int i = 0; i < w; i++) {
+                    const int x = x0 + i;
+                    if (x < 0 || x >= W) continue;
+                    const uint8_t* s = &wm_[((size_t)j * w + i) * 4];
+                    const uint32_t a = s[3];
+                    if (!a) continue;
+                    uint8_t* d = px + (size_t)y * stride + 4 * x;
+                    for (int c = 0; c < 3; c++) d[c] = (uint8_t)(s[c] + (d[c] * (255 - a) + 127) / 255);
+                }
+            }
+        };
+        const int m = 16;  // margin
+        switch (wm_loc_) {
+            case 0: blit(m, m); break;
+            case 1: blit(W - w - m, m); break;
+            case 2: blit(m, H - h - m); break;
+            case 3: blit(W - w - m, H - h - m); break;
+            case 4: blit((W - w) / 2, (H - h) / 2); break;
+            case 5: {
+                const int rx = std::max(1, W - w), ry = std::max(1, H - h);
+                const int px_ = (int)((2 * t) % (2 * rx)), py_ = (int)((2 * t) % (2 * ry));
+                blit(px_ < rx ? px_ : 2 * rx - px_, py_ < ry ? py_ : 2 * ry - py_);
+                break;
+            }
+            case 6:
+                for (int y = 0; y < H; y += h + 2 * m)
+                    for (int x = 0; x < W; x += w + 2 * m) blit(x + m, y + m);
+                break;
+            default: break;
+        }
+    }
+
+    std::vector<uint8_t> wm_;
+    int wm_w_ = 0, wm_h_ = 0, wm_loc_ = -1;
     sk_capture_settings s_{};
     std::string display_;
     sk_stripe_cb cb_ = nullptr;
@@ -178,4 +234,7 @@ int sk_capture_start(void* c, const sk_capture_settings* s, sk_stripe_cb cb, voi
 void sk_capture_stop(void* c) { static_cast<CaptureSession*>(c)->stop(); }
 void sk_capture_request_keyframe(void* c) { static_cast<CaptureSession*>(c)->request_keyframe(); }
 void sk_capture_stats(void* c, double* out, int n) { static_cast<CaptureSession*>(c)->stats(out, n); }
+void sk_capture_set_watermark(void* c, const uint8_t* bgra, int w, int h, int location) {
+    static_cast<CaptureSession*>(c)->set_watermark(bgra, w, h, location);
+}
 }

@@ -88,6 +88,8 @@ void sk_capture_stop(void* c);
 void sk_capture_request_keyframe(void* c);
 // frames, mean encode ms, bytes, packets, source (1 = X11, 0 = synthetic), last encode ms
 void sk_capture_stats(void* c, double* out, int n);
+// Premultiplied BGRA watermark composited before encoding (location enum in capture.cpp).
+void sk_capture_set_watermark(void* c, const uint8_t* bgra, int w, int h, int location);
 
 // ---- X11 input injection (XTest) and cursor watching (XFixes) ----
 // cursor_only=1 opens a connection that only watches cursor changes.

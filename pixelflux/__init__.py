@@ -67,9 +67,26 @@ class ScreenCapture:
         self._settings = None
         self._lock = threading.Lock()
 
+    def set_watermark(self, path: str, location: int) -> bool:
+        """Loads a PNG (alpha respected) to composite at `location` (0-6, see csrc/runtime/capture.cpp)."""
+        try:
+            import numpy as np
+            from PIL import Image
+            im = np.asarray(Image.open(path).convert("RGBA"), dtype=np.uint16)
+        except (OSError, ImportError, ValueError):
+            return False
+        a = im[..., 3:4]
+        bgra = np.concatenate([(im[..., 2::-1] * a + 127) // 255, a], axis=2).astype(np.uint8)
+        bgra = np.ascontiguousarray(bgra)
+        self._wm = bgra
+        self._lib.sk_capture_set_watermark(self._h, bgra.ctypes.data, bgra.shape[1], bgra.shape[0], int(location))
+        return True
+
     def start_capture(self, settings: CaptureSettings, callback) -> None:
         if not isinstance(callback, StripeCallback):
             callback = StripeCallback(callback)
+        if settings.watermark_path and settings.watermark_location_enum >= 0:
+            self.set_watermark(settings.watermark_path.decode(), settings.watermark_location_enum)
         with self._lock:
             self._cb = callback  # keep the thunk alive while the native thread runs
             self._settings = settings

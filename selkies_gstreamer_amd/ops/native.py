@@ -110,6 +110,8 @@ def lib():
         L.sk_capture_stop.argtypes = [ctypes.c_void_p]
         L.sk_capture_request_keyframe.argtypes = [ctypes.c_void_p]
         L.sk_capture_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+        L.sk_capture_set_watermark.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int]
         _lib = L
         return L
 

@@ -153,3 +153,22 @@ def test_pcmflux_contract():
         with pytest.raises(RuntimeError):
             cap.start_capture(s, pcmflux.AudioChunkCallback(lambda r, u: None))
     cap.stop_capture()
+
+
+def test_capture_watermark(tmp_path):
+    import pixelflux
+    png = tmp_path / "wm.png"
+    wm = np.zeros((24, 40, 4), np.uint8)
+    wm[..., 0] = 255   # opaque red
+    wm[..., 3] = 255
+    Image.fromarray(wm, "RGBA").save(png)
+    s = pixelflux.default_settings(160, 96, use_cpu=1, source=2, target_fps=30.0, output_mode=0, stripe_height=32,
+                                   watermark_path=str(png), watermark_location_enum=3)
+    got, _ = _collect(s, 0.4)
+    canvas = np.zeros((96, 160, 3), np.uint8)
+    for _, fid, y, sh, data in got:
+        canvas[y:y + sh] = _decode_jpeg_packet(data)[2]
+    # bottom-right, 16 px margin: rows 56..79, cols 104..143
+    patch = canvas[60:76, 108:140].astype(int)
+    assert patch[..., 0].mean() > 200 and patch[..., 1].mean() < 60 and patch[..., 2].mean() < 60
+    assert canvas[10:20, 10:40, 0].mean() < 200 or canvas[10:20, 10:40, 1].mean() > 60  # not red elsewhere
