@@ -25,7 +25,7 @@ struct FrameArgs {
     int bgrx_stride;
     Planes src, prev, ref, rec;
     uint8_t* mb_dirty;     // [num_mbs]
-    int* stripe_dirty;     // [num_slices]
+    int* dirty_host;       // host-mapped [num_slices * 32] stripe dirty flags (one cache line each)
     SliceTask* tasks;      // [num_slices]
     MeResult* me;          // [num_mbs]
     int16_t* mvfield;      // [num_mbs][2]
@@ -46,9 +46,12 @@ struct FrameArgs {
     int param_set_stride;
     uint8_t* host_out;     // host-mapped packet slots [num_slices][out_slot_bytes]
     int* host_size;        // host-mapped [num_slices] bytes in each slot
-    const int* frame_params;  // device: [0] = frame_id
+    int* frame_params_dev;           // device: [0] = frame_id (loaded by k_load_tasks)
+    const int* frame_params_host;    // host-mapped source
+    SliceTask* tasks_host;           // host-mapped: plan in, final decisions out
     int first_frame;
     unsigned long long* dbg;  // optional s_memtime stamps (SK_STAMPS=1), else nullptr
+    const CavlcTables* cavlc_tabs;  // precomputed CAVLC tables (device memory), copied to LDS per WG
 };
 
 void launch_convert_damage(const FrameArgs& a, hipStream_t s);

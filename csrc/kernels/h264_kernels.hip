@@ -68,6 +68,14 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
+// Copies the precomputed CAVLC tables (device memory) into LDS with dword loads.
+__device__ __forceinline__ void load_cavlc_tables(CavlcTables& dst, const CavlcTables* src) {
+    static_assert(sizeof(CavlcTables) % 4 == 0, "dword copy");
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(&dst);
+    for (int i = threadIdx.x; i < (int)(sizeof(CavlcTables) / 4); i += blockDim.x) d[i] = s[i];
+}
+
 // Exclusive block-wide scan for blockDim = 64 * NW; the block total goes to *total.
 template <int NW>
 __device__ __forceinline__ int block_excl_scan(int v, int* wave_tot, int* total) {
@@ -180,54 +188,77 @@ struct AtomicBitWriter {
 
 // ---------------------------------------------------------------------------
 // K1 + K3: colour conversion and damage detection.
-// Block = 256 threads = 32 x 8 chroma quads = 64 x 16 pixels (4 macroblocks).
+// Workgroup = 256 threads = one MB row segment of 16 MBs (256 x 16 pixels);
+// thread = 8 x 2 pixels (4 chroma quads) with 16-byte BGRx loads. Per-MB dirty
+// flags go to mb_dirty; the stripe flag is one plain store per workgroup into
+// host-mapped memory (no same-line atomics, no device->host copy).
+__device__ __forceinline__ uint32_t bgrx_px(const uint8_t* row, int x, int W) {
+    return *reinterpret_cast<const uint32_t*>(row + 4 * sk_min(x, W - 1));
+}
+
 __global__ __launch_bounds__(256) void k_convert_damage(FrameArgs a) {
-    __shared__ int dirty[4];
-    int t = threadIdx.x;
-    if (t < 4) dirty[t] = 0;
+    __shared__ int mbd[16];
+    const int t = threadIdx.x;
+    if (t < 16) mbd[t] = 0;
     __syncthreads();
-    int qc = t & 31, qr = t >> 5;
-    int qx = blockIdx.x * 32 + qc, qy = blockIdx.y * 8 + qr;
+    const int item = t & 31, qr = t >> 5;          // 32 items across (8 px each), 8 quad rows
+    const int mby = blockIdx.y, mbx0 = blockIdx.x * 16;
+    const int x0 = mbx0 * 16 + item * 8;            // first pixel column of this item
+    const int qy = mby * 8 + qr;
     bool diff = false;
-    if (qx < a.stride_c) {
-        int x0 = min(2 * qx, a.W - 1), x1 = min(2 * qx + 1, a.W - 1);
-        int y0 = min(2 * qy, a.H - 1), y1 = min(2 * qy + 1, a.H - 1);
+    if (x0 < a.stride_y) {
+        const int y0 = min(2 * qy, a.H - 1), y1 = min(2 * qy + 1, a.H - 1);
         const uint8_t* r0 = a.bgrx + (size_t)y0 * a.bgrx_stride;
         const uint8_t* r1 = a.bgrx + (size_t)y1 * a.bgrx_stride;
-        uint32_t p00, p01, p10, p11;
-        if (x1 == x0 + 1) {
-            uint2 v0 = *reinterpret_cast<const uint2*>(r0 + 4 * x0);
-            uint2 v1 = *reinterpret_cast<const uint2*>(r1 + 4 * x0);
-            p00 = v0.x; p01 = v0.y; p10 = v1.x; p11 = v1.y;
+        uint32_t p0[8], p1[8];
+        if (x0 + 7 < a.W && (a.bgrx_stride & 15) == 0) {
+            const uint4 a0 = *reinterpret_cast<const uint4*>(r0 + 4 * x0);
+            const uint4 a1 = *reinterpret_cast<const uint4*>(r0 + 4 * x0 + 16);
+            const uint4 b0 = *reinterpret_cast<const uint4*>(r1 + 4 * x0);
+            const uint4 b1 = *reinterpret_cast<const uint4*>(r1 + 4 * x0 + 16);
+            p0[0] = a0.x; p0[1] = a0.y; p0[2] = a0.z; p0[3] = a0.w;
+            p0[4] = a1.x; p0[5] = a1.y; p0[6] = a1.z; p0[7] = a1.w;
+            p1[0] = b0.x; p1[1] = b0.y; p1[2] = b0.z; p1[3] = b0.w;
+            p1[4] = b1.x; p1[5] = b1.y; p1[6] = b1.z; p1[7] = b1.w;
         } else {
-            p00 = *reinterpret_cast<const uint32_t*>(r0 + 4 * x0);
-            p01 = *reinterpret_cast<const uint32_t*>(r0 + 4 * x1);
-            p10 = *reinterpret_cast<const uint32_t*>(r1 + 4 * x0);
-            p11 = *reinterpret_cast<const uint32_t*>(r1 + 4 * x1);
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                p0[i] = bgrx_px(r0, x0 + i, a.W);
+                p1[i] = bgrx_px(r1, x0 + i, a.W);
+            }
         }
-        uint8_t y[4], cb, cr;
-        bgrx_quad_to_yuv((const uint8_t*)&p00, (const uint8_t*)&p01, (const uint8_t*)&p10,
-                         (const uint8_t*)&p11, a.full_range, y, &cb, &cr);
-        size_t oy = (size_t)(2 * qy) * a.stride_y + 2 * qx;
-        uint16_t ya = (uint16_t)(y[0] | (y[1] << 8)), yb = (uint16_t)(y[2] | (y[3] << 8));
-        uint16_t pa = *reinterpret_cast<const uint16_t*>(a.prev.y + oy);
-        uint16_t pb = *reinterpret_cast<const uint16_t*>(a.prev.y + oy + a.stride_y);
-        size_t oc = (size_t)qy * a.stride_c + qx;
-        diff = (pa != ya) | (pb != yb) | (a.prev.u[oc] != cb) | (a.prev.v[oc] != cr);
-        *reinterpret_cast<uint16_t*>(a.src.y + oy) = ya;
-        *reinterpret_cast<uint16_t*>(a.src.y + oy + a.stride_y) = yb;
-        a.src.u[oc] = cb;
-        a.src.v[oc] = cr;
+        uint32_t ya[2] = {0, 0}, yb[2] = {0, 0}, cbw = 0, crw = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint8_t y[4], cb, cr;
+            bgrx_quad_to_yuv((const uint8_t*)&p0[2 * q], (const uint8_t*)&p0[2 * q + 1], (const uint8_t*)&p1[2 * q],
+                             (const uint8_t*)&p1[2 * q + 1], a.full_range, y, &cb, &cr);
+            const int sh = 16 * (q & 1);
+            ya[q >> 1] |= (uint32_t)(y[0] | (y[1] << 8)) << sh;
+            yb[q >> 1] |= (uint32_t)(y[2] | (y[3] << 8)) << sh;
+            cbw |= (uint32_t)cb << (8 * q);
+            crw |= (uint32_t)cr << (8 * q);
+        }
+        const size_t oy = (size_t)(2 * qy) * a.stride_y + x0;
+        const size_t oc = (size_t)qy * a.stride_c + x0 / 2;
+        const uint2 pa = *reinterpret_cast<const uint2*>(a.prev.y + oy);
+        const uint2 pb = *reinterpret_cast<const uint2*>(a.prev.y + oy + a.stride_y);
+        const uint32_t pu = *reinterpret_cast<const uint32_t*>(a.prev.u + oc);
+        const uint32_t pv = *reinterpret_cast<const uint32_t*>(a.prev.v + oc);
+        diff = (pa.x != ya[0]) | (pa.y != ya[1]) | (pb.x != yb[0]) | (pb.y != yb[1]) | (pu != cbw) | (pv != crw);
+        *reinterpret_cast<uint2*>(a.src.y + oy) = make_uint2(ya[0], ya[1]);
+        *reinterpret_cast<uint2*>(a.src.y + oy + a.stride_y) = make_uint2(yb[0], yb[1]);
+        *reinterpret_cast<uint32_t*>(a.src.u + oc) = cbw;
+        *reinterpret_cast<uint32_t*>(a.src.v + oc) = crw;
     }
-    if (diff || a.first_frame) dirty[qc >> 3] = 1;
+    if (diff || a.first_frame) mbd[item >> 1] = 1;   // 2 items per MB
     __syncthreads();
-    if (t < 4) {
-        int mbx = blockIdx.x * 4 + t, mby = blockIdx.y;
-        if (mbx < a.mb_w) {
-            a.mb_dirty[mby * a.mb_w + mbx] = (uint8_t)dirty[t];
-            if (dirty[t]) atomicOr(&a.stripe_dirty[mby / a.rows_per_slice], 1);
-        }
+    if (t < 16) {
+        const int mbx = mbx0 + t;
+        if (mbx < a.mb_w) a.mb_dirty[mby * a.mb_w + mbx] = (uint8_t)mbd[t];
     }
+    if (__syncthreads_or(t < 16 && mbd[t] && mbx0 + t < a.mb_w) && t == 0)
+        a.dirty_host[32 * (mby / a.rows_per_slice)] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -355,6 +386,16 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
     }
 }
 
+// First graph node: pulls the host's slice plan and frame parameters out of
+// host-mapped memory (replaces two host->device copies per frame).
+__global__ __launch_bounds__(64) void k_load_tasks(FrameArgs a) {
+    const int n = a.num_slices * (int)(sizeof(SliceTask) / 4);
+    const int* src = reinterpret_cast<const int*>(a.tasks_host);
+    int* dst = reinterpret_cast<int*>(a.tasks);
+    for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+    if (threadIdx.x < 4) a.frame_params_dev[threadIdx.x] = a.frame_params_host[threadIdx.x];
+}
+
 // One workgroup per slice: scene-cut decision from the per-MB ME results.
 __global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
     __shared__ long long red[2][4];
@@ -383,7 +424,7 @@ __global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
         const long long ts = red[0][0] + red[0][1] + red[0][2] + red[0][3];
         const long long td = red[1][0] + red[1][1] + red[1][2] + red[1][3];
         t.final_action = (p && ts > td) ? ACT_I : t.action;
-        a.stripe_dirty[s] = 0;  // self-cleaning for the next frame
+        a.tasks_host[s] = t;  // final decision back to the host (host-mapped)
     }
 }
 
@@ -760,10 +801,15 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
 
 // ---------------------------------------------------------------------------
 // K6 inter: one wave per MB of a P slice (SKIPALL slices just record skips).
-__global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
-    __shared__ MbScratch S;
+// 4 waves per workgroup, one MB per wave: the CAVLC tables are loaded once per 4 MBs.
+__global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
+    __shared__ MbScratch Sw[4];
+    __shared__ CavlcTables T;
+    load_cavlc_tables(T, a.cavlc_tabs);
+    __syncthreads();
+    MbScratch& S = Sw[threadIdx.x >> 6];
     int nmb = a.mb_w * a.mb_h;
-    int idx = xcd_remap(blockIdx.x, gridDim.x);
+    int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
     if (idx >= nmb) return;
     int mbx = idx % a.mb_w, mby = idx / a.mb_w;
     int s = mby / a.rows_per_slice;
@@ -780,9 +826,6 @@ __global__ __launch_bounds__(64) void k_code_inter(FrameArgs a) {
         return;
     }
     if (t.final_action != ACT_P) return;
-    __shared__ CavlcTables T;
-    cavlc_tables_copy_range(T, l, 64);
-    __syncthreads();
     // MV prediction from the final motion field (all MBs of a P slice are inter)
     auto nbr = [&](int ox, int oy, bool ok) {
         MvNb n;
@@ -877,7 +920,7 @@ __global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
     __shared__ uint8_t zero16[16];
     __shared__ CavlcTables T;
     if (threadIdx.x < 16) zero16[threadIdx.x] = 0;
-    cavlc_tables_copy_range(T, threadIdx.x, blockDim.x);
+    load_cavlc_tables(T, a.cavlc_tabs);
     __syncthreads();
     int s = blockIdx.x;
     const SliceTask t = a.tasks[s];
@@ -1019,11 +1062,17 @@ __global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
 
 // ---------------------------------------------------------------------------
 // K8: CAVLC, one wave per coded MB.
-__global__ __launch_bounds__(64) void k_cavlc(FrameArgs a) {
-    __shared__ uint32_t bits[kMbSlotBytes / 4];
-    __shared__ int16_t coef[kCoefPerMb];
+// 4 waves per workgroup, one MB per wave (tables shared).
+__global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
+    __shared__ uint32_t bits_w[4][kMbSlotBytes / 4];
+    __shared__ int16_t coef_w[4][kCoefPerMb];
+    __shared__ CavlcTables T;
+    load_cavlc_tables(T, a.cavlc_tabs);
+    __syncthreads();
+    uint32_t* bits = bits_w[threadIdx.x >> 6];
+    int16_t* coef = coef_w[threadIdx.x >> 6];
     int nmb = a.mb_w * a.mb_h;
-    int idx = xcd_remap(blockIdx.x, gridDim.x);
+    int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
     if (idx >= nmb) return;
     int mbx = idx % a.mb_w, mby = idx / a.mb_w;
     int s = mby / a.rows_per_slice;
@@ -1035,9 +1084,6 @@ __global__ __launch_bounds__(64) void k_cavlc(FrameArgs a) {
         if (l == 0) a.mb_nbits[idx] = 0;
         return;
     }
-    __shared__ CavlcTables T;
-    cavlc_tables_copy_range(T, l, 64);
-    __syncthreads();
     bool p_slice = t.final_action == ACT_P;
     int first = t.first_row * a.mb_w;
     // mb_skip_run: skipped MBs since the previous coded MB of the slice
@@ -1228,7 +1274,7 @@ __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
         if (!a.fullframe) {
             const int y = task.first_row * 16;
             const int h = sk_min(a.H, (task.first_row + task.num_rows) * 16) - y;
-            const int fid = a.frame_params[0];
+            const int fid = a.frame_params_dev[0];
             uint8_t pre[10] = {0x04, (uint8_t)(idr ? 1 : 0), (uint8_t)(fid >> 8), (uint8_t)fid, (uint8_t)(y >> 8),
                                (uint8_t)y, (uint8_t)(a.W >> 8), (uint8_t)a.W, (uint8_t)(h >> 8), (uint8_t)h};
             for (int i = 0; i < 10; i++) slot[i] = pre[i];
@@ -1435,54 +1481,63 @@ __global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_commit(FrameArgs a) {
-    int nmb = a.mb_w * a.mb_h;
-    int idx = blockIdx.x;
-    if (idx >= nmb) return;
-    int mbx = idx % a.mb_w, mby = idx / a.mb_w;
-    int s = mby / a.rows_per_slice;
-    int fin = a.tasks[s].final_action;
-    int l = lane_id();
+// Reference update: rec -> ref for coded slices, MV field for the next frame's
+// candidates. One workgroup per MB row segment of 16 MBs, 16-byte accesses.
+__global__ __launch_bounds__(256) void k_commit(FrameArgs a) {
+    const int mby = blockIdx.y, mbx0 = blockIdx.x * 16;
+    const int s = mby / a.rows_per_slice;
+    const int fin = a.tasks[s].final_action;
     if (fin == ACT_NONE) return;
-    if (fin == ACT_SKIPALL) {
-        if (l == 0) { a.mvfield[2 * idx] = 0; a.mvfield[2 * idx + 1] = 0; }
-        return;
+    const int tid = threadIdx.x;
+    const int nmbs = sk_min(16, a.mb_w - mbx0);
+    if (tid < nmbs) {
+        const int idx = mby * a.mb_w + mbx0 + tid;
+        const bool zero = fin == ACT_SKIPALL;
+        a.mvfield[2 * idx] = zero ? 0 : a.me[idx].mvx;
+        a.mvfield[2 * idx + 1] = zero ? 0 : a.me[idx].mvy;
     }
-    // luma 16 rows x 16 bytes: lanes 0..63 copy one u32 each
-    {
-        int row = l >> 2, c4 = (l & 3) * 4;
-        size_t o = (size_t)(mby * 16 + row) * a.stride_y + mbx * 16 + c4;
-        *reinterpret_cast<uint32_t*>(a.ref.y + o) = *reinterpret_cast<const uint32_t*>(a.rec.y + o);
+    if (fin == ACT_SKIPALL) return;  // reference unchanged
+    {   // luma: 16 rows x (nmbs * 16) bytes, one uint4 per thread
+        const int row = tid >> 4, v = tid & 15;
+        if (v < nmbs) {
+            const size_t o = (size_t)(mby * 16 + row) * a.stride_y + (mbx0 + v) * 16;
+            *reinterpret_cast<uint4*>(a.ref.y + o) = *reinterpret_cast<const uint4*>(a.rec.y + o);
+        }
     }
-    if (l < 32) {
-        int comp = l >> 4, row = (l >> 1) & 7, c4 = (l & 1) * 4;
-        size_t o = (size_t)(mby * 8 + row) * a.stride_c + mbx * 8 + c4;
-        uint8_t* dst = comp ? a.ref.v : a.ref.u;
-        const uint8_t* src = comp ? a.rec.v : a.rec.u;
-        *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(src + o);
-    }
-    if (l == 0) {
-        a.mvfield[2 * idx] = a.me[idx].mvx;
-        a.mvfield[2 * idx + 1] = a.me[idx].mvy;
+    if (tid < 128) {  // chroma: 2 planes x 8 rows x (nmbs * 8) bytes, uint4 = 2 MBs
+        const int comp = tid >> 6, row = (tid >> 3) & 7, v = tid & 7;
+        if (2 * v < nmbs) {
+            const size_t o = (size_t)(mby * 8 + row) * a.stride_c + (mbx0 + 2 * v) * 8;
+            uint8_t* dst = comp ? a.ref.v : a.ref.u;
+            const uint8_t* src = comp ? a.rec.v : a.rec.u;
+            if (2 * v + 1 < nmbs && (a.stride_c & 15) == 0) {
+                *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(src + o);
+            } else {  // odd MB count per row: chroma rows are only 8-byte aligned
+                *reinterpret_cast<uint2*>(dst + o) = *reinterpret_cast<const uint2*>(src + o);
+                if (2 * v + 1 < nmbs)
+                    *reinterpret_cast<uint2*>(dst + o + 8) = *reinterpret_cast<const uint2*>(src + o + 8);
+            }
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
 void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
-    dim3 grid((a.mb_w + 3) / 4, a.mb_h);
+    dim3 grid((a.mb_w + 15) / 16, a.mb_h);
     hipLaunchKernelGGL(k_convert_damage, grid, dim3(256), 0, s, a);
 }
 
 void launch_encode(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
+    hipLaunchKernelGGL(k_load_tasks, dim3(1), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_code_inter, dim3(nmb), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     if (a.rows_per_slice <= 4)
         hipLaunchKernelGGL(k_code_intra<4>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
     else
         hipLaunchKernelGGL(k_code_intra<kMaxRows>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
-    hipLaunchKernelGGL(k_cavlc, dim3(nmb), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_slice_scan, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_mb_concat, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     const dim3 tiles(a.max_tiles, a.num_slices);
@@ -1493,7 +1548,8 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
 
 void launch_commit(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
-    hipLaunchKernelGGL(k_commit, dim3(nmb), dim3(64), 0, s, a);
+    (void)nmb;
+    hipLaunchKernelGGL(k_commit, dim3((a.mb_w + 15) / 16, a.mb_h), dim3(256), 0, s, a);
 }
 
 }  // namespace gpu

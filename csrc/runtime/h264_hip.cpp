@@ -58,22 +58,17 @@ class HipBackend : public EncoderBackend {
         }
         if (stride != args_.bgrx_stride) invalidate_graphs();
         set_parity_args(stride);
+        for (int s = 0; s < g_.num_slices; s++) h_dirty_[32 * s] = 0;  // host-mapped, set by k_convert_damage
         HIPCHECK(hipEventRecord(ev_[0], stream_));
         HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, stream_));
         gpu::launch_convert_damage(args_, stream_);
-        HIPCHECK(hipMemcpyAsync(h_dirty_, args_.stripe_dirty, sizeof(int) * g_.num_slices,
-                                hipMemcpyDeviceToHost, stream_));
         HIPCHECK(hipEventRecord(ev_[1], stream_));
         HIPCHECK(hipStreamSynchronize(stream_));
-        for (int s = 0; s < g_.num_slices; s++) dirty8_[s] = (uint8_t)(h_dirty_[s] != 0);
+        for (int s = 0; s < g_.num_slices; s++)
+            dirty8_[s] = (uint8_t)(__atomic_load_n(&h_dirty_[32 * s], __ATOMIC_ACQUIRE) != 0);
         ctl_.plan(dirty8_.data(), h_tasks_);
         h_frame_params_[0] = frame_id;
-        HIPCHECK(hipMemcpyAsync(args_.tasks, h_tasks_, sizeof(SliceTask) * g_.num_slices,
-                                hipMemcpyHostToDevice, stream_));
-        HIPCHECK(hipMemcpyAsync(d_frame_params_, h_frame_params_, 16, hipMemcpyHostToDevice, stream_));
-        run_encode_graph();
-        HIPCHECK(hipMemcpyAsync(h_tasks_, args_.tasks, sizeof(SliceTask) * g_.num_slices,
-                                hipMemcpyDeviceToHost, stream_));
+        run_encode_graph();  // k_load_tasks reads h_tasks_ / h_frame_params_; k_decide writes finals back
         HIPCHECK(hipEventRecord(ev_[2], stream_));
         HIPCHECK(hipStreamSynchronize(stream_));
         build_packets(frame_id);
@@ -134,9 +129,9 @@ class HipBackend : public EncoderBackend {
         return (T*)p;
     }
     template <class T>
-    T* hmalloc(size_t count) {
+    T* hmalloc(size_t count, unsigned flags = hipHostMallocDefault) {
         void* p = nullptr;
-        HIPCHECK(hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault));
+        HIPCHECK(hipHostMalloc(&p, count * sizeof(T), flags));
         memset(p, 0, count * sizeof(T));
         host_allocs_.push_back(p);
         return (T*)p;
@@ -164,7 +159,10 @@ class HipBackend : public EncoderBackend {
         a.ref = make_planes();
         a.rec = make_planes();
         a.mb_dirty = dmalloc<uint8_t>(nmb);
-        a.stripe_dirty = dmalloc<int>(ns);
+        h_dirty_ = hmalloc<int>((size_t)ns * 32);
+        void* dd = nullptr;
+        HIPCHECK(hipHostGetDevicePointer(&dd, h_dirty_, 0));
+        a.dirty_host = (int*)dd;
         a.tasks = dmalloc<SliceTask>(ns);
         a.me = dmalloc<MeResult>(nmb);
         a.mvfield = dmalloc<int16_t>(2 * nmb);
@@ -217,12 +215,19 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipStreamSynchronize(stream_));
         a.param_sets = dps;
         a.param_set_len = dlen;
+        CavlcTables* ct = dmalloc<CavlcTables>(1);
+        HIPCHECK(hipMemcpyAsync(ct, &host_cavlc_tables(), sizeof(CavlcTables), hipMemcpyHostToDevice, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
+        a.cavlc_tabs = ct;
         d_frame_params_ = dmalloc<int>(4);
         if (getenv("SK_STAMPS")) a.dbg = dmalloc<unsigned long long>(64 * 16);
-        a.frame_params = d_frame_params_;
-        h_dirty_ = hmalloc<int>(ns);
-        h_tasks_ = hmalloc<SliceTask>(ns);
-        h_frame_params_ = hmalloc<int>(4);
+        a.frame_params_dev = d_frame_params_;
+        h_tasks_ = hmalloc<SliceTask>(ns, hipHostMallocCoherent);  // read by k_load_tasks
+        HIPCHECK(hipHostGetDevicePointer(&dd, h_tasks_, 0));
+        a.tasks_host = (SliceTask*)dd;
+        h_frame_params_ = hmalloc<int>(4, hipHostMallocCoherent);
+        HIPCHECK(hipHostGetDevicePointer(&dd, h_frame_params_, 0));
+        a.frame_params_host = (const int*)dd;
         dirty8_.assign(ns, 0);
     }
 
@@ -241,7 +246,7 @@ class HipBackend : public EncoderBackend {
 
     void enqueue_encode() {
         const int ns = g_.num_slices;
-        (void)ns;  // stripe_dirty and rbsp are self-cleaning (k_decide / k_ep_write)
+        (void)ns;  // rbsp is self-cleaning (k_ep_write); stripe flags are reset by the host
         gpu::launch_encode(args_, stream_);
         gpu::launch_commit(args_, stream_);
     }
