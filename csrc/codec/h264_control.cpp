@@ -16,6 +16,8 @@
 namespace sk {
 namespace h264 {
 
+static_assert(kFrameNumMask == (1 << kLog2MaxFrameNum) - 1, "frame_num wrap");
+
 void Controller::init(const EncoderConfig& cfg, const Geometry& g) {
     cfg_ = cfg;
     g_ = g;
@@ -29,63 +31,9 @@ void Controller::request_keyframe() {
 }
 
 void Controller::plan(const uint8_t* dirty, SliceTask* tasks) {
-    const bool ff = cfg_.fullframe != 0;
-    for (int s = 0; s < g_.num_slices; s++) {
-        StripeState& st = st_[s];
-        SliceTask& t = tasks[s];
-        memset(&t, 0, sizeof(t));
-        t.first_row = g_.slice_first_row(s);
-        t.num_rows = g_.slice_rows(s);
-        t.pic_row0 = ff ? 0 : t.first_row;
-        t.pic_rows = ff ? g_.mb_h : t.num_rows;
-        t.allow_scenecut = cfg_.scenecut;
-        t.idr_on_intra = ff ? 0 : 1;
-        bool d = dirty[s] != 0;
-        if (d) {
-            st.static_frames = 0;
-            st.dirty_streak++;
-            st.painted = false;
-            st.paint_left = 0;
-            if (st.dirty_streak >= cfg_.damage_threshold) st.hot_left = cfg_.damage_duration;
-        } else {
-            st.static_frames++;
-            st.dirty_streak = 0;
-            if (st.hot_left > 0) st.hot_left--;
-            if (cfg_.use_paint_over && !st.painted && st.static_frames >= cfg_.paint_over_trigger &&
-                st.hot_left == 0) {
-                st.painted = true;
-                st.paint_left = cfg_.paint_over_burst;
-            }
-        }
-        bool paint = false;
-        if (!d && st.paint_left > 0) {
-            paint = true;
-            st.paint_left--;
-        }
-        t.qp = paint ? cfg_.paint_qp : cfg_.qp;
-        bool need_idr = ff ? pic_.need_idr : st.need_idr;
-        if (need_idr) {  // a keyframe counts as a change for paint-over purposes
-            st.painted = false;
-            st.static_frames = 0;
-        }
-        if (need_idr) {
-            t.action = ACT_I;
-            t.allow_scenecut = 0;
-        } else if (d || paint || st.hot_left > 0 || cfg_.streaming_mode) {
-            t.action = ACT_P;
-        } else {
-            t.action = ff ? ACT_SKIPALL : ACT_NONE;
-        }
-        if (ff) {
-            t.frame_num = need_idr ? 0 : pic_.frame_num;
-            t.idr_pic_id = pic_.idr_pic_id;
-            if (need_idr) t.idr_on_intra = 1;
-        } else {
-            t.frame_num = st.frame_num;
-            t.idr_pic_id = st.idr_pic_id;
-        }
-        t.final_action = t.action;
-    }
+    const PlanConfig pc = plan_config(cfg_);
+    for (int s = 0; s < g_.num_slices; s++)
+        plan_stripe(pc, st_[s], pic_, dirty[s] != 0, g_.slice_first_row(s), g_.slice_rows(s), g_.mb_h, tasks[s]);
 }
 
 bool Controller::picture_is_idr(const SliceTask* tasks) const {
@@ -96,27 +44,10 @@ bool Controller::picture_is_idr(const SliceTask* tasks) const {
 
 void Controller::commit(const SliceTask* tasks) {
     if (cfg_.fullframe) {
-        bool idr = picture_is_idr(tasks);
-        if (idr) {
-            pic_.frame_num = 1;
-            pic_.idr_pic_id = (pic_.idr_pic_id + 1) & 0xffff;
-            pic_.need_idr = false;
-        } else {
-            pic_.frame_num = (pic_.frame_num + 1) & ((1 << kLog2MaxFrameNum) - 1);
-        }
+        commit_picture(pic_, picture_is_idr(tasks));
         return;
     }
-    for (int s = 0; s < g_.num_slices; s++) {
-        StripeState& st = st_[s];
-        const SliceTask& t = tasks[s];
-        if (t.final_action == ACT_I) {
-            st.frame_num = 1;
-            st.idr_pic_id = (st.idr_pic_id + 1) & 0xffff;
-            st.need_idr = false;
-        } else if (t.final_action == ACT_P) {
-            st.frame_num = (st.frame_num + 1) & ((1 << kLog2MaxFrameNum) - 1);
-        }
-    }
+    for (int s = 0; s < g_.num_slices; s++) commit_stripe(st_[s], tasks[s].final_action);
 }
 
 // ---------------------------------------------------------------------------

@@ -101,6 +101,94 @@ struct StripeState {
     bool painted = true;   // nothing to paint before the first change
 };
 
+// Controller knobs as a POD, so the same plan code runs on the host (CPU
+// backend) and inside the HIP graph (k_plan), bit-for-bit the same decisions.
+struct PlanConfig {
+    int32_t fullframe, scenecut, use_paint_over, paint_over_trigger, paint_over_burst;
+    int32_t damage_threshold, damage_duration, streaming_mode, qp, paint_qp;
+};
+inline PlanConfig plan_config(const EncoderConfig& c) {
+    return PlanConfig{c.fullframe, c.scenecut, c.use_paint_over, c.paint_over_trigger, c.paint_over_burst,
+                      c.damage_threshold, c.damage_duration, c.streaming_mode, c.qp, c.paint_qp};
+}
+constexpr int kFrameNumMask = (1 << 16) - 1;  // log2_max_frame_num = 16 (h264_syntax.h)
+
+// One stripe's decision for this frame; `pic` is the picture state (full-frame mode).
+SK_HD inline void plan_stripe(const PlanConfig& c, StripeState& st, const StripeState& pic, bool d,
+                              int first_row, int num_rows, int mb_h, SliceTask& t) {
+    const bool ff = c.fullframe != 0;
+    t = SliceTask{};
+    t.first_row = first_row;
+    t.num_rows = num_rows;
+    t.pic_row0 = ff ? 0 : first_row;
+    t.pic_rows = ff ? mb_h : num_rows;
+    t.allow_scenecut = c.scenecut;
+    t.idr_on_intra = ff ? 0 : 1;
+    if (d) {
+        st.static_frames = 0;
+        st.dirty_streak++;
+        st.painted = false;
+        st.paint_left = 0;
+        if (st.dirty_streak >= c.damage_threshold) st.hot_left = c.damage_duration;
+    } else {
+        st.static_frames++;
+        st.dirty_streak = 0;
+        if (st.hot_left > 0) st.hot_left--;
+        if (c.use_paint_over && !st.painted && st.static_frames >= c.paint_over_trigger && st.hot_left == 0) {
+            st.painted = true;
+            st.paint_left = c.paint_over_burst;
+        }
+    }
+    bool paint = false;
+    if (!d && st.paint_left > 0) {
+        paint = true;
+        st.paint_left--;
+    }
+    t.qp = paint ? c.paint_qp : c.qp;
+    const bool need_idr = ff ? pic.need_idr : st.need_idr;
+    if (need_idr) {  // a keyframe counts as a change for paint-over purposes
+        st.painted = false;
+        st.static_frames = 0;
+        t.action = ACT_I;
+        t.allow_scenecut = 0;
+    } else if (d || paint || st.hot_left > 0 || c.streaming_mode) {
+        t.action = ACT_P;
+    } else {
+        t.action = ff ? ACT_SKIPALL : ACT_NONE;
+    }
+    if (ff) {
+        t.frame_num = need_idr ? 0 : pic.frame_num;
+        t.idr_pic_id = pic.idr_pic_id;
+        if (need_idr) t.idr_on_intra = 1;
+    } else {
+        t.frame_num = st.frame_num;
+        t.idr_pic_id = st.idr_pic_id;
+    }
+    t.final_action = t.action;
+}
+
+// Striped mode: stripe state after its slice was coded with `final_action`.
+SK_HD inline void commit_stripe(StripeState& st, int final_action) {
+    if (final_action == ACT_I) {
+        st.frame_num = 1;
+        st.idr_pic_id = (st.idr_pic_id + 1) & 0xffff;
+        st.need_idr = false;
+    } else if (final_action == ACT_P) {
+        st.frame_num = (st.frame_num + 1) & kFrameNumMask;
+    }
+}
+
+// Full-frame mode: picture state after a picture (IDR iff every slice was an IDR slice).
+SK_HD inline void commit_picture(StripeState& pic, bool idr) {
+    if (idr) {
+        pic.frame_num = 1;
+        pic.idr_pic_id = (pic.idr_pic_id + 1) & 0xffff;
+        pic.need_idr = false;
+    } else {
+        pic.frame_num = (pic.frame_num + 1) & kFrameNumMask;
+    }
+}
+
 // Decides, per stripe, what to encode this frame.
 class Controller {
    public:

@@ -25,7 +25,11 @@ struct FrameArgs {
     int bgrx_stride;
     Planes src, prev, ref, rec;
     uint8_t* mb_dirty;     // [num_mbs]
-    int* dirty_host;       // host-mapped [num_slices * 32] stripe dirty flags (one cache line each)
+    int* stripe_dirty;     // [num_slices] set by k_convert_damage, consumed (and cleared) by k_plan
+    StripeState* plan_state;    // [num_slices + 1] controller state (last = picture state)
+    int* plan_ctl;              // [0] keyframe requests seen, [1] frames planned (0 = first frame)
+    const int* key_seq_host;    // host-mapped keyframe request counter
+    PlanConfig plan_cfg;
     SliceTask* tasks;      // [num_slices]
     MeResult* me;          // [num_mbs]
     int16_t* mvfield;      // [num_mbs][2]
@@ -46,16 +50,15 @@ struct FrameArgs {
     int param_set_stride;
     uint8_t* host_out;     // host-mapped packet slots [num_slices][out_slot_bytes]
     int* host_size;        // host-mapped [num_slices] bytes in each slot
-    int* frame_params_dev;           // device: [0] = frame_id (loaded by k_load_tasks)
+    int* frame_params_dev;           // device: [0] = frame_id (loaded by k_plan)
     const int* frame_params_host;    // host-mapped source
-    SliceTask* tasks_host;           // host-mapped: plan in, final decisions out
-    int first_frame;
+    SliceTask* tasks_host;           // host-mapped: final slice decisions (written by k_decide)
     unsigned long long* dbg;  // optional s_memtime stamps (SK_STAMPS=1), else nullptr
     const CavlcTables* cavlc_tabs;  // precomputed CAVLC tables (device memory), copied to LDS per WG
 };
 
 void launch_convert_damage(const FrameArgs& a, hipStream_t s);
-void launch_encode(const FrameArgs& a, hipStream_t s);   // everything after planning
+void launch_encode(const FrameArgs& a, hipStream_t s);   // k_plan and everything after it
 void launch_commit(const FrameArgs& a, hipStream_t s);
 
 }  // namespace gpu

@@ -251,14 +251,14 @@ __global__ __launch_bounds__(256) void k_convert_damage(FrameArgs a) {
         *reinterpret_cast<uint32_t*>(a.src.u + oc) = cbw;
         *reinterpret_cast<uint32_t*>(a.src.v + oc) = crw;
     }
-    if (diff || a.first_frame) mbd[item >> 1] = 1;   // 2 items per MB
+    if (diff || a.plan_ctl[1] == 0) mbd[item >> 1] = 1;   // 2 items per MB; first frame: all dirty
     __syncthreads();
     if (t < 16) {
         const int mbx = mbx0 + t;
         if (mbx < a.mb_w) a.mb_dirty[mby * a.mb_w + mbx] = (uint8_t)mbd[t];
     }
     if (__syncthreads_or(t < 16 && mbd[t] && mbx0 + t < a.mb_w) && t == 0)
-        a.dirty_host[32 * (mby / a.rows_per_slice)] = 1;
+        a.stripe_dirty[mby / a.rows_per_slice] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -386,14 +386,44 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
     }
 }
 
-// First graph node: pulls the host's slice plan and frame parameters out of
-// host-mapped memory (replaces two host->device copies per frame).
-__global__ __launch_bounds__(64) void k_load_tasks(FrameArgs a) {
-    const int n = a.num_slices * (int)(sizeof(SliceTask) / 4);
-    const int* src = reinterpret_cast<const int*>(a.tasks_host);
-    int* dst = reinterpret_cast<int*>(a.tasks);
-    for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
-    if (threadIdx.x < 4) a.frame_params_dev[threadIdx.x] = a.frame_params_host[threadIdx.x];
+// Frame controller on the GPU (one workgroup): commits the previous frame's
+// final slice decisions, applies host keyframe requests (host-mapped counter)
+// and plans this frame from the stripe dirty flags of k_convert_damage — the
+// same plan_stripe/commit_* code the CPU backend runs (codec/h264_encoder.h),
+// so no host round trip sits between damage detection and encoding.
+__global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
+    const int ns = a.num_slices, tid = threadIdx.x;
+    StripeState* st = a.plan_state;
+    StripeState& pic = st[ns];
+    if (a.plan_ctl[1]) {  // deferred commit of the previous frame
+        if (a.fullframe) {
+            bool idr = true;
+            for (int s = tid; s < ns; s += 256) idr &= a.tasks[s].final_action == ACT_I && a.tasks[s].idr_on_intra;
+            idr = __syncthreads_and(idr);
+            if (tid == 0) commit_picture(pic, idr);
+        } else {
+            for (int s = tid; s < ns; s += 256) commit_stripe(st[s], a.tasks[s].final_action);
+        }
+    }
+    const int kq = __hip_atomic_load(a.key_seq_host, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const bool key = kq != a.plan_ctl[0];
+    __syncthreads();
+    if (key) {
+        for (int s = tid; s < ns; s += 256) st[s].need_idr = true;
+        if (tid == 0) pic.need_idr = true;
+    }
+    __syncthreads();
+    for (int s = tid; s < ns; s += 256) {
+        const int r0 = s * a.rows_per_slice, nr = min(a.rows_per_slice, a.mb_h - r0);
+        plan_stripe(a.plan_cfg, st[s], pic, a.stripe_dirty[s] != 0, r0, nr, a.mb_h, a.tasks[s]);
+        a.stripe_dirty[s] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        a.plan_ctl[0] = kq;
+        a.plan_ctl[1] = 1;
+    }
+    if (tid < 4) a.frame_params_dev[tid] = a.frame_params_host[tid];
 }
 
 // One workgroup per slice: scene-cut decision from the per-MB ME results.
@@ -1529,7 +1559,7 @@ void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
 
 void launch_encode(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
-    hipLaunchKernelGGL(k_load_tasks, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);

@@ -1,9 +1,10 @@
 // HIP backend of the H.264 stripe encoder: owns the per-session HBM buffers,
 // the stream, pinned staging, and drives the gfx950 kernels
 // (csrc/kernels/h264_kernels.hip). Frame flow:
-//   H2D(BGRx) -> K1/K3 convert+damage -> D2H(stripe dirty bits) -> host plan ->
-//   H2D(tasks) -> [memsets, K4, decide, K6 inter, K5/K6 intra, K8, K9, gather,
-//   commit] (captured once into a hipGraph per src/prev parity) -> sync -> packets.
+//   H2D(BGRx) -> [K1/K3 convert+damage, k_plan (stripe controller on the GPU),
+//   K4 ME, decide, K6 inter, K5/K6 intra, K8 CAVLC, K9 slice assembly into
+//   host-mapped packet slots, commit] (one hipGraph per src/prev parity)
+//   -> one sync -> packets. No host decision sits inside a frame.
 #include "encoder_iface.h"
 #include "../kernels/h264_gpu.h"
 #include <hip/hip_runtime.h>
@@ -44,7 +45,8 @@ class HipBackend : public EncoderBackend {
         hipStreamDestroy(stream_);
     }
 
-    void request_keyframe() override { ctl_.request_keyframe(); }
+    // Picked up by k_plan at the start of the next frame.
+    void request_keyframe() override { __atomic_fetch_add(h_key_seq_, 1, __ATOMIC_SEQ_CST); }
 
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         HIPCHECK(hipSetDevice(device_));
@@ -58,23 +60,17 @@ class HipBackend : public EncoderBackend {
         }
         if (stride != args_.bgrx_stride) invalidate_graphs();
         set_parity_args(stride);
-        for (int s = 0; s < g_.num_slices; s++) h_dirty_[32 * s] = 0;  // host-mapped, set by k_convert_damage
+        h_frame_params_[0] = frame_id;  // host-mapped, read by k_plan
         HIPCHECK(hipEventRecord(ev_[0], stream_));
         HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, stream_));
-        gpu::launch_convert_damage(args_, stream_);
         HIPCHECK(hipEventRecord(ev_[1], stream_));
-        HIPCHECK(hipStreamSynchronize(stream_));
-        for (int s = 0; s < g_.num_slices; s++)
-            dirty8_[s] = (uint8_t)(__atomic_load_n(&h_dirty_[32 * s], __ATOMIC_ACQUIRE) != 0);
-        ctl_.plan(dirty8_.data(), h_tasks_);
-        h_frame_params_[0] = frame_id;
-        run_encode_graph();  // k_load_tasks reads h_tasks_ / h_frame_params_; k_decide writes finals back
+        // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
+        // one sync; k_decide leaves the final slice decisions in h_tasks_.
+        run_encode_graph();
         HIPCHECK(hipEventRecord(ev_[2], stream_));
         HIPCHECK(hipStreamSynchronize(stream_));
         build_packets(frame_id);
-        ctl_.commit(h_tasks_);
         parity_ ^= 1;
-        first_frame_ = 0;
         float t0 = 0, t1 = 0;
         hipEventElapsedTime(&t0, ev_[0], ev_[1]);
         hipEventElapsedTime(&t1, ev_[1], ev_[2]);
@@ -159,10 +155,20 @@ class HipBackend : public EncoderBackend {
         a.ref = make_planes();
         a.rec = make_planes();
         a.mb_dirty = dmalloc<uint8_t>(nmb);
-        h_dirty_ = hmalloc<int>((size_t)ns * 32);
         void* dd = nullptr;
-        HIPCHECK(hipHostGetDevicePointer(&dd, h_dirty_, 0));
-        a.dirty_host = (int*)dd;
+        a.stripe_dirty = dmalloc<int>(ns);
+        a.plan_ctl = dmalloc<int>(4);
+        a.plan_cfg = plan_config(cfg_);
+        {
+            std::vector<StripeState> init(ns + 1);  // need_idr on every stripe and the picture
+            a.plan_state = dmalloc<StripeState>(ns + 1);
+            HIPCHECK(hipMemcpyAsync(a.plan_state, init.data(), sizeof(StripeState) * (ns + 1),
+                                    hipMemcpyHostToDevice, stream_));
+            HIPCHECK(hipStreamSynchronize(stream_));
+        }
+        h_key_seq_ = hmalloc<int>(16, hipHostMallocCoherent);
+        HIPCHECK(hipHostGetDevicePointer(&dd, h_key_seq_, 0));
+        a.key_seq_host = (const int*)dd;
         a.tasks = dmalloc<SliceTask>(ns);
         a.me = dmalloc<MeResult>(nmb);
         a.mvfield = dmalloc<int16_t>(2 * nmb);
@@ -222,13 +228,12 @@ class HipBackend : public EncoderBackend {
         d_frame_params_ = dmalloc<int>(4);
         if (getenv("SK_STAMPS")) a.dbg = dmalloc<unsigned long long>(64 * 16);
         a.frame_params_dev = d_frame_params_;
-        h_tasks_ = hmalloc<SliceTask>(ns, hipHostMallocCoherent);  // read by k_load_tasks
+        h_tasks_ = hmalloc<SliceTask>(ns, hipHostMallocCoherent);  // final decisions from k_decide
         HIPCHECK(hipHostGetDevicePointer(&dd, h_tasks_, 0));
         a.tasks_host = (SliceTask*)dd;
         h_frame_params_ = hmalloc<int>(4, hipHostMallocCoherent);
         HIPCHECK(hipHostGetDevicePointer(&dd, h_frame_params_, 0));
         a.frame_params_host = (const int*)dd;
-        dirty8_.assign(ns, 0);
     }
 
     void set_parity_args(int stride) {
@@ -236,7 +241,6 @@ class HipBackend : public EncoderBackend {
         args_.bgrx_stride = stride;
         args_.src = planes_src_[parity_];
         args_.prev = planes_src_[parity_ ^ 1];
-        args_.first_frame = first_frame_;
     }
 
     void invalidate_graphs() {
@@ -246,7 +250,8 @@ class HipBackend : public EncoderBackend {
 
     void enqueue_encode() {
         const int ns = g_.num_slices;
-        (void)ns;  // rbsp is self-cleaning (k_ep_write); stripe flags are reset by the host
+        (void)ns;  // rbsp is self-cleaning (k_ep_write); stripe flags are cleared by k_plan
+        gpu::launch_convert_damage(args_, stream_);
         gpu::launch_encode(args_, stream_);
         gpu::launch_commit(args_, stream_);
     }
@@ -308,16 +313,14 @@ class HipBackend : public EncoderBackend {
     gpu::FrameArgs args_;
     gpu::Planes planes_src_[2];
     int parity_ = 0;
-    int first_frame_ = 1;
     uint8_t* bgrx_dev_ = nullptr;
     size_t bgrx_cap_ = 0;
     uint8_t* host_out_ = nullptr;
-    int* h_dirty_ = nullptr;
+    int* h_key_seq_ = nullptr;
     SliceTask* h_tasks_ = nullptr;
     int* h_out_size_ = nullptr;
     int* h_frame_params_ = nullptr;
     int* d_frame_params_ = nullptr;
-    std::vector<uint8_t> dirty8_;
     std::vector<std::vector<uint8_t>> param_sets_;
     std::vector<void*> dev_allocs_, host_allocs_;
     hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};

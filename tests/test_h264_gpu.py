@@ -60,3 +60,23 @@ def test_gpu_escalation_and_odd_geometry():
         assert [p.data for p in gpu.encode(f, t)] == [p.data for p in cpu.encode(f, t)]
     m = gpu.debug_buffer("mbs", MB_INFO_DTYPE)
     assert m["qp"].max() > 4
+
+
+@pytest.mark.parametrize("fullframe", [False, True])
+def test_gpu_controller_matches_cpu(fullframe):
+    """Stripe controller on the GPU (k_plan): damage streaks, paint-over bursts,
+    keyframe requests and frame_num/idr_pic_id bookkeeping match the host controller."""
+    W, H = 160, 96
+    kw = dict(stripe_height=32, fullframe=fullframe, qp=28, paint_qp=20, paint_over_trigger=3,
+              paint_over_burst=2, damage_threshold=2, damage_duration=3)
+    cpu, gpu = _pair(W, H, **kw)
+    moving = list(synthetic_frames(W, H, 5, seed=11))
+    seq = moving[:4] + [moving[3]] * 8 + [moving[4]] * 6
+    for t, f in enumerate(seq):
+        if t in (7, 15):
+            cpu.request_keyframe()
+            gpu.request_keyframe()
+        pc, pg = cpu.encode(f, t), gpu.encode(f, t)
+        ta, tb = cpu.debug_buffer("tasks", TASK_DTYPE), gpu.debug_buffer("tasks", TASK_DTYPE)
+        assert np.array_equal(ta, tb), f"frame {t}: slice plans differ"
+        assert [(p.y, p.key, p.data) for p in pg] == [(p.y, p.key, p.data) for p in pc], f"frame {t}"
