@@ -194,6 +194,11 @@ class Controller {
    public:
     void init(const EncoderConfig& cfg, const Geometry& g);
     void request_keyframe();
+    // Rate control: QP for changed stripes / paint-over from the next frame on.
+    void set_qp(int qp, int paint_qp) {
+        if (qp > 0) cfg_.qp = qp;
+        if (paint_qp > 0) cfg_.paint_qp = paint_qp;
+    }
     // dirty[s] = stripe s changed since last frame. Fills tasks[num_slices].
     void plan(const uint8_t* dirty, SliceTask* tasks);
     // After the backend ran: update frame_num / idr state from final actions.

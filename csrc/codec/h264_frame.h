@@ -26,6 +26,7 @@ class CpuH264Encoder {
    public:
     explicit CpuH264Encoder(const EncoderConfig& cfg);
     void request_keyframe() { ctl_.request_keyframe(); }
+    void set_qp(int qp, int paint_qp) { ctl_.set_qp(qp, paint_qp); }
     // Full pipeline for one captured frame.
     void encode(const uint8_t* bgrx, int stride_bytes, uint16_t frame_id,
                 std::vector<EncodedPacket>& out);

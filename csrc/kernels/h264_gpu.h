@@ -28,7 +28,7 @@ struct FrameArgs {
     int* stripe_dirty;     // [num_slices] set by k_convert_damage, consumed (and cleared) by k_plan
     StripeState* plan_state;    // [num_slices + 1] controller state (last = picture state)
     int* plan_ctl;              // [0] keyframe requests seen, [1] frames planned (0 = first frame)
-    const int* key_seq_host;    // host-mapped keyframe request counter
+    const int* key_seq_host;    // host-mapped: [0] keyframe request counter, [1] qp, [2] paint qp (0 = config)
     PlanConfig plan_cfg;
     SliceTask* tasks;      // [num_slices]
     MeResult* me;          // [num_mbs]

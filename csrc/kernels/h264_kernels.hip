@@ -413,9 +413,14 @@ __global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
         if (tid == 0) pic.need_idr = true;
     }
     __syncthreads();
+    PlanConfig pc = a.plan_cfg;  // rate-control overrides from the host
+    const int qo = __hip_atomic_load(a.key_seq_host + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int po = __hip_atomic_load(a.key_seq_host + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (qo > 0) pc.qp = qo;
+    if (po > 0) pc.paint_qp = po;
     for (int s = tid; s < ns; s += 256) {
         const int r0 = s * a.rows_per_slice, nr = min(a.rows_per_slice, a.mb_h - r0);
-        plan_stripe(a.plan_cfg, st[s], pic, a.stripe_dirty[s] != 0, r0, nr, a.mb_h, a.tasks[s]);
+        plan_stripe(pc, st[s], pic, a.stripe_dirty[s] != 0, r0, nr, a.mb_h, a.tasks[s]);
         a.stripe_dirty[s] = 0;
     }
     __syncthreads();

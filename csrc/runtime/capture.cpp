@@ -47,6 +47,7 @@ class CaptureSession {
             }
         }
         if (!src_) src_ = make_synthetic_source(w, h, s.source >= 1 ? s.source - 1 : 0, 0x1234567u);
+        src_kind_ = strcmp(src_->name(), "x11-shm") == 0 ? 1.0 : 0.0;
         // encoder
         try {
             int backend = s.use_cpu ? 0 : (sk_hip_device_count() > 0 ? 1 : 0);
@@ -94,6 +95,7 @@ class CaptureSession {
     }
 
     void request_keyframe() { key_req_ = true; }
+    void set_qp(int qp, int paint_qp) { qp_req_ = (qp & 0xffff) | (paint_qp & 0xffff) << 16; }
 
     // Premultiplied BGRA watermark, composited onto every captured frame before
     // encoding. location: 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right,
@@ -110,7 +112,7 @@ class CaptureSession {
     void stats(double* out, int n) {
         std::lock_guard<std::mutex> g(mu_);
         double v[6] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
-                       (double)packets_, src_ ? (strcmp(src_->name(), "x11-shm") == 0 ? 1.0 : 0.0) : -1.0,
+                       (double)packets_, src_kind_,
                        last_enc_ms_};
         for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
     }
@@ -124,6 +126,7 @@ class CaptureSession {
         uint16_t frame_id = 0;
         while (running_) {
             if (key_req_.exchange(false)) enc_->request_keyframe();
+            if (int q = qp_req_.exchange(0)) enc_->set_qp(q & 0xffff, q >> 16);
             int stride = 0;
             const uint8_t* px = src_->grab(&stride);
             if (px && wm_loc_ >= 0 && !wm_.empty()) composite_watermark(const_cast<uint8_t*>(px), stride, frame_id);
@@ -216,6 +219,8 @@ class CaptureSession {
     std::unique_ptr<EncoderBackend> enc_;
     std::thread th_;
     std::atomic<bool> running_{false}, key_req_{false};
+    std::atomic<int> qp_req_{0};
+    double src_kind_ = -1.0;  // 1 x11, 0 synthetic, -1 none (kept after stop for stats)
     std::mutex mu_;
     uint64_t frames_ = 0, bytes_ = 0, packets_ = 0;
     double enc_ms_sum_ = 0, last_enc_ms_ = 0;
@@ -233,6 +238,7 @@ int sk_capture_start(void* c, const sk_capture_settings* s, sk_stripe_cb cb, voi
 }
 void sk_capture_stop(void* c) { static_cast<CaptureSession*>(c)->stop(); }
 void sk_capture_request_keyframe(void* c) { static_cast<CaptureSession*>(c)->request_keyframe(); }
+void sk_capture_set_qp(void* c, int qp, int paint_qp) { static_cast<CaptureSession*>(c)->set_qp(qp, paint_qp); }
 void sk_capture_stats(void* c, double* out, int n) { static_cast<CaptureSession*>(c)->stats(out, n); }
 void sk_capture_set_watermark(void* c, const uint8_t* bgra, int w, int h, int location) {
     static_cast<CaptureSession*>(c)->set_watermark(bgra, w, h, location);

@@ -14,6 +14,8 @@ class EncoderBackend {
     virtual int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) = 0;
     virtual int64_t debug_buffer(const char* name, void* dst, int64_t cap) = 0;
     virtual int stage_times(float* dst, int n) { (void)dst; (void)n; return 0; }
+    // H.264 rate control hook (QP <= 0 keeps the current value); JPEG ignores it.
+    virtual void set_qp(int qp, int paint_qp) { (void)qp; (void)paint_qp; }
     std::vector<h264::EncodedPacket> packets_;
 };
 

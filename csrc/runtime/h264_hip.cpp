@@ -47,6 +47,11 @@ class HipBackend : public EncoderBackend {
 
     // Picked up by k_plan at the start of the next frame.
     void request_keyframe() override { __atomic_fetch_add(h_key_seq_, 1, __ATOMIC_SEQ_CST); }
+    // Host-mapped overrides, read by k_plan at the start of the next frame.
+    void set_qp(int qp, int paint_qp) override {
+        if (qp > 0) __atomic_store_n(&h_key_seq_[1], qp, __ATOMIC_SEQ_CST);
+        if (paint_qp > 0) __atomic_store_n(&h_key_seq_[2], paint_qp, __ATOMIC_SEQ_CST);
+    }
 
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         HIPCHECK(hipSetDevice(device_));

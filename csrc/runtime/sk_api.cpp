@@ -19,6 +19,7 @@ class CpuBackend : public EncoderBackend {
    public:
     explicit CpuBackend(const h264::EncoderConfig& c) : enc_(c) {}
     void request_keyframe() override { enc_.request_keyframe(); }
+    void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         packets_.clear();
         enc_.encode(bgrx, stride, frame_id, packets_);
@@ -168,6 +169,7 @@ void* sk_jpeg_create(const sk_jpeg_config* c) {
 
 void sk_h264_destroy(void* enc) { delete static_cast<EncoderBackend*>(enc); }
 void sk_h264_request_keyframe(void* enc) { static_cast<EncoderBackend*>(enc)->request_keyframe(); }
+void sk_h264_set_qp(void* enc, int qp, int paint_qp) { static_cast<EncoderBackend*>(enc)->set_qp(qp, paint_qp); }
 
 int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id) {
     try {

@@ -29,6 +29,8 @@ int sk_hip_device_count(void);
 void* sk_h264_create(const sk_h264_config* cfg);
 void sk_h264_destroy(void* enc);
 void sk_h264_request_keyframe(void* enc);
+// Rate control: QP of changed stripes / paint-over from the next frame (<= 0 keeps the value).
+void sk_h264_set_qp(void* enc, int qp, int paint_qp);
 // Encodes one BGRx frame; returns the number of packets (or < 0 on error).
 int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride_bytes, int32_t frame_id);
 int sk_h264_get_packet(void* enc, int32_t i, sk_packet* out);
@@ -86,6 +88,7 @@ void sk_capture_destroy(void* c);
 int sk_capture_start(void* c, const sk_capture_settings* s, sk_stripe_cb cb, void* user);
 void sk_capture_stop(void* c);
 void sk_capture_request_keyframe(void* c);
+void sk_capture_set_qp(void* c, int qp, int paint_qp);
 // frames, mean encode ms, bytes, packets, source (1 = X11, 0 = synthetic), last encode ms
 void sk_capture_stats(void* c, double* out, int n);
 // Premultiplied BGRA watermark composited before encoding (location enum in capture.cpp).

@@ -105,6 +105,11 @@ class ScreenCapture:
         if self._h:
             self._lib.sk_capture_request_keyframe(self._h)
 
+    def set_qp(self, qp: int, paint_qp: int = 0) -> None:
+        """H.264 rate control from the next frame on (the WebRTC mode's bitrate controller)."""
+        if self._h:
+            self._lib.sk_capture_set_qp(self._h, int(qp), int(paint_qp))
+
     def stats(self) -> dict:
         arr = (ctypes.c_double * 6)()
         self._lib.sk_capture_stats(self._h, arr, 6)

@@ -28,8 +28,12 @@ CXXFLAGS = [
 ] + (["-DSK_STAMPS"] if os.environ.get("SK_STAMPS_BUILD") else [])
 
 
+RTC_LIB = LIBDIR / "libselkies_rtc.so"
+
+
 def _sources():
-    return sorted([p for p in CSRC.rglob("*") if p.suffix in (".cpp", ".hip")])
+    # csrc/rtc is host-only (OpenSSL) and goes into its own library, see build_rtc()
+    return sorted([p for p in CSRC.rglob("*") if p.suffix in (".cpp", ".hip") and "rtc" not in p.parts])
 
 
 def _headers_mtime() -> float:
@@ -71,5 +75,23 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
     return LIB
 
 
+def build_rtc(verbose: bool = False) -> Path:
+    """WebRTC transport core (DTLS-SRTP, SRTP, RTP packetisation): plain C++ on OpenSSL."""
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    srcs = sorted((CSRC / "rtc").glob("*.cpp"))
+    newest = max(p.stat().st_mtime for p in [*srcs, *(CSRC / "rtc").glob("*.h")])
+    if RTC_LIB.exists() and RTC_LIB.stat().st_mtime >= newest:
+        return RTC_LIB
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-Wno-deprecated-declarations", *map(str, srcs), "-o", str(RTC_LIB), "-lssl", "-lcrypto"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"rtc build failed\n{r.stdout}\n{r.stderr}")
+    return RTC_LIB
+
+
 if __name__ == "__main__":
     print(build(verbose="-v" in sys.argv))
+    print(build_rtc(verbose="-v" in sys.argv))

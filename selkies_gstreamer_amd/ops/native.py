@@ -90,6 +90,7 @@ def lib():
         L.sk_h264_create.argtypes = [ctypes.POINTER(SkH264Config)]
         L.sk_h264_destroy.argtypes = [ctypes.c_void_p]
         L.sk_h264_request_keyframe.argtypes = [ctypes.c_void_p]
+        L.sk_h264_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.sk_h264_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_encode.restype = ctypes.c_int
         L.sk_h264_get_packet.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(SkPacket)]
@@ -109,6 +110,7 @@ def lib():
         L.sk_capture_start.restype = ctypes.c_int
         L.sk_capture_stop.argtypes = [ctypes.c_void_p]
         L.sk_capture_request_keyframe.argtypes = [ctypes.c_void_p]
+        L.sk_capture_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.sk_capture_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.sk_capture_set_watermark.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int]
@@ -207,6 +209,10 @@ class H264Encoder:
 
     def request_keyframe(self):
         lib().sk_h264_request_keyframe(self._h)
+
+    def set_qp(self, qp: int, paint_qp: int = 0):
+        """Rate control: QP for changed / paint-over stripes from the next frame (<= 0 keeps)."""
+        lib().sk_h264_set_qp(self._h, int(qp), int(paint_qp))
 
     def encode(self, bgrx: np.ndarray, frame_id: int = 0) -> list[Packet]:
         """bgrx: uint8 array (H, W, 4) or (H, stride) rows. Returns 0x04 stripe packets."""

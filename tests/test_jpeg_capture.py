@@ -100,8 +100,8 @@ def _collect(settings, seconds=0.6):
     cap = pixelflux.ScreenCapture()
     cap.start_capture(settings, pixelflux.StripeCallback(cb))
     time.sleep(seconds)
-    st = cap.stats()
     cap.stop_capture()
+    st = cap.stats()  # after stop: no callback can race the counters
     cap.close()
     return got, st
 
