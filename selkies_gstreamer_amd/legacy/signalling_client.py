@@ -22,7 +22,7 @@ class SignallingError(Exception):
 
 class SignallingClient:
     def __init__(self, server: str, peer_id: int | str, meta: Optional[dict] = None, *,
-                 basic_auth: Optional[tuple] = None, ssl=None):
+                 basic_auth: Optional[tuple] = None, ssl=True):
         self.server, self.id, self.meta = server, str(peer_id), meta
         self.auth = aiohttp.BasicAuth(*basic_auth) if basic_auth else None
         self.ssl = ssl

@@ -62,3 +62,62 @@ assert.equal(pcm.length, 240);
 assert.equal(pcm[0], Math.trunc(0.5 * 0x7fff));
 assert.equal(downsampleToS16Mono([a, b], 48000)[10], 0);
 console.log('client tests ok');
+
+// ---- WebRTC mode (lib/webrtc.js) with fake WebSocket / RTCPeerConnection ----
+import { Signalling, WebRTCClient, parseServerMessage } from '../../selkies_gstreamer_amd/web/lib/webrtc.js';
+
+class FakeWS {
+  constructor(url) { this.url = url; this.sent = []; FakeWS.last = this; }
+  send(m) { this.sent.push(m); }
+}
+class FakeChannel {
+  constructor() { this.readyState = 'open'; this.sent = []; }
+  send(m) { this.sent.push(m); }
+  close() { this.readyState = 'closed'; }
+}
+class FakePC {
+  constructor(cfg) { this.cfg = cfg; this.remote = null; this.candidates = []; FakePC.last = this; }
+  async setRemoteDescription(d) { this.remote = d; }
+  async createAnswer() { return { type: 'answer', sdp: 'v=0 answer' }; }
+  async setLocalDescription(d) { this.localDescription = d; }
+  async addIceCandidate(c) { this.candidates.push(c); }
+  close() { this.closed = true; }
+}
+
+(async () => {
+  const sig = new Signalling('ws://h/ws', 1, FakeWS);
+  sig.connect({ res: '1x1' });
+  FakeWS.last.onopen();
+  assert.ok(FakeWS.last.sent[0].startsWith('HELLO 1 '));
+  const statuses = [];
+  sig.onstatus = (s) => statuses.push(s);
+  sig.handle('HELLO');
+  sig.handle('SESSION_OK');
+  assert.equal(statuses.length, 2);
+  let err = null;
+  sig.onerror = (e) => { err = e; };
+  sig.handle("ERROR peer '1' not found");
+  assert.ok(err && err.message.startsWith('ERROR'));
+
+  const client = new WebRTCClient(null, sig, { iceServers: [] }, FakePC);
+  await client.onSdp({ type: 'offer', sdp: 'v=0 offer' });
+  assert.equal(FakePC.last.remote.sdp, 'v=0 offer');
+  assert.deepEqual(JSON.parse(FakeWS.last.sent[FakeWS.last.sent.length - 1]), { sdp: { type: 'answer', sdp: 'v=0 answer' } });
+  sig.handle(JSON.stringify({ ice: { candidate: 'candidate:1 1 udp 1 10.0.0.1 9 typ host', sdpMLineIndex: 0 } }));
+  await new Promise((r) => setTimeout(r, 0));
+  assert.equal(FakePC.last.candidates.length, 1);
+
+  const ch = new FakeChannel();
+  client.bindChannel(ch);
+  ch.onmessage({ data: JSON.stringify({ type: 'system', data: { action: 'framerate,60' } }) });
+  ch.onmessage({ data: JSON.stringify({ type: 'system', data: { action: 'resolution,1920x1080' } }) });
+  ch.onmessage({ data: JSON.stringify({ type: 'ping', data: { start_time: 12.5 } }) });
+  assert.equal(client.state.framerate, 60);
+  assert.equal(client.state.resolution, '1920x1080');
+  assert.equal(ch.sent[0], 'pong,12.5');
+  client.setVideoBitrate(2500.7);
+  client.requestResolution(1921, 1081);
+  assert.deepEqual(ch.sent.slice(1), ['vb,2500', 'r,1920x1080']);
+  assert.equal(parseServerMessage('nope'), null);
+  assert.deepEqual(parseServerMessage('{"type":"system","data":{"action":"reload"}}').action, ['reload', '']);
+})().then(() => console.log('webrtc client ok'), (e) => { console.error(e); process.exit(1); });

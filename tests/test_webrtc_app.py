@@ -1,0 +1,94 @@
+"""Legacy WebRTC mode end to end on CPU: signalling server + streaming peer
+(synthetic capture, CPU H.264 in full-frame mode) <-> a viewer peer built from
+our own PeerConnection acting as the browser. Checks the signalling call
+flow (HELLO / SESSION / SDP relay), DTLS-SRTP media (decodable IDR), the
+"input" data channel in both directions and runtime bitrate / fps control."""
+import asyncio
+import json
+
+from selkies_gstreamer_amd.legacy import webrtc_app
+from selkies_gstreamer_amd.legacy.signalling_client import SignallingClient
+from selkies_gstreamer_amd.models.h264.decoder import H264Decoder
+from selkies_gstreamer_amd.webrtc.peer import PeerConnection
+
+
+class _RecordingInput:
+    def __init__(self):
+        self.msgs = []
+
+    async def on_message(self, msg):
+        self.msgs.append(msg)
+
+    async def close(self):
+        pass
+
+
+def test_legacy_webrtc_session(tmp_path):
+    args = webrtc_app.parse_args(
+        ["--port", "0", "--enable_basic_auth", "false", "--use_cpu", "true", "--capture_source", "synthetic",
+         "--json_config", str(tmp_path / "cfg.json"), "--rtc_config_json", str(tmp_path / "none.json"),
+         "--framerate", "20", "--initial_resolution", "256x128", "--turn_shared_secret", ""], env={})
+    rec = _RecordingInput()
+
+    async def factory(session):
+        return rec
+
+    async def main():
+        stop = asyncio.Event()
+        srv = asyncio.ensure_future(webrtc_app.serve(args, factory, addresses=["127.0.0.1"], stop=stop))
+        for _ in range(100):
+            if args.port != "0":
+                break
+            await asyncio.sleep(0.05)
+        viewer = PeerConnection(addresses=["127.0.0.1"])
+        frames, msgs, chans = [], [], []
+        viewer.on_video_frame = lambda au, ts: frames.append(au)
+
+        def on_channel(ch):
+            chans.append(ch)
+            ch.on_message = msgs.append
+        viewer.on_datachannel = on_channel
+        sig = SignallingClient(f"ws://127.0.0.1:{args.port}/ws", 1)
+        answered = asyncio.Event()
+
+        async def on_offer(kind, text):
+            await viewer.set_remote_description(text, kind)
+            await sig.send_sdp("answer", await viewer.create_answer())
+            answered.set()
+            await viewer.connect(15)
+        sig.on_sdp = lambda kind, text: asyncio.ensure_future(on_offer(kind, text))
+        await sig.connect()
+        reader = asyncio.ensure_future(sig.start())
+        await asyncio.wait_for(answered.wait(), 20)
+        for _ in range(200):
+            if len(frames) >= 5 and chans and msgs:
+                break
+            await asyncio.sleep(0.05)
+        assert len(frames) >= 5, "no video over SRTP"
+        dec = H264Decoder()
+        out = []
+        for au in frames[:3]:
+            out += dec.decode(au)
+        assert out and out[0][0].shape == (128, 256) and dec.stats["idr"] >= 1
+        sysmsgs = [json.loads(m) for m in msgs]
+        assert {"type": "system", "data": {"action": "framerate,20"}} in sysmsgs
+        ch = chans[0]
+        assert ch.label == "input"
+        ch.send("kd,65")
+        ch.send("vb,2500")
+        ch.send("_arg_fps,30")
+        for _ in range(100):
+            if rec.msgs and any("Video bitrate set to: 2500" in m for m in msgs):
+                break
+            await asyncio.sleep(0.05)
+        assert rec.msgs == ["kd,65"]
+        assert any("Video bitrate set to: 2500" in m for m in msgs)
+        saved = json.loads((tmp_path / "cfg.json").read_text())
+        assert saved["video_bitrate"] == "2500" and saved["framerate"] == "30"
+        await viewer.close()
+        reader.cancel()
+        await sig.stop()
+        stop.set()
+        await asyncio.wait_for(srv, 15)
+
+    asyncio.run(asyncio.wait_for(main(), 90))
