@@ -191,3 +191,27 @@ class RTCConfigMonitor:
     def stop(self):
         if self.task:
             self.task.cancel()
+
+
+def main(argv=None) -> int:
+    """TURN REST micro-service (reference addons/turn-rest): ``python -m
+    selkies_gstreamer_amd.server.turn --port 8008``; configured by TURN_* env."""
+    import argparse
+    from aiohttp import web
+    ap = argparse.ArgumentParser(description="TURN REST API (HMAC-SHA1 time-limited credentials)")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=int(os.environ.get("PORT", "8008")))
+    a = ap.parse_args(argv)
+    app = web.Application()
+    defaults = env_turn_defaults()
+
+    async def handle(request):
+        return await turn_rest_handler(request, defaults)
+    app.router.add_route("GET", "/", handle)
+    app.router.add_route("POST", "/", handle)
+    web.run_app(app, host=a.host, port=a.port)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

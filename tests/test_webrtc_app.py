@@ -6,6 +6,8 @@ flow (HELLO / SESSION / SDP relay), DTLS-SRTP media (decodable IDR), the
 import asyncio
 import json
 
+import pytest
+
 from selkies_gstreamer_amd.legacy import webrtc_app
 from selkies_gstreamer_amd.legacy.signalling_client import SignallingClient
 from selkies_gstreamer_amd.models.h264.decoder import H264Decoder
@@ -23,11 +25,15 @@ class _RecordingInput:
         pass
 
 
-def test_legacy_webrtc_session(tmp_path):
+@pytest.mark.parametrize("backend", ["cpu", pytest.param("hip", marks=pytest.mark.gpu)])
+def test_legacy_webrtc_session(tmp_path, backend):
+    """backend=hip runs the same session on the MI355X encoder (native HIP path, 640x368)."""
+    W, H = (256, 128) if backend == "cpu" else (640, 368)
     args = webrtc_app.parse_args(
-        ["--port", "0", "--enable_basic_auth", "false", "--use_cpu", "true", "--capture_source", "synthetic",
-         "--json_config", str(tmp_path / "cfg.json"), "--rtc_config_json", str(tmp_path / "none.json"),
-         "--framerate", "20", "--initial_resolution", "256x128", "--turn_shared_secret", ""], env={})
+        ["--port", "0", "--enable_basic_auth", "false", "--use_cpu", str(backend == "cpu").lower(),
+         "--capture_source", "synthetic", "--json_config", str(tmp_path / "cfg.json"),
+         "--rtc_config_json", str(tmp_path / "none.json"), "--framerate", "20",
+         "--initial_resolution", f"{W}x{H}", "--turn_shared_secret", ""], env={})
     rec = _RecordingInput()
 
     async def factory(session):
@@ -69,7 +75,7 @@ def test_legacy_webrtc_session(tmp_path):
         out = []
         for au in frames[:3]:
             out += dec.decode(au)
-        assert out and out[0][0].shape == (128, 256) and dec.stats["idr"] >= 1
+        assert out and out[0][0].shape == (H, W) and dec.stats["idr"] >= 1
         sysmsgs = [json.loads(m) for m in msgs]
         assert {"type": "system", "data": {"action": "framerate,20"}} in sysmsgs
         ch = chans[0]
