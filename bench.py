@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--encoder", default="h264", choices=["h264", "jpeg"],
                    help="h264 (headline, x264enc-striped equivalent) or jpeg stripes")
     p.add_argument("--jpeg-quality", type=int, default=40)
+    p.add_argument("--deblock", type=int, default=0,
+                   help="H.264 in-loop deblocking filter (1 on; default off like the reference's x264 ultrafast preset)")
+    p.add_argument("--me-full", type=int, default=1, help="H.264 MFMA +-16 exhaustive search candidate (1 on, 0 off)")
     p.add_argument("--gather", action="store_true", help="gather all packets to rank 0 over RCCL each step")
     return p.parse_args()
 
@@ -85,7 +88,8 @@ def main():
                             device=local_rank, backend=args.backend) for _ in range(S)]
     else:
         encs = [H264Encoder(W, H, stripe_height=args.stripe_height, fullframe=args.mode == "fullframe",
-                            qp=args.qp, use_paint_over=False, device=local_rank, backend=args.backend)
+                            qp=args.qp, use_paint_over=False, device=local_rank, backend=args.backend,
+                            deblock=bool(args.deblock), me_full=bool(args.me_full))
                 for _ in range(S)]
 
     lat = [[] for _ in range(S)]
@@ -179,6 +183,8 @@ def main():
                 "parallelism": f"session-parallel dp{n_gpus} x {S} sessions/GPU",
                 "resolution": f"{W}x{H}",
                 "backend": args.backend,
+                "deblock": bool(args.deblock) if args.encoder == "h264" else None,
+                "me_full": bool(args.me_full) if args.encoder == "h264" else None,
             },
         }
         print(json.dumps(res), flush=True)

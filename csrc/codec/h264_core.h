@@ -42,6 +42,18 @@ struct MbInfo {
 };
 static_assert(sizeof(MbInfo) == 40, "MbInfo layout");
 
+// K4a exhaustive integer search (MFMA on the GPU): candidates dx, dy in
+// [-kFsR, kFsR), reference window (2*kFsR + 16)^2 clamped like every ME read.
+// Candidates are ranked by the SSD proxy |r_d|^2 - 2<s, r_d> (|s|^2 is common to
+// all of them) on 128-offset samples, ties to the lower raster index (dy, dx).
+constexpr int kFsR = 16;
+constexpr int kFsWin = 2 * kFsR + 16;
+SK_HD uint64_t fs_key(int cost, int dyw, int dxw) {
+    return ((uint64_t)(uint32_t)(cost + (1 << 24)) << 10) | (uint64_t)(dyw * (2 * kFsR) + dxw);
+}
+SK_HD int fs_key_dx(uint64_t k) { return (int)(k & (2 * kFsR - 1)) - kFsR; }
+SK_HD int fs_key_dy(uint64_t k) { return (int)((k >> 5) & (2 * kFsR - 1)) - kFsR; }
+
 // ---------------------------------------------------------------------------
 // Bit writers. `put` appends the `len` low bits of `code`, MSB first.
 struct BitCounter {

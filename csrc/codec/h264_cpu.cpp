@@ -4,6 +4,7 @@
 // csrc/kernels/h264_kernels.hip that must produce bit-identical buffers.
 #include "h264_frame.h"
 #include "color.h"
+#include "h264_deblock.h"
 #include <string.h>
 #include <algorithm>
 
@@ -27,6 +28,8 @@ CpuH264Encoder::CpuH264Encoder(const EncoderConfig& c) : cfg(c) {
     coefs.assign((size_t)g.num_mbs() * kCoefPerMb, 0);
     me.assign(g.num_mbs(), MeResult());
     mvfield.assign((size_t)g.num_mbs() * 2, 0);
+    dbinfo.assign(g.num_mbs(), DbInfo());
+    fs_mv.assign((size_t)g.num_mbs() * 2, 0);
     tasks.assign(g.num_slices, SliceTask());
     if (cfg.fullframe) {
         param_sets.resize(1);
@@ -92,6 +95,35 @@ int CpuH264Encoder::sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t)
     return sad;
 }
 
+// K4a reference: exhaustive +-16 search ranked by fs_key (k_me_mfma computes the
+// same integers with int8 MFMA cross-correlations).
+void CpuH264Encoder::full_search(int mbx, int mby, const SliceTask& t, int16_t* out) const {
+    const int y_lo = t.pic_row0 * 16, y_hi = (t.pic_row0 + t.pic_rows) * 16 - 1, x_hi = g.stride_y - 1;
+    static thread_local int win[kFsWin][kFsWin];
+    int sb[16][16];
+    for (int wy = 0; wy < kFsWin; wy++) {
+        const uint8_t* row = &ref[0][(size_t)sk_clip(mby * 16 - kFsR + wy, y_lo, y_hi) * g.stride_y];
+        for (int wx = 0; wx < kFsWin; wx++) win[wy][wx] = (int)row[sk_clip(mbx * 16 - kFsR + wx, 0, x_hi)] - 128;
+    }
+    for (int y = 0; y < 16; y++)
+        for (int x = 0; x < 16; x++) sb[y][x] = (int)src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x] - 128;
+    uint64_t best = ~0ull;
+    for (int dyw = 0; dyw < 2 * kFsR; dyw++)
+        for (int dxw = 0; dxw < 2 * kFsR; dxw++) {
+            int ssq = 0, cross = 0;
+            for (int y = 0; y < 16; y++) {
+                const int* w = &win[dyw + y][dxw];
+                for (int x = 0; x < 16; x++) {
+                    ssq += w[x] * w[x];
+                    cross += sb[y][x] * w[x];
+                }
+            }
+            best = std::min(best, fs_key(ssq - 2 * cross, dyw, dxw));
+        }
+    out[0] = (int16_t)fs_key_dx(best);
+    out[1] = (int16_t)fs_key_dy(best);
+}
+
 void CpuH264Encoder::motion_search(int s) {
     const SliceTask& t = tasks[s];
     const int lam = lambda_for_qp(t.qp);
@@ -104,7 +136,7 @@ void CpuH264Encoder::motion_search(int s) {
     for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
         for (int mbx = 0; mbx < g.mb_w; mbx++) {
             int idx = mby * g.mb_w + mbx;
-            int cx[6], cy[6], n = 0;
+            int cx[7], cy[7], n = 0;
             cx[n] = 0; cy[n] = 0; n++;
             auto add = [&](int ox, int oy) {
                 int j = oy * g.mb_w + ox;
@@ -117,6 +149,12 @@ void CpuH264Encoder::motion_search(int s) {
             if (mbx + 1 < g.mb_w) add(mbx + 1, mby);
             if (mby - 1 >= t.pic_row0) add(mbx, mby - 1);
             if (mby + 1 < t.pic_row0 + t.pic_rows) add(mbx, mby + 1);
+            if (cfg.me_full && mb_dirty[idx]) {
+                full_search(mbx, mby, t, &fs_mv[2 * idx]);
+                cx[n] = sk_clip(fs_mv[2 * idx], -R, R);
+                cy[n] = sk_clip(fs_mv[2 * idx + 1], -R, R);
+                n++;
+            }
             int bx = 0, by = 0, bsad = 0;
             int bcost = cost_of(mbx, mby, 0, 0, &bsad);
             for (int i = 1; i < n; i++) {
@@ -377,6 +415,7 @@ std::vector<uint8_t> CpuH264Encoder::write_slice(int s) {
     h.frame_num = h.idr ? 0 : t.frame_num;
     h.idr_pic_id = t.idr_pic_id;
     h.slice_qp = t.qp;
+    h.deblock = cfg.deblock;
     write_slice_header(w, h);
     if (t.final_action == ACT_SKIPALL) {
         put_ue(w, (uint32_t)nmb);
@@ -451,6 +490,11 @@ void CpuH264Encoder::finish_frame() {
         for (int p = 1; p < 3; p++)
             memcpy(&ref[p][(size_t)(y0 / 2) * g.stride_c], &rec[p][(size_t)(y0 / 2) * g.stride_c],
                    (size_t)(y1 - y0) / 2 * g.stride_c);
+        if (cfg.deblock) {  // K7: the reference picture is the deblocked reconstruction
+            db_slice_info(mbs.data(), g.mb_w, t.first_row, t.num_rows, t.qp, dbinfo.data());
+            deblock_slice_cpu(ref[0].data(), ref[1].data(), ref[2].data(), g.stride_y, g.stride_c, dbinfo.data(),
+                              g.mb_w, t.first_row, t.num_rows);
+        }
         for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
             for (int mbx = 0; mbx < g.mb_w; mbx++) {
                 int j = mby * g.mb_w + mbx;

@@ -36,6 +36,8 @@ struct EncoderConfig {
     int me_iters = 24;           // diamond refinement iterations
     int scenecut = 1;
     float fps = 60.f;
+    int deblock = 0;             // in-loop deblocking filter (idc 2: inside each slice); off = x264 ultrafast
+    int me_full = 1;             // +-16 exhaustive MFMA search candidate (dirty MBs of P slices)
 };
 
 struct Geometry {

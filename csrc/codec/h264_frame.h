@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include "h264_encoder.h"
 #include "h264_mb.h"
+#include "h264_deblock.h"
 
 namespace sk {
 namespace h264 {
@@ -52,6 +53,8 @@ class CpuH264Encoder {
     std::vector<int16_t> coefs;
     std::vector<MeResult> me;
     std::vector<int16_t> mvfield;  // previous integer mv per MB (x, y)
+    std::vector<DbInfo> dbinfo;    // deblocking side info of the current frame
+    std::vector<int16_t> fs_mv;    // K4a full-search winner per MB (x, y), dirty MBs of P slices
     std::vector<SliceTask> tasks;
     std::vector<std::vector<uint8_t>> param_sets;  // per stripe (striped) or [0] (full frame)
     bool first_frame = true;
@@ -62,6 +65,7 @@ class CpuH264Encoder {
     void mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pu,
                    uint8_t* pv) const;
     int sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t) const;
+    void full_search(int mbx, int mby, const SliceTask& t, int16_t* out) const;
 };
 
 }  // namespace h264

@@ -16,6 +16,7 @@ struct SliceHeaderParams {
     int frame_num;
     int idr_pic_id;
     int slice_qp;
+    int deblock;      // 1: filter inside the slice (idc 2), 0: filter off (idc 1)
 };
 
 template <class W>
@@ -38,7 +39,13 @@ SK_HD void write_slice_header(W& w, const SliceHeaderParams& h) {
         w.put(0, 1);  // adaptive_ref_pic_marking_mode_flag
     }
     put_se(w, h.slice_qp - 26);
-    put_ue(w, 1);     // disable_deblocking_filter_idc = 1 (filter off)
+    if (h.deblock) {
+        put_ue(w, 2);  // disable_deblocking_filter_idc = 2: no filtering across slice edges
+        put_se(w, 0);  // slice_alpha_c0_offset_div2
+        put_se(w, 0);  // slice_beta_offset_div2
+    } else {
+        put_ue(w, 1);  // disable_deblocking_filter_idc = 1 (filter off)
+    }
 }
 
 // Neighbour context of one macroblock for nC prediction.

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include "../codec/h264_encoder.h"
 #include "../codec/h264_frame.h"
+#include "../codec/h264_deblock.h"
 
 namespace sk {
 namespace h264 {
@@ -55,11 +56,16 @@ struct FrameArgs {
     SliceTask* tasks_host;           // host-mapped: final slice decisions (written by k_decide)
     unsigned long long* dbg;  // optional s_memtime stamps (SK_STAMPS=1), else nullptr
     const CavlcTables* cavlc_tabs;  // precomputed CAVLC tables (device memory), copied to LDS per WG
+    int deblock;           // K7 on: ref = deblocked rec (k_deblock), else k_commit copies rec
+    int me_full;           // K4a on: MFMA exhaustive-search candidate per dirty MB
+    DbInfo* db;            // [num_mbs] deblocking side info (k_deblock_prep)
+    uint4* dbe;            // [num_mbs][3] per-MB edge record: bS nibbles, packed filter params (k_deblock_edges)
+    int16_t* fs_mv;        // [num_mbs][2] MFMA full-search winner (integer pel)
 };
 
 void launch_convert_damage(const FrameArgs& a, hipStream_t s);
 void launch_encode(const FrameArgs& a, hipStream_t s);   // k_plan and everything after it
-void launch_commit(const FrameArgs& a, hipStream_t s);
+void launch_commit(const FrameArgs& a, hipStream_t s);   // MV field + reference update (+ K7 deblocking)
 
 }  // namespace gpu
 }  // namespace h264

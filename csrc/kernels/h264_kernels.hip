@@ -8,6 +8,7 @@
 //
 // Stages (all bit-exact with the CPU reference csrc/codec/h264_cpu.cpp):
 //   k_convert_damage  K1+K3  BGRx -> NV12-planar YUV 4:2:0 + per-MB damage bits
+//   k_me_mfma         K4a    exhaustive +-16 search: int8 MFMA cross-correlation (SSD)
 //   k_motion_search   K4     candidate + diamond integer search, v_sad_u8
 //   k_decide                 per-slice scene-cut decision
 //   k_code_inter      K6     MC, transform, quant/decimation, QP escalation, recon
@@ -17,7 +18,8 @@
 //   k_slice_scan, k_mb_concat, k_ep_*   K9  slice header + MB offsets, MB bit
 //                            concatenation, tile-parallel emulation prevention
 //                            straight into host-mapped packet slots
-//   k_commit                 reference / MV-field update
+//   k_commit                 MV-field update (+ plain reference copy when K7 is off)
+//   k_deblock_prep, k_deblock  K7  in-loop deblocking rec -> ref (LDS-ring wavefront)
 #include "h264_gpu.h"
 #include "../codec/color.h"
 #include "../codec/h264_mb.h"
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
     const int lam = lambda_for_qp(t.qp);
     const int R = a.me_range;
     // candidates (same order as the CPU reference)
-    int cx[6], cy[6], n = 0;
+    int cx[7], cy[7], n = 0;
     cx[0] = 0; cy[0] = 0; n = 1;
     auto add = [&](int ox, int oy) {
         int j = oy * a.mb_w + ox;
@@ -333,6 +335,11 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
     if (mbx + 1 < a.mb_w) add(mbx + 1, mby);
     if (mby - 1 >= t.pic_row0) add(mbx, mby - 1);
     if (mby + 1 < t.pic_row0 + t.pic_rows) add(mbx, mby + 1);
+    if (a.me_full && a.mb_dirty[idx]) {   // K4a winner (k_me_mfma)
+        cx[n] = sk_clip(a.fs_mv[2 * idx], -R, R);
+        cy[n] = sk_clip(a.fs_mv[2 * idx + 1], -R, R);
+        n++;
+    }
     int bx = 0, by = 0;
     int bsad = me_sad(a, a.ref.y, sw, mbx, mby, 0, 0, ylo, yhi);
     int bcost = bsad + lam * (sk_se_bits(0) + sk_se_bits(0));
@@ -383,6 +390,131 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
         r.sad = bsad;
         r.intra_est = dev;
         a.me[idx] = r;  // per-slice sums are reduced in k_decide (no same-line atomics)
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4a: exhaustive +-16 integer search on the matrix cores, one wave per dirty MB
+// of a P slice (csrc/codec/h264_core.h fs_key; CPU reference full_search).
+// With 128-offset samples s' (block) and w' (48x48 reference window),
+//   cost(dx,dy) = sum w'^2 - 2 sum s' w'   over the 16x16 block at (dx,dy),
+// and the cross term for all 32x32 candidates is one int8 GEMM:
+//   D[dxw][dyw] = sum_{r', c} W[r'][dxw + c] * S[(r', c)][dyw],  S[(r',c)][dyw] = s'[r' - dyw][c]
+// (zero outside the block): 2 (dx) x 2 (dy) tiles of v_mfma_i32_16x16x64_i8, K = 4
+// window rows x 16 columns per instruction, 8 of the 12 K steps per dy tile (the
+// others are all-zero in S) = 32 MFMAs per MB. A fragments are unaligned 16-byte
+// runs of a window row (5 LDS dwords + v_alignbyte), B fragments aligned block rows.
+// sum w'^2 per candidate comes from separable 16-tap box sums in LDS. The wave
+// min of fs_key gives the winner, which k_motion_search adds as a predictor.
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
+    constexpr int WW = kFsWin / 4;                       // window dwords per row (12)
+    __shared__ uint32_t win_s[4][kFsWin * WW];           // raw reference window per wave
+    __shared__ uint32_t blk_s[4][64];                    // raw 16x16 source block
+    __shared__ int sq_s[4][kFsWin * 2 * kFsR];           // row box sums of w'^2, then |r_d|^2
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const int nmb = a.mb_w * a.mb_h;
+    const int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + w;
+    if (idx >= nmb) return;
+    const int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    const SliceTask t = a.tasks[mby / a.rows_per_slice];
+    if (t.action != ACT_P || !a.mb_dirty[idx]) return;
+    uint32_t* win = win_s[w];
+    uint32_t* blk = blk_s[w];
+    int* sq = sq_s[w];
+    const int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    for (int i = l; i < kFsWin * WW; i += 64) {
+        const int wy = i / WW, q = i - wy * WW;
+        const int y = sk_clip(mby * 16 - kFsR + wy, ylo, yhi);
+        win[i] = load_ref4(a.ref.y + (size_t)y * a.stride_y, mbx * 16 - kFsR + 4 * q, a.stride_y);
+    }
+    blk[l] = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + (l >> 2)) * a.stride_y + mbx * 16 +
+                                                (l & 3) * 4);
+    wave_sync();
+    // |r_d|^2: 16-tap row box sums (lane = window row), then 16-tap column sums in place
+    if (l < kFsWin) {
+        const uint8_t* row = reinterpret_cast<const uint8_t*>(win + l * WW);
+        int acc = 0;
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+            const int v = (int)row[c] - 128;
+            acc += v * v;
+        }
+        sq[l * 2 * kFsR] = acc;
+        for (int x = 1; x < 2 * kFsR; x++) {
+            const int vo = (int)row[x - 1] - 128, vn = (int)row[x + 15] - 128;
+            acc += vn * vn - vo * vo;
+            sq[l * 2 * kFsR + x] = acc;
+        }
+    }
+    wave_sync();
+    if (l < 2 * kFsR) {
+        int acc = 0;
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc += sq[r * 2 * kFsR + l];
+        for (int dy = 0; dy < 2 * kFsR; dy++) {
+            const int old = sq[dy * 2 * kFsR + l], nw = sq[(dy + 16) * 2 * kFsR + l];
+            sq[dy * 2 * kFsR + l] = acc;
+            acc += nw - old;
+        }
+    }
+    // cross-correlation on MFMA: lane (i = l & 15, g = l >> 4)
+    const int i16 = l & 15, g = l >> 4;
+    v4i acc[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) acc[mt][nt] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < kFsWin / 4; ks++) {
+        const int rr = 4 * ks + g;                       // window row of this lane's K group
+        v4i bf[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            const int src = rr - (16 * nt + i16);        // block row feeding candidate row dyw
+            const bool in = src >= 0 && src < 16;
+#pragma unroll
+            for (int q = 0; q < 4; q++) bf[nt][q] = in ? (int)(blk[(in ? src : 0) * 4 + q] ^ 0x80808080u) : 0;
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++) {
+            const int b0 = 16 * mt + i16;                // first window column of candidate dxw
+            const uint32_t* wr = win + rr * WW + (b0 >> 2);
+            const int sh = b0 & 3;
+            uint32_t w5[5];
+#pragma unroll
+            for (int q = 0; q < 5; q++) w5[q] = wr[q];
+            v4i af;
+#pragma unroll
+            for (int q = 0; q < 4; q++) af[q] = (int)(__builtin_amdgcn_alignbyte(w5[q + 1], w5[q], sh) ^ 0x80808080u);
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++)
+                if (ks >= 4 * nt && ks <= 4 * nt + 7)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[nt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+    wave_sync();
+    // D[dxw = 16 mt + 4 g + reg][dyw = 16 nt + i16]
+    uint64_t best = ~0ull;
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int reg = 0; reg < 4; reg++) {
+                const int dxw = 16 * mt + 4 * g + reg, dyw = 16 * nt + i16;
+                const uint64_t k = fs_key(sq[dyw * 2 * kFsR + dxw] - 2 * acc[mt][nt][reg], dyw, dxw);
+                best = k < best ? k : best;
+            }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t other = __shfl_xor(best, o);
+        best = other < best ? other : best;
+    }
+    if (l == 0) {
+        a.fs_mv[2 * idx] = (int16_t)fs_key_dx(best);
+        a.fs_mv[2 * idx + 1] = (int16_t)fs_key_dy(best);
     }
 }
 
@@ -1270,6 +1402,7 @@ __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
         h.frame_num = idr ? 0 : task.frame_num;
         h.idr_pic_id = task.idr_pic_id;
         h.slice_qp = task.qp;
+        h.deblock = a.deblock;
         write_slice_header(w, h);
         if (fin == ACT_SKIPALL) put_ue(w, (uint32_t)nmb);
         sh_misc[0] = (int)w.pos;
@@ -1531,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_commit(FrameArgs a) {
         a.mvfield[2 * idx] = zero ? 0 : a.me[idx].mvx;
         a.mvfield[2 * idx + 1] = zero ? 0 : a.me[idx].mvy;
     }
-    if (fin == ACT_SKIPALL) return;  // reference unchanged
+    if (fin == ACT_SKIPALL || a.deblock) return;  // reference unchanged / written by k_deblock
     {   // luma: 16 rows x (nmbs * 16) bytes, one uint4 per thread
         const int row = tid >> 4, v = tid & 15;
         if (v < nmbs) {
@@ -1557,6 +1690,305 @@ __global__ __launch_bounds__(256) void k_commit(FrameArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// K7: in-loop deblocking (8.7; shared filter code in codec/h264_deblock.h).
+//   k_deblock_prep  one wave per MB: QP_Y chain (ballot scan back to the last MB
+//                   of the slice that carried mb_qp_delta) -> DbInfo
+//   k_deblock       one workgroup per coded slice, wave r filters MB row r, MB x at
+//                   step x + 2r + 1. The 2-MB lag covers every raster-order
+//                   dependency of 8.7 (left MB, top MB, and the top-right MB whose
+//                   left edge rewrites the top MB's right columns). Each band keeps
+//                   a 4-slot ring of its MBs in LDS: the next MB is prefetched from
+//                   rec while the current one is filtered, and an MB is written to
+//                   ref three steps after its own step, once the band below has
+//                   filtered its top edge. Lanes 0-15 own a luma row (vertical
+//                   edges) then a luma column (horizontal edges), lanes 16-31 the
+//                   same for Cb/Cr; the 4 (2) edges of a line run in registers.
+__global__ __launch_bounds__(256) void k_deblock_prep(FrameArgs a) {
+    const int nmb = a.mb_w * a.mb_h;
+    const int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    if (idx >= nmb) return;
+    const SliceTask t = a.tasks[(idx / a.mb_w) / a.rows_per_slice];
+    if (t.final_action != ACT_P && t.final_action != ACT_I) return;
+    const int l = lane_id(), first = t.first_row * a.mb_w;
+    const MbInfo mb = a.mbs[idx];
+    int qpy = mb.qp;
+    if (!mb_has_qp_delta(mb)) {
+        qpy = t.qp;
+        int j = idx - 1;
+        while (j >= first) {
+            const int base = j - 63, m = base + l;
+            const unsigned long long msk = __ballot(m >= first && mb_has_qp_delta(a.mbs[m]));
+            if (msk) {
+                qpy = a.mbs[base + 63 - __clzll(msk)].qp;
+                break;
+            }
+            j = base - 1;
+        }
+    }
+    if (l == 0) a.db[idx] = db_info(mb, qpy);
+}
+
+__device__ __forceinline__ void unpack4(uint32_t w, int* d) {
+    d[0] = w & 255;
+    d[1] = (w >> 8) & 255;
+    d[2] = (w >> 16) & 255;
+    d[3] = w >> 24;
+}
+__device__ __forceinline__ uint32_t pack4(const int* d) {
+    return (uint32_t)d[0] | ((uint32_t)d[1] << 8) | ((uint32_t)d[2] << 16) | ((uint32_t)d[3] << 24);
+}
+
+__device__ __forceinline__ DbInfo as_db(uint2 v) {
+    DbInfo d;
+    __builtin_memcpy(&d, &v, sizeof(d));
+    return d;
+}
+
+// Workgroup barrier ordering LDS only: __syncthreads() would also drain vmcnt and
+// stall on the prefetch loads issued this step.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Per-QP filter parameters packed in one dword: alpha | beta << 8 | tC0(bS 1, 2, 3) << 16/21/26.
+__device__ __forceinline__ uint32_t db_pack_par(int i) {
+    return (uint32_t)H264_DB_ALPHA[i] | ((uint32_t)H264_DB_BETA[i] << 8) | ((uint32_t)H264_DB_TC0[i][0] << 16) |
+           ((uint32_t)H264_DB_TC0[i][1] << 21) | ((uint32_t)H264_DB_TC0[i][2] << 26);
+}
+
+// One edge of one line in the unified luma/chroma form: v = {p3 p2 p1 p0 q0 q1 q2 q3}.
+// A chroma line is a luma line whose ap/aq are forced false and whose tC is tC0 + 1
+// (8.7.2.3): then p1/q1/p2/q2 stay, bS < 4 moves p0/q0 by the clipped delta and
+// bS = 4 gives (2p1 + p0 + q1 + 2) >> 2 — exactly db_filter_chroma. One straight-line
+// sequence for all 32 active lanes (no luma/chroma divergence).
+// |a - b| of two samples (0..255) in one v_sad_u16; clip3 as v_max + v_min.
+__device__ __forceinline__ int adiff(int a, int b) { return (int)__builtin_amdgcn_sad_u16((uint32_t)a, (uint32_t)b, 0u); }
+__device__ __forceinline__ int clip3(int x, int lo, int hi) { return min(max(x, lo), hi); }
+
+template <bool kMbEdge>   // bS = 4 only occurs on MB edges: internal edges skip the strong filter
+__device__ __forceinline__ void db_filter_line(int* v, int bs, uint32_t par, bool chroma) {
+    const int alpha = par & 255, beta = (par >> 8) & 31;
+    const int tc0 = __builtin_amdgcn_ubfe(par, 16 + 5 * sk_clip(bs - 1, 0, 2), 5);
+    const int p3 = v[0], p2 = v[1], p1 = v[2], p0 = v[3], q0 = v[4], q1 = v[5], q2 = v[6], q3 = v[7];
+    const bool on = (bs != 0) & (adiff(p0, q0) < alpha) & (adiff(p1, p0) < beta) & (adiff(q1, q0) < beta);
+    const bool ap = !chroma & (adiff(p2, p0) < beta), aq = !chroma & (adiff(q2, q0) < beta);
+    const int tc = tc0 + (chroma ? 1 : (int)ap + (int)aq);
+    const int d = clip3((((q0 - p0) * 4) + (p1 - q1) + 4) >> 3, -tc, tc);
+    const int avg = (p0 + q0 + 1) >> 1;
+    int np0 = sk_clip255(p0 + d), nq0 = sk_clip255(q0 - d);
+    int np1 = ap ? p1 + clip3((p2 + avg - (p1 * 2)) >> 1, -tc0, tc0) : p1;
+    int nq1 = aq ? q1 + clip3((q2 + avg - (q1 * 2)) >> 1, -tc0, tc0) : q1;
+    int np2 = p2, nq2 = q2;
+    if (kMbEdge) {
+        const bool strong = bs == 4;
+        const bool sm = adiff(p0, q0) < ((alpha >> 2) + 2);
+        const bool ps = ap & sm, qs = aq & sm;
+        const int sp0 = ps ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
+        const int sq0 = qs ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
+        np0 = strong ? sp0 : np0;
+        nq0 = strong ? sq0 : nq0;
+        np1 = strong ? (ps ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1) : np1;
+        nq1 = strong ? (qs ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1) : nq1;
+        np2 = (strong & ps) ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : p2;
+        nq2 = (strong & qs) ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : q2;
+    }
+    v[1] = on ? np2 : p2;
+    v[2] = on ? np1 : p1;
+    v[3] = on ? np0 : p0;
+    v[4] = on ? nq0 : q0;
+    v[5] = on ? nq1 : q1;
+    v[6] = on ? nq2 : q2;
+}
+
+// Per-MB edge record (3 x 16 bytes), built in parallel by k_deblock_edges so the
+// sequential wavefront only extracts bits:
+//   w[0..1]  bS of the vertical edges, 4 bits per (edge le, 4x4 row b) at bit 16*(le&1) + 4*b of w[le>>1]
+//   w[2..3]  the same for the horizontal edges (b = 4x4 column)
+//   w[4..6]  luma params (db_pack_par) of the left, top and internal edges
+//   w[7..9]  chroma params of the left, top and internal edges
+//   w[10]    edge mask: bit le (vertical) / 4 + le (horizontal) set if any bS of that edge is non-zero
+// The left edge of MB column 0 and the top edge of a slice's first row are off (idc 2).
+__global__ __launch_bounds__(256) void k_deblock_edges(FrameArgs a) {
+    const int nmb = a.mb_w * a.mb_h;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= nmb) return;
+    const int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    const SliceTask t = a.tasks[mby / a.rows_per_slice];
+    if (t.final_action != ACT_P && t.final_action != ACT_I) return;
+    const DbInfo cur = a.db[idx];
+    const bool hl = mbx > 0, ht = mby > t.first_row;
+    const DbInfo left = hl ? a.db[idx - 1] : cur, top = ht ? a.db[idx - a.mb_w] : cur;
+    uint32_t w[12] = {};
+#pragma unroll
+    for (int le = 0; le < 4; le++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int sh = 16 * (le & 1) + 4 * b;
+            const int pe = le == 0 ? 3 : le - 1;
+            const int bv = (le == 0 && !hl) ? 0 : db_bs(le == 0 ? left : cur, cur, le == 0, b * 4 + pe, b * 4 + le);
+            const int bh = (le == 0 && !ht) ? 0 : db_bs(le == 0 ? top : cur, cur, le == 0, pe * 4 + b, le * 4 + b);
+            w[le >> 1] |= (uint32_t)bv << sh;
+            w[2 + (le >> 1)] |= (uint32_t)bh << sh;
+            w[10] |= (bv ? 1u << le : 0u) | (bh ? 16u << le : 0u);
+        }
+    const int qc = cur.qpy, cc = H264_CHROMA_QP[qc];
+    w[4] = db_pack_par((left.qpy + qc + 1) >> 1);
+    w[5] = db_pack_par((top.qpy + qc + 1) >> 1);
+    w[6] = db_pack_par(qc);
+    w[7] = db_pack_par((H264_CHROMA_QP[left.qpy] + cc + 1) >> 1);
+    w[8] = db_pack_par((H264_CHROMA_QP[top.qpy] + cc + 1) >> 1);
+    w[9] = db_pack_par(cc);
+    uint4* o = a.dbe + 3 * (size_t)idx;
+    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    o[2] = make_uint4(w[8], w[9], w[10], 0);
+}
+
+// K7 deblocking of one slice. Wave r owns MB row r ("band") and filters MB x at step
+// k = x + 2r + 1; the 2-MB lag covers every raster-order dependency of 8.7 (left MB,
+// top MB, and the top-right MB whose left edge rewrites the top MB's right columns).
+// Per band an 8-slot LDS ring holds MBs as 32 lines x 16 bytes (luma rows 0-15, Cb
+// rows 16-23, Cr rows 24-31; chroma lines use 8 of the 16 bytes). Lanes 0-31 own one
+// line each: its row for the vertical edges, its column for the horizontal ones,
+// through the unified filter (db_filter_line). Pixels and side info of MB x + 2 are
+// loaded into registers at step k and land in LDS at step k + 1, so a whole step
+// hides the global latency; MB x - 3 (final once the band below filtered its top
+// edge) is stored to ref. Edges whose bS is 0 on every line are skipped wave-uniformly
+// (static desktop regions: P_Skip runs filter nothing).
+template <int MAXR>
+__global__ __launch_bounds__(64 * MAXR) void k_deblock(FrameArgs a) {
+    constexpr int kSlots = 8;
+    __shared__ uint32_t ring[MAXR][kSlots][32][4];
+    __shared__ uint4 erec[MAXR][kSlots][3];   // edge record (k_deblock_edges) of the slot's MB
+    const SliceTask t = a.tasks[blockIdx.x];
+    if (t.final_action != ACT_P && t.final_action != ACT_I) return;
+    const int r = threadIdx.x >> 6, l = lane_id();
+    const int R = t.num_rows, W = a.mb_w;
+    const int mby = t.first_row + r;
+    const bool band = r < R;
+    const bool act = l < 32, chroma = l >= 16;
+    const int li = chroma ? (l & 7) : (l & 15);      // row / column inside the component
+    const int nrows = chroma ? 8 : 16;
+    const int lbase = chroma ? 16 + (l & 8) : 0;     // first line of the component
+    const int ldw = chroma ? 1 : 3;                  // dword holding a line's last 4 samples
+    const int bsh = 4 * (chroma ? li >> 1 : li >> 2);   // nibble of this line's 4x4 row / column
+    const uint8_t* src = chroma ? ((l & 8) ? a.rec.v : a.rec.u) : a.rec.y;
+    uint8_t* dst = chroma ? ((l & 8) ? a.ref.v : a.ref.u) : a.ref.y;
+    const int mbyc = sk_min(mby, t.first_row + R - 1);   // idle waves of a short slice load valid rows
+    const size_t rowoff = chroma ? (size_t)(mbyc * 8 + li) * a.stride_c : (size_t)(mbyc * 16 + li) * a.stride_y;
+    const int mbbytes = chroma ? 8 : 16;
+
+    // Loads run unconditionally on clamped addresses (results for MBs outside the
+    // slice are never stored): no zero-fill of in-flight registers, no extra waits.
+    // A line is two 8-byte halves; chroma lines (8 bytes) load/store their half twice.
+    const int half2 = chroma ? 0 : 8;
+    auto load_px = [&](int x) {
+        const uint8_t* p0 = src + rowoff + sk_clip(x, 0, W - 1) * mbbytes;
+        const uint2 lo = *reinterpret_cast<const uint2*>(p0), hi = *reinterpret_cast<const uint2*>(p0 + half2);
+        return make_uint4(lo.x, lo.y, hi.x, hi.y);
+    };
+    auto load_rec = [&](int x) {   // lanes 32..34 fetch the 3 x 16-byte edge record
+        return a.dbe[3 * ((size_t)mbyc * W + sk_clip(x, 0, W - 1)) + sk_min(sk_max(l - 32, 0), 2)];
+    };
+
+    int x = -1 - 2 * r;   // MB of step 0
+    // In flight across one step, stored to LDS at the top of the next: no register
+    // rotation of loaded values, so the only wait is for last step's loads.
+    uint4 pre = make_uint4(0, 0, 0, 0);
+    if (band) pre = act ? load_px(x + 1) : load_rec(x + 1);
+    const int steps = W + 2 * R + 2;
+    for (int k = 0; k < steps; k++, x++) {
+        if (band) {
+            if (x + 1 >= 0 && x + 1 < W) {
+                const int sn = (x + 1) & (kSlots - 1);
+                if (act) *reinterpret_cast<uint4*>(ring[r][sn][l]) = pre;
+                else if (l < 35) erec[r][sn][l - 32] = pre;
+            }
+            pre = act ? load_px(x + 2) : load_rec(x + 2);
+            wave_sync();
+
+            if (x >= 0 && x < W) {
+                const int sl = x & (kSlots - 1);
+                const uint4 e0 = erec[r][sl][0], e1 = erec[r][sl][1], e2 = erec[r][sl][2];
+                // slot e runs if luma edge e or, for chroma slot 1, luma edge 2 has a non-zero bS
+                const uint32_t emask = e2.z | ((e2.z & 0x44u) >> 1);
+                // per line: bS of edge slot e (chroma slots 0/1 = luma edges 0/2, slots 2/3 off)
+                auto bs_of = [&](uint32_t w01, uint32_t w23, int e) -> int {
+                    if (chroma) {
+                        if (e >= 2) return 0;
+                        return __builtin_amdgcn_ubfe(e == 0 ? w01 : w23, bsh, 4);
+                    }
+                    return __builtin_amdgcn_ubfe(e < 2 ? w01 : w23, 16 * (e & 1) + bsh, 4);
+                };
+                const uint32_t p_left = chroma ? e1.w : e1.x, p_top = chroma ? e2.x : e1.y;
+                const uint32_t p_in = chroma ? e2.y : e1.z;
+                uint32_t* own = ring[r][sl][0];
+                if (emask & 15u) {   // vertical edges: lane = line (row)
+                    uint32_t* lp = ring[r][(x - 1) & (kSlots - 1)][act ? l : 0];
+                    uint32_t* op = own + 4 * (act ? l : 0);
+                    int v[20];
+                    unpack4((emask & 1u) ? lp[ldw] : 0u, v);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) unpack4(op[q], v + 4 + 4 * q);
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (emask & (1u << e)) {
+                            const int bs = act ? bs_of(e0.x, e0.y, e) : 0;
+                            if (e == 0) db_filter_line<true>(v, bs, p_left, chroma);
+                            else db_filter_line<false>(v + 4 * e, bs, p_in, chroma);
+                        }
+                    if (act) {
+                        if (emask & 1u) lp[ldw] = pack4(v);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) op[q] = pack4(v + 4 + 4 * q);
+                    }
+                    wave_sync();
+                }
+                if (emask & 0xF0u) {   // horizontal edges: lane = line (column)
+                    uint8_t* ob = reinterpret_cast<uint8_t*>(own) + lbase * 16 + li;
+                    uint8_t* tb = reinterpret_cast<uint8_t*>(ring[sk_max(r - 1, 0)][sl][0]) +
+                                  (lbase + nrows - 4) * 16 + li;
+                    const bool top_on = (emask & 16u) && act;
+                    int v[20];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) v[q] = top_on ? tb[q * 16] : 0;
+#pragma unroll
+                    for (int q = 0; q < 16; q++) v[4 + q] = act ? ob[sk_min(q, nrows - 1) * 16] : 0;
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        if (emask & (16u << e)) {
+                            const int bs = act ? bs_of(e0.z, e0.w, e) : 0;
+                            if (e == 0) db_filter_line<true>(v, bs, p_top, chroma);
+                            else db_filter_line<false>(v + 4 * e, bs, p_in, chroma);
+                        }
+                    if (act) {
+                        if (top_on) {
+#pragma unroll
+                            for (int q = 1; q < 4; q++) tb[q * 16] = (uint8_t)v[q];
+                        }
+#pragma unroll
+                        for (int q = 0; q < 16; q++)
+                            if (q < nrows) ob[q * 16] = (uint8_t)v[4 + q];
+                    }
+                    wave_sync();
+                }
+            }
+            // MB x - 3 is final (the band below filtered its top edge last step)
+            const int xb = x - 3;
+            if (act && xb >= 0 && xb < W) {
+                const uint4 q = *reinterpret_cast<const uint4*>(ring[r][xb & (kSlots - 1)][l]);
+                uint8_t* p0 = dst + rowoff + xb * mbbytes;
+                *reinterpret_cast<uint2*>(p0) = make_uint2(q.x, q.y);
+                *reinterpret_cast<uint2*>(p0 + half2) = chroma ? make_uint2(q.x, q.y) : make_uint2(q.z, q.w);
+            }
+        }
+        lds_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------
 void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
     dim3 grid((a.mb_w + 15) / 16, a.mb_h);
     hipLaunchKernelGGL(k_convert_damage, grid, dim3(256), 0, s, a);
@@ -1565,6 +1997,7 @@ void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
 void launch_encode(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, s, a);
+    if (a.me_full) hipLaunchKernelGGL(k_me_mfma, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
@@ -1582,9 +2015,16 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
 }
 
 void launch_commit(const FrameArgs& a, hipStream_t s) {
-    int nmb = a.mb_w * a.mb_h;
-    (void)nmb;
     hipLaunchKernelGGL(k_commit, dim3((a.mb_w + 15) / 16, a.mb_h), dim3(256), 0, s, a);
+    if (a.deblock) {
+        const int nmb = a.mb_w * a.mb_h;
+        hipLaunchKernelGGL(k_deblock_prep, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_deblock_edges, dim3((nmb + 255) / 256), dim3(256), 0, s, a);
+        if (a.rows_per_slice <= 4)
+            hipLaunchKernelGGL(k_deblock<4>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_deblock<kMaxRows>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
+    }
 }
 
 }  // namespace gpu

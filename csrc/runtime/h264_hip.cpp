@@ -39,6 +39,8 @@ class HipBackend : public EncoderBackend {
         hipSetDevice(device_);
         for (auto& gx : graph_exec_)
             if (gx) hipGraphExecDestroy(gx);
+        for (auto& gx : post_exec_)
+            if (gx) hipGraphExecDestroy(gx);
         for (void* p : dev_allocs_) hipFree(p);
         for (void* p : host_allocs_) hipHostFree(p);
         for (int i = 0; i < 4; i++) hipEventDestroy(ev_[i]);
@@ -71,9 +73,12 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipEventRecord(ev_[1], stream_));
         // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
         // one sync; k_decide leaves the final slice decisions in h_tasks_.
-        run_encode_graph();
+        run_graph(graph_exec_[parity_], 0);
         HIPCHECK(hipEventRecord(ev_[2], stream_));
-        HIPCHECK(hipStreamSynchronize(stream_));
+        // MV field / reference update and K7 deblocking run after the packets are done:
+        // the host only waits for ev_[2]; the next frame's work queues behind the update.
+        run_graph(post_exec_[parity_], 1);
+        HIPCHECK(hipEventSynchronize(ev_[2]));
         build_packets(frame_id);
         parity_ ^= 1;
         float t0 = 0, t1 = 0;
@@ -105,6 +110,7 @@ class HipBackend : public EncoderBackend {
         else if (s == "ref_y") { p = args_.ref.y; n = (int64_t)ny; }
         else if (s == "ref_u") { p = args_.ref.u; n = (int64_t)nc; }
         else if (s == "ref_v") { p = args_.ref.v; n = (int64_t)nc; }
+        else if (s == "fs_mv") { p = args_.fs_mv; n = (int64_t)g_.num_mbs() * 4; }
         else if (s == "mbs") { p = args_.mbs; n = (int64_t)g_.num_mbs() * sizeof(MbInfo); }
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
         else if (s == "me") { p = args_.me; n = (int64_t)g_.num_mbs() * sizeof(MeResult); }
@@ -157,6 +163,8 @@ class HipBackend : public EncoderBackend {
         a.stride_y = g_.stride_y; a.stride_c = g_.stride_c;
         a.num_slices = ns; a.rows_per_slice = g_.rows_per_slice; a.fullframe = cfg_.fullframe;
         a.full_range = cfg_.full_range; a.me_range = cfg_.me_range; a.me_iters = cfg_.me_iters;
+        a.deblock = cfg_.deblock;
+        a.me_full = cfg_.me_full;
         a.ref = make_planes();
         a.rec = make_planes();
         a.mb_dirty = dmalloc<uint8_t>(nmb);
@@ -177,6 +185,9 @@ class HipBackend : public EncoderBackend {
         a.tasks = dmalloc<SliceTask>(ns);
         a.me = dmalloc<MeResult>(nmb);
         a.mvfield = dmalloc<int16_t>(2 * nmb);
+        a.fs_mv = dmalloc<int16_t>(2 * nmb);
+        a.db = dmalloc<DbInfo>(nmb);
+        a.dbe = dmalloc<uint4>((size_t)3 * nmb);
         a.mbs = dmalloc<MbInfo>(nmb);
         a.coefs = dmalloc<int16_t>((size_t)nmb * kCoefPerMb);
         a.mb_bits = dmalloc<uint32_t>((size_t)nmb * (gpu::kMbSlotBytes / 4));
@@ -249,28 +260,31 @@ class HipBackend : public EncoderBackend {
     }
 
     void invalidate_graphs() {
-        for (auto& gx : graph_exec_)
-            if (gx) { hipGraphExecDestroy(gx); gx = nullptr; }
+        for (auto* set : {graph_exec_, post_exec_})
+            for (int i = 0; i < 2; i++)
+                if (set[i]) { hipGraphExecDestroy(set[i]); set[i] = nullptr; }
     }
 
-    void enqueue_encode() {
-        const int ns = g_.num_slices;
-        (void)ns;  // rbsp is self-cleaning (k_ep_write); stripe flags are cleared by k_plan
-        gpu::launch_convert_damage(args_, stream_);
-        gpu::launch_encode(args_, stream_);
-        gpu::launch_commit(args_, stream_);
+    // part 0: convert/damage -> ... -> packets; part 1: commit (+ deblocking).
+    // rbsp is self-cleaning (k_ep_write); stripe flags are cleared by k_plan.
+    void enqueue(int part) {
+        if (part == 0) {
+            gpu::launch_convert_damage(args_, stream_);
+            gpu::launch_encode(args_, stream_);
+        } else {
+            gpu::launch_commit(args_, stream_);
+        }
     }
 
-    void run_encode_graph() {
+    void run_graph(hipGraphExec_t& gx, int part) {
         if (!use_graphs_) {
-            enqueue_encode();
+            enqueue(part);
             return;
         }
-        hipGraphExec_t& gx = graph_exec_[parity_];
         if (!gx) {
             hipGraph_t graph;
             HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
-            enqueue_encode();
+            enqueue(part);
             HIPCHECK(hipStreamEndCapture(stream_, &graph));
             HIPCHECK(hipGraphInstantiate(&gx, graph, nullptr, nullptr, 0));
             hipGraphDestroy(graph);
@@ -329,6 +343,7 @@ class HipBackend : public EncoderBackend {
     std::vector<std::vector<uint8_t>> param_sets_;
     std::vector<void*> dev_allocs_, host_allocs_;
     hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
+    hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
     float stage_ms_[4] = {0, 0, 0, 0};
 };

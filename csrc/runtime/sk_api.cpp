@@ -41,6 +41,7 @@ class CpuBackend : public EncoderBackend {
         else if (s == "me") { p = enc_.me.data(); n = (int64_t)(enc_.me.size() * sizeof(h264::MeResult)); }
         else if (s == "tasks") { p = enc_.tasks.data(); n = (int64_t)(enc_.tasks.size() * sizeof(h264::SliceTask)); }
         else if (s == "mb_dirty") plane(enc_.mb_dirty);
+        else if (s == "fs_mv") { p = enc_.fs_mv.data(); n = (int64_t)(enc_.fs_mv.size() * 2); }
         else return -1;
         if (dst && cap >= n) memcpy(dst, p, (size_t)n);
         return n;
@@ -90,6 +91,8 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.me_iters = c->me_iters > 0 ? c->me_iters : 24;
     e.scenecut = c->scenecut;
     e.fps = c->fps > 0 ? c->fps : 60.f;
+    e.deblock = c->deblock > 0 ? 1 : 0;   // off by default, like x264 ultrafast
+    e.me_full = c->me_full >= 0 ? 1 : 0;
     return e;
 }
 

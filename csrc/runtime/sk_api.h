@@ -15,6 +15,8 @@ typedef struct sk_h264_config {
     float fps;
     int32_t device;   // HIP device ordinal for the GPU backend
     int32_t backend;  // 0 = CPU reference, 1 = HIP (gfx950)
+    int32_t deblock;  // in-loop deblocking: 0 = default (off), > 0 on, < 0 off
+    int32_t me_full;  // MFMA +-16 exhaustive search candidate: 0 = default (on), > 0 on, < 0 off
 } sk_h264_config;
 
 typedef struct sk_packet {

@@ -294,6 +294,79 @@ def _clip1(x):
 
 
 # ---------------------------------------------------------------------------
+# deblocking tables (8.7.2.2: Tables 8-16, 8-17)
+_DB_ALPHA = np.array([0] * 16 + [4, 4, 5, 6, 7, 8, 9, 10, 12, 13, 15, 17, 20, 22, 25, 28, 32, 36, 40, 45, 50, 56, 63,
+                                 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255])
+_DB_BETA = np.array([0] * 16 + [2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13,
+                                13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18])
+_DB_TC0 = np.array([[0, 0, 0]] * 17 + [[0, 0, 1]] * 4 + [[0, 1, 1]] * 2 + [[1, 1, 1]] * 4 + [[1, 1, 2]] * 4 +
+                   [[1, 2, 3]] * 2 + [[2, 2, 3], [2, 2, 4], [2, 3, 4], [2, 3, 4], [3, 3, 5], [3, 4, 6], [3, 4, 6],
+                                      [4, 5, 7], [4, 5, 8], [4, 6, 9], [5, 7, 10], [6, 8, 11], [6, 8, 13],
+                                      [7, 10, 14], [8, 11, 16], [9, 12, 18], [10, 13, 20], [11, 15, 23],
+                                      [13, 17, 25]])
+
+
+def _db_qp(m) -> int:
+    return 0 if m.pcm else m.qp
+
+
+def _db_bs(p, q, e: int, j: int, vertical: bool) -> int:
+    """bS (8.7.2.1) of segment j of luma edge e between MB p (left/top, or q itself for e > 0) and q."""
+    pe = 3 if e == 0 else e - 1
+    pb, qb = (j * 4 + pe, j * 4 + e) if vertical else (pe * 4 + j, e * 4 + j)
+    if p.intra or q.intra:
+        return 4 if e == 0 else 3
+    if p.tc_luma[pb] or q.tc_luma[qb]:
+        return 2
+    if p.ref[pb] != q.ref[qb] or abs(int(p.mvx[pb]) - int(q.mvx[qb])) >= 4 or abs(int(p.mvy[pb]) - int(q.mvy[qb])) >= 4:
+        return 1
+    return 0
+
+
+def _db_filter(L: np.ndarray, bs: np.ndarray, qpav: int, fa: int, fb: int, chroma: bool) -> np.ndarray:
+    """Filters the lines of one edge. L: (n, 8) = p3..q3 (luma) or (n, 4) = p1 p0 q0 q1 (chroma)."""
+    ia, ib = min(51, max(0, qpav + fa)), min(51, max(0, qpav + fb))
+    alpha, beta = int(_DB_ALPHA[ia]), int(_DB_BETA[ib])
+    out = L.copy()
+    o = 2 if chroma else 0
+    p1, p0, q0, q1 = L[:, 2 - o], L[:, 3 - o], L[:, 4 - o], L[:, 5 - o]
+    on = (bs > 0) & (np.abs(p0 - q0) < alpha) & (np.abs(p1 - p0) < beta) & (np.abs(q1 - q0) < beta)
+    tc0 = _DB_TC0[ia][np.clip(bs - 1, 0, 2)]
+    weak, strong4 = on & (bs < 4), on & (bs == 4)
+    if chroma:
+        tc = tc0 + 1
+        d = np.clip((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc, tc)
+        out[weak, 1] = np.clip(p0 + d, 0, 255)[weak]
+        out[weak, 2] = np.clip(q0 - d, 0, 255)[weak]
+        out[strong4, 1] = ((2 * p1 + p0 + q1 + 2) >> 2)[strong4]
+        out[strong4, 2] = ((2 * q1 + q0 + p1 + 2) >> 2)[strong4]
+        return out
+    p3, p2, q2, q3 = L[:, 0], L[:, 1], L[:, 6], L[:, 7]
+    ap, aq = np.abs(p2 - p0) < beta, np.abs(q2 - q0) < beta
+    tc = tc0 + ap + aq
+    d = np.clip((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc, tc)
+    out[weak, 3] = np.clip(p0 + d, 0, 255)[weak]
+    out[weak, 4] = np.clip(q0 - d, 0, 255)[weak]
+    m = weak & ap
+    out[m, 2] = (p1 + np.clip((p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1, -tc0, tc0))[m]
+    m = weak & aq
+    out[m, 5] = (q1 + np.clip((q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1, -tc0, tc0))[m]
+    small = np.abs(p0 - q0) < ((alpha >> 2) + 2)
+    sp, sq = strong4 & ap & small, strong4 & aq & small
+    out[sp, 3] = ((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3)[sp]
+    out[sp, 2] = ((p2 + p1 + p0 + q0 + 2) >> 2)[sp]
+    out[sp, 1] = ((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3)[sp]
+    wp = strong4 & ~(ap & small)
+    out[wp, 3] = ((2 * p1 + p0 + q1 + 2) >> 2)[wp]
+    out[sq, 4] = ((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3)[sq]
+    out[sq, 5] = ((p0 + q0 + q1 + q2 + 2) >> 2)[sq]
+    out[sq, 6] = ((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3)[sq]
+    wq = strong4 & ~(aq & small)
+    out[wq, 4] = ((2 * q1 + q0 + p1 + 2) >> 2)[wq]
+    return out
+
+
+# ---------------------------------------------------------------------------
 @dataclass
 class MbState:
     avail: bool = False
@@ -307,6 +380,7 @@ class MbState:
     ref: np.ndarray = field(default_factory=lambda: np.full(16, -1, dtype=np.int64))
     tc_luma: np.ndarray = field(default_factory=lambda: np.zeros(16, dtype=np.int64))  # raster y*4+x
     tc_chroma: np.ndarray = field(default_factory=lambda: np.zeros((2, 4), dtype=np.int64))  # raster 2x2
+    db: tuple = (1, 0, 0)  # (disable_deblocking_filter_idc, FilterOffsetA, FilterOffsetB) of its slice
 
 
 class H264Decoder:
@@ -360,6 +434,7 @@ class H264Decoder:
             self._finish_picture()
 
     def _finish_picture(self):
+        self._deblock_picture()
         sps = self.cur_sps
         y, u, v = self.cur
         cl, cr, ct, cb = sps.crop
@@ -398,13 +473,13 @@ class H264Decoder:
             elif br.u1():
                 raise NotImplementedError("adaptive_ref_pic_marking")
         qp = pps.pic_init_qp + br.se()
+        db = (0, 0, 0)
         if pps.deblocking_filter_control_present:
             dis = br.ue()
-            if dis != 1:
-                raise NotImplementedError("in-loop deblocking filter")
-                # (alpha/beta offsets would follow)
-        else:
-            raise NotImplementedError("in-loop deblocking filter")
+            if dis > 2:
+                raise BitstreamError("disable_deblocking_filter_idc out of range")
+            db = (dis, 0, 0) if dis == 1 else (dis, 2 * br.se(), 2 * br.se())
+        self._db_params = db
 
         new_picture = self.cur is None or first_mb == 0 or frame_num != self.cur_frame_num
         if new_picture and self.cur is not None:
@@ -422,6 +497,7 @@ class H264Decoder:
             raise BitstreamError("P slice without a reference picture")
         self.slice_counter += 1
         self.stats["slices"] += 1
+        self.cur_pps = pps
         self._slice_data(br, sps, pps, first_mb, slice_type, qp, num_ref)
 
     # -------------------------------------------------------------------
@@ -438,6 +514,7 @@ class H264Decoder:
                     if mb_addr >= nmb:
                         raise BitstreamError("mb_skip_run past end of picture")
                     self._decode_skip(sps, mb_addr, sid)
+                    self.mbs[mb_addr].db = self._db_params
                     mb_addr += 1
                 if run > 0:
                     more = br.more_rbsp_data()
@@ -446,8 +523,62 @@ class H264Decoder:
             if mb_addr >= nmb:
                 raise BitstreamError("macroblock address past end of picture")
             self._macroblock(br, sps, pps, mb_addr, sid, slice_type, num_ref)
+            self.mbs[mb_addr].db = self._db_params
             mb_addr += 1
             more = br.more_rbsp_data()
+
+    # ---- in-loop deblocking (8.7) ----------------------------------------------
+    def _deblock_picture(self):
+        """Filters the finished picture in macroblock raster order: per MB the luma vertical
+        edges left to right, the luma horizontal edges top to bottom, then the same for Cb
+        and Cr. Each edge is filtered for all its lines at once (lines are independent)."""
+        sps, pps = self.cur_sps, getattr(self, "cur_pps", None)
+        if pps is None:
+            return
+        Y, U, V = self.cur
+        mbw = sps.mb_w
+        coff = pps.chroma_qp_index_offset
+        for addr, cur in enumerate(self.mbs):
+            if not cur.avail or cur.db[0] == 1:
+                continue
+            mbx, mby = addr % mbw, addr // mbw
+            left = self._db_neighbour(cur, addr - 1) if mbx > 0 else None
+            top = self._db_neighbour(cur, addr - mbw) if mby > 0 else None
+            _, fa, fb = cur.db
+            for vertical, nb in ((True, left), (False, top)):
+                for e in range(4):
+                    p = nb if e == 0 else cur
+                    if p is None:
+                        continue
+                    bs = np.repeat([_db_bs(p, cur, e, j, vertical) for j in range(4)], 4)
+                    if not bs.any():
+                        continue
+                    qpav = (_db_qp(p) + _db_qp(cur) + 1) >> 1
+                    x0, y0 = mbx * 16, mby * 16
+                    seg = (Y[y0:y0 + 16, x0 + 4 * e - 4:x0 + 4 * e + 4] if vertical
+                           else Y[y0 + 4 * e - 4:y0 + 4 * e + 4, x0:x0 + 16].T)
+                    seg[...] = _db_filter(seg.astype(np.int64), bs, qpav, fa, fb, chroma=False)
+            for P in (U, V):
+                for vertical, nb in ((True, left), (False, top)):
+                    for e in range(2):
+                        p = nb if e == 0 else cur
+                        if p is None:
+                            continue
+                        bs = np.repeat([_db_bs(p, cur, 2 * e, j, vertical) for j in range(4)], 2)
+                        if not bs.any():
+                            continue
+                        qpc = lambda m: T.CHROMA_QP[min(51, max(0, _db_qp(m) + coff))]  # noqa: E731
+                        qpav = (qpc(p) + qpc(cur) + 1) >> 1
+                        x0, y0 = mbx * 8, mby * 8
+                        seg = (P[y0:y0 + 8, x0 + 4 * e - 2:x0 + 4 * e + 2] if vertical
+                               else P[y0 + 4 * e - 2:y0 + 4 * e + 2, x0:x0 + 8].T)
+                        seg[...] = _db_filter(seg.astype(np.int64), bs, qpav, fa, fb, chroma=True)
+
+    def _db_neighbour(self, cur, addr):
+        m = self.mbs[addr]
+        if not m.avail or (cur.db[0] == 2 and m.slice_id != cur.slice_id):
+            return None
+        return m
 
     # ---- neighbour helpers ----------------------------------------------
     def _mb(self, sps, mbx, mby, sid):

@@ -28,7 +28,7 @@ class SkH264Config(ctypes.Structure):
         ("streaming_mode", ctypes.c_int32), ("damage_threshold", ctypes.c_int32),
         ("damage_duration", ctypes.c_int32), ("me_range", ctypes.c_int32), ("me_iters", ctypes.c_int32),
         ("scenecut", ctypes.c_int32), ("fps", ctypes.c_float), ("device", ctypes.c_int32),
-        ("backend", ctypes.c_int32),
+        ("backend", ctypes.c_int32), ("deblock", ctypes.c_int32), ("me_full", ctypes.c_int32),
     ]
 
 
@@ -180,7 +180,7 @@ class H264Encoder:
                  paint_over_trigger: int = 15, paint_over_burst: int = 5, streaming_mode: bool = False,
                  damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
-                 backend: str = "cpu"):
+                 backend: str = "cpu", deblock: bool = False, me_full: bool = True):
         L = lib()
         if backend not in ("cpu", "hip"):
             raise ValueError("backend must be 'cpu' or 'hip'")
@@ -189,7 +189,8 @@ class H264Encoder:
         self.cfg = SkH264Config(width, height, stripe_height, int(fullframe), int(full_range), qp, paint_qp,
                                 int(use_paint_over), paint_over_trigger, paint_over_burst, int(streaming_mode),
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
-                                device, 1 if backend == "hip" else 0)
+                                device, 1 if backend == "hip" else 0, 1 if deblock else -1,
+                                1 if me_full else -1)
         self.width, self.height = width, height
         self.backend = backend
         self._h = L.sk_h264_create(ctypes.byref(self.cfg))

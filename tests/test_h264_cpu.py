@@ -6,11 +6,12 @@ from selkies_gstreamer_amd.ops.native import H264Encoder, MB_INFO_DTYPE
 from tests.h264_util import StripeDecoder, synthetic_frames, bgrx_to_y709, psnr
 
 
+@pytest.mark.parametrize("deblock", [False, True])
 @pytest.mark.parametrize("fullframe", [False, True])
 @pytest.mark.parametrize("kind", ["desktop", "noise"])
-def test_cpu_roundtrip_bitexact(fullframe, kind):
+def test_cpu_roundtrip_bitexact(fullframe, kind, deblock):
     W, H = 160, 96
-    enc = H264Encoder(W, H, stripe_height=32, fullframe=fullframe, qp=26, backend="cpu")
+    enc = H264Encoder(W, H, stripe_height=32, fullframe=fullframe, qp=26, backend="cpu", deblock=deblock)
     sd = StripeDecoder(W, H)
     for t, f in enumerate(synthetic_frames(W, H, 5, kind=kind)):
         pk = enc.encode(f, t)
@@ -18,6 +19,10 @@ def test_cpu_roundtrip_bitexact(fullframe, kind):
             sd.feed(p.data)
         ref = enc.debug_buffer("ref_y").reshape(-1, (W + 15) // 16 * 16)[:H, :W]
         assert np.array_equal(sd.Y, ref), f"frame {t}: decoder output != encoder reconstruction"
+        for name, plane in (("ref_u", sd.U), ("ref_v", sd.V)):
+            buf = enc.debug_buffer(name)
+            refc = buf.reshape((H + 15) // 16 * 8, -1)[:H // 2, :W // 2]
+            assert np.array_equal(plane, refc), f"frame {t}: decoder {name} != encoder reconstruction"
         assert psnr(sd.Y, bgrx_to_y709(f)) > 30
 
 

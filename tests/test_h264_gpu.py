@@ -26,11 +26,12 @@ def _compare_state(cpu, gpu, W, t):
         assert np.array_equal(a, b), f"frame {t}: {name} differs ({np.sum(a != b)} bytes)"
 
 
+@pytest.mark.parametrize("deblock", [False, True])
 @pytest.mark.parametrize("fullframe", [False, True])
 @pytest.mark.parametrize("kind", ["desktop", "noise"])
-def test_gpu_matches_cpu_reference(fullframe, kind):
+def test_gpu_matches_cpu_reference(fullframe, kind, deblock):
     W, H = 192, 128
-    cpu, gpu = _pair(W, H, stripe_height=32, fullframe=fullframe, qp=26)
+    cpu, gpu = _pair(W, H, stripe_height=32, fullframe=fullframe, qp=26, deblock=deblock)
     sd = StripeDecoder(W, H)
     for t, f in enumerate(synthetic_frames(W, H, 6, seed=3, kind=kind)):
         pc = cpu.encode(f, t)
@@ -42,9 +43,10 @@ def test_gpu_matches_cpu_reference(fullframe, kind):
         assert psnr(sd.Y, bgrx_to_y709(f)) > 30
 
 
-def test_gpu_1080p_desktop_matches_cpu():
+@pytest.mark.parametrize("deblock", [False, True])
+def test_gpu_1080p_desktop_matches_cpu(deblock):
     W, H = 1920, 1080
-    cpu, gpu = _pair(W, H, stripe_height=64, qp=25)
+    cpu, gpu = _pair(W, H, stripe_height=64, qp=25, deblock=deblock)
     for t, f in enumerate(synthetic_frames(W, H, 3, seed=5)):
         pc = cpu.encode(f, t)
         pg = gpu.encode(f, t)
