@@ -112,6 +112,15 @@ int sk_x11_cursor_image(void* h, uint64_t* serial, int* w, int* hh, int* xhot, i
 void* sk_host_alloc(int64_t bytes);
 void sk_host_free(void* p);
 
+// Telephony audio codecs (codec/telephony.cpp): G.711 u-law (alaw = 0) / A-law,
+// G.722 64 kbit/s (16 kHz PCM, 2 samples per byte).
+int sk_g711_encode(int alaw, const int16_t* pcm, int n, uint8_t* out);
+int sk_g711_decode(int alaw, const uint8_t* in, int n, int16_t* pcm);
+void* sk_g722_create(void);
+void sk_g722_destroy(void* h);
+int sk_g722_encode(void* h, const int16_t* pcm, int n, uint8_t* out);
+int sk_g722_decode(void* h, const uint8_t* in, int n, int16_t* pcm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,7 +6,9 @@ legacy/gstwebrtc_app.py (send-only H.264 + Opus, an "input" data channel,
 keyframe on PLI/FIR, NACK retransmission, REMB-driven bitrate) and the
 vendored aiortc RTCPeerConnection (webrtc/rtcpeerconnection.py). It also
 implements the receiving side so the full stack is testable end to end
-without a browser (tests/test_webrtc.py).
+without a browser (tests/test_webrtc.py): a jitter buffer per SSRC
+(webrtc/jitterbuffer.py), NACK on gaps, PLI on resets, and the delay-based
+GCC estimator (webrtc/rate.py) that reports REMB to the sender.
 
 Media plane per access unit: one native call packetises + SRTP-protects every
 RTP packet (csrc/rtc/rtc.cpp); Python only hands the datagrams to the socket
@@ -18,10 +20,13 @@ import asyncio
 import logging
 import random
 import struct
+import time
 from typing import Callable, Optional
 
 from . import rtp, sdp
 from .ice import Candidate, IceAgent
+from .jitterbuffer import JitterBuffer, RtpPacket as JbPacket
+from .rate import RemoteBitrateEstimator
 from .native import Dtls, RtpPacketizer, Srtp
 from .sctp import SctpAssociation, DataChannel
 
@@ -62,6 +67,9 @@ class PeerConnection:
         self._pending_channels: list = []
         # receive side
         self._depack: dict[int, rtp.H264Depacketizer] = {}
+        self._jitter: dict[int, JitterBuffer] = {}
+        self._rx_rate: dict[int, RemoteBitrateEstimator] = {}
+        self.remb_sent_bps: Optional[int] = None
         self._rx_seq: dict[int, int] = {}
         self.rtt_ms: Optional[float] = None
         self.remb_bps: Optional[int] = None
@@ -327,10 +335,23 @@ class PeerConnection:
             self._rx_seq[h.ssrc] = (h.seq + 1) & 0xFFFF
         payload = data[h.header_len:]
         if h.payload_type == sdp.H264_PT:
+            now_ms = time.monotonic() * 1000.0
+            est = self._rx_rate.setdefault(h.ssrc, RemoteBitrateEstimator())
+            r = est.add(now_ms, h.timestamp / 90.0, len(data))
+            if r is not None and r[1]:
+                self.remb_sent_bps = r[0]
+                self.send_rtcp(rtp.remb(self.video_ssrc, r[0], [h.ssrc]))
+            jb = self._jitter.setdefault(h.ssrc, JitterBuffer(capacity=1024))
+            pli, frames = jb.add(JbPacket(h.seq, h.timestamp, h.marker, payload))
+            if pli:
+                self.request_keyframe(h.ssrc)
             d = self._depack.setdefault(h.ssrc, rtp.H264Depacketizer())
-            au = d.push(payload, h.timestamp, h.marker)
-            if au is not None:
-                self.on_video_frame(au, h.timestamp)
+            for fr in frames:
+                au = None
+                for i, pk in enumerate(fr.packets):
+                    au = d.push(pk.payload, fr.timestamp, pk.marker or i == len(fr.packets) - 1)
+                if au:
+                    self.on_video_frame(au, fr.timestamp)
         else:
             self.on_audio_packet(payload, h.timestamp)
 
