@@ -1,0 +1,266 @@
+// Sidebar dashboard: screen / audio / stats / sharing / gamepad / input panels
+// on top of the basic controls in index.html, with the server's ui_* settings
+// deciding what is shown.
+//
+// Parity target: addons/selkies-dashboard (sidebar sections video, audio,
+// screen, stats, clipboard, files, apps, sharing, gamepads, fullscreen, gaming
+// mode, trackpad, keyboard button, soft buttons; each behind a
+// ui_sidebar_show_* setting, settings.py:36-108). Pure helpers are exported for
+// the node unit tests; the DOM code is plain ES modules without a framework.
+import { TouchGamepad } from './touch-gamepad.js';
+
+// ui_sidebar_show_* flag -> data-section names it controls.
+export const SECTION_FLAGS = {
+  ui_sidebar_show_video_settings: ['video'],
+  ui_sidebar_show_audio_settings: ['audio'],
+  ui_sidebar_show_screen_settings: ['screen'],
+  ui_sidebar_show_stats: ['stats'],
+  ui_sidebar_show_clipboard: ['clipboard'],
+  ui_sidebar_show_files: ['files'],
+  ui_sidebar_show_apps: ['apps'],
+  ui_sidebar_show_sharing: ['sharing'],
+  ui_sidebar_show_gamepads: ['gamepads'],
+  ui_sidebar_show_fullscreen: ['fullscreen'],
+  ui_sidebar_show_gaming_mode: ['gaming'],
+  ui_sidebar_show_trackpad: ['trackpad'],
+  ui_sidebar_show_keyboard_button: ['keyboard'],
+  ui_sidebar_show_soft_buttons: ['softkeys'],
+};
+
+const flag = (st, name, dflt = true) => {
+  const d = st && st[name];
+  if (d == null) return dflt;
+  const v = typeof d === 'object' && 'value' in d ? d.value : d;
+  return v === true || v === 'true' || v === 1;
+};
+
+// Sections to show for a server settings payload (missing flags default to shown).
+export function visibleSections(st) {
+  const out = new Set();
+  if (!flag(st, 'ui_show_sidebar')) return out;
+  for (const [name, sections] of Object.entries(SECTION_FLAGS)) {
+    if (flag(st, name)) sections.forEach((s) => out.add(s));
+  }
+  if (!flag(st, 'audio_enabled')) out.delete('audio');
+  if (!flag(st, 'clipboard_enabled')) out.delete('clipboard');
+  if (!flag(st, 'gamepad_enabled')) out.delete('gamepads');
+  if (!flag(st, 'command_enabled')) out.delete('apps');
+  const ft = st && st.file_transfers;
+  const transfers = ft == null ? 'upload,download' : String(typeof ft === 'object' && 'value' in ft ? ft.value : ft);
+  if (!transfers.includes('upload')) out.delete('files');
+  return out;
+}
+
+// Share links of the current page: view-only and player 2-4 (gamepad-only) URLs.
+export function sharingLinks(href, st) {
+  const base = href.split('#')[0];
+  const links = [];
+  if (!flag(st, 'enable_sharing')) return links;
+  if (flag(st, 'enable_shared')) links.push({ label: 'view only', url: `${base}#shared` });
+  for (const n of [2, 3, 4]) {
+    if (flag(st, `enable_player${n}`)) links.push({ label: `player ${n}`, url: `${base}#player${n}` });
+  }
+  return links;
+}
+
+// Page hash -> display / sharing role.
+export function parseRole(hash) {
+  const h = hash.replace(/^#/, '');
+  const d = /^display2(?:-(left|right|up|down))?$/.exec(h);
+  if (d) return { id: 'display2', position: d[1] || 'right', shared: false, player: 1 };
+  const p = /^player([234])$/.exec(h);
+  if (p) return { id: 'primary', position: 'right', shared: true, player: parseInt(p[1], 10) };
+  return { id: 'primary', position: 'right', shared: h === 'shared', player: h === 'shared' ? 0 : 1 };
+}
+
+// X11 keysyms of the soft buttons (sent as kd/ku pairs; combos press in order, release reversed).
+export const SOFT_KEYS = {
+  Esc: [0xff1b], Tab: [0xff09], Ctrl: [0xffe3], Alt: [0xffe9], Super: [0xffeb], F11: [0xffc8],
+  'Ctrl+Alt+Del': [0xffe3, 0xffe9, 0xffff], 'Alt+Tab': [0xffe9, 0xff09], 'Ctrl+C': [0xffe3, 0x63],
+  'Ctrl+V': [0xffe3, 0x76],
+};
+
+export function softKeyMessages(name) {
+  const keys = SOFT_KEYS[name];
+  if (!keys) return [];
+  return [...keys.map((k) => `kd,${k}`), ...keys.slice().reverse().map((k) => `ku,${k}`)];
+}
+
+// Fixed-length history for the stats sparklines.
+export class Ring {
+  constructor(n = 60) { this.n = n; this.v = []; }
+  push(x) { if (x == null || Number.isNaN(x)) return; this.v.push(+x); if (this.v.length > this.n) this.v.shift(); }
+  max() { return this.v.length ? Math.max(...this.v) : 0; }
+  last() { return this.v.length ? this.v[this.v.length - 1] : null; }
+}
+
+// Polyline points of a sparkline of `ring` in a w x h box (y up, min 0).
+export function sparkPoints(ring, w, h) {
+  const top = Math.max(ring.max(), 1e-9);
+  const n = ring.v.length;
+  return ring.v.map((x, i) => [n > 1 ? (i * (w - 1)) / (ring.n - 1) : 0, h - 1 - (x / top) * (h - 2)]);
+}
+
+export const DPI_CHOICES = [96, 120, 144, 168, 192, 216, 240, 264, 288];
+export const AUDIO_BITRATES = [64000, 128000, 265000, 320000];
+
+// -------------------------------------------------------------------- DOM
+const STAT_KEYS = [['fps', 'fps'], ['mbps', 'Mbit/s'], ['rtt', 'ms'], ['cpu', 'cpu %'], ['gpu', 'gpu']];
+
+export class Dashboard {
+  constructor(client, doc = document) {
+    this.c = client;
+    this.doc = doc;
+    this.rings = Object.fromEntries(STAT_KEYS.map(([k]) => [k, new Ring(60)]));
+    this.touchPad = null;
+  }
+
+  el(tag, attrs = {}, children = []) {
+    const e = this.doc.createElement(tag);
+    for (const [k, v] of Object.entries(attrs)) {
+      if (k === 'text') e.textContent = v; else if (k.startsWith('on')) e[k] = v; else e.setAttribute(k, v);
+    }
+    for (const ch of children) e.appendChild(ch);
+    return e;
+  }
+
+  section(name, title, children) {
+    return this.el('div', { 'data-section': name }, [this.el('h3', { text: title }), ...children]);
+  }
+
+  build() {
+    const sb = this.doc.getElementById('sidebar');
+    const s = this.c.settings;
+    // screen
+    const mw = this.el('input', { type: 'number', min: '320', max: '7680', step: '2', value: s.manual_width || 1920,
+      style: 'width:70px' });
+    const mh = this.el('input', { type: 'number', min: '240', max: '4320', step: '2', value: s.manual_height || 1080,
+      style: 'width:70px' });
+    const manual = this.el('input', { type: 'checkbox' });
+    manual.checked = !!s.is_manual_resolution_mode;
+    const applyRes = () => {
+      const w = parseInt(mw.value, 10) & ~1;
+      const h = parseInt(mh.value, 10) & ~1;
+      this.c.settings.manual_width = w;
+      this.c.settings.manual_height = h;
+      this.c.updateSetting('is_manual_resolution_mode', manual.checked);
+      if (manual.checked) this.c.sendText(`r,${w}x${h},${this.c.display.id}`);
+    };
+    manual.onchange = applyRes;
+    const dpi = this.el('select', {}, DPI_CHOICES.map((d) => this.el('option', { value: d, text: `${d} dpi` })));
+    dpi.value = s.scaling_dpi || 96;
+    dpi.onchange = () => this.c.updateSetting('scaling_dpi', parseInt(dpi.value, 10));
+    const css = this.el('input', { type: 'checkbox' });
+    css.checked = !!s.use_css_scaling;
+    css.onchange = () => this.c.updateSetting('use_css_scaling', css.checked);
+    sb.appendChild(this.section('screen', 'Resolution', [
+      this.el('label', { text: 'manual resolution' }, [manual]),
+      this.el('label', {}, [mw, this.el('span', { text: 'x' }), mh,
+        this.el('button', { text: 'apply', onclick: applyRes })]),
+      this.el('label', { text: 'scaling' }, [dpi]),
+      this.el('label', { text: 'CSS scaling (no HiDPI)' }, [css]),
+    ]));
+    // audio bitrate
+    const ab = this.el('select', {}, AUDIO_BITRATES.map((b) => this.el('option', { value: b, text: `${b / 1000} kbit/s` })));
+    ab.value = s.audio_bitrate || 320000;
+    ab.onchange = () => this.c.updateSetting('audio_bitrate', parseInt(ab.value, 10));
+    this.audioBitrate = ab;
+    sb.appendChild(this.section('audio', 'Audio quality', [this.el('label', { text: 'bitrate' }, [ab])]));
+    // input
+    const gaming = this.el('input', { type: 'checkbox' });
+    gaming.onchange = () => {
+      if (gaming.checked) { this.c.input.requestPointerLock(); this.c.canvas.style.cursor = 'none'; } else {
+        if (this.doc.exitPointerLock) this.doc.exitPointerLock();
+        this.c.canvas.style.cursor = '';
+      }
+    };
+    const tp = this.el('input', { type: 'checkbox' });
+    tp.onchange = () => { this.c.input.trackpad = tp.checked; };
+    const kb = this.el('input', { type: 'text', 'aria-label': 'keyboard', autocapitalize: 'off', autocomplete: 'off',
+      style: 'position:absolute;left:-1000px;opacity:0' });
+    kb.oninput = () => { if (kb.value) { this.c.input.typeText(kb.value); kb.value = ''; } };
+    sb.appendChild(this.section('gaming', 'Input', [this.el('label', { text: 'gaming mode (pointer lock)' }, [gaming])]));
+    sb.appendChild(this.section('trackpad', '', [this.el('label', { text: 'trackpad mode' }, [tp])]));
+    sb.appendChild(this.section('keyboard', '', [kb, this.el('button', { text: 'on-screen keyboard',
+      onclick: () => kb.focus() })]));
+    sb.appendChild(this.section('softkeys', 'Keys', Object.keys(SOFT_KEYS).map((name) => this.el('button', {
+      text: name, onclick: () => softKeyMessages(name).forEach((m) => this.c.sendText(m)) }))));
+    // apps / command
+    const cmd = this.el('input', { type: 'text', placeholder: 'command', style: 'width:150px' });
+    sb.appendChild(this.section('apps', 'Apps', [this.el('label', {}, [cmd, this.el('button', { text: 'run',
+      onclick: () => { if (cmd.value.trim()) this.c.sendText(`cmd,${cmd.value.trim()}`); } })])]));
+    // sharing
+    this.shareBox = this.el('div');
+    sb.appendChild(this.section('sharing', 'Sharing', [this.shareBox]));
+    // gamepads
+    this.padBox = this.el('div', { style: 'white-space:pre;font:12px ui-monospace,monospace' });
+    sb.appendChild(this.section('gamepads', 'Gamepads', [this.padBox, this.el('button', { text: 'touch gamepad',
+      onclick: () => { if (!this.touchPad) this.touchPad = new TouchGamepad(); this.touchPad.toggle(); } })]));
+    // stats sparklines
+    this.sparks = {};
+    const graphs = STAT_KEYS.map(([k, label]) => {
+      const cv = this.el('canvas', { width: 120, height: 22 });
+      const v = this.el('span', { text: '-' });
+      this.sparks[k] = { cv, v };
+      return this.el('label', { text: label }, [cv, v]);
+    });
+    sb.appendChild(this.section('stats', 'Graphs', graphs));
+    // tag the static sections of index.html
+    for (const h of sb.querySelectorAll(':scope > h3')) {
+      const name = { Video: 'video', Audio: 'audio', Screen: 'fullscreen', Clipboard: 'clipboard', Files: 'files',
+        Stats: 'stats' }[h.textContent.trim()];
+      if (name) h.setAttribute('data-section-head', name);
+    }
+    this.timer = setInterval(() => this.tick(), 1000);
+  }
+
+  apply(st) {
+    const vis = visibleSections(st);
+    const sb = this.doc.getElementById('sidebar');
+    for (const node of sb.querySelectorAll('[data-section]')) node.style.display = vis.has(node.dataset.section) ? '' : 'none';
+    // static index.html blocks: hide a heading and the controls up to the next heading
+    for (const h of sb.querySelectorAll('[data-section-head]')) {
+      const show = vis.has(h.dataset.sectionHead);
+      for (let n = h; n && (n === h || n.tagName !== 'H3'); n = n.nextElementSibling) {
+        if (n.dataset && n.dataset.section) break;
+        n.style.display = show ? '' : 'none';
+      }
+    }
+    const toggle = this.doc.getElementById('toggle');
+    if (toggle) toggle.style.display = vis.size ? '' : 'none';
+    this.shareBox.replaceChildren(...sharingLinks(location.href, st).map((l) => this.el('div', {}, [
+      this.el('a', { href: l.url, target: '_blank', text: l.label, style: 'color:#8cf' }),
+      this.el('button', { text: 'copy', onclick: () => navigator.clipboard && navigator.clipboard.writeText(l.url) }),
+    ])));
+    const abDef = st.audio_bitrate;
+    if (abDef && abDef.allowed) {
+      this.audioBitrate.replaceChildren(...abDef.allowed.map((b) => this.el('option', { value: b, text: `${b / 1000} kbit/s` })));
+      this.audioBitrate.value = this.c.settings.audio_bitrate;
+    }
+  }
+
+  tick() {
+    const st = this.c.stats;
+    for (const [k] of STAT_KEYS) {
+      const r = this.rings[k];
+      let v = st[k];
+      if (k === 'gpu' && v != null) v *= 100;
+      r.push(v);
+      const { cv, v: label } = this.sparks[k];
+      label.textContent = r.last() == null ? '-' : `${Math.round(r.last() * 10) / 10}`;
+      const g = cv.getContext && cv.getContext('2d');
+      if (!g) continue;
+      g.clearRect(0, 0, cv.width, cv.height);
+      g.strokeStyle = '#7cf';
+      g.beginPath();
+      sparkPoints(r, cv.width, cv.height).forEach(([x, y], i) => (i ? g.lineTo(x, y) : g.moveTo(x, y)));
+      g.stroke();
+    }
+    if (navigator.getGamepads) {
+      const pads = Array.from(navigator.getGamepads() || []).filter(Boolean);
+      this.padBox.textContent = pads.length ? pads.map((p) => `${p.index}: ${p.id.slice(0, 28)}\n   `
+        + `axes ${p.axes.map((a) => a.toFixed(1)).join(' ')}  buttons ${p.buttons.filter((b) => b.pressed).length}`)
+        .join('\n') : 'no gamepads';
+    }
+  }
+}

@@ -20,6 +20,10 @@ export class Input {
     this.padTimer = null;
     this.smallestWheel = 100;
     this.enabled = false;
+    this.padOffset = 0;         // #player2..4 links map local pads to server slots 1..3
+    this.gamepadOnly = false;   // player links: no keyboard / mouse
+    this.trackpad = false;      // touch drives a relative pointer like a laptop trackpad
+    this._tp = null;
   }
 
   _on(target, type, fn, opts) {
@@ -31,6 +35,12 @@ export class Input {
   attach() {
     if (this.enabled) return;
     this.enabled = true;
+    if (this.gamepadOnly) {
+      this._on(window, 'gamepadconnected', this._padConnected);
+      this._on(window, 'gamepaddisconnected', this._padDisconnected);
+      this.padTimer = setInterval(() => this._pollPads(), GAMEPAD_POLL_MS);
+      return;
+    }
     this._on(window, 'keydown', this._keydown, true);
     this._on(window, 'keyup', this._keyup, true);
     this._on(window, 'blur', this.releaseAll);
@@ -131,10 +141,37 @@ export class Input {
     }
   }
 
+  // Trackpad mode: one finger moves the pointer relatively, a short tap clicks,
+  // two fingers scroll (handled below).
+  _trackpad(e) {
+    const t = e.changedTouches[0];
+    const now = performance.now();
+    if (e.type === 'touchstart') {
+      this._tp = { x: t.clientX, y: t.clientY, x0: t.clientX, y0: t.clientY, t0: now };
+    } else if (e.type === 'touchmove' && this._tp) {
+      const dx = (t.clientX - this._tp.x) * 1.5;
+      const dy = (t.clientY - this._tp.y) * 1.5;
+      this._tp.x = t.clientX;
+      this._tp.y = t.clientY;
+      if (dx || dy) this.send(mouseMessage(true, dx, dy, this.mask));
+    } else if (e.type === 'touchend' && this._tp) {
+      const moved = Math.hypot(t.clientX - this._tp.x0, t.clientY - this._tp.y0);
+      if (now - this._tp.t0 < 200 && moved < 8) {
+        this.send(mouseMessage(true, 0, 0, this.mask | 1));
+        this.send(mouseMessage(true, 0, 0, this.mask & ~1));
+      }
+      this._tp = null;
+    }
+  }
+
   // Single finger = left-button drag, two fingers = vertical scroll.
   _touch(e) {
     e.preventDefault();
     const t = e.touches;
+    if (this.trackpad && (t.length <= 1)) {
+      this._trackpad(e);
+      return;
+    }
     if (t.length === 1) {
       const [x, y] = this._pos(t[0]);
       const down = e.type !== 'touchend';
@@ -165,14 +202,16 @@ export class Input {
     const gp = e.gamepad;
     if (gp.index > 3) return;
     this.pads.set(gp.index, { buttons: gp.buttons.map(() => 0), axes: gp.axes.map(() => 0) });
-    this.send(`js,c,${gp.index},${utf8ToB64(gp.id.slice(0, 255))},${gp.axes.length},${gp.buttons.length}`);
+    this.send(`js,c,${this._slot(gp.index)},${utf8ToB64(gp.id.slice(0, 255))},${gp.axes.length},${gp.buttons.length}`);
   }
 
   _padDisconnected(e) {
     if (!this.pads.has(e.gamepad.index)) return;
     this.pads.delete(e.gamepad.index);
-    this.send(`js,d,${e.gamepad.index}`);
+    this.send(`js,d,${this._slot(e.gamepad.index)}`);
   }
+
+  _slot(index) { return Math.min(3, index + this.padOffset); }
 
   _pollPads() {
     if (!navigator.getGamepads || !this.pads.size) return;
@@ -183,14 +222,14 @@ export class Input {
         const v = Math.round(b.value * 100) / 100;
         if (v !== st.buttons[i]) {
           st.buttons[i] = v;
-          this.send(`js,b,${gp.index},${i},${v}`);
+          this.send(`js,b,${this._slot(gp.index)},${i},${v}`);
         }
       });
       gp.axes.forEach((a, i) => {
         const v = Math.round(a * 100) / 100;
         if (v !== st.axes[i]) {
           st.axes[i] = v;
-          this.send(`js,a,${gp.index},${i},${v}`);
+          this.send(`js,a,${this._slot(gp.index)},${i},${v}`);
         }
       });
     }

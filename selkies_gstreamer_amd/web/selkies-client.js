@@ -3,6 +3,7 @@
 // with WebCodecs, plays Opus audio, forwards input, ACKs frames every 50 ms,
 // reports client fps, handles clipboard, uploads, cursor, multi-display hashes.
 import { AudioPipeline } from './lib/audio.js';
+import { Dashboard, parseRole } from './lib/dashboard.js';
 import { Input } from './lib/input.js';
 import {
   b64decode, b64ToUtf8, evenDown, parseFrame, parseText, utf8ToB64,
@@ -39,7 +40,7 @@ class Client {
       paint_over_jpeg_quality: 90, h264_fullcolor: false, h264_streaming_mode: false, use_cpu: false,
       use_paint_over_quality: true, h264_paintover_crf: 18, h264_paintover_burst_frames: 5, audio_bitrate: 320000,
       is_manual_resolution_mode: false, manual_width: 0, manual_height: 0, scaling_dpi: 96,
-      enable_binary_clipboard: false };
+      enable_binary_clipboard: false, use_css_scaling: false };
     try {
       return Object.assign(defaults, JSON.parse(localStorage.getItem(STORAGE_KEY) || '{}'));
     } catch (e) {
@@ -50,15 +51,17 @@ class Client {
   saveSettings() { localStorage.setItem(STORAGE_KEY, JSON.stringify(this.settings)); }
 
   parseHash() {
-    // #display2-right / #display2-left / #display2-up / #display2-down / #shared
-    const h = location.hash.slice(1);
-    const m = /^display2(?:-(left|right|up|down))?$/.exec(h);
-    if (m) return { id: 'display2', position: m[1] || 'right', shared: false };
-    return { id: 'primary', position: 'right', shared: h === 'shared' };
+    // #display2[-left|-right|-up|-down], #shared (view only), #player2..4 (gamepads only)
+    const role = parseRole(location.hash);
+    if (role.player > 1) {
+      this.input.padOffset = role.player - 1;
+      this.input.gamepadOnly = true;
+    }
+    return role;
   }
 
   settingsMessage() {
-    const dpr = window.devicePixelRatio || 1;
+    const dpr = this.settings.use_css_scaling ? 1 : (window.devicePixelRatio || 1);
     const s = Object.assign({}, this.settings, {
       initialClientWidth: evenDown(window.innerWidth * dpr),
       initialClientHeight: evenDown(window.innerHeight * dpr),
@@ -87,6 +90,7 @@ class Client {
       this.settings.encoder = st.encoder.value;
     }
     if (st.ui_title) document.title = st.ui_title.value;
+    if (this.dashboard) this.dashboard.apply(st);
     this.syncUi();
   }
 
@@ -156,7 +160,7 @@ class Client {
       case 'mode':
         if (!this.display.shared) this.sendText(this.settingsMessage());
         else { this.sendText('STOP_VIDEO'); this.sendText('START_VIDEO'); }
-        this.input.attach();
+        if (this.display.player > 0) this.input.attach();   // view-only links send no input
         this.startTimers();
         break;
       case 'json': this.onJson(m.data); break;
@@ -293,7 +297,7 @@ class Client {
       clearTimeout(resizeTimer);
       resizeTimer = setTimeout(() => {
         if (this.settings.is_manual_resolution_mode || this.display.shared) return;
-        const dpr = window.devicePixelRatio || 1;
+        const dpr = this.settings.use_css_scaling ? 1 : (window.devicePixelRatio || 1);
         this.sendText(`r,${evenDown(window.innerWidth * dpr)}x${evenDown(window.innerHeight * dpr)},${this.display.id}`);
       }, 300);
     });
@@ -302,6 +306,8 @@ class Client {
       this.sendText(document.hidden ? 'STOP_VIDEO' : 'START_VIDEO');
     });
     this.canvas.addEventListener('click', () => { this.canvas.focus(); if (!this.audio.ctx && $('audio').checked) this.audio.start(); });
+    this.dashboard = new Dashboard(this);
+    this.dashboard.build();
     this.syncUi();
   }
 }

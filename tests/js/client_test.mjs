@@ -1,6 +1,8 @@
 // Unit tests of the browser client's pure modules (run by tests/test_web_client.py).
 import assertModule from 'assert';
 const assert = assertModule.strict;
+import * as dash from '../../selkies_gstreamer_amd/web/lib/dashboard.js';
+import * as tg from '../../selkies_gstreamer_amd/web/lib/touch-gamepad.js';
 // node < 16 has no btoa/atob (browsers do)
 if (typeof globalThis.btoa === 'undefined') {
   globalThis.btoa = (s) => Buffer.from(s, 'binary').toString('base64');
@@ -61,6 +63,54 @@ const pcm = downsampleToS16Mono([a, a], 48000);
 assert.equal(pcm.length, 240);
 assert.equal(pcm[0], Math.trunc(0.5 * 0x7fff));
 assert.equal(downsampleToS16Mono([a, b], 48000)[10], 0);
+
+// ---- dashboard helpers (lib/dashboard.js) and the touch gamepad (lib/touch-gamepad.js)
+{
+  const all = dash.visibleSections({});
+  assert.ok(all.has('video') && all.has('sharing') && all.has('softkeys'));
+  const some = dash.visibleSections({ ui_sidebar_show_stats: { value: false }, command_enabled: { value: false },
+    file_transfers: { value: 'download' } });
+  assert.ok(!some.has('stats') && !some.has('apps') && !some.has('files') && some.has('video'));
+  assert.equal(dash.visibleSections({ ui_show_sidebar: { value: false } }).size, 0);
+  const links = dash.sharingLinks('http://h:8082/index.html#x', { enable_player3: { value: false } });
+  assert.deepEqual(links.map((l) => l.url), ['http://h:8082/index.html#shared', 'http://h:8082/index.html#player2',
+    'http://h:8082/index.html#player4']);
+  assert.deepEqual(dash.sharingLinks('http://h/', { enable_sharing: { value: false } }), []);
+  assert.deepEqual(dash.parseRole('#player3'), { id: 'primary', position: 'right', shared: true, player: 3 });
+  assert.equal(dash.parseRole('#shared').player, 0);
+  assert.equal(dash.parseRole('#display2-left').position, 'left');
+  assert.deepEqual(dash.softKeyMessages('Ctrl+Alt+Del'),
+    ['kd,65507', 'kd,65513', 'kd,65535', 'ku,65535', 'ku,65513', 'ku,65507']);
+  const r = new dash.Ring(4);
+  [1, 2, 3, 4, 5].forEach((x) => r.push(x));
+  assert.deepEqual(r.v, [2, 3, 4, 5]);
+  const pts = dash.sparkPoints(r, 4, 10);
+  assert.equal(pts.length, 4);
+  assert.equal(pts[3][1], 1);          // max at the top (y = 1)
+
+  assert.deepEqual(tg.stickAxes(0, 0, 50), [0, 0]);
+  assert.deepEqual(tg.stickAxes(5, 0, 50), [0, 0]);       // inside the dead zone
+  assert.deepEqual(tg.stickAxes(100, 0, 50), [1, 0]);     // clamped to the unit circle
+  const [sx, sy] = tg.stickAxes(30, -30, 50);
+  assert.ok(sx > 0.4 && sy < -0.4 && Math.hypot(sx, sy) <= 1);
+  assert.deepEqual(tg.dpadButtons(10, 0), [tg.BUTTONS.RIGHT]);
+  assert.deepEqual(tg.dpadButtons(10, 10).sort(), [tg.BUTTONS.DOWN, tg.BUTTONS.RIGHT].sort());
+  assert.deepEqual(tg.dpadButtons(0, -10), [tg.BUTTONS.UP]);
+  assert.deepEqual(tg.dpadButtons(0.01, 0.01), []);
+  const pad = new tg.VirtualPad(1);
+  assert.equal(pad.buttons.length, 17);
+  assert.ok(pad.setButton(tg.BUTTONS.A, true));
+  assert.ok(!pad.setButton(tg.BUTTONS.A, true));          // no change
+  pad.setStick('right', 0.5, -0.5);
+  assert.deepEqual(pad.axes, [0, 0, 0.5, -0.5]);
+  const nav = { getGamepads: () => [{ index: 0, id: 'real' }] };
+  assert.equal(tg.freeIndex(nav), 1);
+  const undo = tg.installGetGamepads(nav, pad);
+  assert.equal(nav.getGamepads()[1], pad);
+  undo();
+  assert.equal(nav.getGamepads().length, 1);
+}
+
 console.log('client tests ok');
 
 // ---- WebRTC mode (lib/webrtc.js) with fake WebSocket / RTCPeerConnection ----
