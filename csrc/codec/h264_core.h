@@ -170,7 +170,7 @@ SK_HD int sel3(int c, int a0, int a1, int a2) { return c == 0 ? a0 : (c == 1 ? a
 // Dequantise a non-DC coefficient at raster position `r` (flat scaling lists).
 SK_HD int dequant_coef(int l, int qp, int r) {
     const int32_t* v = H264_DEQUANT_V[qp % 6];
-    return (l * sel3(pos_class(r), v[0], v[1], v[2])) << (qp / 6);
+    return l * sel3(pos_class(r), v[0], v[1], v[2]) * (1 << (qp / 6));   // l may be negative: no <<
 }
 
 // Intra16x16 DC: inverse Hadamard of the 4x4 DC level matrix and scaling (8.5.10).
@@ -180,7 +180,7 @@ SK_HD void i16_dc_dequant(const int* c, int* dcy, int qp) {
     int ls = 16 * H264_DEQUANT_V[qp % 6][0];
     int q6 = qp / 6;
     for (int i = 0; i < 16; i++) {
-        if (qp >= 36) dcy[i] = (f[i] * ls) << (q6 - 6);
+        if (qp >= 36) dcy[i] = f[i] * ls * (1 << (q6 - 6));
         else dcy[i] = (f[i] * ls + (1 << (5 - q6))) >> (6 - q6);
     }
 }
@@ -193,10 +193,10 @@ SK_HD void chroma_dc_dequant(const int* c, int* dcc, int qpc) {
     int f3 = c[0] - c[1] - c[2] + c[3];
     int ls = 16 * H264_DEQUANT_V[qpc % 6][0];
     int q6 = qpc / 6;
-    dcc[0] = ((f0 * ls) << q6) >> 5;
-    dcc[1] = ((f1 * ls) << q6) >> 5;
-    dcc[2] = ((f2 * ls) << q6) >> 5;
-    dcc[3] = ((f3 * ls) << q6) >> 5;
+    dcc[0] = (f0 * ls * (1 << q6)) >> 5;   // multiply: f may be negative
+    dcc[1] = (f1 * ls * (1 << q6)) >> 5;   // multiply: f may be negative
+    dcc[2] = (f2 * ls * (1 << q6)) >> 5;   // multiply: f may be negative
+    dcc[3] = (f3 * ls * (1 << q6)) >> 5;   // multiply: f may be negative
 }
 
 SK_HD int chroma_qp(int qp) { return H264_CHROMA_QP[sk_clip(qp, 0, 51)]; }

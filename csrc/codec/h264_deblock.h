@@ -10,6 +10,7 @@
 // reorders the MBs along anti-diagonals without changing any sample: the result
 // is bit-identical and equals what a conforming decoder (WebCodecs) produces.
 #pragma once
+#include <stddef.h>
 #include "h264_core.h"
 
 namespace sk {

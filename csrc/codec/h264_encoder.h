@@ -116,7 +116,7 @@ inline PlanConfig plan_config(const EncoderConfig& c) {
 constexpr int kFrameNumMask = (1 << 16) - 1;  // log2_max_frame_num = 16 (h264_syntax.h)
 
 // One stripe's decision for this frame; `pic` is the picture state (full-frame mode).
-SK_HD inline void plan_stripe(const PlanConfig& c, StripeState& st, const StripeState& pic, bool d,
+SK_HD void plan_stripe(const PlanConfig& c, StripeState& st, const StripeState& pic, bool d,
                               int first_row, int num_rows, int mb_h, SliceTask& t) {
     const bool ff = c.fullframe != 0;
     t = SliceTask{};
@@ -170,7 +170,7 @@ SK_HD inline void plan_stripe(const PlanConfig& c, StripeState& st, const Stripe
 }
 
 // Striped mode: stripe state after its slice was coded with `final_action`.
-SK_HD inline void commit_stripe(StripeState& st, int final_action) {
+SK_HD void commit_stripe(StripeState& st, int final_action) {
     if (final_action == ACT_I) {
         st.frame_num = 1;
         st.idr_pic_id = (st.idr_pic_id + 1) & 0xffff;
@@ -181,7 +181,7 @@ SK_HD inline void commit_stripe(StripeState& st, int final_action) {
 }
 
 // Full-frame mode: picture state after a picture (IDR iff every slice was an IDR slice).
-SK_HD inline void commit_picture(StripeState& pic, bool idr) {
+SK_HD void commit_picture(StripeState& pic, bool idr) {
     if (idr) {
         pic.frame_num = 1;
         pic.idr_pic_id = (pic.idr_pic_id + 1) & 0xffff;

@@ -7,6 +7,7 @@
 // .frame_id).
 #include "sk_api.h"
 #include "encoder_iface.h"
+#include "trace.h"
 #include "../capture/frame_source.h"
 #include <atomic>
 #include <chrono>
@@ -128,7 +129,11 @@ class CaptureSession {
             if (key_req_.exchange(false)) enc_->request_keyframe();
             if (int q = qp_req_.exchange(0)) enc_->set_qp(q & 0xffff, q >> 16);
             int stride = 0;
-            const uint8_t* px = src_->grab(&stride);
+            const uint8_t* px = nullptr;
+            {
+                trace::Range r("capture.grab");
+                px = src_->grab(&stride);
+            }
             if (px && wm_loc_ >= 0 && !wm_.empty()) composite_watermark(const_cast<uint8_t*>(px), stride, frame_id);
             if (px) {
                 auto t0 = clk::now();

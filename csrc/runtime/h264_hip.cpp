@@ -6,6 +6,7 @@
 //   host-mapped packet slots, commit] (one hipGraph per src/prev parity)
 //   -> one sync -> packets. No host decision sits inside a frame.
 #include "encoder_iface.h"
+#include "trace.h"
 #include "../kernels/h264_gpu.h"
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -56,6 +57,7 @@ class HipBackend : public EncoderBackend {
     }
 
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        trace::Range frame_range("h264.frame");
         HIPCHECK(hipSetDevice(device_));
         packets_.clear();
         const size_t in_bytes = (size_t)stride * g_.H;
@@ -68,18 +70,27 @@ class HipBackend : public EncoderBackend {
         if (stride != args_.bgrx_stride) invalidate_graphs();
         set_parity_args(stride);
         h_frame_params_[0] = frame_id;  // host-mapped, read by k_plan
-        HIPCHECK(hipEventRecord(ev_[0], stream_));
-        HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, stream_));
-        HIPCHECK(hipEventRecord(ev_[1], stream_));
-        // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
-        // one sync; k_decide leaves the final slice decisions in h_tasks_.
-        run_graph(graph_exec_[parity_], 0);
-        HIPCHECK(hipEventRecord(ev_[2], stream_));
-        // MV field / reference update and K7 deblocking run after the packets are done:
-        // the host only waits for ev_[2]; the next frame's work queues behind the update.
-        run_graph(post_exec_[parity_], 1);
-        HIPCHECK(hipEventSynchronize(ev_[2]));
-        build_packets(frame_id);
+        {
+            trace::Range r("h264.submit");
+            HIPCHECK(hipEventRecord(ev_[0], stream_));
+            HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, stream_));
+            HIPCHECK(hipEventRecord(ev_[1], stream_));
+            // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
+            // one sync; k_decide leaves the final slice decisions in h_tasks_.
+            run_graph(graph_exec_[parity_], 0);
+            HIPCHECK(hipEventRecord(ev_[2], stream_));
+            // MV field / reference update and K7 deblocking run after the packets are done:
+            // the host only waits for ev_[2]; the next frame's work queues behind the update.
+            run_graph(post_exec_[parity_], 1);
+        }
+        {
+            trace::Range r("h264.wait");
+            HIPCHECK(hipEventSynchronize(ev_[2]));
+        }
+        {
+            trace::Range r("h264.packets");
+            build_packets(frame_id);
+        }
         parity_ ^= 1;
         float t0 = 0, t1 = 0;
         hipEventElapsedTime(&t0, ev_[0], ev_[1]);

@@ -6,6 +6,7 @@
 //   -> one sync -> packets = [frame_id][y] + cached JFIF header + entropy
 //      segment read straight out of host-mapped memory.
 #include "encoder_iface.h"
+#include "trace.h"
 #include "../kernels/jpeg_gpu.h"
 #include <hip/hip_runtime.h>
 #include <stdexcept>
@@ -58,6 +59,7 @@ class HipJpegBackend : public EncoderBackend {
     }
 
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        trace::Range frame_range("jpeg.frame");
         HIPCHECK(hipSetDevice(device_));
         packets_.clear();
         const size_t bytes = (size_t)stride * L_.H;
