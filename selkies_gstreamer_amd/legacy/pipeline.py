@@ -1,0 +1,223 @@
+"""GStreamer pipeline-string front end for the legacy WebRTC mode.
+
+The reference's legacy engine is a GStreamer graph (legacy/gstwebrtc_app.py:
+``ximagesrc ! videoconvert ! x264enc ... ! rtph264pay ! webrtcbin`` and the
+cuda*/va* variants). This build has no GStreamer: capture,
+conversion and encoding are one fused HIP pipeline. So that deployments that
+describe their media graph as a launch string keep working, this module parses
+the same syntax and maps element names and properties onto the engine's
+settings ("a minimal in-process pipeline string parser that maps
+the same element names and properties to our engine").
+
+Mapping:
+* sources: ``ximagesrc`` (display-name, show-pointer, startx/starty/endx/endy,
+  use-damage), ``videotestsrc`` / ``hipsrc`` → synthetic content;
+* caps ``video/x-raw,width=..,height=..,framerate=N/D``;
+* conversion / upload (``videoconvert``, ``cudaupload``, ``cudaconvert``,
+  ``vapostproc``, ``hipupload``, ``hipconvert``, ``queue``) → fused into the HIP
+  convert kernel (scaling is not: caps must keep the capture size);
+* H.264 encoders (``x264enc``, ``nvh264enc``, ``vah264enc``, ``openh264enc``,
+  ``qsvh264enc``, ``hiph264enc``) → the gfx950 H.264 encoder: ``bitrate`` (kbit/s),
+  ``key-int-max`` / ``gop-size`` / ``keyframe-period``, ``quantizer`` / ``qp-const``;
+  ``jpegenc`` → the JPEG stripe encoder;
+* payloader ``rtph264pay`` (``mtu``), ``webrtcbin`` (``stun-server``, ``latency``);
+* audio ``pulsesrc`` (``device``) → ``opusenc`` (``bitrate``, ``frame-size``) →
+  ``rtpopuspay``.
+H.265 / VP8 / VP9 / AV1 encoder elements are rejected with an explicit error:
+this build's video codecs are H.264 and JPEG.
+"""
+from __future__ import annotations
+
+import shlex
+from dataclasses import dataclass, field
+from typing import Optional
+
+H264_ENCODERS = {"x264enc", "nvh264enc", "vah264enc", "vah264lpenc", "openh264enc", "qsvh264enc", "hiph264enc",
+                 "nvcudah264enc", "nvautogpuh264enc"}
+UNSUPPORTED_ENCODERS = {"x265enc", "nvh265enc", "vah265enc", "qsvh265enc", "vp8enc", "vp9enc", "vavp9enc",
+                        "av1enc", "svtav1enc", "rav1enc", "nvav1enc", "vaav1enc", "qsvav1enc"}
+PASSTHROUGH = {"videoconvert", "cudaupload", "cudaconvert", "cudadownload", "vapostproc", "hipupload",
+               "hipconvert", "queue", "videorate", "capsfilter", "identity", "audioconvert", "audioresample",
+               "tee", "fakesink"}
+
+
+class PipelineError(ValueError):
+    pass
+
+
+@dataclass
+class Element:
+    name: str
+    props: dict = field(default_factory=dict)
+
+
+@dataclass
+class PipelineSpec:
+    source: str = "x11"                 # x11 | synthetic
+    display: Optional[str] = None
+    show_pointer: bool = True
+    region: Optional[tuple] = None      # (x0, y0, x1, y1) inclusive, ximagesrc start/end
+    width: Optional[int] = None
+    height: Optional[int] = None
+    framerate: Optional[float] = None
+    encoder: Optional[str] = None       # "h264" | "jpeg"
+    encoder_element: Optional[str] = None
+    bitrate_kbps: Optional[int] = None
+    keyframe_distance: Optional[int] = None
+    qp: Optional[int] = None
+    mtu: int = 1200
+    stun_server: Optional[str] = None
+    audio: bool = False
+    audio_device: Optional[str] = None
+    audio_bitrate: Optional[int] = None
+    audio_frame_ms: Optional[float] = None
+    elements: list = field(default_factory=list)
+
+
+def _split_links(text: str) -> list[str]:
+    out, cur, quote = [], [], None
+    for ch in text:
+        if quote:
+            cur.append(ch)
+            if ch == quote:
+                quote = None
+        elif ch in "\"'":
+            quote = ch
+            cur.append(ch)
+        elif ch == "!":
+            out.append("".join(cur).strip())
+            cur = []
+        else:
+            cur.append(ch)
+    out.append("".join(cur).strip())
+    if any(not s for s in out):
+        raise PipelineError("empty element between '!' links")
+    return out
+
+
+def _value(v: str):
+    v = v.strip()
+    if len(v) >= 2 and v[0] == v[-1] and v[0] in "\"'":
+        return v[1:-1]
+    low = v.lower()
+    if low in ("true", "false"):
+        return low == "true"
+    if "/" in v and all(p.strip("-").isdigit() for p in v.split("/", 1)):
+        n, d = v.split("/", 1)
+        return int(n) / max(1, int(d))
+    try:
+        return int(v)
+    except ValueError:
+        try:
+            return float(v)
+        except ValueError:
+            return v
+
+
+def _caps(seg: str) -> Element:
+    parts = [p.strip() for p in seg.split(",")]
+    parts[0] = parts[0].split("(", 1)[0]   # caps features: video/x-raw(memory:CUDAMemory|VAMemory)
+    props = {}
+    for p in parts[1:]:
+        if "=" in p:
+            k, v = p.split("=", 1)
+            v = v.split(")", 1)[-1] if v.startswith("(") else v   # (int)1920 / (fraction)60/1
+            props[k.strip()] = _value(v)
+    return Element(parts[0], props)
+
+
+def parse_elements(text: str) -> list[Element]:
+    """Tokenises a gst-launch style description into elements and caps."""
+    elems = []
+    for seg in _split_links(" ".join(text.split())):
+        first = seg.split(None, 1)[0]
+        if "/" in first.split(",")[0] and "=" not in first.split(",")[0]:
+            elems.append(_caps(seg))
+            continue
+        toks = shlex.split(seg)
+        e = Element(toks[0])
+        for t in toks[1:]:
+            if "=" not in t:
+                raise PipelineError(f"bad property {t!r} on {e.name}")
+            k, v = t.split("=", 1)
+            e.props[k] = _value(v)
+        elems.append(e)
+    return elems
+
+
+def parse_pipeline(text: str) -> PipelineSpec:
+    spec = PipelineSpec()
+    spec.elements = parse_elements(text)
+    for e in spec.elements:
+        n, p = e.name, e.props
+        if n == "ximagesrc":
+            spec.source = "x11"
+            spec.display = p.get("display-name")
+            spec.show_pointer = bool(p.get("show-pointer", True))
+            if any(k in p for k in ("startx", "starty", "endx", "endy")):
+                spec.region = (int(p.get("startx", 0)), int(p.get("starty", 0)), int(p.get("endx", 0)),
+                               int(p.get("endy", 0)))
+        elif n in ("videotestsrc", "hipsrc"):
+            spec.source = "synthetic"
+        elif n.startswith("video/"):
+            if n != "video/x-raw":
+                raise PipelineError(f"caps {n}: only raw video caps may precede the encoder")
+            spec.width = p.get("width", spec.width)
+            spec.height = p.get("height", spec.height)
+            if "framerate" in p:
+                spec.framerate = float(p["framerate"])
+        elif n in H264_ENCODERS:
+            spec.encoder, spec.encoder_element = "h264", n
+            if "bitrate" in p:
+                spec.bitrate_kbps = int(p["bitrate"])
+            for k in ("key-int-max", "gop-size", "keyframe-period", "idr-period"):
+                if k in p and int(p[k]) > 0:
+                    spec.keyframe_distance = int(p[k])
+            for k in ("quantizer", "qp-const", "qp", "qp-i"):
+                if k in p:
+                    spec.qp = int(p[k])
+        elif n == "jpegenc":
+            spec.encoder, spec.encoder_element = "jpeg", n
+        elif n in UNSUPPORTED_ENCODERS:
+            raise PipelineError(f"{n}: this build encodes H.264 (HIP) and JPEG; use an H.264 encoder element")
+        elif n in ("rtph264pay", "rtpopuspay"):
+            if "mtu" in p:
+                spec.mtu = int(p["mtu"])
+        elif n == "webrtcbin":
+            spec.stun_server = p.get("stun-server")
+        elif n == "pulsesrc":
+            spec.audio = True
+            spec.audio_device = p.get("device")
+        elif n == "opusenc":
+            spec.audio = True
+            if "bitrate" in p:
+                spec.audio_bitrate = int(p["bitrate"])
+            if "frame-size" in p:
+                spec.audio_frame_ms = float(p["frame-size"])
+        elif n.startswith("audio/"):
+            pass
+        elif n not in PASSTHROUGH:
+            raise PipelineError(f"unknown element {n!r}")
+    return spec
+
+
+def apply_to_args(spec: PipelineSpec, args) -> None:
+    """Overrides the legacy app's argparse namespace with what the pipeline sets."""
+    if spec.encoder == "jpeg":
+        raise PipelineError("jpegenc is for the websocket mode; WebRTC carries H.264")
+    if spec.encoder_element:
+        args.encoder = spec.encoder_element
+    if spec.framerate:
+        args.framerate = str(int(round(spec.framerate)))
+    if spec.bitrate_kbps:
+        args.video_bitrate = str(spec.bitrate_kbps)
+    if spec.keyframe_distance:
+        args.keyframe_distance = str(spec.keyframe_distance)
+    if spec.width and spec.height:
+        args.initial_resolution = f"{spec.width}x{spec.height}"
+    if spec.audio_bitrate:
+        args.audio_bitrate = str(spec.audio_bitrate)
+    if hasattr(args, "capture_source"):
+        args.capture_source = spec.source
+    if hasattr(args, "enable_cursors"):
+        args.enable_cursors = "false" if spec.show_pointer else "true"   # server-side cursor vs client cursors

@@ -98,6 +98,8 @@ FLAGS = [
     ("capture_source", "SELKIES_CAPTURE_SOURCE", "auto", "auto / x11 / synthetic (headless nodes, tests)"),
     ("use_cpu", "SELKIES_USE_CPU", "false", "CPU reference encoder instead of the HIP one"),
     ("initial_resolution", "SELKIES_INITIAL_RESOLUTION", "1920x1080", "capture size until the client resizes"),
+    ("video_pipeline", "SELKIES_VIDEO_PIPELINE", "",
+     "GStreamer launch string (ximagesrc ! ... ! x264enc ... ! rtph264pay); mapped onto the HIP engine"),
 ]
 # values the client may change at runtime and that persist in the JSON overlay
 PERSISTED = ("framerate", "video_bitrate", "audio_bitrate", "enable_resize", "encoder")
@@ -119,6 +121,9 @@ def parse_args(argv=None, env=None) -> argparse.Namespace:
     for k, v in overlay.items():
         if k in PERSISTED and k not in explicit and not env.get(f"SELKIES_{k.upper()}"):
             setattr(args, k, str(v))
+    if args.video_pipeline:
+        from .pipeline import apply_to_args, parse_pipeline
+        apply_to_args(parse_pipeline(args.video_pipeline), args)
     return args
 
 
