@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--deblock", type=int, default=0,
                    help="H.264 in-loop deblocking filter (1 on; default off like the reference's x264 ultrafast preset)")
     p.add_argument("--me-full", type=int, default=1, help="H.264 MFMA +-16 exhaustive search candidate (1 on, 0 off)")
+    p.add_argument("--bands", type=int, default=1,
+                   help="encode each session's frame as N bands of stripes on this GPU (parallel/banded.py): "
+                        "byte-identical output, upload overlapped with encoding")
     p.add_argument("--gather", action="store_true", help="gather all packets to rank 0 over RCCL each step")
     return p.parse_args()
 
@@ -87,10 +90,17 @@ def main():
         encs = [JpegEncoder(W, H, stripe_height=args.stripe_height, quality=args.jpeg_quality, use_paint_over=False,
                             device=local_rank, backend=args.backend) for _ in range(S)]
     else:
-        encs = [H264Encoder(W, H, stripe_height=args.stripe_height, fullframe=args.mode == "fullframe",
-                            qp=args.qp, use_paint_over=False, device=local_rank, backend=args.backend,
-                            deblock=bool(args.deblock), me_full=bool(args.me_full))
-                for _ in range(S)]
+        if args.bands > 1:
+            from selkies_gstreamer_amd.parallel.banded import BandedH264Encoder
+            encs = [BandedH264Encoder(W, H, [local_rank] * args.bands, stripe_height=args.stripe_height, qp=args.qp,
+                                      use_paint_over=False, backend=args.backend, deblock=bool(args.deblock),
+                                      me_full=bool(args.me_full))
+                    for _ in range(S)]
+        else:
+            encs = [H264Encoder(W, H, stripe_height=args.stripe_height, fullframe=args.mode == "fullframe",
+                                qp=args.qp, use_paint_over=False, device=local_rank, backend=args.backend,
+                                deblock=bool(args.deblock), me_full=bool(args.me_full))
+                    for _ in range(S)]
 
     lat = [[] for _ in range(S)]
     nbytes = [0] * S
@@ -185,6 +195,7 @@ def main():
                 "backend": args.backend,
                 "deblock": bool(args.deblock) if args.encoder == "h264" else None,
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
+                "bands_per_session": args.bands,
             },
         }
         print(json.dumps(res), flush=True)

@@ -38,6 +38,7 @@ struct EncoderConfig {
     float fps = 60.f;
     int deblock = 0;             // in-loop deblocking filter (idc 2: inside each slice); off = x264 ultrafast
     int me_full = 1;             // +-16 exhaustive MFMA search candidate (dirty MBs of P slices)
+    int shared_copy = 0;         // HIP: uploads on the device's shared copy stream (in submit order)
 };
 
 struct Geometry {

@@ -12,11 +12,23 @@ class EncoderBackend {
     virtual ~EncoderBackend() = default;
     virtual void request_keyframe() = 0;
     virtual int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) = 0;
+    // Split form of encode(): submit() queues the frame (the caller keeps `bgrx`
+    // alive until finish()), finish() waits and returns the packet count. Several
+    // encoders can be submitted before any is finished (bands of one frame, or
+    // sessions driven from one thread). Default: synchronous.
+    virtual int submit(const uint8_t* bgrx, int stride, uint16_t frame_id) {
+        pending_ = encode(bgrx, stride, frame_id);
+        return pending_ < 0 ? -1 : 0;
+    }
+    virtual int finish() { return pending_; }
     virtual int64_t debug_buffer(const char* name, void* dst, int64_t cap) = 0;
     virtual int stage_times(float* dst, int n) { (void)dst; (void)n; return 0; }
     // H.264 rate control hook (QP <= 0 keeps the current value); JPEG ignores it.
     virtual void set_qp(int qp, int paint_qp) { (void)qp; (void)paint_qp; }
     std::vector<h264::EncodedPacket> packets_;
+
+   protected:
+    int pending_ = 0;
 };
 
 EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c);

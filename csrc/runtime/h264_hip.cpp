@@ -10,6 +10,8 @@
 #include "../kernels/h264_gpu.h"
 #include <hip/hip_runtime.h>
 #include <chrono>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string.h>
 #include <string>
@@ -34,6 +36,7 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipSetDevice(device_));
         HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         for (int i = 0; i < 4; i++) HIPCHECK(hipEventCreate(&ev_[i]));
+        if (cfg_.shared_copy) copy_stream_ = device_copy_stream(device_);
         alloc();
     }
     ~HipBackend() override {
@@ -57,7 +60,12 @@ class HipBackend : public EncoderBackend {
     }
 
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
-        trace::Range frame_range("h264.frame");
+        submit(bgrx, stride, frame_id);
+        return finish();
+    }
+
+    int submit(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        trace::Range frame_range("h264.submit");
         HIPCHECK(hipSetDevice(device_));
         packets_.clear();
         const size_t in_bytes = (size_t)stride * g_.H;
@@ -70,26 +78,38 @@ class HipBackend : public EncoderBackend {
         if (stride != args_.bgrx_stride) invalidate_graphs();
         set_parity_args(stride);
         h_frame_params_[0] = frame_id;  // host-mapped, read by k_plan
-        {
-            trace::Range r("h264.submit");
+        pending_frame_ = frame_id;
+        if (copy_stream_) {
+            // shared per-device copy stream: uploads of encoders submitted back to back
+            // (bands of one frame) run in submission order at full PCIe rate, and each
+            // encoder's kernels start as soon as ITS rows have landed
+            HIPCHECK(hipEventRecord(ev_[0], copy_stream_));
+            HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, copy_stream_));
+            HIPCHECK(hipEventRecord(ev_[1], copy_stream_));
+            HIPCHECK(hipStreamWaitEvent(stream_, ev_[1], 0));
+        } else {
             HIPCHECK(hipEventRecord(ev_[0], stream_));
             HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, stream_));
             HIPCHECK(hipEventRecord(ev_[1], stream_));
-            // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
-            // one sync; k_decide leaves the final slice decisions in h_tasks_.
-            run_graph(graph_exec_[parity_], 0);
-            HIPCHECK(hipEventRecord(ev_[2], stream_));
-            // MV field / reference update and K7 deblocking run after the packets are done:
-            // the host only waits for ev_[2]; the next frame's work queues behind the update.
-            run_graph(post_exec_[parity_], 1);
         }
+        // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
+        // one sync; k_decide leaves the final slice decisions in h_tasks_.
+        run_graph(graph_exec_[parity_], 0);
+        HIPCHECK(hipEventRecord(ev_[2], stream_));
+        // MV field / reference update and K7 deblocking run after the packets are done:
+        // the host only waits for ev_[2]; the next frame's work queues behind the update.
+        run_graph(post_exec_[parity_], 1);
+        return 0;
+    }
+
+    int finish() override {
         {
             trace::Range r("h264.wait");
             HIPCHECK(hipEventSynchronize(ev_[2]));
         }
         {
             trace::Range r("h264.packets");
-            build_packets(frame_id);
+            build_packets(pending_frame_);
         }
         parity_ ^= 1;
         float t0 = 0, t1 = 0;
@@ -356,6 +376,22 @@ class HipBackend : public EncoderBackend {
     hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
     hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
+    hipStream_t copy_stream_ = nullptr;   // shared per device (not owned)
+    uint16_t pending_frame_ = 0;
+
+    // One H2D stream per device for encoders created with shared_copy: lives as long
+    // as the process (encoders come and go, the stream is reused).
+    static hipStream_t device_copy_stream(int device) {
+        static std::mutex mu;
+        static std::map<int, hipStream_t> streams;
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = streams.find(device);
+        if (it != streams.end()) return it->second;
+        hipStream_t s = nullptr;
+        HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        streams[device] = s;
+        return s;
+    }
     float stage_ms_[4] = {0, 0, 0, 0};
 };
 

@@ -93,6 +93,7 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.fps = c->fps > 0 ? c->fps : 60.f;
     e.deblock = c->deblock > 0 ? 1 : 0;   // off by default, like x264 ultrafast
     e.me_full = c->me_full >= 0 ? 1 : 0;
+    e.shared_copy = c->shared_copy > 0 ? 1 : 0;
     return e;
 }
 
@@ -177,6 +178,24 @@ void sk_h264_set_qp(void* enc, int qp, int paint_qp) { static_cast<EncoderBacken
 int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id) {
     try {
         return static_cast<EncoderBackend*>(enc)->encode(bgrx, stride, (uint16_t)frame_id);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
+int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->submit(bgrx, stride, (uint16_t)frame_id);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
+int sk_h264_finish(void* enc) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->finish();
     } catch (const std::exception& ex) {
         set_last_error(ex.what());
         return -1;

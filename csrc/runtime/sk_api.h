@@ -17,6 +17,7 @@ typedef struct sk_h264_config {
     int32_t backend;  // 0 = CPU reference, 1 = HIP (gfx950)
     int32_t deblock;  // in-loop deblocking: 0 = default (off), > 0 on, < 0 off
     int32_t me_full;  // MFMA +-16 exhaustive search candidate: 0 = default (on), > 0 on, < 0 off
+    int32_t shared_copy;  // > 0: H2D on the device's shared copy stream (bands of one frame)
 } sk_h264_config;
 
 typedef struct sk_packet {
@@ -35,6 +36,10 @@ void sk_h264_request_keyframe(void* enc);
 void sk_h264_set_qp(void* enc, int qp, int paint_qp);
 // Encodes one BGRx frame; returns the number of packets (or < 0 on error).
 int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride_bytes, int32_t frame_id);
+// Split encode: submit queues the frame (bgrx must stay valid until finish), finish
+// waits and returns the packet count (then sk_h264_get_packet as after sk_h264_encode).
+int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id);
+int sk_h264_finish(void* enc);
 int sk_h264_get_packet(void* enc, int32_t i, sk_packet* out);
 // Debug / test access to internal buffers ("src_y", "rec_y", "ref_y", "mbs", "coefs", "me", ...).
 int64_t sk_h264_debug_buffer(void* enc, const char* name, void* dst, int64_t cap);

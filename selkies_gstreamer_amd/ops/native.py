@@ -29,6 +29,7 @@ class SkH264Config(ctypes.Structure):
         ("damage_duration", ctypes.c_int32), ("me_range", ctypes.c_int32), ("me_iters", ctypes.c_int32),
         ("scenecut", ctypes.c_int32), ("fps", ctypes.c_float), ("device", ctypes.c_int32),
         ("backend", ctypes.c_int32), ("deblock", ctypes.c_int32), ("me_full", ctypes.c_int32),
+        ("shared_copy", ctypes.c_int32),
     ]
 
 
@@ -93,6 +94,8 @@ def lib():
         L.sk_h264_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.sk_h264_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_encode.restype = ctypes.c_int
+        L.sk_h264_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        L.sk_h264_finish.argtypes = [ctypes.c_void_p]
         L.sk_h264_get_packet.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(SkPacket)]
         L.sk_h264_debug_buffer.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64]
         L.sk_h264_debug_buffer.restype = ctypes.c_int64
@@ -180,7 +183,7 @@ class H264Encoder:
                  paint_over_trigger: int = 15, paint_over_burst: int = 5, streaming_mode: bool = False,
                  damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
-                 backend: str = "cpu", deblock: bool = False, me_full: bool = True):
+                 backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False):
         L = lib()
         if backend not in ("cpu", "hip"):
             raise ValueError("backend must be 'cpu' or 'hip'")
@@ -190,7 +193,7 @@ class H264Encoder:
                                 int(use_paint_over), paint_over_trigger, paint_over_burst, int(streaming_mode),
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
                                 device, 1 if backend == "hip" else 0, 1 if deblock else -1,
-                                1 if me_full else -1)
+                                1 if me_full else -1, 1 if shared_copy else 0)
         self.width, self.height = width, height
         self.backend = backend
         self._h = L.sk_h264_create(ctypes.byref(self.cfg))
@@ -226,6 +229,36 @@ class H264Encoder:
         n = L.sk_h264_encode(self._h, bgrx.ctypes.data, stride, frame_id & 0xFFFF)
         if n < 0:
             raise RuntimeError(f"encode failed: {L.sk_last_error().decode()}")
+        out = []
+        pk = SkPacket()
+        for i in range(n):
+            L.sk_h264_get_packet(self._h, i, ctypes.byref(pk))
+            out.append(Packet(ctypes.string_at(pk.data, pk.size), pk.y, pk.w, pk.h, bool(pk.key)))
+        return out
+
+    def submit(self, bgrx: np.ndarray, frame_id: int = 0) -> None:
+        """Queues a frame and returns at once (HIP: upload + graph launch); the array
+        is kept alive until :meth:`finish`. Submit several encoders, then finish them."""
+        if bgrx.dtype != np.uint8:
+            raise TypeError("bgrx must be uint8")
+        if not bgrx.flags["C_CONTIGUOUS"]:
+            bgrx = np.ascontiguousarray(bgrx)
+        self._inflight = bgrx
+        L = lib()
+        if L.sk_h264_submit(self._h, bgrx.ctypes.data, bgrx.strides[0], frame_id & 0xFFFF) < 0:
+            self._inflight = None
+            raise RuntimeError(f"submit failed: {L.sk_last_error().decode()}")
+
+    def finish(self) -> list[Packet]:
+        L = lib()
+        n = L.sk_h264_finish(self._h)
+        self._inflight = None
+        if n < 0:
+            raise RuntimeError(f"encode failed: {L.sk_last_error().decode()}")
+        return self._packets(n)
+
+    def _packets(self, n: int) -> list[Packet]:
+        L = lib()
         out = []
         pk = SkPacket()
         for i in range(n):
