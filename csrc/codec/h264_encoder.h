@@ -10,6 +10,7 @@
 //  * full-frame mode (encoder "x264enc"): one picture whose slices are the
 //    stripes, emitted as a single 0x04 packet with y = 0.
 #pragma once
+#include <string.h>
 #include <stdint.h>
 #include <vector>
 #include <string>
@@ -208,6 +209,17 @@ class Controller {
     void commit(const SliceTask* tasks);
     bool picture_is_idr(const SliceTask* tasks) const;
     const std::vector<StripeState>& stripes() const { return st_; }
+    // Session-state transfer (EncoderState): committed stripe states + picture state.
+    void export_states(StripeState* out) const {
+        for (size_t s = 0; s < st_.size(); s++) out[s] = st_[s];
+        out[st_.size()] = pic_;
+    }
+    void import_states(const StripeState* in) {
+        for (size_t s = 0; s < st_.size(); s++) st_[s] = in[s];
+        pic_ = in[st_.size()];
+    }
+    int qp() const { return cfg_.qp; }
+    int paint_qp() const { return cfg_.paint_qp; }
 
    private:
     EncoderConfig cfg_;
@@ -215,6 +227,48 @@ class Controller {
     std::vector<StripeState> st_;
     StripeState pic_;  // full-frame mode picture state
 };
+
+// ---- session state transfer --------------------------------------------------
+// Portable snapshot of everything that carries over from one frame to the next,
+// identical for the CPU and HIP backends (so a session can move between GPUs, or
+// between a GPU and the CPU reference, without an IDR):
+//   StateHeader | StripeState[num_slices + 1] (committed; last = picture state) |
+//   ref Y U V | last source Y U V (damage baseline) | mvfield int16[2 * num_mbs]
+struct StateHeader {
+    char magic[4];          // "SKH4"
+    int32_t version;        // 1
+    int32_t W, H, stripe_height, fullframe, num_slices;
+    int32_t started;        // a frame has been encoded (else the next one is all-dirty)
+    int32_t qp, paint_qp;   // rate-control QPs in force
+    int32_t reserved[6];
+};
+static_assert(sizeof(StateHeader) == 64, "StateHeader layout");
+
+inline size_t state_plane_bytes(const Geometry& g) {
+    return (size_t)g.stride_y * g.plane_h_y + 2 * (size_t)g.stride_c * g.plane_h_c;
+}
+inline size_t state_bytes(const Geometry& g) {
+    return sizeof(StateHeader) + sizeof(StripeState) * (size_t)(g.num_slices + 1) + 2 * state_plane_bytes(g) +
+           sizeof(int16_t) * 2 * (size_t)g.num_mbs();
+}
+inline void state_header(const EncoderConfig& c, const Geometry& g, int started, int qp, int paint_qp,
+                         StateHeader& h) {
+    memset(&h, 0, sizeof(h));
+    memcpy(h.magic, "SKH4", 4);
+    h.version = 1;
+    h.W = g.W;
+    h.H = g.H;
+    h.stripe_height = c.stripe_height;
+    h.fullframe = c.fullframe;
+    h.num_slices = g.num_slices;
+    h.started = started;
+    h.qp = qp;
+    h.paint_qp = paint_qp;
+}
+inline bool state_header_matches(const EncoderConfig& c, const Geometry& g, const StateHeader& h) {
+    return memcmp(h.magic, "SKH4", 4) == 0 && h.version == 1 && h.W == g.W && h.H == g.H &&
+           h.stripe_height == c.stripe_height && h.fullframe == c.fullframe && h.num_slices == g.num_slices;
+}
 
 // ---- bitstream packaging (host) -------------------------------------------
 int choose_level_idc(int mb_w, int mb_h, float fps);

@@ -527,7 +527,7 @@ __global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
     const int ns = a.num_slices, tid = threadIdx.x;
     StripeState* st = a.plan_state;
     StripeState& pic = st[ns];
-    if (a.plan_ctl[1]) {  // deferred commit of the previous frame
+    if (a.plan_ctl[1] == 1) {  // deferred commit of the previous frame (2: imported state, committed)
         if (a.fullframe) {
             bool idr = true;
             for (int s = tid; s < ns; s += 256) idr &= a.tasks[s].final_action == ACT_I && a.tasks[s].idr_on_intra;

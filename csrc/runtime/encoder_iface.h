@@ -21,6 +21,11 @@ class EncoderBackend {
         return pending_ < 0 ? -1 : 0;
     }
     virtual int finish() { return pending_; }
+    // Session state transfer (h264::StateHeader layout). `on_device`: the buffer is
+    // device memory of this encoder's GPU (HIP backend) instead of host memory.
+    virtual int64_t state_bytes() { return -1; }
+    virtual int export_state(void* dst, int on_device) { (void)dst; (void)on_device; return -1; }
+    virtual int import_state(const void* src, int on_device) { (void)src; (void)on_device; return -1; }
     virtual int64_t debug_buffer(const char* name, void* dst, int64_t cap) = 0;
     virtual int stage_times(float* dst, int n) { (void)dst; (void)n; return 0; }
     // H.264 rate control hook (QP <= 0 keeps the current value); JPEG ignores it.

@@ -120,6 +120,91 @@ class HipBackend : public EncoderBackend {
         return (int)packets_.size();
     }
 
+    int64_t state_bytes() override { return (int64_t)h264::state_bytes(g_); }
+
+    // Copies `n` bytes between this encoder's device buffer and a caller buffer
+    // that is device (on_device) or host memory.
+    void xfer(void* dst, const void* src, size_t n, bool to_caller, int on_device) {
+        const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice
+                                          : (to_caller ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice);
+        HIPCHECK(hipMemcpyAsync(dst, src, n, k, stream_));
+    }
+
+    int export_state(void* dst, int on_device) override {
+        HIPCHECK(hipSetDevice(device_));
+        HIPCHECK(hipStreamSynchronize(stream_));
+        const int ns = g_.num_slices;
+        int ctl[4];
+        std::vector<StripeState> st(ns + 1);
+        std::vector<SliceTask> tasks(ns);
+        HIPCHECK(hipMemcpy(ctl, args_.plan_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(st.data(), args_.plan_state, sizeof(StripeState) * (ns + 1), hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(tasks.data(), args_.tasks, sizeof(SliceTask) * ns, hipMemcpyDeviceToHost));
+        if (ctl[1] == 1) {   // apply the commit k_plan would run at the next frame
+            if (cfg_.fullframe) {
+                bool idr = ns > 0;
+                for (int s = 0; s < ns; s++) idr &= tasks[s].final_action == ACT_I && tasks[s].idr_on_intra;
+                commit_picture(st[ns], idr);
+            } else {
+                for (int s = 0; s < ns; s++) commit_stripe(st[s], tasks[s].final_action);
+            }
+        }
+        const int qp = h_key_seq_[1] > 0 ? h_key_seq_[1] : cfg_.qp;
+        const int pqp = h_key_seq_[2] > 0 ? h_key_seq_[2] : cfg_.paint_qp;
+        std::vector<uint8_t> head(sizeof(StateHeader) + sizeof(StripeState) * (ns + 1));
+        StateHeader h;
+        state_header(cfg_, g_, ctl[1] != 0, qp, pqp, h);
+        memcpy(head.data(), &h, sizeof(h));
+        memcpy(head.data() + sizeof(h), st.data(), sizeof(StripeState) * (ns + 1));
+        uint8_t* o = static_cast<uint8_t*>(dst);
+        if (on_device) HIPCHECK(hipMemcpyAsync(o, head.data(), head.size(), hipMemcpyHostToDevice, stream_));
+        else memcpy(o, head.data(), head.size());
+        o += head.size();
+        const size_t ny = (size_t)g_.stride_y * g_.plane_h_y, nc = (size_t)g_.stride_c * g_.plane_h_c;
+        const gpu::Planes& last_src = planes_src_[parity_ ^ 1];
+        for (const gpu::Planes* pl : {(const gpu::Planes*)&args_.ref, &last_src}) {
+            xfer(o, pl->y, ny, true, on_device); o += ny;
+            xfer(o, pl->u, nc, true, on_device); o += nc;
+            xfer(o, pl->v, nc, true, on_device); o += nc;
+        }
+        xfer(o, args_.mvfield, sizeof(int16_t) * 2 * (size_t)g_.num_mbs(), true, on_device);
+        HIPCHECK(hipStreamSynchronize(stream_));
+        return 0;
+    }
+
+    int import_state(const void* src, int on_device) override {
+        HIPCHECK(hipSetDevice(device_));
+        HIPCHECK(hipStreamSynchronize(stream_));
+        const int ns = g_.num_slices;
+        std::vector<uint8_t> head(sizeof(StateHeader) + sizeof(StripeState) * (ns + 1));
+        const uint8_t* i = static_cast<const uint8_t*>(src);
+        if (on_device) HIPCHECK(hipMemcpy(head.data(), i, sizeof(StateHeader), hipMemcpyDeviceToHost));
+        else memcpy(head.data(), i, sizeof(StateHeader));
+        StateHeader h;
+        memcpy(&h, head.data(), sizeof(h));
+        if (!state_header_matches(cfg_, g_, h)) {
+            set_last_error("encoder state does not match this encoder's geometry");
+            return -1;
+        }
+        xfer(args_.plan_state, i + sizeof(StateHeader), sizeof(StripeState) * (ns + 1), false, on_device);
+        i += head.size();
+        const size_t ny = (size_t)g_.stride_y * g_.plane_h_y, nc = (size_t)g_.stride_c * g_.plane_h_c;
+        const gpu::Planes& last_src = planes_src_[parity_ ^ 1];
+        for (const gpu::Planes* pl : {(const gpu::Planes*)&args_.ref, &last_src}) {
+            xfer(pl->y, i, ny, false, on_device); i += ny;
+            xfer(pl->u, i, nc, false, on_device); i += nc;
+            xfer(pl->v, i, nc, false, on_device); i += nc;
+        }
+        xfer(args_.mvfield, i, sizeof(int16_t) * 2 * (size_t)g_.num_mbs(), false, on_device);
+        // controller: committed state (2), and the host keyframe counter as already seen
+        int ctl[2] = {__atomic_load_n(&h_key_seq_[0], __ATOMIC_SEQ_CST), h.started ? 2 : 0};
+        HIPCHECK(hipMemcpyAsync(args_.plan_ctl, ctl, sizeof(ctl), hipMemcpyHostToDevice, stream_));
+        HIPCHECK(hipStreamSynchronize(stream_));
+        __atomic_store_n(&h_key_seq_[1], h.qp, __ATOMIC_SEQ_CST);
+        __atomic_store_n(&h_key_seq_[2], h.paint_qp, __ATOMIC_SEQ_CST);
+        return 0;
+    }
+
     int stage_times(float* dst, int n) override {
         int k = n < 2 ? n : 2;
         for (int i = 0; i < k; i++) dst[i] = stage_ms_[i] * 1000.f;

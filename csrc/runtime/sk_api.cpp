@@ -47,6 +47,49 @@ class CpuBackend : public EncoderBackend {
         return n;
     }
 
+    int64_t state_bytes() override { return (int64_t)h264::state_bytes(enc_.g); }
+
+    int export_state(void* dst, int on_device) override {
+        if (on_device) return -1;
+        uint8_t* o = static_cast<uint8_t*>(dst);
+        h264::StateHeader h;
+        h264::state_header(enc_.cfg, enc_.g, enc_.first_frame ? 0 : 1, enc_.ctl_.qp(), enc_.ctl_.paint_qp(), h);
+        memcpy(o, &h, sizeof(h));
+        o += sizeof(h);
+        enc_.ctl_.export_states(reinterpret_cast<h264::StripeState*>(o));
+        o += sizeof(h264::StripeState) * (enc_.g.num_slices + 1);
+        for (auto* planes : {enc_.ref, enc_.prev})
+            for (int p = 0; p < 3; p++) {
+                memcpy(o, planes[p].data(), planes[p].size());
+                o += planes[p].size();
+            }
+        memcpy(o, enc_.mvfield.data(), enc_.mvfield.size() * sizeof(int16_t));
+        return 0;
+    }
+
+    int import_state(const void* src, int on_device) override {
+        if (on_device) return -1;
+        const uint8_t* i = static_cast<const uint8_t*>(src);
+        h264::StateHeader h;
+        memcpy(&h, i, sizeof(h));
+        if (!h264::state_header_matches(enc_.cfg, enc_.g, h)) {
+            set_last_error("encoder state does not match this encoder's geometry");
+            return -1;
+        }
+        i += sizeof(h);
+        enc_.ctl_.import_states(reinterpret_cast<const h264::StripeState*>(i));
+        i += sizeof(h264::StripeState) * (enc_.g.num_slices + 1);
+        for (auto* planes : {enc_.ref, enc_.prev})
+            for (int p = 0; p < 3; p++) {
+                memcpy(planes[p].data(), i, planes[p].size());
+                i += planes[p].size();
+            }
+        memcpy(enc_.mvfield.data(), i, enc_.mvfield.size() * sizeof(int16_t));
+        enc_.first_frame = !h.started;
+        enc_.set_qp(h.qp, h.paint_qp);
+        return 0;
+    }
+
    private:
     h264::CpuH264Encoder enc_;
 };
@@ -196,6 +239,26 @@ int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame
 int sk_h264_finish(void* enc) {
     try {
         return static_cast<EncoderBackend*>(enc)->finish();
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
+int64_t sk_h264_state_bytes(void* enc) { return static_cast<EncoderBackend*>(enc)->state_bytes(); }
+
+int sk_h264_export_state(void* enc, void* dst, int32_t on_device) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->export_state(dst, on_device);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
+int sk_h264_import_state(void* enc, const void* src, int32_t on_device) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->import_state(src, on_device);
     } catch (const std::exception& ex) {
         set_last_error(ex.what());
         return -1;

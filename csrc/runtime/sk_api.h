@@ -40,6 +40,12 @@ int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride_bytes, int32_t
 // waits and returns the packet count (then sk_h264_get_packet as after sk_h264_encode).
 int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id);
 int sk_h264_finish(void* enc);
+// Session state snapshot (codec/h264_encoder.h StateHeader layout, identical for the
+// CPU and HIP backends): move a session between GPUs / processes without an IDR.
+// on_device = 1: `dst`/`src` is device memory on the encoder's GPU (HIP backend).
+int64_t sk_h264_state_bytes(void* enc);
+int sk_h264_export_state(void* enc, void* dst, int32_t on_device);
+int sk_h264_import_state(void* enc, const void* src, int32_t on_device);
 int sk_h264_get_packet(void* enc, int32_t i, sk_packet* out);
 // Debug / test access to internal buffers ("src_y", "rec_y", "ref_y", "mbs", "coefs", "me", ...).
 int64_t sk_h264_debug_buffer(void* enc, const char* name, void* dst, int64_t cap);

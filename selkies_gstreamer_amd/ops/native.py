@@ -96,6 +96,10 @@ def lib():
         L.sk_h264_encode.restype = ctypes.c_int
         L.sk_h264_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_finish.argtypes = [ctypes.c_void_p]
+        L.sk_h264_state_bytes.argtypes = [ctypes.c_void_p]
+        L.sk_h264_state_bytes.restype = ctypes.c_int64
+        L.sk_h264_export_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+        L.sk_h264_import_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
         L.sk_h264_get_packet.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(SkPacket)]
         L.sk_h264_debug_buffer.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int64]
         L.sk_h264_debug_buffer.restype = ctypes.c_int64
@@ -154,6 +158,18 @@ class PinnedBuffer:
             self.close()
         except Exception:
             pass
+
+
+def _buffer_ptr(buf, nbytes: int):
+    """(on_device, address) of a numpy array or a torch tensor of at least nbytes."""
+    if hasattr(buf, "data_ptr"):
+        if buf.numel() * buf.element_size() < nbytes or not buf.is_contiguous():
+            raise ValueError("state tensor too small or not contiguous")
+        return (1 if buf.is_cuda else 0), buf.data_ptr()
+    a = np.asarray(buf)
+    if a.nbytes < nbytes or not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("state buffer too small or not contiguous")
+    return 0, a.ctypes.data
 
 
 @dataclass
@@ -265,6 +281,29 @@ class H264Encoder:
             L.sk_h264_get_packet(self._h, i, ctypes.byref(pk))
             out.append(Packet(ctypes.string_at(pk.data, pk.size), pk.y, pk.w, pk.h, bool(pk.key)))
         return out
+
+    # -- session state transfer (codec/h264_encoder.h StateHeader layout) -----------------
+    def state_bytes(self) -> int:
+        return int(lib().sk_h264_state_bytes(self._h))
+
+    def export_state(self, out=None):
+        """Snapshot of the session (reference, damage baseline, MV field, controller).
+        ``out``: None (returns a host numpy array), a host numpy uint8 array, or a
+        device tensor (``data_ptr()`` + ``is_cuda``) on this encoder's GPU."""
+        n = self.state_bytes()
+        if out is None:
+            out = np.empty(n, np.uint8)
+        on_dev, ptr = _buffer_ptr(out, n)
+        if lib().sk_h264_export_state(self._h, ptr, on_dev) < 0:
+            raise RuntimeError(f"export_state failed: {lib().sk_last_error().decode()}")
+        return out
+
+    def import_state(self, buf) -> None:
+        """Continues the exported session here: the next frame is coded against the
+        imported reference (no IDR), same controller state and QPs."""
+        on_dev, ptr = _buffer_ptr(buf, self.state_bytes())
+        if lib().sk_h264_import_state(self._h, ptr, on_dev) < 0:
+            raise RuntimeError(f"import_state failed: {lib().sk_last_error().decode()}")
 
     def debug_buffer(self, name: str, dtype=np.uint8) -> np.ndarray:
         L = lib()
