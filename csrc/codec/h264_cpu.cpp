@@ -13,6 +13,10 @@ namespace h264 {
 
 CpuH264Encoder::CpuH264Encoder(const EncoderConfig& c) : cfg(c) {
     g.init(cfg);
+    scaled_ = (cfg.src_width > 0 && cfg.src_width != cfg.width) || (cfg.src_height > 0 && cfg.src_height != cfg.height);
+    if (scaled_)
+        scale_ = scale_params(cfg.src_width > 0 ? cfg.src_width : cfg.width,
+                              cfg.src_height > 0 ? cfg.src_height : cfg.height, cfg.width, cfg.height);
     ctl_.init(cfg, g);
     size_t ny = (size_t)g.stride_y * g.plane_h_y, nc = (size_t)g.stride_c * g.plane_h_c;
     for (int p = 0; p < 3; p++) {
@@ -50,8 +54,15 @@ void CpuH264Encoder::load_frame(const uint8_t* bgrx, int stride) {
         for (int qx = 0; qx < g.stride_c; qx++) {
             int x0 = std::min(2 * qx, W - 1), x1 = std::min(2 * qx + 1, W - 1);
             uint8_t y[4], cb, cr;
-            bgrx_quad_to_yuv(r0 + 4 * x0, r0 + 4 * x1, r1 + 4 * x0, r1 + 4 * x1, cfg.full_range, y,
-                             &cb, &cr);
+            if (scaled_) {   // K2: bilinear resample of the capture, same integer math as the kernel
+                uint32_t q[4] = {scale_fetch(bgrx, stride, scale_, x0, y0), scale_fetch(bgrx, stride, scale_, x1, y0),
+                                 scale_fetch(bgrx, stride, scale_, x0, y1), scale_fetch(bgrx, stride, scale_, x1, y1)};
+                bgrx_quad_to_yuv((const uint8_t*)&q[0], (const uint8_t*)&q[1], (const uint8_t*)&q[2],
+                                 (const uint8_t*)&q[3], cfg.full_range, y, &cb, &cr);
+            } else {
+                bgrx_quad_to_yuv(r0 + 4 * x0, r0 + 4 * x1, r1 + 4 * x0, r1 + 4 * x1, cfg.full_range, y,
+                                 &cb, &cr);
+            }
             size_t oy = (size_t)(2 * qy) * g.stride_y + 2 * qx;
             src[0][oy] = y[0];
             src[0][oy + 1] = y[1];

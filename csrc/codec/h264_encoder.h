@@ -40,6 +40,8 @@ struct EncoderConfig {
     int deblock = 0;             // in-loop deblocking filter (idc 2: inside each slice); off = x264 ultrafast
     int me_full = 1;             // +-16 exhaustive MFMA search candidate (dirty MBs of P slices)
     int shared_copy = 0;         // HIP: uploads on the device's shared copy stream (in submit order)
+    int src_width = 0;           // K2: capture size when it differs from width x height (0 = same);
+    int src_height = 0;          //     the frame is resampled (bilinear) inside the K1 conversion
 };
 
 struct Geometry {

@@ -6,6 +6,7 @@
 #include "h264_encoder.h"
 #include "h264_mb.h"
 #include "h264_deblock.h"
+#include "color.h"
 
 namespace sk {
 namespace h264 {
@@ -58,6 +59,8 @@ class CpuH264Encoder {
     std::vector<SliceTask> tasks;
     std::vector<std::vector<uint8_t>> param_sets;  // per stripe (striped) or [0] (full frame)
     bool first_frame = true;
+    bool scaled_ = false;          // K2: capture resampled to width x height
+    ScaleParams scale_ = {};
 
    private:
     void mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb) const;

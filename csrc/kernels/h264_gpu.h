@@ -24,6 +24,8 @@ struct FrameArgs {
     int full_range, me_range, me_iters;
     const uint8_t* bgrx;   // device copy of the captured frame
     int bgrx_stride;
+    int scaled;            // K2: resample the capture (src_w x src_h) to W x H inside K1
+    ScaleParams scale;
     Planes src, prev, ref, rec;
     uint8_t* mb_dirty;     // [num_mbs]
     int* stripe_dirty;     // [num_slices] set by k_convert_damage, consumed (and cleared) by k_plan

@@ -213,7 +213,14 @@ __global__ __launch_bounds__(256) void k_convert_damage(FrameArgs a) {
         const uint8_t* r0 = a.bgrx + (size_t)y0 * a.bgrx_stride;
         const uint8_t* r1 = a.bgrx + (size_t)y1 * a.bgrx_stride;
         uint32_t p0[8], p1[8];
-        if (x0 + 7 < a.W && (a.bgrx_stride & 15) == 0) {
+        if (a.scaled) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int x = sk_min(x0 + i, a.W - 1);
+                p0[i] = scale_fetch(a.bgrx, a.bgrx_stride, a.scale, x, y0);
+                p1[i] = scale_fetch(a.bgrx, a.bgrx_stride, a.scale, x, y1);
+            }
+        } else if (x0 + 7 < a.W && (a.bgrx_stride & 15) == 0) {
             const uint4 a0 = *reinterpret_cast<const uint4*>(r0 + 4 * x0);
             const uint4 a1 = *reinterpret_cast<const uint4*>(r0 + 4 * x0 + 16);
             const uint4 b0 = *reinterpret_cast<const uint4*>(r1 + 4 * x0);

@@ -62,6 +62,12 @@ class CaptureSession {
             } else {
                 h264::EncoderConfig e;
                 e.width = w & ~1; e.height = h & ~1; e.stripe_height = sh;
+                if (s.output_width > 0 && s.output_height > 0 && (s.output_width != w || s.output_height != h)) {
+                    e.src_width = w;   // K2: resample the capture inside the conversion kernel
+                    e.src_height = h;
+                    e.width = s.output_width & ~1;
+                    e.height = s.output_height & ~1;
+                }
                 e.fullframe = s.h264_fullframe; e.full_range = s.h264_fullcolor;
                 e.qp = sk_clip(s.h264_crf, 0, 51);
                 e.paint_qp = sk_clip(s.h264_paintover_crf, 0, 51);

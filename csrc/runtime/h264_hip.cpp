@@ -68,7 +68,7 @@ class HipBackend : public EncoderBackend {
         trace::Range frame_range("h264.submit");
         HIPCHECK(hipSetDevice(device_));
         packets_.clear();
-        const size_t in_bytes = (size_t)stride * g_.H;
+        const size_t in_bytes = (size_t)stride * (args_.scaled ? args_.scale.src_h : g_.H);
         if (in_bytes > bgrx_cap_) {
             if (bgrx_dev_) hipFree(bgrx_dev_);
             HIPCHECK(hipMalloc(&bgrx_dev_, in_bytes));
@@ -281,6 +281,11 @@ class HipBackend : public EncoderBackend {
         a.full_range = cfg_.full_range; a.me_range = cfg_.me_range; a.me_iters = cfg_.me_iters;
         a.deblock = cfg_.deblock;
         a.me_full = cfg_.me_full;
+        a.scaled = (cfg_.src_width > 0 && cfg_.src_width != cfg_.width) ||
+                   (cfg_.src_height > 0 && cfg_.src_height != cfg_.height);
+        if (a.scaled)
+            a.scale = scale_params(cfg_.src_width > 0 ? cfg_.src_width : cfg_.width,
+                                   cfg_.src_height > 0 ? cfg_.src_height : cfg_.height, cfg_.width, cfg_.height);
         a.ref = make_planes();
         a.rec = make_planes();
         a.mb_dirty = dmalloc<uint8_t>(nmb);

@@ -137,6 +137,8 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.deblock = c->deblock > 0 ? 1 : 0;   // off by default, like x264 ultrafast
     e.me_full = c->me_full >= 0 ? 1 : 0;
     e.shared_copy = c->shared_copy > 0 ? 1 : 0;
+    e.src_width = c->src_width > 0 ? c->src_width : 0;
+    e.src_height = c->src_height > 0 ? c->src_height : 0;
     return e;
 }
 

@@ -18,6 +18,7 @@ typedef struct sk_h264_config {
     int32_t deblock;  // in-loop deblocking: 0 = default (off), > 0 on, < 0 off
     int32_t me_full;  // MFMA +-16 exhaustive search candidate: 0 = default (on), > 0 on, < 0 off
     int32_t shared_copy;  // > 0: H2D on the device's shared copy stream (bands of one frame)
+    int32_t src_width, src_height;  // capture size if it differs (K2 resample in K1); 0 = width/height
 } sk_h264_config;
 
 typedef struct sk_packet {
@@ -82,6 +83,7 @@ typedef struct sk_capture_settings {
     int32_t stripe_height;   // 0 -> 64
     int32_t source;          // -1 auto (X11 if reachable), 0 X11 only, 1/2/3 synthetic motion/desktop/noise
     const char* display;     // X display name (nullptr -> $DISPLAY)
+    int32_t output_width, output_height;  // H.264 stream size if it differs from the capture (K2); 0 = same
 } sk_capture_settings;
 
 typedef struct sk_stripe_result {

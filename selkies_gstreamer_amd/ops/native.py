@@ -29,7 +29,7 @@ class SkH264Config(ctypes.Structure):
         ("damage_duration", ctypes.c_int32), ("me_range", ctypes.c_int32), ("me_iters", ctypes.c_int32),
         ("scenecut", ctypes.c_int32), ("fps", ctypes.c_float), ("device", ctypes.c_int32),
         ("backend", ctypes.c_int32), ("deblock", ctypes.c_int32), ("me_full", ctypes.c_int32),
-        ("shared_copy", ctypes.c_int32),
+        ("shared_copy", ctypes.c_int32), ("src_width", ctypes.c_int32), ("src_height", ctypes.c_int32),
     ]
 
 
@@ -58,6 +58,7 @@ class SkCaptureSettings(ctypes.Structure):
         ("watermark_path", ctypes.c_char_p), ("watermark_location_enum", ctypes.c_int32),
         ("device", ctypes.c_int32), ("stripe_height", ctypes.c_int32), ("source", ctypes.c_int32),
         ("display", ctypes.c_char_p),
+        ("output_width", ctypes.c_int32), ("output_height", ctypes.c_int32),
     ]
 
 
@@ -199,7 +200,8 @@ class H264Encoder:
                  paint_over_trigger: int = 15, paint_over_burst: int = 5, streaming_mode: bool = False,
                  damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
-                 backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False):
+                 backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
+                 src_width: int = 0, src_height: int = 0):
         L = lib()
         if backend not in ("cpu", "hip"):
             raise ValueError("backend must be 'cpu' or 'hip'")
@@ -209,7 +211,7 @@ class H264Encoder:
                                 int(use_paint_over), paint_over_trigger, paint_over_burst, int(streaming_mode),
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
                                 device, 1 if backend == "hip" else 0, 1 if deblock else -1,
-                                1 if me_full else -1, 1 if shared_copy else 0)
+                                1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height))
         self.width, self.height = width, height
         self.backend = backend
         self._h = L.sk_h264_create(ctypes.byref(self.cfg))
