@@ -78,6 +78,10 @@ def main():
 
     from selkies_gstreamer_amd.ops.native import H264Encoder, JpegEncoder, PinnedBuffer
     from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
+    from selkies_gstreamer_amd.parallel.numa import bind_to_gpu
+
+    # host threads and pinned frames on the GPU's NUMA node (first touch), before any allocation
+    numa_node = bind_to_gpu(local_rank) if args.backend == "hip" else None
 
     W, H = args.width, args.height
     S = args.sessions
@@ -196,6 +200,7 @@ def main():
                 "deblock": bool(args.deblock) if args.encoder == "h264" else None,
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
                 "bands_per_session": args.bands,
+                "numa_node_rank0": numa_node,
             },
         }
         print(json.dumps(res), flush=True)

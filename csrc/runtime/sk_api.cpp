@@ -156,6 +156,11 @@ int sk_hip_device_count(void) {
     return n;
 }
 
+int sk_hip_pci_bus_id(int device, char* buf, int len) {
+    if (hipDeviceGetPCIBusId(buf, len, device) != hipSuccess) return -1;
+    return 0;
+}
+
 const char* sk_last_error(void) { return g_last_error.c_str(); }
 
 void* sk_host_alloc(int64_t bytes) {

@@ -29,6 +29,8 @@ typedef struct sk_packet {
 
 const char* sk_version(void);
 int sk_hip_device_count(void);
+// PCI address ("0000:c1:00.0") of a HIP device, for NUMA placement of host buffers.
+int sk_hip_pci_bus_id(int device, char* buf, int len);
 
 void* sk_h264_create(const sk_h264_config* cfg);
 void sk_h264_destroy(void* enc);

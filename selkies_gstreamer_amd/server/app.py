@@ -92,6 +92,16 @@ async def serve(argv: Sequence[str], stop: Optional[asyncio.Event] = None, ready
     opts = app_options(argv)
     configure_logging(settings)
     metrics = Metrics(csv_path=opts.metrics_csv or None)
+    if opts.num_gpus == 1 and opts.capture_source != "cpu":
+        try:   # capture/encode threads and pinned frames next to the GPU (parallel/numa.py)
+            from ..parallel.numa import bind_to_gpu
+            from ..ops.native import hip_device_count
+            if hip_device_count() > opts.gpu_id:
+                node = bind_to_gpu(opts.gpu_id)
+                if node is not None:
+                    logging.getLogger("selkies").info("bound to NUMA node %d of GPU %d", node, opts.gpu_id)
+        except (OSError, RuntimeError):
+            pass
     server = DataStreamingServer(settings, upload_dir=opts.upload_dir if "upload" in settings.file_transfers else None,
                                  input_factory=make_input_factory(settings, opts), capture_source=opts.capture_source,
                                  gpu_id=opts.gpu_id, num_gpus=opts.num_gpus, web_root=opts.web_root, metrics=metrics)
