@@ -73,8 +73,15 @@ def main():
         import torch as _torch
         import torch.distributed as _dist
         torch, dist = _torch, _dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "hip":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))   # RCCL
+        else:   # CPU reference backend: rehearse the multi-rank path with gloo
+            dist.init_process_group("gloo")
+
+    def sync():
+        if torch is not None and args.backend == "hip":
+            torch.cuda.synchronize()
 
     from selkies_gstreamer_amd.ops.native import H264Encoder, JpegEncoder, PinnedBuffer
     from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
@@ -133,7 +140,7 @@ def main():
 
     if dist is not None:
         dist.barrier()
-        torch.cuda.synchronize()
+        sync()
     t0 = time.perf_counter()
     run_all(args.warmup, args.steps, True)
     gather_bytes = 0
@@ -144,7 +151,7 @@ def main():
         got = gather_packets(mine)
         gather_bytes = sum(len(d) for _, _, d in got) if got is not None else 0
     if dist is not None:
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
@@ -153,7 +160,7 @@ def main():
     stats = np.array([elapsed, frames, sum(nbytes), np.percentile(all_lat, 50), np.percentile(all_lat, 99)],
                      dtype=np.float64)
     if dist is not None:
-        t = torch.tensor(stats, device="cuda")
+        t = torch.tensor(stats, device="cuda" if args.backend == "hip" else "cpu")
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
