@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--bands", type=int, default=1,
                    help="encode each session's frame as N bands of stripes on this GPU (parallel/banded.py): "
                         "byte-identical output, upload overlapped with encoding")
+    p.add_argument("--overlap", type=int, default=0,
+                   help="1: upload frame n+1 while frame n encodes (upload/finish/launch); latency is "
+                        "measured from the frame's upload to its packets")
     p.add_argument("--gather", action="store_true", help="gather all packets to rank 0 over RCCL each step")
     return p.parse_args()
 
@@ -120,6 +123,25 @@ def main():
     def run(i, first, count, record):
         e = encs[i]
         fr = pool.array
+        if args.overlap and hasattr(e, "upload"):
+            t_up = time.perf_counter()
+            e.upload(fr[(first + 3 * i) % args.pool], first)
+            e.launch()
+            for t in range(first, first + count):
+                nxt = t + 1 < first + count
+                if nxt:
+                    t_next = time.perf_counter()
+                    e.upload(fr[(t + 1 + 3 * i) % args.pool], t + 1)   # overlaps frame t's kernels
+                pk = e.finish()
+                if record:
+                    lat[i].append(time.perf_counter() - t_up)
+                    nbytes[i] += sum(len(p.data) for p in pk)
+                    if args.gather:
+                        out_packets[i].append(pk)
+                if nxt:
+                    e.launch()
+                    t_up = t_next
+            return
         for t in range(first, first + count):
             a = time.perf_counter()
             pk = e.encode(fr[(t + 3 * i) % args.pool], t)
@@ -207,6 +229,7 @@ def main():
                 "deblock": bool(args.deblock) if args.encoder == "h264" else None,
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
                 "bands_per_session": args.bands,
+                "upload_overlap": bool(args.overlap),
                 "numa_node_rank0": numa_node,
             },
         }

@@ -21,6 +21,10 @@ class EncoderBackend {
         return pending_ < 0 ? -1 : 0;
     }
     virtual int finish() { return pending_; }
+    // submit() in two steps, so the next frame's upload can overlap this frame's
+    // kernels: upload(n+1) ... finish(n) ... launch(n+1). Default: upload encodes.
+    virtual int upload(const uint8_t* bgrx, int stride, uint16_t frame_id) { return submit(bgrx, stride, frame_id); }
+    virtual int launch() { return 0; }
     // Session state transfer (h264::StateHeader layout). `on_device`: the buffer is
     // device memory of this encoder's GPU (HIP backend) instead of host memory.
     virtual int64_t state_bytes() { return -1; }

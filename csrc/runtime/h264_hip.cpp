@@ -36,6 +36,7 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipSetDevice(device_));
         HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         for (int i = 0; i < 4; i++) HIPCHECK(hipEventCreate(&ev_[i]));
+        for (auto& e : ev_copy_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (cfg_.shared_copy) copy_stream_ = device_copy_stream(device_);
         alloc();
     }
@@ -48,6 +49,9 @@ class HipBackend : public EncoderBackend {
         for (void* p : dev_allocs_) hipFree(p);
         for (void* p : host_allocs_) hipHostFree(p);
         for (int i = 0; i < 4; i++) hipEventDestroy(ev_[i]);
+        for (auto& e : ev_copy_) hipEventDestroy(e);
+        for (auto* b : bgrx_dev_)
+            if (b) hipFree(b);
         hipStreamDestroy(stream_);
     }
 
@@ -65,33 +69,59 @@ class HipBackend : public EncoderBackend {
     }
 
     int submit(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
-        trace::Range frame_range("h264.submit");
+        if (upload(bgrx, stride, frame_id) < 0) return -1;
+        return launch();
+    }
+
+    // Stage a frame: H2D into the input buffer of the frame's parity on the copy
+    // stream. May be called while the previous frame is still encoding (its upload
+    // then overlaps that frame's kernels); launch() comes after finish() of it.
+    int upload(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        trace::Range frame_range("h264.upload");
+        HIPCHECK(hipSetDevice(device_));
+        const size_t in_bytes = (size_t)stride * (args_.scaled ? args_.scale.src_h : g_.H);
+        if (in_bytes > bgrx_cap_ || stride != args_.bgrx_stride) {
+            HIPCHECK(hipStreamSynchronize(stream_));   // geometry change: drain, then reallocate
+            if (in_bytes > bgrx_cap_) {
+                for (auto*& b : bgrx_dev_) {
+                    if (b) hipFree(b);
+                    HIPCHECK(hipMalloc(&b, in_bytes));
+                }
+                bgrx_cap_ = in_bytes;
+            }
+            invalidate_graphs();
+            args_.bgrx_stride = stride;
+        }
+        const int q = inflight_ ? parity_ ^ 1 : parity_;
+        // Nothing in flight: copy on the encoder's own stream (no cross-stream wait).
+        // Overlapped upload, or bands of one frame: the device's shared copy stream, so
+        // the uploads of all encoders on this GPU run back to back at full PCIe rate
+        // instead of contending (one copy queue, not one per session).
+        hipStream_t cs = stream_;
+        if (copy_stream_ || inflight_) cs = copy_stream_ ? copy_stream_ : device_copy_stream(device_);
+        // the last reader of bgrx_dev_[q] is the graph two frames back: finished
+        HIPCHECK(hipEventRecord(ev_[0], cs));
+        HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyHostToDevice, cs));
+        if (cs != stream_) HIPCHECK(hipEventRecord(ev_copy_[q], cs));
+        staged_on_main_ = cs == stream_;
+        staged_ = true;
+        staged_frame_ = frame_id;
+        return 0;
+    }
+
+    int launch() override {
+        if (!staged_ || inflight_) {
+            set_last_error("launch() needs one uploaded frame and no frame in flight");
+            return -1;
+        }
+        trace::Range frame_range("h264.launch");
         HIPCHECK(hipSetDevice(device_));
         packets_.clear();
-        const size_t in_bytes = (size_t)stride * (args_.scaled ? args_.scale.src_h : g_.H);
-        if (in_bytes > bgrx_cap_) {
-            if (bgrx_dev_) hipFree(bgrx_dev_);
-            HIPCHECK(hipMalloc(&bgrx_dev_, in_bytes));
-            bgrx_cap_ = in_bytes;
-            invalidate_graphs();
-        }
-        if (stride != args_.bgrx_stride) invalidate_graphs();
-        set_parity_args(stride);
-        h_frame_params_[0] = frame_id;  // host-mapped, read by k_plan
-        pending_frame_ = frame_id;
-        if (copy_stream_) {
-            // shared per-device copy stream: uploads of encoders submitted back to back
-            // (bands of one frame) run in submission order at full PCIe rate, and each
-            // encoder's kernels start as soon as ITS rows have landed
-            HIPCHECK(hipEventRecord(ev_[0], copy_stream_));
-            HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, copy_stream_));
-            HIPCHECK(hipEventRecord(ev_[1], copy_stream_));
-            HIPCHECK(hipStreamWaitEvent(stream_, ev_[1], 0));
-        } else {
-            HIPCHECK(hipEventRecord(ev_[0], stream_));
-            HIPCHECK(hipMemcpyAsync(bgrx_dev_, bgrx, in_bytes, hipMemcpyHostToDevice, stream_));
-            HIPCHECK(hipEventRecord(ev_[1], stream_));
-        }
+        set_parity_args(args_.bgrx_stride);   // bgrx = bgrx_dev_[parity_]
+        h_frame_params_[0] = staged_frame_;   // host-mapped, read by k_plan (previous frame is done)
+        pending_frame_ = staged_frame_;
+        if (!staged_on_main_) HIPCHECK(hipStreamWaitEvent(stream_, ev_copy_[parity_], 0));
+        HIPCHECK(hipEventRecord(ev_[1], stream_));
         // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
         // one sync; k_decide leaves the final slice decisions in h_tasks_.
         run_graph(graph_exec_[parity_], 0);
@@ -99,6 +129,8 @@ class HipBackend : public EncoderBackend {
         // MV field / reference update and K7 deblocking run after the packets are done:
         // the host only waits for ev_[2]; the next frame's work queues behind the update.
         run_graph(post_exec_[parity_], 1);
+        staged_ = false;
+        inflight_ = true;
         return 0;
     }
 
@@ -112,6 +144,7 @@ class HipBackend : public EncoderBackend {
             build_packets(pending_frame_);
         }
         parity_ ^= 1;
+        inflight_ = false;
         float t0 = 0, t1 = 0;
         hipEventElapsedTime(&t0, ev_[0], ev_[1]);
         hipEventElapsedTime(&t1, ev_[1], ev_[2]);
@@ -374,7 +407,7 @@ class HipBackend : public EncoderBackend {
     }
 
     void set_parity_args(int stride) {
-        args_.bgrx = bgrx_dev_;
+        args_.bgrx = bgrx_dev_[parity_];
         args_.bgrx_stride = stride;
         args_.src = planes_src_[parity_];
         args_.prev = planes_src_[parity_ ^ 1];
@@ -453,7 +486,10 @@ class HipBackend : public EncoderBackend {
     gpu::FrameArgs args_;
     gpu::Planes planes_src_[2];
     int parity_ = 0;
-    uint8_t* bgrx_dev_ = nullptr;
+    uint8_t* bgrx_dev_[2] = {nullptr, nullptr};   // input frame per parity (upload overlaps the other)
+    hipEvent_t ev_copy_[2];
+    bool staged_ = false, inflight_ = false, staged_on_main_ = true;
+    uint16_t staged_frame_ = 0;
     size_t bgrx_cap_ = 0;
     uint8_t* host_out_ = nullptr;
     int* h_key_seq_ = nullptr;

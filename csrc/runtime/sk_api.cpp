@@ -243,6 +243,24 @@ int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame
     }
 }
 
+int sk_h264_upload(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->upload(bgrx, stride, (uint16_t)frame_id);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
+int sk_h264_launch(void* enc) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->launch();
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
 int sk_h264_finish(void* enc) {
     try {
         return static_cast<EncoderBackend*>(enc)->finish();

@@ -43,6 +43,10 @@ int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride_bytes, int32_t
 // waits and returns the packet count (then sk_h264_get_packet as after sk_h264_encode).
 int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id);
 int sk_h264_finish(void* enc);
+// submit = upload + launch. upload(n+1) may run while frame n encodes (its copy
+// overlaps n's kernels); call launch() for it after sk_h264_finish of frame n.
+int sk_h264_upload(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id);
+int sk_h264_launch(void* enc);
 // Session state snapshot (codec/h264_encoder.h StateHeader layout, identical for the
 // CPU and HIP backends): move a session between GPUs / processes without an IDR.
 // on_device = 1: `dst`/`src` is device memory on the encoder's GPU (HIP backend).

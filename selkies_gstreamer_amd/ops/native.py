@@ -97,6 +97,8 @@ def lib():
         L.sk_h264_encode.restype = ctypes.c_int
         L.sk_h264_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_finish.argtypes = [ctypes.c_void_p]
+        L.sk_h264_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        L.sk_h264_launch.argtypes = [ctypes.c_void_p]
         L.sk_h264_state_bytes.argtypes = [ctypes.c_void_p]
         L.sk_h264_state_bytes.restype = ctypes.c_int64
         L.sk_h264_export_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
@@ -266,6 +268,26 @@ class H264Encoder:
         if L.sk_h264_submit(self._h, bgrx.ctypes.data, bgrx.strides[0], frame_id & 0xFFFF) < 0:
             self._inflight = None
             raise RuntimeError(f"submit failed: {L.sk_last_error().decode()}")
+
+    def upload(self, bgrx: np.ndarray, frame_id: int = 0) -> None:
+        """First half of :meth:`submit`: stages the frame (HIP: H2D on the copy stream).
+        Allowed while the previous frame is still in flight — its upload overlaps that
+        frame's kernels; call :meth:`launch` for it after :meth:`finish` of the previous."""
+        if bgrx.dtype != np.uint8:
+            raise TypeError("bgrx must be uint8")
+        if not bgrx.flags["C_CONTIGUOUS"]:
+            bgrx = np.ascontiguousarray(bgrx)
+        self._staged = bgrx
+        L = lib()
+        if L.sk_h264_upload(self._h, bgrx.ctypes.data, bgrx.strides[0], frame_id & 0xFFFF) < 0:
+            self._staged = None
+            raise RuntimeError(f"upload failed: {L.sk_last_error().decode()}")
+
+    def launch(self) -> None:
+        L = lib()
+        if L.sk_h264_launch(self._h) < 0:
+            raise RuntimeError(f"launch failed: {L.sk_last_error().decode()}")
+        self._inflight, self._staged = getattr(self, "_staged", None), None
 
     def finish(self) -> list[Packet]:
         L = lib()

@@ -82,3 +82,23 @@ def test_gpu_controller_matches_cpu(fullframe):
         ta, tb = cpu.debug_buffer("tasks", TASK_DTYPE), gpu.debug_buffer("tasks", TASK_DTYPE)
         assert np.array_equal(ta, tb), f"frame {t}: slice plans differ"
         assert [(p.y, p.key, p.data) for p in pg] == [(p.y, p.key, p.data) for p in pc], f"frame {t}"
+
+
+def test_gpu_overlapped_upload_matches_sequential():
+    """upload(n+1) while frame n encodes, then finish(n) / launch(n+1): same packets
+    as plain encode() (double-buffered input, frame id read at launch)."""
+    W, H = 320, 192
+    frames = list(synthetic_frames(W, H, 6, seed=12))
+    a = H264Encoder(W, H, stripe_height=64, qp=26, backend="hip")
+    b = H264Encoder(W, H, stripe_height=64, qp=26, backend="hip")
+    ref = [[p.data for p in a.encode(f, t)] for t, f in enumerate(frames)]
+    got = []
+    b.upload(frames[0], 0)
+    b.launch()
+    for t in range(len(frames)):
+        if t + 1 < len(frames):
+            b.upload(frames[t + 1], t + 1)
+        got.append([p.data for p in b.finish()])
+        if t + 1 < len(frames):
+            b.launch()
+    assert got == ref
