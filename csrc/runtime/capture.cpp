@@ -116,12 +116,16 @@ class CaptureSession {
         wm_loc_ = location;
     }
 
+    // out: frames, mean encode ms, bytes, packets, source kind, last encode ms, then
+    // the per-frame encode-time histogram: counts for le = kHistLe[i] ms and +Inf.
+    static constexpr int kHist = 9;
+    static constexpr double kHistLe[kHist - 1] = {0.25, 0.5, 1, 2, 4, 8, 16, 33};
     void stats(double* out, int n) {
         std::lock_guard<std::mutex> g(mu_);
-        double v[6] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
-                       (double)packets_, src_kind_,
-                       last_enc_ms_};
-        for (int i = 0; i < n && i < 6; i++) out[i] = v[i];
+        double v[6 + kHist] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
+                               (double)packets_, src_kind_, last_enc_ms_};
+        for (int i = 0; i < kHist; i++) v[6 + i] = (double)hist_[i];
+        for (int i = 0; i < n && i < 6 + kHist; i++) out[i] = v[i];
     }
 
    private:
@@ -167,6 +171,9 @@ class CaptureSession {
                 {
                     std::lock_guard<std::mutex> g(mu_);
                     frames_++;
+                    int b = 0;
+                    while (b < kHist - 1 && ms > kHistLe[b]) b++;
+                    hist_[b]++;
                     enc_ms_sum_ += ms;
                     last_enc_ms_ = ms;
                     bytes_ += bytes;
@@ -231,6 +238,7 @@ class CaptureSession {
     std::thread th_;
     std::atomic<bool> running_{false}, key_req_{false};
     std::atomic<int> qp_req_{0};
+    uint64_t hist_[kHist] = {};
     double src_kind_ = -1.0;  // 1 x11, 0 synthetic, -1 none (kept after stop for stats)
     std::mutex mu_;
     uint64_t frames_ = 0, bytes_ = 0, packets_ = 0;

@@ -23,6 +23,7 @@ import threading
 from selkies_gstreamer_amd.ops import native as _native
 
 CaptureSettings = _native.SkCaptureSettings
+ENCODE_MS_BUCKETS = (0.25, 0.5, 1, 2, 4, 8, 16, 33, float("inf"))   # csrc/runtime/capture.cpp kHistLe
 StripeEncodeResult = _native.SkStripeResult
 StripeCallback = _native.SK_STRIPE_CB
 
@@ -111,11 +112,13 @@ class ScreenCapture:
             self._lib.sk_capture_set_qp(self._h, int(qp), int(paint_qp))
 
     def stats(self) -> dict:
-        arr = (ctypes.c_double * 6)()
-        self._lib.sk_capture_stats(self._h, arr, 6)
+        arr = (ctypes.c_double * 15)()
+        self._lib.sk_capture_stats(self._h, arr, 15)
         return {"frames": int(arr[0]), "encode_ms_mean": arr[1], "bytes": int(arr[2]),
                 "packets": int(arr[3]), "source": {1.0: "x11", 0.0: "synthetic"}.get(arr[4], "none"),
-                "encode_ms_last": arr[5]}
+                "encode_ms_last": arr[5],
+                # per-frame encode time histogram (native, bucket upper bounds in ms; last = +Inf)
+                "encode_ms_buckets": list(ENCODE_MS_BUCKETS), "encode_ms_counts": [int(x) for x in arr[6:15]]}
 
     def close(self) -> None:
         self.stop_capture()

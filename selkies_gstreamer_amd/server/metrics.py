@@ -27,6 +27,34 @@ except ImportError:  # pragma: no cover
     HAVE_PROM = False
 
 
+class _EncodeHistogram:
+    """Prometheus histogram of per-frame encode time per display, from the native
+    capture session's bucket counters (no per-frame Python work)."""
+
+    def __init__(self, metrics: "Metrics"):
+        self.m = metrics
+
+    def describe(self):
+        return []
+
+    def collect(self):
+        from prometheus_client.core import HistogramMetricFamily
+        fam = HistogramMetricFamily("selkies_encode_seconds", "Per-frame encode time (capture -> packets)",
+                                    labels=["display"])
+        for did, module in list(self.m.captures.items()):
+            try:
+                st = module.stats()
+                les, counts = st["encode_ms_buckets"], st["encode_ms_counts"]
+            except Exception:
+                continue
+            cum, buckets = 0, []
+            for le, c in zip(les, counts):
+                cum += c
+                buckets.append(("+Inf" if le == float("inf") else str(le / 1e3), cum))
+            fam.add_metric([did], buckets, sum_value=st["encode_ms_mean"] * st["frames"] / 1e3)
+        yield fam
+
+
 class Metrics:
     def __init__(self, server=None, csv_path: Optional[str] = None):
         self.server = server
@@ -46,6 +74,7 @@ class Metrics:
             self.frames = Gauge("selkies_frames_total", "Frames encoded", ["display"], registry=r)
             self.bytes = Gauge("selkies_bytes_total", "Bytes produced by the encoder", ["display"], registry=r)
             self.clients = Gauge("selkies_clients", "Connected websocket clients", registry=r)
+            r.register(_EncodeHistogram(self))
 
     # capture lifecycle hooks (called by DataStreamingServer)
     def capture_started(self, did: str, module):

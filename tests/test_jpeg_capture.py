@@ -119,6 +119,25 @@ def test_capture_session_h264_synthetic():
         dec.feed(data)
         n += 1
     assert n == st["packets"]
+    assert sum(st["encode_ms_counts"]) == st["frames"]   # native per-frame encode histogram
+
+
+def test_encode_histogram_reaches_prometheus():
+    import pixelflux
+    from prometheus_client import generate_latest
+    from selkies_gstreamer_amd.server.metrics import Metrics
+    s = pixelflux.default_settings(256, 128, use_cpu=1, source=2, target_fps=30.0, stripe_height=64)
+    cap = pixelflux.ScreenCapture()
+    cap.start_capture(s, lambda r, u: None)
+    import time
+    time.sleep(0.4)
+    cap.stop_capture()
+    m = Metrics()
+    m.capture_started("primary", cap)
+    text = generate_latest(m.registry).decode()
+    cap.close()
+    assert 'selkies_encode_seconds_bucket{display="primary",le="+Inf"}' in text
+    assert "selkies_encode_seconds_count" in text
 
 
 def test_capture_session_jpeg_synthetic():
