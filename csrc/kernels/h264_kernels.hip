@@ -1240,6 +1240,7 @@ __global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
 __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
     __shared__ uint32_t bits_w[4][kMbSlotBytes / 4];
     __shared__ int16_t coef_w[4][kCoefPerMb];
+    __shared__ MbInfo mb_w[4];   // the MB's info in LDS: nnz[] is indexed per lane (a private copy would spill)
     __shared__ CavlcTables T;
     load_cavlc_tables(T, a.cavlc_tabs);
     __syncthreads();
@@ -1253,7 +1254,10 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
     const SliceTask t = a.tasks[s];
     if (t.final_action != ACT_P && t.final_action != ACT_I) return;
     int l = lane_id();
-    const MbInfo mb = a.mbs[idx];
+    MbInfo& mb = mb_w[threadIdx.x >> 6];
+    if (l < (int)(sizeof(MbInfo) / 4))
+        reinterpret_cast<uint32_t*>(&mb)[l] = reinterpret_cast<const uint32_t*>(a.mbs + idx)[l];
+    wave_sync();
     if (mb.type == MB_P_SKIP) {
         if (l == 0) a.mb_nbits[idx] = 0;
         return;
