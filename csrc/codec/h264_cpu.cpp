@@ -161,7 +161,15 @@ void CpuH264Encoder::motion_search(int s) {
             if (mby - 1 >= t.pic_row0) add(mbx, mby - 1);
             if (mby + 1 < t.pic_row0 + t.pic_rows) add(mbx, mby + 1);
             if (cfg.me_full && mb_dirty[idx]) {
-                full_search(mbx, mby, t, &fs_mv[2 * idx]);
+                // the MB's previous vector already matches exactly (scrolls, moving windows):
+                // nothing can beat it, skip the exhaustive search
+                const int px = sk_clip(mvfield[2 * idx], -R, R), py = sk_clip(mvfield[2 * idx + 1], -R, R);
+                if (sad_at(mbx, mby, px, py, t) == 0) {
+                    fs_mv[2 * idx] = (int16_t)px;
+                    fs_mv[2 * idx + 1] = (int16_t)py;
+                } else {
+                    full_search(mbx, mby, t, &fs_mv[2 * idx]);
+                }
                 cx[n] = sk_clip(fs_mv[2 * idx], -R, R);
                 cy[n] = sk_clip(fs_mv[2 * idx + 1], -R, R);
                 n++;

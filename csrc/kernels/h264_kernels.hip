@@ -427,10 +427,23 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
     const int mbx = idx % a.mb_w, mby = idx / a.mb_w;
     const SliceTask t = a.tasks[mby / a.rows_per_slice];
     if (t.action != ACT_P || !a.mb_dirty[idx]) return;
+    const int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    {   // exact match at the MB's previous vector: skip the search (CPU: same rule)
+        const int R = a.me_range;
+        const int px = sk_clip(a.mvfield[2 * idx], -R, R), py = sk_clip(a.mvfield[2 * idx + 1], -R, R);
+        const uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + (l >> 2)) * a.stride_y +
+                                                               mbx * 16 + (l & 3) * 4);
+        if (me_sad(a, a.ref.y, sw, mbx, mby, px, py, ylo, yhi) == 0) {
+            if (l == 0) {
+                a.fs_mv[2 * idx] = (int16_t)px;
+                a.fs_mv[2 * idx + 1] = (int16_t)py;
+            }
+            return;
+        }
+    }
     uint32_t* win = win_s[w];
     uint32_t* blk = blk_s[w];
     int* sq = sq_s[w];
-    const int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
     for (int i = l; i < kFsWin * WW; i += 64) {
         const int wy = i / WW, q = i - wy * WW;
         const int y = sk_clip(mby * 16 - kFsR + wy, ylo, yhi);
