@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
     constexpr int WW = kFsWin / 4;                       // window dwords per row (12)
     __shared__ uint32_t win_s[4][kFsWin * WW];           // raw reference window per wave
     __shared__ uint32_t blk_s[4][64];                    // raw 16x16 source block
-    __shared__ int sq_s[4][kFsWin * 2 * kFsR];           // row box sums of w'^2, then |r_d|^2
+    __shared__ __align__(16) int sq_s[4][kFsWin * 2 * kFsR];   // row box sums of w'^2, then |r_d|^2
     const int w = threadIdx.x >> 6, l = lane_id();
     const int nmb = a.mb_w * a.mb_h;
     const int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + w;
@@ -452,31 +452,46 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
     blk[l] = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + (l >> 2)) * a.stride_y + mbx * 16 +
                                                 (l & 3) * 4);
     wave_sync();
-    // |r_d|^2: 16-tap row box sums (lane = window row), then 16-tap column sums in place
+    // |r_d|^2: 16-tap row box sums (lane = window row), then 16-tap column sums in
+    // place. Each lane loads its whole row / column into registers before it stores
+    // anything: no LDS read waits behind an earlier store (a read-modify-write
+    // sliding loop over LDS serialised ~60 round trips per wave).
     if (l < kFsWin) {
-        const uint8_t* row = reinterpret_cast<const uint8_t*>(win + l * WW);
+        uint32_t rw[WW];
+#pragma unroll
+        for (int q = 0; q < WW; q++) rw[q] = win[l * WW + q];
+        int sqv[kFsWin];
+#pragma unroll
+        for (int c = 0; c < kFsWin; c++) {
+            const int v = (int)((rw[c >> 2] >> (8 * (c & 3))) & 255) - 128;
+            sqv[c] = v * v;
+        }
         int acc = 0;
 #pragma unroll
-        for (int c = 0; c < 16; c++) {
-            const int v = (int)row[c] - 128;
-            acc += v * v;
-        }
-        sq[l * 2 * kFsR] = acc;
+        for (int c = 0; c < 16; c++) acc += sqv[c];
+        int out[2 * kFsR];
+        out[0] = acc;
+#pragma unroll
         for (int x = 1; x < 2 * kFsR; x++) {
-            const int vo = (int)row[x - 1] - 128, vn = (int)row[x + 15] - 128;
-            acc += vn * vn - vo * vo;
-            sq[l * 2 * kFsR + x] = acc;
+            acc += sqv[x + 15] - sqv[x - 1];
+            out[x] = acc;
         }
+#pragma unroll
+        for (int x = 0; x < 2 * kFsR; x += 4)
+            *reinterpret_cast<int4*>(&sq[l * 2 * kFsR + x]) = make_int4(out[x], out[x + 1], out[x + 2], out[x + 3]);
     }
     wave_sync();
     if (l < 2 * kFsR) {
+        int col[kFsWin];
+#pragma unroll
+        for (int r = 0; r < kFsWin; r++) col[r] = sq[r * 2 * kFsR + l];
         int acc = 0;
 #pragma unroll
-        for (int r = 0; r < 16; r++) acc += sq[r * 2 * kFsR + l];
+        for (int r = 0; r < 16; r++) acc += col[r];
+#pragma unroll
         for (int dy = 0; dy < 2 * kFsR; dy++) {
-            const int old = sq[dy * 2 * kFsR + l], nw = sq[(dy + 16) * 2 * kFsR + l];
             sq[dy * 2 * kFsR + l] = acc;
-            acc += nw - old;
+            acc += col[dy + 16] - col[dy];
         }
     }
     // cross-correlation on MFMA: lane (i = l & 15, g = l >> 4)
