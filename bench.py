@@ -58,6 +58,7 @@ def parse():
     p.add_argument("--bands", type=int, default=1,
                    help="encode each session's frame as N bands of stripes on this GPU (parallel/banded.py): "
                         "byte-identical output, upload overlapped with encoding")
+    p.add_argument("--num-refs", type=int, default=1, help="H.264 reference pictures (1 or 2, sliding window)")
     p.add_argument("--overlap", type=int, default=0,
                    help="1: upload frame n+1 while frame n encodes (upload/finish/launch); latency is "
                         "measured from the frame's upload to its packets")
@@ -113,7 +114,7 @@ def main():
         else:
             encs = [H264Encoder(W, H, stripe_height=args.stripe_height, fullframe=args.mode == "fullframe",
                                 qp=args.qp, use_paint_over=False, device=local_rank, backend=args.backend,
-                                deblock=bool(args.deblock), me_full=bool(args.me_full))
+                                deblock=bool(args.deblock), me_full=bool(args.me_full), num_refs=args.num_refs)
                     for _ in range(S)]
 
     lat = [[] for _ in range(S)]
@@ -230,6 +231,7 @@ def main():
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
                 "bands_per_session": args.bands,
                 "upload_overlap": bool(args.overlap),
+                "num_refs": args.num_refs,
                 "numa_node_rank0": numa_node,
             },
         }

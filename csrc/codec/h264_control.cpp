@@ -44,10 +44,10 @@ bool Controller::picture_is_idr(const SliceTask* tasks) const {
 
 void Controller::commit(const SliceTask* tasks) {
     if (cfg_.fullframe) {
-        commit_picture(pic_, picture_is_idr(tasks));
+        commit_picture(pic_, picture_is_idr(tasks), plan_config(cfg_).num_refs);
         return;
     }
-    for (int s = 0; s < g_.num_slices; s++) commit_stripe(st_[s], tasks[s].final_action);
+    for (int s = 0; s < g_.num_slices; s++) commit_stripe(st_[s], tasks[s].final_action, plan_config(cfg_).num_refs);
 }
 
 // ---------------------------------------------------------------------------
@@ -99,7 +99,7 @@ static void rbsp_trailing(BitWriter& w) {
 }
 
 void build_parameter_sets(int width, int height, int full_range, float fps,
-                          std::vector<uint8_t>& out) {
+                          std::vector<uint8_t>& out, int num_refs) {
     int mb_w = (width + 15) / 16, mb_h = (height + 15) / 16;
     uint8_t buf[128];
     memset(buf, 0, sizeof(buf));
@@ -110,7 +110,7 @@ void build_parameter_sets(int width, int height, int full_range, float fps,
     put_ue(w, 0);          // seq_parameter_set_id
     put_ue(w, kLog2MaxFrameNum - 4);
     put_ue(w, 2);          // pic_order_cnt_type
-    put_ue(w, 1);          // max_num_ref_frames
+    put_ue(w, (uint32_t)(num_refs > 1 ? 2 : 1));   // max_num_ref_frames (sliding window)
     w.put(0, 1);           // gaps_in_frame_num_value_allowed_flag
     put_ue(w, (uint32_t)(mb_w - 1));
     put_ue(w, (uint32_t)(mb_h - 1));

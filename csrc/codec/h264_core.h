@@ -38,7 +38,8 @@ struct MbInfo {
     uint8_t cbp;             // bits 0..3 luma 8x8, bits 4..5 chroma (0,1,2)
     uint8_t qp;              // QP used for quantisation
     uint8_t nnz[24];         // TotalCoeff per block: 16 luma (blkIdx), 4 Cb, 4 Cr
-    uint8_t pad[3];
+    uint8_t ref;             // ref_idx_l0 (P_L0_16x16)
+    uint8_t pad[2];
 };
 static_assert(sizeof(MbInfo) == 40, "MbInfo layout");
 
@@ -355,26 +356,25 @@ SK_HD int nc_from(bool availA, int nA, bool availB, int nB) {
 // Motion-vector prediction for a 16x16 partition with one reference (8.4.1.3).
 struct MvNb {
     bool avail;   // neighbour macroblock exists in this slice (already coded)
-    bool inter;   // neighbour is an inter MB (refIdx 0)
+    int ref;      // its refIdxL0; -1 when unavailable or intra
     int mvx, mvy;
 };
 
-SK_HD void mv_pred16x16(MvNb A, MvNb B, MvNb C, int* px, int* py) {
-    // unavailable/intra -> refIdx -1, mv 0
-    int rA = (A.avail && A.inter) ? 0 : -1, rB = (B.avail && B.inter) ? 0 : -1,
-        rC = (C.avail && C.inter) ? 0 : -1;
-    int ax = rA == 0 ? A.mvx : 0, ay = rA == 0 ? A.mvy : 0;
-    int bx = rB == 0 ? B.mvx : 0, by = rB == 0 ? B.mvy : 0;
-    int cx = rC == 0 ? C.mvx : 0, cy = rC == 0 ? C.mvy : 0;
+// mvpLX of a 16x16 partition with refIdx `ref` (8.4.1.3, 8.4.1.3.1).
+SK_HD void mv_pred16x16(MvNb A, MvNb B, MvNb C, int ref, int* px, int* py) {
+    int rA = A.avail ? A.ref : -1, rB = B.avail ? B.ref : -1, rC = C.avail ? C.ref : -1;
+    int ax = rA >= 0 ? A.mvx : 0, ay = rA >= 0 ? A.mvy : 0;
+    int bx = rB >= 0 ? B.mvx : 0, by = rB >= 0 ? B.mvy : 0;
+    int cx = rC >= 0 ? C.mvx : 0, cy = rC >= 0 ? C.mvy : 0;
     if (!B.avail && !C.avail && A.avail) {
         bx = cx = ax;
         by = cy = ay;
         rB = rC = rA;
     }
-    int matches = (rA == 0) + (rB == 0) + (rC == 0);
+    int matches = (rA == ref) + (rB == ref) + (rC == ref);
     if (matches == 1) {
-        if (rA == 0) { *px = ax; *py = ay; }
-        else if (rB == 0) { *px = bx; *py = by; }
+        if (rA == ref) { *px = ax; *py = ay; }
+        else if (rB == ref) { *px = bx; *py = by; }
         else { *px = cx; *py = cy; }
         return;
     }
@@ -382,12 +382,12 @@ SK_HD void mv_pred16x16(MvNb A, MvNb B, MvNb C, int* px, int* py) {
     *py = sk_median(ay, by, cy);
 }
 
-// P_Skip motion vector (8.4.1.1).
+// P_Skip motion vector (8.4.1.1): refIdx 0.
 SK_HD void mv_pskip(MvNb A, MvNb B, MvNb C, int* px, int* py) {
     if (!A.avail || !B.avail) { *px = 0; *py = 0; return; }
-    if (A.inter && A.mvx == 0 && A.mvy == 0) { *px = 0; *py = 0; return; }
-    if (B.inter && B.mvx == 0 && B.mvy == 0) { *px = 0; *py = 0; return; }
-    mv_pred16x16(A, B, C, px, py);
+    if (A.ref == 0 && A.mvx == 0 && A.mvy == 0) { *px = 0; *py = 0; return; }
+    if (B.ref == 0 && B.mvx == 0 && B.mvy == 0) { *px = 0; *py = 0; return; }
+    mv_pred16x16(A, B, C, 0, px, py);
 }
 
 // ---------------------------------------------------------------------------

@@ -24,6 +24,7 @@ CpuH264Encoder::CpuH264Encoder(const EncoderConfig& c) : cfg(c) {
         src[p].assign(n, 0);
         prev[p].assign(n, 0);
         ref[p].assign(n, 0);
+        ref1[p].assign(n, 0);
         rec[p].assign(n, 0);
     }
     mb_dirty.assign(g.num_mbs(), 1);
@@ -37,11 +38,11 @@ CpuH264Encoder::CpuH264Encoder(const EncoderConfig& c) : cfg(c) {
     tasks.assign(g.num_slices, SliceTask());
     if (cfg.fullframe) {
         param_sets.resize(1);
-        build_parameter_sets(g.W, g.H, cfg.full_range, cfg.fps, param_sets[0]);
+        build_parameter_sets(g.W, g.H, cfg.full_range, cfg.fps, param_sets[0], cfg.num_refs);
     } else {
         param_sets.resize(g.num_slices);
         for (int s = 0; s < g.num_slices; s++)
-            build_parameter_sets(g.W, g.slice_pix_h(s), cfg.full_range, cfg.fps, param_sets[s]);
+            build_parameter_sets(g.W, g.slice_pix_h(s), cfg.full_range, cfg.fps, param_sets[s], cfg.num_refs);
     }
 }
 
@@ -90,14 +91,14 @@ void CpuH264Encoder::load_frame(const uint8_t* bgrx, int stride) {
         }
 }
 
-int CpuH264Encoder::sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t) const {
+int CpuH264Encoder::sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t, int refi) const {
     int y_lo = t.pic_row0 * 16, y_hi = (t.pic_row0 + t.pic_rows) * 16 - 1;
     int x_hi = g.stride_y - 1;
     int sad = 0;
     for (int y = 0; y < 16; y++) {
         int sy = sk_clip(mby * 16 + y + dy, y_lo, y_hi);
         const uint8_t* s = &src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16];
-        const uint8_t* r = &ref[0][(size_t)sy * g.stride_y];
+        const uint8_t* r = &refs(refi)[0][(size_t)sy * g.stride_y];
         for (int x = 0; x < 16; x++) {
             int sx = sk_clip(mbx * 16 + x + dx, 0, x_hi);
             sad += sk_abs((int)s[x] - (int)r[sx]);
@@ -201,10 +202,22 @@ void CpuH264Encoder::motion_search(int s) {
             for (int y = 0; y < 16; y++)
                 for (int x = 0; x < 16; x++)
                     dev += sk_abs((int)src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x] - mean);
+            int refi = 0;
+            if (t.num_refs > 1 && mb_dirty[idx]) {
+                // second reference at the zero vector (a window or caret returning to the
+                // state of two pictures ago): worth it when SAD + lambda * 3 bits wins
+                const int s1 = sad_at(mbx, mby, 0, 0, t, 1);
+                if (s1 + 3 * lam < bcost) {
+                    bx = by = 0;
+                    bsad = s1;
+                    refi = 1;
+                }
+            }
             me[idx].mvx = (int16_t)bx;
             me[idx].mvy = (int16_t)by;
             me[idx].sad = bsad;
             me[idx].intra_est = dev;
+            me[idx].ref = refi;
         }
 }
 
@@ -222,24 +235,24 @@ void CpuH264Encoder::decide_scenecut(int s) {
 }
 
 void CpuH264Encoder::mc_luma(int mbx, int mby, int mvx, int mvy, const SliceTask& t,
-                             uint8_t* pred) const {
+                             uint8_t* pred, int refi) const {
     int y_lo = t.pic_row0 * 16, y_hi = (t.pic_row0 + t.pic_rows) * 16 - 1;
     int dx = mvx >> 2, dy = mvy >> 2;  // integer-pel vectors only
     for (int y = 0; y < 16; y++) {
         int sy = sk_clip(mby * 16 + y + dy, y_lo, y_hi);
         for (int x = 0; x < 16; x++) {
             int sx = sk_clip(mbx * 16 + x + dx, 0, g.stride_y - 1);
-            pred[y * 16 + x] = ref[0][(size_t)sy * g.stride_y + sx];
+            pred[y * 16 + x] = refs(refi)[0][(size_t)sy * g.stride_y + sx];
         }
     }
 }
 
 void CpuH264Encoder::mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTask& t,
-                               uint8_t* pu, uint8_t* pv) const {
+                               uint8_t* pu, uint8_t* pv, int refi) const {
     int h = t.pic_rows * 8;
     int y0 = t.pic_row0 * 8;
     for (int c = 0; c < 2; c++) {
-        const uint8_t* base = &ref[1 + c][(size_t)y0 * g.stride_c];
+        const uint8_t* base = &refs(refi)[1 + c][(size_t)y0 * g.stride_c];
         uint8_t* o = c ? pv : pu;
         for (int y = 0; y < 8; y++)
             for (int x = 0; x < 8; x++)
@@ -256,10 +269,11 @@ void CpuH264Encoder::code_slice_inter(int s) {
             MbInfo& mb = mbs[idx];
             memset(&mb, 0, sizeof(mb));
             int mvx = 4 * me[idx].mvx, mvy = 4 * me[idx].mvy;
+            const int refi = me[idx].ref;
             auto nbr = [&](int ox, int oy, bool ok) {
                 MvNb n;
                 n.avail = ok;
-                n.inter = ok;
+                n.ref = ok ? me[oy * g.mb_w + ox].ref : -1;
                 n.mvx = ok ? 4 * me[oy * g.mb_w + ox].mvx : 0;
                 n.mvy = ok ? 4 * me[oy * g.mb_w + ox].mvy : 0;
                 return n;
@@ -270,7 +284,7 @@ void CpuH264Encoder::code_slice_inter(int s) {
             MvNb C = nbr(mbx + 1, mby - 1, top && mbx + 1 < g.mb_w);
             if (!C.avail) C = nbr(mbx - 1, mby - 1, top && mbx > 0);
             int pmx, pmy, smx, smy;
-            mv_pred16x16(A, B, C, &pmx, &pmy);
+            mv_pred16x16(A, B, C, refi, &pmx, &pmy);
             mv_pskip(A, B, C, &smx, &smy);
 
             uint8_t sy[256], su[64], sv[64], py[256], pu[64], pv[64];
@@ -280,8 +294,8 @@ void CpuH264Encoder::code_slice_inter(int s) {
                 memcpy(su + y * 8, &src[1][(size_t)(mby * 8 + y) * g.stride_c + mbx * 8], 8);
                 memcpy(sv + y * 8, &src[2][(size_t)(mby * 8 + y) * g.stride_c + mbx * 8], 8);
             }
-            mc_luma(mbx, mby, mvx, mvy, t, py);
-            mc_chroma(mbx, mby, mvx, mvy, t, pu, pv);
+            mc_luma(mbx, mby, mvx, mvy, t, py, refi);
+            mc_chroma(mbx, mby, mvx, mvy, t, pu, pv, refi);
             MbTransform tr;
             residual_transform(sy, py, su, pu, sv, pv, tr);
             int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
@@ -289,7 +303,8 @@ void CpuH264Encoder::code_slice_inter(int s) {
             int qp = quant_mb_with_budget(tr, t.qp, false, mb, coef, host_cavlc_tables());
             mb.mvx = (int16_t)mvx;
             mb.mvy = (int16_t)mvy;
-            if (mb.cbp == 0 && mvx == smx && mvy == smy) {
+            mb.ref = (uint8_t)refi;
+            if (mb.cbp == 0 && refi == 0 && mvx == smx && mvy == smy) {
                 mb.type = MB_P_SKIP;
             } else {
                 mb.mvdx = (int16_t)(mvx - pmx);
@@ -316,6 +331,7 @@ void CpuH264Encoder::code_slice_intra(int s) {
             MbInfo& mb = mbs[idx];
             memset(&mb, 0, sizeof(mb));
             me[idx].mvx = me[idx].mvy = 0;
+            me[idx].ref = 0;
             bool aT = mby > t.first_row, aL = mbx > 0;
             uint8_t top[16] = {0}, left[16] = {0}, ctop[2][8] = {{0}}, cleft[2][8] = {{0}};
             int tl = 0, ctl[2] = {0, 0};
@@ -408,6 +424,7 @@ void CpuH264Encoder::code_slice_skipall(int s) {
             int idx = mby * g.mb_w + mbx;
             memset(&mbs[idx], 0, sizeof(MbInfo));
             me[idx].mvx = me[idx].mvy = 0;
+            me[idx].ref = 0;
         }
     int y0 = t.first_row * 16, y1 = (t.first_row + t.num_rows) * 16;
     memcpy(&rec[0][(size_t)y0 * g.stride_y], &ref[0][(size_t)y0 * g.stride_y], (size_t)(y1 - y0) * g.stride_y);
@@ -435,6 +452,7 @@ std::vector<uint8_t> CpuH264Encoder::write_slice(int s) {
     h.idr_pic_id = t.idr_pic_id;
     h.slice_qp = t.qp;
     h.deblock = cfg.deblock;
+    h.num_refs = intra ? 1 : t.num_refs;
     write_slice_header(w, h);
     if (t.final_action == ACT_SKIPALL) {
         put_ue(w, (uint32_t)nmb);
@@ -448,7 +466,7 @@ std::vector<uint8_t> CpuH264Encoder::write_slice(int s) {
                 if (!intra) { put_ue(w, (uint32_t)skip_run); skip_run = 0; }
                 int dq = 0;
                 if (mb_has_qp_delta(mb)) { dq = mb.qp - qp_prev; qp_prev = mb.qp; }
-                write_mb_header(w, mb, !intra, dq);
+                write_mb_header(w, mb, !intra, dq, intra ? 1 : t.num_refs);
                 MbNeighbours nb;
                 mb_neighbours(mbx, mby, t.first_row, nb);
                 write_mb_residual(w, mb, nb, &coefs[(size_t)idx * kCoefPerMb], host_cavlc_tables());
@@ -495,6 +513,15 @@ void CpuH264Encoder::package(uint16_t frame_id, std::vector<std::vector<uint8_t>
 void CpuH264Encoder::finish_frame() {
     for (int s = 0; s < g.num_slices; s++) {
         const SliceTask& t = tasks[s];
+        const int y0 = t.first_row * 16, y1 = (t.first_row + t.num_rows) * 16;
+        if (cfg.num_refs > 1 && t.final_action != ACT_NONE) {
+            // sliding window: the picture before the one being added becomes reference 1
+            // (a skip-all picture is a reference too: ref 1 = the old ref 0 = its content)
+            memcpy(&ref1[0][(size_t)y0 * g.stride_y], &ref[0][(size_t)y0 * g.stride_y], (size_t)(y1 - y0) * g.stride_y);
+            for (int p = 1; p < 3; p++)
+                memcpy(&ref1[p][(size_t)(y0 / 2) * g.stride_c], &ref[p][(size_t)(y0 / 2) * g.stride_c],
+                       (size_t)(y1 - y0) / 2 * g.stride_c);
+        }
         if (t.final_action == ACT_NONE || t.final_action == ACT_SKIPALL) {
             if (t.final_action == ACT_SKIPALL)
                 for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
@@ -504,7 +531,6 @@ void CpuH264Encoder::finish_frame() {
                     }
             continue;
         }
-        int y0 = t.first_row * 16, y1 = (t.first_row + t.num_rows) * 16;
         memcpy(&ref[0][(size_t)y0 * g.stride_y], &rec[0][(size_t)y0 * g.stride_y], (size_t)(y1 - y0) * g.stride_y);
         for (int p = 1; p < 3; p++)
             memcpy(&ref[p][(size_t)(y0 / 2) * g.stride_c], &rec[p][(size_t)(y0 / 2) * g.stride_c],

@@ -59,7 +59,7 @@ inline const DbTables& host_db_tables() {
 
 // What the filter needs to know about one macroblock (8 bytes, shared CPU/GPU layout).
 struct DbInfo {
-    uint8_t intra;     // 1 for I16x16
+    uint8_t intra;     // bit 0: I16x16; bits 1+: ref_idx (bS 1 across different reference pictures)
     uint8_t qpy;       // QP_Y as the decoder derives it (mb_qp_delta chain, 7.4.5)
     uint16_t nz;       // bit (by*4+bx): luma 4x4 block at raster (bx,by) has coded coefficients
     int16_t mvx, mvy;  // quarter-pel
@@ -68,7 +68,7 @@ static_assert(sizeof(DbInfo) == 8, "DbInfo layout");
 
 SK_HD DbInfo db_info(const MbInfo& mb, int qpy) {
     DbInfo d;
-    d.intra = mb.type == MB_I16x16 ? 1 : 0;
+    d.intra = (uint8_t)((mb.type == MB_I16x16 ? 1 : 0) | (mb.type == MB_I16x16 ? 0 : mb.ref << 1));
     d.qpy = (uint8_t)qpy;
     uint32_t nz = 0;
     for (int b = 0; b < 16; b++)
@@ -81,8 +81,9 @@ SK_HD DbInfo db_info(const MbInfo& mb, int qpy) {
 
 // Boundary strength (8.7.2.1) between blocks pb (in MB p) and qb (in MB q), raster 4x4 indices.
 SK_HD int db_bs(const DbInfo& p, const DbInfo& q, bool mb_edge, int pb, int qb) {
-    if (p.intra || q.intra) return mb_edge ? 4 : 3;
+    if ((p.intra & 1) || (q.intra & 1)) return mb_edge ? 4 : 3;
     if (((p.nz >> pb) & 1) || ((q.nz >> qb) & 1)) return 2;
+    if ((p.intra >> 1) != (q.intra >> 1)) return 1;   // different reference pictures
     if (sk_abs(p.mvx - q.mvx) >= 4 || sk_abs(p.mvy - q.mvy) >= 4) return 1;
     return 0;
 }

@@ -40,6 +40,8 @@ struct EncoderConfig {
     int deblock = 0;             // in-loop deblocking filter (idc 2: inside each slice); off = x264 ultrafast
     int me_full = 1;             // +-16 exhaustive MFMA search candidate (dirty MBs of P slices)
     int shared_copy = 0;         // HIP: uploads on the device's shared copy stream (in submit order)
+    int num_refs = 1;            // reference frames per stream (sliding-window DPB): 1, or 2 for the
+                                 // previous-but-one picture as a second P reference (blinking/toggling UI)
     int src_width = 0;           // K2: capture size when it differs from width x height (0 = same);
     int src_height = 0;          //     the frame is resampled (bilinear) inside the K1 conversion
 };
@@ -92,7 +94,7 @@ struct SliceTask {
     int32_t allow_scenecut;
     int32_t idr_on_intra;  // striped mode: an I decision makes the stripe an IDR
     int32_t final_action;  // written by the backend (scene-cut may turn P into I)
-    int32_t pad;
+    int32_t num_refs;      // P: reference pictures available to this slice (1..EncoderConfig::num_refs)
 };
 static_assert(sizeof(SliceTask) == 48, "SliceTask layout");
 
@@ -105,17 +107,19 @@ struct StripeState {
     int hot_left = 0;
     int paint_left = 0;
     bool painted = true;   // nothing to paint before the first change
+    int refs = 0;          // pictures in the decoder's DPB for this stream (sliding window)
 };
 
 // Controller knobs as a POD, so the same plan code runs on the host (CPU
 // backend) and inside the HIP graph (k_plan), bit-for-bit the same decisions.
 struct PlanConfig {
     int32_t fullframe, scenecut, use_paint_over, paint_over_trigger, paint_over_burst;
-    int32_t damage_threshold, damage_duration, streaming_mode, qp, paint_qp;
+    int32_t damage_threshold, damage_duration, streaming_mode, qp, paint_qp, num_refs;
 };
 inline PlanConfig plan_config(const EncoderConfig& c) {
     return PlanConfig{c.fullframe, c.scenecut, c.use_paint_over, c.paint_over_trigger, c.paint_over_burst,
-                      c.damage_threshold, c.damage_duration, c.streaming_mode, c.qp, c.paint_qp};
+                      c.damage_threshold, c.damage_duration, c.streaming_mode, c.qp, c.paint_qp,
+                      c.num_refs > 1 ? 2 : 1};
 }
 constexpr int kFrameNumMask = (1 << 16) - 1;  // log2_max_frame_num = 16 (h264_syntax.h)
 
@@ -170,28 +174,34 @@ SK_HD void plan_stripe(const PlanConfig& c, StripeState& st, const StripeState& 
         t.frame_num = st.frame_num;
         t.idr_pic_id = st.idr_pic_id;
     }
+    const int refs = ff ? pic.refs : st.refs;
+    t.num_refs = refs < 1 ? 1 : (refs < c.num_refs ? refs : c.num_refs);
     t.final_action = t.action;
 }
 
 // Striped mode: stripe state after its slice was coded with `final_action`.
-SK_HD void commit_stripe(StripeState& st, int final_action) {
+SK_HD void commit_stripe(StripeState& st, int final_action, int max_refs) {
     if (final_action == ACT_I) {
         st.frame_num = 1;
         st.idr_pic_id = (st.idr_pic_id + 1) & 0xffff;
         st.need_idr = false;
+        st.refs = 1;
     } else if (final_action == ACT_P) {
         st.frame_num = (st.frame_num + 1) & kFrameNumMask;
+        st.refs = st.refs + 1 < max_refs ? st.refs + 1 : max_refs;
     }
 }
 
 // Full-frame mode: picture state after a picture (IDR iff every slice was an IDR slice).
-SK_HD void commit_picture(StripeState& pic, bool idr) {
+SK_HD void commit_picture(StripeState& pic, bool idr, int max_refs) {
     if (idr) {
         pic.frame_num = 1;
         pic.idr_pic_id = (pic.idr_pic_id + 1) & 0xffff;
         pic.need_idr = false;
+        pic.refs = 1;
     } else {
         pic.frame_num = (pic.frame_num + 1) & kFrameNumMask;
+        pic.refs = pic.refs + 1 < max_refs ? pic.refs + 1 : max_refs;
     }
 }
 
@@ -235,10 +245,11 @@ class Controller {
 // identical for the CPU and HIP backends (so a session can move between GPUs, or
 // between a GPU and the CPU reference, without an IDR):
 //   StateHeader | StripeState[num_slices + 1] (committed; last = picture state) |
-//   ref Y U V | last source Y U V (damage baseline) | mvfield int16[2 * num_mbs]
+//   ref Y U V | ref1 Y U V (second reference) | last source Y U V (damage baseline) |
+//   mvfield int16[2 * num_mbs]
 struct StateHeader {
     char magic[4];          // "SKH4"
-    int32_t version;        // 1
+    int32_t version;        // 2 (ref1 planes)
     int32_t W, H, stripe_height, fullframe, num_slices;
     int32_t started;        // a frame has been encoded (else the next one is all-dirty)
     int32_t qp, paint_qp;   // rate-control QPs in force
@@ -250,14 +261,14 @@ inline size_t state_plane_bytes(const Geometry& g) {
     return (size_t)g.stride_y * g.plane_h_y + 2 * (size_t)g.stride_c * g.plane_h_c;
 }
 inline size_t state_bytes(const Geometry& g) {
-    return sizeof(StateHeader) + sizeof(StripeState) * (size_t)(g.num_slices + 1) + 2 * state_plane_bytes(g) +
+    return sizeof(StateHeader) + sizeof(StripeState) * (size_t)(g.num_slices + 1) + 3 * state_plane_bytes(g) +
            sizeof(int16_t) * 2 * (size_t)g.num_mbs();
 }
 inline void state_header(const EncoderConfig& c, const Geometry& g, int started, int qp, int paint_qp,
                          StateHeader& h) {
     memset(&h, 0, sizeof(h));
     memcpy(h.magic, "SKH4", 4);
-    h.version = 1;
+    h.version = 2;
     h.W = g.W;
     h.H = g.H;
     h.stripe_height = c.stripe_height;
@@ -268,7 +279,7 @@ inline void state_header(const EncoderConfig& c, const Geometry& g, int started,
     h.paint_qp = paint_qp;
 }
 inline bool state_header_matches(const EncoderConfig& c, const Geometry& g, const StateHeader& h) {
-    return memcmp(h.magic, "SKH4", 4) == 0 && h.version == 1 && h.W == g.W && h.H == g.H &&
+    return memcmp(h.magic, "SKH4", 4) == 0 && h.version == 2 && h.W == g.W && h.H == g.H &&
            h.stripe_height == c.stripe_height && h.fullframe == c.fullframe && h.num_slices == g.num_slices;
 }
 
@@ -276,7 +287,7 @@ inline bool state_header_matches(const EncoderConfig& c, const Geometry& g, cons
 int choose_level_idc(int mb_w, int mb_h, float fps);
 // SPS + PPS NAL units (Annex-B, with start codes) for a picture of w x h pixels.
 void build_parameter_sets(int width, int height, int full_range, float fps,
-                          std::vector<uint8_t>& out);
+                          std::vector<uint8_t>& out, int num_refs = 1);
 // Appends start code + NAL header + EP-escaped payload.
 void append_nal(std::vector<uint8_t>& out, int nal_header_byte, const uint8_t* rbsp, size_t n);
 size_t emulation_prevent(const uint8_t* in, size_t n, uint8_t* out);

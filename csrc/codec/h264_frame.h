@@ -22,6 +22,7 @@ struct MeResult {
     int16_t mvx, mvy;        // integer-pel motion vector
     int32_t sad;             // SAD of the chosen vector
     int32_t intra_est;       // sum |Y - mean| of the source MB (scene-cut estimate)
+    int32_t ref;             // reference picture index (0 = previous picture, 1 = the one before)
 };
 
 class CpuH264Encoder {
@@ -49,6 +50,7 @@ class CpuH264Encoder {
     Geometry g;
     Controller ctl_;
     std::vector<uint8_t> src[3], prev[3], ref[3], rec[3];
+    std::vector<uint8_t> ref1[3];  // second reference (previous-but-one picture) when num_refs == 2
     std::vector<uint8_t> mb_dirty, stripe_dirty;
     std::vector<MbInfo> mbs;
     std::vector<int16_t> coefs;
@@ -64,10 +66,11 @@ class CpuH264Encoder {
 
    private:
     void mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb) const;
-    void mc_luma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pred) const;
+    void mc_luma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pred, int refi = 0) const;
     void mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pu,
-                   uint8_t* pv) const;
-    int sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t) const;
+                   uint8_t* pv, int refi = 0) const;
+    int sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t, int refi = 0) const;
+    const std::vector<uint8_t>* refs(int refi) const { return refi ? ref1 : ref; }
     void full_search(int mbx, int mby, const SliceTask& t, int16_t* out) const;
 };
 

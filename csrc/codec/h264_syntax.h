@@ -17,6 +17,7 @@ struct SliceHeaderParams {
     int idr_pic_id;
     int slice_qp;
     int deblock;      // 1: filter inside the slice (idc 2), 0: filter off (idc 1)
+    int num_refs;     // P: active references (> 1 overrides the PPS default of 1)
 };
 
 template <class W>
@@ -28,8 +29,13 @@ SK_HD void write_slice_header(W& w, const SliceHeaderParams& h) {
     if (h.idr) put_ue(w, (uint32_t)h.idr_pic_id);
     // pic_order_cnt_type == 2: no POC syntax
     if (h.slice_type == 0) {
-        w.put(0, 1);  // num_ref_idx_active_override_flag
-        w.put(0, 1);  // ref_pic_list_modification_flag_l0
+        if (h.num_refs > 1) {
+            w.put(1, 1);  // num_ref_idx_active_override_flag
+            put_ue(w, (uint32_t)(h.num_refs - 1));
+        } else {
+            w.put(0, 1);
+        }
+        w.put(0, 1);  // ref_pic_list_modification_flag_l0 (default order: most recent first)
     }
     // dec_ref_pic_marking() (nal_ref_idc != 0)
     if (h.idr) {
@@ -82,7 +88,7 @@ SK_HD int chroma_nc(const MbInfo& cur, MbNeighbours nb, int comp, int b) {
 // macroblock_layer() header part (everything before residual()).
 // qp_delta is only written when the syntax carries it.
 template <class W>
-SK_HD void write_mb_header(W& w, const MbInfo& mb, bool p_slice, int qp_delta) {
+SK_HD void write_mb_header(W& w, const MbInfo& mb, bool p_slice, int qp_delta, int num_refs = 1) {
     int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
     if (mb.type == MB_I16x16) {
         put_ue(w, (uint32_t)((p_slice ? 5 : 0) + i16_mb_type(mb.i16_mode, cbp_l, cbp_c)));
@@ -90,6 +96,8 @@ SK_HD void write_mb_header(W& w, const MbInfo& mb, bool p_slice, int qp_delta) {
         put_se(w, qp_delta);
     } else {  // P_L0_16x16
         put_ue(w, 0);
+        if (num_refs == 2) w.put(mb.ref ? 0u : 1u, 1);      // ref_idx_l0 te(v), range 1: one inverted bit
+        else if (num_refs > 2) put_ue(w, mb.ref);
         put_se(w, mb.mvdx);
         put_se(w, mb.mvdy);
         put_ue(w, H264_CBP_TO_CODE_INTER[cbp_l | (cbp_c << 4)]);

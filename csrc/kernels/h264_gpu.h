@@ -27,6 +27,7 @@ struct FrameArgs {
     int scaled;            // K2: resample the capture (src_w x src_h) to W x H inside K1
     ScaleParams scale;
     Planes src, prev, ref, rec;
+    Planes ref1;           // second reference (previous-but-one picture), num_refs == 2
     uint8_t* mb_dirty;     // [num_mbs]
     int* stripe_dirty;     // [num_slices] set by k_convert_damage, consumed (and cleared) by k_plan
     StripeState* plan_state;    // [num_slices + 1] controller state (last = picture state)
@@ -58,6 +59,7 @@ struct FrameArgs {
     SliceTask* tasks_host;           // host-mapped: final slice decisions (written by k_decide)
     unsigned long long* dbg;  // optional s_memtime stamps (SK_STAMPS=1), else nullptr
     const CavlcTables* cavlc_tabs;  // precomputed CAVLC tables (device memory), copied to LDS per WG
+    int num_refs;          // EncoderConfig::num_refs (1 or 2)
     int deblock;           // K7 on: ref = deblocked rec (k_deblock), else k_commit copies rec
     int me_full;           // K4a on: MFMA exhaustive-search candidate per dirty MB
     DbInfo* db;            // [num_mbs] deblocking side info (k_deblock_prep)

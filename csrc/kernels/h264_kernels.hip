@@ -390,12 +390,22 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; i++) dev += sk_abs((int)((sw >> (8 * i)) & 255) - mean);
     dev = wave_sum(dev);
+    int refi = 0;
+    if (t.num_refs > 1 && a.mb_dirty[idx]) {   // second reference at the zero vector (CPU: same rule)
+        const int s1 = me_sad(a, a.ref1.y, sw, mbx, mby, 0, 0, ylo, yhi);
+        if (s1 + 3 * lam < bcost) {
+            bx = by = 0;
+            bsad = s1;
+            refi = 1;
+        }
+    }
     if (l == 0) {
         MeResult r;
         r.mvx = (int16_t)bx;
         r.mvy = (int16_t)by;
         r.sad = bsad;
         r.intra_est = dev;
+        r.ref = refi;
         a.me[idx] = r;  // per-slice sums are reduced in k_decide (no same-line atomics)
     }
 }
@@ -567,9 +577,9 @@ __global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
             bool idr = true;
             for (int s = tid; s < ns; s += 256) idr &= a.tasks[s].final_action == ACT_I && a.tasks[s].idr_on_intra;
             idr = __syncthreads_and(idr);
-            if (tid == 0) commit_picture(pic, idr);
+            if (tid == 0) commit_picture(pic, idr, a.plan_cfg.num_refs);
         } else {
-            for (int s = tid; s < ns; s += 256) commit_stripe(st[s], a.tasks[s].final_action);
+            for (int s = tid; s < ns; s += 256) commit_stripe(st[s], a.tasks[s].final_action, a.plan_cfg.num_refs);
         }
     }
     const int kq = __hip_atomic_load(a.key_seq_host, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1024,6 +1034,7 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
             a.mbs[idx] = z;
             a.me[idx].mvx = 0;
             a.me[idx].mvy = 0;
+            a.me[idx].ref = 0;
         }
         return;
     }
@@ -1032,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     auto nbr = [&](int ox, int oy, bool ok) {
         MvNb n;
         n.avail = ok;
-        n.inter = ok;
+        n.ref = ok ? a.me[oy * a.mb_w + ox].ref : -1;
         n.mvx = ok ? 4 * a.me[oy * a.mb_w + ox].mvx : 0;
         n.mvy = ok ? 4 * a.me[oy * a.mb_w + ox].mvy : 0;
         return n;
@@ -1042,8 +1053,10 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     MvNb B = nbr(mbx, mby - 1, top);
     MvNb C = nbr(mbx + 1, mby - 1, top && mbx + 1 < a.mb_w);
     if (!C.avail) C = nbr(mbx - 1, mby - 1, top && mbx > 0);
+    const int refi = a.me[idx].ref;
+    const Planes& rp = refi ? a.ref1 : a.ref;
     int pmx, pmy, smx, smy;
-    mv_pred16x16(A, B, C, &pmx, &pmy);
+    mv_pred16x16(A, B, C, refi, &pmx, &pmy);
     mv_pskip(A, B, C, &smx, &smy);
     int mvx = 4 * a.me[idx].mvx, mvy = 4 * a.me[idx].mvy;
 
@@ -1054,7 +1067,7 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     int px = mbx * 16 + blk_x(b) * 4, py = mby * 16 + blk_y(b) * 4 + r;
     uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
     int sy = sk_clip(py + (mvy >> 2), ylo, yhi);
-    uint32_t pw = load_ref4(a.ref.y + (size_t)sy * a.stride_y, px + (mvx >> 2), a.stride_y);
+    uint32_t pw = load_ref4(rp.y + (size_t)sy * a.stride_y, px + (mvx >> 2), a.stride_y);
     int src_l[4], pred_l[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -1063,7 +1076,7 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     }
     // chroma source + bilinear MC prediction
     const uint8_t* cs = comp ? a.src.v : a.src.u;
-    const uint8_t* crf = comp ? a.ref.v : a.ref.u;
+    const uint8_t* crf = comp ? rp.v : rp.u;
     int cx0 = mbx * 8 + (cb & 1) * 4, cy0 = mby * 8 + (cb >> 1) * 4 + r;
     uint32_t csw = *reinterpret_cast<const uint32_t*>(cs + (size_t)cy0 * a.stride_c + cx0);
     int src_c[4], pred_c[4];
@@ -1093,7 +1106,8 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     if (l == 0) {
         mb.mvx = (int16_t)mvx;
         mb.mvy = (int16_t)mvy;
-        if (mb.cbp == 0 && mvx == smx && mvy == smy) {
+        mb.ref = (uint8_t)refi;
+        if (mb.cbp == 0 && refi == 0 && mvx == smx && mvy == smy) {
             mb.type = MB_P_SKIP;
         } else {
             mb.mvdx = (int16_t)(mvx - pmx);
@@ -1254,6 +1268,7 @@ __global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
                 a.mbs[idx] = mb;
                 a.me[idx].mvx = 0;
                 a.me[idx].mvy = 0;
+                a.me[idx].ref = 0;
             }
             STAMP(step, 7);
         }
@@ -1340,7 +1355,7 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
         AtomicBitWriter w{bits, 0};
         if (p_slice) put_ue(w, (uint32_t)run);
         int dq = mb_has_qp_delta(mb) ? (int)mb.qp - qp_prev : 0;
-        write_mb_header(w, mb, p_slice, dq);
+        write_mb_header(w, mb, p_slice, dq, p_slice ? t.num_refs : 1);
         hdr_bits = (int)w.pos;
     }
     hdr_bits = __shfl(hdr_bits, 0);
@@ -1442,6 +1457,7 @@ __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
         h.idr_pic_id = task.idr_pic_id;
         h.slice_qp = task.qp;
         h.deblock = a.deblock;
+        h.num_refs = intra ? 1 : task.num_refs;
         write_slice_header(w, h);
         if (fin == ACT_SKIPALL) put_ue(w, (uint32_t)nmb);
         sh_misc[0] = (int)w.pos;
@@ -1703,29 +1719,36 @@ __global__ __launch_bounds__(256) void k_commit(FrameArgs a) {
         a.mvfield[2 * idx] = zero ? 0 : a.me[idx].mvx;
         a.mvfield[2 * idx + 1] = zero ? 0 : a.me[idx].mvy;
     }
-    if (fin == ACT_SKIPALL || a.deblock) return;  // reference unchanged / written by k_deblock
-    {   // luma: 16 rows x (nmbs * 16) bytes, one uint4 per thread
-        const int row = tid >> 4, v = tid & 15;
-        if (v < nmbs) {
-            const size_t o = (size_t)(mby * 16 + row) * a.stride_y + (mbx0 + v) * 16;
-            *reinterpret_cast<uint4*>(a.ref.y + o) = *reinterpret_cast<const uint4*>(a.rec.y + o);
-        }
-    }
-    if (tid < 128) {  // chroma: 2 planes x 8 rows x (nmbs * 8) bytes, uint4 = 2 MBs
-        const int comp = tid >> 6, row = (tid >> 3) & 7, v = tid & 7;
-        if (2 * v < nmbs) {
-            const size_t o = (size_t)(mby * 8 + row) * a.stride_c + (mbx0 + 2 * v) * 8;
-            uint8_t* dst = comp ? a.ref.v : a.ref.u;
-            const uint8_t* src = comp ? a.rec.v : a.rec.u;
-            if (2 * v + 1 < nmbs && (a.stride_c & 15) == 0) {
-                *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(src + o);
-            } else {  // odd MB count per row: chroma rows are only 8-byte aligned
-                *reinterpret_cast<uint2*>(dst + o) = *reinterpret_cast<const uint2*>(src + o);
-                if (2 * v + 1 < nmbs)
-                    *reinterpret_cast<uint2*>(dst + o + 8) = *reinterpret_cast<const uint2*>(src + o + 8);
+    // This segment's samples, one uint4 (luma) / uint2..uint4 (chroma) per thread.
+    auto copy = [&](const Planes& src, const Planes& dst) {
+        {   // luma: 16 rows x (nmbs * 16) bytes
+            const int row = tid >> 4, v = tid & 15;
+            if (v < nmbs) {
+                const size_t o = (size_t)(mby * 16 + row) * a.stride_y + (mbx0 + v) * 16;
+                *reinterpret_cast<uint4*>(dst.y + o) = *reinterpret_cast<const uint4*>(src.y + o);
             }
         }
-    }
+        if (tid < 128) {  // chroma: 2 planes x 8 rows x (nmbs * 8) bytes, uint4 = 2 MBs
+            const int comp = tid >> 6, row = (tid >> 3) & 7, v = tid & 7;
+            if (2 * v < nmbs) {
+                const size_t o = (size_t)(mby * 8 + row) * a.stride_c + (mbx0 + 2 * v) * 8;
+                uint8_t* d = comp ? dst.v : dst.u;
+                const uint8_t* sp = comp ? src.v : src.u;
+                if (2 * v + 1 < nmbs && (a.stride_c & 15) == 0) {
+                    *reinterpret_cast<uint4*>(d + o) = *reinterpret_cast<const uint4*>(sp + o);
+                } else {  // odd MB count per row: chroma rows are only 8-byte aligned
+                    *reinterpret_cast<uint2*>(d + o) = *reinterpret_cast<const uint2*>(sp + o);
+                    if (2 * v + 1 < nmbs)
+                        *reinterpret_cast<uint2*>(d + o + 8) = *reinterpret_cast<const uint2*>(sp + o + 8);
+                }
+            }
+        }
+    };
+    // sliding-window DPB: the current reference becomes reference 1 (a skip-all picture
+    // is a reference too); the same thread then overwrites ref with rec below
+    if (a.num_refs > 1) copy(a.ref, a.ref1);
+    if (fin == ACT_SKIPALL || a.deblock) return;  // reference unchanged / written by k_deblock
+    copy(a.rec, a.ref);
 }
 
 // ---------------------------------------------------------------------------

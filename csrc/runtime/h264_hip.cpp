@@ -177,9 +177,9 @@ class HipBackend : public EncoderBackend {
             if (cfg_.fullframe) {
                 bool idr = ns > 0;
                 for (int s = 0; s < ns; s++) idr &= tasks[s].final_action == ACT_I && tasks[s].idr_on_intra;
-                commit_picture(st[ns], idr);
+                commit_picture(st[ns], idr, cfg_.num_refs > 1 ? 2 : 1);
             } else {
-                for (int s = 0; s < ns; s++) commit_stripe(st[s], tasks[s].final_action);
+                for (int s = 0; s < ns; s++) commit_stripe(st[s], tasks[s].final_action, cfg_.num_refs > 1 ? 2 : 1);
             }
         }
         const int qp = h_key_seq_[1] > 0 ? h_key_seq_[1] : cfg_.qp;
@@ -195,7 +195,7 @@ class HipBackend : public EncoderBackend {
         o += head.size();
         const size_t ny = (size_t)g_.stride_y * g_.plane_h_y, nc = (size_t)g_.stride_c * g_.plane_h_c;
         const gpu::Planes& last_src = planes_src_[parity_ ^ 1];
-        for (const gpu::Planes* pl : {(const gpu::Planes*)&args_.ref, &last_src}) {
+        for (const gpu::Planes* pl : {(const gpu::Planes*)&args_.ref, (const gpu::Planes*)&args_.ref1, &last_src}) {
             xfer(o, pl->y, ny, true, on_device); o += ny;
             xfer(o, pl->u, nc, true, on_device); o += nc;
             xfer(o, pl->v, nc, true, on_device); o += nc;
@@ -223,7 +223,7 @@ class HipBackend : public EncoderBackend {
         i += head.size();
         const size_t ny = (size_t)g_.stride_y * g_.plane_h_y, nc = (size_t)g_.stride_c * g_.plane_h_c;
         const gpu::Planes& last_src = planes_src_[parity_ ^ 1];
-        for (const gpu::Planes* pl : {(const gpu::Planes*)&args_.ref, &last_src}) {
+        for (const gpu::Planes* pl : {(const gpu::Planes*)&args_.ref, (const gpu::Planes*)&args_.ref1, &last_src}) {
             xfer(pl->y, i, ny, false, on_device); i += ny;
             xfer(pl->u, i, nc, false, on_device); i += nc;
             xfer(pl->v, i, nc, false, on_device); i += nc;
@@ -259,6 +259,7 @@ class HipBackend : public EncoderBackend {
         else if (s == "ref_y") { p = args_.ref.y; n = (int64_t)ny; }
         else if (s == "ref_u") { p = args_.ref.u; n = (int64_t)nc; }
         else if (s == "ref_v") { p = args_.ref.v; n = (int64_t)nc; }
+        else if (s == "ref1_y") { p = args_.ref1.y; n = (int64_t)ny; }
         else if (s == "fs_mv") { p = args_.fs_mv; n = (int64_t)g_.num_mbs() * 4; }
         else if (s == "mbs") { p = args_.mbs; n = (int64_t)g_.num_mbs() * sizeof(MbInfo); }
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
@@ -314,12 +315,14 @@ class HipBackend : public EncoderBackend {
         a.full_range = cfg_.full_range; a.me_range = cfg_.me_range; a.me_iters = cfg_.me_iters;
         a.deblock = cfg_.deblock;
         a.me_full = cfg_.me_full;
+        a.num_refs = cfg_.num_refs > 1 ? 2 : 1;
         a.scaled = (cfg_.src_width > 0 && cfg_.src_width != cfg_.width) ||
                    (cfg_.src_height > 0 && cfg_.src_height != cfg_.height);
         if (a.scaled)
             a.scale = scale_params(cfg_.src_width > 0 ? cfg_.src_width : cfg_.width,
                                    cfg_.src_height > 0 ? cfg_.src_height : cfg_.height, cfg_.width, cfg_.height);
         a.ref = make_planes();
+        a.ref1 = make_planes();
         a.rec = make_planes();
         a.mb_dirty = dmalloc<uint8_t>(nmb);
         void* dd = nullptr;
@@ -368,10 +371,10 @@ class HipBackend : public EncoderBackend {
         std::vector<std::vector<uint8_t>> ps;
         if (cfg_.fullframe) {
             ps.resize(1);
-            build_parameter_sets(g_.W, g_.H, cfg_.full_range, cfg_.fps, ps[0]);
+            build_parameter_sets(g_.W, g_.H, cfg_.full_range, cfg_.fps, ps[0], cfg_.num_refs);
         } else {
             ps.resize(ns);
-            for (int s = 0; s < ns; s++) build_parameter_sets(g_.W, g_.slice_pix_h(s), cfg_.full_range, cfg_.fps, ps[s]);
+            for (int s = 0; s < ns; s++) build_parameter_sets(g_.W, g_.slice_pix_h(s), cfg_.full_range, cfg_.fps, ps[s], cfg_.num_refs);
         }
         param_sets_ = ps;
         a.param_set_stride = 256;

@@ -36,6 +36,7 @@ class CpuBackend : public EncoderBackend {
         else if (s == "ref_y") plane(enc_.ref[0]);
         else if (s == "ref_u") plane(enc_.ref[1]);
         else if (s == "ref_v") plane(enc_.ref[2]);
+        else if (s == "ref1_y") plane(enc_.ref1[0]);
         else if (s == "mbs") { p = enc_.mbs.data(); n = (int64_t)(enc_.mbs.size() * sizeof(h264::MbInfo)); }
         else if (s == "coefs") { p = enc_.coefs.data(); n = (int64_t)(enc_.coefs.size() * 2); }
         else if (s == "me") { p = enc_.me.data(); n = (int64_t)(enc_.me.size() * sizeof(h264::MeResult)); }
@@ -58,7 +59,7 @@ class CpuBackend : public EncoderBackend {
         o += sizeof(h);
         enc_.ctl_.export_states(reinterpret_cast<h264::StripeState*>(o));
         o += sizeof(h264::StripeState) * (enc_.g.num_slices + 1);
-        for (auto* planes : {enc_.ref, enc_.prev})
+        for (auto* planes : {enc_.ref, enc_.ref1, enc_.prev})
             for (int p = 0; p < 3; p++) {
                 memcpy(o, planes[p].data(), planes[p].size());
                 o += planes[p].size();
@@ -79,7 +80,7 @@ class CpuBackend : public EncoderBackend {
         i += sizeof(h);
         enc_.ctl_.import_states(reinterpret_cast<const h264::StripeState*>(i));
         i += sizeof(h264::StripeState) * (enc_.g.num_slices + 1);
-        for (auto* planes : {enc_.ref, enc_.prev})
+        for (auto* planes : {enc_.ref, enc_.ref1, enc_.prev})
             for (int p = 0; p < 3; p++) {
                 memcpy(planes[p].data(), i, planes[p].size());
                 i += planes[p].size();
@@ -139,6 +140,7 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.shared_copy = c->shared_copy > 0 ? 1 : 0;
     e.src_width = c->src_width > 0 ? c->src_width : 0;
     e.src_height = c->src_height > 0 ? c->src_height : 0;
+    e.num_refs = c->num_refs > 1 ? 2 : 1;
     return e;
 }
 

@@ -19,6 +19,7 @@ typedef struct sk_h264_config {
     int32_t me_full;  // MFMA +-16 exhaustive search candidate: 0 = default (on), > 0 on, < 0 off
     int32_t shared_copy;  // > 0: H2D on the device's shared copy stream (bands of one frame)
     int32_t src_width, src_height;  // capture size if it differs (K2 resample in K1); 0 = width/height
+    int32_t num_refs;               // reference pictures (sliding-window DPB): 0/1 = one, 2 = two
 } sk_h264_config;
 
 typedef struct sk_packet {

@@ -390,7 +390,9 @@ class H264Decoder:
     def __init__(self):
         self.sps: dict[int, SPS] = {}
         self.pps: dict[int, PPS] = {}
-        self.ref = None          # (Y, U, V) of the reference picture (full coded size)
+        self.dpb: list = []      # short-term reference pictures (Y, U, V), most recent first (8.2.4.2.1)
+        self.cur_ref_idc = 0
+        self.cur_idr = False
         self.cur = None
         self.mbs: list[MbState] = []
         self.cur_sps: SPS | None = None
@@ -442,7 +444,10 @@ class H264Decoder:
         x0, y0 = 2 * cl, 2 * ct
         self.frames.append((y[y0:y0 + H, x0:x0 + W].copy(), u[y0 // 2:(y0 + H) // 2, x0 // 2:(x0 + W) // 2].copy(),
                             v[y0 // 2:(y0 + H) // 2, x0 // 2:(x0 + W) // 2].copy()))
-        self.ref = (y.copy(), u.copy(), v.copy())
+        if self.cur_ref_idc:   # sliding-window marking (8.2.5.3); IDR empties the DPB first
+            pic = (y.copy(), u.copy(), v.copy())
+            self.dpb = [pic] if self.cur_idr else [pic] + self.dpb
+            del self.dpb[max(1, sps.max_num_ref_frames):]
         self.cur = None
 
     # -------------------------------------------------------------------
@@ -487,13 +492,15 @@ class H264Decoder:
         if self.cur is None:
             self.cur_sps = sps
             self.cur_frame_num = frame_num
+            self.cur_ref_idc = ref_idc
+            self.cur_idr = idr
             self.cur = (np.zeros((sps.mb_h * 16, sps.mb_w * 16), np.uint8),
                         np.zeros((sps.mb_h * 8, sps.mb_w * 8), np.uint8),
                         np.zeros((sps.mb_h * 8, sps.mb_w * 8), np.uint8))
             self.mbs = [MbState() for _ in range(sps.mb_w * sps.mb_h)]
             if idr:
                 self.stats["idr"] += 1
-        if slice_type == 0 and self.ref is None:
+        if slice_type == 0 and not self.dpb:
             raise BitstreamError("P slice without a reference picture")
         self.slice_counter += 1
         self.stats["slices"] += 1
@@ -944,14 +951,14 @@ class H264Decoder:
         return (aA, rA, ax, ay), (aB, rB, bx, by), (aC, rC, cx, cy)
 
     @staticmethod
-    def _median_pred(A, B, C):
+    def _median_pred(A, B, C, ref=0):
         aA, rA, ax, ay = A
         aB, rB, bx, by = B
         aC, rC, cx, cy = C
         if not aB and not aC and aA:
             bx, by, rB = ax, ay, rA
             cx, cy, rC = ax, ay, rA
-        m = [r == 0 for r in (rA, rB, rC)]
+        m = [r == ref for r in (rA, rB, rC)]
         if sum(m) == 1:
             if m[0]:
                 return ax, ay
@@ -983,15 +990,20 @@ class H264Decoder:
 
     def _decode_p16(self, br, sps, pps, cur, mbx, mby, sid, num_ref):
         self.stats["p16"] += 1
-        if num_ref > 1:
-            raise NotImplementedError("multiple reference frames")
+        ref_idx = 0
+        if num_ref == 2:
+            ref_idx = 1 - br.u1()          # te(v) with range 1
+        elif num_ref > 2:
+            ref_idx = br.ue()
+        if ref_idx >= num_ref:
+            raise BitstreamError("ref_idx_l0 out of range")
         mvdx, mvdy = br.se(), br.se()
         A, B, C = self._mvp16(sps, mbx, mby, sid)
-        px, py = self._median_pred(A, B, C)
+        px, py = self._median_pred(A, B, C, ref_idx)
         mvx, mvy = px + mvdx, py + mvdy
         cur.mvx[:] = mvx
         cur.mvy[:] = mvy
-        cur.ref[:] = 0
+        cur.ref[:] = ref_idx
         code = br.ue()
         if code > 47:
             raise BitstreamError("coded_block_pattern out of range")
@@ -1011,7 +1023,7 @@ class H264Decoder:
                 levels[blk], tc = self.residual_block(br, nc, 16)
                 cur.tc_luma[by * 4 + bx] = tc
         dc, ac = self._chroma_residual(br, sps, pps, cur, mbx, mby, sid, cbp_c)
-        py_, pu, pv = self._mc(sps, mbx, mby, mvx, mvy, write=False)
+        py_, pu, pv = self._mc(sps, mbx, mby, mvx, mvy, write=False, ref_idx=ref_idx)
         Y = self.cur[0]
         qp = cur.qp
         for blk in range(16):
@@ -1023,8 +1035,10 @@ class H264Decoder:
         self._recon_chroma(sps, pps, cur, mbx, mby, dc, ac, pu, pv)
 
     # ---- motion compensation (8.4.2.2) ------------------------------------------
-    def _mc(self, sps, mbx, mby, mvx, mvy, write=True):
-        rY, rU, rV = self.ref
+    def _mc(self, sps, mbx, mby, mvx, mvy, write=True, ref_idx=0):
+        if ref_idx >= len(self.dpb):
+            raise BitstreamError(f"ref_idx {ref_idx} with {len(self.dpb)} reference pictures")
+        rY, rU, rV = self.dpb[ref_idx]
         H, W = rY.shape
         x0, y0 = mbx * 16, mby * 16
         xi, yi = x0 + (mvx >> 2), y0 + (mvy >> 2)

@@ -30,6 +30,7 @@ class SkH264Config(ctypes.Structure):
         ("scenecut", ctypes.c_int32), ("fps", ctypes.c_float), ("device", ctypes.c_int32),
         ("backend", ctypes.c_int32), ("deblock", ctypes.c_int32), ("me_full", ctypes.c_int32),
         ("shared_copy", ctypes.c_int32), ("src_width", ctypes.c_int32), ("src_height", ctypes.c_int32),
+        ("num_refs", ctypes.c_int32),
     ]
 
 
@@ -186,12 +187,12 @@ class Packet:
 
 MB_INFO_DTYPE = np.dtype([
     ("mvx", "<i2"), ("mvy", "<i2"), ("mvdx", "<i2"), ("mvdy", "<i2"), ("type", "u1"), ("i16_mode", "u1"),
-    ("chroma_mode", "u1"), ("cbp", "u1"), ("qp", "u1"), ("nnz", "u1", (24,)), ("pad", "u1", (3,)),
+    ("chroma_mode", "u1"), ("cbp", "u1"), ("qp", "u1"), ("nnz", "u1", (24,)), ("ref", "u1"), ("pad", "u1", (2,)),
 ])
-ME_DTYPE = np.dtype([("mvx", "<i2"), ("mvy", "<i2"), ("sad", "<i4"), ("intra_est", "<i4")])
+ME_DTYPE = np.dtype([("mvx", "<i2"), ("mvy", "<i2"), ("sad", "<i4"), ("intra_est", "<i4"), ("ref", "<i4")])
 TASK_DTYPE = np.dtype([(n, "<i4") for n in (
     "action", "qp", "first_row", "num_rows", "pic_row0", "pic_rows", "frame_num", "idr_pic_id",
-    "allow_scenecut", "idr_on_intra", "final_action", "pad")])
+    "allow_scenecut", "idr_on_intra", "final_action", "num_refs")])
 
 
 class H264Encoder:
@@ -203,7 +204,7 @@ class H264Encoder:
                  damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
                  backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
-                 src_width: int = 0, src_height: int = 0):
+                 src_width: int = 0, src_height: int = 0, num_refs: int = 1):
         L = lib()
         if backend not in ("cpu", "hip"):
             raise ValueError("backend must be 'cpu' or 'hip'")
@@ -213,7 +214,8 @@ class H264Encoder:
                                 int(use_paint_over), paint_over_trigger, paint_over_burst, int(streaming_mode),
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
                                 device, 1 if backend == "hip" else 0, 1 if deblock else -1,
-                                1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height))
+                                1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height),
+                                int(num_refs))
         self.width, self.height = width, height
         self.backend = backend
         self._h = L.sk_h264_create(ctypes.byref(self.cfg))

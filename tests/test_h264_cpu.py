@@ -6,12 +6,14 @@ from selkies_gstreamer_amd.ops.native import H264Encoder, MB_INFO_DTYPE
 from tests.h264_util import StripeDecoder, synthetic_frames, bgrx_to_y709, psnr
 
 
+@pytest.mark.parametrize("num_refs", [1, 2])
 @pytest.mark.parametrize("deblock", [False, True])
 @pytest.mark.parametrize("fullframe", [False, True])
 @pytest.mark.parametrize("kind", ["desktop", "noise"])
-def test_cpu_roundtrip_bitexact(fullframe, kind, deblock):
+def test_cpu_roundtrip_bitexact(fullframe, kind, deblock, num_refs):
     W, H = 160, 96
-    enc = H264Encoder(W, H, stripe_height=32, fullframe=fullframe, qp=26, backend="cpu", deblock=deblock)
+    enc = H264Encoder(W, H, stripe_height=32, fullframe=fullframe, qp=26, backend="cpu", deblock=deblock,
+                      num_refs=num_refs)
     sd = StripeDecoder(W, H)
     for t, f in enumerate(synthetic_frames(W, H, 5, kind=kind)):
         pk = enc.encode(f, t)
@@ -81,3 +83,35 @@ def test_qp_escalation_bounds_macroblock_size():
     assert mbs["qp"].max() > 0  # noise at QP 0 must escalate
     sd = StripeDecoder(W, H)
     sd.feed(pk[0].data)
+
+
+def _toggle_frames(W, H, n):
+    """A desktop whose caret blinks and a button toggles hover state: frame t
+    equals frame t - 2 (what the second reference picture captures)."""
+    base = next(synthetic_frames(W, H, 1, seed=4))
+    on = base.copy()
+    on[20:36, 40:42, :3] = 10                       # caret
+    on[60:76, 90:130, :3] = (230, 160, 40)          # highlighted button
+    return [base if t % 2 == 0 else on for t in range(n)]
+
+
+@pytest.mark.parametrize("fullframe", [False, True])
+def test_two_reference_pictures_code_toggling_content(fullframe):
+    W, H = 160, 96
+    frames = _toggle_frames(W, H, 8)
+    sizes = {}
+    for refs in (1, 2):
+        enc = H264Encoder(W, H, stripe_height=32, fullframe=fullframe, qp=24, use_paint_over=False,
+                          backend="cpu", num_refs=refs)
+        sd = StripeDecoder(W, H)
+        total = 0
+        for t, f in enumerate(frames):
+            pk = enc.encode(f, t)
+            for p in pk:
+                sd.feed(p.data)
+                if t >= 2:
+                    total += len(p.data)
+            ref = enc.debug_buffer("ref_y").reshape(-1, (W + 15) // 16 * 16)[:H, :W]
+            assert np.array_equal(sd.Y, ref), f"refs={refs} frame {t}: decoder != encoder reconstruction"
+        sizes[refs] = total
+    assert sizes[2] < 0.6 * sizes[1], sizes      # the toggle is a near-free ref_idx 1 copy

@@ -26,12 +26,13 @@ def _compare_state(cpu, gpu, W, t):
         assert np.array_equal(a, b), f"frame {t}: {name} differs ({np.sum(a != b)} bytes)"
 
 
+@pytest.mark.parametrize("num_refs", [1, 2])
 @pytest.mark.parametrize("deblock", [False, True])
 @pytest.mark.parametrize("fullframe", [False, True])
 @pytest.mark.parametrize("kind", ["desktop", "noise"])
-def test_gpu_matches_cpu_reference(fullframe, kind, deblock):
+def test_gpu_matches_cpu_reference(fullframe, kind, deblock, num_refs):
     W, H = 192, 128
-    cpu, gpu = _pair(W, H, stripe_height=32, fullframe=fullframe, qp=26, deblock=deblock)
+    cpu, gpu = _pair(W, H, stripe_height=32, fullframe=fullframe, qp=26, deblock=deblock, num_refs=num_refs)
     sd = StripeDecoder(W, H)
     for t, f in enumerate(synthetic_frames(W, H, 6, seed=3, kind=kind)):
         pc = cpu.encode(f, t)
@@ -102,3 +103,16 @@ def test_gpu_overlapped_upload_matches_sequential():
         if t + 1 < len(frames):
             b.launch()
     assert got == ref
+
+
+@pytest.mark.parametrize("fullframe", [False, True])
+def test_gpu_two_references_toggling_matches_cpu(fullframe):
+    """Second reference picture (sliding-window DPB): caret/button toggles coded as
+    ref_idx 1 copies; HIP bitstreams == CPU reference, ref1 planes identical."""
+    from tests.test_h264_cpu import _toggle_frames
+    W, H = 160, 96
+    kw = dict(stripe_height=32, fullframe=fullframe, qp=24, use_paint_over=False, num_refs=2, deblock=True)
+    cpu, gpu = _pair(W, H, **kw)
+    for t, f in enumerate(_toggle_frames(W, H, 8)):
+        assert [p.data for p in gpu.encode(f, t)] == [p.data for p in cpu.encode(f, t)], f"frame {t}"
+        assert np.array_equal(gpu.debug_buffer("ref1_y"), cpu.debug_buffer("ref1_y")), f"frame {t}"

@@ -28,19 +28,20 @@ def _run(enc, frames, start):
     return [[(p.y, p.key, p.data) for p in enc.encode(f, start + i)] for i, f in enumerate(frames)]
 
 
+@pytest.mark.parametrize("num_refs", [1, 2])
 @pytest.mark.parametrize("fullframe", [False, True])
-def test_migrated_session_continues_bit_exact(fullframe):
+def test_migrated_session_continues_bit_exact(fullframe, num_refs):
     fr = _frames()
-    a = H264Encoder(W, H, fullframe=fullframe, backend="cpu", **KW)
+    a = H264Encoder(W, H, fullframe=fullframe, backend="cpu", num_refs=num_refs, **KW)
     _run(a, fr[:4], 0)
     a.set_qp(30, 19)
     state = a.export_state()
-    b = H264Encoder(W, H, fullframe=fullframe, backend="cpu", **KW)
+    b = H264Encoder(W, H, fullframe=fullframe, backend="cpu", num_refs=num_refs, **KW)
     b.import_state(state)
     ra, rb = _run(a, fr[4:], 4), _run(b, fr[4:], 4)
     assert ra == rb
     assert not any(key for frame in rb for _, key, _ in frame)      # no IDR after the move
-    fresh = H264Encoder(W, H, fullframe=fullframe, backend="cpu", **KW)
+    fresh = H264Encoder(W, H, fullframe=fullframe, backend="cpu", num_refs=num_refs, **KW)
     assert any(key for _, key, _ in _run(fresh, fr[4:5], 4)[0])     # without state: IDR
 
 
