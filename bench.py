@@ -124,6 +124,24 @@ def main():
     def run(i, first, count, record):
         e = encs[i]
         fr = pool.array
+        if args.overlap >= 2 and hasattr(e, "upload"):
+            # two frames in flight: frame t+1 is uploaded and launched before frame t's
+            # packets are collected, so the GPU never waits for the host between frames
+            t_up = {first: time.perf_counter()}
+            e.upload(fr[(first + 3 * i) % args.pool], first)
+            e.launch()
+            for t in range(first, first + count):
+                if t + 1 < first + count:
+                    t_up[t + 1] = time.perf_counter()
+                    e.upload(fr[(t + 1 + 3 * i) % args.pool], t + 1)
+                    e.launch()
+                pk = e.finish()
+                if record:
+                    lat[i].append(time.perf_counter() - t_up.pop(t))
+                    nbytes[i] += sum(len(p.data) for p in pk)
+                    if args.gather:
+                        out_packets[i].append(pk)
+            return
         if args.overlap and hasattr(e, "upload"):
             t_up = time.perf_counter()
             e.upload(fr[(first + 3 * i) % args.pool], first)
@@ -231,6 +249,7 @@ def main():
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
                 "bands_per_session": args.bands,
                 "upload_overlap": bool(args.overlap),
+                "frames_in_flight": 2 if args.overlap >= 2 else 1,
                 "num_refs": args.num_refs,
                 "numa_node_rank0": numa_node,
             },

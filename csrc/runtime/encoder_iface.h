@@ -1,11 +1,14 @@
 // Backend interface behind the C ABI.
 #pragma once
+#include <deque>
 #include <string>
 #include <vector>
 #include "../codec/h264_frame.h"
 #include "../codec/jpeg_encoder.h"
 
 namespace sk {
+
+void set_last_error(const std::string& e);
 
 class EncoderBackend {
    public:
@@ -15,14 +18,26 @@ class EncoderBackend {
     // Split form of encode(): submit() queues the frame (the caller keeps `bgrx`
     // alive until finish()), finish() waits and returns the packet count. Several
     // encoders can be submitted before any is finished (bands of one frame, or
-    // sessions driven from one thread). Default: synchronous.
+    // sessions driven from one thread). Default: synchronous; the packets of each
+    // submitted frame are queued, so two frames may be submitted before finish().
     virtual int submit(const uint8_t* bgrx, int stride, uint16_t frame_id) {
-        pending_ = encode(bgrx, stride, frame_id);
-        return pending_ < 0 ? -1 : 0;
+        if (encode(bgrx, stride, frame_id) < 0) return -1;
+        done_.push_back(std::move(packets_));
+        packets_.clear();
+        return 0;
     }
-    virtual int finish() { return pending_; }
+    virtual int finish() {
+        if (done_.empty()) {
+            set_last_error("finish() without a submitted frame");
+            return -1;
+        }
+        packets_ = std::move(done_.front());
+        done_.pop_front();
+        return (int)packets_.size();
+    }
     // submit() in two steps, so the next frame's upload can overlap this frame's
-    // kernels: upload(n+1) ... finish(n) ... launch(n+1). Default: upload encodes.
+    // kernels: upload(n+1) ... finish(n) ... launch(n+1), or with two frames in
+    // flight upload(n+1) launch(n+1) ... finish(n). Default: upload encodes.
     virtual int upload(const uint8_t* bgrx, int stride, uint16_t frame_id) { return submit(bgrx, stride, frame_id); }
     virtual int launch() { return 0; }
     // Session state transfer (h264::StateHeader layout). `on_device`: the buffer is
@@ -37,13 +52,12 @@ class EncoderBackend {
     std::vector<h264::EncodedPacket> packets_;
 
    protected:
-    int pending_ = 0;
+    std::deque<std::vector<h264::EncodedPacket>> done_;
 };
 
 EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c);
 EncoderBackend* create_hip_backend(const h264::EncoderConfig& c, int device);
 EncoderBackend* create_cpu_jpeg_backend(const jpeg::JpegConfig& c);
 EncoderBackend* create_hip_jpeg_backend(const jpeg::JpegConfig& c, int device);
-void set_last_error(const std::string& e);
 
 }  // namespace sk

@@ -35,7 +35,7 @@ class HipBackend : public EncoderBackend {
         ctl_.init(cfg_, g_);
         HIPCHECK(hipSetDevice(device_));
         HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-        for (int i = 0; i < 4; i++) HIPCHECK(hipEventCreate(&ev_[i]));
+        for (auto& e : ev_) HIPCHECK(hipEventCreate(&e));
         for (auto& e : ev_copy_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (cfg_.shared_copy) copy_stream_ = device_copy_stream(device_);
         alloc();
@@ -48,7 +48,7 @@ class HipBackend : public EncoderBackend {
             if (gx) hipGraphExecDestroy(gx);
         for (void* p : dev_allocs_) hipFree(p);
         for (void* p : host_allocs_) hipHostFree(p);
-        for (int i = 0; i < 4; i++) hipEventDestroy(ev_[i]);
+        for (auto& e : ev_) hipEventDestroy(e);
         for (auto& e : ev_copy_) hipEventDestroy(e);
         for (auto* b : bgrx_dev_)
             if (b) hipFree(b);
@@ -92,15 +92,19 @@ class HipBackend : public EncoderBackend {
             invalidate_graphs();
             args_.bgrx_stride = stride;
         }
-        const int q = inflight_ ? parity_ ^ 1 : parity_;
+        if (inflight() >= 2) {
+            set_last_error("upload(): two frames in flight; finish() the oldest first");
+            return -1;
+        }
+        const int q = launched_ & 1;   // parity this frame is launched with
         // Nothing in flight: copy on the encoder's own stream (no cross-stream wait).
         // Overlapped upload, or bands of one frame: the device's shared copy stream, so
         // the uploads of all encoders on this GPU run back to back at full PCIe rate
         // instead of contending (one copy queue, not one per session).
         hipStream_t cs = stream_;
-        if (copy_stream_ || inflight_) cs = copy_stream_ ? copy_stream_ : device_copy_stream(device_);
+        if (copy_stream_ || inflight()) cs = copy_stream_ ? copy_stream_ : device_copy_stream(device_);
         // the last reader of bgrx_dev_[q] is the graph two frames back: finished
-        HIPCHECK(hipEventRecord(ev_[0], cs));
+        HIPCHECK(hipEventRecord(ev_[3 * q], cs));
         HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyHostToDevice, cs));
         if (cs != stream_) HIPCHECK(hipEventRecord(ev_copy_[q], cs));
         staged_on_main_ = cs == stream_;
@@ -110,44 +114,59 @@ class HipBackend : public EncoderBackend {
     }
 
     int launch() override {
-        if (!staged_ || inflight_) {
-            set_last_error("launch() needs one uploaded frame and no frame in flight");
+        if (!staged_ || inflight() >= 2) {
+            set_last_error("launch() needs one uploaded frame and at most one frame in flight");
             return -1;
         }
         trace::Range frame_range("h264.launch");
         HIPCHECK(hipSetDevice(device_));
-        packets_.clear();
-        set_parity_args(args_.bgrx_stride);   // bgrx = bgrx_dev_[parity_]
-        h_frame_params_[0] = staged_frame_;   // host-mapped, read by k_plan (previous frame is done)
-        pending_frame_ = staged_frame_;
-        if (!staged_on_main_) HIPCHECK(hipStreamWaitEvent(stream_, ev_copy_[parity_], 0));
-        HIPCHECK(hipEventRecord(ev_[1], stream_));
+        const int p = launched_ & 1;
+        parity_ = p;
+        set_parity_args(args_.bgrx_stride);   // bgrx = bgrx_dev_[p], host outputs of parity p
+        // host-mapped, read by this frame's k_plan: per parity, because with two frames
+        // in flight the previous frame's k_plan may not have run yet
+        h_frame_params_[p][0] = staged_frame_;
+        // keyframe request counter and QP overrides as of this launch: a request made
+        // before launch(n) applies to frame n even when frame n-1 has not planned yet
+        for (int i = 0; i < 3; i++) h_key_snap_[p][i] = __atomic_load_n(&h_key_seq_[i], __ATOMIC_SEQ_CST);
+        frame_of_[p] = staged_frame_;
+        if (!staged_on_main_) HIPCHECK(hipStreamWaitEvent(stream_, ev_copy_[p], 0));
+        HIPCHECK(hipEventRecord(ev_[3 * p + 1], stream_));
         // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
-        // one sync; k_decide leaves the final slice decisions in h_tasks_.
-        run_graph(graph_exec_[parity_], 0);
-        HIPCHECK(hipEventRecord(ev_[2], stream_));
+        // one sync; k_decide leaves the final slice decisions in h_tasks_[p].
+        run_graph(graph_exec_[p], 0);
+        HIPCHECK(hipEventRecord(ev_[3 * p + 2], stream_));
         // MV field / reference update and K7 deblocking run after the packets are done:
-        // the host only waits for ev_[2]; the next frame's work queues behind the update.
-        run_graph(post_exec_[parity_], 1);
+        // the host only waits for ev_[3p+2]; the next frame's work queues behind the update.
+        run_graph(post_exec_[p], 1);
         staged_ = false;
-        inflight_ = true;
+        launched_++;
+        parity_ = launched_ & 1;
         return 0;
     }
 
+    // Oldest frame in flight: wait for its packets. Up to two frames may be in flight
+    // (launch(n+1) before finish(n)): the GPU then runs frame n+1's graph while the
+    // host assembles frame n's packets, with no idle gap between the two graphs.
     int finish() override {
+        if (inflight() <= 0) {
+            set_last_error("finish() without a launched frame");
+            return -1;
+        }
+        const int p = finished_ & 1;
         {
             trace::Range r("h264.wait");
-            HIPCHECK(hipEventSynchronize(ev_[2]));
+            HIPCHECK(hipEventSynchronize(ev_[3 * p + 2]));
         }
         {
             trace::Range r("h264.packets");
-            build_packets(pending_frame_);
+            packets_.clear();
+            build_packets(p, frame_of_[p]);
         }
-        parity_ ^= 1;
-        inflight_ = false;
+        finished_++;
         float t0 = 0, t1 = 0;
-        hipEventElapsedTime(&t0, ev_[0], ev_[1]);
-        hipEventElapsedTime(&t1, ev_[1], ev_[2]);
+        hipEventElapsedTime(&t0, ev_[3 * p], ev_[3 * p + 1]);
+        hipEventElapsedTime(&t1, ev_[3 * p + 1], ev_[3 * p + 2]);
         stage_ms_[0] = t0;
         stage_ms_[1] = t1;
         return (int)packets_.size();
@@ -268,7 +287,7 @@ class HipBackend : public EncoderBackend {
         else if (s == "stamps") { if (!args_.dbg) return -1; p = args_.dbg; n = 64 * 16 * 8; }
         else if (s == "tasks") {
             n = (int64_t)g_.num_slices * sizeof(SliceTask);
-            if (dst && cap >= n) memcpy(dst, h_tasks_, (size_t)n);
+            if (dst && cap >= n) memcpy(dst, h_tasks_[(finished_ + 1) & 1], (size_t)n);   // last finished
             return n;
         } else return -1;
         if (dst && cap >= n) HIPCHECK(hipMemcpyAsync(dst, p, (size_t)n, hipMemcpyDeviceToHost, stream_));
@@ -336,9 +355,13 @@ class HipBackend : public EncoderBackend {
                                     hipMemcpyHostToDevice, stream_));
             HIPCHECK(hipStreamSynchronize(stream_));
         }
-        h_key_seq_ = hmalloc<int>(16, hipHostMallocCoherent);
-        HIPCHECK(hipHostGetDevicePointer(&dd, h_key_seq_, 0));
-        a.key_seq_host = (const int*)dd;
+        h_key_seq_ = hmalloc<int>(16, hipHostMallocCoherent);   // written by request_keyframe/set_qp
+        for (int p = 0; p < 2; p++) {   // per-parity snapshot taken at launch, read by k_plan
+            h_key_snap_[p] = hmalloc<int>(4, hipHostMallocCoherent);
+            HIPCHECK(hipHostGetDevicePointer(&dd, h_key_snap_[p], 0));
+            key_snap_dev_[p] = (const int*)dd;
+        }
+        a.key_seq_host = key_snap_dev_[0];
         a.tasks = dmalloc<SliceTask>(ns);
         a.me = dmalloc<MeResult>(nmb);
         a.mvfield = dmalloc<int16_t>(2 * nmb);
@@ -360,13 +383,15 @@ class HipBackend : public EncoderBackend {
         // worst case: header + SPS/PPS + 3/2 emulation-prevention growth, 64-byte multiple
         size_t slot = ((size_t)a.rbsp_slot_words * 4 * 3 / 2 + 1024 + 63) & ~(size_t)63;
         a.out_slot_bytes = (int)slot;
-        host_out_ = hmalloc<uint8_t>(slot * ns);
-        h_out_size_ = hmalloc<int>(ns);
         void* dptr = nullptr;
-        HIPCHECK(hipHostGetDevicePointer(&dptr, host_out_, 0));
-        a.host_out = (uint8_t*)dptr;
-        HIPCHECK(hipHostGetDevicePointer(&dptr, h_out_size_, 0));
-        a.host_size = (int*)dptr;
+        for (int p = 0; p < 2; p++) {   // host outputs per parity (two frames in flight)
+            host_out_[p] = hmalloc<uint8_t>(slot * ns);
+            h_out_size_[p] = hmalloc<int>(ns);
+            HIPCHECK(hipHostGetDevicePointer(&dptr, host_out_[p], 0));
+            host_out_dev_[p] = (uint8_t*)dptr;
+            HIPCHECK(hipHostGetDevicePointer(&dptr, h_out_size_[p], 0));
+            host_size_dev_[p] = (int*)dptr;
+        }
         // parameter sets
         std::vector<std::vector<uint8_t>> ps;
         if (cfg_.fullframe) {
@@ -401,12 +426,14 @@ class HipBackend : public EncoderBackend {
         d_frame_params_ = dmalloc<int>(4);
         if (getenv("SK_STAMPS")) a.dbg = dmalloc<unsigned long long>(64 * 16);
         a.frame_params_dev = d_frame_params_;
-        h_tasks_ = hmalloc<SliceTask>(ns, hipHostMallocCoherent);  // final decisions from k_decide
-        HIPCHECK(hipHostGetDevicePointer(&dd, h_tasks_, 0));
-        a.tasks_host = (SliceTask*)dd;
-        h_frame_params_ = hmalloc<int>(4, hipHostMallocCoherent);
-        HIPCHECK(hipHostGetDevicePointer(&dd, h_frame_params_, 0));
-        a.frame_params_host = (const int*)dd;
+        for (int p = 0; p < 2; p++) {
+            h_tasks_[p] = hmalloc<SliceTask>(ns, hipHostMallocCoherent);  // final decisions from k_decide
+            HIPCHECK(hipHostGetDevicePointer(&dd, h_tasks_[p], 0));
+            tasks_host_dev_[p] = (SliceTask*)dd;
+            h_frame_params_[p] = hmalloc<int>(4, hipHostMallocCoherent);
+            HIPCHECK(hipHostGetDevicePointer(&dd, h_frame_params_[p], 0));
+            frame_params_dev_host_[p] = (const int*)dd;
+        }
     }
 
     void set_parity_args(int stride) {
@@ -414,6 +441,11 @@ class HipBackend : public EncoderBackend {
         args_.bgrx_stride = stride;
         args_.src = planes_src_[parity_];
         args_.prev = planes_src_[parity_ ^ 1];
+        args_.host_out = host_out_dev_[parity_];
+        args_.host_size = host_size_dev_[parity_];
+        args_.tasks_host = tasks_host_dev_[parity_];
+        args_.frame_params_host = frame_params_dev_host_[parity_];
+        args_.key_seq_host = key_snap_dev_[parity_];
     }
 
     void invalidate_graphs() {
@@ -449,33 +481,36 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipGraphLaunch(gx, stream_));
     }
 
-    void build_packets(uint16_t frame_id) {
+    void build_packets(int par, uint16_t frame_id) {
+        const uint8_t* host_out = host_out_[par];
+        const int* h_out_size = h_out_size_[par];
+        const SliceTask* h_tasks = h_tasks_[par];
         const int ns = g_.num_slices;
         std::vector<long> offs(ns);
         for (int s = 0; s < ns; s++) offs[s] = (long)s * args_.out_slot_bytes;
         if (cfg_.fullframe) {
-            bool idr = ctl_.picture_is_idr(h_tasks_);
+            bool idr = ctl_.picture_is_idr(h_tasks);
             EncodedPacket pk;
             pk.y = 0; pk.w = g_.W; pk.h = g_.H; pk.key = idr;
             pk.data.resize(10);
             write_stripe_header(pk.data.data(), idr, frame_id, 0, g_.W, g_.H);
             if (idr) pk.data.insert(pk.data.end(), param_sets_[0].begin(), param_sets_[0].end());
             for (int s = 0; s < ns; s++) {
-                const uint8_t* p = host_out_ + offs[s];
-                pk.data.insert(pk.data.end(), p, p + h_out_size_[s]);
+                const uint8_t* p = host_out + offs[s];
+                pk.data.insert(pk.data.end(), p, p + h_out_size[s]);
             }
             packets_.push_back(std::move(pk));
             return;
         }
         for (int s = 0; s < ns; s++) {
-            if (h_tasks_[s].final_action == ACT_NONE || h_out_size_[s] <= 0) continue;
+            if (h_tasks[s].final_action == ACT_NONE || h_out_size[s] <= 0) continue;
             EncodedPacket pk;
             pk.y = g_.slice_pix_y(s);
             pk.w = g_.W;
             pk.h = g_.slice_pix_h(s);
-            pk.key = h_tasks_[s].final_action == ACT_I;
-            const uint8_t* p = host_out_ + offs[s];
-            pk.data.assign(p, p + h_out_size_[s]);
+            pk.key = h_tasks[s].final_action == ACT_I;
+            const uint8_t* p = host_out + offs[s];
+            pk.data.assign(p, p + h_out_size[s]);
             packets_.push_back(std::move(pk));
         }
     }
@@ -485,20 +520,29 @@ class HipBackend : public EncoderBackend {
     Controller ctl_;
     int device_;
     hipStream_t stream_ = nullptr;
-    hipEvent_t ev_[4];
+    hipEvent_t ev_[6];   // per parity p: [3p] upload, [3p+1] graph start, [3p+2] packets done
     gpu::FrameArgs args_;
     gpu::Planes planes_src_[2];
     int parity_ = 0;
     uint8_t* bgrx_dev_[2] = {nullptr, nullptr};   // input frame per parity (upload overlaps the other)
     hipEvent_t ev_copy_[2];
-    bool staged_ = false, inflight_ = false, staged_on_main_ = true;
+    bool staged_ = false, staged_on_main_ = true;
+    int launched_ = 0, finished_ = 0;   // frames launched / finished; frame k uses parity k & 1
+    int inflight() const { return launched_ - finished_; }
+    uint16_t frame_of_[2] = {0, 0};
     uint16_t staged_frame_ = 0;
     size_t bgrx_cap_ = 0;
-    uint8_t* host_out_ = nullptr;
+    uint8_t* host_out_[2] = {nullptr, nullptr};
+    uint8_t* host_out_dev_[2] = {nullptr, nullptr};
+    int* host_size_dev_[2] = {nullptr, nullptr};
+    SliceTask* tasks_host_dev_[2] = {nullptr, nullptr};
+    const int* frame_params_dev_host_[2] = {nullptr, nullptr};
     int* h_key_seq_ = nullptr;
-    SliceTask* h_tasks_ = nullptr;
-    int* h_out_size_ = nullptr;
-    int* h_frame_params_ = nullptr;
+    SliceTask* h_tasks_[2] = {nullptr, nullptr};
+    int* h_out_size_[2] = {nullptr, nullptr};
+    int* h_frame_params_[2] = {nullptr, nullptr};
+    int* h_key_snap_[2] = {nullptr, nullptr};
+    const int* key_snap_dev_[2] = {nullptr, nullptr};
     int* d_frame_params_ = nullptr;
     std::vector<std::vector<uint8_t>> param_sets_;
     std::vector<void*> dev_allocs_, host_allocs_;
@@ -506,7 +550,6 @@ class HipBackend : public EncoderBackend {
     hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
     hipStream_t copy_stream_ = nullptr;   // shared per device (not owned)
-    uint16_t pending_frame_ = 0;
 
     // One H2D stream per device for encoders created with shared_copy: lives as long
     // as the process (encoders come and go, the stream is reused).

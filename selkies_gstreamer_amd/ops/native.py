@@ -6,6 +6,7 @@ GPU-marked paths: `require_gpu()` raises instead of silently falling back.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 import threading
@@ -221,6 +222,8 @@ class H264Encoder:
         self._h = L.sk_h264_create(ctypes.byref(self.cfg))
         if not self._h:
             raise RuntimeError(f"sk_h264_create failed: {L.sk_last_error().decode()}")
+        self._inflight = collections.deque()   # input frames kept alive until finish()
+        self._staged = None
 
     def close(self):
         if getattr(self, "_h", None):
@@ -265,16 +268,17 @@ class H264Encoder:
             raise TypeError("bgrx must be uint8")
         if not bgrx.flags["C_CONTIGUOUS"]:
             bgrx = np.ascontiguousarray(bgrx)
-        self._inflight = bgrx
         L = lib()
         if L.sk_h264_submit(self._h, bgrx.ctypes.data, bgrx.strides[0], frame_id & 0xFFFF) < 0:
-            self._inflight = None
             raise RuntimeError(f"submit failed: {L.sk_last_error().decode()}")
+        self._inflight.append(bgrx)
 
     def upload(self, bgrx: np.ndarray, frame_id: int = 0) -> None:
         """First half of :meth:`submit`: stages the frame (HIP: H2D on the copy stream).
         Allowed while the previous frame is still in flight — its upload overlaps that
-        frame's kernels; call :meth:`launch` for it after :meth:`finish` of the previous."""
+        frame's kernels. Then either :meth:`launch` it after :meth:`finish` of the previous
+        frame, or launch it at once (two frames in flight: the GPU runs it while the host
+        collects the previous frame's packets) and finish the older frame afterwards."""
         if bgrx.dtype != np.uint8:
             raise TypeError("bgrx must be uint8")
         if not bgrx.flags["C_CONTIGUOUS"]:
@@ -289,12 +293,14 @@ class H264Encoder:
         L = lib()
         if L.sk_h264_launch(self._h) < 0:
             raise RuntimeError(f"launch failed: {L.sk_last_error().decode()}")
-        self._inflight, self._staged = getattr(self, "_staged", None), None
+        self._inflight.append(getattr(self, "_staged", None))
+        self._staged = None
 
     def finish(self) -> list[Packet]:
         L = lib()
         n = L.sk_h264_finish(self._h)
-        self._inflight = None
+        if self._inflight:
+            self._inflight.popleft()
         if n < 0:
             raise RuntimeError(f"encode failed: {L.sk_last_error().decode()}")
         return self._packets(n)

@@ -115,3 +115,22 @@ def test_two_reference_pictures_code_toggling_content(fullframe):
             assert np.array_equal(sd.Y, ref), f"refs={refs} frame {t}: decoder != encoder reconstruction"
         sizes[refs] = total
     assert sizes[2] < 0.6 * sizes[1], sizes      # the toggle is a near-free ref_idx 1 copy
+
+
+def test_cpu_backend_queues_two_submitted_frames():
+    """The synchronous backends queue each submitted frame's packets, so the
+    two-frames-in-flight call pattern (submit n+1 before finish n) works on them too."""
+    W, H = 160, 96
+    frames = list(synthetic_frames(W, H, 5, seed=9))
+    a = H264Encoder(W, H, stripe_height=32, qp=26, backend="cpu")
+    ref = [[p.data for p in a.encode(f, t)] for t, f in enumerate(frames)]
+    b = H264Encoder(W, H, stripe_height=32, qp=26, backend="cpu")
+    got = []
+    b.submit(frames[0], 0)
+    for t in range(len(frames)):
+        if t + 1 < len(frames):
+            b.submit(frames[t + 1], t + 1)
+        got.append([p.data for p in b.finish()])
+    assert got == ref
+    with pytest.raises(RuntimeError):
+        b.finish()

@@ -116,3 +116,35 @@ def test_gpu_two_references_toggling_matches_cpu(fullframe):
     for t, f in enumerate(_toggle_frames(W, H, 8)):
         assert [p.data for p in gpu.encode(f, t)] == [p.data for p in cpu.encode(f, t)], f"frame {t}"
         assert np.array_equal(gpu.debug_buffer("ref1_y"), cpu.debug_buffer("ref1_y")), f"frame {t}"
+
+
+def _two_in_flight(enc, frames, key_at=None):
+    """upload(n+1) + launch(n+1) before finish(n): two frames in flight."""
+    got = []
+    enc.upload(frames[0], 0)
+    enc.launch()
+    for t in range(len(frames)):
+        if t + 1 < len(frames):
+            if key_at == t + 1:
+                enc.request_keyframe()
+            enc.upload(frames[t + 1], t + 1)
+            enc.launch()
+        got.append([(p.y, p.key, p.data) for p in enc.finish()])
+    return got
+
+
+@pytest.mark.parametrize("fullframe", [False, True])
+def test_gpu_two_frames_in_flight_match_cpu(fullframe):
+    """Per-parity host outputs (packets, slice decisions, frame id): with frame n+1
+    launched before frame n is collected, every frame's packets equal the CPU
+    reference's, including a keyframe requested mid-stream."""
+    W, H = 320, 192
+    frames = list(synthetic_frames(W, H, 8, seed=21))
+    cpu = H264Encoder(W, H, stripe_height=64, qp=26, backend="cpu", fullframe=fullframe)
+    ref = []
+    for t, f in enumerate(frames):
+        if t == 5:
+            cpu.request_keyframe()
+        ref.append([(p.y, p.key, p.data) for p in cpu.encode(f, t)])
+    gpu = H264Encoder(W, H, stripe_height=64, qp=26, backend="hip", fullframe=fullframe)
+    assert _two_in_flight(gpu, frames, key_at=5) == ref
