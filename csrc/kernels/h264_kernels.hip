@@ -1135,12 +1135,12 @@ __global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
     __shared__ IntraEdges E;
     __shared__ uint8_t zero16[16];
     __shared__ CavlcTables T;
+    int s = blockIdx.x;
+    const SliceTask t = a.tasks[s];
+    if (t.final_action != ACT_I) return;   // block-uniform: P/skipped slices leave before the table load
     if (threadIdx.x < 16) zero16[threadIdx.x] = 0;
     load_cavlc_tables(T, a.cavlc_tabs);
     __syncthreads();
-    int s = blockIdx.x;
-    const SliceTask t = a.tasks[s];
-    if (t.final_action != ACT_I) return;
     int w = threadIdx.x >> 6;
     int l = lane_id();
     int rows = t.num_rows;

@@ -134,10 +134,12 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipEventRecord(ev_[3 * p + 1], stream_));
         // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
         // one sync; k_decide leaves the final slice decisions in h_tasks_[p].
-        run_graph(graph_exec_[p], 0);
-        HIPCHECK(hipEventRecord(ev_[3 * p + 2], stream_));
         // MV field / reference update and K7 deblocking run after the packets are done:
         // the host only waits for ev_[3p+2]; the next frame's work queues behind the update.
+        // (An event record captured inside one fused graph did not order the host wait
+        // after part 0 on ROCm 7: packets read back empty. Two launches it is.)
+        run_graph(graph_exec_[p], 0);
+        HIPCHECK(hipEventRecord(ev_[3 * p + 2], stream_));
         run_graph(post_exec_[p], 1);
         staged_ = false;
         launched_++;
