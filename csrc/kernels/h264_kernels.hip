@@ -188,6 +188,29 @@ struct AtomicBitWriter {
     }
 };
 
+// Per-lane staging writer (the lane owns `buf`, zeroed): plain LDS read-modify-writes.
+// Bits past `cap` are only counted (ovf): that lane then writes its block again at
+// the final offset.
+struct StageBitWriter {
+    uint32_t* buf;
+    uint32_t pos;
+    uint32_t cap;
+    bool ovf;
+    __device__ void put(uint32_t code, int len) {
+        if (len <= 0) return;
+        if (pos + (uint32_t)len > cap) { ovf = true; pos += len; return; }
+        if (len < 32) code &= (1u << len) - 1u;
+        uint32_t wi = pos >> 5, sh = pos & 31;
+        if (sh + len <= 32) {
+            buf[wi] |= code << (32 - sh - len);
+        } else {
+            buf[wi] |= code >> (sh + len - 32);
+            buf[wi + 1] |= code << (64 - sh - len);
+        }
+        pos += len;
+    }
+};
+
 // ---------------------------------------------------------------------------
 // K1 + K3: colour conversion and damage detection.
 // Workgroup = 256 threads = one MB row segment of 16 MBs (256 x 16 pixels);
@@ -1279,9 +1302,13 @@ __global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
 
 // ---------------------------------------------------------------------------
 // K8: CAVLC, one wave per coded MB.
-// 4 waves per workgroup, one MB per wave (tables shared).
+// 4 waves per workgroup, one MB per wave (tables shared). Lanes 0..26 each code one
+// residual block ONCE into a private LDS stage; a wave scan of the bit counts gives
+// the offsets and the staged words are OR-ed into the MB's bit buffer.
+constexpr int kCavlcStageWords = 24;   // 768 bits per block; longer blocks are re-coded in place
 __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
     __shared__ uint32_t bits_w[4][kMbSlotBytes / 4];
+    __shared__ uint32_t stage_w[4][27 * kCavlcStageWords];
     __shared__ int16_t coef_w[4][kCoefPerMb];
     __shared__ MbInfo mb_w[4];   // the MB's info in LDS: nnz[] is indexed per lane (a private copy would spill)
     __shared__ CavlcTables T;
@@ -1343,6 +1370,8 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
         }
     }
     for (int i = l; i < kMbSlotBytes / 4; i += 64) bits[i] = 0;
+    uint32_t* stage_all = stage_w[threadIdx.x >> 6];
+    for (int i = l; i < 27 * kCavlcStageWords; i += 64) stage_all[i] = 0;
     const int16_t* gc = a.coefs + (size_t)idx * kCoefPerMb;
     for (int i = l; i < kCoefPerMb / 2; i += 64)
         reinterpret_cast<uint32_t*>(coef)[i] = reinterpret_cast<const uint32_t*>(gc)[i];
@@ -1385,16 +1414,28 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
         }
     }
     int nbits = 0;
+    uint32_t* stage = stage_all + (l < 27 ? l : 0) * kCavlcStageWords;
+    StageBitWriter sw{stage, 0, kCavlcStageWords * 32, false};
     if (act) {
-        BitCounter cnt;
-        cavlc_block(cnt, bc, maxn, nc, T);
-        nbits = cnt.n;
+        cavlc_block(sw, bc, maxn, nc, T);
+        nbits = (int)sw.pos;
     }
     int incl = wave_incl_scan(nbits);
     int off = hdr_bits + incl - nbits;
     if (act) {
-        AtomicBitWriter w{bits, (uint32_t)off};
-        cavlc_block(w, bc, maxn, nc, T);
+        if (!sw.ovf) {
+            const uint32_t sh = (uint32_t)off & 31;
+            uint32_t wi = (uint32_t)off >> 5;
+            for (int k = 0; k < (nbits + 31) >> 5; k++, wi++) {
+                const uint32_t v = stage[k];   // zero past nbits
+                atomicOr(&bits[wi], v >> sh);
+                const uint32_t lo = sh ? v << (32 - sh) : 0u;
+                if (lo) atomicOr(&bits[wi + 1], lo);
+            }
+        } else {
+            AtomicBitWriter w{bits, (uint32_t)off};
+            cavlc_block(w, bc, maxn, nc, T);
+        }
     }
     int total = hdr_bits + __shfl(incl, 63);
     wave_sync();
