@@ -325,6 +325,18 @@ __device__ __forceinline__ int me_sad(const FrameArgs& a, const uint8_t* refy, u
 constexpr int kWin = 8;
 constexpr int kWinWords = 10;  // words per LDS row (40 B)
 
+// This lane's 4-pixel share of win_sad (<= 1020, so two candidates pack into one
+// 32-bit wave sum: 64 x 1020 < 65536).
+__device__ __forceinline__ uint32_t win_sad_lane(const uint32_t* win, uint32_t sw, int ox, int oy) {
+    const int l = lane_id();
+    const int row = l >> 2, col4 = (l & 3) * 4;
+    const int bc = col4 + ox + kWin;
+    const uint32_t* w = win + (row + oy + kWin) * kWinWords + (bc >> 2);
+    const int sh = bc & 3;
+    const uint32_t rw = sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+    return __builtin_amdgcn_sad_u8(sw, rw, 0u);
+}
+
 __device__ __forceinline__ int win_sad(const uint32_t* win, uint32_t sw, int ox, int oy) {
     const int l = lane_id();
     const int row = l >> 2, col4 = (l & 3) * 4;
@@ -392,6 +404,32 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
     const int ddx[4] = {0, -1, 1, 0}, ddy[4] = {-1, 0, 0, 1};
     for (int it = 0; it < a.me_iters; it++) {
         int nb = -1, ncost = bcost, nsad = 0;
+        // common case: the whole diamond lies in the LDS window -> 4 SADs in two
+        // packed wave sums (independent chains) instead of four sequential ones
+        bool all_in = true;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int ox = bx + ddx[k] - cx0, oy = by + ddy[k] - cy0;
+            all_in = all_in && ox >= -kWin && ox <= kWin && oy >= -kWin && oy <= kWin;
+        }
+        if (all_in) {
+            uint32_t p[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) p[k] = win_sad_lane(win, sw, bx + ddx[k] - cx0, by + ddy[k] - cy0);
+            const uint32_t s01 = (uint32_t)wave_sum((int)(p[0] | (p[1] << 16)));
+            const uint32_t s23 = (uint32_t)wave_sum((int)(p[2] | (p[3] << 16)));
+            const int sds[4] = {(int)(s01 & 0xffff), (int)(s01 >> 16), (int)(s23 & 0xffff), (int)(s23 >> 16)};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                int x = bx + ddx[k], y = by + ddy[k];
+                if (x < -R || x > R || y < -R || y > R) continue;
+                int c = sds[k] + lam * (sk_se_bits(4 * x) + sk_se_bits(4 * y));
+                if (c < ncost) { ncost = c; nb = k; nsad = sds[k]; }
+            }
+            if (nb < 0) break;
+            bx += ddx[nb]; by += ddy[nb]; bcost = ncost; bsad = nsad;
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             int x = bx + ddx[k], y = by + ddy[k];
