@@ -1078,28 +1078,28 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
 __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     __shared__ MbScratch Sw[4];
     __shared__ CavlcTables T;
-    load_cavlc_tables(T, a.cavlc_tabs);
-    __syncthreads();
     MbScratch& S = Sw[threadIdx.x >> 6];
     int nmb = a.mb_w * a.mb_h;
     int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
-    if (idx >= nmb) return;
-    int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    const bool valid = idx < nmb;
+    int mbx = valid ? idx % a.mb_w : 0, mby = valid ? idx / a.mb_w : 0;
     int s = mby / a.rows_per_slice;
     const SliceTask t = a.tasks[s];
     int l = lane_id();
-    if (t.final_action == ACT_SKIPALL) {
-        if (l == 0) {
-            MbInfo z;
-            memset(&z, 0, sizeof(z));
-            a.mbs[idx] = z;
-            a.me[idx].mvx = 0;
-            a.me[idx].mvy = 0;
-            a.me[idx].ref = 0;
-        }
-        return;
+    if (valid && t.final_action == ACT_SKIPALL && l == 0) {
+        MbInfo z;
+        memset(&z, 0, sizeof(z));
+        a.mbs[idx] = z;
+        a.me[idx].mvx = 0;
+        a.me[idx].mvy = 0;
+        a.me[idx].ref = 0;
     }
-    if (t.final_action != ACT_P) return;
+    // Blocks with no P macroblock (skipped / intra / out-of-range) leave before the table load.
+    const bool coded = valid && t.final_action == ACT_P;
+    if (!__syncthreads_or(coded)) return;
+    load_cavlc_tables(T, a.cavlc_tabs);
+    __syncthreads();
+    if (!coded) return;
     // MV prediction from the final motion field (all MBs of a P slice are inter)
     auto nbr = [&](int ox, int oy, bool ok) {
         MvNb n;
