@@ -22,6 +22,7 @@ how many concurrent 60 fps sessions that throughput sustains.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -49,7 +50,7 @@ def parse():
     p.add_argument("--qp", type=int, default=25)
     p.add_argument("--pool", type=int, default=16, help="pre-rendered frames per session pool")
     p.add_argument("--backend", default="hip", choices=["hip", "cpu"])
-    p.add_argument("--encoder", default="h264", choices=["h264", "jpeg"],
+    p.add_argument("--encoder", default="h264", choices=["h264", "jpeg", "hevc"],
                    help="h264 (headline, x264enc-striped equivalent) or jpeg stripes")
     p.add_argument("--jpeg-quality", type=int, default=40)
     p.add_argument("--deblock", type=int, default=0,
@@ -62,8 +63,56 @@ def parse():
     p.add_argument("--overlap", type=int, default=0,
                    help="1: upload frame n+1 while frame n encodes (upload/finish/launch); latency is "
                         "measured from the frame's upload to its packets")
-    p.add_argument("--gather", action="store_true", help="gather all packets to rank 0 over RCCL each step")
+    p.add_argument("--gather", action="store_true", help="gather all packets to rank 0 over RCCL each step "
+                   "(--path encoder only)")
+    p.add_argument("--path", default="capture", choices=["capture", "encoder"],
+                   help="capture: the production capture sessions (csrc/runtime/capture.cpp: native loop, "
+                        "grab -> upload -> launch with two frames in flight -> packets -> per-frame callback), "
+                        "driven in step mode from a pinned frame pool; encoder: Python threads calling the "
+                        "encoder API directly")
     return p.parse_args()
+
+
+def run_capture_path(args, pool, local_rank):
+    """Times the production serving loop: S native capture sessions on this GPU.
+
+    Each session is a pixelflux ScreenCapture whose frame source is the pinned
+    pool (source 4) in step mode: sk_capture_run grants K frames, the native loop
+    grabs, uploads, launches (two frames in flight) and collects packets exactly
+    as when serving a display; Python only waits.
+    """
+    import pixelflux
+    S = args.sessions
+    H, W = pool.array.shape[1], pool.array.shape[2]
+    caps = []
+    null_cb = ctypes.cast(None, pixelflux.FrameCallback)   # packets stay native: bytes counted in stats()
+
+    for i in range(S):
+        if args.encoder == "jpeg":
+            mode = pixelflux.OUTPUT_MODE_JPEG
+        elif args.encoder == "hevc":
+            mode = pixelflux.OUTPUT_MODE_HEVC
+        else:
+            mode = pixelflux.OUTPUT_MODE_H264
+        cs = pixelflux.default_settings(W, H, output_mode=mode, h264_crf=args.qp, use_paint_over_quality=0,
+                                        jpeg_quality=args.jpeg_quality, stripe_height=args.stripe_height,
+                                        h264_fullframe=int(args.mode == "fullframe"), device=local_rank,
+                                        use_cpu=int(args.backend == "cpu"), source=pixelflux.SOURCE_POOL,
+                                        step_mode=1, pool_frames=args.pool, pool_stride=W * 4,
+                                        pool_phase=3 * i)
+        cs.pool = pool.array.ctypes.data
+        c = pixelflux.ScreenCapture()
+        c.start_frame_capture(cs, null_cb)
+        caps.append(c)
+
+    def run_all(count):
+        for c in caps:
+            c.run(count)
+        for c in caps:
+            if c.wait(600_000) != 0:
+                raise RuntimeError("capture session did not deliver its frames")
+
+    return caps, run_all
 
 
 def main():
@@ -101,7 +150,11 @@ def main():
     pool = PinnedBuffer((args.pool, H, W, 4))
     for i in range(args.pool):
         src.frame(i, out=pool.array[i])
-    if args.encoder == "jpeg":
+    caps = None
+    if args.path == "capture":
+        caps, run_caps = run_capture_path(args, pool, local_rank)
+        encs = []
+    elif args.encoder == "jpeg":
         encs = [JpegEncoder(W, H, stripe_height=args.stripe_height, quality=args.jpeg_quality, use_paint_over=False,
                             device=local_rank, backend=args.backend) for _ in range(S)]
     else:
@@ -177,13 +230,22 @@ def main():
         for x in th:
             x.join()
 
-    run_all(0, args.warmup, False)
+    if caps is not None:
+        run_caps(args.warmup)
+        for c in caps:
+            c.latencies(reset=True)
+        bytes0 = [c.stats()["bytes"] for c in caps]
+    else:
+        run_all(0, args.warmup, False)
 
     if dist is not None:
         dist.barrier()
         sync()
     t0 = time.perf_counter()
-    run_all(args.warmup, args.steps, True)
+    if caps is not None:
+        run_caps(args.steps)
+    else:
+        run_all(args.warmup, args.steps, True)
     gather_bytes = 0
     if args.gather and dist is not None:
         # single-server topology: every rank's packets are gathered to rank 0 over xGMI in one step
@@ -197,7 +259,11 @@ def main():
     elapsed = time.perf_counter() - t0
 
     frames = S * args.steps
-    all_lat = np.concatenate([np.asarray(x) for x in lat]) * 1e3
+    if caps is not None:
+        all_lat = np.concatenate([np.asarray(c.latencies(), dtype=np.float64) for c in caps])
+        nbytes = [c.stats()["bytes"] - b for c, b in zip(caps, bytes0)]
+    else:
+        all_lat = np.concatenate([np.asarray(x) for x in lat]) * 1e3
     stats = np.array([elapsed, frames, sum(nbytes), np.percentile(all_lat, 50), np.percentile(all_lat, 99)],
                      dtype=np.float64)
     if dist is not None:
@@ -229,7 +295,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(fps / BASELINE_FPS, 3),
             "dtype": "uint8 pixels / int32 integer transforms (bit-exact vs CPU reference)",
-            "data": f"synthetic X11-like framebuffer ({args.content}), pinned host pool of {args.pool} frames",
+            "data": f"synthetic X11-like framebuffer ({args.content}), pinned host pool of {args.pool} frames"
+                    + (", served through native capture sessions (step mode)" if args.path == "capture" else ""),
             "p50_encode_latency_ms": round(p50, 3),
             "p99_encode_latency_ms": round(p99, 3),
             "concurrent_60fps_sessions": int(fps // 60) if p99 < 1000.0 / 60 else None,
@@ -248,8 +315,9 @@ def main():
                 "deblock": bool(args.deblock) if args.encoder == "h264" else None,
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
                 "bands_per_session": args.bands,
-                "upload_overlap": bool(args.overlap),
-                "frames_in_flight": 2 if args.overlap >= 2 else 1,
+                "path": args.path,
+                "upload_overlap": bool(args.overlap) or args.path == "capture",
+                "frames_in_flight": 2 if (args.overlap >= 2 or args.path == "capture") else 1,
                 "num_refs": args.num_refs,
                 "numa_node_rank0": numa_node,
             },
@@ -257,6 +325,8 @@ def main():
         print(json.dumps(res), flush=True)
     for e in encs:
         e.close()
+    for c in caps or []:
+        c.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -14,6 +14,10 @@ class FrameSource {
     // Captures one frame; returns a pointer to BGRx pixels (valid until the next
     // grab) and the row stride in bytes, or nullptr on failure.
     virtual const uint8_t* grab(int* stride) = 0;
+    // A pointer returned by grab() stays valid for this many grabs (the one that
+    // returned it included): with ring() >= 2 the capture loop grabs and uploads
+    // frame n+1 while frame n is still being encoded.
+    virtual int ring() const { return 1; }
     virtual const char* name() const = 0;
 };
 
@@ -24,5 +28,9 @@ std::unique_ptr<FrameSource> make_x11_source(const char* display, int x, int y, 
 
 // Synthetic desktop (moving windows, scrolling text, a video-like region).
 std::unique_ptr<FrameSource> make_synthetic_source(int w, int h, int kind, uint32_t seed);
+
+// Caller-owned pool of `frames` BGRx frames (stride bytes per row, h rows each),
+// grabbed round robin starting at `phase`.
+std::unique_ptr<FrameSource> make_pool_source(const uint8_t* base, int frames, int stride, int h, int phase);
 
 }  // namespace sk

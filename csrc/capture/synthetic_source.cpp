@@ -36,21 +36,25 @@ class SyntheticSource : public FrameSource {
                             p[0] = 30; p[1] = 30; p[2] = 40;
                         }
             }
+        // kRing page-locked frames rendered round robin (FrameSource::ring())
         size_t bytes = (size_t)w * h * 4;
-        if (hipHostMalloc((void**)&frame_, bytes, hipHostMallocDefault) != hipSuccess) {
-            own_.resize(bytes);
-            frame_ = own_.data();
+        if (hipHostMalloc((void**)&ring_base_, bytes * kRing, hipHostMallocDefault) != hipSuccess) {
+            own_.resize(bytes * kRing);
+            ring_base_ = own_.data();
         } else {
             pinned_ = true;
         }
+        frame_bytes_ = bytes;
         vh_ = h / 6 > 16 ? h / 6 : 16;
         vw_ = w / 6 > 16 ? w / 6 : 16;
     }
     ~SyntheticSource() override {
-        if (pinned_) hipHostFree(frame_);
+        if (pinned_) hipHostFree(ring_base_);
     }
+    int ring() const override { return kRing; }
     const uint8_t* grab(int* stride) override {
         *stride = w_ * 4;
+        frame_ = ring_base_ + (size_t)(t_ % kRing) * frame_bytes_;
         const size_t row = (size_t)w_ * 4;
         if (kind_ == 2) {
             uint32_t* p = (uint32_t*)frame_;
@@ -99,14 +103,39 @@ class SyntheticSource : public FrameSource {
     int t_ = 0;
     uint32_t rng_;
     std::vector<uint8_t> page_, own_;
+    static constexpr int kRing = 2;
+    uint8_t* ring_base_ = nullptr;
     uint8_t* frame_ = nullptr;
+    size_t frame_bytes_ = 0;
     bool pinned_ = false;
+};
+
+// Caller-owned pool of pre-rendered frames (benchmarks, replay): grab() cycles
+// through them; the pool must outlive the session.
+class PoolSource : public FrameSource {
+   public:
+    PoolSource(const uint8_t* base, int frames, int stride, int h, int phase)
+        : base_(base), frames_(frames), stride_(stride), h_(h), t_(phase) {}
+    const uint8_t* grab(int* stride) override {
+        *stride = stride_;
+        return base_ + (size_t)(t_++ % frames_) * stride_ * h_;
+    }
+    int ring() const override { return frames_; }
+    const char* name() const override { return "pool"; }
+
+   private:
+    const uint8_t* base_;
+    int frames_, stride_, h_, t_;
 };
 
 }  // namespace
 
 std::unique_ptr<FrameSource> make_synthetic_source(int w, int h, int kind, uint32_t seed) {
     return std::unique_ptr<FrameSource>(new SyntheticSource(w, h, kind, seed));
+}
+
+std::unique_ptr<FrameSource> make_pool_source(const uint8_t* base, int frames, int stride, int h, int phase) {
+    return std::unique_ptr<FrameSource>(new PoolSource(base, frames, stride, h, phase));
 }
 
 }  // namespace sk

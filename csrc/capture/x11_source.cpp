@@ -86,18 +86,19 @@ class X11Source : public FrameSource {
    public:
     X11Source(int x, int y, int w, int h, bool cursor) : x_(x), y_(y), w_(w), h_(h), cursor_(cursor) {}
     ~X11Source() override {
-        if (dpy_) {
-            if (attached_) api_.ShmDetach(dpy_, &shm_);
-            if (img_) {
-                img_->data = nullptr;
-                api_.Free(img_);
+        for (Seg& g : seg_) {
+            if (dpy_ && g.attached) api_.ShmDetach(dpy_, &g.shm);
+            if (dpy_ && g.img) {
+                g.img->data = nullptr;
+                api_.Free(g.img);
             }
-            api_.CloseDisplay(dpy_);
         }
-        if (shm_.shmaddr && shm_.shmaddr != (char*)-1) {
-            if (registered_) hipHostUnregister(shm_.shmaddr);
-            shmdt(shm_.shmaddr);
-        }
+        if (dpy_) api_.CloseDisplay(dpy_);
+        for (Seg& g : seg_)
+            if (g.shm.shmaddr && g.shm.shmaddr != (char*)-1) {
+                if (g.registered) hipHostUnregister(g.shm.shmaddr);
+                shmdt(g.shm.shmaddr);
+            }
     }
     bool open(const char* display, std::string* err) {
         if (!api_.load(err)) return false;
@@ -115,52 +116,59 @@ class X11Source : public FrameSource {
             if (err) *err = "X screen depth < 24 not supported";
             return false;
         }
-        memset(&shm_, 0, sizeof(shm_));
-        img_ = api_.ShmCreateImage(dpy_, api_.DefVisual(dpy_, scr), 24, ZPixmap, nullptr, &shm_,
-                                   (unsigned)w_, (unsigned)h_);
-        if (!img_ || img_->bits_per_pixel != 32) {
-            if (err) *err = "XShmCreateImage failed (need 32 bpp)";
-            return false;
+        // kRing MIT-SHM images used round robin: a grabbed frame stays valid while the
+        // next one is captured (its H2D upload overlaps that grab, FrameSource::ring()).
+        for (Seg& g : seg_) {
+            memset(&g.shm, 0, sizeof(g.shm));
+            g.img = api_.ShmCreateImage(dpy_, api_.DefVisual(dpy_, scr), 24, ZPixmap, nullptr, &g.shm,
+                                        (unsigned)w_, (unsigned)h_);
+            if (!g.img || g.img->bits_per_pixel != 32) {
+                if (err) *err = "XShmCreateImage failed (need 32 bpp)";
+                return false;
+            }
+            size_t bytes = (size_t)g.img->bytes_per_line * g.img->height;
+            g.shm.shmid = shmget(IPC_PRIVATE, bytes, IPC_CREAT | 0600);
+            if (g.shm.shmid < 0) {
+                if (err) *err = "shmget failed";
+                return false;
+            }
+            g.shm.shmaddr = (char*)shmat(g.shm.shmid, nullptr, 0);
+            shmctl(g.shm.shmid, IPC_RMID, nullptr);
+            if (g.shm.shmaddr == (char*)-1) {
+                if (err) *err = "shmat failed";
+                return false;
+            }
+            g.img->data = g.shm.shmaddr;
+            g.shm.readOnly = False;
+            if (!api_.ShmAttach(dpy_, &g.shm)) {
+                if (err) *err = "XShmAttach failed";
+                return false;
+            }
+            g.attached = true;
+            api_.Sync(dpy_, False);
+            g.registered = hipHostRegister(g.shm.shmaddr, bytes, hipHostRegisterDefault) == hipSuccess;
         }
-        size_t bytes = (size_t)img_->bytes_per_line * img_->height;
-        shm_.shmid = shmget(IPC_PRIVATE, bytes, IPC_CREAT | 0600);
-        if (shm_.shmid < 0) {
-            if (err) *err = "shmget failed";
-            return false;
-        }
-        shm_.shmaddr = (char*)shmat(shm_.shmid, nullptr, 0);
-        shmctl(shm_.shmid, IPC_RMID, nullptr);
-        if (shm_.shmaddr == (char*)-1) {
-            if (err) *err = "shmat failed";
-            return false;
-        }
-        img_->data = shm_.shmaddr;
-        shm_.readOnly = False;
-        if (!api_.ShmAttach(dpy_, &shm_)) {
-            if (err) *err = "XShmAttach failed";
-            return false;
-        }
-        attached_ = true;
-        api_.Sync(dpy_, False);
-        registered_ = hipHostRegister(shm_.shmaddr, bytes, hipHostRegisterDefault) == hipSuccess;
         root_ = api_.DefRootWindow(dpy_);
         return true;
     }
     const uint8_t* grab(int* stride) override {
-        if (!api_.ShmGetImage(dpy_, root_, img_, x_, y_, AllPlanes)) return nullptr;
-        if (cursor_ && api_.FixesGetCursorImage) composite_cursor();
-        *stride = img_->bytes_per_line;
-        return (const uint8_t*)img_->data;
+        cur_ = (cur_ + 1) % kRing;
+        XImage* img = seg_[cur_].img;
+        if (!api_.ShmGetImage(dpy_, root_, img, x_, y_, AllPlanes)) return nullptr;
+        if (cursor_ && api_.FixesGetCursorImage) composite_cursor(img);
+        *stride = img->bytes_per_line;
+        return (const uint8_t*)img->data;
     }
+    int ring() const override { return kRing; }
     const char* name() const override { return "x11-shm"; }
 
    private:
     // K13: server-side cursor composite (small, CPU; alpha in ARGB32 longs)
-    void composite_cursor() {
+    void composite_cursor(XImage* img) {
         XFixesCursorImage_* ci = api_.FixesGetCursorImage(dpy_);
         if (!ci) return;
         int cx = ci->x - ci->xhot - x_, cy = ci->y - ci->yhot - y_;
-        uint8_t* base = (uint8_t*)img_->data;
+        uint8_t* base = (uint8_t*)img->data;
         for (int j = 0; j < ci->height; j++) {
             int py = cy + j;
             if (py < 0 || py >= h_) continue;
@@ -170,7 +178,7 @@ class X11Source : public FrameSource {
                 uint32_t argb = (uint32_t)ci->pixels[j * ci->width + i];
                 uint32_t a = argb >> 24;
                 if (!a) continue;
-                uint8_t* d = base + (size_t)py * img_->bytes_per_line + 4 * px;
+                uint8_t* d = base + (size_t)py * img->bytes_per_line + 4 * px;
                 for (int c = 0; c < 3; c++) {
                     uint32_t s = (argb >> (8 * c)) & 255;  // premultiplied B, G, R
                     d[c] = (uint8_t)(s + (d[c] * (255 - a) + 127) / 255);
@@ -182,12 +190,17 @@ class X11Source : public FrameSource {
 
     XApi api_;
     Display* dpy_ = nullptr;
-    XImage* img_ = nullptr;
-    XShmSegmentInfo_ shm_{};
+    static constexpr int kRing = 2;
+    struct Seg {
+        XShmSegmentInfo_ shm{};
+        XImage* img = nullptr;
+        bool attached = false, registered = false;
+    };
+    Seg seg_[kRing];
+    int cur_ = kRing - 1;
     Window root_ = 0;
     int x_, y_, w_, h_;
     bool cursor_;
-    bool attached_ = false, registered_ = false;
 };
 
 }  // namespace

@@ -10,6 +10,10 @@
 #include "trace.h"
 #include "../capture/frame_source.h"
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
 #include <chrono>
 #include <mutex>
 #include <string.h>
@@ -20,6 +24,16 @@
 
 
 namespace sk {
+
+// Sessions currently running per GPU (adjusted by `delta`; returns the new count).
+static int device_sessions(int device, int delta) {
+    static std::mutex mu;
+    static std::map<int, int> count;
+    std::lock_guard<std::mutex> g(mu);
+    int& c = count[device];
+    c += delta;
+    return c;
+}
 
 class CaptureSession {
    public:
@@ -47,8 +61,21 @@ class CaptureSession {
                 return -1;
             }
         }
+        pool_ = nullptr;
+        if (s.source == 4) {   // caller-owned frame pool (benchmarks / replay)
+            if (!s.pool || s.pool_frames < 1) {
+                set_last_error("pool source needs pool and pool_frames");
+                return -1;
+            }
+            pool_ = s.pool;
+            src_ = make_pool_source(s.pool, s.pool_frames, s.pool_stride > 0 ? s.pool_stride : w * 4, h, s.pool_phase);
+        }
         if (!src_) src_ = make_synthetic_source(w, h, s.source >= 1 ? s.source - 1 : 0, 0x1234567u);
         src_kind_ = strcmp(src_->name(), "x11-shm") == 0 ? 1.0 : 0.0;
+        {
+            std::lock_guard<std::mutex> g(step_mu_);
+            budget_ = target_ = delivered_ = 0;
+        }
         // encoder
         try {
             int backend = s.use_cpu ? 0 : (sk_hip_device_count() > 0 ? 1 : 0);
@@ -90,30 +117,60 @@ class CaptureSession {
             return -1;
         }
         running_ = true;
+        registered_device_ = s.use_cpu ? -1 : s.device;
+        if (registered_device_ >= 0) device_sessions(registered_device_, +1);
         th_ = std::thread([this] { loop(); });
         return 0;
     }
 
     void stop() {
         running_ = false;
+        {
+            std::lock_guard<std::mutex> g(step_mu_);
+            step_cv_.notify_all();
+        }
         if (th_.joinable()) th_.join();
+        if (registered_device_ >= 0) device_sessions(registered_device_, -1);
+        registered_device_ = -1;
         enc_.reset();
         src_.reset();
     }
 
     void request_keyframe() { key_req_ = true; }
     void set_qp(int qp, int paint_qp) { qp_req_ = (qp & 0xffff) | (paint_qp & 0xffff) << 16; }
+    void set_frame_callback(sk_frame_cb cb, void* user) {
+        frame_cb_ = cb;
+        frame_user_ = user;
+    }
 
     // Premultiplied BGRA watermark, composited onto every captured frame before
     // encoding. location: 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right,
     // 4 centre, 5 bouncing (moves 2 px per frame), 6 tiled; < 0 disables.
     // (pixelflux's own enum is not part of the reference tree; this mapping is ours.)
     void set_watermark(const uint8_t* bgra, int w, int h, int location) {
+        auto wm = std::make_shared<Watermark>();
+        wm->px.assign(bgra, bgra + (size_t)w * h * 4);
+        wm->w = w;
+        wm->h = h;
+        wm->loc = location;
         std::lock_guard<std::mutex> g(mu_);
-        wm_.assign(bgra, bgra + (size_t)w * h * 4);
-        wm_w_ = w;
-        wm_h_ = h;
-        wm_loc_ = location;
+        wm_ = std::move(wm);
+    }
+
+    // Step mode (sk_capture_settings.step_mode): the loop encodes exactly the frames
+    // granted here, unpaced, two in flight; wait() blocks until all are delivered.
+    void run(int64_t frames) {
+        std::lock_guard<std::mutex> g(step_mu_);
+        budget_ += frames;
+        target_ += frames;
+        step_cv_.notify_all();
+    }
+    int wait(int timeout_ms) {
+        std::unique_lock<std::mutex> g(step_mu_);
+        auto ok = [&] { return delivered_ >= target_ || !running_; };
+        if (timeout_ms < 0) step_cv_.wait(g, ok);
+        else if (!step_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms), ok)) return 1;
+        return delivered_ >= target_ ? 0 : -1;
     }
 
     // out: frames, mean encode ms, bytes, packets, source kind, last encode ms, then
@@ -127,70 +184,186 @@ class CaptureSession {
         for (int i = 0; i < kHist; i++) v[6 + i] = (double)hist_[i];
         for (int i = 0; i < n && i < 6 + kHist; i++) out[i] = v[i];
     }
+    // Capture-to-packets latency (ms) of the most recent frames, oldest first;
+    // returns the count copied. reset != 0 clears the record afterwards.
+    int latencies(float* out, int cap, int reset) {
+        std::lock_guard<std::mutex> g(mu_);
+        const int n = (int)std::min<uint64_t>(lat_count_, kLatRing);
+        int k = std::min(cap, n);
+        for (int i = 0; i < k; i++) out[i] = lat_[(lat_count_ - k + i) % kLatRing];
+        if (reset) lat_count_ = 0;
+        return k;
+    }
 
    private:
+    struct Watermark {
+        std::vector<uint8_t> px;
+        int w = 0, h = 0, loc = -1;
+    };
+    using clk = std::chrono::steady_clock;
+    struct InFlight {
+        uint16_t id;
+        clk::time_point t_grab;
+    };
+
+    // Grabs, composites the watermark, uploads and launches frame `id`. Returns false
+    // when the source has no frame (the caller retries at the next tick).
+    bool start_frame(uint16_t id, std::deque<InFlight>& q) {
+        int stride = 0;
+        const uint8_t* px = nullptr;
+        const auto t = clk::now();
+        {
+            trace::Range r("capture.grab");
+            px = src_->grab(&stride);
+        }
+        if (!px) return false;
+        std::shared_ptr<Watermark> wm;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            wm = wm_;
+        }
+        // the grab buffer is ours (SHM segment / ring / copy of a pool frame is not made:
+        // pool frames are never composited)
+        if (wm && wm->loc >= 0 && !wm->px.empty() && pool_ == nullptr)
+            composite_watermark(const_cast<uint8_t*>(px), stride, id, *wm);
+        try {
+            if (enc_->upload(px, stride, id) < 0 || enc_->launch() < 0) return false;
+        } catch (const std::exception& ex) {
+            set_last_error(ex.what());
+            return false;
+        }
+        q.push_back({id, t});
+        return true;
+    }
+
+    void deliver(const InFlight& f, int n) {
+        const double ms = std::chrono::duration<double, std::milli>(clk::now() - f.t_grab).count();
+        size_t bytes = 0;
+        std::vector<sk_stripe_result> res((size_t)std::max(n, 0));
+        for (int i = 0; i < n; i++) {
+            h264::EncodedPacket& p = enc_->packets_[i];
+            sk_stripe_result& r = res[i];
+            r.type = s_.output_mode == 0 ? 0 : (s_.output_mode == 2 ? 2 : 1);
+            r.stripe_y_start = p.y;
+            r.stripe_height = p.h;
+            r.size = (int32_t)p.data.size();
+            r.data = p.data.data();
+            r.frame_id = f.id;
+            bytes += p.data.size();
+        }
+        if (frame_cb_) frame_cb_(res.data(), n, frame_user_);   // one call per frame
+        else if (cb_)
+            for (int i = 0; i < n; i++) cb_(&res[i], user_);      // pixelflux contract: per stripe
+        std::lock_guard<std::mutex> g(mu_);
+        frames_++;
+        int b = 0;
+        while (b < kHist - 1 && ms > kHistLe[b]) b++;
+        hist_[b]++;
+        enc_ms_sum_ += ms;
+        last_enc_ms_ = ms;
+        bytes_ += bytes;
+        packets_ += n > 0 ? n : 0;
+        lat_[lat_count_++ % kLatRing] = (float)ms;
+    }
+
+    // A granted frame that could not be grabbed/launched counts as delivered (with
+    // no packets), so wait() cannot hang on a failing source or encoder.
+    void step_failed() {
+        std::lock_guard<std::mutex> g(step_mu_);
+        delivered_++;
+        step_cv_.notify_all();
+    }
+
+    // Production loop. Paced (target_fps): grab at each tick, encode, deliver at
+    // once (latency first). When the encoder falls behind the tick, or in step
+    // mode, frame n+1 is grabbed, uploaded and launched before frame n is
+    // finished, so the GPU always has the next frame queued (two in flight; needs
+    // a source whose grab buffers survive one more grab, FrameSource::ring()).
     void loop() {
-        using clk = std::chrono::steady_clock;
         const double fps = s_.target_fps > 0 ? s_.target_fps : 60.0;
         const auto period = std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(1.0 / fps));
+        const bool step = s_.step_mode != 0;
+        // Two frames in flight pay off for a session that has its GPU to itself (the
+        // copy of frame n+1 overlaps the kernels of frame n). With several sessions
+        // on one GPU the others fill those gaps, and the extra queued work only
+        // lengthens the in-order hardware queues (GPU_MAX_HW_QUEUES = 4 shared by
+        // every stream): measured 5587 fps with one in flight vs 4567 with two, 8
+        // sessions at 1080p (profiles/r2_capture_pipeline.md). SK_CAPTURE_INFLIGHT
+        // (1 or 2) overrides.
+        const char* inflight_env = getenv("SK_CAPTURE_INFLIGHT");
+        const int forced = inflight_env ? atoi(inflight_env) : 0;
+        auto overlap_now = [&]() {
+            if (src_->ring() < 2 || forced == 1) return false;
+            return forced == 2 || device_sessions(s_.device, 0) <= 1;
+        };
         auto next = clk::now();
         uint16_t frame_id = 0;
+        std::deque<InFlight> q;
+        auto take_budget = [&](bool block) -> bool {   // step mode: one frame of budget
+            std::unique_lock<std::mutex> g(step_mu_);
+            if (block) step_cv_.wait_for(g, std::chrono::milliseconds(50), [&] { return budget_ > 0 || !running_; });
+            if (budget_ <= 0 || !running_) return false;
+            budget_--;
+            return true;
+        };
         while (running_) {
             if (key_req_.exchange(false)) enc_->request_keyframe();
-            if (int q = qp_req_.exchange(0)) enc_->set_qp(q & 0xffff, q >> 16);
-            int stride = 0;
-            const uint8_t* px = nullptr;
-            {
-                trace::Range r("capture.grab");
-                px = src_->grab(&stride);
-            }
-            if (px && wm_loc_ >= 0 && !wm_.empty()) composite_watermark(const_cast<uint8_t*>(px), stride, frame_id);
-            if (px) {
-                auto t0 = clk::now();
-                int n = -1;
-                try {
-                    n = enc_->encode(px, stride, frame_id);
-                } catch (const std::exception& ex) {
-                    set_last_error(ex.what());
-                    n = -1;
+            if (int qq = qp_req_.exchange(0)) enc_->set_qp(qq & 0xffff, qq >> 16);
+            if (q.empty()) {
+                if (step) {
+                    if (!take_budget(true)) continue;
+                } else {
+                    auto now = clk::now();
+                    if (next > now) std::this_thread::sleep_until(next);
+                    next += period;
+                    if (next < clk::now()) next = clk::now();   // behind schedule: do not burst
                 }
-                double ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-                size_t bytes = 0;
-                for (int i = 0; i < n; i++) {
-                    h264::EncodedPacket& p = enc_->packets_[i];
-                    sk_stripe_result r;
-                    r.type = s_.output_mode == 0 ? 0 : 1;
-                    r.stripe_y_start = p.y;
-                    r.stripe_height = p.h;
-                    r.size = (int32_t)p.data.size();
-                    r.data = p.data.data();
-                    r.frame_id = frame_id;
-                    bytes += p.data.size();
-                    if (cb_) cb_(&r, user_);
-                }
-                {
-                    std::lock_guard<std::mutex> g(mu_);
-                    frames_++;
-                    int b = 0;
-                    while (b < kHist - 1 && ms > kHistLe[b]) b++;
-                    hist_[b]++;
-                    enc_ms_sum_ += ms;
-                    last_enc_ms_ = ms;
-                    bytes_ += bytes;
-                    packets_ += n > 0 ? n : 0;
+                if (!start_frame(frame_id, q)) {
+                    if (step) step_failed();
+                    continue;
                 }
                 frame_id++;
             }
-            next += period;
-            auto now = clk::now();
-            if (next < now) next = now;  // behind schedule: do not burst
-            else std::this_thread::sleep_until(next);
+            // queue the next frame behind the one in flight when there is no time to idle
+            if (q.size() < 2 && overlap_now()) {
+                bool go = step ? take_budget(false) : clk::now() >= next;
+                if (go) {
+                    if (!step) {
+                        next += period;
+                        if (next < clk::now()) next = clk::now();
+                    }
+                    if (start_frame(frame_id, q)) frame_id++;
+                    else if (step) step_failed();
+                }
+            }
+            int n = -1;
+            try {
+                n = enc_->finish();
+            } catch (const std::exception& ex) {
+                set_last_error(ex.what());
+            }
+            InFlight f = q.front();
+            q.pop_front();
+            deliver(f, n);
+            if (step) {
+                std::lock_guard<std::mutex> g(step_mu_);
+                delivered_++;
+                step_cv_.notify_all();
+            }
         }
+        while (!q.empty()) {   // drain (the encoder is destroyed after the thread ends)
+            try {
+                enc_->finish();
+            } catch (const std::exception&) {
+            }
+            q.pop_front();
+        }
+        std::lock_guard<std::mutex> g(step_mu_);
+        step_cv_.notify_all();
     }
 
-    void composite_watermark(uint8_t* px, int stride, unsigned t) {
-        std::lock_guard<std::mutex> g(mu_);
-        const int W = s_.capture_width, H = s_.capture_height, w = wm_w_, h = wm_h_;
+    void composite_watermark(uint8_t* px, int stride, unsigned t, const Watermark& wmk) {
+        const int W = s_.capture_width, H = s_.capture_height, w = wmk.w, h = wmk.h;
         auto blit = [&](int x0, int y0) {
             for (int j = 0; j < h; j++) {
                 const int y = y0 + j;
@@ -198,7 +371,7 @@ class CaptureSession {
                 for (int i = 0; i < w; i++) {
                     const int x = x0 + i;
                     if (x < 0 || x >= W) continue;
-                    const uint8_t* s = &wm_[((size_t)j * w + i) * 4];
+                    const uint8_t* s = &wmk.px[((size_t)j * w + i) * 4];
                     const uint32_t a = s[3];
                     if (!a) continue;
                     uint8_t* d = px + (size_t)y * stride + 4 * x;
@@ -207,7 +380,7 @@ class CaptureSession {
             }
         };
         const int m = 16;  // margin
-        switch (wm_loc_) {
+        switch (wmk.loc) {
             case 0: blit(m, m); break;
             case 1: blit(W - w - m, m); break;
             case 2: blit(m, H - h - m); break;
@@ -227,8 +400,17 @@ class CaptureSession {
         }
     }
 
-    std::vector<uint8_t> wm_;
-    int wm_w_ = 0, wm_h_ = 0, wm_loc_ = -1;
+    std::shared_ptr<Watermark> wm_;
+    int registered_device_ = -1;
+    const uint8_t* pool_ = nullptr;
+    sk_frame_cb frame_cb_ = nullptr;
+    void* frame_user_ = nullptr;
+    std::mutex step_mu_;
+    std::condition_variable step_cv_;
+    int64_t budget_ = 0, target_ = 0, delivered_ = 0;
+    static constexpr int kLatRing = 8192;
+    float lat_[kLatRing] = {};
+    uint64_t lat_count_ = 0;
     sk_capture_settings s_{};
     std::string display_;
     sk_stripe_cb cb_ = nullptr;
@@ -253,7 +435,17 @@ extern "C" {
 void* sk_capture_create(void) { return new CaptureSession(); }
 void sk_capture_destroy(void* c) { delete static_cast<CaptureSession*>(c); }
 int sk_capture_start(void* c, const sk_capture_settings* s, sk_stripe_cb cb, void* user) {
+    static_cast<CaptureSession*>(c)->set_frame_callback(nullptr, nullptr);
     return static_cast<CaptureSession*>(c)->start(*s, cb, user);
+}
+int sk_capture_start_frames(void* c, const sk_capture_settings* s, sk_frame_cb cb, void* user) {
+    static_cast<CaptureSession*>(c)->set_frame_callback(cb, user);
+    return static_cast<CaptureSession*>(c)->start(*s, nullptr, nullptr);
+}
+void sk_capture_run(void* c, int64_t frames) { static_cast<CaptureSession*>(c)->run(frames); }
+int sk_capture_wait(void* c, int timeout_ms) { return static_cast<CaptureSession*>(c)->wait(timeout_ms); }
+int sk_capture_latencies(void* c, float* out, int cap, int reset) {
+    return static_cast<CaptureSession*>(c)->latencies(out, cap, reset);
 }
 void sk_capture_stop(void* c) { static_cast<CaptureSession*>(c)->stop(); }
 void sk_capture_request_keyframe(void* c) { static_cast<CaptureSession*>(c)->request_keyframe(); }

@@ -53,6 +53,7 @@ class HipBackend : public EncoderBackend {
         for (auto* b : bgrx_dev_)
             if (b) hipFree(b);
         hipStreamDestroy(stream_);
+        if (up_stream_) hipStreamDestroy(up_stream_);
     }
 
     // Picked up by k_plan at the start of the next frame.
@@ -102,7 +103,11 @@ class HipBackend : public EncoderBackend {
         // the uploads of all encoders on this GPU run back to back at full PCIe rate
         // instead of contending (one copy queue, not one per session).
         hipStream_t cs = stream_;
-        if (copy_stream_ || inflight()) cs = copy_stream_ ? copy_stream_ : device_copy_stream(device_);
+        // Overlapped upload of a session: its own upload stream (the copies of many
+        // sessions then spread over the SDMA engines; SK_SHARED_UPLOAD=1 funnels them
+        // through the device's one shared copy stream instead).
+        if (copy_stream_) cs = copy_stream_;
+        else if (inflight() && upload_mode_ != 0) cs = upload_mode_ == 2 ? device_copy_stream(device_) : upload_stream();
         // the last reader of bgrx_dev_[q] is the graph two frames back: finished
         HIPCHECK(hipEventRecord(ev_[3 * q], cs));
         HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyHostToDevice, cs));
@@ -552,6 +557,14 @@ class HipBackend : public EncoderBackend {
     hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
     hipStream_t copy_stream_ = nullptr;   // shared per device (not owned)
+    hipStream_t up_stream_ = nullptr;     // this session's upload stream (owned, lazily created)
+    // 0: on the session stream (behind the frame in flight), 1: own upload stream,
+    // 2: the device's shared copy stream
+    int upload_mode_ = getenv("SK_UPLOAD_MODE") ? atoi(getenv("SK_UPLOAD_MODE")) : 2;
+    hipStream_t upload_stream() {
+        if (!up_stream_) HIPCHECK(hipStreamCreateWithFlags(&up_stream_, hipStreamNonBlocking));
+        return up_stream_;
+    }
 
     // One H2D stream per device for encoders created with shared_copy: lives as long
     // as the process (encoders come and go, the stream is reused).

@@ -91,10 +91,13 @@ typedef struct sk_capture_settings {
     int32_t source;          // -1 auto (X11 if reachable), 0 X11 only, 1/2/3 synthetic motion/desktop/noise
     const char* display;     // X display name (nullptr -> $DISPLAY)
     int32_t output_width, output_height;  // H.264 stream size if it differs from the capture (K2); 0 = same
+    int32_t step_mode;       // 1: encode only frames granted by sk_capture_run, unpaced (benchmarks)
+    const uint8_t* pool;     // source 4: caller-owned BGRx frames (pool_frames x capture_height rows)
+    int32_t pool_frames, pool_stride, pool_phase;
 } sk_capture_settings;
 
 typedef struct sk_stripe_result {
-    int32_t type;            // 0 = JPEG stripe, 1 = H.264 stripe/frame
+    int32_t type;            // 0 = JPEG stripe, 1 = H.264 stripe/frame, 2 = HEVC stripe/frame
     int32_t stripe_y_start;
     int32_t stripe_height;
     int32_t size;
@@ -103,11 +106,21 @@ typedef struct sk_stripe_result {
 } sk_stripe_result;
 
 typedef void (*sk_stripe_cb)(sk_stripe_result*, void*);
+// One call per encoded frame with all of its stripe packets (n may be 0).
+typedef void (*sk_frame_cb)(const sk_stripe_result*, int32_t n, void*);
 
 void* sk_capture_create(void);
 void sk_capture_destroy(void* c);
 // Starts the capture thread; cb runs on that thread once per stripe packet.
 int sk_capture_start(void* c, const sk_capture_settings* s, sk_stripe_cb cb, void* user);
+// Same session, one callback per frame instead of one per stripe.
+int sk_capture_start_frames(void* c, const sk_capture_settings* s, sk_frame_cb cb, void* user);
+// Step mode: grant `frames` more frames; wait blocks until every granted frame is
+// delivered (0), times out (1, timeout_ms >= 0) or the session stopped (-1).
+void sk_capture_run(void* c, int64_t frames);
+int sk_capture_wait(void* c, int timeout_ms);
+// Capture-to-packets latency in ms of the most recent frames (oldest first).
+int sk_capture_latencies(void* c, float* out, int cap, int reset);
 void sk_capture_stop(void* c);
 void sk_capture_request_keyframe(void* c);
 void sk_capture_set_qp(void* c, int qp, int paint_qp);

@@ -26,9 +26,14 @@ CaptureSettings = _native.SkCaptureSettings
 ENCODE_MS_BUCKETS = (0.25, 0.5, 1, 2, 4, 8, 16, 33, float("inf"))   # csrc/runtime/capture.cpp kHistLe
 StripeEncodeResult = _native.SkStripeResult
 StripeCallback = _native.SK_STRIPE_CB
+# Extension: one call per encoded frame, (results pointer, count, user), so a
+# consumer pays one Python call per frame instead of one per stripe.
+FrameCallback = _native.SK_FRAME_CB
 
 OUTPUT_MODE_JPEG = 0
 OUTPUT_MODE_H264 = 1
+OUTPUT_MODE_HEVC = 2   # extension: H.265 stripes
+SOURCE_POOL = 4        # extension: caller-owned frame pool (settings.pool / pool_frames)
 
 
 def default_settings(width: int = 1920, height: int = 1080, **kw) -> CaptureSettings:
@@ -51,6 +56,9 @@ def default_settings(width: int = 1920, height: int = 1080, **kw) -> CaptureSett
     s.stripe_height = 64
     s.source = -1
     s.display = None
+    s.step_mode = 0
+    s.pool = None
+    s.pool_frames = s.pool_stride = s.pool_phase = 0
     for k, v in kw.items():
         if isinstance(v, str):
             v = v.encode()
@@ -95,6 +103,34 @@ class ScreenCapture:
             if rc != 0:
                 self._cb = None
                 raise RuntimeError(f"start_capture failed: {self._lib.sk_last_error().decode()}")
+
+    def start_frame_capture(self, settings: CaptureSettings, callback) -> None:
+        """Like start_capture, but ``callback(results, n, user)`` runs once per frame."""
+        if not isinstance(callback, FrameCallback):
+            callback = FrameCallback(callback)
+        if settings.watermark_path and settings.watermark_location_enum >= 0:
+            self.set_watermark(settings.watermark_path.decode(), settings.watermark_location_enum)
+        with self._lock:
+            self._cb = callback
+            self._settings = settings
+            rc = self._lib.sk_capture_start_frames(self._h, ctypes.byref(settings), callback, None)
+            if rc != 0:
+                self._cb = None
+                raise RuntimeError(f"start_capture failed: {self._lib.sk_last_error().decode()}")
+
+    def run(self, frames: int) -> None:
+        """Step mode (settings.step_mode = 1): grant `frames` more frames (non-blocking)."""
+        self._lib.sk_capture_run(self._h, int(frames))
+
+    def wait(self, timeout_ms: int = -1) -> int:
+        """Blocks until every granted frame is delivered: 0, 1 on timeout, -1 if stopped."""
+        return int(self._lib.sk_capture_wait(self._h, int(timeout_ms)))
+
+    def latencies(self, reset: bool = False, cap: int = 8192) -> list:
+        """Capture-to-packets latency (ms) of the most recent frames, oldest first."""
+        arr = (ctypes.c_float * cap)()
+        n = self._lib.sk_capture_latencies(self._h, arr, cap, int(reset))
+        return list(arr[:n])
 
     def stop_capture(self) -> None:
         with self._lock:

@@ -61,6 +61,8 @@ class SkCaptureSettings(ctypes.Structure):
         ("device", ctypes.c_int32), ("stripe_height", ctypes.c_int32), ("source", ctypes.c_int32),
         ("display", ctypes.c_char_p),
         ("output_width", ctypes.c_int32), ("output_height", ctypes.c_int32),
+        ("step_mode", ctypes.c_int32), ("pool", ctypes.c_void_p),
+        ("pool_frames", ctypes.c_int32), ("pool_stride", ctypes.c_int32), ("pool_phase", ctypes.c_int32),
     ]
 
 
@@ -70,6 +72,7 @@ class SkStripeResult(ctypes.Structure):
 
 
 SK_STRIPE_CB = ctypes.CFUNCTYPE(None, ctypes.POINTER(SkStripeResult), ctypes.c_void_p)
+SK_FRAME_CB = ctypes.CFUNCTYPE(None, ctypes.POINTER(SkStripeResult), ctypes.c_int32, ctypes.c_void_p)
 
 
 class SkPacket(ctypes.Structure):
@@ -120,6 +123,14 @@ def lib():
         L.sk_capture_start.argtypes = [ctypes.c_void_p, ctypes.POINTER(SkCaptureSettings), SK_STRIPE_CB,
                                        ctypes.c_void_p]
         L.sk_capture_start.restype = ctypes.c_int
+        L.sk_capture_start_frames.argtypes = [ctypes.c_void_p, ctypes.POINTER(SkCaptureSettings), SK_FRAME_CB,
+                                              ctypes.c_void_p]
+        L.sk_capture_start_frames.restype = ctypes.c_int
+        L.sk_capture_run.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        L.sk_capture_wait.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.sk_capture_wait.restype = ctypes.c_int
+        L.sk_capture_latencies.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int]
+        L.sk_capture_latencies.restype = ctypes.c_int
         L.sk_capture_stop.argtypes = [ctypes.c_void_p]
         L.sk_capture_request_keyframe.argtypes = [ctypes.c_void_p]
         L.sk_capture_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]

@@ -21,6 +21,7 @@ MI355X-first differences:
 from __future__ import annotations
 
 import asyncio
+import ctypes
 import json
 import logging
 import os
@@ -47,10 +48,31 @@ VIDEO_KEYS = ("encoder", "framerate", "h264_crf", "h264_fullcolor", "h264_stream
               "use_paint_over_quality")
 
 
-class Client:
-    """One websocket connection with its own ordered outbound queue."""
+class _VideoFrame:
+    """All stripe messages of one encoded frame, queued as one unit."""
+    __slots__ = ("msgs", "key")
 
-    def __init__(self, ws: web.WebSocketResponse, remote: str, meter: BandwidthMeter):
+    def __init__(self, msgs: list, key: bool):
+        self.msgs = msgs
+        self.key = key
+
+
+class Client:
+    """One websocket connection with its own ordered outbound queue.
+
+    Video is bounded per viewer: at most ``MAX_VIDEO_FRAMES`` encoded frames may
+    wait in the queue. A slower viewer loses whole frames (never a partial one),
+    and once its queue has drained it asks for a keyframe through ``on_resync``
+    and skips delta frames until one arrives, so its decoders resynchronise. The
+    reference skips websockets above the write high-water mark in
+    ``websockets.broadcast`` (selkies.py:2818); control and text messages here are
+    never dropped.
+    """
+
+    MAX_VIDEO_FRAMES = 8   # ~133 ms at 60 fps
+
+    def __init__(self, ws: web.WebSocketResponse, remote: str, meter: BandwidthMeter,
+                 on_resync: Optional[Callable[["Client"], None]] = None):
         self.ws = ws
         self.remote = remote
         self.meter = meter
@@ -58,6 +80,10 @@ class Client:
         self.writer = asyncio.create_task(self._write())
         self.display_id: Optional[str] = None
         self.closed = False
+        self.on_resync = on_resync
+        self.video_queued = 0        # video frames waiting in self.out
+        self.video_state = "live"    # live | dropping (queue full) | awaiting_key (resync requested)
+        self.frames_dropped = 0
 
     async def _write(self):
         try:
@@ -65,6 +91,16 @@ class Client:
                 msg = await self.out.get()
                 if msg is None:
                     break
+                if isinstance(msg, _VideoFrame):
+                    for m in msg.msgs:
+                        await self.ws.send_bytes(m)
+                        self.meter.add(len(m))
+                    self.video_queued -= 1
+                    if self.video_state == "dropping" and self.video_queued == 0:
+                        self.video_state = "awaiting_key"
+                        if self.on_resync is not None:
+                            self.on_resync(self)
+                    continue
                 if isinstance(msg, (bytes, bytearray)):
                     await self.ws.send_bytes(msg)
                 else:
@@ -79,6 +115,30 @@ class Client:
         if self.closed or self.ws.closed:
             return False
         self.out.put_nowait(msg)
+        return True
+
+    def send_video(self, msgs: list, key: bool, independent: bool = False) -> bool:
+        """Queues one frame's stripe messages; False if this viewer dropped it.
+
+        ``independent``: every message decodes on its own (JPEG stripes), so a
+        dropped frame needs no keyframe to recover from.
+        """
+        if self.closed or self.ws.closed:
+            return False
+        if self.video_state == "awaiting_key":
+            if not (key or independent):
+                self.frames_dropped += 1
+                return False
+            self.video_state = "live"
+        if self.video_state == "dropping" or self.video_queued >= self.MAX_VIDEO_FRAMES:
+            if self.video_state == "live":
+                log.warning("viewer %s is %d frames behind: dropping video until it drains",
+                            self.remote, self.video_queued)
+                self.video_state = "live" if independent else "dropping"
+            self.frames_dropped += 1
+            return False
+        self.video_queued += 1
+        self.out.put_nowait(_VideoFrame(msgs, key))
         return True
 
     async def send_now(self, msg) -> bool:
@@ -215,6 +275,13 @@ class DataStreamingServer:
         for c in list(clients):
             c.send(msg)
 
+    def _resync_viewer(self, client: "Client"):
+        """A viewer that dropped frames has drained its queue: keyframe on its display."""
+        did = client.display_id if client.display_id in self.captures else "primary"
+        cap = self.captures.get(did)
+        if cap is not None and hasattr(cap.module, "request_keyframe"):
+            cap.module.request_keyframe()
+
     def primary_viewers(self) -> set:
         secondary = {d.client for did, d in self.displays.items() if did != "primary"}
         return self.clients - secondary
@@ -249,7 +316,7 @@ class DataStreamingServer:
         self.recent[ip] = now
         if len(self.recent) > 1000:
             self.recent.popitem(last=False)
-        client = Client(ws, ip, self.meter)
+        client = Client(ws, ip, self.meter, on_resync=self._resync_viewer)
         self.clients.add(client)
         self.settings_received = asyncio.Event() if not self.displays else self.settings_received
         initial_done = False
@@ -621,20 +688,42 @@ class DataStreamingServer:
         queue: asyncio.Queue = asyncio.Queue(maxsize=VIDEO_QUEUE_SIZE)
         jpeg = enc == "jpeg"
 
-        def on_stripe(res_ptr, user):
+        def on_frame(res_ptr, n, user):
+            # one call per encoded frame (native capture thread): copy every stripe out
+            msgs = []
+            key = False
+            fid = 0
+            for i in range(n):
+                r = res_ptr[i]
+                if r.size <= 0:
+                    continue
+                data = ctypes.string_at(r.data, r.size)
+                key = key or (not jpeg and r.size > 1 and data[1] == 1)
+                fid = r.frame_id & 0xFFFF
+                msgs.append(protocol.JPEG_PREFIX + data if jpeg else data)
+            if msgs:
+                loop.call_soon_threadsafe(_put_drop, queue, (msgs, key, fid))
+
+        def on_stripe(res_ptr, user):   # capture modules without a per-frame callback
             r = res_ptr.contents
             if r.size <= 0:
                 return
-            data = bytes(r.data[:r.size])
-            item = (protocol.JPEG_PREFIX + data if jpeg else data, r.frame_id & 0xFFFF)
+            data = ctypes.string_at(r.data, r.size)
+            key = not jpeg and r.size > 1 and data[1] == 1
+            item = ([protocol.JPEG_PREFIX + data if jpeg else data], key, r.frame_id & 0xFFFF)
             loop.call_soon_threadsafe(_put_drop, queue, item)
 
         import pixelflux
-        cb = pixelflux.StripeCallback(on_stripe)
         module = self.capture_factory()
+        if hasattr(module, "start_frame_capture"):
+            cb = pixelflux.FrameCallback(on_frame)
+            start = module.start_frame_capture
+        else:
+            cb = pixelflux.StripeCallback(on_stripe)
+            start = module.start_capture
         sender = asyncio.create_task(self._video_sender(did, queue))
         try:
-            await loop.run_in_executor(None, module.start_capture, cs, cb)
+            await loop.run_in_executor(None, start, cs, cb)
         except Exception as e:
             sender.cancel()
             log.error("capture start failed for %s: %s", did, e)
@@ -668,8 +757,9 @@ class DataStreamingServer:
 
     async def _video_sender(self, did: str, queue: asyncio.Queue):
         was_enabled = True
+        jpeg = None
         while True:
-            data, fid = await queue.get()
+            msgs, key, fid = await queue.get()
             st = self.displays.get(did)
             if st is None:
                 continue
@@ -684,7 +774,9 @@ class DataStreamingServer:
                     cap.module.request_keyframe()
             st.flow.on_sent(fid, self.clock())
             viewers = self.primary_viewers() if did == "primary" else {st.client}
-            self.broadcast(viewers, data)
+            jpeg = msgs[0][:2] == protocol.JPEG_PREFIX
+            for c in list(viewers):
+                c.send_video(msgs, key, independent=jpeg)
 
     # ---------------------------------------------------------------- backpressure
     async def _start_bp(self, did: str):
