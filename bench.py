@@ -117,6 +117,8 @@ def run_capture_path(args, pool, local_rank):
 
 def main():
     args = parse()
+    if args.gather and args.path != "encoder":
+        raise SystemExit("--gather collects packets in Python: use it with --path encoder")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -200,7 +200,15 @@ SK_HD void chroma_dc_dequant(const int* c, int* dcc, int qpc) {
     dcc[3] = (f3 * ls * (1 << q6)) >> 5;   // multiply: f may be negative
 }
 
-SK_HD int chroma_qp(int qp) { return H264_CHROMA_QP[sk_clip(qp, 0, 51)]; }
+// QPc (Table 8-15) without a memory table: on the GPU a table lookup is a vector load
+// that would wait behind the coding kernels' outstanding stores.
+SK_HD int chroma_qp(int qp) {
+    qp = sk_clip(qp, 0, 51);
+    if (qp < 30) return qp;
+    const int i = qp - 30;
+    const uint64_t d = i < 16 ? (0x9888776655433210ULL >> (4 * i)) : (0xaaaa99ULL >> (4 * (i - 16)));
+    return 29 + (int)(d & 15);
+}
 
 // Lagrangian multiplier for motion-vector / mode bits (x264-like 0.85*2^((qp-12)/3)).
 SK_TABLE uint8_t H264_LAMBDA[52] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2,
@@ -471,6 +479,22 @@ SK_HD void chroma_plane_params(const uint8_t* top, const uint8_t* left, int tl, 
     *pa = 16 * (left[7] + top[7]);
     *pb = (34 * H + 32) >> 6;
     *pc = (34 * V + 32) >> 6;
+}
+
+// Full 8x8 chroma prediction of one component for mode m (0 DC, 1 H, 2 V, 3 plane).
+SK_HD void intra_chroma_pred(int m, const uint8_t* top, const uint8_t* left, int tl, bool aT, bool aL,
+                             uint8_t* out) {
+    int qa = 0, qb = 0, qc = 0;
+    if (m == 3) chroma_plane_params(top, left, tl, &qa, &qb, &qc);
+    for (int y = 0; y < 8; y++)
+        for (int x = 0; x < 8; x++) {
+            int v;
+            if (m == 0) v = chroma_dc_block(x >> 2, y >> 2, top, left, aT, aL);
+            else if (m == 1) v = left[y];
+            else if (m == 2) v = top[x];
+            else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
+            out[y * 8 + x] = (uint8_t)v;
+        }
 }
 
 // mb_type ue(v) code number for an I16x16 macroblock in an I slice (add 5 in P slices).

@@ -322,99 +322,128 @@ void CpuH264Encoder::code_slice_inter(int s) {
         }
 }
 
+// Intra 16x16 luma mode (evaluation order DC, V, H, Plane) and chroma mode (DC, H, V,
+// Plane) by SAD against the given neighbour samples. Also returns the chroma prediction.
+static void intra_decide(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* top,
+                         const uint8_t* left, int tl, const uint8_t (*ctop)[8], const uint8_t (*cleft)[8],
+                         const int* ctl, bool aT, bool aL, int* luma_mode, int* chroma_mode) {
+    int dc = i16_dc(top, left, aT, aL);
+    int pa = 0, pb = 0, pc = 0;
+    if (aT && aL) i16_plane_params(top, left, tl, &pa, &pb, &pc);
+    const int order[4] = {2, 0, 1, 3};
+    int best_mode = 2, best_sad = 0x7fffffff;
+    for (int oi = 0; oi < 4; oi++) {
+        int m = order[oi];
+        if ((m == 0 && !aT) || (m == 1 && !aL) || (m == 3 && !(aT && aL))) continue;
+        int sad = 0;
+        for (int y = 0; y < 16; y++)
+            for (int x = 0; x < 16; x++)
+                sad += sk_abs((int)sy[y * 16 + x] - i16_pred_pixel(m, x, y, top, left, tl, aT, aL, dc, pa, pb, pc));
+        if (sad < best_sad) { best_sad = sad; best_mode = m; }
+    }
+    int best_cm = 0, best_csad = 0x7fffffff;
+    for (int m = 0; m < 4; m++) {
+        if ((m == 1 && !aL) || (m == 2 && !aT) || (m == 3 && !(aT && aL))) continue;
+        int sad = 0;
+        for (int c = 0; c < 2; c++) {
+            uint8_t p[64];
+            intra_chroma_pred(m, ctop[c], cleft[c], ctl[c], aT, aL, p);
+            const uint8_t* sp = c ? sv : su;
+            for (int i = 0; i < 64; i++) sad += sk_abs((int)sp[i] - (int)p[i]);
+        }
+        if (sad < best_csad) { best_csad = sad; best_cm = m; }
+    }
+    *luma_mode = best_mode;
+    *chroma_mode = best_cm;
+}
+
+// Edges (row above, column left, corner) of MB (mbx, mby) in plane set P.
+static void mb_edges(const std::vector<uint8_t>* P, const Geometry& g, int mbx, int mby, bool aT, bool aL,
+                     uint8_t* top, uint8_t* left, int* tl, uint8_t (*ctop)[8], uint8_t (*cleft)[8], int* ctl) {
+    const int sy_ = g.stride_y, sc = g.stride_c;
+    memset(top, 0, 16);
+    memset(left, 0, 16);
+    memset(ctop, 0, 16);
+    memset(cleft, 0, 16);
+    *tl = 0;
+    ctl[0] = ctl[1] = 0;
+    if (aT)
+        for (int i = 0; i < 16; i++) top[i] = P[0][(size_t)(mby * 16 - 1) * sy_ + mbx * 16 + i];
+    if (aL)
+        for (int i = 0; i < 16; i++) left[i] = P[0][(size_t)(mby * 16 + i) * sy_ + mbx * 16 - 1];
+    if (aT && aL) *tl = P[0][(size_t)(mby * 16 - 1) * sy_ + mbx * 16 - 1];
+    for (int c = 0; c < 2; c++) {
+        const std::vector<uint8_t>& Q = P[1 + c];
+        if (aT)
+            for (int i = 0; i < 8; i++) ctop[c][i] = Q[(size_t)(mby * 8 - 1) * sc + mbx * 8 + i];
+        if (aL)
+            for (int i = 0; i < 8; i++) cleft[c][i] = Q[(size_t)(mby * 8 + i) * sc + mbx * 8 - 1];
+        if (aT && aL) ctl[c] = Q[(size_t)(mby * 8 - 1) * sc + mbx * 8 - 1];
+    }
+}
+
+// I slices in two passes (same decisions as k_intra_prep + k_code_intra):
+//  1. open loop, every MB independent: modes chosen against the SOURCE neighbours and
+//     the QP escalation the MB needs with that prediction (the start QP);
+//  2. the MB wavefront proper: prediction from the reconstructed neighbours with those
+//     modes, quantisation starting at the start QP (escalating further if still needed).
 void CpuH264Encoder::code_slice_intra(int s) {
     const SliceTask& t = tasks[s];
     const int sy_ = g.stride_y, sc = g.stride_c;
-    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
-        for (int mbx = 0; mbx < g.mb_w; mbx++) {
-            int idx = mby * g.mb_w + mbx;
-            MbInfo& mb = mbs[idx];
-            memset(&mb, 0, sizeof(mb));
-            me[idx].mvx = me[idx].mvy = 0;
-            me[idx].ref = 0;
-            bool aT = mby > t.first_row, aL = mbx > 0;
-            uint8_t top[16] = {0}, left[16] = {0}, ctop[2][8] = {{0}}, cleft[2][8] = {{0}};
-            int tl = 0, ctl[2] = {0, 0};
-            if (aT)
-                for (int i = 0; i < 16; i++) top[i] = rec[0][(size_t)(mby * 16 - 1) * sy_ + mbx * 16 + i];
-            if (aL)
-                for (int i = 0; i < 16; i++) left[i] = rec[0][(size_t)(mby * 16 + i) * sy_ + mbx * 16 - 1];
-            if (aT && aL) tl = rec[0][(size_t)(mby * 16 - 1) * sy_ + mbx * 16 - 1];
-            for (int c = 0; c < 2; c++) {
-                const std::vector<uint8_t>& P = rec[1 + c];
-                if (aT)
-                    for (int i = 0; i < 8; i++) ctop[c][i] = P[(size_t)(mby * 8 - 1) * sc + mbx * 8 + i];
-                if (aL)
-                    for (int i = 0; i < 8; i++) cleft[c][i] = P[(size_t)(mby * 8 + i) * sc + mbx * 8 - 1];
-                if (aT && aL) ctl[c] = P[(size_t)(mby * 8 - 1) * sc + mbx * 8 - 1];
-            }
-            uint8_t sy[256], su[64], sv[64];
-            for (int y = 0; y < 16; y++)
-                memcpy(sy + y * 16, &src[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16], 16);
-            for (int y = 0; y < 8; y++) {
-                memcpy(su + y * 8, &src[1][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
-                memcpy(sv + y * 8, &src[2][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
-            }
-            // luma mode decision (SAD), evaluation order DC, V, H, Plane
-            int dc = i16_dc(top, left, aT, aL);
-            int pa = 0, pb = 0, pc = 0;
-            if (aT && aL) i16_plane_params(top, left, tl, &pa, &pb, &pc);
-            const int order[4] = {2, 0, 1, 3};
-            int best_mode = 2, best_sad = 0x7fffffff;
-            for (int oi = 0; oi < 4; oi++) {
-                int m = order[oi];
-                if ((m == 0 && !aT) || (m == 1 && !aL) || (m == 3 && !(aT && aL))) continue;
-                int sad = 0;
+    for (int pass = 0; pass < 2; pass++)
+        for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+            for (int mbx = 0; mbx < g.mb_w; mbx++) {
+                int idx = mby * g.mb_w + mbx;
+                MbInfo& mb = mbs[idx];
+                bool aT = mby > t.first_row, aL = mbx > 0;
+                uint8_t top[16], left[16], ctop[2][8], cleft[2][8];
+                int tl, ctl[2];
+                mb_edges(pass == 0 ? src : rec, g, mbx, mby, aT, aL, top, left, &tl, ctop, cleft, ctl);
+                uint8_t sy[256], su[64], sv[64];
+                for (int y = 0; y < 16; y++)
+                    memcpy(sy + y * 16, &src[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16], 16);
+                for (int y = 0; y < 8; y++) {
+                    memcpy(su + y * 8, &src[1][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
+                    memcpy(sv + y * 8, &src[2][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
+                }
+                int best_mode, best_cm, start_qp = -1;
+                if (pass == 0) {
+                    intra_decide(sy, su, sv, top, left, tl, ctop, cleft, ctl, aT, aL, &best_mode, &best_cm);
+                } else {
+                    best_mode = mb.i16_mode;
+                    best_cm = mb.chroma_mode;
+                    start_qp = mb.qp;
+                }
+                int dc = i16_dc(top, left, aT, aL);
+                int pa = 0, pb = 0, pc = 0;
+                if (aT && aL) i16_plane_params(top, left, tl, &pa, &pb, &pc);
+                uint8_t py[256], pu[64], pv[64];
                 for (int y = 0; y < 16; y++)
                     for (int x = 0; x < 16; x++)
-                        sad += sk_abs((int)sy[y * 16 + x] -
-                                      i16_pred_pixel(m, x, y, top, left, tl, aT, aL, dc, pa, pb, pc));
-                if (sad < best_sad) { best_sad = sad; best_mode = m; }
-            }
-            uint8_t py[256];
-            for (int y = 0; y < 16; y++)
-                for (int x = 0; x < 16; x++)
-                    py[y * 16 + x] = (uint8_t)i16_pred_pixel(best_mode, x, y, top, left, tl, aT, aL, dc, pa, pb, pc);
-            // chroma mode decision, order DC, H, V, Plane
-            uint8_t pcb[4][2][64];
-            int best_cm = 0, best_csad = 0x7fffffff;
-            for (int m = 0; m < 4; m++) {
-                if ((m == 1 && !aL) || (m == 2 && !aT) || (m == 3 && !(aT && aL))) continue;
-                int sad = 0;
-                for (int c = 0; c < 2; c++) {
-                    int qa = 0, qb = 0, qc = 0;
-                    if (m == 3) chroma_plane_params(ctop[c], cleft[c], ctl[c], &qa, &qb, &qc);
-                    const uint8_t* sp = c ? sv : su;
-                    for (int y = 0; y < 8; y++)
-                        for (int x = 0; x < 8; x++) {
-                            int v;
-                            if (m == 0) v = chroma_dc_block(x >> 2, y >> 2, ctop[c], cleft[c], aT, aL);
-                            else if (m == 1) v = cleft[c][y];
-                            else if (m == 2) v = ctop[c][x];
-                            else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
-                            pcb[m][c][y * 8 + x] = (uint8_t)v;
-                            sad += sk_abs((int)sp[y * 8 + x] - v);
-                        }
+                        py[y * 16 + x] = (uint8_t)i16_pred_pixel(best_mode, x, y, top, left, tl, aT, aL, dc, pa, pb, pc);
+                intra_chroma_pred(best_cm, ctop[0], cleft[0], ctl[0], aT, aL, pu);
+                intra_chroma_pred(best_cm, ctop[1], cleft[1], ctl[1], aT, aL, pv);
+                MbTransform tr;
+                residual_transform(sy, py, su, pu, sv, pv, tr);
+                int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
+                memset(&mb, 0, sizeof(mb));
+                mb.type = MB_I16x16;
+                mb.i16_mode = (uint8_t)best_mode;
+                mb.chroma_mode = (uint8_t)best_cm;
+                int qp = quant_mb_with_budget(tr, t.qp, true, mb, coef, host_cavlc_tables(), start_qp);
+                if (pass == 0) continue;   // mb keeps the modes and the start QP for pass 2
+                me[idx].mvx = me[idx].mvy = 0;
+                me[idx].ref = 0;
+                uint8_t ry[256], ru[64], rv[64];
+                recon_luma(coef, qp, true, mb.cbp & 15, py, ry);
+                recon_chroma(coef, qp, (mb.cbp >> 4) & 3, pu, pv, ru, rv);
+                for (int y = 0; y < 16; y++)
+                    memcpy(&rec[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16], ry + y * 16, 16);
+                for (int y = 0; y < 8; y++) {
+                    memcpy(&rec[1][(size_t)(mby * 8 + y) * sc + mbx * 8], ru + y * 8, 8);
+                    memcpy(&rec[2][(size_t)(mby * 8 + y) * sc + mbx * 8], rv + y * 8, 8);
                 }
-                if (sad < best_csad) { best_csad = sad; best_cm = m; }
             }
-            MbTransform tr;
-            residual_transform(sy, py, su, pcb[best_cm][0], sv, pcb[best_cm][1], tr);
-            int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
-            mb.type = MB_I16x16;
-            mb.i16_mode = (uint8_t)best_mode;
-            mb.chroma_mode = (uint8_t)best_cm;
-            int qp = quant_mb_with_budget(tr, t.qp, true, mb, coef, host_cavlc_tables());
-            uint8_t ry[256], ru[64], rv[64];
-            recon_luma(coef, qp, true, mb.cbp & 15, py, ry);
-            recon_chroma(coef, qp, (mb.cbp >> 4) & 3, pcb[best_cm][0], pcb[best_cm][1], ru, rv);
-            for (int y = 0; y < 16; y++)
-                memcpy(&rec[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16], ry + y * 16, 16);
-            for (int y = 0; y < 8; y++) {
-                memcpy(&rec[1][(size_t)(mby * 8 + y) * sc + mbx * 8], ru + y * 8, 8);
-                memcpy(&rec[2][(size_t)(mby * 8 + y) * sc + mbx * 8], rv + y * 8, 8);
-            }
-        }
 }
 
 void CpuH264Encoder::code_slice_skipall(int s) {

@@ -209,9 +209,11 @@ SK_HD void recon_chroma(const int16_t* coef, int qp, int cbp_c, const uint8_t* p
 
 // Quantise with QP escalation so a macroblock never exceeds the A.3.1 bit limit.
 // Returns the final QP; fills mb.cbp / nnz and coef.
+// `start_qp` (>= slice_qp, a multiple of 6 above it) skips escalation steps already known
+// to be needed (intra: found by the open-loop pre-pass).
 SK_HD int quant_mb_with_budget(const MbTransform& t, int slice_qp, bool intra16, MbInfo& mb,
-                               int16_t* coef, const CavlcTables& T) {
-    int qp = slice_qp;
+                               int16_t* coef, const CavlcTables& T, int start_qp = -1) {
+    int qp = start_qp >= 0 ? start_qp : slice_qp;
     int qp_cap = sk_min(51, slice_qp + 24);
     for (;;) {
         int cbp_l = quant_luma(t, qp, intra16, coef, mb.nnz);

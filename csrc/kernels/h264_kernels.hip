@@ -712,6 +712,7 @@ struct MbScratch {                 // per-wave LDS
     uint8_t nnz[24];               // TotalCoeff per block (luma blkIdx, Cb, Cr)
     uint8_t pad[8];
     int cdcp[8];                   // chroma DC predictions [comp][block]
+    uint8_t nb[64];                // intra neighbour samples (intra_pred_lanes layout)
 };
 
 // In-place 4x4 Hadamard H*X*H of a raster int[16] in LDS: rows by lanes 0..3,
@@ -742,15 +743,15 @@ __device__ __forceinline__ void lds_hadamard4x4(int* x) {
 // suffixLength the block can reach (<= sl_max, 9.2.2.1). With per-TotalCoeff
 // maxima for coeff_token / total_zeros and a 3n+8 bound on run_before this
 // dominates the exact nC-free bound, so bound <= budget implies exact <= budget.
+// (lc >> sl) + 1 + sl is convex in sl and the escape (28) region is a prefix of sl, so
+// the maximum over sl in [1, sl_max] sits at an end point: two evaluations instead of
+// six (checked equal to the loop for every level and sl_max).
 __device__ __forceinline__ int level_bits_bound(int a, int sl_max) {
     int lc = 2 * a - 1;
     int best = lc < 14 ? lc + 1 : (lc < 30 ? 19 : 28);
-#pragma unroll
-    for (int sl = 1; sl <= 6; sl++) {
-        int bsl = lc < (15 << sl) ? (lc >> sl) + 1 + sl : 28;
-        if (sl <= sl_max) best = sk_max(best, bsl);
-    }
-    return best;
+    const int b1 = lc < 30 ? (lc >> 1) + 2 : 28;
+    const int bs = lc < (15 << sl_max) ? (lc >> sl_max) + 1 + sl_max : 28;
+    return sk_max(best, sk_max(b1, bs));
 }
 __device__ __forceinline__ int suffix_len_cap(int maxabs) {
     return sk_min(6, 1 + (maxabs > 3) + (maxabs > 6) + (maxabs > 12) + (maxabs > 24) + (maxabs > 48));
@@ -1038,7 +1039,7 @@ __device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, cons
 __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, const int* pred_c,
                        int slice_qp, bool intra16, MbScratch& S, MbInfo& mb, int* rec_l, int* rec_c,
                        int16_t* gcoef, const CavlcTables& T, unsigned long long* dbg = nullptr,
-                       int step = 0) {
+                       int step = 0, int start_qp = -1, bool quant_only = false) {
     const int l = lane_id();
     const int r = l & 3;
     int x[4], wl[4], wc[4];
@@ -1048,10 +1049,11 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
 #pragma unroll
     for (int j = 0; j < 4; j++) x[j] = src_c[j] - pred_c[j];
     fwd4_quad(x, r, wc);
-    int qp = slice_qp;
+    int qp = start_qp >= 0 ? start_qp : slice_qp;
     int cap = sk_min(51, slice_qp + 24);
     int cbp = 0;
     STAMP_S(dbg, step, 3);
+    qp = __builtin_amdgcn_readfirstlane(qp);   // wave-uniform: table lookups become scalar loads
     for (;;) {
         int bound;
         cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound, T, dbg, step);
@@ -1063,6 +1065,7 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
     STAMP_S(dbg, step, 4);
     mb.cbp = (uint8_t)cbp;
     mb.qp = (uint8_t)qp;
+    if (quant_only) return qp;
     recon_mb_lanes(qp, intra16, cbp, S, pred_l, pred_c, rec_l, rec_c);
     STAMP_S(dbg, step, 5);
     // copy levels to global (816 B = 204 words)
@@ -1180,8 +1183,225 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Luma (I16) and chroma intra modes of one MB by wave-wide SADs: luma in the
+// evaluation order DC, V, H, Plane; chroma DC, H, V, Plane (first minimum wins).
+// topp/leftp/ctop/cleft: neighbour samples (zeros when unavailable), lane layout
+// as everywhere (b, r luma rows; comp/cb chroma rows).
+__device__ void intra_modes_wave(const int* src_l, const int* src_c, const uint8_t* topp, const uint8_t* leftp,
+                                 int tl, const uint8_t* const* ctop, const uint8_t* const* cleft, const int* ctl,
+                                 bool aT, bool aL, int* cdcp, int* luma_mode, int* chroma_mode) {
+    const int l = lane_id();
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    const int lx = blk_x(b) * 4, ly = blk_y(b) * 4 + r;
+    int dc = i16_dc(topp, leftp, aT, aL);
+    int pa = 0, pb = 0, pc = 0;
+    if (aT && aL) i16_plane_params(topp, leftp, tl, &pa, &pb, &pc);
+    const int order[4] = {2, 0, 1, 3};
+    int best_mode = 2, best_sad = 0x7fffffff;
+    for (int oi = 0; oi < 4; oi++) {
+        int m = order[oi];
+        if ((m == 0 && !aT) || (m == 1 && !aL) || (m == 3 && !(aT && aL))) continue;
+        int sad = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            sad += sk_abs(src_l[j] - i16_pred_pixel(m, lx + j, ly, topp, leftp, tl, aT, aL, dc, pa, pb, pc));
+        sad = wave_sum(sad);
+        if (sad < best_sad) { best_sad = sad; best_mode = m; }
+    }
+    const uint8_t* ct = ctop[comp];
+    const uint8_t* cf = cleft[comp];
+    const int clx = (cb & 1) * 4, cly = (cb >> 1) * 4 + r;
+    int qa = 0, qb = 0, qc = 0;
+    if (aT && aL) chroma_plane_params(ct, cf, ctl[comp], &qa, &qb, &qc);
+    if (l < 8) cdcp[l] = chroma_dc_block(l & 1, (l >> 1) & 1, ctop[l >> 2], cleft[l >> 2], aT, aL);
+    wave_sync();
+    const int cdc_mine = cdcp[comp * 4 + cb];
+    int best_cm = 0, best_csad = 0x7fffffff;
+    for (int m = 0; m < 4; m++) {
+        if ((m == 1 && !aL) || (m == 2 && !aT) || (m == 3 && !(aT && aL))) continue;
+        int sad = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            int x = clx + j, y = cly, v;
+            if (m == 0) v = cdc_mine;
+            else if (m == 1) v = cf[y];
+            else if (m == 2) v = ct[x];
+            else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
+            sad += sk_abs(src_c[j] - v);
+        }
+        sad = wave_sum(l < 32 ? sad : 0);
+        if (sad < best_csad) { best_csad = sad; best_cm = m; }
+    }
+    *luma_mode = best_mode;
+    *chroma_mode = best_cm;
+}
+
+// Sum of v over the lanes of a wave-uniform lane mask (DPP + readlanes).
+__device__ __forceinline__ int wave_sum_masked(int v, bool on) { return wave_sum(on ? v : 0); }
+
+// This lane's luma / chroma prediction row for the given (wave-uniform) modes.
+// nb: the wave's neighbour samples in LDS, top 16 | left 16 | ctop[2][8] | cleft[2][8]
+// (zeros when unavailable); tl / ctl: corner samples. Sums (DC, plane gradients) are
+// wave reductions, so no lane walks the edges serially.
+__device__ void intra_pred_lanes(int mode, int cmode, const uint8_t* nb, int tl, const int* ctl, bool aT, bool aL,
+                                 int* pred_l, int* pred_c) {
+    const int l = lane_id();
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    const int lx = blk_x(b) * 4, ly = blk_y(b) * 4 + r;
+    const int clx = (cb & 1) * 4, cly = (cb >> 1) * 4 + r;
+    const int e = nb[l];   // this lane's edge sample
+    // ---- luma ----
+    if (mode == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_l[j] = nb[lx + j];
+    } else if (mode == 1) {
+        const int v = nb[16 + ly];
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_l[j] = v;
+    } else if (mode == 2) {
+        const int st = wave_sum_masked(e, l < 16), sl = wave_sum_masked(e, l >= 16 && l < 32);
+        const int dc = (aT && aL) ? (st + sl + 16) >> 5 : (aL ? (sl + 8) >> 4 : (aT ? (st + 8) >> 4 : 128));
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_l[j] = dc;
+    } else {
+        // lanes 0..7: H terms (top), 8..15: V terms (left); i = l & 7
+        const int i = l & 7, base = l < 8 ? 0 : 16;
+        const int p1 = nb[base + 8 + i];
+        const int p0 = 6 - i >= 0 ? nb[base + sk_max(6 - i, 0)] : tl;
+        const int term = (i + 1) * (p1 - p0);
+        const int H = wave_sum_masked(term, l < 8), V = wave_sum_masked(term, l >= 8 && l < 16);
+        const int pa = 16 * (nb[16 + 15] + nb[15]);
+        const int pb = (5 * H + 32) >> 6, pc = (5 * V + 32) >> 6;
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_l[j] = sk_clip255((pa + pb * (lx + j - 7) + pc * (ly - 7) + 16) >> 5);
+    }
+    // ---- chroma ----
+    const int ct = 32 + 8 * comp, cf = 48 + 8 * comp;   // this lane's component edges in nb
+    if (cmode == 0) {
+        // quad sums over the chroma edge lanes: lane 32 + 8c + 4bx -> top sum of block column bx,
+        // lane 48 + 8c + 4by -> left sum of block row by
+        const int q = quad_sum(e);
+        const int st = __shfl(q, 32 + 8 * comp + 4 * (cb & 1));
+        const int sl = __shfl(q, 48 + 8 * comp + 4 * (cb >> 1));
+        const int bx = cb & 1, by = cb >> 1;
+        int v;
+        if (bx == by) v = (aT && aL) ? (st + sl + 4) >> 3 : (aL ? (sl + 2) >> 2 : (aT ? (st + 2) >> 2 : 128));
+        else if (bx == 1) v = aT ? (st + 2) >> 2 : (aL ? (sl + 2) >> 2 : 128);
+        else v = aL ? (sl + 2) >> 2 : (aT ? (st + 2) >> 2 : 128);
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_c[j] = v;
+    } else if (cmode == 1) {
+        const int v = nb[cf + cly];
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_c[j] = v;
+    } else if (cmode == 2) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_c[j] = nb[ct + clx + j];
+    } else {
+        // lanes 0..31: component l >> 4, (l >> 3) & 1 selects the H (top) or V (left) terms, i = l & 3
+        const int tc = (l >> 4) & 1, isv = (l >> 3) & 1, i = l & 3;
+        const int base = isv ? 48 + 8 * tc : 32 + 8 * tc;
+        const int p1 = nb[base + 4 + i];
+        const int p0 = 2 - i >= 0 ? nb[base + sk_max(2 - i, 0)] : ctl[tc];
+        const int term = (l & 4) ? 0 : (i + 1) * (p1 - p0);   // lanes with (l & 4) are padding
+        const int H0 = wave_sum_masked(term, l < 8), V0 = wave_sum_masked(term, l >= 8 && l < 16);
+        const int H1 = wave_sum_masked(term, l >= 16 && l < 24), V1 = wave_sum_masked(term, l >= 24 && l < 32);
+        const int H = comp ? H1 : H0, V = comp ? V1 : V0;
+        const int pa = 16 * (nb[cf + 7] + nb[ct + 7]);
+        const int pb = (34 * H + 32) >> 6, pc = (34 * V + 32) >> 6;
+#pragma unroll
+        for (int j = 0; j < 4; j++) pred_c[j] = sk_clip255((pa + pb * (clx + j - 3) + pc * (cly - 3) + 16) >> 5);
+    }
+}
+
+// Loads the neighbour layout nb (see intra_pred_lanes) of one MB from a plane set.
+__device__ void load_nb_planes(const Planes& P, int sy, int sc, int mbx, int mby, bool aT, bool aL, uint8_t* nb,
+                               int* tl, int* ctl) {
+    const int l = lane_id();
+    int v = 0;
+    if (l < 16) v = aT ? P.y[(size_t)(mby * 16 - 1) * sy + mbx * 16 + l] : 0;
+    else if (l < 32) v = aL ? P.y[(size_t)(mby * 16 + l - 16) * sy + mbx * 16 - 1] : 0;
+    else if (l < 48) {
+        const uint8_t* C = (l & 8) ? P.v : P.u;
+        v = aT ? C[(size_t)(mby * 8 - 1) * sc + mbx * 8 + (l & 7)] : 0;
+    } else {
+        const uint8_t* C = (l & 8) ? P.v : P.u;
+        v = aL ? C[(size_t)(mby * 8 + (l & 7)) * sc + mbx * 8 - 1] : 0;
+    }
+    nb[l] = (uint8_t)v;
+    *tl = (aT && aL) ? P.y[(size_t)(mby * 16 - 1) * sy + mbx * 16 - 1] : 0;
+    ctl[0] = (aT && aL) ? P.u[(size_t)(mby * 8 - 1) * sc + mbx * 8 - 1] : 0;
+    ctl[1] = (aT && aL) ? P.v[(size_t)(mby * 8 - 1) * sc + mbx * 8 - 1] : 0;
+    wave_sync();
+}
+
+// K5 open-loop pre-pass, one wave per MB of an I slice (all MBs in parallel): intra
+// modes against the SOURCE neighbours and the QP the MB needs under the bit budget
+// with that prediction. k_code_intra's wavefront then only predicts, quantises from
+// that QP and reconstructs (no mode search, usually no escalation in the chain).
+__global__ __launch_bounds__(256) void k_intra_prep(FrameArgs a) {
+    __shared__ MbScratch Sw[4];
+    __shared__ CavlcTables T;
+    __shared__ uint8_t nb_w[4][64];   // top 16 | left 16 | ctop 2x8 | cleft 2x8
+    MbScratch& S = Sw[threadIdx.x >> 6];
+    uint8_t* nb = nb_w[threadIdx.x >> 6];
+    const int nmb = a.mb_w * a.mb_h;
+    const int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    const bool valid = idx < nmb;
+    const int mbx = valid ? idx % a.mb_w : 0, mby = valid ? idx / a.mb_w : 0;
+    const SliceTask t = a.tasks[mby / a.rows_per_slice];
+    const bool coded = valid && t.final_action == ACT_I;
+    if (!__syncthreads_or(coded)) return;
+    load_cavlc_tables(T, a.cavlc_tabs);
+    __syncthreads();
+    if (!coded) return;
+    const int l = lane_id();
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    const bool aT = mby > t.first_row, aL = mbx > 0;
+    // source neighbours into LDS (zeros when unavailable)
+    int tl, ctl[2];
+    load_nb_planes(a.src, a.stride_y, a.stride_c, mbx, mby, aT, aL, nb, &tl, ctl);
+    const uint8_t* ctop[2] = {nb + 32, nb + 40};
+    const uint8_t* cleft[2] = {nb + 48, nb + 56};
+    int px = mbx * 16 + blk_x(b) * 4, py = mby * 16 + blk_y(b) * 4 + r;
+    uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
+    const uint8_t* cs = comp ? a.src.v : a.src.u;
+    int cx0 = mbx * 8 + (cb & 1) * 4, cy0 = mby * 8 + (cb >> 1) * 4 + r;
+    uint32_t csw = *reinterpret_cast<const uint32_t*>(cs + (size_t)cy0 * a.stride_c + cx0);
+    int src_l[4], src_c[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        src_l[j] = (sw >> (8 * j)) & 255;
+        src_c[j] = (csw >> (8 * j)) & 255;
+    }
+    int mode, cmode;
+    intra_modes_wave(src_l, src_c, nb, nb + 16, tl, ctop, cleft, ctl, aT, aL, S.cdcp, &mode, &cmode);
+    int pred_l[4], pred_c[4];
+    intra_pred_lanes(mode, cmode, nb, tl, ctl, aT, aL, pred_l, pred_c);
+    MbInfo mb;
+    memset(&mb, 0, sizeof(mb));
+    int rec_l[4], rec_c[4];
+    const int qp = code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c, nullptr, T, nullptr, 0,
+                           -1, true);
+    if (l == 0) {
+        MbInfo o;
+        memset(&o, 0, sizeof(o));
+        o.type = MB_I16x16;
+        o.i16_mode = (uint8_t)mode;
+        o.chroma_mode = (uint8_t)cmode;
+        o.qp = (uint8_t)qp;
+        a.mbs[idx] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K5+K6 intra: one workgroup per I slice, wave w codes MB row w, MB x at step
-// t = x + 2w (wavefront); neighbour edges travel through LDS rings.
+// t = x + 2w (wavefront); neighbour edges travel through LDS rings. Modes and the
+// start QP come from k_intra_prep, so a step is prediction, quantisation and
+// reconstruction only; the next step's source rows and decisions are loaded ahead.
 constexpr int kMaxRows = 16;
 struct IntraEdges {
     uint8_t bot_y[kMaxRows][4][16];      // bottom luma row of MB (row, x mod 4)
@@ -1190,10 +1410,24 @@ struct IntraEdges {
     uint8_t right_c[kMaxRows][2][8];
 };
 
+// Source samples and pre-pass decisions of one MB, staged in LDS by the producer wave.
+struct IntraSrc {
+    uint32_t y[64];      // 16 rows x 16 px (row-major, 4 words per row)
+    uint32_t c[32];      // Cb 8x8 then Cr 8x8 (2 words per row)
+    int mode, cmode, qp, pad;
+};
+constexpr int kIntraRing = 4;   // MB slots per row in flight (producer runs 2 steps ahead)
+
+// One workgroup of MAXROWS coding waves + 1 producer wave per I slice. Coding wave w
+// owns MB row w and codes MB x at step x + 2w (wavefront, neighbour edges through
+// LDS). The producer wave loads the source rows of the MBs due two steps later into
+// an LDS ring, so a coding wave never issues a global load: its only memory waits
+// are LDS, and its global stores (reconstruction, levels, MB info) are never waited on.
 template <int MAXROWS>
-__global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
+__global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) {
     __shared__ MbScratch Sw[MAXROWS];
     __shared__ IntraEdges E;
+    __shared__ IntraSrc R[MAXROWS][kIntraRing];
     __shared__ uint8_t zero16[16];
     __shared__ CavlcTables T;
     int s = blockIdx.x;
@@ -1201,137 +1435,125 @@ __global__ __launch_bounds__(64 * MAXROWS) void k_code_intra(FrameArgs a) {
     if (t.final_action != ACT_I) return;   // block-uniform: P/skipped slices leave before the table load
     if (threadIdx.x < 16) zero16[threadIdx.x] = 0;
     load_cavlc_tables(T, a.cavlc_tabs);
-    __syncthreads();
     int w = threadIdx.x >> 6;
     int l = lane_id();
-    int rows = t.num_rows;
-    int steps = a.mb_w + 2 * (rows - 1);
-    MbScratch& S = Sw[w];
-    const int b = l >> 2, r = l & 3;
-    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
-    for (int step = 0; step < steps; step++) {
-        int mbx = step - 2 * w;
-        bool active = w < rows && mbx >= 0 && mbx < a.mb_w;
-        if (active) {
-            STAMP(step, 0);
-            int mby = t.first_row + w;
-            int idx = mby * a.mb_w + mbx;
-            bool aT = w > 0, aL = mbx > 0;
-            const uint8_t* top = aT ? E.bot_y[w - 1][mbx & 3] : nullptr;
-            const uint8_t* left = aL ? E.right_y[w] : nullptr;
-            int tl = (aT && aL) ? E.bot_y[w - 1][(mbx - 1) & 3][15] : 0;
-            const uint8_t* topp = aT ? top : zero16;
-            const uint8_t* leftp = aL ? left : zero16;
-            // luma source
-            int px = mbx * 16 + blk_x(b) * 4, py = mby * 16 + blk_y(b) * 4 + r;
-            int lx = blk_x(b) * 4, ly = blk_y(b) * 4 + r;
-            uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
-            int src_l[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) src_l[j] = (sw >> (8 * j)) & 255;
-            int dc = i16_dc(topp, leftp, aT, aL);
-            int pa = 0, pb = 0, pc = 0;
-            if (aT && aL) i16_plane_params(topp, leftp, tl, &pa, &pb, &pc);
-            const int order[4] = {2, 0, 1, 3};
-            int best_mode = 2, best_sad = 0x7fffffff;
-            for (int oi = 0; oi < 4; oi++) {
-                int m = order[oi];
-                if ((m == 0 && !aT) || (m == 1 && !aL) || (m == 3 && !(aT && aL))) continue;
-                int sad = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    sad += sk_abs(src_l[j] - i16_pred_pixel(m, lx + j, ly, topp, leftp, tl, aT, aL, dc, pa, pb, pc));
-                sad = wave_sum(sad);
-                if (sad < best_sad) { best_sad = sad; best_mode = m; }
-            }
-            STAMP(step, 1);
-            int pred_l[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                pred_l[j] = i16_pred_pixel(best_mode, lx + j, ly, topp, leftp, tl, aT, aL, dc, pa, pb, pc);
-            // chroma
-            const uint8_t* ctop = aT ? E.bot_c[w - 1][mbx & 3][comp] : zero16;
-            const uint8_t* cleft = aL ? E.right_c[w][comp] : zero16;
-            int ctl = (aT && aL) ? E.bot_c[w - 1][(mbx - 1) & 3][comp][7] : 0;
-            const uint8_t* cs = comp ? a.src.v : a.src.u;
-            int cx0 = mbx * 8 + (cb & 1) * 4, cy0 = mby * 8 + (cb >> 1) * 4 + r;
-            int clx = (cb & 1) * 4, cly = (cb >> 1) * 4 + r;
-            uint32_t csw = *reinterpret_cast<const uint32_t*>(cs + (size_t)cy0 * a.stride_c + cx0);
-            int src_c[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) src_c[j] = (csw >> (8 * j)) & 255;
-            int qa = 0, qb = 0, qc = 0;
-            if (aT && aL) chroma_plane_params(ctop, cleft, ctl, &qa, &qb, &qc);
-            if (l < 8) {
-                const uint8_t* t8 = aT ? E.bot_c[w - 1][mbx & 3][l >> 2] : zero16;
-                const uint8_t* l8 = aL ? E.right_c[w][l >> 2] : zero16;
-                S.cdcp[l] = chroma_dc_block(l & 1, (l >> 1) & 1, t8, l8, aT, aL);
-            }
-            wave_sync();
-            const int cdc_mine = S.cdcp[comp * 4 + cb];
-            int best_cm = 0, best_csad = 0x7fffffff;
-            for (int m = 0; m < 4; m++) {
-                if ((m == 1 && !aL) || (m == 2 && !aT) || (m == 3 && !(aT && aL))) continue;
-                int sad = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    int x = clx + j, y = cly, v;
-                    if (m == 0) v = cdc_mine;
-                    else if (m == 1) v = cleft[y];
-                    else if (m == 2) v = ctop[x];
-                    else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
-                    sad += sk_abs(src_c[j] - v);
-                }
-                sad = wave_sum(l < 32 ? sad : 0);
-                if (sad < best_csad) { best_csad = sad; best_cm = m; }
-            }
-            int pred_c[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                int x = clx + j, y = cly, v;
-                if (best_cm == 0) v = cdc_mine;
-                else if (best_cm == 1) v = cleft[y];
-                else if (best_cm == 2) v = ctop[x];
-                else v = sk_clip255((qa + qb * (x - 3) + qc * (y - 3) + 16) >> 5);
-                pred_c[j] = v;
-            }
-            STAMP(step, 2);
-            MbInfo mb;
-            memset(&mb, 0, sizeof(mb));
-            mb.type = MB_I16x16;
-            mb.i16_mode = (uint8_t)best_mode;
-            mb.chroma_mode = (uint8_t)best_cm;
-            int rec_l[4], rec_c[4];
-            code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c,
-                    a.coefs + (size_t)idx * kCoefPerMb, T, a.dbg, step);
-            STAMP(step, 6);
-            uint32_t rw = (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) |
-                          ((uint32_t)rec_l[3] << 24);
-            *reinterpret_cast<uint32_t*>(a.rec.y + (size_t)py * a.stride_y + px) = rw;
-            if (l < 32) {
-                uint8_t* crp = comp ? a.rec.v : a.rec.u;
-                uint32_t cw = (uint32_t)rec_c[0] | ((uint32_t)rec_c[1] << 8) | ((uint32_t)rec_c[2] << 16) |
-                              ((uint32_t)rec_c[3] << 24);
-                *reinterpret_cast<uint32_t*>(crp + (size_t)cy0 * a.stride_c + cx0) = cw;
-            }
-            wave_sync();
-            // edges for the neighbours (written after every lane has read the old ones)
-            if (ly == 15)
-                for (int j = 0; j < 4; j++) E.bot_y[w][mbx & 3][lx + j] = (uint8_t)rec_l[j];
-            if (lx + 3 == 15) E.right_y[w][ly] = (uint8_t)rec_l[3];
-            if (l < 32) {
-                if (cly == 7)
-                    for (int j = 0; j < 4; j++) E.bot_c[w][mbx & 3][comp][clx + j] = (uint8_t)rec_c[j];
-                if (clx + 3 == 7) E.right_c[w][comp][cly] = (uint8_t)rec_c[3];
+    const int rows = t.num_rows;
+    const int steps = a.mb_w + 2 * (rows - 1);
+    const bool producer = w == MAXROWS;
+    // producer: stage the MBs coded at step `st` (MB x = st - 2*row of every row)
+    auto produce = [&](int st) {
+        for (int row = 0; row < rows; row++) {
+            const int x = st - 2 * row;
+            if (x < 0 || x >= a.mb_w) continue;
+            const int my = t.first_row + row;
+            IntraSrc& d = R[row][x & (kIntraRing - 1)];
+            // luma: lane l -> row l >> 2, word l & 3
+            d.y[l] = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(my * 16 + (l >> 2)) * a.stride_y + x * 16 +
+                                                        4 * (l & 3));
+            if (l < 32) {   // chroma: comp l >> 4, row (l >> 1) & 7, word l & 1
+                const uint8_t* P = (l >> 4) ? a.src.v : a.src.u;
+                d.c[l] = *reinterpret_cast<const uint32_t*>(P + (size_t)(my * 8 + ((l >> 1) & 7)) * a.stride_c +
+                                                            x * 8 + 4 * (l & 1));
             }
             if (l == 0) {
-                for (int i = 0; i < 24; i++) mb.nnz[i] = S.nnz[i];
-                a.mbs[idx] = mb;
-                a.me[idx].mvx = 0;
-                a.me[idx].mvy = 0;
-                a.me[idx].ref = 0;
+                const MbInfo pre = a.mbs[my * a.mb_w + x];
+                d.mode = pre.i16_mode;
+                d.cmode = pre.chroma_mode;
+                d.qp = pre.qp;
             }
-            STAMP(step, 7);
+        }
+    };
+    if (producer) {
+        __builtin_amdgcn_s_setprio(2);
+        produce(0);
+        produce(1);
+    }
+    __syncthreads();
+    if (!producer) __builtin_amdgcn_s_setprio(3);   // the chain's waves issue first on a shared SIMD
+    MbScratch& S = Sw[producer ? 0 : w];
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    const int lx = blk_x(b) * 4, ly = blk_y(b) * 4 + r;
+    const int clx = (cb & 1) * 4, cly = (cb >> 1) * 4 + r;
+    const int mby = t.first_row + w;
+    for (int step = 0; step < steps; step++) {
+        if (producer) {
+            if (step + 2 < steps) produce(step + 2);
+        } else {
+            const int mbx = step - 2 * w;
+            const bool active = w < rows && mbx >= 0 && mbx < a.mb_w;
+            if (active) {
+                STAMP(step, 0);
+                const IntraSrc& in = R[w][mbx & (kIntraRing - 1)];
+                const uint32_t sw = in.y[ly * 4 + (lx >> 2)];
+                const uint32_t csw = in.c[comp * 16 + cly * 2 + (clx >> 2)];
+                // wave-uniform decisions (scalar registers / branches)
+                const int mode = __builtin_amdgcn_readfirstlane(in.mode);
+                const int cmode = __builtin_amdgcn_readfirstlane(in.cmode);
+                const int start_qp = __builtin_amdgcn_readfirstlane(in.qp);
+                const int idx = mby * a.mb_w + mbx;
+                const bool aT = w > 0, aL = mbx > 0;
+                // neighbour samples of this MB into the wave's nb layout (LDS)
+                uint8_t* nb = S.nb;
+                {
+                    int v = 0;
+                    if (l < 16) v = aT ? E.bot_y[w - 1][mbx & 3][l] : 0;
+                    else if (l < 32) v = aL ? E.right_y[w][l - 16] : 0;
+                    else if (l < 48) v = aT ? E.bot_c[w - 1][mbx & 3][(l >> 3) & 1][l & 7] : 0;
+                    else v = aL ? E.right_c[w][(l >> 3) & 1][l & 7] : 0;
+                    nb[l] = (uint8_t)v;
+                }
+                const int tl = (aT && aL) ? E.bot_y[w - 1][(mbx - 1) & 3][15] : 0;
+                const int ctl[2] = {(aT && aL) ? E.bot_c[w - 1][(mbx - 1) & 3][0][7] : 0,
+                                    (aT && aL) ? E.bot_c[w - 1][(mbx - 1) & 3][1][7] : 0};
+                wave_sync();
+                int src_l[4], src_c[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    src_l[j] = (sw >> (8 * j)) & 255;
+                    src_c[j] = (csw >> (8 * j)) & 255;
+                }
+                int pred_l[4], pred_c[4];
+                intra_pred_lanes(mode, cmode, nb, tl, ctl, aT, aL, pred_l, pred_c);
+                STAMP(step, 2);
+                MbInfo mb;
+                memset(&mb, 0, sizeof(mb));
+                mb.type = MB_I16x16;
+                mb.i16_mode = (uint8_t)mode;
+                mb.chroma_mode = (uint8_t)cmode;
+                int rec_l[4], rec_c[4];
+                code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c,
+                        a.coefs + (size_t)idx * kCoefPerMb, T, a.dbg, step, start_qp);
+                STAMP(step, 6);
+                // edges for the neighbours first (LDS), then the global stores
+                wave_sync();
+                if (ly == 15)
+                    for (int j = 0; j < 4; j++) E.bot_y[w][mbx & 3][lx + j] = (uint8_t)rec_l[j];
+                if (lx + 3 == 15) E.right_y[w][ly] = (uint8_t)rec_l[3];
+                if (l < 32) {
+                    if (cly == 7)
+                        for (int j = 0; j < 4; j++) E.bot_c[w][mbx & 3][comp][clx + j] = (uint8_t)rec_c[j];
+                    if (clx + 3 == 7) E.right_c[w][comp][cly] = (uint8_t)rec_c[3];
+                }
+                const int px = mbx * 16 + lx, py = mby * 16 + ly;
+                uint32_t rw = (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) |
+                              ((uint32_t)rec_l[3] << 24);
+                *reinterpret_cast<uint32_t*>(a.rec.y + (size_t)py * a.stride_y + px) = rw;
+                if (l < 32) {
+                    uint8_t* crp = comp ? a.rec.v : a.rec.u;
+                    uint32_t cw = (uint32_t)rec_c[0] | ((uint32_t)rec_c[1] << 8) | ((uint32_t)rec_c[2] << 16) |
+                                  ((uint32_t)rec_c[3] << 24);
+                    *reinterpret_cast<uint32_t*>(crp + (size_t)(mby * 8 + cly) * a.stride_c + mbx * 8 + clx) = cw;
+                }
+                if (l == 0) {
+                    for (int i = 0; i < 24; i++) mb.nnz[i] = S.nnz[i];
+                    a.mbs[idx] = mb;
+                    a.me[idx].mvx = 0;
+                    a.me[idx].mvy = 0;
+                    a.me[idx].ref = 0;
+                }
+                STAMP(step, 7);
+            }
         }
         __syncthreads();
         if (w == 0) STAMP(step, 8);
@@ -2142,10 +2364,11 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_intra_prep, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     if (a.rows_per_slice <= 4)
-        hipLaunchKernelGGL(k_code_intra<4>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
+        hipLaunchKernelGGL(k_code_intra<4>, dim3(a.num_slices), dim3(64 * 5), 0, s, a);
     else
-        hipLaunchKernelGGL(k_code_intra<kMaxRows>, dim3(a.num_slices), dim3(64 * a.rows_per_slice), 0, s, a);
+        hipLaunchKernelGGL(k_code_intra<kMaxRows - 1>, dim3(a.num_slices), dim3(64 * kMaxRows), 0, s, a);
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_slice_scan, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_mb_concat, dim3((nmb + 3) / 4), dim3(256), 0, s, a);

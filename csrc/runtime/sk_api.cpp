@@ -187,6 +187,13 @@ void* sk_h264_create(const sk_h264_config* c) {
         set_last_error("stripe_height must be a multiple of 16");
         return nullptr;
     }
+    // the HIP intra/deblock wavefronts run one wave per MB row of a stripe (+1 producer wave)
+    // in one workgroup: at most 15 rows (1024 threads). Same limit on the CPU reference so
+    // both backends accept the same configurations.
+    if (c->stripe_height > 240) {
+        set_last_error("stripe_height must be <= 240 (15 macroblock rows per stripe)");
+        return nullptr;
+    }
     if (c->qp < 0 || c->qp > 51 || c->paint_qp < 0 || c->paint_qp > 51) {
         set_last_error("qp out of range");
         return nullptr;

@@ -15,9 +15,11 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[2]
 CSRC = ROOT / "csrc"
-BUILD = ROOT / "build" / "native"
+_STAMPS = bool(os.environ.get("SK_STAMPS_BUILD"))
+BUILD = ROOT / "build" / ("native_stamps" if _STAMPS else "native")
 LIBDIR = ROOT / "selkies_gstreamer_amd" / "_lib"
-LIB = LIBDIR / "libselkies_native.so"
+# diagnostic build with s_memtime stamps (SK_STAMPS_BUILD=1) goes to its own library
+LIB = LIBDIR / ("libselkies_native_stamps.so" if _STAMPS else "libselkies_native.so")
 ARCH = os.environ.get("SK_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

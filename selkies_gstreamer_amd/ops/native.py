@@ -15,7 +15,8 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parents[1] / "_lib" / "libselkies_native.so"
+LIB_PATH = Path(os.environ["SK_NATIVE_LIB"]) if os.environ.get("SK_NATIVE_LIB") else \
+    Path(__file__).resolve().parents[1] / "_lib" / "libselkies_native.so"
 _lib = None
 _lock = threading.Lock()
 

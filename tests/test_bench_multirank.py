@@ -22,7 +22,7 @@ def test_two_rank_cpu_bench():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
            "--backend", "cpu", "--gpus", "2", "--steps", "2", "--warmup", "1", "--sessions", "2",
-           "--width", "256", "--height", "128", "--pool", "2", "--gather"]
+           "--width", "256", "--height", "128", "--pool", "2", "--gather", "--path", "encoder"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -1,9 +1,13 @@
-"""Diagnostic: per-segment cycle shares of the intra wavefront kernel (needs a
-library built with SK_STAMPS_BUILD=1 and SK_STAMPS=1 at run time)."""
+"""Diagnostic: per-segment cycle shares of the H.264 intra wavefront kernel.
+
+Needs the stamps library: SK_STAMPS_BUILD=1 python -m selkies_gstreamer_amd.ops.build
+(-> _lib/libselkies_native_stamps.so); this script selects it and sets SK_STAMPS=1."""
 import os, sys
 import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["SK_STAMPS"] = "1"
-sys.path.insert(0, ".")
+os.environ["SK_NATIVE_LIB"] = os.path.join(ROOT, "selkies_gstreamer_amd", "_lib", "libselkies_native_stamps.so")
+sys.path.insert(0, ROOT)
 from selkies_gstreamer_amd.ops.native import H264Encoder
 from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
 W, H = 1920, 1080
@@ -13,13 +17,18 @@ for t in range(3):
     enc.request_keyframe()
     enc.encode(src.frame(t), t)
 st = enc.debug_buffer("stamps", np.uint64).reshape(64, 16).astype(np.int64)
-names = ["start", "lumamode", "chromamode", "code_mb:in", "quantloop", "recon", "coefcopy", "edges/end"]
-for step in (10, 11, 12, 30, 31):
+# points: 0 start, 2 pred done, 3 fwd transform done, 9 quant lanes in, 10 dc, 11 analysis,
+# 12 crude bound, 4 quant loop done, 5 recon done, 6 code_mb done, 7 edges done, 8 after barrier
+seg = [("pred", 0, 2), ("fwd", 2, 3), ("q_in", 3, 9), ("q_dc", 9, 10), ("q_analysis", 10, 11),
+       ("q_crude", 11, 12), ("q_tail", 12, 4), ("recon", 4, 5), ("copy", 5, 6), ("store+edges", 6, 7),
+       ("barrier", 7, 8)]
+rows = []
+for step in range(10, 60):
     r = st[step]
-    d = [r[i + 1] - r[i] for i in range(7)] + [r[8] - r[0]]
-    print(step, dict(zip(["mode_l", "mode_c", "prep", "quant", "recon", "copy", "edges", "step_total"], d)))
-for step in (10, 11, 12, 30):
-    r = st[step]
-    print(step, "q-in->quant", r[9] - r[3], "dc", r[10] - r[9], "analysis", r[11] - r[10], "crude", r[12] - r[11],
-          "crude_bits", r[14], "iters", r[15] & 0xffff, "bound", r[15] >> 32)
-print("median step cycles (s_memtime ticks):", np.median(st[10:60, 8] - st[9:59, 8]))
+    rows.append([r[b] - r[a] for _, a, b in seg] + [r[8] - r[0], r[15] & 0xffff])
+rows = np.array(rows)
+med = np.median(rows, axis=0)
+for (n, _, _), v in zip(seg, med[:-2]):
+    print(f"{n:12s} {v:8.0f}")
+print(f"{'step total':12s} {med[-2]:8.0f}   quant iterations (median) {med[-1]:.0f}")
+print("median step-to-step cycles:", np.median(st[11:60, 8] - st[10:59, 8]))
