@@ -44,6 +44,7 @@ struct EncoderConfig {
                                  // previous-but-one picture as a second P reference (blinking/toggling UI)
     int src_width = 0;           // K2: capture size when it differs from width x height (0 = same);
     int src_height = 0;          //     the frame is resampled (bilinear) inside the K1 conversion
+    int codec = 0;               // 0 = H.264, 1 = HEVC (hevc_encoder.h: same front end, full frame)
 };
 
 struct Geometry {

@@ -1,0 +1,863 @@
+// H.265 / HEVC Main-profile primitives shared by the CPU reference encoder
+// (hevc_cpu.cpp) and the gfx950 kernels (kernels/hevc_kernels.hip): transforms,
+// (de)quantisation, intra prediction, chroma motion compensation, merge / AMVP
+// candidate lists, the syntax binarisation into CABAC bins and the CABAC
+// arithmetic coder itself.
+//
+// Coding structure (fixed by the parameter sets in hevc_syntax.cpp):
+//   CTB = CU = 16x16 (log2 min CB 4, no split flags), PU 2Nx2N, TU = CU (16x16 luma,
+//   8x8 chroma, no transform split), one reference picture (previous picture),
+//   integer-pel motion, no deblocking / SAO / sign hiding / transform skip,
+//   entropy_coding_sync (WPP): one CABAC substream per CTB row, slices = stripes of
+//   whole CTB rows.
+// Decoder-side operations (inverse transform, dequantisation, intra prediction,
+// chroma interpolation, merge/AMVP derivation, context selection) follow the
+// normative processes of ITU-T H.265 (04/2013) clauses 8 and 9 exactly; forward
+// transform and quantisation are encoder choice (HM-style dead zone).
+#pragma once
+#include <stddef.h>
+#include "sk_common.h"
+
+namespace sk {
+namespace hevc {
+
+constexpr int kCtb = 16;
+constexpr int kCoefPerCu = 384;     // 16x16 luma | 8x8 Cb | 8x8 Cr, raster [y][x] per TU
+constexpr int kCoefCb = 256, kCoefCr = 320;
+constexpr int kCuBinCap = 4096;     // bin entries per CU slot (worst case ~3950, see bin_bound)
+constexpr int kSubstreamCtbBytes = 4608;   // worst-case CABAC bytes per CTB (>= 6 bits x ctx bins)
+
+// ---------------------------------------------------------------------------
+// Per-CU decisions (16 bytes, shared by CPU and GPU buffers; tests diff them).
+enum CuMode : uint8_t { CU_SKIP = 0, CU_MERGE = 1, CU_AMVP = 2, CU_INTRA = 3 };
+struct CuInfo {
+    uint8_t mode;         // CuMode
+    uint8_t merge_idx;    // SKIP / MERGE
+    uint8_t mvp_idx;      // AMVP
+    uint8_t intra_mode;   // IntraPredModeY (chroma: DM, intra_chroma_pred_mode = 4)
+    uint8_t cbf;          // bit0 Y, bit1 Cb, bit2 Cr
+    uint8_t qp;
+    uint8_t pad[2];
+    int16_t mvx, mvy;     // quarter-pel
+    int16_t mvdx, mvdy;   // AMVP: mv - predictor
+};
+static_assert(sizeof(CuInfo) == 16, "CuInfo layout");
+
+// ---------------------------------------------------------------------------
+// Tables.
+SK_TABLE int8_t HEVC_T16[16][16] = {
+    {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64},
+    {90, 87, 80, 70, 57, 43, 25, 9, -9, -25, -43, -57, -70, -80, -87, -90},
+    {89, 75, 50, 18, -18, -50, -75, -89, -89, -75, -50, -18, 18, 50, 75, 89},
+    {87, 57, 9, -43, -80, -90, -70, -25, 25, 70, 90, 80, 43, -9, -57, -87},
+    {83, 36, -36, -83, -83, -36, 36, 83, 83, 36, -36, -83, -83, -36, 36, 83},
+    {80, 9, -70, -87, -25, 57, 90, 43, -43, -90, -57, 25, 87, 70, -9, -80},
+    {75, -18, -89, -50, 50, 89, 18, -75, -75, 18, 89, 50, -50, -89, -18, 75},
+    {70, -43, -87, 9, 90, 25, -80, -57, 57, 80, -25, -90, -9, 87, 43, -70},
+    {64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64},
+    {57, -80, -25, 90, -9, -87, 43, 70, -70, -43, 87, 9, -90, 25, 80, -57},
+    {50, -89, 18, 75, -75, -18, 89, -50, -50, 89, -18, -75, 75, 18, -89, 50},
+    {43, -90, 57, 25, -87, 70, 9, -80, 80, -9, -70, 87, -25, -57, 90, -43},
+    {36, -83, 83, -36, -36, 83, -83, 36, 36, -83, 83, -36, -36, 83, -83, 36},
+    {25, -70, 90, -80, 43, 9, -57, 87, -87, 57, -9, -43, 80, -90, 70, -25},
+    {18, -50, 75, -89, 89, -75, 50, -18, -18, 50, -75, 89, -89, 75, -50, 18},
+    {9, -25, 43, -57, 70, -80, 87, -90, 90, -87, 80, -70, 57, -43, 25, -9}};
+// The 8-point matrix is rows 0, 2, 4, ... of the 16-point one restricted to 8 columns.
+SK_HD int dct_coef(int log2n, int k, int n) { return HEVC_T16[k << (4 - log2n)][n]; }
+
+// Up-right diagonal scan of a 4x4 (sub-)block: scan position -> raster (y*4+x), and back.
+SK_HD int diag4_raster(int n) { return (int)((0xfbe7ad369c258140ULL >> (4 * n)) & 15); }
+SK_HD int diag4_scanpos(int r) { return (int)((0xfda6eb73c8419520ULL >> (4 * r)) & 15); }
+// Sub-block scans: 2x2 for 8x8 TUs, 4x4 for 16x16 TUs (same diagonal rule).
+SK_HD int diag2_raster(int n) { return (int)((0x3120u >> (4 * n)) & 15); }   // (0,0),(0,1),(1,0),(1,1) as y*2+x
+SK_HD int sb_raster(int log2n, int i) {   // sub-block scan index -> raster index in the sub-block grid
+    return log2n == 4 ? diag4_raster(i) : (log2n == 3 ? diag2_raster(i) : 0);
+}
+
+// CABAC (shared with H.264): LPS ranges and LPS state transitions.
+SK_TABLE uint8_t CABAC_LPS[64][4] = {
+    {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205}, {116, 142, 169, 195},
+    {111, 135, 160, 185}, {105, 128, 152, 175}, {100, 122, 144, 166}, {95, 116, 137, 158}, {90, 110, 130, 150},
+    {85, 104, 123, 142},  {81, 99, 117, 135},   {77, 94, 111, 128},   {73, 89, 105, 122},  {69, 85, 100, 116},
+    {66, 80, 95, 110},    {62, 76, 90, 104},    {59, 72, 86, 99},     {56, 69, 81, 94},    {53, 65, 77, 89},
+    {51, 62, 73, 85},     {48, 59, 69, 80},     {46, 56, 66, 76},     {43, 53, 63, 72},    {41, 50, 59, 69},
+    {39, 48, 56, 65},     {37, 45, 54, 62},     {35, 43, 51, 59},     {33, 41, 48, 56},    {32, 39, 46, 53},
+    {30, 37, 43, 50},     {29, 35, 41, 48},     {27, 33, 39, 45},     {26, 31, 37, 43},    {24, 30, 35, 41},
+    {23, 28, 33, 39},     {22, 27, 32, 37},     {21, 26, 30, 35},     {20, 24, 29, 33},    {19, 23, 27, 31},
+    {18, 22, 26, 30},     {17, 21, 25, 28},     {16, 20, 23, 27},     {15, 19, 22, 25},    {14, 18, 21, 24},
+    {14, 17, 20, 23},     {13, 16, 19, 22},     {12, 15, 18, 21},     {12, 14, 17, 20},    {11, 14, 16, 19},
+    {11, 13, 15, 18},     {10, 12, 15, 17},     {10, 12, 14, 16},     {9, 11, 13, 15},     {9, 11, 12, 14},
+    {8, 10, 12, 14},      {8, 9, 11, 13},       {7, 9, 11, 12},       {7, 9, 10, 12},      {7, 8, 10, 11},
+    {6, 8, 9, 11},        {6, 7, 9, 10},        {6, 7, 8, 9},         {2, 2, 2, 2}};
+SK_TABLE uint8_t CABAC_NEXT_LPS[64] = {0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12,
+                                       13, 13, 15, 15, 16, 16, 18, 18, 19, 19, 21, 21, 22, 22, 23, 24,
+                                       24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33,
+                                       33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
+
+// ---------------------------------------------------------------------------
+// Context index space (flat). initValues per initType (0 = I, 1 = P with
+// cabac_init_flag 0): Tables 9-5 .. 9-37 of H.265.
+enum Ctx : int {
+    CTX_SKIP = 0,            // 3 (ctxInc = condL + condA)
+    CTX_PRED_MODE = 3,
+    CTX_PART_MODE = 4,       // first bin only (2Nx2N)
+    CTX_PREV_INTRA = 5,
+    CTX_CHROMA_PRED = 6,
+    CTX_MERGE_FLAG = 7,
+    CTX_MERGE_IDX = 8,
+    CTX_MVP = 9,
+    CTX_RQT_ROOT_CBF = 10,
+    CTX_MVD_G0 = 11,
+    CTX_MVD_G1 = 12,
+    CTX_CBF_LUMA = 13,       // 2
+    CTX_CBF_CHROMA = 15,     // 4
+    CTX_LAST_X = 19,         // 18
+    CTX_LAST_Y = 37,         // 18
+    CTX_CSBF = 55,           // 4
+    CTX_SIG = 59,            // 42
+    CTX_GT1 = 101,           // 24
+    CTX_GT2 = 125,           // 6
+    CTX_COUNT = 131,
+    CTX_TERM = 255           // terminating bin (end_of_slice_segment_flag / end_of_subset_one_bit)
+};
+SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
+    {// I slices
+     154, 154, 154,                 // skip (n/a)
+     154,                           // pred_mode (n/a)
+     184,                           // part_mode
+     184,                           // prev_intra_luma_pred_flag
+     63,                            // intra_chroma_pred_mode
+     154, 154, 154, 154,            // merge_flag, merge_idx, mvp, rqt_root_cbf (n/a)
+     154, 154,                      // mvd (n/a)
+     111, 141,                      // cbf_luma
+     94, 138, 182, 154,             // cbf_cb/cr
+     110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,   // last x
+     110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,   // last y
+     91, 171, 134, 141,             // coded_sub_block_flag
+     111, 111, 125, 110, 110, 94, 124, 108, 124, 107, 125, 141, 179, 153, 125, 107, 125, 141, 179, 153, 125,
+     107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153, 136, 139, 111, 136, 139, 111,
+     140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166, 182, 140, 227,
+     122, 197,                      // greater1
+     138, 153, 136, 167, 152, 152},  // greater2
+    {// P slices (cabac_init_flag = 0)
+     197, 185, 201,                 // cu_skip_flag
+     149,                           // pred_mode_flag
+     154,                           // part_mode
+     154,                           // prev_intra_luma_pred_flag
+     152,                           // intra_chroma_pred_mode
+     110, 122, 168, 79,             // merge_flag, merge_idx, mvp_l0_flag, rqt_root_cbf
+     140, 198,                      // abs_mvd_greater0 / greater1
+     153, 111,                      // cbf_luma
+     149, 107, 167, 154,            // cbf_cb/cr
+     125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,     // last x
+     125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108,     // last y
+     121, 140, 61, 154,             // coded_sub_block_flag
+     155, 154, 139, 153, 139, 123, 123, 63, 153, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153, 154,
+     166, 183, 140, 136, 153, 154, 170, 153, 138, 138, 122, 121, 122, 121, 167, 151, 183, 140, 151, 183, 140,
+     154, 196, 196, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 137, 169, 194, 166, 167, 154, 167,
+     137, 182,                      // greater1
+     107, 167, 91, 122, 107, 167}};  // greater2
+
+// Context state byte: (pStateIdx << 1) | valMps (9.3.2.2).
+SK_HD uint8_t ctx_init_state(int init_value, int slice_qp) {
+    const int slope = init_value >> 4, offset = init_value & 15;
+    const int m = slope * 5 - 45, n = (offset << 3) - 16;
+    const int pre = sk_clip(((m * sk_clip(slice_qp, 0, 51)) >> 4) + n, 1, 126);
+    const int mps = pre <= 63 ? 0 : 1;
+    const int st = mps ? pre - 64 : 63 - pre;
+    return (uint8_t)((st << 1) | mps);
+}
+SK_HD void ctx_init_all(uint8_t* st, int init_type, int slice_qp) {
+    for (int i = 0; i < CTX_COUNT; i++) st[i] = ctx_init_state(HEVC_CTX_INIT[init_type][i], slice_qp);
+}
+// Context adaptation only (no arithmetic coding): used to derive WPP sync states.
+SK_HD void ctx_update(uint8_t& s, int bin) {
+    int st = s >> 1, mps = s & 1;
+    if (bin == mps) st = st < 62 ? st + 1 : 62;
+    else {
+        if (st == 0) mps ^= 1;
+        st = CABAC_NEXT_LPS[st];
+    }
+    s = (uint8_t)((st << 1) | mps);
+}
+
+// ---------------------------------------------------------------------------
+// Bin entries (uint16), produced by the binariser and consumed by the CABAC coder:
+//   context bin  : bit15 = 0, bit8 = bin value, bits 0..7 = context index (CTX_TERM: terminate)
+//   bypass run   : bit15 = 1, bits 12..14 = n - 1 (n = 1..8 bins), bits 0..7 = the bins (MSB first)
+struct BinBuf {
+    uint16_t* p;
+    int n;
+    SK_HD void ctx(int c, int b) { p[n++] = (uint16_t)(((b & 1) << 8) | c); }
+    SK_HD void term(int b) { p[n++] = (uint16_t)(((b & 1) << 8) | CTX_TERM); }
+    SK_HD void bypass(uint32_t v, int nb) {
+        while (nb > 0) {
+            const int k = nb > 8 ? 8 : nb;
+            nb -= k;
+            p[n++] = (uint16_t)(0x8000u | ((uint32_t)(k - 1) << 12) | ((v >> nb) & ((1u << k) - 1)));
+        }
+    }
+};
+struct BinCount {   // same interface, counts entries
+    int n = 0;
+    SK_HD void ctx(int, int) { n++; }
+    SK_HD void term(int) { n++; }
+    SK_HD void bypass(uint32_t, int nb) { n += (nb + 7) >> 3; }
+};
+
+// ---------------------------------------------------------------------------
+// CABAC arithmetic encoder (9.3.4.3 encoder side, HM TEncBinCABAC arithmetic).
+// Output is a byte-aligned substream; finish() appends the terminating bits and the
+// byte_alignment() / rbsp stop bit ('1' + zeros).
+struct CabacEncoder {
+    uint32_t low, range;
+    int32_t bits_left, num_buffered;
+    uint32_t buffered;
+    uint8_t* out;
+    uint32_t pos;   // bytes written
+    SK_HD void start(uint8_t* o) {
+        out = o;
+        pos = 0;
+        low = 0;
+        range = 510;
+        bits_left = 23;
+        num_buffered = 0;
+        buffered = 0xff;
+    }
+    SK_HD void put(uint32_t b) { out[pos++] = (uint8_t)b; }
+    SK_HD void write_out() {
+        const uint32_t lead = low >> (24 - bits_left);
+        bits_left += 8;
+        low &= 0xffffffffu >> bits_left;
+        if (lead == 0xff) {
+            num_buffered++;
+        } else if (num_buffered > 0) {
+            const uint32_t carry = lead >> 8;
+            put(buffered + carry);
+            buffered = lead & 0xff;
+            const uint32_t fill = (0xff + carry) & 0xff;
+            while (num_buffered > 1) {
+                put(fill);
+                num_buffered--;
+            }
+        } else {
+            num_buffered = 1;
+            buffered = lead;
+        }
+    }
+    SK_HD void test_write() {
+        if (bits_left < 12) write_out();
+    }
+    SK_HD void encode(int bin, uint8_t& s) {
+        const int st = s >> 1, mps = s & 1;
+        const uint32_t lps = CABAC_LPS[st][(range >> 6) & 3];
+        range -= lps;
+        if (bin != mps) {
+            const int nbits = 8 - (31 - __builtin_clz(lps));   // renormalisation shift
+            low = (low + range) << nbits;
+            range = lps << nbits;
+            bits_left -= nbits;
+            s = (uint8_t)((CABAC_NEXT_LPS[st] << 1) | (st == 0 ? mps ^ 1 : mps));
+        } else {
+            s = (uint8_t)(((st < 62 ? st + 1 : 62) << 1) | mps);
+            if (range >= 256) return;
+            low <<= 1;
+            range <<= 1;
+            bits_left--;
+        }
+        test_write();
+    }
+    SK_HD void bypass(uint32_t bins, int n) {   // n <= 8
+        low = (low << n) + range * bins;
+        bits_left -= n;
+        test_write();
+    }
+    SK_HD void terminate(int bin) {
+        range -= 2;
+        if (bin) {
+            low += range;
+            low <<= 7;
+            range = 2 << 7;
+            bits_left -= 7;
+        } else if (range >= 256) {
+            return;
+        } else {
+            low <<= 1;
+            range <<= 1;
+            bits_left--;
+        }
+        test_write();
+    }
+    // After terminate(1): flush, then the '1' alignment bit and zero bits to a byte boundary.
+    SK_HD void finish() {
+        if (low >> (32 - bits_left)) {
+            put(buffered + 1);
+            while (num_buffered > 1) {
+                put(0x00);
+                num_buffered--;
+            }
+            low -= 1u << (32 - bits_left);
+        } else {
+            if (num_buffered > 0) put(buffered);
+            while (num_buffered > 1) {
+                put(0xff);
+                num_buffered--;
+            }
+        }
+        // remaining 24 - bits_left bits of low >> 8, then '1', then zeros
+        const int nb = 24 - bits_left;
+        uint64_t acc = ((uint64_t)(low >> 8) & ((1ull << nb) - 1)) << 1 | 1ull;
+        int total = nb + 1;
+        const int pad = (8 - (total & 7)) & 7;
+        acc <<= pad;
+        total += pad;
+        for (int i = total - 8; i >= 0; i -= 8) put((uint32_t)(acc >> i) & 0xff);
+    }
+    // Codes one bin entry (see BinBuf) with context states `ctx`.
+    SK_HD void code_entry(uint16_t e, uint8_t* ctx) {
+        if (e & 0x8000u) {
+            bypass(e & 0xffu, ((e >> 12) & 7) + 1);
+        } else if ((e & 0xffu) == CTX_TERM) {
+            terminate((e >> 8) & 1);
+        } else {
+            encode((e >> 8) & 1, ctx[e & 0xffu]);
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Transforms. Residual / coefficient blocks are raster [y][x] int arrays.
+// Forward (encoder choice, HM partial butterflies as matrix products):
+// shift1 = log2n + bitDepth - 9, shift2 = log2n + 6.
+SK_HD void fwd_transform(const int* res, int log2n, int* coef) {
+    const int n = 1 << log2n;
+    const int sh1 = log2n - 1, sh2 = log2n + 6;
+    int tmp[256];
+    for (int y = 0; y < n; y++)          // horizontal: tmp[y][u]
+        for (int u = 0; u < n; u++) {
+            int s = 0;
+            for (int x = 0; x < n; x++) s += dct_coef(log2n, u, x) * res[y * n + x];
+            tmp[y * n + u] = (s + (1 << (sh1 - 1))) >> sh1;
+        }
+    for (int v = 0; v < n; v++)          // vertical: coef[v][u]
+        for (int u = 0; u < n; u++) {
+            int s = 0;
+            for (int y = 0; y < n; y++) s += dct_coef(log2n, v, y) * tmp[y * n + u];
+            coef[v * n + u] = (s + (1 << (sh2 - 1))) >> sh2;
+        }
+}
+// Inverse (8.6.4.2): columns first, clip to 16 bits after (e + 64) >> 7, then rows,
+// residual = (r + 2048) >> 12 for 8-bit video.
+SK_HD void inv_transform(const int* d, int log2n, int* res) {
+    const int n = 1 << log2n;
+    int g[256];
+    for (int x = 0; x < n; x++)
+        for (int y = 0; y < n; y++) {
+            int s = 0;
+            for (int j = 0; j < n; j++) s += dct_coef(log2n, j, y) * d[j * n + x];
+            g[y * n + x] = sk_clip((s + 64) >> 7, -32768, 32767);
+        }
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) {
+            int s = 0;
+            for (int j = 0; j < n; j++) s += dct_coef(log2n, j, x) * g[y * n + j];
+            res[y * n + x] = (s + 2048) >> 12;
+        }
+}
+
+// Quantisation (HM: quantScale, QUANT_SHIFT 14, transform shift 15 - 8 - log2n,
+// dead-zone offset 171/512 intra, 85/512 inter) and dequantisation (8.6.3, flat m = 16).
+SK_HD int quant_scale(int r) { return r == 0 ? 26214 : r == 1 ? 23302 : r == 2 ? 20560 : r == 3 ? 18396 : r == 4 ? 16384 : 14564; }
+SK_HD int level_scale(int r) { return r == 0 ? 40 : r == 1 ? 45 : r == 2 ? 51 : r == 3 ? 57 : r == 4 ? 64 : 72; }
+constexpr int kMaxLevel = 32767;
+SK_HD int quant_level(int c, int qp, int log2n, bool intra) {
+    const int qbits = 14 + qp / 6 + (7 - log2n);
+    const int64_t add = (int64_t)(intra ? 171 : 85) << (qbits - 9);
+    const int a = sk_abs(c);
+    int l = (int)(((int64_t)a * quant_scale(qp % 6) + add) >> qbits);
+    l = sk_min(l, kMaxLevel);
+    return c < 0 ? -l : l;
+}
+SK_HD int dequant_level(int l, int qp, int log2n) {
+    // d = Clip3(-32768, 32767, (l * m * levelScale[qp % 6] << (qp / 6)) + (1 << (bdShift - 1)) >> bdShift),
+    // m = 16 (flat), bdShift = BitDepth + log2n - 5
+    const int bdshift = 3 + log2n;
+    const int64_t v = ((int64_t)l * 16 * level_scale(qp % 6) * ((int64_t)1 << (qp / 6)) + (1 << (bdshift - 1))) >> bdshift;
+    return (int)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v));
+}
+// QpC for ChromaArrayType 1 (Table 8-10): qPi < 30 -> qPi; 30..43 -> table; > 43 -> qPi - 6.
+SK_HD int chroma_qp(int qpi) {
+    if (qpi < 30) return qpi;
+    if (qpi > 43) return qpi - 6;
+    return 29 + (int)((0x88776655443210ull >> (4 * (qpi - 30))) & 15);
+}
+
+// ---------------------------------------------------------------------------
+// Intra prediction (8.4.4.2). ref[] is the linear reference array of a TU of size
+// N: ref[0] = p[-1][2N-1] (bottom of the left column) ... ref[2N-1] = p[-1][0],
+// ref[2N] = p[-1][-1], ref[2N+1+x] = p[x][-1] (x = 0..2N-1). avail[] flags per
+// entry. Substitution (8.4.4.2.2) in place.
+SK_HD void intra_substitute(uint8_t* ref, const uint8_t* avail, int n) {
+    const int len = 4 * n + 1;
+    int first = -1;
+    for (int i = 0; i < len; i++)
+        if (avail[i]) { first = i; break; }
+    if (first < 0) {
+        for (int i = 0; i < len; i++) ref[i] = 128;
+        return;
+    }
+    for (int i = 0; i < first; i++) ref[i] = ref[first];
+    for (int i = first + 1; i < len; i++)
+        if (!avail[i]) ref[i] = ref[i - 1];
+}
+// [1 2 1] smoothing (8.4.4.2.3) when filterFlag: luma, mode != DC, N > 4 and
+// min(|mode - 26|, |mode - 10|) > thres(N) (7 for 8x8, 1 for 16x16, 0 for 32x32).
+SK_HD bool intra_filter_flag(int mode, int log2n, int cidx) {
+    if (cidx != 0 || mode == 1 || log2n == 2) return false;
+    const int d = sk_min(sk_abs(mode - 26), sk_abs(mode - 10));
+    const int thres = log2n == 3 ? 7 : (log2n == 4 ? 1 : 0);
+    return d > thres;
+}
+SK_HD void intra_filter(const uint8_t* ref, int n, uint8_t* out) {
+    const int len = 4 * n + 1;
+    out[0] = ref[0];
+    out[len - 1] = ref[len - 1];
+    for (int i = 1; i < len - 1; i++) out[i] = (uint8_t)((ref[i - 1] + 2 * ref[i] + ref[i + 1] + 2) >> 2);
+}
+SK_TABLE int8_t HEVC_INTRA_ANGLE[35] = {0,   0,   32,  26,  21,  17,  13,  9,   5,   2,   0,   -2,
+                                        -5,  -9,  -13, -17, -21, -26, -32, -26, -21, -17, -13, -9,
+                                        -5,  -2,  0,   2,   5,   9,   13,  17,  21,  26,  32};
+SK_HD int intra_inv_angle(int mode) {   // modes 11..25
+    const int a = sk_abs(HEVC_INTRA_ANGLE[mode]);
+    return a == 2 ? -4096 : a == 5 ? -1638 : a == 9 ? -910 : a == 13 ? -630 : a == 17 ? -482 : a == 21 ? -390
+                  : a == 26 ? -315 : -256;
+}
+// Prediction sample (x, y) of an N x N block from the (filtered) linear reference.
+SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int cidx, int x, int y) {
+    auto L = [&](int yy) { return (int)ref[2 * n - 1 - yy]; };   // p[-1][yy], yy = -1 .. 2N-1
+    auto T = [&](int xx) { return (int)ref[2 * n + 1 + xx]; };   // p[xx][-1], xx = -1 .. 2N-1
+    if (mode == 0) {
+        return ((n - 1 - x) * L(y) + (x + 1) * T(n) + (n - 1 - y) * T(x) + (y + 1) * L(n) + n) >> (log2n + 1);
+    }
+    if (mode == 1) {
+        int s = n;
+        for (int i = 0; i < n; i++) s += T(i) + L(i);
+        const int dc = s >> (log2n + 1);
+        if (cidx == 0 && n < 32) {
+            if (x == 0 && y == 0) return (L(0) + 2 * dc + T(0) + 2) >> 2;
+            if (y == 0) return (T(x) + 3 * dc + 2) >> 2;
+            if (x == 0) return (L(y) + 3 * dc + 2) >> 2;
+        }
+        return dc;
+    }
+    const int angle = HEVC_INTRA_ANGLE[mode];
+    // main reference array refm[k], k = -N .. 2N (index k + N)
+    int refm[3 * 32 + 1];
+    const bool vert = mode >= 18;
+    auto side = [&](int k) { return vert ? T(k - 1) : L(k - 1); };     // k = 0..2N: main side incl. corner
+    auto other = [&](int k) { return vert ? L(k - 1) : T(k - 1); };    // projected side
+    for (int k = 0; k <= 2 * n; k++) refm[k + n] = side(k);
+    if (angle < 0) {
+        const int last = (n * angle) >> 5;
+        if (last < -1) {
+            const int inv = intra_inv_angle(mode);
+            for (int k = last; k <= -1; k++) refm[k + n] = other(((k * inv + 128) >> 8));
+        }
+    }
+    const int a = vert ? y : x, b = vert ? x : y;   // a: distance from the main side, b: along it
+    const int idx = ((a + 1) * angle) >> 5, fact = ((a + 1) * angle) & 31;
+    int v = fact ? ((32 - fact) * refm[b + idx + 1 + n] + fact * refm[b + idx + 2 + n] + 16) >> 5
+                 : refm[b + idx + 1 + n];
+    if (cidx == 0 && n < 32) {
+        if (mode == 26 && x == 0) v = sk_clip255(T(0) + ((L(y) - L(-1)) >> 1));
+        if (mode == 10 && y == 0) v = sk_clip255(L(0) + ((T(x) - T(-1)) >> 1));
+    }
+    return v;
+}
+
+// Most probable modes (8.4.2) for CTB = CU: candB is always DC (above CTB row).
+SK_HD void intra_mpm(int cand_a, int* list) {
+    const int cand_b = 1;
+    if (cand_a == cand_b) {
+        list[0] = 0; list[1] = 1; list[2] = 26;   // candA < 2
+    } else {
+        list[0] = cand_a;
+        list[1] = cand_b;
+        list[2] = (cand_a != 0 && cand_b != 0) ? 0 : ((cand_a != 1 && cand_b != 1) ? 1 : 26);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Chroma motion compensation (8.5.3.3.3.3) for integer or fractional luma vectors in
+// quarter-pel (4:2:0: chroma fraction in 1/8), uni-prediction weighted to 8 bits.
+SK_HD int chroma_filter_tap(int frac, int i) {
+    // fC[frac][i] (Table 8-13): {0,64,0,0} {-2,58,10,-2} {-4,54,16,-2} {-6,46,28,-4}
+    // {-4,36,36,-4} {-4,28,46,-6} {-2,16,54,-4} {-2,10,58,-2}; outer taps packed as
+    // negated nibbles, inner taps as bytes.
+    const int outer = (int)((0x2242644446242200ull >> (8 * frac + 4 * (i == 3))) & 15);
+    const uint64_t inner0 = 0x0A101C242E363A40ull, inner1 = 0x3A362E241C100A00ull;
+    if (i == 0 || i == 3) return -outer;
+    return (int)(((i == 1 ? inner0 : inner1) >> (8 * frac)) & 0xff);
+}
+SK_HD int chroma_mc_sample(const uint8_t* plane, int stride, int w, int h, int xc, int yc, int mvx, int mvy) {
+    const int xi = xc + (mvx >> 3), yi = yc + (mvy >> 3), fx = mvx & 7, fy = mvy & 7;
+    auto P = [&](int x, int y) { return (int)plane[(size_t)sk_clip(y, 0, h - 1) * stride + sk_clip(x, 0, w - 1)]; };
+    int v;
+    if (fx == 0 && fy == 0) {
+        v = P(xi, yi) << 6;
+    } else if (fy == 0) {
+        v = 0;
+        for (int i = 0; i < 4; i++) v += chroma_filter_tap(fx, i) * P(xi + i - 1, yi);
+    } else if (fx == 0) {
+        v = 0;
+        for (int i = 0; i < 4; i++) v += chroma_filter_tap(fy, i) * P(xi, yi + i - 1);
+    } else {
+        v = 0;
+        for (int r = 0; r < 4; r++) {
+            int t = 0;
+            for (int i = 0; i < 4; i++) t += chroma_filter_tap(fx, i) * P(xi + i - 1, yi + r - 1);
+            v += chroma_filter_tap(fy, r) * t;   // shift1 = 0 for 8-bit
+        }
+        v >>= 6;   // shift2
+    }
+    return sk_clip255((v + 32) >> 6);   // default weighted prediction: shift 14 - 8
+}
+
+// ---------------------------------------------------------------------------
+// Merge candidates (8.5.3.2.2-4) and AMVP predictors (8.5.3.2.6-7) for a 16x16
+// 2Nx2N PU of a P slice with one reference picture. Neighbours: A1 left, B1 above,
+// B0 above-right, B2 above-left (A0 below-left is never decoded yet); `av` flags
+// include "inter" (P slices here carry inter CUs only). MVs quarter-pel.
+struct NbMv {
+    bool av;
+    int mvx, mvy;
+};
+constexpr int kMaxMergeCand = 5;
+SK_HD int merge_list(const NbMv& A1, const NbMv& B1, const NbMv& B0, const NbMv& B2, int* lx, int* ly) {
+    int n = 0;
+    auto same = [](const NbMv& p, const NbMv& q) { return p.av && q.av && p.mvx == q.mvx && p.mvy == q.mvy; };
+    const bool a1 = A1.av;
+    const bool b1 = B1.av && !same(A1, B1);
+    const bool b0 = B0.av && !same(B1, B0);
+    const bool a0 = false;
+    const bool b2 = B2.av && !same(A1, B2) && !same(B1, B2) && ((int)a1 + (int)b1 + (int)b0 + (int)a0) != 4;
+    if (a1) { lx[n] = A1.mvx; ly[n] = A1.mvy; n++; }
+    if (b1) { lx[n] = B1.mvx; ly[n] = B1.mvy; n++; }
+    if (b0) { lx[n] = B0.mvx; ly[n] = B0.mvy; n++; }
+    if (b2) { lx[n] = B2.mvx; ly[n] = B2.mvy; n++; }
+    while (n < kMaxMergeCand) { lx[n] = 0; ly[n] = 0; n++; }   // zero candidates (refIdx 0)
+    return n;
+}
+SK_HD void amvp_list(const NbMv& A1, const NbMv& B1, const NbMv& B0, const NbMv& B2, int* px, int* py) {
+    // A: first available of A0, A1 (same reference picture: all inter neighbours here)
+    bool avA = A1.av;
+    int ax = A1.mvx, ay = A1.mvy;
+    bool avB = false;
+    int bx = 0, by = 0;
+    if (B0.av) { avB = true; bx = B0.mvx; by = B0.mvy; }
+    else if (B1.av) { avB = true; bx = B1.mvx; by = B1.mvy; }
+    else if (B2.av) { avB = true; bx = B2.mvx; by = B2.mvy; }
+    const bool is_scaled = A1.av;   // availableA0 || availableA1
+    if (!is_scaled && avB) { avA = true; ax = bx; ay = by; }
+    if (!is_scaled) {
+        // B re-derived with scaling allowed: identical vector (same POC distance)
+        avB = B0.av || B1.av || B2.av;
+    }
+    int n = 0;
+    if (avA) { px[n] = ax; py[n] = ay; n++; }
+    if (avB && !(avA && ax == bx && ay == by)) { px[n] = bx; py[n] = by; n++; }
+    while (n < 2) { px[n] = 0; py[n] = 0; n++; }
+}
+// EGk bypass bin count and value (9.3.3.3).
+SK_HD int egk_bins(uint32_t v, int k, uint32_t* bits) {
+    int n = 0;
+    uint32_t out = 0;
+    while (v >= (1u << k)) {
+        out = (out << 1) | 1u;
+        n++;
+        v -= 1u << k;
+        k++;
+    }
+    out = (out << 1);
+    n++;
+    out = (out << k) | v;
+    n += k;
+    *bits = out;
+    return n;
+}
+SK_HD int mvd_bits_est(int d) {   // abs_mvd coding cost estimate in bins (AMVP predictor choice)
+    const int a = sk_abs(d);
+    if (a == 0) return 1;
+    if (a == 1) return 3;
+    uint32_t b;
+    return 3 + egk_bins((uint32_t)(a - 2), 1, &b);
+}
+
+// ---------------------------------------------------------------------------
+// Syntax binarisation. residual_coding (7.3.8.11) of one TU from raster levels.
+// last_sig_coeff prefix (group index) of a position and the first position of a group.
+SK_HD int last_group_min(int g) { return (int)((0x310620c418820ull >> (5 * g)) & 31); }
+SK_HD int last_prefix(int p) {
+    if (p < 4) return p;
+    int g = 4;
+    while (g < 9 && p >= last_group_min(g + 1)) g++;
+    return g;
+}
+
+template <class W>
+SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx) {
+    const int n = 1 << log2n;
+    const int sbw = n >> 2;                     // sub-blocks per row
+    const int nsb = sbw * sbw;
+    // last significant coefficient in (sub-block, position) scan order
+    int last_i = -1, last_n = -1;
+    for (int i = nsb - 1; i >= 0 && last_i < 0; i--) {
+        const int sr = sb_raster(log2n, i), xs = log2n == 2 ? 0 : sr % sbw, ys = log2n == 2 ? 0 : sr / sbw;
+        for (int k = 15; k >= 0; k--) {
+            const int r = diag4_raster(k);
+            if (c[(ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3)]) { last_i = i; last_n = k; break; }
+        }
+    }
+    if (last_i < 0) return;   // callers only code TUs with cbf = 1
+    const int lsr = sb_raster(log2n, last_i);
+    const int lx = (log2n == 2 ? 0 : lsr % sbw) * 4 + (diag4_raster(last_n) & 3);
+    const int ly = (log2n == 2 ? 0 : lsr / sbw) * 4 + (diag4_raster(last_n) >> 2);
+    // last_sig_coeff_x/y_prefix (TR, cMax 2*log2n - 1), then suffixes (FL, bypass)
+    const int off = cidx == 0 ? 3 * (log2n - 2) + ((log2n - 1) >> 2) : 15;
+    const int shift = cidx == 0 ? (log2n + 1) >> 2 : log2n - 2;
+    const int cmax = 2 * log2n - 1;
+    const int px = last_prefix(lx), py = last_prefix(ly);
+    for (int b = 0; b < px; b++) w.ctx(CTX_LAST_X + off + (b >> shift), 1);
+    if (px < cmax) w.ctx(CTX_LAST_X + off + (px >> shift), 0);
+    for (int b = 0; b < py; b++) w.ctx(CTX_LAST_Y + off + (b >> shift), 1);
+    if (py < cmax) w.ctx(CTX_LAST_Y + off + (py >> shift), 0);
+    if (px > 3) w.bypass((uint32_t)(lx - last_group_min(px)), (px >> 1) - 1);
+    if (py > 3) w.bypass((uint32_t)(ly - last_group_min(py)), (py >> 1) - 1);
+    // coded_sub_block_flag per sub-block (raster in the sub-block grid)
+    uint32_t csbf = 0;
+    for (int i = 0; i < nsb; i++) {
+        const int sr = sb_raster(log2n, i), xs = sr % sbw, ys = sr / sbw;
+        bool nz = false;
+        for (int k = 0; k < 16 && !nz; k++) nz = c[(ys * 4 + (k >> 2)) * n + xs * 4 + (k & 3)] != 0;
+        if (nz) csbf |= 1u << sr;
+    }
+    int c1_carry = 1;   // greater1 context state carried between sub-blocks (HM c1)
+    bool first_g1_sb = true;
+    for (int i = last_i; i >= 0; i--) {
+        const int sr = sb_raster(log2n, i), xs = sr % sbw, ys = sr / sbw;
+        const int right = (xs + 1 < sbw) ? (int)((csbf >> (sr + 1)) & 1) : 0;
+        const int below = (ys + 1 < sbw) ? (int)((csbf >> (sr + sbw)) & 1) : 0;
+        bool coded = (csbf >> sr) & 1;
+        bool infer_dc = false;
+        if (i < last_i && i > 0) {
+            w.ctx(CTX_CSBF + sk_min(1, right + below) + (cidx ? 2 : 0), coded ? 1 : 0);
+            infer_dc = true;
+        } else {
+            coded = true;   // inferred for the DC and last sub-blocks
+        }
+        const int prev_csbf = right | (below << 1);
+        int lev[16];
+        for (int k = 0; k < 16; k++) {
+            const int r = diag4_raster(k);
+            lev[k] = c[(ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3)];
+        }
+        // sig_coeff_flag
+        uint32_t sig = 0;
+        const int start = (i == last_i) ? last_n - 1 : 15;
+        if (i == last_i) sig |= 1u << last_n;
+        for (int k = start; k >= 0; k--) {
+            if (!coded) break;
+            const int r = diag4_raster(k);
+            const int xc = xs * 4 + (r & 3), yc = ys * 4 + (r >> 2);
+            const bool s = lev[k] != 0;
+            if (k == 0 && infer_dc) {   // inferred 1 when no other flag of the sub-block was 1
+                sig |= 1u;
+                break;
+            }
+            int sctx;
+            if (log2n == 2) {   // ctxIdxMap (4x4 TUs)
+                sctx = (int)((0x877886654325410ull >> (4 * ((yc << 2) + xc))) & 15);
+            } else if (xc + yc == 0) {
+                sctx = 0;
+            } else {
+                const int xp = xc & 3, yp = yc & 3;
+                if (prev_csbf == 0) sctx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+                else if (prev_csbf == 1) sctx = yp == 0 ? 2 : (yp == 1 ? 1 : 0);
+                else if (prev_csbf == 2) sctx = xp == 0 ? 2 : (xp == 1 ? 1 : 0);
+                else sctx = 2;
+                if (cidx == 0) {
+                    if (xs > 0 || ys > 0) sctx += 3;
+                    sctx += log2n == 3 ? 9 : 21;
+                } else {
+                    sctx += log2n == 3 ? 9 : 12;
+                }
+            }
+            w.ctx(CTX_SIG + (cidx == 0 ? sctx : 27 + sctx), s ? 1 : 0);
+            if (s) {
+                sig |= 1u << k;
+                infer_dc = false;
+            }
+        }
+        if (!sig) continue;
+        // greater1 / greater2
+        int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
+        if (!first_g1_sb && c1_carry == 0) ctx_set++;
+        first_g1_sb = false;
+        int g1ctx = 1, ng1 = 0, last_g1_pos = -1;
+        uint32_t g1 = 0;
+        for (int k = 15; k >= 0; k--) {
+            if (!((sig >> k) & 1)) continue;
+            if (ng1 < 8) {
+                const int f = sk_abs(lev[k]) > 1;
+                w.ctx(CTX_GT1 + ctx_set * 4 + sk_min(3, g1ctx) + (cidx ? 16 : 0), f);
+                ng1++;
+                if (f) {
+                    g1 |= 1u << k;
+                    if (last_g1_pos < 0) last_g1_pos = k;
+                }
+                if (g1ctx > 0) g1ctx = f ? 0 : g1ctx + 1;
+            }
+        }
+        c1_carry = g1ctx;
+        int g2 = 0;
+        if (last_g1_pos >= 0) {
+            g2 = sk_abs(lev[last_g1_pos]) > 2;
+            w.ctx(CTX_GT2 + ctx_set + (cidx ? 4 : 0), g2);
+        }
+        // signs
+        {
+            uint32_t bits = 0;
+            int nb = 0;
+            for (int k = 15; k >= 0; k--)
+                if ((sig >> k) & 1) {
+                    bits = (bits << 1) | (lev[k] < 0 ? 1u : 0u);
+                    nb++;
+                }
+            // nb <= 16: two bypass runs at most
+            w.bypass(bits, nb);
+        }
+        // coeff_abs_level_remaining
+        int rice = 0, nsig = 0;
+        for (int k = 15; k >= 0; k--) {
+            if (!((sig >> k) & 1)) continue;
+            const int a = sk_abs(lev[k]);
+            const int base = 1 + (int)((g1 >> k) & 1) + (k == last_g1_pos ? g2 : 0);
+            const int thr = nsig < 8 ? (k == last_g1_pos ? 3 : 2) : 1;
+            if (base == thr) {
+                const uint32_t rem = (uint32_t)(a - base);
+                if (rem < (3u << rice)) {
+                    const int len = (int)(rem >> rice);
+                    w.bypass((1u << (len + 1)) - 2u, len + 1);
+                    if (rice) w.bypass(rem & ((1u << rice) - 1u), rice);
+                } else {
+                    uint32_t v = rem - (3u << rice);
+                    int len = rice;
+                    while (v >= (1u << len)) {
+                        v -= 1u << len;
+                        len++;
+                    }
+                    const int ones = 3 + len + 1 - rice;   // prefix: (ones - 1) ones then a zero
+                    // prefix may exceed 32 bins only for levels far beyond kMaxLevel
+                    int pre = ones;
+                    while (pre > 0) {
+                        const int k2 = pre > 16 ? 16 : pre;
+                        pre -= k2;
+                        const uint32_t chunk = pre == 0 ? ((1u << k2) - 2u) : ((1u << k2) - 1u);
+                        w.bypass(chunk, k2);
+                    }
+                    w.bypass(v, len);
+                }
+                if (a > 3 * (1 << rice)) rice = sk_min(rice + 1, 4);
+            }
+            nsig++;
+        }
+    }
+}
+
+// Whole coding unit (7.3.8.5) for CTB = CU = 16x16. `skip_ctx` = condL + condA of
+// cu_skip_flag; `cand_a` = left intra mode for the MPM list (DC when unavailable).
+template <class W>
+SK_HD void code_cu(W& w, const CuInfo& cu, const int16_t* coef, bool p_slice, int skip_ctx, int cand_a) {
+    if (p_slice) w.ctx(CTX_SKIP + skip_ctx, cu.mode == CU_SKIP);
+    if (cu.mode == CU_SKIP) {
+        // merge_idx: TR cMax 4, first bin context coded
+        w.ctx(CTX_MERGE_IDX, cu.merge_idx > 0);
+        if (cu.merge_idx > 0) {
+            const int rest = cu.merge_idx - 1;   // bins 1..3 bypass, TR with cMax 3
+            if (rest < 3) w.bypass((1u << (rest + 1)) - 2u, rest + 1);
+            else w.bypass(7u, 3);
+        }
+        return;
+    }
+    if (p_slice) w.ctx(CTX_PRED_MODE, cu.mode == CU_INTRA ? 1 : 0);
+    w.ctx(CTX_PART_MODE, 1);   // PART_2Nx2N
+    const int cbf_y = cu.cbf & 1, cbf_cb = (cu.cbf >> 1) & 1, cbf_cr = (cu.cbf >> 2) & 1;
+    if (cu.mode == CU_INTRA) {
+        int mpm[3];
+        intra_mpm(cand_a, mpm);
+        const int m = cu.intra_mode;
+        const int hit = m == mpm[0] ? 0 : (m == mpm[1] ? 1 : (m == mpm[2] ? 2 : -1));
+        w.ctx(CTX_PREV_INTRA, hit >= 0);
+        if (hit >= 0) {
+            if (hit == 0) w.bypass(0, 1);
+            else w.bypass(hit == 1 ? 2u : 3u, 2);
+        } else {
+            int s[3] = {mpm[0], mpm[1], mpm[2]};
+            if (s[0] > s[1]) { int t = s[0]; s[0] = s[1]; s[1] = t; }
+            if (s[0] > s[2]) { int t = s[0]; s[0] = s[2]; s[2] = t; }
+            if (s[1] > s[2]) { int t = s[1]; s[1] = s[2]; s[2] = t; }
+            int rem = m;
+            for (int i = 2; i >= 0; i--)
+                if (rem > s[i]) rem--;
+            w.bypass((uint32_t)rem, 5);
+        }
+        w.ctx(CTX_CHROMA_PRED, 0);   // intra_chroma_pred_mode = 4 (DM)
+    } else {
+        w.ctx(CTX_MERGE_FLAG, cu.mode == CU_MERGE);
+        if (cu.mode == CU_MERGE) {
+            w.ctx(CTX_MERGE_IDX, cu.merge_idx > 0);
+            if (cu.merge_idx > 0) {
+                const int rest = cu.merge_idx - 1;
+                if (rest < 3) w.bypass((1u << (rest + 1)) - 2u, rest + 1);
+                else w.bypass(7u, 3);
+            }
+        } else {
+            const int ax = sk_abs(cu.mvdx), ay = sk_abs(cu.mvdy);
+            w.ctx(CTX_MVD_G0, ax > 0);
+            w.ctx(CTX_MVD_G0, ay > 0);
+            if (ax > 0) w.ctx(CTX_MVD_G1, ax > 1);
+            if (ay > 0) w.ctx(CTX_MVD_G1, ay > 1);
+            if (ax > 0) {
+                if (ax > 1) {
+                    uint32_t b;
+                    const int nb = egk_bins((uint32_t)(ax - 2), 1, &b);
+                    w.bypass(b, nb);
+                }
+                w.bypass(cu.mvdx < 0 ? 1u : 0u, 1);
+            }
+            if (ay > 0) {
+                if (ay > 1) {
+                    uint32_t b;
+                    const int nb = egk_bins((uint32_t)(ay - 2), 1, &b);
+                    w.bypass(b, nb);
+                }
+                w.bypass(cu.mvdy < 0 ? 1u : 0u, 1);
+            }
+            w.ctx(CTX_MVP, cu.mvp_idx);
+        }
+        if (cu.mode != CU_MERGE) {
+            w.ctx(CTX_RQT_ROOT_CBF, cu.cbf != 0);
+            if (cu.cbf == 0) return;
+        }
+    }
+    // transform_tree at depth 0 (no split): cbf_cb, cbf_cr, cbf_luma
+    w.ctx(CTX_CBF_CHROMA + 0, cbf_cb);
+    w.ctx(CTX_CBF_CHROMA + 0, cbf_cr);
+    if (cu.mode == CU_INTRA || cbf_cb || cbf_cr) w.ctx(CTX_CBF_LUMA + 1, cbf_y);
+    if (cbf_y) code_residual(w, coef, 4, 0);
+    if (cbf_cb) code_residual(w, coef + kCoefCb, 3, 1);
+    if (cbf_cr) code_residual(w, coef + kCoefCr, 3, 2);
+}
+
+}  // namespace hevc
+}  // namespace sk

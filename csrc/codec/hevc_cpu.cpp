@@ -1,0 +1,349 @@
+// CPU reference backend of the HEVC encoder: the golden model for the HIP back end
+// (kernels/hevc_kernels.hip produces the same CU decisions, levels, reconstruction,
+// bins and bytes) and the `use_cpu` path.
+#include "hevc_encoder.h"
+#include <string.h>
+#include <algorithm>
+
+namespace sk {
+namespace hevc {
+
+using h264::ACT_I;
+using h264::ACT_P;
+using h264::ACT_SKIPALL;
+using h264::SliceTask;
+
+void build_intra_ref(const uint8_t* plane, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
+                     uint8_t* ref) {
+    uint8_t av[4 * 32 + 1];
+    const int len = 4 * n + 1;
+    memset(av, 0, (size_t)len);
+    memset(ref, 0, (size_t)len);
+    // left column p[-1][y], y = 0..n-1 at ref[2n-1-y]; below-left (y >= n) never available
+    if (left)
+        for (int y = 0; y < n; y++) {
+            ref[2 * n - 1 - y] = plane[(size_t)(y0 + y) * stride + x0 - 1];
+            av[2 * n - 1 - y] = 1;
+        }
+    if (left && top) {
+        ref[2 * n] = plane[(size_t)(y0 - 1) * stride + x0 - 1];
+        av[2 * n] = 1;
+    }
+    if (top)
+        for (int x = 0; x < n; x++) {
+            ref[2 * n + 1 + x] = plane[(size_t)(y0 - 1) * stride + x0 + x];
+            av[2 * n + 1 + x] = 1;
+        }
+    if (tr)
+        for (int x = n; x < 2 * n; x++) {
+            ref[2 * n + 1 + x] = plane[(size_t)(y0 - 1) * stride + x0 + x];
+            av[2 * n + 1 + x] = 1;
+        }
+    intra_substitute(ref, av, n);
+}
+
+void intra_predict(const uint8_t* ref_raw, int log2n, int mode, int cidx, uint8_t* pred) {
+    const int n = 1 << log2n;
+    uint8_t filt[4 * 32 + 1];
+    const uint8_t* ref = ref_raw;
+    if (intra_filter_flag(mode, log2n, cidx)) {
+        intra_filter(ref_raw, n, filt);
+        ref = filt;
+    }
+    for (int y = 0; y < n; y++)
+        for (int x = 0; x < n; x++) pred[y * n + x] = (uint8_t)intra_pred_sample(ref, n, log2n, mode, cidx, x, y);
+}
+
+CpuHevcEncoder::CpuHevcEncoder(const h264::EncoderConfig& cfg) : fe(front_config(cfg)) {
+    geo.init(fe.g);
+    const int n = geo.ctbs();
+    cus.assign(n, CuInfo());
+    coefs.assign((size_t)n * kCoefPerCu, 0);
+    bins.assign((size_t)n * kCuBinCap, 0);
+    bin_n.assign(n, 0);
+    build_parameter_sets(fe.g.W, fe.g.H, cfg.full_range, cfg.fps, param_sets);
+}
+
+void CpuHevcEncoder::load_cu_src(int cx, int cy, uint8_t* y, uint8_t* u, uint8_t* v) const {
+    const h264::Geometry& g = fe.g;
+    for (int r = 0; r < 16; r++) memcpy(y + r * 16, &fe.src[0][(size_t)(cy * 16 + r) * g.stride_y + cx * 16], 16);
+    for (int r = 0; r < 8; r++) {
+        memcpy(u + r * 8, &fe.src[1][(size_t)(cy * 8 + r) * g.stride_c + cx * 8], 8);
+        memcpy(v + r * 8, &fe.src[2][(size_t)(cy * 8 + r) * g.stride_c + cx * 8], 8);
+    }
+}
+
+// Transform + quantisation of one TU from source and prediction; returns cbf and
+// writes the reconstruction.
+static int code_tu(const uint8_t* src, const uint8_t* pred, int log2n, int qp, bool intra, int16_t* lev,
+                   uint8_t* rec) {
+    const int n = 1 << log2n, nn = n * n;
+    int res[256], c[256], d[256], r[256];
+    for (int i = 0; i < nn; i++) res[i] = (int)src[i] - (int)pred[i];
+    fwd_transform(res, log2n, c);
+    int nz = 0;
+    for (int i = 0; i < nn; i++) {
+        const int l = quant_level(c[i], qp, log2n, intra);
+        lev[i] = (int16_t)l;
+        nz |= l;
+        d[i] = dequant_level(l, qp, log2n);
+    }
+    if (nz) {
+        inv_transform(d, log2n, r);
+        for (int i = 0; i < nn; i++) rec[i] = (uint8_t)sk_clip255(pred[i] + r[i]);
+    } else {
+        memcpy(rec, pred, (size_t)nn);
+    }
+    return nz != 0;
+}
+
+void CpuHevcEncoder::code_slice_inter(int s) {
+    const SliceTask& t = fe.tasks[s];
+    const h264::Geometry& g = fe.g;
+    const int qp = t.qp, qpc = chroma_qp(qp);
+    for (int cy = t.first_row; cy < t.first_row + t.num_rows; cy++)
+        for (int cx = 0; cx < geo.ctb_w; cx++) {
+            const int idx = cy * geo.ctb_w + cx;
+            CuInfo& cu = cus[idx];
+            memset(&cu, 0, sizeof(cu));
+            const int mvx = 4 * fe.me[idx].mvx, mvy = 4 * fe.me[idx].mvy;
+            auto nb = [&](int ox, int oy, bool ok) {
+                NbMv m;
+                m.av = ok;
+                m.mvx = ok ? 4 * fe.me[oy * geo.ctb_w + ox].mvx : 0;
+                m.mvy = ok ? 4 * fe.me[oy * geo.ctb_w + ox].mvy : 0;
+                return m;
+            };
+            const bool top = cy > t.first_row;
+            const NbMv A1 = nb(cx - 1, cy, cx > 0), B1 = nb(cx, cy - 1, top);
+            const NbMv B0 = nb(cx + 1, cy - 1, top && cx + 1 < geo.ctb_w), B2 = nb(cx - 1, cy - 1, top && cx > 0);
+            int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];
+            merge_list(A1, B1, B0, B2, mlx, mly);
+            amvp_list(A1, B1, B0, B2, px, py);
+            uint8_t sy[256], su[64], sv[64], pry[256], pru[64], prv[64];
+            load_cu_src(cx, cy, sy, su, sv);
+            const int dx = mvx >> 2, dy = mvy >> 2;
+            for (int y = 0; y < 16; y++)
+                for (int x = 0; x < 16; x++)
+                    pry[y * 16 + x] = fe.ref[0][(size_t)sk_clip(cy * 16 + y + dy, 0, geo.pic_h - 1) * g.stride_y +
+                                                sk_clip(cx * 16 + x + dx, 0, geo.pic_w - 1)];
+            for (int y = 0; y < 8; y++)
+                for (int x = 0; x < 8; x++) {
+                    pru[y * 8 + x] = (uint8_t)chroma_mc_sample(fe.ref[1].data(), g.stride_c, g.stride_c, g.plane_h_c,
+                                                               cx * 8 + x, cy * 8 + y, mvx, mvy);
+                    prv[y * 8 + x] = (uint8_t)chroma_mc_sample(fe.ref[2].data(), g.stride_c, g.stride_c, g.plane_h_c,
+                                                               cx * 8 + x, cy * 8 + y, mvx, mvy);
+                }
+            int16_t* lev = &coefs[(size_t)idx * kCoefPerCu];
+            uint8_t ry[256], ru[64], rv[64];
+            int cbf = code_tu(sy, pry, 4, qp, false, lev, ry);
+            cbf |= code_tu(su, pru, 3, qpc, false, lev + kCoefCb, ru) << 1;
+            cbf |= code_tu(sv, prv, 3, qpc, false, lev + kCoefCr, rv) << 2;
+            int midx = -1;
+            for (int i = 0; i < kMaxMergeCand && midx < 0; i++)
+                if (mlx[i] == mvx && mly[i] == mvy) midx = i;
+            cu.cbf = (uint8_t)cbf;
+            cu.qp = (uint8_t)qp;
+            cu.mvx = (int16_t)mvx;
+            cu.mvy = (int16_t)mvy;
+            if (midx >= 0) {
+                cu.mode = cbf ? CU_MERGE : CU_SKIP;
+                cu.merge_idx = (uint8_t)midx;
+            } else {
+                cu.mode = CU_AMVP;
+                const int c0 = mvd_bits_est(mvx - px[0]) + mvd_bits_est(mvy - py[0]);
+                const int c1 = mvd_bits_est(mvx - px[1]) + mvd_bits_est(mvy - py[1]);
+                const int k = c1 < c0 ? 1 : 0;
+                cu.mvp_idx = (uint8_t)k;
+                cu.mvdx = (int16_t)(mvx - px[k]);
+                cu.mvdy = (int16_t)(mvy - py[k]);
+            }
+            for (int y = 0; y < 16; y++)
+                memcpy(&fe.rec[0][(size_t)(cy * 16 + y) * g.stride_y + cx * 16], ry + y * 16, 16);
+            for (int y = 0; y < 8; y++) {
+                memcpy(&fe.rec[1][(size_t)(cy * 8 + y) * g.stride_c + cx * 8], ru + y * 8, 8);
+                memcpy(&fe.rec[2][(size_t)(cy * 8 + y) * g.stride_c + cx * 8], rv + y * 8, 8);
+            }
+        }
+}
+
+// Candidate intra modes (evaluation order; first minimum SAD wins): DC, planar,
+// vertical, horizontal.
+static const int kIntraCand[4] = {1, 0, 26, 10};
+
+// I slices in two passes, like the H.264 intra path: (1) every CU independently
+// chooses its mode against the SOURCE neighbours (parallel on the GPU), (2) the
+// CTB wavefront predicts from the reconstruction with that mode.
+void CpuHevcEncoder::code_slice_intra(int s) {
+    const SliceTask& t = fe.tasks[s];
+    const h264::Geometry& g = fe.g;
+    const int qp = t.qp, qpc = chroma_qp(qp);
+    for (int pass = 0; pass < 2; pass++)
+        for (int cy = t.first_row; cy < t.first_row + t.num_rows; cy++)
+            for (int cx = 0; cx < geo.ctb_w; cx++) {
+                const int idx = cy * geo.ctb_w + cx;
+                CuInfo& cu = cus[idx];
+                const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < geo.ctb_w;
+                const std::vector<uint8_t>* P = pass == 0 ? fe.src : fe.rec;
+                uint8_t sy[256], su[64], sv[64];
+                load_cu_src(cx, cy, sy, su, sv);
+                uint8_t refy[65], refu[33], refv[33];
+                build_intra_ref(P[0].data(), g.stride_y, cx * 16, cy * 16, 16, left, top, tr, refy);
+                if (pass == 0) {
+                    int best = 1, best_sad = 0x7fffffff;
+                    for (int k = 0; k < 4; k++) {
+                        uint8_t pr[256];
+                        intra_predict(refy, 4, kIntraCand[k], 0, pr);
+                        int sad = 0;
+                        for (int i = 0; i < 256; i++) sad += sk_abs((int)sy[i] - (int)pr[i]);
+                        if (sad < best_sad) { best_sad = sad; best = kIntraCand[k]; }
+                    }
+                    memset(&cu, 0, sizeof(cu));
+                    cu.mode = CU_INTRA;
+                    cu.intra_mode = (uint8_t)best;
+                    continue;
+                }
+                build_intra_ref(P[1].data(), g.stride_c, cx * 8, cy * 8, 8, left, top, tr, refu);
+                build_intra_ref(P[2].data(), g.stride_c, cx * 8, cy * 8, 8, left, top, tr, refv);
+                const int mode = cu.intra_mode;
+                uint8_t pry[256], pru[64], prv[64];
+                intra_predict(refy, 4, mode, 0, pry);
+                intra_predict(refu, 3, mode, 1, pru);
+                intra_predict(refv, 3, mode, 2, prv);
+                int16_t* lev = &coefs[(size_t)idx * kCoefPerCu];
+                uint8_t ry[256], ru[64], rv[64];
+                int cbf = code_tu(sy, pry, 4, qp, true, lev, ry);
+                cbf |= code_tu(su, pru, 3, qpc, true, lev + kCoefCb, ru) << 1;
+                cbf |= code_tu(sv, prv, 3, qpc, true, lev + kCoefCr, rv) << 2;
+                cu.cbf = (uint8_t)cbf;
+                cu.qp = (uint8_t)qp;
+                fe.me[idx].mvx = fe.me[idx].mvy = 0;
+                fe.me[idx].ref = 0;
+                for (int y = 0; y < 16; y++)
+                    memcpy(&fe.rec[0][(size_t)(cy * 16 + y) * g.stride_y + cx * 16], ry + y * 16, 16);
+                for (int y = 0; y < 8; y++) {
+                    memcpy(&fe.rec[1][(size_t)(cy * 8 + y) * g.stride_c + cx * 8], ru + y * 8, 8);
+                    memcpy(&fe.rec[2][(size_t)(cy * 8 + y) * g.stride_c + cx * 8], rv + y * 8, 8);
+                }
+            }
+}
+
+void CpuHevcEncoder::code_slice_skip(int s) {
+    const SliceTask& t = fe.tasks[s];
+    fe.code_slice_skipall(s);   // motion field zero, reconstruction = reference
+    for (int cy = t.first_row; cy < t.first_row + t.num_rows; cy++)
+        for (int cx = 0; cx < geo.ctb_w; cx++) {
+            CuInfo& cu = cus[cy * geo.ctb_w + cx];
+            memset(&cu, 0, sizeof(cu));
+            cu.mode = CU_SKIP;
+            cu.qp = (uint8_t)t.qp;
+        }
+}
+
+void CpuHevcEncoder::binarize_slice(int s) {
+    const SliceTask& t = fe.tasks[s];
+    const bool p_slice = t.final_action != ACT_I;
+    const int last_row = t.first_row + t.num_rows - 1;
+    for (int cy = t.first_row; cy <= last_row; cy++)
+        for (int cx = 0; cx < geo.ctb_w; cx++) {
+            const int idx = cy * geo.ctb_w + cx;
+            const bool left = cx > 0, top = cy > t.first_row;
+            const int skip_ctx = (left && cus[idx - 1].mode == CU_SKIP) + (top && cus[idx - geo.ctb_w].mode == CU_SKIP);
+            const int cand_a = (left && cus[idx - 1].mode == CU_INTRA) ? cus[idx - 1].intra_mode : 1;
+            BinBuf w{&bins[(size_t)idx * kCuBinCap], 0};
+            code_cu(w, cus[idx], &coefs[(size_t)idx * kCoefPerCu], p_slice, skip_ctx, cand_a);
+            w.term(cy == last_row && cx == geo.ctb_w - 1);   // end_of_slice_segment_flag
+            bin_n[idx] = w.n;
+        }
+}
+
+std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
+    const SliceTask& t = fe.tasks[s];
+    const bool p_slice = t.final_action != ACT_I;
+    const int rows = t.num_rows;
+    std::vector<std::vector<uint8_t>> sub(rows);
+    uint8_t sync[CTX_COUNT];
+    for (int r = 0; r < rows; r++) {
+        const int cy = t.first_row + r;
+        uint8_t ctx[CTX_COUNT];
+        if (r == 0 || geo.ctb_w < 2) ctx_init_all(ctx, p_slice ? 1 : 0, t.qp);
+        else memcpy(ctx, sync, CTX_COUNT);
+        size_t cap = 64;
+        for (int cx = 0; cx < geo.ctb_w; cx++) cap += (size_t)bin_n[cy * geo.ctb_w + cx] * 2 + 8;
+        sub[r].assign(cap, 0);
+        CabacEncoder e;
+        e.start(sub[r].data());
+        for (int cx = 0; cx < geo.ctb_w; cx++) {
+            const int idx = cy * geo.ctb_w + cx;
+            const uint16_t* b = &bins[(size_t)idx * kCuBinCap];
+            for (int i = 0; i < bin_n[idx]; i++) e.code_entry(b[i], ctx);
+            if (cx == 1) memcpy(sync, ctx, CTX_COUNT);   // WPP storage after the second CTB
+        }
+        if (r + 1 < rows) e.terminate(1);   // end_of_subset_one_bit
+        e.finish();
+        sub[r].resize(e.pos);
+    }
+    // entry points count emulation-prevention bytes (7.4.7.1)
+    std::vector<int> esc(rows);
+    for (int r = 0; r < rows; r++) esc[r] = ep_escape(sub[r].data(), (int)sub[r].size(), nullptr);
+    uint8_t hdr[1024];
+    memset(hdr, 0, sizeof(hdr));
+    SliceHeader h;
+    h.first_slice = s == 0;
+    h.idr = idr;
+    h.address = t.first_row * geo.ctb_w;
+    h.address_bits = geo.addr_bits;
+    h.slice_type = p_slice ? 1 : 2;
+    h.poc_lsb = poc & ((1 << kLog2MaxPocLsb) - 1);
+    h.qp_delta = t.qp - 26;
+    h.num_entry = rows - 1;
+    h.entry = esc.data();
+    const int hn = write_slice_header(hdr, h);
+    std::vector<uint8_t> rbsp(hdr, hdr + hn);
+    for (int r = 0; r < rows; r++) rbsp.insert(rbsp.end(), sub[r].begin(), sub[r].end());
+    // append_nal escapes the concatenation; pieces end in non-zero bytes, so this equals
+    // escaping each piece on its own (what the entry points were computed from)
+    std::vector<uint8_t> nal;
+    append_nal(nal, idr ? kNalIdrWRadl : kNalTrailR, rbsp.data(), rbsp.size());
+    return nal;
+}
+
+void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
+                            std::vector<h264::EncodedPacket>& out) {
+    fe.load_frame(bgrx, stride);
+    fe.ctl_.plan(fe.stripe_dirty.data(), fe.tasks.data());
+    const int ns = geo.num_slices;
+    for (int s = 0; s < ns; s++)
+        if (fe.tasks[s].action == ACT_P) {
+            fe.motion_search(s);
+            fe.decide_scenecut(s);
+        }
+    for (int s = 0; s < ns; s++) {
+        switch (fe.tasks[s].final_action) {
+            case ACT_P: code_slice_inter(s); break;
+            case ACT_I: code_slice_intra(s); break;
+            default: code_slice_skip(s); break;
+        }
+        binarize_slice(s);
+    }
+    const bool idr = fe.ctl_.picture_is_idr(fe.tasks.data());
+    if (idr) poc = 0;
+    h264::EncodedPacket pk;
+    pk.y = 0;
+    pk.w = fe.g.W;
+    pk.h = fe.g.H;
+    pk.key = idr;
+    pk.data.resize(10);
+    h264::write_stripe_header(pk.data.data(), idr, frame_id, 0, fe.g.W, fe.g.H);
+    if (idr) pk.data.insert(pk.data.end(), param_sets.begin(), param_sets.end());
+    for (int s = 0; s < ns; s++) {
+        std::vector<uint8_t> nal = write_slice(s, idr);
+        pk.data.insert(pk.data.end(), nal.begin(), nal.end());
+    }
+    out.push_back(std::move(pk));
+    fe.finish_frame();
+    poc++;
+}
+
+}  // namespace hevc
+}  // namespace sk

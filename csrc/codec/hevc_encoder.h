@@ -1,0 +1,92 @@
+// H.265 / HEVC Main encoder (session level): geometry, parameter sets and the CPU
+// reference backend. The front end — BGRx -> YUV 4:2:0 conversion (K1/K2), damage
+// (K3), the per-stripe controller (paint-over, keyframes), integer motion search
+// (K4, MFMA exhaustive candidate on the GPU) and scene-cut decisions — is the one of
+// the H.264 encoder run in full-frame mode: a stripe is an HEVC slice of whole CTB
+// rows (CTB = 16 = one H.264 MB, so the MB grids coincide). The HEVC back end codes
+// CUs, binarises them into CABAC bins, codes one WPP substream per CTB row and
+// assembles slice NAL units with entry points.
+//
+// Reference parity: the reference's HEVC paths are GStreamer elements (nvh265enc
+// legacy/gstwebrtc_app.py:369-425, x265enc :667-683, vah265enc :510-543) with the
+// H.265 RTP payloader (PT 100, :848-866); this encoder is the HIP-native equivalent.
+#pragma once
+#include <vector>
+#include "h264_frame.h"
+#include "hevc_core.h"
+#include "hevc_syntax.h"
+
+namespace sk {
+namespace hevc {
+
+struct Geo {
+    int ctb_w = 0, ctb_h = 0, rows_per_slice = 0, num_slices = 0;
+    int pic_w = 0, pic_h = 0;   // coded picture size (multiples of 16)
+    int addr_bits = 0;          // slice_segment_address length
+    void init(const h264::Geometry& g) {
+        ctb_w = g.mb_w;
+        ctb_h = g.mb_h;
+        rows_per_slice = g.rows_per_slice;
+        num_slices = g.num_slices;
+        pic_w = g.stride_y;
+        pic_h = g.plane_h_y;
+        const int n = ctb_w * ctb_h;
+        addr_bits = 0;
+        while ((1 << addr_bits) < n) addr_bits++;
+    }
+    int ctbs() const { return ctb_w * ctb_h; }
+};
+
+// Front-end configuration: full-frame stripes-as-slices, one reference, no H.264 deblock.
+inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
+    h264::EncoderConfig f = c;
+    f.fullframe = 1;
+    f.deblock = 0;
+    f.num_refs = 1;
+    return f;
+}
+
+int choose_level_idc(int w, int h, float fps);
+// VPS + SPS + PPS NAL units (Annex B) for a w x h picture.
+void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<uint8_t>& out);
+// Start code + 2-byte NAL header + emulation-prevented RBSP.
+void append_nal(std::vector<uint8_t>& out, int type, const uint8_t* rbsp, size_t n);
+
+// ---- shared CU-level helpers (CPU reference; the kernels mirror them) ----------
+// Linear intra reference array (see intra_substitute) of an n x n block at (x0, y0)
+// of `plane`; bottom-left is never available (CTB = CU), top-right when tr_avail.
+void build_intra_ref(const uint8_t* plane, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
+                     uint8_t* ref);
+// Prediction of an n x n block for `mode` (cidx 0 luma / 1,2 chroma) from a raw reference.
+void intra_predict(const uint8_t* ref_raw, int log2n, int mode, int cidx, uint8_t* pred);
+
+class CpuHevcEncoder {
+   public:
+    explicit CpuHevcEncoder(const h264::EncoderConfig& cfg);
+    void request_keyframe() { fe.request_keyframe(); }
+    void set_qp(int qp, int paint_qp) { fe.set_qp(qp, paint_qp); }
+    void encode(const uint8_t* bgrx, int stride, uint16_t frame_id, std::vector<h264::EncodedPacket>& out);
+
+    // ---- stages (public for tests) ----
+    void code_slice_inter(int s);
+    void code_slice_intra(int s);
+    void code_slice_skip(int s);
+    void binarize_slice(int s);
+    // CABAC substreams of slice s (one per CTB row) -> slice NAL (Annex B)
+    std::vector<uint8_t> write_slice(int s, bool idr);
+
+    h264::CpuH264Encoder fe;   // front end (full-frame mode)
+    Geo geo;
+    std::vector<CuInfo> cus;
+    std::vector<int16_t> coefs;        // kCoefPerCu per CU
+    std::vector<uint16_t> bins;        // kCuBinCap per CU
+    std::vector<int> bin_n;
+    std::vector<uint8_t> param_sets;   // VPS + SPS + PPS
+    int poc = 0;                       // POC of the next picture
+
+   private:
+    void load_cu_src(int cx, int cy, uint8_t* y, uint8_t* u, uint8_t* v) const;
+};
+
+}  // namespace hevc
+}  // namespace sk

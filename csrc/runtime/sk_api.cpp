@@ -2,6 +2,7 @@
 // access and debug hooks used by the Python layer and the tests.
 #include "sk_api.h"
 #include "encoder_iface.h"
+#include "../codec/hevc_encoder.h"
 #include <hip/hip_runtime_api.h>
 #include <string.h>
 #include <string>
@@ -95,6 +96,41 @@ class CpuBackend : public EncoderBackend {
     h264::CpuH264Encoder enc_;
 };
 
+class CpuHevcBackend : public EncoderBackend {
+   public:
+    explicit CpuHevcBackend(const h264::EncoderConfig& c) : enc_(c) {}
+    void request_keyframe() override { enc_.request_keyframe(); }
+    void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
+    int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        packets_.clear();
+        enc_.encode(bgrx, stride, frame_id, packets_);
+        return (int)packets_.size();
+    }
+    int64_t debug_buffer(const char* name, void* dst, int64_t cap) override {
+        const void* p = nullptr;
+        int64_t n = 0;
+        std::string s(name);
+        auto plane = [&](const std::vector<uint8_t>& v) { p = v.data(); n = (int64_t)v.size(); };
+        if (s == "src_y") plane(enc_.fe.prev[0]);
+        else if (s == "src_u") plane(enc_.fe.prev[1]);
+        else if (s == "src_v") plane(enc_.fe.prev[2]);
+        else if (s == "ref_y") plane(enc_.fe.ref[0]);
+        else if (s == "ref_u") plane(enc_.fe.ref[1]);
+        else if (s == "ref_v") plane(enc_.fe.ref[2]);
+        else if (s == "cus") { p = enc_.cus.data(); n = (int64_t)(enc_.cus.size() * sizeof(hevc::CuInfo)); }
+        else if (s == "coefs") { p = enc_.coefs.data(); n = (int64_t)(enc_.coefs.size() * 2); }
+        else if (s == "bin_n") { p = enc_.bin_n.data(); n = (int64_t)(enc_.bin_n.size() * 4); }
+        else if (s == "me") { p = enc_.fe.me.data(); n = (int64_t)(enc_.fe.me.size() * sizeof(h264::MeResult)); }
+        else if (s == "tasks") { p = enc_.fe.tasks.data(); n = (int64_t)(enc_.fe.tasks.size() * sizeof(h264::SliceTask)); }
+        else return -1;
+        if (dst && cap >= n) memcpy(dst, p, (size_t)n);
+        return n;
+    }
+
+   private:
+    hevc::CpuHevcEncoder enc_;
+};
+
 class CpuJpegBackend : public EncoderBackend {
    public:
     explicit CpuJpegBackend(const jpeg::JpegConfig& c) : enc_(c) {}
@@ -114,7 +150,10 @@ class CpuJpegBackend : public EncoderBackend {
 
 EncoderBackend* create_cpu_jpeg_backend(const jpeg::JpegConfig& c) { return new CpuJpegBackend(c); }
 
-EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c) { return new CpuBackend(c); }
+EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c) {
+    if (c.codec == 1) return new CpuHevcBackend(c);
+    return new CpuBackend(c);
+}
 
 h264::EncoderConfig to_config(const sk_h264_config* c) {
     h264::EncoderConfig e;
@@ -141,6 +180,12 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.src_width = c->src_width > 0 ? c->src_width : 0;
     e.src_height = c->src_height > 0 ? c->src_height : 0;
     e.num_refs = c->num_refs > 1 ? 2 : 1;
+    e.codec = c->codec == 1 ? 1 : 0;
+    if (e.codec == 1) {   // HEVC: full-frame pictures, slices of whole CTB rows, one reference
+        e.fullframe = 1;
+        e.num_refs = 1;
+        e.deblock = 0;
+    }
     return e;
 }
 

@@ -20,6 +20,7 @@ typedef struct sk_h264_config {
     int32_t shared_copy;  // > 0: H2D on the device's shared copy stream (bands of one frame)
     int32_t src_width, src_height;  // capture size if it differs (K2 resample in K1); 0 = width/height
     int32_t num_refs;               // reference pictures (sliding-window DPB): 0/1 = one, 2 = two
+    int32_t codec;                  // 0 = H.264 (stripes or full frame), 1 = HEVC Main (full frame, WPP)
 } sk_h264_config;
 
 typedef struct sk_packet {

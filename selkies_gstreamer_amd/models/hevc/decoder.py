@@ -1,0 +1,1228 @@
+"""H.265 / HEVC Main decoder used to verify the encoder (test oracle).
+
+There is no ffmpeg/PyAV/libde265 in the build environment, so the
+HIP HEVC encoder is checked against this independent implementation of the decoding
+process of ITU-T H.265: clause 7 (VPS/SPS/PPS/slice segment header syntax), 9.3
+(CABAC parsing: context initialisation, WPP storage/synchronisation, arithmetic
+decoding, binarisations and context selection) and 8 (intra sample prediction with
+reference substitution and filtering, merge / AMVP motion vector prediction, 8-tap
+luma and 4-tap chroma interpolation, scaling, inverse DCT/DST, reconstruction).
+
+Supported: Main 8-bit 4:2:0, any CTB/CB/TB sizes with quadtree splits, PART_2Nx2N
+CUs (intra and inter), I and P slices with one reference list, multiple slices,
+entropy_coding_sync (WPP) substreams. NotImplementedError for the rest (B slices,
+tiles, AMP/NxN partitions, PCM, transform skip, scaling lists, SAO, deblocking,
+TMVP, long-term references, sign data hiding, cu_qp_delta).
+
+Written from the specification text, not from the encoder's tables; numpy for the
+sample processes, plain Python for parsing. Intended for test-sized pictures.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from ..h264.decoder import split_annexb, unescape
+
+
+class BitstreamError(ValueError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+class Bits:
+    def __init__(self, data: bytes, pos: int = 0):
+        self.d = data
+        self.p = pos   # bit position
+
+    def u(self, n: int) -> int:
+        v = 0
+        for _ in range(n):
+            byte = self.d[self.p >> 3] if (self.p >> 3) < len(self.d) else 0
+            v = (v << 1) | ((byte >> (7 - (self.p & 7))) & 1)
+            self.p += 1
+        return v
+
+    def ue(self) -> int:
+        z = 0
+        while self.u(1) == 0:
+            z += 1
+            if z > 32:
+                raise BitstreamError("bad ue(v)")
+        return (1 << z) - 1 + self.u(z)
+
+    def se(self) -> int:
+        k = self.ue()
+        return (k + 1) // 2 if k & 1 else -(k // 2)
+
+
+# ---------------------------------------------------------------------------
+# CABAC tables (9.3.4.3.2): rangeTabLps and transIdxLps.
+RANGE_LPS = [
+    (128, 176, 208, 240), (128, 167, 197, 227), (128, 158, 187, 216), (123, 150, 178, 205),
+    (116, 142, 169, 195), (111, 135, 160, 185), (105, 128, 152, 175), (100, 122, 144, 166),
+    (95, 116, 137, 158), (90, 110, 130, 150), (85, 104, 123, 142), (81, 99, 117, 135),
+    (77, 94, 111, 128), (73, 89, 105, 122), (69, 85, 100, 116), (66, 80, 95, 110),
+    (62, 76, 90, 104), (59, 72, 86, 99), (56, 69, 81, 94), (53, 65, 77, 89),
+    (51, 62, 73, 85), (48, 59, 69, 80), (46, 56, 66, 76), (43, 53, 63, 72),
+    (41, 50, 59, 69), (39, 48, 56, 65), (37, 45, 54, 62), (35, 43, 51, 59),
+    (33, 41, 48, 56), (32, 39, 46, 53), (30, 37, 43, 50), (29, 35, 41, 48),
+    (27, 33, 39, 45), (26, 31, 37, 43), (24, 30, 35, 41), (23, 28, 33, 39),
+    (22, 27, 32, 37), (21, 26, 30, 35), (20, 24, 29, 33), (19, 23, 27, 31),
+    (18, 22, 26, 30), (17, 21, 25, 28), (16, 20, 23, 27), (15, 19, 22, 25),
+    (14, 18, 21, 24), (14, 17, 20, 23), (13, 16, 19, 22), (12, 15, 18, 21),
+    (12, 14, 17, 20), (11, 14, 16, 19), (11, 13, 15, 18), (10, 12, 15, 17),
+    (10, 12, 14, 16), (9, 11, 13, 15), (9, 11, 12, 14), (8, 10, 12, 14),
+    (8, 9, 11, 13), (7, 9, 11, 12), (7, 9, 10, 12), (7, 8, 10, 11),
+    (6, 8, 9, 11), (6, 7, 9, 10), (6, 7, 8, 9), (2, 2, 2, 2)]
+TRANS_LPS = [0, 0, 1, 2, 2, 4, 4, 5, 6, 7, 8, 9, 9, 11, 11, 12, 13, 13, 15, 15, 16, 16, 18, 18, 19, 19, 21, 21,
+             22, 22, 23, 24, 24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30, 31, 32, 32, 33, 33, 33, 34, 34, 35,
+             35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63]
+
+# initValue per syntax element, indexed [initType][ctxIdx-within-element] (Tables 9-5..9-37).
+INIT = {
+    "split_cu_flag": [[139, 141, 157], [107, 139, 126], [107, 139, 126]],
+    "cu_skip_flag": [[154, 154, 154], [197, 185, 201], [197, 185, 201]],
+    "pred_mode_flag": [[154], [149], [134]],
+    "part_mode": [[184, 154, 154, 154], [154, 139, 154, 154], [154, 139, 154, 154]],
+    "prev_intra_luma_pred_flag": [[184], [154], [183]],
+    "intra_chroma_pred_mode": [[63], [152], [152]],
+    "rqt_root_cbf": [[154], [79], [79]],
+    "merge_flag": [[154], [110], [154]],
+    "merge_idx": [[154], [122], [137]],
+    "inter_pred_idc": [[154] * 5, [95, 79, 63, 31, 31], [95, 79, 63, 31, 31]],
+    "ref_idx": [[154, 154], [153, 153], [153, 153]],
+    "mvp_flag": [[154], [168], [168]],
+    "split_transform_flag": [[153, 138, 138], [124, 138, 94], [224, 167, 122]],
+    "cbf_luma": [[111, 141], [153, 111], [153, 111]],
+    "cbf_chroma": [[94, 138, 182, 154], [149, 107, 167, 154], [149, 92, 167, 154]],
+    "abs_mvd_greater0_flag": [[154], [140], [169]],
+    "abs_mvd_greater1_flag": [[154], [198], [198]],
+    "cu_qp_delta_abs": [[154, 154], [154, 154], [154, 154]],
+    "transform_skip_flag": [[139, 139], [139, 139], [139, 139]],
+    "last_x_prefix": [
+        [110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63],
+        [125, 110, 94, 110, 95, 79, 125, 111, 110, 78, 110, 111, 111, 95, 94, 108, 123, 108],
+        [125, 110, 124, 110, 95, 94, 125, 111, 111, 79, 125, 126, 111, 111, 79, 108, 123, 93]],
+    "coded_sub_block_flag": [[91, 171, 134, 141], [121, 140, 61, 154], [121, 140, 61, 154]],
+    "sig_coeff_flag": [
+        [111, 111, 125, 110, 110, 94, 124, 108, 124, 107, 125, 141, 179, 153, 125, 107, 125, 141, 179, 153,
+         125, 107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153, 136, 139, 111, 136,
+         139, 111],
+        [155, 154, 139, 153, 139, 123, 123, 63, 153, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153,
+         154, 166, 183, 140, 136, 153, 154, 170, 153, 138, 138, 122, 121, 122, 121, 167, 151, 183, 140, 151,
+         183, 140],
+        [170, 154, 139, 153, 139, 123, 123, 63, 124, 166, 183, 140, 136, 153, 154, 166, 183, 140, 136, 153,
+         154, 166, 183, 140, 136, 153, 154, 170, 153, 123, 123, 107, 121, 107, 121, 167, 151, 183, 140, 151,
+         183, 140]],
+    "coeff_abs_level_greater1_flag": [
+        [140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166, 182, 140,
+         227, 122, 197],
+        [154, 196, 196, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 137, 169, 194, 166, 167,
+         154, 167, 137, 182],
+        [154, 196, 167, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 122, 169, 208, 166, 167,
+         154, 152, 167, 182]],
+    "coeff_abs_level_greater2_flag": [[138, 153, 136, 167, 152, 152], [107, 167, 91, 122, 107, 167],
+                                      [107, 167, 91, 107, 107, 167]],
+}
+INIT["last_y_prefix"] = INIT["last_x_prefix"]
+
+
+def init_contexts(init_type: int, qp: int) -> dict:
+    ctx = {}
+    q = min(max(qp, 0), 51)
+    for name, tabs in INIT.items():
+        states = []
+        for iv in tabs[init_type]:
+            m = (iv >> 4) * 5 - 45
+            n = ((iv & 15) << 3) - 16
+            pre = min(max(((m * q) >> 4) + n, 1), 126)
+            mps = 1 if pre > 63 else 0
+            states.append([pre - 64 if mps else 63 - pre, mps])
+        ctx[name] = states
+    return ctx
+
+
+def copy_contexts(ctx: dict) -> dict:
+    return {k: [list(s) for s in v] for k, v in ctx.items()}
+
+
+class Cabac:
+    """Arithmetic decoding engine (9.3.4.3) over one substream (RBSP bytes)."""
+
+    def __init__(self, data: bytes):
+        self.b = Bits(data)
+        self.range = 510
+        self.offset = self.b.u(9)
+
+    def decision(self, st: list) -> int:
+        p, mps = st
+        lps = RANGE_LPS[p][(self.range >> 6) & 3]
+        self.range -= lps
+        if self.offset >= self.range:
+            binv = 1 - mps
+            self.offset -= self.range
+            self.range = lps
+            if p == 0:
+                st[1] = 1 - mps
+            st[0] = TRANS_LPS[p]
+        else:
+            binv = mps
+            st[0] = min(p + 1, 62)
+        while self.range < 256:
+            self.range <<= 1
+            self.offset = (self.offset << 1) | self.b.u(1)
+        return binv
+
+    def bypass(self) -> int:
+        self.offset = (self.offset << 1) | self.b.u(1)
+        if self.offset >= self.range:
+            self.offset -= self.range
+            return 1
+        return 0
+
+    def bypass_bits(self, n: int) -> int:
+        v = 0
+        for _ in range(n):
+            v = (v << 1) | self.bypass()
+        return v
+
+    def terminate(self) -> int:
+        self.range -= 2
+        if self.offset >= self.range:
+            return 1
+        while self.range < 256:
+            self.range <<= 1
+            self.offset = (self.offset << 1) | self.b.u(1)
+        return 0
+
+
+# ---------------------------------------------------------------------------
+# Transforms (8.6.4.2) and intra tables.
+_C64 = [64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64, 61, 57, 54, 50, 46, 43, 38, 36,
+        31, 25, 22, 18, 13, 9, 4, 0]
+
+
+def _cosv(m: int) -> int:
+    m %= 128
+    if m <= 32:
+        return _C64[m]
+    if m < 64:
+        return -_C64[64 - m]
+    if m <= 96:
+        return -_C64[m - 64]
+    return _C64[128 - m]
+
+
+def dct_matrix(n: int) -> np.ndarray:
+    s = 32 // n
+    t = np.zeros((n, n), dtype=np.int64)
+    t[0, :] = 64
+    for k in range(1, n):
+        for j in range(n):
+            t[k, j] = _cosv((2 * j + 1) * k * s)
+    return t
+
+
+_DCT = {n: dct_matrix(n) for n in (4, 8, 16, 32)}
+_DST = np.array([[29, 55, 74, 84], [74, 74, 0, -74], [84, -29, -74, 55], [55, -84, 74, -29]], dtype=np.int64)
+
+INTRA_ANGLE = [0, 0, 32, 26, 21, 17, 13, 9, 5, 2, 0, -2, -5, -9, -13, -17, -21, -26, -32, -26, -21, -17, -13,
+               -9, -5, -2, 0, 2, 5, 9, 13, 17, 21, 26, 32]
+INV_ANGLE = {11: -4096, 12: -1638, 13: -910, 14: -630, 15: -482, 16: -390, 17: -315, 18: -256, 19: -315,
+             20: -390, 21: -482, 22: -630, 23: -910, 24: -1638, 25: -4096}
+LUMA_FILTER = [[0, 0, 0, 64, 0, 0, 0, 0], [-1, 4, -10, 58, 17, -5, 1, 0], [-1, 4, -11, 40, 40, -11, 4, -1],
+               [0, 1, -5, 17, 58, -10, 4, -1]]
+CHROMA_FILTER = [[0, 64, 0, 0], [-2, 58, 10, -2], [-4, 54, 16, -2], [-6, 46, 28, -4], [-4, 36, 36, -4],
+                 [-4, 28, 46, -6], [-2, 16, 54, -4], [-2, 10, 58, -2]]
+LEVEL_SCALE = [40, 45, 51, 57, 64, 72]
+QPC_TABLE = {30: 29, 31: 30, 32: 31, 33: 32, 34: 33, 35: 33, 36: 34, 37: 34, 38: 35, 39: 35, 40: 36, 41: 36,
+             42: 37, 43: 37}
+
+
+def inverse_transform(d: np.ndarray, n: int, dst: bool) -> np.ndarray:
+    """d[y][x] scaled coefficients -> residual (8-bit video)."""
+    m = _DST if dst else _DCT[n]
+    e = m.T @ d.astype(np.int64)                    # columns: e[y][x] = sum_j m[j][y] d[j][x]
+    g = np.clip((e + 64) >> 7, -32768, 32767)
+    r = g @ m                                       # rows: r[y][x] = sum_j g[y][j] m[j][x]
+    return (r + 2048) >> 12
+
+
+def scan_diag(n: int) -> list:
+    out = []
+    x = y = 0
+    while len(out) < n * n:
+        while y >= 0:
+            if x < n and y < n:
+                out.append((x, y))
+            y -= 1
+            x += 1
+        y = x
+        x = 0
+    return out
+
+
+def scan_order(n: int, scan_idx: int) -> list:
+    if scan_idx == 0:
+        return scan_diag(n)
+    if scan_idx == 1:   # horizontal
+        return [(x, y) for y in range(n) for x in range(n)]
+    return [(x, y) for x in range(n) for y in range(n)]   # vertical
+
+
+# ---------------------------------------------------------------------------
+@dataclass
+class Sps:
+    width: int = 0
+    height: int = 0
+    crop: tuple = (0, 0, 0, 0)
+    log2_min_cb: int = 3
+    log2_ctb: int = 4
+    log2_min_tb: int = 2
+    log2_max_tb: int = 5
+    max_th_inter: int = 0
+    max_th_intra: int = 0
+    log2_poc_lsb: int = 8
+    num_st_rps: int = 0
+    st_rps: list = None
+    amp: bool = False
+    sao: bool = False
+    pcm: bool = False
+    tmvp: bool = False
+    strong_smoothing: bool = False
+    scaling_list: bool = False
+    long_term: bool = False
+
+
+@dataclass
+class Pps:
+    dependent_slices: bool = False
+    output_flag_present: bool = False
+    extra_bits: int = 0
+    sign_hiding: bool = False
+    cabac_init_present: bool = False
+    num_ref_l0: int = 1
+    init_qp: int = 26
+    constrained_intra: bool = False
+    transform_skip: bool = False
+    cu_qp_delta: bool = False
+    cb_qp_offset: int = 0
+    cr_qp_offset: int = 0
+    slice_chroma_qp_offsets: bool = False
+    tiles: bool = False
+    wpp: bool = False
+    loop_filter_across_slices: bool = False
+    deblock_override: bool = False
+    deblock_disabled: bool = False
+    lists_modification: bool = False
+    log2_par_mrg: int = 2
+    slice_header_ext: bool = False
+
+
+class HevcDecoder:
+    def __init__(self):
+        self.sps: Sps | None = None
+        self.pps: Pps | None = None
+        self.ref = None          # previous decoded picture (Y, U, V) for P slices
+        self.poc = 0
+        self.frames = []
+        self.cur = None
+
+    # ---------------- parameter sets ----------------
+    @staticmethod
+    def _ptl(b: Bits, max_sub_layers_minus1: int):
+        b.u(2); b.u(1); b.u(5); b.u(32); b.u(4); b.u(32); b.u(12)
+        b.u(8)   # general_level_idc
+        if max_sub_layers_minus1 > 0:
+            raise NotImplementedError("sub-layers")
+
+    def _parse_sps(self, r: bytes):
+        b = Bits(r)
+        b.u(4)
+        msl = b.u(3)
+        b.u(1)
+        self._ptl(b, msl)
+        b.ue()
+        if b.ue() != 1:
+            raise NotImplementedError("only 4:2:0")
+        s = Sps()
+        s.width, s.height = b.ue(), b.ue()
+        if b.u(1):
+            s.crop = (b.ue(), b.ue(), b.ue(), b.ue())
+        if b.ue() != 0 or b.ue() != 0:
+            raise NotImplementedError("only 8-bit")
+        s.log2_poc_lsb = b.ue() + 4
+        sub = b.u(1)
+        for _ in range(0 if sub else msl, msl + 1):
+            b.ue(); b.ue(); b.ue()
+        s.log2_min_cb = b.ue() + 3
+        s.log2_ctb = s.log2_min_cb + b.ue()
+        s.log2_min_tb = b.ue() + 2
+        s.log2_max_tb = s.log2_min_tb + b.ue()
+        s.max_th_inter = b.ue()
+        s.max_th_intra = b.ue()
+        s.scaling_list = bool(b.u(1))
+        if s.scaling_list:
+            raise NotImplementedError("scaling lists")
+        s.amp = bool(b.u(1))
+        s.sao = bool(b.u(1))
+        s.pcm = bool(b.u(1))
+        if s.pcm:
+            raise NotImplementedError("PCM")
+        s.num_st_rps = b.ue()
+        s.st_rps = []
+        for i in range(s.num_st_rps):
+            s.st_rps.append(self._st_rps(b, i, s.st_rps))
+        s.long_term = bool(b.u(1))
+        if s.long_term:
+            raise NotImplementedError("long-term refs")
+        s.tmvp = bool(b.u(1))
+        s.strong_smoothing = bool(b.u(1))
+        self.sps = s
+
+    @staticmethod
+    def _st_rps(b: Bits, idx: int, prev: list) -> list:
+        if idx != 0 and b.u(1):
+            raise NotImplementedError("inter RPS prediction")
+        nneg, npos = b.ue(), b.ue()
+        deltas = []
+        poc = 0
+        for _ in range(nneg):
+            poc -= b.ue() + 1
+            deltas.append((poc, b.u(1)))
+        poc = 0
+        for _ in range(npos):
+            poc += b.ue() + 1
+            deltas.append((poc, b.u(1)))
+        return deltas
+
+    def _parse_pps(self, r: bytes):
+        b = Bits(r)
+        b.ue(); b.ue()
+        p = Pps()
+        p.dependent_slices = bool(b.u(1))
+        p.output_flag_present = bool(b.u(1))
+        p.extra_bits = b.u(3)
+        p.sign_hiding = bool(b.u(1))
+        p.cabac_init_present = bool(b.u(1))
+        p.num_ref_l0 = b.ue() + 1
+        b.ue()
+        p.init_qp = 26 + b.se()
+        p.constrained_intra = bool(b.u(1))
+        p.transform_skip = bool(b.u(1))
+        p.cu_qp_delta = bool(b.u(1))
+        if p.cu_qp_delta:
+            raise NotImplementedError("cu_qp_delta")
+        p.cb_qp_offset, p.cr_qp_offset = b.se(), b.se()
+        p.slice_chroma_qp_offsets = bool(b.u(1))
+        if b.u(1) or b.u(1):
+            raise NotImplementedError("weighted prediction")
+        if b.u(1):
+            raise NotImplementedError("transquant bypass")
+        p.tiles = bool(b.u(1))
+        if p.tiles:
+            raise NotImplementedError("tiles")
+        p.wpp = bool(b.u(1))
+        p.loop_filter_across_slices = bool(b.u(1))
+        if b.u(1):
+            p.deblock_override = bool(b.u(1))
+            p.deblock_disabled = bool(b.u(1))
+            if not p.deblock_disabled:
+                b.se(); b.se()
+        if b.u(1):
+            raise NotImplementedError("PPS scaling lists")
+        p.lists_modification = bool(b.u(1))
+        p.log2_par_mrg = b.ue() + 2
+        p.slice_header_ext = bool(b.u(1))
+        if p.sign_hiding or p.transform_skip:
+            raise NotImplementedError("sign hiding / transform skip")
+        self.pps = p
+
+    # ---------------- pictures ----------------
+    def decode(self, annexb: bytes) -> list:
+        """Decodes an Annex-B stream; returns the pictures completed by it as (Y, U, V)
+        arrays cropped to the conformance window."""
+        out = []
+        for nal in split_annexb(annexb):
+            if len(nal) < 2:
+                continue
+            t = (nal[0] >> 1) & 63
+            if t == 32:
+                continue
+            if t == 33:
+                self._parse_sps(unescape(nal[2:]))
+            elif t == 34:
+                self._parse_pps(unescape(nal[2:]))
+            elif t in (0, 1, 19, 20, 21):
+                done = self._slice(nal, t)
+                if done is not None:
+                    out.append(done)
+            elif t in (35, 36, 37, 38, 39, 40):
+                continue
+            else:
+                raise NotImplementedError(f"NAL type {t}")
+        if self.cur is not None:
+            out.append(self._finish_picture())
+        return out
+
+    def _finish_picture(self):
+        s = self.sps
+        Y, U, V = self.cur["Y"], self.cur["U"], self.cur["V"]
+        self.ref = (Y.copy(), U.copy(), V.copy())
+        self.cur = None
+        cl, cr, ct, cb = s.crop
+        return (Y[2 * ct:s.height - 2 * cb, 2 * cl:s.width - 2 * cr].copy(),
+                U[ct:s.height // 2 - cb, cl:s.width // 2 - cr].copy(),
+                V[ct:s.height // 2 - cb, cl:s.width // 2 - cr].copy())
+
+    def _new_picture(self):
+        s = self.sps
+        nmin = (s.width // 4) * (s.height // 4)
+        self.cur = {
+            "Y": np.zeros((s.height, s.width), np.uint8),
+            "U": np.zeros((s.height // 2, s.width // 2), np.uint8),
+            "V": np.zeros((s.height // 2, s.width // 2), np.uint8),
+            # per 4x4 block: slice address (-1 = not decoded), pred mode (0 inter, 1 intra), skip,
+            # intra mode, mv, ct depth
+            "slice": np.full((s.height // 4, s.width // 4), -1, np.int64),
+            "intra": np.zeros((s.height // 4, s.width // 4), np.int64),
+            "skip": np.zeros((s.height // 4, s.width // 4), np.int64),
+            "ipm": np.ones((s.height // 4, s.width // 4), np.int64),
+            "mv": np.zeros((s.height // 4, s.width // 4, 2), np.int64),
+            "depth": np.zeros((s.height // 4, s.width // 4), np.int64),
+        }
+        del nmin
+
+    # ---------------- slice ----------------
+    def _slice(self, nal: bytes, nut: int):
+        s, p = self.sps, self.pps
+        if s is None or p is None:
+            raise BitstreamError("slice before parameter sets")
+        payload = nal[2:]
+        r = unescape(payload)
+        b = Bits(r)
+        first = b.u(1)
+        if 16 <= nut <= 23:
+            b.u(1)
+        b.ue()
+        ctb = 1 << s.log2_ctb
+        wc = (s.width + ctb - 1) // ctb
+        hc = (s.height + ctb - 1) // ctb
+        addr = 0
+        if not first:
+            if p.dependent_slices:
+                raise NotImplementedError("dependent slices")
+            nbits = max(1, (wc * hc - 1).bit_length())
+            addr = b.u(nbits)
+        if first:
+            if self.cur is not None:
+                done = self._finish_picture()
+            else:
+                done = None
+            self._new_picture()
+        else:
+            done = None
+            if self.cur is None:
+                raise BitstreamError("slice without a picture")
+        b.u(p.extra_bits)
+        slice_type = b.ue()
+        if slice_type == 0:
+            raise NotImplementedError("B slices")
+        if p.output_flag_present:
+            b.u(1)
+        idr = nut in (19, 20)
+        if not idr:
+            b.u(s.log2_poc_lsb)
+            if not b.u(1):
+                self._st_rps(b, s.num_st_rps, s.st_rps)
+            elif s.num_st_rps > 1:
+                b.u(max(1, (s.num_st_rps - 1).bit_length()))
+            if s.tmvp:
+                if b.u(1):
+                    raise NotImplementedError("TMVP")
+        if s.sao:
+            if b.u(1) or b.u(1):
+                raise NotImplementedError("SAO")
+        num_ref = p.num_ref_l0
+        max_merge = 5
+        if slice_type == 1:
+            if b.u(1):
+                num_ref = b.ue() + 1
+            if p.lists_modification:
+                raise NotImplementedError("list modification")
+            cabac_init = b.u(1) if p.cabac_init_present else 0
+            max_merge = 5 - b.ue()
+        else:
+            cabac_init = 0
+        qp = p.init_qp + b.se()
+        if p.slice_chroma_qp_offsets:
+            b.se(); b.se()
+        deblock_disabled = p.deblock_disabled
+        if p.deblock_override and b.u(1):
+            deblock_disabled = bool(b.u(1))
+            if not deblock_disabled:
+                b.se(); b.se()
+        if not deblock_disabled:
+            raise NotImplementedError("deblocking filter")
+        entry = []
+        if p.tiles or p.wpp:
+            n = b.ue()
+            if n:
+                ln = b.ue() + 1
+                entry = [b.u(ln) + 1 for _ in range(n)]
+        if p.slice_header_ext:
+            b.u(8 * b.ue())
+        # byte_alignment()
+        if b.u(1) != 1:
+            raise BitstreamError("byte_alignment")
+        while b.p & 7:
+            b.u(1)
+        hdr_rbsp = b.p >> 3
+        # map the RBSP header length to the escaped payload (entry points count EP bytes)
+        pos, rb, zeros = 0, 0, 0
+        while rb < hdr_rbsp:
+            byte = payload[pos]
+            if zeros >= 2 and byte == 3:
+                zeros = 0
+                pos += 1
+                continue
+            zeros = zeros + 1 if byte == 0 else 0
+            pos += 1
+            rb += 1
+        starts = [pos]
+        for e in entry:
+            starts.append(starts[-1] + e)
+        subs = [unescape(payload[starts[k]:(starts[k + 1] if k + 1 < len(starts) else len(payload))])
+                for k in range(len(starts))]
+        self._slice_data(addr, slice_type, qp, cabac_init, num_ref, max_merge, subs, wc, hc)
+        return done
+
+    # ---------------- slice data ----------------
+    def _avail(self, xc, yc, xn, yn) -> bool:
+        """z-scan availability (6.4.1) via the decoded map: inside the picture, decoded, same slice."""
+        s = self.sps
+        if xn < 0 or yn < 0 or xn >= s.width or yn >= s.height:
+            return False
+        sa = self.cur["slice"][yn >> 2, xn >> 2]
+        return sa >= 0 and sa == self.slice_addr
+
+    def _slice_data(self, addr, slice_type, qp, cabac_init, num_ref, max_merge, subs, wc, hc):
+        s, p = self.sps, self.pps
+        self.slice_addr = addr
+        self.slice_type = slice_type
+        self.qp = qp
+        self.max_merge = max_merge
+        self.num_ref = num_ref
+        init_type = 0 if slice_type == 2 else (2 if cabac_init else 1)
+        self.init_type = init_type
+        ctb = 1 << s.log2_ctb
+        self.ctx = init_contexts(init_type, qp)
+        sub_i = 0
+        self.cabac = Cabac(subs[0])
+        sync = None
+        a = addr
+        while True:
+            cx, cy = a % wc, a // wc
+            if p.wpp and cx == 0 and a != addr:
+                # new substream: arithmetic decoder restart, contexts from the WPP storage
+                sub_i += 1
+                if sub_i >= len(subs):
+                    raise BitstreamError("missing WPP substream")
+                self.cabac = Cabac(subs[sub_i])
+                tr_x, tr_y = ctb, (cy - 1) * ctb
+                if sync is not None and self._avail(0, cy * ctb, tr_x, tr_y):
+                    self.ctx = copy_contexts(sync)
+                else:
+                    self.ctx = init_contexts(init_type, qp)
+            elif p.wpp and cx == 0 and a == addr:
+                pass
+            self._coding_quadtree(cx * ctb, cy * ctb, s.log2_ctb, 0)
+            if p.wpp and cx == 1:
+                sync = copy_contexts(self.ctx)
+            if p.wpp and wc == 1:
+                sync = None
+            end = self.cabac.terminate()
+            a += 1
+            if end:
+                break
+            if p.wpp and a % wc == 0:
+                if self.cabac.terminate() != 1:
+                    raise BitstreamError("end_of_subset_one_bit")
+            if a >= wc * hc:
+                raise BitstreamError("slice runs past the picture")
+
+    # ---------------- coding tree ----------------
+    def _dec(self, name, idx=0):
+        return self.cabac.decision(self.ctx[name][idx])
+
+    def _coding_quadtree(self, x0, y0, log2, depth):
+        s = self.sps
+        size = 1 << log2
+        if x0 + size <= s.width and y0 + size <= s.height and log2 > s.log2_min_cb:
+            cond = 0
+            if self._avail(x0, y0, x0 - 1, y0) and self.cur["depth"][y0 >> 2, (x0 - 1) >> 2] > depth:
+                cond += 1
+            if self._avail(x0, y0, x0, y0 - 1) and self.cur["depth"][(y0 - 1) >> 2, x0 >> 2] > depth:
+                cond += 1
+            split = self._dec("split_cu_flag", cond)
+        else:
+            split = 1 if log2 > s.log2_min_cb else 0
+        if split:
+            h = size >> 1
+            for dy in (0, h):
+                for dx in (0, h):
+                    if x0 + dx < s.width and y0 + dy < s.height:
+                        self._coding_quadtree(x0 + dx, y0 + dy, log2 - 1, depth + 1)
+            return
+        self._coding_unit(x0, y0, log2, depth)
+
+    def _mark(self, x0, y0, n, **vals):
+        sl = (slice(y0 >> 2, (y0 + n) >> 2), slice(x0 >> 2, (x0 + n) >> 2))
+        for k, v in vals.items():
+            self.cur[k][sl] = v
+
+    def _coding_unit(self, x0, y0, log2, depth):
+        s = self.sps
+        n = 1 << log2
+        skip = 0
+        if self.slice_type != 2:
+            cond = 0
+            if self._avail(x0, y0, x0 - 1, y0) and self.cur["skip"][y0 >> 2, (x0 - 1) >> 2]:
+                cond += 1
+            if self._avail(x0, y0, x0, y0 - 1) and self.cur["skip"][(y0 - 1) >> 2, x0 >> 2]:
+                cond += 1
+            skip = self._dec("cu_skip_flag", cond)
+        if skip:
+            mv = self._prediction_unit(x0, y0, n, skip=True)
+            self._inter_pred(x0, y0, n, mv)
+            self._mark(x0, y0, n, slice=self.slice_addr, intra=0, skip=1, depth=depth, ipm=1)
+            self.cur["mv"][y0 >> 2:(y0 + n) >> 2, x0 >> 2:(x0 + n) >> 2] = mv
+            return
+        intra = 1 if self.slice_type == 2 else self._dec("pred_mode_flag")
+        if not intra or log2 == s.log2_min_cb:
+            if not self._dec("part_mode", 0):
+                raise NotImplementedError("partitions other than 2Nx2N")
+        if intra:
+            prev = self._dec("prev_intra_luma_pred_flag")
+            if prev:
+                mpm_idx = 0
+                if self.cabac.bypass():
+                    mpm_idx = 1 + self.cabac.bypass()
+            else:
+                rem = self.cabac.bypass_bits(5)
+            c = self._dec("intra_chroma_pred_mode")
+            chroma = 4 if c == 0 else self.cabac.bypass_bits(2)
+            # candidate list (8.4.2)
+            cands = []
+            for (xn, yn) in ((x0 - 1, y0), (x0, y0 - 1)):
+                if not self._avail(x0, y0, xn, yn) or not self.cur["intra"][yn >> 2, xn >> 2]:
+                    cands.append(1)
+                elif yn == y0 - 1 and yn < ((y0 >> s.log2_ctb) << s.log2_ctb):
+                    cands.append(1)
+                else:
+                    cands.append(int(self.cur["ipm"][yn >> 2, xn >> 2]))
+            a, b = cands
+            if a == b:
+                lst = [0, 1, 26] if a < 2 else [a, 2 + ((a + 29) % 32), 2 + ((a - 2 + 1) % 32)]
+            else:
+                third = 0 if (a != 0 and b != 0) else (1 if (a != 1 and b != 1) else 26)
+                lst = [a, b, third]
+            if prev:
+                mode = lst[mpm_idx]
+            else:
+                srt = sorted(lst)
+                mode = rem
+                for c2 in srt:
+                    if mode >= c2:
+                        mode += 1
+            if chroma == 4:
+                cmode = mode
+            else:
+                cmode = [0, 26, 10, 1][chroma]
+                if cmode == mode:
+                    cmode = 34
+            # decoded-ness (the slice map) is set per transform unit by _intra_pred, so a TU's
+            # not-yet-decoded neighbours inside this CU stay unavailable
+            self._mark(x0, y0, n, intra=1, skip=0, depth=depth, ipm=mode)
+            self.cur["mv"][y0 >> 2:(y0 + n) >> 2, x0 >> 2:(x0 + n) >> 2] = 0
+            self.cu_intra = (mode, cmode)
+            max_depth = s.max_th_intra
+            self._transform_tree(x0, y0, x0, y0, log2, 0, 0, True, max_depth, (1, 1))
+            return
+        merge = self._dec("merge_flag")
+        mv = self._prediction_unit(x0, y0, n, skip=False, merge=merge)
+        self._inter_pred(x0, y0, n, mv)
+        self._mark(x0, y0, n, slice=self.slice_addr, intra=0, skip=0, depth=depth, ipm=1)
+        self.cur["mv"][y0 >> 2:(y0 + n) >> 2, x0 >> 2:(x0 + n) >> 2] = mv
+        root = 1 if merge else self._dec("rqt_root_cbf")
+        if root:
+            self.cu_intra = None
+            self._transform_tree(x0, y0, x0, y0, log2, 0, 0, False, s.max_th_inter, (1, 1))
+
+    # ---------------- inter ----------------
+    def _mvd(self):
+        g0 = [self._dec("abs_mvd_greater0_flag"), self._dec("abs_mvd_greater0_flag")]
+        g1 = [self._dec("abs_mvd_greater1_flag") if g0[0] else 0, self._dec("abs_mvd_greater1_flag") if g0[1] else 0]
+        out = []
+        for i in range(2):
+            v = 0
+            if g0[i]:
+                v = 1
+                if g1[i]:
+                    # EG1
+                    k = 1
+                    absv = 0
+                    while self.cabac.bypass():
+                        absv += 1 << k
+                        k += 1
+                    absv += self.cabac.bypass_bits(k)
+                    v = absv + 2
+                if self.cabac.bypass():
+                    v = -v
+            out.append(v)
+        return out
+
+    def _nb_motion(self, x0, y0, xn, yn):
+        if not self._avail(x0, y0, xn, yn) or self.cur["intra"][yn >> 2, xn >> 2]:
+            return None
+        return tuple(int(v) for v in self.cur["mv"][yn >> 2, xn >> 2])
+
+    def _merge_cands(self, x0, y0, n):
+        A1 = self._nb_motion(x0, y0, x0 - 1, y0 + n - 1)
+        B1 = self._nb_motion(x0, y0, x0 + n - 1, y0 - 1)
+        B0 = self._nb_motion(x0, y0, x0 + n, y0 - 1)
+        A0 = self._nb_motion(x0, y0, x0 - 1, y0 + n)
+        B2 = self._nb_motion(x0, y0, x0 - 1, y0 - 1)
+        lst = []
+        if A1 is not None:
+            lst.append(A1)
+        if B1 is not None and B1 != A1:
+            lst.append(B1)
+        if B0 is not None and B0 != B1:
+            lst.append(B0)
+        if A0 is not None and A0 != A1:
+            lst.append(A0)
+        cnt = sum(v is not None for v in (A1, B1 if (B1 is not None and B1 != A1) else None,
+                                          B0 if (B0 is not None and B0 != B1) else None,
+                                          A0 if (A0 is not None and A0 != A1) else None))
+        if B2 is not None and B2 != A1 and B2 != B1 and cnt != 4:
+            lst.append(B2)
+        zero_idx = 0
+        while len(lst) < self.max_merge:
+            lst.append((0, 0))   # refIdx min(zeroIdx, numRef-1): same picture, zero vector
+            zero_idx += 1
+        return lst
+
+    def _amvp_cands(self, x0, y0, n):
+        A0 = self._nb_motion(x0, y0, x0 - 1, y0 + n)
+        A1 = self._nb_motion(x0, y0, x0 - 1, y0 + n - 1)
+        B0 = self._nb_motion(x0, y0, x0 + n, y0 - 1)
+        B1 = self._nb_motion(x0, y0, x0 + n - 1, y0 - 1)
+        B2 = self._nb_motion(x0, y0, x0 - 1, y0 - 1)
+        # single reference picture: every inter neighbour refers to it (no scaling)
+        is_scaled = A0 is not None or A1 is not None   # availableA0 || availableA1 (6.4.2: inter only)
+        mvA = A0 if A0 is not None else A1
+        mvB = B0 if B0 is not None else (B1 if B1 is not None else B2)
+        if not is_scaled and mvB is not None:
+            mvA = mvB
+        if not is_scaled:
+            mvB = B0 if B0 is not None else (B1 if B1 is not None else B2)
+        lst = []
+        if mvA is not None:
+            lst.append(mvA)
+        if mvB is not None and not (mvA is not None and mvA == mvB):
+            lst.append(mvB)
+        while len(lst) < 2:
+            lst.append((0, 0))
+        return lst[:2]
+
+    def _prediction_unit(self, x0, y0, n, skip, merge=1):
+        if skip or merge:
+            idx = 0
+            if self.max_merge > 1 and self._dec("merge_idx"):
+                idx = 1
+                while idx < self.max_merge - 1 and self.cabac.bypass():
+                    idx += 1
+            return self._merge_cands(x0, y0, n)[idx]
+        if self.num_ref > 1:
+            raise NotImplementedError("ref_idx")
+        mvd = self._mvd()
+        mvp = self._dec("mvp_flag")
+        pred = self._amvp_cands(x0, y0, n)[mvp]
+        mv = [(pred[i] + mvd[i] + (1 << 16)) % (1 << 16) for i in range(2)]
+        return tuple(v - (1 << 16) if v >= (1 << 15) else v for v in mv)
+
+    def _inter_pred(self, x0, y0, n, mv):
+        if self.ref is None:
+            raise BitstreamError("P slice without a reference picture")
+        s = self.sps
+        RY, RU, RV = (r.astype(np.int64) for r in self.ref)
+        mvx, mvy = mv
+        ys = np.arange(n)[:, None]
+        xs = np.arange(n)[None, :]
+        xi, yi, fx, fy = x0 + (mvx >> 2), y0 + (mvy >> 2), mvx & 3, mvy & 3
+
+        def refl(xx, yy):
+            return RY[np.clip(yy, 0, s.height - 1), np.clip(xx, 0, s.width - 1)]
+        if fx == 0 and fy == 0:
+            pred = refl(xi + xs, yi + ys) << 6
+        elif fy == 0:
+            pred = sum(LUMA_FILTER[fx][i] * refl(xi + xs + i - 3, yi + ys) for i in range(8))
+        elif fx == 0:
+            pred = sum(LUMA_FILTER[fy][i] * refl(xi + xs, yi + ys + i - 3) for i in range(8))
+        else:
+            tmp = [sum(LUMA_FILTER[fx][i] * refl(xi + xs + i - 3, yi + ys + k - 3) for i in range(8)) for k in range(8)]
+            pred = sum(LUMA_FILTER[fy][k] * tmp[k] for k in range(8)) >> 6
+        self.cur["Y"][y0:y0 + n, x0:x0 + n] = np.clip((pred + 32) >> 6, 0, 255)
+        m = n // 2
+        ys = np.arange(m)[:, None]
+        xs = np.arange(m)[None, :]
+        xc0, yc0 = x0 // 2, y0 // 2
+        xi, yi, fx, fy = xc0 + (mvx >> 3), yc0 + (mvy >> 3), mvx & 7, mvy & 7
+        for plane, R in (("U", RU), ("V", RV)):
+            def refc(xx, yy, R=R):
+                return R[np.clip(yy, 0, s.height // 2 - 1), np.clip(xx, 0, s.width // 2 - 1)]
+            if fx == 0 and fy == 0:
+                pred = refc(xi + xs, yi + ys) << 6
+            elif fy == 0:
+                pred = sum(CHROMA_FILTER[fx][i] * refc(xi + xs + i - 1, yi + ys) for i in range(4))
+            elif fx == 0:
+                pred = sum(CHROMA_FILTER[fy][i] * refc(xi + xs, yi + ys + i - 1) for i in range(4))
+            else:
+                tmp = [sum(CHROMA_FILTER[fx][i] * refc(xi + xs + i - 1, yi + ys + k - 1) for i in range(4))
+                       for k in range(4)]
+                pred = sum(CHROMA_FILTER[fy][k] * tmp[k] for k in range(4)) >> 6
+            self.cur[plane][yc0:yc0 + m, xc0:xc0 + m] = np.clip((pred + 32) >> 6, 0, 255)
+
+    # ---------------- transform tree ----------------
+    def _transform_tree(self, x0, y0, xb, yb, log2, depth, blk, intra, max_depth, parent_cbf):
+        s = self.sps
+        if log2 <= s.log2_max_tb and log2 > s.log2_min_tb and depth < max_depth:
+            split = self._dec("split_transform_flag", 5 - log2)
+        else:
+            split = 1 if log2 > s.log2_max_tb else 0
+        cbf_cb = cbf_cr = 0
+        if log2 > 2:
+            if depth == 0 or parent_cbf[0]:
+                cbf_cb = self._dec("cbf_chroma", depth)
+            if depth == 0 or parent_cbf[1]:
+                cbf_cr = self._dec("cbf_chroma", depth)
+        else:
+            cbf_cb, cbf_cr = parent_cbf
+        if split:
+            h = 1 << (log2 - 1)
+            for k, (dx, dy) in enumerate(((0, 0), (h, 0), (0, h), (h, h))):
+                self._transform_tree(x0 + dx, y0 + dy, x0, y0, log2 - 1, depth + 1, k, intra, max_depth,
+                                     (cbf_cb, cbf_cr))
+            return
+        cbf_y = 1
+        if intra or depth != 0 or cbf_cb or cbf_cr:
+            cbf_y = self._dec("cbf_luma", 1 if depth == 0 else 0)
+        self._transform_unit(x0, y0, xb, yb, log2, blk, cbf_y, cbf_cb, cbf_cr, intra)
+
+    def _qp_c(self, off):
+        qpi = min(max(self.qp + off, 0), 57)
+        if qpi < 30:
+            return qpi
+        if qpi > 43:
+            return qpi - 6
+        return QPC_TABLE[qpi]
+
+    def _transform_unit(self, x0, y0, xb, yb, log2, blk, cbf_y, cbf_cb, cbf_cr, intra):
+        p = self.pps
+        n = 1 << log2
+        mode, cmode = self.cu_intra if intra else (None, None)
+        if intra:
+            self._intra_pred("Y", x0, y0, n, mode, 0)
+        if cbf_y:
+            self._residual(x0, y0, log2, 0, mode, self.qp)
+        if log2 > 2:
+            xc, yc, lc = x0 // 2, y0 // 2, log2 - 1
+        elif blk == 3:
+            xc, yc, lc = xb // 2, yb // 2, 2
+        else:
+            return
+        for plane, cbf, off, ci in (("U", cbf_cb, p.cb_qp_offset, 1), ("V", cbf_cr, p.cr_qp_offset, 2)):
+            if intra:
+                self._intra_pred(plane, xc, yc, 1 << lc, cmode, ci)
+            if cbf:
+                self._residual(xc, yc, lc, ci, cmode, self._qp_c(off))
+
+    # ---------------- residual ----------------
+    def _residual(self, x0, y0, log2, cidx, intra_mode, qp):
+        n = 1 << log2
+        scan_idx = 0
+        if intra_mode is not None and (log2 == 2 or (log2 == 3 and cidx == 0)):
+            if 6 <= intra_mode <= 14:
+                scan_idx = 2
+            elif 22 <= intra_mode <= 30:
+                scan_idx = 1
+        # last significant coefficient
+        if cidx == 0:
+            off, sh = 3 * (log2 - 2) + ((log2 - 1) >> 2), (log2 + 1) >> 2
+        else:
+            off, sh = 15, log2 - 2
+        cmax = (log2 << 1) - 1
+
+        def prefix(name):
+            v = 0
+            while v < cmax and self._dec(name, off + (v >> sh)):
+                v += 1
+            return v
+        px, py = prefix("last_x_prefix"), prefix("last_y_prefix")
+
+        def fin(pre):
+            if pre <= 3:
+                return pre
+            nb = (pre >> 1) - 1
+            suf = self.cabac.bypass_bits(nb)
+            return (1 << nb) * (2 + (pre & 1)) + suf
+        lx = fin(px)
+        ly = fin(py)
+        if scan_idx == 2:
+            lx, ly = ly, lx
+        sb = scan_order(n >> 2, scan_idx) if log2 > 2 else [(0, 0)]
+        sc4 = scan_order(4, scan_idx)
+        levels = np.zeros((n, n), np.int64)
+        # locate last sub-block / position
+        last_sb, last_pos = None, None
+        for i, (xs, ys) in enumerate(sb):
+            for k, (xp, yp) in enumerate(sc4):
+                if xs * 4 + xp == lx and ys * 4 + yp == ly:
+                    last_sb, last_pos = i, k
+        if last_sb is None:
+            raise BitstreamError("last position outside the TU")
+        csbf = {}
+        greater1_ctx_prev = None
+        nsb = n >> 2
+        for i in range(last_sb, -1, -1):
+            xs, ys = sb[i]
+            infer_dc = False
+            if i < last_sb and i > 0:
+                c = 0
+                if xs < nsb - 1:
+                    c += csbf.get((xs + 1, ys), 0)
+                if ys < nsb - 1:
+                    c += csbf.get((xs, ys + 1), 0)
+                flag = self._dec("coded_sub_block_flag", min(c, 1) + (2 if cidx else 0))
+                infer_dc = True
+            else:
+                flag = 1
+            csbf[(xs, ys)] = flag
+            sig = [0] * 16
+            start = last_pos - 1 if i == last_sb else 15
+            if i == last_sb:
+                sig[last_pos] = 1
+            prev_csbf = 0
+            if xs < nsb - 1:
+                prev_csbf |= csbf.get((xs + 1, ys), 0)
+            if ys < nsb - 1:
+                prev_csbf |= csbf.get((xs, ys + 1), 0) << 1
+            for k in range(start, -1, -1):
+                if not flag:
+                    break
+                xp, yp = sc4[k]
+                xc, yc = xs * 4 + xp, ys * 4 + yp
+                if k == 0 and infer_dc:
+                    sig[0] = 1
+                    break
+                if log2 == 2:
+                    sctx = [0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8][(yc << 2) + xc]
+                elif xc + yc == 0:
+                    sctx = 0
+                else:
+                    if prev_csbf == 0:
+                        sctx = 2 if xp + yp == 0 else (1 if xp + yp < 3 else 0)
+                    elif prev_csbf == 1:
+                        sctx = 2 if yp == 0 else (1 if yp == 1 else 0)
+                    elif prev_csbf == 2:
+                        sctx = 2 if xp == 0 else (1 if xp == 1 else 0)
+                    else:
+                        sctx = 2
+                    if cidx == 0:
+                        if xs or ys:
+                            sctx += 3
+                        sctx += (9 if scan_idx == 0 else 15) if log2 == 3 else 21
+                    else:
+                        sctx += 9 if log2 == 3 else 12
+                v = self._dec("sig_coeff_flag", sctx if cidx == 0 else 27 + sctx)
+                sig[k] = v
+                if v:
+                    infer_dc = False
+            if not any(sig):
+                continue
+            # greater1
+            ctx_set = 0 if (i == 0 or cidx > 0) else 2
+            if greater1_ctx_prev is not None and greater1_ctx_prev == 0:
+                ctx_set += 1
+            g1ctx = 1
+            g1 = [0] * 16
+            g2 = [0] * 16
+            first_g1 = -1
+            n_g1 = 0
+            for k in range(15, -1, -1):
+                if sig[k]:
+                    if n_g1 < 8:
+                        f = self._dec("coeff_abs_level_greater1_flag", ctx_set * 4 + min(3, g1ctx) + (16 if cidx else 0))
+                        g1[k] = f
+                        n_g1 += 1
+                        if f and first_g1 < 0:
+                            first_g1 = k
+                        if g1ctx > 0:
+                            g1ctx = 0 if f else g1ctx + 1
+            greater1_ctx_prev = g1ctx
+            if first_g1 >= 0:
+                g2[first_g1] = self._dec("coeff_abs_level_greater2_flag", ctx_set + (4 if cidx else 0))
+            signs = [0] * 16
+            for k in range(15, -1, -1):
+                if sig[k]:
+                    signs[k] = self.cabac.bypass()
+            rice = 0
+            nsig = 0
+            for k in range(15, -1, -1):
+                if not sig[k]:
+                    continue
+                base = 1 + g1[k] + g2[k]
+                thr = (3 if k == first_g1 else 2) if nsig < 8 else 1
+                absv = base
+                if base == thr:
+                    # coeff_abs_level_remaining (9.3.3.11): prefix unary, TR / EGk suffix
+                    pre = 0
+                    while self.cabac.bypass():
+                        pre += 1
+                    if pre <= 3:
+                        rem = (pre << rice) + self.cabac.bypass_bits(rice)
+                    else:
+                        k2 = pre - 3 + rice
+                        rem = (((1 << (pre - 3)) + 3 - 1) << rice) + self.cabac.bypass_bits(k2)
+                    absv = base + rem
+                    if absv > 3 * (1 << rice):
+                        rice = min(rice + 1, 4)
+                xp, yp = sc4[k]
+                levels[ys * 4 + yp, xs * 4 + xp] = -absv if signs[k] else absv
+                nsig += 1
+        # scaling (8.6.3), flat m = 16
+        bd = 8 + log2 - 5
+        scale = 16 * LEVEL_SCALE[qp % 6] << (qp // 6)
+        d = np.clip((levels * scale + (1 << (bd - 1))) >> bd, -32768, 32767)
+        dst = cidx == 0 and log2 == 2 and intra_mode is not None
+        r = inverse_transform(d, n, dst)
+        plane = "YUV"[cidx]
+        blk = self.cur[plane][y0:y0 + n, x0:x0 + n].astype(np.int64)
+        self.cur[plane][y0:y0 + n, x0:x0 + n] = np.clip(blk + r, 0, 255)
+
+    # ---------------- intra ----------------
+    def _intra_pred(self, plane, x0, y0, n, mode, cidx):
+        """8.4.4.2: reference samples, substitution, filtering and the prediction."""
+        s = self.sps
+        P = self.cur[plane]
+        sh = 0 if cidx == 0 else 1
+        W = s.width >> sh
+        H = s.height >> sh
+        # p[-1][y] for y = -1 .. 2n-1 and p[x][-1] for x = 0 .. 2n-1
+        left = np.zeros(2 * n + 1, np.int64)   # index y+1
+        top = np.zeros(2 * n, np.int64)
+        lav = np.zeros(2 * n + 1, bool)
+        tav = np.zeros(2 * n, bool)
+
+        def av(xs, ys):   # sample coords in this plane -> availability of the luma location
+            if xs < 0 or ys < 0 or xs >= W or ys >= H:
+                return False
+            return self._avail(x0 << sh, y0 << sh, xs << sh, ys << sh)
+        for y in range(-1, 2 * n):
+            if av(x0 - 1, y0 + y):
+                left[y + 1] = P[y0 + y, x0 - 1]
+                lav[y + 1] = True
+        for x in range(2 * n):
+            if av(x0 + x, y0 - 1):
+                top[x] = P[y0 - 1, x0 + x]
+                tav[x] = True
+        # linear order: p[-1][2n-1] .. p[-1][-1], p[0][-1] .. p[2n-1][-1]
+        lin = [left[y + 1] for y in range(2 * n - 1, -2, -1)] + list(top)
+        lav_ = [lav[y + 1] for y in range(2 * n - 1, -2, -1)] + list(tav)
+        if not any(lav_):
+            lin = [128] * len(lin)
+        else:
+            first = lav_.index(True)
+            for i in range(first):
+                lin[i] = lin[first]
+            for i in range(first + 1, len(lin)):
+                if not lav_[i]:
+                    lin[i] = lin[i - 1]
+        lin = np.array(lin, np.int64)
+        log2 = n.bit_length() - 1
+        if cidx == 0 and mode != 1 and n != 4:
+            thres = {8: 7, 16: 1, 32: 0}[n]
+            if min(abs(mode - 26), abs(mode - 10)) > thres:
+                if s.strong_smoothing and n == 32:
+                    raise NotImplementedError("strong intra smoothing")
+                f = lin.copy()
+                f[1:-1] = (lin[:-2] + 2 * lin[1:-1] + lin[2:] + 2) >> 2
+                lin = f
+
+        def L(y):
+            return lin[2 * n - 1 - y]
+
+        def T(x):
+            return lin[2 * n + 1 + x]
+        pred = np.zeros((n, n), np.int64)
+        if mode == 0:
+            for y in range(n):
+                for x in range(n):
+                    pred[y, x] = ((n - 1 - x) * L(y) + (x + 1) * T(n) + (n - 1 - y) * T(x) + (y + 1) * L(n) + n) >> (log2 + 1)
+        elif mode == 1:
+            dc = (sum(T(x) for x in range(n)) + sum(L(y) for y in range(n)) + n) >> (log2 + 1)
+            pred[:] = dc
+            if cidx == 0 and n < 32:
+                pred[0, 0] = (L(0) + 2 * dc + T(0) + 2) >> 2
+                for x in range(1, n):
+                    pred[0, x] = (T(x) + 3 * dc + 2) >> 2
+                for y in range(1, n):
+                    pred[y, 0] = (L(y) + 3 * dc + 2) >> 2
+        else:
+            ang = INTRA_ANGLE[mode]
+            ref = {}
+            if mode >= 18:
+                for x in range(0, 2 * n + 1):
+                    ref[x] = T(x - 1)
+                if ang < 0 and (n * ang) >> 5 < -1:
+                    for x in range((n * ang) >> 5, 0):
+                        ref[x] = L(-1 + ((x * INV_ANGLE[mode] + 128) >> 8))
+                for y in range(n):
+                    idx, fact = ((y + 1) * ang) >> 5, ((y + 1) * ang) & 31
+                    for x in range(n):
+                        if fact:
+                            pred[y, x] = ((32 - fact) * ref[x + idx + 1] + fact * ref[x + idx + 2] + 16) >> 5
+                        else:
+                            pred[y, x] = ref[x + idx + 1]
+                if mode == 26 and cidx == 0 and n < 32:
+                    for y in range(n):
+                        pred[y, 0] = min(max(T(0) + ((L(y) - L(-1)) >> 1), 0), 255)
+            else:
+                for x in range(0, 2 * n + 1):
+                    ref[x] = L(x - 1)
+                if ang < 0 and (n * ang) >> 5 < -1:
+                    for x in range((n * ang) >> 5, 0):
+                        ref[x] = T(-1 + ((x * INV_ANGLE[mode] + 128) >> 8))
+                for x in range(n):
+                    idx, fact = ((x + 1) * ang) >> 5, ((x + 1) * ang) & 31
+                    for y in range(n):
+                        if fact:
+                            pred[y, x] = ((32 - fact) * ref[y + idx + 1] + fact * ref[y + idx + 2] + 16) >> 5
+                        else:
+                            pred[y, x] = ref[y + idx + 1]
+                if mode == 10 and cidx == 0 and n < 32:
+                    for x in range(n):
+                        pred[0, x] = min(max(L(0) + ((T(x) - T(-1)) >> 1), 0), 255)
+        P[y0:y0 + n, x0:x0 + n] = np.clip(pred, 0, 255)
+        # mark the TU decoded for later intra neighbours (luma drives availability)
+        if cidx == 0:
+            self._mark(x0, y0, n, slice=self.slice_addr)
+
+
+def psnr(a: np.ndarray, b: np.ndarray) -> float:
+    d = a.astype(np.float64) - b.astype(np.float64)
+    mse = float(np.mean(d * d))
+    return 99.0 if mse == 0 else 10 * np.log10(255.0 * 255.0 / mse)

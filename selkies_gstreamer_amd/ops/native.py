@@ -32,7 +32,7 @@ class SkH264Config(ctypes.Structure):
         ("scenecut", ctypes.c_int32), ("fps", ctypes.c_float), ("device", ctypes.c_int32),
         ("backend", ctypes.c_int32), ("deblock", ctypes.c_int32), ("me_full", ctypes.c_int32),
         ("shared_copy", ctypes.c_int32), ("src_width", ctypes.c_int32), ("src_height", ctypes.c_int32),
-        ("num_refs", ctypes.c_int32),
+        ("num_refs", ctypes.c_int32), ("codec", ctypes.c_int32),
     ]
 
 
@@ -217,7 +217,7 @@ class H264Encoder:
                  damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
                  backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
-                 src_width: int = 0, src_height: int = 0, num_refs: int = 1):
+                 src_width: int = 0, src_height: int = 0, num_refs: int = 1, codec: str = "h264"):
         L = lib()
         if backend not in ("cpu", "hip"):
             raise ValueError("backend must be 'cpu' or 'hip'")
@@ -228,7 +228,10 @@ class H264Encoder:
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
                                 device, 1 if backend == "hip" else 0, 1 if deblock else -1,
                                 1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height),
-                                int(num_refs))
+                                int(num_refs), 1 if codec == "hevc" else 0)
+        if codec not in ("h264", "hevc"):
+            raise ValueError("codec must be 'h264' or 'hevc'")
+        self.codec = codec
         self.width, self.height = width, height
         self.backend = backend
         self._h = L.sk_h264_create(ctypes.byref(self.cfg))
@@ -362,6 +365,16 @@ class H264Encoder:
         arr = (ctypes.c_float * n)()
         k = lib().sk_h264_stage_times(self._h, arr, n)
         return list(arr[:k])
+
+
+class HevcEncoder(H264Encoder):
+    """HEVC Main encoder session: full-frame pictures whose slices are stripes of whole
+    16x16-CTB rows (WPP substreams), same front end as the H.264 encoder. Packets carry
+    the 10-byte stripe header + Annex-B (VPS/SPS/PPS on IDR)."""
+
+    def __init__(self, width: int, height: int, **kw):
+        kw.pop("fullframe", None)
+        super().__init__(width, height, codec="hevc", fullframe=True, **kw)
 
 
 class JpegEncoder(H264Encoder):
