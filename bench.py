@@ -288,7 +288,7 @@ def main():
         res = {
             "metric": "encoded fps + glass-to-glass p50 ms at 1920x1080; concurrent 60fps sessions/node",
             "value": round(fps, 2),
-            "unit": f"frames/s ({W}x{H} {'H.264' if args.encoder == 'h264' else 'JPEG'}, all sessions, all GPUs)",
+            "unit": f"frames/s ({W}x{H} {dict(h264='H.264', hevc='HEVC', jpeg='JPEG')[args.encoder]}, all sessions, all GPUs)",
             "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -308,7 +308,9 @@ def main():
             "config": {
                 "model": (f"H.264 Constrained Baseline CAVLC, {args.mode} stripes {args.stripe_height}px, QP {args.qp}"
                           if args.encoder == "h264" else
-                          f"baseline JPEG 4:2:0 stripes {args.stripe_height}px, quality {args.jpeg_quality}"),
+                          (f"HEVC Main CABAC, CTB 16, WPP, slices of {args.stripe_height}px, QP {args.qp}"
+                           if args.encoder == "hevc" else
+                           f"baseline JPEG 4:2:0 stripes {args.stripe_height}px, quality {args.jpeg_quality}")),
                 "global_batch": S * n_gpus,
                 "seq_len": 1,
                 "parallelism": f"session-parallel dp{n_gpus} x {S} sessions/GPU",

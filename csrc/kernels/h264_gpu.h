@@ -69,6 +69,8 @@ struct FrameArgs {
 
 void launch_convert_damage(const FrameArgs& a, hipStream_t s);
 void launch_encode(const FrameArgs& a, hipStream_t s);   // k_plan and everything after it
+// k_plan, motion search and scene-cut decisions only (the HEVC back end follows it)
+void launch_frontend(const FrameArgs& a, hipStream_t s);
 void launch_commit(const FrameArgs& a, hipStream_t s);   // MV field + reference update (+ K7 deblocking)
 
 }  // namespace gpu

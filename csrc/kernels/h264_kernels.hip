@@ -2357,12 +2357,17 @@ void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_convert_damage, grid, dim3(256), 0, s, a);
 }
 
-void launch_encode(const FrameArgs& a, hipStream_t s) {
+void launch_frontend(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
     hipLaunchKernelGGL(k_plan, dim3(1), dim3(256), 0, s, a);
     if (a.me_full) hipLaunchKernelGGL(k_me_mfma, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
+}
+
+void launch_encode(const FrameArgs& a, hipStream_t s) {
+    int nmb = a.mb_w * a.mb_h;
+    launch_frontend(a, s);
     hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_intra_prep, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     if (a.rows_per_slice <= 4)

@@ -1,0 +1,38 @@
+// Device buffers and launch interface of the HIP HEVC back end. It runs after the
+// H.264 front end (k_convert_damage, k_plan, k_me_mfma, k_motion_search, k_decide)
+// on the same FrameArgs and before k_commit (reference / motion-field update).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "h264_gpu.h"
+#include "../codec/hevc_core.h"
+#include "../codec/hevc_syntax.h"
+
+namespace sk {
+namespace hevc {
+namespace gpu {
+
+struct HevcArgs {
+    h264::gpu::FrameArgs f;     // planes, geometry (mb = CTB), tasks, motion field
+    CuInfo* cus;                // [ctbs]
+    int16_t* coefs;             // [ctbs][kCoefPerCu]
+    uint16_t* bins;             // [ctbs][kCuBinCap]
+    int* bin_n;                 // [ctbs]
+    uint8_t* sync;              // [ctb_h][CTX_COUNT] WPP context states at each row start
+    uint8_t* sub;               // [ctb_h][sub_stride] CABAC substreams (one per CTB row)
+    int sub_stride;
+    int* sub_size;              // [ctb_h] bytes
+    int* sub_esc;               // [ctb_h] bytes after emulation prevention
+    int* row_off;               // [ctb_h] byte offset of the row's substream inside its slice NAL
+    uint8_t* out_host;          // host-mapped slice slots [num_slices][out_slot]
+    int* out_size;              // host-mapped [num_slices]: NAL bytes (> out_slot: in out_dev)
+    uint8_t* out_dev;           // device fallback slots [num_slices][out_dev_slot]
+    int out_slot, out_dev_slot;
+    int addr_bits;
+    unsigned long long* dbg;    // optional (SK_STAMPS): per CTB row [cycles, entries, bytes, 0]
+};
+
+void launch_backend(const HevcArgs& a, hipStream_t s);
+
+}  // namespace gpu
+}  // namespace hevc
+}  // namespace sk

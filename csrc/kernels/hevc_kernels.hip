@@ -1,0 +1,830 @@
+// gfx950 (CDNA4) kernels of the HEVC back end. One 64-lane wavefront per 16x16 CU:
+//   k_hevc_inter       P slices: merge/AMVP decision on the front end's motion field,
+//                      integer luma MC + 4-tap chroma MC, 16x16 / 8x8 DCT (LDS, lane =
+//                      row x 4 columns), quantisation, reconstruction (SKIPALL: all skip)
+//   k_hevc_intra_prep  I slices, every CU in parallel: intra mode against the source
+//   k_hevc_intra       I slices: CTB wavefront (wave = CTB row, lag 2 = WPP order)
+//   k_hevc_bins        CU syntax -> CABAC bin entries (hevc_core.h code_cu)
+//   k_hevc_sync        WPP: context states at every CTB row start (state-only replay of
+//                      the first two CTBs of the row above, lane = context)
+//   k_hevc_cabac       one wave per CTB row: arithmetic coding of the row's substream
+//   k_hevc_hdr         slice header with entry points, NAL prefix, substream offsets
+//   k_hevc_ep_copy     wave-parallel emulation prevention + copy into host-mapped slots
+// Bit-exact with the CPU reference (codec/hevc_cpu.cpp): integer math only.
+#include "hevc_gpu.h"
+
+namespace sk {
+namespace hevc {
+namespace gpu {
+
+using h264::ACT_I;
+using h264::ACT_P;
+using h264::ACT_SKIPALL;
+using h264::SliceTask;
+using h264::gpu::FrameArgs;
+using h264::gpu::Planes;
+
+__device__ __forceinline__ int lane() { return threadIdx.x & 63; }
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int wsum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Per-wave LDS working set of one CU.
+struct CuLds {
+    uint8_t src[kCoefPerCu];     // Y 16x16 | Cb 8x8 | Cr 8x8 (raster)
+    uint8_t pred[kCoefPerCu];
+    int32_t a[kCoefPerCu];       // residual / dequantised coefficients
+    int32_t b[kCoefPerCu];       // transform intermediate
+    uint8_t ref[65 + 65 + 33 + 33];   // intra: luma raw | luma filtered | Cb | Cr
+    int misc[4];
+};
+
+// LDS copy of the 16-point DCT matrix (the 8-point one is its even rows).
+__device__ __forceinline__ void load_t16(int8_t* t) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) t[i] = HEVC_T16[i >> 4][i & 15];
+}
+
+// Transform, quantisation and reconstruction of the CU in L (src, pred filled).
+// Lane mapping: luma outputs (row l >> 2, columns 4*(l & 3) .. +3), chroma outputs
+// (component l >> 5, row (l >> 2) & 7, columns 2*(l & 3) .. +1). Writes the levels to
+// `gcoef` (global) and the reconstruction into L.pred; returns the cbf bits.
+__device__ int code_cu_wave(CuLds& L, const int8_t* T, int qp, bool intra, int16_t* gcoef) {
+    const int l = lane();
+    const int qpc = chroma_qp(qp);
+    const int ly = l >> 2, lx0 = 4 * (l & 3);
+    const int cc = l >> 5, cy = (l >> 2) & 7, cx0 = 2 * (l & 3);
+    const int cbase = kCoefCb + cc * 64;
+    for (int i = l; i < kCoefPerCu; i += 64) L.a[i] = (int)L.src[i] - (int)L.pred[i];
+    wsync();
+    // forward stage 1 (rows): b[y][u] = (sum_x T[u][x] a[y][x] + rnd) >> sh1
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int u = lx0 + k;
+        int s = 0;
+#pragma unroll
+        for (int x = 0; x < 16; x++) s += (int)T[u * 16 + x] * L.a[ly * 16 + x];
+        L.b[ly * 16 + u] = (s + 4) >> 3;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int u = cx0 + k;
+        int s = 0;
+#pragma unroll
+        for (int x = 0; x < 8; x++) s += (int)T[(2 * u) * 16 + x] * L.a[cbase + cy * 8 + x];
+        L.b[cbase + cy * 8 + u] = (s + 2) >> 2;
+    }
+    wsync();
+    // forward stage 2 (columns) + quantisation + dequantisation; levels to global
+    int nzl = 0, nzc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int u = lx0 + k, v = ly;
+        int s = 0;
+#pragma unroll
+        for (int y = 0; y < 16; y++) s += (int)T[v * 16 + y] * L.b[y * 16 + u];
+        const int c = (s + 512) >> 10;
+        const int lv = quant_level(c, qp, 4, intra);
+        nzl |= lv;
+        gcoef[v * 16 + u] = (int16_t)lv;
+        L.a[v * 16 + u] = dequant_level(lv, qp, 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int u = cx0 + k, v = cy;
+        int s = 0;
+#pragma unroll
+        for (int y = 0; y < 8; y++) s += (int)T[(2 * v) * 16 + y] * L.b[cbase + y * 8 + u];
+        const int c = (s + 256) >> 9;
+        const int lv = quant_level(c, qpc, 3, intra);
+        nzc |= lv;
+        gcoef[cbase + v * 8 + u] = (int16_t)lv;
+        L.a[cbase + v * 8 + u] = dequant_level(lv, qpc, 3);
+    }
+    const int cbf = (__ballot(nzl != 0) ? 1 : 0) | ((__ballot(nzc != 0 && cc == 0) ? 1 : 0) << 1) |
+                    ((__ballot(nzc != 0 && cc == 1) ? 1 : 0) << 2);
+    wsync();
+    // inverse stage 1 (columns): b[y][x] = clip16((sum_j T[j][y] a[j][x] + 64) >> 7)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int x = lx0 + k, y = ly;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) s += (int)T[j * 16 + y] * L.a[j * 16 + x];
+        L.b[y * 16 + x] = sk_clip((s + 64) >> 7, -32768, 32767);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int x = cx0 + k, y = cy;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) s += (int)T[(2 * j) * 16 + y] * L.a[cbase + j * 8 + x];
+        L.b[cbase + y * 8 + x] = sk_clip((s + 64) >> 7, -32768, 32767);
+    }
+    wsync();
+    // inverse stage 2 (rows) + reconstruction into pred
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int x = lx0 + k, y = ly;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) s += (int)T[j * 16 + x] * L.b[y * 16 + j];
+        const int i = y * 16 + x;
+        L.pred[i] = (uint8_t)sk_clip255((int)L.pred[i] + ((s + 2048) >> 12));
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int x = cx0 + k, y = cy;
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) s += (int)T[(2 * j) * 16 + x] * L.b[cbase + y * 8 + j];
+        const int i = cbase + y * 8 + x;
+        L.pred[i] = (uint8_t)sk_clip255((int)L.pred[i] + ((s + 2048) >> 12));
+    }
+    wsync();
+    return cbf;
+}
+
+// Source samples of CU (cx, cy) into L.src; reconstruction L.pred to the rec planes.
+__device__ void load_src(CuLds& L, const FrameArgs& f, int cx, int cy) {
+    const int l = lane();
+    for (int i = l; i < kCoefPerCu; i += 64) {
+        uint8_t v;
+        if (i < 256) v = f.src.y[(size_t)(cy * 16 + (i >> 4)) * f.stride_y + cx * 16 + (i & 15)];
+        else {
+            const int j = i - 256, c = j >> 6, r = (j >> 3) & 7, x = j & 7;
+            v = (c ? f.src.v : f.src.u)[(size_t)(cy * 8 + r) * f.stride_c + cx * 8 + x];
+        }
+        L.src[i] = v;
+    }
+}
+__device__ void store_rec(const CuLds& L, const FrameArgs& f, int cx, int cy) {
+    const int l = lane();
+    for (int i = l; i < kCoefPerCu; i += 64) {
+        if (i < 256) f.rec.y[(size_t)(cy * 16 + (i >> 4)) * f.stride_y + cx * 16 + (i & 15)] = L.pred[i];
+        else {
+            const int j = i - 256, c = j >> 6, r = (j >> 3) & 7, x = j & 7;
+            (c ? f.rec.v : f.rec.u)[(size_t)(cy * 8 + r) * f.stride_c + cx * 8 + x] = L.pred[i];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K6 inter (P slices) and skip-all slices: one wave per CU, 4 CUs per workgroup.
+__global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
+    __shared__ CuLds Lw[4];
+    __shared__ int8_t T[256];
+    const FrameArgs& f = A.f;
+    CuLds& L = Lw[threadIdx.x >> 6];
+    const int n = f.mb_w * f.mb_h;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const bool valid = idx < n;
+    const int cx = valid ? idx % f.mb_w : 0, cy = valid ? idx / f.mb_w : 0;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const int l = lane();
+    if (valid && t.final_action == ACT_SKIPALL && l == 0) {
+        CuInfo z;
+        memset(&z, 0, sizeof(z));
+        z.mode = CU_SKIP;
+        z.qp = (uint8_t)t.qp;
+        A.cus[idx] = z;
+    }
+    const bool coded = valid && t.final_action == ACT_P;
+    if (!__syncthreads_or(coded)) return;
+    load_t16(T);
+    __syncthreads();
+    if (!coded) return;
+    const int W = f.mb_w;
+    auto nb = [&](int ox, int oy, bool ok) {
+        NbMv m;
+        m.av = ok;
+        m.mvx = ok ? 4 * f.me[oy * W + ox].mvx : 0;
+        m.mvy = ok ? 4 * f.me[oy * W + ox].mvy : 0;
+        return m;
+    };
+    const bool top = cy > t.first_row;
+    const NbMv A1 = nb(cx - 1, cy, cx > 0), B1 = nb(cx, cy - 1, top);
+    const NbMv B0 = nb(cx + 1, cy - 1, top && cx + 1 < W), B2 = nb(cx - 1, cy - 1, top && cx > 0);
+    int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];
+    merge_list(A1, B1, B0, B2, mlx, mly);
+    amvp_list(A1, B1, B0, B2, px, py);
+    const int mvx = 4 * f.me[idx].mvx, mvy = 4 * f.me[idx].mvy;
+    const int pic_w = f.stride_y, pic_h = f.mb_h * 16;
+    load_src(L, f, cx, cy);
+    {   // luma integer MC: lane = row l >> 2, 4 columns
+        const int dx = mvx >> 2, dy = mvy >> 2;
+        const int y = l >> 2;
+        const uint8_t* row = f.ref.y + (size_t)sk_clip(cy * 16 + y + dy, 0, pic_h - 1) * f.stride_y;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int x = 4 * (l & 3) + k;
+            L.pred[y * 16 + x] = row[sk_clip(cx * 16 + x + dx, 0, pic_w - 1)];
+        }
+        // chroma: lane -> component l >> 5, row (l >> 2) & 7, 2 columns
+        const int c = l >> 5, r = (l >> 2) & 7;
+        const uint8_t* plane = c ? f.ref.v : f.ref.u;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int x = 2 * (l & 3) + k;
+            L.pred[kCoefCb + c * 64 + r * 8 + x] = (uint8_t)chroma_mc_sample(
+                plane, f.stride_c, f.stride_c, f.mb_h * 8, cx * 8 + x, cy * 8 + r, mvx, mvy);
+        }
+    }
+    wsync();
+    const int cbf = code_cu_wave(L, T, t.qp, false, A.coefs + (size_t)idx * kCoefPerCu);
+    store_rec(L, f, cx, cy);
+    if (l == 0) {
+        CuInfo cu;
+        memset(&cu, 0, sizeof(cu));
+        int midx = -1;
+        for (int i = 0; i < kMaxMergeCand && midx < 0; i++)
+            if (mlx[i] == mvx && mly[i] == mvy) midx = i;
+        cu.cbf = (uint8_t)cbf;
+        cu.qp = (uint8_t)t.qp;
+        cu.mvx = (int16_t)mvx;
+        cu.mvy = (int16_t)mvy;
+        if (midx >= 0) {
+            cu.mode = cbf ? CU_MERGE : CU_SKIP;
+            cu.merge_idx = (uint8_t)midx;
+        } else {
+            cu.mode = CU_AMVP;
+            const int c0 = mvd_bits_est(mvx - px[0]) + mvd_bits_est(mvy - py[0]);
+            const int c1 = mvd_bits_est(mvx - px[1]) + mvd_bits_est(mvy - py[1]);
+            const int k = c1 < c0 ? 1 : 0;
+            cu.mvp_idx = (uint8_t)k;
+            cu.mvdx = (int16_t)(mvx - px[k]);
+            cu.mvdy = (int16_t)(mvy - py[k]);
+        }
+        A.cus[idx] = cu;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Intra reference samples (8.4.4.2.2, substitution in closed form for CTB = CU: the
+// bottom-left half is never available) of an n x n block at (x0, y0): linear layout
+// of build_intra_ref. Every lane writes the entries i = lane, lane + 64.
+__device__ void fill_ref(const uint8_t* P, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
+                         uint8_t* ref) {
+    const int len = 4 * n + 1;
+    for (int i = lane(); i < len; i += 64) {
+        int v;
+        if (!left && !top) {
+            v = 128;
+        } else if (i < 2 * n) {
+            const int y = 2 * n - 1 - i;
+            v = left ? P[(size_t)(y0 + sk_min(y, n - 1)) * stride + x0 - 1] : P[(size_t)(y0 - 1) * stride + x0];
+        } else if (i == 2 * n) {
+            v = (left && top) ? P[(size_t)(y0 - 1) * stride + x0 - 1]
+                              : (left ? P[(size_t)y0 * stride + x0 - 1] : P[(size_t)(y0 - 1) * stride + x0]);
+        } else {
+            const int x = i - 2 * n - 1;
+            if (x < n) v = top ? P[(size_t)(y0 - 1) * stride + x0 + x] : P[(size_t)y0 * stride + x0 - 1];
+            else v = tr ? P[(size_t)(y0 - 1) * stride + x0 + x]
+                        : (top ? P[(size_t)(y0 - 1) * stride + x0 + n - 1] : P[(size_t)y0 * stride + x0 - 1]);
+        }
+        ref[i] = (uint8_t)v;
+    }
+}
+__device__ void filter_ref(const uint8_t* r, int n, uint8_t* out) {
+    const int len = 4 * n + 1;
+    for (int i = lane(); i < len; i += 64)
+        out[i] = (i == 0 || i == len - 1) ? r[i] : (uint8_t)((r[i - 1] + 2 * r[i] + r[i + 1] + 2) >> 2);
+}
+// Prediction sample for the encoder's modes (planar 0, DC 1, horizontal 10, vertical 26),
+// identical to intra_pred_sample for them. dc: the block's DC value.
+__device__ __forceinline__ int pred_fast(const uint8_t* r, int n, int log2n, int mode, bool luma, int dc, int x,
+                                         int y) {
+    auto Lf = [&](int yy) { return (int)r[2 * n - 1 - yy]; };
+    auto Tf = [&](int xx) { return (int)r[2 * n + 1 + xx]; };
+    if (mode == 0)
+        return ((n - 1 - x) * Lf(y) + (x + 1) * Tf(n) + (n - 1 - y) * Tf(x) + (y + 1) * Lf(n) + n) >> (log2n + 1);
+    if (mode == 1) {
+        if (luma) {
+            if (x == 0 && y == 0) return (Lf(0) + 2 * dc + Tf(0) + 2) >> 2;
+            if (y == 0) return (Tf(x) + 3 * dc + 2) >> 2;
+            if (x == 0) return (Lf(y) + 3 * dc + 2) >> 2;
+        }
+        return dc;
+    }
+    if (mode == 26) return (luma && x == 0) ? sk_clip255(Tf(0) + ((Lf(y) - Lf(-1)) >> 1)) : Tf(x);
+    return (luma && y == 0) ? sk_clip255(Lf(0) + ((Tf(x) - Tf(-1)) >> 1)) : Lf(y);
+}
+// DC value of an n x n block: (sum of n top + n left references + n) >> (log2n + 1).
+__device__ __forceinline__ int dc_value(const uint8_t* r, int n, int log2n) {
+    const int l = lane();
+    int v = 0;
+    if (l < n) v = r[2 * n + 1 + l];               // top
+    else if (l < 2 * n) v = r[2 * n - 1 - (l - n)];   // left
+    return (wsum(v) + n) >> (log2n + 1);
+}
+// Intra prediction of the whole CU into L.pred for `mode` (refs in L.ref).
+__device__ void intra_pred_cu(CuLds& L, int mode) {
+    const int l = lane();
+    uint8_t* ry = (mode == 0) ? L.ref + 65 : L.ref;   // luma planar uses the filtered references
+    const int dcy = dc_value(L.ref, 16, 4);
+    const int dcu = dc_value(L.ref + 130, 8, 3), dcv = dc_value(L.ref + 163, 8, 3);
+    for (int i = l; i < kCoefPerCu; i += 64) {
+        int v;
+        if (i < 256) v = pred_fast(ry, 16, 4, mode, true, dcy, i & 15, i >> 4);
+        else {
+            const int j = i - 256, c = j >> 6;
+            v = pred_fast(L.ref + 130 + 33 * c, 8, 3, mode, false, c ? dcv : dcu, j & 7, (j >> 3) & 7);
+        }
+        L.pred[i] = (uint8_t)v;
+    }
+    wsync();
+}
+__device__ void intra_refs(CuLds& L, const Planes& P, const FrameArgs& f, int cx, int cy, bool left, bool top,
+                           bool tr) {
+    fill_ref(P.y, f.stride_y, cx * 16, cy * 16, 16, left, top, tr, L.ref);
+    fill_ref(P.u, f.stride_c, cx * 8, cy * 8, 8, left, top, tr, L.ref + 130);
+    fill_ref(P.v, f.stride_c, cx * 8, cy * 8, 8, left, top, tr, L.ref + 163);
+    wsync();
+    filter_ref(L.ref, 16, L.ref + 65);
+    wsync();
+}
+
+// Open-loop intra mode per CU of I slices (all CUs in parallel).
+__global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
+    __shared__ CuLds Lw[4];
+    const FrameArgs& f = A.f;
+    CuLds& L = Lw[threadIdx.x >> 6];
+    const int n = f.mb_w * f.mb_h;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (idx >= n) return;   // wave-uniform; no block barriers below
+    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    if (t.final_action != ACT_I) return;
+    const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < f.mb_w;
+    intra_refs(L, f.src, f, cx, cy, left, top, tr);
+    load_src(L, f, cx, cy);
+    wsync();
+    const int l = lane();
+    const int dc = dc_value(L.ref, 16, 4);
+    const int cand[4] = {1, 0, 26, 10};
+    int best = 1, best_sad = 0x7fffffff;
+    for (int k = 0; k < 4; k++) {
+        const int m = cand[k];
+        const uint8_t* r = m == 0 ? L.ref + 65 : L.ref;
+        int sad = 0;
+        for (int i = l; i < 256; i += 64) sad += sk_abs((int)L.src[i] - pred_fast(r, 16, 4, m, true, dc, i & 15, i >> 4));
+        sad = wsum(sad);
+        if (sad < best_sad) { best_sad = sad; best = m; }
+    }
+    if (l == 0) {
+        CuInfo cu;
+        memset(&cu, 0, sizeof(cu));
+        cu.mode = CU_INTRA;
+        cu.intra_mode = (uint8_t)best;
+        A.cus[idx] = cu;
+    }
+}
+
+// I slices: one workgroup per slice, wave w = CTB row w of the slice, CTB x coded at
+// step x + 2w (the top-right CTB is one step older: WPP / intra availability order).
+template <int MAXR>
+__global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
+    __shared__ CuLds Lw[MAXR];
+    __shared__ int8_t T[256];
+    const FrameArgs& f = A.f;
+    const SliceTask t = f.tasks[blockIdx.x];
+    if (t.final_action != ACT_I) return;   // block-uniform
+    load_t16(T);
+    __syncthreads();
+    const int w = threadIdx.x >> 6, l = lane();
+    CuLds& L = Lw[w];
+    const int rows = t.num_rows, steps = f.mb_w + 2 * (rows - 1);
+    const int cy = t.first_row + w;
+    __builtin_amdgcn_s_setprio(3);
+    for (int step = 0; step < steps; step++) {
+        const int cx = step - 2 * w;
+        if (w < rows && cx >= 0 && cx < f.mb_w) {
+            const int idx = cy * f.mb_w + cx;
+            const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < f.mb_w;
+            const int mode = __builtin_amdgcn_readfirstlane(A.cus[idx].intra_mode);
+            intra_refs(L, f.rec, f, cx, cy, left, top, tr);
+            load_src(L, f, cx, cy);
+            intra_pred_cu(L, mode);
+            const int cbf = code_cu_wave(L, T, t.qp, true, A.coefs + (size_t)idx * kCoefPerCu);
+            store_rec(L, f, cx, cy);
+            if (l == 0) {
+                CuInfo cu;
+                memset(&cu, 0, sizeof(cu));
+                cu.mode = CU_INTRA;
+                cu.intra_mode = (uint8_t)mode;
+                cu.cbf = (uint8_t)cbf;
+                cu.qp = (uint8_t)t.qp;
+                A.cus[idx] = cu;
+                f.me[idx].mvx = 0;
+                f.me[idx].mvy = 0;
+                f.me[idx].ref = 0;
+            }
+        }
+        __syncthreads();   // this step's reconstruction is visible to the next step's neighbours
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CU syntax -> bin entries: one thread per CU (a wave binarises 64 CUs at once).
+__global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int n = f.mb_w * f.mb_h;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n) return;
+    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const bool p_slice = t.final_action != ACT_I;
+    const bool left = cx > 0, top = cy > t.first_row;
+    const CuInfo cu = A.cus[idx];
+    const int skip_ctx = (left && A.cus[idx - 1].mode == CU_SKIP) + (top && A.cus[idx - f.mb_w].mode == CU_SKIP);
+    const int cand_a = (left && A.cus[idx - 1].mode == CU_INTRA) ? A.cus[idx - 1].intra_mode : 1;
+    BinBuf w{A.bins + (size_t)idx * kCuBinCap, 0};
+    code_cu(w, cu, A.coefs + (size_t)idx * kCoefPerCu, p_slice, skip_ctx, cand_a);
+    w.term(cy == t.first_row + t.num_rows - 1 && cx == f.mb_w - 1);
+    A.bin_n[idx] = w.n;
+}
+
+// v_writelane equivalent: lane `ln` (wave-uniform) of `v` takes the uniform value `x`.
+__device__ __forceinline__ int writelane(int x, int ln, int v) { return lane() == ln ? x : v; }
+
+// Streams the bin entries of CUs [first, first + count) of one CTB row, 64 at a time:
+// every lane loads one entry (coalesced, next chunk prefetched), the wave-uniform loop
+// body reads entry i with a readlane. fn(entry) is wave-uniform.
+template <class F>
+__device__ __forceinline__ void for_each_entry(const HevcArgs& A, int first, int count, F&& fn) {
+    const int l = lane();
+    for (int idx = first; idx < first + count; idx++) {
+        const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
+        const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
+        uint32_t cur = l < nb ? b[l] : 0u;
+        for (int base = 0; base < nb; base += 64) {
+            const uint32_t nxt = base + 64 + l < nb ? b[base + 64 + l] : 0u;   // prefetch
+            const int m = nb - base < 64 ? nb - base : 64;
+            for (int i = 0; i < m; i++) fn((uint32_t)__builtin_amdgcn_readlane((int)cur, i));
+            cur = nxt;
+        }
+    }
+}
+
+// WPP context states at each row start of a slice: lane c owns contexts c, c+64, c+128
+// (one state byte each) and replays the state transitions of the first two CTBs of the
+// row above (no arithmetic coding needed for the states).
+__global__ __launch_bounds__(64) void k_hevc_sync(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const SliceTask t = f.tasks[blockIdx.x];
+    const int l = lane();
+    const int it = t.final_action == ACT_I ? 0 : 1;
+    uint8_t st[3], init[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const int c = l + 64 * k;
+        init[k] = st[k] = c < CTX_COUNT ? ctx_init_state(HEVC_CTX_INIT[it][c], t.qp) : 0;
+    }
+    auto store_row = [&](int cy) __attribute__((always_inline)) {
+        uint8_t* dst = A.sync + (size_t)cy * CTX_COUNT;
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            if (l + 64 * k < CTX_COUNT) dst[l + 64 * k] = st[k];
+    };
+    store_row(t.first_row);
+    for (int r = 1; r < t.num_rows; r++) {
+        if (f.mb_w >= 2) {
+            for_each_entry(A, (t.first_row + r - 1) * f.mb_w, 2, [&](uint32_t e) __attribute__((always_inline)) {
+                if (e & 0x8000u) return;
+                const int c = e & 0xff;
+                if (c == CTX_TERM || (c & 63) != l) return;
+                const int bin = (e >> 8) & 1;
+                if (c < 64) ctx_update(st[0], bin);
+                else if (c < 128) ctx_update(st[1], bin);
+                else ctx_update(st[2], bin);
+            });
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; k++) st[k] = init[k];
+        }
+        store_row(t.first_row + r);
+    }
+}
+
+// One wave per CTB row: the row's CABAC substream, run on the scalar unit. The coder
+// state (low, range, bits_left, carry buffer) is wave-uniform (SGPRs); context states,
+// the LPS range table and the LPS transition table live across the 64 lanes of three,
+// one and one VGPRs and are accessed with v_readlane (and a lane-select write) at a
+// uniform lane index; output bytes are gathered into a VGPR (lane = 4-byte word) and
+// stored 256 bytes at a time by the whole wave.
+struct WaveCabac {
+    int cs;                     // context states: context c is byte c & 3 of lane c >> 2
+    int lps_v, nxt_v;           // CABAC_LPS[lane] packed, CABAC_NEXT_LPS[lane]
+    uint32_t low, range, buffered, acc;
+    int bits_left, nbuf, opos, flushed;
+    int ob;                     // output chunk
+    uint8_t* out;
+
+    __device__ __forceinline__ void put(uint32_t byte) {
+        acc |= (byte & 0xffu) << (8 * (opos & 3));
+        opos++;
+        if ((opos & 3) == 0) {
+            ob = writelane((int)acc, (opos >> 2) - 1, ob);
+            acc = 0;
+            if (opos == 256) {
+                reinterpret_cast<int*>(out + flushed)[lane()] = ob;
+                flushed += 256;
+                opos = 0;
+            }
+        }
+    }
+    __device__ __forceinline__ void write_out() {
+        const uint32_t lead = low >> (24 - bits_left);
+        bits_left += 8;
+        low &= 0xffffffffu >> bits_left;
+        if (lead == 0xff) {
+            nbuf++;
+        } else if (nbuf > 0) {
+            const uint32_t carry = lead >> 8;
+            put(buffered + carry);
+            buffered = lead & 0xff;
+            const uint32_t fill = (0xff + carry) & 0xff;
+            while (nbuf > 1) {
+                put(fill);
+                nbuf--;
+            }
+        } else {
+            nbuf = 1;
+            buffered = lead;
+        }
+    }
+    // One bin entry (same arithmetic as CabacEncoder): context bins take three
+    // readlanes (state, LPS ranges, LPS transition) and one lane-select write; the
+    // renormalisation shift is a count-leading-zeros; bypass runs and terminating bins
+    // are the other two (rarer) paths. Only the byte output (every ~8 coded bits)
+    // leaves this straight-line code.
+    __device__ __forceinline__ void code(uint32_t e) {
+        if (!(e & 0x8000u) && (e & 0xffu) != CTX_TERM) {
+            const uint32_t c = e & 0xffu, bin = (e >> 8) & 1u;
+            const int wl = (int)(c >> 2), sh = (int)(c & 3u) * 8;
+            const uint32_t word = (uint32_t)__builtin_amdgcn_readlane(cs, wl);
+            const uint32_t s = (word >> sh) & 0xffu;
+            const uint32_t st = s >> 1, mps = s & 1u;
+            const uint32_t lps = ((uint32_t)__builtin_amdgcn_readlane(lps_v, (int)st) >> ((range >> 3) & 24u)) & 0xffu;
+            const uint32_t rmps = range - lps;
+            uint32_t ns, r, lo;
+            if (bin != mps) {
+                const uint32_t nxt = (uint32_t)__builtin_amdgcn_readlane(nxt_v, (int)st);
+                ns = (nxt << 1) | (st == 0 ? mps ^ 1u : mps);
+                r = lps;
+                lo = low + rmps;
+            } else {
+                ns = s + (st < 62 ? 2u : 0u);
+                r = rmps;
+                lo = low;
+            }
+            const int nb = 8 - (31 - __builtin_clz(r));   // <= 0 when r >= 256
+            const int k = nb > 0 ? nb : 0;
+            low = lo << k;
+            range = r << k;
+            bits_left -= k;
+            cs = writelane((int)((word & ~(0xffu << sh)) | (ns << sh)), wl, cs);
+        } else if (e & 0x8000u) {   // bypass run
+            const int n = (int)((e >> 12) & 7u) + 1;
+            low = (low << n) + range * (e & 0xffu);
+            bits_left -= n;
+        } else {                    // terminating bin
+            range -= 2;
+            if ((e >> 8) & 1) {
+                low += range;
+                low <<= 7;
+                range = 2 << 7;
+                bits_left -= 7;
+            } else if (range < 256) {
+                low <<= 1;
+                range <<= 1;
+                bits_left--;
+            }
+        }
+        if (bits_left < 12) write_out();
+    }
+    __device__ __forceinline__ void finish() {
+        if (low >> (32 - bits_left)) {
+            put(buffered + 1);
+            while (nbuf > 1) {
+                put(0x00);
+                nbuf--;
+            }
+            low -= 1u << (32 - bits_left);
+        } else {
+            if (nbuf > 0) put(buffered);
+            while (nbuf > 1) {
+                put(0xff);
+                nbuf--;
+            }
+        }
+        const int nb = 24 - bits_left;
+        uint64_t v = ((uint64_t)(low >> 8) & ((1ull << nb) - 1)) << 1 | 1ull;
+        int total = nb + 1;
+        const int pad = (8 - (total & 7)) & 7;
+        v <<= pad;
+        total += pad;
+        for (int i = total - 8; i >= 0; i -= 8) put((uint32_t)(v >> i) & 0xff);
+        // tail: complete words in ob plus the partial word in acc
+        if (opos & 3) ob = writelane((int)acc, opos >> 2, ob);
+        const int l = lane();
+        const int words = (opos + 3) >> 2;
+        if (l < words) {
+            const uint32_t wv = (uint32_t)ob;
+            uint8_t* d = out + flushed + 4 * l;
+            const int nbytes = l * 4 + 4 <= opos ? 4 : opos - 4 * l;
+            for (int k = 0; k < nbytes; k++) d[k] = (uint8_t)(wv >> (8 * k));
+        }
+    }
+};
+
+__global__ __launch_bounds__(64) void k_hevc_cabac(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int cy = blockIdx.x;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const int l = lane();
+    const uint8_t* srow = A.sync + (size_t)cy * CTX_COUNT;
+    WaveCabac E;
+    {
+        uint32_t w = 0;
+        for (int k = 0; k < 4; k++) {
+            const int c = 4 * l + k;
+            w |= (uint32_t)(c < CTX_COUNT ? srow[c] : 0) << (8 * k);
+        }
+        E.cs = (int)w;
+    }
+    E.lps_v = (int)((uint32_t)CABAC_LPS[l][0] | ((uint32_t)CABAC_LPS[l][1] << 8) | ((uint32_t)CABAC_LPS[l][2] << 16) |
+                    ((uint32_t)CABAC_LPS[l][3] << 24));
+    E.nxt_v = CABAC_NEXT_LPS[l];
+    E.out = A.sub + (size_t)cy * A.sub_stride;
+    E.low = 0;
+    E.range = 510;
+    E.buffered = 0xff;
+    E.acc = 0;
+    E.bits_left = 23;
+    E.nbuf = 0;
+    E.opos = 0;
+    E.flushed = 0;
+    E.ob = 0;
+    const unsigned long long t0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    int entries = 0;
+    for (int idx = cy * f.mb_w; idx < (cy + 1) * f.mb_w; idx++) {
+        const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
+        const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
+        entries += nb;
+        uint32_t cur = l < nb ? b[l] : 0u;
+        for (int base = 0; base < nb; base += 64) {
+            const uint32_t nxt = base + 64 + l < nb ? b[base + 64 + l] : 0u;   // prefetch
+            const int m = nb - base < 64 ? nb - base : 64;
+            for (int i = 0; i < m; i++) E.code((uint32_t)__builtin_amdgcn_readlane((int)cur, i));
+            cur = nxt;
+        }
+    }
+    if (cy < t.first_row + t.num_rows - 1) E.code(CTX_TERM | (1u << 8));   // end_of_subset_one_bit
+    E.finish();
+    if (A.dbg && l == 0) {
+        A.dbg[4 * cy + 0] = __builtin_amdgcn_s_memtime() - t0;
+        A.dbg[4 * cy + 1] = (unsigned long long)entries;
+        A.dbg[4 * cy + 2] = (unsigned long long)(E.flushed + E.opos);
+    }
+    uint8_t* out = E.out;
+    const int size = E.flushed + E.opos;
+    if (l == 0) A.sub_size[cy] = size;
+    // emulation-prevention count (wave-parallel, same rule as k_hevc_ep_copy)
+    __syncthreads();
+    int last_nz = -1, ins_total = 0;
+    for (int base = 0; base < size; base += 64) {
+        const int i = base + l;
+        const int b = i < size ? out[i] : 1;
+        int p = b != 0 ? i : -1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int q = __shfl_up(p, d);
+            if (l >= d) p = max(p, q);
+        }
+        int prev_nz = __shfl_up(p, 1);
+        if (l == 0) prev_nz = -1;
+        prev_nz = max(prev_nz, last_nz);
+        const int z = i - 1 - prev_nz;
+        const int ins = (i < size && b <= 3 && z >= 2 && (z & 1) == 0) ? 1 : 0;
+        ins_total += wsum(ins);
+        last_nz = max(last_nz, __shfl(p, 63));
+    }
+    if (l == 0) A.sub_esc[cy] = size + ins_total;
+}
+
+// Slice header + NAL prefix per slice; substream offsets for k_hevc_ep_copy.
+__global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
+    __shared__ uint8_t hdr[1024];
+    __shared__ int esc[256];
+    const FrameArgs& f = A.f;
+    const int s = blockIdx.x;
+    const SliceTask t = f.tasks[s];
+    const int l = lane();
+    for (int i = l; i < 1024; i += 64) hdr[i] = 0;
+    for (int i = l; i < t.num_rows; i += 64) esc[i] = A.sub_esc[t.first_row + i];
+    bool idr = true;
+    for (int i = l; i < f.num_slices; i += 64) idr &= f.tasks[i].final_action == ACT_I && f.tasks[i].idr_on_intra;
+    idr = __syncthreads_and(idr);
+    if (l == 0) {
+        SliceHeader h;
+        h.first_slice = s == 0;
+        h.idr = idr;
+        h.address = t.first_row * f.mb_w;
+        h.address_bits = A.addr_bits;
+        h.slice_type = t.final_action == ACT_I ? 2 : 1;
+        h.poc_lsb = t.frame_num & ((1 << kLog2MaxPocLsb) - 1);
+        h.qp_delta = t.qp - 26;
+        h.num_entry = t.num_rows - 1;
+        h.entry = esc;
+        const int hn = write_slice_header(hdr, h);
+        const int hesc = ep_escape(hdr, hn, nullptr);
+        int total = 6 + hesc;
+        int off = total;
+        for (int r = 0; r < t.num_rows; r++) {
+            A.row_off[t.first_row + r] = off;
+            off += esc[r];
+        }
+        total = off;
+        const bool fits = total <= A.out_slot;
+        uint8_t* o = fits ? A.out_host + (size_t)s * A.out_slot : A.out_dev + (size_t)s * A.out_dev_slot;
+        o[0] = 0; o[1] = 0; o[2] = 0; o[3] = 1;
+        o[4] = (uint8_t)((idr ? kNalIdrWRadl : kNalTrailR) << 1);
+        o[5] = 1;
+        ep_escape(hdr, hn, o + 6);
+        __hip_atomic_store(A.out_size + s, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Emulation prevention + copy of one row's substream, wave-parallel: byte i of the
+// substream is preceded by an inserted 0x03 iff it is <= 3 and the zero run before it
+// has even length >= 2 (equivalent to the sequential rule; the previous piece ends in a
+// non-zero byte).
+__global__ __launch_bounds__(64) void k_hevc_ep_copy(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int cy = blockIdx.x;
+    const int s = cy / f.rows_per_slice;
+    const int total = __hip_atomic_load(A.out_size + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const bool fits = total <= A.out_slot;
+    uint8_t* o = (fits ? A.out_host + (size_t)s * A.out_slot : A.out_dev + (size_t)s * A.out_dev_slot) + A.row_off[cy];
+    const uint8_t* in = A.sub + (size_t)cy * A.sub_stride;
+    const int n = A.sub_size[cy];
+    const int l = lane();
+    int last_nz = -1;   // index of the last non-zero byte before the current chunk (-1: none yet,
+                        // the byte before the substream is non-zero)
+    int opos = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + l;
+        const int b = i < n ? in[i] : 1;
+        // inclusive max-scan of the positions of non-zero bytes
+        int p = b != 0 ? i : -1;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int q = __shfl_up(p, d);
+            if (l >= d) p = max(p, q);
+        }
+        int prev_nz = __shfl_up(p, 1);
+        if (l == 0) prev_nz = -1;
+        prev_nz = max(prev_nz, last_nz);
+        const int z = i - 1 - prev_nz;   // zeros immediately before byte i
+        const int ins = (i < n && b <= 3 && z >= 2 && (z & 1) == 0) ? 1 : 0;
+        int cnt = ins;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int q = __shfl_up(cnt, d);
+            if (l >= d) cnt += q;
+        }
+        if (i < n) {
+            const int at = i + opos + cnt;   // insertions before this chunk + up to this byte
+            if (ins) o[at - 1] = 3;
+            o[at] = (uint8_t)b;
+        }
+        opos += __shfl(cnt, 63);
+        last_nz = max(last_nz, __shfl(p, 63));
+    }
+}
+
+void launch_backend(const HevcArgs& a, hipStream_t s) {
+    const int n = a.f.mb_w * a.f.mb_h;
+    hipLaunchKernelGGL(k_hevc_inter, dim3((n + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_intra_prep, dim3((n + 3) / 4), dim3(256), 0, s, a);
+    if (a.f.rows_per_slice <= 4)
+        hipLaunchKernelGGL(k_hevc_intra<4>, dim3(a.f.num_slices), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_cabac, dim3(a.f.mb_h), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h), dim3(64), 0, s, a);
+}
+
+}  // namespace gpu
+}  // namespace hevc
+}  // namespace sk

@@ -8,6 +8,8 @@
 #include "encoder_iface.h"
 #include "trace.h"
 #include "../kernels/h264_gpu.h"
+#include "../kernels/hevc_gpu.h"
+#include "../codec/hevc_encoder.h"
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <map>
@@ -39,6 +41,7 @@ class HipBackend : public EncoderBackend {
         for (auto& e : ev_copy_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (cfg_.shared_copy) copy_stream_ = device_copy_stream(device_);
         alloc();
+        if (cfg_.codec == 1) alloc_hevc();
     }
     ~HipBackend() override {
         hipSetDevice(device_);
@@ -288,6 +291,10 @@ class HipBackend : public EncoderBackend {
         else if (s == "ref1_y") { p = args_.ref1.y; n = (int64_t)ny; }
         else if (s == "fs_mv") { p = args_.fs_mv; n = (int64_t)g_.num_mbs() * 4; }
         else if (s == "mbs") { p = args_.mbs; n = (int64_t)g_.num_mbs() * sizeof(MbInfo); }
+        else if (s == "coefs" && cfg_.codec == 1) { p = hargs_.coefs; n = (int64_t)g_.num_mbs() * hevc::kCoefPerCu * 2; }
+        else if (s == "cus" && cfg_.codec == 1) { p = hargs_.cus; n = (int64_t)g_.num_mbs() * sizeof(hevc::CuInfo); }
+        else if (s == "bin_n" && cfg_.codec == 1) { p = hargs_.bin_n; n = (int64_t)g_.num_mbs() * 4; }
+        else if (s == "hevc_stamps" && cfg_.codec == 1) { if (!hargs_.dbg) return -1; p = hargs_.dbg; n = (int64_t)g_.mb_h * 32; }
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
         else if (s == "me") { p = args_.me; n = (int64_t)g_.num_mbs() * sizeof(MeResult); }
         else if (s == "mb_dirty") { p = args_.mb_dirty; n = g_.num_mbs(); }
@@ -466,7 +473,17 @@ class HipBackend : public EncoderBackend {
     void enqueue(int part) {
         if (part == 0) {
             gpu::launch_convert_damage(args_, stream_);
-            gpu::launch_encode(args_, stream_);
+            if (cfg_.codec == 1) {
+                gpu::launch_frontend(args_, stream_);
+                hevc::gpu::HevcArgs ha = hargs_;
+                ha.f = args_;
+                ha.out_host = hevc_out_dev_[parity_];
+                ha.out_size = hevc_size_dev_[parity_];
+                ha.out_dev = hevc_fallback_[parity_];
+                hevc::gpu::launch_backend(ha, stream_);
+            } else {
+                gpu::launch_encode(args_, stream_);
+            }
         } else {
             gpu::launch_commit(args_, stream_);
         }
@@ -488,7 +505,73 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipGraphLaunch(gx, stream_));
     }
 
+    // HEVC back-end buffers (hevc_gpu.h): CU decisions, levels, bin slots, WPP states,
+    // one substream slot per CTB row, host-mapped slice slots + device fallback.
+    void alloc_hevc() {
+        const int n = g_.num_mbs(), ns = g_.num_slices;
+        hevc::Geo geo;
+        geo.init(g_);
+        hevc::gpu::HevcArgs& h = hargs_;
+        memset(&h, 0, sizeof(h));
+        h.cus = dmalloc<hevc::CuInfo>(n);
+        h.coefs = dmalloc<int16_t>((size_t)n * hevc::kCoefPerCu);
+        h.bins = dmalloc<uint16_t>((size_t)n * hevc::kCuBinCap, false);
+        h.bin_n = dmalloc<int>(n);
+        h.sync = dmalloc<uint8_t>((size_t)g_.mb_h * hevc::CTX_COUNT);
+        h.sub_stride = g_.mb_w * hevc::kSubstreamCtbBytes + 64;
+        h.sub = dmalloc<uint8_t>((size_t)g_.mb_h * h.sub_stride, false);
+        h.sub_size = dmalloc<int>(g_.mb_h);
+        h.sub_esc = dmalloc<int>(g_.mb_h);
+        h.row_off = dmalloc<int>(g_.mb_h);
+        h.addr_bits = geo.addr_bits;
+        // host slot: 1.5 KB per CTB (far above practical rates); larger slices go to the
+        // device fallback slot (worst case: 3/2 emulation growth of the substream bound)
+        h.out_slot = (g_.rows_per_slice * g_.mb_w * 1536 + 4096 + 63) & ~63;
+        h.out_dev_slot = (int)(((size_t)g_.rows_per_slice * h.sub_stride * 3 / 2 + 4096 + 63) & ~(size_t)63);
+        void* dptr = nullptr;
+        for (int p = 0; p < 2; p++) {
+            hevc_out_[p] = hmalloc<uint8_t>((size_t)h.out_slot * ns);
+            hevc_size_[p] = hmalloc<int>(ns, hipHostMallocCoherent);
+            HIPCHECK(hipHostGetDevicePointer(&dptr, hevc_out_[p], 0));
+            hevc_out_dev_[p] = (uint8_t*)dptr;
+            HIPCHECK(hipHostGetDevicePointer(&dptr, hevc_size_[p], 0));
+            hevc_size_dev_[p] = (int*)dptr;
+            hevc_fallback_[p] = dmalloc<uint8_t>((size_t)h.out_dev_slot * ns, false);
+        }
+        HIPCHECK(hipStreamSynchronize(stream_));
+        if (getenv("SK_STAMPS")) h.dbg = dmalloc<unsigned long long>((size_t)4 * g_.mb_h);
+        hevc_params_.clear();
+        hevc::build_parameter_sets(g_.W, g_.H, cfg_.full_range, cfg_.fps, hevc_params_);
+    }
+
+    void build_packets_hevc(int par, uint16_t frame_id) {
+        const SliceTask* h_tasks = h_tasks_[par];
+        const int ns = g_.num_slices;
+        const bool idr = ctl_.picture_is_idr(h_tasks);
+        EncodedPacket pk;
+        pk.y = 0; pk.w = g_.W; pk.h = g_.H; pk.key = idr;
+        pk.data.resize(10);
+        write_stripe_header(pk.data.data(), idr, frame_id, 0, g_.W, g_.H);
+        if (idr) pk.data.insert(pk.data.end(), hevc_params_.begin(), hevc_params_.end());
+        for (int s = 0; s < ns; s++) {
+            const int n = hevc_size_[par][s];
+            const size_t o = pk.data.size();
+            pk.data.resize(o + (size_t)n);
+            if (n <= hargs_.out_slot) {
+                memcpy(pk.data.data() + o, hevc_out_[par] + (size_t)s * hargs_.out_slot, (size_t)n);
+            } else {   // rare: the slice did not fit its host slot
+                HIPCHECK(hipMemcpy(pk.data.data() + o, hevc_fallback_[par] + (size_t)s * hargs_.out_dev_slot,
+                                   (size_t)n, hipMemcpyDeviceToHost));
+            }
+        }
+        packets_.push_back(std::move(pk));
+    }
+
     void build_packets(int par, uint16_t frame_id) {
+        if (cfg_.codec == 1) {
+            build_packets_hevc(par, frame_id);
+            return;
+        }
         const uint8_t* host_out = host_out_[par];
         const int* h_out_size = h_out_size_[par];
         const SliceTask* h_tasks = h_tasks_[par];
@@ -526,6 +609,13 @@ class HipBackend : public EncoderBackend {
     Geometry g_;
     Controller ctl_;
     int device_;
+    hevc::gpu::HevcArgs hargs_;
+    uint8_t* hevc_out_[2] = {nullptr, nullptr};
+    uint8_t* hevc_out_dev_[2] = {nullptr, nullptr};
+    int* hevc_size_[2] = {nullptr, nullptr};
+    int* hevc_size_dev_[2] = {nullptr, nullptr};
+    uint8_t* hevc_fallback_[2] = {nullptr, nullptr};
+    std::vector<uint8_t> hevc_params_;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[6];   // per parity p: [3p] upload, [3p+1] graph start, [3p+2] packets done
     gpu::FrameArgs args_;

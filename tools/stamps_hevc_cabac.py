@@ -1,0 +1,18 @@
+"""Diagnostic: cycles and bin entries per CTB row of k_hevc_cabac (SK_STAMPS=1)."""
+import os, sys
+import numpy as np
+os.environ["SK_STAMPS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from selkies_gstreamer_amd.ops.native import HevcEncoder
+from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
+W, H = int(sys.argv[1]) if len(sys.argv) > 1 else 3840, int(sys.argv[2]) if len(sys.argv) > 2 else 2160
+src = SyntheticDesktop(W, H, "motion")
+enc = HevcEncoder(W, H, backend="hip")
+for t in range(3):
+    enc.encode(src.frame(t), t)
+st = np.frombuffer(enc.debug_buffer("hevc_stamps", np.uint8), np.uint64).reshape(-1, 4).astype(np.int64)
+bn = np.frombuffer(enc.debug_buffer("bin_n", np.uint8), np.int32)
+print("rows", len(st), "median cycles/row", np.median(st[:, 0]), "median entries/row", np.median(st[:, 1]),
+      "median bytes/row", np.median(st[:, 2]))
+print("cycles per entry (median over rows):", np.median(st[:, 0] / np.maximum(st[:, 1], 1)))
+print("total entries", bn.sum(), "max per CU", bn.max())
