@@ -692,6 +692,71 @@ int rtc_h264_packetize(void* srtp, const uint8_t* annexb, int n, rtc_rtp_params*
     return w.failed ? -1 : w.count;
 }
 
+// H.265 RFC 7798 packetisation: single NAL unit packets, aggregation packets (AP,
+// type 48) for runs of small NAL units (parameter sets), fragmentation units (FU,
+// type 49) for NAL units larger than the MTU. The 2-byte payload headers keep the
+// NAL's F bit, layer id and temporal id (AP: F = OR, layer / TID = minimum).
+int rtc_h265_packetize(void* srtp, const uint8_t* annexb, int n, rtc_rtp_params* p, uint8_t* out, int cap,
+                       int* lens, int max_pkts) {
+    PacketWriter w{static_cast<Srtp*>(srtp), p, out, cap, 0, 0, lens, max_pkts};
+    const int maxp = p->mtu - 12;
+    if (maxp < 64) return -1;
+    std::vector<Nal> nals = split_annexb(annexb, n);
+    const size_t nn = nals.size();
+    for (size_t i = 0; i < nn;) {
+        if (nals[i].n < 3) { i++; continue; }
+        size_t j = i;
+        int agg = 2;
+        while (j < nn && nals[j].n >= 3 && agg + 2 + nals[j].n <= maxp) agg += 2 + nals[j++].n;
+        if (j - i >= 2) {
+            uint8_t* pl = w.begin(agg);
+            if (!pl) return -1;
+            int f = 0, layer = 63, tid = 7;
+            int o = 2;
+            for (size_t k = i; k < j; k++) {
+                const uint8_t* h = nals[k].p;
+                f |= h[0] & 0x80;
+                const int ly = ((h[0] & 1) << 5) | (h[1] >> 3), t = h[1] & 7;
+                layer = ly < layer ? ly : layer;
+                tid = t < tid ? t : tid;
+                pl[o] = nals[k].n >> 8;
+                pl[o + 1] = nals[k].n & 0xff;
+                memcpy(pl + o + 2, nals[k].p, nals[k].n);
+                o += 2 + nals[k].n;
+            }
+            pl[0] = (uint8_t)(f | (48 << 1) | (layer >> 5));
+            pl[1] = (uint8_t)(((layer & 31) << 3) | tid);
+            w.end(agg, j == nn);
+            i = j;
+            continue;
+        }
+        const Nal& nal = nals[i];
+        if (nal.n <= maxp) {
+            uint8_t* pl = w.begin(nal.n);
+            if (!pl) return -1;
+            memcpy(pl, nal.p, nal.n);
+            w.end(nal.n, i + 1 == nn);
+        } else {
+            const uint8_t h0 = nal.p[0], h1 = nal.p[1];
+            const int type = (h0 >> 1) & 63;
+            const int chunk = maxp - 3;
+            for (int off = 2; off < nal.n; off += chunk) {
+                const int len = nal.n - off < chunk ? nal.n - off : chunk;
+                uint8_t* pl = w.begin(len + 3);
+                if (!pl) return -1;
+                const bool first = off == 2, last = off + len >= nal.n;
+                pl[0] = (uint8_t)((h0 & 0x81) | (49 << 1));
+                pl[1] = h1;
+                pl[2] = (uint8_t)((first ? 0x80 : 0) | (last ? 0x40 : 0) | type);
+                memcpy(pl + 3, nal.p + off, len);
+                w.end(len + 3, last && i + 1 == nn);
+            }
+        }
+        i++;
+    }
+    return w.failed ? -1 : w.count;
+}
+
 int rtc_rtp_packet(void* srtp, const uint8_t* payload, int n, rtc_rtp_params* p, uint8_t* out, int cap) {
     int len = 0;
     PacketWriter w{static_cast<Srtp*>(srtp), p, out, cap, 0, 0, &len, 1};

@@ -17,14 +17,16 @@ Mapping:
   ``vapostproc``, ``hipupload``, ``hipconvert``, ``queue``) → fused into the HIP
   convert kernel (scaling is not: caps must keep the capture size);
 * H.264 encoders (``x264enc``, ``nvh264enc``, ``vah264enc``, ``openh264enc``,
-  ``qsvh264enc``, ``hiph264enc``) → the gfx950 H.264 encoder: ``bitrate`` (kbit/s),
+  ``qsvh264enc``, ``hiph264enc``) → the gfx950 H.264 encoder, H.265 encoders (``x265enc``,
+  ``nvh265enc``, ``vah265enc``, ``qsvh265enc``, ``hiph265enc``) → the gfx950 HEVC encoder:
+  ``bitrate`` (kbit/s),
   ``key-int-max`` / ``gop-size`` / ``keyframe-period``, ``quantizer`` / ``qp-const``;
   ``jpegenc`` → the JPEG stripe encoder;
-* payloader ``rtph264pay`` (``mtu``), ``webrtcbin`` (``stun-server``, ``latency``);
+* payloaders ``rtph264pay`` / ``rtph265pay`` (``mtu``), ``webrtcbin`` (``stun-server``, ``latency``);
 * audio ``pulsesrc`` (``device``) → ``opusenc`` (``bitrate``, ``frame-size``) →
   ``rtpopuspay``.
-H.265 / VP8 / VP9 / AV1 encoder elements are rejected with an explicit error:
-this build's video codecs are H.264 and JPEG.
+VP8 / VP9 / AV1 encoder elements are rejected with an explicit error: this build's
+video codecs are H.264, H.265 and JPEG.
 """
 from __future__ import annotations
 
@@ -34,8 +36,10 @@ from typing import Optional
 
 H264_ENCODERS = {"x264enc", "nvh264enc", "vah264enc", "vah264lpenc", "openh264enc", "qsvh264enc", "hiph264enc",
                  "nvcudah264enc", "nvautogpuh264enc"}
-UNSUPPORTED_ENCODERS = {"x265enc", "nvh265enc", "vah265enc", "qsvh265enc", "vp8enc", "vp9enc", "vavp9enc",
-                        "av1enc", "svtav1enc", "rav1enc", "nvav1enc", "vaav1enc", "qsvav1enc"}
+H265_ENCODERS = {"x265enc", "nvh265enc", "vah265enc", "vah265lpenc", "qsvh265enc", "hiph265enc", "nvcudah265enc",
+                 "nvautogpuh265enc"}
+UNSUPPORTED_ENCODERS = {"vp8enc", "vp9enc", "vavp9enc", "av1enc", "svtav1enc", "rav1enc", "nvav1enc", "vaav1enc",
+                        "qsvav1enc"}
 PASSTHROUGH = {"videoconvert", "cudaupload", "cudaconvert", "cudadownload", "vapostproc", "hipupload",
                "hipconvert", "queue", "videorate", "capsfilter", "identity", "audioconvert", "audioresample",
                "tee", "fakesink"}
@@ -60,7 +64,7 @@ class PipelineSpec:
     width: Optional[int] = None
     height: Optional[int] = None
     framerate: Optional[float] = None
-    encoder: Optional[str] = None       # "h264" | "jpeg"
+    encoder: Optional[str] = None       # "h264" | "h265" | "jpeg"
     encoder_element: Optional[str] = None
     bitrate_kbps: Optional[int] = None
     keyframe_distance: Optional[int] = None
@@ -166,8 +170,8 @@ def parse_pipeline(text: str) -> PipelineSpec:
             spec.height = p.get("height", spec.height)
             if "framerate" in p:
                 spec.framerate = float(p["framerate"])
-        elif n in H264_ENCODERS:
-            spec.encoder, spec.encoder_element = "h264", n
+        elif n in H264_ENCODERS or n in H265_ENCODERS:
+            spec.encoder, spec.encoder_element = ("h265" if n in H265_ENCODERS else "h264"), n
             if "bitrate" in p:
                 spec.bitrate_kbps = int(p["bitrate"])
             for k in ("key-int-max", "gop-size", "keyframe-period", "idr-period"):
@@ -179,8 +183,9 @@ def parse_pipeline(text: str) -> PipelineSpec:
         elif n == "jpegenc":
             spec.encoder, spec.encoder_element = "jpeg", n
         elif n in UNSUPPORTED_ENCODERS:
-            raise PipelineError(f"{n}: this build encodes H.264 (HIP) and JPEG; use an H.264 encoder element")
-        elif n in ("rtph264pay", "rtpopuspay"):
+            raise PipelineError(f"{n}: this build encodes H.264 / H.265 (HIP) and JPEG; use an H.264 or H.265 "
+                                "encoder element")
+        elif n in ("rtph264pay", "rtph265pay", "rtpopuspay"):
             if "mtu" in p:
                 spec.mtu = int(p["mtu"])
         elif n == "webrtcbin":

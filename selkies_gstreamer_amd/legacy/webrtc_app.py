@@ -74,7 +74,8 @@ FLAGS = [
     ("app_ready_file", "SELKIES_APP_READY_FILE", "/tmp/selkies-appready", "app-ready marker file"),
     ("uinput_mouse_socket", "SELKIES_UINPUT_MOUSE_SOCKET", "", "uinput mouse socket path"),
     ("js_socket_path", "SELKIES_JS_SOCKET_PATH", "/tmp", "joystick interposer socket directory"),
-    ("encoder", "SELKIES_ENCODER", "x264enc", "video encoder (every H.264 name maps to the HIP encoder)"),
+    ("encoder", "SELKIES_ENCODER", "x264enc",
+     "video encoder (H.264 names map to the HIP H.264 encoder, x265enc/nvh265enc/vah265enc to HIP HEVC)"),
     ("gpu_id", "SELKIES_GPU_ID", "0", "GPU ordinal"),
     ("framerate", "SELKIES_FRAMERATE", "60", "frames per second"),
     ("video_bitrate", "SELKIES_VIDEO_BITRATE", "8000", "video bitrate (kbit/s)"),
@@ -169,10 +170,13 @@ class StreamSession:
 
     def __init__(self, args, send_sdp, send_ice, input_factory=None, addresses=None):
         self.args = args
+        from selkies_gstreamer_amd.legacy.pipeline import H265_ENCODERS
+        self.hevc = str(getattr(args, "encoder", "")) in H265_ENCODERS
         self.send_sdp, self.send_ice = send_sdp, send_ice
         self.fps = int(args.framerate)
         self.rc = RateController(int(args.video_bitrate) * 1000, self.fps)
-        self.pc = PeerConnection(addresses=addresses, video=True, audio=True, data=True)
+        self.pc = PeerConnection(addresses=addresses, video=True, audio=True, data=True,
+                                 video_codec="H265" if self.hevc else "H264")
         self.channel = None
         self.capture = None
         self.audio = None
@@ -232,6 +236,8 @@ class StreamSession:
         src = {"x11": 0, "synthetic": 2}.get(self.args.capture_source, -1)
         w, h = self.width, self.height
         s = pixelflux.default_settings(w, h, target_fps=float(self.fps), h264_fullframe=1,
+                                       output_mode=pixelflux.OUTPUT_MODE_HEVC if self.hevc else
+                                       pixelflux.OUTPUT_MODE_H264,
                                        h264_crf=self.rc.qp, h264_paintover_crf=self.rc.paint_qp,
                                        use_cpu=1 if _truthy(self.args.use_cpu) else 0, source=src,
                                        device=int(self.args.gpu_id), stripe_height=64,

@@ -46,6 +46,8 @@ def lib():
             "rtc_srtp_session_keys": (None, [vp, ctypes.c_void_p]),
             "rtc_h264_packetize": (i32, [vp, u8p, i32, ctypes.POINTER(RtpParams), ctypes.c_void_p, i32,
                                          ctypes.POINTER(ctypes.c_int), i32]),
+            "rtc_h265_packetize": (i32, [vp, u8p, i32, ctypes.POINTER(RtpParams), ctypes.c_void_p, i32,
+                                         ctypes.POINTER(ctypes.c_int), i32]),
             "rtc_rtp_packet": (i32, [vp, u8p, i32, ctypes.POINTER(RtpParams), ctypes.c_void_p, i32]),
             "rtc_crc32c": (ctypes.c_uint32, [u8p, i32]),
         }
@@ -219,6 +221,25 @@ class RtpPacketizer:
         n = self._L.rtc_h264_packetize(srtp.handle if srtp else None, annexb, len(annexb),
                                        ctypes.byref(self.params), self._out, len(self._out), self._lens,
                                        len(self._lens))
+        if n < 0:
+            raise ValueError("access unit too large for the packetiser buffers")
+        out, off, raw = [], 0, self._out.raw
+        for i in range(n):
+            out.append(raw[off:off + self._lens[i]])
+            off += self._lens[i]
+        return out
+
+    def h265(self, annexb: bytes, timestamp: int, srtp: Srtp | None = None) -> list[bytes]:
+        """RFC 7798 payloads (single NAL / aggregation / fragmentation units) of one access unit."""
+        return self._packetize(self._L.rtc_h265_packetize, annexb, timestamp, srtp)
+
+    def _packetize(self, fn, annexb: bytes, timestamp: int, srtp: Srtp | None) -> list[bytes]:
+        self.params.timestamp = timestamp & 0xFFFFFFFF
+        need = len(annexb) + 64 * (len(annexb) // 1000 + 8)
+        if need > len(self._out):
+            self._out = ctypes.create_string_buffer(need * 2)
+        n = fn(srtp.handle if srtp else None, annexb, len(annexb), ctypes.byref(self.params), self._out,
+               len(self._out), self._lens, len(self._lens))
         if n < 0:
             raise ValueError("access unit too large for the packetiser buffers")
         out, off, raw = [], 0, self._out.raw

@@ -38,7 +38,7 @@ HISTORY = 2048
 class PeerConnection:
     def __init__(self, *, ice_lite: bool = False, addresses: Optional[list[str]] = None, port: int = 0,
                  stun_server: Optional[tuple] = None, video: bool = True, audio: bool = True, data: bool = True,
-                 mtu: int = 1200):
+                 mtu: int = 1200, video_codec: str = "H264"):
         self.ice_lite = ice_lite
         self._ice_args = dict(addresses=addresses, port=port, stun_server=stun_server)
         self.want = dict(video=video, audio=audio, data=data)
@@ -55,7 +55,9 @@ class PeerConnection:
         self.state = "new"
         self.video_ssrc = random.getrandbits(32) or 1
         self.audio_ssrc = random.getrandbits(32) or 2
-        self._vpk = RtpPacketizer(self.video_ssrc, sdp.H264_PT, mtu - 10, random.getrandbits(16))
+        self.video_codec = "H265" if video_codec.upper() in ("H265", "HEVC") else "H264"
+        self._vpt = sdp.H265_PT if self.video_codec == "H265" else sdp.H264_PT
+        self._vpk = RtpPacketizer(self.video_ssrc, self._vpt, mtu - 10, random.getrandbits(16))
         self._apk = RtpPacketizer(self.audio_ssrc, sdp.OPUS_PT, mtu - 10, random.getrandbits(16))
         self._history: dict[int, bytes] = {}
         self._sent = {"video_packets": 0, "video_bytes": 0, "audio_packets": 0, "audio_bytes": 0,
@@ -66,7 +68,7 @@ class PeerConnection:
         self._tasks: list = []
         self._pending_channels: list = []
         # receive side
-        self._depack: dict[int, rtp.H264Depacketizer] = {}
+        self._depack: dict = {}   # ssrc -> H264Depacketizer / H265Depacketizer
         self._jitter: dict[int, JitterBuffer] = {}
         self._rx_rate: dict[int, RemoteBitrateEstimator] = {}
         self.remb_sent_bps: Optional[int] = None
@@ -99,7 +101,7 @@ class PeerConnection:
         self.dtls = Dtls("server")   # actpass: the answerer normally picks active
         self.local_sdp = sdp.build_offer(self.ice.local_ufrag, self.ice.local_pwd, self.dtls.fingerprint,
                                          self.ice.local_candidates, self.video_ssrc, self.audio_ssrc,
-                                         ice_lite=self.ice_lite, **self.want)
+                                         ice_lite=self.ice_lite, video_codec=self.video_codec, **self.want)
         return self.local_sdp.to_string()
 
     async def set_remote_description(self, text: str, kind: str) -> None:
@@ -253,10 +255,10 @@ class PeerConnection:
 
     # -- media send -------------------------------------------------------------------------------
     def send_video(self, annexb: bytes, timestamp: int) -> int:
-        """Sends one H.264 access unit (Annex-B) with a 90 kHz timestamp."""
+        """Sends one H.264 or H.265 access unit (Annex-B) with a 90 kHz timestamp."""
         if self.srtp_tx is None:
             return 0
-        pkts = self._vpk.h264(annexb, timestamp, self.srtp_tx)
+        pkts = (self._vpk.h265 if self.video_codec == "H265" else self._vpk.h264)(annexb, timestamp, self.srtp_tx)
         for p in pkts:
             self.ice.send(p)
             self._history[struct.unpack_from("!H", p, 2)[0]] = p
@@ -334,7 +336,7 @@ class PeerConnection:
         if exp is None or 0 <= ((h.seq - exp) & 0xFFFF) < 0x8000:
             self._rx_seq[h.ssrc] = (h.seq + 1) & 0xFFFF
         payload = data[h.header_len:]
-        if h.payload_type == sdp.H264_PT:
+        if h.payload_type in (sdp.H264_PT, sdp.H265_PT):
             now_ms = time.monotonic() * 1000.0
             est = self._rx_rate.setdefault(h.ssrc, RemoteBitrateEstimator())
             r = est.add(now_ms, h.timestamp / 90.0, len(data))
@@ -345,7 +347,8 @@ class PeerConnection:
             pli, frames = jb.add(JbPacket(h.seq, h.timestamp, h.marker, payload))
             if pli:
                 self.request_keyframe(h.ssrc)
-            d = self._depack.setdefault(h.ssrc, rtp.H264Depacketizer())
+            d = self._depack.setdefault(h.ssrc, rtp.H265Depacketizer() if h.payload_type == sdp.H265_PT
+                                        else rtp.H264Depacketizer())
             for fr in frames:
                 au = None
                 for i, pk in enumerate(fr.packets):

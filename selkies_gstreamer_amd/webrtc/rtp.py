@@ -192,3 +192,42 @@ class H264Depacketizer:
             self._au = []
             return au
         return None
+
+
+class H265Depacketizer:
+    """Reassembles RFC 7798 packets (single NAL, AP type 48, FU type 49) into Annex-B access units."""
+
+    def __init__(self):
+        self._au: list = []
+        self._fu: bytearray | None = None
+        self._ts = None
+
+    def push(self, payload: bytes, timestamp: int, marker: bool) -> bytes | None:
+        if self._ts is not None and timestamp != self._ts and self._au:
+            self._au, self._fu = [], None
+        self._ts = timestamp
+        if len(payload) < 3:
+            return None
+        t = (payload[0] >> 1) & 63
+        if t == 48:
+            pos = 2
+            while pos + 2 <= len(payload):
+                n = struct.unpack_from("!H", payload, pos)[0]
+                self._au.append(payload[pos + 2:pos + 2 + n])
+                pos += 2 + n
+        elif t == 49:
+            fu = payload[2]
+            if fu & 0x80:
+                self._fu = bytearray([(payload[0] & 0x81) | ((fu & 63) << 1), payload[1]])
+            if self._fu is not None:
+                self._fu += payload[3:]
+                if fu & 0x40:
+                    self._au.append(bytes(self._fu))
+                    self._fu = None
+        else:
+            self._au.append(payload)
+        if marker:
+            au = b"".join(b"\x00\x00\x00\x01" + n for n in self._au)
+            self._au = []
+            return au
+        return None

@@ -16,6 +16,7 @@ from typing import Optional
 from .ice import Candidate
 
 H264_PT = 97
+H265_PT = 100   # reference: rtph265pay pt=100 (legacy/gstwebrtc_app.py:848-866)
 OPUS_PT = 111
 SCTP_PORT = 5000
 
@@ -204,17 +205,26 @@ def h264_fmtp(profile_level_id: str = "42e01f") -> str:
     return f"level-asymmetry-allowed=1;packetization-mode=1;profile-level-id={profile_level_id}"
 
 
+def h265_fmtp(level_id: int = 153) -> str:
+    return f"level-id={level_id};profile-id=1;tier-flag=0;tx-mode=SRST"
+
+
 def build_offer(ufrag: str, pwd: str, fingerprint: str, candidates: list, video_ssrc: int, audio_ssrc: int,
                 video: bool = True, audio: bool = True, data: bool = True, cname: str = "selkies",
-                ice_lite: bool = False, profile_level_id: str = "42e01f") -> SessionDescription:
+                ice_lite: bool = False, profile_level_id: str = "42e01f",
+                video_codec: str = "H264") -> SessionDescription:
     sd = SessionDescription(session_id=int(time.time() * 1000), ice_lite=ice_lite)
     common = dict(ice_ufrag=ufrag, ice_pwd=pwd, fingerprint=f"sha-256 {fingerprint}", setup="actpass",
                   candidates=list(candidates), end_of_candidates=True)
     if video:
+        if video_codec.upper() in ("H265", "HEVC"):
+            pt, rtpmap, fmtp = H265_PT, "H265/90000", h265_fmtp()
+        else:
+            pt, rtpmap, fmtp = H264_PT, "H264/90000", h264_fmtp(profile_level_id)
         sd.media.append(Media(
-            "video", fmts=[H264_PT], mid=str(len(sd.media)), direction="sendonly", rtcp_mux=True,
-            rtpmap={H264_PT: "H264/90000"}, fmtp={H264_PT: h264_fmtp(profile_level_id)},
-            rtcp_fb={H264_PT: ["nack", "nack pli", "ccm fir", "goog-remb"]}, ssrc=video_ssrc, cname=cname,
+            "video", fmts=[pt], mid=str(len(sd.media)), direction="sendonly", rtcp_mux=True,
+            rtpmap={pt: rtpmap}, fmtp={pt: fmtp},
+            rtcp_fb={pt: ["nack", "nack pli", "ccm fir", "goog-remb"]}, ssrc=video_ssrc, cname=cname,
             msid="selkies video0", **common))
     if audio:
         sd.media.append(Media(

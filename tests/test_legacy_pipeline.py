@@ -39,7 +39,7 @@ def test_audio_branch_and_region():
     assert a.audio and a.audio_device == "output.monitor" and a.audio_bitrate == 128000 and a.audio_frame_ms == 10
 
 
-@pytest.mark.parametrize("enc", ["vp8enc", "x265enc", "svtav1enc", "nvav1enc"])
+@pytest.mark.parametrize("enc", ["vp8enc", "vp9enc", "svtav1enc", "nvav1enc"])
 def test_unsupported_codecs_are_explicit(enc):
     with pytest.raises(PipelineError, match="H.264"):
         parse_pipeline(f"ximagesrc ! videoconvert ! {enc} ! fakesink")
