@@ -253,6 +253,7 @@ class CaptureSession {
             r.size = (int32_t)p.data.size();
             r.data = p.data.data();
             r.frame_id = f.id;
+            r.grab_ns = (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(f.t_grab.time_since_epoch()).count();
             bytes += p.data.size();
         }
         if (frame_cb_) frame_cb_(res.data(), n, frame_user_);   // one call per frame

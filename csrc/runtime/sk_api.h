@@ -104,6 +104,7 @@ typedef struct sk_stripe_result {
     int32_t size;
     uint8_t* data;
     int32_t frame_id;
+    int64_t grab_ns;         // extension: CLOCK_MONOTONIC time the frame was grabbed (latency tracing)
 } sk_stripe_result;
 
 typedef void (*sk_stripe_cb)(sk_stripe_result*, void*);

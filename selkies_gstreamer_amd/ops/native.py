@@ -69,7 +69,8 @@ class SkCaptureSettings(ctypes.Structure):
 
 class SkStripeResult(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("stripe_y_start", ctypes.c_int32), ("stripe_height", ctypes.c_int32),
-                ("size", ctypes.c_int32), ("data", ctypes.POINTER(ctypes.c_ubyte)), ("frame_id", ctypes.c_int32)]
+                ("size", ctypes.c_int32), ("data", ctypes.POINTER(ctypes.c_ubyte)), ("frame_id", ctypes.c_int32),
+                ("grab_ns", ctypes.c_int64)]
 
 
 SK_STRIPE_CB = ctypes.CFUNCTYPE(None, ctypes.POINTER(SkStripeResult), ctypes.c_void_p)

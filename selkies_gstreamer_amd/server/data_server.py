@@ -180,9 +180,10 @@ class DataStreamingServer:
     def __init__(self, settings: Settings, *, upload_dir: Optional[str] = None, input_factory=None,
                  capture_factory: Optional[Callable[[], Any]] = None, display_manager=None,
                  capture_source: str = "auto", gpu_id: int = 0, num_gpus: int = 1, clock=time.monotonic,
-                 web_root: Optional[str] = None, metrics=None):
+                 web_root: Optional[str] = None, metrics=None, frame_trace: Optional[bool] = None):
         self.settings = settings
         self.clock = clock
+        self.frame_trace = (os.environ.get("SELKIES_FRAME_TRACE") == "1") if frame_trace is None else frame_trace
         self.mode = "websockets"
         self.clients: set[Client] = set()
         self.displays: "OrderedDict[str, DisplayState]" = OrderedDict()
@@ -693,6 +694,7 @@ class DataStreamingServer:
             msgs = []
             key = False
             fid = 0
+            grab = 0
             for i in range(n):
                 r = res_ptr[i]
                 if r.size <= 0:
@@ -700,9 +702,10 @@ class DataStreamingServer:
                 data = ctypes.string_at(r.data, r.size)
                 key = key or (not jpeg and r.size > 1 and data[1] == 1)
                 fid = r.frame_id & 0xFFFF
+                grab = r.grab_ns
                 msgs.append(protocol.JPEG_PREFIX + data if jpeg else data)
             if msgs:
-                loop.call_soon_threadsafe(_put_drop, queue, (msgs, key, fid))
+                loop.call_soon_threadsafe(_put_drop, queue, (msgs, key, fid, grab))
 
         def on_stripe(res_ptr, user):   # capture modules without a per-frame callback
             r = res_ptr.contents
@@ -710,7 +713,7 @@ class DataStreamingServer:
                 return
             data = ctypes.string_at(r.data, r.size)
             key = not jpeg and r.size > 1 and data[1] == 1
-            item = ([protocol.JPEG_PREFIX + data if jpeg else data], key, r.frame_id & 0xFFFF)
+            item = ([protocol.JPEG_PREFIX + data if jpeg else data], key, r.frame_id & 0xFFFF, r.grab_ns)
             loop.call_soon_threadsafe(_put_drop, queue, item)
 
         import pixelflux
@@ -759,7 +762,7 @@ class DataStreamingServer:
         was_enabled = True
         jpeg = None
         while True:
-            msgs, key, fid = await queue.get()
+            msgs, key, fid, grab_ns = await queue.get()
             st = self.displays.get(did)
             if st is None:
                 continue
@@ -775,6 +778,12 @@ class DataStreamingServer:
             st.flow.on_sent(fid, self.clock())
             viewers = self.primary_viewers() if did == "primary" else {st.client}
             jpeg = msgs[0][:2] == protocol.JPEG_PREFIX
+            if self.frame_trace:
+                # latency tracing (SELKIES_FRAME_TRACE=1): the frame's grab time (CLOCK_MONOTONIC ns)
+                # ahead of its stripes, so a client on the same host measures capture -> receive
+                trace = f"FRAME_TS {fid} {grab_ns}"
+                for c in list(viewers):
+                    c.send(trace)
             for c in list(viewers):
                 c.send_video(msgs, key, independent=jpeg)
 

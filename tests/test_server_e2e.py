@@ -8,6 +8,7 @@ The GPU twin of this test lives in test_server_gpu.py.
 import asyncio
 import json
 import os
+import time
 
 import aiohttp
 import numpy as np
@@ -170,6 +171,29 @@ def test_second_screen_refused_when_disabled(tmp_path):
             kill, _ = await _recv_until(ws, lambda m: isinstance(m, str) and m.startswith("KILL"))
             assert "disabled" in kill
             await ws.close()
+        await srv.stop()
+    run(main())
+
+
+def test_frame_trace_timestamps(tmp_path):
+    """SELKIES_FRAME_TRACE: every frame's stripes are preceded by FRAME_TS <fid>
+    <grab_ns>, a CLOCK_MONOTONIC grab time (tools/bench_e2e.py latency source)."""
+    async def main():
+        s = Settings(["--port", "0", "--use-cpu", "true", "--audio-enabled", "false"], env={})
+        srv = DataStreamingServer(s, upload_dir=str(tmp_path / "up"), capture_source="synthetic", frame_trace=True)
+        port = await srv.start("127.0.0.1", 0)
+        async with aiohttp.ClientSession() as sess:
+            async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket") as ws:
+                await ws.send_str(_settings())
+                ts = {}
+                while len(ts) < 3:
+                    m, _ = await _recv_until(ws, lambda m: isinstance(m, str) and m.startswith("FRAME_TS"))
+                    _, fid, g = m.split()
+                    ts[int(fid)] = int(g)
+                    data, _ = await _recv_until(ws, lambda m: isinstance(m, bytes))
+                    now = time.monotonic_ns()
+                    assert int.from_bytes(data[2:4], "big") == int(fid)
+                    assert 0 < now - int(g) < 5_000_000_000
         await srv.stop()
     run(main())
 

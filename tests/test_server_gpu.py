@@ -1,0 +1,88 @@
+"""GPU twin of test_server_e2e.py: a live data-websocket session whose capture
+session runs the HIP encoder (no --use-cpu), decoded stripe by stripe with the
+independent test decoder, plus the frame-trace path (FRAME_TS grab timestamps)
+that tools/bench_e2e.py measures capture -> client latency with."""
+import asyncio
+import json
+import time
+
+import aiohttp
+import numpy as np
+import pytest
+
+from selkies_gstreamer_amd.ops.native import hip_device_count
+from selkies_gstreamer_amd.server.data_server import DataStreamingServer
+from selkies_gstreamer_amd.server.settings import Settings
+from tests.h264_util import StripeDecoder
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _need_gpu():
+    if hip_device_count() < 1:
+        pytest.skip("no HIP device")
+
+
+async def _recv_until(ws, pred, timeout=30.0):
+    seen = []
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while True:
+        msg = await asyncio.wait_for(ws.receive(), max(0.01, end - loop.time()))
+        if msg.type in (aiohttp.WSMsgType.CLOSE, aiohttp.WSMsgType.CLOSED, aiohttp.WSMsgType.ERROR):
+            raise ConnectionError(f"closed: {msg}")
+        seen.append(msg.data)
+        if pred(msg.data):
+            return msg.data, seen
+
+
+@pytest.mark.parametrize("W,H,encoder", [(1920, 1080, "x264enc-striped"), (1280, 720, "x264enc")])
+def test_hip_session_decodes(tmp_path, W, H, encoder):
+    async def main():
+        s = Settings(["--port", "0", "--audio-enabled", "false"], env={})
+        srv = DataStreamingServer(s, upload_dir=str(tmp_path / "up"), capture_source="motion", frame_trace=True)
+        port = await srv.start("127.0.0.1", 0)
+        try:
+            async with aiohttp.ClientSession() as sess:
+                async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket", max_msg_size=0) as ws:
+                    await _recv_until(ws, lambda m: isinstance(m, str) and "server_settings" in m)
+                    await ws.send_str("SETTINGS," + json.dumps({"initialClientWidth": W, "initialClientHeight": H,
+                                                                 "framerate": 60, "encoder": encoder}))
+                    dec = StripeDecoder(W, H)
+                    grabs, lat, frames, pkts = {}, [], set(), []
+                    keyed = False
+                    end = time.monotonic() + 40
+                    while len(frames) < 30 and time.monotonic() < end:
+                        msg = await asyncio.wait_for(ws.receive(), 30)
+                        now = time.monotonic_ns()
+                        d = msg.data
+                        if isinstance(d, str):
+                            if d.startswith("FRAME_TS "):
+                                _, fid, g = d.split()
+                                grabs[int(fid)] = int(g)
+                            continue
+                        if not isinstance(d, bytes) or d[0] != 0x04:
+                            continue
+                        keyed = keyed or d[1] == 1
+                        if not keyed:
+                            continue  # joined mid-GOP: wait for the first IDR
+                        fid = int.from_bytes(d[2:4], "big")
+                        if len(frames) < 3 or (fid in frames and len(frames) == 3):
+                            pkts.append(d)  # first 3 frames; decoded after the run (the Python decoder is slow)
+                        if fid not in frames:
+                            frames.add(fid)
+                            if fid in grabs:
+                                lat.append((now - grabs.pop(fid)) / 1e6)
+                            await ws.send_str(f"CLIENT_FRAME_ACK {fid}")
+                    assert len(frames) >= 30
+                    for d in pkts:
+                        dec.feed(d)
+                    assert dec.Y.std() > 5.0
+                    assert lat, "no FRAME_TS traces"
+                    # capture -> receive must be a few frame intervals at most on one host
+                    assert float(np.median(lat)) < 100.0, lat
+                    assert srv.displays["primary"].flow.acknowledged >= 0
+        finally:
+            await srv.stop()
+    asyncio.run(asyncio.wait_for(main(), 120))

@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""End-to-end session benchmark: real selkies servers, headless websocket clients.
+
+Measures what the driver's encoder bench cannot: the serving path the reference
+runs (capture -> queue_data_for_display -> _video_chunk_sender -> websocket ->
+client, src/selkies/selkies.py:2781-2891; client ACKs every 50 ms,
+addons/gst-web-core/selkies-core.js:2550-2560), end to end on one host.
+
+* N server processes (one per session, the deployment model of parallel/launcher.py),
+  each `python -m selkies_gstreamer_amd` with the synthetic moving-desktop capture
+  source on the same GPU, SELKIES_FRAME_TRACE=1 (the server sends `FRAME_TS <fid>
+  <grab_ns>` — the frame's CLOCK_MONOTONIC grab time — ahead of its stripes).
+* N headless aiohttp clients (sharded over --client-procs processes) speak the reference protocol (MODE,
+  server_settings, SETTINGS, 0x04 stripes, CLIENT_FRAME_ACK every 50 ms) and
+  timestamp the first stripe of every frame on receipt.
+* Reported per N: received fps per session (min / median), capture -> client receive
+  latency p50 / p99 (the server + transport share of glass-to-glass; the browser's
+  decode and paint are not in it), and whether every session sustained the target
+  fps. `--sweep 8,16,24` finds the largest N that does ("concurrent 60 fps sessions").
+
+usage: python tools/bench_e2e.py --sweep 4,8,16 --seconds 6 [--width 1920 --height 1080]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import concurrent.futures
+import json
+import multiprocessing
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import aiohttp
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def start_servers(n: int, args) -> list:
+    procs = []
+    for i in range(n):
+        port = free_port()
+        env = dict(os.environ, SELKIES_FRAME_TRACE="1", PYTHONUNBUFFERED="1")
+        cmd = [sys.executable, "-m", "selkies_gstreamer_amd", "--port", str(port), "--host", "127.0.0.1",
+               "--capture-source", args.source, "--audio-enabled", "false", "--gpu-id", str(args.gpu),
+               "--gamepad-enabled", "false"]
+        if args.use_cpu:
+            cmd += ["--use-cpu", "true"]
+        log = open(os.path.join(args.log_dir, f"server_{n}_{i}.log"), "w")
+        p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+        procs.append((p, port, log))
+    return procs
+
+
+def stop_servers(procs):
+    for p, _, log in procs:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+    for p, _, log in procs:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+        log.close()
+
+
+async def wait_ready(port: int, timeout: float = 90.0):
+    end = time.monotonic() + timeout
+    async with aiohttp.ClientSession() as s:
+        while time.monotonic() < end:
+            try:
+                async with s.get(f"http://127.0.0.1:{port}/health", timeout=aiohttp.ClientTimeout(total=2)) as r:
+                    if r.status == 200:
+                        return
+            except Exception:
+                pass
+            await asyncio.sleep(0.25)
+    raise TimeoutError(f"server on port {port} did not come up")
+
+
+async def client(port: int, args, t_start: float, t_end: float, out: dict):
+    grabs: dict = {}
+    seen: set = set()
+    lat_ms: list = []
+    frames = 0
+    last_fid = None
+    bytes_rx = 0
+    async with aiohttp.ClientSession() as sess:
+        async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket", max_msg_size=0) as ws:
+            settings = {"initialClientWidth": args.width, "initialClientHeight": args.height,
+                        "framerate": args.fps, "encoder": args.encoder, "h264_crf": args.crf}
+            sent_settings = False
+
+            async def acks():
+                while True:
+                    await asyncio.sleep(0.05)
+                    if last_fid is not None:
+                        await ws.send_str(f"CLIENT_FRAME_ACK {last_fid}")
+            ack_task = asyncio.create_task(acks())
+            try:
+                while time.monotonic() < t_end:
+                    try:
+                        msg = await asyncio.wait_for(ws.receive(), max(0.05, t_end - time.monotonic()))
+                    except asyncio.TimeoutError:
+                        break
+                    now_ns = time.monotonic_ns()
+                    if msg.type == aiohttp.WSMsgType.TEXT:
+                        m = msg.data
+                        if not sent_settings and "server_settings" in m:
+                            await ws.send_str("SETTINGS," + json.dumps(settings))
+                            sent_settings = True
+                        elif m.startswith("FRAME_TS "):
+                            _, fid, g = m.split()
+                            grabs[int(fid)] = int(g)
+                    elif msg.type == aiohttp.WSMsgType.BINARY:
+                        d = msg.data
+                        if len(d) >= 10 and d[0] == 0x04:
+                            fid = (d[2] << 8) | d[3]
+                            last_fid = fid
+                            bytes_rx += len(d)
+                            if fid not in seen:
+                                seen.add(fid)
+                                if len(seen) > 4096:
+                                    seen.clear()
+                                if time.monotonic() >= t_start:
+                                    frames += 1
+                                    g = grabs.pop(fid, None)
+                                    if g is not None:
+                                        lat_ms.append((now_ns - g) / 1e6)
+                    else:
+                        break
+            finally:
+                ack_task.cancel()
+    out[port] = dict(frames=frames, lat=lat_ms, bytes=bytes_rx)
+
+
+def client_worker(ports, args, t_start, t_end) -> dict:
+    """One client process drives a shard of the sessions (a single Python
+    process cannot receive ~15k stripe messages/s for 15 sessions by itself)."""
+    async def go():
+        out: dict = {}
+        await asyncio.gather(*(client(p, args, t_start, t_end, out) for p in ports))
+        return out
+    return asyncio.run(go())
+
+
+async def run_n(n: int, args) -> dict:
+    procs = start_servers(n, args)
+    try:
+        await asyncio.gather(*(wait_ready(port) for _, port, _ in procs))
+        t0 = time.monotonic()
+        t_start = t0 + args.warmup
+        t_end = t_start + args.seconds
+        ports = [port for _, port, _ in procs]
+        shards = [ports[i::args.client_procs] for i in range(min(args.client_procs, n))]
+        ctx = multiprocessing.get_context("spawn")
+        loop = asyncio.get_running_loop()
+        with concurrent.futures.ProcessPoolExecutor(len(shards), mp_context=ctx) as ex:
+            parts = await asyncio.gather(*(loop.run_in_executor(ex, client_worker, sh, args, t_start, t_end)
+                                           for sh in shards))
+        out: dict = {}
+        for part in parts:
+            out.update(part)
+    finally:
+        stop_servers(procs)
+    fps = np.array([out[p]["frames"] / args.seconds for _, p, _ in procs]) if out else np.zeros(1)
+    lat = np.concatenate([np.asarray(out[p]["lat"], dtype=np.float64) for _, p, _ in procs]) if out else np.zeros(0)
+    ok = bool(len(fps) == n and fps.min() >= args.fps * args.sustain)
+    return {"sessions": n, "fps_min": round(float(fps.min()), 2), "fps_median": round(float(np.median(fps)), 2),
+            "aggregate_fps": round(float(fps.sum()), 1),
+            "latency_p50_ms": round(float(np.percentile(lat, 50)), 2) if len(lat) else None,
+            "latency_p99_ms": round(float(np.percentile(lat, 99)), 2) if len(lat) else None,
+            "latency_samples": int(len(lat)), "sustained": ok}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sweep", default="1,4,8", help="comma-separated session counts")
+    ap.add_argument("--seconds", type=float, default=6.0)
+    ap.add_argument("--warmup", type=float, default=3.0)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--fps", type=int, default=60)
+    ap.add_argument("--crf", type=int, default=25)
+    ap.add_argument("--encoder", default="x264enc-striped")
+    ap.add_argument("--source", default="motion", choices=["motion", "synthetic", "noise"])
+    ap.add_argument("--gpu", type=int, default=0)
+    ap.add_argument("--use-cpu", action="store_true")
+    ap.add_argument("--client-procs", type=int, default=4, help="client processes the sessions are sharded over")
+    ap.add_argument("--sustain", type=float, default=0.97, help="fraction of --fps every session must receive")
+    ap.add_argument("--log-dir", default=os.path.join(ROOT, "gpurun_out", "e2e_logs"))
+    args = ap.parse_args()
+    os.makedirs(args.log_dir, exist_ok=True)
+    results = []
+    best = 0
+    for n in [int(x) for x in args.sweep.split(",")]:
+        r = asyncio.run(run_n(n, args))
+        results.append(r)
+        print(json.dumps(r), flush=True)
+        if r["sustained"]:
+            best = max(best, n)
+    print(json.dumps({"metric": "concurrent sustained sessions + capture->client latency",
+                      "resolution": f"{args.width}x{args.height}", "target_fps": args.fps,
+                      "encoder": args.encoder, "max_sustained_sessions": best, "runs": results}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
