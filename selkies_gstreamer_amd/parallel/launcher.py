@@ -33,6 +33,7 @@ class SessionSpec:
     port: int
     gpu: int
     extra: list = field(default_factory=list)
+    hw_queues: Optional[int] = None
 
     def command(self, python: str = sys.executable) -> list[str]:
         return [python, "-m", "selkies_gstreamer_amd", "--port", str(self.port), "--gpu-id", str(self.gpu),
@@ -42,7 +43,21 @@ class SessionSpec:
         e = dict(os.environ if base is None else base)
         e["DISPLAY"] = self.display
         e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if self.hw_queues:
+            e.setdefault("GPU_MAX_HW_QUEUES", str(self.hw_queues))
         return e
+
+
+def hw_queues_for(sessions_on_gpu: int) -> Optional[int]:
+    """HIP hardware queues per server process when several share a GPU.
+
+    Every process maps GPU_MAX_HW_QUEUES (default 4) compute queues; with a dozen
+    session processes on one MI355X the queues outnumber what the scheduler keeps
+    resident and frames stall while queues are swapped. Measured with
+    tools/bench_e2e.py at 1080p60 (profiles/r2_e2e_sessions.md): 12 sessions drop to
+    52 fps with 4 queues per process, 15 sustain 60 fps with 1 or 2. A session
+    needs one queue for its frames and one for uploads/copies."""
+    return 2 if sessions_on_gpu > 4 else None
 
 
 def plan_sessions(n: int, gpus: int, base_port: int, display_base: int, width: int = 1920, height: int = 1080,
@@ -54,6 +69,9 @@ def plan_sessions(n: int, gpus: int, base_port: int, display_base: int, width: i
         if gpu is None:
             raise RuntimeError(f"node is full after {i} sessions (capacity {capacity} x 1080p60 per GPU)")
         out.append(SessionSpec(f"s{i}", f":{display_base + i}", base_port + i, gpu, list(extra or [])))
+    per_gpu = {g: sum(1 for s in out if s.gpu == g) for g in {s.gpu for s in out}}
+    for s in out:
+        s.hw_queues = hw_queues_for(per_gpu[s.gpu])
     return out
 
 

@@ -39,6 +39,10 @@ def test_plan_sessions():
     assert specs[1].env({})["DISPLAY"] == ":31"
     with pytest.raises(RuntimeError):
         plan_sessions(5, 1, 9000, 30, capacity=4)
+    assert "GPU_MAX_HW_QUEUES" not in specs[0].env({})  # 2 sessions per GPU: HIP's default queues
+    dense = plan_sessions(12, 1, 9000, 30)
+    assert dense[0].env({})["GPU_MAX_HW_QUEUES"] == "2"
+    assert dense[0].env({"GPU_MAX_HW_QUEUES": "1"})["GPU_MAX_HW_QUEUES"] == "1"  # operator's choice wins
 
 
 class _Crashing(SessionSpec):

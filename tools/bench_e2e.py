@@ -38,6 +38,8 @@ import aiohttp
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from selkies_gstreamer_amd.parallel.launcher import hw_queues_for  # noqa: E402
 
 
 def free_port() -> int:
@@ -53,6 +55,9 @@ def start_servers(n: int, args) -> list:
     for i in range(n):
         port = free_port()
         env = dict(os.environ, SELKIES_FRAME_TRACE="1", PYTHONUNBUFFERED="1")
+        q = args.hw_queues if args.hw_queues is not None else hw_queues_for(n)
+        if q:
+            env["GPU_MAX_HW_QUEUES"] = str(q)  # what parallel/launcher.py gives co-located sessions
         cmd = [sys.executable, "-m", "selkies_gstreamer_amd", "--port", str(port), "--host", "127.0.0.1",
                "--capture-source", args.source, "--audio-enabled", "false", "--gpu-id", str(args.gpu),
                "--gamepad-enabled", "false"]
@@ -202,6 +207,8 @@ def main():
     ap.add_argument("--source", default="motion", choices=["motion", "synthetic", "noise"])
     ap.add_argument("--gpu", type=int, default=0)
     ap.add_argument("--use-cpu", action="store_true")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES per server (default: the launcher's choice for N sessions)")
     ap.add_argument("--client-procs", type=int, default=4, help="client processes the sessions are sharded over")
     ap.add_argument("--sustain", type=float, default=0.97, help="fraction of --fps every session must receive")
     ap.add_argument("--log-dir", default=os.path.join(ROOT, "gpurun_out", "e2e_logs"))
