@@ -94,6 +94,15 @@ def build_rtc(verbose: bool = False) -> Path:
     return RTC_LIB
 
 
+def main(argv=None) -> int:
+    """``selkies-build``: the HIP engine library, the WebRTC media library and the shims."""
+    argv = sys.argv[1:] if argv is None else argv
+    print(build(verbose="-v" in argv))
+    print(build_rtc(verbose="-v" in argv))
+    from .build_shims import build_shims
+    print(build_shims())
+    return 0
+
+
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
-    print(build_rtc(verbose="-v" in sys.argv))
+    sys.exit(main())

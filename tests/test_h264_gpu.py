@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from selkies_gstreamer_amd.ops.native import H264Encoder, MB_INFO_DTYPE, ME_DTYPE, TASK_DTYPE
+from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
 from tests.h264_util import StripeDecoder, synthetic_frames, bgrx_to_y709, psnr
 
 pytestmark = pytest.mark.gpu
@@ -19,8 +20,19 @@ def _compare_state(cpu, gpu, W, t):
         assert np.array_equal(a, b), f"frame {t}: {name} differs ({np.sum(a != b)} bytes)"
     ta, tb = cpu.debug_buffer("tasks", TASK_DTYPE), gpu.debug_buffer("tasks", TASK_DTYPE)
     assert np.array_equal(ta["final_action"], tb["final_action"]), f"frame {t}: slice decisions differ"
+    # per-MB decisions of every coded slice: MVs, MVDs, reference, type, modes, QP, CBP, nnz
+    mb_w = (W + 15) // 16
+    ia, ib = cpu.debug_buffer("mbs", MB_INFO_DTYPE), gpu.debug_buffer("mbs", MB_INFO_DTYPE)
     ma, mb = cpu.debug_buffer("me", ME_DTYPE), gpu.debug_buffer("me", ME_DTYPE)
-    coded = np.repeat(ta["final_action"] == 1, 1)
+    for task in ta:
+        if task["final_action"] not in (1, 2):   # ACT_P / ACT_I (none / skip-all code no MBs)
+            continue
+        sl = slice(task["first_row"] * mb_w, (task["first_row"] + task["num_rows"]) * mb_w)
+        for f in ("type", "mvx", "mvy", "mvdx", "mvdy", "ref", "i16_mode", "chroma_mode", "qp", "cbp", "nnz"):
+            assert np.array_equal(ia[f][sl], ib[f][sl]), f"frame {t}: MB {f} differs in rows from {task['first_row']}"
+        if task["final_action"] == 1:   # P slice: the motion search result it was coded from
+            for f in ("mvx", "mvy", "ref"):
+                assert np.array_equal(ma[f][sl], mb[f][sl]), f"frame {t}: ME {f} differs"
     for name in ("ref_y", "ref_u", "ref_v"):
         a, b = cpu.debug_buffer(name), gpu.debug_buffer(name)
         assert np.array_equal(a, b), f"frame {t}: {name} differs ({np.sum(a != b)} bytes)"
@@ -51,9 +63,25 @@ def test_gpu_1080p_desktop_matches_cpu(deblock):
     for t, f in enumerate(synthetic_frames(W, H, 3, seed=5)):
         pc = cpu.encode(f, t)
         pg = gpu.encode(f, t)
+        _compare_state(cpu, gpu, W, t)
         assert len(pc) == len(pg)
         for a, b in zip(pc, pg):
             assert a.data == b.data, f"frame {t} stripe y={a.y} differs"
+
+
+def test_gpu_1080p_motion_long_matches_cpu():
+    """20 frames of the bench's moving desktop through a 16-frame pool (the wrap is a
+    scene cut: I stripes inside P frames), state and MVs compared every frame."""
+    W, H = 1920, 1080
+    cpu, gpu = _pair(W, H, stripe_height=64, qp=25)
+    src = SyntheticDesktop(W, H, kind="motion")
+    pool = [src.frame(i) for i in range(16)]
+    for t in range(20):
+        f = pool[t % 16]
+        pc = cpu.encode(f, t)
+        pg = gpu.encode(f, t)
+        _compare_state(cpu, gpu, W, t)
+        assert [p.data for p in pg] == [p.data for p in pc], f"frame {t}: bitstreams differ"
 
 
 def test_gpu_escalation_and_odd_geometry():
