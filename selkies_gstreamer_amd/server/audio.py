@@ -15,6 +15,7 @@ import ctypes
 import ctypes.util
 import logging
 import shutil
+import threading
 from typing import Optional
 
 from . import protocol
@@ -22,6 +23,7 @@ from . import protocol
 log = logging.getLogger("audio")
 
 VIRTUAL_SOURCE = "SelkiesVirtualMic"
+MIC_WRITE_CHUNK = 4800   # 100 ms of s16 mono 24 kHz per pa_simple_write
 MASTER_MONITOR = "input.monitor"
 
 
@@ -37,6 +39,11 @@ class MicSink:
         self.failed = False
         self.buffer = bytearray()
         self._warned = False
+        self._cv = threading.Condition()
+        self._thread = None
+        self._stop = False
+        self.written = 0
+        self.dropped = 0
 
     def _load(self) -> bool:
         path = ctypes.util.find_library("pulse-simple")
@@ -87,24 +94,58 @@ class MicSink:
         return True
 
     def push(self, pcm: bytes) -> int:
-        """Buffers and plays one chunk; returns bytes written."""
+        """Queues one chunk for playback and returns at once (called on the event
+        loop). A writer thread drains the ring into pa_simple_write, which blocks for
+        as long as PulseAudio's buffer is full; the ring keeps at most
+        MIC_BUFFER_MAX bytes (2 s) and drops the oldest audio beyond that."""
         if not self.ready or not pcm:
             return 0
-        self.buffer += pcm
-        if len(self.buffer) > protocol.MIC_BUFFER_MAX:
-            del self.buffer[: len(self.buffer) // 2]
-            log.warning("microphone buffer overflow; dropped old audio")
-        n = len(pcm)
-        chunk = bytes(self.buffer[:n])
-        del self.buffer[:n]
+        with self._cv:
+            self.buffer += pcm
+            if len(self.buffer) > protocol.MIC_BUFFER_MAX:
+                drop = len(self.buffer) - protocol.MIC_BUFFER_MAX
+                drop += drop & 1   # whole s16 samples
+                del self.buffer[:drop]
+                self.dropped += drop
+                if not self._warned:
+                    log.warning("microphone buffer overflow; dropping old audio")
+                    self._warned = True
+            self._cv.notify()
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._writer, name="mic-writer", daemon=True)
+            self._thread.start()
+        return len(pcm)
+
+    def _write(self, chunk: bytes) -> bool:
         err = ctypes.c_int(0)
         if self.pa.pa_simple_write(self.stream, chunk, len(chunk), ctypes.byref(err)) < 0:
             log.error("microphone write failed (%d)", err.value)
-            self.close()
-            return 0
-        return len(chunk)
+            return False
+        return True
+
+    def _writer(self):
+        while True:
+            with self._cv:
+                while not self.buffer and not self._stop:
+                    self._cv.wait()
+                if self._stop:
+                    return
+                chunk = bytes(self.buffer[:MIC_WRITE_CHUNK])
+                del self.buffer[:len(chunk)]
+            if not self._write(chunk):
+                with self._cv:
+                    self.ready = False
+                    self.buffer.clear()
+                return
+            self.written += len(chunk)
 
     def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        if self._thread is not None:
+            self._thread.join(timeout=2)
+            self._thread = None
         if self.stream and self.pa:
             self.pa.pa_simple_free(self.stream)
         self.stream = None

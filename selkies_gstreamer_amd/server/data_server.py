@@ -34,7 +34,7 @@ from aiohttp import WSMsgType, web
 
 from . import protocol
 from .audio import AudioPipeline, MicSink
-from .display import XrandrDisplay, compute_layout, set_cursor_size, set_dpi
+from .display import WindowManagerSwap, XrandrDisplay, compute_layout, set_cursor_size, set_dpi
 from .settings import Settings
 from .stats import BandwidthMeter, StatsPublisher
 
@@ -211,6 +211,7 @@ class DataStreamingServer:
             capture_factory = pixelflux.ScreenCapture
         self.capture_factory = capture_factory
         self.display_manager = display_manager or XrandrDisplay()
+        self.wm_swap = WindowManagerSwap() if getattr(self.display_manager, "available", False) else None
         self.capture_source = capture_source
         self.gpu_id, self.num_gpus = gpu_id, max(1, num_gpus)
         self.web_root = web_root
@@ -629,6 +630,8 @@ class DataStreamingServer:
             log.error("display layout is empty; not starting capture")
             return
         self.layouts = layouts
+        if self.wm_swap is not None:
+            await self.wm_swap.update(len(self.displays))
         if getattr(self.display_manager, "available", False):
             ok = await self.display_manager.apply(layouts, tw, th)
             if not ok:

@@ -229,36 +229,145 @@ class XrandrDisplay:
 
 
 # --------------------------------------------------------------------------- DPI
-async def set_dpi(dpi: int) -> bool:
-    """Applies DPI through whatever the desktop offers (xrdb/xsettingsd, XFCE, MATE)."""
+def detect_desktop(which=shutil.which) -> str:
+    """Desktop session, in the reference's probe order (selkies.py:704-741):
+    KDE -> XFCE -> MATE -> i3 -> Openbox -> generic."""
+    for name, probes in (("kde", ("startplasma-x11",)), ("xfce", ("xfce4-session",)), ("mate", ("mate-session",)),
+                         ("i3", ("i3",)), ("openbox", ("openbox-session", "openbox"))):
+        if any(which(p) for p in probes):
+            return name
+    return "generic"
+
+
+def merge_setting_file(path: str, key: str, line: str, sep: str = " ") -> None:
+    """Sets one key of a `key<sep>value` style file, keeping every other line.
+
+    The reference rewrites ~/.Xresources and ~/.xsettingsd wholesale (selkies.py:442-480),
+    losing the user's other resources; this keeps them and only replaces `key`."""
+    try:
+        with open(path) as f:
+            lines = f.read().splitlines()
+    except OSError:
+        lines = []
+    out, done = [], False
+    for ln in lines:
+        k = ln.split(sep, 1)[0].strip().rstrip(":")
+        if k == key.rstrip(":"):
+            if not done:
+                out.append(line)
+                done = True
+            continue
+        out.append(ln)
+    if not done:
+        out.append(line)
+    tmp = path + ".selkies-tmp"
+    with open(tmp, "w") as f:
+        f.write("\n".join(out) + "\n")
+    os.replace(tmp, path)
+
+
+async def _xrdb_dpi(dpi: int) -> bool:
+    """Xft.dpi through xrdb -merge (the resource database, not a file rewrite) plus
+    the Xft/DPI key of ~/.xsettingsd with a SIGHUP to a running xsettingsd."""
+    if not shutil.which("xrdb"):
+        return False
     ok = False
-    if shutil.which("xrdb"):
-        path = os.path.expanduser("~/.Xresources")
-        try:
-            with open(path, "w") as f:
-                f.write(f"Xft.dpi:   {dpi}\n")
-            rc, _ = await run(["xrdb", path])
-            ok |= rc == 0
-            with open(os.path.expanduser("~/.xsettingsd"), "w") as f:
-                f.write("Xft/Antialias 1\nXft/Hinting 1\nXft/HintStyle \"hintfull\"\nXft/RGBA \"rgb\"\n"
-                        f"Xft/DPI {dpi * 1024}\n")
-            rc, out = await run(["pgrep", "xsettingsd"])
-            if rc == 0 and out.strip():
-                await run(["kill", "-1", out.split()[0]])
-        except OSError as e:
-            log.warning("xrdb DPI update failed: %s", e)
-    if shutil.which("xfconf-query"):
-        env = await _session_env("xfce4-session")
-        rc, _ = await run(["xfconf-query", "-c", "xsettings", "-p", "/Xft/DPI", "-s", str(dpi), "--create",
-                           "-t", "int"], env=env)
-        ok |= rc == 0
-    if shutil.which("gsettings"):
-        scale = dpi / 96.0
-        factor = int(scale) if scale == int(scale) else 1
-        rc, _ = await run(["gsettings", "set", "org.mate.interface", "window-scaling-factor", str(max(1, factor))])
-        rc2, _ = await run(["gsettings", "set", "org.mate.font-rendering", "dpi", str(dpi)])
-        ok |= rc == 0 or rc2 == 0
+    try:
+        p = await asyncio.create_subprocess_exec("xrdb", "-merge", stdin=asyncio.subprocess.PIPE,
+                                                 stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
+        await p.communicate(f"Xft.dpi: {dpi}\n".encode())
+        ok = p.returncode == 0
+        merge_setting_file(os.path.expanduser("~/.Xresources"), "Xft.dpi:", f"Xft.dpi:   {dpi}", sep=":")
+        merge_setting_file(os.path.expanduser("~/.xsettingsd"), "Xft/DPI", f"Xft/DPI {dpi * 1024}")
+        rc, out = await run(["pgrep", "-x", "xsettingsd"])
+        if rc == 0 and out.strip():
+            await run(["kill", "-HUP", out.split()[0]])
+    except OSError as e:
+        log.warning("xrdb DPI update failed: %s", e)
     return ok
+
+
+async def _xfconf_dpi(dpi: int) -> bool:
+    if not shutil.which("xfconf-query"):
+        return False
+    env = await _session_env("xfce4-session")
+    rc, _ = await run(["xfconf-query", "-c", "xsettings", "-p", "/Xft/DPI", "-s", str(dpi), "--create", "-t", "int"],
+                      env=env)
+    return rc == 0
+
+
+async def _mate_dpi(dpi: int) -> bool:
+    if not shutil.which("gsettings"):
+        return False
+    scale = dpi / 96.0
+    factor = int(scale) if scale == int(scale) else 1
+    rc, _ = await run(["gsettings", "set", "org.mate.interface", "window-scaling-factor", str(max(1, factor))])
+    rc2, _ = await run(["gsettings", "set", "org.mate.font-rendering", "dpi", str(dpi)])
+    return rc == 0 or rc2 == 0
+
+
+async def set_dpi(dpi: int, desktop: Optional[str] = None) -> bool:
+    """Applies DPI the way the running desktop takes it: XFCE through xfconf only
+    (xrdb as well would scale twice), MATE through gsettings + xrdb, KDE / i3 /
+    Openbox / anything else through xrdb."""
+    try:
+        dpi = int(dpi)
+    except (TypeError, ValueError):
+        return False
+    if dpi <= 0:
+        return False
+    de = desktop or detect_desktop()
+    if de == "xfce":
+        ok = await _xfconf_dpi(dpi)
+    elif de == "mate":
+        ok = await _mate_dpi(dpi)
+        ok = await _xrdb_dpi(dpi) or ok
+    else:
+        ok = await _xrdb_dpi(dpi)
+    if not ok:
+        log.warning("no DPI method succeeded for %d (desktop %s)", dpi, de)
+    return ok
+
+
+class WindowManagerSwap:
+    """Multi-monitor: XFCE's and KDE's window managers place windows on the X
+    screen, not on the per-display xrandr monitors, so with more than one display
+    the session switches to openbox with a minimal config (selkies.py:2631-2647).
+    Unlike the reference this also switches back when the session returns to one
+    display."""
+
+    def __init__(self, which=shutil.which, runner=None):
+        self.which = which
+        self.desktop = detect_desktop(which)
+        self.supported = self.desktop in ("xfce", "kde") and which("openbox") is not None
+        self.swapped = False
+        self._run = runner or self._spawn
+
+    @staticmethod
+    async def _spawn(cmd):
+        try:
+            await asyncio.create_subprocess_exec(*cmd, stdout=asyncio.subprocess.DEVNULL,
+                                                 stderr=asyncio.subprocess.DEVNULL, start_new_session=True)
+        except OSError as e:
+            log.warning("%s failed: %s", cmd[0], e)
+
+    async def update(self, display_count: int) -> None:
+        if not self.supported:
+            return
+        if display_count > 1 and not self.swapped:
+            cfg = os.path.join(os.environ.get("XDG_RUNTIME_DIR") or "/tmp", "selkies_openbox.xml")
+            try:
+                with open(cfg, "w") as f:
+                    f.write("<openbox_config></openbox_config>\n")
+                cmd = ["openbox", "--config-file", cfg, "--replace"]
+            except OSError:
+                cmd = ["openbox", "--replace"]
+            await self._run(cmd)
+            self.swapped = True
+        elif display_count <= 1 and self.swapped:
+            native = ["xfwm4", "--replace"] if self.desktop == "xfce" else ["kwin_x11", "--replace"]
+            await self._run(native)
+            self.swapped = False
 
 
 async def set_cursor_size(size: int) -> bool:
