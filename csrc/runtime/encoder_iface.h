@@ -59,5 +59,8 @@ EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c);
 EncoderBackend* create_hip_backend(const h264::EncoderConfig& c, int device);
 EncoderBackend* create_cpu_jpeg_backend(const jpeg::JpegConfig& c);
 EncoderBackend* create_hip_jpeg_backend(const jpeg::JpegConfig& c, int device);
+// Once per process and device, before the first session's frames: brings up the
+// runtime's host->device copy engines (see h264_hip.cpp). SK_COPY_WARMUP=0 skips it.
+void warm_copy_engines(int device);
 
 }  // namespace sk

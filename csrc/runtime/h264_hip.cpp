@@ -9,6 +9,7 @@
 #include "trace.h"
 #include "../kernels/h264_gpu.h"
 #include "../kernels/hevc_gpu.h"
+#include "../kernels/runtime_kernels.h"
 #include "../codec/hevc_encoder.h"
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -17,6 +18,8 @@
 #include <stdexcept>
 #include <string.h>
 #include <string>
+#include <thread>
+#include <vector>
 
 namespace sk {
 namespace {
@@ -36,6 +39,7 @@ class HipBackend : public EncoderBackend {
         g_.init(cfg_);
         ctl_.init(cfg_, g_);
         HIPCHECK(hipSetDevice(device_));
+        warm_copy_engines(device_);
         HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         for (auto& e : ev_) HIPCHECK(hipEventCreate(&e));
         for (auto& e : ev_copy_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -104,7 +108,8 @@ class HipBackend : public EncoderBackend {
         // Nothing in flight: copy on the encoder's own stream (no cross-stream wait).
         // Overlapped upload, or bands of one frame: the device's shared copy stream, so
         // the uploads of all encoders on this GPU run back to back at full PCIe rate
-        // instead of contending (one copy queue, not one per session).
+        // instead of contending (one copy queue, not one per session). Copies behind
+        // kernels on one stream stall in a fresh process until warm_copy_engines() ran.
         hipStream_t cs = stream_;
         // Overlapped upload of a session: its own upload stream (the copies of many
         // sessions then spread over the SDMA engines; SK_SHARED_UPLOAD=1 funnels them
@@ -673,6 +678,52 @@ class HipBackend : public EncoderBackend {
 };
 
 }  // namespace
+
+// A fresh process pays a one-time cost when several threads queue SDMA copies behind
+// kernels on their streams: during the first ~50 such copies hipMemcpyAsync blocks
+// the calling thread, and every other copying thread with it, for 6-9 ms while the
+// GPU idles (rocprofv3 --hip-runtime-trace of the 8-session bench: all capture
+// threads inside hipMemcpyAsync at once, four times within the first ~40 frames;
+// tools/microbench/h2d_stall.cpp reproduces it with 8 threads x (copy + 12 small
+// kernels): 46 stalled calls; 0 with HSA_ENABLE_SDMA=0, with copies on kernel-free
+// streams, or after this warm-up; profiles/r2_driver_window.md). Whatever the
+// runtime grows in that phase is per process, not per stream: the same pattern run
+// here from 8 threads on streams of their own, destroyed afterwards, leaves the
+// sessions' own streams stall-free. Serving would otherwise pay it inside the first
+// second of the first sessions. SK_COPY_WARMUP=0 skips it.
+void warm_copy_engines(int device) {
+    static std::mutex mu;
+    static std::map<int, bool> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done[device]) return;
+    done[device] = true;
+    const char* env = getenv("SK_COPY_WARMUP");
+    if (env && atoi(env) == 0) return;
+    const int kThreads = 8, kRounds = 60, kKernels = 12;
+    const size_t bytes = (size_t)8 << 20;
+    uint8_t* host = nullptr;
+    if (hipHostMalloc((void**)&host, bytes, hipHostMallocDefault) != hipSuccess) return;
+    for (size_t i = 0; i < bytes; i += 4096) host[i] = 0;
+    std::vector<std::thread> th;
+    for (int t = 0; t < kThreads; t++)
+        th.emplace_back([=] {
+            if (hipSetDevice(device) != hipSuccess) return;
+            hipStream_t s = nullptr;
+            uint8_t* dev = nullptr;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return;
+            if (hipMalloc((void**)&dev, bytes) == hipSuccess) {
+                for (int r = 0; r < kRounds; r++) {
+                    if (hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, s) != hipSuccess) break;
+                    for (int k = 0; k < kKernels; k++) launch_touch_pages(dev, 2000, s);
+                    if (hipStreamSynchronize(s) != hipSuccess) break;
+                }
+                hipFree(dev);
+            }
+            hipStreamDestroy(s);
+        });
+    for (auto& x : th) x.join();
+    hipHostFree(host);
+}
 
 EncoderBackend* create_hip_backend(const h264::EncoderConfig& c, int device) {
     int n = 0;

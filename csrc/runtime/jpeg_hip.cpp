@@ -39,6 +39,7 @@ class HipJpegBackend : public EncoderBackend {
             build_jpeg_header(L_.W, L_.stripe_pix_h(L_.num_stripes - 1), tab_[q], hdr_[q][1]);
         }
         HIPCHECK(hipSetDevice(device_));
+        warm_copy_engines(device_);
         HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         alloc();
     }
