@@ -44,6 +44,7 @@ struct CuLds {
     int32_t b[kCoefPerCu];       // transform intermediate
     uint8_t ref[65 + 65 + 33 + 33];   // intra: luma raw | luma filtered | Cb | Cr
     int misc[4];
+    int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];   // inter: merge / AMVP candidates
 };
 
 // LDS copy of the 16-point DCT matrix (the 8-point one is its even rows).
@@ -55,7 +56,7 @@ __device__ __forceinline__ void load_t16(int8_t* t) {
 // Lane mapping: luma outputs (row l >> 2, columns 4*(l & 3) .. +3), chroma outputs
 // (component l >> 5, row (l >> 2) & 7, columns 2*(l & 3) .. +1). Writes the levels to
 // `gcoef` (global) and the reconstruction into L.pred; returns the cbf bits.
-__device__ int code_cu_wave(CuLds& L, const int8_t* T, int qp, bool intra, int16_t* gcoef) {
+__device__ __forceinline__ int code_cu_wave(CuLds& L, const int8_t* T, int qp, bool intra, int16_t* gcoef) {
     const int l = lane();
     const int qpc = chroma_qp(qp);
     const int ly = l >> 2, lx0 = 4 * (l & 3);
@@ -152,7 +153,7 @@ __device__ int code_cu_wave(CuLds& L, const int8_t* T, int qp, bool intra, int16
 }
 
 // Source samples of CU (cx, cy) into L.src; reconstruction L.pred to the rec planes.
-__device__ void load_src(CuLds& L, const FrameArgs& f, int cx, int cy) {
+__device__ __forceinline__ void load_src(CuLds& L, const FrameArgs& f, int cx, int cy) {
     const int l = lane();
     for (int i = l; i < kCoefPerCu; i += 64) {
         uint8_t v;
@@ -164,7 +165,7 @@ __device__ void load_src(CuLds& L, const FrameArgs& f, int cx, int cy) {
         L.src[i] = v;
     }
 }
-__device__ void store_rec(const CuLds& L, const FrameArgs& f, int cx, int cy) {
+__device__ __forceinline__ void store_rec(const CuLds& L, const FrameArgs& f, int cx, int cy) {
     const int l = lane();
     for (int i = l; i < kCoefPerCu; i += 64) {
         if (i < 256) f.rec.y[(size_t)(cy * 16 + (i >> 4)) * f.stride_y + cx * 16 + (i & 15)] = L.pred[i];
@@ -211,9 +212,12 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     const bool top = cy > t.first_row;
     const NbMv A1 = nb(cx - 1, cy, cx > 0), B1 = nb(cx, cy - 1, top);
     const NbMv B0 = nb(cx + 1, cy - 1, top && cx + 1 < W), B2 = nb(cx - 1, cy - 1, top && cx > 0);
-    int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];
+    // candidate lists in LDS (dynamically indexed: private arrays would live in scratch);
+    // every lane writes the same values
+    int *mlx = L.mlx, *mly = L.mly, *px = L.px, *py = L.py;
     merge_list(A1, B1, B0, B2, mlx, mly);
     amvp_list(A1, B1, B0, B2, px, py);
+    wsync();
     const int mvx = 4 * f.me[idx].mvx, mvy = 4 * f.me[idx].mvy;
     const int pic_w = f.stride_y, pic_h = f.mb_h * 16;
     load_src(L, f, cx, cy);
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
 // Intra reference samples (8.4.4.2.2, substitution in closed form for CTB = CU: the
 // bottom-left half is never available) of an n x n block at (x0, y0): linear layout
 // of build_intra_ref. Every lane writes the entries i = lane, lane + 64.
-__device__ void fill_ref(const uint8_t* P, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
+__device__ __forceinline__ void fill_ref(const uint8_t* P, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
                          uint8_t* ref) {
     const int len = 4 * n + 1;
     for (int i = lane(); i < len; i += 64) {
@@ -291,7 +295,7 @@ __device__ void fill_ref(const uint8_t* P, int stride, int x0, int y0, int n, bo
         ref[i] = (uint8_t)v;
     }
 }
-__device__ void filter_ref(const uint8_t* r, int n, uint8_t* out) {
+__device__ __forceinline__ void filter_ref(const uint8_t* r, int n, uint8_t* out) {
     const int len = 4 * n + 1;
     for (int i = lane(); i < len; i += 64)
         out[i] = (i == 0 || i == len - 1) ? r[i] : (uint8_t)((r[i - 1] + 2 * r[i] + r[i + 1] + 2) >> 2);
@@ -324,7 +328,7 @@ __device__ __forceinline__ int dc_value(const uint8_t* r, int n, int log2n) {
     return (wsum(v) + n) >> (log2n + 1);
 }
 // Intra prediction of the whole CU into L.pred for `mode` (refs in L.ref).
-__device__ void intra_pred_cu(CuLds& L, int mode) {
+__device__ __forceinline__ void intra_pred_cu(CuLds& L, int mode) {
     const int l = lane();
     uint8_t* ry = (mode == 0) ? L.ref + 65 : L.ref;   // luma planar uses the filtered references
     const int dcy = dc_value(L.ref, 16, 4);
@@ -340,7 +344,7 @@ __device__ void intra_pred_cu(CuLds& L, int mode) {
     }
     wsync();
 }
-__device__ void intra_refs(CuLds& L, const Planes& P, const FrameArgs& f, int cx, int cy, bool left, bool top,
+__device__ __forceinline__ void intra_refs(CuLds& L, const Planes& P, const FrameArgs& f, int cx, int cy, bool left, bool top,
                            bool tr) {
     fill_ref(P.y, f.stride_y, cx * 16, cy * 16, 16, left, top, tr, L.ref);
     fill_ref(P.u, f.stride_c, cx * 8, cy * 8, 8, left, top, tr, L.ref + 130);
@@ -673,6 +677,7 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(HevcArgs A) {
     E.flushed = 0;
     E.ob = 0;
     const unsigned long long t0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long rt0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;   // 100 MHz
     int entries = 0;
     for (int idx = cy * f.mb_w; idx < (cy + 1) * f.mb_w; idx++) {
         const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
@@ -691,7 +696,8 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(HevcArgs A) {
     if (A.dbg && l == 0) {
         A.dbg[4 * cy + 0] = __builtin_amdgcn_s_memtime() - t0;
         A.dbg[4 * cy + 1] = (unsigned long long)entries;
-        A.dbg[4 * cy + 2] = (unsigned long long)(E.flushed + E.opos);
+        A.dbg[4 * cy + 2] = rt0;
+        A.dbg[4 * cy + 3] = __builtin_amdgcn_s_memrealtime();
     }
     uint8_t* out = E.out;
     const int size = E.flushed + E.opos;

@@ -13,3 +13,5 @@ timeout -k 10 200 python bench.py --encoder hevc --sessions 8 --steps 30 --warmu
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --encoder hevc --sessions 1 --width 3840 --height 2160 --steps 20 --warmup 3 > "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log" 2>&1
 echo EXIT $?
+SK_NATIVE_LIB=$GRAFT_REPO_ROOT/selkies_gstreamer_amd/_lib/libselkies_native_stamps.so timeout -k 10 120 python "$GRAFT_REPO_ROOT/tools/stamps_hevc_cabac.py" > "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_stamps.txt" 2>&1
+cat "$GRAFT_REPO_ROOT/gpurun_out/${TAG}_stamps.txt"

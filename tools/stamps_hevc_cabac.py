@@ -12,7 +12,14 @@ for t in range(3):
     enc.encode(src.frame(t), t)
 st = np.frombuffer(enc.debug_buffer("hevc_stamps", np.uint8), np.uint64).reshape(-1, 4).astype(np.int64)
 bn = np.frombuffer(enc.debug_buffer("bin_n", np.uint8), np.int32)
-print("rows", len(st), "median cycles/row", np.median(st[:, 0]), "median entries/row", np.median(st[:, 1]),
-      "median bytes/row", np.median(st[:, 2]))
+print("rows", len(st), "median cycles/row", np.median(st[:, 0]), "median entries/row", np.median(st[:, 1]))
+rt = (st[:, 3] - st[:, 2]) / 100.0   # s_memrealtime: 100 MHz -> us
+print("row duration us (realtime): median", np.median(rt), "max", rt.max(),
+      "-> core MHz implied", np.median(st[:, 0] / np.maximum(rt, 1e-3)))
+s0 = st[:, 2] - st[:, 2].min()
+print("row start offsets us: median", np.median(s0) / 100, "max", s0.max() / 100,
+      "kernel span us", (st[:, 3].max() - st[:, 2].min()) / 100)
+order = np.argsort(st[:, 2])
+print("first 12 rows to start:", order[:12].tolist(), "start us", (s0[order[:12]] / 100).round(1).tolist())
 print("cycles per entry (median over rows):", np.median(st[:, 0] / np.maximum(st[:, 1], 1)))
 print("total entries", bn.sum(), "max per CU", bn.max())
