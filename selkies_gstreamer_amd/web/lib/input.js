@@ -214,6 +214,7 @@ export class Input {
   _slot(index) { return Math.min(3, index + this.padOffset); }
 
   _pollPads() {
+    if (this.gamepadsEnabled === false) return;   // gamepadControl {enabled: false} (control.js)
     if (!navigator.getGamepads || !this.pads.size) return;
     for (const gp of navigator.getGamepads()) {
       if (!gp || !this.pads.has(gp.index)) continue;

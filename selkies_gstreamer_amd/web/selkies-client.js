@@ -3,6 +3,9 @@
 // with WebCodecs, plays Opus audio, forwards input, ACKs frames every 50 ms,
 // reports client fps, handles clipboard, uploads, cursor, multi-display hashes.
 import { AudioPipeline } from './lib/audio.js';
+import {
+  ControlApi, FallbackPolicy, ImeComposer, SAFE_DEFAULTS, SharedProbe,
+} from './lib/control.js';
 import { Dashboard, parseRole } from './lib/dashboard.js';
 import { Input } from './lib/input.js';
 import {
@@ -20,7 +23,7 @@ const $ = (id) => document.getElementById(id);
 class Client {
   constructor() {
     this.canvas = $('stream');
-    this.video = new VideoRenderer(this.canvas, (e) => this.status(`decoder error: ${e.message || e}`));
+    this.video = new VideoRenderer(this.canvas, (e) => this.onDecoderError(e));
     this.audio = new AudioPipeline();
     this.input = new Input(this.canvas, (m) => this.sendText(m), () => [this.canvas.width, this.canvas.height]);
     this.ws = null;
@@ -32,6 +35,65 @@ class Client {
     this.timers = [];
     this.lastMetrics = performance.now();
     this.stats = {};
+    this.control = new ControlApi(this);
+    this.fallback = new FallbackPolicy();
+    this.probe = this.display.shared ? new SharedProbe() : null;
+    this.ime = new ImeComposer((m) => this.sendText(m));
+  }
+
+  // ---------------------------------------------------------------- control API host
+  get shared() { return !!this.display.shared; }
+  get displayId() { return this.display.id; }
+  post(obj) { window.postMessage(obj, window.location.origin); }
+  saveSetting(name, value) { this.settings[name] = value; this.saveSettings(); }
+  applySettings(obj) {
+    Object.assign(this.settings, obj);
+    this.saveSettings();
+    this.syncUi();
+    this.sendText(this.settingsMessage());
+  }
+  setManualResolution(w, h) {
+    Object.assign(this.settings, { is_manual_resolution_mode: true, manual_width: w, manual_height: h });
+    this.saveSettings();
+    this.video.reset();
+    this.sendText(`r,${w}x${h},${this.display.id}`);
+  }
+  resetResolution() {
+    Object.assign(this.settings, { is_manual_resolution_mode: false, manual_width: 0, manual_height: 0 });
+    this.saveSettings();
+    this.video.reset();
+    const dpr = this.settings.use_css_scaling ? 1 : (window.devicePixelRatio || 1);
+    this.sendText(`r,${evenDown(window.innerWidth * dpr)}x${evenDown(window.innerHeight * dpr)},${this.display.id}`);
+  }
+  clearVideo() { this.video.reset(); this.video.resize(this.canvas.width, this.canvas.height); }
+  startMic() { this.audio.startMic((b) => this.sendBinary(b)); }
+  stopMic() { this.audio.stopMic(); }
+  audioOn(on) { if (on) this.audio.start(); else this.audio.stop(); }
+  selectAudioDevice(context, deviceId) {
+    if (context === 'output') this.audio.setOutputDevice && this.audio.setOutputDevice(deviceId);
+    else { this.settings.mic_device = deviceId; this.saveSettings(); }
+  }
+  setGamepads(on) { this.input.gamepadsEnabled = on; }
+  setTrackpad(on) { this.input.trackpad = on; }
+  setSynth(v) { this.input.synth = v; }
+  showKeyboard() { const k = $('keyboard-input-assist'); if (k) { k.value = ''; k.focus(); } }
+  fullscreen() { document.documentElement.requestFullscreen(); }
+  setClipboard(text) { this.clipboardOut(text); }
+  updateRendering() {
+    this.canvas.style.imageRendering = this.settings.anti_aliasing === false ? 'pixelated' : 'auto';
+  }
+
+  // Decoder errors: transient ones are survived (the stripe decoder is recreated at the
+  // next keyframe); repeated ones reset to SAFE_DEFAULTS and reload (FallbackPolicy).
+  onDecoderError(e) {
+    this.status(`decoder error: ${e.message || e}`);
+    const act = this.fallback.onError(performance.now(), this.shared);
+    if (!act) return;
+    if (act.resetSettings) { Object.assign(this.settings, SAFE_DEFAULTS); this.saveSettings(); }
+    this.status('video decoding keeps failing: resetting to default settings and reloading');
+    this.killed = true;
+    if (this.ws) this.ws.close();
+    setTimeout(() => window.location.reload(), act.reloadAfterMs);
   }
 
   // ---------------------------------------------------------------- settings
@@ -147,7 +209,15 @@ class Client {
       if (!this.display.shared) this.sendText(`_f,${Math.round(fps)}`);
       this.renderStats();
     }, METRICS_INTERVAL_MS));
+    if (this.probe) {
+      this.timers.push(setInterval(() => {
+        for (const m of this.probe.tick(performance.now())) this.sendText(m);
+        if (this.probe.state === 'error') this.status('no video from the shared session');
+      }, 500));
+    }
   }
+
+  statsSnapshot() { return Object.assign({}, this.stats, { state: this.control.state }); }
 
   stopTimers() {
     for (const t of this.timers) clearInterval(t);
@@ -159,7 +229,7 @@ class Client {
     switch (m.kind) {
       case 'mode':
         if (!this.display.shared) this.sendText(this.settingsMessage());
-        else { this.sendText('STOP_VIDEO'); this.sendText('START_VIDEO'); }
+        else { this.sendText('STOP_VIDEO'); this.sendText('START_VIDEO'); this.probe.reset(performance.now()); }
         if (this.display.player > 0) this.input.attach();   // view-only links send no input
         this.startTimers();
         break;
@@ -204,6 +274,7 @@ class Client {
   onBinary(buf) {
     const pkt = parseFrame(buf);
     if (!pkt) return;
+    if (this.probe && (pkt.type === 'h264' || pkt.type === 'jpeg')) this.probe.onVideo();
     if (pkt.type === 'audio') this.audio.opus(pkt.payload);
     else if (pkt.type === 'h264') {
       if (this.canvas.width < pkt.width || this.canvas.height < pkt.y + pkt.height) {
@@ -306,6 +377,15 @@ class Client {
       this.sendText(document.hidden ? 'STOP_VIDEO' : 'START_VIDEO');
     });
     this.canvas.addEventListener('click', () => { this.canvas.focus(); if (!this.audio.ctx && $('audio').checked) this.audio.start(); });
+    window.addEventListener('message', (ev) => {
+      if (ev.origin !== window.location.origin) return;   // same-origin embedders / dashboards only
+      this.control.handle(ev.data);
+    });
+    const kbd = $('keyboard-input-assist');
+    if (kbd) {
+      kbd.addEventListener('compositionstart', () => this.ime.start());
+      kbd.addEventListener('compositionend', (e) => { this.ime.end(e.data); kbd.value = ''; });
+    }
     this.dashboard = new Dashboard(this);
     this.dashboard.build();
     this.syncUi();

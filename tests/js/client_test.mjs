@@ -2,6 +2,9 @@
 import assertModule from 'assert';
 const assert = assertModule.strict;
 import * as dash from '../../selkies_gstreamer_amd/web/lib/dashboard.js';
+import {
+  ControlApi, FallbackPolicy, SharedProbe, ImeComposer, SAFE_DEFAULTS,
+} from '../../selkies_gstreamer_amd/web/lib/control.js';
 import * as tg from '../../selkies_gstreamer_amd/web/lib/touch-gamepad.js';
 // node < 16 has no btoa/atob (browsers do)
 if (typeof globalThis.btoa === 'undefined') {
@@ -111,6 +114,102 @@ assert.equal(downsampleToS16Mono([a, b], 48000)[10], 0);
   assert.equal(nav.getGamepads().length, 1);
 }
 
+// ---------------------------------------------------------------- postMessage control API
+{
+  const mkHost = (over = {}) => {
+    const h = { sent: [], posted: [], calls: [], saved: {}, shared: false, displayId: 'primary' };
+    const rec = (name) => (...a) => h.calls.push([name, ...a]);
+    Object.assign(h, {
+      sendText: (m) => h.sent.push(m), post: (o) => h.posted.push(o),
+      saveSetting: (k, v) => { h.saved[k] = v; }, applySettings: rec('applySettings'),
+      setManualResolution: (w, hh) => { h.calls.push(['res', w, hh]); h.sent.push(`r,${w}x${hh},primary`); },
+      resetResolution: rec('resetResolution'), clearVideo: rec('clearVideo'), startMic: rec('startMic'),
+      stopMic: rec('stopMic'), audioOn: rec('audioOn'), selectAudioDevice: rec('selectAudioDevice'),
+      setGamepads: rec('setGamepads'), setTrackpad: rec('setTrackpad'), setSynth: rec('setSynth'),
+      showKeyboard: rec('showKeyboard'), fullscreen: rec('fullscreen'), setClipboard: rec('setClipboard'),
+      statsSnapshot: () => ({ fps: 60 }), updateRendering: rec('updateRendering'),
+    }, over);
+    return h;
+  };
+  const h = mkHost();
+  const c = new ControlApi(h);
+  // every reference message type is understood
+  const all = [
+    { type: 'sidebarVisibilityChanged', isOpen: true }, { type: 'setScaleLocally', value: true },
+    { type: 'setSynth', value: 'x' }, { type: 'showVirtualKeyboard' }, { type: 'setUseCssScaling', value: true },
+    { type: 'setAntiAliasing', value: false }, { type: 'setUseBrowserCursors', value: true },
+    { type: 'setManualResolution', width: 1281, height: 721 }, { type: 'resetResolutionToWindow' },
+    { type: 'settings', settings: { framerate: 30 } }, { type: 'getStats' },
+    { type: 'clipboardUpdateFromUI', text: 'hi' }, { type: 'pipelineStatusUpdate', audio: true },
+    { type: 'pipelineControl', pipeline: 'video', enabled: false },
+    { type: 'audioDeviceSelected', context: 'output', deviceId: 'spk' }, { type: 'gamepadControl', enabled: false },
+    { type: 'requestFullscreen' }, { type: 'command', value: 'xterm' }, { type: 'touchinput:trackpad' },
+    { type: 'touchinput:touch' },
+  ];
+  for (const m of all) assert.equal(c.handle(m), true, m.type);
+  assert.equal(c.handle({ type: 'nope' }), false);
+  assert.equal(c.handle(null), false);
+  assert.equal(c.handle({ type: 'setManualResolution', width: 'x', height: 5 }), false);
+  // the WebSocket messages the reference sends for them
+  assert.deepEqual(h.sent, ['r,1280x720,primary', 'STOP_VIDEO', 'cmd,xterm', 'SET_NATIVE_CURSOR_RENDERING,1',
+    'SET_NATIVE_CURSOR_RENDERING,0']);
+  assert.deepEqual(h.posted.find((p) => p.type === 'stats'), { type: 'stats', data: { fps: 60 } });
+  const upd = h.posted.filter((p) => p.type === 'sidebarButtonStatusUpdate');
+  assert.equal(upd.length, 3);   // audio status, video off, gamepad off
+  assert.deepEqual(upd[2], { type: 'sidebarButtonStatusUpdate', video: false, audio: true, microphone: false, gamepad: false });
+  assert.equal(h.saved.use_css_scaling, true);
+  assert.equal(h.saved.anti_aliasing, false);
+  assert.deepEqual(h.calls.find((x) => x[0] === 'applySettings' && x[1].framerate), ['applySettings', { framerate: 30 }]);
+  // pipeline toggles are idempotent; audio only on the primary display; mic start/stop
+  c.handle({ type: 'pipelineControl', pipeline: 'video', enabled: false });
+  assert.equal(h.sent.filter((m) => m === 'STOP_VIDEO').length, 1);
+  c.handle({ type: 'pipelineControl', pipeline: 'audio', enabled: true });
+  c.handle({ type: 'pipelineControl', pipeline: 'microphone', enabled: true });
+  assert.equal(h.sent.includes('START_AUDIO'), false);   // state already on (pipelineStatusUpdate)
+  assert.deepEqual(h.calls.filter((x) => x[0] === 'startMic').length, 1);
+  const h2 = mkHost({ displayId: 'display2' });
+  new ControlApi(h2).handle({ type: 'pipelineControl', pipeline: 'audio', enabled: true });
+  assert.deepEqual(h2.sent, []);
+  // shared (view-only) clients ignore everything that would drive the session
+  const hs = mkHost({ shared: true });
+  const cs = new ControlApi(hs);
+  for (const m of [{ type: 'command', value: 'rm' }, { type: 'setManualResolution', width: 800, height: 600 },
+    { type: 'pipelineControl', pipeline: 'video', enabled: false }, { type: 'clipboardUpdateFromUI', text: 'x' },
+    { type: 'settings', settings: { encoder: 'jpeg' } }]) assert.equal(cs.handle(m), true);
+  assert.deepEqual(hs.sent, []);
+  assert.equal(hs.calls.length, 0);
+
+  // decoder fallback: 3 errors within 10 s -> reset + reload once
+  const fb = new FallbackPolicy();
+  assert.equal(fb.onError(0, false), null);
+  assert.equal(fb.onError(20000, false), null);   // the first one aged out
+  assert.equal(fb.onError(21000, false), null);
+  assert.deepEqual(fb.onError(22000, false), { resetSettings: true, reloadAfterMs: 3000 });
+  assert.equal(fb.onError(22001, false), null);
+  assert.equal(new FallbackPolicy(1).onError(0, true).resetSettings, false);
+  assert.equal(SAFE_DEFAULTS.encoder, 'x264enc');
+
+  // shared-mode probing
+  const pr = new SharedProbe(1000, 3);
+  pr.reset(0);
+  assert.deepEqual(pr.tick(500), []);
+  assert.deepEqual(pr.tick(1000), ['STOP_VIDEO', 'START_VIDEO']);
+  assert.deepEqual(pr.tick(2000), ['STOP_VIDEO', 'START_VIDEO']);
+  assert.deepEqual(pr.tick(3000), []);
+  assert.equal(pr.state, 'error');
+  const pr2 = new SharedProbe(1000, 3);
+  pr2.reset(0);
+  pr2.onVideo();
+  assert.deepEqual(pr2.tick(5000), []);
+  assert.equal(pr2.state, 'streaming');
+
+  // IME: nothing during composition, the committed text as keysyms at the end
+  const out = [];
+  const ime = new ImeComposer((m) => out.push(m));
+  ime.start();
+  assert.equal(ime.end('日本'), 2);
+  assert.deepEqual(out, ['kd,16803301', 'ku,16803301', 'kd,16803628', 'ku,16803628']);
+}
 console.log('client tests ok');
 
 // ---- WebRTC mode (lib/webrtc.js) with fake WebSocket / RTCPeerConnection ----
