@@ -326,8 +326,9 @@ struct PacketWriter {
     int max_pkts;
     bool failed = false;
 
+    int hdr() const { return p->playout_ext_id > 0 && p->playout_ext_id < 15 ? 20 : 12; }
     uint8_t* begin(int payload_len) {
-        const int need = 12 + payload_len + (srtp ? 10 : 0);
+        const int need = hdr() + payload_len + (srtp ? 10 : 0);
         if (count >= max_pkts || used + need > cap) {
             failed = true;
             return nullptr;
@@ -339,12 +340,24 @@ struct PacketWriter {
         h[3] = p->seq & 0xff;
         put_be32(h + 4, p->timestamp);
         put_be32(h + 8, p->ssrc);
-        return h + 12;
+        if (hdr() == 20) {   // X bit, 0xBEDE one-byte profile, 1 word: [id|len-1=2][min 12b][max 12b]
+            h[0] |= 0x10;
+            h[12] = 0xBE;
+            h[13] = 0xDE;
+            h[14] = 0;
+            h[15] = 1;
+            const int mn = p->playout_min & 0xfff, mx = p->playout_max & 0xfff;
+            h[16] = (uint8_t)((p->playout_ext_id << 4) | 2);
+            h[17] = (uint8_t)(mn >> 4);
+            h[18] = (uint8_t)(((mn & 15) << 4) | (mx >> 8));
+            h[19] = (uint8_t)(mx & 0xff);
+        }
+        return h + hdr();
     }
     void end(int payload_len, bool marker) {
         uint8_t* h = out + used;
         if (marker) h[1] |= 0x80;
-        int len = 12 + payload_len;
+        int len = hdr() + payload_len;
         if (srtp) len = rtc_srtp_protect_rtp(srtp, h, len);
         lens[count++] = len;
         used += len;
@@ -640,7 +653,7 @@ int rtc_srtp_unprotect_rtcp(void* p, uint8_t* pkt, int n) {
 int rtc_h264_packetize(void* srtp, const uint8_t* annexb, int n, rtc_rtp_params* p, uint8_t* out, int cap,
                        int* lens, int max_pkts) {
     PacketWriter w{static_cast<Srtp*>(srtp), p, out, cap, 0, 0, lens, max_pkts};
-    const int maxp = p->mtu - 12;
+    const int maxp = p->mtu - ((p->playout_ext_id > 0 && p->playout_ext_id < 15) ? 20 : 12);
     if (maxp < 64) return -1;
     std::vector<Nal> nals = split_annexb(annexb, n);
     const size_t nn = nals.size();
@@ -699,7 +712,7 @@ int rtc_h264_packetize(void* srtp, const uint8_t* annexb, int n, rtc_rtp_params*
 int rtc_h265_packetize(void* srtp, const uint8_t* annexb, int n, rtc_rtp_params* p, uint8_t* out, int cap,
                        int* lens, int max_pkts) {
     PacketWriter w{static_cast<Srtp*>(srtp), p, out, cap, 0, 0, lens, max_pkts};
-    const int maxp = p->mtu - 12;
+    const int maxp = p->mtu - ((p->playout_ext_id > 0 && p->playout_ext_id < 15) ? 20 : 12);
     if (maxp < 64) return -1;
     std::vector<Nal> nals = split_annexb(annexb, n);
     const size_t nn = nals.size();

@@ -67,6 +67,10 @@ struct rtc_rtp_params {
     uint8_t payload_type;
     uint8_t marker;      // raw payloads only (H.264 sets it on the last packet)
     int mtu;             // max RTP packet size before SRTP (e.g. 1200)
+    // playout-delay header extension (http://www.webrtc.org/experiments/rtp-hdrext/playout-delay,
+    // one-byte form, RFC 8285) on every packet when ext id 1..14; delays in 10 ms units
+    // (0/0 = render as soon as decoded). 0 = no extension.
+    int playout_ext_id, playout_min, playout_max;
 };
 // Splits an Annex-B access unit into RFC 6184 packets (single NAL, STAP-A for
 // runs of small NALs such as SPS+PPS, FU-A for large ones), optionally SRTP

@@ -31,6 +31,7 @@ from selkies_gstreamer_amd.server import display as display_mod
 from selkies_gstreamer_amd.server import stats as stats_mod
 from selkies_gstreamer_amd.server.ratecontrol import RateController
 from selkies_gstreamer_amd.server.turn import parse_rtc_config, rtc_config, legacy_rtc_config
+from selkies_gstreamer_amd.webrtc.turn_client import parse_turn_url
 from selkies_gstreamer_amd.webrtc.peer import PeerConnection
 
 from .signalling import SignallingServer
@@ -67,6 +68,8 @@ FLAGS = [
     ("turn_password", "SELKIES_TURN_PASSWORD", "", "long-term TURN password"),
     ("stun_host", "SELKIES_STUN_HOST", "stun.l.google.com", "STUN host"),
     ("stun_port", "SELKIES_STUN_PORT", "19302", "STUN port"),
+    ("ice_transport_policy", "SELKIES_ICE_TRANSPORT_POLICY", "all",
+     "all: host/srflx/relay candidates; relay: only the TURN relay candidate (server behind a UDP-blocking NAT)"),
     ("enable_cloudflare_turn", "SELKIES_ENABLE_CLOUDFLARE_TURN", "false", "Cloudflare TURN (needs network)"),
     ("cloudflare_turn_token_id", "SELKIES_CLOUDFLARE_TURN_TOKEN_ID", "", "Cloudflare token id"),
     ("cloudflare_turn_api_token", "SELKIES_CLOUDFLARE_TURN_API_TOKEN", "", "Cloudflare API token"),
@@ -81,7 +84,8 @@ FLAGS = [
     ("video_bitrate", "SELKIES_VIDEO_BITRATE", "8000", "video bitrate (kbit/s)"),
     ("keyframe_distance", "SELKIES_KEYFRAME_DISTANCE", "-1", "seconds between keyframes (-1: infinite)"),
     ("congestion_control", "SELKIES_CONGESTION_CONTROL", "false", "follow REMB bandwidth estimates"),
-    ("video_packetloss_percent", "SELKIES_VIDEO_PACKETLOSS_PERCENT", "0", "video FEC (NACK/RTX used instead)"),
+    ("video_packetloss_percent", "SELKIES_VIDEO_PACKETLOSS_PERCENT", "0",
+     "expected video packet loss (percent): > 0 adds RED + ULPFEC with that much redundancy (NACK still active)"),
     ("audio_bitrate", "SELKIES_AUDIO_BITRATE", "128000", "audio bitrate (bit/s)"),
     ("audio_channels", "SELKIES_AUDIO_CHANNELS", "2", "audio channels"),
     ("audio_packetloss_percent", "SELKIES_AUDIO_PACKETLOSS_PERCENT", "0", "audio FEC (Opus in-band)"),
@@ -147,6 +151,27 @@ def save_overlay(path: str, args: argparse.Namespace) -> None:
         log.debug("cannot write %s: %s", path, e)
 
 
+def ice_servers_from_rtc(cfg: dict) -> tuple:
+    """(stun (host, port) | None, turn (host, port, user, password) | None) for the
+    server's own ICE agent from an RTCConfiguration dict: the first STUN server and the
+    first UDP TURN server (webrtcbin's stun-server / turn-server, gstwebrtc_app.py:149-197)."""
+    try:
+        stun_urls, turn_urls, _ = parse_rtc_config(cfg)
+    except ValueError:
+        return None, None
+    stun_srv = None
+    for u in stun_urls:
+        host, _, port = u.split(":", 1)[1].partition(":")
+        stun_srv = (host, int(port or 3478))
+        break
+    turn_srv = None
+    for u in turn_urls:
+        turn_srv = parse_turn_url(u)
+        if turn_srv:
+            break
+    return stun_srv, turn_srv
+
+
 def build_rtc_config(args) -> dict:
     """RTC configuration for the browser (and the server's own STUN lookup)."""
     if args.rtc_config_json and os.path.exists(args.rtc_config_json):
@@ -175,8 +200,12 @@ class StreamSession:
         self.send_sdp, self.send_ice = send_sdp, send_ice
         self.fps = int(args.framerate)
         self.rc = RateController(int(args.video_bitrate) * 1000, self.fps)
+        stun_srv, turn_srv = ice_servers_from_rtc(build_rtc_config(args))
         self.pc = PeerConnection(addresses=addresses, video=True, audio=True, data=True,
-                                 video_codec="H265" if self.hevc else "H264")
+                                 video_codec="H265" if self.hevc else "H264", stun_server=stun_srv,
+                                 turn_server=turn_srv,
+                                 fec_percentage=int(float(getattr(args, "video_packetloss_percent", 0) or 0)),
+                                 relay_only=str(getattr(args, "ice_transport_policy", "all")) == "relay")
         self.channel = None
         self.capture = None
         self.audio = None

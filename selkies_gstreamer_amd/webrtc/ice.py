@@ -19,8 +19,13 @@ under the vendored aiortc (webrtc/rtcicetransport.py:1-410). Scope here:
 
 RFC 7983 demultiplexing: STUN stays in the agent, every other datagram
 (DTLS 20-63, RTP/RTCP 128-191) goes to ``on_packet``.
-Relayed (TURN) candidates are not gathered by the server side; browsers still
-use their own TURN relays through our host/srflx candidates.
+Relayed candidates: with a TURN server configured (``turn_server=(host, port,
+user, password)``, from the RTC config's iceServers) the agent allocates a relay on
+its own socket (turn_client.TurnAllocation) and offers a ``relay`` candidate; every
+remote candidate then gets a direct pair and a relayed pair (checks, responses and
+media travel as Send/Data indications, then ChannelData once the selected peer is
+channel-bound). ``relay_only=True`` is the iceTransportPolicy "relay": only the
+relay candidate is offered and only relayed pairs are checked.
 """
 from __future__ import annotations
 
@@ -36,6 +41,7 @@ from dataclasses import dataclass
 from typing import Callable, Optional
 
 from . import stun
+from .turn_client import TurnAllocation
 
 log = logging.getLogger("webrtc.ice")
 
@@ -124,11 +130,13 @@ class _Pair:
     priority: int
     state: str = "waiting"   # waiting, in-progress, succeeded, failed
     nominated: bool = False
+    relayed: bool = False    # local side is the TURN relay candidate
 
 
 class IceAgent:
     def __init__(self, controlling: bool, lite: bool = False, addresses: Optional[list[str]] = None,
-                 port: int = 0, stun_server: Optional[tuple] = None):
+                 port: int = 0, stun_server: Optional[tuple] = None, turn_server: Optional[tuple] = None,
+                 relay_only: bool = False):
         self.controlling = controlling and not lite
         self.lite = lite
         self.local_ufrag = random_string(4)
@@ -139,10 +147,14 @@ class IceAgent:
         self.addresses = addresses
         self.port = port
         self.stun_server = stun_server
+        self.turn_server = turn_server
+        self.relay_only = relay_only
+        self.turn: Optional[TurnAllocation] = None
         self.local_candidates: list[Candidate] = []
         self.remote_candidates: list[Candidate] = []
         self.pairs: dict = {}
         self.selected: Optional[tuple] = None
+        self.selected_relayed = False
         self.state = "new"   # new, checking, connected, failed, closed
         self.on_packet: Callable[[bytes, tuple], None] = lambda data, addr: None
         self.on_state: Callable[[str], None] = lambda st: None
@@ -164,7 +176,8 @@ class IceAgent:
                                                    addr, port, "host"))
         if self.stun_server:
             try:
-                res = await self._request(self.stun_server, stun.Message(stun.BINDING, stun.REQUEST), None,
+                srv = await self._resolve(self.stun_server[0], int(self.stun_server[1]))
+                res = await self._request(srv, stun.Message(stun.BINDING, stun.REQUEST), None,
                                           retries=3, interval=0.2)
                 mapped = res.attrs.get(stun.XOR_MAPPED_ADDRESS)
                 if mapped and all(mapped[0] != c.host for c in self.local_candidates):
@@ -173,7 +186,38 @@ class IceAgent:
                                                            mapped[0], mapped[1], "srflx", base.host, base.port))
             except (asyncio.TimeoutError, OSError) as e:
                 log.info("STUN server %s unreachable: %s", self.stun_server, e)
+        if self.turn_server:
+            host, tport, user, pwd = self.turn_server
+            try:
+                self.turn = TurnAllocation(await self._resolve(host, int(tport)), user, pwd, self._transport.sendto)
+                relayed = await self.turn.allocate()
+                mapped = self.turn.mapped or (self.local_candidates[0].host, port)
+                self.local_candidates.append(Candidate("relay1", 1, "udp", candidate_priority("relay"), relayed[0],
+                                                       relayed[1], "relay", mapped[0], mapped[1]))
+            except (asyncio.TimeoutError, OSError) as e:
+                log.warning("TURN server %s:%s unusable: %s", host, tport, e)
+                self.turn = None
+        if self.relay_only:
+            if self.turn is None:
+                raise ConnectionError("relay-only ICE policy without a TURN allocation")
+            self.local_candidates = [c for c in self.local_candidates if c.type == "relay"]
         return self.local_candidates
+
+    @staticmethod
+    async def _resolve(host: str, port: int, timeout: float = 2.0) -> tuple:
+        """IPv4 address of a STUN/TURN server without blocking the loop (a hostname handed
+        to sendto would resolve synchronously); OSError when it does not resolve in time."""
+        try:
+            return (str(ipaddress.IPv4Address(host)), port)
+        except ValueError:
+            pass
+        loop = asyncio.get_running_loop()
+        try:
+            infos = await asyncio.wait_for(loop.getaddrinfo(host, port, family=socket.AF_INET,
+                                                            type=socket.SOCK_DGRAM), timeout)
+        except asyncio.TimeoutError:
+            raise OSError(f"cannot resolve {host}") from None
+        return (infos[0][4][0], port)
 
     # -- remote description ---------------------------------------------------------
     def set_remote_credentials(self, ufrag: str, pwd: str) -> None:
@@ -193,12 +237,15 @@ class IceAgent:
         if ip.version != 4:
             return
         self.remote_candidates.append(c)
-        key = (c.host, c.port)
-        if key not in self.pairs:
-            local = self.local_candidates[0].priority if self.local_candidates else 0
+        for relayed in ((True,) if self.relay_only else ((False, True) if self.turn else (False,))):
+            key = (c.host, c.port, relayed)
+            if key in self.pairs:
+                continue
+            cands = [lc for lc in self.local_candidates if (lc.type == "relay") == relayed]
+            local = cands[0].priority if cands else 0
             g, d = (local, c.priority) if self.controlling else (c.priority, local)
             prio = (1 << 32) * min(g, d) + 2 * max(g, d) + (1 if g > d else 0)
-            self.pairs[key] = _Pair(key, prio)
+            self.pairs[key] = _Pair((c.host, c.port), prio, relayed=relayed)
             if self.state == "checking" and not self.lite:
                 self._tasks.append(asyncio.ensure_future(self._check(self.pairs[key])))
 
@@ -228,24 +275,35 @@ class IceAgent:
         else:
             req.attrs[stun.ICE_CONTROLLED] = self.tie_breaker
         try:
-            await self._request(pair.remote, req, self.remote_pwd.encode(), retries=7, interval=0.1)
+            if pair.relayed and pair.remote[0] not in self.turn.permissions:
+                await self.turn.create_permission(pair.remote[0])
+            await self._request(pair.remote, req, self.remote_pwd.encode(), retries=7, interval=0.1,
+                                relayed=pair.relayed)
         except (asyncio.TimeoutError, OSError):
             pair.state = "failed"
             return
         pair.state = "succeeded"
         if self.controlling:
             pair.nominated = True
-            self._select(pair.remote)
+            self._select(pair.remote, pair.relayed)
         elif pair.nominated:
-            self._select(pair.remote)
+            self._select(pair.remote, pair.relayed)
 
-    async def _request(self, addr, msg: stun.Message, key: Optional[bytes], retries: int, interval: float):
+    def _send(self, data: bytes, addr, relayed: bool) -> None:
+        if relayed:
+            if self.turn is not None:
+                self.turn.send_to(addr, data)
+        elif self._transport is not None:
+            self._transport.sendto(data, addr)
+
+    async def _request(self, addr, msg: stun.Message, key: Optional[bytes], retries: int, interval: float,
+                       relayed: bool = False):
         fut = asyncio.get_running_loop().create_future()
         self._pending[msg.tid] = (fut, key)
         data = msg.encode(key)
         try:
             for i in range(retries):
-                self._transport.sendto(data, addr)
+                self._send(data, addr, relayed)
                 try:
                     return await asyncio.wait_for(asyncio.shield(fut), interval * (2 ** min(i, 3)))
                 except asyncio.TimeoutError:
@@ -254,12 +312,21 @@ class IceAgent:
         finally:
             self._pending.pop(msg.tid, None)
 
-    def _select(self, remote: tuple) -> None:
+    def _select(self, remote: tuple, relayed: bool = False) -> None:
         if self.selected is None:
             self.selected = remote
-            log.info("ICE selected pair -> %s:%d", *remote)
+            self.selected_relayed = relayed
+            log.info("ICE selected pair -> %s:%d%s", *remote, " (relayed)" if relayed else "")
             self._set_state("connected")
             self._connected.set()
+            if relayed:   # media: 4-byte ChannelData instead of Send indications
+                self._tasks.append(asyncio.ensure_future(self._bind_channel(remote)))
+
+    async def _bind_channel(self, remote: tuple) -> None:
+        try:
+            await self.turn.channel_bind(remote)
+        except (OSError, asyncio.TimeoutError) as e:
+            log.info("TURN channel bind failed (staying on Send indications): %s", e)
 
     def _set_state(self, st: str) -> None:
         if st != self.state:
@@ -278,15 +345,20 @@ class IceAgent:
                 req.attrs[stun.USERNAME] = f"{self.remote_ufrag}:{self.local_ufrag}"
                 req.attrs[stun.PRIORITY] = candidate_priority("prflx")
                 req.attrs[stun.ICE_CONTROLLING if self.controlling else stun.ICE_CONTROLLED] = self.tie_breaker
-                self._transport.sendto(req.encode(self.remote_pwd.encode()), self.selected)
+                self._send(req.encode(self.remote_pwd.encode()), self.selected, self.selected_relayed)
 
     # -- datagrams --------------------------------------------------------------------
-    def _on_datagram(self, data: bytes, addr) -> None:
+    def _on_datagram(self, data: bytes, addr, relayed: bool = False) -> None:
+        if not relayed and self.turn is not None and addr[:2] == self.turn.server:
+            got = self.turn.on_datagram(data)
+            if got is not None:
+                self._on_datagram(got[0], got[1], relayed=True)
+            return
         if not stun.is_stun(data):
-            if self.selected is not None and addr[:2] == self.selected[:2]:
+            if self.selected is not None and addr[:2] == self.selected[:2] and relayed == self.selected_relayed:
                 self._last_rx = time.monotonic()
                 self.on_packet(data, addr)
-            elif self.selected is None and addr[:2] in self.pairs:
+            elif self.selected is None and addr[:2] + (relayed,) in self.pairs:
                 self.on_packet(data, addr)
             return
         try:
@@ -310,51 +382,53 @@ class IceAgent:
                     fut.set_exception(OSError(f"STUN error {msg.attrs.get(stun.ERROR_CODE)}"))
             return
         if msg.method == stun.BINDING and msg.cls == stun.REQUEST:
-            self._on_binding_request(msg, offs, data, addr)
+            self._on_binding_request(msg, offs, data, addr, relayed)
 
-    def _on_binding_request(self, msg: stun.Message, offs: dict, data: bytes, addr) -> None:
+    def _on_binding_request(self, msg: stun.Message, offs: dict, data: bytes, addr, relayed: bool = False) -> None:
         user = msg.attrs.get(stun.USERNAME, "")
         if not user.startswith(self.local_ufrag + ":") or not stun.check_integrity(data, offs,
                                                                                    self.local_pwd.encode()):
-            self._reply_error(msg, addr, 401, "Unauthorized")
+            self._reply_error(msg, addr, 401, "Unauthorized", relayed)
             return
+        if self.relay_only and not relayed:
+            return   # policy "relay": nothing reaches us except through the allocation
         # role conflict (RFC 8445 §7.3.1.1)
         if self.controlling and stun.ICE_CONTROLLING in msg.attrs:
             if self.tie_breaker >= msg.attrs[stun.ICE_CONTROLLING]:
-                self._reply_error(msg, addr, 487, "Role Conflict")
+                self._reply_error(msg, addr, 487, "Role Conflict", relayed)
                 return
             self.controlling = False
         elif not self.controlling and stun.ICE_CONTROLLED in msg.attrs and not self.lite:
             if self.tie_breaker < msg.attrs[stun.ICE_CONTROLLED]:
-                self._reply_error(msg, addr, 487, "Role Conflict")
+                self._reply_error(msg, addr, 487, "Role Conflict", relayed)
                 return
             self.controlling = True
         self._last_rx = time.monotonic()
         res = stun.Message(stun.BINDING, stun.SUCCESS, msg.tid)
         res.attrs[stun.XOR_MAPPED_ADDRESS] = addr[:2]
-        self._transport.sendto(res.encode(self.local_pwd.encode()), addr)
-        key = addr[:2]
+        self._send(res.encode(self.local_pwd.encode()), addr, relayed)
+        key = addr[:2] + (relayed,)
         pair = self.pairs.get(key)
         if pair is None:  # peer-reflexive remote candidate
-            pair = self.pairs[key] = _Pair(key, 0)
+            pair = self.pairs[key] = _Pair(addr[:2], 0, relayed=relayed)
             if not self.lite and self.remote_pwd:
                 self._tasks.append(asyncio.ensure_future(self._check(pair)))
         if stun.USE_CANDIDATE in msg.attrs and not self.controlling:
             pair.nominated = True
             if self.lite or pair.state == "succeeded":
-                self._select(key)
+                self._select(addr[:2], relayed)
             elif self.remote_pwd and pair.state != "in-progress":  # triggered check
                 self._tasks.append(asyncio.ensure_future(self._check(pair)))
 
-    def _reply_error(self, msg: stun.Message, addr, code: int, reason: str) -> None:
+    def _reply_error(self, msg: stun.Message, addr, code: int, reason: str, relayed: bool = False) -> None:
         res = stun.Message(msg.method, stun.ERROR, msg.tid)
         res.attrs[stun.ERROR_CODE] = (code, reason)
-        self._transport.sendto(res.encode(None), addr)
+        self._send(res.encode(None), addr, relayed)
 
     # -- data -----------------------------------------------------------------------------
     def send(self, data: bytes) -> None:
-        if self.selected is not None and self._transport is not None:
-            self._transport.sendto(data, self.selected)
+        if self.selected is not None:
+            self._send(data, self.selected, self.selected_relayed)
 
     @property
     def local_port(self) -> int:
@@ -364,6 +438,9 @@ class IceAgent:
         self._set_state("closed")
         for t in self._tasks:
             t.cancel()
+        if self.turn is not None:
+            await self.turn.close()
+            self.turn = None
         if self._transport:
             self._transport.close()
             self._transport = None

@@ -90,6 +90,14 @@ class JitterBuffer:
     def _pop_frame(self) -> Optional[JitterFrame]:
         """Releases the oldest frame whose packets are all present and that is
         followed by a packet of a later timestamp (or ends with the marker bit)."""
+        # fillers (payload None: ULPFEC packets sharing the RED stream's sequence space)
+        # between frames are consumed here so they never block the next frame
+        while True:
+            p = self._slots[self._origin % self.capacity]
+            if p is None or p.seq != self._origin or p.payload is not None:
+                break
+            self._slots[self._origin % self.capacity] = None
+            self._origin = (self._origin + 1) & 0xFFFF
         frame: list[RtpPacket] = []
         ts = None
         for i in range(self.capacity):
@@ -97,6 +105,8 @@ class JitterBuffer:
             p = self._slots[seq % self.capacity]
             if p is None or p.seq != seq:
                 return None                  # gap: wait for retransmission / reorder
+            if p.payload is None:            # a filler ends the frame before it
+                return self._release(frame, ts, seq) if frame else None
             if ts is None:
                 ts = p.timestamp
             if p.timestamp != ts:

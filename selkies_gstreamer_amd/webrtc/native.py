@@ -13,7 +13,8 @@ _mu = threading.Lock()
 
 class RtpParams(ctypes.Structure):
     _fields_ = [("ssrc", ctypes.c_uint32), ("timestamp", ctypes.c_uint32), ("seq", ctypes.c_uint16),
-                ("payload_type", ctypes.c_uint8), ("marker", ctypes.c_uint8), ("mtu", ctypes.c_int)]
+                ("payload_type", ctypes.c_uint8), ("marker", ctypes.c_uint8), ("mtu", ctypes.c_int),
+                ("playout_ext_id", ctypes.c_int), ("playout_min", ctypes.c_int), ("playout_max", ctypes.c_int)]
 
 
 def lib():
@@ -205,9 +206,16 @@ class RtpPacketizer:
 
     def __init__(self, ssrc: int, payload_type: int, mtu: int = 1200, seq: int = 0):
         self._L = lib()
-        self.params = RtpParams(ssrc, 0, seq & 0xFFFF, payload_type, 0, mtu)
+        self.params = RtpParams(ssrc, 0, seq & 0xFFFF, payload_type, 0, mtu, 0, 0, 0)
         self._out = ctypes.create_string_buffer(1 << 20)
         self._lens = (ctypes.c_int * 4096)()
+
+    def set_playout_delay(self, ext_id: int, min_ms: int = 0, max_ms: int = 0) -> None:
+        """Adds the playout-delay header extension (negotiated extmap id) to every packet;
+        ext_id 0 removes it. Delays are carried in 10 ms units (max 40.95 s)."""
+        self.params.playout_ext_id = ext_id
+        self.params.playout_min = max(0, min(4095, min_ms // 10))
+        self.params.playout_max = max(0, min(4095, max_ms // 10))
 
     @property
     def seq(self) -> int:

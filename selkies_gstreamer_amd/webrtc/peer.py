@@ -24,6 +24,7 @@ import time
 from typing import Callable, Optional
 
 from . import rtp, sdp
+from .fec import FecDecoder, FecEncoder
 from .ice import Candidate, IceAgent
 from .jitterbuffer import JitterBuffer, RtpPacket as JbPacket
 from .rate import RemoteBitrateEstimator
@@ -38,9 +39,11 @@ HISTORY = 2048
 class PeerConnection:
     def __init__(self, *, ice_lite: bool = False, addresses: Optional[list[str]] = None, port: int = 0,
                  stun_server: Optional[tuple] = None, video: bool = True, audio: bool = True, data: bool = True,
-                 mtu: int = 1200, video_codec: str = "H264"):
+                 mtu: int = 1200, video_codec: str = "H264", turn_server: Optional[tuple] = None,
+                 relay_only: bool = False, fec_percentage: int = 0, playout_delay_ms: Optional[tuple] = (0, 0)):
         self.ice_lite = ice_lite
-        self._ice_args = dict(addresses=addresses, port=port, stun_server=stun_server)
+        self._ice_args = dict(addresses=addresses, port=port, stun_server=stun_server, turn_server=turn_server,
+                              relay_only=relay_only)
         self.want = dict(video=video, audio=audio, data=data)
         self.mtu = mtu
         self.ice: Optional[IceAgent] = None
@@ -60,6 +63,10 @@ class PeerConnection:
         self._vpk = RtpPacketizer(self.video_ssrc, self._vpt, mtu - 10, random.getrandbits(16))
         self._apk = RtpPacketizer(self.audio_ssrc, sdp.OPUS_PT, mtu - 10, random.getrandbits(16))
         self._history: dict[int, bytes] = {}
+        self.fec_percentage = fec_percentage      # offered when > 0; active once the answer keeps RED
+        self.playout_delay_ms = playout_delay_ms  # (min, max) ms; None: extension not offered
+        self._fec_tx: Optional[FecEncoder] = None
+        self._fec_rx = FecDecoder()
         self._sent = {"video_packets": 0, "video_bytes": 0, "audio_packets": 0, "audio_bytes": 0,
                       "retransmits": 0, "keyframe_requests": 0}
         self._last_ts = {self.video_ssrc: 0, self.audio_ssrc: 0}
@@ -101,8 +108,22 @@ class PeerConnection:
         self.dtls = Dtls("server")   # actpass: the answerer normally picks active
         self.local_sdp = sdp.build_offer(self.ice.local_ufrag, self.ice.local_pwd, self.dtls.fingerprint,
                                          self.ice.local_candidates, self.video_ssrc, self.audio_ssrc,
-                                         ice_lite=self.ice_lite, video_codec=self.video_codec, **self.want)
+                                         ice_lite=self.ice_lite, video_codec=self.video_codec,
+                                         fec=self.fec_percentage > 0, playout_delay=self.playout_delay_ms is not None,
+                                         **self.want)
         return self.local_sdp.to_string()
+
+    def _apply_negotiated(self) -> None:
+        """After the answer: FEC only if the answer kept RED + ULPFEC, the playout-delay
+        extension only if it kept the extmap (under the id it answered with)."""
+        vid = next((m for m in self.remote_sdp.media if m.kind == "video"), None)
+        if vid is None:
+            return
+        if self.fec_percentage > 0 and sdp.RED_PT in vid.fmts and sdp.ULPFEC_PT in vid.fmts:
+            self._fec_tx = FecEncoder(self.video_ssrc, self.fec_percentage)
+        eid = next((i for i, u in vid.extmap.items() if u == sdp.PLAYOUT_DELAY_URI), None)
+        if eid is not None and self.playout_delay_ms is not None:
+            self._vpk.set_playout_delay(eid, *self.playout_delay_ms)
 
     async def set_remote_description(self, text: str, kind: str) -> None:
         self.remote_sdp = sdp.parse(text)
@@ -113,6 +134,7 @@ class PeerConnection:
             if tr["setup"] == "passive":   # the answerer wants to be the DTLS server
                 self.dtls.set_role("client")
                 self.dtls_role = "client"
+            self._apply_negotiated()
         else:
             # JSEP: the offerer controls unless it is ICE-lite
             await self._gather(controlling=self.remote_sdp.ice_lite)
@@ -258,7 +280,14 @@ class PeerConnection:
         """Sends one H.264 or H.265 access unit (Annex-B) with a 90 kHz timestamp."""
         if self.srtp_tx is None:
             return 0
-        pkts = (self._vpk.h265 if self.video_codec == "H265" else self._vpk.h264)(annexb, timestamp, self.srtp_tx)
+        pack = self._vpk.h265 if self.video_codec == "H265" else self._vpk.h264
+        if self._fec_tx is None:
+            pkts = pack(annexb, timestamp, self.srtp_tx)
+        else:   # RED + ULPFEC over the plaintext packets, then SRTP
+            plain = pack(annexb, timestamp, None)
+            red = self._fec_tx.protect(plain, self._vpk.params.seq)
+            self._vpk.params.seq = (self._vpk.params.seq + len(red) - len(plain)) & 0xFFFF
+            pkts = [self.srtp_tx.protect_rtp(p) for p in red]
         for p in pkts:
             self.ice.send(p)
             self._history[struct.unpack_from("!H", p, 2)[0]] = p
@@ -326,15 +355,31 @@ class PeerConnection:
 
     # -- media receive (test peer / browser-less clients) -----------------------------------------------
     def _on_rtp(self, data: bytes) -> None:
+        if len(data) >= 12 and data[1] & 0x7F == sdp.RED_PT:
+            media, fec_seq = self._fec_rx.push(data)
+            if fec_seq is not None:   # the FEC packet's seq is no loss: a filler for NACK / jitter buffer
+                ssrc = struct.unpack_from("!I", data, 8)[0]
+                self._track_seq(ssrc, fec_seq)
+                jb = self._jitter.setdefault(ssrc, JitterBuffer(capacity=1024))
+                jb.add(JbPacket(fec_seq, struct.unpack_from("!I", data, 4)[0], False, None))
+            for pkt in media:         # unwrapped media, plus FEC-recovered packets
+                self._on_rtp_media(pkt)
+            return
+        self._on_rtp_media(data)
+
+    def _track_seq(self, ssrc: int, seq: int) -> None:
+        exp = self._rx_seq.get(ssrc)
+        if exp is not None and seq != exp and 0 < ((seq - exp) & 0xFFFF) < 64:
+            lost = [(exp + i) & 0xFFFF for i in range((seq - exp) & 0xFFFF)]
+            self.send_rtcp(rtp.nack(self.video_ssrc, ssrc, lost))
+        if exp is None or 0 <= ((seq - exp) & 0xFFFF) < 0x8000:
+            self._rx_seq[ssrc] = (seq + 1) & 0xFFFF
+
+    def _on_rtp_media(self, data: bytes) -> None:
         h = rtp.parse_rtp(data)
         if h is None:
             return
-        exp = self._rx_seq.get(h.ssrc)
-        if exp is not None and h.seq != exp and 0 < ((h.seq - exp) & 0xFFFF) < 64:
-            lost = [(exp + i) & 0xFFFF for i in range((h.seq - exp) & 0xFFFF)]
-            self.send_rtcp(rtp.nack(self.video_ssrc, h.ssrc, lost))
-        if exp is None or 0 <= ((h.seq - exp) & 0xFFFF) < 0x8000:
-            self._rx_seq[h.ssrc] = (h.seq + 1) & 0xFFFF
+        self._track_seq(h.ssrc, h.seq)
         payload = data[h.header_len:]
         if h.payload_type in (sdp.H264_PT, sdp.H265_PT):
             now_ms = time.monotonic() * 1000.0

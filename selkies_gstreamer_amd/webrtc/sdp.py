@@ -18,6 +18,8 @@ from .ice import Candidate
 H264_PT = 97
 H265_PT = 100   # reference: rtph265pay pt=100 (legacy/gstwebrtc_app.py:848-866)
 OPUS_PT = 111
+RED_PT = 123
+ULPFEC_PT = 125
 SCTP_PORT = 5000
 
 
@@ -44,6 +46,11 @@ class Media:
     sctp_port: Optional[int] = None
     max_message_size: Optional[int] = None
     rtcp_mux: bool = False
+    extmap: dict = field(default_factory=dict)     # id -> header extension URI (RFC 8285)
+
+
+PLAYOUT_DELAY_URI = "http://www.webrtc.org/experiments/rtp-hdrext/playout-delay"
+PLAYOUT_DELAY_ID = 6
 
 
 @dataclass
@@ -98,6 +105,8 @@ class SessionDescription:
                 ln.append(f"a=msid:{m.msid}")
             if m.rtcp_mux:
                 ln.append("a=rtcp-mux")
+            for eid, uri in sorted(m.extmap.items()):
+                ln.append(f"a=extmap:{eid} {uri}")
             for pt in m.fmts:
                 if pt in m.rtpmap:
                     ln.append(f"a=rtpmap:{pt} {m.rtpmap[pt]}")
@@ -176,6 +185,11 @@ def parse(text: str) -> SessionDescription:
                     tgt.cname = attr[6:]
             elif name == "msid":
                 tgt.msid = val
+            elif name == "extmap":
+                eid, _, uri = val.partition(" ")
+                eid = eid.split("/")[0]
+                if eid.isdigit():
+                    tgt.extmap[int(eid)] = uri.split()[0] if uri else ""
             elif name == "candidate":
                 try:
                     tgt.candidates.append(Candidate.from_sdp(val))
@@ -212,7 +226,10 @@ def h265_fmtp(level_id: int = 153) -> str:
 def build_offer(ufrag: str, pwd: str, fingerprint: str, candidates: list, video_ssrc: int, audio_ssrc: int,
                 video: bool = True, audio: bool = True, data: bool = True, cname: str = "selkies",
                 ice_lite: bool = False, profile_level_id: str = "42e01f",
-                video_codec: str = "H264") -> SessionDescription:
+                video_codec: str = "H264", fec: bool = False, playout_delay: bool = True) -> SessionDescription:
+    """fec: offer RED + ULPFEC next to the video codec (gstwebrtc_app.py:996-1000);
+    playout_delay: offer the playout-delay header extension (PlayoutDelayExtension,
+    gstwebrtc_app.py:1744-1780)."""
     sd = SessionDescription(session_id=int(time.time() * 1000), ice_lite=ice_lite)
     common = dict(ice_ufrag=ufrag, ice_pwd=pwd, fingerprint=f"sha-256 {fingerprint}", setup="actpass",
                   candidates=list(candidates), end_of_candidates=True)
@@ -221,11 +238,16 @@ def build_offer(ufrag: str, pwd: str, fingerprint: str, candidates: list, video_
             pt, rtpmap, fmtp = H265_PT, "H265/90000", h265_fmtp()
         else:
             pt, rtpmap, fmtp = H264_PT, "H264/90000", h264_fmtp(profile_level_id)
+        fmts, rtpmaps = [pt], {pt: rtpmap}
+        if fec:
+            fmts += [RED_PT, ULPFEC_PT]
+            rtpmaps.update({RED_PT: "red/90000", ULPFEC_PT: "ulpfec/90000"})
         sd.media.append(Media(
-            "video", fmts=[pt], mid=str(len(sd.media)), direction="sendonly", rtcp_mux=True,
-            rtpmap={pt: rtpmap}, fmtp={pt: fmtp},
+            "video", fmts=fmts, mid=str(len(sd.media)), direction="sendonly", rtcp_mux=True,
+            rtpmap=rtpmaps, fmtp={pt: fmtp},
             rtcp_fb={pt: ["nack", "nack pli", "ccm fir", "goog-remb"]}, ssrc=video_ssrc, cname=cname,
-            msid="selkies video0", **common))
+            msid="selkies video0", extmap={PLAYOUT_DELAY_ID: PLAYOUT_DELAY_URI} if playout_delay else {},
+            **common))
     if audio:
         sd.media.append(Media(
             "audio", fmts=[OPUS_PT], mid=str(len(sd.media)), direction="sendonly", rtcp_mux=True,
@@ -249,6 +271,6 @@ def build_answer(offer: SessionDescription, ufrag: str, pwd: str, fingerprint: s
                   rtpmap=dict(om.rtpmap), fmtp=dict(om.fmtp), rtcp_fb={k: list(v) for k, v in om.rtcp_fb.items()},
                   ice_ufrag=ufrag, ice_pwd=pwd, fingerprint=f"sha-256 {fingerprint}", setup=setup,
                   candidates=list(candidates), end_of_candidates=True, sctp_port=om.sctp_port,
-                  max_message_size=om.max_message_size, rtcp_mux=om.rtcp_mux)
+                  max_message_size=om.max_message_size, rtcp_mux=om.rtcp_mux, extmap=dict(om.extmap))
         sd.media.append(m)
     return sd
