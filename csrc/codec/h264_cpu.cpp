@@ -300,7 +300,7 @@ void CpuH264Encoder::code_slice_inter(int s) {
             residual_transform(sy, py, su, pu, sv, pv, tr);
             int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
             mb.type = MB_P_16x16;
-            int qp = quant_mb_with_budget(tr, t.qp, false, mb, coef, host_cavlc_tables());
+            int qp = quant_mb_with_budget(tr, t.qp, false, mb, coef, host_cavlc_tables(), mb_start_qp(t, idx));
             mb.mvx = (int16_t)mvx;
             mb.mvy = (int16_t)mvy;
             mb.ref = (uint8_t)refi;
@@ -406,7 +406,7 @@ void CpuH264Encoder::code_slice_intra(int s) {
                     memcpy(su + y * 8, &src[1][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
                     memcpy(sv + y * 8, &src[2][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
                 }
-                int best_mode, best_cm, start_qp = -1;
+                int best_mode, best_cm, start_qp = mb_start_qp(t, idx);
                 if (pass == 0) {
                     intra_decide(sy, su, sv, top, left, tl, ctop, cleft, ctl, aT, aL, &best_mode, &best_cm);
                 } else {
@@ -581,6 +581,25 @@ void CpuH264Encoder::finish_frame() {
     first_frame = false;
 }
 
+// Per-MB AQ offsets from the source luma (same integer math as k_aq).
+void CpuH264Encoder::compute_aq(int s) {
+    if (cfg.aq_strength <= 0) return;
+    if (aq.size() != (size_t)g.num_mbs()) aq.assign(g.num_mbs(), 0);
+    const SliceTask& t = tasks[s];
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            uint32_t sum = 0, ssq = 0;
+            for (int y = 0; y < 16; y++) {
+                const uint8_t* r = &src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16];
+                for (int x = 0; x < 16; x++) {
+                    sum += r[x];
+                    ssq += (uint32_t)r[x] * r[x];
+                }
+            }
+            aq[(size_t)mby * g.mb_w + mbx] = (int8_t)aq_offset(aq_energy(sum, ssq), cfg.aq_strength);
+        }
+}
+
 void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
                             std::vector<EncodedPacket>& out) {
     load_frame(bgrx, stride);
@@ -592,6 +611,7 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         }
     std::vector<std::vector<uint8_t>> rbsp(g.num_slices);
     for (int s = 0; s < g.num_slices; s++) {
+        if (tasks[s].final_action == ACT_P || tasks[s].final_action == ACT_I) compute_aq(s);
         switch (tasks[s].final_action) {
             case ACT_P: code_slice_inter(s); break;
             case ACT_I: code_slice_intra(s); break;

@@ -45,6 +45,7 @@ struct EncoderConfig {
     int src_width = 0;           // K2: capture size when it differs from width x height (0 = same);
     int src_height = 0;          //     the frame is resampled (bilinear) inside the K1 conversion
     int codec = 0;               // 0 = H.264, 1 = HEVC (hevc_encoder.h: same front end, full frame)
+    int aq_strength = 0;         // MB-level adaptive QP strength, Q4 (16 = 1.0; 0 = off): h264_mb.h aq_offset
 };
 
 struct Geometry {

@@ -38,6 +38,10 @@ class CpuH264Encoder {
     void load_frame(const uint8_t* bgrx, int stride_bytes);  // K1 + K3
     void motion_search(int s);                              // K4 for slice s
     void decide_scenecut(int s);
+    void compute_aq(int s);                                 // AQ offsets of slice s's MBs
+    int mb_start_qp(const SliceTask& t, int idx) const {
+        return cfg.aq_strength > 0 ? aq_start_qp(t.qp, aq[idx]) : -1;
+    }
     void code_slice_inter(int s);
     void code_slice_intra(int s);
     void code_slice_skipall(int s);
@@ -59,6 +63,7 @@ class CpuH264Encoder {
     std::vector<DbInfo> dbinfo;    // deblocking side info of the current frame
     std::vector<int16_t> fs_mv;    // K4a full-search winner per MB (x, y), dirty MBs of P slices
     std::vector<SliceTask> tasks;
+    std::vector<int8_t> aq;        // MB-level QP offsets (cfg.aq_strength > 0), compute_aq()
     std::vector<std::vector<uint8_t>> param_sets;  // per stripe (striped) or [0] (full frame)
     bool first_frame = true;
     bool scaled_ = false;          // K2: capture resampled to width x height

@@ -207,10 +207,36 @@ SK_HD void recon_chroma(const int16_t* coef, int qp, int cbp_c, const uint8_t* p
     }
 }
 
+// Variance-based adaptive quantisation (MB-level AQ, the x264 aq-mode 1 idea in
+// integer form, bit-identical on host and device): the QP offset of a macroblock is
+// strength * (log2(E) - log2(E_ref)), E = luma AC energy sum(x^2) - sum(x)^2 / 256 of
+// the 16x16 source block. Flat areas (gradients, backgrounds) get a lower QP, busy
+// texture a higher one. log2 in Q2 from the leading bit and the next two; strength in
+// Q4 (16 = 1.0); the result is clamped to [kAqMin, kAqMax].
+constexpr int kAqRefQ2 = 58;     // log2(E_ref) = 14.5 (x264's 14.427)
+constexpr int kAqMin = -6, kAqMax = 4;
+SK_HD int aq_log2_q2(uint32_t v) {
+    v += 1;
+    const int e = 31 - __builtin_clz(v);
+    const int frac = e >= 2 ? (int)((v >> (e - 2)) & 3u) : (int)((v << (2 - e)) & 3u);
+    return 4 * e + frac;
+}
+SK_HD int aq_offset(uint32_t energy, int strength_q4) {
+    const int d = ((aq_log2_q2(energy) - kAqRefQ2) * strength_q4 + 32) >> 6;   // Q2 * Q4 = Q6
+    return d < kAqMin ? kAqMin : (d > kAqMax ? kAqMax : d);
+}
+// AC energy of a 16x16 luma block from its pixel sum and sum of squares.
+SK_HD uint32_t aq_energy(uint32_t sum, uint32_t ssq) { return ssq - ((sum * sum) >> 8); }
+// Start QP of a coded macroblock: slice QP + its AQ offset.
+SK_HD int aq_start_qp(int slice_qp, int offset) {
+    const int q = slice_qp + offset;
+    return q < 0 ? 0 : (q > 51 ? 51 : q);
+}
+
 // Quantise with QP escalation so a macroblock never exceeds the A.3.1 bit limit.
 // Returns the final QP; fills mb.cbp / nnz and coef.
-// `start_qp` (>= slice_qp, a multiple of 6 above it) skips escalation steps already known
-// to be needed (intra: found by the open-loop pre-pass).
+// `start_qp` is the first QP tried: the AQ start QP, or (intra) the QP the open-loop
+// pre-pass already found to be needed.
 SK_HD int quant_mb_with_budget(const MbTransform& t, int slice_qp, bool intra16, MbInfo& mb,
                                int16_t* coef, const CavlcTables& T, int start_qp = -1) {
     int qp = start_qp >= 0 ? start_qp : slice_qp;

@@ -62,6 +62,8 @@ struct FrameArgs {
     int num_refs;          // EncoderConfig::num_refs (1 or 2)
     int deblock;           // K7 on: ref = deblocked rec (k_deblock), else k_commit copies rec
     int me_full;           // K4a on: MFMA exhaustive-search candidate per dirty MB
+    int aq_strength;       // MB-level adaptive QP strength (Q4), 0 = off
+    int8_t* aq;            // [num_mbs] AQ offsets (k_aq), valid for MBs of coded slices
     DbInfo* db;            // [num_mbs] deblocking side info (k_deblock_prep)
     uint4* dbe;            // [num_mbs][3] per-MB edge record: bS nibbles, packed filter params (k_deblock_edges)
     int16_t* fs_mv;        // [num_mbs][2] MFMA full-search winner (integer pel)

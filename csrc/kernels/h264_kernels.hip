@@ -1076,6 +1076,34 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
 }
 
 // ---------------------------------------------------------------------------
+// MB-level AQ (h264_mb.h aq_offset): one wave per MB of a coded (P / I) slice, lane =
+// one row quarter (4 pixels); sum and sum of squares by wave reduction.
+__global__ __launch_bounds__(256) void k_aq(FrameArgs a) {
+    const int nmb = a.mb_w * a.mb_h;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (idx >= nmb) return;   // wave-uniform
+    const int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    const int act = a.tasks[mby / a.rows_per_slice].final_action;
+    if (act != ACT_P && act != ACT_I) return;
+    const int l = lane_id();
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + (l >> 2)) * a.stride_y +
+                                                          mbx * 16 + 4 * (l & 3));
+    uint32_t sum = 0, ssq = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t v = (w >> (8 * j)) & 255u;
+        sum += v;
+        ssq += v * v;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o);
+        ssq += __shfl_xor(ssq, o);
+    }
+    if (l == 0) a.aq[idx] = (int8_t)aq_offset(aq_energy(sum, ssq), a.aq_strength);
+}
+
+// ---------------------------------------------------------------------------
 // K6 inter: one wave per MB of a P slice (SKIPALL slices just record skips).
 // 4 waves per workgroup, one MB per wave: the CAVLC tables are loaded once per 4 MBs.
 __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
@@ -1156,7 +1184,8 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     mb.type = MB_P_16x16;
     int rec_l[4], rec_c[4];
     code_mb(src_l, pred_l, src_c, pred_c, t.qp, false, S, mb, rec_l, rec_c,
-            a.coefs + (size_t)idx * kCoefPerMb, T);
+            a.coefs + (size_t)idx * kCoefPerMb, T, nullptr, 0,
+            a.aq_strength > 0 ? aq_start_qp(t.qp, a.aq[idx]) : -1);
     // recon
     uint32_t rw = (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) |
                   ((uint32_t)rec_l[3] << 24);
@@ -1385,7 +1414,7 @@ __global__ __launch_bounds__(256) void k_intra_prep(FrameArgs a) {
     memset(&mb, 0, sizeof(mb));
     int rec_l[4], rec_c[4];
     const int qp = code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c, nullptr, T, nullptr, 0,
-                           -1, true);
+                           a.aq_strength > 0 ? aq_start_qp(t.qp, a.aq[idx]) : -1, true);
     if (l == 0) {
         MbInfo o;
         memset(&o, 0, sizeof(o));
@@ -2368,6 +2397,7 @@ void launch_frontend(const FrameArgs& a, hipStream_t s) {
 void launch_encode(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
     launch_frontend(a, s);
+    if (a.aq_strength > 0) hipLaunchKernelGGL(k_aq, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_intra_prep, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     if (a.rows_per_slice <= 4)

@@ -303,6 +303,7 @@ class HipBackend : public EncoderBackend {
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
         else if (s == "me") { p = args_.me; n = (int64_t)g_.num_mbs() * sizeof(MeResult); }
         else if (s == "mb_dirty") { p = args_.mb_dirty; n = g_.num_mbs(); }
+        else if (s == "aq") { p = args_.aq; n = g_.num_mbs(); }
         else if (s == "stamps") { if (!args_.dbg) return -1; p = args_.dbg; n = 64 * 16 * 8; }
         else if (s == "tasks") {
             n = (int64_t)g_.num_slices * sizeof(SliceTask);
@@ -353,6 +354,8 @@ class HipBackend : public EncoderBackend {
         a.full_range = cfg_.full_range; a.me_range = cfg_.me_range; a.me_iters = cfg_.me_iters;
         a.deblock = cfg_.deblock;
         a.me_full = cfg_.me_full;
+        a.aq_strength = cfg_.codec == 1 ? 0 : cfg_.aq_strength;
+        a.aq = dmalloc<int8_t>(nmb);
         a.num_refs = cfg_.num_refs > 1 ? 2 : 1;
         a.scaled = (cfg_.src_width > 0 && cfg_.src_width != cfg_.width) ||
                    (cfg_.src_height > 0 && cfg_.src_height != cfg_.height);

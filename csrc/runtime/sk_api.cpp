@@ -43,6 +43,7 @@ class CpuBackend : public EncoderBackend {
         else if (s == "me") { p = enc_.me.data(); n = (int64_t)(enc_.me.size() * sizeof(h264::MeResult)); }
         else if (s == "tasks") { p = enc_.tasks.data(); n = (int64_t)(enc_.tasks.size() * sizeof(h264::SliceTask)); }
         else if (s == "mb_dirty") plane(enc_.mb_dirty);
+        else if (s == "aq") { p = enc_.aq.data(); n = (int64_t)enc_.aq.size(); }
         else if (s == "fs_mv") { p = enc_.fs_mv.data(); n = (int64_t)(enc_.fs_mv.size() * 2); }
         else return -1;
         if (dst && cap >= n) memcpy(dst, p, (size_t)n);
@@ -181,7 +182,9 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.src_height = c->src_height > 0 ? c->src_height : 0;
     e.num_refs = c->num_refs > 1 ? 2 : 1;
     e.codec = c->codec == 1 ? 1 : 0;
+    e.aq_strength = c->aq_strength > 0 ? (c->aq_strength > 64 ? 64 : c->aq_strength) : 0;
     if (e.codec == 1) {   // HEVC: full-frame pictures, slices of whole CTB rows, one reference
+        e.aq_strength = 0;   // no cu_qp_delta in this HEVC profile setup
         e.fullframe = 1;
         e.num_refs = 1;
         e.deblock = 0;

@@ -21,6 +21,7 @@ typedef struct sk_h264_config {
     int32_t src_width, src_height;  // capture size if it differs (K2 resample in K1); 0 = width/height
     int32_t num_refs;               // reference pictures (sliding-window DPB): 0/1 = one, 2 = two
     int32_t codec;                  // 0 = H.264 (stripes or full frame), 1 = HEVC Main (full frame, WPP)
+    int32_t aq_strength;            // H.264 MB-level adaptive QP, Q4 (16 = 1.0); 0 = off
 } sk_h264_config;
 
 typedef struct sk_packet {

@@ -32,7 +32,7 @@ class SkH264Config(ctypes.Structure):
         ("scenecut", ctypes.c_int32), ("fps", ctypes.c_float), ("device", ctypes.c_int32),
         ("backend", ctypes.c_int32), ("deblock", ctypes.c_int32), ("me_full", ctypes.c_int32),
         ("shared_copy", ctypes.c_int32), ("src_width", ctypes.c_int32), ("src_height", ctypes.c_int32),
-        ("num_refs", ctypes.c_int32), ("codec", ctypes.c_int32),
+        ("num_refs", ctypes.c_int32), ("codec", ctypes.c_int32), ("aq_strength", ctypes.c_int32),
     ]
 
 
@@ -218,7 +218,10 @@ class H264Encoder:
                  damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
                  backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
-                 src_width: int = 0, src_height: int = 0, num_refs: int = 1, codec: str = "h264"):
+                 src_width: int = 0, src_height: int = 0, num_refs: int = 1, codec: str = "h264",
+                 aq_strength: float = 0.0):
+        """aq_strength: MB-level adaptive QP (h264_mb.h aq_offset), 1.0 = x264 aq-mode 1
+        strength; 0 = constant QP per slice (x264 ultrafast behaviour)."""
         L = lib()
         if backend not in ("cpu", "hip"):
             raise ValueError("backend must be 'cpu' or 'hip'")
@@ -229,7 +232,7 @@ class H264Encoder:
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
                                 device, 1 if backend == "hip" else 0, 1 if deblock else -1,
                                 1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height),
-                                int(num_refs), 1 if codec == "hevc" else 0)
+                                int(num_refs), 1 if codec == "hevc" else 0, int(round(aq_strength * 16)))
         if codec not in ("h264", "hevc"):
             raise ValueError("codec must be 'h264' or 'hevc'")
         self.codec = codec

@@ -176,3 +176,29 @@ def test_gpu_two_frames_in_flight_match_cpu(fullframe):
         ref.append([(p.y, p.key, p.data) for p in cpu.encode(f, t)])
     gpu = H264Encoder(W, H, stripe_height=64, qp=26, backend="hip", fullframe=fullframe)
     assert _two_in_flight(gpu, frames, key_at=5) == ref
+
+
+@pytest.mark.parametrize("fullframe", [False, True])
+@pytest.mark.parametrize("kind", ["desktop", "noise"])
+def test_gpu_aq_matches_cpu(fullframe, kind):
+    """MB-level adaptive QP (k_aq + start QPs in k_code_inter / k_intra_prep): per-MB
+    offsets, QPs and bitstreams identical to the CPU reference; offsets really vary."""
+    W, H = 256, 160
+    cpu, gpu = _pair(W, H, stripe_height=32, fullframe=fullframe, qp=26, aq_strength=1.0)
+    sd = StripeDecoder(W, H)
+    for t, f in enumerate(synthetic_frames(W, H, 5, seed=11, kind=kind)):
+        pc, pg = cpu.encode(f, t), gpu.encode(f, t)
+        ta = cpu.debug_buffer("tasks", TASK_DTYPE)
+        qa = np.frombuffer(cpu.debug_buffer("aq", np.uint8), np.int8).reshape(-1, (W + 15) // 16)
+        qg = np.frombuffer(gpu.debug_buffer("aq", np.uint8), np.int8).reshape(-1, (W + 15) // 16)
+        for task in ta:
+            if task["final_action"] in (1, 2):   # offsets only exist for coded slices
+                rows = slice(task["first_row"], task["first_row"] + task["num_rows"])
+                assert np.array_equal(qa[rows], qg[rows]), f"frame {t}: AQ offsets differ"
+        _compare_state(cpu, gpu, W, t)
+        assert [p.data for p in pg] == [p.data for p in pc], f"frame {t}: bitstreams differ"
+        for p in pg:
+            sd.feed(p.data)
+        if t == 0 and kind == "desktop":
+            assert len(np.unique(qa)) > 1
+        assert psnr(sd.Y, bgrx_to_y709(f)) > 28
