@@ -569,27 +569,26 @@ struct WaveCabac {
     // are the other two (rarer) paths. Only the byte output (every ~8 coded bits)
     // leaves this straight-line code.
     __device__ __forceinline__ void code(uint32_t e) {
-        if (!(e & 0x8000u) && (e & 0xffu) != CTX_TERM) {
+        if (__builtin_expect(!(e & 0x8000u) && (e & 0xffu) != CTX_TERM, 1)) {
+            // context bin, branch-free: both outcomes are computed and selected with
+            // masks (s_cselect / s_and), so the scalar pipe never waits on a branch
             const uint32_t c = e & 0xffu, bin = (e >> 8) & 1u;
             const int wl = (int)(c >> 2), sh = (int)(c & 3u) * 8;
             const uint32_t word = (uint32_t)__builtin_amdgcn_readlane(cs, wl);
             const uint32_t s = (word >> sh) & 0xffu;
             const uint32_t st = s >> 1, mps = s & 1u;
-            const uint32_t lps = ((uint32_t)__builtin_amdgcn_readlane(lps_v, (int)st) >> ((range >> 3) & 24u)) & 0xffu;
+            const uint32_t lps4 = (uint32_t)__builtin_amdgcn_readlane(lps_v, (int)st);
+            const uint32_t nxt = (uint32_t)__builtin_amdgcn_readlane(nxt_v, (int)st);
+            const uint32_t lps = (lps4 >> ((range >> 3) & 24u)) & 0xffu;
             const uint32_t rmps = range - lps;
-            uint32_t ns, r, lo;
-            if (bin != mps) {
-                const uint32_t nxt = (uint32_t)__builtin_amdgcn_readlane(nxt_v, (int)st);
-                ns = (nxt << 1) | (st == 0 ? mps ^ 1u : mps);
-                r = lps;
-                lo = low + rmps;
-            } else {
-                ns = s + (st < 62 ? 2u : 0u);
-                r = rmps;
-                lo = low;
-            }
-            const int nb = 8 - (31 - __builtin_clz(r));   // <= 0 when r >= 256
-            const int k = nb > 0 ? nb : 0;
+            const uint32_t m = 0u - (bin ^ mps);                          // all ones on the LPS path
+            const uint32_t r = (lps & m) | (rmps & ~m);
+            const uint32_t lo = low + (rmps & m);
+            const uint32_t ns_lps = (nxt << 1) | (mps ^ ((st - 1u) >> 31));   // MPS flips at state 0
+            const uint32_t ns_mps = s + (st < 62 ? 2u : 0u);
+            const uint32_t ns = (ns_lps & m) | (ns_mps & ~m);
+            const int z = __builtin_clz(r) - 23;                          // r < 512: shift to >= 256
+            const int k = z & ~(z >> 31);                                 // max(z, 0) without a VALU clamp
             low = lo << k;
             range = r << k;
             bits_left -= k;
@@ -686,7 +685,7 @@ __global__ __launch_bounds__(64) void k_hevc_cabac(HevcArgs A) {
         uint32_t cur = l < nb ? b[l] : 0u;
         for (int base = 0; base < nb; base += 64) {
             const uint32_t nxt = base + 64 + l < nb ? b[base + 64 + l] : 0u;   // prefetch
-            const int m = nb - base < 64 ? nb - base : 64;
+            const int m = __builtin_amdgcn_readfirstlane(nb - base < 64 ? nb - base : 64);   // scalar bound
             for (int i = 0; i < m; i++) E.code((uint32_t)__builtin_amdgcn_readlane((int)cur, i));
             cur = nxt;
         }
