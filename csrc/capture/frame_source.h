@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace sk {
 
@@ -19,6 +20,16 @@ class FrameSource {
     // frame n+1 while frame n is still being encoded.
     virtual int ring() const { return 1; }
     virtual const char* name() const = 0;
+    // K13 on the GPU: with set_cursor_overlay(true) a source that captures the cursor
+    // stops drawing it into the frame and reports it instead; cursor() returns the
+    // state as of the last grab (top-left position in frame coordinates, visibility,
+    // an image serial) and fills `bgra` (premultiplied) when the serial is not `have`.
+    virtual void set_cursor_overlay(bool on) { (void)on; }
+    virtual bool cursor(int* x, int* y, int* w, int* h, unsigned long* serial, unsigned long have,
+                        std::vector<uint8_t>* bgra) {
+        (void)x; (void)y; (void)w; (void)h; (void)serial; (void)have; (void)bgra;
+        return false;
+    }
 };
 
 // X11 region grabber (XShmGetImage of the root window at x,y,w,h). Returns

@@ -155,14 +155,50 @@ class X11Source : public FrameSource {
         cur_ = (cur_ + 1) % kRing;
         XImage* img = seg_[cur_].img;
         if (!api_.ShmGetImage(dpy_, root_, img, x_, y_, AllPlanes)) return nullptr;
-        if (cursor_ && api_.FixesGetCursorImage) composite_cursor(img);
+        if (cursor_ && api_.FixesGetCursorImage) {
+            if (overlay_cursor_) fetch_cursor();
+            else composite_cursor(img);
+        }
         *stride = img->bytes_per_line;
         return (const uint8_t*)img->data;
     }
     int ring() const override { return kRing; }
     const char* name() const override { return "x11-shm"; }
+    void set_cursor_overlay(bool on) override { overlay_cursor_ = on; }
+    bool cursor(int* x, int* y, int* w, int* h, unsigned long* serial, unsigned long have,
+                std::vector<uint8_t>* bgra) override {
+        if (!cursor_ || !overlay_cursor_ || !have_cursor_) return false;
+        *x = cx_;
+        *y = cy_;
+        *w = cw_;
+        *h = ch_;
+        *serial = cserial_;
+        if (have != cserial_ && bgra) *bgra = cpx_;
+        return true;
+    }
 
    private:
+    // Cursor state for the encoder overlay: position every grab, pixels when the
+    // cursor image changes (XFixes cursor_serial).
+    void fetch_cursor() {
+        XFixesCursorImage_* ci = api_.FixesGetCursorImage(dpy_);
+        if (!ci) return;
+        cx_ = ci->x - ci->xhot - x_;
+        cy_ = ci->y - ci->yhot - y_;
+        if (!have_cursor_ || ci->cursor_serial != cserial_ || ci->width != cw_ || ci->height != ch_) {
+            cw_ = ci->width;
+            ch_ = ci->height;
+            cserial_ = ci->cursor_serial;
+            cpx_.resize((size_t)cw_ * ch_ * 4);
+            for (int i = 0; i < cw_ * ch_; i++) {   // ARGB32 longs, premultiplied -> BGRA bytes
+                const uint32_t argb = (uint32_t)ci->pixels[i];
+                for (int c = 0; c < 4; c++) cpx_[(size_t)i * 4 + c] = (uint8_t)(argb >> (8 * c));
+            }
+        }
+        have_cursor_ = true;
+        api_.Free(ci);
+    }
+
     // K13: server-side cursor composite (small, CPU; alpha in ARGB32 longs)
     void composite_cursor(XImage* img) {
         XFixesCursorImage_* ci = api_.FixesGetCursorImage(dpy_);
@@ -201,6 +237,10 @@ class X11Source : public FrameSource {
     Window root_ = 0;
     int x_, y_, w_, h_;
     bool cursor_;
+    bool overlay_cursor_ = false, have_cursor_ = false;
+    int cx_ = 0, cy_ = 0, cw_ = 0, ch_ = 0;
+    unsigned long cserial_ = 0;
+    std::vector<uint8_t> cpx_;
 };
 
 }  // namespace

@@ -46,8 +46,30 @@ CpuH264Encoder::CpuH264Encoder(const EncoderConfig& c) : cfg(c) {
     }
 }
 
+void CpuH264Encoder::set_overlay_image(int slot, const uint8_t* bgra, int w, int h) {
+    if (slot < 0 || slot >= kOverlaySlots) return;
+    w = std::max(0, std::min(w, kOverlayMaxDim));
+    h = std::max(0, std::min(h, kOverlayMaxDim));
+    overlay_img[slot].assign(bgra, bgra + (size_t)w * h * 4);
+    overlay[slot].w = w;
+    overlay[slot].h = h;
+    if (!w || !h) overlay[slot].on = 0;
+}
+
+void CpuH264Encoder::set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy) {
+    if (slot < 0 || slot >= kOverlaySlots) return;
+    OverlayParams& o = overlay[slot];
+    o.on = on && o.w > 0 && o.h > 0;
+    o.x = x;
+    o.y = y;
+    o.tdx = tdx > 0 ? tdx : 0;
+    o.tdy = tdy > 0 ? tdy : 0;
+}
+
 void CpuH264Encoder::load_frame(const uint8_t* bgrx, int stride) {
     const int W = g.W, H = g.H;
+    const bool ov = overlay[0].on || overlay[1].on;
+    const uint8_t* ovimg[kOverlaySlots] = {overlay_img[0].data(), overlay_img[1].data()};
     for (int qy = 0; qy < g.plane_h_c; qy++) {
         int y0 = std::min(2 * qy, H - 1), y1 = std::min(2 * qy + 1, H - 1);
         const uint8_t* r0 = bgrx + (size_t)y0 * stride;
@@ -55,9 +77,25 @@ void CpuH264Encoder::load_frame(const uint8_t* bgrx, int stride) {
         for (int qx = 0; qx < g.stride_c; qx++) {
             int x0 = std::min(2 * qx, W - 1), x1 = std::min(2 * qx + 1, W - 1);
             uint8_t y[4], cb, cr;
-            if (scaled_) {   // K2: bilinear resample of the capture, same integer math as the kernel
-                uint32_t q[4] = {scale_fetch(bgrx, stride, scale_, x0, y0), scale_fetch(bgrx, stride, scale_, x1, y0),
-                                 scale_fetch(bgrx, stride, scale_, x0, y1), scale_fetch(bgrx, stride, scale_, x1, y1)};
+            if (scaled_ || ov) {   // K2: bilinear resample of the capture, same integer math as the kernel
+                uint32_t q[4];
+                if (scaled_) {
+                    q[0] = scale_fetch(bgrx, stride, scale_, x0, y0);
+                    q[1] = scale_fetch(bgrx, stride, scale_, x1, y0);
+                    q[2] = scale_fetch(bgrx, stride, scale_, x0, y1);
+                    q[3] = scale_fetch(bgrx, stride, scale_, x1, y1);
+                } else {
+                    memcpy(&q[0], r0 + 4 * x0, 4);
+                    memcpy(&q[1], r0 + 4 * x1, 4);
+                    memcpy(&q[2], r1 + 4 * x0, 4);
+                    memcpy(&q[3], r1 + 4 * x1, 4);
+                }
+                if (ov) {   // K12/K13 in picture coordinates (padding repeats the edge pixel)
+                    q[0] = overlay_px(q[0], x0, y0, overlay, ovimg);
+                    q[1] = overlay_px(q[1], x1, y0, overlay, ovimg);
+                    q[2] = overlay_px(q[2], x0, y1, overlay, ovimg);
+                    q[3] = overlay_px(q[3], x1, y1, overlay, ovimg);
+                }
                 bgrx_quad_to_yuv((const uint8_t*)&q[0], (const uint8_t*)&q[1], (const uint8_t*)&q[2],
                                  (const uint8_t*)&q[3], cfg.full_range, y, &cb, &cr);
             } else {

@@ -7,6 +7,7 @@
 #include "h264_mb.h"
 #include "h264_deblock.h"
 #include "color.h"
+#include "overlay.h"
 
 namespace sk {
 namespace h264 {
@@ -68,6 +69,11 @@ class CpuH264Encoder {
     bool first_frame = true;
     bool scaled_ = false;          // K2: capture resampled to width x height
     ScaleParams scale_ = {};
+    // K12/K13 overlays (watermark, cursor) blended inside load_frame
+    OverlayParams overlay[kOverlaySlots] = {};
+    std::vector<uint8_t> overlay_img[kOverlaySlots];
+    void set_overlay_image(int slot, const uint8_t* bgra, int w, int h);
+    void set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy);
 
    private:
     void mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb) const;

@@ -1,6 +1,7 @@
 // Device-side buffers and launch interface of the HIP H.264 pipeline.
 #pragma once
 #include <hip/hip_runtime.h>
+#include "../codec/overlay.h"
 #include "../codec/h264_encoder.h"
 #include "../codec/h264_frame.h"
 #include "../codec/h264_deblock.h"
@@ -63,6 +64,8 @@ struct FrameArgs {
     int deblock;           // K7 on: ref = deblocked rec (k_deblock), else k_commit copies rec
     int me_full;           // K4a on: MFMA exhaustive-search candidate per dirty MB
     int aq_strength;       // MB-level adaptive QP strength (Q4), 0 = off
+    const uint8_t* ov_img[kOverlaySlots];   // K12/K13 overlay images (premultiplied BGRA)
+    const OverlayParams* ov;                // [kOverlaySlots] placement of this frame (device copy)
     int8_t* aq;            // [num_mbs] AQ offsets (k_aq), valid for MBs of coded slices
     DbInfo* db;            // [num_mbs] deblocking side info (k_deblock_prep)
     uint4* dbe;            // [num_mbs][3] per-MB edge record: bS nibbles, packed filter params (k_deblock_edges)

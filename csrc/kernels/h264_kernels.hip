@@ -259,6 +259,18 @@ __global__ __launch_bounds__(256) void k_convert_damage(FrameArgs a) {
                 p1[i] = bgrx_px(r1, x0 + i, a.W);
             }
         }
+        {   // K12 watermark / K13 cursor, in picture coordinates (edge padding repeats x = W-1)
+            const OverlayParams o0 = a.ov[0], o1 = a.ov[1];
+            if (o0.on | o1.on) {
+                const OverlayParams op[kOverlaySlots] = {o0, o1};
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const int x = sk_min(x0 + i, a.W - 1);
+                    p0[i] = overlay_px(p0[i], x, y0, op, a.ov_img);
+                    p1[i] = overlay_px(p1[i], x, y1, op, a.ov_img);
+                }
+            }
+        }
         uint32_t ya[2] = {0, 0}, yb[2] = {0, 0}, cbw = 0, crw = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {

@@ -120,6 +120,13 @@ class CaptureSession {
             src_.reset();
             return -1;
         }
+        // H.264 / HEVC encoders composite the cursor themselves (K13 overlay slot 1)
+        cursor_via_enc_ = s.output_mode != 0;
+        cursor_set_ = false;
+        cursor_serial_ = 0;
+        wm_sent_ = nullptr;
+        wm_on_gpu_ = false;
+        src_->set_cursor_overlay(cursor_via_enc_);
         running_ = true;
         registered_device_ = s.use_cpu ? -1 : s.device;
         if (registered_device_ >= 0) device_sessions(registered_device_, +1);
@@ -226,9 +233,40 @@ class CaptureSession {
             std::lock_guard<std::mutex> g(mu_);
             wm = wm_;
         }
-        // the grab buffer is ours (SHM segment / ring / copy of a pool frame is not made:
-        // pool frames are never composited)
-        if (wm && wm->loc >= 0 && !wm->px.empty() && pool_ == nullptr)
+        const bool have_wm = wm && wm->loc >= 0 && !wm->px.empty();
+        if (s_.output_mode != 0 && (have_wm || wm_on_gpu_)) {
+            // H.264 / HEVC: K12 inside the encoder's colour conversion (overlay.h); the
+            // grab buffer is left untouched
+            if (wm.get() != wm_sent_) {
+                wm_sent_ = wm.get();
+                wm_on_gpu_ = have_wm && enc_->set_overlay_image(0, wm->px.data(), wm->w, wm->h) == 0;
+                if (!have_wm) enc_->set_overlay_image(0, nullptr, 0, 0);
+            }
+            if (wm_on_gpu_) {
+                int x, y, tdx, tdy;
+                watermark_place(*wm, id, &x, &y, &tdx, &tdy);
+                enc_->set_overlay_pos(0, 1, x, y, tdx, tdy);
+            }
+        }
+        // K13: the cursor as encoder overlay slot 1 (sources that report it, X11)
+        if (cursor_via_enc_) {
+            int cx, cy, cw, ch;
+            unsigned long serial = 0;
+            if (src_->cursor(&cx, &cy, &cw, &ch, &serial, cursor_serial_, &cursor_px_)) {
+                if (serial != cursor_serial_ || !cursor_set_) {
+                    cursor_set_ = enc_->set_overlay_image(1, cursor_px_.data(), cw, ch) == 0;
+                    cursor_serial_ = serial;
+                    if (!cursor_set_) {   // too large for the overlay buffer: draw it on the host
+                        src_->set_cursor_overlay(false);
+                        cursor_via_enc_ = false;
+                    }
+                }
+                if (cursor_set_) enc_->set_overlay_pos(1, 1, cx, cy, 0, 0);
+            }
+        }
+        // JPEG (or an image the encoder cannot hold): blend on the host into the grab
+        // buffer (ours: SHM segment / ring; pool frames are never composited)
+        if (have_wm && !wm_on_gpu_ && pool_ == nullptr)
             composite_watermark(const_cast<uint8_t*>(px), stride, id, *wm);
         try {
             if (enc_->upload(px, stride, id) < 0 || enc_->launch() < 0) return false;
@@ -367,6 +405,33 @@ class CaptureSession {
         step_cv_.notify_all();
     }
 
+    // Position of the watermark for frame t (location modes of set_watermark); tiled
+    // placement returns the period in tdx/tdy (0 otherwise).
+    void watermark_place(const Watermark& wmk, unsigned t, int* x, int* y, int* tdx, int* tdy) const {
+        const int W = s_.capture_width, H = s_.capture_height, w = wmk.w, h = wmk.h, m = 16;
+        *tdx = *tdy = 0;
+        switch (wmk.loc) {
+            case 0: *x = m; *y = m; break;
+            case 1: *x = W - w - m; *y = m; break;
+            case 2: *x = m; *y = H - h - m; break;
+            case 3: *x = W - w - m; *y = H - h - m; break;
+            case 4: *x = (W - w) / 2; *y = (H - h) / 2; break;
+            case 5: {
+                const int rx = std::max(1, W - w), ry = std::max(1, H - h);
+                const int px_ = (int)((2 * t) % (2 * rx)), py_ = (int)((2 * t) % (2 * ry));
+                *x = px_ < rx ? px_ : 2 * rx - px_;
+                *y = py_ < ry ? py_ : 2 * ry - py_;
+                break;
+            }
+            case 6:    // tiled from (m, m) with a 2m gap
+                *x = m; *y = m; *tdx = w + 2 * m; *tdy = h + 2 * m;
+                break;
+            default:   // unknown location: off screen
+                *x = W; *y = H;
+                break;
+        }
+    }
+
     void composite_watermark(uint8_t* px, int stride, unsigned t, const Watermark& wmk) {
         const int W = s_.capture_width, H = s_.capture_height, w = wmk.w, h = wmk.h;
         auto blit = [&](int x0, int y0) {
@@ -406,6 +471,11 @@ class CaptureSession {
     }
 
     std::shared_ptr<Watermark> wm_;
+    const Watermark* wm_sent_ = nullptr;   // image last handed to the encoder overlay
+    bool wm_on_gpu_ = false;
+    bool cursor_via_enc_ = false, cursor_set_ = false;   // K13 through encoder overlay slot 1
+    unsigned long cursor_serial_ = 0;
+    std::vector<uint8_t> cursor_px_;
     int registered_device_ = -1;
     const uint8_t* pool_ = nullptr;
     sk_frame_cb frame_cb_ = nullptr;

@@ -49,6 +49,16 @@ class EncoderBackend {
     virtual int stage_times(float* dst, int n) { (void)dst; (void)n; return 0; }
     // H.264 rate control hook (QP <= 0 keeps the current value); JPEG ignores it.
     virtual void set_qp(int qp, int paint_qp) { (void)qp; (void)paint_qp; }
+    // K12/K13 overlays (overlay.h), applied inside the colour conversion of the frames
+    // uploaded after the call: slot 0 watermark, 1 cursor; premultiplied BGRA images.
+    virtual int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) {
+        (void)slot; (void)bgra; (void)w; (void)h;
+        return -1;
+    }
+    virtual int set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy) {
+        (void)slot; (void)on; (void)x; (void)y; (void)tdx; (void)tdy;
+        return -1;
+    }
     std::vector<h264::EncodedPacket> packets_;
 
    protected:

@@ -143,6 +143,7 @@ class HipBackend : public EncoderBackend {
         // before launch(n) applies to frame n even when frame n-1 has not planned yet
         for (int i = 0; i < 3; i++) h_key_snap_[p][i] = __atomic_load_n(&h_key_seq_[i], __ATOMIC_SEQ_CST);
         frame_of_[p] = staged_frame_;
+        memcpy(ov_params_host_[p], ov_pending_, sizeof(ov_pending_));   // read by this frame's graph
         if (!staged_on_main_) HIPCHECK(hipStreamWaitEvent(stream_, ev_copy_[p], 0));
         HIPCHECK(hipEventRecord(ev_[3 * p + 1], stream_));
         // convert/damage -> plan -> ME -> code -> CAVLC -> assembly -> commit: one graph,
@@ -278,6 +279,33 @@ class HipBackend : public EncoderBackend {
         return k;
     }
 
+    int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) override {
+        if (slot < 0 || slot >= kOverlaySlots || w < 0 || h < 0 || w > kOverlayMaxDim || h > kOverlayMaxDim) return -1;
+        HIPCHECK(hipSetDevice(device_));
+        const size_t n = (size_t)w * h * 4;
+        if (!ov_stage_) ov_stage_ = hmalloc<uint8_t>((size_t)kOverlayMaxDim * kOverlayMaxDim * 4);
+        HIPCHECK(hipStreamSynchronize(stream_));   // frames in flight may still read the old image
+        if (n) {
+            memcpy(ov_stage_, bgra, n);
+            HIPCHECK(hipMemcpyAsync(ov_img_dev_[slot], ov_stage_, n, hipMemcpyHostToDevice, stream_));
+            HIPCHECK(hipStreamSynchronize(stream_));
+        }
+        ov_pending_[slot].w = w;
+        ov_pending_[slot].h = h;
+        if (!n) ov_pending_[slot].on = 0;
+        return 0;
+    }
+    int set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy) override {
+        if (slot < 0 || slot >= kOverlaySlots) return -1;
+        OverlayParams& o = ov_pending_[slot];
+        o.on = on && o.w > 0 && o.h > 0;
+        o.x = x;
+        o.y = y;
+        o.tdx = tdx > 0 ? tdx : 0;
+        o.tdy = tdy > 0 ? tdy : 0;
+        return 0;
+    }
+
     int64_t debug_buffer(const char* name, void* dst, int64_t cap) override {
         HIPCHECK(hipSetDevice(device_));
         HIPCHECK(hipStreamSynchronize(stream_));
@@ -356,6 +384,14 @@ class HipBackend : public EncoderBackend {
         a.me_full = cfg_.me_full;
         a.aq_strength = cfg_.codec == 1 ? 0 : cfg_.aq_strength;
         a.aq = dmalloc<int8_t>(nmb);
+        for (int k = 0; k < kOverlaySlots; k++) {
+            ov_img_dev_[k] = dmalloc<uint8_t>((size_t)kOverlayMaxDim * kOverlayMaxDim * 4);
+            a.ov_img[k] = ov_img_dev_[k];
+            ov_params_host_[k] = hmalloc<OverlayParams>(kOverlaySlots);   // [parity][slot]
+        }
+        ov_params_dev_ = dmalloc<OverlayParams>(kOverlaySlots);
+        a.ov = ov_params_dev_;
+        memset(ov_pending_, 0, sizeof(ov_pending_));
         a.num_refs = cfg_.num_refs > 1 ? 2 : 1;
         a.scaled = (cfg_.src_width > 0 && cfg_.src_width != cfg_.width) ||
                    (cfg_.src_height > 0 && cfg_.src_height != cfg_.height);
@@ -480,6 +516,9 @@ class HipBackend : public EncoderBackend {
     // rbsp is self-cleaning (k_ep_write); stripe flags are cleared by k_plan.
     void enqueue(int part) {
         if (part == 0) {
+            // this frame's overlay placement (host copy written at launch()) -> device
+            HIPCHECK(hipMemcpyAsync(ov_params_dev_, ov_params_host_[parity_], sizeof(OverlayParams) * kOverlaySlots,
+                                    hipMemcpyHostToDevice, stream_));
             gpu::launch_convert_damage(args_, stream_);
             if (cfg_.codec == 1) {
                 gpu::launch_frontend(args_, stream_);
@@ -652,6 +691,11 @@ class HipBackend : public EncoderBackend {
     std::vector<std::vector<uint8_t>> param_sets_;
     std::vector<void*> dev_allocs_, host_allocs_;
     hipGraphExec_t graph_exec_[2] = {nullptr, nullptr};
+    uint8_t* ov_img_dev_[kOverlaySlots] = {};
+    OverlayParams* ov_params_dev_ = nullptr;
+    OverlayParams* ov_params_host_[2] = {};   // per launch parity: copied into the graph
+    OverlayParams ov_pending_[kOverlaySlots];
+    uint8_t* ov_stage_ = nullptr;
     hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
     hipStream_t copy_stream_ = nullptr;   // shared per device (not owned)

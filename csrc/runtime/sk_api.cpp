@@ -21,6 +21,14 @@ class CpuBackend : public EncoderBackend {
     explicit CpuBackend(const h264::EncoderConfig& c) : enc_(c) {}
     void request_keyframe() override { enc_.request_keyframe(); }
     void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
+    int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) override {
+        enc_.set_overlay_image(slot, bgra, w, h);
+        return 0;
+    }
+    int set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy) override {
+        enc_.set_overlay_pos(slot, on, x, y, tdx, tdy);
+        return 0;
+    }
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         packets_.clear();
         enc_.encode(bgrx, stride, frame_id, packets_);
@@ -102,6 +110,14 @@ class CpuHevcBackend : public EncoderBackend {
     explicit CpuHevcBackend(const h264::EncoderConfig& c) : enc_(c) {}
     void request_keyframe() override { enc_.request_keyframe(); }
     void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
+    int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) override {
+        enc_.fe.set_overlay_image(slot, bgra, w, h);
+        return 0;
+    }
+    int set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy) override {
+        enc_.fe.set_overlay_pos(slot, on, x, y, tdx, tdy);
+        return 0;
+    }
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         packets_.clear();
         enc_.encode(bgrx, stride, frame_id, packets_);
@@ -281,6 +297,12 @@ void* sk_jpeg_create(const sk_jpeg_config* c) {
 void sk_h264_destroy(void* enc) { delete static_cast<EncoderBackend*>(enc); }
 void sk_h264_request_keyframe(void* enc) { static_cast<EncoderBackend*>(enc)->request_keyframe(); }
 void sk_h264_set_qp(void* enc, int qp, int paint_qp) { static_cast<EncoderBackend*>(enc)->set_qp(qp, paint_qp); }
+int sk_h264_set_overlay_image(void* enc, int slot, const uint8_t* bgra, int w, int h) {
+    return static_cast<EncoderBackend*>(enc)->set_overlay_image(slot, bgra, w, h);
+}
+int sk_h264_set_overlay_pos(void* enc, int slot, int on, int x, int y, int tdx, int tdy) {
+    return static_cast<EncoderBackend*>(enc)->set_overlay_pos(slot, on, x, y, tdx, tdy);
+}
 
 int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id) {
     try {

@@ -40,6 +40,12 @@ void sk_h264_destroy(void* enc);
 void sk_h264_request_keyframe(void* enc);
 // Rate control: QP of changed stripes / paint-over from the next frame (<= 0 keeps the value).
 void sk_h264_set_qp(void* enc, int qp, int paint_qp);
+// K12/K13 overlays blended during colour conversion (csrc/codec/overlay.h): slot 0 =
+// watermark, 1 = cursor; premultiplied BGRA, at most 512x512. Positions apply to frames
+// uploaded after the call; tdx/tdy > 0 tile the image with that period. 0 = ok, < 0 =
+// not supported by this encoder (JPEG).
+int sk_h264_set_overlay_image(void* enc, int slot, const uint8_t* bgra, int w, int h);
+int sk_h264_set_overlay_pos(void* enc, int slot, int on, int x, int y, int tdx, int tdy);
 // Encodes one BGRx frame; returns the number of packets (or < 0 on error).
 int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride_bytes, int32_t frame_id);
 // Split encode: submit queues the frame (bgrx must stay valid until finish), finish

@@ -100,6 +100,9 @@ def lib():
         L.sk_h264_destroy.argtypes = [ctypes.c_void_p]
         L.sk_h264_request_keyframe.argtypes = [ctypes.c_void_p]
         L.sk_h264_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.sk_h264_set_overlay_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                                ctypes.c_int]
+        L.sk_h264_set_overlay_pos.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6
         L.sk_h264_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_encode.restype = ctypes.c_int
         L.sk_h264_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
@@ -257,6 +260,26 @@ class H264Encoder:
 
     def request_keyframe(self):
         lib().sk_h264_request_keyframe(self._h)
+
+    def set_overlay(self, slot: int, bgra) -> None:
+        """K12/K13: overlay image for slot 0 (watermark) or 1 (cursor), premultiplied BGRA
+        uint8 (h, w, 4), at most 512x512; None clears it. Blended inside the colour
+        conversion of every following frame (the captured frame is not modified)."""
+        if bgra is None:
+            rc = lib().sk_h264_set_overlay_image(self._h, int(slot), None, 0, 0)
+        else:
+            a = np.ascontiguousarray(bgra, dtype=np.uint8)
+            if a.ndim != 3 or a.shape[2] != 4:
+                raise ValueError("overlay must be (h, w, 4) BGRA")
+            rc = lib().sk_h264_set_overlay_image(self._h, int(slot), a.ctypes.data, a.shape[1], a.shape[0])
+        if rc < 0:
+            raise ValueError("overlay not supported (slot / size / encoder)")
+
+    def set_overlay_pos(self, slot: int, x: int, y: int, tile=None, enabled: bool = True) -> None:
+        """Placement of overlay `slot` for the frames encoded from now on; tile=(dx, dy)
+        repeats the image with that period to the right and downwards."""
+        tdx, tdy = tile if tile else (0, 0)
+        lib().sk_h264_set_overlay_pos(self._h, int(slot), int(bool(enabled)), int(x), int(y), int(tdx), int(tdy))
 
     def set_qp(self, qp: int, paint_qp: int = 0):
         """Rate control: QP for changed / paint-over stripes from the next frame (<= 0 keeps)."""

@@ -191,3 +191,49 @@ def test_capture_watermark(tmp_path):
     patch = canvas[60:76, 108:140].astype(int)
     assert patch[..., 0].mean() > 200 and patch[..., 1].mean() < 60 and patch[..., 2].mean() < 60
     assert canvas[10:20, 10:40, 0].mean() < 200 or canvas[10:20, 10:40, 1].mean() > 60  # not red elsewhere
+
+
+@pytest.mark.parametrize("use_cpu", [1, pytest.param(0, marks=pytest.mark.gpu)])
+def test_capture_watermark_h264_in_encoder(tmp_path, use_cpu):
+    """H.264 capture sessions blend the watermark inside the encoder's colour conversion
+    (K12, overlay.h) instead of writing the grabbed buffer: a pool source (never written)
+    gets the watermark in the decoded picture, bottom-right with a 16 px margin."""
+    import pixelflux
+    from selkies_gstreamer_amd.ops.native import PinnedBuffer, hip_device_count
+    if not use_cpu and hip_device_count() < 1:
+        pytest.skip("no HIP device")
+    png = tmp_path / "wm.png"
+    wm = np.zeros((24, 40, 4), np.uint8)
+    wm[..., 0] = 255   # opaque red (RGBA)
+    wm[..., 3] = 255
+    Image.fromarray(wm, "RGBA").save(png)
+    W, H = 160, 96
+    pool = PinnedBuffer((2, H, W, 4))
+    pool.array[:] = 40
+    before = pool.array.copy()
+    s = pixelflux.default_settings(W, H, use_cpu=use_cpu, source=pixelflux.SOURCE_POOL, step_mode=1, pool_frames=2,
+                                   pool_stride=W * 4, stripe_height=32, output_mode=1, watermark_path=str(png),
+                                   watermark_location_enum=3)
+    s.pool = pool.array.ctypes.data
+    got = []
+
+    def cb(res_ptr, user):
+        r = res_ptr.contents
+        got.append((r.frame_id, r.stripe_y_start, bytes(r.data[:r.size])))
+    cap = pixelflux.ScreenCapture()
+    cap.start_capture(s, pixelflux.StripeCallback(cb))
+    cap.run(3)
+    assert cap.wait(30_000) == 0
+    cap.stop_capture()
+    cap.close()
+    assert np.array_equal(pool.array, before), "the captured frames must not be written"
+    dec = StripeDecoder(W, H)
+    for fid, y, data in got:
+        if fid == 0:
+            dec.feed(data)
+    from tests.h264_util import bgrx_to_y709
+    red = np.zeros((1, 1, 4), np.uint8)
+    red[..., 2] = 255
+    ref_y = int(bgrx_to_y709(red)[0, 0])
+    patch = dec.Y[60:76, 108:140].astype(int)
+    assert abs(patch.mean() - ref_y) < 4 and abs(int(dec.Y[10, 10]) - int(bgrx_to_y709(before[0, :1, :1])[0, 0])) < 4
