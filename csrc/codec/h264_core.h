@@ -503,6 +503,65 @@ SK_HD int i16_mb_type(int pred_mode, int cbp_luma15, int cbp_chroma) {
 }
 
 // Chroma motion compensation sample (8.4.2.2.2), mv in 1/8 chroma pel.
+// ---- quarter-pel luma interpolation (8.4.2.2.1) -----------------------------------
+// Reference samples at clamped coordinates: x in [0, w - 1], y in [ylo, yhi] (the picture
+// a stripe is: rows of its own slice only). Computed on the fly, identically on host
+// and device (no half-pel planes to keep in sync with per-stripe reference commits).
+SK_HD int qp_ref(const uint8_t* ref, int stride, int w, int ylo, int yhi, int x, int y) {
+    return ref[(size_t)sk_clip(y, ylo, yhi) * stride + sk_clip(x, 0, w - 1)];
+}
+SK_HD int qp_tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
+// unclipped horizontal half-sample intermediate b1 at (x + 1/2, y)
+SK_HD int qp_b1(const uint8_t* r, int st, int w, int ylo, int yhi, int x, int y) {
+    return qp_tap6(qp_ref(r, st, w, ylo, yhi, x - 2, y), qp_ref(r, st, w, ylo, yhi, x - 1, y),
+                   qp_ref(r, st, w, ylo, yhi, x, y), qp_ref(r, st, w, ylo, yhi, x + 1, y),
+                   qp_ref(r, st, w, ylo, yhi, x + 2, y), qp_ref(r, st, w, ylo, yhi, x + 3, y));
+}
+SK_HD int qp_h1(const uint8_t* r, int st, int w, int ylo, int yhi, int x, int y) {
+    return qp_tap6(qp_ref(r, st, w, ylo, yhi, x, y - 2), qp_ref(r, st, w, ylo, yhi, x, y - 1),
+                   qp_ref(r, st, w, ylo, yhi, x, y), qp_ref(r, st, w, ylo, yhi, x, y + 1),
+                   qp_ref(r, st, w, ylo, yhi, x, y + 2), qp_ref(r, st, w, ylo, yhi, x, y + 3));
+}
+SK_HD int qp_b(const uint8_t* r, int st, int w, int ylo, int yhi, int x, int y) {
+    return sk_clip255((qp_b1(r, st, w, ylo, yhi, x, y) + 16) >> 5);
+}
+SK_HD int qp_h(const uint8_t* r, int st, int w, int ylo, int yhi, int x, int y) {
+    return sk_clip255((qp_h1(r, st, w, ylo, yhi, x, y) + 16) >> 5);
+}
+SK_HD int qp_j(const uint8_t* r, int st, int w, int ylo, int yhi, int x, int y) {
+    return sk_clip255((qp_tap6(qp_b1(r, st, w, ylo, yhi, x, y - 2), qp_b1(r, st, w, ylo, yhi, x, y - 1),
+                               qp_b1(r, st, w, ylo, yhi, x, y), qp_b1(r, st, w, ylo, yhi, x, y + 1),
+                               qp_b1(r, st, w, ylo, yhi, x, y + 2), qp_b1(r, st, w, ylo, yhi, x, y + 3)) +
+                       512) >> 10);
+}
+// Luma prediction sample at full-sample position (x, y) displaced by the quarter-pel
+// vector (mvx, mvy): Table 8-12 (G, a..s).
+SK_HD int luma_qpel_sample(const uint8_t* r, int st, int w, int ylo, int yhi, int x, int y, int mvx, int mvy) {
+    const int xi = x + (mvx >> 2), yi = y + (mvy >> 2), fx = mvx & 3, fy = mvy & 3;
+    if (!(fx | fy)) return qp_ref(r, st, w, ylo, yhi, xi, yi);
+    if (fy == 0) {
+        const int b = qp_b(r, st, w, ylo, yhi, xi, yi);
+        if (fx == 2) return b;
+        return (qp_ref(r, st, w, ylo, yhi, xi + (fx >> 1), yi) + b + 1) >> 1;   // a (fx 1) / c (fx 3)
+    }
+    if (fx == 0) {
+        const int h = qp_h(r, st, w, ylo, yhi, xi, yi);
+        if (fy == 2) return h;
+        return (qp_ref(r, st, w, ylo, yhi, xi, yi + (fy >> 1)) + h + 1) >> 1;   // d (fy 1) / n (fy 3)
+    }
+    if (fx == 2 && fy == 2) return qp_j(r, st, w, ylo, yhi, xi, yi);
+    if (fx == 2) {   // f (fy 1) / q (fy 3): j with b of the row above / below the half row
+        const int j = qp_j(r, st, w, ylo, yhi, xi, yi);
+        return (qp_b(r, st, w, ylo, yhi, xi, yi + (fy >> 1)) + j + 1) >> 1;
+    }
+    if (fy == 2) {   // i (fx 1) / k (fx 3)
+        const int j = qp_j(r, st, w, ylo, yhi, xi, yi);
+        return (qp_h(r, st, w, ylo, yhi, xi + (fx >> 1), yi) + j + 1) >> 1;
+    }
+    // e, g, p, r: diagonal averages of a horizontal and a vertical half sample
+    return (qp_b(r, st, w, ylo, yhi, xi, yi + (fy >> 1)) + qp_h(r, st, w, ylo, yhi, xi + (fx >> 1), yi) + 1) >> 1;
+}
+
 SK_HD int chroma_mc_sample(const uint8_t* ref, int stride, int w, int h, int x, int y, int mvx,
                            int mvy) {
     int xi = x + (mvx >> 3), yi = y + (mvy >> 3);

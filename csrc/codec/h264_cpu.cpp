@@ -255,7 +255,51 @@ void CpuH264Encoder::motion_search(int s) {
             me[idx].mvy = (int16_t)by;
             me[idx].sad = bsad;
             me[idx].intra_est = dev;
-            me[idx].ref = refi;
+            me[idx].ref = (int16_t)refi;
+            me[idx].fx = me[idx].fy = 0;
+        }
+}
+
+// K4c: quarter-pel refinement of every P macroblock of slice s whose integer SAD is
+// above kSubpelMinSad (after the integer search
+// and the scene-cut decision): the 8 half-sample neighbours of the integer vector, then
+// the 8 quarter-sample neighbours of the best, by SAD against the 6-tap interpolated
+// reference (luma_qpel_sample). A candidate replaces the best only if strictly better.
+void CpuH264Encoder::subpel_refine(int s) {
+    const SliceTask& t = tasks[s];
+    const int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    static const int8_t ring[8][2] = {{-1, -1}, {0, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {0, 1}, {1, 1}};
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            MeResult& r = me[(size_t)mby * g.mb_w + mbx];
+            r.fx = r.fy = 0;
+            if (r.sad <= kSubpelMinSad) continue;
+            const uint8_t* ref = refs(r.ref)[0].data();
+            auto sad_q = [&](int qx, int qy) {
+                int sad = 0;
+                for (int y = 0; y < 16; y++) {
+                    const uint8_t* srow = &src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16];
+                    for (int x = 0; x < 16; x++)
+                        sad += sk_abs((int)srow[x] - luma_qpel_sample(ref, g.stride_y, g.stride_y, ylo, yhi,
+                                                                      mbx * 16 + x, mby * 16 + y, qx, qy));
+                }
+                return sad;
+            };
+            int bx = 4 * r.mvx, by = 4 * r.mvy, best = sad_q(bx, by);
+            for (int step = 2; step >= 1; step--) {
+                const int cx = bx, cy = by;
+                for (int k = 0; k < 8; k++) {
+                    const int qx = cx + step * ring[k][0], qy = cy + step * ring[k][1];
+                    const int c = sad_q(qx, qy);
+                    if (c < best) {
+                        best = c;
+                        bx = qx;
+                        by = qy;
+                    }
+                }
+            }
+            r.fx = (int8_t)(bx - 4 * r.mvx);
+            r.fy = (int8_t)(by - 4 * r.mvy);
         }
 }
 
@@ -275,14 +319,11 @@ void CpuH264Encoder::decide_scenecut(int s) {
 void CpuH264Encoder::mc_luma(int mbx, int mby, int mvx, int mvy, const SliceTask& t,
                              uint8_t* pred, int refi) const {
     int y_lo = t.pic_row0 * 16, y_hi = (t.pic_row0 + t.pic_rows) * 16 - 1;
-    int dx = mvx >> 2, dy = mvy >> 2;  // integer-pel vectors only
-    for (int y = 0; y < 16; y++) {
-        int sy = sk_clip(mby * 16 + y + dy, y_lo, y_hi);
-        for (int x = 0; x < 16; x++) {
-            int sx = sk_clip(mbx * 16 + x + dx, 0, g.stride_y - 1);
-            pred[y * 16 + x] = refs(refi)[0][(size_t)sy * g.stride_y + sx];
-        }
-    }
+    const uint8_t* ref = refs(refi)[0].data();
+    for (int y = 0; y < 16; y++)
+        for (int x = 0; x < 16; x++)
+            pred[y * 16 + x] = (uint8_t)luma_qpel_sample(ref, g.stride_y, g.stride_y, y_lo, y_hi, mbx * 16 + x,
+                                                         mby * 16 + y, mvx, mvy);
 }
 
 void CpuH264Encoder::mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTask& t,
@@ -301,19 +342,20 @@ void CpuH264Encoder::mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTa
 
 void CpuH264Encoder::code_slice_inter(int s) {
     const SliceTask& t = tasks[s];
+    if (cfg.subpel) subpel_refine(s);
     for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
         for (int mbx = 0; mbx < g.mb_w; mbx++) {
             int idx = mby * g.mb_w + mbx;
             MbInfo& mb = mbs[idx];
             memset(&mb, 0, sizeof(mb));
-            int mvx = 4 * me[idx].mvx, mvy = 4 * me[idx].mvy;
+            int mvx = me_qx(me[idx]), mvy = me_qy(me[idx]);
             const int refi = me[idx].ref;
             auto nbr = [&](int ox, int oy, bool ok) {
                 MvNb n;
                 n.avail = ok;
                 n.ref = ok ? me[oy * g.mb_w + ox].ref : -1;
-                n.mvx = ok ? 4 * me[oy * g.mb_w + ox].mvx : 0;
-                n.mvy = ok ? 4 * me[oy * g.mb_w + ox].mvy : 0;
+                n.mvx = ok ? me_qx(me[oy * g.mb_w + ox]) : 0;
+                n.mvy = ok ? me_qy(me[oy * g.mb_w + ox]) : 0;
                 return n;
             };
             bool top = mby > t.first_row;
@@ -472,6 +514,7 @@ void CpuH264Encoder::code_slice_intra(int s) {
                 if (pass == 0) continue;   // mb keeps the modes and the start QP for pass 2
                 me[idx].mvx = me[idx].mvy = 0;
                 me[idx].ref = 0;
+                me[idx].fx = me[idx].fy = 0;
                 uint8_t ry[256], ru[64], rv[64];
                 recon_luma(coef, qp, true, mb.cbp & 15, py, ry);
                 recon_chroma(coef, qp, (mb.cbp >> 4) & 3, pu, pv, ru, rv);
@@ -492,6 +535,7 @@ void CpuH264Encoder::code_slice_skipall(int s) {
             memset(&mbs[idx], 0, sizeof(MbInfo));
             me[idx].mvx = me[idx].mvy = 0;
             me[idx].ref = 0;
+            me[idx].fx = me[idx].fy = 0;
         }
     int y0 = t.first_row * 16, y1 = (t.first_row + t.num_rows) * 16;
     memcpy(&rec[0][(size_t)y0 * g.stride_y], &ref[0][(size_t)y0 * g.stride_y], (size_t)(y1 - y0) * g.stride_y);

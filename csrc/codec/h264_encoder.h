@@ -46,6 +46,7 @@ struct EncoderConfig {
     int src_height = 0;          //     the frame is resampled (bilinear) inside the K1 conversion
     int codec = 0;               // 0 = H.264, 1 = HEVC (hevc_encoder.h: same front end, full frame)
     int aq_strength = 0;         // MB-level adaptive QP strength, Q4 (16 = 1.0; 0 = off): h264_mb.h aq_offset
+    int subpel = 1;              // H.264 quarter-pel refinement of P vectors (K4c); HEVC keeps integer vectors
 };
 
 struct Geometry {

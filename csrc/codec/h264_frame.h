@@ -23,8 +23,15 @@ struct MeResult {
     int16_t mvx, mvy;        // integer-pel motion vector
     int32_t sad;             // SAD of the chosen vector
     int32_t intra_est;       // sum |Y - mean| of the source MB (scene-cut estimate)
-    int32_t ref;             // reference picture index (0 = previous picture, 1 = the one before)
+    int16_t ref;             // reference picture index (0 = previous picture, 1 = the one before)
+    int8_t fx, fy;           // quarter-pel refinement (-3..3) on top of 4 * (mvx, mvy): subpel_refine
 };
+// Integer matches this close (SAD per 16x16, i.e. <= 1 per pixel on average) keep their
+// integer vector: a fractional one could not win back the extra MVD bits.
+constexpr int kSubpelMinSad = 256;
+// Quarter-pel motion vector of an ME result (H.264 MV units).
+SK_HD int me_qx(const MeResult& r) { return 4 * r.mvx + r.fx; }
+SK_HD int me_qy(const MeResult& r) { return 4 * r.mvy + r.fy; }
 
 class CpuH264Encoder {
    public:
@@ -38,6 +45,7 @@ class CpuH264Encoder {
     // ---- stages (public for tests) ----
     void load_frame(const uint8_t* bgrx, int stride_bytes);  // K1 + K3
     void motion_search(int s);                              // K4 for slice s
+    void subpel_refine(int s);                              // K4c: half + quarter-pel refinement
     void decide_scenecut(int s);
     void compute_aq(int s);                                 // AQ offsets of slice s's MBs
     int mb_start_qp(const SliceTask& t, int idx) const {

@@ -219,6 +219,7 @@ void CpuHevcEncoder::code_slice_intra(int s) {
                 cu.qp = (uint8_t)qp;
                 fe.me[idx].mvx = fe.me[idx].mvy = 0;
                 fe.me[idx].ref = 0;
+                fe.me[idx].fx = fe.me[idx].fy = 0;
                 for (int y = 0; y < 16; y++)
                     memcpy(&fe.rec[0][(size_t)(cy * 16 + y) * g.stride_y + cx * 16], ry + y * 16, 16);
                 for (int y = 0; y < 8; y++) {

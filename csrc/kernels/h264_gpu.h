@@ -64,6 +64,7 @@ struct FrameArgs {
     int deblock;           // K7 on: ref = deblocked rec (k_deblock), else k_commit copies rec
     int me_full;           // K4a on: MFMA exhaustive-search candidate per dirty MB
     int aq_strength;       // MB-level adaptive QP strength (Q4), 0 = off
+    int subpel;            // K4c quarter-pel refinement (k_subpel) before K6
     const uint8_t* ov_img[kOverlaySlots];   // K12/K13 overlay images (premultiplied BGRA)
     const OverlayParams* ov;                // [kOverlaySlots] placement of this frame (device copy)
     int8_t* aq;            // [num_mbs] AQ offsets (k_aq), valid for MBs of coded slices

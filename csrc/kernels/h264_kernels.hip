@@ -478,7 +478,8 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
         r.mvy = (int16_t)by;
         r.sad = bsad;
         r.intra_est = dev;
-        r.ref = refi;
+        r.ref = (int16_t)refi;
+        r.fx = r.fy = 0;
         a.me[idx] = r;  // per-slice sums are reduced in k_decide (no same-line atomics)
     }
 }
@@ -1116,10 +1117,128 @@ __global__ __launch_bounds__(256) void k_aq(FrameArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Quarter-pel interpolation through LDS (same values as h264_core.h luma_qpel_sample):
+// a 24x24 window of clamped reference samples around the MB's integer vector, its
+// half-sample planes b (horizontal), h (vertical) and j (centre, from the unclipped b1),
+// then any quarter position (Table 8-12) is one to four LDS reads. Window origin: the
+// integer vector minus 3 samples, so quarter offsets -3..+3 around it stay inside.
+struct QpelLds {
+    uint8_t win[24][24];
+    int16_t b1[24][24];
+    uint8_t bp[24][24], hp[24][24], jp[24][24];
+};
+__device__ __forceinline__ int qtap6(int a, int b, int c, int d, int e, int f) {
+    return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
+}
+__device__ void qpel_fill(QpelLds& Q, const uint8_t* ref, int stride, int w, int ylo, int yhi, int ox, int oy) {
+    const int l = lane_id();
+    for (int i = l; i < 576; i += 64) {
+        const int r = i / 24, c = i - 24 * r;
+        Q.win[r][c] = ref[(size_t)sk_clip(oy + r, ylo, yhi) * stride + sk_clip(ox + c, 0, w - 1)];
+    }
+    wave_sync();
+    for (int i = l; i < 576; i += 64) {
+        const int r = i / 24, c = i - 24 * r;
+        if (c >= 2 && c <= 20) {
+            const int b1 = qtap6(Q.win[r][c - 2], Q.win[r][c - 1], Q.win[r][c], Q.win[r][c + 1], Q.win[r][c + 2],
+                                 Q.win[r][c + 3]);
+            Q.b1[r][c] = (int16_t)b1;
+            Q.bp[r][c] = (uint8_t)sk_clip255((b1 + 16) >> 5);
+        }
+        if (r >= 2 && r <= 20) {
+            const int h1 = qtap6(Q.win[r - 2][c], Q.win[r - 1][c], Q.win[r][c], Q.win[r + 1][c], Q.win[r + 2][c],
+                                 Q.win[r + 3][c]);
+            Q.hp[r][c] = (uint8_t)sk_clip255((h1 + 16) >> 5);
+        }
+    }
+    wave_sync();
+    for (int i = l; i < 576; i += 64) {
+        const int r = i / 24, c = i - 24 * r;
+        if (r >= 2 && r <= 20 && c >= 2 && c <= 20)
+            Q.jp[r][c] = (uint8_t)sk_clip255((qtap6(Q.b1[r - 2][c], Q.b1[r - 1][c], Q.b1[r][c], Q.b1[r + 1][c],
+                                                    Q.b1[r + 2][c], Q.b1[r + 3][c]) + 512) >> 10);
+    }
+    wave_sync();
+}
+// Sample for MB-relative pixel (x, y) at quarter offset (dqx, dqy) in [-3, 3] from the
+// window's integer vector.
+__device__ __forceinline__ int qpel_lookup(const QpelLds& Q, int x, int y, int dqx, int dqy) {
+    const int cx = x + 3 + (dqx >> 2), cy = y + 3 + (dqy >> 2), fx = dqx & 3, fy = dqy & 3;
+    const int G = Q.win[cy][cx];
+    if (!(fx | fy)) return G;
+    if (fy == 0) {
+        const int b = Q.bp[cy][cx];
+        return fx == 2 ? b : ((fx == 1 ? G : Q.win[cy][cx + 1]) + b + 1) >> 1;
+    }
+    if (fx == 0) {
+        const int h = Q.hp[cy][cx];
+        return fy == 2 ? h : ((fy == 1 ? G : Q.win[cy + 1][cx]) + h + 1) >> 1;
+    }
+    if (fx == 2 && fy == 2) return Q.jp[cy][cx];
+    if (fx == 2) return (Q.bp[cy + (fy >> 1)][cx] + Q.jp[cy][cx] + 1) >> 1;
+    if (fy == 2) return (Q.hp[cy][cx + (fx >> 1)] + Q.jp[cy][cx] + 1) >> 1;
+    return (Q.bp[cy + (fy >> 1)][cx] + Q.hp[cy][cx + (fx >> 1)] + 1) >> 1;
+}
+
+// ---------------------------------------------------------------------------
+// K4c quarter-pel refinement (CpuH264Encoder::subpel_refine): one wave per MB of a P
+// slice, lane = 4 pixels of one row; the integer vector, its 8 half-sample and then 8
+// quarter-sample neighbours are scored by SAD against the 6-tap interpolation
+// (luma_qpel_sample, computed on the fly from the reference plane).
+__global__ __launch_bounds__(256) void k_subpel(FrameArgs a) {
+    __shared__ QpelLds Qw[4];
+    QpelLds& Q = Qw[threadIdx.x >> 6];
+    const int nmb = a.mb_w * a.mb_h;
+    const int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    if (idx >= nmb) return;   // wave-uniform; no block barriers below
+    const int mbx = idx % a.mb_w, mby = idx / a.mb_w;
+    const SliceTask t = a.tasks[mby / a.rows_per_slice];
+    if (t.final_action != ACT_P) return;
+    const MeResult r = a.me[idx];
+    const int l = lane_id();
+    if (r.sad <= kSubpelMinSad) {
+        if (l == 0) { a.me[idx].fx = 0; a.me[idx].fy = 0; }
+        return;
+    }
+    const int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
+    qpel_fill(Q, r.ref ? a.ref1.y : a.ref.y, a.stride_y, a.stride_y, ylo, yhi, mbx * 16 + r.mvx - 3,
+              mby * 16 + r.mvy - 3);
+    const int yy = l >> 2, xx = 4 * (l & 3);
+    const uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + yy) * a.stride_y +
+                                                          mbx * 16 + xx);
+    auto sad_q = [&](int dqx, int dqy) __attribute__((always_inline)) {
+        int s = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            s += sk_abs((int)((sw >> (8 * j)) & 255u) - qpel_lookup(Q, xx + j, yy, dqx, dqy));
+        return wave_sum(s);
+    };
+    int bx = 0, by = 0, best = sad_q(0, 0);
+    for (int step = 2; step >= 1; step--) {
+        const int cx = bx, cy = by;
+        for (int k = 0; k < 8; k++) {   // ring order of the host reference
+            const int kk = k < 4 ? k : k + 1;
+            const int qx = cx + step * (kk % 3 - 1), qy = cy + step * (kk / 3 - 1);
+            const int c = sad_q(qx, qy);
+            if (c < best) {
+                best = c;
+                bx = qx;
+                by = qy;
+            }
+        }
+    }
+    if (l == 0) {
+        a.me[idx].fx = (int8_t)bx;
+        a.me[idx].fy = (int8_t)by;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K6 inter: one wave per MB of a P slice (SKIPALL slices just record skips).
 // 4 waves per workgroup, one MB per wave: the CAVLC tables are loaded once per 4 MBs.
 __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     __shared__ MbScratch Sw[4];
+    __shared__ QpelLds Qw[4];   // fractional-MV luma MC
     __shared__ CavlcTables T;
     MbScratch& S = Sw[threadIdx.x >> 6];
     int nmb = a.mb_w * a.mb_h;
@@ -1136,6 +1255,7 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
         a.me[idx].mvx = 0;
         a.me[idx].mvy = 0;
         a.me[idx].ref = 0;
+        a.me[idx].fx = a.me[idx].fy = 0;
     }
     // Blocks with no P macroblock (skipped / intra / out-of-range) leave before the table load.
     const bool coded = valid && t.final_action == ACT_P;
@@ -1148,8 +1268,8 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
         MvNb n;
         n.avail = ok;
         n.ref = ok ? a.me[oy * a.mb_w + ox].ref : -1;
-        n.mvx = ok ? 4 * a.me[oy * a.mb_w + ox].mvx : 0;
-        n.mvy = ok ? 4 * a.me[oy * a.mb_w + ox].mvy : 0;
+        n.mvx = ok ? me_qx(a.me[oy * a.mb_w + ox]) : 0;
+        n.mvy = ok ? me_qy(a.me[oy * a.mb_w + ox]) : 0;
         return n;
     };
     bool top = mby > t.first_row;
@@ -1162,22 +1282,29 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
     int pmx, pmy, smx, smy;
     mv_pred16x16(A, B, C, refi, &pmx, &pmy);
     mv_pskip(A, B, C, &smx, &smy);
-    int mvx = 4 * a.me[idx].mvx, mvy = 4 * a.me[idx].mvy;
+    int mvx = me_qx(a.me[idx]), mvy = me_qy(a.me[idx]);
 
     const int b = l >> 2, r = l & 3;
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
     int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
-    // luma source + integer MC prediction
+    // luma source + MC prediction (integer: one 4-byte load; fractional: 6-tap, qpel)
     int px = mbx * 16 + blk_x(b) * 4, py = mby * 16 + blk_y(b) * 4 + r;
     uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)py * a.stride_y + px);
-    int sy = sk_clip(py + (mvy >> 2), ylo, yhi);
-    uint32_t pw = load_ref4(rp.y + (size_t)sy * a.stride_y, px + (mvx >> 2), a.stride_y);
     int src_l[4], pred_l[4];
+    if (!((mvx | mvy) & 3)) {   // wave-uniform
+        int sy = sk_clip(py + (mvy >> 2), ylo, yhi);
+        uint32_t pw = load_ref4(rp.y + (size_t)sy * a.stride_y, px + (mvx >> 2), a.stride_y);
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        src_l[j] = (sw >> (8 * j)) & 255;
-        pred_l[j] = (pw >> (8 * j)) & 255;
+        for (int j = 0; j < 4; j++) pred_l[j] = (pw >> (8 * j)) & 255;
+    } else {   // fractional: interpolation window through LDS (k_subpel's QpelLds)
+        QpelLds& Q = *reinterpret_cast<QpelLds*>(&Qw[threadIdx.x >> 6]);
+        qpel_fill(Q, rp.y, a.stride_y, a.stride_y, ylo, yhi, mbx * 16 + (mvx >> 2) - 3, mby * 16 + (mvy >> 2) - 3);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            pred_l[j] = qpel_lookup(Q, px - mbx * 16 + j, py - mby * 16, mvx & 3, mvy & 3);
     }
+#pragma unroll
+    for (int j = 0; j < 4; j++) src_l[j] = (sw >> (8 * j)) & 255;
     // chroma source + bilinear MC prediction
     const uint8_t* cs = comp ? a.src.v : a.src.u;
     const uint8_t* crf = comp ? rp.v : rp.u;
@@ -1592,6 +1719,7 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
                     a.me[idx].mvx = 0;
                     a.me[idx].mvy = 0;
                     a.me[idx].ref = 0;
+                    a.me[idx].fx = a.me[idx].fy = 0;
                 }
                 STAMP(step, 7);
             }
@@ -2410,6 +2538,7 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
     launch_frontend(a, s);
     if (a.aq_strength > 0) hipLaunchKernelGGL(k_aq, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
+    if (a.subpel) hipLaunchKernelGGL(k_subpel, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_intra_prep, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     if (a.rows_per_slice <= 4)

@@ -428,6 +428,7 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
                 f.me[idx].mvx = 0;
                 f.me[idx].mvy = 0;
                 f.me[idx].ref = 0;
+                f.me[idx].fx = f.me[idx].fy = 0;
             }
         }
         __syncthreads();   // this step's reconstruction is visible to the next step's neighbours

@@ -199,6 +199,7 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.num_refs = c->num_refs > 1 ? 2 : 1;
     e.codec = c->codec == 1 ? 1 : 0;
     e.aq_strength = c->aq_strength > 0 ? (c->aq_strength > 64 ? 64 : c->aq_strength) : 0;
+    e.subpel = c->subpel >= 0 ? 1 : 0;
     if (e.codec == 1) {   // HEVC: full-frame pictures, slices of whole CTB rows, one reference
         e.aq_strength = 0;   // no cu_qp_delta in this HEVC profile setup
         e.fullframe = 1;

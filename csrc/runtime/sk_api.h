@@ -22,6 +22,7 @@ typedef struct sk_h264_config {
     int32_t num_refs;               // reference pictures (sliding-window DPB): 0/1 = one, 2 = two
     int32_t codec;                  // 0 = H.264 (stripes or full frame), 1 = HEVC Main (full frame, WPP)
     int32_t aq_strength;            // H.264 MB-level adaptive QP, Q4 (16 = 1.0); 0 = off
+    int32_t subpel;                 // H.264 quarter-pel motion refinement: 0 = default (on), < 0 off
 } sk_h264_config;
 
 typedef struct sk_packet {
