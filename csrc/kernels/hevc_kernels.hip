@@ -455,8 +455,14 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
     A.bin_n[idx] = w.n;
 }
 
-// v_writelane equivalent: lane `ln` (wave-uniform) of `v` takes the uniform value `x`.
-__device__ __forceinline__ int writelane(int x, int ln, int v) { return lane() == ln ? x : v; }
+// Lane `ln` (wave-uniform) of `v` takes the uniform value `x`: v_writelane_b32 with the
+// lane index in M0 (one SGPR read per VALU op on gfx9; no compiler builtin for it).
+__device__ __forceinline__ int writelane(int x, int ln, int v) {
+    asm("s_nop 0\n\tv_writelane_b32 %0, %1, m0"
+        : "+v"(v)
+        : "s"(__builtin_amdgcn_readfirstlane(x)), "{m0}"(__builtin_amdgcn_readfirstlane(ln)));
+    return v;
+}
 
 // Streams the bin entries of CUs [first, first + count) of one CTB row, 64 at a time:
 // every lane loads one entry (coalesced, next chunk prefetched), the wave-uniform loop
@@ -517,15 +523,22 @@ __global__ __launch_bounds__(64) void k_hevc_sync(HevcArgs A) {
     }
 }
 
-// One wave per CTB row: the row's CABAC substream, run on the scalar unit. The coder
-// state (low, range, bits_left, carry buffer) is wave-uniform (SGPRs); context states,
-// the LPS range table and the LPS transition table live across the 64 lanes of three,
-// one and one VGPRs and are accessed with v_readlane (and a lane-select write) at a
-// uniform lane index; output bytes are gathered into a VGPR (lane = 4-byte word) and
-// stored 256 bytes at a time by the whole wave.
+// One workgroup of two waves per CTB row codes the row's CABAC substream as a
+// two-stage pipeline through an LDS ring (the coder is SALU-issue bound, so splitting
+// the per-bin work over two waves on two SIMDs roughly halves the time per bin):
+//   modeler wave: context state lookup and transition per context bin (states live
+//                 across the 64 lanes, byte c & 3 of lane c >> 2; v_readlane at a
+//                 uniform index and a lane-select write) and rewrites each entry as
+//                 (LPS state index, is-LPS) -- bypass and terminating entries pass;
+//   coder wave:   the arithmetic coder proper (low, range, outstanding-byte carry) on
+//                 the scalar unit; the LPS range table lives across its lanes.
+// Output bytes are gathered into a VGPR (lane = 4-byte word) and stored 256 bytes at a
+// time by the coder wave. Same arithmetic as CabacEncoder (hevc_core.h).
+constexpr uint32_t kModeled = 0x4000u;   // modelled context bin: bits 0..5 LPS state, bit 6 is-LPS
+constexpr int kRingSize = 1024;          // entries in flight between the two waves (power of two)
+
 struct WaveCabac {
-    int cs;                     // context states: context c is byte c & 3 of lane c >> 2
-    int lps_v, nxt_v;           // CABAC_LPS[lane] packed, CABAC_NEXT_LPS[lane]
+    int lps_v;                  // CABAC_LPS[lane] packed
     uint32_t low, range, buffered, acc;
     int bits_left, nbuf, opos, flushed;
     int ob;                     // output chunk
@@ -564,36 +577,23 @@ struct WaveCabac {
             buffered = lead;
         }
     }
-    // One bin entry (same arithmetic as CabacEncoder): context bins take three
-    // readlanes (state, LPS ranges, LPS transition) and one lane-select write; the
-    // renormalisation shift is a count-leading-zeros; bypass runs and terminating bins
-    // are the other two (rarer) paths. Only the byte output (every ~8 coded bits)
-    // leaves this straight-line code.
+    // One modelled entry: a context bin is one readlane (LPS ranges of its state), a
+    // branch-free MPS/LPS select and a count-leading-zeros renormalisation; bypass runs
+    // and terminating bins are the other two (rarer) paths. Only the byte output (every
+    // ~8 coded bits) leaves this straight-line code.
     __device__ __forceinline__ void code(uint32_t e) {
-        if (__builtin_expect(!(e & 0x8000u) && (e & 0xffu) != CTX_TERM, 1)) {
-            // context bin, branch-free: both outcomes are computed and selected with
-            // masks (s_cselect / s_and), so the scalar pipe never waits on a branch
-            const uint32_t c = e & 0xffu, bin = (e >> 8) & 1u;
-            const int wl = (int)(c >> 2), sh = (int)(c & 3u) * 8;
-            const uint32_t word = (uint32_t)__builtin_amdgcn_readlane(cs, wl);
-            const uint32_t s = (word >> sh) & 0xffu;
-            const uint32_t st = s >> 1, mps = s & 1u;
-            const uint32_t lps4 = (uint32_t)__builtin_amdgcn_readlane(lps_v, (int)st);
-            const uint32_t nxt = (uint32_t)__builtin_amdgcn_readlane(nxt_v, (int)st);
+        if (__builtin_expect((e & 0xC000u) == kModeled, 1)) {
+            const uint32_t lps4 = (uint32_t)__builtin_amdgcn_readlane(lps_v, (int)(e & 63u));
             const uint32_t lps = (lps4 >> ((range >> 3) & 24u)) & 0xffu;
             const uint32_t rmps = range - lps;
-            const uint32_t m = 0u - (bin ^ mps);                          // all ones on the LPS path
+            const uint32_t m = 0u - ((e >> 6) & 1u);                       // all ones on the LPS path
             const uint32_t r = (lps & m) | (rmps & ~m);
             const uint32_t lo = low + (rmps & m);
-            const uint32_t ns_lps = (nxt << 1) | (mps ^ ((st - 1u) >> 31));   // MPS flips at state 0
-            const uint32_t ns_mps = s + (st < 62 ? 2u : 0u);
-            const uint32_t ns = (ns_lps & m) | (ns_mps & ~m);
             const int z = __builtin_clz(r) - 23;                          // r < 512: shift to >= 256
             const int k = z & ~(z >> 31);                                 // max(z, 0) without a VALU clamp
             low = lo << k;
             range = r << k;
             bits_left -= k;
-            cs = writelane((int)((word & ~(0xffu << sh)) | (ns << sh)), wl, cs);
         } else if (e & 0x8000u) {   // bypass run
             const int n = (int)((e >> 12) & 7u) + 1;
             low = (low << n) + range * (e & 0xffu);
@@ -648,62 +648,141 @@ struct WaveCabac {
     }
 };
 
-__global__ __launch_bounds__(64) void k_hevc_cabac(HevcArgs A) {
+struct CabacRing {
+    uint32_t e[kRingSize];
+    int produced, consumed, fin, model_waits;
+};
+__device__ __forceinline__ int lds_acquire(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Modeler wave: context transitions of row cy's entries, 64 modelled entries per ring chunk.
+__device__ __forceinline__ void cabac_model_row(const HevcArgs& A, int cy, bool subset_end, CabacRing& R) {
     const FrameArgs& f = A.f;
-    const int cy = blockIdx.x;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
     const int l = lane();
     const uint8_t* srow = A.sync + (size_t)cy * CTX_COUNT;
-    WaveCabac E;
+    int cs;
     {
         uint32_t w = 0;
         for (int k = 0; k < 4; k++) {
             const int c = 4 * l + k;
             w |= (uint32_t)(c < CTX_COUNT ? srow[c] : 0) << (8 * k);
         }
-        E.cs = (int)w;
+        cs = (int)w;
     }
-    E.lps_v = (int)((uint32_t)CABAC_LPS[l][0] | ((uint32_t)CABAC_LPS[l][1] << 8) | ((uint32_t)CABAC_LPS[l][2] << 16) |
-                    ((uint32_t)CABAC_LPS[l][3] << 24));
-    E.nxt_v = CABAC_NEXT_LPS[l];
-    E.out = A.sub + (size_t)cy * A.sub_stride;
-    E.low = 0;
-    E.range = 510;
-    E.buffered = 0xff;
-    E.acc = 0;
-    E.bits_left = 23;
-    E.nbuf = 0;
-    E.opos = 0;
-    E.flushed = 0;
-    E.ob = 0;
-    const unsigned long long t0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
-    const unsigned long long rt0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;   // 100 MHz
-    int entries = 0;
+    // transition table, lane = LPS state index: byte 0 = next (state << 1) on the MPS path,
+    // byte 1 = next (state << 1 | MPS flip) on the LPS path; the new state byte is the
+    // selected byte XOR the current MPS
+    const int tr_v = (int)(((uint32_t)(l < 62 ? l + 1 : l) << 1) |
+                           ((((uint32_t)CABAC_NEXT_LPS[l] << 1) | (l == 0 ? 1u : 0u)) << 8));
+    int produced = 0, waits = 0;
+    // publish entries [0, m) of `v` (lane = entry) at ring positions produced .. produced + m
+    auto publish = [&](uint32_t v, int m) __attribute__((always_inline)) {
+        while (produced + m - lds_acquire(&R.consumed) > kRingSize) {
+            __builtin_amdgcn_s_sleep(1);
+            waits++;
+        }
+        if (l < m) R.e[(produced + l) & (kRingSize - 1)] = v;
+        produced += m;
+        if (l == 0) lds_release(&R.produced, produced);
+    };
     for (int idx = cy * f.mb_w; idx < (cy + 1) * f.mb_w; idx++) {
         const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
         const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
-        entries += nb;
         uint32_t cur = l < nb ? b[l] : 0u;
         for (int base = 0; base < nb; base += 64) {
-            const uint32_t nxt = base + 64 + l < nb ? b[base + 64 + l] : 0u;   // prefetch
-            const int m = __builtin_amdgcn_readfirstlane(nb - base < 64 ? nb - base : 64);   // scalar bound
-            for (int i = 0; i < m; i++) E.code((uint32_t)__builtin_amdgcn_readlane((int)cur, i));
-            cur = nxt;
+            const uint32_t nxt_in = base + 64 + l < nb ? b[base + 64 + l] : 0u;   // prefetch
+            const int m = __builtin_amdgcn_readfirstlane(nb - base < 64 ? nb - base : 64);
+            for (int i = 0; i < m; i++) {
+                const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)cur, i);
+                if (__builtin_expect((e & 0x80ffu) < (uint32_t)CTX_TERM, 1)) {   // context bin (not bypass / terminate)
+                    const uint32_t c = e & 0xffu, bin = (e >> 8) & 1u;
+                    const int wl = (int)(c >> 2), sh = (int)(c & 3u) * 8;
+                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane(cs, wl);
+                    const uint32_t s = (word >> sh) & 0xffu;
+                    const uint32_t st = s >> 1, mps = s & 1u;
+                    const uint32_t lp = bin ^ mps;
+                    const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane(tr_v, (int)st);
+                    const uint32_t ns = ((tr >> (lp << 3)) & 0xffu) ^ mps;
+                    cs = writelane((int)((word & ~(0xffu << sh)) | (ns << sh)), wl, cs);
+                    cur = (uint32_t)writelane((int)(kModeled | (lp << 6) | st), i, (int)cur);   // in place
+                }
+            }
+            publish(cur, m);
+            cur = nxt_in;
         }
     }
-    if (cy < t.first_row + t.num_rows - 1) E.code(CTX_TERM | (1u << 8));   // end_of_subset_one_bit
-    E.finish();
-    if (A.dbg && l == 0) {
-        A.dbg[4 * cy + 0] = __builtin_amdgcn_s_memtime() - t0;
-        A.dbg[4 * cy + 1] = (unsigned long long)entries;
-        A.dbg[4 * cy + 2] = rt0;
-        A.dbg[4 * cy + 3] = __builtin_amdgcn_s_memrealtime();
+    if (subset_end) publish(CTX_TERM | (1u << 8), 1);   // end_of_subset_one_bit
+    if (l == 0) R.model_waits = waits;   // diagnostics (read after the final barrier)
+    if (l == 0) lds_release(&R.fin, 1);
+}
+
+__global__ __launch_bounds__(128) void k_hevc_cabac(HevcArgs A) {
+    __shared__ CabacRing R;
+    const FrameArgs& f = A.f;
+    const int cy = blockIdx.x;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const int l = lane();
+    const bool coder = threadIdx.x >= 64;
+    if (threadIdx.x == 0) {
+        R.produced = 0;
+        R.consumed = 0;
+        R.fin = 0;
     }
+    __syncthreads();
+    WaveCabac E;
+    E.out = A.sub + (size_t)cy * A.sub_stride;
+    E.flushed = 0;
+    E.opos = 0;
+    if (!coder) {
+        cabac_model_row(A, cy, cy < t.first_row + t.num_rows - 1, R);
+    } else {
+        E.lps_v = (int)((uint32_t)CABAC_LPS[l][0] | ((uint32_t)CABAC_LPS[l][1] << 8) |
+                        ((uint32_t)CABAC_LPS[l][2] << 16) | ((uint32_t)CABAC_LPS[l][3] << 24));
+        E.low = 0;
+        E.range = 510;
+        E.buffered = 0xff;
+        E.acc = 0;
+        E.bits_left = 23;
+        E.nbuf = 0;
+        E.ob = 0;
+        const unsigned long long t0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
+        const unsigned long long rt0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;   // 100 MHz
+        int done = 0, waits = 0;
+        for (;;) {
+            const int fin = lds_acquire(&R.fin);   // before `produced`: once set, produced is final
+            const int avail = lds_acquire(&R.produced) - done;
+            if (avail > 0) {
+                const uint32_t v = R.e[(done + l) & (kRingSize - 1)];
+                const int m = __builtin_amdgcn_readfirstlane(avail < 64 ? avail : 64);
+                for (int i = 0; i < m; i++) E.code((uint32_t)__builtin_amdgcn_readlane((int)v, i));
+                done += m;
+                if (l == 0) lds_release(&R.consumed, done);
+            } else if (fin) {
+                break;
+            } else {
+                __builtin_amdgcn_s_sleep(1);
+                waits++;
+            }
+        }
+        E.finish();
+        if (A.dbg && l == 0) {
+            A.dbg[4 * cy + 0] = __builtin_amdgcn_s_memtime() - t0;
+            A.dbg[4 * cy + 1] = (unsigned long long)done | ((unsigned long long)waits << 24) |
+                                ((unsigned long long)lds_acquire(&R.model_waits) << 44);
+            A.dbg[4 * cy + 2] = rt0;
+            A.dbg[4 * cy + 3] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+    __syncthreads();   // the coder wave's substream bytes are visible to its own lanes
+    if (!coder) return;
     uint8_t* out = E.out;
     const int size = E.flushed + E.opos;
     if (l == 0) A.sub_size[cy] = size;
     // emulation-prevention count (wave-parallel, same rule as k_hevc_ep_copy)
-    __syncthreads();
     int last_nz = -1, ins_total = 0;
     for (int base = 0; base < size; base += 64) {
         const int i = base + l;
@@ -826,7 +905,7 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
     hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_cabac, dim3(a.f.mb_h), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_cabac, dim3(a.f.mb_h), dim3(128), 0, s, a);
     hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h), dim3(64), 0, s, a);
 }
