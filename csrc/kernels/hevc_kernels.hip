@@ -523,64 +523,66 @@ __global__ __launch_bounds__(64) void k_hevc_sync(HevcArgs A) {
     }
 }
 
-// One workgroup of two waves per CTB row codes the row's CABAC substream as a
-// two-stage pipeline through an LDS ring (the coder is SALU-issue bound, so splitting
-// the per-bin work over two waves on two SIMDs roughly halves the time per bin):
+// One workgroup of three waves per CTB row codes the row's CABAC substream as a
+// pipeline through two LDS rings (each stage is SALU-issue bound on one wave, so the
+// per-bin work is spread over three SIMDs):
 //   modeler wave: context state lookup and transition per context bin (states live
 //                 across the 64 lanes, byte c & 3 of lane c >> 2; v_readlane at a
-//                 uniform index and a lane-select write) and rewrites each entry as
+//                 uniform index, v_writelane back) and rewrites each entry as
 //                 (LPS state index, is-LPS) -- bypass and terminating entries pass;
-//   coder wave:   the arithmetic coder proper (low, range, outstanding-byte carry) on
-//                 the scalar unit; the LPS range table lives across its lanes.
-// Output bytes are gathered into a VGPR (lane = 4-byte word) and stored 256 bytes at a
-// time by the coder wave. Same arithmetic as CabacEncoder (hevc_core.h).
+//   coder wave:   the arithmetic coder proper (low, range) on the scalar unit, the LPS
+//                 range table across its lanes; every 8 settled bits it hands the
+//                 9-bit "lead" (byte + carry) to the writer;
+//   writer wave:  outstanding-byte / carry resolution, byte packing (lane = 4-byte
+//                 word, 256-byte wave stores) and the emulation-prevention count.
+// Same arithmetic and bytes as CabacEncoder (hevc_core.h).
 constexpr uint32_t kModeled = 0x4000u;   // modelled context bin: bits 0..5 LPS state, bit 6 is-LPS
-constexpr int kRingSize = 1024;          // entries in flight between the two waves (power of two)
+constexpr int kRingSize = 1024;          // entries in flight modeler -> coder (power of two)
+constexpr int kLeadRing = 256;           // tokens in flight coder -> writer (power of two)
+constexpr uint32_t kTokFlush = 0x1000u;  // writer token: resolve outstanding bytes, carry in bit 0
+constexpr uint32_t kTokRaw = 0x2000u;    // writer token: literal byte in bits 0..7
+
+struct CabacRing {
+    uint32_t e[kRingSize];
+    uint32_t lead[kLeadRing];
+    int produced, consumed, fin, model_waits;
+    int lead_produced, lead_consumed, lead_fin;
+};
+__device__ __forceinline__ int lds_acquire(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 struct WaveCabac {
     int lps_v;                  // CABAC_LPS[lane] packed
-    uint32_t low, range, buffered, acc;
-    int bits_left, nbuf, opos, flushed;
-    int ob;                     // output chunk
-    uint8_t* out;
+    uint32_t low, range;
+    int bits_left;
+    int leads, lpos, lprod;     // writer tokens gathered in a VGPR (lane = token)
+    CabacRing* R;
 
-    __device__ __forceinline__ void put(uint32_t byte) {
-        acc |= (byte & 0xffu) << (8 * (opos & 3));
-        opos++;
-        if ((opos & 3) == 0) {
-            ob = writelane((int)acc, (opos >> 2) - 1, ob);
-            acc = 0;
-            if (opos == 256) {
-                reinterpret_cast<int*>(out + flushed)[lane()] = ob;
-                flushed += 256;
-                opos = 0;
-            }
-        }
+    __device__ __forceinline__ void publish() {
+        const int l = lane();
+        while (lprod + lpos - lds_acquire(&R->lead_consumed) > kLeadRing) __builtin_amdgcn_s_sleep(1);
+        if (l < lpos) R->lead[(lprod + l) & (kLeadRing - 1)] = (uint32_t)leads;
+        lprod += lpos;
+        lpos = 0;
+        if (l == 0) lds_release(&R->lead_produced, lprod);
+    }
+    __device__ __forceinline__ void token(uint32_t t) {
+        leads = writelane((int)t, lpos, leads);
+        if (++lpos == 64) publish();
     }
     __device__ __forceinline__ void write_out() {
         const uint32_t lead = low >> (24 - bits_left);
         bits_left += 8;
         low &= 0xffffffffu >> bits_left;
-        if (lead == 0xff) {
-            nbuf++;
-        } else if (nbuf > 0) {
-            const uint32_t carry = lead >> 8;
-            put(buffered + carry);
-            buffered = lead & 0xff;
-            const uint32_t fill = (0xff + carry) & 0xff;
-            while (nbuf > 1) {
-                put(fill);
-                nbuf--;
-            }
-        } else {
-            nbuf = 1;
-            buffered = lead;
-        }
+        token(lead);
     }
     // One modelled entry: a context bin is one readlane (LPS ranges of its state), a
     // branch-free MPS/LPS select and a count-leading-zeros renormalisation; bypass runs
-    // and terminating bins are the other two (rarer) paths. Only the byte output (every
-    // ~8 coded bits) leaves this straight-line code.
+    // and terminating bins are the other two (rarer) paths.
     __device__ __forceinline__ void code(uint32_t e) {
         if (__builtin_expect((e & 0xC000u) == kModeled, 1)) {
             const uint32_t lps4 = (uint32_t)__builtin_amdgcn_readlane(lps_v, (int)(e & 63u));
@@ -613,29 +615,76 @@ struct WaveCabac {
         }
         if (bits_left < 12) write_out();
     }
+    // Flush (9.3.4.3.5 / HM finish): the final carry resolves the outstanding bytes, then
+    // the remaining bits of low, the stop bit and the alignment zeros as literal bytes.
     __device__ __forceinline__ void finish() {
-        if (low >> (32 - bits_left)) {
-            put(buffered + 1);
-            while (nbuf > 1) {
-                put(0x00);
-                nbuf--;
-            }
-            low -= 1u << (32 - bits_left);
-        } else {
-            if (nbuf > 0) put(buffered);
-            while (nbuf > 1) {
-                put(0xff);
-                nbuf--;
-            }
-        }
+        const uint32_t c = low >> (32 - bits_left);
+        token(kTokFlush | c);
+        if (c) low -= 1u << (32 - bits_left);
         const int nb = 24 - bits_left;
         uint64_t v = ((uint64_t)(low >> 8) & ((1ull << nb) - 1)) << 1 | 1ull;
         int total = nb + 1;
         const int pad = (8 - (total & 7)) & 7;
         v <<= pad;
         total += pad;
-        for (int i = total - 8; i >= 0; i -= 8) put((uint32_t)(v >> i) & 0xff);
-        // tail: complete words in ob plus the partial word in acc
+        for (int i = total - 8; i >= 0; i -= 8) token(kTokRaw | ((uint32_t)(v >> i) & 0xffu));
+        if (lpos) publish();
+        if (lane() == 0) lds_release(&R->lead_fin, 1);
+    }
+};
+
+// Writer wave: carry propagation over the outstanding 0xff bytes and byte packing.
+struct CabacWriter {
+    uint32_t buffered, acc;
+    int nbuf, opos, flushed;
+    int ob;                     // output chunk (lane = 4-byte word)
+    uint8_t* out;
+
+    __device__ __forceinline__ void put(uint32_t byte) {
+        acc |= (byte & 0xffu) << (8 * (opos & 3));
+        opos++;
+        if ((opos & 3) == 0) {
+            ob = writelane((int)acc, (opos >> 2) - 1, ob);
+            acc = 0;
+            if (opos == 256) {
+                reinterpret_cast<int*>(out + flushed)[lane()] = ob;
+                flushed += 256;
+                opos = 0;
+            }
+        }
+    }
+    __device__ __forceinline__ void resolve(uint32_t carry) {   // nbuf > 0
+        put(buffered + carry);
+        const uint32_t fill = (0xff + carry) & 0xff;
+        while (nbuf > 1) {
+            put(fill);
+            nbuf--;
+        }
+    }
+    __device__ __forceinline__ void token(uint32_t t) {
+        if (__builtin_expect(t < 0x200u, 1)) {   // lead: settled byte + carry (HM writeOut)
+            if (t == 0xff) {
+                nbuf++;
+            } else if (nbuf > 0) {
+                resolve(t >> 8);
+                buffered = t & 0xff;
+            } else {
+                nbuf = 1;
+                buffered = t;
+            }
+        } else if (t & kTokRaw) {
+            put(t & 0xffu);
+        } else {                                 // flush (HM finish: the carry case puts even with nbuf == 0)
+            const uint32_t c = t & 1u;
+            if (c || nbuf > 0) put(buffered + c);
+            const uint32_t fill = c ? 0x00u : 0xffu;
+            while (nbuf > 1) {
+                put(fill);
+                nbuf--;
+            }
+        }
+    }
+    __device__ __forceinline__ int tail() {
         if (opos & 3) ob = writelane((int)acc, opos >> 2, ob);
         const int l = lane();
         const int words = (opos + 3) >> 2;
@@ -645,19 +694,9 @@ struct WaveCabac {
             const int nbytes = l * 4 + 4 <= opos ? 4 : opos - 4 * l;
             for (int k = 0; k < nbytes; k++) d[k] = (uint8_t)(wv >> (8 * k));
         }
+        return flushed + opos;
     }
 };
-
-struct CabacRing {
-    uint32_t e[kRingSize];
-    int produced, consumed, fin, model_waits;
-};
-__device__ __forceinline__ int lds_acquire(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_release(int* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // Modeler wave: context transitions of row cy's entries, 64 modelled entries per ring chunk.
 __device__ __forceinline__ void cabac_model_row(const HevcArgs& A, int cy, bool subset_end, CabacRing& R) {
@@ -720,35 +759,32 @@ __device__ __forceinline__ void cabac_model_row(const HevcArgs& A, int cy, bool 
     if (l == 0) lds_release(&R.fin, 1);
 }
 
-__global__ __launch_bounds__(128) void k_hevc_cabac(HevcArgs A) {
+__global__ __launch_bounds__(192) void k_hevc_cabac(HevcArgs A) {
     __shared__ CabacRing R;
     const FrameArgs& f = A.f;
     const int cy = blockIdx.x;
     const SliceTask t = f.tasks[cy / f.rows_per_slice];
     const int l = lane();
-    const bool coder = threadIdx.x >= 64;
+    const int wave = threadIdx.x >> 6;
     if (threadIdx.x == 0) {
-        R.produced = 0;
-        R.consumed = 0;
-        R.fin = 0;
+        R.produced = R.consumed = R.fin = R.model_waits = 0;
+        R.lead_produced = R.lead_consumed = R.lead_fin = 0;
     }
     __syncthreads();
-    WaveCabac E;
-    E.out = A.sub + (size_t)cy * A.sub_stride;
-    E.flushed = 0;
-    E.opos = 0;
-    if (!coder) {
+    int size = 0;
+    if (wave == 0) {
         cabac_model_row(A, cy, cy < t.first_row + t.num_rows - 1, R);
-    } else {
+    } else if (wave == 1) {
+        WaveCabac E;
         E.lps_v = (int)((uint32_t)CABAC_LPS[l][0] | ((uint32_t)CABAC_LPS[l][1] << 8) |
                         ((uint32_t)CABAC_LPS[l][2] << 16) | ((uint32_t)CABAC_LPS[l][3] << 24));
         E.low = 0;
         E.range = 510;
-        E.buffered = 0xff;
-        E.acc = 0;
         E.bits_left = 23;
-        E.nbuf = 0;
-        E.ob = 0;
+        E.leads = 0;
+        E.lpos = 0;
+        E.lprod = 0;
+        E.R = &R;
         const unsigned long long t0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
         const unsigned long long rt0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;   // 100 MHz
         int done = 0, waits = 0;
@@ -776,11 +812,36 @@ __global__ __launch_bounds__(128) void k_hevc_cabac(HevcArgs A) {
             A.dbg[4 * cy + 2] = rt0;
             A.dbg[4 * cy + 3] = __builtin_amdgcn_s_memrealtime();
         }
+    } else {
+        CabacWriter W;
+        W.buffered = 0xff;
+        W.acc = 0;
+        W.nbuf = 0;
+        W.opos = 0;
+        W.flushed = 0;
+        W.ob = 0;
+        W.out = A.sub + (size_t)cy * A.sub_stride;
+        int done = 0;
+        for (;;) {
+            const int fin = lds_acquire(&R.lead_fin);
+            const int avail = lds_acquire(&R.lead_produced) - done;
+            if (avail > 0) {
+                const uint32_t v = R.lead[(done + l) & (kLeadRing - 1)];
+                const int m = __builtin_amdgcn_readfirstlane(avail < 64 ? avail : 64);
+                for (int i = 0; i < m; i++) W.token((uint32_t)__builtin_amdgcn_readlane((int)v, i));
+                done += m;
+                if (l == 0) lds_release(&R.lead_consumed, done);
+            } else if (fin) {
+                break;
+            } else {
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        size = W.tail();
     }
-    __syncthreads();   // the coder wave's substream bytes are visible to its own lanes
-    if (!coder) return;
-    uint8_t* out = E.out;
-    const int size = E.flushed + E.opos;
+    __syncthreads();   // the writer wave's substream bytes are visible to its own lanes
+    if (wave != 2) return;
+    const uint8_t* out = A.sub + (size_t)cy * A.sub_stride;
     if (l == 0) A.sub_size[cy] = size;
     // emulation-prevention count (wave-parallel, same rule as k_hevc_ep_copy)
     int last_nz = -1, ins_total = 0;
@@ -905,7 +966,7 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
     hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_cabac, dim3(a.f.mb_h), dim3(128), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_cabac, dim3(a.f.mb_h), dim3(192), 0, s, a);
     hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h), dim3(64), 0, s, a);
 }
