@@ -63,8 +63,12 @@ def parse():
     p.add_argument("--overlap", type=int, default=0,
                    help="1: upload frame n+1 while frame n encodes (upload/finish/launch); latency is "
                         "measured from the frame's upload to its packets")
-    p.add_argument("--gather", action="store_true", help="gather all packets to rank 0 over RCCL each step "
-                   "(--path encoder only)")
+    p.add_argument("--gather", action="store_true", help="sessions run in lockstep and every step's packets of "
+                   "all ranks are gathered to rank 0 over RCCL in one collective (--path encoder only)")
+    p.add_argument("--dist-bands", action="store_true",
+                   help="ONE session of --width x --height split into one band of stripes per rank "
+                        "(parallel/dist_banded.py): rank 0 scatters the bands over RCCL, every rank encodes its "
+                        "band on its GPU, packets are gathered to rank 0 each step; strong scaling")
     p.add_argument("--e2e-sessions", type=int, default=8,
                    help="after the timed window (single process, HIP, H.264 only): serve this many 1080p60 "
                         "sessions as real server processes to headless websocket clients for --e2e-seconds and "
@@ -144,6 +148,65 @@ def run_e2e(args, W, H):
         return {"sessions": args.e2e_sessions, "error": f"{type(ex).__name__}: {ex}"}
 
 
+def run_dist_bands(args, torch, dist, rank, world, local_rank):
+    """One WxH session across all ranks; returns the result dict on rank 0."""
+    from selkies_gstreamer_amd.parallel.dist_banded import DistBandedEncoder
+    from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
+    W, H = args.width, args.height
+    dev = torch.device("cuda", local_rank) if args.backend == "hip" else torch.device("cpu")
+    pool = None
+    if rank == 0:   # the captured frames live on rank 0's GPU (the capture rank)
+        src = SyntheticDesktop(W, H, kind=args.content, seed=0)
+        pool = torch.empty((args.pool, H, W, 4), dtype=torch.uint8, device=dev)
+        for i in range(args.pool):
+            pool[i].copy_(torch.from_numpy(src.frame(i)))
+    enc = DistBandedEncoder(W, H, stripe_height=args.stripe_height, backend=args.backend, qp=args.qp,
+                            use_paint_over=False, deblock=bool(args.deblock), me_full=bool(args.me_full))
+
+    def sync():
+        if args.backend == "hip":
+            torch.cuda.synchronize()
+
+    nbytes, lat = 0, []
+    for t in range(args.warmup):
+        enc.encode(pool[t % args.pool] if rank == 0 else None, t)
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        a = time.perf_counter()
+        pk = enc.encode(pool[t % args.pool] if rank == 0 else None, t)
+        if pk is not None:
+            lat.append(time.perf_counter() - a)
+            nbytes += sum(len(p.data) for p in pk)
+    sync()
+    dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed[0])
+    enc.close()
+    if rank != 0:
+        return None
+    fps = args.steps / elapsed
+    lat_ms = np.asarray(lat) * 1e3
+    return {
+        "metric": "encoded fps of one session split across GPUs (bands over RCCL)",
+        "value": round(fps, 2),
+        "unit": f"frames/s ({W}x{H} H.264, one session, {world} GPUs)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "uint8 pixels / int32 integer transforms (bit-exact vs CPU reference)",
+        "data": f"synthetic X11-like framebuffer ({args.content}) resident on rank 0's GPU",
+        "p50_frame_latency_ms": round(float(np.percentile(lat_ms, 50)), 3),
+        "p99_frame_latency_ms": round(float(np.percentile(lat_ms, 99)), 3),
+        "kib_per_frame": round(nbytes / args.steps / 1024, 1),
+        "config": {"model": f"H.264 Constrained Baseline CAVLC, stripes {args.stripe_height}px, QP {args.qp}",
+                   "global_batch": 1, "seq_len": 1, "parallelism": f"bands{world} (scatter + gather per step)",
+                   "resolution": f"{W}x{H}", "backend": args.backend, "bands": enc.bands},
+    }
+
+
 def main():
     args = parse()
     if args.gather and args.path != "encoder":
@@ -153,7 +216,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     torch = None
-    if world > 1 or args.gather:
+    if world > 1:
         import torch as _torch
         import torch.distributed as _dist
         torch, dist = _torch, _dist
@@ -166,6 +229,28 @@ def main():
     def sync():
         if torch is not None and args.backend == "hip":
             torch.cuda.synchronize()
+
+    if args.dist_bands:
+        if dist is None:
+            import torch as _torch
+            import torch.distributed as _dist
+            torch, dist = _torch, _dist
+            import socket
+            so = socket.socket()
+            so.bind(("127.0.0.1", 0))
+            url = f"tcp://127.0.0.1:{so.getsockname()[1]}"
+            so.close()
+            if args.backend == "hip":   # one rank: the same device-resident RCCL path as N ranks
+                torch.cuda.set_device(local_rank)
+                dist.init_process_group("nccl", init_method=url, rank=0, world_size=1,
+                                        device_id=torch.device("cuda", local_rank))
+            else:
+                dist.init_process_group("gloo", init_method=url, rank=0, world_size=1)
+        res = run_dist_bands(args, torch, dist, rank, world, local_rank)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+        dist.destroy_process_group()
+        return
 
     from selkies_gstreamer_amd.ops.native import H264Encoder, JpegEncoder, PinnedBuffer
     from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
@@ -210,7 +295,6 @@ def main():
 
     lat = [[] for _ in range(S)]
     nbytes = [0] * S
-    out_packets = [[] for _ in range(S)]
 
     def run(i, first, count, record):
         e = encs[i]
@@ -230,8 +314,6 @@ def main():
                 if record:
                     lat[i].append(time.perf_counter() - t_up.pop(t))
                     nbytes[i] += sum(len(p.data) for p in pk)
-                    if args.gather:
-                        out_packets[i].append(pk)
             return
         if args.overlap and hasattr(e, "upload"):
             t_up = time.perf_counter()
@@ -246,8 +328,6 @@ def main():
                 if record:
                     lat[i].append(time.perf_counter() - t_up)
                     nbytes[i] += sum(len(p.data) for p in pk)
-                    if args.gather:
-                        out_packets[i].append(pk)
                 if nxt:
                     e.launch()
                     t_up = t_next
@@ -258,10 +338,36 @@ def main():
             if record:
                 lat[i].append(time.perf_counter() - a)
                 nbytes[i] += sum(len(p.data) for p in pk)
-                if args.gather:
-                    out_packets[i].append(pk)
+
+    gathered = [0]
+
+    def run_lockstep(first, count, record):
+        # single-server topology (--gather): every step, all sessions of this rank are
+        # submitted, finished, and their packets gathered to rank 0 in one collective
+        from selkies_gstreamer_amd.parallel.fanout import gather_packets
+        fr = pool.array
+        for t in range(first, first + count):
+            a = time.perf_counter()
+            for i, e in enumerate(encs):
+                e.submit(fr[(t + 3 * i) % args.pool], t)
+            step = []
+            for i, e in enumerate(encs):
+                pk = e.finish()
+                step.extend((i, p.data) for p in pk)
+                if record:
+                    nbytes[i] += sum(len(p.data) for p in pk)
+            got = gather_packets(step) if dist is not None else [(0, i, d) for i, d in step]
+            if record:
+                dt = time.perf_counter() - a
+                for i in range(S):
+                    lat[i].append(dt)
+                if got is not None:
+                    gathered[0] += sum(len(d) for _, _, d in got)
 
     def run_all(first, count, record):
+        if args.gather:
+            run_lockstep(first, count, record)
+            return
         th = [threading.Thread(target=run, args=(i, first, count, record)) for i in range(S)]
         for x in th:
             x.start()
@@ -284,13 +390,7 @@ def main():
         run_caps(args.steps)
     else:
         run_all(args.warmup, args.steps, True)
-    gather_bytes = 0
-    if args.gather and dist is not None:
-        # single-server topology: every rank's packets are gathered to rank 0 over xGMI in one step
-        from selkies_gstreamer_amd.parallel.fanout import gather_packets
-        mine = [(i, p.data) for i, s in enumerate(out_packets) for step in s for p in step]
-        got = gather_packets(mine)
-        gather_bytes = sum(len(d) for _, _, d in got) if got is not None else 0
+    gather_bytes = gathered[0]
     if dist is not None:
         sync()
         dist.barrier()

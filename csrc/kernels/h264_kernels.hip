@@ -153,14 +153,17 @@ __device__ __forceinline__ void inv4_quad(const int* d, int r, int* res) {
     }
 }
 
-// Diagnostic stamp: wave 0 of block 0 records s_memtime at numbered points.
+// Diagnostic stamp: wave 0 of block SK_STAMP_BLOCK records s_memtime at numbered points.
+#ifndef SK_STAMP_BLOCK
+#define SK_STAMP_BLOCK 0
+#endif
 #ifdef SK_STAMPS
 __device__ __forceinline__ void stamp(unsigned long long* dbg, int step, int point) {
     __builtin_amdgcn_sched_barrier(0);
     unsigned long long t = __builtin_amdgcn_s_memtime();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
-    if (dbg && blockIdx.x == 0 && threadIdx.x == 0 && step < 64) dbg[step * 16 + point] = t;
+    if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && step < 64) dbg[step * 16 + point] = t;
 }
 #define STAMP(step, pt) stamp(a.dbg, step, pt)
 #define STAMP_S(dbg, step, pt) stamp(dbg, step, pt)
@@ -961,7 +964,7 @@ __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16
     if (cbp_c) total_crude += (cdc_sum_n0 > 0 ? 11 : 2) + (cdc_sum_n1 > 0 ? 11 : 2) + cdc_sum_c;
     wave_sync();
     STAMP_S(dbg, step, 12);
-    if (dbg && blockIdx.x == 0 && threadIdx.x == 0 && step < 64) dbg[step * 16 + 14] = total_crude;
+    if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && step < 64) dbg[step * 16 + 14] = total_crude;
     if (total_crude <= kMbBitBudget) {
         *bound_out = total_crude;
         return cbp_l | (cbp_c << 4);
@@ -1070,7 +1073,7 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
     for (;;) {
         int bound;
         cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound, T, dbg, step);
-        if (dbg && blockIdx.x == 0 && threadIdx.x == 0 && step < 64) dbg[step * 16 + 15] = (dbg[step * 16 + 15] & 0xffff) + 1 + ((unsigned long long)bound << 32);
+        if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && step < 64) dbg[step * 16 + 15] = (dbg[step * 16 + 15] & 0xffff) + 1 + ((unsigned long long)bound << 32);
         if (qp + 6 > cap || bound <= kMbBitBudget) break;
         qp += 6;
         wave_sync();
@@ -1601,6 +1604,11 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
     int s = blockIdx.x;
     const SliceTask t = a.tasks[s];
     if (t.final_action != ACT_I) return;   // block-uniform: P/skipped slices leave before the table load
+#ifdef SK_STAMPS
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    if (a.dbg && blockIdx.x == 0 && (threadIdx.x & 63) == 0)   // HW_ID of each wave (SIMD placement)
+        a.dbg[1024 + 128 + (threadIdx.x >> 6)] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
     if (threadIdx.x < 16) zero16[threadIdx.x] = 0;
     load_cavlc_tables(T, a.cavlc_tabs);
     int w = threadIdx.x >> 6;
@@ -1727,6 +1735,12 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
         __syncthreads();
         if (w == 0) STAMP(step, 8);
     }
+#ifdef SK_STAMPS
+    if (a.dbg && threadIdx.x == 0 && blockIdx.x < 128) {   // per-slice span (100 MHz realtime)
+        a.dbg[1024 + 2 * blockIdx.x] = t_start;
+        a.dbg[1024 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -118,7 +118,9 @@ class HipBackend : public EncoderBackend {
         else if (inflight() && upload_mode_ != 0) cs = upload_mode_ == 2 ? device_copy_stream(device_) : upload_stream();
         // the last reader of bgrx_dev_[q] is the graph two frames back: finished
         HIPCHECK(hipEventRecord(ev_[3 * q], cs));
-        HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyHostToDevice, cs));
+        // hipMemcpyDefault: the frame may be host memory (capture) or device memory (a band
+        // scattered to this GPU over RCCL, parallel/dist_banded.py)
+        HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyDefault, cs));
         if (cs != stream_) HIPCHECK(hipEventRecord(ev_copy_[q], cs));
         staged_on_main_ = cs == stream_;
         staged_ = true;
@@ -332,7 +334,7 @@ class HipBackend : public EncoderBackend {
         else if (s == "me") { p = args_.me; n = (int64_t)g_.num_mbs() * sizeof(MeResult); }
         else if (s == "mb_dirty") { p = args_.mb_dirty; n = g_.num_mbs(); }
         else if (s == "aq") { p = args_.aq; n = g_.num_mbs(); }
-        else if (s == "stamps") { if (!args_.dbg) return -1; p = args_.dbg; n = 64 * 16 * 8; }
+        else if (s == "stamps") { if (!args_.dbg) return -1; p = args_.dbg; n = (64 * 16 + 256) * 8; }
         else if (s == "tasks") {
             n = (int64_t)g_.num_slices * sizeof(SliceTask);
             if (dst && cap >= n) memcpy(dst, h_tasks_[(finished_ + 1) & 1], (size_t)n);   // last finished
@@ -483,7 +485,7 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipStreamSynchronize(stream_));
         a.cavlc_tabs = ct;
         d_frame_params_ = dmalloc<int>(4);
-        if (getenv("SK_STAMPS")) a.dbg = dmalloc<unsigned long long>(64 * 16);
+        if (getenv("SK_STAMPS")) a.dbg = dmalloc<unsigned long long>(64 * 16 + 256);
         a.frame_params_dev = d_frame_params_;
         for (int p = 0; p < 2; p++) {
             h_tasks_[p] = hmalloc<SliceTask>(ns, hipHostMallocCoherent);  // final decisions from k_decide

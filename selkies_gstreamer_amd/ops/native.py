@@ -334,6 +334,16 @@ class H264Encoder:
             self._staged = None
             raise RuntimeError(f"upload failed: {L.sk_last_error().decode()}")
 
+    def upload_ptr(self, ptr: int, stride: int, frame_id: int = 0, keepalive=None) -> None:
+        """:meth:`upload` from a raw address: host memory or, on the HIP backend, device
+        memory of this encoder's GPU (e.g. a torch tensor's ``data_ptr()``; the copy is
+        then device-to-device). ``keepalive`` is held until the frame is finished."""
+        self._staged = keepalive
+        L = lib()
+        if L.sk_h264_upload(self._h, ctypes.c_void_p(int(ptr)), int(stride), frame_id & 0xFFFF) < 0:
+            self._staged = None
+            raise RuntimeError(f"upload failed: {L.sk_last_error().decode()}")
+
     def launch(self) -> None:
         L = lib()
         if L.sk_h264_launch(self._h) < 0:

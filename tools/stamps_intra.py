@@ -16,7 +16,14 @@ enc = H264Encoder(W, H, stripe_height=64, backend="hip")
 for t in range(3):
     enc.request_keyframe()
     enc.encode(src.frame(t), t)
-st = enc.debug_buffer("stamps", np.uint64).reshape(64, 16).astype(np.int64)
+raw = enc.debug_buffer("stamps", np.uint64).astype(np.int64)
+st = raw[:1024].reshape(64, 16)
+span = raw[1024:1024 + 34].reshape(17, 2)
+dur = (span[:, 1] - span[:, 0]) / 100.0
+print("per-slice k_code_intra span us:", dur.round(1).tolist())
+hw = raw[1024 + 128:1024 + 133]
+print("block 0 waves: simd", ((hw >> 4) & 3).tolist(), "wave slot", (hw & 15).tolist(), "cu", ((hw >> 8) & 15).tolist())
+print("slice start offsets us:", ((span[:, 0] - span[:, 0].min()) / 100.0).round(1).tolist())
 # points: 0 start, 2 pred done, 3 fwd transform done, 9 quant lanes in, 10 dc, 11 analysis,
 # 12 crude bound, 4 quant loop done, 5 recon done, 6 code_mb done, 7 edges done, 8 after barrier
 seg = [("pred", 0, 2), ("fwd", 2, 3), ("q_in", 3, 9), ("q_dc", 9, 10), ("q_analysis", 10, 11),
