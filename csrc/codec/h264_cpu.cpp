@@ -269,6 +269,12 @@ void CpuH264Encoder::subpel_refine(int s) {
     const SliceTask& t = tasks[s];
     const int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
     static const int8_t ring[8][2] = {{-1, -1}, {0, -1}, {1, -1}, {-1, 0}, {1, 0}, {-1, 1}, {0, 1}, {1, 1}};
+    StripeState& sst = ctl_.stripes()[s];
+    if (!subpel_gate(t.frame_num, sst.subpel_prev, t.num_rows * g.mb_w)) {
+        for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+            for (int mbx = 0; mbx < g.mb_w; mbx++) me[(size_t)mby * g.mb_w + mbx].fx = me[(size_t)mby * g.mb_w + mbx].fy = 0;
+        return;
+    }
     for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
         for (int mbx = 0; mbx < g.mb_w; mbx++) {
             MeResult& r = me[(size_t)mby * g.mb_w + mbx];
@@ -300,6 +306,7 @@ void CpuH264Encoder::subpel_refine(int s) {
             }
             r.fx = (int8_t)(bx - 4 * r.mvx);
             r.fy = (int8_t)(by - 4 * r.mvy);
+            sst.subpel_hits += (r.fx | r.fy) != 0;
         }
 }
 
@@ -686,6 +693,10 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
                             std::vector<EncodedPacket>& out) {
     load_frame(bgrx, stride);
     ctl_.plan(stripe_dirty.data(), tasks.data());
+    for (auto& st : ctl_.stripes()) {   // k_plan rotates the same pair on the GPU
+        st.subpel_prev = st.subpel_hits;
+        st.subpel_hits = 0;
+    }
     for (int s = 0; s < g.num_slices; s++)
         if (tasks[s].action == ACT_P) {
             motion_search(s);

@@ -111,6 +111,8 @@ struct StripeState {
     int paint_left = 0;
     bool painted = true;   // nothing to paint before the first change
     int refs = 0;          // pictures in the decoder's DPB for this stream (sliding window)
+    int subpel_hits = 0;   // MBs of this stripe's last frame given a fractional vector (K4c)
+    int subpel_prev = 0;   // the same count one frame earlier: the adaptive refinement gate
 };
 
 // Controller knobs as a POD, so the same plan code runs on the host (CPU
@@ -224,6 +226,7 @@ class Controller {
     void commit(const SliceTask* tasks);
     bool picture_is_idr(const SliceTask* tasks) const;
     const std::vector<StripeState>& stripes() const { return st_; }
+    std::vector<StripeState>& stripes() { return st_; }
     // Session-state transfer (EncoderState): committed stripe states + picture state.
     void export_states(StripeState* out) const {
         for (size_t s = 0; s < st_.size(); s++) out[s] = st_[s];

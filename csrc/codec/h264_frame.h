@@ -29,6 +29,16 @@ struct MeResult {
 // Integer matches this close (SAD per 16x16, i.e. <= 1 per pixel on average) keep their
 // integer vector: a fractional one could not win back the extra MVD bits.
 constexpr int kSubpelMinSad = 256;
+// Adaptive refinement, per stripe (stripes stay independent streams): a stripe refines
+// its P vectors when its previous frame's refinement moved >= 1/kSubpelGateDen of its MBs
+// to a fractional vector, and on every kSubpelProbe-th P frame of the stripe
+// (frame_num % 8 == 1, so the first P after an IDR probes). Integer-motion content
+// (scrolling, dragging) then skips the pass. Counts live in StripeState.
+constexpr int kSubpelProbe = 8;
+constexpr int kSubpelGateDen = 128;
+SK_HD bool subpel_gate(int frame_num, int prev_hits, int num_mbs) {
+    return (frame_num & (kSubpelProbe - 1)) == 1 || prev_hits * kSubpelGateDen >= num_mbs;
+}
 // Quarter-pel motion vector of an ME result (H.264 MV units).
 SK_HD int me_qx(const MeResult& r) { return 4 * r.mvx + r.fx; }
 SK_HD int me_qy(const MeResult& r) { return 4 * r.mvy + r.fy; }

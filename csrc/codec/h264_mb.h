@@ -233,7 +233,78 @@ SK_HD int aq_start_qp(int slice_qp, int offset) {
     return q < 0 ? 0 : (q > 51 ? 51 : q);
 }
 
+// Upper bound of the CAVLC bits of one non-zero level of magnitude a, over every
+// suffixLength the block can reach (<= sl_max, 9.2.2.1). With per-TotalCoeff maxima for
+// coeff_token / total_zeros and a 3n+8 bound on run_before this dominates the exact
+// nC-free bound, so bound <= budget implies exact <= budget. (lc >> sl) + 1 + sl is
+// convex in sl and the escape (28) region is a prefix of sl, so the maximum over
+// sl in [1, sl_max] sits at an end point: two evaluations instead of six.
+SK_HD int level_bits_bound(int a, int sl_max) {
+    int lc = 2 * a - 1;
+    int best = lc < 14 ? lc + 1 : (lc < 30 ? 19 : 28);
+    const int b1 = lc < 30 ? (lc >> 1) + 2 : 28;
+    const int bs = lc < (15 << sl_max) ? (lc >> sl_max) + 1 + sl_max : 28;
+    return sk_max(best, sk_max(b1, bs));
+}
+SK_HD int suffix_len_cap(int maxabs) {
+    return sk_min(6, 1 + (maxabs > 3) + (maxabs > 6) + (maxabs > 12) + (maxabs > 24) + (maxabs > 48));
+}
+// Conservative bits of one residual block (levels in scan order, maxn 16 or 15 = AC).
+SK_HD int block_bits_crude(const int16_t* c, int maxn, const CavlcTables& T) {
+    int n = 0, last = -1, mx = 0;
+    for (int k = 0; k < 16; k++)
+        if (c[k]) {
+            n++;
+            last = k;
+            mx = sk_max(mx, sk_abs((int)c[k]));
+        }
+    if (n == 0) return 6;
+    const int sl = suffix_len_cap(mx);
+    int lv = 0;
+    for (int k = 0; k < 16; k++)
+        if (c[k]) lv += level_bits_bound(sk_abs((int)c[k]), sl);
+    const int tz = (maxn == 16 ? last + 1 : last) - n;   // AC blocks (15) start at scan index 1
+    int b = T.ct_max_tc[n] + lv;
+    if (n < maxn) b += T.tz_len[n - 1][tz];
+    if (n > 1 && tz > 0) b += tz <= 2 ? 2 * (n - 1) : (tz <= 6 ? 3 * (n - 1) : 3 * (n - 1) + 8);
+    return b;
+}
+// Conservative macroblock size of an Intra16x16 MB (the same terms the lane-parallel
+// GPU bound sums in quant_mb_lanes): 96 bits of header allowance, the AC blocks when
+// coded, the luma DC block and the chroma blocks.
+SK_HD int mb_bits_crude_i16(const MbInfo& mb, const int16_t* coef, const CavlcTables& T) {
+    const int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
+    int total = 96;
+    if (cbp_l)
+        for (int b = 0; b < 16; b++) total += block_bits_crude(coef + kCoefLuma + b * 16, 15, T);
+    if (cbp_c == 2)
+        for (int b = 0; b < 8; b++) total += block_bits_crude(coef + kCoefChromaAC + b * 16, 15, T);
+    int dn = 0, dc = 0;
+    for (int k = 0; k < 16; k++) {
+        const int a = sk_abs((int)coef[kCoefLumaDC + k]);
+        if (a) { dn++; dc += level_bits_bound(a, 6) + 3; }
+    }
+    total += dn > 0 ? T.ct_max_tc[dn] + (dn < 16 ? T.tz_max_tc[dn] : 0) + 8 + dc : 6;
+    if (cbp_c) {
+        int n0 = 0, n1 = 0, cc = 0;
+        for (int k = 0; k < 8; k++) {
+            const int a = sk_abs((int)coef[kCoefChromaDC + k]);
+            if (a) { (k < 4 ? n0 : n1)++; cc += level_bits_bound(a, 6) + 3; }
+        }
+        total += (n0 > 0 ? 11 : 2) + (n1 > 0 ? 11 : 2) + cc;
+    }
+    return total;
+}
+
+// Escalation threshold: the exact nC-free count of inter MBs is held to kMbBitBudget;
+// the conservative bound of Intra16x16 MBs (header allowance 96 bits >= the <= 25 bits
+// of an I16 header) may use the whole A.3.1 limit, since bound <= limit already implies
+// compliance.
+SK_HD int mb_bit_budget(bool intra16) { return intra16 ? kMaxMbBits : kMbBitBudget; }
+
 // Quantise with QP escalation so a macroblock never exceeds the A.3.1 bit limit.
+// Intra16x16 MBs (I slices: the keyframe wavefront) escalate on the conservative bound
+// alone; inter MBs fall back to the exact nC-free CAVLC count when it is exceeded.
 // Returns the final QP; fills mb.cbp / nnz and coef.
 // `start_qp` is the first QP tried: the AQ start QP, or (intra) the QP the open-loop
 // pre-pass already found to be needed.
@@ -247,7 +318,7 @@ SK_HD int quant_mb_with_budget(const MbTransform& t, int slice_qp, bool intra16,
         mb.cbp = (uint8_t)(cbp_l | (cbp_c << 4));
         mb.qp = (uint8_t)qp;
         if (qp + 6 > qp_cap) break;
-        if (mb_bits_bound(mb, coef, T) <= kMbBitBudget) break;
+        if ((intra16 ? mb_bits_crude_i16(mb, coef, T) : mb_bits_bound(mb, coef, T)) <= mb_bit_budget(intra16)) break;
         qp += 6;
     }
     return qp;

@@ -157,13 +157,17 @@ __device__ __forceinline__ void inv4_quad(const int* d, int r, int* res) {
 #ifndef SK_STAMP_BLOCK
 #define SK_STAMP_BLOCK 0
 #endif
+#ifndef SK_STAMP_STEP0
+#define SK_STAMP_STEP0 0   // first recorded step (64 steps are kept)
+#endif
 #ifdef SK_STAMPS
 __device__ __forceinline__ void stamp(unsigned long long* dbg, int step, int point) {
     __builtin_amdgcn_sched_barrier(0);
     unsigned long long t = __builtin_amdgcn_s_memtime();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
-    if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && step < 64) dbg[step * 16 + point] = t;
+    if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && (unsigned)(step - SK_STAMP_STEP0) < 64u)
+        dbg[(step - SK_STAMP_STEP0) * 16 + point] = t;
 }
 #define STAMP(step, pt) stamp(a.dbg, step, pt)
 #define STAMP_S(dbg, step, pt) stamp(dbg, step, pt)
@@ -673,6 +677,8 @@ __global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
     if (qo > 0) pc.qp = qo;
     if (po > 0) pc.paint_qp = po;
     for (int s = tid; s < ns; s += 256) {
+        st[s].subpel_prev = st[s].subpel_hits;   // adaptive refinement gate (h264_frame.h subpel_gate)
+        st[s].subpel_hits = 0;
         const int r0 = s * a.rows_per_slice, nr = min(a.rows_per_slice, a.mb_h - r0);
         plan_stripe(pc, st[s], pic, a.stripe_dirty[s] != 0, r0, nr, a.mb_h, a.tasks[s]);
         a.stripe_dirty[s] = 0;
@@ -755,23 +761,6 @@ __device__ __forceinline__ void lds_hadamard4x4(int* x) {
     wave_sync();
 }
 
-// Upper bound of the CAVLC bits of one non-zero level of magnitude a, over every
-// suffixLength the block can reach (<= sl_max, 9.2.2.1). With per-TotalCoeff
-// maxima for coeff_token / total_zeros and a 3n+8 bound on run_before this
-// dominates the exact nC-free bound, so bound <= budget implies exact <= budget.
-// (lc >> sl) + 1 + sl is convex in sl and the escape (28) region is a prefix of sl, so
-// the maximum over sl in [1, sl_max] sits at an end point: two evaluations instead of
-// six (checked equal to the loop for every level and sl_max).
-__device__ __forceinline__ int level_bits_bound(int a, int sl_max) {
-    int lc = 2 * a - 1;
-    int best = lc < 14 ? lc + 1 : (lc < 30 ? 19 : 28);
-    const int b1 = lc < 30 ? (lc >> 1) + 2 : 28;
-    const int bs = lc < (15 << sl_max) ? (lc >> sl_max) + 1 + sl_max : 28;
-    return sk_max(best, sk_max(b1, bs));
-}
-__device__ __forceinline__ int suffix_len_cap(int maxabs) {
-    return sk_min(6, 1 + (maxabs > 3) + (maxabs > 6) + (maxabs > 12) + (maxabs > 24) + (maxabs > 48));
-}
 __device__ __forceinline__ int quad_max(int v) {
     v = sk_max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
     v = sk_max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
@@ -964,8 +953,9 @@ __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16
     if (cbp_c) total_crude += (cdc_sum_n0 > 0 ? 11 : 2) + (cdc_sum_n1 > 0 ? 11 : 2) + cdc_sum_c;
     wave_sync();
     STAMP_S(dbg, step, 12);
-    if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && step < 64) dbg[step * 16 + 14] = total_crude;
-    if (total_crude <= kMbBitBudget) {
+    if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && (unsigned)(step - SK_STAMP_STEP0) < 64u)
+        dbg[(step - SK_STAMP_STEP0) * 16 + 14] = total_crude;
+    if (total_crude <= kMbBitBudget || intra16) {   // Intra16x16: the conservative bound decides
         *bound_out = total_crude;
         return cbp_l | (cbp_c << 4);
     }
@@ -1073,8 +1063,11 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
     for (;;) {
         int bound;
         cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound, T, dbg, step);
-        if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && step < 64) dbg[step * 16 + 15] = (dbg[step * 16 + 15] & 0xffff) + 1 + ((unsigned long long)bound << 32);
-        if (qp + 6 > cap || bound <= kMbBitBudget) break;
+        if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && (unsigned)(step - SK_STAMP_STEP0) < 64u) {
+            unsigned long long& d = dbg[(step - SK_STAMP_STEP0) * 16 + 15];
+            d = (d & 0xffff) + 1 + ((unsigned long long)bound << 32);
+        }
+        if (qp + 6 > cap || bound <= mb_bit_budget(intra16)) break;
         qp += 6;
         wave_sync();
     }
@@ -1199,7 +1192,8 @@ __global__ __launch_bounds__(256) void k_subpel(FrameArgs a) {
     if (t.final_action != ACT_P) return;
     const MeResult r = a.me[idx];
     const int l = lane_id();
-    if (r.sad <= kSubpelMinSad) {
+    const int sl = mby / a.rows_per_slice;
+    if (r.sad <= kSubpelMinSad || !subpel_gate(t.frame_num, a.plan_state[sl].subpel_prev, t.num_rows * a.mb_w)) {
         if (l == 0) { a.me[idx].fx = 0; a.me[idx].fy = 0; }
         return;
     }
@@ -1233,6 +1227,7 @@ __global__ __launch_bounds__(256) void k_subpel(FrameArgs a) {
     if (l == 0) {
         a.me[idx].fx = (int8_t)bx;
         a.me[idx].fy = (int8_t)by;
+        if (bx | by) atomicAdd(&a.plan_state[mby / a.rows_per_slice].subpel_hits, 1);
     }
 }
 
@@ -1606,6 +1601,7 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
     if (t.final_action != ACT_I) return;   // block-uniform: P/skipped slices leave before the table load
 #ifdef SK_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c_start = __builtin_amdgcn_s_memtime();
     if (a.dbg && blockIdx.x == 0 && (threadIdx.x & 63) == 0)   // HW_ID of each wave (SIMD placement)
         a.dbg[1024 + 128 + (threadIdx.x >> 6)] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
@@ -1645,6 +1641,9 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
         produce(1);
     }
     __syncthreads();
+#ifdef SK_STAMPS
+    const unsigned long long c_loop = __builtin_amdgcn_s_memtime();
+#endif
     if (!producer) __builtin_amdgcn_s_setprio(3);   // the chain's waves issue first on a shared SIMD
     MbScratch& S = Sw[producer ? 0 : w];
     const int b = l >> 2, r = l & 3;
@@ -1736,9 +1735,17 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
         if (w == 0) STAMP(step, 8);
     }
 #ifdef SK_STAMPS
-    if (a.dbg && threadIdx.x == 0 && blockIdx.x < 128) {   // per-slice span (100 MHz realtime)
+    if (a.dbg && threadIdx.x == 0 && blockIdx.x < 32) {   // per-slice span (100 MHz realtime)
         a.dbg[1024 + 2 * blockIdx.x] = t_start;
         a.dbg[1024 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        if (blockIdx.x < 32) a.dbg[1024 + 64 + 2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - c_start;
+        if (blockIdx.x == SK_STAMP_BLOCK) {
+            a.dbg[1024 + 200] = c_start;
+            a.dbg[1024 + 201] = __builtin_amdgcn_s_memtime();
+            a.dbg[1024 + 202] = c_loop;
+            a.dbg[1024 + 203] = steps;
+        }
+        if (blockIdx.x < 32) a.dbg[1024 + 64 + 2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     }
 #endif
 }

@@ -27,7 +27,8 @@ CXXFLAGS = [
     "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
     "-Wno-unused-variable", "-Wno-unused-but-set-variable", "-Wno-unused-lambda-capture",
     f"-I{CSRC}", f"-I{CSRC / 'codec'}", f"-I{CSRC / 'runtime'}",
-] + (["-DSK_STAMPS", f"-DSK_STAMP_BLOCK={int(os.environ.get('SK_STAMP_BLOCK', '0'))}"]
+] + (["-DSK_STAMPS", f"-DSK_STAMP_BLOCK={int(os.environ.get('SK_STAMP_BLOCK', '0'))}",
+       f"-DSK_STAMP_STEP0={int(os.environ.get('SK_STAMP_STEP0', '0'))}"]
       if os.environ.get("SK_STAMPS_BUILD") else [])
 
 

@@ -65,3 +65,51 @@ def test_subpel_gpu_matches_cpu(num_refs):
         mg, mc = g.debug_buffer("me", ME_DTYPE), c.debug_buffer("me", ME_DTYPE)
         assert np.array_equal(mg["fx"], mc["fx"]) and np.array_equal(mg["fy"], mc["fy"]), f"frame {t}"
         assert [p.data for p in pg] == [p.data for p in pc], f"frame {t}"
+
+
+def _frac_count(enc):
+    me = enc.debug_buffer("me", ME_DTYPE)
+    return int(np.count_nonzero((me["fx"] != 0) | (me["fy"] != 0)))
+
+
+def _texture(W, H, dx, dy):
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    x, y = xx - dx, yy - dy
+    v = 128 + 60 * np.sin(x / 5.3) * np.cos(y / 7.1) + 40 * np.sin((x + y) / 11.0)
+    f = np.zeros((H, W, 4), np.uint8)
+    f[..., 0] = np.clip(v, 0, 255)
+    f[..., 1] = np.clip(255 - v, 0, 255)
+    f[..., 2] = np.clip(v * 0.5 + 60, 0, 255)
+    return f
+
+
+def test_subpel_gate_skips_integer_motion_and_probes():
+    """Adaptive refinement (h264_frame.h subpel_gate): after a probe frame that found no
+    fractional vector, the refinement is off until the next probe (every 8th P frame of
+    a stripe, frame_num % 8 == 1); once a probe finds fractional motion it stays on."""
+    W, H = 192, 128
+    # frame 1 (first P = probe): a whole-pixel shift; then sub-pixel motion from frame 2 on
+    shifts = [(0.0, 0.0), (2.0, 0.0)] + [(2.0 + 0.74 * k, 0.37 * k) for k in range(1, 13)]
+    enc = H264Encoder(W, H, stripe_height=32, qp=12, use_paint_over=False)
+    counts = []
+    for t, (dx, dy) in enumerate(shifts):
+        enc.encode(_texture(W, H, dx, dy), t)
+        counts.append(_frac_count(enc))
+    assert counts[1] * 128 < W * H // 256, counts   # probe: integer motion -> gate closes
+    assert all(c == 0 for c in counts[2:9]), counts  # gate closed: sub-pixel motion ignored
+    assert counts[9] > 0, counts                     # frame_num 9: probe finds the sub-pixel motion
+    assert all(c > 0 for c in counts[10:]), counts   # and the gate stays open
+
+
+def test_subpel_gate_survives_state_migration():
+    W, H = 192, 128
+    frames = subpixel_scene(W, H, 6)
+    a = H264Encoder(W, H, stripe_height=32, qp=24, use_paint_over=False)
+    b = H264Encoder(W, H, stripe_height=32, qp=24, use_paint_over=False)
+    for t in range(3):
+        a.encode(frames[t], t)
+    b.import_state(a.export_state())
+    for t in range(3, 6):
+        pa = [p.data for p in a.encode(frames[t], t)]
+        pb = [p.data for p in b.encode(frames[t], t)]
+        assert pa == pb
