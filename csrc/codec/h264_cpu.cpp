@@ -292,6 +292,7 @@ void CpuH264Encoder::subpel_refine(int s) {
                 return sad;
             };
             int bx = 4 * r.mvx, by = 4 * r.mvy, best = sad_q(bx, by);
+            const int int_sad = best;
             for (int step = 2; step >= 1; step--) {
                 const int cx = bx, cy = by;
                 for (int k = 0; k < 8; k++) {
@@ -306,7 +307,7 @@ void CpuH264Encoder::subpel_refine(int s) {
             }
             r.fx = (int8_t)(bx - 4 * r.mvx);
             r.fy = (int8_t)(by - 4 * r.mvy);
-            sst.subpel_hits += (r.fx | r.fy) != 0;
+            sst.subpel_hits += (r.fx | r.fy) != 0 && subpel_hit(best, int_sad);
         }
 }
 

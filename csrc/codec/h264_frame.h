@@ -34,11 +34,14 @@ constexpr int kSubpelMinSad = 256;
 // to a fractional vector, and on every kSubpelProbe-th P frame of the stripe
 // (frame_num % 8 == 1, so the first P after an IDR probes). Integer-motion content
 // (scrolling, dragging) then skips the pass. Counts live in StripeState.
+// A "hit" is a fractional vector that beats the integer one by >= 1/8 of its SAD (true
+// sub-pixel motion, not fitting the reference's coding noise).
 constexpr int kSubpelProbe = 8;
-constexpr int kSubpelGateDen = 128;
+constexpr int kSubpelGateDen = 32;
 SK_HD bool subpel_gate(int frame_num, int prev_hits, int num_mbs) {
     return (frame_num & (kSubpelProbe - 1)) == 1 || prev_hits * kSubpelGateDen >= num_mbs;
 }
+SK_HD bool subpel_hit(int best_sad, int int_sad) { return best_sad * 8 <= int_sad * 7; }
 // Quarter-pel motion vector of an ME result (H.264 MV units).
 SK_HD int me_qx(const MeResult& r) { return 4 * r.mvx + r.fx; }
 SK_HD int me_qy(const MeResult& r) { return 4 * r.mvy + r.fy; }

@@ -1126,6 +1126,8 @@ struct QpelLds {
 __device__ __forceinline__ int qtap6(int a, int b, int c, int d, int e, int f) {
     return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
 }
+// Compact variant (one output per lane step, few live registers) for k_code_inter,
+// whose occupancy would suffer from qpel_fill_fast's register windows.
 __device__ void qpel_fill(QpelLds& Q, const uint8_t* ref, int stride, int w, int ylo, int yhi, int ox, int oy) {
     const int l = lane_id();
     for (int i = l; i < 576; i += 64) {
@@ -1153,6 +1155,60 @@ __device__ void qpel_fill(QpelLds& Q, const uint8_t* ref, int stride, int w, int
         if (r >= 2 && r <= 20 && c >= 2 && c <= 20)
             Q.jp[r][c] = (uint8_t)sk_clip255((qtap6(Q.b1[r - 2][c], Q.b1[r - 1][c], Q.b1[r][c], Q.b1[r + 1][c],
                                                     Q.b1[r + 2][c], Q.b1[r + 3][c]) + 512) >> 10);
+    }
+    wave_sync();
+}
+// The 6-tap passes slide along a row (b1/bp), a column (hp) or a column of b1 (jp) in
+// registers: each lane reads its <= 15 window samples once instead of 6 per output.
+__device__ void qpel_fill_fast(QpelLds& Q, const uint8_t* ref, int stride, int w, int ylo, int yhi, int ox, int oy) {
+    const int l = lane_id();
+    for (int i = l; i < 576; i += 64) {
+        const int r = i / 24, c = i - 24 * r;
+        Q.win[r][c] = ref[(size_t)sk_clip(oy + r, ylo, yhi) * stride + sk_clip(ox + c, 0, w - 1)];
+    }
+    wave_sync();
+    if (l < 48) {
+        const int k = l >> 1, half = l & 1;
+        // horizontal: b1 / bp of row k, columns [2, 11] or [12, 20]
+        {
+            const int c0 = half ? 12 : 2, n = half ? 9 : 10;
+            int v[15];
+#pragma unroll
+            for (int i = 0; i < 15; i++) v[i] = (i < n + 5) ? Q.win[k][c0 - 2 + i] : 0;
+#pragma unroll
+            for (int i = 0; i < 10; i++) {
+                if (i < n) {
+                    const int b1 = qtap6(v[i], v[i + 1], v[i + 2], v[i + 3], v[i + 4], v[i + 5]);
+                    Q.b1[k][c0 + i] = (int16_t)b1;
+                    Q.bp[k][c0 + i] = (uint8_t)sk_clip255((b1 + 16) >> 5);
+                }
+            }
+        }
+        // vertical: hp of column k, rows [2, 11] or [12, 20]
+        {
+            const int r0 = half ? 12 : 2, n = half ? 9 : 10;
+            int v[15];
+#pragma unroll
+            for (int i = 0; i < 15; i++) v[i] = (i < n + 5) ? Q.win[r0 - 2 + i][k] : 0;
+#pragma unroll
+            for (int i = 0; i < 10; i++)
+                if (i < n)
+                    Q.hp[r0 + i][k] = (uint8_t)sk_clip255((qtap6(v[i], v[i + 1], v[i + 2], v[i + 3], v[i + 4],
+                                                                 v[i + 5]) + 16) >> 5);
+        }
+    }
+    wave_sync();
+    if (l < 57) {   // centre: jp of column 2 + l % 19, rows [2, 8], [9, 14] or [15, 20]
+        const int c = 2 + l % 19, seg = l / 19;
+        const int r0 = seg == 0 ? 2 : (seg == 1 ? 9 : 15), n = seg == 0 ? 7 : 6;
+        int v[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) v[i] = (i < n + 5) ? Q.b1[r0 - 2 + i][c] : 0;
+#pragma unroll
+        for (int i = 0; i < 7; i++)
+            if (i < n)
+                Q.jp[r0 + i][c] = (uint8_t)sk_clip255((qtap6(v[i], v[i + 1], v[i + 2], v[i + 3], v[i + 4], v[i + 5]) +
+                                                       512) >> 10);
     }
     wave_sync();
 }
@@ -1198,7 +1254,7 @@ __global__ __launch_bounds__(256) void k_subpel(FrameArgs a) {
         return;
     }
     const int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
-    qpel_fill(Q, r.ref ? a.ref1.y : a.ref.y, a.stride_y, a.stride_y, ylo, yhi, mbx * 16 + r.mvx - 3,
+    qpel_fill_fast(Q, r.ref ? a.ref1.y : a.ref.y, a.stride_y, a.stride_y, ylo, yhi, mbx * 16 + r.mvx - 3,
               mby * 16 + r.mvy - 3);
     const int yy = l >> 2, xx = 4 * (l & 3);
     const uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + yy) * a.stride_y +
@@ -1211,6 +1267,7 @@ __global__ __launch_bounds__(256) void k_subpel(FrameArgs a) {
         return wave_sum(s);
     };
     int bx = 0, by = 0, best = sad_q(0, 0);
+    const int int_sad = best;
     for (int step = 2; step >= 1; step--) {
         const int cx = bx, cy = by;
         for (int k = 0; k < 8; k++) {   // ring order of the host reference
@@ -1227,7 +1284,7 @@ __global__ __launch_bounds__(256) void k_subpel(FrameArgs a) {
     if (l == 0) {
         a.me[idx].fx = (int8_t)bx;
         a.me[idx].fy = (int8_t)by;
-        if (bx | by) atomicAdd(&a.plan_state[mby / a.rows_per_slice].subpel_hits, 1);
+        if ((bx | by) && subpel_hit(best, int_sad)) atomicAdd(&a.plan_state[mby / a.rows_per_slice].subpel_hits, 1);
     }
 }
 
