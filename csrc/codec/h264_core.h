@@ -13,7 +13,7 @@
 namespace sk {
 namespace h264 {
 
-enum MbType : uint8_t { MB_P_SKIP = 0, MB_P_16x16 = 1, MB_I16x16 = 2 };
+enum MbType : uint8_t { MB_P_SKIP = 0, MB_P_16x16 = 1, MB_I16x16 = 2, MB_I4x4 = 3 };
 enum SliceKind : uint8_t { SLICE_NONE = 0, SLICE_P = 1, SLICE_I = 2 };
 
 constexpr int kMaxLevel = 2063;       // keeps every level inside the Baseline escape range
@@ -40,8 +40,13 @@ struct MbInfo {
     uint8_t nnz[24];         // TotalCoeff per block: 16 luma (blkIdx), 4 Cb, 4 Cr
     uint8_t ref;             // ref_idx_l0 (P_L0_16x16)
     uint8_t pad[2];
+    uint8_t i4[8];           // Intra4x4PredMode per luma4x4BlkIdx, two 4-bit modes per byte (I_NxN)
 };
-static_assert(sizeof(MbInfo) == 40, "MbInfo layout");
+static_assert(sizeof(MbInfo) == 48, "MbInfo layout");
+SK_HD int i4_mode(const MbInfo& mb, int blk) { return (mb.i4[blk >> 1] >> (4 * (blk & 1))) & 15; }
+SK_HD void set_i4_mode(MbInfo& mb, int blk, int mode) {
+    mb.i4[blk >> 1] = (uint8_t)((mb.i4[blk >> 1] & ~(15 << (4 * (blk & 1)))) | (mode << (4 * (blk & 1))));
+}
 
 // K4a exhaustive integer search (MFMA on the GPU): candidates dx, dy in
 // [-kFsR, kFsR), reference window (2*kFsR + 16)^2 clamped like every ME read.

@@ -414,7 +414,8 @@ void CpuH264Encoder::code_slice_inter(int s) {
 // Plane) by SAD against the given neighbour samples. Also returns the chroma prediction.
 static void intra_decide(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* top,
                          const uint8_t* left, int tl, const uint8_t (*ctop)[8], const uint8_t (*cleft)[8],
-                         const int* ctl, bool aT, bool aL, int* luma_mode, int* chroma_mode) {
+                         const int* ctl, bool aT, bool aL, int* luma_mode, int* chroma_mode,
+                         int* luma_sad = nullptr) {
     int dc = i16_dc(top, left, aT, aL);
     int pa = 0, pb = 0, pc = 0;
     if (aT && aL) i16_plane_params(top, left, tl, &pa, &pb, &pc);
@@ -443,6 +444,47 @@ static void intra_decide(const uint8_t* sy, const uint8_t* su, const uint8_t* sv
     }
     *luma_mode = best_mode;
     *chroma_mode = best_cm;
+    if (luma_sad) *luma_sad = best_sad;
+}
+
+// Luma of an Intra4x4 macroblock at `qp`, block by block in decoding order: prediction
+// from `outside(x, y)` (MB-relative samples of the neighbour MBs) and, inside the MB, from
+// the blocks reconstructed so far (or the source itself for the open-loop pre-pass);
+// chroma levels from trc.wc. Fills coef, nnz, cbp and the luma reconstruction `ry`;
+// returns the conservative bit bound (h264_mb.h mb_bits_crude_i16).
+template <class S>
+static int code_i4_at(int qp, const uint8_t* sy, S outside, bool aT, bool aL, bool aTR, bool open_loop,
+                      const MbTransform& trc, MbInfo& mb, int16_t* coef, uint8_t* ry) {
+    const uint8_t* inner = open_loop ? sy : ry;
+    auto sample = [&](int x, int y) -> int {
+        if (x >= 0 && x < 16 && y >= 0) return inner[y * 16 + x];
+        return outside(x, y);
+    };
+    int cbp_l = 0;
+    for (int b = 0; b < 16; b++) {
+        I4Ref r;
+        i4_ref(sample, b, aT, aL, aTR, r);
+        const int m = i4_mode(mb, b), bx = blk_x(b) * 4, by = blk_y(b) * 4;
+        int pred[16], res[16], w[16], rec[16];
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++) {
+                pred[y * 4 + x] = i4_pred_px(m, r, x, y);
+                res[y * 4 + x] = (int)sy[(by + y) * 16 + bx + x] - pred[y * 4 + x];
+            }
+        fdct4x4(res, w);
+        int16_t* c = coef + kCoefLuma + b * 16;
+        const int n = quant_block_i4(w, qp, c);
+        mb.nnz[b] = (uint8_t)n;
+        if (n) cbp_l |= 1 << (b >> 2);
+        recon_block_i4(c, qp, pred, rec);
+        for (int y = 0; y < 4; y++)
+            for (int x = 0; x < 4; x++) ry[(by + y) * 16 + bx + x] = (uint8_t)rec[y * 4 + x];
+    }
+    for (int k = 0; k < 16; k++) coef[kCoefLumaDC + k] = 0;
+    const int cbp_c = quant_chroma(trc, qp, true, coef, mb.nnz);
+    mb.cbp = (uint8_t)(cbp_l | (cbp_c << 4));
+    mb.qp = (uint8_t)qp;
+    return mb_bits_crude_i16(mb, coef, host_cavlc_tables());
 }
 
 // Edges (row above, column left, corner) of MB (mbx, mby) in plane set P.
@@ -495,12 +537,65 @@ void CpuH264Encoder::code_slice_intra(int s) {
                     memcpy(sv + y * 8, &src[2][(size_t)(mby * 8 + y) * sc + mbx * 8], 8);
                 }
                 int best_mode, best_cm, start_qp = mb_start_qp(t, idx);
+                bool i4 = false;
+                const bool aTR = aT && mbx + 1 < g.mb_w;
+                const std::vector<uint8_t>* P = pass == 0 ? src : rec;
+                auto outside = [&](int x, int y) -> int {
+                    return P[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16 + x];
+                };
                 if (pass == 0) {
-                    intra_decide(sy, su, sv, top, left, tl, ctop, cleft, ctl, aT, aL, &best_mode, &best_cm);
+                    int sad16 = 0;
+                    intra_decide(sy, su, sv, top, left, tl, ctop, cleft, ctl, aT, aL, &best_mode, &best_cm, &sad16);
+                    if (cfg.intra4x4) {
+                        MbInfo cand;
+                        memset(&cand, 0, sizeof(cand));
+                        auto src_sample = [&](int x, int y) -> int {
+                            return (x >= 0 && x < 16 && y >= 0) ? (int)sy[y * 16 + x] : outside(x, y);
+                        };
+                        const int cost4 = i4_decide(src_sample, sy, aT, aL, aTR, t.qp, cand);
+                        if (i4_wins(cost4, sad16, t.qp)) {
+                            i4 = true;
+                            memcpy(mb.i4, cand.i4, sizeof(mb.i4));
+                        }
+                    }
                 } else {
+                    i4 = mb.type == MB_I4x4;
                     best_mode = mb.i16_mode;
                     best_cm = mb.chroma_mode;
                     start_qp = mb.qp;
+                }
+                if (i4) {
+                    uint8_t pu[64], pv[64], ry[256], ru[64], rv[64];
+                    intra_chroma_pred(best_cm, ctop[0], cleft[0], ctl[0], aT, aL, pu);
+                    intra_chroma_pred(best_cm, ctop[1], cleft[1], ctl[1], aT, aL, pv);
+                    MbTransform trc;
+                    residual_transform(sy, sy, su, pu, sv, pv, trc);   // chroma part (luma residual is 0)
+                    uint8_t modes[8];
+                    memcpy(modes, mb.i4, sizeof(modes));
+                    int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
+                    memset(&mb, 0, sizeof(mb));
+                    mb.type = MB_I4x4;
+                    mb.chroma_mode = (uint8_t)best_cm;
+                    memcpy(mb.i4, modes, sizeof(modes));
+                    int qp = start_qp >= 0 ? start_qp : t.qp;
+                    const int cap = sk_min(51, t.qp + 24);
+                    for (;;) {
+                        const int bound = code_i4_at(qp, sy, outside, aT, aL, aTR, pass == 0, trc, mb, coef, ry);
+                        if (qp + 6 > cap || bound <= mb_bit_budget(true)) break;
+                        qp += 6;
+                    }
+                    if (pass == 0) continue;   // mb keeps type, modes and the start QP for pass 2
+                    me[idx].mvx = me[idx].mvy = 0;
+                    me[idx].ref = 0;
+                    me[idx].fx = me[idx].fy = 0;
+                    recon_chroma(coef, qp, (mb.cbp >> 4) & 3, pu, pv, ru, rv);
+                    for (int y = 0; y < 16; y++)
+                        memcpy(&rec[0][(size_t)(mby * 16 + y) * sy_ + mbx * 16], ry + y * 16, 16);
+                    for (int y = 0; y < 8; y++) {
+                        memcpy(&rec[1][(size_t)(mby * 8 + y) * sc + mbx * 8], ru + y * 8, 8);
+                        memcpy(&rec[2][(size_t)(mby * 8 + y) * sc + mbx * 8], rv + y * 8, 8);
+                    }
+                    continue;
                 }
                 int dc = i16_dc(top, left, aT, aL);
                 int pa = 0, pb = 0, pc = 0;
@@ -585,9 +680,9 @@ std::vector<uint8_t> CpuH264Encoder::write_slice(int s) {
                 if (!intra) { put_ue(w, (uint32_t)skip_run); skip_run = 0; }
                 int dq = 0;
                 if (mb_has_qp_delta(mb)) { dq = mb.qp - qp_prev; qp_prev = mb.qp; }
-                write_mb_header(w, mb, !intra, dq, intra ? 1 : t.num_refs);
                 MbNeighbours nb;
                 mb_neighbours(mbx, mby, t.first_row, nb);
+                write_mb_header(w, mb, !intra, dq, intra ? 1 : t.num_refs, nb);
                 write_mb_residual(w, mb, nb, &coefs[(size_t)idx * kCoefPerMb], host_cavlc_tables());
             }
         if (skip_run > 0) put_ue(w, (uint32_t)skip_run);

@@ -47,6 +47,8 @@ struct EncoderConfig {
     int codec = 0;               // 0 = H.264, 1 = HEVC (hevc_encoder.h: same front end, full frame)
     int aq_strength = 0;         // MB-level adaptive QP strength, Q4 (16 = 1.0; 0 = off): h264_mb.h aq_offset
     int subpel = 1;              // H.264 quarter-pel refinement of P vectors (K4c); HEVC keeps integer vectors
+    int intra4x4 = 0;            // H.264 I slices may code MBs as I_NxN (nine 4x4 modes) where cheaper; off
+                                 // by default like x264's ultrafast preset (partitions none)
 };
 
 struct Geometry {

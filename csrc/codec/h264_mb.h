@@ -275,6 +275,21 @@ SK_HD int block_bits_crude(const int16_t* c, int maxn, const CavlcTables& T) {
 SK_HD int mb_bits_crude_i16(const MbInfo& mb, const int16_t* coef, const CavlcTables& T) {
     const int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
     int total = 96;
+    if (mb.type == MB_I4x4) {   // 16-coefficient luma blocks of the coded 8x8s, no luma DC block
+        for (int b = 0; b < 16; b++)
+            if (cbp_l & (1 << (b >> 2))) total += block_bits_crude(coef + kCoefLuma + b * 16, 16, T);
+        if (cbp_c == 2)
+            for (int b = 0; b < 8; b++) total += block_bits_crude(coef + kCoefChromaAC + b * 16, 15, T);
+        if (cbp_c) {
+            int n0 = 0, n1 = 0, cc = 0;
+            for (int k = 0; k < 8; k++) {
+                const int a = sk_abs((int)coef[kCoefChromaDC + k]);
+                if (a) { (k < 4 ? n0 : n1)++; cc += level_bits_bound(a, 6) + 3; }
+            }
+            total += (n0 > 0 ? 11 : 2) + (n1 > 0 ? 11 : 2) + cc;
+        }
+        return total;
+    }
     if (cbp_l)
         for (int b = 0; b < 16; b++) total += block_bits_crude(coef + kCoefLuma + b * 16, 15, T);
     if (cbp_c == 2)
@@ -322,6 +337,148 @@ SK_HD int quant_mb_with_budget(const MbTransform& t, int slice_qp, bool intra16,
         qp += 6;
     }
     return qp;
+}
+
+// ---------------------------------------------------------------------------
+// Intra_4x4 (8.3.1): nine directional modes per 4x4 luma block, predicted mode from
+// the left / top blocks, top-right availability by decoding order.
+enum I4Mode { I4_V = 0, I4_H, I4_DC, I4_DDL, I4_DDR, I4_VR, I4_HD, I4_VL, I4_HU };
+
+// Neighbour samples of one 4x4 block: t[0..7] = p[0..7, -1] (p[4..7, -1] replaced by
+// p[3, -1] when the top-right block is not decoded yet), l[0..3] = p[-1, 0..3], m = p[-1, -1].
+struct I4Ref {
+    int t[8], l[4], m;
+    bool hasT, hasL;
+};
+
+// p[4..7, -1] of block b exists: above MB for blocks 0, 1, 4; above-right MB for 5;
+// inside the MB only when that block precedes b in decoding order.
+SK_HD bool i4_tr_avail(int b, bool aT, bool aTR) {
+    if (b == 0 || b == 1 || b == 4) return aT;
+    if (b == 5) return aTR;
+    return !(b == 3 || b == 7 || b == 11 || b == 13 || b == 15);
+}
+SK_HD bool i4_mode_ok(int m, bool hasT, bool hasL) {
+    if (m == I4_V || m == I4_DDL || m == I4_VL) return hasT;
+    if (m == I4_H || m == I4_HU) return hasL;
+    if (m == I4_DC) return true;
+    return hasT && hasL;   // DDR, VR, HD also read p[-1, -1]
+}
+
+// Reference samples of block b; sample(x, y) reads MB-relative luma (x, y >= -1).
+template <class S>
+SK_HD void i4_ref(S sample, int b, bool aT, bool aL, bool aTR, I4Ref& r) {
+    const int bx = blk_x(b) * 4, by = blk_y(b) * 4;
+    r.hasT = by > 0 || aT;
+    r.hasL = bx > 0 || aL;
+    const bool tr = r.hasT && i4_tr_avail(b, aT, aTR);
+    for (int i = 0; i < 4; i++) r.t[i] = r.hasT ? sample(bx + i, by - 1) : 0;
+    for (int i = 4; i < 8; i++) r.t[i] = tr ? sample(bx + i, by - 1) : r.t[3];
+    for (int i = 0; i < 4; i++) r.l[i] = r.hasL ? sample(bx - 1, by + i) : 0;
+    r.m = (r.hasT && r.hasL) ? sample(bx - 1, by - 1) : 0;
+}
+
+// Prediction sample (x, y) of mode m (8.3.1.2.1 - 8.3.1.2.9).
+SK_HD int i4_pred_px(int m, const I4Ref& r, int x, int y) {
+    auto T = [&](int i) { return i < 0 ? r.m : r.t[i]; };   // p[i, -1]
+    auto L = [&](int i) { return i < 0 ? r.m : r.l[i]; };   // p[-1, i]
+    switch (m) {
+        case I4_V: return r.t[x];
+        case I4_H: return r.l[y];
+        case I4_DC:
+            if (r.hasT && r.hasL)
+                return (r.t[0] + r.t[1] + r.t[2] + r.t[3] + r.l[0] + r.l[1] + r.l[2] + r.l[3] + 4) >> 3;
+            if (r.hasL) return (r.l[0] + r.l[1] + r.l[2] + r.l[3] + 2) >> 2;
+            if (r.hasT) return (r.t[0] + r.t[1] + r.t[2] + r.t[3] + 2) >> 2;
+            return 128;
+        case I4_DDL:
+            if (x == 3 && y == 3) return (r.t[6] + 3 * r.t[7] + 2) >> 2;
+            return (r.t[x + y] + 2 * r.t[x + y + 1] + r.t[x + y + 2] + 2) >> 2;
+        case I4_DDR:
+            if (x > y) return (T(x - y - 2) + 2 * T(x - y - 1) + T(x - y) + 2) >> 2;
+            if (x < y) return (L(y - x - 2) + 2 * L(y - x - 1) + L(y - x) + 2) >> 2;
+            return (T(0) + 2 * r.m + L(0) + 2) >> 2;
+        case I4_VR: {
+            const int z = 2 * x - y, k = x - (y >> 1);
+            if (z >= 0) return (z & 1) ? (T(k - 2) + 2 * T(k - 1) + T(k) + 2) >> 2 : (T(k - 1) + T(k) + 1) >> 1;
+            if (z == -1) return (L(0) + 2 * r.m + T(0) + 2) >> 2;
+            return (L(y - 1) + 2 * L(y - 2) + L(y - 3) + 2) >> 2;
+        }
+        case I4_HD: {
+            const int z = 2 * y - x, k = y - (x >> 1);
+            if (z >= 0) return (z & 1) ? (L(k - 2) + 2 * L(k - 1) + L(k) + 2) >> 2 : (L(k - 1) + L(k) + 1) >> 1;
+            if (z == -1) return (L(0) + 2 * r.m + T(0) + 2) >> 2;
+            return (T(x - 1) + 2 * T(x - 2) + T(x - 3) + 2) >> 2;
+        }
+        case I4_VL: {
+            const int k = x + (y >> 1);
+            return (y & 1) ? (r.t[k] + 2 * r.t[k + 1] + r.t[k + 2] + 2) >> 2 : (r.t[k] + r.t[k + 1] + 1) >> 1;
+        }
+        default: {   // I4_HU
+            const int z = x + 2 * y, k = y + (x >> 1);
+            if (z > 5) return r.l[3];
+            if (z == 5) return (r.l[2] + 3 * r.l[3] + 2) >> 2;
+            return (z & 1) ? (r.l[k] + 2 * r.l[k + 1] + r.l[k + 2] + 2) >> 2 : (r.l[k] + r.l[k + 1] + 1) >> 1;
+        }
+    }
+}
+
+// SAD cost weight of the mode bits (1 bit when the mode equals the predicted one, else 4).
+SK_HD int i4_lambda(int qp) { return 1 << ((qp > 12 ? qp - 12 : 0) / 6); }
+
+// Open-loop Intra4x4 decision over SOURCE samples (the pre-pass, every MB on its own):
+// per block in decoding order the mode of least SAD + lambda * mode bits, the predicted
+// mode taken from the blocks already decided in this MB (DC for neighbours in other
+// MBs). Returns the summed cost and fills the modes of `mb`.
+template <class S>
+SK_HD int i4_decide(S src, const uint8_t* sy, bool aT, bool aL, bool aTR, int qp, MbInfo& mb) {
+    const int lam = i4_lambda(qp);
+    MbInfo sideL, sideT;   // stand-ins for the neighbour MBs: any non-Intra4x4 type counts as DC
+    sideL.type = sideT.type = MB_I16x16;
+    int total = 0;
+    for (int b = 0; b < 16; b++) {
+        I4Ref r;
+        i4_ref(src, b, aT, aL, aTR, r);
+        const int pm = i4_predicted(i4_left_mode(mb, aL ? &sideL : nullptr, b), i4_top_mode(mb, aT ? &sideT : nullptr, b));
+        const int bx = blk_x(b) * 4, by = blk_y(b) * 4;
+        int best = 0x7fffffff, bm = I4_DC;
+        for (int m = 0; m < 9; m++) {
+            if (!i4_mode_ok(m, r.hasT, r.hasL)) continue;
+            int cost = lam * (m == pm ? 1 : 4);
+            for (int y = 0; y < 4; y++)
+                for (int x = 0; x < 4; x++) cost += sk_abs((int)sy[(by + y) * 16 + bx + x] - i4_pred_px(m, r, x, y));
+            if (cost < best) { best = cost; bm = m; }
+        }
+        set_i4_mode(mb, b, bm);
+        total += best;
+    }
+    return total;
+}
+// Intra4x4 wins over the best Intra16x16 SAD when clearly cheaper (its header is larger).
+SK_HD bool i4_wins(int cost4, int sad16, int qp) { return cost4 + 8 * i4_lambda(qp) < sad16; }
+
+// One Intra4x4 luma block: quantise the raster transform w into scan-order levels c
+// (intra rounding, all 16 coefficients, no decimation); returns TotalCoeff.
+SK_HD int quant_block_i4(const int* w, int qp, int16_t* c) {
+    const int qbits = 15 + qp / 6, f = quant_f(qbits, true);
+    const int* mf = H264_QUANT_MF[qp % 6];
+    int n = 0;
+    for (int k = 0; k < 16; k++) {
+        const int pos = zigzag4x4(k);
+        c[k] = (int16_t)quant_coef(w[pos], sel3(pos_class(pos), mf[0], mf[1], mf[2]), f, qbits);
+        n += c[k] != 0;
+    }
+    return n;
+}
+// Reconstruction of one Intra4x4 block from its levels: rec = clip(pred + residual).
+SK_HD void recon_block_i4(const int16_t* c, int qp, const int* pred, int* rec) {
+    int d[16], r[16];
+    for (int k = 0; k < 16; k++) {
+        const int pos = zigzag4x4(k);
+        d[pos] = dequant_coef(c[k], qp, pos);
+    }
+    idct4x4(d, r);
+    for (int i = 0; i < 16; i++) rec[i] = sk_clip255(pred[i] + r[i]);
 }
 
 }  // namespace h264

@@ -85,12 +85,45 @@ SK_HD int chroma_nc(const MbInfo& cur, MbNeighbours nb, int comp, int b) {
     return nc_from(aA, nA, aB, nB);
 }
 
+// intraMxMPredModeA / B of block b (8.3.1.1): inside the MB from `cur`; from the left /
+// top macroblock otherwise, 2 when that one is not Intra4x4, -1 when it is unavailable.
+SK_HD int i4_left_mode(const MbInfo& cur, const MbInfo* left, int b) {
+    const int bx = blk_x(b), by = blk_y(b);
+    if (bx > 0) return i4_mode(cur, blk_from_xy(bx - 1, by));
+    if (!left) return -1;
+    return left->type == MB_I4x4 ? i4_mode(*left, blk_from_xy(3, by)) : 2;
+}
+SK_HD int i4_top_mode(const MbInfo& cur, const MbInfo* top, int b) {
+    const int bx = blk_x(b), by = blk_y(b);
+    if (by > 0) return i4_mode(cur, blk_from_xy(bx, by - 1));
+    if (!top) return -1;
+    return top->type == MB_I4x4 ? i4_mode(*top, blk_from_xy(bx, 3)) : 2;
+}
+SK_HD int i4_predicted(int a, int b) { return (a < 0 || b < 0) ? 2 : sk_min(a, b); }
+
 // macroblock_layer() header part (everything before residual()).
-// qp_delta is only written when the syntax carries it.
+// qp_delta is only written when the syntax carries it; `nb` (left / top MBs of the
+// slice) gives the predicted Intra4x4 modes.
 template <class W>
-SK_HD void write_mb_header(W& w, const MbInfo& mb, bool p_slice, int qp_delta, int num_refs = 1) {
+SK_HD void write_mb_header(W& w, const MbInfo& mb, bool p_slice, int qp_delta, int num_refs = 1,
+                           MbNeighbours nb = MbNeighbours{nullptr, nullptr}) {
     int cbp_l = mb.cbp & 15, cbp_c = (mb.cbp >> 4) & 3;
-    if (mb.type == MB_I16x16) {
+    if (mb.type == MB_I4x4) {   // I_NxN (7.3.5.1 mb_pred, transform_size_8x8_flag absent in Baseline)
+        put_ue(w, p_slice ? 5u : 0u);
+        for (int b = 0; b < 16; b++) {
+            const int m = i4_mode(mb, b);
+            const int pm = i4_predicted(i4_left_mode(mb, nb.left, b), i4_top_mode(mb, nb.top, b));
+            if (m == pm) {
+                w.put(1u, 1);
+            } else {
+                w.put(0u, 1);
+                w.put((uint32_t)(m < pm ? m : m - 1), 3);
+            }
+        }
+        put_ue(w, mb.chroma_mode);
+        put_ue(w, H264_CBP_TO_CODE_INTRA[cbp_l | (cbp_c << 4)]);
+        if (mb.cbp) put_se(w, qp_delta);
+    } else if (mb.type == MB_I16x16) {
         put_ue(w, (uint32_t)((p_slice ? 5 : 0) + i16_mb_type(mb.i16_mode, cbp_l, cbp_c)));
         put_ue(w, mb.chroma_mode);
         put_se(w, qp_delta);
@@ -106,7 +139,7 @@ SK_HD void write_mb_header(W& w, const MbInfo& mb, bool p_slice, int qp_delta, i
 }
 
 SK_HD bool mb_has_qp_delta(const MbInfo& mb) {
-    return mb.type == MB_I16x16 || (mb.type == MB_P_16x16 && mb.cbp != 0);
+    return mb.type == MB_I16x16 || ((mb.type == MB_P_16x16 || mb.type == MB_I4x4) && mb.cbp != 0);
 }
 
 // residual() for one macroblock; `coef` points at the MB's kCoefPerMb levels.

@@ -1891,7 +1891,7 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
         AtomicBitWriter w{bits, 0};
         if (p_slice) put_ue(w, (uint32_t)run);
         int dq = mb_has_qp_delta(mb) ? (int)mb.qp - qp_prev : 0;
-        write_mb_header(w, mb, p_slice, dq, p_slice ? t.num_refs : 1);
+        write_mb_header(w, mb, p_slice, dq, p_slice ? t.num_refs : 1, nb);
         hdr_bits = (int)w.pos;
     }
     hdr_bits = __shfl(hdr_bits, 0);

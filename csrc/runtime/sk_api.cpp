@@ -200,6 +200,7 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.codec = c->codec == 1 ? 1 : 0;
     e.aq_strength = c->aq_strength > 0 ? (c->aq_strength > 64 ? 64 : c->aq_strength) : 0;
     e.subpel = c->subpel >= 0 ? 1 : 0;
+    e.intra4x4 = c->intra4x4 > 0 ? 1 : 0;
     if (e.codec == 1) {   // HEVC: full-frame pictures, slices of whole CTB rows, one reference
         e.aq_strength = 0;   // no cu_qp_delta in this HEVC profile setup
         e.fullframe = 1;
@@ -257,6 +258,10 @@ void* sk_h264_create(const sk_h264_config* c) {
     // both backends accept the same configurations.
     if (c->stripe_height > 240) {
         set_last_error("stripe_height must be <= 240 (15 macroblock rows per stripe)");
+        return nullptr;
+    }
+    if (c->intra4x4 > 0 && c->backend == 1) {   // GPU I_NxN path: see k_intra_prep / k_code_intra
+        set_last_error("intra4x4 is not available on the HIP backend yet");
         return nullptr;
     }
     if (c->qp < 0 || c->qp > 51 || c->paint_qp < 0 || c->paint_qp > 51) {

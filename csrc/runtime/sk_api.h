@@ -23,6 +23,7 @@ typedef struct sk_h264_config {
     int32_t codec;                  // 0 = H.264 (stripes or full frame), 1 = HEVC Main (full frame, WPP)
     int32_t aq_strength;            // H.264 MB-level adaptive QP, Q4 (16 = 1.0); 0 = off
     int32_t subpel;                 // H.264 quarter-pel motion refinement: 0 = default (on), < 0 off
+    int32_t intra4x4;               // H.264 Intra4x4 (I_NxN) macroblocks in I slices: > 0 on, else off
 } sk_h264_config;
 
 typedef struct sk_packet {

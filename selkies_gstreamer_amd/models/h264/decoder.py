@@ -380,6 +380,8 @@ class MbState:
     ref: np.ndarray = field(default_factory=lambda: np.full(16, -1, dtype=np.int64))
     tc_luma: np.ndarray = field(default_factory=lambda: np.zeros(16, dtype=np.int64))  # raster y*4+x
     tc_chroma: np.ndarray = field(default_factory=lambda: np.zeros((2, 4), dtype=np.int64))  # raster 2x2
+    i4: bool = False         # coded as Intra_4x4 (I_NxN)
+    i4_modes: np.ndarray = field(default_factory=lambda: np.full(16, 2, dtype=np.int64))  # raster y*4+x
     db: tuple = (1, 0, 0)  # (disable_deblocking_filter_idc, FilterOffsetA, FilterOffsetB) of its slice
 
 
@@ -735,7 +737,7 @@ class H264Decoder:
         if mb_type == 25:
             self._decode_pcm(br, sps, cur, mbx, mby)
         elif mb_type == 0:
-            raise NotImplementedError("I_NxN")
+            self._decode_i4(br, sps, pps, cur, mbx, mby, sid)
         elif 1 <= mb_type <= 24:
             self._decode_i16(br, sps, pps, cur, mbx, mby, sid, mb_type)
         else:
@@ -911,6 +913,167 @@ class H264Decoder:
         pu = self._pred_chroma(chroma_mode, *self._intra_neighbours(sps, pps, self.cur[1], mbx, mby, sid, 8))
         pv = self._pred_chroma(chroma_mode, *self._intra_neighbours(sps, pps, self.cur[2], mbx, mby, sid, 8))
         self._recon_chroma(sps, pps, cur, mbx, mby, dc, acc, pu, pv)
+
+    # ---- Intra_4x4 (8.3.1) ------------------------------------------------------
+    def _i4_nb_mode(self, sps, cur, mbx, mby, x4, y4, sid):
+        """intraMxMPredModeN of the 4x4 block at MB-relative (x4, y4); None if unavailable."""
+        if 0 <= x4 < 4 and 0 <= y4 < 4:
+            return int(cur.i4_modes[y4 * 4 + x4])
+        m, xx, yy = self._nb4(sps, mbx, mby, x4, y4, sid)
+        if m is None:
+            return None
+        return int(m.i4_modes[yy * 4 + xx]) if m.i4 else 2
+
+    def _i4_samples(self, sps, Y, mbx, mby, bx, by, sid):
+        """p[x, -1] for x = -1..7 and p[-1, y] for y = 0..3 of block (bx, by) (None where
+        not available for Intra_4x4 prediction, p[4..7, -1] already substituted)."""
+        x0, y0 = mbx * 16 + bx * 4, mby * 16 + by * 4
+
+        def decoded(x4, y4):   # neighbouring 4x4 block (MB-relative, may be outside) already decoded?
+            if 0 <= x4 < 4 and 0 <= y4 < 4:
+                order = [(T.BLK_X[k], T.BLK_Y[k]) for k in range(16)]
+                return order.index((x4, y4)) < order.index((bx, by))
+            if x4 >= 4 and y4 >= 0:
+                return False   # macroblock to the right: not decoded yet
+            m, _, _ = self._nb4(sps, mbx, mby, x4, y4, sid)
+            return m is not None
+        top = [None] * 9   # index x + 1, x = -1..7
+        left = [None] * 4
+        if decoded(bx, by - 1):
+            for x in range(4):
+                top[x + 1] = int(Y[y0 - 1, x0 + x])
+            if decoded(bx + 1, by - 1):
+                for x in range(4, 8):
+                    top[x + 1] = int(Y[y0 - 1, x0 + x])
+            else:
+                for x in range(4, 8):
+                    top[x + 1] = top[4]
+        if decoded(bx - 1, by):
+            for y in range(4):
+                left[y] = int(Y[y0 + y, x0 - 1])
+        if decoded(bx - 1, by - 1):
+            top[0] = int(Y[y0 - 1, x0 - 1])
+        return top, left
+
+    def _pred_i4(self, mode, top, left):
+        P = np.zeros((4, 4), np.int64)
+        t = lambda x: top[x + 1]           # p[x, -1], x = -1..7
+        l = lambda y: top[0] if y < 0 else left[y]   # p[-1, y], y = -1..3
+        need_t = mode in (0, 3, 4, 5, 6, 7)
+        need_l = mode in (1, 4, 5, 6, 8)
+        if (need_t and top[1] is None) or (need_l and left[0] is None) or (mode in (4, 5, 6) and top[0] is None):
+            raise BitstreamError(f"Intra4x4 mode {mode} without its neighbours")
+        for y in range(4):
+            for x in range(4):
+                if mode == 0:
+                    v = t(x)
+                elif mode == 1:
+                    v = l(y)
+                elif mode == 2:
+                    ht, hl = top[1] is not None, left[0] is not None
+                    if ht and hl:
+                        v = (sum(t(i) for i in range(4)) + sum(l(i) for i in range(4)) + 4) >> 3
+                    elif hl:
+                        v = (sum(l(i) for i in range(4)) + 2) >> 2
+                    elif ht:
+                        v = (sum(t(i) for i in range(4)) + 2) >> 2
+                    else:
+                        v = 128
+                elif mode == 3:   # Diagonal_Down_Left
+                    v = (t(6) + 3 * t(7) + 2) >> 2 if x == 3 and y == 3 else (t(x + y) + 2 * t(x + y + 1) + t(x + y + 2) + 2) >> 2
+                elif mode == 4:   # Diagonal_Down_Right
+                    if x > y:
+                        v = (t(x - y - 2) + 2 * t(x - y - 1) + t(x - y) + 2) >> 2
+                    elif x < y:
+                        v = (l(y - x - 2) + 2 * l(y - x - 1) + l(y - x) + 2) >> 2
+                    else:
+                        v = (t(0) + 2 * t(-1) + l(0) + 2) >> 2
+                elif mode == 5:   # Vertical_Right
+                    z = 2 * x - y
+                    if z in (0, 2, 4, 6):
+                        v = (t(x - (y >> 1) - 1) + t(x - (y >> 1)) + 1) >> 1
+                    elif z in (1, 3, 5):
+                        v = (t(x - (y >> 1) - 2) + 2 * t(x - (y >> 1) - 1) + t(x - (y >> 1)) + 2) >> 2
+                    elif z == -1:
+                        v = (l(0) + 2 * l(-1) + t(0) + 2) >> 2
+                    else:
+                        v = (l(y - 1) + 2 * l(y - 2) + l(y - 3) + 2) >> 2
+                elif mode == 6:   # Horizontal_Down
+                    z = 2 * y - x
+                    if z in (0, 2, 4, 6):
+                        v = (l(y - (x >> 1) - 1) + l(y - (x >> 1)) + 1) >> 1
+                    elif z in (1, 3, 5):
+                        v = (l(y - (x >> 1) - 2) + 2 * l(y - (x >> 1) - 1) + l(y - (x >> 1)) + 2) >> 2
+                    elif z == -1:
+                        v = (l(0) + 2 * l(-1) + t(0) + 2) >> 2
+                    else:
+                        v = (t(x - 1) + 2 * t(x - 2) + t(x - 3) + 2) >> 2
+                elif mode == 7:   # Vertical_Left
+                    if y in (0, 2):
+                        v = (t(x + (y >> 1)) + t(x + (y >> 1) + 1) + 1) >> 1
+                    else:
+                        v = (t(x + (y >> 1)) + 2 * t(x + (y >> 1) + 1) + t(x + (y >> 1) + 2) + 2) >> 2
+                elif mode == 8:   # Horizontal_Up
+                    z = x + 2 * y
+                    if z in (0, 2, 4):
+                        v = (l(y + (x >> 1)) + l(y + (x >> 1) + 1) + 1) >> 1
+                    elif z in (1, 3):
+                        v = (l(y + (x >> 1)) + 2 * l(y + (x >> 1) + 1) + l(y + (x >> 1) + 2) + 2) >> 2
+                    elif z == 5:
+                        v = (l(2) + 3 * l(3) + 2) >> 2
+                    else:
+                        v = l(3)
+                else:
+                    raise BitstreamError(f"Intra4x4 mode {mode}")
+                P[y, x] = v
+        return P
+
+    def _decode_i4(self, br, sps, pps, cur, mbx, mby, sid):
+        self.stats["i4"] += 1
+        cur.intra = True
+        cur.i4 = True
+        for blk in range(16):
+            bx, by = T.BLK_X[blk], T.BLK_Y[blk]
+            a = self._i4_nb_mode(sps, cur, mbx, mby, bx - 1, by, sid)
+            b = self._i4_nb_mode(sps, cur, mbx, mby, bx, by - 1, sid)
+            pred = 2 if a is None or b is None else min(a, b)
+            if br.u1():
+                mode = pred
+            else:
+                rem = br.u(3)
+                mode = rem if rem < pred else rem + 1
+            cur.i4_modes[by * 4 + bx] = mode
+        chroma_mode = br.ue()
+        code = br.ue()
+        if code > 47:
+            raise BitstreamError("coded_block_pattern out of range")
+        cbp = T.CODE_TO_CBP_INTRA[code]
+        cbp_l, cbp_c = cbp & 15, cbp >> 4
+        if cbp:
+            self._read_qp_delta(br)
+        cur.qp = self.qp
+        levels = [[0] * 16 for _ in range(16)]
+        for b8 in range(4):
+            if not cbp_l & (1 << b8):
+                continue
+            for i in range(4):
+                blk = b8 * 4 + i
+                bx, by = T.BLK_X[blk], T.BLK_Y[blk]
+                nc = self._total_coeff_luma(cur, sps, mbx, mby, bx, by, sid)
+                levels[blk], tc = self.residual_block(br, nc, 16)
+                cur.tc_luma[by * 4 + bx] = tc
+        dc, ac = self._chroma_residual(br, sps, pps, cur, mbx, mby, sid, cbp_c)
+        Y = self.cur[0]
+        qp = cur.qp
+        for blk in range(16):   # decoding order: each block predicts from the ones before it
+            bx, by = T.BLK_X[blk], T.BLK_Y[blk]
+            top, left = self._i4_samples(sps, Y, mbx, mby, bx, by, sid)
+            p = self._pred_i4(int(cur.i4_modes[by * 4 + bx]), top, left)
+            r = _idct4(_scale_4x4(_unzigzag(levels[blk]), qp, skip_dc=False))
+            Y[mby * 16 + by * 4:mby * 16 + by * 4 + 4, mbx * 16 + bx * 4:mbx * 16 + bx * 4 + 4] = _clip1(p + r)
+        pu = self._pred_chroma(chroma_mode, *self._intra_neighbours(sps, pps, self.cur[1], mbx, mby, sid, 8))
+        pv = self._pred_chroma(chroma_mode, *self._intra_neighbours(sps, pps, self.cur[2], mbx, mby, sid, 8))
+        self._recon_chroma(sps, pps, cur, mbx, mby, dc, ac, pu, pv)
 
     def _decode_pcm(self, br, sps, cur, mbx, mby):
         self.stats["pcm"] += 1

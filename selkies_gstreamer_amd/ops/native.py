@@ -33,7 +33,7 @@ class SkH264Config(ctypes.Structure):
         ("backend", ctypes.c_int32), ("deblock", ctypes.c_int32), ("me_full", ctypes.c_int32),
         ("shared_copy", ctypes.c_int32), ("src_width", ctypes.c_int32), ("src_height", ctypes.c_int32),
         ("num_refs", ctypes.c_int32), ("codec", ctypes.c_int32), ("aq_strength", ctypes.c_int32),
-        ("subpel", ctypes.c_int32),
+        ("subpel", ctypes.c_int32), ("intra4x4", ctypes.c_int32),
     ]
 
 
@@ -206,6 +206,7 @@ class Packet:
 MB_INFO_DTYPE = np.dtype([
     ("mvx", "<i2"), ("mvy", "<i2"), ("mvdx", "<i2"), ("mvdy", "<i2"), ("type", "u1"), ("i16_mode", "u1"),
     ("chroma_mode", "u1"), ("cbp", "u1"), ("qp", "u1"), ("nnz", "u1", (24,)), ("ref", "u1"), ("pad", "u1", (2,)),
+    ("i4", "u1", (8,)),
 ])
 ME_DTYPE = np.dtype([("mvx", "<i2"), ("mvy", "<i2"), ("sad", "<i4"), ("intra_est", "<i4"), ("ref", "<i2"),
                      ("fx", "i1"), ("fy", "i1")])
@@ -224,7 +225,7 @@ class H264Encoder:
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
                  backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
                  src_width: int = 0, src_height: int = 0, num_refs: int = 1, codec: str = "h264",
-                 aq_strength: float = 0.0, subpel: bool = True):
+                 aq_strength: float = 0.0, subpel: bool = True, intra4x4: bool = False):
         """aq_strength: MB-level adaptive QP (h264_mb.h aq_offset), 1.0 = x264 aq-mode 1
         strength; 0 = constant QP per slice (x264 ultrafast behaviour)."""
         L = lib()
@@ -238,7 +239,7 @@ class H264Encoder:
                                 device, 1 if backend == "hip" else 0, 1 if deblock else -1,
                                 1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height),
                                 int(num_refs), 1 if codec == "hevc" else 0, int(round(aq_strength * 16)),
-                                0 if subpel else -1)
+                                0 if subpel else -1, 1 if intra4x4 else 0)
         if codec not in ("h264", "hevc"):
             raise ValueError("codec must be 'h264' or 'hevc'")
         self.codec = codec
