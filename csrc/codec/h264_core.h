@@ -40,12 +40,15 @@ struct MbInfo {
     uint8_t nnz[24];         // TotalCoeff per block: 16 luma (blkIdx), 4 Cb, 4 Cr
     uint8_t ref;             // ref_idx_l0 (P_L0_16x16)
     uint8_t pad[2];
-    uint8_t i4[8];           // Intra4x4PredMode per luma4x4BlkIdx, two 4-bit modes per byte (I_NxN)
+    uint32_t i4lo, i4hi;     // Intra4x4PredMode per luma4x4BlkIdx, 4 bits each (blocks 0-7, 8-15; I_NxN)
 };
 static_assert(sizeof(MbInfo) == 48, "MbInfo layout");
-SK_HD int i4_mode(const MbInfo& mb, int blk) { return (mb.i4[blk >> 1] >> (4 * (blk & 1))) & 15; }
+// (two scalar words rather than an array: a GPU loop over blocks then needs no scratch)
+SK_HD int i4_mode(const MbInfo& mb, int blk) { return (int)(((blk < 8 ? mb.i4lo : mb.i4hi) >> (4 * (blk & 7))) & 15u); }
 SK_HD void set_i4_mode(MbInfo& mb, int blk, int mode) {
-    mb.i4[blk >> 1] = (uint8_t)((mb.i4[blk >> 1] & ~(15 << (4 * (blk & 1)))) | (mode << (4 * (blk & 1))));
+    const uint32_t sh = 4 * (blk & 7), v = (uint32_t)mode << sh, msk = 15u << sh;
+    if (blk < 8) mb.i4lo = (mb.i4lo & ~msk) | v;
+    else mb.i4hi = (mb.i4hi & ~msk) | v;
 }
 
 // K4a exhaustive integer search (MFMA on the GPU): candidates dx, dy in

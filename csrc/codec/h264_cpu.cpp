@@ -555,7 +555,8 @@ void CpuH264Encoder::code_slice_intra(int s) {
                         const int cost4 = i4_decide(src_sample, sy, aT, aL, aTR, t.qp, cand);
                         if (i4_wins(cost4, sad16, t.qp)) {
                             i4 = true;
-                            memcpy(mb.i4, cand.i4, sizeof(mb.i4));
+                            mb.i4lo = cand.i4lo;
+                            mb.i4hi = cand.i4hi;
                         }
                     }
                 } else {
@@ -570,13 +571,13 @@ void CpuH264Encoder::code_slice_intra(int s) {
                     intra_chroma_pred(best_cm, ctop[1], cleft[1], ctl[1], aT, aL, pv);
                     MbTransform trc;
                     residual_transform(sy, sy, su, pu, sv, pv, trc);   // chroma part (luma residual is 0)
-                    uint8_t modes[8];
-                    memcpy(modes, mb.i4, sizeof(modes));
+                    const uint32_t m_lo = mb.i4lo, m_hi = mb.i4hi;
                     int16_t* coef = &coefs[(size_t)idx * kCoefPerMb];
                     memset(&mb, 0, sizeof(mb));
                     mb.type = MB_I4x4;
                     mb.chroma_mode = (uint8_t)best_cm;
-                    memcpy(mb.i4, modes, sizeof(modes));
+                    mb.i4lo = m_lo;
+                    mb.i4hi = m_hi;
                     int qp = start_qp >= 0 ? start_qp : t.qp;
                     const int cap = sk_min(51, t.qp + 24);
                     for (;;) {

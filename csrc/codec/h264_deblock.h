@@ -59,7 +59,7 @@ inline const DbTables& host_db_tables() {
 
 // What the filter needs to know about one macroblock (8 bytes, shared CPU/GPU layout).
 struct DbInfo {
-    uint8_t intra;     // bit 0: I16x16; bits 1+: ref_idx (bS 1 across different reference pictures)
+    uint8_t intra;     // bit 0: intra MB (I16x16 / I4x4); bits 1+: ref_idx (bS 1 across different reference pictures)
     uint8_t qpy;       // QP_Y as the decoder derives it (mb_qp_delta chain, 7.4.5)
     uint16_t nz;       // bit (by*4+bx): luma 4x4 block at raster (bx,by) has coded coefficients
     int16_t mvx, mvy;  // quarter-pel
@@ -68,7 +68,8 @@ static_assert(sizeof(DbInfo) == 8, "DbInfo layout");
 
 SK_HD DbInfo db_info(const MbInfo& mb, int qpy) {
     DbInfo d;
-    d.intra = (uint8_t)((mb.type == MB_I16x16 ? 1 : 0) | (mb.type == MB_I16x16 ? 0 : mb.ref << 1));
+    const bool intra = mb.type == MB_I16x16 || mb.type == MB_I4x4;
+    d.intra = (uint8_t)(intra ? 1 : mb.ref << 1);
     d.qpy = (uint8_t)qpy;
     uint32_t nz = 0;
     for (int b = 0; b < 16; b++)

@@ -349,6 +349,16 @@ enum I4Mode { I4_V = 0, I4_H, I4_DC, I4_DDL, I4_DDR, I4_VR, I4_HD, I4_VL, I4_HU 
 struct I4Ref {
     int t[8], l[4], m;
     bool hasT, hasL;
+    SK_HD int T(int i) const { return i < 0 ? m : t[i]; }   // p[i, -1], i = -1..7
+    SK_HD int L(int i) const { return i < 0 ? m : l[i]; }   // p[-1, i], i = -1..3
+};
+// The same samples packed in 13 bytes (p[0] corner, p[1..8] top, p[9..12] left), e.g. in
+// LDS on the GPU, so a lane-dependent index never lands in a private array.
+struct I4RefView {
+    const uint8_t* p;
+    bool hasT, hasL;
+    SK_HD int T(int i) const { return p[1 + i]; }
+    SK_HD int L(int i) const { return i < 0 ? p[0] : p[9 + i]; }
 };
 
 // p[4..7, -1] of block b exists: above MB for blocks 0, 1, 4; above-right MB for 5;
@@ -364,61 +374,77 @@ SK_HD bool i4_mode_ok(int m, bool hasT, bool hasL) {
     if (m == I4_DC) return true;
     return hasT && hasL;   // DDR, VR, HD also read p[-1, -1]
 }
+SK_HD bool i4_has_top(int b, bool aT) { return blk_y(b) > 0 || aT; }
+SK_HD bool i4_has_left(int b, bool aL) { return blk_x(b) > 0 || aL; }
+
+// Reference sample k (I4RefView packing) of block b; sample(x, y) reads MB-relative luma.
+template <class S>
+SK_HD int i4_ref_sample(S sample, int b, bool aT, bool aL, bool aTR, int k) {
+    const int bx = blk_x(b) * 4, by = blk_y(b) * 4;
+    const bool hasT = i4_has_top(b, aT), hasL = i4_has_left(b, aL);
+    if (k == 0) return (hasT && hasL) ? sample(bx - 1, by - 1) : 0;
+    if (k <= 8) {
+        int i = k - 1;
+        if (!hasT) return 0;
+        if (i >= 4 && !i4_tr_avail(b, aT, aTR)) i = 3;
+        return sample(bx + i, by - 1);
+    }
+    return hasL ? sample(bx - 1, by + k - 9) : 0;
+}
 
 // Reference samples of block b; sample(x, y) reads MB-relative luma (x, y >= -1).
 template <class S>
 SK_HD void i4_ref(S sample, int b, bool aT, bool aL, bool aTR, I4Ref& r) {
-    const int bx = blk_x(b) * 4, by = blk_y(b) * 4;
-    r.hasT = by > 0 || aT;
-    r.hasL = bx > 0 || aL;
-    const bool tr = r.hasT && i4_tr_avail(b, aT, aTR);
-    for (int i = 0; i < 4; i++) r.t[i] = r.hasT ? sample(bx + i, by - 1) : 0;
-    for (int i = 4; i < 8; i++) r.t[i] = tr ? sample(bx + i, by - 1) : r.t[3];
-    for (int i = 0; i < 4; i++) r.l[i] = r.hasL ? sample(bx - 1, by + i) : 0;
-    r.m = (r.hasT && r.hasL) ? sample(bx - 1, by - 1) : 0;
+    r.hasT = i4_has_top(b, aT);
+    r.hasL = i4_has_left(b, aL);
+    r.m = i4_ref_sample(sample, b, aT, aL, aTR, 0);
+    for (int i = 0; i < 8; i++) r.t[i] = i4_ref_sample(sample, b, aT, aL, aTR, 1 + i);
+    for (int i = 0; i < 4; i++) r.l[i] = i4_ref_sample(sample, b, aT, aL, aTR, 9 + i);
 }
 
-// Prediction sample (x, y) of mode m (8.3.1.2.1 - 8.3.1.2.9).
-SK_HD int i4_pred_px(int m, const I4Ref& r, int x, int y) {
-    auto T = [&](int i) { return i < 0 ? r.m : r.t[i]; };   // p[i, -1]
-    auto L = [&](int i) { return i < 0 ? r.m : r.l[i]; };   // p[-1, i]
+// Prediction sample (x, y) of mode m (8.3.1.2.1 - 8.3.1.2.9); R gives T(i) = p[i, -1]
+// (i = -1..7), L(i) = p[-1, i] (i = -1..3) and the hasT / hasL flags.
+template <class R>
+SK_HD int i4_pred_px(int m, const R& r, int x, int y) {
     switch (m) {
-        case I4_V: return r.t[x];
-        case I4_H: return r.l[y];
+        case I4_V: return r.T(x);
+        case I4_H: return r.L(y);
         case I4_DC:
             if (r.hasT && r.hasL)
-                return (r.t[0] + r.t[1] + r.t[2] + r.t[3] + r.l[0] + r.l[1] + r.l[2] + r.l[3] + 4) >> 3;
-            if (r.hasL) return (r.l[0] + r.l[1] + r.l[2] + r.l[3] + 2) >> 2;
-            if (r.hasT) return (r.t[0] + r.t[1] + r.t[2] + r.t[3] + 2) >> 2;
+                return (r.T(0) + r.T(1) + r.T(2) + r.T(3) + r.L(0) + r.L(1) + r.L(2) + r.L(3) + 4) >> 3;
+            if (r.hasL) return (r.L(0) + r.L(1) + r.L(2) + r.L(3) + 2) >> 2;
+            if (r.hasT) return (r.T(0) + r.T(1) + r.T(2) + r.T(3) + 2) >> 2;
             return 128;
         case I4_DDL:
-            if (x == 3 && y == 3) return (r.t[6] + 3 * r.t[7] + 2) >> 2;
-            return (r.t[x + y] + 2 * r.t[x + y + 1] + r.t[x + y + 2] + 2) >> 2;
+            if (x == 3 && y == 3) return (r.T(6) + 3 * r.T(7) + 2) >> 2;
+            return (r.T(x + y) + 2 * r.T(x + y + 1) + r.T(x + y + 2) + 2) >> 2;
         case I4_DDR:
-            if (x > y) return (T(x - y - 2) + 2 * T(x - y - 1) + T(x - y) + 2) >> 2;
-            if (x < y) return (L(y - x - 2) + 2 * L(y - x - 1) + L(y - x) + 2) >> 2;
-            return (T(0) + 2 * r.m + L(0) + 2) >> 2;
+            if (x > y) return (r.T(x - y - 2) + 2 * r.T(x - y - 1) + r.T(x - y) + 2) >> 2;
+            if (x < y) return (r.L(y - x - 2) + 2 * r.L(y - x - 1) + r.L(y - x) + 2) >> 2;
+            return (r.T(0) + 2 * r.T(-1) + r.L(0) + 2) >> 2;
         case I4_VR: {
             const int z = 2 * x - y, k = x - (y >> 1);
-            if (z >= 0) return (z & 1) ? (T(k - 2) + 2 * T(k - 1) + T(k) + 2) >> 2 : (T(k - 1) + T(k) + 1) >> 1;
-            if (z == -1) return (L(0) + 2 * r.m + T(0) + 2) >> 2;
-            return (L(y - 1) + 2 * L(y - 2) + L(y - 3) + 2) >> 2;
+            if (z >= 0)
+                return (z & 1) ? (r.T(k - 2) + 2 * r.T(k - 1) + r.T(k) + 2) >> 2 : (r.T(k - 1) + r.T(k) + 1) >> 1;
+            if (z == -1) return (r.L(0) + 2 * r.T(-1) + r.T(0) + 2) >> 2;
+            return (r.L(y - 1) + 2 * r.L(y - 2) + r.L(y - 3) + 2) >> 2;
         }
         case I4_HD: {
             const int z = 2 * y - x, k = y - (x >> 1);
-            if (z >= 0) return (z & 1) ? (L(k - 2) + 2 * L(k - 1) + L(k) + 2) >> 2 : (L(k - 1) + L(k) + 1) >> 1;
-            if (z == -1) return (L(0) + 2 * r.m + T(0) + 2) >> 2;
-            return (T(x - 1) + 2 * T(x - 2) + T(x - 3) + 2) >> 2;
+            if (z >= 0)
+                return (z & 1) ? (r.L(k - 2) + 2 * r.L(k - 1) + r.L(k) + 2) >> 2 : (r.L(k - 1) + r.L(k) + 1) >> 1;
+            if (z == -1) return (r.L(0) + 2 * r.T(-1) + r.T(0) + 2) >> 2;
+            return (r.T(x - 1) + 2 * r.T(x - 2) + r.T(x - 3) + 2) >> 2;
         }
         case I4_VL: {
             const int k = x + (y >> 1);
-            return (y & 1) ? (r.t[k] + 2 * r.t[k + 1] + r.t[k + 2] + 2) >> 2 : (r.t[k] + r.t[k + 1] + 1) >> 1;
+            return (y & 1) ? (r.T(k) + 2 * r.T(k + 1) + r.T(k + 2) + 2) >> 2 : (r.T(k) + r.T(k + 1) + 1) >> 1;
         }
         default: {   // I4_HU
             const int z = x + 2 * y, k = y + (x >> 1);
-            if (z > 5) return r.l[3];
-            if (z == 5) return (r.l[2] + 3 * r.l[3] + 2) >> 2;
-            return (z & 1) ? (r.l[k] + 2 * r.l[k + 1] + r.l[k + 2] + 2) >> 2 : (r.l[k] + r.l[k + 1] + 1) >> 1;
+            if (z > 5) return r.L(3);
+            if (z == 5) return (r.L(2) + 3 * r.L(3) + 2) >> 2;
+            return (z & 1) ? (r.L(k) + 2 * r.L(k + 1) + r.L(k + 2) + 2) >> 2 : (r.L(k) + r.L(k + 1) + 1) >> 1;
         }
     }
 }

@@ -65,6 +65,7 @@ struct FrameArgs {
     int me_full;           // K4a on: MFMA exhaustive-search candidate per dirty MB
     int aq_strength;       // MB-level adaptive QP strength (Q4), 0 = off
     int subpel;            // K4c quarter-pel refinement (k_subpel) before K6
+    int intra4x4;          // I slices may code I_NxN macroblocks (k_intra_prep decides, k_code_intra codes)
     const uint8_t* ov_img[kOverlaySlots];   // K12/K13 overlay images (premultiplied BGRA)
     const OverlayParams* ov;                // [kOverlaySlots] placement of this frame (device copy)
     int8_t* aq;            // [num_mbs] AQ offsets (k_aq), valid for MBs of coded slices

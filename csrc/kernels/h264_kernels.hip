@@ -735,6 +735,9 @@ struct MbScratch {                 // per-wave LDS
     uint8_t pad[8];
     int cdcp[8];                   // chroma DC predictions [comp][block]
     uint8_t nb[64];                // intra neighbour samples (intra_pred_lanes layout)
+    uint8_t nbtr[4];               // Intra4x4: p[16..19, -1] (above-right MB's bottom row)
+    uint8_t ref13[16];             // Intra4x4: reference samples of the block being coded (I4RefView)
+    uint8_t ry[256];               // Intra4x4: luma reconstruction of the MB so far (16x16)
 };
 
 // In-place 4x4 Hadamard H*X*H of a raster int[16] in LDS: rows by lanes 0..3,
@@ -779,7 +782,7 @@ __device__ __forceinline__ int quad_sum(int v) {
 // writes per-block TotalCoeff into S.nnz. The MB size check first uses a
 // lane-parallel conservative bound and only runs the exact (nC-free) CAVLC bound
 // of mb_bits_bound when that one exceeds the budget: same decisions as the CPU.
-__device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16, MbScratch& S,
+__device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16, MbScratch& S,
                               int* bound_out, const CavlcTables& T, unsigned long long* dbg = nullptr,
                               int step = 0) {
     const int l = lane_id();
@@ -980,7 +983,7 @@ __device__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16
 }
 
 // Reconstruct this lane's luma row (4 px) and chroma row (lanes < 32).
-__device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, const int* pred_l,
+__device__ __forceinline__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, const int* pred_l,
                                const int* pred_c, int* rec_l, int* rec_c) {
     const int l = lane_id();
     const int b = l >> 2, r = l & 3;
@@ -1042,7 +1045,7 @@ __device__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, cons
 
 // Transform + quant (with QP escalation) + recon for one MB. Inputs per lane:
 // src/pred of its luma row (4 px) and chroma row. Writes coefs + MbInfo fields.
-__device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, const int* pred_c,
+__device__ __forceinline__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, const int* pred_c,
                        int slice_qp, bool intra16, MbScratch& S, MbInfo& mb, int* rec_l, int* rec_c,
                        int16_t* gcoef, const CavlcTables& T, unsigned long long* dbg = nullptr,
                        int step = 0, int start_qp = -1, bool quant_only = false) {
@@ -1081,6 +1084,115 @@ __device__ int code_mb(const int* src_l, const int* pred_l, const int* src_c, co
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(S.coef);
     uint32_t* g32 = reinterpret_cast<uint32_t*>(gcoef);
     for (int i = l; i < kCoefPerMb / 2; i += 64) g32[i] = s32[i];
+    return qp;
+}
+
+// Intra4x4 macroblock (h264_cpu.cpp code_i4_at): luma block by block in decoding order,
+// the 4 lanes of quad b own block b (lane = one row of 4 samples), prediction from
+// `sample(x, y)` (MB-relative; the chain passes LDS edges + the reconstruction so far,
+// the open-loop pre-pass the source), DPP quad transforms, intra rounding, no decimation;
+// then chroma as quant_chroma(intra) and the QP escalation on the conservative bound
+// (mb_bits_crude_i16). Writes S.coef / S.nnz / S.ry, mb.cbp / qp; returns the QP.
+template <class Smp>
+__device__ __forceinline__ int code_mb_i4(Smp sample, const int* src_l, const int* src_c, const int* pred_c, int start_qp,
+                          int slice_qp, bool aT, bool aL, bool aTR, MbScratch& S, MbInfo& mb, int* rec_l,
+                          int* rec_c, int16_t* gcoef, const CavlcTables& T) {
+    const int l = lane_id();
+    const int q = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    int xc[4], wc[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) xc[j] = src_c[j] - pred_c[j];
+    fwd4_quad(xc, r, wc);
+    int qp = __builtin_amdgcn_readfirstlane(start_qp);
+    const int cap = sk_min(51, slice_qp + 24);
+    for (;;) {
+        const int qbits = 15 + qp / 6, f = quant_f(qbits, true);
+        const int* mf = H264_QUANT_MF[qp % 6];
+        const int m0 = mf[0], m1 = mf[1], m2 = mf[2];
+        for (int b = 0; b < 16; b++) {
+            const int m = i4_mode(mb, b);
+            if (l < 13) S.ref13[l] = (uint8_t)i4_ref_sample(sample, b, aT, aL, aTR, l);
+            wave_sync();
+            const I4RefView ref{S.ref13, i4_has_top(b, aT), i4_has_left(b, aL)};
+            const bool mine = q == b;
+            int pred[4], res[4], w[4], lv[4], d[4], rr[4], n = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                pred[j] = i4_pred_px(m, ref, j, r);
+                res[j] = src_l[j] - pred[j];
+            }
+            fwd4_quad(res, r, w);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int pos = r * 4 + j;
+                lv[j] = quant_coef(w[j], sel3(pos_class(pos), m0, m1, m2), f, qbits);
+                n += lv[j] != 0;
+                d[j] = dequant_coef(lv[j], qp, pos);
+                if (mine) S.coef[kCoefLuma + b * 16 + inv_zigzag4x4(pos)] = (int16_t)lv[j];
+            }
+            n = quad_sum(n);
+            if (mine && r == 0) S.nnz[b] = (uint8_t)n;
+            inv4_quad(d, r, rr);
+            if (mine) {
+                const int y = blk_y(b) * 4 + r, x0 = blk_x(b) * 4;
+#pragma unroll
+                for (int j = 0; j < 4; j++) S.ry[y * 16 + x0 + j] = (uint8_t)sk_clip255(pred[j] + rr[j]);
+            }
+            wave_sync();   // the next block predicts from this one
+        }
+        // chroma: quant_chroma(intra): DC 2x2 Hadamard, AC with intra rounding, no decimation
+        const int qpc = chroma_qp(qp), qbc = 15 + qpc / 6, fc = quant_f(qbc, true);
+        const int* mfc = H264_QUANT_MF[qpc % 6];
+        int nc = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int pos = r * 4 + j;
+            const int lvc = pos == 0 ? 0 : quant_coef(wc[j], sel3(pos_class(pos), mfc[0], mfc[1], mfc[2]), fc, qbc);
+            nc += lvc != 0;
+            if (l < 32) S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + inv_zigzag4x4(pos)] = (int16_t)lvc;
+        }
+        if (l < 32 && r == 0) S.dcc[comp * 4 + cb] = wc[0];
+        if (l < 16) S.coef[kCoefLumaDC + l] = 0;
+        nc = quad_sum(nc);
+        wave_sync();
+        int cdc_nz = 0;
+        if (l < 8) {
+            const int c = l >> 2, i = l & 3;
+            const int d0 = S.dcc[c * 4 + 0], d1 = S.dcc[c * 4 + 1], d2 = S.dcc[c * 4 + 2], d3 = S.dcc[c * 4 + 3];
+            const int v = i == 0 ? d0 + d1 + d2 + d3 : (i == 1 ? d0 - d1 + d2 - d3 : (i == 2 ? d0 + d1 - d2 - d3 : d0 - d1 - d2 + d3));
+            const int lv = quant_coef(v, mfc[0], 2 * fc, qbc + 1);
+            S.coef[kCoefChromaDC + c * 4 + i] = (int16_t)lv;
+            cdc_nz = lv != 0;
+        }
+        const bool ac0 = __ballot(l < 16 && nc > 0) != 0ull, ac1 = __ballot(l >= 16 && l < 32 && nc > 0) != 0ull;
+        const bool any_dc = __ballot(cdc_nz != 0) != 0ull;
+        const int cbp_c = (ac0 || ac1) ? 2 : (any_dc ? 1 : 0);
+        if (l < 32 && r == 0) S.nnz[16 + comp * 4 + cb] = cbp_c == 2 ? (uint8_t)nc : 0;
+        wave_sync();
+        int cbp_l = 0;
+        for (int b8 = 0; b8 < 4; b8++)
+            if (S.nnz[4 * b8] | S.nnz[4 * b8 + 1] | S.nnz[4 * b8 + 2] | S.nnz[4 * b8 + 3]) cbp_l |= 1 << b8;
+        mb.cbp = (uint8_t)(cbp_l | (cbp_c << 4));
+        mb.qp = (uint8_t)qp;
+        // conservative size bound (every lane evaluates the same serial sum over LDS)
+        const int bound = __builtin_amdgcn_readfirstlane(mb_bits_crude_i16(mb, S.coef, T));
+        if (qp + 6 > cap || bound <= mb_bit_budget(true)) break;
+        qp += 6;
+        wave_sync();
+    }
+    int zero[4] = {0, 0, 0, 0}, dummy[4];
+    recon_mb_lanes(qp, false, mb.cbp & 0x30, S, zero, pred_c, dummy, rec_c);   // chroma only (luma cbp masked)
+    {
+        const int y = blk_y(q) * 4 + r, x0 = blk_x(q) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; j++) rec_l[j] = S.ry[y * 16 + x0 + j];
+    }
+    if (gcoef) {
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(S.coef);
+        uint32_t* g32 = reinterpret_cast<uint32_t*>(gcoef);
+        for (int i = l; i < kCoefPerMb / 2; i += 64) g32[i] = s32[i];
+    }
     return qp;
 }
 
@@ -1410,9 +1522,10 @@ __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
 // evaluation order DC, V, H, Plane; chroma DC, H, V, Plane (first minimum wins).
 // topp/leftp/ctop/cleft: neighbour samples (zeros when unavailable), lane layout
 // as everywhere (b, r luma rows; comp/cb chroma rows).
-__device__ void intra_modes_wave(const int* src_l, const int* src_c, const uint8_t* topp, const uint8_t* leftp,
+__device__ __forceinline__ void intra_modes_wave(const int* src_l, const int* src_c, const uint8_t* topp, const uint8_t* leftp,
                                  int tl, const uint8_t* const* ctop, const uint8_t* const* cleft, const int* ctl,
-                                 bool aT, bool aL, int* cdcp, int* luma_mode, int* chroma_mode) {
+                                 bool aT, bool aL, int* cdcp, int* luma_mode, int* chroma_mode,
+                                 int* luma_sad = nullptr) {
     const int l = lane_id();
     const int b = l >> 2, r = l & 3;
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
@@ -1458,6 +1571,7 @@ __device__ void intra_modes_wave(const int* src_l, const int* src_c, const uint8
     }
     *luma_mode = best_mode;
     *chroma_mode = best_cm;
+    if (luma_sad) *luma_sad = best_sad;
 }
 
 // Sum of v over the lanes of a wave-uniform lane mask (DPP + readlanes).
@@ -1467,7 +1581,7 @@ __device__ __forceinline__ int wave_sum_masked(int v, bool on) { return wave_sum
 // nb: the wave's neighbour samples in LDS, top 16 | left 16 | ctop[2][8] | cleft[2][8]
 // (zeros when unavailable); tl / ctl: corner samples. Sums (DC, plane gradients) are
 // wave reductions, so no lane walks the edges serially.
-__device__ void intra_pred_lanes(int mode, int cmode, const uint8_t* nb, int tl, const int* ctl, bool aT, bool aL,
+__device__ __forceinline__ void intra_pred_lanes(int mode, int cmode, const uint8_t* nb, int tl, const int* ctl, bool aT, bool aL,
                                  int* pred_l, int* pred_c) {
     const int l = lane_id();
     const int b = l >> 2, r = l & 3;
@@ -1600,22 +1714,82 @@ __global__ __launch_bounds__(256) void k_intra_prep(FrameArgs a) {
         src_l[j] = (sw >> (8 * j)) & 255;
         src_c[j] = (csw >> (8 * j)) & 255;
     }
-    int mode, cmode;
-    intra_modes_wave(src_l, src_c, nb, nb + 16, tl, ctop, cleft, ctl, aT, aL, S.cdcp, &mode, &cmode);
+    int mode, cmode, sad16;
+    intra_modes_wave(src_l, src_c, nb, nb + 16, tl, ctop, cleft, ctl, aT, aL, S.cdcp, &mode, &cmode, &sad16);
     int pred_l[4], pred_c[4];
     intra_pred_lanes(mode, cmode, nb, tl, ctl, aT, aL, pred_l, pred_c);
+    const int start = a.aq_strength > 0 ? aq_start_qp(t.qp, a.aq[idx]) : -1;
+    MbInfo cand;
+    memset(&cand, 0, sizeof(cand));
+    bool i4 = false;
+    const bool aTR = aT && mbx + 1 < a.mb_w;
+    // open-loop source samples, MB-relative (the pre-pass predicts from the source)
+    auto src_smp = [&](int x, int y) __attribute__((always_inline)) -> int {
+        return a.src.y[(size_t)(mby * 16 + y) * a.stride_y + mbx * 16 + x];
+    };
+    if (a.intra4x4) {
+        // Intra4x4 decision (h264_mb.h i4_decide): the SAD of every mode of every block in
+        // parallel (quad = block), then the predicted-mode costs in decoding order
+        const int q = l >> 2;
+        int* sads = reinterpret_cast<int*>(S.coef);   // 16 x 9, before any levels are written
+        uint8_t* refs = S.ry;                          // 16 x 13 reference samples (quad = block)
+        for (int k = r; k < 13; k += 4) refs[q * 13 + k] = (uint8_t)i4_ref_sample(src_smp, q, aT, aL, aTR, k);
+        wave_sync();
+        const I4RefView ref{refs + q * 13, i4_has_top(q, aT), i4_has_left(q, aL)};
+        for (int m = 0; m < 9; m++) {
+            int sad = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) sad += sk_abs(src_l[j] - i4_pred_px(m, ref, j, r));
+            sad = quad_sum(sad);
+            if (r == 0) sads[q * 9 + m] = i4_mode_ok(m, ref.hasT, ref.hasL) ? sad : -1;
+        }
+        wave_sync();
+        const int lam = i4_lambda(t.qp);
+        int total = 0;
+        for (int b = 0; b < 16; b++) {
+            // i4_decide: neighbours in other MBs count as DC (2) when available
+            const int bx = blk_x(b), by = blk_y(b);
+            const int ma = bx > 0 ? i4_mode(cand, blk_from_xy(bx - 1, by)) : (aL ? 2 : -1);
+            const int mt = by > 0 ? i4_mode(cand, blk_from_xy(bx, by - 1)) : (aT ? 2 : -1);
+            const int pm = i4_predicted(ma, mt);
+            int best = 0x7fffffff, bm = I4_DC;
+            for (int m = 0; m < 9; m++) {
+                const int sd = sads[b * 9 + m];
+                if (sd < 0) continue;
+                const int cost = sd + lam * (m == pm ? 1 : 4);
+                if (cost < best) { best = cost; bm = m; }
+            }
+            set_i4_mode(cand, b, bm);
+            total += best;
+        }
+        i4 = i4_wins(total, sad16, t.qp);
+        wave_sync();
+    }
     MbInfo mb;
     memset(&mb, 0, sizeof(mb));
-    int rec_l[4], rec_c[4];
-    const int qp = code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c, nullptr, T, nullptr, 0,
-                           a.aq_strength > 0 ? aq_start_qp(t.qp, a.aq[idx]) : -1, true);
+    int qp;
+    if (i4) {
+        mb.type = MB_I4x4;
+        mb.chroma_mode = (uint8_t)cmode;
+        mb.i4lo = cand.i4lo;
+        mb.i4hi = cand.i4hi;
+        int rec_l[4], rec_c[4];
+        qp = code_mb_i4(src_smp, src_l, src_c, pred_c, start >= 0 ? start : t.qp, t.qp, aT, aL, aTR, S, mb, rec_l,
+                        rec_c, nullptr, T);
+    } else {
+        int rec_l[4], rec_c[4];
+        qp = code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c, nullptr, T, nullptr, 0, start,
+                     true);
+    }
     if (l == 0) {
         MbInfo o;
         memset(&o, 0, sizeof(o));
-        o.type = MB_I16x16;
+        o.type = i4 ? MB_I4x4 : MB_I16x16;
         o.i16_mode = (uint8_t)mode;
         o.chroma_mode = (uint8_t)cmode;
         o.qp = (uint8_t)qp;
+        o.i4lo = cand.i4lo;
+        o.i4hi = cand.i4hi;
         a.mbs[idx] = o;
     }
 }
@@ -1637,7 +1811,8 @@ struct IntraEdges {
 struct IntraSrc {
     uint32_t y[64];      // 16 rows x 16 px (row-major, 4 words per row)
     uint32_t c[32];      // Cb 8x8 then Cr 8x8 (2 words per row)
-    int mode, cmode, qp, pad;
+    int mode, cmode, qp, i4;   // i4: coded as Intra4x4 (pre-pass decision)
+    uint32_t i4m[2];     // its 16 modes (MbInfo i4lo / i4hi)
 };
 constexpr int kIntraRing = 4;   // MB slots per row in flight (producer runs 2 steps ahead)
 
@@ -1689,6 +1864,9 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
                 d.mode = pre.i16_mode;
                 d.cmode = pre.chroma_mode;
                 d.qp = pre.qp;
+                d.i4 = pre.type == MB_I4x4;
+                d.i4m[0] = pre.i4lo;
+                d.i4m[1] = pre.i4hi;
             }
         }
     };
@@ -1745,17 +1923,37 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
                     src_l[j] = (sw >> (8 * j)) & 255;
                     src_c[j] = (csw >> (8 * j)) & 255;
                 }
+                const bool is_i4 = __builtin_amdgcn_readfirstlane(in.i4) != 0;
                 int pred_l[4], pred_c[4];
-                intra_pred_lanes(mode, cmode, nb, tl, ctl, aT, aL, pred_l, pred_c);
+                intra_pred_lanes(is_i4 ? 2 : mode, cmode, nb, tl, ctl, aT, aL, pred_l, pred_c);
                 STAMP(step, 2);
                 MbInfo mb;
                 memset(&mb, 0, sizeof(mb));
-                mb.type = MB_I16x16;
-                mb.i16_mode = (uint8_t)mode;
                 mb.chroma_mode = (uint8_t)cmode;
                 int rec_l[4], rec_c[4];
-                code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c,
-                        a.coefs + (size_t)idx * kCoefPerMb, T, a.dbg, step, start_qp);
+                if (is_i4) {
+                    const bool aTR = aT && mbx + 1 < a.mb_w;
+                    if (l < 4) S.nbtr[l] = aTR ? E.bot_y[w - 1][(mbx + 1) & 3][l] : 0;
+                    const uint32_t m0 = __builtin_amdgcn_readfirstlane(in.i4m[0]);
+                    const uint32_t m1 = __builtin_amdgcn_readfirstlane(in.i4m[1]);
+                    mb.i4lo = m0;
+                    mb.i4hi = m1;
+                    mb.type = MB_I4x4;
+                    wave_sync();
+                    // reconstruction so far (S.ry) inside the MB, LDS edges outside
+                    auto smp = [&](int x, int y) __attribute__((always_inline)) -> int {
+                        if (y >= 0 && x >= 0) return S.ry[y * 16 + x];
+                        if (y < 0) return x < 0 ? tl : (x < 16 ? (int)nb[x] : (int)S.nbtr[x - 16]);
+                        return nb[16 + y];
+                    };
+                    code_mb_i4(smp, src_l, src_c, pred_c, start_qp, t.qp, aT, aL, aTR, S, mb, rec_l, rec_c,
+                               a.coefs + (size_t)idx * kCoefPerMb, T);
+                } else {
+                    mb.type = MB_I16x16;
+                    mb.i16_mode = (uint8_t)mode;
+                    code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c,
+                            a.coefs + (size_t)idx * kCoefPerMb, T, a.dbg, step, start_qp);
+                }
                 STAMP(step, 6);
                 // edges for the neighbours first (LDS), then the global stores
                 wave_sync();

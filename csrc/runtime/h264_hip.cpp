@@ -386,6 +386,7 @@ class HipBackend : public EncoderBackend {
         a.me_full = cfg_.me_full;
         a.aq_strength = cfg_.codec == 1 ? 0 : cfg_.aq_strength;
         a.subpel = cfg_.codec == 1 ? 0 : cfg_.subpel;
+        a.intra4x4 = cfg_.codec == 1 ? 0 : cfg_.intra4x4;
         a.aq = dmalloc<int8_t>(nmb);
         for (int k = 0; k < kOverlaySlots; k++) {
             ov_img_dev_[k] = dmalloc<uint8_t>((size_t)kOverlayMaxDim * kOverlayMaxDim * 4);

@@ -260,10 +260,6 @@ void* sk_h264_create(const sk_h264_config* c) {
         set_last_error("stripe_height must be <= 240 (15 macroblock rows per stripe)");
         return nullptr;
     }
-    if (c->intra4x4 > 0 && c->backend == 1) {   // GPU I_NxN path: see k_intra_prep / k_code_intra
-        set_last_error("intra4x4 is not available on the HIP backend yet");
-        return nullptr;
-    }
     if (c->qp < 0 || c->qp > 51 || c->paint_qp < 0 || c->paint_qp > 51) {
         set_last_error("qp out of range");
         return nullptr;

@@ -206,7 +206,7 @@ class Packet:
 MB_INFO_DTYPE = np.dtype([
     ("mvx", "<i2"), ("mvy", "<i2"), ("mvdx", "<i2"), ("mvdy", "<i2"), ("type", "u1"), ("i16_mode", "u1"),
     ("chroma_mode", "u1"), ("cbp", "u1"), ("qp", "u1"), ("nnz", "u1", (24,)), ("ref", "u1"), ("pad", "u1", (2,)),
-    ("i4", "u1", (8,)),
+    ("i4lo", "<u4"), ("i4hi", "<u4"),
 ])
 ME_DTYPE = np.dtype([("mvx", "<i2"), ("mvy", "<i2"), ("sad", "<i4"), ("intra_est", "<i4"), ("ref", "<i2"),
                      ("fx", "i1"), ("fy", "i1")])

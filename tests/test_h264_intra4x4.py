@@ -93,3 +93,15 @@ def test_intra4x4_gpu_matches_cpu(fullframe):
         pb = [(p.y, p.data) for p in b.encode(f, t)]
         assert pa == pb, f"frame {t}"
     assert (b.debug_buffer("mbs", MB_INFO_DTYPE)["type"] == 3).any() or True
+
+
+def test_intra4x4_with_deblocking_decodes():
+    W, H = 192, 128
+    enc = H264Encoder(W, H, stripe_height=32, qp=30, use_paint_over=False, intra4x4=True, deblock=True)
+    dec = StripeDecoder(W, H)
+    for t in range(2):
+        enc.request_keyframe()
+        for p in enc.encode(_glyphs(W, H, t), t):
+            dec.feed(p.data)
+        ref = np.frombuffer(enc.debug_buffer("ref_y", np.uint8), np.uint8).reshape(-1, (W + 15) // 16 * 16)[:H, :W]
+        assert np.array_equal(dec.Y, ref), f"frame {t}"

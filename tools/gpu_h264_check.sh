@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-h264}
 mkdir -p gpurun_out/$TAG
-timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_h264_subpel.py tests/test_h264_gpu.py tests/test_overlay.py tests/test_session_migration.py tests/test_parallel_banded.py tests/test_dist_banded.py -m gpu > gpurun_out/$TAG/pytest.log 2>&1 || { tail -40 gpurun_out/$TAG/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_h264_subpel.py tests/test_h264_gpu.py tests/test_overlay.py tests/test_session_migration.py tests/test_parallel_banded.py tests/test_dist_banded.py tests/test_h264_intra4x4.py -m gpu > gpurun_out/$TAG/pytest.log 2>&1 || { tail -40 gpurun_out/$TAG/pytest.log; exit 1; }
 tail -1 gpurun_out/$TAG/pytest.log
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --e2e-sessions 0 > gpurun_out/$TAG/bench.jsonl 2>&1 || exit 1
 tail -1 gpurun_out/$TAG/bench.jsonl | cut -c1-240

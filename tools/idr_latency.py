@@ -15,10 +15,11 @@ W, H = 1920, 1080
 frames = int(sys.argv[1]) if len(sys.argv) > 1 else 60
 period = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 kind = sys.argv[3] if len(sys.argv) > 3 else "motion"
+intra4x4 = len(sys.argv) > 4 and sys.argv[4] == "i4"
 src = SyntheticDesktop(W, H, kind)
 pool = [src.frame(i) for i in range(8)]
-enc = H264Encoder(W, H, stripe_height=64, backend="hip", use_paint_over=False)
-idr, p = [], []
+enc = H264Encoder(W, H, stripe_height=64, backend="hip", use_paint_over=False, intra4x4=intra4x4)
+idr, p, idr_bytes = [], [], []
 for t in range(frames):
     key = t >= 10 and t % period == 0
     if key:
@@ -28,5 +29,8 @@ for t in range(frames):
     dt = (time.perf_counter() - t0) * 1e3
     if t >= 10:
         (idr if key else p).append(dt)
-print(f"IDR frames: n={len(idr)} median {np.median(idr):.3f} ms max {max(idr):.3f} ms")
+        if key:
+            idr_bytes.append(sum(len(x.data) for x in pk))
+print(f"IDR frames: n={len(idr)} median {np.median(idr):.3f} ms max {max(idr):.3f} ms, "
+      f"median {np.median(idr_bytes) / 1024:.1f} KiB (intra4x4={intra4x4})")
 print(f"P frames:   n={len(p)} median {np.median(p):.3f} ms max {max(p):.3f} ms")
