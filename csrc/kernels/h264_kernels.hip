@@ -736,7 +736,7 @@ struct MbScratch {                 // per-wave LDS
     int cdcp[8];                   // chroma DC predictions [comp][block]
     uint8_t nb[64];                // intra neighbour samples (intra_pred_lanes layout)
     uint8_t nbtr[4];               // Intra4x4: p[16..19, -1] (above-right MB's bottom row)
-    uint8_t ref13[16];             // Intra4x4: reference samples of the block being coded (I4RefView)
+    uint8_t ref13[32];             // Intra4x4: reference samples of the (<= 2) blocks being coded (I4RefView)
     uint8_t ry[256];               // Intra4x4: luma reconstruction of the MB so far (16x16)
 };
 
@@ -1087,6 +1087,51 @@ __device__ __forceinline__ int code_mb(const int* src_l, const int* pred_l, cons
     return qp;
 }
 
+// mb_bits_crude_i16 of an Intra4x4 MB, lane-parallel: quad q = luma block q (and chroma
+// AC block q for q < 8), each lane 4 scan positions; block terms as block_bits_crude.
+__device__ __forceinline__ int i4_bound_lanes(const MbScratch& S, int cbp, const CavlcTables& T) {
+    const int l = lane_id(), q = l >> 2, r = l & 3;
+    const int cbp_l = cbp & 15, cbp_c = (cbp >> 4) & 3;
+    auto block_term = [&](const int16_t* c, int maxn, bool on) __attribute__((always_inline)) {
+        int n = 0, last = -1, mx = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int v = sk_abs((int)c[r * 4 + j]);
+            if (v) { n++; last = r * 4 + j; mx = sk_max(mx, v); }
+        }
+        n = quad_sum(n);
+        last = quad_max(last);
+        mx = quad_max(mx);
+        const int sl = suffix_len_cap(mx);
+        int lv = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int v = sk_abs((int)c[r * 4 + j]);
+            if (v) lv += level_bits_bound(v, sl);
+        }
+        lv = quad_sum(lv);
+        int b = 6;
+        if (n) {
+            const int tz = (maxn == 16 ? last + 1 : last) - n;
+            b = T.ct_max_tc[n] + lv;
+            if (n < maxn) b += T.tz_len[n - 1][tz];
+            if (n > 1 && tz > 0) b += tz <= 2 ? 2 * (n - 1) : (tz <= 6 ? 3 * (n - 1) : 3 * (n - 1) + 8);
+        }
+        return (on && r == 0) ? b : 0;
+    };
+    int t = block_term(S.coef + kCoefLuma + q * 16, 16, (cbp_l >> (q >> 2)) & 1);
+    t += block_term(S.coef + kCoefChromaAC + (q & 7) * 16, 15, cbp_c == 2 && q < 8);
+    int dn = 0, dc = 0;
+    if (l < 8) {
+        const int a = sk_abs((int)S.coef[kCoefChromaDC + l]);
+        if (a) { dn = 1; dc = level_bits_bound(a, 6) + 3; }
+    }
+    const int n0 = wave_sum(l < 4 ? dn : 0), n1 = wave_sum(l >= 4 && l < 8 ? dn : 0), cc = wave_sum(dc);
+    int total = 96 + wave_sum(t);
+    if (cbp_c) total += (n0 > 0 ? 11 : 2) + (n1 > 0 ? 11 : 2) + cc;
+    return total;
+}
+
 // Intra4x4 macroblock (h264_cpu.cpp code_i4_at): luma block by block in decoding order,
 // the 4 lanes of quad b own block b (lane = one row of 4 samples), prediction from
 // `sample(x, y)` (MB-relative; the chain passes LDS edges + the reconstruction so far,
@@ -1110,16 +1155,31 @@ __device__ __forceinline__ int code_mb_i4(Smp sample, const int* src_l, const in
         const int qbits = 15 + qp / 6, f = quant_f(qbits, true);
         const int* mf = H264_QUANT_MF[qp % 6];
         const int m0 = mf[0], m1 = mf[1], m2 = mf[2];
-        for (int b = 0; b < 16; b++) {
-            const int m = i4_mode(mb, b);
-            if (l < 13) S.ref13[l] = (uint8_t)i4_ref_sample(sample, b, aT, aL, aTR, l);
+        // diagonal wavefront over the 4x4 blocks: stage st codes the blocks with bx + 2 by == st
+        // (left, top, top-left and top-right neighbours all belong to earlier stages), so
+        // 16 blocks take 10 dependent stages with up to two blocks in flight
+        const int qx = blk_x(q), qy = blk_y(q);
+        const int m = i4_mode(mb, q);
+        for (int st = 0; st < 10; st++) {
+            const int by_lo = sk_max(0, (st - 2) >> 1), by_hi = sk_min(3, st >> 1);
+            {   // reference samples: lanes 0..12 for the block of row by_lo, 16..28 for by_lo + 1
+                const int slot = l >> 4, k = l & 15, by = by_lo + slot;
+                if (k < 13 && by <= by_hi)
+                    S.ref13[slot * 16 + k] =
+                        (uint8_t)i4_ref_sample(sample, blk_from_xy(st - 2 * by, by), aT, aL, aTR, k);
+            }
             wave_sync();
-            const I4RefView ref{S.ref13, i4_has_top(b, aT), i4_has_left(b, aL)};
-            const bool mine = q == b;
+            const bool mine = qx + 2 * qy == st;
+            // lanes of idle quads follow the first active block (same mode, same samples), so
+            // the mode switch diverges over at most the two active modes
+            const int b0 = blk_from_xy(st - 2 * by_lo, by_lo);
+            const int qq = mine ? q : b0;
+            const int me = mine ? m : i4_mode(mb, b0);
+            const I4RefView ref{S.ref13 + (mine ? (qy - by_lo) * 16 : 0), i4_has_top(qq, aT), i4_has_left(qq, aL)};
             int pred[4], res[4], w[4], lv[4], d[4], rr[4], n = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                pred[j] = i4_pred_px(m, ref, j, r);
+                pred[j] = i4_pred_px(me, ref, j, r);
                 res[j] = src_l[j] - pred[j];
             }
             fwd4_quad(res, r, w);
@@ -1129,17 +1189,16 @@ __device__ __forceinline__ int code_mb_i4(Smp sample, const int* src_l, const in
                 lv[j] = quant_coef(w[j], sel3(pos_class(pos), m0, m1, m2), f, qbits);
                 n += lv[j] != 0;
                 d[j] = dequant_coef(lv[j], qp, pos);
-                if (mine) S.coef[kCoefLuma + b * 16 + inv_zigzag4x4(pos)] = (int16_t)lv[j];
+                if (mine) S.coef[kCoefLuma + q * 16 + inv_zigzag4x4(pos)] = (int16_t)lv[j];
             }
             n = quad_sum(n);
-            if (mine && r == 0) S.nnz[b] = (uint8_t)n;
+            if (mine && r == 0) S.nnz[q] = (uint8_t)n;
             inv4_quad(d, r, rr);
             if (mine) {
-                const int y = blk_y(b) * 4 + r, x0 = blk_x(b) * 4;
 #pragma unroll
-                for (int j = 0; j < 4; j++) S.ry[y * 16 + x0 + j] = (uint8_t)sk_clip255(pred[j] + rr[j]);
+                for (int j = 0; j < 4; j++) S.ry[(qy * 4 + r) * 16 + qx * 4 + j] = (uint8_t)sk_clip255(pred[j] + rr[j]);
             }
-            wave_sync();   // the next block predicts from this one
+            wave_sync();   // the next stage predicts from these blocks
         }
         // chroma: quant_chroma(intra): DC 2x2 Hadamard, AC with intra rounding, no decimation
         const int qpc = chroma_qp(qp), qbc = 15 + qpc / 6, fc = quant_f(qbc, true);
@@ -1176,7 +1235,7 @@ __device__ __forceinline__ int code_mb_i4(Smp sample, const int* src_l, const in
         mb.cbp = (uint8_t)(cbp_l | (cbp_c << 4));
         mb.qp = (uint8_t)qp;
         // conservative size bound (every lane evaluates the same serial sum over LDS)
-        const int bound = __builtin_amdgcn_readfirstlane(mb_bits_crude_i16(mb, S.coef, T));
+        const int bound = i4_bound_lanes(S, mb.cbp, T);
         if (qp + 6 > cap || bound <= mb_bit_budget(true)) break;
         qp += 6;
         wave_sync();
