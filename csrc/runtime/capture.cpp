@@ -105,9 +105,14 @@ class CaptureSession {
                 e.damage_threshold = s.damage_block_threshold > 0 ? s.damage_block_threshold : 10;
                 e.damage_duration = s.damage_block_duration > 0 ? s.damage_block_duration : 20;
                 e.fps = (float)(s.target_fps > 0 ? s.target_fps : 60.0);
+                e.aq_strength = sk_clip(s.h264_aq_strength, 0, 64);
+                e.subpel = s.h264_subpel >= 0 ? 1 : 0;
+                e.intra4x4 = s.h264_intra4x4 > 0 ? 1 : 0;
                 if (s.output_mode == 2) {   // HEVC: full-frame pictures, slices of CTB rows
                     e.codec = 1;
                     e.fullframe = 1;
+                    e.aq_strength = 0;
+                    e.intra4x4 = 0;
                 }
                 enc_.reset(backend ? create_hip_backend(e, s.device) : create_cpu_backend(e));
             }

@@ -104,6 +104,10 @@ typedef struct sk_capture_settings {
     int32_t step_mode;       // 1: encode only frames granted by sk_capture_run, unpaced (benchmarks)
     const uint8_t* pool;     // source 4: caller-owned BGRx frames (pool_frames x capture_height rows)
     int32_t pool_frames, pool_stride, pool_phase;
+    // H.264 quality tools (0 = defaults: AQ off, quarter-pel on, Intra4x4 off)
+    int32_t h264_aq_strength;  // MB-level adaptive QP, Q4 (16 = x264 aq-strength 1.0)
+    int32_t h264_subpel;       // < 0: integer-pel motion only
+    int32_t h264_intra4x4;     // > 0: I_NxN macroblocks in keyframes
 } sk_capture_settings;
 
 typedef struct sk_stripe_result {

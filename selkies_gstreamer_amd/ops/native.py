@@ -65,6 +65,7 @@ class SkCaptureSettings(ctypes.Structure):
         ("output_width", ctypes.c_int32), ("output_height", ctypes.c_int32),
         ("step_mode", ctypes.c_int32), ("pool", ctypes.c_void_p),
         ("pool_frames", ctypes.c_int32), ("pool_stride", ctypes.c_int32), ("pool_phase", ctypes.c_int32),
+        ("h264_aq_strength", ctypes.c_int32), ("h264_subpel", ctypes.c_int32), ("h264_intra4x4", ctypes.c_int32),
     ]
 
 

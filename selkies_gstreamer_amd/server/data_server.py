@@ -669,6 +669,9 @@ class DataStreamingServer:
             cs.h264_fullcolor = int(bool(p["h264_fullcolor"]))
             cs.h264_streaming_mode = int(bool(p["h264_streaming_mode"]))
             cs.h264_fullframe = int(enc == "x264enc")
+            cs.h264_aq_strength = max(0, min(64, int(self.settings.h264_aq_strength)))
+            cs.h264_subpel = 0 if self.settings.h264_subpel[0] else -1
+            cs.h264_intra4x4 = int(bool(self.settings.h264_intra4x4[0]))
         cs.use_paint_over_quality = int(bool(p["use_paint_over_quality"]))
         cs.paint_over_trigger_frames, cs.damage_block_threshold, cs.damage_block_duration = 15, 10, 20
         cs.use_cpu = int(bool(p["use_cpu"]))

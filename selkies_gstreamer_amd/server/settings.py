@@ -112,6 +112,11 @@ def build_specs() -> list[Spec]:
         _r("jpeg_quality", "1-100", 40, "Allowed JPEG quality range or a fixed value."),
         _b("h264_fullcolor", False, "H.264 full colour range."),
         _b("h264_streaming_mode", False, "H.264 streaming mode (encode every frame)."),
+        Spec("h264_aq_strength", "int", 0, "H.264 MB-level adaptive QP strength in 1/16 (16 = x264 aq-strength "
+             "1.0; 0 = constant QP like the ultrafast preset)."),
+        _b("h264_subpel", True, "H.264 quarter-pel motion refinement (adaptive per stripe)."),
+        _b("h264_intra4x4", False, "H.264 Intra4x4 (I_NxN) macroblocks in keyframes: fewer bits on text, "
+           "~3x the keyframe encode time."),
         _b("use_cpu", False, "Force the CPU reference encoder instead of the MI355X pipeline."),
         _b("use_paint_over_quality", True, "High-quality paint-over for static regions."),
         _r("paint_over_jpeg_quality", "1-100", 90, "JPEG paint-over quality range or value."),
@@ -154,7 +159,8 @@ def build_specs() -> list[Spec]:
 
 
 # Settings that are only meaningful to the server and never sent to clients.
-SERVER_ONLY = ("port", "dri_node", "debug", "audio_device_name", "watermark_path")
+SERVER_ONLY = ("port", "dri_node", "debug", "audio_device_name", "watermark_path", "h264_aq_strength", "h264_subpel",
+               "h264_intra4x4")
 
 
 class Settings:
