@@ -764,6 +764,23 @@ __device__ __forceinline__ void lds_hadamard4x4(int* x) {
     wave_sync();
 }
 
+// 4x4 Hadamard H*X*H of the values in lanes 0..15 (raster: lane = 4y + x) in registers:
+// rows by DPP quad permutes, columns by lane shuffles (no LDS round trip, no wave_sync).
+__device__ __forceinline__ int lane_hadamard16(int v) {
+    const int l = lane_id(), x = l & 3, y = (l >> 2) & 3;
+    int P = __builtin_amdgcn_mov_dpp(v, 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
+    int Q = __builtin_amdgcn_mov_dpp(v, 0xF5, 0xF, 0xF, false);   // quad_perm [1,1,3,3]
+    int a = (x & 1) ? P - Q : P + Q;                               // s01 d01 s23 d23
+    P = __builtin_amdgcn_mov_dpp(a, 0x50, 0xF, 0xF, false);       // quad_perm [0,0,1,1]
+    Q = __builtin_amdgcn_mov_dpp(a, 0xFA, 0xF, 0xF, false);       // quad_perm [2,2,3,3]
+    a = (x == 0 || x == 3) ? P + Q : P - Q;
+    const int pr = __shfl(a, l ^ 4);
+    const int b = (y & 1) ? pr - a : a + pr;
+    P = __shfl(b, (l & ~15) + x + 4 * (y >> 1));
+    Q = __shfl(b, (l & ~15) + x + 4 * (2 + (y >> 1)));
+    return (y == 0 || y == 3) ? P + Q : P - Q;
+}
+
 __device__ __forceinline__ int quad_max(int v) {
     v = sk_max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
     v = sk_max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
@@ -809,7 +826,7 @@ __device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int 
             ln_l += lv != 0;
             if (lv) lastl = sk_max(lastl, (int)((izz_row >> (8 * j)) & 255));
         }
-        if (intra16 && r == 0) S.dcy[blk_y(b) * 4 + blk_x(b)] = wl[0];
+
         if (!intra16 && l < 16) S.coef[kCoefLumaDC + l] = 0;
     }
     // ---- chroma ----
@@ -848,12 +865,14 @@ __device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int 
     // I16 luma DC: Hadamard + quant (lanes 0..15 = raster positions)
     int dc_crude = 0, dc_nz = 0;
     if (intra16) {
-        lds_hadamard4x4(S.dcy);
+        // gather the 16 DC coefficients (block b's lane 4b, row 0) into raster lanes 0..15
+        const int dc_raw = __shfl(wl[0], 4 * blk_from_xy(l & 3, (l >> 2) & 3));
+        const int dc_h = lane_hadamard16(dc_raw);
         if (l < 16) {
             int qbits = 15 + qp / 6;
             int f = quant_f(qbits, true);
             int mf0 = H264_QUANT_MF[qp % 6][0];
-            int lv = quant_coef(i16_dc_fwd_round(S.dcy[l]), mf0, 2 * f, qbits + 1);
+            int lv = quant_coef(i16_dc_fwd_round(dc_h), mf0, 2 * f, qbits + 1);
             S.coef[kCoefLumaDC + inv_zigzag4x4(l)] = (int16_t)lv;
             if (lv) { dc_nz = 1; dc_crude = level_bits_bound(sk_abs(lv), 6) + 3; }
         }
@@ -991,16 +1010,13 @@ __device__ __forceinline__ void recon_mb_lanes(int qp, bool intra16, int cbp, Mb
     int cbp_l = cbp & 15, cbp_c = (cbp >> 4) & 3;
     int qpc = chroma_qp(qp);
     // DC dequant: luma (I16) via the LDS Hadamard, lanes 16..17 chroma components
+    int dcy = 0;   // dequantised luma DC of raster block l (lanes 0..15), I16 only
     if (intra16) {
-        if (l < 16) S.blk_stat[l] = S.coef[kCoefLumaDC + inv_zigzag4x4(l)];
-        wave_sync();
-        lds_hadamard4x4(S.blk_stat);
-        if (l < 16) {
-            int ls = 16 * H264_DEQUANT_V[qp % 6][0];
-            int q6 = qp / 6;
-            int acc = S.blk_stat[l];
-            S.blk_stat[l] = qp >= 36 ? (acc * ls) << (q6 - 6) : (acc * ls + (1 << (5 - q6))) >> (6 - q6);
-        }
+        const int c = l < 16 ? S.coef[kCoefLumaDC + inv_zigzag4x4(l)] : 0;
+        const int acc = lane_hadamard16(c);
+        const int ls = 16 * H264_DEQUANT_V[qp % 6][0];
+        const int q6 = qp / 6;
+        dcy = qp >= 36 ? (acc * ls) << (q6 - 6) : (acc * ls + (1 << (5 - q6))) >> (6 - q6);
     }
     if (l >= 16 && l < 18) {
         int c = l - 16;
@@ -1020,7 +1036,8 @@ __device__ __forceinline__ void recon_mb_lanes(int qp, bool intra16, int cbp, Mb
             int lv = S.coef[kCoefLuma + b * 16 + inv_zigzag4x4(pos)];
             d[j] = coded ? dequant_coef(lv, qp, pos) : 0;
         }
-        if (intra16 && r == 0) d[0] = S.blk_stat[blk_y(b) * 4 + blk_x(b)];
+        const int dc_b = __shfl(dcy, blk_y(b) * 4 + blk_x(b));   // block b's DC from its raster lane
+        if (intra16 && r == 0) d[0] = dc_b;
         int res[4];
         inv4_quad(d, r, res);
 #pragma unroll
