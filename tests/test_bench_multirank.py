@@ -47,3 +47,15 @@ def test_two_rank_cpu_dist_bands():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["bands"] == [[0, 128], [128, 256]]
     assert d["kib_per_frame"] > 0
+
+
+def test_two_rank_cpu_bench_default_capture_path():
+    """The driver's N>1 command shape (default --path capture, no --gather) on gloo."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"),
+           "--backend", "cpu", "--gpus", "2", "--steps", "2", "--warmup", "1", "--sessions", "2",
+           "--width", "256", "--height", "128", "--pool", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["config"]["path"] == "capture"
