@@ -800,8 +800,8 @@ __device__ __forceinline__ int quad_sum(int v) {
 // lane-parallel conservative bound and only runs the exact (nC-free) CAVLC bound
 // of mb_bits_bound when that one exceeds the budget: same decisions as the CPU.
 __device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int qp, bool intra16, MbScratch& S,
-                              int* bound_out, const CavlcTables& T, unsigned long long* dbg = nullptr,
-                              int step = 0) {
+                              int* bound_out, const CavlcTables& T, int* sl, int* sc,
+                              unsigned long long* dbg = nullptr, int step = 0) {
     const int l = lane_id();
     const int b = l >> 2, r = l & 3;
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
@@ -821,6 +821,7 @@ __device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int 
             int pos = r * 4 + j;
             int lv = quant_coef(wl[j], sel3(pos_class(pos), m0, m1, m2), f, qbits);
             if (intra16 && pos == 0) lv = 0;
+            sl[j] = lv;   // kept in registers for the reconstruction
             S.coef[kCoefLuma + b * 16 + ((izz_row >> (8 * j)) & 255)] = (int16_t)lv;
             lvl[j] = sk_abs(lv);
             ln_l += lv != 0;
@@ -840,6 +841,7 @@ __device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int 
         for (int j = 0; j < 4; j++) {
             int pos = r * 4 + j;
             int lv = pos == 0 ? 0 : quant_coef(wc[j], sel3(pos_class(pos), m0, m1, m2), f, qbits);
+            sc[j] = lv;
             if (l < 32) S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + ((izz_row >> (8 * j)) & 255)] = (int16_t)lv;
             lvc[j] = sk_abs(lv);
             ln_c += lv != 0;
@@ -937,12 +939,16 @@ __device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int 
         }
         bn_l = 0;
         bc_l = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) sl[j] = 0;
     }
     if (l < 32 && zero_comp[comp]) {
         if (r == 0)
             for (int k = 0; k < 16; k++) S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + k] = 0;
         bn_c = 0;
         bc_c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) sc[j] = 0;
     }
     // TotalCoeff per block for nC (written by the quad leader)
     if (r == 0) S.nnz[b] = luma_coded ? (uint8_t)bn_l : 0;
@@ -1003,7 +1009,7 @@ __device__ __forceinline__ int quant_mb_lanes(const int* wl, const int* wc, int 
 
 // Reconstruct this lane's luma row (4 px) and chroma row (lanes < 32).
 __device__ __forceinline__ void recon_mb_lanes(int qp, bool intra16, int cbp, MbScratch& S, const int* pred_l,
-                               const int* pred_c, int* rec_l, int* rec_c) {
+                               const int* pred_c, int* rec_l, int* rec_c, const int* sl, const int* sc) {
     const int l = lane_id();
     const int b = l >> 2, r = l & 3;
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
@@ -1033,8 +1039,7 @@ __device__ __forceinline__ void recon_mb_lanes(int qp, bool intra16, int cbp, Mb
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             int pos = r * 4 + j;
-            int lv = S.coef[kCoefLuma + b * 16 + inv_zigzag4x4(pos)];
-            d[j] = coded ? dequant_coef(lv, qp, pos) : 0;
+            d[j] = coded ? dequant_coef(sl[j], qp, pos) : 0;   // this lane's levels (registers)
         }
         const int dc_b = __shfl(dcy, blk_y(b) * 4 + blk_x(b));   // block b's DC from its raster lane
         if (intra16 && r == 0) d[0] = dc_b;
@@ -1049,8 +1054,7 @@ __device__ __forceinline__ void recon_mb_lanes(int qp, bool intra16, int cbp, Mb
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             int pos = r * 4 + j;
-            int lv = S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + inv_zigzag4x4(pos)];
-            d[j] = (cbp_c == 2 && pos != 0) ? dequant_coef(lv, qpc, pos) : 0;
+            d[j] = (cbp_c == 2 && pos != 0) ? dequant_coef(sc[j], qpc, pos) : 0;
         }
         if (r == 0) d[0] = S.blk_stat[16 + comp * 4 + cb];
         int res[4];
@@ -1078,11 +1082,12 @@ __device__ __forceinline__ int code_mb(const int* src_l, const int* pred_l, cons
     int qp = start_qp >= 0 ? start_qp : slice_qp;
     int cap = sk_min(51, slice_qp + 24);
     int cbp = 0;
+    int sl[4], sc[4];   // final levels of this lane's luma / chroma row
     STAMP_S(dbg, step, 3);
     qp = __builtin_amdgcn_readfirstlane(qp);   // wave-uniform: table lookups become scalar loads
     for (;;) {
         int bound;
-        cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound, T, dbg, step);
+        cbp = quant_mb_lanes(wl, wc, qp, intra16, S, &bound, T, sl, sc, dbg, step);
         if (dbg && blockIdx.x == SK_STAMP_BLOCK && threadIdx.x == 0 && (unsigned)(step - SK_STAMP_STEP0) < 64u) {
             unsigned long long& d = dbg[(step - SK_STAMP_STEP0) * 16 + 15];
             d = (d & 0xffff) + 1 + ((unsigned long long)bound << 32);
@@ -1095,7 +1100,7 @@ __device__ __forceinline__ int code_mb(const int* src_l, const int* pred_l, cons
     mb.cbp = (uint8_t)cbp;
     mb.qp = (uint8_t)qp;
     if (quant_only) return qp;
-    recon_mb_lanes(qp, intra16, cbp, S, pred_l, pred_c, rec_l, rec_c);
+    recon_mb_lanes(qp, intra16, cbp, S, pred_l, pred_c, rec_l, rec_c, sl, sc);
     STAMP_S(dbg, step, 5);
     // copy levels to global (816 B = 204 words)
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(S.coef);
@@ -1168,6 +1173,7 @@ __device__ __forceinline__ int code_mb_i4(Smp sample, const int* src_l, const in
     fwd4_quad(xc, r, wc);
     int qp = __builtin_amdgcn_readfirstlane(start_qp);
     const int cap = sk_min(51, slice_qp + 24);
+    int scl[4];   // this lane's chroma AC levels (final iteration)
     for (;;) {
         const int qbits = 15 + qp / 6, f = quant_f(qbits, true);
         const int* mf = H264_QUANT_MF[qp % 6];
@@ -1225,6 +1231,7 @@ __device__ __forceinline__ int code_mb_i4(Smp sample, const int* src_l, const in
         for (int j = 0; j < 4; j++) {
             const int pos = r * 4 + j;
             const int lvc = pos == 0 ? 0 : quant_coef(wc[j], sel3(pos_class(pos), mfc[0], mfc[1], mfc[2]), fc, qbc);
+            scl[j] = lvc;
             nc += lvc != 0;
             if (l < 32) S.coef[kCoefChromaAC + (comp * 4 + cb) * 16 + inv_zigzag4x4(pos)] = (int16_t)lvc;
         }
@@ -1258,7 +1265,7 @@ __device__ __forceinline__ int code_mb_i4(Smp sample, const int* src_l, const in
         wave_sync();
     }
     int zero[4] = {0, 0, 0, 0}, dummy[4];
-    recon_mb_lanes(qp, false, mb.cbp & 0x30, S, zero, pred_c, dummy, rec_c);   // chroma only (luma cbp masked)
+    recon_mb_lanes(qp, false, mb.cbp & 0x30, S, zero, pred_c, dummy, rec_c, zero, scl);   // chroma only
     {
         const int y = blk_y(q) * 4 + r, x0 = blk_x(q) * 4;
 #pragma unroll
