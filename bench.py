@@ -69,11 +69,11 @@ def parse():
                    help="ONE session of --width x --height split into one band of stripes per rank "
                         "(parallel/dist_banded.py): rank 0 scatters the bands over RCCL, every rank encodes its "
                         "band on its GPU, packets are gathered to rank 0 each step; strong scaling")
-    p.add_argument("--e2e-sessions", type=int, default=8,
-                   help="after the timed window (single process, HIP, H.264 only): serve this many 1080p60 "
-                        "sessions as real server processes to headless websocket clients for --e2e-seconds and "
-                        "report measured capture->client latency and whether every session sustained 60 fps "
-                        "(tools/bench_e2e.py); 0 = skip")
+    p.add_argument("--e2e-sessions", default="12,8",
+                   help="before the timed window (single process, HIP, H.264 only): serve N 1080p60 sessions as "
+                        "real server processes to headless websocket clients for --e2e-seconds and report the "
+                        "measured capture->client latency; a comma list is tried in order and the first N at "
+                        "which every session sustains 60 fps is reported (tools/bench_e2e.py); 0 = skip")
     p.add_argument("--e2e-seconds", type=float, default=4.0)
     p.add_argument("--path", default="capture", choices=["capture", "encoder"],
                    help="capture: the production capture sessions (csrc/runtime/capture.cpp: native loop, "
@@ -140,12 +140,23 @@ def run_e2e(args, W, H):
                                    warmup=6.0, hw_queues=None, client_procs=4,
                                    log_dir=os.path.join("gpurun_out", "bench_e2e_logs"))
         os.makedirs(ns.log_dir, exist_ok=True)
-        r = asyncio.run(asyncio.wait_for(bench_e2e.run_n(args.e2e_sessions, ns), 120))
+        tried = []
+        r = None
+        for n in e2e_counts(args):
+            r = asyncio.run(asyncio.wait_for(bench_e2e.run_n(n, ns), 120))
+            tried.append({"sessions": n, "sustained": bool(r.get("sustained")), "fps_min": r.get("fps_min")})
+            if r.get("sustained"):
+                break
+        r["tried"] = tried
         r["method"] = ("measured: server processes + headless websocket clients (reference protocol), "
                        "every session >= 97% of 60 fps; latency = frame grab -> first stripe received")
         return r
     except Exception as ex:   # noqa: BLE001 - reported in the JSON line
-        return {"sessions": args.e2e_sessions, "error": f"{type(ex).__name__}: {ex}"}
+        return {"sessions": e2e_counts(args), "error": f"{type(ex).__name__}: {ex}"}
+
+
+def e2e_counts(args):
+    return [int(x) for x in str(args.e2e_sessions).split(",") if x.strip() and int(x) > 0]
 
 
 def run_dist_bands(args, torch, dist, rank, world, local_rank):
@@ -260,7 +271,7 @@ def main():
     # share the card with nothing else (a live HIP context here, with its hardware queues,
     # cost the sessions ~3 fps and a 59 ms p99 in measurements: profiles/r2_e2e_sessions.md).
     e2e = None
-    if (rank == 0 and world == 1 and args.e2e_sessions > 0 and args.backend == "hip" and args.encoder == "h264"
+    if (rank == 0 and world == 1 and e2e_counts(args) and args.backend == "hip" and args.encoder == "h264"
             and not args.gather):
         e2e = run_e2e(args, args.width, args.height)
     # host threads and pinned frames on the GPU's NUMA node (first touch), before any allocation
