@@ -26,6 +26,8 @@ class Client {
     this.video = new VideoRenderer(this.canvas, (e) => this.onDecoderError(e));
     this.audio = new AudioPipeline();
     this.input = new Input(this.canvas, (m) => this.sendText(m), () => [this.canvas.width, this.canvas.height]);
+    this.input.onMenuHotkey = () => $('sidebar').classList.toggle('open');          // Ctrl+Shift+M
+    this.input.onFullscreenHotkey = () => document.documentElement.requestFullscreen();   // Ctrl+Shift+F
     this.ws = null;
     this.killed = false;
     this.serverSettings = {};

@@ -270,3 +270,95 @@ class FakePC {
   assert.equal(parseServerMessage('nope'), null);
   assert.deepEqual(parseServerMessage('{"type":"system","data":{"action":"reload"}}').action, ['reload', '']);
 })().then(() => console.log('webrtc client ok'), (e) => { console.error(e); process.exit(1); });
+
+// ---- input library state machines (lib/input.js)
+import('../../selkies_gstreamer_amd/web/lib/input.js').then(({ KeyboardTracker, WheelAccumulator, TrackpadGestures, KS }) => {
+  const DOWN = 8, UP = 16, RIGHT = 128;   // protocol.js MASK_WHEEL_*
+  const sent = [];
+  let menu = 0, full = 0;
+  const kb = new KeyboardTracker((m) => sent.push(m), {
+    onMenuHotkey: () => { menu++; }, onFullscreenHotkey: () => { full++; },
+  });
+  const ev = (code, key, extra = {}) => Object.assign({ code, key, timeStamp: 0 }, extra);
+  // plain key + autorepeat + release
+  assert.ok(kb.keydown(ev('KeyA', 'a')));
+  assert.ok(kb.keydown(ev('KeyA', 'a', { repeat: true })));
+  assert.ok(kb.keyup(ev('KeyA', 'a')));
+  assert.deepEqual(sent.splice(0), ['kd,97', 'kd,97', 'ku,97']);
+  // AltGr on Windows: ControlLeft + AltRight with one timestamp -> ISO_Level3_Shift, no Ctrl
+  kb.keydown(ev('ControlLeft', 'Control', { timeStamp: 100 }));
+  kb.keydown(ev('AltRight', 'AltGraph', { timeStamp: 100 }));
+  kb.keydown(ev('KeyE', '€', { timeStamp: 101 }));
+  kb.keyup(ev('KeyE', '€'));
+  kb.keyup(ev('AltRight', 'AltGraph'));
+  assert.deepEqual(sent.splice(0), [`kd,${KS.AltGr}`, 'kd,16785580', 'ku,16785580', `ku,${KS.AltGr}`]);
+  // a real Ctrl is held back until the next key and then sent first
+  kb.keydown(ev('ControlLeft', 'Control', { timeStamp: 200 }));
+  kb.keydown(ev('KeyC', 'c', { timeStamp: 260, ctrlKey: true }));
+  kb.keyup(ev('KeyC', 'c'));
+  kb.keyup(ev('ControlLeft', 'Control'));
+  assert.deepEqual(sent.splice(0), [`kd,${KS.CtrlL}`, 'kd,99', 'ku,99', `ku,${KS.CtrlL}`]);
+  // a lone Ctrl tap still reaches the server
+  kb.keydown(ev('ControlLeft', 'Control', { timeStamp: 300 }));
+  kb.keyup(ev('ControlLeft', 'Control'));
+  assert.deepEqual(sent.splice(0), [`kd,${KS.CtrlL}`, `ku,${KS.CtrlL}`]);
+  // hotkeys are consumed locally
+  assert.ok(kb.keydown(ev('KeyM', 'M', { ctrlKey: true, shiftKey: true })));
+  assert.ok(kb.keydown(ev('KeyF', 'F', { ctrlKey: true, shiftKey: true })));
+  assert.deepEqual([menu, full, sent.length], [1, 1, 0]);
+  // composition keydowns are ignored; unidentified keys pulse
+  assert.equal(kb.keydown(ev('KeyA', 'Process', { keyCode: 229 })), false);
+  kb.keydown(ev('Unidentified', 'x'));
+  assert.deepEqual(sent.splice(0), ['kd,120', 'ku,120']);
+  // macOS: Cmd maps to Ctrl, releasing Cmd releases keys pressed under it
+  const mac = new KeyboardTracker((m) => sent.push(m), { macCmdSwap: true });
+  mac.keydown(ev('MetaLeft', 'Meta'));
+  mac.keydown(ev('KeyV', 'v', { metaKey: true }));
+  mac.keyup(ev('MetaLeft', 'Meta'));
+  assert.deepEqual(sent.splice(0), [`kd,${KS.CtrlL}`, 'kd,118', `ku,${KS.CtrlL}`, 'ku,118']);
+  // blur: everything released, then the server-side reset
+  kb.keydown(ev('ShiftLeft', 'Shift'));
+  kb.keydown(ev('KeyQ', 'Q', { shiftKey: true }));
+  kb.reset();
+  assert.deepEqual(sent.splice(0), ['kd,65505', 'kd,81', 'ku,65505', 'ku,81', 'kr']);
+  // typed text / mobile virtual keyboard
+  kb.typeText('Hi');
+  assert.deepEqual(sent.splice(0), ['kd,65505', 'kd,72', 'ku,72', 'ku,65505', 'kd,105', 'ku,105']);
+  kb.mobileInput({ inputType: 'deleteContentBackward' });
+  kb.mobileInput({ inputType: 'insertText', data: 'é' });
+  assert.deepEqual(sent.splice(0), ['kd,65288', 'ku,65288', 'kd,233', 'ku,233']);
+
+  // wheel: line-mode notches and accumulated fine trackpad deltas
+  const w = new WheelAccumulator();
+  assert.deepEqual(w.feed({ deltaY: 3, deltaMode: 1 }), [{ bit: DOWN, magnitude: 1 }]);   // 120 px -> 1 notch, 20 left
+  assert.deepEqual(w.feed({ deltaY: 30, deltaMode: 0 }), []);
+  assert.deepEqual(w.feed({ deltaY: 60, deltaMode: 0 }), [{ bit: DOWN, magnitude: 1 }]);
+  assert.deepEqual(w.feed({ deltaY: -250, deltaMode: 0 }), [{ bit: UP, magnitude: 2 }]);  // direction change resets
+  assert.deepEqual(w.feed({ deltaX: 100, deltaMode: 0 }).map((p) => p.bit), [RIGHT]);
+
+  // trackpad gestures
+  const g = new TrackpadGestures();
+  const T = (id, x, y) => ({ identifier: id, clientX: x, clientY: y });
+  assert.deepEqual(g.handle('touchstart', [T(1, 10, 10)], 0), []);
+  assert.deepEqual(g.handle('touchend', [T(1, 10, 10)], 100), [{ button: 1, down: true }, { button: 1, down: false }]);
+  // touch again right after a tap: drag with the button held
+  assert.deepEqual(g.handle('touchstart', [T(2, 10, 10)], 200), [{ button: 1, down: true }]);
+  assert.deepEqual(g.handle('touchmove', [T(2, 40, 10)], 250), [{ move: [45, 0] }]);
+  assert.deepEqual(g.handle('touchend', [T(2, 40, 10)], 600), [{ button: 1, down: false }]);
+  // one-finger move below the tap slop does nothing; beyond it moves relatively
+  g.handle('touchstart', [T(3, 0, 0)], 2000);
+  assert.deepEqual(g.handle('touchmove', [T(3, 4, 0)], 2010), []);
+  assert.deepEqual(g.handle('touchmove', [T(3, 20, 0)], 2020), [{ move: [24, 0] }]);
+  assert.deepEqual(g.handle('touchend', [T(3, 20, 0)], 2030), []);
+  // two-finger tap = right click, two-finger drag = scroll, three-finger tap = middle click
+  g.handle('touchstart', [T(4, 0, 100), T(5, 50, 100)], 3000);
+  assert.deepEqual(g.handle('touchend', [T(4, 0, 100), T(5, 50, 100)], 3050), [{ button: 4, down: true }, { button: 4, down: false }]);
+  g.handle('touchstart', [T(6, 0, 100), T(7, 50, 100)], 4000);
+  const sc = g.handle('touchmove', [T(6, 0, 40), T(7, 50, 40)], 4050);
+  assert.equal(sc.length, 2);
+  assert.deepEqual(sc[0], { wheel: DOWN, magnitude: 1 });   // fingers up: content scrolls down
+  g.handle('touchend', [T(6, 0, 40), T(7, 50, 40)], 4100);
+  g.handle('touchstart', [T(8, 0, 0), T(9, 20, 0), T(10, 40, 0)], 5000);
+  assert.deepEqual(g.handle('touchend', [T(8, 0, 0), T(9, 20, 0), T(10, 40, 0)], 5050), [{ button: 2, down: true }, { button: 2, down: false }]);
+  console.log('input lib ok');
+}).catch((e) => { console.error(e); process.exit(1); });
