@@ -156,6 +156,28 @@ void sk_x11_screen_size(void* h, int* w, int* hh);
 int sk_x11_cursor_wait(void* h, int timeout_ms);
 int sk_x11_cursor_image(void* h, uint64_t* serial, int* w, int* hh, int* xhot, int* yhot, uint32_t* argb, int cap);
 
+// ---- Audio capture (pcmflux engine, audio_capture.cpp) ----
+enum { SK_AUDIO_OPUS = 0, SK_AUDIO_PCM = 1 };
+typedef struct sk_audio_settings {
+    const char* device_name;        // PulseAudio source; "synthetic[:hz]" = paced sine tone
+    int32_t sample_rate, channels, opus_bitrate, frame_duration_ms;
+    int32_t use_vbr, use_silence_gate;
+    int32_t codec;                  // SK_AUDIO_OPUS (libopus) or SK_AUDIO_PCM (raw s16le)
+    int32_t synthetic_silence_frames;  // synthetic source: leading all-zero frames
+} sk_audio_settings;
+typedef struct sk_audio_chunk { int32_t size; const uint8_t* data; } sk_audio_chunk;
+typedef void (*sk_audio_cb)(sk_audio_chunk*, void*);
+// bit 0: libpulse-simple loadable, bit 1: libopus loadable
+int sk_audio_available(void);
+void* sk_audio_create(void);
+void sk_audio_destroy(void* a);
+// 0 = capture thread running; < 0 = error (sk_audio_error)
+int sk_audio_start(void* a, const sk_audio_settings* s, sk_audio_cb cb, void* user);
+void sk_audio_stop(void* a);
+// frames read, packets delivered, bytes delivered, frames dropped by the silence gate
+void sk_audio_stats(void* a, double* out, int n);
+const char* sk_audio_error(void* a);
+
 // Page-locked host memory (capture buffers / frame pools): DMA-able by HIP.
 void* sk_host_alloc(int64_t bytes);
 void sk_host_free(void* p);

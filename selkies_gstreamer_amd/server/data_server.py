@@ -309,7 +309,7 @@ class DataStreamingServer:
         ip = request.remote or "?"
         now = self.clock()
         last = self.recent.get(ip)
-        ws = web.WebSocketResponse(max_msg_size=64 * 1024 * 1024, heartbeat=None)
+        ws = web.WebSocketResponse(max_msg_size=64 * 1024 * 1024, heartbeat=None, compress=False)
         await ws.prepare(request)
         if last is not None and (now - last) < RECONNECT_DEBOUNCE_S:
             log.warning("client %s reconnecting too quickly; rejected", ip)
