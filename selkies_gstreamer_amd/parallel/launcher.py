@@ -34,8 +34,16 @@ class SessionSpec:
     gpu: int
     extra: list = field(default_factory=list)
     hw_queues: Optional[int] = None
+    ports: list = field(default_factory=list)      # > 1 entry: a session host (parallel/multi.py)
+    displays: list = field(default_factory=list)
+
+    def all_ports(self) -> list[int]:
+        return self.ports or [self.port]
 
     def command(self, python: str = sys.executable) -> list[str]:
+        if len(self.ports) > 1:
+            return [python, "-m", "selkies_gstreamer_amd.parallel.multi", "--ports", ",".join(map(str, self.ports)),
+                    "--displays", ",".join(self.displays), "--", "--gpu-id", str(self.gpu), *self.extra]
         return [python, "-m", "selkies_gstreamer_amd", "--port", str(self.port), "--gpu-id", str(self.gpu),
                 *self.extra]
 
@@ -75,6 +83,25 @@ def plan_sessions(n: int, gpus: int, base_port: int, display_base: int, width: i
     return out
 
 
+def group_hosts(specs: list[SessionSpec], per_process: int) -> list[SessionSpec]:
+    """Packs the sessions of each GPU into session hosts of up to `per_process`
+    sessions (one process, one HIP context: parallel/multi.py); hardware queues are
+    then sized for the number of processes per GPU, not sessions."""
+    if per_process <= 1:
+        return specs
+    out: list[SessionSpec] = []
+    for gpu in sorted({s.gpu for s in specs}):
+        mine = [s for s in specs if s.gpu == gpu]
+        for i in range(0, len(mine), per_process):
+            grp = mine[i:i + per_process]
+            out.append(SessionSpec(f"h{gpu}.{i // per_process}", grp[0].display, grp[0].port, gpu, list(grp[0].extra),
+                                   ports=[s.port for s in grp], displays=[s.display for s in grp]))
+    per_gpu = {g: sum(1 for s in out if s.gpu == g) for g in {s.gpu for s in out}}
+    for s in out:
+        s.hw_queues = hw_queues_for(per_gpu[s.gpu])
+    return out
+
+
 class Supervisor:
     def __init__(self, specs: list[SessionSpec], health_interval: float = 5.0, max_backoff: float = 60.0,
                  check_health: bool = True):
@@ -96,9 +123,12 @@ class Supervisor:
         import aiohttp
         try:
             async with aiohttp.ClientSession() as s:
-                async with s.get(f"http://127.0.0.1:{spec.port}/health",
-                                 timeout=aiohttp.ClientTimeout(total=3)) as r:
-                    return r.status == 200
+                for port in spec.all_ports():   # a host is healthy when every session answers
+                    async with s.get(f"http://127.0.0.1:{port}/health",
+                                     timeout=aiohttp.ClientTimeout(total=3)) as r:
+                        if r.status != 200:
+                            return False
+                return True
         except Exception:
             return False
 
@@ -150,6 +180,8 @@ def main(argv=None):
     ap.add_argument("--base-port", type=int, default=8082)
     ap.add_argument("--display-base", type=int, default=20)
     ap.add_argument("--capacity", type=float, default=48.0, help="1080p60 sessions per GPU")
+    ap.add_argument("--sessions-per-process", type=int, default=1,
+                    help="> 1: run that many sessions per process (session hosts sharing one HIP context)")
     ap.add_argument("--dry-run", action="store_true", help="print the plan and exit")
     args, extra = ap.parse_known_args(argv)
     if extra and extra[0] == "--":
@@ -157,6 +189,7 @@ def main(argv=None):
     logging.basicConfig(level=logging.INFO)
     specs = plan_sessions(args.sessions, args.gpus, args.base_port, args.display_base, extra=extra,
                           capacity=args.capacity)
+    specs = group_hosts(specs, args.sessions_per_process)
     if args.dry_run:
         for s in specs:
             print(f"{s.name} DISPLAY={s.display} {' '.join(s.command())}")

@@ -51,32 +51,44 @@ def free_port() -> int:
 
 
 def start_servers(n: int, args) -> list:
-    procs = []
-    for i in range(n):
-        port = free_port()
+    """N sessions as processes of --sessions-per-proc sessions each (1 = one server
+    process per session, the reference shape; K > 1 = parallel/multi.py session hosts
+    sharing one HIP context). Returns one (process, port, log) per session."""
+    out = []
+    k = max(1, int(getattr(args, "sessions_per_proc", 1) or 1))
+    nproc = (n + k - 1) // k
+    for j in range(nproc):
+        ports = [free_port() for _ in range(min(k, n - j * k))]
         env = dict(os.environ, SELKIES_FRAME_TRACE="1", PYTHONUNBUFFERED="1")
-        q = args.hw_queues if args.hw_queues is not None else hw_queues_for(n)
+        q = args.hw_queues if args.hw_queues is not None else hw_queues_for(nproc)
         if q:
-            env["GPU_MAX_HW_QUEUES"] = str(q)  # what parallel/launcher.py gives co-located sessions
-        cmd = [sys.executable, "-m", "selkies_gstreamer_amd", "--port", str(port), "--host", "127.0.0.1",
-               "--capture-source", args.source, "--audio-enabled", "false", "--gpu-id", str(args.gpu),
-               "--gamepad-enabled", "false"]
+            env["GPU_MAX_HW_QUEUES"] = str(q)  # what parallel/launcher.py gives co-located processes
+        shared = ["--host", "127.0.0.1", "--capture-source", args.source, "--audio-enabled", "false",
+                  "--gpu-id", str(args.gpu), "--gamepad-enabled", "false"]
         if args.use_cpu:
-            cmd += ["--use-cpu", "true"]
-        log = open(os.path.join(args.log_dir, f"server_{n}_{i}.log"), "w")
+            shared += ["--use-cpu", "true"]
+        if k == 1:
+            cmd = [sys.executable, "-m", "selkies_gstreamer_amd", "--port", str(ports[0]), *shared]
+        else:
+            cmd = [sys.executable, "-m", "selkies_gstreamer_amd.parallel.multi", "--ports",
+                   ",".join(map(str, ports)), "--", *shared]
+        log = open(os.path.join(args.log_dir, f"server_{n}_{j}.log"), "w")
         p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
-        procs.append((p, port, log))
-    return procs
+        out.extend((p, port, log) for port in ports)
+    return out
 
 
 def stop_servers(procs):
+    seen = {}
     for p, _, log in procs:
+        seen[p.pid] = (p, log)
+    for p, log in seen.values():
         if p.poll() is None:
             try:
                 os.killpg(p.pid, signal.SIGTERM)
             except ProcessLookupError:
                 pass
-    for p, _, log in procs:
+    for p, log in seen.values():
         try:
             p.wait(timeout=10)
         except subprocess.TimeoutExpired:
@@ -210,6 +222,8 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES per server (default: the launcher's choice for N sessions)")
     ap.add_argument("--client-procs", type=int, default=4, help="client processes the sessions are sharded over")
+    ap.add_argument("--sessions-per-proc", type=int, default=1,
+                    help="sessions per server process (> 1: parallel/multi.py session hosts)")
     ap.add_argument("--sustain", type=float, default=0.97, help="fraction of --fps every session must receive")
     ap.add_argument("--log-dir", default=os.path.join(ROOT, "gpurun_out", "e2e_logs"))
     args = ap.parse_args()
