@@ -137,6 +137,8 @@ def build_specs() -> list[Spec]:
         _b("ui_show_logo", True, "Show the logo in the sidebar."),
         _b("ui_show_core_buttons", True, "Show core component buttons."),
         _b("ui_show_sidebar", True, "Show the main sidebar UI."),
+        Spec("ui_dashboard", "enum", "selkies", "Dashboard layout (selkies: left sidebar, zinc: right side menu, "
+             "wish: top menu bar; the three reference dashboards).", allowed=["selkies", "zinc", "wish"]),
     ]
     specs += [_b(f"ui_sidebar_show_{f}", True, f"Show the {f.replace('_', ' ')} section in the sidebar.")
               for f in UI_FLAGS]

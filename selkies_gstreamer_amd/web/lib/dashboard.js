@@ -101,6 +101,75 @@ export function sparkPoints(ring, w, h) {
   return ring.v.map((x, i) => [n > 1 ? (i * (w - 1)) / (ring.n - 1) : 0, h - 1 - (x / top) * (h - 2)]);
 }
 
+// Dashboard layouts: the reference ships three dashboards over one client core
+// (addons/selkies-dashboard: left sidebar; addons/selkies-dashboard-zinc: right
+// side menu of collapsible panels; addons/selkies-dashboard-wish: top menu bar).
+// Here they are three layouts of the same panels, picked by `?ui=<name>` or the
+// `ui_dashboard` server setting; index.html styles `body.ui-<name>`.
+export const LAYOUTS = {
+  selkies: { side: 'left', collapsible: false, menu: 'sidebar' },
+  zinc: { side: 'right', collapsible: true, menu: 'side-menu' },
+  wish: { side: 'top', collapsible: true, menu: 'top-menu' },
+};
+
+export function pickLayout(search, st) {
+  const m = /[?&]ui=([a-z]+)/.exec(search || '');
+  if (m && m[1] in LAYOUTS) return m[1];
+  const d = st && st.ui_dashboard;
+  const v = d == null ? null : (typeof d === 'object' && 'value' in d ? d.value : d);
+  return v in LAYOUTS ? v : 'selkies';
+}
+
+// Gamepad visualiser (reference GamepadVisualizer.jsx): standard-mapping pad as
+// a list of shapes: buttons (filled when pressed, opacity = analog value) and the
+// two sticks with their deflection. Rendered to SVG by padSvg().
+const PAD_BUTTONS = [   // standard mapping index -> [x, y, r]
+  [170, 62, 9], [186, 46, 9], [154, 46, 9], [170, 30, 9],      // A B X Y
+  [40, 8, 7], [160, 8, 7], [40, 0, 6], [160, 0, 6],            // LB RB LT RT
+  [84, 46, 5], [116, 46, 5], [72, 84, 10], [128, 84, 10],      // back start L3 R3
+  [30, 30, 6], [30, 62, 6], [14, 46, 6], [46, 46, 6], [100, 30, 6],   // d-pad up/down/left/right, guide
+];
+
+export function padShapes(pad) {
+  const shapes = [];
+  const btn = (i) => (pad.buttons && pad.buttons[i]) || { pressed: false, value: 0 };
+  PAD_BUTTONS.forEach(([x, y, r], i) => {
+    const b = btn(i);
+    const v = typeof b === 'number' ? b : (b.value || (b.pressed ? 1 : 0));
+    shapes.push({ kind: 'button', index: i, x, y, r, on: v > 0.1 || !!b.pressed, value: Math.min(1, Math.max(0, v)) });
+  });
+  const ax = pad.axes || [];
+  [[72, 84, 0, 1], [128, 84, 2, 3]].forEach(([cx, cy, ix, iy], k) => {
+    const dx = Math.max(-1, Math.min(1, ax[ix] || 0)), dy = Math.max(-1, Math.min(1, ax[iy] || 0));
+    shapes.push({ kind: 'stick', index: k, x: cx + dx * 8, y: cy + dy * 8, r: 6 });
+  });
+  return shapes;
+}
+
+export function padSvg(pad) {
+  const body = padShapes(pad).map((s) => (s.kind === 'button'
+    ? `<circle cx="${s.x}" cy="${s.y}" r="${s.r}" fill="${s.on ? '#7cf' : 'none'}" fill-opacity="${s.on ? Math.max(0.3, s.value) : 0}" stroke="#9ab"/>`
+    : `<circle cx="${s.x.toFixed(1)}" cy="${s.y.toFixed(1)}" r="${s.r}" fill="#fc6"/>`)).join('');
+  return `<svg xmlns="http://www.w3.org/2000/svg" viewBox="0 -8 200 110" width="200" height="110">${body}</svg>`;
+}
+
+// System monitor gauges from the server's system_stats / gpu_stats / network_stats
+// messages (server/stats.py; reference system-monitoring.tsx): fractions 0..1.
+export function monitorGauges(stats) {
+  const frac = (x) => (x == null || Number.isNaN(+x) ? null : Math.max(0, Math.min(1, +x)));
+  return [
+    { key: 'cpu', label: 'CPU', value: stats.cpu == null ? null : frac(stats.cpu / 100) },
+    { key: 'mem', label: 'memory', value: frac(stats.mem) },
+    { key: 'gpu', label: 'GPU', value: frac(stats.gpu) },
+    { key: 'vram', label: 'VRAM', value: frac(stats.vram) },
+  ];
+}
+
+// Keyboard shortcuts panel (reference shortcuts-menu.tsx): label -> soft key combo.
+export const SHORTCUTS = [
+  ['Menu', 'Ctrl+Shift+M'], ['Fullscreen', 'Ctrl+Shift+F'], ['Pointer lock', 'Ctrl+Shift+click'],
+];
+
 export const DPI_CHOICES = [96, 120, 144, 168, 192, 216, 240, 264, 288];
 export const AUDIO_BITRATES = [64000, 128000, 265000, 320000];
 
@@ -128,9 +197,32 @@ export class Dashboard {
     return this.el('div', { 'data-section': name }, [this.el('h3', { text: title }), ...children]);
   }
 
+  setLayout(name) {
+    const body = this.doc.body;
+    for (const n of Object.keys(LAYOUTS)) body.classList.remove(`ui-${n}`);
+    body.classList.add(`ui-${name}`);
+    this.layout = name;
+  }
+
+  // zinc / wish: a click on a panel heading folds the panel
+  _collapsible(sb) {
+    for (const h of sb.querySelectorAll('h3')) {
+      h.onclick = () => {
+        if (!LAYOUTS[this.layout || 'selkies'].collapsible) return;
+        const folded = h.classList.toggle('folded');
+        for (let n = h.nextElementSibling; n && n.tagName !== 'H3' && !(n.dataset && n.dataset.section); n = n.nextElementSibling) {
+          n.classList.toggle('fold-hidden', folded);
+        }
+        const sec = h.parentElement && h.parentElement.dataset && h.parentElement.dataset.section ? h.parentElement : null;
+        if (sec) for (const n of sec.children) if (n !== h) n.classList.toggle('fold-hidden', folded);
+      };
+    }
+  }
+
   build() {
     const sb = this.doc.getElementById('sidebar');
     const s = this.c.settings;
+    this.setLayout(pickLayout(typeof location !== 'undefined' ? location.search : '', this.c.serverSettings));
     // screen
     const mw = this.el('input', { type: 'number', min: '320', max: '7680', step: '2', value: s.manual_width || 1920,
       style: 'width:70px' });
@@ -205,6 +297,21 @@ export class Dashboard {
       return this.el('label', { text: label }, [cv, v]);
     });
     sb.appendChild(this.section('stats', 'Graphs', graphs));
+    // system monitor gauges
+    this.gauges = {};
+    const gaugeRows = monitorGauges({}).map((g) => {
+      const bar = this.el('progress', { max: '100', value: '0', style: 'width:130px' });
+      this.gauges[g.key] = bar;
+      return this.el('label', { text: g.label }, [bar]);
+    });
+    sb.appendChild(this.section('stats', 'System monitor', gaugeRows));
+    // gamepad visualiser
+    this.padViz = this.el('div');
+    sb.appendChild(this.section('gamepads', 'Gamepad', [this.padViz]));
+    // shortcuts
+    sb.appendChild(this.section('softkeys', 'Shortcuts', SHORTCUTS.map(([what, keys]) =>
+      this.el('label', { text: what }, [this.el('kbd', { text: keys })]))));
+    this._collapsible(sb);
     // tag the static sections of index.html
     for (const h of sb.querySelectorAll(':scope > h3')) {
       const name = { Video: 'video', Audio: 'audio', Screen: 'fullscreen', Clipboard: 'clipboard', Files: 'files',
@@ -215,6 +322,7 @@ export class Dashboard {
   }
 
   apply(st) {
+    this.setLayout(pickLayout(typeof location !== 'undefined' ? location.search : '', st));
     const vis = visibleSections(st);
     const sb = this.doc.getElementById('sidebar');
     for (const node of sb.querySelectorAll('[data-section]')) node.style.display = vis.has(node.dataset.section) ? '' : 'none';
@@ -256,8 +364,12 @@ export class Dashboard {
       sparkPoints(r, cv.width, cv.height).forEach(([x, y], i) => (i ? g.lineTo(x, y) : g.moveTo(x, y)));
       g.stroke();
     }
+    for (const g of monitorGauges(st)) {
+      if (this.gauges && this.gauges[g.key]) this.gauges[g.key].value = g.value == null ? 0 : Math.round(g.value * 100);
+    }
     if (navigator.getGamepads) {
       const pads = Array.from(navigator.getGamepads() || []).filter(Boolean);
+      if (this.padViz) this.padViz.innerHTML = pads.length ? padSvg(pads[0]) : '';
       this.padBox.textContent = pads.length ? pads.map((p) => `${p.index}: ${p.id.slice(0, 28)}\n   `
         + `axes ${p.axes.map((a) => a.toFixed(1)).join(' ')}  buttons ${p.buttons.filter((b) => b.pressed).length}`)
         .join('\n') : 'no gamepads';

@@ -362,3 +362,24 @@ import('../../selkies_gstreamer_amd/web/lib/input.js').then(({ KeyboardTracker, 
   assert.deepEqual(g.handle('touchend', [T(8, 0, 0), T(9, 20, 0), T(10, 40, 0)], 5050), [{ button: 2, down: true }, { button: 2, down: false }]);
   console.log('input lib ok');
 }).catch((e) => { console.error(e); process.exit(1); });
+
+// ---- dashboard layouts, gamepad visualiser, system monitor
+assert.equal(dash.pickLayout('', {}), 'selkies');
+assert.equal(dash.pickLayout('?x=1&ui=wish', { ui_dashboard: { value: 'zinc' } }), 'wish');
+assert.equal(dash.pickLayout('', { ui_dashboard: { value: 'zinc' } }), 'zinc');
+assert.equal(dash.pickLayout('?ui=bogus', { ui_dashboard: 'nope' }), 'selkies');
+assert.deepEqual(Object.keys(dash.LAYOUTS), ['selkies', 'zinc', 'wish']);
+{
+  const pad = { buttons: [{ pressed: true, value: 1 }, { pressed: false, value: 0 }], axes: [1, -1, 0, 0.5] };
+  const sh = dash.padShapes(pad);
+  assert.equal(sh.filter((x) => x.kind === 'button').length, 17);
+  assert.equal(sh[0].on, true);
+  assert.equal(sh[1].on, false);
+  const sticks = sh.filter((x) => x.kind === 'stick');
+  assert.deepEqual([sticks[0].x, sticks[0].y, sticks[1].x, sticks[1].y], [80, 76, 128, 88]);
+  const svg = dash.padSvg(pad);
+  assert.ok(svg.startsWith('<svg') && (svg.match(/<circle/g) || []).length === 19);
+  const g = dash.monitorGauges({ cpu: 50, mem: 0.25, gpu: 1.7, vram: null });
+  assert.deepEqual(g.map((x) => x.value), [0.5, 0.25, 1, null]);
+}
+console.log('dashboard layouts ok');

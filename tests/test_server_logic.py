@@ -26,7 +26,7 @@ from selkies_gstreamer_amd.server.settings import Settings, build_specs
 # ----------------------------------------------------------------------------- settings
 def test_settings_count_and_defaults():
     specs = build_specs()
-    assert len(specs) == 59   # the reference's 56 + H.264 quality tools (AQ, quarter-pel, Intra4x4)
+    assert len(specs) == 60   # the reference's 56 + H.264 quality tools (AQ, quarter-pel, Intra4x4) + ui_dashboard
     s = Settings([], env={})
     assert s.h264_aq_strength == 0 and s.h264_subpel == (True, False) and s.h264_intra4x4 == (False, False)
     assert s.encoder == "x264enc" and s.framerate == (8, 120) and s.port == 8082
