@@ -69,12 +69,17 @@ def parse():
                    help="ONE session of --width x --height split into one band of stripes per rank "
                         "(parallel/dist_banded.py): rank 0 scatters the bands over RCCL, every rank encodes its "
                         "band on its GPU, packets are gathered to rank 0 each step; strong scaling")
-    p.add_argument("--e2e-sessions", default="12,8",
-                   help="before the timed window (single process, HIP, H.264 only): serve N 1080p60 sessions as "
-                        "real server processes to headless websocket clients for --e2e-seconds and report the "
+    p.add_argument("--e2e-sessions", default="48,32,16",
+                   help="before the timed window (single process, HIP, H.264 only): serve N 1080p60 sessions from "
+                        "real server processes (session hosts) to headless websocket clients for --e2e-seconds and report the "
                         "measured capture->client latency; a comma list is tried in order and the first N at "
                         "which every session sustains 60 fps is reported (tools/bench_e2e.py); 0 = skip")
     p.add_argument("--e2e-seconds", type=float, default=4.0)
+    p.add_argument("--e2e-sessions-per-proc", type=int, default=8,
+                   help="sessions per server process in the end-to-end check (parallel/multi.py session hosts "
+                        "sharing one HIP context; 1 = one process per session)")
+    p.add_argument("--e2e-encoder", default="x264enc", choices=["x264enc", "x264enc-striped"],
+                   help="encoder the e2e clients request (x264enc = full-frame pictures, the server default)")
     p.add_argument("--path", default="capture", choices=["capture", "encoder"],
                    help="capture: the production capture sessions (csrc/runtime/capture.cpp: native loop, "
                         "grab -> upload -> launch with two frames in flight -> packets -> per-frame callback), "
@@ -135,9 +140,10 @@ def run_e2e(args, W, H):
     try:
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
         import bench_e2e
-        ns = types.SimpleNamespace(width=W, height=H, fps=60, crf=args.qp, encoder="x264enc-striped",
+        ns = types.SimpleNamespace(width=W, height=H, fps=60, crf=args.qp, encoder=args.e2e_encoder,
                                    source="motion", gpu=0, use_cpu=False, sustain=0.97, seconds=args.e2e_seconds,
-                                   warmup=6.0, hw_queues=None, client_procs=4,
+                                   warmup=6.0, hw_queues=None, client_procs=8,
+                                   sessions_per_proc=args.e2e_sessions_per_proc,
                                    log_dir=os.path.join("gpurun_out", "bench_e2e_logs"))
         os.makedirs(ns.log_dir, exist_ok=True)
         tried = []
@@ -148,8 +154,9 @@ def run_e2e(args, W, H):
             if r.get("sustained"):
                 break
         r["tried"] = tried
-        r["method"] = ("measured: server processes + headless websocket clients (reference protocol), "
-                       "every session >= 97% of 60 fps; latency = frame grab -> first stripe received")
+        r["method"] = (f"measured: session-host processes of {args.e2e_sessions_per_proc} servers each + headless "
+                       f"websocket clients (reference protocol, encoder {args.e2e_encoder}), every session >= 97% "
+                       "of 60 fps; latency = frame grab -> first packet received")
         return r
     except Exception as ex:   # noqa: BLE001 - reported in the JSON line
         return {"sessions": e2e_counts(args), "error": f"{type(ex).__name__}: {ex}"}
