@@ -281,6 +281,7 @@ def main():
     if (rank == 0 and world == 1 and e2e_counts(args) and args.backend == "hip" and args.encoder == "h264"
             and not args.gather):
         e2e = run_e2e(args, args.width, args.height)
+        time.sleep(3.0)   # let the 48-session check's processes, clients and GPU contexts finish tearing down
     # host threads and pinned frames on the GPU's NUMA node (first touch), before any allocation
     numa_node = bind_to_gpu(local_rank) if args.backend == "hip" else None
 

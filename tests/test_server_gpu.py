@@ -86,3 +86,52 @@ def test_hip_session_decodes(tmp_path, W, H, encoder):
         finally:
             await srv.stop()
     asyncio.run(asyncio.wait_for(main(), 120))
+
+
+def test_session_host_two_hip_sessions():
+    """parallel/multi.py: two servers in one process share the HIP context; both
+    stream decodable H.264 at their own sizes at the same time."""
+    import socket
+    from selkies_gstreamer_amd.parallel.multi import host
+
+    def free_port():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    async def client(port, W, H):
+        async with aiohttp.ClientSession() as sess:
+            async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket", max_msg_size=0) as ws:
+                await _recv_until(ws, lambda m: isinstance(m, str) and "server_settings" in m)
+                await ws.send_str("SETTINGS," + json.dumps({"initialClientWidth": W, "initialClientHeight": H,
+                                                             "framerate": 60, "encoder": "x264enc"}))
+                dec = StripeDecoder(W, H)
+                frames = 0
+                while frames < 2:
+                    d, _ = await _recv_until(ws, lambda m: isinstance(m, bytes) and m[0] == 0x04 and
+                                             (frames > 0 or m[1] == 1))
+                    dec.feed(d)
+                    frames += 1
+                return dec.Y.std(), int.from_bytes(d[6:8], "big")
+
+    async def main():
+        ports = [free_port(), free_port()]
+        up, stop = [], asyncio.Event()
+        task = asyncio.create_task(host(ports, ["--host", "127.0.0.1", "--capture-source", "motion",
+                                                "--audio-enabled", "false", "--gamepad-enabled", "false"],
+                                        stop=stop, ready=lambda srv, port: up.append(port)))
+        try:
+            for _ in range(600):
+                if len(up) == 2:
+                    break
+                await asyncio.sleep(0.05)
+            assert sorted(up) == sorted(ports)
+            (s0, w0), (s1, w1) = await asyncio.wait_for(asyncio.gather(client(ports[0], 640, 368),
+                                                                        client(ports[1], 1280, 720)), 60)
+            assert (w0, w1) == (640, 1280) and s0 > 5.0 and s1 > 5.0
+        finally:
+            stop.set()
+            await asyncio.wait_for(task, 30)
+    asyncio.run(main())
