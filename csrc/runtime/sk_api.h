@@ -178,6 +178,10 @@ void sk_audio_stop(void* a);
 void sk_audio_stats(void* a, double* out, int n);
 const char* sk_audio_error(void* a);
 
+// ---- AV1 multi-symbol entropy coder (codec/av1_ec.h), test entry ----
+int sk_av1_ec_encode(const int32_t* kind, const int32_t* ctx, const int32_t* sym, int n, uint16_t* cdfs,
+                     const int32_t* nsym, int adapt, uint8_t* out, int cap);
+
 // Page-locked host memory (capture buffers / frame pools): DMA-able by HIP.
 void* sk_host_alloc(int64_t bytes);
 void sk_host_free(void* p);
