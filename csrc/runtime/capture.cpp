@@ -262,6 +262,7 @@ class CaptureSession {
                     cursor_set_ = enc_->set_overlay_image(1, cursor_px_.data(), cw, ch) == 0;
                     cursor_serial_ = serial;
                     if (!cursor_set_) {   // too large for the overlay buffer: draw it on the host
+                        enc_->set_overlay_pos(1, 0, 0, 0, 0, 0);   // and drop the stale GPU cursor
                         src_->set_cursor_overlay(false);
                         cursor_via_enc_ = false;
                     }

@@ -23,7 +23,6 @@ from __future__ import annotations
 import argparse
 import asyncio
 import logging
-import os
 import signal
 import sys
 from typing import Optional, Sequence
@@ -31,15 +30,22 @@ from typing import Optional, Sequence
 log = logging.getLogger("session-host")
 
 
-def session_argvs(ports: Sequence[int], shared: Sequence[str]) -> list[list[str]]:
-    """Per-session server argv: the shared flags with that session's port."""
+def session_argvs(ports: Sequence[int], shared: Sequence[str],
+                  displays: Optional[Sequence[str]] = None) -> list[list[str]]:
+    """Per-session server argv: the shared flags with that session's port and X display.
+
+    The display is an explicit ``--display`` flag of each server, never the
+    process-wide DISPLAY: every session of the host captures, injects input and
+    runs xrandr/DPI tools against its own desktop."""
     out = []
-    for p in ports:
+    for i, p in enumerate(ports):
         argv = [a for a in shared]
-        if "--port" in argv:
-            i = argv.index("--port")
-            del argv[i:i + 2]
-        out.append(["--port", str(p), *argv])
+        for flag in ("--port", "--display"):
+            while flag in argv:
+                j = argv.index(flag)
+                del argv[j:j + 2]
+        extra = ["--display", displays[i]] if displays else []
+        out.append(["--port", str(p), *extra, *argv])
     return out
 
 
@@ -55,11 +61,8 @@ async def host(ports: Sequence[int], shared: Sequence[str], displays: Optional[S
             pass
     stops = [asyncio.Event() for _ in ports]
     tasks = []
-    for i, argv in enumerate(session_argvs(ports, shared)):
-        if displays:
-            os.environ["DISPLAY"] = displays[i]   # read by the capture/input setup of this session
+    for i, argv in enumerate(session_argvs(ports, shared, displays)):
         tasks.append(asyncio.create_task(serve(argv, stops[i], ready)))
-        await asyncio.sleep(0)                    # let the session pick its display up
     waiter = asyncio.create_task(stop.wait())
     done, _ = await asyncio.wait([waiter, *tasks], return_when=asyncio.FIRST_COMPLETED)
     for ev in stops:

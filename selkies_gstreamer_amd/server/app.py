@@ -9,7 +9,8 @@ unknown flags from container scripts are still ignored):
 ``--gpu-id`` first HIP device, ``--num-gpus`` devices to spread displays over,
 ``--web-root`` static client directory, ``--upload-dir`` (default
 ``$FILE_MANAGER_PATH`` or ``~/Desktop``), ``--uinput-mouse-socket``,
-``--js-socket-path`` (gamepad socket directory), ``--metrics-csv``.
+``--js-socket-path`` (gamepad socket directory), ``--metrics-csv``, ``--display``
+(X display of this session; default ``$DISPLAY``).
 """
 from __future__ import annotations
 
@@ -41,6 +42,8 @@ def app_options(argv: Sequence[str]):
     p.add_argument("--uinput-mouse-socket", default=os.environ.get("SELKIES_UINPUT_MOUSE_SOCKET", ""))
     p.add_argument("--js-socket-path", default=os.environ.get("SELKIES_JS_SOCKET_PATH", "/tmp"))
     p.add_argument("--metrics-csv", default=os.environ.get("SELKIES_METRICS_CSV", ""))
+    p.add_argument("--display", default=os.environ.get("DISPLAY", ""),
+                   help="X display this session captures and injects into (default $DISPLAY)")
     opts, _ = p.parse_known_args(list(argv))
     return opts
 
@@ -49,7 +52,7 @@ def make_input_factory(settings: Settings, opts):
     async def factory(server):
         from .gamepad import GamepadHub
         from .input import Clipboard, CursorWatcher, InputHandler, Injector, UinputMouse, X11Injector
-        display = os.environ.get("DISPLAY")
+        display = opts.display or None
         inj: Injector = X11Injector(display) if display else Injector()
         if opts.uinput_mouse_socket:
             inj = UinputMouse(opts.uinput_mouse_socket, inj)
@@ -64,7 +67,7 @@ def make_input_factory(settings: Settings, opts):
             return (l["x"], l["y"]) if l else (0, 0)
 
         handler = InputHandler(
-            inj, gamepads=hub, clipboard=Clipboard(), enable_clipboard=clip_mode,
+            inj, gamepads=hub, clipboard=Clipboard(display), enable_clipboard=clip_mode,
             enable_binary_clipboard=settings.enable_binary_clipboard[0], send_clipboard=server.send_clipboard,
             layout_offset=offset, on_client_fps=lambda fps: (server.set_client_fps(fps),
                                                              server.metrics and server.metrics.set_fps(fps)),
@@ -104,7 +107,8 @@ async def serve(argv: Sequence[str], stop: Optional[asyncio.Event] = None, ready
             pass
     server = DataStreamingServer(settings, upload_dir=opts.upload_dir if "upload" in settings.file_transfers else None,
                                  input_factory=make_input_factory(settings, opts), capture_source=opts.capture_source,
-                                 gpu_id=opts.gpu_id, num_gpus=opts.num_gpus, web_root=opts.web_root, metrics=metrics)
+                                 gpu_id=opts.gpu_id, num_gpus=opts.num_gpus, web_root=opts.web_root, metrics=metrics,
+                                 x_display=opts.display)
     metrics.server = server
     port = await server.start(opts.host, settings.port)
     if ready is not None:
@@ -130,7 +134,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         for s in build_specs():
             print(f"  {s.flag:<40} {s.help}")
         print("\nserver options: --host --capture-source --gpu-id --num-gpus --web-root --upload-dir "
-              "--uinput-mouse-socket --js-socket-path --metrics-csv")
+              "--uinput-mouse-socket --js-socket-path --metrics-csv --display")
         return 0
     asyncio.run(serve(argv))
     return 0

@@ -41,7 +41,7 @@ class MicSink:
         self._warned = False
         self._cv = threading.Condition()
         self._thread = None
-        self._stop = False
+        self._job = None          # the running writer's stop/done/orphan flags
         self.written = 0
         self.dropped = 0
 
@@ -112,42 +112,62 @@ class MicSink:
                     self._warned = True
             self._cv.notify()
         if self._thread is None:
-            self._thread = threading.Thread(target=self._writer, name="mic-writer", daemon=True)
+            self._job = {"stop": False, "done": False, "orphan": False}
+            self._thread = threading.Thread(target=self._writer, args=(self.stream, self._job),
+                                            name="mic-writer", daemon=True)
             self._thread.start()
         return len(pcm)
 
-    def _write(self, chunk: bytes) -> bool:
+    def _write(self, stream, chunk: bytes) -> bool:
         err = ctypes.c_int(0)
-        if self.pa.pa_simple_write(self.stream, chunk, len(chunk), ctypes.byref(err)) < 0:
+        if self.pa.pa_simple_write(stream, chunk, len(chunk), ctypes.byref(err)) < 0:
             log.error("microphone write failed (%d)", err.value)
             return False
         return True
 
-    def _writer(self):
-        while True:
-            with self._cv:
-                while not self.buffer and not self._stop:
-                    self._cv.wait()
-                if self._stop:
-                    return
-                chunk = bytes(self.buffer[:MIC_WRITE_CHUNK])
-                del self.buffer[:len(chunk)]
-            if not self._write(chunk):
+    def _writer(self, stream, job: dict):
+        """Drains the ring into ``stream``. ``job`` is this writer's own state: a
+        close() that cannot wait out a blocking pa_simple_write marks it orphaned,
+        and the writer then frees its stream itself once the write returns."""
+        try:
+            while True:
                 with self._cv:
-                    self.ready = False
-                    self.buffer.clear()
-                return
-            self.written += len(chunk)
+                    while not self.buffer and not job["stop"]:
+                        self._cv.wait()
+                    if job["stop"]:
+                        return
+                    chunk = bytes(self.buffer[:MIC_WRITE_CHUNK])
+                    del self.buffer[:len(chunk)]
+                if not self._write(stream, chunk):
+                    with self._cv:
+                        self.ready = False
+                        self.buffer.clear()
+                    return
+                self.written += len(chunk)
+        finally:
+            with self._cv:
+                job["done"] = True
+                orphan = job["orphan"]
+            if orphan:
+                self.pa.pa_simple_free(stream)
 
     def close(self):
+        t, job = self._thread, self._job
         with self._cv:
-            self._stop = True
+            if job is not None:
+                job["stop"] = True
             self._cv.notify_all()
-        if self._thread is not None:
-            self._thread.join(timeout=2)
-            self._thread = None
-        if self.stream and self.pa:
-            self.pa.pa_simple_free(self.stream)
+        if t is not None:
+            t.join(timeout=2)
+        stream = self.stream
+        with self._cv:
+            if job is not None and not job["done"]:
+                # still inside pa_simple_write: never free a stream under it
+                job["orphan"] = True
+                stream = None
+        if stream and self.pa:
+            self.pa.pa_simple_free(stream)
+        self._thread = self._job = None
         self.stream = None
         self.ready = False
         self.buffer.clear()

@@ -34,7 +34,7 @@ from aiohttp import WSMsgType, web
 
 from . import protocol
 from .audio import AudioPipeline, MicSink
-from .display import WindowManagerSwap, XrandrDisplay, compute_layout, set_cursor_size, set_dpi
+from .display import WindowManagerSwap, XrandrDisplay, compute_layout, display_env, set_cursor_size, set_dpi
 from .settings import Settings
 from .stats import BandwidthMeter, StatsPublisher
 
@@ -180,8 +180,13 @@ class DataStreamingServer:
     def __init__(self, settings: Settings, *, upload_dir: Optional[str] = None, input_factory=None,
                  capture_factory: Optional[Callable[[], Any]] = None, display_manager=None,
                  capture_source: str = "auto", gpu_id: int = 0, num_gpus: int = 1, clock=time.monotonic,
-                 web_root: Optional[str] = None, metrics=None, frame_trace: Optional[bool] = None):
+                 web_root: Optional[str] = None, metrics=None, frame_trace: Optional[bool] = None,
+                 x_display: Optional[str] = None):
         self.settings = settings
+        # this session's X display, passed explicitly to capture, xrandr, DPI and
+        # the WM swap: a session host runs several servers in one process, so the
+        # process-wide DISPLAY cannot name each session's desktop (parallel/multi.py)
+        self.x_display = x_display if x_display is not None else os.environ.get("DISPLAY")
         self.clock = clock
         self.frame_trace = (os.environ.get("SELKIES_FRAME_TRACE") == "1") if frame_trace is None else frame_trace
         self.mode = "websockets"
@@ -189,6 +194,7 @@ class DataStreamingServer:
         self.displays: "OrderedDict[str, DisplayState]" = OrderedDict()
         self.layouts: dict = {}
         self.captures: dict[str, Capture] = {}
+        self._resync: set[str] = set()     # displays whose queue overflowed: wait for a keyframe
         self.meter = BandwidthMeter(clock)
         self.recent: "OrderedDict[str, float]" = OrderedDict()
         self.reconfigure_lock = asyncio.Lock()
@@ -210,8 +216,9 @@ class DataStreamingServer:
             import pixelflux
             capture_factory = pixelflux.ScreenCapture
         self.capture_factory = capture_factory
-        self.display_manager = display_manager or XrandrDisplay()
-        self.wm_swap = WindowManagerSwap() if getattr(self.display_manager, "available", False) else None
+        self.display_manager = display_manager or XrandrDisplay(self.x_display)
+        self.wm_swap = (WindowManagerSwap(display=self.x_display)
+                        if getattr(self.display_manager, "available", False) else None)
         self.capture_source = capture_source
         self.gpu_id, self.num_gpus = gpu_id, max(1, num_gpus)
         self.web_root = web_root
@@ -436,8 +443,8 @@ class DataStreamingServer:
             except (ValueError, IndexError):
                 log.error("malformed DPI message %s", m)
             else:
-                await set_dpi(dpi)
-                await set_cursor_size(max(1, round(dpi / 96.0 * CURSOR_SIZE)))
+                await set_dpi(dpi, display=self.x_display)
+                await set_cursor_size(max(1, round(dpi / 96.0 * CURSOR_SIZE)), display=self.x_display)
         elif m.startswith("cmd,"):
             if not s.command_enabled[0]:
                 log.warning("cmd refused: commands disabled")
@@ -447,7 +454,8 @@ class DataStreamingServer:
                     try:
                         p = await asyncio.create_subprocess_shell(cmd, stdout=asyncio.subprocess.DEVNULL,
                                                                   stderr=asyncio.subprocess.DEVNULL,
-                                                                  cwd=os.path.expanduser("~"))
+                                                                  cwd=os.path.expanduser("~"),
+                                                                  env=display_env(self.x_display))
                         log.info("launched '%s' (pid %d)", cmd, p.pid)
                     except OSError as e:
                         log.error("cmd failed: %s", e)
@@ -542,7 +550,7 @@ class DataStreamingServer:
             dpi = s.sanitize("scaling_dpi", parsed.get("scaling_dpi"))
             if dpi is not None and dpi != st.scaling_dpi:
                 if st.scaling_dpi is not None or initial:
-                    await set_dpi(int(dpi))
+                    await set_dpi(int(dpi), display=self.x_display)
                 st.scaling_dpi = dpi
             video_changed = any(st.params.get(k) != old.get(k) for k in VIDEO_KEYS)
         if restart_audio:
@@ -655,6 +663,8 @@ class DataStreamingServer:
         cs.capture_x, cs.capture_y = x, y
         cs.target_fps = float(p.get("framerate") or 60)
         cs.capture_cursor = int(self.capture_cursor)
+        if self.x_display:
+            cs.display = self.x_display.encode()
         cs.debug_logging = int(self.settings.debug[0])
         if enc == "jpeg":
             cs.output_mode = 0
@@ -694,6 +704,7 @@ class DataStreamingServer:
         loop = asyncio.get_running_loop()
         queue: asyncio.Queue = asyncio.Queue(maxsize=VIDEO_QUEUE_SIZE)
         jpeg = enc == "jpeg"
+        self._resync.discard(did)
 
         def on_frame(res_ptr, n, user):
             # one call per encoded frame (native capture thread): copy every stripe out
@@ -711,7 +722,7 @@ class DataStreamingServer:
                 grab = r.grab_ns
                 msgs.append(protocol.JPEG_PREFIX + data if jpeg else data)
             if msgs:
-                loop.call_soon_threadsafe(_put_drop, queue, (msgs, key, fid, grab))
+                loop.call_soon_threadsafe(self._put_frame, did, queue, (msgs, key, fid, grab), jpeg)
 
         def on_stripe(res_ptr, user):   # capture modules without a per-frame callback
             r = res_ptr.contents
@@ -720,7 +731,7 @@ class DataStreamingServer:
             data = ctypes.string_at(r.data, r.size)
             key = not jpeg and r.size > 1 and data[1] == 1
             item = ([protocol.JPEG_PREFIX + data if jpeg else data], key, r.frame_id & 0xFFFF, r.grab_ns)
-            loop.call_soon_threadsafe(_put_drop, queue, item)
+            loop.call_soon_threadsafe(self._put_frame, did, queue, item, jpeg)
 
         import pixelflux
         module = self.capture_factory()
@@ -763,6 +774,29 @@ class DataStreamingServer:
             pass
         if self.metrics is not None:
             self.metrics.capture_stopped(did)
+
+    def _put_frame(self, did: str, queue: asyncio.Queue, item, jpeg: bool) -> None:
+        """Native thread -> event loop hand-off of one encoded frame (runs on the loop).
+
+        A full queue drops the frame for every viewer. JPEG stripes stand alone,
+        but an H.264 frame is a reference for the next ones: after a drop no
+        P frame is queued until the keyframe requested here arrives, so decoders
+        never see a broken reference chain."""
+        if did in self._resync:
+            if not item[1]:
+                return
+            self._resync.discard(did)
+        try:
+            queue.put_nowait(item)
+        except asyncio.QueueFull:
+            if jpeg:
+                return
+            self._resync.add(did)
+            cap = self.captures.get(did)
+            if cap is not None and hasattr(cap.module, "request_keyframe"):
+                cap.module.request_keyframe()
+            if self.metrics is not None and hasattr(self.metrics, "frame_dropped"):
+                self.metrics.frame_dropped(did)
 
     async def _video_sender(self, did: str, queue: asyncio.Queue):
         was_enabled = True
@@ -839,13 +873,6 @@ class DataStreamingServer:
         st = self.displays.get(did)
         if st is not None:
             st.flow.client_fps = float(fps)
-
-
-def _put_drop(q: asyncio.Queue, item):
-    try:
-        q.put_nowait(item)
-    except asyncio.QueueFull:
-        pass
 
 
 class _UploadState:

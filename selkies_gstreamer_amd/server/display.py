@@ -120,6 +120,19 @@ def cvt_modeline(width: int, height: int, refresh: float = 60.0) -> tuple[str, s
 
 
 # --------------------------------------------------------------------------- xrandr
+def display_env(display: Optional[str], base: Optional[dict] = None) -> Optional[dict]:
+    """Environment for an X tool aimed at ``display``; None keeps the process's own.
+
+    A session host serves several desktops from one process (parallel/multi.py),
+    so the X display is passed to every subprocess explicitly instead of being
+    read from the process-wide DISPLAY."""
+    if not display:
+        return base
+    env = dict(os.environ if base is None else base)
+    env["DISPLAY"] = display
+    return env
+
+
 async def run(cmd: list[str], env: Optional[dict] = None, timeout: float = 10.0) -> tuple[int, str]:
     """Runs a command; (returncode, stdout). Missing binaries -> (127, '')."""
     if shutil.which(cmd[0]) is None:
@@ -166,19 +179,24 @@ def parse_xrandr(text: str) -> tuple[Optional[str], Optional[str], list[str]]:
 class XrandrDisplay:
     """Applies a layout to the X screen with xrandr (no-op without X)."""
 
-    def __init__(self):
-        self.available = bool(os.environ.get("DISPLAY")) and shutil.which("xrandr") is not None
+    def __init__(self, display: Optional[str] = None):
+        self.display = display if display is not None else os.environ.get("DISPLAY")
+        self.env = display_env(self.display)
+        self.available = bool(self.display) and shutil.which("xrandr") is not None
+
+    async def _x(self, *args):
+        return await run(["xrandr", *args], env=self.env)
 
     async def query(self):
         if not self.available:
             return None, None, []
-        rc, out = await run(["xrandr"])
+        rc, out = await self._x()
         if rc != 0:
             return None, None, []
         return parse_xrandr(out)
 
     async def monitors(self) -> list[str]:
-        rc, out = await run(["xrandr", "--listmonitors"])
+        rc, out = await self._x("--listmonitors")
         if rc != 0:
             return []
         names = []
@@ -193,11 +211,11 @@ class XrandrDisplay:
             return True
         w, h = (int(x) for x in mode.split("x"))
         _, params = cvt_modeline(w, h)
-        rc, _ = await run(["xrandr", "--newmode", mode] + params.split())
-        rc2, _ = await run(["xrandr", "--addmode", screen, mode])
+        rc, _ = await self._x("--newmode", mode, *params.split())
+        rc2, _ = await self._x("--addmode", screen, mode)
         if rc2 != 0:
-            await run(["xrandr", "--delmode", screen, mode])
-            await run(["xrandr", "--rmmode", mode])
+            await self._x("--delmode", screen, mode)
+            await self._x("--rmmode", mode)
             return False
         return True
 
@@ -207,17 +225,17 @@ class XrandrDisplay:
             return False
         for name in await self.monitors():
             if name.startswith("selkies-"):
-                await run(["xrandr", "--delmonitor", name])
+                await self._x("--delmonitor", name)
         mode = f"{total_w}x{total_h}"
         if not await self.ensure_mode(screen, mode, modes):
             log.error("cannot create mode %s", mode)
             return False
-        await run(["xrandr", "--fb", mode, "--output", screen, "--mode", mode])
+        await self._x("--fb", mode, "--output", screen, "--mode", mode)
         for did, l in layouts.items():
             geom = f"{l['w']}/0x{l['h']}/0+{l['x']}+{l['y']}"
-            await run(["xrandr", "--setmonitor", f"selkies-{did}", geom, screen])
+            await self._x("--setmonitor", f"selkies-{did}", geom, screen)
         if "primary" in layouts:
-            await run(["xrandr", "--output", screen, "--primary"])
+            await self._x("--output", screen, "--primary")
         return True
 
     async def clear(self):
@@ -225,7 +243,7 @@ class XrandrDisplay:
             return
         for name in await self.monitors():
             if name.startswith("selkies-"):
-                await run(["xrandr", "--delmonitor", name])
+                await self._x("--delmonitor", name)
 
 
 # --------------------------------------------------------------------------- DPI
@@ -266,7 +284,7 @@ def merge_setting_file(path: str, key: str, line: str, sep: str = " ") -> None:
     os.replace(tmp, path)
 
 
-async def _xrdb_dpi(dpi: int) -> bool:
+async def _xrdb_dpi(dpi: int, display: Optional[str] = None) -> bool:
     """Xft.dpi through xrdb -merge (the resource database, not a file rewrite) plus
     the Xft/DPI key of ~/.xsettingsd with a SIGHUP to a running xsettingsd."""
     if not shutil.which("xrdb"):
@@ -274,7 +292,8 @@ async def _xrdb_dpi(dpi: int) -> bool:
     ok = False
     try:
         p = await asyncio.create_subprocess_exec("xrdb", "-merge", stdin=asyncio.subprocess.PIPE,
-                                                 stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE)
+                                                 stdout=asyncio.subprocess.DEVNULL, stderr=asyncio.subprocess.PIPE,
+                                                 env=display_env(display))
         await p.communicate(f"Xft.dpi: {dpi}\n".encode())
         ok = p.returncode == 0
         merge_setting_file(os.path.expanduser("~/.Xresources"), "Xft.dpi:", f"Xft.dpi:   {dpi}", sep=":")
@@ -287,26 +306,27 @@ async def _xrdb_dpi(dpi: int) -> bool:
     return ok
 
 
-async def _xfconf_dpi(dpi: int) -> bool:
+async def _xfconf_dpi(dpi: int, display: Optional[str] = None) -> bool:
     if not shutil.which("xfconf-query"):
         return False
-    env = await _session_env("xfce4-session")
+    env = display_env(display, await _session_env("xfce4-session"))
     rc, _ = await run(["xfconf-query", "-c", "xsettings", "-p", "/Xft/DPI", "-s", str(dpi), "--create", "-t", "int"],
                       env=env)
     return rc == 0
 
 
-async def _mate_dpi(dpi: int) -> bool:
+async def _mate_dpi(dpi: int, display: Optional[str] = None) -> bool:
     if not shutil.which("gsettings"):
         return False
     scale = dpi / 96.0
     factor = int(scale) if scale == int(scale) else 1
-    rc, _ = await run(["gsettings", "set", "org.mate.interface", "window-scaling-factor", str(max(1, factor))])
-    rc2, _ = await run(["gsettings", "set", "org.mate.font-rendering", "dpi", str(dpi)])
+    env = display_env(display)
+    rc, _ = await run(["gsettings", "set", "org.mate.interface", "window-scaling-factor", str(max(1, factor))], env=env)
+    rc2, _ = await run(["gsettings", "set", "org.mate.font-rendering", "dpi", str(dpi)], env=env)
     return rc == 0 or rc2 == 0
 
 
-async def set_dpi(dpi: int, desktop: Optional[str] = None) -> bool:
+async def set_dpi(dpi: int, desktop: Optional[str] = None, display: Optional[str] = None) -> bool:
     """Applies DPI the way the running desktop takes it: XFCE through xfconf only
     (xrdb as well would scale twice), MATE through gsettings + xrdb, KDE / i3 /
     Openbox / anything else through xrdb."""
@@ -318,12 +338,12 @@ async def set_dpi(dpi: int, desktop: Optional[str] = None) -> bool:
         return False
     de = desktop or detect_desktop()
     if de == "xfce":
-        ok = await _xfconf_dpi(dpi)
+        ok = await _xfconf_dpi(dpi, display)
     elif de == "mate":
-        ok = await _mate_dpi(dpi)
-        ok = await _xrdb_dpi(dpi) or ok
+        ok = await _mate_dpi(dpi, display)
+        ok = await _xrdb_dpi(dpi, display) or ok
     else:
-        ok = await _xrdb_dpi(dpi)
+        ok = await _xrdb_dpi(dpi, display)
     if not ok:
         log.warning("no DPI method succeeded for %d (desktop %s)", dpi, de)
     return ok
@@ -336,17 +356,18 @@ class WindowManagerSwap:
     Unlike the reference this also switches back when the session returns to one
     display."""
 
-    def __init__(self, which=shutil.which, runner=None):
+    def __init__(self, which=shutil.which, runner=None, display: Optional[str] = None):
         self.which = which
+        self.env = display_env(display)
         self.desktop = detect_desktop(which)
         self.supported = self.desktop in ("xfce", "kde") and which("openbox") is not None
         self.swapped = False
-        self._run = runner or self._spawn
+        self._runner = runner
 
     @staticmethod
-    async def _spawn(cmd):
+    async def _spawn(cmd, env=None):
         try:
-            await asyncio.create_subprocess_exec(*cmd, stdout=asyncio.subprocess.DEVNULL,
+            await asyncio.create_subprocess_exec(*cmd, stdout=asyncio.subprocess.DEVNULL, env=env,
                                                  stderr=asyncio.subprocess.DEVNULL, start_new_session=True)
         except OSError as e:
             log.warning("%s failed: %s", cmd[0], e)
@@ -362,23 +383,30 @@ class WindowManagerSwap:
                 cmd = ["openbox", "--config-file", cfg, "--replace"]
             except OSError:
                 cmd = ["openbox", "--replace"]
-            await self._run(cmd)
+            await self._call(cmd)
             self.swapped = True
         elif display_count <= 1 and self.swapped:
             native = ["xfwm4", "--replace"] if self.desktop == "xfce" else ["kwin_x11", "--replace"]
-            await self._run(native)
+            await self._call(native)
             self.swapped = False
 
+    async def _call(self, cmd):
+        if self._runner is None:
+            await self._spawn(cmd, self.env)
+        else:
+            await self._runner(cmd)
 
-async def set_cursor_size(size: int) -> bool:
+
+async def set_cursor_size(size: int, display: Optional[str] = None) -> bool:
     ok = False
     if shutil.which("xfconf-query"):
-        env = await _session_env("xfce4-session")
+        env = display_env(display, await _session_env("xfce4-session"))
         rc, _ = await run(["xfconf-query", "-c", "xsettings", "-p", "/Gtk/CursorThemeSize", "-s", str(size),
                            "--create", "-t", "int"], env=env)
         ok |= rc == 0
     if shutil.which("gsettings"):
-        rc, _ = await run(["gsettings", "set", "org.mate.peripherals-mouse", "cursor-size", str(size)])
+        rc, _ = await run(["gsettings", "set", "org.mate.peripherals-mouse", "cursor-size", str(size)],
+                          env=display_env(display))
         ok |= rc == 0
     return ok
 

@@ -175,17 +175,20 @@ class Clipboard:
     """X clipboard through xclip (or xsel for text); a no-op when neither exists."""
     IMAGE_TYPES = ("image/png", "image/jpeg", "image/bmp", "image/svg", "image/webp")
 
-    def __init__(self):
+    def __init__(self, display: Optional[str] = None):
         self.xclip = shutil.which("xclip")
         self.xsel = shutil.which("xsel")
+        self.display = display if display is not None else os.environ.get("DISPLAY")
+        self.env = dict(os.environ, DISPLAY=self.display) if self.display else None
 
     @property
     def available(self):
-        return bool(self.xclip or self.xsel) and bool(os.environ.get("DISPLAY"))
+        return bool(self.xclip or self.xsel) and bool(self.display)
 
     async def _run(self, cmd, data: Optional[bytes] = None, timeout=2.0):
         p = await asyncio.create_subprocess_exec(*cmd, stdin=asyncio.subprocess.PIPE if data is not None else None,
-                                                 stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.DEVNULL)
+                                                 stdout=asyncio.subprocess.PIPE, stderr=asyncio.subprocess.DEVNULL,
+                                                 env=self.env)
         out, _ = await asyncio.wait_for(p.communicate(data), timeout)
         return p.returncode, out
 

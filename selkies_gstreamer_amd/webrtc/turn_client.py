@@ -57,6 +57,9 @@ class TurnAllocation:
         self.mapped: Optional[tuple] = None
         self.permissions: dict = {}     # peer ip -> last refresh (loop time)
         self.channels: dict = {}        # peer (ip, port) -> channel number
+        self.bound_at: dict = {}        # peer (ip, port) -> last ChannelBind (loop time)
+        self.permission_refresh_s = PERMISSION_REFRESH_S
+        self.channel_refresh_s = CHANNEL_REFRESH_S
         self.peers_by_channel: dict = {}
         self._next_channel = 0x4000
         self._pending: dict = {}
@@ -124,18 +127,22 @@ class TurnAllocation:
         loop = asyncio.get_running_loop()
         last_alloc = loop.time()
         while True:
-            await asyncio.sleep(min(30.0, max(1.0, self.lifetime / 4)))
+            await asyncio.sleep(min(30.0, max(0.05, self.lifetime / 4), self.permission_refresh_s / 4,
+                                    self.channel_refresh_s / 4))
             now = loop.time()
             try:
                 if now - last_alloc > max(1.0, self.lifetime - 60):
                     await self._authed(lambda: self._refresh_msg(self.lifetime))
                     last_alloc = now
-                for ip, t in list(self.permissions.items()):
-                    if now - t > PERMISSION_REFRESH_S:
-                        await self.create_permission(ip)
+                # a binding's age is its own: permission refreshes do not renew a
+                # channel (RFC 5766 §11), and a binding that lapses after 600 s
+                # takes the relayed media and ICE keepalives with it
                 for peer, ch in list(self.channels.items()):
-                    if now - self.permissions.get(peer[0], 0) > CHANNEL_REFRESH_S:
+                    if now - self.bound_at.get(peer, 0) > self.channel_refresh_s:
                         await self._bind(peer, ch)
+                for ip, t in list(self.permissions.items()):
+                    if now - t > self.permission_refresh_s:
+                        await self.create_permission(ip)
             except (OSError, asyncio.TimeoutError) as e:
                 log.warning("TURN refresh failed: %s", e)
 
@@ -159,6 +166,9 @@ class TurnAllocation:
             m.attrs[stun.XOR_PEER_ADDRESS] = peer
             return m
         await self._authed(req)
+        now = asyncio.get_running_loop().time()
+        self.bound_at[peer] = now
+        self.permissions[peer[0]] = now    # a ChannelBind installs/refreshes the peer's permission too
 
     async def channel_bind(self, peer: tuple) -> int:
         peer = (peer[0], peer[1])
@@ -169,7 +179,6 @@ class TurnAllocation:
         await self._bind(peer, ch)
         self.channels[peer] = ch
         self.peers_by_channel[ch] = peer
-        self.permissions.setdefault(peer[0], asyncio.get_running_loop().time())   # a binding installs one
         return ch
 
     # -- data ------------------------------------------------------------------------------------

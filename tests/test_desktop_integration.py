@@ -39,9 +39,9 @@ def test_set_dpi_dispatch(monkeypatch):
     async def fake(name, ok=True):
         calls.append(name)
         return ok
-    monkeypatch.setattr(display, "_xfconf_dpi", lambda d: fake("xfconf"))
-    monkeypatch.setattr(display, "_mate_dpi", lambda d: fake("mate"))
-    monkeypatch.setattr(display, "_xrdb_dpi", lambda d: fake("xrdb"))
+    monkeypatch.setattr(display, "_xfconf_dpi", lambda d, disp=None: fake("xfconf"))
+    monkeypatch.setattr(display, "_mate_dpi", lambda d, disp=None: fake("mate"))
+    monkeypatch.setattr(display, "_xrdb_dpi", lambda d, disp=None: fake("xrdb"))
     for de, exp in (("xfce", ["xfconf"]), ("mate", ["mate", "xrdb"]), ("kde", ["xrdb"]), ("i3", ["xrdb"]),
                     ("generic", ["xrdb"])):
         calls.clear()
@@ -74,7 +74,7 @@ def test_mic_sink_push_does_not_block():
     release = threading.Event()
     written = []
 
-    def slow_write(chunk):   # PulseAudio's buffer is full: the write blocks
+    def slow_write(stream, chunk):   # PulseAudio's buffer is full: the write blocks
         release.wait(5)
         written.append(len(chunk))
         return True
@@ -93,3 +93,44 @@ def test_mic_sink_push_does_not_block():
     assert not sink.buffer and sum(written) > 0
     sink.close()
     assert sink._thread is None
+
+
+def test_mic_sink_close_never_frees_under_a_blocked_write():
+    """close() waits 2 s; a writer still inside pa_simple_write then owns the stream
+    and frees it itself when the write returns. A reopened sink gets a live writer."""
+    freed = []
+
+    class PA:
+        def pa_simple_free(self, s):
+            freed.append(s)
+    sink = audio.MicSink()
+    sink.pa = PA()
+    release = threading.Event()
+    entered = threading.Event()
+
+    def blocked_write(stream, chunk):
+        entered.set()
+        release.wait(10)
+        return True
+    sink._write = blocked_write
+    sink.stream, sink.ready = "s1", True
+    sink.push(b"\x00\x00" * 480)
+    assert entered.wait(5)
+    t = time.perf_counter()
+    sink.close()
+    assert 1.5 < time.perf_counter() - t < 5 and freed == []     # not freed under the write
+    release.set()
+    deadline = time.time() + 5
+    while not freed and time.time() < deadline:
+        time.sleep(0.01)
+    assert freed == ["s1"]                                         # the writer freed it afterwards
+    got = []
+    sink._write = lambda stream, chunk: got.append(stream) or True
+    sink.stream, sink.ready = "s2", True
+    sink.push(b"\x00\x00" * 480)
+    deadline = time.time() + 5
+    while not got and time.time() < deadline:
+        time.sleep(0.01)
+    assert got == ["s2"]                                           # reopened sink writes again
+    sink.close()
+    assert freed == ["s1", "s2"]

@@ -154,8 +154,15 @@ def test_second_screen_layout(tmp_path):
                                        and "display2" in m)
             assert json.loads(cfg.split(",", 1)[1])["displays"] == ["primary", "display2"]
             assert srv.layouts["display2"] == {"x": 0, "y": 128, "w": 128, "h": 64}
-            data, _ = await _recv_until(d2, lambda m: isinstance(m, bytes))
-            assert int.from_bytes(data[6:8], "big") == 128  # display2's own stream width
+            # until its SETTINGS lands, a new connection is a view-only (#shared) client of
+            # the primary display and may get primary stripes (reference semantics, selkies.py
+            # broadcasts to every client not registered as a secondary display); after that
+            # only display2's own 128-wide stream arrives
+            data, _ = await _recv_until(d2, lambda m: isinstance(m, bytes) and m[0] == 0x04
+                                        and int.from_bytes(m[6:8], "big") == 128)
+            for _ in range(3):
+                data, _ = await _recv_until(d2, lambda m: isinstance(m, bytes) and m[0] == 0x04)
+                assert int.from_bytes(data[6:8], "big") == 128  # display2's own stream width
             await d2.close()
             await p.close()
         await srv.stop()

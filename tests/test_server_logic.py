@@ -301,3 +301,36 @@ def test_input_gamepad_dispatch(tmp_path):
         assert hub.pads[1].client_name is None
         await hub.close()
     asyncio.run(run())
+
+
+def test_queue_overflow_requests_keyframe_and_skips_p_frames():
+    """A full native->loop queue drops an H.264 frame for every viewer: the server
+    asks for a keyframe and queues no P frame until it arrives (JPEG just drops)."""
+    import asyncio as aio
+    from selkies_gstreamer_amd.server.data_server import Capture, DataStreamingServer
+    from selkies_gstreamer_amd.server.settings import Settings
+
+    class Mod:
+        kf = 0
+
+        def request_keyframe(self):
+            Mod.kf += 1
+
+    async def main():
+        srv = DataStreamingServer(Settings([]), capture_factory=Mod)
+        q = aio.Queue(maxsize=2)
+        srv.captures["primary"] = Capture("primary", Mod(), q, None)
+        for fid in range(3):                       # third frame overflows
+            srv._put_frame("primary", q, ([b"p"], fid == 0, fid, 0), False)
+        assert Mod.kf == 1 and q.qsize() == 2
+        q.get_nowait()
+        q.get_nowait()
+        srv._put_frame("primary", q, ([b"p"], False, 3, 0), False)
+        assert q.qsize() == 0                      # P frame after the drop is not queued
+        srv._put_frame("primary", q, ([b"i"], True, 4, 0), False)
+        assert q.qsize() == 1 and "primary" not in srv._resync
+        srv._put_frame("primary", q, ([b"p"], False, 5, 0), False)
+        assert q.qsize() == 2
+        srv._put_frame("primary", q, ([b"j"], False, 6, 0), True)   # JPEG overflow: no keyframe request
+        assert Mod.kf == 1 and "primary" not in srv._resync
+    aio.run(main())

@@ -68,3 +68,56 @@ def test_launcher_groups_sessions_into_hosts():
     assert cmd[:3] == ["python", "-m", "selkies_gstreamer_amd.parallel.multi"]
     assert cmd[cmd.index("--") + 1:][:2] == ["--gpu-id", str(hosts[0].gpu)]
     assert group_hosts(specs, 1) is specs
+
+
+def test_session_argvs_give_each_session_its_display():
+    out = session_argvs([9001, 9002], ["--display", ":0", "--use-cpu", "true"], [":20", ":21"])
+    assert out == [["--port", "9001", "--display", ":20", "--use-cpu", "true"],
+                   ["--port", "9002", "--display", ":21", "--use-cpu", "true"]]
+
+
+def test_two_displays_stay_separate(monkeypatch):
+    """Every session of a host captures, injects into and reconfigures its own X
+    display; the process-wide DISPLAY is never consulted or rewritten."""
+    from selkies_gstreamer_amd.server.data_server import DisplayState
+    from selkies_gstreamer_amd.server.settings import Settings
+    monkeypatch.setenv("DISPLAY", ":99")
+
+    async def main():
+        ports = [_free_port(), _free_port()]
+        servers = {}
+        stop = asyncio.Event()
+        task = asyncio.create_task(host(ports, ["--host", "127.0.0.1", "--use-cpu", "true", "--capture-source",
+                                                "synthetic", "--audio-enabled", "false", "--gamepad-enabled",
+                                                "false"], displays=[":20", ":21"], stop=stop,
+                                        ready=lambda srv, port: servers.__setitem__(port, srv)))
+        for _ in range(200):
+            if len(servers) == 2:
+                break
+            await asyncio.sleep(0.05)
+        import os
+        assert os.environ["DISPLAY"] == ":99"
+        for port, want in zip(ports, (":20", ":21")):
+            srv = servers[port]
+            assert srv.x_display == want
+            assert srv.display_manager.display == want
+            st = DisplayState(client=None)
+            st.params = dict(Settings([]).client_defaults()) if hasattr(Settings([]), "client_defaults") else {}
+            st.params.update({"encoder": "jpeg", "jpeg_quality": 40, "paint_over_jpeg_quality": 90,
+                              "use_paint_over_quality": True, "use_cpu": True, "framerate": 30})
+            srv.displays["primary"] = st
+            cs, _ = srv.capture_settings("primary", 256, 128, 0, 0)
+            assert cs.display == want.encode()
+        stop.set()
+        await asyncio.wait_for(task, 30)
+    asyncio.run(asyncio.wait_for(main(), 90))
+
+
+def test_clipboard_and_xrandr_use_explicit_display(monkeypatch):
+    from selkies_gstreamer_amd.server.display import XrandrDisplay, display_env
+    from selkies_gstreamer_amd.server.input import Clipboard
+    monkeypatch.setenv("DISPLAY", ":99")
+    assert Clipboard(":21").env["DISPLAY"] == ":21"
+    assert XrandrDisplay(":22").env["DISPLAY"] == ":22"
+    assert display_env(None) is None
+    assert display_env(":5", {"A": "1"}) == {"A": "1", "DISPLAY": ":5"}

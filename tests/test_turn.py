@@ -115,3 +115,32 @@ def test_relay_candidate_alongside_host():
         await b.close()
         srv.close()
     run(main())
+
+
+def test_channel_binding_refreshed_independently_of_permissions():
+    """Permission refreshes (every ~240 s) must not reset a channel binding's age:
+    the binding itself is re-sent before its 600 s lifetime runs out (RFC 5766 §11).
+    Lifetimes are shortened 1000x here."""
+    async def main():
+        srv = TurnStub({"alice": "secret"})
+        addr = await srv.start()
+        loop = asyncio.get_running_loop()
+
+        class P(asyncio.DatagramProtocol):
+            def datagram_received(self, data, a):
+                alloc.on_datagram(data)
+        tr, _ = await loop.create_datagram_endpoint(P, local_addr=("127.0.0.1", 0))
+        alloc = TurnAllocation(addr, "alice", "secret", tr.sendto)
+        alloc.permission_refresh_s, alloc.channel_refresh_s = 0.24, 0.54
+        await alloc.allocate()
+        await alloc.create_permission("127.0.0.1")
+        await alloc.channel_bind(("127.0.0.1", 9))
+        await asyncio.sleep(1.5)
+        binds = srv.requests.count(stun.CHANNEL_BIND)
+        perms = srv.requests.count(stun.CREATE_PERMISSION)
+        await alloc.close()
+        tr.close()
+        srv.close()
+        assert binds >= 3, srv.requests         # initial bind + at least two refreshes in 1.5 s
+        assert perms >= 1
+    run(main())

@@ -24,6 +24,7 @@ class _Relay(asyncio.DatagramProtocol):
 
 class TurnStub(asyncio.DatagramProtocol):
     def __init__(self, users: dict, realm: str = "selkies.test"):
+        self.requests: list = []
         self.users, self.realm, self.nonce = users, realm, "n0nce"
         self.allocs: dict = {}      # client addr -> {relay transport, perms, channels, peers_by_ch}
         self.transport = None
@@ -79,6 +80,7 @@ class TurnStub(asyncio.DatagramProtocol):
         asyncio.ensure_future(self._handle(msg, addr, key))
 
     async def _handle(self, msg, addr, key):
+        self.requests.append(msg.method)
         a = self.allocs.get(addr)
         if msg.method == stun.ALLOCATE:
             if a is None:
