@@ -1,0 +1,914 @@
+// AV1 (Main profile, 8-bit 4:2:0) primitives shared by the CPU reference encoder
+// (av1_cpu.cpp) and the gfx950 kernels (kernels/av1_kernels.hip): block geometry,
+// transforms and (de)quantisation, intra prediction, sub-pel motion compensation,
+// the reference-MV stack and the syntax of blocks and coefficients written through
+// a symbol sink (direct arithmetic coding on the host, token lists on the GPU).
+//
+// Decoder-side processes (inverse transform, dequantisation, prediction, MV stack,
+// context selection) follow the normative processes of the AV1 bitstream spec
+// (v1.0.0 + errata) §5.11 / §7.10-7.13 / §8.3; forward transform, quantisation and
+// every mode decision are encoder choices. Conformance is checked by decoding the
+// streams with dav1d (tests/test_av1_encoder.py) and comparing with the encoder's
+// own reconstruction bit for bit.
+//
+// Coding structure (fixed by the sequence / frame headers of av1_cpu.cpp):
+//   64x64 superblocks; blocks are square 8/16/32/64 (PARTITION_NONE or SPLIT only);
+//   TX_MODE_LARGEST (one transform per block, DCT_DCT, reduced_tx_set); intra
+//   DC / V / H / SMOOTH(_V/_H) / PAETH, no filter-intra / CfL / palette / intraBC,
+//   intra edge filter off; one reference (LAST), single prediction, EIGHTTAP
+//   regular filter, quarter-pel vectors (allow_high_precision_mv = 0); no
+//   order hints (no temporal MVs, no skip mode); loop filter / CDEF / LR off.
+#pragma once
+#include "sk_common.h"
+#include "av1_tables.h"
+#include "av1_ec.h"
+
+namespace sk::av1 {
+
+// ---------------------------------------------------------------------------------
+// Enumerations (spec values).
+enum PredMode : uint8_t {
+    DC_PRED = 0, V_PRED, H_PRED, D45_PRED, D135_PRED, D113_PRED, D157_PRED, D203_PRED, D67_PRED,
+    SMOOTH_PRED, SMOOTH_V_PRED, SMOOTH_H_PRED, PAETH_PRED, UV_CFL_PRED,
+    NEARESTMV = 13, NEARMV = 14, GLOBALMV = 15, NEWMV = 16
+};
+enum Partition : int { PARTITION_NONE = 0, PARTITION_HORZ = 1, PARTITION_VERT = 2, PARTITION_SPLIT = 3,
+                       PARTITION_HORZ_A = 4, PARTITION_HORZ_B = 5, PARTITION_VERT_A = 6, PARTITION_VERT_B = 7,
+                       PARTITION_HORZ_4 = 8, PARTITION_VERT_4 = 9 };
+enum TxSize : int { TX_4X4 = 0, TX_8X8 = 1, TX_16X16 = 2, TX_32X32 = 3, TX_64X64 = 4 };
+enum MvJoint : int { MV_JOINT_ZERO = 0, MV_JOINT_HNZVZ = 1, MV_JOINT_HZVNZ = 2, MV_JOINT_HNZVNZ = 3 };
+
+constexpr int kRefCatLevel = 640;
+constexpr int kMaxRefMvStack = 8;
+constexpr int kMvBorder = 128;            // MV_BORDER, 1/8 pel
+constexpr int kIntraFrame = 0, kLastFrame = 1;
+
+// Block sizes are square: bsl = log2(width in 4x4 units) = Mi_Width_Log2: 8x8 -> 1 ... 64x64 -> 4.
+SK_HD int bsl_px(int bsl) { return 4 << bsl; }
+
+// Intra_Mode_Context (kf y-mode contexts)
+SK_HD int intra_mode_ctx(int m) { return (int)((0x0123444430120ull >> (4 * (12 - m))) & 15); }
+
+// ---------------------------------------------------------------------------------
+// Geometry of one frame and its tiles (uniform tile spacing, §5.9.15).
+struct Av1Geo {
+    int W = 0, H = 0;            // frame size
+    int mi_cols = 0, mi_rows = 0;
+    int sb_cols = 0, sb_rows = 0;
+    int tile_cols_log2 = 0, tile_rows_log2 = 0;
+    int tile_cols = 0, tile_rows = 0;
+    int tile_w_sb = 0, tile_h_sb = 0;
+    int min_log2_tile_cols = 0, max_log2_tile_cols = 0, max_log2_tile_rows = 0, min_log2_tiles = 0;
+    int c8 = 0, r8 = 0;          // 8x8 cell grid (mi_cols / 2, mi_rows / 2)
+};
+
+SK_HD int tile_log2(int blk, int target) {
+    int k = 0;
+    while ((blk << k) < target) k++;
+    return k;
+}
+
+// want_cols_log2 / want_rows_log2: requested split, clamped to the legal range.
+SK_HD void geo_init(Av1Geo& g, int W, int H, int want_cols_log2, int want_rows_log2) {
+    g.W = W;
+    g.H = H;
+    g.mi_cols = 2 * ((W + 7) >> 3);
+    g.mi_rows = 2 * ((H + 7) >> 3);
+    g.c8 = g.mi_cols >> 1;
+    g.r8 = g.mi_rows >> 1;
+    g.sb_cols = (g.mi_cols + 15) >> 4;
+    g.sb_rows = (g.mi_rows + 15) >> 4;
+    const int max_tile_w_sb = 4096 >> 6, max_tile_area_sb = (4096 * 2304) >> 12;
+    g.min_log2_tile_cols = tile_log2(max_tile_w_sb, g.sb_cols);
+    g.max_log2_tile_cols = tile_log2(1, sk_min(g.sb_cols, 64));
+    g.max_log2_tile_rows = tile_log2(1, sk_min(g.sb_rows, 64));
+    g.min_log2_tiles = sk_max(g.min_log2_tile_cols, tile_log2(max_tile_area_sb, g.sb_rows * g.sb_cols));
+    g.tile_cols_log2 = sk_clip(want_cols_log2, g.min_log2_tile_cols, g.max_log2_tile_cols);
+    g.tile_w_sb = (g.sb_cols + (1 << g.tile_cols_log2) - 1) >> g.tile_cols_log2;
+    g.tile_cols = (g.sb_cols + g.tile_w_sb - 1) / g.tile_w_sb;
+    const int min_log2_rows = sk_max(g.min_log2_tiles - g.tile_cols_log2, 0);
+    g.tile_rows_log2 = sk_clip(want_rows_log2, min_log2_rows, g.max_log2_tile_rows);
+    g.tile_h_sb = (g.sb_rows + (1 << g.tile_rows_log2) - 1) >> g.tile_rows_log2;
+    g.tile_rows = (g.sb_rows + g.tile_h_sb - 1) / g.tile_h_sb;
+}
+
+struct TileRect {
+    int mi_row0, mi_row1, mi_col0, mi_col1;   // [start, end)
+};
+SK_HD TileRect tile_rect(const Av1Geo& g, int t) {
+    const int tr = t / g.tile_cols, tc = t % g.tile_cols;
+    TileRect r;
+    r.mi_row0 = tr * g.tile_h_sb * 16;
+    r.mi_row1 = sk_min((tr + 1) * g.tile_h_sb * 16, g.mi_rows);
+    r.mi_col0 = tc * g.tile_w_sb * 16;
+    r.mi_col1 = sk_min((tc + 1) * g.tile_w_sb * 16, g.mi_cols);
+    return r;
+}
+SK_HD bool inside(const TileRect& t, int r, int c) {
+    return r >= t.mi_row0 && r < t.mi_row1 && c >= t.mi_col0 && c < t.mi_col1;
+}
+
+// ---------------------------------------------------------------------------------
+// Per-8x8-cell block info (every block is >= 8x8 and 8-aligned, so an 8x8 cell
+// grid holds the spec's per-mi arrays MiSizes / YModes / IsInters / RefFrames /
+// Mvs / Skips at 2x2-mi resolution). 12 bytes, shared by CPU and GPU buffers.
+struct BlkInfo {
+    uint8_t bsl;       // block size (Mi_Width_Log2), 0 = not coded yet
+    uint8_t mode;      // YMode (intra 0..12, inter NEARESTMV..NEWMV)
+    uint8_t uv_mode;   // UVMode (intra)
+    uint8_t flags;     // bit0 is_inter, bit1 skip, bit2 merged-static (encoder), bits 4-5 RefMvIdx
+    int16_t mv_row, mv_col;   // 1/8 pel (LAST), even values (no high-precision MVs)
+    int16_t pad0, pad1;
+};
+static_assert(sizeof(BlkInfo) == 12, "BlkInfo layout");
+SK_HD bool blk_inter(const BlkInfo& b) { return (b.flags & 1) != 0; }
+SK_HD bool blk_skip(const BlkInfo& b) { return (b.flags & 2) != 0; }
+
+// ---------------------------------------------------------------------------------
+// Transforms. Forward: encoder choice, an integer DCT-II scaled to 8x the
+// orthonormal transform (the coefficient domain of AV1's 4/8/16-point transforms,
+// fwd_shift {2,0..-2,0}). Inverse: the normative butterflies (spec §7.13.2,
+// cos_bit 12) with the 2-D row/column shifts of §7.13.3.
+SK_HD int cospi12(int i) {   // round(4096 * cos(i * pi / 128)), i = 0..64
+    constexpr uint16_t t[65] = {4096, 4095, 4091, 4085, 4076, 4065, 4052, 4036, 4017, 3996, 3973, 3948, 3920,
+                                3889, 3857, 3822, 3784, 3745, 3703, 3659, 3612, 3564, 3513, 3461, 3406, 3349,
+                                3290, 3229, 3166, 3102, 3035, 2967, 2896, 2824, 2751, 2675, 2598, 2520, 2440,
+                                2359, 2276, 2191, 2106, 2019, 1931, 1842, 1751, 1660, 1567, 1474, 1380, 1285,
+                                1189, 1092, 995,  897,  799,  700,  601,  501,  401,  301,  201,  101,  0};
+    return t[i];
+}
+SK_HD int32_t hbtf(int w0, int32_t a, int w1, int32_t b) {
+    return (int32_t)(((int64_t)w0 * a + (int64_t)w1 * b + 2048) >> 12);
+}
+
+SK_HD void idct4(int32_t* x) {
+    const int32_t a0 = x[0], a1 = x[2], a2 = x[1], a3 = x[3];
+    const int32_t b0 = hbtf(cospi12(32), a0, cospi12(32), a1);
+    const int32_t b1 = hbtf(cospi12(32), a0, -cospi12(32), a1);
+    const int32_t b2 = hbtf(cospi12(48), a2, -cospi12(16), a3);
+    const int32_t b3 = hbtf(cospi12(16), a2, cospi12(48), a3);
+    x[0] = b0 + b3;
+    x[1] = b1 + b2;
+    x[2] = b1 - b2;
+    x[3] = b0 - b3;
+}
+
+SK_HD void idct8(int32_t* x) {
+    int32_t a[8] = {x[0], x[4], x[2], x[6], x[1], x[5], x[3], x[7]};
+    int32_t b[8];
+    // stage 2
+    b[0] = a[0]; b[1] = a[1]; b[2] = a[2]; b[3] = a[3];
+    b[4] = hbtf(cospi12(56), a[4], -cospi12(8), a[7]);
+    b[5] = hbtf(cospi12(24), a[5], -cospi12(40), a[6]);
+    b[6] = hbtf(cospi12(40), a[5], cospi12(24), a[6]);
+    b[7] = hbtf(cospi12(8), a[4], cospi12(56), a[7]);
+    // stage 3
+    a[0] = hbtf(cospi12(32), b[0], cospi12(32), b[1]);
+    a[1] = hbtf(cospi12(32), b[0], -cospi12(32), b[1]);
+    a[2] = hbtf(cospi12(48), b[2], -cospi12(16), b[3]);
+    a[3] = hbtf(cospi12(16), b[2], cospi12(48), b[3]);
+    a[4] = b[4] + b[5];
+    a[5] = b[4] - b[5];
+    a[6] = -b[6] + b[7];
+    a[7] = b[6] + b[7];
+    // stage 4
+    b[0] = a[0] + a[3];
+    b[1] = a[1] + a[2];
+    b[2] = a[1] - a[2];
+    b[3] = a[0] - a[3];
+    b[4] = a[4];
+    b[5] = hbtf(-cospi12(32), a[5], cospi12(32), a[6]);
+    b[6] = hbtf(cospi12(32), a[5], cospi12(32), a[6]);
+    b[7] = a[7];
+    // stage 5
+    for (int i = 0; i < 4; i++) {
+        x[i] = b[i] + b[7 - i];
+        x[7 - i] = b[i] - b[7 - i];
+    }
+}
+
+SK_HD void idct16(int32_t* x) {
+    int32_t a[16] = {x[0], x[8], x[4], x[12], x[2], x[10], x[6], x[14],
+                     x[1], x[9], x[5], x[13], x[3], x[11], x[7], x[15]};
+    int32_t b[16];
+    // stage 2
+    for (int i = 0; i < 8; i++) b[i] = a[i];
+    b[8] = hbtf(cospi12(60), a[8], -cospi12(4), a[15]);
+    b[9] = hbtf(cospi12(28), a[9], -cospi12(36), a[14]);
+    b[10] = hbtf(cospi12(44), a[10], -cospi12(20), a[13]);
+    b[11] = hbtf(cospi12(12), a[11], -cospi12(52), a[12]);
+    b[12] = hbtf(cospi12(52), a[11], cospi12(12), a[12]);
+    b[13] = hbtf(cospi12(20), a[10], cospi12(44), a[13]);
+    b[14] = hbtf(cospi12(36), a[9], cospi12(28), a[14]);
+    b[15] = hbtf(cospi12(4), a[8], cospi12(60), a[15]);
+    // stage 3
+    for (int i = 0; i < 4; i++) a[i] = b[i];
+    a[4] = hbtf(cospi12(56), b[4], -cospi12(8), b[7]);
+    a[5] = hbtf(cospi12(24), b[5], -cospi12(40), b[6]);
+    a[6] = hbtf(cospi12(40), b[5], cospi12(24), b[6]);
+    a[7] = hbtf(cospi12(8), b[4], cospi12(56), b[7]);
+    a[8] = b[8] + b[9];
+    a[9] = b[8] - b[9];
+    a[10] = -b[10] + b[11];
+    a[11] = b[10] + b[11];
+    a[12] = b[12] + b[13];
+    a[13] = b[12] - b[13];
+    a[14] = -b[14] + b[15];
+    a[15] = b[14] + b[15];
+    // stage 4
+    b[0] = hbtf(cospi12(32), a[0], cospi12(32), a[1]);
+    b[1] = hbtf(cospi12(32), a[0], -cospi12(32), a[1]);
+    b[2] = hbtf(cospi12(48), a[2], -cospi12(16), a[3]);
+    b[3] = hbtf(cospi12(16), a[2], cospi12(48), a[3]);
+    b[4] = a[4] + a[5];
+    b[5] = a[4] - a[5];
+    b[6] = -a[6] + a[7];
+    b[7] = a[6] + a[7];
+    b[8] = a[8];
+    b[9] = hbtf(-cospi12(16), a[9], cospi12(48), a[14]);
+    b[10] = hbtf(-cospi12(48), a[10], -cospi12(16), a[13]);
+    b[11] = a[11];
+    b[12] = a[12];
+    b[13] = hbtf(-cospi12(16), a[10], cospi12(48), a[13]);
+    b[14] = hbtf(cospi12(48), a[9], cospi12(16), a[14]);
+    b[15] = a[15];
+    // stage 5
+    a[0] = b[0] + b[3];
+    a[1] = b[1] + b[2];
+    a[2] = b[1] - b[2];
+    a[3] = b[0] - b[3];
+    a[4] = b[4];
+    a[5] = hbtf(-cospi12(32), b[5], cospi12(32), b[6]);
+    a[6] = hbtf(cospi12(32), b[5], cospi12(32), b[6]);
+    a[7] = b[7];
+    a[8] = b[8] + b[11];
+    a[9] = b[9] + b[10];
+    a[10] = b[9] - b[10];
+    a[11] = b[8] - b[11];
+    a[12] = -b[12] + b[15];
+    a[13] = -b[13] + b[14];
+    a[14] = b[13] + b[14];
+    a[15] = b[12] + b[15];
+    // stage 6
+    for (int i = 0; i < 4; i++) {
+        b[i] = a[i] + a[7 - i];
+        b[7 - i] = a[i] - a[7 - i];
+    }
+    b[8] = a[8];
+    b[9] = a[9];
+    b[10] = hbtf(-cospi12(32), a[10], cospi12(32), a[13]);
+    b[11] = hbtf(-cospi12(32), a[11], cospi12(32), a[12]);
+    b[12] = hbtf(cospi12(32), a[11], cospi12(32), a[12]);
+    b[13] = hbtf(cospi12(32), a[10], cospi12(32), a[13]);
+    b[14] = a[14];
+    b[15] = a[15];
+    // stage 7
+    for (int i = 0; i < 8; i++) {
+        x[i] = b[i] + b[15 - i];
+        x[15 - i] = b[i] - b[15 - i];
+    }
+}
+
+SK_HD void idct_1d(int32_t* x, int log2n) {
+    if (log2n == 2) idct4(x);
+    else if (log2n == 3) idct8(x);
+    else idct16(x);
+}
+
+// 2-D inverse DCT_DCT of an n x n block (n = 4, 8, 16): dequantised coefficients
+// `d` (raster [row][col], row = vertical frequency) -> residual `r`.
+SK_HD void inv_transform(const int32_t* d, int log2n, int32_t* r) {
+    const int n = 1 << log2n;
+    const int row_shift = log2n == 2 ? 0 : (log2n == 3 ? 1 : 2);
+    int32_t t[16];
+    for (int i = 0; i < n; i++) {
+        for (int j = 0; j < n; j++) t[j] = d[i * n + j];
+        idct_1d(t, log2n);
+        for (int j = 0; j < n; j++) {
+            const int32_t v = row_shift ? (t[j] + (1 << (row_shift - 1))) >> row_shift : t[j];
+            r[i * n + j] = sk_clip(v, -32768, 32767);   // colClampRange = 16 bits (8-bit video)
+        }
+    }
+    for (int j = 0; j < n; j++) {
+        for (int i = 0; i < n; i++) t[i] = r[i * n + j];
+        idct_1d(t, log2n);
+        for (int i = 0; i < n; i++) r[i * n + j] = (t[i] + 8) >> 4;
+    }
+}
+
+// Orthonormal DCT-II basis in Q13: K[k][m] = round(8192 * sqrt(2/N) * c_k * cos(pi*(2m+1)*k / 2N)).
+SK_HD int fdct_basis(int log2n, int k, int m) {
+    const int n = 1 << log2n;
+    // cos table at pi/64 resolution, Q14: cos(pi * i / 64), i = 0..64
+    constexpr int16_t c64[65] = {16384, 16364, 16305, 16207, 16069, 15893, 15679, 15426, 15137, 14811, 14449,
+                                 14053, 13623, 13160, 12665, 12140, 11585, 11003, 10394, 9760,  9102,  8423,
+                                 7723,  7005,  6270,  5520,  4756,  3981,  3196,  2404,  1606,  804,   0,
+                                 -804,  -1606, -2404, -3196, -3981, -4756, -5520, -6270, -7005, -7723, -8423,
+                                 -9102, -9760, -10394, -11003, -11585, -12140, -12665, -13160, -13623, -14053,
+                                 -14449, -14811, -15137, -15426, -15679, -15893, -16069, -16207, -16305, -16364,
+                                 -16384};
+    // angle = pi*(2m+1)*k / (2N) = pi * i / 64 with i = (2m+1)*k*(32/N); reduce modulo 128 (2 pi)
+    int i = ((2 * m + 1) * k * (32 >> log2n)) & 127;
+    int c = i <= 64 ? c64[i] : c64[128 - i];
+    // scale: sqrt(2/N) * c_k; Q14 cos -> Q13 basis
+    // sqrt(2/N): N=4 -> 0.70710678, N=8 -> 0.5, N=16 -> 0.35355339
+    int64_t v = (int64_t)c * (log2n == 2 ? 11585 : (log2n == 3 ? 8192 : 5793));   // Q14
+    if (k == 0) v = v * 11585 >> 14;   // c_0 = 1/sqrt(2)
+    (void)n;
+    return (int)((v + (1 << 14)) >> 15);   // Q14 * Q14 -> Q13
+}
+
+// Forward DCT_DCT: residual `x` (n x n raster) -> coefficients in AV1's domain
+// (8 x orthonormal), raster [row][col] with row = vertical frequency.
+SK_HD void fwd_transform(const int32_t* x, int log2n, int32_t* c) {
+    const int n = 1 << log2n;
+    int32_t t[256];
+    // columns: t[k][j] = sum_m K[k][m] x[m][j], kept at 8x (Q13 -> >> 10)
+    for (int k = 0; k < n; k++)
+        for (int j = 0; j < n; j++) {
+            int64_t s = 0;
+            for (int m = 0; m < n; m++) s += (int64_t)fdct_basis(log2n, k, m) * x[m * n + j];
+            t[k * n + j] = (int32_t)((s + 512) >> 10);
+        }
+    // rows: c[k][l] = sum_j t[k][j] K[l][j], Q13 -> >> 13
+    for (int k = 0; k < n; k++)
+        for (int l = 0; l < n; l++) {
+            int64_t s = 0;
+            for (int j = 0; j < n; j++) s += (int64_t)t[k * n + j] * fdct_basis(log2n, l, j);
+            c[k * n + l] = (int32_t)((s + (s >= 0 ? 4096 : 4095)) >> 13);
+        }
+}
+
+// ---------------------------------------------------------------------------------
+// Quantisation. AV1 dequantisation (§7.12.3) for 8-bit, no quantiser matrices,
+// dqDenom 0 (transforms up to 16x16).
+SK_HD int dc_q(int qidx) { return AV1_DC_QLOOKUP[sk_clip(qidx, 0, 255)]; }
+SK_HD int ac_q(int qidx) { return AV1_AC_QLOOKUP[sk_clip(qidx, 0, 255)]; }
+SK_HD int32_t dequant(int level, int q) {
+    const int a = level < 0 ? -level : level;
+    int32_t dq = (int32_t)(((int64_t)a * q) & 0xFFFFFF);
+    dq = level < 0 ? -dq : dq;
+    return sk_clip(dq, -(1 << 15), (1 << 15) - 1);
+}
+// Encoder quantiser: dead-zone rounding (intra 1/3, inter 1/6 of a step), level capped.
+SK_HD int quantize(int32_t c, int q, bool intra) {
+    const int a = c < 0 ? -c : c;
+    const int l = (int)(((int64_t)a * 6 + (intra ? 2 : 1) * q) / (6 * (int64_t)q));
+    const int lc = l > 4095 ? 4095 : l;
+    return c < 0 ? -lc : lc;
+}
+// qindex -> coefficient CDF context (§7.20: <= 20, <= 60, <= 120, else)
+SK_HD int coef_qctx(int qidx) { return qidx <= 20 ? 0 : (qidx <= 60 ? 1 : (qidx <= 120 ? 2 : 3)); }
+
+// ---------------------------------------------------------------------------------
+// Scans: the default (zig-zag) scan of an n x n DCT_DCT block, scan index -> raster position.
+// kScanTransposed selects the orientation of the zig-zag (spec Default_Scan_NxN walk:
+// odd anti-diagonals run down-left, even ones up-right, in raster [row][col]).
+constexpr int kScanTransposed = 0;
+SK_HD int default_scan(int log2n, int idx) {
+    const int n = 1 << log2n;
+    int d = 0, base = 0;
+    while (true) {
+        const int len = d < n ? d + 1 : 2 * n - 1 - d;
+        if (idx < base + len) break;
+        base += len;
+        d++;
+    }
+    const int k = idx - base;
+    const int row_first = d < n ? 0 : d - (n - 1), row_last = d < n ? d : n - 1;
+    const int row = ((d & 1) ^ kScanTransposed) ? row_first + k : row_last - k;
+    return row * n + (d - row);
+}
+
+// ---------------------------------------------------------------------------------
+// Intra prediction (§7.11.2) for DC / V / H (angle delta 0) / SMOOTH* / PAETH.
+// Edges: above[-1..n-1] and left[-1..n-1] per the spec's availability rules.
+struct IntraEdge {
+    uint8_t above[17];   // [0] = top-left, [1..n] = above row
+    uint8_t left[17];    // [0] = top-left, [1..n] = left column
+    bool have_above, have_left;
+};
+
+// plane: pointer to the reconstructed plane, (x, y) block origin, n block size,
+// max_x / max_y: last addressable column / row of the plane (MiCols*4 >> ss) - 1.
+SK_HD void intra_edges(const uint8_t* plane, int stride, int x, int y, int n, bool have_above, bool have_left,
+                       int max_x, int max_y, IntraEdge& e) {
+    e.have_above = have_above;
+    e.have_left = have_left;
+    for (int i = 0; i < n; i++) {
+        if (!have_above && have_left) e.above[1 + i] = plane[(size_t)y * stride + x - 1];
+        else if (!have_above) e.above[1 + i] = 127;
+        else e.above[1 + i] = plane[(size_t)(y - 1) * stride + sk_min(max_x, x + i)];
+        if (!have_left && have_above) e.left[1 + i] = plane[(size_t)(y - 1) * stride + x];
+        else if (!have_left) e.left[1 + i] = 129;
+        else e.left[1 + i] = plane[(size_t)sk_min(max_y, y + i) * stride + x - 1];
+    }
+    uint8_t tl;
+    if (have_above && have_left) tl = plane[(size_t)(y - 1) * stride + x - 1];
+    else if (have_above) tl = plane[(size_t)(y - 1) * stride + x];
+    else if (have_left) tl = plane[(size_t)y * stride + x - 1];
+    else tl = 128;
+    e.above[0] = e.left[0] = tl;
+}
+
+SK_HD int intra_pred_px(const IntraEdge& e, int mode, int log2n, int i /*row*/, int j /*col*/) {
+    const int n = 1 << log2n;
+    const uint8_t* A = e.above + 1;
+    const uint8_t* L = e.left + 1;
+    switch (mode) {
+        case V_PRED: return A[j];
+        case H_PRED: return L[i];
+        case SMOOTH_PRED: {
+            const int wy = AV1_SM_WEIGHTS[n + i], wx = AV1_SM_WEIGHTS[n + j];
+            const int s = wy * A[j] + (256 - wy) * L[n - 1] + wx * L[i] + (256 - wx) * A[n - 1];
+            return (s + 256) >> 9;
+        }
+        case SMOOTH_V_PRED: {
+            const int wy = AV1_SM_WEIGHTS[n + i];
+            return (wy * A[j] + (256 - wy) * L[n - 1] + 128) >> 8;
+        }
+        case SMOOTH_H_PRED: {
+            const int wx = AV1_SM_WEIGHTS[n + j];
+            return (wx * L[i] + (256 - wx) * A[n - 1] + 128) >> 8;
+        }
+        case PAETH_PRED: {
+            const int base = A[j] + L[i] - e.above[0];
+            const int pl = sk_abs(base - L[i]), pt = sk_abs(base - A[j]), ptl = sk_abs(base - e.above[0]);
+            if (pl <= pt && pl <= ptl) return L[i];
+            if (pt <= ptl) return A[j];
+            return e.above[0];
+        }
+        default: return -1;   // DC: see intra_dc
+    }
+}
+
+SK_HD int intra_dc(const IntraEdge& e, int log2n) {
+    const int n = 1 << log2n;
+    int s = 0;
+    if (e.have_above && e.have_left) {
+        for (int k = 0; k < n; k++) s += e.above[1 + k] + e.left[1 + k];
+        return (s + n) >> (log2n + 1);
+    }
+    if (e.have_above) {
+        for (int k = 0; k < n; k++) s += e.above[1 + k];
+        return (s + (n >> 1)) >> log2n;
+    }
+    if (e.have_left) {
+        for (int k = 0; k < n; k++) s += e.left[1 + k];
+        return (s + (n >> 1)) >> log2n;
+    }
+    return 128;
+}
+
+SK_HD void intra_predict(const IntraEdge& e, int mode, int log2n, uint8_t* pred) {
+    const int n = 1 << log2n;
+    if (mode == DC_PRED) {
+        const int dc = intra_dc(e, log2n);
+        for (int k = 0; k < n * n; k++) pred[k] = (uint8_t)dc;
+        return;
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) pred[i * n + j] = (uint8_t)intra_pred_px(e, mode, log2n, i, j);
+}
+
+SK_HD bool is_directional(int mode) { return mode >= V_PRED && mode <= D67_PRED; }
+
+// ---------------------------------------------------------------------------------
+// Inter prediction (§7.11.3.4, no scaling): EIGHTTAP regular, 4-tap variant for
+// blocks 4 wide/high. mv in 1/8 luma pel (row, col); positions clamp to the
+// reference frame's real size (last_x / last_y).
+SK_HD int subpel_tap(int filt4, int frac, int t) {
+    // Subpel_Filters[0] (regular 8-tap) and [4] (regular 4-tap), 1/16 positions
+    constexpr int16_t f8[16][8] = {
+        {0, 0, 0, 128, 0, 0, 0, 0},      {0, 2, -6, 126, 8, -2, 0, 0},    {0, 2, -10, 122, 18, -4, 0, 0},
+        {0, 2, -12, 116, 28, -8, 2, 0},  {0, 2, -14, 110, 38, -10, 2, 0}, {0, 2, -14, 102, 48, -12, 2, 0},
+        {0, 2, -16, 94, 58, -12, 2, 0},  {0, 2, -14, 84, 66, -12, 2, 0},  {0, 2, -14, 76, 76, -14, 2, 0},
+        {0, 2, -12, 66, 84, -14, 2, 0},  {0, 2, -12, 58, 94, -16, 2, 0},  {0, 2, -12, 48, 102, -14, 2, 0},
+        {0, 2, -10, 38, 110, -14, 2, 0}, {0, 2, -8, 28, 116, -12, 2, 0},  {0, 0, -4, 18, 122, -10, 2, 0},
+        {0, 0, -2, 8, 126, -6, 2, 0}};
+    constexpr int16_t f4[16][8] = {
+        {0, 0, 0, 128, 0, 0, 0, 0},     {0, 0, -4, 126, 8, -2, 0, 0},   {0, 0, -8, 122, 18, -4, 0, 0},
+        {0, 0, -10, 116, 28, -6, 0, 0}, {0, 0, -12, 110, 38, -8, 0, 0}, {0, 0, -12, 102, 48, -10, 0, 0},
+        {0, 0, -14, 94, 58, -10, 0, 0}, {0, 0, -12, 84, 66, -10, 0, 0}, {0, 0, -12, 76, 76, -12, 0, 0},
+        {0, 0, -10, 66, 84, -12, 0, 0}, {0, 0, -10, 58, 94, -14, 0, 0}, {0, 0, -10, 48, 102, -12, 0, 0},
+        {0, 0, -8, 38, 110, -12, 0, 0}, {0, 0, -6, 28, 116, -10, 0, 0}, {0, 0, -4, 18, 122, -8, 0, 0},
+        {0, 0, -2, 8, 126, -4, 0, 0}};
+    return filt4 ? f4[frac][t] : f8[frac][t];
+}
+
+// One w x h block of one plane. (x, y): block position in the plane; ss: chroma
+// subsampling shift (0 luma, 1 chroma); ref: reference plane.
+SK_HD void mc_block(const uint8_t* ref, int stride, int last_x, int last_y, int x, int y, int w, int h, int ss,
+                    int mv_row, int mv_col, uint8_t* pred, int pstride) {
+    // positions in 1/16 sample units of this plane
+    const int px16 = (x << 4) + ((2 * mv_col) >> ss);
+    const int py16 = (y << 4) + ((2 * mv_row) >> ss);
+    const int fx = px16 & 15, fy = py16 & 15;
+    const int ix = px16 >> 4, iy = py16 >> 4;
+    const int fh = w <= 4, fv = h <= 4;
+    if (fx == 0 && fy == 0) {   // exact copy (the filter at position 0 is the identity)
+        for (int r = 0; r < h; r++)
+            for (int c = 0; c < w; c++)
+                pred[r * pstride + c] = ref[(size_t)sk_clip(iy + r, 0, last_y) * stride + sk_clip(ix + c, 0, last_x)];
+        return;
+    }
+    int16_t im[(64 + 7) * 64];
+    const int ih = h + 7;
+    for (int r = 0; r < ih; r++) {
+        const uint8_t* row = ref + (size_t)sk_clip(iy + r - 3, 0, last_y) * stride;
+        for (int c = 0; c < w; c++) {
+            int s = 0;
+            for (int t = 0; t < 8; t++) s += subpel_tap(fh, fx, t) * row[sk_clip(ix + c + t - 3, 0, last_x)];
+            im[r * w + c] = (int16_t)((s + 4) >> 3);   // InterRound0 = 3
+        }
+    }
+    for (int r = 0; r < h; r++)
+        for (int c = 0; c < w; c++) {
+            int s = 0;
+            for (int t = 0; t < 8; t++) s += subpel_tap(fv, fy, t) * im[(r + t) * w + c];
+            pred[r * pstride + c] = (uint8_t)sk_clip255((s + 1024) >> 11);   // InterRound1 = 11
+        }
+}
+
+// ---------------------------------------------------------------------------------
+// Reference-MV stack (§7.10.2, single reference LAST, no temporal candidates,
+// identity global motion). The neighbour view is a function over mi positions.
+struct MvStack {
+    int n;                      // NumMvFound
+    int new_count;              // NewMvCount
+    int16_t mv[kMaxRefMvStack][2];   // RefStackMv[..][0] (row, col), clamped
+    int weight[kMaxRefMvStack];
+    int close_matches, total_matches;
+    int newmv_ctx, refmv_ctx;   // NewMvContext, RefMvContext (ZeroMvContext = 0)
+};
+
+// Grid: BlkInfo per 8x8 cell, row stride c8.
+struct BlkGrid {
+    const BlkInfo* b;
+    int c8;
+    SK_HD const BlkInfo& at(int mi_r, int mi_c) const { return b[(mi_r >> 1) * c8 + (mi_c >> 1)]; }
+};
+
+namespace detail {
+SK_HD void search_stack(MvStack& s, const BlkInfo& nb, int weight, bool& found) {
+    int16_t mv[2] = {nb.mv_row, nb.mv_col};
+    for (int i = 0; i < 2; i++)
+        if (mv[i] & 1) mv[i] += mv[i] > 0 ? -1 : 1;   // lower_mv_precision (no high precision)
+    if (nb.mode == NEWMV) s.new_count++;
+    found = true;
+    int idx = 0;
+    for (; idx < s.n; idx++)
+        if (s.mv[idx][0] == mv[0] && s.mv[idx][1] == mv[1]) break;
+    if (idx < s.n) {
+        s.weight[idx] += weight;
+    } else if (s.n < kMaxRefMvStack) {
+        s.mv[s.n][0] = mv[0];
+        s.mv[s.n][1] = mv[1];
+        s.weight[s.n] = weight;
+        s.n++;
+    }
+}
+SK_HD void add_candidate(MvStack& s, const BlkInfo& nb, int weight, bool& found) {
+    if (!blk_inter(nb)) return;
+    search_stack(s, nb, weight, found);   // RefFrames[..][0] == LAST for every inter block
+}
+SK_HD void scan_row(MvStack& s, const BlkGrid& g, const TileRect& t, int mi_rows, int mi_cols, int r, int c,
+                    int bw4, int delta_row, bool& found) {
+    int end4 = sk_min(sk_min(bw4, mi_cols - c), 16);
+    int delta_col = 0;
+    const bool step16 = bw4 >= 16;
+    if (sk_abs(delta_row) > 1) {
+        delta_row += r & 1;
+        delta_col = 1 - (c & 1);
+    }
+    int i = 0;
+    while (i < end4) {
+        const int mr = r + delta_row, mc = c + delta_col + i;
+        if (!inside(t, mr, mc)) break;
+        const BlkInfo& nb = g.at(mr, mc);
+        int len = sk_min(bw4, 1 << nb.bsl);
+        if (sk_abs(delta_row) > 1) len = sk_max(2, len);
+        if (step16) len = sk_max(4, len);
+        add_candidate(s, nb, len * 2, found);
+        i += len;
+    }
+    (void)mi_rows;
+}
+SK_HD void scan_col(MvStack& s, const BlkGrid& g, const TileRect& t, int mi_rows, int mi_cols, int r, int c,
+                    int bh4, int delta_col, bool& found) {
+    int end4 = sk_min(sk_min(bh4, mi_rows - r), 16);
+    int delta_row = 0;
+    const bool step16 = bh4 >= 16;
+    if (sk_abs(delta_col) > 1) {
+        delta_row = 1 - (r & 1);
+        delta_col += c & 1;
+    }
+    int i = 0;
+    while (i < end4) {
+        const int mr = r + delta_row + i, mc = c + delta_col;
+        if (!inside(t, mr, mc)) break;
+        const BlkInfo& nb = g.at(mr, mc);
+        int len = sk_min(bh4, 1 << nb.bsl);
+        if (sk_abs(delta_col) > 1) len = sk_max(2, len);
+        if (step16) len = sk_max(4, len);
+        add_candidate(s, nb, len * 2, found);
+        i += len;
+    }
+    (void)mi_cols;
+}
+}  // namespace detail
+
+// `decoded(mr, mc)`: whether the block covering mi (mr, mc) precedes the current
+// block in coding order (top-right candidate availability).
+template <class Decoded>
+SK_HD void find_mv_stack(MvStack& s, const BlkGrid& g, const TileRect& t, int mi_rows, int mi_cols, int r, int c,
+                         int bsl, const Decoded& decoded) {
+    using namespace detail;
+    const int bw4 = 1 << bsl, bh4 = bw4;
+    s.n = 0;
+    s.new_count = 0;
+    bool found = false;
+    scan_row(s, g, t, mi_rows, mi_cols, r, c, bw4, -1, found);
+    bool found_above = found;
+    found = false;
+    scan_col(s, g, t, mi_rows, mi_cols, r, c, bh4, -1, found);
+    bool found_left = found;
+    found = false;
+    if (sk_max(bw4, bh4) <= 16) {   // top-right
+        const int mr = r - 1, mc = c + bw4;
+        if (inside(t, mr, mc) && decoded(mr, mc)) add_candidate(s, g.at(mr, mc), 4, found);
+    }
+    if (found) found_above = true;
+    s.close_matches = (int)found_above + (int)found_left;
+    const int num_nearest = s.n, num_new = s.new_count;
+    for (int i = 0; i < num_nearest; i++) s.weight[i] += kRefCatLevel;
+    found = false;
+    {   // top-left
+        const int mr = r - 1, mc = c - 1;
+        if (inside(t, mr, mc) && decoded(mr, mc)) add_candidate(s, g.at(mr, mc), 4, found);
+    }
+    if (found) found_above = true;
+    found = false;
+    scan_row(s, g, t, mi_rows, mi_cols, r, c, bw4, -3, found);
+    if (found) found_above = true;
+    found = false;
+    scan_col(s, g, t, mi_rows, mi_cols, r, c, bh4, -3, found);
+    if (found) found_left = true;
+    found = false;
+    if (bh4 > 1) scan_row(s, g, t, mi_rows, mi_cols, r, c, bw4, -5, found);
+    if (found) found_above = true;
+    found = false;
+    if (bw4 > 1) scan_col(s, g, t, mi_rows, mi_cols, r, c, bh4, -5, found);
+    if (found) found_left = true;
+    s.total_matches = (int)found_above + (int)found_left;
+    // sorting (bubble, stable for equal weights) of [0, nearest) and [nearest, n)
+    for (int pass = 0; pass < 2; pass++) {
+        const int start = pass == 0 ? 0 : num_nearest;
+        int end = pass == 0 ? num_nearest : s.n;
+        while (end > start) {
+            int new_end = start;
+            for (int idx = start + 1; idx < end; idx++)
+                if (s.weight[idx - 1] < s.weight[idx]) {
+                    const int w = s.weight[idx - 1];
+                    s.weight[idx - 1] = s.weight[idx];
+                    s.weight[idx] = w;
+                    for (int k = 0; k < 2; k++) {
+                        const int16_t m = s.mv[idx - 1][k];
+                        s.mv[idx - 1][k] = s.mv[idx][k];
+                        s.mv[idx][k] = m;
+                    }
+                    new_end = idx;
+                }
+            end = new_end;
+        }
+    }
+    if (s.n < 2) {   // extra search
+        const int w4 = sk_min(sk_min(16, bw4), mi_cols - c), h4 = sk_min(sk_min(16, bh4), mi_rows - r);
+        const int num4x4 = sk_min(w4, h4);
+        for (int pass = 0; pass < 2 && s.n < 2; pass++) {
+            int idx = 0;
+            while (idx < num4x4 && s.n < 2) {
+                const int mr = pass == 0 ? r - 1 : r + idx, mc = pass == 0 ? c + idx : c - 1;
+                if (!inside(t, mr, mc)) break;
+                const BlkInfo& nb = g.at(mr, mc);
+                if (blk_inter(nb)) {   // add_extra_mv_candidate: same sign bias (single LAST)
+                    const int16_t mv0 = nb.mv_row, mv1 = nb.mv_col;
+                    int k = 0;
+                    for (; k < s.n; k++)
+                        if (s.mv[k][0] == mv0 && s.mv[k][1] == mv1) break;
+                    if (k == s.n) {
+                        s.mv[k][0] = mv0;
+                        s.mv[k][1] = mv1;
+                        s.weight[k] = 2;
+                        s.n++;
+                    }
+                }
+                idx += 1 << nb.bsl;
+            }
+        }
+        for (int k = s.n; k < 2; k++) {   // GlobalMvs[0] = 0
+            s.mv[k][0] = s.mv[k][1] = 0;
+            s.weight[k] = 0;
+        }
+    }
+    // context and clamping
+    const int top = -((r * 4) * 8), bottom = ((mi_rows - bh4 - r) * 4) * 8;
+    const int left = -((c * 4) * 8), right = ((mi_cols - bw4 - c) * 4) * 8;
+    for (int i = 0; i < s.n; i++) {
+        s.mv[i][0] = (int16_t)sk_clip(s.mv[i][0], top - (kMvBorder + bh4 * 32), bottom + kMvBorder + bh4 * 32);
+        s.mv[i][1] = (int16_t)sk_clip(s.mv[i][1], left - (kMvBorder + bw4 * 32), right + kMvBorder + bw4 * 32);
+    }
+    if (s.close_matches == 0) {
+        s.newmv_ctx = sk_min(s.total_matches, 1);
+        s.refmv_ctx = s.total_matches;
+    } else if (s.close_matches == 1) {
+        s.newmv_ctx = 3 - sk_min(num_new, 1);
+        s.refmv_ctx = 2 + s.total_matches;
+    } else {
+        s.newmv_ctx = 5 - sk_min(num_new, 1);
+        s.refmv_ctx = 5;
+    }
+}
+
+SK_HD int drl_ctx(const MvStack& s, int idx) {
+    if (s.weight[idx] >= kRefCatLevel && s.weight[idx + 1] >= kRefCatLevel) return 0;
+    if (s.weight[idx] >= kRefCatLevel && s.weight[idx + 1] < kRefCatLevel) return 1;
+    if (s.weight[idx] < kRefCatLevel && s.weight[idx + 1] < kRefCatLevel) return 2;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------
+// Symbol sinks. A sink offers sym(cdf offset in CdfContext u16 units, N, value),
+// bit(b) (an L(1) equiprobable bit) and lits(value, nbits).
+SK_HD int cdf_off(const CdfContext& base, const uint16_t* p) { return (int)(p - (const uint16_t*)&base); }
+
+// Direct coding: adaptive CDFs in `ctx`, coded by a SymbolCoder.
+template <class Coder>
+struct DirectSink {
+    Coder& coder;
+    CdfContext& ctx;
+    SK_HD void sym(int off, int n, int v) { coder.encode_adapt((uint16_t*)&ctx + off, n, v); }
+    SK_HD void bit(int b) { coder.bool_(b); }
+    SK_HD void lits(uint32_t v, int nbits) { coder.literal(v, nbits); }
+};
+
+// ---------------------------------------------------------------------------------
+// Coefficient syntax (§5.11.39 coeffs) of one transform block.
+// lev: quantised levels, raster [row][col]; txs: TX_4X4..TX_16X16 (square);
+// ctx_skip: all_zero context; ctx_dc: dc_sign context.
+// Returns cul_level | dc_category << 6 (the value the level contexts store).
+struct CoefCtx {
+    int txb_skip, dc_sign;
+};
+
+SK_HD int eob_pt_of(int eob) {
+    if (eob <= 2) return eob;
+    int l = 0;
+    while ((1 << (l + 1)) <= eob - 1) l++;   // floor(log2(eob - 1))
+    return l + 2;
+}
+
+template <class Sink>
+SK_HD int code_coeffs(Sink& w, const CdfContext& cx, const int16_t* lev, int txs, int plane, CoefCtx cc,
+                      bool is_inter, int intra_dir, int qidx) {
+    const int log2n = txs + 2, n = 1 << log2n, nn = n * n;
+    const int ptype = plane > 0;
+    // eob = 1 + last nonzero scan index
+    int eob = 0;
+    for (int c = nn - 1; c >= 0; c--)
+        if (lev[default_scan(log2n, c)] != 0) {
+            eob = c + 1;
+            break;
+        }
+    w.sym(cdf_off(cx, cx.txb_skip[txs][cc.txb_skip]), 2, eob == 0);
+    if (eob == 0) return 0;
+    if (plane == 0 && qidx > 0) {   // transform_type: DCT_DCT (index 1 of the reduced sets)
+        if (is_inter) w.sym(cdf_off(cx, cx.inter_tx_set3[txs]), 2, 1);
+        else w.sym(cdf_off(cx, cx.intra_tx_set2[txs][intra_dir]), 5, 1);
+    }
+    const int eob_multi = 2 * log2n - 4;   // log2(nn) - 4
+    const int eob_pt = eob_pt_of(eob);
+    switch (eob_multi) {
+        case 0: w.sym(cdf_off(cx, cx.eob_pt_16[ptype][0]), 5, eob_pt - 1); break;
+        case 2: w.sym(cdf_off(cx, cx.eob_pt_64[ptype][0]), 7, eob_pt - 1); break;
+        default: w.sym(cdf_off(cx, cx.eob_pt_256[ptype][0]), 9, eob_pt - 1); break;
+    }
+    if (eob_pt >= 3) {
+        const int off = eob - ((1 << (eob_pt - 2)) + 1);
+        const int sh = eob_pt - 3;
+        w.sym(cdf_off(cx, cx.eob_extra[txs][ptype][eob_pt - 3]), 2, (off >> sh) & 1);
+        for (int i = 1; i < eob_pt - 2; i++) w.bit((off >> (sh - i)) & 1);
+    }
+    // base levels + ranges, reverse scan; q holds min(level, 15) as the decoder sees it
+    int16_t q[256];
+    for (int i = 0; i < nn; i++) q[i] = 0;
+    for (int c = eob - 1; c >= 0; c--) {
+        const int pos = default_scan(log2n, c);
+        const int a = sk_abs(lev[pos]);
+        const int row = pos >> log2n, col = pos & (n - 1);
+        if (c == eob - 1) {
+            const int ctx = c == 0 ? 0 : (c <= nn / 8 ? 1 : (c <= nn / 4 ? 2 : 3));
+            w.sym(cdf_off(cx, cx.coeff_base_eob[txs][ptype][ctx]), 3, sk_min(a, 3) - 1);
+        } else {
+            int mag = 0;
+            const int8_t off[5][2] = {{0, 1}, {1, 0}, {1, 1}, {0, 2}, {2, 0}};
+            for (int k = 0; k < 5; k++) {
+                const int rr = row + off[k][0], cc2 = col + off[k][1];
+                if (rr < n && cc2 < n) mag += sk_min(q[(rr << log2n) + cc2], 3);
+            }
+            int ctx = sk_min((mag + 1) >> 1, 4);
+            if (row == 0 && col == 0) ctx = 0;
+            else {
+                const int rm = sk_min(row, 4), cm = sk_min(col, 4);
+                int o;
+                if (txs == TX_4X4) {
+                    constexpr uint8_t t4[5][5] = {{0, 1, 6, 6, 0}, {1, 6, 6, 21, 0}, {6, 6, 21, 21, 0},
+                                                  {6, 21, 21, 21, 0}, {0, 0, 0, 0, 0}};
+                    o = t4[rm][cm];
+                } else {
+                    constexpr uint8_t t8[5][5] = {{0, 1, 6, 6, 21}, {1, 6, 6, 21, 21}, {6, 6, 21, 21, 21},
+                                                  {6, 21, 21, 21, 21}, {21, 21, 21, 21, 21}};
+                    o = t8[rm][cm];
+                }
+                ctx += o;
+            }
+            w.sym(cdf_off(cx, cx.coeff_base[txs][ptype][ctx]), 4, sk_min(a, 3));
+        }
+        if (a > 2) {
+            int mag = 0;
+            const int8_t off[3][2] = {{0, 1}, {1, 0}, {1, 1}};
+            for (int k = 0; k < 3; k++) {
+                const int rr = row + off[k][0], cc2 = col + off[k][1];
+                if (rr < n && cc2 < n) mag += q[(rr << log2n) + cc2];
+            }
+            mag = sk_min((mag + 1) >> 1, 6);
+            const int ctx = pos == 0 ? mag : ((row < 2 && col < 2) ? mag + 7 : mag + 14);
+            int level = 3;
+            for (int idx = 0; idx < 4; idx++) {
+                const int br = sk_min(a - level, 3);
+                w.sym(cdf_off(cx, cx.coeff_br[sk_min(txs, TX_32X32)][ptype][ctx]), 4, br);
+                level += br;
+                if (br < 3) break;
+            }
+        }
+        q[pos] = (int16_t)sk_min(a, 15);
+    }
+    // signs and Golomb remainders, forward scan
+    int cul = 0, dcc = 0;
+    for (int c = 0; c < eob; c++) {
+        const int pos = default_scan(log2n, c);
+        const int l = lev[pos];
+        if (l == 0) continue;
+        const int a = sk_abs(l);
+        if (c == 0) w.sym(cdf_off(cx, cx.dc_sign[ptype][cc.dc_sign]), 2, l < 0);
+        else w.bit(l < 0);
+        if (a > 14) {
+            const uint32_t x = (uint32_t)(a - 14);
+            int len = 0;
+            while ((x >> len) > 1) len++;   // len = bit length - 1
+            for (int i = 0; i < len; i++) w.bit(0);
+            w.bit(1);
+            for (int i = len - 1; i >= 0; i--) w.bit((x >> i) & 1);
+        }
+        if (pos == 0) dcc = l < 0 ? 1 : 2;
+        cul += a;
+    }
+    return sk_min(cul, 63) | (dcc << 6);
+}
+
+// ---------------------------------------------------------------------------------
+// Motion vector syntax (§5.11.32 read_mv, MvCtx 0, no high precision).
+template <class Sink>
+SK_HD void code_mv_component(Sink& w, const CdfContext& cx, int comp, int v) {
+    const uint16_t* sign = comp ? cx.mv1_sign[0] : cx.mv0_sign[0];
+    const uint16_t* classes = comp ? cx.mv1_classes[0] : cx.mv0_classes[0];
+    w.sym(cdf_off(cx, sign), 2, v < 0);
+    const int mag = (v < 0 ? -v : v) - 1;   // ((d << 3) | (fr << 1) | hp), hp = 1
+    int cls = 0;
+    if (mag >= 16) {   // CLASS0_SIZE << 3 = 16
+        cls = 1;
+        while (mag >= (2 << (cls + 3))) cls++;
+    }
+    w.sym(cdf_off(cx, classes), 11, cls);
+    if (cls == 0) {
+        const int d = mag >> 3, fr = (mag >> 1) & 3;
+        w.sym(cdf_off(cx, comp ? cx.mv1_class0[0] : cx.mv0_class0[0]), 2, d);
+        w.sym(cdf_off(cx, comp ? cx.mv1_class0_fp[d] : cx.mv0_class0_fp[d]), 4, fr);
+    } else {
+        const int rem = mag - (2 << (cls + 2));
+        const int d = rem >> 3, fr = (rem >> 1) & 3;
+        for (int i = 0; i < cls; i++) w.sym(cdf_off(cx, comp ? cx.mv1_bits[i] : cx.mv0_bits[i]), 2, (d >> i) & 1);
+        w.sym(cdf_off(cx, comp ? cx.mv1_fp[0] : cx.mv0_fp[0]), 4, fr);
+    }
+}
+
+// diff: (row, col) in 1/8 pel, both even
+template <class Sink>
+SK_HD void code_mv(Sink& w, const CdfContext& cx, int drow, int dcol) {
+    const int joint = (drow != 0 ? 2 : 0) | (dcol != 0 ? 1 : 0);
+    w.sym(cdf_off(cx, cx.mv_joint[0]), 4, joint);
+    if (drow != 0) code_mv_component(w, cx, 0, drow);
+    if (dcol != 0) code_mv_component(w, cx, 1, dcol);
+}
+
+}  // namespace sk::av1

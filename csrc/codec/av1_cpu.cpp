@@ -1,0 +1,661 @@
+// CPU reference backend of the AV1 encoder: headers and OBUs, block decisions,
+// reconstruction and tile entropy coding. It is the golden model of the HIP back
+// end (kernels/av1_kernels.hip produces the same decisions, levels, reconstruction
+// and tile bytes) and the `use_cpu` path; dav1d decodes its output to exactly the
+// reconstruction kept here (tests/test_av1_encoder.py).
+#include "av1_encoder.h"
+#include <string.h>
+#include <algorithm>
+
+namespace sk {
+namespace av1 {
+
+using h264::ACT_I;
+using h264::ACT_NONE;
+using h264::ACT_P;
+using h264::ACT_SKIPALL;
+
+// ------------------------------------------------------------------------------ headers
+void put_leb128(std::vector<uint8_t>& out, uint64_t v) {
+    do {
+        uint8_t b = v & 0x7f;
+        v >>= 7;
+        if (v) b |= 0x80;
+        out.push_back(b);
+    } while (v);
+}
+
+void append_obu(std::vector<uint8_t>& out, int type, const uint8_t* payload, size_t n) {
+    out.push_back((uint8_t)((type << 3) | 2));   // obu_has_size_field
+    put_leb128(out, n);
+    out.insert(out.end(), payload, payload + n);
+}
+
+int choose_level_idx(int W, int H, float fps) {
+    const double ps = (double)W * H, sr = ps * (fps > 0 ? fps : 60.0);
+    struct L { int idx; double ps, sr; };
+    static const L levels[] = {{0, 147456, 4423680},       {1, 278784, 8363520},       {4, 665856, 19975680},
+                               {5, 1065024, 31950720},     {8, 2359296, 70778880},     {9, 2359296, 141557760},
+                               {12, 8912896, 267386880},   {13, 8912896, 534773760},   {14, 8912896, 1069547520},
+                               {16, 35651584, 1069547520}, {17, 35651584, 2139095040}, {18, 35651584, 4278190080.0}};
+    for (const L& l : levels)
+        if (ps <= l.ps && sr <= l.sr) return l.idx;
+    return 31;   // unconstrained
+}
+
+// H.264 QP -> AV1 qindex with the same quantiser step (orthonormal units:
+// H.264 0.625 * 2^(QP/6); AV1 Ac_Qlookup / 8).
+int qidx_for_qp(int qp) {
+    double step = 0.625;
+    for (int i = 0; i < qp; i++) step *= 1.122462048309373;   // 2^(1/6)
+    int best = 1;
+    double bd = 1e30;
+    for (int q = 1; q < 256; q++) {
+        const double d = AV1_AC_QLOOKUP[q] / 8.0 - step;
+        if ((d < 0 ? -d : d) < bd) {
+            bd = d < 0 ? -d : d;
+            best = q;
+        }
+    }
+    return best;
+}
+
+void write_sequence_header(BitWriter& w, int W, int H, int level_idx, int full_range) {
+    w.put(0, 3);   // seq_profile: Main
+    w.put(0, 1);   // still_picture
+    w.put(0, 1);   // reduced_still_picture_header
+    w.put(0, 1);   // timing_info_present_flag
+    w.put(0, 1);   // initial_display_delay_present_flag
+    w.put(0, 5);   // operating_points_cnt_minus_1
+    w.put(0, 12);  // operating_point_idc[0]
+    w.put((uint32_t)level_idx, 5);
+    if (level_idx > 7) w.put(0, 1);   // seq_tier: Main
+    int wb = 1, hb = 1;
+    while ((1 << wb) < W) wb++;
+    while ((1 << hb) < H) hb++;
+    w.put((uint32_t)(wb - 1), 4);
+    w.put((uint32_t)(hb - 1), 4);
+    w.put((uint32_t)(W - 1), wb);
+    w.put((uint32_t)(H - 1), hb);
+    w.put(0, 1);   // frame_id_numbers_present_flag
+    w.put(0, 1);   // use_128x128_superblock
+    w.put(0, 1);   // enable_filter_intra
+    w.put(0, 1);   // enable_intra_edge_filter
+    w.put(0, 1);   // enable_interintra_compound
+    w.put(0, 1);   // enable_masked_compound
+    w.put(0, 1);   // enable_warped_motion
+    w.put(0, 1);   // enable_dual_filter
+    w.put(0, 1);   // enable_order_hint
+    w.put(0, 1);   // seq_choose_screen_content_tools
+    w.put(0, 1);   // seq_force_screen_content_tools (-> seq_force_integer_mv = SELECT, not coded)
+    w.put(0, 1);   // enable_superres
+    w.put(0, 1);   // enable_cdef
+    w.put(0, 1);   // enable_restoration
+    // color_config
+    w.put(0, 1);   // high_bitdepth
+    w.put(0, 1);   // mono_chrome
+    w.put(1, 1);   // color_description_present_flag
+    w.put(1, 8);   // color_primaries BT.709
+    w.put(1, 8);   // transfer_characteristics BT.709
+    w.put(1, 8);   // matrix_coefficients BT.709
+    w.put(full_range ? 1 : 0, 1);   // color_range (h264_fullcolor)
+    w.put(0, 2);   // chroma_sample_position: unknown
+    w.put(0, 1);   // separate_uv_delta_q
+    w.put(0, 1);   // film_grain_params_present
+    w.trailing();
+}
+
+void write_frame_header(BitWriter& w, const Av1Geo& g, const FrameParams& fp) {
+    w.put(0, 1);                        // show_existing_frame
+    w.put(fp.key ? 0 : 1, 2);           // frame_type KEY / INTER
+    w.put(1, 1);                        // show_frame
+    if (!fp.key) w.put(0, 1);           // error_resilient_mode
+    w.put(0, 1);                        // disable_cdf_update
+    w.put(0, 1);                        // frame_size_override_flag
+    if (!fp.key) {
+        w.put(7, 3);                    // primary_ref_frame = PRIMARY_REF_NONE
+        w.put(0x01, 8);                 // refresh_frame_flags: slot 0 holds LAST
+        for (int i = 0; i < 7; i++) w.put(0, 3);   // ref_frame_idx[i] = 0
+        w.put(0, 1);                    // render_and_frame_size_different
+        w.put(0, 1);                    // allow_high_precision_mv
+        w.put(0, 1);                    // is_filter_switchable
+        w.put(0, 2);                    // interpolation_filter = EIGHTTAP
+        w.put(0, 1);                    // is_motion_mode_switchable
+    } else {
+        w.put(0, 1);                    // render_and_frame_size_different
+    }
+    w.put(1, 1);                        // disable_frame_end_update_cdf
+    // tile_info: uniform spacing
+    w.put(1, 1);
+    for (int k = g.min_log2_tile_cols; k < g.max_log2_tile_cols; k++) {
+        const int inc = k < g.tile_cols_log2;
+        w.put((uint32_t)inc, 1);
+        if (!inc) break;
+    }
+    const int min_log2_rows = sk_max(g.min_log2_tiles - g.tile_cols_log2, 0);
+    for (int k = min_log2_rows; k < g.max_log2_tile_rows; k++) {
+        const int inc = k < g.tile_rows_log2;
+        w.put((uint32_t)inc, 1);
+        if (!inc) break;
+    }
+    if (g.tile_cols_log2 > 0 || g.tile_rows_log2 > 0) {
+        w.put(0, g.tile_rows_log2 + g.tile_cols_log2);   // context_update_tile_id
+        w.put((uint32_t)(fp.tile_size_bytes - 1), 2);
+    }
+    // quantization_params
+    w.put((uint32_t)fp.qidx, 8);
+    w.put(0, 1);   // DeltaQYDc
+    w.put(0, 1);   // DeltaQUDc
+    w.put(0, 1);   // DeltaQUAc
+    w.put(0, 1);   // using_qmatrix
+    w.put(0, 1);   // segmentation_enabled
+    if (fp.qidx > 0) w.put(0, 1);   // delta_q_present
+    // loop_filter_params: levels 0 (off), sharpness 0, no deltas
+    w.put(0, 6);
+    w.put(0, 6);
+    w.put(0, 3);
+    w.put(0, 1);
+    w.put(0, 1);   // tx_mode_select = 0 -> TX_MODE_LARGEST
+    if (!fp.key) w.put(0, 1);   // reference_select
+    w.put(1, 1);   // reduced_tx_set
+    if (!fp.key)
+        for (int i = 0; i < 7; i++) w.put(0, 1);   // is_global[LAST..ALTREF]
+    w.align();     // byte_alignment() before the tile group (OBU_FRAME)
+}
+
+// ------------------------------------------------------------------------------ encoder
+CpuAv1Encoder::CpuAv1Encoder(const h264::EncoderConfig& cfg, int tcl, int trl) : fe(front_config(cfg)) {
+    const int W = fe.g.W, H = fe.g.H;
+    // tiles: as many as the level allows (the entropy coder's parallel axis), 16x16 SB max per tile side
+    const int sbc = (W + 63) / 64, sbr = (H + 63) / 64;
+    int want_c = tcl, want_r = trl;
+    if (want_c < 0) want_c = tile_log2(1, std::min(8, sbc));
+    if (want_r < 0) want_r = tile_log2(1, std::min(8, sbr));
+    geo_init(geo, W, H, want_c, want_r);
+    blk.assign((size_t)geo.c8 * geo.r8, BlkInfo{});
+    lev.assign((size_t)fe.g.mb_w * fe.g.mb_h * kLevPerUnit, 0);
+    lctx_w[0] = geo.mi_cols;
+    lctx_h[0] = geo.mi_rows;
+    lctx_w[1] = lctx_w[2] = geo.mi_cols >> 1;
+    lctx_h[1] = lctx_h[2] = geo.mi_rows >> 1;
+    for (int p = 0; p < 3; p++) lctx[p].assign((size_t)lctx_w[p] * lctx_h[p], 0);
+    level_idx = choose_level_idx(W, H, cfg.fps);
+}
+
+void CpuAv1Encoder::set_cells(int r, int c, int bsl, const BlkInfo& b) {
+    const int n8 = (1 << bsl) >> 1;
+    for (int y = 0; y < n8; y++)
+        for (int x = 0; x < n8; x++) {
+            const int ry = (r >> 1) + y, cx = (c >> 1) + x;
+            if (ry < geo.r8 && cx < geo.c8) blk[(size_t)ry * geo.c8 + cx] = b;
+        }
+}
+
+void CpuAv1Encoder::set_lctx(int plane, int x4, int y4, int n4, uint8_t v) {
+    for (int y = 0; y < n4; y++)
+        for (int x = 0; x < n4; x++)
+            if (y4 + y < lctx_h[plane] && x4 + x < lctx_w[plane])
+                lctx[plane][(size_t)(y4 + y) * lctx_w[plane] + x4 + x] = v;
+}
+
+int16_t* CpuAv1Encoder::unit_lev(int r, int c, int bsl, int plane) const {
+    const int ux = c >> 2, uy = r >> 2;
+    int16_t* u = const_cast<int16_t*>(&lev[((size_t)uy * fe.g.mb_w + ux) * kLevPerUnit]);
+    if (bsl >= 2) return u + (plane == 0 ? 0 : (plane == 1 ? 256 : 320));
+    const int k = ((r >> 1) & 1) * 2 + ((c >> 1) & 1);
+    return u + (plane == 0 ? 64 * k : (plane == 1 ? 256 + 16 * k : 320 + 16 * k));
+}
+
+static uint8_t level_summary(const int16_t* lv, int nn) {
+    int cul = 0;
+    for (int i = 0; i < nn; i++) cul += lv[i] < 0 ? -lv[i] : lv[i];
+    const int dc = lv[0] < 0 ? 1 : (lv[0] > 0 ? 2 : 0);
+    return (uint8_t)(sk_min(cul, 63) | (dc << 6));
+}
+
+// Residual of one n x n block of `plane` at (x, y): transform + quantise against
+// `pred`, reconstruct into fe.rec. Levels to `lv`; returns whether any is nonzero.
+static bool code_residual(const uint8_t* src, int sstride, const uint8_t* pred, int log2n, int qidx, bool intra,
+                          int16_t* lv, uint8_t* rec, int rstride) {
+    const int n = 1 << log2n, nn = n * n;
+    int32_t res[256], co[256], dq[256], rr[256];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) res[i * n + j] = (int)src[(size_t)i * sstride + j] - (int)pred[i * n + j];
+    fwd_transform(res, log2n, co);
+    const int qd = dc_q(qidx), qa = ac_q(qidx);
+    bool nz = false;
+    for (int k = 0; k < nn; k++) {
+        const int l = quantize(co[k], k == 0 ? qd : qa, intra);
+        lv[k] = (int16_t)l;
+        nz |= l != 0;
+        dq[k] = dequant(l, k == 0 ? qd : qa);
+    }
+    if (nz) {
+        inv_transform(dq, log2n, rr);
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) rec[(size_t)i * rstride + j] = (uint8_t)sk_clip255(pred[i * n + j] + rr[i * n + j]);
+    } else {
+        for (int i = 0; i < n; i++) memcpy(rec + (size_t)i * rstride, pred + i * n, (size_t)n);
+    }
+    return nz;
+}
+
+// Key frames: DC / V / H / SMOOTH / SMOOTH_V / SMOOTH_H / PAETH by SAD, per plane group.
+static const uint8_t kIntraCands[7] = {DC_PRED, V_PRED, H_PRED, SMOOTH_PRED, SMOOTH_V_PRED, SMOOTH_H_PRED, PAETH_PRED};
+
+void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
+    const h264::Geometry& g = fe.g;
+    const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+    BlkInfo b{};
+    b.bsl = (uint8_t)bsl;
+    const int log2n = bsl + 2, n = 1 << log2n;
+    // luma
+    IntraEdge ey;
+    const int x = c * 4, y = r * 4;
+    intra_edges(fe.rec[0].data(), g.stride_y, x, y, n, au, al, geo.mi_cols * 4 - 1, geo.mi_rows * 4 - 1, ey);
+    uint8_t pred[256], best_pred[256];
+    int best = DC_PRED, best_cost = 1 << 30;
+    for (int m : kIntraCands) {
+        intra_predict(ey, m, log2n, pred);
+        int sad = 0;
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) sad += sk_abs((int)fe.src[0][(size_t)(y + i) * g.stride_y + x + j] - pred[i * n + j]);
+        const int cost = sad + (m == DC_PRED ? 0 : n * 2);   // mode-bits bias
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = m;
+            memcpy(best_pred, pred, (size_t)n * n);
+        }
+    }
+    b.mode = (uint8_t)best;
+    int16_t* ly = unit_lev(r, c, bsl, 0);
+    bool nz = code_residual(&fe.src[0][(size_t)y * g.stride_y + x], g.stride_y, best_pred, log2n, fp.qidx, true, ly,
+                            &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
+    // chroma: UV_DC_PRED. Every other UV mode implies an ADST-family chroma transform
+    // (Mode_To_Txfm, §7.13.3 compute_tx_type); this encoder's transforms are DCT_DCT.
+    const int cl2 = log2n - 1, cn = n >> 1, cx = x >> 1, cy = y >> 1;
+    IntraEdge eu, ev;
+    intra_edges(fe.rec[1].data(), g.stride_c, cx, cy, cn, au, al, geo.mi_cols * 2 - 1, geo.mi_rows * 2 - 1, eu);
+    intra_edges(fe.rec[2].data(), g.stride_c, cx, cy, cn, au, al, geo.mi_cols * 2 - 1, geo.mi_rows * 2 - 1, ev);
+    uint8_t bu[64], bv[64];
+    intra_predict(eu, DC_PRED, cl2, bu);
+    intra_predict(ev, DC_PRED, cl2, bv);
+    const int bestc = DC_PRED;
+    b.uv_mode = (uint8_t)bestc;
+    int16_t* lu = unit_lev(r, c, bsl, 1);
+    int16_t* lvv = unit_lev(r, c, bsl, 2);
+    nz |= code_residual(&fe.src[1][(size_t)cy * g.stride_c + cx], g.stride_c, bu, cl2, fp.qidx, true, lu,
+                        &fe.rec[1][(size_t)cy * g.stride_c + cx], g.stride_c);
+    nz |= code_residual(&fe.src[2][(size_t)cy * g.stride_c + cx], g.stride_c, bv, cl2, fp.qidx, true, lvv,
+                        &fe.rec[2][(size_t)cy * g.stride_c + cx], g.stride_c);
+    b.flags = nz ? 0 : 2;
+    set_cells(r, c, bsl, b);
+    const int n4 = 1 << bsl;
+    set_lctx(0, c, r, n4, nz ? level_summary(ly, n * n) : 0);
+    set_lctx(1, c >> 1, r >> 1, n4 >> 1, nz ? level_summary(lu, cn * cn) : 0);
+    set_lctx(2, c >> 1, r >> 1, n4 >> 1, nz ? level_summary(lvv, cn * cn) : 0);
+}
+
+void CpuAv1Encoder::key_partition(int r, int c, int bsl, const TileRect& t) {
+    if (r >= geo.mi_rows || c >= geo.mi_cols) return;
+    const int half = (1 << bsl) >> 1;
+    const bool has_rows = r + half < geo.mi_rows, has_cols = c + half < geo.mi_cols;
+    if (bsl == 1 || (bsl == 2 && has_rows && has_cols)) {
+        intra_block(r, c, bsl, t);
+        return;
+    }
+    for (int q = 0; q < 4; q++) key_partition(r + (q >> 1) * half, c + (q & 1) * half, bsl - 1, t);
+}
+
+void CpuAv1Encoder::decide_key() {
+    for (int t = 0; t < geo.tile_cols * geo.tile_rows; t++) {
+        const TileRect tr = tile_rect(geo, t);
+        for (int r = tr.mi_row0; r < tr.mi_row1; r += 16)
+            for (int c = tr.mi_col0; c < tr.mi_col1; c += 16) key_partition(r, c, 4, tr);
+    }
+}
+
+// One motion-compensated block: prediction from fe.ref, residual, reconstruction.
+void CpuAv1Encoder::inter_block(int r, int c, int bsl, int mv_row, int mv_col) {
+    const h264::Geometry& g = fe.g;
+    const int log2n = bsl + 2, n = 1 << log2n, x = c * 4, y = r * 4;
+    uint8_t py[256], pu[64], pv[64];
+    mc_block(fe.ref[0].data(), g.stride_y, geo.W - 1, geo.H - 1, x, y, n, n, 0, mv_row, mv_col, py, n);
+    const int cn = n >> 1, cx = x >> 1, cy = y >> 1;
+    const int lxc = ((geo.W + 1) >> 1) - 1, lyc = ((geo.H + 1) >> 1) - 1;
+    mc_block(fe.ref[1].data(), g.stride_c, lxc, lyc, cx, cy, cn, cn, 1, mv_row, mv_col, pu, cn);
+    mc_block(fe.ref[2].data(), g.stride_c, lxc, lyc, cx, cy, cn, cn, 1, mv_row, mv_col, pv, cn);
+    int16_t* ly = unit_lev(r, c, bsl, 0);
+    int16_t* lu = unit_lev(r, c, bsl, 1);
+    int16_t* lvv = unit_lev(r, c, bsl, 2);
+    bool nz = code_residual(&fe.src[0][(size_t)y * g.stride_y + x], g.stride_y, py, log2n, fp.qidx, false, ly,
+                            &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
+    nz |= code_residual(&fe.src[1][(size_t)cy * g.stride_c + cx], g.stride_c, pu, log2n - 1, fp.qidx, false, lu,
+                        &fe.rec[1][(size_t)cy * g.stride_c + cx], g.stride_c);
+    nz |= code_residual(&fe.src[2][(size_t)cy * g.stride_c + cx], g.stride_c, pv, log2n - 1, fp.qidx, false, lvv,
+                        &fe.rec[2][(size_t)cy * g.stride_c + cx], g.stride_c);
+    BlkInfo b{};
+    b.bsl = (uint8_t)bsl;
+    b.flags = (uint8_t)(1 | (nz ? 0 : 2));
+    b.mv_row = (int16_t)mv_row;
+    b.mv_col = (int16_t)mv_col;
+    b.mode = GLOBALMV;
+    set_cells(r, c, bsl, b);
+    const int n4 = 1 << bsl;
+    set_lctx(0, c, r, n4, nz ? level_summary(ly, n * n) : 0);
+    set_lctx(1, c >> 1, r >> 1, n4 >> 1, nz ? level_summary(lu, cn * cn) : 0);
+    set_lctx(2, c >> 1, r >> 1, n4 >> 1, nz ? level_summary(lvv, cn * cn) : 0);
+}
+
+void CpuAv1Encoder::inter_unit(int ux, int uy, int mv_row, int mv_col) {
+    const int r = uy * 4, c = ux * 4;
+    if (r >= geo.mi_rows || c >= geo.mi_cols) return;
+    if (r + 2 < geo.mi_rows && c + 2 < geo.mi_cols) {
+        inter_block(r, c, 2, mv_row, mv_col);
+        return;
+    }
+    for (int q = 0; q < 4; q++) {
+        const int rr = r + (q >> 1) * 2, cc = c + (q & 1) * 2;
+        if (rr < geo.mi_rows && cc < geo.mi_cols) inter_block(rr, cc, 1, mv_row, mv_col);
+    }
+}
+
+void CpuAv1Encoder::decide_inter() {
+    const h264::Geometry& g = fe.g;
+    for (int s = 0; s < g.num_slices; s++) {
+        const h264::SliceTask& t = fe.tasks[s];
+        for (int uy = t.first_row; uy < t.first_row + t.num_rows; uy++)
+            for (int ux = 0; ux < g.mb_w; ux++) {
+                const h264::MeResult& m = fe.me[(size_t)uy * g.mb_w + ux];
+                const bool moving = t.final_action == ACT_P;
+                inter_unit(ux, uy, moving ? 8 * m.mvy : 0, moving ? 8 * m.mvx : 0);
+            }
+    }
+    // static merging: 32x32 then 64x64 blocks whose cells are all skipped with one vector
+    for (int lvl = 3; lvl <= 4; lvl++) {
+        const int sz = 1 << lvl, half = sz >> 1;
+        for (int r = 0; r < geo.mi_rows; r += sz)
+            for (int c = 0; c < geo.mi_cols; c += sz) {
+                if (!(r + half < geo.mi_rows && c + half < geo.mi_cols)) continue;
+                const BlkInfo& b0 = blk[(size_t)(r >> 1) * geo.c8 + (c >> 1)];
+                bool ok = true;
+                for (int y = r >> 1; ok && y < std::min((r + sz) >> 1, geo.r8); y++)
+                    for (int x = c >> 1; ok && x < std::min((c + sz) >> 1, geo.c8); x++) {
+                        const BlkInfo& b = blk[(size_t)y * geo.c8 + x];
+                        ok = blk_skip(b) && b.mv_row == b0.mv_row && b.mv_col == b0.mv_col;
+                    }
+                if (!ok) continue;
+                BlkInfo m = b0;
+                m.bsl = (uint8_t)lvl;
+                set_cells(r, c, lvl, m);
+            }
+    }
+}
+
+// Pass A: each inter block's mode from its MV stack (the stack depends on the
+// neighbours' vectors only, so every block can be decided independently).
+void CpuAv1Encoder::decide_modes() {
+    const BlkGrid grid{blk.data(), geo.c8};
+    for (int t = 0; t < geo.tile_cols * geo.tile_rows; t++) {
+        const TileRect tr = tile_rect(geo, t);
+        for (int y8 = tr.mi_row0 >> 1; y8 < (tr.mi_row1 + 1) >> 1; y8++)
+            for (int x8 = tr.mi_col0 >> 1; x8 < (tr.mi_col1 + 1) >> 1; x8++) {
+                BlkInfo& b = blk[(size_t)y8 * geo.c8 + x8];
+                const int n8 = (1 << b.bsl) >> 1;
+                if (!blk_inter(b) || (y8 & (n8 - 1)) || (x8 & (n8 - 1))) continue;   // block origin cells only
+                const int r = y8 * 2, c = x8 * 2;
+                MvStack s;
+                find_mv_stack(s, grid, tr, geo.mi_rows, geo.mi_cols, r, c, b.bsl,
+                              [&](int mr, int mc) { return decoded_before(mr, mc, r, c); });
+                int mode, idx = 0;
+                if (b.mv_row == 0 && b.mv_col == 0) mode = GLOBALMV;
+                else if (b.mv_row == s.mv[0][0] && b.mv_col == s.mv[0][1]) mode = NEARESTMV;
+                else if (s.n >= 2 && b.mv_row == s.mv[1][0] && b.mv_col == s.mv[1][1]) {
+                    mode = NEARMV;
+                    idx = 1;
+                } else mode = NEWMV;
+                BlkInfo m = b;
+                m.mode = (uint8_t)mode;
+                m.flags = (uint8_t)((m.flags & 0x0f) | (idx << 4));
+                set_cells(r, c, b.bsl, m);
+            }
+    }
+}
+
+// ------------------------------------------------------------------------------ tile coding
+namespace {
+struct TileCoder {
+    const CpuAv1Encoder& e;
+    const TileRect& t;
+    CdfContext cx;
+    SymbolEncoder enc;
+    struct Direct {
+        TileCoder& tc;
+        void sym(int off, int n, int v) { tc.enc.encode_adapt((uint16_t*)&tc.cx + off, n, v); }
+        void bit(int b) { tc.enc.bool_(b); }
+        void lits(uint32_t v, int nb) { tc.enc.literal(v, nb); }
+    };
+    Direct w{*this};
+    BlkGrid grid;
+
+    TileCoder(const CpuAv1Encoder& en, const TileRect& tr) : e(en), t(tr), cx(AV1_DEFAULT_CDF[coef_qctx(en.fp.qidx)]) {
+        grid = BlkGrid{e.blk.data(), e.geo.c8};
+    }
+    const BlkInfo& at(int r, int c) const { return grid.at(r, c); }
+
+    uint8_t lc(int plane, int x4, int y4) const {
+        return e.lctx[plane][(size_t)y4 * e.lctx_w[plane] + x4];
+    }
+    // above / left level contexts of a tx block (plane units of 4 samples), tile-bounded
+    CoefCtx coef_ctx(int plane, int x4, int y4, int n4) const {
+        const int ss = plane ? 1 : 0;
+        const int row0 = t.mi_row0 >> ss, col0 = t.mi_col0 >> ss;
+        const int max_x4 = e.geo.mi_cols >> ss, max_y4 = e.geo.mi_rows >> ss;
+        int above = 0, left = 0, dcs = 0;
+        static const int sgn[3] = {0, -1, 1};
+        if (y4 - 1 >= row0)
+            for (int k = 0; k < n4; k++)
+                if (x4 + k < max_x4) {
+                    const uint8_t v = lc(plane, x4 + k, y4 - 1);
+                    above |= v;
+                    dcs += sgn[v >> 6];
+                }
+        if (x4 - 1 >= col0)
+            for (int k = 0; k < n4; k++)
+                if (y4 + k < max_y4) {
+                    const uint8_t v = lc(plane, x4 - 1, y4 + k);
+                    left |= v;
+                    dcs += sgn[v >> 6];
+                }
+        CoefCtx cc;
+        cc.txb_skip = plane == 0 ? 0 : 7 + (above != 0) + (left != 0);
+        cc.dc_sign = dcs < 0 ? 1 : (dcs > 0 ? 2 : 0);
+        return cc;
+    }
+
+    void residual(int r, int c, const BlkInfo& b) {
+        const int bsl = b.bsl;
+        const int16_t* ly = e.unit_lev(r, c, bsl, 0);
+        code_coeffs(w, cx, ly, bsl, 0, coef_ctx(0, c, r, 1 << bsl), blk_inter(b), b.mode, e.fp.qidx);
+        for (int p = 1; p < 3; p++)
+            code_coeffs(w, cx, e.unit_lev(r, c, bsl, p), bsl - 1, p, coef_ctx(p, c >> 1, r >> 1, (1 << bsl) >> 1),
+                        blk_inter(b), b.mode, e.fp.qidx);
+    }
+
+    void block(int r, int c, int bsl) {
+        const BlkInfo& b = at(r, c);
+        const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+        const int sctx = (au ? blk_skip(at(r - 1, c)) : 0) + (al ? blk_skip(at(r, c - 1)) : 0);
+        w.sym(cdf_off(cx, cx.skip[sctx]), 2, blk_skip(b));
+        if (e.fp.key) {
+            const int am = au ? at(r - 1, c).mode : DC_PRED, lm = al ? at(r, c - 1).mode : DC_PRED;
+            w.sym(cdf_off(cx, cx.kf_y_mode[intra_mode_ctx(am)][intra_mode_ctx(lm)]), 13, b.mode);
+            if (is_directional(b.mode)) w.sym(cdf_off(cx, cx.angle_delta[b.mode - V_PRED]), 7, 3);
+            if (bsl <= 3) w.sym(cdf_off(cx, cx.uv_mode_cfl_allowed[b.mode]), 14, b.uv_mode);
+            else w.sym(cdf_off(cx, cx.uv_mode_cfl_not_allowed[b.mode]), 13, b.uv_mode);
+            if (is_directional(b.uv_mode)) w.sym(cdf_off(cx, cx.angle_delta[b.uv_mode - V_PRED]), 7, 3);
+        } else {
+            // is_inter: every block of an inter frame is inter, so no neighbour is intra (ctx 0)
+            w.sym(cdf_off(cx, cx.intra_inter[0]), 2, 1);
+            const int nref = (au ? 1 : 0) + (al ? 1 : 0);
+            const int rctx = nref == 0 ? 1 : 2;
+            w.sym(cdf_off(cx, cx.single_ref[rctx][0]), 2, 0);   // single_ref_p1: forward
+            w.sym(cdf_off(cx, cx.single_ref[rctx][2]), 2, 0);   // p3: LAST / LAST2
+            w.sym(cdf_off(cx, cx.single_ref[rctx][3]), 2, 0);   // p4: LAST
+            MvStack s;
+            find_mv_stack(s, grid, t, e.geo.mi_rows, e.geo.mi_cols, r, c, bsl,
+                          [&](int mr, int mc) { return decoded_before(mr, mc, r, c); });
+            const int mode = b.mode, idx = (b.flags >> 4) & 3;
+            w.sym(cdf_off(cx, cx.newmv[s.newmv_ctx]), 2, mode != NEWMV);
+            if (mode != NEWMV) {
+                w.sym(cdf_off(cx, cx.zeromv[0]), 2, mode != GLOBALMV);
+                if (mode != GLOBALMV) w.sym(cdf_off(cx, cx.refmv[s.refmv_ctx]), 2, mode != NEARESTMV);
+            }
+            if (mode == NEWMV) {
+                for (int k = 0; k < 2; k++)
+                    if (s.n > k + 1) {
+                        w.sym(cdf_off(cx, cx.drl[drl_ctx(s, k)]), 2, idx != k);
+                        if (idx == k) break;
+                    }
+            } else if (mode == NEARMV) {
+                for (int k = 1; k < 3; k++)
+                    if (s.n > k + 1) {
+                        w.sym(cdf_off(cx, cx.drl[drl_ctx(s, k)]), 2, idx != k);
+                        if (idx == k) break;
+                    }
+            }
+            if (mode == NEWMV) {
+                const int pos = s.n <= 1 ? 0 : idx;
+                code_mv(w, cx, b.mv_row - s.mv[pos][0], b.mv_col - s.mv[pos][1]);
+            }
+        }
+        if (!blk_skip(b)) residual(r, c, b);
+    }
+
+    void partition(int r, int c, int bsl) {
+        if (r >= e.geo.mi_rows || c >= e.geo.mi_cols) return;
+        const int half = (1 << bsl) >> 1;
+        const bool has_rows = r + half < e.geo.mi_rows, has_cols = c + half < e.geo.mi_cols;
+        const int part = at(r, c).bsl == bsl ? PARTITION_NONE : PARTITION_SPLIT;
+        const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+        const int actx = au && at(r - 1, c).bsl < bsl, lctx2 = al && at(r, c - 1).bsl < bsl;
+        const int ctx = lctx2 * 2 + actx;
+        const uint16_t* pc = bsl == 1 ? cx.partition_w8[ctx]
+                             : bsl == 2 ? cx.partition_w16[ctx]
+                             : bsl == 3 ? cx.partition_w32[ctx]
+                                        : cx.partition_w64[ctx];
+        const int np = bsl == 1 ? 4 : 10;
+        if (has_rows && has_cols) {
+            w.sym(cdf_off(cx, pc), np, part);
+        } else if (has_cols || has_rows) {
+            // split_or_horz / split_or_vert: a bool with a CDF gathered from the partition CDF
+            auto P = [&](int k) { return (int)pc[k] - (k > 0 ? (int)pc[k - 1] : 0); };
+            int psum;
+            if (has_cols)   // bottom half outside: SPLIT vs HORZ
+                psum = P(PARTITION_VERT) + P(PARTITION_SPLIT) + P(PARTITION_HORZ_A) + P(PARTITION_VERT_A) +
+                       P(PARTITION_VERT_B) + P(PARTITION_VERT_4);
+            else            // right half outside: SPLIT vs VERT
+                psum = P(PARTITION_HORZ) + P(PARTITION_SPLIT) + P(PARTITION_HORZ_A) + P(PARTITION_HORZ_B) +
+                       P(PARTITION_VERT_A) + P(PARTITION_HORZ_4);
+            const uint16_t bc[3] = {(uint16_t)(32768 - psum), 32768, 0};
+            enc.encode(bc, 2, 1);
+        }
+        if (part == PARTITION_NONE && (has_rows && has_cols)) {
+            block(r, c, bsl);
+            return;
+        }
+        for (int q = 0; q < 4; q++) partition(r + (q >> 1) * half, c + (q & 1) * half, bsl - 1);
+    }
+};
+}  // namespace
+
+std::vector<uint8_t> CpuAv1Encoder::code_tile(int t) {
+    const TileRect tr = tile_rect(geo, t);
+    TileCoder tc(*this, tr);
+    for (int r = tr.mi_row0; r < tr.mi_row1; r += 16)
+        for (int c = tr.mi_col0; c < tr.mi_col1; c += 16) tc.partition(r, c, 4);
+    return tc.enc.finish();
+}
+
+std::vector<uint8_t> CpuAv1Encoder::assemble(const std::vector<std::vector<uint8_t>>& tiles) {
+    size_t maxsz = 1;
+    for (size_t i = 0; i + 1 < tiles.size(); i++) maxsz = std::max(maxsz, tiles[i].size());
+    fp.tile_size_bytes = maxsz <= 0x100 ? 1 : (maxsz <= 0x10000 ? 2 : (maxsz <= 0x1000000 ? 3 : 4));
+    std::vector<uint8_t> out;
+    append_obu(out, 2, nullptr, 0);   // temporal delimiter
+    if (fp.key) {
+        BitWriter sh;
+        write_sequence_header(sh, geo.W, geo.H, level_idx, fe.cfg.full_range);
+        append_obu(out, 1, sh.buf.data(), sh.buf.size());
+    }
+    BitWriter fh;
+    write_frame_header(fh, geo, fp);
+    std::vector<uint8_t> payload = fh.buf;
+    const int nt = (int)tiles.size();
+    if (nt > 1) payload.push_back(0);   // tile_start_and_end_present_flag = 0 + byte_alignment
+    for (int i = 0; i < nt; i++) {
+        if (i + 1 < nt) {
+            const uint32_t sz = (uint32_t)tiles[i].size() - 1;
+            for (int k = 0; k < fp.tile_size_bytes; k++) payload.push_back((uint8_t)(sz >> (8 * k)));
+        }
+        payload.insert(payload.end(), tiles[i].begin(), tiles[i].end());
+    }
+    append_obu(out, 6, payload.data(), payload.size());   // OBU_FRAME
+    return out;
+}
+
+void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, std::vector<h264::EncodedPacket>& out) {
+    fe.load_frame(bgrx, stride);
+    fe.ctl_.plan(fe.stripe_dirty.data(), fe.tasks.data());
+    const int ns = fe.g.num_slices;
+    bool key = false;
+    for (int s = 0; s < ns; s++) {
+        h264::SliceTask& t = fe.tasks[s];
+        t.final_action = t.action;
+        if (t.action == ACT_P) {
+            fe.motion_search(s);
+            fe.decide_scenecut(s);
+        }
+        key |= t.final_action == ACT_I;
+    }
+    if (key)   // AV1 has no intra slices: a key frame refreshes the whole picture
+        for (int s = 0; s < ns; s++) fe.tasks[s].final_action = ACT_I;
+    fp.key = key;
+    fp.qidx = qidx_for_qp(fe.tasks[0].qp);
+    std::fill(blk.begin(), blk.end(), BlkInfo{});
+    if (key) {
+        decide_key();
+    } else {
+        decide_inter();
+        decide_modes();
+    }
+    std::vector<std::vector<uint8_t>> tiles(geo.tile_cols * geo.tile_rows);
+    for (int t = 0; t < (int)tiles.size(); t++) tiles[t] = code_tile(t);
+    h264::EncodedPacket pk;
+    pk.y = 0;
+    pk.w = fe.g.W;
+    pk.h = fe.g.H;
+    pk.key = key;
+    pk.data.resize(10);
+    h264::write_stripe_header(pk.data.data(), key, frame_id, 0, fe.g.W, fe.g.H);
+    std::vector<uint8_t> tu = assemble(tiles);
+    pk.data.insert(pk.data.end(), tu.begin(), tu.end());
+    out.push_back(std::move(pk));
+    // every row of the picture was coded: the reconstruction is the next reference
+    for (int s = 0; s < ns; s++)
+        if (fe.tasks[s].final_action == ACT_NONE || fe.tasks[s].final_action == ACT_SKIPALL)
+            fe.tasks[s].final_action = ACT_P;
+    // rows past the picture bottom repeat the last row (what AV1's reference clamp reads)
+    const h264::Geometry& g = fe.g;
+    for (int y = geo.H; y < g.plane_h_y; y++)
+        memcpy(&fe.rec[0][(size_t)y * g.stride_y], &fe.rec[0][(size_t)(geo.H - 1) * g.stride_y], g.stride_y);
+    const int hc = (geo.H + 1) >> 1;
+    for (int p = 1; p < 3; p++)
+        for (int y = hc; y < g.plane_h_c; y++)
+            memcpy(&fe.rec[p][(size_t)y * g.stride_c], &fe.rec[p][(size_t)(hc - 1) * g.stride_c], g.stride_c);
+    fe.finish_frame();
+    frames++;
+}
+
+}  // namespace av1
+}  // namespace sk

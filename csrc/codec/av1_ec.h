@@ -24,7 +24,7 @@ constexpr int kProbShift = 6;   // EC_PROB_SHIFT
 constexpr int kMinProb = 4;     // EC_MIN_PROB
 
 // Spec update_cdf (8.2.7 / 4.10.x): adapt towards the coded symbol.
-SK_HD inline void update_cdf(uint16_t* cdf, int n, int symbol) {
+SK_HD void update_cdf(uint16_t* cdf, int n, int symbol) {
     const int cnt = cdf[n];
     const int rate = 3 + (cnt > 15) + (cnt > 31) + (n > 3 ? 2 : (n > 1 ? 1 : 0));   // Min(FloorLog2(N), 2)
     for (int i = 0; i < n - 1; i++) {
@@ -123,7 +123,7 @@ private:
 };
 
 // Settled chunks (9 bits: byte + carry) -> bytes, carries propagated backwards.
-SK_HD inline void carry_bytes(const uint16_t* chunks, int n, uint8_t* out) {
+SK_HD void carry_bytes(const uint16_t* chunks, int n, uint8_t* out) {
     uint32_t carry = 0;
     for (int i = n - 1; i >= 0; i--) {
         carry += chunks[i];

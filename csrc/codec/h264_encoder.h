@@ -44,7 +44,9 @@ struct EncoderConfig {
                                  // previous-but-one picture as a second P reference (blinking/toggling UI)
     int src_width = 0;           // K2: capture size when it differs from width x height (0 = same);
     int src_height = 0;          //     the frame is resampled (bilinear) inside the K1 conversion
-    int codec = 0;               // 0 = H.264, 1 = HEVC (hevc_encoder.h: same front end, full frame)
+    int codec = 0;               // 0 = H.264, 1 = HEVC (hevc_encoder.h: same front end, full frame), 2 = AV1
+    int tile_cols_log2 = -1;     // AV1 tiles (av1_encoder.h): -1 = automatic
+    int tile_rows_log2 = -1;
     int aq_strength = 0;         // MB-level adaptive QP strength, Q4 (16 = 1.0; 0 = off): h264_mb.h aq_offset
     int subpel = 1;              // H.264 quarter-pel refinement of P vectors (K4c); HEVC keeps integer vectors
     int intra4x4 = 0;            // H.264 I slices may code MBs as I_NxN (nine 4x4 modes) where cheaper; off

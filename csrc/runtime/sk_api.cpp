@@ -3,6 +3,7 @@
 #include "sk_api.h"
 #include "encoder_iface.h"
 #include "../codec/hevc_encoder.h"
+#include "../codec/av1_encoder.h"
 #include <hip/hip_runtime_api.h>
 #include <string.h>
 #include <string>
@@ -148,6 +149,50 @@ class CpuHevcBackend : public EncoderBackend {
     hevc::CpuHevcEncoder enc_;
 };
 
+class CpuAv1Backend : public EncoderBackend {
+   public:
+    explicit CpuAv1Backend(const h264::EncoderConfig& c) : enc_(c, c.tile_cols_log2, c.tile_rows_log2) {}
+    void request_keyframe() override { enc_.request_keyframe(); }
+    void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
+    int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) override {
+        enc_.fe.set_overlay_image(slot, bgra, w, h);
+        return 0;
+    }
+    int set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy) override {
+        enc_.fe.set_overlay_pos(slot, on, x, y, tdx, tdy);
+        return 0;
+    }
+    int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
+        packets_.clear();
+        enc_.encode(bgrx, stride, frame_id, packets_);
+        return (int)packets_.size();
+    }
+    int64_t debug_buffer(const char* name, void* dst, int64_t cap) override {
+        const void* p = nullptr;
+        int64_t n = 0;
+        std::string s(name);
+        auto plane = [&](const std::vector<uint8_t>& v) { p = v.data(); n = (int64_t)v.size(); };
+        if (s == "src_y") plane(enc_.fe.prev[0]);
+        else if (s == "src_u") plane(enc_.fe.prev[1]);
+        else if (s == "src_v") plane(enc_.fe.prev[2]);
+        else if (s == "ref_y") plane(enc_.fe.ref[0]);
+        else if (s == "ref_u") plane(enc_.fe.ref[1]);
+        else if (s == "ref_v") plane(enc_.fe.ref[2]);
+        else if (s == "blk") { p = enc_.blk.data(); n = (int64_t)(enc_.blk.size() * sizeof(av1::BlkInfo)); }
+        else if (s == "levels") { p = enc_.lev.data(); n = (int64_t)(enc_.lev.size() * 2); }
+        else if (s == "me") { p = enc_.fe.me.data(); n = (int64_t)(enc_.fe.me.size() * sizeof(h264::MeResult)); }
+        else if (s == "tasks") { p = enc_.fe.tasks.data(); n = (int64_t)(enc_.fe.tasks.size() * sizeof(h264::SliceTask)); }
+        else if (s == "av1_geo") { p = &enc_.geo; n = (int64_t)sizeof(av1::Av1Geo); }
+        else if (s == "av1_qidx") { p = &enc_.fp.qidx; n = 4; }
+        else return -1;
+        if (dst && cap >= n) memcpy(dst, p, (size_t)n);
+        return n;
+    }
+
+   private:
+    av1::CpuAv1Encoder enc_;
+};
+
 class CpuJpegBackend : public EncoderBackend {
    public:
     explicit CpuJpegBackend(const jpeg::JpegConfig& c) : enc_(c) {}
@@ -169,6 +214,7 @@ EncoderBackend* create_cpu_jpeg_backend(const jpeg::JpegConfig& c) { return new 
 
 EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c) {
     if (c.codec == 1) return new CpuHevcBackend(c);
+    if (c.codec == 2) return new CpuAv1Backend(c);
     return new CpuBackend(c);
 }
 
@@ -197,11 +243,13 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.src_width = c->src_width > 0 ? c->src_width : 0;
     e.src_height = c->src_height > 0 ? c->src_height : 0;
     e.num_refs = c->num_refs > 1 ? 2 : 1;
-    e.codec = c->codec == 1 ? 1 : 0;
+    e.codec = (c->codec == 1 || c->codec == 2) ? c->codec : 0;
+    e.tile_cols_log2 = c->tile_cols_log2;
+    e.tile_rows_log2 = c->tile_rows_log2;
     e.aq_strength = c->aq_strength > 0 ? (c->aq_strength > 64 ? 64 : c->aq_strength) : 0;
     e.subpel = c->subpel >= 0 ? 1 : 0;
     e.intra4x4 = c->intra4x4 > 0 ? 1 : 0;
-    if (e.codec == 1) {   // HEVC: full-frame pictures, slices of whole CTB rows, one reference
+    if (e.codec >= 1) {   // HEVC / AV1: full-frame pictures, slices of whole CTB rows, one reference
         e.aq_strength = 0;   // no cu_qp_delta in this HEVC profile setup
         e.fullframe = 1;
         e.num_refs = 1;

@@ -20,10 +20,13 @@ typedef struct sk_h264_config {
     int32_t shared_copy;  // > 0: H2D on the device's shared copy stream (bands of one frame)
     int32_t src_width, src_height;  // capture size if it differs (K2 resample in K1); 0 = width/height
     int32_t num_refs;               // reference pictures (sliding-window DPB): 0/1 = one, 2 = two
-    int32_t codec;                  // 0 = H.264 (stripes or full frame), 1 = HEVC Main (full frame, WPP)
+    int32_t codec;                  // 0 = H.264 (stripes or full frame), 1 = HEVC Main (full frame, WPP),
+                                    // 2 = AV1 Main (full frame, tiles)
     int32_t aq_strength;            // H.264 MB-level adaptive QP, Q4 (16 = 1.0); 0 = off
     int32_t subpel;                 // H.264 quarter-pel motion refinement: 0 = default (on), < 0 off
     int32_t intra4x4;               // H.264 Intra4x4 (I_NxN) macroblocks in I slices: > 0 on, else off
+    int32_t tile_cols_log2;         // AV1 tile columns / rows (log2); -1 = automatic
+    int32_t tile_rows_log2;
 } sk_h264_config;
 
 typedef struct sk_packet {

@@ -34,6 +34,7 @@ class SkH264Config(ctypes.Structure):
         ("shared_copy", ctypes.c_int32), ("src_width", ctypes.c_int32), ("src_height", ctypes.c_int32),
         ("num_refs", ctypes.c_int32), ("codec", ctypes.c_int32), ("aq_strength", ctypes.c_int32),
         ("subpel", ctypes.c_int32), ("intra4x4", ctypes.c_int32),
+        ("tile_cols_log2", ctypes.c_int32), ("tile_rows_log2", ctypes.c_int32),
     ]
 
 
@@ -226,7 +227,8 @@ class H264Encoder:
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
                  backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
                  src_width: int = 0, src_height: int = 0, num_refs: int = 1, codec: str = "h264",
-                 aq_strength: float = 0.0, subpel: bool = True, intra4x4: bool = False):
+                 aq_strength: float = 0.0, subpel: bool = True, intra4x4: bool = False,
+                 tile_cols_log2: int = -1, tile_rows_log2: int = -1):
         """aq_strength: MB-level adaptive QP (h264_mb.h aq_offset), 1.0 = x264 aq-mode 1
         strength; 0 = constant QP per slice (x264 ultrafast behaviour)."""
         L = lib()
@@ -239,10 +241,11 @@ class H264Encoder:
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
                                 device, 1 if backend == "hip" else 0, 1 if deblock else -1,
                                 1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height),
-                                int(num_refs), 1 if codec == "hevc" else 0, int(round(aq_strength * 16)),
-                                0 if subpel else -1, 1 if intra4x4 else 0)
-        if codec not in ("h264", "hevc"):
-            raise ValueError("codec must be 'h264' or 'hevc'")
+                                int(num_refs), {"h264": 0, "hevc": 1, "av1": 2}.get(codec, 0),
+                                int(round(aq_strength * 16)), 0 if subpel else -1, 1 if intra4x4 else 0,
+                                int(tile_cols_log2), int(tile_rows_log2))
+        if codec not in ("h264", "hevc", "av1"):
+            raise ValueError("codec must be 'h264', 'hevc' or 'av1'")
         self.codec = codec
         self.width, self.height = width, height
         self.backend = backend
@@ -417,6 +420,17 @@ class HevcEncoder(H264Encoder):
     def __init__(self, width: int, height: int, **kw):
         kw.pop("fullframe", None)
         super().__init__(width, height, codec="hevc", fullframe=True, **kw)
+
+
+class Av1Encoder(H264Encoder):
+    """AV1 Main (8-bit 4:2:0) encoder session: full-frame pictures coded as OBU
+    temporal units (temporal delimiter, sequence header on key frames, one OBU_FRAME
+    with all tiles), same front end as the H.264 encoder. Packets carry the 10-byte
+    stripe header + the temporal unit (low-overhead bitstream format)."""
+
+    def __init__(self, width: int, height: int, **kw):
+        kw.pop("fullframe", None)
+        super().__init__(width, height, codec="av1", fullframe=True, **kw)
 
 
 class JpegEncoder(H264Encoder):
