@@ -240,36 +240,45 @@ static bool code_residual(const uint8_t* src, int sstride, const uint8_t* pred, 
     return nz;
 }
 
-// Key frames: DC / V / H / SMOOTH / SMOOTH_V / SMOOTH_H / PAETH by SAD, per plane group.
+// Key frames: DC / V / H / SMOOTH / SMOOTH_V / SMOOTH_H / PAETH by SAD. The mode is
+// chosen open-loop, predicting from the *source* edges with the decoder's
+// availability rules, so every block is decided independently (in parallel on the
+// GPU); the reconstruction then predicts from the reconstructed edges in coding
+// order (the per-tile wavefront).
 static const uint8_t kIntraCands[7] = {DC_PRED, V_PRED, H_PRED, SMOOTH_PRED, SMOOTH_V_PRED, SMOOTH_H_PRED, PAETH_PRED};
 
-void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
-    const h264::Geometry& g = fe.g;
-    const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
-    BlkInfo b{};
-    b.bsl = (uint8_t)bsl;
-    const int log2n = bsl + 2, n = 1 << log2n;
-    // luma
-    IntraEdge ey;
-    const int x = c * 4, y = r * 4;
-    intra_edges(fe.rec[0].data(), g.stride_y, x, y, n, au, al, geo.mi_cols * 4 - 1, geo.mi_rows * 4 - 1, ey);
-    uint8_t pred[256], best_pred[256];
+int intra_mode_decision(const uint8_t* src, int stride, int x, int y, int log2n, bool au, bool al, int max_x, int max_y) {
+    const int n = 1 << log2n;
+    IntraEdge e;
+    intra_edges(src, stride, x, y, n, au, al, max_x, max_y, e);
+    uint8_t pred[256];
     int best = DC_PRED, best_cost = 1 << 30;
     for (int m : kIntraCands) {
-        intra_predict(ey, m, log2n, pred);
+        intra_predict(e, m, log2n, pred);
         int sad = 0;
         for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) sad += sk_abs((int)fe.src[0][(size_t)(y + i) * g.stride_y + x + j] - pred[i * n + j]);
+            for (int j = 0; j < n; j++) sad += sk_abs((int)src[(size_t)(y + i) * stride + x + j] - pred[i * n + j]);
         const int cost = sad + (m == DC_PRED ? 0 : n * 2);   // mode-bits bias
         if (cost < best_cost) {
             best_cost = cost;
             best = m;
-            memcpy(best_pred, pred, (size_t)n * n);
         }
     }
-    b.mode = (uint8_t)best;
+    return best;
+}
+
+void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
+    const h264::Geometry& g = fe.g;
+    const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+    const int log2n = bsl + 2, n = 1 << log2n;
+    const int x = c * 4, y = r * 4;
+    BlkInfo b = blk[(size_t)(r >> 1) * geo.c8 + (c >> 1)];   // mode from the decision pass
+    IntraEdge ey;
+    intra_edges(fe.rec[0].data(), g.stride_y, x, y, n, au, al, geo.mi_cols * 4 - 1, geo.mi_rows * 4 - 1, ey);
+    uint8_t py[256];
+    intra_predict(ey, b.mode, log2n, py);
     int16_t* ly = unit_lev(r, c, bsl, 0);
-    bool nz = code_residual(&fe.src[0][(size_t)y * g.stride_y + x], g.stride_y, best_pred, log2n, fp.qidx, true, ly,
+    bool nz = code_residual(&fe.src[0][(size_t)y * g.stride_y + x], g.stride_y, py, log2n, fp.qidx, true, ly,
                             &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
     // chroma: UV_DC_PRED. Every other UV mode implies an ADST-family chroma transform
     // (Mode_To_Txfm, §7.13.3 compute_tx_type); this encoder's transforms are DCT_DCT.
@@ -280,8 +289,6 @@ void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
     uint8_t bu[64], bv[64];
     intra_predict(eu, DC_PRED, cl2, bu);
     intra_predict(ev, DC_PRED, cl2, bv);
-    const int bestc = DC_PRED;
-    b.uv_mode = (uint8_t)bestc;
     int16_t* lu = unit_lev(r, c, bsl, 1);
     int16_t* lvv = unit_lev(r, c, bsl, 2);
     nz |= code_residual(&fe.src[1][(size_t)cy * g.stride_c + cx], g.stride_c, bu, cl2, fp.qidx, true, lu,
@@ -296,23 +303,34 @@ void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
     set_lctx(2, c >> 1, r >> 1, n4 >> 1, nz ? level_summary(lvv, cn * cn) : 0);
 }
 
-void CpuAv1Encoder::key_partition(int r, int c, int bsl, const TileRect& t) {
+void CpuAv1Encoder::key_partition(int r, int c, int bsl, const TileRect& t, bool decide) {
     if (r >= geo.mi_rows || c >= geo.mi_cols) return;
     const int half = (1 << bsl) >> 1;
     const bool has_rows = r + half < geo.mi_rows, has_cols = c + half < geo.mi_cols;
     if (bsl == 1 || (bsl == 2 && has_rows && has_cols)) {
-        intra_block(r, c, bsl, t);
+        if (decide) {
+            BlkInfo b{};
+            b.bsl = (uint8_t)bsl;
+            b.uv_mode = DC_PRED;
+            b.mode = (uint8_t)intra_mode_decision(fe.src[0].data(), fe.g.stride_y, c * 4, r * 4, bsl + 2,
+                                                  inside(t, r - 1, c), inside(t, r, c - 1), geo.mi_cols * 4 - 1,
+                                                  geo.mi_rows * 4 - 1);
+            set_cells(r, c, bsl, b);
+        } else {
+            intra_block(r, c, bsl, t);
+        }
         return;
     }
-    for (int q = 0; q < 4; q++) key_partition(r + (q >> 1) * half, c + (q & 1) * half, bsl - 1, t);
+    for (int q = 0; q < 4; q++) key_partition(r + (q >> 1) * half, c + (q & 1) * half, bsl - 1, t, decide);
 }
 
 void CpuAv1Encoder::decide_key() {
-    for (int t = 0; t < geo.tile_cols * geo.tile_rows; t++) {
-        const TileRect tr = tile_rect(geo, t);
-        for (int r = tr.mi_row0; r < tr.mi_row1; r += 16)
-            for (int c = tr.mi_col0; c < tr.mi_col1; c += 16) key_partition(r, c, 4, tr);
-    }
+    for (int pass = 0; pass < 2; pass++)
+        for (int t = 0; t < geo.tile_cols * geo.tile_rows; t++) {
+            const TileRect tr = tile_rect(geo, t);
+            for (int r = tr.mi_row0; r < tr.mi_row1; r += 16)
+                for (int c = tr.mi_col0; c < tr.mi_col1; c += 16) key_partition(r, c, 4, tr, pass == 0);
+        }
 }
 
 // One motion-compensated block: prediction from fe.ref, residual, reconstruction.

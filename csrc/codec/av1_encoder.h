@@ -55,6 +55,9 @@ void write_frame_header(BitWriter& w, const Av1Geo& g, const FrameParams& fp);
 void append_obu(std::vector<uint8_t>& out, int type, const uint8_t* payload, size_t n);
 int choose_level_idx(int W, int H, float fps);
 int qidx_for_qp(int qp);
+// Open-loop intra mode of an n x n luma block (source edges, decoder availability).
+int intra_mode_decision(const uint8_t* src, int stride, int x, int y, int log2n, bool au, bool al, int max_x,
+                        int max_y);
 
 inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
     h264::EncoderConfig f = c;
@@ -96,10 +99,9 @@ class CpuAv1Encoder {
     void intra_block(int r, int c, int bsl, const TileRect& t);
     void inter_unit(int ux, int uy, int mv_row, int mv_col);
     void inter_block(int r, int c, int bsl, int mv_row, int mv_col);
-    void key_partition(int r, int c, int bsl, const TileRect& t);
+    void key_partition(int r, int c, int bsl, const TileRect& t, bool decide);
     void set_cells(int r, int c, int bsl, const BlkInfo& b);
     void set_lctx(int plane, int x4, int y4, int n4, uint8_t v);
-    void recon_plane_block(int plane, int x, int y, int n, const uint8_t* pred, const int16_t* lv, bool intra);
 };
 
 // Is the block containing mi (mr, mc) before the block at (r, c) in coding order?
