@@ -742,6 +742,23 @@ SK_HD int drl_ctx(const MvStack& s, int idx) {
 // bit(b) (an L(1) equiprobable bit) and lits(value, nbits).
 SK_HD int cdf_off(const CdfContext& base, const uint16_t* p) { return (int)(p - (const uint16_t*)&base); }
 
+// split_or_horz / split_or_vert: a binary CDF gathered from the (adapted) partition
+// CDF of the node (spec §9.3.x psum, libaom partition_gather_{vert,horz}_alike).
+// bottom_out: the bottom half lies outside the frame (SPLIT vs HORZ), else the right half.
+SK_HD void gather_partition_cdf(const uint16_t* pc, bool bottom_out, uint16_t* out) {
+    auto P = [&](int k) { return (int)pc[k] - (k > 0 ? (int)pc[k - 1] : 0); };
+    int psum;
+    if (bottom_out)
+        psum = P(PARTITION_VERT) + P(PARTITION_SPLIT) + P(PARTITION_HORZ_A) + P(PARTITION_VERT_A) + P(PARTITION_VERT_B) +
+               P(PARTITION_VERT_4);
+    else
+        psum = P(PARTITION_HORZ) + P(PARTITION_SPLIT) + P(PARTITION_HORZ_A) + P(PARTITION_HORZ_B) + P(PARTITION_VERT_A) +
+               P(PARTITION_HORZ_4);
+    out[0] = (uint16_t)(32768 - psum);
+    out[1] = 32768;
+    out[2] = 0;
+}
+
 // Direct coding: adaptive CDFs in `ctx`, coded by a SymbolCoder.
 template <class Coder>
 struct DirectSink {
@@ -750,7 +767,69 @@ struct DirectSink {
     SK_HD void sym(int off, int n, int v) { coder.encode_adapt((uint16_t*)&ctx + off, n, v); }
     SK_HD void bit(int b) { coder.bool_(b); }
     SK_HD void lits(uint32_t v, int nbits) { coder.literal(v, nbits); }
+    SK_HD void gather(int off, bool bottom_out, int v) {
+        uint16_t c[3];
+        gather_partition_cdf((const uint16_t*)&ctx + off, bottom_out, c);
+        coder.encode(c, 2, v);
+    }
 };
+
+// Token stream (GPU): the block syntax is generated in parallel per 16x16 unit into
+// token lists; one wave per tile then runs the arithmetic coder over them in order.
+//   symbol   [31:30] 0 | [29:26] N-1 | [25:22] value | [21:0] CDF offset (u16 index)
+//   literal  [31:30] 1 | [29:25] bits-1 | [24:0] value (L(1) bits, MSB first)
+//   gather   [31:30] 2 | [29] right-half-out | [28] value | [21:0] partition CDF offset
+SK_HD uint32_t tok_sym(int off, int n, int v) { return ((uint32_t)(n - 1) << 26) | ((uint32_t)v << 22) | (uint32_t)off; }
+SK_HD uint32_t tok_lit(uint32_t v, int nb) { return (1u << 30) | ((uint32_t)(nb - 1) << 25) | v; }
+SK_HD uint32_t tok_gather(int off, bool bottom_out, int v) {
+    return (2u << 30) | ((uint32_t)(bottom_out ? 0 : 1) << 29) | ((uint32_t)v << 28) | (uint32_t)off;
+}
+
+struct TokenSink {
+    uint32_t* p;
+    int n, cap;
+    uint32_t pend;
+    int pend_n;
+    SK_HD void push(uint32_t t) {
+        if (n < cap) p[n] = t;
+        n++;
+    }
+    SK_HD void flush() {
+        if (pend_n) push(tok_lit(pend, pend_n));
+        pend = 0;
+        pend_n = 0;
+    }
+    SK_HD void sym(int off, int n2, int v) {
+        flush();
+        push(tok_sym(off, n2, v));
+    }
+    SK_HD void bit(int b) {
+        pend = (pend << 1) | (uint32_t)(b & 1);
+        if (++pend_n == 24) flush();
+    }
+    SK_HD void lits(uint32_t v, int nbits) {
+        for (int i = nbits - 1; i >= 0; i--) bit((v >> i) & 1);
+    }
+    SK_HD void gather(int off, bool bottom_out, int v) {
+        flush();
+        push(tok_gather(off, bottom_out, v));
+    }
+};
+
+// Replays one token through a coder with the tile's adaptive CDFs.
+template <class Coder>
+SK_HD void code_token(Coder& coder, uint16_t* cdfs, uint32_t t) {
+    const uint32_t kind = t >> 30;
+    if (kind == 0) {
+        coder.encode_adapt(cdfs + (t & 0x3fffff), (int)((t >> 26) & 15) + 1, (int)((t >> 22) & 15));
+    } else if (kind == 1) {
+        coder.literal(t & 0x1ffffff, (int)((t >> 25) & 31) + 1);
+    } else {
+        uint16_t c[3];
+        gather_partition_cdf(cdfs + (t & 0x3fffff), ((t >> 29) & 1) == 0, c);
+        coder.encode(c, 2, (int)((t >> 28) & 1));
+    }
+}
 
 // ---------------------------------------------------------------------------------
 // Coefficient syntax (§5.11.39 coeffs) of one transform block.
@@ -909,6 +988,194 @@ SK_HD void code_mv(Sink& w, const CdfContext& cx, int drow, int dcol) {
     w.sym(cdf_off(cx, cx.mv_joint[0]), 4, joint);
     if (drow != 0) code_mv_component(w, cx, 0, drow);
     if (dcol != 0) code_mv_component(w, cx, 1, dcol);
+}
+
+// ---------------------------------------------------------------------------------
+// Frame view for the block syntax: everything the decisions left behind.
+struct FrameView {
+    Av1Geo geo;
+    const BlkInfo* blk;          // [r8][c8]
+    const int16_t* lev;          // [units][384] (unit grid = front-end MBs, stride unit_w)
+    const uint8_t* lctx[3];      // level contexts (cul | dc << 6), 4x4 units per plane
+    int lctx_w[3];
+    int unit_w;                  // 16x16 units per row
+    int qidx, key;
+    SK_HD const BlkInfo& at(int r, int c) const { return blk[(r >> 1) * geo.c8 + (c >> 1)]; }
+    // levels of the block at mi (r, c) of size bsl in plane p (raster [row][col])
+    SK_HD const int16_t* levels(int r, int c, int bsl, int p) const {
+        const int16_t* u = lev + ((size_t)(r >> 2) * unit_w + (c >> 2)) * 384;
+        if (bsl >= 2) return u + (p == 0 ? 0 : (p == 1 ? 256 : 320));
+        const int k = ((r >> 1) & 1) * 2 + ((c >> 1) & 1);
+        return u + (p == 0 ? 64 * k : (p == 1 ? 256 + 16 * k : 320 + 16 * k));
+    }
+    SK_HD uint8_t lc(int p, int x4, int y4) const { return lctx[p][(size_t)y4 * lctx_w[p] + x4]; }
+};
+
+// above / left level contexts of a tx block (plane units of 4 samples), tile-bounded:
+// AboveLevelContext is cleared at the tile start, LeftLevelContext at every SB row start
+SK_HD CoefCtx coef_ctx(const FrameView& v, const TileRect& t, int plane, int x4, int y4, int n4) {
+    const int ss = plane ? 1 : 0;
+    const int row0 = t.mi_row0 >> ss, col0 = t.mi_col0 >> ss;
+    const int max_x4 = v.geo.mi_cols >> ss, max_y4 = v.geo.mi_rows >> ss;
+    int above = 0, left = 0, dcs = 0;
+    if (y4 - 1 >= row0)
+        for (int k = 0; k < n4; k++)
+            if (x4 + k < max_x4) {
+                const int q = v.lc(plane, x4 + k, y4 - 1);
+                above |= q;
+                dcs += (q >> 6) == 1 ? -1 : ((q >> 6) == 2 ? 1 : 0);
+            }
+    if (x4 - 1 >= col0)
+        for (int k = 0; k < n4; k++)
+            if (y4 + k < max_y4) {
+                const int q = v.lc(plane, x4 - 1, y4 + k);
+                left |= q;
+                dcs += (q >> 6) == 1 ? -1 : ((q >> 6) == 2 ? 1 : 0);
+            }
+    CoefCtx cc;
+    cc.txb_skip = plane == 0 ? 0 : 7 + (above != 0) + (left != 0);
+    cc.dc_sign = dcs < 0 ? 1 : (dcs > 0 ? 2 : 0);
+    return cc;
+}
+
+// Is the block containing mi (mr, mc) before the block at (r, c) in coding order?
+// (raster superblocks, recursive quad-split Z order inside each 64x64 superblock)
+SK_HD uint32_t zorder16(int r, int c) {
+    uint32_t m = 0;
+    for (int b = 3; b >= 0; b--) m = (m << 2) | (uint32_t)(((r >> b) & 1) << 1) | (uint32_t)((c >> b) & 1);
+    return m;
+}
+SK_HD bool decoded_before(int mr, int mc, int r, int c) {
+    const int sr = mr >> 4, sc = mc >> 4, cr = r >> 4, cc = c >> 4;
+    if (sr != cr) return sr < cr;
+    if (sc != cc) return sc < cc;
+    return zorder16(mr & 15, mc & 15) < zorder16(r & 15, c & 15);
+}
+struct DecodedBefore {
+    int r, c;
+    SK_HD bool operator()(int mr, int mc) const { return decoded_before(mr, mc, r, c); }
+};
+
+// Mode info + residual of one block (§5.11.5 decode_block).
+template <class Sink>
+SK_HD void code_block(Sink& w, const CdfContext& cx, const FrameView& v, const TileRect& t, int r, int c, int bsl) {
+    const BlkInfo& b = v.at(r, c);
+    const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+    const int sctx = (au ? (int)blk_skip(v.at(r - 1, c)) : 0) + (al ? (int)blk_skip(v.at(r, c - 1)) : 0);
+    w.sym(cdf_off(cx, cx.skip[sctx]), 2, blk_skip(b));
+    if (v.key) {
+        const int am = au ? v.at(r - 1, c).mode : DC_PRED, lm = al ? v.at(r, c - 1).mode : DC_PRED;
+        w.sym(cdf_off(cx, cx.kf_y_mode[intra_mode_ctx(am)][intra_mode_ctx(lm)]), 13, b.mode);
+        if (is_directional(b.mode)) w.sym(cdf_off(cx, cx.angle_delta[b.mode - V_PRED]), 7, 3);
+        if (bsl <= 3) w.sym(cdf_off(cx, cx.uv_mode_cfl_allowed[b.mode]), 14, b.uv_mode);
+        else w.sym(cdf_off(cx, cx.uv_mode_cfl_not_allowed[b.mode]), 13, b.uv_mode);
+        if (is_directional(b.uv_mode)) w.sym(cdf_off(cx, cx.angle_delta[b.uv_mode - V_PRED]), 7, 3);
+    } else {
+        // is_inter: every block of an inter frame is inter, so no neighbour is intra (ctx 0)
+        w.sym(cdf_off(cx, cx.intra_inter[0]), 2, 1);
+        const int nref = (au ? 1 : 0) + (al ? 1 : 0);
+        const int rctx = nref == 0 ? 1 : 2;
+        w.sym(cdf_off(cx, cx.single_ref[rctx][0]), 2, 0);   // single_ref_p1: forward
+        w.sym(cdf_off(cx, cx.single_ref[rctx][2]), 2, 0);   // p3: LAST / LAST2
+        w.sym(cdf_off(cx, cx.single_ref[rctx][3]), 2, 0);   // p4: LAST
+        MvStack s;
+        const BlkGrid grid{v.blk, v.geo.c8};
+        find_mv_stack(s, grid, t, v.geo.mi_rows, v.geo.mi_cols, r, c, bsl, DecodedBefore{r, c});
+        const int mode = b.mode, idx = (b.flags >> 4) & 3;
+        w.sym(cdf_off(cx, cx.newmv[s.newmv_ctx]), 2, mode != NEWMV);
+        if (mode != NEWMV) {
+            w.sym(cdf_off(cx, cx.zeromv[0]), 2, mode != GLOBALMV);
+            if (mode != GLOBALMV) w.sym(cdf_off(cx, cx.refmv[s.refmv_ctx]), 2, mode != NEARESTMV);
+        }
+        if (mode == NEWMV) {
+            for (int k = 0; k < 2; k++)
+                if (s.n > k + 1) {
+                    w.sym(cdf_off(cx, cx.drl[drl_ctx(s, k)]), 2, idx != k);
+                    if (idx == k) break;
+                }
+        } else if (mode == NEARMV) {
+            for (int k = 1; k < 3; k++)
+                if (s.n > k + 1) {
+                    w.sym(cdf_off(cx, cx.drl[drl_ctx(s, k)]), 2, idx != k);
+                    if (idx == k) break;
+                }
+        }
+        if (mode == NEWMV) {
+            const int pos = s.n <= 1 ? 0 : idx;
+            code_mv(w, cx, b.mv_row - s.mv[pos][0], b.mv_col - s.mv[pos][1]);
+        }
+    }
+    if (blk_skip(b)) return;
+    code_coeffs(w, cx, v.levels(r, c, bsl, 0), bsl, 0, coef_ctx(v, t, 0, c, r, 1 << bsl), blk_inter(b), b.mode, v.qidx);
+    for (int p = 1; p < 3; p++)
+        code_coeffs(w, cx, v.levels(r, c, bsl, p), bsl - 1, p, coef_ctx(v, t, p, c >> 1, r >> 1, (1 << bsl) >> 1),
+                    blk_inter(b), b.mode, v.qidx);
+}
+
+// Partition symbol of the node (r, c, bsl), NONE or SPLIT (gathered bool at edges).
+template <class Sink>
+SK_HD bool code_partition_symbol(Sink& w, const CdfContext& cx, const FrameView& v, const TileRect& t, int r, int c,
+                                 int bsl) {
+    const int half = (1 << bsl) >> 1;
+    const bool has_rows = r + half < v.geo.mi_rows, has_cols = c + half < v.geo.mi_cols;
+    const bool none = v.at(r, c).bsl == bsl && has_rows && has_cols;
+    const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+    const int actx = au && v.at(r - 1, c).bsl < bsl, lctx2 = al && v.at(r, c - 1).bsl < bsl;
+    const int ctx = lctx2 * 2 + actx;
+    const uint16_t* pc = bsl == 1 ? cx.partition_w8[ctx]
+                         : bsl == 2 ? cx.partition_w16[ctx]
+                         : bsl == 3 ? cx.partition_w32[ctx]
+                                    : cx.partition_w64[ctx];
+    if (has_rows && has_cols) w.sym(cdf_off(cx, pc), bsl == 1 ? 4 : 10, none ? PARTITION_NONE : PARTITION_SPLIT);
+    else if (has_cols) w.gather(cdf_off(cx, pc), true, 1);
+    else if (has_rows) w.gather(cdf_off(cx, pc), false, 1);
+    return none;
+}
+
+// Everything the 16x16 unit (ux, uy) contributes to its tile, in coding order: the
+// partition symbols of the 64 / 32 nodes it opens, then its own block(s); a unit
+// inside a larger (merged) block contributes nothing. Units in Z order within
+// raster superblocks reproduce decode_partition's order exactly.
+template <class Sink>
+SK_HD void code_unit(Sink& w, const CdfContext& cx, const FrameView& v, const TileRect& t, int ux, int uy) {
+    const int r = uy * 4, c = ux * 4;
+    if (r >= v.geo.mi_rows || c >= v.geo.mi_cols) return;
+    const int own = v.at(r, c).bsl;
+    for (int L = 4; L >= 3; L--) {
+        const int m = (1 << L) - 1;
+        if ((r & m) || (c & m)) {
+            if (own >= L) return;   // inside a merged block coded by its origin unit
+            continue;
+        }
+        if (code_partition_symbol(w, cx, v, t, r, c, L)) {
+            code_block(w, cx, v, t, r, c, L);
+            return;
+        }
+    }
+    if (code_partition_symbol(w, cx, v, t, r, c, 2)) {
+        code_block(w, cx, v, t, r, c, 2);
+        return;
+    }
+    for (int q = 0; q < 4; q++) {
+        const int rr = r + (q >> 1) * 2, cc = c + (q & 1) * 2;
+        if (rr >= v.geo.mi_rows || cc >= v.geo.mi_cols) continue;
+        code_partition_symbol(w, cx, v, t, rr, cc, 1);
+        code_block(w, cx, v, t, rr, cc, 1);
+    }
+}
+
+// Units of a tile in coding order: index i -> (ux, uy). Returns false past the end.
+SK_HD bool tile_unit(const Av1Geo& g, const TileRect& t, int i, int* ux, int* uy) {
+    const int sbw = (t.mi_col1 - t.mi_col0 + 15) >> 4;
+    const int sb = i >> 4, k = i & 15;
+    const int sr = sb / sbw, sc = sb % sbw;
+    const int ury = (k >> 3 & 1) << 1 | (k >> 1 & 1), urx = (k >> 2 & 1) << 1 | (k & 1);
+    *uy = ((t.mi_row0 >> 4) + sr) * 4 + ury;
+    *ux = ((t.mi_col0 >> 4) + sc) * 4 + urx;
+    return (t.mi_row0 >> 4) + sr < ((t.mi_row1 + 15) >> 4);
+}
+SK_HD int tile_units(const TileRect& t) {
+    return 16 * ((t.mi_col1 - t.mi_col0 + 15) >> 4) * ((t.mi_row1 - t.mi_row0 + 15) >> 4);
 }
 
 }  // namespace sk::av1

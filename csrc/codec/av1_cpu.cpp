@@ -441,158 +441,34 @@ void CpuAv1Encoder::decide_modes() {
 }
 
 // ------------------------------------------------------------------------------ tile coding
-namespace {
-struct TileCoder {
-    const CpuAv1Encoder& e;
-    const TileRect& t;
-    CdfContext cx;
-    SymbolEncoder enc;
-    struct Direct {
-        TileCoder& tc;
-        void sym(int off, int n, int v) { tc.enc.encode_adapt((uint16_t*)&tc.cx + off, n, v); }
-        void bit(int b) { tc.enc.bool_(b); }
-        void lits(uint32_t v, int nb) { tc.enc.literal(v, nb); }
-    };
-    Direct w{*this};
-    BlkGrid grid;
-
-    TileCoder(const CpuAv1Encoder& en, const TileRect& tr) : e(en), t(tr), cx(AV1_DEFAULT_CDF[coef_qctx(en.fp.qidx)]) {
-        grid = BlkGrid{e.blk.data(), e.geo.c8};
+FrameView CpuAv1Encoder::view() const {
+    FrameView v;
+    v.geo = geo;
+    v.blk = blk.data();
+    v.lev = lev.data();
+    for (int p = 0; p < 3; p++) {
+        v.lctx[p] = lctx[p].data();
+        v.lctx_w[p] = lctx_w[p];
     }
-    const BlkInfo& at(int r, int c) const { return grid.at(r, c); }
-
-    uint8_t lc(int plane, int x4, int y4) const {
-        return e.lctx[plane][(size_t)y4 * e.lctx_w[plane] + x4];
-    }
-    // above / left level contexts of a tx block (plane units of 4 samples), tile-bounded
-    CoefCtx coef_ctx(int plane, int x4, int y4, int n4) const {
-        const int ss = plane ? 1 : 0;
-        const int row0 = t.mi_row0 >> ss, col0 = t.mi_col0 >> ss;
-        const int max_x4 = e.geo.mi_cols >> ss, max_y4 = e.geo.mi_rows >> ss;
-        int above = 0, left = 0, dcs = 0;
-        static const int sgn[3] = {0, -1, 1};
-        if (y4 - 1 >= row0)
-            for (int k = 0; k < n4; k++)
-                if (x4 + k < max_x4) {
-                    const uint8_t v = lc(plane, x4 + k, y4 - 1);
-                    above |= v;
-                    dcs += sgn[v >> 6];
-                }
-        if (x4 - 1 >= col0)
-            for (int k = 0; k < n4; k++)
-                if (y4 + k < max_y4) {
-                    const uint8_t v = lc(plane, x4 - 1, y4 + k);
-                    left |= v;
-                    dcs += sgn[v >> 6];
-                }
-        CoefCtx cc;
-        cc.txb_skip = plane == 0 ? 0 : 7 + (above != 0) + (left != 0);
-        cc.dc_sign = dcs < 0 ? 1 : (dcs > 0 ? 2 : 0);
-        return cc;
-    }
-
-    void residual(int r, int c, const BlkInfo& b) {
-        const int bsl = b.bsl;
-        const int16_t* ly = e.unit_lev(r, c, bsl, 0);
-        code_coeffs(w, cx, ly, bsl, 0, coef_ctx(0, c, r, 1 << bsl), blk_inter(b), b.mode, e.fp.qidx);
-        for (int p = 1; p < 3; p++)
-            code_coeffs(w, cx, e.unit_lev(r, c, bsl, p), bsl - 1, p, coef_ctx(p, c >> 1, r >> 1, (1 << bsl) >> 1),
-                        blk_inter(b), b.mode, e.fp.qidx);
-    }
-
-    void block(int r, int c, int bsl) {
-        const BlkInfo& b = at(r, c);
-        const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
-        const int sctx = (au ? blk_skip(at(r - 1, c)) : 0) + (al ? blk_skip(at(r, c - 1)) : 0);
-        w.sym(cdf_off(cx, cx.skip[sctx]), 2, blk_skip(b));
-        if (e.fp.key) {
-            const int am = au ? at(r - 1, c).mode : DC_PRED, lm = al ? at(r, c - 1).mode : DC_PRED;
-            w.sym(cdf_off(cx, cx.kf_y_mode[intra_mode_ctx(am)][intra_mode_ctx(lm)]), 13, b.mode);
-            if (is_directional(b.mode)) w.sym(cdf_off(cx, cx.angle_delta[b.mode - V_PRED]), 7, 3);
-            if (bsl <= 3) w.sym(cdf_off(cx, cx.uv_mode_cfl_allowed[b.mode]), 14, b.uv_mode);
-            else w.sym(cdf_off(cx, cx.uv_mode_cfl_not_allowed[b.mode]), 13, b.uv_mode);
-            if (is_directional(b.uv_mode)) w.sym(cdf_off(cx, cx.angle_delta[b.uv_mode - V_PRED]), 7, 3);
-        } else {
-            // is_inter: every block of an inter frame is inter, so no neighbour is intra (ctx 0)
-            w.sym(cdf_off(cx, cx.intra_inter[0]), 2, 1);
-            const int nref = (au ? 1 : 0) + (al ? 1 : 0);
-            const int rctx = nref == 0 ? 1 : 2;
-            w.sym(cdf_off(cx, cx.single_ref[rctx][0]), 2, 0);   // single_ref_p1: forward
-            w.sym(cdf_off(cx, cx.single_ref[rctx][2]), 2, 0);   // p3: LAST / LAST2
-            w.sym(cdf_off(cx, cx.single_ref[rctx][3]), 2, 0);   // p4: LAST
-            MvStack s;
-            find_mv_stack(s, grid, t, e.geo.mi_rows, e.geo.mi_cols, r, c, bsl,
-                          [&](int mr, int mc) { return decoded_before(mr, mc, r, c); });
-            const int mode = b.mode, idx = (b.flags >> 4) & 3;
-            w.sym(cdf_off(cx, cx.newmv[s.newmv_ctx]), 2, mode != NEWMV);
-            if (mode != NEWMV) {
-                w.sym(cdf_off(cx, cx.zeromv[0]), 2, mode != GLOBALMV);
-                if (mode != GLOBALMV) w.sym(cdf_off(cx, cx.refmv[s.refmv_ctx]), 2, mode != NEARESTMV);
-            }
-            if (mode == NEWMV) {
-                for (int k = 0; k < 2; k++)
-                    if (s.n > k + 1) {
-                        w.sym(cdf_off(cx, cx.drl[drl_ctx(s, k)]), 2, idx != k);
-                        if (idx == k) break;
-                    }
-            } else if (mode == NEARMV) {
-                for (int k = 1; k < 3; k++)
-                    if (s.n > k + 1) {
-                        w.sym(cdf_off(cx, cx.drl[drl_ctx(s, k)]), 2, idx != k);
-                        if (idx == k) break;
-                    }
-            }
-            if (mode == NEWMV) {
-                const int pos = s.n <= 1 ? 0 : idx;
-                code_mv(w, cx, b.mv_row - s.mv[pos][0], b.mv_col - s.mv[pos][1]);
-            }
-        }
-        if (!blk_skip(b)) residual(r, c, b);
-    }
-
-    void partition(int r, int c, int bsl) {
-        if (r >= e.geo.mi_rows || c >= e.geo.mi_cols) return;
-        const int half = (1 << bsl) >> 1;
-        const bool has_rows = r + half < e.geo.mi_rows, has_cols = c + half < e.geo.mi_cols;
-        const int part = at(r, c).bsl == bsl ? PARTITION_NONE : PARTITION_SPLIT;
-        const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
-        const int actx = au && at(r - 1, c).bsl < bsl, lctx2 = al && at(r, c - 1).bsl < bsl;
-        const int ctx = lctx2 * 2 + actx;
-        const uint16_t* pc = bsl == 1 ? cx.partition_w8[ctx]
-                             : bsl == 2 ? cx.partition_w16[ctx]
-                             : bsl == 3 ? cx.partition_w32[ctx]
-                                        : cx.partition_w64[ctx];
-        const int np = bsl == 1 ? 4 : 10;
-        if (has_rows && has_cols) {
-            w.sym(cdf_off(cx, pc), np, part);
-        } else if (has_cols || has_rows) {
-            // split_or_horz / split_or_vert: a bool with a CDF gathered from the partition CDF
-            auto P = [&](int k) { return (int)pc[k] - (k > 0 ? (int)pc[k - 1] : 0); };
-            int psum;
-            if (has_cols)   // bottom half outside: SPLIT vs HORZ
-                psum = P(PARTITION_VERT) + P(PARTITION_SPLIT) + P(PARTITION_HORZ_A) + P(PARTITION_VERT_A) +
-                       P(PARTITION_VERT_B) + P(PARTITION_VERT_4);
-            else            // right half outside: SPLIT vs VERT
-                psum = P(PARTITION_HORZ) + P(PARTITION_SPLIT) + P(PARTITION_HORZ_A) + P(PARTITION_HORZ_B) +
-                       P(PARTITION_VERT_A) + P(PARTITION_HORZ_4);
-            const uint16_t bc[3] = {(uint16_t)(32768 - psum), 32768, 0};
-            enc.encode(bc, 2, 1);
-        }
-        if (part == PARTITION_NONE && (has_rows && has_cols)) {
-            block(r, c, bsl);
-            return;
-        }
-        for (int q = 0; q < 4; q++) partition(r + (q >> 1) * half, c + (q & 1) * half, bsl - 1);
-    }
-};
-}  // namespace
+    v.unit_w = fe.g.mb_w;
+    v.qidx = fp.qidx;
+    v.key = fp.key;
+    return v;
+}
 
 std::vector<uint8_t> CpuAv1Encoder::code_tile(int t) {
     const TileRect tr = tile_rect(geo, t);
-    TileCoder tc(*this, tr);
-    for (int r = tr.mi_row0; r < tr.mi_row1; r += 16)
-        for (int c = tr.mi_col0; c < tr.mi_col1; c += 16) tc.partition(r, c, 4);
-    return tc.enc.finish();
+    const FrameView v = view();
+    CdfContext cx = AV1_DEFAULT_CDF[coef_qctx(fp.qidx)];
+    VectorSink sink;
+    SymbolCoder<VectorSink> coder(sink);
+    DirectSink<SymbolCoder<VectorSink>> w{coder, cx};
+    int ux, uy;
+    for (int i = 0; tile_unit(geo, tr, i, &ux, &uy); i++) code_unit(w, cx, v, tr, ux, uy);
+    coder.finish();
+    std::vector<uint8_t> out(sink.v.size());
+    if (!out.empty()) carry_bytes(sink.v.data(), (int)sink.v.size(), out.data());
+    return out;
 }
 
 std::vector<uint8_t> CpuAv1Encoder::assemble(const std::vector<std::vector<uint8_t>>& tiles) {

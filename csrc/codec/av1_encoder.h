@@ -94,6 +94,7 @@ class CpuAv1Encoder {
     uint64_t frames = 0;
     // levels of the block at mi (r, c) of size bsl, plane 0..2 (raster [row][col])
     int16_t* unit_lev(int r, int c, int bsl, int plane) const;
+    FrameView view() const;
 
    private:
     void intra_block(int r, int c, int bsl, const TileRect& t);
@@ -103,20 +104,6 @@ class CpuAv1Encoder {
     void set_cells(int r, int c, int bsl, const BlkInfo& b);
     void set_lctx(int plane, int x4, int y4, int n4, uint8_t v);
 };
-
-// Is the block containing mi (mr, mc) before the block at (r, c) in coding order?
-// (raster superblocks, recursive quad-split Z order inside each 64x64 superblock)
-SK_HD uint32_t zorder16(int r, int c) {
-    uint32_t m = 0;
-    for (int b = 3; b >= 0; b--) m = (m << 2) | (uint32_t)(((r >> b) & 1) << 1) | (uint32_t)((c >> b) & 1);
-    return m;
-}
-SK_HD bool decoded_before(int mr, int mc, int r, int c) {
-    const int sr = mr >> 4, sc = mc >> 4, cr = r >> 4, cc = c >> 4;
-    if (sr != cr) return sr < cr;
-    if (sc != cc) return sc < cc;
-    return zorder16(mr & 15, mc & 15) < zorder16(r & 15, c & 15);
-}
 
 }  // namespace av1
 }  // namespace sk

@@ -1,0 +1,41 @@
+// Device buffers and launch interface of the HIP AV1 back end. It runs after the
+// H.264 front end (k_convert_damage, k_plan, k_me_mfma, k_motion_search, k_decide)
+// on the same FrameArgs and before k_commit (reference / motion-field update).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "h264_gpu.h"
+#include "../codec/av1_core.h"
+
+namespace sk {
+namespace av1 {
+namespace gpu {
+
+constexpr int kLevPerUnit = 384;
+constexpr int kTokCap = 4096;        // tokens per 16x16 unit slot (worst case ~3.3k, see tok_bound)
+constexpr int kTileChunkCap = 1 << 20;
+
+struct Av1Args {
+    h264::gpu::FrameArgs f;   // planes, geometry (mb = 16x16 unit), tasks, motion field
+    Av1Geo geo;
+    BlkInfo* blk;             // [r8][c8]
+    int16_t* lev;             // [units][kLevPerUnit]
+    uint8_t* lctx[3];         // level contexts per plane (4x4 units), strides lctx_w
+    int lctx_w[3];
+    uint32_t* tok;            // [units][kTokCap]
+    int* tok_n;               // [units]
+    int* frame;               // device: [0] key, [1] qidx
+    int* frame_host;          // host-mapped copy of frame[0..1]
+    const uint8_t* qidx_of_qp;   // [52]
+    uint16_t* chunks;         // [tiles][tile_cap] settled coder chunks
+    int tile_cap;             // chunk capacity per tile
+    int* tile_size;           // device [tiles] bytes
+    uint8_t* out_host;        // host-mapped tile bytes, concatenated [out_cap]
+    int out_cap;
+    int* out_size_host;       // host-mapped [tiles] bytes (-1: did not fit out_cap)
+};
+
+void launch_backend(const Av1Args& a, hipStream_t s);
+
+}  // namespace gpu
+}  // namespace av1
+}  // namespace sk
