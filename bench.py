@@ -50,8 +50,13 @@ def parse():
     p.add_argument("--qp", type=int, default=25)
     p.add_argument("--pool", type=int, default=16, help="pre-rendered frames per session pool")
     p.add_argument("--backend", default="hip", choices=["hip", "cpu"])
-    p.add_argument("--encoder", default="h264", choices=["h264", "jpeg", "hevc"],
-                   help="h264 (headline, x264enc-striped equivalent) or jpeg stripes")
+    p.add_argument("--encoder", default="h264", choices=["h264", "jpeg", "hevc", "av1"],
+                   help="h264 (headline, x264enc-striped equivalent), jpeg stripes, hevc or av1 full frames")
+    p.add_argument("--extra-4k", type=int, default=1,
+                   help="after the timed window: one 3840x2160 HEVC session (BASELINE config 3, 60 fps) and one "
+                        "3840x2160 AV1 session (config 5, 120 fps), each timed over --extra-steps frames and "
+                        "reported as extra keys (0 = skip)")
+    p.add_argument("--extra-steps", type=int, default=60)
     p.add_argument("--jpeg-quality", type=int, default=40)
     p.add_argument("--deblock", type=int, default=0,
                    help="H.264 in-loop deblocking filter (1 on; default off like the reference's x264 ultrafast preset)")
@@ -75,6 +80,10 @@ def parse():
                         "measured capture->client latency; a comma list is tried in order and the first N at "
                         "which every session sustains 60 fps is reported (tools/bench_e2e.py); 0 = skip")
     p.add_argument("--e2e-seconds", type=float, default=4.0)
+    p.add_argument("--e2e-warmup", type=float, default=6.0)
+    p.add_argument("--e2e-force", action="store_true",
+                   help="run the end-to-end check with --backend cpu too (servers use the CPU encoder): the "
+                        "multi-rank rehearsal of the per-GPU check on gloo")
     p.add_argument("--e2e-sessions-per-proc", type=int, default=8,
                    help="sessions per server process in the end-to-end check (parallel/multi.py session hosts "
                         "sharing one HIP context; 1 = one process per session)")
@@ -107,6 +116,8 @@ def run_capture_path(args, pool, local_rank):
             mode = pixelflux.OUTPUT_MODE_JPEG
         elif args.encoder == "hevc":
             mode = pixelflux.OUTPUT_MODE_HEVC
+        elif args.encoder == "av1":
+            mode = pixelflux.OUTPUT_MODE_AV1
         else:
             mode = pixelflux.OUTPUT_MODE_H264
         cs = pixelflux.default_settings(W, H, output_mode=mode, h264_crf=args.qp, use_paint_over_quality=0,
@@ -130,7 +141,7 @@ def run_capture_path(args, pool, local_rank):
     return caps, run_all
 
 
-def run_e2e(args, W, H):
+def run_e2e(args, W, H, gpu=0, counts=None):
     """Short end-to-end check (tools/bench_e2e.py): N server processes on this GPU, N
     headless websocket clients, W x H at 60 fps. Latency is capture (frame grab) to
     client receipt of the frame's first stripe; the browser's decode/paint is not in it.
@@ -141,14 +152,15 @@ def run_e2e(args, W, H):
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
         import bench_e2e
         ns = types.SimpleNamespace(width=W, height=H, fps=60, crf=args.qp, encoder=args.e2e_encoder,
-                                   source="motion", gpu=0, use_cpu=False, sustain=0.97, seconds=args.e2e_seconds,
-                                   warmup=6.0, hw_queues=None, client_procs=8,
+                                   source="motion", gpu=gpu, use_cpu=args.backend == "cpu", sustain=0.97,
+                                   seconds=args.e2e_seconds,
+                                   warmup=args.e2e_warmup, hw_queues=None, client_procs=8,
                                    sessions_per_proc=args.e2e_sessions_per_proc,
-                                   log_dir=os.path.join("gpurun_out", "bench_e2e_logs"))
+                                   log_dir=os.path.join("gpurun_out", "bench_e2e_logs", f"gpu{gpu}"))
         os.makedirs(ns.log_dir, exist_ok=True)
         tried = []
         r = None
-        for n in e2e_counts(args):
+        for n in (counts or e2e_counts(args)):
             r = asyncio.run(asyncio.wait_for(bench_e2e.run_n(n, ns), 120))
             tried.append({"sessions": n, "sustained": bool(r.get("sustained")), "fps_min": r.get("fps_min")})
             if r.get("sustained"):
@@ -159,11 +171,55 @@ def run_e2e(args, W, H):
                        "of 60 fps; latency = frame grab -> first packet received")
         return r
     except Exception as ex:   # noqa: BLE001 - reported in the JSON line
-        return {"sessions": e2e_counts(args), "error": f"{type(ex).__name__}: {ex}"}
+        return {"sessions": counts or e2e_counts(args), "error": f"{type(ex).__name__}: {ex}"}
 
 
-def e2e_counts(args):
-    return [int(x) for x in str(args.e2e_sessions).split(",") if x.strip() and int(x) > 0]
+def e2e_counts(args, world=1):
+    """Session counts tried by the end-to-end check on each GPU. One GPU: the
+    default sweep; a node of N GPUs: every rank serves its share of BASELINE config
+    4 (64 sessions over 8 GPUs -> 8 per GPU) and one step above it."""
+    v = [int(x) for x in str(args.e2e_sessions).split(",") if x.strip() and int(x) > 0]
+    if world > 1 and args.e2e_sessions == "48,32,16":
+        per = max(1, 64 // world)
+        v = [2 * per, per]
+    return v
+
+
+def run_extra(args, W, H, encoder, fps, local_rank, steps):
+    """One W x H session of `encoder` through the production capture loop, timed over
+    `steps` frames after a warm-up (key frame + steady state); runs after the headline
+    window. Reports throughput, capture->packet latency and the frame-interval budget."""
+    import types
+    from selkies_gstreamer_amd.ops.native import PinnedBuffer
+    from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
+    try:
+        src = SyntheticDesktop(W, H, kind=args.content, seed=7)
+        pool = PinnedBuffer((8, H, W, 4))
+        for i in range(8):
+            src.frame(i, out=pool.array[i])
+        a = types.SimpleNamespace(**vars(args))
+        a.sessions, a.encoder, a.pool, a.mode = 1, encoder, 8, "fullframe"
+        caps, run_caps = run_capture_path(a, pool, local_rank)
+        run_caps(10)
+        caps[0].latencies(reset=True)
+        b0 = caps[0].stats()["bytes"]
+        t0 = time.perf_counter()
+        run_caps(steps)
+        el = time.perf_counter() - t0
+        lat = np.asarray(caps[0].latencies(), dtype=np.float64)
+        st = caps[0].stats()
+        for c in caps:
+            c.close()
+        budget = 1000.0 / fps
+        p99 = float(np.percentile(lat, 99))
+        return {"resolution": f"{W}x{H}", "encoder": encoder, "target_fps": fps, "steps": steps,
+                "fps": round(steps / el, 2), "p50_encode_latency_ms": round(float(np.percentile(lat, 50)), 3),
+                "p99_encode_latency_ms": round(p99, 3), "frame_interval_ms": round(budget, 3),
+                "realtime": bool(steps / el >= fps and p99 < budget),
+                "kib_per_frame": round((st["bytes"] - b0) / steps / 1024, 1),
+                "frames_in_flight": st.get("frames_in_flight"), "qp": args.qp}
+    except Exception as ex:   # noqa: BLE001 - reported, never fatal for the headline
+        return {"resolution": f"{W}x{H}", "encoder": encoder, "error": f"{type(ex).__name__}: {ex}"}
 
 
 def run_dist_bands(args, torch, dist, rank, world, local_rank):
@@ -234,6 +290,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     torch = None
+    # End-to-end check first, while this process has not touched the GPU: the servers then
+    # share the card with nothing else (a live HIP context here, with its hardware queues,
+    # cost the sessions ~3 fps and a 59 ms p99 in measurements: profiles/r2_e2e_sessions.md).
+    # Every rank checks its own GPU (servers pinned with --gpu-id); rank 0 sums the node.
+    e2e = None
+    if (e2e_counts(args) and (args.backend == "hip" or args.e2e_force) and args.encoder == "h264"
+            and not args.gather and not args.dist_bands):
+        e2e = run_e2e(args, args.width, args.height, gpu=local_rank, counts=e2e_counts(args, world))
+        time.sleep(3.0)   # let the check's processes, clients and GPU contexts finish tearing down
     if world > 1:
         import torch as _torch
         import torch.distributed as _dist
@@ -274,14 +339,6 @@ def main():
     from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
     from selkies_gstreamer_amd.parallel.numa import bind_to_gpu
 
-    # End-to-end check first, while this process has not touched the GPU: the servers then
-    # share the card with nothing else (a live HIP context here, with its hardware queues,
-    # cost the sessions ~3 fps and a 59 ms p99 in measurements: profiles/r2_e2e_sessions.md).
-    e2e = None
-    if (rank == 0 and world == 1 and e2e_counts(args) and args.backend == "hip" and args.encoder == "h264"
-            and not args.gather):
-        e2e = run_e2e(args, args.width, args.height)
-        time.sleep(3.0)   # let the 48-session check's processes, clients and GPU contexts finish tearing down
     # host threads and pinned frames on the GPU's NUMA node (first touch), before any allocation
     numa_node = bind_to_gpu(local_rank) if args.backend == "hip" else None
 
@@ -416,9 +473,11 @@ def main():
     elapsed = time.perf_counter() - t0
 
     frames = S * args.steps
+    inflight_used = None
     if caps is not None:
         all_lat = np.concatenate([np.asarray(c.latencies(), dtype=np.float64) for c in caps])
         nbytes = [c.stats()["bytes"] - b for c, b in zip(caps, bytes0)]
+        inflight_used = max(c.stats().get("frames_in_flight", 0) for c in caps)
     else:
         all_lat = np.concatenate([np.asarray(x) for x in lat]) * 1e3
     stats = np.array([elapsed, frames, sum(nbytes), np.percentile(all_lat, 50), np.percentile(all_lat, 99)],
@@ -444,12 +503,24 @@ def main():
     for c in caps or []:
         c.close()
     caps = None
+    # node view of the end-to-end checks (every rank ran its own GPU's)
+    e2e_ranks = [e2e]
+    if dist is not None:
+        e2e_ranks = [None] * world
+        dist.all_gather_object(e2e_ranks, e2e)
+    node_sessions = None
+    if all(r and r.get("sustained") for r in e2e_ranks):
+        node_sessions = sum(int(r["sessions"]) for r in e2e_ranks)
+    extras = {}
+    if args.extra_4k and args.backend == "hip" and not args.gather and rank == 0:
+        extras["hevc_4k"] = run_extra(args, 3840, 2160, "hevc", 60, local_rank, args.extra_steps)
+        extras["av1_4k"] = run_extra(args, 3840, 2160, "av1", 120, local_rank, 2 * args.extra_steps)
     if rank == 0:
         n_gpus = max(world, 1)
         res = {
             "metric": "encoded fps + glass-to-glass p50 ms at 1920x1080; concurrent 60fps sessions/node",
             "value": round(fps, 2),
-            "unit": f"frames/s ({W}x{H} {dict(h264='H.264', hevc='HEVC', jpeg='JPEG')[args.encoder]}, all sessions, all GPUs)",
+            "unit": f"frames/s ({W}x{H} {dict(h264='H.264', hevc='HEVC', jpeg='JPEG', av1='AV1')[args.encoder]}, all sessions, all GPUs)",
             "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -462,12 +533,18 @@ def main():
                     + (", served through native capture sessions (step mode)" if args.path == "capture" else ""),
             "p50_encode_latency_ms": round(p50, 3),
             "p99_encode_latency_ms": round(p99, 3),
-            # measured, not derived: N real sessions sustained 60 fps end to end (null if not run / failed)
-            "concurrent_60fps_sessions": (e2e["sessions"] if e2e and e2e.get("sustained") else None),
+            # measured, not derived: N real sessions sustained 60 fps end to end on every GPU of
+            # the node, summed over ranks (null if not run / failed anywhere)
+            "concurrent_60fps_sessions": node_sessions,
             "encoder_capacity_60fps_sessions": int(fps // 60) if p99 < 1000.0 / 60 else None,
             "capture_to_client_p50_ms": e2e.get("latency_p50_ms") if e2e else None,
             "capture_to_client_p99_ms": e2e.get("latency_p99_ms") if e2e else None,
             "e2e": e2e,
+            "e2e_per_gpu": ([{"gpu": i, "sessions": (r or {}).get("sessions"), "sustained": (r or {}).get("sustained"),
+                              "fps_min": (r or {}).get("fps_min"), "latency_p50_ms": (r or {}).get("latency_p50_ms"),
+                              "latency_p99_ms": (r or {}).get("latency_p99_ms"), "error": (r or {}).get("error")}
+                             for i, r in enumerate(e2e_ranks)] if world > 1 else None),
+            **extras,
             "sessions_per_gpu": S,
             "kib_per_frame": round(total_bytes / frames / 1024, 1),
             "gathered_bytes_rank0": gather_bytes,
@@ -476,7 +553,8 @@ def main():
                           if args.encoder == "h264" else
                           (f"HEVC Main CABAC, CTB 16, WPP, slices of {args.stripe_height}px, QP {args.qp}"
                            if args.encoder == "hevc" else
-                           f"baseline JPEG 4:2:0 stripes {args.stripe_height}px, quality {args.jpeg_quality}")),
+                           (f"AV1 Main 8-bit 4:2:0, 64x64 SB, tiles, QP {args.qp}" if args.encoder == "av1" else
+                            f"baseline JPEG 4:2:0 stripes {args.stripe_height}px, quality {args.jpeg_quality}"))),
                 "global_batch": S * n_gpus,
                 "seq_len": 1,
                 "parallelism": f"session-parallel dp{n_gpus} x {S} sessions/GPU",
@@ -486,8 +564,10 @@ def main():
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
                 "bands_per_session": args.bands,
                 "path": args.path,
-                "upload_overlap": bool(args.overlap) or args.path == "capture",
-                "frames_in_flight": 2 if (args.overlap >= 2 or args.path == "capture") else 1,
+                # what the pipeline actually ran with: the capture loop keeps two frames in
+                # flight only for a session that has its GPU to itself (capture.cpp overlap_now)
+                "upload_overlap": (inflight_used or 0) >= 2 if args.path == "capture" else bool(args.overlap),
+                "frames_in_flight": inflight_used if args.path == "capture" else (2 if args.overlap >= 2 else 1),
                 "num_refs": args.num_refs,
                 "numa_node_rank0": numa_node,
             },

@@ -1,110 +1,641 @@
-// AV1 tile entropy coding on the GPU: one wave per tile runs the multi-symbol
-// arithmetic coder of codec/av1_ec.h (the same SymbolCoder, device-side sink) over
-// the tile's symbol list with the tile's own adaptive CDFs in LDS, then resolves
-// the carries and writes the tile's bytes. AV1 tiles are independently decodable
-// (separate CDF state and coder per tile), which is where the parallelism comes
-// from; within a tile the coder is serial, like CABAC rows in hevc_kernels.hip.
-// Byte-identical to the host SymbolEncoder (tests/test_av1_entropy.py, gpu-marked).
-#include <hip/hip_runtime.h>
+// gfx950 (CDNA4) kernels of the AV1 back end (codec/av1_core.h semantics, bit-exact
+// with the CPU reference codec/av1_cpu.cpp):
+//   k_av1_setup        frame type (any intra slice -> key frame) and qindex
+//   k_av1_intra_modes  key frames: open-loop intra mode per block, one wave per 16x16 unit
+//   k_av1_intra_rec    key frames: reconstruction wavefront, one workgroup per tile (intra
+//                      prediction never crosses a tile edge), anti-diagonal steps x + y
+//   k_av1_inter        inter frames: motion compensation (8-tap / 4-tap sub-pel chroma),
+//                      transform, quantisation, reconstruction, one wave per unit
+//   k_av1_merge        inter frames: static 32x32 / 64x64 merging, one wave per superblock
+//   k_av1_modes        inter frames: reference-MV stack -> NEAREST / NEAR / GLOBAL / NEWMV
+//   k_av1_tokens       block syntax -> token lists, one lane per 16x16 unit
+//   k_av1_ec           one wave per tile: arithmetic coding with the tile's CDFs in LDS
+//   k_av1_pack         tile bytes -> host-mapped output (concatenated)
+//   k_av1_finish       padding rows of the reconstruction, slice actions for k_commit
+// Transforms: forward DCT as LDS matrix products (lanes = output coefficients),
+// inverse as the normative butterflies, lane = row / column of a transform block.
+#include "av1_gpu.h"
 
-#include <cstdint>
-#include <cstring>
-#include <vector>
+namespace sk {
+namespace av1 {
+namespace gpu {
 
-#include "../codec/av1_ec.h"
+using h264::ACT_I;
+using h264::ACT_NONE;
+using h264::ACT_P;
+using h264::ACT_SKIPALL;
+using h264::SliceTask;
+using h264::gpu::FrameArgs;
 
-namespace sk::av1 {
+__device__ __forceinline__ int lane() { return threadIdx.x & 63; }
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int wsum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
 
-constexpr int kMaxCtx = 64;          // contexts per tile in LDS (17 x u16 each)
+// Forward DCT bases in LDS: [0] 4-point at 0, 8-point at 16, 16-point at 80.
+struct FdctLds {
+    int16_t k[16 + 64 + 256];
+};
+__device__ __forceinline__ const int16_t* fdct_k(const FdctLds& F, int log2n) {
+    return F.k + (log2n == 2 ? 0 : (log2n == 3 ? 16 : 80));
+}
+__device__ __forceinline__ void load_fdct(FdctLds& F) {
+    for (int i = threadIdx.x; i < 336; i += blockDim.x) {
+        const int log2n = i < 16 ? 2 : (i < 80 ? 3 : 4);
+        const int base = log2n == 2 ? 0 : (log2n == 3 ? 16 : 80);
+        const int n = 1 << log2n, j = i - base;
+        F.k[i] = (int16_t)fdct_basis(log2n, j / n, j % n);
+    }
+}
 
-struct DevSink {
+// One block's working set: luma n x n at 0, U at 256, V at 320 (raster per plane).
+struct BlkLds {
+    uint8_t src[384];
+    uint8_t pred[384];
+    int32_t a[384];
+    int32_t b[384];
+    IntraEdge e[3];      // intra edges of Y, U, V
+};
+// Tile of a unit position (mi r, c).
+__device__ __forceinline__ TileRect tile_of(const Av1Geo& g, int r, int c) {
+    const int tc = (c >> 4) / g.tile_w_sb, tr = (r >> 4) / g.tile_h_sb;
+    return tile_rect(g, tr * g.tile_cols + tc);
+}
+
+// Transform, quantisation and reconstruction of one block held in L (src, pred):
+// luma n = 1 << log2n, chroma n / 2. Writes levels to gl (3 planes), the
+// reconstruction into L.pred, and returns the per-plane level summaries
+// (cul | dc << 6) packed as bytes 0..2, bit 24 = any nonzero.
+__device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int qidx, bool intra, int16_t* gy,
+                                    int16_t* gu, int16_t* gv) {
+    const int l = lane();
+    const int n = 1 << log2n, nn = n * n, cn = n >> 1, cnn = cn * cn;
+    const int qd = dc_q(qidx), qa = ac_q(qidx);
+    // plane p element i: luma [0, nn), U [256, 256 + cnn), V [320, 320 + cnn)
+    auto base = [&](int p) { return p == 0 ? 0 : (p == 1 ? 256 : 320); };
+    for (int p = 0; p < 3; p++) {
+        const int m = p ? cnn : nn, o = base(p);
+        for (int i = l; i < m; i += 64) L.a[o + i] = (int)L.src[o + i] - (int)L.pred[o + i];
+    }
+    wsync();
+    // forward stage 1 (columns): b[k][j] = (sum_m K[k][m] a[m][j] + 512) >> 10
+    for (int p = 0; p < 3; p++) {
+        const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
+        const int16_t* K = fdct_k(F, ln);
+        for (int i = l; i < sz * sz; i += 64) {
+            const int k = i >> ln, j = i & (sz - 1);
+            int s = 0;
+            for (int m2 = 0; m2 < sz; m2++) s += (int)K[k * sz + m2] * L.a[o + m2 * sz + j];
+            L.b[o + i] = (s + 512) >> 10;
+        }
+    }
+    wsync();
+    // forward stage 2 (rows) + quantisation + dequantisation
+    int nzm = 0;
+    uint32_t cul = 0;
+    for (int p = 0; p < 3; p++) {
+        const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
+        const int16_t* K = fdct_k(F, ln);
+        int16_t* g = p == 0 ? gy : (p == 1 ? gu : gv);
+        int sum = 0, nz = 0, first = 0;
+        for (int i = l; i < sz * sz; i += 64) {
+            const int k = i >> ln, lc = i & (sz - 1);
+            int64_t s = 0;
+            for (int j = 0; j < sz; j++) s += (int64_t)L.b[o + k * sz + j] * K[lc * sz + j];
+            const int32_t c = (int32_t)((s + (s >= 0 ? 4096 : 4095)) >> 13);
+            const int q = i == 0 ? qd : qa;
+            const int lv = quantize(c, q, intra);
+            g[i] = (int16_t)lv;
+            if (i == 0) first = lv;
+            sum += lv < 0 ? -lv : lv;
+            nz |= lv;
+            L.a[o + i] = dequant(lv, q);
+        }
+        sum = wsum(sum);
+        const bool any = __ballot(nz != 0) != 0;
+        if (any) nzm |= 1 << p;
+        const int lv0 = __shfl(first, 0);
+        const int dc = lv0 < 0 ? 1 : (lv0 > 0 ? 2 : 0);
+        const uint32_t summ = any ? (uint32_t)(sk_min(sum, 63) | (dc << 6)) : 0u;
+        cul |= summ << (8 * p);
+    }
+    wsync();
+    // inverse: rows (lane = row of one plane's block), then columns
+    const int rows_y = n, rows_c = cn;
+    {
+        const int p = l < rows_y ? 0 : (l < rows_y + rows_c ? 1 : (l < rows_y + 2 * rows_c ? 2 : 3));
+        if (p < 3) {
+            const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
+            const int i = p == 0 ? l : (p == 1 ? l - rows_y : l - rows_y - rows_c);
+            const int rs = ln == 2 ? 0 : (ln == 3 ? 1 : 2);
+            int32_t t[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) t[j] = j < sz ? L.a[o + i * sz + j] : 0;
+            if (ln == 2) idct4(t);
+            else if (ln == 3) idct8(t);
+            else idct16(t);
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                if (j < sz) {
+                    const int32_t v = rs ? (t[j] + (1 << (rs - 1))) >> rs : t[j];
+                    L.b[o + i * sz + j] = sk_clip(v, -32768, 32767);
+                }
+        }
+    }
+    wsync();
+    {
+        const int p = l < rows_y ? 0 : (l < rows_y + rows_c ? 1 : (l < rows_y + 2 * rows_c ? 2 : 3));
+        if (p < 3) {
+            const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
+            const int j = p == 0 ? l : (p == 1 ? l - rows_y : l - rows_y - rows_c);
+            int32_t t[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) t[i] = i < sz ? L.b[o + i * sz + j] : 0;
+            if (ln == 2) idct4(t);
+            else if (ln == 3) idct8(t);
+            else idct16(t);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                if (i < sz) {
+                    const int k = o + i * sz + j;
+                    L.pred[k] = (uint8_t)sk_clip255((int)L.pred[k] + ((t[i] + 8) >> 4));
+                }
+        }
+    }
+    wsync();
+    return cul | (nzm ? (1u << 24) : 0u);
+}
+
+// Block loads / stores (luma n at (x, y); chroma n/2 at (x/2, y/2)).
+__device__ __forceinline__ void load_src_blk(BlkLds& L, const FrameArgs& f, int x, int y, int n) {
+    const int l = lane(), cn = n >> 1;
+    for (int i = l; i < n * n; i += 64) L.src[i] = f.src.y[(size_t)(y + i / n) * f.stride_y + x + i % n];
+    for (int i = l; i < 2 * cn * cn; i += 64) {
+        const int p = i / (cn * cn), j = i % (cn * cn);
+        const uint8_t* P = p ? f.src.v : f.src.u;
+        L.src[(p ? 320 : 256) + j] = P[(size_t)((y >> 1) + j / cn) * f.stride_c + (x >> 1) + j % cn];
+    }
+}
+__device__ __forceinline__ void store_rec_blk(const BlkLds& L, const FrameArgs& f, int x, int y, int n) {
+    const int l = lane(), cn = n >> 1;
+    for (int i = l; i < n * n; i += 64) f.rec.y[(size_t)(y + i / n) * f.stride_y + x + i % n] = L.pred[i];
+    for (int i = l; i < 2 * cn * cn; i += 64) {
+        const int p = i / (cn * cn), j = i % (cn * cn);
+        uint8_t* P = p ? f.rec.v : f.rec.u;
+        P[(size_t)((y >> 1) + j / cn) * f.stride_c + (x >> 1) + j % cn] = L.pred[(p ? 320 : 256) + j];
+    }
+}
+
+// One predicted sample (§7.11.3.4 without scaling): the 2-D separable filter evaluated
+// for a single output (its 8 intermediate rows are those of the block process).
+// (px, py): sample position in the plane; mv in 1/8 luma pel; ss: chroma shift;
+// f4: 4-tap filters (blocks 4 wide / high).
+__device__ __forceinline__ int mc_px(const uint8_t* P, int stride, int last_x, int last_y, int px, int py, int mv_row,
+                                     int mv_col, int ss, int f4) {
+    const int px16 = (px << 4) + ((2 * mv_col) >> ss), py16 = (py << 4) + ((2 * mv_row) >> ss);
+    const int fx = px16 & 15, fy = py16 & 15, ix = px16 >> 4, iy = py16 >> 4;
+    if (fx == 0 && fy == 0) return P[(size_t)sk_clip(iy, 0, last_y) * stride + sk_clip(ix, 0, last_x)];
+    int s2 = 0;
+    for (int rr = 0; rr < 8; rr++) {
+        const int tv = subpel_tap(f4, fy, rr);
+        if (tv == 0) continue;
+        const uint8_t* row = P + (size_t)sk_clip(iy + rr - 3, 0, last_y) * stride;
+        int s1 = 0;
+        for (int tt = 0; tt < 8; tt++) s1 += subpel_tap(f4, fx, tt) * row[sk_clip(ix + tt - 3, 0, last_x)];
+        s2 += tv * ((s1 + 4) >> 3);
+    }
+    return sk_clip255((s2 + 1024) >> 11);
+}
+
+// Per-block side outputs: cells and level contexts.
+__device__ __forceinline__ void set_cells(const Av1Args& A, int r, int c, int bsl, const BlkInfo& b) {
+    const int n8 = (1 << bsl) >> 1;
+    for (int i = lane(); i < n8 * n8; i += 64) {
+        const int ry = (r >> 1) + i / n8, cx = (c >> 1) + i % n8;
+        if (ry < A.geo.r8 && cx < A.geo.c8) A.blk[(size_t)ry * A.geo.c8 + cx] = b;
+    }
+}
+__device__ __forceinline__ void set_lctx(const Av1Args& A, int p, int x4, int y4, int n4, uint8_t v) {
+    const int W = A.lctx_w[p], H = p ? A.geo.mi_rows >> 1 : A.geo.mi_rows;
+    for (int i = lane(); i < n4 * n4; i += 64) {
+        const int yy = y4 + i / n4, xx = x4 + i % n4;
+        if (yy < H && xx < W) A.lctx[p][(size_t)yy * W + xx] = v;
+    }
+}
+__device__ __forceinline__ int16_t* lev_ptr(const Av1Args& A, int r, int c, int bsl, int p) {
+    int16_t* u = A.lev + ((size_t)(r >> 2) * A.f.mb_w + (c >> 2)) * kLevPerUnit;
+    if (bsl >= 2) return u + (p == 0 ? 0 : (p == 1 ? 256 : 320));
+    const int k = ((r >> 1) & 1) * 2 + ((c >> 1) & 1);
+    return u + (p == 0 ? 64 * k : (p == 1 ? 256 + 16 * k : 320 + 16 * k));
+}
+
+// Blocks of a unit: one 16x16, or the inside 8x8s in Z order at frame edges.
+__device__ __forceinline__ int unit_blocks(const Av1Geo& g, int ur, int uc, int* rs, int* cs) {
+    const int r = ur * 4, c = uc * 4;
+    if (r >= g.mi_rows || c >= g.mi_cols) return 0;
+    if (r + 2 < g.mi_rows && c + 2 < g.mi_cols) {
+        rs[0] = r;
+        cs[0] = c;
+        return -1;   // one 16x16
+    }
+    int n = 0;
+    for (int q = 0; q < 4; q++) {
+        const int rr = r + (q >> 1) * 2, cc = c + (q & 1) * 2;
+        if (rr < g.mi_rows && cc < g.mi_cols) {
+            rs[n] = rr;
+            cs[n] = cc;
+            n++;
+        }
+    }
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_av1_setup(Av1Args A) {
+    const FrameArgs& f = A.f;
+    const int ns = f.num_slices;
+    bool key = false;
+    for (int s = threadIdx.x; s < ns; s += 256) key |= f.tasks[s].final_action == ACT_I;
+    key = __syncthreads_or(key);
+    if (key)
+        for (int s = threadIdx.x; s < ns; s += 256) {
+            f.tasks[s].final_action = ACT_I;
+            f.tasks_host[s].final_action = ACT_I;
+        }
+    if (threadIdx.x == 0) {
+        const int qidx = A.qidx_of_qp[sk_clip(f.tasks[0].qp, 0, 51)];
+        A.frame[0] = key;
+        A.frame[1] = qidx;
+        A.frame_host[0] = key;
+        A.frame_host[1] = qidx;
+    }
+}
+
+// Key frames: intra mode per block from the source edges (one wave per unit).
+__global__ __launch_bounds__(256) void k_av1_intra_modes(Av1Args A) {
+    __shared__ IntraEdge E[4];
+    if (!A.frame[0]) return;
+    const FrameArgs& f = A.f;
+    const Av1Geo& g = A.geo;
+    const int w = threadIdx.x >> 6, l = lane();
+    const int u = blockIdx.x * 4 + w;
+    if (u >= f.mb_w * f.mb_h) return;
+    const int ux = u % f.mb_w, uy = u / f.mb_w;
+    int rs[4], cs[4];
+    int nb = unit_blocks(g, uy, ux, rs, cs);
+    const int bsl = nb < 0 ? 2 : 1;
+    if (nb < 0) nb = 1;
+    for (int k = 0; k < nb; k++) {
+        const int r = rs[k], c = cs[k], log2n = bsl + 2, n = 1 << log2n;
+        const TileRect t = tile_of(g, r, c);
+        const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+        if (l == 0) intra_edges(f.src.y, f.stride_y, c * 4, r * 4, n, au, al, g.mi_cols * 4 - 1, g.mi_rows * 4 - 1, E[w]);
+        wsync();
+        const int dc = intra_dc(E[w], log2n);
+        const uint8_t cand[7] = {DC_PRED, V_PRED, H_PRED, SMOOTH_PRED, SMOOTH_V_PRED, SMOOTH_H_PRED, PAETH_PRED};
+        int best = DC_PRED, best_cost = 1 << 30;
+        for (int m = 0; m < 7; m++) {
+            int sad = 0;
+            for (int i = l; i < n * n; i += 64) {
+                const int pr = cand[m] == DC_PRED ? dc : intra_pred_px(E[w], cand[m], log2n, i / n, i % n);
+                sad += sk_abs((int)f.src.y[(size_t)(r * 4 + i / n) * f.stride_y + c * 4 + i % n] - pr);
+            }
+            sad = wsum(sad);
+            const int cost = sad + (cand[m] == DC_PRED ? 0 : n * 2);
+            if (cost < best_cost) {
+                best_cost = cost;
+                best = cand[m];
+            }
+        }
+        BlkInfo b{};
+        b.bsl = (uint8_t)bsl;
+        b.mode = (uint8_t)best;
+        b.uv_mode = DC_PRED;
+        set_cells(A, r, c, bsl, b);
+        wsync();
+    }
+}
+
+// Reconstruction of one intra block (mode from the cells) by one wave.
+__device__ void intra_rec_block(const Av1Args& A, BlkLds& L, const FdctLds& F, int r, int c, int bsl, int qidx) {
+    const FrameArgs& f = A.f;
+    const Av1Geo& g = A.geo;
+    const int l = lane(), log2n = bsl + 2, n = 1 << log2n, cn = n >> 1;
+    const int x = c * 4, y = r * 4;
+    const TileRect t = tile_of(g, r, c);
+    const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
+    BlkInfo b = A.blk[(size_t)(r >> 1) * g.c8 + (c >> 1)];
+    IntraEdge* E = L.e;
+    if (l == 0) {
+        intra_edges(f.rec.y, f.stride_y, x, y, n, au, al, g.mi_cols * 4 - 1, g.mi_rows * 4 - 1, E[0]);
+        intra_edges(f.rec.u, f.stride_c, x >> 1, y >> 1, cn, au, al, g.mi_cols * 2 - 1, g.mi_rows * 2 - 1, E[1]);
+        intra_edges(f.rec.v, f.stride_c, x >> 1, y >> 1, cn, au, al, g.mi_cols * 2 - 1, g.mi_rows * 2 - 1, E[2]);
+    }
+    load_src_blk(L, f, x, y, n);
+    wsync();
+    const int dcy = intra_dc(E[0], log2n), dcu = intra_dc(E[1], log2n - 1), dcv = intra_dc(E[2], log2n - 1);
+    for (int i = l; i < n * n; i += 64)
+        L.pred[i] = (uint8_t)(b.mode == DC_PRED ? dcy : intra_pred_px(E[0], b.mode, log2n, i / n, i % n));
+    for (int i = l; i < cn * cn; i += 64) {
+        L.pred[256 + i] = (uint8_t)dcu;
+        L.pred[320 + i] = (uint8_t)dcv;
+    }
+    wsync();
+    const uint32_t s = code_block_wave(L, F, log2n, qidx, true, lev_ptr(A, r, c, bsl, 0), lev_ptr(A, r, c, bsl, 1),
+                                       lev_ptr(A, r, c, bsl, 2));
+    store_rec_blk(L, f, x, y, n);
+    b.flags = (s >> 24) ? 0 : 2;
+    set_cells(A, r, c, bsl, b);
+    const int n4 = 1 << bsl;
+    set_lctx(A, 0, c, r, n4, (uint8_t)(s & 0xff));
+    set_lctx(A, 1, c >> 1, r >> 1, n4 >> 1, (uint8_t)((s >> 8) & 0xff));
+    set_lctx(A, 2, c >> 1, r >> 1, n4 >> 1, (uint8_t)((s >> 16) & 0xff));
+    wsync();
+}
+
+// Key frames: one workgroup (16 waves) per tile; unit (x, y) of the tile at step x + y.
+__global__ __launch_bounds__(1024) void k_av1_intra_rec(Av1Args A) {
+    __shared__ BlkLds Lw[16];
+    __shared__ FdctLds F;
+    if (!A.frame[0]) return;
+    const Av1Geo& g = A.geo;
+    const int t = blockIdx.x;
+    const TileRect tr = tile_rect(g, t);
+    load_fdct(F);
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    const int ux0 = tr.mi_col0 >> 2, uy0 = tr.mi_row0 >> 2;
+    const int uw = (tr.mi_col1 - tr.mi_col0 + 3) >> 2, uh = (tr.mi_row1 - tr.mi_row0 + 3) >> 2;
+    const int qidx = A.frame[1];
+    const int steps = uw + uh - 1;
+    for (int s = 0; s < steps; s++) {
+        for (int y = w; y < uh; y += 16) {
+            const int x = s - y;
+            if (x < 0 || x >= uw) continue;
+            int rs[4], cs[4];
+            int nb = unit_blocks(g, uy0 + y, ux0 + x, rs, cs);
+            const int bsl = nb < 0 ? 2 : 1;
+            if (nb < 0) nb = 1;
+            for (int k = 0; k < nb; k++) intra_rec_block(A, Lw[w], F, rs[k], cs[k], bsl, qidx);
+        }
+        __syncthreads();
+    }
+}
+
+// Inter frames: one wave per unit, vector from the front end's motion search.
+__global__ __launch_bounds__(256) void k_av1_inter(Av1Args A) {
+    __shared__ BlkLds Lw[4];
+    __shared__ FdctLds F;
+    if (A.frame[0]) return;
+    const FrameArgs& f = A.f;
+    const Av1Geo& g = A.geo;
+    load_fdct(F);
+    __syncthreads();
+    const int w = threadIdx.x >> 6, l = lane();
+    const int u = blockIdx.x * 4 + w;
+    if (u >= f.mb_w * f.mb_h) return;
+    BlkLds& L = Lw[w];
+    const int ux = u % f.mb_w, uy = u / f.mb_w;
+    const SliceTask t = f.tasks[uy / f.rows_per_slice];
+    const h264::MeResult me = f.me[u];
+    const bool moving = t.final_action == ACT_P;
+    const int mv_row = moving ? 8 * me.mvy : 0, mv_col = moving ? 8 * me.mvx : 0;
+    const int qidx = A.frame[1];
+    int rs[4], cs[4];
+    int nb = unit_blocks(g, uy, ux, rs, cs);
+    const int bsl = nb < 0 ? 2 : 1;
+    if (nb < 0) nb = 1;
+    const int lxc = ((g.W + 1) >> 1) - 1, lyc = ((g.H + 1) >> 1) - 1;
+    for (int k = 0; k < nb; k++) {
+        const int r = rs[k], c = cs[k], log2n = bsl + 2, n = 1 << log2n, cn = n >> 1;
+        const int x = c * 4, y = r * 4;
+        load_src_blk(L, f, x, y, n);
+        for (int i = l; i < n * n; i += 64)
+            L.pred[i] = (uint8_t)mc_px(f.ref.y, f.stride_y, g.W - 1, g.H - 1, x + i % n, y + i / n, mv_row, mv_col, 0, n <= 4);
+        for (int i = l; i < 2 * cn * cn; i += 64) {
+            const int p = i / (cn * cn), j = i % (cn * cn);
+            L.pred[(p ? 320 : 256) + j] = (uint8_t)mc_px(p ? f.ref.v : f.ref.u, f.stride_c, lxc, lyc, (x >> 1) + j % cn,
+                                                          (y >> 1) + j / cn, mv_row, mv_col, 1, cn <= 4);
+        }
+        wsync();
+        const uint32_t s = code_block_wave(L, F, log2n, qidx, false, lev_ptr(A, r, c, bsl, 0),
+                                           lev_ptr(A, r, c, bsl, 1), lev_ptr(A, r, c, bsl, 2));
+        store_rec_blk(L, f, x, y, n);
+        BlkInfo b{};
+        b.bsl = (uint8_t)bsl;
+        b.flags = (uint8_t)(1 | ((s >> 24) ? 0 : 2));
+        b.mv_row = (int16_t)mv_row;
+        b.mv_col = (int16_t)mv_col;
+        b.mode = GLOBALMV;
+        set_cells(A, r, c, bsl, b);
+        const int n4 = 1 << bsl;
+        set_lctx(A, 0, c, r, n4, (uint8_t)(s & 0xff));
+        set_lctx(A, 1, c >> 1, r >> 1, n4 >> 1, (uint8_t)((s >> 8) & 0xff));
+        set_lctx(A, 2, c >> 1, r >> 1, n4 >> 1, (uint8_t)((s >> 16) & 0xff));
+        wsync();
+    }
+}
+
+// Static merging per superblock: lane = 8x8 cell of the SB (8 x 8 cells).
+__global__ __launch_bounds__(64) void k_av1_merge(Av1Args A) {
+    if (A.frame[0]) return;
+    const Av1Geo& g = A.geo;
+    const int sb = blockIdx.x, sr = sb / g.sb_cols, sc = sb % g.sb_cols;
+    const int l = lane(), cy = sr * 8 + (l >> 3), cx = sc * 8 + (l & 7);
+    const bool in = cy < g.r8 && cx < g.c8;
+    for (int lvl = 3; lvl <= 4; lvl++) {
+        const int sz = 1 << lvl, half = sz >> 1, cells = sz >> 1;
+        // region of this lane
+        const int r = (cy & ~(cells - 1)) * 2, c = (cx & ~(cells - 1)) * 2;
+        const bool fits = r + half < g.mi_rows && c + half < g.mi_cols;
+        const BlkInfo b0 = A.blk[(size_t)(r >> 1) * g.c8 + (c >> 1)];
+        const BlkInfo me = in ? A.blk[(size_t)cy * g.c8 + cx] : b0;
+        const bool ok_me = !in || (blk_skip(me) && me.mv_row == b0.mv_row && me.mv_col == b0.mv_col);
+        // all lanes of the region must agree: reduce over the region's lanes
+        const uint64_t bad = __ballot(!ok_me);
+        uint64_t mask = 0;
+        for (int k = 0; k < 64; k++) {
+            const int ky = sr * 8 + (k >> 3), kx = sc * 8 + (k & 7);
+            if ((ky & ~(cells - 1)) * 2 == r && (kx & ~(cells - 1)) * 2 == c) mask |= 1ull << k;
+        }
+        wsync();
+        if (fits && !(bad & mask) && in) {
+            BlkInfo m = b0;
+            m.bsl = (uint8_t)lvl;
+            A.blk[(size_t)cy * g.c8 + cx] = m;
+        }
+        wsync();
+        __threadfence_block();
+    }
+}
+
+// Inter modes from the MV stack: one lane per 8x8 cell, block origins only.
+__global__ __launch_bounds__(256) void k_av1_modes(Av1Args A) {
+    if (A.frame[0]) return;
+    const Av1Geo& g = A.geo;
+    const int cell = blockIdx.x * 256 + threadIdx.x;
+    if (cell >= g.c8 * g.r8) return;
+    const int y8 = cell / g.c8, x8 = cell % g.c8;
+    const BlkInfo b = A.blk[cell];
+    const int n8 = (1 << b.bsl) >> 1;
+    if ((y8 & (n8 - 1)) || (x8 & (n8 - 1))) return;
+    const int r = y8 * 2, c = x8 * 2;
+    const TileRect t = tile_of(g, r, c);
+    MvStack s;
+    const BlkGrid grid{A.blk, g.c8};
+    find_mv_stack(s, grid, t, g.mi_rows, g.mi_cols, r, c, b.bsl, DecodedBefore{r, c});
+    int mode, idx = 0;
+    if (b.mv_row == 0 && b.mv_col == 0) mode = GLOBALMV;
+    else if (b.mv_row == s.mv[0][0] && b.mv_col == s.mv[0][1]) mode = NEARESTMV;
+    else if (s.n >= 2 && b.mv_row == s.mv[1][0] && b.mv_col == s.mv[1][1]) {
+        mode = NEARMV;
+        idx = 1;
+    } else mode = NEWMV;
+    for (int yy = 0; yy < n8; yy++)
+        for (int xx = 0; xx < n8; xx++)
+            if (y8 + yy < g.r8 && x8 + xx < g.c8) {
+                BlkInfo& d = A.blk[(size_t)(y8 + yy) * g.c8 + x8 + xx];
+                d.mode = (uint8_t)mode;
+                d.flags = (uint8_t)((d.flags & 0x0f) | (idx << 4));
+            }
+}
+
+// Block syntax -> tokens, one lane per 16x16 unit.
+__global__ __launch_bounds__(64) void k_av1_tokens(Av1Args A) {
+    const int u = blockIdx.x * 64 + threadIdx.x;
+    const FrameArgs& f = A.f;
+    if (u >= f.mb_w * f.mb_h) return;
+    const Av1Geo& g = A.geo;
+    FrameView v;
+    v.geo = g;
+    v.blk = A.blk;
+    v.lev = A.lev;
+    for (int p = 0; p < 3; p++) {
+        v.lctx[p] = A.lctx[p];
+        v.lctx_w[p] = A.lctx_w[p];
+    }
+    v.unit_w = f.mb_w;
+    v.qidx = A.frame[1];
+    v.key = A.frame[0];
+    const int ux = u % f.mb_w, uy = u / f.mb_w;
+    TokenSink sink{A.tok + (size_t)u * kTokCap, 0, kTokCap, 0u, 0};
+    const TileRect t = tile_of(g, uy * 4, ux * 4);
+    code_unit(sink, AV1_DEFAULT_CDF[0], v, t, ux, uy);
+    sink.flush();
+    A.tok_n[u] = sink.n;
+}
+
+struct ChunkSink {
     uint16_t* p;
-    int n;
-    __device__ void push(uint16_t x) { p[n++] = x; }
+    int n, cap;
+    __device__ void push(uint16_t x) {
+        if (n < cap) p[n] = x;
+        n++;
+    }
 };
 
-// sym word: kind << 30 | ctx << 20 | value (kind 0 symbol, 1 bool, 2 literal of ctx bits)
-__global__ __launch_bounds__(64) void k_av1_ec_tiles(const uint32_t* syms, const int32_t* sym_off,
-                                                      const int32_t* sym_n, const uint16_t* cdf_init,
-                                                      const int32_t* nsym, int n_ctx, int adapt,
-                                                      uint16_t* chunks, uint8_t* out, int32_t* out_size) {
-    __shared__ uint16_t cdf[kMaxCtx * 17];
+// One wave per tile: the tile's CDFs in LDS, lane 0 codes the tokens in order.
+__global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
+    __shared__ CdfContext cx;
+    const Av1Geo& g = A.geo;
     const int t = blockIdx.x;
-    for (int i = threadIdx.x; i < n_ctx * 17; i += 64) cdf[i] = cdf_init[i];
+    const int q = coef_qctx(A.frame[1]);
+    const uint16_t* src = (const uint16_t*)&AV1_DEFAULT_CDF[q];
+    uint16_t* dst = (uint16_t*)&cx;
+    for (int i = threadIdx.x; i < (int)(sizeof(CdfContext) / 2); i += 64) dst[i] = src[i];
     __syncthreads();
     if (threadIdx.x != 0) return;
-    const int off = sym_off[t], n = sym_n[t];
-    DevSink sink{chunks + 2 * (size_t)off + 8 * (size_t)t, 0};
-    SymbolCoder<DevSink> coder(sink);
-    for (int i = 0; i < n; i++) {
-        const uint32_t w = syms[off + i];
-        const int kind = (int)(w >> 30), c = (int)((w >> 20) & 1023u), v = (int)(w & 0xfffffu);
-        if (kind == 1) {
-            coder.bool_(v);
-        } else if (kind == 2) {
-            coder.literal((uint32_t)v, c);
-        } else if (adapt) {
-            coder.encode_adapt(cdf + c * 17, nsym[c], v);
-        } else {
-            coder.encode(cdf + c * 17, nsym[c], v);
-        }
+    const TileRect tr = tile_rect(g, t);
+    ChunkSink sink{A.chunks + (size_t)t * A.tile_cap, 0, A.tile_cap};
+    SymbolCoder<ChunkSink> coder(sink);
+    int ux, uy;
+    for (int i = 0; tile_unit(g, tr, i, &ux, &uy); i++) {
+        if (ux * 4 >= g.mi_cols || uy * 4 >= g.mi_rows) continue;
+        const int u = uy * A.f.mb_w + ux;
+        const int n = sk_min(A.tok_n[u], kTokCap);
+        const uint32_t* tk = A.tok + (size_t)u * kTokCap;
+        for (int k = 0; k < n; k++) code_token(coder, dst, tk[k]);
     }
     coder.finish();
-    carry_bytes(sink.p, sink.n, out + 2 * (size_t)off + 8 * (size_t)t);
-    out_size[t] = sink.n;
+    A.tile_size[t] = sink.n <= A.tile_cap ? sink.n : -1;
 }
 
-}  // namespace sk::av1
-
-extern "C" {
-
-// Test entry: codes `tiles` independent symbol lists on the GPU (device 0) and
-// copies each tile's bytes to out + 2 * sym_off[t] + 8 * t, sizes to out_size.
-// Returns 0, or < 0 on a HIP error / too many contexts.
-int sk_av1_ec_encode_tiles_hip(const uint32_t* syms, const int32_t* sym_off, const int32_t* sym_n, int tiles,
-                               const uint16_t* cdfs, const int32_t* nsym, int n_ctx, int adapt, uint8_t* out,
-                               int32_t* out_size) {
-    if (n_ctx > sk::av1::kMaxCtx || tiles <= 0) return -1;
-    int total = 0;
-    for (int t = 0; t < tiles; t++) {
-        if (sym_off[t] < 0 || sym_n[t] < 0) return -1;
-        total = sym_off[t] + sym_n[t] > total ? sym_off[t] + sym_n[t] : total;
+// Tile bytes (carry-resolved) -> host-mapped output at the tiles' prefix offsets.
+__global__ __launch_bounds__(256) void k_av1_pack(Av1Args A) {
+    __shared__ int off_s, n_s;
+    const int t = blockIdx.x;
+    if (threadIdx.x == 0) {
+        int off = 0;
+        for (int k = 0; k < t; k++) off += sk_max(A.tile_size[k], 0);
+        n_s = A.tile_size[t];
+        off_s = off;
+        A.out_size_host[t] = (n_s >= 0 && off + n_s <= A.out_cap) ? n_s : -1;
     }
-    for (int c = 0; c < n_ctx; c++) if (nsym[c] < 2 || nsym[c] > 16) return -1;
-    for (int i = 0; i < total; i++) {   // the kernel indexes LDS by these: validate on the host
-        const uint32_t w = syms[i];
-        const int kind = (int)(w >> 30), c = (int)((w >> 20) & 1023u), v = (int)(w & 0xfffffu);
-        if (kind == 0 && (c >= n_ctx || v >= nsym[c])) return -1;
-        if (kind == 2 && (c < 1 || c > 20)) return -1;
-        if (kind == 3) return -1;
-    }
-    const size_t out_cap = 2 * (size_t)total + 8 * (size_t)tiles;
-    uint32_t* d_syms = nullptr;
-    int32_t *d_off = nullptr, *d_n = nullptr, *d_nsym = nullptr, *d_size = nullptr;
-    uint16_t *d_cdf = nullptr, *d_chunks = nullptr;
-    uint8_t* d_out = nullptr;
-    int rc = 0;
-    auto ok = [&](hipError_t e) { if (e != hipSuccess && rc == 0) rc = -2; return rc == 0; };
-    if (ok(hipMalloc(&d_syms, sizeof(uint32_t) * (total > 0 ? total : 1))) &&
-        ok(hipMalloc(&d_off, sizeof(int32_t) * tiles)) && ok(hipMalloc(&d_n, sizeof(int32_t) * tiles)) &&
-        ok(hipMalloc(&d_nsym, sizeof(int32_t) * n_ctx)) && ok(hipMalloc(&d_size, sizeof(int32_t) * tiles)) &&
-        ok(hipMalloc(&d_cdf, sizeof(uint16_t) * 17 * n_ctx)) &&
-        ok(hipMalloc(&d_chunks, sizeof(uint16_t) * out_cap)) && ok(hipMalloc(&d_out, out_cap)) &&
-        ok(hipMemcpy(d_syms, syms, sizeof(uint32_t) * total, hipMemcpyHostToDevice)) &&
-        ok(hipMemcpy(d_off, sym_off, sizeof(int32_t) * tiles, hipMemcpyHostToDevice)) &&
-        ok(hipMemcpy(d_n, sym_n, sizeof(int32_t) * tiles, hipMemcpyHostToDevice)) &&
-        ok(hipMemcpy(d_nsym, nsym, sizeof(int32_t) * n_ctx, hipMemcpyHostToDevice)) &&
-        ok(hipMemcpy(d_cdf, cdfs, sizeof(uint16_t) * 17 * n_ctx, hipMemcpyHostToDevice))) {
-        hipLaunchKernelGGL(sk::av1::k_av1_ec_tiles, dim3(tiles), dim3(64), 0, 0, d_syms, d_off, d_n, d_cdf, d_nsym,
-                           n_ctx, adapt, d_chunks, d_out, d_size);
-        if (ok(hipGetLastError()) && ok(hipDeviceSynchronize())) {
-            ok(hipMemcpy(out, d_out, out_cap, hipMemcpyDeviceToHost));
-            ok(hipMemcpy(out_size, d_size, sizeof(int32_t) * tiles, hipMemcpyDeviceToHost));
+    __syncthreads();
+    const int n = n_s, off = off_s;
+    if (n < 0 || off + n > A.out_cap) return;
+    const uint16_t* ch = A.chunks + (size_t)t * A.tile_cap;
+    // carry_bytes: byte i = (sum of chunks >= i with carries) -- resolve with a serial
+    // backwards pass on lane 0 into the chunk buffer, then copy out in parallel
+    if (threadIdx.x == 0) {
+        uint16_t* c2 = A.chunks + (size_t)t * A.tile_cap;
+        uint32_t carry = 0;
+        for (int i = n - 1; i >= 0; i--) {
+            carry += c2[i];
+            c2[i] = (uint16_t)(carry & 0xff);
+            carry >>= 8;
         }
     }
-    hipFree(d_syms); hipFree(d_off); hipFree(d_n); hipFree(d_nsym); hipFree(d_size);
-    hipFree(d_cdf); hipFree(d_chunks); hipFree(d_out);
-    return rc;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 256) A.out_host[off + i] = (uint8_t)ch[i];
 }
 
-}  // extern "C"
+// Rows below the picture repeat its last row (the reference clamp AV1's MC reads),
+// and every slice's reconstruction becomes the reference (k_commit copies rec -> ref
+// for every slice that is not ACT_NONE; vectors of re-coded static slices are zero).
+__global__ __launch_bounds__(256) void k_av1_finish(Av1Args A) {
+    const FrameArgs& f = A.f;
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    const int H = A.geo.H, Hc = (H + 1) >> 1;
+    if (x < f.stride_y)
+        for (int y = H; y < f.mb_h * 16; y++) f.rec.y[(size_t)y * f.stride_y + x] = f.rec.y[(size_t)(H - 1) * f.stride_y + x];
+    if (x < f.stride_c)
+        for (int y = Hc; y < f.mb_h * 8; y++) {
+            f.rec.u[(size_t)y * f.stride_c + x] = f.rec.u[(size_t)(Hc - 1) * f.stride_c + x];
+            f.rec.v[(size_t)y * f.stride_c + x] = f.rec.v[(size_t)(Hc - 1) * f.stride_c + x];
+        }
+    if (blockIdx.x == 0)
+        for (int s = threadIdx.x; s < f.num_slices; s += 256) {
+            const int fa = f.tasks[s].final_action;
+            if (fa == ACT_NONE || fa == ACT_SKIPALL) {
+                f.tasks[s].final_action = ACT_SKIPALL;
+                f.tasks_host[s].final_action = ACT_SKIPALL;
+            }
+        }
+}
+
+void launch_backend(const Av1Args& a, hipStream_t s) {
+    const int n = a.f.mb_w * a.f.mb_h;
+    const int tiles = a.geo.tile_cols * a.geo.tile_rows;
+    hipLaunchKernelGGL(k_av1_setup, dim3(1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_intra_modes, dim3((n + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_intra_rec, dim3(tiles), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_av1_inter, dim3((n + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_merge, dim3(a.geo.sb_cols * a.geo.sb_rows), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_av1_modes, dim3((a.geo.c8 * a.geo.r8 + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_tokens, dim3((n + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_finish, dim3((a.f.stride_y + 255) / 256), dim3(256), 0, s, a);
+}
+
+}  // namespace gpu
+}  // namespace av1
+}  // namespace sk

@@ -108,8 +108,8 @@ class CaptureSession {
                 e.aq_strength = sk_clip(s.h264_aq_strength, 0, 64);
                 e.subpel = s.h264_subpel >= 0 ? 1 : 0;
                 e.intra4x4 = s.h264_intra4x4 > 0 ? 1 : 0;
-                if (s.output_mode == 2) {   // HEVC: full-frame pictures, slices of CTB rows
-                    e.codec = 1;
+                if (s.output_mode == 2 || s.output_mode == 3) {   // HEVC / AV1: full-frame pictures
+                    e.codec = s.output_mode == 2 ? 1 : 2;
                     e.fullframe = 1;
                     e.aq_strength = 0;
                     e.intra4x4 = 0;
@@ -195,10 +195,11 @@ class CaptureSession {
     static constexpr double kHistLe[kHist - 1] = {0.25, 0.5, 1, 2, 4, 8, 16, 33};
     void stats(double* out, int n) {
         std::lock_guard<std::mutex> g(mu_);
-        double v[6 + kHist] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
+        double v[7 + kHist] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
                                (double)packets_, src_kind_, last_enc_ms_};
         for (int i = 0; i < kHist; i++) v[6 + i] = (double)hist_[i];
-        for (int i = 0; i < n && i < 6 + kHist; i++) out[i] = v[i];
+        v[6 + kHist] = (double)inflight_max_;   // frames in flight actually used (1 or 2)
+        for (int i = 0; i < n && i < 7 + kHist; i++) out[i] = v[i];
     }
     // Capture-to-packets latency (ms) of the most recent frames, oldest first;
     // returns the count copied. reset != 0 clears the record afterwards.
@@ -291,7 +292,7 @@ class CaptureSession {
         for (int i = 0; i < n; i++) {
             h264::EncodedPacket& p = enc_->packets_[i];
             sk_stripe_result& r = res[i];
-            r.type = s_.output_mode == 0 ? 0 : (s_.output_mode == 2 ? 2 : 1);
+            r.type = s_.output_mode == 0 ? 0 : (s_.output_mode >= 2 ? s_.output_mode : 1);
             r.stripe_y_start = p.y;
             r.stripe_height = p.h;
             r.size = (int32_t)p.data.size();
@@ -385,6 +386,7 @@ class CaptureSession {
                     else if (step) step_failed();
                 }
             }
+            if ((int)q.size() > inflight_max_) inflight_max_ = (int)q.size();
             int n = -1;
             try {
                 n = enc_->finish();
@@ -494,6 +496,7 @@ class CaptureSession {
     uint64_t lat_count_ = 0;
     sk_capture_settings s_{};
     std::string display_;
+    int inflight_max_ = 0;
     sk_stripe_cb cb_ = nullptr;
     void* user_ = nullptr;
     std::unique_ptr<FrameSource> src_;

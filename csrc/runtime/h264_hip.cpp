@@ -9,6 +9,8 @@
 #include "trace.h"
 #include "../kernels/h264_gpu.h"
 #include "../kernels/hevc_gpu.h"
+#include "../kernels/av1_gpu.h"
+#include "../codec/av1_encoder.h"
 #include "../kernels/runtime_kernels.h"
 #include "../codec/hevc_encoder.h"
 #include <hip/hip_runtime.h>
@@ -46,6 +48,7 @@ class HipBackend : public EncoderBackend {
         if (cfg_.shared_copy) copy_stream_ = device_copy_stream(device_);
         alloc();
         if (cfg_.codec == 1) alloc_hevc();
+        if (cfg_.codec == 2) alloc_av1();
     }
     ~HipBackend() override {
         hipSetDevice(device_);
@@ -326,6 +329,14 @@ class HipBackend : public EncoderBackend {
         else if (s == "ref1_y") { p = args_.ref1.y; n = (int64_t)ny; }
         else if (s == "fs_mv") { p = args_.fs_mv; n = (int64_t)g_.num_mbs() * 4; }
         else if (s == "mbs") { p = args_.mbs; n = (int64_t)g_.num_mbs() * sizeof(MbInfo); }
+        else if (s == "blk" && cfg_.codec == 2) { p = aargs_.blk; n = (int64_t)av1_geo_.c8 * av1_geo_.r8 * sizeof(av1::BlkInfo); }
+        else if (s == "levels" && cfg_.codec == 2) { p = aargs_.lev; n = (int64_t)g_.num_mbs() * av1::gpu::kLevPerUnit * 2; }
+        else if (s == "tok_n" && cfg_.codec == 2) { p = aargs_.tok_n; n = (int64_t)g_.num_mbs() * 4; }
+        else if (s == "tile_size" && cfg_.codec == 2) { p = aargs_.tile_size; n = (int64_t)av1_geo_.tile_cols * av1_geo_.tile_rows * 4; }
+        else if (s == "av1_geo" && cfg_.codec == 2) {
+            if (dst && cap >= (int64_t)sizeof(av1_geo_)) memcpy(dst, &av1_geo_, sizeof(av1_geo_));
+            return (int64_t)sizeof(av1_geo_);
+        }
         else if (s == "coefs" && cfg_.codec == 1) { p = hargs_.coefs; n = (int64_t)g_.num_mbs() * hevc::kCoefPerCu * 2; }
         else if (s == "cus" && cfg_.codec == 1) { p = hargs_.cus; n = (int64_t)g_.num_mbs() * sizeof(hevc::CuInfo); }
         else if (s == "bin_n" && cfg_.codec == 1) { p = hargs_.bin_n; n = (int64_t)g_.num_mbs() * 4; }
@@ -524,7 +535,15 @@ class HipBackend : public EncoderBackend {
             HIPCHECK(hipMemcpyAsync(ov_params_dev_, ov_params_host_[parity_], sizeof(OverlayParams) * kOverlaySlots,
                                     hipMemcpyHostToDevice, stream_));
             gpu::launch_convert_damage(args_, stream_);
-            if (cfg_.codec == 1) {
+            if (cfg_.codec == 2) {
+                gpu::launch_frontend(args_, stream_);
+                av1::gpu::Av1Args aa = aargs_;
+                aa.f = args_;
+                aa.frame_host = av1_frame_dev_[parity_];
+                aa.out_host = av1_out_dev_[parity_];
+                aa.out_size_host = av1_size_dev_[parity_];
+                av1::gpu::launch_backend(aa, stream_);
+            } else if (cfg_.codec == 1) {
                 gpu::launch_frontend(args_, stream_);
                 hevc::gpu::HevcArgs ha = hargs_;
                 ha.f = args_;
@@ -595,6 +614,97 @@ class HipBackend : public EncoderBackend {
         hevc::build_parameter_sets(g_.W, g_.H, cfg_.full_range, cfg_.fps, hevc_params_);
     }
 
+    // AV1 back-end buffers (av1_gpu.h): cells, levels, level contexts, token slots per
+    // 16x16 unit, coder chunks per tile, host-mapped frame info and tile bytes.
+    void alloc_av1() {
+        const int n = g_.num_mbs();
+        av1::gpu::Av1Args& a = aargs_;
+        memset(&a, 0, sizeof(a));
+        const int sbc = (g_.W + 63) / 64, sbr = (g_.H + 63) / 64;
+        const int tc = cfg_.tile_cols_log2 >= 0 ? cfg_.tile_cols_log2 : av1::tile_log2(1, std::min(8, sbc));
+        const int tr = cfg_.tile_rows_log2 >= 0 ? cfg_.tile_rows_log2 : av1::tile_log2(1, std::min(8, sbr));
+        av1::geo_init(av1_geo_, g_.W, g_.H, tc, tr);
+        a.geo = av1_geo_;
+        a.blk = dmalloc<av1::BlkInfo>((size_t)av1_geo_.c8 * av1_geo_.r8);
+        a.lev = dmalloc<int16_t>((size_t)n * av1::gpu::kLevPerUnit);
+        a.lctx_w[0] = av1_geo_.mi_cols;
+        a.lctx_w[1] = a.lctx_w[2] = av1_geo_.mi_cols >> 1;
+        a.lctx[0] = dmalloc<uint8_t>((size_t)av1_geo_.mi_cols * av1_geo_.mi_rows);
+        a.lctx[1] = dmalloc<uint8_t>((size_t)(av1_geo_.mi_cols >> 1) * (av1_geo_.mi_rows >> 1));
+        a.lctx[2] = dmalloc<uint8_t>((size_t)(av1_geo_.mi_cols >> 1) * (av1_geo_.mi_rows >> 1));
+        a.tok = dmalloc<uint32_t>((size_t)n * av1::gpu::kTokCap, false);
+        a.tok_n = dmalloc<int>(n);
+        a.frame = dmalloc<int>(4);
+        const int tiles = av1_geo_.tile_cols * av1_geo_.tile_rows;
+        // coder chunks: 4 KB per unit of the largest tile (incompressible content codes
+        // below ~1.5 bytes per sample)
+        const int tile_units = (av1_geo_.tile_w_sb * 4) * (av1_geo_.tile_h_sb * 4);
+        a.tile_cap = tile_units * 4096;
+        a.chunks = dmalloc<uint16_t>((size_t)tiles * a.tile_cap, false);
+        a.tile_size = dmalloc<int>(tiles);
+        a.out_cap = g_.W * g_.H * 3 + 4096;
+        std::vector<uint8_t> q(52);
+        for (int i = 0; i < 52; i++) q[i] = (uint8_t)av1::qidx_for_qp(i);
+        uint8_t* dq = dmalloc<uint8_t>(52);
+        HIPCHECK(hipMemcpy(dq, q.data(), 52, hipMemcpyHostToDevice));
+        a.qidx_of_qp = dq;
+        void* dptr = nullptr;
+        for (int p = 0; p < 2; p++) {
+            av1_out_[p] = hmalloc<uint8_t>((size_t)a.out_cap);
+            av1_size_[p] = hmalloc<int>(tiles, hipHostMallocCoherent);
+            av1_frame_[p] = hmalloc<int>(4, hipHostMallocCoherent);
+            HIPCHECK(hipHostGetDevicePointer(&dptr, av1_out_[p], 0));
+            av1_out_dev_[p] = (uint8_t*)dptr;
+            HIPCHECK(hipHostGetDevicePointer(&dptr, av1_size_[p], 0));
+            av1_size_dev_[p] = (int*)dptr;
+            HIPCHECK(hipHostGetDevicePointer(&dptr, av1_frame_[p], 0));
+            av1_frame_dev_[p] = (int*)dptr;
+        }
+        HIPCHECK(hipStreamSynchronize(stream_));
+        av1_level_ = av1::choose_level_idx(g_.W, g_.H, cfg_.fps);
+    }
+
+    void build_packets_av1(int par, uint16_t frame_id) {
+        const int tiles = av1_geo_.tile_cols * av1_geo_.tile_rows;
+        av1::FrameParams fp;
+        fp.key = av1_frame_[par][0];
+        fp.qidx = av1_frame_[par][1];
+        std::vector<std::vector<uint8_t>> tl(tiles);
+        size_t off = 0;
+        for (int t = 0; t < tiles; t++) {
+            const int n = av1_size_[par][t];
+            if (n < 0) throw std::runtime_error("AV1 tile exceeded its output capacity");
+            tl[t].assign(av1_out_[par] + off, av1_out_[par] + off + n);
+            off += (size_t)n;
+        }
+        size_t maxsz = 1;
+        for (int t = 0; t + 1 < tiles; t++) maxsz = std::max(maxsz, tl[t].size());
+        fp.tile_size_bytes = maxsz <= 0x100 ? 1 : (maxsz <= 0x10000 ? 2 : (maxsz <= 0x1000000 ? 3 : 4));
+        EncodedPacket pk;
+        pk.y = 0; pk.w = g_.W; pk.h = g_.H; pk.key = fp.key;
+        pk.data.resize(10);
+        write_stripe_header(pk.data.data(), fp.key, frame_id, 0, g_.W, g_.H);
+        av1::append_obu(pk.data, 2, nullptr, 0);
+        if (fp.key) {
+            av1::BitWriter sh;
+            av1::write_sequence_header(sh, g_.W, g_.H, av1_level_, cfg_.full_range);
+            av1::append_obu(pk.data, 1, sh.buf.data(), sh.buf.size());
+        }
+        av1::BitWriter fh;
+        av1::write_frame_header(fh, av1_geo_, fp);
+        std::vector<uint8_t> payload = fh.buf;
+        if (tiles > 1) payload.push_back(0);
+        for (int t = 0; t < tiles; t++) {
+            if (t + 1 < tiles) {
+                const uint32_t sz = (uint32_t)tl[t].size() - 1;
+                for (int k = 0; k < fp.tile_size_bytes; k++) payload.push_back((uint8_t)(sz >> (8 * k)));
+            }
+            payload.insert(payload.end(), tl[t].begin(), tl[t].end());
+        }
+        av1::append_obu(pk.data, 6, payload.data(), payload.size());
+        packets_.push_back(std::move(pk));
+    }
+
     void build_packets_hevc(int par, uint16_t frame_id) {
         const SliceTask* h_tasks = h_tasks_[par];
         const int ns = g_.num_slices;
@@ -619,6 +729,10 @@ class HipBackend : public EncoderBackend {
     }
 
     void build_packets(int par, uint16_t frame_id) {
+        if (cfg_.codec == 2) {
+            build_packets_av1(par, frame_id);
+            return;
+        }
         if (cfg_.codec == 1) {
             build_packets_hevc(par, frame_id);
             return;
@@ -661,6 +775,15 @@ class HipBackend : public EncoderBackend {
     Controller ctl_;
     int device_;
     hevc::gpu::HevcArgs hargs_;
+    av1::gpu::Av1Args aargs_;
+    av1::Av1Geo av1_geo_;
+    int av1_level_ = 8;
+    uint8_t* av1_out_[2] = {nullptr, nullptr};
+    uint8_t* av1_out_dev_[2] = {nullptr, nullptr};
+    int* av1_size_[2] = {nullptr, nullptr};
+    int* av1_size_dev_[2] = {nullptr, nullptr};
+    int* av1_frame_[2] = {nullptr, nullptr};
+    int* av1_frame_dev_[2] = {nullptr, nullptr};
     uint8_t* hevc_out_[2] = {nullptr, nullptr};
     uint8_t* hevc_out_dev_[2] = {nullptr, nullptr};
     int* hevc_size_[2] = {nullptr, nullptr};

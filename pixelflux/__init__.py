@@ -32,7 +32,8 @@ FrameCallback = _native.SK_FRAME_CB
 
 OUTPUT_MODE_JPEG = 0
 OUTPUT_MODE_H264 = 1
-OUTPUT_MODE_HEVC = 2   # extension: H.265 stripes
+OUTPUT_MODE_HEVC = 2   # extension: H.265 full-frame pictures
+OUTPUT_MODE_AV1 = 3    # extension: AV1 temporal units (OBUs), full frame
 SOURCE_POOL = 4        # extension: caller-owned frame pool (settings.pool / pool_frames)
 
 
@@ -148,13 +149,14 @@ class ScreenCapture:
             self._lib.sk_capture_set_qp(self._h, int(qp), int(paint_qp))
 
     def stats(self) -> dict:
-        arr = (ctypes.c_double * 15)()
-        self._lib.sk_capture_stats(self._h, arr, 15)
+        arr = (ctypes.c_double * 16)()
+        self._lib.sk_capture_stats(self._h, arr, 16)
         return {"frames": int(arr[0]), "encode_ms_mean": arr[1], "bytes": int(arr[2]),
                 "packets": int(arr[3]), "source": {1.0: "x11", 0.0: "synthetic"}.get(arr[4], "none"),
                 "encode_ms_last": arr[5],
                 # per-frame encode time histogram (native, bucket upper bounds in ms; last = +Inf)
-                "encode_ms_buckets": list(ENCODE_MS_BUCKETS), "encode_ms_counts": [int(x) for x in arr[6:15]]}
+                "encode_ms_buckets": list(ENCODE_MS_BUCKETS), "encode_ms_counts": [int(x) for x in arr[6:15]],
+                "frames_in_flight": int(arr[15])}
 
     def close(self) -> None:
         self.stop_capture()

@@ -114,7 +114,9 @@ async def wait_ready(port: int, timeout: float = 90.0):
 async def client(port: int, args, t_start: float, t_end: float, out: dict):
     grabs: dict = {}
     seen: set = set()
-    lat_ms: list = []
+    lat_ms: list = []        # grab -> first stripe of the frame received
+    lat_last_ms: list = []   # grab -> last stripe of the frame received (whole frame on the client)
+    cur = {"fid": None, "grab": None, "last": 0, "count": False}
     frames = 0
     last_fid = None
     bytes_rx = 0
@@ -151,6 +153,12 @@ async def client(port: int, args, t_start: float, t_end: float, out: dict):
                             fid = (d[2] << 8) | d[3]
                             last_fid = fid
                             bytes_rx += len(d)
+                            if fid != cur["fid"]:
+                                # the previous frame's stripes are complete: its last one arrived at cur["last"]
+                                if cur["count"] and cur["grab"] is not None:
+                                    lat_last_ms.append((cur["last"] - cur["grab"]) / 1e6)
+                                cur.update(fid=fid, grab=None, count=False)
+                            cur["last"] = now_ns
                             if fid not in seen:
                                 seen.add(fid)
                                 if len(seen) > 4096:
@@ -158,13 +166,14 @@ async def client(port: int, args, t_start: float, t_end: float, out: dict):
                                 if time.monotonic() >= t_start:
                                     frames += 1
                                     g = grabs.pop(fid, None)
+                                    cur["grab"], cur["count"] = g, True
                                     if g is not None:
                                         lat_ms.append((now_ns - g) / 1e6)
                     else:
                         break
             finally:
                 ack_task.cancel()
-    out[port] = dict(frames=frames, lat=lat_ms, bytes=bytes_rx)
+    out[port] = dict(frames=frames, lat=lat_ms, lat_last=lat_last_ms, bytes=bytes_rx)
 
 
 def client_worker(ports, args, t_start, t_end) -> dict:
@@ -198,12 +207,17 @@ async def run_n(n: int, args) -> dict:
         stop_servers(procs)
     fps = np.array([out[p]["frames"] / args.seconds for _, p, _ in procs]) if out else np.zeros(1)
     lat = np.concatenate([np.asarray(out[p]["lat"], dtype=np.float64) for _, p, _ in procs]) if out else np.zeros(0)
+    lat_last = (np.concatenate([np.asarray(out[p]["lat_last"], dtype=np.float64) for _, p, _ in procs])
+                if out else np.zeros(0))
     ok = bool(len(fps) == n and fps.min() >= args.fps * args.sustain)
     return {"sessions": n, "fps_min": round(float(fps.min()), 2), "fps_median": round(float(np.median(fps)), 2),
             "aggregate_fps": round(float(fps.sum()), 1),
             "latency_p50_ms": round(float(np.percentile(lat, 50)), 2) if len(lat) else None,
             "latency_p99_ms": round(float(np.percentile(lat, 99)), 2) if len(lat) else None,
-            "latency_samples": int(len(lat)), "sustained": ok}
+            "latency_samples": int(len(lat)),
+            "frame_latency_p50_ms": round(float(np.percentile(lat_last, 50)), 2) if len(lat_last) else None,
+            "frame_latency_p99_ms": round(float(np.percentile(lat_last, 99)), 2) if len(lat_last) else None,
+            "sustained": ok}
 
 
 def main():
