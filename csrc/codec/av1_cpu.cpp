@@ -514,6 +514,7 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
     }
     if (key)   // AV1 has no intra slices: a key frame refreshes the whole picture
         for (int s = 0; s < ns; s++) fe.tasks[s].final_action = ACT_I;
+    fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     fp.key = key;
     fp.qidx = qidx_for_qp(fe.tasks[0].qp);
     std::fill(blk.begin(), blk.end(), BlkInfo{});
@@ -534,6 +535,7 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
     h264::write_stripe_header(pk.data.data(), key, frame_id, 0, fe.g.W, fe.g.H);
     std::vector<uint8_t> tu = assemble(tiles);
     pk.data.insert(pk.data.end(), tu.begin(), tu.end());
+    fe.ctl_.rate_account(8 * (long long)pk.data.size());
     out.push_back(std::move(pk));
     // every row of the picture was coded: the reconstruction is the next reference
     for (int s = 0; s < ns; s++)

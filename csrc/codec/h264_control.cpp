@@ -10,6 +10,7 @@
 //  * a stripe damaged for `damage_threshold` consecutive frames is "hot" and is
 //    encoded every frame for the next `damage_duration` frames.
 #include "h264_encoder.h"
+#include "h264_frame.h"
 #include "h264_syntax.h"
 #include <string.h>
 
@@ -23,6 +24,20 @@ void Controller::init(const EncoderConfig& cfg, const Geometry& g) {
     g_ = g;
     st_.assign(g.num_slices, StripeState());
     pic_ = StripeState();
+    rc_init(rc_, cfg.rc_mode, cfg.qp, cfg.bitrate_kbps, cfg.fps, cfg.width * cfg.height);
+}
+
+void Controller::rate_control(SliceTask* tasks, const MeResult* me) {
+    const int ns = g_.num_slices;
+    std::vector<long long> sad(ns, 0), dev(ns, 0);
+    for (int s = 0; s < ns; s++) {
+        if (tasks[s].action != ACT_P) continue;
+        for (int j = tasks[s].first_row * g_.mb_w; j < (tasks[s].first_row + tasks[s].num_rows) * g_.mb_w; j++) {
+            sad[s] += me[j].sad;
+            dev[s] += me[j].intra_est;
+        }
+    }
+    rc_apply(rc_, tasks, sad.data(), dev.data(), ns, g_.mb_w, cfg_.qp);
 }
 
 void Controller::request_keyframe() {

@@ -799,6 +799,7 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
             motion_search(s);
             decide_scenecut(s);
         }
+    ctl_.rate_control(tasks.data(), me.data());   // K10 (ratecontrol.h)
     std::vector<std::vector<uint8_t>> rbsp(g.num_slices);
     for (int s = 0; s < g.num_slices; s++) {
         if (tasks[s].final_action == ACT_P || tasks[s].final_action == ACT_I) compute_aq(s);
@@ -810,7 +811,11 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         }
         rbsp[s] = write_slice(s);
     }
+    const size_t first = out.size();
     package(frame_id, rbsp, out);
+    long long bits = 0;
+    for (size_t i = first; i < out.size(); i++) bits += 8 * (long long)out[i].data.size();
+    ctl_.rate_account(bits);
     finish_frame();
 }
 

@@ -15,6 +15,7 @@
 #include <vector>
 #include <string>
 #include "h264_core.h"
+#include "ratecontrol.h"
 
 namespace sk {
 namespace h264 {
@@ -47,6 +48,8 @@ struct EncoderConfig {
     int codec = 0;               // 0 = H.264, 1 = HEVC (hevc_encoder.h: same front end, full frame), 2 = AV1
     int tile_cols_log2 = -1;     // AV1 tiles (av1_encoder.h): -1 = automatic
     int tile_rows_log2 = -1;
+    int rc_mode = RC_CQP;        // K10 rate control (ratecontrol.h): CQP, CRF (qp = CRF value), CBR
+    int bitrate_kbps = 0;        // CBR target
     int aq_strength = 0;         // MB-level adaptive QP strength, Q4 (16 = 1.0; 0 = off): h264_mb.h aq_offset
     int subpel = 1;              // H.264 quarter-pel refinement of P vectors (K4c); HEVC keeps integer vectors
     int intra4x4 = 0;            // H.264 I slices may code MBs as I_NxN (nine 4x4 modes) where cheaper; off
@@ -104,6 +107,11 @@ struct SliceTask {
     int32_t num_refs;      // P: reference pictures available to this slice (1..EncoderConfig::num_refs)
 };
 static_assert(sizeof(SliceTask) == 48, "SliceTask layout");
+
+// K10: slices whose QP the rate controller sets (coded, not a paint-over refresh)
+SK_HD bool rc_slice_adjustable(const SliceTask& t, int plan_qp) {
+    return (t.final_action == ACT_P || t.final_action == ACT_I) && t.qp == plan_qp;
+}
 
 struct StripeState {
     int frame_num = 0;     // next frame_num
@@ -214,6 +222,39 @@ SK_HD void commit_picture(StripeState& pic, bool idr, int max_refs) {
     }
 }
 
+struct MeResult;
+
+// K10 frame QP from per-slice complexity sums (sad: motion-compensated SAD of the
+// slice's MBs, dev: their source activity; both only for slices planned as P, where
+// the motion search ran). Same code for the CPU controller and k_rc_qp.
+SK_HD void rc_apply(RcState& rc, SliceTask* tasks, const long long* sad, const long long* dev, int ns, int mb_w,
+                    int plan_qp, int stride = 1) {
+    if (rc.mode == RC_CQP) return;
+    long long cp = 0, ci = 0;
+    int np = 0, ni = 0, ni_known = 0, nidr = 0;
+    for (int s = 0; s < ns; s++) {
+        const SliceTask& t = tasks[s];
+        if (!rc_slice_adjustable(t, plan_qp)) continue;
+        const int mbs = t.num_rows * mb_w;
+        if (t.final_action == ACT_P) {
+            cp += sad[(size_t)s * stride];
+            np += mbs;
+        } else {
+            ni += mbs;
+            if (t.action == ACT_I) nidr += mbs;   // planned key frame (IDR), not a scene cut
+            if (t.action == ACT_P) {
+                ci += dev[(size_t)s * stride];
+                ni_known += mbs;
+            }
+        }
+    }
+    if (np + ni == 0) return;
+    const bool intra = ni > np;
+    const int qp = intra ? rc_frame_qp(rc, ci, ni_known, true, nidr * 2 > ni) : rc_frame_qp(rc, cp, np, false);
+    for (int s = 0; s < ns; s++)
+        if (rc_slice_adjustable(tasks[s], plan_qp)) tasks[s].qp = qp;
+}
+
 // Decides, per stripe, what to encode this frame.
 class Controller {
    public:
@@ -221,9 +262,27 @@ class Controller {
     void request_keyframe();
     // Rate control: QP for changed stripes / paint-over from the next frame on.
     void set_qp(int qp, int paint_qp) {
-        if (qp > 0) cfg_.qp = qp;
+        if (qp > 0) cfg_.qp = rc_.base_qp = qp;
         if (paint_qp > 0) cfg_.paint_qp = paint_qp;
     }
+    // K10: mode (RC_CQP / RC_CRF / RC_CBR) and CBR bitrate from the next frame on.
+    void set_rate(int mode, int kbps) {
+        const RcState old = rc_;
+        rc_init(rc_, mode, cfg_.qp, kbps, cfg_.fps, cfg_.width * cfg_.height);
+        if (old.mode == mode) {   // keep the model; a new budget recentres the buffer
+            for (int k = 0; k < 2; k++) {
+                rc_.last_qp[k] = old.last_qp[k];
+                rc_.last_bits[k] = old.last_bits[k];
+                rc_.last_cplx[k] = old.last_cplx[k];
+            }
+            rc_.cplx_ema = old.cplx_ema;
+        }
+    }
+    // K10 per frame: QP of the coded, non-paint-over slices from the frame complexity
+    // (after motion search / scene cut), then the coded size.
+    void rate_control(SliceTask* tasks, const MeResult* me);
+    void rate_account(long long frame_bits) { rc_account(rc_, frame_bits); }
+    RcState& rc() { return rc_; }
     // dirty[s] = stripe s changed since last frame. Fills tasks[num_slices].
     void plan(const uint8_t* dirty, SliceTask* tasks);
     // After the backend ran: update frame_num / idr state from final actions.
@@ -248,7 +307,10 @@ class Controller {
     Geometry g_;
     std::vector<StripeState> st_;
     StripeState pic_;  // full-frame mode picture state
+    RcState rc_;
 };
+
+
 
 // ---- session state transfer --------------------------------------------------
 // Portable snapshot of everything that carries over from one frame to the next,

@@ -319,6 +319,7 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
             fe.motion_search(s);
             fe.decide_scenecut(s);
         }
+    fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     for (int s = 0; s < ns; s++) {
         switch (fe.tasks[s].final_action) {
             case ACT_P: code_slice_inter(s); break;
@@ -341,6 +342,7 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         std::vector<uint8_t> nal = write_slice(s, idr);
         pk.data.insert(pk.data.end(), nal.begin(), nal.end());
     }
+    fe.ctl_.rate_account(8 * (long long)pk.data.size());
     out.push_back(std::move(pk));
     fe.finish_frame();
     poc++;

@@ -1,0 +1,143 @@
+// K10 rate control, shared by the CPU reference controller and the GPU one
+// (k_rc_qp after the motion search, k_rc_account after the bitstream), so both
+// backends choose the same QP for the same frame.
+//
+// Modes (reference parity):
+//  * CQP  - h264_crf mapped to a constant QP (the round-2 behaviour).
+//  * CRF  - the reference's default (CRF 25, src/selkies/settings.py:48, passed to
+//           pixelflux at selkies.py:2941): a complexity-adaptive QP around the CRF
+//           value. The frame complexity is the motion-compensated SAD per coded
+//           macroblock; frames busier than the running average get a coarser QP
+//           (x264's qcompress 0.6 curve, QP offset 2.4 * log2(C / C_avg)), quiet
+//           frames a finer one.
+//  * CBR  - bitrate with a VBV of 1.5 frame intervals (legacy/gstwebrtc_app.py:101-105,
+//           630-637: vbv-buf-capacity in frame periods). A leaky-bucket decoder
+//           buffer drains one frame budget per frame; each frame's target keeps the
+//           buffer near half full and P frames below 1.25x the budget. The QP comes
+//           from the previous frame of the same type through the log-linear model
+//           bits ~ C * 2^(-QP/6): QP = QP_prev + 6 log2((bits_prev / C_prev) * C / target).
+// Integer-only (Q8 log2 with an 8-bit linear mantissa): bit-exact on host and device.
+#pragma once
+#include "sk_common.h"
+
+namespace sk {
+namespace h264 {
+
+enum RcMode : int32_t { RC_CQP = 0, RC_CRF = 1, RC_CBR = 2 };
+
+struct RcState {
+    int32_t mode, base_qp, qp_min, qp_max;
+    int32_t budget;          // CBR bits per frame
+    int32_t vbv_size;        // CBR bits
+    int32_t fullness;        // bits in the virtual decoder buffer after the last frame
+    int32_t frames;          // frames accounted
+    int32_t last_qp[2];      // [0] inter frames, [1] intra frames
+    int32_t last_bits[2];
+    int32_t last_cplx[2];    // complexity per coded MB (x16)
+    int32_t cplx_ema;        // CRF: running complexity reference (x16), 0 = none yet
+    int32_t cur_qp, cur_intra, cur_cplx;   // the frame in flight (set by rc_frame_qp)
+    int32_t max_p_bits;      // statistics: largest inter frame since reset
+    int32_t seq;             // GPU: host set_rate() counter applied
+    int32_t cur_valid;       // rc_frame_qp chose this frame's QP (its size trains the model)
+    int32_t pixels;          // luma samples per frame
+};
+static_assert(sizeof(RcState) == 88, "RcState layout");
+
+SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x <= 1
+    if (x <= 1) return 0;
+    int m = 31 - __builtin_clz(x);
+    const uint32_t frac = m >= 8 ? (x >> (m - 8)) & 255u : (x << (8 - m)) & 255u;
+    return m * 256 + (int)frac;
+}
+
+SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float fps, int pixels) {
+    rc = RcState{};
+    rc.pixels = pixels;
+    rc.mode = mode;
+    rc.base_qp = base_qp;
+    rc.qp_min = 10;
+    rc.qp_max = 51;
+    const double f = fps > 0 ? fps : 60.0;
+    rc.budget = (int32_t)(bitrate_kbps * 1000.0 / f);
+    rc.vbv_size = rc.budget + rc.budget / 2;   // 1.5 frame intervals
+    rc.fullness = rc.vbv_size / 2;
+    rc.last_qp[0] = rc.last_qp[1] = base_qp;
+}
+
+SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, rc.qp_max); }
+
+// QP of the frame about to be coded. cplx_sum: sum of the complexity measure over
+// coded MBs (ME SAD for inter frames, source activity for intra), coded_mbs > 0.
+SK_HD int rc_frame_qp(RcState& rc, long long cplx_sum, int coded_mbs, bool intra, bool idr = false) {
+    const int k = intra ? 1 : 0;
+    long long c64 = coded_mbs > 0 ? (cplx_sum * 16) / coded_mbs : 0;
+    int cplx = (int)(c64 > (1 << 28) ? (1 << 28) : c64);
+    const bool known = cplx > 0;   // planned key frames have no motion search: complexity unknown
+    int qp = rc.base_qp;
+    if (rc.mode == RC_CRF) {
+        if (!intra) {
+            if (rc.cplx_ema > 0) {
+                const int d = rc_ilog2_q8((uint32_t)cplx) - rc_ilog2_q8((uint32_t)rc.cplx_ema);   // Q8
+                const int off = (d * 24 + (d >= 0 ? 1280 : -1280)) / 2560;   // round(2.4 * d / 256)
+                qp = rc.base_qp + sk_clip(off, -3, 6);
+            }
+            rc.cplx_ema = rc.cplx_ema > 0 ? rc.cplx_ema + (cplx - rc.cplx_ema) / 8 : cplx;
+        }
+    } else if (rc.mode == RC_CBR) {
+        int target = rc.budget + (rc.vbv_size / 2 - rc.fullness) / 4;
+        // key frames (IDR) may use 3 budgets and are paid back by the frames after
+        // them; every other frame, scene-cut intra pictures included, stays under 1.25x
+        if (idr) target = sk_max(target, 3 * rc.budget);
+        else target = sk_min(target, rc.budget + rc.budget / 4);
+        target = sk_max(target, rc.budget / 4);
+        if (target < 64) target = 64;
+        if (rc.last_bits[k] > 0) {
+            // screen content is steeper than 6 QP per halving (sharp text: whole
+            // coefficient runs cross the dead zone together): 5 QP per halving up,
+            // and at most 2 QP finer per frame so a quiet frame cannot set up a burst
+            const int dc = (known && rc.last_cplx[k] > 0)   // complexity ratio only when both were measured
+                               ? rc_ilog2_q8((uint32_t)cplx) - rc_ilog2_q8((uint32_t)rc.last_cplx[k]) : 0;
+            const int d = rc_ilog2_q8((uint32_t)rc.last_bits[k]) + dc - rc_ilog2_q8((uint32_t)target);
+            const int dq = d >= 0 ? (6 * d + 128) / 256 : -((-5 * d + 128) / 256);
+            qp = rc.last_qp[k] + sk_clip(dq, -2, intra ? 16 : 10);
+        } else if (intra) {
+            // no intra model yet: start from the bits per pixel the budget allows
+            // (~0.6 bpp at QP 25 for desktop content, 6 QP per halving)
+            const int bpp_q8 = (int)(((long long)target * 256) / sk_max(rc.pixels, 1));   // target bpp x256
+            const int d = rc_ilog2_q8(154) - rc_ilog2_q8((uint32_t)sk_max(bpp_q8, 1));  // log2(0.6 / bpp)
+            qp = 25 + (6 * d + (d >= 0 ? 128 : -128)) / 256;
+        } else {
+            qp = rc.last_qp[1] + 2;   // first inter frame: a little coarser than the key frame
+        }
+    }
+    qp = rc_clamp_qp(rc, qp);
+    rc.cur_qp = qp;
+    rc.cur_intra = intra;
+    rc.cur_cplx = known ? cplx : 0;   // 0: not measured
+    rc.cur_valid = 1;
+    return qp;
+}
+
+// After the frame: its coded size.
+SK_HD void rc_account(RcState& rc, long long frame_bits) {
+    const int k = rc.cur_intra ? 1 : 0;
+    const int bits = (int)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);
+    // frames whose QP the controller did not choose (all static) do not train the model
+    if (rc.cur_valid) {   // last_cplx 0: not measured (the next prediction assumes no change)
+        rc.last_qp[k] = rc.cur_qp;
+        rc.last_bits[k] = bits > 0 ? bits : 1;
+        rc.last_cplx[k] = rc.cur_cplx;
+    }
+    if (rc.mode == RC_CBR) {
+        // an overflow (a key frame far above the buffer) is written off after one
+        // frame instead of starving the frames behind it for seconds
+        long long f = (long long)rc.fullness + bits - rc.budget;
+        rc.fullness = (int32_t)(f < 0 ? 0 : (f > rc.vbv_size ? rc.vbv_size : f));
+    }
+    if (rc.cur_valid && !rc.cur_intra && bits > rc.max_p_bits) rc.max_p_bits = bits;
+    rc.cur_valid = 0;
+    rc.frames++;
+}
+
+}  // namespace h264
+}  // namespace sk

@@ -72,6 +72,9 @@ struct FrameArgs {
     DbInfo* db;            // [num_mbs] deblocking side info (k_deblock_prep)
     uint4* dbe;            // [num_mbs][3] per-MB edge record: bS nibbles, packed filter params (k_deblock_edges)
     int16_t* fs_mv;        // [num_mbs][2] MFMA full-search winner (integer pel)
+    RcState* rc;           // K10 rate-control state (ratecontrol.h), device
+    long long* rc_slice;   // [num_slices][2] complexity sums of P-planned slices (SAD, activity)
+    float rc_fps;          // session frame rate (CBR frame budget)
 };
 
 void launch_convert_damage(const FrameArgs& a, hipStream_t s);
@@ -79,6 +82,9 @@ void launch_encode(const FrameArgs& a, hipStream_t s);   // k_plan and everythin
 // k_plan, motion search and scene-cut decisions only (the HEVC back end follows it)
 void launch_frontend(const FrameArgs& a, hipStream_t s);
 void launch_commit(const FrameArgs& a, hipStream_t s);   // MV field + reference update (+ K7 deblocking)
+// K10 accounting of the frame just coded: frame bytes = sum of sizes[i * stride],
+// i < n (per_slice: only slices that were coded).
+void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, int per_slice, hipStream_t s);
 
 }  // namespace gpu
 }  // namespace h264

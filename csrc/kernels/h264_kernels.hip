@@ -696,9 +696,10 @@ __global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
     __shared__ long long red[2][4];
     const int s = blockIdx.x;
     SliceTask& t = a.tasks[s];
-    const bool p = t.action == ACT_P && t.allow_scenecut;
+    const bool planned_p = t.action == ACT_P;
+    const bool p = planned_p && t.allow_scenecut;
     long long sad = 0, dev = 0;
-    if (p) {
+    if (planned_p) {
         const int first = t.first_row * a.mb_w, nmb = t.num_rows * a.mb_w;
         for (int i = threadIdx.x; i < nmb; i += 256) {
             const MeResult r = a.me[first + i];
@@ -719,8 +720,46 @@ __global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
         const long long ts = red[0][0] + red[0][1] + red[0][2] + red[0][3];
         const long long td = red[1][0] + red[1][1] + red[1][2] + red[1][3];
         t.final_action = (p && ts > td) ? ACT_I : t.action;
+        a.rc_slice[2 * s] = ts;       // K10 complexity (k_rc_qp)
+        a.rc_slice[2 * s + 1] = td;
         a.tasks_host[s] = t;  // final decision back to the host (host-mapped)
     }
+}
+
+// K10: frame QP from the complexity sums (same rc_apply as the CPU controller).
+// Host overrides: key_seq_host[1] qp, [3] rc mode, [4] kbps, [5] change counter.
+__global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
+    if (threadIdx.x != 0) return;
+    RcState& rc = *a.rc;
+    const int seq = __hip_atomic_load(a.key_seq_host + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    int plan_qp = a.plan_cfg.qp;
+    const int qo = __hip_atomic_load(a.key_seq_host + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (qo > 0) plan_qp = qo;
+    if (seq != rc.seq) {   // set_rate() from the host: re-initialise, keep the model if the mode stays
+        const int mode = __hip_atomic_load(a.key_seq_host + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int kbps = __hip_atomic_load(a.key_seq_host + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const RcState old = rc;
+        rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H);
+        if (old.mode == mode)
+            for (int k = 0; k < 2; k++) {
+                rc.last_qp[k] = old.last_qp[k];
+                rc.last_bits[k] = old.last_bits[k];
+                rc.last_cplx[k] = old.last_cplx[k];
+            }
+        if (old.mode == mode) rc.cplx_ema = old.cplx_ema;
+        rc.seq = seq;
+    }
+    rc.base_qp = plan_qp;
+    rc_apply(rc, a.tasks, a.rc_slice, a.rc_slice + 1, a.num_slices, a.mb_w, plan_qp, 2);
+    for (int s = 0; s < a.num_slices; s++) a.tasks_host[s].qp = a.tasks[s].qp;
+}
+
+__global__ __launch_bounds__(64) void k_rc_account(FrameArgs a, const int* sizes, int n, int stride, int per_slice) {
+    long long b = 0;
+    for (int i = threadIdx.x; i < n; i += 64)
+        if (!per_slice || a.tasks[i].final_action != ACT_NONE) b += sizes[(size_t)i * stride];
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_down(b, o);
+    if (threadIdx.x == 0) rc_account(*a.rc, 8 * b);
 }
 
 // ---------------------------------------------------------------------------
@@ -2891,6 +2930,11 @@ void launch_frontend(const FrameArgs& a, hipStream_t s) {
     if (a.me_full) hipLaunchKernelGGL(k_me_mfma, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rc_qp, dim3(1), dim3(64), 0, s, a);
+}
+
+void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, int per_slice, hipStream_t s) {
+    hipLaunchKernelGGL(k_rc_account, dim3(1), dim3(64), 0, s, a, sizes, n, stride, per_slice);
 }
 
 void launch_encode(const FrameArgs& a, hipStream_t s) {
@@ -2911,6 +2955,7 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_ep_nz, tiles, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_ep_count, tiles, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_ep_write, tiles, dim3(256), 0, s, a);
+    launch_rc_account(a, a.slice_info, a.num_slices, 4, 1, s);
 }
 
 void launch_commit(const FrameArgs& a, hipStream_t s) {

@@ -49,6 +49,10 @@ class EncoderBackend {
     virtual int stage_times(float* dst, int n) { (void)dst; (void)n; return 0; }
     // H.264 rate control hook (QP <= 0 keeps the current value); JPEG ignores it.
     virtual void set_qp(int qp, int paint_qp) { (void)qp; (void)paint_qp; }
+    // K10 rate control (ratecontrol.h): mode RC_CQP / RC_CRF / RC_CBR, CBR bitrate.
+    virtual void set_rate(int mode, int kbps) { (void)mode; (void)kbps; }
+    // RcState words (ratecontrol.h) into out; returns the count (< 0: no controller).
+    virtual int64_t rc_stats(int32_t* out, int n) { (void)out; (void)n; return -1; }
     // K12/K13 overlays (overlay.h), applied inside the colour conversion of the frames
     // uploaded after the call: slot 0 watermark, 1 cursor; premultiplied BGRA images.
     virtual int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) {

@@ -73,6 +73,21 @@ class HipBackend : public EncoderBackend {
         if (qp > 0) __atomic_store_n(&h_key_seq_[1], qp, __ATOMIC_SEQ_CST);
         if (paint_qp > 0) __atomic_store_n(&h_key_seq_[2], paint_qp, __ATOMIC_SEQ_CST);
     }
+    // K10: picked up by k_rc_qp at the next frame (a change counter tells it apart).
+    void set_rate(int mode, int kbps) override {
+        __atomic_store_n(&h_key_seq_[3], mode, __ATOMIC_SEQ_CST);
+        __atomic_store_n(&h_key_seq_[4], kbps, __ATOMIC_SEQ_CST);
+        __atomic_fetch_add(&h_key_seq_[5], 1, __ATOMIC_SEQ_CST);
+    }
+    int64_t rc_stats(int32_t* out, int n) override {
+        HIPCHECK(hipSetDevice(device_));
+        HIPCHECK(hipStreamSynchronize(stream_));
+        RcState rc;
+        HIPCHECK(hipMemcpy(&rc, args_.rc, sizeof(rc), hipMemcpyDeviceToHost));
+        const int k = n < (int)(sizeof(rc) / 4) ? n : (int)(sizeof(rc) / 4);
+        memcpy(out, &rc, (size_t)k * 4);
+        return k;
+    }
 
     int encode(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         submit(bgrx, stride, frame_id);
@@ -146,7 +161,7 @@ class HipBackend : public EncoderBackend {
         h_frame_params_[p][0] = staged_frame_;
         // keyframe request counter and QP overrides as of this launch: a request made
         // before launch(n) applies to frame n even when frame n-1 has not planned yet
-        for (int i = 0; i < 3; i++) h_key_snap_[p][i] = __atomic_load_n(&h_key_seq_[i], __ATOMIC_SEQ_CST);
+        for (int i = 0; i < 6; i++) h_key_snap_[p][i] = __atomic_load_n(&h_key_seq_[i], __ATOMIC_SEQ_CST);
         frame_of_[p] = staged_frame_;
         memcpy(ov_params_host_[p], ov_pending_, sizeof(ov_pending_));   // read by this frame's graph
         if (!staged_on_main_) HIPCHECK(hipStreamWaitEvent(stream_, ev_copy_[p], 0));
@@ -430,7 +445,7 @@ class HipBackend : public EncoderBackend {
         }
         h_key_seq_ = hmalloc<int>(16, hipHostMallocCoherent);   // written by request_keyframe/set_qp
         for (int p = 0; p < 2; p++) {   // per-parity snapshot taken at launch, read by k_plan
-            h_key_snap_[p] = hmalloc<int>(4, hipHostMallocCoherent);
+            h_key_snap_[p] = hmalloc<int>(8, hipHostMallocCoherent);
             HIPCHECK(hipHostGetDevicePointer(&dd, h_key_snap_[p], 0));
             key_snap_dev_[p] = (const int*)dd;
         }
@@ -439,6 +454,16 @@ class HipBackend : public EncoderBackend {
         a.me = dmalloc<MeResult>(nmb);
         a.mvfield = dmalloc<int16_t>(2 * nmb);
         a.fs_mv = dmalloc<int16_t>(2 * nmb);
+        {   // K10 rate control state (ratecontrol.h), initialised like the CPU controller's
+            RcState rc;
+            rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height);
+            a.rc = dmalloc<RcState>(1);
+            HIPCHECK(hipMemcpy(a.rc, &rc, sizeof(rc), hipMemcpyHostToDevice));
+            a.rc_slice = dmalloc<long long>(2 * (size_t)ns);
+            a.rc_fps = cfg_.fps;
+            h_key_seq_[3] = cfg_.rc_mode;
+            h_key_seq_[4] = cfg_.bitrate_kbps;
+        }
         a.db = dmalloc<DbInfo>(nmb);
         a.dbe = dmalloc<uint4>((size_t)3 * nmb);
         a.mbs = dmalloc<MbInfo>(nmb);
@@ -543,6 +568,7 @@ class HipBackend : public EncoderBackend {
                 aa.out_host = av1_out_dev_[parity_];
                 aa.out_size_host = av1_size_dev_[parity_];
                 av1::gpu::launch_backend(aa, stream_);
+                gpu::launch_rc_account(args_, aa.tile_size, av1_geo_.tile_cols * av1_geo_.tile_rows, 1, 0, stream_);
             } else if (cfg_.codec == 1) {
                 gpu::launch_frontend(args_, stream_);
                 hevc::gpu::HevcArgs ha = hargs_;
@@ -551,6 +577,7 @@ class HipBackend : public EncoderBackend {
                 ha.out_size = hevc_size_dev_[parity_];
                 ha.out_dev = hevc_fallback_[parity_];
                 hevc::gpu::launch_backend(ha, stream_);
+                gpu::launch_rc_account(args_, ha.sub_size, g_.mb_h, 1, 0, stream_);
             } else {
                 gpu::launch_encode(args_, stream_);
             }

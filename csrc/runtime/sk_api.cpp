@@ -22,6 +22,12 @@ class CpuBackend : public EncoderBackend {
     explicit CpuBackend(const h264::EncoderConfig& c) : enc_(c) {}
     void request_keyframe() override { enc_.request_keyframe(); }
     void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
+    void set_rate(int mode, int kbps) override { enc_.ctl_.set_rate(mode, kbps); }
+    int64_t rc_stats(int32_t* out, int n) override {
+        const int k = n < (int)(sizeof(h264::RcState) / 4) ? n : (int)(sizeof(h264::RcState) / 4);
+        memcpy(out, &enc_.ctl_.rc(), (size_t)k * 4);
+        return k;
+    }
     int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) override {
         enc_.set_overlay_image(slot, bgra, w, h);
         return 0;
@@ -111,6 +117,12 @@ class CpuHevcBackend : public EncoderBackend {
     explicit CpuHevcBackend(const h264::EncoderConfig& c) : enc_(c) {}
     void request_keyframe() override { enc_.request_keyframe(); }
     void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
+    void set_rate(int mode, int kbps) override { enc_.fe.ctl_.set_rate(mode, kbps); }
+    int64_t rc_stats(int32_t* out, int n) override {
+        const int k = n < (int)(sizeof(h264::RcState) / 4) ? n : (int)(sizeof(h264::RcState) / 4);
+        memcpy(out, &enc_.fe.ctl_.rc(), (size_t)k * 4);
+        return k;
+    }
     int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) override {
         enc_.fe.set_overlay_image(slot, bgra, w, h);
         return 0;
@@ -154,6 +166,12 @@ class CpuAv1Backend : public EncoderBackend {
     explicit CpuAv1Backend(const h264::EncoderConfig& c) : enc_(c, c.tile_cols_log2, c.tile_rows_log2) {}
     void request_keyframe() override { enc_.request_keyframe(); }
     void set_qp(int qp, int paint_qp) override { enc_.set_qp(qp, paint_qp); }
+    void set_rate(int mode, int kbps) override { enc_.fe.ctl_.set_rate(mode, kbps); }
+    int64_t rc_stats(int32_t* out, int n) override {
+        const int k = n < (int)(sizeof(h264::RcState) / 4) ? n : (int)(sizeof(h264::RcState) / 4);
+        memcpy(out, &enc_.fe.ctl_.rc(), (size_t)k * 4);
+        return k;
+    }
     int set_overlay_image(int slot, const uint8_t* bgra, int w, int h) override {
         enc_.fe.set_overlay_image(slot, bgra, w, h);
         return 0;
@@ -246,6 +264,9 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.codec = (c->codec == 1 || c->codec == 2) ? c->codec : 0;
     e.tile_cols_log2 = c->tile_cols_log2;
     e.tile_rows_log2 = c->tile_rows_log2;
+    e.rc_mode = c->rc_mode >= 0 && c->rc_mode <= 2 ? c->rc_mode : 0;
+    e.bitrate_kbps = c->bitrate_kbps > 0 ? c->bitrate_kbps : 0;
+    if (e.rc_mode == h264::RC_CBR && e.bitrate_kbps <= 0) e.rc_mode = h264::RC_CRF;
     e.aq_strength = c->aq_strength > 0 ? (c->aq_strength > 64 ? 64 : c->aq_strength) : 0;
     e.subpel = c->subpel >= 0 ? 1 : 0;
     e.intra4x4 = c->intra4x4 > 0 ? 1 : 0;
@@ -347,6 +368,10 @@ void* sk_jpeg_create(const sk_jpeg_config* c) {
 void sk_h264_destroy(void* enc) { delete static_cast<EncoderBackend*>(enc); }
 void sk_h264_request_keyframe(void* enc) { static_cast<EncoderBackend*>(enc)->request_keyframe(); }
 void sk_h264_set_qp(void* enc, int qp, int paint_qp) { static_cast<EncoderBackend*>(enc)->set_qp(qp, paint_qp); }
+void sk_h264_set_rate(void* enc, int mode, int kbps) { static_cast<EncoderBackend*>(enc)->set_rate(mode, kbps); }
+int sk_h264_rc_stats(void* enc, int32_t* out, int n) {
+    return (int)static_cast<EncoderBackend*>(enc)->rc_stats(out, n);
+}
 int sk_h264_set_overlay_image(void* enc, int slot, const uint8_t* bgra, int w, int h) {
     return static_cast<EncoderBackend*>(enc)->set_overlay_image(slot, bgra, w, h);
 }

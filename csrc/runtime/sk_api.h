@@ -27,6 +27,8 @@ typedef struct sk_h264_config {
     int32_t intra4x4;               // H.264 Intra4x4 (I_NxN) macroblocks in I slices: > 0 on, else off
     int32_t tile_cols_log2;         // AV1 tile columns / rows (log2); -1 = automatic
     int32_t tile_rows_log2;
+    int32_t rc_mode;                // K10 rate control: 0 = constant QP, 1 = CRF (qp = CRF), 2 = CBR
+    int32_t bitrate_kbps;           // CBR target (VBV = 1.5 frame intervals)
 } sk_h264_config;
 
 typedef struct sk_packet {
@@ -45,6 +47,10 @@ void sk_h264_destroy(void* enc);
 void sk_h264_request_keyframe(void* enc);
 // Rate control: QP of changed stripes / paint-over from the next frame (<= 0 keeps the value).
 void sk_h264_set_qp(void* enc, int qp, int paint_qp);
+// K10 rate control from the next frame: mode 0 constant QP, 1 CRF, 2 CBR at kbps.
+void sk_h264_set_rate(void* enc, int mode, int kbps);
+// Rate-control state words (codec/ratecontrol.h RcState); returns the count or -1.
+int sk_h264_rc_stats(void* enc, int32_t* out, int n);
 // K12/K13 overlays blended during colour conversion (csrc/codec/overlay.h): slot 0 =
 // watermark, 1 = cursor; premultiplied BGRA, at most 512x512. Positions apply to frames
 // uploaded after the call; tdx/tdy > 0 tile the image with that period. 0 = ok, < 0 =

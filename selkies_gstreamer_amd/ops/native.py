@@ -35,6 +35,7 @@ class SkH264Config(ctypes.Structure):
         ("num_refs", ctypes.c_int32), ("codec", ctypes.c_int32), ("aq_strength", ctypes.c_int32),
         ("subpel", ctypes.c_int32), ("intra4x4", ctypes.c_int32),
         ("tile_cols_log2", ctypes.c_int32), ("tile_rows_log2", ctypes.c_int32),
+        ("rc_mode", ctypes.c_int32), ("bitrate_kbps", ctypes.c_int32),
     ]
 
 
@@ -103,6 +104,8 @@ def lib():
         L.sk_h264_destroy.argtypes = [ctypes.c_void_p]
         L.sk_h264_request_keyframe.argtypes = [ctypes.c_void_p]
         L.sk_h264_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.sk_h264_set_rate.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.sk_h264_rc_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.sk_h264_set_overlay_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                                 ctypes.c_int]
         L.sk_h264_set_overlay_pos.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6
@@ -217,6 +220,12 @@ TASK_DTYPE = np.dtype([(n, "<i4") for n in (
     "allow_scenecut", "idr_on_intra", "final_action", "num_refs")])
 
 
+RC_MODES = {"cqp": 0, "crf": 1, "cbr": 2}
+RC_FIELDS = ("mode", "base_qp", "qp_min", "qp_max", "budget", "vbv_size", "fullness", "frames", "last_qp_p",
+             "last_qp_i", "last_bits_p", "last_bits_i", "last_cplx_p", "last_cplx_i", "cplx_ema", "cur_qp",
+             "cur_intra", "cur_cplx", "max_p_bits", "seq", "cur_valid")
+
+
 class H264Encoder:
     """Stripe H.264 encoder session (CPU reference backend or HIP backend)."""
 
@@ -228,7 +237,8 @@ class H264Encoder:
                  backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
                  src_width: int = 0, src_height: int = 0, num_refs: int = 1, codec: str = "h264",
                  aq_strength: float = 0.0, subpel: bool = True, intra4x4: bool = False,
-                 tile_cols_log2: int = -1, tile_rows_log2: int = -1):
+                 tile_cols_log2: int = -1, tile_rows_log2: int = -1, rate_control: str = "cqp",
+                 bitrate_kbps: int = 0):
         """aq_strength: MB-level adaptive QP (h264_mb.h aq_offset), 1.0 = x264 aq-mode 1
         strength; 0 = constant QP per slice (x264 ultrafast behaviour)."""
         L = lib()
@@ -243,7 +253,8 @@ class H264Encoder:
                                 1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height),
                                 int(num_refs), {"h264": 0, "hevc": 1, "av1": 2}.get(codec, 0),
                                 int(round(aq_strength * 16)), 0 if subpel else -1, 1 if intra4x4 else 0,
-                                int(tile_cols_log2), int(tile_rows_log2))
+                                int(tile_cols_log2), int(tile_rows_log2),
+                                RC_MODES[rate_control], int(bitrate_kbps))
         if codec not in ("h264", "hevc", "av1"):
             raise ValueError("codec must be 'h264', 'hevc' or 'av1'")
         self.codec = codec
@@ -405,6 +416,15 @@ class H264Encoder:
         buf = np.empty(n, dtype=np.uint8)
         L.sk_h264_debug_buffer(self._h, name.encode(), buf.ctypes.data, n)
         return buf.view(dtype)
+
+    def set_rate(self, mode: str = "crf", kbps: int = 0) -> None:
+        """K10 rate control from the next frame: 'cqp', 'crf' or 'cbr' at `kbps`."""
+        lib().sk_h264_set_rate(self._h, RC_MODES[mode], int(kbps))
+
+    def rc_stats(self) -> dict:
+        arr = (ctypes.c_int32 * 20)()
+        n = lib().sk_h264_rc_stats(self._h, arr, 20)
+        return {k: int(arr[i]) for i, k in enumerate(RC_FIELDS) if i < n}
 
     def stage_times(self, n: int = 16) -> list[float]:
         arr = (ctypes.c_float * n)()
