@@ -535,7 +535,9 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
     h264::write_stripe_header(pk.data.data(), key, frame_id, 0, fe.g.W, fe.g.H);
     std::vector<uint8_t> tu = assemble(tiles);
     pk.data.insert(pk.data.end(), tu.begin(), tu.end());
-    fe.ctl_.rate_account(8 * (long long)pk.data.size());
+    long long payload = 0;   // K10 accounting unit: tile payload bits (k_rc_account: tile sizes)
+    for (const auto& t : tiles) payload += 8 * (long long)t.size();
+    fe.ctl_.rate_account(payload);
     out.push_back(std::move(pk));
     // every row of the picture was coded: the reconstruction is the next reference
     for (int s = 0; s < ns; s++)

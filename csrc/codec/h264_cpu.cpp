@@ -348,9 +348,9 @@ void CpuH264Encoder::mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTa
     }
 }
 
-void CpuH264Encoder::code_slice_inter(int s) {
+void CpuH264Encoder::code_slice_inter(int s, bool redo) {
     const SliceTask& t = tasks[s];
-    if (cfg.subpel) subpel_refine(s);
+    if (cfg.subpel && !redo) subpel_refine(s);
     for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
         for (int mbx = 0; mbx < g.mb_w; mbx++) {
             int idx = mby * g.mb_w + mbx;
@@ -801,6 +801,13 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         }
     ctl_.rate_control(tasks.data(), me.data());   // K10 (ratecontrol.h)
     std::vector<std::vector<uint8_t>> rbsp(g.num_slices);
+    // K10 accounting unit: slice RBSP payload bits (k_rc_account reads the same sizes)
+    auto payload_bits = [&] {
+        long long b = 0;
+        for (int s = 0; s < g.num_slices; s++)
+            if (tasks[s].final_action != ACT_NONE) b += 8 * (long long)rbsp[s].size();
+        return b;
+    };
     for (int s = 0; s < g.num_slices; s++) {
         if (tasks[s].final_action == ACT_P || tasks[s].final_action == ACT_I) compute_aq(s);
         switch (tasks[s].final_action) {
@@ -811,10 +818,18 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         }
         rbsp[s] = write_slice(s);
     }
-    const size_t first = out.size();
+    long long bits = payload_bits();
+    // CBR guard: a frame that overflows the VBV is coded again, coarser (k_rc_guard)
+    if (ctl_.rate_redo(tasks.data(), bits)) {
+        for (int s = 0; s < g.num_slices; s++) {
+            if (tasks[s].final_action == ACT_P) code_slice_inter(s, true);
+            else if (tasks[s].final_action == ACT_I) code_slice_intra(s);
+            else continue;
+            rbsp[s] = write_slice(s);
+        }
+        bits = payload_bits();
+    }
     package(frame_id, rbsp, out);
-    long long bits = 0;
-    for (size_t i = first; i < out.size(); i++) bits += 8 * (long long)out[i].data.size();
     ctl_.rate_account(bits);
     finish_frame();
 }

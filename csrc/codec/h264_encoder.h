@@ -108,9 +108,10 @@ struct SliceTask {
 };
 static_assert(sizeof(SliceTask) == 48, "SliceTask layout");
 
-// K10: slices whose QP the rate controller sets (coded, not a paint-over refresh)
-SK_HD bool rc_slice_adjustable(const SliceTask& t, int plan_qp) {
-    return (t.final_action == ACT_P || t.final_action == ACT_I) && t.qp == plan_qp;
+// K10: slices whose QP the rate controller sets: coded, and not a paint-over refresh
+// (CRF; under CBR the refresh is budgeted like any other slice)
+SK_HD bool rc_slice_adjustable(const SliceTask& t, int plan_qp, int mode = 1) {
+    return (t.final_action == ACT_P || t.final_action == ACT_I) && (t.qp == plan_qp || mode == 2);
 }
 
 struct StripeState {
@@ -234,7 +235,7 @@ SK_HD void rc_apply(RcState& rc, SliceTask* tasks, const long long* sad, const l
     int np = 0, ni = 0, ni_known = 0, nidr = 0;
     for (int s = 0; s < ns; s++) {
         const SliceTask& t = tasks[s];
-        if (!rc_slice_adjustable(t, plan_qp)) continue;
+        if (!rc_slice_adjustable(t, plan_qp, rc.mode)) continue;
         const int mbs = t.num_rows * mb_w;
         if (t.final_action == ACT_P) {
             cp += sad[(size_t)s * stride];
@@ -250,9 +251,28 @@ SK_HD void rc_apply(RcState& rc, SliceTask* tasks, const long long* sad, const l
     }
     if (np + ni == 0) return;
     const bool intra = ni > np;
-    const int qp = intra ? rc_frame_qp(rc, ci, ni_known, true, nidr * 2 > ni) : rc_frame_qp(rc, cp, np, false);
+    const int qp = intra ? rc_frame_qp(rc, ci, ni_known, true, nidr * 2 > ni, np + ni)
+                         : rc_frame_qp(rc, cp, np, false, false, np + ni);
     for (int s = 0; s < ns; s++)
-        if (rc_slice_adjustable(tasks[s], plan_qp)) tasks[s].qp = qp;
+        if (rc_slice_adjustable(tasks[s], plan_qp, rc.mode)) tasks[s].qp = qp;
+}
+
+// K10 CBR guard on a coded frame of `frame_bits` payload bits: when it overflows the
+// VBV, every rate-controlled slice (coded at the frame QP) moves rc_redo_step coarser
+// for a second coding pass. Returns the step applied (0: keep the frame).
+SK_HD int rc_redo(RcState& rc, SliceTask* tasks, int ns, long long frame_bits) {
+    const int step = rc_redo_step(rc, frame_bits);
+    if (!step) return 0;
+    const int q0 = rc.cur_qp, q1 = rc_clamp_qp(rc, q0 + step);
+    rc_raise_floor(rc);
+    if (q1 == q0) return 0;
+    for (int s = 0; s < ns; s++) {
+        SliceTask& t = tasks[s];
+        if ((t.final_action == ACT_P || t.final_action == ACT_I) && t.qp == q0) t.qp = q1;
+    }
+    rc.cur_qp = q1;
+    rc.redos++;
+    return q1 - q0;
 }
 
 // Decides, per stripe, what to encode this frame.
@@ -282,6 +302,7 @@ class Controller {
     // (after motion search / scene cut), then the coded size.
     void rate_control(SliceTask* tasks, const MeResult* me);
     void rate_account(long long frame_bits) { rc_account(rc_, frame_bits); }
+    int rate_redo(SliceTask* tasks, long long frame_bits) { return rc_redo(rc_, tasks, g_.num_slices, frame_bits); }
     RcState& rc() { return rc_; }
     // dirty[s] = stripe s changed since last frame. Fills tasks[num_slices].
     void plan(const uint8_t* dirty, SliceTask* tasks);

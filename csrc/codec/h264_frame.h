@@ -64,7 +64,7 @@ class CpuH264Encoder {
     int mb_start_qp(const SliceTask& t, int idx) const {
         return cfg.aq_strength > 0 ? aq_start_qp(t.qp, aq[idx]) : -1;
     }
-    void code_slice_inter(int s);
+    void code_slice_inter(int s, bool redo = false);   // redo: CBR second pass, vectors kept
     void code_slice_intra(int s);
     void code_slice_skipall(int s);
     std::vector<uint8_t> write_slice(int s);                 // entropy + header -> RBSP

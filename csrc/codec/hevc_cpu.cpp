@@ -283,6 +283,7 @@ std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
         if (r + 1 < rows) e.terminate(1);   // end_of_subset_one_bit
         e.finish();
         sub[r].resize(e.pos);
+        payload_bytes_ += (long long)e.pos;
     }
     // entry points count emulation-prevention bytes (7.4.7.1)
     std::vector<int> esc(rows);
@@ -338,11 +339,12 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
     pk.data.resize(10);
     h264::write_stripe_header(pk.data.data(), idr, frame_id, 0, fe.g.W, fe.g.H);
     if (idr) pk.data.insert(pk.data.end(), param_sets.begin(), param_sets.end());
+    payload_bytes_ = 0;
     for (int s = 0; s < ns; s++) {
         std::vector<uint8_t> nal = write_slice(s, idr);
         pk.data.insert(pk.data.end(), nal.begin(), nal.end());
     }
-    fe.ctl_.rate_account(8 * (long long)pk.data.size());
+    fe.ctl_.rate_account(8 * payload_bytes_);   // K10: substream payload (k_rc_account: sub_size)
     out.push_back(std::move(pk));
     fe.finish_frame();
     poc++;

@@ -74,6 +74,7 @@ class CpuHevcEncoder {
     void binarize_slice(int s);
     // CABAC substreams of slice s (one per CTB row) -> slice NAL (Annex B)
     std::vector<uint8_t> write_slice(int s, bool idr);
+    long long payload_bytes_ = 0;   // substream bytes of the frame being written (K10)
 
     h264::CpuH264Encoder fe;   // front end (full-frame mode)
     Geo geo;

@@ -40,8 +40,14 @@ struct RcState {
     int32_t seq;             // GPU: host set_rate() counter applied
     int32_t cur_valid;       // rc_frame_qp chose this frame's QP (its size trains the model)
     int32_t pixels;          // luma samples per frame
+    int32_t cur_idr;         // the frame in flight is a planned key frame
+    int32_t redos;           // statistics: frames coded twice by the CBR guard
+    int32_t qp_floor;        // CBR: inter QP below which a frame overflowed recently (0: none)
+    int32_t floor_age;       // frames since the floor last moved (it decays 1 QP per 8 frames)
+    int32_t last_mbs[2];     // rate-controlled macroblocks of the model frames
+    int32_t cur_mbs;         // ... of the frame in flight
 };
-static_assert(sizeof(RcState) == 88, "RcState layout");
+static_assert(sizeof(RcState) == 116, "RcState layout");
 
 SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x <= 1
     if (x <= 1) return 0;
@@ -67,8 +73,10 @@ SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float f
 SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, rc.qp_max); }
 
 // QP of the frame about to be coded. cplx_sum: sum of the complexity measure over
-// coded MBs (ME SAD for inter frames, source activity for intra), coded_mbs > 0.
-SK_HD int rc_frame_qp(RcState& rc, long long cplx_sum, int coded_mbs, bool intra, bool idr = false) {
+// coded_mbs measured MBs (ME SAD for inter frames, source activity for intra);
+// mbs: all rate-controlled MBs of the frame (the model scales with their number:
+// striped sessions code only the stripes that changed).
+SK_HD int rc_frame_qp(RcState& rc, long long cplx_sum, int coded_mbs, bool intra, bool idr = false, int mbs = 0) {
     const int k = intra ? 1 : 0;
     long long c64 = coded_mbs > 0 ? (cplx_sum * 16) / coded_mbs : 0;
     int cplx = (int)(c64 > (1 << 28) ? (1 << 28) : c64);
@@ -97,9 +105,14 @@ SK_HD int rc_frame_qp(RcState& rc, long long cplx_sum, int coded_mbs, bool intra
             // and at most 2 QP finer per frame so a quiet frame cannot set up a burst
             const int dc = (known && rc.last_cplx[k] > 0)   // complexity ratio only when both were measured
                                ? rc_ilog2_q8((uint32_t)cplx) - rc_ilog2_q8((uint32_t)rc.last_cplx[k]) : 0;
-            const int d = rc_ilog2_q8((uint32_t)rc.last_bits[k]) + dc - rc_ilog2_q8((uint32_t)target);
+            const int dm = (mbs > 0 && rc.last_mbs[k] > 0)   // coded area ratio
+                               ? rc_ilog2_q8((uint32_t)mbs) - rc_ilog2_q8((uint32_t)rc.last_mbs[k]) : 0;
+            const int d = rc_ilog2_q8((uint32_t)rc.last_bits[k]) + dc + dm - rc_ilog2_q8((uint32_t)target);
             const int dq = d >= 0 ? (6 * d + 128) / 256 : -((-5 * d + 128) / 256);
             qp = rc.last_qp[k] + sk_clip(dq, -2, intra ? 16 : 10);
+            // screen content can jump several-fold within 2 QP (glyph edges crossing the
+            // dead zone together): stay above the QP that last overflowed the buffer
+            if (!intra && rc.qp_floor > qp) qp = rc.qp_floor;
         } else if (intra) {
             // no intra model yet: start from the bits per pixel the budget allows
             // (~0.6 bpp at QP 25 for desktop content, 6 QP per halving)
@@ -115,7 +128,31 @@ SK_HD int rc_frame_qp(RcState& rc, long long cplx_sum, int coded_mbs, bool intra
     rc.cur_intra = intra;
     rc.cur_cplx = known ? cplx : 0;   // 0: not measured
     rc.cur_valid = 1;
+    rc.cur_idr = idr ? 1 : 0;
+    rc.cur_mbs = mbs;
     return qp;
+}
+
+// CBR guard (VBV overflow): a frame whose payload exceeds the buffer (1.5 budgets;
+// key frames: 4 budgets, their target is 3) is coded once more, coarser by the QP
+// step this returns (0: keep it): the model's 6 QP per halving towards the target.
+SK_HD int rc_redo_step(const RcState& rc, long long frame_bits) {
+    if (rc.mode != RC_CBR || !rc.cur_valid) return 0;
+    // payload bits: the packets add stripe headers and NAL framing, ~2 % at 1080p
+    const long long cap = rc.cur_idr ? 4ll * rc.budget : (long long)rc.vbv_size - rc.budget / 16;
+    if (frame_bits <= cap) return 0;
+    const uint32_t b = (uint32_t)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);
+    const int target = sk_max(rc.cur_idr ? 3 * rc.budget : rc.budget, 1);
+    const int d = rc_ilog2_q8(b) - rc_ilog2_q8((uint32_t)target);   // Q8, > 0
+    return sk_clip((6 * d + 128) / 256, 2, 16);
+}
+
+// The frame in flight (first pass at cur_qp) overflowed: remember its QP as a floor
+// for the inter frames after it.
+SK_HD void rc_raise_floor(RcState& rc) {
+    if (rc.cur_intra) return;
+    rc.qp_floor = sk_max(rc.qp_floor, rc.cur_qp + 1);
+    rc.floor_age = 0;
 }
 
 // After the frame: its coded size.
@@ -127,6 +164,7 @@ SK_HD void rc_account(RcState& rc, long long frame_bits) {
         rc.last_qp[k] = rc.cur_qp;
         rc.last_bits[k] = bits > 0 ? bits : 1;
         rc.last_cplx[k] = rc.cur_cplx;
+        rc.last_mbs[k] = rc.cur_mbs;
     }
     if (rc.mode == RC_CBR) {
         // an overflow (a key frame far above the buffer) is written off after one
@@ -135,6 +173,10 @@ SK_HD void rc_account(RcState& rc, long long frame_bits) {
         rc.fullness = (int32_t)(f < 0 ? 0 : (f > rc.vbv_size ? rc.vbv_size : f));
     }
     if (rc.cur_valid && !rc.cur_intra && bits > rc.max_p_bits) rc.max_p_bits = bits;
+    if (rc.qp_floor > 0 && ++rc.floor_age >= 8) {   // 7.5 QP a second at 60 fps
+        rc.qp_floor = rc.qp_floor - 1 > rc.qp_min ? rc.qp_floor - 1 : 0;
+        rc.floor_age = 0;
+    }
     rc.cur_valid = 0;
     rc.frames++;
 }

@@ -23,6 +23,10 @@ struct Av1Args {
     int lctx_w[3];
     uint32_t* tok;            // [units][kTokCap]
     int* tok_n;               // [units]
+    uint32_t* tokc;           // [tiles][tile_tok_cap]: each tile's tokens in coding order
+    int tile_tok_cap;
+    int* tok_off;             // [units] offset of the unit's tokens in its tile's stream
+    int* tile_ntok;           // [tiles]
     int* frame;               // device: [0] key, [1] qidx
     int* frame_host;          // host-mapped copy of frame[0..1]
     const uint8_t* qidx_of_qp;   // [52]

@@ -9,11 +9,16 @@
 //   k_av1_merge        inter frames: static 32x32 / 64x64 merging, one wave per superblock
 //   k_av1_modes        inter frames: reference-MV stack -> NEAREST / NEAR / GLOBAL / NEWMV
 //   k_av1_tokens       block syntax -> token lists, one lane per 16x16 unit
+//   k_av1_tok_scan/copy  per-tile token streams in coding order
 //   k_av1_ec           one wave per tile: arithmetic coding with the tile's CDFs in LDS
-//   k_av1_pack         tile bytes -> host-mapped output (concatenated)
+//                      (scalar coder state, lane-parallel CDF adaptation)
+//   k_av1_pack         carry resolution (segmented, parallel), tile bytes -> host-mapped output
 //   k_av1_finish       padding rows of the reconstruction, slice actions for k_commit
 // Transforms: forward DCT as LDS matrix products (lanes = output coefficients),
 // inverse as the normative butterflies, lane = row / column of a transform block.
+#include <cstring>
+#include <vector>
+
 #include "av1_gpu.h"
 
 namespace sk {
@@ -532,69 +537,276 @@ __global__ __launch_bounds__(64) void k_av1_tokens(Av1Args A) {
     A.tok_n[u] = sink.n;
 }
 
-struct ChunkSink {
-    uint16_t* p;
-    int n, cap;
-    __device__ void push(uint16_t x) {
-        if (n < cap) p[n] = x;
-        n++;
+// Tile token streams: the unit slots of each tile concatenated in coding order, so
+// the coder reads one contiguous stream. k_av1_tok_scan: per-unit offsets (one
+// workgroup per tile, block scan); k_av1_tok_copy: one wave per unit.
+__global__ __launch_bounds__(256) void k_av1_tok_scan(Av1Args A) {
+    __shared__ int wsum_s[4];
+    __shared__ int run_s;
+    const Av1Geo& g = A.geo;
+    const int t = blockIdx.x, tid = threadIdx.x, l = lane(), w = tid >> 6;
+    const TileRect tr = tile_rect(g, t);
+    const int U = tile_units(tr);
+    if (tid == 0) run_s = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < U; b0 += 256) {
+        const int i = b0 + tid;
+        int u = -1, cnt = 0, ux, uy;
+        if (i < U) {
+            tile_unit(g, tr, i, &ux, &uy);
+            if (ux * 4 < g.mi_cols && uy * 4 < g.mi_rows) {
+                u = uy * A.f.mb_w + ux;
+                cnt = sk_min(A.tok_n[u], kTokCap);
+            }
+        }
+        int x = cnt;   // inclusive wave scan
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (l >= o) x += y;
+        }
+        if (l == 63) wsum_s[w] = x;
+        __syncthreads();
+        int pre = run_s;
+        for (int k = 0; k < w; k++) pre += wsum_s[k];
+        if (u >= 0) A.tok_off[u] = pre + x - cnt;
+        __syncthreads();
+        if (tid == 0) run_s += wsum_s[0] + wsum_s[1] + wsum_s[2] + wsum_s[3];
+        __syncthreads();
     }
-};
+    if (tid == 0) A.tile_ntok[t] = run_s;
+}
 
-// One wave per tile: the tile's CDFs in LDS, lane 0 codes the tokens in order.
+__global__ __launch_bounds__(256) void k_av1_tok_copy(Av1Args A) {
+    const Av1Geo& g = A.geo;
+    const int u = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane();
+    if (u >= A.f.mb_w * A.f.mb_h) return;
+    const int ux = u % A.f.mb_w, uy = u / A.f.mb_w;
+    const int t = (uy / 4 / g.tile_h_sb) * g.tile_cols + ux / 4 / g.tile_w_sb;
+    const int n = sk_min(A.tok_n[u], kTokCap);
+    const uint32_t* s = A.tok + (size_t)u * kTokCap;
+    uint32_t* d = A.tokc + (size_t)t * A.tile_tok_cap + A.tok_off[u];
+    for (int i = l; i < n; i += 64) d[i] = s[i];
+}
+
+// One wave per tile codes the tile's token stream. Every lane runs the (uniform)
+// coder state, so it lives in scalar registers; the CDF of a symbol is read and
+// adapted lane-parallel (lane i: cdf[i], lane N: the counter), and the next token's
+// CDF read is issued before the current symbol's interval arithmetic so its LDS
+// latency is hidden. Tokens stream through a 2 x 64 LDS ring (the batch after next is
+// in flight in a register) and are read two ahead; settled chunks go to an LDS ring
+// flushed 1024 at a time. Bit-exact with SymbolCoder (codec/av1_ec.h).
+constexpr int kObRing = 4096;
+constexpr int kObFlush = 1024;
+
+__device__ __forceinline__ uint32_t sgpr(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
 __global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
     __shared__ CdfContext cx;
-    const Av1Geo& g = A.geo;
-    const int t = blockIdx.x;
+    __shared__ uint16_t ob[kObRing];
+    __shared__ uint32_t tq[128];
+    const int t = blockIdx.x, L = threadIdx.x;
     const int q = coef_qctx(A.frame[1]);
-    const uint16_t* src = (const uint16_t*)&AV1_DEFAULT_CDF[q];
-    uint16_t* dst = (uint16_t*)&cx;
-    for (int i = threadIdx.x; i < (int)(sizeof(CdfContext) / 2); i += 64) dst[i] = src[i];
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    const TileRect tr = tile_rect(g, t);
-    ChunkSink sink{A.chunks + (size_t)t * A.tile_cap, 0, A.tile_cap};
-    SymbolCoder<ChunkSink> coder(sink);
-    int ux, uy;
-    for (int i = 0; tile_unit(g, tr, i, &ux, &uy); i++) {
-        if (ux * 4 >= g.mi_cols || uy * 4 >= g.mi_rows) continue;
-        const int u = uy * A.f.mb_w + ux;
-        const int n = sk_min(A.tok_n[u], kTokCap);
-        const uint32_t* tk = A.tok + (size_t)u * kTokCap;
-        for (int k = 0; k < n; k++) code_token(coder, dst, tk[k]);
+    {
+        const uint16_t* src = (const uint16_t*)&AV1_DEFAULT_CDF[q];
+        uint16_t* d16 = (uint16_t*)&cx;
+        for (int i = L; i < (int)(sizeof(CdfContext) / 2); i += 64) d16[i] = src[i];
     }
-    coder.finish();
-    A.tile_size[t] = sink.n <= A.tile_cap ? sink.n : -1;
+    uint16_t* cdfs = (uint16_t*)&cx;
+    const int ntok = A.tile_ntok[t];
+    const int cap = A.tile_cap;
+    const uint32_t* tk = A.tokc + (size_t)t * A.tile_tok_cap;
+    uint16_t* dst = A.chunks + (size_t)t * cap;
+    tq[L] = L < ntok ? tk[L] : 0u;
+    tq[64 + L] = 64 + L < ntok ? tk[64 + L] : 0u;
+    uint32_t R = 128 + L < ntok ? tk[128 + L] : 0u;   // batch 2
+    __syncthreads();
+    uint64_t low = 0;
+    uint32_t rng = 0x8000;
+    int cnt = -9, nb = 0, fl = 0;
+
+    auto put = [&](uint32_t x) {
+        if (L == 0) ob[nb & (kObRing - 1)] = (uint16_t)x;
+        nb++;
+    };
+    auto norm = [&](uint32_t r2) {
+        const int d = __builtin_clz(r2) - 16;
+        int c = cnt, s = c + d;
+        if (s >= 0) {
+            c += 16;
+            uint64_t m = (1ull << c) - 1;
+            if (s >= 8) {
+                put((uint32_t)(low >> c));
+                low &= m;
+                c -= 8;
+                m >>= 8;
+            }
+            put((uint32_t)(low >> c));
+            s = c + d - 24;
+            low &= m;
+        }
+        low <<= d;
+        rng = r2 << d;
+        cnt = s;
+    };
+    // symbol s of n with cdf[s - 1] = clo (s > 0) and cdf[s] = chi
+    auto enc = [&](uint32_t clo, uint32_t chi, int n, int s) {
+        const uint32_t r = rng;
+        const uint32_t v = (((r >> 8) * ((32768u - chi) >> kProbShift)) >> (7 - kProbShift)) + kMinProb * (n - s - 1);
+        const uint32_t u = s > 0 ? (((r >> 8) * ((32768u - clo) >> kProbShift)) >> (7 - kProbShift)) + kMinProb * (n - s) : r;
+        low += r - u;
+        norm(u - v);
+    };
+    auto flush = [&](int upto) {   // ring [fl, upto) -> dst (upto - fl <= kObFlush)
+        wsync();
+#pragma unroll 4
+        for (int j = 0; j < kObFlush; j += 64) {
+            const int i = fl + j + L;
+            if (i < upto && i < cap) dst[i] = ob[i & (kObRing - 1)];
+        }
+        fl = upto;
+        wsync();
+    };
+    auto sym_read = [&](uint32_t tt) -> uint32_t {   // lane i <= N: cdf[i]
+        const int n = (int)((tt >> 26) & 15) + 1;
+        return L <= n ? (uint32_t)cdfs[(tt & 0x3fffff) + L] : 0u;
+    };
+
+    uint32_t tcur = sgpr(tq[0]);
+    uint32_t tn1 = sgpr(tq[1]);   // token k + 1
+    uint32_t vn2 = tq[2];         // token k + 2 (LDS read in flight)
+    uint32_t cv = (ntok > 0 && (tcur >> 30) == 0) ? sym_read(tcur) : 0u;
+    for (int k = 0; k < ntok; k++) {
+        // the coder state is wave-uniform: keep it in scalar registers
+        rng = sgpr(rng);
+        cnt = (int)sgpr((uint32_t)cnt);
+        nb = (int)sgpr((uint32_t)nb);
+        fl = (int)sgpr((uint32_t)fl);
+        low = ((uint64_t)sgpr((uint32_t)(low >> 32)) << 32) | sgpr((uint32_t)low);
+        const uint32_t kind = tcur >> 30;
+        uint32_t clo = 0, chi = 0;
+        int n = 0, s = 0;
+        if (kind == 0) {   // adapt the symbol's CDF (lane-parallel update_cdf)
+            n = (int)((tcur >> 26) & 15) + 1;
+            s = (int)((tcur >> 22) & 15);
+            chi = (uint32_t)__builtin_amdgcn_readlane((int)cv, s);
+            clo = (uint32_t)__builtin_amdgcn_readlane((int)cv, s > 0 ? s - 1 : 0);
+            const int count = __builtin_amdgcn_readlane((int)cv, n);
+            const int rate = 3 + (count > 15) + (count > 31) + (n > 3 ? 2 : (n > 1 ? 1 : 0));
+            const int off = (int)(tcur & 0x3fffff);
+            if (L < n - 1) {
+                const int c = (int)cv;
+                cdfs[off + L] = (uint16_t)(L >= s ? c + ((32768 - c) >> rate) : c - (c >> rate));
+            } else if (L == n && count < 32) {
+                cdfs[off + L] = (uint16_t)(count + 1);
+            }
+        }
+        const int k1 = k + 1;
+        if ((k1 & 63) == 0) {   // entering batch j = k1 / 64: batch j + 1 -> the freed slot
+            tq[(((k1 >> 6) + 1) & 1) * 64 + L] = R;
+            if (nb - fl >= kObFlush) flush(fl + kObFlush);
+            const int nx = k1 + 128 + L;
+            R = nx < ntok ? tk[nx] : 0u;
+        }
+        // token k + 1: its CDF read; token k + 3: its LDS read
+        const uint32_t tnext = tn1;
+        tn1 = sgpr(vn2);
+        vn2 = tq[(k + 3) & 127];
+        if (k1 < ntok && (tnext >> 30) == 0) cv = sym_read(tnext);
+        // interval arithmetic of the current token
+        if (kind == 0) {
+            enc(sgpr(clo), sgpr(chi), (int)sgpr((uint32_t)n), (int)sgpr((uint32_t)s));
+        } else if (kind == 1) {
+            const int nbits = (int)((tcur >> 25) & 31) + 1;
+            for (int i = nbits - 1; i >= 0; i--) {
+                const uint32_t r = rng, split = ((r >> 8) << 7) + kMinProb;
+                if ((tcur >> i) & 1) {
+                    low += r - split;
+                    norm(split);
+                } else {
+                    norm(r - split);
+                }
+            }
+        } else {
+            uint16_t c2[3];
+            gather_partition_cdf(cdfs + (tcur & 0x3fffff), ((tcur >> 29) & 1) == 0, c2);
+            const uint32_t c0 = sgpr(c2[0]);
+            const int v = (int)((tcur >> 28) & 1);
+            enc(v ? c0 : 0u, v ? 32768u : c0, 2, v);
+        }
+        tcur = tnext;
+    }
+    {   // SymbolCoder::finish
+        int c = cnt;
+        const uint64_t m = 0x3fffu;
+        uint64_t e = ((low + m) & ~m) | (m + 1);
+        int s = c + 10;
+        if (s > 0) {
+            uint64_t nm = (1ull << (c + 16)) - 1;
+            do {
+                put((uint32_t)(e >> (c + 16)));
+                e &= nm;
+                s -= 8;
+                nm >>= 8;
+                c -= 8;
+            } while (s > 0);
+        }
+    }
+    while (nb - fl > 0) flush(fl + sk_min(nb - fl, kObFlush));
+    if (L == 0) A.tile_size[t] = nb <= cap ? nb : -1;
 }
 
 // Tile bytes (carry-resolved) -> host-mapped output at the tiles' prefix offsets.
+// carry_bytes (codec/av1_ec.h) in parallel: windows of chunks from the end; each
+// thread resolves a 64-chunk segment for carry-in 0, 1 and 2, a serial pass over the
+// 256 segment outcomes links them, then every thread writes its bytes.
 __global__ __launch_bounds__(256) void k_av1_pack(Av1Args A) {
-    __shared__ int off_s, n_s;
-    const int t = blockIdx.x;
-    if (threadIdx.x == 0) {
+    constexpr int kSeg = 64, kWin = 256 * kSeg;
+    __shared__ uint16_t win[kWin];
+    __shared__ uint8_t cout_s[256][3];
+    __shared__ uint8_t cin_s[256];
+    __shared__ int off_s, n_s, carry_s;
+    const int t = blockIdx.x, tid = threadIdx.x;
+    if (tid == 0) {
         int off = 0;
         for (int k = 0; k < t; k++) off += sk_max(A.tile_size[k], 0);
         n_s = A.tile_size[t];
         off_s = off;
+        carry_s = 0;
         A.out_size_host[t] = (n_s >= 0 && off + n_s <= A.out_cap) ? n_s : -1;
     }
     __syncthreads();
     const int n = n_s, off = off_s;
     if (n < 0 || off + n > A.out_cap) return;
     const uint16_t* ch = A.chunks + (size_t)t * A.tile_cap;
-    // carry_bytes: byte i = (sum of chunks >= i with carries) -- resolve with a serial
-    // backwards pass on lane 0 into the chunk buffer, then copy out in parallel
-    if (threadIdx.x == 0) {
-        uint16_t* c2 = A.chunks + (size_t)t * A.tile_cap;
-        uint32_t carry = 0;
-        for (int i = n - 1; i >= 0; i--) {
-            carry += c2[i];
-            c2[i] = (uint16_t)(carry & 0xff);
-            carry >>= 8;
+    for (int w1 = n; w1 > 0; w1 -= kWin) {   // window [w0, w1)
+        const int w0 = sk_max(w1 - kWin, 0), wn = w1 - w0;
+        for (int i = tid; i < wn; i += 256) win[i] = ch[w0 + i];
+        __syncthreads();
+        const int s0 = tid * kSeg, s1 = sk_min(s0 + kSeg, wn);
+        for (int ci = 0; ci < 3; ci++) {
+            uint32_t c = (uint32_t)ci;
+            for (int i = s1 - 1; i >= s0; i--) c = (c + win[i]) >> 8;
+            cout_s[tid][ci] = (uint8_t)c;
         }
+        __syncthreads();
+        if (tid == 0) {
+            int c = carry_s;
+            for (int sg = 255; sg >= 0; sg--) {
+                cin_s[sg] = (uint8_t)c;
+                if (sg * kSeg < wn) c = cout_s[sg][c];
+            }
+            carry_s = c;
+        }
+        __syncthreads();
+        uint32_t c = cin_s[tid];
+        for (int i = s1 - 1; i >= s0; i--) {
+            c += win[i];
+            A.out_host[off + w0 + i] = (uint8_t)(c & 0xff);
+            c >>= 8;
+        }
+        __syncthreads();
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += 256) A.out_host[off + i] = (uint8_t)ch[i];
 }
 
 // Rows below the picture repeat its last row (the reference clamp AV1's MC reads),
@@ -631,6 +843,8 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_av1_merge, dim3(a.geo.sb_cols * a.geo.sb_rows), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_modes, dim3((a.geo.c8 * a.geo.r8 + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_tokens, dim3((n + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_av1_tok_scan, dim3(tiles), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_tok_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_finish, dim3((a.f.stride_y + 255) / 256), dim3(256), 0, s, a);
@@ -639,3 +853,50 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
 }  // namespace gpu
 }  // namespace av1
 }  // namespace sk
+
+// Test entry: k_av1_ec + k_av1_pack over caller token streams (tile t: tok[offs[t],
+// offs[t] + ns[t])) with the default CDFs of qidx; out receives tile t's bytes at
+// offs_out = prefix of sizes. Returns 0, or -1 on a HIP error.
+extern "C" int sk_av1_ec_tokens_hip(const uint32_t* tok, const int32_t* offs, const int32_t* ns, int tiles, int qidx,
+                                    uint8_t* out, int out_cap, int32_t* sizes) {
+    using namespace sk::av1::gpu;
+    int maxn = 1;
+    for (int t = 0; t < tiles; t++) maxn = ns[t] > maxn ? ns[t] : maxn;
+    Av1Args a;
+    memset(&a, 0, sizeof(a));
+    a.tile_tok_cap = maxn;
+    a.tile_cap = 8 * maxn + 64;
+    a.out_cap = out_cap;
+    std::vector<uint32_t> tc((size_t)tiles * maxn, 0u);
+    for (int t = 0; t < tiles; t++) memcpy(&tc[(size_t)t * maxn], tok + offs[t], sizeof(uint32_t) * ns[t]);
+    int frame[2] = {0, qidx};
+    bool ok = true;
+    auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
+    chk(hipMalloc(&a.tokc, tc.size() * 4));
+    chk(hipMalloc(&a.tile_ntok, tiles * 4));
+    chk(hipMalloc(&a.frame, 8));
+    chk(hipMalloc(&a.chunks, (size_t)tiles * a.tile_cap * 2));
+    chk(hipMalloc(&a.tile_size, tiles * 4));
+    chk(hipMalloc(&a.out_host, out_cap));
+    chk(hipMalloc(&a.out_size_host, tiles * 4));
+    if (ok) {
+        chk(hipMemcpy(a.tokc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice));
+        chk(hipMemcpy(a.tile_ntok, ns, tiles * 4, hipMemcpyHostToDevice));
+        chk(hipMemcpy(a.frame, frame, 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, 0, a);
+        hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, 0, a);
+        chk(hipGetLastError());
+        chk(hipDeviceSynchronize());
+        chk(hipMemcpy(sizes, a.out_size_host, tiles * 4, hipMemcpyDeviceToHost));
+        chk(hipMemcpy(out, a.out_host, out_cap, hipMemcpyDeviceToHost));
+    }
+    (void)hipFree(a.tokc);
+    (void)hipFree(a.tile_ntok);
+    (void)hipFree(a.frame);
+    (void)hipFree(a.chunks);
+    (void)hipFree(a.tile_size);
+    (void)hipFree(a.out_host);
+    (void)hipFree(a.out_size_host);
+    return ok ? 0 : -1;
+}
+

@@ -75,10 +75,13 @@ struct FrameArgs {
     RcState* rc;           // K10 rate-control state (ratecontrol.h), device
     long long* rc_slice;   // [num_slices][2] complexity sums of P-planned slices (SAD, activity)
     float rc_fps;          // session frame rate (CBR frame budget)
+    int* rc_redo;          // K10 CBR guard: device flag, 1 = code the frame again (k_rc_guard)
+    const int* gate;       // second-pass launches: run only when *gate != 0 (null: always)
 };
 
 void launch_convert_damage(const FrameArgs& a, hipStream_t s);
-void launch_encode(const FrameArgs& a, hipStream_t s);   // k_plan and everything after it
+// k_plan and everything after it; guard: CBR overflow guard + gated second coding pass
+void launch_encode(const FrameArgs& a, hipStream_t s, bool guard = false);
 // k_plan, motion search and scene-cut decisions only (the HEVC back end follows it)
 void launch_frontend(const FrameArgs& a, hipStream_t s);
 void launch_commit(const FrameArgs& a, hipStream_t s);   // MV field + reference update (+ K7 deblocking)

@@ -762,6 +762,35 @@ __global__ __launch_bounds__(64) void k_rc_account(FrameArgs a, const int* sizes
     if (threadIdx.x == 0) rc_account(*a.rc, 8 * b);
 }
 
+// K10 CBR guard after k_slice_scan: every workgroup (one per slice) evaluates the same
+// overflow test on the frame's payload; on a redo, workgroup 0 moves the slice QPs
+// (rc_redo) and raises the flag for the gated second pass, and each workgroup clears
+// the header / trailing bits the first k_slice_scan left in its RBSP slot.
+__global__ __launch_bounds__(256) void k_rc_guard(FrameArgs a) {
+    __shared__ long long part[4];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    long long b = 0;
+    for (int i = tid; i < a.num_slices; i += 256)
+        if (a.tasks[i].final_action != ACT_NONE) b += a.slice_info[4 * i];
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_down(b, o);
+    if ((tid & 63) == 0) part[tid >> 6] = b;
+    __syncthreads();
+    const long long bits = 8 * (part[0] + part[1] + part[2] + part[3]);
+    // rc_redo changes only cur_qp / redos / tasks, none of which rc_redo_step reads:
+    // every workgroup takes the same decision whatever the order
+    const int step = rc_redo_step(*a.rc, bits);
+    if (s == 0 && tid == 0) {
+        const int applied = step ? rc_redo(*a.rc, a.tasks, a.num_slices, bits) : 0;
+        *a.rc_redo = applied ? 1 : 0;
+        if (applied)
+            for (int i = 0; i < a.num_slices; i++) a.tasks_host[i].qp = a.tasks[i].qp;
+    }
+    if (!step || a.tasks[s].final_action == ACT_NONE) return;
+    uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    const int words = (a.slice_info[4 * s] + 3) / 4 + 1;
+    for (int i = tid; i < words; i += 256) rbsp[i] = 0u;
+}
+
 // ---------------------------------------------------------------------------
 // Macroblock residual coding shared by the inter and intra kernels.
 struct MbScratch {                 // per-wave LDS
@@ -1526,6 +1555,7 @@ __global__ __launch_bounds__(256) void k_subpel(FrameArgs a) {
 // K6 inter: one wave per MB of a P slice (SKIPALL slices just record skips).
 // 4 waves per workgroup, one MB per wave: the CAVLC tables are loaded once per 4 MBs.
 __global__ __launch_bounds__(256) void k_code_inter(FrameArgs a) {
+    if (a.gate && *a.gate == 0) return;   // CBR second pass not needed
     __shared__ MbScratch Sw[4];
     __shared__ QpelLds Qw[4];   // fractional-MV luma MC
     __shared__ CavlcTables T;
@@ -1801,6 +1831,7 @@ __device__ void load_nb_planes(const Planes& P, int sy, int sc, int mbx, int mby
 // with that prediction. k_code_intra's wavefront then only predicts, quantises from
 // that QP and reconstructs (no mode search, usually no escalation in the chain).
 __global__ __launch_bounds__(256) void k_intra_prep(FrameArgs a) {
+    if (a.gate && *a.gate == 0) return;   // CBR second pass not needed
     __shared__ MbScratch Sw[4];
     __shared__ CavlcTables T;
     __shared__ uint8_t nb_w[4][64];   // top 16 | left 16 | ctop 2x8 | cleft 2x8
@@ -1945,6 +1976,7 @@ constexpr int kIntraRing = 4;   // MB slots per row in flight (producer runs 2 s
 // are LDS, and its global stores (reconstruction, levels, MB info) are never waited on.
 template <int MAXROWS>
 __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) {
+    if (a.gate && *a.gate == 0) return;   // CBR second pass not needed
     __shared__ MbScratch Sw[MAXROWS];
     __shared__ IntraEdges E;
     __shared__ IntraSrc R[MAXROWS][kIntraRing];
@@ -2134,6 +2166,7 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
 // the offsets and the staged words are OR-ed into the MB's bit buffer.
 constexpr int kCavlcStageWords = 24;   // 768 bits per block; longer blocks are re-coded in place
 __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
+    if (a.gate && *a.gate == 0) return;   // CBR second pass not needed
     __shared__ uint32_t bits_w[4][kMbSlotBytes / 4];
     __shared__ uint32_t stage_w[4][27 * kCavlcStageWords];
     __shared__ int16_t coef_w[4][kCoefPerMb];
@@ -2293,6 +2326,7 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
 constexpr int kTile = 4096;
 
 __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
+    if (a.gate && *a.gate == 0) return;   // CBR second pass not needed
     __shared__ uint32_t hdr[32];
     __shared__ int wave_tot[5];
     __shared__ int sh_misc[4];
@@ -2937,11 +2971,9 @@ void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, 
     hipLaunchKernelGGL(k_rc_account, dim3(1), dim3(64), 0, s, a, sizes, n, stride, per_slice);
 }
 
-void launch_encode(const FrameArgs& a, hipStream_t s) {
+// Transform / quantisation / reconstruction / CAVLC / slice scan of every coded slice.
+static void launch_code(const FrameArgs& a, hipStream_t s) {
     int nmb = a.mb_w * a.mb_h;
-    launch_frontend(a, s);
-    if (a.aq_strength > 0) hipLaunchKernelGGL(k_aq, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
-    if (a.subpel) hipLaunchKernelGGL(k_subpel, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_code_inter, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_intra_prep, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     if (a.rows_per_slice <= 4)
@@ -2950,6 +2982,20 @@ void launch_encode(const FrameArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_code_intra<kMaxRows - 1>, dim3(a.num_slices), dim3(64 * kMaxRows), 0, s, a);
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_slice_scan, dim3(a.num_slices), dim3(256), 0, s, a);
+}
+
+void launch_encode(const FrameArgs& a, hipStream_t s, bool guard) {
+    int nmb = a.mb_w * a.mb_h;
+    launch_frontend(a, s);
+    if (a.aq_strength > 0) hipLaunchKernelGGL(k_aq, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
+    if (a.subpel) hipLaunchKernelGGL(k_subpel, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
+    launch_code(a, s);
+    if (guard && a.rc_redo) {   // K10 CBR: VBV overflow -> one coarser pass (kernels exit early otherwise)
+        hipLaunchKernelGGL(k_rc_guard, dim3(a.num_slices), dim3(256), 0, s, a);
+        FrameArgs b = a;
+        b.gate = a.rc_redo;
+        launch_code(b, s);
+    }
     hipLaunchKernelGGL(k_mb_concat, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     const dim3 tiles(a.max_tiles, a.num_slices);
     hipLaunchKernelGGL(k_ep_nz, tiles, dim3(256), 0, s, a);

@@ -108,6 +108,9 @@ class CaptureSession {
                 e.aq_strength = sk_clip(s.h264_aq_strength, 0, 64);
                 e.subpel = s.h264_subpel >= 0 ? 1 : 0;
                 e.intra4x4 = s.h264_intra4x4 > 0 ? 1 : 0;
+                e.rc_mode = s.h264_rc_mode >= 0 && s.h264_rc_mode <= 2 ? s.h264_rc_mode : h264::RC_CQP;
+                e.bitrate_kbps = s.h264_bitrate_kbps > 0 ? s.h264_bitrate_kbps : 0;
+                if (e.rc_mode == h264::RC_CBR && e.bitrate_kbps <= 0) e.rc_mode = h264::RC_CRF;
                 if (s.output_mode == 2 || s.output_mode == 3) {   // HEVC / AV1: full-frame pictures
                     e.codec = s.output_mode == 2 ? 1 : 2;
                     e.fullframe = 1;
@@ -154,6 +157,10 @@ class CaptureSession {
 
     void request_keyframe() { key_req_ = true; }
     void set_qp(int qp, int paint_qp) { qp_req_ = (qp & 0xffff) | (paint_qp & 0xffff) << 16; }
+    // K10: switch the rate control mode / CBR target from the next frame
+    void set_rate(int mode, int kbps) {
+        rate_req_ = (int64_t)1 << 62 | (int64_t)(mode & 0xff) << 32 | (uint32_t)(kbps > 0 ? kbps : 0);
+    }
     void set_frame_callback(sk_frame_cb cb, void* user) {
         frame_cb_ = cb;
         frame_user_ = user;
@@ -359,6 +366,7 @@ class CaptureSession {
         while (running_) {
             if (key_req_.exchange(false)) enc_->request_keyframe();
             if (int qq = qp_req_.exchange(0)) enc_->set_qp(qq & 0xffff, qq >> 16);
+            if (int64_t rr = rate_req_.exchange(0)) enc_->set_rate((int)((rr >> 32) & 0xff), (int)(rr & 0xffffffff));
             if (q.empty()) {
                 if (step) {
                     if (!take_budget(true)) continue;
@@ -504,6 +512,7 @@ class CaptureSession {
     std::thread th_;
     std::atomic<bool> running_{false}, key_req_{false};
     std::atomic<int> qp_req_{0};
+    std::atomic<int64_t> rate_req_{0};
     uint64_t hist_[kHist] = {};
     double src_kind_ = -1.0;  // 1 x11, 0 synthetic, -1 none (kept after stop for stats)
     std::mutex mu_;
@@ -534,6 +543,7 @@ int sk_capture_latencies(void* c, float* out, int cap, int reset) {
 void sk_capture_stop(void* c) { static_cast<CaptureSession*>(c)->stop(); }
 void sk_capture_request_keyframe(void* c) { static_cast<CaptureSession*>(c)->request_keyframe(); }
 void sk_capture_set_qp(void* c, int qp, int paint_qp) { static_cast<CaptureSession*>(c)->set_qp(qp, paint_qp); }
+void sk_capture_set_rate(void* c, int mode, int kbps) { static_cast<CaptureSession*>(c)->set_rate(mode, kbps); }
 void sk_capture_stats(void* c, double* out, int n) { static_cast<CaptureSession*>(c)->stats(out, n); }
 void sk_capture_set_watermark(void* c, const uint8_t* bgra, int w, int h, int location) {
     static_cast<CaptureSession*>(c)->set_watermark(bgra, w, h, location);

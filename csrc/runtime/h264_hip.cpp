@@ -75,6 +75,7 @@ class HipBackend : public EncoderBackend {
     }
     // K10: picked up by k_rc_qp at the next frame (a change counter tells it apart).
     void set_rate(int mode, int kbps) override {
+        cfg_.rc_mode = mode;   // graphs re-captured with / without the CBR guard (launch)
         __atomic_store_n(&h_key_seq_[3], mode, __ATOMIC_SEQ_CST);
         __atomic_store_n(&h_key_seq_[4], kbps, __ATOMIC_SEQ_CST);
         __atomic_fetch_add(&h_key_seq_[5], 1, __ATOMIC_SEQ_CST);
@@ -155,6 +156,11 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipSetDevice(device_));
         const int p = launched_ & 1;
         parity_ = p;
+        if ((cfg_.rc_mode == RC_CBR) != graph_guard_) {   // K10 CBR guard in / out of the graphs
+            HIPCHECK(hipStreamSynchronize(stream_));
+            invalidate_graphs();
+            graph_guard_ = cfg_.rc_mode == RC_CBR;
+        }
         set_parity_args(args_.bgrx_stride);   // bgrx = bgrx_dev_[p], host outputs of parity p
         // host-mapped, read by this frame's k_plan: per parity, because with two frames
         // in flight the previous frame's k_plan may not have run yet
@@ -460,6 +466,8 @@ class HipBackend : public EncoderBackend {
             a.rc = dmalloc<RcState>(1);
             HIPCHECK(hipMemcpy(a.rc, &rc, sizeof(rc), hipMemcpyHostToDevice));
             a.rc_slice = dmalloc<long long>(2 * (size_t)ns);
+            a.rc_redo = dmalloc<int>(1);
+            a.gate = nullptr;
             a.rc_fps = cfg_.fps;
             h_key_seq_[3] = cfg_.rc_mode;
             h_key_seq_[4] = cfg_.bitrate_kbps;
@@ -579,7 +587,7 @@ class HipBackend : public EncoderBackend {
                 hevc::gpu::launch_backend(ha, stream_);
                 gpu::launch_rc_account(args_, ha.sub_size, g_.mb_h, 1, 0, stream_);
             } else {
-                gpu::launch_encode(args_, stream_);
+                gpu::launch_encode(args_, stream_, graph_guard_);
             }
         } else {
             gpu::launch_commit(args_, stream_);
@@ -666,6 +674,10 @@ class HipBackend : public EncoderBackend {
         // coder chunks: 4 KB per unit of the largest tile (incompressible content codes
         // below ~1.5 bytes per sample)
         const int tile_units = (av1_geo_.tile_w_sb * 4) * (av1_geo_.tile_h_sb * 4);
+        a.tile_tok_cap = tile_units * av1::gpu::kTokCap;
+        a.tokc = dmalloc<uint32_t>((size_t)tiles * a.tile_tok_cap, false);
+        a.tok_off = dmalloc<int>(n);
+        a.tile_ntok = dmalloc<int>(tiles);
         a.tile_cap = tile_units * 4096;
         a.chunks = dmalloc<uint16_t>((size_t)tiles * a.tile_cap, false);
         a.tile_size = dmalloc<int>(tiles);
@@ -852,6 +864,7 @@ class HipBackend : public EncoderBackend {
     uint8_t* ov_stage_ = nullptr;
     hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
+    bool graph_guard_ = false;   // the captured H.264 graphs contain the K10 CBR guard
     hipStream_t copy_stream_ = nullptr;   // shared per device (not owned)
     hipStream_t up_stream_ = nullptr;     // this session's upload stream (owned, lazily created)
     // 0: on the session stream (behind the frame in flight), 1: own upload stream,

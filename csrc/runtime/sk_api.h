@@ -117,6 +117,10 @@ typedef struct sk_capture_settings {
     int32_t h264_aq_strength;  // MB-level adaptive QP, Q4 (16 = x264 aq-strength 1.0)
     int32_t h264_subpel;       // < 0: integer-pel motion only
     int32_t h264_intra4x4;     // > 0: I_NxN macroblocks in keyframes
+    // K10 rate control (codec/ratecontrol.h): 0 = constant QP (h264_crf as QP),
+    // 1 = CRF (complexity-adaptive QP around h264_crf), 2 = CBR at h264_bitrate_kbps
+    int32_t h264_rc_mode;
+    int32_t h264_bitrate_kbps;
 } sk_capture_settings;
 
 typedef struct sk_stripe_result {
@@ -148,6 +152,7 @@ int sk_capture_latencies(void* c, float* out, int cap, int reset);
 void sk_capture_stop(void* c);
 void sk_capture_request_keyframe(void* c);
 void sk_capture_set_qp(void* c, int qp, int paint_qp);
+void sk_capture_set_rate(void* c, int mode, int kbps);   // K10: 0 CQP, 1 CRF, 2 CBR at kbps
 // frames, mean encode ms, bytes, packets, source (1 = X11, 0 = synthetic), last encode ms
 void sk_capture_stats(void* c, double* out, int n);
 // Premultiplied BGRA watermark composited before encoding (location enum in capture.cpp).

@@ -3,6 +3,7 @@
 #include <cstring>
 #include <vector>
 
+#include "../codec/av1_core.h"
 #include "../codec/av1_ec.h"
 #include "sk_api.h"
 
@@ -30,6 +31,41 @@ int sk_av1_ec_encode(const int32_t* kind, const int32_t* ctx, const int32_t* sym
     if ((int)b.size() > cap) return -(int)b.size();
     if (!b.empty()) std::memcpy(out, b.data(), b.size());
     return (int)b.size();
+}
+
+// Adaptive CDF arrays of the default context for token-stream tests: field i ->
+// (offset of its first CDF in u16 units, symbols N, number of CDFs). Returns the
+// number of fields when i is out of range.
+int sk_av1_cdf_field(int i, int32_t* off, int32_t* nsym, int32_t* count) {
+    using sk::av1::CdfContext;
+    const CdfContext& c = sk::av1::AV1_DEFAULT_CDF[0];
+    struct F { const uint16_t* p; int n; size_t bytes; };
+#define SK_FIELD(f, n) F{(const uint16_t*)&c.f, n, sizeof(c.f)}
+    const F fs[] = {SK_FIELD(kf_y_mode, 13),   SK_FIELD(uv_mode_cfl_allowed, 14), SK_FIELD(partition_w16, 10),
+                    SK_FIELD(partition_w8, 4), SK_FIELD(eob_pt_16, 5),            SK_FIELD(eob_pt_1024, 11),
+                    SK_FIELD(coeff_base, 4),   SK_FIELD(coeff_br, 4),             SK_FIELD(coeff_base_eob, 3),
+                    SK_FIELD(txb_skip, 2),     SK_FIELD(skip, 2),                 SK_FIELD(mv_joint, 4)};
+#undef SK_FIELD
+    const int nf = (int)(sizeof(fs) / sizeof(fs[0]));
+    if (i < 0 || i >= nf) return nf;
+    *off = (int32_t)(fs[i].p - (const uint16_t*)&c);
+    *nsym = fs[i].n;
+    *count = (int32_t)(fs[i].bytes / (2 * (fs[i].n + 1)));
+    return nf;
+}
+
+// Host replay of a token stream (av1_core.h token format) through SymbolCoder with
+// the default CDFs of qidx: the reference for the GPU coder k_av1_ec.
+int sk_av1_ec_tokens_cpu(const uint32_t* tok, int n, int qidx, uint8_t* out, int cap) {
+    sk::av1::CdfContext cx = sk::av1::AV1_DEFAULT_CDF[sk::av1::coef_qctx(qidx)];
+    sk::av1::VectorSink sink;
+    sk::av1::SymbolCoder<sk::av1::VectorSink> coder(sink);
+    for (int i = 0; i < n; i++) sk::av1::code_token(coder, (uint16_t*)&cx, tok[i]);
+    coder.finish();
+    const int m = (int)sink.v.size();
+    if (m > cap) return -m;
+    if (m) sk::av1::carry_bytes(sink.v.data(), m, out);
+    return m;
 }
 
 }  // extern "C"

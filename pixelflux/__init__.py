@@ -48,6 +48,7 @@ def default_settings(width: int = 1920, height: int = 1080, **kw) -> CaptureSett
     s.jpeg_quality, s.paint_over_jpeg_quality, s.use_paint_over_quality = 40, 90, 1
     s.paint_over_trigger_frames, s.damage_block_threshold, s.damage_block_duration = 15, 10, 20
     s.h264_crf, s.h264_paintover_crf, s.h264_paintover_burst_frames = 25, 18, 5
+    s.h264_rc_mode, s.h264_bitrate_kbps = 1, 0   # K10: CRF around h264_crf (x264 crf semantics)
     s.h264_fullcolor = s.h264_streaming_mode = s.h264_fullframe = 0
     s.use_cpu = 0
     s.vaapi_render_node_index = -1
@@ -147,6 +148,12 @@ class ScreenCapture:
         """H.264 rate control from the next frame on (the WebRTC mode's bitrate controller)."""
         if self._h:
             self._lib.sk_capture_set_qp(self._h, int(qp), int(paint_qp))
+
+    def set_rate(self, mode: str = "crf", kbps: int = 0) -> None:
+        """K10 rate control from the next frame: 'cqp', 'crf' (around h264_crf) or
+        'cbr' at `kbps` with a 1.5-frame VBV (csrc/codec/ratecontrol.h)."""
+        if self._h:
+            self._lib.sk_capture_set_rate(self._h, {"cqp": 0, "crf": 1, "cbr": 2}[mode], int(kbps))
 
     def stats(self) -> dict:
         arr = (ctypes.c_double * 16)()

@@ -268,6 +268,8 @@ class StreamSession:
                                        output_mode=pixelflux.OUTPUT_MODE_HEVC if self.hevc else
                                        pixelflux.OUTPUT_MODE_H264,
                                        h264_crf=self.rc.qp, h264_paintover_crf=self.rc.paint_qp,
+                                       # K10 in the encoder: CBR with a 1.5-frame VBV (gstwebrtc_app.py:101-105)
+                                       h264_rc_mode=2, h264_bitrate_kbps=max(1, self.rc.target_bps // 1000),
                                        use_cpu=1 if _truthy(self.args.use_cpu) else 0, source=src,
                                        device=int(self.args.gpu_id), stripe_height=64,
                                        capture_cursor=0 if _truthy(self.args.enable_cursors) else 1)
@@ -294,9 +296,12 @@ class StreamSession:
         ts = int((time.monotonic() - self._t0) * 90000)
         self.pc.send_video(data[10:], ts)
         self.frames_sent += 1
-        q = self.rc.on_frame(len(data) - 10, key)
-        if q is not None and self.capture is not None:
-            self.capture.set_qp(q, self.rc.paint_qp)
+        self.rc.on_frame(len(data) - 10, key)   # delivered-rate statistics; the encoder runs the CBR loop
+
+    def _apply_rate(self) -> None:
+        """Current target (vb, / REMB) -> the encoder's CBR budget from its next frame."""
+        if self.capture is not None:
+            self.capture.set_rate("cbr", max(1, self.rc.target_bps // 1000))
 
     async def _start_audio(self) -> None:
         from selkies_gstreamer_amd.server.audio import AudioPipeline
@@ -321,6 +326,7 @@ class StreamSession:
     def _on_remb(self, bps: int) -> None:
         if _truthy(self.args.congestion_control):
             self.rc.set_target(min(bps, int(self.args.video_bitrate) * 1000))
+            self._apply_rate()
 
     # -- data channel ------------------------------------------------------------------------------
     def send_message(self, msg_type: str, data) -> None:
@@ -345,6 +351,7 @@ class StreamSession:
                 kbps = int(toks[1])
                 self.args.video_bitrate = str(kbps)
                 self.rc.set_target(kbps * 1000)
+                self._apply_rate()
                 self.send_message("pipeline", {"status": f"Video bitrate set to: {kbps}"})
                 save_overlay(self.args.json_config, self.args)
             elif t == "ab":

@@ -68,6 +68,7 @@ class SkCaptureSettings(ctypes.Structure):
         ("step_mode", ctypes.c_int32), ("pool", ctypes.c_void_p),
         ("pool_frames", ctypes.c_int32), ("pool_stride", ctypes.c_int32), ("pool_phase", ctypes.c_int32),
         ("h264_aq_strength", ctypes.c_int32), ("h264_subpel", ctypes.c_int32), ("h264_intra4x4", ctypes.c_int32),
+        ("h264_rc_mode", ctypes.c_int32), ("h264_bitrate_kbps", ctypes.c_int32),
     ]
 
 
@@ -145,6 +146,7 @@ def lib():
         L.sk_capture_stop.argtypes = [ctypes.c_void_p]
         L.sk_capture_request_keyframe.argtypes = [ctypes.c_void_p]
         L.sk_capture_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.sk_capture_set_rate.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.sk_capture_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.sk_capture_set_watermark.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int]
@@ -223,7 +225,7 @@ TASK_DTYPE = np.dtype([(n, "<i4") for n in (
 RC_MODES = {"cqp": 0, "crf": 1, "cbr": 2}
 RC_FIELDS = ("mode", "base_qp", "qp_min", "qp_max", "budget", "vbv_size", "fullness", "frames", "last_qp_p",
              "last_qp_i", "last_bits_p", "last_bits_i", "last_cplx_p", "last_cplx_i", "cplx_ema", "cur_qp",
-             "cur_intra", "cur_cplx", "max_p_bits", "seq", "cur_valid")
+             "cur_intra", "cur_cplx", "max_p_bits", "seq", "cur_valid", "pixels", "cur_idr", "redos", "qp_floor", "floor_age", "last_mbs_p", "last_mbs_i", "cur_mbs")
 
 
 class H264Encoder:
@@ -422,8 +424,8 @@ class H264Encoder:
         lib().sk_h264_set_rate(self._h, RC_MODES[mode], int(kbps))
 
     def rc_stats(self) -> dict:
-        arr = (ctypes.c_int32 * 20)()
-        n = lib().sk_h264_rc_stats(self._h, arr, 20)
+        arr = (ctypes.c_int32 * 32)()
+        n = lib().sk_h264_rc_stats(self._h, arr, 32)
         return {k: int(arr[i]) for i, k in enumerate(RC_FIELDS) if i < n}
 
     def stage_times(self, n: int = 16) -> list[float]:

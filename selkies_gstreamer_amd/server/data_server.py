@@ -45,7 +45,7 @@ RECONNECT_DEBOUNCE_S = 0.5
 CURSOR_SIZE = 32
 VIDEO_KEYS = ("encoder", "framerate", "h264_crf", "h264_fullcolor", "h264_streaming_mode", "jpeg_quality",
               "paint_over_jpeg_quality", "use_cpu", "h264_paintover_crf", "h264_paintover_burst_frames",
-              "use_paint_over_quality")
+              "use_paint_over_quality", "h264_bitrate")
 
 
 class _VideoFrame:
@@ -511,7 +511,8 @@ class DataStreamingServer:
                 "paint_over_jpeg_quality": s.initial("paint_over_jpeg_quality"), "use_cpu": s.initial("use_cpu"),
                 "h264_paintover_crf": s.initial("h264_paintover_crf"),
                 "h264_paintover_burst_frames": s.initial("h264_paintover_burst_frames"),
-                "use_paint_over_quality": s.initial("use_paint_over_quality")}
+                "use_paint_over_quality": s.initial("use_paint_over_quality"),
+                "h264_bitrate": s.initial("h264_bitrate")}
 
     async def apply_client_settings(self, did: str, parsed: dict, initial: bool):
         st = self.displays.get(did)
@@ -552,7 +553,12 @@ class DataStreamingServer:
                 if st.scaling_dpi is not None or initial:
                     await set_dpi(int(dpi), display=self.x_display)
                 st.scaling_dpi = dpi
-            video_changed = any(st.params.get(k) != old.get(k) for k in VIDEO_KEYS)
+            changed = {k for k in VIDEO_KEYS if st.params.get(k) != old.get(k)}
+            video_changed = bool(changed)
+            if changed == {"h264_bitrate"} and did in self.captures and not initial:
+                # K10 rate change: applied to the running encoder from its next frame
+                self._set_rate(did, int(st.params.get("h264_bitrate") or 0))
+                video_changed = False
         if restart_audio:
             await self.audio.stop()
             await self.audio.start(self.audio_bitrate)
@@ -674,6 +680,8 @@ class DataStreamingServer:
         else:
             cs.output_mode = 1
             cs.h264_crf = int(p["h264_crf"])
+            kbps = int(p.get("h264_bitrate") or 0)   # K10: CRF, or CBR at kbps
+            cs.h264_rc_mode, cs.h264_bitrate_kbps = (2, kbps) if kbps > 0 else (1, 0)
             cs.h264_paintover_crf = int(p["h264_paintover_crf"])
             cs.h264_paintover_burst_frames = int(p["h264_paintover_burst_frames"])
             cs.h264_fullcolor = int(bool(p["h264_fullcolor"]))
@@ -757,6 +765,13 @@ class DataStreamingServer:
             await self._start_bp(did)
         if self.metrics is not None:
             self.metrics.capture_started(did, module)
+
+    def _set_rate(self, did: str, kbps: int) -> None:
+        """K10: CRF (kbps 0) or CBR at kbps on the display's running encoder."""
+        cap = self.captures.get(did)
+        fn = getattr(getattr(cap, "module", None), "set_rate", None)
+        if fn is not None:
+            fn("cbr" if kbps > 0 else "crf", kbps)
 
     async def _stop_capture(self, did: str):
         await self._stop_bp(did)

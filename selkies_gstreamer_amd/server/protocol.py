@@ -51,7 +51,7 @@ MIC_BUFFER_MAX = MIC_SAMPLE_RATE * 2 * 2  # 2 s of s16 mono
 # --------------------------------------------------------------------------- SETTINGS
 _INT_KEYS = ("framerate", "h264_crf", "manual_width", "manual_height", "audio_bitrate", "initialClientWidth",
              "initialClientHeight", "jpeg_quality", "paint_over_jpeg_quality", "h264_paintover_crf",
-             "h264_paintover_burst_frames", "scaling_dpi")
+             "h264_paintover_burst_frames", "scaling_dpi", "h264_bitrate")
 _BOOL_KEYS = ("h264_fullcolor", "h264_streaming_mode", "is_manual_resolution_mode", "use_cpu",
               "use_paint_over_quality", "enable_binary_clipboard")
 _STR_KEYS = ("encoder", "displayId", "displayPosition")

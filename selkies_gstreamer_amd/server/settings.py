@@ -109,6 +109,8 @@ def build_specs() -> list[Spec]:
              allowed=["x264enc", "x264enc-striped", "jpeg"]),
         _r("framerate", "8-120", 60, "Allowed framerate range or a fixed value."),
         _r("h264_crf", "5-50", 25, "Allowed H.264 CRF range or a fixed value."),
+        _r("h264_bitrate", "0-500000", 0, "H.264 bitrate in kbit/s: 0 = CRF (complexity-adaptive QP around "
+           "h264_crf), > 0 = CBR with a 1.5-frame VBV (extension; the reference has CRF only)."),
         _r("jpeg_quality", "1-100", 40, "Allowed JPEG quality range or a fixed value."),
         _b("h264_fullcolor", False, "H.264 full colour range."),
         _b("h264_streaming_mode", False, "H.264 streaming mode (encode every frame)."),

@@ -96,54 +96,99 @@ def test_update_cdf_rule():
     assert cdf == [8192 + (32768 - 8192) // 32, 16384 + 16384 // 32, 24576 + 8192 // 32, 32768, 1]
 
 
+def _fields(L):
+    P = ctypes.POINTER
+    L.sk_av1_cdf_field.argtypes = [ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_int32)]
+    L.sk_av1_cdf_field.restype = ctypes.c_int
+    out, i = [], 0
+    while True:
+        off, n, cnt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        nf = L.sk_av1_cdf_field(i, off, n, cnt)
+        if i >= nf:
+            return out
+        out.append((off.value, n.value, cnt.value))
+        i += 1
+
+
+def _token_streams(L, seed, tiles):
+    """Random token streams in the av1_core.h format: adaptive symbols over a few
+    reused CDFs of each default-context field (counters saturate), L(n) literals of
+    1..25 bits, and gathered partition booleans; one long literal-heavy tile spans
+    several carry-resolution windows of k_av1_pack."""
+    rng = np.random.default_rng(seed)
+    fields = _fields(L)
+    part = [f for f in fields if f[1] == 10][0]          # partition_w16
+    streams = []
+    for t in range(tiles):
+        n = 12000 if t == 0 else int(rng.integers(0, 3000))
+        picks = [fields[int(rng.integers(len(fields)))] for _ in range(6)]
+        ctxs = [(off + int(rng.integers(cnt)) * (ns + 1), ns) for off, ns, cnt in picks]
+        toks = []
+        for _ in range(n):
+            k = int(rng.choice([0, 0, 0, 0, 1, 2])) if t else int(rng.choice([0, 1, 1]))
+            if k == 0:
+                off, ns = ctxs[int(rng.integers(len(ctxs)))]
+                v = int(min(ns - 1, rng.geometric(0.5) - 1))
+                toks.append(((ns - 1) << 26) | (v << 22) | off)
+            elif k == 1:
+                nb = int(rng.integers(1, 26))
+                toks.append((1 << 30) | ((nb - 1) << 25) | int(rng.integers(1 << nb)))
+            else:
+                off = part[0] + int(rng.integers(part[2])) * (part[1] + 1)
+                toks.append((2 << 30) | (int(rng.integers(2)) << 29) | (int(rng.integers(2)) << 28) | off)
+        streams.append(toks)
+    return streams
+
+
+def test_token_replay_cpu():
+    """sk_av1_ec_tokens_cpu (the GPU coder's reference) is deterministic and sized sanely."""
+    L = _lib()
+    L.sk_av1_ec_tokens_cpu.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_uint8), ctypes.c_int]
+    L.sk_av1_ec_tokens_cpu.restype = ctypes.c_int
+    toks = _token_streams(L, 3, 2)[1]
+    arr = (ctypes.c_uint32 * max(1, len(toks)))(*toks)
+    outs = []
+    for _ in range(2):
+        out = (ctypes.c_uint8 * (8 * len(toks) + 64))()
+        n = L.sk_av1_ec_tokens_cpu(arr, len(toks), 100, out, len(out))
+        assert n > 0
+        outs.append(bytes(out[:n]))
+    assert outs[0] == outs[1]
+
+
 @pytest.mark.gpu
 def test_gpu_tiles_match_host_encoder():
-    """k_av1_ec_tiles (csrc/kernels/av1_kernels.hip): 24 independent tiles coded on
-    the GPU, each byte-identical to the host encoder and decodable by the spec model."""
+    """k_av1_ec + k_av1_pack (csrc/kernels/av1_kernels.hip) on synthetic token streams:
+    every tile byte-identical to the host replay through SymbolCoder (av1_ec.h)."""
     from selkies_gstreamer_amd.ops.native import hip_device_count
     if hip_device_count() < 1:
         pytest.skip("no HIP device")
     L = _lib()
     P = ctypes.POINTER
-    L.sk_av1_ec_encode_tiles_hip.argtypes = [P(ctypes.c_uint32), P(ctypes.c_int32), P(ctypes.c_int32), ctypes.c_int,
-                                             P(ctypes.c_uint16), P(ctypes.c_int32), ctypes.c_int, ctypes.c_int,
-                                             P(ctypes.c_uint8), P(ctypes.c_int32)]
-    L.sk_av1_ec_encode_tiles_hip.restype = ctypes.c_int
-    rng = np.random.default_rng(11)
-    nctx = 12
-    nsym = [int(rng.integers(2, 17)) for _ in range(nctx)]
-    cdfs = [_random_cdf(rng, n, 0.5) for n in nsym]
-    tiles, words, offs, ns = 24, [], [], []
-    for t in range(tiles):
-        offs.append(len(words))
-        n = int(rng.integers(0, 2500))
-        ns.append(n)
-        for _ in range(n):
-            k = int(rng.choice([0, 0, 0, 1, 2]))
-            if k == 0:
-                c = int(rng.integers(nctx))
-                words.append((c << 20) | int(rng.integers(nsym[c])))
-            elif k == 1:
-                words.append((1 << 30) | int(rng.integers(2)))
-            else:
-                b = int(rng.integers(1, 17))
-                words.append((2 << 30) | (b << 20) | int(rng.integers(1 << b)))
-    flat = np.zeros(nctx * 17, np.uint16)
-    for c, cdf in enumerate(cdfs):
-        flat[c * 17:c * 17 + len(cdf)] = cdf
-    out = np.zeros(2 * len(words) + 8 * tiles, np.uint8)
-    sizes = np.zeros(tiles, np.int32)
-    a32 = lambda x, t=ctypes.c_int32: (t * len(x))(*x)   # noqa: E731
-    rc = L.sk_av1_ec_encode_tiles_hip(a32(words, ctypes.c_uint32), a32(offs), a32(ns), tiles,
-                                      flat.ctypes.data_as(P(ctypes.c_uint16)), a32(nsym), nctx, 1,
-                                      out.ctypes.data_as(P(ctypes.c_uint8)), sizes.ctypes.data_as(P(ctypes.c_int32)))
-    assert rc == 0
-    for t in range(tiles):
-        w = words[offs[t]:offs[t] + ns[t]]
-        kind = [x >> 30 for x in w]
-        ctx = [(x >> 20) & 1023 for x in w]
-        sym = [x & 0xfffff for x in w]
-        host = _encode(kind, ctx, sym, [list(c) for c in cdfs], nsym, True)
-        base = 2 * offs[t] + 8 * t
-        gpu = bytes(out[base:base + sizes[t]])
-        assert gpu == host, t
+    L.sk_av1_ec_tokens_cpu.argtypes = [P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int, P(ctypes.c_uint8), ctypes.c_int]
+    L.sk_av1_ec_tokens_cpu.restype = ctypes.c_int
+    L.sk_av1_ec_tokens_hip.argtypes = [P(ctypes.c_uint32), P(ctypes.c_int32), P(ctypes.c_int32), ctypes.c_int,
+                                       ctypes.c_int, P(ctypes.c_uint8), ctypes.c_int, P(ctypes.c_int32)]
+    L.sk_av1_ec_tokens_hip.restype = ctypes.c_int
+    for qidx in (10, 100, 200):
+        streams = _token_streams(L, qidx, 24)
+        flat, offs, ns = [], [], []
+        for s in streams:
+            offs.append(len(flat))
+            ns.append(len(s))
+            flat += s
+        cap = 8 * len(flat) + 4096
+        out = np.zeros(cap, np.uint8)
+        sizes = np.zeros(len(streams), np.int32)
+        a32 = lambda x, t=ctypes.c_int32: (t * max(1, len(x)))(*x)   # noqa: E731
+        rc = L.sk_av1_ec_tokens_hip(a32(flat, ctypes.c_uint32), a32(offs), a32(ns), len(streams), qidx,
+                                    out.ctypes.data_as(P(ctypes.c_uint8)), cap, sizes.ctypes.data_as(P(ctypes.c_int32)))
+        assert rc == 0
+        pos = 0
+        for t, s in enumerate(streams):
+            ref = (ctypes.c_uint8 * (8 * len(s) + 64))()
+            m = L.sk_av1_ec_tokens_cpu(a32(s, ctypes.c_uint32), len(s), qidx, ref, len(ref))
+            assert sizes[t] == m, (qidx, t)
+            assert bytes(out[pos:pos + m]) == bytes(ref[:m]), (qidx, t)
+            pos += m

@@ -6,7 +6,7 @@ TAG=${1:-av1}
 MODE=${2:-all}
 mkdir -p gpurun_out/$TAG
 if [ "$MODE" != "bench" ]; then
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_av1_gpu.py \
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_av1_entropy.py tests/test_av1_gpu.py \
     > gpurun_out/$TAG/pytest.log 2>&1 || { tail -30 gpurun_out/$TAG/pytest.log; exit 1; }
 tail -3 gpurun_out/$TAG/pytest.log
 fi
