@@ -26,13 +26,15 @@ from selkies_gstreamer_amd.server.settings import Settings, build_specs
 # ----------------------------------------------------------------------------- settings
 def test_settings_count_and_defaults():
     specs = build_specs()
-    assert len(specs) == 60   # the reference's 56 + H.264 quality tools (AQ, quarter-pel, Intra4x4) + ui_dashboard
+    # the reference's 56 + H.264 quality tools (AQ, quarter-pel, Intra4x4) + ui_dashboard + h264_bitrate (K10 CBR)
+    assert len(specs) == 61
     s = Settings([], env={})
     assert s.h264_aq_strength == 0 and s.h264_subpel == (True, False) and s.h264_intra4x4 == (False, False)
     assert s.encoder == "x264enc" and s.framerate == (8, 120) and s.port == 8082
     assert s.audio_enabled == (True, False)
     assert s.file_transfers == ["upload", "download"]
     assert s.initial("framerate") == 60 and s.initial("h264_crf") == 25 and s.initial("jpeg_quality") == 40
+    assert s.initial("h264_bitrate") == 0      # CRF unless a bitrate is set
 
 
 def test_settings_precedence_cli_env_legacy():
