@@ -47,7 +47,13 @@ def parse():
     p.add_argument("--content", default="motion", choices=["motion", "desktop", "noise"])
     p.add_argument("--mode", default="striped", choices=["striped", "fullframe"])
     p.add_argument("--stripe-height", type=int, default=64)
-    p.add_argument("--qp", type=int, default=25)
+    p.add_argument("--qp", type=int, default=25, help="QP (cqp) or CRF value (crf)")
+    p.add_argument("--rc", default="crf", choices=["cqp", "crf", "cbr"],
+                   help="K10 rate control: crf = the reference's CRF semantics (h264_crf, settings.py:48)")
+    p.add_argument("--kbps", type=int, default=8000, help="CBR bitrate (--rc cbr)")
+    p.add_argument("--av1-kbps", type=int, default=40000,
+                   help="AV1 4K120 extra: CBR bitrate (the reference's AV1 encoders run bitrate-controlled in "
+                        "the WebRTC mode; 40 Mbit/s = AV1 level 5.1 Main tier maximum); 0 = --rc/--qp")
     p.add_argument("--pool", type=int, default=16, help="pre-rendered frames per session pool")
     p.add_argument("--backend", default="hip", choices=["hip", "cpu"])
     p.add_argument("--encoder", default="h264", choices=["h264", "jpeg", "hevc", "av1"],
@@ -125,7 +131,9 @@ def run_capture_path(args, pool, local_rank):
                                         h264_fullframe=int(args.mode == "fullframe"), device=local_rank,
                                         use_cpu=int(args.backend == "cpu"), source=pixelflux.SOURCE_POOL,
                                         step_mode=1, pool_frames=args.pool, pool_stride=W * 4,
-                                        pool_phase=3 * i)
+                                        pool_phase=3 * i,
+                                        h264_rc_mode={"cqp": 0, "crf": 1, "cbr": 2}[args.rc],
+                                        h264_bitrate_kbps=args.kbps if args.rc == "cbr" else 0)
         cs.pool = pool.array.ctypes.data
         c = pixelflux.ScreenCapture()
         c.start_frame_capture(cs, null_cb)
@@ -199,6 +207,8 @@ def run_extra(args, W, H, encoder, fps, local_rank, steps):
             src.frame(i, out=pool.array[i])
         a = types.SimpleNamespace(**vars(args))
         a.sessions, a.encoder, a.pool, a.mode = 1, encoder, 8, "fullframe"
+        if encoder == "av1" and args.av1_kbps > 0:
+            a.rc, a.kbps = "cbr", args.av1_kbps
         caps, run_caps = run_capture_path(a, pool, local_rank)
         run_caps(10)
         caps[0].latencies(reset=True)
@@ -217,9 +227,14 @@ def run_extra(args, W, H, encoder, fps, local_rank, steps):
                 "p99_encode_latency_ms": round(p99, 3), "frame_interval_ms": round(budget, 3),
                 "realtime": bool(steps / el >= fps and p99 < budget),
                 "kib_per_frame": round((st["bytes"] - b0) / steps / 1024, 1),
-                "frames_in_flight": st.get("frames_in_flight"), "qp": args.qp}
+                "frames_in_flight": st.get("frames_in_flight"), "rate_control": rc_desc(a)}
     except Exception as ex:   # noqa: BLE001 - reported, never fatal for the headline
         return {"resolution": f"{W}x{H}", "encoder": encoder, "error": f"{type(ex).__name__}: {ex}"}
+
+
+def rc_desc(args) -> str:
+    """Rate control of a run, as quoted in the JSON config."""
+    return f"CBR {args.kbps} kbit/s" if args.rc == "cbr" else f"{args.rc.upper()} {args.qp}"
 
 
 def run_dist_bands(args, torch, dist, rank, world, local_rank):
@@ -366,7 +381,8 @@ def main():
         else:
             encs = [H264Encoder(W, H, stripe_height=args.stripe_height, fullframe=args.mode == "fullframe",
                                 qp=args.qp, use_paint_over=False, device=local_rank, backend=args.backend,
-                                deblock=bool(args.deblock), me_full=bool(args.me_full), num_refs=args.num_refs)
+                                deblock=bool(args.deblock), me_full=bool(args.me_full), num_refs=args.num_refs,
+                                rate_control=args.rc, bitrate_kbps=args.kbps if args.rc == "cbr" else 0)
                     for _ in range(S)]
 
     lat = [[] for _ in range(S)]
@@ -549,11 +565,11 @@ def main():
             "kib_per_frame": round(total_bytes / frames / 1024, 1),
             "gathered_bytes_rank0": gather_bytes,
             "config": {
-                "model": (f"H.264 Constrained Baseline CAVLC, {args.mode} stripes {args.stripe_height}px, QP {args.qp}"
+                "model": (f"H.264 Constrained Baseline CAVLC, {args.mode} stripes {args.stripe_height}px, {rc_desc(args)}"
                           if args.encoder == "h264" else
-                          (f"HEVC Main CABAC, CTB 16, WPP, slices of {args.stripe_height}px, QP {args.qp}"
+                          (f"HEVC Main CABAC, CTB 16, WPP, slices of {args.stripe_height}px, {rc_desc(args)}"
                            if args.encoder == "hevc" else
-                           (f"AV1 Main 8-bit 4:2:0, 64x64 SB, tiles, QP {args.qp}" if args.encoder == "av1" else
+                           (f"AV1 Main 8-bit 4:2:0, 64x64 SB, tiles, {rc_desc(args)}" if args.encoder == "av1" else
                             f"baseline JPEG 4:2:0 stripes {args.stripe_height}px, quality {args.jpeg_quality}"))),
                 "global_batch": S * n_gpus,
                 "seq_len": 1,

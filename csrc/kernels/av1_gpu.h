@@ -24,6 +24,7 @@ struct Av1Args {
     uint32_t* tok;            // [units][kTokCap]
     int* tok_n;               // [units]
     uint32_t* tokc;           // [tiles][tile_tok_cap]: each tile's tokens in coding order
+    uint32_t* pw;             // [tiles][tile_tok_cap]: interval word of each symbol token (k_av1_cdf)
     int tile_tok_cap;
     int* tok_off;             // [units] offset of the unit's tokens in its tile's stream
     int* tile_ntok;           // [tiles]

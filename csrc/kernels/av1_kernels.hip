@@ -10,8 +10,9 @@
 //   k_av1_modes        inter frames: reference-MV stack -> NEAREST / NEAR / GLOBAL / NEWMV
 //   k_av1_tokens       block syntax -> token lists, one lane per 16x16 unit
 //   k_av1_tok_scan/copy  per-tile token streams in coding order
-//   k_av1_ec           one wave per tile: arithmetic coding with the tile's CDFs in LDS
-//                      (scalar coder state, lane-parallel CDF adaptation)
+//   k_av1_cdf          CDF adaptation, 16 context partitions per tile in parallel ->
+//                      per-symbol interval words
+//   k_av1_ec           one wave per tile: the arithmetic coder (scalar state)
 //   k_av1_pack         carry resolution (segmented, parallel), tile bytes -> host-mapped output
 //   k_av1_finish       padding rows of the reconstruction, slice actions for k_commit
 // Transforms: forward DCT as LDS matrix products (lanes = output coefficients),
@@ -589,38 +590,215 @@ __global__ __launch_bounds__(256) void k_av1_tok_copy(Av1Args A) {
     for (int i = l; i < n; i += 64) d[i] = s[i];
 }
 
-// One wave per tile codes the tile's token stream. Every lane runs the (uniform)
-// coder state, so it lives in scalar registers; the CDF of a symbol is read and
-// adapted lane-parallel (lane i: cdf[i], lane N: the counter), and the next token's
-// CDF read is issued before the current symbol's interval arithmetic so its LDS
-// latency is hidden. Tokens stream through a 2 x 64 LDS ring (the batch after next is
-// in flight in a register) and are read two ahead; settled chunks go to an LDS ring
-// flushed 1024 at a time. Bit-exact with SymbolCoder (codec/av1_ec.h).
+// Entropy coding in two phases.
+//
+// k_av1_cdf (phase A): the CDF adaptation, parallel over contexts. Each tile's CDF
+// slots are split over kEcParts waves by a hash of the slot offset; every wave scans
+// the tile's whole token stream in 64-token batches, takes the symbols of its own
+// contexts in order (ballot + find-first-set) and, with the tile's CDFs in its LDS,
+// adapts them lane-parallel (lane i: cdf[i], lane N: the counter). Per symbol it
+// writes the interval word the coder needs:
+//   [9:0] (32768 - cdf[s]) >> 6 (0 for the last symbol)   [19:10] (32768 - cdf[s-1]) >> 6
+//   [24:20] N - s   [25] s > 0
+// k_av1_ec (phase B): one wave per tile runs the arithmetic coder over the interval
+// words and literal bits with its state in scalar registers (the only serial work
+// left), tokens / words in double-buffered 64-lane vector batches, settled chunks
+// through an LDS ring flushed 1024 at a time. Bit-exact with SymbolCoder (av1_ec.h).
 constexpr int kObRing = 4096;
 constexpr int kObFlush = 1024;
+constexpr int kEcParts = 16;
 
 __device__ __forceinline__ uint32_t sgpr(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v, i); }
+__device__ __forceinline__ int ec_owner(uint32_t off) { return (int)((off * 0x9E3779B1u) >> 28) & (kEcParts - 1); }
+__device__ __forceinline__ uint32_t ec_word(uint32_t clo, uint32_t chi, int n, int s) {
+    const uint32_t fh = s < n - 1 ? (32768u - chi) >> kProbShift : 0u;
+    const uint32_t fl = s > 0 ? (32768u - clo) >> kProbShift : 0u;
+    return fh | fl << 10 | (uint32_t)(n - s) << 20 | (s > 0 ? 1u << 25 : 0u);
+}
 
-__global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
+// Token / word batches: kSub sub-batches of 64 (one VGPR each per lane), two big
+// batches in flight. Loads are unconditional (clamped index) so the wait before a big
+// batch is exact and never covers the batch issued after it.
+constexpr int kSub = 8, kBig = 64 * kSub;
+
+__device__ __forceinline__ void use_regs(const uint32_t* v) {
+#pragma unroll
+    for (int j = 0; j < kSub; j++) asm volatile("" ::"v"(v[j]));
+}
+
+__global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     __shared__ CdfContext cx;
-    __shared__ uint16_t ob[kObRing];
-    __shared__ uint32_t tq[128];
-    const int t = blockIdx.x, L = threadIdx.x;
-    const int q = coef_qctx(A.frame[1]);
+    __shared__ uint32_t wst[64];   // interval words of the sub-batch being adapted
+    const int t = blockIdx.x / kEcParts, part = blockIdx.x % kEcParts, L = threadIdx.x;
     {
-        const uint16_t* src = (const uint16_t*)&AV1_DEFAULT_CDF[q];
+        const uint16_t* src = (const uint16_t*)&AV1_DEFAULT_CDF[coef_qctx(A.frame[1])];
         uint16_t* d16 = (uint16_t*)&cx;
         for (int i = L; i < (int)(sizeof(CdfContext) / 2); i += 64) d16[i] = src[i];
     }
+    __syncthreads();
     uint16_t* cdfs = (uint16_t*)&cx;
-    const int ntok = A.tile_ntok[t];
+    const int ntok = A.tile_ntok[t], last = A.tile_tok_cap - 1;
+    const uint32_t* tk = A.tokc + (size_t)t * A.tile_tok_cap;
+    uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
+    // words of tokens this wave does not own go to its junk slots past the streams
+    uint32_t* junk = A.pw + (size_t)A.geo.tile_cols * A.geo.tile_rows * A.tile_tok_cap + (size_t)blockIdx.x * 64;
+    // One symbol with the whole wave (gathered booleans, alphabets of 16).
+    auto one = [&](uint32_t tt) -> uint32_t {
+        const int off = (int)(tt & 0x3fffff);
+        if ((tt >> 30) == 0) {
+            const int n = (int)((tt >> 26) & 15) + 1, s = (int)((tt >> 22) & 15);
+            const uint32_t cv = L <= n ? (uint32_t)cdfs[off + L] : 0u;
+            const uint32_t chi = sgpr(rdlane(cv, s)), clo = sgpr(rdlane(cv, s > 0 ? s - 1 : 0));
+            const int count = (int)sgpr(rdlane(cv, n));
+            const int rate = 3 + (count > 15) + (count > 31) + (n > 3 ? 2 : (n > 1 ? 1 : 0));
+            if (L < n - 1) {
+                const int c = (int)cv;
+                cdfs[off + L] = (uint16_t)(L >= s ? c + ((32768 - c) >> rate) : c - (c >> rate));
+            } else if (L == n && count < 32) {
+                cdfs[off + L] = (uint16_t)(count + 1);
+            }
+            return ec_word(clo, chi, n, s);
+        }
+        uint16_t c2[3];   // gathered split_or_horz / split_or_vert boolean (read-only CDF)
+        gather_partition_cdf(cdfs + off, ((tt >> 29) & 1) == 0, c2);
+        const uint32_t c0 = sgpr(c2[0]);
+        const int v = (int)((tt >> 28) & 1);
+        return ec_word(c0, v ? 32768u : c0, 2, v);
+    };
+    // Up to four symbols of distinct CDFs (consecutive in this wave's order, so their
+    // relative order does not matter) adapt together, 16 lanes each: lane j of group k
+    // holds cdf[j] of symbol k (alphabets <= 15, the counter in lane N). A run of one
+    // context (the zero-level context of 16x16 luma blocks can be half of a tile's
+    // symbols) stays in registers: lanes 0..15 of `cache` hold that CDF, written back
+    // to LDS only when another group needs LDS.
+    const int grp = L >> 4, jl = L & 15;
+    int cache_off = -1, cache_n = 0;
+    uint32_t cache = 0;
+    auto adapt = [&](uint32_t cv, int n, int s, int lane, int count, uint32_t& nv, bool& wr) {
+        const int rate = 3 + (count > 15) + (count > 31) + (n > 3 ? 2 : (n > 1 ? 1 : 0));
+        const int c = (int)cv;
+        nv = cv;
+        wr = false;
+        if (lane < n - 1) {
+            nv = (uint32_t)(lane >= s ? c + ((32768 - c) >> rate) : c - (c >> rate));
+            wr = true;
+        } else if (lane == n && count < 32) {
+            nv = (uint32_t)(count + 1);
+            wr = true;
+        }
+    };
+    auto sub = [&](uint32_t tv, int b) -> uint32_t {   // 64 tokens from b: this wave's words
+        const bool mine = b + L < ntok && (tv >> 30) != 1 && ec_owner(tv & 0x3fffff) == part;
+        uint64_t m = __ballot(mine);
+        while (m) {
+            uint32_t tg[4] = {0u, 0u, 0u, 0u};
+            int ig[4] = {0, 0, 0, 0};
+            int g = 0;
+            bool stop = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (stop || !m) continue;
+                const int i = __builtin_ctzll(m);
+                const uint32_t tt = sgpr(rdlane(tv, i));
+                const bool wide = (tt >> 30) != 0 || ((tt >> 26) & 15) >= 15;
+                bool clash = wide;
+#pragma unroll
+                for (int q = 0; q < k; q++) clash |= ((tg[q] ^ tt) & 0x3fffff) == 0;
+                if (clash) {
+                    stop = true;
+                    continue;
+                }
+                tg[k] = tt;
+                ig[k] = i;
+                g = k + 1;
+                m &= m - 1;
+            }
+            if (g == 1 && (int)(tg[0] & 0x3fffff) == cache_off) {   // cached run: registers only
+                const int n = (int)((tg[0] >> 26) & 15) + 1, s = (int)((tg[0] >> 22) & 15);
+                const uint32_t chi = sgpr(rdlane(cache, s)), clo = sgpr(rdlane(cache, s > 0 ? s - 1 : 0));
+                uint32_t nv;
+                bool wr;
+                adapt(cache, n, s, L, (int)sgpr(rdlane(cache, n)), nv, wr);
+                cache = nv;
+                const uint32_t w = ec_word(clo, chi, n, s);
+                if (L == 0) wst[ig[0]] = w;
+                continue;
+            }
+            if (cache_off >= 0) {   // write the cached CDF back before LDS is read again
+                if (L <= cache_n) cdfs[cache_off + L] = (uint16_t)cache;
+                cache_off = -1;
+            }
+            if (g == 0) {   // the next symbol needs the whole wave
+                const int i = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t w = one(sgpr(rdlane(tv, i)));
+                if (L == 0) wst[i] = w;
+                continue;
+            }
+            const uint32_t mt = grp == 0 ? tg[0] : (grp == 1 ? tg[1] : (grp == 2 ? tg[2] : tg[3]));
+            const bool act = grp < g;
+            const int n = (int)((mt >> 26) & 15) + 1, s = (int)((mt >> 22) & 15), off = (int)(mt & 0x3fffff);
+            const uint32_t cv = act && jl <= n ? (uint32_t)cdfs[off + jl] : 0u;
+            const int base = grp << 4;
+            const uint32_t chi = (uint32_t)__shfl((int)cv, base + s);
+            const uint32_t clo = (uint32_t)__shfl((int)cv, base + (s > 0 ? s - 1 : 0));
+            uint32_t nv;
+            bool wr;
+            adapt(cv, n, s, jl, __shfl((int)cv, base + n), nv, wr);
+            if (g == 1) {   // a single context: keep it in registers (lanes 0..15)
+                cache = nv;
+                cache_off = off;
+                cache_n = n;
+            } else if (act && wr) {
+                cdfs[off + jl] = (uint16_t)nv;
+            }
+            const uint32_t word = ec_word(clo, chi, n, s);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (k < g) {
+                    const uint32_t wk = sgpr(rdlane(word, 16 * k));
+                    if (L == 0) wst[ig[k]] = wk;
+                }
+        }
+        wsync();
+        const uint32_t out = wst[L];
+        uint32_t* d = mine ? pw + b + L : junk + L;   // unconditional store
+        *d = out;
+        return 0;
+    };
+    uint32_t X[kSub], Y[kSub];
+    auto load = [&](uint32_t* v, int b) {
+#pragma unroll
+        for (int j = 0; j < kSub; j++) v[j] = tk[sk_min(b + 64 * j + L, last)];
+    };
+    auto big = [&](uint32_t* v, int b) {
+#pragma unroll
+        for (int j = 0; j < kSub; j++)
+            if (b + 64 * j < ntok) sub(v[j], b + 64 * j);
+    };
+    load(X, 0);
+    load(Y, kBig);
+    for (int b = 0; b < ntok; b += 2 * kBig) {
+        use_regs(X);
+        big(X, b);
+        load(X, b + 2 * kBig);
+        if (b + kBig < ntok) {
+            use_regs(Y);
+            big(Y, b + kBig);
+        }
+        load(Y, b + 3 * kBig);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
+    __shared__ uint16_t ob[kObRing];
+    const int t = blockIdx.x, L = threadIdx.x;
+    const int ntok = A.tile_ntok[t], last = A.tile_tok_cap - 1;
     const int cap = A.tile_cap;
     const uint32_t* tk = A.tokc + (size_t)t * A.tile_tok_cap;
+    const uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
     uint16_t* dst = A.chunks + (size_t)t * cap;
-    tq[L] = L < ntok ? tk[L] : 0u;
-    tq[64 + L] = 64 + L < ntok ? tk[64 + L] : 0u;
-    uint32_t R = 128 + L < ntok ? tk[128 + L] : 0u;   // batch 2
-    __syncthreads();
     uint64_t low = 0;
     uint32_t rng = 0x8000;
     int cnt = -9, nb = 0, fl = 0;
@@ -649,14 +827,6 @@ __global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
         rng = r2 << d;
         cnt = s;
     };
-    // symbol s of n with cdf[s - 1] = clo (s > 0) and cdf[s] = chi
-    auto enc = [&](uint32_t clo, uint32_t chi, int n, int s) {
-        const uint32_t r = rng;
-        const uint32_t v = (((r >> 8) * ((32768u - chi) >> kProbShift)) >> (7 - kProbShift)) + kMinProb * (n - s - 1);
-        const uint32_t u = s > 0 ? (((r >> 8) * ((32768u - clo) >> kProbShift)) >> (7 - kProbShift)) + kMinProb * (n - s) : r;
-        low += r - u;
-        norm(u - v);
-    };
     auto flush = [&](int upto) {   // ring [fl, upto) -> dst (upto - fl <= kObFlush)
         wsync();
 #pragma unroll 4
@@ -667,74 +837,85 @@ __global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
         fl = upto;
         wsync();
     };
-    auto sym_read = [&](uint32_t tt) -> uint32_t {   // lane i <= N: cdf[i]
-        const int n = (int)((tt >> 26) & 15) + 1;
-        return L <= n ? (uint32_t)cdfs[(tt & 0x3fffff) + L] : 0u;
+    auto emit = [&](int d, int s) {   // norm() for s = cnt + d >= 0 (a byte or two settled)
+        int c = cnt + 16;
+        uint64_t m = (1ull << c) - 1;
+        if (s >= 8) {
+            put((uint32_t)(low >> c));
+            low &= m;
+            c -= 8;
+            m >>= 8;
+        }
+        put((uint32_t)(low >> c));
+        cnt = c + d - 24;
+        low &= m;
     };
-
-    uint32_t tcur = sgpr(tq[0]);
-    uint32_t tn1 = sgpr(tq[1]);   // token k + 1
-    uint32_t vn2 = tq[2];         // token k + 2 (LDS read in flight)
-    uint32_t cv = (ntok > 0 && (tcur >> 30) == 0) ? sym_read(tcur) : 0u;
-    for (int k = 0; k < ntok; k++) {
-        // the coder state is wave-uniform: keep it in scalar registers
-        rng = sgpr(rng);
-        cnt = (int)sgpr((uint32_t)cnt);
-        nb = (int)sgpr((uint32_t)nb);
-        fl = (int)sgpr((uint32_t)fl);
-        low = ((uint64_t)sgpr((uint32_t)(low >> 32)) << 32) | sgpr((uint32_t)low);
-        const uint32_t kind = tcur >> 30;
-        uint32_t clo = 0, chi = 0;
-        int n = 0, s = 0;
-        if (kind == 0) {   // adapt the symbol's CDF (lane-parallel update_cdf)
-            n = (int)((tcur >> 26) & 15) + 1;
-            s = (int)((tcur >> 22) & 15);
-            chi = (uint32_t)__builtin_amdgcn_readlane((int)cv, s);
-            clo = (uint32_t)__builtin_amdgcn_readlane((int)cv, s > 0 ? s - 1 : 0);
-            const int count = __builtin_amdgcn_readlane((int)cv, n);
-            const int rate = 3 + (count > 15) + (count > 31) + (n > 3 ? 2 : (n > 1 ? 1 : 0));
-            const int off = (int)(tcur & 0x3fffff);
-            if (L < n - 1) {
-                const int c = (int)cv;
-                cdfs[off + L] = (uint16_t)(L >= s ? c + ((32768 - c) >> rate) : c - (c >> rate));
-            } else if (L == n && count < 32) {
-                cdfs[off + L] = (uint16_t)(count + 1);
-            }
-        }
-        const int k1 = k + 1;
-        if ((k1 & 63) == 0) {   // entering batch j = k1 / 64: batch j + 1 -> the freed slot
-            tq[(((k1 >> 6) + 1) & 1) * 64 + L] = R;
-            if (nb - fl >= kObFlush) flush(fl + kObFlush);
-            const int nx = k1 + 128 + L;
-            R = nx < ntok ? tk[nx] : 0u;
-        }
-        // token k + 1: its CDF read; token k + 3: its LDS read
-        const uint32_t tnext = tn1;
-        tn1 = sgpr(vn2);
-        vn2 = tq[(k + 3) & 127];
-        if (k1 < ntok && (tnext >> 30) == 0) cv = sym_read(tnext);
-        // interval arithmetic of the current token
-        if (kind == 0) {
-            enc(sgpr(clo), sgpr(chi), (int)sgpr((uint32_t)n), (int)sgpr((uint32_t)s));
-        } else if (kind == 1) {
-            const int nbits = (int)((tcur >> 25) & 31) + 1;
-            for (int i = nbits - 1; i >= 0; i--) {
-                const uint32_t r = rng, split = ((r >> 8) << 7) + kMinProb;
-                if ((tcur >> i) & 1) {
-                    low += r - split;
-                    norm(split);
-                } else {
-                    norm(r - split);
+    auto code = [&](uint32_t tv, uint32_t wv, int b) {
+        const int m = sk_min(64, ntok - b);
+#pragma unroll 2
+        for (int i = 0; i < m; i++) {
+            // the coder state is wave-uniform: keep it in scalar registers
+            rng = sgpr(rng);
+            cnt = (int)sgpr((uint32_t)cnt);
+            nb = (int)sgpr((uint32_t)nb);
+            low = ((uint64_t)sgpr((uint32_t)(low >> 32)) << 32) | sgpr((uint32_t)low);
+            const uint32_t tt = sgpr(rdlane(tv, i));
+            const uint32_t w = sgpr(rdlane(wv, i));
+            if (__builtin_expect((tt >> 30) == 1, 0)) {   // L(n) literal: equiprobable bits
+                const int nbits = (int)((tt >> 25) & 31) + 1;
+                for (int k = nbits - 1; k >= 0; k--) {
+                    const uint32_t rr = rng, split = ((rr >> 8) << 7) + kMinProb;
+                    if ((tt >> k) & 1) {
+                        low += rr - split;
+                        norm(split);
+                    } else {
+                        norm(rr - split);
+                    }
                 }
+                continue;
             }
-        } else {
-            uint16_t c2[3];
-            gather_partition_cdf(cdfs + (tcur & 0x3fffff), ((tcur >> 29) & 1) == 0, c2);
-            const uint32_t c0 = sgpr(c2[0]);
-            const int v = (int)((tcur >> 28) & 1);
-            enc(v ? c0 : 0u, v ? 32768u : c0, 2, v);
+            // symbol: interval from the k_av1_cdf word (straight-line, one rare branch)
+            const uint32_t r = rng, r8 = r >> 8, ns4 = ((w >> 20) & 31) * kMinProb;
+            const uint32_t v = ((r8 * (w & 1023)) >> (7 - kProbShift)) + ns4 - kMinProb;
+            const uint32_t uu = ((r8 * ((w >> 10) & 1023)) >> (7 - kProbShift)) + ns4;
+            const uint32_t u = (w >> 25) & 1 ? uu : r;
+            low += r - u;
+            const uint32_t r2 = u - v;
+            const int d = __builtin_clz(r2) - 16;
+            const int sh = cnt + d;
+            if (__builtin_expect(sh >= 0, 0)) emit(d, sh);
+            else cnt = sh;
+            low <<= d;
+            rng = r2 << d;
         }
-        tcur = tnext;
+    };
+    uint32_t TX[kSub], WX[kSub], TY[kSub], WY[kSub];
+    auto load = [&](uint32_t* tv, uint32_t* wv, int b) {
+#pragma unroll
+        for (int j = 0; j < kSub; j++) {
+            const int i = sk_min(b + 64 * j + L, last);
+            tv[j] = tk[i];
+            wv[j] = pw[i];
+        }
+    };
+    auto big = [&](uint32_t* tv, uint32_t* wv, int b) {
+        use_regs(tv);
+        use_regs(wv);
+#pragma unroll
+        for (int j = 0; j < kSub; j++) {
+            if (b + 64 * j < ntok) code(tv[j], wv[j], b + 64 * j);
+            nb = (int)sgpr((uint32_t)nb);
+            fl = (int)sgpr((uint32_t)fl);
+            if (nb - fl >= kObFlush) flush(fl + kObFlush);   // <= 64 x 4 chunks per sub-batch
+        }
+    };
+    load(TX, WX, 0);
+    load(TY, WY, kBig);
+    for (int b = 0; b < ntok; b += 2 * kBig) {
+        big(TX, WX, b);
+        load(TX, WX, b + 2 * kBig);
+        if (b + kBig < ntok) big(TY, WY, b + kBig);
+        load(TY, WY, b + 3 * kBig);
     }
     {   // SymbolCoder::finish
         int c = cnt;
@@ -845,6 +1026,7 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_av1_tokens, dim3((n + 63) / 64), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_tok_scan, dim3(tiles), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_tok_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_cdf, dim3(tiles * kEcParts), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_finish, dim3((a.f.stride_y + 255) / 256), dim3(256), 0, s, a);
@@ -854,16 +1036,19 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
 }  // namespace av1
 }  // namespace sk
 
-// Test entry: k_av1_ec + k_av1_pack over caller token streams (tile t: tok[offs[t],
-// offs[t] + ns[t])) with the default CDFs of qidx; out receives tile t's bytes at
-// offs_out = prefix of sizes. Returns 0, or -1 on a HIP error.
+// Test entry: k_av1_cdf + k_av1_ec + k_av1_pack over caller token streams (tile t:
+// tok[offs[t], offs[t] + ns[t])) with the default CDFs of qidx; out receives tile t's
+// bytes at the prefix of sizes, words (optional) the interval words of k_av1_cdf.
+// Returns 0, or -1 on a HIP error.
 extern "C" int sk_av1_ec_tokens_hip(const uint32_t* tok, const int32_t* offs, const int32_t* ns, int tiles, int qidx,
-                                    uint8_t* out, int out_cap, int32_t* sizes) {
+                                    uint8_t* out, int out_cap, int32_t* sizes, uint32_t* words) {
     using namespace sk::av1::gpu;
     int maxn = 1;
     for (int t = 0; t < tiles; t++) maxn = ns[t] > maxn ? ns[t] : maxn;
     Av1Args a;
     memset(&a, 0, sizeof(a));
+    a.geo.tile_cols = tiles;
+    a.geo.tile_rows = 1;
     a.tile_tok_cap = maxn;
     a.tile_cap = 8 * maxn + 64;
     a.out_cap = out_cap;
@@ -873,6 +1058,7 @@ extern "C" int sk_av1_ec_tokens_hip(const uint32_t* tok, const int32_t* offs, co
     bool ok = true;
     auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
     chk(hipMalloc(&a.tokc, tc.size() * 4));
+    chk(hipMalloc(&a.pw, (tc.size() + (size_t)tiles * kEcParts * 64) * 4));
     chk(hipMalloc(&a.tile_ntok, tiles * 4));
     chk(hipMalloc(&a.frame, 8));
     chk(hipMalloc(&a.chunks, (size_t)tiles * a.tile_cap * 2));
@@ -883,14 +1069,21 @@ extern "C" int sk_av1_ec_tokens_hip(const uint32_t* tok, const int32_t* offs, co
         chk(hipMemcpy(a.tokc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice));
         chk(hipMemcpy(a.tile_ntok, ns, tiles * 4, hipMemcpyHostToDevice));
         chk(hipMemcpy(a.frame, frame, 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(k_av1_cdf, dim3(tiles * kEcParts), dim3(64), 0, 0, a);
         hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, 0, a);
         hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, 0, a);
         chk(hipGetLastError());
         chk(hipDeviceSynchronize());
         chk(hipMemcpy(sizes, a.out_size_host, tiles * 4, hipMemcpyDeviceToHost));
         chk(hipMemcpy(out, a.out_host, out_cap, hipMemcpyDeviceToHost));
+        if (words) {   // k_av1_cdf's interval words, tile t at offs[t]
+            std::vector<uint32_t> w(tc.size());
+            chk(hipMemcpy(w.data(), a.pw, w.size() * 4, hipMemcpyDeviceToHost));
+            for (int t = 0; t < tiles; t++) memcpy(words + offs[t], &w[(size_t)t * maxn], sizeof(uint32_t) * ns[t]);
+        }
     }
     (void)hipFree(a.tokc);
+    (void)hipFree(a.pw);
     (void)hipFree(a.tile_ntok);
     (void)hipFree(a.frame);
     (void)hipFree(a.chunks);

@@ -39,6 +39,9 @@ class EncoderBackend {
     // kernels: upload(n+1) ... finish(n) ... launch(n+1), or with two frames in
     // flight upload(n+1) launch(n+1) ... finish(n). Default: upload encodes.
     virtual int upload(const uint8_t* bgrx, int stride, uint16_t frame_id) { return submit(bgrx, stride, frame_id); }
+    // The next upload() waits (on the device) for the work queued so far on a foreign
+    // HIP stream of this device, e.g. the torch stream an RCCL scatter wrote the frame on.
+    virtual int wait_stream(void* stream) { (void)stream; return 0; }
     virtual int launch() { return 0; }
     // Session state transfer (h264::StateHeader layout). `on_device`: the buffer is
     // device memory of this encoder's GPU (HIP backend) instead of host memory.

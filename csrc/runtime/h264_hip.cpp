@@ -60,6 +60,7 @@ class HipBackend : public EncoderBackend {
         for (void* p : host_allocs_) hipHostFree(p);
         for (auto& e : ev_) hipEventDestroy(e);
         for (auto& e : ev_copy_) hipEventDestroy(e);
+        if (ev_ext_) hipEventDestroy(ev_ext_);
         for (auto* b : bgrx_dev_)
             if (b) hipFree(b);
         hipStreamDestroy(stream_);
@@ -135,6 +136,10 @@ class HipBackend : public EncoderBackend {
         // through the device's one shared copy stream instead).
         if (copy_stream_) cs = copy_stream_;
         else if (inflight() && upload_mode_ != 0) cs = upload_mode_ == 2 ? device_copy_stream(device_) : upload_stream();
+        if (ext_wait_) {   // wait_stream(): the source is written by another stream's queued work
+            HIPCHECK(hipStreamWaitEvent(cs, ev_ext_, 0));
+            ext_wait_ = false;
+        }
         // the last reader of bgrx_dev_[q] is the graph two frames back: finished
         HIPCHECK(hipEventRecord(ev_[3 * q], cs));
         // hipMemcpyDefault: the frame may be host memory (capture) or device memory (a band
@@ -144,6 +149,14 @@ class HipBackend : public EncoderBackend {
         staged_on_main_ = cs == stream_;
         staged_ = true;
         staged_frame_ = frame_id;
+        return 0;
+    }
+
+    int wait_stream(void* stream) override {
+        HIPCHECK(hipSetDevice(device_));
+        if (!ev_ext_) HIPCHECK(hipEventCreateWithFlags(&ev_ext_, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(ev_ext_, (hipStream_t)stream));
+        ext_wait_ = true;
         return 0;
     }
 
@@ -353,6 +366,8 @@ class HipBackend : public EncoderBackend {
         else if (s == "blk" && cfg_.codec == 2) { p = aargs_.blk; n = (int64_t)av1_geo_.c8 * av1_geo_.r8 * sizeof(av1::BlkInfo); }
         else if (s == "levels" && cfg_.codec == 2) { p = aargs_.lev; n = (int64_t)g_.num_mbs() * av1::gpu::kLevPerUnit * 2; }
         else if (s == "tok_n" && cfg_.codec == 2) { p = aargs_.tok_n; n = (int64_t)g_.num_mbs() * 4; }
+        else if (s == "tokc" && cfg_.codec == 2) { p = aargs_.tokc; n = (int64_t)av1_geo_.tile_cols * av1_geo_.tile_rows * aargs_.tile_tok_cap * 4; }
+        else if (s == "tile_ntok" && cfg_.codec == 2) { p = aargs_.tile_ntok; n = (int64_t)av1_geo_.tile_cols * av1_geo_.tile_rows * 4; }
         else if (s == "tile_size" && cfg_.codec == 2) { p = aargs_.tile_size; n = (int64_t)av1_geo_.tile_cols * av1_geo_.tile_rows * 4; }
         else if (s == "av1_geo" && cfg_.codec == 2) {
             if (dst && cap >= (int64_t)sizeof(av1_geo_)) memcpy(dst, &av1_geo_, sizeof(av1_geo_));
@@ -676,6 +691,8 @@ class HipBackend : public EncoderBackend {
         const int tile_units = (av1_geo_.tile_w_sb * 4) * (av1_geo_.tile_h_sb * 4);
         a.tile_tok_cap = tile_units * av1::gpu::kTokCap;
         a.tokc = dmalloc<uint32_t>((size_t)tiles * a.tile_tok_cap, false);
+        // + per-wave junk slots of k_av1_cdf (words of tokens a wave does not own)
+        a.pw = dmalloc<uint32_t>((size_t)tiles * a.tile_tok_cap + (size_t)tiles * 16 * 64, false);
         a.tok_off = dmalloc<int>(n);
         a.tile_ntok = dmalloc<int>(tiles);
         a.tile_cap = tile_units * 4096;
@@ -865,6 +882,8 @@ class HipBackend : public EncoderBackend {
     hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
     bool graph_guard_ = false;   // the captured H.264 graphs contain the K10 CBR guard
+    hipEvent_t ev_ext_ = nullptr;   // wait_stream(): foreign stream's work before the next upload
+    bool ext_wait_ = false;
     hipStream_t copy_stream_ = nullptr;   // shared per device (not owned)
     hipStream_t up_stream_ = nullptr;     // this session's upload stream (owned, lazily created)
     // 0: on the session stream (behind the frame in flight), 1: own upload stream,

@@ -397,6 +397,15 @@ int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame
     }
 }
 
+int sk_h264_wait_stream(void* enc, void* stream) {
+    try {
+        return static_cast<EncoderBackend*>(enc)->wait_stream(stream);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
+}
+
 int sk_h264_upload(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id) {
     try {
         return static_cast<EncoderBackend*>(enc)->upload(bgrx, stride, (uint16_t)frame_id);

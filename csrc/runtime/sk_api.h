@@ -66,6 +66,9 @@ int sk_h264_finish(void* enc);
 // submit = upload + launch. upload(n+1) may run while frame n encodes (its copy
 // overlaps n's kernels); call launch() for it after sk_h264_finish of frame n.
 int sk_h264_upload(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id);
+// The next sk_h264_upload waits on the device for the work queued on `stream` (a HIP
+// stream of the encoder's device), instead of a host synchronisation.
+int sk_h264_wait_stream(void* enc, void* stream);
 int sk_h264_launch(void* enc);
 // Session state snapshot (codec/h264_encoder.h StateHeader layout, identical for the
 // CPU and HIP backends): move a session between GPUs / processes without an IDR.

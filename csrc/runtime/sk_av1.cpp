@@ -34,23 +34,24 @@ int sk_av1_ec_encode(const int32_t* kind, const int32_t* ctx, const int32_t* sym
 }
 
 // Adaptive CDF arrays of the default context for token-stream tests: field i ->
-// (offset of its first CDF in u16 units, symbols N, number of CDFs). Returns the
-// number of fields when i is out of range.
-int sk_av1_cdf_field(int i, int32_t* off, int32_t* nsym, int32_t* count) {
+// (offset of its first CDF in u16 units, symbols N, number of CDFs, CDF stride in
+// u16). Returns the number of fields when i is out of range.
+int sk_av1_cdf_field(int i, int32_t* off, int32_t* nsym, int32_t* count, int32_t* stride) {
     using sk::av1::CdfContext;
     const CdfContext& c = sk::av1::AV1_DEFAULT_CDF[0];
-    struct F { const uint16_t* p; int n; size_t bytes; };
-#define SK_FIELD(f, n) F{(const uint16_t*)&c.f, n, sizeof(c.f)}
-    const F fs[] = {SK_FIELD(kf_y_mode, 13),   SK_FIELD(uv_mode_cfl_allowed, 14), SK_FIELD(partition_w16, 10),
-                    SK_FIELD(partition_w8, 4), SK_FIELD(eob_pt_16, 5),            SK_FIELD(eob_pt_1024, 11),
-                    SK_FIELD(coeff_base, 4),   SK_FIELD(coeff_br, 4),             SK_FIELD(coeff_base_eob, 3),
-                    SK_FIELD(txb_skip, 2),     SK_FIELD(skip, 2),                 SK_FIELD(mv_joint, 4)};
+    struct F { const uint16_t* p; int n, stride; size_t bytes; };
+#define SK_FIELD(f, n, st) F{(const uint16_t*)&c.f, n, st, sizeof(c.f)}
+    const F fs[] = {SK_FIELD(kf_y_mode, 13, 14),    SK_FIELD(uv_mode_cfl_allowed, 14, 15), SK_FIELD(partition_w16, 10, 11),
+                    SK_FIELD(partition_w8, 4, 11),  SK_FIELD(eob_pt_16, 5, 6),             SK_FIELD(eob_pt_1024, 11, 12),
+                    SK_FIELD(coeff_base, 4, 5),     SK_FIELD(coeff_br, 4, 5),              SK_FIELD(coeff_base_eob, 3, 4),
+                    SK_FIELD(txb_skip, 2, 3),       SK_FIELD(skip, 2, 3),                  SK_FIELD(mv_joint, 4, 5)};
 #undef SK_FIELD
     const int nf = (int)(sizeof(fs) / sizeof(fs[0]));
     if (i < 0 || i >= nf) return nf;
     *off = (int32_t)(fs[i].p - (const uint16_t*)&c);
     *nsym = fs[i].n;
-    *count = (int32_t)(fs[i].bytes / (2 * (fs[i].n + 1)));
+    *stride = fs[i].stride;
+    *count = (int32_t)(fs[i].bytes / (2 * fs[i].stride));
     return nf;
 }
 
@@ -66,6 +67,36 @@ int sk_av1_ec_tokens_cpu(const uint32_t* tok, int n, int qidx, uint8_t* out, int
     if (m > cap) return -m;
     if (m) sk::av1::carry_bytes(sink.v.data(), m, out);
     return m;
+}
+
+// Interval words of k_av1_cdf (av1_kernels.hip) for a token stream, on the host:
+// words[i] for symbol and gathered tokens, 0 for literals.
+int sk_av1_cdf_words_cpu(const uint32_t* tok, int n, int qidx, uint32_t* words) {
+    using namespace sk::av1;
+    CdfContext cx = AV1_DEFAULT_CDF[coef_qctx(qidx)];
+    uint16_t* cdfs = (uint16_t*)&cx;
+    auto word = [](uint32_t clo, uint32_t chi, int nn, int s) {
+        const uint32_t fh = s < nn - 1 ? (32768u - chi) >> kProbShift : 0u;
+        const uint32_t fl = s > 0 ? (32768u - clo) >> kProbShift : 0u;
+        return fh | fl << 10 | (uint32_t)(nn - s) << 20 | (s > 0 ? 1u << 25 : 0u);
+    };
+    for (int i = 0; i < n; i++) {
+        const uint32_t t = tok[i], kind = t >> 30;
+        uint16_t* c = cdfs + (t & 0x3fffff);
+        if (kind == 0) {
+            const int nn = (int)((t >> 26) & 15) + 1, s = (int)((t >> 22) & 15);
+            words[i] = word(s > 0 ? c[s - 1] : 0, c[s], nn, s);
+            update_cdf(c, nn, s);
+        } else if (kind == 1) {
+            words[i] = 0;
+        } else {
+            uint16_t c2[3];
+            gather_partition_cdf(c, ((t >> 29) & 1) == 0, c2);
+            const int v = (int)((t >> 28) & 1);
+            words[i] = word(c2[0], v ? 32768u : c2[0], 2, v);
+        }
+    }
+    return n;
 }
 
 }  // extern "C"

@@ -106,6 +106,7 @@ def lib():
         L.sk_h264_request_keyframe.argtypes = [ctypes.c_void_p]
         L.sk_h264_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.sk_h264_set_rate.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.sk_h264_wait_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.sk_h264_rc_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.sk_h264_set_overlay_image.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                                 ctypes.c_int]
@@ -352,12 +353,17 @@ class H264Encoder:
             self._staged = None
             raise RuntimeError(f"upload failed: {L.sk_last_error().decode()}")
 
-    def upload_ptr(self, ptr: int, stride: int, frame_id: int = 0, keepalive=None) -> None:
+    def upload_ptr(self, ptr: int, stride: int, frame_id: int = 0, keepalive=None, wait_stream: int = 0) -> None:
         """:meth:`upload` from a raw address: host memory or, on the HIP backend, device
         memory of this encoder's GPU (e.g. a torch tensor's ``data_ptr()``; the copy is
-        then device-to-device). ``keepalive`` is held until the frame is finished."""
+        then device-to-device). ``keepalive`` is held until the frame is finished.
+        ``wait_stream``: a HIP stream handle of this device (``torch.cuda.Stream.cuda_stream``)
+        whose queued work produces the source; the copy waits for it on the device."""
         self._staged = keepalive
         L = lib()
+        if wait_stream and L.sk_h264_wait_stream(self._h, ctypes.c_void_p(int(wait_stream))) < 0:
+            self._staged = None
+            raise RuntimeError(f"wait_stream failed: {L.sk_last_error().decode()}")
         if L.sk_h264_upload(self._h, ctypes.c_void_p(int(ptr)), int(stride), frame_id & 0xFFFF) < 0:
             self._staged = None
             raise RuntimeError(f"upload failed: {L.sk_last_error().decode()}")

@@ -86,10 +86,19 @@ class DistBandedEncoder:
         self.recv = torch.empty((self.rows, width, 4), dtype=torch.uint8, device=self.device)
         self.stage = (torch.zeros((self.world, self.rows, width, 4), dtype=torch.uint8, device=self.device)
                       if self.rank == 0 else None)
-        self._ctrl = torch.zeros(3, dtype=torch.int64, device=self.device)
+        # control plane on the host: a gloo twin of an RCCL group, so reading the
+        # broadcast values never synchronises a GPU stream
+        self._cgroup = dist.new_group(ranks=self._ranks(group), backend="gloo") if self.nccl else group
+        self._ctrl = torch.zeros(3, dtype=torch.int64)
         self._key = False
         self._qp = 0
         self.steps = 0
+
+    @staticmethod
+    def _ranks(group) -> list[int]:
+        if group is None:
+            return list(range(dist.get_world_size()))
+        return dist.get_process_group_ranks(group)
 
     # -- control (rank 0; applied on every rank at the next step) ---------------------
     def request_keyframe(self) -> None:
@@ -102,7 +111,7 @@ class DistBandedEncoder:
         if self.rank == 0:
             self._ctrl[0], self._ctrl[1], self._ctrl[2] = frame_id, int(self._key), self._qp
             self._key, self._qp = False, 0
-        dist.broadcast(self._ctrl, src=0, group=self.group)
+        dist.broadcast(self._ctrl, src=self._ranks(self.group)[0], group=self._cgroup)
         fid, key, qp = (int(v) for v in self._ctrl.tolist())
         if key:
             self.enc.request_keyframe()
@@ -120,7 +129,7 @@ class DistBandedEncoder:
             for r, (y0, y1) in enumerate(self.bands):
                 self.stage[r, : y1 - y0].copy_(frame[y0:y1], non_blocking=True)
             chunks = list(self.stage.unbind(0))
-        dist.scatter(self.recv, chunks, src=0, group=self.group)
+        dist.scatter(self.recv, chunks, src=self._ranks(self.group)[0], group=self.group)
 
     def encode(self, frame=None, frame_id: int = 0) -> Optional[list[Packet]]:
         fid = self._control(frame_id)
@@ -128,9 +137,10 @@ class DistBandedEncoder:
         y0, y1 = self.bands[self.rank]
         band = self.recv[: y1 - y0]
         if self.nccl:
-            # the encoder's HIP stream reads what RCCL wrote on torch's stream
-            torch.cuda.current_stream(self.device).synchronize()
-            self.enc.upload_ptr(band.data_ptr(), self.width * 4, fid, keepalive=band)
+            # the encoder's copy waits on the device for what RCCL wrote on torch's stream
+            # (an event, not a host synchronisation)
+            self.enc.upload_ptr(band.data_ptr(), self.width * 4, fid, keepalive=band,
+                                wait_stream=torch.cuda.current_stream(self.device).cuda_stream)
             self.enc.launch()
             mine = self.enc.finish()
         else:

@@ -98,15 +98,15 @@ def test_update_cdf_rule():
 
 def _fields(L):
     P = ctypes.POINTER
-    L.sk_av1_cdf_field.argtypes = [ctypes.c_int, P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_int32)]
+    L.sk_av1_cdf_field.argtypes = [ctypes.c_int] + [P(ctypes.c_int32)] * 4
     L.sk_av1_cdf_field.restype = ctypes.c_int
     out, i = [], 0
     while True:
-        off, n, cnt = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-        nf = L.sk_av1_cdf_field(i, off, n, cnt)
+        off, n, cnt, st = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        nf = L.sk_av1_cdf_field(i, off, n, cnt, st)
         if i >= nf:
             return out
-        out.append((off.value, n.value, cnt.value))
+        out.append((off.value, n.value, cnt.value, st.value))
         i += 1
 
 
@@ -122,7 +122,7 @@ def _token_streams(L, seed, tiles):
     for t in range(tiles):
         n = 12000 if t == 0 else int(rng.integers(0, 3000))
         picks = [fields[int(rng.integers(len(fields)))] for _ in range(6)]
-        ctxs = [(off + int(rng.integers(cnt)) * (ns + 1), ns) for off, ns, cnt in picks]
+        ctxs = [(off + int(rng.integers(cnt)) * st, ns) for off, ns, cnt, st in picks]
         toks = []
         for _ in range(n):
             k = int(rng.choice([0, 0, 0, 0, 1, 2])) if t else int(rng.choice([0, 1, 1]))
@@ -134,7 +134,7 @@ def _token_streams(L, seed, tiles):
                 nb = int(rng.integers(1, 26))
                 toks.append((1 << 30) | ((nb - 1) << 25) | int(rng.integers(1 << nb)))
             else:
-                off = part[0] + int(rng.integers(part[2])) * (part[1] + 1)
+                off = part[0] + int(rng.integers(part[2])) * part[3]
                 toks.append((2 << 30) | (int(rng.integers(2)) << 29) | (int(rng.integers(2)) << 28) | off)
         streams.append(toks)
     return streams
@@ -169,7 +169,10 @@ def test_gpu_tiles_match_host_encoder():
     L.sk_av1_ec_tokens_cpu.argtypes = [P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int, P(ctypes.c_uint8), ctypes.c_int]
     L.sk_av1_ec_tokens_cpu.restype = ctypes.c_int
     L.sk_av1_ec_tokens_hip.argtypes = [P(ctypes.c_uint32), P(ctypes.c_int32), P(ctypes.c_int32), ctypes.c_int,
-                                       ctypes.c_int, P(ctypes.c_uint8), ctypes.c_int, P(ctypes.c_int32)]
+                                       ctypes.c_int, P(ctypes.c_uint8), ctypes.c_int, P(ctypes.c_int32),
+                                       P(ctypes.c_uint32)]
+    L.sk_av1_cdf_words_cpu.argtypes = [P(ctypes.c_uint32), ctypes.c_int, ctypes.c_int, P(ctypes.c_uint32)]
+    L.sk_av1_cdf_words_cpu.restype = ctypes.c_int
     L.sk_av1_ec_tokens_hip.restype = ctypes.c_int
     for qidx in (10, 100, 200):
         streams = _token_streams(L, qidx, 24)
@@ -181,10 +184,19 @@ def test_gpu_tiles_match_host_encoder():
         cap = 8 * len(flat) + 4096
         out = np.zeros(cap, np.uint8)
         sizes = np.zeros(len(streams), np.int32)
+        words = np.zeros(max(1, len(flat)), np.uint32)
         a32 = lambda x, t=ctypes.c_int32: (t * max(1, len(x)))(*x)   # noqa: E731
         rc = L.sk_av1_ec_tokens_hip(a32(flat, ctypes.c_uint32), a32(offs), a32(ns), len(streams), qidx,
-                                    out.ctypes.data_as(P(ctypes.c_uint8)), cap, sizes.ctypes.data_as(P(ctypes.c_int32)))
+                                    out.ctypes.data_as(P(ctypes.c_uint8)), cap, sizes.ctypes.data_as(P(ctypes.c_int32)),
+                                    words.ctypes.data_as(P(ctypes.c_uint32)))
         assert rc == 0
+        for t, s in enumerate(streams):   # phase A (k_av1_cdf) first: interval words
+            ref = np.zeros(max(1, len(s)), np.uint32)
+            L.sk_av1_cdf_words_cpu(a32(s, ctypes.c_uint32), len(s), qidx, ref.ctypes.data_as(P(ctypes.c_uint32)))
+            sym = np.array([(x >> 30) != 1 for x in s], bool)
+            got = words[offs[t]:offs[t] + len(s)]
+            bad = np.nonzero((got != ref[:len(s)]) & sym)[0]
+            assert bad.size == 0, (qidx, t, bad[:5], got[bad[:5]], ref[bad[:5]])
         pos = 0
         for t, s in enumerate(streams):
             ref = (ctypes.c_uint8 * (8 * len(s) + 64))()

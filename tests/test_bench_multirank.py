@@ -1,4 +1,4 @@
-"""The driver's multi-GPU bench path rehearsed on the CPU: torchrun with 2 gloo
+"""The driver's multi-GPU bench path rehearsed on the CPU: torchrun with 2 and 4 gloo
 ranks, the CPU encoder, and the per-GPU end-to-end check on every rank. Rank 0's
 JSON line must carry one e2e record per rank and the node total."""
 import json
@@ -11,7 +11,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_bench_two_ranks_report_per_gpu_e2e(world, tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000), "bench.py",

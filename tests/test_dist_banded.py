@@ -49,7 +49,7 @@ def _worker(rank, world, port, out_dir, W, H, sh):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W,H,sh", [(2, 160, 200, 32), (3, 128, 192, 32)])
+@pytest.mark.parametrize("world,W,H,sh", [(2, 160, 200, 32), (3, 128, 192, 32), (4, 128, 256, 32)])
 def test_dist_banded_matches_single_encoder(tmp_path, world, W, H, sh):
     import torch.multiprocessing as mp
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), W, H, sh), nprocs=world, join=True)
