@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--rc", default="crf", choices=["cqp", "crf", "cbr"],
                    help="K10 rate control: crf = the reference's CRF semantics (h264_crf, settings.py:48)")
     p.add_argument("--kbps", type=int, default=8000, help="CBR bitrate (--rc cbr)")
+    p.add_argument("--fps", type=float, default=60.0,
+                   help="session frame rate the encoders are configured for (CBR frame budget, level)")
     p.add_argument("--av1-kbps", type=int, default=40000,
                    help="AV1 4K120 extra: CBR bitrate (the reference's AV1 encoders run bitrate-controlled in "
                         "the WebRTC mode; 40 Mbit/s = AV1 level 5.1 Main tier maximum); 0 = --rc/--qp")
@@ -132,6 +134,7 @@ def run_capture_path(args, pool, local_rank):
                                         use_cpu=int(args.backend == "cpu"), source=pixelflux.SOURCE_POOL,
                                         step_mode=1, pool_frames=args.pool, pool_stride=W * 4,
                                         pool_phase=3 * i,
+                                        target_fps=float(args.fps),
                                         h264_rc_mode={"cqp": 0, "crf": 1, "cbr": 2}[args.rc],
                                         h264_bitrate_kbps=args.kbps if args.rc == "cbr" else 0)
         cs.pool = pool.array.ctypes.data
@@ -206,7 +209,7 @@ def run_extra(args, W, H, encoder, fps, local_rank, steps):
         for i in range(8):
             src.frame(i, out=pool.array[i])
         a = types.SimpleNamespace(**vars(args))
-        a.sessions, a.encoder, a.pool, a.mode = 1, encoder, 8, "fullframe"
+        a.sessions, a.encoder, a.pool, a.mode, a.fps = 1, encoder, 8, "fullframe", float(fps)
         if encoder == "av1" and args.av1_kbps > 0:
             a.rc, a.kbps = "cbr", args.av1_kbps
         caps, run_caps = run_capture_path(a, pool, local_rank)

@@ -600,6 +600,7 @@ __global__ __launch_bounds__(256) void k_av1_tok_copy(Av1Args A) {
 // writes the interval word the coder needs:
 //   [9:0] (32768 - cdf[s]) >> 6 (0 for the last symbol)   [19:10] (32768 - cdf[s-1]) >> 6
 //   [24:20] N - s   [25] s > 0
+// Literal tokens are copied as their own word (bits 31:30 = 01).
 // k_av1_ec (phase B): one wave per tile runs the arithmetic coder over the interval
 // words and literal bits with its state in scalar registers (the only serial work
 // left), tokens / words in double-buffered 64-lane vector batches, settled chunks
@@ -666,100 +667,52 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
         const int v = (int)((tt >> 28) & 1);
         return ec_word(c0, v ? 32768u : c0, 2, v);
     };
-    // Up to four symbols of distinct CDFs (consecutive in this wave's order, so their
-    // relative order does not matter) adapt together, 16 lanes each: lane j of group k
-    // holds cdf[j] of symbol k (alphabets <= 15, the counter in lane N). A run of one
-    // context (the zero-level context of 16x16 luma blocks can be half of a tile's
-    // symbols) stays in registers: lanes 0..15 of `cache` hold that CDF, written back
-    // to LDS only when another group needs LDS.
-    const int grp = L >> 4, jl = L & 15;
+    // The CDF of the context adapted last stays in a register (lane j: cdf[j], lane N:
+    // the counter) and goes back to LDS only when another context comes up: the hot
+    // contexts (the zero-level context of 16x16 luma blocks can be half of a tile's
+    // symbols) then adapt in registers with no LDS round trip.
     int cache_off = -1, cache_n = 0;
     uint32_t cache = 0;
-    auto adapt = [&](uint32_t cv, int n, int s, int lane, int count, uint32_t& nv, bool& wr) {
-        const int rate = 3 + (count > 15) + (count > 31) + (n > 3 ? 2 : (n > 1 ? 1 : 0));
-        const int c = (int)cv;
-        nv = cv;
-        wr = false;
-        if (lane < n - 1) {
-            nv = (uint32_t)(lane >= s ? c + ((32768 - c) >> rate) : c - (c >> rate));
-            wr = true;
-        } else if (lane == n && count < 32) {
-            nv = (uint32_t)(count + 1);
-            wr = true;
-        }
+    auto evict = [&]() {
+        if (cache_off >= 0 && L <= cache_n) cdfs[cache_off + L] = (uint16_t)cache;
+        cache_off = -1;
     };
     auto sub = [&](uint32_t tv, int b) -> uint32_t {   // 64 tokens from b: this wave's words
-        const bool mine = b + L < ntok && (tv >> 30) != 1 && ec_owner(tv & 0x3fffff) == part;
-        uint64_t m = __ballot(mine);
+        // literal tokens are their own word (partition 0 copies them)
+        const bool lit = (tv >> 30) == 1;
+        const bool mine = b + L < ntok && (lit ? part == 0 : ec_owner(tv & 0x3fffff) == part);
+        wst[L] = tv;
+        uint64_t m = __ballot(mine && !lit);
         while (m) {
-            uint32_t tg[4] = {0u, 0u, 0u, 0u};
-            int ig[4] = {0, 0, 0, 0};
-            int g = 0;
-            bool stop = false;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (stop || !m) continue;
-                const int i = __builtin_ctzll(m);
-                const uint32_t tt = sgpr(rdlane(tv, i));
-                const bool wide = (tt >> 30) != 0 || ((tt >> 26) & 15) >= 15;
-                bool clash = wide;
-#pragma unroll
-                for (int q = 0; q < k; q++) clash |= ((tg[q] ^ tt) & 0x3fffff) == 0;
-                if (clash) {
-                    stop = true;
-                    continue;
+            const int i = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t tt = sgpr(rdlane(tv, i));
+            uint32_t w;
+            if ((tt >> 30) == 0) {
+                const int off = (int)(tt & 0x3fffff);
+                const int n = (int)((tt >> 26) & 15) + 1, s = (int)((tt >> 22) & 15);
+                if (off != cache_off) {
+                    evict();
+                    cache = L <= n ? (uint32_t)cdfs[off + L] : 0u;
+                    cache_off = off;
+                    cache_n = n;
                 }
-                tg[k] = tt;
-                ig[k] = i;
-                g = k + 1;
-                m &= m - 1;
-            }
-            if (g == 1 && (int)(tg[0] & 0x3fffff) == cache_off) {   // cached run: registers only
-                const int n = (int)((tg[0] >> 26) & 15) + 1, s = (int)((tg[0] >> 22) & 15);
                 const uint32_t chi = sgpr(rdlane(cache, s)), clo = sgpr(rdlane(cache, s > 0 ? s - 1 : 0));
-                uint32_t nv;
-                bool wr;
-                adapt(cache, n, s, L, (int)sgpr(rdlane(cache, n)), nv, wr);
-                cache = nv;
-                const uint32_t w = ec_word(clo, chi, n, s);
-                if (L == 0) wst[ig[0]] = w;
-                continue;
+                const int count = (int)sgpr(rdlane(cache, n));
+                const int nr = n > 3 ? 2 : (n > 1 ? 1 : 0);
+                const int rate = (int)sgpr((uint32_t)(3 + (count > 15) + (count > 31) + nr));
+                const int cnt1 = (int)sgpr((uint32_t)(count < 32 ? count + 1 : count));
+                // update_cdf, branch-free: lanes < N-1 move towards 0 / 32768, lane N counts
+                const int c = (int)cache;
+                const int up = c + ((32768 - c) >> rate), dn = c - (c >> rate);
+                const int ad = L >= s ? up : dn;
+                cache = (uint32_t)(L < n - 1 ? ad : (L == n ? cnt1 : c));
+                w = ec_word(clo, chi, n, s);
+            } else {   // gathered boolean: reads a partition CDF from LDS
+                evict();
+                w = one(tt);
             }
-            if (cache_off >= 0) {   // write the cached CDF back before LDS is read again
-                if (L <= cache_n) cdfs[cache_off + L] = (uint16_t)cache;
-                cache_off = -1;
-            }
-            if (g == 0) {   // the next symbol needs the whole wave
-                const int i = __builtin_ctzll(m);
-                m &= m - 1;
-                const uint32_t w = one(sgpr(rdlane(tv, i)));
-                if (L == 0) wst[i] = w;
-                continue;
-            }
-            const uint32_t mt = grp == 0 ? tg[0] : (grp == 1 ? tg[1] : (grp == 2 ? tg[2] : tg[3]));
-            const bool act = grp < g;
-            const int n = (int)((mt >> 26) & 15) + 1, s = (int)((mt >> 22) & 15), off = (int)(mt & 0x3fffff);
-            const uint32_t cv = act && jl <= n ? (uint32_t)cdfs[off + jl] : 0u;
-            const int base = grp << 4;
-            const uint32_t chi = (uint32_t)__shfl((int)cv, base + s);
-            const uint32_t clo = (uint32_t)__shfl((int)cv, base + (s > 0 ? s - 1 : 0));
-            uint32_t nv;
-            bool wr;
-            adapt(cv, n, s, jl, __shfl((int)cv, base + n), nv, wr);
-            if (g == 1) {   // a single context: keep it in registers (lanes 0..15)
-                cache = nv;
-                cache_off = off;
-                cache_n = n;
-            } else if (act && wr) {
-                cdfs[off + jl] = (uint16_t)nv;
-            }
-            const uint32_t word = ec_word(clo, chi, n, s);
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (k < g) {
-                    const uint32_t wk = sgpr(rdlane(word, 16 * k));
-                    if (L == 0) wst[ig[k]] = wk;
-                }
+            if (L == 0) wst[i] = w;
         }
         wsync();
         const uint32_t out = wst[L];
@@ -796,7 +749,6 @@ __global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
     const int t = blockIdx.x, L = threadIdx.x;
     const int ntok = A.tile_ntok[t], last = A.tile_tok_cap - 1;
     const int cap = A.tile_cap;
-    const uint32_t* tk = A.tokc + (size_t)t * A.tile_tok_cap;
     const uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
     uint16_t* dst = A.chunks + (size_t)t * cap;
     uint64_t low = 0;
@@ -850,7 +802,7 @@ __global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
         cnt = c + d - 24;
         low &= m;
     };
-    auto code = [&](uint32_t tv, uint32_t wv, int b) {
+    auto code = [&](uint32_t wv, int b) {
         const int m = sk_min(64, ntok - b);
 #pragma unroll 2
         for (int i = 0; i < m; i++) {
@@ -859,13 +811,12 @@ __global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
             cnt = (int)sgpr((uint32_t)cnt);
             nb = (int)sgpr((uint32_t)nb);
             low = ((uint64_t)sgpr((uint32_t)(low >> 32)) << 32) | sgpr((uint32_t)low);
-            const uint32_t tt = sgpr(rdlane(tv, i));
             const uint32_t w = sgpr(rdlane(wv, i));
-            if (__builtin_expect((tt >> 30) == 1, 0)) {   // L(n) literal: equiprobable bits
-                const int nbits = (int)((tt >> 25) & 31) + 1;
+            if (__builtin_expect((w >> 30) == 1, 0)) {   // L(n) literal token: equiprobable bits
+                const int nbits = (int)((w >> 25) & 31) + 1;
                 for (int k = nbits - 1; k >= 0; k--) {
                     const uint32_t rr = rng, split = ((rr >> 8) << 7) + kMinProb;
-                    if ((tt >> k) & 1) {
+                    if ((w >> k) & 1) {
                         low += rr - split;
                         norm(split);
                     } else {
@@ -889,33 +840,28 @@ __global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
             rng = r2 << d;
         }
     };
-    uint32_t TX[kSub], WX[kSub], TY[kSub], WY[kSub];
-    auto load = [&](uint32_t* tv, uint32_t* wv, int b) {
+    uint32_t WX[kSub], WY[kSub];
+    auto load = [&](uint32_t* wv, int b) {
 #pragma unroll
-        for (int j = 0; j < kSub; j++) {
-            const int i = sk_min(b + 64 * j + L, last);
-            tv[j] = tk[i];
-            wv[j] = pw[i];
-        }
+        for (int j = 0; j < kSub; j++) wv[j] = pw[sk_min(b + 64 * j + L, last)];
     };
-    auto big = [&](uint32_t* tv, uint32_t* wv, int b) {
-        use_regs(tv);
+    auto big = [&](uint32_t* wv, int b) {
         use_regs(wv);
 #pragma unroll
         for (int j = 0; j < kSub; j++) {
-            if (b + 64 * j < ntok) code(tv[j], wv[j], b + 64 * j);
+            if (b + 64 * j < ntok) code(wv[j], b + 64 * j);
             nb = (int)sgpr((uint32_t)nb);
             fl = (int)sgpr((uint32_t)fl);
             if (nb - fl >= kObFlush) flush(fl + kObFlush);   // <= 64 x 4 chunks per sub-batch
         }
     };
-    load(TX, WX, 0);
-    load(TY, WY, kBig);
+    load(WX, 0);
+    load(WY, kBig);
     for (int b = 0; b < ntok; b += 2 * kBig) {
-        big(TX, WX, b);
-        load(TX, WX, b + 2 * kBig);
-        if (b + kBig < ntok) big(TY, WY, b + kBig);
-        load(TY, WY, b + 3 * kBig);
+        big(WX, b);
+        load(WX, b + 2 * kBig);
+        if (b + kBig < ntok) big(WY, b + kBig);
+        load(WY, b + 3 * kBig);
     }
     {   // SymbolCoder::finish
         int c = cnt;

@@ -70,7 +70,7 @@ int sk_av1_ec_tokens_cpu(const uint32_t* tok, int n, int qidx, uint8_t* out, int
 }
 
 // Interval words of k_av1_cdf (av1_kernels.hip) for a token stream, on the host:
-// words[i] for symbol and gathered tokens, 0 for literals.
+// words[i] for symbol and gathered tokens, the token itself for literals.
 int sk_av1_cdf_words_cpu(const uint32_t* tok, int n, int qidx, uint32_t* words) {
     using namespace sk::av1;
     CdfContext cx = AV1_DEFAULT_CDF[coef_qctx(qidx)];
@@ -88,7 +88,7 @@ int sk_av1_cdf_words_cpu(const uint32_t* tok, int n, int qidx, uint32_t* words) 
             words[i] = word(s > 0 ? c[s - 1] : 0, c[s], nn, s);
             update_cdf(c, nn, s);
         } else if (kind == 1) {
-            words[i] = 0;
+            words[i] = t;   // literal tokens are their own word
         } else {
             uint16_t c2[3];
             gather_partition_cdf(c, ((t >> 29) & 1) == 0, c2);
