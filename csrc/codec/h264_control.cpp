@@ -46,7 +46,8 @@ void Controller::request_keyframe() {
 }
 
 void Controller::plan(const uint8_t* dirty, SliceTask* tasks) {
-    const PlanConfig pc = plan_config(cfg_);
+    PlanConfig pc = plan_config(cfg_);
+    if (rc_.mode == RC_CBR) pc.use_paint_over = 0;   // K10 CBR: no paint-over refresh (as k_plan)
     for (int s = 0; s < g_.num_slices; s++)
         plan_stripe(pc, st_[s], pic_, dirty[s] != 0, g_.slice_first_row(s), g_.slice_rows(s), g_.mb_h, tasks[s]);
 }

@@ -151,6 +151,9 @@ SK_HD int rc_redo_step(const RcState& rc, long long frame_bits) {
 // for the inter frames after it.
 SK_HD void rc_raise_floor(RcState& rc) {
     if (rc.cur_intra) return;
+    // a burst (complexity well above the last inter frame's) overflows at any QP the
+    // buffer allows for ordinary frames: re-code it, but keep the floor where it is
+    if (rc.cur_cplx > 0 && rc.last_cplx[0] > 0 && 2 * (long long)rc.cur_cplx > 3 * (long long)rc.last_cplx[0]) return;
     rc.qp_floor = sk_max(rc.qp_floor, rc.cur_qp + 1);
     rc.floor_age = 0;
 }

@@ -676,6 +676,13 @@ __global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
     const int po = __hip_atomic_load(a.key_seq_host + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (qo > 0) pc.qp = qo;
     if (po > 0) pc.paint_qp = po;
+    {   // K10 CBR: no paint-over refresh (the budget codes every slice at the frame QP anyway)
+        const int seq = __hip_atomic_load(a.key_seq_host + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int mode = seq != a.rc->seq ? __hip_atomic_load(a.key_seq_host + 3, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_SYSTEM)
+                                          : a.rc->mode;
+        if (mode == RC_CBR) pc.use_paint_over = 0;
+    }
     for (int s = tid; s < ns; s += 256) {
         st[s].subpel_prev = st[s].subpel_hits;   // adaptive refinement gate (h264_frame.h subpel_gate)
         st[s].subpel_hits = 0;
