@@ -770,6 +770,125 @@ int rtc_h265_packetize(void* srtp, const uint8_t* annexb, int n, rtc_rtp_params*
     return w.failed ? -1 : w.count;
 }
 
+// AV1 RTP payload (AOM "RTP Payload Format for AV1" v1.0): one temporal unit of
+// low-overhead OBUs (obu_has_size_field = 1, as av1_cpu.cpp writes them) -> packets.
+// Aggregation header |Z|Y|W=0|N|000|: every OBU element carries a LEB128 length;
+// temporal delimiters, tile lists and padding are dropped, the OBU size field is
+// removed (the element length replaces it); OBUs larger than a packet are split
+// (Y on the packet holding the head, Z on the packets continuing it); N on the first
+// packet of a temporal unit with a sequence header. Marker = last packet of the TU.
+static int leb128_len(uint32_t v) {
+    int n = 1;
+    while (v >= 0x80) {
+        v >>= 7;
+        n++;
+    }
+    return n;
+}
+static int put_leb128(uint8_t* d, uint32_t v) {
+    int n = 0;
+    do {
+        uint8_t b = v & 0x7f;
+        v >>= 7;
+        d[n++] = (uint8_t)(b | (v ? 0x80 : 0));
+    } while (v);
+    return n;
+}
+
+int rtc_av1_packetize(void* srtp, const uint8_t* tu, int n, rtc_rtp_params* p, uint8_t* out, int cap, int* lens,
+                      int max_pkts) {
+    PacketWriter w{static_cast<Srtp*>(srtp), p, out, cap, 0, 0, lens, max_pkts};
+    const int maxp = p->mtu - ((p->playout_ext_id > 0 && p->playout_ext_id < 15) ? 20 : 12);
+    if (maxp < 64) return -1;
+    struct Elem { uint8_t hdr[2]; int hlen; const uint8_t* pl; int plen; };
+    std::vector<Elem> el;
+    bool seq = false;
+    for (int pos = 0; pos < n;) {   // parse the OBUs
+        const uint8_t h0 = tu[pos];
+        const int type = (h0 >> 3) & 15, ext = (h0 >> 2) & 1, has_size = (h0 >> 1) & 1;
+        int q = pos + 1 + ext;
+        if (q > n) return -1;
+        uint64_t sz = 0;
+        if (has_size) {
+            int sh = 0;
+            for (;;) {
+                if (q >= n || sh > 56) return -1;
+                const uint8_t b = tu[q++];
+                sz |= (uint64_t)(b & 0x7f) << sh;
+                sh += 7;
+                if (!(b & 0x80)) break;
+            }
+        } else {
+            sz = (uint64_t)(n - q);
+        }
+        if (q + (int64_t)sz > n) return -1;
+        if (type == 1) seq = true;
+        if (type != 2 && type != 8 && type != 15) {
+            Elem e;
+            e.hdr[0] = (uint8_t)(h0 & ~2);
+            e.hdr[1] = ext ? tu[pos + 1] : 0;
+            e.hlen = 1 + ext;
+            e.pl = tu + q;
+            e.plen = (int)sz;
+            el.push_back(e);
+        }
+        pos = q + (int)sz;
+    }
+    if (el.empty()) return 0;
+    // packetise: elements in order, split where a packet fills up
+    std::vector<uint8_t> pk((size_t)maxp);
+    int used = 1;          // aggregation header first
+    bool z = false;        // this packet starts with a continuation
+    bool first = true;
+    auto flush = [&](bool y, bool last) -> bool {
+        pk[0] = (uint8_t)((z ? 0x80 : 0) | (y ? 0x40 : 0) | ((first && seq) ? 0x08 : 0));
+        uint8_t* d = w.begin(used);
+        if (!d) return false;
+        memcpy(d, pk.data(), (size_t)used);
+        w.end(used, last);
+        first = false;
+        used = 1;
+        return true;
+    };
+    for (size_t k = 0; k < el.size(); k++) {
+        const Elem& e = el[k];
+        const int total = e.hlen + e.plen;   // element bytes (header + payload)
+        int off = 0;                         // bytes of this element already sent
+        while (off < total) {
+            const int rem = total - off;
+            const int room = maxp - used;
+            if (leb128_len((uint32_t)rem) + rem <= room) {   // the rest fits
+                used += put_leb128(pk.data() + used, (uint32_t)rem);
+                for (int i = 0; i < rem; i++) {
+                    const int b = off + i;
+                    pk[(size_t)used + i] = b < e.hlen ? e.hdr[b] : e.pl[b - e.hlen];
+                }
+                used += rem;
+                off = total;
+                if (k + 1 == el.size()) {
+                    if (!flush(false, true)) return -1;
+                    z = false;
+                }
+            } else if (room >= 8) {   // a fragment fills the packet
+                const int frag = room - leb128_len((uint32_t)room);
+                used += put_leb128(pk.data() + used, (uint32_t)frag);
+                for (int i = 0; i < frag; i++) {
+                    const int b = off + i;
+                    pk[(size_t)used + i] = b < e.hlen ? e.hdr[b] : e.pl[b - e.hlen];
+                }
+                used += frag;
+                off += frag;
+                if (!flush(true, false)) return -1;
+                z = true;
+            } else {   // no useful room left: close this packet before the element
+                if (!flush(false, false)) return -1;
+                z = false;
+            }
+        }
+    }
+    return w.failed ? -1 : w.count;
+}
+
 int rtc_rtp_packet(void* srtp, const uint8_t* payload, int n, rtc_rtp_params* p, uint8_t* out, int cap) {
     int len = 0;
     PacketWriter w{static_cast<Srtp*>(srtp), p, out, cap, 0, 0, &len, 1};

@@ -82,6 +82,9 @@ int rtc_h264_packetize(void* srtp, const uint8_t* annexb, int n, struct rtc_rtp_
 // RFC 7798 (H.265) packetisation: single NAL / AP / FU payloads, same contract.
 int rtc_h265_packetize(void* srtp, const uint8_t* annexb, int n, struct rtc_rtp_params* p, uint8_t* out,
                        int cap, int* lens, int max_pkts);
+// AV1 (AOM RTP payload format): one temporal unit of size-delimited OBUs.
+int rtc_av1_packetize(void* srtp, const uint8_t* tu, int n, rtc_rtp_params* p, uint8_t* out, int cap, int* lens,
+                      int max_pkts);
 // One packet around an arbitrary payload (Opus, ...). Returns its length.
 int rtc_rtp_packet(void* srtp, const uint8_t* payload, int n, struct rtc_rtp_params* p, uint8_t* out, int cap);
 

@@ -18,15 +18,18 @@ Mapping:
   convert kernel (scaling is not: caps must keep the capture size);
 * H.264 encoders (``x264enc``, ``nvh264enc``, ``vah264enc``, ``openh264enc``,
   ``qsvh264enc``, ``hiph264enc``) → the gfx950 H.264 encoder, H.265 encoders (``x265enc``,
-  ``nvh265enc``, ``vah265enc``, ``qsvh265enc``, ``hiph265enc``) → the gfx950 HEVC encoder:
-  ``bitrate`` (kbit/s),
+  ``nvh265enc``, ``vah265enc``, ``qsvh265enc``, ``hiph265enc``) → the gfx950 HEVC encoder,
+  AV1 encoders (``av1enc``, ``svtav1enc``, ``rav1enc``, ``nvav1enc``, ``vaav1enc``,
+  ``qsvav1enc``, ``hipav1enc``) → the gfx950 AV1 encoder:
+  ``bitrate`` / ``target-bitrate`` (kbit/s),
   ``key-int-max`` / ``gop-size`` / ``keyframe-period``, ``quantizer`` / ``qp-const``;
   ``jpegenc`` → the JPEG stripe encoder;
-* payloaders ``rtph264pay`` / ``rtph265pay`` (``mtu``), ``webrtcbin`` (``stun-server``, ``latency``);
+* payloaders ``rtph264pay`` / ``rtph265pay`` / ``rtpav1pay`` (``mtu``), ``webrtcbin`` (``stun-server``,
+  ``latency``);
 * audio ``pulsesrc`` (``device``) → ``opusenc`` (``bitrate``, ``frame-size``) →
   ``rtpopuspay``.
-VP8 / VP9 / AV1 encoder elements are rejected with an explicit error: this build's
-video codecs are H.264, H.265 and JPEG.
+VP8 / VP9 encoder elements are rejected with an explicit error: this build's video
+codecs are H.264, H.265, AV1 and JPEG.
 """
 from __future__ import annotations
 
@@ -38,8 +41,9 @@ H264_ENCODERS = {"x264enc", "nvh264enc", "vah264enc", "vah264lpenc", "openh264en
                  "nvcudah264enc", "nvautogpuh264enc"}
 H265_ENCODERS = {"x265enc", "nvh265enc", "vah265enc", "vah265lpenc", "qsvh265enc", "hiph265enc", "nvcudah265enc",
                  "nvautogpuh265enc"}
-UNSUPPORTED_ENCODERS = {"vp8enc", "vp9enc", "vavp9enc", "av1enc", "svtav1enc", "rav1enc", "nvav1enc", "vaav1enc",
-                        "qsvav1enc"}
+AV1_ENCODERS = {"av1enc", "svtav1enc", "rav1enc", "nvav1enc", "vaav1enc", "qsvav1enc", "hipav1enc",
+                "nvcudaav1enc"}
+UNSUPPORTED_ENCODERS = {"vp8enc", "vp9enc", "vavp9enc"}
 PASSTHROUGH = {"videoconvert", "cudaupload", "cudaconvert", "cudadownload", "vapostproc", "hipupload",
                "hipconvert", "queue", "videorate", "capsfilter", "identity", "audioconvert", "audioresample",
                "tee", "fakesink"}
@@ -64,7 +68,7 @@ class PipelineSpec:
     width: Optional[int] = None
     height: Optional[int] = None
     framerate: Optional[float] = None
-    encoder: Optional[str] = None       # "h264" | "h265" | "jpeg"
+    encoder: Optional[str] = None       # "h264" | "h265" | "av1" | "jpeg"
     encoder_element: Optional[str] = None
     bitrate_kbps: Optional[int] = None
     keyframe_distance: Optional[int] = None
@@ -170,10 +174,12 @@ def parse_pipeline(text: str) -> PipelineSpec:
             spec.height = p.get("height", spec.height)
             if "framerate" in p:
                 spec.framerate = float(p["framerate"])
-        elif n in H264_ENCODERS or n in H265_ENCODERS:
-            spec.encoder, spec.encoder_element = ("h265" if n in H265_ENCODERS else "h264"), n
-            if "bitrate" in p:
-                spec.bitrate_kbps = int(p["bitrate"])
+        elif n in H264_ENCODERS or n in H265_ENCODERS or n in AV1_ENCODERS:
+            spec.encoder = "h265" if n in H265_ENCODERS else ("av1" if n in AV1_ENCODERS else "h264")
+            spec.encoder_element = n
+            for k in ("bitrate", "target-bitrate"):
+                if k in p:
+                    spec.bitrate_kbps = int(p[k]) // (1000 if n == "rav1enc" else 1)   # rav1enc: bit/s
             for k in ("key-int-max", "gop-size", "keyframe-period", "idr-period"):
                 if k in p and int(p[k]) > 0:
                     spec.keyframe_distance = int(p[k])
@@ -183,9 +189,9 @@ def parse_pipeline(text: str) -> PipelineSpec:
         elif n == "jpegenc":
             spec.encoder, spec.encoder_element = "jpeg", n
         elif n in UNSUPPORTED_ENCODERS:
-            raise PipelineError(f"{n}: this build encodes H.264 / H.265 (HIP) and JPEG; use an H.264 or H.265 "
-                                "encoder element")
-        elif n in ("rtph264pay", "rtph265pay", "rtpopuspay"):
+            raise PipelineError(f"{n}: this build encodes H.264 / H.265 / AV1 (HIP) and JPEG; use one of "
+                                "those encoder elements")
+        elif n in ("rtph264pay", "rtph265pay", "rtpav1pay", "rtpopuspay"):
             if "mtu" in p:
                 spec.mtu = int(p["mtu"])
         elif n == "webrtcbin":

@@ -78,7 +78,8 @@ FLAGS = [
     ("uinput_mouse_socket", "SELKIES_UINPUT_MOUSE_SOCKET", "", "uinput mouse socket path"),
     ("js_socket_path", "SELKIES_JS_SOCKET_PATH", "/tmp", "joystick interposer socket directory"),
     ("encoder", "SELKIES_ENCODER", "x264enc",
-     "video encoder (H.264 names map to the HIP H.264 encoder, x265enc/nvh265enc/vah265enc to HIP HEVC)"),
+     "video encoder (H.264 names map to the HIP H.264 encoder, x265enc/nvh265enc/vah265enc to HIP HEVC, "
+     "av1enc/svtav1enc/rav1enc/nvav1enc/vaav1enc to HIP AV1)"),
     ("gpu_id", "SELKIES_GPU_ID", "0", "GPU ordinal"),
     ("framerate", "SELKIES_FRAMERATE", "60", "frames per second"),
     ("video_bitrate", "SELKIES_VIDEO_BITRATE", "8000", "video bitrate (kbit/s)"),
@@ -195,14 +196,16 @@ class StreamSession:
 
     def __init__(self, args, send_sdp, send_ice, input_factory=None, addresses=None):
         self.args = args
-        from selkies_gstreamer_amd.legacy.pipeline import H265_ENCODERS
+        from selkies_gstreamer_amd.legacy.pipeline import AV1_ENCODERS, H265_ENCODERS
         self.hevc = str(getattr(args, "encoder", "")) in H265_ENCODERS
+        self.av1 = str(getattr(args, "encoder", "")) in AV1_ENCODERS
         self.send_sdp, self.send_ice = send_sdp, send_ice
         self.fps = int(args.framerate)
         self.rc = RateController(int(args.video_bitrate) * 1000, self.fps)
         stun_srv, turn_srv = ice_servers_from_rtc(build_rtc_config(args))
         self.pc = PeerConnection(addresses=addresses, video=True, audio=True, data=True,
-                                 video_codec="H265" if self.hevc else "H264", stun_server=stun_srv,
+                                 video_codec="H265" if self.hevc else ("AV1" if self.av1 else "H264"),
+                                 stun_server=stun_srv,
                                  turn_server=turn_srv,
                                  fec_percentage=int(float(getattr(args, "video_packetloss_percent", 0) or 0)),
                                  relay_only=str(getattr(args, "ice_transport_policy", "all")) == "relay")
@@ -266,7 +269,7 @@ class StreamSession:
         w, h = self.width, self.height
         s = pixelflux.default_settings(w, h, target_fps=float(self.fps), h264_fullframe=1,
                                        output_mode=pixelflux.OUTPUT_MODE_HEVC if self.hevc else
-                                       pixelflux.OUTPUT_MODE_H264,
+                                       (pixelflux.OUTPUT_MODE_AV1 if self.av1 else pixelflux.OUTPUT_MODE_H264),
                                        h264_crf=self.rc.qp, h264_paintover_crf=self.rc.paint_qp,
                                        # K10 in the encoder: CBR with a 1.5-frame VBV (gstwebrtc_app.py:101-105)
                                        h264_rc_mode=2, h264_bitrate_kbps=max(1, self.rc.target_bps // 1000),

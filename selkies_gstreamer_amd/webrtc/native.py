@@ -49,6 +49,8 @@ def lib():
                                          ctypes.POINTER(ctypes.c_int), i32]),
             "rtc_h265_packetize": (i32, [vp, u8p, i32, ctypes.POINTER(RtpParams), ctypes.c_void_p, i32,
                                          ctypes.POINTER(ctypes.c_int), i32]),
+            "rtc_av1_packetize": (i32, [vp, u8p, i32, ctypes.POINTER(RtpParams), ctypes.c_void_p, i32,
+                                        ctypes.POINTER(ctypes.c_int), i32]),
             "rtc_rtp_packet": (i32, [vp, u8p, i32, ctypes.POINTER(RtpParams), ctypes.c_void_p, i32]),
             "rtc_crc32c": (ctypes.c_uint32, [u8p, i32]),
         }
@@ -240,6 +242,10 @@ class RtpPacketizer:
     def h265(self, annexb: bytes, timestamp: int, srtp: Srtp | None = None) -> list[bytes]:
         """RFC 7798 payloads (single NAL / aggregation / fragmentation units) of one access unit."""
         return self._packetize(self._L.rtc_h265_packetize, annexb, timestamp, srtp)
+
+    def av1(self, tu: bytes, timestamp: int, srtp: Srtp | None = None) -> list[bytes]:
+        """AV1 RTP payloads (aggregation header, OBU elements, fragments) of one temporal unit."""
+        return self._packetize(self._L.rtc_av1_packetize, tu, timestamp, srtp)
 
     def _packetize(self, fn, annexb: bytes, timestamp: int, srtp: Srtp | None) -> list[bytes]:
         self.params.timestamp = timestamp & 0xFFFFFFFF

@@ -58,8 +58,9 @@ class PeerConnection:
         self.state = "new"
         self.video_ssrc = random.getrandbits(32) or 1
         self.audio_ssrc = random.getrandbits(32) or 2
-        self.video_codec = "H265" if video_codec.upper() in ("H265", "HEVC") else "H264"
-        self._vpt = sdp.H265_PT if self.video_codec == "H265" else sdp.H264_PT
+        vc = video_codec.upper()
+        self.video_codec = "H265" if vc in ("H265", "HEVC") else ("AV1" if vc == "AV1" else "H264")
+        self._vpt = {"H265": sdp.H265_PT, "AV1": sdp.AV1_PT}.get(self.video_codec, sdp.H264_PT)
         self._vpk = RtpPacketizer(self.video_ssrc, self._vpt, mtu - 10, random.getrandbits(16))
         self._apk = RtpPacketizer(self.audio_ssrc, sdp.OPUS_PT, mtu - 10, random.getrandbits(16))
         self._history: dict[int, bytes] = {}
@@ -277,10 +278,11 @@ class PeerConnection:
 
     # -- media send -------------------------------------------------------------------------------
     def send_video(self, annexb: bytes, timestamp: int) -> int:
-        """Sends one H.264 or H.265 access unit (Annex-B) with a 90 kHz timestamp."""
+        """Sends one H.264 / H.265 access unit (Annex-B) or AV1 temporal unit (OBUs) with a
+        90 kHz timestamp."""
         if self.srtp_tx is None:
             return 0
-        pack = self._vpk.h265 if self.video_codec == "H265" else self._vpk.h264
+        pack = {"H265": self._vpk.h265, "AV1": self._vpk.av1}.get(self.video_codec, self._vpk.h264)
         if self._fec_tx is None:
             pkts = pack(annexb, timestamp, self.srtp_tx)
         else:   # RED + ULPFEC over the plaintext packets, then SRTP
@@ -381,7 +383,7 @@ class PeerConnection:
             return
         self._track_seq(h.ssrc, h.seq)
         payload = data[h.header_len:]
-        if h.payload_type in (sdp.H264_PT, sdp.H265_PT):
+        if h.payload_type in (sdp.H264_PT, sdp.H265_PT, sdp.AV1_PT):
             now_ms = time.monotonic() * 1000.0
             est = self._rx_rate.setdefault(h.ssrc, RemoteBitrateEstimator())
             r = est.add(now_ms, h.timestamp / 90.0, len(data))
@@ -392,8 +394,11 @@ class PeerConnection:
             pli, frames = jb.add(JbPacket(h.seq, h.timestamp, h.marker, payload))
             if pli:
                 self.request_keyframe(h.ssrc)
-            d = self._depack.setdefault(h.ssrc, rtp.H265Depacketizer() if h.payload_type == sdp.H265_PT
-                                        else rtp.H264Depacketizer())
+            d = self._depack.get(h.ssrc)
+            if d is None:
+                d = self._depack[h.ssrc] = {sdp.H265_PT: rtp.H265Depacketizer,
+                                            sdp.AV1_PT: rtp.AV1Depacketizer}.get(h.payload_type,
+                                                                                rtp.H264Depacketizer)()
             for fr in frames:
                 au = None
                 for i, pk in enumerate(fr.packets):

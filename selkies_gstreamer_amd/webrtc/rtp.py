@@ -231,3 +231,77 @@ class H265Depacketizer:
             self._au = []
             return au
         return None
+
+
+def _leb128(buf: bytes, pos: int) -> tuple[int, int]:
+    v, sh = 0, 0
+    while True:
+        b = buf[pos]
+        pos += 1
+        v |= (b & 0x7F) << sh
+        sh += 7
+        if not b & 0x80:
+            return v, pos
+
+
+def _put_leb128(v: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = v & 0x7F
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+class AV1Depacketizer:
+    """Reassembles AV1 RTP packets (aggregation header Z/Y/W/N, OBU elements) into a
+    temporal unit of low-overhead OBUs: a temporal delimiter, then every OBU with its
+    size field restored (what a decoder such as dav1d takes)."""
+
+    def __init__(self):
+        self._obus: list = []
+        self._frag: bytearray | None = None
+        self._ts = None
+
+    def push(self, payload: bytes, timestamp: int, marker: bool) -> bytes | None:
+        if self._ts is not None and timestamp != self._ts and self._obus:
+            self._obus, self._frag = [], None
+        self._ts = timestamp
+        if not payload:
+            return None
+        agg = payload[0]
+        z, y, w = bool(agg & 0x80), bool(agg & 0x40), (agg >> 4) & 3
+        pos, elems = 1, []
+        k = 0
+        while pos < len(payload):
+            k += 1
+            if w and k == w:            # last element: no length field
+                n = len(payload) - pos
+            else:
+                n, pos = _leb128(payload, pos)
+            elems.append(payload[pos:pos + n])
+            pos += n
+        for i, e in enumerate(elems):
+            cont = i == 0 and z
+            more = i == len(elems) - 1 and y
+            if cont:
+                if self._frag is None:   # lost the head: drop the fragment
+                    continue
+                self._frag += e
+                if not more:
+                    self._obus.append(bytes(self._frag))
+                    self._frag = None
+            elif more:
+                self._frag = bytearray(e)
+            else:
+                self._obus.append(bytes(e))
+        if marker:
+            out = bytearray(b"\x12\x00")   # temporal delimiter
+            for o in self._obus:
+                ext = (o[0] >> 2) & 1
+                hl = 1 + ext
+                out += bytes([o[0] | 2]) + o[1:hl] + _put_leb128(len(o) - hl) + o[hl:]
+            self._obus, self._frag = [], None
+            return bytes(out)
+        return None

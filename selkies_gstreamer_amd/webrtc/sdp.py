@@ -17,6 +17,7 @@ from .ice import Candidate
 
 H264_PT = 97
 H265_PT = 100   # reference: rtph265pay pt=100 (legacy/gstwebrtc_app.py:848-866)
+AV1_PT = 96     # reference: rtpav1pay payload=96 (legacy/gstwebrtc_app.py:924-934)
 OPUS_PT = 111
 RED_PT = 123
 ULPFEC_PT = 125
@@ -223,6 +224,12 @@ def h265_fmtp(level_id: int = 153) -> str:
     return f"level-id={level_id};profile-id=1;tier-flag=0;tx-mode=SRST"
 
 
+def av1_fmtp(level_idx: int = 8) -> str:
+    """AV1 RTP fmtp: Main profile, Main tier (level_idx 8 = 4.0; the sequence header
+    carries the real level)."""
+    return f"level-idx={level_idx};profile=0;tier=0"
+
+
 def build_offer(ufrag: str, pwd: str, fingerprint: str, candidates: list, video_ssrc: int, audio_ssrc: int,
                 video: bool = True, audio: bool = True, data: bool = True, cname: str = "selkies",
                 ice_lite: bool = False, profile_level_id: str = "42e01f",
@@ -236,6 +243,8 @@ def build_offer(ufrag: str, pwd: str, fingerprint: str, candidates: list, video_
     if video:
         if video_codec.upper() in ("H265", "HEVC"):
             pt, rtpmap, fmtp = H265_PT, "H265/90000", h265_fmtp()
+        elif video_codec.upper() == "AV1":
+            pt, rtpmap, fmtp = AV1_PT, "AV1/90000", av1_fmtp()
         else:
             pt, rtpmap, fmtp = H264_PT, "H264/90000", h264_fmtp(profile_level_id)
         fmts, rtpmaps = [pt], {pt: rtpmap}

@@ -96,3 +96,30 @@ def test_static_content_collapses_to_skip_superblocks():
 def test_1080p_frames():
     res = run(1920, 1080, "motion", 2, qp=25)
     assert res[0][2] > 34 and res[1][1] < res[0][1] / 4
+
+
+@pytest.mark.parametrize("mtu", [1200, 300])
+def test_av1_rtp_roundtrip(mtu):
+    """rtc_av1_packetize (csrc/rtc/rtc.cpp, AV1 RTP payload format) -> AV1Depacketizer
+    (webrtc/rtp.py) rebuilds every temporal unit byte for byte; fragments at a small
+    MTU; N only on the key frame's first packet; marker on the last packet."""
+    from selkies_gstreamer_amd.webrtc import rtp
+    from selkies_gstreamer_amd.webrtc.native import RtpPacketizer
+    W, H = 320, 192
+    src = SyntheticDesktop(W, H, kind="motion")
+    enc = Av1Encoder(W, H, backend="cpu")
+    pk = RtpPacketizer(ssrc=1234, payload_type=96, mtu=mtu)
+    dep = rtp.AV1Depacketizer()
+    for t in range(4):
+        (p,) = enc.encode(src.frame(t), t)
+        tu = p.data[10:]
+        pkts = pk.av1(tu, 3000 * t)
+        assert pkts and all(len(x) <= mtu for x in pkts)
+        hdrs = [rtp.parse_rtp(x) for x in pkts]
+        assert [h.marker for h in hdrs] == [False] * (len(pkts) - 1) + [True]
+        aggs = [x[h.header_len] for x, h in zip(pkts, hdrs)]
+        assert bool(aggs[0] & 0x08) == p.key and not any(a & 0x08 for a in aggs[1:])
+        out = None
+        for x, h in zip(pkts, hdrs):
+            out = dep.push(x[h.header_len:], h.timestamp, h.marker)
+        assert out == tu

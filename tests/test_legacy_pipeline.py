@@ -39,10 +39,18 @@ def test_audio_branch_and_region():
     assert a.audio and a.audio_device == "output.monitor" and a.audio_bitrate == 128000 and a.audio_frame_ms == 10
 
 
-@pytest.mark.parametrize("enc", ["vp8enc", "vp9enc", "svtav1enc", "nvav1enc"])
+@pytest.mark.parametrize("enc", ["vp8enc", "vp9enc", "vavp9enc"])
 def test_unsupported_codecs_are_explicit(enc):
     with pytest.raises(PipelineError, match="H.264"):
         parse_pipeline(f"ximagesrc ! videoconvert ! {enc} ! fakesink")
+
+
+@pytest.mark.parametrize("enc,prop,val,kbps", [("svtav1enc", "target-bitrate", 6000, 6000),
+                                               ("rav1enc", "bitrate", 6000000, 6000),
+                                               ("nvav1enc", "bitrate", 6000, 6000)])
+def test_av1_encoders_map_to_hip_av1(enc, prop, val, kbps):
+    s = parse_pipeline(f"ximagesrc ! videoconvert ! {enc} {prop}={val} ! rtpav1pay mtu=1200")
+    assert (s.encoder, s.encoder_element, s.bitrate_kbps, s.mtu) == ("av1", enc, kbps, 1200)
 
 
 def test_syntax_errors():

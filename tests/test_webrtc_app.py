@@ -25,14 +25,18 @@ class _RecordingInput:
         pass
 
 
-@pytest.mark.parametrize("backend", ["cpu", pytest.param("hip", marks=pytest.mark.gpu)])
-def test_legacy_webrtc_session(tmp_path, backend):
-    """backend=hip runs the same session on the MI355X encoder (native HIP path, 640x368)."""
+@pytest.mark.parametrize("backend,encoder", [("cpu", "x264enc"), ("cpu", "svtav1enc"),
+                                             pytest.param("hip", "x264enc", marks=pytest.mark.gpu),
+                                             pytest.param("hip", "svtav1enc", marks=pytest.mark.gpu)])
+def test_legacy_webrtc_session(tmp_path, backend, encoder):
+    """backend=hip runs the same session on the MI355X encoder (native HIP path, 640x368);
+    encoder=svtav1enc carries AV1 over RTP (rtpav1pay payload format) and the viewer's
+    temporal units are decoded by dav1d."""
     W, H = (256, 128) if backend == "cpu" else (640, 368)
     args = webrtc_app.parse_args(
         ["--port", "0", "--enable_basic_auth", "false", "--use_cpu", str(backend == "cpu").lower(),
          "--capture_source", "synthetic", "--json_config", str(tmp_path / "cfg.json"),
-         "--rtc_config_json", str(tmp_path / "none.json"), "--framerate", "20",
+         "--rtc_config_json", str(tmp_path / "none.json"), "--framerate", "20", "--encoder", encoder,
          "--initial_resolution", f"{W}x{H}", "--turn_shared_secret", ""], env={})
     rec = _RecordingInput()
 
@@ -71,11 +75,19 @@ def test_legacy_webrtc_session(tmp_path, backend):
                 break
             await asyncio.sleep(0.05)
         assert len(frames) >= 5, "no video over SRTP"
-        dec = H264Decoder()
-        out = []
-        for au in frames[:3]:
-            out += dec.decode(au)
-        assert out and out[0][0].shape == (H, W) and dec.stats["idr"] >= 1
+        if encoder == "svtav1enc":
+            from selkies_gstreamer_amd.models.av1 import dav1d
+            assert frames[0][:2] == b"\x12\x00"          # temporal unit rebuilt by AV1Depacketizer
+            if dav1d.available():
+                d = dav1d.Decoder()
+                y, u, v = d.decode(frames[0])
+                assert y.shape == (H, W)
+        else:
+            dec = H264Decoder()
+            out = []
+            for au in frames[:3]:
+                out += dec.decode(au)
+            assert out and out[0][0].shape == (H, W) and dec.stats["idr"] >= 1
         sysmsgs = [json.loads(m) for m in msgs]
         assert {"type": "system", "data": {"action": "framerate,20"}} in sysmsgs
         ch = chans[0]
