@@ -7,7 +7,8 @@
 // Coding structure (fixed by the parameter sets in hevc_syntax.cpp):
 //   CTB = CU = 16x16 (log2 min CB 4, no split flags), PU 2Nx2N, TU = CU (16x16 luma,
 //   8x8 chroma, no transform split), one reference picture (previous picture),
-//   integer-pel motion, no deblocking / SAO / sign hiding / transform skip,
+//   integer-pel motion, deblocking on (CU edges, deblock_picture), no SAO / sign hiding /
+//   transform skip,
 //   entropy_coding_sync (WPP): one CABAC substream per CTB row, slices = stripes of
 //   whole CTB rows.
 // Decoder-side operations (inverse transform, dequantisation, intra prediction,
@@ -857,6 +858,111 @@ SK_HD void code_cu(W& w, const CuInfo& cu, const int16_t* coef, bool p_slice, in
     if (cbf_y) code_residual(w, coef, 4, 0);
     if (cbf_cb) code_residual(w, coef + kCoefCb, 3, 1);
     if (cbf_cr) code_residual(w, coef + kCoefCr, 3, 2);
+}
+
+// ---------------------------------------------------------------------------
+// Deblocking (8.7.2), for this coding structure: CU = PU = TU = 16x16, so the
+// filtered luma edges are the CU boundaries (every 16 samples), one boundary
+// strength per CU edge, and the chroma edges (bS 2 only) are the same boundaries
+// on the 8-sample chroma grid. Edges at the picture border and between slices
+// (pps_loop_filter_across_slices_enabled_flag = 0) are not filtered. All vertical
+// edges of the picture first, then the horizontal ones on their output.
+SK_TABLE uint8_t HEVC_BETA[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+                                  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
+                                  34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};   // Table 8-11 beta'
+SK_TABLE uint8_t HEVC_TC[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  1,  1,  1,  1,  1,  1,  1, 1, 1,
+                                2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+
+// Boundary strength between the CUs on the two sides of an edge (8.7.2.4).
+SK_HD int dbk_bs(const CuInfo& p, const CuInfo& q) {
+    if (p.mode == CU_INTRA || q.mode == CU_INTRA) return 2;
+    if ((p.cbf | q.cbf) & 1) return 1;   // a luma transform block with coefficients
+    const int dx = p.mvx - q.mvx, dy = p.mvy - q.mvy;   // one reference picture: motion only
+    return (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
+}
+
+// One 4-line luma segment (8.7.2.5.3 decisions, 8.7.2.5.7 filtering). q: the q0
+// sample of line 0; step: q0 -> q1 (1 across a vertical edge, the stride across a
+// horizontal one); along: line 0 -> line 1.
+SK_HD void dbk_luma_segment(uint8_t* q, int step, int along, int bs, int qp) {
+    const int beta = HEVC_BETA[sk_clip(qp, 0, 51)];
+    const int tc = HEVC_TC[sk_clip(qp + 2 * (bs - 1), 0, 53)];
+    auto P = [&](int ln, int i) -> int { return q[ln * along - (i + 1) * step]; };
+    auto Q = [&](int ln, int i) -> int { return q[ln * along + i * step]; };
+    const int dp0 = sk_abs(P(0, 2) - 2 * P(0, 1) + P(0, 0)), dp3 = sk_abs(P(3, 2) - 2 * P(3, 1) + P(3, 0));
+    const int dq0 = sk_abs(Q(0, 2) - 2 * Q(0, 1) + Q(0, 0)), dq3 = sk_abs(Q(3, 2) - 2 * Q(3, 1) + Q(3, 0));
+    const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3;
+    if (dpq0 + dpq3 >= beta) return;
+    auto strong = [&](int ln, int dpq) {
+        return 2 * dpq < (beta >> 2) && sk_abs(P(ln, 3) - P(ln, 0)) + sk_abs(Q(ln, 0) - Q(ln, 3)) < (beta >> 3) &&
+               sk_abs(P(ln, 0) - Q(ln, 0)) < ((5 * tc + 1) >> 1);
+    };
+    const bool de2 = strong(0, dpq0) && strong(3, dpq3);
+    const bool dep = dp < ((beta + (beta >> 1)) >> 3), deq = dq < ((beta + (beta >> 1)) >> 3);
+    for (int ln = 0; ln < 4; ln++) {
+        uint8_t* o = q + ln * along;
+        const int p0 = P(ln, 0), p1 = P(ln, 1), p2 = P(ln, 2), p3 = P(ln, 3);
+        const int q0 = Q(ln, 0), q1 = Q(ln, 1), q2 = Q(ln, 2), q3 = Q(ln, 3);
+        if (de2) {
+            const int t2 = 2 * tc;
+            o[-1 * step] = (uint8_t)sk_clip((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, p0 - t2, p0 + t2);
+            o[-2 * step] = (uint8_t)sk_clip((p2 + p1 + p0 + q0 + 2) >> 2, p1 - t2, p1 + t2);
+            o[-3 * step] = (uint8_t)sk_clip((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, p2 - t2, p2 + t2);
+            o[0] = (uint8_t)sk_clip((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, q0 - t2, q0 + t2);
+            o[step] = (uint8_t)sk_clip((p0 + q0 + q1 + q2 + 2) >> 2, q1 - t2, q1 + t2);
+            o[2 * step] = (uint8_t)sk_clip((p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3, q2 - t2, q2 + t2);
+        } else {
+            int d = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
+            if (sk_abs(d) >= tc * 10) continue;
+            d = sk_clip(d, -tc, tc);
+            o[-step] = (uint8_t)sk_clip255(p0 + d);
+            o[0] = (uint8_t)sk_clip255(q0 - d);
+            if (dep) o[-2 * step] = (uint8_t)sk_clip255(p1 + sk_clip((((p2 + p0 + 1) >> 1) - p1 + d) >> 1, -(tc >> 1), tc >> 1));
+            if (deq) o[step] = (uint8_t)sk_clip255(q1 + sk_clip((((q2 + q0 + 1) >> 1) - q1 - d) >> 1, -(tc >> 1), tc >> 1));
+        }
+    }
+}
+
+// One chroma line across an edge with bS 2 (8.7.2.5.5); qp: the luma QP average.
+SK_HD void dbk_chroma_line(uint8_t* q, int step, int qp) {
+    const int tc = HEVC_TC[sk_clip(chroma_qp(sk_clip(qp, 0, 57)) + 2, 0, 53)];
+    const int p0 = q[-step], p1 = q[-2 * step], q0 = q[0], q1 = q[step];
+    const int d = sk_clip((((q0 - p0) * 4) + p1 - q1 + 4) >> 3, -tc, tc);
+    q[-step] = (uint8_t)sk_clip255(p0 + d);
+    q[0] = (uint8_t)sk_clip255(q0 - d);
+}
+
+// The whole picture (CPU reference; k_hevc_dbk_v / k_hevc_dbk_h are the same loops in
+// parallel). cus: [ctb_h][ctb_w]; rows_per_slice: CTB rows per slice.
+SK_HD void deblock_picture(uint8_t* Y, uint8_t* U, uint8_t* V, int sy, int sc, const CuInfo* cus, int ctb_w,
+                           int ctb_h, int rows_per_slice) {
+    for (int cy = 0; cy < ctb_h; cy++)   // vertical edges
+        for (int cx = 1; cx < ctb_w; cx++) {
+            const CuInfo &p = cus[cy * ctb_w + cx - 1], &q = cus[cy * ctb_w + cx];
+            const int bs = dbk_bs(p, q), qp = (p.qp + q.qp + 1) >> 1;
+            if (!bs) continue;
+            for (int k = 0; k < 4; k++)
+                dbk_luma_segment(Y + (size_t)(cy * 16 + 4 * k) * sy + cx * 16, 1, sy, bs, qp);
+            if (bs == 2)
+                for (int l = 0; l < 8; l++) {
+                    dbk_chroma_line(U + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
+                    dbk_chroma_line(V + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
+                }
+        }
+    for (int cy = 1; cy < ctb_h; cy++) {   // horizontal edges (not between slices)
+        if (cy % rows_per_slice == 0) continue;
+        for (int cx = 0; cx < ctb_w; cx++) {
+            const CuInfo &p = cus[(cy - 1) * ctb_w + cx], &q = cus[cy * ctb_w + cx];
+            const int bs = dbk_bs(p, q), qp = (p.qp + q.qp + 1) >> 1;
+            if (!bs) continue;
+            for (int k = 0; k < 4; k++) dbk_luma_segment(Y + (size_t)(cy * 16) * sy + cx * 16 + 4 * k, sy, 1, bs, qp);
+            if (bs == 2)
+                for (int l = 0; l < 8; l++) {
+                    dbk_chroma_line(U + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
+                    dbk_chroma_line(V + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
+                }
+        }
+    }
 }
 
 }  // namespace hevc

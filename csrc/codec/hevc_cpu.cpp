@@ -346,6 +346,9 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
     }
     fe.ctl_.rate_account(8 * payload_bytes_);   // K10: substream payload (k_rc_account: sub_size)
     out.push_back(std::move(pk));
+    // in-loop deblocking of the reconstruction before it becomes the reference
+    deblock_picture(fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data(), fe.g.stride_y, fe.g.stride_c, cus.data(),
+                    geo.ctb_w, geo.ctb_h, geo.rows_per_slice);
     fe.finish_frame();
     poc++;
 }

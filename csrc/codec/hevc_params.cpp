@@ -178,7 +178,9 @@ void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<u
         p.put1(0);            // pps_loop_filter_across_slices_enabled_flag
         p.put1(1);            // deblocking_filter_control_present_flag
         p.put1(0);            // deblocking_filter_override_enabled_flag
-        p.put1(1);            // pps_deblocking_filter_disabled_flag
+        p.put1(0);            // pps_deblocking_filter_disabled_flag: deblocking on (hevc_core.h)
+        p.se(0);              // pps_beta_offset_div2
+        p.se(0);              // pps_tc_offset_div2
         p.put1(0);            // pps_scaling_list_data_present_flag
         p.put1(0);            // lists_modification_present_flag
         p.ue(0);              // log2_parallel_merge_level_minus2

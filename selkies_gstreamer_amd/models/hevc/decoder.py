@@ -11,8 +11,10 @@ luma and 4-tap chroma interpolation, scaling, inverse DCT/DST, reconstruction).
 Supported: Main 8-bit 4:2:0, any CTB/CB/TB sizes with quadtree splits, PART_2Nx2N
 CUs (intra and inter), I and P slices with one reference list, multiple slices,
 entropy_coding_sync (WPP) substreams. NotImplementedError for the rest (B slices,
-tiles, AMP/NxN partitions, PCM, transform skip, scaling lists, SAO, deblocking,
-TMVP, long-term references, sign data hiding, cu_qp_delta).
+tiles, AMP/NxN partitions, PCM, transform skip, scaling lists, SAO, TMVP, long-term
+references, sign data hiding, cu_qp_delta). The deblocking filter (8.7.2) runs on the
+completed picture: transform / prediction block edges on the 8x8 grid, boundary
+strength, luma decisions and strong / normal filters, chroma on bS 2.
 
 Written from the specification text, not from the encoder's tables; numpy for the
 sample processes, plain Python for parsing. Intended for test-sized pictures.
@@ -316,6 +318,8 @@ class Pps:
     loop_filter_across_slices: bool = False
     deblock_override: bool = False
     deblock_disabled: bool = False
+    beta_offset: int = 0
+    tc_offset: int = 0
     lists_modification: bool = False
     log2_par_mrg: int = 2
     slice_header_ext: bool = False
@@ -430,7 +434,7 @@ class HevcDecoder:
             p.deblock_override = bool(b.u(1))
             p.deblock_disabled = bool(b.u(1))
             if not p.deblock_disabled:
-                b.se(); b.se()
+                p.beta_offset, p.tc_offset = 2 * b.se(), 2 * b.se()
         if b.u(1):
             raise NotImplementedError("PPS scaling lists")
         p.lists_modification = bool(b.u(1))
@@ -469,6 +473,8 @@ class HevcDecoder:
 
     def _finish_picture(self):
         s = self.sps
+        if any(v[0] for v in self.cur["dbk_slices"].values()):
+            self._deblock()
         Y, U, V = self.cur["Y"], self.cur["U"], self.cur["V"]
         self.ref = (Y.copy(), U.copy(), V.copy())
         self.cur = None
@@ -476,6 +482,13 @@ class HevcDecoder:
         return (Y[2 * ct:s.height - 2 * cb, 2 * cl:s.width - 2 * cr].copy(),
                 U[ct:s.height // 2 - cb, cl:s.width // 2 - cr].copy(),
                 V[ct:s.height // 2 - cb, cl:s.width // 2 - cr].copy())
+
+    def _deblock(self):
+        c = self.cur
+        c["cb_off"], c["cr_off"] = self.pps.cb_qp_offset, self.pps.cr_qp_offset
+        planes = (c["Y"], c["U"], c["V"])
+        _deblock_pass(c, planes, True, c["dbk_slices"])
+        _deblock_pass(c, planes, False, c["dbk_slices"])
 
     def _new_picture(self):
         s = self.sps
@@ -492,6 +505,13 @@ class HevcDecoder:
             "ipm": np.ones((s.height // 4, s.width // 4), np.int64),
             "mv": np.zeros((s.height // 4, s.width // 4, 2), np.int64),
             "depth": np.zeros((s.height // 4, s.width // 4), np.int64),
+            # deblocking side info per 4x4 block: transform / prediction edge on the left / top
+            # boundary, luma cbf of the transform block, QpY
+            "ev": np.zeros((s.height // 4, s.width // 4), bool),
+            "eh": np.zeros((s.height // 4, s.width // 4), bool),
+            "cbf": np.zeros((s.height // 4, s.width // 4), bool),
+            "qp": np.zeros((s.height // 4, s.width // 4), np.int64),
+            "dbk_slices": {},
         }
         del nmin
 
@@ -560,12 +580,16 @@ class HevcDecoder:
         if p.slice_chroma_qp_offsets:
             b.se(); b.se()
         deblock_disabled = p.deblock_disabled
+        beta_off, tc_off = p.beta_offset, p.tc_offset
         if p.deblock_override and b.u(1):
             deblock_disabled = bool(b.u(1))
             if not deblock_disabled:
-                b.se(); b.se()
-        if not deblock_disabled:
-            raise NotImplementedError("deblocking filter")
+                beta_off, tc_off = 2 * b.se(), 2 * b.se()
+        across = p.loop_filter_across_slices
+        if p.loop_filter_across_slices and not deblock_disabled:
+            across = bool(b.u(1))
+        # per-slice deblocking parameters, looked up by the slice map at filtering time
+        self.cur["dbk_slices"][addr] = (not deblock_disabled, beta_off, tc_off, across)
         entry = []
         if p.tiles or p.wpp:
             n = b.ue()
@@ -686,6 +710,8 @@ class HevcDecoder:
     def _coding_unit(self, x0, y0, log2, depth):
         s = self.sps
         n = 1 << log2
+        self._block_edges(x0, y0, n)
+        self._mark(x0, y0, n, qp=self.qp, cbf=0)
         skip = 0
         if self.slice_type != 2:
             cond = 0
@@ -930,9 +956,16 @@ class HevcDecoder:
             return qpi - 6
         return QPC_TABLE[qpi]
 
+    def _block_edges(self, x0, y0, n):
+        c = self.cur
+        c["ev"][y0 >> 2:(y0 + n) >> 2, x0 >> 2] = True
+        c["eh"][y0 >> 2, x0 >> 2:(x0 + n) >> 2] = True
+
     def _transform_unit(self, x0, y0, xb, yb, log2, blk, cbf_y, cbf_cb, cbf_cr, intra):
         p = self.pps
         n = 1 << log2
+        self._block_edges(x0, y0, n)
+        self._mark(x0, y0, n, cbf=bool(cbf_y))
         mode, cmode = self.cu_intra if intra else (None, None)
         if intra:
             self._intra_pred("Y", x0, y0, n, mode, 0)
@@ -1220,6 +1253,117 @@ class HevcDecoder:
         # mark the TU decoded for later intra neighbours (luma drives availability)
         if cidx == 0:
             self._mark(x0, y0, n, slice=self.slice_addr)
+
+
+BETA_TABLE = [0] * 16 + [6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32, 34, 36, 38, 40,
+                          42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64]                      # Table 8-11 (beta')
+TC_TABLE = [0] * 18 + [1] * 9 + [2] * 4 + [3] * 4 + [4] * 3 + [5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24]
+
+
+def _qpc(qpi: int) -> int:
+    qpi = min(max(qpi, 0), 57)
+    return qpi if qpi < 30 else (qpi - 6 if qpi > 43 else QPC_TABLE[qpi])
+
+
+def _deblock_pass(c: dict, planes: tuple, vertical: bool, slices: dict) -> None:
+    """One direction of 8.7.2 over the whole picture (all edges of a direction are
+    independent: 8 samples apart, at most 3 samples changed per side)."""
+    Y, U, V = planes
+    edge = c["ev"] if vertical else c["eh"]
+    sl, intra, cbf, mv, qp = c["slice"], c["intra"], c["cbf"], c["mv"], c["qp"]
+    h4, w4 = edge.shape
+    yq, xq = np.nonzero(edge)
+    keep = (xq % 2 == 0) & (xq > 0) if vertical else (yq % 2 == 0) & (yq > 0)   # 8x8 grid, not the border
+    yq, xq = yq[keep], xq[keep]
+    yp, xp = (yq, xq - 1) if vertical else (yq - 1, xq)
+    sq, sp = sl[yq, xq], sl[yp, xp]
+    # filterEdgeFlag: slice boundaries only where the q slice allows filtering across
+    ok = np.array([bool(slices.get(int(a), (True, 0, 0, False))[0]) for a in sq], bool)
+    across = np.array([bool(slices.get(int(a), (True, 0, 0, False))[3]) for a in sq], bool)
+    ok &= (sq == sp) | across
+    bs = np.where(intra[yq, xq] | intra[yp, xp], 2,
+                  np.where(cbf[yq, xq] | cbf[yp, xp], 1,
+                           np.where((np.abs(mv[yq, xq] - mv[yp, xp]) >= 4).any(axis=-1), 1, 0)))
+    bs = np.where(ok, bs, 0)
+    qpl = (qp[yq, xq] + qp[yp, xp] + 1) >> 1
+    beta_off = np.array([slices.get(int(a), (True, 0, 0, False))[1] for a in sq], np.int64)
+    tc_off = np.array([slices.get(int(a), (True, 0, 0, False))[2] for a in sq], np.int64)
+    sel = bs > 0
+    # ---- luma: 4-line segments
+    if sel.any():
+        yy, xx, b, q, bo, to = yq[sel], xq[sel], bs[sel], qpl[sel], beta_off[sel], tc_off[sel]
+        beta = np.array(BETA_TABLE)[np.clip(q + bo, 0, 51)]
+        tc = np.array(TC_TABLE)[np.clip(q + 2 * (b - 1) + to, 0, 53)]
+        ln = np.arange(4)
+        off = np.arange(-4, 4)
+        if vertical:
+            rows = (yy * 4)[:, None, None] + ln[None, :, None]
+            cols = (xx * 4)[:, None, None] + off[None, None, :]
+        else:
+            rows = (yy * 4)[:, None, None] + off[None, None, :]
+            cols = (xx * 4)[:, None, None] + ln[None, :, None]
+        blk = Y[rows, cols].astype(np.int64)          # [seg, line, p3 p2 p1 p0 q0 q1 q2 q3]
+        p3, p2, p1, p0, q0, q1, q2, q3 = (blk[:, :, k] for k in range(8))
+        dp = np.abs(p2 - 2 * p1 + p0)
+        dq = np.abs(q2 - 2 * q1 + q0)
+        dpq0, dpq3 = dp[:, 0] + dq[:, 0], dp[:, 3] + dq[:, 3]
+        on = (dpq0 + dpq3) < beta
+
+        def strong(k, dpq):
+            return ((2 * dpq < (beta >> 2)) & (np.abs(p3[:, k] - p0[:, k]) + np.abs(q0[:, k] - q3[:, k]) < (beta >> 3))
+                    & (np.abs(p0[:, k] - q0[:, k]) < ((5 * tc + 1) >> 1)))
+        de2 = strong(0, dpq0) & strong(3, dpq3)
+        side = (beta + (beta >> 1)) >> 3
+        dep = (dp[:, 0] + dp[:, 3]) < side
+        deq = (dq[:, 0] + dq[:, 3]) < side
+        t = tc[:, None]
+        out = blk.copy()
+        # strong filter
+        s2 = (on & de2)[:, None]
+        t2 = 2 * t
+        new = {
+            3: np.clip((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, p0 - t2, p0 + t2),
+            2: np.clip((p2 + p1 + p0 + q0 + 2) >> 2, p1 - t2, p1 + t2),
+            1: np.clip((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, p2 - t2, p2 + t2),
+            4: np.clip((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, q0 - t2, q0 + t2),
+            5: np.clip((p0 + q0 + q1 + q2 + 2) >> 2, q1 - t2, q1 + t2),
+            6: np.clip((p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3, q2 - t2, q2 + t2),
+        }
+        for k, v in new.items():
+            out[:, :, k] = np.where(s2, v, out[:, :, k])
+        # normal filter
+        d = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4
+        nrm = (on & ~de2)[:, None] & (np.abs(d) < t * 10)
+        d = np.clip(d, -t, t)
+        out[:, :, 3] = np.where(nrm, np.clip(p0 + d, 0, 255), out[:, :, 3])
+        out[:, :, 4] = np.where(nrm, np.clip(q0 - d, 0, 255), out[:, :, 4])
+        th = t >> 1
+        dpv = np.clip((((p2 + p0 + 1) >> 1) - p1 + d) >> 1, -th, th)
+        dqv = np.clip((((q2 + q0 + 1) >> 1) - q1 - d) >> 1, -th, th)
+        out[:, :, 2] = np.where(nrm & dep[:, None], np.clip(p1 + dpv, 0, 255), out[:, :, 2])
+        out[:, :, 5] = np.where(nrm & deq[:, None], np.clip(q1 + dqv, 0, 255), out[:, :, 5])
+        Y[rows, cols] = out.astype(np.uint8)
+    # ---- chroma (4:2:0): bS 2 edges on the 8x8 chroma grid, i.e. every 16 luma samples
+    csel = (bs == 2) & (((xq if vertical else yq) % 4) == 0)
+    if csel.any():
+        yy, xx, q, to = yq[csel], xq[csel], qpl[csel], tc_off[csel]
+        ln = np.arange(2)                            # a 4-sample luma segment = 2 chroma lines
+        off = np.arange(-2, 2)
+        for P, cqoff in ((U, c["cb_off"]), (V, c["cr_off"])):
+            tc = np.array(TC_TABLE)[np.clip(np.array([_qpc(int(v) + cqoff) for v in q]) + 2 + to, 0, 53)]
+            if vertical:
+                rows = (yy * 2)[:, None, None] + ln[None, :, None]
+                cols = (xx * 2)[:, None, None] + off[None, None, :]
+            else:
+                rows = (yy * 2)[:, None, None] + off[None, None, :]
+                cols = (xx * 2)[:, None, None] + ln[None, :, None]
+            blk = P[rows, cols].astype(np.int64)
+            p1, p0, q0, q1 = (blk[:, :, k] for k in range(4))
+            t = tc[:, None]
+            d = np.clip((((q0 - p0) * 4) + p1 - q1 + 4) >> 3, -t, t)
+            blk[:, :, 1] = np.clip(p0 + d, 0, 255)
+            blk[:, :, 2] = np.clip(q0 - d, 0, 255)
+            P[rows, cols] = blk.astype(np.uint8)
 
 
 def psnr(a: np.ndarray, b: np.ndarray) -> float:
