@@ -78,10 +78,12 @@ def test_legacy_webrtc_session(tmp_path, backend, encoder):
         if encoder == "svtav1enc":
             from selkies_gstreamer_amd.models.av1 import dav1d
             assert frames[0][:2] == b"\x12\x00"          # temporal unit rebuilt by AV1Depacketizer
+            keys = [i for i, f in enumerate(frames) if len(f) > 2 and (f[2] >> 3) & 15 == 1]   # sequence header
+            assert keys, "no key frame received"
             if dav1d.available():
                 d = dav1d.Decoder()
-                y, u, v = d.decode(frames[0])
-                assert y.shape == (H, W)
+                pics = [d.decode(f) for f in frames[keys[0]:]]
+                assert pics[0] is not None and pics[0][0].shape == (H, W)
         else:
             dec = H264Decoder()
             out = []
