@@ -139,3 +139,19 @@ std::unique_ptr<FrameSource> make_pool_source(const uint8_t* base, int frames, i
 }
 
 }  // namespace sk
+
+extern "C" {
+// Frame t (0-based) of the capture sessions' synthetic source (kind 0 motion, 1 desktop,
+// 2 noise; the session seed), BGRx into out[h][w]: tests compare decoded frames against
+// exactly what a session encoded as frame t.
+int sk_synthetic_render(int w, int h, int kind, int t, uint8_t* out) {
+    if (w <= 0 || h <= 0 || t < 0 || !out) return -1;
+    auto src = sk::make_synthetic_source(w, h, kind, 0x1234567u);
+    int stride = 0;
+    const uint8_t* f = nullptr;
+    for (int i = 0; i <= t; i++) f = src->grab(&stride);
+    for (int y = 0; y < h; y++) memcpy(out + (size_t)y * w * 4, f + (size_t)y * stride, (size_t)w * 4);
+    return 0;
+}
+}
+

@@ -13,9 +13,18 @@ import pytest
 from selkies_gstreamer_amd.ops.native import hip_device_count
 from selkies_gstreamer_amd.server.data_server import DataStreamingServer
 from selkies_gstreamer_amd.server.settings import Settings
-from tests.h264_util import StripeDecoder
+from tests.h264_util import StripeDecoder, bgrx_to_y709, psnr
 
 pytestmark = pytest.mark.gpu
+
+
+def _native():
+    import ctypes
+    from selkies_gstreamer_amd.ops import native
+    L = native.lib()
+    L.sk_synthetic_render.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p]
+    L.sk_synthetic_render.restype = ctypes.c_int
+    return L
 
 
 @pytest.fixture(autouse=True)
@@ -79,6 +88,13 @@ def test_hip_session_decodes(tmp_path, W, H, encoder):
                     for d in pkts:
                         dec.feed(d)
                     assert dec.Y.std() > 5.0
+                    # the picture after the last fed frame against the exact frame the session
+                    # captured (the native synthetic source, rendered again for that frame id)
+                    fid = int.from_bytes(pkts[-1][2:4], "big")
+                    ref = np.empty((H, W, 4), np.uint8)
+                    assert _native().sk_synthetic_render(W, H, 0, fid, ref.ctypes.data) == 0
+                    q = psnr(dec.Y, bgrx_to_y709(ref))
+                    assert q > 30.0, f"decoded frame {fid}: {q:.2f} dB against its source"
                     assert lat, "no FRAME_TS traces"
                     # capture -> receive must be a few frame intervals at most on one host
                     assert float(np.median(lat)) < 100.0, lat
