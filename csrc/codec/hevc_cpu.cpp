@@ -2,8 +2,11 @@
 // (kernels/hevc_kernels.hip produces the same CU decisions, levels, reconstruction,
 // bins and bytes) and the `use_cpu` path.
 #include "hevc_encoder.h"
+#include "hevc_pcabac.h"
+#include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <stdexcept>
 
 namespace sk {
 namespace hevc {
@@ -52,6 +55,76 @@ void intra_predict(const uint8_t* ref_raw, int log2n, int mode, int cidx, uint8_
     }
     for (int y = 0; y < n; y++)
         for (int x = 0; x < n; x++) pred[y * n + x] = (uint8_t)intra_pred_sample(ref, n, log2n, mode, cidx, x, y);
+}
+
+// Host model of the chunk-parallel substream coder (hevc_pcabac.h), chunk = CTB: the
+// same four phases the HIP back end runs, sequentially. `cu` lists each CTB's bin
+// entries (the row's terminating end_of_subset bin included in the last).
+std::vector<uint8_t> pc_code_row_host(const std::vector<std::vector<uint16_t>>& cu, const uint8_t* init_ctx) {
+    const int nc = (int)cu.size();
+    // 1. context modelling (the GPU runs one chain per context; the states are the same)
+    std::vector<std::vector<uint16_t>> mod(cu);
+    uint8_t ctx[CTX_COUNT];
+    memcpy(ctx, init_ctx, CTX_COUNT);
+    for (auto& v : mod)
+        for (auto& e : v)
+            if ((e & 0x80ffu) < (uint32_t)CTX_TERM) e = pc_model(ctx[e & 0xffu], (e >> 8) & 1);
+    // 2. range maps: end range | shifts << 9 for every start range 256..511
+    std::vector<uint32_t> map((size_t)nc * 256);
+    for (int j = 0; j < nc; j++)
+        for (uint32_t r0 = 256; r0 < 512; r0++) {
+            uint32_t r = r0, k = 0;
+            for (uint16_t e : mod[j]) k += (uint32_t)pc_range_step(e, r);
+            map[(size_t)j * 256 + r0 - 256] = r | (k << 9);
+        }
+    // 3. composition: start range and stream bit offset of every chunk
+    std::vector<uint32_t> r0(nc), t0(nc + 1);
+    uint32_t r = 510, t = 0;
+    for (int j = 0; j < nc; j++) {
+        r0[j] = r;
+        t0[j] = t;
+        const uint32_t m = map[(size_t)j * 256 + r - 256];
+        r = m & 511;
+        t += m >> 9;
+    }
+    t0[nc] = t;   // T_f
+    // 4. chunk coding: exclusive bytes in place, the 2 overlapping bytes as a tail
+    std::vector<uint8_t> out((t >> 3) + 2, 0);
+    std::vector<uint32_t> tail(nc, 0);
+    for (int j = 0; j < nc; j++) {
+        const int g0 = (int)(t0[j] >> 3), gn = (int)(t0[j + 1] >> 3);
+        int pos = 0;
+        uint32_t tl = 0;
+        auto emit = [&](uint32_t b) {
+            const int g = g0 + pos++;
+            if (g < gn) out[g] = (uint8_t)b;
+            else if (g - gn < 2) tl |= b << (8 * (g - gn));
+            else throw std::logic_error("pcabac: chunk overran its tail");
+        };
+        PcCoder c;
+        c.start(r0[j], (int)(t0[j] & 7));
+        for (uint16_t e : mod[j]) c.code(e, emit);
+        c.flush(emit);
+        if (g0 + pos != gn + 2) throw std::logic_error("pcabac: chunk byte count");
+        tail[j] = tl;
+    }
+    // merge: add every tail (big-endian 16 bits at its byte) with carries toward the start
+    for (int j = 0; j < nc; j++) {
+        const int p = (int)(t0[j + 1] >> 3);
+        uint32_t v = ((uint32_t)out[p] << 8 | out[p + 1]) + ((tail[j] & 0xff) << 8 | (tail[j] >> 8));
+        out[p + 1] = (uint8_t)v;
+        out[p] = (uint8_t)(v >> 8);
+        for (int q = p - 1; (v >> 16) && q >= 0; q--) {
+            v = (uint32_t)out[q] + 1;
+            out[q] = (uint8_t)v;
+            v <<= 8;
+        }
+    }
+    // stream bits 0..T_f, the rbsp stop bit, zero alignment
+    const uint32_t sb = t + 1;
+    out[sb >> 3] = (uint8_t)((out[sb >> 3] & (0xff00u >> (sb & 7))) | (0x80u >> (sb & 7)));
+    out.resize((sb >> 3) + 1);
+    return out;
 }
 
 CpuHevcEncoder::CpuHevcEncoder(const h264::EncoderConfig& cfg) : fe(front_config(cfg)) {
@@ -269,6 +342,23 @@ std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
         uint8_t ctx[CTX_COUNT];
         if (r == 0 || geo.ctb_w < 2) ctx_init_all(ctx, p_slice ? 1 : 0, t.qp);
         else memcpy(ctx, sync, CTX_COUNT);
+        if (pc_host_) {   // chunk-parallel model (hevc_pcabac.h), must give the same bytes
+            std::vector<std::vector<uint16_t>> cu(geo.ctb_w);
+            for (int cx = 0; cx < geo.ctb_w; cx++) {
+                const uint16_t* b = &bins[(size_t)(cy * geo.ctb_w + cx) * kCuBinCap];
+                cu[cx].assign(b, b + bin_n[cy * geo.ctb_w + cx]);
+            }
+            if (r + 1 < rows) cu.back().push_back((uint16_t)((1u << 8) | CTX_TERM));   // end_of_subset_one_bit
+            sub[r] = pc_code_row_host(cu, ctx);
+            for (int cx = 0; cx < 2 && cx < geo.ctb_w; cx++)
+                for (int i = 0; i < bin_n[cy * geo.ctb_w + cx]; i++) {
+                    const uint16_t e = bins[(size_t)(cy * geo.ctb_w + cx) * kCuBinCap + i];
+                    if ((e & 0x80ffu) < (uint32_t)CTX_TERM) ctx_update(ctx[e & 0xffu], (e >> 8) & 1);
+                }
+            memcpy(sync, ctx, CTX_COUNT);
+            payload_bytes_ += (long long)sub[r].size();
+            continue;
+        }
         size_t cap = 64;
         for (int cx = 0; cx < geo.ctb_w; cx++) cap += (size_t)bin_n[cy * geo.ctb_w + cx] * 2 + 8;
         sub[r].assign(cap, 0);

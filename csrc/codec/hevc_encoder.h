@@ -11,6 +11,7 @@
 // legacy/gstwebrtc_app.py:369-425, x265enc :667-683, vah265enc :510-543) with the
 // H.265 RTP payloader (PT 100, :848-866); this encoder is the HIP-native equivalent.
 #pragma once
+#include <stdlib.h>
 #include <vector>
 #include "h264_frame.h"
 #include "hevc_core.h"
@@ -75,6 +76,7 @@ class CpuHevcEncoder {
     // CABAC substreams of slice s (one per CTB row) -> slice NAL (Annex B)
     std::vector<uint8_t> write_slice(int s, bool idr);
     long long payload_bytes_ = 0;   // substream bytes of the frame being written (K10)
+    bool pc_host_ = getenv("SK_HEVC_PCABAC") != nullptr;   // write rows with pc_code_row_host
 
     h264::CpuH264Encoder fe;   // front end (full-frame mode)
     Geo geo;

@@ -6,6 +6,7 @@
 #include "h264_gpu.h"
 #include "../codec/hevc_core.h"
 #include "../codec/hevc_syntax.h"
+#include "../codec/hevc_pcabac.h"
 
 namespace sk {
 namespace hevc {
@@ -29,6 +30,14 @@ struct HevcArgs {
     int out_slot, out_dev_slot;
     int addr_bits;
     unsigned long long* dbg;    // optional (SK_STAMPS): per CTB row [cycles, entries, bytes, 0]
+    // chunk-parallel substream coding (codec/hevc_pcabac.h), chunk = CTB
+    uint16_t* srt;              // [ctbs][kCuBinCap] the CTB's context bins sorted by context: index << 1 | bin
+    uint16_t* coff;             // [ctbs][kPcCtxOff] start of each context's run in srt (last = count)
+    uint32_t* rmap;             // [ctbs][256] end range | shifts << 9, per start range 256..511
+    uint32_t* cu_t;             // [ctbs] stream bit offset of the CTB's chunk inside its row substream
+    uint16_t* cu_r;             // [ctbs] start range of the chunk
+    uint8_t* tail;              // [ctbs][2] the chunk's two bytes overlapping the next chunk
+    uint32_t* row_bits;         // [ctb_h] shifts of the whole row (T_f)
 };
 
 void launch_backend(const HevcArgs& a, hipStream_t s);

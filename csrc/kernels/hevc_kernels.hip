@@ -7,7 +7,8 @@
 //   k_hevc_bins        CU syntax -> CABAC bin entries (hevc_core.h code_cu)
 //   k_hevc_sync        WPP: context states at every CTB row start (state-only replay of
 //                      the first two CTBs of the row above, lane = context)
-//   k_hevc_cabac       one wave per CTB row: arithmetic coding of the row's substream
+//   k_pc_*             chunk-parallel CABAC of the row substreams (codec/hevc_pcabac.h):
+//                      context chains, range maps, composition, per-CTB coding, merge
 //   k_hevc_hdr         slice header with entry points, NAL prefix, substream offsets
 //   k_hevc_ep_copy     wave-parallel emulation prevention + copy into host-mapped slots
 // Bit-exact with the CPU reference (codec/hevc_cpu.cpp): integer math only.
@@ -451,7 +452,9 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
     const int cand_a = (left && A.cus[idx - 1].mode == CU_INTRA) ? A.cus[idx - 1].intra_mode : 1;
     BinBuf w{A.bins + (size_t)idx * kCuBinCap, 0};
     code_cu(w, cu, A.coefs + (size_t)idx * kCoefPerCu, p_slice, skip_ctx, cand_a);
-    w.term(cy == t.first_row + t.num_rows - 1 && cx == f.mb_w - 1);
+    const bool last_row = cy == t.first_row + t.num_rows - 1;
+    w.term(last_row && cx == f.mb_w - 1);
+    if (!last_row && cx == f.mb_w - 1) w.term(1);   // end_of_subset_one_bit closes the row's substream
     A.bin_n[idx] = w.n;
 }
 
@@ -523,332 +526,404 @@ __global__ __launch_bounds__(64) void k_hevc_sync(HevcArgs A) {
     }
 }
 
-// One workgroup of three waves per CTB row codes the row's CABAC substream as a
-// pipeline through two LDS rings (each stage is SALU-issue bound on one wave, so the
-// per-bin work is spread over three SIMDs):
-//   modeler wave: context state lookup and transition per context bin (states live
-//                 across the 64 lanes, byte c & 3 of lane c >> 2; v_readlane at a
-//                 uniform index, v_writelane back) and rewrites each entry as
-//                 (LPS state index, is-LPS) -- bypass and terminating entries pass;
-//   coder wave:   the arithmetic coder proper (low, range) on the scalar unit, the LPS
-//                 range table across its lanes; every 8 settled bits it hands the
-//                 9-bit "lead" (byte + carry) to the writer;
-//   writer wave:  outstanding-byte / carry resolution, byte packing (lane = 4-byte
-//                 word, 256-byte wave stores) and the emulation-prevention count.
-// Same arithmetic and bytes as CabacEncoder (hevc_core.h).
-constexpr uint32_t kModeled = 0x4000u;   // modelled context bin: bits 0..5 LPS state, bit 6 is-LPS
-constexpr int kRingSize = 1024;          // entries in flight modeler -> coder (power of two)
-constexpr int kLeadRing = 256;           // tokens in flight coder -> writer (power of two)
-constexpr uint32_t kTokFlush = 0x1000u;  // writer token: resolve outstanding bytes, carry in bit 0
-constexpr uint32_t kTokRaw = 0x2000u;    // writer token: literal byte in bits 0..7
+// ---------------------------------------------------------------------------
+// Chunk-parallel substream coding (codec/hevc_pcabac.h has the derivation and the host
+// model): k_pc_sort -> k_pc_model -> k_pc_rmap -> k_pc_compose -> k_pc_code ->
+// k_pc_merge. Chunk = CTB, so every phase but the per-row composition and merge runs
+// one wave per CTB or per (CTB row, context). Same bytes as CabacEncoder (hevc_core.h).
+constexpr int kPcMaxRowCtb = 512;   // CTBs per row (8K width); alloc_hevc checks it
 
-struct CabacRing {
-    uint32_t e[kRingSize];
-    uint32_t lead[kLeadRing];
-    int produced, consumed, fin, model_waits;
-    int lead_produced, lead_consumed, lead_fin;
-};
-__device__ __forceinline__ int lds_acquire(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+// One wave per CTB: stable counting sort of its context bins by context index.
+__global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
+    __shared__ int cnt_s[4][kPcCtxOff];
+    const FrameArgs& f = A.f;
+    const int w = threadIdx.x >> 6, l = lane();
+    const int idx = blockIdx.x * 4 + w;
+    if (idx >= f.mb_w * f.mb_h) return;
+    int* cnt = cnt_s[w];
+    for (int i = l; i < kPcCtxOff; i += 64) cnt[i] = 0;
+    wsync();
+    const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
+    const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
+    for (int base = 0; base < nb; base += 64) {
+        const int i = base + l;
+        const uint32_t e = i < nb ? b[i] : 0x8000u;
+        if ((e & 0x80ffu) < (uint32_t)CTX_TERM) atomicAdd(&cnt[e & 0xffu], 1);
+    }
+    wsync();
+    int v[3], sum = 0;   // exclusive prefix; lane l owns counters 3l .. 3l + 2
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        v[k] = 3 * l + k < kPcCtxOff ? cnt[3 * l + k] : 0;
+        sum += v[k];
+    }
+    int inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o);
+        if (l >= o) inc += t;
+    }
+    int run = inc - sum;
+    wsync();
+    uint16_t* co = A.coff + (size_t)idx * kPcCtxOff;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        if (3 * l + k < kPcCtxOff) {
+            cnt[3 * l + k] = run;
+            co[3 * l + k] = (uint16_t)run;
+        }
+        run += v[k];
+    }
+    wsync();
+    uint16_t* sp = A.srt + (size_t)idx * kCuBinCap;
+    const uint64_t lt = (1ull << l) - 1;
+    for (int base = 0; base < nb; base += 64) {
+        const int i = base + l;
+        const uint32_t e = i < nb ? b[i] : 0x8000u;
+        const bool valid = (e & 0x80ffu) < (uint32_t)CTX_TERM;
+        const uint32_t key = e & 0xffu;
+        uint64_t m = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            const bool kb = (key >> bit) & 1u;
+            const uint64_t bb = __ballot(kb);
+            m &= kb ? bb : ~bb;
+        }
+        const int rank = __popcll(m & lt), tot = __popcll(m);
+        const int at = valid ? cnt[key] : 0;
+        wsync();
+        if (valid && rank == tot - 1) cnt[key] = at + tot;
+        wsync();
+        if (valid) sp[at + rank] = (uint16_t)((i << 1) | ((e >> 8) & 1u));
+    }
 }
-__device__ __forceinline__ void lds_release(int* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+
+// One wave per (CTB row, context): the context's state chain along the row, from its
+// WPP start state; each context bin is rewritten in place as a modelled entry (LPS state,
+// is-LPS). The list of CTBs holding the context is built first; the entries of the next
+// CTB are in flight while the current one is modelled.
+__global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
+    __shared__ uint2 lst_s[4][kPcMaxRowCtb];
+    const FrameArgs& f = A.f;
+    const int w = threadIdx.x >> 6, l = lane();
+    const int cy = blockIdx.x, c = blockIdx.y * 4 + w;
+    if (c >= CTX_COUNT) return;
+    uint2* L = lst_s[w];
+    const int row0 = cy * f.mb_w;
+    const uint64_t lt = (1ull << l) - 1;
+    int n = 0;
+    for (int g = 0; g < f.mb_w; g += 64) {
+        const int cx = g + l;
+        int lo = 0, cnt = 0;
+        if (cx < f.mb_w) {
+            const uint16_t* co = A.coff + (size_t)(row0 + cx) * kPcCtxOff + c;
+            lo = co[0];
+            cnt = co[1] - lo;
+        }
+        const uint64_t m = __ballot(cnt > 0);
+        if (cnt > 0) L[n + __popcll(m & lt)] = make_uint2((uint32_t)cx, (uint32_t)lo | ((uint32_t)cnt << 16));
+        n += __popcll(m);
+    }
+    wsync();
+    if (n == 0) return;
+    uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane(A.sync[(size_t)cy * CTX_COUNT + c]);
+    // transitions, lane = LPS state: byte 0 = next state byte on the MPS path (MPS 0),
+    // byte 1 = next on the LPS path (with the MPS flip of state 0); XOR the current MPS
+    const int tr_v = (int)(((uint32_t)(l < 62 ? l + 1 : l) << 1) |
+                           ((((uint32_t)CABAC_NEXT_LPS[l] << 1) | (l == 0 ? 1u : 0u)) << 8));
+    auto fetch = [&](int k, int& cx, int& lo, int& cnt, uint32_t& v) __attribute__((always_inline)) {
+        const uint2 it = L[k < n ? k : n - 1];
+        cx = __builtin_amdgcn_readfirstlane((int)it.x);
+        lo = __builtin_amdgcn_readfirstlane((int)(it.y & 0xffffu));
+        cnt = __builtin_amdgcn_readfirstlane((int)(it.y >> 16));
+        const uint16_t* sp = A.srt + (size_t)(row0 + cx) * kCuBinCap + lo;
+        v = sp[l < cnt ? l : cnt - 1];
+    };
+    auto model = [&](int cx, int lo, int cnt, uint32_t v) __attribute__((always_inline)) {
+        uint16_t* bp = A.bins + (size_t)(row0 + cx) * kCuBinCap;
+        const uint16_t* sp = A.srt + (size_t)(row0 + cx) * kCuBinCap + lo;
+        for (int k0 = 0; k0 < cnt; k0 += 64) {
+            if (k0) v = sp[k0 + (l < cnt - k0 ? l : cnt - k0 - 1)];
+            const int m = cnt - k0 < 64 ? cnt - k0 : 64;
+            int out = 0;
+            for (int i = 0; i < m; i++) {
+                const uint32_t vi = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+                const uint32_t st = s >> 1, mps = s & 1u, lp = (vi & 1u) ^ mps;
+                out = writelane((int)(kPcModeled | (lp << 6) | st), i, out);
+                const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane(tr_v, (int)st);
+                s = ((tr >> (lp << 3)) & 0xffu) ^ mps;
+            }
+            if (l < m) bp[v >> 1] = (uint16_t)out;
+        }
+    };
+    int cxa, loa, cnta, cxb, lob, cntb;
+    uint32_t va, vb;
+    fetch(0, cxa, loa, cnta, va);
+    for (int k = 0; k < n; k += 2) {
+        fetch(k + 1, cxb, lob, cntb, vb);
+        model(cxa, loa, cnta, va);
+        if (k + 1 >= n) break;
+        fetch(k + 2, cxa, loa, cnta, va);
+        model(cxb, lob, cntb, vb);
+    }
 }
 
-struct WaveCabac {
-    int lps_v;                  // CABAC_LPS[lane] packed
-    uint32_t low, range;
-    int bits_left;
-    int leads, lpos, lprod;     // writer tokens gathered in a VGPR (lane = token)
-    CabacRing* R;
-
-    __device__ __forceinline__ void publish() {
-        const int l = lane();
-        while (lprod + lpos - lds_acquire(&R->lead_consumed) > kLeadRing) __builtin_amdgcn_s_sleep(1);
-        if (l < lpos) R->lead[(lprod + l) & (kLeadRing - 1)] = (uint32_t)leads;
-        lprod += lpos;
-        lpos = 0;
-        if (l == 0) lds_release(&R->lead_produced, lprod);
+// One wave per CTB: the chunk's range map. Lane l follows the start ranges 256 + 4l .. +3
+// through the chunk's entries (bypass runs and terminating bins shift all of them alike).
+__global__ __launch_bounds__(256) void k_pc_rmap(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int w = threadIdx.x >> 6, l = lane();
+    const int idx = blockIdx.x * 4 + w;
+    if (idx >= f.mb_w * f.mb_h) return;
+    const int lps_v = (int)((uint32_t)CABAC_LPS[l][0] | ((uint32_t)CABAC_LPS[l][1] << 8) |
+                            ((uint32_t)CABAC_LPS[l][2] << 16) | ((uint32_t)CABAC_LPS[l][3] << 24));
+    uint32_t r[4], K[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        r[k] = 256u + 4u * (uint32_t)l + (uint32_t)k;
+        K[k] = 0;
     }
-    __device__ __forceinline__ void token(uint32_t t) {
-        leads = writelane((int)t, lpos, leads);
-        if (++lpos == 64) publish();
-    }
-    __device__ __forceinline__ void write_out() {
-        const uint32_t lead = low >> (24 - bits_left);
-        bits_left += 8;
-        low &= 0xffffffffu >> bits_left;
-        token(lead);
-    }
-    // One modelled entry: a context bin is one readlane (LPS ranges of its state), a
-    // branch-free MPS/LPS select and a count-leading-zeros renormalisation; bypass runs
-    // and terminating bins are the other two (rarer) paths.
-    __device__ __forceinline__ void code(uint32_t e) {
-        if (__builtin_expect((e & 0xC000u) == kModeled, 1)) {
-            const uint32_t lps4 = (uint32_t)__builtin_amdgcn_readlane(lps_v, (int)(e & 63u));
-            const uint32_t lps = (lps4 >> ((range >> 3) & 24u)) & 0xffu;
-            const uint32_t rmps = range - lps;
-            const uint32_t m = 0u - ((e >> 6) & 1u);                       // all ones on the LPS path
-            const uint32_t r = (lps & m) | (rmps & ~m);
-            const uint32_t lo = low + (rmps & m);
-            const int z = __builtin_clz(r) - 23;                          // r < 512: shift to >= 256
-            const int k = z & ~(z >> 31);                                 // max(z, 0) without a VALU clamp
-            low = lo << k;
-            range = r << k;
-            bits_left -= k;
-        } else if (e & 0x8000u) {   // bypass run
-            const int n = (int)((e >> 12) & 7u) + 1;
-            low = (low << n) + range * (e & 0xffu);
-            bits_left -= n;
-        } else {                    // terminating bin
-            range -= 2;
-            if ((e >> 8) & 1) {
-                low += range;
-                low <<= 7;
-                range = 2 << 7;
-                bits_left -= 7;
-            } else if (range < 256) {
-                low <<= 1;
-                range <<= 1;
-                bits_left--;
+    uint32_t kb = 0;
+    const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
+    const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
+    uint32_t cur = b[l < nb ? l : nb - 1];
+    for (int base = 0; base < nb; base += 64) {
+        const int pi = base + 64 + l;
+        const uint32_t nxt = b[pi < nb ? pi : nb - 1];
+        const int m = nb - base < 64 ? nb - base : 64;
+        for (int i = 0; i < m; i++) {
+            const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)cur, i);
+            if ((e & 0xC000u) == kPcModeled) {
+                const uint32_t lps4 = (uint32_t)__builtin_amdgcn_readlane(lps_v, (int)(e & 63u));
+                if (e & 64u) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t nr = (lps4 >> ((r[k] >> 3) & 24u)) & 0xffu;
+                        const uint32_t z = (uint32_t)__builtin_clz(nr) - 23u;
+                        r[k] = nr << z;
+                        K[k] += z;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const uint32_t nr = r[k] - ((lps4 >> ((r[k] >> 3) & 24u)) & 0xffu);
+                        const uint32_t z = nr < 256u ? 1u : 0u;
+                        r[k] = nr << z;
+                        K[k] += z;
+                    }
+                }
+            } else if (e & 0x8000u) {
+                kb += ((e >> 12) & 7u) + 1u;
+            } else if ((e >> 8) & 1u) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) r[k] = 256u;
+                kb += 7u;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t nr = r[k] - 2u;
+                    const uint32_t z = nr < 256u ? 1u : 0u;
+                    r[k] = nr << z;
+                    K[k] += z;
+                }
             }
         }
-        if (bits_left < 12) write_out();
+        cur = nxt;
     }
-    // Flush (9.3.4.3.5 / HM finish): the final carry resolves the outstanding bytes, then
-    // the remaining bits of low, the stop bit and the alignment zeros as literal bytes.
-    __device__ __forceinline__ void finish() {
-        const uint32_t c = low >> (32 - bits_left);
-        token(kTokFlush | c);
-        if (c) low -= 1u << (32 - bits_left);
-        const int nb = 24 - bits_left;
-        uint64_t v = ((uint64_t)(low >> 8) & ((1ull << nb) - 1)) << 1 | 1ull;
-        int total = nb + 1;
-        const int pad = (8 - (total & 7)) & 7;
-        v <<= pad;
-        total += pad;
-        for (int i = total - 8; i >= 0; i -= 8) token(kTokRaw | ((uint32_t)(v >> i) & 0xffu));
-        if (lpos) publish();
-        if (lane() == 0) lds_release(&R->lead_fin, 1);
+    uint4 o;
+    o.x = r[0] | ((K[0] + kb) << 9);
+    o.y = r[1] | ((K[1] + kb) << 9);
+    o.z = r[2] | ((K[2] + kb) << 9);
+    o.w = r[3] | ((K[3] + kb) << 9);
+    reinterpret_cast<uint4*>(A.rmap + (size_t)idx * 256)[l] = o;
+}
+
+// One wave per CTB row: start range and stream bit offset of every chunk, one map
+// lookup each (a readlane); the maps of the next 8 CTBs are in flight.
+__global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int cy = blockIdx.x, l = lane();
+    const int row0 = cy * f.mb_w, nw = f.mb_w;
+    constexpr int D = 8;
+    uint4 buf[D];
+#pragma unroll
+    for (int d = 0; d < D; d++)
+        buf[d] = reinterpret_cast<const uint4*>(A.rmap + (size_t)(row0 + (d < nw ? d : nw - 1)) * 256)[l];
+    uint32_t r = 510, T = 0;
+    int vr = 0, vt = 0;   // lane j: chunk j of the current 64
+    for (int cx0 = 0; cx0 < nw; cx0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+            const int cx = cx0 + d;
+            if (cx < nw) {
+                const int j = (int)r - 256, ln = j >> 2, comp = j & 3;
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)buf[d].x, ln);
+                const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)buf[d].y, ln);
+                const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)buf[d].z, ln);
+                const uint32_t ww = (uint32_t)__builtin_amdgcn_readlane((int)buf[d].w, ln);
+                const uint32_t val = comp == 0 ? x : (comp == 1 ? y : (comp == 2 ? z : ww));
+                vr = writelane((int)r, cx & 63, vr);
+                vt = writelane((int)T, cx & 63, vt);
+                if ((cx & 63) == 63 || cx == nw - 1) {
+                    if (l <= (cx & 63)) {
+                        A.cu_r[row0 + (cx & ~63) + l] = (uint16_t)vr;
+                        A.cu_t[row0 + (cx & ~63) + l] = (uint32_t)vt;
+                    }
+                }
+                r = val & 511u;
+                T += val >> 9;
+            }
+            const int nx = cx + D < nw ? cx + D : nw - 1;
+            buf[d] = reinterpret_cast<const uint4*>(A.rmap + (size_t)(row0 + nx) * 256)[l];
+        }
     }
-};
+    if (l == 0) A.row_bits[cy] = T;
+}
 
-// Writer wave: carry propagation over the outstanding 0xff bytes and byte packing.
-struct CabacWriter {
-    uint32_t buffered, acc;
-    int nbuf, opos, flushed;
-    int ob;                     // output chunk (lane = 4-byte word)
-    uint8_t* out;
-
-    __device__ __forceinline__ void put(uint32_t byte) {
+// One wave per CTB: the chunk coded from V = 0 (PcCoder, scalar state) and fully
+// flushed; bytes gathered in a VGPR (lane = 4 bytes) and stored every 256: the exclusive
+// ones into the row substream, the last two into the chunk's tail.
+__global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int w = threadIdx.x >> 6, l = lane();
+    const int idx = blockIdx.x * 4 + w;
+    if (idx >= f.mb_w * f.mb_h) return;
+    const int cy = idx / f.mb_w, cx = idx - cy * f.mb_w;
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.cu_t[idx]);
+    const uint32_t tn = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(cx + 1 < f.mb_w ? A.cu_t[idx + 1] : A.row_bits[cy]));
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.cu_r[idx]);
+    const int g0 = (int)(t0 >> 3), nex = (int)(tn >> 3) - g0;
+    uint8_t* out = A.sub + (size_t)cy * A.sub_stride + g0;
+    uint8_t* tl = A.tail + (size_t)idx * 2;
+    int ob = 0, opos = 0, flushed = 0;
+    uint32_t acc = 0;
+    auto store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p = 4 * l + k;
+            if (p < opos) {
+                const uint8_t byte = (uint8_t)((uint32_t)ob >> (8 * k));
+                const int q = flushed + p;
+                if (q < nex) out[q] = byte;
+                else tl[q - nex] = byte;
+            }
+        }
+        flushed += opos;
+        opos = 0;
+    };
+    auto emit = [&](uint32_t byte) __attribute__((always_inline)) {
         acc |= (byte & 0xffu) << (8 * (opos & 3));
         opos++;
         if ((opos & 3) == 0) {
             ob = writelane((int)acc, (opos >> 2) - 1, ob);
             acc = 0;
-            if (opos == 256) {
-                reinterpret_cast<int*>(out + flushed)[lane()] = ob;
-                flushed += 256;
-                opos = 0;
-            }
+            if (opos == 256) store();
         }
-    }
-    __device__ __forceinline__ void resolve(uint32_t carry) {   // nbuf > 0
-        put(buffered + carry);
-        const uint32_t fill = (0xff + carry) & 0xff;
-        while (nbuf > 1) {
-            put(fill);
-            nbuf--;
-        }
-    }
-    __device__ __forceinline__ void token(uint32_t t) {
-        if (__builtin_expect(t < 0x200u, 1)) {   // lead: settled byte + carry (HM writeOut)
-            if (t == 0xff) {
-                nbuf++;
-            } else if (nbuf > 0) {
-                resolve(t >> 8);
-                buffered = t & 0xff;
-            } else {
-                nbuf = 1;
-                buffered = t;
-            }
-        } else if (t & kTokRaw) {
-            put(t & 0xffu);
-        } else {                                 // flush (HM finish: the carry case puts even with nbuf == 0)
-            const uint32_t c = t & 1u;
-            if (c || nbuf > 0) put(buffered + c);
-            const uint32_t fill = c ? 0x00u : 0xffu;
-            while (nbuf > 1) {
-                put(fill);
-                nbuf--;
-            }
-        }
-    }
-    __device__ __forceinline__ int tail() {
-        if (opos & 3) ob = writelane((int)acc, opos >> 2, ob);
-        const int l = lane();
-        const int words = (opos + 3) >> 2;
-        if (l < words) {
-            const uint32_t wv = (uint32_t)ob;
-            uint8_t* d = out + flushed + 4 * l;
-            const int nbytes = l * 4 + 4 <= opos ? 4 : opos - 4 * l;
-            for (int k = 0; k < nbytes; k++) d[k] = (uint8_t)(wv >> (8 * k));
-        }
-        return flushed + opos;
-    }
-};
-
-// Modeler wave: context transitions of row cy's entries, 64 modelled entries per ring chunk.
-__device__ __forceinline__ void cabac_model_row(const HevcArgs& A, int cy, bool subset_end, CabacRing& R) {
-    const FrameArgs& f = A.f;
-    const int l = lane();
-    const uint8_t* srow = A.sync + (size_t)cy * CTX_COUNT;
-    int cs;
-    {
-        uint32_t w = 0;
-        for (int k = 0; k < 4; k++) {
-            const int c = 4 * l + k;
-            w |= (uint32_t)(c < CTX_COUNT ? srow[c] : 0) << (8 * k);
-        }
-        cs = (int)w;
-    }
-    // transition table, lane = LPS state index: byte 0 = next (state << 1) on the MPS path,
-    // byte 1 = next (state << 1 | MPS flip) on the LPS path; the new state byte is the
-    // selected byte XOR the current MPS
-    const int tr_v = (int)(((uint32_t)(l < 62 ? l + 1 : l) << 1) |
-                           ((((uint32_t)CABAC_NEXT_LPS[l] << 1) | (l == 0 ? 1u : 0u)) << 8));
-    int produced = 0, waits = 0;
-    // publish entries [0, m) of `v` (lane = entry) at ring positions produced .. produced + m
-    auto publish = [&](uint32_t v, int m) __attribute__((always_inline)) {
-        while (produced + m - lds_acquire(&R.consumed) > kRingSize) {
-            __builtin_amdgcn_s_sleep(1);
-            waits++;
-        }
-        if (l < m) R.e[(produced + l) & (kRingSize - 1)] = v;
-        produced += m;
-        if (l == 0) lds_release(&R.produced, produced);
     };
-    for (int idx = cy * f.mb_w; idx < (cy + 1) * f.mb_w; idx++) {
-        const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
-        const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
-        uint32_t cur = l < nb ? b[l] : 0u;
-        for (int base = 0; base < nb; base += 64) {
-            const uint32_t nxt_in = base + 64 + l < nb ? b[base + 64 + l] : 0u;   // prefetch
-            const int m = __builtin_amdgcn_readfirstlane(nb - base < 64 ? nb - base : 64);
-            for (int i = 0; i < m; i++) {
-                const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)cur, i);
-                if (__builtin_expect((e & 0x80ffu) < (uint32_t)CTX_TERM, 1)) {   // context bin (not bypass / terminate)
-                    const uint32_t c = e & 0xffu, bin = (e >> 8) & 1u;
-                    const int wl = (int)(c >> 2), sh = (int)(c & 3u) * 8;
-                    const uint32_t word = (uint32_t)__builtin_amdgcn_readlane(cs, wl);
-                    const uint32_t s = (word >> sh) & 0xffu;
-                    const uint32_t st = s >> 1, mps = s & 1u;
-                    const uint32_t lp = bin ^ mps;
-                    const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane(tr_v, (int)st);
-                    const uint32_t ns = ((tr >> (lp << 3)) & 0xffu) ^ mps;
-                    cs = writelane((int)((word & ~(0xffu << sh)) | (ns << sh)), wl, cs);
-                    cur = (uint32_t)writelane((int)(kModeled | (lp << 6) | st), i, (int)cur);   // in place
-                }
-            }
-            publish(cur, m);
-            cur = nxt_in;
-        }
+    PcCoder c;
+    c.start(r0, (int)(t0 & 7));
+    const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
+    const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
+    uint32_t cur = b[l < nb ? l : nb - 1];
+    for (int base = 0; base < nb; base += 64) {
+        const int pi = base + 64 + l;
+        const uint32_t nxt = b[pi < nb ? pi : nb - 1];
+        const int m = nb - base < 64 ? nb - base : 64;
+        for (int i = 0; i < m; i++) c.code((uint32_t)__builtin_amdgcn_readlane((int)cur, i), emit);
+        cur = nxt;
     }
-    if (subset_end) publish(CTX_TERM | (1u << 8), 1);   // end_of_subset_one_bit
-    if (l == 0) R.model_waits = waits;   // diagnostics (read after the final barrier)
-    if (l == 0) lds_release(&R.fin, 1);
+    c.flush(emit);
+    if (opos & 3) ob = writelane((int)acc, opos >> 2, ob);
+    store();
 }
 
-__global__ __launch_bounds__(192) void k_hevc_cabac(HevcArgs A) {
-    __shared__ CabacRing R;
+// One wave per CTB row: adds every chunk's tail into the substream (a 256-byte window
+// of it in a VGPR; carries run toward the start), writes the rbsp stop bit, then counts
+// the emulation-prevention bytes (same rule as k_hevc_ep_copy).
+__global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
     const FrameArgs& f = A.f;
-    const int cy = blockIdx.x;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
-    const int l = lane();
-    const int wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) {
-        R.produced = R.consumed = R.fin = R.model_waits = 0;
-        R.lead_produced = R.lead_consumed = R.lead_fin = 0;
-    }
-    __syncthreads();
-    int size = 0;
-    if (wave == 0) {
-        cabac_model_row(A, cy, cy < t.first_row + t.num_rows - 1, R);
-    } else if (wave == 1) {
-        WaveCabac E;
-        E.lps_v = (int)((uint32_t)CABAC_LPS[l][0] | ((uint32_t)CABAC_LPS[l][1] << 8) |
-                        ((uint32_t)CABAC_LPS[l][2] << 16) | ((uint32_t)CABAC_LPS[l][3] << 24));
-        E.low = 0;
-        E.range = 510;
-        E.bits_left = 23;
-        E.leads = 0;
-        E.lpos = 0;
-        E.lprod = 0;
-        E.R = &R;
-        const unsigned long long t0 = A.dbg ? __builtin_amdgcn_s_memtime() : 0;
-        const unsigned long long rt0 = A.dbg ? __builtin_amdgcn_s_memrealtime() : 0;   // 100 MHz
-        int done = 0, waits = 0;
-        for (;;) {
-            const int fin = lds_acquire(&R.fin);   // before `produced`: once set, produced is final
-            const int avail = lds_acquire(&R.produced) - done;
-            if (avail > 0) {
-                const uint32_t v = R.e[(done + l) & (kRingSize - 1)];
-                const int m = __builtin_amdgcn_readfirstlane(avail < 64 ? avail : 64);
-                for (int i = 0; i < m; i++) E.code((uint32_t)__builtin_amdgcn_readlane((int)v, i));
-                done += m;
-                if (l == 0) lds_release(&R.consumed, done);
-            } else if (fin) {
-                break;
-            } else {
-                __builtin_amdgcn_s_sleep(1);
-                waits++;
+    const int cy = blockIdx.x, l = lane();
+    const int row0 = cy * f.mb_w;
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.row_bits[cy]);
+    const int excl = (int)(T >> 3), nbytes = excl + 2;
+    uint8_t* out = A.sub + (size_t)cy * A.sub_stride;
+    int wb = 0;
+    uint32_t win = 0;
+    auto load_win = [&]() __attribute__((always_inline)) {
+        const int q = wb + 4 * l;
+        uint32_t v = 0;
+        if (q + 4 <= excl) {
+            v = *reinterpret_cast<const uint32_t*>(out + q);
+        } else {
+            for (int k = 0; k < 4; k++)
+                if (q + k < excl) v |= (uint32_t)out[q + k] << (8 * k);
+        }
+        win = v;
+    };
+    auto store_win = [&]() __attribute__((always_inline)) {
+        const int q = wb + 4 * l;
+        if (q + 4 <= nbytes) {
+            *reinterpret_cast<uint32_t*>(out + q) = win;
+        } else {
+            for (int k = 0; k < 4; k++)
+                if (q + k < nbytes) out[q + k] = (uint8_t)(win >> (8 * k));
+        }
+    };
+    auto get = [&](int q) __attribute__((always_inline)) -> uint32_t {
+        const int o = q - wb;
+        return ((uint32_t)__builtin_amdgcn_readlane((int)win, o >> 2) >> ((o & 3) * 8)) & 0xffu;
+    };
+    auto set = [&](int q, uint32_t byte) __attribute__((always_inline)) {
+        const int o = q - wb, sh = (o & 3) * 8;
+        const uint32_t wv = (uint32_t)__builtin_amdgcn_readlane((int)win, o >> 2);
+        win = (uint32_t)writelane((int)((wv & ~(0xffu << sh)) | (byte << sh)), o >> 2, (int)win);
+    };
+    load_win();
+    for (int g = 0; g < f.mb_w; g += 64) {
+        const int cx = g + l;
+        int p_l = 0, t_l = 0;
+        if (cx < f.mb_w) {
+            p_l = (int)((cx + 1 < f.mb_w ? A.cu_t[row0 + cx + 1] : T) >> 3);
+            t_l = (int)((uint32_t)A.tail[2 * (row0 + cx)] | ((uint32_t)A.tail[2 * (row0 + cx) + 1] << 8));
+        }
+        const int m = f.mb_w - g < 64 ? f.mb_w - g : 64;
+        for (int j = 0; j < m; j++) {
+            const int p = __builtin_amdgcn_readlane(p_l, j);
+            const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane(t_l, j);
+            if (p + 2 > wb + 256) {
+                store_win();
+                __threadfence();
+                wb = p & ~3;
+                load_win();
+            }
+            uint32_t v = ((get(p) << 8) | get(p + 1)) + (((tv & 0xffu) << 8) | (tv >> 8));
+            set(p + 1, v & 0xffu);
+            set(p, (v >> 8) & 0xffu);
+            for (int q = p - 1; (v >> 16) && q >= 0; q--) {   // carry (rare)
+                if (q >= wb) {
+                    v = get(q) + 1;
+                    set(q, v & 0xffu);
+                } else {
+                    __threadfence();
+                    v = (uint32_t)__builtin_amdgcn_readfirstlane((int)out[q]) + 1;
+                    if (l == 0) out[q] = (uint8_t)v;
+                }
+                v <<= 8;
             }
         }
-        E.finish();
-        if (A.dbg && l == 0) {
-            A.dbg[4 * cy + 0] = __builtin_amdgcn_s_memtime() - t0;
-            A.dbg[4 * cy + 1] = (unsigned long long)done | ((unsigned long long)waits << 24) |
-                                ((unsigned long long)lds_acquire(&R.model_waits) << 44);
-            A.dbg[4 * cy + 2] = rt0;
-            A.dbg[4 * cy + 3] = __builtin_amdgcn_s_memrealtime();
-        }
-    } else {
-        CabacWriter W;
-        W.buffered = 0xff;
-        W.acc = 0;
-        W.nbuf = 0;
-        W.opos = 0;
-        W.flushed = 0;
-        W.ob = 0;
-        W.out = A.sub + (size_t)cy * A.sub_stride;
-        int done = 0;
-        for (;;) {
-            const int fin = lds_acquire(&R.lead_fin);
-            const int avail = lds_acquire(&R.lead_produced) - done;
-            if (avail > 0) {
-                const uint32_t v = R.lead[(done + l) & (kLeadRing - 1)];
-                const int m = __builtin_amdgcn_readfirstlane(avail < 64 ? avail : 64);
-                for (int i = 0; i < m; i++) W.token((uint32_t)__builtin_amdgcn_readlane((int)v, i));
-                done += m;
-                if (l == 0) lds_release(&R.lead_consumed, done);
-            } else if (fin) {
-                break;
-            } else {
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        size = W.tail();
     }
-    __syncthreads();   // the writer wave's substream bytes are visible to its own lanes
-    if (wave != 2) return;
-    const uint8_t* out = A.sub + (size_t)cy * A.sub_stride;
-    if (l == 0) A.sub_size[cy] = size;
-    // emulation-prevention count (wave-parallel, same rule as k_hevc_ep_copy)
+    const uint32_t sb = T + 1;   // rbsp stop bit, then zeros
+    const int qs = (int)(sb >> 3);
+    set(qs, (get(qs) & (0xff00u >> (sb & 7))) | (0x80u >> (sb & 7)));
+    store_win();
+    __threadfence();
+    const int size = qs + 1;
     int last_nz = -1, ins_total = 0;
     for (int base = 0; base < size; base += 64) {
         const int i = base + l;
-        const int b = i < size ? out[i] : 1;
-        int p = b != 0 ? i : -1;
+        const int bv = i < size ? out[i] : 1;
+        int p = bv != 0 ? i : -1;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const int q = __shfl_up(p, d);
@@ -858,11 +933,20 @@ __global__ __launch_bounds__(192) void k_hevc_cabac(HevcArgs A) {
         if (l == 0) prev_nz = -1;
         prev_nz = max(prev_nz, last_nz);
         const int z = i - 1 - prev_nz;
-        const int ins = (i < size && b <= 3 && z >= 2 && (z & 1) == 0) ? 1 : 0;
+        const int ins = (i < size && bv <= 3 && z >= 2 && (z & 1) == 0) ? 1 : 0;
         ins_total += wsum(ins);
         last_nz = max(last_nz, __shfl(p, 63));
     }
-    if (l == 0) A.sub_esc[cy] = size + ins_total;
+    if (l == 0) {
+        A.sub_size[cy] = size;
+        A.sub_esc[cy] = size + ins_total;
+        if (A.dbg) {
+            A.dbg[4 * cy + 0] = 0;
+            A.dbg[4 * cy + 1] = T;
+            A.dbg[4 * cy + 2] = (unsigned long long)size;
+            A.dbg[4 * cy + 3] = 0;
+        }
+    }
 }
 
 // Slice header + NAL prefix per slice; substream offsets for k_hevc_ep_copy.
@@ -1012,7 +1096,13 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
     hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_cabac, dim3(a.f.mb_h), dim3(192), 0, s, a);
+    const int nq = (n + 3) / 4;
+    hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pc_model, dim3(a.f.mb_h, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pc_rmap, dim3(nq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pc_compose, dim3(a.f.mb_h), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_pc_code, dim3(nq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pc_merge, dim3(a.f.mb_h), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h), dim3(64), 0, s, a);
     const int cw = a.f.mb_w, ch = a.f.mb_h;

@@ -43,6 +43,7 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipSetDevice(device_));
         warm_copy_engines(device_);
         HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        HIPCHECK(hipStreamCreateWithFlags(&sync_stream_, hipStreamNonBlocking));
         for (auto& e : ev_) HIPCHECK(hipEventCreate(&e));
         for (auto& e : ev_copy_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (cfg_.shared_copy) copy_stream_ = device_copy_stream(device_);
@@ -64,6 +65,7 @@ class HipBackend : public EncoderBackend {
         for (auto* b : bgrx_dev_)
             if (b) hipFree(b);
         hipStreamDestroy(stream_);
+        if (sync_stream_) (void)hipStreamDestroy(sync_stream_);
         if (up_stream_) hipStreamDestroy(up_stream_);
     }
 
@@ -85,7 +87,7 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipSetDevice(device_));
         HIPCHECK(hipStreamSynchronize(stream_));
         RcState rc;
-        HIPCHECK(hipMemcpy(&rc, args_.rc, sizeof(rc), hipMemcpyDeviceToHost));
+        copy_now(&rc, args_.rc, sizeof(rc));
         const int k = n < (int)(sizeof(rc) / 4) ? n : (int)(sizeof(rc) / 4);
         memcpy(out, &rc, (size_t)k * 4);
         return k;
@@ -244,9 +246,9 @@ class HipBackend : public EncoderBackend {
         int ctl[4];
         std::vector<StripeState> st(ns + 1);
         std::vector<SliceTask> tasks(ns);
-        HIPCHECK(hipMemcpy(ctl, args_.plan_ctl, sizeof(ctl), hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemcpy(st.data(), args_.plan_state, sizeof(StripeState) * (ns + 1), hipMemcpyDeviceToHost));
-        HIPCHECK(hipMemcpy(tasks.data(), args_.tasks, sizeof(SliceTask) * ns, hipMemcpyDeviceToHost));
+        copy_now(ctl, args_.plan_ctl, sizeof(ctl));
+        copy_now(st.data(), args_.plan_state, sizeof(StripeState) * (ns + 1));
+        copy_now(tasks.data(), args_.tasks, sizeof(SliceTask) * ns);
         if (ctl[1] == 1) {   // apply the commit k_plan would run at the next frame
             if (cfg_.fullframe) {
                 bool idr = ns > 0;
@@ -285,7 +287,7 @@ class HipBackend : public EncoderBackend {
         const int ns = g_.num_slices;
         std::vector<uint8_t> head(sizeof(StateHeader) + sizeof(StripeState) * (ns + 1));
         const uint8_t* i = static_cast<const uint8_t*>(src);
-        if (on_device) HIPCHECK(hipMemcpy(head.data(), i, sizeof(StateHeader), hipMemcpyDeviceToHost));
+        if (on_device) copy_now(head.data(), i, sizeof(StateHeader));
         else memcpy(head.data(), i, sizeof(StateHeader));
         StateHeader h;
         memcpy(&h, head.data(), sizeof(h));
@@ -479,7 +481,7 @@ class HipBackend : public EncoderBackend {
             RcState rc;
             rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height);
             a.rc = dmalloc<RcState>(1);
-            HIPCHECK(hipMemcpy(a.rc, &rc, sizeof(rc), hipMemcpyHostToDevice));
+            copy_now(a.rc, &rc, sizeof(rc));
             a.rc_slice = dmalloc<long long>(2 * (size_t)ns);
             a.rc_redo = dmalloc<int>(1);
             a.gate = nullptr;
@@ -644,6 +646,14 @@ class HipBackend : public EncoderBackend {
         h.sub_esc = dmalloc<int>(g_.mb_h);
         h.row_off = dmalloc<int>(g_.mb_h);
         h.addr_bits = geo.addr_bits;
+        if (g_.mb_w > 512) throw std::runtime_error("HEVC: more than 512 CTBs per row (8K) is not supported");
+        h.srt = dmalloc<uint16_t>((size_t)n * hevc::kCuBinCap, false);
+        h.coff = dmalloc<uint16_t>((size_t)n * hevc::kPcCtxOff, false);
+        h.rmap = dmalloc<uint32_t>((size_t)n * 256, false);
+        h.cu_t = dmalloc<uint32_t>(n);
+        h.cu_r = dmalloc<uint16_t>(n);
+        h.tail = dmalloc<uint8_t>((size_t)n * 2);
+        h.row_bits = dmalloc<uint32_t>(g_.mb_h);
         // host slot: 1.5 KB per CTB (far above practical rates); larger slices go to the
         // device fallback slot (worst case: 3/2 emulation growth of the substream bound)
         h.out_slot = (g_.rows_per_slice * g_.mb_w * 1536 + 4096 + 63) & ~63;
@@ -702,7 +712,7 @@ class HipBackend : public EncoderBackend {
         std::vector<uint8_t> q(52);
         for (int i = 0; i < 52; i++) q[i] = (uint8_t)av1::qidx_for_qp(i);
         uint8_t* dq = dmalloc<uint8_t>(52);
-        HIPCHECK(hipMemcpy(dq, q.data(), 52, hipMemcpyHostToDevice));
+        copy_now(dq, q.data(), 52);
         a.qidx_of_qp = dq;
         void* dptr = nullptr;
         for (int p = 0; p < 2; p++) {
@@ -777,8 +787,7 @@ class HipBackend : public EncoderBackend {
             if (n <= hargs_.out_slot) {
                 memcpy(pk.data.data() + o, hevc_out_[par] + (size_t)s * hargs_.out_slot, (size_t)n);
             } else {   // rare: the slice did not fit its host slot
-                HIPCHECK(hipMemcpy(pk.data.data() + o, hevc_fallback_[par] + (size_t)s * hargs_.out_dev_slot,
-                                   (size_t)n, hipMemcpyDeviceToHost));
+                copy_now(pk.data.data() + o, hevc_fallback_[par] + (size_t)s * hargs_.out_dev_slot, (size_t)n);
             }
         }
         packets_.push_back(std::move(pk));
@@ -881,6 +890,14 @@ class HipBackend : public EncoderBackend {
     uint8_t* ov_stage_ = nullptr;
     hipGraphExec_t post_exec_[2] = {nullptr, nullptr};
     bool use_graphs_ = getenv("SK_NO_GRAPHS") == nullptr;
+    // Blocking copies go through their own non-blocking stream: a copy on the legacy
+    // stream fails while any stream of the process is capturing a graph (several
+    // sessions share one process in parallel/multi.py session hosts).
+    hipStream_t sync_stream_ = nullptr;
+    void copy_now(void* dst, const void* src, size_t n) {
+        HIPCHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, sync_stream_));
+        HIPCHECK(hipStreamSynchronize(sync_stream_));
+    }
     bool graph_guard_ = false;   // the captured H.264 graphs contain the K10 CBR guard
     hipEvent_t ev_ext_ = nullptr;   // wait_stream(): foreign stream's work before the next upload
     bool ext_wait_ = false;

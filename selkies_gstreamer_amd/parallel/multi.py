@@ -64,7 +64,15 @@ async def host(ports: Sequence[int], shared: Sequence[str], displays: Optional[S
     for i, argv in enumerate(session_argvs(ports, shared, displays)):
         tasks.append(asyncio.create_task(serve(argv, stops[i], ready)))
     waiter = asyncio.create_task(stop.wait())
-    done, _ = await asyncio.wait([waiter, *tasks], return_when=asyncio.FIRST_COMPLETED)
+    pending = set(tasks)
+    # one session that fails (a port taken, a display gone) is logged and the others
+    # keep serving; the host ends on its stop signal or when no session is left
+    while pending and not stop.is_set():
+        done, _ = await asyncio.wait([waiter, *pending], return_when=asyncio.FIRST_COMPLETED)
+        for t in done:
+            if t is waiter:
+                continue
+            pending.discard(t)
     for ev in stops:
         ev.set()
     results = await asyncio.gather(*tasks, return_exceptions=True)

@@ -88,3 +88,20 @@ def test_hevc_qp_changes_size():
     b = _run(W, H, "noise", 2, qp=38)
     assert len(b[1][0].data) < len(a[1][0].data)
     assert a[1][2] > b[1][2]
+
+
+@pytest.mark.parametrize("kind,qp", [("motion", 22), ("noise", 30), ("desktop", 37)])
+def test_hevc_chunk_parallel_cabac_model_is_exact(kind, qp, monkeypatch):
+    """The chunk-parallel substream coder (codec/hevc_pcabac.h: context chains, range
+    maps, composition, per-CTB coding from V = 0, tail merge) -- the algorithm the HIP
+    back end runs -- writes the same bytes as the serial CABAC coder."""
+    W, H = 192, 128
+    src = SyntheticDesktop(W, H, kind=kind)
+    ref = HevcEncoder(W, H, backend="cpu", stripe_height=64, qp=qp)
+    monkeypatch.setenv("SK_HEVC_PCABAC", "1")
+    par = HevcEncoder(W, H, backend="cpu", stripe_height=64, qp=qp)
+    for t in range(4):
+        f = src.frame(t)
+        a = [p.data for p in ref.encode(f, t)]
+        b = [p.data for p in par.encode(f, t)]
+        assert a == b, f"frame {t}"

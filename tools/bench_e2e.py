@@ -42,12 +42,36 @@ sys.path.insert(0, ROOT)
 from selkies_gstreamer_amd.parallel.launcher import hw_queues_for  # noqa: E402
 
 
+_TAKEN: set = set()
+
+
 def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A port below the kernel's ephemeral range. Ports the OS hands out for port 0
+    (every session's data websocket, client sockets) come from that range, so a port
+    picked there and released can be taken again before its server binds it (a 48-session
+    run lost a server that way: 'address already in use')."""
+    lo = 32768
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        pass
+    base = max(1024, lo - 12000)
+    rng = np.random.default_rng()
+    for _ in range(1000):
+        p = int(rng.integers(base, lo))
+        if p in _TAKEN:
+            continue
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+        except OSError:
+            continue
+        finally:
+            s.close()
+        _TAKEN.add(p)
+        return p
+    raise RuntimeError("no free port below the ephemeral range")
 
 
 def start_servers(n: int, args) -> list:
@@ -205,6 +229,7 @@ async def run_n(n: int, args) -> dict:
             out.update(part)
     finally:
         stop_servers(procs)
+        _TAKEN.difference_update(port for _, port, _ in procs)
     fps = np.array([out[p]["frames"] / args.seconds for _, p, _ in procs]) if out else np.zeros(1)
     lat = np.concatenate([np.asarray(out[p]["lat"], dtype=np.float64) for _, p, _ in procs]) if out else np.zeros(0)
     lat_last = (np.concatenate([np.asarray(out[p]["lat_last"], dtype=np.float64) for _, p, _ in procs])
