@@ -102,8 +102,9 @@ std::vector<uint8_t> pc_code_row_host(const std::vector<std::vector<uint16_t>>& 
             else throw std::logic_error("pcabac: chunk overran its tail");
         };
         PcCoder c;
+        PcLpsTable lps;
         c.start(r0[j], (int)(t0[j] & 7));
-        for (uint16_t e : mod[j]) c.code(e, emit);
+        for (uint16_t e : mod[j]) c.code(e, emit, lps);
         c.flush(emit);
         if (g0 + pos != gn + 2) throw std::logic_error("pcabac: chunk byte count");
         tail[j] = tl;

@@ -63,6 +63,14 @@ SK_HD int pc_range_step(uint32_t e, uint32_t& r) {
     return 0;
 }
 
+// Host LPS row lookup for PcCoder::code.
+struct PcLpsTable {
+    SK_HD uint32_t operator()(uint32_t st) const {
+        return (uint32_t)CABAC_LPS[st][0] | ((uint32_t)CABAC_LPS[st][1] << 8) | ((uint32_t)CABAC_LPS[st][2] << 16) |
+               ((uint32_t)CABAC_LPS[st][3] << 24);
+    }
+};
+
 // HM arithmetic coder over modelled entries, started from V = 0 with range r at bit
 // offset o (0..7) inside its first byte; flush() emits every remaining bit of V.
 struct PcCoder {
@@ -96,10 +104,11 @@ struct PcCoder {
             buffered = lead;
         }
     }
-    template <class Emit>
-    SK_HD void code(uint32_t e, Emit& emit) {
+    // lps4(state): the state's four LPS ranges packed in bytes (q = 0..3)
+    template <class Emit, class Lps>
+    SK_HD void code(uint32_t e, Emit& emit, Lps& lps4) {
         if ((e & 0xC000u) == kPcModeled) {
-            const uint32_t lps = CABAC_LPS[e & 63u][(range >> 6) & 3];
+            const uint32_t lps = (lps4(e & 63u) >> ((range >> 3) & 24u)) & 0xffu;
             const uint32_t rmps = range - lps;
             uint32_t nr = rmps;
             if (e & 64u) {

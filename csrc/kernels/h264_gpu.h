@@ -34,6 +34,7 @@ struct FrameArgs {
     StripeState* plan_state;    // [num_slices + 1] controller state (last = picture state)
     int* plan_ctl;              // [0] keyframe requests seen, [1] frames planned (0 = first frame)
     const int* key_seq_host;    // host-mapped: [0] keyframe request counter, [1] qp, [2] paint qp (0 = config)
+    int* key_dev;               // [6] k_plan's device copy of the snapshot (read by k_rc_qp)
     PlanConfig plan_cfg;
     SliceTask* tasks;      // [num_slices]
     MeResult* me;          // [num_mbs]

@@ -21,6 +21,7 @@
 //   k_commit                 MV-field update (+ plain reference copy when K7 is off)
 //   k_deblock_prep, k_deblock  K7  in-loop deblocking rec -> ref (LDS-ring wavefront)
 #include "h264_gpu.h"
+#include <stdlib.h>
 #include "../codec/color.h"
 #include "../codec/h264_mb.h"
 
@@ -663,7 +664,15 @@ __global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
             for (int s = tid; s < ns; s += 256) commit_stripe(st[s], a.tasks[s].final_action, a.plan_cfg.num_refs);
         }
     }
-    const int kq = __hip_atomic_load(a.key_seq_host, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // host overrides (host-mapped snapshot): one round trip, six lanes in parallel; the
+    // device copy is what k_rc_qp reads later in the frame
+    __shared__ int hk[6];
+    if (tid < 6) {
+        hk[tid] = __hip_atomic_load(a.key_seq_host + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        a.key_dev[tid] = hk[tid];
+    }
+    __syncthreads();
+    const int kq = hk[0];
     const bool key = kq != a.plan_ctl[0];
     __syncthreads();
     if (key) {
@@ -672,15 +681,12 @@ __global__ __launch_bounds__(256) void k_plan(FrameArgs a) {
     }
     __syncthreads();
     PlanConfig pc = a.plan_cfg;  // rate-control overrides from the host
-    const int qo = __hip_atomic_load(a.key_seq_host + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const int po = __hip_atomic_load(a.key_seq_host + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int qo = hk[1];
+    const int po = hk[2];
     if (qo > 0) pc.qp = qo;
     if (po > 0) pc.paint_qp = po;
     {   // K10 CBR: no paint-over refresh (the budget codes every slice at the frame QP anyway)
-        const int seq = __hip_atomic_load(a.key_seq_host + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const int mode = seq != a.rc->seq ? __hip_atomic_load(a.key_seq_host + 3, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_SYSTEM)
-                                          : a.rc->mode;
+        const int mode = hk[5] != a.rc->seq ? hk[3] : a.rc->mode;
         if (mode == RC_CBR) pc.use_paint_over = 0;
     }
     for (int s = tid; s < ns; s += 256) {
@@ -738,13 +744,13 @@ __global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
 __global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
     if (threadIdx.x != 0) return;
     RcState& rc = *a.rc;
-    const int seq = __hip_atomic_load(a.key_seq_host + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int seq = a.key_dev[5];   // k_plan's copy of the host snapshot
     int plan_qp = a.plan_cfg.qp;
-    const int qo = __hip_atomic_load(a.key_seq_host + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int qo = a.key_dev[1];
     if (qo > 0) plan_qp = qo;
     if (seq != rc.seq) {   // set_rate() from the host: re-initialise, keep the model if the mode stays
-        const int mode = __hip_atomic_load(a.key_seq_host + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const int kbps = __hip_atomic_load(a.key_seq_host + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int mode = a.key_dev[3];
+        const int kbps = a.key_dev[4];
         const RcState old = rc;
         rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H);
         if (old.mode == mode)
@@ -2971,11 +2977,11 @@ void launch_frontend(const FrameArgs& a, hipStream_t s) {
     if (a.me_full) hipLaunchKernelGGL(k_me_mfma, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_rc_qp, dim3(1), dim3(64), 0, s, a);
+    if (!getenv("SK_EXP_NO_RCK")) hipLaunchKernelGGL(k_rc_qp, dim3(1), dim3(64), 0, s, a);
 }
 
 void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, int per_slice, hipStream_t s) {
-    hipLaunchKernelGGL(k_rc_account, dim3(1), dim3(64), 0, s, a, sizes, n, stride, per_slice);
+    if (!getenv("SK_EXP_NO_RCK")) hipLaunchKernelGGL(k_rc_account, dim3(1), dim3(64), 0, s, a, sizes, n, stride, per_slice);
 }
 
 // Transform / quantisation / reconstruction / CAVLC / slice scan of every coded slice.

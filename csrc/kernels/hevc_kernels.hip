@@ -600,10 +600,12 @@ __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
 
 // One wave per (CTB row, context): the context's state chain along the row, from its
 // WPP start state; each context bin is rewritten in place as a modelled entry (LPS state,
-// is-LPS). The list of CTBs holding the context is built first; the entries of the next
-// CTB are in flight while the current one is modelled.
+// is-LPS). The CTBs holding the context are listed with the prefix of their counts, then
+// the chain's entries are gathered 64 at a time (lane = chain position; the next batch
+// is in flight while the current one is modelled) so the serial part runs on registers
+// and only visits the LPS bins.
 __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
-    __shared__ uint2 lst_s[4][kPcMaxRowCtb];
+    __shared__ uint2 lst_s[4][kPcMaxRowCtb + 1];   // (cx | lo << 16, chain position of its first entry)
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
     const int cy = blockIdx.x, c = blockIdx.y * 4 + w;
@@ -611,7 +613,7 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     uint2* L = lst_s[w];
     const int row0 = cy * f.mb_w;
     const uint64_t lt = (1ull << l) - 1;
-    int n = 0;
+    int n = 0, tot = 0;
     for (int g = 0; g < f.mb_w; g += 64) {
         const int cx = g + l;
         int lo = 0, cnt = 0;
@@ -620,51 +622,73 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
             lo = co[0];
             cnt = co[1] - lo;
         }
+        int inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(inc, o);
+            if (l >= o) inc += t;
+        }
         const uint64_t m = __ballot(cnt > 0);
-        if (cnt > 0) L[n + __popcll(m & lt)] = make_uint2((uint32_t)cx, (uint32_t)lo | ((uint32_t)cnt << 16));
+        if (cnt > 0) L[n + __popcll(m & lt)] = make_uint2((uint32_t)cx | ((uint32_t)lo << 16), (uint32_t)(tot + inc - cnt));
         n += __popcll(m);
+        tot += __builtin_amdgcn_readlane(inc, 63);
     }
+    n = __builtin_amdgcn_readfirstlane(n);
+    tot = __builtin_amdgcn_readfirstlane(tot);
+    if (l == 0) L[n] = make_uint2(0u, (uint32_t)tot);
     wsync();
-    if (n == 0) return;
+    if (tot == 0) return;
     uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane(A.sync[(size_t)cy * CTX_COUNT + c]);
     // transitions, lane = LPS state: byte 0 = next state byte on the MPS path (MPS 0),
     // byte 1 = next on the LPS path (with the MPS flip of state 0); XOR the current MPS
     const int tr_v = (int)(((uint32_t)(l < 62 ? l + 1 : l) << 1) |
                            ((((uint32_t)CABAC_NEXT_LPS[l] << 1) | (l == 0 ? 1u : 0u)) << 8));
-    auto fetch = [&](int k, int& cx, int& lo, int& cnt, uint32_t& v) __attribute__((always_inline)) {
-        const uint2 it = L[k < n ? k : n - 1];
-        cx = __builtin_amdgcn_readfirstlane((int)it.x);
-        lo = __builtin_amdgcn_readfirstlane((int)(it.y & 0xffffu));
-        cnt = __builtin_amdgcn_readfirstlane((int)(it.y >> 16));
-        const uint16_t* sp = A.srt + (size_t)(row0 + cx) * kCuBinCap + lo;
-        v = sp[l < cnt ? l : cnt - 1];
+    int kl = 0;   // this lane's list item (non-decreasing: its chain position only grows)
+    auto gather = [&](int base, uint32_t& v, uint32_t& dst) __attribute__((always_inline)) {
+        const int pos = base + l < tot ? base + l : tot - 1;
+        while ((int)L[kl + 1].y <= pos) kl++;
+        const uint2 it = L[kl];
+        const uint32_t cu = (uint32_t)row0 + (it.x & 0xffffu);
+        v = A.srt[(size_t)cu * kCuBinCap + (it.x >> 16) + (uint32_t)pos - it.y];
+        dst = cu;
     };
-    auto model = [&](int cx, int lo, int cnt, uint32_t v) __attribute__((always_inline)) {
-        uint16_t* bp = A.bins + (size_t)(row0 + cx) * kCuBinCap;
-        const uint16_t* sp = A.srt + (size_t)(row0 + cx) * kCuBinCap + lo;
-        for (int k0 = 0; k0 < cnt; k0 += 64) {
-            if (k0) v = sp[k0 + (l < cnt - k0 ? l : cnt - k0 - 1)];
-            const int m = cnt - k0 < 64 ? cnt - k0 : 64;
-            int out = 0;
-            for (int i = 0; i < m; i++) {
-                const uint32_t vi = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
-                const uint32_t st = s >> 1, mps = s & 1u, lp = (vi & 1u) ^ mps;
-                out = writelane((int)(kPcModeled | (lp << 6) | st), i, out);
-                const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane(tr_v, (int)st);
-                s = ((tr >> (lp << 3)) & 0xffu) ^ mps;
+    // One batch of the chain: MPS runs advance the state by their length (saturating at
+    // 62), so the serial loop steps from LPS to LPS (find-first over the batch's bin mask)
+    // and the lanes of each MPS run take their states in parallel.
+    auto model = [&](int base, uint32_t v, uint32_t dst) __attribute__((always_inline)) {
+        const int m = tot - base < 64 ? tot - base : 64;
+        const uint64_t valid = m == 64 ? ~0ull : ((1ull << m) - 1);
+        const uint64_t ones = __ballot(v & 1u) & valid;
+        int out = 0;
+        int p = 0;
+        for (;;) {
+            const uint32_t st = s >> 1, mps = s & 1u;
+            const uint64_t lpm = (mps ? ~ones : ones) & valid & (p < 64 ? (~0ull << p) : 0ull);
+            const int q = lpm ? (int)__builtin_ctzll(lpm) : m;
+            if (l >= p && l < q) {
+                const uint32_t t = st + (uint32_t)(l - p);
+                out = (int)(kPcModeled | (t < 62u ? t : 62u));
             }
-            if (l < m) bp[v >> 1] = (uint16_t)out;
+            const uint32_t sr = st + (uint32_t)(q - p) < 62u ? st + (uint32_t)(q - p) : 62u;
+            if (q >= m) {
+                s = (sr << 1) | mps;
+                break;
+            }
+            out = writelane((int)(kPcModeled | 64u | sr), q, out);
+            const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane(tr_v, (int)sr);
+            s = ((tr >> 8) & 0xffu) ^ mps;
+            p = q + 1;
         }
+        if (l < m) A.bins[(size_t)dst * kCuBinCap + (v >> 1)] = (uint16_t)out;
     };
-    int cxa, loa, cnta, cxb, lob, cntb;
-    uint32_t va, vb;
-    fetch(0, cxa, loa, cnta, va);
-    for (int k = 0; k < n; k += 2) {
-        fetch(k + 1, cxb, lob, cntb, vb);
-        model(cxa, loa, cnta, va);
-        if (k + 1 >= n) break;
-        fetch(k + 2, cxa, loa, cnta, va);
-        model(cxb, lob, cntb, vb);
+    uint32_t va, da, vb, db;
+    gather(0, va, da);
+    for (int base = 0; base < tot; base += 128) {
+        gather(base + 64, vb, db);
+        model(base, va, da);
+        if (base + 64 >= tot) break;
+        gather(base + 128, va, da);
+        model(base + 64, vb, db);
     }
 }
 
@@ -821,6 +845,11 @@ __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
             if (opos == 256) store();
         }
     };
+    const int lps_v = (int)((uint32_t)CABAC_LPS[l][0] | ((uint32_t)CABAC_LPS[l][1] << 8) |
+                            ((uint32_t)CABAC_LPS[l][2] << 16) | ((uint32_t)CABAC_LPS[l][3] << 24));
+    auto lps4 = [&](uint32_t st) __attribute__((always_inline)) {
+        return (uint32_t)__builtin_amdgcn_readlane(lps_v, (int)st);
+    };
     PcCoder c;
     c.start(r0, (int)(t0 & 7));
     const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
@@ -830,7 +859,7 @@ __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
         const int pi = base + 64 + l;
         const uint32_t nxt = b[pi < nb ? pi : nb - 1];
         const int m = nb - base < 64 ? nb - base : 64;
-        for (int i = 0; i < m; i++) c.code((uint32_t)__builtin_amdgcn_readlane((int)cur, i), emit);
+        for (int i = 0; i < m; i++) c.code((uint32_t)__builtin_amdgcn_readlane((int)cur, i), emit, lps4);
         cur = nxt;
     }
     c.flush(emit);

@@ -106,6 +106,7 @@ async def serve(argv: Sequence[str], stop: Optional[asyncio.Event] = None, ready
         except (OSError, RuntimeError):
             pass
     server = DataStreamingServer(settings, upload_dir=opts.upload_dir if "upload" in settings.file_transfers else None,
+                                 download_dir=opts.upload_dir if "download" in settings.file_transfers else None,
                                  input_factory=make_input_factory(settings, opts), capture_source=opts.capture_source,
                                  gpu_id=opts.gpu_id, num_gpus=opts.num_gpus, web_root=opts.web_root, metrics=metrics,
                                  x_display=opts.display)

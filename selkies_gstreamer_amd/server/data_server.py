@@ -25,7 +25,9 @@ import ctypes
 import json
 import logging
 import os
+import html
 import time
+import urllib.parse
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Any, Callable, Optional
@@ -176,8 +178,31 @@ class Capture:
         self.callback = None
 
 
+def files_listing_html(path: str, rel: str) -> str:
+    """HTML listing of one directory of the download area: sub-directories first,
+    then files with their sizes; names are escaped and links percent-encoded."""
+    rows = []
+    if rel.strip("/"):
+        rows.append('<li><a href="../">../</a></li>')
+    try:
+        entries = sorted((e for e in os.scandir(path) if not e.name.startswith(".")),
+                         key=lambda e: (not e.is_dir(), e.name.lower()))
+    except OSError:
+        entries = []
+    for e in entries:
+        d = e.is_dir()
+        size = "" if d else f" <small>{e.stat().st_size:,} B</small>"
+        rows.append(f'<li><a href="{urllib.parse.quote(e.name)}{"/" if d else ""}">'
+                    f'{html.escape(e.name)}{"/" if d else ""}</a>{size}</li>')
+    title = html.escape("/" + rel.strip("/"))
+    return ("<!DOCTYPE html><html><head><meta charset=\"utf-8\"><title>Files " + title + "</title>"
+            "<style>body{font:13px system-ui,sans-serif;margin:12px}li{margin:3px 0}</style></head>"
+            "<body><h3>Files " + title + "</h3><ul>" + "".join(rows) + "</ul></body></html>")
+
+
 class DataStreamingServer:
-    def __init__(self, settings: Settings, *, upload_dir: Optional[str] = None, input_factory=None,
+    def __init__(self, settings: Settings, *, upload_dir: Optional[str] = None, download_dir: Optional[str] = None,
+                 input_factory=None,
                  capture_factory: Optional[Callable[[], Any]] = None, display_manager=None,
                  capture_source: str = "auto", gpu_id: int = 0, num_gpus: int = 1, clock=time.monotonic,
                  web_root: Optional[str] = None, metrics=None, frame_trace: Optional[bool] = None,
@@ -203,6 +228,7 @@ class DataStreamingServer:
         self.settings_received = asyncio.Event()
         self.capture_cursor = False
         self.last_cursor: Optional[dict] = None
+        self.download_dir = download_dir   # served read-only under /files/ (dashboard files panel)
         self.upload_dir = upload_dir
         if upload_dir:
             try:
@@ -237,8 +263,37 @@ class DataStreamingServer:
         app.router.add_get("/health", self._health)
         if self.metrics is not None:
             app.router.add_get("/metrics", self.metrics.handler)
+        app.router.add_get("/files", self._files_redirect)
+        app.router.add_get("/files/{name:.*}", self._files)
         app.router.add_get("/{tail:.*}", self._root)
         return app
+
+    async def _files_redirect(self, request):
+        raise web.HTTPFound("/files/")
+
+    async def _files(self, request: web.Request):
+        """Read-only listing / download of the file directory (the dashboard's files
+        panel frames ./files/; reference: Sidebar.jsx:3523 iframe on the same path).
+        Dot files are hidden; nothing outside the directory is reachable."""
+        root = self.download_dir
+        if not root or not os.path.isdir(root):
+            raise web.HTTPNotFound()
+        rel = request.match_info.get("name", "")
+        base = os.path.realpath(root)
+        path = os.path.realpath(os.path.join(base, rel))
+        if not (path == base or path.startswith(base + os.sep)):
+            raise web.HTTPNotFound()
+        if any(part.startswith(".") for part in os.path.relpath(path, base).split(os.sep) if part not in ("", ".")):
+            raise web.HTTPNotFound()
+        if os.path.isdir(path):
+            if rel and not rel.endswith("/"):
+                raise web.HTTPFound(request.path + "/")
+            return web.Response(text=files_listing_html(path, rel), content_type="text/html")
+        if os.path.isfile(path):
+            name = os.path.basename(path)
+            return web.FileResponse(path, headers={
+                "Content-Disposition": f"attachment; filename*=UTF-8''{urllib.parse.quote(name)}"})
+        raise web.HTTPNotFound()
 
     async def _health(self, request):
         return web.Response(text="OK\n")

@@ -8,6 +8,8 @@
 // ui_sidebar_show_* setting, settings.py:36-108). Pure helpers are exported for
 // the node unit tests; the DOM code is plain ES modules without a framework.
 import { TouchGamepad } from './touch-gamepad.js';
+import { translator, pickLanguage, isRtl, LANGUAGE_NAMES } from './i18n.js';
+import { parseCatalog, filterApps, appCommand, loadInstalled, updateInstalled, saveInstalled } from './apps.js';
 
 // ui_sidebar_show_* flag -> data-section names it controls.
 export const SECTION_FLAGS = {
@@ -52,13 +54,13 @@ export function visibleSections(st) {
 }
 
 // Share links of the current page: view-only and player 2-4 (gamepad-only) URLs.
-export function sharingLinks(href, st) {
+export function sharingLinks(href, st, t = translator('en')) {
   const base = href.split('#')[0];
   const links = [];
   if (!flag(st, 'enable_sharing')) return links;
-  if (flag(st, 'enable_shared')) links.push({ label: 'view only', url: `${base}#shared` });
+  if (flag(st, 'enable_shared')) links.push({ label: t('sharing.viewOnly'), url: `${base}#shared` });
   for (const n of [2, 3, 4]) {
-    if (flag(st, `enable_player${n}`)) links.push({ label: `player ${n}`, url: `${base}#player${n}` });
+    if (flag(st, `enable_player${n}`)) links.push({ label: t('sharing.player', { n }), url: `${base}#player${n}` });
   }
   return links;
 }
@@ -155,11 +157,11 @@ export function padSvg(pad) {
 
 // System monitor gauges from the server's system_stats / gpu_stats / network_stats
 // messages (server/stats.py; reference system-monitoring.tsx): fractions 0..1.
-export function monitorGauges(stats) {
+export function monitorGauges(stats, t = translator('en')) {
   const frac = (x) => (x == null || Number.isNaN(+x) ? null : Math.max(0, Math.min(1, +x)));
   return [
     { key: 'cpu', label: 'CPU', value: stats.cpu == null ? null : frac(stats.cpu / 100) },
-    { key: 'mem', label: 'memory', value: frac(stats.mem) },
+    { key: 'mem', label: t('monitor.memory'), value: frac(stats.mem) },
     { key: 'gpu', label: 'GPU', value: frac(stats.gpu) },
     { key: 'vram', label: 'VRAM', value: frac(stats.vram) },
   ];
@@ -167,8 +169,14 @@ export function monitorGauges(stats) {
 
 // Keyboard shortcuts panel (reference shortcuts-menu.tsx): label -> soft key combo.
 export const SHORTCUTS = [
-  ['Menu', 'Ctrl+Shift+M'], ['Fullscreen', 'Ctrl+Shift+F'], ['Pointer lock', 'Ctrl+Shift+click'],
+  ['shortcuts.menu', 'Ctrl+Shift+M'], ['shortcuts.fullscreen', 'Ctrl+Shift+F'], ['shortcuts.pointer', 'Ctrl+Shift+click'],
 ];
+
+// Headings of the static index.html blocks -> (section, translation key).
+export const STATIC_HEADS = {
+  Video: ['video', 'section.video'], Audio: ['audio', 'section.audio'], Screen: ['fullscreen', 'section.screen'],
+  Clipboard: ['clipboard', 'section.clipboard'], Files: ['files', 'section.files'], Stats: ['stats', 'section.stats'],
+};
 
 export const DPI_CHOICES = [96, 120, 144, 168, 192, 216, 240, 264, 288];
 export const AUDIO_BITRATES = [64000, 128000, 265000, 320000];
@@ -180,6 +188,10 @@ export class Dashboard {
   constructor(client, doc = document) {
     this.c = client;
     this.doc = doc;
+    const store = typeof localStorage !== 'undefined' ? localStorage : null;
+    const saved = store && store.getItem('selkiesLang');
+    const prefs = typeof navigator !== 'undefined' ? (navigator.languages || [navigator.language]) : [];
+    this.t = translator(pickLanguage(typeof location !== 'undefined' ? location.search : '', [saved, ...prefs]));
     this.rings = Object.fromEntries(STAT_KEYS.map(([k]) => [k, new Ring(60)]));
     this.touchPad = null;
   }
@@ -245,19 +257,24 @@ export class Dashboard {
     const css = this.el('input', { type: 'checkbox' });
     css.checked = !!s.use_css_scaling;
     css.onchange = () => this.c.updateSetting('use_css_scaling', css.checked);
-    sb.appendChild(this.section('screen', 'Resolution', [
-      this.el('label', { text: 'manual resolution' }, [manual]),
+    const t = this.t;
+    if (this.doc.documentElement) {
+      this.doc.documentElement.lang = t.lang;
+      this.doc.documentElement.dir = isRtl(t.lang) ? 'rtl' : 'ltr';
+    }
+    sb.appendChild(this.section('screen', t('section.screen'), [
+      this.el('label', { text: t('screen.manual') }, [manual]),
       this.el('label', {}, [mw, this.el('span', { text: 'x' }), mh,
-        this.el('button', { text: 'apply', onclick: applyRes })]),
-      this.el('label', { text: 'scaling' }, [dpi]),
-      this.el('label', { text: 'CSS scaling (no HiDPI)' }, [css]),
+        this.el('button', { text: t('screen.apply'), onclick: applyRes })]),
+      this.el('label', { text: t('screen.scaling') }, [dpi]),
+      this.el('label', { text: t('screen.css') }, [css]),
     ]));
     // audio bitrate
     const ab = this.el('select', {}, AUDIO_BITRATES.map((b) => this.el('option', { value: b, text: `${b / 1000} kbit/s` })));
     ab.value = s.audio_bitrate || 320000;
     ab.onchange = () => this.c.updateSetting('audio_bitrate', parseInt(ab.value, 10));
     this.audioBitrate = ab;
-    sb.appendChild(this.section('audio', 'Audio quality', [this.el('label', { text: 'bitrate' }, [ab])]));
+    sb.appendChild(this.section('audio', t('section.audio'), [this.el('label', { text: t('audio.bitrate') }, [ab])]));
     // input
     const gaming = this.el('input', { type: 'checkbox' });
     gaming.onchange = () => {
@@ -271,22 +288,29 @@ export class Dashboard {
     const kb = this.el('input', { type: 'text', 'aria-label': 'keyboard', autocapitalize: 'off', autocomplete: 'off',
       style: 'position:absolute;left:-1000px;opacity:0' });
     kb.oninput = () => { if (kb.value) { this.c.input.typeText(kb.value); kb.value = ''; } };
-    sb.appendChild(this.section('gaming', 'Input', [this.el('label', { text: 'gaming mode (pointer lock)' }, [gaming])]));
-    sb.appendChild(this.section('trackpad', '', [this.el('label', { text: 'trackpad mode' }, [tp])]));
-    sb.appendChild(this.section('keyboard', '', [kb, this.el('button', { text: 'on-screen keyboard',
+    sb.appendChild(this.section('gaming', t('section.input'), [this.el('label', { text: t('input.gaming') }, [gaming])]));
+    sb.appendChild(this.section('trackpad', '', [this.el('label', { text: t('input.trackpad') }, [tp])]));
+    sb.appendChild(this.section('keyboard', '', [kb, this.el('button', { text: t('input.keyboard'),
       onclick: () => kb.focus() })]));
-    sb.appendChild(this.section('softkeys', 'Keys', Object.keys(SOFT_KEYS).map((name) => this.el('button', {
+    sb.appendChild(this.section('softkeys', t('section.keys'), Object.keys(SOFT_KEYS).map((name) => this.el('button', {
       text: name, onclick: () => softKeyMessages(name).forEach((m) => this.c.sendText(m)) }))));
-    // apps / command
-    const cmd = this.el('input', { type: 'text', placeholder: 'command', style: 'width:150px' });
-    sb.appendChild(this.section('apps', 'Apps', [this.el('label', {}, [cmd, this.el('button', { text: 'run',
-      onclick: () => { if (cmd.value.trim()) this.c.sendText(`cmd,${cmd.value.trim()}`); } })])]));
+    // apps: catalog with search + install / remove / update, and a free command line
+    const cmd = this.el('input', { type: 'text', placeholder: t('apps.command'), style: 'width:150px' });
+    this.appSearch = this.el('input', { type: 'search', placeholder: t('apps.search'), style: 'width:180px' });
+    this.appList = this.el('div', { style: 'max-height:220px;overflow-y:auto' });
+    this.appSearch.oninput = () => this.renderApps();
+    sb.appendChild(this.section('apps', t('section.apps'), [this.appSearch, this.appList,
+      this.el('label', {}, [cmd, this.el('button', { text: t('apps.run'),
+        onclick: () => { if (cmd.value.trim()) this.c.sendText(`cmd,${cmd.value.trim()}`); } })])]));
+    // files: the server's download directory listing (./files/) in a modal frame
+    sb.appendChild(this.section('files', t('section.files'), [this.el('button', { text: t('files.open'),
+      onclick: () => this.toggleFiles(true) })]));
     // sharing
     this.shareBox = this.el('div');
-    sb.appendChild(this.section('sharing', 'Sharing', [this.shareBox]));
+    sb.appendChild(this.section('sharing', t('section.sharing'), [this.shareBox]));
     // gamepads
     this.padBox = this.el('div', { style: 'white-space:pre;font:12px ui-monospace,monospace' });
-    sb.appendChild(this.section('gamepads', 'Gamepads', [this.padBox, this.el('button', { text: 'touch gamepad',
+    sb.appendChild(this.section('gamepads', t('section.gamepads'), [this.padBox, this.el('button', { text: t('gamepads.touch'),
       onclick: () => { if (!this.touchPad) this.touchPad = new TouchGamepad(); this.touchPad.toggle(); } })]));
     // stats sparklines
     this.sparks = {};
@@ -296,29 +320,95 @@ export class Dashboard {
       this.sparks[k] = { cv, v };
       return this.el('label', { text: label }, [cv, v]);
     });
-    sb.appendChild(this.section('stats', 'Graphs', graphs));
+    sb.appendChild(this.section('stats', t('section.graphs'), graphs));
     // system monitor gauges
     this.gauges = {};
-    const gaugeRows = monitorGauges({}).map((g) => {
+    const gaugeRows = monitorGauges({}, t).map((g) => {
       const bar = this.el('progress', { max: '100', value: '0', style: 'width:130px' });
       this.gauges[g.key] = bar;
       return this.el('label', { text: g.label }, [bar]);
     });
-    sb.appendChild(this.section('stats', 'System monitor', gaugeRows));
+    sb.appendChild(this.section('stats', t('section.monitor'), gaugeRows));
     // gamepad visualiser
     this.padViz = this.el('div');
-    sb.appendChild(this.section('gamepads', 'Gamepad', [this.padViz]));
+    sb.appendChild(this.section('gamepads', t('section.gamepads'), [this.padViz]));
     // shortcuts
-    sb.appendChild(this.section('softkeys', 'Shortcuts', SHORTCUTS.map(([what, keys]) =>
-      this.el('label', { text: what }, [this.el('kbd', { text: keys })]))));
+    sb.appendChild(this.section('softkeys', t('section.shortcuts'), SHORTCUTS.map(([what, keys]) =>
+      this.el('label', { text: t(what) }, [this.el('kbd', { text: keys })]))));
+    // language
+    const lang = this.el('select', {}, Object.entries(LANGUAGE_NAMES).map(([code, name]) =>
+      this.el('option', { value: code, text: name })));
+    lang.value = t.lang;
+    lang.onchange = () => {
+      if (typeof localStorage !== 'undefined') localStorage.setItem('selkiesLang', lang.value);
+      if (typeof location !== 'undefined') location.reload();
+    };
+    sb.appendChild(this.el('div', { 'data-section-lang': '1' }, [this.el('h3', { text: t('section.language') }), lang]));
     this._collapsible(sb);
-    // tag the static sections of index.html
+    // tag (and translate) the static sections of index.html
     for (const h of sb.querySelectorAll(':scope > h3')) {
-      const name = { Video: 'video', Audio: 'audio', Screen: 'fullscreen', Clipboard: 'clipboard', Files: 'files',
-        Stats: 'stats' }[h.textContent.trim()];
-      if (name) h.setAttribute('data-section-head', name);
+      const m = STATIC_HEADS[h.textContent.trim()];
+      if (m) {
+        h.setAttribute('data-section-head', m[0]);
+        h.textContent = t(m[1]);
+      }
     }
+    this.installed = loadInstalled(typeof localStorage !== 'undefined' ? localStorage : null);
+    this.apps = [];
     this.timer = setInterval(() => this.tick(), 1000);
+  }
+
+  // Files modal: the server's ./files/ listing (download directory) in an iframe.
+  toggleFiles(open) {
+    if (!open) {
+      if (this.filesModal) this.filesModal.remove();
+      this.filesModal = null;
+      return;
+    }
+    if (this.filesModal) return;
+    const frame = this.el('iframe', { src: './files/', title: this.t('section.files'),
+      style: 'width:100%;height:calc(100% - 32px);border:0;background:#fff' });
+    this.filesModal = this.el('div', { style: 'position:fixed;inset:8%;z-index:5;background:#18181b;border-radius:6px;padding:4px' }, [
+      this.el('button', { text: this.t('files.close'), onclick: () => this.toggleFiles(false) }), frame]);
+    this.doc.body.appendChild(this.filesModal);
+  }
+
+  async loadApps(url) {
+    try {
+      const r = await fetch(url || './apps.json');
+      if (!r.ok) throw new Error(`HTTP ${r.status}`);
+      this.apps = parseCatalog(await r.json());
+      this.appError = null;
+    } catch (e) {
+      this.apps = [];
+      this.appError = this.t('apps.error');
+    }
+    this.renderApps();
+  }
+
+  appAction(action, name) {
+    this.c.sendText(appCommand(action, name));
+    this.installed = updateInstalled(this.installed, action, name);
+    saveInstalled(typeof localStorage !== 'undefined' ? localStorage : null, this.installed);
+    this.renderApps();
+  }
+
+  renderApps() {
+    if (!this.appList) return;
+    const t = this.t;
+    const shown = filterApps(this.apps || [], this.appSearch ? this.appSearch.value : '');
+    if (!shown.length) {
+      this.appList.replaceChildren(this.el('div', { text: this.appError || t('apps.empty') }));
+      return;
+    }
+    this.appList.replaceChildren(...shown.map((a) => {
+      const have = (this.installed || []).includes(a.name);
+      const acts = have ? ['update', 'remove'] : ['install'];
+      return this.el('div', { title: a.description, style: 'display:flex;gap:6px;align-items:center' }, [
+        this.el('span', { text: a.title, style: 'flex:1' }),
+        ...acts.map((act) => this.el('button', { text: t(`apps.${act}`), onclick: () => this.appAction(act, a.name) })),
+      ]);
+    }));
   }
 
   apply(st) {
@@ -336,10 +426,15 @@ export class Dashboard {
     }
     const toggle = this.doc.getElementById('toggle');
     if (toggle) toggle.style.display = vis.size ? '' : 'none';
-    this.shareBox.replaceChildren(...sharingLinks(location.href, st).map((l) => this.el('div', {}, [
+    this.shareBox.replaceChildren(...sharingLinks(location.href, st, this.t).map((l) => this.el('div', {}, [
       this.el('a', { href: l.url, target: '_blank', text: l.label, style: 'color:#8cf' }),
-      this.el('button', { text: 'copy', onclick: () => navigator.clipboard && navigator.clipboard.writeText(l.url) }),
+      this.el('button', { text: this.t('sharing.copy'), onclick: () => navigator.clipboard && navigator.clipboard.writeText(l.url) }),
     ])));
+    if (vis.has('apps') && !this.appsRequested) {
+      this.appsRequested = true;
+      const u = st.apps_catalog_url;
+      this.loadApps(u && typeof u === 'object' && 'value' in u ? u.value : u);
+    }
     const abDef = st.audio_bitrate;
     if (abDef && abDef.allowed) {
       this.audioBitrate.replaceChildren(...abDef.allowed.map((b) => this.el('option', { value: b, text: `${b / 1000} kbit/s` })));
@@ -364,7 +459,7 @@ export class Dashboard {
       sparkPoints(r, cv.width, cv.height).forEach(([x, y], i) => (i ? g.lineTo(x, y) : g.moveTo(x, y)));
       g.stroke();
     }
-    for (const g of monitorGauges(st)) {
+    for (const g of monitorGauges(st, this.t)) {
       if (this.gauges && this.gauges[g.key]) this.gauges[g.key].value = g.value == null ? 0 : Math.round(g.value * 100);
     }
     if (navigator.getGamepads) {
@@ -372,7 +467,7 @@ export class Dashboard {
       if (this.padViz) this.padViz.innerHTML = pads.length ? padSvg(pads[0]) : '';
       this.padBox.textContent = pads.length ? pads.map((p) => `${p.index}: ${p.id.slice(0, 28)}\n   `
         + `axes ${p.axes.map((a) => a.toFixed(1)).join(' ')}  buttons ${p.buttons.filter((b) => b.pressed).length}`)
-        .join('\n') : 'no gamepads';
+        .join('\n') : this.t('gamepads.none');
     }
   }
 }

@@ -383,3 +383,57 @@ assert.deepEqual(Object.keys(dash.LAYOUTS), ['selkies', 'zinc', 'wish']);
   assert.deepEqual(g.map((x) => x.value), [0.5, 0.25, 1, null]);
 }
 console.log('dashboard layouts ok');
+
+// ---- i18n (reference translations.js languages) and the apps panel helpers
+import('../../selkies_gstreamer_amd/web/lib/i18n.js').then((i18n) => {
+  const langs = Object.keys(i18n.LANGUAGES);
+  assert.deepEqual(langs, ['en', 'es', 'zh', 'hi', 'pt', 'fr', 'ru', 'de', 'tr', 'it', 'nl', 'ar', 'ko', 'ja', 'vi', 'th',
+    'fil', 'da']);
+  const keys = Object.keys(i18n.LANGUAGES.en);
+  for (const l of langs) {
+    assert.deepEqual(Object.keys(i18n.LANGUAGES[l]).sort(), keys.slice().sort(), `keys of ${l}`);
+    assert.ok(i18n.LANGUAGE_NAMES[l], `name of ${l}`);
+    for (const k of keys) if (k.endsWith('player')) assert.ok(i18n.LANGUAGES[l][k].includes('{n}'), `${l} ${k}`);
+  }
+  assert.equal(i18n.pickLanguage('?lang=ja', ['fr']), 'ja');
+  assert.equal(i18n.pickLanguage('', ['xx-YY', 'pt-BR', 'de']), 'pt');
+  assert.equal(i18n.pickLanguage('?lang=zz', []), 'en');
+  const de = i18n.translator('de-DE');
+  assert.equal(de.lang, 'de');
+  assert.equal(de('sharing.player', { n: 3 }), 'Spieler 3');
+  assert.equal(de('no.such.key'), 'no.such.key');
+  assert.equal(i18n.translator('xx')('section.files'), 'Files');
+  assert.equal(i18n.isRtl('ar'), true);
+  assert.equal(i18n.isRtl('fr'), false);
+  const links = dash.sharingLinks('http://h/p#x', { enable_sharing: true, enable_shared: true, enable_player2: true,
+    enable_player3: false, enable_player4: false }, i18n.translator('fr'));
+  assert.deepEqual(links.map((x) => x.label), ['lecture seule', 'joueur 2']);
+  console.log('i18n ok');
+  return import('../../selkies_gstreamer_amd/web/lib/apps.js');
+}).then((apps) => {
+  const cat = apps.parseCatalog({ apps: [
+    { name: 'firefox', full_name: 'Firefox', description: 'Web browser', icon: 'ff.png' },
+    { name: 'gimp', description: 'Image editor' },
+    { name: 'evil; rm -rf /', full_name: 'bad' },
+    { full_name: 'no name' },
+  ] });
+  assert.deepEqual(cat.map((a) => a.name), ['firefox', 'gimp']);
+  assert.equal(cat[1].title, 'gimp');
+  assert.deepEqual(apps.filterApps(cat, 'BROWSER').map((a) => a.name), ['firefox']);
+  assert.deepEqual(apps.filterApps(cat, '').map((a) => a.name), ['firefox', 'gimp']);
+  assert.equal(apps.appCommand('install', 'firefox'), 'cmd,st ~/.local/bin/proot-apps install firefox');
+  assert.throws(() => apps.appCommand('install', 'a b'));
+  assert.throws(() => apps.appCommand('format', 'firefox'));
+  const store = { v: {}, getItem(k) { return this.v[k] || null; }, setItem(k, x) { this.v[k] = x; } };
+  let inst = apps.loadInstalled(store);
+  assert.deepEqual(inst, []);
+  inst = apps.updateInstalled(inst, 'install', 'gimp');
+  inst = apps.updateInstalled(inst, 'install', 'firefox');
+  inst = apps.updateInstalled(inst, 'install', 'gimp');
+  apps.saveInstalled(store, inst);
+  assert.deepEqual(apps.loadInstalled(store), ['firefox', 'gimp']);
+  assert.deepEqual(apps.updateInstalled(inst, 'remove', 'gimp'), ['firefox']);
+  store.v[apps.INSTALLED_KEY] = '{bad json';
+  assert.deepEqual(apps.loadInstalled(store), []);
+  console.log('apps ok');
+});

@@ -250,3 +250,43 @@ def test_static_and_health(tmp_path):
                 assert r.status == 404
         await srv.stop()
     run(main())
+
+
+def test_files_listing_and_download(tmp_path):
+    """The dashboard files panel's ./files/ area: listing (dirs first, escaped names),
+    downloads as attachments, dot files hidden, nothing outside the directory."""
+    async def main():
+        d = tmp_path / "files"
+        (d / "sub").mkdir(parents=True)
+        (d / "a <b>.txt").write_text("hello")
+        (d / "sub" / "x.bin").write_bytes(b"\0\1\2")
+        (d / ".secret").write_text("no")
+        (tmp_path / "outside.txt").write_text("no")
+        s = Settings(["--port", "0"], env={})
+        srv = DataStreamingServer(s, capture_source="synthetic", download_dir=str(d))
+        port = await srv.start("127.0.0.1", 0)
+        base = f"http://127.0.0.1:{port}"
+        async with aiohttp.ClientSession() as sess:
+            async with sess.get(f"{base}/files/") as r:
+                body = await r.text()
+                assert r.status == 200 and "text/html" in r.headers["Content-Type"]
+                assert body.index("sub/") < body.index("a &lt;b&gt;.txt")
+                assert "a%20%3Cb%3E.txt" in body and ".secret" not in body
+            async with sess.get(f"{base}/files/a%20%3Cb%3E.txt") as r:
+                assert r.status == 200 and await r.text() == "hello"
+                assert "attachment" in r.headers["Content-Disposition"]
+            async with sess.get(f"{base}/files/sub", allow_redirects=False) as r:
+                assert r.status == 302 and r.headers["Location"].endswith("/files/sub/")
+            async with sess.get(f"{base}/files/sub/x.bin") as r:
+                assert await r.read() == b"\0\1\2"
+            for bad in ("/files/.secret", "/files/../outside.txt", "/files/%2e%2e/outside.txt"):
+                async with sess.get(base + bad) as r:
+                    assert r.status == 404, bad
+        await srv.stop()
+        srv2 = DataStreamingServer(s, capture_source="synthetic")   # downloads disabled
+        port = await srv2.start("127.0.0.1", 0)
+        async with aiohttp.ClientSession() as sess:
+            async with sess.get(f"http://127.0.0.1:{port}/files/") as r:
+                assert r.status == 404
+        await srv2.stop()
+    run(main())
