@@ -21,7 +21,6 @@
 //   k_commit                 MV-field update (+ plain reference copy when K7 is off)
 //   k_deblock_prep, k_deblock  K7  in-loop deblocking rec -> ref (LDS-ring wavefront)
 #include "h264_gpu.h"
-#include <stdlib.h>
 #include "../codec/color.h"
 #include "../codec/h264_mb.h"
 
@@ -2977,11 +2976,11 @@ void launch_frontend(const FrameArgs& a, hipStream_t s) {
     if (a.me_full) hipLaunchKernelGGL(k_me_mfma, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
-    if (!getenv("SK_EXP_NO_RCK")) hipLaunchKernelGGL(k_rc_qp, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_rc_qp, dim3(1), dim3(64), 0, s, a);
 }
 
 void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, int per_slice, hipStream_t s) {
-    if (!getenv("SK_EXP_NO_RCK")) hipLaunchKernelGGL(k_rc_account, dim3(1), dim3(64), 0, s, a, sizes, n, stride, per_slice);
+    hipLaunchKernelGGL(k_rc_account, dim3(1), dim3(64), 0, s, a, sizes, n, stride, per_slice);
 }
 
 // Transform / quantisation / reconstruction / CAVLC / slice scan of every coded slice.
