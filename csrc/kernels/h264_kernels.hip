@@ -506,11 +506,20 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
 // min of fs_key gives the winner, which k_motion_search adds as a predictor.
 typedef int v4i __attribute__((ext_vector_type(4)));
 
+// LDS row strides are padded against bank conflicts (MI355X_MICROARCH.md §LDS lane
+// groups; modelled per access in tools/lds_bank_model.py): window rows 13 dwords (odd:
+// the box-sum row loads of 48 lanes and the A fragments' two rows per 32-lane group fall
+// on distinct banks), block rows 5 dwords (B fragments read ~17 different rows per
+// group), box-sum rows 36 ints (16-B aligned int4 stores of 8 consecutive lanes cover 32
+// distinct banks; the fs_key reads are int4 too). 1512 -> 584 modelled LDS cycles per MB.
 __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
     constexpr int WW = kFsWin / 4;                       // window dwords per row (12)
-    __shared__ uint32_t win_s[4][kFsWin * WW];           // raw reference window per wave
-    __shared__ uint32_t blk_s[4][64];                    // raw 16x16 source block
-    __shared__ __align__(16) int sq_s[4][kFsWin * 2 * kFsR];   // row box sums of w'^2, then |r_d|^2
+    constexpr int WP = WW + 1;                           // padded window row stride
+    constexpr int BP = 5;                                // padded block row stride
+    constexpr int SP = 2 * kFsR + 4;                     // padded box-sum row stride (ints)
+    __shared__ uint32_t win_s[4][kFsWin * WP];           // raw reference window per wave
+    __shared__ uint32_t blk_s[4][16 * BP];               // raw 16x16 source block
+    __shared__ __align__(16) int sq_s[4][kFsWin * SP];   // row box sums of w'^2, then |r_d|^2
     const int w = threadIdx.x >> 6, l = lane_id();
     const int nmb = a.mb_w * a.mb_h;
     const int idx = xcd_remap(blockIdx.x, gridDim.x) * 4 + w;
@@ -538,10 +547,10 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
     for (int i = l; i < kFsWin * WW; i += 64) {
         const int wy = i / WW, q = i - wy * WW;
         const int y = sk_clip(mby * 16 - kFsR + wy, ylo, yhi);
-        win[i] = load_ref4(a.ref.y + (size_t)y * a.stride_y, mbx * 16 - kFsR + 4 * q, a.stride_y);
+        win[wy * WP + q] = load_ref4(a.ref.y + (size_t)y * a.stride_y, mbx * 16 - kFsR + 4 * q, a.stride_y);
     }
-    blk[l] = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + (l >> 2)) * a.stride_y + mbx * 16 +
-                                                (l & 3) * 4);
+    blk[(l >> 2) * BP + (l & 3)] = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + (l >> 2)) * a.stride_y +
+                                                                     mbx * 16 + (l & 3) * 4);
     wave_sync();
     // |r_d|^2: 16-tap row box sums (lane = window row), then 16-tap column sums in
     // place. Each lane loads its whole row / column into registers before it stores
@@ -550,7 +559,7 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
     if (l < kFsWin) {
         uint32_t rw[WW];
 #pragma unroll
-        for (int q = 0; q < WW; q++) rw[q] = win[l * WW + q];
+        for (int q = 0; q < WW; q++) rw[q] = win[l * WP + q];
         int sqv[kFsWin];
 #pragma unroll
         for (int c = 0; c < kFsWin; c++) {
@@ -569,19 +578,19 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
         }
 #pragma unroll
         for (int x = 0; x < 2 * kFsR; x += 4)
-            *reinterpret_cast<int4*>(&sq[l * 2 * kFsR + x]) = make_int4(out[x], out[x + 1], out[x + 2], out[x + 3]);
+            *reinterpret_cast<int4*>(&sq[l * SP + x]) = make_int4(out[x], out[x + 1], out[x + 2], out[x + 3]);
     }
     wave_sync();
     if (l < 2 * kFsR) {
         int col[kFsWin];
 #pragma unroll
-        for (int r = 0; r < kFsWin; r++) col[r] = sq[r * 2 * kFsR + l];
+        for (int r = 0; r < kFsWin; r++) col[r] = sq[r * SP + l];
         int acc = 0;
 #pragma unroll
         for (int r = 0; r < 16; r++) acc += col[r];
 #pragma unroll
         for (int dy = 0; dy < 2 * kFsR; dy++) {
-            sq[dy * 2 * kFsR + l] = acc;
+            sq[dy * SP + l] = acc;
             acc += col[dy + 16] - col[dy];
         }
     }
@@ -601,12 +610,12 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
             const int src = rr - (16 * nt + i16);        // block row feeding candidate row dyw
             const bool in = src >= 0 && src < 16;
 #pragma unroll
-            for (int q = 0; q < 4; q++) bf[nt][q] = in ? (int)(blk[(in ? src : 0) * 4 + q] ^ 0x80808080u) : 0;
+            for (int q = 0; q < 4; q++) bf[nt][q] = in ? (int)(blk[(in ? src : 0) * BP + q] ^ 0x80808080u) : 0;
         }
 #pragma unroll
         for (int mt = 0; mt < 2; mt++) {
             const int b0 = 16 * mt + i16;                // first window column of candidate dxw
-            const uint32_t* wr = win + rr * WW + (b0 >> 2);
+            const uint32_t* wr = win + rr * WP + (b0 >> 2);
             const int sh = b0 & 3;
             uint32_t w5[5];
 #pragma unroll
@@ -626,13 +635,17 @@ __global__ __launch_bounds__(256) void k_me_mfma(FrameArgs a) {
 #pragma unroll
     for (int mt = 0; mt < 2; mt++)
 #pragma unroll
-        for (int nt = 0; nt < 2; nt++)
+        for (int nt = 0; nt < 2; nt++) {
+            const int dyw = 16 * nt + i16;
+            const int4 sv = *reinterpret_cast<const int4*>(&sq[dyw * SP + 16 * mt + 4 * g]);
+            const int svr[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
             for (int reg = 0; reg < 4; reg++) {
-                const int dxw = 16 * mt + 4 * g + reg, dyw = 16 * nt + i16;
-                const uint64_t k = fs_key(sq[dyw * 2 * kFsR + dxw] - 2 * acc[mt][nt][reg], dyw, dxw);
+                const int dxw = 16 * mt + 4 * g + reg;
+                const uint64_t k = fs_key(svr[reg] - 2 * acc[mt][nt][reg], dyw, dxw);
                 best = k < best ? k : best;
             }
+        }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint64_t other = __shfl_xor(best, o);
