@@ -32,7 +32,7 @@ struct HevcArgs {
     unsigned long long* dbg;    // optional (SK_STAMPS): per CTB row [cycles, entries, bytes, 0]
     // chunk-parallel substream coding (codec/hevc_pcabac.h), chunk = CTB
     uint16_t* srt;              // [ctbs][kCuBinCap] the CTB's context bins sorted by context: index << 1 | bin
-    uint16_t* coff;             // [ctbs][kPcCtxOff] start of each context's run in srt (last = count)
+    uint16_t* coff;             // [ctb_h][kPcCtxOff][ctb_w] start of each context's run in srt (last = count)
     uint32_t* rmap;             // [ctbs][256] end range | shifts << 9, per start range 256..511
     uint32_t* cu_t;             // [ctbs] stream bit offset of the CTB's chunk inside its row substream
     uint16_t* cu_r;             // [ctbs] start range of the chunk

@@ -467,62 +467,39 @@ __device__ __forceinline__ int writelane(int x, int ln, int v) {
     return v;
 }
 
-// Streams the bin entries of CUs [first, first + count) of one CTB row, 64 at a time:
-// every lane loads one entry (coalesced, next chunk prefetched), the wave-uniform loop
-// body reads entry i with a readlane. fn(entry) is wave-uniform.
-template <class F>
-__device__ __forceinline__ void for_each_entry(const HevcArgs& A, int first, int count, F&& fn) {
-    const int l = lane();
-    for (int idx = first; idx < first + count; idx++) {
-        const uint16_t* b = A.bins + (size_t)idx * kCuBinCap;
-        const int nb = __builtin_amdgcn_readfirstlane(A.bin_n[idx]);
-        uint32_t cur = l < nb ? b[l] : 0u;
-        for (int base = 0; base < nb; base += 64) {
-            const uint32_t nxt = base + 64 + l < nb ? b[base + 64 + l] : 0u;   // prefetch
-            const int m = nb - base < 64 ? nb - base : 64;
-            for (int i = 0; i < m; i++) fn((uint32_t)__builtin_amdgcn_readlane((int)cur, i));
-            cur = nxt;
-        }
-    }
-}
-
-// WPP context states at each row start of a slice: lane c owns contexts c, c+64, c+128
-// (one state byte each) and replays the state transitions of the first two CTBs of the
-// row above (no arithmetic coding needed for the states).
-__global__ __launch_bounds__(64) void k_hevc_sync(HevcArgs A) {
+// WPP context states at each row start of a slice (9.3.2.4: the states after the second
+// CTB of the row above). Thread c owns context c and replays only that context's bins
+// of the two CTBs, from k_pc_sort's per-context lists: the chains run in parallel and
+// each is a few entries long.
+__global__ __launch_bounds__(192) void k_hevc_sync(HevcArgs A) {
+    __shared__ uint8_t nlps[64];
     const FrameArgs& f = A.f;
     const SliceTask t = f.tasks[blockIdx.x];
-    const int l = lane();
+    const int c = threadIdx.x;
+    if (c < 64) nlps[c] = CABAC_NEXT_LPS[c];
+    __syncthreads();
+    if (c >= CTX_COUNT) return;
     const int it = t.final_action == ACT_I ? 0 : 1;
-    uint8_t st[3], init[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int c = l + 64 * k;
-        init[k] = st[k] = c < CTX_COUNT ? ctx_init_state(HEVC_CTX_INIT[it][c], t.qp) : 0;
-    }
-    auto store_row = [&](int cy) __attribute__((always_inline)) {
-        uint8_t* dst = A.sync + (size_t)cy * CTX_COUNT;
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-            if (l + 64 * k < CTX_COUNT) dst[l + 64 * k] = st[k];
-    };
-    store_row(t.first_row);
+    const uint8_t init = ctx_init_state(HEVC_CTX_INIT[it][c], t.qp);
+    uint32_t st = init;
+    A.sync[(size_t)t.first_row * CTX_COUNT + c] = init;
     for (int r = 1; r < t.num_rows; r++) {
+        const int prev = t.first_row + r - 1;
         if (f.mb_w >= 2) {
-            for_each_entry(A, (t.first_row + r - 1) * f.mb_w, 2, [&](uint32_t e) __attribute__((always_inline)) {
-                if (e & 0x8000u) return;
-                const int c = e & 0xff;
-                if (c == CTX_TERM || (c & 63) != l) return;
-                const int bin = (e >> 8) & 1;
-                if (c < 64) ctx_update(st[0], bin);
-                else if (c < 128) ctx_update(st[1], bin);
-                else ctx_update(st[2], bin);
-            });
+            const uint16_t* co = A.coff + ((size_t)prev * kPcCtxOff + c) * f.mb_w;
+            for (int cx = 0; cx < 2; cx++) {
+                const uint16_t* sp = A.srt + (size_t)(prev * f.mb_w + cx) * kCuBinCap;
+                const int hi = co[f.mb_w + cx];
+                for (int k = co[cx]; k < hi; k++) {
+                    const uint32_t bin = sp[k] & 1u, mps = st & 1u, s6 = st >> 1;
+                    st = bin == mps ? (((s6 < 62 ? s6 + 1 : 62) << 1) | mps)
+                                    : (((uint32_t)nlps[s6] << 1) | (s6 == 0 ? mps ^ 1u : mps));
+                }
+            }
         } else {
-#pragma unroll
-            for (int k = 0; k < 3; k++) st[k] = init[k];
+            st = init;
         }
-        store_row(t.first_row + r);
+        A.sync[(size_t)(t.first_row + r) * CTX_COUNT + c] = (uint8_t)st;
     }
 }
 
@@ -565,12 +542,15 @@ __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
     }
     int run = inc - sum;
     wsync();
-    uint16_t* co = A.coff + (size_t)idx * kPcCtxOff;
+    // coff is [CTB row][context][CTB column]: k_pc_model and k_hevc_sync read one
+    // context's offsets along a row as one contiguous run
+    const int cy = idx / f.mb_w, cx = idx - cy * f.mb_w;
+    uint16_t* co = A.coff + (size_t)cy * kPcCtxOff * f.mb_w + cx;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         if (3 * l + k < kPcCtxOff) {
             cnt[3 * l + k] = run;
-            co[3 * l + k] = (uint16_t)run;
+            co[(size_t)(3 * l + k) * f.mb_w] = (uint16_t)run;
         }
         run += v[k];
     }
@@ -600,12 +580,11 @@ __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
 
 // One wave per (CTB row, context): the context's state chain along the row, from its
 // WPP start state; each context bin is rewritten in place as a modelled entry (LPS state,
-// is-LPS). The CTBs holding the context are listed with the prefix of their counts, then
-// the chain's entries are gathered 64 at a time (lane = chain position; the next batch
-// is in flight while the current one is modelled) so the serial part runs on registers
-// and only visits the LPS bins.
+// is-LPS). The CTBs holding the context are listed with the prefix of their counts; the
+// chain itself runs as up to 64 speculative segments, one per lane (below).
 __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     __shared__ uint2 lst_s[4][kPcMaxRowCtb + 1];   // (cx | lo << 16, chain position of its first entry)
+    __shared__ uint8_t nl_s[4][64];                // CABAC_NEXT_LPS
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
     const int cy = blockIdx.x, c = blockIdx.y * 4 + w;
@@ -618,9 +597,9 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
         const int cx = g + l;
         int lo = 0, cnt = 0;
         if (cx < f.mb_w) {
-            const uint16_t* co = A.coff + (size_t)(row0 + cx) * kPcCtxOff + c;
+            const uint16_t* co = A.coff + ((size_t)cy * kPcCtxOff + c) * f.mb_w + cx;
             lo = co[0];
-            cnt = co[1] - lo;
+            cnt = co[f.mb_w] - lo;
         }
         int inc = cnt;
 #pragma unroll
@@ -638,57 +617,69 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     if (l == 0) L[n] = make_uint2(0u, (uint32_t)tot);
     wsync();
     if (tot == 0) return;
-    uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane(A.sync[(size_t)cy * CTX_COUNT + c]);
-    // transitions, lane = LPS state: byte 0 = next state byte on the MPS path (MPS 0),
-    // byte 1 = next on the LPS path (with the MPS flip of state 0); XOR the current MPS
-    const int tr_v = (int)(((uint32_t)(l < 62 ? l + 1 : l) << 1) |
-                           ((((uint32_t)CABAC_NEXT_LPS[l] << 1) | (l == 0 ? 1u : 0u)) << 8));
-    int kl = 0;   // this lane's list item (non-decreasing: its chain position only grows)
-    auto gather = [&](int base, uint32_t& v, uint32_t& dst) __attribute__((always_inline)) {
-        const int pos = base + l < tot ? base + l : tot - 1;
-        while ((int)L[kl + 1].y <= pos) kl++;
-        const uint2 it = L[kl];
-        const uint32_t cu = (uint32_t)row0 + (it.x & 0xffffu);
-        v = A.srt[(size_t)cu * kCuBinCap + (it.x >> 16) + (uint32_t)pos - it.y];
-        dst = cu;
-    };
-    // One batch of the chain: MPS runs advance the state by their length (saturating at
-    // 62), so the serial loop steps from LPS to LPS (find-first over the batch's bin mask)
-    // and the lanes of each MPS run take their states in parallel.
-    auto model = [&](int base, uint32_t v, uint32_t dst) __attribute__((always_inline)) {
-        const int m = tot - base < 64 ? tot - base : 64;
-        const uint64_t valid = m == 64 ? ~0ull : ((1ull << m) - 1);
-        const uint64_t ones = __ballot(v & 1u) & valid;
-        int out = 0;
-        int p = 0;
-        for (;;) {
-            const uint32_t st = s >> 1, mps = s & 1u;
-            const uint64_t lpm = (mps ? ~ones : ones) & valid & (p < 64 ? (~0ull << p) : 0ull);
-            const int q = lpm ? (int)__builtin_ctzll(lpm) : m;
-            if (l >= p && l < q) {
-                const uint32_t t = st + (uint32_t)(l - p);
-                out = (int)(kPcModeled | (t < 62u ? t : 62u));
-            }
-            const uint32_t sr = st + (uint32_t)(q - p) < 62u ? st + (uint32_t)(q - p) : 62u;
-            if (q >= m) {
-                s = (sr << 1) | mps;
-                break;
-            }
-            out = writelane((int)(kPcModeled | 64u | sr), q, out);
-            const uint32_t tr = (uint32_t)__builtin_amdgcn_readlane(tr_v, (int)sr);
-            s = ((tr >> 8) & 0xffu) ^ mps;
-            p = q + 1;
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane(A.sync[(size_t)cy * CTX_COUNT + c]);
+    uint8_t* nl = nl_s[w];
+    nl[l] = CABAC_NEXT_LPS[l];
+    wsync();
+    // The chain is cut into up to 64 segments, lane = segment (>= 32 entries each).
+    // Pass 1 runs every segment from a guessed start state; CABAC states forget their
+    // start quickly (MPS runs saturate, LPS steps contract), so segment j-1's end state
+    // from the guess is almost always segment j's true start. Pass 2 runs from those
+    // starts and writes the modelled entries; a start that does not match the true end
+    // of the segment before it is corrected and its segment re-run (loop until none).
+    const int seglen = tot > 64 * 32 ? (tot + 63) / 64 : 32;
+    const int nseg = (tot + seglen - 1) / seglen;
+    const int p0 = l * seglen, p1 = p0 + seglen < tot ? p0 + seglen : tot;
+    const bool act = l < nseg;
+    auto run_seg = [&](uint32_t s, bool write) __attribute__((always_inline)) -> uint32_t {
+        int klo = 0, khi = n;   // the list item holding position p0: L[k].y <= p0 < L[k+1].y
+        while (khi - klo > 1) {
+            const int mid = (klo + khi) >> 1;
+            if ((int)L[mid].y <= p0) klo = mid;
+            else khi = mid;
         }
-        if (l < m) A.bins[(size_t)dst * kCuBinCap + (v >> 1)] = (uint16_t)out;
+        int k = klo;
+        uint2 it = L[k];
+        int nxt = (int)L[k + 1].y;
+        for (int p = p0; p < p1; p += 16) {
+            uint32_t v[16], cu[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) {   // 16 independent loads in flight
+                const int q = p + j < p1 ? p + j : p1 - 1;
+                while (q >= nxt) {
+                    k++;
+                    it = L[k];
+                    nxt = (int)L[k + 1].y;
+                }
+                cu[j] = (uint32_t)row0 + (it.x & 0xffffu);
+                v[j] = A.srt[(size_t)cu[j] * kCuBinCap + (it.x >> 16) + (uint32_t)(q - (int)it.y)];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                if (p + j < p1) {
+                    const uint32_t st6 = s >> 1, mps = s & 1u, lp = (v[j] & 1u) ^ mps;
+                    if (write) A.bins[(size_t)cu[j] * kCuBinCap + (v[j] >> 1)] = (uint16_t)(kPcModeled | (lp << 6) | st6);
+                    s = lp ? (((uint32_t)nl[st6] << 1) | (st6 == 0 ? mps ^ 1u : mps))
+                           : (((st6 < 62u ? st6 + 1u : 62u) << 1) | mps);
+                }
+            }
+        }
+        return s;
     };
-    uint32_t va, da, vb, db;
-    gather(0, va, da);
-    for (int base = 0; base < tot; base += 128) {
-        gather(base + 64, vb, db);
-        model(base, va, da);
-        if (base + 64 >= tot) break;
-        gather(base + 128, va, da);
-        model(base + 64, vb, db);
+    uint32_t e1 = act ? run_seg(s0, false) : 0u;
+    uint32_t T = (uint32_t)__shfl_up((int)e1, 1);
+    if (l == 0) T = s0;
+    bool need = act;
+    for (;;) {
+        const uint32_t e2 = need ? run_seg(T, true) : e1;
+        e1 = e2;   // true end of every segment whose start was right
+        uint32_t tn = (uint32_t)__shfl_up((int)e2, 1);
+        if (l == 0) tn = s0;
+        const uint64_t bad = __ballot(act && tn != T);
+        if (!bad) break;
+        const int first = (int)__builtin_ctzll(bad);
+        need = act && l >= first;
+        if (need) T = tn;
     }
 }
 
@@ -1124,9 +1115,9 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
     else
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
     hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(64), 0, s, a);
     const int nq = (n + 3) / 4;
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(192), 0, s, a);
     hipLaunchKernelGGL(k_pc_model, dim3(a.f.mb_h, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_rmap, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_compose, dim3(a.f.mb_h), dim3(64), 0, s, a);

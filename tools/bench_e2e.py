@@ -210,13 +210,118 @@ def client_worker(ports, args, t_start, t_end) -> dict:
     return asyncio.run(go())
 
 
+class CpuSampler:
+    """Where the CPU goes during the measured window (--sample-cpu): per server process
+    the CPU seconds per second, its busiest thread (the Python main thread holding the
+    GIL shows up here near 1.0) and the native threads; the client processes; and the
+    GPU busy % from rocm-smi. Used to attribute the session-count ceiling."""
+
+    def __init__(self, server_pids, period=0.5):
+        import threading
+        self.pids = sorted(set(server_pids))
+        self.period = period
+        self.samples = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def start(self):
+        self._t.start()
+
+    def stop(self) -> dict:
+        self._stop.set()
+        self._t.join(5)
+        return self.summary()
+
+    def _snap(self):
+        import psutil
+        out = {"t": time.monotonic(), "servers": {}, "clients": 0.0}
+        for pid in self.pids:
+            try:
+                p = psutil.Process(pid)
+                th = {t.id: t.user_time + t.system_time for t in p.threads()}
+                ct = p.cpu_times()
+                out["servers"][pid] = (ct.user + ct.system, th)
+            except (psutil.NoSuchProcess, psutil.AccessDenied):
+                pass
+        me = psutil.Process()
+        for ch in me.children(recursive=True):
+            if ch.pid in self.pids:
+                continue
+            try:
+                ct = ch.cpu_times()
+                out["clients"] += ct.user + ct.system
+            except (psutil.NoSuchProcess, psutil.AccessDenied):
+                pass
+        return out
+
+    def _gpu_busy(self):
+        try:
+            r = subprocess.run(["rocm-smi", "--showuse", "--json"], capture_output=True, text=True, timeout=5)
+            d = json.loads(r.stdout)
+            vals = [float(v.get("GPU use (%)", "nan")) for v in d.values() if isinstance(v, dict)]
+            return max(vals) if vals else None
+        except Exception:   # noqa: BLE001 - optional
+            return None
+
+    def _run(self):
+        prev = self._snap()
+        while not self._stop.wait(self.period):
+            cur = self._snap()
+            dt = cur["t"] - prev["t"]
+            row = {"servers": [], "clients_cpu": (cur["clients"] - prev["clients"]) / dt, "gpu_busy": self._gpu_busy()}
+            for pid, (tot, th) in cur["servers"].items():
+                if pid not in prev["servers"]:
+                    continue
+                ptot, pth = prev["servers"][pid]
+                per = sorted(((th[k] - pth.get(k, th[k])) / dt for k in th), reverse=True)
+                main = (th.get(pid, 0.0) - pth.get(pid, th.get(pid, 0.0))) / dt
+                row["servers"].append({"cpu": (tot - ptot) / dt, "main_thread": main, "busiest_thread": per[0] if per else 0.0,
+                                       "threads_over_half": sum(1 for x in per if x > 0.5)})
+            self.samples.append(row)
+            prev = cur
+
+    def summary(self) -> dict:
+        if not self.samples:
+            return {}
+        import statistics as stt
+        srv = [s for row in self.samples for s in row["servers"]]
+        gb = [row["gpu_busy"] for row in self.samples if row["gpu_busy"] is not None]
+        per_sample_total = [sum(s["cpu"] for s in row["servers"]) for row in self.samples]
+        return {"samples": len(self.samples),
+                "server_procs": len(self.pids),
+                "servers_cpu_total": round(stt.median(per_sample_total), 2),
+                "server_proc_cpu_max": round(max(s["cpu"] for s in srv), 2),
+                "main_thread_cpu_median": round(stt.median(s["main_thread"] for s in srv), 2),
+                "main_thread_cpu_max": round(max(s["main_thread"] for s in srv), 2),
+                "busiest_thread_cpu_max": round(max(s["busiest_thread"] for s in srv), 2),
+                "clients_cpu": round(stt.median(row["clients_cpu"] for row in self.samples), 2),
+                "gpu_busy_median": round(stt.median(gb), 1) if gb else None,
+                "cpus_available": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count(),
+                "cpu_quota": _cgroup_cpus()}
+
+
+def _cgroup_cpus():
+    """CPUs this container may use (cgroup v2 cpu.max quota / period), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 async def run_n(n: int, args) -> dict:
     procs = start_servers(n, args)
+    sampler = None
     try:
         await asyncio.gather(*(wait_ready(port) for _, port, _ in procs))
         t0 = time.monotonic()
         t_start = t0 + args.warmup
         t_end = t_start + args.seconds
+        if getattr(args, "sample_cpu", False):
+            sampler = CpuSampler([p.pid for p, _, _ in procs])
+            loop0 = asyncio.get_running_loop()
+            loop0.call_later(max(0.0, t_start - time.monotonic()), sampler.start)
         ports = [port for _, port, _ in procs]
         shards = [ports[i::args.client_procs] for i in range(min(args.client_procs, n))]
         ctx = multiprocessing.get_context("spawn")
@@ -228,6 +333,7 @@ async def run_n(n: int, args) -> dict:
         for part in parts:
             out.update(part)
     finally:
+        cpu = sampler.stop() if sampler is not None and sampler._t.is_alive() else None
         stop_servers(procs)
         _TAKEN.difference_update(port for _, port, _ in procs)
     fps = np.array([out[p]["frames"] / args.seconds for _, p, _ in procs]) if out else np.zeros(1)
@@ -242,7 +348,7 @@ async def run_n(n: int, args) -> dict:
             "latency_samples": int(len(lat)),
             "frame_latency_p50_ms": round(float(np.percentile(lat_last, 50)), 2) if len(lat_last) else None,
             "frame_latency_p99_ms": round(float(np.percentile(lat_last, 99)), 2) if len(lat_last) else None,
-            "sustained": ok}
+            "sustained": ok, **({"cpu": cpu} if cpu else {})}
 
 
 def main():
@@ -265,6 +371,8 @@ def main():
                     help="sessions per server process (> 1: parallel/multi.py session hosts)")
     ap.add_argument("--sustain", type=float, default=0.97, help="fraction of --fps every session must receive")
     ap.add_argument("--log-dir", default=os.path.join(ROOT, "gpurun_out", "e2e_logs"))
+    ap.add_argument("--sample-cpu", action="store_true",
+                    help="sample server / client CPU (per thread) and GPU busy over the measured window")
     args = ap.parse_args()
     os.makedirs(args.log_dir, exist_ok=True)
     results = []
