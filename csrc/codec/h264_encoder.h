@@ -51,7 +51,7 @@ struct EncoderConfig {
     int rc_mode = RC_CQP;        // K10 rate control (ratecontrol.h): CQP, CRF (qp = CRF value), CBR
     int bitrate_kbps = 0;        // CBR target
     int aq_strength = 0;         // MB-level adaptive QP strength, Q4 (16 = 1.0; 0 = off): h264_mb.h aq_offset
-    int subpel = 1;              // H.264 quarter-pel refinement of P vectors (K4c); HEVC keeps integer vectors
+    int subpel = 1;              // quarter-pel refinement of P vectors (K4c, H.264 and HEVC); AV1 keeps integer vectors
     int intra4x4 = 0;            // H.264 I slices may code MBs as I_NxN (nine 4x4 modes) where cheaper; off
                                  // by default like x264's ultrafast preset (partitions none)
 };

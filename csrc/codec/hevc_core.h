@@ -7,7 +7,7 @@
 // Coding structure (fixed by the parameter sets in hevc_syntax.cpp):
 //   CTB = CU = 16x16 (log2 min CB 4, no split flags), PU 2Nx2N, TU = CU (16x16 luma,
 //   8x8 chroma, no transform split), one reference picture (previous picture),
-//   integer-pel motion, deblocking on (CU edges, deblock_picture), no SAO / sign hiding /
+//   quarter-pel motion (8-tap luma / 4-tap chroma MC), deblocking on (CU edges, deblock_picture), no SAO / sign hiding /
 //   transform skip,
 //   entropy_coding_sync (WPP): one CABAC substream per CTB row, slices = stripes of
 //   whole CTB rows.
@@ -476,6 +476,17 @@ SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int 
     return v;
 }
 
+// Encoder mode decision (open loop, every CU in parallel, so no MPM-dependent cost):
+// all 35 luma modes in this order, first minimum of SAD + bias wins. The four
+// non-directional / axis modes carry no bias; the 31 other directions pay about six
+// bits at the SAD lambda of the QP.
+SK_TABLE int8_t HEVC_INTRA_ORDER[35] = {1,  0,  26, 10, 2,  3,  4,  5,  6,  7,  8,  9,  11, 12, 13, 14, 15, 16,
+                                        17, 18, 19, 20, 21, 22, 23, 24, 25, 27, 28, 29, 30, 31, 32, 33, 34};
+SK_HD bool intra_mode_basic(int mode) { return mode <= 1 || mode == 10 || mode == 26; }
+SK_HD int intra_mode_bias(int mode, int qp) {
+    return intra_mode_basic(mode) ? 0 : 6 * (qp < 12 ? 1 : 1 << ((qp - 12) / 6));
+}
+
 // Most probable modes (8.4.2) for CTB = CU: candB is always DC (above CTB row).
 SK_HD void intra_mpm(int cand_a, int* list) {
     const int cand_b = 1;
@@ -489,6 +500,36 @@ SK_HD void intra_mpm(int cand_a, int* list) {
 }
 
 // ---------------------------------------------------------------------------
+// Luma motion compensation (8.5.3.3.3.1): quarter-pel vectors, 8-tap filters fL
+// (Table 8-12), 8-bit samples (shift1 = 0, shift2 = 6), uni-prediction weighted to 8 bits
+// (shift3 = 6). Written in the separable form every implementation here uses:
+//   h(r) = xFrac ? sum_i fL[xFrac][i] ref(x + i - 3, r) : ref(x, r) << 6
+//   v    = yFrac ? (sum_k fL[yFrac][k] h(y + k - 3)) >> 6 : h(y)
+// which equals the spec's three cases (the << 6 / >> 6 pair is exact).
+SK_TABLE int8_t HEVC_LUMA_FILTER[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+                                          {-1, 4, -10, 58, 17, -5, 1, 0},
+                                          {-1, 4, -11, 40, 40, -11, 4, -1},
+                                          {0, 1, -5, 17, 58, -10, 4, -1}};
+SK_HD int luma_mc_sample(const uint8_t* plane, int stride, int w, int h, int x, int y, int mvx, int mvy) {
+    const int xi = x + (mvx >> 2), yi = y + (mvy >> 2), fx = mvx & 3, fy = mvy & 3;
+    auto P = [&](int xx, int yy) { return (int)plane[(size_t)sk_clip(yy, 0, h - 1) * stride + sk_clip(xx, 0, w - 1)]; };
+    auto H = [&](int yy) {
+        if (!fx) return P(xi, yy) << 6;
+        int s = 0;
+        for (int i = 0; i < 8; i++) s += HEVC_LUMA_FILTER[fx][i] * P(xi + i - 3, yy);
+        return s;
+    };
+    int v;
+    if (!fy) {
+        v = H(yi);
+    } else {
+        v = 0;
+        for (int k = 0; k < 8; k++) v += HEVC_LUMA_FILTER[fy][k] * H(yi + k - 3);
+        v >>= 6;
+    }
+    return sk_clip255((v + 32) >> 6);
+}
+
 // Chroma motion compensation (8.5.3.3.3.3) for integer or fractional luma vectors in
 // quarter-pel (4:2:0: chroma fraction in 1/8), uni-prediction weighted to 8 bits.
 SK_HD int chroma_filter_tap(int frac, int i) {

@@ -180,12 +180,12 @@ void CpuHevcEncoder::code_slice_inter(int s) {
             const int idx = cy * geo.ctb_w + cx;
             CuInfo& cu = cus[idx];
             memset(&cu, 0, sizeof(cu));
-            const int mvx = 4 * fe.me[idx].mvx, mvy = 4 * fe.me[idx].mvy;
+            const int mvx = h264::me_qx(fe.me[idx]), mvy = h264::me_qy(fe.me[idx]);   // quarter-pel (K4c)
             auto nb = [&](int ox, int oy, bool ok) {
                 NbMv m;
                 m.av = ok;
-                m.mvx = ok ? 4 * fe.me[oy * geo.ctb_w + ox].mvx : 0;
-                m.mvy = ok ? 4 * fe.me[oy * geo.ctb_w + ox].mvy : 0;
+                m.mvx = ok ? h264::me_qx(fe.me[oy * geo.ctb_w + ox]) : 0;
+                m.mvy = ok ? h264::me_qy(fe.me[oy * geo.ctb_w + ox]) : 0;
                 return m;
             };
             const bool top = cy > t.first_row;
@@ -196,11 +196,10 @@ void CpuHevcEncoder::code_slice_inter(int s) {
             amvp_list(A1, B1, B0, B2, px, py);
             uint8_t sy[256], su[64], sv[64], pry[256], pru[64], prv[64];
             load_cu_src(cx, cy, sy, su, sv);
-            const int dx = mvx >> 2, dy = mvy >> 2;
             for (int y = 0; y < 16; y++)
                 for (int x = 0; x < 16; x++)
-                    pry[y * 16 + x] = fe.ref[0][(size_t)sk_clip(cy * 16 + y + dy, 0, geo.pic_h - 1) * g.stride_y +
-                                                sk_clip(cx * 16 + x + dx, 0, geo.pic_w - 1)];
+                    pry[y * 16 + x] = (uint8_t)luma_mc_sample(fe.ref[0].data(), g.stride_y, geo.pic_w, geo.pic_h,
+                                                              cx * 16 + x, cy * 16 + y, mvx, mvy);
             for (int y = 0; y < 8; y++)
                 for (int x = 0; x < 8; x++) {
                     pru[y * 8 + x] = (uint8_t)chroma_mc_sample(fe.ref[1].data(), g.stride_c, g.stride_c, g.plane_h_c,
@@ -241,10 +240,6 @@ void CpuHevcEncoder::code_slice_inter(int s) {
         }
 }
 
-// Candidate intra modes (evaluation order; first minimum SAD wins): DC, planar,
-// vertical, horizontal.
-static const int kIntraCand[4] = {1, 0, 26, 10};
-
 // I slices in two passes, like the H.264 intra path: (1) every CU independently
 // chooses its mode against the SOURCE neighbours (parallel on the GPU), (2) the
 // CTB wavefront predicts from the reconstruction with that mode.
@@ -265,12 +260,13 @@ void CpuHevcEncoder::code_slice_intra(int s) {
                 build_intra_ref(P[0].data(), g.stride_y, cx * 16, cy * 16, 16, left, top, tr, refy);
                 if (pass == 0) {
                     int best = 1, best_sad = 0x7fffffff;
-                    for (int k = 0; k < 4; k++) {
+                    for (int k = 0; k < 35; k++) {   // HEVC_INTRA_ORDER, SAD + intra_mode_bias
+                        const int m = HEVC_INTRA_ORDER[k];
                         uint8_t pr[256];
-                        intra_predict(refy, 4, kIntraCand[k], 0, pr);
-                        int sad = 0;
+                        intra_predict(refy, 4, m, 0, pr);
+                        int sad = intra_mode_bias(m, qp);
                         for (int i = 0; i < 256; i++) sad += sk_abs((int)sy[i] - (int)pr[i]);
-                        if (sad < best_sad) { best_sad = sad; best = kIntraCand[k]; }
+                        if (sad < best_sad) { best_sad = sad; best = m; }
                     }
                     memset(&cu, 0, sizeof(cu));
                     cu.mode = CU_INTRA;
@@ -405,6 +401,10 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
                             std::vector<h264::EncodedPacket>& out) {
     fe.load_frame(bgrx, stride);
     fe.ctl_.plan(fe.stripe_dirty.data(), fe.tasks.data());
+    for (auto& st : fe.ctl_.stripes()) {   // K4c gate, rotated by k_plan on the GPU
+        st.subpel_prev = st.subpel_hits;
+        st.subpel_hits = 0;
+    }
     const int ns = geo.num_slices;
     for (int s = 0; s < ns; s++)
         if (fe.tasks[s].action == ACT_P) {
@@ -414,7 +414,10 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
     fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     for (int s = 0; s < ns; s++) {
         switch (fe.tasks[s].final_action) {
-            case ACT_P: code_slice_inter(s); break;
+            case ACT_P:
+                if (fe.cfg.subpel) fe.subpel_refine(s);   // k_subpel
+                code_slice_inter(s);
+                break;
             case ACT_I: code_slice_intra(s); break;
             default: code_slice_skip(s); break;
         }

@@ -2990,6 +2990,9 @@ void launch_frontend(const FrameArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_motion_search, dim3(nmb), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_decide, dim3(a.num_slices), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_rc_qp, dim3(1), dim3(64), 0, s, a);
+    // K4c quarter-pel refinement (H.264 and HEVC; the HEVC back end codes the vectors
+    // with its own 8-tap filters)
+    if (a.subpel) hipLaunchKernelGGL(k_subpel, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
 }
 
 void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, int per_slice, hipStream_t s) {
@@ -3013,7 +3016,6 @@ void launch_encode(const FrameArgs& a, hipStream_t s, bool guard) {
     int nmb = a.mb_w * a.mb_h;
     launch_frontend(a, s);
     if (a.aq_strength > 0) hipLaunchKernelGGL(k_aq, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
-    if (a.subpel) hipLaunchKernelGGL(k_subpel, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
     launch_code(a, s);
     if (guard && a.rc_redo) {   // K10 CBR: VBV overflow -> one coarser pass (kernels exit early otherwise)
         hipLaunchKernelGGL(k_rc_guard, dim3(a.num_slices), dim3(256), 0, s, a);

@@ -1,8 +1,8 @@
 // gfx950 (CDNA4) kernels of the HEVC back end. One 64-lane wavefront per 16x16 CU:
 //   k_hevc_inter       P slices: merge/AMVP decision on the front end's motion field,
-//                      integer luma MC + 4-tap chroma MC, 16x16 / 8x8 DCT (LDS, lane =
+//                      quarter-pel 8-tap luma MC + 4-tap chroma MC, 16x16 / 8x8 DCT (LDS, lane =
 //                      row x 4 columns), quantisation, reconstruction (SKIPALL: all skip)
-//   k_hevc_intra_prep  I slices, every CU in parallel: intra mode against the source
+//   k_hevc_intra_prep  I slices, every CU in parallel: intra mode (all 35) against the source
 //   k_hevc_intra       I slices: CTB wavefront (wave = CTB row, lag 2 = WPP order)
 //   k_hevc_bins        CU syntax -> CABAC bin entries (hevc_core.h code_cu)
 //   k_hevc_sync        WPP: context states at every CTB row start (state-only replay of
@@ -44,6 +44,7 @@ struct CuLds {
     int32_t a[kCoefPerCu];       // residual / dequantised coefficients
     int32_t b[kCoefPerCu];       // transform intermediate
     uint8_t ref[65 + 65 + 33 + 33];   // intra: luma raw | luma filtered | Cb | Cr
+    uint8_t refm[3][64];              // intra, directional modes: main reference arrays (Y, Cb, Cr)
     int misc[4];
     int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];   // inter: merge / AMVP candidates
 };
@@ -206,8 +207,8 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     auto nb = [&](int ox, int oy, bool ok) {
         NbMv m;
         m.av = ok;
-        m.mvx = ok ? 4 * f.me[oy * W + ox].mvx : 0;
-        m.mvy = ok ? 4 * f.me[oy * W + ox].mvy : 0;
+        m.mvx = ok ? h264::me_qx(f.me[oy * W + ox]) : 0;
+        m.mvy = ok ? h264::me_qy(f.me[oy * W + ox]) : 0;
         return m;
     };
     const bool top = cy > t.first_row;
@@ -219,17 +220,44 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     merge_list(A1, B1, B0, B2, mlx, mly);
     amvp_list(A1, B1, B0, B2, px, py);
     wsync();
-    const int mvx = 4 * f.me[idx].mvx, mvy = 4 * f.me[idx].mvy;
+    const int mvx = h264::me_qx(f.me[idx]), mvy = h264::me_qy(f.me[idx]);   // quarter-pel (k_subpel)
     const int pic_w = f.stride_y, pic_h = f.mb_h * 16;
     load_src(L, f, cx, cy);
-    {   // luma integer MC: lane = row l >> 2, 4 columns
-        const int dx = mvx >> 2, dy = mvy >> 2;
+    {   // luma MC (hevc_core.h luma_mc_sample, separable form): the 23x23 integer window
+        // into LDS (L.a as bytes, row pitch 24), horizontal 8-tap pass into L.b (23 rows x
+        // 16), vertical pass into pred (lane = row l >> 2, 4 columns). L.a / L.b are free
+        // until code_cu_wave.
+        const int fx = mvx & 3, fy = mvy & 3;
+        const int x0 = cx * 16 + (mvx >> 2) - 3, y0 = cy * 16 + (mvy >> 2) - 3;
+        uint8_t* win = reinterpret_cast<uint8_t*>(L.a);
+        for (int i = l; i < 23 * 23; i += 64) {
+            const int r = i / 23, c = i - r * 23;
+            win[r * 24 + c] = f.ref.y[(size_t)sk_clip(y0 + r, 0, pic_h - 1) * f.stride_y + sk_clip(x0 + c, 0, pic_w - 1)];
+        }
+        wsync();
+        for (int i = l; i < 23 * 16; i += 64) {
+            const uint8_t* w = win + (i >> 4) * 24 + (i & 15);
+            int s = (int)w[3] << 6;
+            if (fx) {
+                s = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) s += HEVC_LUMA_FILTER[fx][k] * (int)w[k];
+            }
+            L.b[i] = s;
+        }
+        wsync();
         const int y = l >> 2;
-        const uint8_t* row = f.ref.y + (size_t)sk_clip(cy * 16 + y + dy, 0, pic_h - 1) * f.stride_y;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int x = 4 * (l & 3) + k;
-            L.pred[y * 16 + x] = row[sk_clip(cx * 16 + x + dx, 0, pic_w - 1)];
+            int v = L.b[(y + 3) * 16 + x];
+            if (fy) {
+                v = 0;
+#pragma unroll
+                for (int j = 0; j < 8; j++) v += HEVC_LUMA_FILTER[fy][j] * L.b[(y + j) * 16 + x];
+                v >>= 6;
+            }
+            L.pred[y * 16 + x] = (uint8_t)sk_clip255((v + 32) >> 6);
         }
         // chroma: lane -> component l >> 5, row (l >> 2) & 7, 2 columns
         const int c = l >> 5, r = (l >> 2) & 7;
@@ -328,18 +356,62 @@ __device__ __forceinline__ int dc_value(const uint8_t* r, int n, int log2n) {
     else if (l < 2 * n) v = r[2 * n - 1 - (l - n)];   // left
     return (wsum(v) + n) >> (log2n + 1);
 }
+// Main reference array of a directional mode (8.4.4.2.6) for an n x n block from the
+// linear reference r: out[k + n] = ref[k], k = -n .. 2n (lane = k + n), with the other side
+// projected through invAngle for negative angles (entries no sample reads stay 0).
+__device__ __forceinline__ void build_refm(const uint8_t* r, int n, int mode, uint8_t* out) {
+    const int k = lane() - n;
+    if (k > 2 * n) return;
+    const int angle = HEVC_INTRA_ANGLE[mode];
+    const bool vert = mode >= 18;
+    int v = 0;
+    if (k >= 0) {
+        v = vert ? r[2 * n + k] : r[2 * n - k];   // p[k-1][-1] / p[-1][k-1]
+    } else if (angle < 0) {
+        const int last = (n * angle) >> 5;
+        if (last < -1 && k >= last) {
+            const int j = (k * intra_inv_angle(mode) + 128) >> 8;
+            v = vert ? r[2 * n - j] : r[2 * n + j];
+        }
+    }
+    out[k + n] = (uint8_t)v;
+}
+// Directional prediction sample (x, y) from build_refm's array (intra_pred_sample's
+// angular branch; the axis modes 10 / 26 go through pred_fast).
+__device__ __forceinline__ int pred_angular(const uint8_t* refm, int n, int mode, int x, int y) {
+    const int angle = HEVC_INTRA_ANGLE[mode];
+    const bool vert = mode >= 18;
+    const int a = vert ? y : x, b = vert ? x : y;
+    const int idx = ((a + 1) * angle) >> 5, fact = ((a + 1) * angle) & 31;
+    const uint8_t* p = refm + n + b + idx + 1;
+    return fact ? ((32 - fact) * (int)p[0] + fact * (int)p[1] + 16) >> 5 : (int)p[0];
+}
+// Luma references of `mode` for a 16x16 CU: the [1 2 1]-filtered copy when filterFlag.
+__device__ __forceinline__ const uint8_t* luma_ref(const CuLds& L, int mode) {
+    return intra_filter_flag(mode, 4, 0) ? L.ref + 65 : L.ref;
+}
 // Intra prediction of the whole CU into L.pred for `mode` (refs in L.ref).
 __device__ __forceinline__ void intra_pred_cu(CuLds& L, int mode) {
     const int l = lane();
-    uint8_t* ry = (mode == 0) ? L.ref + 65 : L.ref;   // luma planar uses the filtered references
+    const uint8_t* ry = luma_ref(L, mode);
+    const bool basic = intra_mode_basic(mode);
     const int dcy = dc_value(L.ref, 16, 4);
     const int dcu = dc_value(L.ref + 130, 8, 3), dcv = dc_value(L.ref + 163, 8, 3);
+    if (!basic) {
+        build_refm(ry, 16, mode, L.refm[0]);
+        build_refm(L.ref + 130, 8, mode, L.refm[1]);
+        build_refm(L.ref + 163, 8, mode, L.refm[2]);
+        wsync();
+    }
     for (int i = l; i < kCoefPerCu; i += 64) {
         int v;
-        if (i < 256) v = pred_fast(ry, 16, 4, mode, true, dcy, i & 15, i >> 4);
-        else {
+        if (i < 256) {
+            v = basic ? pred_fast(ry, 16, 4, mode, true, dcy, i & 15, i >> 4)
+                      : pred_angular(L.refm[0], 16, mode, i & 15, i >> 4);
+        } else {
             const int j = i - 256, c = j >> 6;
-            v = pred_fast(L.ref + 130 + 33 * c, 8, 3, mode, false, c ? dcv : dcu, j & 7, (j >> 3) & 7);
+            v = basic ? pred_fast(L.ref + 130 + 33 * c, 8, 3, mode, false, c ? dcv : dcu, j & 7, (j >> 3) & 7)
+                      : pred_angular(L.refm[1 + c], 8, mode, j & 7, (j >> 3) & 7);
         }
         L.pred[i] = (uint8_t)v;
     }
@@ -372,15 +444,22 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     wsync();
     const int l = lane();
     const int dc = dc_value(L.ref, 16, 4);
-    const int cand[4] = {1, 0, 26, 10};
     int best = 1, best_sad = 0x7fffffff;
-    for (int k = 0; k < 4; k++) {
-        const int m = cand[k];
-        const uint8_t* r = m == 0 ? L.ref + 65 : L.ref;
+    for (int k = 0; k < 35; k++) {   // HEVC_INTRA_ORDER, SAD + intra_mode_bias (hevc_cpu.cpp)
+        const int m = HEVC_INTRA_ORDER[k];
+        const uint8_t* r = luma_ref(L, m);
+        const bool basic = intra_mode_basic(m);
+        if (!basic) {
+            build_refm(r, 16, m, L.refm[0]);
+            wsync();
+        }
         int sad = 0;
-        for (int i = l; i < 256; i += 64) sad += sk_abs((int)L.src[i] - pred_fast(r, 16, 4, m, true, dc, i & 15, i >> 4));
-        sad = wsum(sad);
+        for (int i = l; i < 256; i += 64)
+            sad += sk_abs((int)L.src[i] - (basic ? pred_fast(r, 16, 4, m, true, dc, i & 15, i >> 4)
+                                                 : pred_angular(L.refm[0], 16, m, i & 15, i >> 4)));
+        sad = wsum(sad) + intra_mode_bias(m, t.qp);
         if (sad < best_sad) { best_sad = sad; best = m; }
+        wsync();   // refm is rebuilt by the next mode
     }
     if (l == 0) {
         CuInfo cu;

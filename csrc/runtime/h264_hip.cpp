@@ -432,7 +432,7 @@ class HipBackend : public EncoderBackend {
         a.deblock = cfg_.deblock;
         a.me_full = cfg_.me_full;
         a.aq_strength = cfg_.codec == 1 ? 0 : cfg_.aq_strength;
-        a.subpel = cfg_.codec == 1 ? 0 : cfg_.subpel;
+        a.subpel = cfg_.codec == 2 ? 0 : cfg_.subpel;   // AV1 keeps integer vectors (av1_encoder.h front_config)
         a.intra4x4 = cfg_.codec == 1 ? 0 : cfg_.intra4x4;
         a.aq = dmalloc<int8_t>(nmb);
         for (int k = 0; k < kOverlaySlots; k++) {

@@ -192,10 +192,16 @@ def build_rtc_config(args) -> dict:
 
 
 class StreamSession:
-    """One browser peer: capture → H.264 → RTP, data-channel input and telemetry."""
+    """One browser peer. media="video" (the reference's uid 0 -> 1 call): capture ->
+    H.264 / H.265 / AV1 -> RTP, data-channel input and telemetry; media="audio" (uid 2 ->
+    3, webrtc.py:554-557, 581, 720-722): the Opus pipeline alone on its own connection;
+    media="both": one connection carrying everything."""
 
-    def __init__(self, args, send_sdp, send_ice, input_factory=None, addresses=None):
+    def __init__(self, args, send_sdp, send_ice, input_factory=None, addresses=None, media: str = "both",
+                 peers: Optional[dict] = None):
         self.args = args
+        self.media = media
+        self.peers = peers if peers is not None else {}   # media -> live session (ab, on the video peer)
         from selkies_gstreamer_amd.legacy.pipeline import AV1_ENCODERS, H265_ENCODERS
         self.hevc = str(getattr(args, "encoder", "")) in H265_ENCODERS
         self.av1 = str(getattr(args, "encoder", "")) in AV1_ENCODERS
@@ -203,7 +209,8 @@ class StreamSession:
         self.fps = int(args.framerate)
         self.rc = RateController(int(args.video_bitrate) * 1000, self.fps)
         stun_srv, turn_srv = ice_servers_from_rtc(build_rtc_config(args))
-        self.pc = PeerConnection(addresses=addresses, video=True, audio=True, data=True,
+        self.pc = PeerConnection(addresses=addresses, video=media != "audio", audio=media != "video",
+                                 data=media != "audio",
                                  video_codec="H265" if self.hevc else ("AV1" if self.av1 else "H264"),
                                  stun_server=stun_srv,
                                  turn_server=turn_srv,
@@ -236,6 +243,9 @@ class StreamSession:
         self.pc.on_state = self._on_state
         offer = await self.pc.create_offer()
         await self.send_sdp("offer", offer)
+        self.peers[self.media] = self
+        if self.media == "audio":
+            return
         self.channel = self.pc.create_data_channel("input")
         self.channel.on_message = lambda m: asyncio.ensure_future(self.on_message(m)) if isinstance(m, str) else None
         self.channel.on_open = self._on_channel_open
@@ -264,6 +274,9 @@ class StreamSession:
 
     # -- media --------------------------------------------------------------------------------
     async def _start_media(self) -> None:
+        if self.media == "audio":
+            self._tasks.append(asyncio.ensure_future(self._start_audio()))
+            return
         import pixelflux
         src = {"x11": 0, "synthetic": 2}.get(self.args.capture_source, -1)
         w, h = self.width, self.height
@@ -287,7 +300,8 @@ class StreamSession:
         self._stripe_cb = pixelflux.StripeCallback(on_stripe)
         await loop.run_in_executor(None, self.capture.start_capture, s, self._stripe_cb)
         self._tasks.append(asyncio.ensure_future(self._telemetry_loop()))
-        self._tasks.append(asyncio.ensure_future(self._start_audio()))
+        if self.media == "both":
+            self._tasks.append(asyncio.ensure_future(self._start_audio()))
         kd = int(self.args.keyframe_distance)
         if kd > 0:
             self._tasks.append(asyncio.ensure_future(self._keyframe_loop(kd)))
@@ -316,6 +330,13 @@ class StreamSession:
                                    int(self.args.audio_channels))
         if not await self.audio.start(int(self.args.audio_bitrate)):
             self.audio = None
+
+    async def restart_audio(self) -> None:
+        """New Opus bitrate: the running audio pipeline is rebuilt at args.audio_bitrate."""
+        if self.audio is not None:
+            aud, self.audio = self.audio, None
+            await aud.stop()
+            await self._start_audio()
 
     def _keyframe(self) -> None:
         if self.capture is not None:
@@ -359,6 +380,8 @@ class StreamSession:
                 save_overlay(self.args.json_config, self.args)
             elif t == "ab":
                 self.args.audio_bitrate = str(int(toks[1]))
+                aud = self.peers.get("audio", self) if self.media == "video" else self
+                await aud.restart_audio()   # the Opus encoder takes the new rate (audio peer's pipeline)
                 self.send_message("pipeline", {"status": f"Audio bitrate set to: {int(toks[1])}"})
                 save_overlay(self.args.json_config, self.args)
             elif t == "_arg_fps":
@@ -437,6 +460,8 @@ class StreamSession:
         if self.closed.is_set():
             return
         self.closed.set()
+        if self.peers.get(self.media) is self:
+            del self.peers[self.media]
         for t in self._tasks:
             t.cancel()
         if self.audio is not None:
@@ -459,7 +484,8 @@ def _run_hook(cmd: str) -> None:
 
 
 async def serve(args, input_factory=None, addresses=None, stop: Optional[asyncio.Event] = None) -> None:
-    """Signalling server + the streaming peer (uid 0) calling the browser (uid 1) in a loop."""
+    """Signalling server + the streaming peers calling the browser in loops: video and input
+    (uid 0 -> 1) and audio (uid 2 -> 3)."""
     if _truthy(args.app_wait_ready):
         while not os.path.exists(args.app_ready_file):
             await asyncio.sleep(0.2)
@@ -483,15 +509,22 @@ async def serve(args, input_factory=None, addresses=None, stop: Optional[asyncio
     scheme = "wss" if _truthy(args.enable_https) else "ws"
     auth = (args.basic_auth_user, args.basic_auth_password) if (_truthy(args.enable_basic_auth) and
                                                                args.basic_auth_password) else None
-    try:
+    url = f"{scheme}://127.0.0.1:{port}/ws"
+    peers: dict = {}
+
+    async def loop(my_id, peer_id, media):
         while not stop.is_set():
-            await _one_session(f"{scheme}://127.0.0.1:{port}/ws", args, auth, input_factory, addresses, stop)
+            await _one_session(url, args, auth, input_factory, addresses, stop, my_id, peer_id, media, peers)
+    try:
+        # two calls like the reference: video + input (0 -> 1) and audio (2 -> 3)
+        await asyncio.gather(loop(0, 1, "video"), loop(2, 3, "audio"))
     finally:
         await server.stop()
 
 
-async def _one_session(url, args, auth, input_factory, addresses, stop) -> None:
-    sig = SignallingClient(url, 0, basic_auth=auth, ssl=False)
+async def _one_session(url, args, auth, input_factory, addresses, stop, my_id=0, peer_id=1, media="both",
+                       peers=None) -> None:
+    sig = SignallingClient(url, my_id, basic_auth=auth, ssl=False)
     await sig.connect()
     session: dict = {}
     done = asyncio.Event()
@@ -503,9 +536,11 @@ async def _one_session(url, args, auth, input_factory, addresses, stop) -> None:
         await sig.send_ice(idx, cand)
 
     async def start_session():
-        s = StreamSession(args, send_sdp, send_ice, input_factory, addresses)
+        s = StreamSession(args, send_sdp, send_ice, input_factory if media != "audio" else None, addresses,
+                          media=media, peers=peers)
         session["s"] = s
-        _run_hook(args.start_after_connect)
+        if media != "audio":
+            _run_hook(args.start_after_connect)
         await s.start()
         await s.closed.wait()
         done.set()
@@ -515,12 +550,12 @@ async def _one_session(url, args, auth, input_factory, addresses, stop) -> None:
             async def retry():
                 await asyncio.sleep(1.0)
                 if not done.is_set() and "s" not in session:
-                    await sig.setup_call(1)
+                    await sig.setup_call(peer_id)
             asyncio.ensure_future(retry())
         else:
             log.error("signalling: %s", e)
 
-    sig.on_connect = lambda: asyncio.ensure_future(sig.setup_call(1))
+    sig.on_connect = lambda: asyncio.ensure_future(sig.setup_call(peer_id))
     sig.on_session = lambda meta: asyncio.ensure_future(start_session())
     sig.on_sdp = lambda kind, text: asyncio.ensure_future(session["s"].on_remote_sdp(kind, text)) \
         if "s" in session else None
@@ -533,7 +568,8 @@ async def _one_session(url, args, auth, input_factory, addresses, stop) -> None:
     stopper.cancel()
     if "s" in session:
         await session["s"].stop()
-        _run_hook(args.start_after_disconnect)
+        if media != "audio":
+            _run_hook(args.start_after_disconnect)
     reader.cancel()
     await sig.stop()
 

@@ -1,8 +1,10 @@
 // WebRTC-mode client core (reference addons/gst-web/src/{signaling.js,
 // webrtc.js,app.js}, SURVEY C38): GStreamer-demo signalling over a websocket,
-// an RTCPeerConnection answering the server's offer, the "input" data channel
-// carrying the same input vocabulary as the websocket mode, and the server's
-// {"type":..., "data":...} telemetry/control messages.
+// two RTCPeerConnections answering the server's offers (video + "input" data
+// channel as peer 1, audio alone as peer 3: app.js:375-378), answer-SDP munging
+// (webrtc.js:271-320), the "input" data channel carrying the same input
+// vocabulary as the websocket mode, the server's {"type":..., "data":...}
+// telemetry/control messages and getStats reports (webrtc.js:494).
 
 export class Signalling {
   // peerId 1 is the browser; the streaming server registers as 0 and calls us.
@@ -62,9 +64,51 @@ export function parseServerMessage(text) {
   return msg;
 }
 
+// Answer-SDP munging before setLocalDescription (the browser's defaults are not what a
+// desktop stream wants): H.264 parameter sets travel with every IDR
+// (sps-pps-idr-in-keyframe=1), and unless the session uses multiopus, Opus is stereo
+// with 10 ms packets (stereo=1, minptime=10). Existing values are overridden, missing
+// ones are inserted before the fmtp parameter they belong with.
+export function mungeAnswerSdp(sdp) {
+  const set = (text, key, value, anchor, present) => {
+    if (new RegExp(`[^-]${key}=${value}[^\\d]`).test(text) || !new RegExp(`[^-]${anchor}=`).test(text)) return text;
+    if (present.test(text)) return text.replace(new RegExp(`${key}=\\d+`, 'g'), `${key}=${value}`);
+    return text.split(`${anchor}=`).join(`${key}=${value};${anchor}=`);
+  };
+  let out = set(sdp, 'sps-pps-idr-in-keyframe', '1', 'packetization-mode', /[^-]sps-pps-idr-in-keyframe=\d+/);
+  if (out.indexOf('multiopus') === -1) {
+    out = set(out, 'stereo', '1', 'useinbandfec', /[^-]stereo=\d+/);
+    out = set(out, 'minptime', '10', 'useinbandfec', /[^-]minptime=\d+/);
+  }
+  return out;
+}
+
+// Flattens an RTCStatsReport into the server's _stats_video / _stats_audio payloads:
+// the inbound-rtp entry of the kind, its codec, and the selected candidate pair.
+export function summariseStats(report, kind) {
+  const byId = new Map();
+  report.forEach((s) => byId.set(s.id, s));
+  const out = {};
+  report.forEach((s) => {
+    if (s.type === 'inbound-rtp' && s.kind === kind) {
+      Object.assign(out, s);
+      const codec = s.codecId && byId.get(s.codecId);
+      if (codec) out.codec = { mimeType: codec.mimeType, clockRate: codec.clockRate, sdpFmtpLine: codec.sdpFmtpLine };
+    }
+    if (s.type === 'candidate-pair' && (s.selected || s.nominated) && s.state === 'succeeded') {
+      out.transport = { currentRoundTripTime: s.currentRoundTripTime, availableIncomingBitrate: s.availableIncomingBitrate,
+        bytesReceived: s.bytesReceived };
+    }
+  });
+  return out;
+}
+
 export class WebRTCClient {
-  constructor(video, signalling, rtcConfig = {}, RTCPeerConnectionImpl = globalThis.RTCPeerConnection) {
+  // media: 'video' (peer 1: video + input channel) or 'audio' (peer 3: audio only); the
+  // element is the <video> or <audio> the remote track plays in.
+  constructor(video, signalling, rtcConfig = {}, RTCPeerConnectionImpl = globalThis.RTCPeerConnection, media = 'video') {
     this.video = video;
+    this.media = media;
     this.sig = signalling;
     this.rtcConfig = rtcConfig;
     this.PC = RTCPeerConnectionImpl;
@@ -83,7 +127,7 @@ export class WebRTCClient {
     this.reset();
     this.pc = new this.PC(this.rtcConfig);
     this.pc.ontrack = (ev) => {
-      if (ev.track.kind === 'video' && this.video) {
+      if (ev.track.kind === this.media && this.video) {
         this.video.srcObject = ev.streams[0] || new MediaStream([ev.track]);
         this.video.play && this.video.play().catch(() => {});
       }
@@ -93,8 +137,7 @@ export class WebRTCClient {
     this.pc.ondatachannel = (ev) => this.bindChannel(ev.channel);
     await this.pc.setRemoteDescription(sdp);
     const answer = await this.pc.createAnswer();
-    // keep latency minimal: no jitter buffering beyond what the stream needs
-    await this.pc.setLocalDescription(answer);
+    await this.pc.setLocalDescription({ type: answer.type, sdp: mungeAnswerSdp(answer.sdp) });
     this.sig.sendSdp(this.pc.localDescription);
   }
 
@@ -136,18 +179,18 @@ export class WebRTCClient {
   requestResolution(w, h) { this.send(`r,${w & ~1}x${h & ~1}`); }
   setScaling(ratio) { this.send(`s,${ratio}`); }
 
-  // Reports client-side stats (getStats) as _stats_video / _stats_audio JSON.
-  async reportStats() {
+  // Reports client-side stats (getStats) as _stats_video / _stats_audio JSON over this
+  // peer's input channel; `audioPeer` (the separate audio connection) supplies the audio
+  // half, as in the reference's two-peer client.
+  async reportStats(audioPeer = null) {
     if (!this.pc || !this.pc.getStats) return;
-    const report = await this.pc.getStats();
-    const video = {}, audio = {};
-    report.forEach((s) => {
-      if (s.type === 'inbound-rtp' && s.kind === 'video') Object.assign(video, s);
-      if (s.type === 'inbound-rtp' && s.kind === 'audio') Object.assign(audio, s);
-    });
+    const video = summariseStats(await this.pc.getStats(), 'video');
+    let audio = summariseStats(await this.pc.getStats(), 'audio');
+    if (audioPeer && audioPeer.pc && audioPeer.pc.getStats) audio = summariseStats(await audioPeer.pc.getStats(), 'audio');
     if (video.framesPerSecond !== undefined) this.send(`_f,${Math.round(video.framesPerSecond)}`);
     this.send('_stats_video,' + JSON.stringify(video));
     this.send('_stats_audio,' + JSON.stringify(audio));
+    return { video, audio };
   }
 
   reset() {

@@ -137,6 +137,10 @@ class PeerConnection:
                 self.dtls_role = "client"
             self._apply_negotiated()
         else:
+            # an offer without an application section (e.g. the audio-only peer) gets no
+            # SCTP association: the answerer would wait for one that never comes
+            if not any(m.kind == "application" for m in self.remote_sdp.media):
+                self.want["data"] = False
             # JSEP: the offerer controls unless it is ICE-lite
             await self._gather(controlling=self.remote_sdp.ice_lite)
         if tr["ufrag"] is None or tr["pwd"] is None or tr["fingerprint"] is None:

@@ -213,7 +213,7 @@ assert.equal(downsampleToS16Mono([a, b], 48000)[10], 0);
 console.log('client tests ok');
 
 // ---- WebRTC mode (lib/webrtc.js) with fake WebSocket / RTCPeerConnection ----
-import { Signalling, WebRTCClient, parseServerMessage } from '../../selkies_gstreamer_amd/web/lib/webrtc.js';
+import { Signalling, WebRTCClient, parseServerMessage, mungeAnswerSdp, summariseStats } from '../../selkies_gstreamer_amd/web/lib/webrtc.js';
 
 class FakeWS {
   constructor(url) { this.url = url; this.sent = []; FakeWS.last = this; }
@@ -268,6 +268,37 @@ class FakePC {
   client.requestResolution(1921, 1081);
   assert.deepEqual(ch.sent.slice(1), ['vb,2500', 'r,1920x1080']);
   assert.equal(parseServerMessage('nope'), null);
+  // answer munging (reference webrtc.js:271-320)
+  const ans = 'a=fmtp:102 level-asymmetry-allowed=1;packetization-mode=1;profile-level-id=42e01f\r\n' +
+    'a=fmtp:111 minptime=20;useinbandfec=1\r\n';
+  const m = mungeAnswerSdp(ans);
+  assert.ok(m.includes('sps-pps-idr-in-keyframe=1;packetization-mode=1'));
+  assert.ok(m.includes('minptime=10;') && !m.includes('minptime=20'));
+  assert.ok(m.includes('stereo=1;useinbandfec=1'));
+  assert.equal(mungeAnswerSdp(m), m);   // idempotent
+  assert.ok(mungeAnswerSdp('a=fmtp:102 sps-pps-idr-in-keyframe=0;packetization-mode=1\r\n').includes('sps-pps-idr-in-keyframe=1;'));
+  const multi = 'a=rtpmap:100 multiopus/48000/6\r\na=fmtp:100 useinbandfec=1\r\n';
+  assert.equal(mungeAnswerSdp(multi), multi);
+  // the answer the client sends is the munged one
+  const client2 = new WebRTCClient(null, sig, {}, class extends FakePC { async createAnswer() { return { type: 'answer', sdp: ans }; } });
+  await client2.onSdp({ type: 'offer', sdp: 'v=0 offer' });
+  assert.ok(JSON.parse(FakeWS.last.sent[FakeWS.last.sent.length - 1]).sdp.sdp.includes('stereo=1'));
+  // stats: video from the video peer, audio from the separate audio peer
+  const rep = (entries) => ({ forEach: (f) => entries.forEach(f) });
+  const vpc = { getStats: async () => rep([{ id: 'c1', type: 'codec', mimeType: 'video/H264', clockRate: 90000 },
+    { id: 'v', type: 'inbound-rtp', kind: 'video', framesPerSecond: 59.6, codecId: 'c1' },
+    { id: 'p', type: 'candidate-pair', nominated: true, state: 'succeeded', currentRoundTripTime: 0.004 }]) };
+  const apc = { getStats: async () => rep([{ id: 'a', type: 'inbound-rtp', kind: 'audio', packetsLost: 3 }]) };
+  assert.equal(summariseStats(await vpc.getStats(), 'video').codec.mimeType, 'video/H264');
+  const vc = new WebRTCClient(null, sig, {}, FakePC);
+  vc.pc = vpc;
+  const chv = new FakeChannel();
+  vc.channel = chv;
+  const st = await vc.reportStats({ pc: apc });
+  assert.equal(st.audio.packetsLost, 3);
+  assert.equal(st.video.transport.currentRoundTripTime, 0.004);
+  assert.equal(chv.sent[0], '_f,60');
+  assert.ok(chv.sent[1].startsWith('_stats_video,') && chv.sent[2].startsWith('_stats_audio,'));
   assert.deepEqual(parseServerMessage('{"type":"system","data":{"action":"reload"}}').action, ['reload', '']);
 })().then(() => console.log('webrtc client ok'), (e) => { console.error(e); process.exit(1); });
 

@@ -105,3 +105,28 @@ def test_hevc_chunk_parallel_cabac_model_is_exact(kind, qp, monkeypatch):
         a = [p.data for p in ref.encode(f, t)]
         b = [p.data for p in par.encode(f, t)]
         assert a == b, f"frame {t}"
+
+
+def _diagonal(W, H):
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    v = 128 + 90 * np.sin((xx * 0.8 + yy * 0.45) / 3.1)
+    f = np.zeros((H, W, 4), np.uint8)
+    f[..., 0] = f[..., 1] = f[..., 2] = np.clip(v, 0, 255)
+    return f
+
+
+def test_hevc_directional_intra_modes():
+    """All 35 luma modes are searched (hevc_core.h HEVC_INTRA_ORDER): oriented texture picks
+    directional modes, the decoder's 8.4.4.2.6 prediction rebuilds the encoder's picture,
+    and the key frame is far smaller than with planar / DC / H / V alone (it was 9996
+    bytes at QP 22 with the four modes, profiles/r3_hevc_tools.md)."""
+    W, H = 384, 256
+    f = _diagonal(W, H)
+    enc = HevcEncoder(W, H, backend="cpu", qp=22)
+    pk = enc.encode(f, 0)[0]
+    Y = HevcDecoder().decode(pk.data[10:])[0][0]
+    assert np.array_equal(Y, _rec_y(enc, W, H))
+    modes = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 16)[:, 3]
+    assert np.count_nonzero(~np.isin(modes, [0, 1, 10, 26])) > len(modes) // 2
+    assert len(pk.data) < 7000, len(pk.data)
+    assert psnr(Y, _luma(f)) > 45

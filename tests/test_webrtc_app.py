@@ -60,8 +60,10 @@ def test_legacy_webrtc_session(tmp_path, backend, encoder):
         viewer.on_datachannel = on_channel
         sig = SignallingClient(f"ws://127.0.0.1:{args.port}/ws", 1)
         answered = asyncio.Event()
+        offers = {}
 
         async def on_offer(kind, text):
+            offers["video"] = text
             await viewer.set_remote_description(text, kind)
             await sig.send_sdp("answer", await viewer.create_answer())
             answered.set()
@@ -105,6 +107,28 @@ def test_legacy_webrtc_session(tmp_path, backend, encoder):
         assert any("Video bitrate set to: 2500" in m for m in msgs)
         saved = json.loads((tmp_path / "cfg.json").read_text())
         assert saved["video_bitrate"] == "2500" and saved["framerate"] == "30"
+        # the second peer (uid 3) gets its own audio-only call from uid 2 (reference two-peer
+        # client, app.js:375-378); the video call carries no audio section
+        assert "m=video" in offers["video"] and "m=audio" not in offers["video"]
+        aviewer = PeerConnection(addresses=["127.0.0.1"])
+        asig = SignallingClient(f"ws://127.0.0.1:{args.port}/ws", 3)
+        aconnected = asyncio.Event()
+
+        async def on_audio_offer(kind, text):
+            offers["audio"] = text
+            await aviewer.set_remote_description(text, kind)
+            await asig.send_sdp("answer", await aviewer.create_answer())
+            await aviewer.connect(15)
+            aconnected.set()
+        asig.on_sdp = lambda kind, text: asyncio.ensure_future(on_audio_offer(kind, text))
+        await asig.connect()
+        areader = asyncio.ensure_future(asig.start())
+        await asyncio.wait_for(aconnected.wait(), 20)
+        assert "m=audio" in offers["audio"] and "m=video" not in offers["audio"]
+        assert "m=application" not in offers["audio"]
+        await aviewer.close()
+        areader.cancel()
+        await asig.stop()
         await viewer.close()
         reader.cancel()
         await sig.stop()
