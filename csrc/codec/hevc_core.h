@@ -7,7 +7,8 @@
 // Coding structure (fixed by the parameter sets in hevc_syntax.cpp):
 //   CTB = CU = 16x16 (log2 min CB 4, no split flags), PU 2Nx2N, TU = CU (16x16 luma,
 //   8x8 chroma, no transform split), one reference picture (previous picture),
-//   quarter-pel motion (8-tap luma / 4-tap chroma MC), deblocking on (CU edges, deblock_picture), no SAO / sign hiding /
+//   quarter-pel motion (8-tap luma / 4-tap chroma MC), deblocking on (CU edges, deblock_picture), SAO
+//   (hevc_sao.h), no sign hiding /
 //   transform skip,
 //   entropy_coding_sync (WPP): one CABAC substream per CTB row, slices = stripes of
 //   whole CTB rows.
@@ -118,7 +119,9 @@ enum Ctx : int {
     CTX_SIG = 59,            // 42
     CTX_GT1 = 101,           // 24
     CTX_GT2 = 125,           // 6
-    CTX_COUNT = 131,
+    CTX_SAO_MERGE = 131,     // sao_merge_left_flag / sao_merge_up_flag
+    CTX_SAO_TYPE = 132,      // first bin of sao_type_idx_luma / _chroma
+    CTX_COUNT = 133,
     CTX_TERM = 255           // terminating bin (end_of_slice_segment_flag / end_of_subset_one_bit)
 };
 SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
@@ -139,7 +142,8 @@ SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
      107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153, 136, 139, 111, 136, 139, 111,
      140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166, 182, 140, 227,
      122, 197,                      // greater1
-     138, 153, 136, 167, 152, 152},  // greater2
+     138, 153, 136, 167, 152, 152,  // greater2
+     153, 200},                     // sao merge, sao type
     {// P slices (cabac_init_flag = 0)
      197, 185, 201,                 // cu_skip_flag
      149,                           // pred_mode_flag
@@ -157,7 +161,8 @@ SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
      166, 183, 140, 136, 153, 154, 170, 153, 138, 138, 122, 121, 122, 121, 167, 151, 183, 140, 151, 183, 140,
      154, 196, 196, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 137, 169, 194, 166, 167, 154, 167,
      137, 182,                      // greater1
-     107, 167, 91, 122, 107, 167}};  // greater2
+     107, 167, 91, 122, 107, 167,   // greater2
+     153, 185}};                    // sao merge, sao type
 
 // Context state byte: (pStateIdx << 1) | valMps (9.3.2.2).
 SK_HD uint8_t ctx_init_state(int init_value, int slice_qp) {

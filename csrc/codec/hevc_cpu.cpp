@@ -135,6 +135,10 @@ CpuHevcEncoder::CpuHevcEncoder(const h264::EncoderConfig& cfg) : fe(front_config
     coefs.assign((size_t)n * kCoefPerCu, 0);
     bins.assign((size_t)n * kCuBinCap, 0);
     bin_n.assign(n, 0);
+    sao_stats.assign((size_t)3 * n, SaoStats{});
+    sao_own.assign(n, SaoParams{});
+    sao.assign(n, SaoParams{});
+    sao_cost.assign(n, 0);
     build_parameter_sets(fe.g.W, fe.g.H, cfg.full_range, cfg.fps, param_sets);
 }
 
@@ -311,6 +315,54 @@ void CpuHevcEncoder::code_slice_skip(int s) {
         }
 }
 
+// Plane geometry for SAO: plane 0 luma (CTB 16), 1 / 2 chroma (CTB 8).
+static SaoPlane sao_plane(const Geo& geo, int c) {
+    const int n = c ? 8 : 16;
+    return SaoPlane{geo.ctb_w * n, geo.ctb_h * n, n, geo.rows_per_slice};
+}
+
+void CpuHevcEncoder::sao_analyse() {
+    const h264::Geometry& g = fe.g;
+    for (int cy = 0; cy < geo.ctb_h; cy++)
+        for (int cx = 0; cx < geo.ctb_w; cx++) {
+            const int idx = cy * geo.ctb_w + cx;
+            // skip-all slices keep the reference as it is (finish_frame does not copy them
+            // back): their stats stay empty, so every CTB there decides "off"
+            const int act = fe.tasks[cy / geo.rows_per_slice].final_action;
+            const bool coded = act == ACT_P || act == ACT_I;
+            for (int c = 0; c < 3; c++) {
+                SaoStats& st = sao_stats[(size_t)3 * idx + c];
+                st = SaoStats{};
+                if (!coded) continue;
+                const SaoPlane pl = sao_plane(geo, c);
+                const int stride = c ? g.stride_c : g.stride_y;
+                for (int y = cy * pl.n; y < (cy + 1) * pl.n; y++)
+                    for (int x = cx * pl.n; x < (cx + 1) * pl.n; x++)
+                        sao_collect(st, pl, fe.rec[c].data(), stride, x, y, fe.src[c][(size_t)y * stride + x]);
+            }
+            sao_cost[idx] = sao_decide(&sao_stats[(size_t)3 * idx], fe.tasks[cy / geo.rows_per_slice].qp, sao_own[idx]);
+        }
+    for (int cy = 0; cy < geo.ctb_h; cy++) {
+        const SliceTask& t = fe.tasks[cy / geo.rows_per_slice];
+        const size_t o = (size_t)cy * geo.ctb_w;
+        sao_row_merge(&sao_stats[3 * o], &sao_own[o], &sao_cost[o], geo.ctb_w, t.qp, cy > t.first_row, &sao[o]);
+    }
+}
+
+void CpuHevcEncoder::sao_apply() {
+    const h264::Geometry& g = fe.g;
+    for (int c = 0; c < 3; c++) {
+        const SaoPlane pl = sao_plane(geo, c);
+        const int stride = c ? g.stride_c : g.stride_y;
+        const std::vector<uint8_t> dbk = fe.rec[c];   // the filter reads deblocked samples only
+        for (int y = 0; y < pl.h; y++)
+            for (int x = 0; x < pl.w; x++) {
+                const SaoParams& p = sao[(size_t)(y / pl.n) * geo.ctb_w + x / pl.n];
+                fe.rec[c][(size_t)y * stride + x] = (uint8_t)sao_apply_sample(p, c, pl, dbk.data(), stride, x, y);
+            }
+    }
+}
+
 void CpuHevcEncoder::binarize_slice(int s) {
     const SliceTask& t = fe.tasks[s];
     const bool p_slice = t.final_action != ACT_I;
@@ -322,6 +374,7 @@ void CpuHevcEncoder::binarize_slice(int s) {
             const int skip_ctx = (left && cus[idx - 1].mode == CU_SKIP) + (top && cus[idx - geo.ctb_w].mode == CU_SKIP);
             const int cand_a = (left && cus[idx - 1].mode == CU_INTRA) ? cus[idx - 1].intra_mode : 1;
             BinBuf w{&bins[(size_t)idx * kCuBinCap], 0};
+            sao_bins(w, sao[idx], left, top);   // CTB-level SAO syntax before the coding quadtree
             code_cu(w, cus[idx], &coefs[(size_t)idx * kCoefPerCu], p_slice, skip_ctx, cand_a);
             w.term(cy == last_row && cx == geo.ctb_w - 1);   // end_of_slice_segment_flag
             bin_n[idx] = w.n;
@@ -421,8 +474,13 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
             case ACT_I: code_slice_intra(s); break;
             default: code_slice_skip(s); break;
         }
-        binarize_slice(s);
     }
+    // in-loop deblocking, then SAO decisions on the deblocked picture (they are syntax of
+    // every CTB, so the binarisation follows them)
+    deblock_picture(fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data(), fe.g.stride_y, fe.g.stride_c, cus.data(),
+                    geo.ctb_w, geo.ctb_h, geo.rows_per_slice);
+    sao_analyse();
+    for (int s = 0; s < ns; s++) binarize_slice(s);
     const bool idr = fe.ctl_.picture_is_idr(fe.tasks.data());
     if (idr) poc = 0;
     h264::EncodedPacket pk;
@@ -440,9 +498,7 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
     }
     fe.ctl_.rate_account(8 * payload_bytes_);   // K10: substream payload (k_rc_account: sub_size)
     out.push_back(std::move(pk));
-    // in-loop deblocking of the reconstruction before it becomes the reference
-    deblock_picture(fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data(), fe.g.stride_y, fe.g.stride_c, cus.data(),
-                    geo.ctb_w, geo.ctb_h, geo.rows_per_slice);
+    sao_apply();   // the SAO output becomes the reference
     fe.finish_frame();
     poc++;
 }

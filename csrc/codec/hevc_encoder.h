@@ -15,6 +15,7 @@
 #include <vector>
 #include "h264_frame.h"
 #include "hevc_core.h"
+#include "hevc_sao.h"
 #include "hevc_syntax.h"
 
 namespace sk {
@@ -73,6 +74,10 @@ class CpuHevcEncoder {
     void code_slice_intra(int s);
     void code_slice_skip(int s);
     void binarize_slice(int s);
+    // SAO (hevc_sao.h) on the deblocked reconstruction: stats + own decision per CTB, then
+    // the merge pass per row (sao_analyse); the filter into the reference (sao_apply)
+    void sao_analyse();
+    void sao_apply();
     // CABAC substreams of slice s (one per CTB row) -> slice NAL (Annex B)
     std::vector<uint8_t> write_slice(int s, bool idr);
     long long payload_bytes_ = 0;   // substream bytes of the frame being written (K10)
@@ -84,6 +89,9 @@ class CpuHevcEncoder {
     std::vector<int16_t> coefs;        // kCoefPerCu per CU
     std::vector<uint16_t> bins;        // kCuBinCap per CU
     std::vector<int> bin_n;
+    std::vector<SaoStats> sao_stats;   // 3 per CTB (Y, Cb, Cr)
+    std::vector<SaoParams> sao_own, sao;   // per CTB: own decision, final (after merges)
+    std::vector<long long> sao_cost;
     std::vector<uint8_t> param_sets;   // VPS + SPS + PPS
     int poc = 0;                       // POC of the next picture
 

@@ -110,7 +110,7 @@ void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<u
         s.ue(0);              // max_transform_hierarchy_depth_intra
         s.put1(0);            // scaling_list_enabled_flag
         s.put1(0);            // amp_enabled_flag
-        s.put1(0);            // sample_adaptive_offset_enabled_flag
+        s.put1(1);            // sample_adaptive_offset_enabled_flag (hevc_sao.h)
         s.put1(0);            // pcm_enabled_flag
         s.ue(1);              // num_short_term_ref_pic_sets
         // st_ref_pic_set(0): one reference, the previous picture

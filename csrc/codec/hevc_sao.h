@@ -1,0 +1,271 @@
+// H.265 sample adaptive offset (SAO, 7.3.8.3 / 8.7.3) shared by the CPU reference
+// (hevc_cpu.cpp) and the gfx950 kernels (k_hevc_sao_stats / k_hevc_sao_row /
+// k_hevc_sao_apply): per-CTB statistics of the deblocked picture against the source,
+// the encoder's parameter decision, the CTB syntax binarisation and the normative
+// filter itself. Slices are stripes of whole CTB rows and
+// pps_loop_filter_across_slices_enabled_flag is 0, so an edge-offset neighbour in another
+// slice (or outside the picture) leaves the sample unchanged.
+#pragma once
+#include "hevc_core.h"
+
+namespace sk {
+namespace hevc {
+
+enum SaoType : uint8_t { SAO_OFF = 0, SAO_BAND = 1, SAO_EDGE = 2 };
+
+// Statistics of one component of one CTB over the samples SAO may change:
+// sum of (source - deblocked) and the count, per edge class and category 1..4, per band.
+struct SaoStats {
+    int32_t eo_s[4][4], eo_n[4][4];
+    int32_t bo_s[32], bo_n[32];
+};
+constexpr int kSaoStatsInts = 96;
+static_assert(sizeof(SaoStats) == kSaoStatsInts * 4, "SaoStats layout");
+
+// Parameters of one CTB (Cr shares type and class with Cb). off[c][k] = SaoOffsetVal[k + 1].
+struct SaoParams {
+    uint8_t type[3];
+    uint8_t eo_class[3];
+    uint8_t band_pos[3];
+    uint8_t merge_left;
+    int8_t off[3][4];
+    int32_t pad;
+};
+static_assert(sizeof(SaoParams) == 28, "SaoParams layout");
+
+// Edge class neighbour offsets (Table 8-? hPos / vPos): 0 horizontal, 1 vertical, 2 135 deg, 3 45 deg.
+SK_HD int sao_dx(int cls, int i) { return cls == 1 ? 0 : (cls == 3 ? (i ? -1 : 1) : (i ? 1 : -1)); }
+SK_HD int sao_dy(int cls, int i) { return cls == 0 ? 0 : (i ? 1 : -1); }
+SK_HD int sk_sign(int v) { return (v > 0) - (v < 0); }
+// edgeIdx (8.7.3.2): 2 + sign(c - a) + sign(c - b), {0,1,2} -> {1,2,0}; 0 = unchanged.
+SK_HD int sao_edge_idx(int c, int a, int b) {
+    const int e = 2 + sk_sign(c - a) + sk_sign(c - b);
+    return e <= 2 ? (e == 2 ? 0 : e + 1) : e;
+}
+
+// Geometry of one plane for SAO: w x h samples, CTB side n (16 luma / 8 chroma), slice
+// rows: a sample row's slice is (y / n) / rows_per_slice.
+struct SaoPlane {
+    int w, h, n, rows_per_slice;
+    SK_HD int slice_of(int y) const { return (y / n) / rows_per_slice; }
+    // Whether an edge-offset class may change sample (x, y): both neighbours inside the
+    // picture and in the sample's slice.
+    SK_HD bool eo_ok(int cls, int x, int y) const {
+        const int s = slice_of(y);
+        for (int i = 0; i < 2; i++) {
+            const int xx = x + sao_dx(cls, i), yy = y + sao_dy(cls, i);
+            if (xx < 0 || yy < 0 || xx >= w || yy >= h || slice_of(yy) != s) return false;
+        }
+        return true;
+    }
+};
+
+// Adds sample (x, y) of the deblocked plane `rec` with source value `src` to the stats.
+SK_HD void sao_collect(SaoStats& st, const SaoPlane& g, const uint8_t* rec, int stride, int x, int y, int src) {
+    const int c = rec[(size_t)y * stride + x], d = src - c;
+    st.bo_s[c >> 3] += d;
+    st.bo_n[c >> 3] += 1;
+    for (int cls = 0; cls < 4; cls++) {
+        if (!g.eo_ok(cls, x, y)) continue;
+        const int a = rec[(size_t)(y + sao_dy(cls, 0)) * stride + x + sao_dx(cls, 0)];
+        const int b = rec[(size_t)(y + sao_dy(cls, 1)) * stride + x + sao_dx(cls, 1)];
+        const int e = sao_edge_idx(c, a, b);
+        if (e) {
+            st.eo_s[cls][e - 1] += d;
+            st.eo_n[cls][e - 1] += 1;
+        }
+    }
+}
+
+// SAO lambda in Q4 per QP: 16 * 0.57 * 2^((QP - 12) / 3) (the HM rate-distortion lambda
+// for SSE distortion); costs below are 16 * SSE change + lambda * bits.
+SK_TABLE int32_t SAO_LAMBDA_Q4[52] = {1,    1,    1,    1,    1,    2,    2,    3,    4,     5,     6,     7,    9,
+                                      11,   14,   18,   23,   29,   36,   46,   58,   73,    92,    116,   146,  184,
+                                      232,  292,  368,  463,  584,  735,  927,  1167, 1471,  1853,  2335,  2942, 3706,
+                                      4669, 5883, 7412, 9339, 11766, 14825, 18678, 23533, 29649, 37356, 47065, 59298, 74711};
+// sao_offset_abs bins: TR, cMax 7.
+SK_HD int sao_abs_bins(int a) { return a < 7 ? a + 1 : 7; }
+// 16 * SSE change of offset o on a category with sum s and count n.
+SK_HD long long sao_dist(int o, int s, int n) { return 16ll * ((long long)n * o * o - 2ll * o * s); }
+
+// Best offset of one category: o in [lo, hi], minimising distortion + lambda * bins
+// (+ one sign bin for a non-zero band offset). First minimum from o = 0 outward wins.
+SK_HD long long sao_best_offset(int s, int n, int lo, int hi, bool sign_bin, int lam, int* best_o) {
+    long long best = 0;
+    int bo = 0;
+    best = (long long)lam * sao_abs_bins(0);
+    for (int m = 1; m <= 7; m++)
+        for (int sg = 0; sg < 2; sg++) {
+            const int o = sg ? -m : m;
+            if (o < lo || o > hi) continue;
+            const long long c = sao_dist(o, s, n) + (long long)lam * (sao_abs_bins(m) + (sign_bin ? 1 : 0));
+            if (c < best) { best = c; bo = o; }
+        }
+    *best_o = bo;
+    return best;
+}
+
+// Own parameters of one CTB from its three components' stats: per component (Cb and Cr
+// jointly for type and class) the cheapest of off / each edge class / the best band
+// window. Returns the total cost (16 * SSE change + lambda * bits) of the chosen set,
+// merge flags excluded.
+SK_HD long long sao_decide(const SaoStats* st, int qp, SaoParams& p) {
+    const int lam = SAO_LAMBDA_Q4[sk_clip(qp, 0, 51)];
+    for (int c = 0; c < 3; c++) {
+        p.type[c] = SAO_OFF;
+        p.eo_class[c] = 0;
+        p.band_pos[c] = 0;
+        for (int k = 0; k < 4; k++) p.off[c][k] = 0;
+    }
+    p.merge_left = 0;
+    p.pad = 0;
+    long long total = 0;
+    for (int grp = 0; grp < 2; grp++) {   // 0: luma, 1: Cb + Cr
+        const int c0 = grp ? 1 : 0, c1 = grp ? 2 : 0;
+        long long best = (long long)lam * 1;   // sao_type_idx = 0: one bin
+        int btype = SAO_OFF, bcls = 0;
+        int boff[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, bpos[2] = {0, 0};
+        for (int cls = 0; cls < 4; cls++) {
+            long long cost = (long long)lam * (2 + (grp ? 2 : 2));   // type (2 bins) + class (2 bits, once)
+            int o[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+            for (int c = c0; c <= c1; c++)
+                for (int k = 0; k < 4; k++)
+                    cost += sao_best_offset(st[c].eo_s[cls][k], st[c].eo_n[cls][k], k < 2 ? 0 : -7, k < 2 ? 7 : 0,
+                                            false, lam, &o[c - c0][k]);
+            if (cost < best) {
+                best = cost;
+                btype = SAO_EDGE;
+                bcls = cls;
+                for (int i = 0; i < 2; i++)
+                    for (int k = 0; k < 4; k++) boff[i][k] = o[i][k];
+            }
+        }
+        {   // band: per component the best window of 4 bands (band_position, 5 bits)
+            long long cost = (long long)lam * 2;
+            int o[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pos[2] = {0, 0};
+            for (int c = c0; c <= c1; c++) {
+                long long bc[32];
+                int bo[32];
+                for (int b = 0; b < 32; b++) bc[b] = sao_best_offset(st[c].bo_s[b], st[c].bo_n[b], -7, 7, true, lam, &bo[b]);
+                long long wbest = 0;
+                int wpos = 0;
+                for (int ps = 0; ps < 32; ps++) {
+                    long long w = (long long)lam * 5;
+                    for (int k = 0; k < 4; k++) w += bc[(ps + k) & 31];
+                    if (ps == 0 || w < wbest) { wbest = w; wpos = ps; }
+                }
+                cost += wbest;
+                pos[c - c0] = wpos;
+                for (int k = 0; k < 4; k++) o[c - c0][k] = bo[(wpos + k) & 31];
+            }
+            if (cost < best) {
+                best = cost;
+                btype = SAO_BAND;
+                for (int i = 0; i < 2; i++) {
+                    bpos[i] = pos[i];
+                    for (int k = 0; k < 4; k++) boff[i][k] = o[i][k];
+                }
+            }
+        }
+        // an "on" set whose offsets are all zero is worse than off: keep off then
+        bool any = false;
+        for (int i = 0; i <= c1 - c0; i++)
+            for (int k = 0; k < 4; k++) any |= boff[i][k] != 0;
+        if (!any) {
+            btype = SAO_OFF;
+            best = (long long)lam * 1;
+        }
+        for (int c = c0; c <= c1; c++) {
+            p.type[c] = (uint8_t)btype;
+            p.eo_class[c] = (uint8_t)(btype == SAO_EDGE ? bcls : 0);
+            p.band_pos[c] = (uint8_t)(btype == SAO_BAND ? bpos[c - c0] : 0);
+            for (int k = 0; k < 4; k++) p.off[c][k] = (int8_t)(btype == SAO_OFF ? 0 : boff[c - c0][k]);
+        }
+        total += best;
+    }
+    return total;
+}
+
+// Distortion change (16 * SSE) of parameter set p on a CTB's stats (merge evaluation).
+SK_HD long long sao_params_dist(const SaoStats* st, const SaoParams& p) {
+    long long d = 0;
+    for (int c = 0; c < 3; c++) {
+        if (p.type[c] == SAO_EDGE)
+            for (int k = 0; k < 4; k++) d += sao_dist(p.off[c][k], st[c].eo_s[p.eo_class[c]][k], st[c].eo_n[p.eo_class[c]][k]);
+        else if (p.type[c] == SAO_BAND)
+            for (int k = 0; k < 4; k++) {
+                const int b = (p.band_pos[c] + k) & 31;
+                d += sao_dist(p.off[c][k], st[c].bo_s[b], st[c].bo_n[b]);
+            }
+    }
+    return d;
+}
+
+// Merge decision along one CTB row (sequential: a merged CTB copies its left neighbour's
+// final parameters). own[x] / own_cost[x]: sao_decide's result per CTB; out[x]: final.
+// Merge-up is never chosen (rows stay independent); its flag is still coded as 0.
+SK_HD void sao_row_merge(const SaoStats* st_row, const SaoParams* own, const long long* own_cost, int ctb_w, int qp,
+                         bool has_up, SaoParams* out) {
+    const int lam = SAO_LAMBDA_Q4[sk_clip(qp, 0, 51)];
+    for (int x = 0; x < ctb_w; x++) {
+        SaoParams p = own[x];
+        if (x > 0) {
+            const long long cown = own_cost[x] + (long long)lam * (has_up ? 2 : 1);   // merge_left = 0 (+ merge_up = 0)
+            const long long cmerge = sao_params_dist(st_row + 3 * x, out[x - 1]) + (long long)lam * 1;
+            if (cmerge < cown) {
+                p = out[x - 1];
+                p.merge_left = 1;
+            }
+        }
+        out[x] = p;
+    }
+}
+
+// CTB syntax sao(rx, ry) (7.3.8.3) as bin entries. left/up: the neighbour CTB exists in
+// this slice.
+SK_HD void sao_bins(BinBuf& w, const SaoParams& p, bool left, bool up) {
+    if (left) w.ctx(CTX_SAO_MERGE, p.merge_left);
+    if (p.merge_left) return;
+    if (up) w.ctx(CTX_SAO_MERGE, 0);
+    for (int c = 0; c < 3; c++) {
+        const int t = p.type[c];
+        if (c < 2) {   // sao_type_idx: TR cMax 2, first bin context, second bypass
+            w.ctx(CTX_SAO_TYPE, t != SAO_OFF);
+            if (t != SAO_OFF) w.bypass(t == SAO_EDGE ? 1u : 0u, 1);
+        }
+        if (t == SAO_OFF) continue;
+        for (int k = 0; k < 4; k++) {   // sao_offset_abs: TR cMax 7, bypass
+            const int a = sk_abs(p.off[c][k]);
+            w.bypass(a < 7 ? ((1u << (a + 1)) - 2u) : 0x7fu, a < 7 ? a + 1 : 7);
+        }
+        if (t == SAO_BAND) {
+            for (int k = 0; k < 4; k++)
+                if (p.off[c][k]) w.bypass(p.off[c][k] < 0 ? 1u : 0u, 1);
+            w.bypass(p.band_pos[c], 5);
+        } else if (c < 2) {
+            w.bypass(p.eo_class[c], 2);
+        }
+    }
+}
+
+// Normative filter (8.7.3) for sample (x, y) of a plane: the deblocked value and its
+// neighbours come from `rec`; returns the SAO output.
+SK_HD int sao_apply_sample(const SaoParams& p, int c, const SaoPlane& g, const uint8_t* rec, int stride, int x, int y) {
+    const int v = rec[(size_t)y * stride + x];
+    if (p.type[c] == SAO_BAND) {
+        const int k = ((v >> 3) - p.band_pos[c]) & 31;
+        return k < 4 ? sk_clip255(v + p.off[c][k]) : v;
+    }
+    if (p.type[c] == SAO_EDGE) {
+        const int cls = p.eo_class[c];
+        if (!g.eo_ok(cls, x, y)) return v;
+        const int a = rec[(size_t)(y + sao_dy(cls, 0)) * stride + x + sao_dx(cls, 0)];
+        const int b = rec[(size_t)(y + sao_dy(cls, 1)) * stride + x + sao_dx(cls, 1)];
+        const int e = sao_edge_idx(v, a, b);
+        return e ? sk_clip255(v + p.off[c][e - 1]) : v;
+    }
+    return v;
+}
+
+}  // namespace hevc
+}  // namespace sk

@@ -67,6 +67,8 @@ SK_HD int write_slice_header(uint8_t* buf, const SliceHeader& h) {
         w.put((uint32_t)h.poc_lsb, kLog2MaxPocLsb);
         w.put1(1);                         // short_term_ref_pic_set_sps_flag (the SPS's one RPS)
     }
+    w.put1(1);                             // slice_sao_luma_flag (per-CTB decisions, hevc_sao.h)
+    w.put1(1);                             // slice_sao_chroma_flag
     if (h.slice_type == 1) {
         w.put1(0);                         // num_ref_idx_active_override_flag
         w.ue(0);                           // five_minus_max_num_merge_cand

@@ -7,6 +7,7 @@
 #include "../codec/hevc_core.h"
 #include "../codec/hevc_syntax.h"
 #include "../codec/hevc_pcabac.h"
+#include "../codec/hevc_sao.h"
 
 namespace sk {
 namespace hevc {
@@ -38,6 +39,12 @@ struct HevcArgs {
     uint16_t* cu_r;             // [ctbs] start range of the chunk
     uint8_t* tail;              // [ctbs][2] the chunk's two bytes overlapping the next chunk
     uint32_t* row_bits;         // [ctb_h] shifts of the whole row (T_f)
+    // SAO (codec/hevc_sao.h) on the deblocked reconstruction
+    SaoStats* sao_stats;        // [ctbs][3] Y, Cb, Cr
+    SaoParams* sao_own;         // [ctbs] each CTB's own decision (k_hevc_sao_stats)
+    long long* sao_cost;        // [ctbs] its cost
+    SaoParams* sao;             // [ctbs] final parameters after the row merge pass (k_hevc_sao_row)
+    h264::gpu::Planes sao_tmp;  // filtered samples of the CTBs SAO changes, copied back into f.rec
 };
 
 void launch_backend(const HevcArgs& a, hipStream_t s);

@@ -11,6 +11,8 @@
 //                      context chains, range maps, composition, per-CTB coding, merge
 //   k_hevc_hdr         slice header with entry points, NAL prefix, substream offsets
 //   k_hevc_ep_copy     wave-parallel emulation prevention + copy into host-mapped slots
+//   k_hevc_dbk_v/h     in-loop deblocking (before the syntax: SAO decides on its output)
+//   k_hevc_sao_*       SAO: stats + own decision per CTB, row merge pass, filter + copy back
 // Bit-exact with the CPU reference (codec/hevc_cpu.cpp): integer math only.
 #include "hevc_gpu.h"
 
@@ -530,6 +532,7 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
     const int skip_ctx = (left && A.cus[idx - 1].mode == CU_SKIP) + (top && A.cus[idx - f.mb_w].mode == CU_SKIP);
     const int cand_a = (left && A.cus[idx - 1].mode == CU_INTRA) ? A.cus[idx - 1].intra_mode : 1;
     BinBuf w{A.bins + (size_t)idx * kCuBinCap, 0};
+    sao_bins(w, A.sao[idx], left, top);   // CTB-level SAO syntax (k_hevc_sao_row's decision)
     code_cu(w, cu, A.coefs + (size_t)idx * kCoefPerCu, p_slice, skip_ctx, cand_a);
     const bool last_row = cy == t.first_row + t.num_rows - 1;
     w.term(last_row && cx == f.mb_w - 1);
@@ -1185,6 +1188,119 @@ __global__ __launch_bounds__(256) void k_hevc_dbk_h(HevcArgs A) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// SAO (codec/hevc_sao.h). Stats + each CTB's own decision: one wave per CTB, lanes
+// accumulate the sample statistics of the deblocked picture with LDS atomics (integer
+// sums, so the result is the host loop's), lane 0 runs the shared decision. Slices
+// that are not coded (skip-all) keep empty stats and decide "off", like the host.
+__device__ __forceinline__ const uint8_t* plane_of(const Planes& P, int c) { return c == 0 ? P.y : (c == 1 ? P.u : P.v); }
+__device__ __forceinline__ uint8_t* plane_of(Planes& P, int c) { return c == 0 ? P.y : (c == 1 ? P.u : P.v); }
+// Sample i (0..383) of CTB (cx, cy): component and plane coordinates.
+__device__ __forceinline__ void ctb_sample(int i, int cx, int cy, int* c, int* x, int* y) {
+    if (i < 256) {
+        *c = 0; *x = cx * 16 + (i & 15); *y = cy * 16 + (i >> 4);
+    } else {
+        const int j = i - 256;
+        *c = 1 + (j >> 6); *x = cx * 8 + (j & 7); *y = cy * 8 + ((j >> 3) & 7);
+    }
+}
+__device__ __forceinline__ SaoPlane sao_plane_of(const FrameArgs& f, int c) {
+    const int n = c ? 8 : 16;
+    return SaoPlane{f.mb_w * n, f.mb_h * n, n, f.rows_per_slice};
+}
+
+__global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
+    __shared__ SaoStats Sw[4][3];
+    const FrameArgs& f = A.f;
+    const int w = threadIdx.x >> 6, l = lane();
+    const int idx = blockIdx.x * 4 + w;
+    if (idx >= f.mb_w * f.mb_h) return;   // wave-uniform; no block barriers below
+    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    SaoStats* st = Sw[w];
+    int32_t* z = reinterpret_cast<int32_t*>(st);
+    for (int i = l; i < 3 * kSaoStatsInts; i += 64) z[i] = 0;
+    wsync();
+    if (t.final_action == ACT_P || t.final_action == ACT_I) {
+        for (int i = l; i < kCoefPerCu; i += 64) {
+            int c, x, y;
+            ctb_sample(i, cx, cy, &c, &x, &y);
+            const SaoPlane pl = sao_plane_of(f, c);
+            const int stride = c ? f.stride_c : f.stride_y;
+            const uint8_t* rec = plane_of(f.rec, c);
+            const int v = rec[(size_t)y * stride + x];
+            const int d = (int)plane_of(f.src, c)[(size_t)y * stride + x] - v;
+            atomicAdd(&st[c].bo_s[v >> 3], d);
+            atomicAdd(&st[c].bo_n[v >> 3], 1);
+#pragma unroll
+            for (int cls = 0; cls < 4; cls++) {
+                if (!pl.eo_ok(cls, x, y)) continue;
+                const int a = rec[(size_t)(y + sao_dy(cls, 0)) * stride + x + sao_dx(cls, 0)];
+                const int b = rec[(size_t)(y + sao_dy(cls, 1)) * stride + x + sao_dx(cls, 1)];
+                const int e = sao_edge_idx(v, a, b);
+                if (e) {
+                    atomicAdd(&st[c].eo_s[cls][e - 1], d);
+                    atomicAdd(&st[c].eo_n[cls][e - 1], 1);
+                }
+            }
+        }
+    }
+    wsync();
+    int32_t* g = reinterpret_cast<int32_t*>(A.sao_stats + (size_t)3 * idx);
+    for (int i = l; i < 3 * kSaoStatsInts; i += 64) g[i] = z[i];
+    if (l == 0) {
+        SaoParams p;
+        A.sao_cost[idx] = sao_decide(st, t.qp, p);
+        A.sao_own[idx] = p;
+    }
+}
+
+// Merge pass: one thread per CTB row, left to right (a merged CTB copies its left
+// neighbour's final parameters).
+__global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int cy = blockIdx.x * 64 + threadIdx.x;
+    if (cy >= f.mb_h) return;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const size_t o = (size_t)cy * f.mb_w;
+    sao_row_merge(A.sao_stats + 3 * o, A.sao_own + o, A.sao_cost + o, f.mb_w, t.qp, cy > t.first_row, A.sao + o);
+}
+
+__device__ __forceinline__ bool sao_any(const SaoParams& p) { return (p.type[0] | p.type[1] | p.type[2]) != 0; }
+
+// The filter (8.7.3) of the CTBs SAO changes, from the deblocked picture into sao_tmp:
+// one wave per CTB; k_hevc_sao_copy then writes those CTBs back (after every CTB has
+// read its deblocked neighbours).
+__global__ __launch_bounds__(256) void k_hevc_sao_apply(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (idx >= f.mb_w * f.mb_h) return;
+    const SaoParams p = A.sao[idx];
+    if (!sao_any(p)) return;
+    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
+    for (int i = lane(); i < kCoefPerCu; i += 64) {
+        int c, x, y;
+        ctb_sample(i, cx, cy, &c, &x, &y);
+        const int stride = c ? f.stride_c : f.stride_y;
+        plane_of(A.sao_tmp, c)[(size_t)y * stride + x] =
+            (uint8_t)sao_apply_sample(p, c, sao_plane_of(f, c), plane_of(f.rec, c), stride, x, y);
+    }
+}
+__global__ __launch_bounds__(256) void k_hevc_sao_copy(HevcArgs A) {
+    const FrameArgs& f = A.f;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (idx >= f.mb_w * f.mb_h) return;
+    if (!sao_any(A.sao[idx])) return;
+    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
+    Planes rec = f.rec;
+    for (int i = lane(); i < kCoefPerCu; i += 64) {
+        int c, x, y;
+        ctb_sample(i, cx, cy, &c, &x, &y);
+        const size_t o = (size_t)y * (c ? f.stride_c : f.stride_y) + x;
+        plane_of(rec, c)[o] = plane_of(A.sao_tmp, c)[o];
+    }
+}
+
 void launch_backend(const HevcArgs& a, hipStream_t s) {
     const int n = a.f.mb_w * a.f.mb_h;
     hipLaunchKernelGGL(k_hevc_inter, dim3((n + 3) / 4), dim3(256), 0, s, a);
@@ -1193,8 +1309,15 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_hevc_intra<4>, dim3(a.f.num_slices), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
+    // in-loop deblocking, then the SAO decisions on the deblocked picture (CTB syntax)
+    const int cw = a.f.mb_w, ch = a.f.mb_h;
+    const int nv = ch * 4 * (cw - 1) + 2 * ch * 8 * (cw - 1), nh = (ch - 1) * cw * 4 + 2 * (ch - 1) * cw * 8;
+    if (nv > 0) hipLaunchKernelGGL(k_hevc_dbk_v, dim3((nv + 255) / 256), dim3(256), 0, s, a);
+    if (nh > 0) hipLaunchKernelGGL(k_hevc_dbk_h, dim3((nh + 255) / 256), dim3(256), 0, s, a);
     const int nq = (n + 3) / 4;
+    hipLaunchKernelGGL(k_hevc_sao_stats, dim3(nq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sao_row, dim3((ch + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(192), 0, s, a);
     hipLaunchKernelGGL(k_pc_model, dim3(a.f.mb_h, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);
@@ -1204,10 +1327,9 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_pc_merge, dim3(a.f.mb_h), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h), dim3(64), 0, s, a);
-    const int cw = a.f.mb_w, ch = a.f.mb_h;
-    const int nv = ch * 4 * (cw - 1) + 2 * ch * 8 * (cw - 1), nh = (ch - 1) * cw * 4 + 2 * (ch - 1) * cw * 8;
-    if (nv > 0) hipLaunchKernelGGL(k_hevc_dbk_v, dim3((nv + 255) / 256), dim3(256), 0, s, a);
-    if (nh > 0) hipLaunchKernelGGL(k_hevc_dbk_h, dim3((nh + 255) / 256), dim3(256), 0, s, a);
+    // the SAO output becomes the reconstruction (k_commit copies it into the reference)
+    hipLaunchKernelGGL(k_hevc_sao_apply, dim3(nq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sao_copy, dim3(nq), dim3(256), 0, s, a);
 }
 
 }  // namespace gpu

@@ -375,6 +375,7 @@ class HipBackend : public EncoderBackend {
         }
         else if (s == "coefs" && cfg_.codec == 1) { p = hargs_.coefs; n = (int64_t)g_.num_mbs() * hevc::kCoefPerCu * 2; }
         else if (s == "cus" && cfg_.codec == 1) { p = hargs_.cus; n = (int64_t)g_.num_mbs() * sizeof(hevc::CuInfo); }
+        else if (s == "sao" && cfg_.codec == 1) { p = hargs_.sao; n = (int64_t)g_.num_mbs() * sizeof(hevc::SaoParams); }
         else if (s == "bin_n" && cfg_.codec == 1) { p = hargs_.bin_n; n = (int64_t)g_.num_mbs() * 4; }
         else if (s == "hevc_stamps" && cfg_.codec == 1) { if (!hargs_.dbg) return -1; p = hargs_.dbg; n = (int64_t)g_.mb_h * 32; }
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
@@ -653,6 +654,13 @@ class HipBackend : public EncoderBackend {
         h.cu_r = dmalloc<uint16_t>(n);
         h.tail = dmalloc<uint8_t>((size_t)n * 2);
         h.row_bits = dmalloc<uint32_t>(g_.mb_h);
+        h.sao_stats = dmalloc<hevc::SaoStats>((size_t)3 * n, false);
+        h.sao_own = dmalloc<hevc::SaoParams>(n);
+        h.sao_cost = dmalloc<long long>(n);
+        h.sao = dmalloc<hevc::SaoParams>(n);
+        h.sao_tmp.y = dmalloc<uint8_t>((size_t)g_.stride_y * g_.mb_h * 16, false);
+        h.sao_tmp.u = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
+        h.sao_tmp.v = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
         // host slot: 1.5 KB per CTB (far above practical rates); larger slices go to the
         // device fallback slot (worst case: 3/2 emulation growth of the substream bound)
         h.out_slot = (g_.rows_per_slice * g_.mb_w * 1536 + 4096 + 63) & ~63;

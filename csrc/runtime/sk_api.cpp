@@ -148,6 +148,7 @@ class CpuHevcBackend : public EncoderBackend {
         else if (s == "ref_u") plane(enc_.fe.ref[1]);
         else if (s == "ref_v") plane(enc_.fe.ref[2]);
         else if (s == "cus") { p = enc_.cus.data(); n = (int64_t)(enc_.cus.size() * sizeof(hevc::CuInfo)); }
+        else if (s == "sao") { p = enc_.sao.data(); n = (int64_t)(enc_.sao.size() * sizeof(hevc::SaoParams)); }
         else if (s == "coefs") { p = enc_.coefs.data(); n = (int64_t)(enc_.coefs.size() * 2); }
         else if (s == "bin_n") { p = enc_.bin_n.data(); n = (int64_t)(enc_.bin_n.size() * 4); }
         else if (s == "me") { p = enc_.fe.me.data(); n = (int64_t)(enc_.fe.me.size() * sizeof(h264::MeResult)); }

@@ -11,10 +11,12 @@ luma and 4-tap chroma interpolation, scaling, inverse DCT/DST, reconstruction).
 Supported: Main 8-bit 4:2:0, any CTB/CB/TB sizes with quadtree splits, PART_2Nx2N
 CUs (intra and inter), I and P slices with one reference list, multiple slices,
 entropy_coding_sync (WPP) substreams. NotImplementedError for the rest (B slices,
-tiles, AMP/NxN partitions, PCM, transform skip, scaling lists, SAO, TMVP, long-term
+tiles, AMP/NxN partitions, PCM, transform skip, scaling lists, TMVP, long-term
 references, sign data hiding, cu_qp_delta). The deblocking filter (8.7.2) runs on the
 completed picture: transform / prediction block edges on the 8x8 grid, boundary
-strength, luma decisions and strong / normal filters, chroma on bS 2.
+strength, luma decisions and strong / normal filters, chroma on bS 2. Sample adaptive
+offset (7.3.8.3 syntax, 8.7.3 band / edge offsets with the picture and slice boundary
+rules) then runs on the deblocked picture.
 
 Written from the specification text, not from the encoder's tables; numpy for the
 sample processes, plain Python for parsing. Intended for test-sized pictures.
@@ -129,6 +131,8 @@ INIT = {
                                       [107, 167, 91, 107, 107, 167]],
 }
 INIT["last_y_prefix"] = INIT["last_x_prefix"]
+INIT["sao_merge_flag"] = [[153], [153], [153]]          # sao_merge_left_flag / sao_merge_up_flag
+INIT["sao_type_idx"] = [[200], [185], [160]]            # sao_type_idx_luma / _chroma (first bin)
 
 
 def init_contexts(init_type: int, qp: int) -> dict:
@@ -475,6 +479,8 @@ class HevcDecoder:
         s = self.sps
         if any(v[0] for v in self.cur["dbk_slices"].values()):
             self._deblock()
+        if self.cur["sao"]:
+            self._sao_filter()
         Y, U, V = self.cur["Y"], self.cur["U"], self.cur["V"]
         self.ref = (Y.copy(), U.copy(), V.copy())
         self.cur = None
@@ -512,6 +518,8 @@ class HevcDecoder:
             "cbf": np.zeros((s.height // 4, s.width // 4), bool),
             "qp": np.zeros((s.height // 4, s.width // 4), np.int64),
             "dbk_slices": {},
+            "sao": {},         # (rx, ry) -> SAO parameters of the CTB
+            "sao_slices": {},  # slice address -> (slice_sao_luma_flag, slice_sao_chroma_flag)
         }
         del nmin
 
@@ -562,9 +570,11 @@ class HevcDecoder:
             if s.tmvp:
                 if b.u(1):
                     raise NotImplementedError("TMVP")
+        sao_luma = sao_chroma = False
         if s.sao:
-            if b.u(1) or b.u(1):
-                raise NotImplementedError("SAO")
+            sao_luma = bool(b.u(1))
+            sao_chroma = bool(b.u(1))   # ChromaArrayType != 0
+        self.cur["sao_slices"][addr] = (sao_luma, sao_chroma)
         num_ref = p.num_ref_l0
         max_merge = 5
         if slice_type == 1:
@@ -586,7 +596,7 @@ class HevcDecoder:
             if not deblock_disabled:
                 beta_off, tc_off = 2 * b.se(), 2 * b.se()
         across = p.loop_filter_across_slices
-        if p.loop_filter_across_slices and not deblock_disabled:
+        if p.loop_filter_across_slices and (sao_luma or sao_chroma or not deblock_disabled):
             across = bool(b.u(1))
         # per-slice deblocking parameters, looked up by the slice map at filtering time
         self.cur["dbk_slices"][addr] = (not deblock_disabled, beta_off, tc_off, across)
@@ -662,6 +672,9 @@ class HevcDecoder:
                     self.ctx = init_contexts(init_type, qp)
             elif p.wpp and cx == 0 and a == addr:
                 pass
+            luma, chroma = self.cur["sao_slices"][addr]
+            if luma or chroma:
+                self._sao_syntax(cx, cy, a, wc, luma, chroma)
             self._coding_quadtree(cx * ctb, cy * ctb, s.log2_ctb, 0)
             if p.wpp and cx == 1:
                 sync = copy_contexts(self.ctx)
@@ -676,6 +689,114 @@ class HevcDecoder:
                     raise BitstreamError("end_of_subset_one_bit")
             if a >= wc * hc:
                 raise BitstreamError("slice runs past the picture")
+
+    # ---------------- SAO ----------------
+    def _sao_syntax(self, rx, ry, ctb_addr, wc, luma, chroma):
+        """sao(rx, ry) (7.3.8.3): merge flags, per-component type / offsets / band position /
+        edge class; stores SaoTypeIdx, SaoOffsetVal[1..4], band position and class."""
+        c = self.cur
+        merge_left = merge_up = 0
+        if rx > 0 and ctb_addr - 1 >= self.slice_addr:
+            merge_left = self._dec("sao_merge_flag")
+        if ry > 0 and not merge_left and ctb_addr - wc >= self.slice_addr:
+            merge_up = self._dec("sao_merge_flag")
+        if merge_left:
+            c["sao"][(rx, ry)] = c["sao"][(rx - 1, ry)]
+            return
+        if merge_up:
+            c["sao"][(rx, ry)] = c["sao"][(rx, ry - 1)]
+            return
+        prm = {"type": [0, 0, 0], "off": [[0] * 4 for _ in range(3)], "band": [0, 0, 0], "cls": [0, 0, 0]}
+        cab = self.cabac
+        for ci in range(3):
+            if not ((luma and ci == 0) or (chroma and ci > 0)):
+                continue
+            if ci < 2:
+                t = 0
+                if self._dec("sao_type_idx"):
+                    t = 2 if cab.bypass() else 1     # TR cMax 2: "10" band, "11" edge
+                prm["type"][ci] = t
+            else:
+                prm["type"][2] = prm["type"][1]
+                prm["cls"][2] = prm["cls"][1]
+            t = prm["type"][ci]
+            if t == 0:
+                continue
+            absv = []
+            for _ in range(4):                     # sao_offset_abs: TR cMax 7, bypass
+                v = 0
+                while v < 7 and cab.bypass():
+                    v += 1
+                absv.append(v)
+            if t == 1:
+                sg = [(-1 if cab.bypass() else 1) if a else 1 for a in absv]
+                prm["band"][ci] = cab.bypass_bits(5)
+                prm["off"][ci] = [a * g for a, g in zip(absv, sg)]
+            else:
+                if ci < 2:
+                    prm["cls"][ci] = cab.bypass_bits(2)
+                prm["off"][ci] = [absv[0], absv[1], -absv[2], -absv[3]]
+        c["sao"][(rx, ry)] = prm
+
+    def _sao_filter(self):
+        """8.7.3 on the deblocked picture: band offsets by (sample >> 3) relative to the band
+        position, edge offsets from the sign pattern against the class's two neighbours;
+        samples whose edge neighbour lies outside the picture or across a slice boundary
+        that may not be filtered stay unchanged."""
+        c = self.cur
+        s = self.sps
+        ctb = 1 << s.log2_ctb
+        hpos = {0: (-1, 1), 1: (0, 0), 2: (-1, 1), 3: (1, -1)}
+        vpos = {0: (0, 0), 1: (-1, 1), 2: (-1, 1), 3: (-1, 1)}
+        slice_map = c["slice"]
+        across = {a: v[3] for a, v in c["dbk_slices"].items()}
+        for ci, name in enumerate(("Y", "U", "V")):
+            sh = 0 if ci == 0 else 1
+            src = c[name].astype(np.int64)
+            out = c[name]
+            H, W = src.shape
+            n = ctb >> sh
+            ys_all, xs_all = np.mgrid[0:H, 0:W]
+            sl = slice_map[(ys_all << sh) >> 2, (xs_all << sh) >> 2]
+            for (rx, ry), prm in c["sao"].items():
+                t = prm["type"][ci]
+                y0, x0 = ry * n, rx * n
+                if t == 0 or y0 >= H or x0 >= W:
+                    continue
+                sao_l, sao_c = c["sao_slices"][int(sl[y0, x0])]
+                if not (sao_l if ci == 0 else sao_c):
+                    continue
+                ys, xs = ys_all[y0:y0 + n, x0:x0 + n], xs_all[y0:y0 + n, x0:x0 + n]
+                v = src[y0:y0 + n, x0:x0 + n]
+                off = prm["off"][ci]
+                if t == 1:
+                    k = ((v >> 3) - prm["band"][ci]) & 31
+                    res = v.copy()
+                    for i in range(4):
+                        res[k == i] += off[i]
+                else:
+                    cls = prm["cls"][ci]
+                    ok = np.ones_like(v, bool)
+                    nb = []
+                    cur_sl = sl[y0:y0 + n, x0:x0 + n]
+                    for i in range(2):
+                        yy, xx = ys + vpos[cls][i], xs + hpos[cls][i]
+                        inside = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+                        yyc, xxc = np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)
+                        nsl = sl[yyc, xxc]
+                        # across a slice boundary: the later slice's flag decides (MinTbAddrZs order)
+                        later = np.where(nsl < cur_sl, cur_sl, nsl)
+                        allow = np.vectorize(lambda a: across.get(int(a), False))(later) if (nsl != cur_sl).any() \
+                            else np.ones_like(v, bool)
+                        ok &= inside & ((nsl == cur_sl) | allow)
+                        nb.append(src[yyc, xxc])
+                    e = 2 + np.sign(v - nb[0]) + np.sign(v - nb[1])
+                    e = np.where(e <= 2, np.where(e == 2, 0, e + 1), e)
+                    e = np.where(ok, e, 0)
+                    res = v.copy()
+                    for i in range(1, 5):
+                        res[e == i] += off[i - 1]
+                out[y0:y0 + n, x0:x0 + n] = np.clip(res, 0, 255)
 
     # ---------------- coding tree ----------------
     def _dec(self, name, idx=0):
