@@ -514,10 +514,12 @@ def main():
 
     frames = S * args.steps
     inflight_used = None
+    upload_fraction = None
     if caps is not None:
         all_lat = np.concatenate([np.asarray(c.latencies(), dtype=np.float64) for c in caps])
         nbytes = [c.stats()["bytes"] - b for c, b in zip(caps, bytes0)]
         inflight_used = max(c.stats().get("frames_in_flight", 0) for c in caps)
+        upload_fraction = round(float(np.mean([c.stats().get("upload_fraction", 1.0) for c in caps])), 3)
     else:
         all_lat = np.concatenate([np.asarray(x) for x in lat]) * 1e3
     stats = np.array([elapsed, frames, sum(nbytes), np.percentile(all_lat, 50), np.percentile(all_lat, 99)],
@@ -608,6 +610,9 @@ def main():
                 # flight only for a session that has its GPU to itself (capture.cpp overlap_now)
                 "upload_overlap": (inflight_used or 0) >= 2 if args.path == "capture" else bool(args.overlap),
                 "frames_in_flight": inflight_used if args.path == "capture" else (2 if args.overlap >= 2 else 1),
+                # damage-driven upload: share of captured rows that crossed PCIe (the pool
+                # source reports changed 16-row bands like XDamage; motion content: all)
+                "upload_fraction": upload_fraction,
                 "num_refs": args.num_refs,
                 "numa_node_rank0": numa_node,
             },

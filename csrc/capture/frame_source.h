@@ -19,6 +19,9 @@ class FrameSource {
     // returned it included): with ring() >= 2 the capture loop grabs and uploads
     // frame n+1 while frame n is still being encoded.
     virtual int ring() const { return 1; }
+    // Row ranges [y0, y1) (pairs in `rows`) of the last grab that differ from the grab
+    // before it; false when the source does not know (the whole frame counts as changed).
+    virtual bool damage(std::vector<int>* rows) { (void)rows; return false; }
     virtual const char* name() const = 0;
     // K13 on the GPU: with set_cursor_overlay(true) a source that captures the cursor
     // stops drawing it into the frame and reports it instead; cursor() returns the

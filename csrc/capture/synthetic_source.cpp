@@ -115,17 +115,42 @@ class SyntheticSource : public FrameSource {
 class PoolSource : public FrameSource {
    public:
     PoolSource(const uint8_t* base, int frames, int stride, int h, int phase)
-        : base_(base), frames_(frames), stride_(stride), h_(h), t_(phase) {}
+        : base_(base), frames_(frames), stride_(stride), h_(h), t_(phase) {
+        // What XDamage reports for a display: the 16-row bands of pool frame j that differ
+        // from frame j - 1 (the frame grabbed before it). The pool is immutable while the
+        // session runs, so this is computed once, here, outside any timed frame.
+        dmg_.resize(frames_);
+        for (int j = 0; j < frames_; j++) {
+            const uint8_t* a = frame(j);
+            const uint8_t* b = frame((j + frames_ - 1) % frames_);
+            std::vector<int>& d = dmg_[j];
+            for (int y0 = 0; y0 < h_; y0 += 16) {
+                const int y1 = y0 + 16 < h_ ? y0 + 16 : h_;
+                if (memcmp(a + (size_t)y0 * stride_, b + (size_t)y0 * stride_, (size_t)(y1 - y0) * stride_) == 0) continue;
+                if (!d.empty() && d.back() == y0) d.back() = y1;   // extend the previous range
+                else { d.push_back(y0); d.push_back(y1); }
+            }
+        }
+    }
     const uint8_t* grab(int* stride) override {
         *stride = stride_;
-        return base_ + (size_t)(t_++ % frames_) * stride_ * h_;
+        cur_ = t_++ % frames_;
+        return frame(cur_);
     }
     int ring() const override { return frames_; }
     const char* name() const override { return "pool"; }
+    bool damage(std::vector<int>* rows) override {
+        if (cur_ < 0) return false;
+        *rows = dmg_[cur_];
+        return true;
+    }
 
    private:
+    const uint8_t* frame(int j) const { return base_ + (size_t)j * stride_ * h_; }
     const uint8_t* base_;
     int frames_, stride_, h_, t_;
+    int cur_ = -1;
+    std::vector<std::vector<int>> dmg_;
 };
 
 }  // namespace

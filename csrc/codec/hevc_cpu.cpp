@@ -139,6 +139,7 @@ CpuHevcEncoder::CpuHevcEncoder(const h264::EncoderConfig& cfg) : fe(front_config
     sao_own.assign(n, SaoParams{});
     sao.assign(n, SaoParams{});
     sao_cost.assign(n, 0);
+    sao_md.assign((size_t)n * kSaoMd, 0);
     build_parameter_sets(fe.g.W, fe.g.H, cfg.full_range, cfg.fps, param_sets);
 }
 
@@ -340,12 +341,21 @@ void CpuHevcEncoder::sao_analyse() {
                     for (int x = cx * pl.n; x < (cx + 1) * pl.n; x++)
                         sao_collect(st, pl, fe.rec[c].data(), stride, x, y, fe.src[c][(size_t)y * stride + x]);
             }
-            sao_cost[idx] = sao_decide(&sao_stats[(size_t)3 * idx], fe.tasks[cy / geo.rows_per_slice].qp, sao_own[idx]);
+            const int lam = sao_lambda(fe.tasks[cy / geo.rows_per_slice].qp);
+            SaoTables tb;
+            for (int i = 0; i < kSaoTableEntries; i++) sao_table_entry(&sao_stats[(size_t)3 * idx], lam, i, tb);
+            for (int i = 0; i < 96; i++) sao_window(lam, i, tb);
+            sao_cost[idx] = sao_pick(tb, lam, sao_own[idx]);
+        }
+    for (int cy = 0; cy < geo.ctb_h; cy++)
+        for (int cx = 0; cx < geo.ctb_w; cx++) {
+            const size_t idx = (size_t)cy * geo.ctb_w + cx;
+            sao_merge_dists(&sao_stats[3 * idx], &sao_own[(size_t)cy * geo.ctb_w], cx, &sao_md[idx * kSaoMd]);
         }
     for (int cy = 0; cy < geo.ctb_h; cy++) {
         const SliceTask& t = fe.tasks[cy / geo.rows_per_slice];
         const size_t o = (size_t)cy * geo.ctb_w;
-        sao_row_merge(&sao_stats[3 * o], &sao_own[o], &sao_cost[o], geo.ctb_w, t.qp, cy > t.first_row, &sao[o]);
+        sao_row_merge(&sao_md[o * kSaoMd], &sao_own[o], &sao_cost[o], geo.ctb_w, t.qp, cy > t.first_row, &sao[o]);
     }
 }
 

@@ -92,6 +92,7 @@ class CpuHevcEncoder {
     std::vector<SaoStats> sao_stats;   // 3 per CTB (Y, Cb, Cr)
     std::vector<SaoParams> sao_own, sao;   // per CTB: own decision, final (after merges)
     std::vector<long long> sao_cost;
+    std::vector<long long> sao_md;     // kSaoMd per CTB: merge-candidate distortions (sao_merge_dists)
     std::vector<uint8_t> param_sets;   // VPS + SPS + PPS
     int poc = 0;                       // POC of the next picture
 

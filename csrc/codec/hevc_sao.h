@@ -105,18 +105,42 @@ SK_HD long long sao_best_offset(int s, int n, int lo, int hi, bool sign_bin, int
     return best;
 }
 
-// Own parameters of one CTB from its three components' stats: per component (Cb and Cr
-// jointly for type and class) the cheapest of off / each edge class / the best band
-// window. Returns the total cost (16 * SSE change + lambda * bits) of the chosen set,
-// merge flags excluded.
-SK_HD long long sao_decide(const SaoStats* st, int qp, SaoParams& p) {
-    const int lam = SAO_LAMBDA_Q4[sk_clip(qp, 0, 51)];
-    for (int c = 0; c < 3; c++) {
-        p.type[c] = SAO_OFF;
-        p.eo_class[c] = 0;
-        p.band_pos[c] = 0;
-        for (int k = 0; k < 4; k++) p.off[c][k] = 0;
+// Own parameters of one CTB, in two steps so the GPU can run the first one lane-parallel:
+// (1) sao_tables: the best offset and its cost for every edge category (component, class,
+// category) and every band, and the cost of every 4-band window; (2) sao_pick: per
+// component group (luma; Cb + Cr, which share type and class) the cheapest of off / each
+// edge class / the best band windows, first minimum in that order. Costs are
+// 16 * SSE change + lambda * bins.
+struct SaoTables {
+    long long eo_c[3][4][4];
+    long long bo_c[3][32];
+    long long win[3][32];
+    int8_t eo_o[3][4][4];
+    int8_t bo_o[3][32];
+};
+// Entry `i` of the best-offset tables: i < 48 edge (c, cls, k), else band (c, b).
+SK_HD void sao_table_entry(const SaoStats* st, int lam, int i, SaoTables& t) {
+    int o;
+    if (i < 48) {
+        const int c = i >> 4, cls = (i >> 2) & 3, k = i & 3;
+        t.eo_c[c][cls][k] = sao_best_offset(st[c].eo_s[cls][k], st[c].eo_n[cls][k], k < 2 ? 0 : -7, k < 2 ? 7 : 0,
+                                            false, lam, &o);
+        t.eo_o[c][cls][k] = (int8_t)o;
+    } else {
+        const int c = (i - 48) >> 5, b = (i - 48) & 31;
+        t.bo_c[c][b] = sao_best_offset(st[c].bo_s[b], st[c].bo_n[b], -7, 7, true, lam, &o);
+        t.bo_o[c][b] = (int8_t)o;
     }
+}
+constexpr int kSaoTableEntries = 48 + 96;
+// Window `i` (c = i >> 5, position i & 31): band_position (5 bits) + its four bands.
+SK_HD void sao_window(int lam, int i, SaoTables& t) {
+    const int c = i >> 5, ps = i & 31;
+    long long w = (long long)lam * 5;
+    for (int k = 0; k < 4; k++) w += t.bo_c[c][(ps + k) & 31];
+    t.win[c][ps] = w;
+}
+SK_HD long long sao_pick(const SaoTables& t, int lam, SaoParams& p) {
     p.merge_left = 0;
     p.pad = 0;
     long long total = 0;
@@ -124,67 +148,42 @@ SK_HD long long sao_decide(const SaoStats* st, int qp, SaoParams& p) {
         const int c0 = grp ? 1 : 0, c1 = grp ? 2 : 0;
         long long best = (long long)lam * 1;   // sao_type_idx = 0: one bin
         int btype = SAO_OFF, bcls = 0;
-        int boff[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, bpos[2] = {0, 0};
         for (int cls = 0; cls < 4; cls++) {
-            long long cost = (long long)lam * (2 + (grp ? 2 : 2));   // type (2 bins) + class (2 bits, once)
-            int o[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+            long long cost = (long long)lam * 4;   // type (2 bins) + class (2 bits, once per group)
             for (int c = c0; c <= c1; c++)
-                for (int k = 0; k < 4; k++)
-                    cost += sao_best_offset(st[c].eo_s[cls][k], st[c].eo_n[cls][k], k < 2 ? 0 : -7, k < 2 ? 7 : 0,
-                                            false, lam, &o[c - c0][k]);
-            if (cost < best) {
-                best = cost;
-                btype = SAO_EDGE;
-                bcls = cls;
-                for (int i = 0; i < 2; i++)
-                    for (int k = 0; k < 4; k++) boff[i][k] = o[i][k];
-            }
+                for (int k = 0; k < 4; k++) cost += t.eo_c[c][cls][k];
+            if (cost < best) { best = cost; btype = SAO_EDGE; bcls = cls; }
         }
-        {   // band: per component the best window of 4 bands (band_position, 5 bits)
-            long long cost = (long long)lam * 2;
-            int o[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pos[2] = {0, 0};
-            for (int c = c0; c <= c1; c++) {
-                long long bc[32];
-                int bo[32];
-                for (int b = 0; b < 32; b++) bc[b] = sao_best_offset(st[c].bo_s[b], st[c].bo_n[b], -7, 7, true, lam, &bo[b]);
-                long long wbest = 0;
-                int wpos = 0;
-                for (int ps = 0; ps < 32; ps++) {
-                    long long w = (long long)lam * 5;
-                    for (int k = 0; k < 4; k++) w += bc[(ps + k) & 31];
-                    if (ps == 0 || w < wbest) { wbest = w; wpos = ps; }
-                }
-                cost += wbest;
-                pos[c - c0] = wpos;
-                for (int k = 0; k < 4; k++) o[c - c0][k] = bo[(wpos + k) & 31];
-            }
-            if (cost < best) {
-                best = cost;
-                btype = SAO_BAND;
-                for (int i = 0; i < 2; i++) {
-                    bpos[i] = pos[i];
-                    for (int k = 0; k < 4; k++) boff[i][k] = o[i][k];
-                }
-            }
+        long long bcost = (long long)lam * 2;
+        int bpos[3] = {0, 0, 0};
+        for (int c = c0; c <= c1; c++) {
+            long long wbest = t.win[c][0];
+            for (int ps = 1; ps < 32; ps++)
+                if (t.win[c][ps] < wbest) { wbest = t.win[c][ps]; bpos[c] = ps; }
+            bcost += wbest;
         }
-        // an "on" set whose offsets are all zero is worse than off: keep off then
+        if (bcost < best) { best = bcost; btype = SAO_BAND; }
         bool any = false;
-        for (int i = 0; i <= c1 - c0; i++)
-            for (int k = 0; k < 4; k++) any |= boff[i][k] != 0;
-        if (!any) {
-            btype = SAO_OFF;
-            best = (long long)lam * 1;
-        }
         for (int c = c0; c <= c1; c++) {
             p.type[c] = (uint8_t)btype;
             p.eo_class[c] = (uint8_t)(btype == SAO_EDGE ? bcls : 0);
-            p.band_pos[c] = (uint8_t)(btype == SAO_BAND ? bpos[c - c0] : 0);
-            for (int k = 0; k < 4; k++) p.off[c][k] = (int8_t)(btype == SAO_OFF ? 0 : boff[c - c0][k]);
+            p.band_pos[c] = (uint8_t)(btype == SAO_BAND ? bpos[c] : 0);
+            for (int k = 0; k < 4; k++) {
+                const int o = btype == SAO_EDGE ? t.eo_o[c][bcls][k]
+                                                : (btype == SAO_BAND ? t.bo_o[c][(bpos[c] + k) & 31] : 0);
+                p.off[c][k] = (int8_t)o;
+                any |= o != 0;
+            }
+        }
+        if (!any) {   // an "on" set whose offsets are all zero is worse than off
+            best = (long long)lam * 1;
+            for (int c = c0; c <= c1; c++) p.type[c] = p.eo_class[c] = p.band_pos[c] = 0;
         }
         total += best;
     }
     return total;
 }
+SK_HD int sao_lambda(int qp) { return SAO_LAMBDA_Q4[sk_clip(qp, 0, 51)]; }
 
 // Distortion change (16 * SSE) of parameter set p on a CTB's stats (merge evaluation).
 SK_HD long long sao_params_dist(const SaoStats* st, const SaoParams& p) {
@@ -200,24 +199,52 @@ SK_HD long long sao_params_dist(const SaoStats* st, const SaoParams& p) {
     }
     return d;
 }
+SK_HD bool sao_same(const SaoParams& a, const SaoParams& b) {
+    for (int c = 0; c < 3; c++) {
+        if (a.type[c] != b.type[c] || a.eo_class[c] != b.eo_class[c] || a.band_pos[c] != b.band_pos[c]) return false;
+        for (int k = 0; k < 4; k++)
+            if (a.off[c][k] != b.off[c][k]) return false;
+    }
+    return true;
+}
 
 // Merge decision along one CTB row (sequential: a merged CTB copies its left neighbour's
-// final parameters). own[x] / own_cost[x]: sao_decide's result per CTB; out[x]: final.
+// final parameters, i.e. the own parameters of the CTB the run started at). The
+// distortion of those parameters on CTB x comes precomputed (all CTBs in parallel):
+// md[x][j] = sao_params_dist(stats of x, own[x - 1 - j]) for j < kSaoMergeWin, and
+// md[x][kSaoMergeWin] = the own parameters' distortion. A run that started further back
+// is continued only with identical parameters (then merging is never worse).
 // Merge-up is never chosen (rows stay independent); its flag is still coded as 0.
-SK_HD void sao_row_merge(const SaoStats* st_row, const SaoParams* own, const long long* own_cost, int ctb_w, int qp,
+constexpr int kSaoMergeWin = 8;
+constexpr int kSaoMd = kSaoMergeWin + 1;
+SK_HD void sao_merge_dists(const SaoStats* st_x, const SaoParams* own_row, int x, long long* md) {
+    for (int j = 0; j < kSaoMergeWin; j++) md[j] = x - 1 - j >= 0 ? sao_params_dist(st_x, own_row[x - 1 - j]) : 0;
+    md[kSaoMergeWin] = sao_params_dist(st_x, own_row[x]);
+}
+SK_HD void sao_row_merge(const long long* md_row, const SaoParams* own, const long long* own_cost, int ctb_w, int qp,
                          bool has_up, SaoParams* out) {
-    const int lam = SAO_LAMBDA_Q4[sk_clip(qp, 0, 51)];
+    const int lam = sao_lambda(qp);
+    int src = 0;   // CTB whose own parameters the previous CTB's final parameters are
     for (int x = 0; x < ctb_w; x++) {
         SaoParams p = own[x];
+        int sx = x;
         if (x > 0) {
+            const int j = x - 1 - src;
+            const long long* md = md_row + (size_t)x * kSaoMd;
+            bool ok = true;
+            long long dm = 0;
+            if (j < kSaoMergeWin) dm = md[j];
+            else if (sao_same(own[x], own[src])) dm = md[kSaoMergeWin];
+            else ok = false;
             const long long cown = own_cost[x] + (long long)lam * (has_up ? 2 : 1);   // merge_left = 0 (+ merge_up = 0)
-            const long long cmerge = sao_params_dist(st_row + 3 * x, out[x - 1]) + (long long)lam * 1;
-            if (cmerge < cown) {
-                p = out[x - 1];
+            if (ok && dm + (long long)lam * 1 < cown) {
+                p = own[src];
                 p.merge_left = 1;
+                sx = src;
             }
         }
         out[x] = p;
+        src = sx;
     }
 }
 

@@ -43,6 +43,7 @@ struct HevcArgs {
     SaoStats* sao_stats;        // [ctbs][3] Y, Cb, Cr
     SaoParams* sao_own;         // [ctbs] each CTB's own decision (k_hevc_sao_stats)
     long long* sao_cost;        // [ctbs] its cost
+    long long* sao_md;          // [ctbs][kSaoMd] merge-candidate distortions (sao_merge_dists)
     SaoParams* sao;             // [ctbs] final parameters after the row merge pass (k_hevc_sao_row)
     h264::gpu::Planes sao_tmp;  // filtered samples of the CTBs SAO changes, copied back into f.rec
 };

@@ -12,7 +12,8 @@
 //   k_hevc_hdr         slice header with entry points, NAL prefix, substream offsets
 //   k_hevc_ep_copy     wave-parallel emulation prevention + copy into host-mapped slots
 //   k_hevc_dbk_v/h     in-loop deblocking (before the syntax: SAO decides on its output)
-//   k_hevc_sao_*       SAO: stats + own decision per CTB, row merge pass, filter + copy back
+//   k_hevc_sao_*       SAO: stats + own decision per CTB (lane-parallel tables), merge
+//                      candidate distortions, row merge pass (LDS), filter + copy back
 // Bit-exact with the CPU reference (codec/hevc_cpu.cpp): integer math only.
 #include "hevc_gpu.h"
 
@@ -1211,6 +1212,7 @@ __device__ __forceinline__ SaoPlane sao_plane_of(const FrameArgs& f, int c) {
 
 __global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
     __shared__ SaoStats Sw[4][3];
+    __shared__ SaoTables Tw[4];
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
     const int idx = blockIdx.x * 4 + w;
@@ -1248,22 +1250,55 @@ __global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
     wsync();
     int32_t* g = reinterpret_cast<int32_t*>(A.sao_stats + (size_t)3 * idx);
     for (int i = l; i < 3 * kSaoStatsInts; i += 64) g[i] = z[i];
+    // the decision's tables lane-parallel (144 best offsets, then 96 band windows), the
+    // pick on lane 0: the same functions, in the same order, as the host
+    SaoTables& T = Tw[w];
+    const int lam = sao_lambda(t.qp);
+    for (int i = l; i < kSaoTableEntries; i += 64) sao_table_entry(st, lam, i, T);
+    wsync();
+    for (int i = l; i < 96; i += 64) sao_window(lam, i, T);
+    wsync();
     if (l == 0) {
         SaoParams p;
-        A.sao_cost[idx] = sao_decide(st, t.qp, p);
+        A.sao_cost[idx] = sao_pick(T, lam, p);
         A.sao_own[idx] = p;
     }
 }
 
-// Merge pass: one thread per CTB row, left to right (a merged CTB copies its left
-// neighbour's final parameters).
-__global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
+// Merge-candidate distortions: one thread per (CTB, candidate) (sao_merge_dists).
+__global__ __launch_bounds__(256) void k_hevc_sao_md(HevcArgs A) {
     const FrameArgs& f = A.f;
-    const int cy = blockIdx.x * 64 + threadIdx.x;
-    if (cy >= f.mb_h) return;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
-    const size_t o = (size_t)cy * f.mb_w;
-    sao_row_merge(A.sao_stats + 3 * o, A.sao_own + o, A.sao_cost + o, f.mb_w, t.qp, cy > t.first_row, A.sao + o);
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= f.mb_w * f.mb_h * kSaoMd) return;
+    const int idx = t / kSaoMd, j = t - idx * kSaoMd, cx = idx % f.mb_w;
+    const SaoParams* own_row = A.sao_own + (idx - cx);
+    const SaoStats* st = A.sao_stats + (size_t)3 * idx;
+    long long d = 0;
+    if (j == kSaoMergeWin) d = sao_params_dist(st, own_row[cx]);
+    else if (cx - 1 - j >= 0) d = sao_params_dist(st, own_row[cx - 1 - j]);
+    A.sao_md[t] = d;
+}
+
+// Merge pass: one workgroup per CTB row. The row's candidate distortions, own
+// parameters and costs are staged in LDS by all lanes; lane 0 then walks the row left to
+// right (a merged CTB copies its left neighbour's final parameters) touching only LDS.
+__global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
+    __shared__ long long md[kPcMaxRowCtb * kSaoMd];
+    __shared__ SaoParams own[kPcMaxRowCtb];
+    __shared__ long long cost[kPcMaxRowCtb];
+    const FrameArgs& f = A.f;
+    const int cy = blockIdx.x, l = threadIdx.x, W = f.mb_w;
+    const size_t o = (size_t)cy * W;
+    for (int i = l; i < W * kSaoMd; i += 64) md[i] = A.sao_md[o * kSaoMd + i];
+    for (int i = l; i < W; i += 64) {
+        own[i] = A.sao_own[o + i];
+        cost[i] = A.sao_cost[o + i];
+    }
+    __syncthreads();
+    if (l == 0) {
+        const SliceTask t = f.tasks[cy / f.rows_per_slice];
+        sao_row_merge(md, own, cost, W, t.qp, cy > t.first_row, A.sao + o);
+    }
 }
 
 __device__ __forceinline__ bool sao_any(const SaoParams& p) { return (p.type[0] | p.type[1] | p.type[2]) != 0; }
@@ -1316,7 +1351,8 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
     if (nh > 0) hipLaunchKernelGGL(k_hevc_dbk_h, dim3((nh + 255) / 256), dim3(256), 0, s, a);
     const int nq = (n + 3) / 4;
     hipLaunchKernelGGL(k_hevc_sao_stats, dim3(nq), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_sao_row, dim3((ch + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sao_md, dim3((n * kSaoMd + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sao_row, dim3(ch), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(192), 0, s, a);

@@ -202,11 +202,12 @@ class CaptureSession {
     static constexpr double kHistLe[kHist - 1] = {0.25, 0.5, 1, 2, 4, 8, 16, 33};
     void stats(double* out, int n) {
         std::lock_guard<std::mutex> g(mu_);
-        double v[7 + kHist] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
+        double v[8 + kHist] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
                                (double)packets_, src_kind_, last_enc_ms_};
         for (int i = 0; i < kHist; i++) v[6 + i] = (double)hist_[i];
         v[6 + kHist] = (double)inflight_max_;   // frames in flight actually used (1 or 2)
-        for (int i = 0; i < n && i < 7 + kHist; i++) out[i] = v[i];
+        v[7 + kHist] = enc_ ? enc_->upload_fraction() : 1.0;   // rows uploaded / rows captured
+        for (int i = 0; i < n && i < 8 + kHist; i++) out[i] = v[i];
     }
     // Capture-to-packets latency (ms) of the most recent frames, oldest first;
     // returns the count copied. reset != 0 clears the record afterwards.
@@ -280,8 +281,14 @@ class CaptureSession {
         }
         // JPEG (or an image the encoder cannot hold): blend on the host into the grab
         // buffer (ours: SHM segment / ring; pool frames are never composited)
-        if (have_wm && !wm_on_gpu_ && pool_ == nullptr)
+        bool composited = false;
+        if (have_wm && !wm_on_gpu_ && pool_ == nullptr) {
             composite_watermark(const_cast<uint8_t*>(px), stride, id, *wm);
+            composited = true;
+        }
+        // damage-driven upload: only rows the source reports as changed cross PCIe
+        if (!composited && src_->damage(&dmg_rows_)) enc_->set_upload_rows(dmg_rows_.data(), (int)dmg_rows_.size() / 2);
+        else enc_->set_upload_rows(nullptr, -1);
         try {
             if (enc_->upload(px, stride, id) < 0 || enc_->launch() < 0) return false;
         } catch (const std::exception& ex) {
@@ -494,6 +501,7 @@ class CaptureSession {
     std::vector<uint8_t> cursor_px_;
     int registered_device_ = -1;
     const uint8_t* pool_ = nullptr;
+    std::vector<int> dmg_rows_;
     sk_frame_cb frame_cb_ = nullptr;
     void* frame_user_ = nullptr;
     std::mutex step_mu_;

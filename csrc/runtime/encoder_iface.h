@@ -39,6 +39,13 @@ class EncoderBackend {
     // kernels: upload(n+1) ... finish(n) ... launch(n+1), or with two frames in
     // flight upload(n+1) launch(n+1) ... finish(n). Default: upload encodes.
     virtual int upload(const uint8_t* bgrx, int stride, uint16_t frame_id) { return submit(bgrx, stride, frame_id); }
+    // Damage of the next upload(): `n` row ranges [r[2i], r[2i+1]) that differ from the
+    // previously uploaded frame (n < 0: unknown, everything). A backend that keeps the
+    // frame on the device may then copy only those rows (HIP: rows changed since the
+    // frame its upload buffer last held).
+    virtual void set_upload_rows(const int* r, int n) { (void)r; (void)n; }
+    // Fraction of frame rows uploaded so far (1.0 without damage-driven uploads).
+    virtual double upload_fraction() const { return 1.0; }
     // The next upload() waits (on the device) for the work queued so far on a foreign
     // HIP stream of this device, e.g. the torch stream an RCCL scatter wrote the frame on.
     virtual int wait_stream(void* stream) { (void)stream; return 0; }

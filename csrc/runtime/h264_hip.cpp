@@ -14,6 +14,7 @@
 #include "../kernels/runtime_kernels.h"
 #include "../codec/hevc_encoder.h"
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <mutex>
@@ -22,6 +23,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <atomic>
 
 namespace sk {
 namespace {
@@ -104,6 +106,50 @@ class HipBackend : public EncoderBackend {
     // Stage a frame: H2D into the input buffer of the frame's parity on the copy
     // stream. May be called while the previous frame is still encoding (its upload
     // then overlaps that frame's kernels); launch() comes after finish() of it.
+    double upload_fraction() const override {
+        const long long t = up_rows_total_.load();
+        return t ? (double)up_rows_copied_.load() / (double)t : 1.0;
+    }
+    void set_upload_rows(const int* r, int n) override {
+        up_next_known_ = n >= 0;
+        up_next_.assign(r && n > 0 ? r : nullptr, r && n > 0 ? r + 2 * n : nullptr);
+    }
+
+    // Damage-driven upload: bgrx_dev_[q] holds the frame uploaded two frames ago, so the
+    // rows that changed since then (this frame's damage and the previous frame's) are
+    // copied; everything else is already on the device. Full copy when either damage is
+    // unknown, the buffer was never filled or the frame is scaled on the device.
+    void upload_copy(int q, const uint8_t* bgrx, int stride, size_t in_bytes, hipStream_t cs) {
+        const int rows = (int)(in_bytes / (size_t)stride);
+        const bool partial = up_valid_[q] && up_next_known_ && up_prev_known_ && !args_.scaled;
+        if (!partial) {
+            HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyDefault, cs));
+        } else {
+            // union of the two damage lists on 16-row bands, copied as maximal row ranges
+            std::vector<uint8_t> band((size_t)(rows + 15) / 16, 0);
+            for (const auto* v : {&up_next_, &up_prev_})
+                for (size_t i = 0; i + 1 < v->size(); i += 2)
+                    for (int y = (*v)[i] / 16; y * 16 < (*v)[i + 1] && y < (int)band.size(); y++) band[y] = 1;
+            for (int b = 0; b < (int)band.size();) {
+                if (!band[b]) { b++; continue; }
+                int e = b;
+                while (e < (int)band.size() && band[e]) e++;
+                const int y0 = b * 16, y1 = std::min(rows, e * 16);
+                HIPCHECK(hipMemcpyAsync(bgrx_dev_[q] + (size_t)y0 * stride, bgrx + (size_t)y0 * stride,
+                                        (size_t)(y1 - y0) * stride, hipMemcpyDefault, cs));
+                up_rows_copied_ += y1 - y0;
+                b = e;
+            }
+        }
+        if (!partial) up_rows_copied_ += rows;
+        up_rows_total_ += rows;
+        up_valid_[q] = true;
+        up_prev_known_ = up_next_known_;
+        up_prev_.swap(up_next_);
+        up_next_known_ = false;   // one damage report per upload
+        up_next_.clear();
+    }
+
     int upload(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         trace::Range frame_range("h264.upload");
         HIPCHECK(hipSetDevice(device_));
@@ -117,6 +163,7 @@ class HipBackend : public EncoderBackend {
                 }
                 bgrx_cap_ = in_bytes;
             }
+            up_valid_[0] = up_valid_[1] = false;
             invalidate_graphs();
             args_.bgrx_stride = stride;
         }
@@ -144,7 +191,7 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipEventRecord(ev_[3 * q], cs));
         // hipMemcpyDefault: the frame may be host memory (capture) or device memory (a band
         // scattered to this GPU over RCCL, parallel/dist_banded.py)
-        HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyDefault, cs));
+        upload_copy(q, bgrx, stride, in_bytes, cs);
         if (cs != stream_) HIPCHECK(hipEventRecord(ev_copy_[q], cs));
         staged_on_main_ = cs == stream_;
         staged_ = true;
@@ -657,6 +704,7 @@ class HipBackend : public EncoderBackend {
         h.sao_stats = dmalloc<hevc::SaoStats>((size_t)3 * n, false);
         h.sao_own = dmalloc<hevc::SaoParams>(n);
         h.sao_cost = dmalloc<long long>(n);
+        h.sao_md = dmalloc<long long>((size_t)n * hevc::kSaoMd);
         h.sao = dmalloc<hevc::SaoParams>(n);
         h.sao_tmp.y = dmalloc<uint8_t>((size_t)g_.stride_y * g_.mb_h * 16, false);
         h.sao_tmp.u = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
@@ -875,6 +923,11 @@ class HipBackend : public EncoderBackend {
     uint16_t frame_of_[2] = {0, 0};
     uint16_t staged_frame_ = 0;
     size_t bgrx_cap_ = 0;
+    // damage-driven upload (set_upload_rows / upload_copy)
+    bool up_valid_[2] = {false, false};      // bgrx_dev_[q] holds a complete frame
+    bool up_next_known_ = false, up_prev_known_ = false;
+    std::vector<int> up_next_, up_prev_;     // row ranges of this frame / the previous one
+    std::atomic<long long> up_rows_copied_{0}, up_rows_total_{0};   // read by the stats thread
     uint8_t* host_out_[2] = {nullptr, nullptr};
     uint8_t* host_out_dev_[2] = {nullptr, nullptr};
     int* host_size_dev_[2] = {nullptr, nullptr};

@@ -156,14 +156,16 @@ class ScreenCapture:
             self._lib.sk_capture_set_rate(self._h, {"cqp": 0, "crf": 1, "cbr": 2}[mode], int(kbps))
 
     def stats(self) -> dict:
-        arr = (ctypes.c_double * 16)()
-        self._lib.sk_capture_stats(self._h, arr, 16)
+        arr = (ctypes.c_double * 17)()
+        self._lib.sk_capture_stats(self._h, arr, 17)
         return {"frames": int(arr[0]), "encode_ms_mean": arr[1], "bytes": int(arr[2]),
                 "packets": int(arr[3]), "source": {1.0: "x11", 0.0: "synthetic"}.get(arr[4], "none"),
                 "encode_ms_last": arr[5],
                 # per-frame encode time histogram (native, bucket upper bounds in ms; last = +Inf)
                 "encode_ms_buckets": list(ENCODE_MS_BUCKETS), "encode_ms_counts": [int(x) for x in arr[6:15]],
-                "frames_in_flight": int(arr[15])}
+                "frames_in_flight": int(arr[15]),
+                # damage-driven upload: fraction of captured rows that crossed PCIe
+                "upload_fraction": arr[16]}
 
     def close(self) -> None:
         self.stop_capture()

@@ -22,9 +22,9 @@ def _pool(W, H, n=4, kind="motion"):
     return pool
 
 
-def _run_step(use_cpu: int, W=256, H=128, frames=6, fullframe=0):
+def _run_step(use_cpu: int, W=256, H=128, frames=6, fullframe=0, kind="motion"):
     import pixelflux
-    pool = _pool(W, H)
+    pool = _pool(W, H, kind=kind)
     got = []
     lock = threading.Lock()
 
@@ -111,13 +111,20 @@ def test_step_mode_hip_two_in_flight():
 
 
 @pytest.mark.gpu
-def test_hip_capture_matches_cpu_capture():
-    """Same pool through the HIP and the CPU capture loops: byte-identical packets."""
+@pytest.mark.parametrize("kind", ["motion", "desktop"])
+def test_hip_capture_matches_cpu_capture(kind):
+    """Same pool through the HIP and the CPU capture loops: byte-identical packets. On
+    desktop content the HIP loop uploads only the rows the pool source reports as damaged
+    (what XDamage gives a display): fewer rows cross PCIe, same bytes out."""
     from selkies_gstreamer_amd.ops.native import require_gpu
     require_gpu()
-    _, g_hip, _, _ = _run_step(use_cpu=0, W=320, H=192, frames=5)
-    _, g_cpu, _, _ = _run_step(use_cpu=1, W=320, H=192, frames=5)
+    _, g_hip, _, st = _run_step(use_cpu=0, W=320, H=192, frames=9, kind=kind)
+    _, g_cpu, _, _ = _run_step(use_cpu=1, W=320, H=192, frames=9, kind=kind)
     assert [[d for *_, d in f] for f in g_hip] == [[d for *_, d in f] for f in g_cpu]
+    if kind == "desktop":
+        assert st["upload_fraction"] < 0.8, st["upload_fraction"]
+    else:
+        assert st["upload_fraction"] > 0.95
 
 
 @pytest.mark.gpu
