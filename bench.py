@@ -105,7 +105,7 @@ def parse():
     return p.parse_args()
 
 
-def run_capture_path(args, pool, local_rank):
+def run_capture_path(args, pool, local_rank, fast_cpu=False):
     """Times the production serving loop: S native capture sessions on this GPU.
 
     Each session is a pixelflux ScreenCapture whose frame source is the pinned
@@ -136,7 +136,9 @@ def run_capture_path(args, pool, local_rank):
                                         pool_phase=3 * i,
                                         target_fps=float(args.fps),
                                         h264_rc_mode={"cqp": 0, "crf": 1, "cbr": 2}[args.rc],
-                                        h264_bitrate_kbps=args.kbps if args.rc == "cbr" else 0)
+                                        h264_bitrate_kbps=args.kbps if args.rc == "cbr" else 0,
+                                        # CPU plumbing (config 1): diamond search, integer vectors
+                                        h264_me_full=-1 if fast_cpu else 0, h264_subpel=-1 if fast_cpu else 0)
         cs.pool = pool.array.ctypes.data
         c = pixelflux.ScreenCapture()
         c.start_frame_capture(cs, null_cb)
@@ -196,7 +198,7 @@ def e2e_counts(args, world=1):
     return v
 
 
-def run_extra(args, W, H, encoder, fps, local_rank, steps):
+def run_extra(args, W, H, encoder, fps, local_rank, steps, backend=None):
     """One W x H session of `encoder` through the production capture loop, timed over
     `steps` frames after a warm-up (key frame + steady state); runs after the headline
     window. Reports throughput, capture->packet latency and the frame-interval budget."""
@@ -210,9 +212,12 @@ def run_extra(args, W, H, encoder, fps, local_rank, steps):
             src.frame(i, out=pool.array[i])
         a = types.SimpleNamespace(**vars(args))
         a.sessions, a.encoder, a.pool, a.mode, a.fps = 1, encoder, 8, "fullframe", float(fps)
+        if backend is not None:
+            a.backend = backend
+        cpu_fast = a.backend == "cpu" and backend is not None   # x264 "ultrafast"-like tools
         if encoder == "av1" and args.av1_kbps > 0:
             a.rc, a.kbps = "cbr", args.av1_kbps
-        caps, run_caps = run_capture_path(a, pool, local_rank)
+        caps, run_caps = run_capture_path(a, pool, local_rank, fast_cpu=cpu_fast)
         run_caps(10)
         caps[0].latencies(reset=True)
         b0 = caps[0].stats()["bytes"]
@@ -251,7 +256,8 @@ def run_extra(args, W, H, encoder, fps, local_rank, steps):
                           "method": f"one frame granted every {budget:.3f} ms (source at {fps} fps)"},
                 "realtime_at_source_rate": bool(steps / el >= fps and pp99 < budget),
                 "kib_per_frame": round((st["bytes"] - b0) / steps / 1024, 1),
-                "frames_in_flight": st.get("frames_in_flight"), "rate_control": rc_desc(a)}
+                "frames_in_flight": st.get("frames_in_flight"), "rate_control": rc_desc(a),
+                "backend": a.backend + (" (diamond ME, integer-pel: x264 ultrafast-like)" if cpu_fast else "")}
     except Exception as ex:   # noqa: BLE001 - reported, never fatal for the headline
         return {"resolution": f"{W}x{H}", "encoder": encoder, "error": f"{type(ex).__name__}: {ex}"}
 
@@ -557,6 +563,9 @@ def main():
     if args.extra_4k and args.backend == "hip" and not args.gather and rank == 0:
         extras["hevc_4k"] = run_extra(args, 3840, 2160, "hevc", 60, local_rank, args.extra_steps)
         extras["av1_4k"] = run_extra(args, 3840, 2160, "av1", 120, local_rank, 2 * args.extra_steps)
+        # BASELINE config 1 (640x480@30, software H.264 plumbing): the CPU reference encoder
+        # through the same capture loop, no GPU involved
+        extras["cpu_480p"] = run_extra(args, 640, 480, "h264", 30, local_rank, args.extra_steps, backend="cpu")
     if rank == 0:
         n_gpus = max(world, 1)
         res = {

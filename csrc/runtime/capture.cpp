@@ -107,6 +107,7 @@ class CaptureSession {
                 e.fps = (float)(s.target_fps > 0 ? s.target_fps : 60.0);
                 e.aq_strength = sk_clip(s.h264_aq_strength, 0, 64);
                 e.subpel = s.h264_subpel >= 0 ? 1 : 0;
+                if (s.h264_me_full < 0) e.me_full = 0;
                 e.intra4x4 = s.h264_intra4x4 > 0 ? 1 : 0;
                 e.rc_mode = s.h264_rc_mode >= 0 && s.h264_rc_mode <= 2 ? s.h264_rc_mode : h264::RC_CQP;
                 e.bitrate_kbps = s.h264_bitrate_kbps > 0 ? s.h264_bitrate_kbps : 0;

@@ -124,6 +124,9 @@ typedef struct sk_capture_settings {
     // 1 = CRF (complexity-adaptive QP around h264_crf), 2 = CBR at h264_bitrate_kbps
     int32_t h264_rc_mode;
     int32_t h264_bitrate_kbps;
+    // < 0: no exhaustive +-16 search candidate, diamond search only (x264 "ultrafast"-like
+    // CPU plumbing; with h264_subpel < 0 the CPU encoder runs 640x480 at ~55 fps on one core)
+    int32_t h264_me_full;
 } sk_capture_settings;
 
 typedef struct sk_stripe_result {

@@ -287,6 +287,10 @@ class StreamSession:
                                        # K10 in the encoder: CBR with a 1.5-frame VBV (gstwebrtc_app.py:101-105)
                                        h264_rc_mode=2, h264_bitrate_kbps=max(1, self.rc.target_bps // 1000),
                                        use_cpu=1 if _truthy(self.args.use_cpu) else 0, source=src,
+                                       # x264enc speed-preset=ultrafast (gstwebrtc_app.py:637) on
+                                       # the CPU: diamond search, integer-pel vectors
+                                       h264_me_full=-1 if _truthy(self.args.use_cpu) else 0,
+                                       h264_subpel=-1 if _truthy(self.args.use_cpu) else 0,
                                        device=int(self.args.gpu_id), stripe_height=64,
                                        capture_cursor=0 if _truthy(self.args.enable_cursors) else 1)
         self.capture = pixelflux.ScreenCapture()

@@ -69,6 +69,7 @@ class SkCaptureSettings(ctypes.Structure):
         ("pool_frames", ctypes.c_int32), ("pool_stride", ctypes.c_int32), ("pool_phase", ctypes.c_int32),
         ("h264_aq_strength", ctypes.c_int32), ("h264_subpel", ctypes.c_int32), ("h264_intra4x4", ctypes.c_int32),
         ("h264_rc_mode", ctypes.c_int32), ("h264_bitrate_kbps", ctypes.c_int32),
+        ("h264_me_full", ctypes.c_int32),
     ]
 
 
