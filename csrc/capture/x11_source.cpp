@@ -6,6 +6,7 @@
 #include "frame_source.h"
 #include <X11/Xlib.h>
 #include <dlfcn.h>
+#include <algorithm>
 #include <hip/hip_runtime_api.h>
 #include <string.h>
 #include <sys/ipc.h>
@@ -49,6 +50,25 @@ struct XApi {
     Bool (*ShmDetach)(Display*, XShmSegmentInfo_*) = nullptr;
     Bool (*ShmGetImage)(Display*, Drawable, XImage*, int, int, unsigned long) = nullptr;
     XFixesCursorImage_* (*FixesGetCursorImage)(Display*) = nullptr;
+    // XDamage (optional, libXdamage): which rows changed since the previous grab
+    void* xdamage = nullptr;
+    Bool (*DamageQueryExtension)(Display*, int*, int*) = nullptr;
+    unsigned long (*DamageCreate)(Display*, Drawable, int) = nullptr;
+    void (*DamageSubtract)(Display*, unsigned long, unsigned long, unsigned long) = nullptr;
+    unsigned long (*FixesCreateRegion)(Display*, XRectangle*, int) = nullptr;
+    XRectangle* (*FixesFetchRegion)(Display*, unsigned long, int*) = nullptr;
+
+    bool load_damage() {
+        if (!xfixes) return false;
+        xdamage = dlopen("libXdamage.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!xdamage) return false;
+        DamageQueryExtension = reinterpret_cast<decltype(DamageQueryExtension)>(dlsym(xdamage, "XDamageQueryExtension"));
+        DamageCreate = reinterpret_cast<decltype(DamageCreate)>(dlsym(xdamage, "XDamageCreate"));
+        DamageSubtract = reinterpret_cast<decltype(DamageSubtract)>(dlsym(xdamage, "XDamageSubtract"));
+        FixesCreateRegion = reinterpret_cast<decltype(FixesCreateRegion)>(dlsym(xfixes, "XFixesCreateRegion"));
+        FixesFetchRegion = reinterpret_cast<decltype(FixesFetchRegion)>(dlsym(xfixes, "XFixesFetchRegion"));
+        return DamageQueryExtension && DamageCreate && DamageSubtract && FixesCreateRegion && FixesFetchRegion;
+    }
 
     bool load(std::string* err) {
         x11 = dlopen("libX11.so.6", RTLD_NOW | RTLD_LOCAL);
@@ -149,11 +169,19 @@ class X11Source : public FrameSource {
             g.registered = hipHostRegister(g.shm.shmaddr, bytes, hipHostRegisterDefault) == hipSuccess;
         }
         root_ = api_.DefRootWindow(dpy_);
+        int ev = 0, er = 0;
+        if (api_.load_damage() && api_.DamageQueryExtension(dpy_, &ev, &er)) {
+            damage_ = api_.DamageCreate(dpy_, root_, 3 /* XDamageReportNonEmpty */);
+            region_ = api_.FixesCreateRegion(dpy_, nullptr, 0);
+        }
         return true;
     }
     const uint8_t* grab(int* stride) override {
         cur_ = (cur_ + 1) % kRing;
         XImage* img = seg_[cur_].img;
+        // the damage accumulated so far, taken BEFORE the image: anything drawn in between
+        // is in the pixels and reported again next frame (over-reporting is harmless)
+        fetch_damage();
         if (!api_.ShmGetImage(dpy_, root_, img, x_, y_, AllPlanes)) return nullptr;
         if (cursor_ && api_.FixesGetCursorImage) {
             if (overlay_cursor_) fetch_cursor();
@@ -164,6 +192,13 @@ class X11Source : public FrameSource {
     }
     int ring() const override { return kRing; }
     const char* name() const override { return "x11-shm"; }
+    // XDamage rows of the capture region; unknown on the first grab, without the
+    // extension, or while the cursor is drawn into the image on the host.
+    bool damage(std::vector<int>* rows) override {
+        if (!dmg_ok_ || (cursor_ && !overlay_cursor_)) return false;
+        *rows = dmg_rows_;
+        return true;
+    }
     void set_cursor_overlay(bool on) override { overlay_cursor_ = on; }
     bool cursor(int* x, int* y, int* w, int* h, unsigned long* serial, unsigned long have,
                 std::vector<uint8_t>* bgra) override {
@@ -178,6 +213,22 @@ class X11Source : public FrameSource {
     }
 
    private:
+    void fetch_damage() {
+        if (!damage_) return;
+        api_.DamageSubtract(dpy_, damage_, 0, region_);
+        int n = 0;
+        XRectangle* r = api_.FixesFetchRegion(dpy_, region_, &n);
+        dmg_rows_.clear();
+        for (int i = 0; r && i < n; i++) {
+            if (r[i].x >= x_ + w_ || r[i].x + (int)r[i].width <= x_) continue;   // outside the region
+            const int y0 = std::max(0, r[i].y - y_), y1 = std::min(h_, r[i].y + (int)r[i].height - y_);
+            if (y0 < y1) { dmg_rows_.push_back(y0); dmg_rows_.push_back(y1); }
+        }
+        if (r) api_.Free(r);
+        api_.Sync(dpy_, True);   // drop the DamageNotify events nobody reads
+        dmg_ok_ = grabs_++ > 0;  // the first grab has no previous frame
+    }
+
     // Cursor state for the encoder overlay: position every grab, pixels when the
     // cursor image changes (XFixes cursor_serial).
     void fetch_cursor() {
@@ -235,6 +286,10 @@ class X11Source : public FrameSource {
     Seg seg_[kRing];
     int cur_ = kRing - 1;
     Window root_ = 0;
+    unsigned long damage_ = 0, region_ = 0;   // XDamage object and the XFixes region it is drained into
+    std::vector<int> dmg_rows_;
+    bool dmg_ok_ = false;
+    long long grabs_ = 0;
     int x_, y_, w_, h_;
     bool cursor_;
     bool overlay_cursor_ = false, have_cursor_ = false;
