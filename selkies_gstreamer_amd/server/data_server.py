@@ -733,7 +733,10 @@ class DataStreamingServer:
             cs.paint_over_jpeg_quality = int(p["paint_over_jpeg_quality"])
             cs.stripe_height = 64
         else:
-            cs.output_mode = 1
+            # H.264 (striped or full frame), HEVC (x265enc) or AV1 (svtav1enc): the same
+            # front end, rate control and packet framing (type 0x04 + 10-byte stripe header);
+            # the client picks its WebCodecs codec from the negotiated encoder
+            cs.output_mode = {"x265enc": 2, "svtav1enc": 3}.get(enc, 1)
             cs.h264_crf = int(p["h264_crf"])
             kbps = int(p.get("h264_bitrate") or 0)   # K10: CRF, or CBR at kbps
             cs.h264_rc_mode, cs.h264_bitrate_kbps = (2, kbps) if kbps > 0 else (1, 0)
@@ -741,7 +744,7 @@ class DataStreamingServer:
             cs.h264_paintover_burst_frames = int(p["h264_paintover_burst_frames"])
             cs.h264_fullcolor = int(bool(p["h264_fullcolor"]))
             cs.h264_streaming_mode = int(bool(p["h264_streaming_mode"]))
-            cs.h264_fullframe = int(enc == "x264enc")
+            cs.h264_fullframe = int(enc in ("x264enc", "x265enc", "svtav1enc"))
             cs.h264_aq_strength = max(0, min(64, int(self.settings.h264_aq_strength)))
             cs.h264_subpel = 0 if self.settings.h264_subpel[0] else -1
             cs.h264_intra4x4 = int(bool(self.settings.h264_intra4x4[0]))

@@ -105,8 +105,9 @@ def build_specs() -> list[Spec]:
         _b("command_enabled", True, "Enable parsing of command websocket messages."),
         Spec("file_transfers", "list", "upload,download", "Allowed file transfer directions.",
              allowed=["upload", "download"]),
-        Spec("encoder", "enum", "x264enc", "The default video encoder.",
-             allowed=["x264enc", "x264enc-striped", "jpeg"]),
+        Spec("encoder", "enum", "x264enc", "The default video encoder (x265enc: HEVC Main full-frame, "
+             "svtav1enc: AV1 Main full-frame; both MI355X-only extensions of the reference's list).",
+             allowed=["x264enc", "x264enc-striped", "jpeg", "x265enc", "svtav1enc"]),
         _r("framerate", "8-120", 60, "Allowed framerate range or a fixed value."),
         _r("h264_crf", "5-50", 25, "Allowed H.264 CRF range or a fixed value."),
         _r("h264_bitrate", "0-500000", 0, "H.264 bitrate in kbit/s: 0 = CRF (complexity-adaptive QP around "

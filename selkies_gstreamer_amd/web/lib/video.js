@@ -1,10 +1,43 @@
 // Stripe video renderer: one WebCodecs VideoDecoder per H.264 stripe (0x04)
 // and createImageBitmap for JPEG stripes (0x03), composited onto one canvas.
-// Full-frame H.264 arrives as a single stripe at y = 0.
+// Full-frame H.264 arrives as a single stripe at y = 0; so do the HEVC (x265enc,
+// Annex B with in-band parameter sets) and AV1 (svtav1enc, OBU temporal units) frames
+// of the MI355X encoders, which use the same 0x04 framing.
+
+// Level tables of the encoders (csrc/codec/hevc_params.cpp choose_level_idc,
+// csrc/codec/av1_cpu.cpp choose_level_idx): the codec string names the stream's level.
+const HEVC_LEVELS = [[30, 36864, 552960], [60, 122880, 3686400], [63, 245760, 7372800], [90, 552960, 16588800],
+  [93, 983040, 33177600], [120, 2228224, 66846720], [123, 2228224, 133693440], [150, 8912896, 267386880],
+  [153, 8912896, 534773760], [156, 8912896, 1069547520], [180, 35651584, 1069547520],
+  [183, 35651584, 2139095040], [186, 35651584, 4278190080]];
+const AV1_LEVELS = [[0, 147456, 4423680], [1, 278784, 8363520], [4, 665856, 19975680], [5, 1065024, 31950720],
+  [8, 2359296, 70778880], [9, 2359296, 141557760], [12, 8912896, 267386880], [13, 8912896, 534773760],
+  [14, 8912896, 1069547520], [16, 35651584, 1069547520], [17, 35651584, 2139095040],
+  [18, 35651584, 4278190080]];
+function pickLevel(table, w, h, fps, dflt) {
+  const ps = w * h, sr = ps * (fps > 0 ? fps : 60);
+  for (const [lv, mps, msr] of table) if (ps <= mps && sr <= msr) return lv;
+  return dflt;
+}
+// WebCodecs codec string of the negotiated encoder for a w x h stream at fps (coded
+// size: HEVC pads to 16, the level limits use it).
+export function codecString(encoder, w, h, fps = 60) {
+  if (encoder === 'x265enc') {
+    const pw = (w + 15) & ~15, ph = (h + 15) & ~15;
+    return `hev1.1.6.L${pickLevel(HEVC_LEVELS, pw, ph, fps, 186)}.B0`;
+  }
+  if (encoder === 'svtav1enc') {
+    const idx = pickLevel(AV1_LEVELS, w, h, fps, 31);
+    return `av01.0.${String(idx).padStart(2, '0')}M.08`;
+  }
+  return 'avc1.42E01E';
+}
 
 export class VideoRenderer {
   constructor(canvas, onError) {
     this.canvas = canvas;
+    this.encoder = 'x264enc';   // set from the negotiated settings (codecString)
+    this.fps = 60;
     this.ctx = canvas.getContext('2d', { alpha: false, desynchronized: true });
     this.decoders = new Map();   // y -> {decoder, width, height, keyed}
     this.onError = onError || ((e) => console.error(e));
@@ -31,7 +64,9 @@ export class VideoRenderer {
 
   _decoderFor(y, width, height) {
     let info = this.decoders.get(y);
-    if (info && info.decoder.state !== 'closed' && info.width === width && info.height === height) return info;
+    const codec = codecString(this.encoder, width, height, this.fps);
+    if (info && info.decoder.state !== 'closed' && info.width === width && info.height === height &&
+        info.codec === codec) return info;
     if (info) {
       try { info.decoder.close(); } catch (e) { /* ignore */ }
     }
@@ -39,8 +74,10 @@ export class VideoRenderer {
       output: (frame) => this._paint(frame, y),
       error: (e) => { this.decoders.delete(y); this.onError(e); },
     });
-    decoder.configure({ codec: 'avc1.42E01E', codedWidth: width, codedHeight: height, optimizeForLatency: true });
-    info = { decoder, width, height, keyed: false };
+    const cfg = { codec, codedWidth: width, codedHeight: height, optimizeForLatency: true };
+    if (codec.startsWith('hev1')) cfg.hevc = { format: 'annexb' };
+    decoder.configure(cfg);
+    info = { decoder, width, height, keyed: false, codec };
     this.decoders.set(y, info);
     return info;
   }

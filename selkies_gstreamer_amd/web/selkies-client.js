@@ -159,6 +159,10 @@ class Client {
   }
 
   syncUi() {
+    if (this.video) {   // the stream's codec follows the negotiated encoder (lib/video.js codecString)
+      this.video.encoder = this.settings.encoder;
+      this.video.fps = Number(this.settings.framerate) || 60;
+    }
     $('encoder').value = this.settings.encoder;
     $('framerate').value = this.settings.framerate;
     $('crf').value = this.settings.h264_crf;

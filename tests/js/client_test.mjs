@@ -468,3 +468,14 @@ import('../../selkies_gstreamer_amd/web/lib/i18n.js').then((i18n) => {
   assert.deepEqual(apps.loadInstalled(store), []);
   console.log('apps ok');
 });
+
+// ---- codec strings of the negotiated encoder (lib/video.js)
+import('../../selkies_gstreamer_amd/web/lib/video.js').then(({ codecString }) => {
+  assert.equal(codecString('x264enc', 1920, 1080, 60), 'avc1.42E01E');
+  assert.equal(codecString('x264enc-striped', 1920, 64, 60), 'avc1.42E01E');
+  assert.equal(codecString('x265enc', 1920, 1080, 60), 'hev1.1.6.L123.B0');   // 1920x1088 coded: level 4.1
+  assert.equal(codecString('x265enc', 3840, 2160, 60), 'hev1.1.6.L153.B0');   // level 5.1
+  assert.equal(codecString('svtav1enc', 3840, 2160, 120), 'av01.0.14M.08');   // level 5.2
+  assert.equal(codecString('svtav1enc', 1920, 1080, 60), 'av01.0.09M.08');    // level 4.1 (4.0 tops out at 30 fps)
+  console.log('codec strings ok');
+}).catch((e) => { console.error(e); process.exit(1); });

@@ -290,3 +290,41 @@ def test_files_listing_and_download(tmp_path):
                 assert r.status == 404
         await srv2.stop()
     run(main())
+
+
+@pytest.mark.parametrize("encoder", ["x265enc", "svtav1enc"])
+def test_session_hevc_and_av1(tmp_path, encoder):
+    """The MI355X encoder extensions over the data websocket: full-frame HEVC (Annex B,
+    in-band parameter sets) and AV1 (OBU temporal units) in the same 0x04 framing; the
+    stream decodes with the independent HEVC decoder / dav1d from its first key frame."""
+    async def main():
+        srv, port, _ = await _server(tmp_path)
+        W, H = 192, 128
+        frames = []
+        async with aiohttp.ClientSession() as sess:
+            async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket") as ws:
+                ss, _ = await _recv_until(ws, lambda m: isinstance(m, str) and "server_settings" in m)
+                assert encoder in json.loads(ss)["settings"]["encoder"]["allowed"]
+                await ws.send_str(_settings(W, H, encoder=encoder))
+                while len(frames) < 4:
+                    data, _ = await _recv_until(ws, lambda m: isinstance(m, bytes) and m[0] == 0x04)
+                    assert int.from_bytes(data[4:6], "big") == 0            # full frame: y = 0
+                    if frames or data[1] == 1:                             # from the first key frame
+                        frames.append(data)
+                    await ws.send_str(f"CLIENT_FRAME_ACK {int.from_bytes(data[2:4], 'big')}")
+        await srv.stop()
+        return frames
+
+    frames = run(main())
+    if encoder == "x265enc":
+        from selkies_gstreamer_amd.models.hevc.decoder import HevcDecoder
+        dec = HevcDecoder()
+        pics = [p for f in frames for p in dec.decode(f[10:])]
+        assert len(pics) == 4 and pics[0][0].shape == (128, 192) and pics[-1][0].std() > 1.0
+    else:
+        from selkies_gstreamer_amd.models.av1 import dav1d
+        if not dav1d.available():
+            pytest.skip("dav1d (libavif) not in this image")
+        d = dav1d.Decoder()
+        pics = [d.decode(f[10:]) for f in frames]
+        assert pics[0] is not None and pics[0][0].shape == (128, 192)

@@ -26,6 +26,7 @@ def test_client_unit_tests():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "client tests ok" in r.stdout
     assert "i18n ok" in r.stdout and "apps ok" in r.stdout
+    assert "webrtc client ok" in r.stdout and "codec strings ok" in r.stdout
 
 
 def test_index_references_existing_modules():
