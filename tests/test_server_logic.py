@@ -76,7 +76,7 @@ def test_server_settings_payload_shape():
     assert "port" not in st and "debug" not in st and "watermark_path" not in st
     assert st["framerate"] == {"value": [8, 120], "min": 8, "max": 120, "default": 60} or \
         st["framerate"] == {"value": (8, 120), "min": 8, "max": 120, "default": 60}
-    assert st["encoder"]["allowed"] == ["x264enc", "x264enc-striped", "jpeg"]
+    assert st["encoder"]["allowed"] == ["x264enc", "x264enc-striped", "jpeg", "x265enc", "svtav1enc"]
     assert st["audio_enabled"] == {"value": True, "locked": False}
     json.dumps(p)
 
