@@ -151,3 +151,43 @@ def test_session_host_two_hip_sessions():
             stop.set()
             await asyncio.wait_for(task, 30)
     asyncio.run(main())
+
+
+def test_hip_session_hevc_decodes(tmp_path):
+    """HEVC (x265enc) over the data websocket from the HIP encoder: the first frames from
+    the key frame decode with the independent HEVC decoder and match their source."""
+    from selkies_gstreamer_amd.models.hevc.decoder import HevcDecoder
+    W, H = 640, 368
+
+    async def main():
+        s = Settings(["--port", "0", "--audio-enabled", "false"], env={})
+        srv = DataStreamingServer(s, upload_dir=str(tmp_path / "up"), capture_source="motion")
+        port = await srv.start("127.0.0.1", 0)
+        pkts = []
+        try:
+            async with aiohttp.ClientSession() as sess:
+                async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket", max_msg_size=0) as ws:
+                    await _recv_until(ws, lambda m: isinstance(m, str) and "server_settings" in m)
+                    await ws.send_str("SETTINGS," + json.dumps({"initialClientWidth": W, "initialClientHeight": H,
+                                                                 "framerate": 60, "encoder": "x265enc"}))
+                    end = time.monotonic() + 40
+                    while len(pkts) < 3 and time.monotonic() < end:
+                        d = (await asyncio.wait_for(ws.receive(), 30)).data
+                        if not isinstance(d, bytes) or d[0] != 0x04 or (not pkts and d[1] != 1):
+                            continue
+                        pkts.append(d)
+                        await ws.send_str(f"CLIENT_FRAME_ACK {int.from_bytes(d[2:4], 'big')}")
+        finally:
+            await srv.stop()
+        return pkts
+
+    pkts = asyncio.run(asyncio.wait_for(main(), 120))
+    assert len(pkts) == 3
+    dec = HevcDecoder()
+    pics = [p for d in pkts for p in dec.decode(d[10:])]
+    assert len(pics) == 3
+    fid = int.from_bytes(pkts[-1][2:4], "big")
+    ref = np.empty((H, W, 4), np.uint8)
+    assert _native().sk_synthetic_render(W, H, 0, fid, ref.ctypes.data) == 0
+    q = psnr(pics[-1][0].astype(np.float64), bgrx_to_y709(ref))
+    assert q > 30.0, f"decoded frame {fid}: {q:.2f} dB against its source"
