@@ -4,6 +4,7 @@
 // and tile bytes) and the `use_cpu` path; dav1d decodes its output to exactly the
 // reconstruction kept here (tests/test_av1_encoder.py).
 #include "av1_encoder.h"
+#include "av1_lf.h"
 #include <string.h>
 #include <algorithm>
 
@@ -150,11 +151,24 @@ void write_frame_header(BitWriter& w, const Av1Geo& g, const FrameParams& fp) {
     w.put(0, 1);   // using_qmatrix
     w.put(0, 1);   // segmentation_enabled
     if (fp.qidx > 0) w.put(0, 1);   // delta_q_present
-    // loop_filter_params: levels 0 (off), sharpness 0, no deltas
-    w.put(0, 6);
-    w.put(0, 6);
-    w.put(0, 3);
-    w.put(0, 1);
+    // loop_filter_params (av1_lf.h): one level for luma V / H and both chroma planes,
+    // sharpness 0, no deltas
+    w.put((uint32_t)fp.lf_level, 6);
+    w.put((uint32_t)fp.lf_level, 6);
+    if (fp.lf_level) {
+        w.put((uint32_t)fp.lf_level, 6);
+        w.put((uint32_t)fp.lf_level, 6);
+    }
+    w.put(0, 3);   // loop_filter_sharpness
+    w.put(1, 1);   // loop_filter_delta_enabled
+    w.put(1, 1);   // loop_filter_delta_update
+    for (int i = 0; i < 8; i++) {   // ref deltas: INTRA_FRAME 1 -> 0, the rest keep their defaults
+        w.put(i == 0 ? 1 : 0, 1);
+        if (i == 0) w.put(0, 7);    // su(1+6) = 0
+    }
+    w.put(1, 1);                    // mode delta 0 (GLOBALMV / zero-motion class) = -63: level 0
+    w.put(128 - 63, 7);             // su(1+6) two's complement of -63
+    w.put(0, 1);                    // mode delta 1 keeps 0
     w.put(0, 1);   // tx_mode_select = 0 -> TX_MODE_LARGEST
     if (!fp.key) w.put(0, 1);   // reference_select
     w.put(1, 1);   // reduced_tx_set
@@ -517,6 +531,7 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
     fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     fp.key = key;
     fp.qidx = qidx_for_qp(fe.tasks[0].qp);
+    fp.lf_level = lf_level_for(ac_q(fp.qidx), key);
     std::fill(blk.begin(), blk.end(), BlkInfo{});
     if (key) {
         decide_key();
@@ -543,8 +558,18 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
     for (int s = 0; s < ns; s++)
         if (fe.tasks[s].final_action == ACT_NONE || fe.tasks[s].final_action == ACT_SKIPALL)
             fe.tasks[s].final_action = ACT_P;
-    // rows past the picture bottom repeat the last row (what AV1's reference clamp reads)
+    // in-loop deblocking (7.14) of the reconstruction: per plane all vertical edges, then
+    // all horizontal ones
     const h264::Geometry& g = fe.g;
+    LfFrame lf{blk.data(), geo.c8, geo.mi_rows, geo.mi_cols, geo.W, geo.H,
+               {fp.lf_level, fp.lf_level, fp.lf_level, fp.lf_level}};
+    if (fp.lf_level)
+        for (int p = 0; p < 3; p++)
+            for (int pass = 0; pass < 2; pass++)
+                for (int r = 0; r < geo.mi_rows; r += p ? 2 : 1)
+                    for (int c = 0; c < geo.mi_cols; c += p ? 2 : 1)
+                        lf_edge(lf, p, pass, r, c, fe.rec[p].data(), p ? g.stride_c : g.stride_y);
+    // rows past the picture bottom repeat the last row (what AV1's reference clamp reads)
     for (int y = geo.H; y < g.plane_h_y; y++)
         memcpy(&fe.rec[0][(size_t)y * g.stride_y], &fe.rec[0][(size_t)(geo.H - 1) * g.stride_y], g.stride_y);
     const int hc = (geo.H + 1) >> 1;

@@ -27,6 +27,7 @@ struct FrameParams {
     int key = 0;
     int qidx = 86;
     int tile_size_bytes = 4;
+    int lf_level = 0;     // loop_filter_level[0..3] (one level, av1_lf.h lf_level_for)
 };
 
 // MSB-first bit writer for headers.

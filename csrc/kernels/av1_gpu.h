@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include "h264_gpu.h"
 #include "../codec/av1_core.h"
+#include "../codec/av1_lf.h"
 
 namespace sk {
 namespace av1 {

@@ -14,6 +14,7 @@
 //                      per-symbol interval words
 //   k_av1_ec           one wave per tile: the arithmetic coder (scalar state)
 //   k_av1_pack         carry resolution (segmented, parallel), tile bytes -> host-mapped output
+//   k_av1_lf           in-loop deblocking (codec/av1_lf.h), one launch per plane and pass
 //   k_av1_finish       padding rows of the reconstruction, slice actions for k_commit
 // Transforms: forward DCT as LDS matrix products (lanes = output coefficients),
 // inverse as the normative butterflies, lane = row / column of a transform block.
@@ -277,10 +278,13 @@ __global__ __launch_bounds__(256) void k_av1_setup(Av1Args A) {
         }
     if (threadIdx.x == 0) {
         const int qidx = A.qidx_of_qp[sk_clip(f.tasks[0].qp, 0, 51)];
+        const int lvl = lf_level_for(ac_q(qidx), key);   // av1_lf.h, the host encoder's choice
         A.frame[0] = key;
         A.frame[1] = qidx;
+        A.frame[2] = lvl;
         A.frame_host[0] = key;
         A.frame_host[1] = qidx;
+        A.frame_host[2] = lvl;
     }
 }
 
@@ -939,6 +943,23 @@ __global__ __launch_bounds__(256) void k_av1_pack(Av1Args A) {
 // Rows below the picture repeat its last row (the reference clamp AV1's MC reads),
 // and every slice's reconstruction becomes the reference (k_commit copies rec -> ref
 // for every slice that is not ACT_NONE; vectors of re-coded static slices are zero).
+// In-loop deblocking (av1_lf.h lf_edge), one launch per (plane, pass): one thread per
+// MI edge position (4 lines), every edge of a pass independent of the others.
+__global__ __launch_bounds__(256) void k_av1_lf(Av1Args A, int plane, int pass) {
+    const int lvl = A.frame[2];
+    if (lvl == 0) return;
+    const Av1Geo& g = A.geo;
+    const int ss = plane ? 1 : 0;
+    const int cols = (g.mi_cols + ss) >> ss, rows = (g.mi_rows + ss) >> ss;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= cols * rows) return;
+    const int r = (t / cols) << ss, c = (t % cols) << ss;
+    const LfFrame lf{A.blk, g.c8, g.mi_rows, g.mi_cols, g.W, g.H, {lvl, lvl, lvl, lvl}};
+    const FrameArgs& f = A.f;
+    uint8_t* buf = plane == 0 ? f.rec.y : (plane == 1 ? f.rec.u : f.rec.v);
+    lf_edge(lf, plane, pass, r, c, buf, plane ? f.stride_c : f.stride_y);
+}
+
 __global__ __launch_bounds__(256) void k_av1_finish(Av1Args A) {
     const FrameArgs& f = A.f;
     const int x = blockIdx.x * 256 + threadIdx.x;
@@ -975,6 +996,11 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_av1_cdf, dim3(tiles * kEcParts), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, s, a);
+    for (int p = 0; p < 3; p++) {   // in-loop deblocking of the reconstruction, plane by plane
+        const int ss = p ? 1 : 0;
+        const int cnt = ((a.geo.mi_cols + ss) >> ss) * ((a.geo.mi_rows + ss) >> ss);
+        for (int pass = 0; pass < 2; pass++) hipLaunchKernelGGL(k_av1_lf, dim3((cnt + 255) / 256), dim3(256), 0, s, a, p, pass);
+    }
     hipLaunchKernelGGL(k_av1_finish, dim3((a.f.stride_y + 255) / 256), dim3(256), 0, s, a);
 }
 

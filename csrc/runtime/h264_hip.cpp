@@ -790,6 +790,7 @@ class HipBackend : public EncoderBackend {
         av1::FrameParams fp;
         fp.key = av1_frame_[par][0];
         fp.qidx = av1_frame_[par][1];
+        fp.lf_level = av1_frame_[par][2];
         std::vector<std::vector<uint8_t>> tl(tiles);
         size_t off = 0;
         for (int t = 0; t < tiles; t++) {
