@@ -5,6 +5,7 @@
 // reconstruction kept here (tests/test_av1_encoder.py).
 #include "av1_encoder.h"
 #include "av1_lf.h"
+#include "av1_cdef.h"
 #include <string.h>
 #include <algorithm>
 
@@ -90,7 +91,7 @@ void write_sequence_header(BitWriter& w, int W, int H, int level_idx, int full_r
     w.put(0, 1);   // seq_choose_screen_content_tools
     w.put(0, 1);   // seq_force_screen_content_tools (-> seq_force_integer_mv = SELECT, not coded)
     w.put(0, 1);   // enable_superres
-    w.put(0, 1);   // enable_cdef
+    w.put(1, 1);   // enable_cdef (av1_cdef.h)
     w.put(0, 1);   // enable_restoration
     // color_config
     w.put(0, 1);   // high_bitdepth
@@ -169,6 +170,14 @@ void write_frame_header(BitWriter& w, const Av1Geo& g, const FrameParams& fp) {
     w.put(1, 1);                    // mode delta 0 (GLOBALMV / zero-motion class) = -63: level 0
     w.put(128 - 63, 7);             // su(1+6) two's complement of -63
     w.put(0, 1);                    // mode delta 1 keeps 0
+    // cdef_params (av1_cdef.h): one strength set, cdef_bits = 0
+    const CdefParams cp = cdef_choose(fp.qidx, ac_q(fp.qidx));
+    w.put((uint32_t)(cp.damping - 3), 2);
+    w.put(0, 2);
+    w.put((uint32_t)cp.y_pri, 4);
+    w.put((uint32_t)(cp.y_sec == 4 ? 3 : cp.y_sec), 2);
+    w.put((uint32_t)cp.uv_pri, 4);
+    w.put((uint32_t)(cp.uv_sec == 4 ? 3 : cp.uv_sec), 2);
     w.put(0, 1);   // tx_mode_select = 0 -> TX_MODE_LARGEST
     if (!fp.key) w.put(0, 1);   // reference_select
     w.put(1, 1);   // reduced_tx_set
@@ -569,6 +578,22 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
                 for (int r = 0; r < geo.mi_rows; r += p ? 2 : 1)
                     for (int c = 0; c < geo.mi_cols; c += p ? 2 : 1)
                         lf_edge(lf, p, pass, r, c, fe.rec[p].data(), p ? g.stride_c : g.stride_y);
+    // CDEF (7.15) on the deblocked picture
+    const CdefParams cp = cdef_choose(fp.qidx, ac_q(fp.qidx));
+    if (cdef_on(cp)) {
+        std::vector<uint8_t> in[3] = {fe.rec[0], fe.rec[1], fe.rec[2]};
+        const uint8_t* ip[3] = {in[0].data(), in[1].data(), in[2].data()};
+        uint8_t* op[3] = {fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data()};
+        const int st[3] = {g.stride_y, g.stride_c, g.stride_c};
+        for (int sr = 0; sr < geo.mi_rows; sr += 16)
+            for (int sc = 0; sc < geo.mi_cols; sc += 16) {
+                if (!cdef_sb_on(blk.data(), geo, sr, sc)) continue;   // cdef_idx -1: every block skipped
+                for (int r = sr; r < sr + 16 && r < geo.mi_rows; r += 2)
+                    for (int c = sc; c < sc + 16 && c < geo.mi_cols; c += 2)
+                        cdef_block(ip, st, op, st, cp, r, c, blk_skip(blk[(size_t)(r >> 1) * geo.c8 + (c >> 1)]),
+                                   geo.mi_rows, geo.mi_cols);
+            }
+    }
     // rows past the picture bottom repeat the last row (what AV1's reference clamp reads)
     for (int y = geo.H; y < g.plane_h_y; y++)
         memcpy(&fe.rec[0][(size_t)y * g.stride_y], &fe.rec[0][(size_t)(geo.H - 1) * g.stride_y], g.stride_y);

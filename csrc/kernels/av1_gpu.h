@@ -6,6 +6,7 @@
 #include "h264_gpu.h"
 #include "../codec/av1_core.h"
 #include "../codec/av1_lf.h"
+#include "../codec/av1_cdef.h"
 
 namespace sk {
 namespace av1 {
@@ -30,7 +31,8 @@ struct Av1Args {
     int* tok_off;             // [units] offset of the unit's tokens in its tile's stream
     int* tile_ntok;           // [tiles]
     int* frame;               // device: [0] key, [1] qidx
-    int* frame_host;          // host-mapped copy of frame[0..1]
+    int* frame_host;          // host-mapped copy of frame[0..2]
+    h264::gpu::Planes cdef_in;   // the deblocked picture CDEF reads (k_av1_cdef writes f.rec)
     const uint8_t* qidx_of_qp;   // [52]
     uint16_t* chunks;         // [tiles][tile_cap] settled coder chunks
     int tile_cap;             // chunk capacity per tile

@@ -15,6 +15,7 @@
 //   k_av1_ec           one wave per tile: the arithmetic coder (scalar state)
 //   k_av1_pack         carry resolution (segmented, parallel), tile bytes -> host-mapped output
 //   k_av1_lf           in-loop deblocking (codec/av1_lf.h), one launch per plane and pass
+//   k_av1_cdef         CDEF (codec/av1_cdef.h) from a copy of the deblocked picture
 //   k_av1_finish       padding rows of the reconstruction, slice actions for k_commit
 // Transforms: forward DCT as LDS matrix products (lanes = output coefficients),
 // inverse as the normative butterflies, lane = row / column of a transform block.
@@ -960,6 +961,23 @@ __global__ __launch_bounds__(256) void k_av1_lf(Av1Args A, int plane, int pass) 
     lf_edge(lf, plane, pass, r, c, buf, plane ? f.stride_c : f.stride_y);
 }
 
+// CDEF (av1_cdef.h cdef_block): one thread per 8x8 block (direction search, luma and
+// both chroma 4x4 filters), reading the deblocked copy in cdef_in, writing f.rec.
+__global__ __launch_bounds__(256) void k_av1_cdef(Av1Args A) {
+    const Av1Geo& g = A.geo;
+    const int cols = g.mi_cols >> 1, rows = g.mi_rows >> 1;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= cols * rows) return;
+    const int r = (t / cols) * 2, c = (t % cols) * 2;
+    const CdefParams p = cdef_choose(A.frame[1], ac_q(A.frame[1]));
+    if (!cdef_on(p) || !cdef_sb_on(A.blk, g, r & ~15, c & ~15)) return;
+    const FrameArgs& f = A.f;
+    const uint8_t* ip[3] = {A.cdef_in.y, A.cdef_in.u, A.cdef_in.v};
+    uint8_t* op[3] = {f.rec.y, f.rec.u, f.rec.v};
+    const int st[3] = {f.stride_y, f.stride_c, f.stride_c};
+    cdef_block(ip, st, op, st, p, r, c, blk_skip(A.blk[(size_t)(r >> 1) * g.c8 + (c >> 1)]), g.mi_rows, g.mi_cols);
+}
+
 __global__ __launch_bounds__(256) void k_av1_finish(Av1Args A) {
     const FrameArgs& f = A.f;
     const int x = blockIdx.x * 256 + threadIdx.x;
@@ -1001,6 +1019,13 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
         const int cnt = ((a.geo.mi_cols + ss) >> ss) * ((a.geo.mi_rows + ss) >> ss);
         for (int pass = 0; pass < 2; pass++) hipLaunchKernelGGL(k_av1_lf, dim3((cnt + 255) / 256), dim3(256), 0, s, a, p, pass);
     }
+    // CDEF reads the deblocked picture: a copy, then the filter writes the reconstruction
+    const size_t ny = (size_t)a.f.stride_y * a.f.mb_h * 16, nc = (size_t)a.f.stride_c * a.f.mb_h * 8;
+    (void)hipMemcpyAsync(a.cdef_in.y, a.f.rec.y, ny, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(a.cdef_in.u, a.f.rec.u, nc, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(a.cdef_in.v, a.f.rec.v, nc, hipMemcpyDeviceToDevice, s);
+    const int nb8 = (a.geo.mi_cols >> 1) * (a.geo.mi_rows >> 1);
+    hipLaunchKernelGGL(k_av1_cdef, dim3((nb8 + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_finish, dim3((a.f.stride_y + 255) / 256), dim3(256), 0, s, a);
 }
 

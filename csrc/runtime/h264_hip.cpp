@@ -750,6 +750,9 @@ class HipBackend : public EncoderBackend {
         a.tok = dmalloc<uint32_t>((size_t)n * av1::gpu::kTokCap, false);
         a.tok_n = dmalloc<int>(n);
         a.frame = dmalloc<int>(4);
+        a.cdef_in.y = dmalloc<uint8_t>((size_t)g_.stride_y * g_.mb_h * 16, false);
+        a.cdef_in.u = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
+        a.cdef_in.v = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
         const int tiles = av1_geo_.tile_cols * av1_geo_.tile_rows;
         // coder chunks: 4 KB per unit of the largest tile (incompressible content codes
         // below ~1.5 bytes per sample)
