@@ -24,33 +24,54 @@ SK_HD int lf_level_for(int ac_q, bool key) {
 
 SK_HD int lf_clamp8(int v) { return sk_clip(v, -128, 127); }
 
+// Wide filter (7.14.6.4) over the samples read: N taps a side (6 for the 14-tap luma
+// filter, 3 for 8-tap luma, 2 for 6-tap chroma), centre weight 2 for |j| <= N2.
+template <int N, int N2, int LOG2>
+SK_HD void lf_wide(const int* P, const int* Q, uint8_t* q0p, int step) {
+    int out[2 * N];
+#pragma unroll
+    for (int i = -N; i < N; i++) {
+        int t = 0;
+#pragma unroll
+        for (int j = -N; j <= N; j++) {
+            const int p = sk_clip(i + j, -(N + 1), N);
+            t += (p >= 0 ? Q[p] : P[-p - 1]) * (sk_abs(j) <= N2 ? 2 : 1);
+        }
+        out[i + N] = (t + (1 << (LOG2 - 1))) >> LOG2;
+    }
+#pragma unroll
+    for (int i = -N; i < N; i++) q0p[i * step] = (uint8_t)out[i + N];
+}
+
 // One line across an edge: q0 at `q0p`, p_i = q0p[-(i + 1) * step], q_i = q0p[i * step]
-// (7.14.6: filter mask, narrow / wide filter).
-SK_HD void lf_line(uint8_t* q0p, int step, int filter_size, int plane, int lvl) {
-    const int len = filter_size == 4 ? 4 : (plane ? 6 : (filter_size == 8 ? 8 : 16));
-    const int rd = len == 4 ? 2 : (len == 6 ? 3 : (len == 8 ? 4 : 7));   // samples read per side
-    int P[7] = {0, 0, 0, 0, 0, 0, 0}, Q[7] = {0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < rd; i++) {
-        P[i] = q0p[-(i + 1) * step];
-        Q[i] = q0p[i * step];
+// (7.14.6: filter mask, narrow / wide filter). LEN = filterLen (4, 6 chroma, 8, 16); the
+// template keeps every sample in registers (compile-time indices) on the GPU.
+template <int LEN>
+SK_HD void lf_line_t(uint8_t* q0p, int step, int lvl) {
+    constexpr int RD = LEN == 4 ? 2 : (LEN == 6 ? 3 : (LEN == 8 ? 4 : 7));   // samples read per side
+    int P[7], Q[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        P[i] = i < RD ? q0p[-(i + 1) * step] : 0;
+        Q[i] = i < RD ? q0p[i * step] : 0;
     }
     const int limit = lvl > 1 ? lvl : 1;   // sharpness 0
     const int blimit = 2 * (lvl + 2) + limit, thresh = lvl >> 4;
     const bool hev = sk_abs(P[1] - P[0]) > thresh || sk_abs(Q[1] - Q[0]) > thresh;
     bool mask = sk_abs(P[1] - P[0]) <= limit && sk_abs(Q[1] - Q[0]) <= limit &&
                 sk_abs(P[0] - Q[0]) * 2 + (sk_abs(P[1] - Q[1]) >> 1) <= blimit;
-    if (len >= 6) mask = mask && sk_abs(P[2] - P[1]) <= limit && sk_abs(Q[2] - Q[1]) <= limit;
-    if (len >= 8) mask = mask && sk_abs(P[3] - P[2]) <= limit && sk_abs(Q[3] - Q[2]) <= limit;
+    if (LEN >= 6) mask = mask && sk_abs(P[2] - P[1]) <= limit && sk_abs(Q[2] - Q[1]) <= limit;
+    if (LEN >= 8) mask = mask && sk_abs(P[3] - P[2]) <= limit && sk_abs(Q[3] - Q[2]) <= limit;
     if (!mask) return;
     bool flat = false, flat2 = false;
-    if (len >= 6) {
+    if (LEN >= 6) {
         flat = sk_abs(P[1] - P[0]) <= 1 && sk_abs(Q[1] - Q[0]) <= 1 && sk_abs(P[2] - P[0]) <= 1 && sk_abs(Q[2] - Q[0]) <= 1;
-        if (len >= 8) flat = flat && sk_abs(P[3] - P[0]) <= 1 && sk_abs(Q[3] - Q[0]) <= 1;
+        if (LEN >= 8) flat = flat && sk_abs(P[3] - P[0]) <= 1 && sk_abs(Q[3] - Q[0]) <= 1;
     }
-    if (len == 16)
+    if (LEN == 16)
         flat2 = sk_abs(P[6] - P[0]) <= 1 && sk_abs(Q[6] - Q[0]) <= 1 && sk_abs(P[5] - P[0]) <= 1 &&
                 sk_abs(Q[5] - Q[0]) <= 1 && sk_abs(P[4] - P[0]) <= 1 && sk_abs(Q[4] - Q[0]) <= 1;
-    if (len == 4 || !flat) {   // narrow filter (7.14.6.3)
+    if (LEN == 4 || !flat) {   // narrow filter (7.14.6.3)
         const int ps1 = P[1] - 128, ps0 = P[0] - 128, qs0 = Q[0] - 128, qs1 = Q[1] - 128;
         int f = hev ? lf_clamp8(ps1 - qs1) : 0;
         f = lf_clamp8(f + 3 * (qs0 - ps0));
@@ -64,21 +85,15 @@ SK_HD void lf_line(uint8_t* q0p, int step, int filter_size, int plane, int lvl) 
         }
         return;
     }
-    // wide filter (7.14.6.4): log2Size 3 (6-tap chroma, 8-tap luma) or 4 (14-tap luma)
-    const int log2 = (len == 16 && flat2) ? 4 : 3;
-    const int n = log2 == 4 ? 6 : (plane == 0 ? 3 : 2);
-    const int n2 = (log2 == 3 && plane == 0) ? 0 : 1;
-    auto smp = [&](int k) { return k >= 0 ? Q[k] : P[-k - 1]; };
-    int out[12];
-    for (int i = -n; i < n; i++) {
-        int t = 0;
-        for (int j = -n; j <= n; j++) {
-            const int p = sk_clip(i + j, -(n + 1), n);
-            t += smp(p) * (sk_abs(j) <= n2 ? 2 : 1);
-        }
-        out[i + n] = (t + (1 << (log2 - 1))) >> log2;
-    }
-    for (int i = -n; i < n; i++) q0p[i * step] = (uint8_t)out[i + n];
+    if (LEN == 6) lf_wide<2, 1, 3>(P, Q, q0p, step);              // 6-tap chroma
+    else if (LEN == 8 || !flat2) lf_wide<3, 0, 3>(P, Q, q0p, step);   // 8-tap luma
+    else lf_wide<6, 1, 4>(P, Q, q0p, step);                        // 14-tap luma
+}
+SK_HD void lf_line(uint8_t* q0p, int step, int filter_size, int plane, int lvl) {
+    if (filter_size == 4) lf_line_t<4>(q0p, step, lvl);
+    else if (plane) lf_line_t<6>(q0p, step, lvl);
+    else if (filter_size == 8) lf_line_t<8>(q0p, step, lvl);
+    else lf_line_t<16>(q0p, step, lvl);
 }
 
 // Filter geometry of the frame: the 8x8 block map (bsl = Mi_Width_Log2 of the block
