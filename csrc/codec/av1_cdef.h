@@ -38,24 +38,23 @@ SK_HD int floor_log2(int v) {
     return n;
 }
 
-// Direction search of the luma 8x8 block at `src` (7.15.2): returns yDir, writes var.
-SK_HD int cdef_find_dir(const uint8_t* src, int stride, int* var) {
+// Direction search (7.15.2) in two steps: the line sums `partial` of the 8x8 luma block
+// (cdef_partial_index: where pixel (i, j) adds in line set d; order-independent, so the GPU
+// accumulates them lane-parallel), then the costs and the best direction.
+SK_HD int cdef_partial_index(int d, int i, int j) {
+    switch (d) {
+        case 0: return i + j;
+        case 1: return i + j / 2;
+        case 2: return i;
+        case 3: return 3 + i - j / 2;
+        case 4: return 7 + i - j;
+        case 5: return 3 - i / 2 + j;
+        case 6: return j;
+        default: return i / 2 + j;
+    }
+}
+SK_HD int cdef_dir_from_partials(const int (*partial)[15], int* var) {
     const int div_table[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
-    int partial[8][15];
-    for (int i = 0; i < 8; i++)
-        for (int j = 0; j < 15; j++) partial[i][j] = 0;
-    for (int i = 0; i < 8; i++)
-        for (int j = 0; j < 8; j++) {
-            const int x = (int)src[(size_t)i * stride + j] - 128;
-            partial[0][i + j] += x;
-            partial[1][i + j / 2] += x;
-            partial[2][i] += x;
-            partial[3][3 + i - j / 2] += x;
-            partial[4][7 + i - j] += x;
-            partial[5][3 - i / 2 + j] += x;
-            partial[6][j] += x;
-            partial[7][i / 2 + j] += x;
-        }
     long long cost[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 8; i++) {
         cost[2] += (long long)partial[2][i] * partial[2][i];
@@ -85,6 +84,18 @@ SK_HD int cdef_find_dir(const uint8_t* src, int stride, int* var) {
     *var = (int)((best - cost[(dir + 4) & 7]) >> 10);
     return dir;
 }
+// Direction of the luma 8x8 block at `src`: returns yDir, writes var.
+SK_HD int cdef_find_dir(const uint8_t* src, int stride, int* var) {
+    int partial[8][15];
+    for (int d = 0; d < 8; d++)
+        for (int k = 0; k < 15; k++) partial[d][k] = 0;
+    for (int i = 0; i < 8; i++)
+        for (int j = 0; j < 8; j++) {
+            const int x = (int)src[(size_t)i * stride + j] - 128;
+            for (int d = 0; d < 8; d++) partial[d][cdef_partial_index(d, i, j)] += x;
+        }
+    return cdef_dir_from_partials(partial, var);
+}
 
 SK_HD int cdef_constrain(int diff, int threshold, int damping) {
     if (!threshold) return 0;
@@ -101,14 +112,14 @@ SK_HD int cdef_dir_off(int dir, int k, int rc) {
     return t[dir][k][rc];
 }
 
-// cdef_filter (7.15.3) of one 8x8 (luma) / 4x4 (chroma) block at plane position (x0, y0):
-// reads `in` (the deblocked plane), writes `out`. mi_rows / mi_cols bound availability.
-SK_HD void cdef_filter_block(const uint8_t* in, int in_stride, uint8_t* out, int out_stride, int ss, int x0, int y0,
-                             int pri, int sec, int damping, int dir, int mi_rows, int mi_cols) {
-    const int n = 8 >> ss;
+// cdef_filter (7.15.3) of sample (i, j) of the 8x8 (luma) / 4x4 (chroma) block at plane
+// position (x0, y0): reads `in` (the deblocked plane), returns the output sample.
+// mi_rows / mi_cols bound availability.
+SK_HD int cdef_filter_px(const uint8_t* in, int in_stride, int ss, int x0, int y0, int i, int j, int pri, int sec,
+                         int damping, int dir, int mi_rows, int mi_cols) {
     const int pt0 = (pri & 1) ? 3 : 4, pt1 = (pri & 1) ? 3 : 2;   // Cdef_Pri_Taps[(priStr >> 0) & 1]
-    for (int i = 0; i < n; i++)
-        for (int j = 0; j < n; j++) {
+    {
+        {
             const int x = in[(size_t)(y0 + i) * in_stride + x0 + j];
             int sum = 0, mx = x, mn = x;
             auto tap = [&](int d, int k, int sign, int* v) {
@@ -135,8 +146,24 @@ SK_HD void cdef_filter_block(const uint8_t* in, int in_stride, uint8_t* out, int
                         }
                     }
                 }
-            out[(size_t)(y0 + i) * out_stride + x0 + j] = (uint8_t)sk_clip(x + ((8 + sum - (sum < 0)) >> 4), mn, mx);
+            return sk_clip(x + ((8 + sum - (sum < 0)) >> 4), mn, mx);
         }
+    }
+}
+SK_HD void cdef_filter_block(const uint8_t* in, int in_stride, uint8_t* out, int out_stride, int ss, int x0, int y0,
+                             int pri, int sec, int damping, int dir, int mi_rows, int mi_cols) {
+    const int n = 8 >> ss;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++)
+            out[(size_t)(y0 + i) * out_stride + x0 + j] =
+                (uint8_t)cdef_filter_px(in, in_stride, ss, x0, y0, i, j, pri, sec, damping, dir, mi_rows, mi_cols);
+}
+// Luma strength and direction of the block from the search (7.15.1): the primary
+// strength is scaled by the block's variance; dir is 0 when the frame's strength is 0.
+SK_HD void cdef_luma_setup(const CdefParams& p, int ydir, int var, int* pri, int* dir) {
+    *dir = p.y_pri == 0 ? 0 : ydir;
+    const int vs = (var >> 6) ? sk_min(floor_log2(var >> 6), 12) : 0;
+    *pri = var ? (p.y_pri * (4 + vs) + 8) >> 4 : 0;
 }
 
 // Whether the 64x64 superblock at MI (sr, sc) has a block that is not skipped (read_cdef
@@ -155,10 +182,8 @@ SK_HD void cdef_block(const uint8_t* const* in, const int* in_stride, uint8_t* c
     if (all_skip) return;
     int var = 0;
     const int ydir = cdef_find_dir(in[0] + (size_t)(r * 4) * in_stride[0] + c * 4, in_stride[0], &var);
-    int pri = p.y_pri;
-    const int dir = pri == 0 ? 0 : ydir;
-    const int vs = (var >> 6) ? sk_min(floor_log2(var >> 6), 12) : 0;
-    pri = var ? (pri * (4 + vs) + 8) >> 4 : 0;
+    int pri, dir;
+    cdef_luma_setup(p, ydir, var, &pri, &dir);
     cdef_filter_block(in[0], in_stride[0], out[0], out_stride[0], 0, c * 4, r * 4, pri, p.y_sec, p.damping, dir,
                       mi_rows, mi_cols);
     const int udir = p.uv_pri == 0 ? 0 : ydir;   // Cdef_Uv_Dir for 4:2:0 is the identity

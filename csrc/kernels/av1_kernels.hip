@@ -15,7 +15,7 @@
 //   k_av1_ec           one wave per tile: the arithmetic coder (scalar state)
 //   k_av1_pack         carry resolution (segmented, parallel), tile bytes -> host-mapped output
 //   k_av1_lf           in-loop deblocking (codec/av1_lf.h), one launch per plane and pass
-//   k_av1_cdef         CDEF (codec/av1_cdef.h) from a copy of the deblocked picture
+//   k_av1_cdef         CDEF (codec/av1_cdef.h), one wave per 8x8, from a copy of the deblocked picture
 //   k_av1_finish       padding rows of the reconstruction, slice actions for k_commit
 // Transforms: forward DCT as LDS matrix products (lanes = output coefficients),
 // inverse as the normative butterflies, lane = row / column of a transform block.
@@ -961,21 +961,51 @@ __global__ __launch_bounds__(256) void k_av1_lf(Av1Args A, int plane, int pass) 
     lf_edge(lf, plane, pass, r, c, buf, plane ? f.stride_c : f.stride_y);
 }
 
-// CDEF (av1_cdef.h cdef_block): one thread per 8x8 block (direction search, luma and
-// both chroma 4x4 filters), reading the deblocked copy in cdef_in, writing f.rec.
+// CDEF (av1_cdef.h): one wave per 8x8 block, lane = luma pixel. The direction's line
+// sums are accumulated with LDS atomics (integer, order-independent), lane 0 turns them
+// into the direction, then every lane filters its luma pixel and lanes 0..31 the 4x4 Cb /
+// Cr pixels, reading the deblocked copy in cdef_in and writing f.rec.
 __global__ __launch_bounds__(256) void k_av1_cdef(Av1Args A) {
+    __shared__ int part[4][8][15];
+    __shared__ int dirvar[4][2];
     const Av1Geo& g = A.geo;
+    const int w = threadIdx.x >> 6, l = lane();
     const int cols = g.mi_cols >> 1, rows = g.mi_rows >> 1;
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= cols * rows) return;
-    const int r = (t / cols) * 2, c = (t % cols) * 2;
+    const int b = blockIdx.x * 4 + w;
+    if (b >= cols * rows) return;   // wave-uniform; no block barriers below
+    const int r = (b / cols) * 2, c = (b % cols) * 2;
     const CdefParams p = cdef_choose(A.frame[1], ac_q(A.frame[1]));
-    if (!cdef_on(p) || !cdef_sb_on(A.blk, g, r & ~15, c & ~15)) return;
+    if (!cdef_on(p) || !cdef_sb_on(A.blk, g, r & ~15, c & ~15) || blk_skip(A.blk[(size_t)(r >> 1) * g.c8 + (c >> 1)]))
+        return;
     const FrameArgs& f = A.f;
-    const uint8_t* ip[3] = {A.cdef_in.y, A.cdef_in.u, A.cdef_in.v};
-    uint8_t* op[3] = {f.rec.y, f.rec.u, f.rec.v};
-    const int st[3] = {f.stride_y, f.stride_c, f.stride_c};
-    cdef_block(ip, st, op, st, p, r, c, blk_skip(A.blk[(size_t)(r >> 1) * g.c8 + (c >> 1)]), g.mi_rows, g.mi_cols);
+    int* pw = &part[w][0][0];
+    for (int k = l; k < 8 * 15; k += 64) pw[k] = 0;
+    wsync();
+    const int i = l >> 3, j = l & 7;
+    const int x = (int)A.cdef_in.y[(size_t)(r * 4 + i) * f.stride_y + c * 4 + j] - 128;
+#pragma unroll
+    for (int d = 0; d < 8; d++) atomicAdd(&part[w][d][cdef_partial_index(d, i, j)], x);
+    wsync();
+    if (l == 0) {
+        int var = 0;
+        dirvar[w][0] = cdef_dir_from_partials(part[w], &var);
+        dirvar[w][1] = var;
+    }
+    wsync();
+    const int ydir = dirvar[w][0], var = dirvar[w][1];
+    int pri, dir;
+    cdef_luma_setup(p, ydir, var, &pri, &dir);
+    const int out = cdef_filter_px(A.cdef_in.y, f.stride_y, 0, c * 4, r * 4, i, j, pri, p.y_sec, p.damping, dir,
+                                   g.mi_rows, g.mi_cols);
+    f.rec.y[(size_t)(r * 4 + i) * f.stride_y + c * 4 + j] = (uint8_t)out;
+    if (l < 32) {   // Cb (lanes 0..15) / Cr (16..31): 4x4 pixel l & 15
+        const int pl = l >> 4, ci = (l & 15) >> 2, cj = l & 3;
+        const uint8_t* in = pl ? A.cdef_in.v : A.cdef_in.u;
+        uint8_t* o = pl ? f.rec.v : f.rec.u;
+        const int udir = p.uv_pri == 0 ? 0 : ydir;   // Cdef_Uv_Dir is the identity for 4:2:0
+        o[(size_t)(r * 2 + ci) * f.stride_c + c * 2 + cj] = (uint8_t)cdef_filter_px(
+            in, f.stride_c, 1, c * 2, r * 2, ci, cj, p.uv_pri, p.uv_sec, p.damping - 1, udir, g.mi_rows, g.mi_cols);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_av1_finish(Av1Args A) {
@@ -1025,7 +1055,7 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
     (void)hipMemcpyAsync(a.cdef_in.u, a.f.rec.u, nc, hipMemcpyDeviceToDevice, s);
     (void)hipMemcpyAsync(a.cdef_in.v, a.f.rec.v, nc, hipMemcpyDeviceToDevice, s);
     const int nb8 = (a.geo.mi_cols >> 1) * (a.geo.mi_rows >> 1);
-    hipLaunchKernelGGL(k_av1_cdef, dim3((nb8 + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_cdef, dim3((nb8 + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_finish, dim3((a.f.stride_y + 255) / 256), dim3(256), 0, s, a);
 }
 
