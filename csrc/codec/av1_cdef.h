@@ -53,8 +53,14 @@ SK_HD int cdef_partial_index(int d, int i, int j) {
         default: return i / 2 + j;
     }
 }
+// Div_Table and Cdef_Directions[dir][k] = (row, col) offsets of the k-th primary tap, in
+// constant memory on the GPU (a function-local table would live in scratch).
+SK_TABLE int32_t CDEF_DIV[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
+SK_TABLE int8_t CDEF_DIRS[8][2][2] = {{{-1, 1}, {-2, 2}}, {{0, 1}, {-1, 2}}, {{0, 1}, {0, 2}}, {{0, 1}, {1, 2}},
+                                      {{1, 1}, {2, 2}},   {{1, 0}, {2, 1}},  {{1, 0}, {2, 0}}, {{1, 0}, {2, -1}}};
+
 SK_HD int cdef_dir_from_partials(const int (*partial)[15], int* var) {
-    const int div_table[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
+    const int32_t* div_table = CDEF_DIV;
     long long cost[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 8; i++) {
         cost[2] += (long long)partial[2][i] * partial[2][i];
@@ -105,12 +111,7 @@ SK_HD int cdef_constrain(int diff, int threshold, int damping) {
     return diff < 0 ? -v : v;
 }
 
-// Cdef_Directions[dir][k] = (row, col) offsets of the k-th primary tap.
-SK_HD int cdef_dir_off(int dir, int k, int rc) {
-    constexpr int8_t t[8][2][2] = {{{-1, 1}, {-2, 2}}, {{0, 1}, {-1, 2}}, {{0, 1}, {0, 2}}, {{0, 1}, {1, 2}},
-                                   {{1, 1}, {2, 2}},   {{1, 0}, {2, 1}},  {{1, 0}, {2, 0}}, {{1, 0}, {2, -1}}};
-    return t[dir][k][rc];
-}
+SK_HD int cdef_dir_off(int dir, int k, int rc) { return CDEF_DIRS[dir][k][rc]; }
 
 // cdef_filter (7.15.3) of sample (i, j) of the 8x8 (luma) / 4x4 (chroma) block at plane
 // position (x0, y0): reads `in` (the deblocked plane), returns the output sample.
