@@ -59,36 +59,40 @@ SK_TABLE int32_t CDEF_DIV[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
 SK_TABLE int8_t CDEF_DIRS[8][2][2] = {{{-1, 1}, {-2, 2}}, {{0, 1}, {-1, 2}}, {{0, 1}, {0, 2}}, {{0, 1}, {1, 2}},
                                       {{1, 1}, {2, 2}},   {{1, 0}, {2, 1}},  {{1, 0}, {2, 0}}, {{1, 0}, {2, -1}}};
 
-SK_HD int cdef_dir_from_partials(const int (*partial)[15], int* var) {
+// Cost of direction d from the line sums (the spec's cost[d]).
+SK_HD long long cdef_dir_cost(const int (*partial)[15], int d) {
     const int32_t* div_table = CDEF_DIV;
-    long long cost[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < 8; i++) {
-        cost[2] += (long long)partial[2][i] * partial[2][i];
-        cost[6] += (long long)partial[6][i] * partial[6][i];
-    }
-    cost[2] *= div_table[8];
-    cost[6] *= div_table[8];
-    for (int i = 0; i < 7; i++) {
-        cost[0] += ((long long)partial[0][i] * partial[0][i] + (long long)partial[0][14 - i] * partial[0][14 - i]) *
-                   div_table[i + 1];
-        cost[4] += ((long long)partial[4][i] * partial[4][i] + (long long)partial[4][14 - i] * partial[4][14 - i]) *
-                   div_table[i + 1];
-    }
-    cost[0] += (long long)partial[0][7] * partial[0][7] * div_table[8];
-    cost[4] += (long long)partial[4][7] * partial[4][7] * div_table[8];
-    for (int i = 1; i < 8; i += 2) {
-        for (int j = 0; j < 5; j++) cost[i] += (long long)partial[i][3 + j] * partial[i][3 + j];
-        cost[i] *= div_table[8];
+    long long c = 0;
+    if (d == 2 || d == 6) {
+        for (int i = 0; i < 8; i++) c += (long long)partial[d][i] * partial[d][i];
+        c *= div_table[8];
+    } else if (d == 0 || d == 4) {
+        for (int i = 0; i < 7; i++)
+            c += ((long long)partial[d][i] * partial[d][i] + (long long)partial[d][14 - i] * partial[d][14 - i]) *
+                 div_table[i + 1];
+        c += (long long)partial[d][7] * partial[d][7] * div_table[8];
+    } else {
+        for (int j = 0; j < 5; j++) c += (long long)partial[d][3 + j] * partial[d][3 + j];
+        c *= div_table[8];
         for (int j = 0; j < 3; j++)
-            cost[i] += ((long long)partial[i][j] * partial[i][j] + (long long)partial[i][10 - j] * partial[i][10 - j]) *
-                       div_table[2 * j + 2];
+            c += ((long long)partial[d][j] * partial[d][j] + (long long)partial[d][10 - j] * partial[d][10 - j]) *
+                 div_table[2 * j + 2];
     }
+    return c;
+}
+// Best direction (first maximum) and var from the eight costs.
+SK_HD int cdef_pick_dir(const long long* cost, int* var) {
     long long best = 0;
     int dir = 0;
     for (int i = 0; i < 8; i++)
         if (cost[i] > best) { best = cost[i]; dir = i; }
     *var = (int)((best - cost[(dir + 4) & 7]) >> 10);
     return dir;
+}
+SK_HD int cdef_dir_from_partials(const int (*partial)[15], int* var) {
+    long long cost[8];
+    for (int d = 0; d < 8; d++) cost[d] = cdef_dir_cost(partial, d);
+    return cdef_pick_dir(cost, var);
 }
 // Direction of the luma 8x8 block at `src`: returns yDir, writes var.
 SK_HD int cdef_find_dir(const uint8_t* src, int stride, int* var) {

@@ -968,6 +968,7 @@ __global__ __launch_bounds__(256) void k_av1_lf(Av1Args A, int plane, int pass) 
 __global__ __launch_bounds__(256) void k_av1_cdef(Av1Args A) {
     __shared__ int part[4][8][15];
     __shared__ int dirvar[4][2];
+    __shared__ long long cost[4][8];
     const Av1Geo& g = A.geo;
     const int w = threadIdx.x >> 6, l = lane();
     const int cols = g.mi_cols >> 1, rows = g.mi_rows >> 1;
@@ -986,9 +987,11 @@ __global__ __launch_bounds__(256) void k_av1_cdef(Av1Args A) {
 #pragma unroll
     for (int d = 0; d < 8; d++) atomicAdd(&part[w][d][cdef_partial_index(d, i, j)], x);
     wsync();
+    if (l < 8) cost[w][l] = cdef_dir_cost(part[w], l);   // one direction per lane
+    wsync();
     if (l == 0) {
         int var = 0;
-        dirvar[w][0] = cdef_dir_from_partials(part[w], &var);
+        dirvar[w][0] = cdef_pick_dir(cost[w], &var);
         dirvar[w][1] = var;
     }
     wsync();
