@@ -182,7 +182,11 @@ class X11Source : public FrameSource {
         // the damage accumulated so far, taken BEFORE the image: anything drawn in between
         // is in the pixels and reported again next frame (over-reporting is harmless)
         fetch_damage();
-        if (!api_.ShmGetImage(dpy_, root_, img, x_, y_, AllPlanes)) return nullptr;
+        if (!api_.ShmGetImage(dpy_, root_, img, x_, y_, AllPlanes)) {
+            dmg_carry_ = true;   // the drained rows are not in any image yet: report them next time
+            return nullptr;
+        }
+        dmg_carry_ = false;
         if (cursor_ && api_.FixesGetCursorImage) {
             if (overlay_cursor_) fetch_cursor();
             else composite_cursor(img);
@@ -218,7 +222,7 @@ class X11Source : public FrameSource {
         api_.DamageSubtract(dpy_, damage_, 0, region_);
         int n = 0;
         XRectangle* r = api_.FixesFetchRegion(dpy_, region_, &n);
-        dmg_rows_.clear();
+        if (!dmg_carry_) dmg_rows_.clear();   // after a failed grab the drained rows stay
         for (int i = 0; r && i < n; i++) {
             if (r[i].x >= x_ + w_ || r[i].x + (int)r[i].width <= x_) continue;   // outside the region
             const int y0 = std::max(0, r[i].y - y_), y1 = std::min(h_, r[i].y + (int)r[i].height - y_);
@@ -289,6 +293,7 @@ class X11Source : public FrameSource {
     unsigned long damage_ = 0, region_ = 0;   // XDamage object and the XFixes region it is drained into
     std::vector<int> dmg_rows_;
     bool dmg_ok_ = false;
+    bool dmg_carry_ = false;   // the last grab failed after draining damage
     long long grabs_ = 0;
     int x_, y_, w_, h_;
     bool cursor_;

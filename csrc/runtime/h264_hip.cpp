@@ -172,6 +172,10 @@ class HipBackend : public EncoderBackend {
             return -1;
         }
         const int q = launched_ & 1;   // parity this frame is launched with
+        // A re-upload before launch (the staged frame was never launched) overwrites
+        // bgrx_dev_[q] again: the two-frames-ago invariant of upload_copy no longer holds
+        // for either parity, so the next two uploads are full copies.
+        if (staged_) up_valid_[0] = up_valid_[1] = false;
         // Nothing in flight: copy on the encoder's own stream (no cross-stream wait).
         // Overlapped upload, or bands of one frame: the device's shared copy stream, so
         // the uploads of all encoders on this GPU run back to back at full PCIe rate

@@ -416,6 +416,11 @@ int sk_h264_upload(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame
     }
 }
 
+int sk_h264_set_upload_rows(void* enc, const int32_t* rows, int32_t n) {
+    static_cast<EncoderBackend*>(enc)->set_upload_rows(rows, n);
+    return 0;
+}
+
 int sk_h264_launch(void* enc) {
     try {
         return static_cast<EncoderBackend*>(enc)->launch();

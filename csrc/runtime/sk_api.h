@@ -69,6 +69,9 @@ int sk_h264_upload(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame
 // The next sk_h264_upload waits on the device for the work queued on `stream` (a HIP
 // stream of the encoder's device), instead of a host synchronisation.
 int sk_h264_wait_stream(void* enc, void* stream);
+// Damage of the next sk_h264_upload: n [y0, y1) row ranges changed since the previous
+// upload (n < 0: unknown -> full copy). The HIP backend then copies only those rows.
+int sk_h264_set_upload_rows(void* enc, const int32_t* rows, int32_t n);
 int sk_h264_launch(void* enc);
 // Session state snapshot (codec/h264_encoder.h StateHeader layout, identical for the
 // CPU and HIP backends): move a session between GPUs / processes without an IDR.

@@ -118,6 +118,7 @@ def lib():
         L.sk_h264_finish.argtypes = [ctypes.c_void_p]
         L.sk_h264_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_launch.argtypes = [ctypes.c_void_p]
+        L.sk_h264_set_upload_rows.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
         L.sk_h264_state_bytes.argtypes = [ctypes.c_void_p]
         L.sk_h264_state_bytes.restype = ctypes.c_int64
         L.sk_h264_export_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
@@ -368,6 +369,16 @@ class H264Encoder:
         if L.sk_h264_upload(self._h, ctypes.c_void_p(int(ptr)), int(stride), frame_id & 0xFFFF) < 0:
             self._staged = None
             raise RuntimeError(f"upload failed: {L.sk_last_error().decode()}")
+
+    def set_upload_rows(self, rows) -> None:
+        """Damage of the next :meth:`upload`: ``[(y0, y1), ...]`` rows changed since the
+        previous upload, or None (unknown: full copy)."""
+        L = lib()
+        if rows is None:
+            L.sk_h264_set_upload_rows(self._h, None, -1)
+            return
+        a = np.ascontiguousarray(np.asarray(rows, np.int32).reshape(-1, 2))
+        L.sk_h264_set_upload_rows(self._h, a.ctypes.data if a.size else None, a.shape[0])
 
     def launch(self) -> None:
         L = lib()

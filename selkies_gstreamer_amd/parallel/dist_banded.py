@@ -64,10 +64,15 @@ class DistBandedEncoder:
 
     ``frame`` on rank 0: a uint8 tensor (H, W, 4) on this rank's device (``cuda`` for
     RCCL, CPU for gloo) or a numpy array (copied to the device). Returns the packets
-    of the whole frame on rank 0, ``None`` on the other ranks."""
+    of the whole frame on rank 0, ``None`` on the other ranks.
+
+    The constructor is collective over the DEFAULT group when ``group`` is an RCCL group
+    and no ``control_group`` is given: it creates the gloo twin with ``dist.new_group``,
+    which every process of the job must call in the same order. With a sub-group, create
+    its gloo twin on all ranks yourself and pass it as ``control_group``."""
 
     def __init__(self, width: int, height: int, *, stripe_height: int = 64, group=None, backend: str = "hip",
-                 **kw):
+                 control_group=None, **kw):
         if kw.get("fullframe"):
             raise ValueError("distributed bands need striped mode (independent stripe streams)")
         self.group = group
@@ -88,7 +93,14 @@ class DistBandedEncoder:
                       if self.rank == 0 else None)
         # control plane on the host: a gloo twin of an RCCL group, so reading the
         # broadcast values never synchronises a GPU stream
-        self._cgroup = dist.new_group(ranks=self._ranks(group), backend="gloo") if self.nccl else group
+        if control_group is not None:
+            self._cgroup = control_group
+        elif not self.nccl:
+            self._cgroup = group
+        elif group is None:
+            self._cgroup = dist.new_group(ranks=self._ranks(group), backend="gloo")
+        else:   # new_group over a sub-group's ranks would hang the ranks outside it
+            raise ValueError("an RCCL sub-group needs control_group= (its gloo twin, created on every rank)")
         self._ctrl = torch.zeros(3, dtype=torch.int64)
         self._key = False
         self._qp = 0

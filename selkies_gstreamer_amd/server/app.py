@@ -88,6 +88,15 @@ def make_input_factory(settings: Settings, opts):
     return factory
 
 
+
+def basic_auth_from_env(env=None):
+    """(user, password) when SELKIES_ENABLE_BASIC_AUTH is true (the legacy signalling
+    server's variables, legacy/signalling.py), else None."""
+    env = os.environ if env is None else env
+    if env.get("SELKIES_ENABLE_BASIC_AUTH", "false").lower() not in ("true", "1", "yes"):
+        return None
+    return env.get("SELKIES_BASIC_AUTH_USER", env.get("USER", "")), env.get("SELKIES_BASIC_AUTH_PASSWORD", "")
+
 async def serve(argv: Sequence[str], stop: Optional[asyncio.Event] = None, ready=None):
     from .data_server import DataStreamingServer
     from .metrics import Metrics
@@ -109,7 +118,7 @@ async def serve(argv: Sequence[str], stop: Optional[asyncio.Event] = None, ready
                                  download_dir=opts.upload_dir if "download" in settings.file_transfers else None,
                                  input_factory=make_input_factory(settings, opts), capture_source=opts.capture_source,
                                  gpu_id=opts.gpu_id, num_gpus=opts.num_gpus, web_root=opts.web_root, metrics=metrics,
-                                 x_display=opts.display)
+                                 x_display=opts.display, basic_auth=basic_auth_from_env())
     metrics.server = server
     port = await server.start(opts.host, settings.port)
     if ready is not None:

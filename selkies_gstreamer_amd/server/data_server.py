@@ -21,7 +21,10 @@ MI355X-first differences:
 from __future__ import annotations
 
 import asyncio
+import base64
+import binascii
 import ctypes
+import hmac
 import json
 import logging
 import os
@@ -200,14 +203,28 @@ def files_listing_html(path: str, rel: str) -> str:
             "<body><h3>Files " + title + "</h3><ul>" + "".join(rows) + "</ul></body></html>")
 
 
+def _basic_auth_ok(request, user: str, password: str) -> bool:
+    h = request.headers.get("Authorization", "")
+    if not h.startswith("Basic "):
+        return False
+    try:
+        got = base64.b64decode(h[6:].strip(), validate=True)
+    except (ValueError, binascii.Error):
+        return False
+    return hmac.compare_digest(got, f"{user}:{password}".encode())
+
+
 class DataStreamingServer:
     def __init__(self, settings: Settings, *, upload_dir: Optional[str] = None, download_dir: Optional[str] = None,
                  input_factory=None,
                  capture_factory: Optional[Callable[[], Any]] = None, display_manager=None,
                  capture_source: str = "auto", gpu_id: int = 0, num_gpus: int = 1, clock=time.monotonic,
                  web_root: Optional[str] = None, metrics=None, frame_trace: Optional[bool] = None,
-                 x_display: Optional[str] = None):
+                 x_display: Optional[str] = None, basic_auth: Optional[tuple] = None):
         self.settings = settings
+        # (user, password) guarding /files/: the reference serves that area from nginx
+        # behind the container's basic auth; here the data server checks it itself
+        self.basic_auth = basic_auth
         # this session's X display, passed explicitly to capture, xrandr, DPI and
         # the WM swap: a session host runs several servers in one process, so the
         # process-wide DISPLAY cannot name each session's desktop (parallel/multi.py)
@@ -278,6 +295,8 @@ class DataStreamingServer:
         root = self.download_dir
         if not root or not os.path.isdir(root):
             raise web.HTTPNotFound()
+        if self.basic_auth is not None and not _basic_auth_ok(request, *self.basic_auth):
+            raise web.HTTPUnauthorized(headers={"WWW-Authenticate": 'Basic realm="selkies"'})
         rel = request.match_info.get("name", "")
         base = os.path.realpath(root)
         path = os.path.realpath(os.path.join(base, rel))

@@ -234,14 +234,18 @@ class H265Depacketizer:
 
 
 def _leb128(buf: bytes, pos: int) -> tuple[int, int]:
+    """LEB128 at pos -> (value, next pos); ValueError when truncated or over 8 bytes."""
     v, sh = 0, 0
-    while True:
+    for _ in range(8):
+        if pos >= len(buf):
+            raise ValueError("truncated leb128")
         b = buf[pos]
         pos += 1
         v |= (b & 0x7F) << sh
         sh += 7
         if not b & 0x80:
             return v, pos
+    raise ValueError("leb128 longer than 8 bytes")
 
 
 def _put_leb128(v: int) -> bytes:
@@ -274,14 +278,20 @@ class AV1Depacketizer:
         z, y, w = bool(agg & 0x80), bool(agg & 0x40), (agg >> 4) & 3
         pos, elems = 1, []
         k = 0
-        while pos < len(payload):
-            k += 1
-            if w and k == w:            # last element: no length field
-                n = len(payload) - pos
-            else:
-                n, pos = _leb128(payload, pos)
-            elems.append(payload[pos:pos + n])
-            pos += n
+        try:
+            while pos < len(payload):
+                k += 1
+                if w and k == w:            # last element: no length field
+                    n = len(payload) - pos
+                else:
+                    n, pos = _leb128(payload, pos)
+                if n == 0 or pos + n > len(payload):
+                    raise ValueError("OBU element exceeds the packet")
+                elems.append(payload[pos:pos + n])
+                pos += n
+        except ValueError:   # malformed packet: drop it and the fragment it may continue
+            self._frag = None
+            return None
         for i, e in enumerate(elems):
             cont = i == 0 and z
             more = i == len(elems) - 1 and y
@@ -301,6 +311,11 @@ class AV1Depacketizer:
             for o in self._obus:
                 ext = (o[0] >> 2) & 1
                 hl = 1 + ext
+                if len(o) < hl:
+                    continue
+                if o[0] & 2:   # the sender kept obu_has_size_field: the OBU is complete as is
+                    out += o
+                    continue
                 out += bytes([o[0] | 2]) + o[1:hl] + _put_leb128(len(o) - hl) + o[hl:]
             self._obus, self._frag = [], None
             return bytes(out)

@@ -123,3 +123,17 @@ def test_av1_rtp_roundtrip(mtu):
         for x, h in zip(pkts, hdrs):
             out = dep.push(x[h.header_len:], h.timestamp, h.marker)
         assert out == tu
+
+
+def test_av1_depacketizer_malformed_and_sized_obus():
+    """Truncated / oversized elements are dropped without raising; an OBU the sender
+    kept obu_has_size_field on passes through unchanged (no second size field)."""
+    from selkies_gstreamer_amd.webrtc import rtp
+    dep = rtp.AV1Depacketizer()
+    assert dep.push(bytes([0x00, 0x85]), 1, True) is None          # leb128 cut short
+    assert dep.push(bytes([0x00, 0x05, 0x30, 0x01]), 2, True) is None  # element longer than the packet
+    sized = bytes([0x32, 0x02, 0xAA, 0xBB])                        # OBU_FRAME with has_size + size 2
+    out = dep.push(bytes([0x10]) + sized, 3, True)                  # W=1: one element, no length
+    assert out == b"\x12\x00" + sized
+    bare = bytes([0x30, 0xAA, 0xBB])                               # no size field: one is added
+    assert dep.push(bytes([0x10]) + bare, 4, True) == b"\x12\x00" + bytes([0x32, 0x02, 0xAA, 0xBB])

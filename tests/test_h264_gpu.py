@@ -202,3 +202,33 @@ def test_gpu_aq_matches_cpu(fullframe, kind):
         if t == 0 and kind == "desktop":
             assert len(np.unique(qa)) > 1
         assert psnr(sd.Y, bgrx_to_y709(f)) > 28
+
+
+def _changed_rows(a, b):
+    rows = np.nonzero((a != b).any(axis=(1, 2)))[0]
+    return [(int(y), int(y) + 1) for y in rows]
+
+
+def test_gpu_damage_upload_survives_reupload():
+    """Damage-driven upload (set_upload_rows): a frame uploaded twice before launch (the
+    capture loop retrying with a newer grab) must not leave stale rows in either parity
+    buffer. Packets equal the CPU encoder fed the frames that were launched."""
+    W, H = 256, 128
+    src = SyntheticDesktop(W, H, kind="desktop")
+    frames = [np.ascontiguousarray(src.frame(t)) for t in range(8)]
+    for t in range(1, 8):   # extra damage in every frame, a different band each time
+        frames[t] = frames[t].copy()
+        frames[t][(t * 16) % H:(t * 16) % H + 8, :, :3] ^= 0x3C
+    cpu, gpu = _pair(W, H, stripe_height=64)
+    launched = [0, 1, 3, 4, 6, 7]   # frames 2 and 5 are uploaded, then replaced before launch
+    prev = None
+    for t in range(8):
+        gpu.set_upload_rows(None if prev is None else _changed_rows(frames[prev], frames[t]))
+        gpu.upload(frames[t], t)
+        prev = t
+        if t not in launched:
+            continue
+        gpu.launch()
+        pg = gpu.finish()
+        pc = cpu.encode(frames[t], t)
+        assert [p.data for p in pg] == [p.data for p in pc], f"frame {t}: HIP packets differ from CPU"

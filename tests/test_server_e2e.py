@@ -283,6 +283,16 @@ def test_files_listing_and_download(tmp_path):
                 async with sess.get(base + bad) as r:
                     assert r.status == 404, bad
         await srv.stop()
+        srv3 = DataStreamingServer(s, capture_source="synthetic", download_dir=str(d), basic_auth=("u", "pw"))
+        port = await srv3.start("127.0.0.1", 0)
+        async with aiohttp.ClientSession() as sess:
+            async with sess.get(f"http://127.0.0.1:{port}/files/") as r:
+                assert r.status == 401 and "Basic" in r.headers["WWW-Authenticate"]
+            async with sess.get(f"http://127.0.0.1:{port}/files/", auth=aiohttp.BasicAuth("u", "bad")) as r:
+                assert r.status == 401
+            async with sess.get(f"http://127.0.0.1:{port}/files/a%20%3Cb%3E.txt", auth=aiohttp.BasicAuth("u", "pw")) as r:
+                assert r.status == 200 and await r.text() == "hello"
+        await srv3.stop()
         srv2 = DataStreamingServer(s, capture_source="synthetic")   # downloads disabled
         port = await srv2.start("127.0.0.1", 0)
         async with aiohttp.ClientSession() as sess:
