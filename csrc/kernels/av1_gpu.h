@@ -34,8 +34,17 @@ struct Av1Args {
     int* frame_host;          // host-mapped copy of frame[0..2]
     h264::gpu::Planes cdef_in;   // the deblocked picture CDEF reads (k_av1_cdef writes f.rec)
     const uint8_t* qidx_of_qp;   // [52]
-    uint16_t* chunks;         // [tiles][tile_cap] settled coder chunks
-    int tile_cap;             // chunk capacity per tile
+    int tile_cap;             // byte capacity per tile
+    // block-parallel coder (k_av1_ec_*): per block 128 candidate (exit rng, shift count)
+    // maps and {first token, end, entry rng, shift prefix}; per tile the big integer low
+    // as 64-bit digit sums (ecv), its carried 32-bit digits (ecf) and its total shift
+    uint2* ecmap;             // [ec_max_blocks][128]
+    int4* ecblk;              // [ec_max_blocks]
+    int ec_max_blocks;
+    unsigned long long* ecv;  // [tiles][ec_vcap]
+    uint32_t* ecf;            // [tiles][ec_vcap]
+    int ec_vcap;
+    int* tile_bits;           // [tiles] total shift D (-1: over capacity)
     int* tile_size;           // device [tiles] bytes
     uint8_t* out_host;        // host-mapped tile bytes, concatenated [out_cap]
     int out_cap;
@@ -43,6 +52,8 @@ struct Av1Args {
 };
 
 void launch_backend(const Av1Args& a, hipStream_t s);
+// Sizes of the coder's block maps and big-integer digits for tiles of tile_bytes.
+void ec_buffers(int tiles, int tile_bytes, int* max_blocks, int* vcap);
 
 }  // namespace gpu
 }  // namespace av1

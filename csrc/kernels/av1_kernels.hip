@@ -12,8 +12,9 @@
 //   k_av1_tok_scan/copy  per-tile token streams in coding order
 //   k_av1_cdf          CDF adaptation, 16 context partitions per tile in parallel ->
 //                      per-symbol interval words
-//   k_av1_ec           one wave per tile: the arithmetic coder (scalar state)
-//   k_av1_pack         carry resolution (segmented, parallel), tile bytes -> host-mapped output
+//   k_av1_ec_map/link/emit/bytes  the arithmetic coder, parallel over token blocks:
+//                      speculative rng per block (128 candidate states), block chaining,
+//                      big-integer accumulation of low, carries -> host-mapped tile bytes
 //   k_av1_lf           in-loop deblocking (codec/av1_lf.h), one launch per plane and pass
 //   k_av1_cdef         CDEF (codec/av1_cdef.h), one wave per 8x8, from a copy of the deblocked picture
 //   k_av1_finish       padding rows of the reconstruction, slice actions for k_commit
@@ -606,12 +607,8 @@ __global__ __launch_bounds__(256) void k_av1_tok_copy(Av1Args A) {
 //   [9:0] (32768 - cdf[s]) >> 6 (0 for the last symbol)   [19:10] (32768 - cdf[s-1]) >> 6
 //   [24:20] N - s   [25] s > 0
 // Literal tokens are copied as their own word (bits 31:30 = 01).
-// k_av1_ec (phase B): one wave per tile runs the arithmetic coder over the interval
-// words and literal bits with its state in scalar registers (the only serial work
-// left), tokens / words in double-buffered 64-lane vector batches, settled chunks
-// through an LDS ring flushed 1024 at a time. Bit-exact with SymbolCoder (av1_ec.h).
-constexpr int kObRing = 4096;
-constexpr int kObFlush = 1024;
+// Phase B (k_av1_ec_*, below k_av1_cdf): the arithmetic coder over the interval words
+// and literal bits, parallel over token blocks. Bit-exact with SymbolCoder (av1_ec.h).
 constexpr int kEcParts = 16;
 
 __device__ __forceinline__ uint32_t sgpr(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
@@ -749,195 +746,333 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     }
 }
 
-__global__ __launch_bounds__(64) void k_av1_ec(Av1Args A) {
-    __shared__ uint16_t ob[kObRing];
-    const int t = blockIdx.x, L = threadIdx.x;
-    const int ntok = A.tile_ntok[t], last = A.tile_tok_cap - 1;
-    const int cap = A.tile_cap;
-    const uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
-    uint16_t* dst = A.chunks + (size_t)t * cap;
-    uint64_t low = 0;
-    uint32_t rng = 0x8000;
-    int cnt = -9, nb = 0, fl = 0;
+// ---------------------------------------------------------------------------
+// Phase B: the arithmetic coder, parallel over token blocks (no per-tile serial pass).
+//
+// The coder state is (low, rng). rng alone evolves serially, and at every token that
+// "resets" it - a symbol with s > 0 (interval bounds u, v from rng >> 8 only) or a
+// literal whose first bit is 1 (split from rng >> 8 only) - the next rng depends on
+// the 7 bits of rng >> 8 (128 values in [32768, 65535]), not on the whole state.
+// low is a sum: symbol i adds a_i = r_i - u_i at bit position P_i = (total shift after
+// i), so the tile is one big integer V = sum a_i << P_i, finished as
+// V' = ((V + 0x3fff) & ~0x3fff) | 0x4000 and emitted as its top 8N bits with
+// N = (D + 8) >> 3 (D = total shift): byte j holds bits [D + 7 - 8j, D + 15 - 8j).
+// (Equal to SymbolCoder in codec/av1_ec.h, carries included; tests/test_av1_entropy.py.)
+//
+//   k_av1_ec_map   blocks of ~kEcBlk tokens, each starting at a resetting token: every
+//                  lane runs the block from two candidate states (rng >> 8 = 128 + l and
+//                  192 + l) -> per candidate the exit rng and the block's shift count
+//   k_av1_ec_link  one wave per tile chains the block maps (LDS-free readlane lookups)
+//                  -> each block's true entry rng and shift prefix; tile sizes
+//   k_av1_ec_emit  each block re-run from its true entry, scalar state: a_i into V's
+//                  64-bit words (coalesced per word, one atomic per word and block)
+//   k_av1_ec_bytes per tile: carries of V (carry-lookahead scan), rounding, bytes ->
+//                  host-mapped output at the tiles' prefix offsets
+constexpr int kEcBlk = 512;      // nominal tokens per block
+constexpr int kEcGrid = 1024;    // workgroups (4 waves) of the block-parallel kernels
 
-    auto put = [&](uint32_t x) {
-        if (L == 0) ob[nb & (kObRing - 1)] = (uint16_t)x;
-        nb++;
-    };
-    auto norm = [&](uint32_t r2) {
-        const int d = __builtin_clz(r2) - 16;
-        int c = cnt, s = c + d;
-        if (s >= 0) {
-            c += 16;
-            uint64_t m = (1ull << c) - 1;
-            if (s >= 8) {
-                put((uint32_t)(low >> c));
-                low &= m;
-                c -= 8;
-                m >>= 8;
-            }
-            put((uint32_t)(low >> c));
-            s = c + d - 24;
-            low &= m;
-        }
-        low <<= d;
-        rng = r2 << d;
-        cnt = s;
-    };
-    auto flush = [&](int upto) {   // ring [fl, upto) -> dst (upto - fl <= kObFlush)
-        wsync();
-#pragma unroll 4
-        for (int j = 0; j < kObFlush; j += 64) {
-            const int i = fl + j + L;
-            if (i < upto && i < cap) dst[i] = ob[i & (kObRing - 1)];
-        }
-        fl = upto;
-        wsync();
-    };
-    auto emit = [&](int d, int s) {   // norm() for s = cnt + d >= 0 (a byte or two settled)
-        int c = cnt + 16;
-        uint64_t m = (1ull << c) - 1;
-        if (s >= 8) {
-            put((uint32_t)(low >> c));
-            low &= m;
-            c -= 8;
-            m >>= 8;
-        }
-        put((uint32_t)(low >> c));
-        cnt = c + d - 24;
-        low &= m;
-    };
-    auto code = [&](uint32_t wv, int b) {
-        const int m = sk_min(64, ntok - b);
-#pragma unroll 2
-        for (int i = 0; i < m; i++) {
-            // the coder state is wave-uniform: keep it in scalar registers
-            rng = sgpr(rng);
-            cnt = (int)sgpr((uint32_t)cnt);
-            nb = (int)sgpr((uint32_t)nb);
-            low = ((uint64_t)sgpr((uint32_t)(low >> 32)) << 32) | sgpr((uint32_t)low);
-            const uint32_t w = sgpr(rdlane(wv, i));
-            if (__builtin_expect((w >> 30) == 1, 0)) {   // L(n) literal token: equiprobable bits
-                const int nbits = (int)((w >> 25) & 31) + 1;
-                for (int k = nbits - 1; k >= 0; k--) {
-                    const uint32_t rr = rng, split = ((rr >> 8) << 7) + kMinProb;
-                    if ((w >> k) & 1) {
-                        low += rr - split;
-                        norm(split);
-                    } else {
-                        norm(rr - split);
-                    }
-                }
-                continue;
-            }
-            // symbol: interval from the k_av1_cdf word (straight-line, one rare branch)
-            const uint32_t r = rng, r8 = r >> 8, ns4 = ((w >> 20) & 31) * kMinProb;
-            const uint32_t v = ((r8 * (w & 1023)) >> (7 - kProbShift)) + ns4 - kMinProb;
-            const uint32_t uu = ((r8 * ((w >> 10) & 1023)) >> (7 - kProbShift)) + ns4;
-            const uint32_t u = (w >> 25) & 1 ? uu : r;
-            low += r - u;
-            const uint32_t r2 = u - v;
-            const int d = __builtin_clz(r2) - 16;
-            const int sh = cnt + d;
-            if (__builtin_expect(sh >= 0, 0)) emit(d, sh);
-            else cnt = sh;
-            low <<= d;
-            rng = r2 << d;
-        }
-    };
-    uint32_t WX[kSub], WY[kSub];
-    auto load = [&](uint32_t* wv, int b) {
+__device__ __forceinline__ bool ec_resets(uint32_t w) {
+    if ((w >> 30) == 1) return (w >> ((w >> 25) & 31)) & 1;   // literal: its first (top) bit
+    return (w >> 25) & 1;                                        // symbol: s > 0
+}
+// Block size of this frame: at least kEcBlk, larger when the frame would need more
+// than max_blocks maps. Lane t < tiles: the tile's block count; returns the total,
+// incl = inclusive prefix over lanes.
+__device__ __forceinline__ int ec_blocks(const Av1Args& A, int tiles, int* bsz, int* incl, int* ntok_l) {
+    const int l = lane();
+    const int nt = l < tiles ? A.tile_ntok[l] : 0;
+    const int tot = wsum(nt);
+    int b = kEcBlk;
+    const int need = (tot + A.ec_max_blocks - tiles - 1) / sk_max(A.ec_max_blocks - tiles, 1);
+    if (need > b) b = (need + 63) & ~63;
+    int n = l < tiles ? (nt + b - 1) / b : 0;
+    if (l < tiles && n == 0) n = 1;
+    int x = n;
 #pragma unroll
-        for (int j = 0; j < kSub; j++) wv[j] = pw[sk_min(b + 64 * j + L, last)];
-    };
-    auto big = [&](uint32_t* wv, int b) {
-        use_regs(wv);
-#pragma unroll
-        for (int j = 0; j < kSub; j++) {
-            if (b + 64 * j < ntok) code(wv[j], b + 64 * j);
-            nb = (int)sgpr((uint32_t)nb);
-            fl = (int)sgpr((uint32_t)fl);
-            if (nb - fl >= kObFlush) flush(fl + kObFlush);   // <= 64 x 4 chunks per sub-batch
-        }
-    };
-    load(WX, 0);
-    load(WY, kBig);
-    for (int b = 0; b < ntok; b += 2 * kBig) {
-        big(WX, b);
-        load(WX, b + 2 * kBig);
-        if (b + kBig < ntok) big(WY, b + kBig);
-        load(WY, b + 3 * kBig);
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (l >= o) x += y;
     }
-    {   // SymbolCoder::finish
-        int c = cnt;
-        const uint64_t m = 0x3fffu;
-        uint64_t e = ((low + m) & ~m) | (m + 1);
-        int s = c + 10;
-        if (s > 0) {
-            uint64_t nm = (1ull << (c + 16)) - 1;
-            do {
-                put((uint32_t)(e >> (c + 16)));
-                e &= nm;
-                s -= 8;
-                nm >>= 8;
-                c -= 8;
-            } while (s > 0);
-        }
+    *bsz = b;
+    *incl = x;
+    *ntok_l = nt;
+    return __shfl(x, 63);
+}
+__device__ int ec_first_reset(const uint32_t* pw, int i, int ntok) {
+    for (; i < ntok; i += 64) {
+        const int k = i + lane();
+        const bool r = k < ntok && ec_resets(pw[k < ntok ? k : 0]);
+        const uint64_t m = __ballot(r);
+        if (m) return i + __builtin_ctzll(m);
     }
-    while (nb - fl > 0) flush(fl + sk_min(nb - fl, kObFlush));
-    if (L == 0) A.tile_size[t] = nb <= cap ? nb : -1;
+    return ntok;
+}
+// One symbol / literal bit on a per-lane rng (VALU): returns r2 (before normalisation).
+__device__ __forceinline__ uint32_t ec_sym_r2(uint32_t r, uint32_t w) {
+    const uint32_t r8 = r >> 8, ns4 = ((w >> 20) & 31) * kMinProb;
+    const uint32_t v = ((r8 * (w & 1023)) >> (7 - kProbShift)) + ns4 - kMinProb;
+    const uint32_t u = (w >> 25) & 1 ? ((r8 * ((w >> 10) & 1023)) >> (7 - kProbShift)) + ns4 : r;
+    return u - v;
+}
+__device__ __forceinline__ void ec_norm(uint32_t& r, uint32_t& D, uint32_t r2) {
+    const uint32_t d = (uint32_t)__builtin_clz(r2) - 16;
+    r = r2 << d;
+    D += d;
+}
+__device__ __forceinline__ void ec_step(uint32_t& r, uint32_t& D, uint32_t w) {
+    if ((w >> 30) == 1) {
+        const int nb = (int)((w >> 25) & 31) + 1;
+        for (int k = nb - 1; k >= 0; k--) {
+            const uint32_t split = ((r >> 8) << 7) + kMinProb;
+            ec_norm(r, D, (w >> k) & 1 ? split : r - split);
+        }
+    } else {
+        ec_norm(r, D, ec_sym_r2(r, w));
+    }
 }
 
-// Tile bytes (carry-resolved) -> host-mapped output at the tiles' prefix offsets.
-// carry_bytes (codec/av1_ec.h) in parallel: windows of chunks from the end; each
-// thread resolves a 64-chunk segment for carry-in 0, 1 and 2, a serial pass over the
-// 256 segment outcomes links them, then every thread writes its bytes.
-__global__ __launch_bounds__(256) void k_av1_pack(Av1Args A) {
-    constexpr int kSeg = 64, kWin = 256 * kSeg;
-    __shared__ uint16_t win[kWin];
-    __shared__ uint8_t cout_s[256][3];
-    __shared__ uint8_t cin_s[256];
-    __shared__ int off_s, n_s, carry_s;
-    const int t = blockIdx.x, tid = threadIdx.x;
+__global__ __launch_bounds__(256) void k_av1_ec_map(Av1Args A) {
+    const int tiles = A.geo.tile_cols * A.geo.tile_rows, l = lane();
+    int bsz, incl, ntl;
+    const int total = ec_blocks(A, tiles, &bsz, &incl, &ntl);
+    const int nw = gridDim.x * 4;
+    for (int g = (int)sgpr(blockIdx.x * 4 + (threadIdx.x >> 6)); g < total; g += nw) {
+        const int t = __popcll(__ballot(l < tiles && incl <= g));
+        const int b = g - (t ? __shfl(incl, t - 1) : 0);
+        const int ntok = __shfl(ntl, t);
+        const uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
+        const int s = b == 0 ? 0 : ec_first_reset(pw, b * bsz, ntok);
+        const int e = (b + 1) * bsz >= ntok ? ntok : ec_first_reset(pw, (b + 1) * bsz, ntok);
+        if (l == 0) A.ecblk[g] = make_int4(s, e, 0, 0);
+        // block 0 starts from the coder's initial state; the others from every candidate
+        uint32_t ra = b == 0 ? 0x8000u : (uint32_t)(128 + l) << 8, rb = b == 0 ? 0x8000u : (uint32_t)(192 + l) << 8;
+        uint32_t da = 0, db = 0;
+        for (int i0 = s; i0 < e; i0 += 64) {
+            const uint32_t wv = pw[sk_min(i0 + l, e - 1)];
+            const int m = sk_min(64, e - i0);
+            for (int j = 0; j < m; j++) {
+                const uint32_t w = rdlane(wv, j);
+                ec_step(ra, da, w);
+                ec_step(rb, db, w);
+            }
+        }
+        uint2* mp = A.ecmap + (size_t)g * 128;
+        mp[l] = make_uint2(ra, da);
+        mp[64 + l] = make_uint2(rb, db);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_av1_ec_link(Av1Args A) {
+    const int tiles = A.geo.tile_cols * A.geo.tile_rows, l = lane(), t = blockIdx.x;
+    int bsz, incl, ntl;
+    ec_blocks(A, tiles, &bsz, &incl, &ntl);
+    const int g0 = t ? __shfl(incl, t - 1) : 0, nb = __shfl(incl, t) - g0;
+    const uint2 m0 = A.ecmap[(size_t)g0 * 128];
+    uint32_t r = sgpr(m0.x), D = sgpr(m0.y);
+    if (l == 0) {
+        A.ecblk[g0].z = 0x8000;
+        A.ecblk[g0].w = 0;
+    }
+    constexpr int kG = 16;   // block maps prefetched per group: lane l holds entries l and 64 + l
+    for (int bb = 1; bb < nb; bb += kG) {
+        uint2 ma[kG], mb[kG];
+        int se = 0;
+#pragma unroll
+        for (int k = 0; k < kG; k++) {
+            const int g = g0 + sk_min(bb + k, nb - 1);
+            ma[k] = A.ecmap[(size_t)g * 128 + l];
+            mb[k] = A.ecmap[(size_t)g * 128 + 64 + l];
+        }
+        if (l < kG && bb + l < nb) {
+            const int4 bi = A.ecblk[g0 + bb + l];
+            se = bi.x < bi.y;
+        }
+        const uint64_t nonempty = __ballot(se);
+#pragma unroll
+        for (int k = 0; k < kG; k++) {
+            if (bb + k >= nb) continue;
+            const int g = g0 + bb + k;
+            if (l == 0) {
+                A.ecblk[g].z = (int)r;
+                A.ecblk[g].w = (int)D;
+            }
+            if ((nonempty >> k) & 1) {   // empty blocks pass the state through
+                const int idx = (int)(r >> 8) - 128;
+                const uint32_t er = idx < 64 ? rdlane(ma[k].x, idx) : rdlane(mb[k].x, idx - 64);
+                const uint32_t ed = idx < 64 ? rdlane(ma[k].y, idx) : rdlane(mb[k].y, idx - 64);
+                r = sgpr(er);
+                D = sgpr(D + ed);
+            }
+        }
+    }
+    // V: bits [0, D + 48) as 64-bit partial sums of 32-bit digits
+    const int nwords = (int)(D >> 5) + 3, nbytes = (int)((D + 8) >> 3);
+    const bool fits = nwords <= A.ec_vcap && nbytes <= A.tile_cap;
+    if (l == 0) A.tile_bits[t] = fits ? (int)D : -1;
+    if (fits) {
+        unsigned long long* V = A.ecv + (size_t)t * A.ec_vcap;
+        for (int i = l; i < nwords; i += 64) V[i] = 0ull;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_av1_ec_emit(Av1Args A) {
+    const int tiles = A.geo.tile_cols * A.geo.tile_rows, l = lane();
+    int bsz, incl, ntl;
+    const int total = ec_blocks(A, tiles, &bsz, &incl, &ntl);
+    const int nw = gridDim.x * 4;
+    for (int g = (int)sgpr(blockIdx.x * 4 + (threadIdx.x >> 6)); g < total; g += nw) {
+        const int t = __popcll(__ballot(l < tiles && incl <= g));
+        const int Dt = A.tile_bits[t];
+        if (Dt < 0) continue;   // tile over capacity: reported by k_av1_ec_bytes
+        const int4 bi = A.ecblk[g];
+        const int s = sgpr(bi.x), e = sgpr(bi.y);
+        const uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
+        unsigned long long* V = A.ecv + (size_t)t * A.ec_vcap;
+        uint32_t r = sgpr(bi.z);
+        int x = Dt - bi.w;   // bit position of the next add
+        x = (int)sgpr((uint32_t)x);
+        int cw = 1 << 30;    // word of accA (accB: cw + 1)
+        unsigned long long accA = 0, accB = 0;
+        auto flush = [&](int w, unsigned long long v) {
+            if (v && l == 0) atomicAdd(V + w, v);
+        };
+        auto put = [&](uint32_t add) {
+            const int k = x >> 5;
+            const unsigned long long v = (unsigned long long)add << (x & 31);
+            if (k != cw) {
+                if (k == cw - 1) {
+                    flush(cw + 1, accB);
+                    accB = accA;
+                } else {
+                    flush(cw, accA);
+                    flush(cw + 1, accB);
+                    accB = 0;
+                }
+                accA = 0;
+                cw = k;
+            }
+            accA += v & 0xffffffffull;
+            accB += v >> 32;
+        };
+        for (int i0 = s; i0 < e; i0 += 64) {
+            const uint32_t wv = pw[sk_min(i0 + l, e - 1)];
+            const int m = sk_min(64, e - i0);
+            for (int j = 0; j < m; j++) {
+                const uint32_t w = sgpr(rdlane(wv, j));
+                r = sgpr(r);
+                x = (int)sgpr((uint32_t)x);
+                if ((w >> 30) == 1) {
+                    const int nb = (int)((w >> 25) & 31) + 1;
+                    for (int k = nb - 1; k >= 0; k--) {
+                        const uint32_t split = ((r >> 8) << 7) + kMinProb;
+                        uint32_t r2 = r - split;
+                        if ((w >> k) & 1) {
+                            put(r - split);
+                            r2 = split;
+                        }
+                        const int d = __builtin_clz(r2) - 16;
+                        r = r2 << d;
+                        x -= d;
+                    }
+                } else {
+                    const uint32_t r8 = r >> 8, ns4 = ((w >> 20) & 31) * kMinProb;
+                    const uint32_t v = ((r8 * (w & 1023)) >> (7 - kProbShift)) + ns4 - kMinProb;
+                    uint32_t u = r;
+                    if ((w >> 25) & 1) {
+                        u = ((r8 * ((w >> 10) & 1023)) >> (7 - kProbShift)) + ns4;
+                        put(r - u);
+                    }
+                    const uint32_t r2 = u - v;
+                    const int d = __builtin_clz(r2) - 16;
+                    r = r2 << d;
+                    x -= d;
+                }
+            }
+        }
+        flush(cw, accA);
+        flush(cw + 1, accB);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_av1_ec_bytes(Av1Args A) {
+    __shared__ uint32_t wg_s[4], wp_s[4];
+    __shared__ int off_s, carry_s;
+    const int t = blockIdx.x, tid = threadIdx.x, l = lane(), w = tid >> 6;
+    const int tiles = A.geo.tile_cols * A.geo.tile_rows;
+    const int D = A.tile_bits[t];
     if (tid == 0) {
         int off = 0;
-        for (int k = 0; k < t; k++) off += sk_max(A.tile_size[k], 0);
-        n_s = A.tile_size[t];
+        for (int k = 0; k < t; k++) {
+            const int dk = A.tile_bits[k];
+            off += dk < 0 ? 0 : (dk + 8) >> 3;
+        }
+        const int n = D < 0 ? -1 : (D + 8) >> 3;
+        A.tile_size[t] = n;
+        A.out_size_host[t] = (n >= 0 && off + n <= A.out_cap) ? n : -1;
         off_s = off;
         carry_s = 0;
-        A.out_size_host[t] = (n_s >= 0 && off + n_s <= A.out_cap) ? n_s : -1;
     }
     __syncthreads();
-    const int n = n_s, off = off_s;
-    if (n < 0 || off + n > A.out_cap) return;
-    const uint16_t* ch = A.chunks + (size_t)t * A.tile_cap;
-    for (int w1 = n; w1 > 0; w1 -= kWin) {   // window [w0, w1)
-        const int w0 = sk_max(w1 - kWin, 0), wn = w1 - w0;
-        for (int i = tid; i < wn; i += 256) win[i] = ch[w0 + i];
-        __syncthreads();
-        const int s0 = tid * kSeg, s1 = sk_min(s0 + kSeg, wn);
-        for (int ci = 0; ci < 3; ci++) {
-            uint32_t c = (uint32_t)ci;
-            for (int i = s1 - 1; i >= s0; i--) c = (c + win[i]) >> 8;
-            cout_s[tid][ci] = (uint8_t)c;
+    const int off = off_s;
+    if (D < 0 || off + ((D + 8) >> 3) > A.out_cap) return;
+    (void)tiles;
+    const unsigned long long* V = A.ecv + (size_t)t * A.ec_vcap;
+    uint32_t* F = A.ecf + (size_t)t * A.ec_vcap;
+    const int nwords = (D >> 5) + 3, N = (D + 8) >> 3;
+    // a_k = lo(V_k) + hi(V_k-1) (+ 0x3fff rounding at k = 0) < 2^33; b_k = lo(a_k) + hi(a_k-1) <= 2^32
+    auto a_of = [&](int k) -> unsigned long long {
+        if (k < 0) return 0ull;
+        return (V[k] & 0xffffffffull) + (k ? V[k - 1] >> 32 : 0ull) + (k == 0 ? 0x3fffull : 0ull);
+    };
+    for (int w0 = 0; w0 < nwords; w0 += 1024) {
+        unsigned long long bk[4];
+        uint32_t G = 0, P = 1;   // carry generate / propagate over this thread's 4 words
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int k = w0 + 4 * tid + q;
+            bk[q] = k < nwords ? (a_of(k) & 0xffffffffull) + (a_of(k - 1) >> 32) : 0ull;
+            const uint32_t g = (uint32_t)(bk[q] >> 32), p = bk[q] == 0xffffffffull;
+            G = g | (p & G);
+            P = P & p;
         }
-        __syncthreads();
-        if (tid == 0) {
-            int c = carry_s;
-            for (int sg = 255; sg >= 0; sg--) {
-                cin_s[sg] = (uint8_t)c;
-                if (sg * kSeg < wn) c = cout_s[sg][c];
+        // exclusive scan of (G, P) over the workgroup, lower words first
+        uint32_t eg = G, ep = P;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t ug = __shfl_up(eg, o), up = __shfl_up(ep, o);
+            if (l >= o) {
+                eg = eg | (ep & ug);
+                ep = ep & up;
             }
-            carry_s = c;
+        }
+        if (l == 63) {
+            wg_s[w] = eg;
+            wp_s[w] = ep;
         }
         __syncthreads();
-        uint32_t c = cin_s[tid];
-        for (int i = s1 - 1; i >= s0; i--) {
-            c += win[i];
-            A.out_host[off + w0 + i] = (uint8_t)(c & 0xff);
-            c >>= 8;
+        uint32_t c = carry_s;   // carry into wave w's first word
+        for (int k = 0; k < w; k++) c = wg_s[k] | (wp_s[k] & c);
+        {   // into this thread: the inclusive scan of the lanes below
+            const uint32_t pg = __shfl_up(eg, 1), pp = __shfl_up(ep, 1);
+            if (l > 0) c = pg | (pp & c);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int k = w0 + 4 * tid + q;
+            if (k < nwords) F[k] = (uint32_t)(bk[q] + c);
+            c = (uint32_t)((bk[q] + c) >> 32);
         }
         __syncthreads();
+        if (tid == 255) carry_s = c;
+        __syncthreads();
+    }
+    if (tid == 0) F[0] = (F[0] & ~0x3fffu) | 0x4000u;
+    __syncthreads();
+    uint8_t* out = A.out_host + off;
+    for (int j = tid; j < N; j += 256) {
+        const int p = D + 7 - 8 * j, k = p >> 5;
+        const unsigned long long v = (unsigned long long)F[k] | ((unsigned long long)(k + 1 < nwords ? F[k + 1] : 0u) << 32);
+        out[j] = (uint8_t)(v >> (p & 31));
     }
 }
 
@@ -1032,6 +1167,18 @@ __global__ __launch_bounds__(256) void k_av1_finish(Av1Args A) {
         }
 }
 
+static void launch_ec(const Av1Args& a, int tiles, hipStream_t s) {
+    hipLaunchKernelGGL(k_av1_ec_map, dim3(kEcGrid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_ec_link, dim3(tiles), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_av1_ec_emit, dim3(kEcGrid), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_av1_ec_bytes, dim3(tiles), dim3(256), 0, s, a);
+}
+
+void ec_buffers(int tiles, int tile_bytes, int* max_blocks, int* vcap) {
+    *max_blocks = 16384 + tiles;
+    *vcap = tile_bytes / 4 + 8;
+}
+
 void launch_backend(const Av1Args& a, hipStream_t s) {
     const int n = a.f.mb_w * a.f.mb_h;
     const int tiles = a.geo.tile_cols * a.geo.tile_rows;
@@ -1045,8 +1192,7 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_av1_tok_scan, dim3(tiles), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_tok_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_cdf, dim3(tiles * kEcParts), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, s, a);
+    launch_ec(a, tiles, s);
     for (int p = 0; p < 3; p++) {   // in-loop deblocking of the reconstruction, plane by plane
         const int ss = p ? 1 : 0;
         const int cnt = ((a.geo.mi_cols + ss) >> ss) * ((a.geo.mi_rows + ss) >> ss);
@@ -1066,7 +1212,7 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
 }  // namespace av1
 }  // namespace sk
 
-// Test entry: k_av1_cdf + k_av1_ec + k_av1_pack over caller token streams (tile t:
+// Test entry: k_av1_cdf + the k_av1_ec_* coder over caller token streams (tile t:
 // tok[offs[t], offs[t] + ns[t])) with the default CDFs of qidx; out receives tile t's
 // bytes at the prefix of sizes, words (optional) the interval words of k_av1_cdf.
 // Returns 0, or -1 on a HIP error.
@@ -1082,16 +1228,21 @@ extern "C" int sk_av1_ec_tokens_hip(const uint32_t* tok, const int32_t* offs, co
     a.tile_tok_cap = maxn;
     a.tile_cap = 8 * maxn + 64;
     a.out_cap = out_cap;
+    ec_buffers(tiles, a.tile_cap, &a.ec_max_blocks, &a.ec_vcap);
     std::vector<uint32_t> tc((size_t)tiles * maxn, 0u);
     for (int t = 0; t < tiles; t++) memcpy(&tc[(size_t)t * maxn], tok + offs[t], sizeof(uint32_t) * ns[t]);
     int frame[2] = {0, qidx};
-    bool ok = true;
+    bool ok = tiles <= 64;
     auto chk = [&](hipError_t e) { ok = ok && e == hipSuccess; };
     chk(hipMalloc(&a.tokc, tc.size() * 4));
     chk(hipMalloc(&a.pw, (tc.size() + (size_t)tiles * kEcParts * 64) * 4));
     chk(hipMalloc(&a.tile_ntok, tiles * 4));
     chk(hipMalloc(&a.frame, 8));
-    chk(hipMalloc(&a.chunks, (size_t)tiles * a.tile_cap * 2));
+    chk(hipMalloc(&a.ecmap, (size_t)a.ec_max_blocks * 128 * sizeof(uint2)));
+    chk(hipMalloc(&a.ecblk, (size_t)a.ec_max_blocks * sizeof(int4)));
+    chk(hipMalloc(&a.ecv, (size_t)tiles * a.ec_vcap * 8));
+    chk(hipMalloc(&a.ecf, (size_t)tiles * a.ec_vcap * 4));
+    chk(hipMalloc(&a.tile_bits, tiles * 4));
     chk(hipMalloc(&a.tile_size, tiles * 4));
     chk(hipMalloc(&a.out_host, out_cap));
     chk(hipMalloc(&a.out_size_host, tiles * 4));
@@ -1100,8 +1251,7 @@ extern "C" int sk_av1_ec_tokens_hip(const uint32_t* tok, const int32_t* offs, co
         chk(hipMemcpy(a.tile_ntok, ns, tiles * 4, hipMemcpyHostToDevice));
         chk(hipMemcpy(a.frame, frame, 8, hipMemcpyHostToDevice));
         hipLaunchKernelGGL(k_av1_cdf, dim3(tiles * kEcParts), dim3(64), 0, 0, a);
-        hipLaunchKernelGGL(k_av1_ec, dim3(tiles), dim3(64), 0, 0, a);
-        hipLaunchKernelGGL(k_av1_pack, dim3(tiles), dim3(256), 0, 0, a);
+        launch_ec(a, tiles, 0);
         chk(hipGetLastError());
         chk(hipDeviceSynchronize());
         chk(hipMemcpy(sizes, a.out_size_host, tiles * 4, hipMemcpyDeviceToHost));
@@ -1112,14 +1262,10 @@ extern "C" int sk_av1_ec_tokens_hip(const uint32_t* tok, const int32_t* offs, co
             for (int t = 0; t < tiles; t++) memcpy(words + offs[t], &w[(size_t)t * maxn], sizeof(uint32_t) * ns[t]);
         }
     }
-    (void)hipFree(a.tokc);
-    (void)hipFree(a.pw);
-    (void)hipFree(a.tile_ntok);
-    (void)hipFree(a.frame);
-    (void)hipFree(a.chunks);
-    (void)hipFree(a.tile_size);
-    (void)hipFree(a.out_host);
-    (void)hipFree(a.out_size_host);
+    for (void* p : {(void*)a.tokc, (void*)a.pw, (void*)a.tile_ntok, (void*)a.frame, (void*)a.ecmap, (void*)a.ecblk,
+                    (void*)a.ecv, (void*)a.ecf, (void*)a.tile_bits, (void*)a.tile_size, (void*)a.out_host,
+                    (void*)a.out_size_host})
+        (void)hipFree(p);
     return ok ? 0 : -1;
 }
 

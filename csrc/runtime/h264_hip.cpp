@@ -734,7 +734,7 @@ class HipBackend : public EncoderBackend {
     }
 
     // AV1 back-end buffers (av1_gpu.h): cells, levels, level contexts, token slots per
-    // 16x16 unit, coder chunks per tile, host-mapped frame info and tile bytes.
+    // 16x16 unit, block-parallel coder state per tile, host-mapped frame info and tile bytes.
     void alloc_av1() {
         const int n = g_.num_mbs();
         av1::gpu::Av1Args& a = aargs_;
@@ -758,7 +758,7 @@ class HipBackend : public EncoderBackend {
         a.cdef_in.u = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
         a.cdef_in.v = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
         const int tiles = av1_geo_.tile_cols * av1_geo_.tile_rows;
-        // coder chunks: 4 KB per unit of the largest tile (incompressible content codes
+        // tile bytes: 4 KB per unit of the largest tile (incompressible content codes
         // below ~1.5 bytes per sample)
         const int tile_units = (av1_geo_.tile_w_sb * 4) * (av1_geo_.tile_h_sb * 4);
         a.tile_tok_cap = tile_units * av1::gpu::kTokCap;
@@ -768,7 +768,13 @@ class HipBackend : public EncoderBackend {
         a.tok_off = dmalloc<int>(n);
         a.tile_ntok = dmalloc<int>(tiles);
         a.tile_cap = tile_units * 4096;
-        a.chunks = dmalloc<uint16_t>((size_t)tiles * a.tile_cap, false);
+        if (tiles > 64) throw std::runtime_error("AV1: at most 64 tiles");
+        av1::gpu::ec_buffers(tiles, a.tile_cap, &a.ec_max_blocks, &a.ec_vcap);
+        a.ecmap = dmalloc<uint2>((size_t)a.ec_max_blocks * 128, false);
+        a.ecblk = dmalloc<int4>((size_t)a.ec_max_blocks, false);
+        a.ecv = dmalloc<unsigned long long>((size_t)tiles * a.ec_vcap, false);
+        a.ecf = dmalloc<uint32_t>((size_t)tiles * a.ec_vcap, false);
+        a.tile_bits = dmalloc<int>(tiles);
         a.tile_size = dmalloc<int>(tiles);
         a.out_cap = g_.W * g_.H * 3 + 4096;
         std::vector<uint8_t> q(52);

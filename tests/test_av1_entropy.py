@@ -120,6 +120,10 @@ def _token_streams(L, seed, tiles):
     part = [f for f in fields if f[1] == 10][0]          # partition_w16
     streams = []
     for t in range(tiles):
+        if t == 1:   # one context, symbol 0 almost always: long runs without a resetting token
+            off, ns, cnt, st = [f for f in fields if f[1] == 2][0]
+            streams.append([((ns - 1) << 26) | ((1 if rng.random() < 3e-4 else 0) << 22) | off for _ in range(20000)])
+            continue
         n = 12000 if t == 0 else int(rng.integers(0, 3000))
         picks = [fields[int(rng.integers(len(fields)))] for _ in range(6)]
         ctxs = [(off + int(rng.integers(cnt)) * st, ns) for off, ns, cnt, st in picks]
@@ -159,7 +163,8 @@ def test_token_replay_cpu():
 
 @pytest.mark.gpu
 def test_gpu_tiles_match_host_encoder():
-    """k_av1_ec + k_av1_pack (csrc/kernels/av1_kernels.hip) on synthetic token streams:
+    """k_av1_cdf + the block-parallel coder k_av1_ec_* (csrc/kernels/av1_kernels.hip) on
+    synthetic token streams (a literal-heavy tile, a tile of long non-resetting runs, empty tiles):
     every tile byte-identical to the host replay through SymbolCoder (av1_ec.h)."""
     from selkies_gstreamer_amd.ops.native import hip_device_count
     if hip_device_count() < 1:
