@@ -359,6 +359,14 @@ SK_HD int quantize(int32_t c, int q, bool intra) {
 }
 // qindex -> coefficient CDF context (§7.20: <= 20, <= 60, <= 120, else)
 SK_HD int coef_qctx(int qidx) { return qidx <= 20 ? 0 : (qidx <= 60 ? 1 : (qidx <= 120 ? 2 : 3)); }
+// Frame qindex of a rate-controlled frame at fractional QP qpf (Q8, ratecontrol.h):
+// AV1 has ~5 qindex steps per H.264 QP at the top of its range, so the fraction is
+// realised in the frame's qindex (tab: qindex of each integer QP 0..51).
+SK_HD int frame_qidx(const uint8_t* tab, int qpf) {
+    const int lo = sk_clip(qpf >> 8, 0, 51), f = qpf & 255;
+    if (lo >= 51) return tab[51];
+    return tab[lo] + (((int)tab[lo + 1] - (int)tab[lo]) * f + 128) / 256;
+}
 
 // ---------------------------------------------------------------------------------
 // Scans: the default (zig-zag) scan of an n x n DCT_DCT block, scan index -> raster position.

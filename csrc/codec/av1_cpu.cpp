@@ -532,6 +532,8 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
         if (t.action == ACT_P) {
             fe.motion_search(s);
             fe.decide_scenecut(s);
+        } else if (t.action == ACT_I) {
+            fe.intra_activity(s);
         }
         key |= t.final_action == ACT_I;
     }
@@ -539,7 +541,12 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
         for (int s = 0; s < ns; s++) fe.tasks[s].final_action = ACT_I;
     fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     fp.key = key;
-    fp.qidx = qidx_for_qp(fe.tasks[0].qp);
+    {   // K10: the frame's fractional QP under CRF / CBR (k_av1_setup: same rule)
+        uint8_t tab[52];
+        for (int q = 0; q < 52; q++) tab[q] = (uint8_t)qidx_for_qp(q);
+        const h264::RcState& rc = fe.ctl_.rc();
+        fp.qidx = rc.mode == h264::RC_CQP ? tab[sk_clip(fe.tasks[0].qp, 0, 51)] : frame_qidx(tab, rc.cur_qpf);
+    }
     fp.lf_level = lf_level_for(ac_q(fp.qidx), key);
     std::fill(blk.begin(), blk.end(), BlkInfo{});
     if (key) {

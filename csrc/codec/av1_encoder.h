@@ -60,6 +60,16 @@ int qidx_for_qp(int qp);
 int intra_mode_decision(const uint8_t* src, int stride, int x, int y, int log2n, bool au, bool al, int max_x,
                         int max_y);
 
+// CBR as svtav1enc runs in the reference (legacy/gstwebrtc_app.py:733-739): rc=2 with
+// buf-optimal-sz=120 ms, intra-period -1 and no scene-change key frames (a cut is coded
+// as an inter frame: a key frame costs several budgets and starves the frames after it).
+// Applied by sk_api's to_config for every back end.
+inline void cbr_config(h264::EncoderConfig& f) {
+    if (f.rc_mode != h264::RC_CBR) return;
+    if (f.vbv_ms <= 0) f.vbv_ms = 120;
+    f.scenecut = 0;
+}
+
 inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
     h264::EncoderConfig f = c;
     f.fullframe = 1;
@@ -67,6 +77,7 @@ inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
     f.num_refs = 1;
     f.subpel = 0;
     f.use_paint_over = 0;   // a paint-over would force key frames; static regions stay at the session QP
+    cbr_config(f);
     return f;
 }
 

@@ -24,14 +24,14 @@ void Controller::init(const EncoderConfig& cfg, const Geometry& g) {
     g_ = g;
     st_.assign(g.num_slices, StripeState());
     pic_ = StripeState();
-    rc_init(rc_, cfg.rc_mode, cfg.qp, cfg.bitrate_kbps, cfg.fps, cfg.width * cfg.height);
+    rc_init(rc_, cfg.rc_mode, cfg.qp, cfg.bitrate_kbps, cfg.fps, cfg.width * cfg.height, cfg.vbv_ms);
 }
 
 void Controller::rate_control(SliceTask* tasks, const MeResult* me) {
     const int ns = g_.num_slices;
     std::vector<long long> sad(ns, 0), dev(ns, 0);
     for (int s = 0; s < ns; s++) {
-        if (tasks[s].action != ACT_P) continue;
+        if (tasks[s].action != ACT_P && tasks[s].action != ACT_I) continue;   // planned I: activity only
         for (int j = tasks[s].first_row * g_.mb_w; j < (tasks[s].first_row + tasks[s].num_rows) * g_.mb_w; j++) {
             sad[s] += me[j].sad;
             dev[s] += me[j].intra_est;

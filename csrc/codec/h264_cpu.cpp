@@ -174,9 +174,28 @@ void CpuH264Encoder::full_search(int mbx, int mby, const SliceTask& t, int16_t* 
     out[1] = (int16_t)fs_key_dy(best);
 }
 
+// sum |Y - mean| of the source MB (k_motion_search mb_activity)
+int CpuH264Encoder::mb_activity(int mbx, int mby) const {
+    int sum = 0;
+    for (int y = 0; y < 16; y++)
+        for (int x = 0; x < 16; x++) sum += src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x];
+    const int mean = (sum + 128) >> 8;
+    int dev = 0;
+    for (int y = 0; y < 16; y++)
+        for (int x = 0; x < 16; x++) dev += sk_abs((int)src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x] - mean);
+    return dev;
+}
+
+// Planned intra slice: the activity of every MB (K10's key-frame complexity), no search.
+void CpuH264Encoder::intra_activity(int s) {
+    const SliceTask& t = tasks[s];
+    for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) me[(size_t)mby * g.mb_w + mbx] = MeResult{0, 0, 0, mb_activity(mbx, mby), 0, 0, 0};
+}
+
 void CpuH264Encoder::motion_search(int s) {
     const SliceTask& t = tasks[s];
-    const int lam = lambda_for_qp(t.qp);
+    const int lam = lambda_for_qp(rc_me_qp(ctl_.rc(), t.qp));
     const int R = cfg.me_range;
     auto cost_of = [&](int mbx, int mby, int dx, int dy, int* sad_out) {
         int sad = sad_at(mbx, mby, dx, dy, t);
@@ -233,13 +252,7 @@ void CpuH264Encoder::motion_search(int s) {
                 if (nb < 0) break;
                 bx += ddx[nb]; by += ddy[nb]; bcost = ncost; bsad = nsad;
             }
-            int sum = 0;
-            for (int y = 0; y < 16; y++)
-                for (int x = 0; x < 16; x++) sum += src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x];
-            int mean = (sum + 128) >> 8, dev = 0;
-            for (int y = 0; y < 16; y++)
-                for (int x = 0; x < 16; x++)
-                    dev += sk_abs((int)src[0][(size_t)(mby * 16 + y) * g.stride_y + mbx * 16 + x] - mean);
+            const int dev = mb_activity(mbx, mby);
             int refi = 0;
             if (t.num_refs > 1 && mb_dirty[idx]) {
                 // second reference at the zero vector (a window or caret returning to the
@@ -798,6 +811,8 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         if (tasks[s].action == ACT_P) {
             motion_search(s);
             decide_scenecut(s);
+        } else if (tasks[s].action == ACT_I) {
+            intra_activity(s);
         }
     ctl_.rate_control(tasks.data(), me.data());   // K10 (ratecontrol.h)
     std::vector<std::vector<uint8_t>> rbsp(g.num_slices);

@@ -50,6 +50,7 @@ struct EncoderConfig {
     int tile_rows_log2 = -1;
     int rc_mode = RC_CQP;        // K10 rate control (ratecontrol.h): CQP, CRF (qp = CRF value), CBR
     int bitrate_kbps = 0;        // CBR target
+    int vbv_ms = 0;              // CBR buffer (ratecontrol.h rc_init): 0 = 1.5 frame intervals
     int aq_strength = 0;         // MB-level adaptive QP strength, Q4 (16 = 1.0; 0 = off): h264_mb.h aq_offset
     int subpel = 1;              // quarter-pel refinement of P vectors (K4c, H.264 and HEVC); AV1 keeps integer vectors
     int intra4x4 = 0;            // H.264 I slices may code MBs as I_NxN (nine 4x4 modes) where cheaper; off
@@ -243,7 +244,7 @@ SK_HD void rc_apply(RcState& rc, SliceTask* tasks, const long long* sad, const l
         } else {
             ni += mbs;
             if (t.action == ACT_I) nidr += mbs;   // planned key frame (IDR), not a scene cut
-            if (t.action == ACT_P) {
+            {   // scene cut (ME's intra estimate) or planned key frame (MB activity, no search)
                 ci += dev[(size_t)s * stride];
                 ni_known += mbs;
             }
@@ -251,10 +252,10 @@ SK_HD void rc_apply(RcState& rc, SliceTask* tasks, const long long* sad, const l
     }
     if (np + ni == 0) return;
     const bool intra = ni > np;
-    const int qp = intra ? rc_frame_qp(rc, ci, ni_known, true, nidr * 2 > ni, np + ni)
-                         : rc_frame_qp(rc, cp, np, false, false, np + ni);
-    for (int s = 0; s < ns; s++)
-        if (rc_slice_adjustable(tasks[s], plan_qp, rc.mode)) tasks[s].qp = qp;
+    const int qpf = intra ? rc_frame_qpf(rc, ci, ni_known, true, nidr * 2 > ni, np + ni)
+                          : rc_frame_qpf(rc, cp, np, false, false, np + ni);
+    for (int s = 0, i = 0; s < ns; s++)
+        if (rc_slice_adjustable(tasks[s], plan_qp, rc.mode)) tasks[s].qp = rc_dither_qp(qpf, i++);
 }
 
 // K10 CBR guard on a coded frame of `frame_bits` payload bits: when it overflows the
@@ -263,16 +264,20 @@ SK_HD void rc_apply(RcState& rc, SliceTask* tasks, const long long* sad, const l
 SK_HD int rc_redo(RcState& rc, SliceTask* tasks, int ns, long long frame_bits) {
     const int step = rc_redo_step(rc, frame_bits);
     if (!step) return 0;
-    const int q0 = rc.cur_qp, q1 = rc_clamp_qp(rc, q0 + step);
+    const int f0 = rc.cur_qpf, f1 = sk_min(f0 + (step << 8), rc.qp_max << 8);
     rc_raise_floor(rc);
-    if (q1 == q0) return 0;
+    if (f1 == f0) return 0;
+    // the frame's slices sit at the two QPs of its dither (rc_dither_qp)
+    const int lo = f0 >> 8, hi = (f0 + 255) >> 8;
     for (int s = 0; s < ns; s++) {
         SliceTask& t = tasks[s];
-        if ((t.final_action == ACT_P || t.final_action == ACT_I) && t.qp == q0) t.qp = q1;
+        if ((t.final_action == ACT_P || t.final_action == ACT_I) && (t.qp == lo || t.qp == hi))
+            t.qp = rc_clamp_qp(rc, t.qp + step);
     }
-    rc.cur_qp = q1;
+    rc.cur_qpf = f1;
+    rc.cur_qp = (f1 + 128) >> 8;
     rc.redos++;
-    return q1 - q0;
+    return (f1 - f0 + 255) >> 8;
 }
 
 // Decides, per stripe, what to encode this frame.
@@ -288,10 +293,11 @@ class Controller {
     // K10: mode (RC_CQP / RC_CRF / RC_CBR) and CBR bitrate from the next frame on.
     void set_rate(int mode, int kbps) {
         const RcState old = rc_;
-        rc_init(rc_, mode, cfg_.qp, kbps, cfg_.fps, cfg_.width * cfg_.height);
+        rc_init(rc_, mode, cfg_.qp, kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms);
         if (old.mode == mode) {   // keep the model; a new budget recentres the buffer
             for (int k = 0; k < 2; k++) {
                 rc_.last_qp[k] = old.last_qp[k];
+                rc_.last_qpf[k] = old.last_qpf[k];
                 rc_.last_bits[k] = old.last_bits[k];
                 rc_.last_cplx[k] = old.last_cplx[k];
             }

@@ -58,6 +58,8 @@ class CpuH264Encoder {
     // ---- stages (public for tests) ----
     void load_frame(const uint8_t* bgrx, int stride_bytes);  // K1 + K3
     void motion_search(int s);                              // K4 for slice s
+    void intra_activity(int s);                             // planned intra slice: MB activity only
+    int mb_activity(int mbx, int mby) const;
     void subpel_refine(int s);                              // K4c: half + quarter-pel refinement
     void decide_scenecut(int s);
     void compute_aq(int s);                                 // AQ offsets of slice s's MBs

@@ -473,6 +473,8 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
         if (fe.tasks[s].action == ACT_P) {
             fe.motion_search(s);
             fe.decide_scenecut(s);
+        } else if (fe.tasks[s].action == ACT_I) {
+            fe.intra_activity(s);
         }
     fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     for (int s = 0; s < ns; s++) {

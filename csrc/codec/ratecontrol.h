@@ -42,12 +42,15 @@ struct RcState {
     int32_t pixels;          // luma samples per frame
     int32_t cur_idr;         // the frame in flight is a planned key frame
     int32_t redos;           // statistics: frames coded twice by the CBR guard
-    int32_t qp_floor;        // CBR: inter QP below which a frame overflowed recently (0: none)
-    int32_t floor_age;       // frames since the floor last moved (it decays 1 QP per 8 frames)
+    int32_t qp_floor;        // CBR: inter QP (Q8) at which a frame overflowed recently (0: none)
+    int32_t floor_age;       // frames since the floor last moved (it decays 1 QP per 16 frames)
     int32_t last_mbs[2];     // rate-controlled macroblocks of the model frames
     int32_t cur_mbs;         // ... of the frame in flight
+    int32_t vbv_ms;          // CBR buffer in ms (0: 1.5 frame intervals), kept across set_rate()
+    int32_t last_qpf[2];     // fractional QP (Q8) of the model frames
+    int32_t cur_qpf;         // ... of the frame in flight: slices dither between its two QPs
 };
-static_assert(sizeof(RcState) == 116, "RcState layout");
+static_assert(sizeof(RcState) == 132, "RcState layout");
 
 SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x <= 1
     if (x <= 1) return 0;
@@ -56,8 +59,12 @@ SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x
     return m * 256 + (int)frac;
 }
 
-SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float fps, int pixels) {
+// vbv_ms: the CBR buffer. 0 = 1.5 frame intervals, the reference's low-latency
+// setting for its H.264 / H.265 encoders (legacy/gstwebrtc_app.py:100-104); AV1
+// passes 120 ms, svtav1enc's buf-optimal-sz (gstwebrtc_app.py:738).
+SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float fps, int pixels, int vbv_ms = 0) {
     rc = RcState{};
+    rc.vbv_ms = vbv_ms;
     rc.pixels = pixels;
     rc.mode = mode;
     rc.base_qp = base_qp;
@@ -65,29 +72,44 @@ SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float f
     rc.qp_max = 51;
     const double f = fps > 0 ? fps : 60.0;
     rc.budget = (int32_t)(bitrate_kbps * 1000.0 / f);
-    rc.vbv_size = rc.budget + rc.budget / 2;   // 1.5 frame intervals
+    const long long vbv = vbv_ms > 0 ? (long long)bitrate_kbps * vbv_ms : 0;   // bits
+    rc.vbv_size = vbv > rc.budget + rc.budget / 2 ? (int32_t)(vbv > (1ll << 30) ? (1ll << 30) : vbv)
+                                                  : rc.budget + rc.budget / 2;   // >= 1.5 frame intervals
     rc.fullness = rc.vbv_size / 2;
     rc.last_qp[0] = rc.last_qp[1] = base_qp;
+    rc.last_qpf[0] = rc.last_qpf[1] = rc.cur_qpf = base_qp << 8;
 }
 
 SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, rc.qp_max); }
 
-// QP of the frame about to be coded. cplx_sum: sum of the complexity measure over
-// coded_mbs measured MBs (ME SAD for inter frames, source activity for intra);
+// QP whose lambda prices motion vectors in the motion search, which runs before the
+// frame's QP is chosen: under CRF / CBR the QP of the last rate-controlled inter frame
+// (the search at the configured QP picks ragged, expensive vectors when the
+// controller runs far coarser), else the planned QP.
+SK_HD int rc_me_qp(const RcState& rc, int plan_qp) {
+    return (rc.mode != RC_CQP && rc.last_bits[0] > 0) ? rc.last_qp[0] : plan_qp;
+}
+
+// QP of the frame about to be coded, fractional (Q8, also left in rc.cur_qpf): the
+// slices dither between its two integer QPs (rc_dither_qp), because screen content
+// has cliffs - sharp text at one contrast crosses the dead zone within one QP (1080p
+// synthetic desktop, H.264: 0.35 budgets at QP 44, above 1.4 at QP 43) - and a
+// whole-frame QP then cannot use the budget. cplx_sum: sum of the complexity measure
+// over coded_mbs measured MBs (ME SAD for inter frames, source activity for intra);
 // mbs: all rate-controlled MBs of the frame (the model scales with their number:
 // striped sessions code only the stripes that changed).
-SK_HD int rc_frame_qp(RcState& rc, long long cplx_sum, int coded_mbs, bool intra, bool idr = false, int mbs = 0) {
+SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intra, bool idr = false, int mbs = 0) {
     const int k = intra ? 1 : 0;
     long long c64 = coded_mbs > 0 ? (cplx_sum * 16) / coded_mbs : 0;
     int cplx = (int)(c64 > (1 << 28) ? (1 << 28) : c64);
     const bool known = cplx > 0;   // planned key frames have no motion search: complexity unknown
-    int qp = rc.base_qp;
+    int qp = rc.base_qp << 8;
     if (rc.mode == RC_CRF) {
         if (!intra) {
             if (rc.cplx_ema > 0) {
                 const int d = rc_ilog2_q8((uint32_t)cplx) - rc_ilog2_q8((uint32_t)rc.cplx_ema);   // Q8
                 const int off = (d * 24 + (d >= 0 ? 1280 : -1280)) / 2560;   // round(2.4 * d / 256)
-                qp = rc.base_qp + sk_clip(off, -3, 6);
+                qp = (rc.base_qp + sk_clip(off, -3, 6)) << 8;
             }
             rc.cplx_ema = rc.cplx_ema > 0 ? rc.cplx_ema + (cplx - rc.cplx_ema) / 8 : cplx;
         }
@@ -108,29 +130,50 @@ SK_HD int rc_frame_qp(RcState& rc, long long cplx_sum, int coded_mbs, bool intra
             const int dm = (mbs > 0 && rc.last_mbs[k] > 0)   // coded area ratio
                                ? rc_ilog2_q8((uint32_t)mbs) - rc_ilog2_q8((uint32_t)rc.last_mbs[k]) : 0;
             const int d = rc_ilog2_q8((uint32_t)rc.last_bits[k]) + dc + dm - rc_ilog2_q8((uint32_t)target);
-            const int dq = d >= 0 ? (6 * d + 128) / 256 : -((-5 * d + 128) / 256);
-            qp = rc.last_qp[k] + sk_clip(dq, -2, intra ? 16 : 10);
-            // screen content can jump several-fold within 2 QP (glyph edges crossing the
+            // a long buffer (AV1, vbv_ms) absorbs a misprediction, so its inter frames move
+            // gently: 3 QP per halving and at most a quarter QP finer per frame. At the top
+            // of AV1's quantiser range an inter frame's size doubles every ~2-3 QP (it
+            // re-codes what the coarser frames before it lost): larger steps oscillate
+            const bool gentle = rc.vbv_ms > 0 && !intra;
+            const int dq = gentle ? 3 * d : (d >= 0 ? 6 * d : 5 * d);   // Q8 QP
+            qp = rc.last_qpf[k] + sk_clip(dq, gentle ? -64 : -512, (intra ? 16 : 10) << 8);
+            // screen content can jump several-fold within one QP (glyph edges crossing the
             // dead zone together): stay above the QP that last overflowed the buffer
             if (!intra && rc.qp_floor > qp) qp = rc.qp_floor;
+        } else if (intra && known) {
+            // no intra model yet, the activity measured (sum |Y - mean| per MB): about
+            // 0.049 bits per unit of activity at QP 39 (dense synthetic text, H.264 and
+            // AV1 alike), 5 QP per halving
+            const long long tb = ((long long)target << 10) / sk_max(mbs > 0 ? mbs : coded_mbs, 1);   // bits/MB x1024
+            const uint32_t est = (uint32_t)sk_min((long long)cplx * 3 + cplx / 8, (long long)1 << 30);   // (0.049 / 16) x1024
+            const int d = rc_ilog2_q8(sk_max(est, 2u)) - rc_ilog2_q8((uint32_t)sk_min(sk_max(tb, 2ll), 1ll << 30));
+            qp = (39 << 8) + 5 * d;
         } else if (intra) {
-            // no intra model yet: start from the bits per pixel the budget allows
-            // (~0.6 bpp at QP 25 for desktop content, 6 QP per halving)
+            // no intra model and no activity: start from the bits per pixel the budget
+            // allows (~0.6 bpp at QP 25 for desktop content, 6 QP per halving)
             const int bpp_q8 = (int)(((long long)target * 256) / sk_max(rc.pixels, 1));   // target bpp x256
             const int d = rc_ilog2_q8(154) - rc_ilog2_q8((uint32_t)sk_max(bpp_q8, 1));  // log2(0.6 / bpp)
-            qp = 25 + (6 * d + (d >= 0 ? 128 : -128)) / 256;
+            qp = ((25 << 8) + 6 * d + 128) & ~255;
         } else {
-            qp = rc.last_qp[1] + 2;   // first inter frame: a little coarser than the key frame
+            qp = rc.last_qpf[1] + 512;   // first inter frame: a little coarser than the key frame
         }
     }
-    qp = rc_clamp_qp(rc, qp);
-    rc.cur_qp = qp;
+    qp = sk_clip(qp, rc.qp_min << 8, rc.qp_max << 8);
+    rc.cur_qpf = qp;
+    rc.cur_qp = (qp + 128) >> 8;
     rc.cur_intra = intra;
     rc.cur_cplx = known ? cplx : 0;   // 0: not measured
     rc.cur_valid = 1;
     rc.cur_idr = idr ? 1 : 0;
     rc.cur_mbs = mbs;
     return qp;
+}
+
+// Integer QP of the i-th rate-controlled slice of a frame at fractional QP qpf: an
+// error-diffusion dither, so a fraction f of the slices runs at the coarser QP.
+SK_HD int rc_dither_qp(int qpf, int i) {
+    const int lo = qpf >> 8, f = qpf & 255;
+    return lo + ((((i + 1) * f + 128) >> 8) - ((i * f + 128) >> 8));
 }
 
 // CBR guard (VBV overflow): a frame whose payload exceeds the buffer (1.5 budgets;
@@ -154,7 +197,8 @@ SK_HD void rc_raise_floor(RcState& rc) {
     // a burst (complexity well above the last inter frame's) overflows at any QP the
     // buffer allows for ordinary frames: re-code it, but keep the floor where it is
     if (rc.cur_cplx > 0 && rc.last_cplx[0] > 0 && 2 * (long long)rc.cur_cplx > 3 * (long long)rc.last_cplx[0]) return;
-    rc.qp_floor = sk_max(rc.qp_floor, rc.cur_qp + 1);
+    // a quarter QP above the QP that overflowed: the dither reaches the cliff's edge
+    rc.qp_floor = sk_max(rc.qp_floor, rc.cur_qpf + 64);
     rc.floor_age = 0;
 }
 
@@ -165,6 +209,7 @@ SK_HD void rc_account(RcState& rc, long long frame_bits) {
     // frames whose QP the controller did not choose (all static) do not train the model
     if (rc.cur_valid) {   // last_cplx 0: not measured (the next prediction assumes no change)
         rc.last_qp[k] = rc.cur_qp;
+        rc.last_qpf[k] = rc.cur_qpf;
         rc.last_bits[k] = bits > 0 ? bits : 1;
         rc.last_cplx[k] = rc.cur_cplx;
         rc.last_mbs[k] = rc.cur_mbs;
@@ -176,9 +221,9 @@ SK_HD void rc_account(RcState& rc, long long frame_bits) {
         rc.fullness = (int32_t)(f < 0 ? 0 : (f > rc.vbv_size ? rc.vbv_size : f));
     }
     if (rc.cur_valid && !rc.cur_intra && bits > rc.max_p_bits) rc.max_p_bits = bits;
-    if (rc.qp_floor > 0 && ++rc.floor_age >= 8) {   // 7.5 QP a second at 60 fps
-        rc.qp_floor = rc.qp_floor - 1 > rc.qp_min ? rc.qp_floor - 1 : 0;
-        rc.floor_age = 0;
+    if (rc.qp_floor > 0) {   // 1 QP per 16 frames (3.75 QP a second at 60 fps)
+        rc.qp_floor = rc.qp_floor - 16 > (rc.qp_min << 8) ? rc.qp_floor - 16 : 0;
+        rc.floor_age++;
     }
     rc.cur_valid = 0;
     rc.frames++;

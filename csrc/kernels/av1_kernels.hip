@@ -279,7 +279,9 @@ __global__ __launch_bounds__(256) void k_av1_setup(Av1Args A) {
             f.tasks_host[s].final_action = ACT_I;
         }
     if (threadIdx.x == 0) {
-        const int qidx = A.qidx_of_qp[sk_clip(f.tasks[0].qp, 0, 51)];
+        // K10: the frame's fractional QP under CRF / CBR (slices dither on H.264 / HEVC)
+        const int qidx = f.rc->mode == h264::RC_CQP ? A.qidx_of_qp[sk_clip(f.tasks[0].qp, 0, 51)]
+                                                    : frame_qidx(A.qidx_of_qp, f.rc->cur_qpf);
         const int lvl = lf_level_for(ac_q(qidx), key);   // av1_lf.h, the host encoder's choice
         A.frame[0] = key;
         A.frame[1] = qidx;

@@ -366,6 +366,16 @@ __device__ __forceinline__ int win_sad(const uint32_t* win, uint32_t sw, int ox,
     return wave_sum((int)__builtin_amdgcn_sad_u8(sw, rw, 0u));
 }
 
+// sum |Y - mean| of a 16x16 MB, one wave (lane: 4 samples of row l / 4)
+__device__ __forceinline__ int mb_activity(uint32_t sw) {
+    const int psum = (int)(sw & 255) + (int)((sw >> 8) & 255) + (int)((sw >> 16) & 255) + (int)(sw >> 24);
+    const int mean = (wave_sum(psum) + 128) >> 8;
+    int dev = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) dev += sk_abs((int)((sw >> (8 * i)) & 255) - mean);
+    return wave_sum(dev);
+}
+
 __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
     __shared__ uint32_t win[32 * kWinWords];
     int nmb = a.mb_w * a.mb_h;
@@ -374,13 +384,18 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
     int mbx = idx % a.mb_w, mby = idx / a.mb_w;
     int s = mby / a.rows_per_slice;
     const SliceTask t = a.tasks[s];
-    if (t.action != ACT_P) return;
+    if (t.action != ACT_P && t.action != ACT_I) return;
     int l = lane_id();
     int row = l >> 2, col4 = (l & 3) * 4;
     uint32_t sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + row) * a.stride_y +
                                                      mbx * 16 + col4);
+    if (t.action == ACT_I) {   // planned key frame: only the activity (K10's intra complexity)
+        const int dev = mb_activity(sw);
+        if (l == 0) a.me[idx] = MeResult{0, 0, 0, dev, 0, 0, 0};
+        return;
+    }
     int ylo = t.pic_row0 * 16, yhi = (t.pic_row0 + t.pic_rows) * 16 - 1;
-    const int lam = lambda_for_qp(t.qp);
+    const int lam = lambda_for_qp(rc_me_qp(*a.rc, t.qp));
     const int R = a.me_range;
     // candidates (same order as the CPU reference)
     int cx[7], cy[7], n = 0;
@@ -463,13 +478,7 @@ __global__ __launch_bounds__(64) void k_motion_search(FrameArgs a) {
         if (nb < 0) break;
         bx += ddx[nb]; by += ddy[nb]; bcost = ncost; bsad = nsad;
     }
-    // scene-cut intra estimate: sum |Y - mean|
-    int psum = (int)(sw & 255) + (int)((sw >> 8) & 255) + (int)((sw >> 16) & 255) + (int)(sw >> 24);
-    int mean = (wave_sum(psum) + 128) >> 8;
-    int dev = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) dev += sk_abs((int)((sw >> (8 * i)) & 255) - mean);
-    dev = wave_sum(dev);
+    const int dev = mb_activity(sw);   // scene-cut intra estimate
     int refi = 0;
     if (t.num_refs > 1 && a.mb_dirty[idx]) {   // second reference at the zero vector (CPU: same rule)
         const int s1 = me_sad(a, a.ref1.y, sw, mbx, mby, 0, 0, ylo, yhi);
@@ -724,7 +733,7 @@ __global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
     const bool planned_p = t.action == ACT_P;
     const bool p = planned_p && t.allow_scenecut;
     long long sad = 0, dev = 0;
-    if (planned_p) {
+    if (planned_p || t.action == ACT_I) {   // planned key frames: activity only (sad 0)
         const int first = t.first_row * a.mb_w, nmb = t.num_rows * a.mb_w;
         for (int i = threadIdx.x; i < nmb; i += 256) {
             const MeResult r = a.me[first + i];
@@ -764,10 +773,11 @@ __global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
         const int mode = a.key_dev[3];
         const int kbps = a.key_dev[4];
         const RcState old = rc;
-        rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H);
+        rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H, old.vbv_ms);
         if (old.mode == mode)
             for (int k = 0; k < 2; k++) {
                 rc.last_qp[k] = old.last_qp[k];
+                rc.last_qpf[k] = old.last_qpf[k];
                 rc.last_bits[k] = old.last_bits[k];
                 rc.last_cplx[k] = old.last_cplx[k];
             }

@@ -530,7 +530,7 @@ class HipBackend : public EncoderBackend {
         a.fs_mv = dmalloc<int16_t>(2 * nmb);
         {   // K10 rate control state (ratecontrol.h), initialised like the CPU controller's
             RcState rc;
-            rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height);
+            rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms);
             a.rc = dmalloc<RcState>(1);
             copy_now(a.rc, &rc, sizeof(rc));
             a.rc_slice = dmalloc<long long>(2 * (size_t)ns);
