@@ -855,6 +855,30 @@ SK_HD int eob_pt_of(int eob) {
     return l + 2;
 }
 
+// Encoder choice: tail trimming of an inter block's levels (raster lev, n x n). The
+// tokens of a block run to its last nonzero level in scan order, so a lone +-1 far
+// behind the others costs a run of zero coeff_base symbols - the serial work of the
+// GPU's CDF adaptation (k_av1_cdf) and bits - for a small error. From the end of the
+// scan, a +-1 more than kTrimGap positions after the previous nonzero level (or the
+// block start) is dropped; the first level that is larger, or closer, ends the trim.
+constexpr int kTrimGap = 4;
+SK_HD bool trim_keep(int level, int s, int prev) { return level > 1 || level < -1 || s - prev <= kTrimGap; }
+SK_HD void trim_tail(int16_t* lev, int log2n) {
+    const int nn = 1 << (2 * log2n);
+    int last = -1, prev = -1;
+    for (int s = nn - 1; s >= 0 && last < 0; s--) {
+        if (!lev[default_scan(log2n, s)]) continue;
+        prev = -1;
+        for (int t2 = s - 1; t2 >= 0; t2--)
+            if (lev[default_scan(log2n, t2)]) {
+                prev = t2;
+                break;
+            }
+        if (trim_keep(lev[default_scan(log2n, s)], s, prev)) last = s;
+    }
+    for (int s = last + 1; s < nn; s++) lev[default_scan(log2n, s)] = 0;
+}
+
 template <class Sink>
 SK_HD int code_coeffs(Sink& w, const CdfContext& cx, const int16_t* lev, int txs, int plane, CoefCtx cc,
                       bool is_inter, int intra_dir, int qidx) {

@@ -247,11 +247,11 @@ static bool code_residual(const uint8_t* src, int sstride, const uint8_t* pred, 
     fwd_transform(res, log2n, co);
     const int qd = dc_q(qidx), qa = ac_q(qidx);
     bool nz = false;
+    for (int k = 0; k < nn; k++) lv[k] = (int16_t)quantize(co[k], k == 0 ? qd : qa, intra);
+    if (!intra) trim_tail(lv, log2n);
     for (int k = 0; k < nn; k++) {
-        const int l = quantize(co[k], k == 0 ? qd : qa, intra);
-        lv[k] = (int16_t)l;
-        nz |= l != 0;
-        dq[k] = dequant(l, k == 0 ? qd : qa);
+        nz |= lv[k] != 0;
+        dq[k] = dequant(lv[k], k == 0 ? qd : qa);
     }
     if (nz) {
         inv_transform(dq, log2n, rr);
@@ -417,7 +417,7 @@ void CpuAv1Encoder::decide_inter() {
         const int sz = 1 << lvl, half = sz >> 1;
         for (int r = 0; r < geo.mi_rows; r += sz)
             for (int c = 0; c < geo.mi_cols; c += sz) {
-                if (!(r + half < geo.mi_rows && c + half < geo.mi_cols)) continue;
+                if (r + sz > geo.mi_rows || c + sz > geo.mi_cols) continue;   // inside the picture (k_av1_merge)
                 const BlkInfo& b0 = blk[(size_t)(r >> 1) * geo.c8 + (c >> 1)];
                 bool ok = true;
                 for (int y = r >> 1; ok && y < std::min((r + sz) >> 1, geo.r8); y++)

@@ -60,12 +60,13 @@ int qidx_for_qp(int qp);
 int intra_mode_decision(const uint8_t* src, int stride, int x, int y, int log2n, bool au, bool al, int max_x,
                         int max_y);
 
-// CBR as svtav1enc runs in the reference (legacy/gstwebrtc_app.py:733-739): rc=2 with
-// buf-optimal-sz=120 ms, intra-period -1 and no scene-change key frames (a cut is coded
-// as an inter frame: a key frame costs several budgets and starves the frames after it).
-// Applied by sk_api's to_config for every back end.
+// Rate control as svtav1enc runs in the reference (legacy/gstwebrtc_app.py:733-739):
+// rc=2 (CBR) with buf-optimal-sz=120 ms, intra-period -1 and no scene-change key frames
+// (a cut is coded as an inter frame: a key frame costs several budgets and starves the
+// frames after it). Set whatever the starting mode, since set_rate() can switch a
+// session to CBR later. Applied by both back ends (front_config here, the HIP back
+// end's constructor).
 inline void cbr_config(h264::EncoderConfig& f) {
-    if (f.rc_mode != h264::RC_CBR) return;
     if (f.vbv_ms <= 0) f.vbv_ms = 120;
     f.scenecut = 0;
 }

@@ -70,6 +70,7 @@ struct BlkLds {
     uint8_t pred[384];
     int32_t a[384];
     int32_t b[384];
+    int16_t lv[384];     // quantised levels (raster per plane) before tail trimming
     IntraEdge e[3];      // intra edges of Y, U, V
 };
 // Tile of a unit position (mi r, c).
@@ -106,21 +107,65 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         }
     }
     wsync();
-    // forward stage 2 (rows) + quantisation + dequantisation
-    int nzm = 0;
-    uint32_t cul = 0;
+    // forward stage 2 (rows) + quantisation
     for (int p = 0; p < 3; p++) {
         const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
         const int16_t* K = fdct_k(F, ln);
-        int16_t* g = p == 0 ? gy : (p == 1 ? gu : gv);
-        int sum = 0, nz = 0, first = 0;
         for (int i = l; i < sz * sz; i += 64) {
             const int k = i >> ln, lc = i & (sz - 1);
             int64_t s = 0;
             for (int j = 0; j < sz; j++) s += (int64_t)L.b[o + k * sz + j] * K[lc * sz + j];
             const int32_t c = (int32_t)((s + (s >= 0 ? 4096 : 4095)) >> 13);
+            L.lv[o + i] = (int16_t)quantize(c, i == 0 ? qd : qa, intra);
+        }
+    }
+    wsync();
+    // inter blocks: tail trimming (av1_core.h trim_tail), lane = scan positions l + 64 k:
+    // nonzero masks by ballot, each lane's previous nonzero from the masks, the cut at
+    // the last level that trim_keep keeps
+    if (!intra)
+        for (int p = 0; p < 3; p++) {
+            const int ln = p ? log2n - 1 : log2n, nn2 = 1 << (2 * ln), o = base(p), nw = (nn2 + 63) >> 6;
+            uint64_t mk[4];
+            int lvk[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int sidx = l + 64 * k;
+                lvk[k] = k < nw && sidx < nn2 ? (int)L.lv[o + default_scan(ln, sidx)] : 0;
+                mk[k] = __ballot(lvk[k] != 0);
+            }
+            int cut = -1;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                int prev = -1;   // highest nonzero scan position below l + 64 k
+                const uint64_t below = l ? (mk[k] & ((1ull << l) - 1)) : 0ull;
+                if (below) prev = 64 * k + 63 - __builtin_clzll(below);
+                else
+                    for (int j = k - 1; j >= 0; j--)
+                        if (mk[j]) {
+                            prev = 64 * j + 63 - __builtin_clzll(mk[j]);
+                            break;
+                        }
+                const uint64_t keep = __ballot(lvk[k] != 0 && trim_keep(lvk[k], l + 64 * k, prev));
+                if (keep) cut = 64 * k + 63 - __builtin_clzll(keep);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int sidx = l + 64 * k;
+                if (k < nw && sidx < nn2 && sidx > cut && lvk[k]) L.lv[o + default_scan(ln, sidx)] = 0;
+            }
+        }
+    wsync();
+    // dequantisation, level summaries
+    int nzm = 0;
+    uint32_t cul = 0;
+    for (int p = 0; p < 3; p++) {
+        const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
+        int16_t* g = p == 0 ? gy : (p == 1 ? gu : gv);
+        int sum = 0, nz = 0, first = 0;
+        for (int i = l; i < sz * sz; i += 64) {
             const int q = i == 0 ? qd : qa;
-            const int lv = quantize(c, q, intra);
+            const int lv = L.lv[o + i];
             g[i] = (int16_t)lv;
             if (i == 0) first = lv;
             sum += lv < 0 ? -lv : lv;
@@ -468,7 +513,8 @@ __global__ __launch_bounds__(64) void k_av1_merge(Av1Args A) {
         const int sz = 1 << lvl, half = sz >> 1, cells = sz >> 1;
         // region of this lane
         const int r = (cy & ~(cells - 1)) * 2, c = (cx & ~(cells - 1)) * 2;
-        const bool fits = r + half < g.mi_rows && c + half < g.mi_cols;
+        // the merged block lies inside the picture (no partially outside 32x32 / 64x64)
+        const bool fits = r + sz <= g.mi_rows && c + sz <= g.mi_cols;
         const BlkInfo b0 = A.blk[(size_t)(r >> 1) * g.c8 + (c >> 1)];
         const BlkInfo me = in ? A.blk[(size_t)cy * g.c8 + cx] : b0;
         const bool ok_me = !in || (blk_skip(me) && me.mv_row == b0.mv_row && me.mv_col == b0.mv_col);
@@ -634,7 +680,8 @@ __device__ __forceinline__ void use_regs(const uint32_t* v) {
 
 __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     __shared__ CdfContext cx;
-    __shared__ uint32_t wst[64];   // interval words of the sub-batch being adapted
+    __shared__ uint32_t wst[64];     // words of the gathered booleans of the sub-batch
+    __shared__ uint16_t cap[64][66]; // per token of the sub-batch: the CDF row before its update (padded: conflict-free column reads)
     const int t = blockIdx.x / kEcParts, part = blockIdx.x % kEcParts, L = threadIdx.x;
     {
         const uint16_t* src = (const uint16_t*)&AV1_DEFAULT_CDF[coef_qctx(A.frame[1])];
@@ -648,78 +695,74 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
     // words of tokens this wave does not own go to its junk slots past the streams
     uint32_t* junk = A.pw + (size_t)A.geo.tile_cols * A.geo.tile_rows * A.tile_tok_cap + (size_t)blockIdx.x * 64;
-    // One symbol with the whole wave (gathered booleans, alphabets of 16).
-    auto one = [&](uint32_t tt) -> uint32_t {
-        const int off = (int)(tt & 0x3fffff);
-        if ((tt >> 30) == 0) {
-            const int n = (int)((tt >> 26) & 15) + 1, s = (int)((tt >> 22) & 15);
-            const uint32_t cv = L <= n ? (uint32_t)cdfs[off + L] : 0u;
-            const uint32_t chi = sgpr(rdlane(cv, s)), clo = sgpr(rdlane(cv, s > 0 ? s - 1 : 0));
-            const int count = (int)sgpr(rdlane(cv, n));
-            const int rate = 3 + (count > 15) + (count > 31) + (n > 3 ? 2 : (n > 1 ? 1 : 0));
-            if (L < n - 1) {
-                const int c = (int)cv;
-                cdfs[off + L] = (uint16_t)(L >= s ? c + ((32768 - c) >> rate) : c - (c >> rate));
-            } else if (L == n && count < 32) {
-                cdfs[off + L] = (uint16_t)(count + 1);
-            }
-            return ec_word(clo, chi, n, s);
-        }
-        uint16_t c2[3];   // gathered split_or_horz / split_or_vert boolean (read-only CDF)
-        gather_partition_cdf(cdfs + off, ((tt >> 29) & 1) == 0, c2);
-        const uint32_t c0 = sgpr(c2[0]);
-        const int v = (int)((tt >> 28) & 1);
-        return ec_word(c0, v ? 32768u : c0, 2, v);
-    };
-    // The CDF of the context adapted last stays in a register (lane j: cdf[j], lane N:
-    // the counter) and goes back to LDS only when another context comes up: the hot
-    // contexts (the zero-level context of 16x16 luma blocks can be half of a tile's
-    // symbols) then adapt in registers with no LDS round trip.
-    int cache_off = -1, cache_n = 0;
+    // The CDF of the context adapted last stays in a register (lane j: cdf[j]; its
+    // counter and adaptation rate in scalars) and goes back to LDS only when another
+    // context comes up: the hot contexts (the zero-level context of 16x16 luma blocks
+    // can be half of a tile's symbols) adapt in registers with no LDS round trip. The
+    // serial loop does only what the next symbol depends on - the lane-parallel update
+    // of the row - and leaves the row it started from in cap[token]; the interval words
+    // are built after the loop, one lane per token.
+    int cache_off = -1, cache_n = 0, cnt = 0, rate = 0, rbase = 0;
     uint32_t cache = 0;
     auto evict = [&]() {
-        if (cache_off >= 0 && L <= cache_n) cdfs[cache_off + L] = (uint16_t)cache;
+        if (cache_off >= 0) {
+            if (L < cache_n - 1) cdfs[cache_off + L] = (uint16_t)cache;
+            else if (L == cache_n) cdfs[cache_off + L] = (uint16_t)cnt;
+        }
         cache_off = -1;
     };
-    auto sub = [&](uint32_t tv, int b) -> uint32_t {   // 64 tokens from b: this wave's words
+    auto sub = [&](uint32_t tv, int b) {   // 64 tokens from b: this wave's words
         // literal tokens are their own word (partition 0 copies them)
-        const bool lit = (tv >> 30) == 1;
+        const uint32_t kind = tv >> 30;
+        const bool lit = kind == 1;
         const bool mine = b + L < ntok && (lit ? part == 0 : ec_owner(tv & 0x3fffff) == part);
-        wst[L] = tv;
         uint64_t m = __ballot(mine && !lit);
         while (m) {
             const int i = __builtin_ctzll(m);
-            m &= m - 1;
+            asm volatile("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(i));   // m &= m - 1 in one SALU op
             const uint32_t tt = sgpr(rdlane(tv, i));
-            uint32_t w;
             if ((tt >> 30) == 0) {
                 const int off = (int)(tt & 0x3fffff);
-                const int n = (int)((tt >> 26) & 15) + 1, s = (int)((tt >> 22) & 15);
                 if (off != cache_off) {
                     evict();
+                    const int n = (int)((tt >> 26) & 15) + 1;
                     cache = L <= n ? (uint32_t)cdfs[off + L] : 0u;
                     cache_off = off;
                     cache_n = n;
+                    cnt = (int)sgpr(rdlane(cache, n));
+                    rbase = 3 + (n > 3 ? 2 : (n > 1 ? 1 : 0));
+                    rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
                 }
-                const uint32_t chi = sgpr(rdlane(cache, s)), clo = sgpr(rdlane(cache, s > 0 ? s - 1 : 0));
-                const int count = (int)sgpr(rdlane(cache, n));
-                const int nr = n > 3 ? 2 : (n > 1 ? 1 : 0);
-                const int rate = (int)sgpr((uint32_t)(3 + (count > 15) + (count > 31) + nr));
-                const int cnt1 = (int)sgpr((uint32_t)(count < 32 ? count + 1 : count));
-                // update_cdf, branch-free: lanes < N-1 move towards 0 / 32768, lane N counts
+                const int s = (int)((tt >> 22) & 15);
+                cap[i][L] = (uint16_t)cache;
+                // update_cdf, branch-free: lanes >= s move towards 32768, the others to 0
+                // (lanes >= N-1 are never written back; the counter lives in cnt)
                 const int c = (int)cache;
                 const int up = c + ((32768 - c) >> rate), dn = c - (c >> rate);
-                const int ad = L >= s ? up : dn;
-                cache = (uint32_t)(L < n - 1 ? ad : (L == n ? cnt1 : c));
-                w = ec_word(clo, chi, n, s);
+                cache = (uint32_t)(L >= s ? up : dn);
+                if (cnt < 32) {
+                    cnt++;
+                    rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
+                }
             } else {   // gathered boolean: reads a partition CDF from LDS
                 evict();
-                w = one(tt);
+                uint16_t c2[3];   // split_or_horz / split_or_vert (read-only CDF)
+                gather_partition_cdf(cdfs + (tt & 0x3fffff), ((tt >> 29) & 1) == 0, c2);
+                const uint32_t c0 = sgpr(c2[0]);
+                const int v = (int)((tt >> 28) & 1);
+                if (L == 0) wst[i] = ec_word(c0, v ? 32768u : c0, 2, v);
             }
-            if (L == 0) wst[i] = w;
         }
         wsync();
-        const uint32_t out = wst[L];
+        uint32_t out = tv;   // literal
+        if (kind == 0) {
+            const int n = (int)((tv >> 26) & 15) + 1, s = (int)((tv >> 22) & 15);
+            const uint32_t chi = s < n - 1 ? (uint32_t)cap[L][s] : 0u, clo = s > 0 ? (uint32_t)cap[L][s - 1] : 0u;
+            out = ec_word(clo, chi, n, s);
+        } else if (kind != 1) {
+            out = wst[L];
+        }
+        wsync();
         uint32_t* d = mine ? pw + b + L : junk + L;   // unconditional store
         *d = out;
         return 0;

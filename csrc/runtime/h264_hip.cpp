@@ -40,6 +40,7 @@ using namespace h264;
 class HipBackend : public EncoderBackend {
    public:
     HipBackend(const EncoderConfig& c, int device) : cfg_(c), device_(device) {
+        if (cfg_.codec == 2) av1::cbr_config(cfg_);   // AV1 CBR as the CPU encoder (av1_encoder.h)
         g_.init(cfg_);
         ctl_.init(cfg_, g_);
         HIPCHECK(hipSetDevice(device_));

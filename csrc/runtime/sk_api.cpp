@@ -277,7 +277,6 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
         e.num_refs = 1;
         e.deblock = 0;
     }
-    if (e.codec == 2) av1::cbr_config(e);
     return e;
 }
 

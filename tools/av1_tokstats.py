@@ -22,12 +22,13 @@ def main():
     ap.add_argument("--kbps", type=int, default=0)
     ap.add_argument("--fps", type=float, default=120.0)
     ap.add_argument("--content", default="motion")
+    ap.add_argument("--qp", type=int, default=25)
     a = ap.parse_args()
     from selkies_gstreamer_amd.ops.native import H264Encoder
     from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
     src = SyntheticDesktop(a.width, a.height, kind=a.content)
     enc = H264Encoder(a.width, a.height, codec="av1", fullframe=True, backend="hip", fps=a.fps,
-                      rate_control=a.mode, bitrate_kbps=a.kbps)
+                      rate_control=a.mode, bitrate_kbps=a.kbps, qp=a.qp)
     for t in range(a.frames):
         pk = enc.encode(src.frame(t), t)
     nbytes = sum(len(p.data) for p in pk)
@@ -53,7 +54,19 @@ def main():
     order = np.argsort(-cnt)
     part = ((offs.astype(np.uint64) * 0x9E3779B1) & 0xFFFFFFFF) >> 28
     loads = np.bincount(part.astype(np.int64), weights=cnt, minlength=16)
-    out = {"max_tile_contexts": int(offs.size),
+    # the critical path of k_av1_cdf: the largest per-wave symbol load over all tiles
+    crit, crit_top = 0, 0
+    for t in range(ntok.size):
+        tt = tokc[t * cap: t * cap + ntok[t]]
+        st = tt[(tt >> 30) != 1] & 0x3fffff
+        if st.size == 0:
+            continue
+        o, c = np.unique(st, return_counts=True)
+        pa = ((o.astype(np.uint64) * 0x9E3779B1) & 0xFFFFFFFF) >> 28
+        crit = max(crit, int(np.bincount(pa.astype(np.int64), weights=c, minlength=16).max()))
+        crit_top = max(crit_top, int(c.max()))
+    out = {"cdf_critical_symbols": crit, "cdf_hottest_context_symbols": crit_top,
+           "max_tile_contexts": int(offs.size),
            "max_tile_top_contexts": [[int(offs[i]), int(cnt[i])] for i in order[:12]],
            "max_tile_partition_loads": [int(x) for x in loads],
            "width": a.width, "height": a.height, "mode": a.mode, "kbps": a.kbps, "frame_bytes": nbytes,

@@ -6,6 +6,7 @@
 #   prof   TAG [BENCH-ARGS...]   rocprofv3 --kernel-trace --stats of bench.py ARGS + kernel table
 #   pmc    TAG [BENCH-ARGS...]   four --pmc passes of bench.py ARGS -> gpurun_out/TAG/pmc.md
 #   py     TAG SCRIPT [ARGS...]  python SCRIPT ARGS > gpurun_out/TAG/out.txt
+#   profpy TAG SCRIPT [ARGS...]  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS + kernel table
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 ROOT=$(pwd)
@@ -31,6 +32,17 @@ prof)
     DB=$(ls "$OUT"/prof/*/run_results.db "$OUT"/prof/run_results.db 2>/dev/null | head -1)
     [ -n "$DB" ] && python tools/rocprof_summary.py "$DB" > "$OUT/kernels.md" && head -40 "$OUT/kernels.md"
     tail -1 "$OUT/prof.log"
+    exit $rc ;;
+profpy)
+    # rocprofv3 --kernel-trace --stats of a python script: profpy TAG SCRIPT [ARGS...]
+    SCRIPT=$1; shift
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 "$ROOT/$SCRIPT" "$@" \
+        > "$OUT/out.txt" 2> "$OUT/prof.log"
+    rc=$?; cd "$ROOT"
+    DB=$(ls "$OUT"/prof/*/run_results.db "$OUT"/prof/run_results.db 2>/dev/null | head -1)
+    [ -n "$DB" ] && python tools/rocprof_summary.py "$DB" > "$OUT/kernels.md" && head -14 "$OUT/kernels.md"
+    tail -3 "$OUT/out.txt"
     exit $rc ;;
 pmc)
     # four counter passes (rocprofv3 does not multiplex: <= 8 SQ, 4 TCC, 2 GRBM per pass)
