@@ -8,3 +8,10 @@ namespace sk {
 // that reads and writes device memory; used by warm_copy_engines()).
 void launch_touch_pages(uint8_t* buf, int pages, hipStream_t s);
 }  // namespace sk
+
+namespace sk {
+// BGRx / BGRA -> I420 (codec/color.h bgrx_quad_to_yuv: the encoders' K1 arithmetic), one
+// thread per 2x2 quad; odd widths / heights repeat the last column / row.
+void launch_bgrx_i420(const uint8_t* bgrx, int stride, int w, int h, int full_range, uint8_t* y, int ys,
+                      uint8_t* u, int us, uint8_t* v, int vs, hipStream_t s);
+}  // namespace sk

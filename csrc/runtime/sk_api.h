@@ -87,6 +87,14 @@ int sk_h264_stage_times(void* enc, float* dst, int32_t n);
 
 const char* sk_last_error(void);
 
+// Standalone BGRx / BGRA -> I420 converter (BT.709; the encoders' K1 arithmetic), backend
+// 0 = CPU, 1 = HIP on `device`; run returns 0 on success. Odd sizes repeat the last
+// column / row into the chroma average; chroma planes are (w+1)/2 x (h+1)/2.
+void* sk_convert_create(int w, int h, int full_range, int backend, int device);
+int sk_convert_run(void* conv, const uint8_t* bgrx, int32_t stride, uint8_t* y, int32_t ys, uint8_t* u, int32_t us,
+                   uint8_t* v, int32_t vs);
+void sk_convert_destroy(void* conv);
+
 typedef struct sk_jpeg_config {
     int32_t width, height, stripe_height;
     int32_t quality, paint_quality, use_paint_over, paint_over_trigger;

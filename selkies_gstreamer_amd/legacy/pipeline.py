@@ -30,6 +30,14 @@ Mapping:
   ``rtpopuspay``.
 VP8 / VP9 encoder elements are rejected with an explicit error: this build's video
 codecs are H.264, H.265, AV1 and JPEG.
+
+When GStreamer itself is installed (the 1.14 under /opt/conda in this image) a launch
+string can also run in real GStreamer: :func:`to_gst_launch` rewrites the reference's
+encoder elements to this build's GStreamer elements (libgsthip, csrc/gst/gsthip.c:
+``hiph264enc`` / ``hiph265enc`` / ``hipav1enc`` / ``hipconvert``) with their
+properties mapped, and :func:`run_gst` runs it with gst-launch-1.0. That covers graphs
+GStreamer can complete here (file / fd / fake sinks); ``webrtcbin`` and the RTP
+payloaders are not in that GStreamer build, so WebRTC stays on the own stack (webrtc/).
 """
 from __future__ import annotations
 
@@ -232,3 +240,95 @@ def apply_to_args(spec: PipelineSpec, args) -> None:
         args.capture_source = spec.source
     if hasattr(args, "enable_cursors"):
         args.enable_cursors = "false" if spec.show_pointer else "true"   # server-side cursor vs client cursors
+
+
+# ---------------------------------------------------------------------------
+# Real GStreamer (gst-launch-1.0 + libgsthip)
+GST_ENCODER_FOR = {**{n: "hiph264enc" for n in H264_ENCODERS}, **{n: "hiph265enc" for n in H265_ENCODERS},
+                   **{n: "hipav1enc" for n in AV1_ENCODERS}}
+# the reference's GPU upload / conversion elements: the hip encoders take BGRx directly
+GST_DROP = {"cudaupload", "cudadownload", "cudaconvert", "vapostproc", "hipupload"}
+GST_NO_ELEMENT = {"webrtcbin", "rtph264pay", "rtph265pay", "rtpav1pay", "rtpopuspay", "pulsesrc", "opusenc"}
+
+
+def _gst_value(v) -> str:
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, float) and v.is_integer():
+        return str(int(v))
+    return str(v)
+
+
+def _gst_encoder_props(name: str, p: dict) -> list[str]:
+    out = []
+    for k in ("bitrate", "target-bitrate"):
+        if k in p:
+            out.append(f"bitrate={int(p[k]) // (1000 if name == 'rav1enc' else 1)}")
+            break
+    for k in ("key-int-max", "gop-size", "keyframe-period", "idr-period", "keyframe-max-dist",
+              "intra-period-length", "max-key-frame-interval"):
+        if k in p:
+            v = int(p[k])
+            out.append(f"key-int-max={v if 0 < v < 2 ** 31 - 1 else -1}")
+            break
+    for k in ("quantizer", "qp-const", "qp"):
+        if k in p:
+            out.append(f"qp={int(p[k])}")
+            break
+    mode = str(p.get("rc-mode", p.get("pass", p.get("end-usage", p.get("rate-control", ""))))).lower()
+    if "cbr" in mode:
+        out.append("rate-control=cbr")
+    elif mode in ("cqp", "constqp", "quant", "qp"):
+        out.append("rate-control=cqp")
+    return out
+
+
+def to_gst_launch(text: str) -> list[str]:
+    """gst-launch-1.0 arguments for a launch string, with this build's GStreamer elements
+    in place of the reference's encoders (see the module docstring)."""
+    out: list[str] = []
+    for e in parse_elements(text):
+        n, p = e.name, e.props
+        if n in UNSUPPORTED_ENCODERS:
+            raise PipelineError(f"{n}: this build encodes H.264 / H.265 / AV1 (HIP) and JPEG")
+        if n in GST_NO_ELEMENT:
+            raise PipelineError(f"{n}: not in this GStreamer build; WebRTC runs on the own stack (legacy app)")
+        if n in GST_DROP:
+            continue
+        if n.startswith("video/") or n.startswith("audio/"):
+            caps = [n] + [f"{k}={_gst_value(v) if k != 'framerate' else _gst_framerate(v)}" for k, v in p.items()]
+            seg = [",".join(caps)]
+        elif n in GST_ENCODER_FOR:
+            seg = [GST_ENCODER_FOR[n], *_gst_encoder_props(n, p)]
+        else:
+            seg = [n, *(f"{k}={_gst_value(v)}" for k, v in p.items())]
+        if out:
+            out.append("!")
+        out.extend(seg)
+    return out
+
+
+def _gst_framerate(v) -> str:
+    from fractions import Fraction
+    f = Fraction(float(v)).limit_denominator(1001)
+    return f"{f.numerator}/{f.denominator}"
+
+
+def gst_available() -> bool:
+    try:
+        from selkies_gstreamer_amd.ops import build_gst
+    except ImportError:
+        return False
+    return build_gst.available() and build_gst.PLUGIN.exists()
+
+
+def run_gst(text: str, timeout: float | None = None):
+    """Runs a launch string in real GStreamer (gst-launch-1.0 with libgsthip); returns the
+    CompletedProcess. Raises PipelineError when GStreamer or the plugin is absent."""
+    import subprocess
+    if not gst_available():
+        raise PipelineError("GStreamer with libgsthip is not available (ops/build_gst.py)")
+    from selkies_gstreamer_amd.ops import build_gst
+    return subprocess.run([build_gst.gst_bin("gst-launch-1.0"), "-q", *to_gst_launch(text)],
+                          env=build_gst.gst_env(), capture_output=True, text=True, timeout=timeout)
+

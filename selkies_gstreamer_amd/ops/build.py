@@ -71,8 +71,11 @@ def build(verbose: bool = False, jobs: int | None = None) -> Path:
         objs = list(ex.map(lambda s: _compile(s, hdr, verbose), srcs))
     newest = max(o.stat().st_mtime for o in objs)
     if not LIB.exists() or LIB.stat().st_mtime < newest:
+        # RUNPATH: the library's own dependencies (HIP runtime, the system libstdc++) resolve
+        # without the RPATH of a host executable that ships an older libstdc++
+        # (gst-launch-1.0 from /opt/conda loading libgsthip)
         cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(LIB), *map(str, objs),
-               "-lpthread", "-ldl"]
+               "-lpthread", "-ldl", "-Wl,--enable-new-dtags,-rpath,/opt/rocm/lib:/usr/lib/x86_64-linux-gnu"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
