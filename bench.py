@@ -87,6 +87,8 @@ def parse():
                         "real server processes (session hosts) to headless websocket clients for --e2e-seconds and report the "
                         "measured capture->client latency; a comma list is tried in order and the first N at "
                         "which every session sustains 60 fps is reported (tools/bench_e2e.py); 0 = skip")
+    p.add_argument("--e2e-no-cpu-cap", action="store_true",
+                   help="try the session counts even above what the CPU quota can drive (cpu_budget)")
     p.add_argument("--e2e-seconds", type=float, default=4.0)
     p.add_argument("--e2e-warmup", type=float, default=6.0)
     p.add_argument("--e2e-force", action="store_true",
@@ -187,15 +189,54 @@ def run_e2e(args, W, H, gpu=0, counts=None):
         return {"sessions": counts or e2e_counts(args), "error": f"{type(ex).__name__}: {ex}"}
 
 
+# CPU cost of one end-to-end 1080p60 session, server and client side together:
+# 8.9 + 1.1 CPUs for 48 sessions (profiles/r3_e2e_collapse.md); one more CPU per rank
+# for the rank's own encoder loop and event handling.
+E2E_CPU_PER_SESSION = 0.21
+E2E_CPU_PER_RANK = 1.0
+
+
+def cpu_budget() -> tuple[float, str]:
+    """CPUs this command may use and where that number comes from: the cgroup v2 quota
+    (/sys/fs/cgroup/cpu.max, what the GPU box enforces), else the affinity mask."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return float(q) / float(per), "cgroup cpu.max"
+    except (OSError, ValueError):
+        pass
+    try:
+        return float(len(os.sched_getaffinity(0))), "sched_getaffinity"
+    except (AttributeError, OSError):
+        return float(os.cpu_count() or 1), "os.cpu_count"
+
+
 def e2e_counts(args, world=1):
     """Session counts tried by the end-to-end check on each GPU. One GPU: the
     default sweep; a node of N GPUs: every rank serves its share of BASELINE config
-    4 (64 sessions over 8 GPUs -> 8 per GPU) and one step above it."""
+    4 (64 sessions over 8 GPUs -> 8 per GPU) and one step above it. Counts above what
+    this rank's share of the CPU quota can drive (E2E_CPU_PER_SESSION) are dropped:
+    past it every session collapses together (profiles/r3_e2e_collapse.md)."""
+    v = e2e_counts_uncapped(args, world)
+    cap = e2e_cpu_cap(world)
+    if v and not getattr(args, "e2e_no_cpu_cap", False):
+        fit = [n for n in v if n <= cap]
+        v = fit if fit else ([cap] if cap >= 1 else [])
+    return v
+
+
+def e2e_counts_uncapped(args, world=1):
     v = [int(x) for x in str(args.e2e_sessions).split(",") if x.strip() and int(x) > 0]
     if world > 1 and args.e2e_sessions == "48,32,16":
         per = max(1, 64 // world)
         v = [2 * per, per]
     return v
+
+
+def e2e_cpu_cap(world=1) -> int:
+    cpus, _ = cpu_budget()
+    return int(max(0.0, cpus / max(world, 1) - E2E_CPU_PER_RANK) // E2E_CPU_PER_SESSION)
 
 
 def run_extra(args, W, H, encoder, fps, local_rank, steps, backend=None):
@@ -613,6 +654,10 @@ def main():
             "capture_to_client_p50_ms": e2e.get("latency_p50_ms") if e2e else None,
             "capture_to_client_p99_ms": e2e.get("latency_p99_ms") if e2e else None,
             "e2e": e2e,
+            "e2e_cpu": {"cpus": round(cpu_budget()[0], 2), "source": cpu_budget()[1], "ranks": max(world, 1),
+                        "cpu_per_session": E2E_CPU_PER_SESSION, "session_cap_per_rank": e2e_cpu_cap(world),
+                        # the sweep was cut to what the CPU quota can drive (the GPU could take more)
+                        "cpu_bound": any(n > e2e_cpu_cap(world) for n in e2e_counts_uncapped(args, world))},
             "e2e_per_gpu": ([{"gpu": i, "sessions": (r or {}).get("sessions"), "sustained": (r or {}).get("sustained"),
                               "fps_min": (r or {}).get("fps_min"), "latency_p50_ms": (r or {}).get("latency_p50_ms"),
                               "latency_p99_ms": (r or {}).get("latency_p99_ms"), "error": (r or {}).get("error")}

@@ -7,6 +7,8 @@
 #   pmc    TAG [BENCH-ARGS...]   four --pmc passes of bench.py ARGS -> gpurun_out/TAG/pmc.md
 #   py     TAG SCRIPT [ARGS...]  python SCRIPT ARGS > gpurun_out/TAG/out.txt
 #   profpy TAG SCRIPT [ARGS...]  rocprofv3 --kernel-trace --stats of python SCRIPT ARGS + kernel table
+#   rate   TAG [CODECS...]       K10 CBR traces (rc_trace.py) per codec + tools/rate_report.py
+#   driver TAG                   the driver's bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 ROOT=$(pwd)
@@ -44,6 +46,26 @@ profpy)
     [ -n "$DB" ] && python tools/rocprof_summary.py "$DB" > "$OUT/kernels.md" && head -14 "$OUT/kernels.md"
     tail -3 "$OUT/out.txt"
     exit $rc ;;
+rate)
+    # K10 traces: rate TAG [CODECS...] - 600 frames of 1080p60 CBR at 8 / 16 Mbit/s on
+    # motion and desktop content per codec (default h264 hevc av1), then the report
+    CODECS=${@:-h264 hevc av1}
+    for codec in $CODECS; do
+      for k in 8000 16000; do
+        for c in motion desktop; do
+          timeout -k 10 300 python -u tools/rc_trace.py --backend hip --codec $codec --frames 600 --content $c \
+              --mode cbr --kbps $k --json "$OUT/${codec}_cbr_${c}_${k}.json" >> "$OUT/summary.jsonl" 2>> "$OUT/err.log" \
+              || { tail -5 "$OUT/err.log"; exit 1; }
+        done
+      done
+    done
+    python tools/rate_report.py "$OUT" > "$OUT/rate.md" && cat "$OUT/rate.md" | head -40
+    exit 0 ;;
+driver)
+    # the driver's round-end command (bench.py --gpus 1 --steps 20 --warmup 5) + its kernel profile
+    timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
+    rc=$?; tail -1 "$OUT/bench.jsonl" | cut -c1-1500; [ $rc -ne 0 ] && { tail -20 "$OUT/bench.err"; exit $rc; }
+    exit 0 ;;
 pmc)
     # four counter passes (rocprofv3 does not multiplex: <= 8 SQ, 4 TCC, 2 GRBM per pass)
     P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT"
