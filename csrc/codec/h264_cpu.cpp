@@ -533,12 +533,18 @@ static void mb_edges(const std::vector<uint8_t>* P, const Geometry& g, int mbx, 
 void CpuH264Encoder::code_slice_intra(int s) {
     const SliceTask& t = tasks[s];
     const int sy_ = g.stride_y, sc = g.stride_c;
+    const bool split = intra_split(t, g.mb_w, cfg.deblock, cfg.intra4x4);
+    const int first = t.first_row * g.mb_w;
     for (int pass = 0; pass < 2; pass++)
         for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
             for (int mbx = 0; mbx < g.mb_w; mbx++) {
                 int idx = mby * g.mb_w + mbx;
                 MbInfo& mb = mbs[idx];
                 bool aT = mby > t.first_row, aL = mbx > 0;
+                if (split) {   // K5 sub-slice: left neighbour inside it only, never the top
+                    aT = false;
+                    aL = aL && (idx - first) % kIntraSubMbs != 0;
+                }
                 uint8_t top[16], left[16], ctop[2][8], cleft[2][8];
                 int tl, ctl[2];
                 mb_edges(pass == 0 ? src : rec, g, mbx, mby, aT, aL, top, left, &tl, ctop, cleft, ctl);
@@ -661,53 +667,61 @@ void CpuH264Encoder::code_slice_skipall(int s) {
                (size_t)(y1 - y0) / 2 * g.stride_c);
 }
 
-void CpuH264Encoder::mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb) const {
-    nb.left = mbx > 0 ? &mbs[mby * g.mb_w + mbx - 1] : nullptr;
-    nb.top = mby > first_row ? &mbs[(mby - 1) * g.mb_w + mbx] : nullptr;
+void CpuH264Encoder::mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb, int sub0) const {
+    const int idx = mby * g.mb_w + mbx;
+    nb.left = mbx > 0 && idx - 1 >= sub0 ? &mbs[idx - 1] : nullptr;
+    nb.top = mby > first_row && idx - g.mb_w >= sub0 ? &mbs[idx - g.mb_w] : nullptr;
 }
 
-std::vector<uint8_t> CpuH264Encoder::write_slice(int s) {
+std::vector<std::vector<uint8_t>> CpuH264Encoder::write_slice(int s) {
     const SliceTask& t = tasks[s];
-    const int nmb = t.num_rows * g.mb_w;
-    std::vector<uint8_t> buf((size_t)nmb * (kMaxMbBits / 8 + 16) + 64, 0);
-    BitWriter w(buf.data());
-    SliceHeaderParams h;
+    const int nmb = t.num_rows * g.mb_w, first = t.first_row * g.mb_w;
     bool intra = t.final_action == ACT_I;
-    h.first_mb = cfg.fullframe ? t.first_row * g.mb_w : 0;
-    h.slice_type = intra ? 2 : 0;
-    h.idr = intra && t.idr_on_intra;
-    h.frame_num = h.idr ? 0 : t.frame_num;
-    h.idr_pic_id = t.idr_pic_id;
-    h.slice_qp = t.qp;
-    h.deblock = cfg.deblock;
-    h.num_refs = intra ? 1 : t.num_refs;
-    write_slice_header(w, h);
-    if (t.final_action == ACT_SKIPALL) {
-        put_ue(w, (uint32_t)nmb);
-    } else {
-        int skip_run = 0, qp_prev = t.qp;
-        for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
-            for (int mbx = 0; mbx < g.mb_w; mbx++) {
-                int idx = mby * g.mb_w + mbx;
+    // one NAL per sub-slice of a split I slice (K5), else one for the slice
+    const bool split = intra_split(t, g.mb_w, cfg.deblock, cfg.intra4x4);
+    const int nsub = split ? intra_sub_count(nmb) : 1, sub_len = split ? kIntraSubMbs : nmb;
+    std::vector<std::vector<uint8_t>> nals;
+    for (int j = 0; j < nsub; j++) {
+        const int k0 = j * sub_len, k1 = sk_min(nmb, k0 + sub_len);   // stripe-relative MB range
+        std::vector<uint8_t> buf((size_t)(k1 - k0) * (kMaxMbBits / 8 + 16) + 64, 0);
+        BitWriter w(buf.data());
+        SliceHeaderParams h;
+        h.first_mb = (cfg.fullframe ? first : 0) + k0;
+        h.slice_type = intra ? 2 : 0;
+        h.idr = intra && t.idr_on_intra;
+        h.frame_num = h.idr ? 0 : t.frame_num;
+        h.idr_pic_id = t.idr_pic_id;
+        h.slice_qp = t.qp;
+        h.deblock = cfg.deblock;
+        h.num_refs = intra ? 1 : t.num_refs;
+        write_slice_header(w, h);
+        if (t.final_action == ACT_SKIPALL) {
+            put_ue(w, (uint32_t)nmb);
+        } else {
+            int skip_run = 0, qp_prev = t.qp;
+            for (int k = k0; k < k1; k++) {
+                const int idx = first + k, mbx = idx % g.mb_w, mby = idx / g.mb_w;
                 const MbInfo& mb = mbs[idx];
                 if (mb.type == MB_P_SKIP) { skip_run++; continue; }
                 if (!intra) { put_ue(w, (uint32_t)skip_run); skip_run = 0; }
                 int dq = 0;
                 if (mb_has_qp_delta(mb)) { dq = mb.qp - qp_prev; qp_prev = mb.qp; }
                 MbNeighbours nb;
-                mb_neighbours(mbx, mby, t.first_row, nb);
+                mb_neighbours(mbx, mby, t.first_row, nb, first + k0);
                 write_mb_header(w, mb, !intra, dq, intra ? 1 : t.num_refs, nb);
                 write_mb_residual(w, mb, nb, &coefs[(size_t)idx * kCoefPerMb], host_cavlc_tables());
             }
-        if (skip_run > 0) put_ue(w, (uint32_t)skip_run);
+            if (skip_run > 0) put_ue(w, (uint32_t)skip_run);
+        }
+        w.put1(1);
+        while (w.pos & 7) w.put1(0);
+        buf.resize(w.pos / 8);
+        nals.push_back(std::move(buf));
     }
-    w.put1(1);
-    while (w.pos & 7) w.put1(0);
-    buf.resize(w.pos / 8);
-    return buf;
+    return nals;
 }
 
-void CpuH264Encoder::package(uint16_t frame_id, std::vector<std::vector<uint8_t>>& rbsp,
+void CpuH264Encoder::package(uint16_t frame_id, std::vector<std::vector<std::vector<uint8_t>>>& rbsp,
                              std::vector<EncodedPacket>& out) {
     if (cfg.fullframe) {
         bool idr = ctl_.picture_is_idr(tasks.data());
@@ -719,7 +733,7 @@ void CpuH264Encoder::package(uint16_t frame_id, std::vector<std::vector<uint8_t>
         for (int s = 0; s < g.num_slices; s++) {
             const SliceTask& t = tasks[s];
             int hdr = (t.final_action == ACT_I && idr) ? 0x65 : 0x41;
-            append_nal(pk.data, hdr, rbsp[s].data(), rbsp[s].size());
+            for (const auto& n : rbsp[s]) append_nal(pk.data, hdr, n.data(), n.size());
         }
         out.push_back(std::move(pk));
         return;
@@ -733,7 +747,7 @@ void CpuH264Encoder::package(uint16_t frame_id, std::vector<std::vector<uint8_t>
         pk.data.resize(10);
         write_stripe_header(pk.data.data(), idr, frame_id, pk.y, pk.w, pk.h);
         if (idr) pk.data.insert(pk.data.end(), param_sets[s].begin(), param_sets[s].end());
-        append_nal(pk.data, idr ? 0x65 : 0x41, rbsp[s].data(), rbsp[s].size());
+        for (const auto& n : rbsp[s]) append_nal(pk.data, idr ? 0x65 : 0x41, n.data(), n.size());
         out.push_back(std::move(pk));
     }
 }
@@ -815,12 +829,13 @@ void CpuH264Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
             intra_activity(s);
         }
     ctl_.rate_control(tasks.data(), me.data());   // K10 (ratecontrol.h)
-    std::vector<std::vector<uint8_t>> rbsp(g.num_slices);
+    std::vector<std::vector<std::vector<uint8_t>>> rbsp(g.num_slices);
     // K10 accounting unit: slice RBSP payload bits (k_rc_account reads the same sizes)
     auto payload_bits = [&] {
         long long b = 0;
         for (int s = 0; s < g.num_slices; s++)
-            if (tasks[s].final_action != ACT_NONE) b += 8 * (long long)rbsp[s].size();
+            if (tasks[s].final_action != ACT_NONE)
+                for (const auto& n : rbsp[s]) b += 8 * (long long)n.size();
         return b;
     };
     for (int s = 0; s < g.num_slices; s++) {

@@ -109,6 +109,27 @@ struct SliceTask {
 };
 static_assert(sizeof(SliceTask) == 48, "SliceTask layout");
 
+// K5 parallel key frames. An I slice of a stripe wider than kIntraSubMbs macroblocks is
+// coded as sub-slices of kIntraSubMbs MBs each (consecutive in raster order, so most
+// start mid-row: first_mb_in_slice at any MB). The reference's encoders split pictures
+// the same way (num-slices 4, legacy/gstwebrtc_app.py:504, 538, 663). Since
+// kIntraSubMbs < mb_w, no MB has its top neighbour in its own sub-slice: a sub-slice
+// predicts from its left neighbours only, its reconstruction chain is at most
+// kIntraSubMbs MBs long, and the sub-slices of a stripe are independent (one wave
+// each on the GPU, k_code_intra_sub). Not with in-loop deblocking (slice-bounded
+// filtering would need the sub-slice map) or Intra4x4 (its top-right rules): those
+// keep one slice per stripe.
+constexpr int kIntraSubMbs = 40;
+SK_HD bool intra_split(const SliceTask& t, int mb_w, int deblock, int intra4x4) {
+    return t.final_action == ACT_I && mb_w > kIntraSubMbs && !deblock && !intra4x4;
+}
+// Sub-slices of a split I slice; nmb = its MBs.
+SK_HD int intra_sub_count(int nmb) { return (nmb + kIntraSubMbs - 1) / kIntraSubMbs; }
+// Upper bound of the NALs one stripe's slice can need (the GPU's per-stripe NAL slots).
+SK_HD int max_nals_per_slice(int rows_per_slice, int mb_w) {
+    return mb_w > kIntraSubMbs ? intra_sub_count(rows_per_slice * mb_w) : 1;
+}
+
 // K10: slices whose QP the rate controller sets: coded, and not a paint-over refresh
 // (CRF; under CBR the refresh is budgeted like any other slice)
 SK_HD bool rc_slice_adjustable(const SliceTask& t, int plan_qp, int mode = 1) {

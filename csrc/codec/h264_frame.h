@@ -69,8 +69,8 @@ class CpuH264Encoder {
     void code_slice_inter(int s, bool redo = false);   // redo: CBR second pass, vectors kept
     void code_slice_intra(int s);
     void code_slice_skipall(int s);
-    std::vector<uint8_t> write_slice(int s);                 // entropy + header -> RBSP
-    void package(uint16_t frame_id, std::vector<std::vector<uint8_t>>& rbsp,
+    std::vector<std::vector<uint8_t>> write_slice(int s);    // entropy + header -> RBSP of each NAL
+    void package(uint16_t frame_id, std::vector<std::vector<std::vector<uint8_t>>>& rbsp,
                  std::vector<EncodedPacket>& out);
     void finish_frame();
 
@@ -99,7 +99,9 @@ class CpuH264Encoder {
     void set_overlay_pos(int slot, int on, int x, int y, int tdx, int tdy);
 
    private:
-    void mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb) const;
+    // neighbours inside the slice; sub0 >= 0: the MB's sub-slice starts at MB index sub0
+    // (split I slice: no top neighbour, left only inside the sub-slice)
+    void mb_neighbours(int mbx, int mby, int first_row, MbNeighbours& nb, int sub0 = -1) const;
     void mc_luma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pred, int refi = 0) const;
     void mc_chroma(int mbx, int mby, int mvx, int mvy, const SliceTask& t, uint8_t* pu,
                    uint8_t* pv, int refi = 0) const;

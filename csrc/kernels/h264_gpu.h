@@ -46,9 +46,9 @@ struct FrameArgs {
     uint32_t* rbsp;        // [num_slices][rbsp_slot_words] (self-cleaning)
     int rbsp_slot_words;
     int* mb_off;           // [num_mbs] bit offset of each MB inside its slice RBSP
-    int* slice_info;       // [num_slices][4]: RBSP bytes, packet prefix bytes
-    int* tile_nz;          // [num_slices][max_tiles] last non-zero RBSP byte per EP tile
-    int* tile_ins;         // [num_slices][max_tiles] emulation-prevention insertions per tile
+    int* slice_info;       // [num_slices * nal_per_slice][4]: RBSP bytes, packet prefix bytes
+    int* tile_nz;          // [num_slices * nal_per_slice][max_tiles] last non-zero RBSP byte per EP tile
+    int* tile_ins;         // [num_slices * nal_per_slice][max_tiles] emulation-prevention insertions per tile
     int max_tiles;
     int out_slot_bytes;    // bytes per slice slot in host_out
     const uint8_t* param_sets;  // [num_slices or 1][kParamSetMax]
@@ -77,6 +77,11 @@ struct FrameArgs {
     long long* rc_slice;   // [num_slices][2] complexity sums of P-planned slices (SAD, activity)
     float rc_fps;          // session frame rate (CBR frame budget)
     int* rc_redo;          // K10 CBR guard: device flag, 1 = code the frame again (k_rc_guard)
+    // K5 sub-slices (h264_encoder.h intra_split): NAL slots per slice. slice_info / tile_nz /
+    // tile_ins are indexed by NAL (slice * nal_per_slice + sub-slice); sub-slice j's RBSP
+    // starts at word j * sub_rbsp_words of its slice's rbsp slot.
+    int nal_per_slice;
+    int sub_rbsp_words;
     const int* gate;       // second-pass launches: run only when *gate != 0 (null: always)
 };
 

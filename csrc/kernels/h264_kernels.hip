@@ -49,6 +49,20 @@ __device__ __forceinline__ int wave_sum(int v) {
            __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
 }
 
+// K5 sub-slices (h264_encoder.h intra_split): does slice t code as sub-slices, and how
+// many NALs does it produce this frame (0: not coded).
+__device__ __forceinline__ bool split_i(const FrameArgs& a, const SliceTask& t) {
+    return a.nal_per_slice > 1 && intra_split(t, a.mb_w, a.deblock, a.intra4x4);
+}
+__device__ __forceinline__ int slice_nals(const FrameArgs& a, const SliceTask& t) {
+    if (t.final_action == ACT_NONE) return 0;
+    return split_i(a, t) ? intra_sub_count(t.num_rows * a.mb_w) : 1;
+}
+// RBSP of NAL j of slice s
+__device__ __forceinline__ uint32_t* nal_rbsp(const FrameArgs& a, int s, int j) {
+    return a.rbsp + (size_t)s * a.rbsp_slot_words + (size_t)j * a.sub_rbsp_words;
+}
+
 __device__ __forceinline__ int wave_incl_scan_max(int v) {
     int l = threadIdx.x & 63;
 #pragma unroll
@@ -789,10 +803,11 @@ __global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
     for (int s = 0; s < a.num_slices; s++) a.tasks_host[s].qp = a.tasks[s].qp;
 }
 
+// per_slice > 0: sizes are per NAL, per_slice NALs per slice, counted for coded slices
 __global__ __launch_bounds__(64) void k_rc_account(FrameArgs a, const int* sizes, int n, int stride, int per_slice) {
     long long b = 0;
     for (int i = threadIdx.x; i < n; i += 64)
-        if (!per_slice || a.tasks[i].final_action != ACT_NONE) b += sizes[(size_t)i * stride];
+        if (!per_slice || i % per_slice < slice_nals(a, a.tasks[i / per_slice])) b += sizes[(size_t)i * stride];
     for (int o = 32; o > 0; o >>= 1) b += __shfl_down(b, o);
     if (threadIdx.x == 0) rc_account(*a.rc, 8 * b);
 }
@@ -805,8 +820,10 @@ __global__ __launch_bounds__(256) void k_rc_guard(FrameArgs a) {
     __shared__ long long part[4];
     const int s = blockIdx.x, tid = threadIdx.x;
     long long b = 0;
-    for (int i = tid; i < a.num_slices; i += 256)
-        if (a.tasks[i].final_action != ACT_NONE) b += a.slice_info[4 * i];
+    for (int i = tid; i < a.num_slices; i += 256) {
+        const int nn = slice_nals(a, a.tasks[i]);
+        for (int j = 0; j < nn; j++) b += a.slice_info[4 * (i * a.nal_per_slice + j)];
+    }
     for (int o = 32; o > 0; o >>= 1) b += __shfl_down(b, o);
     if ((tid & 63) == 0) part[tid >> 6] = b;
     __syncthreads();
@@ -821,9 +838,12 @@ __global__ __launch_bounds__(256) void k_rc_guard(FrameArgs a) {
             for (int i = 0; i < a.num_slices; i++) a.tasks_host[i].qp = a.tasks[i].qp;
     }
     if (!step || a.tasks[s].final_action == ACT_NONE) return;
-    uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
-    const int words = (a.slice_info[4 * s] + 3) / 4 + 1;
-    for (int i = tid; i < words; i += 256) rbsp[i] = 0u;
+    const int nn = slice_nals(a, a.tasks[s]);
+    for (int j = 0; j < nn; j++) {
+        uint32_t* rbsp = nal_rbsp(a, s, j);
+        const int words = (a.slice_info[4 * (s * a.nal_per_slice + j)] + 3) / 4 + 1;
+        for (int i = tid; i < words; i += 256) rbsp[i] = 0u;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1885,7 +1905,11 @@ __global__ __launch_bounds__(256) void k_intra_prep(FrameArgs a) {
     const int l = lane_id();
     const int b = l >> 2, r = l & 3;
     const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
-    const bool aT = mby > t.first_row, aL = mbx > 0;
+    bool aT = mby > t.first_row, aL = mbx > 0;
+    if (split_i(a, t)) {   // K5 sub-slice: left neighbour inside it only, never the top
+        aT = false;
+        aL = aL && (idx - t.first_row * a.mb_w) % kIntraSubMbs != 0;
+    }
     // source neighbours into LDS (zeros when unavailable)
     int tl, ctl[2];
     load_nb_planes(a.src, a.stride_y, a.stride_c, mbx, mby, aT, aL, nb, &tl, ctl);
@@ -2019,7 +2043,8 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
     __shared__ CavlcTables T;
     int s = blockIdx.x;
     const SliceTask t = a.tasks[s];
-    if (t.final_action != ACT_I) return;   // block-uniform: P/skipped slices leave before the table load
+    // block-uniform: P/skipped slices and K5 sub-sliced ones (k_code_intra_sub) leave before the table load
+    if (t.final_action != ACT_I || split_i(a, t)) return;
 #ifdef SK_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     const unsigned long long c_start = __builtin_amdgcn_s_memtime();
@@ -2195,6 +2220,108 @@ __global__ __launch_bounds__(64 * (MAXROWS + 1)) void k_code_intra(FrameArgs a) 
 }
 
 // ---------------------------------------------------------------------------
+// K5+K6 intra of sub-sliced I slices (h264_encoder.h intra_split): one wave per
+// sub-slice of kIntraSubMbs MBs. No MB has its top neighbour in its sub-slice, so a
+// wave's chain is its MBs in raster order, predicting from the left neighbour's right
+// column only (kept in the wave's LDS), and the sub-slices of every slice run in
+// parallel (1080p: 17 slices x 12 sub-slices = 204 waves of at most 40 steps, where
+// k_code_intra's wavefront is 17 chains of 126 steps). Modes and start QPs come from
+// k_intra_prep; the next MB's source samples and decisions are loaded before the
+// current MB is coded.
+__global__ __launch_bounds__(256) void k_code_intra_sub(FrameArgs a) {
+    if (a.gate && *a.gate == 0) return;   // CBR second pass not needed
+    __shared__ MbScratch Sw[4];
+    __shared__ uint8_t right_y[4][16];
+    __shared__ uint8_t right_c[4][2][8];
+    __shared__ CavlcTables T;
+    const int w = threadIdx.x >> 6, l = lane_id();
+    const int gw = blockIdx.x * 4 + w;
+    const int s = gw / a.nal_per_slice, j = gw % a.nal_per_slice;
+    bool mine = false;
+    SliceTask t;
+    if (s < a.num_slices) {
+        t = a.tasks[s];
+        mine = split_i(a, t) && j < intra_sub_count(t.num_rows * a.mb_w);
+    }
+    if (!__syncthreads_or(mine)) return;
+    load_cavlc_tables(T, a.cavlc_tabs);
+    __syncthreads();
+    if (!mine) return;
+    MbScratch& S = Sw[w];
+    const int b = l >> 2, r = l & 3;
+    const int cl = l & 31, comp = cl >> 4, cb = (cl >> 2) & 3;
+    const int lx = blk_x(b) * 4, ly = blk_y(b) * 4 + r;
+    const int clx = (cb & 1) * 4, cly = (cb >> 1) * 4 + r;
+    const int first = t.first_row * a.mb_w;
+    const int k0 = j * kIntraSubMbs, k1 = sk_min(t.num_rows * a.mb_w, k0 + kIntraSubMbs);
+    const uint8_t* cplane = comp ? a.src.v : a.src.u;
+    // source samples + pre-pass decisions of MB k (lane layout of code_mb)
+    auto fetch = [&](int k, uint32_t& sw, uint32_t& csw, MbInfo& pre) {
+        const int idx = first + k, mbx = idx % a.mb_w, mby = idx / a.mb_w;
+        sw = *reinterpret_cast<const uint32_t*>(a.src.y + (size_t)(mby * 16 + ly) * a.stride_y + mbx * 16 + lx);
+        csw = *reinterpret_cast<const uint32_t*>(cplane + (size_t)(mby * 8 + cly) * a.stride_c + mbx * 8 + clx);
+        pre = a.mbs[idx];
+    };
+    uint32_t sw, csw;
+    MbInfo pre;
+    fetch(k0, sw, csw, pre);
+    const int zc[2] = {0, 0};
+    for (int k = k0; k < k1; k++) {
+        const int idx = first + k, mbx = idx % a.mb_w, mby = idx / a.mb_w;
+        const bool aL = mbx > 0 && k > k0;
+        const int mode = __builtin_amdgcn_readfirstlane(pre.i16_mode);
+        const int cmode = __builtin_amdgcn_readfirstlane(pre.chroma_mode);
+        const int start_qp = __builtin_amdgcn_readfirstlane(pre.qp);
+        int src_l[4], src_c[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            src_l[q] = (sw >> (8 * q)) & 255;
+            src_c[q] = (csw >> (8 * q)) & 255;
+        }
+        if (k + 1 < k1) fetch(k + 1, sw, csw, pre);   // in flight while this MB is coded
+        // neighbours: top unavailable (zeros), left = the previous MB's right column
+        uint8_t* nb = S.nb;
+        {
+            int v = 0;
+            if (l >= 16 && l < 32) v = aL ? right_y[w][l - 16] : 0;
+            else if (l >= 48) v = aL ? right_c[w][(l >> 3) & 1][l & 7] : 0;
+            nb[l] = (uint8_t)v;
+        }
+        wave_sync();
+        int pred_l[4], pred_c[4];
+        intra_pred_lanes(mode, cmode, nb, 0, zc, false, aL, pred_l, pred_c);
+        MbInfo mb;
+        memset(&mb, 0, sizeof(mb));
+        mb.type = MB_I16x16;
+        mb.i16_mode = (uint8_t)mode;
+        mb.chroma_mode = (uint8_t)cmode;
+        int rec_l[4], rec_c[4];
+        code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c, a.coefs + (size_t)idx * kCoefPerMb, T,
+                nullptr, 0, start_qp);
+        wave_sync();
+        if (lx + 3 == 15) right_y[w][ly] = (uint8_t)rec_l[3];
+        if (l < 32 && clx + 3 == 7) right_c[w][comp][cly] = (uint8_t)rec_c[3];
+        const int px = mbx * 16 + lx, py = mby * 16 + ly;
+        *reinterpret_cast<uint32_t*>(a.rec.y + (size_t)py * a.stride_y + px) =
+            (uint32_t)rec_l[0] | ((uint32_t)rec_l[1] << 8) | ((uint32_t)rec_l[2] << 16) | ((uint32_t)rec_l[3] << 24);
+        if (l < 32) {
+            uint8_t* crp = comp ? a.rec.v : a.rec.u;
+            *reinterpret_cast<uint32_t*>(crp + (size_t)(mby * 8 + cly) * a.stride_c + mbx * 8 + clx) =
+                (uint32_t)rec_c[0] | ((uint32_t)rec_c[1] << 8) | ((uint32_t)rec_c[2] << 16) | ((uint32_t)rec_c[3] << 24);
+        }
+        if (l == 0) {
+            for (int i = 0; i < 24; i++) mb.nnz[i] = S.nnz[i];
+            a.mbs[idx] = mb;
+            a.me[idx].mvx = 0;
+            a.me[idx].mvy = 0;
+            a.me[idx].ref = 0;
+            a.me[idx].fx = a.me[idx].fy = 0;
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K8: CAVLC, one wave per coded MB.
 // 4 waves per workgroup, one MB per wave (tables shared). Lanes 0..26 each code one
 // residual block ONCE into a private LDS stage; a wave scan of the bit counts gives
@@ -2229,6 +2356,7 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
     }
     bool p_slice = t.final_action == ACT_P;
     int first = t.first_row * a.mb_w;
+    if (split_i(a, t)) first += ((idx - first) / kIntraSubMbs) * kIntraSubMbs;   // K5: the MB's sub-slice
     // mb_skip_run: skipped MBs since the previous coded MB of the slice
     int run = 0;
     if (p_slice) {
@@ -2272,8 +2400,8 @@ __global__ __launch_bounds__(256) void k_cavlc(FrameArgs a) {
         reinterpret_cast<uint32_t*>(coef)[i] = reinterpret_cast<const uint32_t*>(gc)[i];
     wave_sync();
     MbNeighbours nb;
-    nb.left = mbx > 0 ? &a.mbs[idx - 1] : nullptr;
-    nb.top = mby > t.first_row ? &a.mbs[idx - a.mb_w] : nullptr;
+    nb.left = mbx > 0 && idx - 1 >= first ? &a.mbs[idx - 1] : nullptr;
+    nb.top = mby > t.first_row && idx - a.mb_w >= first ? &a.mbs[idx - a.mb_w] : nullptr;
     int hdr_bits = 0;
     if (l == 0) {
         AtomicBitWriter w{bits, 0};
@@ -2365,20 +2493,25 @@ __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
     __shared__ uint32_t hdr[32];
     __shared__ int wave_tot[5];
     __shared__ int sh_misc[4];
-    const int s = blockIdx.x, tid = threadIdx.x;
+    // one workgroup per NAL slot: slice s, sub-slice j (K5; j = 0 is the whole slice otherwise)
+    const int nal = blockIdx.x, s = nal / a.nal_per_slice, j = nal % a.nal_per_slice, tid = threadIdx.x;
     const SliceTask task = a.tasks[s];
     const int fin = task.final_action;
-    int* info = a.slice_info + 4 * s;
-    if (fin == ACT_NONE) {
+    int* info = a.slice_info + 4 * nal;
+    const int nn = slice_nals(a, task);
+    if (j >= nn) {
         if (tid == 0) {
             info[0] = 0;
-            a.host_size[s] = 0;
+            info[1] = 0;
+            if (j == 0) a.host_size[s] = 0;
         }
         return;
     }
-    const int nmb = task.num_rows * a.mb_w;
-    const int first = task.first_row * a.mb_w;
-    uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    const int snmb = task.num_rows * a.mb_w;
+    const int k0 = nn > 1 ? j * kIntraSubMbs : 0;
+    const int nmb = nn > 1 ? sk_min(snmb, k0 + kIntraSubMbs) - k0 : snmb;
+    const int first = task.first_row * a.mb_w + k0;
+    uint32_t* rbsp = nal_rbsp(a, s, j);
     const bool intra = fin == ACT_I;
     const bool idr = intra && task.idr_on_intra;
     if (tid < 32) hdr[tid] = 0;
@@ -2387,7 +2520,7 @@ __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
     if (tid == 0) {
         AtomicBitWriter w{hdr, 0};
         SliceHeaderParams h;
-        h.first_mb = a.fullframe ? first : 0;
+        h.first_mb = (a.fullframe ? task.first_row * a.mb_w : 0) + k0;
         h.slice_type = intra ? 2 : 0;
         h.idr = idr;
         h.frame_num = idr ? 0 : task.frame_num;
@@ -2428,27 +2561,30 @@ __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
         }
         w.put(1, 1);  // rbsp_stop_one_bit
         info[0] = (int)((w.pos + 7) >> 3);
-        // packet prefix, written directly into the host-mapped slot
-        uint8_t* slot = a.host_out + (size_t)s * a.out_slot_bytes;
-        int p = 0;
-        if (!a.fullframe) {
-            const int y = task.first_row * 16;
-            const int h = sk_min(a.H, (task.first_row + task.num_rows) * 16) - y;
-            const int fid = a.frame_params_dev[0];
-            uint8_t pre[10] = {0x04, (uint8_t)(idr ? 1 : 0), (uint8_t)(fid >> 8), (uint8_t)fid, (uint8_t)(y >> 8),
-                               (uint8_t)y, (uint8_t)(a.W >> 8), (uint8_t)a.W, (uint8_t)(h >> 8), (uint8_t)h};
-            for (int i = 0; i < 10; i++) slot[i] = pre[i];
-            p = 10;
-            if (idr) {
-                const int len = a.param_set_len[s];
-                const uint8_t* ps = a.param_sets + (size_t)s * a.param_set_stride;
-                for (int i = 0; i < len; i++) slot[p + i] = ps[i];
-                p += len;
+        if (j > 0) {   // start code + NAL header: written by k_ep_write once the NALs before it are sized
+            info[1] = 5;
+        } else {       // packet prefix, written directly into the host-mapped slot
+            uint8_t* slot = a.host_out + (size_t)s * a.out_slot_bytes;
+            int p = 0;
+            if (!a.fullframe) {
+                const int y = task.first_row * 16;
+                const int h = sk_min(a.H, (task.first_row + task.num_rows) * 16) - y;
+                const int fid = a.frame_params_dev[0];
+                uint8_t pre[10] = {0x04, (uint8_t)(idr ? 1 : 0), (uint8_t)(fid >> 8), (uint8_t)fid, (uint8_t)(y >> 8),
+                                   (uint8_t)y, (uint8_t)(a.W >> 8), (uint8_t)a.W, (uint8_t)(h >> 8), (uint8_t)h};
+                for (int i = 0; i < 10; i++) slot[i] = pre[i];
+                p = 10;
+                if (idr) {
+                    const int len = a.param_set_len[s];
+                    const uint8_t* ps = a.param_sets + (size_t)s * a.param_set_stride;
+                    for (int i = 0; i < len; i++) slot[p + i] = ps[i];
+                    p += len;
+                }
             }
+            slot[p++] = 0; slot[p++] = 0; slot[p++] = 0; slot[p++] = 1;
+            slot[p++] = idr ? 0x65 : 0x41;
+            info[1] = p;
         }
-        slot[p++] = 0; slot[p++] = 0; slot[p++] = 0; slot[p++] = 1;
-        slot[p++] = idr ? 0x65 : 0x41;
-        info[1] = p;
     }
 }
 
@@ -2457,16 +2593,18 @@ __global__ __launch_bounds__(256) void k_mb_concat(FrameArgs a) {
     const int mb = blockIdx.x * 4 + w;
     if (mb >= a.mb_w * a.mb_h) return;
     const int s = (mb / a.mb_w) / a.rows_per_slice;
-    const int fin = a.tasks[s].final_action;
+    const SliceTask& task = a.tasks[s];
+    const int fin = task.final_action;
     if (fin == ACT_NONE || fin == ACT_SKIPALL) return;
     const int nb = a.mb_nbits[mb];
     if (nb <= 0) return;
+    const int sub = split_i(a, task) ? (mb - task.first_row * a.mb_w) / kIntraSubMbs : 0;   // K5 NAL of the MB
     const int p = a.mb_off[mb];
     const int w0 = p >> 5, w1 = (p + nb - 1) >> 5, sh = p & 31;
     const int nw = (nb + 31) >> 5;
     const uint32_t lastmask = (nb & 31) ? ~0u << (32 - (nb & 31)) : ~0u;
     const uint32_t* src = a.mb_bits + (size_t)mb * (kMbSlotBytes / 4);
-    uint32_t* dst = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    uint32_t* dst = nal_rbsp(a, s, sub);
     for (int j = w0 + l; j <= w1; j += 64) {
         const int k = j - w0;
         uint32_t lo = k < nw ? src[k] : 0u;
@@ -2494,12 +2632,12 @@ __device__ __forceinline__ uint8_t rbsp_byte(uint32_t word, int q) { return (uin
 
 __global__ __launch_bounds__(256) void k_ep_nz(FrameArgs a) {
     __shared__ int red[4];
-    const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x;
-    if (a.tasks[s].final_action == ACT_NONE) return;
-    const int n = a.slice_info[4 * s];
+    const int nal = blockIdx.y, s = nal / a.nal_per_slice, j = nal % a.nal_per_slice, t = blockIdx.x, tid = threadIdx.x;
+    if (j >= slice_nals(a, a.tasks[s])) return;
+    const int n = a.slice_info[4 * nal];
     const int t0 = t * kTile;
     if (t0 >= n) return;
-    const uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    const uint32_t* rbsp = nal_rbsp(a, s, j);
     const int i0 = t0 + tid * 16;
     int lastnz = -1;
 #pragma unroll
@@ -2513,7 +2651,7 @@ __global__ __launch_bounds__(256) void k_ep_nz(FrameArgs a) {
     for (int o = 32; o > 0; o >>= 1) lastnz = max(lastnz, __shfl_down(lastnz, o));
     if (lane_id() == 0) red[tid >> 6] = lastnz;
     __syncthreads();
-    if (tid == 0) a.tile_nz[s * a.max_tiles + t] = max(max(red[0], red[1]), max(red[2], red[3]));
+    if (tid == 0) a.tile_nz[nal * a.max_tiles + t] = max(max(red[0], red[1]), max(red[2], red[3]));
 }
 
 // Per-thread EP decisions for 16 bytes starting at i0; `carry` = last non-zero
@@ -2560,50 +2698,63 @@ __device__ __forceinline__ int ep_thread(const uint32_t* rbsp, int n, int t0, in
     return ins;
 }
 
-__device__ __forceinline__ int tile_carry(const FrameArgs& a, int s, int t) {
+__device__ __forceinline__ int tile_carry(const FrameArgs& a, int nal, int t) {
     int c = -1;  // the NAL header byte before the RBSP is non-zero
-    for (int k = 0; k < t; k++) c = max(c, a.tile_nz[s * a.max_tiles + k]);
+    for (int k = 0; k < t; k++) c = max(c, a.tile_nz[nal * a.max_tiles + k]);
     return c;
 }
 
 __global__ __launch_bounds__(256) void k_ep_count(FrameArgs a) {
     __shared__ int scan_lds[4];
     __shared__ int red[4];
-    const int s = blockIdx.y, t = blockIdx.x;
-    if (a.tasks[s].final_action == ACT_NONE) return;
-    const int n = a.slice_info[4 * s];
+    const int nal = blockIdx.y, s = nal / a.nal_per_slice, j = nal % a.nal_per_slice, t = blockIdx.x;
+    if (j >= slice_nals(a, a.tasks[s])) return;
+    const int n = a.slice_info[4 * nal];
     const int t0 = t * kTile;
     if (t0 >= n) return;
-    const uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    const uint32_t* rbsp = nal_rbsp(a, s, j);
     uint8_t by[16];
     uint32_t mask;
-    int ins = ep_thread(rbsp, n, t0, tile_carry(a, s, t), scan_lds, by, &mask);
+    int ins = ep_thread(rbsp, n, t0, tile_carry(a, nal, t), scan_lds, by, &mask);
     for (int o = 32; o > 0; o >>= 1) ins += __shfl_down(ins, o);
     if (lane_id() == 0) red[threadIdx.x >> 6] = ins;
     __syncthreads();
-    if (threadIdx.x == 0) a.tile_ins[s * a.max_tiles + t] = red[0] + red[1] + red[2] + red[3];
+    if (threadIdx.x == 0) a.tile_ins[nal * a.max_tiles + t] = red[0] + red[1] + red[2] + red[3];
 }
 
 __global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
     __shared__ int scan_lds[4];
     __shared__ int wave_tot[5];
-    __shared__ int sh_before;
+    __shared__ int sh_before, sh_base;
     __shared__ uint8_t sOut[kTile + kTile / 2 + 16];
-    const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x;
-    if (a.tasks[s].final_action == ACT_NONE) return;
-    const int n = a.slice_info[4 * s];
+    const int nal = blockIdx.y, s = nal / a.nal_per_slice, j = nal % a.nal_per_slice, t = blockIdx.x, tid = threadIdx.x;
+    const SliceTask& task = a.tasks[s];
+    const int nn = slice_nals(a, task);
+    if (j >= nn) return;
+    const int n = a.slice_info[4 * nal];
     const int t0 = t * kTile;
     if (t0 >= n) return;
     if (tid < 64) {
         int b = 0;
-        for (int k = tid; k < t; k += 64) b += a.tile_ins[s * a.max_tiles + k];
+        for (int k = tid; k < t; k += 64) b += a.tile_ins[nal * a.max_tiles + k];
         b = wave_sum(b);
-        if (tid == 0) sh_before = b;
+        // K5: the slot bytes of the NALs before this one (prefix + RBSP + insertions)
+        int base = 0;
+        for (int jj = 0; jj < j; jj++) {
+            const int q = s * a.nal_per_slice + jj, nq = a.slice_info[4 * q];
+            int ins_q = 0;
+            for (int k = tid; k * kTile < nq; k += 64) ins_q += a.tile_ins[q * a.max_tiles + k];
+            base += a.slice_info[4 * q + 1] + nq + wave_sum(ins_q);
+        }
+        if (tid == 0) {
+            sh_before = b;
+            sh_base = base;
+        }
     }
-    uint32_t* rbsp = a.rbsp + (size_t)s * a.rbsp_slot_words;
+    uint32_t* rbsp = nal_rbsp(a, s, j);
     uint8_t by[16];
     uint32_t mask;
-    const int ins = ep_thread(rbsp, n, t0, tile_carry(a, s, t), scan_lds, by, &mask);
+    const int ins = ep_thread(rbsp, n, t0, tile_carry(a, nal, t), scan_lds, by, &mask);
     int tile_ins;
     const int ex = block_excl_scan<4>(ins, wave_tot, &tile_ins);
     const int i0 = t0 + tid * 16;
@@ -2621,8 +2772,13 @@ __global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
         if (i0 + 4 * q < n) rbsp[(i0 >> 2) + q] = 0u;
     __syncthreads();
     const int len = sk_min(n - t0, kTile) + tile_ins;
-    const int g0 = a.slice_info[4 * s + 1] + t0 + sh_before;
+    const int g0 = sh_base + a.slice_info[4 * nal + 1] + t0 + sh_before;
     uint8_t* dst = a.host_out + (size_t)s * a.out_slot_bytes;
+    if (j > 0 && t == 0 && tid == 0) {   // this NAL's start code and header
+        const bool idr = task.final_action == ACT_I && task.idr_on_intra;
+        dst[sh_base] = 0; dst[sh_base + 1] = 0; dst[sh_base + 2] = 0; dst[sh_base + 3] = 1;
+        dst[sh_base + 4] = idr ? 0x65 : 0x41;
+    }
     const int head = sk_min(len, (16 - (g0 & 15)) & 15);
     if (tid < head) dst[g0 + tid] = sOut[tid];
     const int nvec = (len - head) >> 4;
@@ -2637,7 +2793,7 @@ __global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
     }
     const int tail0 = head + 16 * nvec;
     if (tid < len - tail0) dst[g0 + tail0 + tid] = sOut[tail0 + tid];
-    if (t0 + kTile >= n && tid == 0) a.host_size[s] = g0 + len;
+    if (j == nn - 1 && t0 + kTile >= n && tid == 0) a.host_size[s] = g0 + len;
 }
 
 // ---------------------------------------------------------------------------
@@ -3018,8 +3174,10 @@ static void launch_code(const FrameArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_code_intra<4>, dim3(a.num_slices), dim3(64 * 5), 0, s, a);
     else
         hipLaunchKernelGGL(k_code_intra<kMaxRows - 1>, dim3(a.num_slices), dim3(64 * kMaxRows), 0, s, a);
+    if (a.nal_per_slice > 1)   // K5 sub-sliced I slices: one wave per sub-slice
+        hipLaunchKernelGGL(k_code_intra_sub, dim3((a.num_slices * a.nal_per_slice + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_cavlc, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_slice_scan, dim3(a.num_slices), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_slice_scan, dim3(a.num_slices * a.nal_per_slice), dim3(256), 0, s, a);
 }
 
 void launch_encode(const FrameArgs& a, hipStream_t s, bool guard) {
@@ -3034,11 +3192,11 @@ void launch_encode(const FrameArgs& a, hipStream_t s, bool guard) {
         launch_code(b, s);
     }
     hipLaunchKernelGGL(k_mb_concat, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
-    const dim3 tiles(a.max_tiles, a.num_slices);
+    const dim3 tiles(a.max_tiles, a.num_slices * a.nal_per_slice);
     hipLaunchKernelGGL(k_ep_nz, tiles, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_ep_count, tiles, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_ep_write, tiles, dim3(256), 0, s, a);
-    launch_rc_account(a, a.slice_info, a.num_slices, 4, 1, s);
+    launch_rc_account(a, a.slice_info, a.num_slices * a.nal_per_slice, 4, a.nal_per_slice, s);
 }
 
 void launch_commit(const FrameArgs& a, hipStream_t s) {

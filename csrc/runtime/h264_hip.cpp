@@ -548,13 +548,18 @@ class HipBackend : public EncoderBackend {
         a.mb_bits = dmalloc<uint32_t>((size_t)nmb * (gpu::kMbSlotBytes / 4));
         a.mb_nbits = dmalloc<int>(nmb);
         int max_slice_mbs = g_.rows_per_slice * g_.mb_w;
-        a.rbsp_slot_words = (max_slice_mbs * gpu::kMbSlotBytes + 1024) / 4;
+        // K5: split I slices put one NAL per sub-slice (h264_encoder.h intra_split)
+        const bool can_split = cfg_.codec == 0 && g_.mb_w > kIntraSubMbs && !cfg_.deblock && !a.intra4x4;
+        a.nal_per_slice = can_split ? max_nals_per_slice(g_.rows_per_slice, g_.mb_w) : 1;
+        a.sub_rbsp_words = (kIntraSubMbs * gpu::kMbSlotBytes + 1024) / 4;
+        a.rbsp_slot_words = std::max((max_slice_mbs * gpu::kMbSlotBytes + 1024) / 4,
+                                     can_split ? a.nal_per_slice * a.sub_rbsp_words : 0);
         a.rbsp = dmalloc<uint32_t>((size_t)ns * a.rbsp_slot_words);
         a.mb_off = dmalloc<int>(nmb);
-        a.slice_info = dmalloc<int>(4 * (size_t)ns);
+        a.slice_info = dmalloc<int>(4 * (size_t)ns * a.nal_per_slice);
         a.max_tiles = (a.rbsp_slot_words * 4 + 4095) / 4096;
-        a.tile_nz = dmalloc<int>((size_t)ns * a.max_tiles);
-        a.tile_ins = dmalloc<int>((size_t)ns * a.max_tiles);
+        a.tile_nz = dmalloc<int>((size_t)ns * a.nal_per_slice * a.max_tiles);
+        a.tile_ins = dmalloc<int>((size_t)ns * a.nal_per_slice * a.max_tiles);
         // worst case: header + SPS/PPS + 3/2 emulation-prevention growth, 64-byte multiple
         size_t slot = ((size_t)a.rbsp_slot_words * 4 * 3 / 2 + 1024 + 63) & ~(size_t)63;
         a.out_slot_bytes = (int)slot;
