@@ -118,7 +118,8 @@ struct BlkInfo {
     uint8_t uv_mode;   // UVMode (intra)
     uint8_t flags;     // bit0 is_inter, bit1 skip, bit2 merged-static (encoder), bits 4-5 RefMvIdx
     int16_t mv_row, mv_col;   // 1/8 pel (LAST), even values (no high-precision MVs)
-    int16_t pad0, pad1;
+    int16_t tx_type;   // luma transform type: TX_DCT_DCT (0) or TX_IDTX (1); inter chroma follows it
+    int16_t pad1;
 };
 static_assert(sizeof(BlkInfo) == 12, "BlkInfo layout");
 SK_HD bool blk_inter(const BlkInfo& b) { return (b.flags & 1) != 0; }
@@ -275,15 +276,28 @@ SK_HD void idct_1d(int32_t* x, int log2n) {
     else idct16(x);
 }
 
-// 2-D inverse DCT_DCT of an n x n block (n = 4, 8, 16): dequantised coefficients
-// `d` (raster [row][col], row = vertical frequency) -> residual `r`.
-SK_HD void inv_transform(const int32_t* d, int log2n, int32_t* r) {
+// Identity transform (IDTX, the screen-content transform): inverse of spec 7.13.2.15
+// for n = 4 / 8 / 16; the forward identity is 8 x the residual (the coefficient domain
+// of the DCT path: 8 x orthonormal, so one quantiser serves both).
+SK_HD int32_t iidentity(int32_t x, int log2n) {
+    if (log2n == 2) return (int32_t)(((int64_t)x * 5793 + 2048) >> 12);
+    if (log2n == 3) return x * 2;
+    return (int32_t)(((int64_t)x * 11586 + 2048) >> 12);
+}
+enum TxType : int { TX_DCT_DCT = 0, TX_IDTX = 1 };
+
+// 2-D inverse DCT_DCT (or IDTX) of an n x n block (n = 4, 8, 16): dequantised
+// coefficients `d` (raster [row][col], row = vertical frequency) -> residual `r`.
+SK_HD void inv_transform(const int32_t* d, int log2n, int32_t* r, bool idtx = false) {
     const int n = 1 << log2n;
     const int row_shift = log2n == 2 ? 0 : (log2n == 3 ? 1 : 2);
     int32_t t[16];
     for (int i = 0; i < n; i++) {
         for (int j = 0; j < n; j++) t[j] = d[i * n + j];
-        idct_1d(t, log2n);
+        if (idtx)
+            for (int j = 0; j < n; j++) t[j] = iidentity(t[j], log2n);
+        else
+            idct_1d(t, log2n);
         for (int j = 0; j < n; j++) {
             const int32_t v = row_shift ? (t[j] + (1 << (row_shift - 1))) >> row_shift : t[j];
             r[i * n + j] = sk_clip(v, -32768, 32767);   // colClampRange = 16 bits (8-bit video)
@@ -291,7 +305,10 @@ SK_HD void inv_transform(const int32_t* d, int log2n, int32_t* r) {
     }
     for (int j = 0; j < n; j++) {
         for (int i = 0; i < n; i++) t[i] = r[i * n + j];
-        idct_1d(t, log2n);
+        if (idtx)
+            for (int i = 0; i < n; i++) t[i] = iidentity(t[i], log2n);
+        else
+            idct_1d(t, log2n);
         for (int i = 0; i < n; i++) r[i * n + j] = (t[i] + 8) >> 4;
     }
 }
@@ -357,6 +374,22 @@ SK_HD int quantize(int32_t c, int q, bool intra) {
     const int lc = l > 4095 ? 4095 : l;
     return c < 0 ? -lc : lc;
 }
+// Transform-type decision (encoder choice): J = 256 x (SSE + lambda x bits) for the
+// levels of one transform type, lambda = 0.136 x (ac_q / 8)^2 (x264's SSE lambda at the
+// same quantiser step). dist4 = 4 x sum of squared coefficient errors (the coefficient
+// domain is 8 x orthonormal: pixel SSE = coefficient SSE / 64); rate2 in half bits from
+// tx_bits2 over the scan up to the end of block plus tx_eob_bits2.
+SK_HD int tx_bits2(int level) {
+    const int a = level < 0 ? -level : level;
+    if (a == 0) return 1;
+    if (a == 1) return 6;
+    return 8 + 4 * (31 - __builtin_clz((unsigned)a));
+}
+SK_HD int tx_eob_bits2(int eob) { return eob ? 2 * (32 - __builtin_clz((unsigned)eob)) + 2 : 0; }
+SK_HD long long tx_rd_cost(long long dist4, int rate2, int qa) {
+    return dist4 + (((long long)qa * qa * rate2 * 70) >> 8);
+}
+
 // qindex -> coefficient CDF context (§7.20: <= 20, <= 60, <= 120, else)
 SK_HD int coef_qctx(int qidx) { return qidx <= 20 ? 0 : (qidx <= 60 ? 1 : (qidx <= 120 ? 2 : 3)); }
 // Frame qindex of a rate-controlled frame at fractional QP qpf (Q8, ratecontrol.h):
@@ -881,7 +914,7 @@ SK_HD void trim_tail(int16_t* lev, int log2n) {
 
 template <class Sink>
 SK_HD int code_coeffs(Sink& w, const CdfContext& cx, const int16_t* lev, int txs, int plane, CoefCtx cc,
-                      bool is_inter, int intra_dir, int qidx) {
+                      bool is_inter, int intra_dir, int qidx, int tx_type = TX_DCT_DCT) {
     const int log2n = txs + 2, n = 1 << log2n, nn = n * n;
     const int ptype = plane > 0;
     // eob = 1 + last nonzero scan index
@@ -893,9 +926,10 @@ SK_HD int code_coeffs(Sink& w, const CdfContext& cx, const int16_t* lev, int txs
         }
     w.sym(cdf_off(cx, cx.txb_skip[txs][cc.txb_skip]), 2, eob == 0);
     if (eob == 0) return 0;
-    if (plane == 0 && qidx > 0) {   // transform_type: DCT_DCT (index 1 of the reduced sets)
-        if (is_inter) w.sym(cdf_off(cx, cx.inter_tx_set3[txs]), 2, 1);
-        else w.sym(cdf_off(cx, cx.intra_tx_set2[txs][intra_dir]), 5, 1);
+    if (plane == 0 && qidx > 0) {   // transform_type: IDTX = index 0, DCT_DCT = 1 of the reduced sets
+        const int sym = tx_type == TX_IDTX ? 0 : 1;
+        if (is_inter) w.sym(cdf_off(cx, cx.inter_tx_set3[txs]), 2, sym);
+        else w.sym(cdf_off(cx, cx.intra_tx_set2[txs][intra_dir]), 5, sym);
     }
     const int eob_multi = 2 * log2n - 4;   // log2(nn) - 4
     const int eob_pt = eob_pt_of(eob);
@@ -1138,7 +1172,8 @@ SK_HD void code_block(Sink& w, const CdfContext& cx, const FrameView& v, const T
         }
     }
     if (blk_skip(b)) return;
-    code_coeffs(w, cx, v.levels(r, c, bsl, 0), bsl, 0, coef_ctx(v, t, 0, c, r, 1 << bsl), blk_inter(b), b.mode, v.qidx);
+    code_coeffs(w, cx, v.levels(r, c, bsl, 0), bsl, 0, coef_ctx(v, t, 0, c, r, 1 << bsl), blk_inter(b), b.mode, v.qidx,
+                b.tx_type);
     for (int p = 1; p < 3; p++)
         code_coeffs(w, cx, v.levels(r, c, bsl, p), bsl - 1, p, coef_ctx(v, t, p, c >> 1, r >> 1, (1 << bsl) >> 1),
                     blk_inter(b), b.mode, v.qidx);

@@ -236,31 +236,76 @@ static uint8_t level_summary(const int16_t* lv, int nn) {
     return (uint8_t)(sk_min(cul, 63) | (dc << 6));
 }
 
-// Residual of one n x n block of `plane` at (x, y): transform + quantise against
-// `pred`, reconstruct into fe.rec. Levels to `lv`; returns whether any is nonzero.
-static bool code_residual(const uint8_t* src, int sstride, const uint8_t* pred, int log2n, int qidx, bool intra,
-                          int16_t* lv, uint8_t* rec, int rstride) {
+// Levels of one n x n block against `pred` for transform type tt (TX_DCT_DCT / TX_IDTX)
+// and their RD cost (av1_core.h tx_rd_cost; k_av1_inter / k_av1_intra_rec compute the same).
+static long long quant_block(const uint8_t* src, int sstride, const uint8_t* pred, int log2n, int qidx, bool intra,
+                             int tt, int16_t* lv) {
     const int n = 1 << log2n, nn = n * n;
-    int32_t res[256], co[256], dq[256], rr[256];
+    int32_t res[256], co[256];
     for (int i = 0; i < n; i++)
         for (int j = 0; j < n; j++) res[i * n + j] = (int)src[(size_t)i * sstride + j] - (int)pred[i * n + j];
-    fwd_transform(res, log2n, co);
+    if (tt == TX_IDTX)
+        for (int k = 0; k < nn; k++) co[k] = 8 * res[k];
+    else
+        fwd_transform(res, log2n, co);
+    const int qd = dc_q(qidx), qa = ac_q(qidx);
+    long long d = 0;
+    for (int k = 0; k < nn; k++) {
+        const int q = k == 0 ? qd : qa;
+        lv[k] = (int16_t)quantize(co[k], q, intra);
+        const long long e = (long long)co[k] - dequant(lv[k], q);
+        d += e * e;
+    }
+    int eob = 0;
+    for (int c = nn - 1; c >= 0 && !eob; c--)
+        if (lv[default_scan(log2n, c)]) eob = c + 1;
+    int r2 = tx_eob_bits2(eob);
+    for (int c = 0; c < eob; c++) r2 += tx_bits2(lv[default_scan(log2n, c)]);
+    return tx_rd_cost(4 * d, r2, qa);
+}
+
+// Inter tail trimming, dequantisation and reconstruction of a block's levels into rec
+// (pred where all levels are zero); returns whether any level is nonzero.
+static bool recon_block(int16_t* lv, int log2n, int qidx, bool intra, int tt, const uint8_t* pred, uint8_t* rec,
+                        int rstride) {
+    const int n = 1 << log2n, nn = n * n;
+    int32_t dq[256], rr[256];
+    if (!intra) trim_tail(lv, log2n);
     const int qd = dc_q(qidx), qa = ac_q(qidx);
     bool nz = false;
-    for (int k = 0; k < nn; k++) lv[k] = (int16_t)quantize(co[k], k == 0 ? qd : qa, intra);
-    if (!intra) trim_tail(lv, log2n);
     for (int k = 0; k < nn; k++) {
         nz |= lv[k] != 0;
         dq[k] = dequant(lv[k], k == 0 ? qd : qa);
     }
     if (nz) {
-        inv_transform(dq, log2n, rr);
+        inv_transform(dq, log2n, rr, tt == TX_IDTX);
         for (int i = 0; i < n; i++)
             for (int j = 0; j < n; j++) rec[(size_t)i * rstride + j] = (uint8_t)sk_clip255(pred[i * n + j] + rr[i * n + j]);
     } else {
         for (int i = 0; i < n; i++) memcpy(rec + (size_t)i * rstride, pred + i * n, (size_t)n);
     }
     return nz;
+}
+
+static bool any_nonzero(const int16_t* lv, int nn) {
+    for (int k = 0; k < nn; k++)
+        if (lv[k]) return true;
+    return false;
+}
+// A transform type is only coded with nonzero luma levels; an inter block without them
+// has DCT_DCT chroma (TxTypes of an all-zero luma block, spec transform_block).
+static bool any_after_trim(const int16_t* lv, int log2n) {
+    int16_t t[256];
+    memcpy(t, lv, sizeof(int16_t) << (2 * log2n));
+    trim_tail(t, log2n);
+    return any_nonzero(t, 1 << (2 * log2n));
+}
+
+// DCT_DCT with the reconstruction (chroma of intra blocks: UV_DC_PRED implies DCT_DCT).
+static bool code_residual(const uint8_t* src, int sstride, const uint8_t* pred, int log2n, int qidx, bool intra,
+                          int16_t* lv, uint8_t* rec, int rstride) {
+    quant_block(src, sstride, pred, log2n, qidx, intra, TX_DCT_DCT, lv);
+    return recon_block(lv, log2n, qidx, intra, TX_DCT_DCT, pred, rec, rstride);
 }
 
 // Key frames: DC / V / H / SMOOTH / SMOOTH_V / SMOOTH_H / PAETH by SAD. The mode is
@@ -301,8 +346,14 @@ void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
     uint8_t py[256];
     intra_predict(ey, b.mode, log2n, py);
     int16_t* ly = unit_lev(r, c, bsl, 0);
-    bool nz = code_residual(&fe.src[0][(size_t)y * g.stride_y + x], g.stride_y, py, log2n, fp.qidx, true, ly,
-                            &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
+    // luma transform type: DCT_DCT or IDTX (screen content: sharp text codes as samples), by RD cost
+    int16_t lid[256];
+    const uint8_t* sy = &fe.src[0][(size_t)y * g.stride_y + x];
+    const long long jd = quant_block(sy, g.stride_y, py, log2n, fp.qidx, true, TX_DCT_DCT, ly);
+    const long long ji = quant_block(sy, g.stride_y, py, log2n, fp.qidx, true, TX_IDTX, lid);
+    b.tx_type = (int16_t)(ji < jd && any_nonzero(lid, n * n) ? TX_IDTX : TX_DCT_DCT);
+    if (b.tx_type == TX_IDTX) memcpy(ly, lid, sizeof(int16_t) * n * n);
+    bool nz = recon_block(ly, log2n, fp.qidx, true, b.tx_type, py, &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
     // chroma: UV_DC_PRED. Every other UV mode implies an ADST-family chroma transform
     // (Mode_To_Txfm, §7.13.3 compute_tx_type); this encoder's transforms are DCT_DCT.
     const int cl2 = log2n - 1, cn = n >> 1, cx = x >> 1, cy = y >> 1;
@@ -366,16 +417,34 @@ void CpuAv1Encoder::inter_block(int r, int c, int bsl, int mv_row, int mv_col) {
     const int lxc = ((geo.W + 1) >> 1) - 1, lyc = ((geo.H + 1) >> 1) - 1;
     mc_block(fe.ref[1].data(), g.stride_c, lxc, lyc, cx, cy, cn, cn, 1, mv_row, mv_col, pu, cn);
     mc_block(fe.ref[2].data(), g.stride_c, lxc, lyc, cx, cy, cn, cn, 1, mv_row, mv_col, pv, cn);
-    int16_t* ly = unit_lev(r, c, bsl, 0);
-    int16_t* lu = unit_lev(r, c, bsl, 1);
-    int16_t* lvv = unit_lev(r, c, bsl, 2);
-    bool nz = code_residual(&fe.src[0][(size_t)y * g.stride_y + x], g.stride_y, py, log2n, fp.qidx, false, ly,
-                            &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
-    nz |= code_residual(&fe.src[1][(size_t)cy * g.stride_c + cx], g.stride_c, pu, log2n - 1, fp.qidx, false, lu,
-                        &fe.rec[1][(size_t)cy * g.stride_c + cx], g.stride_c);
-    nz |= code_residual(&fe.src[2][(size_t)cy * g.stride_c + cx], g.stride_c, pv, log2n - 1, fp.qidx, false, lvv,
-                        &fe.rec[2][(size_t)cy * g.stride_c + cx], g.stride_c);
+    int16_t* lp[3] = {unit_lev(r, c, bsl, 0), unit_lev(r, c, bsl, 1), unit_lev(r, c, bsl, 2)};
+    int16_t* ly = lp[0];
+    int16_t* lu = lp[1];
+    int16_t* lvv = lp[2];
+    // transform type of the block (inter chroma follows luma): DCT_DCT or IDTX by the
+    // RD cost over the three planes
+    const uint8_t* sp[3] = {&fe.src[0][(size_t)y * g.stride_y + x], &fe.src[1][(size_t)cy * g.stride_c + cx],
+                            &fe.src[2][(size_t)cy * g.stride_c + cx]};
+    const uint8_t* pp[3] = {py, pu, pv};
+    const int ss[3] = {g.stride_y, g.stride_c, g.stride_c}, ln[3] = {log2n, log2n - 1, log2n - 1};
+    int16_t lid[3][256];
+    long long jd = 0, ji = 0;
+    for (int p = 0; p < 3; p++) {
+        jd += quant_block(sp[p], ss[p], pp[p], ln[p], fp.qidx, false, TX_DCT_DCT, lp[p]);
+        ji += quant_block(sp[p], ss[p], pp[p], ln[p], fp.qidx, false, TX_IDTX, lid[p]);
+    }
+    // IDTX only where the DCT codes something (a block the DCT quantises to nothing stays a
+    // skip) and the luma keeps levels (else chroma is DCT_DCT, see any_after_trim)
+    const bool dct_codes = any_after_trim(lp[0], log2n) || any_after_trim(lp[1], log2n - 1) ||
+                           any_after_trim(lp[2], log2n - 1);
+    int tt = dct_codes && ji < jd && any_after_trim(lid[0], log2n) ? TX_IDTX : TX_DCT_DCT;
+    if (tt == TX_IDTX)
+        for (int p = 0; p < 3; p++) memcpy(lp[p], lid[p], sizeof(int16_t) << (2 * ln[p]));
+    bool nz = recon_block(ly, log2n, fp.qidx, false, tt, py, &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
+    nz |= recon_block(lu, log2n - 1, fp.qidx, false, tt, pu, &fe.rec[1][(size_t)cy * g.stride_c + cx], g.stride_c);
+    nz |= recon_block(lvv, log2n - 1, fp.qidx, false, tt, pv, &fe.rec[2][(size_t)cy * g.stride_c + cx], g.stride_c);
     BlkInfo b{};
+    b.tx_type = (int16_t)(nz ? tt : TX_DCT_DCT);
     b.bsl = (uint8_t)bsl;
     b.flags = (uint8_t)(1 | (nz ? 0 : 2));
     b.mv_row = (int16_t)mv_row;

@@ -71,6 +71,7 @@ struct BlkLds {
     int32_t a[384];
     int32_t b[384];
     int16_t lv[384];     // quantised levels (raster per plane) before tail trimming
+    int16_t lv2[384];    // IDTX levels of the same residual (the transform-type decision)
     IntraEdge e[3];      // intra edges of Y, U, V
 };
 // Tile of a unit position (mi r, c).
@@ -79,10 +80,82 @@ __device__ __forceinline__ TileRect tile_of(const Av1Geo& g, int r, int c) {
     return tile_rect(g, tr * g.tile_cols + tc);
 }
 
+__device__ __forceinline__ long long wsum64(long long v) {
+    int lo = (int)(v & 0xffffffffll), hi = (int)(v >> 32);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned lo2 = (unsigned)__shfl_xor(lo, o), hi2 = (unsigned)__shfl_xor(hi, o);
+        const unsigned long long a = ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+        const unsigned long long b = ((unsigned long long)hi2 << 32) | lo2;
+        const unsigned long long c = a + b;
+        lo = (int)(unsigned)c;
+        hi = (int)(c >> 32);
+    }
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// Tail trimming of levels lv (raster, n = 1 << ln), lanes over scan positions
+// l + 64 k (av1_core.h trim_tail): nonzero masks by ballot, each lane's previous
+// nonzero scan position from them, the cut at the last level trim_keep keeps
+// (wave-uniform; -1: nothing kept). apply: zero the levels past the cut.
+__device__ int trim_cut_wave(int16_t* lv, int ln, bool apply) {
+    const int l = lane(), nn2 = 1 << (2 * ln), nw = (nn2 + 63) >> 6;
+    uint64_t mk[4];
+    int lvk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int sidx = l + 64 * k;
+        lvk[k] = k < nw && sidx < nn2 ? (int)lv[default_scan(ln, sidx)] : 0;
+        mk[k] = __ballot(lvk[k] != 0);
+    }
+    int cut = -1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        int prev = -1;
+        const uint64_t below = l ? (mk[k] & ((1ull << l) - 1)) : 0ull;
+        if (below) prev = 64 * k + 63 - __builtin_clzll(below);
+        else
+            for (int j = k - 1; j >= 0; j--)
+                if (mk[j]) {
+                    prev = 64 * j + 63 - __builtin_clzll(mk[j]);
+                    break;
+                }
+        const uint64_t keep = __ballot(lvk[k] != 0 && trim_keep(lvk[k], l + 64 * k, prev));
+        if (keep) cut = 64 * k + 63 - __builtin_clzll(keep);
+    }
+    if (apply)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int sidx = l + 64 * k;
+            if (k < nw && sidx < nn2 && sidx > cut && lvk[k]) lv[default_scan(ln, sidx)] = 0;
+        }
+    return cut;
+}
+
+// Rate (half bits, av1_core.h tx_bits2 / tx_eob_bits2) of levels lv (raster, n = 1 << ln).
+__device__ int rate2_wave(const int16_t* lv, int ln) {
+    const int l = lane(), nn2 = 1 << (2 * ln), nw = (nn2 + 63) >> 6;
+    int lvk[4], eob = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int sidx = l + 64 * k;
+        lvk[k] = k < nw && sidx < nn2 ? (int)lv[default_scan(ln, sidx)] : 0;
+        const uint64_t m = __ballot(lvk[k] != 0);
+        if (m) eob = 64 * k + 64 - __builtin_clzll(m);
+    }
+    int r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (l + 64 * k < eob) r += tx_bits2(lvk[k]);
+    return wsum(r) + tx_eob_bits2(eob);
+}
+
 // Transform, quantisation and reconstruction of one block held in L (src, pred):
-// luma n = 1 << log2n, chroma n / 2. Writes levels to gl (3 planes), the
-// reconstruction into L.pred, and returns the per-plane level summaries
-// (cul | dc << 6) packed as bytes 0..2, bit 24 = any nonzero.
+// luma n = 1 << log2n, chroma n / 2. The transform type is DCT_DCT or IDTX by RD cost
+// (the CPU encoder's quant_block rule: inter blocks over the three planes, intra blocks
+// luma only, chroma DCT_DCT). Writes levels to gl (3 planes), the reconstruction into
+// L.pred, and returns the per-plane level summaries (cul | dc << 6) packed as bytes
+// 0..2, bit 24 = any nonzero, bit 25 = IDTX.
 __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int qidx, bool intra, int16_t* gy,
                                     int16_t* gu, int16_t* gv) {
     const int l = lane();
@@ -107,54 +180,67 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         }
     }
     wsync();
-    // forward stage 2 (rows) + quantisation
+    // forward stage 2 (rows) + quantisation, DCT levels to L.lv and IDTX levels (8 x the
+    // residual, still in L.a) to L.lv2, with both squared coefficient errors per plane
+    long long dd[3] = {0, 0, 0}, di[3] = {0, 0, 0};
+    const int np = intra ? 1 : 3;   // planes in the decision
     for (int p = 0; p < 3; p++) {
         const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
         const int16_t* K = fdct_k(F, ln);
+        long long ed = 0, ei = 0;
         for (int i = l; i < sz * sz; i += 64) {
             const int k = i >> ln, lc = i & (sz - 1);
             int64_t s = 0;
             for (int j = 0; j < sz; j++) s += (int64_t)L.b[o + k * sz + j] * K[lc * sz + j];
             const int32_t c = (int32_t)((s + (s >= 0 ? 4096 : 4095)) >> 13);
-            L.lv[o + i] = (int16_t)quantize(c, i == 0 ? qd : qa, intra);
+            const int q = i == 0 ? qd : qa;
+            const int lv = quantize(c, q, intra);
+            L.lv[o + i] = (int16_t)lv;
+            const long long e = (long long)c - dequant(lv, q);
+            ed += e * e;
+            if (p < np) {
+                const int32_t ci = 8 * L.a[o + i];
+                const int li = quantize(ci, q, intra);
+                L.lv2[o + i] = (int16_t)li;
+                const long long e2 = (long long)ci - dequant(li, q);
+                ei += e2 * e2;
+            }
+        }
+        dd[p] = wsum64(ed);
+        if (p < np) di[p] = wsum64(ei);
+    }
+    wsync();
+    // transform type: J per plane (av1_core.h tx_rd_cost) summed over the decision planes
+    bool idtx;
+    {
+        long long jd = 0, ji = 0;
+        for (int p = 0; p < np; p++) {
+            const int ln = p ? log2n - 1 : log2n, o = base(p);
+            jd += tx_rd_cost(4 * dd[p], rate2_wave(L.lv + o, ln), qa);
+            ji += tx_rd_cost(4 * di[p], rate2_wave(L.lv2 + o, ln), qa);
+        }
+        if (intra) {
+            // luma keeps a level under IDTX
+            int anyl = 0;
+            for (int i = l; i < nn; i += 64) anyl |= L.lv2[i];
+            idtx = ji < jd && __ballot(anyl != 0) != 0;
+        } else {
+            // IDTX only where the DCT codes something and the luma keeps levels after trimming
+            bool dct_codes = false;
+            for (int p = 0; p < 3; p++) dct_codes |= trim_cut_wave(L.lv + base(p), p ? log2n - 1 : log2n, false) >= 0;
+            idtx = dct_codes && ji < jd && trim_cut_wave(L.lv2, log2n, false) >= 0;
         }
     }
     wsync();
-    // inter blocks: tail trimming (av1_core.h trim_tail), lane = scan positions l + 64 k:
-    // nonzero masks by ballot, each lane's previous nonzero from the masks, the cut at
-    // the last level that trim_keep keeps
-    if (!intra)
-        for (int p = 0; p < 3; p++) {
-            const int ln = p ? log2n - 1 : log2n, nn2 = 1 << (2 * ln), o = base(p), nw = (nn2 + 63) >> 6;
-            uint64_t mk[4];
-            int lvk[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int sidx = l + 64 * k;
-                lvk[k] = k < nw && sidx < nn2 ? (int)L.lv[o + default_scan(ln, sidx)] : 0;
-                mk[k] = __ballot(lvk[k] != 0);
-            }
-            int cut = -1;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                int prev = -1;   // highest nonzero scan position below l + 64 k
-                const uint64_t below = l ? (mk[k] & ((1ull << l) - 1)) : 0ull;
-                if (below) prev = 64 * k + 63 - __builtin_clzll(below);
-                else
-                    for (int j = k - 1; j >= 0; j--)
-                        if (mk[j]) {
-                            prev = 64 * j + 63 - __builtin_clzll(mk[j]);
-                            break;
-                        }
-                const uint64_t keep = __ballot(lvk[k] != 0 && trim_keep(lvk[k], l + 64 * k, prev));
-                if (keep) cut = 64 * k + 63 - __builtin_clzll(keep);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int sidx = l + 64 * k;
-                if (k < nw && sidx < nn2 && sidx > cut && lvk[k]) L.lv[o + default_scan(ln, sidx)] = 0;
-            }
+    if (idtx)
+        for (int p = 0; p < np; p++) {
+            const int m = p ? cnn : nn, o = base(p);
+            for (int i = l; i < m; i += 64) L.lv[o + i] = L.lv2[o + i];
         }
+    wsync();
+    // inter blocks: tail trimming of the chosen levels
+    if (!intra)
+        for (int p = 0; p < 3; p++) trim_cut_wave(L.lv + base(p), p ? log2n - 1 : log2n, true);
     wsync();
     // dequantisation, level summaries
     int nzm = 0;
@@ -192,7 +278,10 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
             int32_t t[16];
 #pragma unroll
             for (int j = 0; j < 16; j++) t[j] = j < sz ? L.a[o + i * sz + j] : 0;
-            if (ln == 2) idct4(t);
+            if (idtx && p < np)
+#pragma unroll
+                for (int j = 0; j < 16; j++) t[j] = iidentity(t[j], ln);
+            else if (ln == 2) idct4(t);
             else if (ln == 3) idct8(t);
             else idct16(t);
 #pragma unroll
@@ -212,7 +301,10 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
             int32_t t[16];
 #pragma unroll
             for (int i = 0; i < 16; i++) t[i] = i < sz ? L.b[o + i * sz + j] : 0;
-            if (ln == 2) idct4(t);
+            if (idtx && p < np)
+#pragma unroll
+                for (int i = 0; i < 16; i++) t[i] = iidentity(t[i], ln);
+            else if (ln == 2) idct4(t);
             else if (ln == 3) idct8(t);
             else idct16(t);
 #pragma unroll
@@ -224,7 +316,7 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         }
     }
     wsync();
-    return cul | (nzm ? (1u << 24) : 0u);
+    return cul | (nzm ? (1u << 24) : 0u) | (idtx ? (1u << 25) : 0u);
 }
 
 // Block loads / stores (luma n at (x, y); chroma n/2 at (x/2, y/2)).
@@ -410,7 +502,8 @@ __device__ void intra_rec_block(const Av1Args& A, BlkLds& L, const FdctLds& F, i
     const uint32_t s = code_block_wave(L, F, log2n, qidx, true, lev_ptr(A, r, c, bsl, 0), lev_ptr(A, r, c, bsl, 1),
                                        lev_ptr(A, r, c, bsl, 2));
     store_rec_blk(L, f, x, y, n);
-    b.flags = (s >> 24) ? 0 : 2;
+    b.flags = (s >> 24) & 1 ? 0 : 2;
+    b.tx_type = (int16_t)((s >> 25) & 1 ? TX_IDTX : TX_DCT_DCT);
     set_cells(A, r, c, bsl, b);
     const int n4 = 1 << bsl;
     set_lctx(A, 0, c, r, n4, (uint8_t)(s & 0xff));
@@ -489,7 +582,8 @@ __global__ __launch_bounds__(256) void k_av1_inter(Av1Args A) {
         store_rec_blk(L, f, x, y, n);
         BlkInfo b{};
         b.bsl = (uint8_t)bsl;
-        b.flags = (uint8_t)(1 | ((s >> 24) ? 0 : 2));
+        b.flags = (uint8_t)(1 | ((s >> 24) & 1 ? 0 : 2));
+        b.tx_type = (int16_t)((s >> 25) & 1 ? TX_IDTX : TX_DCT_DCT);
         b.mv_row = (int16_t)mv_row;
         b.mv_col = (int16_t)mv_col;
         b.mode = GLOBALMV;

@@ -85,15 +85,15 @@ def test_static_content_collapses_to_skip_superblocks():
     frame = SyntheticDesktop(W, H, kind="motion").frame(0)
     dec = dav1d.Decoder()
     sizes = []
-    for t in range(3):
+    for t in range(4):
         pk = enc.encode(frame, t)
         pic = dec.decode(pk[0].data[10:])
         ry, _, _, _ = planes(enc, W, H)
         assert (pic[0] == ry).all()
         sizes.append(len(pk[0].data) - 10)
     blk = enc.debug_buffer("blk").reshape(-1, 12)
-    assert set(blk[:, 0].tolist()) == {4}            # every cell in a 64x64 block
-    assert sizes[2] < 64                              # a handful of bytes per frame
+    assert set(blk[:, 0].tolist()) == {4}            # every cell in a 64x64 block (after two refining frames)
+    assert sizes[3] < 64                              # a handful of bytes per frame
 
 
 def test_1080p_frames():
