@@ -239,7 +239,7 @@ def e2e_cpu_cap(world=1) -> int:
     return int(max(0.0, cpus / max(world, 1) - E2E_CPU_PER_RANK) // E2E_CPU_PER_SESSION)
 
 
-def run_extra(args, W, H, encoder, fps, local_rank, steps, backend=None):
+def run_extra(args, W, H, encoder, fps, local_rank, steps, backend=None, cbr_kbps=0):
     """One W x H session of `encoder` through the production capture loop, timed over
     `steps` frames after a warm-up (key frame + steady state); runs after the headline
     window. Reports throughput, capture->packet latency and the frame-interval budget."""
@@ -258,6 +258,8 @@ def run_extra(args, W, H, encoder, fps, local_rank, steps, backend=None):
         cpu_fast = a.backend == "cpu" and backend is not None   # x264 "ultrafast"-like tools
         if encoder == "av1" and args.av1_kbps > 0:
             a.rc, a.kbps = "cbr", args.av1_kbps
+        if cbr_kbps > 0:
+            a.rc, a.kbps = "cbr", cbr_kbps
         caps, run_caps = run_capture_path(a, pool, local_rank, fast_cpu=cpu_fast)
         run_caps(10)
         caps[0].latencies(reset=True)
@@ -624,6 +626,8 @@ def main():
     extras = {}
     if args.extra_4k and args.backend == "hip" and not args.gather and rank == 0:
         extras["hevc_4k"] = run_extra(args, 3840, 2160, "hevc", 60, local_rank, args.extra_steps)
+        # the same under CBR (the reference's x265enc runs with a bitrate, gstwebrtc_app.py:667-683)
+        extras["hevc_4k_cbr"] = run_extra(args, 3840, 2160, "hevc", 60, local_rank, args.extra_steps, cbr_kbps=20000)
         extras["av1_4k"] = run_extra(args, 3840, 2160, "av1", 120, local_rank, 2 * args.extra_steps)
         # BASELINE config 1 (640x480@30, software H.264 plumbing): the CPU reference encoder
         # through the same capture loop, no GPU involved
