@@ -8,7 +8,7 @@
 //                      transform, quantisation, reconstruction, one wave per unit
 //   k_av1_merge        inter frames: static 32x32 / 64x64 merging, one wave per superblock
 //   k_av1_modes        inter frames: reference-MV stack -> NEAREST / NEAR / GLOBAL / NEWMV
-//   k_av1_tokens       block syntax -> token lists, one lane per 16x16 unit
+//   k_av1_tokens       block syntax -> token lists, one wave per 16x16 unit (coefficients lane-parallel)
 //   k_av1_tok_scan/copy  per-tile token streams in coding order
 //   k_av1_cdf          CDF adaptation, 16 context partitions per tile in parallel ->
 //                      per-symbol interval words
@@ -661,9 +661,243 @@ __global__ __launch_bounds__(256) void k_av1_modes(Av1Args A) {
             }
 }
 
-// Block syntax -> tokens, one lane per 16x16 unit.
-__global__ __launch_bounds__(64) void k_av1_tokens(Av1Args A) {
-    const int u = blockIdx.x * 64 + threadIdx.x;
+// Block syntax -> tokens, one wave per 16x16 unit. The syntax above the coefficients
+// (partitions, modes, vectors) is short and runs wave-uniform (lane 0 stores); the
+// coefficients of every transform block are tokenised lane-parallel by the
+// WaveTokenSink overload of code_coeffs below.
+struct WaveTokenSink {
+    uint32_t* p;
+    int n, cap;
+    uint32_t pend;
+    int pend_n;
+    uint32_t* bits;   // this wave's LDS bit buffer (256 words) for the sign / Golomb run
+    __device__ void push(uint32_t t) {
+        if (n < cap && lane() == 0) p[n] = t;
+        n++;
+    }
+    __device__ void flush() {
+        if (pend_n) push(tok_lit(pend, pend_n));
+        pend = 0;
+        pend_n = 0;
+    }
+    __device__ void sym(int off, int n2, int v) {
+        flush();
+        push(tok_sym(off, n2, v));
+    }
+    __device__ void bit(int b) {
+        pend = (pend << 1) | (uint32_t)(b & 1);
+        if (++pend_n == 24) flush();
+    }
+    __device__ void lits(uint32_t v, int nbits) {
+        for (int i = nbits - 1; i >= 0; i--) bit((v >> i) & 1);
+    }
+    __device__ void gather(int off, bool bottom_out, int v) {
+        flush();
+        push(tok_gather(off, bottom_out, v));
+    }
+};
+
+// Number of coeff_br tokens of a level magnitude a (code_coeffs: up to 4 groups of 3).
+__device__ __forceinline__ int br_count(int a) {
+    if (a <= 2) return 0;
+    int level = 3, k = 0;
+    for (int idx = 0; idx < 4; idx++) {
+        const int br = sk_min(a - level, 3);
+        k++;
+        level += br;
+        if (br < 3) break;
+    }
+    return k;
+}
+
+// Lane-parallel code_coeffs (codec/av1_core.h): the same tokens in the same order.
+// Every coefficient's base / range contexts depend only on the level array (its
+// neighbours lie on later anti-diagonals, already coded in the reverse scan), so lanes
+// take scan positions s = l + 64 k, place their tokens by a suffix sum over the reverse
+// scan, and pack the forward-scan sign / Golomb bits through LDS into 24-bit literals.
+__device__ int code_coeffs(WaveTokenSink& w, const CdfContext& cx, const int16_t* lev, int txs, int plane, CoefCtx cc,
+                           bool is_inter, int intra_dir, int qidx, int tx_type = TX_DCT_DCT) {
+    const int l = lane();
+    const int log2n = txs + 2, n = 1 << log2n, nn = n * n, nw = (nn + 63) >> 6;
+    const int ptype = plane > 0;
+    int lv[4], pos[4];
+    int eob = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int sidx = l + 64 * k;
+        pos[k] = k < nw && sidx < nn ? default_scan(log2n, sidx) : 0;
+        lv[k] = k < nw && sidx < nn ? (int)lev[pos[k]] : 0;
+        const uint64_t m = __ballot(lv[k] != 0);
+        if (m) eob = 64 * k + 64 - __builtin_clzll(m);
+    }
+    w.sym(cdf_off(cx, cx.txb_skip[txs][cc.txb_skip]), 2, eob == 0);
+    if (eob == 0) return 0;
+    if (plane == 0 && qidx > 0) {
+        const int sym = tx_type == TX_IDTX ? 0 : 1;
+        if (is_inter) w.sym(cdf_off(cx, cx.inter_tx_set3[txs]), 2, sym);
+        else w.sym(cdf_off(cx, cx.intra_tx_set2[txs][intra_dir]), 5, sym);
+    }
+    const int eob_multi = 2 * log2n - 4;
+    const int eob_pt = eob_pt_of(eob);
+    switch (eob_multi) {
+        case 0: w.sym(cdf_off(cx, cx.eob_pt_16[ptype][0]), 5, eob_pt - 1); break;
+        case 2: w.sym(cdf_off(cx, cx.eob_pt_64[ptype][0]), 7, eob_pt - 1); break;
+        default: w.sym(cdf_off(cx, cx.eob_pt_256[ptype][0]), 9, eob_pt - 1); break;
+    }
+    if (eob_pt >= 3) {
+        const int off = eob - ((1 << (eob_pt - 2)) + 1);
+        const int sh = eob_pt - 3;
+        w.sym(cdf_off(cx, cx.eob_extra[txs][ptype][eob_pt - 3]), 2, (off >> sh) & 1);
+        for (int i = 1; i < eob_pt - 2; i++) w.bit((off >> (sh - i)) & 1);
+    }
+    w.flush();   // the coefficient symbols follow (each sym flushes; keep n exact for the offsets)
+    // ---- base levels + ranges, reverse scan: tokens of position s at n + (tokens of s' > s)
+    int cnt[4], tot = 0, hi[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int sidx = l + 64 * k;
+        cnt[k] = sidx < eob ? 1 + br_count(lv[k] < 0 ? -lv[k] : lv[k]) : 0;
+    }
+    // suffix sums: chunk totals (uniform), then within a chunk the lanes above
+#pragma unroll
+    for (int k = 3; k >= 0; k--) {
+        int x = cnt[k];   // inclusive suffix scan over lanes (lane 63 first)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_down(x, o);
+            if (l + o < 64) x += y;
+        }
+        hi[k] = tot + x - cnt[k];   // tokens of chunks above + lanes above in this chunk
+        tot += __shfl(x, 0);
+    }
+    auto qv = [&](int rr, int c2) -> int {   // min(level, 15) of a later-coded neighbour (0 outside)
+        if (rr >= n || c2 >= n) return 0;
+        const int a = sk_abs((int)lev[(rr << log2n) + c2]);
+        return a < 15 ? a : 15;
+    };
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int c = l + 64 * k;
+        if (c >= eob) continue;
+        const int a = sk_abs(lv[k]), pz = pos[k];
+        const int row = pz >> log2n, col = pz & (n - 1);
+        int o = w.n + hi[k];
+        uint32_t t;
+        if (c == eob - 1) {
+            const int ctx = c == 0 ? 0 : (c <= nn / 8 ? 1 : (c <= nn / 4 ? 2 : 3));
+            t = tok_sym(cdf_off(cx, cx.coeff_base_eob[txs][ptype][ctx]), 3, sk_min(a, 3) - 1);
+        } else {
+            int mag = sk_min(qv(row, col + 1), 3) + sk_min(qv(row + 1, col), 3) + sk_min(qv(row + 1, col + 1), 3) +
+                      sk_min(qv(row, col + 2), 3) + sk_min(qv(row + 2, col), 3);
+            int ctx = sk_min((mag + 1) >> 1, 4);
+            if (row == 0 && col == 0) ctx = 0;
+            else {
+                const int rm = sk_min(row, 4), cm = sk_min(col, 4);
+                int ofs;
+                if (txs == TX_4X4) {
+                    constexpr uint8_t t4[5][5] = {{0, 1, 6, 6, 0}, {1, 6, 6, 21, 0}, {6, 6, 21, 21, 0},
+                                                  {6, 21, 21, 21, 0}, {0, 0, 0, 0, 0}};
+                    ofs = t4[rm][cm];
+                } else {
+                    constexpr uint8_t t8[5][5] = {{0, 1, 6, 6, 21}, {1, 6, 6, 21, 21}, {6, 6, 21, 21, 21},
+                                                  {6, 21, 21, 21, 21}, {21, 21, 21, 21, 21}};
+                    ofs = t8[rm][cm];
+                }
+                ctx += ofs;
+            }
+            t = tok_sym(cdf_off(cx, cx.coeff_base[txs][ptype][ctx]), 4, sk_min(a, 3));
+        }
+        if (o < w.cap) w.p[o] = t;
+        o++;
+        if (a > 2) {
+            int mag = qv(row, col + 1) + qv(row + 1, col) + qv(row + 1, col + 1);
+            mag = sk_min((mag + 1) >> 1, 6);
+            const int ctx = pz == 0 ? mag : ((row < 2 && col < 2) ? mag + 7 : mag + 14);
+            const int cdf = cdf_off(cx, cx.coeff_br[sk_min(txs, TX_32X32)][ptype][ctx]);
+            int level = 3;
+            for (int idx = 0; idx < 4; idx++) {
+                const int br = sk_min(a - level, 3);
+                if (o < w.cap) w.p[o] = tok_sym(cdf, 4, br);
+                o++;
+                level += br;
+                if (br < 3) break;
+            }
+        }
+    }
+    w.n += tot;
+    // ---- signs and Golomb remainders, forward scan: dc_sign symbol, then one bit run
+    const int l0 = (int)lev[0];
+    if (l0 != 0) w.sym(cdf_off(cx, cx.dc_sign[ptype][cc.dc_sign]), 2, l0 < 0);
+    int nb[4], bsum = 0, cul = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int c = l + 64 * k, a = sk_abs(lv[k]);
+        nb[k] = 0;
+        if (c < eob && a) {
+            nb[k] = c > 0 ? 1 : 0;
+            if (a > 14) nb[k] += 2 * (31 - __builtin_clz((uint32_t)(a - 14))) + 1;
+            cul += a;
+        }
+    }
+    for (int i = l; i < 256; i += 64) w.bits[i] = 0u;
+    wsync();
+    int base = 0, boff[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {   // exclusive prefix over the forward scan
+        int x = nb[k];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (l >= o) x += y;
+        }
+        boff[k] = base + x - nb[k];
+        base += __shfl(x, 63);
+    }
+    bsum = base;
+    auto put_bits = [&](int off, uint32_t v, int cntb) {   // cntb <= 32 bits, MSB first, at bit offset off
+        for (int i = 0; i < cntb; i++)
+            if ((v >> (cntb - 1 - i)) & 1) atomicOr(&w.bits[(off + i) >> 5], 0x80000000u >> ((off + i) & 31));
+    };
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (!nb[k]) continue;
+        const int a = sk_abs(lv[k]), c = l + 64 * k;
+        int off = boff[k];
+        if (c > 0) {
+            put_bits(off, lv[k] < 0 ? 1u : 0u, 1);
+            off++;
+        }
+        if (a > 14) {
+            const uint32_t x = (uint32_t)(a - 14);
+            const int len = 31 - __builtin_clz(x);
+            off += len;                          // len zero bits
+            put_bits(off, x, len + 1);           // the leading one and the len low bits
+        }
+    }
+    wsync();
+    // 24-bit literal tokens, the remainder stays pending (flushed by the next symbol)
+    const int full = bsum / 24, rem = bsum - 24 * full;
+    auto chunk = [&](int start, int cntb) -> uint32_t {
+        uint32_t v = 0;
+        for (int i = 0; i < cntb; i++) v = (v << 1) | ((w.bits[(start + i) >> 5] >> (31 - ((start + i) & 31))) & 1u);
+        return v;
+    };
+    for (int j = l; j < full; j += 64) {
+        const int o = w.n + j;
+        if (o < w.cap) w.p[o] = tok_lit(chunk(24 * j, 24), 24);
+    }
+    w.n += full;
+    w.pend = rem ? chunk(24 * full, rem) : 0u;
+    w.pend_n = rem;
+    wsync();
+    const int dcc = l0 == 0 ? 0 : (l0 < 0 ? 1 : 2);
+    return sk_min(wsum(cul), 63) | (dcc << 6);
+}
+
+__global__ __launch_bounds__(256) void k_av1_tokens(Av1Args A) {
+    __shared__ uint32_t bits_w[4][256];
+    const int w = threadIdx.x >> 6;
+    const int u = blockIdx.x * 4 + w;
     const FrameArgs& f = A.f;
     if (u >= f.mb_w * f.mb_h) return;
     const Av1Geo& g = A.geo;
@@ -679,11 +913,11 @@ __global__ __launch_bounds__(64) void k_av1_tokens(Av1Args A) {
     v.qidx = A.frame[1];
     v.key = A.frame[0];
     const int ux = u % f.mb_w, uy = u / f.mb_w;
-    TokenSink sink{A.tok + (size_t)u * kTokCap, 0, kTokCap, 0u, 0};
+    WaveTokenSink sink{A.tok + (size_t)u * kTokCap, 0, kTokCap, 0u, 0, bits_w[w]};
     const TileRect t = tile_of(g, uy * 4, ux * 4);
     code_unit(sink, AV1_DEFAULT_CDF[0], v, t, ux, uy);
     sink.flush();
-    A.tok_n[u] = sink.n;
+    if (lane() == 0) A.tok_n[u] = sink.n;
 }
 
 // Tile token streams: the unit slots of each tile concatenated in coding order, so
@@ -1327,7 +1561,7 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_av1_inter, dim3((n + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_merge, dim3(a.geo.sb_cols * a.geo.sb_rows), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_av1_modes, dim3((a.geo.c8 * a.geo.r8 + 255) / 256), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_av1_tokens, dim3((n + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_av1_tokens, dim3((n + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_tok_scan, dim3(tiles), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_tok_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_cdf, dim3(tiles * kEcParts), dim3(64), 0, s, a);
