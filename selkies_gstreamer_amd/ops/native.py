@@ -442,8 +442,8 @@ class H264Encoder:
         lib().sk_h264_set_rate(self._h, RC_MODES[mode], int(kbps))
 
     def rc_stats(self) -> dict:
-        arr = (ctypes.c_int32 * 32)()
-        n = lib().sk_h264_rc_stats(self._h, arr, 32)
+        arr = (ctypes.c_int32 * 64)()
+        n = lib().sk_h264_rc_stats(self._h, arr, 64)
         return {k: int(arr[i]) for i, k in enumerate(RC_FIELDS) if i < n}
 
     def stage_times(self, n: int = 16) -> list[float]:

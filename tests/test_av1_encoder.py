@@ -140,3 +140,22 @@ def test_av1_depacketizer_malformed_and_sized_obus():
     assert out == b"\x12\x00" + sized
     bare = bytes([0x30, 0xAA, 0xBB])                               # no size field: one is added
     assert dep.push(bytes([0x10]) + bare, 4, True) == b"\x12\x00" + bytes([0x32, 0x02, 0xAA, 0xBB])
+
+
+def test_idtx_blocks_on_text_decode_exactly():
+    """IDTX (identity transform) is chosen by RD cost where it pays - dense synthetic
+    text - in key and inter frames, and dav1d reconstructs every such block exactly."""
+    W, H = 320, 192
+    enc = Av1Encoder(W, H, backend="cpu", qp=30)
+    src = SyntheticDesktop(W, H, kind="desktop")
+    dec = dav1d.Decoder()
+    idtx = []
+    for t in range(3):
+        pk = enc.encode(src.frame(t), t)
+        pic = dec.decode(pk[0].data[10:])
+        ry, ru, rv, _ = planes(enc, W, H)
+        assert all(np.array_equal(a, b) for a, b in zip(pic, (ry, ru, rv)))
+        blk = enc.debug_buffer("blk").view(np.int16).reshape(-1, 6)
+        idtx.append(int((blk[:, 4] == 1).sum()))
+    dec.close()
+    assert idtx[0] > 0, idtx   # key frame

@@ -10,6 +10,7 @@ no frame other than a key frame above 1.5 budgets."""
 import os
 import sys
 
+import numpy as np
 import pytest
 
 from selkies_gstreamer_amd.ops.native import H264Encoder
@@ -134,3 +135,41 @@ def test_gpu_cbr_guard_matches_cpu():
 def test_gpu_rate_control_matches_cpu_fullframe(codec):
     _parity(codec, "cbr", 600, 30)
     _parity(codec, "crf", 0, 20)
+
+
+def test_av1_cbr_holds_its_budget_cpu():
+    """AV1 CBR as svtav1enc runs it (120 ms buffer, no scene-cut key frames, qindex from
+    the fractional QP): 960x544 at 120 fps, 2.5 Mbit/s -> the mean within 10 % of the
+    target after the key frame, one key frame, no inter frame above 2 budgets."""
+    r = _trace(backend="cpu", codec="av1", width=960, height=544, frames=60, content="motion", mode="cbr",
+               kbps=2500, fps=120.0)
+    t = r["trace"]
+    budget = 2500 * 1000 / 120 / 8
+    inter = t["bytes"][1:]
+    assert r["keyframes"] == 1
+    assert 0.85 <= sum(inter) / len(inter) / budget <= 1.10, r
+    assert max(inter) <= 2.0 * budget, r
+
+
+def test_fractional_qp_dither():
+    """rc_dither_qp (ratecontrol.h) through the CPU controller: a frame at fractional QP
+    lo + f/256 codes round(N f / 256) of its N rate-controlled stripes at lo + 1 and the
+    rest at lo."""
+    from selkies_gstreamer_amd.ops.native import H264Encoder
+    W, H = 320, 512   # 8 stripes of 64 px
+    enc = H264Encoder(W, H, backend="cpu", rate_control="cbr", bitrate_kbps=600, fps=60.0)
+    src = SyntheticDesktop(W, H, kind="motion")
+    seen_frac = 0
+    for t in range(60):
+        enc.encode(src.frame(t), t)
+        st = enc.rc_stats()
+        lo, f = st["cur_qpf"] >> 8, st["cur_qpf"] & 255
+        tasks = enc.debug_buffer("tasks").view(np.int32).reshape(-1, 12)
+        coded = [int(q) for a, q in zip(tasks[:, 10], tasks[:, 1]) if a in (1, 2)]   # final_action P / I
+        if len(coded) != 8:
+            continue
+        assert set(coded) <= {lo, lo + 1}, (t, coded, lo)
+        assert coded.count(lo + 1) == (8 * f + 128) >> 8, (t, coded, f)
+        seen_frac += f > 0
+    enc.close()
+    assert seen_frac > 0   # the controller used fractional QPs
