@@ -5,8 +5,11 @@
 // arithmetic coder itself.
 //
 // Coding structure (fixed by the parameter sets in hevc_syntax.cpp):
-//   CTB = CU = 16x16 (log2 min CB 4, no split flags), PU 2Nx2N, TU = CU (16x16 luma,
-//   8x8 chroma, no transform split), one reference picture (previous picture),
+//   CTB = CU = 16x16 (log2 min CB 4, no split flags), PU 2Nx2N, a residual quadtree of
+//   two levels: TU = CU (16x16 luma, 8x8 chroma), or four 8x8 nodes with 4x4 chroma each,
+//   every node one 8x8 luma TU or four 4x4 ones (DST for intra)
+//   (max_transform_hierarchy_depth 2, the encoder's RD choice), intra prediction per TU,
+//   mode-dependent scans, one reference picture (previous picture),
 //   quarter-pel motion (8-tap luma / 4-tap chroma MC), deblocking on (CU edges, deblock_picture), SAO
 //   (hevc_sao.h), no sign hiding /
 //   transform skip,
@@ -24,26 +27,33 @@ namespace sk {
 namespace hevc {
 
 constexpr int kCtb = 16;
-constexpr int kCoefPerCu = 384;     // 16x16 luma | 8x8 Cb | 8x8 Cr, raster [y][x] per TU
+constexpr int kCoefPerCu = 384;     // 16x16 luma | 8x8 Cb | 8x8 Cr, raster [y][x] per TU; split CUs:
+                                    // luma node q (z order) at 64q (one 8x8 TU, or 4x4 TU j at 64q + 16j),
+                                    // Cb at 256 + 16q, Cr at 320 + 16q
 constexpr int kCoefCb = 256, kCoefCr = 320;
 constexpr int kCuBinCap = 4096;     // bin entries per CU slot (worst case ~3950, see bin_bound)
 constexpr int kSubstreamCtbBytes = 4608;   // worst-case CABAC bytes per CTB (>= 6 bits x ctx bins)
 
 // ---------------------------------------------------------------------------
-// Per-CU decisions (16 bytes, shared by CPU and GPU buffers; tests diff them).
+// Per-CU decisions (24 bytes, shared by CPU and GPU buffers; tests diff them).
 enum CuMode : uint8_t { CU_SKIP = 0, CU_MERGE = 1, CU_AMVP = 2, CU_INTRA = 3 };
 struct CuInfo {
     uint8_t mode;         // CuMode
     uint8_t merge_idx;    // SKIP / MERGE
     uint8_t mvp_idx;      // AMVP
     uint8_t intra_mode;   // IntraPredModeY (chroma: DM, intra_chroma_pred_mode = 4)
-    uint8_t cbf;          // bit0 Y, bit1 Cb, bit2 Cr
+    uint8_t cbf;          // bit0 Y, bit1 Cb, bit2 Cr (split CUs: any TU of the component)
     uint8_t qp;
-    uint8_t pad[2];
+    uint8_t tu;           // bit 4: four 8x8 nodes (split_transform_flag); bits 0..3: node q in four 4x4 TUs
+    uint8_t tuc;          // split CUs: bits 0..3 cbf_cb, bits 4..7 cbf_cr of the four nodes
     int16_t mvx, mvy;     // quarter-pel
     int16_t mvdx, mvdy;   // AMVP: mv - predictor
+    uint16_t ycbf;        // cbf_luma of the TU covering each 4x4 unit (bit = z-order index)
+    uint16_t tsy;         // transform_skip_flag of the 4x4 luma TUs (bit = z-order index)
+    uint8_t tsc;          // transform_skip_flag of the nodes' 4x4 chroma TUs: bits 0..3 Cb, 4..7 Cr
+    uint8_t pad2[3];
 };
-static_assert(sizeof(CuInfo) == 16, "CuInfo layout");
+static_assert(sizeof(CuInfo) == 24, "CuInfo layout");
 
 // ---------------------------------------------------------------------------
 // Tables.
@@ -66,6 +76,11 @@ SK_TABLE int8_t HEVC_T16[16][16] = {
     {9, -25, 43, -57, 70, -80, 87, -90, 90, -87, 80, -70, 57, -43, 25, -9}};
 // The 8-point matrix is rows 0, 2, 4, ... of the 16-point one restricted to 8 columns.
 SK_HD int dct_coef(int log2n, int k, int n) { return HEVC_T16[k << (4 - log2n)][n]; }
+// 4x4 DST-VII (8.6.4.2, intra luma 4x4 TUs).
+SK_TABLE int8_t HEVC_DST4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+SK_HD int tx_coef(int log2n, bool dst, int k, int n) { return dst ? HEVC_DST4[k][n] : dct_coef(log2n, k, n); }
+// z-order index of 4x4 unit (x, y) of a 16x16 CU (x, y = 0..3).
+SK_HD int zorder4(int x, int y) { return (x & 1) | ((y & 1) << 1) | ((x & 2) << 1) | ((y & 2) << 2); }
 
 // Up-right diagonal scan of a 4x4 (sub-)block: scan position -> raster (y*4+x), and back.
 SK_HD int diag4_raster(int n) { return (int)((0xfbe7ad369c258140ULL >> (4 * n)) & 15); }
@@ -74,6 +89,23 @@ SK_HD int diag4_scanpos(int r) { return (int)((0xfda6eb73c8419520ULL >> (4 * r))
 SK_HD int diag2_raster(int n) { return (int)((0x3120u >> (4 * n)) & 15); }   // (0,0),(0,1),(1,0),(1,1) as y*2+x
 SK_HD int sb_raster(int log2n, int i) {   // sub-block scan index -> raster index in the sub-block grid
     return log2n == 4 ? diag4_raster(i) : (log2n == 3 ? diag2_raster(i) : 0);
+}
+// scanIdx (7.4.9.11): 0 up-right diagonal, 1 horizontal, 2 vertical. The horizontal and
+// vertical scans occur for 4x4 / 8x8 TUs only (mode-dependent intra scans).
+enum Scan { SCAN_DIAG = 0, SCAN_HOR = 1, SCAN_VER = 2 };
+SK_HD int scan4_raster(int scan, int k) {   // position k of a 4x4 sub-block -> raster (y*4 + x)
+    return scan == SCAN_DIAG ? diag4_raster(k) : (scan == SCAN_HOR ? k : ((k & 3) << 2) | (k >> 2));
+}
+SK_HD int sb_scan_raster(int log2n, int scan, int i) {   // sub-block i -> raster in the sub-block grid
+    if (scan == SCAN_DIAG || log2n != 3) return sb_raster(log2n, i);
+    return scan == SCAN_HOR ? i : ((i & 1) << 1) | (i >> 1);
+}
+// Intra scans (8.4.4? / 7.4.9.11): luma 4x4 / 8x8 and chroma 4x4 TUs of intra CUs.
+SK_HD int intra_scan(int mode, int log2n, int cidx) {
+    if (!(log2n == 2 || (log2n == 3 && cidx == 0))) return SCAN_DIAG;
+    if (mode >= 6 && mode <= 14) return SCAN_VER;
+    if (mode >= 22 && mode <= 30) return SCAN_HOR;
+    return SCAN_DIAG;
 }
 
 // CABAC (shared with H.264): LPS ranges and LPS state transitions.
@@ -121,7 +153,9 @@ enum Ctx : int {
     CTX_GT2 = 125,           // 6
     CTX_SAO_MERGE = 131,     // sao_merge_left_flag / sao_merge_up_flag
     CTX_SAO_TYPE = 132,      // first bin of sao_type_idx_luma / _chroma
-    CTX_COUNT = 133,
+    CTX_SPLIT_TF = 133,      // 3 split_transform_flag (ctxInc 5 - log2TrafoSize)
+    CTX_TS = 136,            // 2 transform_skip_flag (luma, chroma)
+    CTX_COUNT = 138,
     CTX_TERM = 255           // terminating bin (end_of_slice_segment_flag / end_of_subset_one_bit)
 };
 SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
@@ -143,7 +177,9 @@ SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
      140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166, 182, 140, 227,
      122, 197,                      // greater1
      138, 153, 136, 167, 152, 152,  // greater2
-     153, 200},                     // sao merge, sao type
+     153, 200,                      // sao merge, sao type
+     153, 138, 138,                 // split_transform_flag
+     139, 139},                     // transform_skip_flag
     {// P slices (cabac_init_flag = 0)
      197, 185, 201,                 // cu_skip_flag
      149,                           // pred_mode_flag
@@ -162,7 +198,9 @@ SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
      154, 196, 196, 167, 154, 152, 167, 182, 182, 134, 149, 136, 153, 121, 136, 137, 169, 194, 166, 167, 154, 167,
      137, 182,                      // greater1
      107, 167, 91, 122, 107, 167,   // greater2
-     153, 185}};                    // sao merge, sao type
+     153, 185,                      // sao merge, sao type
+     124, 138, 94,                  // split_transform_flag
+     139, 139}};                    // transform_skip_flag
 
 // Context state byte: (pStateIdx << 1) | valMps (9.3.2.2).
 SK_HD uint8_t ctx_init_state(int init_value, int slice_qp) {
@@ -335,40 +373,49 @@ struct CabacEncoder {
 // Transforms. Residual / coefficient blocks are raster [y][x] int arrays.
 // Forward (encoder choice, HM partial butterflies as matrix products):
 // shift1 = log2n + bitDepth - 9, shift2 = log2n + 6.
-SK_HD void fwd_transform(const int* res, int log2n, int* coef) {
+SK_HD void fwd_transform(const int* res, int log2n, int* coef, bool dst = false) {
     const int n = 1 << log2n;
     const int sh1 = log2n - 1, sh2 = log2n + 6;
     int tmp[256];
     for (int y = 0; y < n; y++)          // horizontal: tmp[y][u]
         for (int u = 0; u < n; u++) {
             int s = 0;
-            for (int x = 0; x < n; x++) s += dct_coef(log2n, u, x) * res[y * n + x];
+            for (int x = 0; x < n; x++) s += tx_coef(log2n, dst, u, x) * res[y * n + x];
             tmp[y * n + u] = (s + (1 << (sh1 - 1))) >> sh1;
         }
     for (int v = 0; v < n; v++)          // vertical: coef[v][u]
         for (int u = 0; u < n; u++) {
             int s = 0;
-            for (int y = 0; y < n; y++) s += dct_coef(log2n, v, y) * tmp[y * n + u];
+            for (int y = 0; y < n; y++) s += tx_coef(log2n, dst, v, y) * tmp[y * n + u];
             coef[v * n + u] = (s + (1 << (sh2 - 1))) >> sh2;
         }
 }
 // Inverse (8.6.4.2): columns first, clip to 16 bits after (e + 64) >> 7, then rows,
 // residual = (r + 2048) >> 12 for 8-bit video.
-SK_HD void inv_transform(const int* d, int log2n, int* res) {
+SK_HD void inv_transform(const int* d, int log2n, int* res, bool dst = false) {
     const int n = 1 << log2n;
     int g[256];
     for (int x = 0; x < n; x++)
         for (int y = 0; y < n; y++) {
             int s = 0;
-            for (int j = 0; j < n; j++) s += dct_coef(log2n, j, y) * d[j * n + x];
+            for (int j = 0; j < n; j++) s += tx_coef(log2n, dst, j, y) * d[j * n + x];
             g[y * n + x] = sk_clip((s + 64) >> 7, -32768, 32767);
         }
     for (int y = 0; y < n; y++)
         for (int x = 0; x < n; x++) {
             int s = 0;
-            for (int j = 0; j < n; j++) s += dct_coef(log2n, j, x) * g[y * n + j];
+            for (int j = 0; j < n; j++) s += tx_coef(log2n, dst, j, x) * g[y * n + j];
             res[y * n + x] = (s + 2048) >> 12;
         }
+}
+
+// Transform skip (4x4, 8.6.4.2): the decoder's residual is (d << 7 + 2^11) >> 12; the
+// encoder's "coefficients" are the residual << 5 (the 4x4 transform's scale).
+SK_HD void ts_forward(const int* res, int* coef) {
+    for (int i = 0; i < 16; i++) coef[i] = res[i] * 32;
+}
+SK_HD void ts_inverse(const int* d, int* res) {
+    for (int i = 0; i < 16; i++) res[i] = (d[i] * 128 + 2048) >> 12;
 }
 
 // Quantisation (HM: quantScale, QUANT_SHIFT 14, transform shift 15 - 8 - log2n,
@@ -482,7 +529,8 @@ SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int 
 }
 
 // Encoder mode decision (open loop, every CU in parallel, so no MPM-dependent cost):
-// all 35 luma modes in this order, first minimum of SAD + bias wins. The four
+// all 35 luma modes in this order, first minimum of SAD + bias wins (SAD of the sixteen
+// 4x4 blocks, each predicted from its source neighbours). The four
 // non-directional / axis modes carry no bias; the 31 other directions pay about six
 // bits at the SAD lambda of the QP.
 SK_TABLE int8_t HEVC_INTRA_ORDER[35] = {1,  0,  26, 10, 2,  3,  4,  5,  6,  7,  8,  9,  11, 12, 13, 14, 15, 16,
@@ -491,6 +539,49 @@ SK_HD bool intra_mode_basic(int mode) { return mode <= 1 || mode == 10 || mode =
 SK_HD int intra_mode_bias(int mode, int qp) {
     return intra_mode_basic(mode) ? 0 : 6 * (qp < 12 ? 1 : 1 << ((qp - 12) / 6));
 }
+
+// Neighbour availability of transform blocks (z order inside the CU) for the intra
+// reference samples: bit 0 below-left, 1 left, 2 above-left, 3 above, 4 above-right.
+enum { AV_BL = 1, AV_L = 2, AV_TL = 4, AV_T = 8, AV_TR = 16 };
+// 16x16 TU (the whole CU): the CU below-left is never decoded yet.
+SK_HD int cu_avail(bool left, bool top, bool tr) {
+    return (left ? AV_L : 0) | (left && top ? AV_TL : 0) | (top ? AV_T : 0) | (tr ? AV_TR : 0);
+}
+// Whether 4x4 unit (ux, uy) of the CU's neighbourhood (-1 .. 7) is decoded before the
+// unit with z-order index z of the CU (left / top / tr: the CU's neighbours).
+SK_HD bool unit_avail(int ux, int uy, int z, bool left, bool top, bool tr) {
+    if (uy < 0) return ux < 0 ? (left && top) : (ux < 4 ? top : (ux < 8 && tr));
+    if (uy >= 4 || ux >= 4) return false;
+    if (ux < 0) return left;
+    return zorder4(ux, uy) < z;
+}
+// The TU of s x s units (s = 1, 2) at unit (bx, by) of the CU: its neighbour segments
+// are whole units of earlier TUs or outside blocks, so their first unit decides.
+SK_HD int tu_avail_at(int bx, int by, int s, bool left, bool top, bool tr) {
+    const int z = zorder4(bx, by);
+    return (unit_avail(bx - 1, by + s, z, left, top, tr) ? AV_BL : 0) | (unit_avail(bx - 1, by, z, left, top, tr) ? AV_L : 0) |
+           (unit_avail(bx - 1, by - 1, z, left, top, tr) ? AV_TL : 0) | (unit_avail(bx, by - 1, z, left, top, tr) ? AV_T : 0) |
+           (unit_avail(bx + s, by - 1, z, left, top, tr) ? AV_TR : 0);
+}
+// 8x8 luma / 4x4 chroma node q of a split CU.
+SK_HD int tu_avail(int q, bool left, bool top, bool tr) { return tu_avail_at(2 * (q & 1), 2 * (q >> 1), 2, left, top, tr); }
+
+// Encoder RD model shared by the CPU reference and the kernels (TU split and TU zeroing
+// decisions): J = 512 * SSE + lambda_q8 * R, R in half bits, lambda = 0.57 * 2^((QP - 12) / 3)
+// (HM's), a coded TU ~4 bits plus, per non-zero level, 2.5 bits + 2 bits per doubling.
+SK_HD int rd_lambda_q8(int qp) {
+    const int e = qp > 12 ? qp - 12 : 0;
+    const int b = e % 3 == 0 ? 146 : (e % 3 == 1 ? 184 : 232);
+    return b << (e / 3);
+}
+SK_HD int level_rate_half(int l) {
+    if (!l) return 0;
+    const uint32_t a = (uint32_t)sk_abs(l);
+    return 5 + 4 * (31 - __builtin_clz(a));
+}
+constexpr int kTuRateHalf = 8;      // cbf / last position of a coded TU
+constexpr int kSplitRateHalf = 12;  // the split CU's extra cbf flags
+constexpr int kSplit8RateHalf = 8;  // an 8x8 node's split flag and extra cbf_luma flags
 
 // Most probable modes (8.4.2) for CTB = CU: candB is always DC (above CTB row).
 SK_HD void intra_mpm(int cand_a, int* list) {
@@ -652,23 +743,25 @@ SK_HD int last_prefix(int p) {
 }
 
 template <class W>
-SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx) {
+SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx, int scan = SCAN_DIAG, int ts = 0) {
     const int n = 1 << log2n;
+    if (log2n == 2) w.ctx(CTX_TS + (cidx ? 1 : 0), ts);   // transform_skip_flag (PPS enables it)
     const int sbw = n >> 2;                     // sub-blocks per row
     const int nsb = sbw * sbw;
     // last significant coefficient in (sub-block, position) scan order
     int last_i = -1, last_n = -1;
     for (int i = nsb - 1; i >= 0 && last_i < 0; i--) {
-        const int sr = sb_raster(log2n, i), xs = log2n == 2 ? 0 : sr % sbw, ys = log2n == 2 ? 0 : sr / sbw;
+        const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
         for (int k = 15; k >= 0; k--) {
-            const int r = diag4_raster(k);
+            const int r = scan4_raster(scan, k);
             if (c[(ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3)]) { last_i = i; last_n = k; break; }
         }
     }
     if (last_i < 0) return;   // callers only code TUs with cbf = 1
-    const int lsr = sb_raster(log2n, last_i);
-    const int lx = (log2n == 2 ? 0 : lsr % sbw) * 4 + (diag4_raster(last_n) & 3);
-    const int ly = (log2n == 2 ? 0 : lsr / sbw) * 4 + (diag4_raster(last_n) >> 2);
+    const int lsr = sb_scan_raster(log2n, scan, last_i);
+    int lx = (lsr % sbw) * 4 + (scan4_raster(scan, last_n) & 3);
+    int ly = (lsr / sbw) * 4 + (scan4_raster(scan, last_n) >> 2);
+    if (scan == SCAN_VER) { const int t = lx; lx = ly; ly = t; }   // coded swapped (7.4.9.11)
     // last_sig_coeff_x/y_prefix (TR, cMax 2*log2n - 1), then suffixes (FL, bypass)
     const int off = cidx == 0 ? 3 * (log2n - 2) + ((log2n - 1) >> 2) : 15;
     const int shift = cidx == 0 ? (log2n + 1) >> 2 : log2n - 2;
@@ -683,7 +776,7 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx) {
     // coded_sub_block_flag per sub-block (raster in the sub-block grid)
     uint32_t csbf = 0;
     for (int i = 0; i < nsb; i++) {
-        const int sr = sb_raster(log2n, i), xs = sr % sbw, ys = sr / sbw;
+        const int sr = sb_raster(log2n, i), xs = sr % sbw, ys = sr / sbw;   // every sub-block once
         bool nz = false;
         for (int k = 0; k < 16 && !nz; k++) nz = c[(ys * 4 + (k >> 2)) * n + xs * 4 + (k & 3)] != 0;
         if (nz) csbf |= 1u << sr;
@@ -691,7 +784,7 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx) {
     int c1_carry = 1;   // greater1 context state carried between sub-blocks (HM c1)
     bool first_g1_sb = true;
     for (int i = last_i; i >= 0; i--) {
-        const int sr = sb_raster(log2n, i), xs = sr % sbw, ys = sr / sbw;
+        const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
         const int right = (xs + 1 < sbw) ? (int)((csbf >> (sr + 1)) & 1) : 0;
         const int below = (ys + 1 < sbw) ? (int)((csbf >> (sr + sbw)) & 1) : 0;
         bool coded = (csbf >> sr) & 1;
@@ -705,7 +798,7 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx) {
         const int prev_csbf = right | (below << 1);
         int lev[16];
         for (int k = 0; k < 16; k++) {
-            const int r = diag4_raster(k);
+            const int r = scan4_raster(scan, k);
             lev[k] = c[(ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3)];
         }
         // sig_coeff_flag
@@ -714,7 +807,7 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx) {
         if (i == last_i) sig |= 1u << last_n;
         for (int k = start; k >= 0; k--) {
             if (!coded) break;
-            const int r = diag4_raster(k);
+            const int r = scan4_raster(scan, k);
             const int xc = xs * 4 + (r & 3), yc = ys * 4 + (r >> 2);
             const bool s = lev[k] != 0;
             if (k == 0 && infer_dc) {   // inferred 1 when no other flag of the sub-block was 1
@@ -734,7 +827,7 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx) {
                 else sctx = 2;
                 if (cidx == 0) {
                     if (xs > 0 || ys > 0) sctx += 3;
-                    sctx += log2n == 3 ? 9 : 21;
+                    sctx += log2n == 3 ? (scan == SCAN_DIAG ? 9 : 15) : 21;
                 } else {
                     sctx += log2n == 3 ? 9 : 12;
                 }
@@ -897,32 +990,69 @@ SK_HD void code_cu(W& w, const CuInfo& cu, const int16_t* coef, bool p_slice, in
             if (cu.cbf == 0) return;
         }
     }
-    // transform_tree at depth 0 (no split): cbf_cb, cbf_cr, cbf_luma
+    // transform_tree (7.3.8.8): split_transform_flag at log2 4 (ctxInc 1), the depth-0
+    // chroma cbfs, then either the 16x16 transform unit or four 8x8 ones (depth 1: no
+    // further split, chroma cbfs under a set parent flag, cbf_luma always coded)
+    const bool intra = cu.mode == CU_INTRA;
+    const bool split = (cu.tu >> 4) & 1;
+    w.ctx(CTX_SPLIT_TF + 1, split);
     w.ctx(CTX_CBF_CHROMA + 0, cbf_cb);
     w.ctx(CTX_CBF_CHROMA + 0, cbf_cr);
-    if (cu.mode == CU_INTRA || cbf_cb || cbf_cr) w.ctx(CTX_CBF_LUMA + 1, cbf_y);
-    if (cbf_y) code_residual(w, coef, 4, 0);
-    if (cbf_cb) code_residual(w, coef + kCoefCb, 3, 1);
-    if (cbf_cr) code_residual(w, coef + kCoefCr, 3, 2);
+    if (!split) {
+        if (intra || cbf_cb || cbf_cr) w.ctx(CTX_CBF_LUMA + 1, cbf_y);
+        const int sy = intra ? intra_scan(cu.intra_mode, 4, 0) : SCAN_DIAG;
+        const int sc = intra ? intra_scan(cu.intra_mode, 3, 1) : SCAN_DIAG;
+        if (cbf_y) code_residual(w, coef, 4, 0, sy);
+        if (cbf_cb) code_residual(w, coef + kCoefCb, 3, 1, sc);
+        if (cbf_cr) code_residual(w, coef + kCoefCr, 3, 2, sc);
+        return;
+    }
+    const int sy = intra ? intra_scan(cu.intra_mode, 3, 0) : SCAN_DIAG;
+    const int s4 = intra ? intra_scan(cu.intra_mode, 2, 0) : SCAN_DIAG;
+    const int sc = intra ? intra_scan(cu.intra_mode, 2, 1) : SCAN_DIAG;
+    for (int q = 0; q < 4; q++) {
+        const int cb = (cu.tuc >> q) & 1, cr = (cu.tuc >> (4 + q)) & 1;
+        const bool split8 = (cu.tu >> q) & 1;
+        w.ctx(CTX_SPLIT_TF + 2, split8);   // log2 3
+        if (cbf_cb) w.ctx(CTX_CBF_CHROMA + 1, cb);
+        if (cbf_cr) w.ctx(CTX_CBF_CHROMA + 1, cr);
+        if (!split8) {
+            const int cy = (cu.ycbf >> (4 * q)) & 1;
+            w.ctx(CTX_CBF_LUMA + 0, cy);
+            if (cy) code_residual(w, coef + 64 * q, 3, 0, sy);
+        } else {
+            for (int j = 0; j < 4; j++) {   // depth 2: chroma of the node after the last 4x4 (blkIdx 3)
+                const int cy = (cu.ycbf >> (4 * q + j)) & 1;
+                w.ctx(CTX_CBF_LUMA + 0, cy);
+                if (cy) code_residual(w, coef + 64 * q + 16 * j, 2, 0, s4, (cu.tsy >> (4 * q + j)) & 1);
+            }
+        }
+        if (cb) code_residual(w, coef + kCoefCb + 16 * q, 2, 1, sc, (cu.tsc >> q) & 1);
+        if (cr) code_residual(w, coef + kCoefCr + 16 * q, 2, 2, sc, (cu.tsc >> (4 + q)) & 1);
+    }
 }
 
 // ---------------------------------------------------------------------------
-// Deblocking (8.7.2), for this coding structure: CU = PU = TU = 16x16, so the
-// filtered luma edges are the CU boundaries (every 16 samples), one boundary
-// strength per CU edge, and the chroma edges (bS 2 only) are the same boundaries
-// on the 8-sample chroma grid. Edges at the picture border and between slices
-// (pps_loop_filter_across_slices_enabled_flag = 0) are not filtered. All vertical
-// edges of the picture first, then the horizontal ones on their output.
+// Deblocking (8.7.2), for this coding structure: CU = PU = 16x16 with 16x16 or 8x8 TUs,
+// so the filtered luma edges are the CU boundaries and the inner TU edges of split CUs
+// (the 8x8 grid), with a boundary strength per 4-sample segment (the TUs on its two
+// sides), and the chroma edges (bS 2 only) are the CU boundaries on the 8-sample chroma
+// grid (inner TU edges fall on chroma 4). Edges at the picture border and between
+// slices (pps_loop_filter_across_slices_enabled_flag = 0) are not filtered. All
+// vertical edges of the picture first, then the horizontal ones on their output.
 SK_TABLE uint8_t HEVC_BETA[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
                                   8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
                                   34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};   // Table 8-11 beta'
 SK_TABLE uint8_t HEVC_TC[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  1,  1,  1,  1,  1,  1,  1, 1, 1,
                                 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
 
-// Boundary strength between the CUs on the two sides of an edge (8.7.2.4).
-SK_HD int dbk_bs(const CuInfo& p, const CuInfo& q) {
+// cbf_luma of the transform block covering luma sample (x, y) of the CU (0..15).
+SK_HD int tu_cbf_y(const CuInfo& c, int x, int y) { return (c.ycbf >> zorder4(x >> 2, y >> 2)) & 1; }
+// Boundary strength of an edge segment (8.7.2.4) between CUs p and q (the same CU for an
+// inner TU edge) whose luma transform blocks on the two sides have cbf pc / qc.
+SK_HD int dbk_bs(const CuInfo& p, const CuInfo& q, int pc, int qc) {
     if (p.mode == CU_INTRA || q.mode == CU_INTRA) return 2;
-    if ((p.cbf | q.cbf) & 1) return 1;   // a luma transform block with coefficients
+    if (pc | qc) return 1;   // a luma transform block with coefficients
     const int dx = p.mvx - q.mvx, dy = p.mvy - q.mvy;   // one reference picture: motion only
     return (dx >= 4 || dx <= -4 || dy >= 4 || dy <= -4) ? 1 : 0;
 }
@@ -980,33 +1110,46 @@ SK_HD void dbk_chroma_line(uint8_t* q, int step, int qp) {
 
 // The whole picture (CPU reference; k_hevc_dbk_v / k_hevc_dbk_h are the same loops in
 // parallel). cus: [ctb_h][ctb_w]; rows_per_slice: CTB rows per slice.
+// One luma segment: the vertical (vert) or horizontal edge at luma position e (a
+// multiple of 8, > 0) of the picture, 4 samples long from position a along the edge.
+// Returns without filtering when the edge is an unsplit CU's inside or bS is 0.
+SK_HD void dbk_luma_edge(uint8_t* Y, int sy, const CuInfo* cus, int ctb_w, bool vert, int e, int a) {
+    const int x = vert ? e : a, y = vert ? a : e;
+    const CuInfo& q = cus[(y >> 4) * ctb_w + (x >> 4)];
+    const CuInfo& p = vert ? cus[(y >> 4) * ctb_w + ((x - 1) >> 4)] : cus[((y - 1) >> 4) * ctb_w + (x >> 4)];
+    if ((e & 8) && !(q.tu & 16)) return;   // no transform edge inside an unsplit CU
+    const int pc = vert ? tu_cbf_y(p, (x - 1) & 15, y & 15) : tu_cbf_y(p, x & 15, (y - 1) & 15);
+    const int bs = dbk_bs(p, q, pc, tu_cbf_y(q, x & 15, y & 15));
+    if (bs) dbk_luma_segment(Y + (size_t)y * sy + x, vert ? 1 : sy, vert ? sy : 1, bs, (p.qp + q.qp + 1) >> 1);
+}
 SK_HD void deblock_picture(uint8_t* Y, uint8_t* U, uint8_t* V, int sy, int sc, const CuInfo* cus, int ctb_w,
                            int ctb_h, int rows_per_slice) {
-    for (int cy = 0; cy < ctb_h; cy++)   // vertical edges
+    for (int x = 8; x < 16 * ctb_w; x += 8)   // vertical edges
+        for (int a = 0; a < 16 * ctb_h; a += 4) dbk_luma_edge(Y, sy, cus, ctb_w, true, x, a);
+    for (int cy = 0; cy < ctb_h; cy++)
         for (int cx = 1; cx < ctb_w; cx++) {
             const CuInfo &p = cus[cy * ctb_w + cx - 1], &q = cus[cy * ctb_w + cx];
-            const int bs = dbk_bs(p, q), qp = (p.qp + q.qp + 1) >> 1;
-            if (!bs) continue;
-            for (int k = 0; k < 4; k++)
-                dbk_luma_segment(Y + (size_t)(cy * 16 + 4 * k) * sy + cx * 16, 1, sy, bs, qp);
-            if (bs == 2)
-                for (int l = 0; l < 8; l++) {
-                    dbk_chroma_line(U + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
-                    dbk_chroma_line(V + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
-                }
+            if (p.mode != CU_INTRA && q.mode != CU_INTRA) continue;   // chroma: bS 2 only
+            const int qp = (p.qp + q.qp + 1) >> 1;
+            for (int l = 0; l < 8; l++) {
+                dbk_chroma_line(U + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
+                dbk_chroma_line(V + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
+            }
         }
-    for (int cy = 1; cy < ctb_h; cy++) {   // horizontal edges (not between slices)
+    for (int y = 8; y < 16 * ctb_h; y += 8) {   // horizontal edges (not between slices)
+        if (!(y & 8) && (y >> 4) % rows_per_slice == 0) continue;
+        for (int a = 0; a < 16 * ctb_w; a += 4) dbk_luma_edge(Y, sy, cus, ctb_w, false, y, a);
+    }
+    for (int cy = 1; cy < ctb_h; cy++) {
         if (cy % rows_per_slice == 0) continue;
         for (int cx = 0; cx < ctb_w; cx++) {
             const CuInfo &p = cus[(cy - 1) * ctb_w + cx], &q = cus[cy * ctb_w + cx];
-            const int bs = dbk_bs(p, q), qp = (p.qp + q.qp + 1) >> 1;
-            if (!bs) continue;
-            for (int k = 0; k < 4; k++) dbk_luma_segment(Y + (size_t)(cy * 16) * sy + cx * 16 + 4 * k, sy, 1, bs, qp);
-            if (bs == 2)
-                for (int l = 0; l < 8; l++) {
-                    dbk_chroma_line(U + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
-                    dbk_chroma_line(V + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
-                }
+            if (p.mode != CU_INTRA && q.mode != CU_INTRA) continue;
+            const int qp = (p.qp + q.qp + 1) >> 1;
+            for (int l = 0; l < 8; l++) {
+                dbk_chroma_line(U + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
+                dbk_chroma_line(V + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
+            }
         }
     }
 }

@@ -16,33 +16,31 @@ using h264::ACT_P;
 using h264::ACT_SKIPALL;
 using h264::SliceTask;
 
-void build_intra_ref(const uint8_t* plane, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
-                     uint8_t* ref) {
+void build_intra_ref_av(const uint8_t* plane, int stride, int x0, int y0, int n, int avail, uint8_t* ref) {
     uint8_t av[4 * 32 + 1];
     const int len = 4 * n + 1;
     memset(av, 0, (size_t)len);
     memset(ref, 0, (size_t)len);
-    // left column p[-1][y], y = 0..n-1 at ref[2n-1-y]; below-left (y >= n) never available
-    if (left)
-        for (int y = 0; y < n; y++) {
+    // left column p[-1][y], y = 0..2n-1 at ref[2n-1-y] (y >= n: below-left)
+    for (int y = 0; y < 2 * n; y++)
+        if (avail & (y < n ? AV_L : AV_BL)) {
             ref[2 * n - 1 - y] = plane[(size_t)(y0 + y) * stride + x0 - 1];
             av[2 * n - 1 - y] = 1;
         }
-    if (left && top) {
+    if (avail & AV_TL) {
         ref[2 * n] = plane[(size_t)(y0 - 1) * stride + x0 - 1];
         av[2 * n] = 1;
     }
-    if (top)
-        for (int x = 0; x < n; x++) {
-            ref[2 * n + 1 + x] = plane[(size_t)(y0 - 1) * stride + x0 + x];
-            av[2 * n + 1 + x] = 1;
-        }
-    if (tr)
-        for (int x = n; x < 2 * n; x++) {
+    for (int x = 0; x < 2 * n; x++)
+        if (avail & (x < n ? AV_T : AV_TR)) {
             ref[2 * n + 1 + x] = plane[(size_t)(y0 - 1) * stride + x0 + x];
             av[2 * n + 1 + x] = 1;
         }
     intra_substitute(ref, av, n);
+}
+void build_intra_ref(const uint8_t* plane, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
+                     uint8_t* ref) {
+    build_intra_ref_av(plane, stride, x0, y0, n, cu_avail(left, top, tr), ref);
 }
 
 void intra_predict(const uint8_t* ref_raw, int log2n, int mode, int cidx, uint8_t* pred) {
@@ -152,34 +150,170 @@ void CpuHevcEncoder::load_cu_src(int cx, int cy, uint8_t* y, uint8_t* u, uint8_t
     }
 }
 
-// Transform + quantisation of one TU from source and prediction; returns cbf and
-// writes the reconstruction.
-static int code_tu(const uint8_t* src, const uint8_t* pred, int log2n, int qp, bool intra, int16_t* lev,
-                   uint8_t* rec) {
+// Transform + quantisation of one TU from source and prediction (n x n rasters); the
+// TU is zeroed when that costs less (hevc_core.h RD model). Returns cbf, writes the
+// levels and the reconstruction and adds the TU's RD cost to *J.
+static int code_tu_1(const uint8_t* src, const uint8_t* pred, int log2n, int qp, bool intra, int lam, int16_t* lev,
+                     uint8_t* rec, long long* J, bool dst, bool ts) {
     const int n = 1 << log2n, nn = n * n;
     int res[256], c[256], d[256], r[256];
     for (int i = 0; i < nn; i++) res[i] = (int)src[i] - (int)pred[i];
-    fwd_transform(res, log2n, c);
-    int nz = 0;
+    if (ts) ts_forward(res, c);
+    else fwd_transform(res, log2n, c, dst);
+    int nz = 0, rate = kTuRateHalf;
+    long long sse0 = 0, sse1 = 0;
     for (int i = 0; i < nn; i++) {
         const int l = quant_level(c[i], qp, log2n, intra);
         lev[i] = (int16_t)l;
         nz |= l;
+        rate += level_rate_half(l);
         d[i] = dequant_level(l, qp, log2n);
+        sse0 += (long long)res[i] * res[i];
     }
     if (nz) {
-        inv_transform(d, log2n, r);
-        for (int i = 0; i < nn; i++) rec[i] = (uint8_t)sk_clip255(pred[i] + r[i]);
-    } else {
+        if (ts) ts_inverse(d, r);
+        else inv_transform(d, log2n, r, dst);
+        for (int i = 0; i < nn; i++) {
+            rec[i] = (uint8_t)sk_clip255(pred[i] + r[i]);
+            const int e = (int)src[i] - (int)rec[i];
+            sse1 += (long long)e * e;
+        }
+        if (512 * sse0 <= 512 * sse1 + (long long)lam * rate) nz = 0;   // zeroing is cheaper
+    }
+    if (!nz) {
+        for (int i = 0; i < nn; i++) lev[i] = 0;
         memcpy(rec, pred, (size_t)nn);
+        *J += 512 * sse0;
+    } else {
+        *J += 512 * sse1 + (long long)lam * rate;
     }
     return nz != 0;
+}
+// code_tu_1 with the transform (DST for intra luma 4x4); 4x4 TUs also try transform
+// skip and keep the cheaper (*ts = 1 when skipping wins; ties keep the transform).
+static int code_tu(const uint8_t* src, const uint8_t* pred, int log2n, int qp, bool intra, int lam, int16_t* lev,
+                   uint8_t* rec, long long* J, bool dst = false, int* ts = nullptr) {
+    if (ts) *ts = 0;
+    if (log2n != 2 || !ts) return code_tu_1(src, pred, log2n, qp, intra, lam, lev, rec, J, dst, false);
+    long long j0 = 0, j1 = 0;
+    int16_t l1[16];
+    uint8_t r1[16];
+    const int f0 = code_tu_1(src, pred, 2, qp, intra, lam, lev, rec, &j0, dst, false);
+    const int f1 = code_tu_1(src, pred, 2, qp, intra, lam, l1, r1, &j1, dst, true);
+    if (f1 && j1 < j0) {
+        memcpy(lev, l1, sizeof(l1));
+        memcpy(rec, r1, sizeof(r1));
+        *ts = 1;
+        *J += j1;
+        return f1;
+    }
+    *J += j0;
+    return f0;
+}
+
+// n x n block at (x, y) of a raster with row pitch `pitch` <-> contiguous n x n.
+static void blk_get(const uint8_t* a, int pitch, int x, int y, int n, uint8_t* out) {
+    for (int r = 0; r < n; r++) memcpy(out + r * n, a + (y + r) * pitch + x, (size_t)n);
+}
+static void blk_put(uint8_t* a, int pitch, int x, int y, int n, const uint8_t* in) {
+    for (int r = 0; r < n; r++) memcpy(a + (y + r) * pitch + x, in + r * n, (size_t)n);
+}
+// One TU of a CU-sized raster (pitch 2^log2p): source / prediction block at (x, y),
+// reconstruction back into rec.
+static int code_tu_at(const uint8_t* src, const uint8_t* pred, int pitch, int x, int y, int log2n, int qp, bool intra,
+                      int lam, int16_t* lev, uint8_t* rec, long long* J, bool dst = false, int* ts = nullptr) {
+    const int n = 1 << log2n;
+    uint8_t s[256], p[256], r[256];
+    blk_get(src, pitch, x, y, n, s);
+    blk_get(pred, pitch, x, y, n, p);
+    const int f = code_tu(s, p, log2n, qp, intra, lam, lev, r, J, dst, ts);
+    blk_put(rec, pitch, x, y, n, r);
+    return f;
+}
+// The 4x4 units (z-order bits) that are 4x4 TUs for the node split mask split8.
+static uint16_t tu_units4(int split8) {
+    uint16_t m = 0;
+    for (int q = 0; q < 4; q++)
+        if ((split8 >> q) & 1) m |= (uint16_t)(15 << (4 * q));
+    return m;
+}
+// Fills ycbf (cbf_luma per 4x4 unit in z order) from the TU structure and luma cbfs:
+// c16 for an unsplit CU, c8 (bit q) for 8x8 TUs, c4 (bit 4q + j) for 4x4 ones.
+static uint16_t make_ycbf(const CuInfo& cu, int c16, int c8, int c4) {
+    if (!(cu.tu & 16)) return c16 ? 0xffff : 0;
+    uint16_t m = 0;
+    for (int q = 0; q < 4; q++)
+        m |= (uint16_t)((((cu.tu >> q) & 1) ? (c4 >> (4 * q)) & 15 : (((c8 >> q) & 1) ? 15 : 0)) << (4 * q));
+    return m;
+}
+
+// Residual of an inter CU (prediction in pry / pru / prv, 16x16 / 8x8 rasters): one
+// 16x16 TU or four 8x8 nodes, each one 8x8 TU or four 4x4 ones, whichever costs less;
+// levels into lev (kCoefPerCu), the reconstruction into ry / ru / rv, the TU fields into cu.
+static void code_inter_residual(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* pry,
+                                const uint8_t* pru, const uint8_t* prv, int qp, int16_t* lev, uint8_t* ry,
+                                uint8_t* ru, uint8_t* rv, CuInfo& cu) {
+    const int qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
+    int16_t la[kCoefPerCu], lb[kCoefPerCu], lc[256];
+    uint8_t ay[256], au[64], av[64], by[256], cy4[256], bu[64], bv[64];
+    long long ja = 0, jc = (long long)lam * kSplitRateHalf;   // jc: the split CU's chroma + flags
+    int cbfa = code_tu(sy, pry, 4, qp, false, lam, la, ay, &ja);
+    cbfa |= code_tu(su, pru, 3, qpc, false, lam, la + kCoefCb, au, &ja) << 1;
+    cbfa |= code_tu(sv, prv, 3, qpc, false, lam, la + kCoefCr, av, &ja) << 2;
+    int c8 = 0, c4 = 0, tuc = 0, split8 = 0, tsy = 0, tsc = 0, f = 0;
+    long long jsplit = 0;
+    for (int q = 0; q < 4; q++) {
+        const int x = 8 * (q & 1), y = 8 * (q >> 1);
+        long long j8 = 0, j4 = (long long)lam * kSplit8RateHalf;
+        c8 |= code_tu_at(sy, pry, 16, x, y, 3, qp, false, lam, lb + 64 * q, by, &j8) << q;
+        for (int j = 0; j < 4; j++) {
+            c4 |= code_tu_at(sy, pry, 16, x + 4 * (j & 1), y + 4 * (j >> 1), 2, qp, false, lam, lc + 64 * q + 16 * j, cy4,
+                             &j4, false, &f) << (4 * q + j);
+            tsy |= f << (4 * q + j);
+        }
+        if (j4 < j8) split8 |= 1 << q;
+        jsplit += j4 < j8 ? j4 : j8;
+        tuc |= code_tu_at(su, pru, 8, x / 2, y / 2, 2, qpc, false, lam, lb + kCoefCb + 16 * q, bu, &jc, false, &f) << q;
+        tsc |= f << q;
+        tuc |= code_tu_at(sv, prv, 8, x / 2, y / 2, 2, qpc, false, lam, lb + kCoefCr + 16 * q, bv, &jc, false, &f) << (q + 4);
+        tsc |= f << (q + 4);
+    }
+    jsplit += jc;
+    int ly = 0;   // luma cbf of the chosen split structure
+    for (int q = 0; q < 4; q++) ly |= ((split8 >> q) & 1) ? (c4 >> (4 * q)) & 15 : ((c8 >> q) & 1);
+    if (jsplit < ja && (ly | tuc)) {
+        for (int q = 0; q < 4; q++)
+            if ((split8 >> q) & 1) {
+                memcpy(lb + 64 * q, lc + 64 * q, 64 * sizeof(int16_t));
+                for (int r = 0; r < 8; r++) memcpy(by + (8 * (q >> 1) + r) * 16 + 8 * (q & 1), cy4 + (8 * (q >> 1) + r) * 16 + 8 * (q & 1), 8);
+            }
+        memcpy(lev, lb, sizeof(lb));
+        memcpy(ry, by, 256);
+        memcpy(ru, bu, 64);
+        memcpy(rv, bv, 64);
+        cu.tu = (uint8_t)(16 | split8);
+        cu.tuc = (uint8_t)tuc;
+        cu.ycbf = make_ycbf(cu, 0, c8, c4);
+        cu.tsy = (uint16_t)(tsy & cu.ycbf & tu_units4(split8));
+        cu.tsc = (uint8_t)(tsc & tuc);
+        cu.cbf = (uint8_t)((cu.ycbf ? 1 : 0) | ((tuc & 15) ? 2 : 0) | ((tuc >> 4) ? 4 : 0));
+    } else {
+        memcpy(lev, la, sizeof(la));
+        memcpy(ry, ay, 256);
+        memcpy(ru, au, 64);
+        memcpy(rv, av, 64);
+        cu.cbf = (uint8_t)cbfa;
+        cu.tu = cu.tuc = 0;
+        cu.ycbf = make_ycbf(cu, cbfa & 1, 0, 0);
+        cu.tsy = 0;
+        cu.tsc = 0;
+    }
 }
 
 void CpuHevcEncoder::code_slice_inter(int s) {
     const SliceTask& t = fe.tasks[s];
     const h264::Geometry& g = fe.g;
-    const int qp = t.qp, qpc = chroma_qp(qp);
+    const int qp = t.qp;
     for (int cy = t.first_row; cy < t.first_row + t.num_rows; cy++)
         for (int cx = 0; cx < geo.ctb_w; cx++) {
             const int idx = cy * geo.ctb_w + cx;
@@ -214,13 +348,11 @@ void CpuHevcEncoder::code_slice_inter(int s) {
                 }
             int16_t* lev = &coefs[(size_t)idx * kCoefPerCu];
             uint8_t ry[256], ru[64], rv[64];
-            int cbf = code_tu(sy, pry, 4, qp, false, lev, ry);
-            cbf |= code_tu(su, pru, 3, qpc, false, lev + kCoefCb, ru) << 1;
-            cbf |= code_tu(sv, prv, 3, qpc, false, lev + kCoefCr, rv) << 2;
+            code_inter_residual(sy, su, sv, pry, pru, prv, qp, lev, ry, ru, rv, cu);
+            const int cbf = cu.cbf;
             int midx = -1;
             for (int i = 0; i < kMaxMergeCand && midx < 0; i++)
                 if (mlx[i] == mvx && mly[i] == mvy) midx = i;
-            cu.cbf = (uint8_t)cbf;
             cu.qp = (uint8_t)qp;
             cu.mvx = (int16_t)mvx;
             cu.mvy = (int16_t)mvy;
@@ -246,31 +378,39 @@ void CpuHevcEncoder::code_slice_inter(int s) {
 }
 
 // I slices in two passes, like the H.264 intra path: (1) every CU independently
-// chooses its mode against the SOURCE neighbours (parallel on the GPU), (2) the
-// CTB wavefront predicts from the reconstruction with that mode.
+// chooses its mode against the SOURCE neighbours (parallel on the GPU), (2) the CTB
+// wavefront codes it from the reconstruction, choosing the transform tree by RD.
 void CpuHevcEncoder::code_slice_intra(int s) {
     const SliceTask& t = fe.tasks[s];
     const h264::Geometry& g = fe.g;
-    const int qp = t.qp, qpc = chroma_qp(qp);
+    const int qp = t.qp, qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
     for (int pass = 0; pass < 2; pass++)
         for (int cy = t.first_row; cy < t.first_row + t.num_rows; cy++)
             for (int cx = 0; cx < geo.ctb_w; cx++) {
                 const int idx = cy * geo.ctb_w + cx;
                 CuInfo& cu = cus[idx];
                 const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < geo.ctb_w;
-                const std::vector<uint8_t>* P = pass == 0 ? fe.src : fe.rec;
                 uint8_t sy[256], su[64], sv[64];
                 load_cu_src(cx, cy, sy, su, sv);
-                uint8_t refy[65], refu[33], refv[33];
-                build_intra_ref(P[0].data(), g.stride_y, cx * 16, cy * 16, 16, left, top, tr, refy);
                 if (pass == 0) {
+                    // the mode whose 4x4-TU prediction (each 4x4 block from its source
+                    // neighbours, as the split tree would predict it) is closest
+                    uint8_t ref4[16][17];
+                    for (int u = 0; u < 16; u++) {   // 4x4 unit u in z order
+                        const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
+                        build_intra_ref_av(fe.src[0].data(), g.stride_y, cx * 16 + 4 * bx, cy * 16 + 4 * by, 4,
+                                           tu_avail_at(bx, by, 1, left, top, tr), ref4[u]);
+                    }
                     int best = 1, best_sad = 0x7fffffff;
                     for (int k = 0; k < 35; k++) {   // HEVC_INTRA_ORDER, SAD + intra_mode_bias
                         const int m = HEVC_INTRA_ORDER[k];
-                        uint8_t pr[256];
-                        intra_predict(refy, 4, m, 0, pr);
                         int sad = intra_mode_bias(m, qp);
-                        for (int i = 0; i < 256; i++) sad += sk_abs((int)sy[i] - (int)pr[i]);
+                        for (int u = 0; u < 16; u++) {
+                            const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
+                            uint8_t pr[16];
+                            intra_predict(ref4[u], 2, m, 0, pr);
+                            for (int i = 0; i < 16; i++) sad += sk_abs((int)sy[(4 * by + (i >> 2)) * 16 + 4 * bx + (i & 3)] - (int)pr[i]);
+                        }
                         if (sad < best_sad) { best_sad = sad; best = m; }
                     }
                     memset(&cu, 0, sizeof(cu));
@@ -278,29 +418,94 @@ void CpuHevcEncoder::code_slice_intra(int s) {
                     cu.intra_mode = (uint8_t)best;
                     continue;
                 }
-                build_intra_ref(P[1].data(), g.stride_c, cx * 8, cy * 8, 8, left, top, tr, refu);
-                build_intra_ref(P[2].data(), g.stride_c, cx * 8, cy * 8, 8, left, top, tr, refv);
+                // closed-loop RD over the transform tree: the 16x16 TU against four 8x8
+                // nodes, each node's 8x8 TU against its four 4x4 TUs (z order, every TU
+                // predicted from the reconstruction of the ones before it)
                 const int mode = cu.intra_mode;
-                uint8_t pry[256], pru[64], prv[64];
-                intra_predict(refy, 4, mode, 0, pry);
-                intra_predict(refu, 3, mode, 1, pru);
-                intra_predict(refv, 3, mode, 2, prv);
                 int16_t* lev = &coefs[(size_t)idx * kCoefPerCu];
-                uint8_t ry[256], ru[64], rv[64];
-                int cbf = code_tu(sy, pry, 4, qp, true, lev, ry);
-                cbf |= code_tu(su, pru, 3, qpc, true, lev + kCoefCb, ru) << 1;
-                cbf |= code_tu(sv, prv, 3, qpc, true, lev + kCoefCr, rv) << 2;
-                cu.cbf = (uint8_t)cbf;
+                uint8_t* P[3] = {fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data()};
+                const int st[3] = {g.stride_y, g.stride_c, g.stride_c};
+                const uint8_t* S[3] = {sy, su, sv};
+                auto region = [&](int c, bool save, uint8_t* buf, int ox, int oy, int n) {
+                    uint8_t* base = P[c] + (size_t)(cy * (c ? 8 : 16) + oy) * st[c] + cx * (c ? 8 : 16) + ox;
+                    if (save) blk_get(base, st[c], 0, 0, n, buf);
+                    else blk_put(base, st[c], 0, 0, n, buf);
+                };
+                int tsf = 0;
+                auto tu = [&](int c, int log2n, int ox, int oy, int av, int16_t* l, long long* J) {
+                    const int n = 1 << log2n, x0 = cx * (c ? 8 : 16) + ox, y0 = cy * (c ? 8 : 16) + oy;
+                    uint8_t ref[65], pr[256], src[256], rec[256];
+                    build_intra_ref_av(P[c], st[c], x0, y0, n, av, ref);
+                    intra_predict(ref, log2n, mode, c, pr);
+                    blk_get(S[c], c ? 8 : 16, ox, oy, n, src);
+                    const int f = code_tu(src, pr, log2n, c ? qpc : qp, true, lam, l, rec, J, c == 0 && log2n == 2, &tsf);
+                    blk_put(P[c] + (size_t)y0 * st[c] + x0, st[c], 0, 0, n, rec);
+                    return f;
+                };
+                // (a) one 16x16 TU
+                int16_t la[kCoefPerCu], lb[kCoefPerCu], l4[64];
+                uint8_t ay[256], au[64], av8[64];
+                long long ja = 0, jb = (long long)lam * kSplitRateHalf;
+                const int avc = cu_avail(left, top, tr);
+                int cbfa = tu(0, 4, 0, 0, avc, la, &ja);
+                cbfa |= tu(1, 3, 0, 0, avc, la + kCoefCb, &ja) << 1;
+                cbfa |= tu(2, 3, 0, 0, avc, la + kCoefCr, &ja) << 2;
+                region(0, true, ay, 0, 0, 16);
+                region(1, true, au, 0, 0, 8);
+                region(2, true, av8, 0, 0, 8);
+                // (b) four nodes
+                int c8 = 0, c4 = 0, tuc = 0, tsy = 0, tsc = 0, split8 = 0;
+                for (int q = 0; q < 4; q++) {
+                    const int av = tu_avail(q, left, top, tr), ox = 8 * (q & 1), oy = 8 * (q >> 1);
+                    long long j8 = 0, j4 = (long long)lam * kSplit8RateHalf;
+                    uint8_t r8[64];
+                    const int f8 = tu(0, 3, ox, oy, av, lb + 64 * q, &j8);
+                    region(0, true, r8, ox, oy, 8);
+                    int f4 = 0, t4 = 0;
+                    for (int j = 0; j < 4; j++) {
+                        const int bx = 2 * (q & 1) + (j & 1), by = 2 * (q >> 1) + (j >> 1);
+                        f4 |= tu(0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, left, top, tr), l4 + 16 * j, &j4) << j;
+                        t4 |= tsf << j;
+                    }
+                    if (j4 < j8) {
+                        split8 |= 1 << q;
+                        memcpy(lb + 64 * q, l4, sizeof(l4));
+                        c4 |= f4 << (4 * q);
+                        tsy |= t4 << (4 * q);
+                        jb += j4;
+                    } else {
+                        region(0, false, r8, ox, oy, 8);
+                        c8 |= f8 << q;
+                        jb += j8;
+                    }
+                    tuc |= tu(1, 2, ox / 2, oy / 2, av, lb + kCoefCb + 16 * q, &jb) << q;
+                    tsc |= tsf << q;
+                    tuc |= tu(2, 2, ox / 2, oy / 2, av, lb + kCoefCr + 16 * q, &jb) << (q + 4);
+                    tsc |= tsf << (q + 4);
+                }
+                if (jb < ja) {
+                    memcpy(lev, lb, sizeof(lb));
+                    cu.tu = (uint8_t)(16 | split8);
+                    cu.tuc = (uint8_t)tuc;
+                    cu.ycbf = make_ycbf(cu, 0, c8, c4);
+                    cu.cbf = (uint8_t)((cu.ycbf ? 1 : 0) | ((tuc & 15) ? 2 : 0) | ((tuc >> 4) ? 4 : 0));
+                    cu.tsy = (uint16_t)tsy;
+                    cu.tsc = (uint8_t)tsc;
+                } else {
+                    memcpy(lev, la, sizeof(la));
+                    region(0, false, ay, 0, 0, 16);
+                    region(1, false, au, 0, 0, 8);
+                    region(2, false, av8, 0, 0, 8);
+                    cu.tu = cu.tuc = 0;
+                    cu.cbf = (uint8_t)cbfa;
+                    cu.ycbf = make_ycbf(cu, cbfa & 1, 0, 0);
+                    cu.tsy = 0;
+                    cu.tsc = 0;
+                }
                 cu.qp = (uint8_t)qp;
                 fe.me[idx].mvx = fe.me[idx].mvy = 0;
                 fe.me[idx].ref = 0;
                 fe.me[idx].fx = fe.me[idx].fy = 0;
-                for (int y = 0; y < 16; y++)
-                    memcpy(&fe.rec[0][(size_t)(cy * 16 + y) * g.stride_y + cx * 16], ry + y * 16, 16);
-                for (int y = 0; y < 8; y++) {
-                    memcpy(&fe.rec[1][(size_t)(cy * 8 + y) * g.stride_c + cx * 8], ru + y * 8, 8);
-                    memcpy(&fe.rec[2][(size_t)(cy * 8 + y) * g.stride_c + cx * 8], rv + y * 8, 8);
-                }
             }
 }
 

@@ -56,9 +56,11 @@ void append_nal(std::vector<uint8_t>& out, int type, const uint8_t* rbsp, size_t
 
 // ---- shared CU-level helpers (CPU reference; the kernels mirror them) ----------
 // Linear intra reference array (see intra_substitute) of an n x n block at (x0, y0)
-// of `plane`; bottom-left is never available (CTB = CU), top-right when tr_avail.
+// of `plane` for the whole CU (bottom-left never available), top-right when tr.
 void build_intra_ref(const uint8_t* plane, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
                      uint8_t* ref);
+// Same for any transform block, with the neighbour availability `avail` (AV_* bits).
+void build_intra_ref_av(const uint8_t* plane, int stride, int x0, int y0, int n, int avail, uint8_t* ref);
 // Prediction of an n x n block for `mode` (cidx 0 luma / 1,2 chroma) from a raw reference.
 void intra_predict(const uint8_t* ref_raw, int log2n, int mode, int cidx, uint8_t* pred);
 

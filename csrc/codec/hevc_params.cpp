@@ -106,8 +106,8 @@ void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<u
         s.ue(0);              // log2_diff_max_min_luma_coding_block_size: CTB 16x16
         s.ue(0);              // log2_min_luma_transform_block_size_minus2: 4x4
         s.ue(2);              // log2_diff_max_min_luma_transform_block_size: 16x16
-        s.ue(0);              // max_transform_hierarchy_depth_inter
-        s.ue(0);              // max_transform_hierarchy_depth_intra
+        s.ue(2);              // max_transform_hierarchy_depth_inter: 16x16, 8x8 or 4x4 TUs
+        s.ue(2);              // max_transform_hierarchy_depth_intra
         s.put1(0);            // scaling_list_enabled_flag
         s.put1(0);            // amp_enabled_flag
         s.put1(1);            // sample_adaptive_offset_enabled_flag (hevc_sao.h)
@@ -165,7 +165,7 @@ void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<u
         p.ue(0);              // num_ref_idx_l1_default_active_minus1
         p.se(0);              // init_qp_minus26
         p.put1(0);            // constrained_intra_pred_flag
-        p.put1(0);            // transform_skip_enabled_flag
+        p.put1(1);            // transform_skip_enabled_flag (4x4 TUs, the encoder's RD choice)
         p.put1(0);            // cu_qp_delta_enabled_flag
         p.se(0);              // pps_cb_qp_offset
         p.se(0);              // pps_cr_qp_offset

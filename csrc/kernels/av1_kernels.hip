@@ -1044,7 +1044,7 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
         const uint32_t kind = tv >> 30;
         const bool lit = kind == 1;
         const bool mine = b + L < ntok && (lit ? part == 0 : ec_owner(tv & 0x3fffff) == part);
-        uint64_t m = __ballot(mine && !lit);
+        uint64_t m = __ballot(mine && !lit), fast = 0;
         while (m) {
             const int i = __builtin_ctzll(m);
             asm volatile("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(i));   // m &= m - 1 in one SALU op
@@ -1071,6 +1071,29 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
                 if (cnt < 32) {
                     cnt++;
                     rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
+                } else {
+                    // A run: the next tokens of this wave repeat this one (the zero level
+                    // of a sparse block's high frequencies, in the same context, comes
+                    // in runs). With the rate fixed, every lane's update is a fixed
+                    // contraction: in y = (lane >= s ? 32768 - c : c) it is y -= y >> rate,
+                    // two VALU ops per symbol. The rows are captured in the y form and
+                    // the word builder converts them back (the `fast` tokens).
+                    const uint64_t eq = __ballot(tv == tt) & m;
+                    const uint64_t ne = m & ~eq;
+                    uint64_t run = eq & (ne ? (ne & (0 - ne)) - 1 : ~0ull);
+                    if (run) {
+                        m &= ~run;
+                        fast |= run;
+                        const bool hi = L >= s;
+                        int y = hi ? 32768 - (int)cache : (int)cache;
+                        do {
+                            const int j = __builtin_ctzll(run);
+                            asm volatile("s_bitset0_b64 %0, %1" : "+s"(run) : "s"(j));
+                            cap[j][L] = (uint16_t)y;
+                            y -= y >> rate;
+                        } while (run);
+                        cache = (uint32_t)(hi ? 32768 - y : y);
+                    }
                 }
             } else {   // gathered boolean: reads a partition CDF from LDS
                 evict();
@@ -1085,7 +1108,9 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
         uint32_t out = tv;   // literal
         if (kind == 0) {
             const int n = (int)((tv >> 26) & 15) + 1, s = (int)((tv >> 22) & 15);
-            const uint32_t chi = s < n - 1 ? (uint32_t)cap[L][s] : 0u, clo = s > 0 ? (uint32_t)cap[L][s - 1] : 0u;
+            uint32_t chi = s < n - 1 ? (uint32_t)cap[L][s] : 0u;
+            const uint32_t clo = s > 0 ? (uint32_t)cap[L][s - 1] : 0u;
+            if (s < n - 1 && ((fast >> L) & 1)) chi = 32768u - chi;   // a run token's row is in y form
             out = ec_word(clo, chi, n, s);
         } else if (kind != 1) {
             out = wst[L];

@@ -1143,48 +1143,47 @@ __global__ __launch_bounds__(64) void k_hevc_ep_copy(HevcArgs A) {
     }
 }
 
-// Deblocking (hevc_core.h deblock_picture, in parallel): every CU edge segment is an
-// independent work item (edges are 16 samples apart and a filter changes at most 3
-// samples per side). k_hevc_dbk_v: all vertical edges (luma 4-line segments, chroma
-// lines); k_hevc_dbk_h: the horizontal edges on its output, none between slices.
+// Deblocking (hevc_core.h deblock_picture, in parallel): every edge segment is an
+// independent work item (edges are 8 samples apart and a filter reads 4 / changes at
+// most 3 samples per side). k_hevc_dbk_v: all vertical edges (luma 4-line segments on
+// the 8x8 grid, chroma lines of CU edges); k_hevc_dbk_h: the horizontal edges on its
+// output, none between slices.
+__device__ __forceinline__ bool cu_intra_edge(const CuInfo& p, const CuInfo& q) {
+    return p.mode == CU_INTRA || q.mode == CU_INTRA;
+}
 __global__ __launch_bounds__(256) void k_hevc_dbk_v(HevcArgs A) {
     const h264::gpu::FrameArgs& f = A.f;
-    const int cw = f.mb_w, ch = f.mb_h, ne = cw - 1;
-    if (ne <= 0) return;
+    const int cw = f.mb_w, ch = f.mb_h, ne = cw - 1, nel = 2 * cw - 1;
     const int e = blockIdx.x * 256 + threadIdx.x;
-    const int nl = ch * 4 * ne, nc = ch * 8 * ne;
+    const int nl = ch * 4 * nel, nc = ch * 8 * ne;
     if (e < nl) {
-        const int cx = 1 + e % ne, seg = e / ne, cy = seg >> 2;
-        const CuInfo p = A.cus[cy * cw + cx - 1], q = A.cus[cy * cw + cx];
-        const int bs = dbk_bs(p, q);
-        if (bs) dbk_luma_segment(f.rec.y + (size_t)(seg * 4) * f.stride_y + cx * 16, 1, f.stride_y, bs, (p.qp + q.qp + 1) >> 1);
+        const int x = 8 * (1 + e % nel), seg = e / nel;
+        dbk_luma_edge(f.rec.y, f.stride_y, A.cus, cw, true, x, 4 * seg);
     } else if (e < nl + 2 * nc) {
         const int k0 = e - nl, plane = k0 / nc, k = k0 % nc;
         const int cx = 1 + k % ne, line = k / ne, cy = line >> 3;
         const CuInfo p = A.cus[cy * cw + cx - 1], q = A.cus[cy * cw + cx];
-        if (dbk_bs(p, q) == 2)
+        if (cu_intra_edge(p, q))
             dbk_chroma_line((plane ? f.rec.v : f.rec.u) + (size_t)line * f.stride_c + cx * 8, 1, (p.qp + q.qp + 1) >> 1);
     }
 }
 
 __global__ __launch_bounds__(256) void k_hevc_dbk_h(HevcArgs A) {
     const h264::gpu::FrameArgs& f = A.f;
-    const int cw = f.mb_w, ch = f.mb_h, ne = ch - 1;
-    if (ne <= 0) return;
+    const int cw = f.mb_w, ch = f.mb_h, ne = ch - 1, nel = 2 * ch - 1;
+    if (nel <= 0) return;
     const int e = blockIdx.x * 256 + threadIdx.x;
-    const int nl = ne * cw * 4, nc = ne * cw * 8;
+    const int nl = nel * cw * 4, nc = ne * cw * 8;
     if (e < nl) {
-        const int cy = 1 + e / (cw * 4), x4 = e % (cw * 4), cx = x4 >> 2;
-        if (cy % f.rows_per_slice == 0) return;   // slice boundary
-        const CuInfo p = A.cus[(cy - 1) * cw + cx], q = A.cus[cy * cw + cx];
-        const int bs = dbk_bs(p, q);
-        if (bs) dbk_luma_segment(f.rec.y + (size_t)(cy * 16) * f.stride_y + x4 * 4, f.stride_y, 1, bs, (p.qp + q.qp + 1) >> 1);
+        const int y = 8 * (1 + e / (cw * 4)), x4 = e % (cw * 4);
+        if (!(y & 8) && (y >> 4) % f.rows_per_slice == 0) return;   // slice boundary
+        dbk_luma_edge(f.rec.y, f.stride_y, A.cus, cw, false, y, 4 * x4);
     } else if (e < nl + 2 * nc) {
         const int k0 = e - nl, plane = k0 / nc, k = k0 % nc;
         const int cy = 1 + k / (cw * 8), col = k % (cw * 8), cx = col >> 3;
         if (cy % f.rows_per_slice == 0) return;
         const CuInfo p = A.cus[(cy - 1) * cw + cx], q = A.cus[cy * cw + cx];
-        if (dbk_bs(p, q) == 2)
+        if (cu_intra_edge(p, q))
             dbk_chroma_line((plane ? f.rec.v : f.rec.u) + (size_t)(cy * 8) * f.stride_c + col, f.stride_c, (p.qp + q.qp + 1) >> 1);
     }
 }
@@ -1346,7 +1345,7 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
     // in-loop deblocking, then the SAO decisions on the deblocked picture (CTB syntax)
     const int cw = a.f.mb_w, ch = a.f.mb_h;
-    const int nv = ch * 4 * (cw - 1) + 2 * ch * 8 * (cw - 1), nh = (ch - 1) * cw * 4 + 2 * (ch - 1) * cw * 8;
+    const int nv = ch * 4 * (2 * cw - 1) + 2 * ch * 8 * (cw - 1), nh = (2 * ch - 1) * cw * 4 + 2 * (ch - 1) * cw * 8;
     if (nv > 0) hipLaunchKernelGGL(k_hevc_dbk_v, dim3((nv + 255) / 256), dim3(256), 0, s, a);
     if (nh > 0) hipLaunchKernelGGL(k_hevc_dbk_h, dim3((nh + 255) / 256), dim3(256), 0, s, a);
     const int nq = (n + 3) / 4;

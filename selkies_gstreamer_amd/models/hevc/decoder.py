@@ -444,8 +444,8 @@ class HevcDecoder:
         p.lists_modification = bool(b.u(1))
         p.log2_par_mrg = b.ue() + 2
         p.slice_header_ext = bool(b.u(1))
-        if p.sign_hiding or p.transform_skip:
-            raise NotImplementedError("sign hiding / transform skip")
+        if p.sign_hiding:
+            raise NotImplementedError("sign data hiding")
         self.pps = p
 
     # ---------------- pictures ----------------
@@ -1113,6 +1113,8 @@ class HevcDecoder:
                 scan_idx = 2
             elif 22 <= intra_mode <= 30:
                 scan_idx = 1
+        # transform_skip_flag (7.3.8.11): 4x4 TUs when the PPS enables it
+        ts = bool(self.pps.transform_skip and log2 == 2 and self._dec("transform_skip_flag", 0 if cidx == 0 else 1))
         # last significant coefficient
         if cidx == 0:
             off, sh = 3 * (log2 - 2) + ((log2 - 1) >> 2), (log2 + 1) >> 2
@@ -1262,7 +1264,10 @@ class HevcDecoder:
         scale = 16 * LEVEL_SCALE[qp % 6] << (qp // 6)
         d = np.clip((levels * scale + (1 << (bd - 1))) >> bd, -32768, 32767)
         dst = cidx == 0 and log2 == 2 and intra_mode is not None
-        r = inverse_transform(d, n, dst)
+        if ts:   # 8.6.4.2: r = d << 7, then the same (r + 2^11) >> 12 as after a transform
+            r = ((d << 7) + (1 << 11)) >> 12
+        else:
+            r = inverse_transform(d, n, dst)
         plane = "YUV"[cidx]
         blk = self.cur[plane][y0:y0 + n, x0:x0 + n].astype(np.int64)
         self.cur[plane][y0:y0 + n, x0:x0 + n] = np.clip(blk + r, 0, 255)

@@ -77,7 +77,7 @@ def test_hevc_static_content_is_all_skip():
         assert np.array_equal(Y, _rec_y(enc, W, H))
         sizes.append(len(pk.data))
     assert max(sizes) < 60   # skip-all slices: a few bytes each
-    cus = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 16)
+    cus = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 24)
     assert (cus[:, 0] == 0).all()   # CU_SKIP
     enc.close()
 
@@ -126,7 +126,7 @@ def test_hevc_directional_intra_modes():
     pk = enc.encode(f, 0)[0]
     Y = HevcDecoder().decode(pk.data[10:])[0][0]
     assert np.array_equal(Y, _rec_y(enc, W, H))
-    modes = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 16)[:, 3]
+    modes = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 24)[:, 3]
     assert np.count_nonzero(~np.isin(modes, [0, 1, 10, 26])) > len(modes) // 2
     assert len(pk.data) < 7000, len(pk.data)
     assert psnr(Y, _luma(f)) > 45

@@ -55,17 +55,29 @@ def main():
     part = ((offs.astype(np.uint64) * 0x9E3779B1) & 0xFFFFFFFF) >> 28
     loads = np.bincount(part.astype(np.int64), weights=cnt, minlength=16)
     # the critical path of k_av1_cdf: the largest per-wave symbol load over all tiles
-    crit, crit_top = 0, 0
+    # and its serial steps when a run of identical tokens in one wave's stream costs one
+    # step (the k_av1_cdf run path; runs are cut at 64-token sub-batches)
+    crit, crit_top, crit_runs = 0, 0, 0
     for t in range(ntok.size):
         tt = tokc[t * cap: t * cap + ntok[t]]
-        st = tt[(tt >> 30) != 1] & 0x3fffff
+        idx = np.nonzero((tt >> 30) != 1)[0]
+        full = tt[idx]
+        st = full & 0x3fffff
         if st.size == 0:
             continue
         o, c = np.unique(st, return_counts=True)
         pa = ((o.astype(np.uint64) * 0x9E3779B1) & 0xFFFFFFFF) >> 28
         crit = max(crit, int(np.bincount(pa.astype(np.int64), weights=c, minlength=16).max()))
         crit_top = max(crit_top, int(c.max()))
-    out = {"cdf_critical_symbols": crit, "cdf_hottest_context_symbols": crit_top,
+        owner = (((st.astype(np.uint64) * 0x9E3779B1) & 0xFFFFFFFF) >> 28).astype(np.int64)
+        for p_ in range(16):
+            sel = owner == p_
+            w, pos = full[sel], idx[sel]
+            if w.size:
+                head = np.ones(w.size, bool)
+                head[1:] = (w[1:] != w[:-1]) | (pos[1:] // 64 != pos[:-1] // 64)
+                crit_runs = max(crit_runs, int(head.sum()))
+    out = {"cdf_critical_symbols": crit, "cdf_critical_run_heads": crit_runs, "cdf_hottest_context_symbols": crit_top,
            "max_tile_contexts": int(offs.size),
            "max_tile_top_contexts": [[int(offs[i]), int(cnt[i])] for i in order[:12]],
            "max_tile_partition_loads": [int(x) for x in loads],
