@@ -503,24 +503,20 @@ SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int 
         }
         return dc;
     }
+    // main reference array (8.4.4.2.6) in closed form: refm(k), k = -N .. 2N, the main
+    // side for k >= 0, the other side projected through invAngle for k < 0 (read only
+    // for the negative angles that need it)
     const int angle = HEVC_INTRA_ANGLE[mode];
-    // main reference array refm[k], k = -N .. 2N (index k + N)
-    int refm[3 * 32 + 1];
     const bool vert = mode >= 18;
-    auto side = [&](int k) { return vert ? T(k - 1) : L(k - 1); };     // k = 0..2N: main side incl. corner
-    auto other = [&](int k) { return vert ? L(k - 1) : T(k - 1); };    // projected side
-    for (int k = 0; k <= 2 * n; k++) refm[k + n] = side(k);
-    if (angle < 0) {
-        const int last = (n * angle) >> 5;
-        if (last < -1) {
-            const int inv = intra_inv_angle(mode);
-            for (int k = last; k <= -1; k++) refm[k + n] = other(((k * inv + 128) >> 8));
-        }
-    }
+    auto refm = [&](int k) {
+        if (k >= 0) return vert ? T(k - 1) : L(k - 1);
+        const int j = (k * intra_inv_angle(mode) + 128) >> 8;
+        return vert ? L(j - 1) : T(j - 1);
+    };
     const int a = vert ? y : x, b = vert ? x : y;   // a: distance from the main side, b: along it
     const int idx = ((a + 1) * angle) >> 5, fact = ((a + 1) * angle) & 31;
-    int v = fact ? ((32 - fact) * refm[b + idx + 1 + n] + fact * refm[b + idx + 2 + n] + 16) >> 5
-                 : refm[b + idx + 1 + n];
+    const int k0 = b + idx + 1;
+    int v = fact ? ((32 - fact) * refm(k0) + fact * refm(k0 + 1) + 16) >> 5 : refm(k0);
     if (cidx == 0 && n < 32) {
         if (mode == 26 && x == 0) v = sk_clip255(T(0) + ((L(y) - L(-1)) >> 1));
         if (mode == 10 && y == 0) v = sk_clip255(L(0) + ((T(x) - T(-1)) >> 1));

@@ -40,124 +40,177 @@ __device__ __forceinline__ int wsum(int v) {
     return v;
 }
 
-// Per-wave LDS working set of one CU.
+// Per-wave LDS working set of one CU. Sample rasters (src, pred, rec*) hold the CU's
+// 384 samples: Y 16x16 (pitch 16) | Cb 8x8 | Cr 8x8 (pitch 8).
 struct CuLds {
-    uint8_t src[kCoefPerCu];     // Y 16x16 | Cb 8x8 | Cr 8x8 (raster)
+    uint8_t src[kCoefPerCu];
     uint8_t pred[kCoefPerCu];
-    int32_t a[kCoefPerCu];       // residual / dequantised coefficients
-    int32_t b[kCoefPerCu];       // transform intermediate
-    uint8_t ref[65 + 65 + 33 + 33];   // intra: luma raw | luma filtered | Cb | Cr
-    uint8_t refm[3][64];              // intra, directional modes: main reference arrays (Y, Cb, Cr)
-    int misc[4];
+    uint8_t recA[kCoefPerCu];    // the 16x16 TU (+ 8x8 chroma TUs)
+    uint8_t recS[kCoefPerCu];    // the split tree (inter: 8x8 luma TUs + 4x4 chroma; intra: its committed reconstruction)
+    uint8_t rec4[kCoefPerCu];    // 4x4 luma TUs | trials with transform skip
+    uint8_t rec4t[kCoefPerCu];   // 4x4 luma TUs with transform skip | intra: the node's 8x8 trial
+    int32_t a[256], b[256];      // batch intermediates (compact, TU-major)
+    int16_t levA[kCoefPerCu], lev8[256], lev4[256], lev4t[256], levc[128], levct[128];
+    int acc[4][16];              // per-TU sums of a batch: SSE of the prediction, of the reconstruction, rate, non-zero
+    long long tj[6][16];         // per-TU RD cost: 0 Y16 Cb8 Cr8, 1 Y8, 2 Y4, 3 Y4 transform skip, 4 C4, 5 C4 skip
+    int tf[6][16];               // per-TU cbf, same slots
+    uint8_t ref[2][68];          // intra: the TU's reference samples (raw, [1 2 1]-filtered)
+    uint8_t ref4[16][17];        // intra mode decision: the sixteen 4x4 blocks' references
     int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];   // inter: merge / AMVP candidates
 };
 
-// LDS copy of the 16-point DCT matrix (the 8-point one is its even rows).
+// LDS copy of the 16-point DCT matrix (the 8 / 4-point ones are its rows 2k / 4k).
 __device__ __forceinline__ void load_t16(int8_t* t) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) t[i] = HEVC_T16[i >> 4][i & 15];
 }
-
-// Transform, quantisation and reconstruction of the CU in L (src, pred filled).
-// Lane mapping: luma outputs (row l >> 2, columns 4*(l & 3) .. +3), chroma outputs
-// (component l >> 5, row (l >> 2) & 7, columns 2*(l & 3) .. +1). Writes the levels to
-// `gcoef` (global) and the reconstruction into L.pred; returns the cbf bits.
-__device__ __forceinline__ int code_cu_wave(CuLds& L, const int8_t* T, int qp, bool intra, int16_t* gcoef) {
-    const int l = lane();
-    const int qpc = chroma_qp(qp);
-    const int ly = l >> 2, lx0 = 4 * (l & 3);
-    const int cc = l >> 5, cy = (l >> 2) & 7, cx0 = 2 * (l & 3);
-    const int cbase = kCoefCb + cc * 64;
-    for (int i = l; i < kCoefPerCu; i += 64) L.a[i] = (int)L.src[i] - (int)L.pred[i];
-    wsync();
-    // forward stage 1 (rows): b[y][u] = (sum_x T[u][x] a[y][x] + rnd) >> sh1
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int u = lx0 + k;
-        int s = 0;
-#pragma unroll
-        for (int x = 0; x < 16; x++) s += (int)T[u * 16 + x] * L.a[ly * 16 + x];
-        L.b[ly * 16 + u] = (s + 4) >> 3;
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int u = cx0 + k;
-        int s = 0;
-#pragma unroll
-        for (int x = 0; x < 8; x++) s += (int)T[(2 * u) * 16 + x] * L.a[cbase + cy * 8 + x];
-        L.b[cbase + cy * 8 + u] = (s + 2) >> 2;
-    }
-    wsync();
-    // forward stage 2 (columns) + quantisation + dequantisation; levels to global
-    int nzl = 0, nzc = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int u = lx0 + k, v = ly;
-        int s = 0;
-#pragma unroll
-        for (int y = 0; y < 16; y++) s += (int)T[v * 16 + y] * L.b[y * 16 + u];
-        const int c = (s + 512) >> 10;
-        const int lv = quant_level(c, qp, 4, intra);
-        nzl |= lv;
-        gcoef[v * 16 + u] = (int16_t)lv;
-        L.a[v * 16 + u] = dequant_level(lv, qp, 4);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int u = cx0 + k, v = cy;
-        int s = 0;
-#pragma unroll
-        for (int y = 0; y < 8; y++) s += (int)T[(2 * v) * 16 + y] * L.b[cbase + y * 8 + u];
-        const int c = (s + 256) >> 9;
-        const int lv = quant_level(c, qpc, 3, intra);
-        nzc |= lv;
-        gcoef[cbase + v * 8 + u] = (int16_t)lv;
-        L.a[cbase + v * 8 + u] = dequant_level(lv, qpc, 3);
-    }
-    const int cbf = (__ballot(nzl != 0) ? 1 : 0) | ((__ballot(nzc != 0 && cc == 0) ? 1 : 0) << 1) |
-                    ((__ballot(nzc != 0 && cc == 1) ? 1 : 0) << 2);
-    wsync();
-    // inverse stage 1 (columns): b[y][x] = clip16((sum_j T[j][y] a[j][x] + 64) >> 7)
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int x = lx0 + k, y = ly;
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) s += (int)T[j * 16 + y] * L.a[j * 16 + x];
-        L.b[y * 16 + x] = sk_clip((s + 64) >> 7, -32768, 32767);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int x = cx0 + k, y = cy;
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) s += (int)T[(2 * j) * 16 + y] * L.a[cbase + j * 8 + x];
-        L.b[cbase + y * 8 + x] = sk_clip((s + 64) >> 7, -32768, 32767);
-    }
-    wsync();
-    // inverse stage 2 (rows) + reconstruction into pred
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int x = lx0 + k, y = ly;
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) s += (int)T[j * 16 + x] * L.b[y * 16 + j];
-        const int i = y * 16 + x;
-        L.pred[i] = (uint8_t)sk_clip255((int)L.pred[i] + ((s + 2048) >> 12));
-    }
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const int x = cx0 + k, y = cy;
-        int s = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) s += (int)T[(2 * j) * 16 + x] * L.b[cbase + y * 8 + j];
-        const int i = cbase + y * 8 + x;
-        L.pred[i] = (uint8_t)sk_clip255((int)L.pred[i] + ((s + 2048) >> 12));
-    }
-    wsync();
-    return cbf;
+__device__ __forceinline__ int tx_m(const int8_t* T, int log2n, bool dst, int k, int x) {
+    return dst ? (int)HEVC_DST4[k][x] : (int)T[(k << (4 - log2n)) * 16 + x];
 }
 
-// Source samples of CU (cx, cy) into L.src; reconstruction L.pred to the rec planes.
+// TU t of a batch: CU-raster index of its top-left sample (the pitch follows: 16 in the
+// luma part, 8 in the chroma part). kind 0: luma TUs of size n in z order; 1: chroma
+// TUs, the Cb ones then the Cr ones; 2: the single TU at sb.
+__device__ __forceinline__ int tu_base(int kind, int log2n, int t, int sb) {
+    if (kind == 2) return sb;
+    const int n = 1 << log2n;
+    if (kind == 0) {
+        const int bx = (t & 1) | ((t >> 1) & 2), by = ((t >> 1) & 1) | ((t >> 2) & 2);
+        return by * n * 16 + bx * n;
+    }
+    const int half = (8 >> log2n) * (8 >> log2n), c = t / half, q = t % half;
+    return kCoefCb + 64 * c + (q >> 1) * n * 8 + (q & 1) * n;
+}
+
+// A batch of ntu same-size TUs coded in parallel, each exactly as hevc_cpu.cpp code_tu_1
+// (forward transform / DST / transform skip, quantisation, reconstruction, RD zeroing):
+// levels (compact, TU-major, raster inside the TU) into lev, the reconstruction into the
+// CU raster rec, per-TU RD cost and cbf into tj / tf. Items = samples, lane-strided.
+__device__ void tu_batch(CuLds& L, const int8_t* T, int kind, int sb, int log2n, int ntu, bool dst, bool ts, int qp,
+                         bool intra, int lam, int16_t* lev, uint8_t* rec, long long* tj, int* tf) {
+    const int l = lane(), n = 1 << log2n, nn = n * n, cnt = ntu * nn;
+    const int sh1 = log2n - 1, sh2 = log2n + 6;
+    if (l < 16) L.acc[0][l] = L.acc[1][l] = L.acc[2][l] = L.acc[3][l] = 0;
+    wsync();
+    // forward, rows: b[t][y][u] = sum_k M[u][k] res[t][y][k] (transform skip: res << 5)
+    for (int i = l; i < cnt; i += 64) {
+        const int t = i >> (2 * log2n), y = (i >> log2n) & (n - 1), u = i & (n - 1);
+        const int base = tu_base(kind, log2n, t, sb), o = base + y * (base < 256 ? 16 : 8);
+        const int e = (int)L.src[o + u] - (int)L.pred[o + u];
+        atomicAdd(&L.acc[0][t], e * e);
+        int v = e * 32;
+        if (!ts) {
+            int s = 0;
+            for (int k = 0; k < n; k++) s += tx_m(T, log2n, dst, u, k) * ((int)L.src[o + k] - (int)L.pred[o + k]);
+            v = (s + (1 << (sh1 - 1))) >> sh1;
+        }
+        L.b[i] = v;
+    }
+    wsync();
+    // forward, columns + quantisation + dequantisation
+    for (int i = l; i < cnt; i += 64) {
+        const int t = i >> (2 * log2n), v = (i >> log2n) & (n - 1), u = i & (n - 1);
+        int c = L.b[i];
+        if (!ts) {
+            int s = 0;
+            const int* bt = L.b + t * nn + u;
+            for (int k = 0; k < n; k++) s += tx_m(T, log2n, dst, v, k) * bt[k * n];
+            c = (s + (1 << (sh2 - 1))) >> sh2;
+        }
+        const int lv = quant_level(c, qp, log2n, intra);
+        lev[i] = (int16_t)lv;
+        L.a[i] = dequant_level(lv, qp, log2n);
+        if (lv) {
+            atomicAdd(&L.acc[2][t], level_rate_half(lv));
+            atomicOr(&L.acc[3][t], 1);
+        }
+    }
+    wsync();
+    // inverse, columns: b[t][y][x] = clip16((sum_j M[j][y] d[t][j][x] + 64) >> 7)
+    for (int i = l; i < cnt; i += 64) {
+        const int t = i >> (2 * log2n), y = (i >> log2n) & (n - 1), x = i & (n - 1);
+        int g = L.a[i];
+        if (!ts) {
+            int s = 0;
+            const int* at = L.a + t * nn + x;
+            for (int j = 0; j < n; j++) s += tx_m(T, log2n, dst, j, y) * at[j * n];
+            g = sk_clip((s + 64) >> 7, -32768, 32767);
+        }
+        L.b[i] = g;
+    }
+    wsync();
+    // inverse, rows + reconstruction
+    for (int i = l; i < cnt; i += 64) {
+        const int t = i >> (2 * log2n), y = (i >> log2n) & (n - 1), x = i & (n - 1);
+        const int base = tu_base(kind, log2n, t, sb), o = base + y * (base < 256 ? 16 : 8) + x;
+        int r;
+        if (ts) {
+            r = (L.b[i] * 128 + 2048) >> 12;
+        } else {
+            int s = 0;
+            const int* gt = L.b + t * nn + y * n;
+            for (int j = 0; j < n; j++) s += tx_m(T, log2n, dst, j, x) * gt[j];
+            r = (s + 2048) >> 12;
+        }
+        const int rv = sk_clip255((int)L.pred[o] + r);
+        rec[o] = (uint8_t)rv;
+        const int e = (int)L.src[o] - rv;
+        atomicAdd(&L.acc[1][t], e * e);
+    }
+    wsync();
+    if (l < ntu) {   // RD zeroing (code_tu_1's rule)
+        const long long s0 = L.acc[0][l], s1 = L.acc[1][l];
+        const int rate = kTuRateHalf + L.acc[2][l];
+        int nz = L.acc[3][l];
+        if (nz && 512 * s0 <= 512 * s1 + (long long)lam * rate) nz = 0;
+        tf[l] = nz;
+        tj[l] = nz ? 512 * s1 + (long long)lam * rate : 512 * s0;
+    }
+    wsync();
+    for (int i = l; i < cnt; i += 64) {   // zeroed TUs: no levels, reconstruction = prediction
+        const int t = i >> (2 * log2n);
+        if (tf[t]) continue;
+        const int base = tu_base(kind, log2n, t, sb);
+        const int o = base + ((i >> log2n) & (n - 1)) * (base < 256 ? 16 : 8) + (i & (n - 1));
+        lev[i] = 0;
+        rec[o] = L.pred[o];
+    }
+    wsync();
+}
+
+// 4x4 TUs of a batch and of its transform-skip twin: each TU keeps the skip variant when
+// it codes and costs less (code_tu's rule). Returns the per-TU skip mask.
+__device__ int merge_ts(CuLds& L, int kind, int sb, int ntu, int16_t* lev, uint8_t* rec, long long* tj, int* tf,
+                        const int16_t* levt, const uint8_t* rect, const long long* tjt, const int* tft) {
+    const int l = lane();
+    int mask = 0;
+    for (int t = 0; t < ntu; t++)
+        if (tft[t] && tjt[t] < tj[t]) mask |= 1 << t;
+    for (int i = l; i < ntu * 16; i += 64) {
+        const int t = i >> 4;
+        if (!((mask >> t) & 1)) continue;
+        lev[i] = levt[i];
+        const int base = tu_base(kind, 2, t, sb), o = base + ((i >> 2) & 3) * (base < 256 ? 16 : 8) + (i & 3);
+        rec[o] = rect[o];
+    }
+    wsync();
+    if (l < ntu && ((mask >> l) & 1)) {
+        tj[l] = tjt[l];
+        tf[l] = tft[l];
+    }
+    wsync();
+    return mask;
+}
+
+// Copies the n x n block at CU-raster index o (pitch from o) from one raster to another.
+__device__ __forceinline__ void blk_copy(uint8_t* dst, const uint8_t* src, int o, int n) {
+    const int pitch = o < 256 ? 16 : 8;
+    for (int i = lane(); i < n * n; i += 64) {
+        const int k = o + (i / n) * pitch + (i % n);
+        dst[k] = src[k];
+    }
+}
+
+// Source samples of CU (cx, cy) into L.src; a CU raster to the rec planes.
 __device__ __forceinline__ void load_src(CuLds& L, const FrameArgs& f, int cx, int cy) {
     const int l = lane();
     for (int i = l; i < kCoefPerCu; i += 64) {
@@ -170,15 +223,85 @@ __device__ __forceinline__ void load_src(CuLds& L, const FrameArgs& f, int cx, i
         L.src[i] = v;
     }
 }
-__device__ __forceinline__ void store_rec(const CuLds& L, const FrameArgs& f, int cx, int cy) {
+__device__ __forceinline__ void store_rec(const uint8_t* rec, const FrameArgs& f, int cx, int cy) {
     const int l = lane();
     for (int i = l; i < kCoefPerCu; i += 64) {
-        if (i < 256) f.rec.y[(size_t)(cy * 16 + (i >> 4)) * f.stride_y + cx * 16 + (i & 15)] = L.pred[i];
+        if (i < 256) f.rec.y[(size_t)(cy * 16 + (i >> 4)) * f.stride_y + cx * 16 + (i & 15)] = rec[i];
         else {
             const int j = i - 256, c = j >> 6, r = (j >> 3) & 7, x = j & 7;
-            (c ? f.rec.v : f.rec.u)[(size_t)(cy * 8 + r) * f.stride_c + cx * 8 + x] = L.pred[i];
+            (c ? f.rec.v : f.rec.u)[(size_t)(cy * 8 + r) * f.stride_c + cx * 8 + x] = rec[i];
         }
     }
+}
+
+// Residual of an inter CU (hevc_cpu.cpp code_inter_residual; prediction in L.pred): all
+// trees coded in parallel batches, then the RD choice. Levels to gcoef, the TU fields into
+// cu; returns the raster holding the chosen reconstruction.
+__device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int16_t* gcoef, CuInfo& cu) {
+    const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
+    tu_batch(L, T, 0, 0, 4, 1, false, false, qp, false, lam, L.levA, L.recA, L.tj[0], L.tf[0]);
+    tu_batch(L, T, 1, 0, 3, 2, false, false, qpc, false, lam, L.levA + kCoefCb, L.recA, L.tj[0] + 1, L.tf[0] + 1);
+    tu_batch(L, T, 0, 0, 3, 4, false, false, qp, false, lam, L.lev8, L.recS, L.tj[1], L.tf[1]);
+    tu_batch(L, T, 0, 0, 2, 16, false, false, qp, false, lam, L.lev4, L.rec4, L.tj[2], L.tf[2]);
+    tu_batch(L, T, 0, 0, 2, 16, false, true, qp, false, lam, L.lev4t, L.rec4t, L.tj[3], L.tf[3]);
+    const int tsy = merge_ts(L, 0, 0, 16, L.lev4, L.rec4, L.tj[2], L.tf[2], L.lev4t, L.rec4t, L.tj[3], L.tf[3]);
+    tu_batch(L, T, 1, 0, 2, 8, false, false, qpc, false, lam, L.levc, L.recS, L.tj[4], L.tf[4]);
+    tu_batch(L, T, 1, 0, 2, 8, false, true, qpc, false, lam, L.levct, L.rec4, L.tj[5], L.tf[5]);
+    const int tsc = merge_ts(L, 1, 0, 8, L.levc, L.recS, L.tj[4], L.tf[4], L.levct, L.rec4, L.tj[5], L.tf[5]);
+    // the decision (every lane, from LDS)
+    const long long ja = L.tj[0][0] + L.tj[0][1] + L.tj[0][2];
+    const int cbfa = L.tf[0][0] | (L.tf[0][1] << 1) | (L.tf[0][2] << 2);
+    long long js = (long long)lam * kSplitRateHalf;
+    int tuc = 0, split8 = 0, c8 = 0, c4 = 0, ly = 0;
+    for (int t = 0; t < 8; t++) {
+        js += L.tj[4][t];
+        tuc |= L.tf[4][t] << t;
+    }
+    for (int q = 0; q < 4; q++) {
+        const long long j8 = L.tj[1][q];
+        long long j4 = (long long)lam * kSplit8RateHalf;
+        for (int j = 0; j < 4; j++) {
+            j4 += L.tj[2][4 * q + j];
+            c4 |= L.tf[2][4 * q + j] << (4 * q + j);
+        }
+        c8 |= L.tf[1][q] << q;
+        if (j4 < j8) split8 |= 1 << q;
+        js += j4 < j8 ? j4 : j8;
+        ly |= (j4 < j8) ? (c4 >> (4 * q)) & 15 : (c8 >> q) & 1;
+    }
+    if (js < ja && (ly | tuc)) {
+        for (int i = l; i < 256; i += 64) {
+            const int q = i >> 6;
+            gcoef[i] = ((split8 >> q) & 1) ? L.lev4[i] : L.lev8[i];
+            if ((split8 >> q) & 1) {   // node reconstruction from the 4x4 trees
+                const int o = (8 * (q >> 1) + ((i >> 3) & 7)) * 16 + 8 * (q & 1) + (i & 7);
+                L.recS[o] = L.rec4[o];
+            }
+        }
+        for (int i = l; i < 128; i += 64) gcoef[kCoefCb + i] = L.levc[i];
+        cu.tu = (uint8_t)(16 | split8);
+        cu.tuc = (uint8_t)tuc;
+        uint16_t m = 0;
+        for (int q = 0; q < 4; q++)
+            m |= (uint16_t)((((split8 >> q) & 1) ? (c4 >> (4 * q)) & 15 : (((c8 >> q) & 1) ? 15 : 0)) << (4 * q));
+        uint16_t u4 = 0;
+        for (int q = 0; q < 4; q++)
+            if ((split8 >> q) & 1) u4 |= (uint16_t)(15 << (4 * q));
+        cu.ycbf = m;
+        cu.cbf = (uint8_t)((m ? 1 : 0) | ((tuc & 15) ? 2 : 0) | ((tuc >> 4) ? 4 : 0));
+        cu.tsy = (uint16_t)(tsy & m & u4);
+        cu.tsc = (uint8_t)(tsc & tuc);
+        wsync();
+        return L.recS;
+    }
+    for (int i = l; i < kCoefPerCu; i += 64) gcoef[i] = L.levA[i];
+    cu.cbf = (uint8_t)cbfa;
+    cu.tu = cu.tuc = 0;
+    cu.ycbf = (cbfa & 1) ? 0xffff : 0;
+    cu.tsy = 0;
+    cu.tsc = 0;
+    wsync();
+    return L.recA;
 }
 
 // ---------------------------------------------------------------------------
@@ -229,10 +352,11 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     {   // luma MC (hevc_core.h luma_mc_sample, separable form): the 23x23 integer window
         // into LDS (L.a as bytes, row pitch 24), horizontal 8-tap pass into L.b (23 rows x
         // 16), vertical pass into pred (lane = row l >> 2, 4 columns). L.a / L.b are free
-        // until code_cu_wave.
+        // until the residual batches.
         const int fx = mvx & 3, fy = mvy & 3;
         const int x0 = cx * 16 + (mvx >> 2) - 3, y0 = cy * 16 + (mvy >> 2) - 3;
         uint8_t* win = reinterpret_cast<uint8_t*>(L.a);
+        int* hb = reinterpret_cast<int*>(L.lev8);   // 23 x 16 ints: L.lev8 .. L.lev4t are free too
         for (int i = l; i < 23 * 23; i += 64) {
             const int r = i / 23, c = i - r * 23;
             win[r * 24 + c] = f.ref.y[(size_t)sk_clip(y0 + r, 0, pic_h - 1) * f.stride_y + sk_clip(x0 + c, 0, pic_w - 1)];
@@ -246,18 +370,18 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
 #pragma unroll
                 for (int k = 0; k < 8; k++) s += HEVC_LUMA_FILTER[fx][k] * (int)w[k];
             }
-            L.b[i] = s;
+            hb[i] = s;
         }
         wsync();
         const int y = l >> 2;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int x = 4 * (l & 3) + k;
-            int v = L.b[(y + 3) * 16 + x];
+            int v = hb[(y + 3) * 16 + x];
             if (fy) {
                 v = 0;
 #pragma unroll
-                for (int j = 0; j < 8; j++) v += HEVC_LUMA_FILTER[fy][j] * L.b[(y + j) * 16 + x];
+                for (int j = 0; j < 8; j++) v += HEVC_LUMA_FILTER[fy][j] * hb[(y + j) * 16 + x];
                 v >>= 6;
             }
             L.pred[y * 16 + x] = (uint8_t)sk_clip255((v + 32) >> 6);
@@ -273,20 +397,19 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
         }
     }
     wsync();
-    const int cbf = code_cu_wave(L, T, t.qp, false, A.coefs + (size_t)idx * kCoefPerCu);
-    store_rec(L, f, cx, cy);
+    CuInfo cu;
+    memset(&cu, 0, sizeof(cu));
+    const uint8_t* rec = inter_residual(L, T, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu);
+    store_rec(rec, f, cx, cy);
     if (l == 0) {
-        CuInfo cu;
-        memset(&cu, 0, sizeof(cu));
         int midx = -1;
         for (int i = 0; i < kMaxMergeCand && midx < 0; i++)
             if (mlx[i] == mvx && mly[i] == mvy) midx = i;
-        cu.cbf = (uint8_t)cbf;
         cu.qp = (uint8_t)t.qp;
         cu.mvx = (int16_t)mvx;
         cu.mvy = (int16_t)mvy;
         if (midx >= 0) {
-            cu.mode = cbf ? CU_MERGE : CU_SKIP;
+            cu.mode = cu.cbf ? CU_MERGE : CU_SKIP;
             cu.merge_idx = (uint8_t)midx;
         } else {
             cu.mode = CU_AMVP;
@@ -302,135 +425,87 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// Intra reference samples (8.4.4.2.2, substitution in closed form for CTB = CU: the
-// bottom-left half is never available) of an n x n block at (x0, y0): linear layout
-// of build_intra_ref. Every lane writes the entries i = lane, lane + 64.
-__device__ __forceinline__ void fill_ref(const uint8_t* P, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
-                         uint8_t* ref) {
-    const int len = 4 * n + 1;
-    for (int i = lane(); i < len; i += 64) {
-        int v;
-        if (!left && !top) {
-            v = 128;
-        } else if (i < 2 * n) {
-            const int y = 2 * n - 1 - i;
-            v = left ? P[(size_t)(y0 + sk_min(y, n - 1)) * stride + x0 - 1] : P[(size_t)(y0 - 1) * stride + x0];
+// Intra reference samples (8.4.4.2.2) of the n x n TU of component c at (x0, y0) in
+// CU-relative component coordinates (n <= 16), availability av (AV_* bits): samples
+// inside the CU from the CU raster W (nullptr: everything from the plane P, whose CU
+// origin is (px0, py0)), substitution in closed form by ballot. Lane i: entry i (entry
+// 64 of a 16x16 TU: lane 0's second one).
+__device__ void tu_refs(const uint8_t* W, const uint8_t* P, int stride, int px0, int py0, int c, int x0, int y0,
+                        int n, int av, uint8_t* out) {
+    const int l = lane(), len = 4 * n + 1, cn = c ? 8 : 16, wb = c == 0 ? 0 : (c == 1 ? kCoefCb : kCoefCr);
+    auto fetch = [&](int i, bool& ok) {
+        int x, y, bit;
+        if (i < 2 * n) {
+            const int yy = 2 * n - 1 - i;
+            x = x0 - 1;
+            y = y0 + yy;
+            bit = yy < n ? AV_L : AV_BL;
         } else if (i == 2 * n) {
-            v = (left && top) ? P[(size_t)(y0 - 1) * stride + x0 - 1]
-                              : (left ? P[(size_t)y0 * stride + x0 - 1] : P[(size_t)(y0 - 1) * stride + x0]);
+            x = x0 - 1;
+            y = y0 - 1;
+            bit = AV_TL;
         } else {
-            const int x = i - 2 * n - 1;
-            if (x < n) v = top ? P[(size_t)(y0 - 1) * stride + x0 + x] : P[(size_t)y0 * stride + x0 - 1];
-            else v = tr ? P[(size_t)(y0 - 1) * stride + x0 + x]
-                        : (top ? P[(size_t)(y0 - 1) * stride + x0 + n - 1] : P[(size_t)y0 * stride + x0 - 1]);
+            const int xx = i - 2 * n - 1;
+            x = x0 + xx;
+            y = y0 - 1;
+            bit = xx < n ? AV_T : AV_TR;
         }
-        ref[i] = (uint8_t)v;
+        ok = (av & bit) != 0;
+        if (!ok) return 0;
+        if (W && x >= 0 && y >= 0 && x < cn && y < cn) return (int)W[wb + y * cn + x];
+        return (int)P[(size_t)(py0 + y) * stride + px0 + x];
+    };
+    bool ok = false;
+    const int v = l < len ? fetch(l, ok) : 0;
+    const uint64_t M = __ballot(ok);
+    int src = l;
+    if (!ok) {
+        const uint64_t below = l ? (M & ((1ull << l) - 1)) : 0ull;
+        src = below ? 63 - __builtin_clzll(below) : (M ? __builtin_ctzll(M) : l);
     }
+    int r = __shfl(v, src);
+    if (!M) r = 128;
+    if (l < len) out[l] = (uint8_t)r;
+    if (len > 64) {   // entry 64 (top-right end of a 16x16 TU)
+        bool ok64 = false;
+        const int v64 = fetch(64, ok64);
+        const int r63 = __shfl(r, 63);
+        if (l == 0) out[64] = (uint8_t)(ok64 ? v64 : r63);
+    }
+    wsync();
 }
-__device__ __forceinline__ void filter_ref(const uint8_t* r, int n, uint8_t* out) {
+// [1 2 1] filtering of the references (8.4.4.2.3), n <= 16.
+__device__ __forceinline__ void ref_filter(const uint8_t* r, int n, uint8_t* out) {
     const int len = 4 * n + 1;
     for (int i = lane(); i < len; i += 64)
         out[i] = (i == 0 || i == len - 1) ? r[i] : (uint8_t)((r[i - 1] + 2 * r[i] + r[i + 1] + 2) >> 2);
-}
-// Prediction sample for the encoder's modes (planar 0, DC 1, horizontal 10, vertical 26),
-// identical to intra_pred_sample for them. dc: the block's DC value.
-__device__ __forceinline__ int pred_fast(const uint8_t* r, int n, int log2n, int mode, bool luma, int dc, int x,
-                                         int y) {
-    auto Lf = [&](int yy) { return (int)r[2 * n - 1 - yy]; };
-    auto Tf = [&](int xx) { return (int)r[2 * n + 1 + xx]; };
-    if (mode == 0)
-        return ((n - 1 - x) * Lf(y) + (x + 1) * Tf(n) + (n - 1 - y) * Tf(x) + (y + 1) * Lf(n) + n) >> (log2n + 1);
-    if (mode == 1) {
-        if (luma) {
-            if (x == 0 && y == 0) return (Lf(0) + 2 * dc + Tf(0) + 2) >> 2;
-            if (y == 0) return (Tf(x) + 3 * dc + 2) >> 2;
-            if (x == 0) return (Lf(y) + 3 * dc + 2) >> 2;
-        }
-        return dc;
-    }
-    if (mode == 26) return (luma && x == 0) ? sk_clip255(Tf(0) + ((Lf(y) - Lf(-1)) >> 1)) : Tf(x);
-    return (luma && y == 0) ? sk_clip255(Lf(0) + ((Tf(x) - Tf(-1)) >> 1)) : Lf(y);
-}
-// DC value of an n x n block: (sum of n top + n left references + n) >> (log2n + 1).
-__device__ __forceinline__ int dc_value(const uint8_t* r, int n, int log2n) {
-    const int l = lane();
-    int v = 0;
-    if (l < n) v = r[2 * n + 1 + l];               // top
-    else if (l < 2 * n) v = r[2 * n - 1 - (l - n)];   // left
-    return (wsum(v) + n) >> (log2n + 1);
-}
-// Main reference array of a directional mode (8.4.4.2.6) for an n x n block from the
-// linear reference r: out[k + n] = ref[k], k = -n .. 2n (lane = k + n), with the other side
-// projected through invAngle for negative angles (entries no sample reads stay 0).
-__device__ __forceinline__ void build_refm(const uint8_t* r, int n, int mode, uint8_t* out) {
-    const int k = lane() - n;
-    if (k > 2 * n) return;
-    const int angle = HEVC_INTRA_ANGLE[mode];
-    const bool vert = mode >= 18;
-    int v = 0;
-    if (k >= 0) {
-        v = vert ? r[2 * n + k] : r[2 * n - k];   // p[k-1][-1] / p[-1][k-1]
-    } else if (angle < 0) {
-        const int last = (n * angle) >> 5;
-        if (last < -1 && k >= last) {
-            const int j = (k * intra_inv_angle(mode) + 128) >> 8;
-            v = vert ? r[2 * n - j] : r[2 * n + j];
-        }
-    }
-    out[k + n] = (uint8_t)v;
-}
-// Directional prediction sample (x, y) from build_refm's array (intra_pred_sample's
-// angular branch; the axis modes 10 / 26 go through pred_fast).
-__device__ __forceinline__ int pred_angular(const uint8_t* refm, int n, int mode, int x, int y) {
-    const int angle = HEVC_INTRA_ANGLE[mode];
-    const bool vert = mode >= 18;
-    const int a = vert ? y : x, b = vert ? x : y;
-    const int idx = ((a + 1) * angle) >> 5, fact = ((a + 1) * angle) & 31;
-    const uint8_t* p = refm + n + b + idx + 1;
-    return fact ? ((32 - fact) * (int)p[0] + fact * (int)p[1] + 16) >> 5 : (int)p[0];
-}
-// Luma references of `mode` for a 16x16 CU: the [1 2 1]-filtered copy when filterFlag.
-__device__ __forceinline__ const uint8_t* luma_ref(const CuLds& L, int mode) {
-    return intra_filter_flag(mode, 4, 0) ? L.ref + 65 : L.ref;
-}
-// Intra prediction of the whole CU into L.pred for `mode` (refs in L.ref).
-__device__ __forceinline__ void intra_pred_cu(CuLds& L, int mode) {
-    const int l = lane();
-    const uint8_t* ry = luma_ref(L, mode);
-    const bool basic = intra_mode_basic(mode);
-    const int dcy = dc_value(L.ref, 16, 4);
-    const int dcu = dc_value(L.ref + 130, 8, 3), dcv = dc_value(L.ref + 163, 8, 3);
-    if (!basic) {
-        build_refm(ry, 16, mode, L.refm[0]);
-        build_refm(L.ref + 130, 8, mode, L.refm[1]);
-        build_refm(L.ref + 163, 8, mode, L.refm[2]);
-        wsync();
-    }
-    for (int i = l; i < kCoefPerCu; i += 64) {
-        int v;
-        if (i < 256) {
-            v = basic ? pred_fast(ry, 16, 4, mode, true, dcy, i & 15, i >> 4)
-                      : pred_angular(L.refm[0], 16, mode, i & 15, i >> 4);
-        } else {
-            const int j = i - 256, c = j >> 6;
-            v = basic ? pred_fast(L.ref + 130 + 33 * c, 8, 3, mode, false, c ? dcv : dcu, j & 7, (j >> 3) & 7)
-                      : pred_angular(L.refm[1 + c], 8, mode, j & 7, (j >> 3) & 7);
-        }
-        L.pred[i] = (uint8_t)v;
-    }
     wsync();
 }
-__device__ __forceinline__ void intra_refs(CuLds& L, const Planes& P, const FrameArgs& f, int cx, int cy, bool left, bool top,
-                           bool tr) {
-    fill_ref(P.y, f.stride_y, cx * 16, cy * 16, 16, left, top, tr, L.ref);
-    fill_ref(P.u, f.stride_c, cx * 8, cy * 8, 8, left, top, tr, L.ref + 130);
-    fill_ref(P.v, f.stride_c, cx * 8, cy * 8, 8, left, top, tr, L.ref + 163);
+// Prediction of the n x n TU of component c at CU-raster index o into L.pred.
+__device__ __forceinline__ void tu_pred(CuLds& L, const uint8_t* ref, int c, int log2n, int mode, int o) {
+    const int n = 1 << log2n, pitch = o < 256 ? 16 : 8;
+    for (int i = lane(); i < n * n; i += 64)
+        L.pred[o + (i >> log2n) * pitch + (i & (n - 1))] =
+            (uint8_t)intra_pred_sample(ref, n, log2n, mode, c, i & (n - 1), i >> log2n);
     wsync();
-    filter_ref(L.ref, 16, L.ref + 65);
-    wsync();
+}
+// References + prediction of one intra TU (component c, n x n at CU-relative (x0, y0)).
+__device__ void intra_tu_pred(CuLds& L, const uint8_t* W, const Planes& P, const FrameArgs& f, int cx, int cy, int c,
+                              int log2n, int x0, int y0, int av, int mode) {
+    const int n = 1 << log2n, cn = c ? 8 : 16;
+    const uint8_t* plane = c == 0 ? P.y : (c == 1 ? P.u : P.v);
+    tu_refs(W, plane, c ? f.stride_c : f.stride_y, cx * cn, cy * cn, c, x0, y0, n, av, L.ref[0]);
+    const uint8_t* r = L.ref[0];
+    if (intra_filter_flag(mode, log2n, c)) {
+        ref_filter(L.ref[0], n, L.ref[1]);
+        r = L.ref[1];
+    }
+    const int o = (c == 0 ? 0 : (c == 1 ? kCoefCb : kCoefCr)) + y0 * cn + x0;
+    tu_pred(L, r, c, log2n, mode, o);
 }
 
-// Open-loop intra mode per CU of I slices (all CUs in parallel).
+// Open-loop intra mode per CU of I slices (all CUs in parallel): the mode whose sixteen
+// 4x4 predictions from their source neighbours are closest (hevc_cpu.cpp pass 0).
 __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     __shared__ CuLds Lw[4];
     const FrameArgs& f = A.f;
@@ -442,27 +517,23 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     const SliceTask t = f.tasks[cy / f.rows_per_slice];
     if (t.final_action != ACT_I) return;
     const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < f.mb_w;
-    intra_refs(L, f.src, f, cx, cy, left, top, tr);
     load_src(L, f, cx, cy);
-    wsync();
-    const int l = lane();
-    const int dc = dc_value(L.ref, 16, 4);
+    for (int u = 0; u < 16; u++) {
+        const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
+        tu_refs(nullptr, f.src.y, f.stride_y, cx * 16, cy * 16, 0, 4 * bx, 4 * by, 4, tu_avail_at(bx, by, 1, left, top, tr),
+                L.ref4[u]);
+    }
+    const int l = lane(), u = l >> 2, row = l & 3;
+    const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
     int best = 1, best_sad = 0x7fffffff;
-    for (int k = 0; k < 35; k++) {   // HEVC_INTRA_ORDER, SAD + intra_mode_bias (hevc_cpu.cpp)
+    for (int k = 0; k < 35; k++) {   // HEVC_INTRA_ORDER, SAD + intra_mode_bias
         const int m = HEVC_INTRA_ORDER[k];
-        const uint8_t* r = luma_ref(L, m);
-        const bool basic = intra_mode_basic(m);
-        if (!basic) {
-            build_refm(r, 16, m, L.refm[0]);
-            wsync();
-        }
         int sad = 0;
-        for (int i = l; i < 256; i += 64)
-            sad += sk_abs((int)L.src[i] - (basic ? pred_fast(r, 16, 4, m, true, dc, i & 15, i >> 4)
-                                                 : pred_angular(L.refm[0], 16, m, i & 15, i >> 4)));
+#pragma unroll
+        for (int x = 0; x < 4; x++)
+            sad += sk_abs((int)L.src[(4 * by + row) * 16 + 4 * bx + x] - intra_pred_sample(L.ref4[u], 4, 2, m, 0, x, row));
         sad = wsum(sad) + intra_mode_bias(m, t.qp);
         if (sad < best_sad) { best_sad = sad; best = m; }
-        wsync();   // refm is rebuilt by the next mode
     }
     if (l == 0) {
         CuInfo cu;
@@ -471,6 +542,90 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
         cu.intra_mode = (uint8_t)best;
         A.cus[idx] = cu;
     }
+}
+
+// One intra CU (hevc_cpu.cpp code_slice_intra pass 1): the 16x16 TU against the split
+// tree, each 8x8 node's TU against its four 4x4 TUs (transform skip tried), every TU
+// predicted from the reconstruction before it. The committed split reconstruction lives
+// in L.recS. Levels to gcoef, fields into cu; returns the chosen reconstruction.
+__device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f, int cx, int cy, bool left, bool top,
+                                   bool tr, int mode, int qp, int16_t* gcoef, CuInfo& cu) {
+    const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
+    const Planes& P = f.rec;
+    // (a) one 16x16 TU
+    const int avc = cu_avail(left, top, tr);
+    intra_tu_pred(L, nullptr, P, f, cx, cy, 0, 4, 0, 0, avc, mode);
+    intra_tu_pred(L, nullptr, P, f, cx, cy, 1, 3, 0, 0, avc, mode);
+    intra_tu_pred(L, nullptr, P, f, cx, cy, 2, 3, 0, 0, avc, mode);
+    tu_batch(L, T, 0, 0, 4, 1, false, false, qp, true, lam, L.levA, L.recA, L.tj[0], L.tf[0]);
+    tu_batch(L, T, 1, 0, 3, 2, false, false, qpc, true, lam, L.levA + kCoefCb, L.recA, L.tj[0] + 1, L.tf[0] + 1);
+    // (b) four nodes, reconstruction committed into W = L.recS
+    uint8_t* W = L.recS;
+    long long jb = (long long)lam * kSplitRateHalf;
+    int split8 = 0, c8 = 0, c4 = 0, tuc = 0, tsy = 0, tsc = 0;
+    for (int q = 0; q < 4; q++) {
+        const int av = tu_avail(q, left, top, tr), ox = 8 * (q & 1), oy = 8 * (q >> 1), o8 = oy * 16 + ox;
+        intra_tu_pred(L, W, P, f, cx, cy, 0, 3, ox, oy, av, mode);
+        tu_batch(L, T, 2, o8, 3, 1, false, false, qp, true, lam, L.lev8 + 64 * q, L.rec4t, L.tj[1] + q, L.tf[1] + q);
+        long long j4 = (long long)lam * kSplit8RateHalf;
+        for (int j = 0; j < 4; j++) {
+            const int bx = 2 * (q & 1) + (j & 1), by = 2 * (q >> 1) + (j >> 1), t4 = 4 * q + j, o4 = 4 * by * 16 + 4 * bx;
+            intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, left, top, tr), mode);
+            tu_batch(L, T, 2, o4, 2, 1, true, false, qp, true, lam, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4);
+            tu_batch(L, T, 2, o4, 2, 1, true, true, qp, true, lam, L.lev4t + 16 * t4, L.rec4, L.tj[3] + t4, L.tf[3] + t4);
+            const int m = merge_ts(L, 2, o4, 1, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4, L.lev4t + 16 * t4, L.rec4,
+                                   L.tj[3] + t4, L.tf[3] + t4);
+            tsy |= m << t4;
+            j4 += L.tj[2][t4];
+            c4 |= L.tf[2][t4] << t4;
+        }
+        const long long j8 = L.tj[1][q];
+        c8 |= L.tf[1][q] << q;
+        if (j4 < j8) {
+            split8 |= 1 << q;
+            jb += j4;
+        } else {
+            blk_copy(W, L.rec4t, o8, 8);
+            tsy &= ~(15 << (4 * q));
+            jb += j8;
+            wsync();
+        }
+        for (int c = 1; c < 3; c++) {
+            const int t = q + 4 * (c - 1), oc = (c == 1 ? kCoefCb : kCoefCr) + (oy / 2) * 8 + ox / 2;
+            intra_tu_pred(L, W, P, f, cx, cy, c, 2, ox / 2, oy / 2, av, mode);
+            tu_batch(L, T, 2, oc, 2, 1, false, false, qpc, true, lam, L.levc + 16 * t, W, L.tj[4] + t, L.tf[4] + t);
+            tu_batch(L, T, 2, oc, 2, 1, false, true, qpc, true, lam, L.levct + 16 * t, L.rec4, L.tj[5] + t, L.tf[5] + t);
+            tsc |= merge_ts(L, 2, oc, 1, L.levc + 16 * t, W, L.tj[4] + t, L.tf[4] + t, L.levct + 16 * t, L.rec4,
+                            L.tj[5] + t, L.tf[5] + t) << t;
+            jb += L.tj[4][t];
+            tuc |= L.tf[4][t] << t;
+        }
+    }
+    const long long ja = L.tj[0][0] + L.tj[0][1] + L.tj[0][2];
+    if (jb < ja) {
+        for (int i = l; i < 256; i += 64) gcoef[i] = ((split8 >> (i >> 6)) & 1) ? L.lev4[i] : L.lev8[i];
+        for (int i = l; i < 128; i += 64) gcoef[kCoefCb + i] = L.levc[i];
+        cu.tu = (uint8_t)(16 | split8);
+        cu.tuc = (uint8_t)tuc;
+        uint16_t m = 0;
+        for (int q = 0; q < 4; q++)
+            m |= (uint16_t)((((split8 >> q) & 1) ? (c4 >> (4 * q)) & 15 : (((c8 >> q) & 1) ? 15 : 0)) << (4 * q));
+        cu.ycbf = m;
+        cu.cbf = (uint8_t)((m ? 1 : 0) | ((tuc & 15) ? 2 : 0) | ((tuc >> 4) ? 4 : 0));
+        cu.tsy = (uint16_t)tsy;
+        cu.tsc = (uint8_t)tsc;
+        wsync();
+        return W;
+    }
+    const int cbfa = L.tf[0][0] | (L.tf[0][1] << 1) | (L.tf[0][2] << 2);
+    for (int i = l; i < kCoefPerCu; i += 64) gcoef[i] = L.levA[i];
+    cu.tu = cu.tuc = 0;
+    cu.cbf = (uint8_t)cbfa;
+    cu.ycbf = (cbfa & 1) ? 0xffff : 0;
+    cu.tsy = 0;
+    cu.tsc = 0;
+    wsync();
+    return L.recA;
 }
 
 // I slices: one workgroup per slice, wave w = CTB row w of the slice, CTB x coded at
@@ -495,17 +650,15 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
             const int idx = cy * f.mb_w + cx;
             const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < f.mb_w;
             const int mode = __builtin_amdgcn_readfirstlane(A.cus[idx].intra_mode);
-            intra_refs(L, f.rec, f, cx, cy, left, top, tr);
             load_src(L, f, cx, cy);
-            intra_pred_cu(L, mode);
-            const int cbf = code_cu_wave(L, T, t.qp, true, A.coefs + (size_t)idx * kCoefPerCu);
-            store_rec(L, f, cx, cy);
+            wsync();
+            CuInfo cu;
+            memset(&cu, 0, sizeof(cu));
+            const uint8_t* rec = intra_cu(L, T, f, cx, cy, left, top, tr, mode, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu);
+            store_rec(rec, f, cx, cy);
             if (l == 0) {
-                CuInfo cu;
-                memset(&cu, 0, sizeof(cu));
                 cu.mode = CU_INTRA;
                 cu.intra_mode = (uint8_t)mode;
-                cu.cbf = (uint8_t)cbf;
                 cu.qp = (uint8_t)t.qp;
                 A.cus[idx] = cu;
                 f.me[idx].mvx = 0;

@@ -130,3 +130,41 @@ def test_hevc_directional_intra_modes():
     assert np.count_nonzero(~np.isin(modes, [0, 1, 10, 26])) > len(modes) // 2
     assert len(pk.data) < 7000, len(pk.data)
     assert psnr(Y, _luma(f)) > 45
+
+
+def _cus(enc):
+    c = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 24)
+    tu = c[:, 6]
+    tsy = c[:, 18].astype(np.int64) | (c[:, 19].astype(np.int64) << 8)
+    return c[:, 0], tu, tsy, c[:, 20]
+
+
+def test_hevc_transform_tree_tools():
+    """Residual quadtree (hevc_core.h code_cu, max_transform_hierarchy_depth 2): on text-like
+    content the RD choices use 16x16, 8x8 and 4x4 TUs (DST for intra 4x4 luma), transform
+    skip on 4x4 luma and chroma, in I and P pictures, and the decoder's Y, Cb and Cr equal
+    the encoder's reconstruction (inner TU edges deblocked on both sides alike)."""
+    W, H = 256, 144
+    src = SyntheticDesktop(W, H, kind="motion")
+    enc = HevcEncoder(W, H, backend="cpu", qp=27)
+    dec = HevcDecoder()
+    cw = (W + 1) // 2
+    seen = {"split": 0, "whole": 0, "split8": 0, "ts": 0, "inter_split": 0}
+    for t in range(3):
+        pk = enc.encode(src.frame(t), t)[0]
+        Y, U, V = dec.decode(pk.data[10:])[0]
+        assert np.array_equal(Y, _rec_y(enc, W, H))
+        pcw = (W + 15) // 16 * 8
+        for name, P in (("ref_u", U), ("ref_v", V)):
+            rec = np.frombuffer(enc.debug_buffer(name, np.uint8), np.uint8).reshape(-1, pcw)[:(H + 1) // 2, :cw]
+            assert np.array_equal(P, rec), name
+        mode, tu, tsy, tsc = _cus(enc)
+        split = (tu & 16) != 0
+        seen["split"] += int(split.sum())
+        seen["whole"] += int((~split & (mode != 0)).sum())
+        seen["split8"] += int(((tu & 15) != 0).sum())
+        seen["ts"] += int(((tsy != 0) | (tsc != 0)).sum())
+        if t:
+            seen["inter_split"] += int((split & (mode != 3)).sum())
+    assert all(v > 0 for v in seen.values()), seen
+    enc.close()
