@@ -51,7 +51,7 @@ struct CuLds {
     uint8_t rec4t[kCoefPerCu];   // 4x4 luma TUs with transform skip | intra: the node's 8x8 trial
     int32_t a[256], b[256];      // batch intermediates (compact, TU-major)
     int16_t levA[kCoefPerCu], lev8[256], lev4[256], lev4t[256], levc[128], levct[128];
-    int acc[4][16];              // per-TU sums of a batch: SSE of the prediction, of the reconstruction, rate, non-zero
+    int acc[4][32];              // per-TU sums of a batch (twin: + 16): SSE of the prediction, of the reconstruction, rate, non-zero
     long long tj[6][16];         // per-TU RD cost: 0 Y16 Cb8 Cr8, 1 Y8, 2 Y4, 3 Y4 transform skip, 4 C4, 5 C4 skip
     int tf[6][16];               // per-TU cbf, same slots
     uint8_t ref[2][68];          // intra: the TU's reference samples (raw, [1 2 1]-filtered)
@@ -69,9 +69,11 @@ __device__ __forceinline__ int tx_m(const int8_t* T, int log2n, bool dst, int k,
 
 // TU t of a batch: CU-raster index of its top-left sample (the pitch follows: 16 in the
 // luma part, 8 in the chroma part). kind 0: luma TUs of size n in z order; 1: chroma
-// TUs, the Cb ones then the Cr ones; 2: the single TU at sb.
+// TUs, the Cb ones then the Cr ones; 2: the single TU at sb; 3: the Cb TU at sb and the
+// Cr TU at the same place (sb + 64).
 __device__ __forceinline__ int tu_base(int kind, int log2n, int t, int sb) {
     if (kind == 2) return sb;
+    if (kind == 3) return sb + 64 * t;
     const int n = 1 << log2n;
     if (kind == 0) {
         const int bx = (t & 1) | ((t >> 1) & 2), by = ((t >> 1) & 1) | ((t >> 2) & 2);
@@ -85,20 +87,26 @@ __device__ __forceinline__ int tu_base(int kind, int log2n, int t, int sb) {
 // (forward transform / DST / transform skip, quantisation, reconstruction, RD zeroing):
 // levels (compact, TU-major, raster inside the TU) into lev, the reconstruction into the
 // CU raster rec, per-TU RD cost and cbf into tj / tf. Items = samples, lane-strided.
+// With a twin (4x4 TUs, 2 * ntu * 16 <= 256): every TU also coded with transform skip
+// into levt / rect / tjt / tft in the same passes.
 __device__ void tu_batch(CuLds& L, const int8_t* T, int kind, int sb, int log2n, int ntu, bool dst, bool ts, int qp,
-                         bool intra, int lam, int16_t* lev, uint8_t* rec, long long* tj, int* tf) {
+                         bool intra, int lam, int16_t* lev, uint8_t* rec, long long* tj, int* tf, int16_t* levt = nullptr,
+                         uint8_t* rect = nullptr, long long* tjt = nullptr, int* tft = nullptr) {
     const int l = lane(), n = 1 << log2n, nn = n * n, cnt = ntu * nn;
+    const bool twin = levt != nullptr;
+    const int all = twin ? 2 * cnt : cnt;
     const int sh1 = log2n - 1, sh2 = log2n + 6;
-    if (l < 16) L.acc[0][l] = L.acc[1][l] = L.acc[2][l] = L.acc[3][l] = 0;
+    if (l < 32) L.acc[0][l] = L.acc[1][l] = L.acc[2][l] = L.acc[3][l] = 0;
     wsync();
     // forward, rows: b[t][y][u] = sum_k M[u][k] res[t][y][k] (transform skip: res << 5)
-    for (int i = l; i < cnt; i += 64) {
-        const int t = i >> (2 * log2n), y = (i >> log2n) & (n - 1), u = i & (n - 1);
+    for (int i = l; i < all; i += 64) {
+        const int var = i >= cnt, ii = i - var * cnt;
+        const int t = ii >> (2 * log2n), y = (ii >> log2n) & (n - 1), u = ii & (n - 1);
         const int base = tu_base(kind, log2n, t, sb), o = base + y * (base < 256 ? 16 : 8);
         const int e = (int)L.src[o + u] - (int)L.pred[o + u];
-        atomicAdd(&L.acc[0][t], e * e);
+        atomicAdd(&L.acc[0][t + 16 * var], e * e);
         int v = e * 32;
-        if (!ts) {
+        if (!(ts || var)) {
             int s = 0;
             for (int k = 0; k < n; k++) s += tx_m(T, log2n, dst, u, k) * ((int)L.src[o + k] - (int)L.pred[o + k]);
             v = (s + (1 << (sh1 - 1))) >> sh1;
@@ -107,29 +115,31 @@ __device__ void tu_batch(CuLds& L, const int8_t* T, int kind, int sb, int log2n,
     }
     wsync();
     // forward, columns + quantisation + dequantisation
-    for (int i = l; i < cnt; i += 64) {
-        const int t = i >> (2 * log2n), v = (i >> log2n) & (n - 1), u = i & (n - 1);
+    for (int i = l; i < all; i += 64) {
+        const int var = i >= cnt, ii = i - var * cnt;
+        const int t = ii >> (2 * log2n), v = (ii >> log2n) & (n - 1), u = ii & (n - 1);
         int c = L.b[i];
-        if (!ts) {
+        if (!(ts || var)) {
             int s = 0;
             const int* bt = L.b + t * nn + u;
             for (int k = 0; k < n; k++) s += tx_m(T, log2n, dst, v, k) * bt[k * n];
             c = (s + (1 << (sh2 - 1))) >> sh2;
         }
         const int lv = quant_level(c, qp, log2n, intra);
-        lev[i] = (int16_t)lv;
+        (var ? levt : lev)[ii] = (int16_t)lv;
         L.a[i] = dequant_level(lv, qp, log2n);
         if (lv) {
-            atomicAdd(&L.acc[2][t], level_rate_half(lv));
-            atomicOr(&L.acc[3][t], 1);
+            atomicAdd(&L.acc[2][t + 16 * var], level_rate_half(lv));
+            atomicOr(&L.acc[3][t + 16 * var], 1);
         }
     }
     wsync();
     // inverse, columns: b[t][y][x] = clip16((sum_j M[j][y] d[t][j][x] + 64) >> 7)
-    for (int i = l; i < cnt; i += 64) {
-        const int t = i >> (2 * log2n), y = (i >> log2n) & (n - 1), x = i & (n - 1);
+    for (int i = l; i < all; i += 64) {
+        const int var = i >= cnt, ii = i - var * cnt;
+        const int t = ii >> (2 * log2n), y = (ii >> log2n) & (n - 1), x = ii & (n - 1);
         int g = L.a[i];
-        if (!ts) {
+        if (!(ts || var)) {
             int s = 0;
             const int* at = L.a + t * nn + x;
             for (int j = 0; j < n; j++) s += tx_m(T, log2n, dst, j, y) * at[j * n];
@@ -139,11 +149,12 @@ __device__ void tu_batch(CuLds& L, const int8_t* T, int kind, int sb, int log2n,
     }
     wsync();
     // inverse, rows + reconstruction
-    for (int i = l; i < cnt; i += 64) {
-        const int t = i >> (2 * log2n), y = (i >> log2n) & (n - 1), x = i & (n - 1);
+    for (int i = l; i < all; i += 64) {
+        const int var = i >= cnt, ii = i - var * cnt;
+        const int t = ii >> (2 * log2n), y = (ii >> log2n) & (n - 1), x = ii & (n - 1);
         const int base = tu_base(kind, log2n, t, sb), o = base + y * (base < 256 ? 16 : 8) + x;
         int r;
-        if (ts) {
+        if (ts || var) {
             r = (L.b[i] * 128 + 2048) >> 12;
         } else {
             int s = 0;
@@ -152,27 +163,29 @@ __device__ void tu_batch(CuLds& L, const int8_t* T, int kind, int sb, int log2n,
             r = (s + 2048) >> 12;
         }
         const int rv = sk_clip255((int)L.pred[o] + r);
-        rec[o] = (uint8_t)rv;
+        (var ? rect : rec)[o] = (uint8_t)rv;
         const int e = (int)L.src[o] - rv;
-        atomicAdd(&L.acc[1][t], e * e);
+        atomicAdd(&L.acc[1][t + 16 * var], e * e);
     }
     wsync();
-    if (l < ntu) {   // RD zeroing (code_tu_1's rule)
-        const long long s0 = L.acc[0][l], s1 = L.acc[1][l];
-        const int rate = kTuRateHalf + L.acc[2][l];
-        int nz = L.acc[3][l];
+    if (l < (twin ? 2 : 1) * ntu) {   // RD zeroing (code_tu_1's rule)
+        const int var = l >= ntu, t = l - var * ntu, k = t + 16 * var;
+        const long long s0 = L.acc[0][k], s1 = L.acc[1][k];
+        const int rate = kTuRateHalf + L.acc[2][k];
+        int nz = L.acc[3][k];
         if (nz && 512 * s0 <= 512 * s1 + (long long)lam * rate) nz = 0;
-        tf[l] = nz;
-        tj[l] = nz ? 512 * s1 + (long long)lam * rate : 512 * s0;
+        (var ? tft : tf)[t] = nz;
+        (var ? tjt : tj)[t] = nz ? 512 * s1 + (long long)lam * rate : 512 * s0;
     }
     wsync();
-    for (int i = l; i < cnt; i += 64) {   // zeroed TUs: no levels, reconstruction = prediction
-        const int t = i >> (2 * log2n);
-        if (tf[t]) continue;
+    for (int i = l; i < all; i += 64) {   // zeroed TUs: no levels, reconstruction = prediction
+        const int var = i >= cnt, ii = i - var * cnt;
+        const int t = ii >> (2 * log2n);
+        if ((var ? tft : tf)[t]) continue;
         const int base = tu_base(kind, log2n, t, sb);
-        const int o = base + ((i >> log2n) & (n - 1)) * (base < 256 ? 16 : 8) + (i & (n - 1));
-        lev[i] = 0;
-        rec[o] = L.pred[o];
+        const int o = base + ((ii >> log2n) & (n - 1)) * (base < 256 ? 16 : 8) + (ii & (n - 1));
+        (var ? levt : lev)[ii] = 0;
+        (var ? rect : rec)[o] = L.pred[o];
     }
     wsync();
 }
@@ -571,8 +584,8 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
         for (int j = 0; j < 4; j++) {
             const int bx = 2 * (q & 1) + (j & 1), by = 2 * (q >> 1) + (j >> 1), t4 = 4 * q + j, o4 = 4 * by * 16 + 4 * bx;
             intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, left, top, tr), mode);
-            tu_batch(L, T, 2, o4, 2, 1, true, false, qp, true, lam, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4);
-            tu_batch(L, T, 2, o4, 2, 1, true, true, qp, true, lam, L.lev4t + 16 * t4, L.rec4, L.tj[3] + t4, L.tf[3] + t4);
+            tu_batch(L, T, 2, o4, 2, 1, true, false, qp, true, lam, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4,
+                     L.lev4t + 16 * t4, L.rec4, L.tj[3] + t4, L.tf[3] + t4);
             const int m = merge_ts(L, 2, o4, 1, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4, L.lev4t + 16 * t4, L.rec4,
                                    L.tj[3] + t4, L.tf[3] + t4);
             tsy |= m << t4;
@@ -590,16 +603,23 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
             jb += j8;
             wsync();
         }
-        for (int c = 1; c < 3; c++) {
-            const int t = q + 4 * (c - 1), oc = (c == 1 ? kCoefCb : kCoefCr) + (oy / 2) * 8 + ox / 2;
-            intra_tu_pred(L, W, P, f, cx, cy, c, 2, ox / 2, oy / 2, av, mode);
-            tu_batch(L, T, 2, oc, 2, 1, false, false, qpc, true, lam, L.levc + 16 * t, W, L.tj[4] + t, L.tf[4] + t);
-            tu_batch(L, T, 2, oc, 2, 1, false, true, qpc, true, lam, L.levct + 16 * t, L.rec4, L.tj[5] + t, L.tf[5] + t);
-            tsc |= merge_ts(L, 2, oc, 1, L.levc + 16 * t, W, L.tj[4] + t, L.tf[4] + t, L.levct + 16 * t, L.rec4,
-                            L.tj[5] + t, L.tf[5] + t) << t;
-            jb += L.tj[4][t];
-            tuc |= L.tf[4][t] << t;
+        // the node's Cb and Cr 4x4 TUs in one batch (slots q, q + 4)
+        const int ocb = kCoefCb + (oy / 2) * 8 + ox / 2;
+        intra_tu_pred(L, W, P, f, cx, cy, 1, 2, ox / 2, oy / 2, av, mode);
+        intra_tu_pred(L, W, P, f, cx, cy, 2, 2, ox / 2, oy / 2, av, mode);
+        int16_t* lc = L.levct + 64;   // scratch pair: Cb / Cr levels of this node (compact), copied below
+        int16_t* lct = L.levct + 96;
+        tu_batch(L, T, 3, ocb, 2, 2, false, false, qpc, true, lam, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4,
+                 L.tj[5] + 8, L.tf[5] + 8);
+        const int mc = merge_ts(L, 3, ocb, 2, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4, L.tj[5] + 8, L.tf[5] + 8);
+        for (int i = l; i < 32; i += 64) L.levc[16 * (q + 4 * (i >> 4)) + (i & 15)] = lc[i];
+        for (int c = 0; c < 2; c++) {
+            const int t = q + 4 * c;
+            tsc |= ((mc >> c) & 1) << t;
+            jb += L.tj[4][8 + c];
+            tuc |= L.tf[4][8 + c] << t;
         }
+        wsync();
     }
     const long long ja = L.tj[0][0] + L.tj[0][1] + L.tj[0][2];
     if (jb < ja) {
