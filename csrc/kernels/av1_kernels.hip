@@ -182,7 +182,8 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
     wsync();
     // forward stage 2 (rows) + quantisation, DCT levels to L.lv and IDTX levels (8 x the
     // residual, still in L.a) to L.lv2, with both squared coefficient errors per plane
-    long long dd[3] = {0, 0, 0}, di[3] = {0, 0, 0};
+    // transform type: J per plane (av1_core.h tx_rd_cost) summed over the decision planes
+    long long jd = 0, ji = 0;
     const int np = intra ? 1 : 3;   // planes in the decision
     for (int p = 0; p < 3; p++) {
         const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
@@ -190,9 +191,11 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         long long ed = 0, ei = 0;
         for (int i = l; i < sz * sz; i += 64) {
             const int k = i >> ln, lc = i & (sz - 1);
-            int64_t s = 0;
-            for (int j = 0; j < sz; j++) s += (int64_t)L.b[o + k * sz + j] * K[lc * sz + j];
-            const int32_t c = (int32_t)((s + (s >= 0 ? 4096 : 4095)) >> 13);
+            // |sum| <= |t|_2 |K|_2 < 2^31 (orthonormal Q13 rows, |t| <= 8 * 255 * sqrt(N)):
+            // the 32-bit sum equals av1_core.h fwd_transform's 64-bit one
+            int s = 0;
+            for (int j = 0; j < sz; j++) s += L.b[o + k * sz + j] * (int)K[lc * sz + j];
+            const int32_t c = (s + (s >= 0 ? 4096 : 4095)) >> 13;
             const int q = i == 0 ? qd : qa;
             const int lv = quantize(c, q, intra);
             L.lv[o + i] = (int16_t)lv;
@@ -206,19 +209,16 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
                 ei += e2 * e2;
             }
         }
-        dd[p] = wsum64(ed);
-        if (p < np) di[p] = wsum64(ei);
+        const long long dp = wsum64(ed), ip = wsum64(ei);
+        if (p < np) {
+            wsync();   // the plane's levels, for the rate estimates
+            jd += tx_rd_cost(4 * dp, rate2_wave(L.lv + o, ln), qa);
+            ji += tx_rd_cost(4 * ip, rate2_wave(L.lv2 + o, ln), qa);
+        }
     }
     wsync();
-    // transform type: J per plane (av1_core.h tx_rd_cost) summed over the decision planes
     bool idtx;
     {
-        long long jd = 0, ji = 0;
-        for (int p = 0; p < np; p++) {
-            const int ln = p ? log2n - 1 : log2n, o = base(p);
-            jd += tx_rd_cost(4 * dd[p], rate2_wave(L.lv + o, ln), qa);
-            ji += tx_rd_cost(4 * di[p], rate2_wave(L.lv2 + o, ln), qa);
-        }
         if (intra) {
             // luma keeps a level under IDTX
             int anyl = 0;
@@ -339,25 +339,45 @@ __device__ __forceinline__ void store_rec_blk(const BlkLds& L, const FrameArgs& 
     }
 }
 
-// One predicted sample (§7.11.3.4 without scaling): the 2-D separable filter evaluated
-// for a single output (its 8 intermediate rows are those of the block process).
-// (px, py): sample position in the plane; mv in 1/8 luma pel; ss: chroma shift;
+// Motion-compensated prediction of an n x n block (§7.11.3.4 without scaling), separably
+// through LDS (every sample of the block shares the filter phases): the (n + 7)^2 reference
+// window into win (bytes), the horizontal pass into h (ints, (n + 7) rows x n), the vertical
+// pass into out (pitch n): h = (sum_tt tap * ref + 4) >> 3, out = clip((sum_rr tap * h + 1024)
+// >> 11). P: plane; (px0, py0): the block in the plane; mv in 1/8 luma pel; ss: chroma shift;
 // f4: 4-tap filters (blocks 4 wide / high).
-__device__ __forceinline__ int mc_px(const uint8_t* P, int stride, int last_x, int last_y, int px, int py, int mv_row,
-                                     int mv_col, int ss, int f4) {
-    const int px16 = (px << 4) + ((2 * mv_col) >> ss), py16 = (py << 4) + ((2 * mv_row) >> ss);
-    const int fx = px16 & 15, fy = py16 & 15, ix = px16 >> 4, iy = py16 >> 4;
-    if (fx == 0 && fy == 0) return P[(size_t)sk_clip(iy, 0, last_y) * stride + sk_clip(ix, 0, last_x)];
-    int s2 = 0;
-    for (int rr = 0; rr < 8; rr++) {
-        const int tv = subpel_tap(f4, fy, rr);
-        if (tv == 0) continue;
-        const uint8_t* row = P + (size_t)sk_clip(iy + rr - 3, 0, last_y) * stride;
-        int s1 = 0;
-        for (int tt = 0; tt < 8; tt++) s1 += subpel_tap(f4, fx, tt) * row[sk_clip(ix + tt - 3, 0, last_x)];
-        s2 += tv * ((s1 + 4) >> 3);
+__device__ void mc_block(const uint8_t* P, int stride, int last_x, int last_y, int px0, int py0, int n, int mv_row,
+                         int mv_col, int ss, int f4, uint8_t* win, int* h, uint8_t* out) {
+    const int l = lane();
+    const int dx = (2 * mv_col) >> ss, dy = (2 * mv_row) >> ss;
+    const int fx = dx & 15, fy = dy & 15, ix0 = px0 + (dx >> 4), iy0 = py0 + (dy >> 4);
+    if (fx == 0 && fy == 0) {
+        for (int i = l; i < n * n; i += 64)
+            out[i] = P[(size_t)sk_clip(iy0 + i / n, 0, last_y) * stride + sk_clip(ix0 + i % n, 0, last_x)];
+        return;
     }
-    return sk_clip255((s2 + 1024) >> 11);
+    const int wn = n + 7;
+    for (int i = l; i < wn * wn; i += 64) {
+        const int r = i / wn, c = i - r * wn;
+        win[i] = P[(size_t)sk_clip(iy0 - 3 + r, 0, last_y) * stride + sk_clip(ix0 - 3 + c, 0, last_x)];
+    }
+    wsync();
+    for (int i = l; i < wn * n; i += 64) {
+        const int r = i / n, c = i - r * n;
+        const uint8_t* w = win + r * wn + c;
+        int s1 = 0;
+#pragma unroll
+        for (int tt = 0; tt < 8; tt++) s1 += subpel_tap(f4, fx, tt) * (int)w[tt];
+        h[i] = (s1 + 4) >> 3;
+    }
+    wsync();
+    for (int i = l; i < n * n; i += 64) {
+        const int r = i / n, c = i - r * n;
+        int s2 = 0;
+#pragma unroll
+        for (int rr = 0; rr < 8; rr++) s2 += subpel_tap(f4, fy, rr) * h[(r + rr) * n + c];
+        out[i] = (uint8_t)sk_clip255((s2 + 1024) >> 11);
+    }
+    wsync();
 }
 
 // Per-block side outputs: cells and level contexts.
@@ -382,25 +402,31 @@ __device__ __forceinline__ int16_t* lev_ptr(const Av1Args& A, int r, int c, int 
     return u + (p == 0 ? 64 * k : (p == 1 ? 256 + 16 * k : 320 + 16 * k));
 }
 
-// Blocks of a unit: one 16x16, or the inside 8x8s in Z order at frame edges.
-__device__ __forceinline__ int unit_blocks(const Av1Geo& g, int ur, int uc, int* rs, int* cs) {
+// Blocks of a unit: one 16x16 (returns -1), or the inside 8x8s in Z order at frame edges
+// (returns their count; 0 outside the frame). unit_block: the k-th of them (no arrays:
+// dynamically indexed private arrays would live in scratch).
+__device__ __forceinline__ int unit_blocks(const Av1Geo& g, int ur, int uc) {
     const int r = ur * 4, c = uc * 4;
     if (r >= g.mi_rows || c >= g.mi_cols) return 0;
-    if (r + 2 < g.mi_rows && c + 2 < g.mi_cols) {
-        rs[0] = r;
-        cs[0] = c;
-        return -1;   // one 16x16
-    }
+    if (r + 2 < g.mi_rows && c + 2 < g.mi_cols) return -1;
+    int n = 0;
+    for (int q = 0; q < 4; q++) n += (r + (q >> 1) * 2 < g.mi_rows && c + (q & 1) * 2 < g.mi_cols) ? 1 : 0;
+    return n;
+}
+__device__ __forceinline__ void unit_block(const Av1Geo& g, int ur, int uc, int k, int& r, int& c) {
+    r = ur * 4;
+    c = uc * 4;
     int n = 0;
     for (int q = 0; q < 4; q++) {
-        const int rr = r + (q >> 1) * 2, cc = c + (q & 1) * 2;
+        const int rr = ur * 4 + (q >> 1) * 2, cc = uc * 4 + (q & 1) * 2;
         if (rr < g.mi_rows && cc < g.mi_cols) {
-            rs[n] = rr;
-            cs[n] = cc;
+            if (n == k) {
+                r = rr;
+                c = cc;
+            }
             n++;
         }
     }
-    return n;
 }
 
 // ---------------------------------------------------------------------------
@@ -439,12 +465,13 @@ __global__ __launch_bounds__(256) void k_av1_intra_modes(Av1Args A) {
     const int u = blockIdx.x * 4 + w;
     if (u >= f.mb_w * f.mb_h) return;
     const int ux = u % f.mb_w, uy = u / f.mb_w;
-    int rs[4], cs[4];
-    int nb = unit_blocks(g, uy, ux, rs, cs);
+    int nb = unit_blocks(g, uy, ux);
     const int bsl = nb < 0 ? 2 : 1;
     if (nb < 0) nb = 1;
     for (int k = 0; k < nb; k++) {
-        const int r = rs[k], c = cs[k], log2n = bsl + 2, n = 1 << log2n;
+        int r, c;
+        unit_block(g, uy, ux, k, r, c);
+        const int log2n = bsl + 2, n = 1 << log2n;
         const TileRect t = tile_of(g, r, c);
         const bool au = inside(t, r - 1, c), al = inside(t, r, c - 1);
         if (l == 0) intra_edges(f.src.y, f.stride_y, c * 4, r * 4, n, au, al, g.mi_cols * 4 - 1, g.mi_rows * 4 - 1, E[w]);
@@ -531,11 +558,14 @@ __global__ __launch_bounds__(1024) void k_av1_intra_rec(Av1Args A) {
         for (int y = w; y < uh; y += 16) {
             const int x = s - y;
             if (x < 0 || x >= uw) continue;
-            int rs[4], cs[4];
-            int nb = unit_blocks(g, uy0 + y, ux0 + x, rs, cs);
+            int nb = unit_blocks(g, uy0 + y, ux0 + x);
             const int bsl = nb < 0 ? 2 : 1;
             if (nb < 0) nb = 1;
-            for (int k = 0; k < nb; k++) intra_rec_block(A, Lw[w], F, rs[k], cs[k], bsl, qidx);
+            for (int k = 0; k < nb; k++) {
+                int r, c;
+                unit_block(g, uy0 + y, ux0 + x, k, r, c);
+                intra_rec_block(A, Lw[w], F, r, c, bsl, qidx);
+            }
         }
         __syncthreads();
     }
@@ -560,22 +590,22 @@ __global__ __launch_bounds__(256) void k_av1_inter(Av1Args A) {
     const bool moving = t.final_action == ACT_P;
     const int mv_row = moving ? 8 * me.mvy : 0, mv_col = moving ? 8 * me.mvx : 0;
     const int qidx = A.frame[1];
-    int rs[4], cs[4];
-    int nb = unit_blocks(g, uy, ux, rs, cs);
+    int nb = unit_blocks(g, uy, ux);
     const int bsl = nb < 0 ? 2 : 1;
     if (nb < 0) nb = 1;
     const int lxc = ((g.W + 1) >> 1) - 1, lyc = ((g.H + 1) >> 1) - 1;
     for (int k = 0; k < nb; k++) {
-        const int r = rs[k], c = cs[k], log2n = bsl + 2, n = 1 << log2n, cn = n >> 1;
+        int r, c;
+        unit_block(g, uy, ux, k, r, c);
+        const int log2n = bsl + 2, n = 1 << log2n, cn = n >> 1;
         const int x = c * 4, y = r * 4;
         load_src_blk(L, f, x, y, n);
-        for (int i = l; i < n * n; i += 64)
-            L.pred[i] = (uint8_t)mc_px(f.ref.y, f.stride_y, g.W - 1, g.H - 1, x + i % n, y + i / n, mv_row, mv_col, 0, n <= 4);
-        for (int i = l; i < 2 * cn * cn; i += 64) {
-            const int p = i / (cn * cn), j = i % (cn * cn);
-            L.pred[(p ? 320 : 256) + j] = (uint8_t)mc_px(p ? f.ref.v : f.ref.u, f.stride_c, lxc, lyc, (x >> 1) + j % cn,
-                                                          (y >> 1) + j / cn, mv_row, mv_col, 1, cn <= 4);
-        }
+        // prediction (mc_block: window in L.lv, horizontal pass in L.a; both free until
+        // code_block_wave)
+        uint8_t* win = reinterpret_cast<uint8_t*>(L.lv);
+        mc_block(f.ref.y, f.stride_y, g.W - 1, g.H - 1, x, y, n, mv_row, mv_col, 0, n <= 4, win, L.a, L.pred);
+        mc_block(f.ref.u, f.stride_c, lxc, lyc, x >> 1, y >> 1, cn, mv_row, mv_col, 1, cn <= 4, win, L.a, L.pred + 256);
+        mc_block(f.ref.v, f.stride_c, lxc, lyc, x >> 1, y >> 1, cn, mv_row, mv_col, 1, cn <= 4, win, L.a, L.pred + 320);
         wsync();
         const uint32_t s = code_block_wave(L, F, log2n, qidx, false, lev_ptr(A, r, c, bsl, 0),
                                            lev_ptr(A, r, c, bsl, 1), lev_ptr(A, r, c, bsl, 2));
