@@ -1026,20 +1026,15 @@ __device__ __forceinline__ uint32_t ec_word(uint32_t clo, uint32_t chi, int n, i
     return fh | fl << 10 | (uint32_t)(n - s) << 20 | (s > 0 ? 1u << 25 : 0u);
 }
 
-// Token / word batches: kSub sub-batches of 64 (one VGPR each per lane), two big
-// batches in flight. Loads are unconditional (clamped index) so the wait before a big
-// batch is exact and never covers the batch issued after it.
-constexpr int kSub = 8, kBig = 64 * kSub;
-
-__device__ __forceinline__ void use_regs(const uint32_t* v) {
-#pragma unroll
-    for (int j = 0; j < kSub; j++) asm volatile("" ::"v"(v[j]));
-}
+// Tokens per compaction chunk: 16 loads per lane in flight, then this wave's tokens of
+// the chunk (about 1 / kEcParts of them, plus the literals for partition 0) in LDS.
+constexpr int kChunk = 1024;
 
 __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     __shared__ CdfContext cx;
     __shared__ uint32_t wst[64];     // words of the gathered booleans of the sub-batch
     __shared__ uint16_t cap[64][66]; // per token of the sub-batch: the CDF row before its update (padded: conflict-free column reads)
+    __shared__ uint32_t ctok[kChunk], cpos[kChunk];   // this wave's tokens of the chunk, in order, and their stream positions
     const int t = blockIdx.x / kEcParts, part = blockIdx.x % kEcParts, L = threadIdx.x;
     {
         const uint16_t* src = (const uint16_t*)&AV1_DEFAULT_CDF[coef_qctx(A.frame[1])];
@@ -1051,15 +1046,15 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     const int ntok = A.tile_ntok[t], last = A.tile_tok_cap - 1;
     const uint32_t* tk = A.tokc + (size_t)t * A.tile_tok_cap;
     uint32_t* pw = A.pw + (size_t)t * A.tile_tok_cap;
-    // words of tokens this wave does not own go to its junk slots past the streams
-    uint32_t* junk = A.pw + (size_t)A.geo.tile_cols * A.geo.tile_rows * A.tile_tok_cap + (size_t)blockIdx.x * 64;
     // The CDF of the context adapted last stays in a register (lane j: cdf[j]; its
     // counter and adaptation rate in scalars) and goes back to LDS only when another
     // context comes up: the hot contexts (the zero-level context of 16x16 luma blocks
     // can be half of a tile's symbols) adapt in registers with no LDS round trip. The
     // serial loop does only what the next symbol depends on - the lane-parallel update
     // of the row - and leaves the row it started from in cap[token]; the interval words
-    // are built after the loop, one lane per token.
+    // are built after the loop, one lane per token. Every wave first compacts its own
+    // tokens of a chunk (ballot + prefix count), so the serial batches hold only them and
+    // each word is stored once, at its stream position.
     int cache_off = -1, cache_n = 0, cnt = 0, rate = 0, rbase = 0;
     uint32_t cache = 0;
     auto evict = [&]() {
@@ -1069,12 +1064,11 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
         }
         cache_off = -1;
     };
-    auto sub = [&](uint32_t tv, int b) {   // 64 tokens from b: this wave's words
-        // literal tokens are their own word (partition 0 copies them)
-        const uint32_t kind = tv >> 30;
-        const bool lit = kind == 1;
-        const bool mine = b + L < ntok && (lit ? part == 0 : ec_owner(tv & 0x3fffff) == part);
-        uint64_t m = __ballot(mine && !lit), fast = 0;
+    auto sub = [&](int b, int nown) {   // own tokens b .. b + 63 of the chunk
+        const bool valid = b + L < nown;
+        const uint32_t tv = valid ? ctok[b + L] : (1u << 30);
+        const uint32_t kind = tv >> 30;   // literal tokens are their own word (partition 0's)
+        uint64_t m = __ballot(valid && kind != 1);
         while (m) {
             const int i = __builtin_ctzll(m);
             asm volatile("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(i));   // m &= m - 1 in one SALU op
@@ -1101,29 +1095,6 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
                 if (cnt < 32) {
                     cnt++;
                     rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
-                } else {
-                    // A run: the next tokens of this wave repeat this one (the zero level
-                    // of a sparse block's high frequencies, in the same context, comes
-                    // in runs). With the rate fixed, every lane's update is a fixed
-                    // contraction: in y = (lane >= s ? 32768 - c : c) it is y -= y >> rate,
-                    // two VALU ops per symbol. The rows are captured in the y form and
-                    // the word builder converts them back (the `fast` tokens).
-                    const uint64_t eq = __ballot(tv == tt) & m;
-                    const uint64_t ne = m & ~eq;
-                    uint64_t run = eq & (ne ? (ne & (0 - ne)) - 1 : ~0ull);
-                    if (run) {
-                        m &= ~run;
-                        fast |= run;
-                        const bool hi = L >= s;
-                        int y = hi ? 32768 - (int)cache : (int)cache;
-                        do {
-                            const int j = __builtin_ctzll(run);
-                            asm volatile("s_bitset0_b64 %0, %1" : "+s"(run) : "s"(j));
-                            cap[j][L] = (uint16_t)y;
-                            y -= y >> rate;
-                        } while (run);
-                        cache = (uint32_t)(hi ? 32768 - y : y);
-                    }
                 }
             } else {   // gathered boolean: reads a partition CDF from LDS
                 evict();
@@ -1138,39 +1109,38 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
         uint32_t out = tv;   // literal
         if (kind == 0) {
             const int n = (int)((tv >> 26) & 15) + 1, s = (int)((tv >> 22) & 15);
-            uint32_t chi = s < n - 1 ? (uint32_t)cap[L][s] : 0u;
-            const uint32_t clo = s > 0 ? (uint32_t)cap[L][s - 1] : 0u;
-            if (s < n - 1 && ((fast >> L) & 1)) chi = 32768u - chi;   // a run token's row is in y form
+            const uint32_t chi = s < n - 1 ? (uint32_t)cap[L][s] : 0u, clo = s > 0 ? (uint32_t)cap[L][s - 1] : 0u;
             out = ec_word(clo, chi, n, s);
         } else if (kind != 1) {
             out = wst[L];
         }
+        if (valid) pw[cpos[b + L]] = out;
         wsync();
-        uint32_t* d = mine ? pw + b + L : junk + L;   // unconditional store
-        *d = out;
-        return 0;
     };
-    uint32_t X[kSub], Y[kSub];
-    auto load = [&](uint32_t* v, int b) {
+    uint32_t v[kChunk / 64];
+    auto load = [&](int c0) {
 #pragma unroll
-        for (int j = 0; j < kSub; j++) v[j] = tk[sk_min(b + 64 * j + L, last)];
+        for (int j = 0; j < kChunk / 64; j++) v[j] = tk[sk_min(c0 + 64 * j + L, last)];
     };
-    auto big = [&](uint32_t* v, int b) {
+    load(0);
+    for (int c0 = 0; c0 < ntok; c0 += kChunk) {
+        int nown = 0;
 #pragma unroll
-        for (int j = 0; j < kSub; j++)
-            if (b + 64 * j < ntok) sub(v[j], b + 64 * j);
-    };
-    load(X, 0);
-    load(Y, kBig);
-    for (int b = 0; b < ntok; b += 2 * kBig) {
-        use_regs(X);
-        big(X, b);
-        load(X, b + 2 * kBig);
-        if (b + kBig < ntok) {
-            use_regs(Y);
-            big(Y, b + kBig);
+        for (int j = 0; j < kChunk / 64; j++) {
+            const int i = c0 + 64 * j + L;
+            const uint32_t tv = v[j];
+            const bool mine = i < ntok && ((tv >> 30) == 1 ? part == 0 : ec_owner(tv & 0x3fffff) == part);
+            const uint64_t m = __ballot(mine);
+            const int k = nown + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (mine) {
+                ctok[k] = tv;
+                cpos[k] = (uint32_t)i;
+            }
+            nown += __builtin_popcountll(m);
         }
-        load(Y, b + 3 * kBig);
+        wsync();
+        load(c0 + kChunk);   // the next chunk's loads fly during the serial pass
+        for (int b = 0; b < nown; b += 64) sub(b, nown);
     }
 }
 

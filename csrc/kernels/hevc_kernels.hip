@@ -252,6 +252,25 @@ __device__ __forceinline__ void store_rec(const uint8_t* rec, const FrameArgs& f
 // cu; returns the raster holding the chosen reconstruction.
 __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int16_t* gcoef, CuInfo& cu) {
     const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
+    {   // Every coded TU costs at least lam * (kTuRateHalf + 5) (one level): when the CU's whole
+        // prediction error is below that, every TU of every tree zeroes and the 16x16 tree wins
+        // (the split one pays its flags too) - the CPU's choice, without coding the trees.
+        int e2 = 0;
+        for (int i = l; i < kCoefPerCu; i += 64) {
+            const int e = (int)L.src[i] - (int)L.pred[i];
+            e2 += e * e;
+        }
+        const long long sse = wsum(e2);
+        if (512 * sse < (long long)lam * (kTuRateHalf + 5)) {
+            for (int i = l; i < kCoefPerCu; i += 64) gcoef[i] = 0;
+            cu.cbf = 0;
+            cu.tu = cu.tuc = 0;
+            cu.ycbf = 0;
+            cu.tsy = 0;
+            cu.tsc = 0;
+            return L.pred;
+        }
+    }
     tu_batch(L, T, 0, 0, 4, 1, false, false, qp, false, lam, L.levA, L.recA, L.tj[0], L.tf[0]);
     tu_batch(L, T, 1, 0, 3, 2, false, false, qpc, false, lam, L.levA + kCoefCb, L.recA, L.tj[0] + 1, L.tf[0] + 1);
     tu_batch(L, T, 0, 0, 3, 4, false, false, qp, false, lam, L.lev8, L.recS, L.tj[1], L.tf[1]);
