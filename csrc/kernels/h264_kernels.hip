@@ -2630,13 +2630,17 @@ __global__ __launch_bounds__(256) void k_mb_concat(FrameArgs a) {
 
 __device__ __forceinline__ uint8_t rbsp_byte(uint32_t word, int q) { return (uint8_t)(word >> (24 - 8 * q)); }
 
+// EP kernels: grid (tile, slice); a block loops over the slice's NALs (one for every
+// slice but the sub-sliced I ones, so P pictures launch no per-NAL blocks).
 __global__ __launch_bounds__(256) void k_ep_nz(FrameArgs a) {
     __shared__ int red[4];
-    const int nal = blockIdx.y, s = nal / a.nal_per_slice, j = nal % a.nal_per_slice, t = blockIdx.x, tid = threadIdx.x;
-    if (j >= slice_nals(a, a.tasks[s])) return;
+    const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x;
+    const int nn = slice_nals(a, a.tasks[s]);
+    for (int j = 0; j < nn; j++) {
+    const int nal = s * a.nal_per_slice + j;
     const int n = a.slice_info[4 * nal];
     const int t0 = t * kTile;
-    if (t0 >= n) return;
+    if (t0 >= n) continue;
     const uint32_t* rbsp = nal_rbsp(a, s, j);
     const int i0 = t0 + tid * 16;
     int lastnz = -1;
@@ -2645,13 +2649,15 @@ __global__ __launch_bounds__(256) void k_ep_nz(FrameArgs a) {
         const int iq = i0 + 4 * q;
         const uint32_t wd = iq < n ? rbsp[iq >> 2] : 0u;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (iq + j < n && rbsp_byte(wd, j)) lastnz = iq + j;
+        for (int b = 0; b < 4; b++)
+            if (iq + b < n && rbsp_byte(wd, b)) lastnz = iq + b;
     }
     for (int o = 32; o > 0; o >>= 1) lastnz = max(lastnz, __shfl_down(lastnz, o));
     if (lane_id() == 0) red[tid >> 6] = lastnz;
     __syncthreads();
     if (tid == 0) a.tile_nz[nal * a.max_tiles + t] = max(max(red[0], red[1]), max(red[2], red[3]));
+    __syncthreads();
+    }
 }
 
 // Per-thread EP decisions for 16 bytes starting at i0; `carry` = last non-zero
@@ -2707,19 +2713,23 @@ __device__ __forceinline__ int tile_carry(const FrameArgs& a, int nal, int t) {
 __global__ __launch_bounds__(256) void k_ep_count(FrameArgs a) {
     __shared__ int scan_lds[4];
     __shared__ int red[4];
-    const int nal = blockIdx.y, s = nal / a.nal_per_slice, j = nal % a.nal_per_slice, t = blockIdx.x;
-    if (j >= slice_nals(a, a.tasks[s])) return;
-    const int n = a.slice_info[4 * nal];
-    const int t0 = t * kTile;
-    if (t0 >= n) return;
-    const uint32_t* rbsp = nal_rbsp(a, s, j);
-    uint8_t by[16];
-    uint32_t mask;
-    int ins = ep_thread(rbsp, n, t0, tile_carry(a, nal, t), scan_lds, by, &mask);
-    for (int o = 32; o > 0; o >>= 1) ins += __shfl_down(ins, o);
-    if (lane_id() == 0) red[threadIdx.x >> 6] = ins;
-    __syncthreads();
-    if (threadIdx.x == 0) a.tile_ins[nal * a.max_tiles + t] = red[0] + red[1] + red[2] + red[3];
+    const int s = blockIdx.y, t = blockIdx.x;
+    const int nn = slice_nals(a, a.tasks[s]);
+    for (int j = 0; j < nn; j++) {
+        const int nal = s * a.nal_per_slice + j;
+        const int n = a.slice_info[4 * nal];
+        const int t0 = t * kTile;
+        if (t0 >= n) continue;
+        const uint32_t* rbsp = nal_rbsp(a, s, j);
+        uint8_t by[16];
+        uint32_t mask;
+        int ins = ep_thread(rbsp, n, t0, tile_carry(a, nal, t), scan_lds, by, &mask);
+        for (int o = 32; o > 0; o >>= 1) ins += __shfl_down(ins, o);
+        if (lane_id() == 0) red[threadIdx.x >> 6] = ins;
+        __syncthreads();
+        if (threadIdx.x == 0) a.tile_ins[nal * a.max_tiles + t] = red[0] + red[1] + red[2] + red[3];
+        __syncthreads();
+    }
 }
 
 __global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
@@ -2727,13 +2737,14 @@ __global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
     __shared__ int wave_tot[5];
     __shared__ int sh_before, sh_base;
     __shared__ uint8_t sOut[kTile + kTile / 2 + 16];
-    const int nal = blockIdx.y, s = nal / a.nal_per_slice, j = nal % a.nal_per_slice, t = blockIdx.x, tid = threadIdx.x;
+    const int s = blockIdx.y, t = blockIdx.x, tid = threadIdx.x;
     const SliceTask& task = a.tasks[s];
     const int nn = slice_nals(a, task);
-    if (j >= nn) return;
+    for (int j = 0; j < nn; j++) {
+    const int nal = s * a.nal_per_slice + j;
     const int n = a.slice_info[4 * nal];
     const int t0 = t * kTile;
-    if (t0 >= n) return;
+    if (t0 >= n) continue;
     if (tid < 64) {
         int b = 0;
         for (int k = tid; k < t; k += 64) b += a.tile_ins[nal * a.max_tiles + k];
@@ -2794,6 +2805,8 @@ __global__ __launch_bounds__(256) void k_ep_write(FrameArgs a) {
     const int tail0 = head + 16 * nvec;
     if (tid < len - tail0) dst[g0 + tail0 + tid] = sOut[tail0 + tid];
     if (j == nn - 1 && t0 + kTile >= n && tid == 0) a.host_size[s] = g0 + len;
+    __syncthreads();   // sOut / sh_* are rewritten by the next NAL
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -3192,7 +3205,7 @@ void launch_encode(const FrameArgs& a, hipStream_t s, bool guard) {
         launch_code(b, s);
     }
     hipLaunchKernelGGL(k_mb_concat, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
-    const dim3 tiles(a.max_tiles, a.num_slices * a.nal_per_slice);
+    const dim3 tiles(a.max_tiles, a.num_slices);
     hipLaunchKernelGGL(k_ep_nz, tiles, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_ep_count, tiles, dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_ep_write, tiles, dim3(256), 0, s, a);
