@@ -56,6 +56,8 @@ struct CuLds {
     int tf[6][16];               // per-TU cbf, same slots
     uint8_t ref[2][68];          // intra: the TU's reference samples (raw, [1 2 1]-filtered)
     uint8_t ref4[16][17];        // intra mode decision: the sixteen 4x4 blocks' references
+    uint8_t nbt[3][33];          // intra: the row above the CU per component (x = -1 .. 2N - 1)
+    uint8_t nbl[3][16];          // intra: the column left of the CU (y = 0 .. N - 1)
     int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];   // inter: merge / AMVP candidates
 };
 
@@ -463,7 +465,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
 // origin is (px0, py0)), substitution in closed form by ballot. Lane i: entry i (entry
 // 64 of a 16x16 TU: lane 0's second one).
 __device__ void tu_refs(const uint8_t* W, const uint8_t* P, int stride, int px0, int py0, int c, int x0, int y0,
-                        int n, int av, uint8_t* out) {
+                        int n, int av, uint8_t* out, const CuLds* nb = nullptr) {
     const int l = lane(), len = 4 * n + 1, cn = c ? 8 : 16, wb = c == 0 ? 0 : (c == 1 ? kCoefCb : kCoefCr);
     auto fetch = [&](int i, bool& ok) {
         int x, y, bit;
@@ -485,6 +487,7 @@ __device__ void tu_refs(const uint8_t* W, const uint8_t* P, int stride, int px0,
         ok = (av & bit) != 0;
         if (!ok) return 0;
         if (W && x >= 0 && y >= 0 && x < cn && y < cn) return (int)W[wb + y * cn + x];
+        if (nb) return y < 0 ? (int)nb->nbt[c][x + 1] : (int)nb->nbl[c][y];   // outside the CU: prefetched
         return (int)P[(size_t)(py0 + y) * stride + px0 + x];
     };
     bool ok = false;
@@ -526,7 +529,7 @@ __device__ void intra_tu_pred(CuLds& L, const uint8_t* W, const Planes& P, const
                               int log2n, int x0, int y0, int av, int mode) {
     const int n = 1 << log2n, cn = c ? 8 : 16;
     const uint8_t* plane = c == 0 ? P.y : (c == 1 ? P.u : P.v);
-    tu_refs(W, plane, c ? f.stride_c : f.stride_y, cx * cn, cy * cn, c, x0, y0, n, av, L.ref[0]);
+    tu_refs(W, plane, c ? f.stride_c : f.stride_y, cx * cn, cy * cn, c, x0, y0, n, av, L.ref[0], &L);
     const uint8_t* r = L.ref[0];
     if (intra_filter_flag(mode, log2n, c)) {
         ref_filter(L.ref[0], n, L.ref[1]);
@@ -534,6 +537,28 @@ __device__ void intra_tu_pred(CuLds& L, const uint8_t* W, const Planes& P, const
     }
     const int o = (c == 0 ? 0 : (c == 1 ? kCoefCb : kCoefCr)) + y0 * cn + x0;
     tu_pred(L, r, c, log2n, mode, o);
+}
+
+// The CU's outside neighbours (row above incl. the corner and the top-right CU's
+// bottom row, column left) of every component into L.nbt / L.nbl, once per CU: the
+// TU chain then reads its references from LDS only. Unavailable entries are never read.
+__device__ void load_nb(CuLds& L, const Planes& P, const FrameArgs& f, int cx, int cy, bool left, bool top, bool tr) {
+    for (int i = lane(); i < 99; i += 64) {
+        int c, x, y;
+        if (i < 33) { c = 0; x = i - 1; y = -1; }
+        else if (i < 67) { c = 1 + (i - 33) / 17; x = (i - 33) % 17 - 1; y = -1; }
+        else if (i < 83) { c = 0; x = -1; y = i - 67; }
+        else { c = 1 + (i - 83) / 8; x = -1; y = (i - 83) % 8; }
+        const int cn = c ? 8 : 16;
+        const bool ok = y < 0 ? (x < 0 ? left && top : (x < cn ? top : tr)) : left;
+        if (!ok) continue;
+        const uint8_t* pl = c == 0 ? P.y : (c == 1 ? P.u : P.v);
+        const int stride = c ? f.stride_c : f.stride_y;
+        const uint8_t v = pl[(size_t)(cy * cn + y) * stride + cx * cn + x];
+        if (y < 0) L.nbt[c][x + 1] = v;
+        else L.nbl[c][y] = v;
+    }
+    wsync();
 }
 
 // Open-loop intra mode per CU of I slices (all CUs in parallel): the mode whose sixteen
@@ -584,6 +609,7 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
                                    bool tr, int mode, int qp, int16_t* gcoef, CuInfo& cu) {
     const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
     const Planes& P = f.rec;
+    load_nb(L, P, f, cx, cy, left, top, tr);
     // (a) one 16x16 TU
     const int avc = cu_avail(left, top, tr);
     intra_tu_pred(L, nullptr, P, f, cx, cy, 0, 4, 0, 0, avc, mode);
