@@ -370,7 +370,9 @@ SK_HD int32_t dequant(int level, int q) {
 // Encoder quantiser: dead-zone rounding (intra 1/3, inter 1/6 of a step), level capped.
 SK_HD int quantize(int32_t c, int q, bool intra) {
     const int a = c < 0 ? -c : c;
-    const int l = (int)(((int64_t)a * 6 + (intra ? 2 : 1) * q) / (6 * (int64_t)q));
+    // |c| < 2^17 and q <= 1828: the numerator stays far below 2^32 (32-bit division; the
+    // 64-bit one is a long software sequence on the GPU)
+    const int l = (int)(((uint32_t)a * 6u + (uint32_t)((intra ? 2 : 1) * q)) / (6u * (uint32_t)q));
     const int lc = l > 4095 ? 4095 : l;
     return c < 0 ? -lc : lc;
 }
@@ -406,19 +408,30 @@ SK_HD int frame_qidx(const uint8_t* tab, int qpf) {
 // kScanTransposed selects the orientation of the zig-zag (spec Default_Scan_NxN walk:
 // odd anti-diagonals run down-left, even ones up-right, in raster [row][col]).
 constexpr int kScanTransposed = 0;
+// 4x4 | 8x8 | 16x16 scans, generated from the walk below (kept as the definition):
+//   n = 1 << log2n; anti-diagonal d of length d < n ? d + 1 : 2n - 1 - d holding idx;
+//   k = idx - (positions before d); row = (d & 1) ^ kScanTransposed ? row_first + k
+//   : row_last - k (row_first = max(0, d - n + 1), row_last = min(d, n - 1)); pos = row * n + d - row.
+// A table: the walk costs ~200 instructions per call on the GPU, where the token and
+// residual kernels call it for every coefficient.
+SK_TABLE uint8_t AV1_DEFAULT_SCAN[336] = {
+    0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15, 0, 1, 8, 16, 9, 2, 3, 10,
+    17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46,
+    53, 60, 61, 54, 47, 55, 62, 63, 0, 1, 16, 32, 17, 2, 3, 18, 33, 48, 64, 49, 34, 19, 4, 5,
+    20, 35, 50, 65, 80, 96, 81, 66, 51, 36, 21, 6, 7, 22, 37, 52, 67, 82, 97, 112, 128, 113, 98, 83,
+    68, 53, 38, 23, 8, 9, 24, 39, 54, 69, 84, 99, 114, 129, 144, 160, 145, 130, 115, 100, 85, 70, 55, 40,
+    25, 10, 11, 26, 41, 56, 71, 86, 101, 116, 131, 146, 161, 176, 192, 177, 162, 147, 132, 117, 102, 87, 72, 57,
+    42, 27, 12, 13, 28, 43, 58, 73, 88, 103, 118, 133, 148, 163, 178, 193, 208, 224, 209, 194, 179, 164, 149, 134,
+    119, 104, 89, 74, 59, 44, 29, 14, 15, 30, 45, 60, 75, 90, 105, 120, 135, 150, 165, 180, 195, 210, 225, 240,
+    241, 226, 211, 196, 181, 166, 151, 136, 121, 106, 91, 76, 61, 46, 31, 47, 62, 77, 92, 107, 122, 137, 152, 167,
+    182, 197, 212, 227, 242, 243, 228, 213, 198, 183, 168, 153, 138, 123, 108, 93, 78, 63, 79, 94, 109, 124, 139, 154,
+    169, 184, 199, 214, 229, 244, 245, 230, 215, 200, 185, 170, 155, 140, 125, 110, 95, 111, 126, 141, 156, 171, 186, 201,
+    216, 231, 246, 247, 232, 217, 202, 187, 172, 157, 142, 127, 143, 158, 173, 188, 203, 218, 233, 248, 249, 234, 219, 204,
+    189, 174, 159, 175, 190, 205, 220, 235, 250, 251, 236, 221, 206, 191, 207, 222, 237, 252, 253, 238, 223, 239, 254, 255,
+};
 SK_HD int default_scan(int log2n, int idx) {
-    const int n = 1 << log2n;
-    int d = 0, base = 0;
-    while (true) {
-        const int len = d < n ? d + 1 : 2 * n - 1 - d;
-        if (idx < base + len) break;
-        base += len;
-        d++;
-    }
-    const int k = idx - base;
-    const int row_first = d < n ? 0 : d - (n - 1), row_last = d < n ? d : n - 1;
-    const int row = ((d & 1) ^ kScanTransposed) ? row_first + k : row_last - k;
-    return row * n + (d - row);
+    return AV1_DEFAULT_SCAN[(log2n == 2 ? 0 : (log2n == 3 ? 16 : 80)) + idx];
 }
 
 // ---------------------------------------------------------------------------------

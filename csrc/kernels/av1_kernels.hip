@@ -108,20 +108,14 @@ __device__ int trim_cut_wave(int16_t* lv, int ln, bool apply) {
         lvk[k] = k < nw && sidx < nn2 ? (int)lv[default_scan(ln, sidx)] : 0;
         mk[k] = __ballot(lvk[k] != 0);
     }
-    int cut = -1;
+    int cut = -1, last_before = -1;   // last_before: the last non-zero position of the earlier groups
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        int prev = -1;
         const uint64_t below = l ? (mk[k] & ((1ull << l) - 1)) : 0ull;
-        if (below) prev = 64 * k + 63 - __builtin_clzll(below);
-        else
-            for (int j = k - 1; j >= 0; j--)
-                if (mk[j]) {
-                    prev = 64 * j + 63 - __builtin_clzll(mk[j]);
-                    break;
-                }
+        const int prev = below ? 64 * k + 63 - __builtin_clzll(below) : last_before;
         const uint64_t keep = __ballot(lvk[k] != 0 && trim_keep(lvk[k], l + 64 * k, prev));
         if (keep) cut = 64 * k + 63 - __builtin_clzll(keep);
+        if (mk[k]) last_before = 64 * k + 63 - __builtin_clzll(mk[k]);
     }
     if (apply)
 #pragma unroll
