@@ -39,12 +39,21 @@ struct Geo {
     int ctbs() const { return ctb_w * ctb_h; }
 };
 
+// CBR sessions code no scene-cut intra slices (as the AV1 encoder, av1_encoder.h
+// cbr_config): on a bitrate budget a slice recoded as intra costs more bits at the same
+// quality and its CTB wavefront is the picture's longest serial chain. Key frames on
+// request and the GOP stay. Applied by both back ends (front_config, HipBackend).
+inline void cbr_config(h264::EncoderConfig& f) {
+    if (f.rc_mode == h264::RC_CBR) f.scenecut = 0;
+}
+
 // Front-end configuration: full-frame stripes-as-slices, one reference, no H.264 deblock.
 inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
     h264::EncoderConfig f = c;
     f.fullframe = 1;
     f.deblock = 0;
     f.num_refs = 1;
+    cbr_config(f);
     return f;
 }
 

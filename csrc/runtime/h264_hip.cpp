@@ -41,6 +41,7 @@ class HipBackend : public EncoderBackend {
    public:
     HipBackend(const EncoderConfig& c, int device) : cfg_(c), device_(device) {
         if (cfg_.codec == 2) av1::cbr_config(cfg_);   // AV1 CBR as the CPU encoder (av1_encoder.h)
+        if (cfg_.codec == 1) hevc::cbr_config(cfg_);  // HEVC CBR: no scene-cut intra slices (hevc_encoder.h)
         g_.init(cfg_);
         ctl_.init(cfg_, g_);
         HIPCHECK(hipSetDevice(device_));
