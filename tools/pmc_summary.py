@@ -44,8 +44,8 @@ def main():
     sums, dur, calls = load(a.dirs)
     order = sorted(dur, key=lambda k: -sum(dur[k]))[: a.top]
     print("| kernel | calls | us/call | VALU busy % | VALU util % | MFMA busy % | occupancy % | LDS conflict cyc/LDS instr | "
-          "fetch KB/call | write KB/call | GB/s | L2 hit % |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
+          "fetch KB/call | write KB/call | GB/s | L2 hit % | VALU / SALU / LDS / VMEM instr per wave |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
     for k in order:
         s = sums[k]
         n = len(dur[k])
@@ -62,8 +62,11 @@ def main():
         write = s.get("WRITE_SIZE", 0) / npass
         bw = (fetch + write) * 1024 / (us * 1e3) if us else 0
         hit = 100 * s.get("TCC_HIT", 0) / max(s.get("TCC_HIT", 0) + s.get("TCC_MISS", 0), 1)
+        waves = max(s.get("SQ_WAVES", 0), 1)   # same pass as the VALU / SALU counts
+        ipw = "/".join(f"{s.get(c, 0) / waves:.0f}" for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU"))
+        ipw += "/" + "/".join(f"{s.get(c, 0) / waves:.0f}" for c in ("SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"))
         print(f"| {k} | {n} | {us:.1f} | {f(valu)} | {f(valu_u)} | {f(mfma)} | {f(occ)} | {lds:.2f} | {fetch:.0f} | "
-              f"{write:.0f} | {bw:.1f} | {f(hit)} |")
+              f"{write:.0f} | {bw:.1f} | {f(hit)} | {ipw} |")
 
 
 if __name__ == "__main__":
