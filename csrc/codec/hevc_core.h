@@ -486,9 +486,11 @@ SK_HD int intra_inv_angle(int mode) {   // modes 11..25
                   : a == 26 ? -315 : -256;
 }
 // Prediction sample (x, y) of an N x N block from the (filtered) linear reference.
-SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int cidx, int x, int y) {
-    auto L = [&](int yy) { return (int)ref[2 * n - 1 - yy]; };   // p[-1][yy], yy = -1 .. 2N-1
-    auto T = [&](int xx) { return (int)ref[2 * n + 1 + xx]; };   // p[xx][-1], xx = -1 .. 2N-1
+// R: reference accessor, i -> ref[i] (an array, or LDS / cross-lane reads on the GPU).
+template <class R>
+SK_HD int intra_pred_at(R ref, int n, int log2n, int mode, int cidx, int x, int y) {
+    auto L = [&](int yy) { return (int)ref(2 * n - 1 - yy); };   // p[-1][yy], yy = -1 .. 2N-1
+    auto T = [&](int xx) { return (int)ref(2 * n + 1 + xx); };   // p[xx][-1], xx = -1 .. 2N-1
     if (mode == 0) {
         return ((n - 1 - x) * L(y) + (x + 1) * T(n) + (n - 1 - y) * T(x) + (y + 1) * L(n) + n) >> (log2n + 1);
     }
@@ -522,6 +524,9 @@ SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int 
         if (mode == 10 && y == 0) v = sk_clip255(L(0) + ((T(x) - T(-1)) >> 1));
     }
     return v;
+}
+SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int cidx, int x, int y) {
+    return intra_pred_at([&](int i) { return (int)ref[i]; }, n, log2n, mode, cidx, x, y);
 }
 
 // Encoder mode decision (open loop, every CU in parallel, so no MPM-dependent cost):

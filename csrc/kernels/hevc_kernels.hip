@@ -601,6 +601,144 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     }
 }
 
+__device__ __forceinline__ long long shfl64(long long v, int src) {
+    const int lo = __shfl((int)(v & 0xffffffffll), src), hi = __shfl((int)(v >> 32), src);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// One intra 4x4 luma TU of a split node - the hot step of the TU chain (hevc_cpu.cpp
+// code_slice_intra's tu(0, 2, ...): code_tu with the DST and the transform-skip trial) -
+// in registers: lanes 0..15 take sample s (x = s & 3, y = s >> 2) with the DST, lanes
+// 16..31 the same sample with transform skip (lanes 32..63 repeat them); transforms and
+// RD sums by cross-lane shuffles instead of LDS phases. The references go through LDS
+// once (the prediction reads them at sample-dependent positions). The reconstruction
+// lands in W, the levels in lev; returns the cbf, *J the TU's RD cost, *ts the choice.
+__device__ int intra4x4_step(CuLds& L, uint8_t* W, int bx, int by, int av, int mode, int qp, int lam, int16_t* lev,
+                             long long* J, int* ts) {
+    const int l = lane(), s = l & 15, var = (l >> 4) & 1, base = l & ~15;
+    const int x = s & 3, y = s >> 2, o = (4 * by + y) * 16 + 4 * bx + x;
+    tu_refs(W, nullptr, 0, 0, 0, 0, 4 * bx, 4 * by, 4, av, L.ref[0], &L);
+    const uint8_t* ref = L.ref[0];
+    const int p = intra_pred_at([&](int i) { return (int)ref[i]; }, 4, 2, mode, 0, x, y);
+    const int e = (int)L.src[o] - p;
+    auto M = [](int k, int m) { return (int)HEVC_DST4[k][m]; };
+    // forward DST: rows t[y][u] = (sum_k M[u][k] e[y][k] + 1) >> 1, columns (+ 128) >> 8
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) t += M(x, k) * __shfl(e, base + 4 * y + k);
+    t = (t + 1) >> 1;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) c += M(y, k) * __shfl(t, base + 4 * k + x);
+    c = (c + 128) >> 8;
+    if (var) c = e * 32;   // transform skip: the residual << 5
+    const int lv = quant_level(c, qp, 2, true);
+    const int d = dequant_level(lv, qp, 2);
+    // inverse: columns g = clip16((sum_j M[j][y] d[j][x] + 64) >> 7), rows (sum_j M[j][x] g[y][j] + 2048) >> 12
+    int g = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) g += M(j, y) * __shfl(d, base + 4 * j + x);
+    g = sk_clip((g + 64) >> 7, -32768, 32767);
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) r += M(j, x) * __shfl(g, base + 4 * y + j);
+    r = (r + 2048) >> 12;
+    if (var) r = (d * 128 + 2048) >> 12;
+    const int rec = sk_clip255(p + r), e1 = (int)L.src[o] - rec;
+    int s0 = e * e, s1 = e1 * e1, rt = level_rate_half(lv), nz = lv != 0;
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+        s0 += __shfl_xor(s0, m);
+        s1 += __shfl_xor(s1, m);
+        rt += __shfl_xor(rt, m);
+        nz |= __shfl_xor(nz, m);
+    }
+    const int rate = kTuRateHalf + rt;
+    int f = nz;
+    if (f && 512ll * s0 <= 512ll * s1 + (long long)lam * rate) f = 0;   // RD zeroing (code_tu_1)
+    const long long j = f ? 512ll * s1 + (long long)lam * rate : 512ll * s0;
+    const int f0 = __shfl(f, 0), f1 = __shfl(f, 16);
+    const long long j0 = shfl64(j, 0), j1 = shfl64(j, 16);
+    const int use = (f1 && j1 < j0) ? 1 : 0;   // code_tu: transform skip when it codes and costs less
+    const int fsel = use ? f1 : f0;
+    const int lv_t = __shfl(lv, 16 + s), rec_t = __shfl(rec, 16 + s);
+    if (l < 16) {
+        lev[s] = (int16_t)(fsel ? (use ? lv_t : lv) : 0);
+        W[o] = (uint8_t)(fsel ? (use ? rec_t : rec) : p);
+    }
+    *J = use ? j1 : j0;
+    *ts = use;
+    wsync();   // W for the next TU's references
+    return fsel;
+}
+
+// A split node's Cb and Cr 4x4 TUs (code_tu with the DCT and the transform-skip trial), as
+// intra4x4_step: lanes 0..31 Cb, 32..63 Cr, each half DCT (first 16) | transform skip.
+// (ox, oy): the TUs in chroma coordinates of the CU. Levels to lev_c[0] (Cb) / lev_c[64]
+// (Cr), reconstruction into W; per component cbf, RD cost and skip choice.
+__device__ void intra_c4_pair(CuLds& L, const int8_t* T, uint8_t* W, int ox, int oy, int av, int mode, int qpc, int lam,
+                              int16_t* lev_c, int* fc, long long* Jc, int* tsc) {
+    const int l = lane(), s = l & 15, var = (l >> 4) & 1, comp = l >> 5, base = l & ~15;
+    const int x = s & 3, y = s >> 2, o = (comp ? kCoefCr : kCoefCb) + (oy + y) * 8 + ox + x;
+    tu_refs(W, nullptr, 0, 0, 0, 1, ox, oy, 4, av, L.ref[0], &L);
+    tu_refs(W, nullptr, 0, 0, 0, 2, ox, oy, 4, av, L.ref[1], &L);
+    const uint8_t* ref = L.ref[comp];
+    const int p = intra_pred_at([&](int i) { return (int)ref[i]; }, 4, 2, mode, 1 + comp, x, y);
+    const int e = (int)L.src[o] - p;
+    auto M = [&](int k, int m) { return (int)T[(k << 2) * 16 + m]; };   // 4-point DCT rows of T16
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) t += M(x, k) * __shfl(e, base + 4 * y + k);
+    t = (t + 1) >> 1;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) c += M(y, k) * __shfl(t, base + 4 * k + x);
+    c = (c + 128) >> 8;
+    if (var) c = e * 32;
+    const int lv = quant_level(c, qpc, 2, true);
+    const int d = dequant_level(lv, qpc, 2);
+    int g = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) g += M(j, y) * __shfl(d, base + 4 * j + x);
+    g = sk_clip((g + 64) >> 7, -32768, 32767);
+    int r = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) r += M(j, x) * __shfl(g, base + 4 * y + j);
+    r = (r + 2048) >> 12;
+    if (var) r = (d * 128 + 2048) >> 12;
+    const int rec = sk_clip255(p + r), e1 = (int)L.src[o] - rec;
+    int s0 = e * e, s1 = e1 * e1, rt = level_rate_half(lv), nz = lv != 0;
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+        s0 += __shfl_xor(s0, m);
+        s1 += __shfl_xor(s1, m);
+        rt += __shfl_xor(rt, m);
+        nz |= __shfl_xor(nz, m);
+    }
+    const int rate = kTuRateHalf + rt;
+    int f = nz;
+    if (f && 512ll * s0 <= 512ll * s1 + (long long)lam * rate) f = 0;
+    const long long j = f ? 512ll * s1 + (long long)lam * rate : 512ll * s0;
+    const int g0 = comp * 32;
+    const int f0 = __shfl(f, g0), f1 = __shfl(f, g0 + 16);
+    const long long j0 = shfl64(j, g0), j1 = shfl64(j, g0 + 16);
+    const int use = (f1 && j1 < j0) ? 1 : 0;
+    const int fsel = use ? f1 : f0;
+    const int lv_t = __shfl(lv, g0 + 16 + s), rec_t = __shfl(rec, g0 + 16 + s);
+    if (!var) {
+        lev_c[64 * comp + s] = (int16_t)(fsel ? (use ? lv_t : lv) : 0);
+        W[o] = (uint8_t)(fsel ? (use ? rec_t : rec) : p);
+    }
+    // every lane returns both components' results
+    fc[0] = __shfl(fsel, 0);
+    fc[1] = __shfl(fsel, 32);
+    Jc[0] = shfl64(use ? j1 : j0, 0);
+    Jc[1] = shfl64(use ? j1 : j0, 32);
+    tsc[0] = __shfl(use, 0);
+    tsc[1] = __shfl(use, 32);
+    wsync();
+}
+
 // One intra CU (hevc_cpu.cpp code_slice_intra pass 1): the 16x16 TU against the split
 // tree, each 8x8 node's TU against its four 4x4 TUs (transform skip tried), every TU
 // predicted from the reconstruction before it. The committed split reconstruction lives
@@ -628,14 +766,13 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
         long long j4 = (long long)lam * kSplit8RateHalf;
         for (int j = 0; j < 4; j++) {
             const int bx = 2 * (q & 1) + (j & 1), by = 2 * (q >> 1) + (j >> 1), t4 = 4 * q + j, o4 = 4 * by * 16 + 4 * bx;
-            intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, left, top, tr), mode);
-            tu_batch(L, T, 2, o4, 2, 1, true, false, qp, true, lam, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4,
-                     L.lev4t + 16 * t4, L.rec4, L.tj[3] + t4, L.tf[3] + t4);
-            const int m = merge_ts(L, 2, o4, 1, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4, L.lev4t + 16 * t4, L.rec4,
-                                   L.tj[3] + t4, L.tf[3] + t4);
-            tsy |= m << t4;
-            j4 += L.tj[2][t4];
-            c4 |= L.tf[2][t4] << t4;
+            long long jt;
+            int tsb;
+            const int f4 = intra4x4_step(L, W, bx, by, tu_avail_at(bx, by, 1, left, top, tr), mode, qp, lam,
+                                         L.lev4 + 16 * t4, &jt, &tsb);
+            tsy |= tsb << t4;
+            j4 += jt;
+            c4 |= f4 << t4;
         }
         const long long j8 = L.tj[1][q];
         c8 |= L.tf[1][q] << q;
@@ -648,23 +785,17 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
             jb += j8;
             wsync();
         }
-        // the node's Cb and Cr 4x4 TUs in one batch (slots q, q + 4)
-        const int ocb = kCoefCb + (oy / 2) * 8 + ox / 2;
-        intra_tu_pred(L, W, P, f, cx, cy, 1, 2, ox / 2, oy / 2, av, mode);
-        intra_tu_pred(L, W, P, f, cx, cy, 2, 2, ox / 2, oy / 2, av, mode);
-        int16_t* lc = L.levct + 64;   // scratch pair: Cb / Cr levels of this node (compact), copied below
-        int16_t* lct = L.levct + 96;
-        tu_batch(L, T, 3, ocb, 2, 2, false, false, qpc, true, lam, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4,
-                 L.tj[5] + 8, L.tf[5] + 8);
-        const int mc = merge_ts(L, 3, ocb, 2, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4, L.tj[5] + 8, L.tf[5] + 8);
-        for (int i = l; i < 32; i += 64) L.levc[16 * (q + 4 * (i >> 4)) + (i & 15)] = lc[i];
+        // the node's Cb and Cr 4x4 TUs (slots q, q + 4)
+        int fcc[2], tcc[2];
+        long long jcc[2];
+        intra_c4_pair(L, T, W, ox / 2, oy / 2, av, mode, qpc, lam, L.levc + 16 * q, fcc, jcc, tcc);
+#pragma unroll
         for (int c = 0; c < 2; c++) {
             const int t = q + 4 * c;
-            tsc |= ((mc >> c) & 1) << t;
-            jb += L.tj[4][8 + c];
-            tuc |= L.tf[4][8 + c] << t;
+            tsc |= tcc[c] << t;
+            jb += jcc[c];
+            tuc |= fcc[c] << t;
         }
-        wsync();
     }
     const long long ja = L.tj[0][0] + L.tj[0][1] + L.tj[0][2];
     if (jb < ja) {
