@@ -61,12 +61,15 @@ struct CuLds {
     int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];   // inter: merge / AMVP candidates
 };
 
-// LDS copy of the 16-point DCT matrix (the 8 / 4-point ones are its rows 2k / 4k).
+// LDS copy of the 16-point DCT matrix (the 8 / 4-point ones are its rows 2k / 4k) and, at
+// 256 + 4k + m, the 4x4 DST. (Read at lane-dependent positions: LDS, not __constant__.)
+constexpr int kTabT = 256 + 16;
 __device__ __forceinline__ void load_t16(int8_t* t) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) t[i] = HEVC_T16[i >> 4][i & 15];
+    for (int i = threadIdx.x; i < kTabT; i += blockDim.x)
+        t[i] = i < 256 ? HEVC_T16[i >> 4][i & 15] : HEVC_DST4[(i - 256) >> 2][i & 3];
 }
 __device__ __forceinline__ int tx_m(const int8_t* T, int log2n, bool dst, int k, int x) {
-    return dst ? (int)HEVC_DST4[k][x] : (int)T[(k << (4 - log2n)) * 16 + x];
+    return dst ? (int)T[256 + 4 * k + x] : (int)T[(k << (4 - log2n)) * 16 + x];
 }
 
 // TU t of a batch: CU-raster index of its top-left sample (the pitch follows: 16 in the
@@ -342,7 +345,7 @@ __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int1
 // K6 inter (P slices) and skip-all slices: one wave per CU, 4 CUs per workgroup.
 __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     __shared__ CuLds Lw[4];
-    __shared__ int8_t T[256];
+    __shared__ int8_t T[kTabT];
     const FrameArgs& f = A.f;
     CuLds& L = Lw[threadIdx.x >> 6];
     const int n = f.mb_w * f.mb_h;
@@ -613,15 +616,15 @@ __device__ __forceinline__ long long shfl64(long long v, int src) {
 // RD sums by cross-lane shuffles instead of LDS phases. The references go through LDS
 // once (the prediction reads them at sample-dependent positions). The reconstruction
 // lands in W, the levels in lev; returns the cbf, *J the TU's RD cost, *ts the choice.
-__device__ int intra4x4_step(CuLds& L, uint8_t* W, int bx, int by, int av, int mode, int qp, int lam, int16_t* lev,
-                             long long* J, int* ts) {
+__device__ int intra4x4_step(CuLds& L, const int8_t* T, uint8_t* W, int bx, int by, int av, int mode, int qp, int lam,
+                             int16_t* lev, long long* J, int* ts) {
     const int l = lane(), s = l & 15, var = (l >> 4) & 1, base = l & ~15;
     const int x = s & 3, y = s >> 2, o = (4 * by + y) * 16 + 4 * bx + x;
     tu_refs(W, nullptr, 0, 0, 0, 0, 4 * bx, 4 * by, 4, av, L.ref[0], &L);
     const uint8_t* ref = L.ref[0];
     const int p = intra_pred_at([&](int i) { return (int)ref[i]; }, 4, 2, mode, 0, x, y);
     const int e = (int)L.src[o] - p;
-    auto M = [](int k, int m) { return (int)HEVC_DST4[k][m]; };
+    auto M = [&](int k, int m) { return (int)T[256 + 4 * k + m]; };   // the DST (load_t16)
     // forward DST: rows t[y][u] = (sum_k M[u][k] e[y][k] + 1) >> 1, columns (+ 128) >> 8
     int t = 0;
 #pragma unroll
@@ -768,7 +771,7 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
             const int bx = 2 * (q & 1) + (j & 1), by = 2 * (q >> 1) + (j >> 1), t4 = 4 * q + j, o4 = 4 * by * 16 + 4 * bx;
             long long jt;
             int tsb;
-            const int f4 = intra4x4_step(L, W, bx, by, tu_avail_at(bx, by, 1, left, top, tr), mode, qp, lam,
+            const int f4 = intra4x4_step(L, T, W, bx, by, tu_avail_at(bx, by, 1, left, top, tr), mode, qp, lam,
                                          L.lev4 + 16 * t4, &jt, &tsb);
             tsy |= tsb << t4;
             j4 += jt;
@@ -829,7 +832,7 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
 template <int MAXR>
 __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
     __shared__ CuLds Lw[MAXR];
-    __shared__ int8_t T[256];
+    __shared__ int8_t T[kTabT];
     const FrameArgs& f = A.f;
     const SliceTask t = f.tasks[blockIdx.x];
     if (t.final_action != ACT_I) return;   // block-uniform
