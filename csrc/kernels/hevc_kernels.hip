@@ -747,7 +747,7 @@ __device__ void intra_c4_pair(CuLds& L, const int8_t* T, uint8_t* W, int ox, int
 // predicted from the reconstruction before it. The committed split reconstruction lives
 // in L.recS. Levels to gcoef, fields into cu; returns the chosen reconstruction.
 __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f, int cx, int cy, bool left, bool top,
-                                   bool tr, int mode, int qp, int16_t* gcoef, CuInfo& cu) {
+                                   bool tr, int mode, int qp, int16_t* gcoef, CuInfo& cu, bool reg) {
     const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
     const Planes& P = f.rec;
     load_nb(L, P, f, cx, cy, left, top, tr);
@@ -769,13 +769,24 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
         long long j4 = (long long)lam * kSplit8RateHalf;
         for (int j = 0; j < 4; j++) {
             const int bx = 2 * (q & 1) + (j & 1), by = 2 * (q >> 1) + (j >> 1), t4 = 4 * q + j, o4 = 4 * by * 16 + 4 * bx;
-            long long jt;
-            int tsb;
-            const int f4 = intra4x4_step(L, T, W, bx, by, tu_avail_at(bx, by, 1, left, top, tr), mode, qp, lam,
-                                         L.lev4 + 16 * t4, &jt, &tsb);
-            tsy |= tsb << t4;
-            j4 += jt;
-            c4 |= f4 << t4;
+            if (reg) {   // registers (intra4x4_step)
+                long long jt;
+                int tsb;
+                const int f4 = intra4x4_step(L, T, W, bx, by, tu_avail_at(bx, by, 1, left, top, tr), mode, qp, lam,
+                                             L.lev4 + 16 * t4, &jt, &tsb);
+                tsy |= tsb << t4;
+                j4 += jt;
+                c4 |= f4 << t4;
+                continue;
+            }
+            intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, left, top, tr), mode);
+            tu_batch(L, T, 2, o4, 2, 1, true, false, qp, true, lam, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4,
+                     L.lev4t + 16 * t4, L.rec4, L.tj[3] + t4, L.tf[3] + t4);
+            const int m = merge_ts(L, 2, o4, 1, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4, L.lev4t + 16 * t4, L.rec4,
+                                   L.tj[3] + t4, L.tf[3] + t4);
+            tsy |= m << t4;
+            j4 += L.tj[2][t4];
+            c4 |= L.tf[2][t4] << t4;
         }
         const long long j8 = L.tj[1][q];
         c8 |= L.tf[1][q] << q;
@@ -789,16 +800,35 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
             wsync();
         }
         // the node's Cb and Cr 4x4 TUs (slots q, q + 4)
-        int fcc[2], tcc[2];
-        long long jcc[2];
-        intra_c4_pair(L, T, W, ox / 2, oy / 2, av, mode, qpc, lam, L.levc + 16 * q, fcc, jcc, tcc);
+        if (reg) {   // registers (intra_c4_pair)
+            int fcc[2], tcc[2];
+            long long jcc[2];
+            intra_c4_pair(L, T, W, ox / 2, oy / 2, av, mode, qpc, lam, L.levc + 16 * q, fcc, jcc, tcc);
 #pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const int t = q + 4 * c;
+                tsc |= tcc[c] << t;
+                jb += jcc[c];
+                tuc |= fcc[c] << t;
+            }
+            continue;
+        }
+        const int ocb = kCoefCb + (oy / 2) * 8 + ox / 2;
+        intra_tu_pred(L, W, P, f, cx, cy, 1, 2, ox / 2, oy / 2, av, mode);
+        intra_tu_pred(L, W, P, f, cx, cy, 2, 2, ox / 2, oy / 2, av, mode);
+        int16_t* lc = L.levct + 64;   // scratch pair: Cb / Cr levels of this node (compact), copied below
+        int16_t* lct = L.levct + 96;
+        tu_batch(L, T, 3, ocb, 2, 2, false, false, qpc, true, lam, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4,
+                 L.tj[5] + 8, L.tf[5] + 8);
+        const int mc = merge_ts(L, 3, ocb, 2, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4, L.tj[5] + 8, L.tf[5] + 8);
+        for (int i = l; i < 32; i += 64) L.levc[16 * (q + 4 * (i >> 4)) + (i & 15)] = lc[i];
         for (int c = 0; c < 2; c++) {
             const int t = q + 4 * c;
-            tsc |= tcc[c] << t;
-            jb += jcc[c];
-            tuc |= fcc[c] << t;
+            tsc |= ((mc >> c) & 1) << t;
+            jb += L.tj[4][8 + c];
+            tuc |= L.tf[4][8 + c] << t;
         }
+        wsync();
     }
     const long long ja = L.tj[0][0] + L.tj[0][1] + L.tj[0][2];
     if (jb < ja) {
@@ -853,7 +883,8 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
             wsync();
             CuInfo cu;
             memset(&cu, 0, sizeof(cu));
-            const uint8_t* rec = intra_cu(L, T, f, cx, cy, left, top, tr, mode, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu);
+            const uint8_t* rec = intra_cu(L, T, f, cx, cy, left, top, tr, mode, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu,
+                                          A.reg_steps != 0);
             store_rec(rec, f, cx, cy);
             if (l == 0) {
                 cu.mode = CU_INTRA;
