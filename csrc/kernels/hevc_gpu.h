@@ -31,7 +31,7 @@ struct HevcArgs {
     int out_slot, out_dev_slot;
     int addr_bits;
     unsigned long long* dbg;    // optional (SK_STAMPS): per CTB row [cycles, entries, bytes, 0]
-    int reg_steps;              // k_hevc_intra: 4x4 TUs in registers (SK_HEVC_REG_STEPS=1; default: LDS batches)
+    int reg_steps;              // k_hevc_intra: 4x4 TUs in registers (default; SK_HEVC_REG_STEPS=0: LDS batches)
     // chunk-parallel substream coding (codec/hevc_pcabac.h), chunk = CTB
     uint16_t* srt;              // [ctbs][kCuBinCap] the CTB's context bins sorted by context: index << 1 | bin
     uint16_t* coff;             // [ctb_h][kPcCtxOff][ctb_w] start of each context's run in srt (last = count)
