@@ -384,6 +384,9 @@ class CaptureSession {
                     next += period;
                     if (next < clk::now()) next = clk::now();   // behind schedule: do not burst
                 }
+                // a key-frame request that arrived while this thread waited for the budget /
+                // the next tick belongs to the frame about to start, not the one after it
+                if (key_req_.exchange(false)) enc_->request_keyframe();
                 if (!start_frame(frame_id, q)) {
                     if (step) step_failed();
                     continue;
@@ -398,6 +401,7 @@ class CaptureSession {
                         next += period;
                         if (next < clk::now()) next = clk::now();
                     }
+                    if (key_req_.exchange(false)) enc_->request_keyframe();
                     if (start_frame(frame_id, q)) frame_id++;
                     else if (step) step_failed();
                 }
