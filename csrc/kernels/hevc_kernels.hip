@@ -522,22 +522,6 @@ __device__ __forceinline__ void ref_filter(const uint8_t* r, int n, uint8_t* out
 // Prediction of the n x n TU of component c at CU-raster index o into L.pred.
 __device__ __forceinline__ void tu_pred(CuLds& L, const uint8_t* ref, int c, int log2n, int mode, int o) {
     const int n = 1 << log2n, pitch = o < 256 ? 16 : 8;
-    if (mode == 1) {   // DC: the block value once per TU (intra_pred_at sums 2N references per sample)
-        const int l = lane();
-        const int dc = (wsum(l < n ? (int)ref[2 * n + 1 + l] + (int)ref[2 * n - 1 - l] : 0) + n) >> (log2n + 1);
-        for (int i = l; i < n * n; i += 64) {
-            const int x = i & (n - 1), y = i >> log2n;
-            int v = dc;
-            if (c == 0 && n < 32) {   // edge filters of luma DC (8.4.4.2.5)
-                if (x == 0 && y == 0) v = ((int)ref[2 * n - 1] + 2 * dc + (int)ref[2 * n + 1] + 2) >> 2;
-                else if (y == 0) v = ((int)ref[2 * n + 1 + x] + 3 * dc + 2) >> 2;
-                else if (x == 0) v = ((int)ref[2 * n - 1 - y] + 3 * dc + 2) >> 2;
-            }
-            L.pred[o + y * pitch + x] = (uint8_t)v;
-        }
-        wsync();
-        return;
-    }
     for (int i = lane(); i < n * n; i += 64)
         L.pred[o + (i >> log2n) * pitch + (i & (n - 1))] =
             (uint8_t)intra_pred_sample(ref, n, log2n, mode, c, i & (n - 1), i >> log2n);
