@@ -79,6 +79,29 @@ class EncoderBackend {
     std::deque<std::vector<h264::EncodedPacket>> done_;
 };
 
+// Damage-driven upload: the union of row-range lists (pairs [y0, y1), any order, from
+// the public API) on 16-row bands, as maximal row ranges clamped to [0, rows). Empty,
+// inverted and out-of-frame pairs contribute nothing.
+inline std::vector<std::pair<int, int>> upload_ranges(const std::vector<const std::vector<int>*>& lists, int rows) {
+    std::vector<std::pair<int, int>> out;
+    if (rows <= 0) return out;
+    std::vector<uint8_t> band((size_t)(rows + 15) / 16, 0);
+    for (const auto* v : lists)
+        for (size_t i = 0; i + 1 < v->size(); i += 2) {
+            const int y0 = (*v)[i] < 0 ? 0 : (*v)[i], y1 = (*v)[i + 1] > rows ? rows : (*v)[i + 1];
+            if (y0 >= y1) continue;
+            for (int y = y0 / 16; y * 16 < y1; y++) band[y] = 1;
+        }
+    for (int b = 0; b < (int)band.size();) {
+        if (!band[b]) { b++; continue; }
+        int e = b;
+        while (e < (int)band.size() && band[e]) e++;
+        out.emplace_back(b * 16, e * 16 < rows ? e * 16 : rows);
+        b = e;
+    }
+    return out;
+}
+
 EncoderBackend* create_cpu_backend(const h264::EncoderConfig& c);
 EncoderBackend* create_hip_backend(const h264::EncoderConfig& c, int device);
 EncoderBackend* create_cpu_jpeg_backend(const jpeg::JpegConfig& c);

@@ -128,19 +128,10 @@ class HipBackend : public EncoderBackend {
             HIPCHECK(hipMemcpyAsync(bgrx_dev_[q], bgrx, in_bytes, hipMemcpyDefault, cs));
         } else {
             // union of the two damage lists on 16-row bands, copied as maximal row ranges
-            std::vector<uint8_t> band((size_t)(rows + 15) / 16, 0);
-            for (const auto* v : {&up_next_, &up_prev_})
-                for (size_t i = 0; i + 1 < v->size(); i += 2)
-                    for (int y = (*v)[i] / 16; y * 16 < (*v)[i + 1] && y < (int)band.size(); y++) band[y] = 1;
-            for (int b = 0; b < (int)band.size();) {
-                if (!band[b]) { b++; continue; }
-                int e = b;
-                while (e < (int)band.size() && band[e]) e++;
-                const int y0 = b * 16, y1 = std::min(rows, e * 16);
-                HIPCHECK(hipMemcpyAsync(bgrx_dev_[q] + (size_t)y0 * stride, bgrx + (size_t)y0 * stride,
-                                        (size_t)(y1 - y0) * stride, hipMemcpyDefault, cs));
-                up_rows_copied_ += y1 - y0;
-                b = e;
+            for (const auto& r : upload_ranges({&up_next_, &up_prev_}, rows)) {
+                HIPCHECK(hipMemcpyAsync(bgrx_dev_[q] + (size_t)r.first * stride, bgrx + (size_t)r.first * stride,
+                                        (size_t)(r.second - r.first) * stride, hipMemcpyDefault, cs));
+                up_rows_copied_ += r.second - r.first;
             }
         }
         if (!partial) up_rows_copied_ += rows;

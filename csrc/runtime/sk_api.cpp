@@ -421,6 +421,16 @@ int sk_h264_set_upload_rows(void* enc, const int32_t* rows, int32_t n) {
     return 0;
 }
 
+int sk_upload_ranges(const int32_t* pairs, int32_t n, int32_t rows, int32_t* out, int32_t cap) {
+    std::vector<int> v(pairs && n > 0 ? pairs : nullptr, pairs && n > 0 ? pairs + 2 * n : nullptr);
+    const auto r = upload_ranges({&v}, rows);
+    for (int i = 0; i < (int)r.size() && i < cap; i++) {
+        out[2 * i] = r[i].first;
+        out[2 * i + 1] = r[i].second;
+    }
+    return (int)r.size();
+}
+
 int sk_h264_launch(void* enc) {
     try {
         return static_cast<EncoderBackend*>(enc)->launch();

@@ -72,6 +72,9 @@ int sk_h264_wait_stream(void* enc, void* stream);
 // Damage of the next sk_h264_upload: n [y0, y1) row ranges changed since the previous
 // upload (n < 0: unknown -> full copy). The HIP backend then copies only those rows.
 int sk_h264_set_upload_rows(void* enc, const int32_t* rows, int32_t n);
+// The row ranges a damage-driven upload copies for `n` pairs (clamped to [0, rows),
+// 16-row bands); returns the range count, the first `cap` go to out as pairs.
+int sk_upload_ranges(const int32_t* pairs, int32_t n, int32_t rows, int32_t* out, int32_t cap);
 int sk_h264_launch(void* enc);
 // Session state snapshot (codec/h264_encoder.h StateHeader layout, identical for the
 // CPU and HIP backends): move a session between GPUs / processes without an IDR.

@@ -119,6 +119,7 @@ def lib():
         L.sk_h264_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_launch.argtypes = [ctypes.c_void_p]
         L.sk_h264_set_upload_rows.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
+        L.sk_upload_ranges.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
         L.sk_h264_state_bytes.argtypes = [ctypes.c_void_p]
         L.sk_h264_state_bytes.restype = ctypes.c_int64
         L.sk_h264_export_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
@@ -159,6 +160,16 @@ def lib():
 
 def hip_device_count() -> int:
     return int(lib().sk_hip_device_count())
+
+
+def upload_ranges(pairs, rows: int):
+    """Row ranges a damage-driven upload copies for ``pairs`` [(y0, y1), ...] of a
+    ``rows``-row frame (the HIP backend's band union, clamped; bad pairs drop out)."""
+    a = np.ascontiguousarray(np.asarray(pairs, np.int32).reshape(-1, 2))
+    cap = max(1, (int(rows) + 15) // 16)
+    out = np.zeros((cap, 2), np.int32)
+    n = lib().sk_upload_ranges(a.ctypes.data if a.size else None, a.shape[0], int(rows), out.ctypes.data, cap)
+    return [tuple(int(v) for v in r) for r in out[:n]]
 
 
 def require_gpu():

@@ -222,8 +222,14 @@ class DataStreamingServer:
                  web_root: Optional[str] = None, metrics=None, frame_trace: Optional[bool] = None,
                  x_display: Optional[str] = None, basic_auth: Optional[tuple] = None):
         self.settings = settings
-        # (user, password) guarding /files/: the reference serves that area from nginx
-        # behind the container's basic auth; here the data server checks it itself
+        # (user, password) guarding every route, the websocket upgrade included: the
+        # reference puts its whole nginx server block, /ws too, behind basic auth
+        # (addons/example/selkies-gstreamer-entrypoint.sh:89) and its signalling server
+        # refuses an empty password (legacy/signalling_web.py:157-159). /health stays
+        # open for container liveness probes.
+        if basic_auth is not None and not basic_auth[1]:
+            raise ValueError("basic auth is enabled but the password is empty "
+                             "(set SELKIES_BASIC_AUTH_PASSWORD)")
         self.basic_auth = basic_auth
         # this session's X display, passed explicitly to capture, xrandr, DPI and
         # the WM swap: a session host runs several servers in one process, so the
@@ -275,8 +281,17 @@ class DataStreamingServer:
         self.framerate = settings.initial("framerate")
 
     # ================================================================ app / routes
+    AUTH_EXEMPT = ("/health",)
+
+    @web.middleware
+    async def _auth_middleware(self, request: web.Request, handler):
+        if (self.basic_auth is not None and request.path not in self.AUTH_EXEMPT
+                and not _basic_auth_ok(request, *self.basic_auth)):
+            raise web.HTTPUnauthorized(headers={"WWW-Authenticate": 'Basic realm="selkies"'})
+        return await handler(request)
+
     def make_app(self) -> web.Application:
-        app = web.Application(client_max_size=64 * 1024 * 1024)
+        app = web.Application(client_max_size=64 * 1024 * 1024, middlewares=[self._auth_middleware])
         app.router.add_get("/health", self._health)
         if self.metrics is not None:
             app.router.add_get("/metrics", self.metrics.handler)
@@ -295,8 +310,6 @@ class DataStreamingServer:
         root = self.download_dir
         if not root or not os.path.isdir(root):
             raise web.HTTPNotFound()
-        if self.basic_auth is not None and not _basic_auth_ok(request, *self.basic_auth):
-            raise web.HTTPUnauthorized(headers={"WWW-Authenticate": 'Basic realm="selkies"'})
         rel = request.match_info.get("name", "")
         base = os.path.realpath(root)
         path = os.path.realpath(os.path.join(base, rel))

@@ -154,3 +154,19 @@ def test_paced_hip_session_synthetic_decodes():
             if data[1] == 1:
                 decs[y] = H264Decoder()
             assert len(decs[y].decode(data[10:])) == 1
+
+
+def test_upload_ranges_clamp_bad_pairs():
+    """Damage rows reach the HIP upload from the public API (set_upload_rows): negative,
+    inverted, empty and out-of-frame pairs must not index outside the frame (the band
+    union is clamped to [0, rows); bad pairs contribute nothing)."""
+    from selkies_gstreamer_amd.ops.native import upload_ranges
+    assert upload_ranges([(0, 16)], 64) == [(0, 16)]
+    assert upload_ranges([(5, 20)], 64) == [(0, 32)]                  # 16-row bands
+    assert upload_ranges([(-64, 8)], 64) == [(0, 16)]                 # negative start clamped
+    assert upload_ranges([(-100, -20)], 64) == []                     # wholly before the frame
+    assert upload_ranges([(40, 10), (30, 30)], 64) == []              # inverted / empty
+    assert upload_ranges([(50, 1000)], 60) == [(48, 60)]              # past the end, partial band
+    assert upload_ranges([(0, 8), (16, 20), (48, 50)], 64) == [(0, 32), (48, 64)]
+    assert upload_ranges([(2**31 - 1, -2**31)], 64) == []
+    assert upload_ranges([], 64) == []

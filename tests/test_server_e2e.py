@@ -302,6 +302,49 @@ def test_files_listing_and_download(tmp_path):
     run(main())
 
 
+def test_basic_auth_guards_every_route(tmp_path):
+    """SELKIES_ENABLE_BASIC_AUTH protects the whole server like the reference's nginx
+    block (selkies-gstreamer-entrypoint.sh:89): the websocket upgrade, the web root and
+    /metrics answer 401 without credentials; /health stays open; an empty password is
+    refused at startup (legacy/signalling_web.py:157-159)."""
+    from selkies_gstreamer_amd.server.app import basic_auth_from_env
+    from selkies_gstreamer_amd.server.metrics import Metrics
+
+    async def main():
+        web = tmp_path / "web"
+        web.mkdir()
+        (web / "index.html").write_text("<html>ok</html>")
+        s = Settings(["--port", "0"], env={})
+        srv = DataStreamingServer(s, capture_source="synthetic", web_root=str(web), metrics=Metrics(),
+                                  basic_auth=("u", "pw"))
+        port = await srv.start("127.0.0.1", 0)
+        base = f"http://127.0.0.1:{port}"
+        good = aiohttp.BasicAuth("u", "pw")
+        async with aiohttp.ClientSession() as sess:
+            for path in ("/", "/index.html", "/metrics"):
+                async with sess.get(base + path) as r:
+                    assert r.status == 401, path
+                async with sess.get(base + path, auth=aiohttp.BasicAuth("u", "nope")) as r:
+                    assert r.status == 401, path
+            async with sess.get(base + "/", auth=good) as r:
+                assert r.status == 200 and "ok" in await r.text()
+            async with sess.get(base + "/health") as r:
+                assert r.status == 200
+            with pytest.raises(aiohttp.WSServerHandshakeError) as ei:
+                async with sess.ws_connect(base + "/"):
+                    pass
+            assert ei.value.status == 401
+            async with sess.ws_connect(base + "/", auth=good) as ws:
+                msg = await ws.receive(timeout=10)
+                assert msg.type in (aiohttp.WSMsgType.TEXT, aiohttp.WSMsgType.BINARY)
+        await srv.stop()
+    run(main())
+    with pytest.raises(ValueError):
+        DataStreamingServer(Settings(["--port", "0"], env={}), capture_source="synthetic", basic_auth=("u", ""))
+    assert basic_auth_from_env({"SELKIES_ENABLE_BASIC_AUTH": "true", "SELKIES_BASIC_AUTH_USER": "a",
+                                "SELKIES_BASIC_AUTH_PASSWORD": "b"}) == ("a", "b")
+
+
 @pytest.mark.parametrize("encoder", ["x265enc", "svtav1enc"])
 def test_session_hevc_and_av1(tmp_path, encoder):
     """The MI355X encoder extensions over the data websocket: full-frame HEVC (Annex B,

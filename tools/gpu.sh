@@ -21,6 +21,9 @@ tests)
         > "$OUT/pytest.log" 2>&1
     rc=$?; tail -5 "$OUT/pytest.log"
     [ $rc -ne 0 ] && grep -E "FAILED|Error" "$OUT/pytest.log" | tail -20
+    # a hung test (pytest-timeout) or a fatal signal in a test process ends the GPU work
+    # of the call like a time limit does (gpu_steps.sh stops at 124)
+    grep -qE "^E? *Failed: Timeout|Timeout \(>|Fatal Python error|Segmentation fault|Aborted" "$OUT/pytest.log" && exit 124
     exit $rc ;;
 bench)
     timeout -k 10 500 python -u bench.py "$@" > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
@@ -54,8 +57,8 @@ rate)
       for k in 8000 16000; do
         for c in motion desktop; do
           timeout -k 10 300 python -u tools/rc_trace.py --backend hip --codec $codec --frames 600 --content $c \
-              --mode cbr --kbps $k --json "$OUT/${codec}_cbr_${c}_${k}.json" >> "$OUT/summary.jsonl" 2>> "$OUT/err.log" \
-              || { tail -5 "$OUT/err.log"; exit 1; }
+              --mode cbr --kbps $k --json "$OUT/${codec}_cbr_${c}_${k}.json" >> "$OUT/summary.jsonl" 2>> "$OUT/err.log"
+          rc=$?; [ $rc -ne 0 ] && { tail -5 "$OUT/err.log"; exit $rc; }
         done
       done
     done
@@ -77,7 +80,8 @@ pmc)
     for P in "$P1" "$P2" "$P3" "$P4"; do
         i=$((i+1))
         timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/bench.py" "$@" \
-            > "$OUT/p$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+            > "$OUT/p$i.log" 2>&1
+        rc=$?; [ $rc -ne 0 ] && { echo "pmc pass $i failed"; tail -5 "$OUT/p$i.log"; exit $rc; }
         dirs="$dirs $(dirname $(ls "$OUT"/p$i/*counter_collection.csv "$OUT"/p$i/*/*counter_collection.csv 2>/dev/null | head -1))"
     done
     cd "$ROOT"
