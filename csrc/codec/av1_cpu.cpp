@@ -610,22 +610,35 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
         for (int s = 0; s < ns; s++) fe.tasks[s].final_action = ACT_I;
     fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     fp.key = key;
-    {   // K10: the frame's fractional QP under CRF / CBR (k_av1_setup: same rule)
-        uint8_t tab[52];
-        for (int q = 0; q < 52; q++) tab[q] = (uint8_t)qidx_for_qp(q);
-        const h264::RcState& rc = fe.ctl_.rc();
-        fp.qidx = rc.mode == h264::RC_CQP ? tab[sk_clip(fe.tasks[0].qp, 0, 51)] : frame_qidx(tab, rc.cur_qpf);
-    }
-    fp.lf_level = lf_level_for(ac_q(fp.qidx), key);
-    std::fill(blk.begin(), blk.end(), BlkInfo{});
-    if (key) {
-        decide_key();
-    } else {
-        decide_inter();
-        decide_modes();
-    }
+    uint8_t tab[52];
+    for (int q = 0; q < 52; q++) tab[q] = (uint8_t)qidx_for_qp(q);
     std::vector<std::vector<uint8_t>> tiles(geo.tile_cols * geo.tile_rows);
-    for (int t = 0; t < (int)tiles.size(); t++) tiles[t] = code_tile(t);
+    long long payload = 0;   // K10 accounting unit: tile payload bits (k_rc_account: tile sizes)
+    // block decisions, reconstruction and tile coding at the frame's qindex; every block
+    // of the picture is rewritten, so a second pass starts clean
+    auto code_picture = [&] {
+        {   // K10: the frame's fractional QP under CRF / CBR (k_av1_setup: same rule)
+            const h264::RcState& rc = fe.ctl_.rc();
+            fp.qidx = rc.mode == h264::RC_CQP ? tab[sk_clip(fe.tasks[0].qp, 0, 51)] : frame_qidx(tab, rc.cur_qpf);
+        }
+        fp.lf_level = lf_level_for(ac_q(fp.qidx), key);
+        std::fill(blk.begin(), blk.end(), BlkInfo{});
+        if (key) {
+            decide_key();
+        } else {
+            decide_inter();
+            decide_modes();
+        }
+        payload = 0;
+        for (int t = 0; t < (int)tiles.size(); t++) {
+            tiles[t] = code_tile(t);
+            payload += 8 * (long long)tiles[t].size();
+        }
+    };
+    code_picture();
+    // K10 per-frame cap (ratecontrol.h rc_frame_cap): a frame over it is coded again at a
+    // coarser qindex, up to twice (k_rc_guard_sizes gates the GPU back end's passes)
+    for (int r = 0; r < h264::kMaxRecodes && fe.ctl_.rate_redo(fe.tasks.data(), payload); r++) code_picture();
     h264::EncodedPacket pk;
     pk.y = 0;
     pk.w = fe.g.W;
@@ -635,8 +648,6 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
     h264::write_stripe_header(pk.data.data(), key, frame_id, 0, fe.g.W, fe.g.H);
     std::vector<uint8_t> tu = assemble(tiles);
     pk.data.insert(pk.data.end(), tu.begin(), tu.end());
-    long long payload = 0;   // K10 accounting unit: tile payload bits (k_rc_account: tile sizes)
-    for (const auto& t : tiles) payload += 8 * (long long)t.size();
     fe.ctl_.rate_account(payload);
     out.push_back(std::move(pk));
     // every row of the picture was coded: the reconstruction is the next reference

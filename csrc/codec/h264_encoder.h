@@ -288,6 +288,8 @@ SK_HD int rc_redo(RcState& rc, SliceTask* tasks, int ns, long long frame_bits) {
     const int f0 = rc.cur_qpf, f1 = sk_min(f0 + (step << 8), rc.qp_max << 8);
     rc_raise_floor(rc);
     if (f1 == f0) return 0;
+    rc.redo_qpf = f0;   // the pass being replaced: a slope for a further step and the model point
+    rc.redo_bits = (int32_t)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);
     // the frame's slices sit at the two QPs of its dither (rc_dither_qp)
     const int lo = f0 >> 8, hi = (f0 + 255) >> 8;
     for (int s = 0; s < ns; s++) {
@@ -298,6 +300,7 @@ SK_HD int rc_redo(RcState& rc, SliceTask* tasks, int ns, long long frame_bits) {
     rc.cur_qpf = f1;
     rc.cur_qp = (f1 + 128) >> 8;
     rc.redos++;
+    rc.cur_redo++;
     return (f1 - f0 + 255) >> 8;
 }
 
@@ -314,7 +317,7 @@ class Controller {
     // K10: mode (RC_CQP / RC_CRF / RC_CBR) and CBR bitrate from the next frame on.
     void set_rate(int mode, int kbps) {
         const RcState old = rc_;
-        rc_init(rc_, mode, cfg_.qp, kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms);
+        rc_init(rc_, mode, cfg_.qp, kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms, old.qp_min);
         if (old.mode == mode) {   // keep the model; a new budget recentres the buffer
             for (int k = 0; k < 2; k++) {
                 rc_.last_qp[k] = old.last_qp[k];

@@ -682,24 +682,39 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
             fe.intra_activity(s);
         }
     fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
-    for (int s = 0; s < ns; s++) {
-        switch (fe.tasks[s].final_action) {
-            case ACT_P:
-                if (fe.cfg.subpel) fe.subpel_refine(s);   // k_subpel
-                code_slice_inter(s);
-                break;
-            case ACT_I: code_slice_intra(s); break;
-            default: code_slice_skip(s); break;
+    // CU coding at the slice QPs, in-loop deblocking, then the SAO decisions on the
+    // deblocked picture (they are syntax of every CTB, so the binarisation follows them).
+    // Every coded sample of the picture is rewritten, so a second pass starts clean.
+    auto code_picture = [&] {
+        for (int s = 0; s < ns; s++) {
+            switch (fe.tasks[s].final_action) {
+                case ACT_P: code_slice_inter(s); break;
+                case ACT_I: code_slice_intra(s); break;
+                default: code_slice_skip(s); break;
+            }
         }
-    }
-    // in-loop deblocking, then SAO decisions on the deblocked picture (they are syntax of
-    // every CTB, so the binarisation follows them)
-    deblock_picture(fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data(), fe.g.stride_y, fe.g.stride_c, cus.data(),
-                    geo.ctb_w, geo.ctb_h, geo.rows_per_slice);
-    sao_analyse();
-    for (int s = 0; s < ns; s++) binarize_slice(s);
+        deblock_picture(fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data(), fe.g.stride_y, fe.g.stride_c,
+                        cus.data(), geo.ctb_w, geo.ctb_h, geo.rows_per_slice);
+        sao_analyse();
+        for (int s = 0; s < ns; s++) binarize_slice(s);
+    };
+    for (int s = 0; s < ns; s++)   // K4c quarter-pel refinement once, before the first pass
+        if (fe.tasks[s].final_action == ACT_P && fe.cfg.subpel) fe.subpel_refine(s);   // k_subpel
+    code_picture();
     const bool idr = fe.ctl_.picture_is_idr(fe.tasks.data());
     if (idr) poc = 0;
+    std::vector<std::vector<uint8_t>> nals(ns);
+    auto write_picture = [&] {
+        payload_bytes_ = 0;
+        for (int s = 0; s < ns; s++) nals[s] = write_slice(s, idr);
+    };
+    write_picture();
+    // K10 per-frame cap (ratecontrol.h rc_frame_cap): a frame over it is coded again,
+    // coarser, up to twice (k_rc_guard_sizes gates the GPU back end's passes the same way)
+    for (int r = 0; r < h264::kMaxRecodes && fe.ctl_.rate_redo(fe.tasks.data(), 8 * payload_bytes_); r++) {
+        code_picture();
+        write_picture();
+    }
     h264::EncodedPacket pk;
     pk.y = 0;
     pk.w = fe.g.W;
@@ -708,11 +723,7 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
     pk.data.resize(10);
     h264::write_stripe_header(pk.data.data(), idr, frame_id, 0, fe.g.W, fe.g.H);
     if (idr) pk.data.insert(pk.data.end(), param_sets.begin(), param_sets.end());
-    payload_bytes_ = 0;
-    for (int s = 0; s < ns; s++) {
-        std::vector<uint8_t> nal = write_slice(s, idr);
-        pk.data.insert(pk.data.end(), nal.begin(), nal.end());
-    }
+    for (int s = 0; s < ns; s++) pk.data.insert(pk.data.end(), nals[s].begin(), nals[s].end());
     fe.ctl_.rate_account(8 * payload_bytes_);   // K10: substream payload (k_rc_account: sub_size)
     out.push_back(std::move(pk));
     sao_apply();   // the SAO output becomes the reference

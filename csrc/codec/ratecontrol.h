@@ -25,6 +25,10 @@ namespace h264 {
 
 enum RcMode : int32_t { RC_CQP = 0, RC_CRF = 1, RC_CBR = 2 };
 
+// Re-code passes the HEVC / AV1 encoders may add to a frame over its per-frame cap
+// (H.264 adds one: its CAVLC pass is cheap and its model overshoots less).
+constexpr int kMaxRecodes = 2;
+
 struct RcState {
     int32_t mode, base_qp, qp_min, qp_max;
     int32_t budget;          // CBR bits per frame
@@ -49,8 +53,11 @@ struct RcState {
     int32_t vbv_ms;          // CBR buffer in ms (0: 1.5 frame intervals), kept across set_rate()
     int32_t last_qpf[2];     // fractional QP (Q8) of the model frames
     int32_t cur_qpf;         // ... of the frame in flight: slices dither between its two QPs
+    int32_t cur_redo;        // re-code passes of the frame in flight (rc_redo)
+    int32_t redo_qpf;        // ... the fractional QP and payload bits of its pass before the
+    int32_t redo_bits;       //     last one (valid when cur_redo > 0)
 };
-static_assert(sizeof(RcState) == 132, "RcState layout");
+static_assert(sizeof(RcState) == 144, "RcState layout");
 
 SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x <= 1
     if (x <= 1) return 0;
@@ -62,13 +69,15 @@ SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x
 // vbv_ms: the CBR buffer. 0 = 1.5 frame intervals, the reference's low-latency
 // setting for its H.264 / H.265 encoders (legacy/gstwebrtc_app.py:100-104); AV1
 // passes 120 ms, svtav1enc's buf-optimal-sz (gstwebrtc_app.py:738).
-SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float fps, int pixels, int vbv_ms = 0) {
+// qp_min: the finest QP the controller picks (rc_qp_min_for).
+SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float fps, int pixels, int vbv_ms = 0,
+                   int qp_min = 10) {
     rc = RcState{};
     rc.vbv_ms = vbv_ms;
     rc.pixels = pixels;
     rc.mode = mode;
     rc.base_qp = base_qp;
-    rc.qp_min = 10;
+    rc.qp_min = qp_min;
     rc.qp_max = 51;
     const double f = fps > 0 ? fps : 60.0;
     rc.budget = (int32_t)(bitrate_kbps * 1000.0 / f);
@@ -81,6 +90,24 @@ SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float f
 }
 
 SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, rc.qp_max); }
+
+// Finest controller QP per codec (EncoderConfig::codec). H.264 stops at 10. HEVC goes
+// down to 0 like x265's qpmin: its transform skip and residual quadtree code a desktop
+// at QP 10 in ~0.65 of a 16 Mbit/s 1080p60 budget, so CBR needs finer QPs to reach the
+// rate (the per-frame guard bounds what a burst coded that fine costs).
+SK_HD int rc_qp_min_for(int codec) { return codec == 1 ? 0 : 10; }
+
+// Per-frame cap of a non-key frame: the VBV (1.5 frame intervals, the reference's
+// x264enc / x265enc setting, legacy/gstwebrtc_app.py:101-105, 633) and never above 1.5
+// budgets even when the buffer is longer (AV1's 120 ms, svtav1enc buf-optimal-sz
+// :738): a frame several budgets large stalls the link for several frame intervals.
+// A little under the cap because the packets add stripe headers and NAL framing (~2 %
+// at 1080p). Key frames (IDR) may use 4 budgets (their target is 3).
+SK_HD long long rc_frame_cap(const RcState& rc, bool key) {
+    if (key) return 4ll * rc.budget;
+    const long long vbv = sk_min((long long)rc.vbv_size, (long long)rc.budget + rc.budget / 2);
+    return vbv - rc.budget / 16;
+}
 
 // QP whose lambda prices motion vectors in the motion search, which runs before the
 // frame's QP is chosen: under CRF / CBR the QP of the last rate-controlled inter frame
@@ -129,14 +156,21 @@ SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intr
                                ? rc_ilog2_q8((uint32_t)cplx) - rc_ilog2_q8((uint32_t)rc.last_cplx[k]) : 0;
             const int dm = (mbs > 0 && rc.last_mbs[k] > 0)   // coded area ratio
                                ? rc_ilog2_q8((uint32_t)mbs) - rc_ilog2_q8((uint32_t)rc.last_mbs[k]) : 0;
-            const int d = rc_ilog2_q8((uint32_t)rc.last_bits[k]) + dc + dm - rc_ilog2_q8((uint32_t)target);
+            // a large complexity drop (the ordinary frame after a burst: a window opened,
+            // a page of text arrived) moves the QP finer at once, outside the per-frame
+            // limits below: at 2 QP (AV1: half a QP) per frame the frames after every burst
+            // ran at 0.4-0.7 of the budget for a quarter second
+            const int dc_down = dc < -128 ? dc : 0;
+            const int d = rc_ilog2_q8((uint32_t)rc.last_bits[k]) + (dc - dc_down) + dm - rc_ilog2_q8((uint32_t)target);
             // a long buffer (AV1, vbv_ms) absorbs a misprediction, so its inter frames move
             // gently: 3 QP per halving and at most a quarter QP finer per frame. At the top
             // of AV1's quantiser range an inter frame's size doubles every ~2-3 QP (it
             // re-codes what the coarser frames before it lost): larger steps oscillate
+            // (half a QP finer per frame: the per-frame cap catches an overshoot, and a
+            // quarter QP left the stream at 0.5-0.7 of its rate for seconds after a burst)
             const bool gentle = rc.vbv_ms > 0 && !intra;
             const int dq = gentle ? 3 * d : (d >= 0 ? 6 * d : 5 * d);   // Q8 QP
-            qp = rc.last_qpf[k] + sk_clip(dq, gentle ? -64 : -512, (intra ? 16 : 10) << 8);
+            qp = rc.last_qpf[k] + sk_clip(dq, gentle ? -128 : -512, (intra ? 16 : 10) << 8) + (gentle ? 3 : 5) * dc_down;
             // screen content can jump several-fold within one QP (glyph edges crossing the
             // dead zone together): stay above the QP that last overflowed the buffer
             if (!intra && rc.qp_floor > qp) qp = rc.qp_floor;
@@ -166,6 +200,7 @@ SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intr
     rc.cur_valid = 1;
     rc.cur_idr = idr ? 1 : 0;
     rc.cur_mbs = mbs;
+    rc.cur_redo = 0;
     return qp;
 }
 
@@ -176,18 +211,49 @@ SK_HD int rc_dither_qp(int qpf, int i) {
     return lo + ((((i + 1) * f + 128) >> 8) - ((i * f + 128) >> 8));
 }
 
-// CBR guard (VBV overflow): a frame whose payload exceeds the buffer (1.5 budgets;
-// key frames: 4 budgets, their target is 3) is coded once more, coarser by the QP
-// step this returns (0: keep it): the model's 6 QP per halving towards the target.
+// CBR guard (per-frame cap, rc_frame_cap): a frame whose payload exceeds its cap is
+// coded once more, coarser by the QP step this returns (0: keep it). The first step
+// assumes the model's 6 QP per halving towards the target; a further one uses the
+// slope the frame itself showed between its last two passes (screen content is far
+// flatter or steeper than 6 QP per halving). Every codec runs it (H.264 k_rc_guard,
+// HEVC / AV1 k_rc_guard_sizes, the CPU encoders alike). When the last pass still
+// overflows at QP 51 the frame is sent as coded: the encoder keeps no B frames or
+// frame drops, the buffer accounting (rc_account) clamps at the VBV and the next
+// frames pay it back.
 SK_HD int rc_redo_step(const RcState& rc, long long frame_bits) {
     if (rc.mode != RC_CBR || !rc.cur_valid) return 0;
-    // payload bits: the packets add stripe headers and NAL framing, ~2 % at 1080p
-    const long long cap = rc.cur_idr ? 4ll * rc.budget : (long long)rc.vbv_size - rc.budget / 16;
+    const long long cap = rc_frame_cap(rc, rc.cur_idr != 0);
     if (frame_bits <= cap) return 0;
     const uint32_t b = (uint32_t)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);
     const int target = sk_max(rc.cur_idr ? 3 * rc.budget : rc.budget, 1);
-    const int d = rc_ilog2_q8(b) - rc_ilog2_q8((uint32_t)target);   // Q8, > 0
-    return sk_clip((6 * d + 128) / 256, 2, 16);
+    const int d = rc_ilog2_q8(b) - rc_ilog2_q8((uint32_t)target);   // Q8 halvings, > 0
+    int slope = 6 << 8;                                               // Q8 QP per halving
+    if (rc.cur_redo > 0) {
+        const int dq = rc.cur_qpf - rc.redo_qpf;
+        const int dl = rc_ilog2_q8((uint32_t)sk_max(rc.redo_bits, 2)) - rc_ilog2_q8(b);
+        slope = (dq > 0 && dl > 0) ? sk_clip((int)(((long long)dq << 8) / dl), 3 << 8, 24 << 8) : 24 << 8;
+    }
+    return sk_clip((int)(((long long)slope * d + 32768) >> 16), 2, 24);
+}
+
+// Model point of a re-coded inter frame: the QP at which its content meets the budget,
+// interpolated in log size between its last two passes (extrapolated at their slope
+// past the coarser one). Training the model on the coarse re-code itself left the next
+// frames several QP too coarse (screen content falls 10x within 4 QP); the first pass
+// alone would repeat the overflow.
+SK_HD int rc_redo_model_qpf(const RcState& rc, int bits, int target) {
+    const int l1 = rc_ilog2_q8((uint32_t)sk_max(rc.redo_bits, 2)), l2 = rc_ilog2_q8((uint32_t)sk_max(bits, 2));
+    const int lt = rc_ilog2_q8((uint32_t)sk_max(target, 2));
+    const int dq = rc.cur_qpf - rc.redo_qpf;
+    if (dq <= 0 || l1 <= l2) return rc.cur_qpf;
+    const long long q = (long long)rc.redo_qpf + (long long)dq * (l1 - lt) / (l1 - l2);
+    return (int)sk_min(sk_max(q, (long long)rc.qp_min << 8), (long long)rc.qp_max << 8);
+}
+
+// A burst: the frame in flight is far busier than the last inter frame (a window
+// opening, a page of new text), measured by the motion search before coding.
+SK_HD bool rc_burst(const RcState& rc) {
+    return rc.cur_cplx > 0 && rc.last_cplx[0] > 0 && 2 * (long long)rc.cur_cplx > 3 * (long long)rc.last_cplx[0];
 }
 
 // The frame in flight (first pass at cur_qp) overflowed: remember its QP as a floor
@@ -196,7 +262,7 @@ SK_HD void rc_raise_floor(RcState& rc) {
     if (rc.cur_intra) return;
     // a burst (complexity well above the last inter frame's) overflows at any QP the
     // buffer allows for ordinary frames: re-code it, but keep the floor where it is
-    if (rc.cur_cplx > 0 && rc.last_cplx[0] > 0 && 2 * (long long)rc.cur_cplx > 3 * (long long)rc.last_cplx[0]) return;
+    if (rc_burst(rc)) return;
     // a quarter QP above the QP that overflowed: the dither reaches the cliff's edge
     rc.qp_floor = sk_max(rc.qp_floor, rc.cur_qpf + 64);
     rc.floor_age = 0;
@@ -208,9 +274,16 @@ SK_HD void rc_account(RcState& rc, long long frame_bits) {
     const int bits = (int)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);
     // frames whose QP the controller did not choose (all static) do not train the model
     if (rc.cur_valid) {   // last_cplx 0: not measured (the next prediction assumes no change)
-        rc.last_qp[k] = rc.cur_qp;
-        rc.last_qpf[k] = rc.cur_qpf;
-        rc.last_bits[k] = bits > 0 ? bits : 1;
+        if (rc.cur_redo > 0 && !rc.cur_intra) {   // re-coded: the budget point (rc_redo_model_qpf)
+            const int q = rc_redo_model_qpf(rc, bits, rc.budget);
+            rc.last_qpf[k] = q;
+            rc.last_qp[k] = (q + 128) >> 8;
+            rc.last_bits[k] = sk_max(rc.budget, 1);
+        } else {
+            rc.last_qp[k] = rc.cur_qp;
+            rc.last_qpf[k] = rc.cur_qpf;
+            rc.last_bits[k] = bits > 0 ? bits : 1;
+        }
         rc.last_cplx[k] = rc.cur_cplx;
         rc.last_mbs[k] = rc.cur_mbs;
     }
@@ -223,11 +296,11 @@ SK_HD void rc_account(RcState& rc, long long frame_bits) {
     if (rc.cur_valid && !rc.cur_intra && bits > rc.max_p_bits) rc.max_p_bits = bits;
     if (rc.qp_floor > 0) {
         // 1 QP per 16 frames (3.75 QP a second at 60 fps); an inter frame coded AT the
-        // floor (not above it, not re-coded) in half its budget or less says the cliff
+        // floor (not above it, not re-coded) in 3/4 of its budget or less says the cliff
         // has passed: half a QP per frame (1080p synthetic desktop, H.264 16 Mbit/s: 7 s
         // at 0.3-0.6 budgets under the slow decay alone)
         const bool at_floor = rc.cur_valid && !rc.cur_intra && rc.cur_qpf <= rc.qp_floor;
-        const int step = (at_floor && 2ll * bits < rc.budget) ? 128 : 16;
+        const int step = (at_floor && 4ll * bits < 3ll * rc.budget) ? 128 : 16;
         rc.qp_floor = rc.qp_floor - step > (rc.qp_min << 8) ? rc.qp_floor - step : 0;
         rc.floor_age++;
     }

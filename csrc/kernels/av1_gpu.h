@@ -51,7 +51,9 @@ struct Av1Args {
     int* out_size_host;       // host-mapped [tiles] bytes (-1: did not fit out_cap)
 };
 
-void launch_backend(const Av1Args& a, hipStream_t s);
+// redo: the K10 re-code flag (CBR sessions): the coding kernels run a second time,
+// gated on it, after k_rc_guard_sizes checked the frame against its cap; nullptr: one pass.
+void launch_backend(const Av1Args& a, hipStream_t s, int* redo = nullptr);
 // Sizes of the coder's block maps and big-integer digits for tiles of tile_bytes.
 void ec_buffers(int tiles, int tile_bytes, int* max_blocks, int* vcap);
 

@@ -37,6 +37,9 @@ using h264::SliceTask;
 using h264::gpu::FrameArgs;
 
 __device__ __forceinline__ int lane() { return threadIdx.x & 63; }
+// K10 per-frame cap: the coding kernels run a second time, gated, after k_rc_guard_sizes
+// (f.gate = the re-code flag); they return at once unless the frame overflowed.
+__device__ __forceinline__ bool second_pass_skipped(const FrameArgs& f) { return f.gate && *f.gate == 0; }
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -425,6 +428,7 @@ __device__ __forceinline__ void unit_block(const Av1Geo& g, int ur, int uc, int 
 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_av1_setup(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int ns = f.num_slices;
     bool key = false;
@@ -451,6 +455,7 @@ __global__ __launch_bounds__(256) void k_av1_setup(Av1Args A) {
 
 // Key frames: intra mode per block from the source edges (one wave per unit).
 __global__ __launch_bounds__(256) void k_av1_intra_modes(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ IntraEdge E[4];
     if (!A.frame[0]) return;
     const FrameArgs& f = A.f;
@@ -535,6 +540,7 @@ __device__ void intra_rec_block(const Av1Args& A, BlkLds& L, const FdctLds& F, i
 
 // Key frames: one workgroup (16 waves) per tile; unit (x, y) of the tile at step x + y.
 __global__ __launch_bounds__(1024) void k_av1_intra_rec(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ BlkLds Lw[16];
     __shared__ FdctLds F;
     if (!A.frame[0]) return;
@@ -567,6 +573,7 @@ __global__ __launch_bounds__(1024) void k_av1_intra_rec(Av1Args A) {
 
 // Inter frames: one wave per unit, vector from the front end's motion search.
 __global__ __launch_bounds__(256) void k_av1_inter(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ BlkLds Lw[4];
     __shared__ FdctLds F;
     if (A.frame[0]) return;
@@ -622,6 +629,7 @@ __global__ __launch_bounds__(256) void k_av1_inter(Av1Args A) {
 
 // Static merging per superblock: lane = 8x8 cell of the SB (8 x 8 cells).
 __global__ __launch_bounds__(64) void k_av1_merge(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     if (A.frame[0]) return;
     const Av1Geo& g = A.geo;
     const int sb = blockIdx.x, sr = sb / g.sb_cols, sc = sb % g.sb_cols;
@@ -656,6 +664,7 @@ __global__ __launch_bounds__(64) void k_av1_merge(Av1Args A) {
 
 // Inter modes from the MV stack: one lane per 8x8 cell, block origins only.
 __global__ __launch_bounds__(256) void k_av1_modes(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     if (A.frame[0]) return;
     const Av1Geo& g = A.geo;
     const int cell = blockIdx.x * 256 + threadIdx.x;
@@ -919,6 +928,7 @@ __device__ int code_coeffs(WaveTokenSink& w, const CdfContext& cx, const int16_t
 }
 
 __global__ __launch_bounds__(256) void k_av1_tokens(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint32_t bits_w[4][256];
     const int w = threadIdx.x >> 6;
     const int u = blockIdx.x * 4 + w;
@@ -948,6 +958,7 @@ __global__ __launch_bounds__(256) void k_av1_tokens(Av1Args A) {
 // the coder reads one contiguous stream. k_av1_tok_scan: per-unit offsets (one
 // workgroup per tile, block scan); k_av1_tok_copy: one wave per unit.
 __global__ __launch_bounds__(256) void k_av1_tok_scan(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ int wsum_s[4];
     __shared__ int run_s;
     const Av1Geo& g = A.geo;
@@ -985,6 +996,7 @@ __global__ __launch_bounds__(256) void k_av1_tok_scan(Av1Args A) {
 }
 
 __global__ __launch_bounds__(256) void k_av1_tok_copy(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const Av1Geo& g = A.geo;
     const int u = blockIdx.x * 4 + (threadIdx.x >> 6), l = lane();
     if (u >= A.f.mb_w * A.f.mb_h) return;
@@ -1025,6 +1037,7 @@ __device__ __forceinline__ uint32_t ec_word(uint32_t clo, uint32_t chi, int n, i
 constexpr int kChunk = 1024;
 
 __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CdfContext cx;
     __shared__ uint32_t wst[64];     // words of the gathered booleans of the sub-batch
     __shared__ uint16_t cap[64][66]; // per token of the sub-batch: the CDF row before its update (padded: conflict-free column reads)
@@ -1224,6 +1237,7 @@ __device__ __forceinline__ void ec_step(uint32_t& r, uint32_t& D, uint32_t w) {
 }
 
 __global__ __launch_bounds__(256) void k_av1_ec_map(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const int tiles = A.geo.tile_cols * A.geo.tile_rows, l = lane();
     int bsz, incl, ntl;
     const int total = ec_blocks(A, tiles, &bsz, &incl, &ntl);
@@ -1255,6 +1269,7 @@ __global__ __launch_bounds__(256) void k_av1_ec_map(Av1Args A) {
 }
 
 __global__ __launch_bounds__(64) void k_av1_ec_link(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const int tiles = A.geo.tile_cols * A.geo.tile_rows, l = lane(), t = blockIdx.x;
     int bsz, incl, ntl;
     ec_blocks(A, tiles, &bsz, &incl, &ntl);
@@ -1308,6 +1323,7 @@ __global__ __launch_bounds__(64) void k_av1_ec_link(Av1Args A) {
 }
 
 __global__ __launch_bounds__(256) void k_av1_ec_emit(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const int tiles = A.geo.tile_cols * A.geo.tile_rows, l = lane();
     int bsz, incl, ntl;
     const int total = ec_blocks(A, tiles, &bsz, &incl, &ntl);
@@ -1387,6 +1403,7 @@ __global__ __launch_bounds__(256) void k_av1_ec_emit(Av1Args A) {
 }
 
 __global__ __launch_bounds__(256) void k_av1_ec_bytes(Av1Args A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint32_t wg_s[4], wp_s[4];
     __shared__ int off_s, carry_s;
     const int t = blockIdx.x, tid = threadIdx.x, l = lane(), w = tid >> 6;
@@ -1571,7 +1588,9 @@ void ec_buffers(int tiles, int tile_bytes, int* max_blocks, int* vcap) {
     *vcap = tile_bytes / 4 + 8;
 }
 
-void launch_backend(const Av1Args& a, hipStream_t s) {
+// Block decisions, reconstruction and the arithmetic-coded tiles: everything the coded
+// size depends on (the K10 guard re-runs it, gated).
+static void launch_code(const Av1Args& a, hipStream_t s) {
     const int n = a.f.mb_w * a.f.mb_h;
     const int tiles = a.geo.tile_cols * a.geo.tile_rows;
     hipLaunchKernelGGL(k_av1_setup, dim3(1), dim3(256), 0, s, a);
@@ -1585,6 +1604,19 @@ void launch_backend(const Av1Args& a, hipStream_t s) {
     hipLaunchKernelGGL(k_av1_tok_copy, dim3((n + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_av1_cdf, dim3(tiles * kEcParts), dim3(64), 0, s, a);
     launch_ec(a, tiles, s);
+}
+
+void launch_backend(const Av1Args& a, hipStream_t s, int* redo) {
+    const int tiles = a.geo.tile_cols * a.geo.tile_rows;
+    launch_code(a, s);
+    if (redo) {   // K10 CBR per-frame cap: payload = the tile bytes (as k_rc_account)
+        Av1Args b = a;
+        b.f.gate = redo;
+        for (int r = 0; r < h264::gpu::kMaxRecodes; r++) {
+            h264::gpu::launch_rc_guard_sizes(a.f, a.tile_size, tiles, redo, r > 0, s);
+            launch_code(b, s);
+        }
+    }
     for (int p = 0; p < 3; p++) {   // in-loop deblocking of the reconstruction, plane by plane
         const int ss = p ? 1 : 0;
         const int cnt = ((a.geo.mi_cols + ss) >> ss) * ((a.geo.mi_rows + ss) >> ss);

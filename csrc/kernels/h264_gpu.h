@@ -94,6 +94,10 @@ void launch_commit(const FrameArgs& a, hipStream_t s);   // MV field + reference
 // K10 accounting of the frame just coded: frame bytes = sum of sizes[i * stride],
 // i < n (per_slice: only slices that were coded).
 void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, int per_slice, hipStream_t s);
+// K10 per-frame cap of a back end whose payload is the sum of n byte counts (HEVC / AV1);
+// chained: the check after a re-code pass (runs only when *redo is up)
+void launch_rc_guard_sizes(const FrameArgs& a, const int* sizes, int n, int* redo, bool chained, hipStream_t s);
+using h264::kMaxRecodes;   // re-code passes of the HEVC / AV1 back ends (ratecontrol.h)
 
 }  // namespace gpu
 }  // namespace h264

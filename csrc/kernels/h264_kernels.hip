@@ -787,7 +787,7 @@ __global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
         const int mode = a.key_dev[3];
         const int kbps = a.key_dev[4];
         const RcState old = rc;
-        rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H, old.vbv_ms);
+        rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H, old.vbv_ms, old.qp_min);
         if (old.mode == mode)
             for (int k = 0; k < 2; k++) {
                 rc.last_qp[k] = old.last_qp[k];
@@ -844,6 +844,29 @@ __global__ __launch_bounds__(256) void k_rc_guard(FrameArgs a) {
         const int words = (a.slice_info[4 * (s * a.nal_per_slice + j)] + 3) / 4 + 1;
         for (int i = tid; i < words; i += 256) rbsp[i] = 0u;
     }
+}
+
+// K10 per-frame cap of the HEVC / AV1 back ends: the frame's payload is the sum of
+// `sizes` (bytes: HEVC substreams, AV1 tiles, the units k_rc_account counts); over the
+// cap, rc_redo moves the slice QPs / the frame QP coarser and raises *redo for the
+// gated next coding pass. One workgroup; *redo is rewritten by the first guard of every
+// frame; a later guard (chained: it checks the pass the flag ran) returns at once
+// when the flag is down, leaving it down.
+__global__ __launch_bounds__(256) void k_rc_guard_sizes(FrameArgs a, const int* sizes, int n, int* redo, int chained) {
+    __shared__ long long part[4];
+    if (chained && *redo == 0) return;
+    const int tid = threadIdx.x;
+    long long b = 0;
+    for (int i = tid; i < n; i += 256) b += sizes[i];
+    for (int o = 32; o > 0; o >>= 1) b += __shfl_down(b, o);
+    if ((tid & 63) == 0) part[tid >> 6] = b;
+    __syncthreads();
+    if (tid != 0) return;
+    const long long bits = 8 * (part[0] + part[1] + part[2] + part[3]);
+    const int applied = rc_redo_step(*a.rc, bits) ? rc_redo(*a.rc, a.tasks, a.num_slices, bits) : 0;
+    *redo = applied ? 1 : 0;
+    if (applied)
+        for (int i = 0; i < a.num_slices; i++) a.tasks_host[i].qp = a.tasks[i].qp;
 }
 
 // ---------------------------------------------------------------------------
@@ -3172,6 +3195,10 @@ void launch_frontend(const FrameArgs& a, hipStream_t s) {
     // K4c quarter-pel refinement (H.264 and HEVC; the HEVC back end codes the vectors
     // with its own 8-tap filters)
     if (a.subpel) hipLaunchKernelGGL(k_subpel, dim3((nmb + 3) / 4), dim3(256), 0, s, a);
+}
+
+void launch_rc_guard_sizes(const FrameArgs& a, const int* sizes, int n, int* redo, bool chained, hipStream_t s) {
+    hipLaunchKernelGGL(k_rc_guard_sizes, dim3(1), dim3(256), 0, s, a, sizes, n, redo, chained ? 1 : 0);
 }
 
 void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, int per_slice, hipStream_t s) {

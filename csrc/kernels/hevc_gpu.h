@@ -49,7 +49,9 @@ struct HevcArgs {
     h264::gpu::Planes sao_tmp;  // filtered samples of the CTBs SAO changes, copied back into f.rec
 };
 
-void launch_backend(const HevcArgs& a, hipStream_t s);
+// redo: the K10 re-code flag (CBR sessions): the coding kernels run a second time,
+// gated on it, after k_rc_guard_sizes checked the frame against its cap; nullptr: one pass.
+void launch_backend(const HevcArgs& a, hipStream_t s, int* redo = nullptr);
 
 }  // namespace gpu
 }  // namespace hevc

@@ -40,6 +40,10 @@ __device__ __forceinline__ int wsum(int v) {
     return v;
 }
 
+// K10 per-frame cap: the coding kernels run a second time, gated, after k_rc_guard_sizes
+// (f.gate = the re-code flag); they return at once unless the frame overflowed.
+__device__ __forceinline__ bool second_pass_skipped(const FrameArgs& f) { return f.gate && *f.gate == 0; }
+
 // Per-wave LDS working set of one CU. Sample rasters (src, pred, rec*) hold the CU's
 // 384 samples: Y 16x16 (pitch 16) | Cb 8x8 | Cr 8x8 (pitch 8).
 struct CuLds {
@@ -344,6 +348,7 @@ __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int1
 // ---------------------------------------------------------------------------
 // K6 inter (P slices) and skip-all slices: one wave per CU, 4 CUs per workgroup.
 __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
     __shared__ int8_t T[kTabT];
     const FrameArgs& f = A.f;
@@ -567,6 +572,7 @@ __device__ void load_nb(CuLds& L, const Planes& P, const FrameArgs& f, int cx, i
 // Open-loop intra mode per CU of I slices (all CUs in parallel): the mode whose sixteen
 // 4x4 predictions from their source neighbours are closest (hevc_cpu.cpp pass 0).
 __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
     const FrameArgs& f = A.f;
     CuLds& L = Lw[threadIdx.x >> 6];
@@ -861,6 +867,7 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
 // step x + 2w (the top-right CTB is one step older: WPP / intra availability order).
 template <int MAXR>
 __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[MAXR];
     __shared__ int8_t T[kTabT];
     const FrameArgs& f = A.f;
@@ -904,6 +911,7 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
 // ---------------------------------------------------------------------------
 // CU syntax -> bin entries: one thread per CU (a wave binarises 64 CUs at once).
 __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int n = f.mb_w * f.mb_h;
     const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -938,6 +946,7 @@ __device__ __forceinline__ int writelane(int x, int ln, int v) {
 // of the two CTBs, from k_pc_sort's per-context lists: the chains run in parallel and
 // each is a few entries long.
 __global__ __launch_bounds__(192) void k_hevc_sync(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint8_t nlps[64];
     const FrameArgs& f = A.f;
     const SliceTask t = f.tasks[blockIdx.x];
@@ -978,6 +987,7 @@ constexpr int kPcMaxRowCtb = 512;   // CTBs per row (8K width); alloc_hevc check
 
 // One wave per CTB: stable counting sort of its context bins by context index.
 __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ int cnt_s[4][kPcCtxOff];
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
@@ -1049,6 +1059,7 @@ __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
 // is-LPS). The CTBs holding the context are listed with the prefix of their counts; the
 // chain itself runs as up to 64 speculative segments, one per lane (below).
 __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint2 lst_s[4][kPcMaxRowCtb + 1];   // (cx | lo << 16, chain position of its first entry)
     __shared__ uint8_t nl_s[4][64];                // CABAC_NEXT_LPS
     const FrameArgs& f = A.f;
@@ -1152,6 +1163,7 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
 // One wave per CTB: the chunk's range map. Lane l follows the start ranges 256 + 4l .. +3
 // through the chunk's entries (bypass runs and terminating bins shift all of them alike).
 __global__ __launch_bounds__(256) void k_pc_rmap(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
     const int idx = blockIdx.x * 4 + w;
@@ -1222,6 +1234,7 @@ __global__ __launch_bounds__(256) void k_pc_rmap(HevcArgs A) {
 // One wave per CTB row: start range and stream bit offset of every chunk, one map
 // lookup each (a readlane); the maps of the next 8 CTBs are in flight.
 __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int cy = blockIdx.x, l = lane();
     const int row0 = cy * f.mb_w, nw = f.mb_w;
@@ -1265,6 +1278,7 @@ __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
 // flushed; bytes gathered in a VGPR (lane = 4 bytes) and stored every 256: the exclusive
 // ones into the row substream, the last two into the chunk's tail.
 __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
     const int idx = blockIdx.x * 4 + w;
@@ -1328,6 +1342,7 @@ __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
 // of it in a VGPR; carries run toward the start), writes the rbsp stop bit, then counts
 // the emulation-prevention bytes (same rule as k_hevc_ep_copy).
 __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int cy = blockIdx.x, l = lane();
     const int row0 = cy * f.mb_w;
@@ -1535,6 +1550,7 @@ __device__ __forceinline__ bool cu_intra_edge(const CuInfo& p, const CuInfo& q) 
     return p.mode == CU_INTRA || q.mode == CU_INTRA;
 }
 __global__ __launch_bounds__(256) void k_hevc_dbk_v(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const h264::gpu::FrameArgs& f = A.f;
     const int cw = f.mb_w, ch = f.mb_h, ne = cw - 1, nel = 2 * cw - 1;
     const int e = blockIdx.x * 256 + threadIdx.x;
@@ -1552,6 +1568,7 @@ __global__ __launch_bounds__(256) void k_hevc_dbk_v(HevcArgs A) {
 }
 
 __global__ __launch_bounds__(256) void k_hevc_dbk_h(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const h264::gpu::FrameArgs& f = A.f;
     const int cw = f.mb_w, ch = f.mb_h, ne = ch - 1, nel = 2 * ch - 1;
     if (nel <= 0) return;
@@ -1593,6 +1610,7 @@ __device__ __forceinline__ SaoPlane sao_plane_of(const FrameArgs& f, int c) {
 }
 
 __global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ SaoStats Sw[4][3];
     __shared__ SaoTables Tw[4];
     const FrameArgs& f = A.f;
@@ -1649,6 +1667,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
 
 // Merge-candidate distortions: one thread per (CTB, candidate) (sao_merge_dists).
 __global__ __launch_bounds__(256) void k_hevc_sao_md(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int t = blockIdx.x * 256 + threadIdx.x;
     if (t >= f.mb_w * f.mb_h * kSaoMd) return;
@@ -1665,6 +1684,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao_md(HevcArgs A) {
 // parameters and costs are staged in LDS by all lanes; lane 0 then walks the row left to
 // right (a merged CTB copies its left neighbour's final parameters) touching only LDS.
 __global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ long long md[kPcMaxRowCtb * kSaoMd];
     __shared__ SaoParams own[kPcMaxRowCtb];
     __shared__ long long cost[kPcMaxRowCtb];
@@ -1718,7 +1738,9 @@ __global__ __launch_bounds__(256) void k_hevc_sao_copy(HevcArgs A) {
     }
 }
 
-void launch_backend(const HevcArgs& a, hipStream_t s) {
+// CU coding, deblocking, SAO decisions and the CABAC substreams: everything the coded
+// size depends on (the K10 guard re-runs it, gated).
+static void launch_code(const HevcArgs& a, hipStream_t s) {
     const int n = a.f.mb_w * a.f.mb_h;
     hipLaunchKernelGGL(k_hevc_inter, dim3((n + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_intra_prep, dim3((n + 3) / 4), dim3(256), 0, s, a);
@@ -1743,9 +1765,23 @@ void launch_backend(const HevcArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_pc_compose, dim3(a.f.mb_h), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_pc_code, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_merge, dim3(a.f.mb_h), dim3(64), 0, s, a);
+}
+
+void launch_backend(const HevcArgs& a, hipStream_t s, int* redo) {
+    const int n = a.f.mb_w * a.f.mb_h;
+    launch_code(a, s);
+    if (redo) {   // K10 CBR per-frame cap: payload = the substream bytes (as k_rc_account)
+        HevcArgs b = a;
+        b.f.gate = redo;
+        for (int r = 0; r < h264::gpu::kMaxRecodes; r++) {
+            h264::gpu::launch_rc_guard_sizes(a.f, a.sub_size, a.f.mb_h, redo, r > 0, s);
+            launch_code(b, s);
+        }
+    }
     hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h), dim3(64), 0, s, a);
     // the SAO output becomes the reconstruction (k_commit copies it into the reference)
+    const int nq = (n + 3) / 4;
     hipLaunchKernelGGL(k_hevc_sao_apply, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sao_copy, dim3(nq), dim3(256), 0, s, a);
 }

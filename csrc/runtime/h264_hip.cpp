@@ -523,7 +523,8 @@ class HipBackend : public EncoderBackend {
         a.fs_mv = dmalloc<int16_t>(2 * nmb);
         {   // K10 rate control state (ratecontrol.h), initialised like the CPU controller's
             RcState rc;
-            rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms);
+            rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms,
+                    rc_qp_min_for(cfg_.codec));
             a.rc = dmalloc<RcState>(1);
             copy_now(a.rc, &rc, sizeof(rc));
             a.rc_slice = dmalloc<long long>(2 * (size_t)ns);
@@ -641,7 +642,7 @@ class HipBackend : public EncoderBackend {
                 aa.frame_host = av1_frame_dev_[parity_];
                 aa.out_host = av1_out_dev_[parity_];
                 aa.out_size_host = av1_size_dev_[parity_];
-                av1::gpu::launch_backend(aa, stream_);
+                av1::gpu::launch_backend(aa, stream_, graph_guard_ ? args_.rc_redo : nullptr);
                 gpu::launch_rc_account(args_, aa.tile_size, av1_geo_.tile_cols * av1_geo_.tile_rows, 1, 0, stream_);
             } else if (cfg_.codec == 1) {
                 gpu::launch_frontend(args_, stream_);
@@ -650,7 +651,7 @@ class HipBackend : public EncoderBackend {
                 ha.out_host = hevc_out_dev_[parity_];
                 ha.out_size = hevc_size_dev_[parity_];
                 ha.out_dev = hevc_fallback_[parity_];
-                hevc::gpu::launch_backend(ha, stream_);
+                hevc::gpu::launch_backend(ha, stream_, graph_guard_ ? args_.rc_redo : nullptr);
                 gpu::launch_rc_account(args_, ha.sub_size, g_.mb_h, 1, 0, stream_);
             } else {
                 gpu::launch_encode(args_, stream_, graph_guard_);

@@ -133,8 +133,24 @@ def test_gpu_cbr_guard_matches_cpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("codec", ["hevc", "av1"])
 def test_gpu_rate_control_matches_cpu_fullframe(codec):
-    _parity(codec, "cbr", 600, 30)
+    """HEVC / AV1 CBR on the HIP encoder: the per-frame cap's gated re-code passes
+    (k_rc_guard_sizes + the coding kernels again) reproduce the CPU encoder's second and
+    third codings byte for byte."""
+    st = _parity(codec, "cbr", 480, 90)
+    assert st["redos"] > 0
     _parity(codec, "crf", 0, 20)
+
+
+@pytest.mark.parametrize("codec", ["hevc", "av1"])
+@pytest.mark.parametrize("content", ["motion", "desktop"])
+def test_cbr_frame_cap_hevc_av1_cpu(codec, content):
+    """The per-frame cap (ratecontrol.h rc_frame_cap) on the full-frame encoders: no
+    non-key frame above 1.5 budgets - AV1 included, whose 120 ms buffer alone would
+    allow 7 - and the mean rate near the target."""
+    r = _trace(backend="cpu", codec=codec, width=320, height=192, frames=150, content=content, mode="cbr", kbps=480)
+    assert r["nonkey_over_1p5"] == 0, r
+    assert 0.85 <= r["rate_ratio"] <= 1.10, r
+    assert r["redos"] > 0, r
 
 
 def test_av1_cbr_holds_its_budget_cpu():
