@@ -24,8 +24,7 @@ void Controller::init(const EncoderConfig& cfg, const Geometry& g) {
     g_ = g;
     st_.assign(g.num_slices, StripeState());
     pic_ = StripeState();
-    rc_init(rc_, cfg.rc_mode, cfg.qp, cfg.bitrate_kbps, cfg.fps, cfg.width * cfg.height, cfg.vbv_ms,
-            rc_qp_min_for(cfg.codec));
+    rc_init(rc_, cfg.rc_mode, cfg.qp, cfg.bitrate_kbps, cfg.fps, cfg.width * cfg.height, cfg.vbv_ms, cfg.codec);
 }
 
 void Controller::rate_control(SliceTask* tasks, const MeResult* me) {

@@ -66,8 +66,45 @@ void CpuH264Encoder::set_overlay_pos(int slot, int on, int x, int y, int tdx, in
     o.tdy = tdy > 0 ? tdy : 0;
 }
 
+// K3: per-MB damage against the previous source, per-stripe dirty flags.
+void CpuH264Encoder::detect_damage() {
+    std::fill(stripe_dirty.begin(), stripe_dirty.end(), 0);
+    for (int mby = 0; mby < g.mb_h; mby++)
+        for (int mbx = 0; mbx < g.mb_w; mbx++) {
+            bool d = first_frame;
+            for (int y = 0; y < 16 && !d; y++) {
+                size_t o = (size_t)(mby * 16 + y) * g.stride_y + mbx * 16;
+                d = memcmp(&src[0][o], &prev[0][o], 16) != 0;
+            }
+            for (int p = 1; p < 3 && !d; p++)
+                for (int y = 0; y < 8 && !d; y++) {
+                    size_t o = (size_t)(mby * 8 + y) * g.stride_c + mbx * 8;
+                    d = memcmp(&src[p][o], &prev[p][o], 8) != 0;
+                }
+            mb_dirty[mby * g.mb_w + mbx] = d;
+            if (d) stripe_dirty[mby / g.rows_per_slice] = 1;
+        }
+}
+
+void CpuH264Encoder::load_frame_yuv() {
+    const int W = g.W, H = g.H;
+    for (int y = 0; y < g.plane_h_y; y++)
+        for (int x = 0; x < g.stride_y; x++)
+            src[0][(size_t)y * g.stride_y + x] = yuv_sample(yuv_in.fmt, yuv_in.p, yuv_in.stride, 0, x, y, W, H);
+    for (int c = 1; c < 3; c++)
+        for (int y = 0; y < g.plane_h_c; y++)
+            for (int x = 0; x < g.stride_c; x++)
+                src[c][(size_t)y * g.stride_c + x] = yuv_sample(yuv_in.fmt, yuv_in.p, yuv_in.stride, c, x, y, W, H);
+}
+
 void CpuH264Encoder::load_frame(const uint8_t* bgrx, int stride) {
     const int W = g.W, H = g.H;
+    if (yuv_in.fmt != YUV_NONE) {   // planar input: no K1, straight to the damage pass
+        load_frame_yuv();
+        yuv_in.fmt = YUV_NONE;
+        detect_damage();
+        return;
+    }
     const bool ov = overlay[0].on || overlay[1].on;
     const uint8_t* ovimg[kOverlaySlots] = {overlay_img[0].data(), overlay_img[1].data()};
     for (int qy = 0; qy < g.plane_h_c; qy++) {
@@ -111,22 +148,7 @@ void CpuH264Encoder::load_frame(const uint8_t* bgrx, int stride) {
             src[2][(size_t)qy * g.stride_c + qx] = cr;
         }
     }
-    std::fill(stripe_dirty.begin(), stripe_dirty.end(), 0);
-    for (int mby = 0; mby < g.mb_h; mby++)
-        for (int mbx = 0; mbx < g.mb_w; mbx++) {
-            bool d = first_frame;
-            for (int y = 0; y < 16 && !d; y++) {
-                size_t o = (size_t)(mby * 16 + y) * g.stride_y + mbx * 16;
-                d = memcmp(&src[0][o], &prev[0][o], 16) != 0;
-            }
-            for (int p = 1; p < 3 && !d; p++)
-                for (int y = 0; y < 8 && !d; y++) {
-                    size_t o = (size_t)(mby * 8 + y) * g.stride_c + mbx * 8;
-                    d = memcmp(&src[p][o], &prev[p][o], 8) != 0;
-                }
-            mb_dirty[mby * g.mb_w + mbx] = d;
-            if (d) stripe_dirty[mby / g.rows_per_slice] = 1;
-        }
+    detect_damage();
 }
 
 int CpuH264Encoder::sad_at(int mbx, int mby, int dx, int dy, const SliceTask& t, int refi) const {

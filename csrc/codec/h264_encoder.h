@@ -317,7 +317,7 @@ class Controller {
     // K10: mode (RC_CQP / RC_CRF / RC_CBR) and CBR bitrate from the next frame on.
     void set_rate(int mode, int kbps) {
         const RcState old = rc_;
-        rc_init(rc_, mode, cfg_.qp, kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms, old.qp_min);
+        rc_init(rc_, mode, cfg_.qp, kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms, old.codec);
         if (old.mode == mode) {   // keep the model; a new budget recentres the buffer
             for (int k = 0; k < 2; k++) {
                 rc_.last_qp[k] = old.last_qp[k];

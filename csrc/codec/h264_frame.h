@@ -46,6 +46,25 @@ SK_HD bool subpel_hit(int best_sad, int int_sad) { return best_sad * 8 <= int_sa
 SK_HD int me_qx(const MeResult& r) { return 4 * r.mvx + r.fx; }
 SK_HD int me_qy(const MeResult& r) { return 4 * r.mvy + r.fy; }
 
+enum YuvFormat : int32_t { YUV_NONE = 0, YUV_I420 = 1, YUV_NV12 = 2 };
+struct YuvInput {
+    int32_t fmt;
+    const uint8_t* p[3];
+    int32_t stride[3];
+};
+
+// Sample of a planar 4:2:0 input at clamped coordinates (edge padding repeats the last
+// row / column, as the BGRx path does): plane 0 luma, 1 Cb, 2 Cr.
+SK_HD uint8_t yuv_sample(int fmt, const uint8_t* const* p, const int32_t* stride, int plane, int x, int y, int W,
+                         int H) {
+    if (plane == 0) return p[0][(size_t)sk_min(y, H - 1) * stride[0] + sk_min(x, W - 1)];
+    const int cw = (W + 1) >> 1, ch = (H + 1) >> 1;
+    x = sk_min(x, cw - 1);
+    y = sk_min(y, ch - 1);
+    if (fmt == YUV_NV12) return p[1][(size_t)y * stride[1] + 2 * x + (plane - 1)];
+    return p[plane][(size_t)y * stride[plane] + x];
+}
+
 class CpuH264Encoder {
    public:
     explicit CpuH264Encoder(const EncoderConfig& cfg);
@@ -56,7 +75,9 @@ class CpuH264Encoder {
                 std::vector<EncodedPacket>& out);
 
     // ---- stages (public for tests) ----
-    void load_frame(const uint8_t* bgrx, int stride_bytes);  // K1 + K3
+    void load_frame(const uint8_t* bgrx, int stride_bytes);  // K1 + K3 (or yuv_in: K3 only)
+    void load_frame_yuv();                                  // planar input: edge padding
+    void detect_damage();                                   // K3 on src against prev
     void motion_search(int s);                              // K4 for slice s
     void intra_activity(int s);                             // planned intra slice: MB activity only
     int mb_activity(int mbx, int mby) const;
@@ -92,6 +113,11 @@ class CpuH264Encoder {
     bool first_frame = true;
     bool scaled_ = false;          // K2: capture resampled to width x height
     ScaleParams scale_ = {};
+    // Planar 4:2:0 input (GStreamer NV12 / I420 caps): the next load_frame() takes these
+    // planes instead of BGRx (no colour conversion, no overlays, no resampling); fmt 0:
+    // none. Planes of W x H luma and ((W + 1) / 2) x ((H + 1) / 2) chroma; I420 p[1] / p[2]
+    // = U / V, NV12 p[1] = interleaved UV.
+    YuvInput yuv_in = {};
     // K12/K13 overlays (watermark, cursor) blended inside load_frame
     OverlayParams overlay[kOverlaySlots] = {};
     std::vector<uint8_t> overlay_img[kOverlaySlots];

@@ -25,9 +25,12 @@ namespace h264 {
 
 enum RcMode : int32_t { RC_CQP = 0, RC_CRF = 1, RC_CBR = 2 };
 
-// Re-code passes the HEVC / AV1 encoders may add to a frame over its per-frame cap
-// (H.264 adds one: its CAVLC pass is cheap and its model overshoots less).
+// Re-code passes an encoder may add to a frame over its per-frame cap (rc_redo_step):
+// HEVC two (a scene cut coded at QP 0 needs ~26 QP), H.264 and AV1 one (AV1 sits at the
+// top of its quantiser range on 4K120 content, where a further pass rarely gains, and a
+// third 4K pass would cost the frame interval).
 constexpr int kMaxRecodes = 2;
+SK_HD int rc_max_recodes(int codec) { return codec == 1 ? 2 : 1; }
 
 struct RcState {
     int32_t mode, base_qp, qp_min, qp_max;
@@ -56,8 +59,9 @@ struct RcState {
     int32_t cur_redo;        // re-code passes of the frame in flight (rc_redo)
     int32_t redo_qpf;        // ... the fractional QP and payload bits of its pass before the
     int32_t redo_bits;       //     last one (valid when cur_redo > 0)
+    int32_t codec;           // EncoderConfig::codec (rc_qp_min_for, rc_redo_step)
 };
-static_assert(sizeof(RcState) == 144, "RcState layout");
+static_assert(sizeof(RcState) == 148, "RcState layout");
 
 SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x <= 1
     if (x <= 1) return 0;
@@ -69,15 +73,22 @@ SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x
 // vbv_ms: the CBR buffer. 0 = 1.5 frame intervals, the reference's low-latency
 // setting for its H.264 / H.265 encoders (legacy/gstwebrtc_app.py:100-104); AV1
 // passes 120 ms, svtav1enc's buf-optimal-sz (gstwebrtc_app.py:738).
-// qp_min: the finest QP the controller picks (rc_qp_min_for).
+// Finest controller QP per codec (EncoderConfig::codec). H.264 stops at 10. HEVC goes
+// down to 0 like x265's qpmin: its transform skip and residual quadtree code a desktop
+// at QP 10 in ~0.65 of a 16 Mbit/s 1080p60 budget, so CBR needs finer QPs to reach the
+// rate (the per-frame guard bounds what a burst coded that fine costs).
+SK_HD int rc_qp_min_for(int codec) { return codec == 1 ? 0 : 10; }
+
+// codec: EncoderConfig::codec (0 H.264, 1 HEVC, 2 AV1).
 SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float fps, int pixels, int vbv_ms = 0,
-                   int qp_min = 10) {
+                   int codec = 0) {
     rc = RcState{};
     rc.vbv_ms = vbv_ms;
     rc.pixels = pixels;
     rc.mode = mode;
     rc.base_qp = base_qp;
-    rc.qp_min = qp_min;
+    rc.codec = codec;
+    rc.qp_min = rc_qp_min_for(codec);
     rc.qp_max = 51;
     const double f = fps > 0 ? fps : 60.0;
     rc.budget = (int32_t)(bitrate_kbps * 1000.0 / f);
@@ -91,11 +102,6 @@ SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float f
 
 SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, rc.qp_max); }
 
-// Finest controller QP per codec (EncoderConfig::codec). H.264 stops at 10. HEVC goes
-// down to 0 like x265's qpmin: its transform skip and residual quadtree code a desktop
-// at QP 10 in ~0.65 of a 16 Mbit/s 1080p60 budget, so CBR needs finer QPs to reach the
-// rate (the per-frame guard bounds what a burst coded that fine costs).
-SK_HD int rc_qp_min_for(int codec) { return codec == 1 ? 0 : 10; }
 
 // Per-frame cap of a non-key frame: the VBV (1.5 frame intervals, the reference's
 // x264enc / x265enc setting, legacy/gstwebrtc_app.py:101-105, 633) and never above 1.5
@@ -144,8 +150,11 @@ SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intr
         int target = rc.budget + (rc.vbv_size / 2 - rc.fullness) / 4;
         // key frames (IDR) may use 3 budgets and are paid back by the frames after
         // them; every other frame, scene-cut intra pictures included, stays under 1.25x
+        // (a long buffer, AV1's 120 ms: 1.125x, its frames vary +-30 % at one qindex and
+        // the per-frame cap is 1.5 budgets; aiming at 1.25x re-coded every 4th frame of
+        // the 4K120 bench content)
         if (idr) target = sk_max(target, 3 * rc.budget);
-        else target = sk_min(target, rc.budget + rc.budget / 4);
+        else target = sk_min(target, rc.budget + (rc.vbv_ms > 0 ? rc.budget / 8 : rc.budget / 4));
         target = sk_max(target, rc.budget / 4);
         if (target < 64) target = 64;
         if (rc.last_bits[k] > 0) {
@@ -222,6 +231,11 @@ SK_HD int rc_dither_qp(int qpf, int i) {
 // frames pay it back.
 SK_HD int rc_redo_step(const RcState& rc, long long frame_bits) {
     if (rc.mode != RC_CBR || !rc.cur_valid) return 0;
+    // HEVC / AV1 key frames are not re-coded: their intra pass is the longest of the
+    // picture (a second one doubled the 4K key-frame latency); the frames after a key
+    // frame pay its overshoot back through the buffer, as they pay its planned 3 budgets
+    if (rc.cur_idr && rc.codec != 0) return 0;
+    if (rc.cur_redo >= rc_max_recodes(rc.codec)) return 0;
     const long long cap = rc_frame_cap(rc, rc.cur_idr != 0);
     if (frame_bits <= cap) return 0;
     const uint32_t b = (uint32_t)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);

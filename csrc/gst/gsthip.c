@@ -1,40 +1,41 @@
 /* libgsthip: GStreamer 1.x elements over the gfx950 media engine (libselkies_native.so).
  *
- *   hiph264enc  H.264 Constrained Baseline (CAVLC), slices of stripe-height rows
- *   hiph265enc  HEVC Main (CABAC, WPP), slices of CTB rows
- *   hipav1enc   AV1 Main 8-bit 4:2:0 (tiles), OBU temporal units
- *   hipconvert  BGRx / BGRA -> I420 (BT.709, the encoders' K1 colour conversion)
+ *   hiph264enc     H.264 Constrained Baseline (CAVLC), slices of stripe-height rows
+ *   hiph265enc     HEVC Main (CABAC, WPP), slices of CTB rows
+ *   hipav1enc      AV1 Main 8-bit 4:2:0 (tiles), OBU temporal units
+ *   hipconvert     BGRx / BGRA -> I420 / NV12 (BT.709, the encoders' K1 colour conversion)
+ *   hipupload      system memory -> memory:HIPMemory      (gsthipmemory.c)
+ *   hipdownload    memory:HIPMemory -> system memory
+ *   hipximagesrc   X11 MIT-SHM screen source              (gsthipximagesrc.c)
  *
- * The encoders are GstVideoEncoder subclasses taking BGRx / BGRA (what ximagesrc and
- * the capture path deliver); conversion to 4:2:0 is fused into the encoder's first
- * kernel, so a pipeline needs no videoconvert in front of them. They replace the
- * reference's encoder elements in its GStreamer graph (legacy/gstwebrtc_app.py:
- * 200-1001, x264enc / nvh264enc / vah264enc at :352-663, x265enc at :667-683,
- * svtav1enc / av1enc / rav1enc at :724-783) with the reference's property names:
- * bitrate (kbit/s), key-int-max (gop-size alias), rate-control, qp, plus
- * backend=auto|cpu|hip and device. Output buffers are byte-stream access units
- * (Annex B for H.264 / H.265, low-overhead OBUs for AV1): the native encoder's packet
- * minus its 10-byte stripe header, byte for byte.
+ * The encoders are GstVideoEncoder subclasses taking BGRx / BGRA (what ximagesrc and the
+ * capture path deliver; conversion to 4:2:0 is fused into the encoder's first kernel)
+ * or I420 / NV12 (what `videoconvert ! video/x-raw,format=NV12` hands x264enc in the
+ * reference, legacy/gstwebrtc_app.py:611-617), each in system memory or in
+ * memory:HIPMemory (`hipupload ! hipconvert ! video/x-raw(memory:HIPMemory),format=NV12
+ * ! hiph264enc`, the reference's cudaupload / cudaconvert / nvh264enc chain at :261-284:
+ * the frame crosses PCIe once). They replace the reference's encoder elements in its
+ * GStreamer graph (legacy/gstwebrtc_app.py:200-1001, x264enc / nvh264enc / vah264enc at
+ * :352-663, x265enc at :667-683, svtav1enc / av1enc / rav1enc at :724-783) with the
+ * reference's property names: bitrate (kbit/s), key-int-max (gop-size alias),
+ * rate-control, qp, plus backend=auto|cpu|hip and device. Output buffers are
+ * byte-stream access units (Annex B for H.264 / H.265, low-overhead OBUs for AV1): the
+ * native encoder's packet minus its 10-byte stripe header, byte for byte.
  */
-#include <gst/gst.h>
-#include <gst/base/gstbasetransform.h>
-#include <gst/video/video.h>
-#include <gst/video/gstvideoencoder.h>
-#include <string.h>
+#include "gsthip.h"
 
-#include "../runtime/sk_api.h"
+#include <string.h>
 
 #define PACKAGE "selkies-mi355x"
 #define VERSION "0.1"
 
-GST_DEBUG_CATEGORY_STATIC(gst_hip_debug);
+GST_DEBUG_CATEGORY(gst_hip_debug);
 #define GST_CAT_DEFAULT gst_hip_debug
 
 /* ------------------------------------------------------------------ enums */
-typedef enum { HIP_BACKEND_AUTO = 0, HIP_BACKEND_CPU = 1, HIP_BACKEND_HIP = 2 } GstHipBackend;
 typedef enum { HIP_RC_CQP = 0, HIP_RC_CRF = 1, HIP_RC_CBR = 2 } GstHipRateControl;
 
-static GType gst_hip_backend_get_type(void) {
+GType gst_hip_backend_get_type(void) {
     static gsize id = 0;
     static const GEnumValue values[] = {
         {HIP_BACKEND_AUTO, "HIP when a device is present, else the CPU reference", "auto"},
@@ -56,7 +57,7 @@ static GType gst_hip_rate_control_get_type(void) {
     return (GType)id;
 }
 
-static int resolve_backend(int b) {
+int gst_hip_resolve_backend(int b) {
     if (b == HIP_BACKEND_CPU) return 0;
     if (b == HIP_BACKEND_HIP) return 1;
     return sk_hip_device_count() > 0 ? 1 : 0;
@@ -199,7 +200,7 @@ static gboolean hipenc_set_format(GstVideoEncoder* e, GstVideoCodecState* state)
                 ? (float)GST_VIDEO_INFO_FPS_N(info) / (float)GST_VIDEO_INFO_FPS_D(info)
                 : 60.f;
     c.device = s->device;
-    c.backend = resolve_backend(s->backend);
+    c.backend = gst_hip_resolve_backend(s->backend);
     c.codec = codec;
     c.tile_cols_log2 = c.tile_rows_log2 = -1;
     c.rc_mode = hipenc_rc_mode(s);
@@ -221,6 +222,9 @@ static gboolean hipenc_set_format(GstVideoEncoder* e, GstVideoCodecState* state)
 
     GstCaps* caps = hipenc_src_caps(codec);
     GstVideoCodecState* out = gst_video_encoder_set_output_state(e, caps, state);
+    /* the coded size (odd input sizes lose their last column / row) */
+    out->info.width = c.width;
+    out->info.height = c.height;
     gst_video_codec_state_unref(out);
     /* one frame in, one access unit out: no reordering; latency of one frame interval */
     GstClockTime lat = gst_util_uint64_scale_int(GST_SECOND, GST_VIDEO_INFO_FPS_D(info) > 0 ? GST_VIDEO_INFO_FPS_D(info) : 1,
@@ -229,9 +233,47 @@ static gboolean hipenc_set_format(GstVideoEncoder* e, GstVideoCodecState* state)
     return gst_video_encoder_negotiate(e);
 }
 
+/* One frame through the native encoder: BGRx / BGRA or I420 / NV12 planes, from
+ * device pointers when the buffer is HIPMemory and the encoder runs on HIP (no host
+ * copy), else from a host map (HIPMemory maps stage a copy). Returns the packet count. */
+static int hipenc_encode_buffer(GstHipEnc* s, GstBuffer* buf) {
+    const GstVideoInfo* info = &s->in_state->info;
+    const GstVideoFormat fmt = GST_VIDEO_INFO_FORMAT(info);
+    const gboolean planar = fmt == GST_VIDEO_FORMAT_I420 || fmt == GST_VIDEO_FORMAT_NV12;
+    const int yfmt = fmt == GST_VIDEO_FORMAT_NV12 ? 2 : 1;
+    gint dev = -1;
+    guint8* d = gst_hip_resolve_backend(s->backend) == 1 ? gst_hip_buffer_device_ptr(buf, &dev) : NULL;
+    if (d && dev == s->device) {
+        gsize off[GST_VIDEO_MAX_PLANES];
+        gint st[GST_VIDEO_MAX_PLANES];
+        gst_hip_buffer_planes(buf, info, off, st);
+        if (!planar) return sk_h264_encode(s->enc, d + off[0], st[0], s->frame_id++);
+        return sk_h264_encode_yuv(s->enc, yfmt, d + off[0], st[0], d + off[1], st[1],
+                                  yfmt == 1 ? d + off[2] : NULL, yfmt == 1 ? st[2] : 0, 1, s->frame_id++);
+    }
+    GstVideoFrame vf;
+    if (!gst_video_frame_map(&vf, info, buf, GST_MAP_READ)) return -2;   /* -2: not mappable */
+    int n;
+    if (!planar) {
+        n = sk_h264_encode(s->enc, (const uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&vf, 0),
+                           GST_VIDEO_FRAME_PLANE_STRIDE(&vf, 0), s->frame_id++);
+    } else {
+        n = sk_h264_encode_yuv(s->enc, yfmt, (const uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&vf, 0),
+                               GST_VIDEO_FRAME_PLANE_STRIDE(&vf, 0), (const uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&vf, 1),
+                               GST_VIDEO_FRAME_PLANE_STRIDE(&vf, 1),
+                               yfmt == 1 ? (const uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&vf, 2) : NULL,
+                               yfmt == 1 ? GST_VIDEO_FRAME_PLANE_STRIDE(&vf, 2) : 0, 0, s->frame_id++);
+    }
+    gst_video_frame_unmap(&vf);
+    return n;
+}
+
 static GstFlowReturn hipenc_handle_frame(GstVideoEncoder* e, GstVideoCodecFrame* frame) {
     GstHipEnc* s = HIPENC(e);
     if (!s->enc || !s->in_state) {
+        /* finish_frame without an output buffer is how 1.14 drops a frame (and releases
+         * it); the error stops the stream */
+        GST_ELEMENT_ERROR(s, CORE, NEGOTIATION, ("no encoder: caps were never set"), (NULL));
         gst_video_encoder_finish_frame(e, frame);
         return GST_FLOW_NOT_NEGOTIATED;
     }
@@ -247,14 +289,12 @@ static GstFlowReturn hipenc_handle_frame(GstVideoEncoder* e, GstVideoCodecFrame*
     if (GST_VIDEO_CODEC_FRAME_IS_FORCE_KEYFRAME(frame) || (kim > 0 && s->since_key >= kim))
         sk_h264_request_keyframe(s->enc);
 
-    GstVideoFrame vf;
-    if (!gst_video_frame_map(&vf, &s->in_state->info, frame->input_buffer, GST_MAP_READ)) {
+    const int n = hipenc_encode_buffer(s, frame->input_buffer);
+    if (n == -2) {
+        GST_ELEMENT_ERROR(s, STREAM, ENCODE, ("cannot map the input frame"), (NULL));
         gst_video_encoder_finish_frame(e, frame);
         return GST_FLOW_ERROR;
     }
-    const int n = sk_h264_encode(s->enc, (const uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&vf, 0),
-                                 GST_VIDEO_FRAME_PLANE_STRIDE(&vf, 0), s->frame_id++);
-    gst_video_frame_unmap(&vf);
     if (n < 0) {
         GST_ELEMENT_ERROR(s, STREAM, ENCODE, ("encode failed"), ("%s", sk_last_error()));
         gst_video_encoder_finish_frame(e, frame);
@@ -355,7 +395,9 @@ static void hipenc_class_init(gpointer klass, gpointer data) {
         g_param_spec_uint("stripe-height", "Stripe height", "Rows per slice (multiple of 16)", 16, 4096, 64, rw));
 
     GstCaps* sink = gst_caps_from_string(
-        "video/x-raw, format=(string){ BGRx, BGRA }, width=(int)[ 16, 8192 ], height=(int)[ 16, 8192 ], "
+        "video/x-raw(" GST_CAPS_FEATURE_MEMORY_HIP "), format=(string)" GST_HIP_RAW_FORMATS ", "
+        "width=(int)[ 16, 8192 ], height=(int)[ 16, 8192 ], framerate=(fraction)[ 0/1, MAX ]; "
+        "video/x-raw, format=(string)" GST_HIP_RAW_FORMATS ", width=(int)[ 16, 8192 ], height=(int)[ 16, 8192 ], "
         "framerate=(fraction)[ 0/1, MAX ]");
     gst_element_class_add_pad_template(ec, gst_pad_template_new("sink", GST_PAD_SINK, GST_PAD_ALWAYS, sink));
     gst_caps_unref(sink);
@@ -363,11 +405,12 @@ static void hipenc_class_init(gpointer klass, gpointer data) {
     gst_element_class_add_pad_template(ec, gst_pad_template_new("src", GST_PAD_SRC, GST_PAD_ALWAYS, src));
     gst_caps_unref(src);
     gst_element_class_set_static_metadata(ec, kEncLong[codec], "Codec/Encoder/Video/Hardware",
-                                          "Encodes BGRx frames on the MI355X (gfx950) media kernels",
+                                          "Encodes BGRx / I420 / NV12 frames (system or HIP memory) on the MI355X "
+                                          "(gfx950) media kernels",
                                           "selkies-mi355x");
 }
 
-static GType hipenc_register(int codec) {
+GType gst_hip_enc_register(int codec) {
     GTypeInfo info;
     memset(&info, 0, sizeof(info));
     info.class_size = sizeof(GstHipEncClass);
@@ -379,163 +422,17 @@ static GType hipenc_register(int codec) {
     return g_type_register_static(GST_TYPE_VIDEO_ENCODER, tnames[codec], &info, (GTypeFlags)0);
 }
 
-/* ------------------------------------------------------------------ hipconvert */
-typedef struct {
-    GstBaseTransform parent;
-    void* conv;
-    gint backend, device;
-    GstVideoInfo in_info, out_info;
-} GstHipConvert;
-typedef struct {
-    GstBaseTransformClass parent_class;
-} GstHipConvertClass;
-
-enum { CPROP_0, CPROP_BACKEND, CPROP_DEVICE };
-static GstBaseTransformClass* hipconv_parent_class = NULL;
-
-static void hipconv_set_property(GObject* obj, guint id, const GValue* v, GParamSpec* ps) {
-    GstHipConvert* s = (GstHipConvert*)obj;
-    switch (id) {
-        case CPROP_BACKEND: s->backend = g_value_get_enum(v); break;
-        case CPROP_DEVICE: s->device = g_value_get_int(v); break;
-        default: G_OBJECT_WARN_INVALID_PROPERTY_ID(obj, id, ps); break;
-    }
-}
-static void hipconv_get_property(GObject* obj, guint id, GValue* v, GParamSpec* ps) {
-    GstHipConvert* s = (GstHipConvert*)obj;
-    switch (id) {
-        case CPROP_BACKEND: g_value_set_enum(v, s->backend); break;
-        case CPROP_DEVICE: g_value_set_int(v, s->device); break;
-        default: G_OBJECT_WARN_INVALID_PROPERTY_ID(obj, id, ps); break;
-    }
-}
-
-static GstCaps* hipconv_transform_caps(GstBaseTransform* t, GstPadDirection dir, GstCaps* caps, GstCaps* filter) {
-    (void)t;
-    GstCaps* res = gst_caps_new_empty();
-    for (guint i = 0; i < gst_caps_get_size(caps); i++) {
-        GstStructure* st = gst_structure_copy(gst_caps_get_structure(caps, i));
-        if (dir == GST_PAD_SINK) {
-            gst_structure_set(st, "format", G_TYPE_STRING, "I420", NULL);
-        } else {
-            GValue list = G_VALUE_INIT, v = G_VALUE_INIT;
-            g_value_init(&list, GST_TYPE_LIST);
-            g_value_init(&v, G_TYPE_STRING);
-            g_value_set_string(&v, "BGRx");
-            gst_value_list_append_value(&list, &v);
-            g_value_set_string(&v, "BGRA");
-            gst_value_list_append_value(&list, &v);
-            gst_structure_take_value(st, "format", &list);
-            g_value_unset(&v);
-        }
-        gst_structure_remove_fields(st, "colorimetry", "chroma-site", NULL);
-        res = gst_caps_merge_structure(res, st);
-    }
-    if (filter) {
-        GstCaps* f = gst_caps_intersect_full(filter, res, GST_CAPS_INTERSECT_FIRST);
-        gst_caps_unref(res);
-        res = f;
-    }
-    return res;
-}
-
-static gboolean hipconv_set_caps(GstBaseTransform* t, GstCaps* in, GstCaps* out) {
-    GstHipConvert* s = (GstHipConvert*)t;
-    if (!gst_video_info_from_caps(&s->in_info, in) || !gst_video_info_from_caps(&s->out_info, out)) return FALSE;
-    if (GST_VIDEO_INFO_WIDTH(&s->in_info) != GST_VIDEO_INFO_WIDTH(&s->out_info) ||
-        GST_VIDEO_INFO_HEIGHT(&s->in_info) != GST_VIDEO_INFO_HEIGHT(&s->out_info))
-        return FALSE;
-    if (s->conv) sk_convert_destroy(s->conv);
-    s->conv = sk_convert_create(GST_VIDEO_INFO_WIDTH(&s->in_info), GST_VIDEO_INFO_HEIGHT(&s->in_info), 0,
-                                resolve_backend(s->backend), s->device);
-    if (!s->conv) {
-        GST_ELEMENT_ERROR(s, LIBRARY, INIT, ("converter init failed"), ("%s", sk_last_error()));
-        return FALSE;
-    }
-    return TRUE;
-}
-
-static GstFlowReturn hipconv_transform(GstBaseTransform* t, GstBuffer* inbuf, GstBuffer* outbuf) {
-    GstHipConvert* s = (GstHipConvert*)t;
-    GstVideoFrame fi, fo;
-    if (!gst_video_frame_map(&fi, &s->in_info, inbuf, GST_MAP_READ)) return GST_FLOW_ERROR;
-    if (!gst_video_frame_map(&fo, &s->out_info, outbuf, GST_MAP_WRITE)) {
-        gst_video_frame_unmap(&fi);
-        return GST_FLOW_ERROR;
-    }
-    const int rc = sk_convert_run(s->conv, (const uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&fi, 0),
-                                  GST_VIDEO_FRAME_PLANE_STRIDE(&fi, 0), (uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&fo, 0),
-                                  GST_VIDEO_FRAME_PLANE_STRIDE(&fo, 0), (uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&fo, 1),
-                                  GST_VIDEO_FRAME_PLANE_STRIDE(&fo, 1), (uint8_t*)GST_VIDEO_FRAME_PLANE_DATA(&fo, 2),
-                                  GST_VIDEO_FRAME_PLANE_STRIDE(&fo, 2));
-    gst_video_frame_unmap(&fo);
-    gst_video_frame_unmap(&fi);
-    return rc == 0 ? GST_FLOW_OK : GST_FLOW_ERROR;
-}
-
-static gboolean hipconv_stop(GstBaseTransform* t) {
-    GstHipConvert* s = (GstHipConvert*)t;
-    if (s->conv) sk_convert_destroy(s->conv);
-    s->conv = NULL;
-    return TRUE;
-}
-
-static void hipconv_init(GTypeInstance* inst, gpointer klass) {
-    (void)klass;
-    GstHipConvert* s = (GstHipConvert*)inst;
-    s->conv = NULL;
-    s->backend = HIP_BACKEND_AUTO;
-    s->device = 0;
-}
-
-static void hipconv_class_init(gpointer klass, gpointer data) {
-    (void)data;
-    GObjectClass* oc = G_OBJECT_CLASS(klass);
-    GstElementClass* ec = GST_ELEMENT_CLASS(klass);
-    GstBaseTransformClass* bc = GST_BASE_TRANSFORM_CLASS(klass);
-    hipconv_parent_class = (GstBaseTransformClass*)g_type_class_peek_parent(klass);
-    oc->set_property = hipconv_set_property;
-    oc->get_property = hipconv_get_property;
-    bc->transform_caps = hipconv_transform_caps;
-    bc->set_caps = hipconv_set_caps;
-    bc->transform = hipconv_transform;
-    bc->stop = hipconv_stop;
-    bc->passthrough_on_same_caps = FALSE;
-    const GParamFlags rw = (GParamFlags)(G_PARAM_READWRITE | G_PARAM_STATIC_STRINGS);
-    g_object_class_install_property(oc, CPROP_BACKEND,
-        g_param_spec_enum("backend", "Backend", "Conversion back end", gst_hip_backend_get_type(), HIP_BACKEND_AUTO, rw));
-    g_object_class_install_property(oc, CPROP_DEVICE, g_param_spec_int("device", "Device", "HIP device ordinal", 0, 63, 0, rw));
-    GstCaps* sink = gst_caps_from_string(
-        "video/x-raw, format=(string){ BGRx, BGRA }, width=(int)[ 2, 8192 ], height=(int)[ 2, 8192 ], "
-        "framerate=(fraction)[ 0/1, MAX ]");
-    GstCaps* src = gst_caps_from_string(
-        "video/x-raw, format=(string)I420, width=(int)[ 2, 8192 ], height=(int)[ 2, 8192 ], "
-        "framerate=(fraction)[ 0/1, MAX ]");
-    gst_element_class_add_pad_template(ec, gst_pad_template_new("sink", GST_PAD_SINK, GST_PAD_ALWAYS, sink));
-    gst_element_class_add_pad_template(ec, gst_pad_template_new("src", GST_PAD_SRC, GST_PAD_ALWAYS, src));
-    gst_caps_unref(sink);
-    gst_caps_unref(src);
-    gst_element_class_set_static_metadata(ec, "BGRx to I420 converter (gfx950 HIP)", "Filter/Converter/Video/Hardware",
-                                          "BT.709 limited-range colour conversion on the MI355X", "selkies-mi355x");
-}
-
-static GType hipconv_register(void) {
-    GTypeInfo info;
-    memset(&info, 0, sizeof(info));
-    info.class_size = sizeof(GstHipConvertClass);
-    info.class_init = hipconv_class_init;
-    info.instance_size = sizeof(GstHipConvert);
-    info.instance_init = hipconv_init;
-    return g_type_register_static(GST_TYPE_BASE_TRANSFORM, "GstHipConvert", &info, (GTypeFlags)0);
-}
-
 /* ------------------------------------------------------------------ plugin */
 static gboolean plugin_init(GstPlugin* plugin) {
     GST_DEBUG_CATEGORY_INIT(gst_hip_debug, "hip", 0, "gfx950 media elements");
     for (int c = 0; c < 3; c++)
-        if (!gst_element_register(plugin, kEncNames[c], GST_RANK_PRIMARY + 1, hipenc_register(c))) return FALSE;
-    return gst_element_register(plugin, "hipconvert", GST_RANK_NONE, hipconv_register());
+        if (!gst_element_register(plugin, kEncNames[c], GST_RANK_PRIMARY + 1, gst_hip_enc_register(c))) return FALSE;
+    return gst_element_register(plugin, "hipconvert", GST_RANK_NONE, gst_hip_convert_get_type()) &&
+           gst_element_register(plugin, "hipupload", GST_RANK_NONE, gst_hip_upload_get_type()) &&
+           gst_element_register(plugin, "hipdownload", GST_RANK_NONE, gst_hip_download_get_type()) &&
+           gst_element_register(plugin, "hipximagesrc", GST_RANK_NONE, gst_hip_ximage_src_get_type());
 }
 
-GST_PLUGIN_DEFINE(GST_VERSION_MAJOR, GST_VERSION_MINOR, hip, "gfx950 (MI355X) media elements: H.264 / H.265 / AV1 encoders, BGRx->I420",
+GST_PLUGIN_DEFINE(GST_VERSION_MAJOR, GST_VERSION_MINOR, hip,
+                  "gfx950 (MI355X) media elements: H.264 / H.265 / AV1 encoders, conversion, HIP memory, X11 source",
                   plugin_init, VERSION, "LGPL", PACKAGE, "selkies-mi355x")

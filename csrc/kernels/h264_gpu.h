@@ -83,9 +83,14 @@ struct FrameArgs {
     int nal_per_slice;
     int sub_rbsp_words;
     const int* gate;       // second-pass launches: run only when *gate != 0 (null: always)
+    // planar 4:2:0 input (YuvInput, h264_frame.h) staged on the device: W x H luma (pitch
+    // W), then I420 U and V ((W+1)/2 x (H+1)/2 each) or NV12 interleaved UV (pitch
+    // 2 * ((W+1)/2)); yuv_fmt 0: BGRx input through k_convert_damage
+    const uint8_t* yuv;
+    int yuv_fmt;
 };
 
-void launch_convert_damage(const FrameArgs& a, hipStream_t s);
+void launch_convert_damage(const FrameArgs& a, hipStream_t s);   // K1 + K3, or k_yuv_damage for planar input
 // k_plan and everything after it; guard: CBR overflow guard + gated second coding pass
 void launch_encode(const FrameArgs& a, hipStream_t s, bool guard = false);
 // k_plan, motion search and scene-cut decisions only (the HEVC back end follows it)
@@ -97,7 +102,6 @@ void launch_rc_account(const FrameArgs& a, const int* sizes, int n, int stride, 
 // K10 per-frame cap of a back end whose payload is the sum of n byte counts (HEVC / AV1);
 // chained: the check after a re-code pass (runs only when *redo is up)
 void launch_rc_guard_sizes(const FrameArgs& a, const int* sizes, int n, int* redo, bool chained, hipStream_t s);
-using h264::kMaxRecodes;   // re-code passes of the HEVC / AV1 back ends (ratecontrol.h)
 
 }  // namespace gpu
 }  // namespace h264

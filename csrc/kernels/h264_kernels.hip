@@ -326,6 +326,69 @@ __global__ __launch_bounds__(256) void k_convert_damage(FrameArgs a) {
         a.stripe_dirty[mby / a.rows_per_slice] = 1;
 }
 
+// K3 for planar 4:2:0 input (GStreamer NV12 / I420, h264_frame.h YuvInput): the staged
+// planes are copied into the source planes with the edge padding of yuv_sample and
+// compared with the previous source, in the thread layout of k_convert_damage (thread
+// = 8 x 2 luma samples and their 4 x 1 chroma samples of each plane).
+__global__ __launch_bounds__(256) void k_yuv_damage(FrameArgs a) {
+    __shared__ int mbd[16];
+    const int t = threadIdx.x;
+    if (t < 16) mbd[t] = 0;
+    __syncthreads();
+    const int item = t & 31, qr = t >> 5;
+    const int mby = blockIdx.y, mbx0 = blockIdx.x * 16;
+    const int x0 = mbx0 * 16 + item * 8;
+    const int qy = mby * 8 + qr;
+    bool diff = false;
+    if (x0 < a.stride_y) {
+        const int W = a.W, H = a.H, cw = (W + 1) >> 1, ch = (H + 1) >> 1;
+        const uint8_t* py = a.yuv;
+        const uint8_t* pc = a.yuv + (size_t)W * H;
+        const int y0 = min(2 * qy, H - 1), y1 = min(2 * qy + 1, H - 1), cy = min(qy, ch - 1);
+        uint32_t ya[2] = {0, 0}, yb[2] = {0, 0}, cbw = 0, crw = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int x = min(x0 + i, W - 1);
+            ya[i >> 2] |= (uint32_t)py[(size_t)y0 * W + x] << (8 * (i & 3));
+            yb[i >> 2] |= (uint32_t)py[(size_t)y1 * W + x] << (8 * (i & 3));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int cx = min((x0 >> 1) + q, cw - 1);
+            uint32_t u, v;
+            if (a.yuv_fmt == 2) {   // NV12: UV interleaved
+                const uint8_t* r = pc + (size_t)cy * (2 * cw) + 2 * cx;
+                u = r[0];
+                v = r[1];
+            } else {                // I420
+                u = pc[(size_t)cy * cw + cx];
+                v = pc[(size_t)cw * ch + (size_t)cy * cw + cx];
+            }
+            cbw |= u << (8 * q);
+            crw |= v << (8 * q);
+        }
+        const size_t oy = (size_t)(2 * qy) * a.stride_y + x0;
+        const size_t oc = (size_t)qy * a.stride_c + x0 / 2;
+        const uint2 pa = *reinterpret_cast<const uint2*>(a.prev.y + oy);
+        const uint2 pb = *reinterpret_cast<const uint2*>(a.prev.y + oy + a.stride_y);
+        const uint32_t pu = *reinterpret_cast<const uint32_t*>(a.prev.u + oc);
+        const uint32_t pv = *reinterpret_cast<const uint32_t*>(a.prev.v + oc);
+        diff = (pa.x != ya[0]) | (pa.y != ya[1]) | (pb.x != yb[0]) | (pb.y != yb[1]) | (pu != cbw) | (pv != crw);
+        *reinterpret_cast<uint2*>(a.src.y + oy) = make_uint2(ya[0], ya[1]);
+        *reinterpret_cast<uint2*>(a.src.y + oy + a.stride_y) = make_uint2(yb[0], yb[1]);
+        *reinterpret_cast<uint32_t*>(a.src.u + oc) = cbw;
+        *reinterpret_cast<uint32_t*>(a.src.v + oc) = crw;
+    }
+    if (diff || a.plan_ctl[1] == 0) mbd[item >> 1] = 1;
+    __syncthreads();
+    if (t < 16) {
+        const int mbx = mbx0 + t;
+        if (mbx < a.mb_w) a.mb_dirty[mby * a.mb_w + mbx] = (uint8_t)mbd[t];
+    }
+    if (__syncthreads_or(t < 16 && mbd[t] && mbx0 + t < a.mb_w) && t == 0)
+        a.stripe_dirty[mby / a.rows_per_slice] = 1;
+}
+
 // ---------------------------------------------------------------------------
 // K4: integer motion search (one wave per MB).
 __device__ __forceinline__ uint32_t load_ref4(const uint8_t* row, int x, int stride) {
@@ -787,7 +850,7 @@ __global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
         const int mode = a.key_dev[3];
         const int kbps = a.key_dev[4];
         const RcState old = rc;
-        rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H, old.vbv_ms, old.qp_min);
+        rc_init(rc, mode, plan_qp, kbps, (float)a.rc_fps, a.W * a.H, old.vbv_ms, old.codec);
         if (old.mode == mode)
             for (int k = 0; k < 2; k++) {
                 rc.last_qp[k] = old.last_qp[k];
@@ -3182,7 +3245,8 @@ __global__ __launch_bounds__(64 * MAXR) void k_deblock(FrameArgs a) {
 // ---------------------------------------------------------------------------
 void launch_convert_damage(const FrameArgs& a, hipStream_t s) {
     dim3 grid((a.mb_w + 15) / 16, a.mb_h);
-    hipLaunchKernelGGL(k_convert_damage, grid, dim3(256), 0, s, a);
+    if (a.yuv_fmt) hipLaunchKernelGGL(k_yuv_damage, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_convert_damage, grid, dim3(256), 0, s, a);
 }
 
 void launch_frontend(const FrameArgs& a, hipStream_t s) {

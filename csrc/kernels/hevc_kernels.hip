@@ -1773,7 +1773,7 @@ void launch_backend(const HevcArgs& a, hipStream_t s, int* redo) {
     if (redo) {   // K10 CBR per-frame cap: payload = the substream bytes (as k_rc_account)
         HevcArgs b = a;
         b.f.gate = redo;
-        for (int r = 0; r < h264::gpu::kMaxRecodes; r++) {
+        for (int r = 0; r < h264::rc_max_recodes(1); r++) {
             h264::gpu::launch_rc_guard_sizes(a.f, a.sub_size, a.f.mb_h, redo, r > 0, s);
             launch_code(b, s);
         }

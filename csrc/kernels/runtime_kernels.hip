@@ -12,9 +12,10 @@ void launch_touch_pages(uint8_t* buf, int pages, hipStream_t s) {
     hipLaunchKernelGGL(k_touch_pages, dim3((pages + 255) / 256), dim3(256), 0, s, buf, pages);
 }
 
+// nv12: u is the interleaved UV plane (Cb at 2 qx, Cr at 2 qx + 1), v unused.
 __global__ __launch_bounds__(256) void k_bgrx_i420(const uint8_t* __restrict__ bgrx, int stride, int w, int h,
                                                    int full, uint8_t* __restrict__ y, int ys, uint8_t* __restrict__ u,
-                                                   int us, uint8_t* __restrict__ v, int vs) {
+                                                   int us, uint8_t* __restrict__ v, int vs, int nv12) {
     const int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
     const int qx = blockIdx.x * 256 + threadIdx.x, qy = blockIdx.y;
     if (qx >= cw || qy >= ch) return;
@@ -29,15 +30,20 @@ __global__ __launch_bounds__(256) void k_bgrx_i420(const uint8_t* __restrict__ b
         y[(size_t)y1 * ys + x0] = yy[2];
         if (x1 != x0) y[(size_t)y1 * ys + x1] = yy[3];
     }
-    u[(size_t)qy * us + qx] = cb;
-    v[(size_t)qy * vs + qx] = cr;
+    if (nv12) {
+        u[(size_t)qy * us + 2 * qx] = cb;
+        u[(size_t)qy * us + 2 * qx + 1] = cr;
+    } else {
+        u[(size_t)qy * us + qx] = cb;
+        v[(size_t)qy * vs + qx] = cr;
+    }
 }
 
 void launch_bgrx_i420(const uint8_t* bgrx, int stride, int w, int h, int full_range, uint8_t* y, int ys,
-                      uint8_t* u, int us, uint8_t* v, int vs, hipStream_t s) {
+                      uint8_t* u, int us, uint8_t* v, int vs, hipStream_t s, int nv12) {
     const int cw = (w + 1) >> 1, ch = (h + 1) >> 1;
     hipLaunchKernelGGL(k_bgrx_i420, dim3((cw + 255) / 256, ch), dim3(256), 0, s, bgrx, stride, w, h, full_range, y,
-                       ys, u, us, v, vs);
+                       ys, u, us, v, vs, nv12);
 }
 
 }  // namespace sk

@@ -8,7 +8,9 @@
 #include "../codec/color.h"
 #include "../kernels/runtime_kernels.h"
 #include <hip/hip_runtime.h>
+#include <string.h>
 #include <string>
+#include <vector>
 
 namespace sk {
 namespace {
@@ -102,6 +104,93 @@ int sk_convert_run(void* conv, const uint8_t* bgrx, int32_t stride, uint8_t* y, 
         !ok(hipMemcpy2DAsync(u, (size_t)us, du, (size_t)cw, (size_t)cw, ch, hipMemcpyDeviceToHost, c->stream), "U") ||
         !ok(hipMemcpy2DAsync(v, (size_t)vs, dv, (size_t)cw, (size_t)cw, ch, hipMemcpyDeviceToHost, c->stream), "V"))
         return -1;
+    return ok(hipStreamSynchronize(c->stream), "sync") ? 0 : -1;
+}
+
+// General form for the GStreamer elements: source BGRx in host or device memory, I420
+// (fmt 1) or NV12 (fmt 2, u = interleaved UV plane) into host or device planes. Device
+// pointers belong to the converter's device. The HIP path reads a device source in place
+// and writes device planes in place (no host round trip: hipupload ! hipconvert !
+// video/x-raw(memory:HIPMemory) ! hiph264enc keeps the frame on the GPU).
+int sk_convert_run_ex(void* conv, const uint8_t* bgrx, int32_t stride, int32_t src_on_device, int32_t fmt,
+                      uint8_t* y, int32_t ys, uint8_t* u, int32_t us, uint8_t* v, int32_t vs,
+                      int32_t dst_on_device) {
+    Converter* c = static_cast<Converter*>(conv);
+    if (!c || !bgrx || !y || !u || (fmt == 1 && !v) || (fmt != 1 && fmt != 2)) {
+        set_last_error("convert: bad arguments");
+        return -1;
+    }
+    const int w = c->w, h = c->h, cw = (w + 1) / 2, ch = (h + 1) / 2;
+    const bool nv12 = fmt == 2;
+    if (!c->backend) {
+        // CPU: stage device memory through the host, then the reference arithmetic
+        std::vector<uint8_t> hin, hout;
+        const uint8_t* src = bgrx;
+        int sstride = stride;
+        if (src_on_device) {
+            hin.resize((size_t)w * 4 * h);
+            if (!ok(hipMemcpy2D(hin.data(), (size_t)w * 4, bgrx, (size_t)stride, (size_t)w * 4, h,
+                                hipMemcpyDeviceToHost), "download"))
+                return -1;
+            src = hin.data();
+            sstride = w * 4;
+        }
+        hout.resize((size_t)w * h + 2 * (size_t)cw * ch);
+        uint8_t* hy = hout.data();
+        uint8_t* hu = hy + (size_t)w * h;
+        uint8_t* hv = hu + (size_t)cw * ch;
+        if (sk_convert_run(conv, src, sstride, hy, w, hu, cw, hv, cw) < 0) return -1;
+        std::vector<uint8_t> uv;
+        if (nv12) {
+            uv.resize((size_t)2 * cw * ch);
+            for (size_t i = 0; i < (size_t)cw * ch; i++) {
+                uv[2 * i] = hu[i];
+                uv[2 * i + 1] = hv[i];
+            }
+        }
+        // host destinations with plain row copies (no HIP runtime needed on CPU-only hosts)
+        auto put = [&](uint8_t* d, int dst, const uint8_t* sp, int sst, int bw, int bh, const char* what) {
+            if (dst_on_device)
+                return ok(hipMemcpy2D(d, (size_t)dst, sp, (size_t)sst, (size_t)bw, bh, hipMemcpyHostToDevice), what);
+            for (int r = 0; r < bh; r++) memcpy(d + (size_t)r * dst, sp + (size_t)r * sst, (size_t)bw);
+            return true;
+        };
+        bool good = put(y, ys, hy, w, w, h, "Y");
+        if (nv12) good = good && put(u, us, uv.data(), 2 * cw, 2 * cw, ch, "UV");
+        else good = good && put(u, us, hu, cw, cw, ch, "U") && put(v, vs, hv, cw, cw, ch, "V");
+        return good ? 0 : -1;
+    }
+    if (!ok(hipSetDevice(c->device), "hipSetDevice")) return -1;
+    const uint8_t* din = bgrx;
+    int dstride = stride;
+    if (!src_on_device) {
+        if (!ok(hipMemcpy2DAsync(c->d_in, (size_t)w * 4, bgrx, (size_t)stride, (size_t)w * 4, h,
+                                 hipMemcpyHostToDevice, c->stream), "upload"))
+            return -1;
+        din = c->d_in;
+        dstride = w * 4;
+    }
+    uint8_t* dy = dst_on_device ? y : c->d_out;
+    uint8_t* du = dst_on_device ? u : c->d_out + (size_t)w * h;
+    uint8_t* dv = dst_on_device ? v : c->d_out + (size_t)w * h + (size_t)cw * ch;
+    const int yst = dst_on_device ? ys : w, ust = dst_on_device ? us : (nv12 ? 2 * cw : cw),
+              vst = dst_on_device ? vs : cw;
+    launch_bgrx_i420(din, dstride, w, h, c->full, dy, yst, du, ust, dv, vst, c->stream, nv12 ? 1 : 0);
+    if (!dst_on_device) {
+        bool good = ok(hipMemcpy2DAsync(y, (size_t)ys, dy, (size_t)w, (size_t)w, h, hipMemcpyDeviceToHost, c->stream),
+                       "Y");
+        if (nv12) {
+            good = good && ok(hipMemcpy2DAsync(u, (size_t)us, du, (size_t)2 * cw, (size_t)2 * cw, ch,
+                                               hipMemcpyDeviceToHost, c->stream), "UV");
+        } else {
+            good = good &&
+                   ok(hipMemcpy2DAsync(u, (size_t)us, du, (size_t)cw, (size_t)cw, ch, hipMemcpyDeviceToHost, c->stream),
+                      "U") &&
+                   ok(hipMemcpy2DAsync(v, (size_t)vs, dv, (size_t)cw, (size_t)cw, ch, hipMemcpyDeviceToHost, c->stream),
+                      "V");
+        }
+        if (!good) return -1;
+    }
     return ok(hipStreamSynchronize(c->stream), "sync") ? 0 : -1;
 }
 

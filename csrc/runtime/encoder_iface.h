@@ -50,6 +50,14 @@ class EncoderBackend {
     // HIP stream of this device, e.g. the torch stream an RCCL scatter wrote the frame on.
     virtual int wait_stream(void* stream) { (void)stream; return 0; }
     virtual int launch() { return 0; }
+    // Planar 4:2:0 input (h264::YuvInput: fmt YUV_I420 / YUV_NV12, planes and strides)
+    // instead of BGRx; on_device: the planes are device memory of this encoder's GPU.
+    // Encodes the frame like encode() and returns the packet count.
+    virtual int encode_yuv(const h264::YuvInput& in, int on_device, uint16_t frame_id) {
+        (void)in; (void)on_device; (void)frame_id;
+        set_last_error("this encoder takes BGRx input only");
+        return -1;
+    }
     // Session state transfer (h264::StateHeader layout). `on_device`: the buffer is
     // device memory of this encoder's GPU (HIP backend) instead of host memory.
     virtual int64_t state_bytes() { return -1; }

@@ -143,9 +143,62 @@ class HipBackend : public EncoderBackend {
         up_next_.clear();
     }
 
+    // Planar input: the planes are staged (2D copies, H2D or D2D) into this parity's
+    // staging buffer in the packed layout k_yuv_damage reads; the graphs are captured
+    // per input kind (BGRx / I420 / NV12).
+    int encode_yuv(const YuvInput& in, int on_device, uint16_t frame_id) override {
+        if (upload_yuv(in, on_device, frame_id) < 0) return -1;
+        if (launch() < 0) return -1;
+        return finish();
+    }
+
+    int upload_yuv(const YuvInput& in, int on_device, uint16_t frame_id) {
+        trace::Range frame_range("h264.upload_yuv");
+        HIPCHECK(hipSetDevice(device_));
+        if (args_.scaled) {
+            set_last_error("planar input cannot be resampled (src size != encoder size)");
+            return -1;
+        }
+        if (inflight() >= 2) {
+            set_last_error("upload(): two frames in flight; finish() the oldest first");
+            return -1;
+        }
+        const int W = g_.W, H = g_.H, cw = (W + 1) / 2, ch = (H + 1) / 2;
+        const size_t need = (size_t)W * H + (size_t)2 * cw * ch;
+        if (!yuv_dev_[0] || yuv_mode_ != in.fmt) {
+            HIPCHECK(hipStreamSynchronize(stream_));
+            if (!yuv_dev_[0])
+                for (auto& b : yuv_dev_) b = dmalloc<uint8_t>(need, false);
+            invalidate_graphs();
+            yuv_mode_ = in.fmt;
+        }
+        const int q = launched_ & 1;
+        HIPCHECK(hipEventRecord(ev_[3 * q], stream_));
+        const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        uint8_t* d = yuv_dev_[q];
+        HIPCHECK(hipMemcpy2DAsync(d, W, in.p[0], in.stride[0], W, H, k, stream_));
+        if (in.fmt == YUV_NV12) {
+            HIPCHECK(hipMemcpy2DAsync(d + (size_t)W * H, 2 * cw, in.p[1], in.stride[1], 2 * cw, ch, k, stream_));
+        } else {
+            HIPCHECK(hipMemcpy2DAsync(d + (size_t)W * H, cw, in.p[1], in.stride[1], cw, ch, k, stream_));
+            HIPCHECK(hipMemcpy2DAsync(d + (size_t)W * H + (size_t)cw * ch, cw, in.p[2], in.stride[2], cw, ch, k,
+                                      stream_));
+        }
+        up_valid_[0] = up_valid_[1] = false;   // the BGRx buffers no longer hold the last frames
+        staged_on_main_ = true;
+        staged_ = true;
+        staged_frame_ = frame_id;
+        return 0;
+    }
+
     int upload(const uint8_t* bgrx, int stride, uint16_t frame_id) override {
         trace::Range frame_range("h264.upload");
         HIPCHECK(hipSetDevice(device_));
+        if (yuv_mode_) {   // back to BGRx input: graphs with k_convert_damage
+            HIPCHECK(hipStreamSynchronize(stream_));
+            invalidate_graphs();
+            yuv_mode_ = 0;
+        }
         const size_t in_bytes = (size_t)stride * (args_.scaled ? args_.scale.src_h : g_.H);
         if (in_bytes > bgrx_cap_ || stride != args_.bgrx_stride) {
             HIPCHECK(hipStreamSynchronize(stream_));   // geometry change: drain, then reallocate
@@ -523,8 +576,7 @@ class HipBackend : public EncoderBackend {
         a.fs_mv = dmalloc<int16_t>(2 * nmb);
         {   // K10 rate control state (ratecontrol.h), initialised like the CPU controller's
             RcState rc;
-            rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms,
-                    rc_qp_min_for(cfg_.codec));
+            rc_init(rc, cfg_.rc_mode, cfg_.qp, cfg_.bitrate_kbps, cfg_.fps, cfg_.width * cfg_.height, cfg_.vbv_ms, cfg_.codec);
             a.rc = dmalloc<RcState>(1);
             copy_now(a.rc, &rc, sizeof(rc));
             a.rc_slice = dmalloc<long long>(2 * (size_t)ns);
@@ -610,6 +662,8 @@ class HipBackend : public EncoderBackend {
     }
 
     void set_parity_args(int stride) {
+        args_.yuv = yuv_dev_[parity_];
+        args_.yuv_fmt = yuv_mode_;
         args_.bgrx = bgrx_dev_[parity_];
         args_.bgrx_stride = stride;
         args_.src = planes_src_[parity_];
@@ -975,6 +1029,8 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipStreamSynchronize(stream_));
     }
     bool graph_guard_ = false;   // the captured H.264 graphs contain the K10 CBR guard
+    uint8_t* yuv_dev_[2] = {nullptr, nullptr};   // planar input staging per parity (upload_yuv)
+    int yuv_mode_ = 0;                           // YuvFormat of the captured graphs (0: BGRx)
     hipEvent_t ev_ext_ = nullptr;   // wait_stream(): foreign stream's work before the next upload
     bool ext_wait_ = false;
     hipStream_t copy_stream_ = nullptr;   // shared per device (not owned)

@@ -17,6 +17,29 @@ void set_last_error(const std::string& e) { g_last_error = e; }
 
 namespace {
 
+// Planar input for a CPU encoder: device planes are copied to host memory first.
+struct HostYuv {
+    std::vector<uint8_t> buf[3];
+    h264::YuvInput in;
+    int load(const h264::YuvInput& src, int on_device, int W, int H) {
+        in = src;
+        if (!on_device) return 0;
+        const int cw = (W + 1) / 2, ch = (H + 1) / 2;
+        const int nplanes = src.fmt == h264::YUV_NV12 ? 2 : 3;
+        for (int p = 0; p < nplanes; p++) {
+            const int w = p == 0 ? W : (src.fmt == h264::YUV_NV12 ? 2 * cw : cw), h = p == 0 ? H : ch;
+            buf[p].resize((size_t)w * h);
+            if (hipMemcpy2D(buf[p].data(), w, src.p[p], src.stride[p], w, h, hipMemcpyDeviceToHost) != hipSuccess) {
+                set_last_error("device planes: copy to the host failed");
+                return -1;
+            }
+            in.p[p] = buf[p].data();
+            in.stride[p] = w;
+        }
+        return 0;
+    }
+};
+
 class CpuBackend : public EncoderBackend {
    public:
     explicit CpuBackend(const h264::EncoderConfig& c) : enc_(c) {}
@@ -40,6 +63,13 @@ class CpuBackend : public EncoderBackend {
         packets_.clear();
         enc_.encode(bgrx, stride, frame_id, packets_);
         return (int)packets_.size();
+    }
+    int encode_yuv(const h264::YuvInput& in, int on_device, uint16_t frame_id) override {
+        if (enc_.scaled_) { set_last_error("planar input cannot be resampled"); return -1; }
+        HostYuv h;
+        if (h.load(in, on_device, enc_.g.W, enc_.g.H) < 0) return -1;
+        enc_.yuv_in = h.in;
+        return encode(nullptr, 0, frame_id);
     }
     int64_t debug_buffer(const char* name, void* dst, int64_t cap) override {
         const void* p = nullptr;
@@ -136,6 +166,13 @@ class CpuHevcBackend : public EncoderBackend {
         enc_.encode(bgrx, stride, frame_id, packets_);
         return (int)packets_.size();
     }
+    int encode_yuv(const h264::YuvInput& in, int on_device, uint16_t frame_id) override {
+        if (enc_.fe.scaled_) { set_last_error("planar input cannot be resampled"); return -1; }
+        HostYuv h;
+        if (h.load(in, on_device, enc_.fe.g.W, enc_.fe.g.H) < 0) return -1;
+        enc_.fe.yuv_in = h.in;
+        return encode(nullptr, 0, frame_id);
+    }
     int64_t debug_buffer(const char* name, void* dst, int64_t cap) override {
         const void* p = nullptr;
         int64_t n = 0;
@@ -185,6 +222,13 @@ class CpuAv1Backend : public EncoderBackend {
         packets_.clear();
         enc_.encode(bgrx, stride, frame_id, packets_);
         return (int)packets_.size();
+    }
+    int encode_yuv(const h264::YuvInput& in, int on_device, uint16_t frame_id) override {
+        if (enc_.fe.scaled_) { set_last_error("planar input cannot be resampled"); return -1; }
+        HostYuv h;
+        if (h.load(in, on_device, enc_.fe.g.W, enc_.fe.g.H) < 0) return -1;
+        enc_.fe.yuv_in = h.in;
+        return encode(nullptr, 0, frame_id);
     }
     int64_t debug_buffer(const char* name, void* dst, int64_t cap) override {
         const void* p = nullptr;
@@ -429,6 +473,24 @@ int sk_upload_ranges(const int32_t* pairs, int32_t n, int32_t rows, int32_t* out
         out[2 * i + 1] = r[i].second;
     }
     return (int)r.size();
+}
+
+int sk_h264_encode_yuv(void* enc, int32_t fmt, const uint8_t* y, int32_t ys, const uint8_t* u, int32_t us,
+                       const uint8_t* v, int32_t vs, int32_t on_device, int32_t frame_id) {
+    if (fmt != h264::YUV_I420 && fmt != h264::YUV_NV12) {
+        set_last_error("planar format must be 1 (I420) or 2 (NV12)");
+        return -1;
+    }
+    h264::YuvInput in;
+    in.fmt = fmt;
+    in.p[0] = y; in.p[1] = u; in.p[2] = fmt == h264::YUV_NV12 ? u : v;
+    in.stride[0] = ys; in.stride[1] = us; in.stride[2] = fmt == h264::YUV_NV12 ? us : vs;
+    try {
+        return static_cast<EncoderBackend*>(enc)->encode_yuv(in, on_device, (uint16_t)frame_id);
+    } catch (const std::exception& ex) {
+        set_last_error(ex.what());
+        return -1;
+    }
 }
 
 int sk_h264_launch(void* enc) {

@@ -59,6 +59,11 @@ int sk_h264_set_overlay_image(void* enc, int slot, const uint8_t* bgra, int w, i
 int sk_h264_set_overlay_pos(void* enc, int slot, int on, int x, int y, int tdx, int tdy);
 // Encodes one BGRx frame; returns the number of packets (or < 0 on error).
 int sk_h264_encode(void* enc, const uint8_t* bgrx, int32_t stride_bytes, int32_t frame_id);
+// Planar 4:2:0 input instead of BGRx (GStreamer NV12 / I420): fmt 1 = I420 (y, u, v planes),
+// 2 = NV12 (y plane, interleaved uv in u / us); on_device: the planes are HIP device memory
+// (of the encoder's GPU for the HIP backend). Returns the packet count like sk_h264_encode.
+int sk_h264_encode_yuv(void* enc, int32_t fmt, const uint8_t* y, int32_t ys, const uint8_t* u, int32_t us,
+                       const uint8_t* v, int32_t vs, int32_t on_device, int32_t frame_id);
 // Split encode: submit queues the frame (bgrx must stay valid until finish), finish
 // waits and returns the packet count (then sk_h264_get_packet as after sk_h264_encode).
 int sk_h264_submit(void* enc, const uint8_t* bgrx, int32_t stride, int32_t frame_id);
@@ -96,7 +101,30 @@ const char* sk_last_error(void);
 void* sk_convert_create(int w, int h, int full_range, int backend, int device);
 int sk_convert_run(void* conv, const uint8_t* bgrx, int32_t stride, uint8_t* y, int32_t ys, uint8_t* u, int32_t us,
                    uint8_t* v, int32_t vs);
+// General form: BGRx source in host or device memory; fmt 1 = I420, 2 = NV12 (u = the
+// interleaved UV plane, v unused); destination planes in host or device memory.
+int sk_convert_run_ex(void* conv, const uint8_t* bgrx, int32_t stride, int32_t src_on_device, int32_t fmt,
+                      uint8_t* y, int32_t ys, uint8_t* u, int32_t us, uint8_t* v, int32_t vs,
+                      int32_t dst_on_device);
 void sk_convert_destroy(void* conv);
+
+// Frame sources for hipximagesrc (csrc/runtime/source_api.cpp): kind 0 = X11 MIT-SHM
+// region (x, y, w, h of `display`, XFixes cursor when show_pointer), 1 / 2 / 3 =
+// synthetic motion / desktop / noise frames (headless hosts; seed). grab() returns BGRx
+// rows valid until the next grab, the stride, and the changed row ranges (pairs, at
+// most cap; *nrows = -1 when the source cannot tell).
+void* sk_source_open(int32_t kind, const char* display, int32_t x, int32_t y, int32_t w, int32_t h,
+                     int32_t show_pointer, uint32_t seed);
+const uint8_t* sk_source_grab(void* src, int32_t* stride, int32_t* rows, int32_t cap, int32_t* nrows);
+const char* sk_source_name(void* src);
+void sk_source_close(void* src);
+// Device memory of the GStreamer HIPMemory allocator. kind: 0 host->device,
+// 1 device->host, 2 device->device, 3 either (unified addressing). 0 on success.
+void* sk_dev_alloc(int32_t device, int64_t bytes);
+void sk_dev_free(int32_t device, void* p);
+int sk_dev_copy(int32_t device, void* dst, const void* src, int64_t bytes, int32_t kind);
+int sk_dev_copy2d(int32_t device, void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
+                  int64_t height, int32_t kind);
 
 typedef struct sk_jpeg_config {
     int32_t width, height, stripe_height;

@@ -33,9 +33,11 @@ codecs are H.264, H.265, AV1 and JPEG.
 
 When GStreamer itself is installed (the 1.14 under /opt/conda in this image) a launch
 string can also run in real GStreamer: :func:`to_gst_launch` rewrites the reference's
-encoder elements to this build's GStreamer elements (libgsthip, csrc/gst/gsthip.c:
-``hiph264enc`` / ``hiph265enc`` / ``hipav1enc`` / ``hipconvert``) with their
-properties mapped, and :func:`run_gst` runs it with gst-launch-1.0. That covers graphs
+encoder elements to this build's GStreamer elements (libgsthip, csrc/gst/: ``hiph264enc``
+/ ``hiph265enc`` / ``hipav1enc``) with their properties mapped, ``ximagesrc`` to
+``hipximagesrc``, ``cudaupload`` / ``cudaconvert`` / ``cudadownload`` to ``hipupload`` /
+``hipconvert`` / ``hipdownload`` and ``memory:CUDAMemory`` caps to ``memory:HIPMemory``,
+and :func:`run_gst` runs it with gst-launch-1.0. That covers graphs
 GStreamer can complete here (file / fd / fake sinks); ``webrtcbin`` and the RTP
 payloaders are not in that GStreamer build, so WebRTC stays on the own stack (webrtc/).
 """
@@ -65,6 +67,7 @@ class PipelineError(ValueError):
 class Element:
     name: str
     props: dict = field(default_factory=dict)
+    features: str = ""   # caps features, e.g. "memory:CUDAMemory"
 
 
 @dataclass
@@ -132,6 +135,7 @@ def _value(v: str):
 
 def _caps(seg: str) -> Element:
     parts = [p.strip() for p in seg.split(",")]
+    feats = parts[0].split("(", 1)[1].rstrip(")") if "(" in parts[0] else ""
     parts[0] = parts[0].split("(", 1)[0]   # caps features: video/x-raw(memory:CUDAMemory|VAMemory)
     props = {}
     for p in parts[1:]:
@@ -139,7 +143,7 @@ def _caps(seg: str) -> Element:
             k, v = p.split("=", 1)
             v = v.split(")", 1)[-1] if v.startswith("(") else v   # (int)1920 / (fraction)60/1
             props[k.strip()] = _value(v)
-    return Element(parts[0], props)
+    return Element(parts[0], props, feats)
 
 
 def parse_elements(text: str) -> list[Element]:
@@ -246,9 +250,17 @@ def apply_to_args(spec: PipelineSpec, args) -> None:
 # Real GStreamer (gst-launch-1.0 + libgsthip)
 GST_ENCODER_FOR = {**{n: "hiph264enc" for n in H264_ENCODERS}, **{n: "hiph265enc" for n in H265_ENCODERS},
                    **{n: "hipav1enc" for n in AV1_ENCODERS}}
-# the reference's GPU upload / conversion elements: the hip encoders take BGRx directly
-GST_DROP = {"cudaupload", "cudadownload", "cudaconvert", "vapostproc", "hipupload"}
+# the reference's GPU memory elements map to libgsthip's (device frames as memory:HIPMemory):
+# cudaupload / cudaconvert / cudadownload (gstwebrtc_app.py:261-284); ximagesrc (not in this
+# image's GStreamer) to hipximagesrc with the same properties
+GST_RENAME = {"cudaupload": "hipupload", "cudaconvert": "hipconvert", "cudadownload": "hipdownload",
+              "ximagesrc": "hipximagesrc"}
+GST_CAPS_FEATURES = {"memory:CUDAMemory": "memory:HIPMemory", "memory:VAMemory": "memory:HIPMemory"}
+# VA post-processing has no counterpart: the encoders convert BGRx themselves
+GST_DROP = {"vapostproc"}
 GST_NO_ELEMENT = {"webrtcbin", "rtph264pay", "rtph265pay", "rtpav1pay", "rtpopuspay", "pulsesrc", "opusenc"}
+# ximagesrc properties hipximagesrc does not take (xid / xname windows are not captured)
+GST_XIMAGESRC_PROPS = {"display-name", "show-pointer", "use-damage", "startx", "starty", "endx", "endy", "remote"}
 
 
 def _gst_value(v) -> str:
@@ -296,16 +308,30 @@ def to_gst_launch(text: str) -> list[str]:
         if n in GST_DROP:
             continue
         if n.startswith("video/") or n.startswith("audio/"):
-            caps = [n] + [f"{k}={_gst_value(v) if k != 'framerate' else _gst_framerate(v)}" for k, v in p.items()]
+            feats = GST_CAPS_FEATURES.get(e.features, e.features)
+            if feats == "memory:HIPMemory" and not _hip_devices():
+                feats = ""   # CPU-only host: hipupload / hipconvert keep frames in system memory
+            head = f"{n}({feats})" if feats else n
+            caps = [head] + [f"{k}={_gst_value(v) if k != 'framerate' else _gst_framerate(v)}" for k, v in p.items()]
             seg = [",".join(caps)]
         elif n in GST_ENCODER_FOR:
             seg = [GST_ENCODER_FOR[n], *_gst_encoder_props(n, p)]
+        elif n == "ximagesrc":
+            seg = ["hipximagesrc", *(f"{k}={_gst_value(v)}" for k, v in p.items() if k in GST_XIMAGESRC_PROPS)]
         else:
-            seg = [n, *(f"{k}={_gst_value(v)}" for k, v in p.items())]
+            seg = [GST_RENAME.get(n, n), *(f"{k}={_gst_value(v)}" for k, v in p.items())]
         if out:
             out.append("!")
         out.extend(seg)
     return out
+
+
+def _hip_devices() -> int:
+    try:
+        from selkies_gstreamer_amd.ops.native import hip_device_count
+        return hip_device_count()
+    except (OSError, RuntimeError):
+        return 0
 
 
 def _gst_framerate(v) -> str:

@@ -20,6 +20,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[2]
 SRC = ROOT / "csrc" / "gst" / "gsthip.c"
+SRCS = sorted((ROOT / "csrc" / "gst").glob("*.c"))
 LIBDIR = ROOT / "selkies_gstreamer_amd" / "_lib"
 PLUGDIR = LIBDIR / "gstreamer-1.0"
 PLUGIN = PLUGDIR / "libgsthip.so"
@@ -117,12 +118,13 @@ def build(verbose: bool = False) -> Path:
     from selkies_gstreamer_amd.ops.build import build as build_native
     native = build_native()
     PLUGDIR.mkdir(parents=True, exist_ok=True)
-    if PLUGIN.exists() and PLUGIN.stat().st_mtime >= max(SRC.stat().st_mtime, native.stat().st_mtime,
-                                                          Path(__file__).stat().st_mtime):
+    newest = max([p.stat().st_mtime for p in SRCS + sorted((ROOT / "csrc" / "gst").glob("*.h"))] +
+                 [native.stat().st_mtime, Path(__file__).stat().st_mtime])
+    if PLUGIN.exists() and PLUGIN.stat().st_mtime >= newest:
         return PLUGIN
     cflags, libs = pkg_flags("gstreamer-video-1.0", "gstreamer-base-1.0")
     cc = shutil.which("gcc") or "cc"
-    cmd = [cc, "-O2", "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-std=gnu11", *cflags, str(SRC),
+    cmd = [cc, "-O2", "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-std=gnu11", *cflags, *map(str, SRCS),
            "-o", str(PLUGIN), *libs, f"-L{LIBDIR}", "-lselkies_native",
            f"-Wl,--enable-new-dtags,-rpath,$ORIGIN/..:{PREFIX / 'lib'}", "-Wl,--no-undefined"]
     if verbose:

@@ -114,6 +114,9 @@ def lib():
         L.sk_h264_set_overlay_pos.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 6
         L.sk_h264_encode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_encode.restype = ctypes.c_int
+        L.sk_h264_encode_yuv.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                         ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         L.sk_h264_finish.argtypes = [ctypes.c_void_p]
         L.sk_h264_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
@@ -160,6 +163,37 @@ def lib():
 
 def hip_device_count() -> int:
     return int(lib().sk_hip_device_count())
+
+
+def convert_bgrx(bgrx: np.ndarray, fmt: str = "i420", backend: str = "cpu", device: int = 0,
+                 full_range: bool = False):
+    """BGRx (H, W, 4) -> 4:2:0 planes with the encoders' K1 arithmetic (hipconvert's
+    converter): ``fmt`` "i420" -> (y, u, v), "nv12" -> (y, uv)."""
+    L = lib()
+    for name, res, args in (("sk_convert_create", ctypes.c_void_p, [ctypes.c_int] * 5),
+                            ("sk_convert_run_ex", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                                                 ctypes.c_int32, ctypes.c_int32] +
+                             [ctypes.c_void_p, ctypes.c_int32] * 3 + [ctypes.c_int32]),
+                            ("sk_convert_destroy", None, [ctypes.c_void_p])):
+        getattr(L, name).restype = res
+        getattr(L, name).argtypes = args
+    H, W = bgrx.shape[:2]
+    bgrx = np.ascontiguousarray(bgrx)
+    cw, ch = (W + 1) // 2, (H + 1) // 2
+    y = np.zeros((H, W), np.uint8)
+    nv12 = fmt.lower() == "nv12"
+    u = np.zeros((ch, 2 * cw if nv12 else cw), np.uint8)
+    v = np.zeros((ch, cw), np.uint8)
+    c = L.sk_convert_create(W, H, int(full_range), 1 if backend == "hip" else 0, device)
+    if not c:
+        raise RuntimeError(L.sk_last_error().decode())
+    try:
+        if L.sk_convert_run_ex(c, bgrx.ctypes.data, bgrx.strides[0], 0, 2 if nv12 else 1, y.ctypes.data, W,
+                               u.ctypes.data, u.strides[0], v.ctypes.data, cw, 0) < 0:
+            raise RuntimeError(L.sk_last_error().decode())
+    finally:
+        L.sk_convert_destroy(c)
+    return (y, u) if nv12 else (y, u, v)
 
 
 def upload_ranges(pairs, rows: int):
@@ -240,7 +274,7 @@ RC_MODES = {"cqp": 0, "crf": 1, "cbr": 2}
 RC_FIELDS = ("mode", "base_qp", "qp_min", "qp_max", "budget", "vbv_size", "fullness", "frames", "last_qp_p",
              "last_qp_i", "last_bits_p", "last_bits_i", "last_cplx_p", "last_cplx_i", "cplx_ema", "cur_qp",
              "cur_intra", "cur_cplx", "max_p_bits", "seq", "cur_valid", "pixels", "cur_idr", "redos", "qp_floor", "floor_age", "last_mbs_p", "last_mbs_i", "cur_mbs", "vbv_ms", "last_qpf_p", "last_qpf_i", "cur_qpf",
-             "cur_redo", "redo_qpf", "redo_bits")
+             "cur_redo", "redo_qpf", "redo_bits", "codec")
 
 
 class H264Encoder:
@@ -332,6 +366,39 @@ class H264Encoder:
         n = L.sk_h264_encode(self._h, bgrx.ctypes.data, stride, frame_id & 0xFFFF)
         if n < 0:
             raise RuntimeError(f"encode failed: {L.sk_last_error().decode()}")
+        out = []
+        pk = SkPacket()
+        for i in range(n):
+            L.sk_h264_get_packet(self._h, i, ctypes.byref(pk))
+            out.append(Packet(ctypes.string_at(pk.data, pk.size), pk.y, pk.w, pk.h, bool(pk.key)))
+        return out
+
+    def encode_yuv(self, fmt: str, y, u, v=None, frame_id: int = 0) -> list[Packet]:
+        """Planar 4:2:0 input instead of BGRx (GStreamer NV12 / I420 caps): ``fmt`` "i420"
+        (y, u, v planes) or "nv12" (y plane, interleaved uv as ``u``). Planes are numpy
+        uint8 arrays (host) or torch uint8 tensors on this encoder's GPU (device input,
+        no host copy). W x H luma, ((W+1)/2) x ((H+1)/2) chroma (x2 wide for NV12 uv)."""
+        code = {"i420": 1, "nv12": 2}[fmt.lower()]
+        planes = [y, u] + ([v] if code == 1 else [u])
+        on_dev = int(hasattr(y, "data_ptr") and bool(getattr(y, "is_cuda", False)))
+        ptrs, strides = [], []
+        for p in planes:
+            if hasattr(p, "data_ptr"):
+                if p.dim() != 2 or p.stride(1) != 1:
+                    raise ValueError("planes must be 2-D with unit column stride")
+                ptrs.append(p.data_ptr())
+                strides.append(p.stride(0) * p.element_size())
+            else:
+                a = np.asarray(p)
+                if a.dtype != np.uint8 or a.ndim != 2 or a.strides[1] != 1:
+                    raise ValueError("planes must be 2-D uint8 arrays with unit column stride")
+                ptrs.append(a.ctypes.data)
+                strides.append(a.strides[0])
+        L = lib()
+        n = L.sk_h264_encode_yuv(self._h, code, ptrs[0], strides[0], ptrs[1], strides[1], ptrs[2], strides[2],
+                                 on_dev, frame_id & 0xFFFF)
+        if n < 0:
+            raise RuntimeError(f"encode_yuv failed: {L.sk_last_error().decode()}")
         out = []
         pk = SkPacket()
         for i in range(n):

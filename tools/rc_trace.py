@@ -22,19 +22,22 @@ if ROOT not in sys.path:
 
 
 def run(backend: str, width: int, height: int, frames: int, content: str, mode: str, kbps: int,
-        codec: str = "h264", fps: float = 60.0, qp: int = 25, stripe_height: int = 64) -> dict:
+        codec: str = "h264", fps: float = 60.0, qp: int = 25, stripe_height: int = 64, pool: int = 0) -> dict:
     from selkies_gstreamer_amd.ops.native import H264Encoder
     from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
     src = SyntheticDesktop(width, height, kind=content)
     enc = H264Encoder(width, height, stripe_height=stripe_height, fullframe=codec != "h264", backend=backend,
                       codec=codec, qp=qp, fps=fps, rate_control=mode, bitrate_kbps=kbps)
-    sizes, keys, qps = [], [], []
+    sizes, keys, qps, redo = [], [], [], []
+    frames_pool = [src.frame(i) for i in range(pool)] if pool > 0 else None   # bench.py's cycling pool
     t0 = time.perf_counter()
     for t in range(frames):
-        pk = enc.encode(src.frame(t), t & 0xFFFF)
+        pk = enc.encode(frames_pool[t % pool] if frames_pool else src.frame(t), t & 0xFFFF)
         sizes.append(sum(len(p.data) for p in pk))
         keys.append(any(p.key for p in pk))
-        qps.append(enc.rc_stats().get("cur_qp", qp))
+        st = enc.rc_stats()
+        qps.append(st.get("cur_qp", qp))
+        redo.append(st.get("cur_redo", 0))
     wall = time.perf_counter() - t0
     st = enc.rc_stats()
     enc.close()
@@ -51,7 +54,8 @@ def run(backend: str, width: int, height: int, frames: int, content: str, mode: 
         out["max_nonkey_budgets"] = round(max(non_key) / budget, 3) if non_key else None
         out["nonkey_over_1p5"] = sum(1 for s in non_key if s > 1.5 * budget)
         out["max_key_budgets"] = round(max((s for s, k in zip(sizes, keys) if k), default=0) / budget, 3)
-    out["trace"] = {"bytes": sizes, "key": [int(k) for k in keys], "qp": qps}
+    out["recoded_frames"] = sum(1 for r in redo if r)
+    out["trace"] = {"bytes": sizes, "key": [int(k) for k in keys], "qp": qps, "redo": redo}
     return out
 
 
@@ -67,9 +71,10 @@ def main() -> None:
     ap.add_argument("--kbps", type=int, default=8000)
     ap.add_argument("--fps", type=float, default=60.0)
     ap.add_argument("--qp", type=int, default=25)
+    ap.add_argument("--pool", type=int, default=0, help="cycle this many source frames (bench.py's pool)")
     ap.add_argument("--json", default="", help="write the full trace here")
     a = ap.parse_args()
-    r = run(a.backend, a.width, a.height, a.frames, a.content, a.mode, a.kbps, a.codec, a.fps, a.qp)
+    r = run(a.backend, a.width, a.height, a.frames, a.content, a.mode, a.kbps, a.codec, a.fps, a.qp, pool=a.pool)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(r, f)
