@@ -14,7 +14,8 @@
 //   (hevc_sao.h), no sign hiding /
 //   transform skip,
 //   entropy_coding_sync (WPP): one CABAC substream per CTB row, slices = stripes of
-//   whole CTB rows.
+//   whole CTB rows; intra slices split every row into slices of ~kIntraSegCtbs CTBs
+//   (SliceMap: a key frame's CTB chain is a segment, not a row).
 // Decoder-side operations (inverse transform, dequantisation, intra prediction,
 // chroma interpolation, merge/AMVP derivation, context selection) follow the
 // normative processes of ITU-T H.265 (04/2013) clauses 8 and 9 exactly; forward
@@ -22,9 +23,42 @@
 #pragma once
 #include <stddef.h>
 #include "sk_common.h"
+#include "h264_encoder.h"   // h264::SliceTask (the front end's slice decisions)
 
 namespace sk {
 namespace hevc {
+
+// Slice layout of a picture, in CTBs. Slices are stripes of rows_per_slice CTB rows
+// (one WPP substream per row). A row of an intra slice is instead cut into K slices of
+// about mb_w / K CTBs each, K = ceil(mb_w / kIntraSegCtbs): the closed-loop intra coding
+// of a CTB waits for its left neighbour, so a key frame's longest serial chain is one
+// segment (40 CTBs at 4K) instead of one row (240) - the same cut as the H.264 IDR
+// sub-slices (h264_encoder.h intra_split). Such a slice starts mid-row and ends in the
+// same row, as 7.4.7.1 requires under entropy_coding_sync; it has no top neighbours
+// and restarts CABAC, so the cost is some intra and context-adaptation efficiency.
+// Neighbours in another slice are unavailable to prediction, CABAC context selection,
+// SAO merging, and (pps_loop_filter_across_slices_enabled_flag = 0) to deblocking and
+// SAO edge offsets. Per-segment arrays are indexed by slot = cy * K + k.
+constexpr int kIntraSegCtbs = 40;
+SK_HD int intra_seg_count(int mb_w, int seg_ctbs) {
+    return seg_ctbs > 0 && mb_w > seg_ctbs ? (mb_w + seg_ctbs - 1) / seg_ctbs : 1;
+}
+struct SliceMap {
+    const h264::SliceTask* tasks;
+    int mb_w, rows_per_slice, K;
+    SK_HD bool split(int cy) const { return K > 1 && tasks[cy / rows_per_slice].final_action == h264::ACT_I; }
+    SK_HD int nseg(int cy) const { return split(cy) ? K : 1; }
+    SK_HD int seg(int cx, int cy) const { return split(cy) ? ((cx + 1) * K - 1) / mb_w : 0; }
+    SK_HD int x0(int cy, int k) const { return split(cy) ? k * mb_w / K : 0; }
+    SK_HD int x1(int cy, int k) const { return split(cy) ? (k + 1) * mb_w / K : mb_w; }
+    SK_HD int slot(int cx, int cy) const { return cy * K + seg(cx, cy); }
+    SK_HD int id(int cx, int cy) const { return split(cy) ? 2 * (cy * K + seg(cx, cy)) + 1 : 2 * (cy / rows_per_slice); }
+    SK_HD bool same(int ax, int ay, int bx, int by) const { return id(ax, ay) == id(bx, by); }
+    // neighbour CTBs available to (cx, cy): decoded before it (raster order) and in its slice
+    SK_HD bool left(int cx, int cy) const { return cx > 0 && same(cx - 1, cy, cx, cy); }
+    SK_HD bool top(int cx, int cy) const { return cy > 0 && same(cx, cy - 1, cx, cy); }
+    SK_HD bool top_right(int cx, int cy) const { return cy > 0 && cx + 1 < mb_w && same(cx + 1, cy - 1, cx, cy); }
+};
 
 constexpr int kCtb = 16;
 constexpr int kCoefPerCu = 384;     // 16x16 luma | 8x8 Cb | 8x8 Cr, raster [y][x] per TU; split CUs:
@@ -1110,7 +1144,7 @@ SK_HD void dbk_chroma_line(uint8_t* q, int step, int qp) {
 }
 
 // The whole picture (CPU reference; k_hevc_dbk_v / k_hevc_dbk_h are the same loops in
-// parallel). cus: [ctb_h][ctb_w]; rows_per_slice: CTB rows per slice.
+// parallel). cus: [ctb_h][ctb_w]; m: the slice layout (edges between slices stay).
 // One luma segment: the vertical (vert) or horizontal edge at luma position e (a
 // multiple of 8, > 0) of the picture, 4 samples long from position a along the edge.
 // Returns without filtering when the edge is an unsplit CU's inside or bS is 0.
@@ -1124,35 +1158,39 @@ SK_HD void dbk_luma_edge(uint8_t* Y, int sy, const CuInfo* cus, int ctb_w, bool 
     if (bs) dbk_luma_segment(Y + (size_t)y * sy + x, vert ? 1 : sy, vert ? sy : 1, bs, (p.qp + q.qp + 1) >> 1);
 }
 SK_HD void deblock_picture(uint8_t* Y, uint8_t* U, uint8_t* V, int sy, int sc, const CuInfo* cus, int ctb_w,
-                           int ctb_h, int rows_per_slice) {
-    for (int x = 8; x < 16 * ctb_w; x += 8)   // vertical edges
-        for (int a = 0; a < 16 * ctb_h; a += 4) dbk_luma_edge(Y, sy, cus, ctb_w, true, x, a);
+                           int ctb_h, const SliceMap& m) {
+    for (int x = 8; x < 16 * ctb_w; x += 8)   // vertical edges (not between slices)
+        for (int a = 0; a < 16 * ctb_h; a += 4) {
+            if (!(x & 8) && !m.same((x >> 4) - 1, a >> 4, x >> 4, a >> 4)) continue;
+            dbk_luma_edge(Y, sy, cus, ctb_w, true, x, a);
+        }
     for (int cy = 0; cy < ctb_h; cy++)
         for (int cx = 1; cx < ctb_w; cx++) {
             const CuInfo &p = cus[cy * ctb_w + cx - 1], &q = cus[cy * ctb_w + cx];
             if (p.mode != CU_INTRA && q.mode != CU_INTRA) continue;   // chroma: bS 2 only
+            if (!m.same(cx - 1, cy, cx, cy)) continue;
             const int qp = (p.qp + q.qp + 1) >> 1;
             for (int l = 0; l < 8; l++) {
                 dbk_chroma_line(U + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
                 dbk_chroma_line(V + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
             }
         }
-    for (int y = 8; y < 16 * ctb_h; y += 8) {   // horizontal edges (not between slices)
-        if (!(y & 8) && (y >> 4) % rows_per_slice == 0) continue;
-        for (int a = 0; a < 16 * ctb_w; a += 4) dbk_luma_edge(Y, sy, cus, ctb_w, false, y, a);
-    }
-    for (int cy = 1; cy < ctb_h; cy++) {
-        if (cy % rows_per_slice == 0) continue;
+    for (int y = 8; y < 16 * ctb_h; y += 8)   // horizontal edges (not between slices)
+        for (int a = 0; a < 16 * ctb_w; a += 4) {
+            if (!(y & 8) && !m.same(a >> 4, (y >> 4) - 1, a >> 4, y >> 4)) continue;
+            dbk_luma_edge(Y, sy, cus, ctb_w, false, y, a);
+        }
+    for (int cy = 1; cy < ctb_h; cy++)
         for (int cx = 0; cx < ctb_w; cx++) {
             const CuInfo &p = cus[(cy - 1) * ctb_w + cx], &q = cus[cy * ctb_w + cx];
             if (p.mode != CU_INTRA && q.mode != CU_INTRA) continue;
+            if (!m.same(cx, cy - 1, cx, cy)) continue;
             const int qp = (p.qp + q.qp + 1) >> 1;
             for (int l = 0; l < 8; l++) {
                 dbk_chroma_line(U + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
                 dbk_chroma_line(V + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);
             }
         }
-    }
 }
 
 }  // namespace hevc

@@ -139,6 +139,7 @@ CpuHevcEncoder::CpuHevcEncoder(const h264::EncoderConfig& cfg) : fe(front_config
     sao_cost.assign(n, 0);
     sao_md.assign((size_t)n * kSaoMd, 0);
     build_parameter_sets(fe.g.W, fe.g.H, cfg.full_range, cfg.fps, param_sets);
+    seg_k = intra_seg_k(geo.ctb_w);
 }
 
 void CpuHevcEncoder::load_cu_src(int cx, int cy, uint8_t* y, uint8_t* u, uint8_t* v) const {
@@ -384,12 +385,13 @@ void CpuHevcEncoder::code_slice_intra(int s) {
     const SliceTask& t = fe.tasks[s];
     const h264::Geometry& g = fe.g;
     const int qp = t.qp, qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
+    const SliceMap m = smap();   // split rows: each segment its own slice (no top, left inside it)
     for (int pass = 0; pass < 2; pass++)
         for (int cy = t.first_row; cy < t.first_row + t.num_rows; cy++)
             for (int cx = 0; cx < geo.ctb_w; cx++) {
                 const int idx = cy * geo.ctb_w + cx;
                 CuInfo& cu = cus[idx];
-                const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < geo.ctb_w;
+                const bool left = m.left(cx, cy), top = m.top(cx, cy), tr = m.top_right(cx, cy);
                 uint8_t sy[256], su[64], sv[64];
                 load_cu_src(cx, cy, sy, su, sv);
                 if (pass == 0) {
@@ -522,9 +524,9 @@ void CpuHevcEncoder::code_slice_skip(int s) {
 }
 
 // Plane geometry for SAO: plane 0 luma (CTB 16), 1 / 2 chroma (CTB 8).
-static SaoPlane sao_plane(const Geo& geo, int c) {
+static SaoPlane sao_plane(const Geo& geo, int c, const SliceMap& m) {
     const int n = c ? 8 : 16;
-    return SaoPlane{geo.ctb_w * n, geo.ctb_h * n, n, geo.rows_per_slice};
+    return SaoPlane{geo.ctb_w * n, geo.ctb_h * n, n, m};
 }
 
 void CpuHevcEncoder::sao_analyse() {
@@ -540,7 +542,7 @@ void CpuHevcEncoder::sao_analyse() {
                 SaoStats& st = sao_stats[(size_t)3 * idx + c];
                 st = SaoStats{};
                 if (!coded) continue;
-                const SaoPlane pl = sao_plane(geo, c);
+                const SaoPlane pl = sao_plane(geo, c, smap());
                 const int stride = c ? g.stride_c : g.stride_y;
                 for (int y = cy * pl.n; y < (cy + 1) * pl.n; y++)
                     for (int x = cx * pl.n; x < (cx + 1) * pl.n; x++)
@@ -560,14 +562,14 @@ void CpuHevcEncoder::sao_analyse() {
     for (int cy = 0; cy < geo.ctb_h; cy++) {
         const SliceTask& t = fe.tasks[cy / geo.rows_per_slice];
         const size_t o = (size_t)cy * geo.ctb_w;
-        sao_row_merge(&sao_md[o * kSaoMd], &sao_own[o], &sao_cost[o], geo.ctb_w, t.qp, cy > t.first_row, &sao[o]);
+        sao_row_merge(&sao_md[o * kSaoMd], &sao_own[o], &sao_cost[o], geo.ctb_w, t.qp, smap(), cy, &sao[o]);
     }
 }
 
 void CpuHevcEncoder::sao_apply() {
     const h264::Geometry& g = fe.g;
     for (int c = 0; c < 3; c++) {
-        const SaoPlane pl = sao_plane(geo, c);
+        const SaoPlane pl = sao_plane(geo, c, smap());
         const int stride = c ? g.stride_c : g.stride_y;
         const std::vector<uint8_t> dbk = fe.rec[c];   // the filter reads deblocked samples only
         for (int y = 0; y < pl.h; y++)
@@ -582,40 +584,45 @@ void CpuHevcEncoder::binarize_slice(int s) {
     const SliceTask& t = fe.tasks[s];
     const bool p_slice = t.final_action != ACT_I;
     const int last_row = t.first_row + t.num_rows - 1;
+    const SliceMap m = smap();
     for (int cy = t.first_row; cy <= last_row; cy++)
         for (int cx = 0; cx < geo.ctb_w; cx++) {
             const int idx = cy * geo.ctb_w + cx;
-            const bool left = cx > 0, top = cy > t.first_row;
+            const bool left = m.left(cx, cy), top = m.top(cx, cy);
             const int skip_ctx = (left && cus[idx - 1].mode == CU_SKIP) + (top && cus[idx - geo.ctb_w].mode == CU_SKIP);
             const int cand_a = (left && cus[idx - 1].mode == CU_INTRA) ? cus[idx - 1].intra_mode : 1;
             BinBuf w{&bins[(size_t)idx * kCuBinCap], 0};
             sao_bins(w, sao[idx], left, top);   // CTB-level SAO syntax before the coding quadtree
             code_cu(w, cus[idx], &coefs[(size_t)idx * kCoefPerCu], p_slice, skip_ctx, cand_a);
-            w.term(cy == last_row && cx == geo.ctb_w - 1);   // end_of_slice_segment_flag
+            // end_of_slice_segment_flag: the last CTB of the slice (a split row: of its segment)
+            const bool end = m.split(cy) ? cx + 1 == m.x1(cy, m.seg(cx, cy))
+                                         : cy == last_row && cx == geo.ctb_w - 1;
+            w.term(end);
             bin_n[idx] = w.n;
         }
 }
 
-std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
-    const SliceTask& t = fe.tasks[s];
+// One slice segment NAL: CTB rows cy0 .. cy0 + rows - 1, columns [x0, x1) of each (a
+// split row: one row, one segment), one CABAC substream per row with WPP storage
+// after the second CTB, entry points for the rows after the first.
+std::vector<uint8_t> CpuHevcEncoder::write_segment(const SliceTask& t, int cy0, int rows, int x0, int x1, bool idr) {
     const bool p_slice = t.final_action != ACT_I;
-    const int rows = t.num_rows;
     std::vector<std::vector<uint8_t>> sub(rows);
     uint8_t sync[CTX_COUNT];
     for (int r = 0; r < rows; r++) {
-        const int cy = t.first_row + r;
+        const int cy = cy0 + r;
         uint8_t ctx[CTX_COUNT];
         if (r == 0 || geo.ctb_w < 2) ctx_init_all(ctx, p_slice ? 1 : 0, t.qp);
         else memcpy(ctx, sync, CTX_COUNT);
         if (pc_host_) {   // chunk-parallel model (hevc_pcabac.h), must give the same bytes
-            std::vector<std::vector<uint16_t>> cu(geo.ctb_w);
-            for (int cx = 0; cx < geo.ctb_w; cx++) {
+            std::vector<std::vector<uint16_t>> cu(x1 - x0);
+            for (int cx = x0; cx < x1; cx++) {
                 const uint16_t* b = &bins[(size_t)(cy * geo.ctb_w + cx) * kCuBinCap];
-                cu[cx].assign(b, b + bin_n[cy * geo.ctb_w + cx]);
+                cu[cx - x0].assign(b, b + bin_n[cy * geo.ctb_w + cx]);
             }
             if (r + 1 < rows) cu.back().push_back((uint16_t)((1u << 8) | CTX_TERM));   // end_of_subset_one_bit
             sub[r] = pc_code_row_host(cu, ctx);
-            for (int cx = 0; cx < 2 && cx < geo.ctb_w; cx++)
+            for (int cx = x0; cx < x0 + 2 && cx < x1; cx++)
                 for (int i = 0; i < bin_n[cy * geo.ctb_w + cx]; i++) {
                     const uint16_t e = bins[(size_t)(cy * geo.ctb_w + cx) * kCuBinCap + i];
                     if ((e & 0x80ffu) < (uint32_t)CTX_TERM) ctx_update(ctx[e & 0xffu], (e >> 8) & 1);
@@ -625,15 +632,15 @@ std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
             continue;
         }
         size_t cap = 64;
-        for (int cx = 0; cx < geo.ctb_w; cx++) cap += (size_t)bin_n[cy * geo.ctb_w + cx] * 2 + 8;
+        for (int cx = x0; cx < x1; cx++) cap += (size_t)bin_n[cy * geo.ctb_w + cx] * 2 + 8;
         sub[r].assign(cap, 0);
         CabacEncoder e;
         e.start(sub[r].data());
-        for (int cx = 0; cx < geo.ctb_w; cx++) {
+        for (int cx = x0; cx < x1; cx++) {
             const int idx = cy * geo.ctb_w + cx;
             const uint16_t* b = &bins[(size_t)idx * kCuBinCap];
             for (int i = 0; i < bin_n[idx]; i++) e.code_entry(b[i], ctx);
-            if (cx == 1) memcpy(sync, ctx, CTX_COUNT);   // WPP storage after the second CTB
+            if (cx == x0 + 1) memcpy(sync, ctx, CTX_COUNT);   // WPP storage after the second CTB
         }
         if (r + 1 < rows) e.terminate(1);   // end_of_subset_one_bit
         e.finish();
@@ -646,9 +653,9 @@ std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
     uint8_t hdr[1024];
     memset(hdr, 0, sizeof(hdr));
     SliceHeader h;
-    h.first_slice = s == 0;
+    h.address = cy0 * geo.ctb_w + x0;
+    h.first_slice = h.address == 0;
     h.idr = idr;
-    h.address = t.first_row * geo.ctb_w;
     h.address_bits = geo.addr_bits;
     h.slice_type = p_slice ? 1 : 2;
     h.poc_lsb = poc & ((1 << kLog2MaxPocLsb) - 1);
@@ -663,6 +670,19 @@ std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
     std::vector<uint8_t> nal;
     append_nal(nal, idr ? kNalIdrWRadl : kNalTrailR, rbsp.data(), rbsp.size());
     return nal;
+}
+
+std::vector<uint8_t> CpuHevcEncoder::write_slice(int s, bool idr) {
+    const SliceTask& t = fe.tasks[s];
+    const SliceMap m = smap();
+    if (!m.split(t.first_row)) return write_segment(t, t.first_row, t.num_rows, 0, geo.ctb_w, idr);
+    std::vector<uint8_t> out;   // a split intra slice: one slice NAL per row segment
+    for (int cy = t.first_row; cy < t.first_row + t.num_rows; cy++)
+        for (int k = 0; k < m.nseg(cy); k++) {
+            const std::vector<uint8_t> nal = write_segment(t, cy, 1, m.x0(cy, k), m.x1(cy, k), idr);
+            out.insert(out.end(), nal.begin(), nal.end());
+        }
+    return out;
 }
 
 void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
@@ -694,7 +714,7 @@ void CpuHevcEncoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id,
             }
         }
         deblock_picture(fe.rec[0].data(), fe.rec[1].data(), fe.rec[2].data(), fe.g.stride_y, fe.g.stride_c,
-                        cus.data(), geo.ctb_w, geo.ctb_h, geo.rows_per_slice);
+                        cus.data(), geo.ctb_w, geo.ctb_h, smap());
         sao_analyse();
         for (int s = 0; s < ns; s++) binarize_slice(s);
     };

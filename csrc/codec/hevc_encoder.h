@@ -57,6 +57,13 @@ inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
     return f;
 }
 
+// Slices per CTB row of intra slices (SliceMap::K): ceil(ctb_w / kIntraSegCtbs);
+// SK_HEVC_SEG_CTBS=<n> sets the segment width (tests exercise the split at small sizes).
+inline int intra_seg_k(int ctb_w) {
+    const char* e = getenv("SK_HEVC_SEG_CTBS");
+    return intra_seg_count(ctb_w, e && atoi(e) > 0 ? atoi(e) : kIntraSegCtbs);
+}
+
 int choose_level_idc(int w, int h, float fps);
 // VPS + SPS + PPS NAL units (Annex B) for a w x h picture.
 void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<uint8_t>& out);
@@ -89,8 +96,10 @@ class CpuHevcEncoder {
     // the merge pass per row (sao_analyse); the filter into the reference (sao_apply)
     void sao_analyse();
     void sao_apply();
-    // CABAC substreams of slice s (one per CTB row) -> slice NAL (Annex B)
+    // CABAC substreams of slice s (one per CTB row) -> slice NAL (Annex B); a split intra
+    // slice -> one NAL per row segment (SliceMap)
     std::vector<uint8_t> write_slice(int s, bool idr);
+    std::vector<uint8_t> write_segment(const h264::SliceTask& t, int cy0, int rows, int x0, int x1, bool idr);
     long long payload_bytes_ = 0;   // substream bytes of the frame being written (K10)
     bool pc_host_ = getenv("SK_HEVC_PCABAC") != nullptr;   // write rows with pc_code_row_host
 
@@ -106,6 +115,8 @@ class CpuHevcEncoder {
     std::vector<long long> sao_md;     // kSaoMd per CTB: merge-candidate distortions (sao_merge_dists)
     std::vector<uint8_t> param_sets;   // VPS + SPS + PPS
     int poc = 0;                       // POC of the next picture
+    int seg_k = 1;                     // intra slices: slices per CTB row (SliceMap::K)
+    SliceMap smap() const { return SliceMap{fe.tasks.data(), geo.ctb_w, geo.rows_per_slice, seg_k}; }
 
    private:
     void load_cu_src(int cx, int cy, uint8_t* y, uint8_t* u, uint8_t* v) const;

@@ -43,18 +43,18 @@ SK_HD int sao_edge_idx(int c, int a, int b) {
     return e <= 2 ? (e == 2 ? 0 : e + 1) : e;
 }
 
-// Geometry of one plane for SAO: w x h samples, CTB side n (16 luma / 8 chroma), slice
-// rows: a sample row's slice is (y / n) / rows_per_slice.
+// Geometry of one plane for SAO: w x h samples, CTB side n (16 luma / 8 chroma), and
+// the picture's slice layout (SliceMap, hevc_core.h).
 struct SaoPlane {
-    int w, h, n, rows_per_slice;
-    SK_HD int slice_of(int y) const { return (y / n) / rows_per_slice; }
+    int w, h, n;
+    SliceMap m;
     // Whether an edge-offset class may change sample (x, y): both neighbours inside the
     // picture and in the sample's slice.
     SK_HD bool eo_ok(int cls, int x, int y) const {
-        const int s = slice_of(y);
+        const int s = m.id(x / n, y / n);
         for (int i = 0; i < 2; i++) {
             const int xx = x + sao_dx(cls, i), yy = y + sao_dy(cls, i);
-            if (xx < 0 || yy < 0 || xx >= w || yy >= h || slice_of(yy) != s) return false;
+            if (xx < 0 || yy < 0 || xx >= w || yy >= h || m.id(xx / n, yy / n) != s) return false;
         }
         return true;
     }
@@ -221,14 +221,17 @@ SK_HD void sao_merge_dists(const SaoStats* st_x, const SaoParams* own_row, int x
     for (int j = 0; j < kSaoMergeWin; j++) md[j] = x - 1 - j >= 0 ? sao_params_dist(st_x, own_row[x - 1 - j]) : 0;
     md[kSaoMergeWin] = sao_params_dist(st_x, own_row[x]);
 }
+// m / cy: the row's slices (a CTB merges left only inside its slice, and codes the
+// merge-up flag only under a CTB of its slice).
 SK_HD void sao_row_merge(const long long* md_row, const SaoParams* own, const long long* own_cost, int ctb_w, int qp,
-                         bool has_up, SaoParams* out) {
+                         const SliceMap& m, int cy, SaoParams* out) {
     const int lam = sao_lambda(qp);
     int src = 0;   // CTB whose own parameters the previous CTB's final parameters are
     for (int x = 0; x < ctb_w; x++) {
         SaoParams p = own[x];
         int sx = x;
-        if (x > 0) {
+        const bool has_up = m.top(x, cy);
+        if (m.left(x, cy)) {
             const int j = x - 1 - src;
             const long long* md = md_row + (size_t)x * kSaoMd;
             bool ok = true;

@@ -47,6 +47,11 @@ struct HevcArgs {
     long long* sao_md;          // [ctbs][kSaoMd] merge-candidate distortions (sao_merge_dists)
     SaoParams* sao;             // [ctbs] final parameters after the row merge pass (k_hevc_sao_row)
     h264::gpu::Planes sao_tmp;  // filtered samples of the CTBs SAO changes, copied back into f.rec
+    // intra slices cut every CTB row into seg_k slices (SliceMap, hevc_core.h); the
+    // substream arrays (sync, sub_size, sub_esc, row_off, row_bits) hold mb_h * seg_k
+    // slots (slot = cy * seg_k + k, k = 0 for whole rows); segment k of row cy codes its
+    // substream at sub + cy * sub_stride + x0 * kSubstreamCtbBytes + 64 * k
+    int seg_k;
 };
 
 // redo: the K10 re-code flag (CBR sessions): the coding kernels run a second time,

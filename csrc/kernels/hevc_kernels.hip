@@ -44,6 +44,14 @@ __device__ __forceinline__ int wsum(int v) {
 // (f.gate = the re-code flag); they return at once unless the frame overflowed.
 __device__ __forceinline__ bool second_pass_skipped(const FrameArgs& f) { return f.gate && *f.gate == 0; }
 
+// The picture's slice layout (hevc_core.h SliceMap) and the substream of a slot.
+__device__ __forceinline__ SliceMap smap(const HevcArgs& A) {
+    return SliceMap{A.f.tasks, A.f.mb_w, A.f.rows_per_slice, A.seg_k};
+}
+__device__ __forceinline__ size_t sub_base(const HevcArgs& A, const SliceMap& m, int cy, int k) {
+    return (size_t)cy * A.sub_stride + (size_t)m.x0(cy, k) * kSubstreamCtbBytes + 64 * (size_t)k;
+}
+
 // Per-wave LDS working set of one CU. Sample rasters (src, pred, rec*) hold the CU's
 // 384 samples: Y 16x16 (pitch 16) | Cb 8x8 | Cr 8x8 (pitch 8).
 struct CuLds {
@@ -582,7 +590,8 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     const int cx = idx % f.mb_w, cy = idx / f.mb_w;
     const SliceTask t = f.tasks[cy / f.rows_per_slice];
     if (t.final_action != ACT_I) return;
-    const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < f.mb_w;
+    const SliceMap m = smap(A);
+    const bool left = m.left(cx, cy), top = m.top(cx, cy), tr = m.top_right(cx, cy);
     load_src(L, f, cx, cy);
     for (int u = 0; u < 16; u++) {
         const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
@@ -872,7 +881,7 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
     __shared__ int8_t T[kTabT];
     const FrameArgs& f = A.f;
     const SliceTask t = f.tasks[blockIdx.x];
-    if (t.final_action != ACT_I) return;   // block-uniform
+    if (t.final_action != ACT_I || A.seg_k > 1) return;   // block-uniform; split rows: k_hevc_intra_seg
     load_t16(T);
     __syncthreads();
     const int w = threadIdx.x >> 6, l = lane();
@@ -908,6 +917,52 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
     }
 }
 
+// I slices cut into row segments (SliceMap, seg_k > 1): one wave per segment, its CTBs
+// left to right; no top neighbours, so the segments of all rows run at once (a 4K key
+// frame: 810 chains of 40 CTBs instead of 34 workgroups of 246 steps).
+__global__ __launch_bounds__(256) void k_hevc_intra_seg(HevcArgs A) {
+    if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
+    __shared__ CuLds Lw[4];
+    __shared__ int8_t T[kTabT];
+    const FrameArgs& f = A.f;
+    load_t16(T);
+    __syncthreads();   // the only block barrier: waves run independent segments below
+    const int w = threadIdx.x >> 6, l = lane();
+    const int slot = blockIdx.x * 4 + w;
+    if (slot >= f.mb_h * A.seg_k) return;
+    const SliceMap m = smap(A);
+    const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
+    if (!m.split(cy)) return;
+    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    CuLds& L = Lw[w];
+    __builtin_amdgcn_s_setprio(3);
+    for (int cx = m.x0(cy, k); cx < m.x1(cy, k); cx++) {
+        const int idx = cy * f.mb_w + cx;
+        const bool left = m.left(cx, cy);
+        const int mode = __builtin_amdgcn_readfirstlane(A.cus[idx].intra_mode);
+        load_src(L, f, cx, cy);
+        wsync();
+        CuInfo cu;
+        memset(&cu, 0, sizeof(cu));
+        const uint8_t* rec = intra_cu(L, T, f, cx, cy, left, false, false, mode, t.qp, A.coefs + (size_t)idx * kCoefPerCu,
+                                      cu, A.reg_steps != 0);
+        store_rec(rec, f, cx, cy);
+        if (l == 0) {
+            cu.mode = CU_INTRA;
+            cu.intra_mode = (uint8_t)mode;
+            cu.qp = (uint8_t)t.qp;
+            A.cus[idx] = cu;
+            f.me[idx].mvx = 0;
+            f.me[idx].mvy = 0;
+            f.me[idx].ref = 0;
+            f.me[idx].fx = f.me[idx].fy = 0;
+        }
+        // this CTB's reconstruction (global memory) is the next one's left neighbour
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wsync();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // CU syntax -> bin entries: one thread per CU (a wave binarises 64 CUs at once).
 __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
@@ -919,7 +974,8 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
     const int cx = idx % f.mb_w, cy = idx / f.mb_w;
     const SliceTask t = f.tasks[cy / f.rows_per_slice];
     const bool p_slice = t.final_action != ACT_I;
-    const bool left = cx > 0, top = cy > t.first_row;
+    const SliceMap m = smap(A);
+    const bool left = m.left(cx, cy), top = m.top(cx, cy);
     const CuInfo cu = A.cus[idx];
     const int skip_ctx = (left && A.cus[idx - 1].mode == CU_SKIP) + (top && A.cus[idx - f.mb_w].mode == CU_SKIP);
     const int cand_a = (left && A.cus[idx - 1].mode == CU_INTRA) ? A.cus[idx - 1].intra_mode : 1;
@@ -927,8 +983,12 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
     sao_bins(w, A.sao[idx], left, top);   // CTB-level SAO syntax (k_hevc_sao_row's decision)
     code_cu(w, cu, A.coefs + (size_t)idx * kCoefPerCu, p_slice, skip_ctx, cand_a);
     const bool last_row = cy == t.first_row + t.num_rows - 1;
-    w.term(last_row && cx == f.mb_w - 1);
-    if (!last_row && cx == f.mb_w - 1) w.term(1);   // end_of_subset_one_bit closes the row's substream
+    if (m.split(cy)) {   // each row segment is a slice: end_of_slice_segment_flag at its end
+        w.term(cx + 1 == m.x1(cy, m.seg(cx, cy)));
+    } else {
+        w.term(last_row && cx == f.mb_w - 1);
+        if (!last_row && cx == f.mb_w - 1) w.term(1);   // end_of_subset_one_bit closes the row's substream
+    }
     A.bin_n[idx] = w.n;
 }
 
@@ -956,8 +1016,13 @@ __global__ __launch_bounds__(192) void k_hevc_sync(HevcArgs A) {
     if (c >= CTX_COUNT) return;
     const int it = t.final_action == ACT_I ? 0 : 1;
     const uint8_t init = ctx_init_state(HEVC_CTX_INIT[it][c], t.qp);
+    const int K = A.seg_k;
+    if (smap(A).split(t.first_row)) {   // every row segment is a slice: initial states
+        for (int i = 0; i < t.num_rows * K; i++) A.sync[((size_t)t.first_row * K + i) * CTX_COUNT + c] = init;
+        return;
+    }
     uint32_t st = init;
-    A.sync[(size_t)t.first_row * CTX_COUNT + c] = init;
+    A.sync[(size_t)t.first_row * K * CTX_COUNT + c] = init;
     for (int r = 1; r < t.num_rows; r++) {
         const int prev = t.first_row + r - 1;
         if (f.mb_w >= 2) {
@@ -974,7 +1039,7 @@ __global__ __launch_bounds__(192) void k_hevc_sync(HevcArgs A) {
         } else {
             st = init;
         }
-        A.sync[(size_t)(t.first_row + r) * CTX_COUNT + c] = (uint8_t)st;
+        A.sync[(size_t)(t.first_row + r) * K * CTX_COUNT + c] = (uint8_t)st;
     }
 }
 
@@ -1064,16 +1129,20 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     __shared__ uint8_t nl_s[4][64];                // CABAC_NEXT_LPS
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
-    const int cy = blockIdx.x, c = blockIdx.y * 4 + w;
+    const int slot = blockIdx.x, c = blockIdx.y * 4 + w;
     if (c >= CTX_COUNT) return;
+    const SliceMap m = smap(A);
+    const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
+    if (k >= m.nseg(cy)) return;   // slot of a whole row: only k = 0
+    const int xa = m.x0(cy, k), xb = m.x1(cy, k);
     uint2* L = lst_s[w];
     const int row0 = cy * f.mb_w;
     const uint64_t lt = (1ull << l) - 1;
     int n = 0, tot = 0;
-    for (int g = 0; g < f.mb_w; g += 64) {
+    for (int g = xa; g < xb; g += 64) {
         const int cx = g + l;
         int lo = 0, cnt = 0;
-        if (cx < f.mb_w) {
+        if (cx < xb) {
             const uint16_t* co = A.coff + ((size_t)cy * kPcCtxOff + c) * f.mb_w + cx;
             lo = co[0];
             cnt = co[f.mb_w] - lo;
@@ -1094,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     if (l == 0) L[n] = make_uint2(0u, (uint32_t)tot);
     wsync();
     if (tot == 0) return;
-    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane(A.sync[(size_t)cy * CTX_COUNT + c]);
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane(A.sync[(size_t)slot * CTX_COUNT + c]);
     uint8_t* nl = nl_s[w];
     nl[l] = CABAC_NEXT_LPS[l];
     wsync();
@@ -1236,8 +1305,12 @@ __global__ __launch_bounds__(256) void k_pc_rmap(HevcArgs A) {
 __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
-    const int cy = blockIdx.x, l = lane();
-    const int row0 = cy * f.mb_w, nw = f.mb_w;
+    const int slot = blockIdx.x, l = lane();
+    const SliceMap m = smap(A);
+    const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
+    if (k >= m.nseg(cy)) return;
+    // the segment's CTBs as a row of their own: chunk j = CTB row0 + j
+    const int row0 = cy * f.mb_w + m.x0(cy, k), nw = m.x1(cy, k) - m.x0(cy, k);
     constexpr int D = 8;
     uint4 buf[D];
 #pragma unroll
@@ -1271,7 +1344,7 @@ __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
             buf[d] = reinterpret_cast<const uint4*>(A.rmap + (size_t)(row0 + nx) * 256)[l];
         }
     }
-    if (l == 0) A.row_bits[cy] = T;
+    if (l == 0) A.row_bits[slot] = T;
 }
 
 // One wave per CTB: the chunk coded from V = 0 (PcCoder, scalar state) and fully
@@ -1284,12 +1357,14 @@ __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
     const int idx = blockIdx.x * 4 + w;
     if (idx >= f.mb_w * f.mb_h) return;
     const int cy = idx / f.mb_w, cx = idx - cy * f.mb_w;
+    const SliceMap m = smap(A);
+    const int k = m.seg(cx, cy), slot = cy * A.seg_k + k;
     const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.cu_t[idx]);
     const uint32_t tn = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(cx + 1 < f.mb_w ? A.cu_t[idx + 1] : A.row_bits[cy]));
+        (int)(cx + 1 < m.x1(cy, k) ? A.cu_t[idx + 1] : A.row_bits[slot]));
     const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.cu_r[idx]);
     const int g0 = (int)(t0 >> 3), nex = (int)(tn >> 3) - g0;
-    uint8_t* out = A.sub + (size_t)cy * A.sub_stride + g0;
+    uint8_t* out = A.sub + sub_base(A, m, cy, k) + g0;
     uint8_t* tl = A.tail + (size_t)idx * 2;
     int ob = 0, opos = 0, flushed = 0;
     uint32_t acc = 0;
@@ -1344,11 +1419,17 @@ __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
 __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
-    const int cy = blockIdx.x, l = lane();
-    const int row0 = cy * f.mb_w;
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.row_bits[cy]);
+    const int slot = blockIdx.x, l = lane();
+    const SliceMap m = smap(A);
+    const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
+    if (k >= m.nseg(cy)) {   // unused slot: no substream (k_rc_account sums every slot)
+        if (l == 0) A.sub_size[slot] = A.sub_esc[slot] = 0;
+        return;
+    }
+    const int row0 = cy * f.mb_w + m.x0(cy, k), nw = m.x1(cy, k) - m.x0(cy, k);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.row_bits[slot]);
     const int excl = (int)(T >> 3), nbytes = excl + 2;
-    uint8_t* out = A.sub + (size_t)cy * A.sub_stride;
+    uint8_t* out = A.sub + sub_base(A, m, cy, k);
     int wb = 0;
     uint32_t win = 0;
     auto load_win = [&]() __attribute__((always_inline)) {
@@ -1381,15 +1462,15 @@ __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
         win = (uint32_t)writelane((int)((wv & ~(0xffu << sh)) | (byte << sh)), o >> 2, (int)win);
     };
     load_win();
-    for (int g = 0; g < f.mb_w; g += 64) {
-        const int cx = g + l;
+    for (int g = 0; g < nw; g += 64) {
+        const int cx = g + l;   // CTB row0 + cx of the segment
         int p_l = 0, t_l = 0;
-        if (cx < f.mb_w) {
-            p_l = (int)((cx + 1 < f.mb_w ? A.cu_t[row0 + cx + 1] : T) >> 3);
+        if (cx < nw) {
+            p_l = (int)((cx + 1 < nw ? A.cu_t[row0 + cx + 1] : T) >> 3);
             t_l = (int)((uint32_t)A.tail[2 * (row0 + cx)] | ((uint32_t)A.tail[2 * (row0 + cx) + 1] << 8));
         }
-        const int m = f.mb_w - g < 64 ? f.mb_w - g : 64;
-        for (int j = 0; j < m; j++) {
+        const int mm = nw - g < 64 ? nw - g : 64;
+        for (int j = 0; j < mm; j++) {
             const int p = __builtin_amdgcn_readlane(p_l, j);
             const uint32_t tv = (uint32_t)__builtin_amdgcn_readlane(t_l, j);
             if (p + 2 > wb + 256) {
@@ -1439,9 +1520,9 @@ __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
         last_nz = max(last_nz, __shfl(p, 63));
     }
     if (l == 0) {
-        A.sub_size[cy] = size;
-        A.sub_esc[cy] = size + ins_total;
-        if (A.dbg) {
+        A.sub_size[slot] = size;
+        A.sub_esc[slot] = size + ins_total;
+        if (A.dbg && k == 0) {
             A.dbg[4 * cy + 0] = 0;
             A.dbg[4 * cy + 1] = T;
             A.dbg[4 * cy + 2] = (unsigned long long)size;
@@ -1450,19 +1531,80 @@ __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
     }
 }
 
-// Slice header + NAL prefix per slice; substream offsets for k_hevc_ep_copy.
+// Slice header + NAL prefix per slice; substream offsets for k_hevc_ep_copy. A split
+// intra slice (SliceMap) is one slice NAL per row segment, laid out back to back in the
+// slice's output slot: lane j writes segment j's header, a scan places them.
+constexpr int kMaxSegsPerSlice = 256;
 __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
     __shared__ uint8_t hdr[1024];
     __shared__ int esc[256];
+    __shared__ int offs[kMaxSegsPerSlice + 1];
+    __shared__ uint8_t shdr[64][48];
     const FrameArgs& f = A.f;
     const int s = blockIdx.x;
     const SliceTask t = f.tasks[s];
     const int l = lane();
-    for (int i = l; i < 1024; i += 64) hdr[i] = 0;
-    for (int i = l; i < t.num_rows; i += 64) esc[i] = A.sub_esc[t.first_row + i];
+    const SliceMap m = smap(A);
     bool idr = true;
     for (int i = l; i < f.num_slices; i += 64) idr &= f.tasks[i].final_action == ACT_I && f.tasks[i].idr_on_intra;
     idr = __syncthreads_and(idr);
+    auto seg_header = [&](int cy, int k, uint8_t* buf) {   // header RBSP of a row segment
+        for (int i = 0; i < 48; i++) buf[i] = 0;
+        SliceHeader h;
+        h.address = cy * f.mb_w + m.x0(cy, k);
+        h.first_slice = h.address == 0;
+        h.idr = idr;
+        h.address_bits = A.addr_bits;
+        h.slice_type = 2;
+        h.poc_lsb = t.frame_num & ((1 << kLog2MaxPocLsb) - 1);
+        h.qp_delta = t.qp - 26;
+        h.num_entry = 0;
+        h.entry = nullptr;
+        return write_slice_header(buf, h);
+    };
+    if (m.split(t.first_row)) {
+        const int K = A.seg_k, nseg = t.num_rows * K;
+        int run = 0;
+        for (int base = 0; base < nseg; base += 64) {   // pass 1: NAL lengths -> offsets
+            const int j = base + l;
+            int len = 0;
+            if (j < nseg) {
+                const int cy = t.first_row + j / K, k = j % K;
+                const int hn = seg_header(cy, k, shdr[l]);
+                len = 6 + ep_escape(shdr[l], hn, nullptr) + A.sub_esc[cy * K + k];
+            }
+            int inc = len;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(inc, o);
+                if (l >= o) inc += v;
+            }
+            if (j < nseg) offs[j] = run + inc - len;
+            run += __shfl(inc, 63);
+        }
+        __syncthreads();
+        const int total = run;
+        const bool fits = total <= A.out_slot;
+        uint8_t* o = fits ? A.out_host + (size_t)s * A.out_slot : A.out_dev + (size_t)s * A.out_dev_slot;
+        for (int base = 0; base < nseg; base += 64) {   // pass 2: NAL prefixes and headers
+            const int j = base + l;
+            if (j < nseg) {
+                const int cy = t.first_row + j / K, k = j % K;
+                const int hn = seg_header(cy, k, shdr[l]);
+                uint8_t* d = o + offs[j];
+                d[0] = 0; d[1] = 0; d[2] = 0; d[3] = 1;
+                d[4] = (uint8_t)((idr ? kNalIdrWRadl : kNalTrailR) << 1);
+                d[5] = 1;
+                const int hesc = ep_escape(shdr[l], hn, d + 6);
+                A.row_off[cy * K + k] = offs[j] + 6 + hesc;
+            }
+        }
+        if (l == 0) __hip_atomic_store(A.out_size + s, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    for (int i = l; i < 1024; i += 64) hdr[i] = 0;
+    for (int i = l; i < t.num_rows; i += 64) esc[i] = A.sub_esc[(t.first_row + i) * A.seg_k];
+    __syncthreads();
     if (l == 0) {
         SliceHeader h;
         h.first_slice = s == 0;
@@ -1479,7 +1621,7 @@ __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
         int total = 6 + hesc;
         int off = total;
         for (int r = 0; r < t.num_rows; r++) {
-            A.row_off[t.first_row + r] = off;
+            A.row_off[(t.first_row + r) * A.seg_k] = off;
             off += esc[r];
         }
         total = off;
@@ -1493,19 +1635,22 @@ __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
     }
 }
 
-// Emulation prevention + copy of one row's substream, wave-parallel: byte i of the
+// Emulation prevention + copy of one slot's substream (a row, or a row segment), wave-parallel: byte i of the
 // substream is preceded by an inserted 0x03 iff it is <= 3 and the zero run before it
 // has even length >= 2 (equivalent to the sequential rule; the previous piece ends in a
 // non-zero byte).
 __global__ __launch_bounds__(64) void k_hevc_ep_copy(HevcArgs A) {
     const FrameArgs& f = A.f;
-    const int cy = blockIdx.x;
+    const int slot = blockIdx.x;
+    const SliceMap m = smap(A);
+    const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
+    if (k >= m.nseg(cy)) return;
     const int s = cy / f.rows_per_slice;
     const int total = __hip_atomic_load(A.out_size + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const bool fits = total <= A.out_slot;
-    uint8_t* o = (fits ? A.out_host + (size_t)s * A.out_slot : A.out_dev + (size_t)s * A.out_dev_slot) + A.row_off[cy];
-    const uint8_t* in = A.sub + (size_t)cy * A.sub_stride;
-    const int n = A.sub_size[cy];
+    uint8_t* o = (fits ? A.out_host + (size_t)s * A.out_slot : A.out_dev + (size_t)s * A.out_dev_slot) + A.row_off[slot];
+    const uint8_t* in = A.sub + sub_base(A, m, cy, k);
+    const int n = A.sub_size[slot];
     const int l = lane();
     int last_nz = -1;   // index of the last non-zero byte before the current chunk (-1: none yet,
                         // the byte before the substream is non-zero)
@@ -1555,14 +1700,16 @@ __global__ __launch_bounds__(256) void k_hevc_dbk_v(HevcArgs A) {
     const int cw = f.mb_w, ch = f.mb_h, ne = cw - 1, nel = 2 * cw - 1;
     const int e = blockIdx.x * 256 + threadIdx.x;
     const int nl = ch * 4 * nel, nc = ch * 8 * ne;
+    const SliceMap m = smap(A);
     if (e < nl) {
         const int x = 8 * (1 + e % nel), seg = e / nel;
+        if (!(x & 8) && !m.same((x >> 4) - 1, seg >> 2, x >> 4, seg >> 2)) return;   // slice boundary
         dbk_luma_edge(f.rec.y, f.stride_y, A.cus, cw, true, x, 4 * seg);
     } else if (e < nl + 2 * nc) {
         const int k0 = e - nl, plane = k0 / nc, k = k0 % nc;
         const int cx = 1 + k % ne, line = k / ne, cy = line >> 3;
         const CuInfo p = A.cus[cy * cw + cx - 1], q = A.cus[cy * cw + cx];
-        if (cu_intra_edge(p, q))
+        if (cu_intra_edge(p, q) && m.same(cx - 1, cy, cx, cy))
             dbk_chroma_line((plane ? f.rec.v : f.rec.u) + (size_t)line * f.stride_c + cx * 8, 1, (p.qp + q.qp + 1) >> 1);
     }
 }
@@ -1574,14 +1721,15 @@ __global__ __launch_bounds__(256) void k_hevc_dbk_h(HevcArgs A) {
     if (nel <= 0) return;
     const int e = blockIdx.x * 256 + threadIdx.x;
     const int nl = nel * cw * 4, nc = ne * cw * 8;
+    const SliceMap m = smap(A);
     if (e < nl) {
         const int y = 8 * (1 + e / (cw * 4)), x4 = e % (cw * 4);
-        if (!(y & 8) && (y >> 4) % f.rows_per_slice == 0) return;   // slice boundary
+        if (!(y & 8) && !m.same(x4 >> 2, (y >> 4) - 1, x4 >> 2, y >> 4)) return;   // slice boundary
         dbk_luma_edge(f.rec.y, f.stride_y, A.cus, cw, false, y, 4 * x4);
     } else if (e < nl + 2 * nc) {
         const int k0 = e - nl, plane = k0 / nc, k = k0 % nc;
         const int cy = 1 + k / (cw * 8), col = k % (cw * 8), cx = col >> 3;
-        if (cy % f.rows_per_slice == 0) return;
+        if (!m.same(cx, cy - 1, cx, cy)) return;
         const CuInfo p = A.cus[(cy - 1) * cw + cx], q = A.cus[cy * cw + cx];
         if (cu_intra_edge(p, q))
             dbk_chroma_line((plane ? f.rec.v : f.rec.u) + (size_t)(cy * 8) * f.stride_c + col, f.stride_c, (p.qp + q.qp + 1) >> 1);
@@ -1604,9 +1752,9 @@ __device__ __forceinline__ void ctb_sample(int i, int cx, int cy, int* c, int* x
         *c = 1 + (j >> 6); *x = cx * 8 + (j & 7); *y = cy * 8 + ((j >> 3) & 7);
     }
 }
-__device__ __forceinline__ SaoPlane sao_plane_of(const FrameArgs& f, int c) {
+__device__ __forceinline__ SaoPlane sao_plane_of(const HevcArgs& A, int c) {
     const int n = c ? 8 : 16;
-    return SaoPlane{f.mb_w * n, f.mb_h * n, n, f.rows_per_slice};
+    return SaoPlane{A.f.mb_w * n, A.f.mb_h * n, n, smap(A)};
 }
 
 __global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
@@ -1627,7 +1775,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
         for (int i = l; i < kCoefPerCu; i += 64) {
             int c, x, y;
             ctb_sample(i, cx, cy, &c, &x, &y);
-            const SaoPlane pl = sao_plane_of(f, c);
+            const SaoPlane pl = sao_plane_of(A, c);
             const int stride = c ? f.stride_c : f.stride_y;
             const uint8_t* rec = plane_of(f.rec, c);
             const int v = rec[(size_t)y * stride + x];
@@ -1699,7 +1847,7 @@ __global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
     __syncthreads();
     if (l == 0) {
         const SliceTask t = f.tasks[cy / f.rows_per_slice];
-        sao_row_merge(md, own, cost, W, t.qp, cy > t.first_row, A.sao + o);
+        sao_row_merge(md, own, cost, W, t.qp, smap(A), cy, A.sao + o);
     }
 }
 
@@ -1720,7 +1868,7 @@ __global__ __launch_bounds__(256) void k_hevc_sao_apply(HevcArgs A) {
         ctb_sample(i, cx, cy, &c, &x, &y);
         const int stride = c ? f.stride_c : f.stride_y;
         plane_of(A.sao_tmp, c)[(size_t)y * stride + x] =
-            (uint8_t)sao_apply_sample(p, c, sao_plane_of(f, c), plane_of(f.rec, c), stride, x, y);
+            (uint8_t)sao_apply_sample(p, c, sao_plane_of(A, c), plane_of(f.rec, c), stride, x, y);
     }
 }
 __global__ __launch_bounds__(256) void k_hevc_sao_copy(HevcArgs A) {
@@ -1748,6 +1896,8 @@ static void launch_code(const HevcArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_hevc_intra<4>, dim3(a.f.num_slices), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
+    const int slots = a.f.mb_h * a.seg_k;   // substream slots (SliceMap)
+    if (a.seg_k > 1) hipLaunchKernelGGL(k_hevc_intra_seg, dim3((slots + 3) / 4), dim3(256), 0, s, a);
     // in-loop deblocking, then the SAO decisions on the deblocked picture (CTB syntax)
     const int cw = a.f.mb_w, ch = a.f.mb_h;
     const int nv = ch * 4 * (2 * cw - 1) + 2 * ch * 8 * (cw - 1), nh = (2 * ch - 1) * cw * 4 + 2 * (ch - 1) * cw * 8;
@@ -1760,11 +1910,11 @@ static void launch_code(const HevcArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(192), 0, s, a);
-    hipLaunchKernelGGL(k_pc_model, dim3(a.f.mb_h, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pc_model, dim3(slots, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_rmap, dim3(nq), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_pc_compose, dim3(a.f.mb_h), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_pc_compose, dim3(slots), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_pc_code, dim3(nq), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_pc_merge, dim3(a.f.mb_h), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_pc_merge, dim3(slots), dim3(64), 0, s, a);
 }
 
 void launch_backend(const HevcArgs& a, hipStream_t s, int* redo) {
@@ -1774,12 +1924,12 @@ void launch_backend(const HevcArgs& a, hipStream_t s, int* redo) {
         HevcArgs b = a;
         b.f.gate = redo;
         for (int r = 0; r < h264::rc_max_recodes(1); r++) {
-            h264::gpu::launch_rc_guard_sizes(a.f, a.sub_size, a.f.mb_h, redo, r > 0, s);
+            h264::gpu::launch_rc_guard_sizes(a.f, a.sub_size, a.f.mb_h * a.seg_k, redo, r > 0, s);
             launch_code(b, s);
         }
     }
     hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h * a.seg_k), dim3(64), 0, s, a);
     // the SAO output becomes the reconstruction (k_commit copies it into the reference)
     const int nq = (n + 3) / 4;
     hipLaunchKernelGGL(k_hevc_sao_apply, dim3(nq), dim3(256), 0, s, a);

@@ -706,7 +706,7 @@ class HipBackend : public EncoderBackend {
                 ha.out_size = hevc_size_dev_[parity_];
                 ha.out_dev = hevc_fallback_[parity_];
                 hevc::gpu::launch_backend(ha, stream_, graph_guard_ ? args_.rc_redo : nullptr);
-                gpu::launch_rc_account(args_, ha.sub_size, g_.mb_h, 1, 0, stream_);
+                gpu::launch_rc_account(args_, ha.sub_size, g_.mb_h * ha.seg_k, 1, 0, stream_);
             } else {
                 gpu::launch_encode(args_, stream_, graph_guard_);
             }
@@ -743,12 +743,17 @@ class HipBackend : public EncoderBackend {
         h.coefs = dmalloc<int16_t>((size_t)n * hevc::kCoefPerCu);
         h.bins = dmalloc<uint16_t>((size_t)n * hevc::kCuBinCap, false);
         h.bin_n = dmalloc<int>(n);
-        h.sync = dmalloc<uint8_t>((size_t)g_.mb_h * hevc::CTX_COUNT);
-        h.sub_stride = g_.mb_w * hevc::kSubstreamCtbBytes + 64;
+        // intra slices: seg_k slices per CTB row (hevc_core.h SliceMap); per-substream
+        // arrays hold mb_h * seg_k slots
+        h.seg_k = hevc::intra_seg_k(g_.mb_w);
+        if (g_.rows_per_slice * h.seg_k > 256) throw std::runtime_error("HEVC: more than 256 row segments per slice");
+        const size_t slots = (size_t)g_.mb_h * h.seg_k;
+        h.sync = dmalloc<uint8_t>(slots * hevc::CTX_COUNT);
+        h.sub_stride = g_.mb_w * hevc::kSubstreamCtbBytes + 64 * h.seg_k + 64;
         h.sub = dmalloc<uint8_t>((size_t)g_.mb_h * h.sub_stride, false);
-        h.sub_size = dmalloc<int>(g_.mb_h);
-        h.sub_esc = dmalloc<int>(g_.mb_h);
-        h.row_off = dmalloc<int>(g_.mb_h);
+        h.sub_size = dmalloc<int>(slots);
+        h.sub_esc = dmalloc<int>(slots);
+        h.row_off = dmalloc<int>(slots);
         h.addr_bits = geo.addr_bits;
         if (g_.mb_w > 512) throw std::runtime_error("HEVC: more than 512 CTBs per row (8K) is not supported");
         h.srt = dmalloc<uint16_t>((size_t)n * hevc::kCuBinCap, false);
@@ -757,7 +762,7 @@ class HipBackend : public EncoderBackend {
         h.cu_t = dmalloc<uint32_t>(n);
         h.cu_r = dmalloc<uint16_t>(n);
         h.tail = dmalloc<uint8_t>((size_t)n * 2);
-        h.row_bits = dmalloc<uint32_t>(g_.mb_h);
+        h.row_bits = dmalloc<uint32_t>(slots);
         h.sao_stats = dmalloc<hevc::SaoStats>((size_t)3 * n, false);
         h.sao_own = dmalloc<hevc::SaoParams>(n);
         h.sao_cost = dmalloc<long long>(n);

@@ -168,3 +168,27 @@ def test_hevc_transform_tree_tools():
             seen["inter_split"] += int((split & (mode != 3)).sum())
     assert all(v > 0 for v in seen.values()), seen
     enc.close()
+
+
+@pytest.mark.parametrize("kind", ["desktop", "motion", "noise"])
+def test_hevc_split_intra_slices(kind, monkeypatch):
+    """Intra slices cut every CTB row into slices (hevc_core.h SliceMap; 40 CTBs at
+    full size, 4 here via SK_HEVC_SEG_CTBS so a 320-wide picture splits 5 ways): mid-row
+    slice starts under entropy_coding_sync, no top neighbours, no deblocking or SAO
+    across the cuts. The independent decoder returns the encoder's reconstruction
+    bit-exactly for key frames and the P frames predicted from them, and the serial and
+    chunk-parallel CABAC models agree on the split layout."""
+    monkeypatch.setenv("SK_HEVC_SEG_CTBS", "4")
+    W, H = 320, 192
+    res = _run(W, H, kind, 5, qp=27)
+    key = res[0][0].data[10:]
+    types = [(n[0] >> 1) & 63 for n in split_annexb(key)]
+    assert types[:3] == [32, 33, 34] and types[3:] == [19] * (12 * 5)   # 12 rows x 5 segments
+    assert all(q > 30 for _, _, q in res)
+    src = SyntheticDesktop(W, H, kind=kind)
+    ref = HevcEncoder(W, H, backend="cpu", qp=27)
+    monkeypatch.setenv("SK_HEVC_PCABAC", "1")
+    par = HevcEncoder(W, H, backend="cpu", qp=27)
+    for t in range(2):
+        f = src.frame(t)
+        assert [p.data for p in ref.encode(f, t)] == [p.data for p in par.encode(f, t)]
