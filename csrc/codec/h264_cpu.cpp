@@ -800,9 +800,10 @@ void CpuH264Encoder::finish_frame() {
             memcpy(&ref[p][(size_t)(y0 / 2) * g.stride_c], &rec[p][(size_t)(y0 / 2) * g.stride_c],
                    (size_t)(y1 - y0) / 2 * g.stride_c);
         if (cfg.deblock) {  // K7: the reference picture is the deblocked reconstruction
-            db_slice_info(mbs.data(), g.mb_w, t.first_row, t.num_rows, t.qp, dbinfo.data());
+            const int sub_len = intra_split(t, g.mb_w, cfg.deblock, cfg.intra4x4) ? kIntraSubMbs : 0;
+            db_slice_info(mbs.data(), g.mb_w, t.first_row, t.num_rows, t.qp, dbinfo.data(), sub_len);
             deblock_slice_cpu(ref[0].data(), ref[1].data(), ref[2].data(), g.stride_y, g.stride_c, dbinfo.data(),
-                              g.mb_w, t.first_row, t.num_rows);
+                              g.mb_w, t.first_row, t.num_rows, sub_len);
         }
         for (int mby = t.first_row; mby < t.first_row + t.num_rows; mby++)
             for (int mbx = 0; mbx < g.mb_w; mbx++) {

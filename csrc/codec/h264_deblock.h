@@ -197,25 +197,34 @@ SK_HD void db_chroma_line(int* line, const DbInfo& cur, const DbInfo& nb, bool h
 
 // Host-only helpers of the CPU reference (never called from device code).
 // QP_Y of every MB of a slice in raster order (skip / cbp-0 MBs inherit, 7.4.5).
+// sub_len > 0: the slice is coded as sub-slices of sub_len MBs (h264_encoder.h
+// intra_split): QP_Y,PRED restarts at the slice QP at every sub-slice start.
 inline void db_slice_info(const MbInfo* mbs, int mb_w, int first_row, int num_rows, int slice_qp,
-                          DbInfo* out) {
+                          DbInfo* out, int sub_len = 0) {
     int qp = slice_qp;
+    const int first = first_row * mb_w;
     for (int r = first_row; r < first_row + num_rows; r++)
         for (int x = 0; x < mb_w; x++) {
-            const MbInfo& mb = mbs[r * mb_w + x];
+            const int idx = r * mb_w + x;
+            if (sub_len > 0 && (idx - first) % sub_len == 0) qp = slice_qp;
+            const MbInfo& mb = mbs[idx];
             if (mb_has_qp_delta(mb)) qp = mb.qp;
-            out[r * mb_w + x] = db_info(mb, qp);
+            out[idx] = db_info(mb, qp);
         }
 }
 
 // Reference deblocking of one slice in place, raster macroblock order (8.7).
+// sub_len > 0: sub-slices of sub_len MBs; with disable_deblocking_filter_idc 2 no edge
+// between two of them is filtered (the left / top MB must lie in the MB's sub-slice).
 inline void deblock_slice_cpu(uint8_t* y, uint8_t* u, uint8_t* v, int stride_y, int stride_c, const DbInfo* info,
-                              int mb_w, int first_row, int num_rows) {
+                              int mb_w, int first_row, int num_rows, int sub_len = 0) {
+    const int first = first_row * mb_w;
     for (int r = first_row; r < first_row + num_rows; r++)
         for (int x = 0; x < mb_w; x++) {
             const DbTables& T = host_db_tables();
             const DbInfo& cur = info[r * mb_w + x];
-            const bool hl = x > 0, ht = r > first_row;
+            const int idx = r * mb_w + x, sub0 = sub_len > 0 ? first + ((idx - first) / sub_len) * sub_len : first;
+            const bool hl = x > 0 && idx - 1 >= sub0, ht = r > first_row && idx - mb_w >= sub0;
             const DbInfo& left = info[r * mb_w + x - (hl ? 1 : 0)];
             const DbInfo& top = info[(r - (ht ? 1 : 0)) * mb_w + x];
             int buf[20];

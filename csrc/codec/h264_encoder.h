@@ -116,12 +116,15 @@ static_assert(sizeof(SliceTask) == 48, "SliceTask layout");
 // kIntraSubMbs < mb_w, no MB has its top neighbour in its own sub-slice: a sub-slice
 // predicts from its left neighbours only, its reconstruction chain is at most
 // kIntraSubMbs MBs long, and the sub-slices of a stripe are independent (one wave
-// each on the GPU, k_code_intra_sub). Not with in-loop deblocking (slice-bounded
-// filtering would need the sub-slice map) or Intra4x4 (its top-right rules): those
-// keep one slice per stripe.
+// each on the GPU, k_code_intra_sub). With in-loop deblocking (disable_deblocking_filter_idc
+// 2) the filter keeps off the sub-slice edges and restarts the QP_Y chain at each
+// sub-slice (h264_deblock.h, k_deblock_prep / k_deblock_edges); Intra4x4 blocks see no
+// top or top-right neighbour outside their sub-slice (k_code_intra_sub's I_NxN path).
 constexpr int kIntraSubMbs = 40;
 SK_HD bool intra_split(const SliceTask& t, int mb_w, int deblock, int intra4x4) {
-    return t.final_action == ACT_I && mb_w > kIntraSubMbs && !deblock && !intra4x4;
+    (void)deblock;
+    (void)intra4x4;
+    return t.final_action == ACT_I && mb_w > kIntraSubMbs;
 }
 // Sub-slices of a split I slice; nmb = its MBs.
 SK_HD int intra_sub_count(int nmb) { return (nmb + kIntraSubMbs - 1) / kIntraSubMbs; }

@@ -2374,16 +2374,32 @@ __global__ __launch_bounds__(256) void k_code_intra_sub(FrameArgs a) {
             nb[l] = (uint8_t)v;
         }
         wave_sync();
+        const bool is_i4 = __builtin_amdgcn_readfirstlane((int)pre.type) == MB_I4x4;   // k_intra_prep's choice
+        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pre.i4lo);
+        const uint32_t m1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pre.i4hi);
         int pred_l[4], pred_c[4];
-        intra_pred_lanes(mode, cmode, nb, 0, zc, false, aL, pred_l, pred_c);
+        intra_pred_lanes(is_i4 ? 2 : mode, cmode, nb, 0, zc, false, aL, pred_l, pred_c);
         MbInfo mb;
         memset(&mb, 0, sizeof(mb));
-        mb.type = MB_I16x16;
-        mb.i16_mode = (uint8_t)mode;
         mb.chroma_mode = (uint8_t)cmode;
         int rec_l[4], rec_c[4];
-        code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c, a.coefs + (size_t)idx * kCoefPerMb, T,
-                nullptr, 0, start_qp);
+        if (is_i4) {   // I_NxN: blocks in decoding order from the reconstruction so far and the left column
+            mb.type = MB_I4x4;
+            mb.i4lo = m0;
+            mb.i4hi = m1;
+            auto smp = [&](int x, int y) __attribute__((always_inline)) -> int {
+                if (y >= 0 && x >= 0) return S.ry[y * 16 + x];
+                if (y < 0) return 0;   // no top / top-right neighbour inside a sub-slice
+                return nb[16 + y];
+            };
+            code_mb_i4(smp, src_l, src_c, pred_c, start_qp, t.qp, false, aL, false, S, mb, rec_l, rec_c,
+                       a.coefs + (size_t)idx * kCoefPerMb, T);
+        } else {
+            mb.type = MB_I16x16;
+            mb.i16_mode = (uint8_t)mode;
+            code_mb(src_l, pred_l, src_c, pred_c, t.qp, true, S, mb, rec_l, rec_c, a.coefs + (size_t)idx * kCoefPerMb,
+                    T, nullptr, 0, start_qp);
+        }
         wave_sync();
         if (lx + 3 == 15) right_y[w][ly] = (uint8_t)rec_l[3];
         if (l < 32 && clx + 3 == 7) right_c[w][comp][cly] = (uint8_t)rec_c[3];
@@ -2963,7 +2979,9 @@ __global__ __launch_bounds__(256) void k_deblock_prep(FrameArgs a) {
     if (idx >= nmb) return;
     const SliceTask t = a.tasks[(idx / a.mb_w) / a.rows_per_slice];
     if (t.final_action != ACT_P && t.final_action != ACT_I) return;
-    const int l = lane_id(), first = t.first_row * a.mb_w;
+    const int l = lane_id();
+    int first = t.first_row * a.mb_w;
+    if (split_i(a, t)) first += ((idx - first) / kIntraSubMbs) * kIntraSubMbs;   // K5: the chain restarts per sub-slice
     const MbInfo mb = a.mbs[idx];
     int qpy = mb.qp;
     if (!mb_has_qp_delta(mb)) {
@@ -3063,7 +3081,8 @@ __device__ __forceinline__ void db_filter_line(int* v, int bs, uint32_t par, boo
 //   w[4..6]  luma params (db_pack_par) of the left, top and internal edges
 //   w[7..9]  chroma params of the left, top and internal edges
 //   w[10]    edge mask: bit le (vertical) / 4 + le (horizontal) set if any bS of that edge is non-zero
-// The left edge of MB column 0 and the top edge of a slice's first row are off (idc 2).
+// The left edge of MB column 0 and the top edge of a slice's first row are off (idc 2),
+// as are the edges between the sub-slices of a split I slice.
 __global__ __launch_bounds__(256) void k_deblock_edges(FrameArgs a) {
     const int nmb = a.mb_w * a.mb_h;
     const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -3072,7 +3091,9 @@ __global__ __launch_bounds__(256) void k_deblock_edges(FrameArgs a) {
     const SliceTask t = a.tasks[mby / a.rows_per_slice];
     if (t.final_action != ACT_P && t.final_action != ACT_I) return;
     const DbInfo cur = a.db[idx];
-    const bool hl = mbx > 0, ht = mby > t.first_row;
+    int sub0 = t.first_row * a.mb_w;   // K5 sub-slices: no edge leaves the MB's sub-slice (idc 2)
+    if (split_i(a, t)) sub0 += ((idx - sub0) / kIntraSubMbs) * kIntraSubMbs;
+    const bool hl = mbx > 0 && idx - 1 >= sub0, ht = mby > t.first_row && idx - a.mb_w >= sub0;
     const DbInfo left = hl ? a.db[idx - 1] : cur, top = ht ? a.db[idx - a.mb_w] : cur;
     uint32_t w[12] = {};
 #pragma unroll

@@ -594,7 +594,7 @@ class HipBackend : public EncoderBackend {
         a.mb_nbits = dmalloc<int>(nmb);
         int max_slice_mbs = g_.rows_per_slice * g_.mb_w;
         // K5: split I slices put one NAL per sub-slice (h264_encoder.h intra_split)
-        const bool can_split = cfg_.codec == 0 && g_.mb_w > kIntraSubMbs && !cfg_.deblock && !a.intra4x4;
+        const bool can_split = cfg_.codec == 0 && g_.mb_w > kIntraSubMbs;
         a.nal_per_slice = can_split ? max_nals_per_slice(g_.rows_per_slice, g_.mb_w) : 1;
         a.sub_rbsp_words = (kIntraSubMbs * gpu::kMbSlotBytes + 1024) / 4;
         a.rbsp_slot_words = std::max((max_slice_mbs * gpu::kMbSlotBytes + 1024) / 4,

@@ -105,3 +105,52 @@ def test_intra4x4_with_deblocking_decodes():
             dec.feed(p.data)
         ref = np.frombuffer(enc.debug_buffer("ref_y", np.uint8), np.uint8).reshape(-1, (W + 15) // 16 * 16)[:H, :W]
         assert np.array_equal(dec.Y, ref), f"frame {t}"
+
+
+@pytest.mark.parametrize("deblock,intra4x4", [(True, False), (False, True), (True, True)])
+def test_subslice_keyframes_with_deblock_and_intra4x4(deblock, intra4x4):
+    """K5 sub-slices (h264_encoder.h intra_split) now also cover in-loop deblocking
+    (disable_deblocking_filter_idc 2: no filtering across sub-slice edges, the QP_Y chain
+    restarting per sub-slice) and Intra4x4 (no top / top-right neighbours in a
+    sub-slice): 1280 px wide, so every key-frame stripe splits into 40-MB slices. The
+    independent decoder reproduces the encoder's deblocked reference exactly."""
+    W, H = 1280, 96
+    frames = [_glyphs(W, H, s) for s in range(3)]
+    enc = H264Encoder(W, H, stripe_height=32, qp=26, use_paint_over=False, intra4x4=intra4x4, deblock=deblock)
+    dec = StripeDecoder(W, H)
+    n_slices = 0
+    for t, f in enumerate(frames):
+        if t != 1:
+            enc.request_keyframe()
+        pk = enc.encode(f, t)
+        decs = [dec.feed(p.data) for p in pk]
+        if t == 0:
+            n_slices = sum(p.data.count(b"\x00\x00\x01\x25") + p.data.count(b"\x00\x00\x01\x65") for p in pk)
+        ref = np.frombuffer(enc.debug_buffer("ref_y", np.uint8), np.uint8).reshape(-1, W)[:H, :W]
+        assert np.array_equal(dec.Y, ref), f"frame {t}: decoder != encoder reconstruction"
+        assert psnr(dec.Y, bgrx_to_y709(f)) > 30
+    assert n_slices == 3 * 4   # 3 stripes x (2 rows x 80 MBs / 40)
+    if intra4x4:
+        assert (enc.debug_buffer("mbs", MB_INFO_DTYPE)["type"] == 3).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deblock,intra4x4", [(True, False), (False, True), (True, True)])
+def test_subslice_keyframes_gpu_matches_cpu(deblock, intra4x4):
+    """The same at 1080p on the GPU: k_code_intra_sub (I_NxN path), k_deblock_prep /
+    k_deblock_edges with sub-slice bounds, byte-identical to the CPU."""
+    if hip_device_count() < 1:
+        pytest.skip("no HIP device")
+    W, H = 1920, 1080
+    src = SyntheticDesktop(W, H, kind="desktop")
+    kw = dict(stripe_height=64, qp=26, use_paint_over=False, intra4x4=intra4x4, deblock=deblock)
+    cpu, gpu = H264Encoder(W, H, backend="cpu", **kw), H264Encoder(W, H, backend="hip", **kw)
+    for t in range(4):
+        if t == 2:
+            cpu.request_keyframe()
+            gpu.request_keyframe()
+        f = src.frame(t)
+        pc, pg = cpu.encode(f, t), gpu.encode(f, t)
+        assert [p.data for p in pc] == [p.data for p in pg], f"frame {t}"
+        for name in ("ref_y", "ref_u"):
+            assert np.array_equal(cpu.debug_buffer(name), gpu.debug_buffer(name)), (t, name)
