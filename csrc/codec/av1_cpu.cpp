@@ -650,10 +650,15 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
     pk.data.insert(pk.data.end(), tu.begin(), tu.end());
     fe.ctl_.rate_account(payload);
     out.push_back(std::move(pk));
-    // every row of the picture was coded: the reconstruction is the next reference
+    // every row of the picture was coded: the reconstruction is the next reference;
+    // static slices were coded as zero-motion skips (zero MV field, k_av1_finish)
     for (int s = 0; s < ns; s++)
-        if (fe.tasks[s].final_action == ACT_NONE || fe.tasks[s].final_action == ACT_SKIPALL)
-            fe.tasks[s].final_action = ACT_P;
+        if (fe.tasks[s].final_action == ACT_NONE || fe.tasks[s].final_action == ACT_SKIPALL) {
+            h264::SliceTask& t = fe.tasks[s];
+            t.final_action = ACT_P;
+            for (int j = t.first_row * fe.g.mb_w; j < (t.first_row + t.num_rows) * fe.g.mb_w; j++)
+                fe.me[j].mvx = fe.me[j].mvy = 0;
+        }
     // in-loop deblocking (7.14) of the reconstruction: per plane all vertical edges, then
     // all horizontal ones
     const h264::Geometry& g = fe.g;

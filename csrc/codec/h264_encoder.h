@@ -373,28 +373,37 @@ class Controller {
 //   StateHeader | StripeState[num_slices + 1] (committed; last = picture state) |
 //   ref Y U V | ref1 Y U V (second reference) | last source Y U V (damage baseline) |
 //   mvfield int16[2 * num_mbs]
+// Session state (parallel/migrate.py), the same for every codec and both backends:
+//   StateHeader | StripeState[num_slices + 1] (controller; the last is the picture's, whose
+//   frame_num is also the next HEVC POC) | RcState (K10) | ref | ref1 | last source
+//   (4:2:0 planes) | MV field. The reference planes are what the next frame predicts from
+//   (HEVC: after deblocking + SAO, AV1: after loop filter + CDEF).
 struct StateHeader {
     char magic[4];          // "SKH4"
-    int32_t version;        // 2 (ref1 planes)
+    int32_t version;        // 3 (codec, RcState)
     int32_t W, H, stripe_height, fullframe, num_slices;
     int32_t started;        // a frame has been encoded (else the next one is all-dirty)
     int32_t qp, paint_qp;   // rate-control QPs in force
-    int32_t reserved[6];
+    int32_t codec;          // EncoderConfig::codec
+    int32_t reserved[5];
 };
 static_assert(sizeof(StateHeader) == 64, "StateHeader layout");
 
 inline size_t state_plane_bytes(const Geometry& g) {
     return (size_t)g.stride_y * g.plane_h_y + 2 * (size_t)g.stride_c * g.plane_h_c;
 }
+inline size_t state_head_bytes(const Geometry& g) {   // header + controller + rate control
+    return sizeof(StateHeader) + sizeof(StripeState) * (size_t)(g.num_slices + 1) + sizeof(RcState);
+}
 inline size_t state_bytes(const Geometry& g) {
-    return sizeof(StateHeader) + sizeof(StripeState) * (size_t)(g.num_slices + 1) + 3 * state_plane_bytes(g) +
-           sizeof(int16_t) * 2 * (size_t)g.num_mbs();
+    return state_head_bytes(g) + 3 * state_plane_bytes(g) + sizeof(int16_t) * 2 * (size_t)g.num_mbs();
 }
 inline void state_header(const EncoderConfig& c, const Geometry& g, int started, int qp, int paint_qp,
                          StateHeader& h) {
     memset(&h, 0, sizeof(h));
     memcpy(h.magic, "SKH4", 4);
-    h.version = 2;
+    h.version = 3;
+    h.codec = c.codec;
     h.W = g.W;
     h.H = g.H;
     h.stripe_height = c.stripe_height;
@@ -405,7 +414,7 @@ inline void state_header(const EncoderConfig& c, const Geometry& g, int started,
     h.paint_qp = paint_qp;
 }
 inline bool state_header_matches(const EncoderConfig& c, const Geometry& g, const StateHeader& h) {
-    return memcmp(h.magic, "SKH4", 4) == 0 && h.version == 2 && h.W == g.W && h.H == g.H &&
+    return memcmp(h.magic, "SKH4", 4) == 0 && h.version == 3 && h.codec == c.codec && h.W == g.W && h.H == g.H &&
            h.stripe_height == c.stripe_height && h.fullframe == c.fullframe && h.num_slices == g.num_slices;
 }
 

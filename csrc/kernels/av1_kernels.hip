@@ -1486,8 +1486,9 @@ __global__ __launch_bounds__(256) void k_av1_ec_bytes(Av1Args A) {
 }
 
 // Rows below the picture repeat its last row (the reference clamp AV1's MC reads),
-// and every slice's reconstruction becomes the reference (k_commit copies rec -> ref
-// for every slice that is not ACT_NONE; vectors of re-coded static slices are zero).
+// and every slice's reconstruction becomes the reference: static slices (coded as
+// zero-motion skips) become ACT_P with zero vectors, so k_commit copies rec -> ref (the
+// loop filter and CDEF may have touched their rows) and gives them a zero MV field.
 // In-loop deblocking (av1_lf.h lf_edge), one launch per (plane, pass): one thread per
 // MI edge position (4 lines), every edge of a pass independent of the others.
 __global__ __launch_bounds__(256) void k_av1_lf(Av1Args A, int plane, int pass) {
@@ -1569,9 +1570,11 @@ __global__ __launch_bounds__(256) void k_av1_finish(Av1Args A) {
     if (blockIdx.x == 0)
         for (int s = threadIdx.x; s < f.num_slices; s += 256) {
             const int fa = f.tasks[s].final_action;
-            if (fa == ACT_NONE || fa == ACT_SKIPALL) {
-                f.tasks[s].final_action = ACT_SKIPALL;
-                f.tasks_host[s].final_action = ACT_SKIPALL;
+            if (fa == ACT_NONE || fa == ACT_SKIPALL) {   // coded as zero-motion skips
+                f.tasks[s].final_action = ACT_P;
+                f.tasks_host[s].final_action = ACT_P;
+                const int j0 = f.tasks[s].first_row * f.mb_w, j1 = j0 + f.tasks[s].num_rows * f.mb_w;
+                for (int j = j0; j < j1; j++) f.me[j].mvx = f.me[j].mvy = 0;
             }
         }
 }

@@ -85,6 +85,7 @@ class CaptureSession {
                 j.width = w; j.height = h; j.stripe_height = sh;
                 j.quality = s.jpeg_quality; j.paint_quality = s.paint_over_jpeg_quality;
                 j.use_paint_over = s.use_paint_over_quality; j.paint_over_trigger = s.paint_over_trigger_frames;
+                jcfg_ = j;
                 enc_.reset(backend ? create_hip_jpeg_backend(j, s.device) : create_cpu_jpeg_backend(j));
             } else {
                 h264::EncoderConfig e;
@@ -118,8 +119,10 @@ class CaptureSession {
                     e.aq_strength = 0;
                     e.intra4x4 = 0;
                 }
+                ecfg_ = e;
                 enc_.reset(backend ? create_hip_backend(e, s.device) : create_cpu_backend(e));
             }
+            backend_ = backend;
         } catch (const std::exception& ex) {
             set_last_error(std::string("encoder init failed: ") + ex.what());
             src_.reset();
@@ -158,6 +161,39 @@ class CaptureSession {
 
     void request_keyframe() { key_req_ = true; }
     void set_qp(int qp, int paint_qp) { qp_req_ = (qp & 0xffff) | (paint_qp & 0xffff) << 16; }
+
+    // Live move of the session's encoder to GPU `device` (load rebalancing across the
+    // GPUs of a node, parallel/rebalance.py). The capture thread does it between two
+    // frames: a new encoder is created on `device`, the old one's inter-frame state
+    // (StateHeader v3: references, damage baseline, MV field, controller, K10 state) is
+    // exported into a buffer on the old GPU, copied GPU-to-GPU (peer copy over xGMI)
+    // and imported, so the next frame is a P frame continuing the same stream — the
+    // client's decoder never sees the move. When the state cannot be carried (JPEG,
+    // an export that fails) the new encoder starts with a key frame instead.
+    // Returns 0 moved with the stream continued, 1 moved with a key frame, -1 not
+    // moved (CPU session, target GPU unusable, timeout; last error says why).
+    int move_to(int device, int timeout_ms) {
+        if (!running_) {
+            set_last_error("capture not running");
+            return -1;
+        }
+        std::unique_lock<std::mutex> g(move_mu_);
+        const uint64_t ticket = ++move_ticket_;
+        move_dev_ = device;
+        move_pending_ = true;   // the loop stops queueing a second frame until it is served
+        auto done = [&] { return move_done_ >= ticket || !running_; };
+        if (!move_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 10000), done)) {
+            set_last_error("move timed out");
+            return -1;
+        }
+        if (move_done_ < ticket) {
+            set_last_error("capture stopped during the move");
+            return -1;
+        }
+        if (move_rc_ < 0) set_last_error(move_err_);
+        return move_rc_;
+    }
+    int device() const { return registered_device_; }
     // K10: switch the rate control mode / CBR target from the next frame
     void set_rate(int mode, int kbps) {
         rate_req_ = (int64_t)1 << 62 | (int64_t)(mode & 0xff) << 32 | (uint32_t)(kbps > 0 ? kbps : 0);
@@ -372,9 +408,11 @@ class CaptureSession {
             return true;
         };
         while (running_) {
+            if (q.empty()) serve_move();   // a requested GPU move, between two frames
             if (key_req_.exchange(false)) enc_->request_keyframe();
-            if (int qq = qp_req_.exchange(0)) enc_->set_qp(qq & 0xffff, qq >> 16);
-            if (int64_t rr = rate_req_.exchange(0)) enc_->set_rate((int)((rr >> 32) & 0xff), (int)(rr & 0xffffffff));
+            if (int qq = qp_req_.exchange(0)) enc_->set_qp(qq & 0xffff, qq >> 16), last_qp_ = qq;
+            if (int64_t rr = rate_req_.exchange(0))
+                enc_->set_rate((int)((rr >> 32) & 0xff), (int)(rr & 0xffffffff)), last_rate_ = rr;
             if (q.empty()) {
                 if (step) {
                     if (!take_budget(true)) continue;
@@ -394,7 +432,7 @@ class CaptureSession {
                 frame_id++;
             }
             // queue the next frame behind the one in flight when there is no time to idle
-            if (q.size() < 2 && overlap_now()) {
+            if (q.size() < 2 && overlap_now() && !move_pending_) {
                 bool go = step ? take_budget(false) : clk::now() >= next;
                 if (go) {
                     if (!step) {
@@ -422,6 +460,10 @@ class CaptureSession {
                 step_cv_.notify_all();
             }
         }
+        {   // a move requested while stopping is not done
+            std::lock_guard<std::mutex> g(move_mu_);
+            move_cv_.notify_all();
+        }
         while (!q.empty()) {   // drain (the encoder is destroyed after the thread ends)
             try {
                 enc_->finish();
@@ -431,6 +473,72 @@ class CaptureSession {
         }
         std::lock_guard<std::mutex> g(step_mu_);
         step_cv_.notify_all();
+    }
+
+    // Capture thread, no frame in flight: performs a pending move_to().
+    void serve_move() {
+        int dev;
+        uint64_t ticket;
+        {
+            std::lock_guard<std::mutex> g(move_mu_);
+            if (move_done_ >= move_ticket_) return;
+            move_pending_ = false;
+            dev = move_dev_;
+            ticket = move_ticket_;
+        }
+        std::string err;
+        const int rc = do_move(dev, &err);
+        std::lock_guard<std::mutex> g(move_mu_);
+        move_rc_ = rc;
+        move_err_ = err;
+        move_done_ = ticket;
+        move_cv_.notify_all();
+    }
+
+    int do_move(int dev, std::string* err) {
+        trace::Range r("capture.move");
+        if (!backend_ || dev < 0 || dev >= sk_hip_device_count()) {
+            *err = backend_ ? "no such GPU" : "CPU session: nothing to move";
+            return -1;
+        }
+        std::unique_ptr<EncoderBackend> nenc;
+        try {
+            nenc.reset(s_.output_mode == 0 ? create_hip_jpeg_backend(jcfg_, dev) : create_hip_backend(ecfg_, dev));
+        } catch (const std::exception& ex) {
+            *err = std::string("encoder init on the target GPU failed: ") + ex.what();
+            return -1;
+        }
+        if (!nenc) {
+            *err = "encoder init on the target GPU failed";
+            return -1;
+        }
+        bool carried = false;
+        const int64_t n = enc_->state_bytes();
+        if (n > 0 && nenc->state_bytes() == n) {
+            void* a = sk_dev_alloc(s_.device, n);
+            void* b = sk_dev_alloc(dev, n);
+            try {
+                carried = a && b && enc_->export_state(a, 1) == 0 && sk_dev_copy(dev, b, a, n, 3) == 0 &&
+                          nenc->import_state(b, 1) == 0;
+            } catch (const std::exception&) {
+                carried = false;
+            }
+            if (a) sk_dev_free(s_.device, a);
+            if (b) sk_dev_free(dev, b);
+        }
+        if (!carried) {   // a fresh stream: key frame, with the rate control last asked for
+            nenc->request_keyframe();
+            if (last_qp_) nenc->set_qp(last_qp_ & 0xffff, last_qp_ >> 16);
+            if (last_rate_) nenc->set_rate((int)((last_rate_ >> 32) & 0xff), (int)(last_rate_ & 0xffffffff));
+        }
+        enc_ = std::move(nenc);   // the old encoder (and its GPU memory) goes here
+        if (registered_device_ >= 0) device_sessions(registered_device_, -1);
+        registered_device_ = s_.device = dev;
+        device_sessions(dev, +1);
+        wm_sent_ = nullptr;       // overlays (watermark, cursor) are re-sent to the new encoder
+        wm_on_gpu_ = false;
+        cursor_set_ = false;
+        return carried ? 0 : 1;
     }
 
     // Position of the watermark for frame t (location modes of set_watermark); tiled
@@ -523,9 +631,19 @@ class CaptureSession {
     std::unique_ptr<FrameSource> src_;
     std::unique_ptr<EncoderBackend> enc_;
     std::thread th_;
-    std::atomic<bool> running_{false}, key_req_{false};
+    std::atomic<bool> running_{false}, key_req_{false}, move_pending_{false};
     std::atomic<int> qp_req_{0};
     std::atomic<int64_t> rate_req_{0};
+    int last_qp_ = 0;
+    int64_t last_rate_ = 0;
+    int backend_ = 0;               // 0 CPU reference, 1 HIP
+    h264::EncoderConfig ecfg_{};    // the configuration a moved encoder is created with
+    jpeg::JpegConfig jcfg_{};
+    std::mutex move_mu_;
+    std::condition_variable move_cv_;
+    uint64_t move_ticket_ = 0, move_done_ = 0;
+    int move_dev_ = -1, move_rc_ = -1;
+    std::string move_err_;
     uint64_t hist_[kHist] = {};
     double src_kind_ = -1.0;  // 1 x11, 0 synthetic, -1 none (kept after stop for stats)
     std::mutex mu_;
@@ -558,6 +676,10 @@ void sk_capture_request_keyframe(void* c) { static_cast<CaptureSession*>(c)->req
 void sk_capture_set_qp(void* c, int qp, int paint_qp) { static_cast<CaptureSession*>(c)->set_qp(qp, paint_qp); }
 void sk_capture_set_rate(void* c, int mode, int kbps) { static_cast<CaptureSession*>(c)->set_rate(mode, kbps); }
 void sk_capture_stats(void* c, double* out, int n) { static_cast<CaptureSession*>(c)->stats(out, n); }
+int sk_capture_move(void* c, int device, int timeout_ms) {
+    return static_cast<CaptureSession*>(c)->move_to(device, timeout_ms);
+}
+int sk_capture_device(void* c) { return static_cast<CaptureSession*>(c)->device(); }
 void sk_capture_set_watermark(void* c, const uint8_t* bgra, int w, int h, int location) {
     static_cast<CaptureSession*>(c)->set_watermark(bgra, w, h, location);
 }

@@ -355,11 +355,12 @@ class HipBackend : public EncoderBackend {
         }
         const int qp = h_key_seq_[1] > 0 ? h_key_seq_[1] : cfg_.qp;
         const int pqp = h_key_seq_[2] > 0 ? h_key_seq_[2] : cfg_.paint_qp;
-        std::vector<uint8_t> head(sizeof(StateHeader) + sizeof(StripeState) * (ns + 1));
+        std::vector<uint8_t> head(state_head_bytes(g_));
         StateHeader h;
         state_header(cfg_, g_, ctl[1] != 0, qp, pqp, h);
         memcpy(head.data(), &h, sizeof(h));
         memcpy(head.data() + sizeof(h), st.data(), sizeof(StripeState) * (ns + 1));
+        copy_now(head.data() + sizeof(h) + sizeof(StripeState) * (ns + 1), args_.rc, sizeof(RcState));   // K10
         uint8_t* o = static_cast<uint8_t*>(dst);
         if (on_device) HIPCHECK(hipMemcpyAsync(o, head.data(), head.size(), hipMemcpyHostToDevice, stream_));
         else memcpy(o, head.data(), head.size());
@@ -380,17 +381,24 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipSetDevice(device_));
         HIPCHECK(hipStreamSynchronize(stream_));
         const int ns = g_.num_slices;
-        std::vector<uint8_t> head(sizeof(StateHeader) + sizeof(StripeState) * (ns + 1));
+        std::vector<uint8_t> head(state_head_bytes(g_));
         const uint8_t* i = static_cast<const uint8_t*>(src);
-        if (on_device) copy_now(head.data(), i, sizeof(StateHeader));
-        else memcpy(head.data(), i, sizeof(StateHeader));
+        if (on_device) copy_now(head.data(), i, head.size());
+        else memcpy(head.data(), i, head.size());
         StateHeader h;
         memcpy(&h, head.data(), sizeof(h));
         if (!state_header_matches(cfg_, g_, h)) {
-            set_last_error("encoder state does not match this encoder's geometry");
+            set_last_error("encoder state does not match this encoder's geometry / codec");
             return -1;
         }
         xfer(args_.plan_state, i + sizeof(StateHeader), sizeof(StripeState) * (ns + 1), false, on_device);
+        {   // K10 state; its set_rate() counter is this encoder's, so k_rc_qp keeps it
+            RcState rc;
+            memcpy(&rc, head.data() + sizeof(StateHeader) + sizeof(StripeState) * (ns + 1), sizeof(rc));
+            rc.seq = __atomic_load_n(&h_key_seq_[5], __ATOMIC_SEQ_CST);
+            HIPCHECK(hipMemcpyAsync(args_.rc, &rc, sizeof(rc), hipMemcpyHostToDevice, stream_));
+            HIPCHECK(hipStreamSynchronize(stream_));
+        }
         i += head.size();
         const size_t ny = (size_t)g_.stride_y * g_.plane_h_y, nc = (size_t)g_.stride_c * g_.plane_h_c;
         const gpu::Planes& last_src = planes_src_[parity_ ^ 1];

@@ -40,6 +40,53 @@ struct HostYuv {
     }
 };
 
+// Session state of a CPU encoder (h264_encoder.h StateHeader layout); HEVC / AV1 keep
+// all their inter-frame state in the shared front end (references, controller, K10).
+int cpu_export_state(h264::CpuH264Encoder& e, void* dst, int on_device) {
+    if (on_device) return -1;
+    uint8_t* o = static_cast<uint8_t*>(dst);
+    h264::StateHeader h;
+    h264::state_header(e.cfg, e.g, e.first_frame ? 0 : 1, e.ctl_.qp(), e.ctl_.paint_qp(), h);
+    memcpy(o, &h, sizeof(h));
+    o += sizeof(h);
+    e.ctl_.export_states(reinterpret_cast<h264::StripeState*>(o));
+    o += sizeof(h264::StripeState) * (e.g.num_slices + 1);
+    memcpy(o, &e.ctl_.rc(), sizeof(h264::RcState));
+    o += sizeof(h264::RcState);
+    for (auto* planes : {e.ref, e.ref1, e.prev})
+        for (int p = 0; p < 3; p++) {
+            memcpy(o, planes[p].data(), planes[p].size());
+            o += planes[p].size();
+        }
+    memcpy(o, e.mvfield.data(), e.mvfield.size() * sizeof(int16_t));
+    return 0;
+}
+
+int cpu_import_state(h264::CpuH264Encoder& e, const void* src, int on_device) {
+    if (on_device) return -1;
+    const uint8_t* i = static_cast<const uint8_t*>(src);
+    h264::StateHeader h;
+    memcpy(&h, i, sizeof(h));
+    if (!h264::state_header_matches(e.cfg, e.g, h)) {
+        set_last_error("encoder state does not match this encoder's geometry / codec");
+        return -1;
+    }
+    i += sizeof(h);
+    e.ctl_.import_states(reinterpret_cast<const h264::StripeState*>(i));
+    i += sizeof(h264::StripeState) * (e.g.num_slices + 1);
+    memcpy(&e.ctl_.rc(), i, sizeof(h264::RcState));
+    i += sizeof(h264::RcState);
+    for (auto* planes : {e.ref, e.ref1, e.prev})
+        for (int p = 0; p < 3; p++) {
+            memcpy(planes[p].data(), i, planes[p].size());
+            i += planes[p].size();
+        }
+    memcpy(e.mvfield.data(), i, e.mvfield.size() * sizeof(int16_t));
+    e.first_frame = !h.started;
+    e.set_qp(h.qp, h.paint_qp);
+    return 0;
+}
+
 class CpuBackend : public EncoderBackend {
    public:
     explicit CpuBackend(const h264::EncoderConfig& c) : enc_(c) {}
@@ -96,47 +143,8 @@ class CpuBackend : public EncoderBackend {
     }
 
     int64_t state_bytes() override { return (int64_t)h264::state_bytes(enc_.g); }
-
-    int export_state(void* dst, int on_device) override {
-        if (on_device) return -1;
-        uint8_t* o = static_cast<uint8_t*>(dst);
-        h264::StateHeader h;
-        h264::state_header(enc_.cfg, enc_.g, enc_.first_frame ? 0 : 1, enc_.ctl_.qp(), enc_.ctl_.paint_qp(), h);
-        memcpy(o, &h, sizeof(h));
-        o += sizeof(h);
-        enc_.ctl_.export_states(reinterpret_cast<h264::StripeState*>(o));
-        o += sizeof(h264::StripeState) * (enc_.g.num_slices + 1);
-        for (auto* planes : {enc_.ref, enc_.ref1, enc_.prev})
-            for (int p = 0; p < 3; p++) {
-                memcpy(o, planes[p].data(), planes[p].size());
-                o += planes[p].size();
-            }
-        memcpy(o, enc_.mvfield.data(), enc_.mvfield.size() * sizeof(int16_t));
-        return 0;
-    }
-
-    int import_state(const void* src, int on_device) override {
-        if (on_device) return -1;
-        const uint8_t* i = static_cast<const uint8_t*>(src);
-        h264::StateHeader h;
-        memcpy(&h, i, sizeof(h));
-        if (!h264::state_header_matches(enc_.cfg, enc_.g, h)) {
-            set_last_error("encoder state does not match this encoder's geometry");
-            return -1;
-        }
-        i += sizeof(h);
-        enc_.ctl_.import_states(reinterpret_cast<const h264::StripeState*>(i));
-        i += sizeof(h264::StripeState) * (enc_.g.num_slices + 1);
-        for (auto* planes : {enc_.ref, enc_.ref1, enc_.prev})
-            for (int p = 0; p < 3; p++) {
-                memcpy(planes[p].data(), i, planes[p].size());
-                i += planes[p].size();
-            }
-        memcpy(enc_.mvfield.data(), i, enc_.mvfield.size() * sizeof(int16_t));
-        enc_.first_frame = !h.started;
-        enc_.set_qp(h.qp, h.paint_qp);
-        return 0;
-    }
+    int export_state(void* dst, int on_device) override { return cpu_export_state(enc_, dst, on_device); }
+    int import_state(const void* src, int on_device) override { return cpu_import_state(enc_, src, on_device); }
 
    private:
     h264::CpuH264Encoder enc_;
@@ -195,6 +203,17 @@ class CpuHevcBackend : public EncoderBackend {
         return n;
     }
 
+    int64_t state_bytes() override { return (int64_t)h264::state_bytes(enc_.fe.g); }
+    int export_state(void* dst, int on_device) override { return cpu_export_state(enc_.fe, dst, on_device); }
+    int import_state(const void* src, int on_device) override {
+        if (cpu_import_state(enc_.fe, src, on_device) < 0) return -1;
+        // the next POC: the picture state's frame_num (the GPU back end codes POC from it)
+        std::vector<h264::StripeState> st(enc_.fe.g.num_slices + 1);
+        enc_.fe.ctl_.export_states(st.data());
+        enc_.poc = st.back().frame_num;
+        return 0;
+    }
+
    private:
     hevc::CpuHevcEncoder enc_;
 };
@@ -251,6 +270,10 @@ class CpuAv1Backend : public EncoderBackend {
         if (dst && cap >= n) memcpy(dst, p, (size_t)n);
         return n;
     }
+
+    int64_t state_bytes() override { return (int64_t)h264::state_bytes(enc_.fe.g); }
+    int export_state(void* dst, int on_device) override { return cpu_export_state(enc_.fe, dst, on_device); }
+    int import_state(const void* src, int on_device) override { return cpu_import_state(enc_.fe, src, on_device); }
 
    private:
     av1::CpuAv1Encoder enc_;

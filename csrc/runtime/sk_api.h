@@ -201,6 +201,11 @@ void sk_capture_stop(void* c);
 void sk_capture_request_keyframe(void* c);
 void sk_capture_set_qp(void* c, int qp, int paint_qp);
 void sk_capture_set_rate(void* c, int mode, int kbps);   // K10: 0 CQP, 1 CRF, 2 CBR at kbps
+// Moves a running HIP session's encoder to GPU `device` between two frames, carrying the
+// inter-frame state GPU-to-GPU: 0 stream continued (P frames), 1 moved with a key frame,
+// -1 not moved (sk_last_error). Blocks up to timeout_ms (<= 0: 10 s).
+int sk_capture_move(void* c, int device, int timeout_ms);
+int sk_capture_device(void* c);   // GPU the session encodes on (-1: CPU)
 // frames, mean encode ms, bytes, packets, source (1 = X11, 0 = synthetic), last encode ms
 void sk_capture_stats(void* c, double* out, int n);
 // Premultiplied BGRA watermark composited before encoding (location enum in capture.cpp).

@@ -155,6 +155,22 @@ class ScreenCapture:
         if self._h:
             self._lib.sk_capture_set_rate(self._h, {"cqp": 0, "crf": 1, "cbr": 2}[mode], int(kbps))
 
+    def move_to(self, device: int, timeout_ms: int = 10000) -> str:
+        """Moves the running session's encoder to GPU `device` between two frames
+        (csrc/runtime/capture.cpp CaptureSession::move_to). Returns "continued" when the
+        inter-frame state was carried GPU-to-GPU (the stream goes on with P frames) or
+        "keyframe" when the new encoder had to start a fresh stream; raises when the
+        session stays where it is."""
+        rc = self._lib.sk_capture_move(self._h, int(device), int(timeout_ms)) if self._h else -1
+        if rc < 0:
+            raise RuntimeError(f"move_to({device}) failed: {self._lib.sk_last_error().decode()}")
+        return "continued" if rc == 0 else "keyframe"
+
+    @property
+    def device(self) -> int:
+        """GPU the session encodes on (-1: CPU reference encoder or not running)."""
+        return int(self._lib.sk_capture_device(self._h)) if self._h else -1
+
     def stats(self) -> dict:
         arr = (ctypes.c_double * 17)()
         self._lib.sk_capture_stats(self._h, arr, 17)

@@ -154,6 +154,10 @@ def lib():
         L.sk_capture_request_keyframe.argtypes = [ctypes.c_void_p]
         L.sk_capture_set_qp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.sk_capture_set_rate.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.sk_capture_move.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.sk_capture_move.restype = ctypes.c_int
+        L.sk_capture_device.argtypes = [ctypes.c_void_p]
+        L.sk_capture_device.restype = ctypes.c_int
         L.sk_capture_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         L.sk_capture_set_watermark.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int]
@@ -194,6 +198,39 @@ def convert_bgrx(bgrx: np.ndarray, fmt: str = "i420", backend: str = "cpu", devi
     finally:
         L.sk_convert_destroy(c)
     return (y, u) if nv12 else (y, u, v)
+
+
+class DevicePlane:
+    """A 2-D uint8 plane copied into HIP device memory of `device` (libselkies_native's
+    sk_dev_* allocator, no torch): pass it to :meth:`H264Encoder.encode_yuv` for device
+    input. Freed on close / GC."""
+
+    def __init__(self, array: np.ndarray, device: int = 0):
+        L = lib()
+        L.sk_dev_alloc.restype = ctypes.c_void_p
+        L.sk_dev_alloc.argtypes = [ctypes.c_int32, ctypes.c_int64]
+        L.sk_dev_free.argtypes = [ctypes.c_int32, ctypes.c_void_p]
+        L.sk_dev_copy.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32]
+        a = np.ascontiguousarray(array, np.uint8)
+        if a.ndim != 2:
+            raise ValueError("planes are 2-D")
+        self.device, self.shape, self.stride = device, a.shape, a.strides[0]
+        self.dev_ptr = L.sk_dev_alloc(device, max(1, a.nbytes))
+        if not self.dev_ptr:
+            raise MemoryError(L.sk_last_error().decode())
+        if a.nbytes and L.sk_dev_copy(device, self.dev_ptr, a.ctypes.data, a.nbytes, 0) != 0:
+            raise RuntimeError(L.sk_last_error().decode())
+
+    def close(self):
+        if getattr(self, "dev_ptr", None):
+            lib().sk_dev_free(self.device, self.dev_ptr)
+            self.dev_ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def upload_ranges(pairs, rows: int):
@@ -377,13 +414,17 @@ class H264Encoder:
         """Planar 4:2:0 input instead of BGRx (GStreamer NV12 / I420 caps): ``fmt`` "i420"
         (y, u, v planes) or "nv12" (y plane, interleaved uv as ``u``). Planes are numpy
         uint8 arrays (host) or torch uint8 tensors on this encoder's GPU (device input,
-        no host copy). W x H luma, ((W+1)/2) x ((H+1)/2) chroma (x2 wide for NV12 uv)."""
+        no host copy) or :class:`DevicePlane`. W x H luma, ((W+1)/2) x ((H+1)/2) chroma
+        (x2 wide for NV12 uv)."""
         code = {"i420": 1, "nv12": 2}[fmt.lower()]
         planes = [y, u] + ([v] if code == 1 else [u])
-        on_dev = int(hasattr(y, "data_ptr") and bool(getattr(y, "is_cuda", False)))
+        on_dev = int(isinstance(y, DevicePlane) or (hasattr(y, "data_ptr") and bool(getattr(y, "is_cuda", False))))
         ptrs, strides = [], []
         for p in planes:
-            if hasattr(p, "data_ptr"):
+            if isinstance(p, DevicePlane):
+                ptrs.append(p.dev_ptr)
+                strides.append(p.stride)
+            elif hasattr(p, "data_ptr"):
                 if p.dim() != 2 or p.stride(1) != 1:
                     raise ValueError("planes must be 2-D with unit column stride")
                 ptrs.append(p.data_ptr())

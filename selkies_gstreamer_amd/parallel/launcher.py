@@ -158,11 +158,35 @@ class Supervisor:
             await asyncio.sleep(backoff)
             backoff = min(self.max_backoff, backoff * 2)
 
-    async def run(self):
-        await asyncio.gather(*(self._watch(s) for s in self.specs))
+    async def relocate(self, name: str, gpu: int) -> None:
+        """Restarts session `name` on GPU `gpu` (its own GPU stopped answering, so its
+        encoder state cannot be carried: the viewers get a key frame after reconnecting)."""
+        spec = next((s for s in self.specs if s.name == name), None)
+        if spec is None or spec.gpu == gpu:
+            return
+        log.warning("session %s: relocating from GPU %d to GPU %d", name, spec.gpu, gpu)
+        spec.gpu = gpu
+        p = self.procs.get(name)
+        if p is not None and p.returncode is None:
+            p.terminate()   # _watch respawns it with the new spec
+
+    async def run(self, rebalance: Optional[float] = None, gpus: Optional[list] = None, capacity: float = 48.0):
+        """Supervises every session; with `rebalance` (poll interval, s) a Rebalancer
+        moves displays between `gpus` while they run (parallel/rebalance.py)."""
+        tasks = [self._watch(s) for s in self.specs]
+        if rebalance:
+            from .rebalance import Rebalancer
+            self.rebalancer = Rebalancer({s.name: s.all_ports() for s in self.specs},
+                                         gpus if gpus is not None else sorted({s.gpu for s in self.specs}),
+                                         capacity=capacity, on_failed_move=self.relocate)
+            self._rb_stop = asyncio.Event()
+            tasks.append(self.rebalancer.run(rebalance, self._rb_stop))
+        await asyncio.gather(*tasks)
 
     async def stop(self):
         self.stopping = True
+        if getattr(self, "_rb_stop", None) is not None:
+            self._rb_stop.set()
         for p in self.procs.values():
             if p.returncode is None:
                 p.send_signal(signal.SIGTERM)
@@ -182,6 +206,9 @@ def main(argv=None):
     ap.add_argument("--capacity", type=float, default=48.0, help="1080p60 sessions per GPU")
     ap.add_argument("--sessions-per-process", type=int, default=1,
                     help="> 1: run that many sessions per process (session hosts sharing one HIP context)")
+    ap.add_argument("--rebalance", type=float, default=0.0, metavar="SECONDS",
+                    help="> 0: move running displays between GPUs on overload or a stalled GPU, polling "
+                         "every SECONDS (P-frame continuation, parallel/rebalance.py)")
     ap.add_argument("--dry-run", action="store_true", help="print the plan and exit")
     args, extra = ap.parse_known_args(argv)
     if extra and extra[0] == "--":
@@ -201,7 +228,7 @@ def main(argv=None):
         stop = asyncio.Event()
         for sig in (signal.SIGINT, signal.SIGTERM):
             loop.add_signal_handler(sig, stop.set)
-        task = asyncio.create_task(sup.run())
+        task = asyncio.create_task(sup.run(args.rebalance or None, list(range(args.gpus)), args.capacity))
         await stop.wait()
         await sup.stop()
         task.cancel()

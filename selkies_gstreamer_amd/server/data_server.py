@@ -179,6 +179,7 @@ class Capture:
     def __init__(self, display_id: str, module, queue: asyncio.Queue, sender: asyncio.Task):
         self.display_id, self.module, self.queue, self.sender = display_id, module, queue, sender
         self.callback = None
+        self.size, self.fps = (0, 0), 60.0
 
 
 def files_listing_html(path: str, rel: str) -> str:
@@ -270,6 +271,7 @@ class DataStreamingServer:
                         if getattr(self.display_manager, "available", False) else None)
         self.capture_source = capture_source
         self.gpu_id, self.num_gpus = gpu_id, max(1, num_gpus)
+        self._gpu_of: dict = {}   # display -> GPU after a move (/api/move)
         self.web_root = web_root
         self.metrics = metrics
         self.audio = AudioPipeline(self._broadcast_audio, settings.audio_device_name,
@@ -295,6 +297,8 @@ class DataStreamingServer:
         app.router.add_get("/health", self._health)
         if self.metrics is not None:
             app.router.add_get("/metrics", self.metrics.handler)
+        app.router.add_get("/api/placement", self._api_placement)
+        app.router.add_post("/api/move", self._api_move)
         app.router.add_get("/files", self._files_redirect)
         app.router.add_get("/files/{name:.*}", self._files)
         app.router.add_get("/{tail:.*}", self._root)
@@ -329,6 +333,65 @@ class DataStreamingServer:
 
     async def _health(self, request):
         return web.Response(text="OK\n")
+
+    # ---- node control (parallel/rebalance.py): loopback callers only, on top of auth
+    @staticmethod
+    def _loopback(request: web.Request) -> bool:
+        return (request.remote or "") in ("127.0.0.1", "::1", "::ffff:127.0.0.1")
+
+    def placement(self) -> dict:
+        """Per display: the GPU its encoder runs on and its encode load (mean and last
+        capture-to-packets ms, frames, target fps)."""
+        out = {}
+        for did, cap in self.captures.items():
+            mod = cap.module
+            st = {}
+            try:
+                st = mod.stats()
+            except Exception:
+                pass
+            dev = getattr(mod, "device", None)
+            out[did] = {"gpu": dev if isinstance(dev, int) and dev >= 0 else self._gpu_of.get(did),
+                        "encode_ms_mean": st.get("encode_ms_mean"), "encode_ms_last": st.get("encode_ms_last"),
+                        "frames": st.get("frames"), "fps": cap.fps,
+                        "width": cap.size[0], "height": cap.size[1]}
+        return out
+
+    async def _api_placement(self, request):
+        if not self._loopback(request):
+            raise web.HTTPForbidden()
+        return web.json_response({"gpu_id": self.gpu_id, "displays": self.placement()})
+
+    async def move_display(self, did: str, gpu: int) -> str:
+        """Moves display `did`'s running encoder to GPU `gpu` (P-frame continuation when
+        the state can be carried, pixelflux ScreenCapture.move_to); later capture restarts
+        of the display (resolution changes) stay on that GPU."""
+        cap = self.captures.get(did)
+        if cap is None:
+            raise KeyError(did)
+        fn = getattr(cap.module, "move_to", None)
+        if fn is None:
+            raise RuntimeError("capture module cannot move")
+        res = await asyncio.get_running_loop().run_in_executor(None, fn, int(gpu))
+        self._gpu_of[did] = int(gpu)   # "keyframe": the new stream opens with an IDR itself
+        log.info("display %s moved to GPU %d (%s)", did, gpu, res)
+        return res
+
+    async def _api_move(self, request):
+        if not self._loopback(request):
+            raise web.HTTPForbidden()
+        did = request.query.get("display", "primary")
+        try:
+            gpu = int(request.query["gpu"])
+        except (KeyError, ValueError):
+            raise web.HTTPBadRequest(text="gpu=<index> required")
+        try:
+            res = await self.move_display(did, gpu)
+        except KeyError:
+            raise web.HTTPNotFound(text=f"no running capture for display {did}")
+        except RuntimeError as e:
+            return web.json_response({"display": did, "gpu": gpu, "error": str(e)}, status=409)
+        return web.json_response({"display": did, "gpu": gpu, "result": res})
 
     async def _root(self, request: web.Request):
         if request.headers.get("Upgrade", "").lower() == "websocket":
@@ -784,7 +847,7 @@ class DataStreamingServer:
         cs.paint_over_trigger_frames, cs.damage_block_threshold, cs.damage_block_duration = 15, 10, 20
         cs.use_cpu = int(bool(p["use_cpu"]))
         index = list(self.displays).index(did)
-        cs.device = (self.gpu_id + index) % self.num_gpus
+        cs.device = self._gpu_of.get(did, (self.gpu_id + index) % self.num_gpus)
         cs.source = {"auto": -1, "x11": 0, "synthetic": 2, "motion": 1, "noise": 3}.get(self.capture_source, -1)
         wm = self.settings.watermark_path
         if wm and os.path.exists(wm):
@@ -847,6 +910,7 @@ class DataStreamingServer:
             log.error("capture start failed for %s: %s", did, e)
             return
         cap = Capture(did, module, queue, sender)
+        cap.size, cap.fps = (int(cs.capture_width), int(cs.capture_height)), float(cs.target_fps)
         cap.callback = cb
         self.captures[did] = cap
         st = self.displays.get(did)

@@ -14,7 +14,8 @@ from selkies_gstreamer_amd.webrtc.peer import PeerConnection
 
 
 def _au(n):
-    return b"\x00\x00\x00\x01\x65" + os.urandom(n)
+    # no zero bytes: random payload could otherwise hold a start code and split the NAL
+    return b"\x00\x00\x00\x01\x65" + bytes(b | 1 for b in os.urandom(n))
 
 
 def _seq(p):

@@ -63,9 +63,8 @@ def test_converter_nv12_matches_i420_cpu():
 @pytest.mark.parametrize("codec", ["h264", "hevc", "av1"])
 def test_planar_input_hip_matches_cpu(codec):
     """k_yuv_damage (HIP) == load_frame_yuv (CPU) for host planes and for device planes
-    (torch tensors on the GPU: the encoder reads them without a host copy)."""
-    import torch
-    from selkies_gstreamer_amd.ops.native import require_gpu
+    (DevicePlane: hipMalloc'd, the encoder reads them without a host copy)."""
+    from selkies_gstreamer_amd.ops.native import DevicePlane, require_gpu
     require_gpu()
     W, H = 200, 90   # unaligned: exercises the padding rule
     src = SyntheticDesktop(W, H, kind="motion")
@@ -76,9 +75,10 @@ def test_planar_input_hip_matches_cpu(codec):
         planes = convert_bgrx(f, fmt)
         pc = cpu.encode_yuv(fmt, *planes, frame_id=t)
         ph = hip_host.encode_yuv(fmt, *planes, frame_id=t)
-        dev = [torch.from_numpy(np.ascontiguousarray(p)).cuda() for p in planes]
-        torch.cuda.synchronize()
+        dev = [DevicePlane(p) for p in planes]
         pd = hip_dev.encode_yuv(fmt, *dev, frame_id=t)
+        for d in dev:
+            d.close()
         assert [p.data for p in ph] == [p.data for p in pc], (codec, t, "host planes")
         assert [p.data for p in pd] == [p.data for p in pc], (codec, t, "device planes")
     # back to BGRx on the same session: graphs re-captured with k_convert_damage
