@@ -87,6 +87,9 @@ def parse():
                         "real server processes (session hosts) to headless websocket clients for --e2e-seconds and report the "
                         "measured capture->client latency; a comma list is tried in order and the first N at "
                         "which every session sustains 60 fps is reported (tools/bench_e2e.py); 0 = skip")
+    p.add_argument("--e2e-av1", default="3840x2160@120:40000",
+                   help="WxH@fps:kbps of the AV1 end-to-end group (one session, encoder svtav1enc, the headless "
+                        "client decodes every frame with dav1d: capture->decoded latency); 'none' = skip")
     p.add_argument("--e2e-no-cpu-cap", action="store_true",
                    help="try the session counts even above what the CPU quota can drive (cpu_budget)")
     p.add_argument("--e2e-seconds", type=float, default=4.0)
@@ -187,6 +190,36 @@ def run_e2e(args, W, H, gpu=0, counts=None):
         return r
     except Exception as ex:   # noqa: BLE001 - reported in the JSON line
         return {"sessions": counts or e2e_counts(args), "error": f"{type(ex).__name__}: {ex}"}
+
+
+def run_e2e_av1(args, gpu=0):
+    """AV1 session group of the end-to-end check: one 4K120 CBR session whose headless
+    client decodes every frame with dav1d (models/av1/dav1d.py, 4 threads) on a thread of
+    its own. Reports capture -> first packet and capture -> decoded picture; the browser's
+    paint is not measured."""
+    import asyncio
+    import types
+    try:
+        geo, _, rest = args.e2e_av1.partition("@")
+        w, h = (int(x) for x in geo.split("x"))
+        fps, _, kbps = rest.partition(":")
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+        import bench_e2e
+        ns = types.SimpleNamespace(width=w, height=h, fps=int(fps), crf=args.qp, encoder="svtav1enc", kbps=int(kbps or 0),
+                                   source="motion", gpu=gpu, use_cpu=False, sustain=0.97, seconds=args.e2e_seconds,
+                                   warmup=args.e2e_warmup, hw_queues=None, client_procs=1, sessions_per_proc=1,
+                                   decode=True, decode_threads=4,
+                                   log_dir=os.path.join("gpurun_out", "bench_e2e_logs", f"av1_gpu{gpu}"))
+        os.makedirs(ns.log_dir, exist_ok=True)
+        r = asyncio.run(asyncio.wait_for(bench_e2e.run_n(1, ns), 150))
+        r.update(resolution=f"{w}x{h}", target_fps=int(fps), rate_control=f"CBR {kbps} kbit/s" if kbps else "CRF",
+                 browser_paint="UNMEASURED",
+                 method="measured: one server + one headless websocket client (reference protocol, encoder "
+                        "svtav1enc); latency_* = frame grab -> first packet received, decoded_latency_* = frame grab "
+                        "-> dav1d returned the picture (4 decoder threads, fed on receipt)")
+        return r
+    except Exception as ex:   # noqa: BLE001 - reported in the JSON line
+        return {"error": f"{type(ex).__name__}: {ex}"}
 
 
 # CPU cost of one end-to-end 1080p60 session, server and client side together:
@@ -407,6 +440,11 @@ def main():
             and not args.gather and not args.dist_bands):
         e2e = run_e2e(args, args.width, args.height, gpu=local_rank, counts=e2e_counts(args, world))
         time.sleep(3.0)   # let the check's processes, clients and GPU contexts finish tearing down
+    e2e_av1 = None
+    if (world == 1 and args.e2e_av1 != "none" and args.backend == "hip" and args.encoder == "h264"
+            and not args.gather and not args.dist_bands):
+        e2e_av1 = run_e2e_av1(args, gpu=local_rank)
+        time.sleep(2.0)
     if world > 1:
         import torch as _torch
         import torch.distributed as _dist
@@ -658,6 +696,7 @@ def main():
             "capture_to_client_p50_ms": e2e.get("latency_p50_ms") if e2e else None,
             "capture_to_client_p99_ms": e2e.get("latency_p99_ms") if e2e else None,
             "e2e": e2e,
+            "e2e_av1_4k": e2e_av1,
             "e2e_cpu": {"cpus": round(cpu_budget()[0], 2), "source": cpu_budget()[1], "ranks": max(world, 1),
                         "cpu_per_session": E2E_CPU_PER_SESSION, "session_cap_per_rank": e2e_cpu_cap(world),
                         # the sweep was cut to what the CPU quota can drive (the GPU could take more)

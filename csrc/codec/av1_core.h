@@ -13,11 +13,13 @@
 //
 // Coding structure (fixed by the sequence / frame headers of av1_cpu.cpp):
 //   64x64 superblocks; blocks are square 8/16/32/64 (PARTITION_NONE or SPLIT only);
-//   TX_MODE_LARGEST (one transform per block, DCT_DCT, reduced_tx_set); intra
-//   DC / V / H / SMOOTH(_V/_H) / PAETH, no filter-intra / CfL / palette / intraBC,
+//   TX_MODE_LARGEST (one transform per block, reduced_tx_set: DCT_DCT or IDTX, the
+//   screen-content identity transform, chosen per luma block); intra DC / V / H /
+//   SMOOTH(_V/_H) / PAETH / directional, no filter-intra / CfL / palette / intraBC,
 //   intra edge filter off; one reference (LAST), single prediction, EIGHTTAP
-//   regular filter, quarter-pel vectors (allow_high_precision_mv = 0); no
-//   order hints (no temporal MVs, no skip mode); loop filter / CDEF / LR off.
+//   regular filter, quarter-pel vectors (allow_high_precision_mv = 0); no order
+//   hints (no temporal MVs, no skip mode); in-loop deblocking (av1_lf.h) and CDEF
+//   (av1_cdef.h) on, loop restoration off.
 #pragma once
 #include "sk_common.h"
 #include "av1_tables.h"

@@ -80,13 +80,14 @@ class Dav1dError(RuntimeError):
 
 class Decoder:
     """Feed one temporal unit at a time, get the shown frame back (low latency:
-    max_frame_delay 1, one thread)."""
+    max_frame_delay 1; `n_threads` > 1 lets dav1d decode the frame's tiles in parallel,
+    what a browser's decoder does for 4K)."""
 
-    def __init__(self):
+    def __init__(self, n_threads: int = 1):
         L = self.L = _lib()
         settings = ctypes.create_string_buffer(1024)
         L.dav1d_default_settings(settings)
-        ctypes.c_int.from_buffer(settings, 0).value = 1   # n_threads
+        ctypes.c_int.from_buffer(settings, 0).value = max(1, int(n_threads))   # n_threads
         ctypes.c_int.from_buffer(settings, 4).value = 1   # max_frame_delay
         self.ctx = ctypes.c_void_p()
         rc = L.dav1d_open(ctypes.byref(self.ctx), settings)
@@ -104,8 +105,10 @@ class Decoder:
         except Exception:
             pass
 
-    def decode(self, tu: bytes):
-        """One temporal unit -> (Y, U, V) uint8 arrays, or None if no picture came out."""
+    def decode(self, tu: bytes, planes: bool = True):
+        """One temporal unit -> (Y, U, V) uint8 arrays, or None if no picture came out.
+        planes=False: the picture is released without a copy and (w, h) is returned
+        (latency measurements: the copy out of dav1d's buffers is not decoding)."""
         L = self.L
         data = ctypes.create_string_buffer(256)
         buf = L.dav1d_data_create(data, len(tu))
@@ -121,19 +124,19 @@ class Decoder:
             if rc < 0 and rc != EAGAIN:
                 L.dav1d_data_unref(data)
                 raise Dav1dError(f"dav1d_send_data: error {rc}")
-            p = self._get()
+            p = self._get(planes)
             if p is not None:
                 pics.append(p)
             if rc == EAGAIN:
                 continue
         while True:
-            p = self._get()
+            p = self._get(planes)
             if p is None:
                 break
             pics.append(p)
         return pics[-1] if pics else None
 
-    def _get(self):
+    def _get(self, planes: bool = True):
         L = self.L
         pic = ctypes.create_string_buffer(1024)
         rc = L.dav1d_get_picture(self.ctx, pic)
@@ -147,6 +150,9 @@ class Decoder:
         if bpc != 8:
             L.dav1d_picture_unref(pic)
             raise Dav1dError(f"unexpected bit depth {bpc}")
+        if not planes:
+            L.dav1d_picture_unref(pic)
+            return (w, h)
         planes = []
         for i, (pw, ph) in enumerate(((w, h), ((w + 1) // 2, (h + 1) // 2), ((w + 1) // 2, (h + 1) // 2))):
             st = strides[0 if i == 0 else 1]

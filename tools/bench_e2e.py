@@ -135,8 +135,53 @@ async def wait_ready(port: int, timeout: float = 90.0):
     raise TimeoutError(f"server on port {port} did not come up")
 
 
+class DecodeThread:
+    """The client's decoder for full-frame AV1 sessions (--decode): dav1d on its own
+    thread (ctypes releases the GIL, as a browser decodes off its main thread), fed each
+    frame's temporal unit on receipt. Records grab -> decoded picture per frame."""
+
+    def __init__(self, threads: int):
+        import queue
+        import threading
+        from selkies_gstreamer_amd.models.av1.dav1d import Decoder
+        self.dec = Decoder(n_threads=threads)
+        self.q: "queue.Queue" = queue.Queue()
+        self.lat_ms: list = []
+        self.dec_ms: list = []
+        self.errors = 0
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def push(self, tu: bytes, grab_ns, count: bool):
+        self.q.put((tu, grab_ns, count))
+
+    def _run(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                break
+            tu, g, count = item
+            t0 = time.monotonic_ns()
+            try:
+                pic = self.dec.decode(tu, planes=False)
+            except Exception:
+                self.errors += 1
+                continue
+            t1 = time.monotonic_ns()
+            if count and pic is not None:
+                self.dec_ms.append((t1 - t0) / 1e6)
+                if g is not None:
+                    self.lat_ms.append((t1 - g) / 1e6)
+
+    def close(self):
+        self.q.put(None)
+        self.t.join(timeout=30)
+        self.dec.close()
+
+
 async def client(port: int, args, t_start: float, t_end: float, out: dict):
     grabs: dict = {}
+    decoder = DecodeThread(getattr(args, "decode_threads", 4)) if getattr(args, "decode", False) else None
     seen: set = set()
     lat_ms: list = []        # grab -> first stripe of the frame received
     lat_last_ms: list = []   # grab -> last stripe of the frame received (whole frame on the client)
@@ -148,6 +193,8 @@ async def client(port: int, args, t_start: float, t_end: float, out: dict):
         async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket", max_msg_size=0) as ws:
             settings = {"initialClientWidth": args.width, "initialClientHeight": args.height,
                         "framerate": args.fps, "encoder": args.encoder, "h264_crf": args.crf}
+            if getattr(args, "kbps", 0):
+                settings["h264_bitrate"] = int(args.kbps)
             sent_settings = False
 
             async def acks():
@@ -187,17 +234,24 @@ async def client(port: int, args, t_start: float, t_end: float, out: dict):
                                 seen.add(fid)
                                 if len(seen) > 4096:
                                     seen.clear()
-                                if time.monotonic() >= t_start:
+                                counted = time.monotonic() >= t_start
+                                g = grabs.pop(fid, None)
+                                if counted:
                                     frames += 1
-                                    g = grabs.pop(fid, None)
                                     cur["grab"], cur["count"] = g, True
                                     if g is not None:
                                         lat_ms.append((now_ns - g) / 1e6)
+                                if decoder is not None:   # full-frame: one packet = one temporal unit
+                                    decoder.push(bytes(d[10:]), g, counted)
                     else:
                         break
             finally:
                 ack_task.cancel()
-    out[port] = dict(frames=frames, lat=lat_ms, lat_last=lat_last_ms, bytes=bytes_rx)
+    dec = {}
+    if decoder is not None:
+        decoder.close()
+        dec = dict(lat_dec=decoder.lat_ms, dec_ms=decoder.dec_ms, dec_errors=decoder.errors)
+    out[port] = dict(frames=frames, lat=lat_ms, lat_last=lat_last_ms, bytes=bytes_rx, **dec)
 
 
 def client_worker(ports, args, t_start, t_end) -> dict:
@@ -341,6 +395,14 @@ async def run_n(n: int, args) -> dict:
     lat_last = (np.concatenate([np.asarray(out[p]["lat_last"], dtype=np.float64) for _, p, _ in procs])
                 if out else np.zeros(0))
     ok = bool(len(fps) == n and fps.min() >= args.fps * args.sustain)
+    dec = {}
+    if getattr(args, "decode", False) and out:
+        ld = np.concatenate([np.asarray(out[p].get("lat_dec", []), dtype=np.float64) for _, p, _ in procs])
+        dm = np.concatenate([np.asarray(out[p].get("dec_ms", []), dtype=np.float64) for _, p, _ in procs])
+        pct = lambda a, q: round(float(np.percentile(a, q)), 2) if len(a) else None   # noqa: E731
+        dec = {"decoded_latency_p50_ms": pct(ld, 50), "decoded_latency_p99_ms": pct(ld, 99),
+               "decoded_samples": int(len(ld)), "dav1d_decode_p50_ms": pct(dm, 50), "dav1d_decode_p99_ms": pct(dm, 99),
+               "decode_errors": int(sum(out[p].get("dec_errors", 0) for _, p, _ in procs))}
     return {"sessions": n, "fps_min": round(float(fps.min()), 2), "fps_median": round(float(np.median(fps)), 2),
             "aggregate_fps": round(float(fps.sum()), 1),
             "latency_p50_ms": round(float(np.percentile(lat, 50)), 2) if len(lat) else None,
@@ -348,7 +410,7 @@ async def run_n(n: int, args) -> dict:
             "latency_samples": int(len(lat)),
             "frame_latency_p50_ms": round(float(np.percentile(lat_last, 50)), 2) if len(lat_last) else None,
             "frame_latency_p99_ms": round(float(np.percentile(lat_last, 99)), 2) if len(lat_last) else None,
-            "sustained": ok, **({"cpu": cpu} if cpu else {})}
+            "sustained": ok, **dec, **({"cpu": cpu} if cpu else {})}
 
 
 def main():
@@ -370,6 +432,11 @@ def main():
     ap.add_argument("--sessions-per-proc", type=int, default=1,
                     help="sessions per server process (> 1: parallel/multi.py session hosts)")
     ap.add_argument("--sustain", type=float, default=0.97, help="fraction of --fps every session must receive")
+    ap.add_argument("--kbps", type=int, default=0, help="> 0: CBR at this bitrate (h264_bitrate setting)")
+    ap.add_argument("--decode", action="store_true",
+                    help="full-frame AV1 (--encoder svtav1enc): the clients decode every frame with dav1d and "
+                         "report grab -> decoded picture latency")
+    ap.add_argument("--decode-threads", type=int, default=4)
     ap.add_argument("--log-dir", default=os.path.join(ROOT, "gpurun_out", "e2e_logs"))
     ap.add_argument("--sample-cpu", action="store_true",
                     help="sample server / client CPU (per thread) and GPU busy over the measured window")
