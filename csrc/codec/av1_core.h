@@ -121,7 +121,8 @@ struct BlkInfo {
     uint8_t flags;     // bit0 is_inter, bit1 skip, bit2 merged-static (encoder), bits 4-5 RefMvIdx
     int16_t mv_row, mv_col;   // 1/8 pel (LAST), even values (no high-precision MVs)
     int16_t tx_type;   // luma transform type: TX_DCT_DCT (0) or TX_IDTX (1); inter chroma follows it
-    int16_t pad1;
+    uint8_t pal_n;     // PaletteSizeY (0: no palette; colours in the frame's palette cells)
+    uint8_t pad1;
 };
 static_assert(sizeof(BlkInfo) == 12, "BlkInfo layout");
 SK_HD bool blk_inter(const BlkInfo& b) { return (b.flags & 1) != 0; }
@@ -1081,7 +1082,12 @@ struct FrameView {
     int lctx_w[3];
     int unit_w;                  // 16x16 units per row
     int qidx, key;
+    int screen;                  // allow_screen_content_tools (palette syntax)
+    const uint8_t* pal;          // [r8][c8][8] palette colours of each cell's block
+    const uint8_t* src_y;        // source luma: the colour index map of a palette block
+    int stride_y;
     SK_HD const BlkInfo& at(int r, int c) const { return blk[(r >> 1) * geo.c8 + (c >> 1)]; }
+    SK_HD const uint8_t* pal_at(int r, int c) const { return pal + ((size_t)(r >> 1) * geo.c8 + (c >> 1)) * 8; }
     // levels of the block at mi (r, c) of size bsl in plane p (raster [row][col])
     SK_HD const int16_t* levels(int r, int c, int bsl, int p) const {
         const int16_t* u = lev + ((size_t)(r >> 2) * unit_w + (c >> 2)) * 384;
@@ -1119,6 +1125,203 @@ SK_HD CoefCtx coef_ctx(const FrameView& v, const TileRect& t, int plane, int x4,
     return cc;
 }
 
+// ---------------------------------------------------------------------------------
+// Palette (screen content tools; §5.11.46 palette_mode_info, §5.11.49 palette_tokens,
+// §7.11.4 get_palette_cache / get_palette_color_context), luma only, on key frames.
+// Encoder choice (av1_cpu.cpp intra_block = k_av1_intra_rec): a fully visible block
+// whose source luma takes 2..8 distinct values can be coded as that exact palette, with
+// no luma residual, when palette_rate2's cost is below the transform path's J.
+constexpr int kPalMax = 8;
+SK_HD int ceil_log2(int x) {
+    if (x < 2) return 0;
+    int i = 1, p = 2;
+    while (p < x) {
+        i++;
+        p <<= 1;
+    }
+    return i;
+}
+
+// PaletteCache: the sorted union of the above (only inside the same 64-row superblock
+// row) and left blocks' palettes, duplicates dropped. Returns its size.
+SK_HD int palette_cache(const FrameView& v, const TileRect& t, int r, int c, uint8_t* cache) {
+    const int an = inside(t, r - 1, c) && (r & 15) ? v.at(r - 1, c).pal_n : 0;
+    const int ln = inside(t, r, c - 1) ? v.at(r, c - 1).pal_n : 0;
+    const uint8_t* ac = an ? v.pal_at(r - 1, c) : nullptr;
+    const uint8_t* lc = ln ? v.pal_at(r, c - 1) : nullptr;
+    int ai = 0, li = 0, n = 0;
+    while (ai < an && li < ln) {
+        const int a = ac[ai], l = lc[li];
+        if (l < a) {
+            if (n == 0 || l != cache[n - 1]) cache[n++] = (uint8_t)l;
+            li++;
+        } else {
+            if (n == 0 || a != cache[n - 1]) cache[n++] = (uint8_t)a;
+            ai++;
+            if (l == a) li++;
+        }
+    }
+    for (; ai < an; ai++)
+        if (n == 0 || ac[ai] != cache[n - 1]) cache[n++] = ac[ai];
+    for (; li < ln; li++)
+        if (n == 0 || lc[li] != cache[n - 1]) cache[n++] = lc[li];
+    return n;
+}
+
+// ColorOrder and ColorContextHash -> context of the index at (i, j) of a colour map
+// (pitch n); returns the context, order[0..k) the colours by neighbour score.
+SK_HD int palette_color_context(const uint8_t* map, int n, int i, int j, int k, uint8_t* order) {
+    int sc[kPalMax];
+    for (int q = 0; q < kPalMax; q++) {
+        sc[q] = 0;
+        order[q] = (uint8_t)q;
+    }
+    if (j > 0) sc[map[i * n + j - 1]] += 2;
+    if (i > 0 && j > 0) sc[map[(i - 1) * n + j - 1]] += 1;
+    if (i > 0) sc[map[(i - 1) * n + j]] += 2;
+    for (int q = 0; q < 3; q++) {
+        int best = sc[q], bi = q;
+        for (int x = q + 1; x < k; x++)
+            if (sc[x] > best) {
+                best = sc[x];
+                bi = x;
+            }
+        if (bi != q) {
+            const int o = order[bi];
+            for (int x = bi; x > q; x--) {
+                sc[x] = sc[x - 1];
+                order[x] = order[x - 1];
+            }
+            sc[q] = best;
+            order[q] = (uint8_t)o;
+        }
+    }
+    const int hash = sc[0] + 2 * sc[1] + 2 * sc[2];
+    constexpr int8_t kCtx[9] = {-1, -1, 0, -1, -1, 4, 3, 2, 1};
+    return kCtx[hash];
+}
+
+// Index of each sample of a palette block (raster, pitch n): its source value's position
+// in the block's colours.
+SK_HD int palette_index(const uint8_t* col, int k, int v) {
+    int x = 0;
+    for (int q = 0; q < k; q++) x = col[q] == v ? q : x;
+    return x;
+}
+
+// ns(n) (§4.10.10) value x
+template <class Sink>
+SK_HD void code_ns(Sink& w, int n, int x) {
+    int wb = 0;
+    while ((1 << wb) <= n) wb++;
+    const int m = (1 << wb) - n;
+    if (x < m) {
+        w.lits((uint32_t)x, wb - 1);
+    } else {
+        w.lits((uint32_t)((x + m) >> 1), wb - 1);
+        w.bit((x + m) & 1);
+    }
+}
+
+// palette_mode_info of a key-frame intra block (luma palette; has_palette_uv = 0)
+template <class Sink>
+SK_HD void code_palette_mode_info(Sink& w, const CdfContext& cx, const FrameView& v, const TileRect& t, int r, int c,
+                                  int bsl, const BlkInfo& b) {
+    const int bctx = 2 * bsl - 2;   // Mi_Width_Log2 + Mi_Height_Log2 - 2 (square blocks)
+    const int k = b.pal_n;
+    if (b.mode == DC_PRED) {
+        const int ctx = (inside(t, r - 1, c) && v.at(r - 1, c).pal_n > 0) + (inside(t, r, c - 1) && v.at(r, c - 1).pal_n > 0);
+        w.sym(cdf_off(cx, cx.palette_y_mode[bctx][ctx]), 2, k > 0);
+        if (k > 0) {
+            w.sym(cdf_off(cx, cx.palette_y_size[bctx]), 7, k - 2);
+            const uint8_t* col = v.pal_at(r, c);
+            uint8_t cache[2 * kPalMax];
+            const int cn = palette_cache(v, t, r, c, cache);
+            uint32_t from_cache = 0;   // bit q: colour q comes from the cache
+            int idx = 0;
+            for (int i = 0; i < cn && idx < k; i++) {
+                int hit = -1;
+                for (int q = 0; q < k; q++) hit = col[q] == cache[i] ? q : hit;
+                w.bit(hit >= 0);
+                if (hit >= 0) {
+                    from_cache |= 1u << hit;
+                    idx++;
+                }
+            }
+            // the remaining colours ascending: the first as 8 bits, then deltas - 1 in
+            // paletteBits bits (5 + palette_num_extra_bits, shrinking with the range left)
+            int lit[kPalMax], m = 0;
+            for (int q = 0; q < k; q++)
+                if (!((from_cache >> q) & 1)) lit[m++] = col[q];
+            if (m > 0) w.lits((uint32_t)lit[0], 8);
+            if (m > 1) {
+                int need = 0;
+                for (int q = 1; q < m; q++) need = sk_max(need, ceil_log2(lit[q] - lit[q - 1]));
+                const int extra = sk_max(need - 5, 0);
+                w.lits((uint32_t)extra, 2);
+                int bits = 5 + extra;
+                for (int q = 1; q < m; q++) {
+                    w.lits((uint32_t)(lit[q] - lit[q - 1] - 1), bits);
+                    bits = sk_min(bits, ceil_log2(255 - lit[q]));
+                }
+            }
+        }
+    }
+    if (b.uv_mode == DC_PRED) w.sym(cdf_off(cx, cx.palette_uv_mode[k > 0]), 2, 0);
+}
+
+// palette_tokens: the colour index map, first index as ns(k), then every other sample on
+// anti-diagonals (top-right to bottom-left) as its rank in the neighbour colour order.
+template <class Sink>
+SK_HD void code_palette_tokens(Sink& w, const CdfContext& cx, const FrameView& v, int r, int c, int bsl, int k) {
+    const int n = 4 << bsl;
+    const uint8_t* col = v.pal_at(r, c);
+    uint8_t map[256];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++)
+            map[i * n + j] = (uint8_t)palette_index(col, k, v.src_y[(size_t)(r * 4 + i) * v.stride_y + c * 4 + j]);
+    code_ns(w, k, map[0]);
+    for (int d = 1; d < 2 * n - 1; d++)
+        for (int j = sk_min(d, n - 1); j >= sk_max(0, d - n + 1); j--) {
+            const int i = d - j;
+            uint8_t order[kPalMax];
+            const int ctx = palette_color_context(map, n, i, j, k, order);
+            int rank = 0;
+            for (int q = 0; q < k; q++) rank = order[q] == map[i * n + j] ? q : rank;
+            w.sym(cdf_off(cx, cx.palette_y_color[k - 2][ctx]), k, rank);
+        }
+}
+
+// Encoder: the distinct luma values (ascending) of the n x n block at src when there are
+// 2..kPalMax of them (returns the count, else 0).
+SK_HD int palette_colors(const uint8_t* src, int stride, int n, uint8_t* col) {
+    uint32_t seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            const int v = src[(size_t)i * stride + j];
+            seen[v >> 5] |= 1u << (v & 31);
+        }
+    int k = 0;
+    for (int w = 0; w < 8; w++) k += __builtin_popcount(seen[w]);
+    if (k < 2 || k > kPalMax) return 0;
+    int q = 0;
+    for (int v = 0; v < 256; v++)
+        if ((seen[v >> 5] >> (v & 31)) & 1) col[q++] = (uint8_t)v;
+    return k;
+}
+
+// Encoder: estimated rate (half bits) of coding an n x n block as its k-colour palette
+// (map: raster indices, pitch n) - header, then per sample 0.5 bit when it repeats its
+// left or top neighbour's index, else 1 + log2(k) bits. (i, j) one sample; the block's
+// total is palette_rate2_head + the sum of palette_rate2_px over its samples.
+SK_HD int palette_rate2_head(int k) { return 2 * (1 + 3 + 8 + 2 + 5 * (k - 1)); }
+SK_HD int palette_rate2_px(const uint8_t* map, int n, int i, int j, int k) {
+    const int x = map[i * n + j];
+    if (i == 0 && j == 0) return 2 * ceil_log2(k);
+    const bool rep = (j > 0 && map[i * n + j - 1] == x) || (i > 0 && map[(i - 1) * n + j] == x);
+    return rep ? 1 : 2 + 2 * ceil_log2(k);
+}
+
 // Is the block containing mi (mr, mc) before the block at (r, c) in coding order?
 // (raster superblocks, recursive quad-split Z order inside each 64x64 superblock)
 SK_HD uint32_t zorder16(int r, int c) {
@@ -1151,6 +1354,7 @@ SK_HD void code_block(Sink& w, const CdfContext& cx, const FrameView& v, const T
         if (bsl <= 3) w.sym(cdf_off(cx, cx.uv_mode_cfl_allowed[b.mode]), 14, b.uv_mode);
         else w.sym(cdf_off(cx, cx.uv_mode_cfl_not_allowed[b.mode]), 13, b.uv_mode);
         if (is_directional(b.uv_mode)) w.sym(cdf_off(cx, cx.angle_delta[b.uv_mode - V_PRED]), 7, 3);
+        if (v.screen) code_palette_mode_info(w, cx, v, t, r, c, bsl, b);
     } else {
         // is_inter: every block of an inter frame is inter, so no neighbour is intra (ctx 0)
         w.sym(cdf_off(cx, cx.intra_inter[0]), 2, 1);
@@ -1186,6 +1390,7 @@ SK_HD void code_block(Sink& w, const CdfContext& cx, const FrameView& v, const T
             code_mv(w, cx, b.mv_row - s.mv[pos][0], b.mv_col - s.mv[pos][1]);
         }
     }
+    if (b.pal_n) code_palette_tokens(w, cx, v, r, c, bsl, b.pal_n);
     if (blk_skip(b)) return;
     code_coeffs(w, cx, v.levels(r, c, bsl, 0), bsl, 0, coef_ctx(v, t, 0, c, r, 1 << bsl), blk_inter(b), b.mode, v.qidx,
                 b.tx_type);

@@ -88,8 +88,9 @@ void write_sequence_header(BitWriter& w, int W, int H, int level_idx, int full_r
     w.put(0, 1);   // enable_warped_motion
     w.put(0, 1);   // enable_dual_filter
     w.put(0, 1);   // enable_order_hint
-    w.put(0, 1);   // seq_choose_screen_content_tools
-    w.put(0, 1);   // seq_force_screen_content_tools (-> seq_force_integer_mv = SELECT, not coded)
+    w.put(1, 1);   // seq_choose_screen_content_tools: allow_screen_content_tools per frame
+    w.put(0, 1);   // seq_choose_integer_mv
+    w.put(0, 1);   // seq_force_integer_mv = 0 (fractional vectors)
     w.put(0, 1);   // enable_superres
     w.put(1, 1);   // enable_cdef (av1_cdef.h)
     w.put(0, 1);   // enable_restoration
@@ -113,6 +114,7 @@ void write_frame_header(BitWriter& w, const Av1Geo& g, const FrameParams& fp) {
     w.put(1, 1);                        // show_frame
     if (!fp.key) w.put(0, 1);           // error_resilient_mode
     w.put(0, 1);                        // disable_cdf_update
+    w.put(fp.screen ? 1 : 0, 1);        // allow_screen_content_tools (palette, key frames)
     w.put(0, 1);                        // frame_size_override_flag
     if (!fp.key) {
         w.put(7, 3);                    // primary_ref_frame = PRIMARY_REF_NONE
@@ -125,6 +127,7 @@ void write_frame_header(BitWriter& w, const Av1Geo& g, const FrameParams& fp) {
         w.put(0, 1);                    // is_motion_mode_switchable
     } else {
         w.put(0, 1);                    // render_and_frame_size_different
+        if (fp.screen) w.put(0, 1);     // allow_intrabc
     }
     w.put(1, 1);                        // disable_frame_end_update_cdf
     // tile_info: uniform spacing
@@ -200,6 +203,7 @@ CpuAv1Encoder::CpuAv1Encoder(const h264::EncoderConfig& cfg, int tcl, int trl) :
     lctx_w[0] = geo.mi_cols;
     lctx_h[0] = geo.mi_rows;
     lctx_w[1] = lctx_w[2] = geo.mi_cols >> 1;
+    pal.assign((size_t)geo.c8 * geo.r8 * 8, 0);
     lctx_h[1] = lctx_h[2] = geo.mi_rows >> 1;
     for (int p = 0; p < 3; p++) lctx[p].assign((size_t)lctx_w[p] * lctx_h[p], 0);
     level_idx = choose_level_idx(W, H, cfg.fps);
@@ -353,6 +357,26 @@ void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
     const long long ji = quant_block(sy, g.stride_y, py, log2n, fp.qidx, true, TX_IDTX, lid);
     b.tx_type = (int16_t)(ji < jd && any_nonzero(lid, n * n) ? TX_IDTX : TX_DCT_DCT);
     if (b.tx_type == TX_IDTX) memcpy(ly, lid, sizeof(int16_t) * n * n);
+    b.pal_n = 0;
+    uint8_t col[kPalMax] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int k = fp.screen && r + (1 << bsl) <= geo.mi_rows && c + (1 << bsl) <= geo.mi_cols
+                      ? palette_colors(sy, g.stride_y, n, col) : 0;
+    if (k) {   // exact palette vs the transform path (J of the levels just chosen)
+        uint8_t map[256];
+        int rate2 = palette_rate2_head(k);
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) map[i * n + j] = (uint8_t)palette_index(col, k, sy[(size_t)i * g.stride_y + j]);
+        for (int i = 0; i < n; i++)
+            for (int j = 0; j < n; j++) rate2 += palette_rate2_px(map, n, i, j, k);
+        if (tx_rd_cost(0, rate2, ac_q(fp.qidx)) < (jd < ji ? jd : ji)) {
+            b.pal_n = (uint8_t)k;
+            b.mode = DC_PRED;
+            b.tx_type = TX_DCT_DCT;
+            memset(ly, 0, sizeof(int16_t) * n * n);
+            for (int i = 0; i < n; i++) memcpy(&py[i * n], sy + (size_t)i * g.stride_y, (size_t)n);
+            set_palette(r, c, bsl, col);
+        }
+    }
     bool nz = recon_block(ly, log2n, fp.qidx, true, b.tx_type, py, &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
     // chroma: UV_DC_PRED. Every other UV mode implies an ADST-family chroma transform
     // (Mode_To_Txfm, §7.13.3 compute_tx_type); this encoder's transforms are DCT_DCT.
@@ -375,6 +399,15 @@ void CpuAv1Encoder::intra_block(int r, int c, int bsl, const TileRect& t) {
     set_lctx(0, c, r, n4, nz ? level_summary(ly, n * n) : 0);
     set_lctx(1, c >> 1, r >> 1, n4 >> 1, nz ? level_summary(lu, cn * cn) : 0);
     set_lctx(2, c >> 1, r >> 1, n4 >> 1, nz ? level_summary(lvv, cn * cn) : 0);
+}
+
+void CpuAv1Encoder::set_palette(int r, int c, int bsl, const uint8_t* col) {
+    const int n8 = (1 << bsl) >> 1;
+    for (int y = 0; y < n8; y++)
+        for (int x = 0; x < n8; x++) {
+            const int ry = (r >> 1) + y, cx = (c >> 1) + x;
+            if (ry < geo.r8 && cx < geo.c8) memcpy(&pal[((size_t)ry * geo.c8 + cx) * 8], col, kPalMax);
+        }
 }
 
 void CpuAv1Encoder::key_partition(int r, int c, int bsl, const TileRect& t, bool decide) {
@@ -545,6 +578,10 @@ FrameView CpuAv1Encoder::view() const {
     v.unit_w = fe.g.mb_w;
     v.qidx = fp.qidx;
     v.key = fp.key;
+    v.screen = fp.screen;
+    v.pal = pal.data();
+    v.src_y = fe.src[0].data();
+    v.stride_y = fe.g.stride_y;
     return v;
 }
 
@@ -610,6 +647,7 @@ void CpuAv1Encoder::encode(const uint8_t* bgrx, int stride, uint16_t frame_id, s
         for (int s = 0; s < ns; s++) fe.tasks[s].final_action = ACT_I;
     fe.ctl_.rate_control(fe.tasks.data(), fe.me.data());   // K10
     fp.key = key;
+    fp.screen = key && palette_on;
     uint8_t tab[52];
     for (int q = 0; q < 52; q++) tab[q] = (uint8_t)qidx_for_qp(q);
     std::vector<std::vector<uint8_t>> tiles(geo.tile_cols * geo.tile_rows);

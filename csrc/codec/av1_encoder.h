@@ -12,6 +12,7 @@
 // :724-783) with the AV1 RTP payloader (PT 96, :848-938); this is the HIP-native
 // equivalent (kernels/av1_kernels.hip).
 #pragma once
+#include <stdlib.h>
 #include <vector>
 #include "av1_core.h"
 #include "h264_frame.h"
@@ -28,7 +29,14 @@ struct FrameParams {
     int qidx = 86;
     int tile_size_bytes = 4;
     int lf_level = 0;     // loop_filter_level[0..3] (one level, av1_lf.h lf_level_for)
+    int screen = 0;       // allow_screen_content_tools: palette blocks (key frames)
 };
+
+// Palette coding of key frames (av1_core.h): on unless SK_AV1_PALETTE=0 (A/B runs).
+inline bool palette_enabled() {
+    const char* e = getenv("SK_AV1_PALETTE");
+    return !(e && e[0] == '0');
+}
 
 // MSB-first bit writer for headers.
 struct BitWriter {
@@ -102,6 +110,8 @@ class CpuAv1Encoder {
     std::vector<BlkInfo> blk;        // c8 * r8
     std::vector<int16_t> lev;        // kLevPerUnit per 16x16 unit (front-end MB grid)
     std::vector<uint8_t> lctx[3];    // level contexts (cul | dc << 6) at 4x4 granularity per plane
+    std::vector<uint8_t> pal;        // c8 * r8 * 8: palette colours of each cell's block
+    bool palette_on = palette_enabled();
     int lctx_w[3] = {0, 0, 0}, lctx_h[3] = {0, 0, 0};
     int level_idx = 8;
     uint64_t frames = 0;
@@ -116,6 +126,7 @@ class CpuAv1Encoder {
     void key_partition(int r, int c, int bsl, const TileRect& t, bool decide);
     void set_cells(int r, int c, int bsl, const BlkInfo& b);
     void set_lctx(int plane, int x4, int y4, int n4, uint8_t v);
+    void set_palette(int r, int c, int bsl, const uint8_t* col);
 };
 
 }  // namespace av1

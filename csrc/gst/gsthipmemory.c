@@ -334,10 +334,13 @@ static GstFlowReturn hipxfer_transform(GstBaseTransform* t, GstBuffer* in, GstBu
     if (!gst_video_frame_map(&hf, info, hbuf, s->to_device ? GST_MAP_READ : GST_MAP_WRITE)) return GST_FLOW_ERROR;
     GstFlowReturn ret = GST_FLOW_OK;
     for (guint p = 0; p < GST_VIDEO_INFO_N_PLANES(info); p++) {
-        const gint64 wb = (gint64)GST_VIDEO_FRAME_COMP_WIDTH(&hf, p) * GST_VIDEO_FRAME_COMP_PSTRIDE(&hf, p);
         const gint64 hb = GST_VIDEO_FRAME_COMP_HEIGHT(&hf, p);
         guint8* hp = (guint8*)GST_VIDEO_FRAME_PLANE_DATA(&hf, p);
         const gint hs = GST_VIDEO_FRAME_PLANE_STRIDE(&hf, p);
+        /* equal strides (both sides in the GstVideoInfo layout): whole rows, padding
+           included, so a round trip returns the buffer byte for byte */
+        const gint64 wb = hs == dstr[p] ? (gint64)hs
+                                        : (gint64)GST_VIDEO_FRAME_COMP_WIDTH(&hf, p) * GST_VIDEO_FRAME_COMP_PSTRIDE(&hf, p);
         const int rc = s->to_device ? sk_dev_copy2d(dev_id, d + doff[p], dstr[p], hp, hs, wb, hb, 0)
                                     : sk_dev_copy2d(dev_id, hp, hs, d + doff[p], dstr[p], wb, hb, 1);
         if (rc != 0) {

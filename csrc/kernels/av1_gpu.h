@@ -20,6 +20,8 @@ struct Av1Args {
     h264::gpu::FrameArgs f;   // planes, geometry (mb = 16x16 unit), tasks, motion field
     Av1Geo geo;
     BlkInfo* blk;             // [r8][c8]
+    uint8_t* pal;             // [r8][c8][8] palette colours of each cell's block (key frames)
+    int palette;              // palette coding of key frames enabled (av1_encoder.h palette_enabled)
     int16_t* lev;             // [units][kLevPerUnit]
     uint8_t* lctx[3];         // level contexts per plane (4x4 units), strides lctx_w
     int lctx_w[3];

@@ -154,7 +154,7 @@ __device__ int rate2_wave(const int16_t* lv, int ln) {
 // L.pred, and returns the per-plane level summaries (cul | dc << 6) packed as bytes
 // 0..2, bit 24 = any nonzero, bit 25 = IDTX.
 __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int qidx, bool intra, int16_t* gy,
-                                    int16_t* gu, int16_t* gv) {
+                                    int16_t* gu, int16_t* gv, long long* jmin = nullptr) {
     const int l = lane();
     const int n = 1 << log2n, nn = n * n, cn = n >> 1, cnn = cn * cn;
     const int qd = dc_q(qidx), qa = ac_q(qidx);
@@ -214,6 +214,7 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         }
     }
     wsync();
+    if (jmin) *jmin = jd < ji ? jd : ji;   // intra: the luma J of the cheaper transform type
     bool idtx;
     {
         if (intra) {
@@ -525,11 +526,55 @@ __device__ void intra_rec_block(const Av1Args& A, BlkLds& L, const FdctLds& F, i
         L.pred[320 + i] = (uint8_t)dcv;
     }
     wsync();
-    const uint32_t s = code_block_wave(L, F, log2n, qidx, true, lev_ptr(A, r, c, bsl, 0), lev_ptr(A, r, c, bsl, 1),
-                                       lev_ptr(A, r, c, bsl, 2));
+    long long jreg = 0;
+    uint32_t s = code_block_wave(L, F, log2n, qidx, true, lev_ptr(A, r, c, bsl, 0), lev_ptr(A, r, c, bsl, 1),
+                                 lev_ptr(A, r, c, bsl, 2), &jreg);
+    b.tx_type = (int16_t)((s >> 25) & 1 ? TX_IDTX : TX_DCT_DCT);
+    b.pal_n = 0;
+    if (A.palette && r + (1 << bsl) <= g.mi_rows && c + (1 << bsl) <= g.mi_cols) {
+        // exact palette of the source luma vs the transform path (av1_cpu.cpp intra_block)
+        uint32_t* seen = (uint32_t*)L.b;   // free after code_block_wave
+        uint8_t* map = (uint8_t*)L.a;
+        uint8_t* col = map + 256;
+        if (l < 8) seen[l] = 0u;
+        wsync();
+        for (int i = l; i < n * n; i += 64) atomicOr(&seen[L.src[i] >> 5], 1u << (L.src[i] & 31));
+        wsync();
+        const int k = wsum(l < 8 ? __builtin_popcount(seen[l]) : 0);
+        if (k >= 2 && k <= kPalMax) {
+            if (l == 0) {
+                int q = 0;
+                for (int v = 0; v < 256; v++)
+                    if ((seen[v >> 5] >> (v & 31)) & 1) col[q++] = (uint8_t)v;
+            }
+            wsync();
+            for (int i = l; i < n * n; i += 64) map[i] = (uint8_t)palette_index(col, k, L.src[i]);
+            wsync();
+            int r2 = 0;
+            for (int i = l; i < n * n; i += 64) r2 += palette_rate2_px(map, n, i / n, i % n, k);
+            r2 = wsum(r2) + palette_rate2_head(k);
+            if (tx_rd_cost(0, r2, ac_q(qidx)) < jreg) {
+                b.pal_n = (uint8_t)k;
+                b.mode = DC_PRED;
+                b.tx_type = TX_DCT_DCT;
+                int16_t* gy = lev_ptr(A, r, c, bsl, 0);
+                for (int i = l; i < n * n; i += 64) {
+                    gy[i] = 0;
+                    L.pred[i] = L.src[i];
+                }
+                s &= ~0xffu;   // no luma levels: the summary and the skip flag come from chroma
+                s = (s & ~(1u << 24)) | ((s & 0xffff00u) ? (1u << 24) : 0u);
+                const int n8 = (1 << bsl) >> 1;
+                for (int i = l; i < n8 * n8 * 8; i += 64) {
+                    const int cell = i >> 3, ry = (r >> 1) + cell / n8, cx = (c >> 1) + cell % n8;
+                    A.pal[((size_t)ry * g.c8 + cx) * 8 + (i & 7)] = (i & 7) < k ? col[i & 7] : 0;
+                }
+            }
+        }
+        wsync();
+    }
     store_rec_blk(L, f, x, y, n);
     b.flags = (s >> 24) & 1 ? 0 : 2;
-    b.tx_type = (int16_t)((s >> 25) & 1 ? TX_IDTX : TX_DCT_DCT);
     set_cells(A, r, c, bsl, b);
     const int n4 = 1 << bsl;
     set_lctx(A, 0, c, r, n4, (uint8_t)(s & 0xff));
@@ -927,6 +972,37 @@ __device__ int code_coeffs(WaveTokenSink& w, const CdfContext& cx, const int16_t
     return sk_min(wsum(cul), 63) | (dcc << 6);
 }
 
+// Lane-parallel palette_tokens (codec/av1_core.h code_palette_tokens): every sample's
+// colour context depends only on the index map, so lanes rank their samples at once and
+// store each token at its anti-diagonal position.
+__device__ void code_palette_tokens(WaveTokenSink& w, const CdfContext& cx, const FrameView& v, int r, int c, int bsl,
+                                    int k) {
+    const int l = lane(), n = 4 << bsl;
+    const uint8_t* col = v.pal_at(r, c);
+    uint8_t* map = (uint8_t*)w.bits;   // the wave's LDS bit buffer (1 KB), unused here
+    for (int i = l; i < n * n; i += 64)
+        map[i] = (uint8_t)palette_index(col, k, v.src_y[(size_t)(r * 4 + i / n) * v.stride_y + c * 4 + i % n]);
+    wsync();
+    code_ns(w, k, map[0]);
+    w.flush();
+    for (int i = l; i < n * n; i += 64) {
+        if (i == 0) continue;
+        const int y = i / n, x = i % n, d = x + y;
+        // samples before (y, x) in the scan: the diagonals before d, then the ones of d
+        // with a larger column (the scan runs j from the top-right end down)
+        const int before = d < n ? d * (d + 1) / 2 : n * n - (2 * n - 1 - d) * (2 * n - d) / 2;
+        const int jmax = d < n ? d : n - 1;
+        const int o = w.n + before + (jmax - x) - 1;
+        uint8_t order[kPalMax];
+        const int ctx = palette_color_context(map, n, y, x, k, order);
+        int rank = 0;
+        for (int q = 0; q < k; q++) rank = order[q] == map[i] ? q : rank;
+        if (o < w.cap) w.p[o] = tok_sym(cdf_off(cx, cx.palette_y_color[k - 2][ctx]), k, rank);
+    }
+    w.n += n * n - 1;
+    wsync();
+}
+
 __global__ __launch_bounds__(256) void k_av1_tokens(Av1Args A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint32_t bits_w[4][256];
@@ -946,6 +1022,10 @@ __global__ __launch_bounds__(256) void k_av1_tokens(Av1Args A) {
     v.unit_w = f.mb_w;
     v.qidx = A.frame[1];
     v.key = A.frame[0];
+    v.screen = A.frame[0] && A.palette;
+    v.pal = A.pal;
+    v.src_y = f.src.y;
+    v.stride_y = f.stride_y;
     const int ux = u % f.mb_w, uy = u / f.mb_w;
     WaveTokenSink sink{A.tok + (size_t)u * kTokCap, 0, kTokCap, 0u, 0, bits_w[w]};
     const TileRect t = tile_of(g, uy * 4, ux * 4);

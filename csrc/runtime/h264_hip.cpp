@@ -812,6 +812,8 @@ class HipBackend : public EncoderBackend {
         av1::geo_init(av1_geo_, g_.W, g_.H, tc, tr);
         a.geo = av1_geo_;
         a.blk = dmalloc<av1::BlkInfo>((size_t)av1_geo_.c8 * av1_geo_.r8);
+        a.pal = dmalloc<uint8_t>((size_t)av1_geo_.c8 * av1_geo_.r8 * 8);
+        a.palette = av1::palette_enabled() ? 1 : 0;
         a.lev = dmalloc<int16_t>((size_t)n * av1::gpu::kLevPerUnit);
         a.lctx_w[0] = av1_geo_.mi_cols;
         a.lctx_w[1] = a.lctx_w[2] = av1_geo_.mi_cols >> 1;
@@ -871,6 +873,7 @@ class HipBackend : public EncoderBackend {
         fp.key = av1_frame_[par][0];
         fp.qidx = av1_frame_[par][1];
         fp.lf_level = av1_frame_[par][2];
+        fp.screen = fp.key && aargs_.palette;
         std::vector<std::vector<uint8_t>> tl(tiles);
         size_t off = 0;
         for (int t = 0; t < tiles; t++) {

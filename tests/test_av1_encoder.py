@@ -159,3 +159,21 @@ def test_idtx_blocks_on_text_decode_exactly():
         idtx.append(int((blk[:, 4] == 1).sum()))
     dec.close()
     assert idtx[0] > 0, idtx   # key frame
+
+
+def test_palette_key_frames_decode_exactly_and_save_bytes(monkeypatch):
+    """Screen content tools on key frames (allow_screen_content_tools, luma palettes of
+    2..8 colours; av1_core.h code_palette_mode_info / code_palette_tokens): blocks of
+    text and flat UI become exact palettes. dav1d decodes them to the encoder's
+    reconstruction, and the key frame is smaller and closer to the source than the
+    same encoder with palettes off (SK_AV1_PALETTE=0)."""
+    W, H = 640, 360
+    enc = Av1Encoder(W, H, backend="cpu", qp=22)
+    enc.encode(SyntheticDesktop(W, H, kind="desktop").frame(0), 0)
+    blk = enc.debug_buffer("blk").reshape(-1, 12)
+    pal_n = blk[:, 10]
+    assert (pal_n > 0).sum() > 50 and pal_n.max() <= 8 and pal_n[pal_n > 0].min() >= 2
+    on = run(W, H, "desktop", 3, qp=22)
+    monkeypatch.setenv("SK_AV1_PALETTE", "0")
+    off = run(W, H, "desktop", 3, qp=22)
+    assert on[0][1] < 0.85 * off[0][1] and on[0][2] > off[0][2] + 5

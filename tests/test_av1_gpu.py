@@ -53,3 +53,11 @@ def test_gpu_tiles_and_noise():
 
 def test_gpu_1080p():
     _check(1920, 1080, "motion", 3, qp=25)
+
+
+def test_gpu_palette_key_frames():
+    """Palette blocks (desktop content: text and flat UI on key frames): the GPU's
+    decisions (k_av1_intra_rec), colour caches and lane-parallel index-map tokens equal
+    the CPU reference's."""
+    _check(640, 360, "desktop", 3, qp=22)
+    _check(1920, 1080, "desktop", 2, qp=30)

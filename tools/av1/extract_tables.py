@@ -191,6 +191,17 @@ def main():
     if not img.find([32768 - v for v in dq[:3]] + [0, 0]):
         raise SystemExit("delta_q cdf not found")
     put("delta_q", [dq], [1], 5)
+    # ---- palette (screen content tools, key frames): has_palette_y [bsize ctx 7][neighbour
+    # ctx 3] and has_palette_uv [2] are binary (confirmed in dav1d's struct), the size CDF
+    # [7] and the luma colour-index CDFs [size 2..8][5 contexts] are libaom arrays (the
+    # index table's rows have 2..8 symbols at a 9-entry stride)
+    put("palette_y_mode", img.confirm_binary("palette_y_mode", [31676, 3419, 1261, 31912, 2859, 980, 31823, 3400, 781,
+                                                                  32030, 3561, 904, 32309, 7337, 1462, 32265, 4015, 1521,
+                                                                  32450, 7946, 129]), [7, 3], 3)
+    put("palette_uv_mode", img.confirm_binary("palette_uv_mode", [32461, 21488]), [2], 3)
+    put("palette_y_size", img.aom_table([7952, 13000, 18149, 21478, 25527, 29241], 7, 8, 7), [7], 8)
+    put("palette_y_color", img.aom_table([[28710], [16384], [10553], [27036], [31603]], 35, 9,
+                                         [n for n in range(2, 9) for _ in range(5)]), [7, 5], 9)
     # ---- motion vectors (libaom nmv_context: joints, then two nmv_component structs)
     mv = img.aom_struct([4096, 11264, 19328], [(1, 4), (1, 11), (2, 4), (1, 4), (1, 2), (1, 2), (1, 2), (1, 2), (10, 2),
                                                (1, 11), (2, 4), (1, 4), (1, 2), (1, 2), (1, 2), (1, 2), (10, 2)])

@@ -69,7 +69,34 @@ def main():
     ap.add_argument("--backend", default="cpu", choices=("cpu", "hip"))
     ap.add_argument("--content", default="motion,desktop")
     ap.add_argument("--json", default="")
+    ap.add_argument("--ab", default="", metavar="CODEC:ENV",
+                    help="A/B one encoder tool: CODEC with ENV=0 (tool off) against the default (on), "
+                         "e.g. av1:SK_AV1_PALETTE; prints the tool's BD-rate")
     a = ap.parse_args()
+    if a.ab:
+        codec, env = a.ab.split(":")
+        res = {}
+        for kind in a.content.split(","):
+            os.environ[env] = "0"
+            off = [run_point(codec, q, a.width, a.height, a.frames, kind, a.backend) for q in QPS]
+            os.environ.pop(env)
+            on = [run_point(codec, q, a.width, a.height, a.frames, kind, a.backend) for q in QPS]
+            res[kind] = {"off": off, "on": on, "bd_rate_pct": bd_rate(off, on)}
+        if a.json:
+            with open(a.json, "w") as f:
+                json.dump(res, f)
+        print(f"# {codec} with {env} on vs off, {a.width}x{a.height}, {a.frames} frames per point, "
+              f"QP {', '.join(map(str, QPS))}, backend {a.backend}\n")
+        print("| content | QP | off bytes/frame | off Y-PSNR | on bytes/frame | on Y-PSNR |")
+        print("|---|---|---|---|---|---|")
+        for kind, r in res.items():
+            for p0, p1 in zip(r["off"], r["on"]):
+                print(f"| {kind} | {p0['qp']} | {p0['bytes'] / a.frames:.0f} | {p0['psnr']:.2f} | "
+                      f"{p1['bytes'] / a.frames:.0f} | {p1['psnr']:.2f} |")
+        print("\nBD-rate of the tool (on against off, equal Y-PSNR; negative = fewer bytes):\n")
+        for kind, r in res.items():
+            print(f"- {kind}: {r['bd_rate_pct']:+.1f} %")
+        return
     out = {}
     for kind in a.content.split(","):
         out[kind] = {c: [run_point(c, q, a.width, a.height, a.frames, kind, a.backend) for q in QPS]
