@@ -256,6 +256,19 @@ def inverse_transform(d: np.ndarray, n: int, dst: bool) -> np.ndarray:
     return (r + 2048) >> 12
 
 
+def residual_from_levels(levels: np.ndarray, qp: int, log2: int, ts: bool, dst: bool) -> np.ndarray:
+    """TransCoeffLevel -> residual of one n x n TB, 8-bit video: scaling (8.6.3, flat
+    m = 16, bdShift = BitDepth + log2 - 5), then transform skip (8.6.4.2: r = d << 7) or
+    the inverse DCT / DST, and the final (r + 2^11) >> 12 (bdShift 20 - BitDepth)."""
+    n = 1 << log2
+    bd = 8 + log2 - 5
+    scale = 16 * LEVEL_SCALE[qp % 6] << (qp // 6)
+    d = np.clip((np.asarray(levels, np.int64) * scale + (1 << (bd - 1))) >> bd, -32768, 32767)
+    if ts:
+        return ((d << 7) + (1 << 11)) >> 12
+    return inverse_transform(d, n, dst)
+
+
 def scan_diag(n: int) -> list:
     out = []
     x = y = 0
@@ -1259,15 +1272,8 @@ class HevcDecoder:
                 xp, yp = sc4[k]
                 levels[ys * 4 + yp, xs * 4 + xp] = -absv if signs[k] else absv
                 nsig += 1
-        # scaling (8.6.3), flat m = 16
-        bd = 8 + log2 - 5
-        scale = 16 * LEVEL_SCALE[qp % 6] << (qp // 6)
-        d = np.clip((levels * scale + (1 << (bd - 1))) >> bd, -32768, 32767)
         dst = cidx == 0 and log2 == 2 and intra_mode is not None
-        if ts:   # 8.6.4.2: r = d << 7, then the same (r + 2^11) >> 12 as after a transform
-            r = ((d << 7) + (1 << 11)) >> 12
-        else:
-            r = inverse_transform(d, n, dst)
+        r = residual_from_levels(levels, qp, log2, ts, dst)
         plane = "YUV"[cidx]
         blk = self.cur[plane][y0:y0 + n, x0:x0 + n].astype(np.int64)
         self.cur[plane][y0:y0 + n, x0:x0 + n] = np.clip(blk + r, 0, 255)
