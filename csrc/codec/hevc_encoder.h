@@ -58,9 +58,11 @@ inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
 }
 
 // Slices per CTB row of intra slices (SliceMap::K): ceil(ctb_w / kIntraSegCtbs);
-// SK_HEVC_SEG_CTBS=<n> sets the segment width (tests exercise the split at small sizes).
+// SK_HEVC_SEG_CTBS=<n> sets the segment width (tests exercise the split at small sizes),
+// SK_HEVC_SEG_CTBS=0 turns the split off (one slice per row band: RD A/B runs).
 inline int intra_seg_k(int ctb_w) {
     const char* e = getenv("SK_HEVC_SEG_CTBS");
+    if (e && e[0] == '0') return 1;
     return intra_seg_count(ctb_w, e && atoi(e) > 0 ? atoi(e) : kIntraSegCtbs);
 }
 

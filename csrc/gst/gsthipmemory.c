@@ -333,6 +333,24 @@ static GstFlowReturn hipxfer_transform(GstBaseTransform* t, GstBuffer* in, GstBu
     GstVideoFrame hf;
     if (!gst_video_frame_map(&hf, info, hbuf, s->to_device ? GST_MAP_READ : GST_MAP_WRITE)) return GST_FLOW_ERROR;
     GstFlowReturn ret = GST_FLOW_OK;
+    /* both sides in the same layout (strides and plane offsets): one copy of the whole
+       frame, row and plane padding included, so a round trip is byte-exact */
+    gboolean same = hf.map[0].size >= GST_VIDEO_INFO_SIZE(info);
+    for (guint p = 0; p < GST_VIDEO_INFO_N_PLANES(info); p++)
+        same = same && GST_VIDEO_FRAME_PLANE_STRIDE(&hf, p) == dstr[p] &&
+               (gsize)((guint8*)GST_VIDEO_FRAME_PLANE_DATA(&hf, p) - (guint8*)GST_VIDEO_FRAME_PLANE_DATA(&hf, 0)) ==
+                   doff[p] - doff[0];
+    if (same) {
+        guint8* hp = (guint8*)GST_VIDEO_FRAME_PLANE_DATA(&hf, 0);
+        const gint64 n = (gint64)GST_VIDEO_INFO_SIZE(info) - (gint64)GST_VIDEO_INFO_PLANE_OFFSET(info, 0);
+        const int rc = s->to_device ? sk_dev_copy(dev_id, d + doff[0], hp, n, 0) : sk_dev_copy(dev_id, hp, d + doff[0], n, 1);
+        if (rc != 0) {
+            GST_ELEMENT_ERROR(s, RESOURCE, FAILED, ("frame copy failed"), ("%s", sk_last_error()));
+            ret = GST_FLOW_ERROR;
+        }
+        gst_video_frame_unmap(&hf);
+        return ret;
+    }
     for (guint p = 0; p < GST_VIDEO_INFO_N_PLANES(info); p++) {
         const gint64 hb = GST_VIDEO_FRAME_COMP_HEIGHT(&hf, p);
         guint8* hp = (guint8*)GST_VIDEO_FRAME_PLANE_DATA(&hf, p);
