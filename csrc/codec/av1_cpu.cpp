@@ -243,7 +243,7 @@ static uint8_t level_summary(const int16_t* lv, int nn) {
 // Levels of one n x n block against `pred` for transform type tt (TX_DCT_DCT / TX_IDTX)
 // and their RD cost (av1_core.h tx_rd_cost; k_av1_inter / k_av1_intra_rec compute the same).
 static long long quant_block(const uint8_t* src, int sstride, const uint8_t* pred, int log2n, int qidx, bool intra,
-                             int tt, int16_t* lv) {
+                             int tt, int16_t* lv, long long* jzero = nullptr) {
     const int n = 1 << log2n, nn = n * n;
     int32_t res[256], co[256];
     for (int i = 0; i < n; i++)
@@ -253,13 +253,15 @@ static long long quant_block(const uint8_t* src, int sstride, const uint8_t* pre
     else
         fwd_transform(res, log2n, co);
     const int qd = dc_q(qidx), qa = ac_q(qidx);
-    long long d = 0;
+    long long d = 0, z = 0;
     for (int k = 0; k < nn; k++) {
         const int q = k == 0 ? qd : qa;
         lv[k] = (int16_t)quantize(co[k], q, intra);
         const long long e = (long long)co[k] - dequant(lv[k], q);
         d += e * e;
+        z += (long long)co[k] * co[k];
     }
+    if (jzero) *jzero += 4 * z;   // J of coding nothing (the skip alternative: no rate)
     int eob = 0;
     for (int c = nn - 1; c >= 0 && !eob; c--)
         if (lv[default_scan(log2n, c)]) eob = c + 1;
@@ -461,9 +463,9 @@ void CpuAv1Encoder::inter_block(int r, int c, int bsl, int mv_row, int mv_col) {
     const uint8_t* pp[3] = {py, pu, pv};
     const int ss[3] = {g.stride_y, g.stride_c, g.stride_c}, ln[3] = {log2n, log2n - 1, log2n - 1};
     int16_t lid[3][256];
-    long long jd = 0, ji = 0;
+    long long jd = 0, ji = 0, jz = 0;
     for (int p = 0; p < 3; p++) {
-        jd += quant_block(sp[p], ss[p], pp[p], ln[p], fp.qidx, false, TX_DCT_DCT, lp[p]);
+        jd += quant_block(sp[p], ss[p], pp[p], ln[p], fp.qidx, false, TX_DCT_DCT, lp[p], &jz);
         ji += quant_block(sp[p], ss[p], pp[p], ln[p], fp.qidx, false, TX_IDTX, lid[p]);
     }
     // IDTX only where the DCT codes something (a block the DCT quantises to nothing stays a
@@ -473,6 +475,11 @@ void CpuAv1Encoder::inter_block(int r, int c, int bsl, int mv_row, int mv_col) {
     int tt = dct_codes && ji < jd && any_after_trim(lid[0], log2n) ? TX_IDTX : TX_DCT_DCT;
     if (tt == TX_IDTX)
         for (int p = 0; p < 3; p++) memcpy(lp[p], lid[p], sizeof(int16_t) << (2 * ln[p]));
+    // RD skip: the levels must pay for themselves against the prediction alone (static
+    // screen content at fine quantisers otherwise re-codes every block's last grain of
+    // error in one frame: 2x budgets at the QP where it starts)
+    if (jz <= (tt == TX_IDTX ? ji : jd))
+        for (int p = 0; p < 3; p++) memset(lp[p], 0, sizeof(int16_t) << (2 * ln[p]));
     bool nz = recon_block(ly, log2n, fp.qidx, false, tt, py, &fe.rec[0][(size_t)y * g.stride_y + x], g.stride_y);
     nz |= recon_block(lu, log2n - 1, fp.qidx, false, tt, pu, &fe.rec[1][(size_t)cy * g.stride_c + cx], g.stride_c);
     nz |= recon_block(lvv, log2n - 1, fp.qidx, false, tt, pv, &fe.rec[2][(size_t)cy * g.stride_c + cx], g.stride_c);

@@ -179,7 +179,14 @@ SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intr
             // quarter QP left the stream at 0.5-0.7 of its rate for seconds after a burst)
             const bool gentle = rc.vbv_ms > 0 && !intra;
             const int dq = gentle ? 3 * d : (d >= 0 ? 6 * d : 5 * d);   // Q8 QP
-            qp = rc.last_qpf[k] + sk_clip(dq, gentle ? -128 : -512, (intra ? 16 : 10) << 8) + (gentle ? 3 : 5) * dc_down;
+            // ... except far below the target (under half of it: the frames after a
+            // key frame coded at the top of the range ran at 0.1-0.4 of the budget for the
+            // first 40 frames at half a QP per frame): 1.5 QP per frame
+            const int fine = gentle ? (d < -(1 << 8) ? -384 : -128) : -512;
+            // a complexity drop moves a long-buffer session at most 1 QP at once (the motion
+            // search's complexity of screen content swings while the coded size does not)
+            const int drop = gentle ? sk_max(3 * dc_down, -256) : 5 * dc_down;
+            qp = rc.last_qpf[k] + sk_clip(dq, fine, (intra ? 16 : 10) << 8) + drop;
             // screen content can jump several-fold within one QP (glyph edges crossing the
             // dead zone together): stay above the QP that last overflowed the buffer
             if (!intra && rc.qp_floor > qp) qp = rc.qp_floor;
@@ -241,7 +248,10 @@ SK_HD int rc_redo_step(const RcState& rc, long long frame_bits) {
     const uint32_t b = (uint32_t)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);
     const int target = sk_max(rc.cur_idr ? 3 * rc.budget : rc.budget, 1);
     const int d = rc_ilog2_q8(b) - rc_ilog2_q8((uint32_t)target);   // Q8 halvings, > 0
-    int slope = 6 << 8;                                               // Q8 QP per halving
+    // Q8 QP per halving: 6, except AV1 below QP 24, where screen content measured ~2 QP
+    // per halving (1.65 -> 0.37 budgets over 4 QP at QP 17): 6 sent a 2x overflow to a
+    // third of the budget there (at QP 40+ it still needs the 6)
+    int slope = rc.codec == 2 && rc.cur_qpf < (24 << 8) ? 3 << 8 : 6 << 8;
     if (rc.cur_redo > 0) {
         const int dq = rc.cur_qpf - rc.redo_qpf;
         const int dl = rc_ilog2_q8((uint32_t)sk_max(rc.redo_bits, 2)) - rc_ilog2_q8(b);

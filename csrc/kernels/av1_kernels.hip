@@ -180,12 +180,12 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
     // forward stage 2 (rows) + quantisation, DCT levels to L.lv and IDTX levels (8 x the
     // residual, still in L.a) to L.lv2, with both squared coefficient errors per plane
     // transform type: J per plane (av1_core.h tx_rd_cost) summed over the decision planes
-    long long jd = 0, ji = 0;
+    long long jd = 0, ji = 0, jz = 0;
     const int np = intra ? 1 : 3;   // planes in the decision
     for (int p = 0; p < 3; p++) {
         const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
         const int16_t* K = fdct_k(F, ln);
-        long long ed = 0, ei = 0;
+        long long ed = 0, ei = 0, ez = 0;
         for (int i = l; i < sz * sz; i += 64) {
             const int k = i >> ln, lc = i & (sz - 1);
             // |sum| <= |t|_2 |K|_2 < 2^31 (orthonormal Q13 rows, |t| <= 8 * 255 * sqrt(N)):
@@ -198,6 +198,7 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
             L.lv[o + i] = (int16_t)lv;
             const long long e = (long long)c - dequant(lv, q);
             ed += e * e;
+            ez += (long long)c * c;
             if (p < np) {
                 const int32_t ci = 8 * L.a[o + i];
                 const int li = quantize(ci, q, intra);
@@ -207,6 +208,7 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
             }
         }
         const long long dp = wsum64(ed), ip = wsum64(ei);
+        jz += 4 * wsum64(ez);
         if (p < np) {
             wsync();   // the plane's levels, for the rate estimates
             jd += tx_rd_cost(4 * dp, rate2_wave(L.lv + o, ln), qa);
@@ -234,6 +236,12 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         for (int p = 0; p < np; p++) {
             const int m = p ? cnn : nn, o = base(p);
             for (int i = l; i < m; i += 64) L.lv[o + i] = L.lv2[o + i];
+        }
+    // inter RD skip (av1_cpu.cpp inter_block): nothing coded when the levels do not pay
+    if (!intra && jz <= (idtx ? ji : jd))
+        for (int p = 0; p < 3; p++) {
+            const int m = p ? cnn : nn, o = base(p);
+            for (int i = l; i < m; i += 64) L.lv[o + i] = 0;
         }
     wsync();
     // inter blocks: tail trimming of the chosen levels
@@ -314,7 +322,7 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         }
     }
     wsync();
-    return cul | (nzm ? (1u << 24) : 0u) | (idtx ? (1u << 25) : 0u);
+    return cul | (nzm ? (1u << 24) : 0u) | (idtx && nzm ? (1u << 25) : 0u);   // no levels: DCT_DCT
 }
 
 // Block loads / stores (luma n at (x, y); chroma n/2 at (x/2, y/2)).

@@ -2358,6 +2358,10 @@ __global__ __launch_bounds__(256) void k_code_intra_sub(FrameArgs a) {
         const int mode = __builtin_amdgcn_readfirstlane(pre.i16_mode);
         const int cmode = __builtin_amdgcn_readfirstlane(pre.chroma_mode);
         const int start_qp = __builtin_amdgcn_readfirstlane(pre.qp);
+        // k_intra_prep's choice for this MB: read before `pre` is overwritten by the prefetch
+        const bool is_i4 = __builtin_amdgcn_readfirstlane((int)pre.type) == MB_I4x4;
+        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pre.i4lo);
+        const uint32_t m1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pre.i4hi);
         int src_l[4], src_c[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -2374,9 +2378,6 @@ __global__ __launch_bounds__(256) void k_code_intra_sub(FrameArgs a) {
             nb[l] = (uint8_t)v;
         }
         wave_sync();
-        const bool is_i4 = __builtin_amdgcn_readfirstlane((int)pre.type) == MB_I4x4;   // k_intra_prep's choice
-        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pre.i4lo);
-        const uint32_t m1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pre.i4hi);
         int pred_l[4], pred_c[4];
         intra_pred_lanes(is_i4 ? 2 : mode, cmode, nb, 0, zc, false, aL, pred_l, pred_c);
         MbInfo mb;
