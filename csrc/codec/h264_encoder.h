@@ -279,7 +279,7 @@ SK_HD void rc_apply(RcState& rc, SliceTask* tasks, const long long* sad, const l
     const int qpf = intra ? rc_frame_qpf(rc, ci, ni_known, true, nidr * 2 > ni, np + ni)
                           : rc_frame_qpf(rc, cp, np, false, false, np + ni);
     for (int s = 0, i = 0; s < ns; s++)
-        if (rc_slice_adjustable(tasks[s], plan_qp, rc.mode)) tasks[s].qp = rc_dither_qp(qpf, i++);
+        if (rc_slice_adjustable(tasks[s], plan_qp, rc.mode)) tasks[s].qp = rc_clamp_qp(rc, rc_dither_qp(qpf, i++));
 }
 
 // K10 CBR guard on a coded frame of `frame_bits` payload bits: when it overflows the
@@ -302,6 +302,7 @@ SK_HD int rc_redo(RcState& rc, SliceTask* tasks, int ns, long long frame_bits) {
     }
     rc.cur_qpf = f1;
     rc.cur_qp = (f1 + 128) >> 8;
+    rc.lam_boost = rc_lam_boost(f1);
     rc.redos++;
     rc.cur_redo++;
     return (f1 - f0 + 255) >> 8;

@@ -605,6 +605,7 @@ SK_HD int tu_avail(int q, bool left, bool top, bool tr) { return tu_avail_at(2 *
 // decisions): J = 512 * SSE + lambda_q8 * R, R in half bits, lambda = 0.57 * 2^((QP - 12) / 3)
 // (HM's), a coded TU ~4 bits plus, per non-zero level, 2.5 bits + 2 bits per doubling.
 SK_HD int rd_lambda_q8(int qp) {
+    qp = qp < 69 ? qp : 69;   // qp + the rate controller's lam_boost (ratecontrol.h kLamBoostMax)
     const int e = qp > 12 ? qp - 12 : 0;
     const int b = e % 3 == 0 ? 146 : (e % 3 == 1 ? 184 : 232);
     return b << (e / 3);

@@ -253,8 +253,8 @@ static uint16_t make_ycbf(const CuInfo& cu, int c16, int c8, int c4) {
 // levels into lev (kCoefPerCu), the reconstruction into ry / ru / rv, the TU fields into cu.
 static void code_inter_residual(const uint8_t* sy, const uint8_t* su, const uint8_t* sv, const uint8_t* pry,
                                 const uint8_t* pru, const uint8_t* prv, int qp, int16_t* lev, uint8_t* ry,
-                                uint8_t* ru, uint8_t* rv, CuInfo& cu) {
-    const int qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
+                                uint8_t* ru, uint8_t* rv, CuInfo& cu, int lam_boost) {
+    const int qpc = chroma_qp(qp), lam = rd_lambda_q8(qp + lam_boost);
     int16_t la[kCoefPerCu], lb[kCoefPerCu], lc[256];
     uint8_t ay[256], au[64], av[64], by[256], cy4[256], bu[64], bv[64];
     long long ja = 0, jc = (long long)lam * kSplitRateHalf;   // jc: the split CU's chroma + flags
@@ -349,7 +349,7 @@ void CpuHevcEncoder::code_slice_inter(int s) {
                 }
             int16_t* lev = &coefs[(size_t)idx * kCoefPerCu];
             uint8_t ry[256], ru[64], rv[64];
-            code_inter_residual(sy, su, sv, pry, pru, prv, qp, lev, ry, ru, rv, cu);
+            code_inter_residual(sy, su, sv, pry, pru, prv, qp, lev, ry, ru, rv, cu, fe.ctl_.rc().lam_boost);
             const int cbf = cu.cbf;
             int midx = -1;
             for (int i = 0; i < kMaxMergeCand && midx < 0; i++)

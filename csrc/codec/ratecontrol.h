@@ -60,8 +60,9 @@ struct RcState {
     int32_t redo_qpf;        // ... the fractional QP and payload bits of its pass before the
     int32_t redo_bits;       //     last one (valid when cur_redo > 0)
     int32_t codec;           // EncoderConfig::codec (rc_qp_min_for, rc_redo_step)
+    int32_t lam_boost;       // HEVC: QPs above 51 of the frame in flight, added to the RD model's lambda
 };
-static_assert(sizeof(RcState) == 148, "RcState layout");
+static_assert(sizeof(RcState) == 152, "RcState layout");
 
 SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x <= 1
     if (x <= 1) return 0;
@@ -69,6 +70,14 @@ SK_HD int rc_ilog2_q8(uint32_t x) {   // log2(x) * 256, linear mantissa; 0 for x
     const uint32_t frac = m >= 8 ? (x >> (m - 8)) & 255u : (x << (8 - m)) & 255u;
     return m * 256 + (int)frac;
 }
+
+// HEVC CBR continues past QP 51: a controller QP 51 + b codes at QP 51 with the RD
+// model's lambda b QPs higher (hevc_core.h rd_lambda_q8), so the TU zeroing drops every
+// residual that does not pay for itself at that rate - 4K motion content at 20 Mbit/s
+// overflowed its frames 1.9x at QP 51. The model, the steps and the re-code passes run on
+// the extended scale as on the real one.
+constexpr int kLamBoostMax = 18;
+SK_HD int rc_lam_boost(int qpf) { return qpf > (51 << 8) ? ((qpf + 128) >> 8) - 51 : 0; }
 
 // vbv_ms: the CBR buffer. 0 = 1.5 frame intervals, the reference's low-latency
 // setting for its H.264 / H.265 encoders (legacy/gstwebrtc_app.py:100-104); AV1
@@ -89,7 +98,7 @@ SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float f
     rc.base_qp = base_qp;
     rc.codec = codec;
     rc.qp_min = rc_qp_min_for(codec);
-    rc.qp_max = 51;
+    rc.qp_max = codec == 1 ? 51 + kLamBoostMax : 51;
     const double f = fps > 0 ? fps : 60.0;
     rc.budget = (int32_t)(bitrate_kbps * 1000.0 / f);
     const long long vbv = vbv_ms > 0 ? (long long)bitrate_kbps * vbv_ms : 0;   // bits
@@ -100,7 +109,9 @@ SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float f
     rc.last_qpf[0] = rc.last_qpf[1] = rc.cur_qpf = base_qp << 8;
 }
 
-SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, rc.qp_max); }
+// Slice QP of a controller QP: the coded range ends at 51 (HEVC's controller QPs above it
+// are lambda boosts, rc_lam_boost).
+SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, sk_min(rc.qp_max, 51)); }
 
 
 // Per-frame cap of a non-key frame: the VBV (1.5 frame intervals, the reference's
@@ -217,6 +228,7 @@ SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intr
     rc.cur_idr = idr ? 1 : 0;
     rc.cur_mbs = mbs;
     rc.cur_redo = 0;
+    rc.lam_boost = rc_lam_boost(qp);
     return qp;
 }
 

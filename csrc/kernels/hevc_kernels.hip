@@ -267,8 +267,9 @@ __device__ __forceinline__ void store_rec(const uint8_t* rec, const FrameArgs& f
 // Residual of an inter CU (hevc_cpu.cpp code_inter_residual; prediction in L.pred): all
 // trees coded in parallel batches, then the RD choice. Levels to gcoef, the TU fields into
 // cu; returns the raster holding the chosen reconstruction.
-__device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int16_t* gcoef, CuInfo& cu) {
-    const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
+__device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int16_t* gcoef, CuInfo& cu,
+                                         int lam_boost) {
+    const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp + lam_boost);
     {   // Every coded TU costs at least lam * (kTuRateHalf + 5) (one level): when the CU's whole
         // prediction error is below that, every TU of every tree zeroes and the 16x16 tree wins
         // (the split one pays its flags too) - the CPU's choice, without coding the trees.
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     wsync();
     CuInfo cu;
     memset(&cu, 0, sizeof(cu));
-    const uint8_t* rec = inter_residual(L, T, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu);
+    const uint8_t* rec = inter_residual(L, T, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu, A.f.rc->lam_boost);
     store_rec(rec, f, cx, cy);
     if (l == 0) {
         int midx = -1;

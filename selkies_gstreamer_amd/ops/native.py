@@ -311,7 +311,7 @@ RC_MODES = {"cqp": 0, "crf": 1, "cbr": 2}
 RC_FIELDS = ("mode", "base_qp", "qp_min", "qp_max", "budget", "vbv_size", "fullness", "frames", "last_qp_p",
              "last_qp_i", "last_bits_p", "last_bits_i", "last_cplx_p", "last_cplx_i", "cplx_ema", "cur_qp",
              "cur_intra", "cur_cplx", "max_p_bits", "seq", "cur_valid", "pixels", "cur_idr", "redos", "qp_floor", "floor_age", "last_mbs_p", "last_mbs_i", "cur_mbs", "vbv_ms", "last_qpf_p", "last_qpf_i", "cur_qpf",
-             "cur_redo", "redo_qpf", "redo_bits", "codec")
+             "cur_redo", "redo_qpf", "redo_bits", "codec", "lam_boost")
 
 
 class H264Encoder:
