@@ -1169,36 +1169,39 @@ SK_HD int palette_cache(const FrameView& v, const TileRect& t, int r, int c, uin
 }
 
 // ColorOrder and ColorContextHash -> context of the index at (i, j) of a colour map
-// (pitch n); returns the context, order[0..k) the colours by neighbour score.
-SK_HD int palette_color_context(const uint8_t* map, int n, int i, int j, int k, uint8_t* order) {
-    int sc[kPalMax];
-    for (int q = 0; q < kPalMax; q++) {
-        sc[q] = 0;
-        order[q] = (uint8_t)q;
-    }
-    if (j > 0) sc[map[i * n + j - 1]] += 2;
-    if (i > 0 && j > 0) sc[map[(i - 1) * n + j - 1]] += 1;
-    if (i > 0) sc[map[(i - 1) * n + j]] += 2;
+// (pitch n); *order gets the colours by neighbour score as nibbles (colour of rank r in
+// bits 4r..4r+3). Scores (<= 5) and the order live in packed registers: no arrays the GPU
+// would index dynamically (scratch memory).
+SK_HD int palette_color_context(const uint8_t* map, int n, int i, int j, int k, uint32_t* order) {
+    uint32_t sc = 0, ord = 0x76543210u;   // nibble q: score / colour of rank q
+    if (j > 0) sc += 2u << (4 * map[i * n + j - 1]);
+    if (i > 0 && j > 0) sc += 1u << (4 * map[(i - 1) * n + j - 1]);
+    if (i > 0) sc += 2u << (4 * map[(i - 1) * n + j]);
+    auto nib = [](uint32_t w, int q) { return (int)((w >> (4 * q)) & 15u); };
     for (int q = 0; q < 3; q++) {
-        int best = sc[q], bi = q;
+        int best = nib(sc, q), bi = q;
         for (int x = q + 1; x < k; x++)
-            if (sc[x] > best) {
-                best = sc[x];
+            if (nib(sc, x) > best) {
+                best = nib(sc, x);
                 bi = x;
             }
-        if (bi != q) {
-            const int o = order[bi];
-            for (int x = bi; x > q; x--) {
-                sc[x] = sc[x - 1];
-                order[x] = order[x - 1];
-            }
-            sc[q] = best;
-            order[q] = (uint8_t)o;
+        if (bi != q) {   // move rank bi to rank q, ranks q..bi-1 down one
+            const uint32_t lo = (1u << (4 * q)) - 1u, mid = ((1u << (4 * bi)) - 1u) & ~lo;
+            const uint32_t hi = bi == 7 ? 0u : ~((1u << (4 * (bi + 1))) - 1u);
+            const uint32_t o = (uint32_t)nib(ord, bi);
+            sc = (sc & (lo | hi)) | ((sc & mid) << 4) | ((uint32_t)best << (4 * q));
+            ord = (ord & (lo | hi)) | ((ord & mid) << 4) | (o << (4 * q));
         }
     }
-    const int hash = sc[0] + 2 * sc[1] + 2 * sc[2];
-    constexpr int8_t kCtx[9] = {-1, -1, 0, -1, -1, 4, 3, 2, 1};
-    return kCtx[hash];
+    *order = ord;
+    const int hash = nib(sc, 0) + 2 * nib(sc, 1) + 2 * nib(sc, 2);
+    return hash == 2 ? 0 : (hash == 5 ? 4 : (hash == 6 ? 3 : (hash == 7 ? 2 : (hash == 8 ? 1 : -1))));
+}
+// Rank of colour x in a packed order.
+SK_HD int palette_rank(uint32_t order, int k, int x) {
+    int rank = 0;
+    for (int q = 0; q < k; q++) rank = (int)((order >> (4 * q)) & 15u) == x ? q : rank;
+    return rank;
 }
 
 // Index of each sample of a palette block (raster, pitch n): its source value's position
@@ -1284,11 +1287,9 @@ SK_HD void code_palette_tokens(Sink& w, const CdfContext& cx, const FrameView& v
     for (int d = 1; d < 2 * n - 1; d++)
         for (int j = sk_min(d, n - 1); j >= sk_max(0, d - n + 1); j--) {
             const int i = d - j;
-            uint8_t order[kPalMax];
-            const int ctx = palette_color_context(map, n, i, j, k, order);
-            int rank = 0;
-            for (int q = 0; q < k; q++) rank = order[q] == map[i * n + j] ? q : rank;
-            w.sym(cdf_off(cx, cx.palette_y_color[k - 2][ctx]), k, rank);
+            uint32_t order;
+            const int ctx = palette_color_context(map, n, i, j, k, &order);
+            w.sym(cdf_off(cx, cx.palette_y_color[k - 2][ctx]), k, palette_rank(order, k, map[i * n + j]));
         }
 }
 

@@ -1001,11 +1001,9 @@ __device__ void code_palette_tokens(WaveTokenSink& w, const CdfContext& cx, cons
         const int before = d < n ? d * (d + 1) / 2 : n * n - (2 * n - 1 - d) * (2 * n - d) / 2;
         const int jmax = d < n ? d : n - 1;
         const int o = w.n + before + (jmax - x) - 1;
-        uint8_t order[kPalMax];
-        const int ctx = palette_color_context(map, n, y, x, k, order);
-        int rank = 0;
-        for (int q = 0; q < k; q++) rank = order[q] == map[i] ? q : rank;
-        if (o < w.cap) w.p[o] = tok_sym(cdf_off(cx, cx.palette_y_color[k - 2][ctx]), k, rank);
+        uint32_t order;
+        const int ctx = palette_color_context(map, n, y, x, k, &order);
+        if (o < w.cap) w.p[o] = tok_sym(cdf_off(cx, cx.palette_y_color[k - 2][ctx]), k, palette_rank(order, k, map[i]));
     }
     w.n += n * n - 1;
     wsync();
