@@ -259,9 +259,11 @@ static long long quant_block(const uint8_t* src, int sstride, const uint8_t* pre
         lv[k] = (int16_t)quantize(co[k], q, intra);
         const long long e = (long long)co[k] - dequant(lv[k], q);
         d += e * e;
-        z += (long long)co[k] * co[k];
+        z += (long long)res[k] * res[k];
     }
-    if (jzero) *jzero += 4 * z;   // J of coding nothing (the skip alternative: no rate)
+    // J of coding nothing (the skip alternative, no rate): 256 x the residual's SSE, the
+    // coefficient-domain scale of tx_rd_cost's distortion (8 x orthonormal, x4)
+    if (jzero) *jzero += 256 * z;
     int eob = 0;
     for (int c = nn - 1; c >= 0 && !eob; c--)
         if (lv[default_scan(log2n, c)]) eob = c + 1;

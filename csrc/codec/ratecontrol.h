@@ -123,7 +123,9 @@ SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min,
 SK_HD long long rc_frame_cap(const RcState& rc, bool key) {
     if (key) return 4ll * rc.budget;
     const long long vbv = sk_min((long long)rc.vbv_size, (long long)rc.budget + rc.budget / 2);
-    return vbv - rc.budget / 16;
+    // a long buffer (AV1) keeps a thinner margin under 1.5 budgets: its 4K120 frames swing
+    // +-30 % at one qindex and every re-code is a second coding pass inside the frame interval
+    return vbv - (rc.vbv_ms > 0 ? rc.budget / 32 : rc.budget / 16);
 }
 
 // QP whose lambda prices motion vectors in the motion search, which runs before the
@@ -161,11 +163,11 @@ SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intr
         int target = rc.budget + (rc.vbv_size / 2 - rc.fullness) / 4;
         // key frames (IDR) may use 3 budgets and are paid back by the frames after
         // them; every other frame, scene-cut intra pictures included, stays under 1.25x
-        // (a long buffer, AV1's 120 ms: 1.125x, its frames vary +-30 % at one qindex and
+        // (a long buffer, AV1's 120 ms: 1.0625x, its frames vary +-30 % at one qindex and
         // the per-frame cap is 1.5 budgets; aiming at 1.25x re-coded every 4th frame of
-        // the 4K120 bench content)
+        // the 4K120 bench content, 1.125x every 8th)
         if (idr) target = sk_max(target, 3 * rc.budget);
-        else target = sk_min(target, rc.budget + (rc.vbv_ms > 0 ? rc.budget / 8 : rc.budget / 4));
+        else target = sk_min(target, rc.budget + (rc.vbv_ms > 0 ? rc.budget / 16 : rc.budget / 4));
         target = sk_max(target, rc.budget / 4);
         if (target < 64) target = 64;
         if (rc.last_bits[k] > 0) {

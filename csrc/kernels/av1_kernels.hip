@@ -75,6 +75,7 @@ struct BlkLds {
     int32_t b[384];
     int16_t lv[384];     // quantised levels (raster per plane) before tail trimming
     int16_t lv2[384];    // IDTX levels of the same residual (the transform-type decision)
+    long long jreg;      // intra: the luma J of the cheaper transform type (palette decision)
     IntraEdge e[3];      // intra edges of Y, U, V
 };
 // Tile of a unit position (mi r, c).
@@ -154,16 +155,22 @@ __device__ int rate2_wave(const int16_t* lv, int ln) {
 // L.pred, and returns the per-plane level summaries (cul | dc << 6) packed as bytes
 // 0..2, bit 24 = any nonzero, bit 25 = IDTX.
 __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int qidx, bool intra, int16_t* gy,
-                                    int16_t* gu, int16_t* gv, long long* jmin = nullptr) {
+                                    int16_t* gu, int16_t* gv) {
     const int l = lane();
     const int n = 1 << log2n, nn = n * n, cn = n >> 1, cnn = cn * cn;
     const int qd = dc_q(qidx), qa = ac_q(qidx);
     // plane p element i: luma [0, nn), U [256, 256 + cnn), V [320, 320 + cnn)
     auto base = [&](int p) { return p == 0 ? 0 : (p == 1 ? 256 : 320); };
+    int e2 = 0;   // the residual's SSE: J of coding nothing (inter RD skip)
     for (int p = 0; p < 3; p++) {
         const int m = p ? cnn : nn, o = base(p);
-        for (int i = l; i < m; i += 64) L.a[o + i] = (int)L.src[o + i] - (int)L.pred[o + i];
+        for (int i = l; i < m; i += 64) {
+            const int e = (int)L.src[o + i] - (int)L.pred[o + i];
+            L.a[o + i] = e;
+            e2 += e * e;
+        }
     }
+    const long long jz = 256ll * wsum(e2);
     wsync();
     // forward stage 1 (columns): b[k][j] = (sum_m K[k][m] a[m][j] + 512) >> 10
     for (int p = 0; p < 3; p++) {
@@ -180,12 +187,12 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
     // forward stage 2 (rows) + quantisation, DCT levels to L.lv and IDTX levels (8 x the
     // residual, still in L.a) to L.lv2, with both squared coefficient errors per plane
     // transform type: J per plane (av1_core.h tx_rd_cost) summed over the decision planes
-    long long jd = 0, ji = 0, jz = 0;
+    long long jd = 0, ji = 0;
     const int np = intra ? 1 : 3;   // planes in the decision
     for (int p = 0; p < 3; p++) {
         const int ln = p ? log2n - 1 : log2n, sz = 1 << ln, o = base(p);
         const int16_t* K = fdct_k(F, ln);
-        long long ed = 0, ei = 0, ez = 0;
+        long long ed = 0, ei = 0;
         for (int i = l; i < sz * sz; i += 64) {
             const int k = i >> ln, lc = i & (sz - 1);
             // |sum| <= |t|_2 |K|_2 < 2^31 (orthonormal Q13 rows, |t| <= 8 * 255 * sqrt(N)):
@@ -198,7 +205,6 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
             L.lv[o + i] = (int16_t)lv;
             const long long e = (long long)c - dequant(lv, q);
             ed += e * e;
-            ez += (long long)c * c;
             if (p < np) {
                 const int32_t ci = 8 * L.a[o + i];
                 const int li = quantize(ci, q, intra);
@@ -208,7 +214,6 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
             }
         }
         const long long dp = wsum64(ed), ip = wsum64(ei);
-        jz += 4 * wsum64(ez);
         if (p < np) {
             wsync();   // the plane's levels, for the rate estimates
             jd += tx_rd_cost(4 * dp, rate2_wave(L.lv + o, ln), qa);
@@ -216,7 +221,9 @@ __device__ uint32_t code_block_wave(BlkLds& L, const FdctLds& F, int log2n, int 
         }
     }
     wsync();
-    if (jmin) *jmin = jd < ji ? jd : ji;   // intra: the luma J of the cheaper transform type
+    // intra: the luma J of the cheaper transform type, through LDS (an out-pointer kept jd /
+    // ji live across the inter kernel too: 256 VGPRs, occupancy 1)
+    if (intra && l == 0) L.jreg = jd < ji ? jd : ji;
     bool idtx;
     {
         if (intra) {
@@ -534,9 +541,9 @@ __device__ void intra_rec_block(const Av1Args& A, BlkLds& L, const FdctLds& F, i
         L.pred[320 + i] = (uint8_t)dcv;
     }
     wsync();
-    long long jreg = 0;
     uint32_t s = code_block_wave(L, F, log2n, qidx, true, lev_ptr(A, r, c, bsl, 0), lev_ptr(A, r, c, bsl, 1),
-                                 lev_ptr(A, r, c, bsl, 2), &jreg);
+                                 lev_ptr(A, r, c, bsl, 2));
+    const long long jreg = L.jreg;
     b.tx_type = (int16_t)((s >> 25) & 1 ? TX_IDTX : TX_DCT_DCT);
     b.pal_n = 0;
     if (A.palette && r + (1 << bsl) <= g.mi_rows && c + (1 << bsl) <= g.mi_cols) {
