@@ -26,11 +26,15 @@ namespace h264 {
 enum RcMode : int32_t { RC_CQP = 0, RC_CRF = 1, RC_CBR = 2 };
 
 // Re-code passes an encoder may add to a frame over its per-frame cap (rc_redo_step):
-// HEVC two (a scene cut coded at QP 0 needs ~26 QP), H.264 and AV1 one (AV1 sits at the
-// top of its quantiser range on 4K120 content, where a further pass rarely gains, and a
-// third 4K pass would cost the frame interval).
+// HEVC two (a scene cut coded at QP 0 needs ~26 QP), H.264 one, AV1 two below 4K (a
+// burst - a window opening - can start at 40x the budget; one slope-guessed step left
+// 1080p desktop frames at 2-3x) and one at 4K (it sits at the top of its quantiser range
+// on 4K120 content, where a further pass rarely gains, and a third 4K pass would cost the
+// frame interval). pixels: luma samples per frame.
 constexpr int kMaxRecodes = 2;
-SK_HD int rc_max_recodes(int codec) { return codec == 1 ? 2 : 1; }
+SK_HD int rc_max_recodes(int codec, int pixels = 0) {
+    return codec == 1 ? 2 : (codec == 2 && pixels < 3840 * 2160 / 2 ? 2 : 1);
+}
 
 struct RcState {
     int32_t mode, base_qp, qp_min, qp_max;
@@ -241,6 +245,12 @@ SK_HD int rc_dither_qp(int qpf, int i) {
     return lo + ((((i + 1) * f + 128) >> 8) - ((i * f + 128) >> 8));
 }
 
+// A burst: the frame in flight is far busier than the last inter frame (a window
+// opening, a page of new text), measured by the motion search before coding.
+SK_HD bool rc_burst(const RcState& rc) {
+    return rc.cur_cplx > 0 && rc.last_cplx[0] > 0 && 2 * (long long)rc.cur_cplx > 3 * (long long)rc.last_cplx[0];
+}
+
 // CBR guard (per-frame cap, rc_frame_cap): a frame whose payload exceeds its cap is
 // coded once more, coarser by the QP step this returns (0: keep it). The first step
 // assumes the model's 6 QP per halving towards the target; a further one uses the
@@ -256,7 +266,7 @@ SK_HD int rc_redo_step(const RcState& rc, long long frame_bits) {
     // picture (a second one doubled the 4K key-frame latency); the frames after a key
     // frame pay its overshoot back through the buffer, as they pay its planned 3 budgets
     if (rc.cur_idr && rc.codec != 0) return 0;
-    if (rc.cur_redo >= rc_max_recodes(rc.codec)) return 0;
+    if (rc.cur_redo >= rc_max_recodes(rc.codec, rc.pixels)) return 0;
     const long long cap = rc_frame_cap(rc, rc.cur_idr != 0);
     if (frame_bits <= cap) return 0;
     const uint32_t b = (uint32_t)(frame_bits > (1ll << 30) ? (1ll << 30) : frame_bits);
@@ -265,7 +275,7 @@ SK_HD int rc_redo_step(const RcState& rc, long long frame_bits) {
     // Q8 QP per halving: 6, except AV1 below QP 24, where screen content measured ~2 QP
     // per halving (1.65 -> 0.37 budgets over 4 QP at QP 17): 6 sent a 2x overflow to a
     // third of the budget there (at QP 40+ it still needs the 6)
-    int slope = rc.codec == 2 && rc.cur_qpf < (24 << 8) ? 3 << 8 : 6 << 8;
+    int slope = rc.codec == 2 && rc.cur_qpf < (24 << 8) && !rc_burst(rc) ? 3 << 8 : 6 << 8;
     if (rc.cur_redo > 0) {
         const int dq = rc.cur_qpf - rc.redo_qpf;
         const int dl = rc_ilog2_q8((uint32_t)sk_max(rc.redo_bits, 2)) - rc_ilog2_q8(b);
@@ -286,12 +296,6 @@ SK_HD int rc_redo_model_qpf(const RcState& rc, int bits, int target) {
     if (dq <= 0 || l1 <= l2) return rc.cur_qpf;
     const long long q = (long long)rc.redo_qpf + (long long)dq * (l1 - lt) / (l1 - l2);
     return (int)sk_min(sk_max(q, (long long)rc.qp_min << 8), (long long)rc.qp_max << 8);
-}
-
-// A burst: the frame in flight is far busier than the last inter frame (a window
-// opening, a page of new text), measured by the motion search before coding.
-SK_HD bool rc_burst(const RcState& rc) {
-    return rc.cur_cplx > 0 && rc.last_cplx[0] > 0 && 2 * (long long)rc.cur_cplx > 3 * (long long)rc.last_cplx[0];
 }
 
 // The frame in flight (first pass at cur_qp) overflowed: remember its QP as a floor

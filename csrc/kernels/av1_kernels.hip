@@ -1708,7 +1708,7 @@ void launch_backend(const Av1Args& a, hipStream_t s, int* redo) {
     if (redo) {   // K10 CBR per-frame cap: payload = the tile bytes (as k_rc_account)
         Av1Args b = a;
         b.f.gate = redo;
-        for (int r = 0; r < h264::rc_max_recodes(2); r++) {
+        for (int r = 0; r < h264::rc_max_recodes(2, a.geo.W * a.geo.H); r++) {
             h264::gpu::launch_rc_guard_sizes(a.f, a.tile_size, tiles, redo, r > 0, s);
             launch_code(b, s);
         }
