@@ -9,3 +9,4 @@ for rep in 1 2 3; do
     python -c "import json,sys; d=json.loads(open('gpurun_out/r5b/${t}_$rep.json').read().strip().splitlines()[-1]); print('$t', $rep, d['value'], d['p50_encode_latency_ms'], d['p99_encode_latency_ms'])"
   done
 done
+bash tools/gpu.sh prof r5b_h264prof --gpus 1 --steps 20 --warmup 5 --e2e-sessions 0 --extra-4k 0 --e2e-av1 none
