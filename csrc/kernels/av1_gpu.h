@@ -22,6 +22,9 @@ struct Av1Args {
     BlkInfo* blk;             // [r8][c8]
     uint8_t* pal;             // [r8][c8][8] palette colours of each cell's block (key frames)
     int palette;              // palette coding of key frames enabled (av1_encoder.h palette_enabled)
+    int* pal_rate;            // [r8][c8] key frames: palette_rate2 of the block at that origin cell
+                              // (k_av1_intra_modes; its colour count rides in BlkInfo.pad1 until
+                              // k_av1_intra_rec decides)
     int16_t* lev;             // [units][kLevPerUnit]
     uint8_t* lctx[3];         // level contexts per plane (4x4 units), strides lctx_w
     int lctx_w[3];

@@ -473,6 +473,8 @@ __global__ __launch_bounds__(256) void k_av1_setup(Av1Args A) {
 __global__ __launch_bounds__(256) void k_av1_intra_modes(Av1Args A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ IntraEdge E[4];
+    __shared__ uint32_t pal_seen[4][8];
+    __shared__ uint8_t pal_map[4][256], pal_col[4][8];
     if (!A.frame[0]) return;
     const FrameArgs& f = A.f;
     const Av1Geo& g = A.geo;
@@ -511,6 +513,45 @@ __global__ __launch_bounds__(256) void k_av1_intra_modes(Av1Args A) {
         b.bsl = (uint8_t)bsl;
         b.mode = (uint8_t)best;
         b.uv_mode = DC_PRED;
+        // palette candidate (source only, so decided here in parallel rather than in the
+        // reconstruction wavefront): the block's distinct luma values, its colours into
+        // the palette cells, palette_rate2 for k_av1_intra_rec's RD comparison
+        if (A.palette && r + (1 << bsl) <= g.mi_rows && c + (1 << bsl) <= g.mi_cols) {
+            uint32_t* seen = pal_seen[w];
+            uint8_t* map = pal_map[w];
+            uint8_t* col = pal_col[w];
+            if (l < 8) seen[l] = 0u;
+            wsync();
+            for (int i = l; i < n * n; i += 64) {
+                const int v = f.src.y[(size_t)(r * 4 + i / n) * f.stride_y + c * 4 + i % n];
+                atomicOr(&seen[v >> 5], 1u << (v & 31));
+            }
+            wsync();
+            const int k = wsum(l < 8 ? __builtin_popcount(seen[l]) : 0);
+            if (k >= 2 && k <= kPalMax) {
+                if (l == 0) {
+                    int q = 0;
+                    for (int v = 0; v < 256; v++)
+                        if ((seen[v >> 5] >> (v & 31)) & 1) col[q++] = (uint8_t)v;
+                    for (; q < 8; q++) col[q] = 0;
+                }
+                wsync();
+                for (int i = l; i < n * n; i += 64)
+                    map[i] = (uint8_t)palette_index(col, k, f.src.y[(size_t)(r * 4 + i / n) * f.stride_y + c * 4 + i % n]);
+                wsync();
+                int r2 = 0;
+                for (int i = l; i < n * n; i += 64) r2 += palette_rate2_px(map, n, i / n, i % n, k);
+                r2 = wsum(r2) + palette_rate2_head(k);
+                const int n8 = (1 << bsl) >> 1;
+                for (int i = l; i < n8 * n8 * 8; i += 64) {
+                    const int cell = i >> 3, ry = (r >> 1) + cell / n8, cx = (c >> 1) + cell % n8;
+                    A.pal[((size_t)ry * g.c8 + cx) * 8 + (i & 7)] = col[i & 7];
+                }
+                if (l == 0) A.pal_rate[(size_t)(r >> 1) * g.c8 + (c >> 1)] = r2;
+                b.pad1 = (uint8_t)k;
+            }
+            wsync();
+        }
         set_cells(A, r, c, bsl, b);
         wsync();
     }
@@ -545,47 +586,22 @@ __device__ void intra_rec_block(const Av1Args& A, BlkLds& L, const FdctLds& F, i
                                  lev_ptr(A, r, c, bsl, 2));
     const long long jreg = L.jreg;
     b.tx_type = (int16_t)((s >> 25) & 1 ? TX_IDTX : TX_DCT_DCT);
+    // palette candidate from k_av1_intra_modes (colours already in the palette cells):
+    // exact palette of the source luma vs the transform path (av1_cpu.cpp intra_block)
+    const int kc = b.pad1;
+    b.pad1 = 0;
     b.pal_n = 0;
-    if (A.palette && r + (1 << bsl) <= g.mi_rows && c + (1 << bsl) <= g.mi_cols) {
-        // exact palette of the source luma vs the transform path (av1_cpu.cpp intra_block)
-        uint32_t* seen = (uint32_t*)L.b;   // free after code_block_wave
-        uint8_t* map = (uint8_t*)L.a;
-        uint8_t* col = map + 256;
-        if (l < 8) seen[l] = 0u;
-        wsync();
-        for (int i = l; i < n * n; i += 64) atomicOr(&seen[L.src[i] >> 5], 1u << (L.src[i] & 31));
-        wsync();
-        const int k = wsum(l < 8 ? __builtin_popcount(seen[l]) : 0);
-        if (k >= 2 && k <= kPalMax) {
-            if (l == 0) {
-                int q = 0;
-                for (int v = 0; v < 256; v++)
-                    if ((seen[v >> 5] >> (v & 31)) & 1) col[q++] = (uint8_t)v;
-            }
-            wsync();
-            for (int i = l; i < n * n; i += 64) map[i] = (uint8_t)palette_index(col, k, L.src[i]);
-            wsync();
-            int r2 = 0;
-            for (int i = l; i < n * n; i += 64) r2 += palette_rate2_px(map, n, i / n, i % n, k);
-            r2 = wsum(r2) + palette_rate2_head(k);
-            if (tx_rd_cost(0, r2, ac_q(qidx)) < jreg) {
-                b.pal_n = (uint8_t)k;
-                b.mode = DC_PRED;
-                b.tx_type = TX_DCT_DCT;
-                int16_t* gy = lev_ptr(A, r, c, bsl, 0);
-                for (int i = l; i < n * n; i += 64) {
-                    gy[i] = 0;
-                    L.pred[i] = L.src[i];
-                }
-                s &= ~0xffu;   // no luma levels: the summary and the skip flag come from chroma
-                s = (s & ~(1u << 24)) | ((s & 0xffff00u) ? (1u << 24) : 0u);
-                const int n8 = (1 << bsl) >> 1;
-                for (int i = l; i < n8 * n8 * 8; i += 64) {
-                    const int cell = i >> 3, ry = (r >> 1) + cell / n8, cx = (c >> 1) + cell % n8;
-                    A.pal[((size_t)ry * g.c8 + cx) * 8 + (i & 7)] = (i & 7) < k ? col[i & 7] : 0;
-                }
-            }
+    if (kc && tx_rd_cost(0, A.pal_rate[(size_t)(r >> 1) * g.c8 + (c >> 1)], ac_q(qidx)) < jreg) {
+        b.pal_n = (uint8_t)kc;
+        b.mode = DC_PRED;
+        b.tx_type = TX_DCT_DCT;
+        int16_t* gy = lev_ptr(A, r, c, bsl, 0);
+        for (int i = l; i < n * n; i += 64) {
+            gy[i] = 0;
+            L.pred[i] = L.src[i];
         }
+        s &= ~0xffu;   // no luma levels: the summary and the skip flag come from chroma
+        s = (s & ~(1u << 24)) | ((s & 0xffff00u) ? (1u << 24) : 0u);
         wsync();
     }
     store_rec_blk(L, f, x, y, n);

@@ -814,6 +814,7 @@ class HipBackend : public EncoderBackend {
         a.blk = dmalloc<av1::BlkInfo>((size_t)av1_geo_.c8 * av1_geo_.r8);
         a.pal = dmalloc<uint8_t>((size_t)av1_geo_.c8 * av1_geo_.r8 * 8);
         a.palette = av1::palette_enabled() ? 1 : 0;
+        a.pal_rate = dmalloc<int>((size_t)av1_geo_.c8 * av1_geo_.r8);
         a.lev = dmalloc<int16_t>((size_t)n * av1::gpu::kLevPerUnit);
         a.lctx_w[0] = av1_geo_.mi_cols;
         a.lctx_w[1] = a.lctx_w[2] = av1_geo_.mi_cols >> 1;
