@@ -99,8 +99,12 @@ def main():
         return
     out = {}
     for kind in a.content.split(","):
-        out[kind] = {c: [run_point(c, q, a.width, a.height, a.frames, kind, a.backend) for q in QPS]
-                     for c in ("h264", "hevc", "av1")}
+        out[kind] = {}
+        for c in ("h264", "hevc", "av1"):
+            out[kind][c] = []
+            for q in QPS:
+                out[kind][c].append(run_point(c, q, a.width, a.height, a.frames, kind, a.backend))
+                print(f"# {kind} {c} QP {q}: {out[kind][c][-1]}", file=sys.stderr, flush=True)   # progress
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f)
