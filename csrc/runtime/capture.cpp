@@ -16,6 +16,7 @@
 #include <memory>
 #include <chrono>
 #include <mutex>
+#include <stdio.h>
 #include <string.h>
 #include <string>
 #include <thread>
@@ -513,20 +514,29 @@ class CaptureSession {
             return -1;
         }
         bool carried = false;
+        std::string why;
         const int64_t n = enc_->state_bytes();
-        if (n > 0 && nenc->state_bytes() == n) {
+        if (n <= 0) {
+            why = "the encoder keeps no inter-frame state";
+        } else if (nenc->state_bytes() != n) {
+            why = "state sizes differ";
+        } else {
             void* a = sk_dev_alloc(s_.device, n);
             void* b = sk_dev_alloc(dev, n);
             try {
-                carried = a && b && enc_->export_state(a, 1) == 0 && sk_dev_copy(dev, b, a, n, 3) == 0 &&
-                          nenc->import_state(b, 1) == 0;
-            } catch (const std::exception&) {
-                carried = false;
+                if (!a || !b) why = "device buffers: " + std::string(sk_last_error());
+                else if (enc_->export_state(a, 1) != 0) why = "export: " + std::string(sk_last_error());
+                else if (sk_dev_copy(dev, b, a, n, 3) != 0) why = "peer copy: " + std::string(sk_last_error());
+                else if (nenc->import_state(b, 1) != 0) why = "import: " + std::string(sk_last_error());
+                else carried = true;
+            } catch (const std::exception& ex) {
+                why = std::string("exception: ") + ex.what();
             }
             if (a) sk_dev_free(s_.device, a);
             if (b) sk_dev_free(dev, b);
         }
         if (!carried) {   // a fresh stream: key frame, with the rate control last asked for
+            fprintf(stderr, "[capture] move to GPU %d: state not carried (%s), key frame\n", dev, why.c_str());
             nenc->request_keyframe();
             if (last_qp_) nenc->set_qp(last_qp_ & 0xffff, last_qp_ >> 16);
             if (last_rate_) nenc->set_rate((int)((last_rate_ >> 32) & 0xff), (int)(last_rate_ & 0xffffffff));

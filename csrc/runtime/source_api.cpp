@@ -114,7 +114,11 @@ int sk_dev_copy(int32_t device, void* dst, const void* src, int64_t bytes, int32
         return -1;
     }
     if (!hip_ok(hipSetDevice(device), "hipSetDevice")) return -1;
-    return hip_ok(hipMemcpy(dst, src, (size_t)bytes, kinds[kind]), "hipMemcpy") ? 0 : -1;
+    // A device-to-device hipMemcpy may return before the copy lands, and the encoders'
+    // streams are non-blocking (no implicit ordering with the null stream): wait for it,
+    // so the caller can hand `dst` to any stream.
+    return hip_ok(hipMemcpy(dst, src, (size_t)bytes, kinds[kind]), "hipMemcpy") &&
+                   hip_ok(hipStreamSynchronize(nullptr), "hipStreamSynchronize") ? 0 : -1;
 }
 
 int sk_dev_copy2d(int32_t device, void* dst, int64_t dpitch, const void* src, int64_t spitch, int64_t width,
@@ -127,7 +131,7 @@ int sk_dev_copy2d(int32_t device, void* dst, int64_t dpitch, const void* src, in
     }
     if (!hip_ok(hipSetDevice(device), "hipSetDevice")) return -1;
     return hip_ok(hipMemcpy2D(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)height, kinds[kind]),
-                  "hipMemcpy2D") ? 0 : -1;
+                  "hipMemcpy2D") && hip_ok(hipStreamSynchronize(nullptr), "hipStreamSynchronize") ? 0 : -1;
 }
 
 }  // extern "C"
