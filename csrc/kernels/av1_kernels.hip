@@ -1145,6 +1145,11 @@ __device__ __forceinline__ uint32_t ec_word(uint32_t clo, uint32_t chi, int n, i
 // the chunk (about 1 / kEcParts of them, plus the literals for partition 0) in LDS.
 constexpr int kChunk = 1024;
 
+// update_cdf of one CDF entry in one dependent step: towards 32768 (target 32768) or
+// towards 0 (target (1 << rate) - 1, which makes the arithmetic shift round the way
+// c - (c >> rate) does); equal to both forms for every c in [0, 32768].
+__device__ __forceinline__ int cdf_step(int c, int target, int rate) { return c + ((target - c) >> rate); }
+
 __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CdfContext cx;
@@ -1171,12 +1176,19 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
     // are built after the loop, one lane per token. Every wave first compacts its own
     // tokens of a chunk (ballot + prefix count), so the serial batches hold only them and
     // each word is stored once, at its stream position.
+    // A run of consecutive tokens in the cached context with its counter saturated
+    // (`hot`) takes a tight loop with no context or counter checks, and the update is one
+    // dependent step per entry (cdf_step).
     int cache_off = -1, cache_n = 0, cnt = 0, rate = 0, rbase = 0;
     uint32_t cache = 0;
+    uint32_t hot = ~0u;   // token bits (kind, N, slot) of the cached context once its counter saturated
     auto evict = [&]() {
         if (cache_off >= 0) {
-            if (L < cache_n - 1) cdfs[cache_off + L] = (uint16_t)cache;
-            else if (L == cache_n) cdfs[cache_off + L] = (uint16_t)cnt;
+            if (L < cache_n - 1) {
+                cdfs[cache_off + L] = (uint16_t)cache;
+            } else if (L == cache_n) {
+                cdfs[cache_off + L] = (uint16_t)cnt;
+            }
         }
         cache_off = -1;
     };
@@ -1184,41 +1196,59 @@ __global__ __launch_bounds__(64) void k_av1_cdf(Av1Args A) {
         const bool valid = b + L < nown;
         const uint32_t tv = valid ? ctok[b + L] : (1u << 30);
         const uint32_t kind = tv >> 30;   // literal tokens are their own word (partition 0's)
+        const uint32_t sv = (tv >> 22) & 15;   // the symbol of a symbol token
         uint64_t m = __ballot(valid && kind != 1);
+        int i = m ? __builtin_ctzll(m) : 0;
+        uint32_t tt = sgpr(rdlane(tv, i));
         while (m) {
-            const int i = __builtin_ctzll(m);
-            asm volatile("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(i));   // m &= m - 1 in one SALU op
-            const uint32_t tt = sgpr(rdlane(tv, i));
-            if ((tt >> 30) == 0) {
-                const int off = (int)(tt & 0x3fffff);
-                if (off != cache_off) {
-                    evict();
+            if ((tt & 0xFC3FFFFFu) == hot) {
+                // a run of consecutive tokens in the cached context, its counter saturated:
+                // a tight loop (no context checks, no counter updates)
+                const uint64_t above = __ballot((tv & 0xFC3FFFFFu) == hot) >> i;
+                const int e = i + (~above ? __builtin_ctzll(~above) : 64);
+                m = e >= 64 ? 0ull : m & (~0ull << e);
+                const int lo = (1 << rate) - 1;
+                for (int j = i; j < e; j++) {
+                    const int sj = (int)sgpr(rdlane(sv, j));
+                    cap[j][L] = (uint16_t)cache;
+                    cache = (uint32_t)cdf_step((int)cache, L >= sj ? 32768 : lo, rate);
+                }
+            } else {
+                asm volatile("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(i));   // m &= m - 1 in one SALU op
+                if ((tt >> 30) == 0) {
+                    const int off = (int)(tt & 0x3fffff);
                     const int n = (int)((tt >> 26) & 15) + 1;
-                    cache = L <= n ? (uint32_t)cdfs[off + L] : 0u;
-                    cache_off = off;
-                    cache_n = n;
-                    cnt = (int)sgpr(rdlane(cache, n));
-                    rbase = 3 + (n > 3 ? 2 : (n > 1 ? 1 : 0));
-                    rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
+                    const int s = (int)((tt >> 22) & 15);
+                    if (off != cache_off) {
+                        evict();
+                        cache_off = off;
+                        cache_n = n;
+                        rbase = 3 + (n > 3 ? 2 : (n > 1 ? 1 : 0));
+                        cache = L <= n ? (uint32_t)cdfs[off + L] : 0u;
+                        cnt = (int)sgpr(rdlane(cache, n));
+                        rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
+                    }
+                    cap[i][L] = (uint16_t)cache;
+                    // update_cdf, branch-free: lanes >= s move towards 32768, the others to 0
+                    // (lanes >= N-1 are never written back; the counter lives in cnt)
+                    cache = (uint32_t)cdf_step((int)cache, L >= s ? 32768 : (1 << rate) - 1, rate);
+                    if (cnt < 32) {
+                        cnt++;
+                        rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
+                    }
+                } else {   // gathered boolean: reads a partition CDF from LDS
+                    evict();
+                    uint16_t c2[3];   // split_or_horz / split_or_vert (read-only CDF)
+                    gather_partition_cdf(cdfs + (tt & 0x3fffff), ((tt >> 29) & 1) == 0, c2);
+                    const uint32_t c0 = sgpr(c2[0]);
+                    const int v = (int)((tt >> 28) & 1);
+                    if (L == 0) wst[i] = ec_word(c0, v ? 32768u : c0, 2, v);
                 }
-                const int s = (int)((tt >> 22) & 15);
-                cap[i][L] = (uint16_t)cache;
-                // update_cdf, branch-free: lanes >= s move towards 32768, the others to 0
-                // (lanes >= N-1 are never written back; the counter lives in cnt)
-                const int c = (int)cache;
-                const int up = c + ((32768 - c) >> rate), dn = c - (c >> rate);
-                cache = (uint32_t)(L >= s ? up : dn);
-                if (cnt < 32) {
-                    cnt++;
-                    rate = (int)sgpr((uint32_t)(rbase + (cnt > 15) + (cnt > 31)));
-                }
-            } else {   // gathered boolean: reads a partition CDF from LDS
-                evict();
-                uint16_t c2[3];   // split_or_horz / split_or_vert (read-only CDF)
-                gather_partition_cdf(cdfs + (tt & 0x3fffff), ((tt >> 29) & 1) == 0, c2);
-                const uint32_t c0 = sgpr(c2[0]);
-                const int v = (int)((tt >> 28) & 1);
-                if (L == 0) wst[i] = ec_word(c0, v ? 32768u : c0, 2, v);
+                hot = sgpr(cache_off >= 0 && cnt >= 32 ? (uint32_t)cache_off | (uint32_t)(cache_n - 1) << 26 : ~0u);
+            }
+            if (m) {
+                i = __builtin_ctzll(m);
+                tt = sgpr(rdlane(tv, i));
             }
         }
         wsync();

@@ -473,6 +473,7 @@ class HipBackend : public EncoderBackend {
         else if (s == "tok_n" && cfg_.codec == 2) { p = aargs_.tok_n; n = (int64_t)g_.num_mbs() * 4; }
         else if (s == "tokc" && cfg_.codec == 2) { p = aargs_.tokc; n = (int64_t)av1_geo_.tile_cols * av1_geo_.tile_rows * aargs_.tile_tok_cap * 4; }
         else if (s == "tile_ntok" && cfg_.codec == 2) { p = aargs_.tile_ntok; n = (int64_t)av1_geo_.tile_cols * av1_geo_.tile_rows * 4; }
+        else if (s == "frame" && cfg_.codec == 2) { p = aargs_.frame; n = 16; }   // key, qidx, lf level, -
         else if (s == "tile_size" && cfg_.codec == 2) { p = aargs_.tile_size; n = (int64_t)av1_geo_.tile_cols * av1_geo_.tile_rows * 4; }
         else if (s == "av1_geo" && cfg_.codec == 2) {
             if (dst && cap >= (int64_t)sizeof(av1_geo_)) memcpy(dst, &av1_geo_, sizeof(av1_geo_));

@@ -23,12 +23,14 @@ def main():
     ap.add_argument("--fps", type=float, default=120.0)
     ap.add_argument("--content", default="motion")
     ap.add_argument("--qp", type=int, default=25)
+    ap.add_argument("--tiles", default="-1,-1", help="tile_cols_log2,tile_rows_log2 (-1: automatic)")
     a = ap.parse_args()
     from selkies_gstreamer_amd.ops.native import H264Encoder
     from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
     src = SyntheticDesktop(a.width, a.height, kind=a.content)
     enc = H264Encoder(a.width, a.height, codec="av1", fullframe=True, backend="hip", fps=a.fps,
-                      rate_control=a.mode, bitrate_kbps=a.kbps, qp=a.qp)
+                      rate_control=a.mode, bitrate_kbps=a.kbps, qp=a.qp,
+                      tile_cols_log2=int(a.tiles.split(",")[0]), tile_rows_log2=int(a.tiles.split(",")[1]))
     for t in range(a.frames):
         pk = enc.encode(src.frame(t), t)
     nbytes = sum(len(p.data) for p in pk)

@@ -69,6 +69,23 @@ driver)
     timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
     rc=$?; tail -1 "$OUT/bench.jsonl" | cut -c1-1500; [ $rc -ne 0 ] && { tail -20 "$OUT/bench.err"; exit $rc; }
     exit 0 ;;
+pmcpy)
+    # the first two counter passes of `pmc` over a python script: pmcpy TAG SCRIPT [ARGS...]
+    SCRIPT=$1; shift
+    P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT"
+    P2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
+    cd /tmp && export TMPDIR=/tmp
+    i=0; dirs=""
+    for P in "$P1" "$P2"; do
+        i=$((i+1))
+        timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/$SCRIPT" "$@" \
+            > "$OUT/p$i.log" 2>&1
+        rc=$?; [ $rc -ne 0 ] && { echo "pmc pass $i failed"; tail -5 "$OUT/p$i.log"; exit $rc; }
+        dirs="$dirs $(dirname $(ls "$OUT"/p$i/*counter_collection.csv "$OUT"/p$i/*/*counter_collection.csv 2>/dev/null | head -1))"
+    done
+    cd "$ROOT"
+    python tools/pmc_summary.py $dirs > "$OUT/pmc.md" 2>&1; head -40 "$OUT/pmc.md"
+    exit 0 ;;
 pmc)
     # four counter passes (rocprofv3 does not multiplex: <= 8 SQ, 4 TCC, 2 GRBM per pass)
     P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE GRBM_COUNT"

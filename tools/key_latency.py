@@ -25,11 +25,13 @@ ap.add_argument("--rc", default="crf")
 ap.add_argument("--kbps", type=int, default=0)
 ap.add_argument("--fps", type=float, default=60.0)
 ap.add_argument("--content", default="motion")
+ap.add_argument("--tiles", default="-1,-1", help="AV1 tile_cols_log2,tile_rows_log2 (-1: automatic)")
 a = ap.parse_args()
 src = SyntheticDesktop(a.width, a.height, a.content, seed=7)
 pool = [src.frame(i) for i in range(8)]
 enc = H264Encoder(a.width, a.height, codec=a.codec, fullframe=True, backend="hip", fps=a.fps, rate_control=a.rc,
-                  bitrate_kbps=a.kbps, use_paint_over=False)
+                  bitrate_kbps=a.kbps, use_paint_over=False,
+                  tile_cols_log2=int(a.tiles.split(",")[0]), tile_rows_log2=int(a.tiles.split(",")[1]))
 key, inter = [], []
 for t in range(a.frames):
     want_key = t >= 10 and t % a.period == 0
