@@ -1086,6 +1086,7 @@ struct FrameView {
     const uint8_t* pal;          // [r8][c8][8] palette colours of each cell's block
     const uint8_t* src_y;        // source luma: the colour index map of a palette block
     int stride_y;
+    MvStack* stk = nullptr;      // the reference MV stack's storage (set by the caller; GPU: this wave's LDS slot)
     SK_HD const BlkInfo& at(int r, int c) const { return blk[(r >> 1) * geo.c8 + (c >> 1)]; }
     SK_HD const uint8_t* pal_at(int r, int c) const { return pal + ((size_t)(r >> 1) * geo.c8 + (c >> 1)) * 8; }
     // levels of the block at mi (r, c) of size bsl in plane p (raster [row][col])
@@ -1095,7 +1096,12 @@ struct FrameView {
         const int k = ((r >> 1) & 1) * 2 + ((c >> 1) & 1);
         return u + (p == 0 ? 64 * k : (p == 1 ? 256 + 16 * k : 320 + 16 * k));
     }
-    SK_HD uint8_t lc(int p, int x4, int y4) const { return lctx[p][(size_t)y4 * lctx_w[p] + x4]; }
+    // selects without indexing lctx / lctx_w by a run-time plane: an indexed member array
+    // keeps the whole view in GPU scratch memory
+    SK_HD uint8_t lc(int p, int x4, int y4) const {
+        const uint8_t* b = p == 0 ? lctx[0] : (p == 1 ? lctx[1] : lctx[2]);
+        return b[(size_t)y4 * (p == 0 ? lctx_w[0] : lctx_w[1]) + x4];
+    }
 };
 
 // above / left level contexts of a tx block (plane units of 4 samples), tile-bounded:
@@ -1364,7 +1370,7 @@ SK_HD void code_block(Sink& w, const CdfContext& cx, const FrameView& v, const T
         w.sym(cdf_off(cx, cx.single_ref[rctx][0]), 2, 0);   // single_ref_p1: forward
         w.sym(cdf_off(cx, cx.single_ref[rctx][2]), 2, 0);   // p3: LAST / LAST2
         w.sym(cdf_off(cx, cx.single_ref[rctx][3]), 2, 0);   // p4: LAST
-        MvStack s;
+        MvStack& s = *v.stk;   // caller's (GPU: LDS; a per-lane array indexed at run time lives in scratch)
         const BlkGrid grid{v.blk, v.geo.c8};
         find_mv_stack(s, grid, t, v.geo.mi_rows, v.geo.mi_cols, r, c, bsl, DecodedBefore{r, c});
         const int mode = b.mode, idx = (b.flags >> 4) & 3;

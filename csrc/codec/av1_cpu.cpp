@@ -596,7 +596,9 @@ FrameView CpuAv1Encoder::view() const {
 
 std::vector<uint8_t> CpuAv1Encoder::code_tile(int t) {
     const TileRect tr = tile_rect(geo, t);
-    const FrameView v = view();
+    MvStack stk;
+    FrameView v = view();
+    v.stk = &stk;
     CdfContext cx = AV1_DEFAULT_CDF[coef_qctx(fp.qidx)];
     VectorSink sink;
     SymbolCoder<VectorSink> coder(sink);

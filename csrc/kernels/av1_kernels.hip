@@ -824,8 +824,9 @@ __device__ __forceinline__ int br_count(int a) {
 // neighbours lie on later anti-diagonals, already coded in the reverse scan), so lanes
 // take scan positions s = l + 64 k, place their tokens by a suffix sum over the reverse
 // scan, and pack the forward-scan sign / Golomb bits through LDS into 24-bit literals.
-__device__ int code_coeffs(WaveTokenSink& w, const CdfContext& cx, const int16_t* lev, int txs, int plane, CoefCtx cc,
-                           bool is_inter, int intra_dir, int qidx, int tx_type = TX_DCT_DCT) {
+__device__ __forceinline__ int code_coeffs_regs(WaveTokenSink& w, const CdfContext& cx, const int16_t* lev, int txs,
+                                                int plane, CoefCtx cc, bool is_inter, int intra_dir, int qidx,
+                                                int tx_type) {
     const int l = lane();
     const int log2n = txs + 2, n = 1 << log2n, nn = n * n, nw = (nn + 63) >> 6;
     const int ptype = plane > 0;
@@ -1003,6 +1004,17 @@ __device__ int code_coeffs(WaveTokenSink& w, const CdfContext& cx, const int16_t
     return sk_min(wsum(cul), 63) | (dcc << 6);
 }
 
+// code_coeffs is too large to inline at its nine call sites; the sink it updates per
+// token then lives behind a pointer in scratch memory. The call works on a register copy
+// and writes the sink back once.
+__device__ int code_coeffs(WaveTokenSink& wr, const CdfContext& cx, const int16_t* lev, int txs, int plane, CoefCtx cc,
+                           bool is_inter, int intra_dir, int qidx, int tx_type = TX_DCT_DCT) {
+    WaveTokenSink w = wr;
+    const int r = code_coeffs_regs(w, cx, lev, txs, plane, cc, is_inter, intra_dir, qidx, tx_type);
+    wr = w;
+    return r;
+}
+
 // Lane-parallel palette_tokens (codec/av1_core.h code_palette_tokens): every sample's
 // colour context depends only on the index map, so lanes rank their samples at once and
 // store each token at its anti-diagonal position.
@@ -1035,12 +1047,14 @@ __device__ void code_palette_tokens(WaveTokenSink& w, const CdfContext& cx, cons
 __global__ __launch_bounds__(256) void k_av1_tokens(Av1Args A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint32_t bits_w[4][256];
+    __shared__ MvStack stk_w[4];
     const int w = threadIdx.x >> 6;
     const int u = blockIdx.x * 4 + w;
     const FrameArgs& f = A.f;
     if (u >= f.mb_w * f.mb_h) return;
     const Av1Geo& g = A.geo;
     FrameView v;
+    v.stk = &stk_w[w];
     v.geo = g;
     v.blk = A.blk;
     v.lev = A.lev;
