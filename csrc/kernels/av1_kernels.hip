@@ -648,7 +648,7 @@ __global__ __launch_bounds__(1024) void k_av1_intra_rec(Av1Args A) {
 }
 
 // Inter frames: one wave per unit, vector from the front end's motion search.
-__global__ __launch_bounds__(256) void k_av1_inter(Av1Args A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_av1_inter(Av1Args A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ BlkLds Lw[4];
     __shared__ FdctLds F;
@@ -1044,7 +1044,7 @@ __device__ void code_palette_tokens(WaveTokenSink& w, const CdfContext& cx, cons
     wsync();
 }
 
-__global__ __launch_bounds__(256) void k_av1_tokens(Av1Args A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_av1_tokens(Av1Args A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint32_t bits_w[4][256];
     __shared__ MvStack stk_w[4];
