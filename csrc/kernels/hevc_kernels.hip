@@ -965,12 +965,17 @@ __global__ __launch_bounds__(256) void k_hevc_intra_seg(HevcArgs A) {
 }
 
 // ---------------------------------------------------------------------------
-// CU syntax -> bin entries: one thread per CU (a wave binarises 64 CUs at once).
-__global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
+// CU syntax -> bin entries: one thread per CU, `lpw` CUs per wave. The lanes diverge (each
+// binarises its own CU's coefficients), so a wave runs about as long as its busiest CU;
+// with 64 CUs per wave a 4K frame is only ~500 waves and half the SIMDs idle, with no
+// second wave to hide the global-memory latency behind.
+__global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A, int lpw) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int n = f.mb_w * f.mb_h;
-    const int idx = blockIdx.x * 256 + threadIdx.x;
+    const int l = threadIdx.x & 63;
+    if (l >= lpw) return;
+    const int idx = (blockIdx.x * 4 + (threadIdx.x >> 6)) * lpw + l;
     if (idx >= n) return;
     const int cx = idx % f.mb_w, cy = idx / f.mb_w;
     const SliceTask t = f.tasks[cy / f.rows_per_slice];
@@ -1908,7 +1913,8 @@ static void launch_code(const HevcArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_hevc_sao_stats, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sao_md, dim3((n * kSaoMd + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sao_row, dim3(ch), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_bins, dim3((n + 255) / 256), dim3(256), 0, s, a);
+    static const int lpw = getenv("SK_HEVC_BINS_LPW") ? sk_clip(atoi(getenv("SK_HEVC_BINS_LPW")), 1, 64) : 32;
+    hipLaunchKernelGGL(k_hevc_bins, dim3((n + 4 * lpw - 1) / (4 * lpw)), dim3(256), 0, s, a, lpw);
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(192), 0, s, a);
     hipLaunchKernelGGL(k_pc_model, dim3(slots, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);
