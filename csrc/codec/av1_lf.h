@@ -107,7 +107,9 @@ struct LfFrame {
 // Filter level of a block (7.14.4 with the deltas above): 0 for GLOBALMV inter blocks.
 SK_HD int lf_block_level(const LfFrame& f, const BlkInfo& b, int plane, int pass) {
     if (blk_inter(b) && b.mode == GLOBALMV) return 0;
-    return f.lvl[plane == 0 ? pass : plane + 1];
+    // selected, not indexed: a run-time index into lvl[] keeps the LfFrame in GPU scratch
+    const int k = plane == 0 ? pass : plane + 1;
+    return k == 0 ? f.lvl[0] : (k == 1 ? f.lvl[1] : (k == 2 ? f.lvl[2] : f.lvl[3]));
 }
 
 // edge_loop_filter (7.14.2) of MI (row, col) for one plane / pass: the four lines of the

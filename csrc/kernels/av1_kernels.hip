@@ -740,6 +740,7 @@ __global__ __launch_bounds__(64) void k_av1_merge(Av1Args A) {
 
 // Inter modes from the MV stack: one lane per 8x8 cell, block origins only.
 __global__ __launch_bounds__(256) void k_av1_modes(Av1Args A) {
+    __shared__ MvStack stk[256];
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     if (A.frame[0]) return;
     const Av1Geo& g = A.geo;
@@ -751,7 +752,7 @@ __global__ __launch_bounds__(256) void k_av1_modes(Av1Args A) {
     if ((y8 & (n8 - 1)) || (x8 & (n8 - 1))) return;
     const int r = y8 * 2, c = x8 * 2;
     const TileRect t = tile_of(g, r, c);
-    MvStack s;
+    MvStack& s = stk[threadIdx.x];   // LDS: a per-lane stack indexed at run time would live in scratch
     const BlkGrid grid{A.blk, g.c8};
     find_mv_stack(s, grid, t, g.mi_rows, g.mi_cols, r, c, b.bsl, DecodedBefore{r, c});
     int mode, idx = 0;
