@@ -562,7 +562,10 @@ void CpuHevcEncoder::sao_analyse() {
     for (int cy = 0; cy < geo.ctb_h; cy++) {
         const SliceTask& t = fe.tasks[cy / geo.rows_per_slice];
         const size_t o = (size_t)cy * geo.ctb_w;
-        sao_row_merge(&sao_md[o * kSaoMd], &sao_own[o], &sao_cost[o], geo.ctb_w, t.qp, smap(), cy, &sao[o]);
+        std::vector<uint16_t> sel(geo.ctb_w);
+        std::vector<uint8_t> fl(geo.ctb_w);
+        sao_row_merge(&sao_md[o * kSaoMd], &sao_own[o], &sao_cost[o], geo.ctb_w, t.qp, smap(), cy, &sao[o], sel.data(),
+                      fl.data());
     }
 }
 

@@ -6,6 +6,7 @@
 // pps_loop_filter_across_slices_enabled_flag is 0, so an edge-offset neighbour in another
 // slice (or outside the picture) leaves the sample unchanged.
 #pragma once
+#include <cstddef>
 #include "hevc_core.h"
 
 namespace sk {
@@ -199,13 +200,14 @@ SK_HD long long sao_params_dist(const SaoStats* st, const SaoParams& p) {
     }
     return d;
 }
+// Equal types, classes, band positions and offsets (merge_left and the padding aside):
+// six masked words instead of 21 byte compares (the sequential SAO merge chain runs it).
 SK_HD bool sao_same(const SaoParams& a, const SaoParams& b) {
-    for (int c = 0; c < 3; c++) {
-        if (a.type[c] != b.type[c] || a.eo_class[c] != b.eo_class[c] || a.band_pos[c] != b.band_pos[c]) return false;
-        for (int k = 0; k < 4; k++)
-            if (a.off[c][k] != b.off[c][k]) return false;
-    }
-    return true;
+    static_assert(offsetof(SaoParams, merge_left) == 9 && offsetof(SaoParams, off) == 10, "SaoParams layout");
+    const uint32_t* x = reinterpret_cast<const uint32_t*>(&a);
+    const uint32_t* y = reinterpret_cast<const uint32_t*>(&b);
+    return x[0] == y[0] && x[1] == y[1] && ((x[2] ^ y[2]) & 0xffff00ffu) == 0 && x[3] == y[3] && x[4] == y[4] &&
+           ((x[5] ^ y[5]) & 0x0000ffffu) == 0;
 }
 
 // Merge decision along one CTB row (sequential: a merged CTB copies its left neighbour's
@@ -223,15 +225,21 @@ SK_HD void sao_merge_dists(const SaoStats* st_x, const SaoParams* own_row, int x
 }
 // m / cy: the row's slices (a CTB merges left only inside its slice, and codes the
 // merge-up flag only under a CTB of its slice).
-SK_HD void sao_row_merge(const long long* md_row, const SaoParams* own, const long long* own_cost, int ctb_w, int qp,
-                         const SliceMap& m, int cy, SaoParams* out) {
+// The decisions alone: sel[x] = the CTB whose own parameters CTB x takes, bit 15 set when
+// x merges left (the GPU runs this on one lane and copies the parameters with all 64).
+// fl[x]: bit 0 = CTB x has a left neighbour in its slice, bit 1 = an upper one (the slice
+// map's tests, precomputed so the sequential chain does not evaluate them).
+SK_HD uint8_t sao_row_flags(const SliceMap& m, int cy, int x) {
+    return (uint8_t)((m.left(x, cy) ? 1 : 0) | (m.top(x, cy) ? 2 : 0));
+}
+SK_HD void sao_row_decide(const long long* md_row, const SaoParams* own, const long long* own_cost, int ctb_w, int qp,
+                          const uint8_t* fl, uint16_t* sel) {
     const int lam = sao_lambda(qp);
     int src = 0;   // CTB whose own parameters the previous CTB's final parameters are
     for (int x = 0; x < ctb_w; x++) {
-        SaoParams p = own[x];
         int sx = x;
-        const bool has_up = m.top(x, cy);
-        if (m.left(x, cy)) {
+        uint16_t merge = 0;
+        if (fl[x] & 1) {
             const int j = x - 1 - src;
             const long long* md = md_row + (size_t)x * kSaoMd;
             bool ok = true;
@@ -239,16 +247,26 @@ SK_HD void sao_row_merge(const long long* md_row, const SaoParams* own, const lo
             if (j < kSaoMergeWin) dm = md[j];
             else if (sao_same(own[x], own[src])) dm = md[kSaoMergeWin];
             else ok = false;
-            const long long cown = own_cost[x] + (long long)lam * (has_up ? 2 : 1);   // merge_left = 0 (+ merge_up = 0)
+            const long long cown = own_cost[x] + (long long)lam * ((fl[x] & 2) ? 2 : 1);   // merge_left = 0 (+ merge_up = 0)
             if (ok && dm + (long long)lam * 1 < cown) {
-                p = own[src];
-                p.merge_left = 1;
                 sx = src;
+                merge = 0x8000;
             }
         }
-        out[x] = p;
+        sel[x] = (uint16_t)(sx | merge);
         src = sx;
     }
+}
+SK_HD void sao_row_apply_sel(const SaoParams* own, uint16_t sel, SaoParams* out) {
+    SaoParams p = own[sel & 0x7fff];
+    p.merge_left = (sel >> 15) & 1;
+    *out = p;
+}
+SK_HD void sao_row_merge(const long long* md_row, const SaoParams* own, const long long* own_cost, int ctb_w, int qp,
+                         const SliceMap& m, int cy, SaoParams* out, uint16_t* sel, uint8_t* fl) {
+    for (int x = 0; x < ctb_w; x++) fl[x] = sao_row_flags(m, cy, x);
+    sao_row_decide(md_row, own, own_cost, ctb_w, qp, fl, sel);
+    for (int x = 0; x < ctb_w; x++) sao_row_apply_sel(own, sel[x], out + x);
 }
 
 // CTB syntax sao(rx, ry) (7.3.8.3) as bin entries. left/up: the neighbour CTB exists in
@@ -280,11 +298,18 @@ SK_HD void sao_bins(BinBuf& w, const SaoParams& p, bool left, bool up) {
 
 // Normative filter (8.7.3) for sample (x, y) of a plane: the deblocked value and its
 // neighbours come from `rec`; returns the SAO output.
+// off[c][k] through a packed word and a shift: a run-time index into the array keeps the
+// parameters in GPU scratch memory
+SK_HD int sao_off(const SaoParams& p, int c, int k) {
+    const uint32_t w = (uint32_t)(uint8_t)p.off[c][0] | (uint32_t)(uint8_t)p.off[c][1] << 8 |
+                       (uint32_t)(uint8_t)p.off[c][2] << 16 | (uint32_t)(uint8_t)p.off[c][3] << 24;
+    return (int)(int8_t)(uint8_t)(w >> (8 * k));
+}
 SK_HD int sao_apply_sample(const SaoParams& p, int c, const SaoPlane& g, const uint8_t* rec, int stride, int x, int y) {
     const int v = rec[(size_t)y * stride + x];
     if (p.type[c] == SAO_BAND) {
         const int k = ((v >> 3) - p.band_pos[c]) & 31;
-        return k < 4 ? sk_clip255(v + p.off[c][k]) : v;
+        return k < 4 ? sk_clip255(v + sao_off(p, c, k)) : v;
     }
     if (p.type[c] == SAO_EDGE) {
         const int cls = p.eo_class[c];
@@ -292,7 +317,7 @@ SK_HD int sao_apply_sample(const SaoParams& p, int c, const SaoPlane& g, const u
         const int a = rec[(size_t)(y + sao_dy(cls, 0)) * stride + x + sao_dx(cls, 0)];
         const int b = rec[(size_t)(y + sao_dy(cls, 1)) * stride + x + sao_dx(cls, 1)];
         const int e = sao_edge_idx(v, a, b);
-        return e ? sk_clip255(v + p.off[c][e - 1]) : v;
+        return e ? sk_clip255(v + sao_off(p, c, e - 1)) : v;
     }
     return v;
 }

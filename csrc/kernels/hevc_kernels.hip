@@ -1842,19 +1842,25 @@ __global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
     __shared__ long long md[kPcMaxRowCtb * kSaoMd];
     __shared__ SaoParams own[kPcMaxRowCtb];
     __shared__ long long cost[kPcMaxRowCtb];
+    __shared__ uint16_t sel[kPcMaxRowCtb];
+    __shared__ uint8_t fl[kPcMaxRowCtb];
     const FrameArgs& f = A.f;
     const int cy = blockIdx.x, l = threadIdx.x, W = f.mb_w;
     const size_t o = (size_t)cy * W;
+    const SliceMap m = smap(A);
     for (int i = l; i < W * kSaoMd; i += 64) md[i] = A.sao_md[o * kSaoMd + i];
     for (int i = l; i < W; i += 64) {
         own[i] = A.sao_own[o + i];
         cost[i] = A.sao_cost[o + i];
+        fl[i] = sao_row_flags(m, cy, i);
     }
     __syncthreads();
-    if (l == 0) {
+    if (l == 0) {   // the decision chain is sequential along the row
         const SliceTask t = f.tasks[cy / f.rows_per_slice];
-        sao_row_merge(md, own, cost, W, t.qp, smap(A), cy, A.sao + o);
+        sao_row_decide(md, own, cost, W, t.qp, fl, sel);
     }
+    __syncthreads();
+    for (int x = l; x < W; x += 64) sao_row_apply_sel(own, sel[x], A.sao + o + x);
 }
 
 __device__ __forceinline__ bool sao_any(const SaoParams& p) { return (p.type[0] | p.type[1] | p.type[2]) != 0; }
