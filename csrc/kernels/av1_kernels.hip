@@ -781,27 +781,27 @@ struct WaveTokenSink {
     uint32_t pend;
     int pend_n;
     uint32_t* bits;   // this wave's LDS bit buffer (256 words) for the sign / Golomb run
-    __device__ void push(uint32_t t) {
+    __device__ __forceinline__ void push(uint32_t t) {
         if (n < cap && lane() == 0) p[n] = t;
         n++;
     }
-    __device__ void flush() {
+    __device__ __forceinline__ void flush() {
         if (pend_n) push(tok_lit(pend, pend_n));
         pend = 0;
         pend_n = 0;
     }
-    __device__ void sym(int off, int n2, int v) {
+    __device__ __forceinline__ void sym(int off, int n2, int v) {
         flush();
         push(tok_sym(off, n2, v));
     }
-    __device__ void bit(int b) {
+    __device__ __forceinline__ void bit(int b) {
         pend = (pend << 1) | (uint32_t)(b & 1);
         if (++pend_n == 24) flush();
     }
-    __device__ void lits(uint32_t v, int nbits) {
+    __device__ __forceinline__ void lits(uint32_t v, int nbits) {
         for (int i = nbits - 1; i >= 0; i--) bit((v >> i) & 1);
     }
-    __device__ void gather(int off, bool bottom_out, int v) {
+    __device__ __forceinline__ void gather(int off, bool bottom_out, int v) {
         flush();
         push(tok_gather(off, bottom_out, v));
     }
@@ -1005,15 +1005,24 @@ __device__ __forceinline__ int code_coeffs_regs(WaveTokenSink& w, const CdfConte
     return sk_min(wsum(cul), 63) | (dcc << 6);
 }
 
-// code_coeffs is too large to inline at its nine call sites; the sink it updates per
-// token then lives behind a pointer in scratch memory. The call works on a register copy
-// and writes the sink back once.
-__device__ int code_coeffs(WaveTokenSink& wr, const CdfContext& cx, const int16_t* lev, int txs, int plane, CoefCtx cc,
-                           bool is_inter, int intra_dir, int qidx, int tx_type = TX_DCT_DCT) {
-    WaveTokenSink w = wr;
+// code_coeffs is too large to inline at its nine call sites, and a sink passed by
+// reference to a call lives in scratch memory (on both sides of the call). The call takes
+// the sink by value and returns it, so it stays in registers in the caller and the callee.
+struct SinkResult {
+    WaveTokenSink w;
+    int r;
+};
+__device__ __noinline__ SinkResult code_coeffs_call(WaveTokenSink w, const CdfContext& cx, const int16_t* lev, int txs,
+                                                    int plane, CoefCtx cc, bool is_inter, int intra_dir, int qidx,
+                                                    int tx_type) {
     const int r = code_coeffs_regs(w, cx, lev, txs, plane, cc, is_inter, intra_dir, qidx, tx_type);
-    wr = w;
-    return r;
+    return SinkResult{w, r};
+}
+__device__ __forceinline__ int code_coeffs(WaveTokenSink& w, const CdfContext& cx, const int16_t* lev, int txs, int plane,
+                                           CoefCtx cc, bool is_inter, int intra_dir, int qidx, int tx_type = TX_DCT_DCT) {
+    const SinkResult res = code_coeffs_call(w, cx, lev, txs, plane, cc, is_inter, intra_dir, qidx, tx_type);
+    w = res.w;
+    return res.r;
 }
 
 // Lane-parallel palette_tokens (codec/av1_core.h code_palette_tokens): every sample's
