@@ -1763,7 +1763,7 @@ __device__ __forceinline__ SaoPlane sao_plane_of(const HevcArgs& A, int c) {
     return SaoPlane{A.f.mb_w * n, A.f.mb_h * n, n, smap(A)};
 }
 
-__global__ __launch_bounds__(256) void k_hevc_sao_stats(HevcArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_hevc_sao_stats(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ SaoStats Sw[4][3];
     __shared__ SaoTables Tw[4];
