@@ -15,8 +15,9 @@
 //   64x64 superblocks; blocks are square 8/16/32/64 (PARTITION_NONE or SPLIT only);
 //   TX_MODE_LARGEST (one transform per block, reduced_tx_set: DCT_DCT or IDTX, the
 //   screen-content identity transform, chosen per luma block); intra DC / V / H /
-//   SMOOTH(_V/_H) / PAETH / directional, no filter-intra / CfL / palette / intraBC,
-//   intra edge filter off; one reference (LAST), single prediction, EIGHTTAP
+//   SMOOTH(_V/_H) / PAETH / directional, luma palettes of 2..8 colours on key frames
+//   (code_palette_mode_info / code_palette_tokens), no filter-intra / CfL / chroma
+//   palette / intraBC, intra edge filter off; one reference (LAST), single prediction, EIGHTTAP
 //   regular filter, quarter-pel vectors (allow_high_precision_mv = 0); no order
 //   hints (no temporal MVs, no skip mode); in-loop deblocking (av1_lf.h) and CDEF
 //   (av1_cdef.h) on, loop restoration off.

@@ -173,18 +173,46 @@ class CaptureSession {
     // an export that fails) the new encoder starts with a key frame instead.
     // Returns 0 moved with the stream continued, 1 moved with a key frame, -1 not
     // moved (CPU session, target GPU unusable, timeout; last error says why).
+    // The target encoder (allocations, hipGraph capture: the slow part) is built here, on
+    // the caller's thread, while the capture thread keeps encoding on the old GPU; between
+    // two frames the capture thread only exports, peer-copies and imports the state and
+    // swaps encoders. That stall is recorded (stats: move_stall_ms).
     int move_to(int device, int timeout_ms) {
         if (!running_) {
             set_last_error("capture not running");
             return -1;
         }
+        std::unique_ptr<EncoderBackend> nenc;
+        if (backend_ && device >= 0 && device < sk_hip_device_count()) {
+            try {
+                nenc.reset(s_.output_mode == 0 ? create_hip_jpeg_backend(jcfg_, device)
+                                               : create_hip_backend(ecfg_, device));
+            } catch (const std::exception& ex) {
+                set_last_error((std::string("encoder init on the target GPU failed: ") + ex.what()).c_str());
+                return -1;
+            }
+            if (!nenc) {
+                set_last_error("encoder init on the target GPU failed");
+                return -1;
+            }
+        }
         std::unique_lock<std::mutex> g(move_mu_);
         const uint64_t ticket = ++move_ticket_;
         move_dev_ = device;
+        move_enc_ = std::move(nenc);   // null: do_move reports why nothing can move
         move_pending_ = true;   // the loop stops queueing a second frame until it is served
         auto done = [&] { return move_done_ >= ticket || !running_; };
         if (!move_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 10000), done)) {
-            set_last_error("move timed out");
+            if (move_serving_ != ticket) {
+                // the capture thread has not reached it: withdraw the request, so no move
+                // happens after the caller has been told it failed
+                move_done_ = ticket;
+                move_pending_ = false;
+                set_last_error("move timed out before the capture thread reached it (cancelled)");
+            } else {
+                set_last_error("move timed out while in progress on the capture thread (it completes there; "
+                               "the device reports where the session ended up)");
+            }
             return -1;
         }
         if (move_done_ < ticket) {
@@ -240,12 +268,13 @@ class CaptureSession {
     static constexpr double kHistLe[kHist - 1] = {0.25, 0.5, 1, 2, 4, 8, 16, 33};
     void stats(double* out, int n) {
         std::lock_guard<std::mutex> g(mu_);
-        double v[8 + kHist] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
+        double v[9 + kHist] = {(double)frames_, frames_ ? enc_ms_sum_ / frames_ : 0.0, (double)bytes_,
                                (double)packets_, src_kind_, last_enc_ms_};
         for (int i = 0; i < kHist; i++) v[6 + i] = (double)hist_[i];
         v[6 + kHist] = (double)inflight_max_;   // frames in flight actually used (1 or 2)
         v[7 + kHist] = enc_ ? enc_->upload_fraction() : 1.0;   // rows uploaded / rows captured
-        for (int i = 0; i < n && i < 8 + kHist; i++) out[i] = v[i];
+        v[8 + kHist] = move_stall_ms_;   // last live move: capture thread time between two frames
+        for (int i = 0; i < n && i < 9 + kHist; i++) out[i] = v[i];
     }
     // Capture-to-packets latency (ms) of the most recent frames, oldest first;
     // returns the count copied. reset != 0 clears the record afterwards.
@@ -478,39 +507,36 @@ class CaptureSession {
 
     // Capture thread, no frame in flight: performs a pending move_to().
     void serve_move() {
+        std::unique_ptr<EncoderBackend> nenc;
         int dev;
         uint64_t ticket;
         {
             std::lock_guard<std::mutex> g(move_mu_);
-            if (move_done_ >= move_ticket_) return;
+            if (move_done_ >= move_ticket_) return;   // none pending, or withdrawn by a timed-out caller
             move_pending_ = false;
             dev = move_dev_;
             ticket = move_ticket_;
+            move_serving_ = ticket;
+            nenc = std::move(move_enc_);
         }
         std::string err;
-        const int rc = do_move(dev, &err);
+        const auto t0 = clk::now();
+        const int rc = do_move(dev, std::move(nenc), &err);
+        {
+            std::lock_guard<std::mutex> gs(mu_);
+            move_stall_ms_ = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        }
         std::lock_guard<std::mutex> g(move_mu_);
         move_rc_ = rc;
         move_err_ = err;
-        move_done_ = ticket;
+        move_done_ = std::max(move_done_, ticket);   // a withdrawn later ticket stays withdrawn
         move_cv_.notify_all();
     }
 
-    int do_move(int dev, std::string* err) {
+    int do_move(int dev, std::unique_ptr<EncoderBackend> nenc, std::string* err) {
         trace::Range r("capture.move");
-        if (!backend_ || dev < 0 || dev >= sk_hip_device_count()) {
+        if (!backend_ || dev < 0 || dev >= sk_hip_device_count() || !nenc) {
             *err = backend_ ? "no such GPU" : "CPU session: nothing to move";
-            return -1;
-        }
-        std::unique_ptr<EncoderBackend> nenc;
-        try {
-            nenc.reset(s_.output_mode == 0 ? create_hip_jpeg_backend(jcfg_, dev) : create_hip_backend(ecfg_, dev));
-        } catch (const std::exception& ex) {
-            *err = std::string("encoder init on the target GPU failed: ") + ex.what();
-            return -1;
-        }
-        if (!nenc) {
-            *err = "encoder init on the target GPU failed";
             return -1;
         }
         bool carried = false;
@@ -651,9 +677,11 @@ class CaptureSession {
     jpeg::JpegConfig jcfg_{};
     std::mutex move_mu_;
     std::condition_variable move_cv_;
-    uint64_t move_ticket_ = 0, move_done_ = 0;
+    uint64_t move_ticket_ = 0, move_done_ = 0, move_serving_ = 0;
     int move_dev_ = -1, move_rc_ = -1;
     std::string move_err_;
+    std::unique_ptr<EncoderBackend> move_enc_;   // target encoder built by move_to's caller
+    double move_stall_ms_ = 0.0;
     uint64_t hist_[kHist] = {};
     double src_kind_ = -1.0;  // 1 x11, 0 synthetic, -1 none (kept after stop for stats)
     std::mutex mu_;

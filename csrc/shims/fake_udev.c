@@ -12,6 +12,7 @@
  * Monitors never report hot-plug events; hwdb and queue calls are inert.
  */
 #define _GNU_SOURCE
+#include <errno.h>
 #include <fcntl.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -61,6 +62,9 @@ struct udev_enumerate {
     int nsub;
     char sysname[64];
     char prop_key[64], prop_val[64];
+    char devnode[64];    /* add_match_devicenode (glob) */
+    char sysnum[16];     /* add_match_sysnum: the trailing digits of the sysname */
+    int parent;          /* add_match_parent: node index, -1 none */
     struct udev_list_entry* list;
 };
 
@@ -370,6 +374,7 @@ EXPORT struct udev_enumerate* udev_enumerate_new(struct udev* u) {
     if (!e) return NULL;
     e->refs = 1;
     e->udev = udev_ref(u);
+    e->parent = -1;
     return e;
 }
 EXPORT struct udev_enumerate* udev_enumerate_ref(struct udev_enumerate* e) {
@@ -412,7 +417,21 @@ EXPORT int udev_enumerate_add_match_sysname(struct udev_enumerate* e, const char
     return 0;
 }
 EXPORT int udev_enumerate_add_match_tag(struct udev_enumerate* e, const char* t) { (void)e; (void)t; return 0; }
-EXPORT int udev_enumerate_add_match_parent(struct udev_enumerate* e, struct udev_device* p) { (void)e; (void)p; return 0; }
+EXPORT int udev_enumerate_add_match_parent(struct udev_enumerate* e, struct udev_device* p) {
+    if (!e) return -1;
+    e->parent = p ? node_by_syspath(NODE(p)->syspath) : -1;
+    return 0;
+}
+EXPORT int udev_enumerate_add_match_devicenode(struct udev_enumerate* e, const char* n) {
+    if (!e || !n) return -1;
+    snprintf(e->devnode, sizeof(e->devnode), "%s", n);
+    return 0;
+}
+EXPORT int udev_enumerate_add_match_sysnum(struct udev_enumerate* e, const char* n) {
+    if (!e || !n) return -1;
+    snprintf(e->sysnum, sizeof(e->sysnum), "%s", n);
+    return 0;
+}
 EXPORT int udev_enumerate_add_match_is_initialized(struct udev_enumerate* e) { (void)e; return 0; }
 EXPORT int udev_enumerate_add_syspath(struct udev_enumerate* e, const char* p) {
     return e && node_by_syspath(p) >= 0 && list_add(&e->list, p, NULL) ? 0 : -1;
@@ -424,22 +443,53 @@ static int glob_match(const char* pat, const char* s) {
     return *s && (*pat == '?' || *pat == *s) && glob_match(pat + 1, s + 1);
 }
 
+/* The digits at the end of a sysname ("js2" -> "2"; "" when there are none). */
+static const char* sysnum_of(const char* sysname) {
+    const char* p = sysname + strlen(sysname);
+    while (p > sysname && p[-1] >= '0' && p[-1] <= '9') p--;
+    return p;
+}
+/* Whether node i is `anc` or below it (libudev's match_parent includes the parent itself). */
+static int node_under(int i, int anc) {
+    for (int k = i; k >= 0; k = g_nodes[k].parent)
+        if (k == anc) return 1;
+    return 0;
+}
+static int enum_match(const struct udev_enumerate* e, int i) {
+    const node_t* n = &g_nodes[i];
+    if (e->nsub) {
+        int ok = 0;
+        for (int k = 0; k < e->nsub; k++) ok |= !strcmp(e->subsystems[k], n->subsystem);
+        if (!ok) return 0;
+    }
+    if (e->sysname[0] && !glob_match(e->sysname, n->sysname)) return 0;
+    if (e->devnode[0] && !(n->devnode[0] && glob_match(e->devnode, n->devnode))) return 0;
+    if (e->sysnum[0] && !glob_match(e->sysnum, sysnum_of(n->sysname))) return 0;
+    if (e->prop_key[0]) {
+        const char* v = kv_get(n->props, 24, e->prop_key);
+        if (!v || (e->prop_val[0] && !glob_match(e->prop_val, v))) return 0;
+    }
+    if (e->parent >= 0 && !node_under(i, e->parent)) return 0;
+    return 1;
+}
+/* scan_children: the devices below the add_match_parent device (that device included),
+   the other filters applied as in scan_devices. */
+EXPORT int udev_enumerate_scan_children(struct udev_enumerate* e) {
+    if (!e) return -1;
+    if (e->parent < 0) return -EINVAL;
+    list_free(e->list);
+    e->list = NULL;
+    for (int i = 0; i < NUM_PADS * NODES_PER_PAD; i++)
+        if (enum_match(e, i)) list_add(&e->list, g_nodes[i].syspath, NULL);
+    return 0;
+}
 EXPORT int udev_enumerate_scan_devices(struct udev_enumerate* e) {
     if (!e) return -1;
     list_free(e->list);
     e->list = NULL;
     for (int i = 0; i < NUM_PADS * NODES_PER_PAD; i++) {
+        if (!enum_match(e, i)) continue;
         node_t* n = &g_nodes[i];
-        if (e->nsub) {
-            int ok = 0;
-            for (int k = 0; k < e->nsub; k++) ok |= !strcmp(e->subsystems[k], n->subsystem);
-            if (!ok) continue;
-        }
-        if (e->sysname[0] && !glob_match(e->sysname, n->sysname)) continue;
-        if (e->prop_key[0]) {
-            const char* v = kv_get(n->props, 24, e->prop_key);
-            if (!v || (e->prop_val[0] && !glob_match(e->prop_val, v))) continue;
-        }
         list_add(&e->list, n->syspath, NULL);
     }
     return 0;

@@ -172,8 +172,8 @@ class ScreenCapture:
         return int(self._lib.sk_capture_device(self._h)) if self._h else -1
 
     def stats(self) -> dict:
-        arr = (ctypes.c_double * 17)()
-        self._lib.sk_capture_stats(self._h, arr, 17)
+        arr = (ctypes.c_double * 18)()
+        self._lib.sk_capture_stats(self._h, arr, 18)
         return {"frames": int(arr[0]), "encode_ms_mean": arr[1], "bytes": int(arr[2]),
                 "packets": int(arr[3]), "source": {1.0: "x11", 0.0: "synthetic"}.get(arr[4], "none"),
                 "encode_ms_last": arr[5],
@@ -181,7 +181,9 @@ class ScreenCapture:
                 "encode_ms_buckets": list(ENCODE_MS_BUCKETS), "encode_ms_counts": [int(x) for x in arr[6:15]],
                 "frames_in_flight": int(arr[15]),
                 # damage-driven upload: fraction of captured rows that crossed PCIe
-                "upload_fraction": arr[16]}
+                "upload_fraction": arr[16],
+                # last live move (move_to): ms the capture thread spent between two frames on it
+                "move_stall_ms": arr[17]}
 
     def close(self) -> None:
         self.stop_capture()

@@ -9,9 +9,10 @@ MI355X path: the GStreamer element chain (ximagesrc → convert → encoder →
 rtph264pay → webrtcbin) is replaced by the native capture session (X11 SHM →
 HIP convert/damage/H.264 in full-frame mode, csrc/runtime/capture.cpp) feeding
 :class:`~selkies_gstreamer_amd.webrtc.peer.PeerConnection`, whose per-frame
-RTP packetisation + SRTP is C++ (csrc/rtc). Bitrate requests (``vb``, REMB)
-drive :class:`~selkies_gstreamer_amd.server.ratecontrol.RateController`, which
-sets the encoder QP at runtime; PLI/FIR and new sessions force an IDR.
+RTP packetisation + SRTP is C++ (csrc/rtc). Bitrate requests (``vb``, REMB) set
+the encoder's CBR target at runtime (``ScreenCapture.set_rate``: the native K10
+controller, csrc/codec/ratecontrol.h, runs the VBV loop); PLI/FIR and new sessions
+force an IDR.
 
     python -m selkies_gstreamer_amd.legacy.webrtc_app --port 8080 --web_root selkies_gstreamer_amd/web
 """
@@ -29,7 +30,6 @@ from typing import Optional
 
 from selkies_gstreamer_amd.server import display as display_mod
 from selkies_gstreamer_amd.server import stats as stats_mod
-from selkies_gstreamer_amd.server.ratecontrol import RateController
 from selkies_gstreamer_amd.server.turn import parse_rtc_config, rtc_config, legacy_rtc_config
 from selkies_gstreamer_amd.webrtc.turn_client import parse_turn_url
 from selkies_gstreamer_amd.webrtc.peer import PeerConnection
@@ -207,7 +207,7 @@ class StreamSession:
         self.av1 = str(getattr(args, "encoder", "")) in AV1_ENCODERS
         self.send_sdp, self.send_ice = send_sdp, send_ice
         self.fps = int(args.framerate)
-        self.rc = RateController(int(args.video_bitrate) * 1000, self.fps)
+        self.target_bps = max(100_000, int(args.video_bitrate) * 1000)   # CBR target of the encoder
         stun_srv, turn_srv = ice_servers_from_rtc(build_rtc_config(args))
         self.pc = PeerConnection(addresses=addresses, video=media != "audio", audio=media != "video",
                                  data=media != "audio",
@@ -223,6 +223,7 @@ class StreamSession:
         self.input = None
         self.loop: Optional[asyncio.AbstractEventLoop] = None
         self.frames_sent = 0
+        self.bytes_sent = 0
         self.client_fps = 0
         self.client_latency = 0
         self.ping_sent: Optional[float] = None
@@ -283,9 +284,10 @@ class StreamSession:
         s = pixelflux.default_settings(w, h, target_fps=float(self.fps), h264_fullframe=1,
                                        output_mode=pixelflux.OUTPUT_MODE_HEVC if self.hevc else
                                        (pixelflux.OUTPUT_MODE_AV1 if self.av1 else pixelflux.OUTPUT_MODE_H264),
-                                       h264_crf=self.rc.qp, h264_paintover_crf=self.rc.paint_qp,
-                                       # K10 in the encoder: CBR with a 1.5-frame VBV (gstwebrtc_app.py:101-105)
-                                       h264_rc_mode=2, h264_bitrate_kbps=max(1, self.rc.target_bps // 1000),
+                                       # K10 in the encoder: CBR with a 1.5-frame VBV (gstwebrtc_app.py:101-105),
+                                       # starting from the reference's default CRF / paint-over CRF
+                                       h264_crf=25, h264_paintover_crf=18,
+                                       h264_rc_mode=2, h264_bitrate_kbps=max(1, self.target_bps // 1000),
                                        use_cpu=1 if _truthy(self.args.use_cpu) else 0, source=src,
                                        # x264enc speed-preset=ultrafast (gstwebrtc_app.py:637) on
                                        # the CPU: diamond search, integer-pel vectors
@@ -317,12 +319,12 @@ class StreamSession:
         ts = int((time.monotonic() - self._t0) * 90000)
         self.pc.send_video(data[10:], ts)
         self.frames_sent += 1
-        self.rc.on_frame(len(data) - 10, key)   # delivered-rate statistics; the encoder runs the CBR loop
+        self.bytes_sent += len(data) - 10
 
     def _apply_rate(self) -> None:
         """Current target (vb, / REMB) -> the encoder's CBR budget from its next frame."""
         if self.capture is not None:
-            self.capture.set_rate("cbr", max(1, self.rc.target_bps // 1000))
+            self.capture.set_rate("cbr", max(1, self.target_bps // 1000))
 
     async def _start_audio(self) -> None:
         from selkies_gstreamer_amd.server.audio import AudioPipeline
@@ -353,7 +355,7 @@ class StreamSession:
 
     def _on_remb(self, bps: int) -> None:
         if _truthy(self.args.congestion_control):
-            self.rc.set_target(min(bps, int(self.args.video_bitrate) * 1000))
+            self.target_bps = max(100_000, min(bps, int(self.args.video_bitrate) * 1000))
             self._apply_rate()
 
     # -- data channel ------------------------------------------------------------------------------
@@ -378,7 +380,7 @@ class StreamSession:
             if t == "vb":
                 kbps = int(toks[1])
                 self.args.video_bitrate = str(kbps)
-                self.rc.set_target(kbps * 1000)
+                self.target_bps = max(100_000, kbps * 1000)
                 self._apply_rate()
                 self.send_message("pipeline", {"status": f"Video bitrate set to: {kbps}"})
                 save_overlay(self.args.json_config, self.args)
@@ -391,7 +393,6 @@ class StreamSession:
             elif t == "_arg_fps":
                 self.fps = int(toks[1])
                 self.args.framerate = str(self.fps)
-                self.rc.set_fps(self.fps)
                 save_overlay(self.args.json_config, self.args)
                 self.send_message("system", {"action": f"framerate,{self.fps}"})
             elif t == "r":

@@ -15,6 +15,7 @@ import argparse
 import asyncio
 import logging
 import os
+import secrets
 import signal
 import sys
 import time
@@ -47,9 +48,11 @@ class SessionSpec:
         return [python, "-m", "selkies_gstreamer_amd", "--port", str(self.port), "--gpu-id", str(self.gpu),
                 *self.extra]
 
-    def env(self, base: Optional[dict] = None) -> dict:
+    def env(self, base: Optional[dict] = None, control_token: Optional[str] = None) -> dict:
         e = dict(os.environ if base is None else base)
         e["DISPLAY"] = self.display
+        if control_token:   # the node control API (/api/*) of the server answers this token only
+            e["SELKIES_CONTROL_TOKEN"] = control_token
         e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if self.hw_queues:
             e.setdefault("GPU_MAX_HW_QUEUES", str(self.hw_queues))
@@ -111,9 +114,12 @@ class Supervisor:
         self.health_interval, self.max_backoff = health_interval, max_backoff
         self.check_health = check_health
         self.stopping = False
+        # shared secret of the node's control API: every server gets it in its environment,
+        # the Rebalancer sends it; nothing reaching a server through a proxy knows it
+        self.control_token = secrets.token_hex(16)
 
     async def _spawn(self, spec: SessionSpec):
-        p = await asyncio.create_subprocess_exec(*spec.command(), env=spec.env())
+        p = await asyncio.create_subprocess_exec(*spec.command(), env=spec.env(control_token=self.control_token))
         self.procs[spec.name] = p
         log.info("session %s: pid %d, display %s, port %d, gpu %d", spec.name, p.pid, spec.display, spec.port,
                  spec.gpu)
@@ -166,6 +172,8 @@ class Supervisor:
             return
         log.warning("session %s: relocating from GPU %d to GPU %d", name, spec.gpu, gpu)
         spec.gpu = gpu
+        per_gpu = sum(1 for s in self.specs if s.gpu == gpu)   # processes on the new GPU, this one included
+        spec.hw_queues = hw_queues_for(per_gpu)
         p = self.procs.get(name)
         if p is not None and p.returncode is None:
             p.terminate()   # _watch respawns it with the new spec
@@ -178,7 +186,8 @@ class Supervisor:
             from .rebalance import Rebalancer
             self.rebalancer = Rebalancer({s.name: s.all_ports() for s in self.specs},
                                          gpus if gpus is not None else sorted({s.gpu for s in self.specs}),
-                                         capacity=capacity, on_failed_move=self.relocate)
+                                         capacity=capacity, on_failed_move=self.relocate,
+                                         token=self.control_token)
             self._rb_stop = asyncio.Event()
             tasks.append(self.rebalancer.run(rebalance, self._rb_stop))
         await asyncio.gather(*tasks)

@@ -131,27 +131,44 @@ def plan_moves(loads: list[DisplayLoad], gpus: Iterable[int], capacity: float = 
 Fetch = Callable[[int], Awaitable[Optional[dict]]]
 Move = Callable[[int, str, int], Awaitable[Optional[str]]]
 
+# Header carrying the node's control token (launcher -> every session server through
+# SELKIES_CONTROL_TOKEN; server/data_server.py refuses /api/* without it).
+CONTROL_HEADER = "X-Selkies-Control-Token"
 
-async def http_fetch(port: int) -> Optional[dict]:
+
+def _control_headers(token: Optional[str]) -> dict:
+    return {CONTROL_HEADER: token} if token else {}
+
+
+async def http_fetch(port: int, token: Optional[str] = None) -> Optional[dict]:
     import aiohttp
     try:
         async with aiohttp.ClientSession() as s:
-            async with s.get(f"http://127.0.0.1:{port}/api/placement", timeout=aiohttp.ClientTimeout(total=3)) as r:
-                return await r.json() if r.status == 200 else None
-    except Exception:
+            async with s.get(f"http://127.0.0.1:{port}/api/placement", headers=_control_headers(token),
+                             timeout=aiohttp.ClientTimeout(total=3)) as r:
+                if r.status != 200:
+                    log.warning("placement poll of port %d: HTTP %d", port, r.status)
+                    return None
+                return await r.json()
+    except Exception as e:
+        log.debug("placement poll of port %d failed: %r", port, e)
         return None
 
 
-async def http_move(port: int, display: str, gpu: int) -> Optional[str]:
+async def http_move(port: int, display: str, gpu: int, token: Optional[str] = None) -> Optional[str]:
     """'continued' / 'keyframe' on success, None when the server could not move."""
     import aiohttp
     try:
         async with aiohttp.ClientSession() as s:
             async with s.post(f"http://127.0.0.1:{port}/api/move", params={"display": display, "gpu": str(gpu)},
-                              timeout=aiohttp.ClientTimeout(total=15)) as r:
-                doc = await r.json()
-                return doc.get("result") if r.status == 200 else None
-    except Exception:
+                              headers=_control_headers(token), timeout=aiohttp.ClientTimeout(total=15)) as r:
+                if r.status != 200:
+                    log.warning("move of display %s on port %d: HTTP %d %s", display, port, r.status,
+                                (await r.text())[:200])
+                    return None
+                return (await r.json()).get("result")
+    except Exception as e:
+        log.warning("move of display %s on port %d failed: %r", display, port, e)
         return None
 
 
@@ -160,16 +177,19 @@ class Rebalancer:
 
     ``sessions``: {session name: [ports]}; ``on_failed_move(session, gpu)`` is called
     when a display of a stalled GPU could not be moved (the GPU does not answer): the
-    launcher then restarts that session on ``gpu``. A failed overload move is only
-    logged (the display keeps running where it is)."""
+    launcher then restarts that session on ``gpu``, once per session and poll. A failed
+    overload move is only logged (the display keeps running where it is). ``token``: the
+    node's control token, sent with every request of the default HTTP fetch / move."""
 
     def __init__(self, sessions: dict, gpus: Iterable[int], capacity: float = 48.0, overload: float = 0.75,
-                 cooldown_s: float = 30.0, fetch: Fetch = http_fetch, move: Move = http_move,
-                 on_failed_move: Optional[Callable[[str, int], Awaitable[None]]] = None, clock=time.monotonic):
+                 cooldown_s: float = 30.0, fetch: Optional[Fetch] = None, move: Optional[Move] = None,
+                 on_failed_move: Optional[Callable[[str, int], Awaitable[None]]] = None, clock=time.monotonic,
+                 token: Optional[str] = None):
         self.sessions = sessions
         self.gpus = list(gpus)
         self.capacity, self.overload, self.cooldown_s = capacity, overload, cooldown_s
-        self.fetch, self.move = fetch, move
+        self.fetch = fetch or (lambda port: http_fetch(port, token))
+        self.move = move or (lambda port, display, gpu: http_move(port, display, gpu, token))
         self.on_failed_move = on_failed_move
         self.clock = clock
         self._frames: dict = {}       # display key -> frames at the previous poll
@@ -186,7 +206,9 @@ class Rebalancer:
         return out
 
     def stalled_gpus(self, loads: list[DisplayLoad]) -> set:
-        """GPUs whose every display made no frame since the previous poll."""
+        """GPUs whose every display made no frame since the previous poll. A count
+        that went down is a new capture of that display (a resize, a restart or a
+        relocation recreates it from 0): a fresh baseline and a live GPU, not a stall."""
         alive, seen = set(), set()
         for d in loads:
             prev = self._frames.get(d.key)
@@ -194,7 +216,7 @@ class Rebalancer:
             if prev is None or d.gpu not in self.gpus:
                 continue
             seen.add(d.gpu)
-            if d.frames > prev:
+            if d.frames != prev:
                 alive.add(d.gpu)
         return seen - alive
 
@@ -206,14 +228,20 @@ class Rebalancer:
         if failed:
             log.error("GPU(s) %s stalled: evacuating their displays", sorted(failed))
         done = []
+        relocate: dict = {}   # session -> target GPU of its first display that could not move
         for d, gpu in plan_moves(loads, self.gpus, self.capacity, failed, self.overload, cooling=cooling):
             res = await self.move(d.port, d.display, gpu)
             self._moved_at[d.key] = now
             self.history.append((d.key, d.gpu, gpu, res))
             log.info("display %s of %s: GPU %d -> %d: %s", d.display, d.session, d.gpu, gpu, res or "failed")
-            if res is None and d.gpu in failed and self.on_failed_move is not None:
-                await self.on_failed_move(d.session, gpu)
+            if res is None and d.gpu in failed:
+                relocate.setdefault(d.session, gpu)
             done.append((d, gpu, res))
+        # one restart per session and poll: a multi-display session host whose displays
+        # were planned onto different GPUs restarts once, on the first target
+        if self.on_failed_move is not None:
+            for session, gpu in relocate.items():
+                await self.on_failed_move(session, gpu)
         return done
 
     async def run(self, interval: float = 5.0, stop: Optional[asyncio.Event] = None) -> None:

@@ -221,8 +221,15 @@ class DataStreamingServer:
                  capture_factory: Optional[Callable[[], Any]] = None, display_manager=None,
                  capture_source: str = "auto", gpu_id: int = 0, num_gpus: int = 1, clock=time.monotonic,
                  web_root: Optional[str] = None, metrics=None, frame_trace: Optional[bool] = None,
-                 x_display: Optional[str] = None, basic_auth: Optional[tuple] = None):
+                 x_display: Optional[str] = None, basic_auth: Optional[tuple] = None,
+                 control_token: Optional[str] = None):
         self.settings = settings
+        # node control API (/api/placement, /api/move; parallel/rebalance.py): answered only
+        # to direct loopback callers that present the launcher's token. Without a token the
+        # API is off: behind a reverse proxy every client arrives from 127.0.0.1, so the
+        # peer address alone proves nothing (deploy/nginx.conf also denies /api/).
+        self.control_token = (control_token if control_token is not None
+                              else os.environ.get("SELKIES_CONTROL_TOKEN")) or None
         # (user, password) guarding every route, the websocket upgrade included: the
         # reference puts its whole nginx server block, /ws too, behind basic auth
         # (addons/example/selkies-gstreamer-entrypoint.sh:89) and its signalling server
@@ -244,6 +251,7 @@ class DataStreamingServer:
         self.layouts: dict = {}
         self.captures: dict[str, Capture] = {}
         self._resync: set[str] = set()     # displays whose queue overflowed: wait for a keyframe
+        self._key_requested: dict = {}     # display -> time of the last REQUEST_KEYFRAME served
         self.meter = BandwidthMeter(clock)
         self.recent: "OrderedDict[str, float]" = OrderedDict()
         self.reconfigure_lock = asyncio.Lock()
@@ -284,10 +292,13 @@ class DataStreamingServer:
 
     # ================================================================ app / routes
     AUTH_EXEMPT = ("/health",)
+    KEY_REQUEST_MIN_S = 0.2
 
     @web.middleware
     async def _auth_middleware(self, request: web.Request, handler):
+        # /api/* carries its own (stronger) token check instead of the viewers' password
         if (self.basic_auth is not None and request.path not in self.AUTH_EXEMPT
+                and not request.path.startswith("/api/")
                 and not _basic_auth_ok(request, *self.basic_auth)):
             raise web.HTTPUnauthorized(headers={"WWW-Authenticate": 'Basic realm="selkies"'})
         return await handler(request)
@@ -334,10 +345,19 @@ class DataStreamingServer:
     async def _health(self, request):
         return web.Response(text="OK\n")
 
-    # ---- node control (parallel/rebalance.py): loopback callers only, on top of auth
-    @staticmethod
-    def _loopback(request: web.Request) -> bool:
-        return (request.remote or "") in ("127.0.0.1", "::1", "::ffff:127.0.0.1")
+    # ---- node control (parallel/rebalance.py): direct loopback callers with the token
+    CONTROL_HEADER = "X-Selkies-Control-Token"
+    PROXY_HEADERS = ("X-Forwarded-For", "X-Real-IP", "Forwarded")
+
+    def _control_ok(self, request: web.Request) -> bool:
+        if not self.control_token:
+            return False
+        if (request.remote or "") not in ("127.0.0.1", "::1", "::ffff:127.0.0.1"):
+            return False
+        if any(h in request.headers for h in self.PROXY_HEADERS):   # relayed by a proxy
+            return False
+        return hmac.compare_digest(request.headers.get(self.CONTROL_HEADER, "").encode(),
+                                   self.control_token.encode())
 
     def placement(self) -> dict:
         """Per display: the GPU its encoder runs on and its encode load (mean and last
@@ -353,12 +373,12 @@ class DataStreamingServer:
             dev = getattr(mod, "device", None)
             out[did] = {"gpu": dev if isinstance(dev, int) and dev >= 0 else self._gpu_of.get(did),
                         "encode_ms_mean": st.get("encode_ms_mean"), "encode_ms_last": st.get("encode_ms_last"),
-                        "frames": st.get("frames"), "fps": cap.fps,
+                        "frames": st.get("frames"), "fps": cap.fps, "move_stall_ms": st.get("move_stall_ms"),
                         "width": cap.size[0], "height": cap.size[1]}
         return out
 
     async def _api_placement(self, request):
-        if not self._loopback(request):
+        if not self._control_ok(request):
             raise web.HTTPForbidden()
         return web.json_response({"gpu_id": self.gpu_id, "displays": self.placement()})
 
@@ -378,7 +398,7 @@ class DataStreamingServer:
         return res
 
     async def _api_move(self, request):
-        if not self._loopback(request):
+        if not self._control_ok(request):
             raise web.HTTPForbidden()
         did = request.query.get("display", "primary")
         try:
@@ -562,6 +582,17 @@ class DataStreamingServer:
                     self.displays[did].flow.on_ack(protocol.parse_frame_ack(m), self.clock())
                 except ValueError:
                     log.warning("malformed ACK: %s", m)
+        elif m == "REQUEST_KEYFRAME":
+            # a viewer's decoder lost its reference (web/lib/video.js drops deltas when it
+            # falls behind): the display's next frame is a key frame; one request per
+            # KEY_REQUEST_MIN_S per display, however many viewers ask
+            did = client.display_id
+            cap = self.captures.get(did) if did else None
+            now = self.clock()
+            if cap is not None and hasattr(cap.module, "request_keyframe") and \
+                    now - self._key_requested.get(did, -1e9) >= self.KEY_REQUEST_MIN_S:
+                self._key_requested[did] = now
+                cap.module.request_keyframe()
         elif m == "START_VIDEO":
             await self._start_video(client)
         elif m == "STOP_VIDEO":

@@ -33,9 +33,17 @@ export function codecString(encoder, w, h, fps = 60) {
   return 'avc1.42E01E';
 }
 
+// Least time between two key-frame requests of one stripe (REQUEST_KEYFRAME).
+export const KEY_REQUEST_INTERVAL_MS = 250;
+
 export class VideoRenderer {
-  constructor(canvas, onError) {
+  // onKeyframeNeeded(y): the stripe at y cannot decode deltas any more (a chunk was dropped,
+  // or its decoder was recreated) and needs a key frame; the client sends REQUEST_KEYFRAME.
+  constructor(canvas, onError, onKeyframeNeeded) {
     this.canvas = canvas;
+    this.onKeyframeNeeded = onKeyframeNeeded || (() => {});
+    this.keyRequestedAt = new Map();   // y -> time of the last request
+    this.dropped = 0;                  // delta chunks dropped because the decoder fell behind
     this.encoder = 'x264enc';   // set from the negotiated settings (codecString)
     this.fps = 60;
     this.ctx = canvas.getContext('2d', { alpha: false, desynchronized: true });
@@ -91,14 +99,35 @@ export class VideoRenderer {
     }
   }
 
+  _requestKey(y) {
+    const now = performance.now();
+    const last = this.keyRequestedAt.get(y);
+    if (last !== undefined && now - last < KEY_REQUEST_INTERVAL_MS) return;
+    this.keyRequestedAt.set(y, now);
+    this.onKeyframeNeeded(y);
+  }
+
   h264(pkt) {
     this.frameIds.add(pkt.frameId);
     this.lastFrameId = pkt.frameId;
     if (typeof VideoDecoder === 'undefined') return;
     const info = this._decoderFor(pkt.y, pkt.width, pkt.height);
-    if (!pkt.key && !info.keyed) return;   // wait for this stripe's IDR
-    if (pkt.key) info.keyed = true;
-    if (info.decoder.decodeQueueSize > 30) return;  // decoder falling behind: drop deltas until next key
+    if (!pkt.key && !info.keyed) {   // no reference for this delta: wait for the stripe's key frame
+      this._requestKey(pkt.y);        // (the default GOP is infinite: ask for one)
+      return;
+    }
+    if (pkt.key) {
+      info.keyed = true;
+      this.keyRequestedAt.delete(pkt.y);
+    }
+    if (!pkt.key && info.decoder.decodeQueueSize > 30) {
+      // the decoder fell behind: drop this delta, and with it every delta up to the next
+      // key frame (they predict from the dropped one), which is requested now
+      info.keyed = false;
+      this.dropped++;
+      this._requestKey(pkt.y);
+      return;
+    }
     info.decoder.decode(new EncodedVideoChunk({
       type: pkt.key ? 'key' : 'delta', timestamp: performance.now() * 1000, data: pkt.payload,
     }));

@@ -23,7 +23,7 @@ const $ = (id) => document.getElementById(id);
 class Client {
   constructor() {
     this.canvas = $('stream');
-    this.video = new VideoRenderer(this.canvas, (e) => this.onDecoderError(e));
+    this.video = new VideoRenderer(this.canvas, (e) => this.onDecoderError(e), () => this.sendText('REQUEST_KEYFRAME'));
     this.audio = new AudioPipeline();
     this.input = new Input(this.canvas, (m) => this.sendText(m), () => [this.canvas.width, this.canvas.height]);
     this.input.onMenuHotkey = () => $('sidebar').classList.toggle('open');          // Ctrl+Shift+M

@@ -479,3 +479,38 @@ import('../../selkies_gstreamer_amd/web/lib/video.js').then(({ codecString }) =>
   assert.equal(codecString('svtav1enc', 1920, 1080, 60), 'av01.0.09M.08');    // level 4.1 (4.0 tops out at 30 fps)
   console.log('codec strings ok');
 }).catch((e) => { console.error(e); process.exit(1); });
+
+// ---- decode-queue drop: no delta after a drop is decoded before the next key frame, and a
+// key frame is requested (lib/video.js VideoRenderer.h264)
+import('../../selkies_gstreamer_amd/web/lib/video.js').then(({ VideoRenderer, KEY_REQUEST_INTERVAL_MS }) => {
+  if (typeof globalThis.performance === 'undefined') globalThis.performance = { now: () => Date.now() };
+  const decoded = [];
+  let queue = 0;
+  globalThis.EncodedVideoChunk = class { constructor(o) { Object.assign(this, o); } };
+  globalThis.VideoDecoder = class {
+    constructor() { this.state = 'configured'; }
+    configure() {}
+    get decodeQueueSize() { return queue; }
+    decode(c) { decoded.push(c.data[0]); }
+    close() { this.state = 'closed'; }
+  };
+  const canvas = { width: 0, height: 0, getContext: () => ({ fillRect() {}, drawImage() {} }) };
+  const requests = [];
+  const v = new VideoRenderer(canvas, null, (y) => requests.push(y));
+  const pkt = (n, key) => ({ frameId: n, y: 0, width: 1920, height: 1080, key, payload: new Uint8Array([n]) });
+  v.h264(pkt(0, true));
+  // 40 queued deltas: the decoder falls behind at delta 10 and recovers at delta 20
+  for (let n = 1; n <= 40; n++) {
+    queue = n >= 10 && n < 20 ? 31 : 0;
+    v.h264(pkt(n, false));
+  }
+  assert.deepEqual(decoded, [0, ...Array.from({ length: 9 }, (_, i) => i + 1)]);   // nothing after the drop
+  assert.ok(requests.length >= 1 && requests.every((y) => y === 0));
+  assert.ok(requests.length <= 2);   // rate limited (KEY_REQUEST_INTERVAL_MS)
+  assert.ok(KEY_REQUEST_INTERVAL_MS > 0 && v.dropped === 1);   // the rest wait unkeyed
+  v.h264(pkt(41, true));             // the requested key frame resumes decoding
+  v.h264(pkt(42, false));
+  assert.deepEqual(decoded.slice(-2), [41, 42]);
+  console.log('decode-drop resync ok');
+}).catch((e) => { console.error(e); process.exit(1); });
+

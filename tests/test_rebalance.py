@@ -99,14 +99,105 @@ def test_rebalancer_detects_a_stalled_gpu_and_relocates_what_cannot_move():
     asyncio.run(main())
 
 
-def test_server_control_endpoints(tmp_path):
+def test_stall_check_treats_a_frame_count_reset_as_alive():
+    """A display whose capture was recreated (resize, restart) counts from 0 again: the
+    lower count is a new baseline, its GPU is alive and nothing is evacuated."""
+    state = {"frames": 500}
+    moves = []
+
+    async def fetch(port):
+        return {"displays": {"primary": {"gpu": 0, "encode_ms_mean": 3.0, "frames": state["frames"],
+                                         "fps": 60.0, "width": 1920, "height": 1080}}}
+
+    async def move(port, display, gpu):
+        moves.append(gpu)
+        return "continued"
+    rb = Rebalancer({"a": [8000]}, [0, 1], capacity=8, fetch=fetch, move=move)
+
+    async def main():
+        await rb.step()
+        state["frames"] = 3            # capture recreated: counts restart
+        assert rb.stalled_gpus(await rb.snapshot()) == set()
+        state["frames"] = 9            # and it advances from the new baseline
+        assert await rb.step() == []
+        assert rb.stalled_gpus(await rb.snapshot()) == {0}   # a real stall still shows
+    asyncio.run(main())
+    assert moves == []
+
+
+def test_failed_moves_relocate_a_session_once_per_poll():
+    """Two displays of one session host on a stalled GPU, planned onto different GPUs and
+    both unmovable: the session is restarted once, on the first target."""
+    state = {"frames": 10}
+    relocated = []
+
+    async def fetch(port):
+        d = {"gpu": 0, "encode_ms_mean": 3.0, "frames": state["frames"], "fps": 60.0, "width": 1920, "height": 1080}
+        return {"displays": {"primary": dict(d), "display2": dict(d)}}
+
+    async def move(port, display, gpu):
+        return None
+
+    async def relocate(name, gpu):
+        relocated.append((name, gpu))
+    rb = Rebalancer({"h": [8000]}, [0, 1, 2], capacity=8, fetch=fetch, move=move, on_failed_move=relocate)
+
+    async def main():
+        await rb.step()
+        done = await rb.step()           # no frames since: GPU 0 stalled
+        assert len(done) == 2 and len({t for _, t, _ in done}) == 2
+    asyncio.run(main())
+    assert len(relocated) == 1 and relocated[0][0] == "h"
+
+
+def test_control_api_requires_the_token_and_a_direct_caller(tmp_path):
+    """The control API answers the launcher's token only: no token configured = off,
+    a wrong or missing token or a proxied request (X-Forwarded-For) = 403. With basic
+    auth on, the Rebalancer's token requests still get through (no viewer password)."""
+    from selkies_gstreamer_amd.parallel.rebalance import http_fetch
+    from selkies_gstreamer_amd.server.data_server import DataStreamingServer
+    from selkies_gstreamer_amd.server.settings import Settings
+
+    async def main():
+        for token, auth in ((None, None), ("t0k", ("u", "pw"))):
+            srv = DataStreamingServer(Settings(["--port", "0", "--use-cpu", "true", "--audio-enabled", "false"], env={}),
+                                      capture_source="synthetic", control_token=token or "",
+                                      basic_auth=auth)
+            port = await srv.start("127.0.0.1", 0)
+            try:
+                async with aiohttp.ClientSession() as sess:
+                    hdr = {"X-Selkies-Control-Token": token or "x"}
+                    async with sess.get(f"http://127.0.0.1:{port}/api/placement", headers=hdr) as r:
+                        assert r.status == (200 if token else 403)
+                    if token:
+                        async with sess.get(f"http://127.0.0.1:{port}/api/placement",
+                                            headers={"X-Selkies-Control-Token": "nope"}) as r:
+                            assert r.status == 403
+                        async with sess.get(f"http://127.0.0.1:{port}/api/placement",
+                                            headers={**hdr, "X-Forwarded-For": "10.0.0.9"}) as r:
+                            assert r.status == 403
+                        async with sess.post(f"http://127.0.0.1:{port}/api/move", params={"gpu": "1"}) as r:
+                            assert r.status == 403
+                        # the viewers' routes keep basic auth
+                        async with sess.get(f"http://127.0.0.1:{port}/") as r:
+                            assert r.status == 401
+                        assert (await http_fetch(port, token))["displays"] == {}
+                        assert await http_fetch(port, None) is None
+            finally:
+                await srv.stop()
+    asyncio.run(asyncio.wait_for(main(), 60))
+
+
+def test_server_control_endpoints(tmp_path, monkeypatch):
     """/api/placement lists the running display; /api/move hands the move to the capture
     module (a CPU session cannot move: 409) and pins later restarts to the new GPU."""
     from tests.test_server_e2e import _server, _settings, _recv_until
+    monkeypatch.setenv("SELKIES_CONTROL_TOKEN", "tok")
+    H = {"X-Selkies-Control-Token": "tok"}
 
     async def main():
         srv, port, _ = await _server(tmp_path)
-        async with aiohttp.ClientSession() as sess:
+        async with aiohttp.ClientSession(headers=H) as sess:
             async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket") as ws:
                 await ws.send_str(_settings())
                 await _recv_until(ws, lambda m: isinstance(m, bytes))
@@ -156,10 +247,13 @@ def test_launcher_relocate_restarts_on_the_new_gpu():
         def terminate(self):
             self.terminated = True
     spec = SessionSpec("s0", ":20", 8082, 0)
-    sup = Supervisor([spec], check_health=False)
+    others = [SessionSpec(f"o{i}", f":{30 + i}", 9000 + i, 5) for i in range(5)]
+    sup = Supervisor([spec, *others], check_health=False)
     sup.procs["s0"] = p = Proc()
     asyncio.run(sup.relocate("s0", 5))
     assert spec.gpu == 5 and p.terminated
+    assert spec.hw_queues == 2            # six processes on GPU 5 now: queues resized
+    assert spec.env(control_token=sup.control_token)["SELKIES_CONTROL_TOKEN"] == sup.control_token
     assert "--gpu-id" in spec.command() and spec.command()[spec.command().index("--gpu-id") + 1] == "5"
 
 

@@ -101,6 +101,33 @@ def test_session_h264_striped(tmp_path):
     run(main())
 
 
+def test_keyframe_request_resyncs_a_viewer(tmp_path):
+    """REQUEST_KEYFRAME (sent by web/lib/video.js when its decoder dropped a delta) makes
+    the display's next frames start with a 0x04 key frame within two frames."""
+    async def main():
+        srv, port, _ = await _server(tmp_path)
+        async with aiohttp.ClientSession() as sess:
+            async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket") as ws:
+                await ws.send_str(_settings(encoder="x264enc"))
+                frames = []
+                while len(frames) < 6:
+                    data = (await asyncio.wait_for(ws.receive(), 10)).data
+                    if isinstance(data, bytes) and data[0] == 0x04:
+                        frames.append(data[1])
+                assert frames[0] == 1 and not any(frames[1:])   # one IDR, then P frames
+                await ws.send_str("REQUEST_KEYFRAME")
+                await ws.send_str("REQUEST_KEYFRAME")             # a second viewer / repeat: one IDR
+                after = []
+                while len(after) < 8:
+                    data = (await asyncio.wait_for(ws.receive(), 10)).data
+                    if isinstance(data, bytes) and data[0] == 0x04:
+                        after.append(data[1])
+                assert 1 in after[:2], after
+                assert sum(after) == 1, after
+        await srv.stop()
+    run(main())
+
+
 def test_session_jpeg_and_fullframe(tmp_path):
     async def main():
         srv, port, _ = await _server(tmp_path)

@@ -173,3 +173,97 @@ def test_fake_udev_enumeration(shims):
     syms = subprocess.run(["objdump", "-T", str(udev_path)], capture_output=True, text=True).stdout
     for ver in ("LIBUDEV_183", "LIBUDEV_189", "LIBUDEV_196", "LIBUDEV_199", "LIBUDEV_215", "LIBUDEV_247"):
         assert ver in syms
+
+
+REF_UDEV_SYM = "/root/reference/addons/fake-udev/libudev.sym"
+
+
+def test_fake_udev_exports_every_reference_symbol(shims):
+    _, udev_path = shims
+    """Every symbol of the reference's version script (libudev.sym) is exported, with its
+    version node; a game linked against any of them resolves under the preload."""
+    import re
+    if not os.path.exists(REF_UDEV_SYM):
+        pytest.skip("reference tree not mounted")
+    want = {}
+    node = None
+    for line in open(REF_UDEV_SYM):
+        m = re.match(r"\s*(LIBUDEV_\d+)\s*\{", line)
+        if m:
+            node = m.group(1)
+            continue
+        m = re.match(r"\s*(udev_\w+)\s*;", line)
+        if m and node:
+            want[m.group(1)] = node
+    assert len(want) >= 90
+    out = subprocess.run(["objdump", "-T", str(udev_path)], capture_output=True, text=True).stdout
+    have = {}
+    for line in out.splitlines():
+        f = line.split()
+        if len(f) >= 2 and f[-1].startswith("udev_"):
+            have[f[-1]] = f[-2]
+    missing = sorted(set(want) - set(have))
+    assert not missing, missing
+    wrong = {k: (have[k], v) for k, v in want.items() if have[k].strip("()") != v}
+    assert not wrong, wrong
+
+
+def test_fake_udev_children_devicenode_sysnum(shims):
+    _, udev_path = shims
+    """udev_enumerate_scan_children lists the parent and what is below it;
+    add_match_devicenode / add_match_sysnum filter like libudev (glob patterns)."""
+    L = ctypes.CDLL(str(udev_path))
+    L.udev_new.restype = ctypes.c_void_p
+    L.udev_enumerate_new.restype = ctypes.c_void_p
+    L.udev_enumerate_new.argtypes = [ctypes.c_void_p]
+    L.udev_enumerate_get_list_entry.restype = ctypes.c_void_p
+    L.udev_enumerate_get_list_entry.argtypes = [ctypes.c_void_p]
+    L.udev_list_entry_get_next.restype = ctypes.c_void_p
+    L.udev_list_entry_get_next.argtypes = [ctypes.c_void_p]
+    L.udev_list_entry_get_name.restype = ctypes.c_char_p
+    L.udev_list_entry_get_name.argtypes = [ctypes.c_void_p]
+    for f in ("udev_enumerate_add_match_devicenode", "udev_enumerate_add_match_sysnum",
+              "udev_enumerate_add_match_subsystem"):
+        getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    L.udev_enumerate_add_match_parent.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    for f in ("udev_enumerate_scan_devices", "udev_enumerate_scan_children", "udev_enumerate_unref"):
+        getattr(L, f).argtypes = [ctypes.c_void_p]
+    L.udev_device_new_from_syspath.restype = ctypes.c_void_p
+    L.udev_device_new_from_syspath.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    L.udev_device_get_parent_with_subsystem_devtype.restype = ctypes.c_void_p
+    L.udev_device_get_parent_with_subsystem_devtype.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
+    L.udev_device_get_syspath.restype = ctypes.c_char_p
+    L.udev_device_get_syspath.argtypes = [ctypes.c_void_p]
+
+    def names(e):
+        out, it = [], L.udev_enumerate_get_list_entry(e)
+        while it:
+            out.append(L.udev_list_entry_get_name(it).decode())
+            it = L.udev_list_entry_get_next(it)
+        return out
+    u = L.udev_new()
+    e = L.udev_enumerate_new(u)
+    L.udev_enumerate_add_match_devicenode(e, b"/dev/input/js*")
+    assert L.udev_enumerate_scan_devices(e) == 0
+    js = names(e)
+    assert len(js) == 4 and all(p.split("/")[-1].startswith("js") for p in js)
+    L.udev_enumerate_unref(e)
+    e = L.udev_enumerate_new(u)
+    L.udev_enumerate_add_match_subsystem(e, b"input")
+    L.udev_enumerate_add_match_sysnum(e, b"1002")
+    assert L.udev_enumerate_scan_devices(e) == 0
+    assert [p.split("/")[-1] for p in names(e)] == ["event1002"]
+    L.udev_enumerate_unref(e)
+    # children of pad 1's USB device: its input node and the js / event nodes below it
+    d = L.udev_device_new_from_syspath(u, js[1].encode())
+    usb = L.udev_device_get_parent_with_subsystem_devtype(d, b"usb", b"usb_device")
+    assert usb
+    e = L.udev_enumerate_new(u)
+    assert L.udev_enumerate_scan_children(e) < 0          # no parent set
+    L.udev_enumerate_add_match_parent(e, usb)
+    assert L.udev_enumerate_scan_children(e) == 0
+    kids = names(e)
+    assert L.udev_device_get_syspath(usb).decode() in kids and js[1] in kids
+    assert not any(k in kids for k in js if k != js[1])
+    L.udev_enumerate_unref(e)
+
