@@ -82,11 +82,12 @@ def parse():
                    help="ONE session of --width x --height split into one band of stripes per rank "
                         "(parallel/dist_banded.py): rank 0 scatters the bands over RCCL, every rank encodes its "
                         "band on its GPU, packets are gathered to rank 0 each step; strong scaling")
-    p.add_argument("--e2e-sessions", default="48,32,16",
+    p.add_argument("--e2e-sessions", default="auto",
                    help="before the timed window (single process, HIP, H.264 only): serve N 1080p60 sessions from "
                         "real server processes (session hosts) to headless websocket clients for --e2e-seconds and report the "
                         "measured capture->client latency; a comma list is tried in order and the first N at "
-                        "which every session sustains 60 fps is reported (tools/bench_e2e.py); 0 = skip")
+                        "which every session sustains 60 fps is reported (tools/bench_e2e.py); 'auto' descends "
+                        "from the CPU quota's cap in steps of 8; 0 = skip")
     p.add_argument("--e2e-av1", default="3840x2160@120:40000",
                    help="WxH@fps:kbps of the AV1 end-to-end group (one session, encoder svtav1enc, the headless "
                         "client decodes every frame with dav1d: capture->decoded latency); 'none' = skip")
@@ -262,6 +263,17 @@ def e2e_counts(args, world=1):
 
 
 def e2e_counts_uncapped(args, world=1):
+    """'auto' (the default): one GPU descends in steps of 8 sessions from the most this
+    rank's CPU share can drive (e2e_cpu_cap) and stops at the first count every session
+    sustains, so the reported count is the measured knee and `tried` holds the failing
+    count above it; a node of N GPUs serves BASELINE config 4's share per rank."""
+    if str(args.e2e_sessions) == "auto":
+        if world > 1:
+            per = max(1, 64 // world)
+            return [2 * per, per]
+        top = max(8, e2e_cpu_cap(world) // 8 * 8)
+        v = list(range(top, 47, -8))
+        return v + [n for n in (32, 16) if n <= top and n not in v]
     v = [int(x) for x in str(args.e2e_sessions).split(",") if x.strip() and int(x) > 0]
     if world > 1 and args.e2e_sessions == "48,32,16":
         per = max(1, 64 // world)
