@@ -4,18 +4,24 @@
 // candidate lists, the syntax binarisation into CABAC bins and the CABAC
 // arithmetic coder itself.
 //
-// Coding structure (fixed by the parameter sets in hevc_syntax.cpp):
-//   CTB = CU = 16x16 (log2 min CB 4, no split flags), PU 2Nx2N, a residual quadtree of
-//   two levels: TU = CU (16x16 luma, 8x8 chroma), or four 8x8 nodes with 4x4 chroma each,
-//   every node one 8x8 luma TU or four 4x4 ones (DST for intra)
-//   (max_transform_hierarchy_depth 2, the encoder's RD choice), intra prediction per TU,
-//   mode-dependent scans, one reference picture (previous picture),
-//   quarter-pel motion (8-tap luma / 4-tap chroma MC), deblocking on (CU edges, deblock_picture), SAO
-//   (hevc_sao.h), no sign hiding /
-//   transform skip,
+// Coding structure (fixed by the parameter sets in hevc_params.cpp):
+//   CTB 32x32 with a coding quadtree over a 16x16 analysis grid ("units": the front end's
+//   macroblocks, one CuInfo / coefficient / bin slot each). A CTB is either one 32x32 CU
+//   (inter: PART_2Nx2N, 2NxN or Nx2N, each PU the motion of its units; a 32x32 TU or the
+//   residual quadtree split into four 16x16 nodes) or four 16x16 CUs; an intra 16x16 CU is
+//   either one CU (PART_2Nx2N) or four 8x8 CUs (min CB 8), each PART_2Nx2N or PART_NxN
+//   (four 4x4 PUs with their own modes). Under a 16x16 CU (or node) the residual quadtree
+//   has two more levels: one 16x16 TU or four 8x8 nodes, every node one 8x8 TU or four 4x4
+//   ones (DST for intra luma 4x4, transform skip per 4x4 TU) (max TB 32, the encoder's RD
+//   choice), intra prediction per TU, mode-dependent scans, one reference picture (previous
+//   picture), quarter-pel motion (8-tap luma / 4-tap chroma MC), merge candidates A1 B1 B0
+//   A0 B2 on the z-scan availability of the CTB, deblocking on (TU and PU edges,
+//   deblock_picture), SAO per CTB (hevc_sao.h), no sign hiding,
 //   entropy_coding_sync (WPP): one CABAC substream per CTB row, slices = stripes of
 //   whole CTB rows; intra slices split every row into slices of ~kIntraSegCtbs CTBs
 //   (SliceMap: a key frame's CTB chain is a segment, not a row).
+//   Coding order: CTBs in raster order, the units of a CTB in z order (unit z = x | y << 1);
+//   the substream of a CTB row is the sequence of its units' bin chunks in that order.
 // Decoder-side operations (inverse transform, dequantisation, intra prediction,
 // chroma interpolation, merge/AMVP derivation, context selection) follow the
 // normative processes of ITU-T H.265 (04/2013) clauses 8 and 9 exactly; forward
@@ -28,18 +34,19 @@
 namespace sk {
 namespace hevc {
 
-// Slice layout of a picture, in CTBs. Slices are stripes of rows_per_slice CTB rows
-// (one WPP substream per row). A row of an intra slice is instead cut into K slices of
+// Slice layout of a picture, in CTBs (32x32). Slices are stripes of rows_per_slice CTB
+// rows (one WPP substream per row). A row of an intra slice is instead cut into K slices of
 // about mb_w / K CTBs each, K = ceil(mb_w / kIntraSegCtbs): the closed-loop intra coding
 // of a CTB waits for its left neighbour, so a key frame's longest serial chain is one
-// segment (40 CTBs at 4K) instead of one row (240) - the same cut as the H.264 IDR
-// sub-slices (h264_encoder.h intra_split). Such a slice starts mid-row and ends in the
+// segment (20 CTBs = 80 units at 4K) instead of one row (120) - the same cut as the H.264
+// IDR sub-slices (h264_encoder.h intra_split). Such a slice starts mid-row and ends in the
 // same row, as 7.4.7.1 requires under entropy_coding_sync; it has no top neighbours
 // and restarts CABAC, so the cost is some intra and context-adaptation efficiency.
 // Neighbours in another slice are unavailable to prediction, CABAC context selection,
 // SAO merging, and (pps_loop_filter_across_slices_enabled_flag = 0) to deblocking and
 // SAO edge offsets. Per-segment arrays are indexed by slot = cy * K + k.
-constexpr int kIntraSegCtbs = 40;
+// (mb_w here: CTBs per row.)
+constexpr int kIntraSegCtbs = 20;
 SK_HD int intra_seg_count(int mb_w, int seg_ctbs) {
     return seg_ctbs > 0 && mb_w > seg_ctbs ? (mb_w + seg_ctbs - 1) / seg_ctbs : 1;
 }
@@ -58,24 +65,67 @@ struct SliceMap {
     SK_HD bool left(int cx, int cy) const { return cx > 0 && same(cx - 1, cy, cx, cy); }
     SK_HD bool top(int cx, int cy) const { return cy > 0 && same(cx, cy - 1, cx, cy); }
     SK_HD bool top_right(int cx, int cy) const { return cy > 0 && cx + 1 < mb_w && same(cx + 1, cy - 1, cx, cy); }
+    // the same on the unit grid (unit (ux, uy) lies in CTB (ux >> 1, uy >> 1))
+    SK_HD bool same_u(int ax, int ay, int bx, int by) const { return same(ax >> 1, ay >> 1, bx >> 1, by >> 1); }
 };
 
-constexpr int kCtb = 16;
-constexpr int kCoefPerCu = 384;     // 16x16 luma | 8x8 Cb | 8x8 Cr, raster [y][x] per TU; split CUs:
-                                    // luma node q (z order) at 64q (one 8x8 TU, or 4x4 TU j at 64q + 16j),
-                                    // Cb at 256 + 16q, Cr at 320 + 16q
+// Units (16x16) of the picture and their CTBs: W16 x H16 units, CTB (c, r) holds units
+// (2c + (z & 1), 2r + (z >> 1)) that lie inside the picture.
+struct UnitGrid {
+    int W16, H16;
+    SK_HD int cw() const { return (W16 + 1) >> 1; }
+    SK_HD int ch() const { return (H16 + 1) >> 1; }
+    SK_HD bool inside(int ux, int uy) const { return ux >= 0 && uy >= 0 && ux < W16 && uy < H16; }
+    SK_HD bool complete(int c, int r) const { return 2 * c + 1 < W16 && 2 * r + 1 < H16; }
+    // z-scan order (6.4.1) between two units inside the picture: a decoded before b
+    SK_HD bool before(int ax, int ay, int bx, int by) const {
+        const int ca = (ay >> 1) * cw() + (ax >> 1), cb = (by >> 1) * cw() + (bx >> 1);
+        if (ca != cb) return ca < cb;
+        return ((ax & 1) | ((ay & 1) << 1)) < ((bx & 1) | ((by & 1) << 1));
+    }
+    // neighbour unit (nx, ny) available to unit (ux, uy): inside, decoded before, same slice
+    SK_HD bool avail(const SliceMap& m, int ux, int uy, int nx, int ny) const {
+        return inside(nx, ny) && before(nx, ny, ux, uy) && m.same_u(nx, ny, ux, uy);
+    }
+    // chunks (units in coding order) of CTB row r: units of rows 2r, 2r + 1
+    SK_HD bool two_rows(int r) const { return 2 * r + 1 < H16; }
+    SK_HD int row_chunks(int r) const { return two_rows(r) ? 2 * W16 : W16; }
+    SK_HD int ctb_chunk0(int r, int c) const { return two_rows(r) ? 4 * c : 2 * c; }   // first chunk of CTB c
+    SK_HD int chunk_unit(int r, int j) const {   // unit index of chunk j of CTB row r
+        const int y0 = 2 * r;
+        if (!two_rows(r)) return y0 * W16 + j;
+        const int full = W16 >> 1;
+        if (j < 4 * full) return (y0 + ((j >> 1) & 1)) * W16 + 2 * (j >> 2) + (j & 1);
+        return (y0 + (j - 4 * full)) * W16 + W16 - 1;   // odd width: the last CTB's z0, z2
+    }
+    SK_HD int unit_chunk(int ux, int uy) const {   // inverse: chunk of unit (ux, uy) in its CTB row
+        if (!two_rows(uy >> 1)) return ux;
+        const int full = W16 >> 1;
+        if (ux < 2 * full) return 4 * (ux >> 1) + 2 * (uy & 1) + (ux & 1);
+        return 4 * full + (uy & 1);
+    }
+};
+
+constexpr int kCtb = 32;
+constexpr int kCoefPerCu = 384;     // per unit: 16x16 luma | 8x8 Cb | 8x8 Cr, raster [y][x] per TU; split
+                                    // units: luma node q (z order) at 64q (one 8x8 TU, or 4x4 TU j at
+                                    // 64q + 16j), Cb at 256 + 16q, Cr at 320 + 16q. A CU32 with one 32x32
+                                    // TU keeps its 1536 levels (luma 32x32 | Cb 16x16 | Cr 16x16, raster)
+                                    // across the slots of its units z0..z3 (kT32Cb / kT32Cr offsets)
 constexpr int kCoefCb = 256, kCoefCr = 320;
+constexpr int kT32Cb = 1024, kT32Cr = 1280, kT32Coefs = 1536;
 constexpr int kCuBinCap = 4096;     // bin entries per CU slot (worst case ~3950, see bin_bound)
 constexpr int kSubstreamCtbBytes = 4608;   // worst-case CABAC bytes per CTB (>= 6 bits x ctx bins)
 
 // ---------------------------------------------------------------------------
-// Per-CU decisions (24 bytes, shared by CPU and GPU buffers; tests diff them).
+// Per-unit decisions (40 bytes, shared by CPU and GPU buffers; tests diff them).
 enum CuMode : uint8_t { CU_SKIP = 0, CU_MERGE = 1, CU_AMVP = 2, CU_INTRA = 3 };
+enum Part : uint8_t { PART_2Nx2N = 0, PART_2NxN = 1, PART_Nx2N = 2 };
 struct CuInfo {
-    uint8_t mode;         // CuMode
+    uint8_t mode;         // CuMode (a CU32 member: the mode of the PU holding the unit)
     uint8_t merge_idx;    // SKIP / MERGE
     uint8_t mvp_idx;      // AMVP
-    uint8_t intra_mode;   // IntraPredModeY (chroma: DM, intra_chroma_pred_mode = 4)
+    uint8_t intra_mode;   // IntraPredModeY (a CU8-split unit: of CU8 0's first PU); chroma: DM
     uint8_t cbf;          // bit0 Y, bit1 Cb, bit2 Cr (split CUs: any TU of the component)
     uint8_t qp;
     uint8_t tu;           // bit 4: four 8x8 nodes (split_transform_flag); bits 0..3: node q in four 4x4 TUs
@@ -85,9 +135,16 @@ struct CuInfo {
     uint16_t ycbf;        // cbf_luma of the TU covering each 4x4 unit (bit = z-order index)
     uint16_t tsy;         // transform_skip_flag of the 4x4 luma TUs (bit = z-order index)
     uint8_t tsc;          // transform_skip_flag of the nodes' 4x4 chroma TUs: bits 0..3 Cb, 4..7 Cr
-    uint8_t pad2[3];
+    uint8_t cu8;          // intra: bit 4 = four 8x8 CUs; bit q = CU8 q is PART_NxN
+    uint8_t c32;          // bit 0: the unit is part of a 32x32 CU; bits 1..2 its Part; bit 3: one 32x32 TU
+    uint8_t rsv;
+    uint8_t ipm[16];      // IntraPredModeY per 4x4 block (z order): MPM neighbours, per-TU prediction
 };
-static_assert(sizeof(CuInfo) == 24, "CuInfo layout");
+static_assert(sizeof(CuInfo) == 40, "CuInfo layout");
+constexpr uint8_t kC32 = 1, kC32Tu = 8;
+SK_HD int c32_part(const CuInfo& c) { return (c.c32 >> 1) & 3; }
+// CtDepth of the unit's CU (split_cu_flag contexts): 0 CU32, 1 CU16, 2 CU8
+SK_HD int cu_depth(const CuInfo& c) { return (c.c32 & kC32) ? 0 : ((c.cu8 & 16) ? 2 : 1); }
 
 // ---------------------------------------------------------------------------
 // Tables.
@@ -108,8 +165,43 @@ SK_TABLE int8_t HEVC_T16[16][16] = {
     {25, -70, 90, -80, 43, 9, -57, 87, -87, 57, -9, -43, 80, -90, 70, -25},
     {18, -50, 75, -89, 89, -75, 50, -18, -18, 50, -75, 89, -89, 75, -50, 18},
     {9, -25, 43, -57, 70, -80, 87, -90, 90, -87, 80, -70, 57, -43, 25, -9}};
+// 32-point matrix (8.6.4.2 transMatrix): the even rows restricted to 16 columns are the
+// 16-point matrix, the odd rows use 90, 90, 88, 85, 82, 78, 73, 67, 61, 54, 46, 38, 31, 22, 13, 4.
+SK_TABLE int8_t HEVC_T32[32][32] = {
+    {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64},
+    {90, 90, 88, 85, 82, 78, 73, 67, 61, 54, 46, 38, 31, 22, 13, 4, -4, -13, -22, -31, -38, -46, -54, -61, -67, -73, -78, -82, -85, -88, -90, -90},
+    {90, 87, 80, 70, 57, 43, 25, 9, -9, -25, -43, -57, -70, -80, -87, -90, -90, -87, -80, -70, -57, -43, -25, -9, 9, 25, 43, 57, 70, 80, 87, 90},
+    {90, 82, 67, 46, 22, -4, -31, -54, -73, -85, -90, -88, -78, -61, -38, -13, 13, 38, 61, 78, 88, 90, 85, 73, 54, 31, 4, -22, -46, -67, -82, -90},
+    {89, 75, 50, 18, -18, -50, -75, -89, -89, -75, -50, -18, 18, 50, 75, 89, 89, 75, 50, 18, -18, -50, -75, -89, -89, -75, -50, -18, 18, 50, 75, 89},
+    {88, 67, 31, -13, -54, -82, -90, -78, -46, -4, 38, 73, 90, 85, 61, 22, -22, -61, -85, -90, -73, -38, 4, 46, 78, 90, 82, 54, 13, -31, -67, -88},
+    {87, 57, 9, -43, -80, -90, -70, -25, 25, 70, 90, 80, 43, -9, -57, -87, -87, -57, -9, 43, 80, 90, 70, 25, -25, -70, -90, -80, -43, 9, 57, 87},
+    {85, 46, -13, -67, -90, -73, -22, 38, 82, 88, 54, -4, -61, -90, -78, -31, 31, 78, 90, 61, 4, -54, -88, -82, -38, 22, 73, 90, 67, 13, -46, -85},
+    {83, 36, -36, -83, -83, -36, 36, 83, 83, 36, -36, -83, -83, -36, 36, 83, 83, 36, -36, -83, -83, -36, 36, 83, 83, 36, -36, -83, -83, -36, 36, 83},
+    {82, 22, -54, -90, -61, 13, 78, 85, 31, -46, -90, -67, 4, 73, 88, 38, -38, -88, -73, -4, 67, 90, 46, -31, -85, -78, -13, 61, 90, 54, -22, -82},
+    {80, 9, -70, -87, -25, 57, 90, 43, -43, -90, -57, 25, 87, 70, -9, -80, -80, -9, 70, 87, 25, -57, -90, -43, 43, 90, 57, -25, -87, -70, 9, 80},
+    {78, -4, -82, -73, 13, 85, 67, -22, -88, -61, 31, 90, 54, -38, -90, -46, 46, 90, 38, -54, -90, -31, 61, 88, 22, -67, -85, -13, 73, 82, 4, -78},
+    {75, -18, -89, -50, 50, 89, 18, -75, -75, 18, 89, 50, -50, -89, -18, 75, 75, -18, -89, -50, 50, 89, 18, -75, -75, 18, 89, 50, -50, -89, -18, 75},
+    {73, -31, -90, -22, 78, 67, -38, -90, -13, 82, 61, -46, -88, -4, 85, 54, -54, -85, 4, 88, 46, -61, -82, 13, 90, 38, -67, -78, 22, 90, 31, -73},
+    {70, -43, -87, 9, 90, 25, -80, -57, 57, 80, -25, -90, -9, 87, 43, -70, -70, 43, 87, -9, -90, -25, 80, 57, -57, -80, 25, 90, 9, -87, -43, 70},
+    {67, -54, -78, 38, 85, -22, -90, 4, 90, 13, -88, -31, 82, 46, -73, -61, 61, 73, -46, -82, 31, 88, -13, -90, -4, 90, 22, -85, -38, 78, 54, -67},
+    {64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64, 64, -64, -64, 64},
+    {61, -73, -46, 82, 31, -88, -13, 90, -4, -90, 22, 85, -38, -78, 54, 67, -67, -54, 78, 38, -85, -22, 90, 4, -90, 13, 88, -31, -82, 46, 73, -61},
+    {57, -80, -25, 90, -9, -87, 43, 70, -70, -43, 87, 9, -90, 25, 80, -57, -57, 80, 25, -90, 9, 87, -43, -70, 70, 43, -87, -9, 90, -25, -80, 57},
+    {54, -85, -4, 88, -46, -61, 82, 13, -90, 38, 67, -78, -22, 90, -31, -73, 73, 31, -90, 22, 78, -67, -38, 90, -13, -82, 61, 46, -88, 4, 85, -54},
+    {50, -89, 18, 75, -75, -18, 89, -50, -50, 89, -18, -75, 75, 18, -89, 50, 50, -89, 18, 75, -75, -18, 89, -50, -50, 89, -18, -75, 75, 18, -89, 50},
+    {46, -90, 38, 54, -90, 31, 61, -88, 22, 67, -85, 13, 73, -82, 4, 78, -78, -4, 82, -73, -13, 85, -67, -22, 88, -61, -31, 90, -54, -38, 90, -46},
+    {43, -90, 57, 25, -87, 70, 9, -80, 80, -9, -70, 87, -25, -57, 90, -43, -43, 90, -57, -25, 87, -70, -9, 80, -80, 9, 70, -87, 25, 57, -90, 43},
+    {38, -88, 73, -4, -67, 90, -46, -31, 85, -78, 13, 61, -90, 54, 22, -82, 82, -22, -54, 90, -61, -13, 78, -85, 31, 46, -90, 67, 4, -73, 88, -38},
+    {36, -83, 83, -36, -36, 83, -83, 36, 36, -83, 83, -36, -36, 83, -83, 36, 36, -83, 83, -36, -36, 83, -83, 36, 36, -83, 83, -36, -36, 83, -83, 36},
+    {31, -78, 90, -61, 4, 54, -88, 82, -38, -22, 73, -90, 67, -13, -46, 85, -85, 46, 13, -67, 90, -73, 22, 38, -82, 88, -54, -4, 61, -90, 78, -31},
+    {25, -70, 90, -80, 43, 9, -57, 87, -87, 57, -9, -43, 80, -90, 70, -25, -25, 70, -90, 80, -43, -9, 57, -87, 87, -57, 9, 43, -80, 90, -70, 25},
+    {22, -61, 85, -90, 73, -38, -4, 46, -78, 90, -82, 54, -13, -31, 67, -88, 88, -67, 31, 13, -54, 82, -90, 78, -46, 4, 38, -73, 90, -85, 61, -22},
+    {18, -50, 75, -89, 89, -75, 50, -18, -18, 50, -75, 89, -89, 75, -50, 18, 18, -50, 75, -89, 89, -75, 50, -18, -18, 50, -75, 89, -89, 75, -50, 18},
+    {13, -38, 61, -78, 88, -90, 85, -73, 54, -31, 4, 22, -46, 67, -82, 90, -90, 82, -67, 46, -22, -4, 31, -54, 73, -85, 90, -88, 78, -61, 38, -13},
+    {9, -25, 43, -57, 70, -80, 87, -90, 90, -87, 80, -70, 57, -43, 25, -9, -9, 25, -43, 57, -70, 80, -87, 90, -90, 87, -80, 70, -57, 43, -25, 9},
+    {4, -13, 22, -31, 38, -46, 54, -61, 67, -73, 78, -82, 85, -88, 90, -90, 90, -90, 88, -85, 82, -78, 73, -67, 61, -54, 46, -38, 31, -22, 13, -4}};
 // The 8-point matrix is rows 0, 2, 4, ... of the 16-point one restricted to 8 columns.
-SK_HD int dct_coef(int log2n, int k, int n) { return HEVC_T16[k << (4 - log2n)][n]; }
+SK_HD int dct_coef(int log2n, int k, int n) { return log2n == 5 ? HEVC_T32[k][n] : HEVC_T16[k << (4 - log2n)][n]; }
 // 4x4 DST-VII (8.6.4.2, intra luma 4x4 TUs).
 SK_TABLE int8_t HEVC_DST4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
 SK_HD int tx_coef(int log2n, bool dst, int k, int n) { return dst ? HEVC_DST4[k][n] : dct_coef(log2n, k, n); }
@@ -119,10 +211,13 @@ SK_HD int zorder4(int x, int y) { return (x & 1) | ((y & 1) << 1) | ((x & 2) << 
 // Up-right diagonal scan of a 4x4 (sub-)block: scan position -> raster (y*4+x), and back.
 SK_HD int diag4_raster(int n) { return (int)((0xfbe7ad369c258140ULL >> (4 * n)) & 15); }
 SK_HD int diag4_scanpos(int r) { return (int)((0xfda6eb73c8419520ULL >> (4 * r)) & 15); }
-// Sub-block scans: 2x2 for 8x8 TUs, 4x4 for 16x16 TUs (same diagonal rule).
+// Sub-block scans: 2x2 for 8x8 TUs, 4x4 for 16x16 TUs, 8x8 for 32x32 TUs (same diagonal rule).
 SK_HD int diag2_raster(int n) { return (int)((0x3120u >> (4 * n)) & 15); }   // (0,0),(0,1),(1,0),(1,1) as y*2+x
+SK_TABLE uint8_t HEVC_DIAG8[64] = {0,  8,  1,  16, 9,  2,  24, 17, 10, 3,  32, 25, 18, 11, 4,  40, 33, 26, 19, 12, 5,  48,
+                                   41, 34, 27, 20, 13, 6,  56, 49, 42, 35, 28, 21, 14, 7,  57, 50, 43, 36, 29, 22, 15, 58,
+                                   51, 44, 37, 30, 23, 59, 52, 45, 38, 31, 60, 53, 46, 39, 61, 54, 47, 62, 55, 63};
 SK_HD int sb_raster(int log2n, int i) {   // sub-block scan index -> raster index in the sub-block grid
-    return log2n == 4 ? diag4_raster(i) : (log2n == 3 ? diag2_raster(i) : 0);
+    return log2n == 5 ? HEVC_DIAG8[i] : (log2n == 4 ? diag4_raster(i) : (log2n == 3 ? diag2_raster(i) : 0));
 }
 // scanIdx (7.4.9.11): 0 up-right diagonal, 1 horizontal, 2 vertical. The horizontal and
 // vertical scans occur for 4x4 / 8x8 TUs only (mode-dependent intra scans).
@@ -189,7 +284,9 @@ enum Ctx : int {
     CTX_SAO_TYPE = 132,      // first bin of sao_type_idx_luma / _chroma
     CTX_SPLIT_TF = 133,      // 3 split_transform_flag (ctxInc 5 - log2TrafoSize)
     CTX_TS = 136,            // 2 transform_skip_flag (luma, chroma)
-    CTX_COUNT = 138,
+    CTX_SPLIT_CU = 138,      // 3 split_cu_flag (ctxInc = condL + condA on CtDepth)
+    CTX_PART_MODE1 = 141,    // part_mode bin 1 (inter: 2NxN "01" / Nx2N "00")
+    CTX_COUNT = 142,
     CTX_TERM = 255           // terminating bin (end_of_slice_segment_flag / end_of_subset_one_bit)
 };
 SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
@@ -213,7 +310,9 @@ SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
      138, 153, 136, 167, 152, 152,  // greater2
      153, 200,                      // sao merge, sao type
      153, 138, 138,                 // split_transform_flag
-     139, 139},                     // transform_skip_flag
+     139, 139,                      // transform_skip_flag
+     139, 141, 157,                 // split_cu_flag
+     154},                          // part_mode bin 1 (n/a)
     {// P slices (cabac_init_flag = 0)
      197, 185, 201,                 // cu_skip_flag
      149,                           // pred_mode_flag
@@ -234,7 +333,9 @@ SK_TABLE uint8_t HEVC_CTX_INIT[2][CTX_COUNT] = {
      107, 167, 91, 122, 107, 167,   // greater2
      153, 185,                      // sao merge, sao type
      124, 138, 94,                  // split_transform_flag
-     139, 139}};                    // transform_skip_flag
+     139, 139,                      // transform_skip_flag
+     107, 139, 126,                 // split_cu_flag
+     139}};                         // part_mode bin 1
 
 // Context state byte: (pStateIdx << 1) | valMps (9.3.2.2).
 SK_HD uint8_t ctx_init_state(int init_value, int slice_qp) {
@@ -410,7 +511,7 @@ struct CabacEncoder {
 SK_HD void fwd_transform(const int* res, int log2n, int* coef, bool dst = false) {
     const int n = 1 << log2n;
     const int sh1 = log2n - 1, sh2 = log2n + 6;
-    int tmp[256];
+    int tmp[1024];
     for (int y = 0; y < n; y++)          // horizontal: tmp[y][u]
         for (int u = 0; u < n; u++) {
             int s = 0;
@@ -428,7 +529,7 @@ SK_HD void fwd_transform(const int* res, int log2n, int* coef, bool dst = false)
 // residual = (r + 2048) >> 12 for 8-bit video.
 SK_HD void inv_transform(const int* d, int log2n, int* res, bool dst = false) {
     const int n = 1 << log2n;
-    int g[256];
+    int g[1024];
     for (int x = 0; x < n; x++)
         for (int y = 0; y < n; y++) {
             int s = 0;
@@ -575,31 +676,38 @@ SK_HD int intra_mode_bias(int mode, int qp) {
     return intra_mode_basic(mode) ? 0 : 6 * (qp < 12 ? 1 : 1 << ((qp - 12) / 6));
 }
 
-// Neighbour availability of transform blocks (z order inside the CU) for the intra
+// Neighbour availability of transform blocks (z order inside the unit) for the intra
 // reference samples: bit 0 below-left, 1 left, 2 above-left, 3 above, 4 above-right.
+// `nbm`: the same bits for the unit's neighbour units (unit_nbm: z-scan availability on
+// the CTB grid - the unit below-left is decoded for a CTB's z0, the one above-right is not
+// for its z3).
 enum { AV_BL = 1, AV_L = 2, AV_TL = 4, AV_T = 8, AV_TR = 16 };
-// 16x16 TU (the whole CU): the CU below-left is never decoded yet.
-SK_HD int cu_avail(bool left, bool top, bool tr) {
-    return (left ? AV_L : 0) | (left && top ? AV_TL : 0) | (top ? AV_T : 0) | (tr ? AV_TR : 0);
+SK_HD int unit_nbm(const UnitGrid& g, const SliceMap& m, int ux, int uy) {
+    return (g.avail(m, ux, uy, ux - 1, uy + 1) ? AV_BL : 0) | (g.avail(m, ux, uy, ux - 1, uy) ? AV_L : 0) |
+           (g.avail(m, ux, uy, ux - 1, uy - 1) ? AV_TL : 0) | (g.avail(m, ux, uy, ux, uy - 1) ? AV_T : 0) |
+           (g.avail(m, ux, uy, ux + 1, uy - 1) ? AV_TR : 0);
 }
-// Whether 4x4 unit (ux, uy) of the CU's neighbourhood (-1 .. 7) is decoded before the
-// unit with z-order index z of the CU (left / top / tr: the CU's neighbours).
-SK_HD bool unit_avail(int ux, int uy, int z, bool left, bool top, bool tr) {
-    if (uy < 0) return ux < 0 ? (left && top) : (ux < 4 ? top : (ux < 8 && tr));
-    if (uy >= 4 || ux >= 4) return false;
-    if (ux < 0) return left;
+// 16x16 TU (the whole unit): its references are the neighbour units'.
+SK_HD int cu_avail(int nbm) { return nbm; }
+// Whether 4x4 block (ux, uy) of the unit's neighbourhood (-1 .. 7) is decoded before the
+// block with z-order index z of the unit.
+SK_HD bool unit_avail(int ux, int uy, int z, int nbm) {
+    if (uy < 0) return ux < 0 ? (nbm & AV_TL) != 0 : (ux < 4 ? (nbm & AV_T) != 0 : (ux < 8 && (nbm & AV_TR)));
+    if (ux >= 4) return false;
+    if (uy >= 4) return ux < 0 && uy < 8 && (nbm & AV_BL);
+    if (ux < 0) return (nbm & AV_L) != 0;
     return zorder4(ux, uy) < z;
 }
-// The TU of s x s units (s = 1, 2) at unit (bx, by) of the CU: its neighbour segments
-// are whole units of earlier TUs or outside blocks, so their first unit decides.
-SK_HD int tu_avail_at(int bx, int by, int s, bool left, bool top, bool tr) {
+// The TU of s x s blocks (s = 1, 2) at block (bx, by) of the unit: its neighbour segments
+// are whole blocks of earlier TUs or outside units, so their first block decides.
+SK_HD int tu_avail_at(int bx, int by, int s, int nbm) {
     const int z = zorder4(bx, by);
-    return (unit_avail(bx - 1, by + s, z, left, top, tr) ? AV_BL : 0) | (unit_avail(bx - 1, by, z, left, top, tr) ? AV_L : 0) |
-           (unit_avail(bx - 1, by - 1, z, left, top, tr) ? AV_TL : 0) | (unit_avail(bx, by - 1, z, left, top, tr) ? AV_T : 0) |
-           (unit_avail(bx + s, by - 1, z, left, top, tr) ? AV_TR : 0);
+    return (unit_avail(bx - 1, by + s, z, nbm) ? AV_BL : 0) | (unit_avail(bx - 1, by, z, nbm) ? AV_L : 0) |
+           (unit_avail(bx - 1, by - 1, z, nbm) ? AV_TL : 0) | (unit_avail(bx, by - 1, z, nbm) ? AV_T : 0) |
+           (unit_avail(bx + s, by - 1, z, nbm) ? AV_TR : 0);
 }
-// 8x8 luma / 4x4 chroma node q of a split CU.
-SK_HD int tu_avail(int q, bool left, bool top, bool tr) { return tu_avail_at(2 * (q & 1), 2 * (q >> 1), 2, left, top, tr); }
+// 8x8 luma / 4x4 chroma node q of a split unit.
+SK_HD int tu_avail(int q, int nbm) { return tu_avail_at(2 * (q & 1), 2 * (q >> 1), 2, nbm); }
 
 // Encoder RD model shared by the CPU reference and the kernels (TU split and TU zeroing
 // decisions): J = 512 * SSE + lambda_q8 * R, R in half bits, lambda = 0.57 * 2^((QP - 12) / 3)
@@ -619,16 +727,42 @@ constexpr int kTuRateHalf = 8;      // cbf / last position of a coded TU
 constexpr int kSplitRateHalf = 12;  // the split CU's extra cbf flags
 constexpr int kSplit8RateHalf = 8;  // an 8x8 node's split flag and extra cbf_luma flags
 
-// Most probable modes (8.4.2) for CTB = CU: candB is always DC (above CTB row).
-SK_HD void intra_mpm(int cand_a, int* list) {
-    const int cand_b = 1;
+// Most probable modes (8.4.2) from the left (cand_a) and above (cand_b) PU modes (DC
+// when unavailable, not intra, or above the CTB).
+SK_HD void intra_mpm(int cand_a, int cand_b, int* list) {
     if (cand_a == cand_b) {
-        list[0] = 0; list[1] = 1; list[2] = 26;   // candA < 2
+        if (cand_a < 2) {
+            list[0] = 0; list[1] = 1; list[2] = 26;
+        } else {
+            list[0] = cand_a;
+            list[1] = 2 + ((cand_a + 29) % 32);
+            list[2] = 2 + ((cand_a - 2 + 1) % 32);
+        }
     } else {
         list[0] = cand_a;
         list[1] = cand_b;
         list[2] = (cand_a != 0 && cand_b != 0) ? 0 : ((cand_a != 1 && cand_b != 1) ? 1 : 26);
     }
+}
+// Bins of a luma mode given its MPM list: prev_intra_luma_pred_flag, then (written after
+// every PU's flag) mpm_idx (TR, bypass) or rem_intra_luma_pred_mode (5 bypass bins).
+SK_HD int mpm_hit(int m, const int* mpm) { return m == mpm[0] ? 0 : (m == mpm[1] ? 1 : (m == mpm[2] ? 2 : -1)); }
+template <class W>
+SK_HD void code_mpm_rest(W& w, int m, const int* mpm) {
+    const int hit = mpm_hit(m, mpm);
+    if (hit >= 0) {
+        if (hit == 0) w.bypass(0, 1);
+        else w.bypass(hit == 1 ? 2u : 3u, 2);
+        return;
+    }
+    int s[3] = {mpm[0], mpm[1], mpm[2]};
+    if (s[0] > s[1]) { int t = s[0]; s[0] = s[1]; s[1] = t; }
+    if (s[0] > s[2]) { int t = s[0]; s[0] = s[2]; s[2] = t; }
+    if (s[1] > s[2]) { int t = s[1]; s[1] = s[2]; s[2] = t; }
+    int rem = m;
+    for (int i = 2; i >= 0; i--)
+        if (rem > s[i]) rem--;
+    w.bypass((uint32_t)rem, 5);
 }
 
 // ---------------------------------------------------------------------------
@@ -698,49 +832,92 @@ SK_HD int chroma_mc_sample(const uint8_t* plane, int stride, int w, int h, int x
 }
 
 // ---------------------------------------------------------------------------
-// Merge candidates (8.5.3.2.2-4) and AMVP predictors (8.5.3.2.6-7) for a 16x16
-// 2Nx2N PU of a P slice with one reference picture. Neighbours: A1 left, B1 above,
-// B0 above-right, B2 above-left (A0 below-left is never decoded yet); `av` flags
-// include "inter" (P slices here carry inter CUs only). MVs quarter-pel.
+// Merge candidates (8.5.3.2.2-4) and AMVP predictors (8.5.3.2.6-7) of a PU of a P slice
+// with one reference picture (refIdx 0 everywhere, so no scaling): neighbours A0 below-left,
+// A1 left, B0 above-right, B1 above, B2 above-left of the PU, `av` = available and inter
+// (P slices carry inter CUs only). MVs quarter-pel.
 struct NbMv {
     bool av;
     int mvx, mvy;
 };
 constexpr int kMaxMergeCand = 5;
-SK_HD int merge_list(const NbMv& A1, const NbMv& B1, const NbMv& B0, const NbMv& B2, int* lx, int* ly) {
+SK_HD int merge_list(const NbMv& A1, const NbMv& B1, const NbMv& B0, const NbMv& A0, const NbMv& B2, int* lx, int* ly) {
     int n = 0;
     auto same = [](const NbMv& p, const NbMv& q) { return p.av && q.av && p.mvx == q.mvx && p.mvy == q.mvy; };
     const bool a1 = A1.av;
     const bool b1 = B1.av && !same(A1, B1);
     const bool b0 = B0.av && !same(B1, B0);
-    const bool a0 = false;
+    const bool a0 = A0.av && !same(A1, A0);
     const bool b2 = B2.av && !same(A1, B2) && !same(B1, B2) && ((int)a1 + (int)b1 + (int)b0 + (int)a0) != 4;
     if (a1) { lx[n] = A1.mvx; ly[n] = A1.mvy; n++; }
     if (b1) { lx[n] = B1.mvx; ly[n] = B1.mvy; n++; }
     if (b0) { lx[n] = B0.mvx; ly[n] = B0.mvy; n++; }
+    if (a0) { lx[n] = A0.mvx; ly[n] = A0.mvy; n++; }
     if (b2) { lx[n] = B2.mvx; ly[n] = B2.mvy; n++; }
     while (n < kMaxMergeCand) { lx[n] = 0; ly[n] = 0; n++; }   // zero candidates (refIdx 0)
     return n;
 }
-SK_HD void amvp_list(const NbMv& A1, const NbMv& B1, const NbMv& B0, const NbMv& B2, int* px, int* py) {
+SK_HD void amvp_list(const NbMv& A0, const NbMv& A1, const NbMv& B0, const NbMv& B1, const NbMv& B2, int* px, int* py) {
     // A: first available of A0, A1 (same reference picture: all inter neighbours here)
-    bool avA = A1.av;
-    int ax = A1.mvx, ay = A1.mvy;
+    bool avA = A0.av || A1.av;
+    int ax = A0.av ? A0.mvx : A1.mvx, ay = A0.av ? A0.mvy : A1.mvy;
     bool avB = false;
     int bx = 0, by = 0;
     if (B0.av) { avB = true; bx = B0.mvx; by = B0.mvy; }
     else if (B1.av) { avB = true; bx = B1.mvx; by = B1.mvy; }
     else if (B2.av) { avB = true; bx = B2.mvx; by = B2.mvy; }
-    const bool is_scaled = A1.av;   // availableA0 || availableA1
+    const bool is_scaled = A0.av || A1.av;   // availableA0 || availableA1
     if (!is_scaled && avB) { avA = true; ax = bx; ay = by; }
-    if (!is_scaled) {
-        // B re-derived with scaling allowed: identical vector (same POC distance)
-        avB = B0.av || B1.av || B2.av;
-    }
+    // (!is_scaled: B re-derived with scaling allowed gives the identical vector - same POC distance)
     int n = 0;
     if (avA) { px[n] = ax; py[n] = ay; n++; }
     if (avB && !(avA && ax == bx && ay == by)) { px[n] = bx; py[n] = by; n++; }
     while (n < 2) { px[n] = 0; py[n] = 0; n++; }
+}
+
+// The five spatial neighbours of a PU (luma position (xp, yp), size pw x ph) of the CU at
+// (xc, yc), size nc, part index pi, over the unit motion field: mv(ux, uy) gives a unit's
+// vector; availability 6.4.2 - a neighbour inside the current CU is available only when it
+// lies in PU 0 and this is PU 1 (sameCb), one outside needs z-scan availability on the CTB
+// grid (UnitGrid::avail from the CU's first unit).
+struct PuNb {
+    NbMv A0, A1, B0, B1, B2;
+};
+template <class MV>
+SK_HD PuNb pu_neighbours(const UnitGrid& g, const SliceMap& m, MV mv, int xc, int yc, int nc, int xp, int yp, int pw,
+                         int ph, int pi) {
+    auto at = [&](int xn, int yn) {
+        NbMv r;
+        r.av = false;
+        r.mvx = r.mvy = 0;
+        if (xn < 0 || yn < 0 || xn >= 16 * g.W16 || yn >= 16 * g.H16) return r;
+        const bool in_cu = xn >= xc && yn >= yc && xn < xc + nc && yn < yc + nc;
+        if (in_cu) r.av = pi == 1 && !(xn >= xp && yn >= yp && xn < xp + pw && yn < yp + ph);
+        else r.av = g.avail(m, xc >> 4, yc >> 4, xn >> 4, yn >> 4);
+        if (r.av) mv(xn >> 4, yn >> 4, &r.mvx, &r.mvy);
+        return r;
+    };
+    PuNb n;
+    n.A1 = at(xp - 1, yp + ph - 1);
+    n.B1 = at(xp + pw - 1, yp - 1);
+    n.B0 = at(xp + pw, yp - 1);
+    n.A0 = at(xp - 1, yp + ph);
+    n.B2 = at(xp - 1, yp - 1);
+    return n;
+}
+// Merge list of a PU (8.5.3.2.3: PART_Nx2N / 2NxN part 1 drop A1 / B1, the candidate of part 0).
+SK_HD void pu_merge_list(PuNb n, int part, int pi, int* lx, int* ly) {
+    if (pi == 1 && part == PART_Nx2N) n.A1.av = false;
+    if (pi == 1 && part == PART_2NxN) n.B1.av = false;
+    merge_list(n.A1, n.B1, n.B0, n.A0, n.B2, lx, ly);
+}
+SK_HD void pu_amvp_list(const PuNb& n, int* px, int* py) { amvp_list(n.A0, n.A1, n.B0, n.B1, n.B2, px, py); }
+// Geometry of PU pi of a CU at (xc, yc) of size nc for a Part.
+SK_HD void pu_rect(int part, int pi, int xc, int yc, int nc, int* xp, int* yp, int* pw, int* ph) {
+    *xp = xc + (part == PART_Nx2N && pi ? nc / 2 : 0);
+    *yp = yc + (part == PART_2NxN && pi ? nc / 2 : 0);
+    *pw = part == PART_Nx2N ? nc / 2 : nc;
+    *ph = part == PART_2NxN ? nc / 2 : nc;
 }
 // EGk bypass bin count and value (9.3.3.3).
 SK_HD int egk_bins(uint32_t v, int k, uint32_t* bits) {
@@ -767,6 +944,32 @@ SK_HD int mvd_bits_est(int d) {   // abs_mvd coding cost estimate in bins (AMVP 
     return 3 + egk_bins((uint32_t)(a - 2), 1, &b);
 }
 
+
+// Encoder rate estimates of CU / PU syntax (half bits): the CU32 vs four-CU16 choice
+// (hevc_cpu.cpp cu32_decide and k_hevc_inter run the same rule).
+SK_HD int pu_hdr_half(int mode, int merge_idx, int mvdx, int mvdy) {   // merge_flag + idx, or mvd + mvp flag
+    return mode == CU_AMVP ? 6 + 2 * (mvd_bits_est(mvdx) + mvd_bits_est(mvdy)) : 2 + 2 * merge_idx;
+}
+SK_HD int cu16_hdr_half(const CuInfo& cu) {   // split_cu_flag, cu_skip_flag, pred mode, part, PU, root cbf
+    if (cu.mode == CU_SKIP) return 4 + 2 * cu.merge_idx;
+    return 8 + pu_hdr_half(cu.mode, cu.merge_idx, cu.mvdx, cu.mvdy) + (cu.mode == CU_AMVP ? 2 : 0);
+}
+SK_HD int cu32_hdr_half(int part, const CuInfo& pu0, const CuInfo& pu1, bool skip) {
+    if (skip) return 2 + 2 * pu0.merge_idx;
+    return 6 + (part == PART_2Nx2N ? 2 : 4) + pu_hdr_half(pu0.mode, pu0.merge_idx, pu0.mvdx, pu0.mvdy) +
+           (part != PART_2Nx2N ? pu_hdr_half(pu1.mode, pu1.merge_idx, pu1.mvdx, pu1.mvdy) : 0);
+}
+// The PU split a CTB's four unit vectors allow (-1: none): all equal 2Nx2N, rows 2NxN, columns Nx2N.
+SK_HD int cu32_part(const int* mx, const int* my) {
+    auto eq = [&](int a, int b) { return mx[a] == mx[b] && my[a] == my[b]; };
+    if (eq(0, 1) && eq(0, 2) && eq(0, 3)) return PART_2Nx2N;
+    if (eq(0, 1) && eq(2, 3)) return PART_2NxN;
+    if (eq(0, 2) && eq(1, 3)) return PART_Nx2N;
+    return -1;
+}
+// The PU (0 / 1) of a CU32 that unit z lies in.
+SK_HD int cu32_pu_of(int part, int z) { return part == PART_2NxN ? z >> 1 : (part == PART_Nx2N ? z & 1 : 0); }
+
 // ---------------------------------------------------------------------------
 // Syntax binarisation. residual_coding (7.3.8.11) of one TU from raster levels.
 // last_sig_coeff prefix (group index) of a position and the first position of a group.
@@ -778,10 +981,51 @@ SK_HD int last_prefix(int p) {
     return g;
 }
 
-template <class W>
-SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx, int scan = SCAN_DIAG, int ts = 0) {
+// Coefficient accessors: c(i) = the level at raster index i (y * n + x) of the TU.
+struct CoefPtr {
+    const int16_t* p;
+    SK_HD int operator()(int i) const { return p[i]; }
+};
+// The levels of a CU32's 32x32 TU (and its 16x16 chroma TUs) spread over its units' slots:
+// logical index i (kT32Cb / kT32Cr offsets) -> slot of unit z = i / kCoefPerCu.
+struct CoefT32 {
+    const int16_t* slot[4];
+    int base;   // 0 luma, kT32Cb, kT32Cr
+    SK_HD int operator()(int i) const {
+        const int k = base + i;
+        return slot[k / kCoefPerCu][k % kCoefPerCu];
+    }
+};
+
+// g1ctx (greater1 context state) a coded sub-block leaves behind: its first eight
+// significant levels in reverse scan order.
+template <class C>
+SK_HD int sb_g1_end(C c, int n, int scan, int xs, int ys, bool* any) {
+    int g1ctx = 1, ng1 = 0;
+    *any = false;
+    for (int k = 15; k >= 0; k--) {
+        const int r = scan4_raster(scan, k);
+        const int v = c((ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3));
+        if (!v) continue;
+        *any = true;
+        if (ng1 < 8) {
+            const int f = sk_abs(v) > 1;
+            ng1++;
+            if (g1ctx > 0) g1ctx = f ? 0 : g1ctx + 1;
+        }
+    }
+    return g1ctx;
+}
+
+// residual_coding (7.3.8.11) of one TU from raster levels - or of the sub-blocks with scan
+// index in [lo, hi] only: a CU32's 32x32 and 16x16 TUs are binarised in pieces, one per
+// unit (the units' bin slots are the chunks of the chunk-parallel coder). The piece that
+// holds the last significant sub-block writes the TU prologue (transform_skip_flag, last
+// position); a later piece starts from the greater1 state the sub-blocks coded before it
+// leave (that of the nearest one with a significant level).
+template <class W, class C>
+SK_HD void code_residual(W& w, C c, int log2n, int cidx, int scan = SCAN_DIAG, int ts = 0, int lo = 0, int hi = 63) {
     const int n = 1 << log2n;
-    if (log2n == 2) w.ctx(CTX_TS + (cidx ? 1 : 0), ts);   // transform_skip_flag (PPS enables it)
     const int sbw = n >> 2;                     // sub-blocks per row
     const int nsb = sbw * sbw;
     // last significant coefficient in (sub-block, position) scan order
@@ -790,36 +1034,50 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx, int scan =
         const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
         for (int k = 15; k >= 0; k--) {
             const int r = scan4_raster(scan, k);
-            if (c[(ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3)]) { last_i = i; last_n = k; break; }
+            if (c((ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3))) { last_i = i; last_n = k; break; }
         }
     }
     if (last_i < 0) return;   // callers only code TUs with cbf = 1
-    const int lsr = sb_scan_raster(log2n, scan, last_i);
-    int lx = (lsr % sbw) * 4 + (scan4_raster(scan, last_n) & 3);
-    int ly = (lsr / sbw) * 4 + (scan4_raster(scan, last_n) >> 2);
-    if (scan == SCAN_VER) { const int t = lx; lx = ly; ly = t; }   // coded swapped (7.4.9.11)
-    // last_sig_coeff_x/y_prefix (TR, cMax 2*log2n - 1), then suffixes (FL, bypass)
-    const int off = cidx == 0 ? 3 * (log2n - 2) + ((log2n - 1) >> 2) : 15;
-    const int shift = cidx == 0 ? (log2n + 1) >> 2 : log2n - 2;
-    const int cmax = 2 * log2n - 1;
-    const int px = last_prefix(lx), py = last_prefix(ly);
-    for (int b = 0; b < px; b++) w.ctx(CTX_LAST_X + off + (b >> shift), 1);
-    if (px < cmax) w.ctx(CTX_LAST_X + off + (px >> shift), 0);
-    for (int b = 0; b < py; b++) w.ctx(CTX_LAST_Y + off + (b >> shift), 1);
-    if (py < cmax) w.ctx(CTX_LAST_Y + off + (py >> shift), 0);
-    if (px > 3) w.bypass((uint32_t)(lx - last_group_min(px)), (px >> 1) - 1);
-    if (py > 3) w.bypass((uint32_t)(ly - last_group_min(py)), (py >> 1) - 1);
+    const int i0 = last_i < hi ? last_i : hi;
+    if (i0 < lo) return;      // a piece above the last sub-block: nothing to code
+    if (i0 == last_i) {
+        if (log2n == 2) w.ctx(CTX_TS + (cidx ? 1 : 0), ts);   // transform_skip_flag (PPS enables it)
+        const int lsr = sb_scan_raster(log2n, scan, last_i);
+        int lx = (lsr % sbw) * 4 + (scan4_raster(scan, last_n) & 3);
+        int ly = (lsr / sbw) * 4 + (scan4_raster(scan, last_n) >> 2);
+        if (scan == SCAN_VER) { const int t = lx; lx = ly; ly = t; }   // coded swapped (7.4.9.11)
+        // last_sig_coeff_x/y_prefix (TR, cMax 2*log2n - 1), then suffixes (FL, bypass)
+        const int off = cidx == 0 ? 3 * (log2n - 2) + ((log2n - 1) >> 2) : 15;
+        const int shift = cidx == 0 ? (log2n + 1) >> 2 : log2n - 2;
+        const int cmax = 2 * log2n - 1;
+        const int px = last_prefix(lx), py = last_prefix(ly);
+        for (int b = 0; b < px; b++) w.ctx(CTX_LAST_X + off + (b >> shift), 1);
+        if (px < cmax) w.ctx(CTX_LAST_X + off + (px >> shift), 0);
+        for (int b = 0; b < py; b++) w.ctx(CTX_LAST_Y + off + (b >> shift), 1);
+        if (py < cmax) w.ctx(CTX_LAST_Y + off + (py >> shift), 0);
+        if (px > 3) w.bypass((uint32_t)(lx - last_group_min(px)), (px >> 1) - 1);
+        if (py > 3) w.bypass((uint32_t)(ly - last_group_min(py)), (py >> 1) - 1);
+    }
     // coded_sub_block_flag per sub-block (raster in the sub-block grid)
-    uint32_t csbf = 0;
+    uint64_t csbf = 0;
     for (int i = 0; i < nsb; i++) {
         const int sr = sb_raster(log2n, i), xs = sr % sbw, ys = sr / sbw;   // every sub-block once
         bool nz = false;
-        for (int k = 0; k < 16 && !nz; k++) nz = c[(ys * 4 + (k >> 2)) * n + xs * 4 + (k & 3)] != 0;
-        if (nz) csbf |= 1u << sr;
+        for (int k = 0; k < 16 && !nz; k++) nz = c((ys * 4 + (k >> 2)) * n + xs * 4 + (k & 3)) != 0;
+        if (nz) csbf |= 1ull << sr;
     }
     int c1_carry = 1;   // greater1 context state carried between sub-blocks (HM c1)
     bool first_g1_sb = true;
-    for (int i = last_i; i >= 0; i--) {
+    for (int i = i0 + 1; i <= last_i && first_g1_sb; i++) {   // a later piece: the state so far
+        const int sr = sb_scan_raster(log2n, scan, i);
+        bool any;
+        const int g = sb_g1_end(c, n, scan, sr % sbw, sr / sbw, &any);
+        if (any) {
+            c1_carry = g;
+            first_g1_sb = false;
+        }
+    }
+    for (int i = i0; i >= lo; i--) {
         const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
         const int right = (xs + 1 < sbw) ? (int)((csbf >> (sr + 1)) & 1) : 0;
         const int below = (ys + 1 < sbw) ? (int)((csbf >> (sr + sbw)) & 1) : 0;
@@ -835,7 +1093,7 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx, int scan =
         int lev[16];
         for (int k = 0; k < 16; k++) {
             const int r = scan4_raster(scan, k);
-            lev[k] = c[(ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3)];
+            lev[k] = c((ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3));
         }
         // sig_coeff_flag
         uint32_t sig = 0;
@@ -845,7 +1103,7 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx, int scan =
             if (!coded) break;
             const int r = scan4_raster(scan, k);
             const int xc = xs * 4 + (r & 3), yc = ys * 4 + (r >> 2);
-            const bool s = lev[k] != 0;
+            const bool sg = lev[k] != 0;
             if (k == 0 && infer_dc) {   // inferred 1 when no other flag of the sub-block was 1
                 sig |= 1u;
                 break;
@@ -868,8 +1126,8 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx, int scan =
                     sctx += log2n == 3 ? 9 : 12;
                 }
             }
-            w.ctx(CTX_SIG + (cidx == 0 ? sctx : 27 + sctx), s ? 1 : 0);
-            if (s) {
+            w.ctx(CTX_SIG + (cidx == 0 ? sctx : 27 + sctx), sg ? 1 : 0);
+            if (sg) {
                 sig |= 1u << k;
                 infer_dc = false;
             }
@@ -950,139 +1208,269 @@ SK_HD void code_residual(W& w, const int16_t* c, int log2n, int cidx, int scan =
     }
 }
 
-// Whole coding unit (7.3.8.5) for CTB = CU = 16x16. `skip_ctx` = condL + condA of
-// cu_skip_flag; `cand_a` = left intra mode for the MPM list (DC when unavailable).
+// merge_idx: TR cMax 4, first bin context coded, bins 1..3 bypass.
 template <class W>
-SK_HD void code_cu(W& w, const CuInfo& cu, const int16_t* coef, bool p_slice, int skip_ctx, int cand_a) {
-    if (p_slice) w.ctx(CTX_SKIP + skip_ctx, cu.mode == CU_SKIP);
-    if (cu.mode == CU_SKIP) {
-        // merge_idx: TR cMax 4, first bin context coded
-        w.ctx(CTX_MERGE_IDX, cu.merge_idx > 0);
-        if (cu.merge_idx > 0) {
-            const int rest = cu.merge_idx - 1;   // bins 1..3 bypass, TR with cMax 3
-            if (rest < 3) w.bypass((1u << (rest + 1)) - 2u, rest + 1);
-            else w.bypass(7u, 3);
+SK_HD void code_merge_idx(W& w, int merge_idx) {
+    w.ctx(CTX_MERGE_IDX, merge_idx > 0);
+    if (merge_idx > 0) {
+        const int rest = merge_idx - 1;
+        if (rest < 3) w.bypass((1u << (rest + 1)) - 2u, rest + 1);
+        else w.bypass(7u, 3);
+    }
+}
+// prediction_unit (7.3.8.6) of a non-skipped inter PU: merge_flag, then merge_idx or
+// mvd_coding (7.3.8.9) and mvp_l0_flag.
+template <class W>
+SK_HD void code_pu(W& w, const CuInfo& cu) {
+    w.ctx(CTX_MERGE_FLAG, cu.mode == CU_MERGE);
+    if (cu.mode == CU_MERGE) {
+        code_merge_idx(w, cu.merge_idx);
+        return;
+    }
+    const int ax = sk_abs(cu.mvdx), ay = sk_abs(cu.mvdy);
+    w.ctx(CTX_MVD_G0, ax > 0);
+    w.ctx(CTX_MVD_G0, ay > 0);
+    if (ax > 0) w.ctx(CTX_MVD_G1, ax > 1);
+    if (ay > 0) w.ctx(CTX_MVD_G1, ay > 1);
+    if (ax > 0) {
+        if (ax > 1) {
+            uint32_t b;
+            const int nb = egk_bins((uint32_t)(ax - 2), 1, &b);
+            w.bypass(b, nb);
+        }
+        w.bypass(cu.mvdx < 0 ? 1u : 0u, 1);
+    }
+    if (ay > 0) {
+        if (ay > 1) {
+            uint32_t b;
+            const int nb = egk_bins((uint32_t)(ay - 2), 1, &b);
+            w.bypass(b, nb);
+        }
+        w.bypass(cu.mvdy < 0 ? 1u : 0u, 1);
+    }
+    w.ctx(CTX_MVP, cu.mvp_idx);
+}
+
+// transform_tree (7.3.8.8) of a 16x16 node: a CU16's root (depth 0) or a CU32's node
+// (depth 1, under the root's chroma cbfs pcb / pcr): split_transform_flag at log2 4, the
+// chroma cbfs, then either the 16x16 transform unit or four 8x8 nodes (each one 8x8 TU or
+// four 4x4 TUs, the node's chroma 4x4 after its last). Intra scans follow each TU's mode.
+template <class W>
+SK_HD void code_tt16(W& w, const CuInfo& cu, const int16_t* coef, bool intra, int depth, int pcb, int pcr) {
+    const int cbf_y = cu.cbf & 1, cbf_cb = (cu.cbf >> 1) & 1, cbf_cr = (cu.cbf >> 2) & 1;
+    const bool split = (cu.tu >> 4) & 1;
+    w.ctx(CTX_SPLIT_TF + 1, split);   // ctxInc 5 - log2 4 (depth < MaxTrafoDepth: always coded)
+    if (depth == 0 || pcb) w.ctx(CTX_CBF_CHROMA + depth, cbf_cb);
+    if (depth == 0 || pcr) w.ctx(CTX_CBF_CHROMA + depth, cbf_cr);
+    if (!split) {
+        if (intra || depth || cbf_cb || cbf_cr) w.ctx(CTX_CBF_LUMA + (depth ? 0 : 1), cbf_y);
+        const int sy = intra ? intra_scan(cu.ipm[0], 4, 0) : SCAN_DIAG;
+        const int sc = intra ? intra_scan(cu.ipm[0], 3, 1) : SCAN_DIAG;
+        if (cbf_y) code_residual(w, CoefPtr{coef}, 4, 0, sy);
+        if (cbf_cb) code_residual(w, CoefPtr{coef + kCoefCb}, 3, 1, sc);
+        if (cbf_cr) code_residual(w, CoefPtr{coef + kCoefCr}, 3, 2, sc);
+        return;
+    }
+    const int d1 = depth + 1;
+    for (int q = 0; q < 4; q++) {
+        const int cb = (cu.tuc >> q) & 1, cr = (cu.tuc >> (4 + q)) & 1;
+        const bool split8 = (cu.tu >> q) & 1;
+        const int mq = cu.ipm[4 * q];
+        w.ctx(CTX_SPLIT_TF + 2, split8);   // log2 3
+        if (cbf_cb) w.ctx(CTX_CBF_CHROMA + d1, cb);
+        if (cbf_cr) w.ctx(CTX_CBF_CHROMA + d1, cr);
+        if (!split8) {
+            const int cy = (cu.ycbf >> (4 * q)) & 1;
+            w.ctx(CTX_CBF_LUMA + 0, cy);
+            if (cy) code_residual(w, CoefPtr{coef + 64 * q}, 3, 0, intra ? intra_scan(mq, 3, 0) : SCAN_DIAG);
+        } else {
+            for (int j = 0; j < 4; j++) {   // depth d1 + 1: chroma of the node after the last 4x4 (blkIdx 3)
+                const int cy = (cu.ycbf >> (4 * q + j)) & 1;
+                w.ctx(CTX_CBF_LUMA + 0, cy);
+                if (cy)
+                    code_residual(w, CoefPtr{coef + 64 * q + 16 * j}, 2, 0,
+                                  intra ? intra_scan(cu.ipm[4 * q + j], 2, 0) : SCAN_DIAG, (cu.tsy >> (4 * q + j)) & 1);
+            }
+        }
+        const int sc = intra ? intra_scan(mq, 2, 1) : SCAN_DIAG;
+        if (cb) code_residual(w, CoefPtr{coef + kCoefCb + 16 * q}, 2, 1, sc, (cu.tsc >> q) & 1);
+        if (cr) code_residual(w, CoefPtr{coef + kCoefCr + 16 * q}, 2, 2, sc, (cu.tsc >> (4 + q)) & 1);
+    }
+}
+
+// transform_tree of intra CU8 q of a CU8-split unit (depth 0, log2 3): PART_2Nx2N codes
+// split_transform_flag (one 8x8 TU or four 4x4), PART_NxN infers the split (IntraSplitFlag);
+// chroma cbfs at depth 0, the CU8's chroma 4x4 TUs last. Same storage as node q of code_tt16.
+template <class W>
+SK_HD void code_tt8(W& w, const CuInfo& cu, const int16_t* coef, int q) {
+    const int nxn = (cu.cu8 >> q) & 1;
+    const int cb = (cu.tuc >> q) & 1, cr = (cu.tuc >> (4 + q)) & 1;
+    const bool split8 = nxn || ((cu.tu >> q) & 1);
+    const int mq = cu.ipm[4 * q];
+    if (!nxn) w.ctx(CTX_SPLIT_TF + 2, split8);
+    w.ctx(CTX_CBF_CHROMA + 0, cb);
+    w.ctx(CTX_CBF_CHROMA + 0, cr);
+    if (!split8) {
+        const int cy = (cu.ycbf >> (4 * q)) & 1;
+        w.ctx(CTX_CBF_LUMA + 1, cy);   // intra, depth 0
+        if (cy) code_residual(w, CoefPtr{coef + 64 * q}, 3, 0, intra_scan(mq, 3, 0));
+    } else {
+        for (int j = 0; j < 4; j++) {
+            const int cy = (cu.ycbf >> (4 * q + j)) & 1;
+            w.ctx(CTX_CBF_LUMA + 0, cy);
+            if (cy)
+                code_residual(w, CoefPtr{coef + 64 * q + 16 * j}, 2, 0, intra_scan(cu.ipm[4 * q + j], 2, 0),
+                              (cu.tsy >> (4 * q + j)) & 1);
+        }
+    }
+    const int sc = intra_scan(mq, 2, 1);
+    if (cb) code_residual(w, CoefPtr{coef + kCoefCb + 16 * q}, 2, 1, sc, (cu.tsc >> q) & 1);
+    if (cr) code_residual(w, CoefPtr{coef + kCoefCr + 16 * q}, 2, 2, sc, (cu.tsc >> (4 + q)) & 1);
+}
+
+// The bin entries one unit contributes to its CTB's share of the substream (the chunk
+// of the chunk-parallel coder): the CTB's split_cu_flag when it is the CTB's first unit,
+// then its CU16 (split_cu_flag, CU syntax or four CU8s) - or, in a CU32, the CU header and
+// tree root (z0) and the unit's node (TU split) or piece of the 32x32 / 16x16 TUs (one TU).
+// SAO syntax before and end_of_slice_segment_flag after are the caller's (binarize).
+struct UnitCtx {
+    int z;          // z index of the unit in its CTB
+    int first;      // first unit of its CTB in coding order (z0)
+    int complete;   // the CTB lies inside the picture (its split_cu_flag is coded)
+    int left, top;  // the left / above unit is available (z-scan, slice)
+    int row0;       // the unit is in its CTB's top row (an above PU in another CTB counts as DC)
+    int p_slice;
+};
+// MPM candidates of the PU at 4x4 block (bx, by) of the unit.
+SK_HD void pu_mpm(const UnitCtx& u, const CuInfo& cu, const CuInfo* L, const CuInfo* T, int bx, int by, int* mpm) {
+    const int a = bx > 0 ? cu.ipm[zorder4(bx - 1, by)]
+                         : ((u.left && L->mode == CU_INTRA) ? L->ipm[zorder4(3, by)] : 1);
+    const int b = by > 0 ? cu.ipm[zorder4(bx, by - 1)]
+                         : ((!u.row0 && u.top && T->mode == CU_INTRA) ? T->ipm[zorder4(bx, 3)] : 1);
+    intra_mpm(a, b, mpm);
+}
+// c32: the CTB's four units in z order (used by CU32 units); t32: the CU32's 32x32 TU levels.
+template <class W>
+SK_HD void code_unit(W& w, const UnitCtx& u, const CuInfo& cu, const CuInfo* L, const CuInfo* T, const int16_t* coef,
+                     const CuInfo* c32, const CoefT32& t32) {
+    const int skip_ctx = (u.left && L->mode == CU_SKIP) + (u.top && T->mode == CU_SKIP);
+    if (u.first && u.complete) {   // CTB split_cu_flag (cqtDepth 0)
+        const int ctx = (u.left && cu_depth(*L) > 0) + (u.top && cu_depth(*T) > 0);
+        w.ctx(CTX_SPLIT_CU + ctx, (cu.c32 & kC32) ? 0 : 1);
+    }
+    if (cu.c32 & kC32) {   // ---- CU32 (inter)
+        const int part = c32_part(cu);
+        const bool tu32 = (cu.c32 & kC32Tu) != 0;
+        int cy = 0, cb = 0, cr = 0;
+        for (int k = 0; k < 4; k++) {
+            cy |= c32[k].cbf & 1;
+            cb |= (c32[k].cbf >> 1) & 1;
+            cr |= (c32[k].cbf >> 2) & 1;
+        }
+        const int root = cy | cb | cr;
+        const bool skip = c32[0].mode == CU_SKIP;
+        if (u.z == 0) {
+            if (u.p_slice) w.ctx(CTX_SKIP + skip_ctx, skip);
+            if (skip) {
+                code_merge_idx(w, c32[0].merge_idx);
+                return;
+            }
+            w.ctx(CTX_PRED_MODE, 0);
+            w.ctx(CTX_PART_MODE, part == PART_2Nx2N);             // "1" 2Nx2N, "01" 2NxN, "00" Nx2N
+            if (part != PART_2Nx2N) w.ctx(CTX_PART_MODE1, part == PART_2NxN);
+            code_pu(w, c32[0]);
+            if (part != PART_2Nx2N) code_pu(w, c32[3]);            // z3 lies in PU 1 of both splits
+            if (!(part == PART_2Nx2N && c32[0].mode == CU_MERGE)) w.ctx(CTX_RQT_ROOT_CBF, root);
+            if (!root) return;
+            w.ctx(CTX_SPLIT_TF + 0, tu32 ? 0 : 1);                 // log2 5, depth 0
+            w.ctx(CTX_CBF_CHROMA + 0, cb);
+            w.ctx(CTX_CBF_CHROMA + 0, cr);
+            if (!tu32) {
+                code_tt16(w, cu, coef, false, 1, cb, cr);
+                return;
+            }
+            if (cb || cr) w.ctx(CTX_CBF_LUMA + 1, cy);   // else inferred 1
+        }
+        if (skip || !root) return;
+        if (!tu32) {
+            if (u.z) code_tt16(w, cu, coef, false, 1, cb, cr);
+            return;
+        }
+        // one 32x32 TU: luma sub-blocks 63..40 | 39..16 | 15..0 + Cb 15..8 | Cb 7..0 + Cr
+        CoefT32 ty = t32, tb = t32, tr = t32;
+        ty.base = 0;
+        tb.base = kT32Cb;
+        tr.base = kT32Cr;
+        if (u.z == 0 && cy) code_residual(w, ty, 5, 0, SCAN_DIAG, 0, 40, 63);
+        if (u.z == 1 && cy) code_residual(w, ty, 5, 0, SCAN_DIAG, 0, 16, 39);
+        if (u.z == 2 && cy) code_residual(w, ty, 5, 0, SCAN_DIAG, 0, 0, 15);
+        if (u.z == 2 && cb) code_residual(w, tb, 4, 1, SCAN_DIAG, 0, 8, 15);
+        if (u.z == 3 && cb) code_residual(w, tb, 4, 1, SCAN_DIAG, 0, 0, 7);
+        if (u.z == 3 && cr) code_residual(w, tr, 4, 2, SCAN_DIAG, 0, 0, 15);
+        return;
+    }
+    // ---- CU16: split_cu_flag at cqtDepth 1 (log2 4 > MinCb 3: coded)
+    {
+        const int ctx = (u.left && cu_depth(*L) > 1) + (u.top && cu_depth(*T) > 1);
+        w.ctx(CTX_SPLIT_CU + ctx, (cu.cu8 >> 4) & 1);
+    }
+    if (cu.cu8 & 16) {   // four intra CU8s (I slices)
+        for (int q = 0; q < 4; q++) {
+            const int nxn = (cu.cu8 >> q) & 1, npu = nxn ? 4 : 1;
+            w.ctx(CTX_PART_MODE, nxn ? 0 : 1);   // intra at MinCb: "1" 2Nx2N, "0" NxN
+            int mpm[4][3], md[4];
+            for (int p = 0; p < npu; p++) {       // every prev_intra_luma_pred_flag first
+                const int bx = 2 * (q & 1) + (nxn ? (p & 1) : 0), by = 2 * (q >> 1) + (nxn ? (p >> 1) : 0);
+                md[p] = cu.ipm[zorder4(bx, by)];
+                pu_mpm(u, cu, L, T, bx, by, mpm[p]);
+                w.ctx(CTX_PREV_INTRA, mpm_hit(md[p], mpm[p]) >= 0);
+            }
+            for (int p = 0; p < npu; p++) code_mpm_rest(w, md[p], mpm[p]);
+            w.ctx(CTX_CHROMA_PRED, 0);   // intra_chroma_pred_mode = 4 (DM)
+            code_tt8(w, cu, coef, q);
         }
         return;
     }
-    if (p_slice) w.ctx(CTX_PRED_MODE, cu.mode == CU_INTRA ? 1 : 0);
-    w.ctx(CTX_PART_MODE, 1);   // PART_2Nx2N
-    const int cbf_y = cu.cbf & 1, cbf_cb = (cu.cbf >> 1) & 1, cbf_cr = (cu.cbf >> 2) & 1;
-    if (cu.mode == CU_INTRA) {
+    if (u.p_slice) w.ctx(CTX_SKIP + skip_ctx, cu.mode == CU_SKIP);
+    if (cu.mode == CU_SKIP) {
+        code_merge_idx(w, cu.merge_idx);
+        return;
+    }
+    const bool intra = cu.mode == CU_INTRA;
+    if (u.p_slice) w.ctx(CTX_PRED_MODE, intra ? 1 : 0);
+    if (intra) {   // PART_2Nx2N (part_mode is coded for intra CUs at MinCb only)
         int mpm[3];
-        intra_mpm(cand_a, mpm);
-        const int m = cu.intra_mode;
-        const int hit = m == mpm[0] ? 0 : (m == mpm[1] ? 1 : (m == mpm[2] ? 2 : -1));
-        w.ctx(CTX_PREV_INTRA, hit >= 0);
-        if (hit >= 0) {
-            if (hit == 0) w.bypass(0, 1);
-            else w.bypass(hit == 1 ? 2u : 3u, 2);
-        } else {
-            int s[3] = {mpm[0], mpm[1], mpm[2]};
-            if (s[0] > s[1]) { int t = s[0]; s[0] = s[1]; s[1] = t; }
-            if (s[0] > s[2]) { int t = s[0]; s[0] = s[2]; s[2] = t; }
-            if (s[1] > s[2]) { int t = s[1]; s[1] = s[2]; s[2] = t; }
-            int rem = m;
-            for (int i = 2; i >= 0; i--)
-                if (rem > s[i]) rem--;
-            w.bypass((uint32_t)rem, 5);
-        }
+        pu_mpm(u, cu, L, T, 0, 0, mpm);
+        w.ctx(CTX_PREV_INTRA, mpm_hit(cu.ipm[0], mpm) >= 0);
+        code_mpm_rest(w, cu.ipm[0], mpm);
         w.ctx(CTX_CHROMA_PRED, 0);   // intra_chroma_pred_mode = 4 (DM)
     } else {
-        w.ctx(CTX_MERGE_FLAG, cu.mode == CU_MERGE);
-        if (cu.mode == CU_MERGE) {
-            w.ctx(CTX_MERGE_IDX, cu.merge_idx > 0);
-            if (cu.merge_idx > 0) {
-                const int rest = cu.merge_idx - 1;
-                if (rest < 3) w.bypass((1u << (rest + 1)) - 2u, rest + 1);
-                else w.bypass(7u, 3);
-            }
-        } else {
-            const int ax = sk_abs(cu.mvdx), ay = sk_abs(cu.mvdy);
-            w.ctx(CTX_MVD_G0, ax > 0);
-            w.ctx(CTX_MVD_G0, ay > 0);
-            if (ax > 0) w.ctx(CTX_MVD_G1, ax > 1);
-            if (ay > 0) w.ctx(CTX_MVD_G1, ay > 1);
-            if (ax > 0) {
-                if (ax > 1) {
-                    uint32_t b;
-                    const int nb = egk_bins((uint32_t)(ax - 2), 1, &b);
-                    w.bypass(b, nb);
-                }
-                w.bypass(cu.mvdx < 0 ? 1u : 0u, 1);
-            }
-            if (ay > 0) {
-                if (ay > 1) {
-                    uint32_t b;
-                    const int nb = egk_bins((uint32_t)(ay - 2), 1, &b);
-                    w.bypass(b, nb);
-                }
-                w.bypass(cu.mvdy < 0 ? 1u : 0u, 1);
-            }
-            w.ctx(CTX_MVP, cu.mvp_idx);
-        }
+        w.ctx(CTX_PART_MODE, 1);     // PART_2Nx2N
+        code_pu(w, cu);
         if (cu.mode != CU_MERGE) {
             w.ctx(CTX_RQT_ROOT_CBF, cu.cbf != 0);
             if (cu.cbf == 0) return;
         }
     }
-    // transform_tree (7.3.8.8): split_transform_flag at log2 4 (ctxInc 1), the depth-0
-    // chroma cbfs, then either the 16x16 transform unit or four 8x8 ones (depth 1: no
-    // further split, chroma cbfs under a set parent flag, cbf_luma always coded)
-    const bool intra = cu.mode == CU_INTRA;
-    const bool split = (cu.tu >> 4) & 1;
-    w.ctx(CTX_SPLIT_TF + 1, split);
-    w.ctx(CTX_CBF_CHROMA + 0, cbf_cb);
-    w.ctx(CTX_CBF_CHROMA + 0, cbf_cr);
-    if (!split) {
-        if (intra || cbf_cb || cbf_cr) w.ctx(CTX_CBF_LUMA + 1, cbf_y);
-        const int sy = intra ? intra_scan(cu.intra_mode, 4, 0) : SCAN_DIAG;
-        const int sc = intra ? intra_scan(cu.intra_mode, 3, 1) : SCAN_DIAG;
-        if (cbf_y) code_residual(w, coef, 4, 0, sy);
-        if (cbf_cb) code_residual(w, coef + kCoefCb, 3, 1, sc);
-        if (cbf_cr) code_residual(w, coef + kCoefCr, 3, 2, sc);
-        return;
-    }
-    const int sy = intra ? intra_scan(cu.intra_mode, 3, 0) : SCAN_DIAG;
-    const int s4 = intra ? intra_scan(cu.intra_mode, 2, 0) : SCAN_DIAG;
-    const int sc = intra ? intra_scan(cu.intra_mode, 2, 1) : SCAN_DIAG;
-    for (int q = 0; q < 4; q++) {
-        const int cb = (cu.tuc >> q) & 1, cr = (cu.tuc >> (4 + q)) & 1;
-        const bool split8 = (cu.tu >> q) & 1;
-        w.ctx(CTX_SPLIT_TF + 2, split8);   // log2 3
-        if (cbf_cb) w.ctx(CTX_CBF_CHROMA + 1, cb);
-        if (cbf_cr) w.ctx(CTX_CBF_CHROMA + 1, cr);
-        if (!split8) {
-            const int cy = (cu.ycbf >> (4 * q)) & 1;
-            w.ctx(CTX_CBF_LUMA + 0, cy);
-            if (cy) code_residual(w, coef + 64 * q, 3, 0, sy);
-        } else {
-            for (int j = 0; j < 4; j++) {   // depth 2: chroma of the node after the last 4x4 (blkIdx 3)
-                const int cy = (cu.ycbf >> (4 * q + j)) & 1;
-                w.ctx(CTX_CBF_LUMA + 0, cy);
-                if (cy) code_residual(w, coef + 64 * q + 16 * j, 2, 0, s4, (cu.tsy >> (4 * q + j)) & 1);
-            }
-        }
-        if (cb) code_residual(w, coef + kCoefCb + 16 * q, 2, 1, sc, (cu.tsc >> q) & 1);
-        if (cr) code_residual(w, coef + kCoefCr + 16 * q, 2, 2, sc, (cu.tsc >> (4 + q)) & 1);
-    }
+    code_tt16(w, cu, coef, intra, 0, 1, 1);
 }
 
 // ---------------------------------------------------------------------------
-// Deblocking (8.7.2), for this coding structure: CU = PU = 16x16 with 16x16 or 8x8 TUs,
-// so the filtered luma edges are the CU boundaries and the inner TU edges of split CUs
-// (the 8x8 grid), with a boundary strength per 4-sample segment (the TUs on its two
-// sides), and the chroma edges (bS 2 only) are the CU boundaries on the 8-sample chroma
-// grid (inner TU edges fall on chroma 4). Edges at the picture border and between
-// slices (pps_loop_filter_across_slices_enabled_flag = 0) are not filtered. All
-// vertical edges of the picture first, then the horizontal ones on their output.
+// Deblocking (8.7.2) for this coding structure: the luma edges on the 8x8 grid that are
+// transform or prediction block edges - unit boundaries (CU edges, or TU edges inside a
+// CU32 split into 16x16 nodes), the inner edges of split units (8x8 nodes, CU8s), and
+// inside a CU32 with one 32x32 TU only its PU edge (2NxN / Nx2N, bS from the motion) - with
+// a boundary strength per 4-sample segment, and the chroma edges (bS 2 only) on the
+// 8-sample chroma grid (unit boundaries between intra CUs). Edges at the picture border
+// and between slices (pps_loop_filter_across_slices_enabled_flag = 0) are not filtered.
+// All vertical edges of the picture first, then the horizontal ones on their output.
 SK_TABLE uint8_t HEVC_BETA[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
                                   8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
                                   34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};   // Table 8-11 beta'
 SK_TABLE uint8_t HEVC_TC[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  1,  1,  1,  1,  1,  1,  1, 1, 1,
                                 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
 
-// cbf_luma of the transform block covering luma sample (x, y) of the CU (0..15).
+// cbf_luma of the transform block covering luma sample (x, y) of the unit (0..15).
 SK_HD int tu_cbf_y(const CuInfo& c, int x, int y) { return (c.ycbf >> zorder4(x >> 2, y >> 2)) & 1; }
 // Boundary strength of an edge segment (8.7.2.4) between CUs p and q (the same CU for an
 // inner TU edge) whose luma transform blocks on the two sides have cbf pc / qc.
@@ -1145,47 +1533,58 @@ SK_HD void dbk_chroma_line(uint8_t* q, int step, int qp) {
 }
 
 // The whole picture (CPU reference; k_hevc_dbk_v / k_hevc_dbk_h are the same loops in
-// parallel). cus: [ctb_h][ctb_w]; m: the slice layout (edges between slices stay).
+// parallel). cus: [H16][W16] units; m: the slice layout (edges between slices stay).
 // One luma segment: the vertical (vert) or horizontal edge at luma position e (a
 // multiple of 8, > 0) of the picture, 4 samples long from position a along the edge.
-// Returns without filtering when the edge is an unsplit CU's inside or bS is 0.
-SK_HD void dbk_luma_edge(uint8_t* Y, int sy, const CuInfo* cus, int ctb_w, bool vert, int e, int a) {
+// Returns without filtering when the edge is no transform / prediction edge or bS is 0.
+SK_HD void dbk_luma_edge(uint8_t* Y, int sy, const CuInfo* cus, int W16, bool vert, int e, int a) {
     const int x = vert ? e : a, y = vert ? a : e;
-    const CuInfo& q = cus[(y >> 4) * ctb_w + (x >> 4)];
-    const CuInfo& p = vert ? cus[(y >> 4) * ctb_w + ((x - 1) >> 4)] : cus[((y - 1) >> 4) * ctb_w + (x >> 4)];
-    if ((e & 8) && !(q.tu & 16)) return;   // no transform edge inside an unsplit CU
-    const int pc = vert ? tu_cbf_y(p, (x - 1) & 15, y & 15) : tu_cbf_y(p, x & 15, (y - 1) & 15);
-    const int bs = dbk_bs(p, q, pc, tu_cbf_y(q, x & 15, y & 15));
+    const CuInfo& q = cus[(y >> 4) * W16 + (x >> 4)];
+    const CuInfo& p = vert ? cus[(y >> 4) * W16 + ((x - 1) >> 4)] : cus[((y - 1) >> 4) * W16 + (x >> 4)];
+    if ((e & 8) && !(q.tu & 16)) return;   // no transform edge inside an unsplit unit
+    int bs;
+    if ((e & 31) == 16 && (q.c32 & kC32) && (p.c32 & kC32)) {   // inside one CU32
+        if (q.c32 & kC32Tu) {   // one 32x32 TU: only the PU edge, motion only
+            if (c32_part(q) != (vert ? PART_Nx2N : PART_2NxN)) return;
+            bs = dbk_bs(p, q, 0, 0);
+        } else {
+            const int pc = vert ? tu_cbf_y(p, (x - 1) & 15, y & 15) : tu_cbf_y(p, x & 15, (y - 1) & 15);
+            bs = dbk_bs(p, q, pc, tu_cbf_y(q, x & 15, y & 15));
+        }
+    } else {
+        const int pc = vert ? tu_cbf_y(p, (x - 1) & 15, y & 15) : tu_cbf_y(p, x & 15, (y - 1) & 15);
+        bs = dbk_bs(p, q, pc, tu_cbf_y(q, x & 15, y & 15));
+    }
     if (bs) dbk_luma_segment(Y + (size_t)y * sy + x, vert ? 1 : sy, vert ? sy : 1, bs, (p.qp + q.qp + 1) >> 1);
 }
-SK_HD void deblock_picture(uint8_t* Y, uint8_t* U, uint8_t* V, int sy, int sc, const CuInfo* cus, int ctb_w,
-                           int ctb_h, const SliceMap& m) {
-    for (int x = 8; x < 16 * ctb_w; x += 8)   // vertical edges (not between slices)
-        for (int a = 0; a < 16 * ctb_h; a += 4) {
-            if (!(x & 8) && !m.same((x >> 4) - 1, a >> 4, x >> 4, a >> 4)) continue;
-            dbk_luma_edge(Y, sy, cus, ctb_w, true, x, a);
+SK_HD void deblock_picture(uint8_t* Y, uint8_t* U, uint8_t* V, int sy, int sc, const CuInfo* cus, int W16, int H16,
+                           const SliceMap& m) {
+    for (int x = 8; x < 16 * W16; x += 8)   // vertical edges (not between slices)
+        for (int a = 0; a < 16 * H16; a += 4) {
+            if (!(x & 8) && !m.same_u((x >> 4) - 1, a >> 4, x >> 4, a >> 4)) continue;
+            dbk_luma_edge(Y, sy, cus, W16, true, x, a);
         }
-    for (int cy = 0; cy < ctb_h; cy++)
-        for (int cx = 1; cx < ctb_w; cx++) {
-            const CuInfo &p = cus[cy * ctb_w + cx - 1], &q = cus[cy * ctb_w + cx];
+    for (int cy = 0; cy < H16; cy++)
+        for (int cx = 1; cx < W16; cx++) {
+            const CuInfo &p = cus[cy * W16 + cx - 1], &q = cus[cy * W16 + cx];
             if (p.mode != CU_INTRA && q.mode != CU_INTRA) continue;   // chroma: bS 2 only
-            if (!m.same(cx - 1, cy, cx, cy)) continue;
+            if (!m.same_u(cx - 1, cy, cx, cy)) continue;
             const int qp = (p.qp + q.qp + 1) >> 1;
             for (int l = 0; l < 8; l++) {
                 dbk_chroma_line(U + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
                 dbk_chroma_line(V + (size_t)(cy * 8 + l) * sc + cx * 8, 1, qp);
             }
         }
-    for (int y = 8; y < 16 * ctb_h; y += 8)   // horizontal edges (not between slices)
-        for (int a = 0; a < 16 * ctb_w; a += 4) {
-            if (!(y & 8) && !m.same(a >> 4, (y >> 4) - 1, a >> 4, y >> 4)) continue;
-            dbk_luma_edge(Y, sy, cus, ctb_w, false, y, a);
+    for (int y = 8; y < 16 * H16; y += 8)   // horizontal edges (not between slices)
+        for (int a = 0; a < 16 * W16; a += 4) {
+            if (!(y & 8) && !m.same_u(a >> 4, (y >> 4) - 1, a >> 4, y >> 4)) continue;
+            dbk_luma_edge(Y, sy, cus, W16, false, y, a);
         }
-    for (int cy = 1; cy < ctb_h; cy++)
-        for (int cx = 0; cx < ctb_w; cx++) {
-            const CuInfo &p = cus[(cy - 1) * ctb_w + cx], &q = cus[cy * ctb_w + cx];
+    for (int cy = 1; cy < H16; cy++)
+        for (int cx = 0; cx < W16; cx++) {
+            const CuInfo &p = cus[(cy - 1) * W16 + cx], &q = cus[cy * W16 + cx];
             if (p.mode != CU_INTRA && q.mode != CU_INTRA) continue;
-            if (!m.same(cx, cy - 1, cx, cy)) continue;
+            if (!m.same_u(cx, cy - 1, cx, cy)) continue;
             const int qp = (p.qp + q.qp + 1) >> 1;
             for (int l = 0; l < 8; l++) {
                 dbk_chroma_line(U + (size_t)(cy * 8) * sc + cx * 8 + l, sc, qp);

@@ -21,14 +21,18 @@
 namespace sk {
 namespace hevc {
 
+// Picture geometry: CTBs (32x32) and the 16x16 unit grid of the front end (its MBs).
 struct Geo {
-    int ctb_w = 0, ctb_h = 0, rows_per_slice = 0, num_slices = 0;
+    int ctb_w = 0, ctb_h = 0, rows_per_slice = 0, num_slices = 0;   // CTB counts, slices in CTB rows
+    int W16 = 0, H16 = 0;       // units
     int pic_w = 0, pic_h = 0;   // coded picture size (multiples of 16)
     int addr_bits = 0;          // slice_segment_address length
     void init(const h264::Geometry& g) {
-        ctb_w = g.mb_w;
-        ctb_h = g.mb_h;
-        rows_per_slice = g.rows_per_slice;
+        W16 = g.mb_w;
+        H16 = g.mb_h;
+        ctb_w = (W16 + 1) >> 1;
+        ctb_h = (H16 + 1) >> 1;
+        rows_per_slice = g.rows_per_slice >> 1;   // stripes are whole CTB rows (hevc_geometry)
         num_slices = g.num_slices;
         pic_w = g.stride_y;
         pic_h = g.plane_h_y;
@@ -37,7 +41,14 @@ struct Geo {
         while ((1 << addr_bits) < n) addr_bits++;
     }
     int ctbs() const { return ctb_w * ctb_h; }
+    int units() const { return W16 * H16; }
+    UnitGrid grid() const { return UnitGrid{W16, H16}; }
 };
+
+// Stripes (the front end's slices) of whole CTB rows: a multiple of 32 lines.
+inline void hevc_geometry(h264::EncoderConfig& f) {
+    f.stripe_height = f.stripe_height < 32 ? 32 : (f.stripe_height + 31) & ~31;
+}
 
 // CBR sessions code no scene-cut intra slices (as the AV1 encoder, av1_encoder.h
 // cbr_config): on a bitrate budget a slice recoded as intra costs more bits at the same
@@ -54,10 +65,11 @@ inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
     f.deblock = 0;
     f.num_refs = 1;
     cbr_config(f);
+    hevc_geometry(f);
     return f;
 }
 
-// Slices per CTB row of intra slices (SliceMap::K): ceil(ctb_w / kIntraSegCtbs);
+// Slices per CTB row of intra slices (SliceMap::K): ceil(ctb_w / kIntraSegCtbs) (CTB32s);
 // SK_HEVC_SEG_CTBS=<n> sets the segment width (tests exercise the split at small sizes),
 // SK_HEVC_SEG_CTBS=0 turns the split off (one slice per row band: RD A/B runs).
 inline int intra_seg_k(int ctb_w) {
@@ -73,14 +85,19 @@ void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<u
 void append_nal(std::vector<uint8_t>& out, int type, const uint8_t* rbsp, size_t n);
 
 // ---- shared CU-level helpers (CPU reference; the kernels mirror them) ----------
-// Linear intra reference array (see intra_substitute) of an n x n block at (x0, y0)
-// of `plane` for the whole CU (bottom-left never available), top-right when tr.
-void build_intra_ref(const uint8_t* plane, int stride, int x0, int y0, int n, bool left, bool top, bool tr,
-                     uint8_t* ref);
-// Same for any transform block, with the neighbour availability `avail` (AV_* bits).
+// Linear intra reference array (see intra_substitute) of an n x n block at (x0, y0) of
+// `plane` for a transform block with the neighbour availability `avail` (AV_* bits).
 void build_intra_ref_av(const uint8_t* plane, int stride, int x0, int y0, int n, int avail, uint8_t* ref);
 // Prediction of an n x n block for `mode` (cidx 0 luma / 1,2 chroma) from a raw reference.
 void intra_predict(const uint8_t* ref_raw, int log2n, int mode, int cidx, uint8_t* pred);
+
+// Per-CTB scratch of the inter coding: each unit's source and prediction rasters
+// (Y 16x16 | Cb 8x8 | Cr 8x8) and the RD cost of its 16x16 CU's residual tree.
+struct Cu32Work {
+    bool in[4];
+    uint8_t src[4][kCoefPerCu], pred[4][kCoefPerCu];
+    long long j[4];
+};
 
 class CpuHevcEncoder {
    public:
@@ -107,9 +124,9 @@ class CpuHevcEncoder {
 
     h264::CpuH264Encoder fe;   // front end (full-frame mode)
     Geo geo;
-    std::vector<CuInfo> cus;
-    std::vector<int16_t> coefs;        // kCoefPerCu per CU
-    std::vector<uint16_t> bins;        // kCuBinCap per CU
+    std::vector<CuInfo> cus;           // per unit
+    std::vector<int16_t> coefs;        // kCoefPerCu per unit
+    std::vector<uint16_t> bins;        // kCuBinCap per unit
     std::vector<int> bin_n;
     std::vector<SaoStats> sao_stats;   // 3 per CTB (Y, Cb, Cr)
     std::vector<SaoParams> sao_own, sao;   // per CTB: own decision, final (after merges)
@@ -122,6 +139,10 @@ class CpuHevcEncoder {
 
    private:
     void load_cu_src(int cx, int cy, uint8_t* y, uint8_t* u, uint8_t* v) const;
+    void put_unit_rec(int ux, int uy, const uint8_t* rec);   // a unit raster into the rec planes
+    template <class MV>
+    void cu32_decide(int c, int r, const Cu32Work& wk, int qp, int lam_boost, MV mv);
+    void code_unit_intra(int ux, int uy, int qp);            // closed-loop intra coding of one unit
 };
 
 }  // namespace hevc

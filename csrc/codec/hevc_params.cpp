@@ -102,12 +102,12 @@ void build_parameter_sets(int w, int h, int full_range, float fps, std::vector<u
         s.ue(1);              // sps_max_dec_pic_buffering_minus1
         s.ue(0);              // sps_max_num_reorder_pics
         s.ue(0);              // sps_max_latency_increase_plus1
-        s.ue(1);              // log2_min_luma_coding_block_size_minus3: 16x16
-        s.ue(0);              // log2_diff_max_min_luma_coding_block_size: CTB 16x16
+        s.ue(0);              // log2_min_luma_coding_block_size_minus3: 8x8 (intra CU8s)
+        s.ue(2);              // log2_diff_max_min_luma_coding_block_size: CTB 32x32
         s.ue(0);              // log2_min_luma_transform_block_size_minus2: 4x4
-        s.ue(2);              // log2_diff_max_min_luma_transform_block_size: 16x16
-        s.ue(2);              // max_transform_hierarchy_depth_inter: 16x16, 8x8 or 4x4 TUs
-        s.ue(2);              // max_transform_hierarchy_depth_intra
+        s.ue(3);              // log2_diff_max_min_luma_transform_block_size: 32x32
+        s.ue(3);              // max_transform_hierarchy_depth_inter: CU32 -> 32, 16, 8, 4
+        s.ue(2);              // max_transform_hierarchy_depth_intra (+1 under PART_NxN)
         s.put1(0);            // scaling_list_enabled_flag
         s.put1(0);            // amp_enabled_flag
         s.put1(1);            // sample_adaptive_offset_enabled_flag (hevc_sao.h)

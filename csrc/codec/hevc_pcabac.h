@@ -25,7 +25,7 @@ namespace sk {
 namespace hevc {
 
 constexpr uint32_t kPcModeled = 0x4000u;   // modelled context bin: bits 0..5 LPS state, bit 6 is-LPS
-constexpr int kPcCtxOff = 140;             // per-CU context offsets: CTX_COUNT + 1 entries, padded
+constexpr int kPcCtxOff = 144;             // per-CU context offsets: CTX_COUNT + 1 entries, padded
 static_assert(kPcCtxOff >= CTX_COUNT + 1 && kPcCtxOff % 4 == 0 && kPcCtxOff <= 192,
               "k_pc_sort: three counters per lane, 64 lanes");
 

@@ -29,6 +29,9 @@ using h264::gpu::FrameArgs;
 using h264::gpu::Planes;
 
 __device__ __forceinline__ int lane() { return threadIdx.x & 63; }
+__device__ __forceinline__ int nbm_of(bool left, bool top, bool tr) {
+    return (left ? AV_L : 0) | (top ? AV_T : 0) | (left && top ? AV_TL : 0) | (tr ? AV_TR : 0);
+}
 __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -394,8 +397,9 @@ __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     // candidate lists in LDS (dynamically indexed: private arrays would live in scratch);
     // every lane writes the same values
     int *mlx = L.mlx, *mly = L.mly, *px = L.px, *py = L.py;
-    merge_list(A1, B1, B0, B2, mlx, mly);
-    amvp_list(A1, B1, B0, B2, px, py);
+    const NbMv A0{false, 0, 0};
+    merge_list(A1, B1, B0, A0, B2, mlx, mly);
+    amvp_list(A0, A1, B0, B1, B2, px, py);
     wsync();
     const int mvx = h264::me_qx(f.me[idx]), mvy = h264::me_qy(f.me[idx]);   // quarter-pel (k_subpel)
     const int pic_w = f.stride_y, pic_h = f.mb_h * 16;
@@ -596,7 +600,7 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     load_src(L, f, cx, cy);
     for (int u = 0; u < 16; u++) {
         const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
-        tu_refs(nullptr, f.src.y, f.stride_y, cx * 16, cy * 16, 0, 4 * bx, 4 * by, 4, tu_avail_at(bx, by, 1, left, top, tr),
+        tu_refs(nullptr, f.src.y, f.stride_y, cx * 16, cy * 16, 0, 4 * bx, 4 * by, 4, tu_avail_at(bx, by, 1, nbm_of(left, top, tr)),
                 L.ref4[u]);
     }
     const int l = lane(), u = l >> 2, row = l & 3;
@@ -768,7 +772,7 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
     const Planes& P = f.rec;
     load_nb(L, P, f, cx, cy, left, top, tr);
     // (a) one 16x16 TU
-    const int avc = cu_avail(left, top, tr);
+    const int avc = cu_avail(nbm_of(left, top, tr));
     intra_tu_pred(L, nullptr, P, f, cx, cy, 0, 4, 0, 0, avc, mode);
     intra_tu_pred(L, nullptr, P, f, cx, cy, 1, 3, 0, 0, avc, mode);
     intra_tu_pred(L, nullptr, P, f, cx, cy, 2, 3, 0, 0, avc, mode);
@@ -779,7 +783,7 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
     long long jb = (long long)lam * kSplitRateHalf;
     int split8 = 0, c8 = 0, c4 = 0, tuc = 0, tsy = 0, tsc = 0;
     for (int q = 0; q < 4; q++) {
-        const int av = tu_avail(q, left, top, tr), ox = 8 * (q & 1), oy = 8 * (q >> 1), o8 = oy * 16 + ox;
+        const int av = tu_avail(q, nbm_of(left, top, tr)), ox = 8 * (q & 1), oy = 8 * (q >> 1), o8 = oy * 16 + ox;
         intra_tu_pred(L, W, P, f, cx, cy, 0, 3, ox, oy, av, mode);
         tu_batch(L, T, 2, o8, 3, 1, false, false, qp, true, lam, L.lev8 + 64 * q, L.rec4t, L.tj[1] + q, L.tf[1] + q);
         long long j4 = (long long)lam * kSplit8RateHalf;
@@ -788,14 +792,14 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
             if (reg) {   // registers (intra4x4_step)
                 long long jt;
                 int tsb;
-                const int f4 = intra4x4_step(L, T, W, bx, by, tu_avail_at(bx, by, 1, left, top, tr), mode, qp, lam,
+                const int f4 = intra4x4_step(L, T, W, bx, by, tu_avail_at(bx, by, 1, nbm_of(left, top, tr)), mode, qp, lam,
                                              L.lev4 + 16 * t4, &jt, &tsb);
                 tsy |= tsb << t4;
                 j4 += jt;
                 c4 |= f4 << t4;
                 continue;
             }
-            intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, left, top, tr), mode);
+            intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, nbm_of(left, top, tr)), mode);
             tu_batch(L, T, 2, o4, 2, 1, true, false, qp, true, lam, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4,
                      L.lev4t + 16 * t4, L.rec4, L.tj[3] + t4, L.tf[3] + t4);
             const int m = merge_ts(L, 2, o4, 1, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4, L.lev4t + 16 * t4, L.rec4,
@@ -987,7 +991,7 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A, int lpw) {
     const int cand_a = (left && A.cus[idx - 1].mode == CU_INTRA) ? A.cus[idx - 1].intra_mode : 1;
     BinBuf w{A.bins + (size_t)idx * kCuBinCap, 0};
     sao_bins(w, A.sao[idx], left, top);   // CTB-level SAO syntax (k_hevc_sao_row's decision)
-    code_cu(w, cu, A.coefs + (size_t)idx * kCoefPerCu, p_slice, skip_ctx, cand_a);
+    (void)skip_ctx; (void)cand_a; (void)p_slice; (void)cu;   // TODO CTB32
     const bool last_row = cy == t.first_row + t.num_rows - 1;
     if (m.split(cy)) {   // each row segment is a slice: end_of_slice_segment_flag at its end
         w.term(cx + 1 == m.x1(cy, m.seg(cx, cy)));

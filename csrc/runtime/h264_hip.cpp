@@ -41,7 +41,10 @@ class HipBackend : public EncoderBackend {
    public:
     HipBackend(const EncoderConfig& c, int device) : cfg_(c), device_(device) {
         if (cfg_.codec == 2) av1::cbr_config(cfg_);   // AV1 CBR as the CPU encoder (av1_encoder.h)
-        if (cfg_.codec == 1) hevc::cbr_config(cfg_);  // HEVC CBR: no scene-cut intra slices (hevc_encoder.h)
+        if (cfg_.codec == 1) {   // HEVC: CBR without scene-cut intra slices, stripes of whole CTB rows (hevc_encoder.h)
+            hevc::cbr_config(cfg_);
+            hevc::hevc_geometry(cfg_);
+        }
         g_.init(cfg_);
         ctl_.init(cfg_, g_);
         HIPCHECK(hipSetDevice(device_));

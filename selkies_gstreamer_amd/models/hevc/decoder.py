@@ -8,13 +8,14 @@ decoding, binarisations and context selection) and 8 (intra sample prediction wi
 reference substitution and filtering, merge / AMVP motion vector prediction, 8-tap
 luma and 4-tap chroma interpolation, scaling, inverse DCT/DST, reconstruction).
 
-Supported: Main 8-bit 4:2:0, any CTB/CB/TB sizes with quadtree splits, PART_2Nx2N
-CUs (intra and inter), I and P slices with one reference list, multiple slices,
-entropy_coding_sync (WPP) substreams. NotImplementedError for the rest (B slices,
-tiles, AMP/NxN partitions, PCM, transform skip, scaling lists, TMVP, long-term
-references, sign data hiding, cu_qp_delta). The deblocking filter (8.7.2) runs on the
-completed picture: transform / prediction block edges on the 8x8 grid, boundary
-strength, luma decisions and strong / normal filters, chroma on bS 2. Sample adaptive
+Supported: Main 8-bit 4:2:0, any CTB/CB/TB sizes with quadtree splits, intra
+PART_2Nx2N / PART_NxN CUs and inter PART_2Nx2N / 2NxN / Nx2N CUs, I and P slices with one
+reference list, multiple slices, entropy_coding_sync (WPP) substreams, transform skip.
+NotImplementedError for the rest (B slices, tiles, AMP and inter NxN partitions, PCM,
+scaling lists, TMVP, long-term references, sign data hiding, cu_qp_delta). The
+deblocking filter (8.7.2) runs on the completed picture: transform and prediction block
+edges on the 8x8 grid, boundary strength (the coefficient rule on transform edges only),
+luma decisions and strong / normal filters, chroma on bS 2. Sample adaptive
 offset (7.3.8.3 syntax, 8.7.3 band / edge offsets with the picture and slice boundary
 rules) then runs on the deblocked picture.
 
@@ -528,6 +529,8 @@ class HevcDecoder:
             # boundary, luma cbf of the transform block, QpY
             "ev": np.zeros((s.height // 4, s.width // 4), bool),
             "eh": np.zeros((s.height // 4, s.width // 4), bool),
+            "tev": np.zeros((s.height // 4, s.width // 4), bool),   # transform block edges
+            "teh": np.zeros((s.height // 4, s.width // 4), bool),
             "cbf": np.zeros((s.height // 4, s.width // 4), bool),
             "qp": np.zeros((s.height // 4, s.width // 4), np.int64),
             "dbk_slices": {},
@@ -861,65 +864,100 @@ class HevcDecoder:
             self.cur["mv"][y0 >> 2:(y0 + n) >> 2, x0 >> 2:(x0 + n) >> 2] = mv
             return
         intra = 1 if self.slice_type == 2 else self._dec("pred_mode_flag")
-        if not intra or log2 == s.log2_min_cb:
-            if not self._dec("part_mode", 0):
-                raise NotImplementedError("partitions other than 2Nx2N")
+        part = 0   # 0 2Nx2N, 1 2NxN, 2 Nx2N, 3 NxN (Table 7-10 order aside)
         if intra:
-            prev = self._dec("prev_intra_luma_pred_flag")
-            if prev:
-                mpm_idx = 0
-                if self.cabac.bypass():
-                    mpm_idx = 1 + self.cabac.bypass()
-            else:
-                rem = self.cabac.bypass_bits(5)
+            if log2 == s.log2_min_cb and not self._dec("part_mode", 0):
+                part = 3
+        elif not self._dec("part_mode", 0):
+            if log2 > s.log2_min_cb and s.amp:
+                raise NotImplementedError("AMP")
+            if log2 == s.log2_min_cb and log2 > 3:
+                raise NotImplementedError("inter NxN")
+            part = 1 if self._dec("part_mode", 1) else 2
+        if intra:
+            npu = 4 if part == 3 else 1
+            h = n // 2 if part == 3 else n
+            pus = [(x0 + (k & 1) * h, y0 + (k >> 1) * h) for k in range(npu)]
+            prev = [self._dec("prev_intra_luma_pred_flag") for _ in pus]
+            local = {}   # modes of this CU's PUs (z-scan available to the later ones, 6.4.1)
+            modes = []
+            for k, (xp, yp) in enumerate(pus):
+                if prev[k]:
+                    mpm_idx = 0
+                    if self.cabac.bypass():
+                        mpm_idx = 1 + self.cabac.bypass()
+                else:
+                    rem = self.cabac.bypass_bits(5)
+                # candidate list (8.4.2)
+                cands = []
+                for (xn, yn) in ((xp - 1, yp), (xp, yp - 1)):
+                    inside = x0 <= xn < x0 + n and y0 <= yn < y0 + n
+                    if inside:
+                        cands.append(local[(xn - x0) // h, (yn - y0) // h])
+                    elif not self._avail(x0, y0, xn, yn) or not self.cur["intra"][yn >> 2, xn >> 2]:
+                        cands.append(1)
+                    elif yn == yp - 1 and yn < ((yp >> s.log2_ctb) << s.log2_ctb):
+                        cands.append(1)
+                    else:
+                        cands.append(int(self.cur["ipm"][yn >> 2, xn >> 2]))
+                a, b = cands
+                if a == b:
+                    lst = [0, 1, 26] if a < 2 else [a, 2 + ((a + 29) % 32), 2 + ((a - 2 + 1) % 32)]
+                else:
+                    third = 0 if (a != 0 and b != 0) else (1 if (a != 1 and b != 1) else 26)
+                    lst = [a, b, third]
+                if prev[k]:
+                    mode = lst[mpm_idx]
+                else:
+                    mode = rem
+                    for c2 in sorted(lst):
+                        if mode >= c2:
+                            mode += 1
+                local[(xp - x0) // h, (yp - y0) // h] = mode
+                modes.append(mode)
             c = self._dec("intra_chroma_pred_mode")
             chroma = 4 if c == 0 else self.cabac.bypass_bits(2)
-            # candidate list (8.4.2)
-            cands = []
-            for (xn, yn) in ((x0 - 1, y0), (x0, y0 - 1)):
-                if not self._avail(x0, y0, xn, yn) or not self.cur["intra"][yn >> 2, xn >> 2]:
-                    cands.append(1)
-                elif yn == y0 - 1 and yn < ((y0 >> s.log2_ctb) << s.log2_ctb):
-                    cands.append(1)
-                else:
-                    cands.append(int(self.cur["ipm"][yn >> 2, xn >> 2]))
-            a, b = cands
-            if a == b:
-                lst = [0, 1, 26] if a < 2 else [a, 2 + ((a + 29) % 32), 2 + ((a - 2 + 1) % 32)]
-            else:
-                third = 0 if (a != 0 and b != 0) else (1 if (a != 1 and b != 1) else 26)
-                lst = [a, b, third]
-            if prev:
-                mode = lst[mpm_idx]
-            else:
-                srt = sorted(lst)
-                mode = rem
-                for c2 in srt:
-                    if mode >= c2:
-                        mode += 1
+            mode0 = modes[0]
             if chroma == 4:
-                cmode = mode
+                cmode = mode0
             else:
                 cmode = [0, 26, 10, 1][chroma]
-                if cmode == mode:
+                if cmode == mode0:
                     cmode = 34
             # decoded-ness (the slice map) is set per transform unit by _intra_pred, so a TU's
             # not-yet-decoded neighbours inside this CU stay unavailable
-            self._mark(x0, y0, n, intra=1, skip=0, depth=depth, ipm=mode)
+            self._mark(x0, y0, n, intra=1, skip=0, depth=depth)
+            for (xp, yp), mode in zip(pus, modes):
+                self._mark(xp, yp, h, ipm=mode)
             self.cur["mv"][y0 >> 2:(y0 + n) >> 2, x0 >> 2:(x0 + n) >> 2] = 0
-            self.cu_intra = (mode, cmode)
-            max_depth = s.max_th_intra
-            self._transform_tree(x0, y0, x0, y0, log2, 0, 0, True, max_depth, (1, 1))
+            self.cu_intra = (None, cmode)   # luma modes: per TU from the ipm map
+            self._transform_tree(x0, y0, x0, y0, log2, 0, 0, True, s.max_th_intra + (1 if part == 3 else 0), (1, 1),
+                                 intra_split=part == 3)
             return
-        merge = self._dec("merge_flag")
-        mv = self._prediction_unit(x0, y0, n, skip=False, merge=merge)
-        self._inter_pred(x0, y0, n, mv)
+        rects = {0: [(x0, y0, n, n)], 1: [(x0, y0, n, n // 2), (x0, y0 + n // 2, n, n // 2)],
+                 2: [(x0, y0, n // 2, n), (x0 + n // 2, y0, n // 2, n)]}[part]
+        merge0 = 0
+        for pi, (xp, yp, pw, ph) in enumerate(rects):
+            merge = self._dec("merge_flag")
+            if pi == 0:
+                merge0 = merge
+            mv = self._prediction_unit(xp, yp, pw, skip=False, merge=merge, ph=ph, part=part, pidx=pi)
+            self._inter_pred(xp, yp, pw, mv, ph)
+            self._mark(xp, yp, 0, slice=self.slice_addr)
+            sl = (slice(yp >> 2, (yp + ph) >> 2), slice(xp >> 2, (xp + pw) >> 2))
+            self.cur["slice"][sl] = self.slice_addr
+            self.cur["mv"][sl] = mv
+            if pi == 1:   # prediction block edge (8.7.2.4)
+                if part == 1:
+                    self.cur["eh"][yp >> 2, xp >> 2:(xp + pw) >> 2] = True
+                else:
+                    self.cur["ev"][yp >> 2:(yp + ph) >> 2, xp >> 2] = True
         self._mark(x0, y0, n, slice=self.slice_addr, intra=0, skip=0, depth=depth, ipm=1)
-        self.cur["mv"][y0 >> 2:(y0 + n) >> 2, x0 >> 2:(x0 + n) >> 2] = mv
-        root = 1 if merge else self._dec("rqt_root_cbf")
+        root = 1 if (merge0 and part == 0) else self._dec("rqt_root_cbf")
         if root:
             self.cu_intra = None
-            self._transform_tree(x0, y0, x0, y0, log2, 0, 0, False, s.max_th_inter, (1, 1))
+            self._transform_tree(x0, y0, x0, y0, log2, 0, 0, False, s.max_th_inter, (1, 1),
+                                 inter_split=s.max_th_inter == 0 and part != 0)
 
     # ---------------- inter ----------------
     def _mvd(self):
@@ -949,12 +987,16 @@ class HevcDecoder:
             return None
         return tuple(int(v) for v in self.cur["mv"][yn >> 2, xn >> 2])
 
-    def _merge_cands(self, x0, y0, n):
-        A1 = self._nb_motion(x0, y0, x0 - 1, y0 + n - 1)
-        B1 = self._nb_motion(x0, y0, x0 + n - 1, y0 - 1)
-        B0 = self._nb_motion(x0, y0, x0 + n, y0 - 1)
-        A0 = self._nb_motion(x0, y0, x0 - 1, y0 + n)
+    def _merge_cands(self, x0, y0, w, h, part=0, pidx=0):
+        A1 = self._nb_motion(x0, y0, x0 - 1, y0 + h - 1)
+        B1 = self._nb_motion(x0, y0, x0 + w - 1, y0 - 1)
+        B0 = self._nb_motion(x0, y0, x0 + w, y0 - 1)
+        A0 = self._nb_motion(x0, y0, x0 - 1, y0 + h)
         B2 = self._nb_motion(x0, y0, x0 - 1, y0 - 1)
+        if pidx == 1 and part == 2:   # 8.5.3.2.3: PART_Nx2N / 2NxN part 1 ignore A1 / B1
+            A1 = None
+        if pidx == 1 and part == 1:
+            B1 = None
         lst = []
         if A1 is not None:
             lst.append(A1)
@@ -975,11 +1017,11 @@ class HevcDecoder:
             zero_idx += 1
         return lst
 
-    def _amvp_cands(self, x0, y0, n):
-        A0 = self._nb_motion(x0, y0, x0 - 1, y0 + n)
-        A1 = self._nb_motion(x0, y0, x0 - 1, y0 + n - 1)
-        B0 = self._nb_motion(x0, y0, x0 + n, y0 - 1)
-        B1 = self._nb_motion(x0, y0, x0 + n - 1, y0 - 1)
+    def _amvp_cands(self, x0, y0, w, h):
+        A0 = self._nb_motion(x0, y0, x0 - 1, y0 + h)
+        A1 = self._nb_motion(x0, y0, x0 - 1, y0 + h - 1)
+        B0 = self._nb_motion(x0, y0, x0 + w, y0 - 1)
+        B1 = self._nb_motion(x0, y0, x0 + w - 1, y0 - 1)
         B2 = self._nb_motion(x0, y0, x0 - 1, y0 - 1)
         # single reference picture: every inter neighbour refers to it (no scaling)
         is_scaled = A0 is not None or A1 is not None   # availableA0 || availableA1 (6.4.2: inter only)
@@ -998,29 +1040,31 @@ class HevcDecoder:
             lst.append((0, 0))
         return lst[:2]
 
-    def _prediction_unit(self, x0, y0, n, skip, merge=1):
+    def _prediction_unit(self, x0, y0, n, skip, merge=1, ph=None, part=0, pidx=0):
+        h = n if ph is None else ph
         if skip or merge:
             idx = 0
             if self.max_merge > 1 and self._dec("merge_idx"):
                 idx = 1
                 while idx < self.max_merge - 1 and self.cabac.bypass():
                     idx += 1
-            return self._merge_cands(x0, y0, n)[idx]
+            return self._merge_cands(x0, y0, n, h, part, pidx)[idx]
         if self.num_ref > 1:
             raise NotImplementedError("ref_idx")
         mvd = self._mvd()
         mvp = self._dec("mvp_flag")
-        pred = self._amvp_cands(x0, y0, n)[mvp]
+        pred = self._amvp_cands(x0, y0, n, h)[mvp]
         mv = [(pred[i] + mvd[i] + (1 << 16)) % (1 << 16) for i in range(2)]
         return tuple(v - (1 << 16) if v >= (1 << 15) else v for v in mv)
 
-    def _inter_pred(self, x0, y0, n, mv):
+    def _inter_pred(self, x0, y0, n, mv, ph=None):
         if self.ref is None:
             raise BitstreamError("P slice without a reference picture")
         s = self.sps
+        hgt = n if ph is None else ph
         RY, RU, RV = (r.astype(np.int64) for r in self.ref)
         mvx, mvy = mv
-        ys = np.arange(n)[:, None]
+        ys = np.arange(hgt)[:, None]
         xs = np.arange(n)[None, :]
         xi, yi, fx, fy = x0 + (mvx >> 2), y0 + (mvy >> 2), mvx & 3, mvy & 3
 
@@ -1035,9 +1079,9 @@ class HevcDecoder:
         else:
             tmp = [sum(LUMA_FILTER[fx][i] * refl(xi + xs + i - 3, yi + ys + k - 3) for i in range(8)) for k in range(8)]
             pred = sum(LUMA_FILTER[fy][k] * tmp[k] for k in range(8)) >> 6
-        self.cur["Y"][y0:y0 + n, x0:x0 + n] = np.clip((pred + 32) >> 6, 0, 255)
-        m = n // 2
-        ys = np.arange(m)[:, None]
+        self.cur["Y"][y0:y0 + hgt, x0:x0 + n] = np.clip((pred + 32) >> 6, 0, 255)
+        m, mh = n // 2, hgt // 2
+        ys = np.arange(mh)[:, None]
         xs = np.arange(m)[None, :]
         xc0, yc0 = x0 // 2, y0 // 2
         xi, yi, fx, fy = xc0 + (mvx >> 3), yc0 + (mvy >> 3), mvx & 7, mvy & 7
@@ -1054,15 +1098,17 @@ class HevcDecoder:
                 tmp = [sum(CHROMA_FILTER[fx][i] * refc(xi + xs + i - 1, yi + ys + k - 1) for i in range(4))
                        for k in range(4)]
                 pred = sum(CHROMA_FILTER[fy][k] * tmp[k] for k in range(4)) >> 6
-            self.cur[plane][yc0:yc0 + m, xc0:xc0 + m] = np.clip((pred + 32) >> 6, 0, 255)
+            self.cur[plane][yc0:yc0 + mh, xc0:xc0 + m] = np.clip((pred + 32) >> 6, 0, 255)
 
     # ---------------- transform tree ----------------
-    def _transform_tree(self, x0, y0, xb, yb, log2, depth, blk, intra, max_depth, parent_cbf):
+    def _transform_tree(self, x0, y0, xb, yb, log2, depth, blk, intra, max_depth, parent_cbf, intra_split=False,
+                        inter_split=False):
         s = self.sps
-        if log2 <= s.log2_max_tb and log2 > s.log2_min_tb and depth < max_depth:
+        forced = (intra_split or inter_split) and depth == 0
+        if log2 <= s.log2_max_tb and log2 > s.log2_min_tb and depth < max_depth and not forced:
             split = self._dec("split_transform_flag", 5 - log2)
         else:
-            split = 1 if log2 > s.log2_max_tb else 0
+            split = 1 if (log2 > s.log2_max_tb or forced) else 0
         cbf_cb = cbf_cr = 0
         if log2 > 2:
             if depth == 0 or parent_cbf[0]:
@@ -1091,9 +1137,12 @@ class HevcDecoder:
         return QPC_TABLE[qpi]
 
     def _block_edges(self, x0, y0, n):
+        """Coding / transform block edges (left and top boundary of the block)."""
         c = self.cur
-        c["ev"][y0 >> 2:(y0 + n) >> 2, x0 >> 2] = True
-        c["eh"][y0 >> 2, x0 >> 2:(x0 + n) >> 2] = True
+        for k in ("ev", "tev"):
+            c[k][y0 >> 2:(y0 + n) >> 2, x0 >> 2] = True
+        for k in ("eh", "teh"):
+            c[k][y0 >> 2, x0 >> 2:(x0 + n) >> 2] = True
 
     def _transform_unit(self, x0, y0, xb, yb, log2, blk, cbf_y, cbf_cb, cbf_cr, intra):
         p = self.pps
@@ -1102,6 +1151,7 @@ class HevcDecoder:
         self._mark(x0, y0, n, cbf=bool(cbf_y))
         mode, cmode = self.cu_intra if intra else (None, None)
         if intra:
+            mode = int(self.cur["ipm"][y0 >> 2, x0 >> 2])   # the PU covering this TU
             self._intra_pred("Y", x0, y0, n, mode, 0)
         if cbf_y:
             self._residual(x0, y0, log2, 0, mode, self.qp)
@@ -1402,6 +1452,7 @@ def _deblock_pass(c: dict, planes: tuple, vertical: bool, slices: dict) -> None:
     independent: 8 samples apart, at most 3 samples changed per side)."""
     Y, U, V = planes
     edge = c["ev"] if vertical else c["eh"]
+    tedge = c["tev"] if vertical else c["teh"]
     sl, intra, cbf, mv, qp = c["slice"], c["intra"], c["cbf"], c["mv"], c["qp"]
     h4, w4 = edge.shape
     yq, xq = np.nonzero(edge)
@@ -1414,7 +1465,7 @@ def _deblock_pass(c: dict, planes: tuple, vertical: bool, slices: dict) -> None:
     across = np.array([bool(slices.get(int(a), (True, 0, 0, False))[3]) for a in sq], bool)
     ok &= (sq == sp) | across
     bs = np.where(intra[yq, xq] | intra[yp, xp], 2,
-                  np.where(cbf[yq, xq] | cbf[yp, xp], 1,
+                  np.where(tedge[yq, xq] & (cbf[yq, xq] | cbf[yp, xp]), 1,
                            np.where((np.abs(mv[yq, xq] - mv[yp, xp]) >= 4).any(axis=-1), 1, 0)))
     bs = np.where(ok, bs, 0)
     qpl = (qp[yq, xq] + qp[yp, xp] + 1) >> 1

@@ -10,6 +10,9 @@ from selkies_gstreamer_amd.ops.native import HevcEncoder
 from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
 
 
+CUINFO = 40   # sizeof(hevc::CuInfo)
+
+
 def _rec_y(enc, W, H):
     pw = (W + 15) // 16 * 16
     return np.frombuffer(enc.debug_buffer("ref_y", np.uint8), np.uint8).reshape(-1, pw)[:H, :W]
@@ -77,8 +80,9 @@ def test_hevc_static_content_is_all_skip():
         assert np.array_equal(Y, _rec_y(enc, W, H))
         sizes.append(len(pk.data))
     assert max(sizes) < 60   # skip-all slices: a few bytes each
-    cus = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 24)
+    cus = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, CUINFO)
     assert (cus[:, 0] == 0).all()   # CU_SKIP
+    assert (cus[:, 22] & 1).all()   # complete CTBs: one skipped 32x32 CU each
     enc.close()
 
 
@@ -126,14 +130,14 @@ def test_hevc_directional_intra_modes():
     pk = enc.encode(f, 0)[0]
     Y = HevcDecoder().decode(pk.data[10:])[0][0]
     assert np.array_equal(Y, _rec_y(enc, W, H))
-    modes = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 24)[:, 3]
-    assert np.count_nonzero(~np.isin(modes, [0, 1, 10, 26])) > len(modes) // 2
+    modes = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, CUINFO)[:, 24:40]
+    assert np.count_nonzero(~np.isin(modes, [0, 1, 10, 26])) > modes.size // 2
     assert len(pk.data) < 7000, len(pk.data)
     assert psnr(Y, _luma(f)) > 45
 
 
 def _cus(enc):
-    c = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, 24)
+    c = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, CUINFO)
     tu = c[:, 6]
     tsy = c[:, 18].astype(np.int64) | (c[:, 19].astype(np.int64) << 8)
     return c[:, 0], tu, tsy, c[:, 20]
@@ -172,18 +176,18 @@ def test_hevc_transform_tree_tools():
 
 @pytest.mark.parametrize("kind", ["desktop", "motion", "noise"])
 def test_hevc_split_intra_slices(kind, monkeypatch):
-    """Intra slices cut every CTB row into slices (hevc_core.h SliceMap; 40 CTBs at
-    full size, 4 here via SK_HEVC_SEG_CTBS so a 320-wide picture splits 5 ways): mid-row
+    """Intra slices cut every CTB row into slices (hevc_core.h SliceMap; 20 CTBs of 32x32 at
+    full size, 2 here via SK_HEVC_SEG_CTBS so a 320-wide picture splits 5 ways): mid-row
     slice starts under entropy_coding_sync, no top neighbours, no deblocking or SAO
     across the cuts. The independent decoder returns the encoder's reconstruction
     bit-exactly for key frames and the P frames predicted from them, and the serial and
     chunk-parallel CABAC models agree on the split layout."""
-    monkeypatch.setenv("SK_HEVC_SEG_CTBS", "4")
+    monkeypatch.setenv("SK_HEVC_SEG_CTBS", "2")
     W, H = 320, 192
     res = _run(W, H, kind, 5, qp=27)
     key = res[0][0].data[10:]
     types = [(n[0] >> 1) & 63 for n in split_annexb(key)]
-    assert types[:3] == [32, 33, 34] and types[3:] == [19] * (12 * 5)   # 12 rows x 5 segments
+    assert types[:3] == [32, 33, 34] and types[3:] == [19] * (6 * 5)   # 6 CTB rows x 5 segments
     assert all(q > 30 for _, _, q in res)
     src = SyntheticDesktop(W, H, kind=kind)
     ref = HevcEncoder(W, H, backend="cpu", qp=27)
@@ -192,3 +196,39 @@ def test_hevc_split_intra_slices(kind, monkeypatch):
     for t in range(2):
         f = src.frame(t)
         assert [p.data for p in ref.encode(f, t)] == [p.data for p in par.encode(f, t)]
+
+
+def _structure(enc):
+    c = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, CUINFO)
+    c32, cu8 = c[:, 22], c[:, 21]
+    return {"cu32": int((c32 & 1).sum()) // 4, "tu32": int(((c32 & 9) == 9).sum()) // 4,
+            "2NxN": int(((c32 & 1) & (((c32 >> 1) & 3) == 1)).sum()) // 4,
+            "Nx2N": int(((c32 & 1) & (((c32 >> 1) & 3) == 2)).sum()) // 4,
+            "cu8": int(((cu8 >> 4) & 1).sum()), "nxn": int(sum(bin(int(v) & 15).count("1") for v in cu8 if v & 16))}
+
+
+@pytest.mark.parametrize("W,H,kind,qp", [(256, 144, "motion", 27), (200, 100, "desktop", 32), (336, 208, "motion", 22)])
+def test_hevc_coding_quadtree(W, H, kind, qp):
+    """CTB 32 coding quadtree (hevc_core.h): key frames use intra CU16s and CU8s with
+    PART_NxN (four 4x4 PUs, own modes and MPM lists), P frames 32x32 CUs with PART_2Nx2N /
+    2NxN / Nx2N over the unit motion field, under a 32x32 TU or a split root; picture sizes
+    with odd unit counts leave partial CTBs (split_cu_flag inferred). The independent
+    decoder returns the encoder's reconstruction (all planes) for every picture."""
+    src = SyntheticDesktop(W, H, kind=kind)
+    enc = HevcEncoder(W, H, backend="cpu", qp=qp, paint_qp=qp, use_paint_over=False, rate_control="cqp")
+    dec = HevcDecoder()
+    seen = {}
+    cw, pcw = (W + 1) // 2, (W + 15) // 16 * 8
+    for t in range(5):
+        pk = enc.encode(src.frame(t), t)[0]
+        Y, U, V = dec.decode(pk.data[10:])[0]
+        assert np.array_equal(Y, _rec_y(enc, W, H)), f"frame {t}"
+        for name, P in (("ref_u", U), ("ref_v", V)):
+            rec = np.frombuffer(enc.debug_buffer(name, np.uint8), np.uint8).reshape(-1, pcw)[:(H + 1) // 2, :cw]
+            assert np.array_equal(P, rec), (name, t)
+        for k, v in _structure(enc).items():
+            seen[k] = seen.get(k, 0) + v
+    for k in ("cu32", "tu32", "cu8", "nxn"):
+        assert seen[k] > 0, seen
+    assert seen["2NxN"] + seen["Nx2N"] > 0, seen
+
