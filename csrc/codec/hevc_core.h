@@ -672,6 +672,10 @@ SK_HD int intra_pred_sample(const uint8_t* ref, int n, int log2n, int mode, int 
 SK_TABLE int8_t HEVC_INTRA_ORDER[35] = {1,  0,  26, 10, 2,  3,  4,  5,  6,  7,  8,  9,  11, 12, 13, 14, 15, 16,
                                         17, 18, 19, 20, 21, 22, 23, 24, 25, 27, 28, 29, 30, 31, 32, 33, 34};
 SK_HD bool intra_mode_basic(int mode) { return mode <= 1 || mode == 10 || mode == 26; }
+// CU8 decision (hevc_cpu.cpp intra_decide, k_hevc_intra_prep): penalties of the split and
+// of PART_NxN in SAD units (x intra_lam_sad) for their extra signalling.
+SK_HD int intra_lam_sad(int qp) { return qp < 12 ? 1 : 1 << ((qp - 12) / 6); }
+constexpr int kPenSplit = 8, kPenNxN = 32;   // tuned on tools/rd_codecs.py content (open-loop SADs favour NxN)
 SK_HD int intra_mode_bias(int mode, int qp) {
     return intra_mode_basic(mode) ? 0 : 6 * (qp < 12 ? 1 : 1 << ((qp - 12) / 6));
 }
@@ -944,6 +948,31 @@ SK_HD int mvd_bits_est(int d) {   // abs_mvd coding cost estimate in bins (AMVP 
     return 3 + egk_bins((uint32_t)(a - 2), 1, &b);
 }
 
+
+// Merge / AMVP choice of a PU with vector (mvx, mvy) from its candidate lists (the first
+// merge candidate that equals it, else the AMVP predictor with the cheaper difference).
+SK_HD void pu_choose(CuInfo& cu, int mvx, int mvy, const int* mlx, const int* mly, const int* px, const int* py) {
+    int midx = -1;
+    for (int i = 0; i < kMaxMergeCand && midx < 0; i++)
+        if (mlx[i] == mvx && mly[i] == mvy) midx = i;
+    cu.mvx = (int16_t)mvx;
+    cu.mvy = (int16_t)mvy;
+    if (midx >= 0) {
+        cu.mode = CU_MERGE;
+        cu.merge_idx = (uint8_t)midx;
+        cu.mvp_idx = 0;
+        cu.mvdx = cu.mvdy = 0;
+    } else {
+        cu.mode = CU_AMVP;
+        cu.merge_idx = 0;
+        const int c0 = mvd_bits_est(mvx - px[0]) + mvd_bits_est(mvy - py[0]);
+        const int c1 = mvd_bits_est(mvx - px[1]) + mvd_bits_est(mvy - py[1]);
+        const int k = c1 < c0 ? 1 : 0;
+        cu.mvp_idx = (uint8_t)k;
+        cu.mvdx = (int16_t)(mvx - px[k]);
+        cu.mvdy = (int16_t)(mvy - py[k]);
+    }
+}
 
 // Encoder rate estimates of CU / PU syntax (half bits): the CU32 vs four-CU16 choice
 // (hevc_cpu.cpp cu32_decide and k_hevc_inter run the same rule).

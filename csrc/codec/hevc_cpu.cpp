@@ -309,31 +309,6 @@ static long long code_inter_residual(const uint8_t* sy, const uint8_t* su, const
     return ja;
 }
 
-// Merge / AMVP choice of a PU with vector (mvx, mvy) from its candidate lists (the first
-// merge candidate that equals it, else the AMVP predictor with the cheaper difference).
-static void pu_choose(CuInfo& cu, int mvx, int mvy, const int* mlx, const int* mly, const int* px, const int* py) {
-    int midx = -1;
-    for (int i = 0; i < kMaxMergeCand && midx < 0; i++)
-        if (mlx[i] == mvx && mly[i] == mvy) midx = i;
-    cu.mvx = (int16_t)mvx;
-    cu.mvy = (int16_t)mvy;
-    if (midx >= 0) {
-        cu.mode = CU_MERGE;
-        cu.merge_idx = (uint8_t)midx;
-        cu.mvp_idx = 0;
-        cu.mvdx = cu.mvdy = 0;
-    } else {
-        cu.mode = CU_AMVP;
-        cu.merge_idx = 0;
-        const int c0 = mvd_bits_est(mvx - px[0]) + mvd_bits_est(mvy - py[0]);
-        const int c1 = mvd_bits_est(mvx - px[1]) + mvd_bits_est(mvy - py[1]);
-        const int k = c1 < c0 ? 1 : 0;
-        cu.mvp_idx = (uint8_t)k;
-        cu.mvdx = (int16_t)(mvx - px[k]);
-        cu.mvdy = (int16_t)(mvy - py[k]);
-    }
-}
-
 void CpuHevcEncoder::put_unit_rec(int ux, int uy, const uint8_t* rec) {
     const h264::Geometry& g = fe.g;
     for (int y = 0; y < 16; y++) memcpy(&fe.rec[0][(size_t)(uy * 16 + y) * g.stride_y + ux * 16], rec + y * 16, 16);
@@ -401,11 +376,15 @@ void CpuHevcEncoder::cu32_decide(int c, int r, const Cu32Work& wk, int qp, int l
     }
     int16_t l32[kT32Coefs];
     long long j32 = 0;
-    const int qpc = chroma_qp(qp);
-    int cbf32 = code_tu_1(s32, p32, 5, qp, false, lam, l32, r32, &j32, false, false);
-    cbf32 |= code_tu_1(s32 + kT32Cb, p32 + kT32Cb, 4, qpc, false, lam, l32 + kT32Cb, r32 + kT32Cb, &j32, false, false) << 1;
-    cbf32 |= code_tu_1(s32 + kT32Cr, p32 + kT32Cr, 4, qpc, false, lam, l32 + kT32Cr, r32 + kT32Cr, &j32, false, false) << 2;
-    const bool tu32 = j32 < jsum;
+    int cbf32 = 0;
+    bool tu32 = false;
+    if (cbf_units) {   // the 32x32 TU is tried when some unit codes a residual (k_hevc_inter: same rule)
+        const int qpc = chroma_qp(qp);
+        cbf32 = code_tu_1(s32, p32, 5, qp, false, lam, l32, r32, &j32, false, false);
+        cbf32 |= code_tu_1(s32 + kT32Cb, p32 + kT32Cb, 4, qpc, false, lam, l32 + kT32Cb, r32 + kT32Cb, &j32, false, false) << 1;
+        cbf32 |= code_tu_1(s32 + kT32Cr, p32 + kT32Cr, 4, qpc, false, lam, l32 + kT32Cr, r32 + kT32Cr, &j32, false, false) << 2;
+        tu32 = j32 < jsum;
+    }
     const int root = tu32 ? cbf32 : cbf_units;
     const bool skip = part == PART_2Nx2N && pu[0].mode == CU_MERGE && !root;
     const long long jc = (long long)lam * cu32_hdr_half(part, pu[0], pu[1], skip) + (tu32 ? j32 : jsum);
@@ -499,8 +478,6 @@ void CpuHevcEncoder::code_slice_inter(int s) {
 // neighbours, gives the best mode of the 16x16 CU, of each 8x8 CU and of each 4x4 PU
 // (SAD + intra_mode_bias); four CU8s (each PART_2Nx2N or PART_NxN, the cheaper) replace the
 // CU16 when their total plus a split penalty is lower.
-SK_HD int intra_lam_sad(int qp) { return qp < 12 ? 1 : 1 << ((qp - 12) / 6); }
-constexpr int kPenSplit = 6, kPenNxN = 6;   // x intra_lam_sad: the CU8 split / NxN signalling
 void intra_decide(const uint32_t sad[16][35], int qp, CuInfo& cu) {
     const int lam = intra_lam_sad(qp);
     int best16 = 1, c16 = 0x7fffffff;

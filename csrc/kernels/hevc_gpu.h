@@ -13,18 +13,23 @@ namespace sk {
 namespace hevc {
 namespace gpu {
 
+// Geometry: f.mb_w x f.mb_h are the 16x16 units (the front end's macroblocks); the CTBs
+// (32x32) are cw x ch, slices rows_per_slice CTB rows (f.rows_per_slice is in units).
+// Per-unit arrays are indexed by unit (uy * mb_w + ux); the chunk-parallel coder's chunks
+// are the units of a CTB row in coding order (UnitGrid::chunk_unit).
 struct HevcArgs {
-    h264::gpu::FrameArgs f;     // planes, geometry (mb = CTB), tasks, motion field
-    CuInfo* cus;                // [ctbs]
-    int16_t* coefs;             // [ctbs][kCoefPerCu]
-    uint16_t* bins;             // [ctbs][kCuBinCap]
-    int* bin_n;                 // [ctbs]
-    uint8_t* sync;              // [ctb_h][CTX_COUNT] WPP context states at each row start
-    uint8_t* sub;               // [ctb_h][sub_stride] CABAC substreams (one per CTB row)
+    h264::gpu::FrameArgs f;     // planes, geometry (mb = unit), tasks, motion field
+    int cw, ch, rps;            // CTBs per row / column, CTB rows per slice
+    CuInfo* cus;                // [units]
+    int16_t* coefs;             // [units][kCoefPerCu]
+    uint16_t* bins;             // [units][kCuBinCap]
+    int* bin_n;                 // [units]
+    uint8_t* sync;              // [ch][CTX_COUNT] WPP context states at each row start
+    uint8_t* sub;               // [ch][sub_stride] CABAC substreams (one per CTB row)
     int sub_stride;
-    int* sub_size;              // [ctb_h] bytes
-    int* sub_esc;               // [ctb_h] bytes after emulation prevention
-    int* row_off;               // [ctb_h] byte offset of the row's substream inside its slice NAL
+    int* sub_size;              // [ch] bytes
+    int* sub_esc;               // [ch] bytes after emulation prevention
+    int* row_off;               // [ch] byte offset of the row's substream inside its slice NAL
     uint8_t* out_host;          // host-mapped slice slots [num_slices][out_slot]
     int* out_size;              // host-mapped [num_slices]: NAL bytes (> out_slot: in out_dev)
     uint8_t* out_dev;           // device fallback slots [num_slices][out_dev_slot]
@@ -32,16 +37,16 @@ struct HevcArgs {
     int addr_bits;
     unsigned long long* dbg;    // optional (SK_STAMPS): per CTB row [cycles, entries, bytes, 0]
     int reg_steps;              // k_hevc_intra: 4x4 TUs in registers (default; SK_HEVC_REG_STEPS=0: LDS batches)
-    // chunk-parallel substream coding (codec/hevc_pcabac.h), chunk = CTB
-    uint16_t* srt;              // [ctbs][kCuBinCap] the CTB's context bins sorted by context: index << 1 | bin
-    uint16_t* coff;             // [ctb_h][kPcCtxOff][ctb_w] start of each context's run in srt (last = count)
-    uint32_t* rmap;             // [ctbs][256] end range | shifts << 9, per start range 256..511
-    uint32_t* cu_t;             // [ctbs] stream bit offset of the CTB's chunk inside its row substream
-    uint16_t* cu_r;             // [ctbs] start range of the chunk
-    uint8_t* tail;              // [ctbs][2] the chunk's two bytes overlapping the next chunk
-    uint32_t* row_bits;         // [ctb_h] shifts of the whole row (T_f)
+    // chunk-parallel substream coding (codec/hevc_pcabac.h), chunk = unit
+    uint16_t* srt;              // [units][kCuBinCap] the unit's context bins sorted by context: index << 1 | bin
+    uint16_t* coff;             // [ch][kPcCtxOff][2 * mb_w] start of each context's run in srt, per chunk (last = count)
+    uint32_t* rmap;             // [units][256] end range | shifts << 9, per start range 256..511
+    uint32_t* cu_t;             // [units] stream bit offset of the unit's chunk inside its row substream
+    uint16_t* cu_r;             // [units] start range of the chunk
+    uint8_t* tail;              // [units][2] the chunk's two bytes overlapping the next chunk
+    uint32_t* row_bits;         // [ch] shifts of the whole row (T_f)
     // SAO (codec/hevc_sao.h) on the deblocked reconstruction
-    SaoStats* sao_stats;        // [ctbs][3] Y, Cb, Cr
+    SaoStats* sao_stats;        // [ctbs][3] Y, Cb, Cr (CTB = 32x32)
     SaoParams* sao_own;         // [ctbs] each CTB's own decision (k_hevc_sao_stats)
     long long* sao_cost;        // [ctbs] its cost
     long long* sao_md;          // [ctbs][kSaoMd] merge-candidate distortions (sao_merge_dists)
@@ -49,8 +54,8 @@ struct HevcArgs {
     h264::gpu::Planes sao_tmp;  // filtered samples of the CTBs SAO changes, copied back into f.rec
     // intra slices cut every CTB row into seg_k slices (SliceMap, hevc_core.h); the
     // substream arrays (sync, sub_size, sub_esc, row_off, row_bits) hold mb_h * seg_k
-    // slots (slot = cy * seg_k + k, k = 0 for whole rows); segment k of row cy codes its
-    // substream at sub + cy * sub_stride + x0 * kSubstreamCtbBytes + 64 * k
+    // slots (slot = cy * seg_k + k, k = 0 for whole rows); segment k of CTB row cy codes its
+    // substream at sub + cy * sub_stride + x0 * 4 * kSubstreamCtbBytes + 64 * k
     int seg_k;
 };
 

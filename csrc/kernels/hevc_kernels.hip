@@ -47,13 +47,17 @@ __device__ __forceinline__ int wsum(int v) {
 // (f.gate = the re-code flag); they return at once unless the frame overflowed.
 __device__ __forceinline__ bool second_pass_skipped(const FrameArgs& f) { return f.gate && *f.gate == 0; }
 
-// The picture's slice layout (hevc_core.h SliceMap) and the substream of a slot.
+// The picture's slice layout on the CTB grid (hevc_core.h SliceMap), its unit grid, and
+// the substream of a slot (CTB row cy, segment k).
 __device__ __forceinline__ SliceMap smap(const HevcArgs& A) {
-    return SliceMap{A.f.tasks, A.f.mb_w, A.f.rows_per_slice, A.seg_k};
+    return SliceMap{A.f.tasks, A.cw, A.rps, A.seg_k};
 }
+__device__ __forceinline__ UnitGrid ugrid(const HevcArgs& A) { return UnitGrid{A.f.mb_w, A.f.mb_h}; }
 __device__ __forceinline__ size_t sub_base(const HevcArgs& A, const SliceMap& m, int cy, int k) {
-    return (size_t)cy * A.sub_stride + (size_t)m.x0(cy, k) * kSubstreamCtbBytes + 64 * (size_t)k;
+    return (size_t)cy * A.sub_stride + (size_t)m.x0(cy, k) * 4 * kSubstreamCtbBytes + 64 * (size_t)k;
 }
+// The slice task of CTB row r.
+__device__ __forceinline__ const SliceTask& ctb_task(const HevcArgs& A, int r) { return A.f.tasks[r / A.rps]; }
 
 // Per-wave LDS working set of one CU. Sample rasters (src, pred, rec*) hold the CU's
 // 384 samples: Y 16x16 (pitch 16) | Cb 8x8 | Cr 8x8 (pitch 8).
@@ -72,7 +76,7 @@ struct CuLds {
     uint8_t ref[2][68];          // intra: the TU's reference samples (raw, [1 2 1]-filtered)
     uint8_t ref4[16][17];        // intra mode decision: the sixteen 4x4 blocks' references
     uint8_t nbt[3][33];          // intra: the row above the CU per component (x = -1 .. 2N - 1)
-    uint8_t nbl[3][16];          // intra: the column left of the CU (y = 0 .. N - 1)
+    uint8_t nbl[3][32];          // intra: the column left of the CU (y = 0 .. 2N - 1, below-left included)
     int mlx[kMaxMergeCand], mly[kMaxMergeCand], px[2], py[2];   // inter: merge / AMVP candidates
 };
 
@@ -271,7 +275,7 @@ __device__ __forceinline__ void store_rec(const uint8_t* rec, const FrameArgs& f
 // trees coded in parallel batches, then the RD choice. Levels to gcoef, the TU fields into
 // cu; returns the raster holding the chosen reconstruction.
 __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int16_t* gcoef, CuInfo& cu,
-                                         int lam_boost) {
+                                         int lam_boost, long long* Jout) {
     const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp + lam_boost);
     {   // Every coded TU costs at least lam * (kTuRateHalf + 5) (one level): when the CU's whole
         // prediction error is below that, every TU of every tree zeroes and the 16x16 tree wins
@@ -283,6 +287,7 @@ __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int1
         }
         const long long sse = wsum(e2);
         if (512 * sse < (long long)lam * (kTuRateHalf + 5)) {
+            *Jout = 512 * sse;
             for (int i = l; i < kCoefPerCu; i += 64) gcoef[i] = 0;
             cu.cbf = 0;
             cu.tu = cu.tuc = 0;
@@ -323,6 +328,7 @@ __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int1
         ly |= (j4 < j8) ? (c4 >> (4 * q)) & 15 : (c8 >> q) & 1;
     }
     if (js < ja && (ly | tuc)) {
+        *Jout = js;
         for (int i = l; i < 256; i += 64) {
             const int q = i >> 6;
             gcoef[i] = ((split8 >> q) & 1) ? L.lev4[i] : L.lev8[i];
@@ -347,6 +353,7 @@ __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int1
         wsync();
         return L.recS;
     }
+    *Jout = ja;
     for (int i = l; i < kCoefPerCu; i += 64) gcoef[i] = L.levA[i];
     cu.cbf = (uint8_t)cbfa;
     cu.tu = cu.tuc = 0;
@@ -358,125 +365,305 @@ __device__ const uint8_t* inter_residual(CuLds& L, const int8_t* T, int qp, int1
 }
 
 // ---------------------------------------------------------------------------
-// K6 inter (P slices) and skip-all slices: one wave per CU, 4 CUs per workgroup.
+// The 32x32 TU trial of a CU32 (hevc_cpu.cpp cu32_decide: code_tu_1 of the 32x32 luma TU
+// and the two 16x16 chroma TUs) on all 256 lanes of the CTB's workgroup, after the units'
+// CU16 coding: residual from the units' src / pred rasters, forward DCT (rows, columns),
+// quantisation, inverse, reconstruction and the RD zeroing, per TU. Storage overlays the
+// units' dead working sets: A and B (1536 ints each) and the levels (1536 int16) in 256-int
+// chunks of Lw[k].a.. (4 KB per unit), the reconstruction in the units' recA rasters.
+struct T32Acc {
+    int sse0[3], sse1[3], rate[3], nz[3];
+};
+static_assert(offsetof(CuLds, levct) + sizeof(int16_t) * 128 >= offsetof(CuLds, a) + 4096, "CuLds: 4 KB from a");
+__device__ __forceinline__ int* t32_chunk(CuLds* Lw, int c) { return reinterpret_cast<int*>(Lw[c >> 2].a) + (c & 3) * 256; }
+__device__ __forceinline__ int& t32_A(CuLds* Lw, int i) { return t32_chunk(Lw, i >> 8)[i & 255]; }
+__device__ __forceinline__ int& t32_B(CuLds* Lw, int i) { return t32_chunk(Lw, 6 + (i >> 8))[i & 255]; }
+__device__ __forceinline__ int16_t& t32_L(CuLds* Lw, int i) {
+    return reinterpret_cast<int16_t*>(t32_chunk(Lw, 12 + (i >> 9)))[i & 511];
+}
+// Logical element i (luma 32x32 raster | Cb 16x16 | Cr 16x16) -> unit z and its CU raster index.
+__device__ __forceinline__ void t32_where(int i, int* z, int* o) {
+    if (i < kT32Cb) {
+        const int y = i >> 5, x = i & 31;
+        *z = (x >> 4) | ((y >> 4) << 1);
+        *o = (y & 15) * 16 + (x & 15);
+    } else {
+        const int k = i >= kT32Cr, j = i - (k ? kT32Cr : kT32Cb), y = j >> 4, x = j & 15;
+        *z = (x >> 3) | ((y >> 3) << 1);
+        *o = 256 + 64 * k + (y & 7) * 8 + (x & 7);
+    }
+}
+__device__ __forceinline__ int t32_tu(int i) { return i < kT32Cb ? 0 : (i < kT32Cr ? 1 : 2); }
+__device__ int t32_res(CuLds* Lw, int i) {
+    int z, o;
+    t32_where(i, &z, &o);
+    return (int)Lw[z].src[o] - (int)Lw[z].pred[o];
+}
+// Returns the cbf bits; *J the trial's RD cost (every thread).
+__device__ int tu32_trial(CuLds* Lw, const int8_t* T32, int qp, int lam, T32Acc& acc, long long* J) {
+    const int t = threadIdx.x, qpc = chroma_qp(qp);
+    if (t < 3) acc.sse0[t] = acc.sse1[t] = acc.rate[t] = acc.nz[t] = 0;
+    __syncthreads();
+    auto M = [&](int log2n, int k, int m) { return (int)T32[(log2n == 5 ? k : 2 * k) * 32 + m]; };
+    // forward, rows: A[tu][y][u] = (sum_x M[u][x] res[y][x] + rnd) >> sh1
+    for (int i = t; i < kT32Coefs; i += 256) {
+        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
+        const int j = i - base, y = j >> log2n, u = j & (n - 1), sh1 = log2n - 1;
+        int sum = 0;
+        for (int x = 0; x < n; x++) sum += M(log2n, u, x) * t32_res(Lw, base + y * n + x);
+        t32_A(Lw, i) = (sum + (1 << (sh1 - 1))) >> sh1;
+        const int e = t32_res(Lw, i);
+        atomicAdd(&acc.sse0[tu], e * e);
+    }
+    __syncthreads();
+    // forward, columns + quantisation + dequantisation
+    for (int i = t; i < kT32Coefs; i += 256) {
+        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
+        const int j = i - base, v = j >> log2n, u = j & (n - 1), sh2 = log2n + 6, q = tu ? qpc : qp;
+        int sum = 0;
+        for (int y = 0; y < n; y++) sum += M(log2n, v, y) * t32_A(Lw, base + y * n + u);
+        const int lv = quant_level((sum + (1 << (sh2 - 1))) >> sh2, q, log2n, false);
+        t32_L(Lw, i) = (int16_t)lv;
+        t32_B(Lw, i) = dequant_level(lv, q, log2n);
+        if (lv) {
+            atomicAdd(&acc.rate[tu], level_rate_half(lv));
+            atomicOr(&acc.nz[tu], 1);
+        }
+    }
+    __syncthreads();
+    // inverse, columns: A = clip16((sum_j M[j][y] B[j][x] + 64) >> 7)
+    for (int i = t; i < kT32Coefs; i += 256) {
+        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
+        const int j = i - base, y = j >> log2n, x = j & (n - 1);
+        int sum = 0;
+        if (acc.nz[tu])
+            for (int k = 0; k < n; k++) sum += M(log2n, k, y) * t32_B(Lw, base + k * n + x);
+        t32_A(Lw, i) = sk_clip((sum + 64) >> 7, -32768, 32767);
+    }
+    __syncthreads();
+    // inverse, rows + reconstruction (into the units' recA)
+    for (int i = t; i < kT32Coefs; i += 256) {
+        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
+        const int j = i - base, y = j >> log2n, x = j & (n - 1);
+        int sum = 0;
+        for (int k = 0; k < n; k++) sum += M(log2n, k, x) * t32_A(Lw, base + y * n + k);
+        int z, o;
+        t32_where(i, &z, &o);
+        const int rv = sk_clip255((int)Lw[z].pred[o] + ((sum + 2048) >> 12));
+        Lw[z].recA[o] = (uint8_t)rv;
+        const int e = (int)Lw[z].src[o] - rv;
+        atomicAdd(&acc.sse1[tu], e * e);
+    }
+    __syncthreads();
+    long long jt = 0;
+    int cbf = 0, keep[3];
+    for (int tu = 0; tu < 3; tu++) {   // RD zeroing (code_tu_1's rule), every thread alike
+        const long long s0 = acc.sse0[tu], s1 = acc.sse1[tu];
+        const int rate = kTuRateHalf + acc.rate[tu];
+        int nz = acc.nz[tu];
+        if (nz && 512 * s0 <= 512 * s1 + (long long)lam * rate) nz = 0;
+        keep[tu] = nz;
+        cbf |= nz << tu;
+        jt += nz ? 512 * s1 + (long long)lam * rate : 512 * s0;
+    }
+    for (int i = t; i < kT32Coefs; i += 256) {   // zeroed TUs: no levels, reconstruction = prediction
+        if (keep[t32_tu(i)]) continue;
+        int z, o;
+        t32_where(i, &z, &o);
+        t32_L(Lw, i) = 0;
+        Lw[z].recA[o] = Lw[z].pred[o];
+    }
+    __syncthreads();
+    *J = jt;
+    return cbf;
+}
+
+// K6 inter (P slices) and skip-all slices: one workgroup per CTB, wave z = the CTB's unit
+// z. Phase 1: every unit as a 16x16 CU (merge / AMVP candidates of its z-scan neighbours
+// on the unit motion field, quarter-pel MC, the residual trees); phase 2 (the whole
+// workgroup): the CTB as one 32x32 CU instead, with a 32x32 TU trial
+// (hevc_cpu.cpp code_slice_inter + cu32_decide, the same decisions).
 __global__ __launch_bounds__(256) void k_hevc_inter(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
     __shared__ int8_t T[kTabT];
+    __shared__ int8_t T32[1024];
+    __shared__ long long jw[4];
+    __shared__ CuInfo cw4[4], pus[2];
+    __shared__ T32Acc acc;
     const FrameArgs& f = A.f;
-    CuLds& L = Lw[threadIdx.x >> 6];
-    const int n = f.mb_w * f.mb_h;
-    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const bool valid = idx < n;
-    const int cx = valid ? idx % f.mb_w : 0, cy = valid ? idx / f.mb_w : 0;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
-    const int l = lane();
-    if (valid && t.final_action == ACT_SKIPALL && l == 0) {
-        CuInfo z;
-        memset(&z, 0, sizeof(z));
-        z.mode = CU_SKIP;
-        z.qp = (uint8_t)t.qp;
-        A.cus[idx] = z;
+    const int w = threadIdx.x >> 6, l = lane();
+    const int c = blockIdx.x % A.cw, r = blockIdx.x / A.cw;
+    const UnitGrid ug = ugrid(A);
+    const SliceMap m = smap(A);
+    const int ux = 2 * c + (w & 1), uy = 2 * r + (w >> 1);
+    const bool inside = ug.inside(ux, uy);
+    const int idx = uy * f.mb_w + ux;
+    const SliceTask t = ctb_task(A, r);
+    if (t.final_action == ACT_SKIPALL) {   // block-uniform: skipped CU32 / CU16s (code_slice_skip)
+        if (inside && l == 0) {
+            CuInfo z;
+            memset(&z, 0, sizeof(z));
+            z.mode = CU_SKIP;
+            z.qp = (uint8_t)t.qp;
+            for (int i = 0; i < 16; i++) z.ipm[i] = 1;
+            if (ug.complete(c, r)) z.c32 = kC32;
+            A.cus[idx] = z;
+        }
+        return;
     }
-    const bool coded = valid && t.final_action == ACT_P;
-    if (!__syncthreads_or(coded)) return;
+    if (t.final_action != ACT_P) return;   // block-uniform
     load_t16(T);
+    for (int i = threadIdx.x; i < 1024; i += 256) T32[i] = HEVC_T32[i >> 5][i & 31];
     __syncthreads();
-    if (!coded) return;
     const int W = f.mb_w;
-    auto nb = [&](int ox, int oy, bool ok) {
-        NbMv m;
-        m.av = ok;
-        m.mvx = ok ? h264::me_qx(f.me[oy * W + ox]) : 0;
-        m.mvy = ok ? h264::me_qy(f.me[oy * W + ox]) : 0;
-        return m;
+    auto mvf = [&](int nx, int ny, int* x, int* y) {
+        *x = h264::me_qx(f.me[ny * W + nx]);
+        *y = h264::me_qy(f.me[ny * W + nx]);
     };
-    const bool top = cy > t.first_row;
-    const NbMv A1 = nb(cx - 1, cy, cx > 0), B1 = nb(cx, cy - 1, top);
-    const NbMv B0 = nb(cx + 1, cy - 1, top && cx + 1 < W), B2 = nb(cx - 1, cy - 1, top && cx > 0);
-    // candidate lists in LDS (dynamically indexed: private arrays would live in scratch);
-    // every lane writes the same values
-    int *mlx = L.mlx, *mly = L.mly, *px = L.px, *py = L.py;
-    const NbMv A0{false, 0, 0};
-    merge_list(A1, B1, B0, A0, B2, mlx, mly);
-    amvp_list(A0, A1, B0, B1, B2, px, py);
-    wsync();
-    const int mvx = h264::me_qx(f.me[idx]), mvy = h264::me_qy(f.me[idx]);   // quarter-pel (k_subpel)
-    const int pic_w = f.stride_y, pic_h = f.mb_h * 16;
-    load_src(L, f, cx, cy);
-    {   // luma MC (hevc_core.h luma_mc_sample, separable form): the 23x23 integer window
-        // into LDS (L.a as bytes, row pitch 24), horizontal 8-tap pass into L.b (23 rows x
-        // 16), vertical pass into pred (lane = row l >> 2, 4 columns). L.a / L.b are free
-        // until the residual batches.
-        const int fx = mvx & 3, fy = mvy & 3;
-        const int x0 = cx * 16 + (mvx >> 2) - 3, y0 = cy * 16 + (mvy >> 2) - 3;
-        uint8_t* win = reinterpret_cast<uint8_t*>(L.a);
-        int* hb = reinterpret_cast<int*>(L.lev8);   // 23 x 16 ints: L.lev8 .. L.lev4t are free too
-        for (int i = l; i < 23 * 23; i += 64) {
-            const int r = i / 23, c = i - r * 23;
-            win[r * 24 + c] = f.ref.y[(size_t)sk_clip(y0 + r, 0, pic_h - 1) * f.stride_y + sk_clip(x0 + c, 0, pic_w - 1)];
+    CuLds& L = Lw[w];
+    const int lam_boost = A.f.rc->lam_boost;
+    if (inside) {   // ---- phase 1 (wave-uniform)
+        const PuNb nb = pu_neighbours(ug, m, mvf, 16 * ux, 16 * uy, 16, 16 * ux, 16 * uy, 16, 16, 0);
+        // candidate lists in LDS (dynamically indexed: private arrays would live in scratch);
+        // every lane writes the same values
+        pu_merge_list(nb, PART_2Nx2N, 0, L.mlx, L.mly);
+        pu_amvp_list(nb, L.px, L.py);
+        wsync();
+        const int mvx = h264::me_qx(f.me[idx]), mvy = h264::me_qy(f.me[idx]);   // quarter-pel (k_subpel)
+        const int pic_w = f.stride_y, pic_h = f.mb_h * 16;
+        load_src(L, f, ux, uy);
+        {   // luma MC (hevc_core.h luma_mc_sample, separable form): the 23x23 integer window
+            // into LDS (L.a as bytes, row pitch 24), horizontal 8-tap pass into L.b (23 rows x
+            // 16), vertical pass into pred (lane = row l >> 2, 4 columns). L.a / L.b are free
+            // until the residual batches.
+            const int fx = mvx & 3, fy = mvy & 3;
+            const int x0 = ux * 16 + (mvx >> 2) - 3, y0 = uy * 16 + (mvy >> 2) - 3;
+            uint8_t* win = reinterpret_cast<uint8_t*>(L.a);
+            int* hb = reinterpret_cast<int*>(L.lev8);   // 23 x 16 ints: L.lev8 .. L.lev4t are free too
+            for (int i = l; i < 23 * 23; i += 64) {
+                const int rr = i / 23, cc = i - rr * 23;
+                win[rr * 24 + cc] =
+                    f.ref.y[(size_t)sk_clip(y0 + rr, 0, pic_h - 1) * f.stride_y + sk_clip(x0 + cc, 0, pic_w - 1)];
+            }
+            wsync();
+            for (int i = l; i < 23 * 16; i += 64) {
+                const uint8_t* wp = win + (i >> 4) * 24 + (i & 15);
+                int sm = (int)wp[3] << 6;
+                if (fx) {
+                    sm = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) sm += HEVC_LUMA_FILTER[fx][k] * (int)wp[k];
+                }
+                hb[i] = sm;
+            }
+            wsync();
+            const int y = l >> 2;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int x = 4 * (l & 3) + k;
+                int v = hb[(y + 3) * 16 + x];
+                if (fy) {
+                    v = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) v += HEVC_LUMA_FILTER[fy][j] * hb[(y + j) * 16 + x];
+                    v >>= 6;
+                }
+                L.pred[y * 16 + x] = (uint8_t)sk_clip255((v + 32) >> 6);
+            }
+            // chroma: lane -> component l >> 5, row (l >> 2) & 7, 2 columns
+            const int cc = l >> 5, rr = (l >> 2) & 7;
+            const uint8_t* plane = cc ? f.ref.v : f.ref.u;
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int x = 2 * (l & 3) + k;
+                L.pred[kCoefCb + cc * 64 + rr * 8 + x] = (uint8_t)chroma_mc_sample(
+                    plane, f.stride_c, f.stride_c, f.mb_h * 8, ux * 8 + x, uy * 8 + rr, mvx, mvy);
+            }
         }
         wsync();
-        for (int i = l; i < 23 * 16; i += 64) {
-            const uint8_t* w = win + (i >> 4) * 24 + (i & 15);
-            int s = (int)w[3] << 6;
-            if (fx) {
-                s = 0;
-#pragma unroll
-                for (int k = 0; k < 8; k++) s += HEVC_LUMA_FILTER[fx][k] * (int)w[k];
-            }
-            hb[i] = s;
-        }
-        wsync();
-        const int y = l >> 2;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int x = 4 * (l & 3) + k;
-            int v = hb[(y + 3) * 16 + x];
-            if (fy) {
-                v = 0;
-#pragma unroll
-                for (int j = 0; j < 8; j++) v += HEVC_LUMA_FILTER[fy][j] * hb[(y + j) * 16 + x];
-                v >>= 6;
-            }
-            L.pred[y * 16 + x] = (uint8_t)sk_clip255((v + 32) >> 6);
-        }
-        // chroma: lane -> component l >> 5, row (l >> 2) & 7, 2 columns
-        const int c = l >> 5, r = (l >> 2) & 7;
-        const uint8_t* plane = c ? f.ref.v : f.ref.u;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const int x = 2 * (l & 3) + k;
-            L.pred[kCoefCb + c * 64 + r * 8 + x] = (uint8_t)chroma_mc_sample(
-                plane, f.stride_c, f.stride_c, f.mb_h * 8, cx * 8 + x, cy * 8 + r, mvx, mvy);
+        CuInfo cu;
+        memset(&cu, 0, sizeof(cu));
+        long long J = 0;
+        const uint8_t* rec = inter_residual(L, T, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu, lam_boost, &J);
+        store_rec(rec, f, ux, uy);
+        if (l == 0) {
+            cu.qp = (uint8_t)t.qp;
+            pu_choose(cu, mvx, mvy, L.mlx, L.mly, L.px, L.py);
+            if (cu.mode == CU_MERGE && !cu.cbf) cu.mode = CU_SKIP;
+            for (int i = 0; i < 16; i++) cu.ipm[i] = 1;
+            A.cus[idx] = cu;
+            cw4[w] = cu;
+            jw[w] = J;
         }
     }
-    wsync();
-    CuInfo cu;
-    memset(&cu, 0, sizeof(cu));
-    const uint8_t* rec = inter_residual(L, T, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu, A.f.rc->lam_boost);
-    store_rec(rec, f, cx, cy);
-    if (l == 0) {
-        int midx = -1;
-        for (int i = 0; i < kMaxMergeCand && midx < 0; i++)
-            if (mlx[i] == mvx && mly[i] == mvy) midx = i;
-        cu.qp = (uint8_t)t.qp;
-        cu.mvx = (int16_t)mvx;
-        cu.mvy = (int16_t)mvy;
-        if (midx >= 0) {
-            cu.mode = cu.cbf ? CU_MERGE : CU_SKIP;
-            cu.merge_idx = (uint8_t)midx;
-        } else {
-            cu.mode = CU_AMVP;
-            const int c0 = mvd_bits_est(mvx - px[0]) + mvd_bits_est(mvy - py[0]);
-            const int c1 = mvd_bits_est(mvx - px[1]) + mvd_bits_est(mvy - py[1]);
-            const int k = c1 < c0 ? 1 : 0;
-            cu.mvp_idx = (uint8_t)k;
-            cu.mvdx = (int16_t)(mvx - px[k]);
-            cu.mvdy = (int16_t)(mvy - py[k]);
-        }
-        A.cus[idx] = cu;
+    __syncthreads();
+    if (!ug.complete(c, r)) return;   // ---- phase 2 (block-uniform from here)
+    int mx[4], my[4];
+    for (int z = 0; z < 4; z++) {
+        mx[z] = cw4[z].mvx;
+        my[z] = cw4[z].mvy;
     }
+    const int part = cu32_part(mx, my);
+    if (part < 0) return;
+    if (w == 0) {   // the PUs' merge / AMVP syntax (uniform values)
+        for (int pi = 0; pi < (part == PART_2Nx2N ? 1 : 2); pi++) {
+            int xp, yp, pw, ph;
+            pu_rect(part, pi, 32 * c, 32 * r, 32, &xp, &yp, &pw, &ph);
+            const PuNb nb = pu_neighbours(ug, m, mvf, 32 * c, 32 * r, 32, xp, yp, pw, ph, pi);
+            pu_merge_list(nb, part, pi, L.mlx, L.mly);
+            pu_amvp_list(nb, L.px, L.py);
+            wsync();
+            CuInfo p;
+            memset(&p, 0, sizeof(p));
+            const int z = pi == 0 ? 0 : 3;
+            pu_choose(p, mx[z], my[z], L.mlx, L.mly, L.px, L.py);
+            if (l == 0) pus[pi] = p;
+            wsync();
+        }
+        if (part == PART_2Nx2N && l == 0) pus[1] = pus[0];
+    }
+    __syncthreads();
+    const int lam = rd_lambda_q8(t.qp + lam_boost);
+    long long jsum = 0;
+    int hsplit = 0, cbf_units = 0;
+    for (int z = 0; z < 4; z++) {
+        jsum += jw[z];
+        hsplit += cu16_hdr_half(cw4[z]);
+        cbf_units |= cw4[z].cbf;
+    }
+    long long j32 = 0;
+    int cbf32 = 0;
+    bool tu32 = false;
+    if (cbf_units) {   // the 32x32 TU is tried when some unit codes a residual (cu32_decide)
+        cbf32 = tu32_trial(Lw, T32, t.qp, lam, acc, &j32);
+        tu32 = j32 < jsum;
+    }
+    const int root = tu32 ? cbf32 : cbf_units;
+    const bool skip = part == PART_2Nx2N && pus[0].mode == CU_MERGE && !root;
+    const long long jc = (long long)lam * cu32_hdr_half(part, pus[0], pus[1], skip) + (tu32 ? j32 : jsum);
+    const long long js = (long long)lam * hsplit + jsum;
+    if (jc >= js) return;
+    // the CU32 replaces the four CU16s: wave z rewrites unit z
+    CuInfo cu = cw4[w];
+    const CuInfo& p = pus[cu32_pu_of(part, w)];
+    cu.mode = skip ? CU_SKIP : p.mode;
+    cu.merge_idx = p.merge_idx;
+    cu.mvp_idx = p.mvp_idx;
+    cu.mvdx = p.mvdx;
+    cu.mvdy = p.mvdy;
+    cu.c32 = (uint8_t)(kC32 | (part << 1) | (tu32 ? kC32Tu : 0));
+    if (tu32) {
+        cu.cbf = (uint8_t)cbf32;
+        cu.tu = cu.tuc = 0;
+        cu.ycbf = (cbf32 & 1) ? 0xffff : 0;
+        cu.tsy = 0;
+        cu.tsc = 0;
+        int16_t* g = A.coefs + (size_t)idx * kCoefPerCu;
+        for (int i = l; i < kCoefPerCu; i += 64) g[i] = t32_L(Lw, w * kCoefPerCu + i);
+        store_rec(L.recA, f, ux, uy);
+    }
+    if (l == 0) A.cus[idx] = cu;
 }
 
 // ---------------------------------------------------------------------------
@@ -560,18 +747,20 @@ __device__ void intra_tu_pred(CuLds& L, const uint8_t* W, const Planes& P, const
     tu_pred(L, r, c, log2n, mode, o);
 }
 
-// The CU's outside neighbours (row above incl. the corner and the top-right CU's
-// bottom row, column left) of every component into L.nbt / L.nbl, once per CU: the
-// TU chain then reads its references from LDS only. Unavailable entries are never read.
-__device__ void load_nb(CuLds& L, const Planes& P, const FrameArgs& f, int cx, int cy, bool left, bool top, bool tr) {
-    for (int i = lane(); i < 99; i += 64) {
+// The unit's outside neighbours (row above incl. the corner and the top-right unit's
+// bottom row, column left incl. the below-left unit's right column) of every component
+// into L.nbt / L.nbl, once per unit: the TU chain then reads its references from LDS only.
+// nbm: the neighbour units' availability (AV_* bits); unavailable entries are never read.
+__device__ void load_nb(CuLds& L, const Planes& P, const FrameArgs& f, int cx, int cy, int nbm) {
+    for (int i = lane(); i < 147; i += 64) {
         int c, x, y;
         if (i < 33) { c = 0; x = i - 1; y = -1; }
         else if (i < 67) { c = 1 + (i - 33) / 17; x = (i - 33) % 17 - 1; y = -1; }
-        else if (i < 83) { c = 0; x = -1; y = i - 67; }
-        else { c = 1 + (i - 83) / 8; x = -1; y = (i - 83) % 8; }
+        else if (i < 99) { c = 0; x = -1; y = i - 67; }
+        else { c = 1 + (i - 99) / 16; x = -1; y = (i - 99) % 16; }
         const int cn = c ? 8 : 16;
-        const bool ok = y < 0 ? (x < 0 ? left && top : (x < cn ? top : tr)) : left;
+        const bool ok = y < 0 ? (x < 0 ? (nbm & AV_TL) != 0 : (x < cn ? (nbm & AV_T) != 0 : (nbm & AV_TR) != 0))
+                              : (y < cn ? (nbm & AV_L) != 0 : (nbm & AV_BL) != 0);
         if (!ok) continue;
         const uint8_t* pl = c == 0 ? P.y : (c == 1 ? P.u : P.v);
         const int stride = c ? f.stride_c : f.stride_y;
@@ -582,8 +771,9 @@ __device__ void load_nb(CuLds& L, const Planes& P, const FrameArgs& f, int cx, i
     wsync();
 }
 
-// Open-loop intra mode per CU of I slices (all CUs in parallel): the mode whose sixteen
-// 4x4 predictions from their source neighbours are closest (hevc_cpu.cpp pass 0).
+// Open-loop intra decision per unit of I slices (all units in parallel; hevc_cpu.cpp
+// intra_decide): lane = (4x4 block l >> 2, row l & 3); per mode the block / 8x8 / 16x16 SADs
+// by shuffles, the best mode of each, then CU16 against four CU8s (PART_2Nx2N / NxN).
 __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
@@ -593,35 +783,56 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
     const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (idx >= n) return;   // wave-uniform; no block barriers below
     const int cx = idx % f.mb_w, cy = idx / f.mb_w;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const SliceTask t = ctb_task(A, cy >> 1);
     if (t.final_action != ACT_I) return;
-    const SliceMap m = smap(A);
-    const bool left = m.left(cx, cy), top = m.top(cx, cy), tr = m.top_right(cx, cy);
+    const int nbm = unit_nbm(ugrid(A), smap(A), cx, cy);
     load_src(L, f, cx, cy);
     for (int u = 0; u < 16; u++) {
         const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
-        tu_refs(nullptr, f.src.y, f.stride_y, cx * 16, cy * 16, 0, 4 * bx, 4 * by, 4, tu_avail_at(bx, by, 1, nbm_of(left, top, tr)),
-                L.ref4[u]);
+        tu_refs(nullptr, f.src.y, f.stride_y, cx * 16, cy * 16, 0, 4 * bx, 4 * by, 4, tu_avail_at(bx, by, 1, nbm), L.ref4[u]);
     }
     const int l = lane(), u = l >> 2, row = l & 3;
     const int bx = (u & 1) | ((u >> 1) & 2), by = ((u >> 1) & 1) | ((u >> 2) & 2);
-    int best = 1, best_sad = 0x7fffffff;
-    for (int k = 0; k < 35; k++) {   // HEVC_INTRA_ORDER, SAD + intra_mode_bias
+    int b4 = 1, c4 = 0x7fffffff, b8 = 1, c8 = 0x7fffffff, b16 = 1, c16 = 0x7fffffff;
+    for (int k = 0; k < 35; k++) {   // HEVC_INTRA_ORDER, SAD + intra_mode_bias, first minimum wins
         const int m = HEVC_INTRA_ORDER[k];
         int sad = 0;
 #pragma unroll
         for (int x = 0; x < 4; x++)
             sad += sk_abs((int)L.src[(4 * by + row) * 16 + 4 * bx + x] - intra_pred_sample(L.ref4[u], 4, 2, m, 0, x, row));
-        sad = wsum(sad) + intra_mode_bias(m, t.qp);
-        if (sad < best_sad) { best_sad = sad; best = m; }
+        sad += __shfl_xor(sad, 1);
+        sad += __shfl_xor(sad, 2);    // the block
+        int s8 = sad + __shfl_xor(sad, 4);
+        s8 += __shfl_xor(s8, 8);      // the 8x8 quadrant
+        int s16 = s8 + __shfl_xor(s8, 16);
+        s16 += __shfl_xor(s16, 32);   // the unit
+        const int bias = intra_mode_bias(m, t.qp);
+        if (sad + bias < c4) { c4 = sad + bias; b4 = m; }
+        if (s8 + bias < c8) { c8 = s8 + bias; b8 = m; }
+        if (s16 + bias < c16) { c16 = s16 + bias; b16 = m; }
     }
-    if (l == 0) {
-        CuInfo cu;
-        memset(&cu, 0, sizeof(cu));
-        cu.mode = CU_INTRA;
-        cu.intra_mode = (uint8_t)best;
-        A.cus[idx] = cu;
+    const int lam = intra_lam_sad(t.qp);
+    int cn = c4 + __shfl_xor(c4, 4);
+    cn += __shfl_xor(cn, 8);
+    cn += kPenNxN * lam;
+    const int nxn_q = cn < c8 ? 1 : 0;
+    int cq = nxn_q ? cn : c8;
+    cq += __shfl_xor(cq, 16);
+    cq += __shfl_xor(cq, 32);
+    const int csplit = kPenSplit * lam + cq;
+    const bool split = csplit < c16;
+    CuInfo cu;
+    memset(&cu, 0, sizeof(cu));
+    cu.mode = CU_INTRA;
+    int nxn = 0;
+    for (int q = 0; q < 4; q++) nxn |= __shfl(nxn_q, 16 * q) << q;
+    for (int v = 0; v < 16; v++) {
+        const int m4 = __shfl(b4, 4 * v), m8 = __shfl(b8, 4 * v);
+        cu.ipm[v] = (uint8_t)(split ? (((nxn >> (v >> 2)) & 1) ? m4 : m8) : b16);
     }
+    cu.cu8 = (uint8_t)(split ? 16 | nxn : 0);
+    cu.intra_mode = cu.ipm[0];
+    if (l == 0) A.cus[idx] = cu;
 }
 
 __device__ __forceinline__ long long shfl64(long long v, int src) {
@@ -762,54 +973,66 @@ __device__ void intra_c4_pair(CuLds& L, const int8_t* T, uint8_t* W, int ox, int
     wsync();
 }
 
-// One intra CU (hevc_cpu.cpp code_slice_intra pass 1): the 16x16 TU against the split
-// tree, each 8x8 node's TU against its four 4x4 TUs (transform skip tried), every TU
-// predicted from the reconstruction before it. The committed split reconstruction lives
-// in L.recS. Levels to gcoef, fields into cu; returns the chosen reconstruction.
-__device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f, int cx, int cy, bool left, bool top,
-                                   bool tr, int mode, int qp, int16_t* gcoef, CuInfo& cu, bool reg) {
+// One intra unit (hevc_cpu.cpp code_unit_intra): a CU16 chooses the 16x16 TU against the
+// split tree, each 8x8 node's TU against its four 4x4 TUs (transform skip tried); a
+// CU8-split unit codes each CU8 with its own modes (PART_2Nx2N: 8x8 TU or four 4x4,
+// PART_NxN: four 4x4 TUs, one per PU); every TU is predicted from the reconstruction before
+// it. `ci` holds the modes (ipm) and the CU8 structure. The committed split reconstruction
+// lives in L.recS. Levels to gcoef, fields into cu; returns the chosen reconstruction.
+__device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f, int cx, int cy, int nbm,
+                                   const CuInfo& ci, int qp, int16_t* gcoef, CuInfo& cu, bool reg) {
     const int l = lane(), qpc = chroma_qp(qp), lam = rd_lambda_q8(qp);
     const Planes& P = f.rec;
-    load_nb(L, P, f, cx, cy, left, top, tr);
-    // (a) one 16x16 TU
-    const int avc = cu_avail(nbm_of(left, top, tr));
-    intra_tu_pred(L, nullptr, P, f, cx, cy, 0, 4, 0, 0, avc, mode);
-    intra_tu_pred(L, nullptr, P, f, cx, cy, 1, 3, 0, 0, avc, mode);
-    intra_tu_pred(L, nullptr, P, f, cx, cy, 2, 3, 0, 0, avc, mode);
-    tu_batch(L, T, 0, 0, 4, 1, false, false, qp, true, lam, L.levA, L.recA, L.tj[0], L.tf[0]);
-    tu_batch(L, T, 1, 0, 3, 2, false, false, qpc, true, lam, L.levA + kCoefCb, L.recA, L.tj[0] + 1, L.tf[0] + 1);
-    // (b) four nodes, reconstruction committed into W = L.recS
+    const bool cu8 = (ci.cu8 & 16) != 0;
+    load_nb(L, P, f, cx, cy, nbm);
+    // (a) one 16x16 TU (CU16 only)
+    long long ja = 0x7fffffffffffffffll;
+    if (!cu8) {
+        const int avc = cu_avail(nbm), m0 = ci.ipm[0];
+        intra_tu_pred(L, nullptr, P, f, cx, cy, 0, 4, 0, 0, avc, m0);
+        intra_tu_pred(L, nullptr, P, f, cx, cy, 1, 3, 0, 0, avc, m0);
+        intra_tu_pred(L, nullptr, P, f, cx, cy, 2, 3, 0, 0, avc, m0);
+        tu_batch(L, T, 0, 0, 4, 1, false, false, qp, true, lam, L.levA, L.recA, L.tj[0], L.tf[0]);
+        tu_batch(L, T, 1, 0, 3, 2, false, false, qpc, true, lam, L.levA + kCoefCb, L.recA, L.tj[0] + 1, L.tf[0] + 1);
+        ja = L.tj[0][0] + L.tj[0][1] + L.tj[0][2];
+    }
+    // (b) four nodes / CU8s, reconstruction committed into W = L.recS
     uint8_t* W = L.recS;
     long long jb = (long long)lam * kSplitRateHalf;
     int split8 = 0, c8 = 0, c4 = 0, tuc = 0, tsy = 0, tsc = 0;
     for (int q = 0; q < 4; q++) {
-        const int av = tu_avail(q, nbm_of(left, top, tr)), ox = 8 * (q & 1), oy = 8 * (q >> 1), o8 = oy * 16 + ox;
-        intra_tu_pred(L, W, P, f, cx, cy, 0, 3, ox, oy, av, mode);
-        tu_batch(L, T, 2, o8, 3, 1, false, false, qp, true, lam, L.lev8 + 64 * q, L.rec4t, L.tj[1] + q, L.tf[1] + q);
+        const int av = tu_avail(q, nbm), ox = 8 * (q & 1), oy = 8 * (q >> 1), o8 = oy * 16 + ox;
+        const int mq = ci.ipm[4 * q], nxn = cu8 && ((ci.cu8 >> q) & 1);
+        long long j8 = 0x7fffffffffffffffll;
+        if (!nxn) {
+            intra_tu_pred(L, W, P, f, cx, cy, 0, 3, ox, oy, av, mq);
+            tu_batch(L, T, 2, o8, 3, 1, false, false, qp, true, lam, L.lev8 + 64 * q, L.rec4t, L.tj[1] + q, L.tf[1] + q);
+            j8 = L.tj[1][q];
+        }
         long long j4 = (long long)lam * kSplit8RateHalf;
         for (int j = 0; j < 4; j++) {
             const int bx = 2 * (q & 1) + (j & 1), by = 2 * (q >> 1) + (j >> 1), t4 = 4 * q + j, o4 = 4 * by * 16 + 4 * bx;
+            const int m4 = ci.ipm[t4];
             if (reg) {   // registers (intra4x4_step)
                 long long jt;
                 int tsb;
-                const int f4 = intra4x4_step(L, T, W, bx, by, tu_avail_at(bx, by, 1, nbm_of(left, top, tr)), mode, qp, lam,
-                                             L.lev4 + 16 * t4, &jt, &tsb);
+                const int f4 = intra4x4_step(L, T, W, bx, by, tu_avail_at(bx, by, 1, nbm), m4, qp, lam, L.lev4 + 16 * t4,
+                                             &jt, &tsb);
                 tsy |= tsb << t4;
                 j4 += jt;
                 c4 |= f4 << t4;
                 continue;
             }
-            intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, nbm_of(left, top, tr)), mode);
+            intra_tu_pred(L, W, P, f, cx, cy, 0, 2, 4 * bx, 4 * by, tu_avail_at(bx, by, 1, nbm), m4);
             tu_batch(L, T, 2, o4, 2, 1, true, false, qp, true, lam, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4,
                      L.lev4t + 16 * t4, L.rec4, L.tj[3] + t4, L.tf[3] + t4);
-            const int m = merge_ts(L, 2, o4, 1, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4, L.lev4t + 16 * t4, L.rec4,
-                                   L.tj[3] + t4, L.tf[3] + t4);
-            tsy |= m << t4;
+            const int mm = merge_ts(L, 2, o4, 1, L.lev4 + 16 * t4, W, L.tj[2] + t4, L.tf[2] + t4, L.lev4t + 16 * t4, L.rec4,
+                                    L.tj[3] + t4, L.tf[3] + t4);
+            tsy |= mm << t4;
             j4 += L.tj[2][t4];
             c4 |= L.tf[2][t4] << t4;
         }
-        const long long j8 = L.tj[1][q];
-        c8 |= L.tf[1][q] << q;
+        if (!nxn) c8 |= L.tf[1][q] << q;
         if (j4 < j8) {
             split8 |= 1 << q;
             jb += j4;
@@ -819,38 +1042,37 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
             jb += j8;
             wsync();
         }
-        // the node's Cb and Cr 4x4 TUs (slots q, q + 4)
+        // the node's Cb and Cr 4x4 TUs (slots q, q + 4), the CU8's / CU16's chroma mode
         if (reg) {   // registers (intra_c4_pair)
             int fcc[2], tcc[2];
             long long jcc[2];
-            intra_c4_pair(L, T, W, ox / 2, oy / 2, av, mode, qpc, lam, L.levc + 16 * q, fcc, jcc, tcc);
+            intra_c4_pair(L, T, W, ox / 2, oy / 2, av, mq, qpc, lam, L.levc + 16 * q, fcc, jcc, tcc);
 #pragma unroll
-            for (int c = 0; c < 2; c++) {
-                const int t = q + 4 * c;
-                tsc |= tcc[c] << t;
-                jb += jcc[c];
-                tuc |= fcc[c] << t;
+            for (int cc = 0; cc < 2; cc++) {
+                const int t = q + 4 * cc;
+                tsc |= tcc[cc] << t;
+                jb += jcc[cc];
+                tuc |= fcc[cc] << t;
             }
             continue;
         }
         const int ocb = kCoefCb + (oy / 2) * 8 + ox / 2;
-        intra_tu_pred(L, W, P, f, cx, cy, 1, 2, ox / 2, oy / 2, av, mode);
-        intra_tu_pred(L, W, P, f, cx, cy, 2, 2, ox / 2, oy / 2, av, mode);
+        intra_tu_pred(L, W, P, f, cx, cy, 1, 2, ox / 2, oy / 2, av, mq);
+        intra_tu_pred(L, W, P, f, cx, cy, 2, 2, ox / 2, oy / 2, av, mq);
         int16_t* lc = L.levct + 64;   // scratch pair: Cb / Cr levels of this node (compact), copied below
         int16_t* lct = L.levct + 96;
         tu_batch(L, T, 3, ocb, 2, 2, false, false, qpc, true, lam, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4,
                  L.tj[5] + 8, L.tf[5] + 8);
         const int mc = merge_ts(L, 3, ocb, 2, lc, W, L.tj[4] + 8, L.tf[4] + 8, lct, L.rec4, L.tj[5] + 8, L.tf[5] + 8);
         for (int i = l; i < 32; i += 64) L.levc[16 * (q + 4 * (i >> 4)) + (i & 15)] = lc[i];
-        for (int c = 0; c < 2; c++) {
-            const int t = q + 4 * c;
-            tsc |= ((mc >> c) & 1) << t;
-            jb += L.tj[4][8 + c];
-            tuc |= L.tf[4][8 + c] << t;
+        for (int cc = 0; cc < 2; cc++) {
+            const int t = q + 4 * cc;
+            tsc |= ((mc >> cc) & 1) << t;
+            jb += L.tj[4][8 + cc];
+            tuc |= L.tf[4][8 + cc] << t;
         }
         wsync();
     }
-    const long long ja = L.tj[0][0] + L.tj[0][1] + L.tj[0][2];
     if (jb < ja) {
         for (int i = l; i < 256; i += 64) gcoef[i] = ((split8 >> (i >> 6)) & 1) ? L.lev4[i] : L.lev8[i];
         for (int i = l; i < 128; i += 64) gcoef[kCoefCb + i] = L.levc[i];
@@ -877,8 +1099,32 @@ __device__ const uint8_t* intra_cu(CuLds& L, const int8_t* T, const FrameArgs& f
     return L.recA;
 }
 
+// Codes intra unit (ux, uy) (its decisions from k_hevc_intra_prep) and commits it.
+__device__ void intra_unit(const HevcArgs& A, CuLds& L, const int8_t* T, int ux, int uy, int qp) {
+    const FrameArgs& f = A.f;
+    const int idx = uy * f.mb_w + ux, l = lane();
+    const int nbm = unit_nbm(ugrid(A), smap(A), ux, uy);
+    CuInfo cu = A.cus[idx];   // mode, cu8, ipm from k_hevc_intra_prep
+    load_src(L, f, ux, uy);
+    wsync();
+    const uint8_t* rec = intra_cu(L, T, f, ux, uy, nbm, cu, qp, A.coefs + (size_t)idx * kCoefPerCu, cu, A.reg_steps != 0);
+    store_rec(rec, f, ux, uy);
+    if (l == 0) {
+        cu.qp = (uint8_t)qp;
+        A.cus[idx] = cu;
+        f.me[idx].mvx = 0;
+        f.me[idx].mvy = 0;
+        f.me[idx].ref = 0;
+        f.me[idx].fx = f.me[idx].fy = 0;
+    }
+    // this unit's reconstruction (global memory) is the next one's neighbour
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    wsync();
+}
+
 // I slices: one workgroup per slice, wave w = CTB row w of the slice, CTB x coded at
-// step x + 2w (the top-right CTB is one step older: WPP / intra availability order).
+// step x + 2w (the top-right CTB is one step older: WPP / intra availability order), its
+// units in z order.
 template <int MAXR>
 __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
@@ -889,90 +1135,55 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
     if (t.final_action != ACT_I || A.seg_k > 1) return;   // block-uniform; split rows: k_hevc_intra_seg
     load_t16(T);
     __syncthreads();
-    const int w = threadIdx.x >> 6, l = lane();
+    const int w = threadIdx.x >> 6;
     CuLds& L = Lw[w];
-    const int rows = t.num_rows, steps = f.mb_w + 2 * (rows - 1);
-    const int cy = t.first_row + w;
+    const UnitGrid ug = ugrid(A);
+    const int r0 = t.first_row >> 1, rows = ((t.first_row + t.num_rows + 1) >> 1) - r0;
+    const int steps = A.cw + 2 * (rows - 1);
+    const int r = r0 + w;
     __builtin_amdgcn_s_setprio(3);
     for (int step = 0; step < steps; step++) {
-        const int cx = step - 2 * w;
-        if (w < rows && cx >= 0 && cx < f.mb_w) {
-            const int idx = cy * f.mb_w + cx;
-            const bool left = cx > 0, top = cy > t.first_row, tr = top && cx + 1 < f.mb_w;
-            const int mode = __builtin_amdgcn_readfirstlane(A.cus[idx].intra_mode);
-            load_src(L, f, cx, cy);
-            wsync();
-            CuInfo cu;
-            memset(&cu, 0, sizeof(cu));
-            const uint8_t* rec = intra_cu(L, T, f, cx, cy, left, top, tr, mode, t.qp, A.coefs + (size_t)idx * kCoefPerCu, cu,
-                                          A.reg_steps != 0);
-            store_rec(rec, f, cx, cy);
-            if (l == 0) {
-                cu.mode = CU_INTRA;
-                cu.intra_mode = (uint8_t)mode;
-                cu.qp = (uint8_t)t.qp;
-                A.cus[idx] = cu;
-                f.me[idx].mvx = 0;
-                f.me[idx].mvy = 0;
-                f.me[idx].ref = 0;
-                f.me[idx].fx = f.me[idx].fy = 0;
+        const int c = step - 2 * w;
+        if (w < rows && c >= 0 && c < A.cw)
+            for (int z = 0; z < 4; z++) {
+                const int ux = 2 * c + (z & 1), uy = 2 * r + (z >> 1);
+                if (ug.inside(ux, uy)) intra_unit(A, L, T, ux, uy, t.qp);
             }
-        }
         __syncthreads();   // this step's reconstruction is visible to the next step's neighbours
     }
 }
 
 // I slices cut into row segments (SliceMap, seg_k > 1): one wave per segment, its CTBs
-// left to right; no top neighbours, so the segments of all rows run at once (a 4K key
-// frame: 810 chains of 40 CTBs instead of 34 workgroups of 246 steps).
+// left to right (units in z order); no top neighbours, so the segments of all rows run at
+// once (a 4K key frame: 408 chains of 80 units instead of 34 workgroups of 124 steps).
 __global__ __launch_bounds__(256) void k_hevc_intra_seg(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
     __shared__ int8_t T[kTabT];
-    const FrameArgs& f = A.f;
     load_t16(T);
     __syncthreads();   // the only block barrier: waves run independent segments below
-    const int w = threadIdx.x >> 6, l = lane();
+    const int w = threadIdx.x >> 6;
     const int slot = blockIdx.x * 4 + w;
-    if (slot >= f.mb_h * A.seg_k) return;
+    if (slot >= A.ch * A.seg_k) return;
     const SliceMap m = smap(A);
-    const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
-    if (!m.split(cy)) return;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const int r = slot / A.seg_k, k = slot - r * A.seg_k;
+    if (!m.split(r)) return;
+    const SliceTask t = ctb_task(A, r);
+    const UnitGrid ug = ugrid(A);
     CuLds& L = Lw[w];
     __builtin_amdgcn_s_setprio(3);
-    for (int cx = m.x0(cy, k); cx < m.x1(cy, k); cx++) {
-        const int idx = cy * f.mb_w + cx;
-        const bool left = m.left(cx, cy);
-        const int mode = __builtin_amdgcn_readfirstlane(A.cus[idx].intra_mode);
-        load_src(L, f, cx, cy);
-        wsync();
-        CuInfo cu;
-        memset(&cu, 0, sizeof(cu));
-        const uint8_t* rec = intra_cu(L, T, f, cx, cy, left, false, false, mode, t.qp, A.coefs + (size_t)idx * kCoefPerCu,
-                                      cu, A.reg_steps != 0);
-        store_rec(rec, f, cx, cy);
-        if (l == 0) {
-            cu.mode = CU_INTRA;
-            cu.intra_mode = (uint8_t)mode;
-            cu.qp = (uint8_t)t.qp;
-            A.cus[idx] = cu;
-            f.me[idx].mvx = 0;
-            f.me[idx].mvy = 0;
-            f.me[idx].ref = 0;
-            f.me[idx].fx = f.me[idx].fy = 0;
+    for (int c = m.x0(r, k); c < m.x1(r, k); c++)
+        for (int z = 0; z < 4; z++) {
+            const int ux = 2 * c + (z & 1), uy = 2 * r + (z >> 1);
+            if (ug.inside(ux, uy)) intra_unit(A, L, T, ux, uy, t.qp);
         }
-        // this CTB's reconstruction (global memory) is the next one's left neighbour
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        wsync();
-    }
 }
 
 // ---------------------------------------------------------------------------
-// CU syntax -> bin entries: one thread per CU, `lpw` CUs per wave. The lanes diverge (each
-// binarises its own CU's coefficients), so a wave runs about as long as its busiest CU;
-// with 64 CUs per wave a 4K frame is only ~500 waves and half the SIMDs idle, with no
-// second wave to hide the global-memory latency behind.
+// Unit syntax -> bin entries (hevc_cpu.cpp binarize_slice: SAO of the CTB at its first
+// unit, code_unit, end_of_slice_segment_flag / end_of_subset_one_bit after its last):
+// one thread per unit, `lpw` units per wave. The lanes diverge (each binarises its own
+// unit's coefficients), so a wave runs about as long as its busiest unit.
 __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A, int lpw) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
@@ -981,23 +1192,46 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A, int lpw) {
     if (l >= lpw) return;
     const int idx = (blockIdx.x * 4 + (threadIdx.x >> 6)) * lpw + l;
     if (idx >= n) return;
-    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    const int W = f.mb_w;
+    const int ux = idx % W, uy = idx / W, c = ux >> 1, r = uy >> 1;
+    const SliceTask t = ctb_task(A, r);
     const bool p_slice = t.final_action != ACT_I;
     const SliceMap m = smap(A);
-    const bool left = m.left(cx, cy), top = m.top(cx, cy);
+    const UnitGrid ug = ugrid(A);
+    UnitCtx u;
+    u.z = (ux & 1) | ((uy & 1) << 1);
+    u.first = u.z == 0;
+    u.complete = ug.complete(c, r);
+    u.left = ug.avail(m, ux, uy, ux - 1, uy);
+    u.top = ug.avail(m, ux, uy, ux, uy - 1);
+    u.row0 = (uy & 1) == 0;
+    u.p_slice = p_slice;
     const CuInfo cu = A.cus[idx];
-    const int skip_ctx = (left && A.cus[idx - 1].mode == CU_SKIP) + (top && A.cus[idx - f.mb_w].mode == CU_SKIP);
-    const int cand_a = (left && A.cus[idx - 1].mode == CU_INTRA) ? A.cus[idx - 1].intra_mode : 1;
+    CuInfo c32[4];
+    CoefT32 t32;
+    t32.base = 0;
+    for (int k = 0; k < 4; k++) {
+        const int kx = 2 * c + (k & 1), ky = 2 * r + (k >> 1);
+        const int ki = ug.inside(kx, ky) ? ky * W + kx : idx;
+        if (cu.c32 & kC32) c32[k] = A.cus[ki];
+        t32.slot[k] = A.coefs + (size_t)ki * kCoefPerCu;
+    }
+    CuInfo Lc, Tc;
+    if (u.left) Lc = A.cus[idx - 1];
+    if (u.top) Tc = A.cus[idx - W];
     BinBuf w{A.bins + (size_t)idx * kCuBinCap, 0};
-    sao_bins(w, A.sao[idx], left, top);   // CTB-level SAO syntax (k_hevc_sao_row's decision)
-    (void)skip_ctx; (void)cand_a; (void)p_slice; (void)cu;   // TODO CTB32
-    const bool last_row = cy == t.first_row + t.num_rows - 1;
-    if (m.split(cy)) {   // each row segment is a slice: end_of_slice_segment_flag at its end
-        w.term(cx + 1 == m.x1(cy, m.seg(cx, cy)));
-    } else {
-        w.term(last_row && cx == f.mb_w - 1);
-        if (!last_row && cx == f.mb_w - 1) w.term(1);   // end_of_subset_one_bit closes the row's substream
+    if (u.first) sao_bins(w, A.sao[r * A.cw + c], m.left(c, r), m.top(c, r));   // CTB-level SAO syntax
+    code_unit(w, u, cu, &Lc, &Tc, A.coefs + (size_t)idx * kCoefPerCu, c32, t32);
+    bool last = true;   // the CTB's last unit in coding order
+    for (int k = u.z + 1; k < 4; k++) last &= !ug.inside(2 * c + (k & 1), 2 * r + (k >> 1));
+    if (last) {
+        const int r1 = ((t.first_row + t.num_rows + 1) >> 1) - 1;   // the slice's last CTB row
+        if (m.split(r)) {   // each row segment is a slice: end_of_slice_segment_flag at its end
+            w.term(c + 1 == m.x1(r, m.seg(c, r)));
+        } else {
+            w.term(r == r1 && c == A.cw - 1);
+            if (r != r1 && c == A.cw - 1) w.term(1);   // end_of_subset_one_bit closes the row's substream
+        }
     }
     A.bin_n[idx] = w.n;
 }
@@ -1011,10 +1245,10 @@ __device__ __forceinline__ int writelane(int x, int ln, int v) {
     return v;
 }
 
-// WPP context states at each row start of a slice (9.3.2.4: the states after the second
-// CTB of the row above). Thread c owns context c and replays only that context's bins
-// of the two CTBs, from k_pc_sort's per-context lists: the chains run in parallel and
-// each is a few entries long.
+// WPP context states at each CTB row start of a slice (9.3.2.4: the states after the
+// second CTB of the row above). Thread c owns context c and replays only that context's
+// bins of the two CTBs' chunks (their units), from k_pc_sort's per-context lists: the
+// chains run in parallel and each is a few entries long.
 __global__ __launch_bounds__(192) void k_hevc_sync(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint8_t nlps[64];
@@ -1024,23 +1258,26 @@ __global__ __launch_bounds__(192) void k_hevc_sync(HevcArgs A) {
     if (c < 64) nlps[c] = CABAC_NEXT_LPS[c];
     __syncthreads();
     if (c >= CTX_COUNT) return;
+    const UnitGrid ug = ugrid(A);
+    const int RC = 2 * f.mb_w;   // coff row stride (chunks)
     const int it = t.final_action == ACT_I ? 0 : 1;
     const uint8_t init = ctx_init_state(HEVC_CTX_INIT[it][c], t.qp);
-    const int K = A.seg_k;
-    if (smap(A).split(t.first_row)) {   // every row segment is a slice: initial states
-        for (int i = 0; i < t.num_rows * K; i++) A.sync[((size_t)t.first_row * K + i) * CTX_COUNT + c] = init;
+    const int K = A.seg_k, r0 = t.first_row >> 1, nr = ((t.first_row + t.num_rows + 1) >> 1) - r0;
+    if (smap(A).split(r0)) {   // every row segment is a slice: initial states
+        for (int i = 0; i < nr * K; i++) A.sync[((size_t)r0 * K + i) * CTX_COUNT + c] = init;
         return;
     }
     uint32_t st = init;
-    A.sync[(size_t)t.first_row * K * CTX_COUNT + c] = init;
-    for (int r = 1; r < t.num_rows; r++) {
-        const int prev = t.first_row + r - 1;
-        if (f.mb_w >= 2) {
-            const uint16_t* co = A.coff + ((size_t)prev * kPcCtxOff + c) * f.mb_w;
-            for (int cx = 0; cx < 2; cx++) {
-                const uint16_t* sp = A.srt + (size_t)(prev * f.mb_w + cx) * kCuBinCap;
-                const int hi = co[f.mb_w + cx];
-                for (int k = co[cx]; k < hi; k++) {
+    A.sync[(size_t)r0 * K * CTX_COUNT + c] = init;
+    for (int rr = 1; rr < nr; rr++) {
+        const int prev = r0 + rr - 1;
+        if (A.cw >= 2) {
+            const uint16_t* co = A.coff + ((size_t)prev * kPcCtxOff + c) * RC;
+            const int jn = ug.ctb_chunk0(prev, 2);
+            for (int j = 0; j < jn; j++) {
+                const uint16_t* sp = A.srt + (size_t)ug.chunk_unit(prev, j) * kCuBinCap;
+                const int hi = co[RC + j];
+                for (int k = co[j]; k < hi; k++) {
                     const uint32_t bin = sp[k] & 1u, mps = st & 1u, s6 = st >> 1;
                     st = bin == mps ? (((s6 < 62 ? s6 + 1 : 62) << 1) | mps)
                                     : (((uint32_t)nlps[s6] << 1) | (s6 == 0 ? mps ^ 1u : mps));
@@ -1049,16 +1286,18 @@ __global__ __launch_bounds__(192) void k_hevc_sync(HevcArgs A) {
         } else {
             st = init;
         }
-        A.sync[(size_t)(t.first_row + r) * K * CTX_COUNT + c] = (uint8_t)st;
+        A.sync[(size_t)(r0 + rr) * K * CTX_COUNT + c] = (uint8_t)st;
     }
 }
 
 // ---------------------------------------------------------------------------
 // Chunk-parallel substream coding (codec/hevc_pcabac.h has the derivation and the host
 // model): k_pc_sort -> k_pc_model -> k_pc_rmap -> k_pc_compose -> k_pc_code ->
-// k_pc_merge. Chunk = CTB, so every phase but the per-row composition and merge runs
-// one wave per CTB or per (CTB row, context). Same bytes as CabacEncoder (hevc_core.h).
-constexpr int kPcMaxRowCtb = 512;   // CTBs per row (8K width); alloc_hevc checks it
+// k_pc_merge. Chunk = unit (the units of a CTB row in coding order, UnitGrid::chunk_unit),
+// so every phase but the per-row composition and merge runs one wave per unit or per (CTB
+// row, context). Same bytes as CabacEncoder (hevc_core.h).
+constexpr int kPcMaxRowChunks = 1024;   // units per CTB row (8K width); alloc_hevc checks it
+constexpr int kPcMaxRowCtb = 512;       // CTBs per row (SAO row pass)
 
 // One wave per CTB: stable counting sort of its context bins by context index.
 __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
@@ -1093,15 +1332,15 @@ __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
     }
     int run = inc - sum;
     wsync();
-    // coff is [CTB row][context][CTB column]: k_pc_model and k_hevc_sync read one
-    // context's offsets along a row as one contiguous run
-    const int cy = idx / f.mb_w, cx = idx - cy * f.mb_w;
-    uint16_t* co = A.coff + (size_t)cy * kPcCtxOff * f.mb_w + cx;
+    // coff is [CTB row][context][chunk]: k_pc_model and k_hevc_sync read one context's
+    // offsets along a row as one contiguous run
+    const int uy = idx / f.mb_w, ux = idx - uy * f.mb_w, RC = 2 * f.mb_w;
+    uint16_t* co = A.coff + (size_t)(uy >> 1) * kPcCtxOff * RC + ugrid(A).unit_chunk(ux, uy);
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         if (3 * l + k < kPcCtxOff) {
             cnt[3 * l + k] = run;
-            co[(size_t)(3 * l + k) * f.mb_w] = (uint16_t)run;
+            co[(size_t)(3 * l + k) * RC] = (uint16_t)run;
         }
         run += v[k];
     }
@@ -1129,13 +1368,14 @@ __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
     }
 }
 
-// One wave per (CTB row, context): the context's state chain along the row, from its
-// WPP start state; each context bin is rewritten in place as a modelled entry (LPS state,
-// is-LPS). The CTBs holding the context are listed with the prefix of their counts; the
-// chain itself runs as up to 64 speculative segments, one per lane (below).
+// One wave per (CTB row or row segment, context): the context's state chain along the
+// row's chunks, from its WPP start state; each context bin is rewritten in place as a
+// modelled entry (LPS state, is-LPS). The chunks holding the context are listed with the
+// prefix of their counts; the chain itself runs as up to 64 speculative segments, one per
+// lane (below).
 __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
-    __shared__ uint2 lst_s[4][kPcMaxRowCtb + 1];   // (cx | lo << 16, chain position of its first entry)
+    __shared__ uint2 lst_s[4][kPcMaxRowChunks + 1];   // (chunk | lo << 16, chain position of its first entry)
     __shared__ uint8_t nl_s[4][64];                // CABAC_NEXT_LPS
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
@@ -1144,18 +1384,20 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     const SliceMap m = smap(A);
     const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
     if (k >= m.nseg(cy)) return;   // slot of a whole row: only k = 0
-    const int xa = m.x0(cy, k), xb = m.x1(cy, k);
+    const UnitGrid ug = ugrid(A);
+    const int RC = 2 * f.mb_w;
+    const int xa = ug.ctb_chunk0(cy, m.x0(cy, k));
+    const int xb = m.x1(cy, k) < A.cw ? ug.ctb_chunk0(cy, m.x1(cy, k)) : ug.row_chunks(cy);
     uint2* L = lst_s[w];
-    const int row0 = cy * f.mb_w;
     const uint64_t lt = (1ull << l) - 1;
     int n = 0, tot = 0;
     for (int g = xa; g < xb; g += 64) {
         const int cx = g + l;
         int lo = 0, cnt = 0;
         if (cx < xb) {
-            const uint16_t* co = A.coff + ((size_t)cy * kPcCtxOff + c) * f.mb_w + cx;
+            const uint16_t* co = A.coff + ((size_t)cy * kPcCtxOff + c) * RC + cx;
             lo = co[0];
-            cnt = co[f.mb_w] - lo;
+            cnt = co[RC] - lo;
         }
         int inc = cnt;
 #pragma unroll
@@ -1207,7 +1449,7 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
                     it = L[k];
                     nxt = (int)L[k + 1].y;
                 }
-                cu[j] = (uint32_t)row0 + (it.x & 0xffffu);
+                cu[j] = (uint32_t)ug.chunk_unit(cy, (int)(it.x & 0xffffu));
                 v[j] = A.srt[(size_t)cu[j] * kCuBinCap + (it.x >> 16) + (uint32_t)(q - (int)it.y)];
             }
 #pragma unroll
@@ -1319,13 +1561,16 @@ __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
     const SliceMap m = smap(A);
     const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
     if (k >= m.nseg(cy)) return;
-    // the segment's CTBs as a row of their own: chunk j = CTB row0 + j
-    const int row0 = cy * f.mb_w + m.x0(cy, k), nw = m.x1(cy, k) - m.x0(cy, k);
+    // the segment's chunks as a row of their own: chunk j0 + d = unit ug.chunk_unit(cy, j0 + d)
+    const UnitGrid ug = ugrid(A);
+    const int j0 = ug.ctb_chunk0(cy, m.x0(cy, k));
+    const int nw = (m.x1(cy, k) < A.cw ? ug.ctb_chunk0(cy, m.x1(cy, k)) : ug.row_chunks(cy)) - j0;
+    auto unit = [&](int d) { return ug.chunk_unit(cy, j0 + d); };
     constexpr int D = 8;
     uint4 buf[D];
 #pragma unroll
     for (int d = 0; d < D; d++)
-        buf[d] = reinterpret_cast<const uint4*>(A.rmap + (size_t)(row0 + (d < nw ? d : nw - 1)) * 256)[l];
+        buf[d] = reinterpret_cast<const uint4*>(A.rmap + (size_t)unit(d < nw ? d : nw - 1) * 256)[l];
     uint32_t r = 510, T = 0;
     int vr = 0, vt = 0;   // lane j: chunk j of the current 64
     for (int cx0 = 0; cx0 < nw; cx0 += D) {
@@ -1343,15 +1588,16 @@ __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
                 vt = writelane((int)T, cx & 63, vt);
                 if ((cx & 63) == 63 || cx == nw - 1) {
                     if (l <= (cx & 63)) {
-                        A.cu_r[row0 + (cx & ~63) + l] = (uint16_t)vr;
-                        A.cu_t[row0 + (cx & ~63) + l] = (uint32_t)vt;
+                        const int u = unit((cx & ~63) + l);
+                        A.cu_r[u] = (uint16_t)vr;
+                        A.cu_t[u] = (uint32_t)vt;
                     }
                 }
                 r = val & 511u;
                 T += val >> 9;
             }
             const int nx = cx + D < nw ? cx + D : nw - 1;
-            buf[d] = reinterpret_cast<const uint4*>(A.rmap + (size_t)(row0 + nx) * 256)[l];
+            buf[d] = reinterpret_cast<const uint4*>(A.rmap + (size_t)unit(nx) * 256)[l];
         }
     }
     if (l == 0) A.row_bits[slot] = T;
@@ -1366,12 +1612,15 @@ __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
     const int w = threadIdx.x >> 6, l = lane();
     const int idx = blockIdx.x * 4 + w;
     if (idx >= f.mb_w * f.mb_h) return;
-    const int cy = idx / f.mb_w, cx = idx - cy * f.mb_w;
+    const int uy = idx / f.mb_w, ux = idx - uy * f.mb_w, cy = uy >> 1, cx = ux >> 1;
     const SliceMap m = smap(A);
+    const UnitGrid ug = ugrid(A);
     const int k = m.seg(cx, cy), slot = cy * A.seg_k + k;
+    const int j = ug.unit_chunk(ux, uy);
+    const int jend = m.x1(cy, k) < A.cw ? ug.ctb_chunk0(cy, m.x1(cy, k)) : ug.row_chunks(cy);
     const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.cu_t[idx]);
     const uint32_t tn = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(cx + 1 < m.x1(cy, k) ? A.cu_t[idx + 1] : A.row_bits[slot]));
+        (int)(j + 1 < jend ? A.cu_t[ug.chunk_unit(cy, j + 1)] : A.row_bits[slot]));
     const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.cu_r[idx]);
     const int g0 = (int)(t0 >> 3), nex = (int)(tn >> 3) - g0;
     uint8_t* out = A.sub + sub_base(A, m, cy, k) + g0;
@@ -1436,7 +1685,9 @@ __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
         if (l == 0) A.sub_size[slot] = A.sub_esc[slot] = 0;
         return;
     }
-    const int row0 = cy * f.mb_w + m.x0(cy, k), nw = m.x1(cy, k) - m.x0(cy, k);
+    const UnitGrid ug = ugrid(A);
+    const int j0 = ug.ctb_chunk0(cy, m.x0(cy, k));
+    const int nw = (m.x1(cy, k) < A.cw ? ug.ctb_chunk0(cy, m.x1(cy, k)) : ug.row_chunks(cy)) - j0;
     const uint32_t T = (uint32_t)__builtin_amdgcn_readfirstlane((int)A.row_bits[slot]);
     const int excl = (int)(T >> 3), nbytes = excl + 2;
     uint8_t* out = A.sub + sub_base(A, m, cy, k);
@@ -1473,11 +1724,12 @@ __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
     };
     load_win();
     for (int g = 0; g < nw; g += 64) {
-        const int cx = g + l;   // CTB row0 + cx of the segment
+        const int cx = g + l;   // chunk j0 + cx of the segment
         int p_l = 0, t_l = 0;
         if (cx < nw) {
-            p_l = (int)((cx + 1 < nw ? A.cu_t[row0 + cx + 1] : T) >> 3);
-            t_l = (int)((uint32_t)A.tail[2 * (row0 + cx)] | ((uint32_t)A.tail[2 * (row0 + cx) + 1] << 8));
+            const int u = ug.chunk_unit(cy, j0 + cx);
+            p_l = (int)((cx + 1 < nw ? A.cu_t[ug.chunk_unit(cy, j0 + cx + 1)] : T) >> 3);
+            t_l = (int)((uint32_t)A.tail[2 * u] | ((uint32_t)A.tail[2 * u + 1] << 8));
         }
         const int mm = nw - g < 64 ? nw - g : 64;
         for (int j = 0; j < mm; j++) {
@@ -1558,10 +1810,11 @@ __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
     bool idr = true;
     for (int i = l; i < f.num_slices; i += 64) idr &= f.tasks[i].final_action == ACT_I && f.tasks[i].idr_on_intra;
     idr = __syncthreads_and(idr);
+    const int r0 = t.first_row >> 1, nr = ((t.first_row + t.num_rows + 1) >> 1) - r0;   // CTB rows
     auto seg_header = [&](int cy, int k, uint8_t* buf) {   // header RBSP of a row segment
         for (int i = 0; i < 48; i++) buf[i] = 0;
         SliceHeader h;
-        h.address = cy * f.mb_w + m.x0(cy, k);
+        h.address = cy * A.cw + m.x0(cy, k);
         h.first_slice = h.address == 0;
         h.idr = idr;
         h.address_bits = A.addr_bits;
@@ -1572,14 +1825,14 @@ __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
         h.entry = nullptr;
         return write_slice_header(buf, h);
     };
-    if (m.split(t.first_row)) {
-        const int K = A.seg_k, nseg = t.num_rows * K;
+    if (m.split(r0)) {
+        const int K = A.seg_k, nseg = nr * K;
         int run = 0;
         for (int base = 0; base < nseg; base += 64) {   // pass 1: NAL lengths -> offsets
             const int j = base + l;
             int len = 0;
             if (j < nseg) {
-                const int cy = t.first_row + j / K, k = j % K;
+                const int cy = r0 + j / K, k = j % K;
                 const int hn = seg_header(cy, k, shdr[l]);
                 len = 6 + ep_escape(shdr[l], hn, nullptr) + A.sub_esc[cy * K + k];
             }
@@ -1599,7 +1852,7 @@ __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
         for (int base = 0; base < nseg; base += 64) {   // pass 2: NAL prefixes and headers
             const int j = base + l;
             if (j < nseg) {
-                const int cy = t.first_row + j / K, k = j % K;
+                const int cy = r0 + j / K, k = j % K;
                 const int hn = seg_header(cy, k, shdr[l]);
                 uint8_t* d = o + offs[j];
                 d[0] = 0; d[1] = 0; d[2] = 0; d[3] = 1;
@@ -1613,25 +1866,25 @@ __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
         return;
     }
     for (int i = l; i < 1024; i += 64) hdr[i] = 0;
-    for (int i = l; i < t.num_rows; i += 64) esc[i] = A.sub_esc[(t.first_row + i) * A.seg_k];
+    for (int i = l; i < nr; i += 64) esc[i] = A.sub_esc[(r0 + i) * A.seg_k];
     __syncthreads();
     if (l == 0) {
         SliceHeader h;
         h.first_slice = s == 0;
         h.idr = idr;
-        h.address = t.first_row * f.mb_w;
+        h.address = r0 * A.cw;
         h.address_bits = A.addr_bits;
         h.slice_type = t.final_action == ACT_I ? 2 : 1;
         h.poc_lsb = t.frame_num & ((1 << kLog2MaxPocLsb) - 1);
         h.qp_delta = t.qp - 26;
-        h.num_entry = t.num_rows - 1;
+        h.num_entry = nr - 1;
         h.entry = esc;
         const int hn = write_slice_header(hdr, h);
         const int hesc = ep_escape(hdr, hn, nullptr);
         int total = 6 + hesc;
         int off = total;
-        for (int r = 0; r < t.num_rows; r++) {
-            A.row_off[(t.first_row + r) * A.seg_k] = off;
+        for (int r = 0; r < nr; r++) {
+            A.row_off[(r0 + r) * A.seg_k] = off;
             off += esc[r];
         }
         total = off;
@@ -1655,7 +1908,7 @@ __global__ __launch_bounds__(64) void k_hevc_ep_copy(HevcArgs A) {
     const SliceMap m = smap(A);
     const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
     if (k >= m.nseg(cy)) return;
-    const int s = cy / f.rows_per_slice;
+    const int s = cy / A.rps;
     const int total = __hip_atomic_load(A.out_size + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const bool fits = total <= A.out_slot;
     uint8_t* o = (fits ? A.out_host + (size_t)s * A.out_slot : A.out_dev + (size_t)s * A.out_dev_slot) + A.row_off[slot];
@@ -1707,19 +1960,19 @@ __device__ __forceinline__ bool cu_intra_edge(const CuInfo& p, const CuInfo& q) 
 __global__ __launch_bounds__(256) void k_hevc_dbk_v(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const h264::gpu::FrameArgs& f = A.f;
-    const int cw = f.mb_w, ch = f.mb_h, ne = cw - 1, nel = 2 * cw - 1;
+    const int cw = f.mb_w, ch = f.mb_h, ne = cw - 1, nel = 2 * cw - 1;   // units
     const int e = blockIdx.x * 256 + threadIdx.x;
     const int nl = ch * 4 * nel, nc = ch * 8 * ne;
     const SliceMap m = smap(A);
     if (e < nl) {
         const int x = 8 * (1 + e % nel), seg = e / nel;
-        if (!(x & 8) && !m.same((x >> 4) - 1, seg >> 2, x >> 4, seg >> 2)) return;   // slice boundary
+        if (!(x & 8) && !m.same_u((x >> 4) - 1, seg >> 2, x >> 4, seg >> 2)) return;   // slice boundary
         dbk_luma_edge(f.rec.y, f.stride_y, A.cus, cw, true, x, 4 * seg);
     } else if (e < nl + 2 * nc) {
         const int k0 = e - nl, plane = k0 / nc, k = k0 % nc;
         const int cx = 1 + k % ne, line = k / ne, cy = line >> 3;
         const CuInfo p = A.cus[cy * cw + cx - 1], q = A.cus[cy * cw + cx];
-        if (cu_intra_edge(p, q) && m.same(cx - 1, cy, cx, cy))
+        if (cu_intra_edge(p, q) && m.same_u(cx - 1, cy, cx, cy))
             dbk_chroma_line((plane ? f.rec.v : f.rec.u) + (size_t)line * f.stride_c + cx * 8, 1, (p.qp + q.qp + 1) >> 1);
     }
 }
@@ -1727,19 +1980,19 @@ __global__ __launch_bounds__(256) void k_hevc_dbk_v(HevcArgs A) {
 __global__ __launch_bounds__(256) void k_hevc_dbk_h(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const h264::gpu::FrameArgs& f = A.f;
-    const int cw = f.mb_w, ch = f.mb_h, ne = ch - 1, nel = 2 * ch - 1;
+    const int cw = f.mb_w, ch = f.mb_h, ne = ch - 1, nel = 2 * ch - 1;   // units
     if (nel <= 0) return;
     const int e = blockIdx.x * 256 + threadIdx.x;
     const int nl = nel * cw * 4, nc = ne * cw * 8;
     const SliceMap m = smap(A);
     if (e < nl) {
         const int y = 8 * (1 + e / (cw * 4)), x4 = e % (cw * 4);
-        if (!(y & 8) && !m.same(x4 >> 2, (y >> 4) - 1, x4 >> 2, y >> 4)) return;   // slice boundary
+        if (!(y & 8) && !m.same_u(x4 >> 2, (y >> 4) - 1, x4 >> 2, y >> 4)) return;   // slice boundary
         dbk_luma_edge(f.rec.y, f.stride_y, A.cus, cw, false, y, 4 * x4);
     } else if (e < nl + 2 * nc) {
         const int k0 = e - nl, plane = k0 / nc, k = k0 % nc;
         const int cy = 1 + k / (cw * 8), col = k % (cw * 8), cx = col >> 3;
-        if (!m.same(cx, cy - 1, cx, cy)) return;
+        if (!m.same_u(cx, cy - 1, cx, cy)) return;
         const CuInfo p = A.cus[(cy - 1) * cw + cx], q = A.cus[cy * cw + cx];
         if (cu_intra_edge(p, q))
             dbk_chroma_line((plane ? f.rec.v : f.rec.u) + (size_t)(cy * 8) * f.stride_c + col, f.stride_c, (p.qp + q.qp + 1) >> 1);
@@ -1753,18 +2006,21 @@ __global__ __launch_bounds__(256) void k_hevc_dbk_h(HevcArgs A) {
 // that are not coded (skip-all) keep empty stats and decide "off", like the host.
 __device__ __forceinline__ const uint8_t* plane_of(const Planes& P, int c) { return c == 0 ? P.y : (c == 1 ? P.u : P.v); }
 __device__ __forceinline__ uint8_t* plane_of(Planes& P, int c) { return c == 0 ? P.y : (c == 1 ? P.u : P.v); }
-// Sample i (0..383) of CTB (cx, cy): component and plane coordinates.
-__device__ __forceinline__ void ctb_sample(int i, int cx, int cy, int* c, int* x, int* y) {
-    if (i < 256) {
-        *c = 0; *x = cx * 16 + (i & 15); *y = cy * 16 + (i >> 4);
-    } else {
-        const int j = i - 256;
-        *c = 1 + (j >> 6); *x = cx * 8 + (j & 7); *y = cy * 8 + ((j >> 3) & 7);
+// Sample i (0..1535) of CTB (cx, cy): component and plane coordinates; false when it lies
+// outside the picture (the partial CTBs of the last row / column).
+constexpr int kCtbSamples = 1536;
+__device__ __forceinline__ bool ctb_sample(const HevcArgs& A, int i, int cx, int cy, int* c, int* x, int* y) {
+    if (i < 1024) {
+        *c = 0; *x = cx * 32 + (i & 31); *y = cy * 32 + (i >> 5);
+        return *x < A.f.mb_w * 16 && *y < A.f.mb_h * 16;
     }
+    const int j = i - 1024;
+    *c = 1 + (j >> 8); *x = cx * 16 + (j & 15); *y = cy * 16 + ((j >> 4) & 15);
+    return *x < A.f.mb_w * 8 && *y < A.f.mb_h * 8;
 }
 __device__ __forceinline__ SaoPlane sao_plane_of(const HevcArgs& A, int c) {
-    const int n = c ? 8 : 16;
-    return SaoPlane{A.f.mb_w * n, A.f.mb_h * n, n, smap(A)};
+    const int n = c ? 16 : 32, u = c ? 8 : 16;
+    return SaoPlane{A.f.mb_w * u, A.f.mb_h * u, n, smap(A)};
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_hevc_sao_stats(HevcArgs A) {
@@ -1774,17 +2030,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
     const int idx = blockIdx.x * 4 + w;
-    if (idx >= f.mb_w * f.mb_h) return;   // wave-uniform; no block barriers below
-    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
-    const SliceTask t = f.tasks[cy / f.rows_per_slice];
+    if (idx >= A.cw * A.ch) return;   // wave-uniform; no block barriers below
+    const int cx = idx % A.cw, cy = idx / A.cw;
+    const SliceTask t = ctb_task(A, cy);
     SaoStats* st = Sw[w];
     int32_t* z = reinterpret_cast<int32_t*>(st);
     for (int i = l; i < 3 * kSaoStatsInts; i += 64) z[i] = 0;
     wsync();
     if (t.final_action == ACT_P || t.final_action == ACT_I) {
-        for (int i = l; i < kCoefPerCu; i += 64) {
+        for (int i = l; i < kCtbSamples; i += 64) {
             int c, x, y;
-            ctb_sample(i, cx, cy, &c, &x, &y);
+            if (!ctb_sample(A, i, cx, cy, &c, &x, &y)) continue;
             const SaoPlane pl = sao_plane_of(A, c);
             const int stride = c ? f.stride_c : f.stride_y;
             const uint8_t* rec = plane_of(f.rec, c);
@@ -1828,8 +2084,8 @@ __global__ __launch_bounds__(256) void k_hevc_sao_md(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= f.mb_w * f.mb_h * kSaoMd) return;
-    const int idx = t / kSaoMd, j = t - idx * kSaoMd, cx = idx % f.mb_w;
+    if (t >= A.cw * A.ch * kSaoMd) return;
+    const int idx = t / kSaoMd, j = t - idx * kSaoMd, cx = idx % A.cw;
     const SaoParams* own_row = A.sao_own + (idx - cx);
     const SaoStats* st = A.sao_stats + (size_t)3 * idx;
     long long d = 0;
@@ -1849,7 +2105,7 @@ __global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
     __shared__ uint16_t sel[kPcMaxRowCtb];
     __shared__ uint8_t fl[kPcMaxRowCtb];
     const FrameArgs& f = A.f;
-    const int cy = blockIdx.x, l = threadIdx.x, W = f.mb_w;
+    const int cy = blockIdx.x, l = threadIdx.x, W = A.cw;
     const size_t o = (size_t)cy * W;
     const SliceMap m = smap(A);
     for (int i = l; i < W * kSaoMd; i += 64) md[i] = A.sao_md[o * kSaoMd + i];
@@ -1860,7 +2116,7 @@ __global__ __launch_bounds__(64) void k_hevc_sao_row(HevcArgs A) {
     }
     __syncthreads();
     if (l == 0) {   // the decision chain is sequential along the row
-        const SliceTask t = f.tasks[cy / f.rows_per_slice];
+        const SliceTask t = ctb_task(A, cy);
         sao_row_decide(md, own, cost, W, t.qp, fl, sel);
     }
     __syncthreads();
@@ -1875,13 +2131,13 @@ __device__ __forceinline__ bool sao_any(const SaoParams& p) { return (p.type[0] 
 __global__ __launch_bounds__(256) void k_hevc_sao_apply(HevcArgs A) {
     const FrameArgs& f = A.f;
     const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (idx >= f.mb_w * f.mb_h) return;
+    if (idx >= A.cw * A.ch) return;
     const SaoParams p = A.sao[idx];
     if (!sao_any(p)) return;
-    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
-    for (int i = lane(); i < kCoefPerCu; i += 64) {
+    const int cx = idx % A.cw, cy = idx / A.cw;
+    for (int i = lane(); i < kCtbSamples; i += 64) {
         int c, x, y;
-        ctb_sample(i, cx, cy, &c, &x, &y);
+        if (!ctb_sample(A, i, cx, cy, &c, &x, &y)) continue;
         const int stride = c ? f.stride_c : f.stride_y;
         plane_of(A.sao_tmp, c)[(size_t)y * stride + x] =
             (uint8_t)sao_apply_sample(p, c, sao_plane_of(A, c), plane_of(f.rec, c), stride, x, y);
@@ -1890,13 +2146,13 @@ __global__ __launch_bounds__(256) void k_hevc_sao_apply(HevcArgs A) {
 __global__ __launch_bounds__(256) void k_hevc_sao_copy(HevcArgs A) {
     const FrameArgs& f = A.f;
     const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (idx >= f.mb_w * f.mb_h) return;
+    if (idx >= A.cw * A.ch) return;
     if (!sao_any(A.sao[idx])) return;
-    const int cx = idx % f.mb_w, cy = idx / f.mb_w;
+    const int cx = idx % A.cw, cy = idx / A.cw;
     Planes rec = f.rec;
-    for (int i = lane(); i < kCoefPerCu; i += 64) {
+    for (int i = lane(); i < kCtbSamples; i += 64) {
         int c, x, y;
-        ctb_sample(i, cx, cy, &c, &x, &y);
+        if (!ctb_sample(A, i, cx, cy, &c, &x, &y)) continue;
         const size_t o = (size_t)y * (c ? f.stride_c : f.stride_y) + x;
         plane_of(rec, c)[o] = plane_of(A.sao_tmp, c)[o];
     }
@@ -1905,24 +2161,24 @@ __global__ __launch_bounds__(256) void k_hevc_sao_copy(HevcArgs A) {
 // CU coding, deblocking, SAO decisions and the CABAC substreams: everything the coded
 // size depends on (the K10 guard re-runs it, gated).
 static void launch_code(const HevcArgs& a, hipStream_t s) {
-    const int n = a.f.mb_w * a.f.mb_h;
-    hipLaunchKernelGGL(k_hevc_inter, dim3((n + 3) / 4), dim3(256), 0, s, a);
+    const int n = a.f.mb_w * a.f.mb_h, nc = a.cw * a.ch;   // units, CTBs
+    hipLaunchKernelGGL(k_hevc_inter, dim3(nc), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_intra_prep, dim3((n + 3) / 4), dim3(256), 0, s, a);
-    if (a.f.rows_per_slice <= 4)
+    if (a.rps <= 4)
         hipLaunchKernelGGL(k_hevc_intra<4>, dim3(a.f.num_slices), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(k_hevc_intra<15>, dim3(a.f.num_slices), dim3(64 * 15), 0, s, a);
-    const int slots = a.f.mb_h * a.seg_k;   // substream slots (SliceMap)
+    const int slots = a.ch * a.seg_k;   // substream slots (SliceMap)
     if (a.seg_k > 1) hipLaunchKernelGGL(k_hevc_intra_seg, dim3((slots + 3) / 4), dim3(256), 0, s, a);
     // in-loop deblocking, then the SAO decisions on the deblocked picture (CTB syntax)
     const int cw = a.f.mb_w, ch = a.f.mb_h;
     const int nv = ch * 4 * (2 * cw - 1) + 2 * ch * 8 * (cw - 1), nh = (2 * ch - 1) * cw * 4 + 2 * (ch - 1) * cw * 8;
     if (nv > 0) hipLaunchKernelGGL(k_hevc_dbk_v, dim3((nv + 255) / 256), dim3(256), 0, s, a);
     if (nh > 0) hipLaunchKernelGGL(k_hevc_dbk_h, dim3((nh + 255) / 256), dim3(256), 0, s, a);
-    const int nq = (n + 3) / 4;
-    hipLaunchKernelGGL(k_hevc_sao_stats, dim3(nq), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_sao_md, dim3((n * kSaoMd + 255) / 256), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_sao_row, dim3(ch), dim3(64), 0, s, a);
+    const int nq = (n + 3) / 4, ncq = (nc + 3) / 4;
+    hipLaunchKernelGGL(k_hevc_sao_stats, dim3(ncq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sao_md, dim3((nc * kSaoMd + 255) / 256), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sao_row, dim3(a.ch), dim3(64), 0, s, a);
     static const int lpw = getenv("SK_HEVC_BINS_LPW") ? sk_clip(atoi(getenv("SK_HEVC_BINS_LPW")), 1, 64) : 32;
     hipLaunchKernelGGL(k_hevc_bins, dim3((n + 4 * lpw - 1) / (4 * lpw)), dim3(256), 0, s, a, lpw);
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
@@ -1935,22 +2191,22 @@ static void launch_code(const HevcArgs& a, hipStream_t s) {
 }
 
 void launch_backend(const HevcArgs& a, hipStream_t s, int* redo) {
-    const int n = a.f.mb_w * a.f.mb_h;
+    const int nc = a.cw * a.ch;
     launch_code(a, s);
     if (redo) {   // K10 CBR per-frame cap: payload = the substream bytes (as k_rc_account)
         HevcArgs b = a;
         b.f.gate = redo;
         for (int r = 0; r < h264::rc_max_recodes(1); r++) {
-            h264::gpu::launch_rc_guard_sizes(a.f, a.sub_size, a.f.mb_h * a.seg_k, redo, r > 0, s);
+            h264::gpu::launch_rc_guard_sizes(a.f, a.sub_size, a.ch * a.seg_k, redo, r > 0, s);
             launch_code(b, s);
         }
     }
     hipLaunchKernelGGL(k_hevc_hdr, dim3(a.f.num_slices), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.f.mb_h * a.seg_k), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_ep_copy, dim3(a.ch * a.seg_k), dim3(64), 0, s, a);
     // the SAO output becomes the reconstruction (k_commit copies it into the reference)
-    const int nq = (n + 3) / 4;
-    hipLaunchKernelGGL(k_hevc_sao_apply, dim3(nq), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_hevc_sao_copy, dim3(nq), dim3(256), 0, s, a);
+    const int ncq = (nc + 3) / 4;
+    hipLaunchKernelGGL(k_hevc_sao_apply, dim3(ncq), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hevc_sao_copy, dim3(ncq), dim3(256), 0, s, a);
 }
 
 }  // namespace gpu

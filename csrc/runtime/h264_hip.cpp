@@ -484,9 +484,9 @@ class HipBackend : public EncoderBackend {
         }
         else if (s == "coefs" && cfg_.codec == 1) { p = hargs_.coefs; n = (int64_t)g_.num_mbs() * hevc::kCoefPerCu * 2; }
         else if (s == "cus" && cfg_.codec == 1) { p = hargs_.cus; n = (int64_t)g_.num_mbs() * sizeof(hevc::CuInfo); }
-        else if (s == "sao" && cfg_.codec == 1) { p = hargs_.sao; n = (int64_t)g_.num_mbs() * sizeof(hevc::SaoParams); }
+        else if (s == "sao" && cfg_.codec == 1) { p = hargs_.sao; n = (int64_t)hargs_.cw * hargs_.ch * sizeof(hevc::SaoParams); }
         else if (s == "bin_n" && cfg_.codec == 1) { p = hargs_.bin_n; n = (int64_t)g_.num_mbs() * 4; }
-        else if (s == "hevc_stamps" && cfg_.codec == 1) { if (!hargs_.dbg) return -1; p = hargs_.dbg; n = (int64_t)g_.mb_h * 32; }
+        else if (s == "hevc_stamps" && cfg_.codec == 1) { if (!hargs_.dbg) return -1; p = hargs_.dbg; n = (int64_t)hargs_.ch * 32; }
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
         else if (s == "me") { p = args_.me; n = (int64_t)g_.num_mbs() * sizeof(MeResult); }
         else if (s == "mb_dirty") { p = args_.mb_dirty; n = g_.num_mbs(); }
@@ -718,7 +718,7 @@ class HipBackend : public EncoderBackend {
                 ha.out_size = hevc_size_dev_[parity_];
                 ha.out_dev = hevc_fallback_[parity_];
                 hevc::gpu::launch_backend(ha, stream_, graph_guard_ ? args_.rc_redo : nullptr);
-                gpu::launch_rc_account(args_, ha.sub_size, g_.mb_h * ha.seg_k, 1, 0, stream_);
+                gpu::launch_rc_account(args_, ha.sub_size, ha.ch * ha.seg_k, 1, 0, stream_);
             } else {
                 gpu::launch_encode(args_, stream_, graph_guard_);
             }
@@ -751,42 +751,47 @@ class HipBackend : public EncoderBackend {
         geo.init(g_);
         hevc::gpu::HevcArgs& h = hargs_;
         memset(&h, 0, sizeof(h));
+        h.cw = geo.ctb_w;
+        h.ch = geo.ctb_h;
+        h.rps = geo.rows_per_slice;
+        if (g_.rows_per_slice & 1) throw std::runtime_error("HEVC: stripes must be whole CTB rows");
+        const int nc = geo.ctbs();
         h.cus = dmalloc<hevc::CuInfo>(n);
         h.coefs = dmalloc<int16_t>((size_t)n * hevc::kCoefPerCu);
         h.bins = dmalloc<uint16_t>((size_t)n * hevc::kCuBinCap, false);
         h.bin_n = dmalloc<int>(n);
         // intra slices: seg_k slices per CTB row (hevc_core.h SliceMap); per-substream
-        // arrays hold mb_h * seg_k slots
-        h.seg_k = hevc::intra_seg_k(g_.mb_w);
-        if (g_.rows_per_slice * h.seg_k > 256) throw std::runtime_error("HEVC: more than 256 row segments per slice");
-        const size_t slots = (size_t)g_.mb_h * h.seg_k;
+        // arrays hold ch * seg_k slots
+        h.seg_k = hevc::intra_seg_k(h.cw);
+        if (h.rps * h.seg_k > 256) throw std::runtime_error("HEVC: more than 256 row segments per slice");
+        const size_t slots = (size_t)h.ch * h.seg_k;
         h.sync = dmalloc<uint8_t>(slots * hevc::CTX_COUNT);
-        h.sub_stride = g_.mb_w * hevc::kSubstreamCtbBytes + 64 * h.seg_k + 64;
-        h.sub = dmalloc<uint8_t>((size_t)g_.mb_h * h.sub_stride, false);
+        h.sub_stride = h.cw * 4 * hevc::kSubstreamCtbBytes + 64 * h.seg_k + 64;
+        h.sub = dmalloc<uint8_t>((size_t)h.ch * h.sub_stride, false);
         h.sub_size = dmalloc<int>(slots);
         h.sub_esc = dmalloc<int>(slots);
         h.row_off = dmalloc<int>(slots);
         h.addr_bits = geo.addr_bits;
-        if (g_.mb_w > 512) throw std::runtime_error("HEVC: more than 512 CTBs per row (8K) is not supported");
+        if (2 * g_.mb_w > 1024) throw std::runtime_error("HEVC: more than 1024 units per CTB row (8K) is not supported");
         h.srt = dmalloc<uint16_t>((size_t)n * hevc::kCuBinCap, false);
-        h.coff = dmalloc<uint16_t>((size_t)n * hevc::kPcCtxOff, false);
+        h.coff = dmalloc<uint16_t>((size_t)h.ch * hevc::kPcCtxOff * 2 * g_.mb_w, false);
         h.rmap = dmalloc<uint32_t>((size_t)n * 256, false);
         h.cu_t = dmalloc<uint32_t>(n);
         h.cu_r = dmalloc<uint16_t>(n);
         h.tail = dmalloc<uint8_t>((size_t)n * 2);
         h.row_bits = dmalloc<uint32_t>(slots);
-        h.sao_stats = dmalloc<hevc::SaoStats>((size_t)3 * n, false);
-        h.sao_own = dmalloc<hevc::SaoParams>(n);
-        h.sao_cost = dmalloc<long long>(n);
-        h.sao_md = dmalloc<long long>((size_t)n * hevc::kSaoMd);
-        h.sao = dmalloc<hevc::SaoParams>(n);
+        h.sao_stats = dmalloc<hevc::SaoStats>((size_t)3 * nc, false);
+        h.sao_own = dmalloc<hevc::SaoParams>(nc);
+        h.sao_cost = dmalloc<long long>(nc);
+        h.sao_md = dmalloc<long long>((size_t)nc * hevc::kSaoMd);
+        h.sao = dmalloc<hevc::SaoParams>(nc);
         h.sao_tmp.y = dmalloc<uint8_t>((size_t)g_.stride_y * g_.mb_h * 16, false);
         h.sao_tmp.u = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
         h.sao_tmp.v = dmalloc<uint8_t>((size_t)g_.stride_c * g_.mb_h * 8, false);
         // host slot: 1.5 KB per CTB (far above practical rates); larger slices go to the
         // device fallback slot (worst case: 3/2 emulation growth of the substream bound)
         h.out_slot = (g_.rows_per_slice * g_.mb_w * 1536 + 4096 + 63) & ~63;
-        h.out_dev_slot = (int)(((size_t)g_.rows_per_slice * h.sub_stride * 3 / 2 + 4096 + 63) & ~(size_t)63);
+        h.out_dev_slot = (int)(((size_t)h.rps * h.sub_stride * 3 / 2 + 4096 + 63) & ~(size_t)63);
         void* dptr = nullptr;
         for (int p = 0; p < 2; p++) {
             hevc_out_[p] = hmalloc<uint8_t>((size_t)h.out_slot * ns);
@@ -798,7 +803,7 @@ class HipBackend : public EncoderBackend {
             hevc_fallback_[p] = dmalloc<uint8_t>((size_t)h.out_dev_slot * ns, false);
         }
         HIPCHECK(hipStreamSynchronize(stream_));
-        if (getenv("SK_STAMPS")) h.dbg = dmalloc<unsigned long long>((size_t)4 * g_.mb_h);
+        if (getenv("SK_STAMPS")) h.dbg = dmalloc<unsigned long long>((size_t)4 * h.ch);
         h.reg_steps = getenv("SK_HEVC_REG_STEPS") ? atoi(getenv("SK_HEVC_REG_STEPS")) : 1;
         hevc_params_.clear();
         hevc::build_parameter_sets(g_.W, g_.H, cfg_.full_range, cfg_.fps, hevc_params_);

@@ -84,7 +84,7 @@ def test_hevc_hip_split_intra_slices(kind, seg, monkeypatch):
     NAL per segment from k_hevc_hdr - byte-identical to the CPU, key frames on request
     included, and decoded to the encoder's reconstruction."""
     monkeypatch.setenv("SK_HEVC_SEG_CTBS", seg)
-    W, H = 336, 208   # 21 x 13 CTBs: uneven segments, a partial last slice
+    W, H = 336, 208   # 21 x 13 units = 11 x 7 CTBs: partial CTBs, uneven segments, a partial last slice
     gpu, cpu = _pair(W, H, qp=27)
     src = SyntheticDesktop(W, H, kind=kind)
     dec = HevcDecoder()
@@ -104,7 +104,7 @@ def test_hevc_hip_split_intra_slices(kind, seg, monkeypatch):
 
 
 def test_hevc_hip_4k_keyframe_parity():
-    """3840x2160 key frames (6 segments per CTB row, 810 slices) and the P frames after
+    """3840x2160 key frames (6 segments per CTB row, 408 slices) and the P frames after
     them: GPU == CPU."""
     W, H = 3840, 2160
     gpu, cpu = _pair(W, H)
