@@ -54,7 +54,9 @@ void intra_predict(const uint8_t* ref_raw, int log2n, int mode, int cidx, uint8_
 // Host model of the chunk-parallel substream coder (hevc_pcabac.h), chunk = CTB: the
 // same four phases the HIP back end runs, sequentially. `cu` lists each CTB's bin
 // entries (the row's terminating end_of_subset bin included in the last).
-std::vector<uint8_t> pc_code_row_host(const std::vector<std::vector<uint16_t>>& cu, const uint8_t* init_ctx) {
+std::vector<uint8_t> pc_code_row_host(const std::vector<std::vector<uint16_t>>& cu, const uint8_t* init_ctx,
+                                      std::vector<uint32_t>* dbg_t = nullptr, std::vector<uint32_t>* dbg_r = nullptr,
+                                      std::vector<uint32_t>* dbg_tail = nullptr) {
     const int nc = (int)cu.size();
     // 1. context modelling (the GPU runs one chain per context; the states are the same)
     std::vector<std::vector<uint16_t>> mod(cu);
@@ -102,6 +104,11 @@ std::vector<uint8_t> pc_code_row_host(const std::vector<std::vector<uint16_t>>& 
         c.flush(emit);
         if (g0 + pos != gn + 2) throw std::logic_error("pcabac: chunk byte count");
         tail[j] = tl;
+    }
+    if (dbg_t) {   // per chunk: stream bit offset, start range, tail (the GPU's cu_t / cu_r / tail)
+        dbg_t->assign(t0.begin(), t0.end() - 1);
+        dbg_r->assign(r0.begin(), r0.end());
+        dbg_tail->assign(tail.begin(), tail.end());
     }
     // merge: add every tail (big-endian 16 bits at its byte) with carries toward the start
     for (int j = 0; j < nc; j++) {
@@ -830,7 +837,15 @@ std::vector<uint8_t> CpuHevcEncoder::write_segment(const SliceTask& t, int cy0, 
                 cu[j - j0].assign(b, b + bin_n[u]);
             }
             if (r + 1 < rows) cu.back().push_back((uint16_t)((1u << 8) | CTX_TERM));   // end_of_subset_one_bit
-            sub[r] = pc_code_row_host(cu, ctx);
+            std::vector<uint32_t> dt, dr, dtl;
+            sub[r] = pc_code_row_host(cu, ctx, &dt, &dr, &dtl);
+            if (pc_dbg_.size() != (size_t)3 * geo.units()) pc_dbg_.assign((size_t)3 * geo.units(), 0);
+            for (int j = j0; j < jn; j++) {
+                const int u = ug.chunk_unit(cy, j);
+                pc_dbg_[3 * (size_t)u] = dt[j - j0];
+                pc_dbg_[3 * (size_t)u + 1] = dr[j - j0];
+                pc_dbg_[3 * (size_t)u + 2] = dtl[j - j0];
+            }
             for (int j = j0; j < jsync_end; j++) {
                 const int u = ug.chunk_unit(cy, j);
                 for (int i = 0; i < bin_n[u]; i++) {

@@ -121,6 +121,7 @@ class CpuHevcEncoder {
     std::vector<uint8_t> write_segment(const h264::SliceTask& t, int cy0, int rows, int x0, int x1, bool idr);
     long long payload_bytes_ = 0;   // substream bytes of the frame being written (K10)
     bool pc_host_ = getenv("SK_HEVC_PCABAC") != nullptr;   // write rows with pc_code_row_host
+    std::vector<uint32_t> pc_dbg_;   // pc_host_: per unit chunk bit offset, start range, tail (tests)
 
     h264::CpuH264Encoder fe;   // front end (full-frame mode)
     Geo geo;

@@ -1693,14 +1693,21 @@ __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
     uint8_t* out = A.sub + sub_base(A, m, cy, k);
     int wb = 0;
     uint32_t win = 0;
+    // bytes excl, excl + 1 (past the chunks' exclusive bytes) start as zero: cleared here so
+    // that a window reloaded after tails were added there (and stored) reads them back
+    if (l == 0) {
+        out[excl] = 0;
+        out[excl + 1] = 0;
+    }
+    __threadfence();
     auto load_win = [&]() __attribute__((always_inline)) {
         const int q = wb + 4 * l;
         uint32_t v = 0;
-        if (q + 4 <= excl) {
-            v = *reinterpret_cast<const uint32_t*>(out + q);
+        if (q + 4 <= nbytes) {
+            for (int k = 0; k < 4; k++) v |= (uint32_t)out[q + k] << (8 * k);
         } else {
             for (int k = 0; k < 4; k++)
-                if (q + k < excl) v |= (uint32_t)out[q + k] << (8 * k);
+                if (q + k < nbytes) v |= (uint32_t)out[q + k] << (8 * k);
         }
         win = v;
     };

@@ -486,6 +486,12 @@ class HipBackend : public EncoderBackend {
         else if (s == "cus" && cfg_.codec == 1) { p = hargs_.cus; n = (int64_t)g_.num_mbs() * sizeof(hevc::CuInfo); }
         else if (s == "sao" && cfg_.codec == 1) { p = hargs_.sao; n = (int64_t)hargs_.cw * hargs_.ch * sizeof(hevc::SaoParams); }
         else if (s == "bin_n" && cfg_.codec == 1) { p = hargs_.bin_n; n = (int64_t)g_.num_mbs() * 4; }
+        else if (s == "cu_t" && cfg_.codec == 1) { p = hargs_.cu_t; n = (int64_t)g_.num_mbs() * 4; }
+        else if (s == "cu_r" && cfg_.codec == 1) { p = hargs_.cu_r; n = (int64_t)g_.num_mbs() * 2; }
+        else if (s == "tail" && cfg_.codec == 1) { p = hargs_.tail; n = (int64_t)g_.num_mbs() * 2; }
+        else if (s == "sub" && cfg_.codec == 1) { p = hargs_.sub; n = (int64_t)hargs_.ch * hargs_.sub_stride; }
+        else if (s == "sub_size" && cfg_.codec == 1) { p = hargs_.sub_size; n = (int64_t)hargs_.ch * hargs_.seg_k * 4; }
+        else if (s == "row_bits" && cfg_.codec == 1) { p = hargs_.row_bits; n = (int64_t)hargs_.ch * hargs_.seg_k * 4; }
         else if (s == "hevc_stamps" && cfg_.codec == 1) { if (!hargs_.dbg) return -1; p = hargs_.dbg; n = (int64_t)hargs_.ch * 32; }
         else if (s == "coefs") { p = args_.coefs; n = (int64_t)g_.num_mbs() * kCoefPerMb * 2; }
         else if (s == "me") { p = args_.me; n = (int64_t)g_.num_mbs() * sizeof(MeResult); }

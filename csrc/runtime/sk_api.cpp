@@ -196,6 +196,7 @@ class CpuHevcBackend : public EncoderBackend {
         else if (s == "sao") { p = enc_.sao.data(); n = (int64_t)(enc_.sao.size() * sizeof(hevc::SaoParams)); }
         else if (s == "coefs") { p = enc_.coefs.data(); n = (int64_t)(enc_.coefs.size() * 2); }
         else if (s == "bin_n") { p = enc_.bin_n.data(); n = (int64_t)(enc_.bin_n.size() * 4); }
+        else if (s == "pc_dbg") { p = enc_.pc_dbg_.data(); n = (int64_t)(enc_.pc_dbg_.size() * 4); }
         else if (s == "me") { p = enc_.fe.me.data(); n = (int64_t)(enc_.fe.me.size() * sizeof(h264::MeResult)); }
         else if (s == "tasks") { p = enc_.fe.tasks.data(); n = (int64_t)(enc_.fe.tasks.size() * sizeof(h264::SliceTask)); }
         else return -1;
