@@ -365,6 +365,7 @@ SK_HD void ctx_update(uint8_t& s, int bin) {
 //   context bin  : bit15 = 0, bit8 = bin value, bits 0..7 = context index (CTX_TERM: terminate)
 //   bypass run   : bit15 = 1, bits 12..14 = n - 1 (n = 1..8 bins), bits 0..7 = the bins (MSB first)
 struct BinBuf {
+    static constexpr bool kWave = false;
     uint16_t* p;
     int n;
     SK_HD void ctx(int c, int b) { p[n++] = (uint16_t)(((b & 1) << 8) | c); }
@@ -378,6 +379,7 @@ struct BinBuf {
     }
 };
 struct BinCount {   // same interface, counts entries
+    static constexpr bool kWave = false;
     int n = 0;
     SK_HD void ctx(int, int) { n++; }
     SK_HD void term(int) { n++; }
@@ -1010,229 +1012,293 @@ SK_HD int last_prefix(int p) {
     return g;
 }
 
-// Coefficient accessors: c(i) = the level at raster index i (y * n + x) of the TU.
+// Four levels (one sub-block row) at an 8-byte aligned address, 16 bits each: one load.
+SK_HD uint64_t load4(const int16_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(p, 8), 8);
+    return v;
+}
+// Coefficient accessors: c(i) = the level at raster index i (y * n + x) of the TU,
+// c.row4(i) = the four levels at i .. i + 3 (i a multiple of 4).
 struct CoefPtr {
     const int16_t* p;
     SK_HD int operator()(int i) const { return p[i]; }
+    SK_HD uint64_t row4(int i) const { return load4(p + i); }
+};
+// The CTB's four units in z order inside the raster unit arrays (CuInfo and coefficient
+// slots, `W` units per row). Only a complete CTB's view is dereferenced (CU32s are).
+struct Ctb4 {
+    const CuInfo* cu;      // the CTB's unit z0
+    const int16_t* coef;   // its coefficient slot
+    int W;
+    SK_HD const CuInfo& operator[](int z) const { return cu[(z >> 1) * W + (z & 1)]; }
+    SK_HD const int16_t* slot(int z) const { return coef + (size_t)((z >> 1) * W + (z & 1)) * kCoefPerCu; }
 };
 // The levels of a CU32's 32x32 TU (and its 16x16 chroma TUs) spread over its units' slots:
 // logical index i (kT32Cb / kT32Cr offsets) -> slot of unit z = i / kCoefPerCu.
 struct CoefT32 {
-    const int16_t* slot[4];
+    Ctb4 q;
     int base;   // 0 luma, kT32Cb, kT32Cr
     SK_HD int operator()(int i) const {
         const int k = base + i;
-        return slot[k / kCoefPerCu][k % kCoefPerCu];
+        return q.slot(k / kCoefPerCu)[k % kCoefPerCu];
+    }
+    SK_HD uint64_t row4(int i) const {   // kCoefPerCu % 4 == 0: a row never straddles two slots
+        const int k = base + i;
+        return load4(q.slot(k / kCoefPerCu) + k % kCoefPerCu);
     }
 };
-
-// g1ctx (greater1 context state) a coded sub-block leaves behind: its first eight
-// significant levels in reverse scan order.
+// A 4x4 sub-block's levels as four packed rows.
+struct Sb4 {
+    uint64_t r0, r1, r2, r3;
+    SK_HD bool nz() const { return (r0 | r1 | r2 | r3) != 0; }
+    SK_HD int at(int i) const {   // level i (0..15): raster position, or scan position of a scan-ordered Sb4
+        // masks, not a select of member addresses (which would pin the struct in scratch)
+        const uint64_t m1 = 0 - (uint64_t)((i >> 2) & 1), m2 = 0 - (uint64_t)((i >> 3) & 1);
+        const uint64_t lo = (r0 & ~m1) | (r1 & m1), hi = (r2 & ~m1) | (r3 & m1);
+        const uint64_t v = (lo & ~m2) | (hi & m2);
+        return (int16_t)(uint16_t)(v >> (16 * (i & 3)));
+    }
+    SK_HD void set(int i, int x) {   // i a compile-time constant after unrolling
+        const uint64_t m = (uint64_t)(uint16_t)x << (16 * (i & 3));
+        if (i < 4) r0 |= m; else if (i < 8) r1 |= m; else if (i < 12) r2 |= m; else r3 |= m;
+    }
+};
 template <class C>
-SK_HD int sb_g1_end(C c, int n, int scan, int xs, int ys, bool* any) {
+SK_HD Sb4 load_sb(C c, int n, int xs, int ys) {
+    const int o = ys * 4 * n + xs * 4;
+    return Sb4{c.row4(o), c.row4(o + n), c.row4(o + 2 * n), c.row4(o + 3 * n)};
+}
+
+// g1ctx (greater1 context state) a sub-block with a significant level leaves behind: its
+// first eight significant levels in reverse scan order.
+SK_HD int sb_g1(const Sb4& s, int scan) {
     int g1ctx = 1, ng1 = 0;
-    *any = false;
-    for (int k = 15; k >= 0; k--) {
-        const int r = scan4_raster(scan, k);
-        const int v = c((ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3));
+    for (int k = 15; k >= 0 && ng1 < 8; k--) {
+        const int v = s.at(scan4_raster(scan, k));
         if (!v) continue;
-        *any = true;
-        if (ng1 < 8) {
-            const int f = sk_abs(v) > 1;
-            ng1++;
-            if (g1ctx > 0) g1ctx = f ? 0 : g1ctx + 1;
-        }
+        ng1++;
+        if (g1ctx > 0) g1ctx = sk_abs(v) > 1 ? 0 : g1ctx + 1;
     }
     return g1ctx;
 }
 
-// residual_coding (7.3.8.11) of one TU from raster levels - or of the sub-blocks with scan
-// index in [lo, hi] only: a CU32's 32x32 and 16x16 TUs are binarised in pieces, one per
-// unit (the units' bin slots are the chunks of the chunk-parallel coder). The piece that
-// holds the last significant sub-block writes the TU prologue (transform_skip_flag, last
-// position); a later piece starts from the greater1 state the sub-blocks coded before it
-// leave (that of the nearest one with a significant level).
+// residual_coding (7.3.8.11), split into the TU prologue (code_last) and one sub-block's
+// syntax (code_sb); code_residual runs them over a TU in coding order.
+//
+// The prologue: transform_skip_flag (4x4), the last significant position (sub-block last_i,
+// scan position last_n).
+template <class W>
+SK_HD void code_last(W& w, int log2n, int cidx, int scan, int ts, int last_i, int last_n) {
+    const int sbw = 1 << (log2n - 2);
+    if (log2n == 2) w.ctx(CTX_TS + (cidx ? 1 : 0), ts);   // transform_skip_flag (PPS enables it)
+    const int lsr = sb_scan_raster(log2n, scan, last_i);
+    int lx = (lsr % sbw) * 4 + (scan4_raster(scan, last_n) & 3);
+    int ly = (lsr / sbw) * 4 + (scan4_raster(scan, last_n) >> 2);
+    if (scan == SCAN_VER) { const int t = lx; lx = ly; ly = t; }   // coded swapped (7.4.9.11)
+    // last_sig_coeff_x/y_prefix (TR, cMax 2*log2n - 1), then suffixes (FL, bypass)
+    const int off = cidx == 0 ? 3 * (log2n - 2) + ((log2n - 1) >> 2) : 15;
+    const int shift = cidx == 0 ? (log2n + 1) >> 2 : log2n - 2;
+    const int cmax = 2 * log2n - 1;
+    const int px = last_prefix(lx), py = last_prefix(ly);
+    for (int b = 0; b < px; b++) w.ctx(CTX_LAST_X + off + (b >> shift), 1);
+    if (px < cmax) w.ctx(CTX_LAST_X + off + (px >> shift), 0);
+    for (int b = 0; b < py; b++) w.ctx(CTX_LAST_Y + off + (b >> shift), 1);
+    if (py < cmax) w.ctx(CTX_LAST_Y + off + (py >> shift), 0);
+    if (px > 3) w.bypass((uint32_t)(lx - last_group_min(px)), (px >> 1) - 1);
+    if (py > 3) w.bypass((uint32_t)(ly - last_group_min(py)), (py >> 1) - 1);
+}
+// Last significant position of a TU: sub-block scan index (-1: no level) and position.
+SK_HD int sb_last_pos(const Sb4& s, int scan) {
+    for (int k = 15; k >= 0; k--)
+        if (s.at(scan4_raster(scan, k))) return k;
+    return -1;
+}
+// The syntax of sub-block i (scan order; levels s in raster order, at (xs, ys) of the
+// sub-block grid) from coded_sub_block_flag to coeff_abs_level_remaining. right / below:
+// the neighbours' coded_sub_block_flag; first_g1 / c1_in: whether a sub-block with a
+// significant level was coded before in the TU, and the greater1 state it left (HM c1).
+// The state this sub-block leaves is sb_g1's when it holds a level (else unchanged).
+template <class W>
+SK_HD void code_sb(W& w, const Sb4& s, int log2n, int cidx, int scan, int i, int last_i, int last_n, int xs, int ys,
+                   int right, int below, bool first_g1, int c1_in) {
+    bool coded = s.nz();
+    bool infer_dc = false;
+    if (i < last_i && i > 0) {
+        w.ctx(CTX_CSBF + sk_min(1, right + below) + (cidx ? 2 : 0), coded ? 1 : 0);
+        infer_dc = true;
+    } else {
+        coded = true;   // inferred for the DC and last sub-blocks
+    }
+    if (!coded) return;   // no flags beyond coded_sub_block_flag
+    const int prev_csbf = right | (below << 1);
+    Sb4 lev{0, 0, 0, 0};   // the sub-block's levels in scan order (registers, no local array)
+#pragma unroll
+    for (int k = 0; k < 16; k++) lev.set(k, s.at(scan4_raster(scan, k)));
+    // sig_coeff_flag
+    uint32_t sig = 0;
+    const int start = (i == last_i) ? last_n - 1 : 15;
+    if (i == last_i) sig |= 1u << last_n;
+    for (int k = start; k >= 0; k--) {
+        const int r = scan4_raster(scan, k);
+        const int xc = xs * 4 + (r & 3), yc = ys * 4 + (r >> 2);
+        const bool sg = lev.at(k) != 0;
+        if (k == 0 && infer_dc) {   // inferred 1 when no other flag of the sub-block was 1
+            sig |= 1u;
+            break;
+        }
+        int sctx;
+        if (log2n == 2) {   // ctxIdxMap (4x4 TUs)
+            sctx = (int)((0x877886654325410ull >> (4 * ((yc << 2) + xc))) & 15);
+        } else if (xc + yc == 0) {
+            sctx = 0;
+        } else {
+            const int xp = xc & 3, yp = yc & 3;
+            if (prev_csbf == 0) sctx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+            else if (prev_csbf == 1) sctx = yp == 0 ? 2 : (yp == 1 ? 1 : 0);
+            else if (prev_csbf == 2) sctx = xp == 0 ? 2 : (xp == 1 ? 1 : 0);
+            else sctx = 2;
+            if (cidx == 0) {
+                if (xs > 0 || ys > 0) sctx += 3;
+                sctx += log2n == 3 ? (scan == SCAN_DIAG ? 9 : 15) : 21;
+            } else {
+                sctx += log2n == 3 ? 9 : 12;
+            }
+        }
+        w.ctx(CTX_SIG + (cidx == 0 ? sctx : 27 + sctx), sg ? 1 : 0);
+        if (sg) {
+            sig |= 1u << k;
+            infer_dc = false;
+        }
+    }
+    if (!sig) return;
+    // greater1 / greater2
+    int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
+    if (!first_g1 && c1_in == 0) ctx_set++;
+    int g1ctx = 1, ng1 = 0, last_g1_pos = -1;
+    uint32_t g1 = 0;
+    for (int k = 15; k >= 0; k--) {
+        if (!((sig >> k) & 1)) continue;
+        if (ng1 < 8) {
+            const int f = sk_abs(lev.at(k)) > 1;
+            w.ctx(CTX_GT1 + ctx_set * 4 + sk_min(3, g1ctx) + (cidx ? 16 : 0), f);
+            ng1++;
+            if (f) {
+                g1 |= 1u << k;
+                if (last_g1_pos < 0) last_g1_pos = k;
+            }
+            if (g1ctx > 0) g1ctx = f ? 0 : g1ctx + 1;
+        }
+    }
+    int g2 = 0;
+    if (last_g1_pos >= 0) {
+        g2 = sk_abs(lev.at(last_g1_pos)) > 2;
+        w.ctx(CTX_GT2 + ctx_set + (cidx ? 4 : 0), g2);
+    }
+    // signs
+    {
+        uint32_t bits = 0;
+        int nb = 0;
+        for (int k = 15; k >= 0; k--)
+            if ((sig >> k) & 1) {
+                bits = (bits << 1) | (lev.at(k) < 0 ? 1u : 0u);
+                nb++;
+            }
+        // nb <= 16: two bypass runs at most
+        w.bypass(bits, nb);
+    }
+    // coeff_abs_level_remaining
+    int rice = 0, nsig = 0;
+    for (int k = 15; k >= 0; k--) {
+        if (!((sig >> k) & 1)) continue;
+        const int a = sk_abs(lev.at(k));
+        const int base = 1 + (int)((g1 >> k) & 1) + (k == last_g1_pos ? g2 : 0);
+        const int thr = nsig < 8 ? (k == last_g1_pos ? 3 : 2) : 1;
+        if (base == thr) {
+            const uint32_t rem = (uint32_t)(a - base);
+            if (rem < (3u << rice)) {
+                const int len = (int)(rem >> rice);
+                w.bypass((1u << (len + 1)) - 2u, len + 1);
+                if (rice) w.bypass(rem & ((1u << rice) - 1u), rice);
+            } else {
+                uint32_t v = rem - (3u << rice);
+                int len = rice;
+                while (v >= (1u << len)) {
+                    v -= 1u << len;
+                    len++;
+                }
+                const int ones = 3 + len + 1 - rice;   // prefix: (ones - 1) ones then a zero
+                // prefix may exceed 32 bins only for levels far beyond kMaxLevel
+                int pre = ones;
+                while (pre > 0) {
+                    const int k2 = pre > 16 ? 16 : pre;
+                    pre -= k2;
+                    const uint32_t chunk = pre == 0 ? ((1u << k2) - 2u) : ((1u << k2) - 1u);
+                    w.bypass(chunk, k2);
+                }
+                w.bypass(v, len);
+            }
+            if (a > 3 * (1 << rice)) rice = sk_min(rice + 1, 4);
+        }
+        nsig++;
+    }
+}
+
+// residual_coding of one TU from raster levels - or of the sub-blocks with scan index in
+// [lo, hi] only: a CU32's 32x32 and 16x16 TUs are binarised in pieces, one per unit (the
+// units' bin slots are the chunks of the chunk-parallel coder). The piece that holds the
+// last significant sub-block writes the prologue; a later piece starts from the greater1
+// state the sub-blocks coded before it leave (that of the nearest one with a level).
+// A writer with W::kWave set (k_hevc_bins) codes the sub-blocks on the lanes of a wave.
 template <class W, class C>
 SK_HD void code_residual(W& w, C c, int log2n, int cidx, int scan = SCAN_DIAG, int ts = 0, int lo = 0, int hi = 63) {
-    const int n = 1 << log2n;
-    const int sbw = n >> 2;                     // sub-blocks per row
-    const int nsb = sbw * sbw;
-    // last significant coefficient in (sub-block, position) scan order
-    int last_i = -1, last_n = -1;
-    for (int i = nsb - 1; i >= 0 && last_i < 0; i--) {
-        const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
-        for (int k = 15; k >= 0; k--) {
-            const int r = scan4_raster(scan, k);
-            if (c((ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3))) { last_i = i; last_n = k; break; }
+    if constexpr (W::kWave) {
+        w.residual(c, log2n, cidx, scan, ts, lo, hi);
+    } else {
+        const int n = 1 << log2n;
+        const int sbw = n >> 2;                     // sub-blocks per row
+        const int nsb = sbw * sbw;
+        int last_i = -1, last_n = -1;
+        for (int i = nsb - 1; i >= 0; i--) {
+            const int sr = sb_scan_raster(log2n, scan, i);
+            const Sb4 s = load_sb(c, n, sr % sbw, sr / sbw);
+            if (!s.nz()) continue;
+            last_i = i;
+            last_n = sb_last_pos(s, scan);
+            break;
         }
-    }
-    if (last_i < 0) return;   // callers only code TUs with cbf = 1
-    const int i0 = last_i < hi ? last_i : hi;
-    if (i0 < lo) return;      // a piece above the last sub-block: nothing to code
-    if (i0 == last_i) {
-        if (log2n == 2) w.ctx(CTX_TS + (cidx ? 1 : 0), ts);   // transform_skip_flag (PPS enables it)
-        const int lsr = sb_scan_raster(log2n, scan, last_i);
-        int lx = (lsr % sbw) * 4 + (scan4_raster(scan, last_n) & 3);
-        int ly = (lsr / sbw) * 4 + (scan4_raster(scan, last_n) >> 2);
-        if (scan == SCAN_VER) { const int t = lx; lx = ly; ly = t; }   // coded swapped (7.4.9.11)
-        // last_sig_coeff_x/y_prefix (TR, cMax 2*log2n - 1), then suffixes (FL, bypass)
-        const int off = cidx == 0 ? 3 * (log2n - 2) + ((log2n - 1) >> 2) : 15;
-        const int shift = cidx == 0 ? (log2n + 1) >> 2 : log2n - 2;
-        const int cmax = 2 * log2n - 1;
-        const int px = last_prefix(lx), py = last_prefix(ly);
-        for (int b = 0; b < px; b++) w.ctx(CTX_LAST_X + off + (b >> shift), 1);
-        if (px < cmax) w.ctx(CTX_LAST_X + off + (px >> shift), 0);
-        for (int b = 0; b < py; b++) w.ctx(CTX_LAST_Y + off + (b >> shift), 1);
-        if (py < cmax) w.ctx(CTX_LAST_Y + off + (py >> shift), 0);
-        if (px > 3) w.bypass((uint32_t)(lx - last_group_min(px)), (px >> 1) - 1);
-        if (py > 3) w.bypass((uint32_t)(ly - last_group_min(py)), (py >> 1) - 1);
-    }
-    // coded_sub_block_flag per sub-block (raster in the sub-block grid)
-    uint64_t csbf = 0;
-    for (int i = 0; i < nsb; i++) {
-        const int sr = sb_raster(log2n, i), xs = sr % sbw, ys = sr / sbw;   // every sub-block once
-        bool nz = false;
-        for (int k = 0; k < 16 && !nz; k++) nz = c((ys * 4 + (k >> 2)) * n + xs * 4 + (k & 3)) != 0;
-        if (nz) csbf |= 1ull << sr;
-    }
-    int c1_carry = 1;   // greater1 context state carried between sub-blocks (HM c1)
-    bool first_g1_sb = true;
-    for (int i = i0 + 1; i <= last_i && first_g1_sb; i++) {   // a later piece: the state so far
-        const int sr = sb_scan_raster(log2n, scan, i);
-        bool any;
-        const int g = sb_g1_end(c, n, scan, sr % sbw, sr / sbw, &any);
-        if (any) {
-            c1_carry = g;
-            first_g1_sb = false;
+        if (last_i < 0) return;   // callers only code TUs with cbf = 1
+        const int i0 = last_i < hi ? last_i : hi;
+        if (i0 < lo) return;      // a piece above the last sub-block: nothing to code
+        if (i0 == last_i) code_last(w, log2n, cidx, scan, ts, last_i, last_n);
+        // coded_sub_block_flag per sub-block (raster in the sub-block grid). The right / below
+        // neighbours a sub-block's contexts read come later in every scan, and nothing after
+        // last_i is coded: the flags of scan positions lo .. last_i are all that is read.
+        uint64_t csbf = 0;
+        for (int i = lo; i <= last_i; i++) {
+            const int sr = sb_scan_raster(log2n, scan, i);
+            if (load_sb(c, n, sr % sbw, sr / sbw).nz()) csbf |= 1ull << sr;
         }
-    }
-    for (int i = i0; i >= lo; i--) {
-        const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
-        const int right = (xs + 1 < sbw) ? (int)((csbf >> (sr + 1)) & 1) : 0;
-        const int below = (ys + 1 < sbw) ? (int)((csbf >> (sr + sbw)) & 1) : 0;
-        bool coded = (csbf >> sr) & 1;
-        bool infer_dc = false;
-        if (i < last_i && i > 0) {
-            w.ctx(CTX_CSBF + sk_min(1, right + below) + (cidx ? 2 : 0), coded ? 1 : 0);
-            infer_dc = true;
-        } else {
-            coded = true;   // inferred for the DC and last sub-blocks
-        }
-        const int prev_csbf = right | (below << 1);
-        int lev[16];
-        for (int k = 0; k < 16; k++) {
-            const int r = scan4_raster(scan, k);
-            lev[k] = c((ys * 4 + (r >> 2)) * n + xs * 4 + (r & 3));
-        }
-        // sig_coeff_flag
-        uint32_t sig = 0;
-        const int start = (i == last_i) ? last_n - 1 : 15;
-        if (i == last_i) sig |= 1u << last_n;
-        for (int k = start; k >= 0; k--) {
-            if (!coded) break;
-            const int r = scan4_raster(scan, k);
-            const int xc = xs * 4 + (r & 3), yc = ys * 4 + (r >> 2);
-            const bool sg = lev[k] != 0;
-            if (k == 0 && infer_dc) {   // inferred 1 when no other flag of the sub-block was 1
-                sig |= 1u;
-                break;
-            }
-            int sctx;
-            if (log2n == 2) {   // ctxIdxMap (4x4 TUs)
-                sctx = (int)((0x877886654325410ull >> (4 * ((yc << 2) + xc))) & 15);
-            } else if (xc + yc == 0) {
-                sctx = 0;
-            } else {
-                const int xp = xc & 3, yp = yc & 3;
-                if (prev_csbf == 0) sctx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
-                else if (prev_csbf == 1) sctx = yp == 0 ? 2 : (yp == 1 ? 1 : 0);
-                else if (prev_csbf == 2) sctx = xp == 0 ? 2 : (xp == 1 ? 1 : 0);
-                else sctx = 2;
-                if (cidx == 0) {
-                    if (xs > 0 || ys > 0) sctx += 3;
-                    sctx += log2n == 3 ? (scan == SCAN_DIAG ? 9 : 15) : 21;
-                } else {
-                    sctx += log2n == 3 ? 9 : 12;
-                }
-            }
-            w.ctx(CTX_SIG + (cidx == 0 ? sctx : 27 + sctx), sg ? 1 : 0);
-            if (sg) {
-                sig |= 1u << k;
-                infer_dc = false;
+        int c1 = 1;   // greater1 state carried between sub-blocks
+        bool first_g1 = true;
+        for (int i = i0 + 1; i <= last_i && first_g1; i++) {   // a later piece: the state so far
+            const int sr = sb_scan_raster(log2n, scan, i);
+            const Sb4 s = load_sb(c, n, sr % sbw, sr / sbw);
+            if (s.nz()) {
+                c1 = sb_g1(s, scan);
+                first_g1 = false;
             }
         }
-        if (!sig) continue;
-        // greater1 / greater2
-        int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
-        if (!first_g1_sb && c1_carry == 0) ctx_set++;
-        first_g1_sb = false;
-        int g1ctx = 1, ng1 = 0, last_g1_pos = -1;
-        uint32_t g1 = 0;
-        for (int k = 15; k >= 0; k--) {
-            if (!((sig >> k) & 1)) continue;
-            if (ng1 < 8) {
-                const int f = sk_abs(lev[k]) > 1;
-                w.ctx(CTX_GT1 + ctx_set * 4 + sk_min(3, g1ctx) + (cidx ? 16 : 0), f);
-                ng1++;
-                if (f) {
-                    g1 |= 1u << k;
-                    if (last_g1_pos < 0) last_g1_pos = k;
-                }
-                if (g1ctx > 0) g1ctx = f ? 0 : g1ctx + 1;
+        for (int i = i0; i >= lo; i--) {
+            const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
+            const int right = (xs + 1 < sbw) ? (int)((csbf >> (sr + 1)) & 1) : 0;
+            const int below = (ys + 1 < sbw) ? (int)((csbf >> (sr + sbw)) & 1) : 0;
+            const Sb4 s = load_sb(c, n, xs, ys);
+            code_sb(w, s, log2n, cidx, scan, i, last_i, last_n, xs, ys, right, below, first_g1, c1);
+            if (s.nz()) {
+                c1 = sb_g1(s, scan);
+                first_g1 = false;
             }
-        }
-        c1_carry = g1ctx;
-        int g2 = 0;
-        if (last_g1_pos >= 0) {
-            g2 = sk_abs(lev[last_g1_pos]) > 2;
-            w.ctx(CTX_GT2 + ctx_set + (cidx ? 4 : 0), g2);
-        }
-        // signs
-        {
-            uint32_t bits = 0;
-            int nb = 0;
-            for (int k = 15; k >= 0; k--)
-                if ((sig >> k) & 1) {
-                    bits = (bits << 1) | (lev[k] < 0 ? 1u : 0u);
-                    nb++;
-                }
-            // nb <= 16: two bypass runs at most
-            w.bypass(bits, nb);
-        }
-        // coeff_abs_level_remaining
-        int rice = 0, nsig = 0;
-        for (int k = 15; k >= 0; k--) {
-            if (!((sig >> k) & 1)) continue;
-            const int a = sk_abs(lev[k]);
-            const int base = 1 + (int)((g1 >> k) & 1) + (k == last_g1_pos ? g2 : 0);
-            const int thr = nsig < 8 ? (k == last_g1_pos ? 3 : 2) : 1;
-            if (base == thr) {
-                const uint32_t rem = (uint32_t)(a - base);
-                if (rem < (3u << rice)) {
-                    const int len = (int)(rem >> rice);
-                    w.bypass((1u << (len + 1)) - 2u, len + 1);
-                    if (rice) w.bypass(rem & ((1u << rice) - 1u), rice);
-                } else {
-                    uint32_t v = rem - (3u << rice);
-                    int len = rice;
-                    while (v >= (1u << len)) {
-                        v -= 1u << len;
-                        len++;
-                    }
-                    const int ones = 3 + len + 1 - rice;   // prefix: (ones - 1) ones then a zero
-                    // prefix may exceed 32 bins only for levels far beyond kMaxLevel
-                    int pre = ones;
-                    while (pre > 0) {
-                        const int k2 = pre > 16 ? 16 : pre;
-                        pre -= k2;
-                        const uint32_t chunk = pre == 0 ? ((1u << k2) - 2u) : ((1u << k2) - 1u);
-                        w.bypass(chunk, k2);
-                    }
-                    w.bypass(v, len);
-                }
-                if (a > 3 * (1 << rice)) rice = sk_min(rice + 1, 4);
-            }
-            nsig++;
         }
     }
 }
@@ -1378,10 +1444,10 @@ SK_HD void pu_mpm(const UnitCtx& u, const CuInfo& cu, const CuInfo* L, const CuI
                          : ((!u.row0 && u.top && T->mode == CU_INTRA) ? T->ipm[zorder4(bx, 3)] : 1);
     intra_mpm(a, b, mpm);
 }
-// c32: the CTB's four units in z order (used by CU32 units); t32: the CU32's 32x32 TU levels.
+// c32: the CTB's four units in z order with their coefficient slots (read by CU32 units).
 template <class W>
 SK_HD void code_unit(W& w, const UnitCtx& u, const CuInfo& cu, const CuInfo* L, const CuInfo* T, const int16_t* coef,
-                     const CuInfo* c32, const CoefT32& t32) {
+                     const Ctb4& c32) {
     const int skip_ctx = (u.left && L->mode == CU_SKIP) + (u.top && T->mode == CU_SKIP);
     if (u.first && u.complete) {   // CTB split_cu_flag (cqtDepth 0)
         const int ctx = (u.left && cu_depth(*L) > 0) + (u.top && cu_depth(*T) > 0);
@@ -1426,10 +1492,7 @@ SK_HD void code_unit(W& w, const UnitCtx& u, const CuInfo& cu, const CuInfo* L, 
             return;
         }
         // one 32x32 TU: luma sub-blocks 63..40 | 39..16 | 15..0 + Cb 15..8 | Cb 7..0 + Cr
-        CoefT32 ty = t32, tb = t32, tr = t32;
-        ty.base = 0;
-        tb.base = kT32Cb;
-        tr.base = kT32Cr;
+        const CoefT32 ty{c32, 0}, tb{c32, kT32Cb}, tr{c32, kT32Cr};
         if (u.z == 0 && cy) code_residual(w, ty, 5, 0, SCAN_DIAG, 0, 40, 63);
         if (u.z == 1 && cy) code_residual(w, ty, 5, 0, SCAN_DIAG, 0, 16, 39);
         if (u.z == 2 && cy) code_residual(w, ty, 5, 0, SCAN_DIAG, 0, 0, 15);
@@ -1447,14 +1510,15 @@ SK_HD void code_unit(W& w, const UnitCtx& u, const CuInfo& cu, const CuInfo* L, 
         for (int q = 0; q < 4; q++) {
             const int nxn = (cu.cu8 >> q) & 1, npu = nxn ? 4 : 1;
             w.ctx(CTX_PART_MODE, nxn ? 0 : 1);   // intra at MinCb: "1" 2Nx2N, "0" NxN
-            int mpm[4][3], md[4];
-            for (int p = 0; p < npu; p++) {       // every prev_intra_luma_pred_flag first
-                const int bx = 2 * (q & 1) + (nxn ? (p & 1) : 0), by = 2 * (q >> 1) + (nxn ? (p >> 1) : 0);
-                md[p] = cu.ipm[zorder4(bx, by)];
-                pu_mpm(u, cu, L, T, bx, by, mpm[p]);
-                w.ctx(CTX_PREV_INTRA, mpm_hit(md[p], mpm[p]) >= 0);
-            }
-            for (int p = 0; p < npu; p++) code_mpm_rest(w, md[p], mpm[p]);
+            for (int pass = 0; pass < 2; pass++)   // every prev_intra_luma_pred_flag first, then the rest
+                for (int p = 0; p < npu; p++) {
+                    const int bx = 2 * (q & 1) + (nxn ? (p & 1) : 0), by = 2 * (q >> 1) + (nxn ? (p >> 1) : 0);
+                    const int md = cu.ipm[zorder4(bx, by)];
+                    int mpm[3];
+                    pu_mpm(u, cu, L, T, bx, by, mpm);
+                    if (pass == 0) w.ctx(CTX_PREV_INTRA, mpm_hit(md, mpm) >= 0);
+                    else code_mpm_rest(w, md, mpm);
+                }
             w.ctx(CTX_CHROMA_PRED, 0);   // intra_chroma_pred_mode = 4 (DM)
             code_tt8(w, cu, coef, q);
         }

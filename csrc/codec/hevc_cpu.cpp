@@ -790,17 +790,9 @@ void CpuHevcEncoder::binarize_slice(int s) {
             const UnitCtx u = unit_ctx(ug, m, ux, uy, p_slice);
             BinBuf w{&bins[(size_t)idx * kCuBinCap], 0};
             if (u.first) sao_bins(w, sao[r * geo.ctb_w + c], m.left(c, r), m.top(c, r));   // CTB-level SAO syntax
-            CuInfo c32[4];
-            CoefT32 t32;
-            t32.base = 0;
-            for (int k = 0; k < 4; k++) {
-                const int kx = 2 * c + (k & 1), ky = 2 * r + (k >> 1);
-                const int ki = ug.inside(kx, ky) ? ky * W + kx : idx;
-                c32[k] = cus[ki];
-                t32.slot[k] = &coefs[(size_t)ki * kCoefPerCu];
-            }
+            const size_t i0 = (size_t)2 * r * W + 2 * c;   // the CTB's unit z0
             code_unit(w, u, cus[idx], u.left ? &cus[idx - 1] : nullptr, u.top ? &cus[idx - W] : nullptr,
-                      &coefs[(size_t)idx * kCoefPerCu], c32, t32);
+                      &coefs[(size_t)idx * kCoefPerCu], Ctb4{&cus[i0], &coefs[i0 * kCoefPerCu], W});
             if (ctb_last_unit(ug, ux, uy)) {
                 // end_of_slice_segment_flag: the last CTB of the slice (a split row: of its segment)
                 const bool end = m.split(r) ? c + 1 == m.x1(r, m.seg(c, r)) : r == r1 - 1 && c == geo.ctb_w - 1;

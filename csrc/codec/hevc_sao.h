@@ -271,7 +271,8 @@ SK_HD void sao_row_merge(const long long* md_row, const SaoParams* own, const lo
 
 // CTB syntax sao(rx, ry) (7.3.8.3) as bin entries. left/up: the neighbour CTB exists in
 // this slice.
-SK_HD void sao_bins(BinBuf& w, const SaoParams& p, bool left, bool up) {
+template <class W>
+SK_HD void sao_bins(W& w, const SaoParams& p, bool left, bool up) {
     if (left) w.ctx(CTX_SAO_MERGE, p.merge_left);
     if (p.merge_left) return;
     if (up) w.ctx(CTX_SAO_MERGE, 0);

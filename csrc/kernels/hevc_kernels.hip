@@ -399,60 +399,116 @@ __device__ int t32_res(CuLds* Lw, int i) {
     t32_where(i, &z, &o);
     return (int)Lw[z].src[o] - (int)Lw[z].pred[o];
 }
+// Element k of thread t: i = t + 256 k; k 0..3 luma, 4 Cb, 5 Cr (TU boundaries are multiples
+// of 256, so the TU is uniform per k). Sums go per wave through shuffles, then one LDS atomic.
+__device__ __forceinline__ void t32_add(int* dst, int v) {
+    v = wsum(v);
+    if (lane() == 0 && v) atomicAdd(dst, v);
+}
+// Row-contiguous access: the 32 (16) entries of a TU row never straddle a 256-int chunk.
+__device__ __forceinline__ const int* t32_rowA(CuLds* Lw, int i) { return &t32_A(Lw, i); }
+__device__ __forceinline__ const int* t32_rowB(CuLds* Lw, int i) { return &t32_B(Lw, i); }
+// Column sum over a TU of the chunked array X (A or B): sum_y M[y] X[base + y n + u], the
+// chunk pointer fetched once per 256 / n rows.
+template <bool IsB>
+__device__ __forceinline__ int t32_colsum(CuLds* Lw, const int8_t* Mrow, int mstride, int base, int log2n, int u) {
+    const int n = 1 << log2n, rpc = 256 >> log2n;
+    int sum = 0;
+    for (int y0 = 0; y0 < n; y0 += rpc) {
+        const int* p = IsB ? &t32_B(Lw, base + y0 * n + u) : &t32_A(Lw, base + y0 * n + u);
+        for (int y = 0; y < rpc; y++) sum += (int)Mrow[(y0 + y) * mstride] * p[y * n];
+    }
+    return sum;
+}
 // Returns the cbf bits; *J the trial's RD cost (every thread).
 __device__ int tu32_trial(CuLds* Lw, const int8_t* T32, int qp, int lam, T32Acc& acc, long long* J) {
     const int t = threadIdx.x, qpc = chroma_qp(qp);
     if (t < 3) acc.sse0[t] = acc.sse1[t] = acc.rate[t] = acc.nz[t] = 0;
     __syncthreads();
-    auto M = [&](int log2n, int k, int m) { return (int)T32[(log2n == 5 ? k : 2 * k) * 32 + m]; };
+    // the residual into B (free until the dequantised levels), the zero-residual SSE
+    {
+        int s0[3] = {0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int i = t + 256 * k, e = t32_res(Lw, i);
+            t32_B(Lw, i) = e;
+            s0[k < 4 ? 0 : k - 3] += e * e;
+        }
+#pragma unroll
+        for (int tu = 0; tu < 3; tu++) t32_add(&acc.sse0[tu], s0[tu]);
+    }
+    __syncthreads();
     // forward, rows: A[tu][y][u] = (sum_x M[u][x] res[y][x] + rnd) >> sh1
-    for (int i = t; i < kT32Coefs; i += 256) {
-        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
-        const int j = i - base, y = j >> log2n, u = j & (n - 1), sh1 = log2n - 1;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const int i = t + 256 * k, tu = k < 4 ? 0 : k - 3, log2n = tu ? 4 : 5, n = 1 << log2n;
+        const int base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr), sh1 = log2n - 1;
+        const int j = i - base, y = j >> log2n, u = j & (n - 1);
+        const int* rp = t32_rowB(Lw, base + y * n);
+        const int8_t* Mr = T32 + (tu ? 2 * u : u) * 32;
         int sum = 0;
-        for (int x = 0; x < n; x++) sum += M(log2n, u, x) * t32_res(Lw, base + y * n + x);
+        for (int x = 0; x < n; x++) sum += (int)Mr[x] * rp[x];
         t32_A(Lw, i) = (sum + (1 << (sh1 - 1))) >> sh1;
-        const int e = t32_res(Lw, i);
-        atomicAdd(&acc.sse0[tu], e * e);
     }
     __syncthreads();
     // forward, columns + quantisation + dequantisation
-    for (int i = t; i < kT32Coefs; i += 256) {
-        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
-        const int j = i - base, v = j >> log2n, u = j & (n - 1), sh2 = log2n + 6, q = tu ? qpc : qp;
-        int sum = 0;
-        for (int y = 0; y < n; y++) sum += M(log2n, v, y) * t32_A(Lw, base + y * n + u);
-        const int lv = quant_level((sum + (1 << (sh2 - 1))) >> sh2, q, log2n, false);
-        t32_L(Lw, i) = (int16_t)lv;
-        t32_B(Lw, i) = dequant_level(lv, q, log2n);
-        if (lv) {
-            atomicAdd(&acc.rate[tu], level_rate_half(lv));
-            atomicOr(&acc.nz[tu], 1);
+    {
+        int rate[3] = {0, 0, 0}, nz[3] = {0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int i = t + 256 * k, tu = k < 4 ? 0 : k - 3, log2n = tu ? 4 : 5, n = 1 << log2n;
+            const int base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr), sh2 = log2n + 6, q = tu ? qpc : qp;
+            const int j = i - base, v = j >> log2n, u = j & (n - 1);
+            // M[v][y] for y = 0..n-1: row v of the matrix (stride 1)
+            const int sum = t32_colsum<false>(Lw, T32 + (tu ? 2 * v : v) * 32, 1, base, log2n, u);
+            const int lv = quant_level((sum + (1 << (sh2 - 1))) >> sh2, q, log2n, false);
+            t32_L(Lw, i) = (int16_t)lv;
+            // B is read by other threads' row pass only before the barrier above: free now
+            t32_B(Lw, i) = dequant_level(lv, q, log2n);
+            if (lv) {
+                rate[k < 4 ? 0 : k - 3] += level_rate_half(lv);
+                nz[k < 4 ? 0 : k - 3] = 1;
+            }
+        }
+#pragma unroll
+        for (int tu = 0; tu < 3; tu++) {
+            t32_add(&acc.rate[tu], rate[tu]);
+            t32_add(&acc.nz[tu], nz[tu]);
         }
     }
     __syncthreads();
     // inverse, columns: A = clip16((sum_j M[j][y] B[j][x] + 64) >> 7)
-    for (int i = t; i < kT32Coefs; i += 256) {
-        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const int i = t + 256 * k, tu = k < 4 ? 0 : k - 3, log2n = tu ? 4 : 5, n = 1 << log2n;
+        const int base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
         const int j = i - base, y = j >> log2n, x = j & (n - 1);
-        int sum = 0;
-        if (acc.nz[tu])
-            for (int k = 0; k < n; k++) sum += M(log2n, k, y) * t32_B(Lw, base + k * n + x);
+        // M[j][y] for j = 0..n-1: column y of the matrix (stride 32, or 64 for the 16-point rows)
+        const int sum = acc.nz[tu] ? t32_colsum<true>(Lw, T32 + y, tu ? 64 : 32, base, log2n, x) : 0;
         t32_A(Lw, i) = sk_clip((sum + 64) >> 7, -32768, 32767);
     }
     __syncthreads();
     // inverse, rows + reconstruction (into the units' recA)
-    for (int i = t; i < kT32Coefs; i += 256) {
-        const int tu = t32_tu(i), log2n = tu ? 4 : 5, n = 1 << log2n, base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
-        const int j = i - base, y = j >> log2n, x = j & (n - 1);
-        int sum = 0;
-        for (int k = 0; k < n; k++) sum += M(log2n, k, x) * t32_A(Lw, base + y * n + k);
-        int z, o;
-        t32_where(i, &z, &o);
-        const int rv = sk_clip255((int)Lw[z].pred[o] + ((sum + 2048) >> 12));
-        Lw[z].recA[o] = (uint8_t)rv;
-        const int e = (int)Lw[z].src[o] - rv;
-        atomicAdd(&acc.sse1[tu], e * e);
+    {
+        int s1[3] = {0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const int i = t + 256 * k, tu = k < 4 ? 0 : k - 3, log2n = tu ? 4 : 5, n = 1 << log2n;
+            const int base = tu == 0 ? 0 : (tu == 1 ? kT32Cb : kT32Cr);
+            const int j = i - base, y = j >> log2n, x = j & (n - 1);
+            const int* rp = t32_rowA(Lw, base + y * n);
+            const int ms = tu ? 64 : 32;
+            int sum = 0;
+            for (int kk = 0; kk < n; kk++) sum += (int)T32[kk * ms + x] * rp[kk];
+            int z, o;
+            t32_where(i, &z, &o);
+            const int rv = sk_clip255((int)Lw[z].pred[o] + ((sum + 2048) >> 12));
+            Lw[z].recA[o] = (uint8_t)rv;
+            const int e = (int)Lw[z].src[o] - rv;
+            s1[k < 4 ? 0 : k - 3] += e * e;
+        }
+#pragma unroll
+        for (int tu = 0; tu < 3; tu++) t32_add(&acc.sse1[tu], s1[tu]);
     }
     __syncthreads();
     long long jt = 0;
@@ -460,14 +516,16 @@ __device__ int tu32_trial(CuLds* Lw, const int8_t* T32, int qp, int lam, T32Acc&
     for (int tu = 0; tu < 3; tu++) {   // RD zeroing (code_tu_1's rule), every thread alike
         const long long s0 = acc.sse0[tu], s1 = acc.sse1[tu];
         const int rate = kTuRateHalf + acc.rate[tu];
-        int nz = acc.nz[tu];
+        int nz = acc.nz[tu] != 0;
         if (nz && 512 * s0 <= 512 * s1 + (long long)lam * rate) nz = 0;
         keep[tu] = nz;
         cbf |= nz << tu;
         jt += nz ? 512 * s1 + (long long)lam * rate : 512 * s0;
     }
-    for (int i = t; i < kT32Coefs; i += 256) {   // zeroed TUs: no levels, reconstruction = prediction
-        if (keep[t32_tu(i)]) continue;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {   // zeroed TUs: no levels, reconstruction = prediction
+        const int i = t + 256 * k;
+        if (keep[k < 4 ? 0 : k - 3]) continue;
         int z, o;
         t32_where(i, &z, &o);
         t32_L(Lw, i) = 0;
@@ -1181,17 +1239,90 @@ __global__ __launch_bounds__(256) void k_hevc_intra_seg(HevcArgs A) {
 
 // ---------------------------------------------------------------------------
 // Unit syntax -> bin entries (hevc_cpu.cpp binarize_slice: SAO of the CTB at its first
-// unit, code_unit, end_of_slice_segment_flag / end_of_subset_one_bit after its last):
-// one thread per unit, `lpw` units per wave. The lanes diverge (each binarises its own
-// unit's coefficients), so a wave runs about as long as its busiest unit.
-__global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A, int lpw) {
+// unit, code_unit, end_of_slice_segment_flag / end_of_subset_one_bit after its last): one
+// wave per unit. The CU syntax runs wave-uniform (lane 0 stores); each TU's residual runs
+// sub-block-parallel, lane j = sub-block j of the scan: every lane derives its sub-block's
+// coded_sub_block_flag neighbours and entering greater1 state from ballots / shuffles, counts
+// its entries, and writes them at its offset in coding order (descending j) after a wave
+// scan. The same code_last / code_sb as the CPU's serial code_residual: identical bins.
+__device__ __forceinline__ uint64_t wor64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+        v |= ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+struct WaveBinBuf {
+    static constexpr bool kWave = true;
+    uint16_t* p;
+    int n;   // wave-uniform
+    __device__ __forceinline__ void ctx(int c, int b) {
+        if (lane() == 0) p[n] = (uint16_t)(((b & 1) << 8) | c);
+        n++;
+    }
+    __device__ __forceinline__ void term(int b) {
+        if (lane() == 0) p[n] = (uint16_t)(((b & 1) << 8) | CTX_TERM);
+        n++;
+    }
+    __device__ __forceinline__ void bypass(uint32_t v, int nb) {
+        if (lane() == 0) {
+            BinBuf t{p, n};
+            t.bypass(v, nb);
+        }
+        n += (nb + 7) >> 3;
+    }
+    template <class C>
+    __device__ void residual(C c, int log2n, int cidx, int scan, int ts, int lo, int hi) {
+        const int j = lane(), n4 = 1 << log2n, sbw = n4 >> 2, nsb = sbw * sbw;
+        int sr = 0, xs = 0, ys = 0;
+        Sb4 s{0, 0, 0, 0};
+        if (j < nsb) {
+            sr = sb_scan_raster(log2n, scan, j);
+            xs = sr % sbw;
+            ys = sr / sbw;
+            s = load_sb(c, n4, xs, ys);
+        }
+        const bool nz = j < nsb && s.nz();
+        const uint64_t M = __ballot(nz);
+        if (!M) return;   // callers only code TUs with cbf = 1
+        const int last_i = 63 - __builtin_clzll(M);
+        const int last_n = __shfl(nz ? sb_last_pos(s, scan) : 0, last_i);
+        const int i0 = last_i < hi ? last_i : hi;
+        if (i0 < lo) return;   // a piece above the last sub-block
+        if (i0 == last_i) code_last(*this, log2n, cidx, scan, ts, last_i, last_n);
+        const uint64_t cs = wor64(nz ? 1ull << sr : 0ull);   // coded_sub_block_flags, raster
+        const int right = (xs + 1 < sbw) ? (int)((cs >> (sr + 1)) & 1) : 0;
+        const int below = (ys + 1 < sbw) ? (int)((cs >> (sr + sbw)) & 1) : 0;
+        // the greater1 state entering sub-block j: that of the nearest sub-block above j
+        // (coded before it) holding a level
+        const int g = nz ? sb_g1(s, scan) : 0;
+        const uint64_t above = M & ~((2ull << j) - 1);   // j = 63: 2 << 63 wraps to 0, mask 0
+        const int c1 = __shfl(g, above ? __builtin_ctzll(above) : j);
+        const bool act = j >= lo && j <= i0;
+        BinCount bc;
+        if (act) code_sb(bc, s, log2n, cidx, scan, j, last_i, last_n, xs, ys, right, below, above == 0, c1);
+        int incl = bc.n;   // inclusive prefix over lanes 0..j
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o);
+            if (j >= o) incl += t;
+        }
+        const int total = __shfl(incl, 63);
+        if (act) {
+            BinBuf wb{p, n + total - incl};   // after the entries of the lanes above j
+            code_sb(wb, s, log2n, cidx, scan, j, last_i, last_n, xs, ys, right, below, above == 0, c1);
+        }
+        n += total;
+    }
+};
+
+__global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int n = f.mb_w * f.mb_h;
-    const int l = threadIdx.x & 63;
-    if (l >= lpw) return;
-    const int idx = (blockIdx.x * 4 + (threadIdx.x >> 6)) * lpw + l;
-    if (idx >= n) return;
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (idx >= n) return;   // wave-uniform
     const int W = f.mb_w;
     const int ux = idx % W, uy = idx / W, c = ux >> 1, r = uy >> 1;
     const SliceTask t = ctb_task(A, r);
@@ -1206,22 +1337,13 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A, int lpw) {
     u.top = ug.avail(m, ux, uy, ux, uy - 1);
     u.row0 = (uy & 1) == 0;
     u.p_slice = p_slice;
-    const CuInfo cu = A.cus[idx];
-    CuInfo c32[4];
-    CoefT32 t32;
-    t32.base = 0;
-    for (int k = 0; k < 4; k++) {
-        const int kx = 2 * c + (k & 1), ky = 2 * r + (k >> 1);
-        const int ki = ug.inside(kx, ky) ? ky * W + kx : idx;
-        if (cu.c32 & kC32) c32[k] = A.cus[ki];
-        t32.slot[k] = A.coefs + (size_t)ki * kCoefPerCu;
-    }
-    CuInfo Lc, Tc;
-    if (u.left) Lc = A.cus[idx - 1];
-    if (u.top) Tc = A.cus[idx - W];
-    BinBuf w{A.bins + (size_t)idx * kCuBinCap, 0};
+    const CuInfo& cu = A.cus[idx];
+    const size_t i0 = (size_t)2 * r * W + 2 * c;   // the CTB's unit z0
+    WaveBinBuf w{A.bins + (size_t)idx * kCuBinCap, 0};
     if (u.first) sao_bins(w, A.sao[r * A.cw + c], m.left(c, r), m.top(c, r));   // CTB-level SAO syntax
-    code_unit(w, u, cu, &Lc, &Tc, A.coefs + (size_t)idx * kCoefPerCu, c32, t32);
+    // neighbours and the CU32's units are read in place (no private copies: no scratch)
+    code_unit(w, u, cu, A.cus + idx - 1, A.cus + idx - W, A.coefs + (size_t)idx * kCoefPerCu,
+              Ctb4{A.cus + i0, A.coefs + i0 * kCoefPerCu, W});
     bool last = true;   // the CTB's last unit in coding order
     for (int k = u.z + 1; k < 4; k++) last &= !ug.inside(2 * c + (k & 1), 2 * r + (k >> 1));
     if (last) {
@@ -1233,7 +1355,7 @@ __global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A, int lpw) {
             if (r != r1 && c == A.cw - 1) w.term(1);   // end_of_subset_one_bit closes the row's substream
         }
     }
-    A.bin_n[idx] = w.n;
+    if (lane() == 0) A.bin_n[idx] = w.n;
 }
 
 // Lane `ln` (wave-uniform) of `v` takes the uniform value `x`: v_writelane_b32 with the
@@ -2186,8 +2308,7 @@ static void launch_code(const HevcArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_hevc_sao_stats, dim3(ncq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sao_md, dim3((nc * kSaoMd + 255) / 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sao_row, dim3(a.ch), dim3(64), 0, s, a);
-    static const int lpw = getenv("SK_HEVC_BINS_LPW") ? sk_clip(atoi(getenv("SK_HEVC_BINS_LPW")), 1, 64) : 32;
-    hipLaunchKernelGGL(k_hevc_bins, dim3((n + 4 * lpw - 1) / (4 * lpw)), dim3(256), 0, s, a, lpw);
+    hipLaunchKernelGGL(k_hevc_bins, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(192), 0, s, a);
     hipLaunchKernelGGL(k_pc_model, dim3(slots, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);

@@ -201,9 +201,14 @@ def test_server_control_endpoints(tmp_path, monkeypatch):
             async with sess.ws_connect(f"http://127.0.0.1:{port}/websocket") as ws:
                 await ws.send_str(_settings())
                 await _recv_until(ws, lambda m: isinstance(m, bytes))
-                async with sess.get(f"http://127.0.0.1:{port}/api/placement") as r:
-                    doc = await r.json()
-                d = doc["displays"]["primary"]
+                # the native frame counter moves after the packet callback: poll briefly
+                for _ in range(50):
+                    async with sess.get(f"http://127.0.0.1:{port}/api/placement") as r:
+                        doc = await r.json()
+                    d = doc["displays"]["primary"]
+                    if d["frames"] >= 1:
+                        break
+                    await asyncio.sleep(0.1)
                 assert d["width"] == 256 and d["height"] == 128 and d["frames"] >= 1
                 async with sess.post(f"http://127.0.0.1:{port}/api/move", params={"gpu": "1"}) as r:
                     assert r.status == 409 and "CPU" in (await r.json())["error"]
