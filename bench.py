@@ -65,6 +65,10 @@ def parse():
                         "3840x2160 AV1 session (config 5, 120 fps), each timed over --extra-steps frames and "
                         "reported as extra keys (0 = skip)")
     p.add_argument("--extra-steps", type=int, default=60)
+    p.add_argument("--extra-8k", type=int, default=1,
+                   help="after the 4K extras: one 7680x4320 HEVC session at 60 fps and one 7680x4320 AV1 session "
+                        "at 60 fps (the reference's largest display, selkies.py:266) on ONE GPU, --extra-steps / 2 "
+                        "frames each (0 = skip)")
     p.add_argument("--jpeg-quality", type=int, default=40)
     p.add_argument("--deblock", type=int, default=0,
                    help="H.264 in-loop deblocking filter (1 on; default off like the reference's x264 ultrafast preset)")
@@ -681,6 +685,11 @@ def main():
         # the same under CBR (the reference's x265enc runs with a bitrate, gstwebrtc_app.py:667-683)
         extras["hevc_4k_cbr"] = run_extra(args, 3840, 2160, "hevc", 60, local_rank, args.extra_steps, cbr_kbps=20000)
         extras["av1_4k"] = run_extra(args, 3840, 2160, "av1", 120, local_rank, 2 * args.extra_steps)
+    if args.extra_8k and args.backend == "hip" and not args.gather and rank == 0:
+        # one 8K display (MAX_W x MAX_H of the reference's resize path) on one GPU, 60 fps
+        extras["hevc_8k"] = run_extra(args, 7680, 4320, "hevc", 60, local_rank, max(args.extra_steps // 2, 4))
+        extras["av1_8k"] = run_extra(args, 7680, 4320, "av1", 60, local_rank, max(args.extra_steps // 2, 4))
+    if args.extra_4k and args.backend == "hip" and not args.gather and rank == 0:
         # BASELINE config 1 (640x480@30, software H.264 plumbing): the CPU reference encoder
         # through the same capture loop, no GPU involved
         extras["cpu_480p"] = run_extra(args, 640, 480, "h264", 30, local_rank, args.extra_steps, backend="cpu")

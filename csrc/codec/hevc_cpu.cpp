@@ -142,7 +142,7 @@ CpuHevcEncoder::CpuHevcEncoder(const h264::EncoderConfig& cfg) : fe(front_config
     sao_cost.assign(nc, 0);
     sao_md.assign((size_t)nc * kSaoMd, 0);
     build_parameter_sets(fe.g.W, fe.g.H, cfg.full_range, cfg.fps, param_sets);
-    seg_k = intra_seg_k(geo.ctb_w);
+    seg_k = intra_seg_k(geo.ctb_w, geo.ctb_h);
 }
 
 void CpuHevcEncoder::load_cu_src(int cx, int cy, uint8_t* y, uint8_t* u, uint8_t* v) const {

@@ -118,18 +118,21 @@ SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float f
 SK_HD int rc_clamp_qp(const RcState& rc, int qp) { return sk_clip(qp, rc.qp_min, sk_min(rc.qp_max, 51)); }
 
 
-// Per-frame cap of a non-key frame: the VBV (1.5 frame intervals, the reference's
-// x264enc / x265enc setting, legacy/gstwebrtc_app.py:101-105, 633) and never above 1.5
-// budgets even when the buffer is longer (AV1's 120 ms, svtav1enc buf-optimal-sz
-// :738): a frame several budgets large stalls the link for several frame intervals.
+// Per-frame cap of a non-key frame. A short buffer (vbv_ms 0: 1.5 frame intervals, the
+// reference's x264enc / x265enc setting, legacy/gstwebrtc_app.py:101-105, 633): the VBV
+// itself. A long buffer (AV1: 120 ms, svtav1enc buf-optimal-sz, :738) is a leaky bucket:
+// the frame may fill the buffer but not overflow it (fullness + bits - budget <= size),
+// and never above 2.5 budgets (svtav1enc maxsection-pct=250): an empty buffer lets a busy
+// frame through at up to 2.5 budgets, a full one holds it to one budget.
 // A little under the cap because the packets add stripe headers and NAL framing (~2 %
 // at 1080p). Key frames (IDR) may use 4 budgets (their target is 3).
 SK_HD long long rc_frame_cap(const RcState& rc, bool key) {
     if (key) return 4ll * rc.budget;
-    const long long vbv = sk_min((long long)rc.vbv_size, (long long)rc.budget + rc.budget / 2);
-    // a long buffer (AV1) keeps a thinner margin under 1.5 budgets: its 4K120 frames swing
-    // +-30 % at one qindex and every re-code is a second coding pass inside the frame interval
-    return vbv - (rc.vbv_ms > 0 ? rc.budget / 32 : rc.budget / 16);
+    if (rc.vbv_ms > 0) {
+        const long long room = (long long)rc.vbv_size - rc.fullness + rc.budget;   // >= budget
+        return sk_min(room, 5ll * rc.budget / 2) - rc.budget / 32;
+    }
+    return (long long)rc.vbv_size - rc.budget / 16;
 }
 
 // QP whose lambda prices motion vectors in the motion search, which runs before the
@@ -166,12 +169,13 @@ SK_HD int rc_frame_qpf(RcState& rc, long long cplx_sum, int coded_mbs, bool intr
     } else if (rc.mode == RC_CBR) {
         int target = rc.budget + (rc.vbv_size / 2 - rc.fullness) / 4;
         // key frames (IDR) may use 3 budgets and are paid back by the frames after
-        // them; every other frame, scene-cut intra pictures included, stays under 1.25x
-        // (a long buffer, AV1's 120 ms: 1.0625x, its frames vary +-30 % at one qindex and
-        // the per-frame cap is 1.5 budgets; aiming at 1.25x re-coded every 4th frame of
-        // the 4K120 bench content, 1.125x every 8th)
+        // them; every other frame, scene-cut intra pictures included, stays under 1.25x.
+        // A long buffer (AV1's 120 ms) drains an under-full buffer back towards half full
+        // at up to 1.5 budgets per frame (its frames vary +-30 % at one qindex, under the
+        // 2.5-budget cap) and never aims above the budget when it is over half full.
         if (idr) target = sk_max(target, 3 * rc.budget);
-        else target = sk_min(target, rc.budget + (rc.vbv_ms > 0 ? rc.budget / 16 : rc.budget / 4));
+        else if (rc.vbv_ms > 0) target = sk_min(target, rc.budget + rc.budget / 2);
+        else target = sk_min(target, rc.budget + rc.budget / 4);
         target = sk_max(target, rc.budget / 4);
         if (target < 64) target = 64;
         if (rc.last_bits[k] > 0) {

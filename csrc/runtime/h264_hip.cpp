@@ -768,7 +768,7 @@ class HipBackend : public EncoderBackend {
         h.bin_n = dmalloc<int>(n);
         // intra slices: seg_k slices per CTB row (hevc_core.h SliceMap); per-substream
         // arrays hold ch * seg_k slots
-        h.seg_k = hevc::intra_seg_k(h.cw);
+        h.seg_k = hevc::intra_seg_k(h.cw, h.ch);
         if (h.rps * h.seg_k > 256) throw std::runtime_error("HEVC: more than 256 row segments per slice");
         const size_t slots = (size_t)h.ch * h.seg_k;
         h.sync = dmalloc<uint8_t>(slots * hevc::CTX_COUNT);

@@ -574,7 +574,7 @@ class H264Encoder:
 
 class HevcEncoder(H264Encoder):
     """HEVC Main encoder session: full-frame pictures whose slices are stripes of whole
-    16x16-CTB rows (WPP substreams), same front end as the H.264 encoder. Packets carry
+    32x32-CTB rows (WPP substreams), same front end as the H.264 encoder. Packets carry
     the 10-byte stripe header + Annex-B (VPS/SPS/PPS on IDR)."""
 
     def __init__(self, width: int, height: int, **kw):

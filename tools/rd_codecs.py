@@ -69,6 +69,9 @@ def main():
     ap.add_argument("--backend", default="cpu", choices=("cpu", "hip"))
     ap.add_argument("--content", default="motion,desktop")
     ap.add_argument("--json", default="")
+    ap.add_argument("--vs", default="", metavar="TABLE.md",
+                    help="an earlier run's markdown table (e.g. profiles/r5_rd_codecs_1080p.md): also print each "
+                         "codec's BD-rate against the same codec there")
     ap.add_argument("--ab", default="", metavar="CODEC:ENV",
                     help="A/B one encoder tool: CODEC with ENV=0 (tool off) against the default (on), "
                          "e.g. av1:SK_AV1_PALETTE; prints the tool's BD-rate")
@@ -121,6 +124,26 @@ def main():
     print("|---|---|---|")
     for kind, cs in out.items():
         print(f"| {kind} | {bd_rate(cs['h264'], cs['hevc']):+.1f} % | {bd_rate(cs['h264'], cs['av1']):+.1f} % |")
+    if a.vs:
+        old = read_table(a.vs, a.frames)
+        print(f"\nBD-rate against the same codec in `{a.vs}` (negative = fewer bytes at equal Y-PSNR):\n")
+        print("| content | H.264 | HEVC | AV1 |")
+        print("|---|---|---|---|")
+        for kind, cs in out.items():
+            cells = [f"{bd_rate(old[kind][c], cs[c]):+.1f} %" if old.get(kind, {}).get(c) else "-"
+                     for c in ("h264", "hevc", "av1")]
+            print(f"| {kind} | " + " | ".join(cells) + " |")
+
+
+def read_table(path, frames):
+    """Rows `| content | codec | QP | bytes/frame | Y-PSNR dB |` of an earlier run's table."""
+    out = {}
+    for line in open(path):
+        f = [x.strip() for x in line.strip().strip("|").split("|")]
+        if len(f) == 5 and f[1] in ("h264", "hevc", "av1") and f[2].isdigit():
+            out.setdefault(f[0], {}).setdefault(f[1], []).append(
+                {"qp": int(f[2]), "bytes": float(f[3]) * frames, "psnr": float(f[4])})
+    return out
 
 
 if __name__ == "__main__":
