@@ -70,8 +70,9 @@ def parse():
                         "at 60 fps (the reference's largest display, selkies.py:266) on ONE GPU, --extra-steps / 2 "
                         "frames each (0 = skip)")
     p.add_argument("--jpeg-quality", type=int, default=40)
-    p.add_argument("--deblock", type=int, default=0,
-                   help="H.264 in-loop deblocking filter (1 on; default off like the reference's x264 ultrafast preset)")
+    p.add_argument("--deblock", default="auto", choices=["0", "1", "auto"],
+                   help="H.264 in-loop deblocking filter: 1 on, 0 off, auto (the default, as the server runs it): "
+                        "the slices coded at QP >= 34 (off at CRF 25 like the reference's x264 ultrafast preset)")
     p.add_argument("--me-full", type=int, default=1, help="H.264 MFMA +-16 exhaustive search candidate (1 on, 0 off)")
     p.add_argument("--bands", type=int, default=1,
                    help="encode each session's frame as N bands of stripes on this GPU (parallel/banded.py): "
@@ -376,6 +377,11 @@ def run_extra(args, W, H, encoder, fps, local_rank, steps, backend=None, cbr_kbp
         return {"resolution": f"{W}x{H}", "encoder": encoder, "error": f"{type(ex).__name__}: {ex}"}
 
 
+def deblock_arg(args):
+    """--deblock as the encoder API takes it (True / False / "auto")."""
+    return "auto" if args.deblock == "auto" else args.deblock == "1"
+
+
 def rc_desc(args) -> str:
     """Rate control of a run, as quoted in the JSON config."""
     return f"CBR {args.kbps} kbit/s" if args.rc == "cbr" else f"{args.rc.upper()} {args.qp}"
@@ -394,7 +400,7 @@ def run_dist_bands(args, torch, dist, rank, world, local_rank):
         for i in range(args.pool):
             pool[i].copy_(torch.from_numpy(src.frame(i)))
     enc = DistBandedEncoder(W, H, stripe_height=args.stripe_height, backend=args.backend, qp=args.qp,
-                            use_paint_over=False, deblock=bool(args.deblock), me_full=bool(args.me_full))
+                            use_paint_over=False, deblock=deblock_arg(args), me_full=bool(args.me_full))
 
     def sync():
         if args.backend == "hip":
@@ -524,13 +530,13 @@ def main():
         if args.bands > 1:
             from selkies_gstreamer_amd.parallel.banded import BandedH264Encoder
             encs = [BandedH264Encoder(W, H, [local_rank] * args.bands, stripe_height=args.stripe_height, qp=args.qp,
-                                      use_paint_over=False, backend=args.backend, deblock=bool(args.deblock),
+                                      use_paint_over=False, backend=args.backend, deblock=deblock_arg(args),
                                       me_full=bool(args.me_full))
                     for _ in range(S)]
         else:
             encs = [H264Encoder(W, H, stripe_height=args.stripe_height, fullframe=args.mode == "fullframe",
                                 qp=args.qp, use_paint_over=False, device=local_rank, backend=args.backend,
-                                deblock=bool(args.deblock), me_full=bool(args.me_full), num_refs=args.num_refs,
+                                deblock=deblock_arg(args), me_full=bool(args.me_full), num_refs=args.num_refs,
                                 rate_control=args.rc, bitrate_kbps=args.kbps if args.rc == "cbr" else 0)
                     for _ in range(S)]
 
@@ -744,7 +750,7 @@ def main():
                 "parallelism": f"session-parallel dp{n_gpus} x {S} sessions/GPU",
                 "resolution": f"{W}x{H}",
                 "backend": args.backend,
-                "deblock": bool(args.deblock) if args.encoder == "h264" else None,
+                "deblock": args.deblock if args.encoder == "h264" else None,
                 "me_full": bool(args.me_full) if args.encoder == "h264" else None,
                 "bands_per_session": args.bands,
                 "path": args.path,

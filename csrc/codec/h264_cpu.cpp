@@ -714,7 +714,7 @@ std::vector<std::vector<uint8_t>> CpuH264Encoder::write_slice(int s) {
         h.frame_num = h.idr ? 0 : t.frame_num;
         h.idr_pic_id = t.idr_pic_id;
         h.slice_qp = t.qp;
-        h.deblock = cfg.deblock;
+        h.deblock = slice_deblock(cfg.deblock, t);
         h.num_refs = intra ? 1 : t.num_refs;
         write_slice_header(w, h);
         if (t.final_action == ACT_SKIPALL) {
@@ -799,7 +799,7 @@ void CpuH264Encoder::finish_frame() {
         for (int p = 1; p < 3; p++)
             memcpy(&ref[p][(size_t)(y0 / 2) * g.stride_c], &rec[p][(size_t)(y0 / 2) * g.stride_c],
                    (size_t)(y1 - y0) / 2 * g.stride_c);
-        if (cfg.deblock) {  // K7: the reference picture is the deblocked reconstruction
+        if (slice_deblock(cfg.deblock, t)) {  // K7: the reference picture is the deblocked reconstruction
             const int sub_len = intra_split(t, g.mb_w, cfg.deblock, cfg.intra4x4) ? kIntraSubMbs : 0;
             db_slice_info(mbs.data(), g.mb_w, t.first_row, t.num_rows, t.qp, dbinfo.data(), sub_len);
             deblock_slice_cpu(ref[0].data(), ref[1].data(), ref[2].data(), g.stride_y, g.stride_c, dbinfo.data(),

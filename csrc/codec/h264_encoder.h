@@ -38,7 +38,8 @@ struct EncoderConfig {
     int me_iters = 24;           // diamond refinement iterations
     int scenecut = 1;
     float fps = 60.f;
-    int deblock = 0;             // in-loop deblocking filter (idc 2: inside each slice); off = x264 ultrafast
+    int deblock = 2;             // in-loop deblocking (idc 2: inside each slice): 0 off (x264 ultrafast), 1 on,
+                                 // 2 automatic: the slices coded at QP >= kAutoDeblockQp (slice_deblock)
     int me_full = 1;             // +-16 exhaustive MFMA search candidate (dirty MBs of P slices)
     int shared_copy = 0;         // HIP: uploads on the device's shared copy stream (in submit order)
     int num_refs = 1;            // reference frames per stream (sliding-window DPB): 1, or 2 for the
@@ -121,6 +122,15 @@ static_assert(sizeof(SliceTask) == 48, "SliceTask layout");
 // sub-slice (h264_deblock.h, k_deblock_prep / k_deblock_edges); Intra4x4 blocks see no
 // top or top-right neighbour outside their sub-slice (k_code_intra_sub's I_NxN path).
 constexpr int kIntraSubMbs = 40;
+// Automatic deblocking (EncoderConfig::deblock = 2): a slice is filtered when it is coded
+// at QP >= 34 - CBR under a tight budget, where the 4x4 / 16x16 block edges become
+// visible - and left unfiltered at the CRF-25 default, as x264's ultrafast preset
+// (legacy/gstwebrtc_app.py:637). Per slice, in its disable_deblocking_filter_idc (2 or 1):
+// the stripes of one frame run at different (dithered) QPs.
+constexpr int kAutoDeblockQp = 34;
+SK_HD bool slice_deblock(int deblock, const SliceTask& t) {
+    return deblock == 1 || (deblock == 2 && t.qp >= kAutoDeblockQp);
+}
 SK_HD bool intra_split(const SliceTask& t, int mb_w, int deblock, int intra4x4) {
     (void)deblock;
     (void)intra4x4;

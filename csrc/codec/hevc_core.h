@@ -1145,6 +1145,7 @@ SK_HD void code_sb(W& w, const Sb4& s, int log2n, int cidx, int scan, int i, int
     uint32_t sig = 0;
     const int start = (i == last_i) ? last_n - 1 : 15;
     if (i == last_i) sig |= 1u << last_n;
+#pragma unroll 1
     for (int k = start; k >= 0; k--) {
         const int r = scan4_raster(scan, k);
         const int xc = xs * 4 + (r & 3), yc = ys * 4 + (r >> 2);
@@ -1183,6 +1184,7 @@ SK_HD void code_sb(W& w, const Sb4& s, int log2n, int cidx, int scan, int i, int
     if (!first_g1 && c1_in == 0) ctx_set++;
     int g1ctx = 1, ng1 = 0, last_g1_pos = -1;
     uint32_t g1 = 0;
+#pragma unroll 1
     for (int k = 15; k >= 0; k--) {
         if (!((sig >> k) & 1)) continue;
         if (ng1 < 8) {
@@ -1205,6 +1207,7 @@ SK_HD void code_sb(W& w, const Sb4& s, int log2n, int cidx, int scan, int i, int
     {
         uint32_t bits = 0;
         int nb = 0;
+#pragma unroll 1
         for (int k = 15; k >= 0; k--)
             if ((sig >> k) & 1) {
                 bits = (bits << 1) | (lev.at(k) < 0 ? 1u : 0u);
@@ -1215,6 +1218,7 @@ SK_HD void code_sb(W& w, const Sb4& s, int log2n, int cidx, int scan, int i, int
     }
     // coeff_abs_level_remaining
     int rice = 0, nsig = 0;
+#pragma unroll 1
     for (int k = 15; k >= 0; k--) {
         if (!((sig >> k) & 1)) continue;
         const int a = sk_abs(lev.at(k));
@@ -1257,14 +1261,20 @@ SK_HD void code_sb(W& w, const Sb4& s, int log2n, int cidx, int scan, int i, int
 // state the sub-blocks coded before it leave (that of the nearest one with a level).
 // A writer with W::kWave set (k_hevc_bins) codes the sub-blocks on the lanes of a wave.
 template <class W, class C>
+SK_HD void code_residual_serial(W& w, C c, int log2n, int cidx, int scan, int ts, int lo, int hi);
+template <class W, class C>
 SK_HD void code_residual(W& w, C c, int log2n, int cidx, int scan = SCAN_DIAG, int ts = 0, int lo = 0, int hi = 63) {
-    if constexpr (W::kWave) {
-        w.residual(c, log2n, cidx, scan, ts, lo, hi);
-    } else {
+    if constexpr (W::kWave) w.residual(c, log2n, cidx, scan, ts, lo, hi);
+    else code_residual_serial(w, c, log2n, cidx, scan, ts, lo, hi);
+}
+template <class W, class C>
+SK_HD void code_residual_serial(W& w, C c, int log2n, int cidx, int scan, int ts, int lo, int hi) {
+    {
         const int n = 1 << log2n;
         const int sbw = n >> 2;                     // sub-blocks per row
         const int nsb = sbw * sbw;
         int last_i = -1, last_n = -1;
+#pragma unroll 1
         for (int i = nsb - 1; i >= 0; i--) {
             const int sr = sb_scan_raster(log2n, scan, i);
             const Sb4 s = load_sb(c, n, sr % sbw, sr / sbw);
@@ -1281,12 +1291,14 @@ SK_HD void code_residual(W& w, C c, int log2n, int cidx, int scan = SCAN_DIAG, i
         // neighbours a sub-block's contexts read come later in every scan, and nothing after
         // last_i is coded: the flags of scan positions lo .. last_i are all that is read.
         uint64_t csbf = 0;
+#pragma unroll 1
         for (int i = lo; i <= last_i; i++) {
             const int sr = sb_scan_raster(log2n, scan, i);
             if (load_sb(c, n, sr % sbw, sr / sbw).nz()) csbf |= 1ull << sr;
         }
         int c1 = 1;   // greater1 state carried between sub-blocks
         bool first_g1 = true;
+#pragma unroll 1
         for (int i = i0 + 1; i <= last_i && first_g1; i++) {   // a later piece: the state so far
             const int sr = sb_scan_raster(log2n, scan, i);
             const Sb4 s = load_sb(c, n, sr % sbw, sr / sbw);
@@ -1295,6 +1307,7 @@ SK_HD void code_residual(W& w, C c, int log2n, int cidx, int scan = SCAN_DIAG, i
                 first_g1 = false;
             }
         }
+#pragma unroll 1
         for (int i = i0; i >= lo; i--) {
             const int sr = sb_scan_raster(log2n, scan, i), xs = sr % sbw, ys = sr / sbw;
             const int right = (xs + 1 < sbw) ? (int)((csbf >> (sr + 1)) & 1) : 0;

@@ -86,11 +86,12 @@ SK_HD int rc_lam_boost(int qpf) { return qpf > (51 << 8) ? ((qpf + 128) >> 8) - 
 // vbv_ms: the CBR buffer. 0 = 1.5 frame intervals, the reference's low-latency
 // setting for its H.264 / H.265 encoders (legacy/gstwebrtc_app.py:100-104); AV1
 // passes 120 ms, svtav1enc's buf-optimal-sz (gstwebrtc_app.py:738).
-// Finest controller QP per codec (EncoderConfig::codec). H.264 stops at 10. HEVC goes
-// down to 0 like x265's qpmin: its transform skip and residual quadtree code a desktop
-// at QP 10 in ~0.65 of a 16 Mbit/s 1080p60 budget, so CBR needs finer QPs to reach the
-// rate (the per-frame guard bounds what a burst coded that fine costs).
-SK_HD int rc_qp_min_for(int codec) { return codec == 1 ? 0 : 10; }
+// Finest controller QP per codec (EncoderConfig::codec). H.264 stops at 10. HEVC and AV1
+// go down to 0 like x265's qpmin / svtav1enc's min-qp: transform skip / IDTX and the
+// residual trees code a desktop at QP 10 in ~0.65 (HEVC) / ~0.7 (AV1) of a 1080p60 budget
+// at 16 Mbit/s, so CBR needs finer QPs to reach the rate (the per-frame guard bounds what
+// a burst coded that fine costs). AV1 maps the QP to the qindex of the same step.
+SK_HD int rc_qp_min_for(int codec) { return codec == 0 ? 10 : 0; }
 
 // codec: EncoderConfig::codec (0 H.264, 1 HEVC, 2 AV1).
 SK_HD void rc_init(RcState& rc, int mode, int base_qp, int bitrate_kbps, float fps, int pixels, int vbv_ms = 0,

@@ -2629,7 +2629,7 @@ __global__ __launch_bounds__(256) void k_slice_scan(FrameArgs a) {
         h.frame_num = idr ? 0 : task.frame_num;
         h.idr_pic_id = task.idr_pic_id;
         h.slice_qp = task.qp;
-        h.deblock = a.deblock;
+        h.deblock = slice_deblock(a.deblock, task);
         h.num_refs = intra ? 1 : task.num_refs;
         write_slice_header(w, h);
         if (fin == ACT_SKIPALL) put_ue(w, (uint32_t)nmb);
@@ -2956,7 +2956,7 @@ __global__ __launch_bounds__(256) void k_commit(FrameArgs a) {
     // sliding-window DPB: the current reference becomes reference 1 (a skip-all picture
     // is a reference too); the same thread then overwrites ref with rec below
     if (a.num_refs > 1) copy(a.ref, a.ref1);
-    if (fin == ACT_SKIPALL || a.deblock) return;  // reference unchanged / written by k_deblock
+    if (fin == ACT_SKIPALL || slice_deblock(a.deblock, a.tasks[s])) return;  // reference unchanged / written by k_deblock
     copy(a.rec, a.ref);
 }
 
@@ -2980,6 +2980,7 @@ __global__ __launch_bounds__(256) void k_deblock_prep(FrameArgs a) {
     if (idx >= nmb) return;
     const SliceTask t = a.tasks[(idx / a.mb_w) / a.rows_per_slice];
     if (t.final_action != ACT_P && t.final_action != ACT_I) return;
+    if (!slice_deblock(a.deblock, t)) return;   // automatic deblocking: an unfiltered slice
     const int l = lane_id();
     int first = t.first_row * a.mb_w;
     if (split_i(a, t)) first += ((idx - first) / kIntraSubMbs) * kIntraSubMbs;   // K5: the chain restarts per sub-slice
@@ -3091,6 +3092,7 @@ __global__ __launch_bounds__(256) void k_deblock_edges(FrameArgs a) {
     const int mbx = idx % a.mb_w, mby = idx / a.mb_w;
     const SliceTask t = a.tasks[mby / a.rows_per_slice];
     if (t.final_action != ACT_P && t.final_action != ACT_I) return;
+    if (!slice_deblock(a.deblock, t)) return;
     const DbInfo cur = a.db[idx];
     int sub0 = t.first_row * a.mb_w;   // K5 sub-slices: no edge leaves the MB's sub-slice (idc 2)
     if (split_i(a, t)) sub0 += ((idx - sub0) / kIntraSubMbs) * kIntraSubMbs;
@@ -3140,6 +3142,7 @@ __global__ __launch_bounds__(64 * MAXR) void k_deblock(FrameArgs a) {
     __shared__ uint4 erec[MAXR][kSlots][3];   // edge record (k_deblock_edges) of the slot's MB
     const SliceTask t = a.tasks[blockIdx.x];
     if (t.final_action != ACT_P && t.final_action != ACT_I) return;
+    if (!slice_deblock(a.deblock, t)) return;   // k_commit copied rec -> ref
     const int r = threadIdx.x >> 6, l = lane_id();
     const int R = t.num_rows, W = a.mb_w;
     const int mby = t.first_row + r;

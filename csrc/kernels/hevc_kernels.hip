@@ -1274,6 +1274,16 @@ struct WaveBinBuf {
     }
     template <class C>
     __device__ void residual(C c, int log2n, int cidx, int scan, int ts, int lo, int hi) {
+        if (log2n == 2) {   // one sub-block: lane 0 alone, serially (no ballots, scans or second pass)
+            int cnt = 0;
+            if (lane() == 0) {
+                BinBuf b{p, n};
+                code_residual_serial(b, c, log2n, cidx, scan, ts, lo, hi);
+                cnt = b.n - n;
+            }
+            n += __shfl(cnt, 0);
+            return;
+        }
         const int j = lane(), n4 = 1 << log2n, sbw = n4 >> 2, nsb = sbw * sbw;
         int sr = 0, xs = 0, ys = 0;
         Sb4 s{0, 0, 0, 0};

@@ -324,7 +324,7 @@ h264::EncoderConfig to_config(const sk_h264_config* c) {
     e.me_iters = c->me_iters > 0 ? c->me_iters : 24;
     e.scenecut = c->scenecut;
     e.fps = c->fps > 0 ? c->fps : 60.f;
-    e.deblock = c->deblock > 0 ? 1 : 0;   // off by default, like x264 ultrafast
+    e.deblock = c->deblock < 0 ? 0 : (c->deblock == 1 ? 1 : 2);   // default automatic (h264_encoder.h slice_deblock)
     e.me_full = c->me_full >= 0 ? 1 : 0;
     e.shared_copy = c->shared_copy > 0 ? 1 : 0;
     e.src_width = c->src_width > 0 ? c->src_width : 0;

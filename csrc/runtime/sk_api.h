@@ -15,7 +15,7 @@ typedef struct sk_h264_config {
     float fps;
     int32_t device;   // HIP device ordinal for the GPU backend
     int32_t backend;  // 0 = CPU reference, 1 = HIP (gfx950)
-    int32_t deblock;  // in-loop deblocking: 0 = default (off), > 0 on, < 0 off
+    int32_t deblock;  // in-loop deblocking: 0 = default (automatic: slices at QP >= 34), 1 on, 2 automatic, < 0 off
     int32_t me_full;  // MFMA +-16 exhaustive search candidate: 0 = default (on), > 0 on, < 0 off
     int32_t shared_copy;  // > 0: H2D on the device's shared copy stream (bands of one frame)
     int32_t src_width, src_height;  // capture size if it differs (K2 resample in K1); 0 = width/height

@@ -314,6 +314,15 @@ RC_FIELDS = ("mode", "base_qp", "qp_min", "qp_max", "budget", "vbv_size", "fulln
              "cur_redo", "redo_qpf", "redo_bits", "codec", "lam_boost")
 
 
+def deblock_mode(deblock) -> int:
+    """SkH264Config.deblock of a Python value: True -> 1 (on), False -> -1 (off), "auto" -> 2."""
+    if isinstance(deblock, str):
+        if deblock != "auto":
+            raise ValueError("deblock must be True, False or 'auto'")
+        return 2
+    return 1 if deblock else -1
+
+
 class H264Encoder:
     """Stripe H.264 encoder session (CPU reference backend or HIP backend)."""
 
@@ -322,13 +331,14 @@ class H264Encoder:
                  paint_over_trigger: int = 15, paint_over_burst: int = 5, streaming_mode: bool = False,
                  damage_threshold: int = 10, damage_duration: int = 20, me_range: int = 64,
                  me_iters: int = 24, scenecut: bool = True, fps: float = 60.0, device: int = 0,
-                 backend: str = "cpu", deblock: bool = False, me_full: bool = True, shared_copy: bool = False,
+                 backend: str = "cpu", deblock="auto", me_full: bool = True, shared_copy: bool = False,
                  src_width: int = 0, src_height: int = 0, num_refs: int = 1, codec: str = "h264",
                  aq_strength: float = 0.0, subpel: bool = True, intra4x4: bool = False,
                  tile_cols_log2: int = -1, tile_rows_log2: int = -1, rate_control: str = "cqp",
                  bitrate_kbps: int = 0):
         """aq_strength: MB-level adaptive QP (h264_mb.h aq_offset), 1.0 = x264 aq-mode 1
-        strength; 0 = constant QP per slice (x264 ultrafast behaviour)."""
+        strength; 0 = constant QP per slice (x264 ultrafast behaviour). deblock: True / False,
+        or "auto" (the slices coded at QP >= 34, h264_encoder.h slice_deblock)."""
         L = lib()
         if backend not in ("cpu", "hip"):
             raise ValueError("backend must be 'cpu' or 'hip'")
@@ -337,7 +347,7 @@ class H264Encoder:
         self.cfg = SkH264Config(width, height, stripe_height, int(fullframe), int(full_range), qp, paint_qp,
                                 int(use_paint_over), paint_over_trigger, paint_over_burst, int(streaming_mode),
                                 damage_threshold, damage_duration, me_range, me_iters, int(scenecut), fps,
-                                device, 1 if backend == "hip" else 0, 1 if deblock else -1,
+                                device, 1 if backend == "hip" else 0, deblock_mode(deblock),
                                 1 if me_full else -1, 1 if shared_copy else 0, int(src_width), int(src_height),
                                 int(num_refs), {"h264": 0, "hevc": 1, "av1": 2}.get(codec, 0),
                                 int(round(aq_strength * 16)), 0 if subpel else -1, 1 if intra4x4 else 0,

@@ -134,3 +134,44 @@ def test_cpu_backend_queues_two_submitted_frames():
     assert got == ref
     with pytest.raises(RuntimeError):
         b.finish()
+
+
+def _deblock_idc(nal: bytes) -> int:
+    """disable_deblocking_filter_idc of a P / I slice NAL of this encoder's streams
+    (Baseline, POC type 2, frame_num 16 bits: codec/h264_syntax.h write_slice_header)."""
+    from selkies_gstreamer_amd.models.h264.decoder import BitReader, unescape
+    r = BitReader(unescape(nal[1:]))
+    r.ue()                                    # first_mb_in_slice
+    st = r.ue() % 5                           # slice_type
+    r.ue()                                    # pic_parameter_set_id
+    r.u(16)                                   # frame_num
+    idr = (nal[0] & 31) == 5
+    if idr:
+        r.ue()                                # idr_pic_id
+    if st == 0:
+        if r.u(1):                            # num_ref_idx_active_override_flag
+            r.ue()
+        r.u(1)                                # ref_pic_list_modification_flag_l0 (0)
+    r.u(2 if idr else 1)                      # dec_ref_pic_marking
+    r.se()                                    # slice_qp_delta
+    return r.ue()
+
+
+@pytest.mark.parametrize("qp,idc", [(26, 1), (38, 2)])
+def test_auto_deblock_follows_slice_qp(qp, idc):
+    """deblock='auto' (the default): slices coded at QP >= 34 are deblocked (idc 2), those
+    below are not (idc 1, the CRF-25 default stays x264-ultrafast-like); the independent
+    decoder reproduces the encoder's reference either way."""
+    W, H = 160, 96
+    enc = H264Encoder(W, H, stripe_height=32, qp=qp, paint_qp=qp, use_paint_over=False, backend="cpu")
+    sd = StripeDecoder(W, H)
+    seen = set()
+    for t, f in enumerate(synthetic_frames(W, H, 4, kind="desktop")):
+        for p in enc.encode(f, t):
+            sd.feed(p.data)
+            for nal in p.data[10:].split(b"\x00\x00\x00\x01")[1:]:
+                if nal[0] & 31 in (1, 5):
+                    seen.add(_deblock_idc(nal))
+        ref = enc.debug_buffer("ref_y").reshape(-1, (W + 15) // 16 * 16)[:H, :W]
+        assert np.array_equal(sd.Y, ref), f"frame {t}"
+    assert seen == {idc}

@@ -56,6 +56,34 @@ def test_gpu_matches_cpu_reference(fullframe, kind, deblock, num_refs):
         assert psnr(sd.Y, bgrx_to_y709(f)) > 30
 
 
+@pytest.mark.parametrize("fullframe", [False, True])
+def test_gpu_auto_deblock_cbr_matches_cpu(fullframe):
+    """deblock='auto' under a tight CBR: the controller's dithered slice QPs straddle 34,
+    so some stripes of a frame are deblocked and others not (per-slice idc); the GPU
+    (k_commit / k_deblock_* gated per slice) equals the CPU reference, and the decoder
+    reproduces the reference."""
+    W, H = 320, 192
+    kw = dict(stripe_height=32, fullframe=fullframe, deblock="auto", rate_control="cbr", bitrate_kbps=2500,
+              use_paint_over=False)
+    cpu, gpu = _pair(W, H, **kw)
+    sd = StripeDecoder(W, H)
+    src = SyntheticDesktop(W, H, kind="motion")
+    qps = set()
+    for t in range(40):
+        f = src.frame(t)
+        pc = cpu.encode(f, t)
+        pg = gpu.encode(f, t)
+        _compare_state(cpu, gpu, W, t)
+        assert [p.data for p in pg] == [p.data for p in pc], f"frame {t}: bitstreams differ"
+        for p in pg:
+            sd.feed(p.data)
+        ref = gpu.debug_buffer("ref_y").reshape(-1, (W + 15) // 16 * 16)[:H, :W]
+        assert np.array_equal(sd.Y, ref), f"frame {t}: decoder != reference"
+        tk = cpu.debug_buffer("tasks", TASK_DTYPE)
+        qps |= {int(q) for a, q in zip(tk["final_action"], tk["qp"]) if a in (1, 2)}
+    assert min(qps) < 34 <= max(qps), qps   # both kinds of slices occurred
+
+
 @pytest.mark.parametrize("deblock", [False, True])
 def test_gpu_1080p_desktop_matches_cpu(deblock):
     W, H = 1920, 1080

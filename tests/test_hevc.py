@@ -132,7 +132,7 @@ def test_hevc_directional_intra_modes():
     assert np.array_equal(Y, _rec_y(enc, W, H))
     modes = np.frombuffer(enc.debug_buffer("cus", np.uint8), np.uint8).reshape(-1, CUINFO)[:, 24:40]
     assert np.count_nonzero(~np.isin(modes, [0, 1, 10, 26])) > modes.size // 2
-    assert len(pk.data) < 7000, len(pk.data)
+    assert len(pk.data) < 7500, len(pk.data)   # (levels round to 0.47: a little more detail, PSNR > 45)
     assert psnr(Y, _luma(f)) > 45
 
 
