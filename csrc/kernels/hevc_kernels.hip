@@ -1213,7 +1213,7 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
 
 // I slices cut into row segments (SliceMap, seg_k > 1): one wave per segment, its CTBs
 // left to right (units in z order); no top neighbours, so the segments of all rows run at
-// once (a 4K key frame: 816 chains of 40 units instead of 34 workgroups of 124 steps).
+// once (a 4K key frame: 1632 chains of 20 units instead of 34 workgroups of 124 steps).
 __global__ __launch_bounds__(256) void k_hevc_intra_seg(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
