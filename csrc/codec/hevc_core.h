@@ -38,7 +38,7 @@ namespace hevc {
 // rows (one WPP substream per row). A row of an intra slice is instead cut into K slices of
 // about mb_w / K CTBs each, K = ceil(mb_w / kIntraSegCtbs): the closed-loop intra coding
 // of a CTB waits for its left neighbour, so a key frame's longest serial chain is one
-// segment (5 CTBs = 20 units at 4K, hevc_encoder.h intra_seg_k) instead of one row (120
+// segment (10 CTBs = 40 units at 4K, hevc_encoder.h intra_seg_k) instead of one row (120
 // CTBs) - the same cut as the H.264
 // IDR sub-slices (h264_encoder.h intra_split). Such a slice starts mid-row and ends in the
 // same row, as 7.4.7.1 requires under entropy_coding_sync; it has no top neighbours

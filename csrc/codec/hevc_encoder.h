@@ -70,14 +70,15 @@ inline h264::EncoderConfig front_config(const h264::EncoderConfig& c) {
 }
 
 // Slices per CTB row of intra slices (SliceMap::K): ceil(ctb_w / kIntraSegCtbs) (CTB32s);
-// above 1440p (4096 CTBs) segments of kIntraSegCtbs / 4: a key frame takes as long as
-// one segment's closed-loop chain (20 units at 4K: 1632 chains, two waves per SIMD hide
-// each other's latency); +2 % key-frame bytes at 4K against 10-CTB segments, -0.07 dB. SK_HEVC_SEG_CTBS=<n> sets the segment width (tests exercise
+// above 1440p (4096 CTBs) segments of kIntraSegCtbs / 2: a key frame takes about as long
+// as one segment's closed-loop chain (40 units at 4K: 816 chains, one wave per SIMD;
+// 5-CTB segments measured 2.2 against 2.4 ms - the chains then share SIMDs - for +1 %
+// key-frame bytes). SK_HEVC_SEG_CTBS=<n> sets the segment width (tests exercise
 // the split at small sizes), SK_HEVC_SEG_CTBS=0 turns the split off (RD A/B runs).
 inline int intra_seg_k(int ctb_w, int ctb_h) {
     const char* e = getenv("SK_HEVC_SEG_CTBS");
     if (e && e[0] == '0') return 1;
-    const int seg = e && atoi(e) > 0 ? atoi(e) : (ctb_w * ctb_h > 4096 ? kIntraSegCtbs / 4 : kIntraSegCtbs);
+    const int seg = e && atoi(e) > 0 ? atoi(e) : (ctb_w * ctb_h > 4096 ? kIntraSegCtbs / 2 : kIntraSegCtbs);
     return intra_seg_count(ctb_w, seg);
 }
 

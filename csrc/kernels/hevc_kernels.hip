@@ -1213,7 +1213,7 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
 
 // I slices cut into row segments (SliceMap, seg_k > 1): one wave per segment, its CTBs
 // left to right (units in z order); no top neighbours, so the segments of all rows run at
-// once (a 4K key frame: 1632 chains of 20 units instead of 34 workgroups of 124 steps).
+// once (a 4K key frame: 816 chains of 40 units instead of 34 workgroups of 124 steps).
 __global__ __launch_bounds__(256) void k_hevc_intra_seg(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
@@ -1500,24 +1500,30 @@ __global__ __launch_bounds__(256) void k_pc_sort(HevcArgs A) {
     }
 }
 
-// One wave per (CTB row or row segment, context): the context's state chain along the
+// One wave per (CTB row, context, slice group): the context's state chain along the
 // row's chunks, from its WPP start state; each context bin is rewritten in place as a
 // modelled entry (LPS state, is-LPS). The chunks holding the context are listed with the
 // prefix of their counts; the chain itself runs as up to 64 speculative segments, one per
 // lane (below).
+constexpr int kPcModelZ = 4;   // k_pc_model workgroups per (row, context group)
 __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ uint2 lst_s[4][kPcMaxRowChunks + 1];   // (chunk | lo << 16, chain position of its first entry)
     __shared__ uint8_t nl_s[4][64];                // CABAC_NEXT_LPS
     const FrameArgs& f = A.f;
     const int w = threadIdx.x >> 6, l = lane();
-    const int slot = blockIdx.x, c = blockIdx.y * 4 + w;
+    const int cy = blockIdx.x, c = blockIdx.y * 4 + w;
     if (c >= CTX_COUNT) return;
     const SliceMap m = smap(A);
-    const int cy = slot / A.seg_k, k = slot - cy * A.seg_k;
-    if (k >= m.nseg(cy)) return;   // slot of a whole row: only k = 0
     const UnitGrid ug = ugrid(A);
     const int RC = 2 * f.mb_w;
+    uint8_t* nl = nl_s[w];
+    nl[l] = CABAC_NEXT_LPS[l];
+    // the row's slices k = z, z + kPcModelZ, ... (a split key-frame row: its segments'
+    // short chains, a few per wave; a grid of every possible slot launched tens of
+    // thousands of LDS-heavy workgroups that exit at once on the P frames)
+    for (int k = blockIdx.z; k < m.nseg(cy); k += kPcModelZ) {
+    const int slot = cy * A.seg_k + k;
     const int xa = ug.ctb_chunk0(cy, m.x0(cy, k));
     const int xb = m.x1(cy, k) < A.cw ? ug.ctb_chunk0(cy, m.x1(cy, k)) : ug.row_chunks(cy);
     uint2* L = lst_s[w];
@@ -1546,11 +1552,8 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     tot = __builtin_amdgcn_readfirstlane(tot);
     if (l == 0) L[n] = make_uint2(0u, (uint32_t)tot);
     wsync();
-    if (tot == 0) return;
+    if (tot == 0) continue;
     const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane(A.sync[(size_t)slot * CTX_COUNT + c]);
-    uint8_t* nl = nl_s[w];
-    nl[l] = CABAC_NEXT_LPS[l];
-    wsync();
     // The chain is cut into up to 64 segments, lane = segment (>= 32 entries each).
     // Pass 1 runs every segment from a guessed start state; CABAC states forget their
     // start quickly (MPS runs saturate, LPS steps contract), so segment j-1's end state
@@ -1610,6 +1613,8 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
         const int first = (int)__builtin_ctzll(bad);
         need = act && l >= first;
         if (need) T = tn;
+    }
+    wsync();   // L is rebuilt for the next slice of the row
     }
 }
 
@@ -2321,7 +2326,7 @@ static void launch_code(const HevcArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_hevc_bins, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_sort, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hevc_sync, dim3(a.f.num_slices), dim3(192), 0, s, a);
-    hipLaunchKernelGGL(k_pc_model, dim3(slots, (CTX_COUNT + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_pc_model, dim3(a.ch, (CTX_COUNT + 3) / 4, sk_min(a.seg_k, kPcModelZ)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_rmap, dim3(nq), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_pc_compose, dim3(slots), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_pc_code, dim3(nq), dim3(256), 0, s, a);

@@ -104,7 +104,7 @@ def test_hevc_hip_split_intra_slices(kind, seg, monkeypatch):
 
 
 def test_hevc_hip_4k_keyframe_parity():
-    """3840x2160 key frames (24 segments per CTB row, 1632 slices) and the P frames after
+    """3840x2160 key frames (12 segments per CTB row, 816 slices) and the P frames after
     them: GPU == CPU."""
     W, H = 3840, 2160
     gpu, cpu = _pair(W, H)
