@@ -1690,7 +1690,7 @@ __global__ __launch_bounds__(256) void k_pc_rmap(HevcArgs A) {
 }
 
 // One wave per CTB row: start range and stream bit offset of every chunk, one map
-// lookup each (a readlane); the maps of the next 8 CTBs are in flight.
+// lookup each (a readlane); the maps of the next 16 chunks are in flight.
 __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
@@ -1703,7 +1703,7 @@ __global__ __launch_bounds__(64) void k_pc_compose(HevcArgs A) {
     const int j0 = ug.ctb_chunk0(cy, m.x0(cy, k));
     const int nw = (m.x1(cy, k) < A.cw ? ug.ctb_chunk0(cy, m.x1(cy, k)) : ug.row_chunks(cy)) - j0;
     auto unit = [&](int d) { return ug.chunk_unit(cy, j0 + d); };
-    constexpr int D = 8;
+    constexpr int D = 16;
     uint4 buf[D];
 #pragma unroll
     for (int d = 0; d < D; d++)

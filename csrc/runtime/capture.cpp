@@ -119,6 +119,7 @@ class CaptureSession {
                     e.fullframe = 1;
                     e.aq_strength = 0;
                     e.intra4x4 = 0;
+                    e.deblock = 0;   // their own in-loop filters, not the H.264 front end's
                 }
                 ecfg_ = e;
                 enc_.reset(backend ? create_hip_backend(e, s.device) : create_cpu_backend(e));

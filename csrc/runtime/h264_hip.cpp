@@ -545,7 +545,7 @@ class HipBackend : public EncoderBackend {
         a.stride_y = g_.stride_y; a.stride_c = g_.stride_c;
         a.num_slices = ns; a.rows_per_slice = g_.rows_per_slice; a.fullframe = cfg_.fullframe;
         a.full_range = cfg_.full_range; a.me_range = cfg_.me_range; a.me_iters = cfg_.me_iters;
-        a.deblock = cfg_.deblock;
+        a.deblock = cfg_.codec == 0 ? cfg_.deblock : 0;   // HEVC / AV1 filter in their own back ends
         a.me_full = cfg_.me_full;
         a.aq_strength = cfg_.codec == 1 ? 0 : cfg_.aq_strength;
         a.subpel = cfg_.codec == 2 ? 0 : cfg_.subpel;   // AV1 keeps integer vectors (av1_encoder.h front_config)

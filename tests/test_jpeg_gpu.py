@@ -97,3 +97,43 @@ def test_gpu_server_session():
             await ws.close()
         await srv.stop()
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("mode", [2, 3])   # pixelflux OUTPUT_MODE_HEVC / OUTPUT_MODE_AV1
+def test_gpu_capture_cbr_hevc_av1_match_cpu(mode):
+    """HEVC / AV1 capture sessions (step mode over a pinned pool) under a tight CBR, where
+    the controller runs at QP >= 34: the HIP session's packets equal the CPU session's. The
+    H.264 front end's automatic deblocking must stay off for them (their own in-loop filters
+    make the reference; filtering it again drifted the HIP encoder from the decoder)."""
+    import ctypes
+    import numpy as np
+    import pixelflux
+    from selkies_gstreamer_amd.ops.native import PinnedBuffer
+    from selkies_gstreamer_amd.utils.synthetic import SyntheticDesktop
+    W, H, N = 320, 192, 24
+    src = SyntheticDesktop(W, H, kind="motion", seed=3)
+    pool = PinnedBuffer((8, H, W, 4))
+    for i in range(8):
+        src.frame(i, out=pool.array[i])
+    outs = []
+    for use_cpu in (1, 0):
+        got, lock = [], threading.Lock()
+
+        def cb(res_ptr, n, user):
+            with lock:
+                got.append(b"".join(bytes(res_ptr[i].data[:res_ptr[i].size]) for i in range(n)))
+        s = pixelflux.default_settings(W, H, output_mode=mode, use_paint_over_quality=0, use_cpu=use_cpu,
+                                       source=pixelflux.SOURCE_POOL, step_mode=1, pool_frames=8, pool_stride=W * 4,
+                                       target_fps=60.0, h264_rc_mode=2, h264_bitrate_kbps=300)
+        s.pool = pool.array.ctypes.data
+        cap = pixelflux.ScreenCapture()
+        thunk = pixelflux.FrameCallback(cb)
+        cap.start_frame_capture(s, thunk)
+        cap.run(N)
+        assert cap.wait(120_000) == 0
+        cap.close()
+        outs.append(got)
+    cpu, gpu = outs
+    assert len(cpu) == len(gpu) == N
+    for t, (a, b) in enumerate(zip(cpu, gpu)):
+        assert a == b, f"frame {t}: HIP capture packets differ from the CPU session's"
