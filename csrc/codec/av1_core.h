@@ -71,6 +71,22 @@ SK_HD int tile_log2(int blk, int target) {
     return k;
 }
 
+// Automatic tile split (log2 columns / rows) of a frame of sbc x sbr superblocks: up to
+// 8 x 8 tiles; from 48 superblock columns (3072 px: 4K, 8K) 16 columns x 4 rows, the
+// level-5.1 limits (MaxTileCols 16, MaxTiles 64). A key frame's tile is one workgroup of
+// 16 waves stepping along anti-diagonals of 16x16 units (k_av1_intra_rec): 4K tiles of
+// 16 x 36 units never hold more units on a diagonal than there are waves, where 8 x 7 tiles
+// of 32 x 20 units needed a second round on 19 of their 51 steps.
+SK_HD void auto_tiles(int sbc, int sbr, int* cols_log2, int* rows_log2) {
+    if (sbc >= 48) {
+        *cols_log2 = 4;
+        *rows_log2 = tile_log2(1, sk_min(4, sbr));
+        return;
+    }
+    *cols_log2 = tile_log2(1, sk_min(8, sbc));
+    *rows_log2 = tile_log2(1, sk_min(8, sbr));
+}
+
 // want_cols_log2 / want_rows_log2: requested split, clamped to the legal range.
 SK_HD void geo_init(Av1Geo& g, int W, int H, int want_cols_log2, int want_rows_log2) {
     g.W = W;

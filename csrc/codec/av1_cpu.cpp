@@ -195,8 +195,10 @@ CpuAv1Encoder::CpuAv1Encoder(const h264::EncoderConfig& cfg, int tcl, int trl) :
     // tiles: as many as the level allows (the entropy coder's parallel axis), 16x16 SB max per tile side
     const int sbc = (W + 63) / 64, sbr = (H + 63) / 64;
     int want_c = tcl, want_r = trl;
-    if (want_c < 0) want_c = tile_log2(1, std::min(8, sbc));
-    if (want_r < 0) want_r = tile_log2(1, std::min(8, sbr));
+    int auto_c, auto_r;
+    auto_tiles(sbc, sbr, &auto_c, &auto_r);
+    if (want_c < 0) want_c = auto_c;
+    if (want_r < 0) want_r = auto_r;
     geo_init(geo, W, H, want_c, want_r);
     blk.assign((size_t)geo.c8 * geo.r8, BlkInfo{});
     lev.assign((size_t)fe.g.mb_w * fe.g.mb_h * kLevPerUnit, 0);

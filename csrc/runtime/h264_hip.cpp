@@ -822,8 +822,10 @@ class HipBackend : public EncoderBackend {
         av1::gpu::Av1Args& a = aargs_;
         memset(&a, 0, sizeof(a));
         const int sbc = (g_.W + 63) / 64, sbr = (g_.H + 63) / 64;
-        const int tc = cfg_.tile_cols_log2 >= 0 ? cfg_.tile_cols_log2 : av1::tile_log2(1, std::min(8, sbc));
-        const int tr = cfg_.tile_rows_log2 >= 0 ? cfg_.tile_rows_log2 : av1::tile_log2(1, std::min(8, sbr));
+        int ac, ar;
+        av1::auto_tiles(sbc, sbr, &ac, &ar);
+        const int tc = cfg_.tile_cols_log2 >= 0 ? cfg_.tile_cols_log2 : ac;
+        const int tr = cfg_.tile_rows_log2 >= 0 ? cfg_.tile_rows_log2 : ar;
         av1::geo_init(av1_geo_, g_.W, g_.H, tc, tr);
         a.geo = av1_geo_;
         a.blk = dmalloc<av1::BlkInfo>((size_t)av1_geo_.c8 * av1_geo_.r8);

@@ -57,6 +57,13 @@ def test_key_and_inter_frames_decode_exactly(W, H):
     assert min(p for _, _, p in res) > 30
 
 
+def test_auto_tiles_from_3072_px_decode_exactly():
+    """Frames 48+ superblocks wide take 16 tile columns (av1_core.h auto_tiles: the 4K key
+    frame's per-tile wavefront fits 16 waves); dav1d decodes them exactly."""
+    res = run(3072, 192, "motion", 2, qp=30)
+    assert res[0][0] and min(p for _, _, p in res) > 30
+
+
 def test_noise_cuts_stay_inter_frames():
     """No scene-cut key frames (svtav1enc in the reference runs intra-period -1 with
     no scene-change detection, legacy/gstwebrtc_app.py:733-739): a frame of new noise

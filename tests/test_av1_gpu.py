@@ -55,6 +55,12 @@ def test_gpu_1080p():
     _check(1920, 1080, "motion", 3, qp=25)
 
 
+def test_gpu_4k_tile_layout():
+    """3840x2160: the automatic 16 x 4 tile split (av1_core.h auto_tiles), key and inter
+    frames, GPU == CPU."""
+    _check(3840, 2160, "desktop", 2, qp=30)
+
+
 def test_gpu_palette_key_frames():
     """Palette blocks (desktop content: text and flat UI on key frames): the GPU's
     decisions (k_av1_intra_rec), colour caches and lane-parallel index-map tokens equal
