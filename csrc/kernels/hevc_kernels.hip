@@ -1809,6 +1809,57 @@ __global__ __launch_bounds__(256) void k_pc_code(HevcArgs A) {
     store();
 }
 
+// Emulation prevention over 256 bytes per wave step: lane l holds bytes i0 .. i0 + 3 (word
+// w, little-endian; bytes at or past n read as 1). Byte i is preceded by an inserted 0x03
+// iff it is <= 3 and the zero run before it has even length >= 2 (the sequential rule,
+// given a non-zero byte before the piece). Returns the lane's insertion mask (bit j: before
+// byte i0 + j); *excl = insertions of the lanes before it, *tot = of the step; last_nz
+// carries the last non-zero position across steps.
+__device__ __forceinline__ int ep_step(uint32_t w, int i0, int n, int& last_nz, int* excl, int* tot) {
+    const int l = lane();
+    int lane_last = -1;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if ((w >> (8 * j)) & 255u) lane_last = i0 + j;
+    int p = lane_last;   // inclusive max-scan of non-zero positions
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int q = __shfl_up(p, d);
+        if (l >= d) p = max(p, q);
+    }
+    int prev = __shfl_up(p, 1);
+    if (l == 0) prev = -1;
+    prev = max(prev, last_nz);
+    int m = 0, c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int i = i0 + j, b = (int)((w >> (8 * j)) & 255u), z = i - 1 - prev;
+        if (i < n && b <= 3 && z >= 2 && (z & 1) == 0) {
+            m |= 1 << j;
+            c++;
+        }
+        if (b) prev = i;
+    }
+    int inc = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int q = __shfl_up(inc, d);
+        if (l >= d) inc += q;
+    }
+    *excl = inc - c;
+    *tot = __shfl(inc, 63);
+    last_nz = max(last_nz, __shfl(p, 63));
+    return m;
+}
+// Word wi of a substream of n bytes (4-byte aligned base), bytes at or past n as 1.
+__device__ __forceinline__ uint32_t ep_word(const uint8_t* in, int wi, int n) {
+    const int i = 4 * wi;
+    if (i >= n) return 0x01010101u;
+    uint32_t w = *reinterpret_cast<const uint32_t*>(in + i);
+    if (i + 4 > n) w = (w & (0xffffffffu >> (8 * (i + 4 - n)))) | (0x01010101u << (8 * (n - i)));
+    return w;
+}
+
 // One wave per CTB row: adds every chunk's tail into the substream (a 256-byte window
 // of it in a VGPR; carries run toward the start), writes the rbsp stop bit, then counts
 // the emulation-prevention bytes (same rule as k_hevc_ep_copy).
@@ -1908,22 +1959,11 @@ __global__ __launch_bounds__(64) void k_pc_merge(HevcArgs A) {
     __threadfence();
     const int size = qs + 1;
     int last_nz = -1, ins_total = 0;
-    for (int base = 0; base < size; base += 64) {
-        const int i = base + l;
-        const int bv = i < size ? out[i] : 1;
-        int p = bv != 0 ? i : -1;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int q = __shfl_up(p, d);
-            if (l >= d) p = max(p, q);
-        }
-        int prev_nz = __shfl_up(p, 1);
-        if (l == 0) prev_nz = -1;
-        prev_nz = max(prev_nz, last_nz);
-        const int z = i - 1 - prev_nz;
-        const int ins = (i < size && bv <= 3 && z >= 2 && (z & 1) == 0) ? 1 : 0;
-        ins_total += wsum(ins);
-        last_nz = max(last_nz, __shfl(p, 63));
+    for (int base = 0; base < size; base += 256) {
+        const int wi = (base >> 2) + l;
+        int ex, tot;
+        ep_step(ep_word(out, wi, size), 4 * wi, size, last_nz, &ex, &tot);
+        ins_total += tot;
     }
     if (l == 0) {
         A.sub_size[slot] = size;
@@ -2042,10 +2082,10 @@ __global__ __launch_bounds__(64) void k_hevc_hdr(HevcArgs A) {
     }
 }
 
-// Emulation prevention + copy of one slot's substream (a row, or a row segment), wave-parallel: byte i of the
-// substream is preceded by an inserted 0x03 iff it is <= 3 and the zero run before it
-// has even length >= 2 (equivalent to the sequential rule; the previous piece ends in a
-// non-zero byte).
+// Emulation prevention + copy of one slot's substream (a row, or a row segment), wave-parallel
+// over 256-byte steps (ep_step): byte i of the substream is preceded by an inserted 0x03 iff it
+// is <= 3 and the zero run before it has even length >= 2 (equivalent to the sequential rule;
+// the previous piece ends in a non-zero byte).
 __global__ __launch_bounds__(64) void k_hevc_ep_copy(HevcArgs A) {
     const FrameArgs& f = A.f;
     const int slot = blockIdx.x;
@@ -2059,37 +2099,24 @@ __global__ __launch_bounds__(64) void k_hevc_ep_copy(HevcArgs A) {
     const uint8_t* in = A.sub + sub_base(A, m, cy, k);
     const int n = A.sub_size[slot];
     const int l = lane();
-    int last_nz = -1;   // index of the last non-zero byte before the current chunk (-1: none yet,
+    int last_nz = -1;   // the last non-zero byte before the current step (-1: none yet,
                         // the byte before the substream is non-zero)
     int opos = 0;
-    for (int base = 0; base < n; base += 64) {
-        const int i = base + l;
-        const int b = i < n ? in[i] : 1;
-        // inclusive max-scan of the positions of non-zero bytes
-        int p = b != 0 ? i : -1;
+    uint32_t w = ep_word(in, l, n);
+    for (int base = 0; base < n; base += 256) {
+        const int wi = (base >> 2) + l;
+        const uint32_t wn = ep_word(in, wi + 64, n);   // the next step's word in flight
+        int ex, tot;
+        const int m = ep_step(w, 4 * wi, n, last_nz, &ex, &tot);
+        int at = 4 * wi + opos + ex;   // output position of byte 4 wi (before its own insertions)
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int q = __shfl_up(p, d);
-            if (l >= d) p = max(p, q);
+        for (int j = 0; j < 4; j++) {
+            if (4 * wi + j >= n) break;
+            if ((m >> j) & 1) o[at++] = 3;
+            o[at++] = (uint8_t)((w >> (8 * j)) & 255u);
         }
-        int prev_nz = __shfl_up(p, 1);
-        if (l == 0) prev_nz = -1;
-        prev_nz = max(prev_nz, last_nz);
-        const int z = i - 1 - prev_nz;   // zeros immediately before byte i
-        const int ins = (i < n && b <= 3 && z >= 2 && (z & 1) == 0) ? 1 : 0;
-        int cnt = ins;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int q = __shfl_up(cnt, d);
-            if (l >= d) cnt += q;
-        }
-        if (i < n) {
-            const int at = i + opos + cnt;   // insertions before this chunk + up to this byte
-            if (ins) o[at - 1] = 3;
-            o[at] = (uint8_t)b;
-        }
-        opos += __shfl(cnt, 63);
-        last_nz = max(last_nz, __shfl(p, 63));
+        opos += tot;
+        w = wn;
     }
 }
 
