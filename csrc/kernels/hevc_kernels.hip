@@ -1327,7 +1327,7 @@ struct WaveBinBuf {
     }
 };
 
-__global__ __launch_bounds__(256) void k_hevc_bins(HevcArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_hevc_bins(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     const FrameArgs& f = A.f;
     const int n = f.mb_w * f.mb_h;
