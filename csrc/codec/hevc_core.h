@@ -684,8 +684,8 @@ SK_HD bool intra_mode_basic(int mode) { return mode <= 1 || mode == 10 || mode =
 // of PART_NxN in SAD units (x intra_lam_sad) for their extra signalling.
 SK_HD int intra_lam_sad(int qp) { return qp < 12 ? 1 : 1 << ((qp - 12) / 6); }
 constexpr int kPenSplit = 8, kPenNxN = 32;   // tuned on tools/rd_codecs.py content (open-loop SADs favour NxN)
-SK_HD int intra_mode_bias(int mode, int qp) {
-    return intra_mode_basic(mode) ? 0 : 6 * (qp < 12 ? 1 : 1 << ((qp - 12) / 6));
+SK_HD int intra_mode_bias(int mode, int qp) {   // 2 x lambda_sad (tuned with the CU quadtree)
+    return intra_mode_basic(mode) ? 0 : 2 * (qp < 12 ? 1 : 1 << ((qp - 12) / 6));
 }
 
 // Neighbour availability of transform blocks (z order inside the unit) for the intra
