@@ -839,8 +839,7 @@ __global__ __launch_bounds__(256) void k_decide(FrameArgs a) {
 
 // K10: frame QP from the complexity sums (same rc_apply as the CPU controller).
 // Host overrides: key_seq_host[1] qp, [3] rc mode, [4] kbps, [5] change counter.
-__global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
-    if (threadIdx.x != 0) return;
+__device__ void rc_qp_serial(const FrameArgs& a) {
     RcState& rc = *a.rc;
     const int seq = a.key_dev[5];   // k_plan's copy of the host snapshot
     int plan_qp = a.plan_cfg.qp;
@@ -863,7 +862,13 @@ __global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
     }
     rc.base_qp = plan_qp;
     rc_apply(rc, a.tasks, a.rc_slice, a.rc_slice + 1, a.num_slices, a.mb_w, plan_qp, 2);
-    for (int s = 0; s < a.num_slices; s++) a.tasks_host[s].qp = a.tasks[s].qp;
+}
+__global__ __launch_bounds__(64) void k_rc_qp(FrameArgs a) {
+    if (threadIdx.x == 0) rc_qp_serial(a);
+    __syncthreads();
+    // the slice QPs to the host-mapped task copies, one lane per slice (uncached PCIe
+    // writes: one wave-wide burst instead of a serial loop on lane 0)
+    for (int s = threadIdx.x; s < a.num_slices; s += 64) a.tasks_host[s].qp = a.tasks[s].qp;
 }
 
 // per_slice > 0: sizes are per NAL, per_slice NALs per slice, counted for coded slices
