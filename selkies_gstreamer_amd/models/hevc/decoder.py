@@ -822,11 +822,9 @@ class HevcDecoder:
         s = self.sps
         size = 1 << log2
         if x0 + size <= s.width and y0 + size <= s.height and log2 > s.log2_min_cb:
-            cond = 0
-            if self._avail(x0, y0, x0 - 1, y0) and self.cur["depth"][y0 >> 2, (x0 - 1) >> 2] > depth:
-                cond += 1
-            if self._avail(x0, y0, x0, y0 - 1) and self.cur["depth"][(y0 - 1) >> 2, x0 >> 2] > depth:
-                cond += 1
+            al, aa = self._avail(x0, y0, x0 - 1, y0), self._avail(x0, y0, x0, y0 - 1)
+            cond = split_cu_ctx_inc(al, int(self.cur["depth"][y0 >> 2, (x0 - 1) >> 2]) if al else 0,
+                                    aa, int(self.cur["depth"][(y0 - 1) >> 2, x0 >> 2]) if aa else 0, depth)
             split = self._dec("split_cu_flag", cond)
         else:
             split = 1 if log2 > s.log2_min_cb else 0
@@ -865,15 +863,8 @@ class HevcDecoder:
             return
         intra = 1 if self.slice_type == 2 else self._dec("pred_mode_flag")
         part = 0   # 0 2Nx2N, 1 2NxN, 2 Nx2N, 3 NxN (Table 7-10 order aside)
-        if intra:
-            if log2 == s.log2_min_cb and not self._dec("part_mode", 0):
-                part = 3
-        elif not self._dec("part_mode", 0):
-            if log2 > s.log2_min_cb and s.amp:
-                raise NotImplementedError("AMP")
-            if log2 == s.log2_min_cb and log2 > 3:
-                raise NotImplementedError("inter NxN")
-            part = 1 if self._dec("part_mode", 1) else 2
+        if not intra or log2 == s.log2_min_cb:   # intra part_mode only at the minimum CB size
+            part = part_mode_of_bins(lambda i: self._dec("part_mode", i), bool(intra), log2, s.log2_min_cb, s.amp)
         if intra:
             npu = 4 if part == 3 else 1
             h = n // 2 if part == 3 else n
@@ -900,19 +891,8 @@ class HevcDecoder:
                         cands.append(1)
                     else:
                         cands.append(int(self.cur["ipm"][yn >> 2, xn >> 2]))
-                a, b = cands
-                if a == b:
-                    lst = [0, 1, 26] if a < 2 else [a, 2 + ((a + 29) % 32), 2 + ((a - 2 + 1) % 32)]
-                else:
-                    third = 0 if (a != 0 and b != 0) else (1 if (a != 1 and b != 1) else 26)
-                    lst = [a, b, third]
-                if prev[k]:
-                    mode = lst[mpm_idx]
-                else:
-                    mode = rem
-                    for c2 in sorted(lst):
-                        if mode >= c2:
-                            mode += 1
+                lst = mpm_list(*cands)
+                mode = lst[mpm_idx] if prev[k] else mode_from_rem(rem, lst)
                 local[(xp - x0) // h, (yp - y0) // h] = mode
                 modes.append(mode)
             c = self._dec("intra_chroma_pred_mode")
@@ -1440,6 +1420,42 @@ class HevcDecoder:
 BETA_TABLE = [0] * 16 + [6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32, 34, 36, 38, 40,
                           42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64]                      # Table 8-11 (beta')
 TC_TABLE = [0] * 18 + [1] * 9 + [2] * 4 + [3] * 4 + [4] * 3 + [5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24]
+
+
+def split_cu_ctx_inc(avail_l: bool, depth_l: int, avail_a: bool, depth_a: int, cqt_depth: int) -> int:
+    """ctxInc of split_cu_flag (9.3.4.2.2, Table 9-41 condTerm CtDepth[xNb][yNb] > cqtDepth)."""
+    return int(avail_l and depth_l > cqt_depth) + int(avail_a and depth_a > cqt_depth)
+
+
+def part_mode_of_bins(dec, intra: bool, log2_cb: int, log2_min_cb: int, amp: bool) -> int:
+    """part_mode (7.4.9.5) from its bins (Table 9-43; AMP off), `dec(ctx_inc)` the next
+    context-coded bin: 0 PART_2Nx2N, 1 PART_2NxN, 2 PART_Nx2N, 3 PART_NxN."""
+    if dec(0):
+        return 0
+    if intra:
+        return 3   # only coded at the minimum CB size: "0" = NxN
+    if log2_cb > log2_min_cb and amp:
+        raise NotImplementedError("AMP")
+    if log2_cb == log2_min_cb and log2_cb > 3:
+        raise NotImplementedError("inter NxN")
+    return 1 if dec(1) else 2
+
+
+def mpm_list(a: int, b: int) -> list:
+    """candModeList (8.4.2) from candIntraPredModeA / B."""
+    if a == b:
+        return [0, 1, 26] if a < 2 else [a, 2 + ((a + 29) % 32), 2 + ((a - 2 + 1) % 32)]
+    third = 0 if (a != 0 and b != 0) else (1 if (a != 1 and b != 1) else 26)
+    return [a, b, third]
+
+
+def mode_from_rem(rem: int, lst: list) -> int:
+    """IntraPredModeY from rem_intra_luma_pred_mode (8.4.2: ascending candidates, increment)."""
+    mode = rem
+    for c in sorted(lst):
+        if mode >= c:
+            mode += 1
+    return mode
 
 
 def _qpc(qpi: int) -> int:
