@@ -37,10 +37,33 @@ __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// DPP lane exchanges (VALU, no LDS round trip; the xor shuffles compile to ds_bpermute):
+// quad_perm [1,0,3,2] / [2,3,0,1] are the xor-1 / xor-2 partners; once every lane of a quad
+// (eight lanes) holds the same value, row_half_mirror (i <-> 7 - i) / row_mirror (i <-> 15 - i)
+// reach a lane of the other quad (eight) - the same sum as the xor-4 / xor-8 partner.
+__device__ __forceinline__ int dpp_x1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_x2(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_hm(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_m(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false); }
+__device__ __forceinline__ int qsum(int v) {   // over the lane's quad (4 lanes)
+    v += dpp_x1(v);
+    return v + dpp_x2(v);
+}
+__device__ __forceinline__ int rsum16(int v) {   // over the lane's row (16 lanes)
+    v = qsum(v);
+    v += dpp_hm(v);
+    return v + dpp_m(v);
+}
+__device__ __forceinline__ int ror16(int v) {   // OR over the lane's row
+    v |= dpp_x1(v);
+    v |= dpp_x2(v);
+    v |= dpp_hm(v);
+    return v | dpp_m(v);
+}
 __device__ __forceinline__ int wsum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v = rsum16(v);
+    v += __shfl_xor(v, 16);
+    return v + __shfl_xor(v, 32);
 }
 
 // K10 per-frame cap: the coding kernels run a second time, gated, after k_rc_guard_sizes
@@ -858,10 +881,9 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
 #pragma unroll
         for (int x = 0; x < 4; x++)
             sad += sk_abs((int)L.src[(4 * by + row) * 16 + 4 * bx + x] - intra_pred_sample(L.ref4[u], 4, 2, m, 0, x, row));
-        sad += __shfl_xor(sad, 1);
-        sad += __shfl_xor(sad, 2);    // the block
-        int s8 = sad + __shfl_xor(sad, 4);
-        s8 += __shfl_xor(s8, 8);      // the 8x8 quadrant
+        sad = qsum(sad);              // the block
+        int s8 = sad + dpp_hm(sad);
+        s8 += dpp_m(s8);              // the 8x8 quadrant
         int s16 = s8 + __shfl_xor(s8, 16);
         s16 += __shfl_xor(s16, 32);   // the unit
         const int bias = intra_mode_bias(m, t.qp);
@@ -870,8 +892,8 @@ __global__ __launch_bounds__(256) void k_hevc_intra_prep(HevcArgs A) {
         if (s16 + bias < c16) { c16 = s16 + bias; b16 = m; }
     }
     const int lam = intra_lam_sad(t.qp);
-    int cn = c4 + __shfl_xor(c4, 4);
-    cn += __shfl_xor(cn, 8);
+    int cn = c4 + dpp_hm(c4);   // c4 is uniform over the block's quad
+    cn += dpp_m(cn);
     cn += kPenNxN * lam;
     const int nxn_q = cn < c8 ? 1 : 0;
     int cq = nxn_q ? cn : c8;
@@ -938,13 +960,10 @@ __device__ int intra4x4_step(CuLds& L, const int8_t* T, uint8_t* W, int bx, int 
     if (var) r = (d * 128 + 2048) >> 12;
     const int rec = sk_clip255(p + r), e1 = (int)L.src[o] - rec;
     int s0 = e * e, s1 = e1 * e1, rt = level_rate_half(lv), nz = lv != 0;
-#pragma unroll
-    for (int m = 1; m < 16; m <<= 1) {
-        s0 += __shfl_xor(s0, m);
-        s1 += __shfl_xor(s1, m);
-        rt += __shfl_xor(rt, m);
-        nz |= __shfl_xor(nz, m);
-    }
+    s0 = rsum16(s0);   // over the 16 lanes of the variant (rows of 16)
+    s1 = rsum16(s1);
+    rt = rsum16(rt);
+    nz = ror16(nz);
     const int rate = kTuRateHalf + rt;
     int f = nz;
     if (f && 512ll * s0 <= 512ll * s1 + (long long)lam * rate) f = 0;   // RD zeroing (code_tu_1)
@@ -1000,13 +1019,10 @@ __device__ void intra_c4_pair(CuLds& L, const int8_t* T, uint8_t* W, int ox, int
     if (var) r = (d * 128 + 2048) >> 12;
     const int rec = sk_clip255(p + r), e1 = (int)L.src[o] - rec;
     int s0 = e * e, s1 = e1 * e1, rt = level_rate_half(lv), nz = lv != 0;
-#pragma unroll
-    for (int m = 1; m < 16; m <<= 1) {
-        s0 += __shfl_xor(s0, m);
-        s1 += __shfl_xor(s1, m);
-        rt += __shfl_xor(rt, m);
-        nz |= __shfl_xor(nz, m);
-    }
+    s0 = rsum16(s0);   // over the 16 lanes of the variant (rows of 16)
+    s1 = rsum16(s1);
+    rt = rsum16(rt);
+    nz = ror16(nz);
     const int rate = kTuRateHalf + rt;
     int f = nz;
     if (f && 512ll * s0 <= 512ll * s1 + (long long)lam * rate) f = 0;
@@ -1214,7 +1230,7 @@ __global__ __launch_bounds__(64 * MAXR) void k_hevc_intra(HevcArgs A) {
 // I slices cut into row segments (SliceMap, seg_k > 1): one wave per segment, its CTBs
 // left to right (units in z order); no top neighbours, so the segments of all rows run at
 // once (a 4K key frame: 816 chains of 40 units instead of 34 workgroups of 124 steps).
-__global__ __launch_bounds__(256) void k_hevc_intra_seg(HevcArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_hevc_intra_seg(HevcArgs A) {
     if (second_pass_skipped(A.f)) return;   // K10: no re-code this frame
     __shared__ CuLds Lw[4];
     __shared__ int8_t T[kTabT];
