@@ -66,9 +66,9 @@ def parse():
                         "reported as extra keys (0 = skip)")
     p.add_argument("--extra-steps", type=int, default=60)
     p.add_argument("--extra-8k", type=int, default=1,
-                   help="after the 4K extras: one 7680x4320 HEVC session at 60 fps and one 7680x4320 AV1 session "
-                        "at 60 fps (the reference's largest display, selkies.py:266) on ONE GPU, --extra-steps / 2 "
-                        "frames each (0 = skip)")
+                   help="after the 4K extras: one 7680x4320 HEVC session at 60 fps (CRF 25 and CBR 40 Mbit/s) and "
+                        "one 7680x4320 AV1 session at 60 fps (the reference's largest display, selkies.py:266) on ONE "
+                        "GPU, --extra-steps / 2 frames each (0 = skip)")
     p.add_argument("--jpeg-quality", type=int, default=40)
     p.add_argument("--deblock", default="auto", choices=["0", "1", "auto"],
                    help="H.264 in-loop deblocking filter: 1 on, 0 off, auto (the default, as the server runs it): "
@@ -694,6 +694,10 @@ def main():
     if args.extra_8k and args.backend == "hip" and not args.gather and rank == 0:
         # one 8K display (MAX_W x MAX_H of the reference's resize path) on one GPU, 60 fps
         extras["hevc_8k"] = run_extra(args, 7680, 4320, "hevc", 60, local_rank, max(args.extra_steps // 2, 4))
+        # rate-controlled like the reference's x265enc (and like av1_8k): the pool's wrap-around
+        # frames (a full-screen change every 8 frames) no longer code at CRF size
+        extras["hevc_8k_cbr"] = run_extra(args, 7680, 4320, "hevc", 60, local_rank, max(args.extra_steps // 2, 4),
+                                          cbr_kbps=40000)
         extras["av1_8k"] = run_extra(args, 7680, 4320, "av1", 60, local_rank, max(args.extra_steps // 2, 4))
     if args.extra_4k and args.backend == "hip" and not args.gather and rank == 0:
         # BASELINE config 1 (640x480@30, software H.264 plumbing): the CPU reference encoder

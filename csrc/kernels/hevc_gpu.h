@@ -57,6 +57,7 @@ struct HevcArgs {
     // slots (slot = cy * seg_k + k, k = 0 for whole rows); segment k of CTB row cy codes its
     // substream at sub + cy * sub_stride + x0 * 4 * kSubstreamCtbBytes + 64 * k
     int seg_k;
+    int pc_seg;                 // k_pc_model: shortest speculative chain segment (SK_HEVC_PC_SEG, default 32)
 };
 
 // redo: the K10 re-code flag (CBR sessions): the coding kernels run a second time,

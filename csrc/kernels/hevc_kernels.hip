@@ -1576,7 +1576,7 @@ __global__ __launch_bounds__(256) void k_pc_model(HevcArgs A) {
     // from the guess is almost always segment j's true start. Pass 2 runs from those
     // starts and writes the modelled entries; a start that does not match the true end
     // of the segment before it is corrected and its segment re-run (loop until none).
-    const int seglen = tot > 64 * 32 ? (tot + 63) / 64 : 32;
+    const int seglen = tot > 64 * A.pc_seg ? (tot + 63) / 64 : A.pc_seg;
     const int nseg = (tot + seglen - 1) / seglen;
     const int p0 = l * seglen, p1 = p0 + seglen < tot ? p0 + seglen : tot;
     const bool act = l < nseg;

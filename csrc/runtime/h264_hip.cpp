@@ -811,6 +811,7 @@ class HipBackend : public EncoderBackend {
         HIPCHECK(hipStreamSynchronize(stream_));
         if (getenv("SK_STAMPS")) h.dbg = dmalloc<unsigned long long>((size_t)4 * h.ch);
         h.reg_steps = getenv("SK_HEVC_REG_STEPS") ? atoi(getenv("SK_HEVC_REG_STEPS")) : 1;
+        h.pc_seg = getenv("SK_HEVC_PC_SEG") ? sk_max(atoi(getenv("SK_HEVC_PC_SEG")), 1) : 32;
         hevc_params_.clear();
         hevc::build_parameter_sets(g_.W, g_.H, cfg_.full_range, cfg_.fps, hevc_params_);
     }
