@@ -745,7 +745,7 @@ def main():
             "config": {
                 "model": (f"H.264 Constrained Baseline CAVLC, {args.mode} stripes {args.stripe_height}px, {rc_desc(args)}"
                           if args.encoder == "h264" else
-                          (f"HEVC Main CABAC, CTB 16, WPP, slices of {args.stripe_height}px, {rc_desc(args)}"
+                          (f"HEVC Main CABAC, CTB 32 quadtree (CU 32/16/8), WPP, slices of {args.stripe_height}px, {rc_desc(args)}"
                            if args.encoder == "hevc" else
                            (f"AV1 Main 8-bit 4:2:0, 64x64 SB, tiles, {rc_desc(args)}" if args.encoder == "av1" else
                             f"baseline JPEG 4:2:0 stripes {args.stripe_height}px, quality {args.jpeg_quality}"))),

@@ -3,8 +3,9 @@
 // (K3), the per-stripe controller (paint-over, keyframes), integer motion search
 // (K4, MFMA exhaustive candidate on the GPU) and scene-cut decisions — is the one of
 // the H.264 encoder run in full-frame mode: a stripe is an HEVC slice of whole CTB
-// rows (CTB = 16 = one H.264 MB, so the MB grids coincide). The HEVC back end codes
-// CUs, binarises them into CABAC bins, codes one WPP substream per CTB row and
+// rows (CTB 32 = 2x2 H.264 MBs: the MB grid is the quadtree's 16x16 unit grid, units in
+// z order inside a CTB). The HEVC back end decides the CTB's CU split (32 / 16 / 8),
+// codes the CUs, binarises them into CABAC bins, codes one WPP substream per CTB row and
 // assembles slice NAL units with entry points.
 //
 // Reference parity: the reference's HEVC paths are GStreamer elements (nvh265enc
