@@ -60,6 +60,22 @@ __device__ __forceinline__ int ror16(int v) {   // OR over the lane's row
     v |= dpp_hm(v);
     return v | dpp_m(v);
 }
+// 4x4 blocks in 16-lane rows (lane 4y + x): the block's values at (y, k), k = 0..3, by quad
+// broadcasts, and at ((y - d) & 3, x), d = 0..3, by rotating the row 4 lanes at a time
+// (row_ror: lane i reads lane i - n of its row)
+template <int C> __device__ __forceinline__ int dppc(int v) { return __builtin_amdgcn_update_dpp(0, v, C, 0xF, 0xF, false); }
+__device__ __forceinline__ void blk_row(int v, int (&o)[4]) {
+    o[0] = dppc<0x00>(v);
+    o[1] = dppc<0x55>(v);
+    o[2] = dppc<0xAA>(v);
+    o[3] = dppc<0xFF>(v);
+}
+__device__ __forceinline__ void blk_col(int v, int (&o)[4]) {
+    o[0] = v;
+    o[1] = dppc<0x124>(v);
+    o[2] = dppc<0x128>(v);
+    o[3] = dppc<0x12C>(v);
+}
 __device__ __forceinline__ int wsum(int v) {
     v = rsum16(v);
     v += __shfl_xor(v, 16);
@@ -929,7 +945,7 @@ __device__ __forceinline__ long long shfl64(long long v, int src) {
 // lands in W, the levels in lev; returns the cbf, *J the TU's RD cost, *ts the choice.
 __device__ int intra4x4_step(CuLds& L, const int8_t* T, uint8_t* W, int bx, int by, int av, int mode, int qp, int lam,
                              int16_t* lev, long long* J, int* ts) {
-    const int l = lane(), s = l & 15, var = (l >> 4) & 1, base = l & ~15;
+    const int l = lane(), s = l & 15, var = (l >> 4) & 1;
     const int x = s & 3, y = s >> 2, o = (4 * by + y) * 16 + 4 * bx + x;
     tu_refs(W, nullptr, 0, 0, 0, 0, 4 * bx, 4 * by, 4, av, L.ref[0], &L);
     const uint8_t* ref = L.ref[0];
@@ -937,25 +953,27 @@ __device__ int intra4x4_step(CuLds& L, const int8_t* T, uint8_t* W, int bx, int 
     const int e = (int)L.src[o] - p;
     auto M = [&](int k, int m) { return (int)T[256 + 4 * k + m]; };   // the DST (load_t16)
     // forward DST: rows t[y][u] = (sum_k M[u][k] e[y][k] + 1) >> 1, columns (+ 128) >> 8
-    int t = 0;
+    int t = 0, c = 0, nb[4];
+    blk_row(e, nb);
 #pragma unroll
-    for (int k = 0; k < 4; k++) t += M(x, k) * __shfl(e, base + 4 * y + k);
+    for (int k = 0; k < 4; k++) t += M(x, k) * nb[k];
     t = (t + 1) >> 1;
-    int c = 0;
+    blk_col(t, nb);
 #pragma unroll
-    for (int k = 0; k < 4; k++) c += M(y, k) * __shfl(t, base + 4 * k + x);
+    for (int k = 0; k < 4; k++) c += M(y, (y - k) & 3) * nb[k];
     c = (c + 128) >> 8;
     if (var) c = e * 32;   // transform skip: the residual << 5
     const int lv = quant_level(c, qp, 2, true);
     const int d = dequant_level(lv, qp, 2);
     // inverse: columns g = clip16((sum_j M[j][y] d[j][x] + 64) >> 7), rows (sum_j M[j][x] g[y][j] + 2048) >> 12
-    int g = 0;
+    int g = 0, r = 0;
+    blk_col(d, nb);
 #pragma unroll
-    for (int j = 0; j < 4; j++) g += M(j, y) * __shfl(d, base + 4 * j + x);
+    for (int j = 0; j < 4; j++) g += M((y - j) & 3, y) * nb[j];
     g = sk_clip((g + 64) >> 7, -32768, 32767);
-    int r = 0;
+    blk_row(g, nb);
 #pragma unroll
-    for (int j = 0; j < 4; j++) r += M(j, x) * __shfl(g, base + 4 * y + j);
+    for (int j = 0; j < 4; j++) r += M(j, x) * nb[j];
     r = (r + 2048) >> 12;
     if (var) r = (d * 128 + 2048) >> 12;
     const int rec = sk_clip255(p + r), e1 = (int)L.src[o] - rec;
@@ -989,7 +1007,7 @@ __device__ int intra4x4_step(CuLds& L, const int8_t* T, uint8_t* W, int bx, int 
 // (Cr), reconstruction into W; per component cbf, RD cost and skip choice.
 __device__ void intra_c4_pair(CuLds& L, const int8_t* T, uint8_t* W, int ox, int oy, int av, int mode, int qpc, int lam,
                               int16_t* lev_c, int* fc, long long* Jc, int* tsc) {
-    const int l = lane(), s = l & 15, var = (l >> 4) & 1, comp = l >> 5, base = l & ~15;
+    const int l = lane(), s = l & 15, var = (l >> 4) & 1, comp = l >> 5;
     const int x = s & 3, y = s >> 2, o = (comp ? kCoefCr : kCoefCb) + (oy + y) * 8 + ox + x;
     tu_refs(W, nullptr, 0, 0, 0, 1, ox, oy, 4, av, L.ref[0], &L);
     tu_refs(W, nullptr, 0, 0, 0, 2, ox, oy, 4, av, L.ref[1], &L);
@@ -997,24 +1015,26 @@ __device__ void intra_c4_pair(CuLds& L, const int8_t* T, uint8_t* W, int ox, int
     const int p = intra_pred_at([&](int i) { return (int)ref[i]; }, 4, 2, mode, 1 + comp, x, y);
     const int e = (int)L.src[o] - p;
     auto M = [&](int k, int m) { return (int)T[(k << 2) * 16 + m]; };   // 4-point DCT rows of T16
-    int t = 0;
+    int t = 0, c = 0, nb[4];
+    blk_row(e, nb);
 #pragma unroll
-    for (int k = 0; k < 4; k++) t += M(x, k) * __shfl(e, base + 4 * y + k);
+    for (int k = 0; k < 4; k++) t += M(x, k) * nb[k];
     t = (t + 1) >> 1;
-    int c = 0;
+    blk_col(t, nb);
 #pragma unroll
-    for (int k = 0; k < 4; k++) c += M(y, k) * __shfl(t, base + 4 * k + x);
+    for (int k = 0; k < 4; k++) c += M(y, (y - k) & 3) * nb[k];
     c = (c + 128) >> 8;
     if (var) c = e * 32;
     const int lv = quant_level(c, qpc, 2, true);
     const int d = dequant_level(lv, qpc, 2);
-    int g = 0;
+    int g = 0, r = 0;
+    blk_col(d, nb);
 #pragma unroll
-    for (int j = 0; j < 4; j++) g += M(j, y) * __shfl(d, base + 4 * j + x);
+    for (int j = 0; j < 4; j++) g += M((y - j) & 3, y) * nb[j];
     g = sk_clip((g + 64) >> 7, -32768, 32767);
-    int r = 0;
+    blk_row(g, nb);
 #pragma unroll
-    for (int j = 0; j < 4; j++) r += M(j, x) * __shfl(g, base + 4 * y + j);
+    for (int j = 0; j < 4; j++) r += M(j, x) * nb[j];
     r = (r + 2048) >> 12;
     if (var) r = (d * 128 + 2048) >> 12;
     const int rec = sk_clip255(p + r), e1 = (int)L.src[o] - rec;
