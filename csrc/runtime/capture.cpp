@@ -174,10 +174,12 @@ class CaptureSession {
     // an export that fails) the new encoder starts with a key frame instead.
     // Returns 0 moved with the stream continued, 1 moved with a key frame, -1 not
     // moved (CPU session, target GPU unusable, timeout; last error says why).
-    // The target encoder (allocations, hipGraph capture: the slow part) is built here, on
-    // the caller's thread, while the capture thread keeps encoding on the old GPU; between
-    // two frames the capture thread only exports, peer-copies and imports the state and
-    // swaps encoders. That stall is recorded (stats: move_stall_ms).
+    // The target encoder (allocations, hipGraph capture: the slow part) and the state's
+    // staging buffers are made here, on the caller's thread, while the capture thread keeps
+    // encoding on the old GPU; between two frames the capture thread only exports,
+    // peer-copies and imports the state and swaps encoders. That stall is recorded (stats:
+    // move_stall_ms). The old encoder and the staging buffers are released back here too
+    // (hipFree synchronises the device: not on the capture thread).
     int move_to(int device, int timeout_ms) {
         if (!running_) {
             set_last_error("capture not running");
@@ -197,10 +199,22 @@ class CaptureSession {
                 return -1;
             }
         }
+        std::shared_ptr<void> sa, sb;
+        const int sdev = registered_device_;   // where the state is exported (checked again by do_move)
+        if (nenc && sdev >= 0) {
+            const int64_t n = nenc->state_bytes();
+            if (n > 0) {
+                sa = dev_buf(sdev, n);
+                sb = dev_buf(device, n);
+            }
+        }
         std::unique_lock<std::mutex> g(move_mu_);
         const uint64_t ticket = ++move_ticket_;
         move_dev_ = device;
         move_enc_ = std::move(nenc);   // null: do_move reports why nothing can move
+        move_a_ = std::move(sa);
+        move_b_ = std::move(sb);
+        move_a_dev_ = sdev;
         move_pending_ = true;   // the loop stops queueing a second frame until it is served
         auto done = [&] { return move_done_ >= ticket || !running_; };
         if (!move_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms > 0 ? timeout_ms : 10000), done)) {
@@ -221,7 +235,17 @@ class CaptureSession {
             return -1;
         }
         if (move_rc_ < 0) set_last_error(move_err_);
-        return move_rc_;
+        const int rc = move_rc_;
+        std::unique_ptr<EncoderBackend> old = std::move(move_old_);   // released on this thread
+        sa = std::move(move_a_);
+        sb = std::move(move_b_);
+        g.unlock();
+        return rc;
+    }
+    static std::shared_ptr<void> dev_buf(int dev, int64_t n) {
+        void* p = sk_dev_alloc(dev, n);
+        if (!p) return nullptr;
+        return std::shared_ptr<void>(p, [dev](void* q) { sk_dev_free(dev, q); });
     }
     int device() const { return registered_device_; }
     // K10: switch the rate control mode / CBR target from the next frame
@@ -508,8 +532,9 @@ class CaptureSession {
 
     // Capture thread, no frame in flight: performs a pending move_to().
     void serve_move() {
-        std::unique_ptr<EncoderBackend> nenc;
-        int dev;
+        std::unique_ptr<EncoderBackend> nenc, old;
+        std::shared_ptr<void> a, b;
+        int dev, adev;
         uint64_t ticket;
         {
             std::lock_guard<std::mutex> g(move_mu_);
@@ -519,22 +544,31 @@ class CaptureSession {
             ticket = move_ticket_;
             move_serving_ = ticket;
             nenc = std::move(move_enc_);
+            a = std::move(move_a_);
+            b = std::move(move_b_);
+            adev = move_a_dev_;
         }
         std::string err;
         const auto t0 = clk::now();
-        const int rc = do_move(dev, std::move(nenc), &err);
+        const int rc = do_move(dev, std::move(nenc), adev == s_.device ? a.get() : nullptr, b.get(), &old, &err);
         {
             std::lock_guard<std::mutex> gs(mu_);
             move_stall_ms_ = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
         }
         std::lock_guard<std::mutex> g(move_mu_);
+        move_old_ = std::move(old);   // the caller releases them (a timed-out caller: the next move / close)
+        move_a_ = std::move(a);
+        move_b_ = std::move(b);
         move_rc_ = rc;
         move_err_ = err;
         move_done_ = std::max(move_done_, ticket);   // a withdrawn later ticket stays withdrawn
         move_cv_.notify_all();
     }
 
-    int do_move(int dev, std::unique_ptr<EncoderBackend> nenc, std::string* err) {
+    // sa / sb: staging buffers made by move_to's caller on the old / new GPU (null: made here).
+    // The replaced encoder goes to *old (released by the caller, off this thread).
+    int do_move(int dev, std::unique_ptr<EncoderBackend> nenc, void* sa, void* sb,
+                std::unique_ptr<EncoderBackend>* old, std::string* err) {
         trace::Range r("capture.move");
         if (!backend_ || dev < 0 || dev >= sk_hip_device_count() || !nenc) {
             *err = backend_ ? "no such GPU" : "CPU session: nothing to move";
@@ -548,8 +582,11 @@ class CaptureSession {
         } else if (nenc->state_bytes() != n) {
             why = "state sizes differ";
         } else {
-            void* a = sk_dev_alloc(s_.device, n);
-            void* b = sk_dev_alloc(dev, n);
+            std::shared_ptr<void> own_a, own_b;   // fallback staging (no buffers from the caller)
+            if (!sa) own_a = dev_buf(s_.device, n);
+            if (!sb) own_b = dev_buf(dev, n);
+            void* a = sa ? sa : own_a.get();
+            void* b = sb ? sb : own_b.get();
             try {
                 if (!a || !b) why = "device buffers: " + std::string(sk_last_error());
                 else if (enc_->export_state(a, 1) != 0) why = "export: " + std::string(sk_last_error());
@@ -559,8 +596,6 @@ class CaptureSession {
             } catch (const std::exception& ex) {
                 why = std::string("exception: ") + ex.what();
             }
-            if (a) sk_dev_free(s_.device, a);
-            if (b) sk_dev_free(dev, b);
         }
         if (!carried) {   // a fresh stream: key frame, with the rate control last asked for
             fprintf(stderr, "[capture] move to GPU %d: state not carried (%s), key frame\n", dev, why.c_str());
@@ -568,7 +603,8 @@ class CaptureSession {
             if (last_qp_) nenc->set_qp(last_qp_ & 0xffff, last_qp_ >> 16);
             if (last_rate_) nenc->set_rate((int)((last_rate_ >> 32) & 0xff), (int)(last_rate_ & 0xffffffff));
         }
-        enc_ = std::move(nenc);   // the old encoder (and its GPU memory) goes here
+        *old = std::move(enc_);   // the old encoder (and its GPU memory): released by the caller
+        enc_ = std::move(nenc);
         if (registered_device_ >= 0) device_sessions(registered_device_, -1);
         registered_device_ = s_.device = dev;
         device_sessions(dev, +1);
@@ -682,6 +718,9 @@ class CaptureSession {
     int move_dev_ = -1, move_rc_ = -1;
     std::string move_err_;
     std::unique_ptr<EncoderBackend> move_enc_;   // target encoder built by move_to's caller
+    std::unique_ptr<EncoderBackend> move_old_;   // replaced encoder, released by move_to's caller
+    std::shared_ptr<void> move_a_, move_b_;      // state staging on the old / new GPU
+    int move_a_dev_ = -1;
     double move_stall_ms_ = 0.0;
     uint64_t hist_[kHist] = {};
     double src_kind_ = -1.0;  // 1 x11, 0 synthetic, -1 none (kept after stop for stats)
