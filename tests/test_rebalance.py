@@ -289,6 +289,9 @@ def _capture_run(mode, move_after=None, frames=8, W=256, H=128):
         assert cap.device == 0
         cap.run(frames - move_after)
         assert cap.wait(120_000) == 0
+        # the capture thread only swaps state and encoders between two frames: the target's
+        # build and the old encoder's teardown run on move_to's thread (profiles/r6_move_stall.md)
+        assert cap.stats()["move_stall_ms"] < 10.0
     cap.close()
     return got, res
 
