@@ -103,7 +103,9 @@ def test_session_h264_striped(tmp_path):
 
 def test_keyframe_request_resyncs_a_viewer(tmp_path):
     """REQUEST_KEYFRAME (sent by web/lib/video.js when its decoder dropped a delta) makes
-    the display's next frames start with a 0x04 key frame within two frames."""
+    the display's next frames start with a 0x04 key frame within a few frames: the frames
+    already encoded or queued on the socket when the request lands (up to two under a
+    loaded CPU) arrive first."""
     async def main():
         srv, port, _ = await _server(tmp_path)
         async with aiohttp.ClientSession() as sess:
@@ -118,11 +120,11 @@ def test_keyframe_request_resyncs_a_viewer(tmp_path):
                 await ws.send_str("REQUEST_KEYFRAME")
                 await ws.send_str("REQUEST_KEYFRAME")             # a second viewer / repeat: one IDR
                 after = []
-                while len(after) < 8:
+                while len(after) < 10:
                     data = (await asyncio.wait_for(ws.receive(), 10)).data
                     if isinstance(data, bytes) and data[0] == 0x04:
                         after.append(data[1])
-                assert 1 in after[:2], after
+                assert 1 in after[:4], after
                 assert sum(after) == 1, after
         await srv.stop()
     run(main())
